@@ -1,0 +1,136 @@
+"""Defaulting (SetDefaults_*) for the kinds amdkube serves.
+
+Reference: pkg/apis/core/v1/defaults.go:131 (SetDefaults_Pod), :164-179 (fork: copy
+ExtendedResources limits into requests), container/pod defaults in the same file,
+pkg/apis/apps/v1 defaults for DaemonSet/ReplicaSet/Deployment.
+"""
+from __future__ import annotations
+
+from .scheme import register_hooks
+
+
+def _default_container(c: dict):
+    c.setdefault("terminationMessagePath", "/dev/termination-log")
+    c.setdefault("terminationMessagePolicy", "File")
+    img = c.get("image") or ""
+    if "imagePullPolicy" not in c:
+        c["imagePullPolicy"] = "Always" if img.endswith(":latest") or ":" not in img.rsplit("/", 1)[-1] else "IfNotPresent"
+    res = c.get("resources")
+    if res and res.get("limits"):
+        req = res.setdefault("requests", {})
+        for k, v in res["limits"].items():
+            req.setdefault(k, v)
+    for p in c.get("ports") or []:
+        p.setdefault("protocol", "TCP")
+    for probe in ("livenessProbe", "readinessProbe"):
+        pr = c.get(probe)
+        if pr:
+            pr.setdefault("timeoutSeconds", 1)
+            pr.setdefault("periodSeconds", 10)
+            pr.setdefault("successThreshold", 1)
+            pr.setdefault("failureThreshold", 3)
+
+
+def default_pod_spec(spec: dict):
+    spec.setdefault("restartPolicy", "Always")
+    spec.setdefault("dnsPolicy", "ClusterFirst")
+    spec.setdefault("terminationGracePeriodSeconds", 30)
+    spec.setdefault("schedulerName", "default-scheduler")
+    spec.setdefault("securityContext", {})
+    for c in spec.get("containers") or []:
+        _default_container(c)
+    for c in spec.get("initContainers") or []:
+        _default_container(c)
+    # fork: ExtendedResources requests := limits (defaults.go:164-179)
+    for pres in spec.get("extendedResources") or []:
+        res = pres.setdefault("resources", {})
+        lim = res.get("limits") or {}
+        if lim and not res.get("requests"):
+            res["requests"] = dict(lim)
+        pres.setdefault("affinity", {})
+    for v in spec.get("volumes") or []:
+        if not any(k for k in v if k != "name"):
+            v["emptyDir"] = {}
+
+
+def default_pod(pod: dict):
+    pod.setdefault("spec", {})
+    default_pod_spec(pod["spec"])
+    return pod
+
+
+def default_node(node: dict):
+    node.setdefault("spec", {})
+    st = node.setdefault("status", {})
+    if st.get("capacity") and not st.get("allocatable"):
+        st["allocatable"] = dict(st["capacity"])
+    return node
+
+
+def default_namespace(ns: dict):
+    ns.setdefault("spec", {}).setdefault("finalizers", ["kubernetes"])
+    ns.setdefault("status", {}).setdefault("phase", "Active")
+    return ns
+
+
+def _default_template_owner(obj: dict, replicas=True):
+    spec = obj.setdefault("spec", {})
+    if replicas:
+        spec.setdefault("replicas", 1)
+    tpl = spec.setdefault("template", {})
+    default_pod_spec(tpl.setdefault("spec", {}))
+    if "selector" not in spec and (tpl.get("metadata") or {}).get("labels"):
+        spec["selector"] = {"matchLabels": dict(tpl["metadata"]["labels"])}
+    return obj
+
+
+def default_daemonset(ds: dict):
+    _default_template_owner(ds, replicas=False)
+    ds["spec"].setdefault("updateStrategy", {"type": "RollingUpdate", "rollingUpdate": {"maxUnavailable": 1}})
+    ds["spec"].setdefault("revisionHistoryLimit", 10)
+    return ds
+
+
+def default_replicaset(rs: dict):
+    return _default_template_owner(rs)
+
+
+def default_deployment(d: dict):
+    _default_template_owner(d)
+    d["spec"].setdefault("strategy", {"type": "RollingUpdate",
+                                      "rollingUpdate": {"maxUnavailable": "25%", "maxSurge": "25%"}})
+    d["spec"].setdefault("revisionHistoryLimit", 10)
+    d["spec"].setdefault("progressDeadlineSeconds", 600)
+    return d
+
+
+def default_job(j: dict):
+    spec = j.setdefault("spec", {})
+    spec.setdefault("completions", 1)
+    spec.setdefault("parallelism", 1)
+    spec.setdefault("backoffLimit", 6)
+    tpl = spec.setdefault("template", {})
+    tspec = tpl.setdefault("spec", {})
+    tspec.setdefault("restartPolicy", "OnFailure")
+    default_pod_spec(tspec)
+    return j
+
+
+def default_service(s: dict):
+    spec = s.setdefault("spec", {})
+    spec.setdefault("type", "ClusterIP")
+    spec.setdefault("sessionAffinity", "None")
+    for p in spec.get("ports") or []:
+        p.setdefault("protocol", "TCP")
+        p.setdefault("targetPort", p.get("port"))
+    return s
+
+
+register_hooks("Pod", defaulter=default_pod)
+register_hooks("Node", defaulter=default_node)
+register_hooks("Namespace", defaulter=default_namespace)
+register_hooks("Service", defaulter=default_service)
+register_hooks("DaemonSet", "apps/v1", defaulter=default_daemonset)
+register_hooks("ReplicaSet", "apps/v1", defaulter=default_replicaset)
+register_hooks("Deployment", "apps/v1", defaulter=default_deployment)
+register_hooks("Job", "batch/v1", defaulter=default_job)

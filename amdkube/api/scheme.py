@@ -1,0 +1,211 @@
+"""The type registry (runtime.Scheme analogue) and codecs.
+
+Reference: staging/src/k8s.io/apimachinery/pkg/runtime/scheme.go:160 (AddKnownTypes),
+:392 (Default), :404 (Convert); codecs in .../runtime/serializer (json/yaml/protobuf).
+
+amdkube keeps objects as JSON dicts, so the scheme is a table of ResourceInfo records
+(group/version/kind/plural/scope/short names) plus per-kind defaulting and validation
+hooks that the registry and kubectl look up. Only the external version exists (no
+internal<->v1 conversion round trip), which removes a whole copy per request.
+"""
+from __future__ import annotations
+
+import json
+from dataclasses import dataclass, field
+from typing import Callable
+
+import yaml
+
+
+@dataclass
+class ResourceInfo:
+    group: str
+    version: str
+    kind: str
+    plural: str
+    namespaced: bool
+    short_names: tuple = ()
+    subresources: tuple = ()
+    list_kind: str = ""
+    verbs: tuple = ("create", "delete", "deletecollection", "get", "list", "patch", "update", "watch")
+    defaulter: Callable | None = field(default=None, repr=False)
+    validator: Callable | None = field(default=None, repr=False)
+
+    @property
+    def api_version(self) -> str:
+        return f"{self.group}/{self.version}" if self.group else self.version
+
+    @property
+    def group_resource(self) -> str:
+        return f"{self.plural}.{self.group}" if self.group else self.plural
+
+    def api_prefix(self) -> str:
+        return f"/apis/{self.group}/{self.version}" if self.group else f"/api/{self.version}"
+
+
+class Scheme:
+    def __init__(self):
+        self.by_kind: dict[tuple[str, str], ResourceInfo] = {}
+        self.by_plural: dict[tuple[str, str], ResourceInfo] = {}
+        self.by_name: dict[str, ResourceInfo] = {}
+
+    def add(self, ri: ResourceInfo):
+        ri.list_kind = ri.list_kind or ri.kind + "List"
+        self.by_kind[(ri.api_version, ri.kind)] = ri
+        self.by_plural[(ri.group, ri.plural)] = ri
+        for n in (ri.plural, ri.kind.lower(), *ri.short_names, ri.group_resource):
+            self.by_name.setdefault(n, ri)
+
+    def for_kind(self, api_version: str, kind: str) -> ResourceInfo | None:
+        return self.by_kind.get((api_version, kind))
+
+    def for_plural(self, group: str, plural: str) -> ResourceInfo | None:
+        return self.by_plural.get((group, plural))
+
+    def for_object(self, obj: dict) -> ResourceInfo | None:
+        return self.for_kind(obj.get("apiVersion", ""), obj.get("kind", ""))
+
+    def resolve(self, name: str) -> ResourceInfo | None:
+        """kubectl-style lookup: 'po', 'pods', 'pod', 'daemonsets.apps', 'ds'."""
+        return self.by_name.get(name.lower())
+
+    def groups(self) -> dict[str, list[ResourceInfo]]:
+        out: dict[str, list[ResourceInfo]] = {}
+        for ri in self.by_kind.values():
+            out.setdefault(ri.api_version, []).append(ri)
+        return out
+
+    def default(self, obj: dict) -> dict:
+        ri = self.for_object(obj)
+        if ri and ri.defaulter:
+            ri.defaulter(obj)
+        return obj
+
+    def validate(self, obj: dict, old: dict | None = None) -> list[str]:
+        ri = self.for_object(obj)
+        if ri and ri.validator:
+            return ri.validator(obj, old)
+        return []
+
+
+SCHEME = Scheme()
+
+_CORE = [
+    ("Pod", "pods", True, ("po",), ("status", "binding", "eviction", "log")),
+    ("Node", "nodes", False, ("no",), ("status",)),
+    ("Binding", "bindings", True, (), ()),
+    ("Event", "events", True, ("ev",), ()),
+    ("Namespace", "namespaces", False, ("ns",), ("status", "finalize")),
+    ("Service", "services", True, ("svc",), ("status",)),
+    ("Endpoints", "endpoints", True, ("ep",), ()),
+    ("ConfigMap", "configmaps", True, ("cm",), ()),
+    ("Secret", "secrets", True, (), ()),
+    ("ServiceAccount", "serviceaccounts", True, ("sa",), ()),
+    ("LimitRange", "limitranges", True, ("limits",), ()),
+    ("ResourceQuota", "resourcequotas", True, ("quota",), ("status",)),
+    ("PersistentVolume", "persistentvolumes", False, ("pv",), ("status",)),
+    ("PersistentVolumeClaim", "persistentvolumeclaims", True, ("pvc",), ("status",)),
+]
+_APPS = [
+    ("DaemonSet", "daemonsets", True, ("ds",), ("status",)),
+    ("ReplicaSet", "replicasets", True, ("rs",), ("status", "scale")),
+    ("Deployment", "deployments", True, ("deploy",), ("status", "scale")),
+]
+_BATCH = [("Job", "jobs", True, (), ("status",))]
+_COORD = [("Lease", "leases", True, (), ())]
+_SCHED = [("PriorityClass", "priorityclasses", False, ("pc",), ())]
+
+for group, version, table in (("", "v1", _CORE), ("apps", "v1", _APPS), ("batch", "v1", _BATCH),
+                              ("coordination.k8s.io", "v1", _COORD), ("scheduling.k8s.io", "v1", _SCHED)):
+    for kind, plural, ns, short, subs in table:
+        SCHEME.add(ResourceInfo(group, version, kind, plural, ns, short, subs))
+
+
+def register_hooks(kind: str, api_version: str = "v1", defaulter=None, validator=None):
+    ri = SCHEME.for_kind(api_version, kind)
+    if ri is None:
+        raise KeyError(kind)
+    if defaulter:
+        ri.defaulter = defaulter
+    if validator:
+        ri.validator = validator
+
+
+# ------------------------------------------------------------------------ codecs
+def encode(obj) -> bytes:
+    return json.dumps(obj, separators=(",", ":")).encode()
+
+
+def decode(data: bytes | str):
+    return json.loads(data)
+
+
+def load_manifests(text: str) -> list[dict]:
+    """YAML or JSON, multi-document; `kind: List` is flattened (kubectl create -f)."""
+    text = text.strip()
+    docs = []
+    if text.startswith("{") or text.startswith("["):
+        d = json.loads(text)
+        docs = d if isinstance(d, list) else [d]
+    else:
+        docs = [d for d in yaml.safe_load_all(text) if d]
+    out = []
+    for d in docs:
+        if isinstance(d, dict) and d.get("kind", "").endswith("List") and "items" in d:
+            out.extend(d["items"])
+        else:
+            out.append(d)
+    return out
+
+
+def dump_yaml(obj) -> str:
+    return yaml.safe_dump(obj, default_flow_style=False, sort_keys=False)
+
+
+# Protobuf envelope (`k8s\x00` + runtime.Unknown). amdkube serves JSON; the envelope is
+# implemented for content negotiation parity (reference serializer/protobuf/protobuf.go:42,88)
+# with the JSON object as the raw payload and contentType application/json.
+PROTO_MAGIC = b"k8s\x00"
+
+
+def _varint(n: int) -> bytes:
+    out = bytearray()
+    while True:
+        b = n & 0x7F
+        n >>= 7
+        if n:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def _field(num: int, payload: bytes) -> bytes:
+    return _varint(num << 3 | 2) + _varint(len(payload)) + payload
+
+
+def encode_envelope(obj: dict) -> bytes:
+    tm = _field(1, obj.get("apiVersion", "").encode()) + _field(2, obj.get("kind", "").encode())
+    return PROTO_MAGIC + _field(1, tm) + _field(2, encode(obj)) + _field(4, b"application/json")
+
+
+def decode_envelope(data: bytes) -> dict:
+    if not data.startswith(PROTO_MAGIC):
+        raise ValueError("missing k8s protobuf magic")
+    buf, i, fields = data[4:], 0, {}
+    while i < len(buf):
+        key, shift = 0, 0
+        while True:
+            b = buf[i]; i += 1
+            key |= (b & 0x7F) << shift; shift += 7
+            if not b & 0x80:
+                break
+        ln, shift = 0, 0
+        while True:
+            b = buf[i]; i += 1
+            ln |= (b & 0x7F) << shift; shift += 7
+            if not b & 0x80:
+                break
+        fields[key >> 3] = buf[i:i + ln]
+        i += ln
+    return decode(fields[2])

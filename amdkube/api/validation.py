@@ -1,0 +1,369 @@
+"""Validation for the served kinds.
+
+Reference: pkg/apis/core/validation/validation.go — ValidatePod/ValidatePodSpec,
+fork ValidateExtendedResources (:2950-2987) and validateContainersExtendedResources
+(:2457-2483, applied to Containers at :2883-2888), ValidatePodBinding (:3416-3429),
+ValidateNode. Deliberate fixes: #9 init containers' extendedResourceRequests
+are validated too; #10 the binding's extendedResourceBinding is validated (statically
+here, against node state in the registry).
+"""
+from __future__ import annotations
+
+from .helpers import HEALTHY, UNHEALTHY, is_extended_resource_name, is_native_resource
+from .labels import (SelectorError, is_dns1123_label, is_dns1123_subdomain, is_qualified_name,
+                     is_valid_label_value, node_requirements_as_selector, selector_from_label_selector)
+from .quantity import Quantity, QuantityError
+from .scheme import register_hooks
+
+RESTART_POLICIES = ("Always", "OnFailure", "Never")
+
+
+def validate_object_meta(obj: dict, namespaced: bool, name_fn=is_dns1123_subdomain) -> list[str]:
+    errs = []
+    md = obj.get("metadata") or {}
+    name = md.get("name") or ""
+    if not name and not md.get("generateName"):
+        errs.append("metadata.name: Required value: name or generateName is required")
+    elif name:
+        errs += [f"metadata.name: Invalid value: {name!r}: {e}" for e in name_fn(name)]
+    ns = md.get("namespace") or ""
+    if namespaced and not ns:
+        errs.append("metadata.namespace: Required value")
+    if not namespaced and ns:
+        errs.append("metadata.namespace: Forbidden: not allowed on this type")
+    if ns:
+        errs += [f"metadata.namespace: Invalid value: {ns!r}: {e}" for e in is_dns1123_label(ns)]
+    for k, v in (md.get("labels") or {}).items():
+        errs += [f"metadata.labels: Invalid value: {k!r}: {e}" for e in is_qualified_name(k)]
+        errs += [f"metadata.labels: Invalid value: {v!r}: {e}" for e in is_valid_label_value(str(v))]
+    ann = md.get("annotations") or {}
+    for k in ann:
+        errs += [f"metadata.annotations: Invalid value: {k!r}: {e}" for e in is_qualified_name(k.lower())]
+    if sum(len(k) + len(str(v)) for k, v in ann.items()) > 256 * 1024:
+        errs.append("metadata.annotations: Too long: must have at most 262144 characters")
+    return errs
+
+
+def _validate_resource_list(rl: dict | None, path: str) -> list[str]:
+    errs = []
+    for k, v in (rl or {}).items():
+        if is_qualified_name(k):
+            errs.append(f"{path}[{k}]: Invalid value: {k!r}: must be a standard resource name or fully qualified")
+        try:
+            q = Quantity(v)
+            if q.as_fraction() < 0:
+                errs.append(f"{path}[{k}]: Invalid value: {v!r}: must be greater than or equal to 0")
+            if not is_native_resource(k) and q.as_fraction().denominator != 1:
+                errs.append(f"{path}[{k}]: Invalid value: {v!r}: must be an integer")
+        except QuantityError as e:
+            errs.append(f"{path}[{k}]: Invalid value: {v!r}: {e}")
+    return errs
+
+
+def validate_resource_requirements(res: dict | None, path: str) -> list[str]:
+    res = res or {}
+    lim, req = res.get("limits") or {}, res.get("requests") or {}
+    errs = _validate_resource_list(lim, path + ".limits") + _validate_resource_list(req, path + ".requests")
+    if errs:
+        return errs
+    for k, v in req.items():
+        if k in lim:
+            if Quantity(v) > Quantity(lim[k]):
+                errs.append(f"{path}.requests[{k}]: Invalid value: {v!r}: must be less than or equal to {k} limit")
+            if is_extended_resource_name(k) and Quantity(v) != Quantity(lim[k]):
+                errs.append(f"{path}.requests[{k}]: Invalid value: {v!r}: must be equal to {k} limit")
+        elif is_extended_resource_name(k):
+            errs.append(f"{path}.limits[{k}]: Required value: Limit must be set for non overcommitable resources")
+    return errs
+
+
+def validate_extended_resources(pres_list: list[dict] | None, path="spec.extendedResources") -> tuple[dict, list[str]]:
+    """Port of the fork's ValidateExtendedResources semantics (validation.go:2950-2987)."""
+    coll: dict[str, int] = {}
+    errs: list[str] = []
+    for i, r in enumerate(pres_list or []):
+        p = f"{path}[{i}]"
+        name = r.get("name") or ""
+        if not name:
+            errs.append(f"{p}.name: Invalid value: Extended resource name can't be empty")
+        if name in coll:
+            errs.append(f"{p}.name: Invalid value: {name!r}: Extended resource name should be unique")
+        coll[name] = 0
+        res = r.get("resources") or {}
+        lim, req = res.get("limits") or {}, res.get("requests") or {}
+        if len(lim) != 1:
+            errs.append(f"{p}.resources.limits: Invalid value: unexpected limits length {len(lim)} != 1")
+        if len(req) != 1:
+            errs.append(f"{p}.resources.requests: Invalid value: unexpected requests length {len(req)} != 1")
+        for rname, lval in lim.items():
+            try:
+                if rname not in req or Quantity(req[rname]) != Quantity(lval):
+                    errs.append(f"{p}.resources: Invalid value: Invalid Requests, Limits and Requests should be equal")
+                elif Quantity(lval).as_fraction() <= 0 or Quantity(lval).as_fraction().denominator != 1:
+                    errs.append(f"{p}.resources.limits[{rname}]: Invalid value: must be a positive integer")
+            except QuantityError as e:
+                errs.append(f"{p}.resources: Invalid value: {e}")
+            if not is_extended_resource_name(rname):
+                errs.append(f"{p}.resources.limits[{rname}]: Invalid value: must be an extended resource name")
+        try:
+            node_requirements_as_selector((r.get("affinity") or {}).get("required"))
+        except SelectorError as e:
+            errs.append(f"{p}.affinity.required: Invalid value: {e}")
+        for j, did in enumerate(r.get("assigned") or []):
+            if not isinstance(did, str) or not did:
+                errs.append(f"{p}.assigned[{j}]: Invalid value: device IDs must be non-empty strings")
+    return coll, errs
+
+
+def validate_containers_extended_resources(containers, names: dict, path: str) -> list[str]:
+    """validation.go:2457-2483 — each reference must exist and be used at most once."""
+    errs = []
+    for ci, c in enumerate(containers or []):
+        for ref in c.get("extendedResourceRequests") or []:
+            if ref not in names:
+                errs.append(f"{path}[{ci}].extendedResourceRequests: Invalid value: {ref!r}: Reference to unknown extended resource")
+                continue
+            if names[ref] != 0:
+                errs.append(f"{path}[{ci}].extendedResourceRequests: Invalid value: {ref!r}: Multiple reference to extended resource (sharing is not allowed)")
+                continue
+            names[ref] += 1
+    return errs
+
+
+def _validate_container(c: dict, path: str, init: bool) -> list[str]:
+    errs = []
+    name = c.get("name") or ""
+    if not name:
+        errs.append(f"{path}.name: Required value")
+    else:
+        errs += [f"{path}.name: Invalid value: {name!r}: {e}" for e in is_dns1123_label(name)]
+    if not c.get("image"):
+        errs.append(f"{path}.image: Required value")
+    errs += validate_resource_requirements(c.get("resources"), path + ".resources")
+    ports = set()
+    for i, p in enumerate(c.get("ports") or []):
+        cp = p.get("containerPort")
+        if not isinstance(cp, int) or not 0 < cp < 65536:
+            errs.append(f"{path}.ports[{i}].containerPort: Invalid value: {cp!r}: must be between 1 and 65535")
+        hp = p.get("hostPort") or 0
+        if hp and not 0 < hp < 65536:
+            errs.append(f"{path}.ports[{i}].hostPort: Invalid value: {hp!r}")
+        if p.get("protocol", "TCP") not in ("TCP", "UDP", "SCTP"):
+            errs.append(f"{path}.ports[{i}].protocol: Unsupported value: {p.get('protocol')!r}")
+        key = (hp, p.get("protocol", "TCP"))
+        if hp and key in ports:
+            errs.append(f"{path}.ports[{i}].hostPort: Duplicate value: {hp}")
+        ports.add(key)
+    for i, e in enumerate(c.get("env") or []):
+        if not e.get("name"):
+            errs.append(f"{path}.env[{i}].name: Required value")
+    if init:
+        for probe in ("livenessProbe", "readinessProbe"):
+            if c.get(probe):
+                errs.append(f"{path}.{probe}: Invalid value: must not be set for init containers")
+    return errs
+
+
+def _validate_node_selector_terms(terms, path) -> list[str]:
+    errs = []
+    for i, t in enumerate(terms or []):
+        try:
+            node_requirements_as_selector(t.get("matchExpressions"))
+        except SelectorError as e:
+            errs.append(f"{path}[{i}].matchExpressions: Invalid value: {e}")
+    return errs
+
+
+def validate_pod_spec(spec: dict, path="spec") -> list[str]:
+    errs = []
+    containers = spec.get("containers") or []
+    inits = spec.get("initContainers") or []
+    if not containers:
+        errs.append(f"{path}.containers: Required value")
+    names = set()
+    for kind, lst in (("initContainers", inits), ("containers", containers)):
+        for i, c in enumerate(lst):
+            errs += _validate_container(c, f"{path}.{kind}[{i}]", kind == "initContainers")
+            n = c.get("name")
+            if n in names:
+                errs.append(f"{path}.{kind}[{i}].name: Duplicate value: {n!r}")
+            names.add(n)
+    rp = spec.get("restartPolicy", "Always")
+    if rp not in RESTART_POLICIES:
+        errs.append(f"{path}.restartPolicy: Unsupported value: {rp!r}")
+    vols = set()
+    for i, v in enumerate(spec.get("volumes") or []):
+        n = v.get("name") or ""
+        errs += [f"{path}.volumes[{i}].name: Invalid value: {n!r}: {e}" for e in is_dns1123_label(n)]
+        if n in vols:
+            errs.append(f"{path}.volumes[{i}].name: Duplicate value: {n!r}")
+        vols.add(n)
+    for kind, lst in (("initContainers", inits), ("containers", containers)):
+        for i, c in enumerate(lst):
+            for j, m in enumerate(c.get("volumeMounts") or []):
+                if m.get("name") not in vols:
+                    errs.append(f"{path}.{kind}[{i}].volumeMounts[{j}].name: Not found: {m.get('name')!r}")
+    for k, v in (spec.get("nodeSelector") or {}).items():
+        errs += [f"{path}.nodeSelector: Invalid value: {k!r}: {e}" for e in is_qualified_name(k)]
+        errs += [f"{path}.nodeSelector: Invalid value: {v!r}: {e}" for e in is_valid_label_value(str(v))]
+    for i, t in enumerate(spec.get("tolerations") or []):
+        op = t.get("operator") or "Equal"
+        if op not in ("Equal", "Exists"):
+            errs.append(f"{path}.tolerations[{i}].operator: Unsupported value: {op!r}")
+        if op == "Exists" and t.get("value"):
+            errs.append(f"{path}.tolerations[{i}].operator: Invalid value: value must be empty when `operator` is 'Exists'")
+        if t.get("effect") not in (None, "", "NoSchedule", "PreferNoSchedule", "NoExecute"):
+            errs.append(f"{path}.tolerations[{i}].effect: Unsupported value: {t.get('effect')!r}")
+    na = ((spec.get("affinity") or {}).get("nodeAffinity") or {})
+    req = na.get("requiredDuringSchedulingIgnoredDuringExecution") or {}
+    errs += _validate_node_selector_terms(req.get("nodeSelectorTerms"),
+                                          f"{path}.affinity.nodeAffinity.requiredDuringSchedulingIgnoredDuringExecution.nodeSelectorTerms")
+    for i, pt in enumerate(na.get("preferredDuringSchedulingIgnoredDuringExecution") or []):
+        w = pt.get("weight", 0)
+        if not 1 <= int(w) <= 100:
+            errs.append(f"{path}.affinity.nodeAffinity.preferredDuringSchedulingIgnoredDuringExecution[{i}].weight: Invalid value: {w}: must be in the range 1-100")
+    gp = spec.get("terminationGracePeriodSeconds")
+    if gp is not None and gp < 0:
+        errs.append(f"{path}.terminationGracePeriodSeconds: Invalid value: must be >= 0")
+    ads = spec.get("activeDeadlineSeconds")
+    if ads is not None and ads <= 0:
+        errs.append(f"{path}.activeDeadlineSeconds: Invalid value: must be > 0")
+    coll, xerrs = validate_extended_resources(spec.get("extendedResources"), f"{path}.extendedResources")
+    errs += xerrs
+    errs += validate_containers_extended_resources(containers, dict(coll), f"{path}.containers")
+    errs += validate_containers_extended_resources(inits, dict(coll), f"{path}.initContainers")  # fix #9
+    return errs
+
+
+_MUTABLE_CONTAINER_FIELDS = ("image",)
+
+
+def _strip_mutable(spec: dict) -> dict:
+    import copy
+    s = copy.deepcopy(spec)
+    for kind in ("containers", "initContainers"):
+        for c in s.get(kind) or []:
+            for f in _MUTABLE_CONTAINER_FIELDS:
+                c.pop(f, None)
+    s.pop("activeDeadlineSeconds", None)
+    s.pop("tolerations", None)
+    for pres in s.get("extendedResources") or []:
+        pres.pop("assigned", None)  # only pods/binding writes assigned
+        if not pres.get("affinity"):
+            pres.pop("affinity", None)
+    return s
+
+
+def validate_pod(pod: dict, old: dict | None = None) -> list[str]:
+    errs = validate_object_meta(pod, True)
+    errs += validate_pod_spec(pod.get("spec") or {})
+    if old is not None:
+        if _strip_mutable(pod.get("spec") or {}) != _strip_mutable(old.get("spec") or {}):
+            errs.append("spec: Forbidden: pod updates may not change fields other than `spec.containers[*].image`, "
+                        "`spec.initContainers[*].image`, `spec.activeDeadlineSeconds` or `spec.tolerations` (only additions to existing tolerations)")
+        old_nn = (old.get("spec") or {}).get("nodeName")
+        if old_nn and (pod.get("spec") or {}).get("nodeName") != old_nn:
+            errs.append("spec.nodeName: Forbidden: field is immutable once set")
+    return errs
+
+
+def validate_node(node: dict, old: dict | None = None) -> list[str]:
+    errs = validate_object_meta(node, False)
+    st = node.get("status") or {}
+    errs += _validate_resource_list(st.get("capacity"), "status.capacity")
+    errs += _validate_resource_list(st.get("allocatable"), "status.allocatable")
+    for rname, dom in (st.get("extendedResources") or {}).items():
+        if not is_extended_resource_name(rname):
+            errs.append(f"status.extendedResources[{rname}]: Invalid value: must be an extended resource name")
+        for did, dev in ((dom or {}).get("resources") or {}).items():
+            p = f"status.extendedResources[{rname}].resources[{did}]"
+            if dev.get("id", did) != did:
+                errs.append(f"{p}.id: Invalid value: must equal the map key")
+            if dev.get("health", HEALTHY) not in (HEALTHY, UNHEALTHY):
+                errs.append(f"{p}.health: Unsupported value: {dev.get('health')!r}")
+            for k, v in (dev.get("attributes") or {}).items():
+                errs += [f"{p}.attributes: Invalid value: {k!r}: {e}" for e in is_qualified_name(k)]
+                errs += [f"{p}.attributes: Invalid value: {v!r}: {e}" for e in is_valid_label_value(str(v))]
+    for i, t in enumerate((node.get("spec") or {}).get("taints") or []):
+        if t.get("effect") not in ("NoSchedule", "PreferNoSchedule", "NoExecute"):
+            errs.append(f"spec.taints[{i}].effect: Unsupported value: {t.get('effect')!r}")
+        errs += [f"spec.taints[{i}].key: Invalid value: {e}" for e in is_qualified_name(t.get("key") or "")]
+    return errs
+
+
+def validate_binding(b: dict) -> list[str]:
+    """Static half of fix #10 (node-state half: apiserver pods/binding registry)."""
+    errs = []
+    tgt = b.get("target") or {}
+    if tgt.get("kind") not in (None, "", "Node"):
+        errs.append("target.kind: Invalid value: must be empty or 'Node'")
+    if not tgt.get("name"):
+        errs.append("target.name: Required value")
+    for k, v in (tgt.get("extendedResourceBinding") or {}).items():
+        ids = (v or {}).get("resources")
+        if not isinstance(ids, list) or not all(isinstance(x, str) and x for x in ids):
+            errs.append(f"target.extendedResourceBinding[{k}].resources: Invalid value: must be a list of device IDs")
+        elif len(set(ids)) != len(ids):
+            errs.append(f"target.extendedResourceBinding[{k}].resources: Duplicate value: device IDs must be unique")
+    return errs
+
+
+def validate_namespace(ns: dict, old=None) -> list[str]:
+    return validate_object_meta(ns, False, is_dns1123_label)
+
+
+def _validate_template_owner(obj: dict, old=None, needs_selector=True) -> list[str]:
+    errs = validate_object_meta(obj, True)
+    spec = obj.get("spec") or {}
+    tpl = spec.get("template") or {}
+    errs += validate_pod_spec(tpl.get("spec") or {}, "spec.template.spec")
+    if needs_selector:
+        try:
+            sel = selector_from_label_selector(spec.get("selector"))
+            if not sel.matches((tpl.get("metadata") or {}).get("labels") or {}):
+                errs.append("spec.template.metadata.labels: Invalid value: `selector` does not match template `labels`")
+        except SelectorError as e:
+            errs.append(f"spec.selector: Invalid value: {e}")
+    if "replicas" in spec and (not isinstance(spec["replicas"], int) or spec["replicas"] < 0):
+        errs.append("spec.replicas: Invalid value: must be greater than or equal to 0")
+    return errs
+
+
+def validate_daemonset(ds, old=None):
+    errs = _validate_template_owner(ds, old)
+    rp = ((ds.get("spec") or {}).get("template") or {}).get("spec", {}).get("restartPolicy", "Always")
+    if rp != "Always":
+        errs.append("spec.template.spec.restartPolicy: Unsupported value: only 'Always' is supported")
+    return errs
+
+
+def validate_job(j, old=None):
+    errs = _validate_template_owner(j, old, needs_selector=False)
+    rp = ((j.get("spec") or {}).get("template") or {}).get("spec", {}).get("restartPolicy")
+    if rp not in ("OnFailure", "Never"):
+        errs.append("spec.template.spec.restartPolicy: Unsupported value: must be OnFailure or Never")
+    return errs
+
+
+def validate_generic_namespaced(obj, old=None):
+    return validate_object_meta(obj, True)
+
+
+def validate_event(ev, old=None):
+    errs = validate_object_meta(ev, True)
+    if not (ev.get("involvedObject") or {}).get("kind"):
+        errs.append("involvedObject.kind: Required value")
+    return errs
+
+
+register_hooks("Pod", validator=validate_pod)
+register_hooks("Node", validator=validate_node)
+register_hooks("Namespace", validator=validate_namespace)
+register_hooks("Event", validator=validate_event)
+register_hooks("DaemonSet", "apps/v1", validator=validate_daemonset)
+register_hooks("ReplicaSet", "apps/v1", validator=_validate_template_owner)
+register_hooks("Deployment", "apps/v1", validator=_validate_template_owner)
+register_hooks("Job", "batch/v1", validator=validate_job)
+for _k in ("ConfigMap", "Secret", "ServiceAccount", "Endpoints", "Service", "LimitRange", "ResourceQuota",
+           "PersistentVolumeClaim"):
+    register_hooks(_k, validator=validate_generic_namespaced)

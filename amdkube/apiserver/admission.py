@@ -1,0 +1,328 @@
+"""Admission chain: ordered mutating (`admit`) then validating (`validate`) plugins.
+
+Reference: staging/src/k8s.io/apiserver/pkg/admission (chain, Attributes, Handler with
+operation filter); plugin registry names in cmd/kube-apiserver/app/options/plugins.go:51,82.
+
+Plugins implemented:
+  * ResourceV2 — the fork's rewrite of legacy container limits into device-granular
+    PodSpec.extendedResources (plugin/pkg/admission/resourcev2/admission.go:51-118).
+    Deliberate change: the converted resource names are configurable
+    and default to amd.com/gpu (the reference hard-codes nvidia.com/gpu at :64,79).
+  * ExtendedResourceToleration — tolerate NoSchedule taints keyed by requested extended
+    resources (plugin/pkg/admission/extendedresourcetoleration/admission.go:32-80); it
+    also considers the fork's pod-level extendedResources.
+  * NamespaceLifecycle, NamespaceAutoProvision/Exists, LimitRanger (default requests/
+    limits), ResourceQuota (object-count + requests quota), ServiceAccount (default SA
+    name), DefaultTolerationSeconds, Priority, PodNodeSelector, AlwaysAdmit, AlwaysDeny.
+"""
+from __future__ import annotations
+
+import uuid
+
+from ..api import meta as m
+from ..api.helpers import (GPU_RESOURCE, pod_extended_resource_name, pod_requests, ExtendedResourceError,
+                           is_extended_resource_name)
+from ..api.quantity import Quantity
+
+CREATE, UPDATE, DELETE, CONNECT = "CREATE", "UPDATE", "DELETE", "CONNECT"
+
+
+class Attributes:
+    __slots__ = ("operation", "resource", "subresource", "namespace", "name", "obj", "old", "user", "kind")
+
+    def __init__(self, operation, resource, subresource, namespace, name, obj, old=None, user=None, kind=""):
+        self.operation, self.resource, self.subresource = operation, resource, subresource
+        self.namespace, self.name, self.obj, self.old, self.user, self.kind = namespace, name, obj, old, user, kind
+
+
+class Plugin:
+    name = ""
+    operations = (CREATE, UPDATE)
+
+    def handles(self, op: str) -> bool:
+        return op in self.operations
+
+    def admit(self, a: Attributes, ctx) -> None:  # mutating
+        pass
+
+    def validate(self, a: Attributes, ctx) -> None:  # validating
+        pass
+
+
+class ResourceV2(Plugin):
+    name = "ResourceV2"
+
+    def __init__(self, resource_names=(GPU_RESOURCE,)):
+        self.resource_names = tuple(resource_names)
+
+    def admit(self, a, ctx):
+        if a.subresource or a.resource != "pods":
+            return
+        spec = a.obj.setdefault("spec", {})
+        for kind in ("initContainers", "containers"):
+            for c in spec.get(kind) or []:
+                res = c.get("resources") or {}
+                lim = res.get("limits") or {}
+                for rname in [r for r in lim if r in self.resource_names]:
+                    val = lim[rname]
+                    if Quantity(val).is_zero():
+                        continue
+                    name = str(uuid.uuid4())
+                    spec.setdefault("extendedResources", []).append({
+                        "name": name,
+                        "resources": {"limits": {rname: val}, "requests": {rname: val}},
+                    })
+                    c["extendedResourceRequests"] = list(c.get("extendedResourceRequests") or []) + [name]
+                    lim.pop(rname, None)
+                    (res.get("requests") or {}).pop(rname, None)
+
+
+class ExtendedResourceToleration(Plugin):
+    name = "ExtendedResourceToleration"
+
+    def admit(self, a, ctx):
+        if a.subresource or a.resource != "pods":
+            return
+        spec = a.obj.setdefault("spec", {})
+        names = set()
+        for kind in ("initContainers", "containers"):
+            for c in spec.get(kind) or []:
+                for rl in ((c.get("resources") or {}).get("requests") or {}, (c.get("resources") or {}).get("limits") or {}):
+                    names.update(r for r in rl if is_extended_resource_name(r))
+        for pres in spec.get("extendedResources") or []:
+            try:
+                names.add(pod_extended_resource_name(pres))
+            except ExtendedResourceError:
+                pass
+        tols = spec.get("tolerations") or []
+        for n in sorted(names):
+            if not any(t.get("key") == n and t.get("operator") == "Exists" and t.get("effect") in ("NoSchedule", None, "") for t in tols):
+                tols.append({"key": n, "operator": "Exists", "effect": "NoSchedule"})
+        if tols:
+            spec["tolerations"] = tols
+
+
+class NamespaceLifecycle(Plugin):
+    """Reject creation in missing/terminating namespaces; protect system namespaces."""
+    name = "NamespaceLifecycle"
+    operations = (CREATE, UPDATE, DELETE)
+    immortal = ("default", "kube-system", "kube-public")
+
+    def validate(self, a, ctx):
+        if a.resource == "namespaces":
+            if a.operation == DELETE and a.name in self.immortal:
+                raise m.forbidden(f'namespace "{a.name}" is protected and cannot be deleted')
+            return
+        if not a.namespace or a.operation != CREATE:
+            return
+        if a.resource in ("events",) or a.subresource:
+            return
+        ns = ctx.get_namespace(a.namespace)
+        if ns is None:
+            raise m.not_found("namespaces", a.namespace)
+        if (ns.get("status") or {}).get("phase") == "Terminating":
+            raise m.forbidden(f'unable to create new content in namespace {a.namespace} because it is being terminated')
+
+
+class NamespaceAutoProvision(Plugin):
+    name = "NamespaceAutoProvision"
+    operations = (CREATE,)
+
+    def admit(self, a, ctx):
+        if a.namespace and a.resource != "namespaces" and ctx.get_namespace(a.namespace) is None:
+            ctx.create_namespace(a.namespace)
+
+
+class NamespaceExists(Plugin):
+    name = "NamespaceExists"
+    operations = (CREATE, UPDATE, DELETE)
+
+    def validate(self, a, ctx):
+        if a.namespace and a.resource != "namespaces" and ctx.get_namespace(a.namespace) is None:
+            raise m.not_found("namespaces", a.namespace)
+
+
+class ServiceAccount(Plugin):
+    name = "ServiceAccount"
+    operations = (CREATE,)
+
+    def admit(self, a, ctx):
+        if a.resource == "pods" and not a.subresource:
+            a.obj.setdefault("spec", {}).setdefault("serviceAccountName", "default")
+
+
+class DefaultTolerationSeconds(Plugin):
+    name = "DefaultTolerationSeconds"
+    operations = (CREATE,)
+
+    def __init__(self, seconds=300):
+        self.seconds = seconds
+
+    def admit(self, a, ctx):
+        if a.resource != "pods" or a.subresource:
+            return
+        tols = a.obj.setdefault("spec", {}).setdefault("tolerations", [])
+        for key in ("node.kubernetes.io/not-ready", "node.kubernetes.io/unreachable"):
+            if not any(t.get("key") == key and t.get("effect") in ("NoExecute", None, "") for t in tols):
+                tols.append({"key": key, "operator": "Exists", "effect": "NoExecute", "tolerationSeconds": self.seconds})
+
+
+class LimitRanger(Plugin):
+    """Apply LimitRange container defaults (default / defaultRequest) and max checks."""
+    name = "LimitRanger"
+    operations = (CREATE,)
+
+    def admit(self, a, ctx):
+        if a.resource != "pods" or a.subresource:
+            return
+        for lr in ctx.list_objects("limitranges", a.namespace):
+            for item in (lr.get("spec") or {}).get("limits") or []:
+                if item.get("type") != "Container":
+                    continue
+                for c in a.obj.get("spec", {}).get("containers") or []:
+                    res = c.setdefault("resources", {})
+                    for k, v in (item.get("default") or {}).items():
+                        res.setdefault("limits", {}).setdefault(k, v)
+                    for k, v in (item.get("defaultRequest") or {}).items():
+                        res.setdefault("requests", {}).setdefault(k, v)
+
+    def validate(self, a, ctx):
+        if a.resource != "pods" or a.subresource:
+            return
+        for lr in ctx.list_objects("limitranges", a.namespace):
+            for item in (lr.get("spec") or {}).get("limits") or []:
+                if item.get("type") != "Container":
+                    continue
+                for c in a.obj.get("spec", {}).get("containers") or []:
+                    lim = (c.get("resources") or {}).get("limits") or {}
+                    for k, mx in (item.get("max") or {}).items():
+                        if k in lim and Quantity(lim[k]) > Quantity(mx):
+                            raise m.forbidden(f"maximum {k} usage per Container is {mx}, but limit is {lim[k]}")
+
+
+class ResourceQuota(Plugin):
+    """Enforce `pods`, `count/<res>`, `requests.<r>` and extended-resource hard limits."""
+    name = "ResourceQuota"
+    operations = (CREATE,)
+
+    def validate(self, a, ctx):
+        if a.subresource or not a.namespace:
+            return
+        quotas = ctx.list_objects("resourcequotas", a.namespace)
+        if not quotas:
+            return
+        pods = [p for p in ctx.list_objects("pods", a.namespace)
+                if (p.get("status") or {}).get("phase") not in ("Succeeded", "Failed")] if a.resource == "pods" else []
+        for q in quotas:
+            hard = (q.get("spec") or {}).get("hard") or {}
+            for k, v in hard.items():
+                lim = Quantity(v)
+                if a.resource == "pods" and k == "pods" and len(pods) + 1 > lim.value():
+                    raise m.forbidden(f'exceeded quota: {m.name_of(q)}, requested: pods=1, used: pods={len(pods)}, limited: pods={v}')
+                if k == f"count/{a.resource}" and len(ctx.list_objects(a.resource, a.namespace)) + 1 > lim.value():
+                    raise m.forbidden(f"exceeded quota: {m.name_of(q)}, requested: {k}=1, limited: {k}={v}")
+                if a.resource == "pods" and (k.startswith("requests.") or is_extended_resource_name(k)):
+                    r = k[len("requests."):] if k.startswith("requests.") else k
+                    used = sum(_pod_usage(p, r) for p in pods)
+                    want = _pod_usage(a.obj, r)
+                    if want and used + want > (lim.milli_value() if r == "cpu" else lim.value()):
+                        raise m.forbidden(f"exceeded quota: {m.name_of(q)}, requested: {k}={want}, used: {k}={used}, limited: {k}={v}")
+
+
+def _pod_usage(pod, r):
+    req = pod_requests(pod)
+    if r in req:
+        return req[r]
+    n = 0
+    for pres in (pod.get("spec") or {}).get("extendedResources") or []:
+        lim = (pres.get("resources") or {}).get("limits") or {}
+        if r in lim:
+            n += Quantity(lim[r]).value()
+    return n
+
+
+class Priority(Plugin):
+    name = "Priority"
+    operations = (CREATE,)
+
+    def admit(self, a, ctx):
+        if a.resource != "pods" or a.subresource:
+            return
+        spec = a.obj.setdefault("spec", {})
+        pcn = spec.get("priorityClassName")
+        if pcn:
+            pc = ctx.get_object("priorityclasses", "", pcn)
+            if pc is None:
+                if pcn in ("system-cluster-critical", "system-node-critical"):
+                    spec["priority"] = 2000000000 if pcn == "system-cluster-critical" else 2000001000
+                    return
+                raise m.forbidden(f"no PriorityClass with name {pcn} was found")
+            spec["priority"] = int(pc.get("value", 0))
+        else:
+            default = [pc for pc in ctx.list_objects("priorityclasses", "") if pc.get("globalDefault")]
+            spec.setdefault("priority", int(default[0].get("value", 0)) if default else 0)
+
+
+class PodNodeSelector(Plugin):
+    """Merge the namespace annotation scheduler.alpha.kubernetes.io/node-selector."""
+    name = "PodNodeSelector"
+    operations = (CREATE,)
+    ANNOTATION = "scheduler.alpha.kubernetes.io/node-selector"
+
+    def admit(self, a, ctx):
+        if a.resource != "pods" or a.subresource:
+            return
+        ns = ctx.get_namespace(a.namespace) or {}
+        sel = m.annotations_of(ns).get(self.ANNOTATION)
+        if not sel:
+            return
+        ns_sel = dict(kv.split("=", 1) for kv in sel.split(",") if "=" in kv)
+        pod_sel = a.obj.setdefault("spec", {}).setdefault("nodeSelector", {})
+        for k, v in ns_sel.items():
+            if k in pod_sel and pod_sel[k] != v:
+                raise m.forbidden("pod node label selector conflicts with its namespace node label selector")
+            pod_sel[k] = v
+
+
+class AlwaysAdmit(Plugin):
+    name = "AlwaysAdmit"
+
+
+class AlwaysDeny(Plugin):
+    name = "AlwaysDeny"
+    operations = (CREATE, UPDATE, DELETE, CONNECT)
+
+    def validate(self, a, ctx):
+        raise m.forbidden("admission control is denying all modifications")
+
+
+REGISTRY = {p.name: p for p in (ResourceV2, ExtendedResourceToleration, NamespaceLifecycle, NamespaceAutoProvision,
+                                 NamespaceExists, ServiceAccount, DefaultTolerationSeconds, LimitRanger, ResourceQuota,
+                                 Priority, PodNodeSelector, AlwaysAdmit, AlwaysDeny)}
+
+# Matches the fork's recommended ordering (hack/local-up-cluster.sh:424 adds ResourceV2).
+DEFAULT_CHAIN = ("NamespaceLifecycle", "LimitRanger", "ServiceAccount", "DefaultTolerationSeconds", "Priority",
+                 "ResourceV2", "ExtendedResourceToleration", "ResourceQuota")
+
+
+class Chain:
+    def __init__(self, names=DEFAULT_CHAIN, config: dict | None = None):
+        config = config or {}
+        self.plugins: list[Plugin] = []
+        for n in names:
+            n = n.strip()
+            if not n:
+                continue
+            if n not in REGISTRY:
+                raise ValueError(f"unknown admission plugin {n!r}")
+            self.plugins.append(REGISTRY[n](**config.get(n, {})))
+
+    def admit(self, a: Attributes, ctx):
+        for p in self.plugins:
+            if p.handles(a.operation):
+                p.admit(a, ctx)
+
+    def validate(self, a: Attributes, ctx):
+        for p in self.plugins:
+            if p.handles(a.operation):
+                p.validate(a, ctx)

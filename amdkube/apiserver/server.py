@@ -1,0 +1,463 @@
+"""kube-apiserver equivalent: REST + chunked watch over aiohttp on the embedded MVCC store.
+
+Reference: handler chain and verbs — staging/src/k8s.io/apiserver/pkg/endpoints/handlers/
+{create.go:37-170, get.go, update.go, patch.go, delete.go, watch.go}; filters
+(authn/authz/max-in-flight) staging/.../server/filters; discovery /api, /apis; request
+metrics staging/.../endpoints/metrics/metrics.go:41-93; profiling routes/profiling.go.
+
+Fast paths (all single-threaded on the event loop, no locks):
+  * GET/LIST stream stored JSON bytes straight from the store (resourceVersion was
+    embedded at commit) — no decode/encode unless a selector must be evaluated;
+  * watch frames are `{"type":T,"object":<stored bytes>}` lines, one decode per event
+    shared by every filtered watcher (storage.event_object cache).
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import random
+import time
+
+from aiohttp import ClientSession, ClientTimeout, web
+
+from .. import GIT_VERSION
+from ..api import meta as m
+from ..api.scheme import SCHEME
+from ..store import MVCCStore, PUT
+from ..utils import profiling
+from ..utils.metrics import CONTENT_TYPE, MICRO_BUCKETS, Counter, Histogram, new_registry, render
+from . import admission as adm
+from .registry import Registry
+
+log = logging.getLogger("amdkube.apiserver")
+
+_JSON = "application/json"
+
+
+def _resp(obj, status=200) -> web.Response:
+    body = obj if isinstance(obj, (bytes, bytearray)) else json.dumps(obj, separators=(",", ":")).encode()
+    return web.Response(body=body, status=status, content_type=_JSON)
+
+
+def _err(e: m.StatusError) -> web.Response:
+    return _resp(e.status(), e.code)
+
+
+class APIServer:
+    def __init__(self, store: MVCCStore | None = None, admission_plugins=adm.DEFAULT_CHAIN, admission_config=None,
+                 token_auth: dict | None = None, authorization_mode: str = "AlwaysAllow",
+                 max_in_flight: int = 400, max_mutating_in_flight: int = 200, event_ttl: float = 3600.0,
+                 anonymous_auth: bool = True):
+        self.store = store or MVCCStore()
+        self.admission = adm.Chain(admission_plugins, admission_config)
+        self.registry = Registry(self.store, self.admission)
+        self.tokens = token_auth or {}
+        self.anonymous = anonymous_auth
+        self.authz_mode = authorization_mode
+        self._ro = asyncio.Semaphore(max_in_flight) if max_in_flight else None
+        self._rw = asyncio.Semaphore(max_mutating_in_flight) if max_mutating_in_flight else None
+        self.event_ttl = event_ttl
+        self.metrics = new_registry()
+        self.m_count = Counter("apiserver_request_count", "Counter of apiserver requests broken out for each verb, API resource, client, and HTTP response contentType and code.",
+                               ["verb", "resource", "subresource", "code"], registry=self.metrics)
+        self.m_lat = Histogram("apiserver_request_latencies", "Response latency distribution in microseconds for each verb, resource and subresource.",
+                               ["verb", "resource", "subresource"], buckets=MICRO_BUCKETS, registry=self.metrics)
+        self.watch_count = 0
+        self.app = web.Application(client_max_size=64 * 1024 * 1024)
+        self.app.router.add_get("/healthz", self.healthz)
+        self.app.router.add_get("/healthz/{check}", self.healthz)
+        self.app.router.add_get("/version", self.version)
+        self.app.router.add_get("/metrics", self.metrics_handler)
+        self.app.router.add_get("/api", self.api_versions)
+        self.app.router.add_get("/apis", self.api_groups)
+        profiling.add_routes(self.app)
+        self.app.router.add_route("*", "/api/{tail:.*}", self.dispatch)
+        self.app.router.add_route("*", "/apis/{tail:.*}", self.dispatch)
+        self._runner = None
+        self._site = None
+        self._bg: list[asyncio.Task] = []
+        self.port = None
+        self._http: ClientSession | None = None
+        self._bootstrap()
+
+    def _bootstrap(self):
+        for ns in ("default", "kube-system", "kube-public"):
+            if self.registry.get_namespace(ns) is None:
+                self.registry.create_namespace(ns)
+
+    # ---------------------------------------------------------------- lifecycle
+    async def start(self, host="127.0.0.1", port=0):
+        self._runner = web.AppRunner(self.app, access_log=None, handler_cancellation=True)
+        await self._runner.setup()
+        self._site = web.TCPSite(self._runner, host, port, backlog=1024, reuse_address=True)
+        await self._site.start()
+        self.port = self._site._server.sockets[0].getsockname()[1]
+        self.host = host
+        self._bg.append(asyncio.create_task(self._event_gc()))
+        log.info("apiserver serving on http://%s:%d", host, self.port)
+        return self
+
+    @property
+    def url(self):
+        return f"http://{self.host}:{self.port}"
+
+    async def stop(self):
+        for t in self._bg:
+            t.cancel()
+        for w in list(self.store.watchers):
+            w.close()
+        if self._http:
+            await self._http.close()
+        if self._runner:
+            await self._runner.cleanup()
+
+    async def _event_gc(self):
+        rs = self.registry.rs("events")
+        while True:
+            await asyncio.sleep(min(60.0, self.event_ttl / 2))
+            cutoff = time.time() - self.event_ttl
+            for ev in rs.list()[0]:
+                ts = m.parse_time(ev.get("lastTimestamp") or (ev.get("metadata") or {}).get("creationTimestamp"))
+                if ts is not None and ts < cutoff:
+                    try:
+                        rs.storage.delete(rs.key(m.namespace_of(ev), m.name_of(ev)))
+                    except m.StatusError:
+                        pass
+
+    # ----------------------------------------------------------- misc handlers
+    async def healthz(self, request):
+        return web.Response(text="ok")
+
+    async def version(self, request):
+        return _resp({"major": "1", "minor": "9", "gitVersion": GIT_VERSION, "platform": "linux/amd64",
+                      "compiler": "cpython", "goVersion": "n/a"})
+
+    async def metrics_handler(self, request):
+        return web.Response(body=render(self.metrics), headers={"Content-Type": CONTENT_TYPE})
+
+    async def api_versions(self, request):
+        return _resp({"kind": "APIVersions", "versions": ["v1"],
+                      "serverAddressByClientCIDRs": [{"clientCIDR": "0.0.0.0/0", "serverAddress": request.host}]})
+
+    async def api_groups(self, request):
+        groups = {}
+        for ri in SCHEME.by_kind.values():
+            if ri.group:
+                groups.setdefault(ri.group, set()).add(ri.version)
+        return _resp({"kind": "APIGroupList", "apiVersion": "v1", "groups": [
+            {"name": g, "versions": [{"groupVersion": f"{g}/{v}", "version": v} for v in sorted(vs)],
+             "preferredVersion": {"groupVersion": f"{g}/{sorted(vs)[0]}", "version": sorted(vs)[0]}}
+            for g, vs in sorted(groups.items())]})
+
+    def _resource_list(self, group, version):
+        res = []
+        for ri in SCHEME.by_kind.values():
+            if ri.group == group and ri.version == version:
+                res.append({"name": ri.plural, "singularName": ri.kind.lower(), "namespaced": ri.namespaced,
+                            "kind": ri.kind, "verbs": list(ri.verbs), "shortNames": list(ri.short_names)})
+                for sub in ri.subresources:
+                    res.append({"name": f"{ri.plural}/{sub}", "singularName": "", "namespaced": ri.namespaced,
+                                "kind": "Binding" if sub == "binding" else ri.kind, "verbs": ["get", "create", "update", "patch"]})
+        return {"kind": "APIResourceList", "apiVersion": "v1", "groupVersion": f"{group}/{version}" if group else version,
+                "resources": res}
+
+    # ------------------------------------------------------------------ auth
+    def _authenticate(self, request):
+        h = request.headers.get("Authorization", "")
+        if h.startswith("Bearer "):
+            user = self.tokens.get(h[7:].strip())
+            if user is None:
+                raise m.unauthorized()
+            return user
+        if self.tokens and not self.anonymous:
+            raise m.unauthorized()
+        return {"name": "system:anonymous", "groups": ["system:unauthenticated"]}
+
+    def _authorize(self, user, verb, resource):
+        if self.authz_mode == "AlwaysDeny":
+            raise m.forbidden(f'User "{user["name"]}" cannot {verb} {resource}')
+        if self.authz_mode == "RBACLite" and "system:masters" not in (user.get("groups") or []) \
+                and user["name"].startswith("system:anonymous") and verb not in ("get", "list", "watch"):
+            raise m.forbidden(f'User "{user["name"]}" cannot {verb} {resource}')
+
+    # -------------------------------------------------------------- dispatch
+    def _parse(self, path: str):
+        parts = [p for p in path.split("/") if p]
+        if parts[0] == "api":
+            if len(parts) < 2:
+                raise m.not_found("path", path)
+            group, version, rest = "", parts[1], parts[2:]
+        else:
+            if len(parts) < 3:
+                if len(parts) == 2:
+                    return parts[1], None, None, None, None, None, False
+                raise m.not_found("path", path)
+            group, version, rest = parts[1], parts[2], parts[3:]
+        watch = False
+        if rest and rest[0] == "watch":
+            watch, rest = True, rest[1:]
+        ns = ""
+        if len(rest) >= 3 and rest[0] == "namespaces":
+            ns, rest = rest[1], rest[2:]
+        resource = rest[0] if rest else None
+        name = rest[1] if len(rest) > 1 else None
+        sub = "/".join(rest[2:]) if len(rest) > 2 else ""
+        if resource == "namespaces" and name and not ns:
+            pass
+        return group, version, resource, ns, name, sub, watch
+
+    async def dispatch(self, request: web.Request):
+        t0 = time.perf_counter()
+        verb, resource, sub, code = request.method, "", "", 500
+        sem = None
+        try:
+            user = self._authenticate(request)
+            group, version, resource, ns, name, sub, watch = self._parse(request.path)
+            if resource is None:
+                if version is None:  # /apis/<group>
+                    vs = sorted({ri.version for ri in SCHEME.by_kind.values() if ri.group == group})
+                    if not vs:
+                        raise m.not_found("group", group)
+                    code = 200
+                    return _resp({"kind": "APIGroup", "apiVersion": "v1", "name": group,
+                                  "versions": [{"groupVersion": f"{group}/{v}", "version": v} for v in vs],
+                                  "preferredVersion": {"groupVersion": f"{group}/{vs[0]}", "version": vs[0]}})
+                code = 200
+                return _resp(self._resource_list(group, version))
+            rs = self.registry.resources.get((group, resource))
+            if rs is None or rs.ri.version != version:
+                raise m.not_found("resource", f"{group}/{version}/{resource}")
+            q = request.query
+            is_watch = watch or q.get("watch") in ("true", "1")
+            kverb = {"GET": "watch" if is_watch else ("get" if name else "list"), "POST": "create", "PUT": "update",
+                     "PATCH": "patch", "DELETE": "delete" if name else "deletecollection"}.get(verb, verb.lower())
+            verb = kverb.upper()
+            self._authorize(user, kverb, resource)
+            if is_watch:
+                code = 200
+                return await self._watch(request, rs, ns, name, q)
+            sem = self._rw if request.method in ("POST", "PUT", "PATCH", "DELETE") else self._ro
+            if sem is not None:
+                if sem.locked():
+                    raise m.too_many_requests()
+                await sem.acquire()
+            resp = await self._handle(request, rs, ns, name, sub, user, q)
+            code = resp.status
+            return resp
+        except m.StatusError as e:
+            code = e.code
+            return _err(e)
+        except (ValueError, KeyError, TypeError) as e:
+            code = 400
+            log.debug("bad request %s %s: %r", request.method, request.path, e)
+            return _err(m.bad_request(f"{type(e).__name__}: {e}"))
+        finally:
+            if sem is not None:
+                sem.release()
+            self.m_count.labels(verb, resource or "", sub or "", str(code)).inc()
+            if verb != "WATCH":
+                self.m_lat.labels(verb, resource or "", sub or "").observe((time.perf_counter() - t0) * 1e6)
+
+    async def _body(self, request):
+        data = await request.read()
+        if not data:
+            raise m.bad_request("empty request body")
+        ct = request.headers.get("Content-Type", _JSON)
+        if "yaml" in ct:
+            import yaml
+            return yaml.safe_load(data)
+        if data.startswith(b"k8s\x00"):
+            from ..api.scheme import decode_envelope
+            return decode_envelope(data)
+        return json.loads(data)
+
+    async def _handle(self, request, rs, ns, name, sub, user, q):
+        meth = request.method
+        ri = rs.ri
+        if ri.namespaced is False:
+            ns = ""
+        if meth == "GET":
+            if name and sub == "log" and ri.plural == "pods":
+                return await self._pod_log(request, ns, name, q)
+            if name:
+                if sub and sub not in ("status", "scale"):
+                    raise m.not_found("subresource", sub)
+                raw = rs.storage.get_raw(rs.key(ns, name))
+                if raw is None:
+                    raise m.not_found(ri.group_resource, name)
+                return _resp(raw)
+            return self._list(rs, ns, q)
+        if meth == "POST":
+            body = await self._body(request)
+            if name and sub == "binding" and ri.plural == "pods":
+                body.setdefault("metadata", {}).setdefault("name", name)
+                return _resp(self.registry.bind(ns, body, user), 201)
+            if name and sub == "eviction" and ri.plural == "pods":
+                obj, _ = rs.delete(ns, name, grace=((body.get("deleteOptions") or {}).get("gracePeriodSeconds")), user=user)
+                return _resp(m.success_status(), 201)
+            if ri.plural == "pods" and sub == "" and name is None and body.get("kind") == "Binding":
+                return _resp(self.registry.bind(ns, body, user), 201)
+            if name:
+                raise m.method_not_allowed("POST on a named resource")
+            dry = q.get("dryRun") == "All"
+            obj = rs.create(ns, body, user, dry_run=dry)
+            return _resp(obj, 201)
+        if meth == "PUT":
+            if not name:
+                raise m.method_not_allowed("PUT on a collection")
+            body = await self._body(request)
+            subr = sub if sub in ("status",) else ""
+            if sub == "finalize" and ri.plural == "namespaces":
+                subr = "finalize"
+            obj, created = rs.update(ns, name, body, subresource=subr, user=user)
+            return _resp(obj, 201 if created else 200)
+        if meth == "PATCH":
+            if not name:
+                raise m.method_not_allowed("PATCH on a collection")
+            data = await request.read()
+            ct = request.headers.get("Content-Type", "application/merge-patch+json")
+            obj, _ = rs.update(ns, name, None, subresource=sub if sub == "status" else "", user=user, patch=data,
+                               content_type=ct)
+            return _resp(obj)
+        if meth == "DELETE":
+            opts = {}
+            data = await request.read()
+            if data:
+                try:
+                    opts = json.loads(data)
+                except ValueError:
+                    raise m.bad_request("invalid DeleteOptions")
+            grace = opts.get("gracePeriodSeconds")
+            if "gracePeriodSeconds" in q:
+                grace = int(q["gracePeriodSeconds"])
+            prop = opts.get("propagationPolicy") or q.get("propagationPolicy")
+            if opts.get("orphanDependents") is True:
+                prop = "Orphan"
+            uid = (opts.get("preconditions") or {}).get("uid")
+            if name:
+                obj, now = rs.delete(ns, name, grace=grace, precond_uid=uid, user=user, propagation=prop)
+                return _resp(obj if not now or ri.plural == "pods" else m.success_status(
+                    {"name": name, "kind": ri.plural, "uid": m.uid_of(obj)}))
+            items, _, _ = rs.list(ns, q.get("labelSelector"), q.get("fieldSelector"))
+            for it in items:
+                try:
+                    rs.delete(m.namespace_of(it), m.name_of(it), grace=grace, user=user, propagation=prop)
+                except m.StatusError as e:
+                    if not m.is_not_found(e):
+                        raise
+            return _resp({"kind": ri.list_kind, "apiVersion": ri.api_version, "metadata": {}, "items": items})
+        raise m.method_not_allowed(meth)
+
+    def _list(self, rs, ns, q):
+        ri = rs.ri
+        limit = int(q.get("limit", "0") or 0)
+        cont = q.get("continue") or None
+        ls, fs = q.get("labelSelector"), q.get("fieldSelector")
+        if not ls and not fs and not limit and not cont:
+            raws, rev = rs.storage.list_raw(rs.prefix(ns))
+            body = (b'{"kind":"' + ri.list_kind.encode() + b'","apiVersion":"' + ri.api_version.encode() +
+                    b'","metadata":{"resourceVersion":"' + str(rev).encode() + b'"},"items":[' + b",".join(raws) + b"]}")
+            return _resp(body)
+        items, rev, nxt = rs.list(ns, ls, fs, limit, cont)
+        md = {"resourceVersion": str(rev)}
+        if nxt:
+            md["continue"] = nxt
+        return _resp({"kind": ri.list_kind, "apiVersion": ri.api_version, "metadata": md, "items": items})
+
+    async def _watch(self, request, rs, ns, name, q):
+        ri = rs.ri
+        if not ri.namespaced:
+            ns = ""
+        rv = q.get("resourceVersion", "")
+        ls, fs = q.get("labelSelector"), q.get("fieldSelector")
+        if name:
+            fs = f"metadata.name={name}" + (f",{fs}" if fs else "")
+        timeout = float(q.get("timeoutSeconds") or (1800 + random.random() * 1800))
+        initial = []
+        if rv in ("", "0"):
+            items, list_rev, _ = rs.list(ns, ls, fs)
+            initial = items
+            w = rs.watch(ns, str(list_rev), ls, fs)
+        else:
+            w = rs.watch(ns, rv, ls, fs)
+        resp = web.StreamResponse(status=200, headers={"Content-Type": _JSON, "Transfer-Encoding": "chunked"})
+        resp.enable_chunked_encoding()
+        await resp.prepare(request)
+        self.watch_count += 1
+        loop = asyncio.get_running_loop()
+        deadline = loop.time() + timeout
+        try:
+            if initial:
+                buf = bytearray()
+                for o in initial:
+                    buf += b'{"type":"ADDED","object":' + json.dumps(o, separators=(",", ":")).encode() + b"}\n"
+                await resp.write(bytes(buf))
+            while True:
+                rem = deadline - loop.time()
+                if rem <= 0:
+                    break
+                ev = await w.next(rem)
+                if ev is None:
+                    if w.closed:
+                        if getattr(w.w, "err", None):
+                            st = m.gone(f"watch closed: {w.w.err}").status()
+                            await resp.write(b'{"type":"ERROR","object":' + json.dumps(st).encode() + b"}\n")
+                        break
+                    continue
+                buf = bytearray(self._frame(ev))
+                # drain whatever else is already queued into the same chunk (batching)
+                while not w.w.queue.empty():
+                    nxt = w.w.queue.get_nowait()
+                    if nxt is None:
+                        break
+                    t = w._translate(nxt)
+                    if t is not None:
+                        buf += self._frame(t)
+                await resp.write(bytes(buf))
+        except (ConnectionResetError, asyncio.CancelledError):
+            pass
+        finally:
+            w.close()
+            self.watch_count -= 1
+        try:
+            await resp.write_eof()
+        except Exception:
+            pass
+        return resp
+
+    @staticmethod
+    def _frame(t) -> bytes:
+        typ, obj, ev = t
+        if ev.type == PUT:
+            data = ev.kv.value
+        else:
+            data = json.dumps(obj, separators=(",", ":")).encode()
+        return b'{"type":"' + typ.encode() + b'","object":' + data + b"}\n"
+
+    async def _pod_log(self, request, ns, name, q):
+        pod = self.registry.rs("pods").get(ns, name)
+        node_name = (pod.get("spec") or {}).get("nodeName")
+        if not node_name:
+            raise m.bad_request(f'pod "{name}" is not scheduled yet')
+        node = self.registry.rs("nodes").get("", node_name)
+        st = node.get("status") or {}
+        port = (((st.get("daemonEndpoints") or {}).get("kubeletEndpoint")) or {}).get("Port")
+        addr = next((a["address"] for a in st.get("addresses") or [] if a.get("type") == "InternalIP"), None) or \
+            next((a["address"] for a in st.get("addresses") or [] if a.get("type") == "Hostname"), "127.0.0.1")
+        if not port:
+            raise m.bad_request(f"node {node_name} has no kubelet endpoint")
+        container = q.get("container") or ((pod.get("spec") or {}).get("containers") or [{}])[0].get("name", "")
+        params = {k: v for k, v in q.items() if k in ("tailLines", "follow", "previous", "sinceSeconds", "timestamps")}
+        if self._http is None:
+            self._http = ClientSession(timeout=ClientTimeout(total=None))
+        url = f"http://{addr}:{port}/containerLogs/{ns}/{name}/{container}"
+        async with self._http.get(url, params=params) as r:
+            if r.status != 200:
+                raise m.StatusError(r.status, "BadRequest", (await r.text())[:500])
+            out = web.StreamResponse(status=200, headers={"Content-Type": "text/plain"})
+            await out.prepare(request)
+            async for chunk in r.content.iter_any():
+                await out.write(chunk)
+            await out.write_eof()
+            return out

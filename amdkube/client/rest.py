@@ -1,0 +1,251 @@
+"""Async REST client (client-go rest + typed clientset equivalent).
+
+Reference: staging/src/k8s.io/client-go/rest (request building, errors → StatusError,
+QPS/burst token-bucket throttling), watch decoding (rest/watch + streamwatcher), and the
+fork's Binding with extendedResourceBinding (plugin/pkg/scheduler/scheduler.go:483-491).
+Fault injection: `chaos` = probability of a simulated "connection reset by peer" before
+a request is sent (pkg/client/chaosclient/chaosclient.go:37-110, kubelet --chaos-chance).
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import random
+import time
+from urllib.parse import quote
+
+import aiohttp
+
+from ..api import meta as m
+from ..api.scheme import SCHEME, ResourceInfo
+
+
+class ChaosError(ConnectionResetError):
+    pass
+
+
+class TokenBucket:
+    def __init__(self, qps: float, burst: int):
+        self.qps, self.burst = qps, max(1, burst)
+        self.tokens = float(self.burst)
+        self.t = time.monotonic()
+
+    async def wait(self):
+        while True:
+            now = time.monotonic()
+            self.tokens = min(self.burst, self.tokens + (now - self.t) * self.qps)
+            self.t = now
+            if self.tokens >= 1:
+                self.tokens -= 1
+                return
+            await asyncio.sleep((1 - self.tokens) / self.qps)
+
+
+class Client:
+    def __init__(self, server: str, token: str | None = None, qps: float = 0, burst: int = 0,
+                 chaos: float = 0.0, user_agent: str = "amdkube", timeout: float = 60.0, pool: int = 64):
+        self.server = server.rstrip("/")
+        self.headers = {"User-Agent": user_agent, "Accept": "application/json"}
+        if token:
+            self.headers["Authorization"] = f"Bearer {token}"
+        self.limiter = TokenBucket(qps, burst or int(qps * 2) or 1) if qps else None
+        self.chaos = chaos
+        self.timeout = timeout
+        self.pool = pool
+        self._session: aiohttp.ClientSession | None = None
+        self._loop = None
+
+    # ---------------------------------------------------------------- session
+    @property
+    def session(self) -> aiohttp.ClientSession:
+        loop = asyncio.get_running_loop()
+        if self._session is None or self._session.closed or self._loop is not loop:
+            conn = aiohttp.TCPConnector(limit=self.pool, keepalive_timeout=60, ttl_dns_cache=None)
+            self._session = aiohttp.ClientSession(connector=conn, headers=self.headers,
+                                                  timeout=aiohttp.ClientTimeout(total=None, sock_connect=10))
+            self._loop = loop
+        return self._session
+
+    async def close(self):
+        if self._session is not None and not self._session.closed:
+            await self._session.close()
+        self._session = None
+
+    # ---------------------------------------------------------------- paths
+    @staticmethod
+    def resource_info(resource: str) -> ResourceInfo:
+        ri = SCHEME.resolve(resource)
+        if ri is None:
+            raise KeyError(f"unknown resource {resource!r}")
+        return ri
+
+    def path(self, ri: ResourceInfo, ns: str = "", name: str | None = None, sub: str = "") -> str:
+        p = ri.api_prefix()
+        if ri.namespaced and ns:
+            p += f"/namespaces/{quote(ns)}"
+        p += f"/{ri.plural}"
+        if name:
+            p += f"/{quote(name)}"
+        if sub:
+            p += f"/{sub}"
+        return p
+
+    # -------------------------------------------------------------- request
+    async def request(self, method: str, path: str, params=None, body=None, content_type="application/json",
+                      raw=False, timeout=None):
+        if self.limiter:
+            await self.limiter.wait()
+        if self.chaos and random.random() < self.chaos:
+            raise ChaosError("connection reset by peer (chaos)")
+        data = None
+        headers = None
+        if body is not None:
+            data = body if isinstance(body, (bytes, str)) else json.dumps(body, separators=(",", ":"))
+            headers = {"Content-Type": content_type}
+        to = aiohttp.ClientTimeout(total=timeout or self.timeout)
+        async with self.session.request(method, self.server + path, params=params, data=data, headers=headers,
+                                        timeout=to) as r:
+            payload = await r.read()
+            if r.status >= 400:
+                try:
+                    st = json.loads(payload)
+                    if isinstance(st, dict) and st.get("kind") == "Status":
+                        raise m.StatusError.from_status(st)
+                except ValueError:
+                    pass
+                raise m.StatusError(r.status, "Unknown", payload.decode(errors="replace")[:500])
+            if raw:
+                return payload
+            return json.loads(payload) if payload else None
+
+    # ------------------------------------------------------------ typed verbs
+    async def get(self, resource: str, name: str, ns: str = "") -> dict:
+        ri = self.resource_info(resource)
+        return await self.request("GET", self.path(ri, ns, name))
+
+    async def get_or_none(self, resource: str, name: str, ns: str = "") -> dict | None:
+        try:
+            return await self.get(resource, name, ns)
+        except m.StatusError as e:
+            if m.is_not_found(e):
+                return None
+            raise
+
+    async def list(self, resource: str, ns: str = "", label_selector=None, field_selector=None, limit=0):
+        """Returns (items, resourceVersion)."""
+        ri = self.resource_info(resource)
+        params = {}
+        if label_selector:
+            params["labelSelector"] = label_selector
+        if field_selector:
+            params["fieldSelector"] = field_selector
+        items, cont = [], None
+        while True:
+            if limit:
+                params["limit"] = str(limit)
+            if cont:
+                params["continue"] = cont
+            d = await self.request("GET", self.path(ri, ns), params=params)
+            items.extend(d.get("items") or [])
+            cont = (d.get("metadata") or {}).get("continue")
+            if not cont:
+                return items, (d.get("metadata") or {}).get("resourceVersion", "")
+
+    async def create(self, obj: dict, ns: str | None = None) -> dict:
+        ri = SCHEME.for_object(obj)
+        if ri is None:
+            raise KeyError(f"unknown kind {obj.get('apiVersion')}/{obj.get('kind')}")
+        ns = ns if ns is not None else (m.namespace_of(obj) or ("default" if ri.namespaced else ""))
+        return await self.request("POST", self.path(ri, ns), body=obj)
+
+    async def update(self, obj: dict, sub: str = "") -> dict:
+        ri = SCHEME.for_object(obj)
+        return await self.request("PUT", self.path(ri, m.namespace_of(obj), m.name_of(obj), sub), body=obj)
+
+    async def update_status(self, obj: dict) -> dict:
+        return await self.update(obj, "status")
+
+    async def patch(self, resource: str, name: str, patch, ns: str = "", sub: str = "",
+                    patch_type: str = "application/merge-patch+json") -> dict:
+        ri = self.resource_info(resource)
+        return await self.request("PATCH", self.path(ri, ns, name, sub), body=patch, content_type=patch_type)
+
+    async def delete(self, resource: str, name: str, ns: str = "", grace: int | None = None,
+                     uid: str | None = None, propagation: str | None = None):
+        ri = self.resource_info(resource)
+        opts = {"kind": "DeleteOptions", "apiVersion": "v1"}
+        if grace is not None:
+            opts["gracePeriodSeconds"] = grace
+        if uid:
+            opts["preconditions"] = {"uid": uid}
+        if propagation:
+            opts["propagationPolicy"] = propagation
+        return await self.request("DELETE", self.path(ri, ns, name), body=opts)
+
+    async def delete_collection(self, resource: str, ns: str = "", label_selector=None, grace=None):
+        ri = self.resource_info(resource)
+        params = {"labelSelector": label_selector} if label_selector else None
+        body = {"gracePeriodSeconds": grace} if grace is not None else None
+        return await self.request("DELETE", self.path(ri, ns), params=params, body=body)
+
+    async def bind(self, ns: str, name: str, node: str, ext_binding: dict | None = None, uid: str | None = None):
+        b = {"apiVersion": "v1", "kind": "Binding", "metadata": {"name": name, "namespace": ns},
+             "target": {"apiVersion": "v1", "kind": "Node", "name": node}}
+        if uid:
+            b["metadata"]["uid"] = uid
+        if ext_binding:
+            b["target"]["extendedResourceBinding"] = ext_binding
+        ri = self.resource_info("pods")
+        return await self.request("POST", self.path(ri, ns, name, "binding"), body=b)
+
+    async def evict(self, ns: str, name: str):
+        ri = self.resource_info("pods")
+        body = {"apiVersion": "policy/v1beta1", "kind": "Eviction", "metadata": {"name": name, "namespace": ns}}
+        return await self.request("POST", self.path(ri, ns, name, "eviction"), body=body)
+
+    async def logs(self, ns: str, name: str, container: str | None = None, tail: int | None = None) -> str:
+        ri = self.resource_info("pods")
+        params = {}
+        if container:
+            params["container"] = container
+        if tail is not None:
+            params["tailLines"] = str(tail)
+        return (await self.request("GET", self.path(ri, ns, name, "log"), params=params, raw=True)).decode(errors="replace")
+
+    async def watch(self, resource: str, ns: str = "", resource_version: str = "", label_selector=None,
+                    field_selector=None, timeout_seconds: int | None = None):
+        """Async generator of (type, obj). Raises StatusError(410) on ERROR/Expired frames."""
+        ri = self.resource_info(resource)
+        params = {"watch": "true", "resourceVersion": resource_version or ""}
+        if label_selector:
+            params["labelSelector"] = label_selector
+        if field_selector:
+            params["fieldSelector"] = field_selector
+        if timeout_seconds:
+            params["timeoutSeconds"] = str(timeout_seconds)
+        if self.limiter:
+            await self.limiter.wait()
+        if self.chaos and random.random() < self.chaos:
+            raise ChaosError("connection reset by peer (chaos)")
+        async with self.session.get(self.server + self.path(ri, ns), params=params,
+                                    timeout=aiohttp.ClientTimeout(total=None, sock_read=None)) as r:
+            if r.status >= 400:
+                payload = await r.read()
+                try:
+                    raise m.StatusError.from_status(json.loads(payload))
+                except ValueError:
+                    raise m.StatusError(r.status, "Unknown", payload.decode(errors="replace"))
+            buf = b""
+            async for chunk in r.content.iter_any():
+                buf += chunk
+                while True:
+                    i = buf.find(b"\n")
+                    if i < 0:
+                        break
+                    line, buf = buf[:i], buf[i + 1:]
+                    if not line.strip():
+                        continue
+                    ev = json.loads(line)
+                    if ev.get("type") == "ERROR":
+                        raise m.StatusError.from_status(ev.get("object") or {})
+                    yield ev["type"], ev["object"]

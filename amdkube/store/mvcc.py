@@ -1,0 +1,326 @@
+"""Embedded MVCC key-value store with revisioned watch, compaction and WAL+snapshot.
+
+Replaces external etcd v3 (reference SURVEY L0/U7: the apiserver's etcd3 adapter does
+Create as `Txn(If ModRevision==0).Then(Put)` — staging/.../storage/etcd3/store.go:152-200 —
+GuaranteedUpdate as a ModRevision CAS loop (:263) and Watch from a revision (:661)).
+
+Design (single writer, in-process):
+  * one global monotonically increasing revision; every KV keeps create/mod revision and
+    a per-key version, exactly like etcd;
+  * all mutations are compare-and-swap on mod_revision (0 == "must not exist");
+  * an in-memory event history ring serves watch-from-revision; reading before the
+    compaction point raises Compacted (HTTP 410 "too old resource version" upstream);
+  * durability: an append-only WAL (one JSON line per committed revision) plus periodic
+    snapshots; recovery = snapshot + WAL replay, revisions preserved;
+  * watcher fan-out happens on commit with per-watcher queues; slow watchers whose queue
+    exceeds `max_queue` are terminated (cacher.go behaviour) so they re-list.
+Values are opaque bytes (the apiserver stores compact JSON).
+"""
+from __future__ import annotations
+
+import asyncio
+import base64
+import collections
+import json
+import os
+import threading
+import time
+
+
+class KeyExists(Exception):
+    pass
+
+
+class KeyNotFound(Exception):
+    pass
+
+
+class CASFailed(Exception):
+    def __init__(self, current):
+        super().__init__("mod revision mismatch")
+        self.current = current
+
+
+class Compacted(Exception):
+    def __init__(self, compact_rev):
+        super().__init__(f"required revision has been compacted (compacted at {compact_rev})")
+        self.compact_rev = compact_rev
+
+
+class KV:
+    __slots__ = ("key", "value", "create_rev", "mod_rev", "version")
+
+    def __init__(self, key, value, create_rev, mod_rev, version):
+        self.key, self.value, self.create_rev, self.mod_rev, self.version = key, value, create_rev, mod_rev, version
+
+    def __repr__(self):
+        return f"KV({self.key!r}, rev={self.mod_rev})"
+
+
+PUT, DELETE = "PUT", "DELETE"
+
+
+class Event:
+    __slots__ = ("type", "kv", "prev", "rev", "cache")
+
+    def __init__(self, type_, kv, prev, rev):
+        self.type, self.kv, self.prev, self.rev = type_, kv, prev, rev
+        self.cache = None  # decoded-object cache shared by all watchers of this event
+
+
+class Watcher:
+    __slots__ = ("prefix", "exact", "queue", "closed", "store", "_loop", "err")
+
+    def __init__(self, store, prefix, exact, loop):
+        self.store, self.prefix, self.exact = store, prefix, exact
+        self.queue: asyncio.Queue = asyncio.Queue()
+        self.closed = False
+        self.err = None
+        self._loop = loop
+
+    def wants(self, key: str) -> bool:
+        return key == self.prefix if self.exact else key.startswith(self.prefix)
+
+    def _deliver(self, ev):
+        if self.closed:
+            return
+        if self.queue.qsize() >= self.store.max_queue:
+            self.err = "watcher too slow"
+            self.close()
+            return
+        self.queue.put_nowait(ev)
+
+    def deliver(self, ev):
+        try:
+            running = asyncio.get_running_loop()
+        except RuntimeError:
+            running = None
+        if running is self._loop:
+            self._deliver(ev)
+        else:
+            self._loop.call_soon_threadsafe(self._deliver, ev)
+
+    def close(self):
+        if not self.closed:
+            self.closed = True
+            self.store._remove_watcher(self)
+            try:
+                self.queue.put_nowait(None)
+            except Exception:  # pragma: no cover
+                pass
+
+    async def next(self, timeout: float | None = None):
+        """Next Event, or None when closed/timeout."""
+        if self.closed and self.queue.empty():
+            return None
+        try:
+            if timeout is None:
+                return await self.queue.get()
+            return await asyncio.wait_for(self.queue.get(), timeout)
+        except asyncio.TimeoutError:
+            return None
+
+    def __aiter__(self):
+        return self
+
+    async def __anext__(self):
+        ev = await self.next()
+        if ev is None:
+            raise StopAsyncIteration
+        return ev
+
+
+class MVCCStore:
+    def __init__(self, data_dir: str | None = None, history: int = 200_000, max_queue: int = 500_000,
+                 snapshot_every: int = 50_000, fsync: bool = False):
+        self.kv: dict[str, KV] = {}
+        self.rev = 0
+        self.compact_rev = 0
+        self.history: collections.deque[Event] = collections.deque()
+        self.history_limit = history
+        self.max_queue = max_queue
+        self.watchers: list[Watcher] = []
+        self._lock = threading.RLock()
+        self.data_dir = data_dir
+        self.snapshot_every = snapshot_every
+        self.fsync = fsync
+        self._wal = None
+        self._since_snapshot = 0
+        self.commit_hooks = []  # fn(Event) called synchronously on commit (apiserver indexes)
+        if data_dir:
+            os.makedirs(data_dir, exist_ok=True)
+            self._recover()
+            self._wal = open(os.path.join(data_dir, "wal.log"), "ab", buffering=0)
+
+    # ----------------------------------------------------------------- reads
+    def get(self, key: str) -> KV | None:
+        return self.kv.get(key)
+
+    def range(self, prefix: str, limit: int = 0, start_after: str | None = None):
+        """Keys with `prefix`, sorted; returns (kvs, rev, more)."""
+        with self._lock:
+            keys = sorted(k for k in self.kv if k.startswith(prefix) and (start_after is None or k > start_after))
+            more = False
+            if limit and len(keys) > limit:
+                keys, more = keys[:limit], True
+            return [self.kv[k] for k in keys], self.rev, more
+
+    def count(self, prefix: str) -> int:
+        return sum(1 for k in self.kv if k.startswith(prefix))
+
+    # ------------------------------------------------------------- mutations
+    def put(self, key: str, value, expect_mod_rev: int | None = None) -> KV:
+        """CAS put. expect_mod_rev: None = unconditional, 0 = must not exist, n = must match.
+
+        `value` may be bytes or a callable rev -> bytes (lets the caller embed the commit
+        revision, e.g. metadata.resourceVersion, into the stored bytes).
+        """
+        with self._lock:
+            cur = self.kv.get(key)
+            if expect_mod_rev is not None:
+                if expect_mod_rev == 0 and cur is not None:
+                    raise KeyExists(key)
+                if expect_mod_rev and (cur is None or cur.mod_rev != expect_mod_rev):
+                    if cur is None:
+                        raise KeyNotFound(key)
+                    raise CASFailed(cur)
+            rev = self.rev + 1
+            data = value(rev) if callable(value) else value
+            new = KV(key, data, cur.create_rev if cur else rev, rev, (cur.version + 1) if cur else 1)
+            self.rev = rev
+            self.kv[key] = new
+            self._commit(Event(PUT, new, cur, rev), {"r": rev, "o": "p", "k": key, "v": _b(data)})
+            return new
+
+    def delete(self, key: str, expect_mod_rev: int | None = None) -> KV:
+        with self._lock:
+            cur = self.kv.get(key)
+            if cur is None:
+                raise KeyNotFound(key)
+            if expect_mod_rev and cur.mod_rev != expect_mod_rev:
+                raise CASFailed(cur)
+            rev = self.rev + 1
+            self.rev = rev
+            del self.kv[key]
+            tomb = KV(key, cur.value, cur.create_rev, rev, 0)
+            self._commit(Event(DELETE, tomb, cur, rev), {"r": rev, "o": "d", "k": key})
+            return cur
+
+    def _commit(self, ev: Event, rec: dict):
+        if self._wal is not None:
+            self._wal.write((json.dumps(rec, separators=(",", ":")) + "\n").encode())
+            if self.fsync:
+                os.fsync(self._wal.fileno())
+            self._since_snapshot += 1
+            if self._since_snapshot >= self.snapshot_every:
+                self.snapshot()
+        self.history.append(ev)
+        if len(self.history) > self.history_limit:
+            old = self.history.popleft()
+            self.compact_rev = old.rev
+        for h in self.commit_hooks:
+            h(ev)
+        key = ev.kv.key
+        for w in list(self.watchers):
+            if w.wants(key):
+                w.deliver(ev)
+
+    def compact(self, rev: int):
+        """Drop history at or below `rev` (etcd Compact)."""
+        with self._lock:
+            while self.history and self.history[0].rev <= rev:
+                self.history.popleft()
+            self.compact_rev = max(self.compact_rev, min(rev, self.rev))
+
+    # ----------------------------------------------------------------- watch
+    def watch(self, prefix: str, start_rev: int = 0, exact: bool = False) -> Watcher:
+        """Events with rev >= start_rev (0 = from now on)."""
+        loop = asyncio.get_running_loop()
+        with self._lock:
+            if start_rev and start_rev <= self.compact_rev:
+                raise Compacted(self.compact_rev)
+            w = Watcher(self, prefix, exact, loop)
+            if start_rev:
+                for ev in self.history:
+                    if ev.rev >= start_rev and w.wants(ev.kv.key):
+                        w.queue.put_nowait(ev)
+            self.watchers.append(w)
+            return w
+
+    def _remove_watcher(self, w):
+        with self._lock:
+            try:
+                self.watchers.remove(w)
+            except ValueError:
+                pass
+
+    # ------------------------------------------------------------ durability
+    def snapshot(self):
+        if not self.data_dir:
+            return
+        path = os.path.join(self.data_dir, "snapshot.json")
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump({"rev": self.rev, "compact_rev": self.compact_rev,
+                       "kv": [[k.key, _b(k.value), k.create_rev, k.mod_rev, k.version] for k in self.kv.values()]}, f)
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, path)
+        if self._wal is not None:
+            self._wal.close()
+        self._wal = open(os.path.join(self.data_dir, "wal.log"), "wb", buffering=0)
+        self._since_snapshot = 0
+
+    def _recover(self):
+        snap = os.path.join(self.data_dir, "snapshot.json")
+        if os.path.exists(snap):
+            with open(snap) as f:
+                s = json.load(f)
+            self.rev = s["rev"]
+            self.compact_rev = s["rev"]
+            for key, v, cr, mr, ver in s["kv"]:
+                self.kv[key] = KV(key, _unb(v), cr, mr, ver)
+        wal = os.path.join(self.data_dir, "wal.log")
+        if os.path.exists(wal):
+            with open(wal, "rb") as f:
+                for line in f:
+                    try:
+                        rec = json.loads(line)
+                    except ValueError:
+                        break  # torn tail write
+                    r = rec["r"]
+                    if r <= self.rev:
+                        continue
+                    key = rec["k"]
+                    cur = self.kv.get(key)
+                    if rec["o"] == "p":
+                        self.kv[key] = KV(key, _unb(rec["v"]), cur.create_rev if cur else r, r,
+                                          (cur.version + 1) if cur else 1)
+                    else:
+                        self.kv.pop(key, None)
+                    self.rev = r
+            self.compact_rev = self.rev
+
+    def close(self):
+        for w in list(self.watchers):
+            w.close()
+        if self._wal is not None:
+            self._wal.close()
+            self._wal = None
+
+
+def _b(v: bytes) -> str:
+    try:
+        return v.decode()
+    except UnicodeDecodeError:
+        return "b64:" + base64.b64encode(v).decode()
+
+
+def _unb(s: str) -> bytes:
+    if s.startswith("b64:"):
+        return base64.b64decode(s[4:])
+    return s.encode()
+
+
+def now() -> float:
+    return time.time()

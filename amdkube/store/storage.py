@@ -1,0 +1,234 @@
+"""storage.Interface over the MVCC store: typed (JSON) objects, preconditions, CAS update
+loops, filtered list and watch with in/out-of-filter event translation.
+
+Reference: staging/src/k8s.io/apiserver/pkg/storage/interfaces.go (Interface), etcd3
+store.go:152 (Create), :263 (GuaranteedUpdate: read → tryUpdate → CAS, retry on
+conflict), :477 (List), :661 (Watch); cacher.go:292/:469 (watch fan-out with filter,
+where an object leaving the filter is delivered as DELETED and entering as ADDED).
+
+Objects are stored as compact JSON whose metadata.resourceVersion already equals the
+commit revision (embedded at commit time), so GET/LIST/WATCH can stream stored bytes
+without re-encoding.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+from typing import Callable
+
+from ..api import meta as m
+from .mvcc import CASFailed, Compacted, KeyExists, KeyNotFound, MVCCStore, PUT, DELETE, Event
+
+
+def _with_rv(obj: dict):
+    def build(rev: int) -> bytes:
+        obj.setdefault("metadata", {})["resourceVersion"] = str(rev)
+        return json.dumps(obj, separators=(",", ":")).encode()
+    return build
+
+
+def decode_kv(value: bytes) -> dict:
+    return json.loads(value)
+
+
+def event_object(ev: Event) -> dict:
+    """Decoded object for an event (cached on the event, shared read-only)."""
+    if ev.cache is None:
+        if ev.type == PUT:
+            ev.cache = json.loads(ev.kv.value)
+        else:
+            o = json.loads(ev.prev.value)
+            o.setdefault("metadata", {})["resourceVersion"] = str(ev.rev)
+            ev.cache = o
+    return ev.cache
+
+
+def event_prev_object(ev: Event) -> dict | None:
+    return json.loads(ev.prev.value) if ev.prev is not None else None
+
+
+class Filter:
+    """Label/field predicate (storage.SelectionPredicate)."""
+    __slots__ = ("label", "field", "fields_fn")
+
+    def __init__(self, label=None, field=None, fields_fn: Callable | None = None):
+        self.label, self.field, self.fields_fn = label, field, fields_fn
+
+    def empty(self) -> bool:
+        return (self.label is None or self.label.empty()) and (self.field is None or self.field.empty())
+
+    def matches(self, obj: dict) -> bool:
+        if self.label is not None and not self.label.empty():
+            if not self.label.matches(m.labels_of(obj)):
+                return False
+        if self.field is not None and not self.field.empty():
+            fields = self.fields_fn(obj) if self.fields_fn else {"metadata.name": m.name_of(obj),
+                                                                  "metadata.namespace": m.namespace_of(obj)}
+            if not self.field.matches(fields):
+                return False
+        return True
+
+
+class Storage:
+    def __init__(self, store: MVCCStore, resource: str = "object"):
+        self.store = store
+        self.resource = resource
+
+    # -------------------------------------------------------------- basic ops
+    def create(self, key: str, obj: dict) -> dict:
+        try:
+            self.store.put(key, _with_rv(obj), expect_mod_rev=0)
+        except KeyExists:
+            raise m.already_exists(self.resource, key.rsplit("/", 1)[-1])
+        return obj
+
+    def get(self, key: str, ignore_not_found=False) -> dict | None:
+        kv = self.store.get(key)
+        if kv is None:
+            if ignore_not_found:
+                return None
+            raise m.not_found(self.resource, key.rsplit("/", 1)[-1])
+        return decode_kv(kv.value)
+
+    def get_raw(self, key: str) -> bytes | None:
+        kv = self.store.get(key)
+        return kv.value if kv else None
+
+    def guaranteed_update(self, key: str, try_update: Callable[[dict], dict | None],
+                          precond_uid: str | None = None, precond_rv: str | None = None,
+                          ignore_not_found=False, max_retries: int = 100) -> dict:
+        """Read-modify-CAS loop. try_update returns the new object (or None = no change).
+
+        A precondition on resourceVersion turns a CAS miss into a Conflict error instead of
+        a retry (optimistic concurrency for client updates).
+        """
+        for _ in range(max_retries):
+            kv = self.store.get(key)
+            if kv is None:
+                if not ignore_not_found:
+                    raise m.not_found(self.resource, key.rsplit("/", 1)[-1])
+                cur, mod = None, 0
+            else:
+                cur, mod = decode_kv(kv.value), kv.mod_rev
+                if precond_uid and m.uid_of(cur) != precond_uid:
+                    raise m.conflict(self.resource, m.name_of(cur),
+                                     f"Precondition failed: UID in precondition: {precond_uid}, UID in object meta: {m.uid_of(cur)}")
+                if precond_rv and precond_rv != str(mod):
+                    raise m.conflict(self.resource, m.name_of(cur),
+                                     "the object has been modified; please apply your changes to the latest version and try again")
+            new = try_update(cur)
+            if new is None:
+                return cur
+            try:
+                self.store.put(key, _with_rv(new), expect_mod_rev=mod)
+                return new
+            except (CASFailed, KeyExists, KeyNotFound):
+                continue
+        raise m.conflict(self.resource, key, "too many conflicting updates")
+
+    def delete(self, key: str, precond_uid: str | None = None, precond_rv: str | None = None) -> dict:
+        while True:
+            kv = self.store.get(key)
+            if kv is None:
+                raise m.not_found(self.resource, key.rsplit("/", 1)[-1])
+            cur = decode_kv(kv.value)
+            if precond_uid and m.uid_of(cur) != precond_uid:
+                raise m.conflict(self.resource, m.name_of(cur), "Precondition failed: UID mismatch")
+            if precond_rv and precond_rv != str(kv.mod_rev):
+                raise m.conflict(self.resource, m.name_of(cur), "the object has been modified")
+            try:
+                self.store.delete(key, expect_mod_rev=kv.mod_rev)
+            except CASFailed:
+                continue
+            except KeyNotFound:
+                raise m.not_found(self.resource, key.rsplit("/", 1)[-1])
+            cur["metadata"]["resourceVersion"] = str(self.store.rev)
+            return cur
+
+    def list(self, prefix: str, flt: Filter | None = None, limit: int = 0, continue_key: str | None = None):
+        """Returns (items, list_rv, continue_token)."""
+        kvs, rev, more = self.store.range(prefix, 0, continue_key)
+        items, last = [], None
+        for kv in kvs:
+            o = decode_kv(kv.value)
+            if flt is None or flt.matches(o):
+                items.append(o)
+                last = kv.key
+                if limit and len(items) >= limit:
+                    break
+        cont = None
+        if limit and len(items) >= limit and last is not None and kvs and last != kvs[-1].key:
+            cont = last
+        return items, rev, cont
+
+    def list_raw(self, prefix: str):
+        kvs, rev, _ = self.store.range(prefix)
+        return [kv.value for kv in kvs], rev
+
+    # ------------------------------------------------------------------ watch
+    def watch(self, prefix: str, rv: str | int | None, flt: Filter | None = None, exact=False) -> "FilteredWatch":
+        start = int(rv) + 1 if rv not in (None, "", "0", 0) else 0
+        try:
+            w = self.store.watch(prefix, start, exact)
+        except Compacted as e:
+            raise m.gone(f"too old resource version: {rv} ({e.compact_rev})")
+        return FilteredWatch(w, flt)
+
+
+class FilteredWatch:
+    """Translates raw KV events into (type, obj) honouring a filter (cacher semantics)."""
+
+    def __init__(self, w, flt: Filter | None):
+        self.w, self.flt = w, flt if (flt is not None and not flt.empty()) else None
+
+    def close(self):
+        self.w.close()
+
+    @property
+    def closed(self):
+        return self.w.closed
+
+    def _translate(self, ev: Event):
+        obj = event_object(ev)
+        if self.flt is None:
+            if ev.type == DELETE:
+                return m.DELETED, obj, ev
+            return (m.ADDED if ev.prev is None else m.MODIFIED), obj, ev
+        cur_ok = ev.type == PUT and self.flt.matches(obj)
+        prev_ok = False
+        if ev.prev is not None:
+            prev_obj = obj if ev.type == DELETE else event_prev_object(ev)
+            prev_ok = self.flt.matches(prev_obj)
+        if ev.type == DELETE:
+            return (m.DELETED, obj, ev) if prev_ok else None
+        if cur_ok and prev_ok:
+            return m.MODIFIED, obj, ev
+        if cur_ok:
+            return m.ADDED, obj, ev
+        if prev_ok:
+            return m.DELETED, obj, ev
+        return None
+
+    async def next(self, timeout: float | None = None):
+        """(type, obj, raw_event) or None when closed / timed out."""
+        loop = asyncio.get_running_loop()
+        deadline = None if timeout is None else loop.time() + timeout
+        while True:
+            rem = None if deadline is None else max(0.0, deadline - loop.time())
+            ev = await self.w.next(rem)
+            if ev is None:
+                return None
+            t = self._translate(ev)
+            if t is not None:
+                return t
+            if deadline is not None and loop.time() >= deadline:
+                return None
+
+    def __aiter__(self):
+        return self
+
+    async def __anext__(self):
+        r = await self.next()
+        if r is None:
+            raise StopAsyncIteration
+        return r

@@ -1,0 +1,24 @@
+import asyncio
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (run via gpurun)")
+    config.addinivalue_line("markers", "slow: long-running test")
+
+
+def run(coro, timeout=60):
+    """Run a coroutine to completion on a fresh event loop (no pytest-asyncio here)."""
+    return asyncio.run(asyncio.wait_for(coro, timeout))
+
+
+@pytest.fixture
+def arun():
+    return run
