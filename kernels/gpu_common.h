@@ -1,0 +1,378 @@
+// amdkube GPU validation workloads for MI355X (gfx950 / CDNA4).
+//
+// The reference's only GPU workload is the CUDA-samples vectorAdd image its e2e tests run
+// in GPU pods (test/images/cuda-vector-add/Dockerfile:15-26; 50,000 fp32 elements), plus
+// device health that comes solely from the plugin (api.proto:97). amdkube replaces that
+// with three CDNA4-native kernels shared by the standalone pod binaries (rocm-vector-add,
+// hbm-probe, gpu-burn) and the in-process Python extension (_hipops):
+//
+//   vector add   wave64 grid-stride, 16-B (float4) loads, grid sized to the chip
+//   HBM probe    address-hashed write / verify / read / copy over buffers larger than
+//                the 256 MiB Infinity Cache, 16 B per lane, 4-deep unrolled so every CU
+//                keeps ~32 KiB in flight — the pattern MI355X_MICROARCH measures at
+//                ~6.3 TB/s; verify counts mismatches (ECC-sensitive health check)
+//   MFMA burn    register-resident v_mfma_f32_32x32x16_bf16 chains, 2 independent
+//                accumulators per wave, for matrix-core load / utilisation validation
+//
+// Every launch is bounded by construction (grid-stride loops over checked sizes) and uses
+// no inter-workgroup synchronisation, so no launch can hang the device.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace amdkube {
+
+#define AK_HIP(call)                                                                       \
+  do {                                                                                     \
+    hipError_t e_ = (call);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      throw std::runtime_error(std::string(#call) + ": " + hipGetErrorString(e_));         \
+  } while (0)
+
+struct DevInfo {
+  std::string name, arch, pci_bus_id, uuid;
+  size_t total_mem = 0;
+  int cu_count = 0;
+  int device = 0;
+};
+
+inline std::string uuid_string(const hipUUID& u) {
+  // HIP reports the 16 raw bytes; AMD exposes them as the ASCII unique id, print both forms
+  bool printable = true;
+  for (int i = 0; i < 16; ++i) {
+    unsigned char c = static_cast<unsigned char>(u.bytes[i]);
+    if (c != 0 && (c < 0x20 || c > 0x7e)) printable = false;
+  }
+  if (printable) {
+    std::string s(u.bytes, u.bytes + 16);
+    s = s.c_str();
+    if (!s.empty()) return "GPU-" + s;
+  }
+  char buf[40];
+  for (int i = 0; i < 16; ++i) std::snprintf(buf + 2 * i, 3, "%02x", static_cast<unsigned char>(u.bytes[i]));
+  return std::string("GPU-") + buf;
+}
+
+inline DevInfo dev_info(int dev) {
+  DevInfo d;
+  d.device = dev;
+  hipDeviceProp_t p;
+  AK_HIP(hipGetDeviceProperties(&p, dev));
+  d.name = p.name;
+  d.arch = p.gcnArchName;
+  d.total_mem = p.totalGlobalMem;
+  d.cu_count = p.multiProcessorCount;
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) == hipSuccess) d.pci_bus_id = bus;
+  hipUUID u;
+  if (hipDeviceGetUuid(&u, dev) == hipSuccess) d.uuid = uuid_string(u);
+  return d;
+}
+
+// ---------------------------------------------------------------------------- kernels
+__global__ __launch_bounds__(256) void vadd_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                   float* __restrict__ c, size_t n) {
+  const size_t n4 = n >> 2;
+  const float4* a4 = reinterpret_cast<const float4*>(a);
+  const float4* b4 = reinterpret_cast<const float4*>(b);
+  float4* c4 = reinterpret_cast<float4*>(c);
+  const size_t tid = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  for (size_t i = tid; i < n4; i += stride) {
+    float4 x = a4[i], y = b4[i];
+    c4[i] = make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
+  }
+  for (size_t i = (n4 << 2) + tid; i < n; i += stride) c[i] = a[i] + b[i];
+}
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ uint4 pattern(size_t i, uint32_t seed) {
+  uint32_t base = static_cast<uint32_t>(i * 4) ^ seed ^ static_cast<uint32_t>(i >> 30);
+  return make_uint4(mix32(base), mix32(base + 1), mix32(base + 2), mix32(base + 3));
+}
+
+constexpr int HBM_UNROLL = 4;
+
+__global__ __launch_bounds__(256) void hbm_write_kernel(uint4* __restrict__ buf, size_t n16, uint32_t seed) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (; i + (HBM_UNROLL - 1) * stride < n16; i += HBM_UNROLL * stride) {
+#pragma unroll
+    for (int u = 0; u < HBM_UNROLL; ++u) buf[i + u * stride] = pattern(i + u * stride, seed);
+  }
+  for (; i < n16; i += stride) buf[i] = pattern(i, seed);
+}
+
+__global__ __launch_bounds__(256) void hbm_verify_kernel(const uint4* __restrict__ buf, size_t n16, uint32_t seed,
+                                                         unsigned long long* __restrict__ errors) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  unsigned long long bad = 0;
+  size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (; i + (HBM_UNROLL - 1) * stride < n16; i += HBM_UNROLL * stride) {
+    uint4 v[HBM_UNROLL];
+#pragma unroll
+    for (int u = 0; u < HBM_UNROLL; ++u) v[u] = buf[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < HBM_UNROLL; ++u) {
+      uint4 e = pattern(i + u * stride, seed);
+      bad += (v[u].x != e.x) + (v[u].y != e.y) + (v[u].z != e.z) + (v[u].w != e.w);
+    }
+  }
+  for (; i < n16; i += stride) {
+    uint4 v = buf[i], e = pattern(i, seed);
+    bad += (v.x != e.x) + (v.y != e.y) + (v.z != e.z) + (v.w != e.w);
+  }
+  if (bad) atomicAdd(errors, bad);  // errors are rare: no contention on a healthy part
+}
+
+__global__ __launch_bounds__(256) void hbm_read_kernel(const uint4* __restrict__ buf, size_t n16, uint32_t* sink) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  uint32_t acc = 0;
+  size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (; i + (HBM_UNROLL - 1) * stride < n16; i += HBM_UNROLL * stride) {
+    uint4 v[HBM_UNROLL];
+#pragma unroll
+    for (int u = 0; u < HBM_UNROLL; ++u) v[u] = buf[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < HBM_UNROLL; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  for (; i < n16; i += stride) {
+    uint4 v = buf[i];
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x9e3779b9u) sink[0] = acc;  // keeps the loads live
+}
+
+__global__ __launch_bounds__(256) void hbm_copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                       size_t n16) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (; i + (HBM_UNROLL - 1) * stride < n16; i += HBM_UNROLL * stride) {
+    uint4 v[HBM_UNROLL];
+#pragma unroll
+    for (int u = 0; u < HBM_UNROLL; ++u) v[u] = src[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < HBM_UNROLL; ++u) dst[i + u * stride] = v[u];
+  }
+  for (; i < n16; i += stride) dst[i] = src[i];
+}
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// 2 independent 32x32x16 bf16 MFMA accumulator chains per wave, operands in registers.
+__global__ __launch_bounds__(256) void mfma_burn_kernel(float* __restrict__ out, int iters) {
+  bf16x8 a, b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a[j] = static_cast<__bf16>(1.0f / (1 + ((threadIdx.x + j) & 7)));
+    b[j] = static_cast<__bf16>(0.001f * (j + 1));
+  }
+  f32x16 c0 = {}, c1 = {};
+  for (int it = 0; it < iters; ++it) {
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, a, c1, 0, 0, 0);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) s += c0[j] + c1[j];
+  out[static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x] = s;
+}
+
+// ---------------------------------------------------------------------------- runners
+inline int stream_grid(size_t items, int cu_count, int per_cu = 8) {
+  size_t want = (items + 255) / 256;
+  size_t cap = static_cast<size_t>(cu_count > 0 ? cu_count : 256) * per_cu;
+  if (want < 1) want = 1;
+  return static_cast<int>(want < cap ? want : cap);
+}
+
+struct VaddResult {
+  bool ok = false;
+  double kernel_ms = 0;
+  size_t mismatches = 0;
+};
+
+inline VaddResult run_vector_add(size_t n, int dev) {
+  VaddResult r;
+  if (n == 0) throw std::invalid_argument("n must be > 0");
+  AK_HIP(hipSetDevice(dev));
+  DevInfo info = dev_info(dev);
+  std::vector<float> ha(n), hb(n), hc(n);
+  uint32_t s = 12345u;
+  for (size_t i = 0; i < n; ++i) {
+    s = s * 1664525u + 1013904223u;
+    ha[i] = static_cast<float>(s >> 8) / 16777216.0f;
+    s = s * 1664525u + 1013904223u;
+    hb[i] = static_cast<float>(s >> 8) / 16777216.0f;
+  }
+  float *da = nullptr, *db = nullptr, *dc = nullptr;
+  const size_t bytes = n * sizeof(float);
+  AK_HIP(hipMalloc(&da, bytes));
+  AK_HIP(hipMalloc(&db, bytes));
+  AK_HIP(hipMalloc(&dc, bytes));
+  try {
+    AK_HIP(hipMemcpy(da, ha.data(), bytes, hipMemcpyHostToDevice));
+    AK_HIP(hipMemcpy(db, hb.data(), bytes, hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    AK_HIP(hipEventCreate(&e0));
+    AK_HIP(hipEventCreate(&e1));
+    int grid = stream_grid((n + 3) / 4, info.cu_count);
+    AK_HIP(hipEventRecord(e0));
+    hipLaunchKernelGGL(vadd_kernel, dim3(grid), dim3(256), 0, 0, da, db, dc, n);
+    AK_HIP(hipGetLastError());
+    AK_HIP(hipEventRecord(e1));
+    AK_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    AK_HIP(hipEventElapsedTime(&ms, e0, e1));
+    r.kernel_ms = ms;
+    AK_HIP(hipMemcpy(hc.data(), dc, bytes, hipMemcpyDeviceToHost));
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+  } catch (...) {
+    hipFree(da);
+    hipFree(db);
+    hipFree(dc);
+    throw;
+  }
+  hipFree(da);
+  hipFree(db);
+  hipFree(dc);
+  for (size_t i = 0; i < n; ++i) {
+    float d = hc[i] - (ha[i] + hb[i]);
+    if (d > 1e-5f || d < -1e-5f) ++r.mismatches;
+  }
+  r.ok = r.mismatches == 0;
+  return r;
+}
+
+struct HbmResult {
+  double write_gbps = 0, read_gbps = 0, copy_gbps = 0, verify_gbps = 0;
+  unsigned long long errors = 0;
+  size_t bytes = 0;
+  int iters = 0;
+};
+
+inline HbmResult run_hbm_probe(size_t bytes, int iters, int dev, uint32_t seed = 0x5eedu) {
+  HbmResult r;
+  if (iters < 1) iters = 1;
+  bytes &= ~static_cast<size_t>(15);
+  if (bytes < (1u << 20)) throw std::invalid_argument("hbm probe needs at least 1 MiB");
+  AK_HIP(hipSetDevice(dev));
+  DevInfo info = dev_info(dev);
+  const size_t n16 = bytes / 16;
+  uint4 *a = nullptr, *b = nullptr;
+  unsigned long long* errs = nullptr;
+  uint32_t* sink = nullptr;
+  AK_HIP(hipMalloc(&a, bytes));
+  if (hipMalloc(&b, bytes) != hipSuccess) {
+    hipFree(a);
+    throw std::runtime_error("hipMalloc failed for hbm probe buffer");
+  }
+  AK_HIP(hipMalloc(&errs, sizeof(unsigned long long)));
+  AK_HIP(hipMalloc(&sink, sizeof(uint32_t)));
+  AK_HIP(hipMemset(errs, 0, sizeof(unsigned long long)));
+  hipEvent_t e0, e1;
+  AK_HIP(hipEventCreate(&e0));
+  AK_HIP(hipEventCreate(&e1));
+  const int grid = stream_grid(n16, info.cu_count, 8);
+  auto timed = [&](auto&& launch) {
+    launch();  // warm-up (page-in / first-touch)
+    AK_HIP(hipGetLastError());
+    AK_HIP(hipEventRecord(e0));
+    for (int it = 0; it < iters; ++it) launch();
+    AK_HIP(hipEventRecord(e1));
+    AK_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    AK_HIP(hipEventElapsedTime(&ms, e0, e1));
+    return static_cast<double>(ms) / iters;
+  };
+  double w = timed([&] { hipLaunchKernelGGL(hbm_write_kernel, dim3(grid), dim3(256), 0, 0, a, n16, seed); });
+  double rd = timed([&] { hipLaunchKernelGGL(hbm_read_kernel, dim3(grid), dim3(256), 0, 0, a, n16, sink); });
+  double cp = timed([&] { hipLaunchKernelGGL(hbm_copy_kernel, dim3(grid), dim3(256), 0, 0, a, b, n16); });
+  AK_HIP(hipMemset(errs, 0, sizeof(unsigned long long)));
+  AK_HIP(hipEventRecord(e0));
+  hipLaunchKernelGGL(hbm_verify_kernel, dim3(grid), dim3(256), 0, 0, b, n16, seed, errs);
+  AK_HIP(hipGetLastError());
+  AK_HIP(hipEventRecord(e1));
+  AK_HIP(hipEventSynchronize(e1));
+  float vms = 0;
+  AK_HIP(hipEventElapsedTime(&vms, e0, e1));
+  AK_HIP(hipMemcpy(&r.errors, errs, sizeof(r.errors), hipMemcpyDeviceToHost));
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipFree(a);
+  hipFree(b);
+  hipFree(errs);
+  hipFree(sink);
+  r.bytes = bytes;
+  r.iters = iters;
+  r.write_gbps = bytes / (w * 1e6);
+  r.read_gbps = bytes / (rd * 1e6);
+  r.copy_gbps = 2.0 * bytes / (cp * 1e6);
+  r.verify_gbps = bytes / (vms * 1e6);
+  return r;
+}
+
+struct BurnResult {
+  double ms = 0, tflops = 0;
+  long long iters = 0;
+  int blocks = 0;
+};
+
+inline BurnResult run_mfma_burn(double target_ms, int dev) {
+  BurnResult r;
+  AK_HIP(hipSetDevice(dev));
+  DevInfo info = dev_info(dev);
+  const int blocks = (info.cu_count > 0 ? info.cu_count : 256) * 4;  // 16 waves / CU
+  float* out = nullptr;
+  AK_HIP(hipMalloc(&out, static_cast<size_t>(blocks) * 256 * sizeof(float)));
+  hipEvent_t e0, e1;
+  AK_HIP(hipEventCreate(&e0));
+  AK_HIP(hipEventCreate(&e1));
+  auto run = [&](int iters) {
+    AK_HIP(hipEventRecord(e0));
+    hipLaunchKernelGGL(mfma_burn_kernel, dim3(blocks), dim3(256), 0, 0, out, iters);
+    AK_HIP(hipGetLastError());
+    AK_HIP(hipEventRecord(e1));
+    AK_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    AK_HIP(hipEventElapsedTime(&ms, e0, e1));
+    return static_cast<double>(ms);
+  };
+  int iters = 2000;
+  double ms = run(iters);
+  if (target_ms > ms && ms > 0) {
+    double scale = target_ms / ms;
+    double want = iters * scale;
+    iters = want > 2.0e9 ? 2000000000 : static_cast<int>(want);
+    ms = run(iters);
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipFree(out);
+  const double flops = static_cast<double>(blocks) * 4 /*waves*/ * iters * 2 /*chains*/ * (2.0 * 32 * 32 * 16);
+  r.ms = ms;
+  r.iters = iters;
+  r.blocks = blocks;
+  r.tflops = flops / (ms * 1e9);
+  return r;
+}
+
+}  // namespace amdkube

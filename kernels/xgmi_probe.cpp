@@ -1,0 +1,123 @@
+// xgmi-probe: RCCL-over-xGMI validation of the GPU set a pod was given.
+//
+// The reference has no collective or interconnect awareness at all. For
+// topology-aware placement amdkube needs ground truth: this probe runs, over every GPU
+// visible to the pod (one process, one communicator via ncclCommInitAll), an all-reduce
+// bus-bandwidth sweep and a pairwise hipMemcpyPeer matrix. On an 8x MI355X node every GPU
+// pair has one direct xGMI link (7 links x ~153 GB/s per GPU), so a ring all-reduce over k
+// GPUs is per-link bound; the probe reports algbw and busbw = algbw * 2(k-1)/k.
+//   xgmi-probe [--max-mib M] [--iters K] [--no-p2p]
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#define CHECK_HIP(x)                                                                          \
+  do {                                                                                        \
+    hipError_t e = (x);                                                                       \
+    if (e != hipSuccess) throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e)); \
+  } while (0)
+#define CHECK_NCCL(x)                                                                             \
+  do {                                                                                            \
+    ncclResult_t r = (x);                                                                         \
+    if (r != ncclSuccess) throw std::runtime_error(std::string(#x) + ": " + ncclGetErrorString(r)); \
+  } while (0)
+
+int main(int argc, char** argv) {
+  size_t max_mib = 256;
+  int iters = 10;
+  bool p2p = true;
+  for (int i = 1; i < argc; ++i) {
+    if (!std::strcmp(argv[i], "--max-mib") && i + 1 < argc) max_mib = std::strtoull(argv[++i], nullptr, 10);
+    else if (!std::strcmp(argv[i], "--iters") && i + 1 < argc) iters = std::atoi(argv[++i]);
+    else if (!std::strcmp(argv[i], "--no-p2p")) p2p = false;
+  }
+  try {
+    int n = 0;
+    CHECK_HIP(hipGetDeviceCount(&n));
+    if (n < 1) throw std::runtime_error("no GPUs visible");
+    std::printf("{\"gpus\":%d,\"allreduce\":[", n);
+    std::vector<ncclComm_t> comms(n);
+    std::vector<int> devs(n);
+    for (int i = 0; i < n; ++i) devs[i] = i;
+    CHECK_NCCL(ncclCommInitAll(comms.data(), n, devs.data()));
+    std::vector<float*> buf(n);
+    std::vector<hipStream_t> st(n);
+    const size_t max_bytes = max_mib << 20;
+    for (int i = 0; i < n; ++i) {
+      CHECK_HIP(hipSetDevice(i));
+      CHECK_HIP(hipMalloc(&buf[i], max_bytes));
+      CHECK_HIP(hipMemset(buf[i], 0, max_bytes));
+      CHECK_HIP(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
+    }
+    bool first = true;
+    for (size_t bytes = 1 << 20; bytes <= max_bytes; bytes <<= 2) {
+      size_t count = bytes / sizeof(float);
+      auto run = [&]() {
+        CHECK_NCCL(ncclGroupStart());
+        for (int i = 0; i < n; ++i) CHECK_NCCL(ncclAllReduce(buf[i], buf[i], count, ncclFloat, ncclSum, comms[i], st[i]));
+        CHECK_NCCL(ncclGroupEnd());
+      };
+      run();
+      for (int i = 0; i < n; ++i) {
+        CHECK_HIP(hipSetDevice(i));
+        CHECK_HIP(hipStreamSynchronize(st[i]));
+      }
+      auto t0 = std::chrono::steady_clock::now();
+      for (int it = 0; it < iters; ++it) run();
+      for (int i = 0; i < n; ++i) {
+        CHECK_HIP(hipSetDevice(i));
+        CHECK_HIP(hipStreamSynchronize(st[i]));
+      }
+      double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / iters;
+      double alg = bytes / s / 1e9;
+      double bus = n > 1 ? alg * 2.0 * (n - 1) / n : alg;
+      std::printf("%s{\"bytes\":%zu,\"us\":%.1f,\"algbw_gbps\":%.2f,\"busbw_gbps\":%.2f}", first ? "" : ",", bytes, s * 1e6,
+                  alg, bus);
+      first = false;
+    }
+    std::printf("],\"p2p_gbps\":[");
+    for (int i = 0; i < n; ++i) {
+      std::printf("%s[", i ? "," : "");
+      for (int j = 0; j < n; ++j) {
+        double gbps = 0;
+        if (p2p && i != j) {
+          int can = 0;
+          CHECK_HIP(hipDeviceCanAccessPeer(&can, i, j));
+          if (can) {
+            CHECK_HIP(hipSetDevice(i));
+            hipDeviceEnablePeerAccess(j, 0);
+            (void)hipGetLastError();
+            size_t bytes = max_bytes;
+            CHECK_HIP(hipMemcpyPeer(buf[j], j, buf[i], i, bytes));
+            CHECK_HIP(hipDeviceSynchronize());
+            auto t0 = std::chrono::steady_clock::now();
+            for (int it = 0; it < 3; ++it) CHECK_HIP(hipMemcpyPeer(buf[j], j, buf[i], i, bytes));
+            CHECK_HIP(hipDeviceSynchronize());
+            double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / 3;
+            gbps = bytes / s / 1e9;
+          }
+        }
+        std::printf("%s%.1f", j ? "," : "", gbps);
+      }
+      std::printf("]");
+    }
+    std::printf("]}\n");
+    for (int i = 0; i < n; ++i) {
+      ncclCommDestroy(comms[i]);
+      hipSetDevice(i);
+      hipFree(buf[i]);
+      hipStreamDestroy(st[i]);
+    }
+    return 0;
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "xgmi-probe: %s\n", e.what());
+    return 4;
+  }
+}

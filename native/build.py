@@ -1,0 +1,122 @@
+"""Build every native artefact in-tree (so it travels to the GPU box with the snapshot).
+
+  python native/build.py            # CPU-side pybind modules + pause (g++), HIP targets (hipcc, gfx950)
+  python native/build.py --cpu-only # just the g++ targets (used by the CPU test tier)
+  python native/build.py --sanitize # also the ASan/UBSan host builds (pause, topo self-test)
+
+Outputs: amdkube/_native/{_amdsmi,_topo,_hipops}.<ext> and amdkube/_native/bin/{pause,
+rocm-vector-add,hbm-probe,gpu-burn,xgmi-probe[,topo-selftest-asan,pause-asan]}.
+Targets are rebuilt only when a source/header is newer than the output.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "amdkube", "_native")
+BIN = os.path.join(OUT, "bin")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def _py_includes():
+    import pybind11
+    return [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
+
+
+def _hipcc():
+    p = os.path.join(ROCM, "bin", "hipcc")
+    return p if os.path.exists(p) else shutil.which("hipcc")
+
+
+def targets(sanitize=False, cpu_only=False):
+    py = _py_includes()
+    rocm_inc = [f"-I{ROCM}/include"]
+    rpath = [f"-L{ROCM}/lib", f"-Wl,-rpath,{ROCM}/lib"]
+    n = lambda *p: os.path.join(ROOT, *p)  # noqa: E731
+    t = [
+        (n(OUT, "_topo" + EXT), [n("native/topo_alloc.cpp"), n("native/topo_core.h")],
+         ["g++", "-O3", "-std=c++17", "-shared", "-fPIC", *py, n("native/topo_alloc.cpp"), "-o", "{out}"]),
+        (n(OUT, "_amdsmi" + EXT), [n("native/amdsmi_shim.cpp")],
+         ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", *py, *rocm_inc, n("native/amdsmi_shim.cpp"), *rpath,
+          "-lamd_smi", "-o", "{out}"]),
+        (n(BIN, "pause"), [n("native/pause.cpp")],
+         ["g++", "-O2", "-std=c++17", n("native/pause.cpp"), "-o", "{out}"]),
+    ]
+    if sanitize:
+        san = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-g"]
+        t += [
+            (n(BIN, "topo-selftest-asan"), [n("native/topo_selftest.cpp"), n("native/topo_core.h")],
+             ["g++", "-O1", "-std=c++17", *san, n("native/topo_selftest.cpp"), "-o", "{out}"]),
+            (n(BIN, "pause-asan"), [n("native/pause.cpp")],
+             ["g++", "-O1", "-std=c++17", *san, n("native/pause.cpp"), "-o", "{out}"]),
+        ]
+    if not cpu_only:
+        hip = _hipcc()
+        if hip is None:
+            raise SystemExit("hipcc not found: cannot build gfx950 targets")
+        ho = [hip, f"--offload-arch={ARCH}", "-O3", "-std=c++17"]
+        hdr = n("kernels/gpu_common.h")
+        t += [
+            (n(OUT, "_hipops" + EXT), [n("native/hipops.hip"), hdr],
+             [*ho, "-shared", "-fPIC", *py, n("native/hipops.hip"), "-o", "{out}"]),
+            (n(BIN, "rocm-vector-add"), [n("kernels/vector_add.hip"), hdr], [*ho, n("kernels/vector_add.hip"), "-o", "{out}"]),
+            (n(BIN, "hbm-probe"), [n("kernels/hbm_probe.hip"), hdr], [*ho, n("kernels/hbm_probe.hip"), "-o", "{out}"]),
+            (n(BIN, "gpu-burn"), [n("kernels/gpu_burn.hip"), hdr], [*ho, n("kernels/gpu_burn.hip"), "-o", "{out}"]),
+            (n(BIN, "xgmi-probe"), [n("kernels/xgmi_probe.cpp")],
+             [*ho, "-x", "hip", n("kernels/xgmi_probe.cpp"), *rocm_inc, *rpath, "-lrccl", "-o", "{out}"]),
+        ]
+    return t
+
+
+def stale(out, deps):
+    if not os.path.exists(out):
+        return True
+    mt = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > mt for d in deps)
+
+
+def build(sanitize=False, cpu_only=False, force=False, jobs=4, verbose=False):
+    os.makedirs(BIN, exist_ok=True)
+    init = os.path.join(OUT, "__init__.py")
+    if not os.path.exists(init):
+        open(init, "w").write('"""Built native artefacts (see native/build.py)."""\n')
+    todo = [(o, d, c) for o, d, c in targets(sanitize, cpu_only) if force or stale(o, d)]
+
+    def one(item):
+        out, _, cmd = item
+        cmd = [c.replace("{out}", out + ".tmp") for c in cmd]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"build of {os.path.basename(out)} failed:\n{r.stderr[-4000:]}")
+        os.replace(out + ".tmp", out)
+        return os.path.basename(out)
+
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        built = list(ex.map(one, todo))
+    return built
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sanitize", action="store_true")
+    ap.add_argument("--cpu-only", action="store_true")
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", type=int, default=4)
+    ap.add_argument("-v", action="store_true")
+    a = ap.parse_args()
+    built = build(a.sanitize, a.cpu_only, a.force, a.j, a.v)
+    print("built:", ", ".join(built) if built else "(up to date)")
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,193 @@
+// xGMI/NUMA topology-aware GPU subset allocator (core, shared by the pybind11 module _topo and the sanitizer self-test).
+//
+// The reference scheduler picks devices by iterating a Go map and taking the first N that
+// match the attribute selector (plugin/pkg/scheduler/core/extended_resources.go:126-142):
+// random order, no topology. Here the candidate set (free, healthy, selector-matching
+// devices of one node) is scored exhaustively when C(n,k) is small — always true on an
+// 8-GPU MI355X node (C(8,4) = 70) — and greedily otherwise, minimising
+//
+//   cost(S) = W_NUMA * (numa nodes spanned by S - minimum possible)
+//           + W_LINK * mean pairwise link cost inside S        (xGMI hops / weights)
+//           + W_FRAG * fragmentation of the devices left free   (best fit)
+//
+// Fragmentation keeps the remaining free GPUs concentrated in as few NUMA groups / aligned
+// pairs as possible, so that after a 4-GPU gang lands on one socket the other socket is
+// still whole for the next 4-GPU gang. Ties break on the
+// lexicographically smallest index set, so placement is deterministic. The Python
+// fallback in amdkube/ops/topology.py implements the identical function.
+#pragma once
+
+#include <algorithm>
+#include <cmath>
+#include <limits>
+#include <map>
+#include <set>
+#include <stdexcept>
+#include <tuple>
+#include <vector>
+
+
+namespace topo {
+
+constexpr double W_NUMA = 100.0;
+constexpr double W_LINK = 10.0;
+constexpr double W_FRAG = 1.0;
+constexpr long long MAX_ENUM = 200000;
+
+struct Problem {
+  std::vector<int> free;                 // candidate device indices (node-local)
+  std::vector<std::vector<double>> link; // normalised link cost in [0,1], indexed by device index
+  std::vector<int> numa;                 // numa group per device index
+  std::vector<int> all_free;             // every free device on the node (for fragmentation)
+  int k;
+};
+
+inline long long n_choose_k(int n, int k) {
+  if (k < 0 || k > n) return 0;
+  long long r = 1;
+  for (int i = 1; i <= k; ++i) {
+    r = r * (n - k + i) / i;
+    if (r > MAX_ENUM * 10) return r;
+  }
+  return r;
+}
+
+inline int min_groups_needed(const Problem& p) {
+  std::map<int, int> cnt;
+  for (int d : p.free) cnt[p.numa[d]]++;
+  std::vector<int> c;
+  for (auto& kv : cnt) c.push_back(kv.second);
+  std::sort(c.rbegin(), c.rend());
+  int need = p.k, g = 0;
+  for (int x : c) {
+    if (need <= 0) break;
+    need -= x;
+    ++g;
+  }
+  return std::max(g, p.k > 0 ? 1 : 0);
+}
+
+inline double fragmentation(const Problem& p, const std::vector<int>& chosen) {
+  // remaining free devices after taking `chosen`; quality = sum_g c_g^2 + sum_pairs both-free
+  std::set<int> taken(chosen.begin(), chosen.end());
+  std::map<int, int> per_group;
+  std::set<int> rem;
+  for (int d : p.all_free)
+    if (!taken.count(d)) {
+      per_group[p.numa[d]]++;
+      rem.insert(d);
+    }
+  int total = static_cast<int>(rem.size());
+  if (total == 0) return 0.0;
+  double q = 0.0;
+  for (auto& kv : per_group) q += static_cast<double>(kv.second) * kv.second;
+  double pairs = 0.0;
+  for (int d : rem)
+    if ((d % 2) == 0 && rem.count(d + 1) && p.numa[d] == p.numa[d + 1]) pairs += 1.0;
+  double best_q = static_cast<double>(total) * total;  // everything in one group
+  double frag_groups = 1.0 - q / best_q;
+  double frag_pairs = 1.0 - (2.0 * pairs) / total;
+  return 0.75 * frag_groups + 0.25 * std::max(0.0, frag_pairs);
+}
+
+inline double cost(const Problem& p, const std::vector<int>& s, int min_groups) {
+  std::set<int> groups;
+  for (int d : s) groups.insert(p.numa[d]);
+  double link = 0.0;
+  int pairs = 0;
+  for (size_t a = 0; a < s.size(); ++a)
+    for (size_t b = a + 1; b < s.size(); ++b) {
+      link += p.link[s[a]][s[b]];
+      ++pairs;
+    }
+  double mean_link = pairs ? link / pairs : 0.0;
+  return W_NUMA * (static_cast<double>(groups.size()) - min_groups) + W_LINK * mean_link +
+         W_FRAG * fragmentation(p, s);
+}
+
+inline std::tuple<std::vector<int>, double> solve(const Problem& p) {
+  int n = static_cast<int>(p.free.size());
+  if (p.k <= 0) return std::make_tuple(std::vector<int>{}, 0.0);
+  if (p.k > n) return std::make_tuple(std::vector<int>{}, std::numeric_limits<double>::infinity());
+  int mg = min_groups_needed(p);
+  std::vector<int> best;
+  double best_cost = std::numeric_limits<double>::infinity();
+  std::vector<int> sorted_free = p.free;
+  std::sort(sorted_free.begin(), sorted_free.end());
+  if (n_choose_k(n, p.k) <= MAX_ENUM) {
+    std::vector<int> idx(p.k);
+    for (int i = 0; i < p.k; ++i) idx[i] = i;
+    std::vector<int> s(p.k);
+    while (true) {
+      for (int i = 0; i < p.k; ++i) s[i] = sorted_free[idx[i]];
+      double c = cost(p, s, mg);
+      if (c < best_cost - 1e-12) {
+        best_cost = c;
+        best = s;
+      }
+      int i = p.k - 1;
+      while (i >= 0 && idx[i] == n - p.k + i) --i;
+      if (i < 0) break;
+      ++idx[i];
+      for (int j = i + 1; j < p.k; ++j) idx[j] = idx[j - 1] + 1;
+    }
+    return std::make_tuple(best, best_cost);
+  }
+  // greedy: grow from every seed, keep the cheapest
+  for (int seed : sorted_free) {
+    std::vector<int> s{seed};
+    std::set<int> used{seed};
+    while (static_cast<int>(s.size()) < p.k) {
+      int pick = -1;
+      double pc = std::numeric_limits<double>::infinity();
+      for (int d : sorted_free) {
+        if (used.count(d)) continue;
+        s.push_back(d);
+        double c = cost(p, s, mg);
+        s.pop_back();
+        if (c < pc - 1e-12) {
+          pc = c;
+          pick = d;
+        }
+      }
+      s.push_back(pick);
+      used.insert(pick);
+    }
+    std::sort(s.begin(), s.end());
+    double c = cost(p, s, mg);
+    if (c < best_cost - 1e-12) {
+      best_cost = c;
+      best = s;
+    }
+  }
+  return std::make_tuple(best, best_cost);
+}
+
+inline Problem make(const std::vector<int>& free, int k, const std::vector<std::vector<double>>& link,
+             const std::vector<int>& numa, const std::vector<int>& all_free) {
+  Problem p;
+  p.free = free;
+  p.k = k;
+  p.numa = numa;
+  p.all_free = all_free.empty() ? free : all_free;
+  size_t n = numa.size();
+  if (link.size() != n) throw std::invalid_argument("link matrix must be N x N with N == len(numa)");
+  double mx = 0.0;
+  for (auto& r : link) {
+    if (r.size() != n) throw std::invalid_argument("link matrix must be square");
+    for (double v : r) mx = std::max(mx, v);
+  }
+  p.link.assign(n, std::vector<double>(n, 0.0));
+  for (size_t i = 0; i < n; ++i)
+    for (size_t j = 0; j < n; ++j) p.link[i][j] = mx > 0 ? link[i][j] / mx : 0.0;
+  for (int d : p.free)
+    if (d < 0 || static_cast<size_t>(d) >= n) throw std::out_of_range("device index out of range");
+  for (int d : p.all_free)
+    if (d < 0 || static_cast<size_t>(d) >= n) throw std::out_of_range("device index out of range");
+  return p;
+}
+
+inline double max_cost(int n_groups) { return W_NUMA * std::max(0, n_groups - 1) + W_LINK + W_FRAG; }
+
+}  // namespace topo
+
