@@ -1,0 +1,192 @@
+"""The AMD Instinct (MI355X) device plugin: advertises `amd.com/gpu` with device attributes,
+tracks health from amd-smi RAS/ECC counters (plus an optional on-device HBM pattern probe),
+and injects /dev/kfd + the GPU's DRM render node into containers.
+
+Replaces the out-of-tree NVIDIA plugin the reference's DaemonSet deploys
+(cluster/addons/device-plugins/nvidia-gpu/daemonset.yaml) and the legacy in-kubelet NVIDIA
+path (pkg/kubelet/gpu/nvidia/nvidia_gpu_manager.go: /dev/nvidia* + nvidiactl + nvidia-uvm).
+
+Published per-device Attributes (matchable by PodSpec extendedResources[].affinity.required,
+SURVEY Appendix A.3; keys are single-slash qualified names, values label-safe — quirk #13):
+  amd.com/gpu-type      MI355X            amd.com/gpu-memory  294896 (MiB, integer → Gt/Lt)
+  amd.com/gfx           gfx950            amd.com/cu-count    256
+  amd.com/numa-node     0                 amd.com/xgmi-hive   42a9…  (hex)
+  amd.com/partition     SPX               amd.com/memory-partition NPS1
+  amd.com/index         node-local index  amd.com/pci-bus     0000-23-00.0
+Plugin labels (GetPluginInfoResponse.labels, field 2 of the fork's wire format) carry the
+node's GPU link matrix as `amd.com/gpu-topology` JSON, which the kubelet copies into a node
+annotation for the scheduler's xGMI/NUMA scorer.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import os
+import subprocess
+
+from ..grpcdesc.deviceplugin import DEVICE_PLUGINS_PATH, HEALTHY, UNHEALTHY
+from ..smi import Backend, device_id, visibility_token
+from .server import DevicePluginServer
+
+log = logging.getLogger("amdkube.deviceplugin.amd")
+
+RESOURCE = "amd.com/gpu"
+TOPOLOGY_LABEL = "amd.com/gpu-topology"
+RUNTIME_ANNOTATION = "io.amdkube.runtime"
+BIN_DIR = os.path.join(os.path.dirname(os.path.dirname(__file__)), "_native", "bin")
+
+
+def gpu_type(g: dict) -> str:
+    name = (g.get("market_name") or g.get("product_name") or "").replace("AMD Instinct", "").strip()
+    for known in ("MI355", "MI350", "MI325", "MI308", "MI300"):
+        if known in name:
+            return known + "X" if not name.startswith(known + "A") else known + "A"
+    tok = name.split()[0] if name else (g.get("gfx_target") or "unknown")
+    return "".join(ch for ch in tok if ch.isalnum() or ch in "-_.") or "unknown"
+
+
+def attributes(g: dict) -> dict:
+    a = {"amd.com/gpu-type": gpu_type(g), "amd.com/index": str(g.get("index", 0))}
+    if g.get("vram_total_bytes"):
+        a["amd.com/gpu-memory"] = str(int(g["vram_total_bytes"]) >> 20)
+    if g.get("gfx_target"):
+        a["amd.com/gfx"] = g["gfx_target"]
+    if g.get("num_cu"):
+        a["amd.com/cu-count"] = str(g["num_cu"])
+    if g.get("numa_node") is not None:
+        a["amd.com/numa-node"] = str(g["numa_node"])
+    if g.get("xgmi_hive_id"):
+        a["amd.com/xgmi-hive"] = f"{int(g['xgmi_hive_id']):x}"
+    if g.get("compute_partition"):
+        a["amd.com/partition"] = g["compute_partition"]
+    if g.get("memory_partition"):
+        a["amd.com/memory-partition"] = g["memory_partition"]
+    if g.get("bdf"):
+        a["amd.com/pci-bus"] = g["bdf"].replace(":", "-")
+    return a
+
+
+def topology_label(gpus: list[dict], topo: list[list[dict]]) -> str:
+    ids = [device_id(g) for g in gpus]
+    link = []
+    for i, row in enumerate(topo):
+        r = []
+        for j, e in enumerate(row):
+            if i == j:
+                r.append(0)
+                continue
+            w = e.get("weight")
+            if not w:
+                w = {"xgmi": 15, "pcie": 40}.get(e.get("type"), 60) * max(1, int(e.get("hops") or 1))
+            r.append(int(w))
+        link.append(r)
+    return json.dumps({"ids": ids, "numa": [int(g.get("numa_node") or 0) for g in gpus], "link": link,
+                       "type": [[(e.get("type") or "")[:4] for e in row] for row in topo]}, separators=(",", ":"))
+
+
+class AMDGPUPlugin(DevicePluginServer):
+    def __init__(self, backend: Backend, resource_name: str = RESOURCE, plugins_dir: str = DEVICE_PLUGINS_PATH,
+                 health_interval: float = 10.0, health_probe: str = "none", dev_root: str = "/dev",
+                 ecc_threshold: int = 0, expose_card: bool = True, init_timeout: int = 10):
+        super().__init__(resource_name, plugins_dir, init_timeout)
+        self.backend = backend
+        self.health_interval = health_interval
+        self.health_probe = health_probe
+        self.dev_root = dev_root
+        self.ecc_threshold = ecc_threshold
+        self.expose_card = expose_card
+        self.gpus = backend.gpus()
+        self.by_id = {device_id(g): g for g in self.gpus}
+        self.reasons: dict[str, str] = {}
+        self._task: asyncio.Task | None = None
+        try:
+            self.labels[TOPOLOGY_LABEL] = topology_label(self.gpus, backend.topology())
+        except Exception as e:  # topology is an optimisation, never a reason not to serve
+            log.warning("gpu topology unavailable: %s", e)
+        if self.gpus:
+            self.labels["amd.com/gpu.product"] = gpu_type(self.gpus[0])
+            self.labels["amd.com/gpu.count"] = str(len(self.gpus))
+        self.devices = [{"ID": device_id(g), "health": HEALTHY, "Attributes": attributes(g)} for g in self.gpus]
+
+    async def start(self):
+        if self.health_probe != "none":
+            await self._probe_all()
+        self._check_health(push=False)
+        await super().start()
+        self._task = asyncio.create_task(self._health_loop(), name="amd-gpu-health")
+        return self
+
+    async def stop(self, grace: float = 0.5):
+        if self._task:
+            self._task.cancel()
+        await super().stop(grace)
+
+    # ------------------------------------------------------------------ health
+    def _check_health(self, push=True):
+        devs = []
+        for d in self.devices:
+            g = self.by_id[d["ID"]]
+            ok, why = self.backend.health(g["index"], self.ecc_threshold)
+            if d["ID"] in self.reasons and self.reasons[d["ID"]].startswith("probe:"):
+                ok, why = False, self.reasons[d["ID"]]
+            self.reasons[d["ID"]] = "" if ok else why
+            h = HEALTHY if ok else UNHEALTHY
+            if h != d.get("health"):
+                log.warning("gpu %s is now %s %s", d["ID"], h, why)
+            devs.append(dict(d, health=h))
+        if devs != self.devices:
+            if push:
+                self.update(devs)
+            else:
+                self.devices = devs
+
+    async def _health_loop(self):
+        while True:
+            await asyncio.sleep(self.health_interval)
+            try:
+                self._check_health()
+            except Exception as e:  # keep serving; the next tick retries
+                log.error("health check failed: %s", e)
+
+    async def _probe_all(self):
+        """Run the HBM pattern probe on each GPU (subprocess → isolated HIP context)."""
+        binp = os.path.join(BIN_DIR, "hbm-probe")
+        for g in self.gpus:
+            did = device_id(g)
+            env = {k: v for k, v in os.environ.items() if k not in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")}
+            env["ROCR_VISIBLE_DEVICES"] = visibility_token(g)
+            try:
+                r = await asyncio.to_thread(subprocess.run, [binp, "--mib", "512", "--iters", "2"], env=env,
+                                            capture_output=True, text=True, timeout=60)
+                if r.returncode != 0:
+                    self.reasons[did] = f"probe: hbm-probe failed rc={r.returncode} {r.stdout.strip()[-200:]}"
+            except Exception as e:
+                self.reasons[did] = f"probe: {e}"
+
+    # ------------------------------------------------------------ allocation
+    def admit_pod(self, pod_name, containers, init_containers):
+        for ids in list(containers.values()) + list(init_containers.values()):
+            for did in ids:
+                if did not in self.by_id:
+                    raise ValueError(f"unknown device {did}")
+        all_ids = sorted({d for ids in containers.values() for d in ids} | {d for ids in init_containers.values() for d in ids})
+        return {"amd.com/gpu-devices": ",".join(all_ids)} if all_ids else {}
+
+    def init_container(self, name, device_ids):
+        gpus = [self.by_id[d] for d in device_ids if d in self.by_id]
+        if len(gpus) != len(device_ids):
+            raise ValueError(f"unknown device(s) in {device_ids}")
+        devs = [{"container_path": f"{self.dev_root}/kfd", "host_path": f"{self.dev_root}/kfd", "permissions": "rw"}]
+        for g in gpus:
+            if g.get("render_minor") is not None:
+                p = f"{self.dev_root}/dri/renderD{g['render_minor']}"
+                devs.append({"container_path": p, "host_path": p, "permissions": "rw"})
+            if self.expose_card and g.get("card_minor") is not None:
+                p = f"{self.dev_root}/dri/card{g['card_minor']}"
+                devs.append({"container_path": p, "host_path": p, "permissions": "rw"})
+        envs = {"ROCR_VISIBLE_DEVICES": ",".join(visibility_token(g) for g in gpus),
+                "AMD_GPU_DEVICE_IDS": ",".join(device_ids),
+                "AMD_GPU_COUNT": str(len(gpus))}
+        return {"envs": envs, "devices": devs, "mounts": [],
+                "annotations": {"amd.com/gpus": ",".join(device_ids), RUNTIME_ANNOTATION: "rocm"}}
