@@ -33,6 +33,7 @@ service RuntimeService {
   rpc ListContainerStats(ListContainerStatsRequest) returns (ListContainerStatsResponse) {}
   rpc UpdateRuntimeConfig(UpdateRuntimeConfigRequest) returns (UpdateRuntimeConfigResponse) {}
   rpc Status(StatusRequest) returns (StatusResponse) {}
+  rpc GetContainerEvents(GetEventsRequest) returns (stream ContainerEventResponse) {}
 }
 service ImageService {
   rpc ListImages(ListImagesRequest) returns (ListImagesResponse) {}
@@ -167,6 +168,15 @@ message ContainerAttributes { string id = 1; ContainerMetadata metadata = 2; map
 message ContainerStats { ContainerAttributes attributes = 1; CpuUsage cpu = 2; MemoryUsage memory = 3; FilesystemUsage writable_layer = 4; }
 message CpuUsage { int64 timestamp = 1; UInt64Value usage_core_nano_seconds = 2; }
 message MemoryUsage { int64 timestamp = 1; UInt64Value working_set_bytes = 2; }
+message GetEventsRequest {}
+enum ContainerEventType { CONTAINER_CREATED_EVENT = 0; CONTAINER_STARTED_EVENT = 1; CONTAINER_STOPPED_EVENT = 2; CONTAINER_DELETED_EVENT = 3; }
+message ContainerEventResponse {
+  string container_id = 1; ContainerEventType container_event_type = 2; int64 created_at = 3;
+  PodSandboxStatus pod_sandbox_status = 4; repeated ContainerStatus containers_statuses = 5;
+}
 """, "runtime/v1alpha1/api.proto")
+# GetContainerEvents is the evented-PLEG stream of later CRI versions (KEP-3386) back-ported
+# into amdkube's CRI: the kubelet learns about container starts/exits immediately instead of
+# waiting for the next relist (the relist still runs as the consistency backstop).
 
 API_VERSION = "0.1.0"

@@ -1,0 +1,117 @@
+"""Remote CRI client (reference pkg/kubelet/remote/remote_runtime.go:42,177 and
+remote_image.go): typed async wrappers over the RuntimeService/ImageService stubs with
+per-call timeouts and operation metrics (kubelet_runtime_operations{operation_type})."""
+from __future__ import annotations
+
+import time
+
+import grpc
+
+from ..grpcdesc.cri import CRI as C
+
+
+class CRIClient:
+    def __init__(self, socket_path: str, timeout: float = 10.0, metrics=None):
+        self.socket = socket_path
+        self.timeout = timeout
+        self.ch = None
+        self.rt = self.img = None
+        self.metrics = metrics  # (ops Counter, errs Counter, latency Summary) or None
+
+    async def connect(self, wait: float = 10.0):
+        self.ch = grpc.aio.insecure_channel("unix://" + self.socket)
+        import asyncio
+        await asyncio.wait_for(self.ch.channel_ready(), wait)
+        self.rt = C.RuntimeService.stub(self.ch)
+        self.img = C.ImageService.stub(self.ch)
+        return self
+
+    async def close(self):
+        if self.ch is not None:
+            await self.ch.close()
+
+    async def _call(self, op, fn, req, timeout=None):
+        t0 = time.perf_counter()
+        try:
+            return await fn(req, timeout=timeout or self.timeout)
+        except grpc.RpcError:
+            if self.metrics:
+                self.metrics[1].labels(op).inc()
+            raise
+        finally:
+            if self.metrics:
+                self.metrics[0].labels(op).inc()
+                self.metrics[2].labels(op).observe((time.perf_counter() - t0) * 1e6)
+
+    # ------------------------------------------------------------- runtime
+    async def version(self):
+        return await self._call("version", self.rt.Version, C.VersionRequest(version="v1alpha1"))
+
+    async def status(self):
+        return await self._call("status", self.rt.Status, C.StatusRequest(verbose=True))
+
+    async def run_pod_sandbox(self, cfg) -> str:
+        return (await self._call("run_podsandbox", self.rt.RunPodSandbox, C.RunPodSandboxRequest(config=cfg))).pod_sandbox_id
+
+    async def stop_pod_sandbox(self, sid):
+        await self._call("stop_podsandbox", self.rt.StopPodSandbox, C.StopPodSandboxRequest(pod_sandbox_id=sid), timeout=60)
+
+    async def remove_pod_sandbox(self, sid):
+        await self._call("remove_podsandbox", self.rt.RemovePodSandbox, C.RemovePodSandboxRequest(pod_sandbox_id=sid), timeout=60)
+
+    async def list_pod_sandbox(self, uid: str | None = None):
+        f = C.PodSandboxFilter(label_selector={"io.kubernetes.pod.uid": uid}) if uid else None
+        req = C.ListPodSandboxRequest(filter=f) if f else C.ListPodSandboxRequest()
+        return list((await self._call("list_podsandbox", self.rt.ListPodSandbox, req)).items)
+
+    async def pod_sandbox_status(self, sid):
+        return (await self._call("podsandbox_status", self.rt.PodSandboxStatus, C.PodSandboxStatusRequest(pod_sandbox_id=sid))).status
+
+    async def create_container(self, sid, cfg, sandbox_cfg) -> str:
+        req = C.CreateContainerRequest(pod_sandbox_id=sid, config=cfg, sandbox_config=sandbox_cfg)
+        return (await self._call("create_container", self.rt.CreateContainer, req)).container_id
+
+    async def start_container(self, cid):
+        await self._call("start_container", self.rt.StartContainer, C.StartContainerRequest(container_id=cid))
+
+    async def stop_container(self, cid, timeout: int):
+        await self._call("stop_container", self.rt.StopContainer, C.StopContainerRequest(container_id=cid, timeout=timeout),
+                         timeout=timeout + 30)
+
+    async def remove_container(self, cid):
+        await self._call("remove_container", self.rt.RemoveContainer, C.RemoveContainerRequest(container_id=cid))
+
+    async def list_containers(self, sandbox_id: str | None = None):
+        f = C.ContainerFilter(pod_sandbox_id=sandbox_id) if sandbox_id else None
+        req = C.ListContainersRequest(filter=f) if f else C.ListContainersRequest()
+        return list((await self._call("list_containers", self.rt.ListContainers, req)).containers)
+
+    async def container_status(self, cid, verbose=False):
+        r = await self._call("container_status", self.rt.ContainerStatus, C.ContainerStatusRequest(container_id=cid, verbose=verbose))
+        return r.status, dict(r.info)
+
+    async def exec_sync(self, cid, cmd, timeout=10):
+        r = await self._call("exec_sync", self.rt.ExecSync, C.ExecSyncRequest(container_id=cid, cmd=cmd, timeout=timeout),
+                             timeout=timeout + 5)
+        return r.stdout, r.stderr, r.exit_code
+
+    async def list_container_stats(self):
+        return list((await self._call("list_container_stats", self.rt.ListContainerStats, C.ListContainerStatsRequest())).stats)
+
+    def container_events(self):
+        return self.rt.GetContainerEvents(C.GetEventsRequest())
+
+    # --------------------------------------------------------------- images
+    async def image_status(self, image):
+        r = await self._call("image_status", self.img.ImageStatus, C.ImageStatusRequest(image=C.ImageSpec(image=image)))
+        return r.image if r.HasField("image") else None
+
+    async def pull_image(self, image) -> str:
+        return (await self._call("pull_image", self.img.PullImage, C.PullImageRequest(image=C.ImageSpec(image=image)),
+                                 timeout=300)).image_ref
+
+    async def list_images(self):
+        return list((await self._call("list_images", self.img.ListImages, C.ListImagesRequest())).images)
+
+    async def image_fs_info(self):
+        return list((await self._call("image_fs_info", self.img.ImageFsInfo, C.ImageFsInfoRequest())).image_filesystems)

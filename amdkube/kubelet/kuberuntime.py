@@ -1,0 +1,272 @@
+"""kuberuntime: pod lifecycle against a CRI runtime.
+
+Reference pkg/kubelet/kuberuntime: SyncPod (kuberuntime_manager.go:568) driven by
+computePodActions (:441) — create a sandbox when none is ready (killing stragglers), run
+init containers one at a time, start/restart app containers per restartPolicy with
+CrashLoopBackOff, kill containers whose spec hash changed; createPodSandbox +
+generatePodSandboxConfig (kuberuntime_sandbox.go:35,62) whose annotations carry the device
+plugins' AdmitPod annotations (:93, fork); startContainer + generateContainerConfig
+(kuberuntime_container.go:88,180-231) whose devices/envs/mounts/annotations come from the
+DeviceManager's merged InitContainer responses (makeDevices :277, labels.go:108-114).
+"""
+from __future__ import annotations
+
+import asyncio
+import hashlib
+import json
+import logging
+import os
+import time
+
+import grpc
+
+from ..grpcdesc.cri import CRI as C
+from .cri_client import CRIClient
+
+log = logging.getLogger("amdkube.kuberuntime")
+
+L_POD_NAME, L_POD_NS, L_POD_UID = "io.kubernetes.pod.name", "io.kubernetes.pod.namespace", "io.kubernetes.pod.uid"
+L_CONTAINER = "io.kubernetes.container.name"
+A_HASH, A_RESTARTS, A_INIT = "io.kubernetes.container.hash", "io.kubernetes.container.restartCount", "io.amdkube.container.init"
+
+BACKOFF_BASE, BACKOFF_MAX = 10.0, 300.0
+
+
+def container_hash(c: dict) -> str:
+    return hashlib.sha1(json.dumps(c, sort_keys=True).encode()).hexdigest()[:16]
+
+
+class ContainerRuntimeStatus:
+    __slots__ = ("id", "name", "state", "exit_code", "reason", "message", "created_at", "started_at", "finished_at",
+                 "restart_count", "hash", "image", "image_ref", "init", "log_path")
+
+    @classmethod
+    def from_cri(cls, st, ann):
+        s = cls()
+        s.id, s.name, s.state = st.id, st.metadata.name, st.state
+        s.exit_code, s.reason, s.message = st.exit_code, st.reason, st.message
+        s.created_at, s.started_at, s.finished_at = st.created_at, st.started_at, st.finished_at
+        s.restart_count = int(ann.get(A_RESTARTS, "0") or 0)
+        s.hash = ann.get(A_HASH, "")
+        s.init = ann.get(A_INIT) == "true"
+        s.image, s.image_ref, s.log_path = st.image.image, st.image_ref, st.log_path
+        return s
+
+
+class PodRuntimeStatus:
+    def __init__(self, uid):
+        self.uid = uid
+        self.sandboxes = []  # newest first: (id, state, attempt, created_at)
+        self.containers: dict[str, list[ContainerRuntimeStatus]] = {}  # name -> newest first
+
+    def ready_sandbox(self):
+        for s in self.sandboxes:
+            if s[1] == C.SANDBOX_READY:
+                return s
+        return None
+
+    def latest(self, name) -> ContainerRuntimeStatus | None:
+        lst = self.containers.get(name)
+        return lst[0] if lst else None
+
+    def running(self):
+        return [c for lst in self.containers.values() for c in lst if c.state == C.CONTAINER_RUNNING]
+
+
+class RuntimeManager:
+    def __init__(self, cri: CRIClient, device_manager, root_dir: str, recorder=None, image_pull_qps: float = 0):
+        self.cri = cri
+        self.dm = device_manager
+        self.root = root_dir
+        self.recorder = recorder
+        self.backoff: dict[tuple[str, str], tuple[float, float]] = {}  # (uid, name) -> (until, last delay)
+
+    # ----------------------------------------------------------------- status
+    async def pod_status(self, uid: str, sandboxes=None) -> PodRuntimeStatus:
+        st = PodRuntimeStatus(uid)
+        sbs = sandboxes if sandboxes is not None else await self.cri.list_pod_sandbox(uid)
+        sbs = sorted(sbs, key=lambda s: s.created_at, reverse=True)
+        st.sandboxes = [(s.id, s.state, s.metadata.attempt, s.created_at) for s in sbs]
+        for s in sbs:
+            for c in await self.cri.list_containers(s.id):
+                try:
+                    cs, _ = await self.cri.container_status(c.id)
+                except grpc.RpcError:
+                    continue
+                st.containers.setdefault(c.metadata.name, []).append(ContainerRuntimeStatus.from_cri(cs, dict(c.annotations)))
+        for lst in st.containers.values():
+            lst.sort(key=lambda x: x.created_at, reverse=True)
+        return st
+
+    # ---------------------------------------------------------------- sandbox
+    def sandbox_config(self, pod: dict, attempt: int, annotations: dict) -> "C.PodSandboxConfig":
+        md, spec = pod["metadata"], pod.get("spec") or {}
+        log_dir = os.path.join(self.root, "pods", md["uid"], "logs")
+        os.makedirs(log_dir, exist_ok=True)
+        ports = [C.PortMapping(container_port=p.get("containerPort", 0), host_port=p.get("hostPort", 0),
+                               protocol=C.UDP if p.get("protocol") == "UDP" else C.TCP)
+                 for c in spec.get("containers") or [] for p in c.get("ports") or []]
+        ann = dict(md.get("annotations") or {})
+        ann.update(annotations or {})
+        return C.PodSandboxConfig(
+            metadata=C.PodSandboxMetadata(name=md["name"], uid=md["uid"], namespace=md.get("namespace", ""), attempt=attempt),
+            hostname=spec.get("hostname") or md["name"], log_directory=log_dir, port_mappings=ports,
+            labels={**(md.get("labels") or {}), L_POD_NAME: md["name"], L_POD_NS: md.get("namespace", ""), L_POD_UID: md["uid"]},
+            annotations=ann,
+            linux=C.LinuxPodSandboxConfig(security_context=C.LinuxSandboxSecurityContext(
+                namespace_options=C.NamespaceOption(host_network=True, host_pid=bool(spec.get("hostPID")),
+                                                    host_ipc=bool(spec.get("hostIPC"))))))
+
+    # -------------------------------------------------------------- containers
+    async def ensure_image(self, c: dict):
+        image = c["image"]
+        policy = c.get("imagePullPolicy", "IfNotPresent")
+        present = await self.cri.image_status(image)
+        if policy == "Never" and present is None:
+            raise RuntimeError(f"ErrImageNeverPull: image {image} not present with pull policy Never")
+        if present is None or policy == "Always":
+            try:
+                await self.cri.pull_image(image)
+            except grpc.RpcError as e:
+                if present is None:
+                    raise RuntimeError(f"ErrImagePull: {e.details()}")
+
+    async def start_container(self, pod: dict, c: dict, sid: str, sandbox_cfg, ctx: dict, restart_count: int, init: bool):
+        await self.ensure_image(c)
+        opts = await self.dm.init_container(pod, c)
+        envs = [C.KeyValue(key=k, value=v) for k, v in (ctx.get("env", {}).get(c["name"]) or {}).items()]
+        envs += [C.KeyValue(key=k, value=v) for k, v in opts["envs"].items()]
+        mounts = [C.Mount(container_path=m["container_path"], host_path=m["host_path"], readonly=bool(m.get("read_only")))
+                  for m in (ctx.get("mounts", {}).get(c["name"]) or []) + opts["mounts"]]
+        devices = [C.Device(container_path=d["container_path"], host_path=d["host_path"], permissions=d.get("permissions", "rw"))
+                   for d in opts["devices"]]
+        ann = dict(opts["annotations"])
+        ann.update({A_HASH: container_hash(c), A_RESTARTS: str(restart_count), A_INIT: "true" if init else "false"})
+        res = (c.get("resources") or {}).get("limits") or {}
+        lres = C.LinuxContainerResources()
+        if "memory" in res:
+            from ..api.quantity import Quantity
+            lres.memory_limit_in_bytes = Quantity(res["memory"]).value()
+        if "cpu" in res:
+            from ..api.quantity import Quantity
+            lres.cpu_period = 100000
+            lres.cpu_quota = max(1000, Quantity(res["cpu"]).milli_value() * 100)
+        md = pod["metadata"]
+        cfg = C.ContainerConfig(
+            metadata=C.ContainerMetadata(name=c["name"], attempt=restart_count), image=C.ImageSpec(image=c["image"]),
+            command=c.get("command") or [], args=c.get("args") or [], working_dir=c.get("workingDir") or "",
+            envs=envs, mounts=mounts, devices=devices,
+            labels={L_POD_NAME: md["name"], L_POD_NS: md.get("namespace", ""), L_POD_UID: md["uid"], L_CONTAINER: c["name"]},
+            annotations=ann, log_path=f"{c['name']}/{restart_count}.log", linux=C.LinuxContainerConfig(resources=lres))
+        cid = await self.cri.create_container(sid, cfg, sandbox_cfg)
+        await self.cri.start_container(cid)
+        return cid
+
+    # ------------------------------------------------------------------ sync
+    async def sync_pod(self, pod: dict, st: PodRuntimeStatus, ctx: dict, liveness_failed: set | None = None) -> list[str]:
+        """One reconciliation step. Returns errors (pod-level messages)."""
+        errors = []
+        spec = pod.get("spec") or {}
+        uid = pod["metadata"]["uid"]
+        policy = spec.get("restartPolicy", "Always")
+        sb = st.ready_sandbox()
+        ever_ran = any(c.state == C.CONTAINER_EXITED for lst in st.containers.values() for c in lst)
+        if sb is None:
+            if policy == "Never" and ever_ran:
+                return errors  # terminal; never recreate the sandbox
+            for c in st.running():
+                await self.cri.stop_container(c.id, 2)
+            attempt = (st.sandboxes[0][2] + 1) if st.sandboxes else 0
+            sandbox_cfg = self.sandbox_config(pod, attempt, self.dm.pod_resources(pod))
+            sid = await self.cri.run_pod_sandbox(sandbox_cfg)
+            st = PodRuntimeStatus(uid)
+            st.sandboxes = [(sid, C.SANDBOX_READY, attempt, time.time_ns())]
+        else:
+            sid = sb[0]
+            sandbox_cfg = self.sandbox_config(pod, sb[2], self.dm.pod_resources(pod))
+        # init containers, strictly in order
+        for ic in spec.get("initContainers") or []:
+            cur = st.latest(ic["name"])
+            if cur is not None and cur.state == C.CONTAINER_RUNNING:
+                return errors
+            if cur is not None and cur.state == C.CONTAINER_EXITED and cur.exit_code == 0:
+                continue
+            if cur is not None and cur.state == C.CONTAINER_EXITED:
+                if policy == "Never":
+                    return errors
+                if not self._backoff_ok(uid, ic["name"]):
+                    return errors
+            rc = (cur.restart_count + 1) if cur is not None else 0
+            try:
+                await self.start_container(pod, ic, sid, sandbox_cfg, ctx, rc, True)
+            except Exception as e:
+                errors.append(f"init container {ic['name']}: {e}")
+            return errors
+        for c in spec.get("containers") or []:
+            cur = st.latest(c["name"])
+            h = container_hash(c)
+            if cur is not None and cur.state == C.CONTAINER_RUNNING:
+                if cur.hash and cur.hash != h or (liveness_failed and c["name"] in liveness_failed):
+                    await self.cri.stop_container(cur.id, int(spec.get("terminationGracePeriodSeconds", 30)))
+                    if self.recorder:
+                        self.recorder.event(pod, "Normal", "Killing", f"Killing container {c['name']} (spec changed or liveness failed)")
+                else:
+                    continue
+                cur = None if policy != "Never" else cur
+            if cur is not None and cur.state in (C.CONTAINER_EXITED, C.CONTAINER_UNKNOWN):
+                if policy == "Never" or (policy == "OnFailure" and cur.exit_code == 0):
+                    continue
+                if not self._backoff_ok(uid, c["name"]):
+                    continue
+            elif cur is not None and cur.state == C.CONTAINER_CREATED:
+                try:
+                    await self.cri.start_container(cur.id)
+                except grpc.RpcError as e:
+                    errors.append(f"start {c['name']}: {e.details()}")
+                continue
+            rc = (cur.restart_count + 1) if cur is not None else 0
+            try:
+                await self.start_container(pod, c, sid, sandbox_cfg, ctx, rc, False)
+            except grpc.RpcError as e:
+                errors.append(f"container {c['name']}: {e.details()}")
+            except Exception as e:
+                errors.append(f"container {c['name']}: {e}")
+        return errors
+
+    def _backoff_ok(self, uid, name) -> bool:
+        now = time.monotonic()
+        until, last = self.backoff.get((uid, name), (0.0, 0.0))
+        if now < until:
+            return False
+        delay = min(BACKOFF_MAX, last * 2 if last else BACKOFF_BASE)
+        self.backoff[(uid, name)] = (now + delay, delay)
+        return True
+
+    def backoff_remaining(self, uid, name) -> float:
+        until, _ = self.backoff.get((uid, name), (0.0, 0.0))
+        return max(0.0, until - time.monotonic())
+
+    async def kill_pod(self, uid: str, grace: int = 30, pod: dict | None = None):
+        sbs = await self.cri.list_pod_sandbox(uid)
+        for s in sbs:
+            conts = await self.cri.list_containers(s.id)
+            await asyncio.gather(*(self._kill_container(pod, c, grace) for c in conts if c.state == C.CONTAINER_RUNNING))
+            await self.cri.stop_pod_sandbox(s.id)
+        for k in [k for k in self.backoff if k[0] == uid]:
+            del self.backoff[k]
+
+    async def _kill_container(self, pod, c, grace):
+        if pod is not None:
+            for sc in (pod.get("spec") or {}).get("containers") or []:
+                if sc["name"] == c.metadata.name:
+                    pre = ((sc.get("lifecycle") or {}).get("preStop") or {}).get("exec")
+                    if pre:
+                        try:
+                            await self.cri.exec_sync(c.id, pre.get("command") or [], min(grace, 30) or 1)
+                        except grpc.RpcError:
+                            pass
+        await self.cri.stop_container(c.id, grace)
+
+    async def remove_pod(self, uid: str):
+        for s in await self.cri.list_pod_sandbox(uid):
+            await self.cri.remove_pod_sandbox(s.id)

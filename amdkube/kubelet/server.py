@@ -1,0 +1,196 @@
+"""Kubelet HTTP API (reference pkg/kubelet/server/server.go:260-411): /healthz (with the
+syncloop check), /pods, /runningpods/, /metrics, /metrics/cadvisor (per-container
+accelerator series), /stats/summary (stats/v1alpha1 incl. Accelerators[], types.go:121-122,
+213-230), /spec, /containerLogs/{ns}/{pod}/{container}, /run/{ns}/{pod}/{container}
+(exec-sync) and /debug/pprof."""
+from __future__ import annotations
+
+import asyncio
+import json
+import os
+import time
+
+from aiohttp import web
+
+from ..api import meta as m
+from ..grpcdesc.cri import CRI as C
+from ..utils import profiling
+from ..utils.metrics import CONTENT_TYPE, render
+from .kuberuntime import L_POD_UID
+
+
+class KubeletServer:
+    def __init__(self, kubelet):
+        self.k = kubelet
+        app = self.app = web.Application()
+        app.router.add_get("/healthz", self.healthz)
+        app.router.add_get("/healthz/syncloop", self.healthz)
+        app.router.add_get("/pods", self.pods)
+        app.router.add_get("/runningpods/", self.running_pods)
+        app.router.add_get("/metrics", self.metrics)
+        app.router.add_get("/metrics/cadvisor", self.metrics_cadvisor)
+        app.router.add_get("/stats/summary", self.summary)
+        app.router.add_get("/stats/", self.summary)
+        app.router.add_get("/spec/", self.spec)
+        app.router.add_get("/spec", self.spec)
+        app.router.add_get("/containerLogs/{ns}/{pod}/{container}", self.logs)
+        app.router.add_post("/run/{ns}/{pod}/{container}", self.run)
+        profiling.add_routes(app)
+        self.runner = None
+        self.port = None
+
+    async def start(self, host, port):
+        self.runner = web.AppRunner(self.app, access_log=None)
+        await self.runner.setup()
+        site = web.TCPSite(self.runner, host, port, reuse_address=True)
+        await site.start()
+        self.port = site._server.sockets[0].getsockname()[1]
+        return self
+
+    async def stop(self):
+        if self.runner:
+            await self.runner.cleanup()
+
+    async def healthz(self, req):
+        # the sync loop is healthy if a pod worker or the housekeeping pass ran recently
+        if time.time() - self.k.last_sync_loop > max(120.0, 2 * self.k.cfg.sync_frequency):
+            return web.Response(status=500, text="syncloop failed: no sync in the last interval")
+        return web.Response(text="ok")
+
+    async def pods(self, req):
+        items = []
+        for uid, p in self.k.pods.items():
+            p = dict(p)
+            st = self.k.status.get(uid)
+            if st:
+                p["status"] = st
+            items.append(p)
+        return web.json_response({"kind": "PodList", "apiVersion": "v1", "metadata": {}, "items": items})
+
+    async def running_pods(self, req):
+        out = []
+        for s in await self.k.cri.list_pod_sandbox():
+            if s.state != C.SANDBOX_READY:
+                continue
+            cs = await self.k.cri.list_containers(s.id)
+            out.append({"metadata": {"name": s.metadata.name, "namespace": s.metadata.namespace, "uid": s.metadata.uid},
+                        "spec": {"containers": [{"name": c.metadata.name, "image": c.image.image} for c in cs
+                                                if c.state == C.CONTAINER_RUNNING]}})
+        return web.json_response({"kind": "PodList", "apiVersion": "v1", "metadata": {}, "items": out})
+
+    async def metrics(self, req):
+        return web.Response(body=render(self.k.metrics), headers={"Content-Type": CONTENT_TYPE})
+
+    async def metrics_cadvisor(self, req):
+        from ..monitoring.collector import AcceleratorCollector
+        col = AcceleratorCollector(self.k.smi, self.k.node_name)
+        text = col.render_container_metrics(self._pod_devices())
+        return web.Response(text=text, headers={"Content-Type": CONTENT_TYPE})
+
+    def _pod_devices(self) -> list[dict]:
+        """[{namespace, pod, container, devices: [ids]}] for running pods on this node."""
+        from .devicemanager import container_device_requests
+        out = []
+        for uid, p in self.k.pods.items():
+            st = self.k.status.get(uid) or {}
+            if st.get("phase") != "Running":
+                continue
+            for c in (p.get("spec") or {}).get("containers") or []:
+                ids = [d for lst in container_device_requests(p, c).values() for d in lst]
+                if ids:
+                    out.append({"namespace": m.namespace_of(p), "pod": m.name_of(p), "container": c["name"], "devices": ids})
+        return out
+
+    async def summary(self, req):
+        import psutil
+        now = m.now_rfc3339()
+        vm = psutil.virtual_memory()
+        cpu = psutil.cpu_times()
+        stats = {s.attributes.id: s for s in await self.k.cri.list_container_stats()}
+        conts = await self.k.cri.list_containers()
+        from ..monitoring.collector import AcceleratorCollector
+        accel = AcceleratorCollector(self.k.smi, self.k.node_name)
+        dev_map = {(d["namespace"], d["pod"], d["container"]): d["devices"] for d in self._pod_devices()}
+        pods = {}
+        for c in conts:
+            if c.state != C.CONTAINER_RUNNING:
+                continue
+            uid = c.labels.get(L_POD_UID, "")
+            p = self.k.pods.get(uid)
+            if p is None:
+                continue
+            ent = pods.setdefault(uid, {"podRef": {"name": m.name_of(p), "namespace": m.namespace_of(p), "uid": uid},
+                                        "startTime": (p.get("status") or {}).get("startTime"), "containers": []})
+            s = stats.get(c.id)
+            cont = {"name": c.metadata.name, "startTime": now,
+                    "cpu": {"time": now, "usageCoreNanoSeconds": s.cpu.usage_core_nano_seconds.value if s else 0},
+                    "memory": {"time": now, "workingSetBytes": s.memory.working_set_bytes.value if s else 0}}
+            ids = dev_map.get((m.namespace_of(p), m.name_of(p), c.metadata.name))
+            if ids:
+                cont["accelerators"] = accel.accelerator_stats(ids)
+            ent["containers"].append(cont)
+        return web.json_response({
+            "node": {"nodeName": self.k.node_name, "startTime": m.now_rfc3339(),
+                     "cpu": {"time": now, "usageCoreNanoSeconds": int((cpu.user + cpu.system) * 1e9)},
+                     "memory": {"time": now, "availableBytes": vm.available, "usageBytes": vm.total - vm.available,
+                                "workingSetBytes": vm.total - vm.available},
+                     "accelerators": accel.accelerator_stats(None)},
+            "pods": list(pods.values())})
+
+    async def spec(self, req):
+        import psutil
+        return web.json_response({"num_cores": psutil.cpu_count(), "memory_capacity": psutil.virtual_memory().total,
+                                  "machine_id": "", "system_uuid": "", "boot_id": "",
+                                  "accelerators": [dict(g) for g in (self.k.smi.gpus() if self.k.smi else [])]})
+
+    async def _find_container(self, ns, pod, cname):
+        for uid, p in self.k.pods.items():
+            if m.namespace_of(p) == ns and m.name_of(p) == pod:
+                rt = await self.k.runtime.pod_status(uid)
+                return rt.latest(cname)
+        return None
+
+    async def logs(self, req):
+        ns, pod, cname = req.match_info["ns"], req.match_info["pod"], req.match_info["container"]
+        cs = await self._find_container(ns, pod, cname)
+        if cs is None:
+            return web.Response(status=404, text=f"container {cname} of pod {ns}/{pod} not found")
+        _, info = await self.k.cri.container_status(cs.id, verbose=True)
+        path = cs.log_path
+        if not path or not os.path.exists(path):
+            return web.Response(text="")
+        tail = req.query.get("tailLines")
+        follow = req.query.get("follow") in ("true", "1")
+        with open(path, "rb") as f:
+            data = f.read()
+        if tail:
+            lines = data.splitlines(keepends=True)
+            data = b"".join(lines[-int(tail):])
+        if not follow:
+            return web.Response(body=data, content_type="text/plain")
+        resp = web.StreamResponse()
+        await resp.prepare(req)
+        await resp.write(data)
+        off = os.path.getsize(path)
+        for _ in range(3600):
+            await asyncio.sleep(0.5)
+            st, _ = await self.k.cri.container_status(cs.id)
+            with open(path, "rb") as f:
+                f.seek(off)
+                chunk = f.read()
+            if chunk:
+                await resp.write(chunk)
+                off += len(chunk)
+            if st.state != C.CONTAINER_RUNNING:
+                break
+        await resp.write_eof()
+        return resp
+
+    async def run(self, req):
+        ns, pod, cname = req.match_info["ns"], req.match_info["pod"], req.match_info["container"]
+        cs = await self._find_container(ns, pod, cname)
+        if cs is None:
+            return web.Response(status=404, text="container not found")
+        cmd = req.query.getall("cmd", None) or (await req.text()).split()
+        out, err, rc = await self.k.cri.exec_sync(cs.id, cmd, int(req.query.get("timeout", "30")))
+        return web.Response(body=out + err, status=200 if rc == 0 else 500, headers={"X-Exit-Code": str(rc)})

@@ -1,0 +1,126 @@
+"""In-process single-node cluster: apiserver + scheduler + controller-manager + rocshim +
+AMD device plugin + kubelet on one event loop (the reference's integration framework
+starts the master in-process over httptest, test/integration/framework/master_utils.go:174,
+and hack/local-up-cluster.sh wires the same components as processes, :394-784).
+
+Used by the integration tests, `bench.py` and `python -m amdkube local-up`.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import os
+import shutil
+import tempfile
+
+from .apiserver import APIServer
+from .client import Client
+from .deviceplugin import AMDGPUPlugin
+from .kubelet.kubelet import Kubelet, KubeletConfig
+from .runtime import RocShim
+from .scheduler import Scheduler
+from .smi import open_backend
+
+log = logging.getLogger("amdkube.localcluster")
+
+
+class LocalCluster:
+    def __init__(self, gpus: str = "fake", n_gpus: int | None = None, node_name: str = "mi355x-node-0",
+                 base_dir: str | None = None, with_controllers: bool = True, relist_period: float = 1.0,
+                 node_status_update_frequency: float = 10.0, scheduler_kw: dict | None = None, isolation: str = "env",
+                 health_probe: str = "none", kubelet_kw: dict | None = None, with_kubelet: bool = True):
+        self.gpus, self.n_gpus, self.node_name = gpus, n_gpus, node_name
+        self._own_dir = base_dir is None
+        self.base = base_dir or tempfile.mkdtemp(prefix="ak-", dir="/tmp")
+        self.with_controllers = with_controllers
+        self.relist_period = relist_period
+        self.nsuf = node_status_update_frequency
+        self.scheduler_kw = scheduler_kw or {}
+        self.kubelet_kw = kubelet_kw or {}
+        self.isolation = isolation
+        self.health_probe = health_probe
+        self.with_kubelet = with_kubelet
+        self.api = self.client = self.scheduler = self.controllers = self.shim = self.plugin = self.kubelet = None
+        self.backend = None
+
+    async def start(self):
+        b = self.base
+        self.api = await APIServer().start()
+        self.client = Client(self.api.url, pool=256)
+        self.scheduler = await Scheduler(Client(self.api.url, pool=256), **self.scheduler_kw).start()
+        if self.with_controllers:
+            from .controllers import ControllerManager
+            self.controllers = await ControllerManager(Client(self.api.url)).start()
+        if not self.with_kubelet:
+            return self
+        self.shim = await RocShim(os.path.join(b, "rocshim.sock"), os.path.join(b, "rocshim"),
+                                  hooks_dir=os.path.join(b, "hooks.d"), isolation=self.isolation).start()
+        if self.gpus != "none":
+            self.backend = open_backend(self.gpus, n=self.n_gpus)
+            self.plugin = AMDGPUPlugin(self.backend, plugins_dir=os.path.join(b, "plugins"), health_interval=5.0,
+                                       health_probe=self.health_probe)
+        cfg = KubeletConfig(node_name=self.node_name, root_dir=os.path.join(b, "kubelet"), plugins_dir=os.path.join(b, "plugins"),
+                            cri_socket=os.path.join(b, "rocshim.sock"), port=0, relist_period=self.relist_period,
+                            node_status_update_frequency=self.nsuf, **self.kubelet_kw)
+        self.kubelet = await Kubelet(Client(self.api.url, pool=128), cfg, smi_backend=self.backend).start()
+        if self.plugin is not None:
+            await self.plugin.start()
+            await self.plugin.wait_for_registration(10)
+        return self
+
+    async def wait_gpus(self, n: int, timeout: float = 15.0):
+        loop = asyncio.get_running_loop()
+        end = loop.time() + timeout
+        while loop.time() < end:
+            node = await self.client.get_or_none("nodes", self.node_name)
+            if node and int(((node.get("status") or {}).get("allocatable") or {}).get("amd.com/gpu", 0)) >= n:
+                ext = (node.get("status") or {}).get("extendedResources") or {}
+                if len(((ext.get("amd.com/gpu") or {}).get("resources") or {})) >= n:
+                    return node
+            await asyncio.sleep(0.05)
+        raise TimeoutError(f"node never advertised {n} GPUs")
+
+    async def stop(self):
+        for comp in (self.kubelet, self.plugin):
+            if comp is not None:
+                try:
+                    await comp.stop()
+                except Exception as e:
+                    log.debug("stop %s: %r", comp, e)
+        if self.shim is not None:
+            await self.shim.stop(kill_pods=True)
+        for comp in (self.controllers, self.scheduler):
+            if comp is not None:
+                await comp.stop()
+                await comp.client.close()
+        if self.kubelet is not None:
+            await self.kubelet.client.close()
+        if self.client is not None:
+            await self.client.close()
+        if self.api is not None:
+            await self.api.stop()
+        if self.backend is not None:
+            try:
+                self.backend.close()
+            except Exception:
+                pass
+        if self._own_dir:
+            shutil.rmtree(self.base, ignore_errors=True)
+
+    async def __aenter__(self):
+        return await self.start()
+
+    async def __aexit__(self, *exc):
+        await self.stop()
+
+
+async def wait_pod(client: Client, ns: str, name: str, phases=("Running",), timeout: float = 30.0) -> dict:
+    loop = asyncio.get_running_loop()
+    end = loop.time() + timeout
+    last = None
+    while loop.time() < end:
+        last = await client.get_or_none("pods", name, ns)
+        if last and (last.get("status") or {}).get("phase") in phases:
+            return last
+        await asyncio.sleep(0.02)
+    raise TimeoutError(f"pod {ns}/{name} did not reach {phases}: {(last or {}).get('status')}")

@@ -1,0 +1,69 @@
+"""GPU metric collection (node + per-container) on top of the SMI backends.
+
+Replaces cAdvisor's NVML accelerator collector (vendor/github.com/google/cadvisor/
+accelerators/nvidia.go:140-252 — per-container AcceleratorStats{Make, Model, ID,
+MemoryTotal, MemoryUsed, DutyCycle} found by parsing the devices cgroup for c 195:<minor>)
+and its Prometheus export (vendor/github.com/google/cadvisor/metrics/prometheus.go:275-306).
+The container↔GPU mapping comes from the kubelet's own allocation record (assigned device
+IDs), not from cgroup-v1 parsing.
+"""
+from __future__ import annotations
+
+import time
+
+from ..smi import device_id
+
+
+class AcceleratorCollector:
+    def __init__(self, backend, node: str = ""):
+        self.b = backend
+        self.node = node
+        self._gpus = None
+
+    def gpus(self):
+        if self._gpus is None:
+            self._gpus = self.b.gpus() if self.b else []
+        return self._gpus
+
+    def by_id(self):
+        return {device_id(g): g for g in self.gpus()}
+
+    def accelerator_stats(self, ids: list[str] | None) -> list[dict]:
+        """stats/v1alpha1 AcceleratorStats for the given device IDs (None = all GPUs)."""
+        if not self.b:
+            return []
+        out = []
+        bid = self.by_id()
+        for did in (ids if ids is not None else list(bid)):
+            g = bid.get(did)
+            if g is None:
+                continue
+            try:
+                s = self.b.sample(g["index"])
+            except Exception:
+                s = {}
+            out.append({"make": "amd", "model": g.get("market_name", ""), "id": did,
+                        "memoryTotal": int(g.get("vram_total_bytes") or 0), "memoryUsed": int(s.get("vram_used_bytes") or 0),
+                        "dutyCycle": int(s.get("gfx_activity") or 0)})
+        return out
+
+    def render_container_metrics(self, pod_devices: list[dict]) -> str:
+        """container_accelerator_* exposition text (cadvisor metric names + labels)."""
+        lines = ["# HELP container_accelerator_memory_total_bytes Total accelerator memory.",
+                 "# TYPE container_accelerator_memory_total_bytes gauge",
+                 "# HELP container_accelerator_memory_used_bytes Total accelerator memory allocated.",
+                 "# TYPE container_accelerator_memory_used_bytes gauge",
+                 "# HELP container_accelerator_duty_cycle Percent of time over the past sample period during which the accelerator was actively processing.",
+                 "# TYPE container_accelerator_duty_cycle gauge"]
+        for pd in pod_devices:
+            for st in self.accelerator_stats(pd["devices"]):
+                lab = (f'container_name="{pd["container"]}",pod_name="{pd["pod"]}",namespace="{pd["namespace"]}",'
+                       f'make="{st["make"]}",model="{st["model"]}",acc_id="{st["id"]}"')
+                lines.append(f"container_accelerator_memory_total_bytes{{{lab}}} {st['memoryTotal']}")
+                lines.append(f"container_accelerator_memory_used_bytes{{{lab}}} {st['memoryUsed']}")
+                lines.append(f"container_accelerator_duty_cycle{{{lab}}} {st['dutyCycle']}")
+        return "\n".join(lines) + "\n"
+
+
+def now() -> float:
+    return time.time()

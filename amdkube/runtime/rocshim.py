@@ -1,0 +1,659 @@
+"""rocshim — amdkube's CRI runtime for MI355X nodes (replaces dockershim + dockerd + the
+nvidia OCI runtime hook; reference pkg/kubelet/dockershim).
+
+CRI v1alpha1 RuntimeService + ImageService over a Unix socket. A pod sandbox is a `pause`
+process (native/pause.cpp, child subreaper); containers are process trees started with
+their own session so the whole tree can be signalled. GPU injection follows the device
+plugin's InitContainer response as carried in the CRI ContainerConfig:
+  * env  — ROCR_VISIBLE_DEVICES from the plugin; inherited HIP/CUDA/ROCR visibility
+           variables are scrubbed so a container sees exactly its assigned GPUs, and a
+           container with no GPU devices gets HIP_VISIBLE_DEVICES=-1 (sees none);
+  * devices — /dev/kfd + /dev/dri/renderD<N>: in `isolation=namespaces` mode (root) the
+           native `amdkube-nsexec` helper gives the container a private /dev/dri holding
+           only its render nodes and joins a cgroup-v2 leaf with cpu/memory limits; in the
+           default `env` mode (unprivileged) the device list is validated and recorded.
+The runtime handler for a container is chosen by the hooks.d service (F21 semantics).
+
+State (sandboxes + containers) is checkpointed as JSON so a restarted rocshim re-adopts
+running pods instead of orphaning them; exit codes of re-adopted processes
+are recovered from the per-container exit file written by the launcher.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import os
+import shutil
+import signal
+import time
+import uuid
+
+import grpc
+
+from ..grpcdesc.cri import API_VERSION, CRI as C
+from .hooks import DEFAULT_HOOKS_DIR, HookService
+from .images import NATIVE_BIN, ImageStore
+
+log = logging.getLogger("amdkube.rocshim")
+
+RUNTIME_NAME = "rocshim"
+RUNTIME_VERSION = "0.1.0"
+HANDLERS = {"rocm", "default"}
+SCRUB_ENV = ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL",
+             "OMPI_COMM_WORLD_LOCAL_RANK", "LOCAL_RANK", "RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+             "TORCHELASTIC_RUN_ID", "GROUP_RANK", "LOCAL_WORLD_SIZE", "ROLE_RANK")
+
+
+def now_ns() -> int:
+    return time.time_ns()
+
+
+class Sandbox:
+    def __init__(self, sid, config_bytes, meta, labels, annotations, log_dir):
+        self.id, self.config_bytes = sid, config_bytes
+        self.meta, self.labels, self.annotations, self.log_dir = meta, labels, annotations, log_dir
+        self.state = C.SANDBOX_READY
+        self.created_at = now_ns()
+        self.pid = 0
+        self.proc = None
+
+    def to_json(self):
+        return {"id": self.id, "meta": self.meta, "labels": self.labels, "annotations": self.annotations,
+                "log_dir": self.log_dir, "state": self.state, "created_at": self.created_at, "pid": self.pid}
+
+
+class Container:
+    def __init__(self, cid, sandbox_id, name, attempt, image, image_ref, argv, env, cwd, log_path, labels, annotations,
+                 mounts, devices, handler, resources):
+        self.id, self.sandbox_id, self.name, self.attempt = cid, sandbox_id, name, attempt
+        self.image, self.image_ref, self.argv, self.env, self.cwd = image, image_ref, argv, env, cwd
+        self.log_path, self.labels, self.annotations = log_path, labels, annotations
+        self.mounts, self.devices, self.handler, self.resources = mounts, devices, handler, resources
+        self.state = C.CONTAINER_CREATED
+        self.created_at = now_ns()
+        self.started_at = 0
+        self.finished_at = 0
+        self.exit_code = 0
+        self.reason = ""
+        self.message = ""
+        self.pid = 0
+        self.proc: asyncio.subprocess.Process | None = None
+        self.waiter: asyncio.Task | None = None
+
+    def to_json(self):
+        d = {k: getattr(self, k) for k in ("id", "sandbox_id", "name", "attempt", "image", "image_ref", "argv", "env", "cwd",
+                                            "log_path", "labels", "annotations", "mounts", "devices", "handler", "resources",
+                                            "state", "created_at", "started_at", "finished_at", "exit_code", "reason",
+                                            "message", "pid")}
+        return d
+
+
+class RocShim:
+    def __init__(self, socket_path: str, state_dir: str, hooks_dir: str = DEFAULT_HOOKS_DIR, isolation: str = "env",
+                 cgroup_root: str = "/sys/fs/cgroup/amdkube", dev_root: str = "/dev"):
+        self.socket = socket_path
+        self.state_dir = state_dir
+        os.makedirs(os.path.join(state_dir, "sandboxes"), exist_ok=True)
+        os.makedirs(os.path.join(state_dir, "containers"), exist_ok=True)
+        os.makedirs(os.path.join(state_dir, "rootfs"), exist_ok=True)
+        self.images = ImageStore(state_dir)
+        self.hooks = HookService(hooks_dir, HANDLERS)
+        self.isolation = isolation
+        self.cgroup_root = cgroup_root
+        self.dev_root = dev_root
+        self.sandboxes: dict[str, Sandbox] = {}
+        self.containers: dict[str, Container] = {}
+        self.server: grpc.aio.Server | None = None
+        self.pause_bin = os.path.join(NATIVE_BIN, "pause")
+        self.nsexec_bin = os.path.join(NATIVE_BIN, "amdkube-nsexec")
+        self.started = 0
+        self._adopt_tasks: set = set()
+        self._event_streams: set[asyncio.Queue] = set()
+
+    def _emit(self, c: "Container", etype: int):
+        if not self._event_streams:
+            return
+        ev = (c.id, c.sandbox_id, etype, now_ns())
+        for q in list(self._event_streams):
+            q.put_nowait(ev)
+
+    # ------------------------------------------------------------------ lifecycle
+    async def start(self):
+        await self.hooks.start()
+        self._recover()
+        os.makedirs(os.path.dirname(self.socket), exist_ok=True)
+        if os.path.exists(self.socket):
+            os.unlink(self.socket)
+        self.server = grpc.aio.server()
+        self.server.add_generic_rpc_handlers((C.RuntimeService.handler(_Runtime(self)), C.ImageService.handler(_Images(self))))
+        self.server.add_insecure_port("unix://" + self.socket)
+        await self.server.start()
+        log.info("rocshim serving CRI on %s (isolation=%s)", self.socket, self.isolation)
+        return self
+
+    async def stop(self, kill_pods: bool = False):
+        if kill_pods:
+            for s in list(self.sandboxes.values()):
+                await self.stop_sandbox(s.id)
+        await self.hooks.stop()
+        if self.server:
+            await self.server.stop(0.5)
+        for t in list(self._adopt_tasks):
+            t.cancel()
+
+    # --------------------------------------------------------------- checkpoints
+    def _ckpt(self, kind: str, obj):
+        p = os.path.join(self.state_dir, kind, obj.id + ".json")
+        tmp = p + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump(obj.to_json(), f)
+        os.replace(tmp, p)
+
+    def _unckpt(self, kind: str, oid: str):
+        try:
+            os.unlink(os.path.join(self.state_dir, kind, oid + ".json"))
+        except FileNotFoundError:
+            pass
+
+    def _recover(self):
+        for name in os.listdir(os.path.join(self.state_dir, "sandboxes")):
+            if not name.endswith(".json"):
+                continue
+            try:
+                d = json.load(open(os.path.join(self.state_dir, "sandboxes", name)))
+            except (OSError, ValueError):
+                continue
+            s = Sandbox(d["id"], b"", d["meta"], d["labels"], d["annotations"], d["log_dir"])
+            s.state, s.created_at, s.pid = d["state"], d["created_at"], d["pid"]
+            if s.state == C.SANDBOX_READY and not _alive(s.pid):
+                s.state = C.SANDBOX_NOTREADY
+            self.sandboxes[s.id] = s
+        for name in os.listdir(os.path.join(self.state_dir, "containers")):
+            if not name.endswith(".json"):
+                continue
+            try:
+                d = json.load(open(os.path.join(self.state_dir, "containers", name)))
+            except (OSError, ValueError):
+                continue
+            c = Container(d["id"], d["sandbox_id"], d["name"], d["attempt"], d["image"], d["image_ref"], d["argv"], d["env"],
+                          d["cwd"], d["log_path"], d["labels"], d["annotations"], d["mounts"], d["devices"], d["handler"],
+                          d["resources"])
+            for k in ("state", "created_at", "started_at", "finished_at", "exit_code", "reason", "message", "pid"):
+                setattr(c, k, d[k])
+            self.containers[c.id] = c
+            if c.state == C.CONTAINER_RUNNING:
+                if _alive(c.pid):
+                    t = asyncio.create_task(self._adopt(c))
+                    self._adopt_tasks.add(t)
+                    t.add_done_callback(self._adopt_tasks.discard)
+                else:
+                    self._finish(c, self._exit_code_file(c))
+        log.info("recovered %d sandboxes, %d containers", len(self.sandboxes), len(self.containers))
+
+    def _exit_code_file(self, c) -> int | None:
+        try:
+            with open(os.path.join(self.state_dir, "containers", c.id + ".exit")) as f:
+                return int(f.read().strip())
+        except (OSError, ValueError):
+            return None
+
+    async def _adopt(self, c: Container):
+        while _alive(c.pid):
+            await asyncio.sleep(0.2)
+        self._finish(c, self._exit_code_file(c))
+
+    # ----------------------------------------------------------------- sandboxes
+    async def run_sandbox(self, cfg) -> str:
+        sid = uuid.uuid4().hex
+        meta = {"name": cfg.metadata.name, "uid": cfg.metadata.uid, "namespace": cfg.metadata.namespace,
+                "attempt": cfg.metadata.attempt}
+        log_dir = cfg.log_directory or os.path.join(self.state_dir, "logs", sid)
+        os.makedirs(log_dir, exist_ok=True)
+        s = Sandbox(sid, cfg.SerializeToString(), meta, dict(cfg.labels), dict(cfg.annotations), log_dir)
+        os.makedirs(os.path.join(self.state_dir, "rootfs", sid), exist_ok=True)
+        proc = await asyncio.create_subprocess_exec(self.pause_bin, stdin=asyncio.subprocess.DEVNULL,
+                                                    stdout=asyncio.subprocess.DEVNULL, stderr=asyncio.subprocess.DEVNULL,
+                                                    start_new_session=True)
+        s.proc, s.pid = proc, proc.pid
+        self.sandboxes[sid] = s
+        self._ckpt("sandboxes", s)
+        return sid
+
+    async def stop_sandbox(self, sid: str):
+        s = self.sandboxes.get(sid)
+        if s is None:
+            return
+        await asyncio.gather(*(self.stop_container(c.id, 2) for c in list(self.containers.values()) if c.sandbox_id == sid))
+        if s.pid and _alive(s.pid):
+            try:
+                os.kill(s.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+            if s.proc is not None:
+                try:
+                    await asyncio.wait_for(s.proc.wait(), 2)
+                except asyncio.TimeoutError:
+                    os.kill(s.pid, signal.SIGKILL)
+        s.state = C.SANDBOX_NOTREADY
+        self._ckpt("sandboxes", s)
+
+    async def remove_sandbox(self, sid: str):
+        s = self.sandboxes.get(sid)
+        if s is None:
+            return
+        if s.state == C.SANDBOX_READY:
+            await self.stop_sandbox(sid)
+        for c in [c for c in self.containers.values() if c.sandbox_id == sid]:
+            await self.remove_container(c.id)
+        self.sandboxes.pop(sid, None)
+        self._unckpt("sandboxes", sid)
+        shutil.rmtree(os.path.join(self.state_dir, "rootfs", sid), ignore_errors=True)
+
+    # --------------------------------------------------------------- containers
+    def create_container(self, sid: str, cfg, sandbox_cfg) -> str:
+        s = self.sandboxes.get(sid)
+        if s is None or s.state != C.SANDBOX_READY:
+            raise LookupError(f"sandbox {sid} not found or not ready")
+        res = self.images.resolve(cfg.image.image)
+        if res is None:
+            raise LookupError(f"image {cfg.image.image!r} not present (PullImage first)")
+        iname, ispec = res
+        entry = list(cfg.command) or list(ispec.get("entrypoint") or [])
+        args = list(cfg.args) if (cfg.args or cfg.command) else list(ispec.get("cmd") or [])
+        argv = entry + args
+        if not argv:
+            raise ValueError("no command specified and the image has no entrypoint")
+        env = {k: v for k, v in os.environ.items() if k not in SCRUB_ENV}
+        env.update(ispec.get("env") or {})
+        for kv in cfg.envs:
+            env[kv.key] = kv.value
+        devices = [{"container_path": d.container_path, "host_path": d.host_path, "permissions": d.permissions}
+                   for d in cfg.devices]
+        has_gpu = any(d["host_path"].endswith("/kfd") for d in devices)
+        if not has_gpu:
+            env.pop("ROCR_VISIBLE_DEVICES", None)
+            env["HIP_VISIBLE_DEVICES"] = "-1"  # non-GPU containers see no GPU
+        for d in devices:
+            if not os.path.exists(d["host_path"]) and self.isolation == "namespaces":
+                raise FileNotFoundError(f"device {d['host_path']} does not exist on this host")
+        tags = [iname]
+        handler = self.hooks.get_runtime(tags, dict(cfg.annotations), dict(sandbox_cfg.annotations) if sandbox_cfg else {})
+        if not handler:
+            handler = "rocm" if has_gpu else "default"
+        cid = uuid.uuid4().hex
+        root = os.path.join(self.state_dir, "rootfs", sid, cfg.metadata.name)
+        os.makedirs(root, exist_ok=True)
+        cwd = cfg.working_dir or ispec.get("workdir") or root
+        if not os.path.isdir(cwd):
+            cwd = root
+        log_path = os.path.join(s.log_dir, cfg.log_path) if cfg.log_path else os.path.join(s.log_dir, f"{cfg.metadata.name}_{cfg.metadata.attempt}.log")
+        os.makedirs(os.path.dirname(log_path), exist_ok=True)
+        mounts = [{"container_path": m.container_path, "host_path": m.host_path, "readonly": m.readonly} for m in cfg.mounts]
+        # without a mount namespace, expose volumes as symlinks under the container's root
+        for mnt in mounts:
+            if self.isolation != "namespaces" and mnt["container_path"].startswith("/"):
+                link = os.path.join(root, mnt["container_path"].lstrip("/"))
+                os.makedirs(os.path.dirname(link), exist_ok=True)
+                if not os.path.lexists(link):
+                    os.symlink(mnt["host_path"], link)
+        env["AMDKUBE_ROOTFS"] = root
+        r = cfg.linux.resources if cfg.HasField("linux") else None
+        resources = {"cpu_quota": r.cpu_quota, "cpu_period": r.cpu_period, "memory_limit": r.memory_limit_in_bytes} if r else {}
+        c = Container(cid, sid, cfg.metadata.name, cfg.metadata.attempt, cfg.image.image, self.images.image_id(iname), argv,
+                      env, cwd, log_path, dict(cfg.labels), dict(cfg.annotations), mounts, devices, handler, resources)
+        self.containers[cid] = c
+        self._ckpt("containers", c)
+        self._emit(c, C.CONTAINER_CREATED_EVENT)
+        return cid
+
+    def _launch_argv(self, c: Container) -> list[str]:
+        if self.isolation != "namespaces":
+            return c.argv
+        keep = [d["host_path"] for d in c.devices if "/dri/" in d["host_path"]]
+        cg = os.path.join(self.cgroup_root, c.sandbox_id, c.id)
+        a = [self.nsexec_bin, "--dev-root", self.dev_root, "--cgroup", cg]
+        for k in keep:
+            a += ["--keep", k]
+        if c.resources.get("memory_limit"):
+            a += ["--memory-max", str(c.resources["memory_limit"])]
+        if c.resources.get("cpu_quota") and c.resources.get("cpu_period"):
+            a += ["--cpu-max", f"{c.resources['cpu_quota']} {c.resources['cpu_period']}"]
+        if not any(d["host_path"].endswith("/kfd") for d in c.devices):
+            a += ["--hide-kfd"]
+        return a + ["--"] + c.argv
+
+    async def start_container(self, cid: str):
+        c = self.containers.get(cid)
+        if c is None:
+            raise LookupError(f"container {cid} not found")
+        if c.state != C.CONTAINER_CREATED:
+            raise ValueError(f"container {cid} is not in created state")
+        logf = open(c.log_path, "ab", buffering=0)
+        try:
+            proc = await asyncio.create_subprocess_exec(*self._launch_argv(c), stdin=asyncio.subprocess.DEVNULL, stdout=logf,
+                                                        stderr=logf, env=c.env, cwd=c.cwd, start_new_session=True)
+        except (OSError, ValueError) as e:
+            logf.close()
+            c.state, c.exit_code, c.reason, c.message = C.CONTAINER_EXITED, 128, "StartError", str(e)
+            c.finished_at = now_ns()
+            self._ckpt("containers", c)
+            raise
+        logf.close()
+        c.proc, c.pid = proc, proc.pid
+        c.state, c.started_at = C.CONTAINER_RUNNING, now_ns()
+        self.started += 1
+        self._ckpt("containers", c)
+        self._emit(c, C.CONTAINER_STARTED_EVENT)
+        c.waiter = asyncio.create_task(self._wait(c))
+
+    async def _wait(self, c: Container):
+        rc = await c.proc.wait()
+        try:
+            with open(os.path.join(self.state_dir, "containers", c.id + ".exit"), "w") as f:
+                f.write(str(rc))
+        except OSError:
+            pass
+        self._finish(c, rc)
+
+    def _finish(self, c: Container, rc):
+        if c.state == C.CONTAINER_EXITED:
+            return
+        c.state = C.CONTAINER_EXITED
+        c.finished_at = now_ns()
+        if rc is None:
+            c.exit_code, c.reason = 255, "ContainerStatusUnknown"
+        elif rc < 0:
+            c.exit_code, c.reason = 128 - rc, "Error"
+            if -rc == signal.SIGKILL:
+                c.reason = "OOMKilled" if False else "Killed"
+        else:
+            c.exit_code, c.reason = rc, ("Completed" if rc == 0 else "Error")
+        self._ckpt("containers", c)
+        self._emit(c, C.CONTAINER_STOPPED_EVENT)
+
+    async def stop_container(self, cid: str, timeout: int = 10):
+        c = self.containers.get(cid)
+        if c is None or c.state != C.CONTAINER_RUNNING:
+            return
+        try:
+            os.killpg(c.pid, signal.SIGTERM)
+        except (ProcessLookupError, PermissionError):
+            pass
+        deadline = time.monotonic() + max(0, timeout)
+        while c.state == C.CONTAINER_RUNNING and time.monotonic() < deadline:
+            await asyncio.sleep(0.02)
+        if c.state == C.CONTAINER_RUNNING:
+            try:
+                os.killpg(c.pid, signal.SIGKILL)
+            except (ProcessLookupError, PermissionError):
+                pass
+            if c.waiter is not None:
+                try:
+                    await asyncio.wait_for(asyncio.shield(c.waiter), 5)
+                except asyncio.TimeoutError:
+                    pass
+            else:
+                self._finish(c, -signal.SIGKILL)
+        try:  # reap stragglers of the group even after the leader exited
+            os.killpg(c.pid, signal.SIGKILL)
+        except (ProcessLookupError, PermissionError):
+            pass
+
+    async def remove_container(self, cid: str):
+        c = self.containers.get(cid)
+        if c is None:
+            return
+        if c.state == C.CONTAINER_RUNNING:
+            await self.stop_container(cid, 0)
+        self.containers.pop(cid, None)
+        self._unckpt("containers", cid)
+        self._emit(c, C.CONTAINER_DELETED_EVENT)
+        try:
+            os.unlink(os.path.join(self.state_dir, "containers", cid + ".exit"))
+        except FileNotFoundError:
+            pass
+
+    async def exec_sync(self, cid: str, cmd: list[str], timeout: int):
+        c = self.containers.get(cid)
+        if c is None or c.state != C.CONTAINER_RUNNING:
+            raise LookupError(f"container {cid} is not running")
+        p = await asyncio.create_subprocess_exec(*cmd, env=c.env, cwd=c.cwd, stdout=asyncio.subprocess.PIPE,
+                                                 stderr=asyncio.subprocess.PIPE)
+        try:
+            out, err = await asyncio.wait_for(p.communicate(), timeout or None)
+        except asyncio.TimeoutError:
+            p.kill()
+            return b"", b"timeout", 124
+        return out, err, p.returncode
+
+
+def _alive(pid: int) -> bool:
+    if not pid:
+        return False
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+    try:  # zombies count as dead
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().split(")")[-1].split()[0] != "Z"
+    except OSError:
+        return False
+
+
+def _proc_stats(pid: int) -> tuple[int, int]:
+    """(cpu ns, rss bytes) of a process (best effort)."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            parts = f.read().split(")")[-1].split()
+        tck = os.sysconf("SC_CLK_TCK")
+        cpu = (int(parts[11]) + int(parts[12])) * 1_000_000_000 // tck
+        rss = int(parts[21]) * os.sysconf("SC_PAGE_SIZE")
+        return cpu, rss
+    except (OSError, IndexError, ValueError):
+        return 0, 0
+
+
+def _abort(ctx, e):
+    code = grpc.StatusCode.NOT_FOUND if isinstance(e, LookupError) else (
+        grpc.StatusCode.FAILED_PRECONDITION if isinstance(e, (ValueError, FileNotFoundError)) else grpc.StatusCode.UNKNOWN)
+    return ctx.abort(code, str(e))
+
+
+class _Runtime:
+    def __init__(self, r: RocShim):
+        self.r = r
+
+    async def Version(self, req, ctx):
+        return C.VersionResponse(version=API_VERSION, runtime_name=RUNTIME_NAME, runtime_version=RUNTIME_VERSION,
+                                 runtime_api_version="v1alpha1")
+
+    async def Status(self, req, ctx):
+        conds = [C.RuntimeCondition(type="RuntimeReady", status=True), C.RuntimeCondition(type="NetworkReady", status=True)]
+        return C.StatusResponse(status=C.RuntimeStatus(conditions=conds),
+                                info={"isolation": self.r.isolation, "handlers": ",".join(sorted(HANDLERS))} if req.verbose else {})
+
+    async def RunPodSandbox(self, req, ctx):
+        try:
+            return C.RunPodSandboxResponse(pod_sandbox_id=await self.r.run_sandbox(req.config))
+        except Exception as e:
+            await _abort(ctx, e)
+
+    async def StopPodSandbox(self, req, ctx):
+        await self.r.stop_sandbox(req.pod_sandbox_id)
+        return C.StopPodSandboxResponse()
+
+    async def RemovePodSandbox(self, req, ctx):
+        await self.r.remove_sandbox(req.pod_sandbox_id)
+        return C.RemovePodSandboxResponse()
+
+    def _sb_meta(self, s):
+        return C.PodSandboxMetadata(name=s.meta["name"], uid=s.meta["uid"], namespace=s.meta["namespace"],
+                                    attempt=s.meta.get("attempt", 0))
+
+    async def PodSandboxStatus(self, req, ctx):
+        s = self.r.sandboxes.get(req.pod_sandbox_id)
+        if s is None:
+            await ctx.abort(grpc.StatusCode.NOT_FOUND, f"sandbox {req.pod_sandbox_id} not found")
+        if s.state == C.SANDBOX_READY and not _alive(s.pid):
+            s.state = C.SANDBOX_NOTREADY
+        st = C.PodSandboxStatus(id=s.id, metadata=self._sb_meta(s), state=s.state, created_at=s.created_at,
+                                network=C.PodSandboxNetworkStatus(ip="127.0.0.1"), labels=s.labels, annotations=s.annotations)
+        return C.PodSandboxStatusResponse(status=st, info={"pid": str(s.pid)} if req.verbose else {})
+
+    async def ListPodSandbox(self, req, ctx):
+        f = req.filter if req.HasField("filter") else None
+        out = []
+        for s in self.r.sandboxes.values():
+            if f is not None:
+                if f.id and f.id != s.id:
+                    continue
+                if f.HasField("state") and f.state.state != s.state:
+                    continue
+                if any(s.labels.get(k) != v for k, v in f.label_selector.items()):
+                    continue
+            out.append(C.PodSandbox(id=s.id, metadata=self._sb_meta(s), state=s.state, created_at=s.created_at,
+                                    labels=s.labels, annotations=s.annotations))
+        return C.ListPodSandboxResponse(items=out)
+
+    async def CreateContainer(self, req, ctx):
+        try:
+            return C.CreateContainerResponse(container_id=self.r.create_container(req.pod_sandbox_id, req.config,
+                                                                                  req.sandbox_config))
+        except Exception as e:
+            await _abort(ctx, e)
+
+    async def StartContainer(self, req, ctx):
+        try:
+            await self.r.start_container(req.container_id)
+        except Exception as e:
+            await _abort(ctx, e)
+        return C.StartContainerResponse()
+
+    async def StopContainer(self, req, ctx):
+        await self.r.stop_container(req.container_id, req.timeout)
+        return C.StopContainerResponse()
+
+    async def RemoveContainer(self, req, ctx):
+        await self.r.remove_container(req.container_id)
+        return C.RemoveContainerResponse()
+
+    def _c(self, c):
+        return C.Container(id=c.id, pod_sandbox_id=c.sandbox_id, metadata=C.ContainerMetadata(name=c.name, attempt=c.attempt),
+                           image=C.ImageSpec(image=c.image), image_ref=c.image_ref, state=c.state, created_at=c.created_at,
+                           labels=c.labels, annotations=c.annotations)
+
+    async def ListContainers(self, req, ctx):
+        f = req.filter if req.HasField("filter") else None
+        out = []
+        for c in self.r.containers.values():
+            if f is not None:
+                if f.id and f.id != c.id:
+                    continue
+                if f.pod_sandbox_id and f.pod_sandbox_id != c.sandbox_id:
+                    continue
+                if f.HasField("state") and f.state.state != c.state:
+                    continue
+                if any(c.labels.get(k) != v for k, v in f.label_selector.items()):
+                    continue
+            out.append(self._c(c))
+        return C.ListContainersResponse(containers=out)
+
+    async def ContainerStatus(self, req, ctx):
+        c = self.r.containers.get(req.container_id)
+        if c is None:
+            await ctx.abort(grpc.StatusCode.NOT_FOUND, f"container {req.container_id} not found")
+        st = C.ContainerStatus(id=c.id, metadata=C.ContainerMetadata(name=c.name, attempt=c.attempt), state=c.state,
+                               created_at=c.created_at, started_at=c.started_at, finished_at=c.finished_at,
+                               exit_code=c.exit_code, image=C.ImageSpec(image=c.image), image_ref=c.image_ref,
+                               reason=c.reason, message=c.message, labels=c.labels, annotations=c.annotations,
+                               mounts=[C.Mount(container_path=m["container_path"], host_path=m["host_path"], readonly=m["readonly"])
+                                       for m in c.mounts], log_path=c.log_path)
+        info = {"pid": str(c.pid), "handler": c.handler, "devices": json.dumps(c.devices)} if req.verbose else {}
+        return C.ContainerStatusResponse(status=st, info=info)
+
+    async def UpdateContainerResources(self, req, ctx):
+        c = self.r.containers.get(req.container_id)
+        if c is not None:
+            c.resources = {"cpu_quota": req.linux.cpu_quota, "cpu_period": req.linux.cpu_period,
+                           "memory_limit": req.linux.memory_limit_in_bytes}
+        return C.UpdateContainerResourcesResponse()
+
+    async def ExecSync(self, req, ctx):
+        try:
+            out, err, rc = await self.r.exec_sync(req.container_id, list(req.cmd), req.timeout)
+        except Exception as e:
+            await _abort(ctx, e)
+        return C.ExecSyncResponse(stdout=out, stderr=err, exit_code=rc)
+
+    def _stats(self, c):
+        cpu, rss = _proc_stats(c.pid) if c.state == C.CONTAINER_RUNNING else (0, 0)
+        ts = now_ns()
+        return C.ContainerStats(attributes=C.ContainerAttributes(id=c.id, metadata=C.ContainerMetadata(name=c.name, attempt=c.attempt),
+                                                                 labels=c.labels, annotations=c.annotations),
+                                cpu=C.CpuUsage(timestamp=ts, usage_core_nano_seconds=C.UInt64Value(value=cpu)),
+                                memory=C.MemoryUsage(timestamp=ts, working_set_bytes=C.UInt64Value(value=rss)))
+
+    async def ContainerStats(self, req, ctx):
+        c = self.r.containers.get(req.container_id)
+        if c is None:
+            await ctx.abort(grpc.StatusCode.NOT_FOUND, "not found")
+        return C.ContainerStatsResponse(stats=self._stats(c))
+
+    async def ListContainerStats(self, req, ctx):
+        f = req.filter if req.HasField("filter") else None
+        out = [self._stats(c) for c in self.r.containers.values()
+               if c.state == C.CONTAINER_RUNNING and (f is None or ((not f.id or f.id == c.id) and
+                                                                    (not f.pod_sandbox_id or f.pod_sandbox_id == c.sandbox_id)))]
+        return C.ListContainerStatsResponse(stats=out)
+
+    async def UpdateRuntimeConfig(self, req, ctx):
+        return C.UpdateRuntimeConfigResponse()
+
+    async def GetContainerEvents(self, req, ctx):
+        q: asyncio.Queue = asyncio.Queue()
+        self.r._event_streams.add(q)
+        try:
+            while True:
+                cid, sid, etype, ts = await q.get()
+                yield C.ContainerEventResponse(container_id=cid, container_event_type=etype, created_at=ts,
+                                               pod_sandbox_status=C.PodSandboxStatus(id=sid))
+        finally:
+            self.r._event_streams.discard(q)
+
+
+class _Images:
+    def __init__(self, r: RocShim):
+        self.r = r
+
+    def _img(self, name, iid):
+        return C.Image(id=iid, repo_tags=[name], size=0)
+
+    async def ListImages(self, req, ctx):
+        return C.ListImagesResponse(images=[self._img(n, i) for n, i, _ in self.r.images.list()])
+
+    async def ImageStatus(self, req, ctx):
+        res = self.r.images.resolve(req.image.image)
+        if res is None:
+            return C.ImageStatusResponse()
+        return C.ImageStatusResponse(image=self._img(res[0], self.r.images.image_id(res[0])))
+
+    async def PullImage(self, req, ctx):
+        try:
+            return C.PullImageResponse(image_ref=self.r.images.pull(req.image.image))
+        except KeyError as e:
+            await ctx.abort(grpc.StatusCode.NOT_FOUND, str(e))
+
+    async def RemoveImage(self, req, ctx):
+        self.r.images.remove(req.image.image)
+        return C.RemoveImageResponse()
+
+    async def ImageFsInfo(self, req, ctx):
+        st = os.statvfs(self.r.state_dir)
+        used = (st.f_blocks - st.f_bfree) * st.f_frsize
+        return C.ImageFsInfoResponse(image_filesystems=[C.FilesystemUsage(
+            timestamp=now_ns(), storage_id=C.StorageIdentifier(uuid="rocshim"), used_bytes=C.UInt64Value(value=used),
+            inodes_used=C.UInt64Value(value=st.f_files - st.f_ffree))])

@@ -1,0 +1,88 @@
+"""Device-granular extended-resource allocation (the fork's scheduler core).
+
+Reference: plugin/pkg/scheduler/core/extended_resources.go — GetExtendedResources (:42-81)
+runs after the predicates for every surviving node, hasExtendedResources (:83-111) allocates
+each pod ExtendedResource from a copy of the node's available devices, allocateResources
+(:113-150) takes the first N devices whose Attributes match the selector (isDeviceAMatch,
+:152-167) in Go-map (random) order; failures become "Insufficient <res>".
+
+amdkube keeps the contract (output: ExtendedResourceBinding per node, i.e. {pres name:
+{"resources": [ids]}}) and changes the choice: among the matching healthy free devices the
+subset is chosen by the native xGMI/NUMA topology allocator (amdkube.ops.topology) when the
+node publishes a topology, otherwise deterministically by device ID. Feasibility is a count
+check, so the (more expensive) subset choice runs only for the selected host.
+"""
+from __future__ import annotations
+
+from ..ops import topology as topo
+
+
+def matching_free(pi, ni, rname, selector, exclude=()) -> list[str]:
+    avail = ni.available_devices(rname)
+    if not avail:
+        return []
+    if selector.empty():
+        return [d for d in avail if d not in exclude]
+    return [d for d, dev in avail.items() if d not in exclude and selector.matches(dev.get("attributes") or {})]
+
+
+def fits(pi, ni) -> tuple[bool, list[str]]:
+    if pi.ext_error:
+        return False, [pi.ext_error]
+    if not pi.ext:
+        return True, []
+    need: dict[str, int] = {}
+    for _, rname, n, sel in pi.ext:
+        cand = matching_free(pi, ni, rname, sel)
+        need[rname] = need.get(rname, 0) + n
+        if len(cand) < n or len(ni.available_devices(rname)) < need[rname]:
+            return False, [f"Insufficient {rname}"]
+    return True, []
+
+
+def allocate(pi, ni, use_topology: bool = True) -> dict | None:
+    """ExtendedResourceBinding for this node, or None if it does not fit."""
+    if pi.ext_error:
+        return None
+    binding = {}
+    taken: set[str] = set()
+    t = ni.topology() if use_topology else None
+    for pname, rname, n, sel in pi.ext:
+        cand = matching_free(pi, ni, rname, sel, taken)
+        if len(cand) < n:
+            return None
+        chosen = None
+        if t is not None:
+            ids, index, numa, link = t
+            if all(d in index for d in cand):
+                free_all = [index[d] for d in ni.available_devices(rname) if d in index and d not in taken]
+                sel_idx, cost = topo.select([index[d] for d in cand], n, link, numa, free_all)
+                if len(sel_idx) == n:
+                    chosen = [ids[i] for i in sel_idx]
+        if chosen is None:
+            chosen = sorted(cand)[:n]
+        taken.update(chosen)
+        binding[pname] = {"resources": chosen}
+    return binding
+
+
+def topology_score(pi, ni) -> float:
+    """0..10: how well the pod's GPUs can be placed on this node (GPUTopologyPriority)."""
+    t = ni.topology()
+    if not pi.ext:
+        return 10.0 if not ni.devices else 0.0
+    if t is None:
+        return 5.0
+    ids, index, numa, link = t
+    total = 0.0
+    for _, rname, n, sel in pi.ext:
+        cand = matching_free(pi, ni, rname, sel)
+        if not all(d in index for d in cand):
+            return 5.0
+        free_all = [index[d] for d in ni.available_devices(rname) if d in index]
+        total += topo.score([index[d] for d in cand], n, link, numa, free_all)
+    s = total / len(pi.ext)
+    # best fit across nodes: prefer the node whose free GPUs are closest to the request
+    free = sum(len(ni.available_devices(r)) for r in {r for _, r, _, _ in pi.ext})
+    slack = max(0, free - pi.gpu_count)
+    return max(0.0, min(10.0, 0.8 * s + 2.0 * (1.0 - slack / max(1.0, float(free)))))

@@ -1,0 +1,309 @@
+"""kube-scheduler equivalent: watch → queue → schedule → assume (with devices) → async bind.
+
+Reference: plugin/pkg/scheduler/scheduler.go:170-180 (Run: scheduleOne loop), :430-497
+(scheduleOne: schedule, assume, bind in a goroutine; the fork puts the chosen device IDs into
+Binding.Target.ExtendedResources at :483-491), :194/:425 (FailedScheduling / Scheduled
+events); factory/factory.go:554-830 (informer handlers: unscheduled pods → queue, assigned
+non-terminated pods → cache, node events → cache + MoveAllToActiveQueue); metrics
+plugin/pkg/scheduler/metrics/metrics.go:34-50; policy file & algorithm providers
+(plugin/cmd/kube-scheduler/app/server.go:218-290, algorithmprovider/defaults).
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import time
+
+from aiohttp import web
+
+from ..api import meta as m
+from ..api.helpers import is_pod_terminal
+from ..client import Client, EventRecorder, Informer, LeaderElector
+from ..utils import profiling
+from ..utils.features import FeatureGate
+from ..utils.metrics import CONTENT_TYPE, MICRO_BUCKETS, Counter, Histogram, new_registry, render
+from .cache import SchedulerCache
+from .extender import HTTPExtender
+from .generic import FitError, GenericScheduler
+from .predicates import DEFAULT_PREDICATES
+from .priorities import DEFAULT_PRIORITIES
+from .queue import SchedulingQueue
+
+log = logging.getLogger("amdkube.scheduler")
+
+PROVIDERS = {
+    "DefaultProvider": (DEFAULT_PREDICATES, DEFAULT_PRIORITIES),
+    "ClusterAutoscalerProvider": (DEFAULT_PREDICATES, {**{k: v for k, v in DEFAULT_PRIORITIES.items() if k != "LeastRequestedPriority"},
+                                                       "MostRequestedPriority": 1}),
+}
+
+
+def load_policy(path_or_dict) -> tuple[list, dict, list]:
+    pol = path_or_dict
+    if isinstance(path_or_dict, str):
+        with open(path_or_dict) as f:
+            pol = json.load(f)
+    preds = [p["name"] for p in pol.get("predicates") or []] if "predicates" in pol else list(DEFAULT_PREDICATES)
+    prios = {p["name"]: int(p.get("weight", 1)) for p in pol.get("priorities") or []} if "priorities" in pol else dict(DEFAULT_PRIORITIES)
+    return preds, prios, list(pol.get("extenders") or [])
+
+
+class Scheduler:
+    def __init__(self, client: Client, scheduler_name: str = "default-scheduler", policy=None,
+                 algorithm_provider: str = "DefaultProvider", feature_gates: str = "", leader_elect: bool = False,
+                 identity: str | None = None, port: int | None = None, disable_preemption: bool = False,
+                 bind_concurrency: int = 256):
+        self.client = client
+        self.name = scheduler_name
+        self.gates = FeatureGate(feature_gates)
+        if policy is not None:
+            preds, prios, exts = load_policy(policy)
+        else:
+            preds, prios = PROVIDERS[algorithm_provider]
+            exts = []
+        if not self.gates("GPUTopologyScheduling"):
+            prios = {k: v for k, v in prios.items() if k != "GPUTopologyPriority"}
+        self.extenders = [HTTPExtender(e) for e in exts]
+        self.cache = SchedulerCache()
+        self.algo = GenericScheduler(self.cache, preds, prios, self.extenders, use_topology=self.gates("GPUTopologyScheduling"))
+        self.queue = SchedulingQueue(self.gates("PodPriority"))
+        self.recorder = EventRecorder(client, self.name)
+        self.leader_elect = leader_elect
+        self.identity = identity or f"{self.name}-{id(self):x}"
+        self.port = port
+        self.disable_preemption = disable_preemption
+        self.bind_sem = asyncio.Semaphore(bind_concurrency)
+        self.metrics = new_registry()
+        r = self.metrics
+        self.m_e2e = Histogram("scheduler_e2e_scheduling_latency_microseconds", "E2e scheduling latency (scheduling algorithm + binding)", buckets=MICRO_BUCKETS, registry=r)
+        self.m_algo = Histogram("scheduler_scheduling_algorithm_latency_microseconds", "Scheduling algorithm latency", buckets=MICRO_BUCKETS, registry=r)
+        self.m_bind = Histogram("scheduler_binding_latency_microseconds", "Binding latency", buckets=MICRO_BUCKETS, registry=r)
+        self.m_attempts = Counter("scheduler_schedule_attempts", "Number of attempts to schedule pods, by the result.", ["result"], registry=r)
+        self.m_preempt = Counter("scheduler_total_preemption_attempts", "Total preemption attempts in the cluster till now", registry=r)
+        self.pod_inf = self.node_inf = None
+        self._tasks: list[asyncio.Task] = []
+        self._binds: set[asyncio.Task] = set()
+        self.scheduled = 0
+        self.failed = 0
+        self.bind_errors = 0
+        self._runner = None
+
+    # ----------------------------------------------------------- informers
+    def _responsible(self, pod) -> bool:
+        return (pod.get("spec") or {}).get("schedulerName", "default-scheduler") == self.name
+
+    def _unassigned(self, pod) -> bool:
+        return not (pod.get("spec") or {}).get("nodeName") and not is_pod_terminal(pod) and \
+            not (pod.get("metadata") or {}).get("deletionTimestamp") and self._responsible(pod)
+
+    @staticmethod
+    def _assigned_live(pod) -> bool:
+        return bool((pod.get("spec") or {}).get("nodeName")) and not is_pod_terminal(pod)
+
+    def _on_pod_add(self, pod):
+        if self._assigned_live(pod):
+            self.cache.add_pod(pod)
+        elif self._unassigned(pod):
+            self.queue.add(pod)
+
+    def _on_pod_update(self, old, pod):
+        if self._assigned_live(pod):
+            self.cache.update_pod(old, pod)
+            self.queue.delete(pod)
+        elif (pod.get("spec") or {}).get("nodeName"):
+            # bound pod went terminal → its resources (incl. GPUs) are free again
+            if self._assigned_live(old) or self.cache.is_assumed(pod) or m.key_of(pod) in self.cache.pod_states:
+                self.cache.remove_pod(pod)
+                self.queue.move_all_to_active()
+        elif self._unassigned(pod):
+            self.queue.update(pod)
+        else:
+            self.queue.delete(pod)
+
+    def _on_pod_delete(self, pod):
+        if (pod.get("spec") or {}).get("nodeName"):
+            self.cache.remove_pod(pod)
+            self.queue.move_all_to_active()
+        else:
+            self.queue.delete(pod)
+
+    def _on_node(self, node):
+        self.cache.add_node(node)
+        self.queue.move_all_to_active()
+
+    def _on_node_update(self, old, node):
+        self.cache.update_node(node)
+        if (old.get("status") or {}).get("extendedResources") != (node.get("status") or {}).get("extendedResources") or \
+                (old.get("spec") or {}) != (node.get("spec") or {}) or \
+                (old.get("status") or {}).get("allocatable") != (node.get("status") or {}).get("allocatable"):
+            self.queue.move_all_to_active()
+
+    # ------------------------------------------------------------ lifecycle
+    async def start(self):
+        self.recorder.start()
+        if self.port is not None:
+            await self._serve()
+        if self.leader_elect:
+            le = LeaderElector(self.client, "kube-scheduler", self.identity)
+            self._tasks.append(asyncio.create_task(le.run(self._run_informers_and_loop)))
+        else:
+            await self._start_informers()
+            self._tasks.append(asyncio.create_task(self.run(), name="schedule-loop"))
+            self._tasks.append(asyncio.create_task(self._housekeeping(), name="sched-housekeeping"))
+        return self
+
+    async def _run_informers_and_loop(self):
+        await self._start_informers()
+        self._tasks.append(asyncio.create_task(self._housekeeping()))
+        await self.run()
+
+    async def _start_informers(self):
+        self.node_inf = Informer(self.client, "nodes")
+        self.node_inf.add_handler(on_add=self._on_node, on_update=self._on_node_update,
+                                  on_delete=lambda n: self.cache.remove_node(n))
+        self.pod_inf = Informer(self.client, "pods")
+        self.pod_inf.add_handler(on_add=self._on_pod_add, on_update=self._on_pod_update, on_delete=self._on_pod_delete)
+        self.node_inf.start()
+        await self.node_inf.wait_synced(30)
+        self.pod_inf.start()
+        await self.pod_inf.wait_synced(30)
+
+    async def stop(self):
+        for t in self._tasks:
+            t.cancel()
+        for t in list(self._binds):
+            t.cancel()
+        for inf in (self.pod_inf, self.node_inf):
+            if inf:
+                await inf.stop()
+        await self.recorder.stop()
+        for e in self.extenders:
+            await e.close()
+        if self._runner:
+            await self._runner.cleanup()
+
+    async def _housekeeping(self):
+        while True:
+            await asyncio.sleep(1.0)
+            self.cache.cleanup_expired()
+
+    async def _serve(self):
+        app = web.Application()
+
+        async def healthz(r):
+            return web.Response(text="ok")
+
+        async def metrics(r):
+            return web.Response(body=render(self.metrics), headers={"Content-Type": CONTENT_TYPE})
+        app.router.add_get("/healthz", healthz)
+        app.router.add_get("/metrics", metrics)
+        profiling.add_routes(app)
+        self._runner = web.AppRunner(app, access_log=None)
+        await self._runner.setup()
+        site = web.TCPSite(self._runner, "127.0.0.1", self.port)
+        await site.start()
+        self.port = site._server.sockets[0].getsockname()[1]
+
+    # ------------------------------------------------------------ main loop
+    async def run(self):
+        while True:
+            pod = await self.queue.pop()
+            try:
+                await self.schedule_one(pod)
+            except asyncio.CancelledError:
+                raise
+            except Exception as e:
+                log.exception("scheduling %s crashed: %r", m.key_of(pod), e)
+                self.queue.add_unschedulable(pod)
+
+    async def schedule_one(self, pod: dict):
+        key = m.key_of(pod)
+        cur = self.pod_inf.get(key) if self.pod_inf else pod
+        if cur is None or not self._unassigned(cur) or self.cache.is_assumed(cur):
+            return
+        pod = cur
+        t0 = time.perf_counter()
+        try:
+            host, binding = await self.algo.schedule(pod)
+        except FitError as e:
+            self.failed += 1
+            self.m_attempts.labels("unschedulable").inc()
+            self.recorder.event(pod, "Warning", "FailedScheduling", str(e))
+            asyncio.create_task(self._mark_unschedulable(pod, str(e)))
+            if not self.disable_preemption and self.gates("PodPriority") and int((pod.get("spec") or {}).get("priority") or 0) > 0:
+                await self._preempt(pod)
+            self.queue.add_unschedulable(pod)
+            return
+        self.m_algo.observe((time.perf_counter() - t0) * 1e6)
+        # assume: nodeName + chosen devices (fix #1: devices are reserved before the bind)
+        assumed = json.loads(json.dumps(pod))
+        assumed["spec"]["nodeName"] = host
+        if binding and self.gates("ReserveDevicesOnAssume"):
+            for pres in assumed["spec"].get("extendedResources") or []:
+                if pres.get("name") in binding:
+                    pres["assigned"] = list(binding[pres["name"]]["resources"])
+        try:
+            self.cache.assume_pod(assumed)
+        except KeyError:
+            return
+        t = asyncio.create_task(self._bind(pod, assumed, host, binding, t0))
+        self._binds.add(t)
+        t.add_done_callback(self._binds.discard)
+
+    async def _bind(self, pod, assumed, host, binding, t0):
+        async with self.bind_sem:
+            tb = time.perf_counter()
+            try:
+                bound_by_ext = False
+                for ext in self.extenders:
+                    if ext.bind_verb:
+                        await ext.bind(pod, host)
+                        bound_by_ext = True
+                        break
+                if not bound_by_ext:
+                    await self.client.bind(m.namespace_of(pod), m.name_of(pod), host, binding or None, uid=m.uid_of(pod))
+            except Exception as e:
+                self.bind_errors += 1
+                self.m_attempts.labels("error").inc()
+                self.cache.forget_pod(assumed)
+                log.info("binding %s to %s rejected: %s", m.key_of(pod), host, e)
+                self.recorder.event(pod, "Warning", "FailedScheduling", f"Binding rejected: {e}")
+                if not (isinstance(e, m.StatusError) and (m.is_not_found(e) or "already assigned" in e.message)):
+                    self.queue.add_unschedulable(pod)
+                    self.queue.move_all_to_active()
+                return
+            self.cache.finish_binding(assumed)
+            now = time.perf_counter()
+            self.m_bind.observe((now - tb) * 1e6)
+            self.m_e2e.observe((now - t0) * 1e6)
+            self.m_attempts.labels("scheduled").inc()
+            self.scheduled += 1
+            self.recorder.event(pod, "Normal", "Scheduled", f"Successfully assigned {m.name_of(pod)} to {host}")
+
+    async def _mark_unschedulable(self, pod, msg):
+        cond = {"type": "PodScheduled", "status": "False", "reason": "Unschedulable", "message": msg,
+                "lastProbeTime": None, "lastTransitionTime": m.now_rfc3339()}
+        for c in (pod.get("status") or {}).get("conditions") or []:
+            if c.get("type") == "PodScheduled" and c.get("message") == msg:
+                return
+        try:
+            await self.client.patch("pods", m.name_of(pod), {"status": {"conditions": [cond]}}, m.namespace_of(pod), sub="status")
+        except Exception:
+            pass
+
+    async def _preempt(self, pod):
+        self.m_preempt.inc()
+        node, victims = self.algo.preempt(pod)
+        if not node:
+            return
+        for v in victims:
+            self.recorder.event(v, "Normal", "Preempted", f"by {m.key_of(pod)} on node {node}")
+            try:
+                await self.client.delete("pods", m.name_of(v), m.namespace_of(v))
+            except m.StatusError:
+                pass
+        try:
+            await self.client.patch("pods", m.name_of(pod), {"status": {"nominatedNodeName": node}}, m.namespace_of(pod), sub="status")
+        except m.StatusError:
+            pass

@@ -49,6 +49,8 @@ def targets(sanitize=False, cpu_only=False):
           "-lamd_smi", "-o", "{out}"]),
         (n(BIN, "pause"), [n("native/pause.cpp")],
          ["g++", "-O2", "-std=c++17", n("native/pause.cpp"), "-o", "{out}"]),
+        (n(BIN, "amdkube-nsexec"), [n("native/nsexec.cpp")],
+         ["g++", "-O2", "-std=c++17", n("native/nsexec.cpp"), "-o", "{out}"]),
     ]
     if sanitize:
         san = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-g"]

@@ -1,0 +1,119 @@
+// amdkube-nsexec: rocshim's privileged container launcher (the OCI-runtime-hook analogue).
+//
+// The reference hands GPU containers to the `nvidia` OCI runtime through the Docker hooks
+// service (pkg/kubelet/dockershim/docker_hooks.go) which injects /dev/nvidia*. On MI355X
+// the devices are /dev/kfd (one node for all compute) plus one DRM render node per GPU, so
+// isolation = "the container's /dev/dri contains only its own render nodes":
+//
+//   amdkube-nsexec [--dev-root /dev] [--keep /dev/dri/renderD128 ...] [--hide-kfd]
+//                  [--cgroup /sys/fs/cgroup/amdkube/<pod>/<ctr>] [--memory-max BYTES]
+//                  [--cpu-max "QUOTA PERIOD"] -- argv...
+//
+//  1. join (creating) a cgroup-v2 leaf and apply memory.max / cpu.max;
+//  2. unshare a private mount namespace;
+//  3. open every kept device node with O_PATH (inside the new namespace), mount a fresh tmpfs over <dev-root>/dri and
+//     bind the kept nodes back from /proc/self/fd (no CAP_MKNOD needed);
+//  4. --hide-kfd: bind /dev/null over <dev-root>/kfd for containers without GPUs;
+//  5. exec the container's argv.
+// Any isolation step that fails is fatal (exit 126): a container never silently runs with
+// more devices than it was given.
+#include <fcntl.h>
+#include <sched.h>
+#include <sys/mount.h>
+#include <sys/stat.h>
+#include <sys/types.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+static int die(const char* what) {
+  std::fprintf(stderr, "amdkube-nsexec: %s: %s\n", what, std::strerror(errno));
+  return 126;
+}
+
+static bool write_file(const std::string& path, const std::string& val) {
+  int fd = open(path.c_str(), O_WRONLY | O_CLOEXEC);
+  if (fd < 0) return false;
+  bool ok = write(fd, val.data(), val.size()) == static_cast<ssize_t>(val.size());
+  close(fd);
+  return ok;
+}
+
+static int mkdir_p(const std::string& p) {
+  std::string cur;
+  for (size_t i = 0; i < p.size(); ++i) {
+    cur += p[i];
+    if ((p[i] == '/' && i > 0) || i + 1 == p.size()) {
+      if (mkdir(cur.c_str(), 0755) < 0 && errno != EEXIST) return -1;
+    }
+  }
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  std::string dev_root = "/dev", cgroup, mem_max, cpu_max;
+  std::vector<std::string> keep;
+  bool hide_kfd = false;
+  int i = 1;
+  for (; i < argc; ++i) {
+    std::string a = argv[i];
+    if (a == "--") {
+      ++i;
+      break;
+    } else if (a == "--dev-root" && i + 1 < argc) dev_root = argv[++i];
+    else if (a == "--keep" && i + 1 < argc) keep.push_back(argv[++i]);
+    else if (a == "--hide-kfd") hide_kfd = true;
+    else if (a == "--cgroup" && i + 1 < argc) cgroup = argv[++i];
+    else if (a == "--memory-max" && i + 1 < argc) mem_max = argv[++i];
+    else if (a == "--cpu-max" && i + 1 < argc) cpu_max = argv[++i];
+    else {
+      std::fprintf(stderr, "amdkube-nsexec: unknown argument %s\n", a.c_str());
+      return 126;
+    }
+  }
+  if (i >= argc) {
+    std::fprintf(stderr, "usage: amdkube-nsexec [options] -- argv...\n");
+    return 126;
+  }
+  if (!cgroup.empty()) {
+    if (mkdir_p(cgroup) < 0) return die("create cgroup");
+    if (!mem_max.empty()) write_file(cgroup + "/memory.max", mem_max);
+    if (!cpu_max.empty()) write_file(cgroup + "/cpu.max", cpu_max);
+    if (!write_file(cgroup + "/cgroup.procs", std::to_string(getpid()))) return die("join cgroup");
+  }
+  if (unshare(CLONE_NEWNS) < 0) return die("unshare(CLONE_NEWNS)");
+  if (mount(nullptr, "/", nullptr, MS_REC | MS_PRIVATE, nullptr) < 0) return die("make / rprivate");
+  // open the kept nodes inside the new namespace (a bind source must belong to it)
+  std::vector<int> fds;
+  for (auto& k : keep) {
+    int fd = open(k.c_str(), O_PATH | O_CLOEXEC);
+    if (fd < 0) return die(("open kept device " + k).c_str());
+    fds.push_back(fd);
+  }
+  std::string dri = dev_root + "/dri";
+  struct stat st;
+  if (stat(dri.c_str(), &st) == 0) {
+    if (mount("tmpfs", dri.c_str(), "tmpfs", MS_NOSUID | MS_NOEXEC, "mode=755,size=64k") < 0) return die("mount tmpfs on dri");
+    for (size_t k = 0; k < keep.size(); ++k) {
+      const char* base = std::strrchr(keep[k].c_str(), '/');
+      std::string target = dri + "/" + (base ? base + 1 : keep[k].c_str());
+      int tfd = open(target.c_str(), O_CREAT | O_WRONLY | O_CLOEXEC, 0666);
+      if (tfd < 0) return die(("create mount point " + target).c_str());
+      close(tfd);
+      std::string src = "/proc/self/fd/" + std::to_string(fds[k]);
+      if (mount(src.c_str(), target.c_str(), nullptr, MS_BIND, nullptr) < 0) return die(("bind " + target).c_str());
+    }
+  }
+  if (hide_kfd) {
+    std::string kfd = dev_root + "/kfd";
+    if (stat(kfd.c_str(), &st) == 0 && mount("/dev/null", kfd.c_str(), nullptr, MS_BIND, nullptr) < 0) return die("hide kfd");
+  }
+  for (int fd : fds) close(fd);
+  execvp(argv[i], argv + i);
+  return die(("exec " + std::string(argv[i])).c_str());
+}
