@@ -1,0 +1,196 @@
+"""GPU-pod density / startup benchmark driver (runs the whole node in one process).
+
+Metric (BASELINE.json): p50 GPU-pod startup latency + sustained GPU-pod throughput at
+1/2/4/8 allocatable MI355X. One "step" = a burst of `pods_per_gpu × N` GPU pods, each
+requesting `amd.com/gpu: 1` through the legacy limits path (ResourceV2 → device-granular
+binding), each running the real gfx950 `rocm/vector-add` workload (the reference's
+cuda-vector-add e2e image, 50,000 fp32 elements) on exactly its assigned GPU; the step ends
+when every pod has Succeeded. Pods are deleted as they finish. Measured per pod from a
+watch (the density test's method, test/e2e/scalability/density.go:771-819):
+  create → scheduled (bind observed) → started (container running/terminated observed) → Succeeded.
+
+Startup latency (the SLO metric, ≤ 5 s p50/p90/p99) is reported for the first wave of each
+burst (pods that found a free GPU at creation, i.e. no queueing); node-side latency
+(bind → start) is reported for every pod.
+
+Protocol (stdin/stdout JSON lines, used by bench.py): {"cmd":"run","steps":K} → result line;
+{"cmd":"quit"}.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import logging
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+from amdkube.api import meta as m  # noqa: E402
+from amdkube.localcluster import LocalCluster  # noqa: E402
+
+
+def pct(xs, q):
+    if not xs:
+        return None
+    xs = sorted(xs)
+    k = min(len(xs) - 1, max(0, int(round(q / 100.0 * (len(xs) - 1)))))
+    return xs[k]
+
+
+class PodBench:
+    def __init__(self, lc: LocalCluster, n_gpus: int, pods_per_gpu: int, image: str, args: list[str]):
+        self.lc, self.n, self.ppg, self.image, self.args = lc, n_gpus, pods_per_gpu, image, args
+        self.seq = 0
+        self.t: dict[str, dict] = {}
+        self.done_events: dict[str, asyncio.Event] = {}
+        self.failed: list[str] = []
+        self._watch_task = None
+        self.deleting: set = set()
+
+    def pod(self, name):
+        return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "default", "labels": {"app": "podbench"}},
+                "spec": {"restartPolicy": "Never", "terminationGracePeriodSeconds": 0,
+                         "containers": [{"name": "vector-add", "image": self.image, "args": self.args,
+                                         "resources": {"limits": {"amd.com/gpu": "1"}}}]}}
+
+    async def start(self):
+        self._watch_task = asyncio.create_task(self._watch())
+        await asyncio.sleep(0.2)
+
+    async def _watch(self):
+        c = self.lc.client
+        while True:
+            try:
+                async for typ, obj in c.watch("pods", "default", "", label_selector="app=podbench", timeout_seconds=3600):
+                    self._observe(typ, obj)
+            except asyncio.CancelledError:
+                raise
+            except Exception:
+                await asyncio.sleep(0.05)
+
+    def _observe(self, typ, obj):
+        name = m.name_of(obj)
+        rec = self.t.get(name)
+        if rec is None:
+            return
+        now = time.perf_counter()
+        if "bound" not in rec and (obj.get("spec") or {}).get("nodeName"):
+            rec["bound"] = now
+        st = obj.get("status") or {}
+        if "started" not in rec:
+            for cs in st.get("containerStatuses") or []:
+                s = cs.get("state") or {}
+                if "running" in s or "terminated" in s:
+                    rec["started"] = now
+        ph = st.get("phase")
+        if ph in ("Succeeded", "Failed") and "done" not in rec:
+            rec["done"] = now
+            rec.setdefault("started", now)
+            rec.setdefault("bound", now)
+            if ph == "Failed":
+                self.failed.append(f"{name}: {st.get('reason')} {st.get('message')} {json.dumps(st.get('containerStatuses'))[:300]}")
+            ev = self.done_events.get(name)
+            if ev:
+                ev.set()
+            if name not in self.deleting:
+                self.deleting.add(name)
+                asyncio.create_task(self._delete(name))
+
+    async def _delete(self, name):
+        try:
+            await self.lc.client.delete("pods", name, "default", grace=0)
+        except Exception:
+            pass
+
+    async def step(self, timeout=300.0):
+        total = self.n * self.ppg
+        names = []
+        for i in range(total):
+            self.seq += 1
+            names.append(f"vadd-{self.seq:06d}")
+        for nm in names:
+            self.t[nm] = {"wave": 0}
+            self.done_events[nm] = asyncio.Event()
+        for i, nm in enumerate(names):
+            self.t[nm]["wave"] = i // self.n
+        creates = []
+        for nm in names:
+            self.t[nm]["create"] = time.perf_counter()
+            creates.append(self.lc.client.create(self.pod(nm), "default"))
+        await asyncio.gather(*creates)
+        await asyncio.wait_for(asyncio.gather(*(self.done_events[nm].wait() for nm in names)), timeout)
+        return names
+
+    async def run(self, steps: int):
+        t0 = time.perf_counter()
+        names = []
+        for _ in range(steps):
+            names += await self.step()
+        el = time.perf_counter() - t0
+        recs = [self.t[n] for n in names]
+        first = [r["started"] - r["create"] for r in recs if r["wave"] == 0]
+        allstart = [r["started"] - r["create"] for r in recs]
+        node = [r["started"] - r["bound"] for r in recs]
+        sched = [r["bound"] - r["create"] for r in recs if r["wave"] == 0]
+        life = [r["done"] - r["started"] for r in recs]
+        ms = lambda v: None if v is None else round(v * 1000, 2)  # noqa: E731
+        return {"pods": len(names), "elapsed_s": el, "pods_per_s": len(names) / el if el else 0.0,
+                "failed": len(self.failed), "failures": self.failed[:5],
+                "p50_startup_ms": ms(pct(first, 50)), "p90_startup_ms": ms(pct(first, 90)), "p99_startup_ms": ms(pct(first, 99)),
+                "p50_startup_all_ms": ms(pct(allstart, 50)), "p50_node_startup_ms": ms(pct(node, 50)),
+                "p99_node_startup_ms": ms(pct(node, 99)), "p50_schedule_ms": ms(pct(sched, 50)),
+                "p50_pod_runtime_ms": ms(pct(life, 50))}
+
+
+async def serve(args):
+    logging.basicConfig(level=logging.WARNING, stream=sys.stderr)
+    lc = LocalCluster(gpus=args.backend, n_gpus=args.gpus, relist_period=1.0, with_controllers=False,
+                      health_probe=args.health_probe)
+    await lc.start()
+    await lc.wait_gpus(args.gpus, 60)
+    node = await lc.client.get("nodes", lc.node_name)
+    devs = list(((node["status"].get("extendedResources") or {}).get("amd.com/gpu") or {}).get("resources") or {})
+    pb = PodBench(lc, args.gpus, args.pods_per_gpu, args.image, args.args)
+    await pb.start()
+    print(json.dumps({"ready": True, "gpus": devs, "backend": lc.backend.name if lc.backend else "none"}), flush=True)
+    loop = asyncio.get_running_loop()
+    reader = asyncio.StreamReader()
+    await loop.connect_read_pipe(lambda: asyncio.StreamReaderProtocol(reader), sys.stdin)
+    try:
+        while True:
+            line = await reader.readline()
+            if not line:
+                break
+            cmd = json.loads(line)
+            if cmd.get("cmd") == "quit":
+                break
+            if cmd.get("cmd") == "run":
+                res = await pb.run(int(cmd.get("steps", 1)))
+                res["scheduler"] = {"scheduled": lc.scheduler.scheduled, "bind_errors": lc.scheduler.bind_errors}
+                print(json.dumps(res), flush=True)
+            if cmd.get("cmd") == "schedperf":
+                from amdkube.benchmark.schedperf import run_schedperf
+                res = await run_schedperf(int(cmd.get("nodes", 100)), int(cmd.get("pods", 3000)), gpus_per_node=8)
+                print(json.dumps(res), flush=True)
+    finally:
+        await lc.stop()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--pods-per-gpu", type=int, default=4)
+    ap.add_argument("--backend", default="auto")
+    ap.add_argument("--image", default="rocm/vector-add")
+    ap.add_argument("--health-probe", default="none")
+    ap.add_argument("args", nargs="*", default=[])
+    asyncio.run(serve(ap.parse_args()))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,94 @@
+"""scheduler_perf equivalent: in-process apiserver + scheduler + fake nodes (API objects only).
+
+Reference: test/integration/scheduler_perf/scheduler_test.go:35-92 — 100 nodes
+(4 CPU / 32 Gi / 110 pods), 3,000 pods, minimum-interval QPS must stay ≥ 30 pods/s
+(warn < 100). amdkube's variant gives every fake node 8 MI355X devices (fixture attributes
++ topology annotation) and can make every pod request one GPU, so the device allocator and
+xGMI/NUMA scorer are on the measured path.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import time
+
+from ..apiserver import APIServer
+from ..client import Client
+from ..deviceplugin.amd import attributes, topology_label
+from ..scheduler import Scheduler
+from ..smi import FakeBackend, device_id
+
+
+def fake_node(i: int, gpus: int, backend: FakeBackend | None):
+    st = {"capacity": {"cpu": "4", "memory": "32Gi", "pods": "110"}, "allocatable": {"cpu": "4", "memory": "32Gi", "pods": "110"},
+          "conditions": [{"type": "Ready", "status": "True", "lastHeartbeatTime": "2030-01-01T00:00:00Z"}]}
+    md = {"name": f"node-{i:04d}", "labels": {"kubernetes.io/hostname": f"node-{i:04d}"}}
+    if gpus and backend is not None:
+        gl = backend.gpus()[:gpus]
+        devs = {}
+        for g in gl:
+            did = f"{device_id(g)}-n{i}"
+            devs[did] = {"id": did, "health": "Healthy", "attributes": attributes(g)}
+        st["capacity"]["amd.com/gpu"] = st["allocatable"]["amd.com/gpu"] = str(gpus)
+        st["extendedResources"] = {"amd.com/gpu": {"resources": devs}}
+        topo = json.loads(topology_label(gl, [r[:gpus] for r in backend.topology()[:gpus]]))
+        topo["ids"] = [f"{x}-n{i}" for x in topo["ids"]]
+        md["annotations"] = {"amd.com/gpu-topology": json.dumps(topo)}
+    return {"apiVersion": "v1", "kind": "Node", "metadata": md, "status": st}
+
+
+def pod(i: int, gpu: bool):
+    c = {"name": "c", "image": "k8s.gcr.io/pause:3.1",
+         "resources": {"requests": {"cpu": "10m", "memory": "10Mi"}, "limits": {"cpu": "10m", "memory": "10Mi"}}}
+    if gpu:
+        c["resources"]["limits"]["amd.com/gpu"] = "1"
+    return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": f"pod-{i:06d}", "namespace": "default"},
+            "spec": {"containers": [c]}}
+
+
+async def run_schedperf(n_nodes=100, n_pods=3000, gpus_per_node=8, gpu_pods=True, create_concurrency=64):
+    api = await APIServer(event_ttl=3600).start()
+    client = Client(api.url, pool=128)
+    fb = FakeBackend()
+    try:
+        for i in range(n_nodes):
+            await client.create(fake_node(i, gpus_per_node, fb))
+        sched = await Scheduler(Client(api.url, pool=256)).start()
+        sched.recorder.enabled = False  # events are not on the measured path in scheduler_perf either
+        want = min(n_pods, n_nodes * gpus_per_node) if gpu_pods else n_pods
+        sem = asyncio.Semaphore(create_concurrency)
+
+        async def mk(i):
+            async with sem:
+                await client.create(pod(i, gpu_pods))
+        t0 = time.perf_counter()
+        creator = asyncio.ensure_future(asyncio.gather(*(mk(i) for i in range(want))))
+        samples = []
+        last, last_t = 0, t0
+        while sched.scheduled < want:
+            await asyncio.sleep(0.25)
+            now = time.perf_counter()
+            samples.append((sched.scheduled - last) / (now - last_t))
+            last, last_t = sched.scheduled, now
+            if now - t0 > 600:
+                break
+        el = time.perf_counter() - t0
+        await creator
+        # verify: no device handed out twice
+        items, _ = await client.list("pods", "default")
+        seen, dup = set(), 0
+        for p in items:
+            for pres in (p.get("spec") or {}).get("extendedResources") or []:
+                for d in pres.get("assigned") or []:
+                    dup += d in seen
+                    seen.add(d)
+        steady = samples[1:-1] or samples
+        res = {"nodes": n_nodes, "pods": want, "gpu_pods": gpu_pods, "scheduled": sched.scheduled, "elapsed_s": round(el, 3),
+               "avg_pods_per_s": round(sched.scheduled / el, 1), "min_interval_pods_per_s": round(min(steady), 1) if steady else 0,
+               "bind_errors": sched.bind_errors, "double_assigned": dup}
+        await sched.stop()
+        await sched.client.close()
+        return res
+    finally:
+        await client.close()
+        await api.stop()

@@ -1,0 +1,134 @@
+"""amdkube headline benchmark: GPU-pod throughput + p50 GPU-pod startup latency on one
+MI355X node with N allocatable GPUs (BASELINE.json metric; SURVEY §6 mapping).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--pods-per-gpu P]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU; rank 0 drives)
+
+Rank 0 launches the node (apiserver, scheduler, rocshim, AMD device plugin on amd-smi,
+kubelet) in a child process BEFORE any GPU initialisation in this process, then every rank
+brackets exactly K steps with barrier + torch.cuda.synchronize(). One step = P×N GPU pods
+(`amd.com/gpu: 1` each) running the real gfx950 vector-add workload on exactly their
+assigned GPU; the step ends when all have Succeeded. value = pods completed per second over
+the whole job (all N GPUs); extra fields carry startup-latency percentiles and the
+scheduler_perf (100 nodes / 3000 pods) result.
+
+Baselines: density saturation ≥ 8 pods/s (vs_baseline = value / 8),
+pod startup p50/p90/p99 ≤ 5 s, scheduler throughput ≥ 30 pods/s (goal 100).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+METRIC = "p50 GPU-pod startup latency + scheduling throughput (pods/s) at 1/2/4/8 MI355X"
+BASELINE_PODS_PER_S = 8.0      # test/e2e/scalability/density.go:55-56 MinPodsPerSecondThroughput
+SLO_STARTUP_MS = 5000.0        # test/e2e/framework/metrics_util.go:46
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=None)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--pods-per-gpu", type=int, default=4)
+    ap.add_argument("--backend", default="auto", help="amdsmi|sysfs|fake|auto")
+    ap.add_argument("--no-sched-perf", action="store_true")
+    a = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    n = a.gpus or world
+
+    worker = None
+    if rank == 0:
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        env["AMDKUBE_REQUIRE_NATIVE"] = "1"
+        for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "MASTER_ADDR", "MASTER_PORT",
+                  "TORCHELASTIC_RUN_ID"):
+            env.pop(k, None)
+        worker = subprocess.Popen([sys.executable, "-m", "amdkube.benchmark.podbench", "--gpus", str(n),
+                                   "--pods-per-gpu", str(a.pods_per_gpu), "--backend", a.backend],
+                                  cwd=ROOT, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
+        ready = json.loads(worker.stdout.readline() or "{}")
+        if not ready.get("ready"):
+            worker.kill()
+            raise SystemExit("cluster worker failed to start")
+        print(f"[bench] node ready: {len(ready['gpus'])} GPU(s) via {ready['backend']}", file=sys.stderr, flush=True)
+
+    import torch
+    import torch.distributed as dist
+    cuda = torch.cuda.is_available()
+    if cuda:
+        torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
+    if world > 1:
+        dist.init_process_group("nccl" if cuda else "gloo")
+
+    def barrier():
+        if world > 1:
+            if cuda:
+                dist.barrier(device_ids=[torch.cuda.current_device()])
+            else:
+                dist.barrier()
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+
+    def drive(steps):
+        worker.stdin.write(json.dumps({"cmd": "run", "steps": steps}) + "\n")
+        worker.stdin.flush()
+        return json.loads(worker.stdout.readline())
+
+    if rank == 0 and a.warmup > 0:
+        drive(a.warmup)
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    res = drive(a.steps) if rank == 0 else None
+    barrier()
+    sync()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda" if cuda else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if rank == 0:
+        sched = None
+        if not a.no_sched_perf:
+            worker.stdin.write(json.dumps({"cmd": "schedperf", "nodes": 100, "pods": 3000}) + "\n")
+            worker.stdin.flush()
+            sched = json.loads(worker.stdout.readline())
+        worker.stdin.write(json.dumps({"cmd": "quit"}) + "\n")
+        worker.stdin.flush()
+        try:
+            worker.wait(60)
+        except subprocess.TimeoutExpired:
+            worker.kill()
+        pods = res["pods"]
+        value = pods / el
+        out = {"metric": METRIC, "value": round(value, 3), "unit": "pods/s", "n_gpus": n, "steps": a.steps, "warmup": a.warmup,
+               "ms_per_step": round(el * 1000 / a.steps, 2), "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": round(value / BASELINE_PODS_PER_S, 3), "dtype": "fp32",
+               "data": "synthetic: rocm/vector-add GPU pods (50,000 fp32 elements each, cuda-vector-add equivalent)",
+               "config": {"model": "GPU-pod density: 1 node, amd.com/gpu=1 pods, ResourceV2 → device-granular binding",
+                          "global_batch": n * a.pods_per_gpu, "seq_len": None, "parallelism": f"{n} allocatable MI355X"},
+               "p50_startup_ms": res["p50_startup_ms"], "p90_startup_ms": res["p90_startup_ms"],
+               "p99_startup_ms": res["p99_startup_ms"], "startup_slo_ms": SLO_STARTUP_MS,
+               "p50_node_startup_ms": res["p50_node_startup_ms"], "p50_schedule_ms": res["p50_schedule_ms"],
+               "p50_pod_runtime_ms": res["p50_pod_runtime_ms"], "failed_pods": res["failed"],
+               "sched_perf": sched}
+        if res["failed"]:
+            out["failures"] = res["failures"]
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

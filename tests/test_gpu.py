@@ -1,0 +1,113 @@
+"""GPU tier (real MI355X via gpurun). Ordering matters: every test that spawns processes
+(pods, probes) runs before the tests that initialise HIP inside this pytest process.
+
+Numerics: the HIP kernels are checked against a host fp32 reference (vector add compares
+every element with |c - (a+b)| ≤ 1e-5; the HBM probe re-derives every written word).
+"""
+import asyncio
+import json
+import os
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from amdkube.localcluster import LocalCluster, wait_pod  # noqa: E402
+from tests.conftest import run  # noqa: E402
+
+BIN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "amdkube", "_native", "bin")
+
+
+def vadd_pod(name, gpu=True, args=("--print-uuid",)):
+    c = {"name": "vadd", "image": "rocm/vector-add", "args": list(args)}
+    if gpu:
+        c["resources"] = {"limits": {"amd.com/gpu": "1"}}
+    return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "default"},
+            "spec": {"restartPolicy": "Never", "containers": [c]}}
+
+
+def test_01_amdsmi_backend_enumerates_mi355x():
+    from amdkube.smi import AmdSmiBackend, device_id, visibility_token
+    b = AmdSmiBackend()
+    gpus = b.gpus()
+    assert gpus, "amd-smi found no GPU"
+    g = gpus[0]
+    assert g["gfx_target"] == "gfx950"
+    assert g["vram_total_bytes"] >= 250 * 2 ** 30
+    assert g["num_cu"] == 256
+    assert visibility_token(g).startswith("GPU-")
+    assert device_id(g)
+    s = b.sample(0)
+    assert "vram_used_bytes" in s
+    topo = b.topology()
+    assert topo[0][0]["type"] == "self"
+    b.close()
+
+
+def test_02_gpu_pod_runs_on_its_assigned_device():
+    async def go():
+        async with LocalCluster(gpus="amdsmi", n_gpus=1, relist_period=0.5, with_controllers=False) as lc:
+            node = await lc.wait_gpus(1, 60)
+            dev = node["status"]["extendedResources"]["amd.com/gpu"]["resources"]
+            [did] = list(dev)
+            assert dev[did]["attributes"]["amd.com/gfx"] == "gfx950"
+            assert dev[did]["attributes"]["amd.com/gpu-type"] == "MI355X"
+            await lc.client.create(vadd_pod("gpu-pod"))
+            p = await wait_pod(lc.client, "default", "gpu-pod", ("Succeeded", "Failed"), 120)
+            logs = await lc.client.logs("default", "gpu-pod")
+            assert p["status"]["phase"] == "Succeeded", (p["status"], logs)
+            assert "Test PASSED" in logs
+            assert p["spec"]["extendedResources"][0]["assigned"] == [did]
+            tok = lc.plugin.by_id[did]["hip_uuid"]
+            assert f"uuid={tok}" in logs, logs
+            # a pod without amd.com/gpu must not see the GPU (isolation)
+            await lc.client.create(vadd_pod("cpu-pod", gpu=False, args=()))
+            p = await wait_pod(lc.client, "default", "cpu-pod", ("Succeeded", "Failed"), 120)
+            assert p["status"]["phase"] == "Failed", p["status"]
+            cpu_logs = await lc.client.logs("default", "cpu-pod")
+            assert "no GPU visible" in cpu_logs or "no ROCm-capable device" in cpu_logs, cpu_logs
+    run(go(), 300)
+
+
+def test_03_plugin_hbm_health_probe_marks_healthy():
+    async def go():
+        async with LocalCluster(gpus="amdsmi", n_gpus=1, with_controllers=False, health_probe="hbm") as lc:
+            node = await lc.wait_gpus(1, 120)
+            devs = node["status"]["extendedResources"]["amd.com/gpu"]["resources"]
+            assert all(d["health"] == "Healthy" for d in devs.values()), lc.plugin.reasons
+    run(go(), 300)
+
+
+def test_04_probe_binaries():
+    r = subprocess.run([os.path.join(BIN, "hbm-probe"), "--mib", "1024", "--iters", "3"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout)
+    assert d["errors"] == 0 and d["copy_gbps"] > 2000, d
+    r = subprocess.run([os.path.join(BIN, "xgmi-probe"), "--max-mib", "16", "--iters", "2"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([os.path.join(BIN, "gpu-burn"), "--ms", "100"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and json.loads(r.stdout)["bf16_tflops"] > 500, r.stdout
+
+
+# --- in-process HIP from here on (no process spawning after this point) -------------------
+def test_90_hip_vector_add_matches_fp32_reference():
+    from amdkube.ops import hip
+    for n in (1, 3, 50000, 1 << 22, (1 << 22) + 7):
+        r = hip.vector_add(n, 0)
+        assert r["ok"] and r["mismatches"] == 0, (n, r)
+
+
+def test_91_hip_hbm_probe_pattern_and_bandwidth():
+    from amdkube.ops import hip
+    r = hip.hbm_probe(1024, 3, 0)
+    assert r["errors"] == 0
+    assert r["read_gbps"] > 3000 and r["copy_gbps"] > 2000, r
+
+
+def test_92_hip_mfma_burn():
+    from amdkube.ops import hip
+    info = hip.device_info(0)
+    assert info["arch"].startswith("gfx950")
+    r = hip.mfma_burn(50.0, 0)
+    assert r["bf16_tflops"] > 500, r
