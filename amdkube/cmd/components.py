@@ -1,0 +1,340 @@
+"""Component entry points: `python -m amdkube <component> [flags]`.
+
+Flag names follow the reference binaries (cmd/kube-apiserver/app/options, plugin/cmd/
+kube-scheduler/app/server.go:106-160, cmd/kubelet/app/options/options.go,
+cmd/kube-controller-manager) where a counterpart exists. `local-up` mirrors
+hack/local-up-cluster.sh (:394-784): apiserver → controller-manager → scheduler → rocshim →
+device plugin → kubelet as separate processes with logs under --log-dir.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import logging
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+
+from ..utils import log as klog
+
+
+def _run_forever(coro_factory):
+    async def main():
+        comp = await coro_factory()
+        stop = asyncio.Event()
+        loop = asyncio.get_running_loop()
+        for s in (signal.SIGINT, signal.SIGTERM):
+            loop.add_signal_handler(s, stop.set)
+        await stop.wait()
+        if hasattr(comp, "stop"):
+            await comp.stop()
+    asyncio.run(main())
+
+
+def apiserver(argv):
+    ap = argparse.ArgumentParser("amdkube apiserver")
+    ap.add_argument("--bind-address", default="127.0.0.1")
+    ap.add_argument("--port", "--insecure-port", type=int, default=8080)
+    ap.add_argument("--data-dir", default=None, help="MVCC store WAL/snapshot directory (etcd replacement)")
+    ap.add_argument("--admission-control", default=None, help="ordered, comma-separated admission plugins")
+    ap.add_argument("--resource-v2-resources", default="amd.com/gpu", help="container limits ResourceV2 converts")
+    ap.add_argument("--token-auth-file", default=None)
+    ap.add_argument("--anonymous-auth", default="true")
+    ap.add_argument("--authorization-mode", default="AlwaysAllow")
+    ap.add_argument("--max-requests-inflight", type=int, default=400)
+    ap.add_argument("--max-mutating-requests-inflight", type=int, default=200)
+    ap.add_argument("--event-ttl", type=float, default=3600.0)
+    ap.add_argument("-v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "apiserver")
+    from ..apiserver import APIServer
+    from ..apiserver.admission import DEFAULT_CHAIN
+    from ..store import MVCCStore
+    tokens = {}
+    if a.token_auth_file:
+        for line in open(a.token_auth_file):
+            parts = [p.strip().strip('"') for p in line.strip().split(",")]
+            if len(parts) >= 2:
+                tokens[parts[0]] = {"name": parts[1], "uid": parts[2] if len(parts) > 2 else parts[1],
+                                    "groups": parts[3].split(",") if len(parts) > 3 else []}
+
+    async def mk():
+        srv = APIServer(MVCCStore(a.data_dir), admission_plugins=(a.admission_control.split(",") if a.admission_control else DEFAULT_CHAIN),
+                        admission_config={"ResourceV2": {"resource_names": tuple(a.resource_v2_resources.split(","))}},
+                        token_auth=tokens, authorization_mode=a.authorization_mode, anonymous_auth=a.anonymous_auth == "true",
+                        max_in_flight=a.max_requests_inflight, max_mutating_in_flight=a.max_mutating_requests_inflight,
+                        event_ttl=a.event_ttl)
+        return await srv.start(a.bind_address, a.port)
+    _run_forever(mk)
+
+
+def scheduler(argv):
+    ap = argparse.ArgumentParser("amdkube scheduler")
+    ap.add_argument("--master", "--server", dest="server", default="http://127.0.0.1:8080")
+    ap.add_argument("--policy-config-file", default=None)
+    ap.add_argument("--algorithm-provider", default="DefaultProvider")
+    ap.add_argument("--scheduler-name", default="default-scheduler")
+    ap.add_argument("--leader-elect", default="false")
+    ap.add_argument("--port", type=int, default=10251)
+    ap.add_argument("--feature-gates", default="")
+    ap.add_argument("--kube-api-qps", type=float, default=0)
+    ap.add_argument("--disable-preemption", action="store_true")
+    ap.add_argument("-v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "scheduler")
+    from ..client import Client
+    from ..scheduler import Scheduler
+
+    async def mk():
+        return await Scheduler(Client(a.server, qps=a.kube_api_qps), a.scheduler_name, a.policy_config_file, a.algorithm_provider,
+                               a.feature_gates, a.leader_elect == "true", port=a.port, disable_preemption=a.disable_preemption).start()
+    _run_forever(mk)
+
+
+def controller_manager(argv):
+    ap = argparse.ArgumentParser("amdkube controller-manager")
+    ap.add_argument("--master", "--server", dest="server", default="http://127.0.0.1:8080")
+    ap.add_argument("--controllers", default="*")
+    ap.add_argument("--leader-elect", default="false")
+    ap.add_argument("--node-monitor-grace-period", type=float, default=40.0)
+    ap.add_argument("--pod-eviction-timeout", type=float, default=300.0)
+    ap.add_argument("-v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "controller-manager")
+    from ..client import Client
+    from ..controllers import ALL, ControllerManager
+    names = list(ALL) if a.controllers in ("*", "") else a.controllers.split(",")
+
+    async def mk():
+        return await ControllerManager(Client(a.server), names, a.leader_elect == "true", socket.gethostname(),
+                                       a.node_monitor_grace_period, a.pod_eviction_timeout).start()
+    _run_forever(mk)
+
+
+def kubelet(argv):
+    ap = argparse.ArgumentParser("amdkube kubelet")
+    ap.add_argument("--api-servers", "--server", dest="server", default="http://127.0.0.1:8080")
+    ap.add_argument("--hostname-override", "--node-name", dest="node_name", default=socket.gethostname())
+    ap.add_argument("--root-dir", default="/var/lib/kubelet")
+    ap.add_argument("--device-plugin-dir", default=None)
+    ap.add_argument("--device-plugin-v1beta1-socket", default=None)
+    ap.add_argument("--container-runtime-endpoint", default="/var/run/amdkube/rocshim.sock")
+    ap.add_argument("--address", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=10250)
+    ap.add_argument("--node-ip", default="127.0.0.1")
+    ap.add_argument("--node-status-update-frequency", type=float, default=10.0)
+    ap.add_argument("--pleg-relist-period", type=float, default=1.0)
+    ap.add_argument("--max-pods", type=int, default=110)
+    ap.add_argument("--node-labels", default="")
+    ap.add_argument("--register-with-taints", default="")
+    ap.add_argument("--feature-gates", default="")
+    ap.add_argument("--chaos-chance", type=float, default=0.0)
+    ap.add_argument("--gpu-stats-backend", default="auto")
+    ap.add_argument("--kube-api-qps", type=float, default=0)
+    ap.add_argument("-v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "kubelet")
+    from ..client import Client
+    from ..kubelet.kubelet import Kubelet, KubeletConfig
+    labels = dict(kv.split("=", 1) for kv in a.node_labels.split(",") if "=" in kv)
+    taints = []
+    for t in filter(None, a.register_with_taints.split(",")):
+        kv, eff = t.split(":")
+        k, _, v = kv.partition("=")
+        taints.append({"key": k, "value": v, "effect": eff})
+    cfg = KubeletConfig(node_name=a.node_name, root_dir=a.root_dir,
+                        plugins_dir=a.device_plugin_dir or os.path.join(a.root_dir, "device-plugin", "plugins"),
+                        v1beta1_socket=a.device_plugin_v1beta1_socket, cri_socket=a.container_runtime_endpoint,
+                        address=a.address, port=a.port, node_ip=a.node_ip, node_status_update_frequency=a.node_status_update_frequency,
+                        relist_period=a.pleg_relist_period, max_pods=a.max_pods, node_labels=labels,
+                        register_with_taints=taints, feature_gates=a.feature_gates, chaos_chance=a.chaos_chance,
+                        gpu_stats_backend=a.gpu_stats_backend)
+
+    async def mk():
+        smi = None
+        if a.gpu_stats_backend != "none":
+            from ..smi import open_backend
+            try:
+                smi = open_backend(a.gpu_stats_backend)
+            except Exception as e:
+                logging.getLogger("amdkube.kubelet").warning("no GPU stats backend: %s", e)
+        return await Kubelet(Client(a.server, qps=a.kube_api_qps, chaos=a.chaos_chance), cfg, smi_backend=smi).start()
+    _run_forever(mk)
+
+
+def rocshim(argv):
+    ap = argparse.ArgumentParser("amdkube rocshim")
+    ap.add_argument("--listen", default="/var/run/amdkube/rocshim.sock")
+    ap.add_argument("--state-dir", default="/var/lib/amdkube/rocshim")
+    ap.add_argument("--hooks-dir", default="/usr/share/containers/docker/hooks.d")
+    ap.add_argument("--isolation", default="env", choices=("env", "namespaces"))
+    ap.add_argument("-v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "rocshim")
+    from ..runtime import RocShim
+
+    async def mk():
+        return await RocShim(a.listen, a.state_dir, a.hooks_dir, a.isolation).start()
+    _run_forever(mk)
+
+
+def device_plugin(argv):
+    ap = argparse.ArgumentParser("amdkube amd-device-plugin")
+    ap.add_argument("--backend", default="auto", help="amdsmi|sysfs|fake|auto")
+    ap.add_argument("--fixture", default=None)
+    ap.add_argument("--plugins-dir", default="/var/lib/kubelet/device-plugin/plugins")
+    ap.add_argument("--resource-name", default="amd.com/gpu")
+    ap.add_argument("--health-interval", type=float, default=10.0)
+    ap.add_argument("--health-probe", default="none", choices=("none", "hbm"))
+    ap.add_argument("--max-gpus", type=int, default=None)
+    ap.add_argument("--register-v1beta1", default=None, help="kubelet.sock of an upstream v1beta1 kubelet")
+    ap.add_argument("-v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "amd-device-plugin")
+    from ..deviceplugin import AMDGPUPlugin
+    from ..smi import open_backend
+
+    async def mk():
+        p = AMDGPUPlugin(open_backend(a.backend, a.fixture, a.max_gpus), a.resource_name, a.plugins_dir, a.health_interval,
+                         a.health_probe)
+        await p.start()
+        if a.register_v1beta1:
+            await p.register_v1beta1(a.register_v1beta1)
+        return p
+    _run_forever(mk)
+
+
+def exporter(argv):
+    ap = argparse.ArgumentParser("amdkube amdgpu-exporter")
+    ap.add_argument("--backend", default="auto")
+    ap.add_argument("--port", type=int, default=9400)
+    ap.add_argument("--address", default="0.0.0.0")
+    ap.add_argument("--node-name", default=socket.gethostname())
+    ap.add_argument("--kubelet-url", default=None)
+    ap.add_argument("-v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "amdgpu-exporter")
+    from ..monitoring.exporter import Exporter
+    from ..smi import open_backend
+
+    async def mk():
+        return await Exporter(open_backend(a.backend), a.node_name, a.kubelet_url).start(a.address, a.port)
+    _run_forever(mk)
+
+
+def hollow_node(argv):
+    ap = argparse.ArgumentParser("amdkube hollow-node")
+    ap.add_argument("--server", default="http://127.0.0.1:8080")
+    ap.add_argument("--name-prefix", default="hollow-node")
+    ap.add_argument("--count", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=8)
+    ap.add_argument("--run-seconds", type=float, default=None)
+    ap.add_argument("-v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "hollow-node")
+    from ..hollow.hollow_node import HollowNode
+
+    class Group:
+        def __init__(self, nodes):
+            self.nodes = nodes
+
+        async def stop(self):
+            for n in self.nodes:
+                await n.stop()
+
+    async def mk():
+        nodes = [await HollowNode(a.server, f"{a.name_prefix}-{i}", a.gpus, a.run_seconds).start() for i in range(a.count)]
+        return Group(nodes)
+    _run_forever(mk)
+
+
+def local_up(argv):
+    """hack/local-up-cluster.sh equivalent: every component as its own process."""
+    ap = argparse.ArgumentParser("amdkube local-up")
+    ap.add_argument("--base-dir", default="/tmp/amdkube-local")
+    ap.add_argument("--port", type=int, default=8080)
+    ap.add_argument("--backend", default="auto")
+    ap.add_argument("--max-gpus", type=int, default=None)
+    ap.add_argument("--isolation", default="env")
+    ap.add_argument("--no-gpus", action="store_true")
+    ap.add_argument("--exporter-port", type=int, default=9400)
+    a = ap.parse_args(argv)
+    b = a.base_dir
+    os.makedirs(os.path.join(b, "logs"), exist_ok=True)
+    server = f"http://127.0.0.1:{a.port}"
+    py = [sys.executable, "-m", "amdkube"]
+    procs = []
+
+    def spawn(name, args):
+        logf = open(os.path.join(b, "logs", f"{name}.log"), "ab")
+        p = subprocess.Popen(py + args, stdout=logf, stderr=subprocess.STDOUT)
+        procs.append((name, p))
+        return p
+
+    def wait_http(url, timeout=30):
+        import urllib.request
+        end = time.time() + timeout
+        while time.time() < end:
+            try:
+                urllib.request.urlopen(url, timeout=1)
+                return True
+            except Exception:
+                time.sleep(0.1)
+        return False
+
+    spawn("apiserver", ["apiserver", "--port", str(a.port), "--data-dir", os.path.join(b, "store")])
+    if not wait_http(server + "/healthz"):
+        raise SystemExit("apiserver did not come up; see " + os.path.join(b, "logs", "apiserver.log"))
+    spawn("controller-manager", ["controller-manager", "--server", server])
+    spawn("scheduler", ["scheduler", "--server", server, "--port", "0"])
+    sock = os.path.join(b, "rocshim.sock")
+    spawn("rocshim", ["rocshim", "--listen", sock, "--state-dir", os.path.join(b, "rocshim"), "--hooks-dir",
+                      os.path.join(b, "hooks.d"), "--isolation", a.isolation])
+    plugins = os.path.join(b, "device-plugin", "plugins")
+    if not a.no_gpus:
+        dp = ["amd-device-plugin", "--backend", a.backend, "--plugins-dir", plugins]
+        if a.max_gpus:
+            dp += ["--max-gpus", str(a.max_gpus)]
+        spawn("amd-device-plugin", dp)
+        spawn("amdgpu-exporter", ["amdgpu-exporter", "--backend", a.backend, "--port", str(a.exporter_port),
+                                  "--kubelet-url", "http://127.0.0.1:10250"])
+    for _ in range(100):
+        if os.path.exists(sock):
+            break
+        time.sleep(0.1)
+    spawn("kubelet", ["kubelet", "--server", server, "--root-dir", os.path.join(b, "kubelet"), "--device-plugin-dir", plugins,
+                      "--container-runtime-endpoint", sock, "--gpu-stats-backend", "none" if a.no_gpus else a.backend])
+    os.makedirs(os.path.expanduser("~/.amdkube"), exist_ok=True)
+    json.dump({"server": server}, open(os.path.expanduser("~/.amdkube/config"), "w"))
+    print(f"amdkube local cluster is running: {server}  (logs: {b}/logs)\n"
+          f"  python -m amdkube kubectl get nodes\n  python -m amdkube kubectl run vadd --image rocm/vector-add --gpus 1 --restart Never",
+          flush=True)
+    stop = {"flag": False}
+    signal.signal(signal.SIGTERM, lambda *_: stop.update(flag=True))
+    try:
+        while not stop["flag"]:
+            for name, p in procs:
+                if p.poll() is not None:
+                    print(f"{name} exited with {p.returncode}; see {b}/logs/{name}.log", flush=True)
+                    stop["flag"] = True
+            time.sleep(0.5)
+    except KeyboardInterrupt:
+        pass
+    finally:
+        for name, p in reversed(procs):
+            p.send_signal(signal.SIGTERM)
+        for name, p in procs:
+            try:
+                p.wait(10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+
+
+COMPONENTS = {"apiserver": apiserver, "kube-apiserver": apiserver, "scheduler": scheduler, "kube-scheduler": scheduler,
+              "controller-manager": controller_manager, "kube-controller-manager": controller_manager, "kubelet": kubelet,
+              "rocshim": rocshim, "amd-device-plugin": device_plugin, "device-plugin": device_plugin,
+              "amdgpu-exporter": exporter, "exporter": exporter, "hollow-node": hollow_node, "local-up": local_up}

@@ -1,0 +1,463 @@
+"""kubectl for amdkube.
+
+Reference command set: pkg/kubectl/cmd/cmd.go:216 (create/apply/get/describe/delete/logs/
+exec/label/annotate/cordon/uncordon/drain/scale/patch/run/top/version/api-resources/
+cluster-info/explain), create.go:64,146. Output: tables (GPU columns added, SURVEY §7.6
+#17), -o json|yaml|name|wide|jsonpath={...}. Server from --server, $AMDKUBE_SERVER or
+~/.amdkube/config ({"server": ..., "token": ...}).
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import re
+import sys
+import time
+
+from ..api import meta as m
+from ..api.scheme import SCHEME, dump_yaml, load_manifests
+from ..client import Client
+from . import printers
+
+CONFIG = os.path.expanduser("~/.amdkube/config")
+
+
+def _client(a) -> Client:
+    server, token = a.server, a.token
+    if not server:
+        server = os.environ.get("AMDKUBE_SERVER")
+    if (not server or not token) and os.path.exists(CONFIG):
+        cfg = json.load(open(CONFIG))
+        server = server or cfg.get("server")
+        token = token or cfg.get("token")
+    return Client(server or "http://127.0.0.1:8080", token=token, user_agent="kubectl/amdkube")
+
+
+def _jsonpath(obj, expr: str):
+    expr = expr.strip()
+    if expr.startswith("{") and expr.endswith("}"):
+        expr = expr[1:-1]
+    cur = [obj]
+    for part in re.findall(r"\.([^.\[]+)|\[(\*|\d+)\]", expr):
+        key, idx = part
+        nxt = []
+        for c in cur:
+            if key:
+                if isinstance(c, dict) and key in c:
+                    nxt.append(c[key])
+            elif idx == "*":
+                nxt.extend(c if isinstance(c, list) else [])
+            elif isinstance(c, list) and int(idx) < len(c):
+                nxt.append(c[int(idx)])
+        cur = nxt
+    return " ".join(json.dumps(x) if isinstance(x, (dict, list)) else str(x) for x in cur)
+
+
+def _emit(objs, a, kind=None, single=False, out=sys.stdout):
+    o = a.output or ""
+    if o == "json":
+        if single and len(objs) == 1:
+            print(json.dumps(objs[0], indent=2), file=out)
+        else:
+            print(json.dumps({"apiVersion": "v1", "kind": "List", "items": objs}, indent=2), file=out)
+    elif o == "yaml":
+        print(dump_yaml(objs[0] if single and len(objs) == 1 else {"apiVersion": "v1", "kind": "List", "items": objs}), file=out, end="")
+    elif o == "name":
+        for x in objs:
+            print(f"{(x.get('kind') or kind or '').lower()}/{m.name_of(x)}", file=out)
+    elif o.startswith("jsonpath="):
+        expr = o[len("jsonpath="):]
+        if single and len(objs) == 1:
+            print(_jsonpath(objs[0], expr), file=out)
+        else:
+            print(_jsonpath({"items": objs}, expr), file=out)
+    else:
+        wide = o == "wide"
+        all_ns = getattr(a, "all_namespaces", False)
+        k = kind or (objs[0].get("kind") if objs else "")
+        if k == "Pod":
+            txt = printers.pods_table(objs, wide, all_ns)
+        elif k == "Node":
+            txt = printers.nodes_table(objs, wide)
+        else:
+            txt = printers.generic_table(objs, k, all_ns)
+        if objs:
+            print(txt, file=out)
+        else:
+            print(f"No resources found.", file=out)
+
+
+def _read_files(paths) -> list[dict]:
+    docs = []
+    for p in paths:
+        if p == "-":
+            docs += load_manifests(sys.stdin.read())
+        elif os.path.isdir(p):
+            for f in sorted(os.listdir(p)):
+                if f.endswith((".yaml", ".yml", ".json")):
+                    docs += load_manifests(open(os.path.join(p, f)).read())
+        else:
+            docs += load_manifests(open(p).read())
+    return docs
+
+
+def _ns(a, ri=None):
+    if ri is not None and not ri.namespaced:
+        return ""
+    return "" if getattr(a, "all_namespaces", False) else (a.namespace or "default")
+
+
+def _split_targets(args):
+    """['pods', 'a', 'b'] | ['pod/a', 'node/b'] -> [(resource, name|None)]"""
+    out = []
+    if not args:
+        return out
+    if all("/" in x for x in args):
+        for x in args:
+            r, n = x.split("/", 1)
+            out.append((r, n))
+        return out
+    res = args[0].split(",")
+    names = args[1:]
+    for r in res:
+        if names:
+            out += [(r, n) for n in names]
+        else:
+            out.append((r, None))
+    return out
+
+
+async def cmd_get(c, a):
+    targets = _split_targets(a.args)
+    if not targets:
+        raise SystemExit("error: you must specify the type of resource to get")
+    for r, name in targets:
+        ri = SCHEME.resolve(r)
+        if ri is None:
+            raise SystemExit(f'error: the server doesn\'t have a resource type "{r}"')
+        ns = _ns(a, ri)
+        if name:
+            objs = [await c.get(ri.plural if not ri.group else f"{ri.plural}.{ri.group}", name, ns)]
+            _emit(objs, a, ri.kind, single=True)
+        else:
+            items, rv = await c.list(ri.plural if not ri.group else f"{ri.plural}.{ri.group}", ns, a.selector, a.field_selector)
+            for it in items:
+                it.setdefault("kind", ri.kind)
+                it.setdefault("apiVersion", ri.api_version)
+            _emit(items, a, ri.kind)
+            if a.watch:
+                async for typ, obj in c.watch(ri.plural, ns, rv, a.selector, a.field_selector):
+                    _emit([obj], a, ri.kind)
+
+
+async def cmd_describe(c, a):
+    for r, name in _split_targets(a.args):
+        ri = SCHEME.resolve(r)
+        ns = _ns(a, ri)
+        objs = [await c.get(ri.plural, name, ns)] if name else (await c.list(ri.plural, ns, a.selector))[0]
+        for o in objs:
+            o.setdefault("kind", ri.kind)
+            evs, _ = await c.list("events", m.namespace_of(o) or "default",
+                                  field_selector=f"involvedObject.name={m.name_of(o)},involvedObject.kind={ri.kind}")
+            print(printers.describe(o, evs))
+            print()
+
+
+async def _create_or_apply(c, a, apply=False):
+    for doc in _read_files(a.filename):
+        ri = SCHEME.for_object(doc)
+        if ri is None:
+            raise SystemExit(f"error: unknown kind {doc.get('apiVersion')}/{doc.get('kind')}")
+        ns = (m.namespace_of(doc) or a.namespace or "default") if ri.namespaced else ""
+        if ri.namespaced:
+            doc.setdefault("metadata", {})["namespace"] = ns
+        name = m.name_of(doc)
+        res = ri.plural if not ri.group else f"{ri.plural}.{ri.group}"
+        if apply and name:
+            cur = await c.get_or_none(res, name, ns)
+            if cur is not None:
+                patch = {k: v for k, v in doc.items() if k not in ("status",)}
+                patch.setdefault("metadata", {}).setdefault("annotations", {})[
+                    "kubectl.kubernetes.io/last-applied-configuration"] = json.dumps(doc, sort_keys=True)
+                await c.patch(res, name, patch, ns, patch_type="application/strategic-merge-patch+json")
+                print(f"{ri.kind.lower()}/{name} configured")
+                continue
+            doc.setdefault("metadata", {}).setdefault("annotations", {})[
+                "kubectl.kubernetes.io/last-applied-configuration"] = json.dumps(doc, sort_keys=True)
+        obj = await c.create(doc, ns)
+        print(f"{ri.kind.lower()}/{m.name_of(obj)} created")
+
+
+async def cmd_create(c, a):
+    await _create_or_apply(c, a)
+
+
+async def cmd_apply(c, a):
+    await _create_or_apply(c, a, apply=True)
+
+
+async def cmd_delete(c, a):
+    targets = []
+    if a.filename:
+        for d in _read_files(a.filename):
+            ri = SCHEME.for_object(d)
+            targets.append((ri, m.name_of(d), m.namespace_of(d) or a.namespace or "default"))
+    else:
+        for r, name in _split_targets(a.args):
+            ri = SCHEME.resolve(r)
+            ns = _ns(a, ri) or ("default" if ri.namespaced else "")
+            if name:
+                targets.append((ri, name, ns))
+            elif a.all or a.selector:
+                items, _ = await c.list(ri.plural, ns, a.selector)
+                targets += [(ri, m.name_of(i), m.namespace_of(i)) for i in items]
+    for ri, name, ns in targets:
+        res = ri.plural if not ri.group else f"{ri.plural}.{ri.group}"
+        try:
+            await c.delete(res, name, ns if ri.namespaced else "", grace=a.grace_period if a.grace_period >= 0 else None,
+                           propagation="Background" if a.cascade else "Orphan")
+            print(f'{ri.kind.lower()} "{name}" deleted')
+        except m.StatusError as e:
+            if not (a.ignore_not_found and m.is_not_found(e)):
+                print(f"Error from server ({e.reason}): {e.message}", file=sys.stderr)
+
+
+async def cmd_logs(c, a):
+    name = a.args[0].split("/", 1)[-1]
+    print(await c.logs(a.namespace or "default", name, a.container, a.tail if a.tail >= 0 else None), end="")
+
+
+async def cmd_exec(c, a):
+    name = a.args[0].split("/", 1)[-1]
+    pod = await c.get("pods", name, a.namespace or "default")
+    node = await c.get("nodes", pod["spec"]["nodeName"])
+    st = node.get("status") or {}
+    port = st["daemonEndpoints"]["kubeletEndpoint"]["Port"]
+    addr = next((x["address"] for x in st.get("addresses") or [] if x.get("type") == "InternalIP"), "127.0.0.1")
+    container = a.container or pod["spec"]["containers"][0]["name"]
+    import aiohttp
+    async with aiohttp.ClientSession() as s:
+        async with s.post(f"http://{addr}:{port}/run/{a.namespace or 'default'}/{name}/{container}",
+                          params=[("cmd", x) for x in a.command]) as r:
+            sys.stdout.write(await r.text())
+            return int(r.headers.get("X-Exit-Code", "0"))
+
+
+async def _meta_edit(c, a, field):
+    r, name = _split_targets(a.args[:1])[0] if "/" in a.args[0] else (a.args[0], a.args[1])
+    kvs = a.args[1:] if "/" in a.args[0] else a.args[2:]
+    ri = SCHEME.resolve(r)
+    patch = {}
+    for kv in kvs:
+        if kv.endswith("-"):
+            patch[kv[:-1]] = None
+        else:
+            k, v = kv.split("=", 1)
+            patch[k] = v
+    await c.patch(ri.plural, name, {"metadata": {field: patch}}, _ns(a, ri))
+    print(f"{ri.kind.lower()}/{name} {'labeled' if field == 'labels' else 'annotated'}")
+
+
+async def cmd_label(c, a):
+    await _meta_edit(c, a, "labels")
+
+
+async def cmd_annotate(c, a):
+    await _meta_edit(c, a, "annotations")
+
+
+async def cmd_cordon(c, a, value=True):
+    for n in a.args:
+        await c.patch("nodes", n.split("/", 1)[-1], {"spec": {"unschedulable": value or None}})
+        print(f"node/{n.split('/', 1)[-1]} {'cordoned' if value else 'uncordoned'}")
+
+
+async def cmd_uncordon(c, a):
+    await cmd_cordon(c, a, False)
+
+
+async def cmd_drain(c, a):
+    node = a.args[0].split("/", 1)[-1]
+    await cmd_cordon(c, argparse.Namespace(args=[node]), True)
+    pods, _ = await c.list("pods", "", field_selector=f"spec.nodeName={node}")
+    for p in pods:
+        ref = m.controller_ref(p) or {}
+        if ref.get("kind") == "DaemonSet" and a.ignore_daemonsets:
+            continue
+        await c.evict(m.namespace_of(p), m.name_of(p))
+        print(f"pod/{m.name_of(p)} evicted")
+    print(f"node/{node} drained")
+
+
+async def cmd_scale(c, a):
+    r, name = _split_targets(a.args)[0]
+    ri = SCHEME.resolve(r)
+    await c.patch(f"{ri.plural}.{ri.group}" if ri.group else ri.plural, name, {"spec": {"replicas": a.replicas}}, _ns(a, ri))
+    print(f"{ri.kind.lower()}/{name} scaled")
+
+
+async def cmd_patch(c, a):
+    r, name = _split_targets(a.args)[0] if "/" in a.args[0] else (a.args[0], a.args[1])
+    ri = SCHEME.resolve(r)
+    pt = {"json": "application/json-patch+json", "merge": "application/merge-patch+json",
+          "strategic": "application/strategic-merge-patch+json"}[a.type]
+    await c.patch(ri.plural, name, json.loads(a.patch), _ns(a, ri), patch_type=pt)
+    print(f"{ri.kind.lower()}/{name} patched")
+
+
+async def cmd_run(c, a):
+    c0 = {"name": a.args[0], "image": a.image}
+    if a.command:
+        c0["command"] = a.command
+    if a.gpus:
+        c0["resources"] = {"limits": {"amd.com/gpu": str(a.gpus)}}
+    pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": a.args[0], "labels": {"run": a.args[0]}},
+           "spec": {"restartPolicy": a.restart, "containers": [c0]}}
+    obj = await c.create(pod, a.namespace or "default")
+    print(f"pod/{m.name_of(obj)} created")
+
+
+async def cmd_top(c, a):
+    what = a.args[0] if a.args else "node"
+    nodes, _ = await c.list("nodes")
+    import aiohttp
+    rows = []
+    async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=10)) as s:
+        for n in nodes:
+            st = n.get("status") or {}
+            port = ((st.get("daemonEndpoints") or {}).get("kubeletEndpoint") or {}).get("Port")
+            addr = next((x["address"] for x in st.get("addresses") or [] if x.get("type") == "InternalIP"), "127.0.0.1")
+            if not port:
+                continue
+            try:
+                async with s.get(f"http://{addr}:{port}/stats/summary") as r:
+                    summ = await r.json()
+            except Exception:
+                continue
+            if what in ("node", "nodes", "no"):
+                mem = summ["node"]["memory"]
+                rows.append([m.name_of(n), f"{mem['usageBytes'] >> 20}Mi", str(len(summ["node"].get("accelerators") or []))])
+            else:  # gpu
+                owner = {}
+                for p in summ.get("pods") or []:
+                    for ct in p.get("containers") or []:
+                        for acc in ct.get("accelerators") or []:
+                            owner[acc["id"]] = f"{p['podRef']['namespace']}/{p['podRef']['name']}"
+                for acc in summ["node"].get("accelerators") or []:
+                    rows.append([m.name_of(n), acc["id"], acc["model"], f"{acc['dutyCycle']}%",
+                                 f"{acc['memoryUsed'] >> 20}Mi/{acc['memoryTotal'] >> 20}Mi", owner.get(acc["id"], "-")])
+    head = ["NAME", "MEMORY", "GPUS"] if what in ("node", "nodes", "no") else ["NODE", "GPU", "MODEL", "UTIL", "VRAM", "POD"]
+    print(printers.table([head] + rows))
+
+
+async def cmd_version(c, a):
+    from .. import GIT_VERSION
+    print(f"Client Version: {GIT_VERSION}")
+    try:
+        v = await c.request("GET", "/version")
+        print(f"Server Version: {v['gitVersion']}")
+    except Exception as e:
+        print(f"Server Version: unavailable ({e})")
+
+
+async def cmd_api_resources(c, a):
+    rows = [["NAME", "SHORTNAMES", "APIGROUP", "NAMESPACED", "KIND"]]
+    for ri in sorted(SCHEME.by_kind.values(), key=lambda r: (r.group, r.plural)):
+        rows.append([ri.plural, ",".join(ri.short_names), ri.group, str(ri.namespaced).lower(), ri.kind])
+    print(printers.table(rows))
+
+
+async def cmd_cluster_info(c, a):
+    print(f"Kubernetes master is running at {c.server}")
+
+
+async def cmd_wait(c, a):
+    r, name = _split_targets(a.args)[0]
+    ri = SCHEME.resolve(r)
+    cond = a.for_.split("=", 1)[1] if "=" in a.for_ else a.for_
+    end = time.time() + a.timeout
+    while time.time() < end:
+        o = await c.get_or_none(ri.plural, name, _ns(a, ri))
+        if a.for_ == "delete" and o is None:
+            print(f"{ri.kind.lower()}/{name} deleted")
+            return
+        if o is not None:
+            st = o.get("status") or {}
+            if st.get("phase") == cond or any(x.get("type") == cond and x.get("status") == "True" for x in st.get("conditions") or []):
+                print(f"{ri.kind.lower()}/{name} condition met")
+                return
+        await asyncio.sleep(0.2)
+    raise SystemExit(f"error: timed out waiting for the condition on {r}/{name}")
+
+
+COMMANDS = {"get": cmd_get, "describe": cmd_describe, "create": cmd_create, "apply": cmd_apply, "delete": cmd_delete,
+            "logs": cmd_logs, "exec": cmd_exec, "label": cmd_label, "annotate": cmd_annotate, "cordon": cmd_cordon,
+            "uncordon": cmd_uncordon, "drain": cmd_drain, "scale": cmd_scale, "patch": cmd_patch, "run": cmd_run,
+            "top": cmd_top, "version": cmd_version, "api-resources": cmd_api_resources, "cluster-info": cmd_cluster_info,
+            "wait": cmd_wait}
+
+
+def parser():
+    p = argparse.ArgumentParser(prog="kubectl", description="amdkube kubectl")
+    p.add_argument("--server", "-s", default=None)
+    p.add_argument("--token", default=None)
+    p.add_argument("-n", "--namespace", default=None)
+    sub = p.add_subparsers(dest="cmd", required=True)
+    for name in COMMANDS:
+        sp = sub.add_parser(name)
+        sp.add_argument("args", nargs="*")
+        sp.add_argument("-n", "--namespace", default=argparse.SUPPRESS)
+        sp.add_argument("-o", "--output", default=None)
+        sp.add_argument("-l", "--selector", default=None)
+        sp.add_argument("--field-selector", default=None)
+        sp.add_argument("-A", "--all-namespaces", action="store_true")
+        sp.add_argument("-w", "--watch", action="store_true")
+        sp.add_argument("-f", "--filename", action="append", default=[])
+        sp.add_argument("-c", "--container", default=None)
+        sp.add_argument("--tail", type=int, default=-1)
+        sp.add_argument("--all", action="store_true")
+        sp.add_argument("--grace-period", type=int, default=-1)
+        sp.add_argument("--cascade", type=lambda s: s != "false", default=True)
+        sp.add_argument("--ignore-not-found", action="store_true")
+        sp.add_argument("--ignore-daemonsets", action="store_true")
+        sp.add_argument("--replicas", type=int, default=1)
+        sp.add_argument("-p", "--patch", default="{}")
+        sp.add_argument("--type", default="strategic")
+        sp.add_argument("--image", default="busybox")
+        sp.add_argument("--gpus", type=int, default=0)
+        sp.add_argument("--restart", default="Always")
+        sp.add_argument("--for", dest="for_", default="condition=Ready")
+        sp.add_argument("--timeout", type=float, default=30.0)
+        sp.add_argument("--command", nargs=argparse.REMAINDER, default=None)
+    return p
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    cmd_tail = []
+    if "--" in argv:
+        i = argv.index("--")
+        argv, cmd_tail = argv[:i], argv[i + 1:]
+    a = parser().parse_args(argv)
+    if cmd_tail:
+        a.command = cmd_tail
+    elif a.command is None:
+        a.command = []
+
+    async def go():
+        c = _client(a)
+        try:
+            return await COMMANDS[a.cmd](c, a)
+        except m.StatusError as e:
+            print(f"Error from server ({e.reason}): {e.message}", file=sys.stderr)
+            return 1
+        finally:
+            await c.close()
+    rc = asyncio.run(go())
+    return rc if isinstance(rc, int) else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
