@@ -78,6 +78,8 @@ class ManagerImpl:
     # ---------------------------------------------------------------- lifecycle
     async def start(self):
         await self.watcher.start()
+        self._initial = set(self.watcher._known)  # sockets that existed before this kubelet started
+        self._settled: set[str] = set()
         self._tasks.append(asyncio.create_task(self._run(), name="devicemanager-run"))
         self._tasks.append(asyncio.create_task(self._run_removed(), name="devicemanager-removed"))
         if self.v1beta1_socket:
@@ -101,10 +103,25 @@ class ManagerImpl:
 
     async def _add(self, path, domain, kind="v1alpha2"):
         try:
-            await self.handler.new_endpoint(path, domain, kind)
+            e = await self.handler.new_endpoint(path, domain, kind)
+            # settled once the first ListAndWatch snapshot has been applied
+            for _ in range(100):
+                if e.store.devs() or e.ch.get_state() not in (grpc.ChannelConnectivity.READY, grpc.ChannelConnectivity.IDLE):
+                    break
+                await asyncio.sleep(0.01)
         except RegistrationError as e:
             self.registration_errors.append(str(e))
             log.warning("device plugin registration failed: %s", e)
+        finally:
+            getattr(self, "_settled", set()).add(path)
+
+    async def wait_initial_registration(self, timeout: float = 5.0):
+        """Kubelet restart: give plugins whose sockets already existed a bounded grace period to
+        re-register before pods are (re-)admitted (their devices must be known by then)."""
+        loop = asyncio.get_running_loop()
+        end = loop.time() + timeout
+        while loop.time() < end and not self._initial <= self._settled:
+            await asyncio.sleep(0.02)
 
     async def _run_removed(self):
         while True:
@@ -206,6 +223,9 @@ class ManagerStub:
         return self
 
     async def stop(self):
+        pass
+
+    async def wait_initial_registration(self, timeout: float = 5.0):
         pass
 
     def get_capacity(self):

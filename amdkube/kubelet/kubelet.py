@@ -144,6 +144,7 @@ class Kubelet:
         from .server import KubeletServer
         self.server = await KubeletServer(self).start(self.cfg.address, self.cfg.port)
         await self.register_node()
+        await self.dm.wait_initial_registration(5.0)
         self.informer = Informer(self.client, "pods", field_selector=f"spec.nodeName={self.node_name}")
         self.informer.add_handler(on_add=self._on_pod_add, on_update=self._on_pod_update, on_delete=self._on_pod_delete)
         self.informer.start()
@@ -395,6 +396,14 @@ class Kubelet:
         if uid not in self.admitted:
             if is_pod_terminal(pod):
                 self.admitted.add(uid)  # e.g. kubelet restart: nothing to run
+            elif await self._already_running(uid):
+                # kubelet restart: the pod was admitted by the previous incarnation and is running;
+                # never kill it because a device plugin has not re-registered yet
+                self.admitted.add(uid)
+                try:
+                    await self.dm.admit_pod(pod)  # refresh plugin annotations, best effort
+                except Exception:
+                    pass
             elif not await self._admit(pod):
                 return False
         if md.get("deletionTimestamp"):
@@ -434,6 +443,13 @@ class Kubelet:
                 asyncio.get_running_loop().call_later(rem + 0.05, self.dispatch, uid)
                 break
         return False
+
+    async def _already_running(self, uid: str) -> bool:
+        try:
+            rt = await self.runtime.pod_status(uid)
+        except Exception:
+            return False
+        return rt.ready_sandbox() is not None and bool(rt.running())
 
     async def _finalize_delete(self, pod):
         uid = m.uid_of(pod)

@@ -1,0 +1,153 @@
+"""Kubelet behaviour on an in-process node. Ports the fork's node e2e
+(test/e2e_node/gpu_device_plugin.go:45-143): GPU assignment survives a kubelet restart; a
+second pod gets a different GPU; after the plugin is removed capacity drops to 0 while running
+pods keep their GPUs, also across another kubelet restart. Plus restart policy / init
+containers / readiness probes / admission rejection / volumes + downward env."""
+import asyncio
+import os
+
+import pytest
+
+from amdkube.api import meta as m
+from amdkube.client import Client
+from amdkube.kubelet.kubelet import Kubelet
+from amdkube.localcluster import LocalCluster, wait_pod
+from tests.conftest import run
+
+
+def gpu_sleeper(name, secs=60):
+    return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "default"},
+            "spec": {"containers": [{"name": "c", "image": "busybox", "command": ["sh", "-c", f"echo $ROCR_VISIBLE_DEVICES; sleep {secs}"],
+                                     "resources": {"limits": {"amd.com/gpu": "1"}}}]}}
+
+
+async def restart_kubelet(lc: LocalCluster):
+    cfg = lc.kubelet.cfg
+    await lc.kubelet.stop()
+    await lc.kubelet.client.close()
+    lc.kubelet = await Kubelet(Client(lc.api.url), cfg, smi_backend=lc.backend).start()
+
+
+def test_gpu_assignment_survives_kubelet_and_plugin_restart():
+    async def go():
+        async with LocalCluster(gpus="fake", n_gpus=2, relist_period=0.2, node_status_update_frequency=0.5) as lc:
+            c = lc.client
+            await lc.wait_gpus(2)
+            await c.create(gpu_sleeper("p1"))
+            p1 = await wait_pod(c, "default", "p1", ("Running",), 20)
+            g1 = p1["spec"]["extendedResources"][0]["assigned"]
+            cid1 = p1["status"]["containerStatuses"][0]["containerID"]
+            await restart_kubelet(lc)
+            await asyncio.sleep(1.0)
+            p1 = await c.get("pods", "p1", "default")
+            assert p1["status"]["phase"] == "Running"
+            assert p1["status"]["containerStatuses"][0]["containerID"] == cid1          # not restarted
+            assert p1["spec"]["extendedResources"][0]["assigned"] == g1                  # same GPU
+            await c.create(gpu_sleeper("p2"))
+            p2 = await wait_pod(c, "default", "p2", ("Running",), 20)
+            assert p2["spec"]["extendedResources"][0]["assigned"] != g1                  # different GPU
+            # delete the device plugin: capacity → 0, running pods keep their GPUs
+            await lc.plugin.stop()
+            for _ in range(100):
+                node = await c.get("nodes", lc.node_name)
+                if (node["status"].get("capacity") or {}).get("amd.com/gpu") in (None, "0"):
+                    break
+                await asyncio.sleep(0.1)
+            assert "amd.com/gpu" not in (node["status"].get("extendedResources") or {})
+            await restart_kubelet(lc)
+            await asyncio.sleep(1.0)
+            for name, cid in (("p1", cid1),):
+                p = await c.get("pods", name, "default")
+                assert p["status"]["phase"] == "Running" and p["status"]["containerStatuses"][0]["containerID"] == cid
+    run(go(), 120)
+
+
+def test_restart_policy_init_containers_probes_and_volumes():
+    async def go():
+        async with LocalCluster(gpus="none", relist_period=0.2) as lc:
+            c = lc.client
+            await c.create({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "cfg", "namespace": "default"},
+                            "data": {"greeting": "hello-cm"}})
+            pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "w", "namespace": "default", "labels": {"app": "w"}},
+                   "spec": {"restartPolicy": "OnFailure",
+                            "volumes": [{"name": "work", "emptyDir": {}}, {"name": "cfg", "configMap": {"name": "cfg"}}],
+                            "initContainers": [{"name": "init", "image": "busybox", "command": ["sh", "-c", "echo ready > $AMDKUBE_ROOTFS/work/flag"],
+                                                "volumeMounts": [{"name": "work", "mountPath": "/work"}]}],
+                            "containers": [{"name": "main", "image": "busybox",
+                                            "command": ["sh", "-c", "cat $AMDKUBE_ROOTFS/work/flag; cat $AMDKUBE_ROOTFS/etc/cfg/greeting; echo; echo POD=$MY_POD; sleep 30"],
+                                            "env": [{"name": "MY_POD", "valueFrom": {"fieldRef": {"fieldPath": "metadata.name"}}}],
+                                            "volumeMounts": [{"name": "work", "mountPath": "/work"}, {"name": "cfg", "mountPath": "/etc/cfg"}],
+                                            "readinessProbe": {"exec": {"command": ["true"]}, "periodSeconds": 1}}]}}
+            await c.create(pod)
+            p = await wait_pod(c, "default", "w", ("Running",), 20)
+            for _ in range(100):
+                p = await c.get("pods", "w", "default")
+                if p["status"]["containerStatuses"][0]["ready"]:
+                    break
+                await asyncio.sleep(0.1)
+            assert p["status"]["containerStatuses"][0]["ready"]
+            assert p["status"]["initContainerStatuses"][0]["state"]["terminated"]["exitCode"] == 0
+            logs = (await c.logs("default", "w", "main")).split()
+            assert logs == ["ready", "hello-cm", "POD=w"], logs
+            # OnFailure: failing container is restarted (restartCount increments)
+            await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "crash", "namespace": "default"},
+                            "spec": {"restartPolicy": "OnFailure", "containers": [{"name": "c", "image": "busybox", "command": ["sh", "-c", "exit 1"]}]}})
+            lc.kubelet.runtime.backoff.clear()
+            import amdkube.kubelet.kuberuntime as kr
+            old = kr.BACKOFF_BASE
+            kr.BACKOFF_BASE = 0.2
+            try:
+                for _ in range(150):
+                    p = await c.get("pods", "crash", "default")
+                    cs = (p["status"].get("containerStatuses") or [{}])[0]
+                    if cs.get("restartCount", 0) >= 1:
+                        break
+                    await asyncio.sleep(0.1)
+                assert cs.get("restartCount", 0) >= 1, p["status"]
+            finally:
+                kr.BACKOFF_BASE = old
+    run(go(), 120)
+
+
+def test_admission_rejects_pod_that_does_not_fit():
+    async def go():
+        async with LocalCluster(gpus="none", relist_period=0.2, kubelet_kw={"cpu_capacity": 2}) as lc:
+            c = lc.client
+            # bypass the scheduler (nodeName preset) so the kubelet's own admission decides
+            await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "big", "namespace": "default"},
+                            "spec": {"nodeName": lc.node_name, "containers": [{"name": "c", "image": "busybox", "command": ["sleep", "5"],
+                                                                                "resources": {"requests": {"cpu": "4"}}}]}})
+            p = await wait_pod(c, "default", "big", ("Failed",), 20)
+            assert p["status"]["reason"] == "OutOfcpu"
+            # a GPU pod pinned to a node without an assignment is rejected by the DeviceManager
+            await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "nogpu", "namespace": "default"},
+                            "spec": {"nodeName": lc.node_name, "extendedResources": [{"name": "g", "resources": {"limits": {"amd.com/gpu": "1"}}}],
+                                     "containers": [{"name": "c", "image": "busybox", "extendedResourceRequests": ["g"]}]}})
+            p = await wait_pod(c, "default", "nogpu", ("Failed",), 20)
+            assert p["status"]["reason"] == "UnexpectedAdmissionError"
+    run(go(), 60)
+
+
+def test_kubelet_http_api_and_metrics():
+    async def go():
+        async with LocalCluster(gpus="fake", n_gpus=2, relist_period=0.2) as lc:
+            await lc.wait_gpus(2)
+            await lc.client.create(gpu_sleeper("s", 20))
+            await wait_pod(lc.client, "default", "s", ("Running",), 20)
+            import aiohttp
+            base = f"http://127.0.0.1:{lc.kubelet.server.port}"
+            async with aiohttp.ClientSession() as s:
+                assert (await (await s.get(base + "/healthz")).text()) == "ok"
+                pods = await (await s.get(base + "/pods")).json()
+                assert [p["metadata"]["name"] for p in pods["items"]] == ["s"]
+                summ = await (await s.get(base + "/stats/summary")).json()
+                assert len(summ["node"]["accelerators"]) == 2
+                acc = summ["pods"][0]["containers"][0]["accelerators"]
+                assert len(acc) == 1 and acc[0]["make"] == "amd"
+                cad = await (await s.get(base + "/metrics/cadvisor")).text()
+                assert 'container_accelerator_memory_total_bytes{container_name="c",pod_name="s"' in cad
+                met = await (await s.get(base + "/metrics")).text()
+                assert "kubelet_device_plugin_registration_count_total" in met and "kubelet_pod_start_latency_microseconds" in met
+                logs = await (await s.get(base + "/containerLogs/default/s/c")).text()
+                assert logs.strip().startswith("GPU-")
+    run(go(), 60)
