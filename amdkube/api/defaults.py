@@ -6,10 +6,27 @@ pkg/apis/apps/v1 defaults for DaemonSet/ReplicaSet/Deployment.
 """
 from __future__ import annotations
 
+from .quantity import Quantity, QuantityError
 from .scheme import register_hooks
 
 
+def normalize_resource_list(rl: dict | None):
+    """Quantities are strings on the wire ("2", "500m", "288Gi"), whatever the manifest held."""
+    if not rl:
+        return
+    for k, v in list(rl.items()):
+        if not isinstance(v, str):
+            try:
+                rl[k] = str(Quantity(v))
+            except (QuantityError, TypeError, ValueError):
+                pass
+
+
 def _default_container(c: dict):
+    res = c.get("resources")
+    if res:
+        normalize_resource_list(res.get("limits"))
+        normalize_resource_list(res.get("requests"))
     c.setdefault("terminationMessagePath", "/dev/termination-log")
     c.setdefault("terminationMessagePolicy", "File")
     img = c.get("image") or ""
@@ -44,6 +61,8 @@ def default_pod_spec(spec: dict):
     # fork: ExtendedResources requests := limits (defaults.go:164-179)
     for pres in spec.get("extendedResources") or []:
         res = pres.setdefault("resources", {})
+        normalize_resource_list(res.get("limits"))
+        normalize_resource_list(res.get("requests"))
         lim = res.get("limits") or {}
         if lim and not res.get("requests"):
             res["requests"] = dict(lim)
@@ -62,6 +81,8 @@ def default_pod(pod: dict):
 def default_node(node: dict):
     node.setdefault("spec", {})
     st = node.setdefault("status", {})
+    normalize_resource_list(st.get("capacity"))
+    normalize_resource_list(st.get("allocatable"))
     if st.get("capacity") and not st.get("allocatable"):
         st["allocatable"] = dict(st["capacity"])
     return node

@@ -59,6 +59,7 @@ class ResourceV2(Plugin):
         if a.subresource or a.resource != "pods":
             return
         spec = a.obj.setdefault("spec", {})
+        existing = {p.get("name"): p for p in spec.get("extendedResources") or []}
         for kind in ("initContainers", "containers"):
             for c in spec.get(kind) or []:
                 res = c.get("resources") or {}
@@ -66,6 +67,15 @@ class ResourceV2(Plugin):
                 for rname in [r for r in lim if r in self.resource_names]:
                     val = lim[rname]
                     if Quantity(val).is_zero():
+                        continue
+                    # UPDATE of an already converted pod (e.g. `kubectl apply` of the original
+                    # manifest): reuse the container's existing extended resource, do not mint a new one
+                    reuse = [ref for ref in c.get("extendedResourceRequests") or []
+                             if ((existing.get(ref) or {}).get("resources") or {}).get("limits", {}).get(rname) is not None
+                             and Quantity(existing[ref]["resources"]["limits"][rname]) == Quantity(val)]
+                    if a.operation == UPDATE and reuse:
+                        lim.pop(rname, None)
+                        (res.get("requests") or {}).pop(rname, None)
                         continue
                     name = str(uuid.uuid4())
                     spec.setdefault("extendedResources", []).append({

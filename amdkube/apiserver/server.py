@@ -198,7 +198,9 @@ class APIServer:
         if rest and rest[0] == "watch":
             watch, rest = True, rest[1:]
         ns = ""
-        if len(rest) >= 3 and rest[0] == "namespaces":
+        # /namespaces/<ns>/<resource>... vs the namespace object's own subresources
+        # (/namespaces/<name>/status, /namespaces/<name>/finalize)
+        if len(rest) >= 3 and rest[0] == "namespaces" and not (len(rest) == 3 and rest[2] in ("status", "finalize")):
             ns, rest = rest[1], rest[2:]
         resource = rest[0] if rest else None
         name = rest[1] if len(rest) > 1 else None

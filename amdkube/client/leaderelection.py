@@ -22,7 +22,9 @@ ANNOTATION = "control-plane.alpha.kubernetes.io/leader"
 
 
 def _ts(t: float) -> str:
-    return time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(t))
+    # microsecond resolution: every renew must change the record, or followers with a short
+    # lease would mistake an unchanged (same-second) record for a dead leader
+    return time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime(t)) + f".{int((t % 1) * 1e6):06d}Z"
 
 
 class LeaderElector:
@@ -58,7 +60,8 @@ class LeaderElector:
         if cur != self.observed:
             self.observed, self.observed_time = cur, now
         holder = cur.get("holderIdentity")
-        if holder and holder != self.identity and self.observed_time + cur.get("leaseDurationSeconds", self.lease) > now:
+        # like client-go, the observer's own LeaseDuration decides expiry (leaderelection.go:152+)
+        if holder and holder != self.identity and self.observed_time + self.lease > now:
             return False
         if holder == self.identity:
             rec["acquireTime"] = cur.get("acquireTime", rec["acquireTime"])

@@ -55,7 +55,8 @@ def _jsonpath(obj, expr: str):
     return " ".join(json.dumps(x) if isinstance(x, (dict, list)) else str(x) for x in cur)
 
 
-def _emit(objs, a, kind=None, single=False, out=sys.stdout):
+def _emit(objs, a, kind=None, single=False, out=None):
+    out = out or sys.stdout
     o = a.output or ""
     if o == "json":
         if single and len(objs) == 1:
