@@ -13,7 +13,7 @@ from __future__ import annotations
 import math
 import re
 from fractions import Fraction
-from functools import total_ordering
+from functools import lru_cache, total_ordering
 
 DECIMAL_SI = "DecimalSI"
 BINARY_SI = "BinarySI"
@@ -100,6 +100,7 @@ class Quantity:
         return str(self)
 
 
+@lru_cache(maxsize=8192)
 def _parse(s: str):
     s = s.strip()
     if not s:

@@ -9,6 +9,8 @@ here, against node state in the registry).
 """
 from __future__ import annotations
 
+import json
+
 from .helpers import HEALTHY, UNHEALTHY, is_extended_resource_name, is_native_resource
 from .labels import (SelectorError, is_dns1123_label, is_dns1123_subdomain, is_qualified_name,
                      is_valid_label_value, node_requirements_as_selector, selector_from_label_selector)
@@ -240,7 +242,7 @@ _MUTABLE_CONTAINER_FIELDS = ("image",)
 
 def _strip_mutable(spec: dict) -> dict:
     import copy
-    s = copy.deepcopy(spec)
+    s = json.loads(json.dumps(spec))
     for kind in ("containers", "initContainers"):
         for c in s.get(kind) or []:
             for f in _MUTABLE_CONTAINER_FIELDS:

@@ -276,13 +276,13 @@ class ResourceStore:
                 md.pop(k, None)
         new["apiVersion"], new["kind"] = self.ri.api_version, self.ri.kind
         if subresource == "status":
-            new["spec"] = copy.deepcopy(cur.get("spec"))
-            keep = copy.deepcopy(cmd)
+            new["spec"] = m.deepcopy(cur.get("spec"))
+            keep = m.deepcopy(cmd)
             keep["resourceVersion"] = md.get("resourceVersion", cmd.get("resourceVersion"))
             new["metadata"] = keep
         elif self.has_status:
             if "status" in cur:
-                new["status"] = copy.deepcopy(cur["status"])
+                new["status"] = m.deepcopy(cur["status"])
             else:
                 new.pop("status", None)
         if self.generation:
@@ -316,7 +316,7 @@ class ResourceStore:
             if patch is not None:
                 new = apply_patch(cur, patch, content_type)
             else:
-                new = copy.deepcopy(obj)
+                new = m.deepcopy(obj)
             nmd = new.setdefault("metadata", {})
             if nmd.get("name", name) != name:
                 raise m.bad_request("the name of the object does not match the name on the URL")
@@ -370,8 +370,7 @@ class ResourceStore:
         ns_finalizers = self.ri.plural == "namespaces" and ((cur.get("spec") or {}).get("finalizers"))
         if graceful or finalizers or ns_finalizers:
             def mark(c):
-                c = copy.deepcopy(c)
-                cm = c.setdefault("metadata", {})
+                cm = c.setdefault("metadata", {})  # c is a fresh decode: mutate in place
                 if precond_uid and cm.get("uid") != precond_uid:
                     raise m.conflict(self.ri.plural, name, "Precondition failed: UID mismatch")
                 if not cm.get("deletionTimestamp"):
@@ -505,7 +504,7 @@ class Registry:
 
         def assign(cur):
             nonlocal node
-            pod = copy.deepcopy(cur)
+            pod = cur  # freshly decoded from the store by guaranteed_update: safe to mutate
             md = pod.setdefault("metadata", {})
             if md.get("deletionTimestamp"):
                 raise m.conflict("pods", name, "pod is being deleted, cannot be assigned to a host")

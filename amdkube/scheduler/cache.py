@@ -145,13 +145,23 @@ def nonzero_requests(pod: dict) -> tuple[int, int]:
     return cpu, mem
 
 
+def _has_anti_affinity(pod) -> bool:
+    return bool((((pod.get("spec") or {}).get("affinity") or {}).get("podAntiAffinity") or {})
+                .get("requiredDuringSchedulingIgnoredDuringExecution"))
+
+
 class SchedulerCache:
     def __init__(self, ttl: float = 30.0):
+        self.anti_affinity_pods = 0  # pods carrying required anti-affinity (MatchInterPodAffinity fast path)
         self.nodes: dict[str, NodeInfo] = {}
         self.pod_node: dict[str, str] = {}          # pod key -> node name
         self.pod_states: dict[str, dict] = {}       # pod key -> pod
         self.assumed: dict[str, float | None] = {}  # pod key -> deadline (None until binding finished)
         self.ttl = ttl
+
+    def _track(self, pod, delta):
+        if _has_anti_affinity(pod):
+            self.anti_affinity_pods += delta
 
     def _ni(self, name) -> NodeInfo:
         ni = self.nodes.get(name)
@@ -190,6 +200,7 @@ class SchedulerCache:
         self.pod_node[key] = node
         self.pod_states[key] = pod
         self.assumed[key] = None
+        self._track(pod, 1)
 
     def finish_binding(self, pod: dict):
         key = m.key_of(pod)
@@ -203,7 +214,9 @@ class SchedulerCache:
         node = self.pod_node.pop(key, None)
         if node and node in self.nodes:
             self.nodes[node].remove_pod(key)
-        self.pod_states.pop(key, None)
+        old = self.pod_states.pop(key, None)
+        if old is not None:
+            self._track(old, -1)
         self.assumed.pop(key, None)
 
     def add_pod(self, pod: dict):
@@ -215,11 +228,15 @@ class SchedulerCache:
             old_node = self.pod_node.get(key)
             if old_node and old_node in self.nodes:
                 self.nodes[old_node].remove_pod(key)
+            old = self.pod_states.get(key)
+            if old is not None:
+                self._track(old, -1)
         elif key in self.pod_states:
             self.remove_pod(self.pod_states[key])
         self._ni(node).add_pod(key, pod)
         self.pod_node[key] = node
         self.pod_states[key] = pod
+        self._track(pod, 1)
 
     def update_pod(self, old: dict, new: dict):
         self.add_pod(new)
@@ -232,7 +249,9 @@ class SchedulerCache:
             ni.remove_pod(key)
             if ni.node is None and not ni.pods:
                 del self.nodes[node]
-        self.pod_states.pop(key, None)
+        old = self.pod_states.pop(key, None)
+        if old is not None:
+            self._track(old, -1)
         self.assumed.pop(key, None)
 
     def is_assumed(self, pod) -> bool:

@@ -22,6 +22,11 @@ from .priorities import PRIORITIES
 log = logging.getLogger("amdkube.scheduler")
 
 
+# priorities whose per-node value depends only on that node and the pod (cacheable per node generation)
+LOCAL_PRIORITIES = {"LeastRequestedPriority", "MostRequestedPriority", "BalancedResourceAllocation",
+                    "NodePreferAvoidPodsPriority", "ImageLocalityPriority", "GPUTopologyPriority"}
+
+
 class FitError(Exception):
     def __init__(self, pod, n_nodes, failed: dict):
         self.pod, self.n_nodes, self.failed = pod, n_nodes, failed
@@ -51,11 +56,32 @@ class GenericScheduler:
         self.use_topology = use_topology
         self.last_index = 0
         self.trace_threshold = trace_threshold
+        self.ecache: dict[str, dict[str, tuple]] = {}
+        self.ecache_hits = 0
 
     def _ctx(self, nodes):
-        anti = any((((p.get("spec") or {}).get("affinity") or {}).get("podAntiAffinity") or {})
-                   for ni in nodes for p in ni.pods.values())
-        return Context(nodes, anti)
+        return Context(nodes, self.cache.anti_affinity_pods > 0)
+
+    # Equivalence cache (reference plugin/pkg/scheduler/core/equivalence_cache.go:38): pods with the
+    # same scheduling-relevant spec get the same per-node answer as long as the node is unchanged.
+    # Keyed by (equivalence class, node) and validated by the node's generation, which moves on
+    # every node update and every pod add/remove on that node — so only nodes that changed since
+    # the last identical pod are re-evaluated. Pods with inter-pod (anti-)affinity, or any cluster
+    # with anti-affinity pods, bypass it (their answer depends on other nodes).
+    def _equiv_key(self, pi):
+        if pi.pod_affinity or pi.pod_anti_affinity or pi.pref_affinity or pi.pref_anti or self.cache.anti_affinity_pods:
+            return None
+        if pi.ext_error:
+            return None
+        spec = pi.spec
+        import json as _json
+        rel = {"c": [(c.get("resources"), c.get("ports")) for c in spec.get("containers") or []],
+               "i": [c.get("resources") for c in spec.get("initContainers") or []],
+               "ns": spec.get("nodeSelector"), "aff": spec.get("affinity"), "tol": spec.get("tolerations"),
+               "nn": spec.get("nodeName"), "x": [(r.get("resources"), r.get("affinity")) for r in spec.get("extendedResources") or []],
+               "v": [v for v in spec.get("volumes") or [] if len(v) > 1 and "emptyDir" not in v],
+               "o": (pi.owner or {}).get("uid"), "be": pi.best_effort}
+        return _json.dumps(rel, sort_keys=True, separators=(",", ":"))
 
     def pod_fits_on_node(self, pi, ni, ctx) -> tuple[bool, list[str]]:
         reasons = []
@@ -74,8 +100,21 @@ class GenericScheduler:
         ctx = self._ctx(nodes) if (pi.pod_affinity or pi.pod_anti_affinity) or any(
             n == "MatchInterPodAffinity" for n, _ in self.predicates) else None
         fit, failed = [], {}
+        ek = self._equiv_key(pi)
+        pi.equiv = ek
+        cache = self.ecache.setdefault(ek, {}) if ek is not None else None
+        if cache is not None and len(self.ecache) > 4096:
+            self.ecache.clear()
+            cache = self.ecache.setdefault(ek, {})
         for ni in nodes:
-            ok, reasons = self.pod_fits_on_node(pi, ni, ctx)
+            hit = cache.get(ni.name) if cache is not None else None
+            if hit is not None and hit[0] == ni.generation:
+                ok, reasons = hit[1], hit[2]
+                self.ecache_hits += 1
+            else:
+                ok, reasons = self.pod_fits_on_node(pi, ni, ctx)
+                if cache is not None:
+                    cache[ni.name] = (ni.generation, ok, reasons, None)
             if ok:
                 fit.append(ni)
             else:
@@ -96,7 +135,30 @@ class GenericScheduler:
         if not self.priorities and not self.extenders:
             return [1.0] * len(nodes)
         total = [0.0] * len(nodes)
-        for name, fn, w in self.priorities:
+        # per-node scores depend only on (pod class, node state) unless a priority normalises across
+        # nodes; only the normalising ones (spread, affinity, taints) are recomputed every time
+        cache = self.ecache.get(pi.equiv) if getattr(pi, "equiv", None) is not None else None
+        local = [(n, fn, w) for n, fn, w in self.priorities if n in LOCAL_PRIORITIES]
+        others = [(n, fn, w) for n, fn, w in self.priorities if n not in LOCAL_PRIORITIES]
+        need = []
+        for i, ni in enumerate(nodes):
+            hit = cache.get(ni.name) if cache is not None else None
+            if hit is not None and hit[0] == ni.generation and hit[3] is not None:
+                total[i] += hit[3]
+            else:
+                need.append(i)
+        if need:
+            sub = [nodes[i] for i in need]
+            part = [0.0] * len(sub)
+            for name, fn, w in local:
+                for j, s in enumerate(fn(pi, sub, ctx)):
+                    part[j] += s * w
+            for j, i in enumerate(need):
+                total[i] += part[j]
+                if cache is not None and nodes[i].name in cache and cache[nodes[i].name][0] == nodes[i].generation:
+                    g, ok, reasons, _ = cache[nodes[i].name]
+                    cache[nodes[i].name] = (g, ok, reasons, part[j])
+        for name, fn, w in others:
             scores = fn(pi, nodes, ctx)
             for i, s in enumerate(scores):
                 total[i] += s * w

@@ -19,8 +19,11 @@ MAX = 10.0
 
 
 def _cpu_mem(pi):
-    from .cache import nonzero_requests
-    return nonzero_requests(pi.pod)
+    nz = getattr(pi, "_nz", None)
+    if nz is None:
+        from .cache import nonzero_requests
+        nz = pi._nz = nonzero_requests(pi.pod)
+    return nz
 
 
 def least_requested(pi, nodes, ctx=None):

@@ -134,6 +134,10 @@ class MVCCStore:
     def __init__(self, data_dir: str | None = None, history: int = 200_000, max_queue: int = 500_000,
                  snapshot_every: int = 50_000, fsync: bool = False):
         self.kv: dict[str, KV] = {}
+        # keys bucketed by their first two path components ("/registry/pods/"), so a range over one
+        # resource never scans the others (admission lists quotas/limitranges on every create)
+        self.buckets: dict[str, dict[str, KV]] = {}
+        self._sorted: dict[str, list[str]] = {}
         self.rev = 0
         self.compact_rev = 0
         self.history: collections.deque[Event] = collections.deque()
@@ -156,17 +160,53 @@ class MVCCStore:
     def get(self, key: str) -> KV | None:
         return self.kv.get(key)
 
+    @staticmethod
+    def _bucket_of(key: str) -> str:
+        i = key.find("/", 1)
+        j = key.find("/", i + 1) if i >= 0 else -1
+        return key[:j + 1] if j >= 0 else key
+
+    def _index_put(self, key: str, kv: KV):
+        b = self._bucket_of(key)
+        bucket = self.buckets.setdefault(b, {})
+        if key not in bucket:
+            self._sorted.pop(b, None)
+        bucket[key] = kv
+
+    def _index_del(self, key: str):
+        b = self._bucket_of(key)
+        bucket = self.buckets.get(b)
+        if bucket is not None and bucket.pop(key, None) is not None:
+            self._sorted.pop(b, None)
+
+    def _candidates(self, prefix: str) -> list[str]:
+        b = self._bucket_of(prefix)
+        if len(b) <= len(prefix) and prefix.startswith(b) and b.endswith("/"):
+            keys = self._sorted.get(b)
+            if keys is None:
+                keys = self._sorted[b] = sorted(self.buckets.get(b, ()))
+            if b == prefix:
+                return keys
+            import bisect
+            lo = bisect.bisect_left(keys, prefix)
+            hi = bisect.bisect_left(keys, prefix + "￿")
+            return keys[lo:hi]
+        return sorted(k for k in self.kv if k.startswith(prefix))
+
     def range(self, prefix: str, limit: int = 0, start_after: str | None = None):
         """Keys with `prefix`, sorted; returns (kvs, rev, more)."""
         with self._lock:
-            keys = sorted(k for k in self.kv if k.startswith(prefix) and (start_after is None or k > start_after))
+            keys = self._candidates(prefix)
+            if start_after is not None:
+                import bisect
+                keys = keys[bisect.bisect_right(keys, start_after):]
             more = False
             if limit and len(keys) > limit:
                 keys, more = keys[:limit], True
             return [self.kv[k] for k in keys], self.rev, more
 
     def count(self, prefix: str) -> int:
-        return sum(1 for k in self.kv if k.startswith(prefix))
+        return len(self._candidates(prefix))
 
     # ------------------------------------------------------------- mutations
     def put(self, key: str, value, expect_mod_rev: int | None = None) -> KV:
@@ -189,6 +229,7 @@ class MVCCStore:
             new = KV(key, data, cur.create_rev if cur else rev, rev, (cur.version + 1) if cur else 1)
             self.rev = rev
             self.kv[key] = new
+            self._index_put(key, new)
             self._commit(Event(PUT, new, cur, rev), {"r": rev, "o": "p", "k": key, "v": _b(data)})
             return new
 
@@ -202,6 +243,7 @@ class MVCCStore:
             rev = self.rev + 1
             self.rev = rev
             del self.kv[key]
+            self._index_del(key)
             tomb = KV(key, cur.value, cur.create_rev, rev, 0)
             self._commit(Event(DELETE, tomb, cur, rev), {"r": rev, "o": "d", "k": key})
             return cur
@@ -300,6 +342,8 @@ class MVCCStore:
                         self.kv.pop(key, None)
                     self.rev = r
             self.compact_rev = self.rev
+        for key, kv in self.kv.items():
+            self._index_put(key, kv)
 
     def close(self):
         for w in list(self.watchers):
