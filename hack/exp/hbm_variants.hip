@@ -1,0 +1,56 @@
+// Experiment: HBM copy/read bandwidth vs grid size, unroll depth and non-temporal access.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void copy_k(const v4u* __restrict__ s, v4u* __restrict__ d, size_t n) {
+  const size_t st = (size_t)gridDim.x * blockDim.x;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + (U - 1) * st < n; i += U * st) {
+    v4u v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(s + i + u * st) : s[i + u * st];
+#pragma unroll
+    for (int u = 0; u < U; ++u) { if (NT) __builtin_nontemporal_store(v[u], d + i + u * st); else d[i + u * st] = v[u]; }
+  }
+  for (; i < n; i += st) d[i] = s[i];
+}
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void read_k(const v4u* __restrict__ s, size_t n, unsigned* sink) {
+  const size_t st = (size_t)gridDim.x * blockDim.x;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned acc = 0;
+  for (; i + (U - 1) * st < n; i += U * st) {
+    v4u v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(s + i + u * st) : s[i + u * st];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  for (; i < n; i += st) { v4u v = s[i]; acc ^= v.x ^ v.y ^ v.z ^ v.w; }
+  if (acc == 0x9e3779b9u) sink[0] = acc;
+}
+template <typename F> float timeit(F f, int it) {
+  hipEvent_t a, b; (void)hipEventCreate(&a); (void)hipEventCreate(&b);
+  f(); (void)hipEventRecord(a); for (int i = 0; i < it; ++i) f(); (void)hipEventRecord(b); (void)hipEventSynchronize(b);
+  float ms; (void)hipEventElapsedTime(&ms, a, b); return ms / it;
+}
+int main() {
+  size_t bytes = 4ull << 30, n = bytes / 16;
+  v4u *s, *d; unsigned* sink;
+  if (hipMalloc(&s, bytes) || hipMalloc(&d, bytes) || hipMalloc(&sink, 4)) return 1;
+  (void)hipMemset(s, 1, bytes); (void)hipMemset(d, 0, bytes);
+  printf("[");
+  bool first = true;
+  for (int per_cu : {4, 8, 16, 32}) {
+    int grid = 256 * per_cu;
+#define RUN(U, NT) { \
+      float c = timeit([&] { hipLaunchKernelGGL((copy_k<U, NT>), dim3(grid), dim3(256), 0, 0, s, d, n); }, 10); \
+      float r = timeit([&] { hipLaunchKernelGGL((read_k<U, NT>), dim3(grid), dim3(256), 0, 0, s, n, sink); }, 10); \
+      printf("%s{\"per_cu\":%d,\"unroll\":%d,\"nt\":%d,\"copy_gbps\":%.0f,\"read_gbps\":%.0f}", first ? "" : ",", per_cu, U, NT, 2.0 * bytes / (c * 1e6), bytes / (r * 1e6)); first = false; }
+    RUN(4, false) RUN(8, false) RUN(4, true) RUN(8, true) RUN(2, false)
+  }
+  printf("]\n");
+  return 0;
+}

@@ -12,6 +12,9 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run via gpurun)")
     config.addinivalue_line("markers", "slow: long-running test")
+    # native artefacts are not versioned: (re)build whatever is missing or stale (no-op when fresh)
+    from native import build as nb
+    nb.build(sanitize=True)
 
 
 def run(coro, timeout=60):
