@@ -9,6 +9,8 @@ gets). Upstream helpers: IsExtendedResourceName (helpers.go), resource request s
 """
 from __future__ import annotations
 
+import re
+
 from .labels import is_qualified_name, node_requirements_as_selector, Selector
 from .quantity import Quantity
 
@@ -95,16 +97,24 @@ def pod_assigned_devices(pod: dict) -> dict[str, set[str]]:
     return out
 
 
-def pod_gpu_request(pod: dict, rname: str = GPU_RESOURCE) -> int:
+_PARTITION_RE = re.compile(r"^amd\.com/(spx|dpx|qpx|cpx)_nps[12]$")
+
+
+def is_gpu_resource(rname: str) -> bool:
+    """amd.com/gpu or one of the MI355X partition resources (amd.com/cpx_nps2, ...)."""
+    return rname == GPU_RESOURCE or bool(_PARTITION_RE.match(rname))
+
+
+def pod_gpu_request(pod: dict, rname: str | None = None) -> int:
+    """GPUs (or GPU partitions) the pod asks for; rname=None counts every GPU resource."""
+    match = is_gpu_resource if rname is None else (lambda r: r == rname)
     n = 0
     for pres in (pod.get("spec") or {}).get("extendedResources") or []:
         lim = (pres.get("resources") or {}).get("limits") or {}
-        if rname in lim:
-            n += Quantity(lim[rname]).value()
+        n += sum(Quantity(v).value() for r, v in lim.items() if match(r))
     for c in (pod.get("spec") or {}).get("containers") or []:
         lim = (c.get("resources") or {}).get("limits") or {}
-        if rname in lim:
-            n += Quantity(lim[rname]).value()
+        n += sum(Quantity(v).value() for r, v in lim.items() if match(r))
     return n
 
 

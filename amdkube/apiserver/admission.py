@@ -49,10 +49,14 @@ class Plugin:
         pass
 
 
+# MI355X partition resources advertised by the AMD plugin's "mixed" naming strategy
+PARTITION_RESOURCES = tuple(f"amd.com/{cp}_{mp}" for cp in ("spx", "dpx", "qpx", "cpx") for mp in ("nps1", "nps2"))
+
+
 class ResourceV2(Plugin):
     name = "ResourceV2"
 
-    def __init__(self, resource_names=(GPU_RESOURCE,)):
+    def __init__(self, resource_names=(GPU_RESOURCE,) + PARTITION_RESOURCES):
         self.resource_names = tuple(resource_names)
 
     def admit(self, a, ctx):

@@ -190,21 +190,34 @@ def device_plugin(argv):
     ap.add_argument("--resource-name", default="amd.com/gpu")
     ap.add_argument("--health-interval", type=float, default=10.0)
     ap.add_argument("--health-probe", default="none", choices=("none", "hbm"))
-    ap.add_argument("--max-gpus", type=int, default=None)
+    ap.add_argument("--max-gpus", type=int, default=None, help="advertise only the first N physical GPUs")
+    ap.add_argument("--resource-naming", default="single", choices=("single", "mixed"),
+                    help="partitioned GPUs: single=amd.com/gpu for all, mixed=amd.com/<cpx>_<nps> per partition type")
+    ap.add_argument("--partition", default=None, help="fake backend only: compute/memory mode, e.g. CPX/NPS2")
     ap.add_argument("--register-v1beta1", default=None, help="kubelet.sock of an upstream v1beta1 kubelet")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     klog.setup(a.v, "amd-device-plugin")
-    from ..deviceplugin import AMDGPUPlugin
+    from ..deviceplugin.amd import make_plugins
     from ..smi import open_backend
 
+    class _Group:
+        def __init__(self, plugins):
+            self.plugins = plugins
+
+        async def stop(self):
+            for p in self.plugins:
+                await p.stop()
+
     async def mk():
-        p = AMDGPUPlugin(open_backend(a.backend, a.fixture, a.max_gpus), a.resource_name, a.plugins_dir, a.health_interval,
-                         a.health_probe)
-        await p.start()
-        if a.register_v1beta1:
-            await p.register_v1beta1(a.register_v1beta1)
-        return p
+        backend = open_backend(a.backend, a.fixture, a.max_gpus, a.partition)
+        plugins = make_plugins(backend, a.resource_naming, a.resource_name, plugins_dir=a.plugins_dir,
+                               health_interval=a.health_interval, health_probe=a.health_probe)
+        for p in plugins:
+            await p.start()
+            if a.register_v1beta1:
+                await p.register_v1beta1(a.register_v1beta1)
+        return _Group(plugins)
     _run_forever(mk)
 
 
@@ -233,6 +246,8 @@ def hollow_node(argv):
     ap.add_argument("--count", type=int, default=1)
     ap.add_argument("--gpus", type=int, default=8)
     ap.add_argument("--run-seconds", type=float, default=None)
+    ap.add_argument("--partition", default="SPX/NPS1", help="simulated compute/memory partition mode, e.g. CPX/NPS2")
+    ap.add_argument("--resource-naming", default="single", choices=("single", "mixed"))
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     klog.setup(a.v, "hollow-node")
@@ -247,7 +262,8 @@ def hollow_node(argv):
                 await n.stop()
 
     async def mk():
-        nodes = [await HollowNode(a.server, f"{a.name_prefix}-{i}", a.gpus, a.run_seconds).start() for i in range(a.count)]
+        nodes = [await HollowNode(a.server, f"{a.name_prefix}-{i}", a.gpus, a.run_seconds, partition=a.partition,
+                                  resource_naming=a.resource_naming).start() for i in range(a.count)]
         return Group(nodes)
     _run_forever(mk)
 

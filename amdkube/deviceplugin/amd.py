@@ -13,6 +13,11 @@ SURVEY Appendix A.3; keys are single-slash qualified names, values label-safe â€
   amd.com/numa-node     0                 amd.com/xgmi-hive   42a9â€¦  (hex)
   amd.com/partition     SPX               amd.com/memory-partition NPS1
   amd.com/index         node-local index  amd.com/pci-bus     0000-23-00.0
+  amd.com/partition-id  0..7 (partitioned GPUs only)   amd.com/parent-gpu  0000-23-00.0
+Partitioned MI355X (compute partition DPX/QPX/CPX, memory NPS1/NPS2): every partition is a
+device. Resource naming (`resource_groups`): "single" advertises everything as amd.com/gpu
+(select partitions with the attributes above); "mixed" advertises whole GPUs as amd.com/gpu
+and partitions as amd.com/<compute>_<memory> (e.g. amd.com/cpx_nps2), one plugin socket each.
 Plugin labels (GetPluginInfoResponse.labels, field 2 of the fork's wire format) carry the
 node's GPU link matrix as `amd.com/gpu-topology` JSON, which the kubelet copies into a node
 annotation for the scheduler's xGMI/NUMA scorer.
@@ -27,6 +32,7 @@ import subprocess
 
 from ..grpcdesc.deviceplugin import DEVICE_PLUGINS_PATH, HEALTHY, UNHEALTHY
 from ..smi import Backend, device_id, visibility_token
+from ..smi.backend import parent_key, partition_count
 from .server import DevicePluginServer
 
 log = logging.getLogger("amdkube.deviceplugin.amd")
@@ -64,7 +70,26 @@ def attributes(g: dict) -> dict:
         a["amd.com/memory-partition"] = g["memory_partition"]
     if g.get("bdf"):
         a["amd.com/pci-bus"] = g["bdf"].replace(":", "-")
+    if partition_count(g) > 1:
+        a["amd.com/partition-id"] = str(int(g.get("partition_id") or 0))
+        a["amd.com/parent-gpu"] = parent_key(g).replace(":", "-")
     return a
+
+
+def resource_groups(gpus: list[dict], strategy: str = "single", base: str = RESOURCE) -> dict[str, list[dict]]:
+    """Split a node's devices into advertised resources (see module doc)."""
+    if strategy not in ("single", "mixed"):
+        raise ValueError(f"unknown resource naming strategy {strategy!r} (single|mixed)")
+    out: dict[str, list[dict]] = {}
+    for g in gpus:
+        if strategy == "single" or partition_count(g) <= 1 and str(g.get("memory_partition") or "NPS1").upper() == "NPS1":
+            name = base
+        else:
+            cp = str(g.get("compute_partition") or "SPX").lower()
+            mp = str(g.get("memory_partition") or "NPS1").lower()
+            name = f"{base.split('/')[0]}/{cp}_{mp}"
+        out.setdefault(name, []).append(g)
+    return out
 
 
 def topology_label(gpus: list[dict], topo: list[list[dict]]) -> str:
@@ -81,14 +106,19 @@ def topology_label(gpus: list[dict], topo: list[list[dict]]) -> str:
                 w = {"xgmi": 15, "pcie": 40}.get(e.get("type"), 60) * max(1, int(e.get("hops") or 1))
             r.append(int(w))
         link.append(r)
-    return json.dumps({"ids": ids, "numa": [int(g.get("numa_node") or 0) for g in gpus], "link": link,
-                       "type": [[(e.get("type") or "")[:4] for e in row] for row in topo]}, separators=(",", ":"))
+    out = {"ids": ids, "numa": [int(g.get("numa_node") or 0) for g in gpus], "link": link,
+           "type": [[(e.get("type") or "")[:4] for e in row] for row in topo]}
+    if any(partition_count(g) > 1 for g in gpus):
+        pk: dict[str, int] = {}
+        out["parent"] = [pk.setdefault(parent_key(g), len(pk)) for g in gpus]
+    return json.dumps(out, separators=(",", ":"))
 
 
 class AMDGPUPlugin(DevicePluginServer):
     def __init__(self, backend: Backend, resource_name: str = RESOURCE, plugins_dir: str = DEVICE_PLUGINS_PATH,
                  health_interval: float = 10.0, health_probe: str = "none", dev_root: str = "/dev",
-                 ecc_threshold: int = 0, expose_card: bool = True, init_timeout: int = 10):
+                 ecc_threshold: int = 0, expose_card: bool = True, init_timeout: int = 10,
+                 devices: list[dict] | None = None):
         super().__init__(resource_name, plugins_dir, init_timeout)
         self.backend = backend
         self.health_interval = health_interval
@@ -96,17 +126,23 @@ class AMDGPUPlugin(DevicePluginServer):
         self.dev_root = dev_root
         self.ecc_threshold = ecc_threshold
         self.expose_card = expose_card
-        self.gpus = backend.gpus()
+        node_gpus = backend.gpus()
+        # `devices`: the subset this socket advertises (resource_groups); topology stays node-wide
+        self.gpus = node_gpus if devices is None else list(devices)
         self.by_id = {device_id(g): g for g in self.gpus}
+        if len(self.by_id) != len(self.gpus):
+            raise ValueError("device IDs are not unique on this node (partitions without distinct ids?)")
         self.reasons: dict[str, str] = {}
         self._task: asyncio.Task | None = None
         try:
-            self.labels[TOPOLOGY_LABEL] = topology_label(self.gpus, backend.topology())
+            self.labels[TOPOLOGY_LABEL] = topology_label(node_gpus, backend.topology())
         except Exception as e:  # topology is an optimisation, never a reason not to serve
             log.warning("gpu topology unavailable: %s", e)
-        if self.gpus:
-            self.labels["amd.com/gpu.product"] = gpu_type(self.gpus[0])
-            self.labels["amd.com/gpu.count"] = str(len(self.gpus))
+        if node_gpus:  # node-wide facts: identical from every socket of a mixed-strategy plugin
+            self.labels["amd.com/gpu.product"] = gpu_type(node_gpus[0])
+            self.labels["amd.com/gpu.count"] = str(len({parent_key(g) for g in node_gpus}))
+            modes = sorted({f"{g.get('compute_partition') or 'SPX'}_{g.get('memory_partition') or 'NPS1'}" for g in node_gpus})
+            self.labels["amd.com/gpu.partition-modes"] = ",".join(modes)
         self.devices = [{"ID": device_id(g), "health": HEALTHY, "Attributes": attributes(g)} for g in self.gpus]
 
     async def start(self):
@@ -190,3 +226,11 @@ class AMDGPUPlugin(DevicePluginServer):
                 "AMD_GPU_COUNT": str(len(gpus))}
         return {"envs": envs, "devices": devs, "mounts": [],
                 "annotations": {"amd.com/gpus": ",".join(device_ids), RUNTIME_ANNOTATION: "rocm"}}
+
+
+def make_plugins(backend: Backend, strategy: str = "single", resource_name: str = RESOURCE, **kw) -> list[AMDGPUPlugin]:
+    """One AMDGPUPlugin (socket) per advertised resource of this node (see resource_groups)."""
+    groups = resource_groups(backend.gpus(), strategy, resource_name)
+    if not groups:
+        return [AMDGPUPlugin(backend, resource_name, devices=[], **kw)]
+    return [AMDGPUPlugin(backend, name, devices=devs, **kw) for name, devs in sorted(groups.items())]

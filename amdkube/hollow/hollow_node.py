@@ -21,7 +21,7 @@ import uuid
 import grpc
 
 from ..client import Client
-from ..deviceplugin import AMDGPUPlugin
+from ..deviceplugin.amd import make_plugins
 from ..grpcdesc.cri import API_VERSION, CRI as C
 from ..kubelet.kubelet import Kubelet, KubeletConfig
 from ..smi import FakeBackend
@@ -192,8 +192,10 @@ class _FakeImages:
 
 class HollowNode:
     def __init__(self, server: str, name: str, gpus: int = 8, run_seconds: float | None = None, base_dir: str | None = None,
-                 status_period: float = 10.0):
+                 status_period: float = 10.0, partition: str = "SPX/NPS1", resource_naming: str = "single"):
         self.server, self.name, self.gpus, self.run_seconds = server, name, gpus, run_seconds
+        self.partition, self.resource_naming = partition, resource_naming
+        self.plugins: list = []
         self.base = base_dir or tempfile.mkdtemp(prefix="hollow-", dir="/tmp")
         self.status_period = status_period
         self.runtime = self.plugin = self.kubelet = None
@@ -201,7 +203,8 @@ class HollowNode:
     async def start(self):
         b = self.base
         self.runtime = await FakeRuntime(os.path.join(b, "cri.sock"), self.run_seconds).start()
-        backend = FakeBackend(n=self.gpus) if self.gpus else None
+        cp, _, mp = self.partition.partition("/")
+        backend = FakeBackend(n=self.gpus, compute_partition=cp or "SPX", memory_partition=mp or "NPS1") if self.gpus else None
         cfg = KubeletConfig(node_name=self.name, root_dir=os.path.join(b, "kubelet"), plugins_dir=os.path.join(b, "plugins"),
                             cri_socket=os.path.join(b, "cri.sock"), port=0, relist_period=2.0,
                             node_status_update_frequency=self.status_period, eviction_interval=3600.0,
@@ -211,13 +214,16 @@ class HollowNode:
             # per-node unique device IDs (a real cluster has distinct GPUs on every node)
             for g in backend.data["gpus"]:
                 g["uuid"] = g["hip_uuid"] = f"{g['uuid']}-{self.name}"
-            self.plugin = AMDGPUPlugin(backend, plugins_dir=os.path.join(b, "plugins"), health_interval=30.0)
-            await self.plugin.start()
-            await self.plugin.wait_for_registration(10)
+            self.plugins = make_plugins(backend, self.resource_naming, plugins_dir=os.path.join(b, "plugins"),
+                                        health_interval=30.0)
+            self.plugin = self.plugins[0]
+            for p in self.plugins:
+                await p.start()
+                await p.wait_for_registration(10)
         return self
 
     async def stop(self):
-        for c in (self.kubelet, self.plugin, self.runtime):
+        for c in (self.kubelet, *self.plugins, self.runtime):
             if c is not None:
                 try:
                     await c.stop()

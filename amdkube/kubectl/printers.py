@@ -10,7 +10,7 @@ from __future__ import annotations
 import time
 
 from ..api import meta as m
-from ..api.helpers import get_condition, pod_gpu_request
+from ..api.helpers import get_condition, is_gpu_resource, pod_gpu_request
 
 
 def age(ts: str | None) -> str:
@@ -85,13 +85,21 @@ def pods_table(items, wide=False, all_ns=False) -> str:
 
 
 def node_gpu_summary(node) -> tuple[str, str, str, str]:
+    """Totals over amd.com/gpu and the partition resources; model shows the partition mode
+    when the node's GPUs are partitioned (e.g. MI355X/CPX)."""
     st = node.get("status") or {}
-    cap = (st.get("capacity") or {}).get("amd.com/gpu", "0")
-    alloc = (st.get("allocatable") or {}).get("amd.com/gpu", "0")
-    devs = (((st.get("extendedResources") or {}).get("amd.com/gpu") or {}).get("resources") or {})
+    cap = sum(int(v) for r, v in (st.get("capacity") or {}).items() if is_gpu_resource(r))
+    alloc = sum(int(v) for r, v in (st.get("allocatable") or {}).items() if is_gpu_resource(r))
+    devs = {}
+    for r, dom in ((st.get("extendedResources") or {}).items()):
+        if is_gpu_resource(r):
+            devs.update((dom or {}).get("resources") or {})
     healthy = sum(1 for d in devs.values() if d.get("health") == "Healthy")
-    model = next((d.get("attributes", {}).get("amd.com/gpu-type") for d in devs.values()), None) or "-"
-    return cap, alloc, str(healthy), model
+    attrs = next((d.get("attributes") or {} for d in devs.values()), {})
+    model = attrs.get("amd.com/gpu-type") or "-"
+    if attrs.get("amd.com/partition-id") is not None and attrs.get("amd.com/partition"):
+        model += "/" + attrs["amd.com/partition"]
+    return str(cap), str(alloc), str(healthy), model
 
 
 def nodes_table(items, wide=False) -> str:

@@ -15,7 +15,7 @@ import tempfile
 
 from .apiserver import APIServer
 from .client import Client
-from .deviceplugin import AMDGPUPlugin
+from .deviceplugin.amd import make_plugins
 from .kubelet.kubelet import Kubelet, KubeletConfig
 from .runtime import RocShim
 from .scheduler import Scheduler
@@ -28,8 +28,11 @@ class LocalCluster:
     def __init__(self, gpus: str = "fake", n_gpus: int | None = None, node_name: str = "mi355x-node-0",
                  base_dir: str | None = None, with_controllers: bool = True, relist_period: float = 1.0,
                  node_status_update_frequency: float = 10.0, scheduler_kw: dict | None = None, isolation: str = "env",
-                 health_probe: str = "none", kubelet_kw: dict | None = None, with_kubelet: bool = True):
+                 health_probe: str = "none", kubelet_kw: dict | None = None, with_kubelet: bool = True,
+                 partition: str | None = None, resource_naming: str = "single"):
         self.gpus, self.n_gpus, self.node_name = gpus, n_gpus, node_name
+        self.partition, self.resource_naming = partition, resource_naming
+        self.plugins: list = []
         self._own_dir = base_dir is None
         self.base = base_dir or tempfile.mkdtemp(prefix="ak-", dir="/tmp")
         self.with_controllers = with_controllers
@@ -56,32 +59,33 @@ class LocalCluster:
         self.shim = await RocShim(os.path.join(b, "rocshim.sock"), os.path.join(b, "rocshim"),
                                   hooks_dir=os.path.join(b, "hooks.d"), isolation=self.isolation).start()
         if self.gpus != "none":
-            self.backend = open_backend(self.gpus, n=self.n_gpus)
-            self.plugin = AMDGPUPlugin(self.backend, plugins_dir=os.path.join(b, "plugins"), health_interval=5.0,
-                                       health_probe=self.health_probe)
+            self.backend = open_backend(self.gpus, n=self.n_gpus, partition=self.partition)
+            self.plugins = make_plugins(self.backend, self.resource_naming, plugins_dir=os.path.join(b, "plugins"),
+                                        health_interval=5.0, health_probe=self.health_probe)
+            self.plugin = self.plugins[0]
         cfg = KubeletConfig(node_name=self.node_name, root_dir=os.path.join(b, "kubelet"), plugins_dir=os.path.join(b, "plugins"),
                             cri_socket=os.path.join(b, "rocshim.sock"), port=0, relist_period=self.relist_period,
                             node_status_update_frequency=self.nsuf, **self.kubelet_kw)
         self.kubelet = await Kubelet(Client(self.api.url, pool=128), cfg, smi_backend=self.backend).start()
-        if self.plugin is not None:
-            await self.plugin.start()
-            await self.plugin.wait_for_registration(10)
+        for p in self.plugins:
+            await p.start()
+            await p.wait_for_registration(10)
         return self
 
-    async def wait_gpus(self, n: int, timeout: float = 15.0):
+    async def wait_gpus(self, n: int, timeout: float = 15.0, resource: str = "amd.com/gpu"):
         loop = asyncio.get_running_loop()
         end = loop.time() + timeout
         while loop.time() < end:
             node = await self.client.get_or_none("nodes", self.node_name)
-            if node and int(((node.get("status") or {}).get("allocatable") or {}).get("amd.com/gpu", 0)) >= n:
+            if node and int(((node.get("status") or {}).get("allocatable") or {}).get(resource, 0)) >= n:
                 ext = (node.get("status") or {}).get("extendedResources") or {}
-                if len(((ext.get("amd.com/gpu") or {}).get("resources") or {})) >= n:
+                if len(((ext.get(resource) or {}).get("resources") or {})) >= n:
                     return node
             await asyncio.sleep(0.05)
         raise TimeoutError(f"node never advertised {n} GPUs")
 
     async def stop(self):
-        for comp in (self.kubelet, self.plugin):
+        for comp in (self.kubelet, *self.plugins):
             if comp is not None:
                 try:
                     await comp.stop()

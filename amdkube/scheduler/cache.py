@@ -107,7 +107,8 @@ class NodeInfo:
         return list((self.devices.get(rname) or {}).keys())
 
     def topology(self):
-        """(ids, index map, numa list, link matrix) from the node's gpu-topology annotation."""
+        """(ids, index map, numa list, link matrix, parent list | None) from the node's
+        gpu-topology annotation; `parent` groups the partitions of one physical GPU."""
         src = m.annotations_of(self.node or {}).get(TOPOLOGY_ANNOTATION)
         if src != self._topo_src:
             self._topo_src = src
@@ -116,7 +117,7 @@ class NodeInfo:
                 try:
                     t = json.loads(src)
                     ids = t["ids"]
-                    self._topo = (ids, {d: i for i, d in enumerate(ids)}, t["numa"], t["link"])
+                    self._topo = (ids, {d: i for i, d in enumerate(ids)}, t["numa"], t["link"], t.get("parent"))
                 except (ValueError, KeyError, TypeError):
                     self._topo = None
         return self._topo

@@ -53,10 +53,10 @@ def allocate(pi, ni, use_topology: bool = True) -> dict | None:
             return None
         chosen = None
         if t is not None:
-            ids, index, numa, link = t
+            ids, index, numa, link, parent = t
             if all(d in index for d in cand):
                 free_all = [index[d] for d in ni.available_devices(rname) if d in index and d not in taken]
-                sel_idx, cost = topo.select([index[d] for d in cand], n, link, numa, free_all)
+                sel_idx, cost = topo.select([index[d] for d in cand], n, link, numa, free_all, parent)
                 if len(sel_idx) == n:
                     chosen = [ids[i] for i in sel_idx]
         if chosen is None:
@@ -73,14 +73,14 @@ def topology_score(pi, ni) -> float:
         return 10.0 if not ni.devices else 0.0
     if t is None:
         return 5.0
-    ids, index, numa, link = t
+    ids, index, numa, link, parent = t
     total = 0.0
     for _, rname, n, sel in pi.ext:
         cand = matching_free(pi, ni, rname, sel)
         if not all(d in index for d in cand):
             return 5.0
         free_all = [index[d] for d in ni.available_devices(rname) if d in index]
-        total += topo.score([index[d] for d in cand], n, link, numa, free_all)
+        total += topo.score([index[d] for d in cand], n, link, numa, free_all, parent)
     s = total / len(pi.ext)
     # best fit across nodes: prefer the node whose free GPUs are closest to the request
     free = sum(len(ni.available_devices(r)) for r in {r for _, r, _, _ in pi.ext})

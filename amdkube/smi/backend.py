@@ -32,19 +32,93 @@ class SMIError(RuntimeError):
 
 
 def device_id(g: dict) -> str:
-    """Stable device-plugin ID for a GPU (what the scheduler writes into `assigned`)."""
+    """Stable device-plugin ID for a GPU (what the scheduler writes into `assigned`).
+
+    A compute partition (CPX/QPX/DPX) of a physical GPU may report its parent's UUID, so
+    partitions get a `-p<partition>` suffix whenever they are not the whole device.
+    """
     u = g.get("uuid") or g.get("hip_uuid") or ""
     if u:
-        return u if u.startswith("GPU-") else "GPU-" + u
-    return "GPU-" + (g.get("bdf") or str(g.get("index"))).replace(":", "-")
+        base = u if u.startswith("GPU-") else "GPU-" + u
+    else:
+        base = "GPU-" + (g.get("bdf") or str(g.get("index"))).replace(":", "-")
+    if partition_count(g) > 1 and not g.get("uuid_is_unique"):
+        return f"{base}-p{int(g.get('partition_id') or 0)}"
+    return base
 
 
 def visibility_token(g: dict) -> str:
-    """Value for ROCR_VISIBLE_DEVICES selecting exactly this GPU."""
+    """Value for ROCR_VISIBLE_DEVICES selecting exactly this GPU (or GPU partition).
+
+    The HIP UUID is position-independent and preferred; partitions that share their parent's
+    UUID are selected by their ROCr agent ordinal instead.
+    """
     hu = g.get("hip_uuid") or ""
-    if hu.startswith("GPU-") and len(hu) > 4:
+    if hu.startswith("GPU-") and len(hu) > 4 and (partition_count(g) <= 1 or g.get("uuid_is_unique")):
         return hu
     return str(g.get("hip_id", g.get("index", 0)))
+
+
+COMPUTE_PARTITIONS = {"SPX": 1, "DPX": 2, "QPX": 4, "CPX": 8}   # MI355X: 8 XCDs split 1/2/4/8 ways
+MEMORY_PARTITIONS = {"NPS1": 1, "NPS2": 2}                      # MI355X: HBM interleaved 1 or 2 ways
+
+
+def partition_count(g: dict) -> int:
+    return COMPUTE_PARTITIONS.get(str(g.get("compute_partition") or "SPX").upper(), 1)
+
+
+def parent_key(g: dict) -> str:
+    """Identity of the physical GPU a (possibly partitioned) device belongs to."""
+    return str(g.get("parent_bdf") or g.get("bdf") or g.get("uuid") or g.get("index"))
+
+
+def partition_fixture(data: dict, compute: str = "SPX", memory: str = "NPS1") -> dict:
+    """Expand a whole-GPU fixture into the devices a node in `compute`/`memory` mode exposes.
+
+    Each physical MI355X (8 XCDs × 32 CUs, 288 GiB HBM3E) becomes `parts` KFD nodes / render
+    nodes / HIP devices with 256/parts CUs. Under NPS1 every partition addresses all of HBM;
+    under NPSn each partition sees its 1/n memory domain. Partitions of one GPU link to
+    each other on-package (type "xcp", cheaper than an xGMI hop); cross-GPU links inherit the
+    parents' xGMI entries.
+    """
+    compute, memory = compute.upper(), memory.upper()
+    if compute not in COMPUTE_PARTITIONS or memory not in MEMORY_PARTITIONS:
+        raise ValueError(f"unknown partition mode {compute}/{memory}")
+    parts, nps = COMPUTE_PARTITIONS[compute], MEMORY_PARTITIONS[memory]
+    if parts % nps:
+        raise ValueError(f"{compute} cannot be combined with {memory} (partitions must divide evenly over memory domains)")
+    out = copy.deepcopy(data)
+    if parts == 1 and nps == 1:
+        return out
+    gpus, topo = out["gpus"], out["topology"]
+    new_gpus, owner = [], []
+    for g in gpus:
+        for pid in range(parts):
+            d = dict(g)
+            i = len(new_gpus)
+            d.update(index=i, hip_id=i, hsa_id=i + 1,
+                     compute_partition=compute, memory_partition=memory, partition_id=pid,
+                     parent_index=g["index"], parent_bdf=g.get("bdf"), num_cu=int(g.get("num_cu", 256)) // parts,
+                     vram_total_bytes=int(g.get("vram_total_bytes", 0)) // nps,
+                     render_minor=128 + i, card_minor=None if pid else g.get("card_minor"),
+                     kfd_node_id=int(g.get("kfd_node_id", 0)) * parts + pid)
+            new_gpus.append(d)
+            owner.append(g["index"])
+    pos = {g["index"]: k for k, g in enumerate(gpus)}
+    new_topo = []
+    for i, pi in enumerate(owner):
+        row = []
+        for j, pj in enumerate(owner):
+            if i == j:
+                row.append({"type": "self", "hops": 0, "weight": 0, "p2p": True})
+            elif pi == pj:
+                row.append({"type": "xcp", "hops": 0, "weight": 5, "p2p": True})
+            else:
+                row.append(dict(topo[pos[pi]][pos[pj]]))
+        new_topo.append(row)
+    out["gpus"], out["topology"] = new_gpus, new_topo
+    out["description"] = f"{out.get('description', '')} [{compute}/{memory}: {len(gpus)} GPUs x {parts} partitions]"
+    return out
 
 
 class Backend:
@@ -189,16 +263,18 @@ class FakeBackend(Backend):
     """Fixture-driven backend; mutable so tests can inject faults (ECC errors, lost GPUs)."""
     name = "fake"
 
-    def __init__(self, fixture: str | dict | None = None, n: int | None = None):
+    def __init__(self, fixture: str | dict | None = None, n: int | None = None, compute_partition: str = "SPX",
+                 memory_partition: str = "NPS1"):
         if isinstance(fixture, dict):
             data = fixture
         else:
             with open(fixture or DEFAULT_FIXTURE) as f:
                 data = json.load(f)
         self.data = copy.deepcopy(data)
-        if n is not None:
+        if n is not None:  # n physical GPUs (before partitioning)
             self.data["gpus"] = self.data["gpus"][:n]
             self.data["topology"] = [row[:n] for row in self.data["topology"][:n]]
+        self.data = partition_fixture(self.data, compute_partition, memory_partition)
         self.samples = {g["index"]: dict(self.data.get("sample_defaults", {})) for g in self.data["gpus"]}
         self.procs: dict[int, list] = {}
 
@@ -217,9 +293,15 @@ class FakeBackend(Backend):
         return list(self.procs.get(index, []))
 
     def link_metrics(self, index):
-        n = len(self.data["gpus"])
-        return [{"peer_bdf": self.data["gpus"][j]["bdf"], "type": "xgmi", "bit_rate_gbps": 32, "max_bandwidth_gbps": 1224,
-                 "read_kb": 0, "write_kb": 0} for j in range(n) if j != index]
+        gpus = self.data["gpus"]
+        me = parent_key(gpus[index])
+        peers = []
+        for g in gpus:  # one xGMI link per peer physical GPU, whatever the partition mode
+            k = parent_key(g)
+            if k != me and k not in peers:
+                peers.append(k)
+        return [{"peer_bdf": k, "type": "xgmi", "bit_rate_gbps": 32, "max_bandwidth_gbps": 1224,
+                 "read_kb": 0, "write_kb": 0} for k in peers]
 
     # fault injection
     def inject_ecc(self, index, uncorrectable=1):
@@ -233,10 +315,12 @@ def has_kfd() -> bool:
     return os.path.exists("/dev/kfd")
 
 
-def open_backend(kind: str = "auto", fixture: str | None = None, n: int | None = None) -> Backend:
+def open_backend(kind: str = "auto", fixture: str | None = None, n: int | None = None, partition: str | None = None) -> Backend:
+    """`partition` ("CPX/NPS2" style) applies to the fake backend; real GPUs report their own mode."""
     kind = kind or "auto"
     if kind == "fake":
-        return FakeBackend(fixture, n)
+        cp, _, mp = (partition or "SPX/NPS1").partition("/")
+        return FakeBackend(fixture, n, cp or "SPX", mp or "NPS1")
     errs = []
     if kind in ("auto", "amdsmi"):
         try:
@@ -260,20 +344,32 @@ def open_backend(kind: str = "auto", fixture: str | None = None, n: int | None =
 
 
 class _Limited(Backend):
-    """Expose only the first n GPUs (allocatable-GPU scaling runs: 1/2/4/8)."""
+    """Expose only the first n physical GPUs (allocatable-GPU scaling runs: 1/2/4/8); on a
+    partitioned node every partition of those GPUs stays visible."""
 
     def __init__(self, inner: Backend, n: int):
         self.inner, self.n = inner, n
         self.name = inner.name
+        parents: list[str] = []
+        self.keep: list[int] = []
+        for pos, g in enumerate(inner.gpus()):
+            k = parent_key(g)
+            if k not in parents:
+                if len(parents) >= n:
+                    continue
+                parents.append(k)
+            self.keep.append(pos)
 
     def gpus(self):
-        return self.inner.gpus()[: self.n]
+        all_ = self.inner.gpus()
+        return [all_[i] for i in self.keep]
 
     def sample(self, index):
         return self.inner.sample(index)
 
     def topology(self):
-        return [row[: self.n] for row in self.inner.topology()[: self.n]]
+        t = self.inner.topology()
+        return [[t[i][j] for j in self.keep] for i in self.keep]
 
     def processes(self, index):
         return self.inner.processes(index)

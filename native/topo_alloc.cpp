@@ -12,8 +12,8 @@ PYBIND11_MODULE(_topo, m) {
   m.def(
       "select",
       [](const std::vector<int>& free, int k, const std::vector<std::vector<double>>& link,
-         const std::vector<int>& numa, const std::vector<int>& all_free) {
-        Problem p = make(free, k, link, numa, all_free);
+         const std::vector<int>& numa, const std::vector<int>& all_free, const std::vector<int>& parent) {
+        Problem p = make(free, k, link, numa, all_free, parent);
         std::tuple<std::vector<int>, double> r;
         {
           py::gil_scoped_release nogil;
@@ -22,12 +22,13 @@ PYBIND11_MODULE(_topo, m) {
         return r;
       },
       py::arg("free"), py::arg("k"), py::arg("link"), py::arg("numa"), py::arg("all_free") = std::vector<int>{},
+      py::arg("parent") = std::vector<int>{},
       "Best k-subset of `free` -> (sorted indices, cost); cost=inf if infeasible");
   m.def(
       "score",
       [](const std::vector<int>& free, int k, const std::vector<std::vector<double>>& link,
-         const std::vector<int>& numa, const std::vector<int>& all_free) {
-        Problem p = make(free, k, link, numa, all_free);
+         const std::vector<int>& numa, const std::vector<int>& all_free, const std::vector<int>& parent) {
+        Problem p = make(free, k, link, numa, all_free, parent);
         auto r = solve(p);
         double c = std::get<1>(r);
         if (!std::isfinite(c)) return 0.0;
@@ -36,6 +37,7 @@ PYBIND11_MODULE(_topo, m) {
         return std::max(0.0, std::min(10.0, s));
       },
       py::arg("free"), py::arg("k"), py::arg("link"), py::arg("numa"), py::arg("all_free") = std::vector<int>{},
+      py::arg("parent") = std::vector<int>{},
       "Node score in [0,10] for placing k devices (GPUTopologyPriority)");
   m.attr("W_NUMA") = W_NUMA;
   m.attr("W_LINK") = W_LINK;

@@ -15,6 +15,11 @@
 // still whole for the next 4-GPU gang. Ties break on the
 // lexicographically smallest index set, so placement is deterministic. The Python
 // fallback in amdkube/ops/topology.py implements the identical function.
+//
+// Partitioned GPUs (MI355X CPX/QPX/DPX compute partitions): every partition is a device and
+// `parent[d]` names its physical GPU. The fragmentation term then scores how whole the
+// remaining physical GPUs stay (instead of aligned pairs), so small partition requests pack
+// onto already-split GPUs and full-GPU-sized requests land on one GPU's partitions.
 #pragma once
 
 #include <algorithm>
@@ -39,6 +44,11 @@ struct Problem {
   std::vector<std::vector<double>> link; // normalised link cost in [0,1], indexed by device index
   std::vector<int> numa;                 // numa group per device index
   std::vector<int> all_free;             // every free device on the node (for fragmentation)
+  std::vector<int> parent;               // physical GPU per device index, dense 0..n_parents-1 (empty: unpartitioned)
+  int parent_size = 1;                   // largest number of devices sharing one parent
+  int n_parents = 0;
+  std::vector<int> group;                // numa group per device, dense 0..n_groups-1
+  int n_groups = 0;
   int k;
 };
 
@@ -68,24 +78,34 @@ inline int min_groups_needed(const Problem& p) {
 }
 
 inline double fragmentation(const Problem& p, const std::vector<int>& chosen) {
-  // remaining free devices after taking `chosen`; quality = sum_g c_g^2 + sum_pairs both-free
-  std::set<int> taken(chosen.begin(), chosen.end());
-  std::map<int, int> per_group;
-  std::set<int> rem;
-  for (int d : p.all_free)
-    if (!taken.count(d)) {
-      per_group[p.numa[d]]++;
-      rem.insert(d);
+  // remaining free devices after taking `chosen`; flat per-device / per-group counters keep
+  // this O(n) so the greedy path stays cheap on 64-partition (CPX) nodes
+  const size_t n = p.numa.size();
+  std::vector<char> rem(n, 0);
+  for (int d : p.all_free) rem[d] = 1;
+  for (int d : chosen) rem[d] = 0;
+  std::vector<int> per_group(p.n_groups, 0), per_parent(p.parent_size > 1 ? p.n_parents : 0, 0);
+  int total = 0;
+  for (size_t d = 0; d < n; ++d)
+    if (rem[d]) {
+      ++total;
+      per_group[p.group[d]]++;
+      if (p.parent_size > 1) per_parent[p.parent[d]]++;
     }
-  int total = static_cast<int>(rem.size());
   if (total == 0) return 0.0;
   double q = 0.0;
-  for (auto& kv : per_group) q += static_cast<double>(kv.second) * kv.second;
-  double pairs = 0.0;
-  for (int d : rem)
-    if ((d % 2) == 0 && rem.count(d + 1) && p.numa[d] == p.numa[d + 1]) pairs += 1.0;
+  for (int c : per_group) q += static_cast<double>(c) * c;
   double best_q = static_cast<double>(total) * total;  // everything in one group
   double frag_groups = 1.0 - q / best_q;
+  if (p.parent_size > 1) {
+    double qp = 0.0;
+    for (int c : per_parent) qp += static_cast<double>(c) * c;
+    double frag_parent = 1.0 - qp / (static_cast<double>(total) * std::min(total, p.parent_size));
+    return 0.5 * frag_groups + 0.5 * std::max(0.0, frag_parent);
+  }
+  double pairs = 0.0;
+  for (size_t d = 0; d + 1 < n; d += 2)
+    if (rem[d] && rem[d + 1] && p.numa[d] == p.numa[d + 1]) pairs += 1.0;
   double frag_pairs = 1.0 - (2.0 * pairs) / total;
   return 0.75 * frag_groups + 0.25 * std::max(0.0, frag_pairs);
 }
@@ -133,8 +153,18 @@ inline std::tuple<std::vector<int>, double> solve(const Problem& p) {
     }
     return std::make_tuple(best, best_cost);
   }
-  // greedy: grow from every seed, keep the cheapest
-  for (int seed : sorted_free) {
+  // greedy: grow from every seed, keep the cheapest. Partitions of one physical GPU are
+  // interchangeable as seeds, so a partitioned node seeds once per parent (8 instead of 64).
+  std::vector<int> seeds;
+  std::vector<char> seeded(p.n_parents, 0);
+  for (int d : sorted_free) {
+    if (p.parent_size > 1) {
+      if (seeded[p.parent[d]]) continue;
+      seeded[p.parent[d]] = 1;
+    }
+    seeds.push_back(d);
+  }
+  for (int seed : seeds) {
     std::vector<int> s{seed};
     std::set<int> used{seed};
     while (static_cast<int>(s.size()) < p.k) {
@@ -164,7 +194,8 @@ inline std::tuple<std::vector<int>, double> solve(const Problem& p) {
 }
 
 inline Problem make(const std::vector<int>& free, int k, const std::vector<std::vector<double>>& link,
-             const std::vector<int>& numa, const std::vector<int>& all_free) {
+             const std::vector<int>& numa, const std::vector<int>& all_free,
+             const std::vector<int>& parent = std::vector<int>{}) {
   Problem p;
   p.free = free;
   p.k = k;
@@ -184,6 +215,28 @@ inline Problem make(const std::vector<int>& free, int k, const std::vector<std::
     if (d < 0 || static_cast<size_t>(d) >= n) throw std::out_of_range("device index out of range");
   for (int d : p.all_free)
     if (d < 0 || static_cast<size_t>(d) >= n) throw std::out_of_range("device index out of range");
+  std::map<int, int> gid;
+  p.group.resize(n);
+  for (size_t d = 0; d < n; ++d) {
+    auto it = gid.emplace(numa[d], static_cast<int>(gid.size())).first;
+    p.group[d] = it->second;
+  }
+  p.n_groups = static_cast<int>(gid.size());
+  if (!parent.empty()) {
+    if (parent.size() != n) throw std::invalid_argument("parent must have one entry per device");
+    std::map<int, int> pid, sz;
+    std::vector<int> dense(n);
+    for (size_t d = 0; d < n; ++d) {
+      dense[d] = pid.emplace(parent[d], static_cast<int>(pid.size())).first->second;
+      p.parent_size = std::max(p.parent_size, ++sz[parent[d]]);
+    }
+    if (p.parent_size > 1) {
+      p.parent = dense;
+      p.n_parents = static_cast<int>(pid.size());
+    } else {
+      p.parent_size = 1;
+    }
+  }
   return p;
 }
 

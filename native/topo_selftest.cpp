@@ -41,6 +41,39 @@ int main() {
       ++checked;
     }
   }
+  // partitioned nodes: 8 GPUs x {2,4,8} partitions, parent = physical GPU
+  for (int parts : {2, 4, 8}) {
+    const int n = 8 * parts;
+    for (int trial = 0; trial < 20; ++trial) {
+      std::vector<std::vector<double>> link(n, std::vector<double>(n, 0.0));
+      std::vector<int> numa(n), parent(n);
+      for (int i = 0; i < n; ++i) {
+        parent[i] = i / parts;
+        numa[i] = parent[i] / 4;
+      }
+      for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j)
+          if (i != j) link[i][j] = parent[i] == parent[j] ? 5.0 : (numa[i] == numa[j] ? 15.0 : 30.0);
+      std::vector<int> freev;
+      for (int i = 0; i < n; ++i)
+        if (rng() % 3) freev.push_back(i);
+      int k = 1 + static_cast<int>(rng() % std::min<size_t>(freev.size(), 12));
+      topo::Problem p = topo::make(freev, k, link, numa, freev, parent);
+      auto r1 = topo::solve(p);
+      const auto& s = std::get<0>(r1);
+      std::set<int> u(s.begin(), s.end()), cand(freev.begin(), freev.end());
+      if (static_cast<int>(s.size()) != k || u.size() != s.size()) {
+        std::printf("FAIL partitioned n=%d k=%d size=%zu\n", n, k, s.size());
+        return 1;
+      }
+      for (int d : s)
+        if (!cand.count(d)) {
+          std::printf("FAIL: picked non-candidate %d\n", d);
+          return 1;
+        }
+      ++checked;
+    }
+  }
   std::printf("topo selftest OK (%d cases)\n", checked);
   return 0;
 }
