@@ -49,10 +49,14 @@ class HTTPExtender:
             return {}
         return {e["host"]: int(e["score"]) for e in res or []}
 
-    async def bind(self, pod, node):
+    async def bind(self, pod, node, ext_binding: dict | None = None):
+        """ExtenderBindingArgs; `extendedResourceBinding` (the chosen device IDs) is an amdkube
+        addition — without it an extender that binds would drop the pod's GPU assignment."""
         md = pod["metadata"]
-        res = await self._post(self.bind_verb, {"podName": md["name"], "podNamespace": md.get("namespace", ""),
-                                                "podUID": md.get("uid", ""), "node": node})
+        body = {"podName": md["name"], "podNamespace": md.get("namespace", ""), "podUID": md.get("uid", ""), "node": node}
+        if ext_binding:
+            body["extendedResourceBinding"] = ext_binding
+        res = await self._post(self.bind_verb, body)
         if res and res.get("error"):
             raise RuntimeError(res["error"])
 

@@ -258,7 +258,7 @@ class Scheduler:
                 bound_by_ext = False
                 for ext in self.extenders:
                     if ext.bind_verb:
-                        await ext.bind(pod, host)
+                        await ext.bind(pod, host, binding or None)
                         bound_by_ext = True
                         break
                 if not bound_by_ext:

@@ -1,0 +1,201 @@
+"""Scheduler integration: real apiserver + scheduler over HTTP with API-only nodes, the
+reference's test/integration/scheduler harness shape (framework.RunAMasterUsingServer + fake
+Node objects):
+
+  extender_test.go        -> test_extender_filter_prioritize_bind (HTTP extender incl. bindVerb,
+                             which also receives the chosen device IDs)
+  predicates_test.go      -> test_interpod_affinity_and_anti_affinity
+  taint_test.go           -> test_extended_resource_taint_toleration (ExtendedResourceToleration)
+  preemption_test.go      -> test_priority_preemption_frees_devices
+"""
+import asyncio
+
+from aiohttp import web
+
+from amdkube.apiserver import APIServer
+from amdkube.benchmark.schedperf import fake_node
+from amdkube.client import Client
+from amdkube.scheduler import Scheduler
+from amdkube.smi import FakeBackend
+from tests.conftest import run
+
+
+async def _cluster(n_nodes=3, gpus=0, **kw):
+    api = await APIServer().start()
+    c = Client(api.url)
+    fb = FakeBackend()
+    for i in range(n_nodes):
+        await c.create(fake_node(i, gpus, fb))
+    s = await Scheduler(Client(api.url), **kw).start()
+    return api, c, s
+
+
+async def _stop(api, c, s):
+    await s.stop()
+    await s.client.close()
+    await c.close()
+    await api.stop()
+
+
+def _pod(name, labels=None, gpus=0, prio=None, affinity=None, cpu="100m"):
+    c = {"name": "c", "image": "busybox", "resources": {"requests": {"cpu": cpu}, "limits": {"cpu": cpu}}}
+    if gpus:
+        c["resources"]["limits"]["amd.com/gpu"] = str(gpus)
+    spec = {"containers": [c]}
+    if prio is not None:
+        spec["priority"] = prio
+    if affinity:
+        spec["affinity"] = affinity
+    return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "default", "labels": labels or {}},
+            "spec": spec}
+
+
+async def _node_of(c, name, timeout=10.0):
+    loop = asyncio.get_running_loop()
+    end = loop.time() + timeout
+    while loop.time() < end:
+        p = await c.get("pods", name, "default")
+        if (p.get("spec") or {}).get("nodeName"):
+            return p["spec"]["nodeName"]
+        await asyncio.sleep(0.02)
+    raise AssertionError(f"{name} never scheduled")
+
+
+async def _condition(c, name, timeout=10.0):
+    loop = asyncio.get_running_loop()
+    end = loop.time() + timeout
+    while loop.time() < end:
+        p = await c.get("pods", name, "default")
+        for cond in (p.get("status") or {}).get("conditions") or []:
+            if cond.get("type") == "PodScheduled" and cond.get("status") == "False":
+                return cond
+        await asyncio.sleep(0.02)
+    raise AssertionError(f"{name} never marked unschedulable")
+
+
+def test_extender_filter_prioritize_bind():
+    async def go():
+        seen = {"filter": 0, "prioritize": 0, "bind": []}
+        api_holder = {}
+
+        async def filt(r):
+            body = await r.json()
+            seen["filter"] += 1
+            items = [n for n in body["nodes"]["items"] if n["metadata"]["name"] != "node-0002"]
+            return web.json_response({"nodes": {"items": items}, "failedNodes": {"node-0002": "extender says no"}})
+
+        async def prio(r):
+            body = await r.json()
+            seen["prioritize"] += 1
+            return web.json_response([{"host": n["metadata"]["name"], "score": 10 if n["metadata"]["name"] == "node-0001" else 0}
+                                      for n in body["nodes"]["items"]])
+
+        async def bind(r):
+            body = await r.json()
+            seen["bind"].append(body)
+            await api_holder["c"].bind(body["podNamespace"], body["podName"], body["node"], body.get("extendedResourceBinding"))
+            return web.json_response({})
+
+        app = web.Application()
+        app.router.add_post("/ext/filter", filt)
+        app.router.add_post("/ext/prioritize", prio)
+        app.router.add_post("/ext/bind", bind)
+        runner = web.AppRunner(app)
+        await runner.setup()
+        site = web.TCPSite(runner, "127.0.0.1", 0)
+        await site.start()
+        port = site._server.sockets[0].getsockname()[1]
+        policy = {"kind": "Policy", "extenders": [{"urlPrefix": f"http://127.0.0.1:{port}/ext", "filterVerb": "filter",
+                                                   "prioritizeVerb": "prioritize", "bindVerb": "bind", "weight": 100}]}
+        api, c, s = await _cluster(3, gpus=8, policy=policy)
+        api_holder["c"] = c
+        try:
+            await c.create(_pod("e1", gpus=2))
+            assert await _node_of(c, "e1") == "node-0001"
+            p = await c.get("pods", "e1", "default")
+            assert len(p["spec"]["extendedResources"][0]["assigned"]) == 2
+            assert seen["filter"] >= 1 and seen["prioritize"] >= 1 and len(seen["bind"]) == 1
+            assert list(seen["bind"][0]["extendedResourceBinding"].values())[0]["resources"] == \
+                p["spec"]["extendedResources"][0]["assigned"]
+        finally:
+            await _stop(api, c, s)
+            await runner.cleanup()
+    run(go())
+
+
+def test_interpod_affinity_and_anti_affinity():
+    anti = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+        {"labelSelector": {"matchLabels": {"app": "db"}}, "topologyKey": "kubernetes.io/hostname"}]}}
+    aff = {"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+        {"labelSelector": {"matchLabels": {"app": "db"}}, "topologyKey": "kubernetes.io/hostname"}]}}
+
+    async def go():
+        api, c, s = await _cluster(2)
+        try:
+            await c.create(_pod("db-0", {"app": "db"}, affinity=anti))
+            n0 = await _node_of(c, "db-0")
+            await c.create(_pod("db-1", {"app": "db"}, affinity=anti))
+            n1 = await _node_of(c, "db-1")
+            assert {n0, n1} == {"node-0000", "node-0001"}
+            await c.create(_pod("db-2", {"app": "db"}, affinity=anti))
+            cond = await _condition(c, "db-2")
+            assert "0/2 nodes are available" in cond["message"]
+            await c.create(_pod("web", {"app": "web"}, affinity=aff))
+            assert await _node_of(c, "web") in (n0, n1)
+        finally:
+            await _stop(api, c, s)
+    run(go())
+
+
+def test_extended_resource_taint_toleration():
+    async def go():
+        api, c, s = await _cluster(0)
+        fb = FakeBackend()
+        gpu = fake_node(0, 8, fb)
+        gpu["spec"] = {"taints": [{"key": "amd.com/gpu", "value": "present", "effect": "NoSchedule"}]}
+        await c.create(gpu)
+        await c.create(fake_node(1, 0, fb))
+        try:
+            # the CPU pod must avoid the tainted GPU node; the GPU pod is admitted with a
+            # toleration for the amd.com/gpu taint by ExtendedResourceToleration
+            for i in range(4):
+                await c.create(_pod(f"cpu-{i}"))
+            await c.create(_pod("gpu", gpus=1))
+            for i in range(4):
+                assert await _node_of(c, f"cpu-{i}") == "node-0001"
+            assert await _node_of(c, "gpu") == "node-0000"
+            p = await c.get("pods", "gpu", "default")
+            assert any(t.get("key") == "amd.com/gpu" and t.get("operator") == "Exists" for t in p["spec"]["tolerations"])
+        finally:
+            await _stop(api, c, s)
+    run(go())
+
+
+def test_priority_preemption_frees_devices():
+    async def go():
+        api, c, s = await _cluster(1, gpus=2)
+        try:
+            for i in range(2):
+                await c.create(_pod(f"low-{i}", gpus=1, prio=1))
+                await _node_of(c, f"low-{i}")
+            await c.create(_pod("high", gpus=2, prio=1000))
+            loop = asyncio.get_running_loop()
+            end = loop.time() + 10
+            while loop.time() < end:
+                h = await c.get("pods", "high", "default")
+                if (h.get("status") or {}).get("nominatedNodeName"):
+                    break
+                await asyncio.sleep(0.02)
+            assert h["status"]["nominatedNodeName"] == "node-0000"
+            # both 1-GPU victims are gone (or terminating); once removed, the 2-GPU pod binds
+            for i in range(2):
+                v = await c.get_or_none("pods", f"low-{i}", "default")
+                assert v is None or (v.get("metadata") or {}).get("deletionTimestamp")
+                if v is not None:
+                    await c.delete("pods", f"low-{i}", "default", grace=0)
+            assert await _node_of(c, "high", timeout=15) == "node-0000"
+            h = await c.get("pods", "high", "default")
+            assert len(h["spec"]["extendedResources"][0]["assigned"]) == 2
+        finally:
+            await _stop(api, c, s)
+    run(go())
