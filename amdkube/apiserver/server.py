@@ -413,9 +413,7 @@ class APIServer:
                     nxt = w.w.queue.get_nowait()
                     if nxt is None:
                         break
-                    t = w._translate(nxt)
-                    if t is not None:
-                        buf += self._frame(t)
+                    buf += self._frame(nxt)
                 await resp.write(bytes(buf))
         except (ConnectionResetError, asyncio.CancelledError):
             pass

@@ -65,9 +65,7 @@ def selector_spread(pi, nodes, ctx=None):
     if pi.owner is None:
         return [MAX] * len(nodes)
     uid = pi.owner.get("uid")
-    counts = []
-    for ni in nodes:
-        counts.append(sum(1 for p in ni.pods.values() if (m.controller_ref(p) or {}).get("uid") == uid))
+    counts = [ni.owners.get(uid, 0) for ni in nodes]
     mx = max(counts) if counts else 0
     return [MAX * (mx - c) / mx if mx else MAX for c in counts]
 

@@ -61,18 +61,24 @@ PUT, DELETE = "PUT", "DELETE"
 
 
 class Event:
-    __slots__ = ("type", "kv", "prev", "rev", "cache")
+    __slots__ = ("type", "kv", "prev", "rev", "cache", "prev_cache", "fields")
 
     def __init__(self, type_, kv, prev, rev):
         self.type, self.kv, self.prev, self.rev = type_, kv, prev, rev
-        self.cache = None  # decoded-object cache shared by all watchers of this event
+        self.cache = None       # decoded-object cache shared by all watchers of this event
+        self.prev_cache = None  # decoded previous object (filtered watchers)
+        self.fields = None      # field-selector sets of cur/prev, computed once per event
 
 
 class Watcher:
-    __slots__ = ("prefix", "exact", "queue", "closed", "store", "_loop", "err")
+    """One watch. `transform(ev)` (optional) runs at commit time: it returns the item to queue, or
+    None to drop the event, so a watcher never wakes up for events its filter rejects (the cacher
+    fan-out: 100 kubelets watching spec.nodeName=<self> cost one dict probe each per pod event,
+    not a decode + wakeup each)."""
+    __slots__ = ("prefix", "exact", "queue", "closed", "store", "_loop", "err", "transform")
 
-    def __init__(self, store, prefix, exact, loop):
-        self.store, self.prefix, self.exact = store, prefix, exact
+    def __init__(self, store, prefix, exact, loop, transform=None):
+        self.store, self.prefix, self.exact, self.transform = store, prefix, exact, transform
         self.queue: asyncio.Queue = asyncio.Queue()
         self.closed = False
         self.err = None
@@ -84,6 +90,15 @@ class Watcher:
     def _deliver(self, ev):
         if self.closed:
             return
+        if self.transform is not None:
+            try:
+                ev = self.transform(ev)
+            except Exception as e:  # a broken filter must not break the writer's commit
+                self.err = f"watch filter failed: {e!r}"
+                self.close()
+                return
+            if ev is None:
+                return
         if self.queue.qsize() >= self.store.max_queue:
             self.err = "watcher too slow"
             self.close()
@@ -275,17 +290,19 @@ class MVCCStore:
             self.compact_rev = max(self.compact_rev, min(rev, self.rev))
 
     # ----------------------------------------------------------------- watch
-    def watch(self, prefix: str, start_rev: int = 0, exact: bool = False) -> Watcher:
+    def watch(self, prefix: str, start_rev: int = 0, exact: bool = False, transform=None) -> Watcher:
         """Events with rev >= start_rev (0 = from now on)."""
         loop = asyncio.get_running_loop()
         with self._lock:
             if start_rev and start_rev <= self.compact_rev:
                 raise Compacted(self.compact_rev)
-            w = Watcher(self, prefix, exact, loop)
+            w = Watcher(self, prefix, exact, loop, transform)
             if start_rev:
                 for ev in self.history:
                     if ev.rev >= start_rev and w.wants(ev.kv.key):
-                        w.queue.put_nowait(ev)
+                        item = ev if transform is None else transform(ev)
+                        if item is not None:
+                            w.queue.put_nowait(item)
             self.watchers.append(w)
             return w
 

@@ -44,7 +44,11 @@ def event_object(ev: Event) -> dict:
 
 
 def event_prev_object(ev: Event) -> dict | None:
-    return json.loads(ev.prev.value) if ev.prev is not None else None
+    if ev.prev is None:
+        return None
+    if ev.prev_cache is None:
+        ev.prev_cache = json.loads(ev.prev.value)
+    return ev.prev_cache
 
 
 class Filter:
@@ -57,16 +61,31 @@ class Filter:
     def empty(self) -> bool:
         return (self.label is None or self.label.empty()) and (self.field is None or self.field.empty())
 
-    def matches(self, obj: dict) -> bool:
+    def fields_of(self, obj: dict) -> dict:
+        return self.fields_fn(obj) if self.fields_fn else {"metadata.name": m.name_of(obj),
+                                                           "metadata.namespace": m.namespace_of(obj)}
+
+    def matches(self, obj: dict, fields: dict | None = None) -> bool:
         if self.label is not None and not self.label.empty():
             if not self.label.matches(m.labels_of(obj)):
                 return False
         if self.field is not None and not self.field.empty():
-            fields = self.fields_fn(obj) if self.fields_fn else {"metadata.name": m.name_of(obj),
-                                                                  "metadata.namespace": m.namespace_of(obj)}
-            if not self.field.matches(fields):
+            if not self.field.matches(fields if fields is not None else self.fields_of(obj)):
                 return False
         return True
+
+    def matches_event(self, ev: Event, obj: dict, which: int) -> bool:
+        """matches() with the field set cached on the event (computed once for all watchers)."""
+        if self.field is None or self.field.empty():
+            return self.matches(obj)
+        key = (which, self.fields_fn)
+        fc = ev.fields
+        if fc is None:
+            fc = ev.fields = {}
+        f = fc.get(key)
+        if f is None:
+            f = fc[key] = self.fields_of(obj)
+        return self.matches(obj, f)
 
 
 class Storage:
@@ -168,15 +187,20 @@ class Storage:
     # ------------------------------------------------------------------ watch
     def watch(self, prefix: str, rv: str | int | None, flt: Filter | None = None, exact=False) -> "FilteredWatch":
         start = int(rv) + 1 if rv not in (None, "", "0", 0) else 0
+        fw = FilteredWatch(None, flt)
         try:
-            w = self.store.watch(prefix, start, exact)
+            fw.w = self.store.watch(prefix, start, exact, transform=fw._translate)
         except Compacted as e:
             raise m.gone(f"too old resource version: {rv} ({e.compact_rev})")
-        return FilteredWatch(w, flt)
+        return fw
 
 
 class FilteredWatch:
-    """Translates raw KV events into (type, obj) honouring a filter (cacher semantics)."""
+    """Translates raw KV events into (type, obj, ev) honouring a filter (cacher semantics).
+
+    The translation runs as the store watcher's commit-time transform, so the queue only ever
+    holds events this watch delivers, already translated.
+    """
 
     def __init__(self, w, flt: Filter | None):
         self.w, self.flt = w, flt if (flt is not None and not flt.empty()) else None
@@ -194,11 +218,13 @@ class FilteredWatch:
             if ev.type == DELETE:
                 return m.DELETED, obj, ev
             return (m.ADDED if ev.prev is None else m.MODIFIED), obj, ev
-        cur_ok = ev.type == PUT and self.flt.matches(obj)
+        cur_ok = ev.type == PUT and self.flt.matches_event(ev, obj, 0)
         prev_ok = False
         if ev.prev is not None:
-            prev_obj = obj if ev.type == DELETE else event_prev_object(ev)
-            prev_ok = self.flt.matches(prev_obj)
+            if ev.type == DELETE:
+                prev_ok = self.flt.matches_event(ev, obj, 0)
+            else:
+                prev_ok = self.flt.matches_event(ev, event_prev_object(ev), 1)
         if ev.type == DELETE:
             return (m.DELETED, obj, ev) if prev_ok else None
         if cur_ok and prev_ok:
@@ -211,18 +237,7 @@ class FilteredWatch:
 
     async def next(self, timeout: float | None = None):
         """(type, obj, raw_event) or None when closed / timed out."""
-        loop = asyncio.get_running_loop()
-        deadline = None if timeout is None else loop.time() + timeout
-        while True:
-            rem = None if deadline is None else max(0.0, deadline - loop.time())
-            ev = await self.w.next(rem)
-            if ev is None:
-                return None
-            t = self._translate(ev)
-            if t is not None:
-                return t
-            if deadline is not None and loop.time() >= deadline:
-                return None
+        return await self.w.next(timeout)
 
     def __aiter__(self):
         return self

@@ -13,7 +13,9 @@ the whole job (all N GPUs); extra fields carry startup-latency percentiles and t
 scheduler_perf (100 nodes / 3000 pods) result.
 
 Baselines: density saturation ≥ 8 pods/s (vs_baseline = value / 8),
-pod startup p50/p90/p99 ≤ 5 s, scheduler throughput ≥ 30 pods/s (goal 100).
+pod startup p50/p90/p99 ≤ 5 s, scheduler throughput ≥ 30 pods/s (goal 100). The extra
+`density` field is the reference density test itself (100 hollow nodes × 30 pods, 8 of them
+GPU pods per node; amdkube/benchmark/density.py), run after the timed region.
 """
 from __future__ import annotations
 
@@ -38,6 +40,7 @@ def main():
     ap.add_argument("--pods-per-gpu", type=int, default=4)
     ap.add_argument("--backend", default="auto", help="amdsmi|sysfs|fake|auto")
     ap.add_argument("--no-sched-perf", action="store_true")
+    ap.add_argument("--density-nodes", type=int, default=100, help="hollow-node density run (0 = skip)")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -104,6 +107,17 @@ def main():
             worker.stdin.write(json.dumps({"cmd": "schedperf", "nodes": 100, "pods": 3000}) + "\n")
             worker.stdin.flush()
             sched = json.loads(worker.stdout.readline())
+        density = None
+        if a.density_nodes:
+            # the reference's headline density test (30 pods/node saturation) on hollow MI355X nodes;
+            # a child process so its control plane does not share this rank's core (not timed)
+            env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+            try:
+                r = subprocess.run([sys.executable, "-m", "amdkube.benchmark.density", "--nodes", str(a.density_nodes),
+                                    "--node-procs", "4"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+                density = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else {"error": r.stderr[-500:]}
+            except Exception as e:
+                density = {"error": repr(e)}
         worker.stdin.write(json.dumps({"cmd": "quit"}) + "\n")
         worker.stdin.flush()
         try:
@@ -122,7 +136,7 @@ def main():
                "p99_startup_ms": res["p99_startup_ms"], "startup_slo_ms": SLO_STARTUP_MS,
                "p50_node_startup_ms": res["p50_node_startup_ms"], "p50_schedule_ms": res["p50_schedule_ms"],
                "p50_pod_runtime_ms": res["p50_pod_runtime_ms"], "failed_pods": res["failed"],
-               "sched_perf": sched}
+               "sched_perf": sched, "density": density}
         if res["failed"]:
             out["failures"] = res["failures"]
         print(json.dumps(out), flush=True)
