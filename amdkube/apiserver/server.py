@@ -105,7 +105,7 @@ class APIServer:
     async def stop(self):
         for t in self._bg:
             t.cancel()
-        for w in list(self.store.watchers):
+        for w in self.store.all_watchers():
             w.close()
         if self._http:
             await self._http.close()

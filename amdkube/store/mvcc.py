@@ -75,10 +75,11 @@ class Watcher:
     None to drop the event, so a watcher never wakes up for events its filter rejects (the cacher
     fan-out: 100 kubelets watching spec.nodeName=<self> cost one dict probe each per pod event,
     not a decode + wakeup each)."""
-    __slots__ = ("prefix", "exact", "queue", "closed", "store", "_loop", "err", "transform")
+    __slots__ = ("prefix", "exact", "queue", "closed", "store", "_loop", "err", "transform", "trigger")
 
-    def __init__(self, store, prefix, exact, loop, transform=None):
+    def __init__(self, store, prefix, exact, loop, transform=None, trigger=None):
         self.store, self.prefix, self.exact, self.transform = store, prefix, exact, transform
+        self.trigger = trigger  # (fn, value): only events whose fn(ev) contains value can match
         self.queue: asyncio.Queue = asyncio.Queue()
         self.closed = False
         self.err = None
@@ -159,6 +160,10 @@ class MVCCStore:
         self.history_limit = history
         self.max_queue = max_queue
         self.watchers: list[Watcher] = []
+        # trigger index (cacher.go triggerFunc, e.g. pods by spec.nodeName): (prefix, fn) -> value -> watchers.
+        # fn(ev) returns every value a filter keyed on it could match (old and new object), so a
+        # watcher outside that set is skipped without running its filter.
+        self.triggered: dict[tuple, dict[str, list[Watcher]]] = {}
         self._lock = threading.RLock()
         self.data_dir = data_dir
         self.snapshot_every = snapshot_every
@@ -281,6 +286,14 @@ class MVCCStore:
         for w in list(self.watchers):
             if w.wants(key):
                 w.deliver(ev)
+        if self.triggered:
+            for (prefix, fn), idx in list(self.triggered.items()):
+                if not key.startswith(prefix):
+                    continue
+                for v in fn(ev):
+                    for w in list(idx.get(v, ())):
+                        if w.wants(key):
+                            w.deliver(ev)
 
     def compact(self, rev: int):
         """Drop history at or below `rev` (etcd Compact)."""
@@ -290,28 +303,53 @@ class MVCCStore:
             self.compact_rev = max(self.compact_rev, min(rev, self.rev))
 
     # ----------------------------------------------------------------- watch
-    def watch(self, prefix: str, start_rev: int = 0, exact: bool = False, transform=None) -> Watcher:
-        """Events with rev >= start_rev (0 = from now on)."""
+    def watch(self, prefix: str, start_rev: int = 0, exact: bool = False, transform=None, trigger=None) -> Watcher:
+        """Events with rev >= start_rev (0 = from now on). `trigger=(fn, value)` indexes the
+        watcher (see self.triggered); it is an optimisation only, `transform` stays the filter."""
         loop = asyncio.get_running_loop()
         with self._lock:
             if start_rev and start_rev <= self.compact_rev:
                 raise Compacted(self.compact_rev)
-            w = Watcher(self, prefix, exact, loop, transform)
+            w = Watcher(self, prefix, exact, loop, transform, None if exact else trigger)
             if start_rev:
                 for ev in self.history:
                     if ev.rev >= start_rev and w.wants(ev.kv.key):
                         item = ev if transform is None else transform(ev)
                         if item is not None:
                             w.queue.put_nowait(item)
-            self.watchers.append(w)
+            if w.trigger is not None:
+                fn, value = w.trigger
+                self.triggered.setdefault((prefix, fn), {}).setdefault(value, []).append(w)
+            else:
+                self.watchers.append(w)
             return w
+
+    def all_watchers(self) -> list[Watcher]:
+        out = list(self.watchers)
+        for idx in self.triggered.values():
+            for ws in idx.values():
+                out.extend(ws)
+        return out
 
     def _remove_watcher(self, w):
         with self._lock:
-            try:
-                self.watchers.remove(w)
-            except ValueError:
-                pass
+            if w.trigger is None:
+                try:
+                    self.watchers.remove(w)
+                except ValueError:
+                    pass
+                return
+            fn, value = w.trigger
+            idx = self.triggered.get((w.prefix, fn))
+            if idx is None:
+                return
+            ws = idx.get(value)
+            if ws and w in ws:
+                ws.remove(w)
+                if not ws:
+                    del idx[value]
+                    if not idx:
+                        del self.triggered[(w.prefix, fn)]
 
     # ------------------------------------------------------------ durability
     def snapshot(self):
@@ -363,7 +401,7 @@ class MVCCStore:
             self._index_put(key, kv)
 
     def close(self):
-        for w in list(self.watchers):
+        for w in self.all_watchers():
             w.close()
         if self._wal is not None:
             self._wal.close()

@@ -88,7 +88,38 @@ class Filter:
         return self.matches(obj, f)
 
 
+_TRIGGERS: dict[tuple, Callable] = {}
+
+
+def field_trigger(fields_fn: Callable, field: str) -> Callable:
+    """Trigger function for exact `field=value` watches: the field's value in the new and the
+    old object of an event (one shared function per (fields_fn, field), so the store groups all
+    such watchers under one index). Uses the same per-event field cache as Filter.matches_event."""
+    key = (fields_fn, field)
+    fn = _TRIGGERS.get(key)
+    if fn is None:
+        def fn(ev: Event, _fields_fn=fields_fn, _field=field):
+            fc = ev.fields
+            if fc is None:
+                fc = ev.fields = {}
+            f0 = fc.get((0, _fields_fn))
+            if f0 is None:
+                f0 = fc[(0, _fields_fn)] = _fields_fn(event_object(ev))
+            vals = {f0.get(_field, "")}
+            if ev.prev is not None and ev.type == PUT:
+                f1 = fc.get((1, _fields_fn))
+                if f1 is None:
+                    f1 = fc[(1, _fields_fn)] = _fields_fn(event_prev_object(ev))
+                vals.add(f1.get(_field, ""))
+            return vals
+        _TRIGGERS[key] = fn
+    return fn
+
+
 class Storage:
+    # fields whose exact-match watches are indexed (cacher.go: pods by spec.nodeName)
+    TRIGGER_FIELDS = ("spec.nodeName",)
+
     def __init__(self, store: MVCCStore, resource: str = "object"):
         self.store = store
         self.resource = resource
@@ -188,8 +219,14 @@ class Storage:
     def watch(self, prefix: str, rv: str | int | None, flt: Filter | None = None, exact=False) -> "FilteredWatch":
         start = int(rv) + 1 if rv not in (None, "", "0", 0) else 0
         fw = FilteredWatch(None, flt)
+        trigger = None
+        if flt is not None and flt.fields_fn is not None and flt.field is not None:
+            for f, op, v in flt.field.terms:
+                if op == "=" and f in self.TRIGGER_FIELDS:
+                    trigger = (field_trigger(flt.fields_fn, f), v)
+                    break
         try:
-            fw.w = self.store.watch(prefix, start, exact, transform=fw._translate)
+            fw.w = self.store.watch(prefix, start, exact, transform=fw._translate, trigger=trigger)
         except Compacted as e:
             raise m.gone(f"too old resource version: {rv} ({e.compact_rev})")
         return fw

@@ -7,6 +7,7 @@ import pytest
 from hypothesis import given, settings, strategies as st
 
 from amdkube.store import CASFailed, Compacted, KeyExists, MVCCStore, Storage, Filter, PUT, DELETE
+from amdkube.store.storage import FilteredWatch
 from amdkube.api import labels as L
 from amdkube.api import meta as m
 from tests.conftest import run
@@ -104,3 +105,47 @@ def test_store_matches_model(ops):
             elif op == "del":
                 assert key not in model
         assert {kk: (v.value, v.mod_rev) for kk, v in s.kv.items()} == model
+
+
+@settings(max_examples=40, deadline=None)
+@given(st.lists(st.tuples(st.sampled_from(["create", "bind", "status", "del"]), st.integers(0, 5),
+                          st.sampled_from(["", "n1", "n2"])), max_size=40))
+def test_triggered_watch_equals_filtered_watch(ops):
+    """The spec.nodeName trigger index (store.triggered) is an optimisation only: a watch it
+    indexes must deliver exactly the events an unindexed watch with the same filter delivers."""
+    from amdkube.apiserver.registry import pod_fields
+    from amdkube.store.storage import field_trigger
+
+    async def go():
+        s = MVCCStore()
+        st_ = Storage(s, "pods")
+        flt = lambda: Filter(None, L.parse_field_selector("spec.nodeName=n1"), pod_fields)  # noqa: E731
+        indexed = st_.watch("/registry/pods/", "0", flt())
+        assert indexed.w.trigger is not None and indexed.w not in s.watchers
+        plain = FilteredWatch(None, flt())
+        plain.w = s.watch("/registry/pods/", 0, transform=plain._translate)  # no trigger
+        for op, i, node in ops:
+            key = f"/registry/pods/default/p{i}"
+            try:
+                if op == "create":
+                    st_.create(key, {"metadata": {"name": f"p{i}"}, "spec": {"nodeName": node}, "status": {}})
+                elif op == "bind":
+                    st_.guaranteed_update(key, lambda c: {**c, "spec": {"nodeName": node}})
+                elif op == "status":
+                    st_.guaranteed_update(key, lambda c: {**c, "status": {"phase": node or "Pending"}})
+                else:
+                    st_.delete(key)
+            except m.StatusError:
+                pass
+
+        def drain(w):
+            out = []
+            while not w.w.queue.empty():
+                typ, obj, ev = w.w.queue.get_nowait()
+                out.append((typ, obj["metadata"]["name"], ev.rev))
+            return out
+        assert drain(indexed) == drain(plain)
+        indexed.close()
+        plain.close()
+        assert not s.triggered
+    run(go())
