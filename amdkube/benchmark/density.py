@@ -5,8 +5,9 @@ at 30 pods/node (:55-56, :364-367) and fails below 8 pods/s. It reports pod star
 phases from a watch: create→schedule, schedule→run, run→watch, and e2e (:771-819). The SLO is
 p50/p90/p99 ≤ 5 s (test/e2e/framework/metrics_util.go:46).
 
-amdkube runs the same experiment with the real control plane in this process:
-  * apiserver, scheduler and controller-manager (ReplicaSet controller);
+amdkube runs the same experiment with the real control plane:
+  * apiserver in this process; scheduler and controller-manager (ReplicaSet controller) as their
+    own processes, as in a real deployment (`--in-process` keeps all three here);
   * N hollow nodes in a child process (`python -m amdkube hollow-node --count N`). Each hollow
     node is a real kubelet with the real AMD device plugin over a simulated 8×MI355X and a fake
     CRI runtime. The reference's kubemark had no GPUs at all.
@@ -56,19 +57,28 @@ def _rs(name, replicas, gpu):
 
 
 async def run_density(n_nodes: int = 10, pods_per_node: int = 30, gpus_per_node: int = 8, node_procs: int = 2,
-                      timeout: float = 300.0) -> dict:
+                      timeout: float = 300.0, in_process: bool = False) -> dict:
     api = await APIServer(event_ttl=3600).start()
     client = Client(api.url, pool=128)
-    sched = await Scheduler(Client(api.url, pool=256)).start()
-    cm = await ControllerManager(Client(api.url, pool=128), controllers=["replicaset"]).start()
+    sched = cm = None
     procs = []
-    per = [n_nodes // node_procs + (1 if i < n_nodes % node_procs else 0) for i in range(node_procs)]
     env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    if in_process:
+        sched = await Scheduler(Client(api.url, pool=256)).start()
+        cm = await ControllerManager(Client(api.url, pool=128), controllers=["replicaset"]).start()
+    else:
+        for argv in (["scheduler", "--master", api.url, "--port", "0"],
+                     ["controller-manager", "--master", api.url, "--controllers", "replicaset"]):
+            procs.append(subprocess.Popen([sys.executable, "-m", "amdkube", *argv], cwd=ROOT, env=env,
+                                          stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL))
+    per = [n_nodes // node_procs + (1 if i < n_nodes % node_procs else 0) for i in range(node_procs)]
     try:
         for i, cnt in enumerate(per):
             if cnt:
+                prof = os.environ.get("AMDKUBE_PROFILE_HOLLOW")  # cProfile output path for hollow process 0
+                pre = ["-m", "cProfile", "-o", prof] if prof and i == 0 else []
                 procs.append(subprocess.Popen(
-                    [sys.executable, "-m", "amdkube", "hollow-node", "--server", api.url, "--count", str(cnt),
+                    [sys.executable, *pre, "-m", "amdkube", "hollow-node", "--server", api.url, "--count", str(cnt),
                      "--gpus", str(gpus_per_node), "--name-prefix", f"hollow{i}"],
                     cwd=ROOT, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL))
         loop = asyncio.get_running_loop()
@@ -141,10 +151,12 @@ async def run_density(n_nodes: int = 10, pods_per_node: int = 30, gpus_per_node:
                 p.wait(10)
             except subprocess.TimeoutExpired:
                 p.kill()
-        await cm.stop()
-        await sched.stop()
-        await sched.client.close()
-        await cm.client.close()
+        if cm is not None:
+            await cm.stop()
+            await cm.client.close()
+        if sched is not None:
+            await sched.stop()
+            await sched.client.close()
         await client.close()
         await api.stop()
 
@@ -155,8 +167,10 @@ def main(argv=None):
     ap.add_argument("--pods-per-node", type=int, default=30)
     ap.add_argument("--gpus-per-node", type=int, default=8)
     ap.add_argument("--node-procs", type=int, default=2)
+    ap.add_argument("--in-process", action="store_true", help="scheduler + controller-manager in the apiserver process")
     a = ap.parse_args(argv)
-    print(json.dumps(asyncio.run(run_density(a.nodes, a.pods_per_node, a.gpus_per_node, a.node_procs))))
+    print(json.dumps(asyncio.run(run_density(a.nodes, a.pods_per_node, a.gpus_per_node, a.node_procs,
+                                             in_process=a.in_process))))
 
 
 if __name__ == "__main__":

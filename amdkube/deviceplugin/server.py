@@ -25,6 +25,7 @@ import grpc
 
 from ..grpcdesc.deviceplugin import (DEVICE_PLUGINS_PATH, HEALTHY, REGISTRATION as R, V1ALPHA2 as P, V1BETA1 as B,
                                      VERSION, V1BETA1_VERSION)
+from ..utils.grpcutil import uds_channel
 
 log = logging.getLogger("amdkube.deviceplugin")
 
@@ -123,7 +124,7 @@ class DevicePluginServer:
 
     async def register_v1beta1(self, kubelet_socket: str, endpoint: str | None = None):
         """Upstream-style registration: call Registration.Register on the kubelet socket."""
-        async with grpc.aio.insecure_channel("unix://" + kubelet_socket) as ch:
+        async with uds_channel(kubelet_socket) as ch:
             stub = B.Registration.stub(ch)
             await stub.Register(B.RegisterRequest(version=V1BETA1_VERSION, endpoint=endpoint or os.path.basename(self.socket),
                                                   resource_name=self.resource_name,

@@ -8,6 +8,7 @@ import time
 import grpc
 
 from ..grpcdesc.cri import CRI as C
+from ..utils.grpcutil import uds_channel
 
 
 class CRIClient:
@@ -19,7 +20,7 @@ class CRIClient:
         self.metrics = metrics  # (ops Counter, errs Counter, latency Summary) or None
 
     async def connect(self, wait: float = 10.0):
-        self.ch = grpc.aio.insecure_channel("unix://" + self.socket)
+        self.ch = uds_channel(self.socket)
         import asyncio
         await asyncio.wait_for(self.ch.channel_ready(), wait)
         self.rt = C.RuntimeService.stub(self.ch)
@@ -30,8 +31,14 @@ class CRIClient:
         if self.ch is not None:
             await self.ch.close()
 
+    _MUTATING = frozenset(("run_podsandbox", "stop_podsandbox", "remove_podsandbox", "create_container", "start_container",
+                           "stop_container", "remove_container"))
+    mutations = 0  # mutating RPCs issued (invalidates the kubelet's runtime-status cache)
+
     async def _call(self, op, fn, req, timeout=None):
         t0 = time.perf_counter()
+        if op in self._MUTATING:
+            self.mutations += 1
         try:
             return await fn(req, timeout=timeout or self.timeout)
         except grpc.RpcError:

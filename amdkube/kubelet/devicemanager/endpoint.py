@@ -25,6 +25,7 @@ import grpc
 from ...api.helpers import is_extended_resource_name
 from ...grpcdesc.deviceplugin import REGISTRATION as R, V1ALPHA2 as P, V1BETA1 as B, VERSION
 from .stores import AlwaysEmptyDeviceStore, DeviceStore
+from ...utils.grpcutil import uds_channel
 
 log = logging.getLogger("amdkube.devicemanager")
 
@@ -37,7 +38,7 @@ class RegistrationError(Exception):
 
 
 async def dial(path: str, timeout: float = DIAL_TIMEOUT) -> grpc.aio.Channel:
-    ch = grpc.aio.insecure_channel("unix://" + path)
+    ch = uds_channel(path)
     try:
         await asyncio.wait_for(ch.channel_ready(), timeout)
     except (asyncio.TimeoutError, Exception) as e:

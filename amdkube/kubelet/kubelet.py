@@ -82,6 +82,12 @@ class PodWorker:
         self.last_sync = 0.0
 
 
+def _semantic(pod: dict):
+    md = pod.get("metadata") or {}
+    return (pod.get("spec"), md.get("labels"), md.get("annotations"), md.get("deletionTimestamp"),
+            md.get("deletionGracePeriodSeconds"))
+
+
 class Kubelet:
     def __init__(self, client: Client, config: KubeletConfig, smi_backend=None):
         self.client = client
@@ -113,6 +119,11 @@ class Kubelet:
         self._node_dirty = asyncio.Event()
         self._sandbox_uid: dict[str, str] = {}
         self._pleg_snapshot: dict[str, int] = {}
+        # runtime pod-status cache (reference kubecontainer.Cache fed by PLEG, GetNewerThan): the
+        # status observed after a sync stays valid until a PLEG event for the pod (generation bump)
+        # or any mutating CRI call by this kubelet
+        self._rt_gen: dict[str, int] = {}
+        self._rt_cache: dict[str, tuple] = {}
         self.smi = smi_backend
         self.server = None
         self.first_seen: dict[str, float] = {}
@@ -288,7 +299,11 @@ class Kubelet:
 
     def _on_pod_update(self, old, pod):
         self.pods[m.uid_of(pod)] = pod
-        self.dispatch(m.uid_of(pod))
+        # only semantic changes wake the pod worker (reference pkg/kubelet/config/config.go
+        # checkAndUpdatePod / podsDifferSemantically): the kubelet's own status writes echo back
+        # through the watch and must not trigger another runtime sync
+        if old is None or _semantic(old) != _semantic(pod):
+            self.dispatch(m.uid_of(pod))
 
     def _on_pod_delete(self, pod):
         uid = m.uid_of(pod)
@@ -422,9 +437,11 @@ class Kubelet:
             await self.runtime.kill_pod(uid, 0, pod)
             return False
         ctx = await self._pod_context(pod)
-        rt = await self.runtime.pod_status(uid)
+        rt = await self._cached_status(uid)
+        mut0 = self.cri.mutations
         errors = await self.runtime.sync_pod(pod, rt, ctx, self.liveness_failed.pop(uid, None))
-        rt = await self.runtime.pod_status(uid)
+        if self.cri.mutations != mut0 or errors:
+            rt = await self._cached_status(uid, fresh=True)
         for sb in rt.sandboxes:
             self._sandbox_uid[sb[0]] = uid
         st = generate_status(pod, rt, self.cfg.node_ip, self.readiness.get(uid, {}), errors, m.now_rfc3339())
@@ -468,7 +485,22 @@ class Kubelet:
     def _on_terminal(self, uid):
         pass
 
+    async def _cached_status(self, uid: str, fresh: bool = False):
+        key = (self._rt_gen.get(uid, 0), self.cri.mutations)
+        hit = self._rt_cache.get(uid)
+        if not fresh and hit is not None and hit[0] == key:
+            return hit[1]
+        rt = await self.runtime.pod_status(uid)
+        self._rt_cache[uid] = (key, rt)  # key taken before the fetch: a concurrent event invalidates it
+        return rt
+
+    def _pleg_event(self, uid: str):
+        self._rt_gen[uid] = self._rt_gen.get(uid, 0) + 1
+        self.dispatch(uid)
+
     def _cleanup(self, uid):
+        self._rt_gen.pop(uid, None)
+        self._rt_cache.pop(uid, None)
         self.admitted.discard(uid)
         self.rejected.pop(uid, None)
         self.status.forget(uid)
@@ -586,14 +618,14 @@ class Kubelet:
                 running_c += 1
             if self._pleg_snapshot.get(c.id) != c.state:
                 uids_changed.add(self._sandbox_uid.get(c.pod_sandbox_id) or c.labels.get(L_POD_UID, ""))
-        for cid in set(self._pleg_snapshot) - set(cur):
-            uids_changed.add("")  # removed container; owning pod unknown → periodic sync covers it
+        if set(self._pleg_snapshot) - set(cur):
+            self._rt_cache.clear()  # a container vanished and its owner is unknown: drop every cached status
         self._pleg_snapshot = cur
         self.m_running_pods.set(running_pods)
         self.m_running_containers.set(running_c)
         for uid in uids_changed:
             if uid and (uid in self.pods or uid in self.workers):
-                self.dispatch(uid)
+                self._pleg_event(uid)
         # orphaned sandboxes (pod deleted while the kubelet was down)
         for s in sbs:
             uid = s.labels.get(L_POD_UID, "")
@@ -614,7 +646,7 @@ class Kubelet:
                         uid = self._sandbox_uid.get(sid)
                     if uid and ev.container_event_type in (C.CONTAINER_STOPPED_EVENT, C.CONTAINER_STARTED_EVENT):
                         if uid in self.pods or uid in self.workers:
-                            self.dispatch(uid)
+                            self._pleg_event(uid)
             except asyncio.CancelledError:
                 raise
             except Exception as e:
@@ -627,7 +659,7 @@ class Kubelet:
         while True:
             await asyncio.sleep(self.cfg.sync_frequency)
             for uid in list(self.pods):
-                self.dispatch(uid)
+                self._pleg_event(uid)  # periodic resync re-reads the runtime (never trusts the cache)
             self.last_sync_loop = time.time()
 
     # ================================================================ probes
