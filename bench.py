@@ -114,7 +114,7 @@ def main():
             env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
             try:
                 r = subprocess.run([sys.executable, "-m", "amdkube.benchmark.density", "--nodes", str(a.density_nodes),
-                                    "--node-procs", "4"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+                                    "--node-procs", "6"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
                 density = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else {"error": r.stderr[-500:]}
             except Exception as e:
                 density = {"error": repr(e)}
