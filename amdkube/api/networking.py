@@ -1,0 +1,62 @@
+"""Service validation and defaulting (reference pkg/apis/core/validation/validation.go
+ValidateService, pkg/apis/core/v1/defaults.go SetDefaults_Service)."""
+from __future__ import annotations
+
+from .labels import is_dns1123_label
+
+SERVICE_TYPES = ("ClusterIP", "NodePort", "LoadBalancer", "ExternalName")
+
+
+def validate_service(svc: dict, old=None) -> list[str]:
+    from .validation import validate_object_meta
+    errs = validate_object_meta(svc, True, is_dns1123_label)
+    spec = svc.get("spec") or {}
+    t = spec.get("type", "ClusterIP")
+    if t not in SERVICE_TYPES:
+        errs.append(f"spec.type: Unsupported value: {t!r}: supported values: {', '.join(SERVICE_TYPES)}")
+    if t == "ExternalName":
+        if not spec.get("externalName"):
+            errs.append("spec.externalName: Required value")
+        return errs
+    ports = spec.get("ports") or []
+    if not ports and spec.get("clusterIP") != "None":
+        errs.append("spec.ports: Required value")
+    seen_names, seen_ports = set(), set()
+    for i, p in enumerate(ports):
+        pref = f"spec.ports[{i}]"
+        if len(ports) > 1 and not p.get("name"):
+            errs.append(f"{pref}.name: Required value")
+        if p.get("name"):
+            if p["name"] in seen_names:
+                errs.append(f"{pref}.name: Duplicate value: {p['name']!r}")
+            seen_names.add(p["name"])
+        port = p.get("port")
+        if not isinstance(port, int) or not 0 < port < 65536:
+            errs.append(f"{pref}.port: Invalid value: {port!r}: must be between 1 and 65535, inclusive")
+        proto = p.get("protocol", "TCP")
+        if proto not in ("TCP", "UDP"):
+            errs.append(f"{pref}.protocol: Unsupported value: {proto!r}: supported values: TCP, UDP")
+        if (proto, port) in seen_ports:
+            errs.append(f"{pref}: Duplicate value: {proto}/{port}")
+        seen_ports.add((proto, port))
+        tp = p.get("targetPort")
+        if tp is not None and not ((isinstance(tp, int) and 0 < tp < 65536) or (isinstance(tp, str) and tp)):
+            errs.append(f"{pref}.targetPort: Invalid value: {tp!r}")
+        if p.get("nodePort") and t == "ClusterIP":
+            errs.append(f"{pref}.nodePort: Forbidden: may not be used when `type` is 'ClusterIP'")
+    aff = spec.get("sessionAffinity", "None")
+    if aff not in ("None", "ClientIP"):
+        errs.append(f"spec.sessionAffinity: Unsupported value: {aff!r}")
+    sel = spec.get("selector") or {}
+    if not isinstance(sel, dict):
+        errs.append("spec.selector: Invalid value: must be a map")
+    return errs
+
+
+def default_service(svc: dict):
+    spec = svc.setdefault("spec", {})
+    spec.setdefault("type", "ClusterIP")
+    spec.setdefault("sessionAffinity", "None")
+    for p in spec.get("ports") or []:
+        p.setdefault("protocol", "TCP")
+        p.setdefault("targetPort", p.get("port"))

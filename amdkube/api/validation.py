@@ -366,6 +366,8 @@ register_hooks("DaemonSet", "apps/v1", validator=validate_daemonset)
 register_hooks("ReplicaSet", "apps/v1", validator=_validate_template_owner)
 register_hooks("Deployment", "apps/v1", validator=_validate_template_owner)
 register_hooks("Job", "batch/v1", validator=validate_job)
-for _k in ("ConfigMap", "Secret", "ServiceAccount", "Endpoints", "Service", "LimitRange", "ResourceQuota",
+from .networking import default_service, validate_service  # noqa: E402
+register_hooks("Service", defaulter=default_service, validator=validate_service)
+for _k in ("ConfigMap", "Secret", "ServiceAccount", "Endpoints", "LimitRange", "ResourceQuota",
            "PersistentVolumeClaim"):
     register_hooks(_k, validator=validate_generic_namespaced)

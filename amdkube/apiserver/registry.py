@@ -27,6 +27,7 @@ from ..api.scheme import SCHEME, ResourceInfo
 from ..api.validation import validate_binding
 from ..store import Filter, MVCCStore, Storage, event_object, PUT
 from . import admission as adm
+from .service import ServiceAllocator
 
 
 def _json_merge_patch(target, patch):
@@ -265,6 +266,9 @@ class ResourceStore:
             obj["status"] = {"phase": "Active"}
         elif p in _STATUS_KINDS and p not in ("nodes",):
             obj["status"] = {}
+        if p == "services":
+            md = obj["metadata"]
+            self.api.services.prepare_create(self.key(md.get("namespace", ""), md.get("name", "")), obj)
 
     def _prepare_update(self, new, cur, subresource):
         md, cmd = new.setdefault("metadata", {}), cur.get("metadata") or {}
@@ -287,6 +291,8 @@ class ResourceStore:
                 new.pop("status", None)
         if self.generation:
             md["generation"] = cmd.get("generation", 1) + (1 if new.get("spec") != cur.get("spec") else 0)
+        if self.ri.plural == "services" and subresource != "status":
+            self.api.services.prepare_update(self.key(md.get("namespace", ""), md.get("name", "")), new, cur)
         if self.ri.plural == "pods" and subresource != "status":
             # only pods/binding may write spec.nodeName and extendedResources[].assigned
             cur_spec = cur.get("spec") or {}
@@ -414,9 +420,10 @@ def _validate_pod_status(pod):
 class Registry:
     """All resource stores + admission context + the node device-assignment index."""
 
-    def __init__(self, store: MVCCStore, admission: adm.Chain):
+    def __init__(self, store: MVCCStore, admission: adm.Chain, services: ServiceAllocator | None = None):
         self.store = store
         self.admission = admission
+        self.services = services or ServiceAllocator()
         self.resources: dict[tuple[str, str], ResourceStore] = {}
         for ri in SCHEME.by_kind.values():
             if ri.plural == "bindings":
@@ -476,14 +483,16 @@ class Registry:
 
     def _on_commit(self, ev):
         k = ev.kv.key
-        if not k.startswith("/registry/pods/"):
-            return
-        self._index_pod(k, event_object(ev) if ev.type == PUT else None)
+        if k.startswith("/registry/pods/"):
+            self._index_pod(k, event_object(ev) if ev.type == PUT else None)
+        elif k.startswith("/registry/services/"):
+            self.services.index(k, event_object(ev) if ev.type == PUT else None)
 
     def _rebuild_index(self):
         kvs, _, _ = self.store.range("/registry/pods/")
         for kv in kvs:
             self._index_pod(kv.key, json.loads(kv.value))
+        self.services.rebuild(self.store.range("/registry/services/")[0])  # ipallocator/portallocator repair
 
     # ------------------------------------------------------------- binding
     def bind(self, ns: str, binding: dict, user=None) -> dict:

@@ -29,6 +29,7 @@ from ..utils import profiling
 from ..utils.metrics import CONTENT_TYPE, MICRO_BUCKETS, Counter, Histogram, new_registry, render
 from . import admission as adm
 from .registry import Registry
+from .service import ServiceAllocator, parse_port_range
 
 log = logging.getLogger("amdkube.apiserver")
 
@@ -48,10 +49,10 @@ class APIServer:
     def __init__(self, store: MVCCStore | None = None, admission_plugins=adm.DEFAULT_CHAIN, admission_config=None,
                  token_auth: dict | None = None, authorization_mode: str = "AlwaysAllow",
                  max_in_flight: int = 400, max_mutating_in_flight: int = 200, event_ttl: float = 3600.0,
-                 anonymous_auth: bool = True):
+                 anonymous_auth: bool = True, service_cidr: str = "10.0.0.0/24", node_port_range: str = "30000-32767"):
         self.store = store or MVCCStore()
         self.admission = adm.Chain(admission_plugins, admission_config)
-        self.registry = Registry(self.store, self.admission)
+        self.registry = Registry(self.store, self.admission, ServiceAllocator(service_cidr, parse_port_range(node_port_range)))
         self.tokens = token_auth or {}
         self.anonymous = anonymous_auth
         self.authz_mode = authorization_mode
@@ -95,8 +96,35 @@ class APIServer:
         self.port = self._site._server.sockets[0].getsockname()[1]
         self.host = host
         self._bg.append(asyncio.create_task(self._event_gc()))
+        self._reconcile_master_service()
         log.info("apiserver serving on http://%s:%d", host, self.port)
         return self
+
+    def _reconcile_master_service(self):
+        """pkg/master/controller.go: the `kubernetes` service (first IP of the service range, port
+        443 "https") and its endpoints pointing at this apiserver."""
+        alloc = self.registry.services
+        first = str(next(alloc.net.hosts())) if alloc.net.num_addresses > 2 else str(alloc.net.network_address)
+        svc = {"apiVersion": "v1", "kind": "Service", "metadata": {"name": "kubernetes", "namespace": "default",
+                                                                    "labels": {"component": "apiserver", "provider": "kubernetes"}},
+               "spec": {"clusterIP": first, "ports": [{"name": "https", "port": 443, "protocol": "TCP", "targetPort": self.port}],
+                        "sessionAffinity": "ClientIP"}}
+        rs = self.registry.rs("services")
+        try:
+            if rs.storage.get(rs.key("default", "kubernetes"), ignore_not_found=True) is None:
+                rs.create("default", svc)
+        except m.StatusError as e:
+            log.warning("cannot create the kubernetes service: %s", e)
+        ip = self.host if self.host not in ("0.0.0.0", "", "::") else "127.0.0.1"
+        ep = {"apiVersion": "v1", "kind": "Endpoints", "metadata": {"name": "kubernetes", "namespace": "default"},
+              "subsets": [{"addresses": [{"ip": ip}], "ports": [{"name": "https", "port": self.port, "protocol": "TCP"}]}]}
+        ers = self.registry.rs("endpoints")
+        cur = ers.storage.get(ers.key("default", "kubernetes"), ignore_not_found=True)
+        if cur is None:
+            ers.create("default", ep)
+        elif cur.get("subsets") != ep["subsets"]:
+            ep["metadata"]["resourceVersion"] = cur["metadata"]["resourceVersion"]
+            ers.update("default", "kubernetes", ep)
 
     @property
     def url(self):

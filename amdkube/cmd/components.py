@@ -48,6 +48,8 @@ def apiserver(argv):
     ap.add_argument("--max-requests-inflight", type=int, default=400)
     ap.add_argument("--max-mutating-requests-inflight", type=int, default=200)
     ap.add_argument("--event-ttl", type=float, default=3600.0)
+    ap.add_argument("--service-cluster-ip-range", default="10.0.0.0/24")
+    ap.add_argument("--service-node-port-range", default="30000-32767")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     klog.setup(a.v, "apiserver")
@@ -67,7 +69,8 @@ def apiserver(argv):
                         admission_config={"ResourceV2": {"resource_names": tuple(a.resource_v2_resources.split(","))}},
                         token_auth=tokens, authorization_mode=a.authorization_mode, anonymous_auth=a.anonymous_auth == "true",
                         max_in_flight=a.max_requests_inflight, max_mutating_in_flight=a.max_mutating_requests_inflight,
-                        event_ttl=a.event_ttl)
+                        event_ttl=a.event_ttl, service_cidr=a.service_cluster_ip_range,
+                        node_port_range=a.service_node_port_range)
         return await srv.start(a.bind_address, a.port)
     _run_forever(mk)
 
@@ -102,16 +105,22 @@ def controller_manager(argv):
     ap.add_argument("--leader-elect", default="false")
     ap.add_argument("--node-monitor-grace-period", type=float, default=40.0)
     ap.add_argument("--pod-eviction-timeout", type=float, default=300.0)
+    ap.add_argument("--allocate-node-cidrs", default="false")
+    ap.add_argument("--cluster-cidr", default="10.244.0.0/16")
+    ap.add_argument("--node-cidr-mask-size", type=int, default=24)
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     klog.setup(a.v, "controller-manager")
     from ..client import Client
-    from ..controllers import ALL, ControllerManager
-    names = list(ALL) if a.controllers in ("*", "") else a.controllers.split(",")
+    from ..controllers import ALL, OPT_IN, ControllerManager
+    alloc = a.allocate_node_cidrs == "true"
+    names = [n for n in ALL if n not in OPT_IN or (n == "nodeipam" and alloc)] if a.controllers in ("*", "") \
+        else a.controllers.split(",")
 
     async def mk():
         return await ControllerManager(Client(a.server), names, a.leader_elect == "true", socket.gethostname(),
-                                       a.node_monitor_grace_period, a.pod_eviction_timeout).start()
+                                       a.node_monitor_grace_period, a.pod_eviction_timeout, a.cluster_cidr,
+                                       a.node_cidr_mask_size, alloc).start()
     _run_forever(mk)
 
 
@@ -172,13 +181,24 @@ def rocshim(argv):
     ap.add_argument("--state-dir", default="/var/lib/amdkube/rocshim")
     ap.add_argument("--hooks-dir", default="/usr/share/containers/docker/hooks.d")
     ap.add_argument("--isolation", default="env", choices=("env", "namespaces"))
+    ap.add_argument("--network-plugin", default="host", choices=("host", "cni"))
+    ap.add_argument("--cni-conf-dir", default="/etc/cni/net.d")
+    ap.add_argument("--cni-bin-dir", default=None, help="default: /opt/cni/bin plus amdkube's bundled plugins")
+    ap.add_argument("--node-ip", default="127.0.0.1")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     klog.setup(a.v, "rocshim")
     from ..runtime import RocShim
+    from ..runtime.images import NATIVE_BIN
+    from ..runtime.network import CNINetwork, HostNetwork
+    if a.network_plugin == "cni":
+        bins = a.cni_bin_dir.split(",") if a.cni_bin_dir else ["/opt/cni/bin", os.path.join(NATIVE_BIN, "cni")]
+        net = CNINetwork(a.cni_conf_dir, bins, a.node_ip)
+    else:
+        net = HostNetwork(a.node_ip)
 
     async def mk():
-        return await RocShim(a.listen, a.state_dir, a.hooks_dir, a.isolation).start()
+        return await RocShim(a.listen, a.state_dir, a.hooks_dir, a.isolation, network=net).start()
     _run_forever(mk)
 
 
@@ -268,6 +288,28 @@ def hollow_node(argv):
     _run_forever(mk)
 
 
+def proxy(argv):
+    ap = argparse.ArgumentParser("amdkube proxy")
+    ap.add_argument("--master", "--server", dest="server", default="http://127.0.0.1:8080")
+    ap.add_argument("--proxy-mode", default="userspace", choices=("userspace", "iptables"))
+    ap.add_argument("--bind-address", default="0.0.0.0", help="node address NodePorts listen on")
+    ap.add_argument("--cluster-cidr", default="")
+    ap.add_argument("--iptables-sync-period", type=float, default=30.0)
+    ap.add_argument("--iptables-min-sync-period", type=float, default=0.0)
+    ap.add_argument("--healthz-port", type=int, default=10256)
+    ap.add_argument("--iptables-dump-file", default=None, help="write every rendered ruleset here (dry-run inspection)")
+    ap.add_argument("-v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "proxy")
+    from ..client import Client
+    from ..proxy import ProxyServer
+
+    async def mk():
+        return await ProxyServer(Client(a.server), a.proxy_mode, a.bind_address, a.cluster_cidr, a.iptables_sync_period,
+                                 a.iptables_min_sync_period, a.healthz_port, a.iptables_dump_file).start()
+    _run_forever(mk)
+
+
 def local_up(argv):
     """hack/local-up-cluster.sh equivalent: every component as its own process."""
     ap = argparse.ArgumentParser("amdkube local-up")
@@ -350,7 +392,7 @@ def local_up(argv):
                 p.kill()
 
 
-COMPONENTS = {"apiserver": apiserver, "kube-apiserver": apiserver, "scheduler": scheduler, "kube-scheduler": scheduler,
+COMPONENTS = {"proxy": proxy, "kube-proxy": proxy, "apiserver": apiserver, "kube-apiserver": apiserver, "scheduler": scheduler, "kube-scheduler": scheduler,
               "controller-manager": controller_manager, "kube-controller-manager": controller_manager, "kubelet": kubelet,
               "rocshim": rocshim, "amd-device-plugin": device_plugin, "device-plugin": device_plugin,
               "amdgpu-exporter": exporter, "exporter": exporter, "hollow-node": hollow_node, "local-up": local_up}

@@ -8,26 +8,33 @@ import asyncio
 
 from ..client import Client, LeaderElector, SharedInformerFactory
 from .lifecycle import GarbageCollector, NamespaceController, NodeLifecycleController, PodGCController
+from .networking import EndpointsController, NodeIPAMController
 from .workloads import DaemonSetController, DeploymentController, JobController, ReplicaSetController
 
 ALL = {"nodelifecycle": NodeLifecycleController, "replicaset": ReplicaSetController, "deployment": DeploymentController,
        "daemonset": DaemonSetController, "job": JobController, "namespace": NamespaceController,
-       "garbagecollector": GarbageCollector, "podgc": PodGCController}
+       "garbagecollector": GarbageCollector, "podgc": PodGCController, "endpoint": EndpointsController,
+       "nodeipam": NodeIPAMController}
+# controllers the reference starts only when asked (--allocate-node-cidrs for node IPAM)
+OPT_IN = {"nodeipam"}
 
 
 class ControllerManager:
     def __init__(self, client: Client, controllers=None, leader_elect: bool = False, identity: str = "controller-manager",
-                 node_monitor_grace: float = 40.0, pod_eviction_timeout: float = 300.0):
+                 node_monitor_grace: float = 40.0, pod_eviction_timeout: float = 300.0, cluster_cidr: str = "10.244.0.0/16",
+                 node_cidr_mask_size: int = 24, allocate_node_cidrs: bool = False):
         self.client = client
         self.factory = SharedInformerFactory(client)
         self.pods = self.factory.informer("pods")
         self.nodes = self.factory.informer("nodes")
-        names = controllers or list(ALL)
+        names = controllers or [n for n in ALL if n not in OPT_IN or (n == "nodeipam" and allocate_node_cidrs)]
         self.controllers = []
         for n in names:
             cls = ALL[n]
             if cls is NodeLifecycleController:
                 self.controllers.append(cls(self, grace=node_monitor_grace, eviction_timeout=pod_eviction_timeout))
+            elif cls is NodeIPAMController:
+                self.controllers.append(cls(self, cluster_cidr, node_cidr_mask_size))
             else:
                 self.controllers.append(cls(self))
         self.leader_elect = leader_elect

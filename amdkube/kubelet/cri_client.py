@@ -71,6 +71,10 @@ class CRIClient:
         req = C.ListPodSandboxRequest(filter=f) if f else C.ListPodSandboxRequest()
         return list((await self._call("list_podsandbox", self.rt.ListPodSandbox, req)).items)
 
+    async def update_runtime_config(self, pod_cidr: str):
+        req = C.UpdateRuntimeConfigRequest(runtime_config=C.RuntimeConfig(network_config=C.NetworkConfig(pod_cidr=pod_cidr)))
+        await self._call("update_runtime_config", self.rt.UpdateRuntimeConfig, req)
+
     async def pod_sandbox_status(self, sid):
         return (await self._call("podsandbox_status", self.rt.PodSandboxStatus, C.PodSandboxStatusRequest(pod_sandbox_id=sid))).status
 

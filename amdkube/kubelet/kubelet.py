@@ -265,6 +265,11 @@ class Kubelet:
             ann[TOPOLOGY_LABEL] = labels[TOPOLOGY_LABEL]
         try:
             self.node = await self.client.patch("nodes", self.node_name, patch, sub="status")
+            cidr = (self.node.get("spec") or {}).get("podCIDR") or ""
+            if cidr and cidr != getattr(self, "_pod_cidr", ""):
+                # kubelet_network.go updatePodCIDR → CRI UpdateRuntimeConfig
+                await self.cri.update_runtime_config(cidr)
+                self._pod_cidr = cidr
             if ann and any(m.annotations_of(self.node).get(k) != v for k, v in ann.items()):
                 self.node = await self.client.patch("nodes", self.node_name, {"metadata": {"annotations": ann}})
         except m.StatusError as e:

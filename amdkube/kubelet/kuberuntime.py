@@ -57,6 +57,7 @@ class PodRuntimeStatus:
     def __init__(self, uid):
         self.uid = uid
         self.sandboxes = []  # newest first: (id, state, attempt, created_at)
+        self.ip = ""        # the ready sandbox's pod IP (network plugin / CNI result)
         self.containers: dict[str, list[ContainerRuntimeStatus]] = {}  # name -> newest first
 
     def ready_sandbox(self):
@@ -80,6 +81,7 @@ class RuntimeManager:
         self.root = root_dir
         self.recorder = recorder
         self.backoff: dict[tuple[str, str], tuple[float, float]] = {}  # (uid, name) -> (until, last delay)
+        self.sandbox_ips: dict[str, str] = {}   # sandbox id -> IP (PodSandboxStatus is asked once per sandbox)
 
     # ----------------------------------------------------------------- status
     async def pod_status(self, uid: str, sandboxes=None) -> PodRuntimeStatus:
@@ -87,6 +89,17 @@ class RuntimeManager:
         sbs = sandboxes if sandboxes is not None else await self.cri.list_pod_sandbox(uid)
         sbs = sorted(sbs, key=lambda s: s.created_at, reverse=True)
         st.sandboxes = [(s.id, s.state, s.metadata.attempt, s.created_at) for s in sbs]
+        ready = st.ready_sandbox()
+        if ready is not None:
+            ip = self.sandbox_ips.get(ready[0])
+            if ip is None:
+                try:
+                    ip = (await self.cri.pod_sandbox_status(ready[0])).network.ip
+                except grpc.RpcError:
+                    ip = ""
+                if ip:
+                    self.sandbox_ips[ready[0]] = ip
+            st.ip = ip or ""
         for s in sbs:
             for c in await self.cri.list_containers(s.id):
                 try:
@@ -114,7 +127,7 @@ class RuntimeManager:
             labels={**(md.get("labels") or {}), L_POD_NAME: md["name"], L_POD_NS: md.get("namespace", ""), L_POD_UID: md["uid"]},
             annotations=ann,
             linux=C.LinuxPodSandboxConfig(security_context=C.LinuxSandboxSecurityContext(
-                namespace_options=C.NamespaceOption(host_network=True, host_pid=bool(spec.get("hostPID")),
+                namespace_options=C.NamespaceOption(host_network=bool(spec.get("hostNetwork")), host_pid=bool(spec.get("hostPID")),
                                                     host_ipc=bool(spec.get("hostIPC"))))))
 
     # -------------------------------------------------------------- containers
@@ -270,3 +283,4 @@ class RuntimeManager:
     async def remove_pod(self, uid: str):
         for s in await self.cri.list_pod_sandbox(uid):
             await self.cri.remove_pod_sandbox(s.id)
+            self.sandbox_ips.pop(s.id, None)

@@ -80,7 +80,9 @@ def generate_status(pod: dict, rt, node_ip: str, readiness: dict, errors: list[s
             continue
         if rs.state == C.CONTAINER_RUNNING:
             running += 1
-            ready = readiness.get(c["name"], True)
+            # a container with a readiness probe starts unready until its first success
+            # (reference prober/worker.go: readiness initialValue = results.Failure)
+            ready = readiness.get(c["name"], not c.get("readinessProbe"))
             all_ready &= ready
             statuses.append(container_status(c, rs, ready, False, ""))
         elif rs.state in (C.CONTAINER_EXITED, C.CONTAINER_UNKNOWN):
@@ -129,7 +131,8 @@ def generate_status(pod: dict, rt, node_ip: str, readiness: dict, errors: list[s
     ready = phase == "Running" and all_ready and bool(conts)
     cond("ContainersReady", ready, "ContainersNotReady")
     cond("Ready", ready, "ContainersNotReady")
-    st = {"phase": phase, "conditions": conds, "hostIP": node_ip, "podIP": node_ip,
+    pod_ip = node_ip if spec.get("hostNetwork") else (getattr(rt, "ip", "") or node_ip)
+    st = {"phase": phase, "conditions": conds, "hostIP": node_ip, "podIP": pod_ip,
           "startTime": old.get("startTime") or now, "containerStatuses": statuses,
           "initContainerStatuses": init_statuses or None, "qosClass": old.get("qosClass"),
           "message": "; ".join(errors) if errors else None, "reason": None}

@@ -29,7 +29,8 @@ class LocalCluster:
                  base_dir: str | None = None, with_controllers: bool = True, relist_period: float = 1.0,
                  node_status_update_frequency: float = 10.0, scheduler_kw: dict | None = None, isolation: str = "env",
                  health_probe: str = "none", kubelet_kw: dict | None = None, with_kubelet: bool = True,
-                 partition: str | None = None, resource_naming: str = "single"):
+                 partition: str | None = None, resource_naming: str = "single", api_kw: dict | None = None,
+                 controllers_kw: dict | None = None, shim_kw: dict | None = None):
         self.gpus, self.n_gpus, self.node_name = gpus, n_gpus, node_name
         self.partition, self.resource_naming = partition, resource_naming
         self.plugins: list = []
@@ -43,21 +44,22 @@ class LocalCluster:
         self.isolation = isolation
         self.health_probe = health_probe
         self.with_kubelet = with_kubelet
+        self.api_kw, self.controllers_kw, self.shim_kw = api_kw or {}, controllers_kw or {}, shim_kw or {}
         self.api = self.client = self.scheduler = self.controllers = self.shim = self.plugin = self.kubelet = None
         self.backend = None
 
     async def start(self):
         b = self.base
-        self.api = await APIServer().start()
+        self.api = await APIServer(**self.api_kw).start()
         self.client = Client(self.api.url, pool=256)
         self.scheduler = await Scheduler(Client(self.api.url, pool=256), **self.scheduler_kw).start()
         if self.with_controllers:
             from .controllers import ControllerManager
-            self.controllers = await ControllerManager(Client(self.api.url)).start()
+            self.controllers = await ControllerManager(Client(self.api.url), **self.controllers_kw).start()
         if not self.with_kubelet:
             return self
         self.shim = await RocShim(os.path.join(b, "rocshim.sock"), os.path.join(b, "rocshim"),
-                                  hooks_dir=os.path.join(b, "hooks.d"), isolation=self.isolation).start()
+                                  hooks_dir=os.path.join(b, "hooks.d"), isolation=self.isolation, **self.shim_kw).start()
         if self.gpus != "none":
             self.backend = open_backend(self.gpus, n=self.n_gpus, partition=self.partition)
             self.plugins = make_plugins(self.backend, self.resource_naming, plugins_dir=os.path.join(b, "plugins"),

@@ -34,6 +34,7 @@ import grpc
 from ..grpcdesc.cri import API_VERSION, CRI as C
 from .hooks import DEFAULT_HOOKS_DIR, HookService
 from .images import NATIVE_BIN, ImageStore
+from .network import HostNetwork, NetworkError
 
 log = logging.getLogger("amdkube.rocshim")
 
@@ -57,10 +58,13 @@ class Sandbox:
         self.created_at = now_ns()
         self.pid = 0
         self.proc = None
+        self.ip = ""
+        self.pod_network = False   # the network plugin set this sandbox up (CNI DEL on teardown)
 
     def to_json(self):
         return {"id": self.id, "meta": self.meta, "labels": self.labels, "annotations": self.annotations,
-                "log_dir": self.log_dir, "state": self.state, "created_at": self.created_at, "pid": self.pid}
+                "log_dir": self.log_dir, "state": self.state, "created_at": self.created_at, "pid": self.pid,
+                "ip": self.ip, "pod_network": self.pod_network}
 
 
 class Container:
@@ -91,7 +95,7 @@ class Container:
 
 class RocShim:
     def __init__(self, socket_path: str, state_dir: str, hooks_dir: str = DEFAULT_HOOKS_DIR, isolation: str = "env",
-                 cgroup_root: str = "/sys/fs/cgroup/amdkube", dev_root: str = "/dev"):
+                 cgroup_root: str = "/sys/fs/cgroup/amdkube", dev_root: str = "/dev", network=None):
         self.socket = socket_path
         self.state_dir = state_dir
         os.makedirs(os.path.join(state_dir, "sandboxes"), exist_ok=True)
@@ -100,6 +104,7 @@ class RocShim:
         self.images = ImageStore(state_dir)
         self.hooks = HookService(hooks_dir, HANDLERS)
         self.isolation = isolation
+        self.network = network or HostNetwork()
         self.cgroup_root = cgroup_root
         self.dev_root = dev_root
         self.sandboxes: dict[str, Sandbox] = {}
@@ -166,6 +171,7 @@ class RocShim:
                 continue
             s = Sandbox(d["id"], b"", d["meta"], d["labels"], d["annotations"], d["log_dir"])
             s.state, s.created_at, s.pid = d["state"], d["created_at"], d["pid"]
+            s.ip, s.pod_network = d.get("ip", ""), d.get("pod_network", False)
             if s.state == C.SANDBOX_READY and not _alive(s.pid):
                 s.state = C.SANDBOX_NOTREADY
             self.sandboxes[s.id] = s
@@ -216,6 +222,22 @@ class RocShim:
                                                     stdout=asyncio.subprocess.DEVNULL, stderr=asyncio.subprocess.DEVNULL,
                                                     start_new_session=True)
         s.proc, s.pid = proc, proc.pid
+        host_net = True
+        try:
+            host_net = cfg.linux.security_context.namespace_options.host_network
+        except AttributeError:
+            pass
+        if host_net or isinstance(self.network, HostNetwork):
+            s.ip = self.network.node_ip
+        else:
+            try:
+                s.ip = await self.network.setup(sid, meta, f"/proc/{s.pid}/ns/net")
+                s.pod_network = True
+            except Exception:
+                _kill(s.pid, signal.SIGKILL)
+                await proc.wait()
+                await self.network.teardown(sid, meta, f"/proc/{s.pid}/ns/net")  # release a partial ADD
+                raise
         self.sandboxes[sid] = s
         self._ckpt("sandboxes", s)
         return sid
@@ -232,6 +254,9 @@ class RocShim:
                     await asyncio.wait_for(s.proc.wait(), 2)
                 except asyncio.TimeoutError:
                     _kill(s.pid, signal.SIGKILL)
+        if s.pod_network:
+            await self.network.teardown(sid, s.meta, f"/proc/{s.pid}/ns/net")
+            s.pod_network = False
         s.state = C.SANDBOX_NOTREADY
         self._ckpt("sandboxes", s)
 
@@ -480,7 +505,10 @@ class _Runtime:
                                  runtime_api_version="v1alpha1")
 
     async def Status(self, req, ctx):
-        conds = [C.RuntimeCondition(type="RuntimeReady", status=True), C.RuntimeCondition(type="NetworkReady", status=True)]
+        net_ok, net_msg = self.r.network.status()
+        conds = [C.RuntimeCondition(type="RuntimeReady", status=True),
+                 C.RuntimeCondition(type="NetworkReady", status=net_ok, reason="" if net_ok else "NetworkPluginNotReady",
+                                    message=net_msg)]
         return C.StatusResponse(status=C.RuntimeStatus(conditions=conds),
                                 info={"isolation": self.r.isolation, "handlers": ",".join(sorted(HANDLERS))} if req.verbose else {})
 
@@ -509,7 +537,8 @@ class _Runtime:
         if s.state == C.SANDBOX_READY and not _alive(s.pid):
             s.state = C.SANDBOX_NOTREADY
         st = C.PodSandboxStatus(id=s.id, metadata=self._sb_meta(s), state=s.state, created_at=s.created_at,
-                                network=C.PodSandboxNetworkStatus(ip="127.0.0.1"), labels=s.labels, annotations=s.annotations)
+                                network=C.PodSandboxNetworkStatus(ip=s.ip or self.r.network.node_ip), labels=s.labels,
+                                annotations=s.annotations)
         return C.PodSandboxStatusResponse(status=st, info={"pid": str(s.pid)} if req.verbose else {})
 
     async def ListPodSandbox(self, req, ctx):
@@ -619,6 +648,9 @@ class _Runtime:
         return C.ListContainerStatsResponse(stats=out)
 
     async def UpdateRuntimeConfig(self, req, ctx):
+        cidr = req.runtime_config.network_config.pod_cidr
+        if cidr:
+            self.r.network.set_pod_cidr(cidr)
         return C.UpdateRuntimeConfigResponse()
 
     async def GetContainerEvents(self, req, ctx):

@@ -51,6 +51,8 @@ def targets(sanitize=False, cpu_only=False):
          ["g++", "-O2", "-std=c++17", n("native/pause.cpp"), "-o", "{out}"]),
         (n(BIN, "amdkube-nsexec"), [n("native/nsexec.cpp")],
          ["g++", "-O2", "-std=c++17", n("native/nsexec.cpp"), "-o", "{out}"]),
+        (n(BIN, "cni", "amdkube-cni"), [n("native/cni_ipam.cpp")],
+         ["g++", "-O2", "-std=c++17", n("native/cni_ipam.cpp"), "-o", "{out}"]),
     ]
     if sanitize:
         san = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-g"]
@@ -86,7 +88,7 @@ def stale(out, deps):
 
 
 def build(sanitize=False, cpu_only=False, force=False, jobs=4, verbose=False):
-    os.makedirs(BIN, exist_ok=True)
+    os.makedirs(os.path.join(BIN, "cni"), exist_ok=True)
     init = os.path.join(OUT, "__init__.py")
     if not os.path.exists(init):
         open(init, "w").write('"""Built native artefacts (see native/build.py)."""\n')

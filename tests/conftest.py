@@ -25,3 +25,13 @@ def run(coro, timeout=60):
 @pytest.fixture
 def arun():
     return run
+
+
+@pytest.hookimpl(tryfirst=True)
+def pytest_pyfunc_call(pyfuncitem):
+    """`async def test_*` runs on a fresh event loop with a 120 s cap."""
+    if asyncio.iscoroutinefunction(pyfuncitem.obj):
+        args = {k: pyfuncitem.funcargs[k] for k in pyfuncitem._fixtureinfo.argnames}
+        run(pyfuncitem.obj(**args), timeout=120)
+        return True
+    return None
