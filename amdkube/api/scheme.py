@@ -105,18 +105,37 @@ _CORE = [
     ("ResourceQuota", "resourcequotas", True, ("quota",), ("status",)),
     ("PersistentVolume", "persistentvolumes", False, ("pv",), ("status",)),
     ("PersistentVolumeClaim", "persistentvolumeclaims", True, ("pvc",), ("status",)),
+    ("ReplicationController", "replicationcontrollers", True, ("rc",), ("status", "scale")),
+    ("PodTemplate", "podtemplates", True, (), ()),
 ]
 _APPS = [
     ("DaemonSet", "daemonsets", True, ("ds",), ("status",)),
     ("ReplicaSet", "replicasets", True, ("rs",), ("status", "scale")),
     ("Deployment", "deployments", True, ("deploy",), ("status", "scale")),
+    ("StatefulSet", "statefulsets", True, ("sts",), ("status", "scale")),
+    ("ControllerRevision", "controllerrevisions", True, (), ()),
 ]
 _BATCH = [("Job", "jobs", True, (), ("status",))]
+_BATCH_BETA = [("CronJob", "cronjobs", True, ("cj",), ("status",))]
 _COORD = [("Lease", "leases", True, (), ())]
 _SCHED = [("PriorityClass", "priorityclasses", False, ("pc",), ())]
+_AUTOSCALING = [("HorizontalPodAutoscaler", "horizontalpodautoscalers", True, ("hpa",), ("status",))]
+_POLICY = [("PodDisruptionBudget", "poddisruptionbudgets", True, ("pdb",), ("status",))]
+_CERTS = [("CertificateSigningRequest", "certificatesigningrequests", False, ("csr",), ("status", "approval"))]
+_RBAC = [("Role", "roles", True, (), ()), ("ClusterRole", "clusterroles", False, (), ()),
+         ("RoleBinding", "rolebindings", True, (), ()), ("ClusterRoleBinding", "clusterrolebindings", False, (), ())]
+_STORAGE = [("StorageClass", "storageclasses", False, ("sc",), ())]
+_STORAGE_BETA = [("VolumeAttachment", "volumeattachments", False, (), ("status",))]
+_AUTHZ = [("SubjectAccessReview", "subjectaccessreviews", False, (), ())]
+_AUTHN = [("TokenReview", "tokenreviews", False, (), ())]
 
 for group, version, table in (("", "v1", _CORE), ("apps", "v1", _APPS), ("batch", "v1", _BATCH),
-                              ("coordination.k8s.io", "v1", _COORD), ("scheduling.k8s.io", "v1", _SCHED)):
+                              ("batch", "v1beta1", _BATCH_BETA), ("coordination.k8s.io", "v1", _COORD),
+                              ("scheduling.k8s.io", "v1", _SCHED), ("autoscaling", "v1", _AUTOSCALING),
+                              ("policy", "v1beta1", _POLICY), ("certificates.k8s.io", "v1beta1", _CERTS),
+                              ("rbac.authorization.k8s.io", "v1", _RBAC), ("storage.k8s.io", "v1", _STORAGE),
+                              ("storage.k8s.io", "v1beta1", _STORAGE_BETA),
+                              ("authorization.k8s.io", "v1", _AUTHZ), ("authentication.k8s.io", "v1", _AUTHN)):
     for kind, plural, ns, short, subs in table:
         SCHEME.add(ResourceInfo(group, version, kind, plural, ns, short, subs))
 

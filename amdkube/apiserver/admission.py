@@ -298,6 +298,42 @@ class PodNodeSelector(Plugin):
             pod_sel[k] = v
 
 
+class DefaultStorageClass(Plugin):
+    """plugin/pkg/admission/storageclass/setdefault: a claim without a class gets the class
+    annotated storageclass.kubernetes.io/is-default-class=true (more than one default: 403)."""
+    name = "DefaultStorageClass"
+    operations = (CREATE,)
+
+    def admit(self, a, ctx):
+        if a.resource != "persistentvolumeclaims" or a.subresource:
+            return
+        spec = a.obj.setdefault("spec", {})
+        if "storageClassName" in spec or "volume.beta.kubernetes.io/storage-class" in (a.obj.get("metadata") or {}).get(
+                "annotations", {}):
+            return
+        defaults = [sc for sc in ctx.list_objects("storageclasses", "", "storage.k8s.io")
+                    if ((sc.get("metadata") or {}).get("annotations") or {}).get("storageclass.kubernetes.io/is-default-class") == "true"]
+        if len(defaults) > 1:
+            raise m.forbidden(f"{len(defaults)} default StorageClasses were found")
+        if defaults:
+            spec["storageClassName"] = m.name_of(defaults[0])
+
+
+class StorageObjectInUseProtection(Plugin):
+    """plugin/pkg/admission/storageobjectinuseprotection: new claims and volumes carry the
+    kubernetes.io/pvc-protection / pv-protection finalizers."""
+    name = "StorageObjectInUseProtection"
+    operations = (CREATE,)
+
+    def admit(self, a, ctx):
+        fin = {"persistentvolumeclaims": "kubernetes.io/pvc-protection", "persistentvolumes": "kubernetes.io/pv-protection"}.get(
+            a.resource)
+        if fin and not a.subresource:
+            md = a.obj.setdefault("metadata", {})
+            if fin not in (md.get("finalizers") or []):
+                md["finalizers"] = list(md.get("finalizers") or []) + [fin]
+
+
 class AlwaysAdmit(Plugin):
     name = "AlwaysAdmit"
 
@@ -312,11 +348,13 @@ class AlwaysDeny(Plugin):
 
 REGISTRY = {p.name: p for p in (ResourceV2, ExtendedResourceToleration, NamespaceLifecycle, NamespaceAutoProvision,
                                  NamespaceExists, ServiceAccount, DefaultTolerationSeconds, LimitRanger, ResourceQuota,
-                                 Priority, PodNodeSelector, AlwaysAdmit, AlwaysDeny)}
+                                 Priority, PodNodeSelector, DefaultStorageClass, StorageObjectInUseProtection,
+                                 AlwaysAdmit, AlwaysDeny)}
 
 # Matches the fork's recommended ordering (hack/local-up-cluster.sh:424 adds ResourceV2).
 DEFAULT_CHAIN = ("NamespaceLifecycle", "LimitRanger", "ServiceAccount", "DefaultTolerationSeconds", "Priority",
-                 "ResourceV2", "ExtendedResourceToleration", "ResourceQuota")
+                 "ResourceV2", "ExtendedResourceToleration", "DefaultStorageClass", "StorageObjectInUseProtection",
+                 "ResourceQuota")
 
 
 class Chain:

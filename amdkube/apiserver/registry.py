@@ -165,8 +165,11 @@ def default_fields(o):
 FIELDS = {"pods": pod_fields, "nodes": node_fields, "events": event_fields, "namespaces": ns_fields}
 
 _STATUS_KINDS = {"pods", "nodes", "namespaces", "services", "daemonsets", "replicasets", "deployments", "jobs",
-                 "resourcequotas", "persistentvolumes", "persistentvolumeclaims"}
-_GENERATION_KINDS = {"daemonsets", "replicasets", "deployments", "jobs"}
+                 "resourcequotas", "persistentvolumes", "persistentvolumeclaims", "statefulsets", "replicationcontrollers",
+                 "cronjobs", "horizontalpodautoscalers", "poddisruptionbudgets", "certificatesigningrequests",
+                 "volumeattachments"}
+_GENERATION_KINDS = {"daemonsets", "replicasets", "deployments", "jobs", "statefulsets", "replicationcontrollers",
+                     "poddisruptionbudgets", "horizontalpodautoscalers"}
 
 
 def pod_qos(pod) -> str:
@@ -493,6 +496,41 @@ class Registry:
         for kv in kvs:
             self._index_pod(kv.key, json.loads(kv.value))
         self.services.rebuild(self.store.range("/registry/services/")[0])  # ipallocator/portallocator repair
+
+    # ------------------------------------------------------------ eviction
+    def evict(self, ns: str, name: str, body: dict, user=None):
+        """POST pods/<name>/eviction (pkg/registry/core/pod/storage/eviction.go): a pod covered by
+        a PodDisruptionBudget is deleted only while the budget allows a disruption; the budget's
+        disruptionsAllowed is decremented and the pod recorded in status.disruptedPods in the same
+        CAS update, so concurrent evictions cannot overdraw it (429 otherwise)."""
+        from ..api.labels import selector_from_label_selector
+        pods = self.rs("pods")
+        pod = pods.get(ns, name)
+        grace = (body.get("deleteOptions") or {}).get("gracePeriodSeconds")
+        if not is_pod_terminal(pod) and (pod.get("status") or {}).get("phase") != "Pending":
+            labels = (pod.get("metadata") or {}).get("labels") or {}
+            pdbs = [p for p in self.rs("poddisruptionbudgets", "policy").list(ns)[0]
+                    if (p.get("spec") or {}).get("selector") and
+                    selector_from_label_selector(p["spec"]["selector"]).matches(labels)]
+            if len(pdbs) > 1:
+                raise m.StatusError(500, "InternalError", "This pod has more than one PodDisruptionBudget, which the eviction "
+                                                          "subresource does not support.")
+            if pdbs:
+                pdb = pdbs[0]
+                prs = self.rs("poddisruptionbudgets", "policy")
+
+                def take(cur):
+                    st = cur.setdefault("status", {})
+                    if st.get("observedGeneration", 0) < (cur.get("metadata") or {}).get("generation", 1):
+                        raise m.too_many_requests("Cannot evict pod as it would violate the pod's disruption budget: "
+                                                  "the budget's status is out of date")
+                    if int(st.get("disruptionsAllowed", st.get("podDisruptionsAllowed", 0)) or 0) <= 0:
+                        raise m.too_many_requests("Cannot evict pod as it would violate the pod's disruption budget.")
+                    st["disruptionsAllowed"] = int(st.get("disruptionsAllowed", 0)) - 1
+                    st.setdefault("disruptedPods", {})[name] = m.now_rfc3339()
+                    return cur
+                prs.storage.guaranteed_update(prs.key(ns, m.name_of(pdb)), take)
+        return pods.delete(ns, name, grace=grace, user=user)
 
     # ------------------------------------------------------------- binding
     def bind(self, ns: str, binding: dict, user=None) -> dict:

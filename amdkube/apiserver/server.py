@@ -30,6 +30,7 @@ from ..utils.metrics import CONTENT_TYPE, MICRO_BUCKETS, Counter, Histogram, new
 from . import admission as adm
 from .registry import Registry
 from .service import ServiceAllocator, parse_port_range
+from .auth import Attributes, Authenticator, UnionAuthorizer, ensure_bootstrap_policy
 
 log = logging.getLogger("amdkube.apiserver")
 
@@ -49,13 +50,22 @@ class APIServer:
     def __init__(self, store: MVCCStore | None = None, admission_plugins=adm.DEFAULT_CHAIN, admission_config=None,
                  token_auth: dict | None = None, authorization_mode: str = "AlwaysAllow",
                  max_in_flight: int = 400, max_mutating_in_flight: int = 200, event_ttl: float = 3600.0,
-                 anonymous_auth: bool = True, service_cidr: str = "10.0.0.0/24", node_port_range: str = "30000-32767"):
+                 anonymous_auth: bool = True, service_cidr: str = "10.0.0.0/24", node_port_range: str = "30000-32767",
+                 service_account_key: bytes | None = None):
         self.store = store or MVCCStore()
         self.admission = adm.Chain(admission_plugins, admission_config)
         self.registry = Registry(self.store, self.admission, ServiceAllocator(service_cidr, parse_port_range(node_port_range)))
-        self.tokens = token_auth or {}
+        self.tokens = dict(token_auth or {})
+        # genericapiserver loopback client: the apiserver's own (and in-process components')
+        # credential, a random bearer token for system:apiserver in system:masters
+        self.loopback_token = m.new_uid()
+        self.tokens[self.loopback_token] = {"name": "system:apiserver", "uid": "", "groups": ["system:masters"]}
         self.anonymous = anonymous_auth
         self.authz_mode = authorization_mode
+        self.sa_key = service_account_key
+        self.authn = Authenticator(self.registry, self.tokens, service_account_key, anonymous_auth)
+        self.authn.user_tokens = len(token_auth or {})
+        self.authz = UnionAuthorizer(authorization_mode, self.registry)
         self._ro = asyncio.Semaphore(max_in_flight) if max_in_flight else None
         self._rw = asyncio.Semaphore(max_mutating_in_flight) if max_mutating_in_flight else None
         self.event_ttl = event_ttl
@@ -86,6 +96,8 @@ class APIServer:
         for ns in ("default", "kube-system", "kube-public"):
             if self.registry.get_namespace(ns) is None:
                 self.registry.create_namespace(ns)
+        if "RBAC" in self.authz.modes:
+            ensure_bootstrap_policy(self.registry)
 
     # ---------------------------------------------------------------- lifecycle
     async def start(self, host="127.0.0.1", port=0):
@@ -192,22 +204,35 @@ class APIServer:
 
     # ------------------------------------------------------------------ auth
     def _authenticate(self, request):
-        h = request.headers.get("Authorization", "")
-        if h.startswith("Bearer "):
-            user = self.tokens.get(h[7:].strip())
-            if user is None:
-                raise m.unauthorized()
-            return user
-        if self.tokens and not self.anonymous:
-            raise m.unauthorized()
-        return {"name": "system:anonymous", "groups": ["system:unauthenticated"]}
+        return self.authn.authenticate(request.headers)
 
-    def _authorize(self, user, verb, resource):
-        if self.authz_mode == "AlwaysDeny":
-            raise m.forbidden(f'User "{user["name"]}" cannot {verb} {resource}')
-        if self.authz_mode == "RBACLite" and "system:masters" not in (user.get("groups") or []) \
-                and user["name"].startswith("system:anonymous") and verb not in ("get", "list", "watch"):
-            raise m.forbidden(f'User "{user["name"]}" cannot {verb} {resource}')
+    def _authorize(self, user, verb, resource, group="", ns="", name="", sub=""):
+        ok, _ = self.authz.authorize(Attributes(user, verb, group, resource, sub, ns, name))
+        if not ok:
+            what = f"{resource}/{sub}" if sub else resource
+            where = f' in the namespace "{ns}"' if ns else " at the cluster scope"
+            raise m.forbidden(f'User "{user.get("name")}" cannot {verb} {what}{" " + repr(name) if name else ""}'
+                              f'{" in API group " + repr(group) if group else ""}{where}')
+
+    def _review(self, plural, body):
+        """SubjectAccessReview / TokenReview (authorization.k8s.io, authentication.k8s.io): computed, not stored."""
+        spec = body.get("spec") or {}
+        if plural == "tokenreviews":
+            u = self.authn.authenticate_token(spec.get("token", "")) if spec.get("token") else None
+            st = {"authenticated": u is not None}
+            if u is not None:
+                st["user"] = {"username": u.get("name"), "uid": u.get("uid", ""), "groups": u.get("groups") or []}
+        else:
+            user = {"name": spec.get("user", ""), "groups": spec.get("groups") or []}
+            ra, nra = spec.get("resourceAttributes"), spec.get("nonResourceAttributes")
+            if ra:
+                a = Attributes(user, ra.get("verb", ""), ra.get("group", ""), ra.get("resource", ""), ra.get("subresource", ""),
+                               ra.get("namespace", ""), ra.get("name", ""))
+            else:
+                a = Attributes(user, (nra or {}).get("verb", ""), path=(nra or {}).get("path", ""), resource_request=False)
+            ok, why = self.authz.authorize(a)
+            st = {"allowed": ok, "reason": why}
+        return dict(body, status=st)
 
     # -------------------------------------------------------------- dispatch
     def _parse(self, path: str):
@@ -263,7 +288,8 @@ class APIServer:
             kverb = {"GET": "watch" if is_watch else ("get" if name else "list"), "POST": "create", "PUT": "update",
                      "PATCH": "patch", "DELETE": "delete" if name else "deletecollection"}.get(verb, verb.lower())
             verb = kverb.upper()
-            self._authorize(user, kverb, resource)
+            self._authorize(user, kverb, resource, group, "" if not rs.ri.namespaced else ns, name or "",
+                            "" if sub in ("",) else sub.split("/")[0])
             if is_watch:
                 code = 200
                 return await self._watch(request, rs, ns, name, q)
@@ -324,8 +350,10 @@ class APIServer:
                 body.setdefault("metadata", {}).setdefault("name", name)
                 return _resp(self.registry.bind(ns, body, user), 201)
             if name and sub == "eviction" and ri.plural == "pods":
-                obj, _ = rs.delete(ns, name, grace=((body.get("deleteOptions") or {}).get("gracePeriodSeconds")), user=user)
+                self.registry.evict(ns, name, body, user)
                 return _resp(m.success_status(), 201)
+            if ri.plural in ("subjectaccessreviews", "tokenreviews"):
+                return _resp(self._review(ri.plural, body), 201)
             if ri.plural == "pods" and sub == "" and name is None and body.get("kind") == "Binding":
                 return _resp(self.registry.bind(ns, body, user), 201)
             if name:
@@ -337,7 +365,7 @@ class APIServer:
             if not name:
                 raise m.method_not_allowed("PUT on a collection")
             body = await self._body(request)
-            subr = sub if sub in ("status",) else ""
+            subr = "status" if sub in ("status", "approval") else ""
             if sub == "finalize" and ri.plural == "namespaces":
                 subr = "finalize"
             obj, created = rs.update(ns, name, body, subresource=subr, user=user)

@@ -1,0 +1,233 @@
+"""Cloud-provider interface and the providers amdkube ships.
+
+Reference: pkg/cloudprovider/cloud.go (Interface: Instances, LoadBalancer, Routes, Zones,
+ProviderName, HasClusterID), plugins.go (RegisterCloudProvider / GetCloudProvider by
+--cloud-provider name) and providers/fake (the recording fake used by controller tests).
+
+The reference ships AWS / GCE / Azure / vSphere / OpenStack / … drivers. An
+MI355X node runs on-prem or on a GPU cloud with no Kubernetes cloud integration, so the
+providers here are:
+  * `baremetal`: load balancers get addresses from a configured pool (the MetalLB model),
+    routes are kept in a table and programmed with `ip route` when privileged, and instance
+    data comes from the Node objects;
+  * `fake`: the reference's recording fake, for tests.
+"""
+from __future__ import annotations
+
+import ipaddress
+import logging
+import os
+import shutil
+import subprocess
+from dataclasses import dataclass
+
+from ..api import meta as m
+
+log = logging.getLogger("amdkube.cloudprovider")
+
+
+@dataclass(frozen=True)
+class Route:
+    name: str
+    target_node: str
+    destination_cidr: str
+
+
+@dataclass(frozen=True)
+class Zone:
+    failure_domain: str = ""
+    region: str = ""
+
+
+class Interface:
+    """cloud.go Interface. Sub-interfaces return None when unsupported, like the reference's (x, false)."""
+    name = "none"
+
+    def initialize(self, client=None):
+        pass
+
+    def load_balancer(self):
+        return None
+
+    def instances(self):
+        return None
+
+    def zones(self):
+        return None
+
+    def routes(self):
+        return None
+
+    def has_cluster_id(self) -> bool:
+        return True
+
+
+class BareMetalLoadBalancer:
+    def __init__(self, pool: str):
+        self.pool = [str(ip) for ip in ipaddress.ip_network(pool, strict=False).hosts()] if pool else []
+        self.assigned: dict[str, str] = {}   # service key -> ip
+
+    def get(self, cluster: str, svc: dict):
+        ip = self.assigned.get(m.key_of(svc))
+        return ({"ingress": [{"ip": ip}]}, True) if ip else (None, False)
+
+    def ensure(self, cluster: str, svc: dict, nodes: list[dict]) -> dict:
+        key = m.key_of(svc)
+        want = (svc.get("spec") or {}).get("loadBalancerIP")
+        ip = self.assigned.get(key)
+        if want and ip != want:
+            if want in self.assigned.values() or (self.pool and want not in self.pool):
+                raise ValueError(f"requested loadBalancerIP {want} is unavailable")
+            ip = want
+        if ip is None:
+            used = set(self.assigned.values())
+            ip = next((a for a in self.pool if a not in used), None)
+            if ip is None:
+                raise RuntimeError("load-balancer address pool exhausted")
+        self.assigned[key] = ip
+        return {"ingress": [{"ip": ip}]}
+
+    def update(self, cluster: str, svc: dict, nodes: list[dict]):
+        pass   # addresses are announced by every node's proxy; nothing per-node to program
+
+    def ensure_deleted(self, cluster: str, svc: dict):
+        self.assigned.pop(m.key_of(svc), None)
+
+
+class BareMetalRoutes:
+    def __init__(self, program: bool | None = None):
+        self.table: dict[str, Route] = {}
+        can = shutil.which("ip") is not None and os.geteuid() == 0
+        self.program = can if program is None else program
+        self.node_ips: dict[str, str] = {}
+
+    def list(self, cluster: str) -> list[Route]:
+        return list(self.table.values())
+
+    def create(self, cluster: str, name_hint: str, route: Route):
+        if self.program and route.target_node in self.node_ips:
+            r = subprocess.run(["ip", "route", "replace", route.destination_cidr, "via", self.node_ips[route.target_node]],
+                               capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(r.stderr.strip())
+        self.table[route.name] = route
+
+    def delete(self, cluster: str, route: Route):
+        if self.program:
+            subprocess.run(["ip", "route", "del", route.destination_cidr], capture_output=True)
+        self.table.pop(route.name, None)
+
+
+class BareMetalInstances:
+    def __init__(self, client=None):
+        self.client = client
+
+    async def node_addresses(self, node_name: str) -> list[dict]:
+        n = await self.client.get_or_none("nodes", node_name) if self.client else None
+        return list(((n or {}).get("status") or {}).get("addresses") or [])
+
+    async def instance_exists(self, node_name: str) -> bool:
+        return (await self.client.get_or_none("nodes", node_name) if self.client else None) is not None
+
+    async def instance_type(self, node_name: str) -> str:
+        n = await self.client.get_or_none("nodes", node_name) if self.client else None
+        return m.labels_of(n or {}).get("beta.kubernetes.io/instance-type", "amd-mi355x-8gpu")
+
+
+class BareMetal(Interface):
+    name = "baremetal"
+
+    def __init__(self, config: dict | None = None):
+        config = config or {}
+        self._lb = BareMetalLoadBalancer(config.get("loadBalancerIPRange", ""))
+        self._routes = BareMetalRoutes(config.get("programRoutes"))
+        self._zone = Zone(config.get("zone", ""), config.get("region", ""))
+        self._instances = BareMetalInstances()
+
+    def initialize(self, client=None):
+        self._instances.client = client
+
+    def load_balancer(self):
+        return self._lb if self._lb.pool else None
+
+    def routes(self):
+        return self._routes
+
+    def zones(self):
+        return self._zone
+
+    def instances(self):
+        return self._instances
+
+
+class Fake(Interface):
+    """providers/fake/fake.go: records every call; load balancers get 1.2.3.<n>."""
+    name = "fake"
+
+    def __init__(self, config: dict | None = None):
+        self.calls: list[str] = []
+        self.balancers: dict[str, dict] = {}
+        self.route_table: dict[str, Route] = {}
+        self.err: Exception | None = None
+        outer = self
+
+        class LB:
+            def get(self, cluster, svc):
+                outer.calls.append("get")
+                st = outer.balancers.get(m.key_of(svc))
+                return (st, st is not None)
+
+            def ensure(self, cluster, svc, nodes):
+                outer.calls.append("create")
+                if outer.err:
+                    raise outer.err
+                st = outer.balancers.get(m.key_of(svc)) or {"ingress": [{"ip": f"1.2.3.{len(outer.balancers) + 1}"}]}
+                outer.balancers[m.key_of(svc)] = st
+                return st
+
+            def update(self, cluster, svc, nodes):
+                outer.calls.append("update")
+
+            def ensure_deleted(self, cluster, svc):
+                outer.calls.append("delete")
+                outer.balancers.pop(m.key_of(svc), None)
+
+        class Routes:
+            def list(self, cluster):
+                outer.calls.append("list-routes")
+                return list(outer.route_table.values())
+
+            def create(self, cluster, hint, route):
+                outer.calls.append("create-route")
+                outer.route_table[route.name] = route
+
+            def delete(self, cluster, route):
+                outer.calls.append("delete-route")
+                outer.route_table.pop(route.name, None)
+        self._lb, self._routes = LB(), Routes()
+
+    def load_balancer(self):
+        return self._lb
+
+    def routes(self):
+        return self._routes
+
+    def zones(self):
+        return Zone("fake-zone", "fake-region")
+
+
+_PROVIDERS = {"baremetal": BareMetal, "fake": Fake}
+
+
+def register_cloud_provider(name: str, factory):
+    if name in _PROVIDERS:
+        raise ValueError(f"cloud provider {name!r} was registered twice")
+    _PROVIDERS[name] = factory
+
+
+def get_cloud_provider(name: str, config: dict | None = None) -> Interface | None:
+    if not name:
+        return None
+    if name not in _PROVIDERS:
+        raise ValueError(f"unknown cloud provider {name!r} (have: {', '.join(sorted(_PROVIDERS))})")
+    return _PROVIDERS[name](config)

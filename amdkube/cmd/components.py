@@ -50,6 +50,7 @@ def apiserver(argv):
     ap.add_argument("--event-ttl", type=float, default=3600.0)
     ap.add_argument("--service-cluster-ip-range", default="10.0.0.0/24")
     ap.add_argument("--service-node-port-range", default="30000-32767")
+    ap.add_argument("--service-account-key-file", default=None, help="HMAC key for service-account tokens")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     klog.setup(a.v, "apiserver")
@@ -70,7 +71,8 @@ def apiserver(argv):
                         token_auth=tokens, authorization_mode=a.authorization_mode, anonymous_auth=a.anonymous_auth == "true",
                         max_in_flight=a.max_requests_inflight, max_mutating_in_flight=a.max_mutating_requests_inflight,
                         event_ttl=a.event_ttl, service_cidr=a.service_cluster_ip_range,
-                        node_port_range=a.service_node_port_range)
+                        node_port_range=a.service_node_port_range,
+                        service_account_key=open(a.service_account_key_file, "rb").read().strip() if a.service_account_key_file else None)
         return await srv.start(a.bind_address, a.port)
     _run_forever(mk)
 
@@ -101,26 +103,48 @@ def scheduler(argv):
 def controller_manager(argv):
     ap = argparse.ArgumentParser("amdkube controller-manager")
     ap.add_argument("--master", "--server", dest="server", default="http://127.0.0.1:8080")
-    ap.add_argument("--controllers", default="*")
+    ap.add_argument("--controllers", default="*", help="'*' = defaults; 'name' enables, '-name' disables")
     ap.add_argument("--leader-elect", default="false")
     ap.add_argument("--node-monitor-grace-period", type=float, default=40.0)
     ap.add_argument("--pod-eviction-timeout", type=float, default=300.0)
     ap.add_argument("--allocate-node-cidrs", default="false")
     ap.add_argument("--cluster-cidr", default="10.244.0.0/16")
     ap.add_argument("--node-cidr-mask-size", type=int, default=24)
+    ap.add_argument("--cloud-provider", default="")
+    ap.add_argument("--cloud-config", default=None, help="JSON/YAML provider config (baremetal: loadBalancerIPRange, zone)")
+    ap.add_argument("--configure-cloud-routes", default="true")
+    ap.add_argument("--cluster-name", default="kubernetes")
+    ap.add_argument("--service-account-private-key-file", default=None)
+    ap.add_argument("--root-ca-file", default=None)
+    ap.add_argument("--cluster-signing-cert-file", default=None)
+    ap.add_argument("--cluster-signing-key-file", default=None)
+    ap.add_argument("--horizontal-pod-autoscaler-sync-period", type=float, default=30.0)
+    ap.add_argument("--horizontal-pod-autoscaler-upscale-delay", type=float, default=180.0)
+    ap.add_argument("--horizontal-pod-autoscaler-downscale-delay", type=float, default=300.0)
+    ap.add_argument("--hostpath-pv-root", default="/var/lib/amdkube/hostpath-pv")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     klog.setup(a.v, "controller-manager")
+    import yaml
     from ..client import Client
-    from ..controllers import ALL, OPT_IN, ControllerManager
-    alloc = a.allocate_node_cidrs == "true"
-    names = [n for n in ALL if n not in OPT_IN or (n == "nodeipam" and alloc)] if a.controllers in ("*", "") \
-        else a.controllers.split(",")
+    from ..cloudprovider import get_cloud_provider
+    from ..controllers import ControllerManager, Options, resolve_controllers
+    cfg = yaml.safe_load(open(a.cloud_config)) if a.cloud_config else None
+    rd = lambda p: open(p, "rb").read().strip() if p else None  # noqa: E731
+    opts = Options(node_monitor_grace=a.node_monitor_grace_period, pod_eviction_timeout=a.pod_eviction_timeout,
+                   cluster_cidr=a.cluster_cidr, node_cidr_mask_size=a.node_cidr_mask_size,
+                   allocate_node_cidrs=a.allocate_node_cidrs == "true", configure_cloud_routes=a.configure_cloud_routes == "true",
+                   cloud=get_cloud_provider(a.cloud_provider, cfg), cluster_name=a.cluster_name,
+                   service_account_key=rd(a.service_account_private_key_file), root_ca=rd(a.root_ca_file) or b"",
+                   cluster_signing_cert_file=a.cluster_signing_cert_file, cluster_signing_key_file=a.cluster_signing_key_file,
+                   hostpath_pv_root=a.hostpath_pv_root, hpa_sync_period=a.horizontal_pod_autoscaler_sync_period,
+                   hpa_upscale_delay=a.horizontal_pod_autoscaler_upscale_delay,
+                   hpa_downscale_delay=a.horizontal_pod_autoscaler_downscale_delay)
+    names = resolve_controllers(a.controllers, opts)
 
     async def mk():
         return await ControllerManager(Client(a.server), names, a.leader_elect == "true", socket.gethostname(),
-                                       a.node_monitor_grace_period, a.pod_eviction_timeout, a.cluster_cidr,
-                                       a.node_cidr_mask_size, alloc).start()
+                                       options=opts).start()
     _run_forever(mk)
 
 

@@ -129,7 +129,9 @@ class NamespaceController(Controller):
 
 class GarbageCollector(Controller):
     name = "garbagecollector"
-    OWNED = ("pods", "replicasets", "jobs", "daemonsets", "deployments")
+    OWNED = ("pods", "replicasets", "jobs", "daemonsets", "deployments", "replicationcontrollers", "statefulsets",
+             "controllerrevisions", "cronjobs", "services", "endpoints", "configmaps", "secrets", "persistentvolumeclaims",
+             "horizontalpodautoscalers", "poddisruptionbudgets", "serviceaccounts")
 
     def __init__(self, mgr, period: float = 2.0):
         super().__init__(mgr)
@@ -163,11 +165,28 @@ class GarbageCollector(Controller):
                     await self._finalize(r, o, alive)
                     continue
                 refs = md.get("ownerReferences") or []
-                if refs and all(ref.get("uid") not in alive for ref in refs):
+                if refs and not any([await self._owner_alive(ref, o, alive) for ref in refs]):
                     try:
                         await self.client.delete(r, m.name_of(o), m.namespace_of(o), propagation="Background")
                     except m.StatusError:
                         pass
+
+    async def _owner_alive(self, ref, dependent, alive) -> bool:
+        """An owner of a watched kind is checked in the cache; any other kind with a GET
+        (garbagecollector.go attemptToDeleteItem → isDangling), unknown kinds count as alive."""
+        if ref.get("uid") in alive:
+            return True
+        from ..api.scheme import SCHEME
+        ri = SCHEME.for_kind(ref.get("apiVersion", ""), ref.get("kind", ""))
+        if ri is None:
+            return True
+        if ri.plural in self.infs:
+            return False
+        try:
+            o = await self.client.get(ri.plural, ref.get("name", ""), m.namespace_of(dependent) if ri.namespaced else "")
+        except m.StatusError as e:
+            return not m.is_not_found(e)
+        return m.uid_of(o) == ref.get("uid")
 
     async def _finalize(self, r, owner, alive):
         uid = m.uid_of(owner)

@@ -40,6 +40,7 @@ def _pod_from_template(owner, api_version, kind, extra_labels=None, node=None):
 class ReplicaSetController(Controller):
     name = "replicaset"
     burst = 500
+    owner_api, owner_kind, plural = "apps/v1", "ReplicaSet", "replicasets"
 
     def setup(self):
         f = self.mgr.factory
@@ -64,7 +65,7 @@ class ReplicaSetController(Controller):
         diff = want - len(pods)
         if diff > 0:
             for _ in range(min(diff, self.burst)):
-                await self.client.create(_pod_from_template(rs, "apps/v1", "ReplicaSet"), ns)
+                await self.client.create(_pod_from_template(rs, self.owner_api, self.owner_kind), ns)
         elif diff < 0:
             # delete not-ready / unscheduled pods first (controller_utils ActivePods ordering)
             pods.sort(key=lambda p: (bool((p.get("spec") or {}).get("nodeName")), is_pod_ready(p),
@@ -78,7 +79,7 @@ class ReplicaSetController(Controller):
         st = {"replicas": len(pods), "readyReplicas": ready, "availableReplicas": ready,
               "fullyLabeledReplicas": len(pods), "observedGeneration": (rs.get("metadata") or {}).get("generation", 1)}
         if {k: (rs.get("status") or {}).get(k) for k in st} != st:
-            await self.client.patch("replicasets", name, {"status": st}, ns, sub="status")
+            await self.client.patch(self.plural, name, {"status": st}, ns, sub="status")
 
 
 def template_hash(tpl) -> str:

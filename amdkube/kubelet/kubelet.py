@@ -546,6 +546,29 @@ class Kubelet:
                     if not ref.get("optional"):
                         raise RuntimeError(f"volume {name}: {kind[:-1]} {oname} not found") from e
                 vols[name] = d
+            elif "persistentVolumeClaim" in v:
+                # volumemanager/populator: claim → bound volume → its host path (hostPath / local)
+                claim = v["persistentVolumeClaim"].get("claimName", "")
+                pvc = await self.client.get_or_none("persistentvolumeclaims", claim, ns)
+                pv_name = ((pvc or {}).get("spec") or {}).get("volumeName")
+                if not pv_name or ((pvc or {}).get("status") or {}).get("phase") != "Bound":
+                    raise RuntimeError(f"volume {name}: PersistentVolumeClaim {claim} is not bound")
+                pv = await self.client.get("persistentvolumes", pv_name)
+                ps = pv.get("spec") or {}
+                path = (ps.get("hostPath") or {}).get("path") or (ps.get("local") or {}).get("path")
+                if not path:
+                    raise RuntimeError(f"volume {name}: PersistentVolume {pv_name} has no host-local source")
+                os.makedirs(path, exist_ok=True)
+                vols[name] = path
+            elif "downwardAPI" in v:
+                d = os.path.join(base, "kubernetes.io~downward-api", name)
+                os.makedirs(d, exist_ok=True)
+                for it in (v["downwardAPI"].get("items") or []):
+                    fr = it.get("fieldRef") or {}
+                    val = await self._env_from(pod, {"fieldRef": fr}) if fr else ""
+                    with open(os.path.join(d, it["path"]), "w") as f:
+                        f.write(val)
+                vols[name] = d
             else:  # emptyDir (and unknown types degrade to emptyDir)
                 d = os.path.join(base, "kubernetes.io~empty-dir", name)
                 os.makedirs(d, exist_ok=True)

@@ -51,11 +51,11 @@ class LocalCluster:
     async def start(self):
         b = self.base
         self.api = await APIServer(**self.api_kw).start()
-        self.client = Client(self.api.url, pool=256)
-        self.scheduler = await Scheduler(Client(self.api.url, pool=256), **self.scheduler_kw).start()
+        self.client = Client(self.api.url, token=self.api.loopback_token, pool=256)
+        self.scheduler = await Scheduler(Client(self.api.url, token=self.api.loopback_token, pool=256), **self.scheduler_kw).start()
         if self.with_controllers:
             from .controllers import ControllerManager
-            self.controllers = await ControllerManager(Client(self.api.url), **self.controllers_kw).start()
+            self.controllers = await ControllerManager(Client(self.api.url, token=self.api.loopback_token), **self.controllers_kw).start()
         if not self.with_kubelet:
             return self
         self.shim = await RocShim(os.path.join(b, "rocshim.sock"), os.path.join(b, "rocshim"),
@@ -68,7 +68,7 @@ class LocalCluster:
         cfg = KubeletConfig(node_name=self.node_name, root_dir=os.path.join(b, "kubelet"), plugins_dir=os.path.join(b, "plugins"),
                             cri_socket=os.path.join(b, "rocshim.sock"), port=0, relist_period=self.relist_period,
                             node_status_update_frequency=self.nsuf, **self.kubelet_kw)
-        self.kubelet = await Kubelet(Client(self.api.url, pool=128), cfg, smi_backend=self.backend).start()
+        self.kubelet = await Kubelet(Client(self.api.url, token=self.api.loopback_token, pool=128), cfg, smi_backend=self.backend).start()
         for p in self.plugins:
             await p.start()
             await p.wait_for_registration(10)
