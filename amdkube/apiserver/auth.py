@@ -131,13 +131,31 @@ class Authenticator:
             g.append("system:authenticated")
         return dict(u, groups=g)
 
-    def authenticate(self, headers) -> dict:
+    @staticmethod
+    def from_peer_cert(pc: dict) -> dict | None:
+        """x509 request authenticator (authentication/request/x509: CommonNameUserConversion):
+        a client certificate verified against --client-ca-file names the user in its CN and
+        the groups in its O entries."""
+        cn, groups = None, []
+        for rdn in pc.get("subject") or ():
+            for k, v in rdn:
+                if k == "commonName":
+                    cn = v
+                elif k == "organizationName":
+                    groups.append(v)
+        return {"name": cn, "uid": "", "groups": groups} if cn else None
+
+    def authenticate(self, headers, peercert: dict | None = None) -> dict:
         h = headers.get("Authorization", "")
         if h.startswith("Bearer "):
             u = self.authenticate_token(h[7:].strip())
             if u is None:
                 raise m.unauthorized()
             return u
+        if peercert:
+            u = self.from_peer_cert(peercert)
+            if u is not None:
+                return self._with_authenticated(u)
         if self.secured and not self.anonymous:
             raise m.unauthorized()
         return {"name": "system:anonymous", "groups": ["system:unauthenticated"]}

@@ -51,7 +51,8 @@ class APIServer:
                  token_auth: dict | None = None, authorization_mode: str = "AlwaysAllow",
                  max_in_flight: int = 400, max_mutating_in_flight: int = 200, event_ttl: float = 3600.0,
                  anonymous_auth: bool = True, service_cidr: str = "10.0.0.0/24", node_port_range: str = "30000-32767",
-                 service_account_key: bytes | None = None):
+                 service_account_key: bytes | None = None, tls_cert_file: str | None = None, tls_key_file: str | None = None,
+                 client_ca_file: str | None = None):
         self.store = store or MVCCStore()
         self.admission = adm.Chain(admission_plugins, admission_config)
         self.registry = Registry(self.store, self.admission, ServiceAllocator(service_cidr, parse_port_range(node_port_range)))
@@ -63,6 +64,7 @@ class APIServer:
         self.anonymous = anonymous_auth
         self.authz_mode = authorization_mode
         self.sa_key = service_account_key
+        self.tls = (tls_cert_file, tls_key_file, client_ca_file) if tls_cert_file else None
         self.authn = Authenticator(self.registry, self.tokens, service_account_key, anonymous_auth)
         self.authn.user_tokens = len(token_auth or {})
         self.authz = UnionAuthorizer(authorization_mode, self.registry)
@@ -103,7 +105,16 @@ class APIServer:
     async def start(self, host="127.0.0.1", port=0):
         self._runner = web.AppRunner(self.app, access_log=None, handler_cancellation=True)
         await self._runner.setup()
-        self._site = web.TCPSite(self._runner, host, port, backlog=1024, reuse_address=True)
+        ctx = None
+        if self.tls:
+            import ssl
+            cert, key, ca = self.tls
+            ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+            ctx.load_cert_chain(cert, key)
+            if ca:   # --client-ca-file: request (not require) client certificates
+                ctx.load_verify_locations(ca)
+                ctx.verify_mode = ssl.CERT_OPTIONAL
+        self._site = web.TCPSite(self._runner, host, port, backlog=1024, reuse_address=True, ssl_context=ctx)
         await self._site.start()
         self.port = self._site._server.sockets[0].getsockname()[1]
         self.host = host
@@ -140,7 +151,7 @@ class APIServer:
 
     @property
     def url(self):
-        return f"http://{self.host}:{self.port}"
+        return f"{'https' if self.tls else 'http'}://{self.host}:{self.port}"
 
     async def stop(self):
         for t in self._bg:
@@ -204,7 +215,8 @@ class APIServer:
 
     # ------------------------------------------------------------------ auth
     def _authenticate(self, request):
-        return self.authn.authenticate(request.headers)
+        pc = request.transport.get_extra_info("peercert") if self.tls and request.transport is not None else None
+        return self.authn.authenticate(request.headers, pc)
 
     def _authorize(self, user, verb, resource, group="", ns="", name="", sub=""):
         ok, _ = self.authz.authorize(Attributes(user, verb, group, resource, sub, ns, name))

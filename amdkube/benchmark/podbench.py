@@ -175,7 +175,8 @@ async def serve(args):
                 print(json.dumps(res), flush=True)
             if cmd.get("cmd") == "schedperf":
                 from amdkube.benchmark.schedperf import run_schedperf
-                res = await run_schedperf(int(cmd.get("nodes", 100)), int(cmd.get("pods", 3000)), gpus_per_node=8)
+                res = await run_schedperf(int(cmd.get("nodes", 100)), int(cmd.get("pods", 3000)), gpus_per_node=8,
+                                          gpu_pods=cmd.get("gpu_pods", "mixed"))
                 print(json.dumps(res), flush=True)
     finally:
         await lc.stop()

@@ -9,6 +9,7 @@ a request is sent (pkg/client/chaosclient/chaosclient.go:37-110, kubelet --chaos
 from __future__ import annotations
 
 import asyncio
+import os
 import json
 import random
 import time
@@ -41,10 +42,61 @@ class TokenBucket:
             await asyncio.sleep((1 - self.tokens) / self.qps)
 
 
+def _ssl_context(ca_file=None, ca_data=None, cert_file=None, key_file=None, insecure=False):
+    import ssl
+    ctx = ssl.create_default_context(ssl.Purpose.SERVER_AUTH)
+    if insecure:
+        ctx.check_hostname = False
+        ctx.verify_mode = ssl.CERT_NONE
+    elif ca_file or ca_data:
+        ctx.load_verify_locations(cafile=ca_file, cadata=ca_data)
+        ctx.check_hostname = False   # certificates name the cluster IPs / node names, not always the dial address
+    if cert_file:
+        ctx.load_cert_chain(cert_file, key_file)
+    return ctx
+
+
+def load_kubeconfig(path: str | None = None, context: str | None = None) -> dict:
+    """clientcmd: KUBECONFIG / ~/.kube/config YAML (clusters, users, contexts, current-context) →
+    {"server", "token", "ca_data", "cert_file"/"key_file" (data is spilled to a private temp dir)}."""
+    import base64
+    import tempfile
+    import yaml
+    path = path or os.environ.get("KUBECONFIG") or os.path.expanduser("~/.kube/config")
+    with open(path) as f:
+        cfg = yaml.safe_load(f) or {}
+    ctx_name = context or cfg.get("current-context")
+    ctxs = {c["name"]: c.get("context") or {} for c in cfg.get("contexts") or []}
+    ctx = ctxs.get(ctx_name) or (next(iter(ctxs.values())) if ctxs else {})
+    cluster = next((c.get("cluster") or {} for c in cfg.get("clusters") or [] if c["name"] == ctx.get("cluster")),
+                   (cfg.get("clusters") or [{}])[0].get("cluster") or {})
+    user = next((u.get("user") or {} for u in cfg.get("users") or [] if u["name"] == ctx.get("user")), {})
+    out = {"server": cluster.get("server", "http://127.0.0.1:8080"), "token": user.get("token"),
+           "insecure": bool(cluster.get("insecure-skip-tls-verify"))}
+    base = os.path.dirname(os.path.abspath(path))
+    rel = lambda p: p if os.path.isabs(p) else os.path.join(base, p)  # noqa: E731
+    if cluster.get("certificate-authority-data"):
+        out["ca_data"] = base64.b64decode(cluster["certificate-authority-data"]).decode()
+    elif cluster.get("certificate-authority"):
+        out["ca_file"] = rel(cluster["certificate-authority"])
+    if user.get("client-certificate-data"):
+        d = tempfile.mkdtemp(prefix="amdkube-kc-")
+        os.chmod(d, 0o700)
+        out["cert_file"], out["key_file"] = os.path.join(d, "c.crt"), os.path.join(d, "c.key")
+        open(out["cert_file"], "wb").write(base64.b64decode(user["client-certificate-data"]))
+        open(out["key_file"], "wb").write(base64.b64decode(user["client-key-data"]))
+    elif user.get("client-certificate"):
+        out["cert_file"], out["key_file"] = rel(user["client-certificate"]), rel(user.get("client-key", ""))
+    return out
+
+
 class Client:
     def __init__(self, server: str, token: str | None = None, qps: float = 0, burst: int = 0,
-                 chaos: float = 0.0, user_agent: str = "amdkube", timeout: float = 60.0, pool: int = 64):
+                 chaos: float = 0.0, user_agent: str = "amdkube", timeout: float = 60.0, pool: int = 64,
+                 ca_file: str | None = None, ca_data: str | None = None, cert_file: str | None = None,
+                 key_file: str | None = None, insecure: bool = False):
         self.server = server.rstrip("/")
+        self.ssl = _ssl_context(ca_file, ca_data, cert_file, key_file, insecure) if self.server.startswith("https") else None
         self.headers = {"User-Agent": user_agent, "Accept": "application/json"}
         if token:
             self.headers["Authorization"] = f"Bearer {token}"
@@ -60,7 +112,8 @@ class Client:
     def session(self) -> aiohttp.ClientSession:
         loop = asyncio.get_running_loop()
         if self._session is None or self._session.closed or self._loop is not loop:
-            conn = aiohttp.TCPConnector(limit=self.pool, keepalive_timeout=60, ttl_dns_cache=None)
+            conn = aiohttp.TCPConnector(limit=self.pool, keepalive_timeout=60, ttl_dns_cache=None,
+                                        ssl=self.ssl if self.ssl is not None else None)
             self._session = aiohttp.ClientSession(connector=conn, headers=self.headers,
                                                   timeout=aiohttp.ClientTimeout(total=None, sock_connect=10))
             self._loop = loop
@@ -70,6 +123,12 @@ class Client:
         if self._session is not None and not self._session.closed:
             await self._session.close()
         self._session = None
+
+    @classmethod
+    def from_kubeconfig(cls, path: str | None = None, context: str | None = None, **kw) -> "Client":
+        c = load_kubeconfig(path, context)
+        return cls(c["server"], token=c.get("token"), ca_file=c.get("ca_file"), ca_data=c.get("ca_data"),
+                   cert_file=c.get("cert_file"), key_file=c.get("key_file"), insecure=c.get("insecure", False), **kw)
 
     # ---------------------------------------------------------------- paths
     @staticmethod

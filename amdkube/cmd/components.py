@@ -22,6 +22,14 @@ import time
 from ..utils import log as klog
 
 
+def _client(a, **kw):
+    """--kubeconfig wins over --server (plus the kubelet's --token from TLS bootstrap)."""
+    from ..client import Client
+    if getattr(a, "kubeconfig", None):
+        return Client.from_kubeconfig(a.kubeconfig, **kw)
+    return Client(a.server, token=getattr(a, "token", None), **kw)
+
+
 def _run_forever(coro_factory):
     async def main():
         comp = await coro_factory()
@@ -51,6 +59,9 @@ def apiserver(argv):
     ap.add_argument("--service-cluster-ip-range", default="10.0.0.0/24")
     ap.add_argument("--service-node-port-range", default="30000-32767")
     ap.add_argument("--service-account-key-file", default=None, help="HMAC key for service-account tokens")
+    ap.add_argument("--tls-cert-file", default=None)
+    ap.add_argument("--tls-private-key-file", default=None)
+    ap.add_argument("--client-ca-file", default=None)
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     klog.setup(a.v, "apiserver")
@@ -72,7 +83,8 @@ def apiserver(argv):
                         max_in_flight=a.max_requests_inflight, max_mutating_in_flight=a.max_mutating_requests_inflight,
                         event_ttl=a.event_ttl, service_cidr=a.service_cluster_ip_range,
                         node_port_range=a.service_node_port_range,
-                        service_account_key=open(a.service_account_key_file, "rb").read().strip() if a.service_account_key_file else None)
+                        service_account_key=open(a.service_account_key_file, "rb").read().strip() if a.service_account_key_file else None,
+                        tls_cert_file=a.tls_cert_file, tls_key_file=a.tls_private_key_file, client_ca_file=a.client_ca_file)
         return await srv.start(a.bind_address, a.port)
     _run_forever(mk)
 
@@ -80,6 +92,7 @@ def apiserver(argv):
 def scheduler(argv):
     ap = argparse.ArgumentParser("amdkube scheduler")
     ap.add_argument("--master", "--server", dest="server", default="http://127.0.0.1:8080")
+    ap.add_argument("--kubeconfig", default=None, help="kubeconfig with the server, CA and credentials")
     ap.add_argument("--policy-config-file", default=None)
     ap.add_argument("--algorithm-provider", default="DefaultProvider")
     ap.add_argument("--scheduler-name", default="default-scheduler")
@@ -95,7 +108,7 @@ def scheduler(argv):
     from ..scheduler import Scheduler
 
     async def mk():
-        return await Scheduler(Client(a.server, qps=a.kube_api_qps), a.scheduler_name, a.policy_config_file, a.algorithm_provider,
+        return await Scheduler(_client(a, qps=a.kube_api_qps), a.scheduler_name, a.policy_config_file, a.algorithm_provider,
                                a.feature_gates, a.leader_elect == "true", port=a.port, disable_preemption=a.disable_preemption).start()
     _run_forever(mk)
 
@@ -103,6 +116,7 @@ def scheduler(argv):
 def controller_manager(argv):
     ap = argparse.ArgumentParser("amdkube controller-manager")
     ap.add_argument("--master", "--server", dest="server", default="http://127.0.0.1:8080")
+    ap.add_argument("--kubeconfig", default=None, help="kubeconfig with the server, CA and credentials")
     ap.add_argument("--controllers", default="*", help="'*' = defaults; 'name' enables, '-name' disables")
     ap.add_argument("--leader-elect", default="false")
     ap.add_argument("--node-monitor-grace-period", type=float, default=40.0)
@@ -143,7 +157,7 @@ def controller_manager(argv):
     names = resolve_controllers(a.controllers, opts)
 
     async def mk():
-        return await ControllerManager(Client(a.server), names, a.leader_elect == "true", socket.gethostname(),
+        return await ControllerManager(_client(a), names, a.leader_elect == "true", socket.gethostname(),
                                        options=opts).start()
     _run_forever(mk)
 
@@ -151,6 +165,7 @@ def controller_manager(argv):
 def kubelet(argv):
     ap = argparse.ArgumentParser("amdkube kubelet")
     ap.add_argument("--api-servers", "--server", dest="server", default="http://127.0.0.1:8080")
+    ap.add_argument("--kubeconfig", default=None, help="kubeconfig with the server, CA and credentials")
     ap.add_argument("--hostname-override", "--node-name", dest="node_name", default=socket.gethostname())
     ap.add_argument("--root-dir", default="/var/lib/kubelet")
     ap.add_argument("--device-plugin-dir", default=None)
@@ -166,6 +181,9 @@ def kubelet(argv):
     ap.add_argument("--register-with-taints", default="")
     ap.add_argument("--feature-gates", default="")
     ap.add_argument("--chaos-chance", type=float, default=0.0)
+    ap.add_argument("--pod-manifest-path", default=None, help="directory of static pod manifests")
+    ap.add_argument("--file-check-frequency", type=float, default=20.0)
+    ap.add_argument("--token", default=None, help="bearer token for the apiserver (e.g. from TLS bootstrap)")
     ap.add_argument("--gpu-stats-backend", default="auto")
     ap.add_argument("--kube-api-qps", type=float, default=0)
     ap.add_argument("-v", type=int, default=0)
@@ -185,6 +203,7 @@ def kubelet(argv):
                         address=a.address, port=a.port, node_ip=a.node_ip, node_status_update_frequency=a.node_status_update_frequency,
                         relist_period=a.pleg_relist_period, max_pods=a.max_pods, node_labels=labels,
                         register_with_taints=taints, feature_gates=a.feature_gates, chaos_chance=a.chaos_chance,
+                        pod_manifest_path=a.pod_manifest_path, file_check_frequency=a.file_check_frequency,
                         gpu_stats_backend=a.gpu_stats_backend)
 
     async def mk():
@@ -195,7 +214,7 @@ def kubelet(argv):
                 smi = open_backend(a.gpu_stats_backend)
             except Exception as e:
                 logging.getLogger("amdkube.kubelet").warning("no GPU stats backend: %s", e)
-        return await Kubelet(Client(a.server, qps=a.kube_api_qps, chaos=a.chaos_chance), cfg, smi_backend=smi).start()
+        return await Kubelet(_client(a, qps=a.kube_api_qps, chaos=a.chaos_chance), cfg, smi_backend=smi).start()
     _run_forever(mk)
 
 
@@ -315,6 +334,7 @@ def hollow_node(argv):
 def proxy(argv):
     ap = argparse.ArgumentParser("amdkube proxy")
     ap.add_argument("--master", "--server", dest="server", default="http://127.0.0.1:8080")
+    ap.add_argument("--kubeconfig", default=None, help="kubeconfig with the server, CA and credentials")
     ap.add_argument("--proxy-mode", default="userspace", choices=("userspace", "iptables"))
     ap.add_argument("--bind-address", default="0.0.0.0", help="node address NodePorts listen on")
     ap.add_argument("--cluster-cidr", default="")
@@ -329,7 +349,7 @@ def proxy(argv):
     from ..proxy import ProxyServer
 
     async def mk():
-        return await ProxyServer(Client(a.server), a.proxy_mode, a.bind_address, a.cluster_cidr, a.iptables_sync_period,
+        return await ProxyServer(_client(a), a.proxy_mode, a.bind_address, a.cluster_cidr, a.iptables_sync_period,
                                  a.iptables_min_sync_period, a.healthz_port, a.iptables_dump_file).start()
     _run_forever(mk)
 

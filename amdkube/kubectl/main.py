@@ -25,6 +25,9 @@ CONFIG = os.path.expanduser("~/.amdkube/config")
 
 
 def _client(a) -> Client:
+    kc = getattr(a, "kubeconfig", None) or os.environ.get("KUBECONFIG")
+    if kc and not a.server:
+        return Client.from_kubeconfig(kc, getattr(a, "context", None), user_agent="kubectl/amdkube")
     server, token = a.server, a.token
     if not server:
         server = os.environ.get("AMDKUBE_SERVER")
@@ -404,6 +407,8 @@ def parser():
     p = argparse.ArgumentParser(prog="kubectl", description="amdkube kubectl")
     p.add_argument("--server", "-s", default=None)
     p.add_argument("--token", default=None)
+    p.add_argument("--kubeconfig", default=None)
+    p.add_argument("--context", default=None)
     p.add_argument("-n", "--namespace", default=None)
     sub = p.add_subparsers(dest="cmd", required=True)
     for name in COMMANDS:

@@ -45,6 +45,11 @@ from .status import StatusManager, generate_status
 
 log = logging.getLogger("amdkube.kubelet")
 
+# pkg/kubelet/types/pod_update.go
+SOURCE_ANNOTATION = "kubernetes.io/config.source"
+HASH_ANNOTATION = "kubernetes.io/config.hash"
+MIRROR_ANNOTATION = "kubernetes.io/config.mirror"
+
 
 @dataclass
 class KubeletConfig:
@@ -70,6 +75,8 @@ class KubeletConfig:
     gpu_stats_backend: str = "none"                 # amdsmi|sysfs|fake|auto|none (per-container accelerator stats)
     cpu_capacity: int | None = None
     memory_capacity: int | None = None
+    pod_manifest_path: str | None = None            # static pods (--pod-manifest-path)
+    file_check_frequency: float = 20.0              # kubeletconfig FileCheckFrequency
 
 
 class PodWorker:
@@ -130,6 +137,9 @@ class Kubelet:
         self.started_at = time.time()
         self.last_sync_loop = time.time()
         self.sync_errors: dict[str, str] = {}
+        self.static: dict[str, dict] = {}      # uid -> static pod from --pod-manifest-path
+        self.mirrors: dict[tuple, dict] = {}   # (ns, name) -> mirror pod in the API
+        self._static_dirty = asyncio.Event()
 
     def _init_metrics(self):
         r = self.metrics
@@ -167,6 +177,8 @@ class Kubelet:
                         asyncio.create_task(self._eviction_loop(), name="eviction")]
         if self.cfg.evented_pleg:
             self._tasks.append(asyncio.create_task(self._evented_pleg(), name="pleg-events"))
+        if self.cfg.pod_manifest_path:
+            self._tasks.append(asyncio.create_task(self._static_pods_loop(), name="static-pods"))
         log.info("kubelet %s started (cri=%s, devicePlugins=%s)", self.node_name, self.cfg.cri_socket, self.gates("DevicePlugins"))
         return self
 
@@ -297,12 +309,18 @@ class Kubelet:
                 and (self.status.get(uid) or {}).get("phase") not in ("Succeeded", "Failed")]
 
     def _on_pod_add(self, pod):
+        if MIRROR_ANNOTATION in m.annotations_of(pod):
+            self.mirrors[(m.namespace_of(pod), m.name_of(pod))] = pod
+            return
         uid = m.uid_of(pod)
         self.pods[uid] = pod
         self.first_seen.setdefault(uid, time.time())
         self.dispatch(uid)
 
     def _on_pod_update(self, old, pod):
+        if MIRROR_ANNOTATION in m.annotations_of(pod):
+            self.mirrors[(m.namespace_of(pod), m.name_of(pod))] = pod
+            return
         self.pods[m.uid_of(pod)] = pod
         # only semantic changes wake the pod worker (reference pkg/kubelet/config/config.go
         # checkAndUpdatePod / podsDifferSemantically): the kubelet's own status writes echo back
@@ -311,9 +329,115 @@ class Kubelet:
             self.dispatch(m.uid_of(pod))
 
     def _on_pod_delete(self, pod):
+        if MIRROR_ANNOTATION in m.annotations_of(pod):
+            key = (m.namespace_of(pod), m.name_of(pod))
+            if self.mirrors.get(key, {}).get("metadata", {}).get("uid") == m.uid_of(pod):
+                self.mirrors.pop(key, None)
+            self._static_dirty.set()   # a deleted mirror pod is recreated (mirror_client.go)
+            return
         uid = m.uid_of(pod)
         self.pods.pop(uid, None)
         self.dispatch(uid)
+
+    # ============================================================= static pods
+    def _read_manifests(self) -> dict[str, dict]:
+        """pkg/kubelet/config/file.go: every *.yaml/*.yml/*.json in --pod-manifest-path is a pod;
+        it is named <name>-<node>, defaults to namespace `default`, and gets a UID derived from
+        the node name and the file content (config/common.go applyDefaults)."""
+        import hashlib
+        import uuid as _uuid
+        from ..api.scheme import load_manifests
+        out = {}
+        d = self.cfg.pod_manifest_path
+        try:
+            files = sorted(f for f in os.listdir(d) if f.endswith((".yaml", ".yml", ".json")) and not f.startswith("."))
+        except OSError:
+            return out
+        for f in files:
+            try:
+                with open(os.path.join(d, f)) as fh:
+                    text = fh.read()
+                docs = [x for x in load_manifests(text) if x.get("kind", "Pod") == "Pod"]
+            except Exception as e:
+                log.warning("static pod manifest %s is invalid: %r", f, e)
+                continue
+            for doc in docs:
+                md = doc.setdefault("metadata", {})
+                md["name"] = f"{md.get('name', os.path.splitext(f)[0])}-{self.node_name}"
+                md["namespace"] = md.get("namespace") or "default"
+                h = hashlib.md5((self.node_name + json.dumps(doc, sort_keys=True)).encode()).hexdigest()
+                md["uid"] = str(_uuid.UUID(h))
+                md.setdefault("annotations", {}).update({HASH_ANNOTATION: h, SOURCE_ANNOTATION: "file"})
+                md.setdefault("creationTimestamp", m.now_rfc3339())
+                doc["apiVersion"], doc["kind"] = "v1", "Pod"
+                doc.setdefault("spec", {})["nodeName"] = self.node_name
+                doc["spec"].setdefault("restartPolicy", "Always")
+                doc.setdefault("status", {"phase": "Pending"})
+                out[md["uid"]] = doc
+        return out
+
+    async def _static_pods_loop(self):
+        while True:
+            want = self._read_manifests()
+            for uid in [u for u in self.static if u not in want]:   # manifest removed or changed
+                old = self.static.pop(uid)
+                self.pods.pop(uid, None)
+                self.dispatch(uid)
+                mirror = self.mirrors.get((m.namespace_of(old), m.name_of(old)))
+                if mirror is not None and m.annotations_of(mirror).get(MIRROR_ANNOTATION) == uid.replace("-", "") \
+                        and not any(m.name_of(p) == m.name_of(old) and m.namespace_of(p) == m.namespace_of(old)
+                                    for p in want.values()):
+                    await self._delete_mirror(mirror)
+            for uid, pod in want.items():
+                if uid not in self.static:
+                    self.static[uid] = pod
+                    self.pods[uid] = pod
+                    self.first_seen.setdefault(uid, time.time())
+                    self.dispatch(uid)
+                try:
+                    await self._ensure_mirror(pod)
+                except Exception as e:
+                    log.debug("mirror pod for %s: %r", m.name_of(pod), e)
+            self._static_dirty.clear()
+            try:
+                await asyncio.wait_for(self._static_dirty.wait(), self.cfg.file_check_frequency)
+            except asyncio.TimeoutError:
+                pass
+
+    async def _ensure_mirror(self, pod):
+        """pkg/kubelet/pod/mirror_client.go: the API object that stands for a static pod."""
+        key = (m.namespace_of(pod), m.name_of(pod))
+        h = m.annotations_of(pod)[HASH_ANNOTATION]
+        cur = self.mirrors.get(key) or await self.client.get_or_none("pods", key[1], key[0])
+        if cur is not None and m.annotations_of(cur).get(MIRROR_ANNOTATION) == h and \
+                not (cur.get("metadata") or {}).get("deletionTimestamp"):
+            self.mirrors[key] = cur
+            return
+        if cur is not None:
+            await self._delete_mirror(cur)
+        body = json.loads(json.dumps(pod))
+        md = body["metadata"]
+        md.pop("uid", None)
+        md.pop("creationTimestamp", None)
+        md["annotations"][MIRROR_ANNOTATION] = h
+        body.pop("status", None)
+        try:
+            self.mirrors[key] = await self.client.create(body, key[0])
+        except m.StatusError as e:
+            if not m.is_already_exists(e):
+                raise
+        st = self.status.get(m.uid_of(pod))
+        if st:
+            self.status.forget(m.uid_of(pod))
+            self.status.set(pod, st)     # the status written before the mirror existed
+
+    async def _delete_mirror(self, mirror):
+        try:
+            await self.client.delete("pods", m.name_of(mirror), m.namespace_of(mirror), grace=0, uid=m.uid_of(mirror))
+        except m.StatusError as e:
+            if not (m.is_not_found(e) or m.is_conflict(e)):
+                raise
+        self.mirrors.pop((m.namespace_of(mirror), m.name_of(mirror)), None)
 
     def dispatch(self, uid: str):
         w = self.workers.get(uid)
