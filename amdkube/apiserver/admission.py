@@ -334,6 +334,33 @@ class StorageObjectInUseProtection(Plugin):
                 md["finalizers"] = list(md.get("finalizers") or []) + [fin]
 
 
+class NodeRestriction(Plugin):
+    """plugin/pkg/admission/noderestriction: a kubelet (system:node:<name> in system:nodes) may
+    create only mirror pods bound to itself, update the status of its own pods, and modify only
+    its own Node object."""
+    name = "NodeRestriction"
+    operations = (CREATE, UPDATE, DELETE)
+
+    def admit(self, a, ctx):
+        u = a.user or {}
+        if "system:nodes" not in (u.get("groups") or []) or not u.get("name", "").startswith("system:node:"):
+            return
+        node = u["name"][len("system:node:"):]
+        if a.resource == "nodes":
+            if a.name != node and m.name_of(a.obj or {}) != node:
+                raise m.forbidden(f'node "{node}" cannot modify node "{a.name}"')
+        elif a.resource == "pods":
+            pod = a.obj if a.operation == CREATE else (a.old or {})
+            if a.operation == CREATE and not a.subresource:
+                ann = ((pod.get("metadata") or {}).get("annotations") or {})
+                if "kubernetes.io/config.mirror" not in ann:
+                    raise m.forbidden(f'pod does not have "kubernetes.io/config.mirror" annotation, node "{node}" can only create mirror pods')
+                if (pod.get("spec") or {}).get("nodeName") != node:
+                    raise m.forbidden(f'node "{node}" can only create pods with spec.nodeName set to itself')
+            elif a.subresource in ("status", "") and (pod.get("spec") or {}).get("nodeName") != node:
+                raise m.forbidden(f'node "{node}" can only update or delete pods bound to itself')
+
+
 class AlwaysAdmit(Plugin):
     name = "AlwaysAdmit"
 
@@ -348,7 +375,7 @@ class AlwaysDeny(Plugin):
 
 REGISTRY = {p.name: p for p in (ResourceV2, ExtendedResourceToleration, NamespaceLifecycle, NamespaceAutoProvision,
                                  NamespaceExists, ServiceAccount, DefaultTolerationSeconds, LimitRanger, ResourceQuota,
-                                 Priority, PodNodeSelector, DefaultStorageClass, StorageObjectInUseProtection,
+                                 Priority, PodNodeSelector, DefaultStorageClass, StorageObjectInUseProtection, NodeRestriction,
                                  AlwaysAdmit, AlwaysDeny)}
 
 # Matches the fork's recommended ordering (hack/local-up-cluster.sh:424 adds ResourceV2).

@@ -248,6 +248,12 @@ class ResourceStore:
             md["generation"] = 1
         SCHEME.default(obj)
         self.prepare_for_create(obj)
+        if ri.plural == "certificatesigningrequests" and user is not None:
+            # certificates/strategy.go PrepareForCreate: the requester is who authenticated, not
+            # what the body claims
+            spec = obj.setdefault("spec", {})
+            spec["username"], spec["uid"] = user.get("name", ""), user.get("uid", "")
+            spec["groups"] = list(user.get("groups") or [])
         attrs = adm.Attributes(adm.CREATE, ri.plural, "", md.get("namespace", ""), md.get("name", ""), obj, None, user, ri.kind)
         self.api.admission.admit(attrs, self.api)
         SCHEME.default(obj)  # admission may add fields (e.g. ResourceV2) that need defaults

@@ -164,23 +164,40 @@ class Kubelet:
             self.dm.store.listeners.append(lambda rname: self._node_dirty.set())
         from .server import KubeletServer
         self.server = await KubeletServer(self).start(self.cfg.address, self.cfg.port)
-        await self.register_node()
-        await self.dm.wait_initial_registration(5.0)
-        self.informer = Informer(self.client, "pods", field_selector=f"spec.nodeName={self.node_name}")
-        self.informer.add_handler(on_add=self._on_pod_add, on_update=self._on_pod_update, on_delete=self._on_pod_delete)
-        self.informer.start()
-        await self.informer.wait_synced(30)
-        self._tasks += [asyncio.create_task(self._node_status_loop(), name="node-status"),
-                        asyncio.create_task(self._relist_loop(), name="pleg-relist"),
+        self._tasks += [asyncio.create_task(self._relist_loop(), name="pleg-relist"),
                         asyncio.create_task(self._prober_loop(), name="prober"),
                         asyncio.create_task(self._housekeeping(), name="housekeeping"),
                         asyncio.create_task(self._eviction_loop(), name="eviction")]
         if self.cfg.evented_pleg:
             self._tasks.append(asyncio.create_task(self._evented_pleg(), name="pleg-events"))
         if self.cfg.pod_manifest_path:
+            # static pods run with or without an apiserver (kubeadm: the apiserver IS a static
+            # pod), so registration is retried in the background (kubelet_node_status.go
+            # registerWithAPIServer: exponential back-off up to 7 s)
             self._tasks.append(asyncio.create_task(self._static_pods_loop(), name="static-pods"))
+            self._tasks.append(asyncio.create_task(self._connect_api(), name="api-connect"))
+        else:
+            await self._connect_api()
         log.info("kubelet %s started (cri=%s, devicePlugins=%s)", self.node_name, self.cfg.cri_socket, self.gates("DevicePlugins"))
         return self
+
+    async def _connect_api(self):
+        delay = 0.1
+        while True:
+            try:
+                await self.register_node()
+                break
+            except (aiohttp.ClientError, OSError, asyncio.TimeoutError) as e:
+                log.info("unable to register node %s with the API server: %r; retrying in %.1fs", self.node_name, e, delay)
+                await asyncio.sleep(delay)
+                delay = min(7.0, delay * 2)
+        await self.dm.wait_initial_registration(5.0)
+        self.informer = Informer(self.client, "pods", field_selector=f"spec.nodeName={self.node_name}")
+        self.informer.add_handler(on_add=self._on_pod_add, on_update=self._on_pod_update, on_delete=self._on_pod_delete)
+        self.informer.start()
+        await self.informer.wait_synced(30)
+        self._tasks.append(asyncio.create_task(self._node_status_loop(), name="node-status"))
+        self._static_dirty.set()   # create mirror pods now that the API is there
 
     async def stop(self):
         for t in self._tasks:
@@ -210,6 +227,7 @@ class Kubelet:
         node = {"apiVersion": "v1", "kind": "Node", "metadata": {"name": self.node_name, "labels": labels},
                 "spec": {"taints": list(self.cfg.register_with_taints)} if self.cfg.register_with_taints else {},
                 "status": self._node_status_body({})}
+        node["status"].pop("_removed", None)
         try:
             self.node = await self.client.create(node)
         except m.StatusError as e:

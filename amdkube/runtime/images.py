@@ -33,6 +33,7 @@ def builtin_images() -> dict[str, dict]:
         "amdkube/xgmi-probe:latest": {"entrypoint": [_b("xgmi-probe")]},
         "busybox:latest": {"entrypoint": [sh]},
         "python:3": {"entrypoint": [py]},
+        "amdkube/amdkube:latest": {"entrypoint": [py, "-m", "amdkube"]},
         "nginx:latest": {"entrypoint": [py, "-m", "http.server", "--bind", "127.0.0.1"], "cmd": ["8080"]},
         "k8s.gcr.io/pause:3.1": {"entrypoint": [_b("pause")]},
     }

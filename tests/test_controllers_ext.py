@@ -341,16 +341,33 @@ async def test_node_csr_auto_approved_and_signed(tmp_path):
              "-subj", "/O=system:nodes/CN=system:node:mi355x-1")
     _openssl("req", "-new", "-newkey", "rsa:2048", "-nodes", "-keyout", f"{d}/u.key", "-out", f"{d}/u.csr", "-subj", "/CN=alice")
     kw = {"cluster_signing_cert_file": f"{d}/ca.crt", "cluster_signing_key_file": f"{d}/ca.key"}
-    async with LocalCluster(gpus="none", api_kw={"authorization_mode": "RBAC"}, controllers_kw=kw, with_kubelet=False) as lc:
+    users = {"mallory-token": {"name": "mallory", "groups": []}, "alice-token": {"name": "alice", "groups": []}}
+    async with LocalCluster(gpus="none", api_kw={"authorization_mode": "RBAC", "token_auth": users}, controllers_kw=kw,
+                            with_kubelet=False) as lc:
         c = lc.client
+        b = lambda s: base64.b64encode(s.encode()).decode()  # noqa: E731
+        await c.create({"apiVersion": "v1", "kind": "Secret", "type": "bootstrap.kubernetes.io/token",
+                        "metadata": {"name": "bootstrap-token-abcdef"},
+                        "data": {"token-id": b("abcdef"), "token-secret": b("0123456789abcdef"),
+                                 "usage-bootstrap-authentication": b("true")}}, "kube-system")
+        # anyone may request certificates (RBAC here: bootstrappers via policy, others via this binding)
+        await c.create({"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRoleBinding",
+                        "metadata": {"name": "csr-create"},
+                        "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole", "name": "system:node-bootstrapper"},
+                        "subjects": [{"kind": "Group", "name": "system:authenticated"}]})
 
-        def csr(name, path, user, groups):
+        def csr(name, path):
             return {"apiVersion": "certificates.k8s.io/v1beta1", "kind": "CertificateSigningRequest", "metadata": {"name": name},
-                    "spec": {"request": base64.b64encode(open(path, "rb").read()).decode(), "username": user, "groups": groups,
-                             "usages": ["digital signature", "key encipherment", "client auth"]}}
-        await c.create(csr("node-csr", f"{d}/n.csr", "system:bootstrap:abcdef", ["system:bootstrappers", "system:authenticated"]))
-        await c.create(csr("alice-csr", f"{d}/u.csr", "alice", ["system:authenticated"]))
-        await c.create(csr("rogue-csr", f"{d}/n.csr", "mallory", ["system:authenticated"]))
+                    "spec": {"request": base64.b64encode(open(path, "rb").read()).decode(), "username": "spoofed",
+                             "groups": ["system:masters"], "usages": ["digital signature", "key encipherment", "client auth"]}}
+        for token, name, path in (("abcdef.0123456789abcdef", "node-csr", f"{d}/n.csr"), ("alice-token", "alice-csr", f"{d}/u.csr"),
+                                  ("mallory-token", "rogue-csr", f"{d}/n.csr")):
+            uc = Client(lc.api.url, token=token)
+            try:
+                o = await uc.create(csr(name, path))
+            finally:
+                await uc.close()
+            assert o["spec"]["username"] != "spoofed" and "system:masters" not in o["spec"]["groups"]
 
         async def issued():
             o = await c.get("certificatesigningrequests", "node-csr")

@@ -1,0 +1,111 @@
+"""kubeadm init → join → schedule → token → reset, every component a real process (reference
+cmd/kubeadm/app/cmd/{init,join,reset,token}.go; test/e2e_kubeadm). TLS everywhere: the
+apiserver serves the kubeadm-generated certificate and authenticates components by client
+certificate; the worker joins through token discovery + TLS bootstrap (CSR auto-approved and
+signed by the cluster CA)."""
+from __future__ import annotations
+
+import asyncio
+import os
+import re
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from amdkube.api import meta as m
+from amdkube.client import Client
+from amdkube.kubeadm import ca_cert_hash, new_token
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _kubeadm(*args, timeout=180):
+    return subprocess.run([sys.executable, "-m", "amdkube", "kubeadm", *args], cwd=ROOT, capture_output=True, text=True,
+                          timeout=timeout, env=dict(os.environ, PYTHONPATH=ROOT))
+
+
+def test_token_format_and_ca_pin(tmp_path):
+    t = new_token()
+    assert re.fullmatch(r"[a-z0-9]{6}\.[a-z0-9]{16}", t)
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", str(tmp_path / "k"), "-out",
+                    str(tmp_path / "c"), "-days", "1", "-subj", "/CN=x"], check=True, capture_output=True)
+    h = ca_cert_hash(open(tmp_path / "c", "rb").read())
+    assert h.startswith("sha256:") and len(h) == 7 + 64
+
+
+@pytest.mark.slow
+def test_kubeadm_init_join_reset(tmp_path):
+    master, worker = str(tmp_path / "master"), str(tmp_path / "worker")
+    port = _free_port()
+    try:
+        r = _kubeadm("init", "--base-dir", master, "--apiserver-bind-port", str(port), "--node-name", "master-0",
+                     "--start-kubelet", "--kubelet-port", "0", "--pod-network-cidr", "10.244.0.0/16", "--service-cidr",
+                     "10.96.0.0/12", "--timeout", "90")
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+        assert "initialized successfully" in r.stdout
+        join = re.search(r"kubeadm join (\S+) --token (\S+) --discovery-token-ca-cert-hash (\S+)", r.stdout)
+        assert join, r.stdout
+        server, token, h = join.groups()
+        # a wrong CA pin is refused
+        bad = _kubeadm("join", server, "--token", token, "--discovery-token-ca-cert-hash", "sha256:" + "0" * 64,
+                       "--base-dir", str(tmp_path / "bad"), "--node-name", "bad", "--timeout", "20")
+        assert bad.returncode != 0 and "does not match" in bad.stderr
+        r = _kubeadm("join", server, "--token", token, "--discovery-token-ca-cert-hash", h, "--base-dir", worker,
+                     "--node-name", "worker-1", "--start-kubelet", "--kubelet-port", "0")
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+        asyncio.run(_check_cluster(os.path.join(master, "admin.conf")))
+        r = _kubeadm("token", "list", "--kubeconfig", os.path.join(master, "admin.conf"))
+        assert token.split(".")[0] in r.stdout, r.stdout + r.stderr
+    finally:
+        for d in (worker, master):
+            _kubeadm("reset", "--base-dir", d, "--drain-seconds", "1.5")
+
+
+async def _check_cluster(admin_conf):
+    c = Client.from_kubeconfig(admin_conf)
+    try:
+        assert c.server.startswith("https://")
+
+        async def ready(name):
+            n = await c.get_or_none("nodes", name)
+            conds = {x["type"]: x["status"] for x in ((n or {}).get("status") or {}).get("conditions") or []}
+            return n if conds.get("Ready") == "True" else None
+        end = asyncio.get_running_loop().time() + 60
+        nodes = {}
+        while asyncio.get_running_loop().time() < end and len(nodes) < 2:
+            for name in ("master-0", "worker-1"):
+                n = await ready(name)
+                if n:
+                    nodes[name] = n
+            await asyncio.sleep(0.3)
+        assert set(nodes) == {"master-0", "worker-1"}
+        assert "node-role.kubernetes.io/master" in m.labels_of(nodes["master-0"])
+        assert any(t["effect"] == "NoSchedule" for t in nodes["master-0"]["spec"].get("taints") or [])
+        # control plane runs as static pods with mirror pods
+        pods, _ = await c.list("pods", "kube-system")
+        names = {m.name_of(p) for p in pods}
+        assert {"kube-apiserver-master-0", "kube-controller-manager-master-0", "kube-scheduler-master-0"} <= names
+        # a workload lands on the worker (the master is tainted) and runs
+        await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "hello"},
+                        "spec": {"containers": [{"name": "c", "image": "amdkube/pause:3.1"}]}}, "default")
+        end = asyncio.get_running_loop().time() + 60
+        p = None
+        while asyncio.get_running_loop().time() < end:
+            p = await c.get("pods", "hello", "default")
+            if (p.get("status") or {}).get("phase") == "Running":
+                break
+            await asyncio.sleep(0.3)
+        assert p["spec"]["nodeName"] == "worker-1" and p["status"]["phase"] == "Running", p.get("status")
+        # the worker's kubelet identity is a node identity (NodeRestriction): it cannot touch the master
+        csrs, _ = await c.list("certificatesigningrequests")
+        assert any(x["spec"]["username"].startswith("system:bootstrap:") and x["status"].get("certificate") for x in csrs)
+    finally:
+        await c.close()
