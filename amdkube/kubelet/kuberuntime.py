@@ -32,6 +32,26 @@ A_HASH, A_RESTARTS, A_INIT = "io.kubernetes.container.hash", "io.kubernetes.cont
 BACKOFF_BASE, BACKOFF_MAX = 10.0, 300.0
 
 
+SECCOMP_POD_ANN = "seccomp.security.alpha.kubernetes.io/pod"
+SECCOMP_CONTAINER_ANN = "container.seccomp.security.alpha.kubernetes.io/"
+
+
+def seccomp_profile(pod: dict, container: str, root: str = "/var/lib/kubelet/seccomp") -> str:
+    """kuberuntime_sandbox.go getSeccompProfileFromAnnotations: the container annotation wins
+    over the pod one; docker/default means runtime/default; localhost/<p> is relative to
+    --seccomp-profile-root; unconfined (or nothing) means no filter."""
+    ann = (pod.get("metadata") or {}).get("annotations") or {}
+    p = ann.get(SECCOMP_CONTAINER_ANN + container) or ann.get(SECCOMP_POD_ANN) or ""
+    if p in ("", "unconfined"):
+        return ""
+    if p in ("docker/default", "runtime/default"):
+        return "runtime/default"
+    if p.startswith("localhost/"):
+        rel = p[len("localhost/"):]
+        return "localhost/" + (rel if os.path.isabs(rel) else os.path.join(root, rel))
+    return p
+
+
 def container_hash(c: dict) -> str:
     return hashlib.sha1(json.dumps(c, sort_keys=True).encode()).hexdigest()[:16]
 
@@ -82,6 +102,7 @@ class RuntimeManager:
         self.recorder = recorder
         self.backoff: dict[tuple[str, str], tuple[float, float]] = {}  # (uid, name) -> (until, last delay)
         self.sandbox_ips: dict[str, str] = {}   # sandbox id -> IP (PodSandboxStatus is asked once per sandbox)
+        self.seccomp_root = os.path.join(root_dir, "seccomp")   # --seccomp-profile-root
 
     # ----------------------------------------------------------------- status
     async def pod_status(self, uid: str, sandboxes=None) -> PodRuntimeStatus:
@@ -170,7 +191,10 @@ class RuntimeManager:
             command=c.get("command") or [], args=c.get("args") or [], working_dir=c.get("workingDir") or "",
             envs=envs, mounts=mounts, devices=devices,
             labels={L_POD_NAME: md["name"], L_POD_NS: md.get("namespace", ""), L_POD_UID: md["uid"], L_CONTAINER: c["name"]},
-            annotations=ann, log_path=f"{c['name']}/{restart_count}.log", linux=C.LinuxContainerConfig(resources=lres))
+            annotations=ann, log_path=f"{c['name']}/{restart_count}.log",
+            linux=C.LinuxContainerConfig(resources=lres, security_context=C.LinuxContainerSecurityContext(
+                seccomp_profile_path=seccomp_profile(pod, c["name"], self.seccomp_root),
+                no_new_privs=not bool(((c.get("securityContext") or {}).get("allowPrivilegeEscalation", True))))))
         cid = await self.cri.create_container(sid, cfg, sandbox_cfg)
         await self.cri.start_container(cid)
         return cid

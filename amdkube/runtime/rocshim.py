@@ -322,6 +322,9 @@ class RocShim:
         env["AMDKUBE_ROOTFS"] = root
         r = cfg.linux.resources if cfg.HasField("linux") else None
         resources = {"cpu_quota": r.cpu_quota, "cpu_period": r.cpu_period, "memory_limit": r.memory_limit_in_bytes} if r else {}
+        sec = cfg.linux.security_context.seccomp_profile_path if cfg.HasField("linux") else ""
+        if sec:
+            resources["seccomp_profile"] = self._seccomp_file(sec)
         c = Container(cid, sid, cfg.metadata.name, cfg.metadata.attempt, cfg.image.image, self.images.image_id(iname), argv,
                       env, cwd, log_path, dict(cfg.labels), dict(cfg.annotations), mounts, devices, handler, resources)
         self.containers[cid] = c
@@ -329,12 +332,27 @@ class RocShim:
         self._emit(c, C.CONTAINER_CREATED_EVENT)
         return cid
 
+    @staticmethod
+    def _seccomp_file(spec: str) -> str:
+        """CRI seccomp_profile_path: runtime/default → rocshim's built-in profile, localhost/<abs path>."""
+        if spec in ("runtime/default", "docker/default"):
+            return os.path.join(os.path.dirname(__file__), "seccomp_default.json")
+        if spec.startswith("localhost/"):
+            p = spec[len("localhost"):]
+            if not os.path.isfile(p):
+                raise LookupError(f"seccomp profile {p} not found")
+            return p
+        raise ValueError(f"unsupported seccomp profile {spec!r}")
+
     def _launch_argv(self, c: Container) -> list[str]:
+        sec = c.resources.get("seccomp_profile")
         if self.isolation != "namespaces":
-            return c.argv
+            return [self.nsexec_bin, "--no-namespaces", "--seccomp", sec, "--"] + c.argv if sec else c.argv
         keep = [d["host_path"] for d in c.devices if "/dri/" in d["host_path"]]
         cg = os.path.join(self.cgroup_root, c.sandbox_id, c.id)
         a = [self.nsexec_bin, "--dev-root", self.dev_root, "--cgroup", cg]
+        if sec:
+            a += ["--seccomp", sec]
         for k in keep:
             a += ["--keep", k]
         if c.resources.get("memory_limit"):
