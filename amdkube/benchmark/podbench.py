@@ -42,15 +42,30 @@ def pct(xs, q):
     return xs[k]
 
 
+def cpu_pods_for(n_gpus: int) -> int:
+    """Density composition: the reference's 30 pods per node (density.go) as 8 GPU pods (one
+    per MI355X of a full node) + 22 pause pods, scaled to N allocatable GPUs (weak scaling)."""
+    return int(round(22 * n_gpus / 8.0 + 1e-9)) if n_gpus != 1 else 3
+
+
 class PodBench:
-    def __init__(self, lc: LocalCluster, n_gpus: int, pods_per_gpu: int, image: str, args: list[str]):
+    def __init__(self, lc: LocalCluster, n_gpus: int, pods_per_gpu: int, image: str, args: list[str], mode: str = "density"):
         self.lc, self.n, self.ppg, self.image, self.args = lc, n_gpus, pods_per_gpu, image, args
+        self.mode = mode
+        self.cpu_per_step = cpu_pods_for(n_gpus)
+        self.pending_cleanup: list[str] = []
         self.seq = 0
         self.t: dict[str, dict] = {}
         self.done_events: dict[str, asyncio.Event] = {}
         self.failed: list[str] = []
         self._watch_task = None
         self.deleting: set = set()
+
+    def cpu_pod(self, name):
+        return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "default", "labels": {"app": "podbench"}},
+                "spec": {"terminationGracePeriodSeconds": 0,
+                         "containers": [{"name": "pause", "image": "amdkube/pause:3.1",
+                                         "resources": {"requests": {"cpu": "10m", "memory": "10Mi"}}}]}}
 
     def pod(self, name):
         return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "default", "labels": {"app": "podbench"}},
@@ -88,6 +103,17 @@ class PodBench:
                 if "running" in s or "terminated" in s:
                     rec["started"] = now
         ph = st.get("phase")
+        if rec.get("cpu"):
+            if ph == "Running" and "started" in rec and "done" not in rec:
+                rec["done"] = now
+                ev = self.done_events.get(name)
+                if ev:
+                    ev.set()
+            elif ph == "Failed" and "done" not in rec:
+                rec["done"] = now
+                self.failed.append(f"{name}: {st.get('reason')} {st.get('message')}")
+                self.done_events[name].set()
+            return
         if ph in ("Succeeded", "Failed") and "done" not in rec:
             rec["done"] = now
             rec.setdefault("started", now)
@@ -126,12 +152,43 @@ class PodBench:
         await asyncio.wait_for(asyncio.gather(*(self.done_events[nm].wait() for nm in names)), timeout)
         return names
 
+    async def density_step(self, timeout=300.0):
+        """density.go on the real node: N GPU pods (one per MI355X, real vector-add run to
+        completion on its assigned GPU) + the density share of pause pods, created at once; the
+        step ends when every pause pod is Running and every GPU pod has Succeeded. The previous
+        step's pause pods are deleted while this one runs."""
+        old, self.pending_cleanup = self.pending_cleanup, []
+        for nm in old:
+            self.deleting.add(nm)
+            asyncio.create_task(self._delete(nm))
+        gpu, cpu = [], []
+        for _ in range(self.n):
+            self.seq += 1
+            gpu.append(f"vadd-{self.seq:06d}")
+        for _ in range(self.cpu_per_step):
+            self.seq += 1
+            cpu.append(f"pause-{self.seq:06d}")
+        for nm in gpu + cpu:
+            self.t[nm] = {"wave": 0, "cpu": nm in cpu}
+            self.done_events[nm] = asyncio.Event()
+        creates = []
+        for nm in gpu + cpu:
+            self.t[nm]["create"] = time.perf_counter()
+            creates.append(self.lc.client.create(self.pod(nm) if nm in gpu else self.cpu_pod(nm), "default"))
+        await asyncio.gather(*creates)
+        await asyncio.wait_for(asyncio.gather(*(self.done_events[nm].wait() for nm in gpu + cpu)), timeout)
+        self.pending_cleanup = cpu
+        return gpu + cpu
+
     async def run(self, steps: int):
         t0 = time.perf_counter()
         names = []
         for _ in range(steps):
-            names += await self.step()
+            names += await (self.density_step() if self.mode == "density" else self.step())
         el = time.perf_counter() - t0
+        cpu_recs = [self.t[n] for n in names if self.t[n].get("cpu")]
+        names_all = names
+        names = [n for n in names if not self.t[n].get("cpu")]
         recs = [self.t[n] for n in names]
         first = [r["started"] - r["create"] for r in recs if r["wave"] == 0]
         allstart = [r["started"] - r["create"] for r in recs]
@@ -139,7 +196,12 @@ class PodBench:
         sched = [r["bound"] - r["create"] for r in recs if r["wave"] == 0]
         life = [r["done"] - r["started"] for r in recs]
         ms = lambda v: None if v is None else round(v * 1000, 2)  # noqa: E731
-        return {"pods": len(names), "elapsed_s": el, "pods_per_s": len(names) / el if el else 0.0,
+        cpu_start = [r["started"] - r["create"] for r in cpu_recs]
+        every = allstart + cpu_start
+        return {"pods": len(names_all), "gpu_pods": len(names), "cpu_pods": len(cpu_recs), "elapsed_s": el,
+                "pods_per_s": len(names_all) / el if el else 0.0, "gpu_pods_per_s": len(names) / el if el else 0.0,
+                "p50_startup_all_pods_ms": ms(pct(every, 50)), "p90_startup_all_pods_ms": ms(pct(every, 90)),
+                "p99_startup_all_pods_ms": ms(pct(every, 99)), "p50_cpu_pod_startup_ms": ms(pct(cpu_start, 50)),
                 "failed": len(self.failed), "failures": self.failed[:5],
                 "p50_startup_ms": ms(pct(first, 50)), "p90_startup_ms": ms(pct(first, 90)), "p99_startup_ms": ms(pct(first, 99)),
                 "p50_startup_all_ms": ms(pct(allstart, 50)), "p50_node_startup_ms": ms(pct(node, 50)),
@@ -155,7 +217,7 @@ async def serve(args):
     await lc.wait_gpus(args.gpus, 60)
     node = await lc.client.get("nodes", lc.node_name)
     devs = list(((node["status"].get("extendedResources") or {}).get("amd.com/gpu") or {}).get("resources") or {})
-    pb = PodBench(lc, args.gpus, args.pods_per_gpu, args.image, args.args)
+    pb = PodBench(lc, args.gpus, args.pods_per_gpu, args.image, args.args, args.mode)
     await pb.start()
     print(json.dumps({"ready": True, "gpus": devs, "backend": lc.backend.name if lc.backend else "none"}), flush=True)
     loop = asyncio.get_running_loop()
@@ -185,7 +247,8 @@ async def serve(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--pods-per-gpu", type=int, default=4)
+    ap.add_argument("--pods-per-gpu", type=int, default=4, help="churn mode: GPU pods per GPU per step")
+    ap.add_argument("--mode", default="density", choices=("density", "churn"))
     ap.add_argument("--backend", default="auto")
     ap.add_argument("--image", default="rocm/vector-add")
     ap.add_argument("--health-probe", default="none")

@@ -1,21 +1,27 @@
-"""amdkube headline benchmark: GPU-pod throughput + p50 GPU-pod startup latency on one
+"""amdkube headline benchmark: pod density throughput + p50 GPU-pod startup latency on one
 MI355X node with N allocatable GPUs (BASELINE.json metric; SURVEY §6 mapping).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--pods-per-gpu P]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode density|churn]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU; rank 0 drives)
 
 Rank 0 launches the node (apiserver, scheduler, rocshim, AMD device plugin on amd-smi,
 kubelet) in a child process BEFORE any GPU initialisation in this process, then every rank
-brackets exactly K steps with barrier + torch.cuda.synchronize(). One step = P×N GPU pods
-(`amd.com/gpu: 1` each) running the real gfx950 vector-add workload on exactly their
-assigned GPU; the step ends when all have Succeeded. value = pods completed per second over
-the whole job (all N GPUs); extra fields carry startup-latency percentiles and the
-scheduler_perf (100 nodes / 3000 pods) result.
+brackets exactly K steps with barrier + torch.cuda.synchronize().
+
+density (default) — the reference's headline test, test/e2e/scalability/density.go (30 pods
+per node; saturation throughput ≥ 8 pods/s, startup p50/p90/p99 ≤ 5 s), run on the real
+MI355X node: one step creates N GPU pods (`amd.com/gpu: 1` each through ResourceV2 →
+device-granular binding, running the real gfx950 vector-add to completion on exactly its
+assigned GPU) plus the density share of pause pods (22 per 8 GPUs, i.e. 30 pods at N=8);
+the step ends when every pause pod is Running and every GPU pod has Succeeded.
+value = all pods per second over the job; gpu_pods_per_s, GPU-pod and all-pod startup
+percentiles are reported beside it. churn — GPU pods only, P per GPU per step (the per-GPU
+process-lifetime bound; docs/PERFORMANCE.md).
 
 Baselines: density saturation ≥ 8 pods/s (vs_baseline = value / 8),
-pod startup p50/p90/p99 ≤ 5 s, scheduler throughput ≥ 30 pods/s (goal 100). The extra
-`density` field is the reference density test itself (100 hollow nodes × 30 pods, 8 of them
-GPU pods per node; amdkube/benchmark/density.py), run after the timed region.
+pod startup p50/p90/p99 ≤ 5 s, scheduler throughput ≥ 30 pods/s (goal 100). Extra fields:
+scheduler_perf (100 nodes / 3000 pods) and the density test on 100 hollow 8×MI355X nodes
+(amdkube/benchmark/density.py), both run after the timed region.
 """
 from __future__ import annotations
 
@@ -37,7 +43,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=None)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--pods-per-gpu", type=int, default=4)
+    ap.add_argument("--pods-per-gpu", type=int, default=4, help="churn mode only")
+    ap.add_argument("--mode", default="density", choices=("density", "churn"),
+                    help="density: the reference density.go mix on the real node (default); churn: GPU pods only")
     ap.add_argument("--backend", default="auto", help="amdsmi|sysfs|fake|auto")
     ap.add_argument("--no-sched-perf", action="store_true")
     ap.add_argument("--density-nodes", type=int, default=100, help="hollow-node density run (0 = skip)")
@@ -56,7 +64,7 @@ def main():
                   "TORCHELASTIC_RUN_ID"):
             env.pop(k, None)
         worker = subprocess.Popen([sys.executable, "-m", "amdkube.benchmark.podbench", "--gpus", str(n),
-                                   "--pods-per-gpu", str(a.pods_per_gpu), "--backend", a.backend],
+                                   "--pods-per-gpu", str(a.pods_per_gpu), "--backend", a.backend, "--mode", a.mode],
                                   cwd=ROOT, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
         ready = json.loads(worker.stdout.readline() or "{}")
         if not ready.get("ready"):
@@ -126,14 +134,25 @@ def main():
             worker.kill()
         pods = res["pods"]
         value = pods / el
+        if a.mode == "density":
+            data = (f"synthetic: per step {n} rocm/vector-add GPU pod(s) (one per allocatable MI355X, 50,000 fp32 elements, run to "
+                    f"completion on the assigned GPU) + {res['cpu_pods'] // a.steps} pause pods, the reference density.go mix of "
+                    "30 pods/node at 8 GPUs scaled to N")
+            model = "density.go on one real MI355X node: GPU pods (amd.com/gpu=1, ResourceV2 → device binding) + pause pods"
+            gbatch = res["pods"] // a.steps
+        else:
+            data = "synthetic: rocm/vector-add GPU pods (50,000 fp32 elements each, cuda-vector-add equivalent)"
+            model = "GPU-pod churn: 1 node, amd.com/gpu=1 pods, ResourceV2 → device-granular binding"
+            gbatch = n * a.pods_per_gpu
         out = {"metric": METRIC, "value": round(value, 3), "unit": "pods/s", "n_gpus": n, "steps": a.steps, "warmup": a.warmup,
                "ms_per_step": round(el * 1000 / a.steps, 2), "higher_is_better": True, "scaling": "weak",
-               "vs_baseline": round(value / BASELINE_PODS_PER_S, 3), "dtype": "fp32",
-               "data": "synthetic: rocm/vector-add GPU pods (50,000 fp32 elements each, cuda-vector-add equivalent)",
-               "config": {"model": "GPU-pod density: 1 node, amd.com/gpu=1 pods, ResourceV2 → device-granular binding",
-                          "global_batch": n * a.pods_per_gpu, "seq_len": None, "parallelism": f"{n} allocatable MI355X"},
+               "vs_baseline": round(value / BASELINE_PODS_PER_S, 3), "dtype": "fp32", "data": data,
+               "config": {"model": model, "global_batch": gbatch, "seq_len": None, "parallelism": f"{n} allocatable MI355X",
+                          "mode": a.mode},
+               "gpu_pods_per_s": round(res["gpu_pods"] / el, 3), "gpu_pods": res["gpu_pods"], "cpu_pods": res["cpu_pods"],
                "p50_startup_ms": res["p50_startup_ms"], "p90_startup_ms": res["p90_startup_ms"],
                "p99_startup_ms": res["p99_startup_ms"], "startup_slo_ms": SLO_STARTUP_MS,
+               "p50_startup_all_pods_ms": res["p50_startup_all_pods_ms"], "p99_startup_all_pods_ms": res["p99_startup_all_pods_ms"],
                "p50_node_startup_ms": res["p50_node_startup_ms"], "p50_schedule_ms": res["p50_schedule_ms"],
                "p50_pod_runtime_ms": res["p50_pod_runtime_ms"], "failed_pods": res["failed"],
                "sched_perf": sched, "density": density}
