@@ -211,8 +211,12 @@ class PodBench:
 
 async def serve(args):
     logging.basicConfig(level=logging.WARNING, stream=sys.stderr)
-    lc = LocalCluster(gpus=args.backend, n_gpus=args.gpus, relist_period=1.0, with_controllers=False,
-                      health_probe=args.health_probe)
+    if args.procs:
+        from amdkube.benchmark.procnode import ProcessNode
+        lc = ProcessNode(args.backend, args.gpus, relist_period=1.0, health_probe=args.health_probe)
+    else:
+        lc = LocalCluster(gpus=args.backend, n_gpus=args.gpus, relist_period=1.0, with_controllers=False,
+                          health_probe=args.health_probe)
     await lc.start()
     await lc.wait_gpus(args.gpus, 60)
     node = await lc.client.get("nodes", lc.node_name)
@@ -249,6 +253,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--pods-per-gpu", type=int, default=4, help="churn mode: GPU pods per GPU per step")
     ap.add_argument("--mode", default="density", choices=("density", "churn"))
+    ap.add_argument("--procs", type=int, default=1, help="1: rocshim, device plugin and kubelet as separate processes")
     ap.add_argument("--backend", default="auto")
     ap.add_argument("--image", default="rocm/vector-add")
     ap.add_argument("--health-probe", default="none")

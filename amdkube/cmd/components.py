@@ -40,6 +40,17 @@ def _run_forever(coro_factory):
         await stop.wait()
         if hasattr(comp, "stop"):
             await comp.stop()
+    prof_path = os.environ.get("AMDKUBE_CPROFILE")   # whole-process profile of a daemon, written on SIGTERM
+    if prof_path:
+        import cProfile
+        pr = cProfile.Profile()
+        pr.enable()
+        try:
+            asyncio.run(main())
+        finally:
+            pr.disable()
+            pr.dump_stats(f"{prof_path}.{os.getpid()}")
+        return
     asyncio.run(main())
 
 

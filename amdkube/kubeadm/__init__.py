@@ -494,7 +494,7 @@ def reset(a) -> int:
     # runtime still tracks (each runs in its own session)
     for kind in ("containers", "sandboxes"):
         sd = os.path.join(cfg["node_dir"], "rocshim", kind)
-        for f in os.listdir(sd) if os.path.isdir(sd) else ():
+        for f in [x for x in os.listdir(sd) if x.endswith(".json")] if os.path.isdir(sd) else ():
             try:
                 pid = json.load(open(os.path.join(sd, f))).get("pid") or 0
                 if pid > 1:

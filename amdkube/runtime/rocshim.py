@@ -152,7 +152,7 @@ class RocShim:
         p = os.path.join(self.state_dir, kind, obj.id + ".json")
         tmp = p + ".tmp"
         with open(tmp, "w") as f:
-            json.dump(obj.to_json(), f)
+            f.write(json.dumps(obj.to_json(), separators=(",", ":")))   # one-shot C encoder (json.dump is pure Python)
         os.replace(tmp, p)
 
     def _unckpt(self, kind: str, oid: str):

@@ -24,7 +24,9 @@ async def profile_handler(request: web.Request) -> web.Response:
     finally:
         pr.disable()
     out = io.StringIO()
-    pstats.Stats(pr, stream=out).sort_stats("cumulative").print_stats(60)
+    sort = request.query.get("sort", "cumulative")
+    pstats.Stats(pr, stream=out).sort_stats(sort if sort in ("cumulative", "tottime", "ncalls") else "cumulative").print_stats(
+        int(request.query.get("lines", "60")))
     return web.Response(text=out.getvalue())
 
 
