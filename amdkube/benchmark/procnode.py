@@ -34,9 +34,21 @@ class _Backend:
         self.name = name
 
 
+class _SchedulerStats:
+    """Stand-in for the in-process Scheduler's counters when it runs as its own process."""
+    scheduled = bind_errors = 0
+
+    def __init__(self, client):
+        self.client = client
+
+    async def stop(self):
+        pass
+
+
 class ProcessNode:
     def __init__(self, backend: str = "auto", n_gpus: int | None = None, node_name: str = "mi355x-node-0",
-                 relist_period: float = 1.0, health_probe: str = "none"):
+                 relist_period: float = 1.0, health_probe: str = "none", scheduler_process: bool = True):
+        self.scheduler_process = scheduler_process
         self.backend_name, self.n_gpus, self.node_name = backend, n_gpus, node_name
         self.relist_period, self.health_probe = relist_period, health_probe
         self.base = tempfile.mkdtemp(prefix="ak-proc-", dir="/tmp")
@@ -58,7 +70,11 @@ class ProcessNode:
         b = self.base
         self.api = await APIServer().start()
         self.client = Client(self.api.url, token=self.api.loopback_token, pool=256)
-        self.scheduler = await Scheduler(Client(self.api.url, token=self.api.loopback_token, pool=256)).start()
+        if self.scheduler_process:
+            self._spawn("scheduler", ["scheduler", "--server", self.api.url, "--token", self.api.loopback_token, "--port", "0"])
+            self.scheduler = _SchedulerStats(self.client)
+        else:
+            self.scheduler = await Scheduler(Client(self.api.url, token=self.api.loopback_token, pool=256)).start()
         sock = os.path.join(b, "rocshim.sock")
         plugins = os.path.join(b, "plugins")
         self._spawn("rocshim", ["rocshim", "--listen", sock, "--state-dir", os.path.join(b, "rocshim"),

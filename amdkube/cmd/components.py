@@ -104,6 +104,7 @@ def scheduler(argv):
     ap = argparse.ArgumentParser("amdkube scheduler")
     ap.add_argument("--master", "--server", dest="server", default="http://127.0.0.1:8080")
     ap.add_argument("--kubeconfig", default=None, help="kubeconfig with the server, CA and credentials")
+    ap.add_argument("--token", default=None, help="bearer token for the apiserver")
     ap.add_argument("--policy-config-file", default=None)
     ap.add_argument("--algorithm-provider", default="DefaultProvider")
     ap.add_argument("--scheduler-name", default="default-scheduler")
@@ -128,6 +129,7 @@ def controller_manager(argv):
     ap = argparse.ArgumentParser("amdkube controller-manager")
     ap.add_argument("--master", "--server", dest="server", default="http://127.0.0.1:8080")
     ap.add_argument("--kubeconfig", default=None, help="kubeconfig with the server, CA and credentials")
+    ap.add_argument("--token", default=None, help="bearer token for the apiserver")
     ap.add_argument("--controllers", default="*", help="'*' = defaults; 'name' enables, '-name' disables")
     ap.add_argument("--leader-elect", default="false")
     ap.add_argument("--node-monitor-grace-period", type=float, default=40.0)
@@ -177,6 +179,7 @@ def kubelet(argv):
     ap = argparse.ArgumentParser("amdkube kubelet")
     ap.add_argument("--api-servers", "--server", dest="server", default="http://127.0.0.1:8080")
     ap.add_argument("--kubeconfig", default=None, help="kubeconfig with the server, CA and credentials")
+    ap.add_argument("--token", default=None, help="bearer token for the apiserver")
     ap.add_argument("--hostname-override", "--node-name", dest="node_name", default=socket.gethostname())
     ap.add_argument("--root-dir", default="/var/lib/kubelet")
     ap.add_argument("--device-plugin-dir", default=None)
@@ -194,7 +197,6 @@ def kubelet(argv):
     ap.add_argument("--chaos-chance", type=float, default=0.0)
     ap.add_argument("--pod-manifest-path", default=None, help="directory of static pod manifests")
     ap.add_argument("--file-check-frequency", type=float, default=20.0)
-    ap.add_argument("--token", default=None, help="bearer token for the apiserver (e.g. from TLS bootstrap)")
     ap.add_argument("--gpu-stats-backend", default="auto")
     ap.add_argument("--kube-api-qps", type=float, default=0)
     ap.add_argument("-v", type=int, default=0)
@@ -346,6 +348,7 @@ def proxy(argv):
     ap = argparse.ArgumentParser("amdkube proxy")
     ap.add_argument("--master", "--server", dest="server", default="http://127.0.0.1:8080")
     ap.add_argument("--kubeconfig", default=None, help="kubeconfig with the server, CA and credentials")
+    ap.add_argument("--token", default=None, help="bearer token for the apiserver")
     ap.add_argument("--proxy-mode", default="userspace", choices=("userspace", "iptables"))
     ap.add_argument("--bind-address", default="0.0.0.0", help="node address NodePorts listen on")
     ap.add_argument("--cluster-cidr", default="")

@@ -3,6 +3,7 @@ remote_image.go): typed async wrappers over the RuntimeService/ImageService stub
 per-call timeouts and operation metrics (kubelet_runtime_operations{operation_type})."""
 from __future__ import annotations
 
+import contextvars
 import time
 
 import grpc
@@ -10,9 +11,14 @@ import grpc
 from ..grpcdesc.cri import CRI as C
 from ..utils.grpcutil import uds_channel
 
+# the pod a kubelet pod worker is syncing (set once per worker task; asyncio copies it into
+# every await chain the worker starts)
+CURRENT_POD: contextvars.ContextVar[str | None] = contextvars.ContextVar("amdkube_current_pod", default=None)
+
 
 class CRIClient:
     def __init__(self, socket_path: str, timeout: float = 10.0, metrics=None):
+        self._pod_mut: dict[str, int] = {}
         self.socket = socket_path
         self.timeout = timeout
         self.ch = None
@@ -35,10 +41,21 @@ class CRIClient:
                            "stop_container", "remove_container"))
     mutations = 0  # mutating RPCs issued (invalidates the kubelet's runtime-status cache)
 
+    def pod_mutations(self, uid: str) -> int:
+        """Mutating RPCs issued on behalf of one pod: its cached runtime status stays valid across
+        other pods' container starts (a global counter made 30 concurrent pods refetch ~6× each)."""
+        return self._pod_mut.get(uid, 0)
+
+    def forget_pod(self, uid: str):
+        self._pod_mut.pop(uid, None)
+
     async def _call(self, op, fn, req, timeout=None):
         t0 = time.perf_counter()
         if op in self._MUTATING:
             self.mutations += 1
+            uid = CURRENT_POD.get()
+            if uid is not None:
+                self._pod_mut[uid] = self._pod_mut.get(uid, 0) + 1
         try:
             return await fn(req, timeout=timeout or self.timeout)
         except grpc.RpcError:

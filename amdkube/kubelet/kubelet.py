@@ -38,7 +38,7 @@ from ..deviceplugin.amd import TOPOLOGY_LABEL
 from ..grpcdesc.cri import CRI as C
 from ..utils.features import FeatureGate
 from ..utils.metrics import MICRO_BUCKETS, Counter, Gauge, Histogram, Summary, new_registry
-from .cri_client import CRIClient
+from .cri_client import CURRENT_POD, CRIClient
 from .devicemanager import AdmissionError, ManagerImpl, ManagerStub
 from .kuberuntime import L_POD_UID, RuntimeManager
 from .status import StatusManager, generate_status
@@ -465,6 +465,7 @@ class Kubelet:
         w.pending.set()
 
     async def _worker_loop(self, w: PodWorker):
+        CURRENT_POD.set(w.uid)   # task-local: CRI mutations are attributed to this pod
         while True:
             await w.pending.wait()
             w.pending.clear()
@@ -546,8 +547,7 @@ class Kubelet:
         """Returns True when the worker for this pod is finished (pod gone from the node)."""
         pod = self.pods.get(uid)
         if pod is None:
-            await self.runtime.kill_pod(uid, 0)
-            await self.runtime.remove_pod(uid)
+            await self.runtime.kill_and_remove(uid)
             self._cleanup(uid)
             return True
         md = pod.get("metadata") or {}
@@ -558,7 +558,7 @@ class Kubelet:
         if uid not in self.admitted:
             if is_pod_terminal(pod):
                 self.admitted.add(uid)  # e.g. kubelet restart: nothing to run
-            elif await self._already_running(uid):
+            elif (m.parse_time(md.get("creationTimestamp")) or 0) < self.started_at - 1.0 and await self._already_running(uid):
                 # kubelet restart: the pod was admitted by the previous incarnation and is running;
                 # never kill it because a device plugin has not re-registered yet
                 self.admitted.add(uid)
@@ -585,9 +585,9 @@ class Kubelet:
             return False
         ctx = await self._pod_context(pod)
         rt = await self._cached_status(uid)
-        mut0 = self.cri.mutations
+        mut0 = self.cri.pod_mutations(uid)
         errors = await self.runtime.sync_pod(pod, rt, ctx, self.liveness_failed.pop(uid, None))
-        if self.cri.mutations != mut0 or errors:
+        if self.cri.pod_mutations(uid) != mut0 or errors:
             rt = await self._cached_status(uid, fresh=True)
         for sb in rt.sandboxes:
             self._sandbox_uid[sb[0]] = uid
@@ -633,7 +633,7 @@ class Kubelet:
         pass
 
     async def _cached_status(self, uid: str, fresh: bool = False):
-        key = (self._rt_gen.get(uid, 0), self.cri.mutations)
+        key = (self._rt_gen.get(uid, 0), self.cri.pod_mutations(uid))
         hit = self._rt_cache.get(uid)
         if not fresh and hit is not None and hit[0] == key:
             return hit[1]
@@ -648,6 +648,7 @@ class Kubelet:
     def _cleanup(self, uid):
         self._rt_gen.pop(uid, None)
         self._rt_cache.pop(uid, None)
+        self.cri.forget_pod(uid)
         self.admitted.discard(uid)
         self.rejected.pop(uid, None)
         self.status.forget(uid)

@@ -103,6 +103,7 @@ class RuntimeManager:
         self.backoff: dict[tuple[str, str], tuple[float, float]] = {}  # (uid, name) -> (until, last delay)
         self.sandbox_ips: dict[str, str] = {}   # sandbox id -> IP (PodSandboxStatus is asked once per sandbox)
         self.seccomp_root = os.path.join(root_dir, "seccomp")   # --seccomp-profile-root
+        self._image_seen: dict[str, float] = {}
 
     # ----------------------------------------------------------------- status
     async def pod_status(self, uid: str, sandboxes=None) -> PodRuntimeStatus:
@@ -155,7 +156,11 @@ class RuntimeManager:
     async def ensure_image(self, c: dict):
         image = c["image"]
         policy = c.get("imagePullPolicy", "IfNotPresent")
+        if policy != "Always" and self._image_seen.get(image, 0.0) > time.monotonic():
+            return   # present a moment ago (image GC runs on minutes, not per pod)
         present = await self.cri.image_status(image)
+        if present is not None:
+            self._image_seen[image] = time.monotonic() + 30.0
         if policy == "Never" and present is None:
             raise RuntimeError(f"ErrImageNeverPull: image {image} not present with pull policy Never")
         if present is None or policy == "Always":
@@ -283,14 +288,26 @@ class RuntimeManager:
         until, _ = self.backoff.get((uid, name), (0.0, 0.0))
         return max(0.0, until - time.monotonic())
 
-    async def kill_pod(self, uid: str, grace: int = 30, pod: dict | None = None):
-        sbs = await self.cri.list_pod_sandbox(uid)
+    async def kill_pod(self, uid: str, grace: int = 30, pod: dict | None = None, sandboxes=None):
+        sbs = sandboxes if sandboxes is not None else await self.cri.list_pod_sandbox(uid)
+        hooks = pod is not None and any(((sc.get("lifecycle") or {}).get("preStop"))
+                                        for sc in (pod.get("spec") or {}).get("containers") or [])
         for s in sbs:
-            conts = await self.cri.list_containers(s.id)
-            await asyncio.gather(*(self._kill_container(pod, c, grace) for c in conts if c.state == C.CONTAINER_RUNNING))
+            if s.state != C.SANDBOX_READY:
+                continue   # already stopped: its containers are gone with it
+            if grace or hooks:
+                conts = await self.cri.list_containers(s.id)
+                await asyncio.gather(*(self._kill_container(pod, c, grace) for c in conts if c.state == C.CONTAINER_RUNNING))
+            # grace 0 and no preStop hook: StopPodSandbox kills the containers itself (one RPC, not 2 + N)
             await self.cri.stop_pod_sandbox(s.id)
         for k in [k for k in self.backoff if k[0] == uid]:
             del self.backoff[k]
+
+    async def kill_and_remove(self, uid: str):
+        """The pod is gone from the API: one list, stop what still runs, remove everything."""
+        sbs = await self.cri.list_pod_sandbox(uid)
+        await self.kill_pod(uid, 0, None, sbs)
+        await self.remove_pod(uid, sbs)
 
     async def _kill_container(self, pod, c, grace):
         if pod is not None:
@@ -304,7 +321,7 @@ class RuntimeManager:
                             pass
         await self.cri.stop_container(c.id, grace)
 
-    async def remove_pod(self, uid: str):
-        for s in await self.cri.list_pod_sandbox(uid):
+    async def remove_pod(self, uid: str, sandboxes=None):
+        for s in sandboxes if sandboxes is not None else await self.cri.list_pod_sandbox(uid):
             await self.cri.remove_pod_sandbox(s.id)
             self.sandbox_ips.pop(s.id, None)
