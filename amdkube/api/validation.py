@@ -72,7 +72,8 @@ def validate_resource_requirements(res: dict | None, path: str) -> list[str]:
         if k in lim:
             if Quantity(v) > Quantity(lim[k]):
                 errs.append(f"{path}.requests[{k}]: Invalid value: {v!r}: must be less than or equal to {k} limit")
-            if is_extended_resource_name(k) and Quantity(v) != Quantity(lim[k]):
+            if (is_extended_resource_name(k) or k == "alpha.kubernetes.io/amd-gpu") and Quantity(v) != Quantity(lim[k]):
+                # extended resources and the legacy GPU resource (validation.go:4448-4449) cannot overcommit
                 errs.append(f"{path}.requests[{k}]: Invalid value: {v!r}: must be equal to {k} limit")
         elif is_extended_resource_name(k):
             errs.append(f"{path}.limits[{k}]: Required value: Limit must be set for non overcommitable resources")

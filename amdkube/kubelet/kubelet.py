@@ -116,6 +116,11 @@ class Kubelet:
             self.dm = ManagerStub()
         self.recorder = EventRecorder(client, "kubelet", self.node_name)
         self.runtime = RuntimeManager(self.cri, self.dm, config.root_dir, self.recorder)
+        self.gpu_legacy = None
+        if self.gates("Accelerators"):   # legacy whole-GPU path (kubelet.go:907-919), alpha
+            from .gpu_legacy import AMDGPUManager
+            self.gpu_legacy = AMDGPUManager(smi_backend).start()
+            self.runtime.legacy, self.runtime.active_pods = self.gpu_legacy, self.active_pods
         self.status = StatusManager(client, on_terminal=self._on_terminal)
         self.node: dict | None = None
         self.informer: Informer | None = None
@@ -157,6 +162,9 @@ class Kubelet:
     async def start(self):
         os.makedirs(os.path.join(self.cfg.root_dir, "pods"), exist_ok=True)
         await self.cri.connect()
+        if self.gpu_legacy is not None:   # in-use GPUs survive a kubelet restart (the reference inspects docker)
+            self.gpu_legacy.rebuild([(c.labels.get(L_POD_UID, ""), c.metadata.name, dict(c.annotations))
+                                     for c in await self.cri.list_containers() if c.state == C.CONTAINER_RUNNING])
         await self.dm.start()
         self.recorder.start()
         self.status.start()
@@ -219,7 +227,11 @@ class Kubelet:
         import psutil
         cpu = self.cfg.cpu_capacity or psutil.cpu_count() or 1
         mem = self.cfg.memory_capacity or psutil.virtual_memory().total
-        return {"cpu": str(cpu), "memory": f"{mem // 1024}Ki", "pods": str(self.cfg.max_pods)}
+        cap = {"cpu": str(cpu), "memory": f"{mem // 1024}Ki", "pods": str(self.cfg.max_pods)}
+        if self.gpu_legacy is not None:   # kubelet_node_status.go:557-562
+            from .gpu_legacy import RESOURCE
+            cap[RESOURCE] = str(self.gpu_legacy.capacity())
+        return cap
 
     async def register_node(self):
         labels = {"kubernetes.io/hostname": self.node_name, "beta.kubernetes.io/os": "linux",
@@ -649,6 +661,8 @@ class Kubelet:
         self._rt_gen.pop(uid, None)
         self._rt_cache.pop(uid, None)
         self.cri.forget_pod(uid)
+        if self.gpu_legacy is not None:
+            self.gpu_legacy.release(uid)
         self.admitted.discard(uid)
         self.rejected.pop(uid, None)
         self.status.forget(uid)

@@ -104,6 +104,8 @@ class RuntimeManager:
         self.sandbox_ips: dict[str, str] = {}   # sandbox id -> IP (PodSandboxStatus is asked once per sandbox)
         self.seccomp_root = os.path.join(root_dir, "seccomp")   # --seccomp-profile-root
         self._image_seen: dict[str, float] = {}
+        self.legacy = None          # gpu_legacy.AMDGPUManager when the Accelerators gate is on
+        self.active_pods = None
 
     # ----------------------------------------------------------------- status
     async def pod_status(self, uid: str, sandboxes=None) -> PodRuntimeStatus:
@@ -173,6 +175,11 @@ class RuntimeManager:
     async def start_container(self, pod: dict, c: dict, sid: str, sandbox_cfg, ctx: dict, restart_count: int, init: bool):
         await self.ensure_image(c)
         opts = await self.dm.init_container(pod, c)
+        if self.legacy is not None:   # Accelerators gate: kubelet_pods.go:486-490 AllocateGPU
+            la = self.legacy.allocate(pod, c, self.active_pods() if self.active_pods else [])
+            if la["devices"]:
+                opts = dict(opts, devices=list(opts["devices"]) + [d for d in la["devices"] if d not in opts["devices"]],
+                            envs={**opts["envs"], **la["envs"]}, annotations={**opts["annotations"], **la["annotations"]})
         envs = [C.KeyValue(key=k, value=v) for k, v in (ctx.get("env", {}).get(c["name"]) or {}).items()]
         envs += [C.KeyValue(key=k, value=v) for k, v in opts["envs"].items()]
         mounts = [C.Mount(container_path=m["container_path"], host_path=m["host_path"], readonly=bool(m.get("read_only")))

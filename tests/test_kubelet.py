@@ -151,3 +151,84 @@ def test_kubelet_http_api_and_metrics():
                 logs = await (await s.get(base + "/containerLogs/default/s/c")).text()
                 assert logs.strip().startswith("GPU-")
     run(go(), 60)
+
+
+def test_legacy_accelerators_gate_whole_gpu_allocation():
+    """Accelerators gate (reference pkg/kubelet/gpu/nvidia/nvidia_gpu_manager_test.go):
+    alpha.kubernetes.io/amd-gpu capacity from the render nodes, disjoint whole-GPU allocation,
+    the shared /dev/kfd control node, request == limit validation, release on deletion."""
+    import asyncio
+    from amdkube.api import meta as m
+    from amdkube.kubelet.gpu_legacy import ANNOTATION, RESOURCE
+    from amdkube.localcluster import LocalCluster, wait_pod
+
+    def pod(name, n):
+        return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name},
+                "spec": {"containers": [{"name": "c", "image": "amdkube/pause:3.1",
+                                         "resources": {"limits": {RESOURCE: str(n)}}}]}}
+
+    async def go():
+        async with LocalCluster(gpus="fake", relist_period=0.2, kubelet_kw={"feature_gates": "Accelerators=true"}) as lc:
+            c = lc.client
+            for _ in range(100):
+                node = await c.get("nodes", lc.node_name)
+                if node["status"]["allocatable"].get(RESOURCE) == "8":
+                    break
+                await asyncio.sleep(0.05)
+            assert node["status"]["capacity"][RESOURCE] == "8"
+            await c.create(pod("a", 4), "default")
+            await c.create(pod("b", 4), "default")
+            for n in ("a", "b"):
+                await wait_pod(c, "default", n, ("Running",), 20)
+            devs = {}
+            for ct in lc.shim.containers.values():
+                paths = [d["host_path"] for d in ct.devices]
+                assert any(p.endswith("/kfd") for p in paths)
+                devs[ct.annotations.get("io.kubernetes.pod.name", ct.id)] = {p for p in paths if "renderD" in p}
+                assert ct.annotations.get(ANNOTATION)
+            sets = list(devs.values())
+            assert len(sets) == 2 and all(len(s) == 4 for s in sets) and not (sets[0] & sets[1])
+            # no GPUs left: the scheduler keeps the third pod pending
+            await c.create(pod("c", 1), "default")
+            await asyncio.sleep(0.5)
+            assert (await c.get("pods", "c", "default"))["status"]["phase"] == "Pending"
+            bad = pod("d", 1)
+            bad["spec"]["containers"][0]["resources"]["requests"] = {RESOURCE: "2"}
+            try:
+                await c.create(bad, "default")
+                raise AssertionError("request != limit must be rejected")
+            except m.StatusError as e:
+                assert e.code == 422
+            # deleting a pod frees its GPUs for the pending one
+            await c.delete("pods", "a", "default", grace=0)
+            await wait_pod(c, "default", "c", ("Running",), 20)
+
+    from tests.conftest import run
+    run(go(), 90)
+
+
+def test_legacy_gpu_manager_rebuild_after_restart():
+    """In-use state comes back from running containers' annotations (reference
+    nvidia_gpu_manager.go updateAllocatedGPUs), and terminated pods free their GPUs."""
+    from amdkube.kubelet.gpu_legacy import ANNOTATION, RESOURCE, AMDGPUManager, LegacyGPUError
+
+    class Smi:
+        def gpus(self):
+            return [{"render_minor": 128 + i, "uuid": f"GPU-{i}"} for i in range(4)]
+
+    g = AMDGPUManager(Smi()).start()
+    assert g.capacity() == 4
+    g.rebuild([("u1", "c", {ANNOTATION: "/dev/dri/renderD128,/dev/dri/renderD129"})])
+    pod = lambda uid, phase="Running": {"metadata": {"uid": uid, "name": uid}, "status": {"phase": phase}}
+    ctr = {"name": "c", "resources": {"limits": {RESOURCE: "2"}}}
+    a = g.allocate(pod("u2"), ctr, [pod("u1"), pod("u2")])
+    assert a["annotations"][ANNOTATION] == "/dev/dri/renderD130,/dev/dri/renderD131"
+    assert a["envs"]["ROCR_VISIBLE_DEVICES"] and a["devices"][0]["host_path"] == "/dev/kfd"
+    assert g.allocate(pod("u2"), ctr, [pod("u1"), pod("u2")]) == a      # idempotent on restart
+    try:
+        g.allocate(pod("u3"), ctr, [pod("u1"), pod("u2"), pod("u3")])
+        raise AssertionError("over-allocation")
+    except LegacyGPUError:
+        pass
+    b = g.allocate(pod("u3"), ctr, [pod("u1", "Succeeded"), pod("u2"), pod("u3")])
+    assert b["annotations"][ANNOTATION] == "/dev/dri/renderD128,/dev/dri/renderD129"
