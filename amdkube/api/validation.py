@@ -260,6 +260,10 @@ def _strip_mutable(spec: dict) -> dict:
 def validate_pod(pod: dict, old: dict | None = None) -> list[str]:
     errs = validate_object_meta(pod, True)
     errs += validate_pod_spec(pod.get("spec") or {})
+    from ..security import validate_seccomp_annotations
+    from ..security.apparmor import validate_pod_annotations
+    errs += validate_seccomp_annotations((pod.get("metadata") or {}).get("annotations"))
+    errs += validate_pod_annotations(pod)
     if old is not None:
         if _strip_mutable(pod.get("spec") or {}) != _strip_mutable(old.get("spec") or {}):
             errs.append("spec: Forbidden: pod updates may not change fields other than `spec.containers[*].image`, "

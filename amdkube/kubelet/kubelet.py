@@ -77,6 +77,7 @@ class KubeletConfig:
     memory_capacity: int | None = None
     pod_manifest_path: str | None = None            # static pods (--pod-manifest-path)
     file_check_frequency: float = 20.0              # kubeletconfig FileCheckFrequency
+    apparmor_fs: str | None = None                  # securityfs apparmor dir (None: discover from /proc/mounts)
 
 
 class PodWorker:
@@ -121,6 +122,8 @@ class Kubelet:
             from .gpu_legacy import AMDGPUManager
             self.gpu_legacy = AMDGPUManager(smi_backend).start()
             self.runtime.legacy, self.runtime.active_pods = self.gpu_legacy, self.active_pods
+        from ..security.apparmor import Validator as AppArmorValidator
+        self.apparmor = AppArmorValidator(self.gates("AppArmor"), apparmor_fs=config.apparmor_fs)
         self.status = StatusManager(client, on_terminal=self._on_terminal)
         self.node: dict | None = None
         self.informer: Informer | None = None
@@ -531,6 +534,9 @@ class Kubelet:
                                        ("NoExecute",))
         if taint:
             return False, "Taint", f"pod does not tolerate taint {taint.get('key')}={taint.get('value', '')}:NoExecute"
+        err = self.apparmor.validate(pod)   # lifecycle/handlers.go:142-165
+        if err:
+            return False, "AppArmor", f"Cannot enforce AppArmor: {err}"
         return True, "", ""
 
     async def _admit(self, pod: dict) -> bool:

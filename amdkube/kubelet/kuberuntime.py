@@ -20,6 +20,7 @@ import time
 
 import grpc
 
+from ..security.apparmor import profile_name as apparmor_profile_name
 from ..grpcdesc.cri import CRI as C
 from .cri_client import CRIClient
 
@@ -206,6 +207,7 @@ class RuntimeManager:
             annotations=ann, log_path=f"{c['name']}/{restart_count}.log",
             linux=C.LinuxContainerConfig(resources=lres, security_context=C.LinuxContainerSecurityContext(
                 seccomp_profile_path=seccomp_profile(pod, c["name"], self.seccomp_root),
+                apparmor_profile=apparmor_profile_name(pod, c["name"]),     # security_context.go:40
                 no_new_privs=not bool(((c.get("securityContext") or {}).get("allowPrivilegeEscalation", True))))))
         cid = await self.cri.create_container(sid, cfg, sandbox_cfg)
         await self.cri.start_container(cid)

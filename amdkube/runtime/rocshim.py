@@ -325,6 +325,11 @@ class RocShim:
         sec = cfg.linux.security_context.seccomp_profile_path if cfg.HasField("linux") else ""
         if sec:
             resources["seccomp_profile"] = self._seccomp_file(sec)
+        aa = cfg.linux.security_context.apparmor_profile if cfg.HasField("linux") else ""
+        if aa.startswith("localhost/"):   # runtime/default and unconfined: no transition
+            resources["apparmor_profile"] = aa[len("localhost/"):]
+        elif aa not in ("", "runtime/default", "unconfined"):
+            raise ValueError(f"unsupported AppArmor profile {aa!r}")
         c = Container(cid, sid, cfg.metadata.name, cfg.metadata.attempt, cfg.image.image, self.images.image_id(iname), argv,
                       env, cwd, log_path, dict(cfg.labels), dict(cfg.annotations), mounts, devices, handler, resources)
         self.containers[cid] = c
@@ -345,14 +350,19 @@ class RocShim:
         raise ValueError(f"unsupported seccomp profile {spec!r}")
 
     def _launch_argv(self, c: Container) -> list[str]:
-        sec = c.resources.get("seccomp_profile")
+        sec, aa = c.resources.get("seccomp_profile"), c.resources.get("apparmor_profile")
         if self.isolation != "namespaces":
-            return [self.nsexec_bin, "--no-namespaces", "--seccomp", sec, "--"] + c.argv if sec else c.argv
+            if not (sec or aa):
+                return c.argv
+            return ([self.nsexec_bin, "--no-namespaces"] + (["--seccomp", sec] if sec else []) +
+                    (["--apparmor", aa] if aa else []) + ["--"] + c.argv)
         keep = [d["host_path"] for d in c.devices if "/dri/" in d["host_path"]]
         cg = os.path.join(self.cgroup_root, c.sandbox_id, c.id)
         a = [self.nsexec_bin, "--dev-root", self.dev_root, "--cgroup", cg]
         if sec:
             a += ["--seccomp", sec]
+        if aa:
+            a += ["--apparmor", aa]
         for k in keep:
             a += ["--keep", k]
         if c.resources.get("memory_limit"):

@@ -13,7 +13,26 @@ KNOWN = {
     "GPUTopologyScheduling": (True, "Beta"),     # amdkube: xGMI/NUMA-aware device scoring
     "ReserveDevicesOnAssume": (True, "Beta"),    # amdkube: SURVEY §7.6 #1 fix
     "DeviceHealthFiltering": (True, "Beta"),     # amdkube: SURVEY §7.6 #6 fix
+    "AppArmor": (True, "Beta"),                  # kubelet admit + CRI apparmor_profile (amdkube/security/apparmor.py)
 }
+# the rest of the reference's gate names (kube_features.go:196-240), accepted so a reference
+# flag line parses; the behaviour they switch is either always on here or not applicable
+for _name, _spec in {
+    "ExternalTrafficLocalOnly": (True, "GA"), "DynamicKubeletConfig": (False, "Alpha"), "KubeletConfigFile": (False, "Alpha"),
+    "ExperimentalHostUserNamespaceDefaulting": (False, "Beta"), "ExperimentalCriticalPodAnnotation": (False, "Alpha"),
+    "TaintBasedEvictions": (False, "Alpha"), "RotateKubeletServerCertificate": (False, "Alpha"),
+    "RotateKubeletClientCertificate": (True, "Beta"), "PersistentLocalVolumes": (False, "Alpha"),
+    "LocalStorageCapacityIsolation": (False, "Alpha"), "HugePages": (False, "Alpha"), "DebugContainers": (False, "Alpha"),
+    "EnableEquivalenceClassCache": (False, "Alpha"), "MountPropagation": (False, "Alpha"),
+    "ExpandPersistentVolumes": (False, "Alpha"), "CPUManager": (False, "Alpha"), "ServiceNodeExclusion": (False, "Alpha"),
+    "MountContainers": (False, "Alpha"), "VolumeScheduling": (False, "Alpha"), "CSIPersistentVolume": (False, "Alpha"),
+    "CustomPodDNS": (False, "Alpha"), "BlockVolume": (False, "Alpha"), "PVCProtection": (False, "Alpha"),
+    "ResourceLimitsPriorityFunction": (False, "Alpha"), "SupportIPVSProxyMode": (False, "Beta"), "VolumeSubpath": (True, "GA"),
+    "StreamingProxyRedirects": (True, "Beta"), "AdvancedAuditing": (True, "Beta"), "APIResponseCompression": (False, "Alpha"),
+    "Initializers": (False, "Alpha"), "APIListChunking": (True, "Beta"), "CustomResourceValidation": (True, "Beta"),
+    "ServiceProxyAllowExternalIPs": (False, "Deprecated"), "ReadOnlyAPIDataVolumes": (True, "Deprecated"),
+}.items():
+    KNOWN.setdefault(_name, _spec)
 
 
 class FeatureGate:
