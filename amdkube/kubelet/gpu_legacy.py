@@ -88,7 +88,8 @@ class AMDGPUManager:
             self.allocated[(uid, cname)] = have
         devs = [{"container_path": f"{self.dev_root}/kfd", "host_path": f"{self.dev_root}/kfd", "permissions": "rw"}]
         devs += [{"container_path": p, "host_path": p, "permissions": "rw"} for p in have]
-        toks = [visibility_token(self.gpus[p]) for p in have if self.gpus[p].get("uuid")]
+        toks = [visibility_token(g) for g in map(self.gpus.get, have)
+                if g.get("hip_uuid") or g.get("uuid") or "hip_id" in g]   # /dev/dri scans carry no identity
         envs = {"ROCR_VISIBLE_DEVICES": ",".join(toks)} if len(toks) == len(have) else {}
         return {"devices": devs, "envs": envs, "annotations": {ANNOTATION: ",".join(have)}}
 

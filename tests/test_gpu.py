@@ -70,6 +70,33 @@ def test_02_gpu_pod_runs_on_its_assigned_device():
     run(go(), 300)
 
 
+def test_02b_legacy_accelerators_pod_on_real_gpu():
+    """Accelerators gate (F22): alpha.kubernetes.io/amd-gpu from the real render nodes; the pod
+    gets /dev/kfd + its render node + ROCR_VISIBLE_DEVICES and vector-add passes."""
+    from amdkube.kubelet.gpu_legacy import ANNOTATION, RESOURCE
+
+    async def go():
+        async with LocalCluster(gpus="amdsmi", n_gpus=1, relist_period=0.5, with_controllers=False,
+                                kubelet_kw={"feature_gates": "Accelerators=true"}) as lc:
+            node = await lc.wait_gpus(1, 60)
+            for _ in range(100):
+                node = await lc.client.get("nodes", lc.node_name)
+                if int(node["status"]["allocatable"].get(RESOURCE, "0")) >= 1:
+                    break
+                await asyncio.sleep(0.1)
+            assert int(node["status"]["capacity"][RESOURCE]) >= 1
+            pod = vadd_pod("legacy")
+            pod["spec"]["containers"][0]["resources"] = {"limits": {RESOURCE: "1"}}
+            await lc.client.create(pod)
+            p = await wait_pod(lc.client, "default", "legacy", ("Succeeded", "Failed"), 120)
+            logs = await lc.client.logs("default", "legacy")
+            assert p["status"]["phase"] == "Succeeded" and "Test PASSED" in logs, (p["status"], logs)
+            [ct] = [c for c in lc.shim.containers.values() if c.annotations.get(ANNOTATION)]
+            assert any(d["host_path"].endswith("/kfd") for d in ct.devices)
+            assert ct.env.get("ROCR_VISIBLE_DEVICES")
+    run(go(), 300)
+
+
 def test_03_plugin_hbm_health_probe_marks_healthy():
     async def go():
         async with LocalCluster(gpus="amdsmi", n_gpus=1, with_controllers=False, health_probe="hbm") as lc:
