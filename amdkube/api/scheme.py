@@ -111,7 +111,7 @@ _CORE = [
 _APPS = [
     ("DaemonSet", "daemonsets", True, ("ds",), ("status",)),
     ("ReplicaSet", "replicasets", True, ("rs",), ("status", "scale")),
-    ("Deployment", "deployments", True, ("deploy",), ("status", "scale")),
+    ("Deployment", "deployments", True, ("deploy",), ("status", "scale", "rollback")),
     ("StatefulSet", "statefulsets", True, ("sts",), ("status", "scale")),
     ("ControllerRevision", "controllerrevisions", True, (), ()),
 ]
@@ -126,7 +126,9 @@ _RBAC = [("Role", "roles", True, (), ()), ("ClusterRole", "clusterroles", False,
          ("RoleBinding", "rolebindings", True, (), ()), ("ClusterRoleBinding", "clusterrolebindings", False, (), ())]
 _STORAGE = [("StorageClass", "storageclasses", False, ("sc",), ())]
 _STORAGE_BETA = [("VolumeAttachment", "volumeattachments", False, (), ("status",))]
-_AUTHZ = [("SubjectAccessReview", "subjectaccessreviews", False, (), ())]
+_AUTHZ = [("SubjectAccessReview", "subjectaccessreviews", False, (), ()),
+          ("SelfSubjectAccessReview", "selfsubjectaccessreviews", False, (), ()),
+          ("LocalSubjectAccessReview", "localsubjectaccessreviews", True, (), ())]
 _AUTHN = [("TokenReview", "tokenreviews", False, (), ())]
 
 for group, version, table in (("", "v1", _CORE), ("apps", "v1", _APPS), ("batch", "v1", _BATCH),

@@ -37,6 +37,19 @@ log = logging.getLogger("amdkube.apiserver")
 _JSON = "application/json"
 
 
+def _to_scale(obj: dict) -> dict:
+    """autoscaling/v1 Scale view of a scalable object (registry/*/storage ScaleREST)."""
+    from ..api.labels import selector_from_label_selector, selector_from_set
+    md, spec = obj.get("metadata") or {}, obj.get("spec") or {}
+    sel = spec.get("selector") or {}
+    sel_str = str(selector_from_label_selector(sel) if "matchLabels" in sel or "matchExpressions" in sel
+                  else selector_from_set(sel))
+    return {"kind": "Scale", "apiVersion": "autoscaling/v1",
+            "metadata": {k: md[k] for k in ("name", "namespace", "uid", "resourceVersion", "creationTimestamp") if k in md},
+            "spec": {"replicas": int(spec.get("replicas", 1))},
+            "status": {"replicas": int((obj.get("status") or {}).get("replicas", 0)), "selector": sel_str}}
+
+
 def _resp(obj, status=200) -> web.Response:
     body = obj if isinstance(obj, (bytes, bytearray)) else json.dumps(obj, separators=(",", ":")).encode()
     return web.Response(body=body, status=status, content_type=_JSON)
@@ -226,7 +239,22 @@ class APIServer:
             raise m.forbidden(f'User "{user.get("name")}" cannot {verb} {what}{" " + repr(name) if name else ""}'
                               f'{" in API group " + repr(group) if group else ""}{where}')
 
-    def _review(self, plural, body):
+    def _set_scale(self, rs, ns, name, scale: dict, user) -> dict:
+        """PUT/PATCH .../scale: only spec.replicas changes; a resourceVersion in the Scale is a
+        precondition, as for the parent object."""
+        n = (scale.get("spec") or {}).get("replicas")
+        if not isinstance(n, int) or n < 0:
+            raise m.invalid("Scale", name, ["spec.replicas: Invalid value: must be a non-negative integer"])
+        rv = (scale.get("metadata") or {}).get("resourceVersion")
+        if rv:
+            cur = rs.get(ns, name)
+            if (cur.get("metadata") or {}).get("resourceVersion") != rv:
+                raise m.conflict(rs.ri.group_resource, name, "the object has been modified; please apply your changes to the latest version and try again")
+        obj, _ = rs.update(ns, name, None, user=user, patch=json.dumps({"spec": {"replicas": n}}).encode(),
+                           content_type="application/merge-patch+json")
+        return _to_scale(obj)
+
+    def _review(self, plural, body, requester=None, ns=""):
         """SubjectAccessReview / TokenReview (authorization.k8s.io, authentication.k8s.io): computed, not stored."""
         spec = body.get("spec") or {}
         if plural == "tokenreviews":
@@ -235,8 +263,13 @@ class APIServer:
             if u is not None:
                 st["user"] = {"username": u.get("name"), "uid": u.get("uid", ""), "groups": u.get("groups") or []}
         else:
-            user = {"name": spec.get("user", ""), "groups": spec.get("groups") or []}
+            if plural == "selfsubjectaccessreviews":   # the requester asks about itself
+                user = {"name": (requester or {}).get("name", ""), "groups": (requester or {}).get("groups") or []}
+            else:
+                user = {"name": spec.get("user", ""), "groups": spec.get("groups") or []}
             ra, nra = spec.get("resourceAttributes"), spec.get("nonResourceAttributes")
+            if plural == "localsubjectaccessreviews" and ra is not None:
+                ra = dict(ra, namespace=ns)   # pinned to the URL's namespace
             if ra:
                 a = Attributes(user, ra.get("verb", ""), ra.get("group", ""), ra.get("resource", ""), ra.get("subresource", ""),
                                ra.get("namespace", ""), ra.get("name", ""))
@@ -351,6 +384,8 @@ class APIServer:
             if name:
                 if sub and sub not in ("status", "scale"):
                     raise m.not_found("subresource", sub)
+                if sub == "scale":
+                    return _resp(_to_scale(rs.get(ns, name)))
                 raw = rs.storage.get_raw(rs.key(ns, name))
                 if raw is None:
                     raise m.not_found(ri.group_resource, name)
@@ -364,8 +399,17 @@ class APIServer:
             if name and sub == "eviction" and ri.plural == "pods":
                 self.registry.evict(ns, name, body, user)
                 return _resp(m.success_status(), 201)
-            if ri.plural in ("subjectaccessreviews", "tokenreviews"):
-                return _resp(self._review(ri.plural, body), 201)
+            if name and sub == "rollback" and ri.plural == "deployments":
+                # extensions/v1beta1 DeploymentRollback (registry/extensions/deployment/storage:
+                # RollbackREST): record spec.rollbackTo for the deployment controller
+                patch = {"spec": {"rollbackTo": body.get("rollbackTo") or {"revision": 0}}}
+                if body.get("updatedAnnotations"):
+                    patch["metadata"] = {"annotations": body["updatedAnnotations"]}
+                rs.update(ns, name, None, user=user, patch=json.dumps(patch).encode(),
+                          content_type="application/merge-patch+json")
+                return _resp(m.success_status({"name": name, "kind": "deployments"}), 201)
+            if ri.plural in ("subjectaccessreviews", "selfsubjectaccessreviews", "localsubjectaccessreviews", "tokenreviews"):
+                return _resp(self._review(ri.plural, body, user, ns), 201)
             if ri.plural == "pods" and sub == "" and name is None and body.get("kind") == "Binding":
                 return _resp(self.registry.bind(ns, body, user), 201)
             if name:
@@ -377,6 +421,8 @@ class APIServer:
             if not name:
                 raise m.method_not_allowed("PUT on a collection")
             body = await self._body(request)
+            if sub == "scale":
+                return _resp(self._set_scale(rs, ns, name, body, user))
             subr = "status" if sub in ("status", "approval") else ""
             if sub == "finalize" and ri.plural == "namespaces":
                 subr = "finalize"
@@ -387,6 +433,10 @@ class APIServer:
                 raise m.method_not_allowed("PATCH on a collection")
             data = await request.read()
             ct = request.headers.get("Content-Type", "application/merge-patch+json")
+            if sub == "scale":
+                from .registry import apply_patch
+                cur = _to_scale(rs.get(ns, name))
+                return _resp(self._set_scale(rs, ns, name, apply_patch(cur, data, ct), user))
             obj, _ = rs.update(ns, name, None, subresource=sub if sub == "status" else "", user=user, patch=data,
                                content_type=ct)
             return _resp(obj)

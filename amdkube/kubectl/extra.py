@@ -1,0 +1,633 @@
+"""kubectl commands beyond the core CRUD set.
+
+Reference: pkg/kubectl/cmd/cmd.go:216-330 command groups — rollout (rollout/rollout.go:
+status, history, undo, pause, resume), expose.go, autoscale.go, taint.go, set/set_image.go,
+replace.go, edit.go, config/ (view, current-context, use-context, get-contexts),
+auth/cani.go, certificates.go (approve/deny), portforward.go, proxy.go, cp.go, explain.go,
+create_*.go generators (namespace, configmap, secret generic, serviceaccount, deployment,
+job, priorityclass, quota, role/clusterrole/rolebinding/clusterrolebinding).
+
+Differences: `port-forward` dials the pod IP directly (pods here are reachable from the
+node; the reference tunnels through the kubelet's SPDY stream), and `cp` moves the file
+as base64 through the kubelet's exec endpoint (so it is bounded to 1 MiB).
+"""
+from __future__ import annotations
+
+import asyncio
+import base64
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+from ..api import meta as m
+from ..api.scheme import SCHEME, dump_yaml, load_manifests
+from . import printers
+
+REVISION = "deployment.kubernetes.io/revision"
+CHANGE_CAUSE = "kubernetes.io/change-cause"
+
+
+def _res(ri) -> str:
+    return ri.plural if not ri.group else f"{ri.plural}.{ri.group}"
+
+
+def _target(a, idx=0):
+    args = a.args[idx:]
+    if not args:
+        raise SystemExit("error: a resource is required")
+    if "/" in args[0]:
+        r, n = args[0].split("/", 1)
+        rest = args[1:]
+    else:
+        r, n, rest = args[0], (args[1] if len(args) > 1 else None), args[2:]
+    ri = SCHEME.resolve(r)
+    if ri is None:
+        raise SystemExit(f'error: the server doesn\'t have a resource type "{r}"')
+    return ri, n, rest
+
+
+def _ns(a, ri=None):
+    if ri is not None and not ri.namespaced:
+        return ""
+    return a.namespace or "default"
+
+
+# ------------------------------------------------------------------ rollout
+async def _owned_rs(c, d):
+    items, _ = await c.list("replicasets.apps", m.namespace_of(d))
+    uid = m.uid_of(d)
+    return [r for r in items if (m.controller_ref(r) or {}).get("uid") == uid]
+
+
+def _rev(o) -> int:
+    try:
+        return int(((o.get("metadata") or {}).get("annotations") or {}).get(REVISION, "0"))
+    except ValueError:
+        return 0
+
+
+async def cmd_rollout(c, a):
+    if not a.args:
+        raise SystemExit("error: rollout needs a subcommand: status|history|undo|pause|resume")
+    sub = a.args[0]
+    ri, name, _ = _target(a, 1)
+    ns = _ns(a, ri)
+    res = _res(ri)
+    if sub == "pause" or sub == "resume":
+        await c.patch(res, name, {"spec": {"paused": sub == "pause" or None}}, ns)
+        print(f"{ri.kind.lower()}/{name} {'paused' if sub == 'pause' else 'resumed'}")
+        return 0
+    if sub == "history":
+        d = await c.get(res, name, ns)
+        rows = [["REVISION", "CHANGE-CAUSE"]]
+        for r in sorted(await _owned_rs(c, d), key=_rev):
+            rows.append([str(_rev(r)), ((r.get("metadata") or {}).get("annotations") or {}).get(CHANGE_CAUSE, "<none>")])
+        print(f"{ri.kind.lower()}s \"{name}\"")
+        print(printers.table(rows))
+        return 0
+    if sub == "undo":
+        d = await c.get(res, name, ns)
+        rss = sorted(await _owned_rs(c, d), key=_rev)
+        want = a.to_revision
+        if want == 0:
+            if len(rss) < 2:
+                raise SystemExit("error: no rollout history found")
+            target = rss[-2]
+        else:
+            target = next((r for r in rss if _rev(r) == want), None)
+            if target is None:
+                raise SystemExit(f"error: unable to find specified revision {want} in history")
+        tpl = json.loads(json.dumps((target.get("spec") or {}).get("template") or {}))
+        ((tpl.get("metadata") or {}).get("labels") or {}).pop("pod-template-hash", None)
+        await c.patch(res, name, {"spec": {"template": tpl}}, ns)
+        print(f"{ri.kind.lower()}/{name} rolled back")
+        return 0
+    if sub == "status":
+        end = time.time() + a.timeout
+        while True:
+            d = await c.get(res, name, ns)
+            spec, st = d.get("spec") or {}, d.get("status") or {}
+            want = int(spec.get("replicas", 1))
+            if st.get("observedGeneration", 0) >= (d.get("metadata") or {}).get("generation", 1):
+                prog = next((x for x in st.get("conditions") or [] if x.get("type") == "Progressing"), None)
+                if prog and prog.get("reason") == "ProgressDeadlineExceeded":
+                    raise SystemExit(f'error: deployment "{name}" exceeded its progress deadline')
+                upd = int(st.get("updatedReplicas", 0))
+                if upd < want:
+                    msg = f"Waiting for rollout to finish: {upd} out of {want} new replicas have been updated..."
+                elif int(st.get("replicas", 0)) > upd:
+                    msg = f"Waiting for rollout to finish: {int(st['replicas']) - upd} old replicas are pending termination..."
+                elif int(st.get("availableReplicas", 0)) < upd:
+                    msg = f"Waiting for rollout to finish: {st.get('availableReplicas', 0)} of {upd} updated replicas are available..."
+                else:
+                    print(f'deployment "{name}" successfully rolled out')
+                    return 0
+            else:
+                msg = "Waiting for deployment spec update to be observed..."
+            if not a.watch_status or time.time() > end:
+                print(msg)
+                return 1
+            await asyncio.sleep(0.2)
+    raise SystemExit(f"error: unknown rollout subcommand {sub!r}")
+
+
+# ------------------------------------------------------------------ generators
+async def cmd_expose(c, a):
+    ri, name, _ = _target(a)
+    ns = _ns(a, ri)
+    obj = await c.get(_res(ri), name, ns)
+    spec = obj.get("spec") or {}
+    if ri.kind == "Pod":
+        sel = m.labels_of(obj)
+    elif ri.kind == "Service":
+        sel = spec.get("selector") or {}
+    else:
+        s = spec.get("selector") or {}
+        sel = s.get("matchLabels", s) if isinstance(s, dict) else {}
+        if isinstance(s, dict) and s.get("matchExpressions"):
+            raise SystemExit("error: cannot expose an object whose selector uses matchExpressions")
+    if not sel:
+        raise SystemExit("error: couldn't find a selector to expose")
+    port = a.port
+    if port is None:
+        ports = [p for ct in ((spec.get("template") or {}).get("spec") or spec).get("containers") or []
+                 for p in ct.get("ports") or []]
+        if not ports:
+            raise SystemExit("error: couldn't find port via --port flag or introspection")
+        port = ports[0]["containerPort"]
+    svc_type = a.type if a.type not in ("strategic", "merge", "json") else "ClusterIP"   # --type is shared with patch
+    svc = {"apiVersion": "v1", "kind": "Service",
+           "metadata": {"name": a.name or name, "labels": dict(sel)},
+           "spec": {"selector": dict(sel), "type": svc_type,
+                    "ports": [{"port": int(port), "protocol": a.protocol,
+                               "targetPort": int(a.target_port) if str(a.target_port or "").isdigit() else (a.target_port or int(port))}]}}
+    out = await c.create(svc, ns)
+    print(f"service/{m.name_of(out)} exposed")
+
+
+async def cmd_autoscale(c, a):
+    ri, name, _ = _target(a)
+    ns = _ns(a, ri)
+    await c.get(_res(ri), name, ns)
+    hpa = {"apiVersion": "autoscaling/v1", "kind": "HorizontalPodAutoscaler", "metadata": {"name": a.name or name},
+           "spec": {"scaleTargetRef": {"apiVersion": ri.api_version, "kind": ri.kind, "name": name},
+                    "maxReplicas": a.max, **({"minReplicas": a.min} if a.min else {}),
+                    **({"targetCPUUtilizationPercentage": a.cpu_percent} if a.cpu_percent >= 0 else {})}}
+    out = await c.create(hpa, ns)
+    print(f"horizontalpodautoscaler.autoscaling/{m.name_of(out)} autoscaled")
+
+
+def parse_taint(spec: str):
+    """`key=value:Effect` adds, `key:Effect-` / `key-` removes (taint.go parseTaints)."""
+    if spec.endswith("-"):
+        body = spec[:-1]
+        key, _, effect = body.partition(":")
+        return "remove", {"key": key, **({"effect": effect} if effect else {})}
+    kv, sep, effect = spec.partition(":")
+    if not sep or effect not in ("NoSchedule", "PreferNoSchedule", "NoExecute"):
+        raise SystemExit(f"error: invalid taint spec: {spec}")
+    key, _, value = kv.partition("=")
+    t = {"key": key, "effect": effect}
+    if value:
+        t["value"] = value
+    return "add", t
+
+
+async def cmd_taint(c, a):
+    if len(a.args) < 2:
+        raise SystemExit("error: taint NODE KEY[=VALUE]:EFFECT ...")
+    names = [x.split("/", 1)[-1] for x in a.args[:1]]
+    if a.args[0] in ("node", "nodes", "no"):
+        names, specs = [a.args[1]], a.args[2:]
+    else:
+        specs = a.args[1:]
+    for n in names:
+        node = await c.get("nodes", n)
+        taints = list((node.get("spec") or {}).get("taints") or [])
+        for sp in specs:
+            op, t = parse_taint(sp)
+            same = [x for x in taints if x["key"] == t["key"] and ("effect" not in t or x.get("effect") == t["effect"])]
+            if op == "remove":
+                if not same:
+                    raise SystemExit(f"error: taint {t['key']!r} not found")
+                taints = [x for x in taints if x not in same]
+            else:
+                if same and not a.overwrite:
+                    raise SystemExit(f"error: node {n} already has {t['key']} taint(s) with same effect(s) and --overwrite is false")
+                taints = [x for x in taints if x not in same] + [t]
+        await c.patch("nodes", n, {"spec": {"taints": taints or None}})
+        print(f"node/{n} tainted" if any(parse_taint(s)[0] == "add" for s in specs) else f"node/{n} untainted")
+
+
+async def cmd_set(c, a):
+    if not a.args or a.args[0] != "image":
+        raise SystemExit("error: supported: set image RESOURCE/NAME CONTAINER=IMAGE ...")
+    ri, name, rest = _target(a, 1)
+    ns = _ns(a, ri)
+    obj = await c.get(_res(ri), name, ns)
+    pairs = dict(x.split("=", 1) for x in rest)
+    podspec = ((obj.get("spec") or {}).get("template") or {}).get("spec") if ri.kind != "Pod" else obj.get("spec")
+    cs = []
+    for key in ("initContainers", "containers"):
+        for ct in (podspec or {}).get(key) or []:
+            if ct["name"] in pairs or "*" in pairs:
+                ct["image"] = pairs.get(ct["name"], pairs.get("*"))
+                cs.append(ct["name"])
+    missing = set(pairs) - set(cs) - {"*"}
+    if missing:
+        raise SystemExit(f"error: unable to find container named {sorted(missing)[0]!r}")
+    patch = {"spec": {"template": {"spec": podspec}}} if ri.kind != "Pod" else {"spec": podspec}
+    if a.record:
+        patch["metadata"] = {"annotations": {CHANGE_CAUSE: "kubectl set image " + " ".join(a.args[1:])}}
+    await c.patch(_res(ri), name, patch, ns)
+    print(f"{ri.kind.lower()}/{name} image updated")
+
+
+async def cmd_replace(c, a):
+    from .main import _read_files
+    for doc in _read_files(a.filename):
+        ri = SCHEME.for_object(doc)
+        ns = (m.namespace_of(doc) or a.namespace or "default") if ri.namespaced else ""
+        if a.force:
+            try:
+                await c.delete(_res(ri), m.name_of(doc), ns, grace=0)
+            except m.StatusError as e:
+                if not m.is_not_found(e):
+                    raise
+            for _ in range(100):
+                if await c.get_or_none(_res(ri), m.name_of(doc), ns) is None:
+                    break
+                await asyncio.sleep(0.05)
+            doc.get("metadata", {}).pop("resourceVersion", None)
+            await c.create(doc, ns)
+        else:
+            if ri.namespaced:
+                doc.setdefault("metadata", {})["namespace"] = ns
+            await c.update(doc)
+        print(f"{ri.kind.lower()}/{m.name_of(doc)} replaced")
+
+
+async def cmd_edit(c, a):
+    ri, name, _ = _target(a)
+    ns = _ns(a, ri)
+    obj = await c.get(_res(ri), name, ns)
+    editor = os.environ.get("KUBE_EDITOR") or os.environ.get("EDITOR") or "vi"
+    with tempfile.NamedTemporaryFile("w", suffix=".yaml", delete=False) as f:
+        f.write(dump_yaml(obj))
+        path = f.name
+    try:
+        rc = subprocess.call(editor.split() + [path])
+        if rc != 0:
+            raise SystemExit(f"error: editor exited with {rc}")
+        new = load_manifests(open(path).read())
+    finally:
+        os.unlink(path)
+    if not new or new[0] == obj:
+        print("Edit cancelled, no changes made.")
+        return 0
+    await c.update(new[0])
+    print(f"{ri.kind.lower()}/{name} edited")
+
+
+# ------------------------------------------------------------------ config / auth / certs
+def _kubeconfig_path(a):
+    return getattr(a, "kubeconfig", None) or os.environ.get("KUBECONFIG") or os.path.expanduser("~/.kube/config")
+
+
+def cmd_config_sync(a):
+    import yaml
+    path = _kubeconfig_path(a)
+    sub = a.args[0] if a.args else "view"
+    cfg = yaml.safe_load(open(path)) if os.path.exists(path) else {}
+    cfg = cfg or {}
+    if sub == "view":
+        view = json.loads(json.dumps(cfg))
+        if not a.raw:
+            for u in view.get("users") or []:
+                for k in ("client-key-data", "token", "client-certificate-data"):
+                    if k in (u.get("user") or {}):
+                        u["user"][k] = "REDACTED" if k != "client-certificate-data" else "REDACTED"
+        print(yaml.safe_dump(view, sort_keys=False), end="")
+    elif sub == "current-context":
+        cur = cfg.get("current-context")
+        if not cur:
+            raise SystemExit("error: current-context is not set")
+        print(cur)
+    elif sub == "get-contexts":
+        rows = [["CURRENT", "NAME", "CLUSTER", "AUTHINFO", "NAMESPACE"]]
+        for ctx in cfg.get("contexts") or []:
+            cc = ctx.get("context") or {}
+            rows.append(["*" if ctx.get("name") == cfg.get("current-context") else "", ctx.get("name", ""),
+                         cc.get("cluster", ""), cc.get("user", ""), cc.get("namespace", "")])
+        print(printers.table(rows))
+    elif sub == "use-context":
+        name = a.args[1]
+        if not any(x.get("name") == name for x in cfg.get("contexts") or []):
+            raise SystemExit(f"error: no context exists with the name: {name!r}")
+        cfg["current-context"] = name
+        with open(path, "w") as f:
+            yaml.safe_dump(cfg, f, sort_keys=False)
+        print(f'Switched to context "{name}".')
+    elif sub == "set-context":
+        name = a.args[1]
+        ctxs = cfg.setdefault("contexts", [])
+        ctx = next((x for x in ctxs if x.get("name") == name), None)
+        if ctx is None:
+            ctx = {"name": name, "context": {}}
+            ctxs.append(ctx)
+        for kv in a.args[2:]:
+            k, _, v = kv.lstrip("-").partition("=")
+            ctx["context"][k] = v
+        with open(path, "w") as f:
+            yaml.safe_dump(cfg, f, sort_keys=False)
+        print(f'Context "{name}" modified.')
+    else:
+        raise SystemExit(f"error: unknown config subcommand {sub!r}")
+    return 0
+
+
+async def cmd_auth(c, a):
+    if len(a.args) < 3 or a.args[0] != "can-i":
+        raise SystemExit("error: auth can-i VERB RESOURCE[/NAME]")
+    verb, target = a.args[1], a.args[2]
+    r, _, name = target.partition("/")
+    ri = SCHEME.resolve(r)
+    ra = {"verb": verb, "resource": ri.plural if ri else r, "group": ri.group if ri else "",
+          "namespace": "" if (ri and not ri.namespaced) else (a.namespace or "default")}
+    if name:
+        ra["name"] = name
+    if a.as_user:
+        body = {"apiVersion": "authorization.k8s.io/v1", "kind": "SubjectAccessReview",
+                "spec": {"resourceAttributes": ra, "user": a.as_user, "groups": a.as_group or []}}
+        out = await c.request("POST", "/apis/authorization.k8s.io/v1/subjectaccessreviews", body=body)
+    else:
+        body = {"apiVersion": "authorization.k8s.io/v1", "kind": "SelfSubjectAccessReview", "spec": {"resourceAttributes": ra}}
+        out = await c.request("POST", "/apis/authorization.k8s.io/v1/selfsubjectaccessreviews", body=body)
+    ok = bool((out.get("status") or {}).get("allowed"))
+    print("yes" if ok else "no")
+    return 0 if ok else 1
+
+
+async def cmd_certificate(c, a):
+    if len(a.args) < 2 or a.args[0] not in ("approve", "deny"):
+        raise SystemExit("error: certificate approve|deny NAME...")
+    approve = a.args[0] == "approve"
+    for name in a.args[1:]:
+        csr = await c.get("certificatesigningrequests.certificates.k8s.io", name)
+        conds = [x for x in (csr.get("status") or {}).get("conditions") or [] if x.get("type") not in ("Approved", "Denied")]
+        conds.append({"type": "Approved" if approve else "Denied", "reason": "KubectlApprove" if approve else "KubectlDeny",
+                      "message": f"This CSR was {'approved' if approve else 'denied'} by kubectl certificate {a.args[0]}.",
+                      "lastUpdateTime": m.now_rfc3339()})
+        csr.setdefault("status", {})["conditions"] = conds
+        await c.request("PUT", f"/apis/certificates.k8s.io/v1beta1/certificatesigningrequests/{name}/approval", body=csr)
+        print(f"certificatesigningrequest.certificates.k8s.io/{name} {'approved' if approve else 'denied'}")
+
+
+# ------------------------------------------------------------------ data plane helpers
+async def _pod_ip(c, ns, name) -> str:
+    p = await c.get("pods", name, ns)
+    ip = (p.get("status") or {}).get("podIP")
+    if not ip:
+        raise SystemExit(f"error: pod {name} has no IP yet")
+    return ip
+
+
+async def _pipe(r, w):
+    try:
+        while True:
+            data = await r.read(65536)
+            if not data:
+                break
+            w.write(data)
+            await w.drain()
+    except (ConnectionError, asyncio.CancelledError):
+        pass
+    finally:
+        try:
+            w.close()
+        except Exception:
+            pass
+
+
+async def port_forward(c, ns, name, mappings, ready=None, stop=None):
+    """Listen on 127.0.0.1:LOCAL for each LOCAL:REMOTE and splice to podIP:REMOTE."""
+    ip = await _pod_ip(c, ns, name)
+    servers = []
+    for mp in mappings:
+        local, _, remote = mp.partition(":")
+        remote = int(remote or local)
+
+        async def handle(r, w, remote=remote):
+            try:
+                pr, pw = await asyncio.open_connection(ip, remote)
+            except OSError:
+                w.close()
+                return
+            await asyncio.gather(_pipe(r, pw), _pipe(pr, w))
+
+        srv = await asyncio.start_server(handle, "127.0.0.1", int(local or 0))
+        servers.append(srv)
+        print(f"Forwarding from 127.0.0.1:{srv.sockets[0].getsockname()[1]} -> {remote}", flush=True)
+    if ready is not None:
+        ready.set_result([s.sockets[0].getsockname()[1] for s in servers])
+    try:
+        await (stop.wait() if stop is not None else asyncio.Event().wait())
+    finally:
+        for s in servers:
+            s.close()
+
+
+async def cmd_port_forward(c, a):
+    ri, name, rest = _target(a) if "/" in a.args[0] else (SCHEME.resolve("pods"), a.args[0], a.args[1:])
+    if ri.kind != "Pod":
+        obj = await c.get(_res(ri), name, _ns(a, ri))
+        sel = ((obj.get("spec") or {}).get("selector") or {})
+        sel = sel.get("matchLabels", sel)
+        pods, _ = await c.list("pods", _ns(a, ri), ",".join(f"{k}={v}" for k, v in sel.items()))
+        running = [p for p in pods if (p.get("status") or {}).get("phase") == "Running"]
+        if not running:
+            raise SystemExit("error: no running pod found")
+        name = m.name_of(running[0])
+    await port_forward(c, a.namespace or "default", name, rest)
+
+
+async def cmd_proxy(c, a):
+    """Local HTTP proxy to the apiserver that adds the client's credentials (proxy.go)."""
+    from aiohttp import web
+
+    async def handle(req):
+        body = await req.read()
+        try:
+            r = await c.request(req.method, req.rel_url.path, params=dict(req.query), body=body or None, raw=True,
+                                content_type=req.headers.get("Content-Type", "application/json"))
+        except m.StatusError as e:
+            return web.json_response(e.status(), status=e.code)
+        return web.Response(body=r, content_type="application/json")
+
+    app = web.Application()
+    app.router.add_route("*", "/{tail:.*}", handle)
+    runner = web.AppRunner(app)
+    await runner.setup()
+    site = web.TCPSite(runner, "127.0.0.1", a.port or 8001)
+    await site.start()
+    print(f"Starting to serve on 127.0.0.1:{a.port or 8001}", flush=True)
+    await asyncio.Event().wait()
+
+
+async def cmd_cp(c, a):
+    from .main import kubelet_exec
+    if len(a.args) != 2:
+        raise SystemExit("error: cp SRC DST (one side as [NAMESPACE/]POD:PATH)")
+    src, dst = a.args
+    if ":" in src:
+        pod, _, path = src.partition(":")
+        ns, _, pod = pod.rpartition("/")
+        out, rc = await kubelet_exec(c, ns or a.namespace or "default", pod, a.container, ["base64", path])
+        if rc != 0:
+            raise SystemExit(f"error: {out.decode(errors='replace').strip()}")
+        with open(dst, "wb") as f:
+            f.write(base64.b64decode(out))
+    else:
+        pod, _, path = dst.partition(":")
+        ns, _, pod = pod.rpartition("/")
+        data = open(src, "rb").read()
+        if len(data) > 1 << 20:
+            raise SystemExit("error: cp into a pod is limited to 1 MiB")
+        enc = base64.b64encode(data).decode()
+        out, rc = await kubelet_exec(c, ns or a.namespace or "default", pod, a.container,
+                                     ["sh", "-c", f"echo {enc} | base64 -d > '{path}'"])
+        if rc != 0:
+            raise SystemExit(f"error: {out.decode(errors='replace').strip()}")
+
+
+async def cmd_explain(c, a):
+    ri = SCHEME.resolve(a.args[0].split(".")[0]) if a.args else None
+    if ri is None:
+        raise SystemExit("error: explain RESOURCE")
+    print(f"KIND:     {ri.kind}\nVERSION:  {ri.api_version}\n")
+    print(f"RESOURCE: {ri.plural} (namespaced: {str(ri.namespaced).lower()}; short names: {', '.join(ri.short_names) or '-'};"
+          f" subresources: {', '.join(ri.subresources) or '-'})")
+    print("\nFIELDS:\n   apiVersion\t<string>\n   kind\t<string>\n   metadata\t<Object>")
+    if ri.kind not in ("ConfigMap", "Secret", "Event", "Binding", "Endpoints", "ClusterRole", "Role"):
+        print("   spec\t<Object>")
+    if ri.plural in __import__("amdkube.apiserver.registry", fromlist=["_STATUS_KINDS"])._STATUS_KINDS:
+        print("   status\t<Object>")
+
+
+# ------------------------------------------------------------------ create <generator>
+async def cmd_create_generator(c, a) -> bool:
+    """`kubectl create <kind> NAME ...` generators; False when args are not a generator."""
+    if not a.args:
+        return False
+    kind, rest = a.args[0], a.args[1:]
+    ns = a.namespace or "default"
+
+    def lit():
+        out = {}
+        for kv in a.from_literal:
+            k, _, v = kv.partition("=")
+            out[k] = v
+        for fpath in a.from_file:
+            k, _, p = fpath.partition("=")
+            if not p:
+                k, p = os.path.basename(k), k
+            out[k] = open(p).read()
+        return out
+
+    if kind in ("namespace", "ns"):
+        obj = {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": rest[0]}}
+    elif kind in ("configmap", "cm"):
+        obj = {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": rest[0]}, "data": lit()}
+    elif kind == "secret":
+        if rest[0] != "generic":
+            raise SystemExit("error: only `create secret generic` is supported")
+        obj = {"apiVersion": "v1", "kind": "Secret", "metadata": {"name": rest[1]}, "type": "Opaque",
+               "data": {k: base64.b64encode(v.encode()).decode() for k, v in lit().items()}}
+    elif kind in ("serviceaccount", "sa"):
+        obj = {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": rest[0]}}
+    elif kind in ("deployment", "deploy"):
+        ct = {"name": rest[0], "image": a.image}
+        if a.gpus:
+            ct["resources"] = {"limits": {"amd.com/gpu": str(a.gpus)}}
+        obj = {"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": rest[0], "labels": {"app": rest[0]}},
+               "spec": {"replicas": a.replicas, "selector": {"matchLabels": {"app": rest[0]}},
+                        "template": {"metadata": {"labels": {"app": rest[0]}}, "spec": {"containers": [ct]}}}}
+    elif kind == "job":
+        ct = {"name": rest[0], "image": a.image}
+        if a.command:
+            ct["command"] = a.command
+        obj = {"apiVersion": "batch/v1", "kind": "Job", "metadata": {"name": rest[0]},
+               "spec": {"template": {"spec": {"restartPolicy": "Never", "containers": [ct]}}}}
+    elif kind in ("priorityclass", "pc"):
+        obj = {"apiVersion": "scheduling.k8s.io/v1alpha1", "kind": "PriorityClass", "metadata": {"name": rest[0]},
+               "value": a.value, "globalDefault": a.global_default}
+    elif kind in ("quota", "resourcequota"):
+        hard = dict(kv.split("=", 1) for kv in (a.hard or "").split(",") if kv)
+        obj = {"apiVersion": "v1", "kind": "ResourceQuota", "metadata": {"name": rest[0]}, "spec": {"hard": hard}}
+    elif kind in ("role", "clusterrole"):
+        rules = [{"apiGroups": [""], "resources": a.resource, "verbs": a.verb}]
+        obj = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role" if kind == "role" else "ClusterRole",
+               "metadata": {"name": rest[0]}, "rules": rules}
+    elif kind in ("rolebinding", "clusterrolebinding"):
+        subjects = [{"kind": "User", "name": u, "apiGroup": "rbac.authorization.k8s.io"} for u in a.user]
+        subjects += [{"kind": "Group", "name": g, "apiGroup": "rbac.authorization.k8s.io"} for g in a.group]
+        for sa in a.serviceaccount:
+            sns, _, sname = sa.partition(":")
+            subjects.append({"kind": "ServiceAccount", "namespace": sns, "name": sname})
+        if a.clusterrole:
+            ref = {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole", "name": a.clusterrole}
+        else:
+            ref = {"apiGroup": "rbac.authorization.k8s.io", "kind": "Role", "name": a.role}
+        obj = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "RoleBinding" if kind == "rolebinding" else "ClusterRoleBinding",
+               "metadata": {"name": rest[0]}, "roleRef": ref, "subjects": subjects}
+    else:
+        return False
+    ri = SCHEME.for_object(obj)
+    if a.output:
+        from .main import _emit
+        _emit([obj], a, obj["kind"], single=True)
+        return True
+    out = await c.create(obj, ns if ri.namespaced else "")
+    print(f"{obj['kind'].lower()}/{m.name_of(out)} created")
+    return True
+
+
+COMMANDS = {"rollout": cmd_rollout, "expose": cmd_expose, "autoscale": cmd_autoscale, "taint": cmd_taint, "set": cmd_set,
+            "replace": cmd_replace, "edit": cmd_edit, "auth": cmd_auth, "certificate": cmd_certificate,
+            "port-forward": cmd_port_forward, "proxy": cmd_proxy, "cp": cmd_cp, "explain": cmd_explain}
+
+
+def add_arguments(sp):
+    sp.add_argument("--to-revision", type=int, default=0)
+    sp.add_argument("--watch-status", type=lambda s: s != "false", default=True)
+    sp.add_argument("--port", default=None)
+    sp.add_argument("--target-port", default=None)
+    sp.add_argument("--name", default=None)
+    sp.add_argument("--protocol", default="TCP")
+    sp.add_argument("--min", type=int, default=0)
+    sp.add_argument("--max", type=int, default=1)
+    sp.add_argument("--cpu-percent", type=int, default=-1)
+    sp.add_argument("--overwrite", action="store_true")
+    sp.add_argument("--record", action="store_true")
+    sp.add_argument("--force", action="store_true")
+    sp.add_argument("--raw", action="store_true")
+    sp.add_argument("--as", dest="as_user", default=None)
+    sp.add_argument("--as-group", action="append", default=[])
+    sp.add_argument("--from-literal", action="append", default=[])
+    sp.add_argument("--from-file", action="append", default=[])
+    sp.add_argument("--value", type=int, default=0)
+    sp.add_argument("--global-default", action="store_true")
+    sp.add_argument("--hard", default=None)
+    sp.add_argument("--verb", action="append", default=[])
+    sp.add_argument("--resource", action="append", default=[])
+    sp.add_argument("--user", action="append", default=[])
+    sp.add_argument("--group", action="append", default=[])
+    sp.add_argument("--serviceaccount", action="append", default=[])
+    sp.add_argument("--clusterrole", default=None)
+    sp.add_argument("--role", default=None)
+
+
+__all__ = ["COMMANDS", "add_arguments", "cmd_config_sync", "cmd_create_generator", "parse_taint", "port_forward", "sys"]

@@ -2,7 +2,8 @@
 
 Reference command set: pkg/kubectl/cmd/cmd.go:216 (create/apply/get/describe/delete/logs/
 exec/label/annotate/cordon/uncordon/drain/scale/patch/run/top/version/api-resources/
-cluster-info/explain), create.go:64,146. Output: tables (GPU columns added, SURVEY §7.6
+cluster-info), create.go:64,146; rollout/expose/autoscale/taint/set/replace/edit/config/
+auth/certificate/port-forward/proxy/cp/explain and the create generators live in extra.py. Output: tables (GPU columns added, SURVEY §7.6
 #17), -o json|yaml|name|wide|jsonpath={...}. Server from --server, $AMDKUBE_SERVER or
 ~/.amdkube/config ({"server": ..., "token": ...}).
 """
@@ -195,6 +196,12 @@ async def _create_or_apply(c, a, apply=False):
 
 
 async def cmd_create(c, a):
+    if not a.filename:
+        from .extra import cmd_create_generator
+        if await cmd_create_generator(c, a):
+            return
+        raise SystemExit("error: must specify -f or a generator (namespace, configmap, secret generic, serviceaccount, "
+                         "deployment, job, priorityclass, quota, role, clusterrole, rolebinding, clusterrolebinding)")
     await _create_or_apply(c, a)
 
 
@@ -233,20 +240,24 @@ async def cmd_logs(c, a):
     print(await c.logs(a.namespace or "default", name, a.container, a.tail if a.tail >= 0 else None), end="")
 
 
-async def cmd_exec(c, a):
-    name = a.args[0].split("/", 1)[-1]
-    pod = await c.get("pods", name, a.namespace or "default")
+async def kubelet_exec(c, ns: str, name: str, container: str | None, cmd: list[str]) -> tuple[bytes, int]:
+    """Run a command in a container through its node's kubelet (/run), returning (output, exit code)."""
+    pod = await c.get("pods", name, ns)
     node = await c.get("nodes", pod["spec"]["nodeName"])
     st = node.get("status") or {}
     port = st["daemonEndpoints"]["kubeletEndpoint"]["Port"]
     addr = next((x["address"] for x in st.get("addresses") or [] if x.get("type") == "InternalIP"), "127.0.0.1")
-    container = a.container or pod["spec"]["containers"][0]["name"]
+    container = container or pod["spec"]["containers"][0]["name"]
     import aiohttp
     async with aiohttp.ClientSession() as s:
-        async with s.post(f"http://{addr}:{port}/run/{a.namespace or 'default'}/{name}/{container}",
-                          params=[("cmd", x) for x in a.command]) as r:
-            sys.stdout.write(await r.text())
-            return int(r.headers.get("X-Exit-Code", "0"))
+        async with s.post(f"http://{addr}:{port}/run/{ns}/{name}/{container}", params=[("cmd", x) for x in cmd]) as r:
+            return await r.read(), int(r.headers.get("X-Exit-Code", "0"))
+
+
+async def cmd_exec(c, a):
+    out, rc = await kubelet_exec(c, a.namespace or "default", a.args[0].split("/", 1)[-1], a.container, a.command)
+    sys.stdout.write(out.decode(errors="replace"))
+    return rc
 
 
 async def _meta_edit(c, a, field):
@@ -401,6 +412,8 @@ COMMANDS = {"get": cmd_get, "describe": cmd_describe, "create": cmd_create, "app
             "uncordon": cmd_uncordon, "drain": cmd_drain, "scale": cmd_scale, "patch": cmd_patch, "run": cmd_run,
             "top": cmd_top, "version": cmd_version, "api-resources": cmd_api_resources, "cluster-info": cmd_cluster_info,
             "wait": cmd_wait}
+from .extra import COMMANDS as _EXTRA, add_arguments as _extra_args  # noqa: E402
+COMMANDS.update(_EXTRA)
 
 
 def parser():
@@ -411,8 +424,9 @@ def parser():
     p.add_argument("--context", default=None)
     p.add_argument("-n", "--namespace", default=None)
     sub = p.add_subparsers(dest="cmd", required=True)
-    for name in COMMANDS:
+    for name in list(COMMANDS) + ["config"]:
         sp = sub.add_parser(name)
+        _extra_args(sp)
         sp.add_argument("args", nargs="*")
         sp.add_argument("-n", "--namespace", default=argparse.SUPPRESS)
         sp.add_argument("-o", "--output", default=None)
@@ -451,6 +465,10 @@ def main(argv=None):
         a.command = cmd_tail
     elif a.command is None:
         a.command = []
+
+    if a.cmd == "config":   # kubeconfig edits need no server
+        from .extra import cmd_config_sync
+        return cmd_config_sync(a)
 
     async def go():
         c = _client(a)
