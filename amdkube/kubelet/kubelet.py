@@ -40,7 +40,7 @@ from ..utils.features import FeatureGate
 from ..utils.metrics import MICRO_BUCKETS, Counter, Gauge, Histogram, Summary, new_registry
 from .cri_client import CURRENT_POD, CRIClient
 from .devicemanager import AdmissionError, ManagerImpl, ManagerStub
-from .kuberuntime import L_POD_UID, RuntimeManager
+from .kuberuntime import L_POD_UID, RuntimeManager, SandboxRef, apply_event
 from .status import StatusManager, generate_status
 
 log = logging.getLogger("amdkube.kubelet")
@@ -134,11 +134,13 @@ class Kubelet:
         self._node_dirty = asyncio.Event()
         self._sandbox_uid: dict[str, str] = {}
         self._pleg_snapshot: dict[str, int] = {}
+        self._pleg_owner: dict[str, str] = {}
         # runtime pod-status cache (reference kubecontainer.Cache fed by PLEG, GetNewerThan): the
         # status observed after a sync stays valid until a PLEG event for the pod (generation bump)
         # or any mutating CRI call by this kubelet
         self._rt_gen: dict[str, int] = {}
-        self._rt_cache: dict[str, tuple] = {}
+        self._rt_cache: dict[str, tuple] = {}     # uid -> ((gen, mutations), PodRuntimeStatus, fetch start ns)
+        self._rt_pending: dict[str, list] = {}    # uid -> full-status events that arrived while the cache was stale
         self.smi = smi_backend
         self.server = None
         self.first_seen: dict[str, float] = {}
@@ -565,7 +567,7 @@ class Kubelet:
         """Returns True when the worker for this pod is finished (pod gone from the node)."""
         pod = self.pods.get(uid)
         if pod is None:
-            await self.runtime.kill_and_remove(uid)
+            await self.runtime.kill_and_remove(uid, self._cached_sandboxes(uid))
             self._cleanup(uid)
             return True
         md = pod.get("metadata") or {}
@@ -599,7 +601,7 @@ class Kubelet:
             return False
         sent_phase = (self.status.get(uid) or {}).get("phase") or (pod.get("status") or {}).get("phase")
         if sent_phase in ("Succeeded", "Failed") and uid in self.status.terminal:
-            await self.runtime.kill_pod(uid, 0, pod)
+            await self.runtime.kill_pod(uid, 0, pod, self._cached_sandboxes(uid))
             return False
         ctx = await self._pod_context(pod)
         rt = await self._cached_status(uid)
@@ -617,7 +619,8 @@ class Kubelet:
             if ct:
                 self.m_pod_start.observe(max(0.0, time.time() - ct) * 1e6)
         if st["phase"] in ("Succeeded", "Failed"):
-            await self.runtime.kill_pod(uid, 0, pod)  # release the sandbox (devices stay API-assigned)
+            # release the sandbox (devices stay API-assigned)
+            await self.runtime.kill_pod(uid, 0, pod, self._cached_sandboxes(uid))
         # container restarts waiting on back-off: re-sync when the back-off expires
         for c in (pod.get("spec") or {}).get("containers") or []:
             rem = self.runtime.backoff_remaining(uid, c["name"])
@@ -650,14 +653,41 @@ class Kubelet:
     def _on_terminal(self, uid):
         pass
 
-    async def _cached_status(self, uid: str, fresh: bool = False):
-        key = (self._rt_gen.get(uid, 0), self.cri.pod_mutations(uid))
+    def _cache_valid(self, uid: str):
         hit = self._rt_cache.get(uid)
-        if not fresh and hit is not None and hit[0] == key:
+        if hit is not None and hit[0] == (self._rt_gen.get(uid, 0), self.cri.pod_mutations(uid)):
+            return hit
+        return None
+
+    async def _cached_status(self, uid: str, fresh: bool = False):
+        """The pod's runtime status: the cache while no mutation/invalidation happened since it
+        was filled (events keep it current), otherwise one fetch (1 + sandboxes + containers RPCs)
+        with the full-status events newer than the fetch applied on top."""
+        hit = self._cache_valid(uid)
+        if not fresh and hit is not None:
             return hit[1]
+        key = (self._rt_gen.get(uid, 0), self.cri.pod_mutations(uid))
+        t0 = time.time_ns()
         rt = await self.runtime.pod_status(uid)
-        self._rt_cache[uid] = (key, rt)  # key taken before the fetch: a concurrent event invalidates it
+        for ev in self._rt_pending.pop(uid, ()):
+            if ev.created_at > t0:
+                rt = apply_event(rt, ev, self.runtime.sandbox_ips)
+        self._rt_cache[uid] = (key, rt, t0)  # key taken before the fetch: a concurrent invalidation wins
         return rt
+
+    def _cached_sandboxes(self, uid: str):
+        hit = self._cache_valid(uid)
+        return [SandboxRef(x[0], x[1]) for x in hit[1].sandboxes] if hit is not None else None
+
+    def _apply_full_event(self, uid: str, ev):
+        hit = self._cache_valid(uid)
+        if hit is not None:
+            if ev.created_at > hit[2]:
+                self._rt_cache[uid] = (hit[0], apply_event(hit[1], ev, self.runtime.sandbox_ips), hit[2])
+        else:
+            pend = self._rt_pending.setdefault(uid, [])
+            pend.append(ev)
+            del pend[:-64]
 
     def _pleg_event(self, uid: str):
         self._rt_gen[uid] = self._rt_gen.get(uid, 0) + 1
@@ -666,6 +696,7 @@ class Kubelet:
     def _cleanup(self, uid):
         self._rt_gen.pop(uid, None)
         self._rt_cache.pop(uid, None)
+        self._rt_pending.pop(uid, None)
         self.cri.forget_pod(uid)
         if self.gpu_legacy is not None:
             self.gpu_legacy.release(uid)
@@ -803,15 +834,27 @@ class Kubelet:
                 running_pods += 1
         conts = await self.cri.list_containers()
         running_c = 0
+        owner = {}
         for c in conts:
             cur[c.id] = c.state
+            uid = self._sandbox_uid.get(c.pod_sandbox_id) or c.labels.get(L_POD_UID, "")
+            owner[c.id] = uid
             if c.state == C.CONTAINER_RUNNING:
                 running_c += 1
             if self._pleg_snapshot.get(c.id) != c.state:
-                uids_changed.add(self._sandbox_uid.get(c.pod_sandbox_id) or c.labels.get(L_POD_UID, ""))
-        if set(self._pleg_snapshot) - set(cur):
-            self._rt_cache.clear()  # a container vanished and its owner is unknown: drop every cached status
+                hit = self._cache_valid(uid) if uid else None
+                if hit is None or hit[1].container_state(c.id) != c.state:   # events already told us
+                    uids_changed.add(uid)
+        for cid in set(self._pleg_snapshot) - set(cur):
+            uid = self._pleg_owner.get(cid)
+            if uid is None:
+                self._rt_cache.clear()  # a container vanished and its owner is unknown: drop every cached status
+                break
+            hit = self._cache_valid(uid)
+            if hit is not None and hit[1].container_state(cid) is not None:
+                self._rt_gen[uid] = self._rt_gen.get(uid, 0) + 1
         self._pleg_snapshot = cur
+        self._pleg_owner = owner
         self.m_running_pods.set(running_pods)
         self.m_running_containers.set(running_c)
         for uid in uids_changed:
@@ -829,15 +872,26 @@ class Kubelet:
             try:
                 async for ev in self.cri.container_events():
                     backoff = 0.1
-                    sid = ev.pod_sandbox_status.id
+                    sst = ev.pod_sandbox_status
+                    sid = sst.id
+                    full = bool(sst.metadata.uid)   # the runtime sends complete pod state (KEP-3386)
+                    if full:
+                        self._sandbox_uid[sid] = sst.metadata.uid
                     uid = self._sandbox_uid.get(sid)
                     if uid is None:
                         for s in await self.cri.list_pod_sandbox():
                             self._sandbox_uid[s.id] = s.labels.get(L_POD_UID, "")
                         uid = self._sandbox_uid.get(sid)
-                    if uid and ev.container_event_type in (C.CONTAINER_STOPPED_EVENT, C.CONTAINER_STARTED_EVENT):
+                    if not uid:
+                        continue
+                    if full:
+                        self._apply_full_event(uid, ev)
+                    if ev.container_event_type in (C.CONTAINER_STOPPED_EVENT, C.CONTAINER_STARTED_EVENT) and ev.container_id != sid:
                         if uid in self.pods or uid in self.workers:
-                            self._pleg_event(uid)
+                            if full:
+                                self.dispatch(uid)     # the cache already holds the new state
+                            else:
+                                self._pleg_event(uid)
             except asyncio.CancelledError:
                 raise
             except Exception as e:

@@ -59,11 +59,12 @@ def container_hash(c: dict) -> str:
 
 class ContainerRuntimeStatus:
     __slots__ = ("id", "name", "state", "exit_code", "reason", "message", "created_at", "started_at", "finished_at",
-                 "restart_count", "hash", "image", "image_ref", "init", "log_path")
+                 "restart_count", "hash", "image", "image_ref", "init", "log_path", "sandbox_id")
 
     @classmethod
-    def from_cri(cls, st, ann):
+    def from_cri(cls, st, ann, sandbox_id: str = ""):
         s = cls()
+        s.sandbox_id = sandbox_id
         s.id, s.name, s.state = st.id, st.metadata.name, st.state
         s.exit_code, s.reason, s.message = st.exit_code, st.reason, st.message
         s.created_at, s.started_at, s.finished_at = st.created_at, st.started_at, st.finished_at
@@ -93,6 +94,49 @@ class PodRuntimeStatus:
 
     def running(self):
         return [c for lst in self.containers.values() for c in lst if c.state == C.CONTAINER_RUNNING]
+
+    def container_state(self, cid: str):
+        for lst in self.containers.values():
+            for c in lst:
+                if c.id == cid:
+                    return c.state
+        return None
+
+
+class SandboxRef:
+    """(id, state) of a sandbox, enough for kill_pod/remove_pod without a ListPodSandbox."""
+    __slots__ = ("id", "state")
+
+    def __init__(self, sid, state):
+        self.id, self.state = sid, state
+
+
+def apply_event(rt: PodRuntimeStatus, ev, sandbox_ips: dict) -> PodRuntimeStatus:
+    """A new PodRuntimeStatus = rt with one sandbox (and all its containers) replaced by the
+    full state an evented-PLEG event carries (KEP-3386 ContainerEventResponse). rt itself is
+    never mutated: a pod sync may still hold it."""
+    sst = ev.pod_sandbox_status
+    sid = sst.id
+    gone = ev.container_event_type == C.CONTAINER_DELETED_EVENT and ev.container_id == sid
+    new = PodRuntimeStatus(rt.uid)
+    sbs = [x for x in rt.sandboxes if x[0] != sid]
+    if not gone:
+        sbs.append((sid, sst.state, sst.metadata.attempt, sst.created_at))
+    new.sandboxes = sorted(sbs, key=lambda x: x[3], reverse=True)
+    for name, lst in rt.containers.items():
+        keep = [c for c in lst if c.sandbox_id != sid]
+        if keep:
+            new.containers[name] = keep
+    if not gone:
+        for cs in ev.containers_statuses:
+            new.containers.setdefault(cs.metadata.name, []).append(ContainerRuntimeStatus.from_cri(cs, dict(cs.annotations), sid))
+    for lst in new.containers.values():
+        lst.sort(key=lambda x: x.created_at, reverse=True)
+    if not gone and sst.state == C.SANDBOX_READY and sst.network.ip:
+        sandbox_ips.setdefault(sid, sst.network.ip)
+    ready = new.ready_sandbox()
+    new.ip = sandbox_ips.get(ready[0], "") if ready is not None else ""
+    return new
 
 
 class RuntimeManager:
@@ -131,7 +175,7 @@ class RuntimeManager:
                     cs, _ = await self.cri.container_status(c.id)
                 except grpc.RpcError:
                     continue
-                st.containers.setdefault(c.metadata.name, []).append(ContainerRuntimeStatus.from_cri(cs, dict(c.annotations)))
+                st.containers.setdefault(c.metadata.name, []).append(ContainerRuntimeStatus.from_cri(cs, dict(c.annotations), s.id))
         for lst in st.containers.values():
             lst.sort(key=lambda x: x.created_at, reverse=True)
         return st
@@ -312,9 +356,9 @@ class RuntimeManager:
         for k in [k for k in self.backoff if k[0] == uid]:
             del self.backoff[k]
 
-    async def kill_and_remove(self, uid: str):
+    async def kill_and_remove(self, uid: str, sandboxes=None):
         """The pod is gone from the API: one list, stop what still runs, remove everything."""
-        sbs = await self.cri.list_pod_sandbox(uid)
+        sbs = sandboxes if sandboxes is not None else await self.cri.list_pod_sandbox(uid)
         await self.kill_pod(uid, 0, None, sbs)
         await self.remove_pod(uid, sbs)
 

@@ -116,10 +116,29 @@ class RocShim:
         self._adopt_tasks: set = set()
         self._event_streams: set[asyncio.Queue] = set()
 
-    def _emit(self, c: "Container", etype: int):
+    def _emit(self, c: "Container | None", etype: int, sid: str | None = None):
+        """Evented PLEG (KEP-3386 ContainerEventResponse): every event carries the sandbox's full
+        status and the statuses of all its containers as of emission, so the kubelet updates its
+        runtime cache from the stream instead of re-listing (3 RPCs per pod sync). Sandbox
+        lifecycle events use the sandbox id as container_id."""
         if not self._event_streams:
             return
-        ev = (c.id, c.sandbox_id, etype, now_ns())
+        sid = sid or c.sandbox_id
+        sb = self.sandboxes.get(sid)
+        ts = now_ns()
+        sst = sandbox_status_msg(sb, self.network.node_ip) if sb is not None else C.PodSandboxStatus(id=sid)
+        ev = C.ContainerEventResponse(container_id=c.id if c is not None else sid, container_event_type=etype, created_at=ts,
+                                      pod_sandbox_status=sst,
+                                      containers_statuses=[container_status_msg(x) for x in self.containers.values()
+                                                           if x.sandbox_id == sid])
+        for q in list(self._event_streams):
+            q.put_nowait(ev)
+
+    def _emit_removed(self, s: "Sandbox"):
+        if not self._event_streams:
+            return
+        ev = C.ContainerEventResponse(container_id=s.id, container_event_type=C.CONTAINER_DELETED_EVENT, created_at=now_ns(),
+                                      pod_sandbox_status=C.PodSandboxStatus(id=s.id, metadata=sandbox_meta(s)))
         for q in list(self._event_streams):
             q.put_nowait(ev)
 
@@ -240,6 +259,7 @@ class RocShim:
                 raise
         self.sandboxes[sid] = s
         self._ckpt("sandboxes", s)
+        self._emit(None, C.CONTAINER_STARTED_EVENT, sid)
         return sid
 
     async def stop_sandbox(self, sid: str):
@@ -259,6 +279,7 @@ class RocShim:
             s.pod_network = False
         s.state = C.SANDBOX_NOTREADY
         self._ckpt("sandboxes", s)
+        self._emit(None, C.CONTAINER_STOPPED_EVENT, sid)
 
     async def remove_sandbox(self, sid: str):
         s = self.sandboxes.get(sid)
@@ -270,6 +291,8 @@ class RocShim:
             await self.remove_container(c.id)
         self.sandboxes.pop(sid, None)
         self._unckpt("sandboxes", sid)
+        if s.meta.get("uid"):
+            self._emit_removed(s)
         shutil.rmtree(os.path.join(self.state_dir, "rootfs", sid), ignore_errors=True)
 
     # --------------------------------------------------------------- containers
@@ -469,6 +492,25 @@ class RocShim:
         return out, err, p.returncode
 
 
+def sandbox_meta(s) -> "C.PodSandboxMetadata":
+    return C.PodSandboxMetadata(name=s.meta["name"], uid=s.meta["uid"], namespace=s.meta["namespace"],
+                                attempt=s.meta.get("attempt", 0))
+
+
+def sandbox_status_msg(s, node_ip: str) -> "C.PodSandboxStatus":
+    return C.PodSandboxStatus(id=s.id, metadata=sandbox_meta(s), state=s.state, created_at=s.created_at,
+                              network=C.PodSandboxNetworkStatus(ip=s.ip or node_ip), labels=s.labels, annotations=s.annotations)
+
+
+def container_status_msg(c) -> "C.ContainerStatus":
+    return C.ContainerStatus(id=c.id, metadata=C.ContainerMetadata(name=c.name, attempt=c.attempt), state=c.state,
+                             created_at=c.created_at, started_at=c.started_at, finished_at=c.finished_at,
+                             exit_code=c.exit_code, image=C.ImageSpec(image=c.image), image_ref=c.image_ref,
+                             reason=c.reason, message=c.message, labels=c.labels, annotations=c.annotations,
+                             mounts=[C.Mount(container_path=m["container_path"], host_path=m["host_path"], readonly=m["readonly"])
+                                     for m in c.mounts], log_path=c.log_path)
+
+
 def _killpg(pid, sig) -> None:
     """Signal a container's process group. Never signal pid/pgid 0 or 1, our own group, or our
     own process: killpg(0) would hit the runtime (and whatever launched it)."""
@@ -555,8 +597,7 @@ class _Runtime:
         return C.RemovePodSandboxResponse()
 
     def _sb_meta(self, s):
-        return C.PodSandboxMetadata(name=s.meta["name"], uid=s.meta["uid"], namespace=s.meta["namespace"],
-                                    attempt=s.meta.get("attempt", 0))
+        return sandbox_meta(s)
 
     async def PodSandboxStatus(self, req, ctx):
         s = self.r.sandboxes.get(req.pod_sandbox_id)
@@ -564,9 +605,7 @@ class _Runtime:
             await ctx.abort(grpc.StatusCode.NOT_FOUND, f"sandbox {req.pod_sandbox_id} not found")
         if s.state == C.SANDBOX_READY and not _alive(s.pid):
             s.state = C.SANDBOX_NOTREADY
-        st = C.PodSandboxStatus(id=s.id, metadata=self._sb_meta(s), state=s.state, created_at=s.created_at,
-                                network=C.PodSandboxNetworkStatus(ip=s.ip or self.r.network.node_ip), labels=s.labels,
-                                annotations=s.annotations)
+        st = sandbox_status_msg(s, self.r.network.node_ip)
         return C.PodSandboxStatusResponse(status=st, info={"pid": str(s.pid)} if req.verbose else {})
 
     async def ListPodSandbox(self, req, ctx):
@@ -631,12 +670,7 @@ class _Runtime:
         c = self.r.containers.get(req.container_id)
         if c is None:
             await ctx.abort(grpc.StatusCode.NOT_FOUND, f"container {req.container_id} not found")
-        st = C.ContainerStatus(id=c.id, metadata=C.ContainerMetadata(name=c.name, attempt=c.attempt), state=c.state,
-                               created_at=c.created_at, started_at=c.started_at, finished_at=c.finished_at,
-                               exit_code=c.exit_code, image=C.ImageSpec(image=c.image), image_ref=c.image_ref,
-                               reason=c.reason, message=c.message, labels=c.labels, annotations=c.annotations,
-                               mounts=[C.Mount(container_path=m["container_path"], host_path=m["host_path"], readonly=m["readonly"])
-                                       for m in c.mounts], log_path=c.log_path)
+        st = container_status_msg(c)
         info = {"pid": str(c.pid), "handler": c.handler, "devices": json.dumps(c.devices)} if req.verbose else {}
         return C.ContainerStatusResponse(status=st, info=info)
 
@@ -686,9 +720,7 @@ class _Runtime:
         self.r._event_streams.add(q)
         try:
             while True:
-                cid, sid, etype, ts = await q.get()
-                yield C.ContainerEventResponse(container_id=cid, container_event_type=etype, created_at=ts,
-                                               pod_sandbox_status=C.PodSandboxStatus(id=sid))
+                yield await q.get()
         finally:
             self.r._event_streams.discard(q)
 

@@ -232,3 +232,31 @@ def test_legacy_gpu_manager_rebuild_after_restart():
         pass
     b = g.allocate(pod("u3"), ctr, [pod("u1", "Succeeded"), pod("u2"), pod("u3")])
     assert b["annotations"][ANNOTATION] == "/dev/dri/renderD128,/dev/dri/renderD129"
+
+
+def test_full_status_event_merges_into_runtime_cache():
+    """Evented PLEG with complete pod state (KEP-3386 ContainerEventResponse): one sandbox and
+    all its containers are replaced, other sandboxes are kept, a removed sandbox disappears."""
+    from amdkube.grpcdesc.cri import CRI as C
+    from amdkube.kubelet.kuberuntime import ContainerRuntimeStatus, PodRuntimeStatus, apply_event
+
+    def cs(cid, name, state, created):
+        return C.ContainerStatus(id=cid, metadata=C.ContainerMetadata(name=name), state=state, created_at=created,
+                                 annotations={"io.kubernetes.container.restartCount": "1"})
+    rt = PodRuntimeStatus("u")
+    rt.sandboxes = [("old", C.SANDBOX_NOTREADY, 0, 1)]
+    rt.containers = {"c": [ContainerRuntimeStatus.from_cri(cs("c0", "c", C.CONTAINER_EXITED, 1), {}, "old")]}
+    ev = C.ContainerEventResponse(
+        container_id="c1", container_event_type=C.CONTAINER_STARTED_EVENT, created_at=10,
+        pod_sandbox_status=C.PodSandboxStatus(id="new", metadata=C.PodSandboxMetadata(uid="u", attempt=1), state=C.SANDBOX_READY,
+                                              created_at=5, network=C.PodSandboxNetworkStatus(ip="10.1.0.7")),
+        containers_statuses=[cs("c1", "c", C.CONTAINER_RUNNING, 6)])
+    ips = {}
+    new = apply_event(rt, ev, ips)
+    assert [s[0] for s in new.sandboxes] == ["new", "old"] and new.ip == "10.1.0.7" and ips == {"new": "10.1.0.7"}
+    assert [c.id for c in new.containers["c"]] == ["c1", "c0"] and new.latest("c").restart_count == 1
+    assert rt.sandboxes == [("old", C.SANDBOX_NOTREADY, 0, 1)]          # the input is never mutated
+    gone = C.ContainerEventResponse(container_id="old", container_event_type=C.CONTAINER_DELETED_EVENT, created_at=11,
+                                    pod_sandbox_status=C.PodSandboxStatus(id="old", metadata=C.PodSandboxMetadata(uid="u")))
+    after = apply_event(new, gone, ips)
+    assert [s[0] for s in after.sandboxes] == ["new"] and [c.id for c in after.containers["c"]] == ["c1"]
