@@ -30,6 +30,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+from amdkube.utils.trace import POD_TRACE
 from amdkube.api import meta as m  # noqa: E402
 from amdkube.localcluster import LocalCluster  # noqa: E402
 
@@ -94,14 +95,17 @@ class PodBench:
         if rec is None:
             return
         now = time.perf_counter()
+        uid = m.uid_of(obj)
         if "bound" not in rec and (obj.get("spec") or {}).get("nodeName"):
             rec["bound"] = now
+            POD_TRACE(uid, "bench_bound")
         st = obj.get("status") or {}
         if "started" not in rec:
             for cs in st.get("containerStatuses") or []:
                 s = cs.get("state") or {}
                 if "running" in s or "terminated" in s:
                     rec["started"] = now
+                    POD_TRACE(uid, "bench_started")
         ph = st.get("phase")
         if rec.get("cpu"):
             if ph == "Running" and "started" in rec and "done" not in rec:
@@ -172,10 +176,12 @@ class PodBench:
             self.t[nm] = {"wave": 0, "cpu": nm in cpu}
             self.done_events[nm] = asyncio.Event()
         creates = []
+        tw = time.time()
         for nm in gpu + cpu:
             self.t[nm]["create"] = time.perf_counter()
             creates.append(self.lc.client.create(self.pod(nm) if nm in gpu else self.cpu_pod(nm), "default"))
-        await asyncio.gather(*creates)
+        for obj in await asyncio.gather(*creates):
+            POD_TRACE(m.uid_of(obj), "bench_create", tw)
         await asyncio.wait_for(asyncio.gather(*(self.done_events[nm].wait() for nm in gpu + cpu)), timeout)
         self.pending_cleanup = cpu
         return gpu + cpu

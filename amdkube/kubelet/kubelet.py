@@ -40,6 +40,7 @@ from ..utils.features import FeatureGate
 from ..utils.metrics import MICRO_BUCKETS, Counter, Gauge, Histogram, Summary, new_registry
 from .cri_client import CURRENT_POD, CRIClient
 from .devicemanager import AdmissionError, ManagerImpl, ManagerStub
+from ..utils.trace import POD_TRACE
 from .kuberuntime import L_POD_UID, RuntimeManager, SandboxRef, apply_event
 from .status import StatusManager, generate_status
 
@@ -350,6 +351,7 @@ class Kubelet:
         uid = m.uid_of(pod)
         self.pods[uid] = pod
         self.first_seen.setdefault(uid, time.time())
+        POD_TRACE(uid, "kubelet_seen")
         self.dispatch(uid)
 
     def _on_pod_update(self, old, pod):
@@ -553,6 +555,7 @@ class Kubelet:
                 ok, reason, msg = False, "UnexpectedAdmissionError", f"device admission failed: {e!r}"
         if ok:
             self.admitted.add(uid)
+            POD_TRACE(uid, "admitted")
             return True
         self.rejected[uid] = (reason, msg)
         log.warning("pod %s/%s rejected: %s %s", m.namespace_of(pod), m.name_of(pod), reason, msg)
@@ -604,6 +607,7 @@ class Kubelet:
             await self.runtime.kill_pod(uid, 0, pod, self._cached_sandboxes(uid))
             return False
         ctx = await self._pod_context(pod)
+        POD_TRACE(uid, "sync_ctx")
         rt = await self._cached_status(uid)
         mut0 = self.cri.pod_mutations(uid)
         errors = await self.runtime.sync_pod(pod, rt, ctx, self.liveness_failed.pop(uid, None))
@@ -614,6 +618,8 @@ class Kubelet:
         st = generate_status(pod, rt, self.cfg.node_ip, self.readiness.get(uid, {}), errors, m.now_rfc3339())
         prev_phase = (self.status.get(uid) or {}).get("phase")
         self.status.set(pod, st)
+        if st["phase"] != prev_phase:
+            POD_TRACE(uid, "status_" + st["phase"])
         if st["phase"] == "Running" and prev_phase != "Running" and uid in self.first_seen:
             ct = m.parse_time(md.get("creationTimestamp"))
             if ct:

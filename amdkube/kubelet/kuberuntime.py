@@ -21,6 +21,7 @@ import time
 import grpc
 
 from ..security.apparmor import profile_name as apparmor_profile_name
+from ..utils.trace import POD_TRACE
 from ..grpcdesc.cri import CRI as C
 from .cri_client import CRIClient
 
@@ -255,6 +256,7 @@ class RuntimeManager:
                 no_new_privs=not bool(((c.get("securityContext") or {}).get("allowPrivilegeEscalation", True))))))
         cid = await self.cri.create_container(sid, cfg, sandbox_cfg)
         await self.cri.start_container(cid)
+        POD_TRACE(pod["metadata"]["uid"], "container_started")
         return cid
 
     # ------------------------------------------------------------------ sync
@@ -273,7 +275,9 @@ class RuntimeManager:
                 await self.cri.stop_container(c.id, 2)
             attempt = (st.sandboxes[0][2] + 1) if st.sandboxes else 0
             sandbox_cfg = self.sandbox_config(pod, attempt, self.dm.pod_resources(pod))
+            POD_TRACE(uid, "sandbox_start")
             sid = await self.cri.run_pod_sandbox(sandbox_cfg)
+            POD_TRACE(uid, "sandbox_ready")
             st = PodRuntimeStatus(uid)
             st.sandboxes = [(sid, C.SANDBOX_READY, attempt, time.time_ns())]
         else:

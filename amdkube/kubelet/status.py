@@ -12,6 +12,7 @@ import logging
 import time
 
 from ..api import meta as m
+from ..utils.trace import POD_TRACE
 from ..grpcdesc.cri import CRI as C
 
 log = logging.getLogger("amdkube.kubelet.status")
@@ -203,6 +204,7 @@ class StatusManager:
             return
         try:
             await self.client.patch("pods", ref["name"], {"status": status}, ref["namespace"], sub="status")
+            POD_TRACE(uid, "sent_" + str(status.get("phase")))
             self.sent[uid] = status
             self.updates += 1
             if status.get("phase") in ("Succeeded", "Failed"):

@@ -17,6 +17,7 @@ import time
 
 from aiohttp import web
 
+from ..utils.trace import POD_TRACE
 from ..api import meta as m
 from ..api.helpers import is_pod_terminal
 from ..client import Client, EventRecorder, Informer, LeaderElector
@@ -224,6 +225,7 @@ class Scheduler:
             return
         pod = cur
         t0 = time.perf_counter()
+        POD_TRACE(m.uid_of(pod), "sched_start")
         try:
             host, binding = await self.algo.schedule(pod)
         except FitError as e:
@@ -252,6 +254,7 @@ class Scheduler:
         t.add_done_callback(self._binds.discard)
 
     async def _bind(self, pod, assumed, host, binding, t0):
+        POD_TRACE(m.uid_of(pod), "sched_assumed")
         async with self.bind_sem:
             tb = time.perf_counter()
             try:
@@ -277,6 +280,7 @@ class Scheduler:
             now = time.perf_counter()
             self.m_bind.observe((now - tb) * 1e6)
             self.m_e2e.observe((now - t0) * 1e6)
+            POD_TRACE(m.uid_of(pod), "sched_bound")
             self.m_attempts.labels("scheduled").inc()
             self.scheduled += 1
             self.recorder.event(pod, "Normal", "Scheduled", f"Successfully assigned {m.name_of(pod)} to {host}")

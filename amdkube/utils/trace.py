@@ -45,3 +45,26 @@ class Trace:
 
     def __exit__(self, *exc):
         return False
+
+
+class PodStageTracer:
+    """Pod-startup stage timestamps, one JSON line per (pod uid, stage, wall time), written when
+    AMDKUBE_POD_TRACE names a file. Every component appends to its own file (<path>.<pid>);
+    hack/pod_timeline.py joins them into per-stage latency percentiles. Wall-clock times
+    (time.time) so processes on one node line up."""
+
+    def __init__(self, path: str | None = None):
+        import os
+        path = path if path is not None else os.environ.get("AMDKUBE_POD_TRACE")
+        self.f = open(f"{path}.{os.getpid()}", "a", buffering=1 << 16) if path else None
+
+    def __call__(self, uid: str, stage: str, t: float | None = None):
+        if self.f is not None:
+            self.f.write(f'{{"uid":"{uid}","stage":"{stage}","t":{time.time() if t is None else t:.6f}}}\n')
+
+    def flush(self):
+        if self.f is not None:
+            self.f.flush()
+
+
+POD_TRACE = PodStageTracer()
