@@ -91,12 +91,12 @@ class Scheme:
 SCHEME = Scheme()
 
 _CORE = [
-    ("Pod", "pods", True, ("po",), ("status", "binding", "eviction", "log")),
-    ("Node", "nodes", False, ("no",), ("status",)),
+    ("Pod", "pods", True, ("po",), ("status", "binding", "eviction", "log", "exec", "attach", "portforward", "proxy")),
+    ("Node", "nodes", False, ("no",), ("status", "proxy")),
     ("Binding", "bindings", True, (), ()),
     ("Event", "events", True, ("ev",), ()),
     ("Namespace", "namespaces", False, ("ns",), ("status", "finalize")),
-    ("Service", "services", True, ("svc",), ("status",)),
+    ("Service", "services", True, ("svc",), ("status", "proxy")),
     ("Endpoints", "endpoints", True, ("ep",), ()),
     ("ConfigMap", "configmaps", True, ("cm",), ()),
     ("Secret", "secrets", True, (), ()),

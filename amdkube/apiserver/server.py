@@ -37,6 +37,9 @@ log = logging.getLogger("amdkube.apiserver")
 _JSON = "application/json"
 
 
+_STREAMING_SUBS = {"exec", "attach", "portforward", "proxy"}
+
+
 def _to_scale(obj: dict) -> dict:
     """autoscaling/v1 Scale view of a scalable object (registry/*/storage ScaleREST)."""
     from ..api.labels import selector_from_label_selector, selector_from_set
@@ -332,12 +335,18 @@ class APIServer:
             is_watch = watch or q.get("watch") in ("true", "1")
             kverb = {"GET": "watch" if is_watch else ("get" if name else "list"), "POST": "create", "PUT": "update",
                      "PATCH": "patch", "DELETE": "delete" if name else "deletecollection"}.get(verb, verb.lower())
+            top_sub = sub.split("/")[0] if sub else ""
+            if name and top_sub in _STREAMING_SUBS:
+                kverb = "create"   # exec/attach/portforward/proxy always need create on the subresource
             verb = kverb.upper()
-            self._authorize(user, kverb, resource, group, "" if not rs.ri.namespaced else ns, name or "",
-                            "" if sub in ("",) else sub.split("/")[0])
+            self._authorize(user, kverb, resource, group, "" if not rs.ri.namespaced else ns, name or "", top_sub)
             if is_watch:
                 code = 200
                 return await self._watch(request, rs, ns, name, q)
+            if name and top_sub in _STREAMING_SUBS:   # long-running: exempt from max-in-flight, like watches
+                resp = await self._stream(request, rs, ns, name, sub, q)
+                code = resp.status
+                return resp
             sem = self._rw if request.method in ("POST", "PUT", "PATCH", "DELETE") else self._ro
             if sem is not None:
                 if sem.locked():
@@ -552,6 +561,83 @@ class APIServer:
         else:
             data = json.dumps(obj, separators=(",", ":")).encode()
         return b'{"type":"' + typ.encode() + b'","object":' + data + b"}\n"
+
+    def _kubelet_addr(self, node_name: str) -> tuple[str, int]:
+        node = self.registry.rs("nodes").get("", node_name)
+        st = node.get("status") or {}
+        port = (((st.get("daemonEndpoints") or {}).get("kubeletEndpoint")) or {}).get("Port")
+        addr = next((a["address"] for a in st.get("addresses") or [] if a.get("type") == "InternalIP"), None) or \
+            next((a["address"] for a in st.get("addresses") or [] if a.get("type") == "Hostname"), "127.0.0.1")
+        if not port:
+            raise m.bad_request(f"node {node_name} has no kubelet endpoint")
+        return addr, int(port)
+
+    async def _stream(self, request, rs, ns, name, sub, q):
+        """pods/{name}/exec|attach|portforward (WebSocket relayed to the node's kubelet,
+        registry/core/pod/rest/subresources.go) and pods|services|nodes/{name}/proxy/{path}
+        (HTTP proxy to the pod IP, a service endpoint or the kubelet)."""
+        from ..runtime.streaming import CHANNEL_PROTOCOLS, PORTFORWARD_PROTOCOLS, bridge
+        plural = rs.ri.plural
+        top, _, rest = sub.partition("/")
+        if top == "proxy":
+            return await self._proxy(request, plural, ns, name, rest, q)
+        if plural != "pods":
+            raise m.not_found("subresource", sub)
+        pod = rs.get(ns, name)
+        node_name = (pod.get("spec") or {}).get("nodeName")
+        if not node_name:
+            raise m.bad_request(f'pod "{name}" is not scheduled yet')
+        addr, port = self._kubelet_addr(node_name)
+        qs = request.query_string
+        if top == "portforward":
+            url, protos = f"http://{addr}:{port}/portForward/{ns}/{name}?{qs}", PORTFORWARD_PROTOCOLS
+        else:
+            container = q.get("container") or ((pod.get("spec") or {}).get("containers") or [{}])[0].get("name", "")
+            url, protos = f"http://{addr}:{port}/{top}/{ns}/{name}/{container}?{qs}", CHANNEL_PROTOCOLS
+        ws = web.WebSocketResponse(protocols=protos, max_msg_size=0)
+        if not ws.can_prepare(request).ok:
+            raise m.bad_request(f"{top} needs a WebSocket upgrade (protocols {', '.join(protos)})")
+        await ws.prepare(request)
+        return await bridge(ws, url, [ws.ws_protocol or protos[0]])
+
+    async def _proxy(self, request, plural, ns, name, path, q):
+        if self._http is None:
+            self._http = ClientSession(timeout=ClientTimeout(total=None))
+        if plural == "nodes":
+            addr, port = self._kubelet_addr(name)
+            target = f"http://{addr}:{port}"
+        elif plural == "pods":
+            pod_name, _, pport = name.partition(":")
+            pod = self.registry.rs("pods").get(ns, pod_name)
+            ip = (pod.get("status") or {}).get("podIP")
+            if not ip:
+                raise m.bad_request(f'pod "{pod_name}" has no IP')
+            if not pport:
+                ports = [p for c in (pod.get("spec") or {}).get("containers") or [] for p in c.get("ports") or []]
+                pport = str(ports[0]["containerPort"]) if ports else "80"
+            target = f"http://{ip}:{pport}"
+        elif plural == "services":
+            svc_name, _, sport = name.partition(":")
+            ep = self.registry.rs("endpoints").get(ns, svc_name)
+            for subset in ep.get("subsets") or []:
+                addrs = subset.get("addresses") or []
+                ports = subset.get("ports") or []
+                if not addrs or not ports:
+                    continue
+                p = next((x for x in ports if not sport or x.get("name") == sport or str(x.get("port")) == sport), None)
+                if p is not None:
+                    target = f"http://{addrs[0]['ip']}:{p['port']}"
+                    break
+            else:
+                raise m.StatusError(503, "ServiceUnavailable", f'no endpoints available for service "{svc_name}"')
+        else:
+            raise m.not_found("subresource", "proxy")
+        body = await request.read()
+        hdrs = {k: v for k, v in request.headers.items() if k.lower() not in ("host", "authorization", "content-length")}
+        async with self._http.request(request.method, f"{target}/{path}", params=q, data=body or None, headers=hdrs) as r:
+            data = await r.read()
+            return web.Response(status=r.status, body=data,
+                                headers={k: v for k, v in r.headers.items() if k.lower() in ("content-type", "cache-control")})
 
     async def _pod_log(self, request, ns, name, q):
         pod = self.registry.rs("pods").get(ns, name)

@@ -3,8 +3,8 @@
 Field numbers follow pkg/kubelet/apis/cri/v1alpha1/runtime/api.proto (services :17-104,
 Device :572-582, ContainerConfig :586-645, ContainerStatus :762-797) so that a CRI
 client written against that proto interoperates with amdkube's rocshim. Messages not
-needed by amdkube (Exec/Attach/PortForward streaming URLs, SELinux details) are kept
-minimal but wire-compatible where present.
+needed by amdkube (SELinux details, …) are left out; Exec/Attach/PortForward return URLs of
+rocshim's streaming server (runtime/streaming.py) as in the reference.
 """
 from __future__ import annotations
 
@@ -29,6 +29,9 @@ service RuntimeService {
   rpc ContainerStatus(ContainerStatusRequest) returns (ContainerStatusResponse) {}
   rpc UpdateContainerResources(UpdateContainerResourcesRequest) returns (UpdateContainerResourcesResponse) {}
   rpc ExecSync(ExecSyncRequest) returns (ExecSyncResponse) {}
+  rpc Exec(ExecRequest) returns (ExecResponse) {}
+  rpc Attach(AttachRequest) returns (AttachResponse) {}
+  rpc PortForward(PortForwardRequest) returns (PortForwardResponse) {}
   rpc ContainerStats(ContainerStatsRequest) returns (ContainerStatsResponse) {}
   rpc ListContainerStats(ListContainerStatsRequest) returns (ListContainerStatsResponse) {}
   rpc UpdateRuntimeConfig(UpdateRuntimeConfigRequest) returns (UpdateRuntimeConfigResponse) {}
@@ -135,6 +138,12 @@ message UpdateContainerResourcesRequest { string container_id = 1; LinuxContaine
 message UpdateContainerResourcesResponse {}
 message ExecSyncRequest { string container_id = 1; repeated string cmd = 2; int64 timeout = 3; }
 message ExecSyncResponse { bytes stdout = 1; bytes stderr = 2; int32 exit_code = 3; }
+message ExecRequest { string container_id = 1; repeated string cmd = 2; bool tty = 3; bool stdin = 4; bool stdout = 5; bool stderr = 6; }
+message ExecResponse { string url = 1; }
+message AttachRequest { string container_id = 1; bool stdin = 2; bool tty = 3; bool stdout = 4; bool stderr = 5; }
+message AttachResponse { string url = 1; }
+message PortForwardRequest { string pod_sandbox_id = 1; repeated int32 port = 2; }
+message PortForwardResponse { string url = 1; }
 message ImageFilter { ImageSpec image = 1; }
 message ListImagesRequest { ImageFilter filter = 1; }
 message Image { string id = 1; repeated string repo_tags = 2; repeated string repo_digests = 3; uint64 size = 4; Int64Value uid = 5; string username = 6; }

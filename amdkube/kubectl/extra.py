@@ -7,9 +7,8 @@ auth/cani.go, certificates.go (approve/deny), portforward.go, proxy.go, cp.go, e
 create_*.go generators (namespace, configmap, secret generic, serviceaccount, deployment,
 job, priorityclass, quota, role/clusterrole/rolebinding/clusterrolebinding).
 
-Differences: `port-forward` dials the pod IP directly (pods here are reachable from the
-node; the reference tunnels through the kubelet's SPDY stream), and `cp` moves the file
-as base64 through the kubelet's exec endpoint (so it is bounded to 1 MiB).
+exec/attach/port-forward/cp go through the apiserver's WebSocket subresources (the reference
+also speaks SPDY; amdkube serves the WebSocket channel protocols only).
 """
 from __future__ import annotations
 
@@ -441,6 +440,8 @@ async def port_forward(c, ns, name, mappings, ready=None, stop=None):
 
 
 async def cmd_port_forward(c, a):
+    """Through the apiserver (pods/portforward WebSocket → kubelet → runtime), like the reference."""
+    from ..client.stream import port_forward as api_port_forward
     ri, name, rest = _target(a) if "/" in a.args[0] else (SCHEME.resolve("pods"), a.args[0], a.args[1:])
     if ri.kind != "Pod":
         obj = await c.get(_res(ri), name, _ns(a, ri))
@@ -451,7 +452,7 @@ async def cmd_port_forward(c, a):
         if not running:
             raise SystemExit("error: no running pod found")
         name = m.name_of(running[0])
-    await port_forward(c, a.namespace or "default", name, rest)
+    await api_port_forward(c, a.namespace or "default", name, rest)
 
 
 async def cmd_proxy(c, a):
@@ -478,29 +479,30 @@ async def cmd_proxy(c, a):
 
 
 async def cmd_cp(c, a):
-    from .main import kubelet_exec
+    """Files move through exec streams (cat / sh -c 'cat > f'), as kubectl cp uses tar over exec."""
+    from ..client.stream import exec_stream
     if len(a.args) != 2:
         raise SystemExit("error: cp SRC DST (one side as [NAMESPACE/]POD:PATH)")
     src, dst = a.args
+    errb = bytearray()
     if ":" in src:
         pod, _, path = src.partition(":")
         ns, _, pod = pod.rpartition("/")
-        out, rc = await kubelet_exec(c, ns or a.namespace or "default", pod, a.container, ["base64", path])
+        outb = bytearray()
+        rc = await exec_stream(c, ns or a.namespace or "default", pod, ["cat", path], a.container,
+                               on_stdout=outb.extend, on_stderr=errb.extend)
         if rc != 0:
-            raise SystemExit(f"error: {out.decode(errors='replace').strip()}")
+            raise SystemExit(f"error: {errb.decode(errors='replace').strip()}")
         with open(dst, "wb") as f:
-            f.write(base64.b64decode(out))
+            f.write(outb)
     else:
         pod, _, path = dst.partition(":")
         ns, _, pod = pod.rpartition("/")
         data = open(src, "rb").read()
-        if len(data) > 1 << 20:
-            raise SystemExit("error: cp into a pod is limited to 1 MiB")
-        enc = base64.b64encode(data).decode()
-        out, rc = await kubelet_exec(c, ns or a.namespace or "default", pod, a.container,
-                                     ["sh", "-c", f"echo {enc} | base64 -d > '{path}'"])
+        rc = await exec_stream(c, ns or a.namespace or "default", pod, ["sh", "-c", 'cat > "$0"', path], a.container,
+                               stdin=data, on_stderr=errb.extend)
         if rc != 0:
-            raise SystemExit(f"error: {out.decode(errors='replace').strip()}")
+            raise SystemExit(f"error: {errb.decode(errors='replace').strip()}")
 
 
 async def cmd_explain(c, a):

@@ -254,10 +254,29 @@ async def kubelet_exec(c, ns: str, name: str, container: str | None, cmd: list[s
             return await r.read(), int(r.headers.get("X-Exit-Code", "0"))
 
 
+async def _stdin_chunks():
+    loop = asyncio.get_running_loop()
+    while True:
+        data = await loop.run_in_executor(None, sys.stdin.buffer.read1, 65536)
+        if not data:
+            return
+        yield data
+
+
 async def cmd_exec(c, a):
-    out, rc = await kubelet_exec(c, a.namespace or "default", a.args[0].split("/", 1)[-1], a.container, a.command)
-    sys.stdout.write(out.decode(errors="replace"))
-    return rc
+    """exec through the apiserver (pods/exec WebSocket), -i forwards stdin, -t asks for a tty."""
+    from ..client.stream import exec_stream
+    out = lambda b: (sys.stdout.buffer.write(b), sys.stdout.buffer.flush())   # noqa: E731
+    err = lambda b: (sys.stderr.buffer.write(b), sys.stderr.buffer.flush())   # noqa: E731
+    return await exec_stream(c, a.namespace or "default", a.args[0].split("/", 1)[-1], a.command, a.container,
+                             stdin=_stdin_chunks() if a.stdin else None, tty=a.tty, on_stdout=out, on_stderr=err)
+
+
+async def cmd_attach(c, a):
+    from ..client.stream import exec_stream
+    out = lambda b: (sys.stdout.buffer.write(b), sys.stdout.buffer.flush())   # noqa: E731
+    return await exec_stream(c, a.namespace or "default", a.args[0].split("/", 1)[-1], [], a.container, attach=True,
+                             on_stdout=out, on_stderr=out)
 
 
 async def _meta_edit(c, a, field):
@@ -411,7 +430,7 @@ COMMANDS = {"get": cmd_get, "describe": cmd_describe, "create": cmd_create, "app
             "logs": cmd_logs, "exec": cmd_exec, "label": cmd_label, "annotate": cmd_annotate, "cordon": cmd_cordon,
             "uncordon": cmd_uncordon, "drain": cmd_drain, "scale": cmd_scale, "patch": cmd_patch, "run": cmd_run,
             "top": cmd_top, "version": cmd_version, "api-resources": cmd_api_resources, "cluster-info": cmd_cluster_info,
-            "wait": cmd_wait}
+            "wait": cmd_wait, "attach": cmd_attach}
 from .extra import COMMANDS as _EXTRA, add_arguments as _extra_args  # noqa: E402
 COMMANDS.update(_EXTRA)
 
@@ -436,6 +455,8 @@ def parser():
         sp.add_argument("-w", "--watch", action="store_true")
         sp.add_argument("-f", "--filename", action="append", default=[])
         sp.add_argument("-c", "--container", default=None)
+        sp.add_argument("-i", "--stdin", action="store_true")
+        sp.add_argument("-t", "--tty", action="store_true")
         sp.add_argument("--tail", type=int, default=-1)
         sp.add_argument("--all", action="store_true")
         sp.add_argument("--grace-period", type=int, default=-1)

@@ -123,6 +123,17 @@ class CRIClient:
                              timeout=timeout + 5)
         return r.stdout, r.stderr, r.exit_code
 
+    async def exec_url(self, cid, cmd, tty=False, stdin=False, stdout=True, stderr=True) -> str:
+        req = C.ExecRequest(container_id=cid, cmd=cmd, tty=tty, stdin=stdin, stdout=stdout, stderr=stderr)
+        return (await self._call("exec", self.rt.Exec, req)).url
+
+    async def attach_url(self, cid, tty=False, stdin=False, stdout=True, stderr=True) -> str:
+        req = C.AttachRequest(container_id=cid, tty=tty, stdin=stdin, stdout=stdout, stderr=stderr)
+        return (await self._call("attach", self.rt.Attach, req)).url
+
+    async def port_forward_url(self, sid, ports) -> str:
+        return (await self._call("port_forward", self.rt.PortForward, C.PortForwardRequest(pod_sandbox_id=sid, port=ports))).url
+
     async def list_container_stats(self):
         return list((await self._call("list_container_stats", self.rt.ListContainerStats, C.ListContainerStatsRequest())).stats)
 

@@ -2,7 +2,9 @@
 syncloop check), /pods, /runningpods/, /metrics, /metrics/cadvisor (per-container
 accelerator series), /stats/summary (stats/v1alpha1 incl. Accelerators[], types.go:121-122,
 213-230), /spec, /containerLogs/{ns}/{pod}/{container}, /run/{ns}/{pod}/{container}
-(exec-sync) and /debug/pprof."""
+(exec-sync), the streaming endpoints /exec, /attach and /portForward (relayed WebSockets to
+the runtime's streaming server, server.go:296-330 with redirect-container-streaming=false) and
+/debug/pprof."""
 from __future__ import annotations
 
 import asyncio
@@ -35,6 +37,10 @@ class KubeletServer:
         app.router.add_get("/spec", self.spec)
         app.router.add_get("/containerLogs/{ns}/{pod}/{container}", self.logs)
         app.router.add_post("/run/{ns}/{pod}/{container}", self.run)
+        for meth in ("GET", "POST"):
+            app.router.add_route(meth, "/exec/{ns}/{pod}/{container}", self.exec_stream)
+            app.router.add_route(meth, "/attach/{ns}/{pod}/{container}", self.attach_stream)
+            app.router.add_route(meth, "/portForward/{ns}/{pod}", self.port_forward)
         profiling.add_routes(app)
         self.runner = None
         self.port = None
@@ -149,6 +155,55 @@ class KubeletServer:
                 rt = await self.k.runtime.pod_status(uid)
                 return rt.latest(cname)
         return None
+
+    @staticmethod
+    def _flag(req, name, default=False) -> bool:
+        v = req.query.get(name)
+        return default if v is None else v.lower() in ("1", "true", "yes")
+
+    async def exec_stream(self, req):
+        from ..runtime.streaming import CHANNEL_PROTOCOLS, bridge
+        ns, pod, cname = req.match_info["ns"], req.match_info["pod"], req.match_info["container"]
+        cmd = req.query.getall("command", [])
+        cs = await self._find_container(ns, pod, cname)
+        if cs is None:
+            return web.Response(status=404, text=f"container {cname} of pod {ns}/{pod} not found")
+        if not cmd:
+            return web.Response(status=400, text="command is required")
+        url = await self.k.cri.exec_url(cs.id, cmd, self._flag(req, "tty"), self._flag(req, "stdin"),
+                                        self._flag(req, "stdout", True), self._flag(req, "stderr", True))
+        ws = web.WebSocketResponse(protocols=CHANNEL_PROTOCOLS, max_msg_size=0)
+        await ws.prepare(req)
+        return await bridge(ws, url, [ws.ws_protocol or CHANNEL_PROTOCOLS[0]])
+
+    async def attach_stream(self, req):
+        from ..runtime.streaming import CHANNEL_PROTOCOLS, bridge
+        ns, pod, cname = req.match_info["ns"], req.match_info["pod"], req.match_info["container"]
+        cs = await self._find_container(ns, pod, cname)
+        if cs is None:
+            return web.Response(status=404, text=f"container {cname} of pod {ns}/{pod} not found")
+        url = await self.k.cri.attach_url(cs.id, self._flag(req, "tty"), self._flag(req, "stdin"),
+                                          self._flag(req, "stdout", True), self._flag(req, "stderr", True))
+        ws = web.WebSocketResponse(protocols=CHANNEL_PROTOCOLS, max_msg_size=0)
+        await ws.prepare(req)
+        return await bridge(ws, url, [ws.ws_protocol or CHANNEL_PROTOCOLS[0]])
+
+    async def port_forward(self, req):
+        from ..runtime.streaming import PORTFORWARD_PROTOCOLS, bridge
+        ns, pod = req.match_info["ns"], req.match_info["pod"]
+        ports = [int(p) for p in req.query.getall("port", []) + req.query.getall("ports", []) for p in p.split(",") if p]
+        sid = None
+        for uid, p in self.k.pods.items():
+            if m.namespace_of(p) == ns and m.name_of(p) == pod:
+                rt = await self.k.runtime.pod_status(uid)
+                ready = rt.ready_sandbox()
+                sid = ready[0] if ready else None
+        if sid is None or not ports:
+            return web.Response(status=404 if sid is None else 400, text="pod sandbox not ready" if sid is None else "port is required")
+        url = await self.k.cri.port_forward_url(sid, ports)
+        ws = web.WebSocketResponse(protocols=PORTFORWARD_PROTOCOLS, max_msg_size=0)
+        await ws.prepare(req)
+        return await bridge(ws, url + "?" + "&".join(f"port={p}" for p in ports), [ws.ws_protocol or PORTFORWARD_PROTOCOLS[0]])
 
     async def logs(self, req):
         ns, pod, cname = req.match_info["ns"], req.match_info["pod"], req.match_info["container"]

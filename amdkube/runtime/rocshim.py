@@ -26,6 +26,7 @@ import logging
 import os
 import shutil
 import signal
+import subprocess
 import time
 import uuid
 
@@ -49,6 +50,47 @@ SCRUB_ENV = ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICE
 def now_ns() -> int:
     return time.time_ns()
 
+
+
+class PidProc:
+    """A child process watched through a pidfd on the event loop (Linux ≥ 5.3): no transport,
+    pipes or per-child waiter thread, which asyncio.create_subprocess_exec costs per spawn
+    (ThreadedChildWatcher). `wait()` returns the returncode as subprocess does (−signal)."""
+    __slots__ = ("pid", "returncode", "_popen", "_fd", "_fut")
+
+    def __init__(self, popen: subprocess.Popen, fd: int):
+        loop = asyncio.get_running_loop()
+        self.pid, self.returncode, self._popen, self._fd = popen.pid, None, popen, fd
+        self._fut = loop.create_future()
+        loop.add_reader(fd, self._exited)
+
+    def _exited(self):
+        asyncio.get_running_loop().remove_reader(self._fd)
+        os.close(self._fd)
+        self.returncode = self._popen.wait()
+        if not self._fut.done():
+            self._fut.set_result(self.returncode)
+
+    async def wait(self):
+        return await asyncio.shield(self._fut)
+
+
+async def spawn(argv, stdout=None, stderr=None, env=None, cwd=None):
+    """Start argv in its own session with stdin from /dev/null; pidfd-watched when possible."""
+    p = subprocess.Popen(argv, stdin=subprocess.DEVNULL, stdout=stdout if stdout is not None else subprocess.DEVNULL,
+                         stderr=stderr if stderr is not None else subprocess.DEVNULL, env=env, cwd=cwd,
+                         start_new_session=True)
+    try:
+        fd = os.pidfd_open(p.pid)
+    except (AttributeError, OSError):
+        fd = None
+    if fd is None:   # old kernel: a thread waits for the child
+        loop = asyncio.get_running_loop()
+        proc = PidProc.__new__(PidProc)
+        proc.pid, proc.returncode, proc._popen, proc._fd = p.pid, None, p, -1
+        proc._fut = loop.run_in_executor(None, p.wait)
+        return proc
+    return PidProc(p, fd)
 
 class Sandbox:
     def __init__(self, sid, config_bytes, meta, labels, annotations, log_dir):
@@ -82,7 +124,7 @@ class Container:
         self.reason = ""
         self.message = ""
         self.pid = 0
-        self.proc: asyncio.subprocess.Process | None = None
+        self.proc: PidProc | None = None
         self.waiter: asyncio.Task | None = None
 
     def to_json(self):
@@ -115,6 +157,8 @@ class RocShim:
         self.started = 0
         self._adopt_tasks: set = set()
         self._event_streams: set[asyncio.Queue] = set()
+        self.streaming = None
+        self.streaming_port = 0     # loopback port of the exec/attach/port-forward server (0: any)
 
     def _emit(self, c: "Container | None", etype: int, sid: str | None = None):
         """Evented PLEG (KEP-3386 ContainerEventResponse): every event carries the sandbox's full
@@ -153,6 +197,8 @@ class RocShim:
         self.server.add_generic_rpc_handlers((C.RuntimeService.handler(_Runtime(self)), C.ImageService.handler(_Images(self))))
         self.server.add_insecure_port("unix://" + self.socket)
         await self.server.start()
+        from .streaming import StreamingServer
+        self.streaming = await StreamingServer(self, port=self.streaming_port).start()
         log.info("rocshim serving CRI on %s (isolation=%s)", self.socket, self.isolation)
         return self
 
@@ -161,6 +207,8 @@ class RocShim:
             for s in list(self.sandboxes.values()):
                 await self.stop_sandbox(s.id)
         await self.hooks.stop()
+        if self.streaming is not None:
+            await self.streaming.stop()
         if self.server:
             await self.server.stop(0.5)
         for t in list(self._adopt_tasks):
@@ -237,9 +285,7 @@ class RocShim:
         os.makedirs(log_dir, exist_ok=True)
         s = Sandbox(sid, cfg.SerializeToString(), meta, dict(cfg.labels), dict(cfg.annotations), log_dir)
         os.makedirs(os.path.join(self.state_dir, "rootfs", sid), exist_ok=True)
-        proc = await asyncio.create_subprocess_exec(self.pause_bin, stdin=asyncio.subprocess.DEVNULL,
-                                                    stdout=asyncio.subprocess.DEVNULL, stderr=asyncio.subprocess.DEVNULL,
-                                                    start_new_session=True)
+        proc = await spawn([self.pause_bin])
         s.proc, s.pid = proc, proc.pid
         host_net = True
         try:
@@ -404,8 +450,7 @@ class RocShim:
             raise ValueError(f"container {cid} is not in created state")
         logf = open(c.log_path, "ab", buffering=0)
         try:
-            proc = await asyncio.create_subprocess_exec(*self._launch_argv(c), stdin=asyncio.subprocess.DEVNULL, stdout=logf,
-                                                        stderr=logf, env=c.env, cwd=c.cwd, start_new_session=True)
+            proc = await spawn(self._launch_argv(c), stdout=logf, stderr=logf, env=c.env, cwd=c.cwd)
         except (OSError, ValueError) as e:
             logf.close()
             c.state, c.exit_code, c.reason, c.message = C.CONTAINER_EXITED, 128, "StartError", str(e)
@@ -680,6 +725,25 @@ class _Runtime:
             c.resources = {"cpu_quota": req.linux.cpu_quota, "cpu_period": req.linux.cpu_period,
                            "memory_limit": req.linux.memory_limit_in_bytes}
         return C.UpdateContainerResourcesResponse()
+
+    async def Exec(self, req, ctx):
+        c = self.r.containers.get(req.container_id)
+        if c is None or c.state != C.CONTAINER_RUNNING:
+            await ctx.abort(grpc.StatusCode.NOT_FOUND, f"container {req.container_id} is not running")
+        if not req.cmd:
+            await ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, "cmd is required")
+        return C.ExecResponse(url=self.r.streaming.get_exec(req.container_id, req.cmd, req.tty, req.stdin, req.stdout, req.stderr))
+
+    async def Attach(self, req, ctx):
+        if req.container_id not in self.r.containers:
+            await ctx.abort(grpc.StatusCode.NOT_FOUND, f"container {req.container_id} not found")
+        return C.AttachResponse(url=self.r.streaming.get_attach(req.container_id, req.tty, req.stdin, req.stdout, req.stderr))
+
+    async def PortForward(self, req, ctx):
+        s = self.r.sandboxes.get(req.pod_sandbox_id)
+        if s is None or s.state != C.SANDBOX_READY:
+            await ctx.abort(grpc.StatusCode.NOT_FOUND, f"sandbox {req.pod_sandbox_id} is not ready")
+        return C.PortForwardResponse(url=self.r.streaming.get_portforward(req.pod_sandbox_id, list(req.port)))
 
     async def ExecSync(self, req, ctx):
         try:
