@@ -196,6 +196,9 @@ def kubelet(argv):
     ap.add_argument("--feature-gates", default="")
     ap.add_argument("--chaos-chance", type=float, default=0.0)
     ap.add_argument("--pod-manifest-path", default=None, help="directory of static pod manifests")
+    ap.add_argument("--cluster-dns", default="", help="comma-separated DNS server IPs for ClusterFirst pods")
+    ap.add_argument("--cluster-domain", default="", help="cluster DNS domain (e.g. cluster.local)")
+    ap.add_argument("--resolv-conf", default="/etc/resolv.conf", help="resolver file used as the base of pod DNS")
     ap.add_argument("--file-check-frequency", type=float, default=20.0)
     ap.add_argument("--gpu-stats-backend", default="auto")
     ap.add_argument("--kube-api-qps", type=float, default=0)
@@ -217,7 +220,9 @@ def kubelet(argv):
                         relist_period=a.pleg_relist_period, max_pods=a.max_pods, node_labels=labels,
                         register_with_taints=taints, feature_gates=a.feature_gates, chaos_chance=a.chaos_chance,
                         pod_manifest_path=a.pod_manifest_path, file_check_frequency=a.file_check_frequency,
-                        gpu_stats_backend=a.gpu_stats_backend)
+                        gpu_stats_backend=a.gpu_stats_backend,
+                        cluster_dns=[x for x in a.cluster_dns.split(",") if x], cluster_domain=a.cluster_domain,
+                        resolv_conf=a.resolv_conf)
 
     async def mk():
         smi = None
@@ -368,6 +373,27 @@ def proxy(argv):
     _run_forever(mk)
 
 
+def dns(argv):
+    """Cluster DNS addon (kube-dns equivalent, amdkube/dns)."""
+    ap = argparse.ArgumentParser("amdkube dns")
+    ap.add_argument("--master", "--server", dest="server", default="http://127.0.0.1:8080")
+    ap.add_argument("--kubeconfig", default=None)
+    ap.add_argument("--token", default=None)
+    ap.add_argument("--domain", "--cluster-domain", dest="domain", default="cluster.local")
+    ap.add_argument("--dns-bind-address", default="127.0.0.1")
+    ap.add_argument("--dns-port", type=int, default=53)
+    ap.add_argument("--upstream", default=None, help="comma-separated upstream servers (default: the host's resolv.conf)")
+    ap.add_argument("-v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "dns")
+    from ..dns import DNSServer
+
+    async def mk():
+        up = [x for x in a.upstream.split(",") if x] if a.upstream is not None else None
+        return await DNSServer(_client(a), a.domain, a.dns_bind_address, a.dns_port, up).start()
+    _run_forever(mk)
+
+
 def local_up(argv):
     """hack/local-up-cluster.sh equivalent: every component as its own process."""
     ap = argparse.ArgumentParser("amdkube local-up")
@@ -407,6 +433,11 @@ def local_up(argv):
         raise SystemExit("apiserver did not come up; see " + os.path.join(b, "logs", "apiserver.log"))
     spawn("controller-manager", ["controller-manager", "--server", server])
     spawn("scheduler", ["scheduler", "--server", server, "--port", "0"])
+    spawn("proxy", ["proxy", "--server", server, "--healthz-port", "0"])
+    # cluster DNS: on :53 it is the pods' nameserver (root); otherwise it still serves on :10053
+    dns_port = 53 if os.geteuid() == 0 else 10053
+    spawn("dns", ["dns", "--server", server, "--dns-port", str(dns_port), "--dns-bind-address", "127.0.0.1"])
+    dns_flags = ["--cluster-dns", "127.0.0.1", "--cluster-domain", "cluster.local"] if dns_port == 53 else []
     sock = os.path.join(b, "rocshim.sock")
     spawn("rocshim", ["rocshim", "--listen", sock, "--state-dir", os.path.join(b, "rocshim"), "--hooks-dir",
                       os.path.join(b, "hooks.d"), "--isolation", a.isolation])
@@ -423,7 +454,8 @@ def local_up(argv):
             break
         time.sleep(0.1)
     spawn("kubelet", ["kubelet", "--server", server, "--root-dir", os.path.join(b, "kubelet"), "--device-plugin-dir", plugins,
-                      "--container-runtime-endpoint", sock, "--gpu-stats-backend", "none" if a.no_gpus else a.backend])
+                      "--container-runtime-endpoint", sock, "--gpu-stats-backend", "none" if a.no_gpus else a.backend]
+          + dns_flags)
     os.makedirs(os.path.expanduser("~/.amdkube"), exist_ok=True)
     json.dump({"server": server}, open(os.path.expanduser("~/.amdkube/config"), "w"))
     print(f"amdkube local cluster is running: {server}  (logs: {b}/logs)\n"
@@ -455,7 +487,7 @@ def kubeadm(argv):
     return main(argv)
 
 
-COMPONENTS = {"kubeadm": kubeadm, "proxy": proxy, "kube-proxy": proxy, "apiserver": apiserver, "kube-apiserver": apiserver, "scheduler": scheduler, "kube-scheduler": scheduler,
+COMPONENTS = {"dns": dns, "kube-dns": dns, "kubeadm": kubeadm, "proxy": proxy, "kube-proxy": proxy, "apiserver": apiserver, "kube-apiserver": apiserver, "scheduler": scheduler, "kube-scheduler": scheduler,
               "controller-manager": controller_manager, "kube-controller-manager": controller_manager, "kubelet": kubelet,
               "rocshim": rocshim, "amd-device-plugin": device_plugin, "device-plugin": device_plugin,
               "amdgpu-exporter": exporter, "exporter": exporter, "hollow-node": hollow_node, "local-up": local_up}

@@ -114,6 +114,9 @@ class EndpointsController(Controller):
             addr = {"ip": ip, "nodeName": (pod.get("spec") or {}).get("nodeName", ""),
                     "targetRef": {"kind": "Pod", "namespace": ns, "name": m.name_of(pod), "uid": m.uid_of(pod),
                                   "resourceVersion": pmd.get("resourceVersion", "")}}
+            pspec = pod.get("spec") or {}
+            if pspec.get("hostname") and pspec.get("subdomain") == m.name_of(svc):
+                addr["hostname"] = pspec["hostname"]   # endpoints_controller.go: per-pod DNS names
             ports = []
             for sp in spec.get("ports") or []:
                 port = find_port(pod, sp)

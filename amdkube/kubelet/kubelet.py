@@ -79,6 +79,9 @@ class KubeletConfig:
     pod_manifest_path: str | None = None            # static pods (--pod-manifest-path)
     file_check_frequency: float = 20.0              # kubeletconfig FileCheckFrequency
     apparmor_fs: str | None = None                  # securityfs apparmor dir (None: discover from /proc/mounts)
+    cluster_dns: list = field(default_factory=list)   # --cluster-dns
+    cluster_domain: str = ""                          # --cluster-domain
+    resolv_conf: str = "/etc/resolv.conf"             # --resolv-conf
 
 
 class PodWorker:
@@ -118,6 +121,9 @@ class Kubelet:
             self.dm = ManagerStub()
         self.recorder = EventRecorder(client, "kubelet", self.node_name)
         self.runtime = RuntimeManager(self.cri, self.dm, config.root_dir, self.recorder)
+        from .dns import DNSConfigurer
+        self.runtime.dns = DNSConfigurer(config.cluster_dns, config.cluster_domain, config.resolv_conf, config.node_ip,
+                                         self.recorder)
         self.gpu_legacy = None
         if self.gates("Accelerators"):   # legacy whole-GPU path (kubelet.go:907-919), alpha
             from .gpu_legacy import AMDGPUManager

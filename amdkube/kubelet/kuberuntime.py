@@ -151,6 +151,7 @@ class RuntimeManager:
         self.seccomp_root = os.path.join(root_dir, "seccomp")   # --seccomp-profile-root
         self._image_seen: dict[str, float] = {}
         self.legacy = None          # gpu_legacy.AMDGPUManager when the Accelerators gate is on
+        self.dns = None             # dns.DNSConfigurer (pod resolv.conf)
         self.active_pods = None
 
     # ----------------------------------------------------------------- status
@@ -195,7 +196,7 @@ class RuntimeManager:
             metadata=C.PodSandboxMetadata(name=md["name"], uid=md["uid"], namespace=md.get("namespace", ""), attempt=attempt),
             hostname=spec.get("hostname") or md["name"], log_directory=log_dir, port_mappings=ports,
             labels={**(md.get("labels") or {}), L_POD_NAME: md["name"], L_POD_NS: md.get("namespace", ""), L_POD_UID: md["uid"]},
-            annotations=ann,
+            annotations=ann, dns_config=self.dns.cri_config(pod) if self.dns is not None else None,
             linux=C.LinuxPodSandboxConfig(security_context=C.LinuxSandboxSecurityContext(
                 namespace_options=C.NamespaceOption(host_network=bool(spec.get("hostNetwork")), host_pid=bool(spec.get("hostPID")),
                                                     host_ipc=bool(spec.get("hostIPC"))))))

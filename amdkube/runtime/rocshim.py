@@ -285,6 +285,16 @@ class RocShim:
         os.makedirs(log_dir, exist_ok=True)
         s = Sandbox(sid, cfg.SerializeToString(), meta, dict(cfg.labels), dict(cfg.annotations), log_dir)
         os.makedirs(os.path.join(self.state_dir, "rootfs", sid), exist_ok=True)
+        dns = cfg.dns_config if cfg.HasField("dns_config") else None
+        if dns is not None and (dns.servers or dns.searches or dns.options):
+            # the pod's resolv.conf (dockershim rewriteResolvFile), mounted at /etc/resolv.conf
+            lines = [f"nameserver {x}" for x in dns.servers]
+            if dns.searches:
+                lines.append("search " + " ".join(dns.searches))
+            if dns.options:
+                lines.append("options " + " ".join(dns.options))
+            with open(os.path.join(self.state_dir, "rootfs", sid, "resolv.conf"), "w") as f:
+                f.write("\n".join(lines) + "\n")
         proc = await spawn([self.pause_bin])
         s.proc, s.pid = proc, proc.pid
         host_net = True
@@ -381,6 +391,9 @@ class RocShim:
         log_path = os.path.join(s.log_dir, cfg.log_path) if cfg.log_path else os.path.join(s.log_dir, f"{cfg.metadata.name}_{cfg.metadata.attempt}.log")
         os.makedirs(os.path.dirname(log_path), exist_ok=True)
         mounts = [{"container_path": m.container_path, "host_path": m.host_path, "readonly": m.readonly} for m in cfg.mounts]
+        resolv = os.path.join(self.state_dir, "rootfs", sid, "resolv.conf")
+        if os.path.exists(resolv) and not any(x["container_path"] == "/etc/resolv.conf" for x in mounts):
+            mounts.append({"container_path": "/etc/resolv.conf", "host_path": resolv, "readonly": True})
         # without a mount namespace, expose volumes as symlinks under the container's root
         for mnt in mounts:
             if self.isolation != "namespaces" and mnt["container_path"].startswith("/"):
@@ -432,6 +445,9 @@ class RocShim:
             a += ["--seccomp", sec]
         if aa:
             a += ["--apparmor", aa]
+        for mnt in c.mounts:   # volumes and the pod's resolv.conf in the private mount namespace
+            if mnt["container_path"].startswith("/") and os.path.exists(mnt["host_path"]):
+                a += ["--bind", f"{mnt['host_path']}:{mnt['container_path']}" + (":ro" if mnt.get("readonly") else "")]
         for k in keep:
             a += ["--keep", k]
         if c.resources.get("memory_limit"):
