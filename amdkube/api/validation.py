@@ -372,6 +372,14 @@ register_hooks("ReplicaSet", "apps/v1", validator=_validate_template_owner)
 register_hooks("Deployment", "apps/v1", validator=_validate_template_owner)
 register_hooks("Job", "batch/v1", validator=validate_job)
 from .networking import default_service, validate_service  # noqa: E402
+
+
+def _validate_crd(obj, old=None):
+    from ..apiserver.crd import validate_crd
+    return validate_object_meta(obj, False) + validate_crd(obj, old)
+
+
+register_hooks("CustomResourceDefinition", "apiextensions.k8s.io/v1beta1", validator=_validate_crd)
 register_hooks("Service", defaulter=default_service, validator=validate_service)
 for _k in ("ConfigMap", "Secret", "ServiceAccount", "Endpoints", "LimitRange", "ResourceQuota",
            "PersistentVolumeClaim"):

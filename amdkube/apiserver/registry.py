@@ -192,17 +192,19 @@ class ResourceStore:
         self.api, self.ri = api, ri
         self.storage = Storage(api.store, ri.plural)
         self.fields_fn = FIELDS.get(ri.plural, default_fields)
-        self.has_status = ri.plural in _STATUS_KINDS
+        self.has_status = ri.plural in _STATUS_KINDS or ri.plural == "customresourcedefinitions"
         self.generation = ri.plural in _GENERATION_KINDS
+        self.storage_prefix = f"/registry/{ri.plural}"   # custom resources: /registry/crd/<group>/<plural>
 
     # ----------------------------------------------------------------- keys
     def key(self, ns, name):
-        return f"/registry/{self.ri.plural}/{ns}/{name}" if self.ri.namespaced else f"/registry/{self.ri.plural}/{name}"
+        p = self.storage_prefix
+        return f"{p}/{ns}/{name}" if self.ri.namespaced else f"{p}/{name}"
 
     def prefix(self, ns=""):
         if self.ri.namespaced and ns:
-            return f"/registry/{self.ri.plural}/{ns}/"
-        return f"/registry/{self.ri.plural}/"
+            return f"{self.storage_prefix}/{ns}/"
+        return f"{self.storage_prefix}/"
 
     def filter(self, label_selector=None, field_selector=None) -> Filter | None:
         ls = parse_selector(label_selector) if label_selector else None

@@ -72,6 +72,8 @@ class APIServer:
         self.store = store or MVCCStore()
         self.admission = adm.Chain(admission_plugins, admission_config)
         self.registry = Registry(self.store, self.admission, ServiceAllocator(service_cidr, parse_port_range(node_port_range)))
+        from .crd import CRDManager
+        self.crds = CRDManager(self.registry)
         self.tokens = dict(token_auth or {})
         # genericapiserver loopback client: the apiserver's own (and in-process components')
         # credential, a random bearer token for system:apiserver in system:masters
@@ -135,6 +137,8 @@ class APIServer:
         self.port = self._site._server.sockets[0].getsockname()[1]
         self.host = host
         self._bg.append(asyncio.create_task(self._event_gc()))
+        self.crds.start()
+        self._bg.append(self.crds._task)
         self._reconcile_master_service()
         log.info("apiserver serving on http://%s:%d", host, self.port)
         return self

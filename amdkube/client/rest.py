@@ -130,6 +130,30 @@ class Client:
         return cls(c["server"], token=c.get("token"), ca_file=c.get("ca_file"), ca_data=c.get("ca_data"),
                    cert_file=c.get("cert_file"), key_file=c.get("key_file"), insecure=c.get("insecure", False), **kw)
 
+    async def discover(self) -> int:
+        """Learn resources the local scheme does not know (custom resources) from the server's
+        discovery documents (/apis → /apis/<group>/<version>), as kubectl's discovery client
+        does. Returns how many were added."""
+        from ..api.scheme import SCHEME, ResourceInfo
+        added = 0
+        groups = (await self.request("GET", "/apis")).get("groups") or []
+        for g in groups:
+            for v in g.get("versions") or []:
+                gv = v["groupVersion"]
+                group, _, version = gv.partition("/")
+                try:
+                    rl = await self.request("GET", f"/apis/{gv}")
+                except m.StatusError:
+                    continue
+                for r in rl.get("resources") or []:
+                    if "/" in r["name"] or SCHEME.for_plural(group, r["name"]) is not None:
+                        continue
+                    subs = tuple(x["name"].split("/", 1)[1] for x in rl["resources"] if x["name"].startswith(r["name"] + "/"))
+                    SCHEME.add(ResourceInfo(group, version, r["kind"], r["name"], bool(r.get("namespaced")),
+                                            tuple(r.get("shortNames") or ()), subs))
+                    added += 1
+        return added
+
     # ---------------------------------------------------------------- paths
     @staticmethod
     def resource_info(resource: str) -> ResourceInfo:

@@ -102,8 +102,13 @@ class NamespaceController(Controller):
         if ns is None:
             return
         remaining = 0
-        for ri in SCHEME.by_kind.values():
-            if not ri.namespaced or ri.plural in ("bindings",) or "list" not in ri.verbs:
+        if (ns.get("metadata") or {}).get("deletionTimestamp"):
+            try:
+                await self.client.discover()   # custom resources are namespace content too
+            except Exception:
+                pass
+        for ri in list(SCHEME.by_kind.values()):
+            if not ri.namespaced or ri.plural in ("bindings", "localsubjectaccessreviews") or "list" not in ri.verbs:
                 continue
             try:
                 items, _ = await self.client.list(ri.plural if not ri.group else f"{ri.plural}.{ri.group}", key)

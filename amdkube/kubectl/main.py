@@ -435,6 +435,10 @@ from .extra import COMMANDS as _EXTRA, add_arguments as _extra_args  # noqa: E40
 COMMANDS.update(_EXTRA)
 
 
+_RESOURCE_CMDS = {"get", "describe", "delete", "label", "annotate", "scale", "patch", "wait", "edit", "explain", "expose",
+                  "autoscale"}
+
+
 def parser():
     p = argparse.ArgumentParser(prog="kubectl", description="amdkube kubectl")
     p.add_argument("--server", "-s", default=None)
@@ -494,6 +498,12 @@ def main(argv=None):
     async def go():
         c = _client(a)
         try:
+            if a.cmd in _RESOURCE_CMDS and a.args:
+                first = a.args[0].split("/")[0].split(",")[0]
+                if SCHEME.resolve(first) is None:
+                    await c.discover()          # a custom resource: learn it from the server
+            elif a.filename and any(SCHEME.for_object(d) is None for d in _read_files(a.filename)):
+                await c.discover()
             return await COMMANDS[a.cmd](c, a)
         except m.StatusError as e:
             print(f"Error from server ({e.reason}): {e.message}", file=sys.stderr)
