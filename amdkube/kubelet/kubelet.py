@@ -121,6 +121,8 @@ class Kubelet:
             self.dm = ManagerStub()
         self.recorder = EventRecorder(client, "kubelet", self.node_name)
         self.runtime = RuntimeManager(self.cri, self.dm, config.root_dir, self.recorder)
+        import psutil as _ps
+        self.runtime.memory_capacity = config.memory_capacity or _ps.virtual_memory().total
         from .dns import DNSConfigurer
         self.runtime.dns = DNSConfigurer(config.cluster_dns, config.cluster_domain, config.resolv_conf, config.node_ip,
                                          self.recorder)

@@ -22,6 +22,7 @@ import grpc
 
 from ..security.apparmor import profile_name as apparmor_profile_name
 from ..utils.trace import POD_TRACE
+from .qos import cgroup_parent
 from ..grpcdesc.cri import CRI as C
 from .cri_client import CRIClient
 
@@ -152,6 +153,7 @@ class RuntimeManager:
         self._image_seen: dict[str, float] = {}
         self.legacy = None          # gpu_legacy.AMDGPUManager when the Accelerators gate is on
         self.dns = None             # dns.DNSConfigurer (pod resolv.conf)
+        self.memory_capacity = 1 << 40   # node memory (burstable OOM score scaling), set by the kubelet
         self.active_pods = None
 
     # ----------------------------------------------------------------- status
@@ -197,7 +199,7 @@ class RuntimeManager:
             hostname=spec.get("hostname") or md["name"], log_directory=log_dir, port_mappings=ports,
             labels={**(md.get("labels") or {}), L_POD_NAME: md["name"], L_POD_NS: md.get("namespace", ""), L_POD_UID: md["uid"]},
             annotations=ann, dns_config=self.dns.cri_config(pod) if self.dns is not None else None,
-            linux=C.LinuxPodSandboxConfig(security_context=C.LinuxSandboxSecurityContext(
+            linux=C.LinuxPodSandboxConfig(cgroup_parent=cgroup_parent(pod), security_context=C.LinuxSandboxSecurityContext(
                 namespace_options=C.NamespaceOption(host_network=bool(spec.get("hostNetwork")), host_pid=bool(spec.get("hostPID")),
                                                     host_ipc=bool(spec.get("hostIPC"))))))
 
@@ -236,14 +238,16 @@ class RuntimeManager:
         ann = dict(opts["annotations"])
         ann.update({A_HASH: container_hash(c), A_RESTARTS: str(restart_count), A_INIT: "true" if init else "false"})
         res = (c.get("resources") or {}).get("limits") or {}
-        lres = C.LinuxContainerResources()
+        from ..api.quantity import Quantity
+        from .qos import oom_score_adj
+        lres = C.LinuxContainerResources(oom_score_adj=oom_score_adj(pod, c, self.memory_capacity))
         if "memory" in res:
-            from ..api.quantity import Quantity
             lres.memory_limit_in_bytes = Quantity(res["memory"]).value()
         if "cpu" in res:
-            from ..api.quantity import Quantity
             lres.cpu_period = 100000
             lres.cpu_quota = max(1000, Quantity(res["cpu"]).milli_value() * 100)
+        req_cpu = ((c.get("resources") or {}).get("requests") or {}).get("cpu") or res.get("cpu")
+        lres.cpu_shares = max(2, Quantity(req_cpu).milli_value() * 1024 // 1000) if req_cpu else 2   # MilliCPUToShares
         md = pod["metadata"]
         cfg = C.ContainerConfig(
             metadata=C.ContainerMetadata(name=c["name"], attempt=restart_count), image=C.ImageSpec(image=c["image"]),

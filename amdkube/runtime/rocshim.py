@@ -403,7 +403,10 @@ class RocShim:
                     os.symlink(mnt["host_path"], link)
         env["AMDKUBE_ROOTFS"] = root
         r = cfg.linux.resources if cfg.HasField("linux") else None
-        resources = {"cpu_quota": r.cpu_quota, "cpu_period": r.cpu_period, "memory_limit": r.memory_limit_in_bytes} if r else {}
+        resources = {"cpu_quota": r.cpu_quota, "cpu_period": r.cpu_period, "memory_limit": r.memory_limit_in_bytes,
+                     "cpu_shares": r.cpu_shares, "oom_score_adj": r.oom_score_adj} if r else {}
+        if sandbox_cfg is not None and sandbox_cfg.HasField("linux") and sandbox_cfg.linux.cgroup_parent:
+            resources["cgroup_parent"] = sandbox_cfg.linux.cgroup_parent.strip("/")
         sec = cfg.linux.security_context.seccomp_profile_path if cfg.HasField("linux") else ""
         if sec:
             resources["seccomp_profile"] = self._seccomp_file(sec)
@@ -438,9 +441,15 @@ class RocShim:
                 return c.argv
             return ([self.nsexec_bin, "--no-namespaces"] + (["--seccomp", sec] if sec else []) +
                     (["--apparmor", aa] if aa else []) + ["--"] + c.argv)
+        # (env isolation: the OOM score is applied to the spawned process directly, see start_container)
         keep = [d["host_path"] for d in c.devices if "/dri/" in d["host_path"]]
-        cg = os.path.join(self.cgroup_root, c.sandbox_id, c.id)
+        # QoS hierarchy from the kubelet (kubepods/[burstable|besteffort]/pod<uid>), else per sandbox
+        cg = os.path.join(self.cgroup_root, c.resources.get("cgroup_parent") or c.sandbox_id, c.id)
         a = [self.nsexec_bin, "--dev-root", self.dev_root, "--cgroup", cg]
+        if c.resources.get("cpu_shares"):
+            a += ["--cpu-weight", str(_shares_to_weight(c.resources["cpu_shares"]))]
+        if c.resources.get("oom_score_adj"):
+            a += ["--oom-score-adj", str(c.resources["oom_score_adj"])]
         if sec:
             a += ["--seccomp", sec]
         if aa:
@@ -475,6 +484,8 @@ class RocShim:
             raise
         logf.close()
         c.proc, c.pid = proc, proc.pid
+        if self.isolation != "namespaces" and c.resources.get("oom_score_adj"):
+            _set_oom_score_adj(proc.pid, c.resources["oom_score_adj"])
         c.state, c.started_at = C.CONTAINER_RUNNING, now_ns()
         self.started += 1
         self._ckpt("containers", c)
@@ -551,6 +562,21 @@ class RocShim:
             p.kill()
             return b"", b"timeout", 124
         return out, err, p.returncode
+
+
+def _shares_to_weight(shares: int) -> int:
+    """cgroup v1 cpu.shares → v2 cpu.weight (the runc/systemd conversion)."""
+    return max(1, min(10000, 1 + ((shares - 2) * 9999) // 262142))
+
+
+def _set_oom_score_adj(pid: int, adj: int):
+    """Best effort without privileges: raising a score is always allowed, lowering it needs
+    CAP_SYS_RESOURCE (then the kernel refuses and the container keeps the inherited value)."""
+    try:
+        with open(f"/proc/{pid}/oom_score_adj", "w") as f:
+            f.write(str(adj))
+    except OSError:
+        pass
 
 
 def sandbox_meta(s) -> "C.PodSandboxMetadata":

@@ -9,7 +9,8 @@
 //                  [--cgroup /sys/fs/cgroup/amdkube/<pod>/<ctr>] [--memory-max BYTES]
 //                  [--cpu-max "QUOTA PERIOD"] -- argv...
 //
-//  1. join (creating) a cgroup-v2 leaf and apply memory.max / cpu.max;
+//  1. join (creating) a cgroup-v2 leaf and apply memory.max / cpu.max / cpu.weight
+//     (--cpu-weight, from the kubelet's cpu shares) and the OOM score (--oom-score-adj, QoS);
 //  2. unshare a private mount namespace;
 //  3. open every kept device node with O_PATH (inside the new namespace), mount a fresh tmpfs over <dev-root>/dri and
 //     bind the kept nodes back from /proc/self/fd (no CAP_MKNOD needed);
@@ -81,7 +82,7 @@ static int mkdir_p(const std::string& p) {
 }
 
 int main(int argc, char** argv) {
-  std::string dev_root = "/dev", cgroup, mem_max, cpu_max;
+  std::string dev_root = "/dev", cgroup, mem_max, cpu_max, cpu_weight, oom_adj;
   std::vector<std::string> keep, binds;
   bool hide_kfd = false, no_ns = false;
   std::string seccomp_profile, apparmor;
@@ -98,6 +99,8 @@ int main(int argc, char** argv) {
     else if (a == "--cgroup" && i + 1 < argc) cgroup = argv[++i];
     else if (a == "--memory-max" && i + 1 < argc) mem_max = argv[++i];
     else if (a == "--cpu-max" && i + 1 < argc) cpu_max = argv[++i];
+    else if (a == "--cpu-weight" && i + 1 < argc) cpu_weight = argv[++i];
+    else if (a == "--oom-score-adj" && i + 1 < argc) oom_adj = argv[++i];
     else if (a == "--seccomp" && i + 1 < argc) seccomp_profile = argv[++i];
     else if (a == "--apparmor" && i + 1 < argc) apparmor = argv[++i];
     else if (a == "--no-namespaces") no_ns = true;
@@ -136,8 +139,11 @@ int main(int argc, char** argv) {
     if (mkdir_p(cgroup) < 0) return die("create cgroup");
     if (!mem_max.empty()) write_file(cgroup + "/memory.max", mem_max);
     if (!cpu_max.empty()) write_file(cgroup + "/cpu.max", cpu_max);
+    if (!cpu_weight.empty()) write_file(cgroup + "/cpu.weight", cpu_weight);
     if (!write_file(cgroup + "/cgroup.procs", std::to_string(getpid()))) return die("join cgroup");
   }
+  // lowering the score needs CAP_SYS_RESOURCE, which the privileged launcher has
+  if (!oom_adj.empty() && !write_file("/proc/self/oom_score_adj", oom_adj)) return die("oom_score_adj");
   if (unshare(CLONE_NEWNS) < 0) return die("unshare(CLONE_NEWNS)");
   if (mount(nullptr, "/", nullptr, MS_REC | MS_PRIVATE, nullptr) < 0) return die("make / rprivate");
   // open the kept nodes inside the new namespace (a bind source must belong to it)
