@@ -130,6 +130,8 @@ _AUTHZ = [("SubjectAccessReview", "subjectaccessreviews", False, (), ()),
           ("SelfSubjectAccessReview", "selfsubjectaccessreviews", False, (), ()),
           ("LocalSubjectAccessReview", "localsubjectaccessreviews", True, (), ())]
 _AUTHN = [("TokenReview", "tokenreviews", False, (), ())]
+_ADMREG = [("MutatingWebhookConfiguration", "mutatingwebhookconfigurations", False, (), ()),
+           ("ValidatingWebhookConfiguration", "validatingwebhookconfigurations", False, (), ())]
 _APIEXT = [("CustomResourceDefinition", "customresourcedefinitions", False, ("crd", "crds"), ("status",))]
 
 for group, version, table in (("", "v1", _CORE), ("apps", "v1", _APPS), ("batch", "v1", _BATCH),
@@ -139,7 +141,8 @@ for group, version, table in (("", "v1", _CORE), ("apps", "v1", _APPS), ("batch"
                               ("rbac.authorization.k8s.io", "v1", _RBAC), ("storage.k8s.io", "v1", _STORAGE),
                               ("storage.k8s.io", "v1beta1", _STORAGE_BETA),
                               ("authorization.k8s.io", "v1", _AUTHZ), ("authentication.k8s.io", "v1", _AUTHN),
-                              ("apiextensions.k8s.io", "v1beta1", _APIEXT)):
+                              ("apiextensions.k8s.io", "v1beta1", _APIEXT),
+                              ("admissionregistration.k8s.io", "v1beta1", _ADMREG)):
     for kind, plural, ns, short, subs in table:
         SCHEME.add(ResourceInfo(group, version, kind, plural, ns, short, subs))
 

@@ -73,7 +73,9 @@ class APIServer:
         self.admission = adm.Chain(admission_plugins, admission_config)
         self.registry = Registry(self.store, self.admission, ServiceAllocator(service_cidr, parse_port_range(node_port_range)))
         from .crd import CRDManager
+        from .webhook import WebhookDispatcher
         self.crds = CRDManager(self.registry)
+        self.webhooks = WebhookDispatcher(self.registry)
         self.tokens = dict(token_auth or {})
         # genericapiserver loopback client: the apiserver's own (and in-process components')
         # credential, a random bearer token for system:apiserver in system:masters
@@ -176,6 +178,7 @@ class APIServer:
     async def stop(self):
         for t in self._bg:
             t.cancel()
+        await self.webhooks.close()
         for w in self.store.all_watchers():
             w.close()
         if self._http:
@@ -428,6 +431,12 @@ class APIServer:
             if name:
                 raise m.method_not_allowed("POST on a named resource")
             dry = q.get("dryRun") == "All"
+            mut, val = self.webhooks.active("CREATE", ri, sub, ns)
+            if mut:
+                body = await self.webhooks.mutate(mut, "CREATE", ri, sub, ns, None, body, None, user)
+            if val:
+                final = rs.create(ns, json.loads(json.dumps(body)), user, dry_run=True)
+                await self.webhooks.validate(val, "CREATE", ri, sub, ns, None, final, None, user)
             obj = rs.create(ns, body, user, dry_run=dry)
             return _resp(obj, 201)
         if meth == "PUT":
@@ -439,6 +448,13 @@ class APIServer:
             subr = "status" if sub in ("status", "approval") else ""
             if sub == "finalize" and ri.plural == "namespaces":
                 subr = "finalize"
+            mut, val = self.webhooks.active("UPDATE", ri, sub, ns)
+            if mut or val:
+                old = rs.get(ns, name)
+                if mut:
+                    body = await self.webhooks.mutate(mut, "UPDATE", ri, sub, ns, name, body, old, user)
+                if val:
+                    await self.webhooks.validate(val, "UPDATE", ri, sub, ns, name, body, old, user)
             obj, created = rs.update(ns, name, body, subresource=subr, user=user)
             return _resp(obj, 201 if created else 200)
         if meth == "PATCH":
@@ -450,6 +466,20 @@ class APIServer:
                 from .registry import apply_patch
                 cur = _to_scale(rs.get(ns, name))
                 return _resp(self._set_scale(rs, ns, name, apply_patch(cur, data, ct), user))
+            mut, val = self.webhooks.active("UPDATE", ri, sub, ns)
+            if mut or val:
+                # webhooks see the patched object; it is then written as an update conditioned on the
+                # resourceVersion it was computed from (a concurrent writer gets a 409 to retry)
+                from .registry import apply_patch
+                old = rs.get(ns, name)
+                new = apply_patch(old, data, ct)
+                if mut:
+                    new = await self.webhooks.mutate(mut, "UPDATE", ri, sub, ns, name, new, old, user)
+                if val:
+                    await self.webhooks.validate(val, "UPDATE", ri, sub, ns, name, new, old, user)
+                new.setdefault("metadata", {})["resourceVersion"] = (old.get("metadata") or {}).get("resourceVersion")
+                obj, _ = rs.update(ns, name, new, subresource=sub if sub == "status" else "", user=user)
+                return _resp(obj)
             obj, _ = rs.update(ns, name, None, subresource=sub if sub == "status" else "", user=user, patch=data,
                                content_type=ct)
             return _resp(obj)
@@ -468,6 +498,9 @@ class APIServer:
             if opts.get("orphanDependents") is True:
                 prop = "Orphan"
             uid = (opts.get("preconditions") or {}).get("uid")
+            _, val = self.webhooks.active("DELETE", ri, sub, ns)
+            if val and name:
+                await self.webhooks.validate(val, "DELETE", ri, sub, ns, name, None, rs.get(ns, name), user)
             if name:
                 obj, now = rs.delete(ns, name, grace=grace, precond_uid=uid, user=user, propagation=prop)
                 return _resp(obj if not now or ri.plural == "pods" else m.success_status(

@@ -1,0 +1,121 @@
+"""Dynamic admission webhooks (reference staging/src/k8s.io/apiserver/pkg/admission/plugin/
+webhook/{mutating,validating}/*_test.go and rules/rules_test.go: rule matching, ordered
+mutation with JSONPatch, parallel validation, failurePolicy, namespaceSelector, https+caBundle)."""
+import asyncio
+import base64
+import json
+import os
+import ssl
+import subprocess
+
+from aiohttp import web
+
+from amdkube.api import meta as m
+from amdkube.apiserver.webhook import rule_matches
+from amdkube.localcluster import LocalCluster
+
+
+def test_rule_matching():
+    r = {"operations": ["CREATE"], "apiGroups": [""], "apiVersions": ["v1"], "resources": ["pods"]}
+    assert rule_matches(r, "CREATE", "", "v1", "pods", "")
+    assert not rule_matches(r, "UPDATE", "", "v1", "pods", "")
+    assert not rule_matches(r, "CREATE", "", "v1", "pods", "status")
+    assert not rule_matches(r, "CREATE", "apps", "v1", "pods", "")
+    star = {"operations": ["*"], "apiGroups": ["*"], "apiVersions": ["*"], "resources": ["*/*"]}
+    assert rule_matches(star, "DELETE", "apps", "v1", "deployments", "scale")
+    assert rule_matches({**star, "resources": ["pods/*"]}, "UPDATE", "", "v1", "pods", "status")
+    assert not rule_matches({**star, "resources": ["pods/*"]}, "UPDATE", "", "v1", "pods", "")
+
+
+def _cert(tmp_path):
+    key, crt = tmp_path / "k.pem", tmp_path / "c.pem"
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", str(key), "-out", str(crt),
+                    "-days", "1", "-subj", "/CN=127.0.0.1", "-addext", "subjectAltName=IP:127.0.0.1"],
+                   check=True, capture_output=True)
+    return str(crt), str(key)
+
+
+async def test_mutating_and_validating_webhooks(tmp_path):
+    crt, key = _cert(tmp_path)
+    calls = []
+
+    async def mutate(req):
+        rv = await req.json()
+        r = rv["request"]
+        calls.append(("mutate", r["operation"], r["kind"]["kind"], r["userInfo"]["username"]))
+        pod = r["object"]
+        patch = [{"op": "add", "path": "/metadata/labels", "value": {**(pod["metadata"].get("labels") or {}), "gpu-admitted": "yes"}}]
+        if not any(t.get("key") == "amd.com/gpu" for t in pod["spec"].get("tolerations") or []):
+            patch.append({"op": "add", "path": "/spec/tolerations",
+                          "value": (pod["spec"].get("tolerations") or []) + [{"key": "amd.com/gpu", "operator": "Exists"}]})
+        return web.json_response({"response": {"uid": r["uid"], "allowed": True, "patchType": "JSONPatch",
+                                                "patch": base64.b64encode(json.dumps(patch).encode()).decode()}})
+
+    async def validate(req):
+        rv = await req.json()
+        r = rv["request"]
+        calls.append(("validate", r["operation"], r["name"]))
+        obj = r["object"] or r["oldObject"]
+        if r["operation"] == "DELETE" and obj["metadata"].get("labels", {}).get("protected") == "true":
+            return web.json_response({"response": {"uid": r["uid"], "allowed": False,
+                                                    "status": {"message": "protected pod", "code": 403}}})
+        ok = obj["metadata"].get("labels", {}).get("gpu-admitted") == "yes" or r["operation"] == "DELETE"
+        return web.json_response({"response": {"uid": r["uid"], "allowed": ok,
+                                                "status": {"message": "not mutated first"}}})
+
+    app = web.Application()
+    app.router.add_post("/mutate", mutate)
+    app.router.add_post("/validate", validate)
+    runner = web.AppRunner(app, access_log=None)
+    await runner.setup()
+    ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+    ctx.load_cert_chain(crt, key)
+    site = web.TCPSite(runner, "127.0.0.1", 0, ssl_context=ctx)
+    await site.start()
+    port = site._server.sockets[0].getsockname()[1]
+    ca = base64.b64encode(open(crt, "rb").read()).decode()
+    try:
+        async with LocalCluster(gpus="none", with_kubelet=False, with_controllers=False) as lc:
+            c = lc.client
+            pods_rule = [{"operations": ["CREATE", "UPDATE"], "apiGroups": [""], "apiVersions": ["v1"], "resources": ["pods"]}]
+            await c.create({"apiVersion": "admissionregistration.k8s.io/v1beta1", "kind": "MutatingWebhookConfiguration",
+                            "metadata": {"name": "gpu-defaults"},
+                            "webhooks": [{"name": "defaults.amd.com", "rules": pods_rule, "failurePolicy": "Fail",
+                                          "clientConfig": {"url": f"https://127.0.0.1:{port}/mutate", "caBundle": ca}}]})
+            await c.create({"apiVersion": "admissionregistration.k8s.io/v1beta1", "kind": "ValidatingWebhookConfiguration",
+                            "metadata": {"name": "gpu-policy"},
+                            "webhooks": [{"name": "policy.amd.com", "failurePolicy": "Fail",
+                                          "namespaceSelector": {"matchLabels": {"gpu-policy": "on"}},
+                                          "rules": [{**pods_rule[0], "operations": ["CREATE", "UPDATE", "DELETE"]}],
+                                          "clientConfig": {"url": f"https://127.0.0.1:{port}/validate", "caBundle": ca}}]})
+            await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "ml", "labels": {"gpu-policy": "on"}}})
+            pod = lambda n, labels=None: {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": n, "labels": labels or {}},
+                                          "spec": {"containers": [{"name": "c", "image": "busybox"}]}}
+            p = await c.create(pod("a", {"protected": "true"}), "ml")
+            assert p["metadata"]["labels"]["gpu-admitted"] == "yes"
+            assert {"key": "amd.com/gpu", "operator": "Exists"} in p["spec"]["tolerations"]
+            p = await c.create(pod("b"), "default")          # outside the validating namespaceSelector
+            assert p["metadata"]["labels"]["gpu-admitted"] == "yes"
+            assert ("validate", "CREATE", "b") not in calls and ("validate", "CREATE", "a") in calls
+            # PATCH goes through both webhooks on the patched object
+            p = await c.patch("pods", "a", {"metadata": {"labels": {"team": "x"}}}, "ml")
+            assert p["metadata"]["labels"]["team"] == "x" and p["metadata"]["labels"]["gpu-admitted"] == "yes"
+            # validating denial on DELETE
+            try:
+                await c.delete("pods", "a", "ml")
+                raise AssertionError("deletion must be denied")
+            except m.StatusError as e:
+                assert e.code == 403 and "protected pod" in e.message
+            # failurePolicy Fail: an unreachable webhook rejects; Ignore lets the request through
+            await site.stop()
+            try:
+                await c.create(pod("c"), "default")
+                raise AssertionError("Fail policy must reject when the webhook is down")
+            except m.StatusError as e:
+                assert e.code == 500 and "defaults.amd.com" in e.message
+            cfg = await c.get("mutatingwebhookconfigurations.admissionregistration.k8s.io", "gpu-defaults")
+            cfg["webhooks"][0]["failurePolicy"] = "Ignore"
+            await c.update(cfg)
+            assert (await c.create(pod("d"), "default"))["metadata"]["labels"] == {}
+    finally:
+        await runner.cleanup()
