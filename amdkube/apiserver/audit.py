@@ -1,0 +1,158 @@
+"""Advanced auditing (AdvancedAuditing beta, on): policy + log backend.
+
+Reference: staging/src/k8s.io/apiserver/pkg/audit — policy/checker.go (first matching rule
+decides the level: None | Metadata | Request | RequestResponse; rule fields users, userGroups,
+verbs, resources[{group, resources, resourceNames}] (with "resource/subresource"),
+namespaces, nonResourceURLs (with trailing "*"), omitStages), request.go (Event fields:
+auditID, stage, requestURI, verb, user, sourceIPs, objectRef, responseStatus, request/response
+objects at Request/RequestResponse level, requestReceivedTimestamp/stageTimestamp),
+plugin/pkg/audit/log (one JSON event per line, --audit-log-path; rotation by
+--audit-log-maxsize MB keeping --audit-log-maxbackup files).
+
+Stages recorded: RequestReceived and ResponseComplete (ResponseStarted is the long-running
+stage; watches and streams log it when they start), Panic on handler crashes.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+import uuid
+
+from ..api import meta as m
+
+LEVELS = ("None", "Metadata", "Request", "RequestResponse")
+
+
+def load_policy(path: str | None) -> dict:
+    if not path:
+        return {"rules": [{"level": "Metadata"}]}
+    import yaml
+    with open(path) as f:
+        doc = yaml.safe_load(f) or {}
+    if doc.get("kind") not in (None, "Policy"):
+        raise ValueError(f"audit policy {path}: kind must be Policy")
+    for r in doc.get("rules") or []:
+        if r.get("level") not in LEVELS:
+            raise ValueError(f"audit policy {path}: unknown level {r.get('level')!r}")
+    return doc
+
+
+def _match_resource(rule_res: list, group: str, resource: str, sub: str, name: str) -> bool:
+    for gr in rule_res:
+        if gr.get("group", "") != group and gr.get("group") != "*":
+            continue
+        names = gr.get("resourceNames") or []
+        if names and name not in names:
+            continue
+        rs = gr.get("resources") or []
+        if not rs:
+            return True
+        full = f"{resource}/{sub}" if sub else resource
+        for r in rs:
+            if r in (full, "*", "*/*") or (r == f"{resource}/*" and sub) or (r == f"*/{sub}" and sub):
+                return True
+    return False
+
+
+def level_for(policy: dict, user: dict, verb: str, group: str, resource: str, sub: str, ns: str, name: str,
+              path: str) -> tuple[str, set]:
+    groups = set(user.get("groups") or [])
+    for r in policy.get("rules") or []:
+        if r.get("users") and user.get("name") not in r["users"]:
+            continue
+        if r.get("userGroups") and not groups & set(r["userGroups"]):
+            continue
+        if r.get("verbs") and verb not in r["verbs"]:
+            continue
+        if resource:
+            if r.get("nonResourceURLs"):
+                continue
+            if r.get("resources") and not _match_resource(r["resources"], group, resource, sub, name):
+                continue
+            if r.get("namespaces") and ns not in r["namespaces"]:
+                continue
+        else:
+            urls = r.get("nonResourceURLs")
+            if r.get("resources") or r.get("namespaces"):
+                continue
+            if urls and not any(path == u or (u.endswith("*") and path.startswith(u[:-1])) for u in urls):
+                continue
+        return r["level"], set(r.get("omitStages") or []) | set(policy.get("omitStages") or [])
+    return "None", set()
+
+
+class LogBackend:
+    def __init__(self, path: str, max_size_mb: int = 0, max_backup: int = 0):
+        self.path, self.max_bytes, self.max_backup = path, max_size_mb * (1 << 20), max_backup
+        self.f = None if path == "-" else open(path, "a", buffering=1)
+        self.events = 0
+
+    def write(self, ev: dict):
+        line = json.dumps(ev, separators=(",", ":")) + "\n"
+        self.events += 1
+        if self.f is None:
+            import sys
+            sys.stdout.write(line)
+            return
+        if self.max_bytes and self.f.tell() + len(line) > self.max_bytes:
+            self._rotate()
+        self.f.write(line)
+
+    def _rotate(self):
+        self.f.close()
+        stamp = time.strftime("%Y-%m-%dT%H-%M-%S", time.gmtime())
+        os.replace(self.path, f"{self.path}-{stamp}.{time.time_ns() % 1000000:06d}")
+        if self.max_backup:
+            base = os.path.basename(self.path) + "-"
+            d = os.path.dirname(os.path.abspath(self.path))
+            olds = sorted(f for f in os.listdir(d) if f.startswith(base))
+            for f in olds[:-self.max_backup]:
+                os.unlink(os.path.join(d, f))
+        self.f = open(self.path, "a", buffering=1)
+
+    def close(self):
+        if self.f is not None:
+            self.f.close()
+
+
+class Auditor:
+    def __init__(self, policy: dict, backend: LogBackend):
+        self.policy, self.backend = policy, backend
+
+    def begin(self, request, user, verb, group, version, resource, sub, ns, name):
+        lvl, omit = level_for(self.policy, user or {}, verb, group, resource, sub, ns, name, request.path)
+        if lvl == "None":
+            return None
+        ev = {"kind": "Event", "apiVersion": "audit.k8s.io/v1beta1", "level": lvl,
+              "timestamp": m.now_rfc3339_micro(), "auditID": str(uuid.uuid4()), "stage": "RequestReceived",
+              "requestURI": request.path_qs, "verb": verb,
+              "user": {"username": (user or {}).get("name", ""), "groups": (user or {}).get("groups") or []},
+              "sourceIPs": [request.remote or ""],
+              "requestReceivedTimestamp": m.now_rfc3339_micro(), "stageTimestamp": m.now_rfc3339_micro()}
+        if resource:
+            ev["objectRef"] = {k: v for k, v in (("resource", resource), ("namespace", ns), ("name", name),
+                                                  ("apiGroup", group), ("apiVersion", version),
+                                                  ("subresource", sub)) if v}
+        if "RequestReceived" not in omit:
+            self.backend.write(dict(ev))
+        return ev, omit
+
+    def stage(self, ctx, stage: str, code: int, request_body: bytes | None = None, response=None):
+        if ctx is None:
+            return
+        ev, omit = ctx
+        if stage in omit:
+            return
+        out = dict(ev, stage=stage, stageTimestamp=m.now_rfc3339_micro(), responseStatus={"metadata": {}, "code": code})
+        if ev["level"] in ("Request", "RequestResponse") and request_body:
+            try:
+                out["requestObject"] = json.loads(request_body)
+            except ValueError:
+                pass
+        if ev["level"] == "RequestResponse" and response is not None and getattr(response, "body", None):
+            try:
+                out["responseObject"] = json.loads(response.body)
+            except (ValueError, TypeError):
+                pass
+        self.backend.write(out)

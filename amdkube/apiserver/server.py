@@ -68,7 +68,8 @@ class APIServer:
                  max_in_flight: int = 400, max_mutating_in_flight: int = 200, event_ttl: float = 3600.0,
                  anonymous_auth: bool = True, service_cidr: str = "10.0.0.0/24", node_port_range: str = "30000-32767",
                  service_account_key: bytes | None = None, tls_cert_file: str | None = None, tls_key_file: str | None = None,
-                 client_ca_file: str | None = None):
+                 client_ca_file: str | None = None, audit_log_path: str | None = None, audit_policy_file: str | None = None,
+                 audit_log_maxsize: int = 0, audit_log_maxbackup: int = 0):
         self.store = store or MVCCStore()
         self.admission = adm.Chain(admission_plugins, admission_config)
         self.registry = Registry(self.store, self.admission, ServiceAllocator(service_cidr, parse_port_range(node_port_range)))
@@ -76,6 +77,11 @@ class APIServer:
         from .webhook import WebhookDispatcher
         self.crds = CRDManager(self.registry)
         self.webhooks = WebhookDispatcher(self.registry)
+        self.auditor = None
+        if audit_log_path:
+            from .audit import Auditor, LogBackend, load_policy
+            self.auditor = Auditor(load_policy(audit_policy_file), LogBackend(audit_log_path, audit_log_maxsize,
+                                                                               audit_log_maxbackup))
         self.tokens = dict(token_auth or {})
         # genericapiserver loopback client: the apiserver's own (and in-process components')
         # credential, a random bearer token for system:apiserver in system:masters
@@ -320,7 +326,7 @@ class APIServer:
     async def dispatch(self, request: web.Request):
         t0 = time.perf_counter()
         verb, resource, sub, code = request.method, "", "", 500
-        sem = None
+        sem = actx = resp = None
         try:
             user = self._authenticate(request)
             group, version, resource, ns, name, sub, watch = self._parse(request.path)
@@ -346,11 +352,17 @@ class APIServer:
             if name and top_sub in _STREAMING_SUBS:
                 kverb = "create"   # exec/attach/portforward/proxy always need create on the subresource
             verb = kverb.upper()
+            if self.auditor is not None:
+                actx = self.auditor.begin(request, user, kverb, group, version, resource, sub, ns, name or "")
             self._authorize(user, kverb, resource, group, "" if not rs.ri.namespaced else ns, name or "", top_sub)
             if is_watch:
                 code = 200
+                if actx is not None:
+                    self.auditor.stage(actx, "ResponseStarted", 200)
                 return await self._watch(request, rs, ns, name, q)
             if name and top_sub in _STREAMING_SUBS:   # long-running: exempt from max-in-flight, like watches
+                if actx is not None:
+                    self.auditor.stage(actx, "ResponseStarted", 101)
                 resp = await self._stream(request, rs, ns, name, sub, q)
                 code = resp.status
                 return resp
@@ -364,7 +376,8 @@ class APIServer:
             return resp
         except m.StatusError as e:
             code = e.code
-            return _err(e)
+            resp = _err(e)
+            return resp
         except (ValueError, KeyError, TypeError) as e:
             code = 400
             log.debug("bad request %s %s: %r", request.method, request.path, e)
@@ -372,6 +385,8 @@ class APIServer:
         finally:
             if sem is not None:
                 sem.release()
+            if actx is not None:
+                self.auditor.stage(actx, "ResponseComplete", code, getattr(request, "_read_bytes", None), resp)
             self.m_count.labels(verb, resource or "", sub or "", str(code)).inc()
             if verb != "WATCH":
                 self.m_lat.labels(verb, resource or "", sub or "").observe((time.perf_counter() - t0) * 1e6)

@@ -74,6 +74,10 @@ def apiserver(argv):
     ap.add_argument("--tls-private-key-file", default=None)
     ap.add_argument("--client-ca-file", default=None)
     ap.add_argument("-v", type=int, default=0)
+    ap.add_argument("--audit-log-path", default=None, help="write audit events (JSON lines) here; - for stdout")
+    ap.add_argument("--audit-policy-file", default=None, help="audit.k8s.io Policy (default: everything at Metadata)")
+    ap.add_argument("--audit-log-maxsize", type=int, default=0, help="rotate the audit log at this many MB")
+    ap.add_argument("--audit-log-maxbackup", type=int, default=0, help="rotated audit logs to keep")
     a = ap.parse_args(argv)
     klog.setup(a.v, "apiserver")
     from ..apiserver import APIServer
@@ -95,7 +99,9 @@ def apiserver(argv):
                         event_ttl=a.event_ttl, service_cidr=a.service_cluster_ip_range,
                         node_port_range=a.service_node_port_range,
                         service_account_key=open(a.service_account_key_file, "rb").read().strip() if a.service_account_key_file else None,
-                        tls_cert_file=a.tls_cert_file, tls_key_file=a.tls_private_key_file, client_ca_file=a.client_ca_file)
+                        tls_cert_file=a.tls_cert_file, tls_key_file=a.tls_private_key_file, client_ca_file=a.client_ca_file,
+                        audit_log_path=a.audit_log_path, audit_policy_file=a.audit_policy_file,
+                        audit_log_maxsize=a.audit_log_maxsize, audit_log_maxbackup=a.audit_log_maxbackup)
         return await srv.start(a.bind_address, a.port)
     _run_forever(mk)
 
