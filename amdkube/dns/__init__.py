@@ -259,9 +259,17 @@ class DNSServer:
         await self.ep_inf.wait_synced(30)
         self._rebuild()
         loop = asyncio.get_running_loop()
-        self._udp, _ = await loop.create_datagram_endpoint(lambda: _UDP(self), local_addr=(self.address, self.port))
-        self.port = self._udp.get_extra_info("sockname")[1]
-        self._tcp = await asyncio.start_server(self._tcp_conn, self.address, self.port)
+        want = self.port
+        for attempt in range(20):   # port 0: UDP picks a port, TCP must get the same number
+            self._udp, _ = await loop.create_datagram_endpoint(lambda: _UDP(self), local_addr=(self.address, want))
+            self.port = self._udp.get_extra_info("sockname")[1]
+            try:
+                self._tcp = await asyncio.start_server(self._tcp_conn, self.address, self.port)
+                break
+            except OSError:
+                self._udp.close()
+                if want != 0 or attempt == 19:
+                    raise
         log.info("cluster DNS for %s on %s:%d", self.records.domain, self.address, self.port)
         return self
 
