@@ -197,6 +197,9 @@ def kubelet(argv):
     ap.add_argument("--node-status-update-frequency", type=float, default=10.0)
     ap.add_argument("--pleg-relist-period", type=float, default=1.0)
     ap.add_argument("--max-pods", type=int, default=110)
+    ap.add_argument("--maximum-dead-containers-per-container", type=int, default=1)
+    ap.add_argument("--maximum-dead-containers", type=int, default=-1)
+    ap.add_argument("--minimum-container-ttl-duration", type=float, default=0.0, help="seconds")
     ap.add_argument("--node-labels", default="")
     ap.add_argument("--register-with-taints", default="")
     ap.add_argument("--feature-gates", default="")
@@ -228,7 +231,10 @@ def kubelet(argv):
                         pod_manifest_path=a.pod_manifest_path, file_check_frequency=a.file_check_frequency,
                         gpu_stats_backend=a.gpu_stats_backend,
                         cluster_dns=[x for x in a.cluster_dns.split(",") if x], cluster_domain=a.cluster_domain,
-                        resolv_conf=a.resolv_conf)
+                        resolv_conf=a.resolv_conf,
+                        maximum_dead_containers_per_container=a.maximum_dead_containers_per_container,
+                        maximum_dead_containers=a.maximum_dead_containers,
+                        minimum_container_ttl_duration=a.minimum_container_ttl_duration)
 
     async def mk():
         smi = None

@@ -82,6 +82,10 @@ class KubeletConfig:
     cluster_dns: list = field(default_factory=list)   # --cluster-dns
     cluster_domain: str = ""                          # --cluster-domain
     resolv_conf: str = "/etc/resolv.conf"             # --resolv-conf
+    gc_period: float = 60.0                           # container GC cadence (kubelet.go ContainerGCPeriod)
+    maximum_dead_containers_per_container: int = 1    # --maximum-dead-containers-per-container
+    maximum_dead_containers: int = -1                 # --maximum-dead-containers
+    minimum_container_ttl_duration: float = 0.0       # --minimum-container-ttl-duration (s)
 
 
 class PodWorker:
@@ -189,6 +193,7 @@ class Kubelet:
         self._tasks += [asyncio.create_task(self._relist_loop(), name="pleg-relist"),
                         asyncio.create_task(self._prober_loop(), name="prober"),
                         asyncio.create_task(self._housekeeping(), name="housekeeping"),
+                        asyncio.create_task(self._gc_loop(), name="container-gc"),
                         asyncio.create_task(self._eviction_loop(), name="eviction")]
         if self.cfg.evented_pleg:
             self._tasks.append(asyncio.create_task(self._evented_pleg(), name="pleg-events"))
@@ -912,6 +917,21 @@ class Kubelet:
                 log.debug("container event stream ended: %r", e)
             await asyncio.sleep(backoff)
             backoff = min(2.0, backoff * 2)
+
+    async def container_gc(self) -> dict:
+        """One pass of the container/sandbox garbage collector (active pods keep their newest
+        dead container per container name for logs and restart accounting)."""
+        active = lambda uid: uid in self.pods and uid not in self.terminated_deleted   # noqa: E731
+        return await self.runtime.garbage_collect(active, self.cfg.maximum_dead_containers_per_container,
+                                                  self.cfg.maximum_dead_containers, self.cfg.minimum_container_ttl_duration)
+
+    async def _gc_loop(self):
+        while True:
+            await asyncio.sleep(self.cfg.gc_period)
+            try:
+                await self.container_gc()
+            except Exception as e:
+                log.debug("container GC failed: %r", e)
 
     async def _housekeeping(self):
         """Periodic resync (syncFrequency) of every pod; keeps the sync loop health probe fresh."""

@@ -383,6 +383,73 @@ class RuntimeManager:
                             pass
         await self.cri.stop_container(c.id, grace)
 
+    # ------------------------------------------------------------ garbage collection
+    async def garbage_collect(self, is_active, max_per_pod_container: int = 1, max_containers: int = -1,
+                              min_age: float = 0.0, now_ns: int | None = None) -> dict:
+        """kuberuntime_gc.go: dead containers older than min_age are evictable; per (pod,
+        container name) the newest max_per_pod_container stay (all go once the pod is gone);
+        then, with max_containers ≥ 0, the oldest are removed until the node is under it;
+        finally dead sandboxes without containers go, except each active pod's newest one.
+        Container log files are removed with their containers."""
+        now_ns = now_ns or time.time_ns()
+        sbs = await self.cri.list_pod_sandbox()
+        conts = await self.cri.list_containers()
+        sb_uid = {s.id: s.labels.get(L_POD_UID, "") for s in sbs}
+        groups: dict[tuple[str, str], list] = {}
+        for c in conts:
+            if c.state == C.CONTAINER_RUNNING or c.state == C.CONTAINER_CREATED:
+                continue
+            if now_ns - c.created_at < min_age * 1e9:
+                continue
+            uid = sb_uid.get(c.pod_sandbox_id) or c.labels.get(L_POD_UID, "")
+            groups.setdefault((uid, c.metadata.name), []).append(c)
+        evict = []
+        for (uid, _name), lst in groups.items():
+            lst.sort(key=lambda c: c.created_at, reverse=True)
+            keep = max_per_pod_container if is_active(uid) else 0
+            evict += lst[keep:]
+            groups[(uid, _name)] = lst[:keep]
+        if max_containers >= 0:
+            rest = sorted((c for lst in groups.values() for c in lst), key=lambda c: c.created_at)
+            evict += rest[:max(0, len(rest) - max_containers)]
+        removed = 0
+        for c in evict:
+            try:
+                st, _ = await self.cri.container_status(c.id)
+                log_path = st.log_path
+            except grpc.RpcError:
+                log_path = ""
+            try:
+                await self.cri.remove_container(c.id)
+                removed += 1
+            except grpc.RpcError:
+                continue
+            if log_path:
+                try:
+                    os.unlink(log_path)
+                except OSError:
+                    pass
+        left = {c.pod_sandbox_id for c in conts if c not in evict}
+        newest: dict[str, object] = {}
+        for s in sbs:
+            uid = sb_uid[s.id]
+            if uid and (uid not in newest or s.created_at > newest[uid].created_at):
+                newest[uid] = s
+        sb_removed = 0
+        for s in sbs:
+            if s.state == C.SANDBOX_READY or s.id in left:
+                continue
+            uid = sb_uid[s.id]
+            if is_active(uid) and newest.get(uid) is s:
+                continue
+            try:
+                await self.cri.remove_pod_sandbox(s.id)
+                self.sandbox_ips.pop(s.id, None)
+                sb_removed += 1
+            except grpc.RpcError:
+                pass
+        return {"containers": removed, "sandboxes": sb_removed}
+
     async def remove_pod(self, uid: str, sandboxes=None):
         for s in sandboxes if sandboxes is not None else await self.cri.list_pod_sandbox(uid):
             await self.cri.remove_pod_sandbox(s.id)

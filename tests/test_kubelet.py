@@ -260,3 +260,61 @@ def test_full_status_event_merges_into_runtime_cache():
                                     pod_sandbox_status=C.PodSandboxStatus(id="old", metadata=C.PodSandboxMetadata(uid="u")))
     after = apply_event(new, gone, ips)
     assert [s[0] for s in after.sandboxes] == ["new"] and [c.id for c in after.containers["c"]] == ["c1"]
+
+
+def test_container_gc_keeps_newest_dead_container_per_pod_container():
+    """kuberuntime_gc_test.go: per (pod, container) the newest dead container stays for an
+    active pod, all go for a deleted pod, dead sandboxes without containers are removed except
+    an active pod's newest one, and container logs go with their containers."""
+    import asyncio
+    import os
+    from amdkube.localcluster import LocalCluster, wait_pod
+
+    async def go():
+        async with LocalCluster(gpus="none", relist_period=0.2, with_controllers=False,
+                                kubelet_kw={"gc_period": 3600}) as lc:
+            c = lc.client
+            await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "crash"},
+                            "spec": {"restartPolicy": "OnFailure",
+                                     "containers": [{"name": "c", "image": "busybox", "command": ["sh", "-c", "exit 3"]}]}},
+                           "default")
+            await wait_pod(c, "default", "crash", ("Running", "Pending", "Failed"), 20)
+            uid = (await c.get("pods", "crash", "default"))["metadata"]["uid"]
+            # two more attempts of the same container, created the way a restart does
+            for _ in range(60):
+                dead = [x for x in lc.shim.containers.values() if x.labels.get("io.kubernetes.pod.uid") == uid and x.state == 2]
+                if dead:
+                    break
+                await asyncio.sleep(0.05)
+            assert dead
+            sid = dead[0].sandbox_id
+            import copy
+            for i in range(2):
+                clone = copy.copy(dead[0])
+                clone.id = f"{dead[0].id[:-1]}{i}"
+                clone.created_at = dead[0].created_at - (i + 1) * 10**9
+                clone.log_path = dead[0].log_path + f".old{i}"
+                open(clone.log_path, "w").write("old\n")
+                lc.shim.containers[clone.id] = clone
+            before = [(x.id, x.state, x.created_at) for x in lc.shim.containers.values() if x.labels.get("io.kubernetes.pod.uid") == uid]
+            out = await lc.kubelet.container_gc()
+            left = [x for x in lc.shim.containers.values() if x.labels.get("io.kubernetes.pod.uid") == uid]
+            dead_before = [b for b in before if b[1] == 2]
+            newest = max(dead_before, key=lambda b: b[2])[0]
+            running = [b for b in before if b[1] != 2]
+            assert out["containers"] == len(dead_before) - 1, (out, before)
+            assert {x.id for x in left} == {newest} | {b[0] for b in running}
+            assert not any(os.path.exists(dead[0].log_path + f".old{i}") for i in range(2))
+            assert sid in lc.shim.sandboxes
+            # once the pod is gone from the API, everything of it is collected
+            await c.delete("pods", "crash", "default", grace=0)
+            for _ in range(100):
+                if not [x for x in lc.shim.containers.values() if x.labels.get("io.kubernetes.pod.uid") == uid] \
+                        and sid not in lc.shim.sandboxes:
+                    break
+                await lc.kubelet.container_gc()
+                await asyncio.sleep(0.05)
+            assert sid not in lc.shim.sandboxes
+
+    from tests.conftest import run
+    run(go(), 60)
