@@ -199,6 +199,12 @@ def kubelet(argv):
     ap.add_argument("--max-pods", type=int, default=110)
     ap.add_argument("--maximum-dead-containers-per-container", type=int, default=1)
     ap.add_argument("--maximum-dead-containers", type=int, default=-1)
+    ap.add_argument("--eviction-hard", default=None, help="e.g. memory.available<100Mi,nodefs.available<10%%")
+    ap.add_argument("--eviction-soft", default="")
+    ap.add_argument("--eviction-soft-grace-period", default="")
+    ap.add_argument("--eviction-minimum-reclaim", default="")
+    ap.add_argument("--eviction-pressure-transition-period", type=float, default=300.0, help="seconds")
+    ap.add_argument("--eviction-max-pod-grace-period", type=int, default=0)
     ap.add_argument("--minimum-container-ttl-duration", type=float, default=0.0, help="seconds")
     ap.add_argument("--node-labels", default="")
     ap.add_argument("--register-with-taints", default="")
@@ -234,7 +240,12 @@ def kubelet(argv):
                         resolv_conf=a.resolv_conf,
                         maximum_dead_containers_per_container=a.maximum_dead_containers_per_container,
                         maximum_dead_containers=a.maximum_dead_containers,
-                        minimum_container_ttl_duration=a.minimum_container_ttl_duration)
+                        minimum_container_ttl_duration=a.minimum_container_ttl_duration,
+                        eviction_hard=a.eviction_hard, eviction_soft=a.eviction_soft,
+                        eviction_soft_grace_period=a.eviction_soft_grace_period,
+                        eviction_minimum_reclaim=a.eviction_minimum_reclaim,
+                        eviction_pressure_transition_period=a.eviction_pressure_transition_period,
+                        eviction_max_pod_grace_period=a.eviction_max_pod_grace_period)
 
     async def mk():
         smi = None

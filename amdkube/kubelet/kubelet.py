@@ -72,6 +72,12 @@ class KubeletConfig:
     evented_pleg: bool = True
     eviction_memory_available_bytes: int = 100 * 2 ** 20
     eviction_interval: float = 10.0
+    eviction_hard: str | None = None                # --eviction-hard (default: memory.available<eviction_memory_available_bytes)
+    eviction_soft: str = ""                         # --eviction-soft
+    eviction_soft_grace_period: str = ""            # --eviction-soft-grace-period
+    eviction_minimum_reclaim: str = ""              # --eviction-minimum-reclaim
+    eviction_pressure_transition_period: float = 300.0
+    eviction_max_pod_grace_period: int = 0
     chaos_chance: float = 0.0
     gpu_stats_backend: str = "none"                 # amdsmi|sysfs|fake|auto|none (per-container accelerator stats)
     cpu_capacity: int | None = None
@@ -137,6 +143,13 @@ class Kubelet:
             self.runtime.legacy, self.runtime.active_pods = self.gpu_legacy, self.active_pods
         from ..security.apparmor import Validator as AppArmorValidator
         self.apparmor = AppArmorValidator(self.gates("AppArmor"), apparmor_fs=config.apparmor_fs)
+        from .eviction import EvictionManager, observe, parse_thresholds
+        hard = config.eviction_hard if config.eviction_hard is not None else f"memory.available<{config.eviction_memory_available_bytes}"
+        self.eviction = EvictionManager(parse_thresholds(hard, config.eviction_soft, config.eviction_soft_grace_period,
+                                                         config.eviction_minimum_reclaim),
+                                        config.eviction_pressure_transition_period, config.eviction_max_pod_grace_period)
+        self.eviction_observer = lambda: observe(config.root_dir if os.path.isdir(config.root_dir) else "/")
+        self.pressure: set[str] = set()
         self.status = StatusManager(client, on_terminal=self._on_terminal)
         self.node: dict | None = None
         self.informer: Informer | None = None
@@ -287,13 +300,12 @@ class Kubelet:
             p = prev_conds.get(t)
             return {"type": t, "status": st, "reason": reason, "message": msg, "lastHeartbeatTime": now,
                     "lastTransitionTime": p["lastTransitionTime"] if p and p.get("status") == st else now}
-        import psutil
-        mem_avail = psutil.virtual_memory().available
-        mem_pressure = mem_avail < self.cfg.eviction_memory_available_bytes
+        mem_pressure, disk_pressure = "MemoryPressure" in self.pressure, "DiskPressure" in self.pressure
         conds = [cond("Ready", True, "KubeletReady", "kubelet is posting ready status"),
                  cond("MemoryPressure", mem_pressure, "KubeletHasSufficientMemory" if not mem_pressure else "KubeletHasInsufficientMemory",
-                      "kubelet has sufficient memory available" if not mem_pressure else "memory pressure"),
-                 cond("DiskPressure", False, "KubeletHasNoDiskPressure", "kubelet has no disk pressure"),
+                      "kubelet has sufficient memory available" if not mem_pressure else "kubelet has insufficient memory available"),
+                 cond("DiskPressure", disk_pressure, "KubeletHasNoDiskPressure" if not disk_pressure else "KubeletHasDiskPressure",
+                      "kubelet has no disk pressure" if not disk_pressure else "kubelet has disk pressure"),
                  cond("OutOfDisk", False, "KubeletHasSufficientDisk", "kubelet has sufficient disk space available")]
         st = {"capacity": cap, "allocatable": alloc, "conditions": conds,
               "addresses": [{"type": "InternalIP", "address": self.cfg.node_ip}, {"type": "Hostname", "address": self.node_name}],
@@ -551,6 +563,9 @@ class Kubelet:
                                        ("NoExecute",))
         if taint:
             return False, "Taint", f"pod does not tolerate taint {taint.get('key')}={taint.get('value', '')}:NoExecute"
+        ok, msg = self.eviction.admit(pod, self.pressure)   # eviction_manager.go Admit
+        if not ok:
+            return False, "Evicted", msg
         err = self.apparmor.validate(pod)   # lifecycle/handlers.go:142-165
         if err:
             return False, "AppArmor", f"Cannot enforce AppArmor: {err}"
@@ -1005,18 +1020,55 @@ class Kubelet:
 
     # ================================================================ eviction
     async def _eviction_loop(self):
-        import psutil
         while True:
             await asyncio.sleep(self.cfg.eviction_interval)
-            if psutil.virtual_memory().available >= self.cfg.eviction_memory_available_bytes:
-                continue
-            victims = sorted(self.active_pods(), key=lambda p: ({"BestEffort": 0, "Burstable": 1}.get(
-                (p.get("status") or {}).get("qosClass"), 2), -(m.parse_time(m.meta(p).get("creationTimestamp")) or 0)))
-            if not victims:
-                continue
-            v = victims[0]
-            self.m_evictions.labels("memory.available").inc()
-            self.recorder.event(v, "Warning", "Evicted", "The node was low on resource: memory.")
-            await self.runtime.kill_pod(m.uid_of(v), 0, v)
-            self.status.set(v, {"phase": "Failed", "reason": "Evicted", "message": "The node was low on resource: memory.",
-                                "conditions": (v.get("status") or {}).get("conditions") or []})
+            try:
+                await self.eviction_pass()
+            except Exception as e:
+                log.debug("eviction pass failed: %r", e)
+
+    async def _pod_usage(self, signal: str) -> dict[str, int]:
+        """Per-pod usage for ranking: memory working set from the runtime's container stats,
+        or bytes of logs + emptyDir volumes for disk signals."""
+        from .eviction import MEMORY
+        usage: dict[str, int] = {}
+        if signal == MEMORY:
+            for st in await self.cri.list_container_stats():
+                uid = st.attributes.labels.get(L_POD_UID, "")
+                usage[uid] = usage.get(uid, 0) + int(st.memory.working_set_bytes.value)
+            return usage
+        for uid in self.pods:
+            tot = 0
+            for sub in ("logs", "volumes"):
+                for dp, _dn, fns in os.walk(os.path.join(self.cfg.root_dir, "pods", uid, sub)):
+                    for fn in fns:
+                        try:
+                            tot += os.path.getsize(os.path.join(dp, fn))
+                        except OSError:
+                            pass
+            usage[uid] = tot
+        return usage
+
+    async def eviction_pass(self):
+        """One synchronize() of the eviction manager: conditions, then at most one eviction."""
+        obs = self.eviction_observer()
+        pressure = self.eviction.conditions(obs)
+        if pressure != self.pressure:
+            self.pressure = pressure
+            self._node_dirty.set()
+        met = self.eviction.met(obs)
+        if not met:
+            return None
+        sig = sorted(met, key=lambda x: x.signal != "memory.available")[0].signal
+        victim, t = self.eviction.choose(self.active_pods(), obs, await self._pod_usage(sig))
+        if victim is None:
+            return None
+        res = {"memory.available": "memory"}.get(t.signal, "ephemeral-storage")
+        msg = f"The node was low on resource: {res}."
+        self.eviction.evictions += 1
+        self.m_evictions.labels(t.signal).inc()
+        self.recorder.event(victim, "Warning", "Evicted", msg)
+        await self.runtime.kill_pod(m.uid_of(victim), self.eviction.grace_for(victim, t), victim)
+        self.status.set(victim, {"phase": "Failed", "reason": "Evicted", "message": msg,
+                                 "conditions": (victim.get("status") or {}).get("conditions") or []})
+        return victim
