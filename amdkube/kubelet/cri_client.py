@@ -19,6 +19,9 @@ CURRENT_POD: contextvars.ContextVar[str | None] = contextvars.ContextVar("amdkub
 class CRIClient:
     def __init__(self, socket_path: str, timeout: float = 10.0, metrics=None):
         self._pod_mut: dict[str, int] = {}
+        self._cid_sid: dict[str, str] = {}
+        # uid -> {sandbox id: start time (ns) of the last mutating call on it}; None: unknown target
+        self._touched: dict[str, dict[str, int] | None] = {}
         self.socket = socket_path
         self.timeout = timeout
         self.ch = None
@@ -48,6 +51,25 @@ class CRIClient:
 
     def forget_pod(self, uid: str):
         self._pod_mut.pop(uid, None)
+        self._touched.pop(uid, None)
+
+    def take_touched(self, uid: str):
+        """Sandboxes the pod's worker mutated since the last call, with the start time of the last
+        mutation on each (None when a call's sandbox was unknown)."""
+        return self._touched.pop(uid, {})
+
+    def _touch(self, sid: str | None, t0: int):
+        uid = CURRENT_POD.get()
+        if uid is None:
+            return
+        cur = self._touched.get(uid, {})
+        if cur is None:
+            return
+        if sid is None:
+            self._touched[uid] = None
+        else:
+            cur[sid] = t0
+            self._touched[uid] = cur
 
     async def _call(self, op, fn, req, timeout=None):
         t0 = time.perf_counter()
@@ -75,12 +97,17 @@ class CRIClient:
         return await self._call("status", self.rt.Status, C.StatusRequest(verbose=True))
 
     async def run_pod_sandbox(self, cfg) -> str:
-        return (await self._call("run_podsandbox", self.rt.RunPodSandbox, C.RunPodSandboxRequest(config=cfg))).pod_sandbox_id
+        t0 = time.time_ns()
+        sid = (await self._call("run_podsandbox", self.rt.RunPodSandbox, C.RunPodSandboxRequest(config=cfg))).pod_sandbox_id
+        self._touch(sid, t0)
+        return sid
 
     async def stop_pod_sandbox(self, sid):
+        self._touch(sid, time.time_ns())
         await self._call("stop_podsandbox", self.rt.StopPodSandbox, C.StopPodSandboxRequest(pod_sandbox_id=sid), timeout=60)
 
     async def remove_pod_sandbox(self, sid):
+        self._touch(sid, time.time_ns())
         await self._call("remove_podsandbox", self.rt.RemovePodSandbox, C.RemovePodSandboxRequest(pod_sandbox_id=sid), timeout=60)
 
     async def list_pod_sandbox(self, uid: str | None = None):
@@ -96,17 +123,23 @@ class CRIClient:
         return (await self._call("podsandbox_status", self.rt.PodSandboxStatus, C.PodSandboxStatusRequest(pod_sandbox_id=sid))).status
 
     async def create_container(self, sid, cfg, sandbox_cfg) -> str:
+        self._touch(sid, time.time_ns())
         req = C.CreateContainerRequest(pod_sandbox_id=sid, config=cfg, sandbox_config=sandbox_cfg)
-        return (await self._call("create_container", self.rt.CreateContainer, req)).container_id
+        cid = (await self._call("create_container", self.rt.CreateContainer, req)).container_id
+        self._cid_sid[cid] = sid
+        return cid
 
     async def start_container(self, cid):
+        self._touch(self._cid_sid.get(cid), time.time_ns())
         await self._call("start_container", self.rt.StartContainer, C.StartContainerRequest(container_id=cid))
 
     async def stop_container(self, cid, timeout: int):
+        self._touch(self._cid_sid.get(cid), time.time_ns())
         await self._call("stop_container", self.rt.StopContainer, C.StopContainerRequest(container_id=cid, timeout=timeout),
                          timeout=timeout + 30)
 
     async def remove_container(self, cid):
+        self._touch(self._cid_sid.pop(cid, None), time.time_ns())
         await self._call("remove_container", self.rt.RemoveContainer, C.RemoveContainerRequest(container_id=cid))
 
     async def list_containers(self, sandbox_id: str | None = None):

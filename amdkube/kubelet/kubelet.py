@@ -167,6 +167,8 @@ class Kubelet:
         self._rt_gen: dict[str, int] = {}
         self._rt_cache: dict[str, tuple] = {}     # uid -> ((gen, mutations), PodRuntimeStatus, fetch start ns)
         self._rt_pending: dict[str, list] = {}    # uid -> full-status events that arrived while the cache was stale
+        self._pending_waiters: dict[str, asyncio.Event] = {}
+        self._full_events = False                 # the runtime's events carry complete pod state
         self.smi = smi_backend
         self.server = None
         self.first_seen: dict[str, float] = {}
@@ -638,9 +640,14 @@ class Kubelet:
         POD_TRACE(uid, "sync_ctx")
         rt = await self._cached_status(uid)
         mut0 = self.cri.pod_mutations(uid)
+        self.cri.take_touched(uid)
         errors = await self.runtime.sync_pod(pod, rt, ctx, self.liveness_failed.pop(uid, None))
         if self.cri.pod_mutations(uid) != mut0 or errors:
-            rt = await self._cached_status(uid, fresh=True)
+            touched = self.cri.take_touched(uid)
+            new_rt = None
+            if touched and not errors and self._full_events:
+                new_rt = await self._status_from_events(uid, touched)
+            rt = new_rt if new_rt is not None else await self._cached_status(uid, fresh=True)
         for sb in rt.sandboxes:
             self._sandbox_uid[sb[0]] = uid
         st = generate_status(pod, rt, self.cfg.node_ip, self.readiness.get(uid, {}), errors, m.now_rfc3339())
@@ -702,7 +709,15 @@ class Kubelet:
             return hit[1]
         key = (self._rt_gen.get(uid, 0), self.cri.pod_mutations(uid))
         t0 = time.time_ns()
-        rt = await self.runtime.pod_status(uid)
+        pod = self.pods.get(uid)
+        if not fresh and uid not in self._rt_cache and self._full_events and pod is not None and \
+                (m.parse_time((pod.get("metadata") or {}).get("creationTimestamp")) or 0) >= self.started_at + 1.0:
+            # created after this kubelet started and never synced: the runtime cannot hold
+            # anything of it yet (its sandboxes would be reported through the event stream)
+            from .kuberuntime import PodRuntimeStatus
+            rt = PodRuntimeStatus(uid)
+        else:
+            rt = await self.runtime.pod_status(uid)
         for ev in self._rt_pending.pop(uid, ()):
             if ev.created_at > t0:
                 rt = apply_event(rt, ev, self.runtime.sandbox_ips)
@@ -714,14 +729,52 @@ class Kubelet:
         return [SandboxRef(x[0], x[1]) for x in hit[1].sandboxes] if hit is not None else None
 
     def _apply_full_event(self, uid: str, ev):
+        for cs in ev.containers_statuses:
+            self.cri._cid_sid[cs.id] = ev.pod_sandbox_status.id
         hit = self._cache_valid(uid)
         if hit is not None:
             if ev.created_at > hit[2]:
-                self._rt_cache[uid] = (hit[0], apply_event(hit[1], ev, self.runtime.sandbox_ips), hit[2])
+                self._rt_cache[uid] = (hit[0], apply_event(hit[1], ev, self.runtime.sandbox_ips), max(hit[2], ev.created_at))
         else:
             pend = self._rt_pending.setdefault(uid, [])
             pend.append(ev)
             del pend[:-64]
+            w = self._pending_waiters.get(uid)
+            if w is not None:
+                w.set()
+
+    async def _status_from_events(self, uid: str, touched: dict, timeout: float = 0.25):
+        """The pod's status after its own mutations, from the runtime's events instead of a
+        re-list: every mutated sandbox's state is taken from an event emitted after the last
+        mutation on it (each mutating CRI call emits one with the complete sandbox state before
+        it returns); untouched sandboxes keep the cached state. None → the caller re-lists."""
+        base = self._rt_cache.get(uid)
+        if base is None:
+            return None
+        loop = asyncio.get_running_loop()
+        deadline = loop.time() + timeout
+        while True:
+            pend = self._rt_pending.get(uid, ())
+            if all(any(e.pod_sandbox_status.id == sid and e.created_at >= t for e in pend) for sid, t in touched.items()):
+                break
+            rem = deadline - loop.time()
+            if rem <= 0:
+                return None
+            w = self._pending_waiters.setdefault(uid, asyncio.Event())
+            w.clear()
+            try:
+                await asyncio.wait_for(w.wait(), rem)
+            except asyncio.TimeoutError:
+                return None
+        key = (self._rt_gen.get(uid, 0), self.cri.pod_mutations(uid))
+        rt, t_last = base[1], base[2]
+        for e in self._rt_pending.pop(uid, ()):
+            if e.created_at > base[2]:
+                rt = apply_event(rt, e, self.runtime.sandbox_ips)
+                t_last = max(t_last, e.created_at)
+        self._pending_waiters.pop(uid, None)
+        self._rt_cache[uid] = (key, rt, t_last)
+        return rt
 
     def _pleg_event(self, uid: str):
         self._rt_gen[uid] = self._rt_gen.get(uid, 0) + 1
@@ -731,6 +784,7 @@ class Kubelet:
         self._rt_gen.pop(uid, None)
         self._rt_cache.pop(uid, None)
         self._rt_pending.pop(uid, None)
+        self._pending_waiters.pop(uid, None)
         self.cri.forget_pod(uid)
         if self.gpu_legacy is not None:
             self.gpu_legacy.release(uid)
@@ -911,6 +965,7 @@ class Kubelet:
                     full = bool(sst.metadata.uid)   # the runtime sends complete pod state (KEP-3386)
                     if full:
                         self._sandbox_uid[sid] = sst.metadata.uid
+                        self._full_events = True
                     uid = self._sandbox_uid.get(sid)
                     if uid is None:
                         for s in await self.cri.list_pod_sandbox():

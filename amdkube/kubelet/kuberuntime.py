@@ -173,8 +173,11 @@ class RuntimeManager:
                 if ip:
                     self.sandbox_ips[ready[0]] = ip
             st.ip = ip or ""
+        if len(self.cri._cid_sid) > 100000:
+            self.cri._cid_sid.clear()
         for s in sbs:
             for c in await self.cri.list_containers(s.id):
+                self.cri._cid_sid[c.id] = s.id
                 try:
                     cs, _ = await self.cri.container_status(c.id)
                 except grpc.RpcError:
