@@ -189,3 +189,6 @@ message ContainerEventResponse {
 # waiting for the next relist (the relist still runs as the consistency backstop).
 
 API_VERSION = "0.1.0"
+# trailing-metadata key of rocshim's mutating calls: "<sandbox id>:<created_at>" of the newest
+# event emitted for the call's sandbox when it returned ("" = no event to wait for)
+EVENT_TRAILER = "amdkube-event"

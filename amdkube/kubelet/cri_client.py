@@ -8,7 +8,7 @@ import time
 
 import grpc
 
-from ..grpcdesc.cri import CRI as C
+from ..grpcdesc.cri import CRI as C, EVENT_TRAILER
 from ..utils.grpcutil import uds_channel
 
 # the pod a kubelet pod worker is syncing (set once per worker task; asyncio copies it into
@@ -20,7 +20,8 @@ class CRIClient:
     def __init__(self, socket_path: str, timeout: float = 10.0, metrics=None):
         self._pod_mut: dict[str, int] = {}
         self._cid_sid: dict[str, str] = {}
-        # uid -> {sandbox id: start time (ns) of the last mutating call on it}; None: unknown target
+        # uid -> {sandbox id: created_at of the runtime event that carries the sandbox's state after
+        # the pod worker's last mutating call on it}; None: a call's final event is unknown
         self._touched: dict[str, dict[str, int] | None] = {}
         self.socket = socket_path
         self.timeout = timeout
@@ -54,32 +55,46 @@ class CRIClient:
         self._touched.pop(uid, None)
 
     def take_touched(self, uid: str):
-        """Sandboxes the pod's worker mutated since the last call, with the start time of the last
-        mutation on each (None when a call's sandbox was unknown)."""
+        """Sandboxes the pod's worker mutated since the last call, each with the created_at of the
+        runtime event that reflects the last of those mutations (None when some call's final event
+        is unknown: a runtime that does not return the event trailer)."""
         return self._touched.pop(uid, {})
 
-    def _touch(self, sid: str | None, t0: int):
+    def _touch(self, mark: str | None):
+        """Record a mutating call's event trailer for the pod being synced: "" means the call
+        emitted nothing to wait for (e.g. removing an already-removed container)."""
         uid = CURRENT_POD.get()
         if uid is None:
             return
         cur = self._touched.get(uid, {})
         if cur is None:
             return
-        if sid is None:
+        if mark is None:
             self._touched[uid] = None
-        else:
-            cur[sid] = t0
+        elif mark:
+            sid, _, ts = mark.rpartition(":")
+            cur[sid] = max(cur.get(sid, 0), int(ts))
             self._touched[uid] = cur
 
     async def _call(self, op, fn, req, timeout=None):
         t0 = time.perf_counter()
-        if op in self._MUTATING:
+        mutating = op in self._MUTATING
+        if mutating:
             self.mutations += 1
             uid = CURRENT_POD.get()
             if uid is not None:
                 self._pod_mut[uid] = self._pod_mut.get(uid, 0) + 1
         try:
-            return await fn(req, timeout=timeout or self.timeout)
+            if not mutating:
+                return await fn(req, timeout=timeout or self.timeout)
+            call = fn(req, timeout=timeout or self.timeout)
+            resp = await call
+            mark = None
+            for k, v in (await call.trailing_metadata()) or ():
+                if k == EVENT_TRAILER:
+                    mark = v
+            self._touch(mark)
+            return resp
         except grpc.RpcError:
             if self.metrics:
                 self.metrics[1].labels(op).inc()
@@ -97,17 +112,12 @@ class CRIClient:
         return await self._call("status", self.rt.Status, C.StatusRequest(verbose=True))
 
     async def run_pod_sandbox(self, cfg) -> str:
-        t0 = time.time_ns()
-        sid = (await self._call("run_podsandbox", self.rt.RunPodSandbox, C.RunPodSandboxRequest(config=cfg))).pod_sandbox_id
-        self._touch(sid, t0)
-        return sid
+        return (await self._call("run_podsandbox", self.rt.RunPodSandbox, C.RunPodSandboxRequest(config=cfg))).pod_sandbox_id
 
     async def stop_pod_sandbox(self, sid):
-        self._touch(sid, time.time_ns())
         await self._call("stop_podsandbox", self.rt.StopPodSandbox, C.StopPodSandboxRequest(pod_sandbox_id=sid), timeout=60)
 
     async def remove_pod_sandbox(self, sid):
-        self._touch(sid, time.time_ns())
         await self._call("remove_podsandbox", self.rt.RemovePodSandbox, C.RemovePodSandboxRequest(pod_sandbox_id=sid), timeout=60)
 
     async def list_pod_sandbox(self, uid: str | None = None):
@@ -123,23 +133,20 @@ class CRIClient:
         return (await self._call("podsandbox_status", self.rt.PodSandboxStatus, C.PodSandboxStatusRequest(pod_sandbox_id=sid))).status
 
     async def create_container(self, sid, cfg, sandbox_cfg) -> str:
-        self._touch(sid, time.time_ns())
         req = C.CreateContainerRequest(pod_sandbox_id=sid, config=cfg, sandbox_config=sandbox_cfg)
         cid = (await self._call("create_container", self.rt.CreateContainer, req)).container_id
         self._cid_sid[cid] = sid
         return cid
 
     async def start_container(self, cid):
-        self._touch(self._cid_sid.get(cid), time.time_ns())
         await self._call("start_container", self.rt.StartContainer, C.StartContainerRequest(container_id=cid))
 
     async def stop_container(self, cid, timeout: int):
-        self._touch(self._cid_sid.get(cid), time.time_ns())
         await self._call("stop_container", self.rt.StopContainer, C.StopContainerRequest(container_id=cid, timeout=timeout),
                          timeout=timeout + 30)
 
     async def remove_container(self, cid):
-        self._touch(self._cid_sid.pop(cid, None), time.time_ns())
+        self._cid_sid.pop(cid, None)
         await self._call("remove_container", self.rt.RemoveContainer, C.RemoveContainerRequest(container_id=cid))
 
     async def list_containers(self, sandbox_id: str | None = None):

@@ -33,11 +33,19 @@ class Threshold:
     quantity: int | None = None       # absolute (bytes / inodes)
     percentage: float | None = None   # of capacity
     grace: float = 0.0                # soft thresholds
-    min_reclaim: int = 0
+    min_reclaim: int = 0              # absolute minimum reclaim
+    min_reclaim_pct: float = 0.0      # minimum reclaim as a fraction of capacity
     hard: bool = True
 
     def value(self, capacity: int) -> int:
         return self.quantity if self.quantity is not None else int(capacity * (self.percentage or 0.0))
+
+    def reclaim(self, capacity: int) -> int:
+        return self.min_reclaim + int(capacity * self.min_reclaim_pct)
+
+    @property
+    def key(self):
+        return (self.signal, self.hard)
 
 
 def _duration(s: str) -> float:
@@ -79,7 +87,10 @@ def parse_thresholds(hard: str = "", soft: str = "", soft_grace: str = "", min_r
                 t.grace = graces[sig]
             if sig in reclaims:
                 r = reclaims[sig]
-                t.min_reclaim = int(Quantity(r).value()) if not r.endswith("%") else -int(float(r[:-1]) * 100)
+                if r.endswith("%"):
+                    t.min_reclaim_pct = float(r[:-1]) / 100.0
+                else:
+                    t.min_reclaim = int(Quantity(r).value())
             out.append(t)
     return out
 
@@ -99,27 +110,28 @@ def observe(root_dir: str = "/", image_dir: str | None = None) -> dict:
     return obs
 
 
-QOS_ORDER = {"BestEffort": 0, "Burstable": 1, "Guaranteed": 2}
+def _requests(p: dict, resource: str) -> int:
+    tot = 0
+    for c in (p.get("spec") or {}).get("containers") or []:
+        res = c.get("resources") or {}
+        r = (res.get("requests") or {}).get(resource) or (res.get("limits") or {}).get(resource)   # defaulting: requests := limits
+        tot += Quantity(r).value() if r else 0
+    return tot
 
 
-def rank(pods: list[dict], signal: str, usage: dict[str, int]) -> list[dict]:
-    """rank.go: lowest QoS first; within a class the pod furthest above its requests (memory)
-    or using the most disk goes first; priority (lower first) breaks ties like the 1.9 code."""
-    from .qos import pod_qos
-
-    def requests(p):
-        if RESOURCE[signal] != "memory":
-            return 0
-        tot = 0
-        for c in (p.get("spec") or {}).get("containers") or []:
-            r = ((c.get("resources") or {}).get("requests") or {}).get("memory")
-            tot += Quantity(r).value() if r else 0
-        return tot
+def rank(pods: list[dict], signal: str, usage: dict[str, int], use_priority: bool = True) -> list[dict]:
+    """helpers.go:695-703 orderedBy(exceedRequests, priority, usage): pods without stats first,
+    then pods whose usage exceeds their request of the starved resource, then lower priority
+    (only with the PodPriority gate, helpers.go:519-533), then the larger usage above request."""
+    res = "memory" if RESOURCE[signal] == "memory" else "ephemeral-storage"
 
     def key(p):
         uid = (p.get("metadata") or {}).get("uid", "")
-        u = usage.get(uid, 0)
-        return (QOS_ORDER[pod_qos(p)], int((p.get("spec") or {}).get("priority") or 0), -(u - requests(p)))
+        if uid not in usage:
+            return (0, 0, 0, 0)
+        u, req = usage[uid], _requests(p, res)
+        prio = int((p.get("spec") or {}).get("priority") or 0) if use_priority else 0
+        return (1, 0 if u > req else 1, prio, -(u - req))
     return sorted(pods, key=key)
 
 
@@ -130,23 +142,29 @@ class EvictionManager:
     max_pod_grace: int = 0
     observer: object = None
     clock: object = time.monotonic
+    use_priority: bool = True
     first_seen: dict = field(default_factory=dict)     # signal → when the (soft) threshold was first met
     pressure_since: dict = field(default_factory=dict)  # condition → last time it was observed
+    last_met: set = field(default_factory=set)          # keys of thresholds met at the last pass (m.thresholdsMet)
     evictions: int = 0
 
     def met(self, obs: dict) -> list[Threshold]:
+        """eviction_manager.go:267-275: thresholds met now, merged with previously met ones that
+        are not yet resolved, i.e. still below threshold + minimum reclaim."""
         out = []
         now = self.clock()
         for t in self.thresholds:
             if t.signal not in obs:
                 continue
             avail, cap = obs[t.signal]
-            if avail < t.value(cap):
-                self.first_seen.setdefault((t.signal, t.hard), now)
-                if t.hard or now - self.first_seen[(t.signal, t.hard)] >= t.grace:
+            bound = t.value(cap) + (t.reclaim(cap) if t.key in self.last_met else 0)
+            if avail < bound:
+                self.first_seen.setdefault(t.key, now)
+                if t.hard or now - self.first_seen[t.key] >= t.grace:
                     out.append(t)
             else:
-                self.first_seen.pop((t.signal, t.hard), None)
+                self.first_seen.pop(t.key, None)
+        self.last_met = {t.key for t in out}
         return out
 
     def conditions(self, obs: dict) -> set[str]:
@@ -170,10 +188,9 @@ class EvictionManager:
         if not met or not pods:
             return None, None
         t = sorted(met, key=lambda x: (x.signal != MEMORY, not x.hard))[0]   # memory first (reference order)
-        return rank(pods, t.signal, usage)[0], t
+        return rank(pods, t.signal, usage, self.use_priority)[0], t
 
     def grace_for(self, pod: dict, t: Threshold) -> int:
-        if t.hard:
-            return 0
-        g = int((pod.get("spec") or {}).get("terminationGracePeriodSeconds", 30))
-        return min(g, self.max_pod_grace) if self.max_pod_grace else g
+        """eviction_manager.go:391-396: hard evictions kill immediately; soft ones get
+        MaxPodGracePeriodSeconds (default 0), not the pod's own grace period."""
+        return 0 if t.hard else int(self.max_pod_grace)

@@ -42,6 +42,7 @@ from .cri_client import CURRENT_POD, CRIClient
 from .devicemanager import AdmissionError, ManagerImpl, ManagerStub
 from ..utils.trace import POD_TRACE
 from .kuberuntime import L_POD_UID, RuntimeManager, SandboxRef, apply_event
+from .qos import CRITICAL_ANNOTATION
 from .status import StatusManager, generate_status
 
 log = logging.getLogger("amdkube.kubelet")
@@ -50,6 +51,22 @@ log = logging.getLogger("amdkube.kubelet")
 SOURCE_ANNOTATION = "kubernetes.io/config.source"
 HASH_ANNOTATION = "kubernetes.io/config.hash"
 MIRROR_ANNOTATION = "kubernetes.io/config.mirror"
+
+
+def _atomic_write(path: str, data: bytes):
+    """pkg/volume/util/atomic_writer.go: a running container never sees a half-written volume
+    file; unchanged content is not rewritten (every pod sync resolves the volumes again)."""
+    try:
+        with open(path, "rb") as f:
+            if f.read() == data:
+                return
+    except OSError:
+        pass
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    tmp = f"{path}.{os.getpid()}.tmp"
+    with open(tmp, "wb") as f:
+        f.write(data)
+    os.replace(tmp, path)
 
 
 @dataclass
@@ -147,7 +164,8 @@ class Kubelet:
         hard = config.eviction_hard if config.eviction_hard is not None else f"memory.available<{config.eviction_memory_available_bytes}"
         self.eviction = EvictionManager(parse_thresholds(hard, config.eviction_soft, config.eviction_soft_grace_period,
                                                          config.eviction_minimum_reclaim),
-                                        config.eviction_pressure_transition_period, config.eviction_max_pod_grace_period)
+                                        config.eviction_pressure_transition_period, config.eviction_max_pod_grace_period,
+                                        use_priority=self.gates("PodPriority"))
         self.eviction_observer = lambda: observe(config.root_dir if os.path.isdir(config.root_dir) else "/")
         self.pressure: set[str] = set()
         self.status = StatusManager(client, on_terminal=self._on_terminal)
@@ -173,6 +191,8 @@ class Kubelet:
         self.server = None
         self.first_seen: dict[str, float] = {}
         self.started_at = time.time()
+        self._runtime_uids: set[str] = set()
+        self._static_read = False
         self.last_sync_loop = time.time()
         self.sync_errors: dict[str, str] = {}
         self.static: dict[str, dict] = {}      # uid -> static pod from --pod-manifest-path
@@ -195,6 +215,10 @@ class Kubelet:
     async def start(self):
         os.makedirs(os.path.join(self.cfg.root_dir, "pods"), exist_ok=True)
         await self.cri.connect()
+        # pods the runtime already holds anything of (a previous kubelet incarnation): decided
+        # from runtime state, never from creation timestamps (static pods get a fresh
+        # creationTimestamp on every manifest read; API clocks may run ahead of the node's)
+        self._runtime_uids = {s.labels.get(L_POD_UID, "") for s in await self.cri.list_pod_sandbox()} - {""}
         if self.gpu_legacy is not None:   # in-use GPUs survive a kubelet restart (the reference inspects docker)
             self.gpu_legacy.rebuild([(c.labels.get(L_POD_UID, ""), c.metadata.name, dict(c.annotations))
                                      for c in await self.cri.list_containers() if c.state == C.CONTAINER_RUNNING])
@@ -463,6 +487,7 @@ class Kubelet:
                 except Exception as e:
                     log.debug("mirror pod for %s: %r", m.name_of(pod), e)
             self._static_dirty.clear()
+            self._static_read = True
             try:
                 await asyncio.wait_for(self._static_dirty.wait(), self.cfg.file_check_frequency)
             except asyncio.TimeoutError:
@@ -611,7 +636,7 @@ class Kubelet:
         if uid not in self.admitted:
             if is_pod_terminal(pod):
                 self.admitted.add(uid)  # e.g. kubelet restart: nothing to run
-            elif (m.parse_time(md.get("creationTimestamp")) or 0) < self.started_at - 1.0 and await self._already_running(uid):
+            elif uid in self._runtime_uids and await self._already_running(uid):
                 # kubelet restart: the pod was admitted by the previous incarnation and is running;
                 # never kill it because a device plugin has not re-registered yet
                 self.admitted.add(uid)
@@ -645,7 +670,7 @@ class Kubelet:
         if self.cri.pod_mutations(uid) != mut0 or errors:
             touched = self.cri.take_touched(uid)
             new_rt = None
-            if touched and not errors and self._full_events:
+            if touched is not None and not errors and self._full_events:
                 new_rt = await self._status_from_events(uid, touched)
             rt = new_rt if new_rt is not None else await self._cached_status(uid, fresh=True)
         for sb in rt.sandboxes:
@@ -711,9 +736,9 @@ class Kubelet:
         t0 = time.time_ns()
         pod = self.pods.get(uid)
         if not fresh and uid not in self._rt_cache and self._full_events and pod is not None and \
-                (m.parse_time((pod.get("metadata") or {}).get("creationTimestamp")) or 0) >= self.started_at + 1.0:
-            # created after this kubelet started and never synced: the runtime cannot hold
-            # anything of it yet (its sandboxes would be reported through the event stream)
+                uid not in self._runtime_uids:
+            # absent from the runtime when this kubelet started and never synced since: the
+            # runtime cannot hold anything of it (its sandboxes would come through the event stream)
             from .kuberuntime import PodRuntimeStatus
             rt = PodRuntimeStatus(uid)
         else:
@@ -745,9 +770,12 @@ class Kubelet:
 
     async def _status_from_events(self, uid: str, touched: dict, timeout: float = 0.25):
         """The pod's status after its own mutations, from the runtime's events instead of a
-        re-list: every mutated sandbox's state is taken from an event emitted after the last
-        mutation on it (each mutating CRI call emits one with the complete sandbox state before
-        it returns); untouched sandboxes keep the cached state. None → the caller re-lists."""
+        re-list. Every mutating CRI call returns (trailer) the created_at of the event that carries
+        its sandbox's complete state as of the call's return; each touched sandbox's state is
+        taken once that exact event (or a newer one) has arrived, so earlier events of the same
+        call (e.g. StopPodSandbox's per-container events that still show the sandbox READY) never
+        stand for the final state. Untouched sandboxes keep the cached state; calls that emitted
+        nothing (no-ops) need no event. None → the caller re-lists (timeout)."""
         base = self._rt_cache.get(uid)
         if base is None:
             return None
@@ -755,7 +783,8 @@ class Kubelet:
         deadline = loop.time() + timeout
         while True:
             pend = self._rt_pending.get(uid, ())
-            if all(any(e.pod_sandbox_status.id == sid and e.created_at >= t for e in pend) for sid, t in touched.items()):
+            if all(t <= base[2] or any(e.pod_sandbox_status.id == sid and e.created_at >= t for e in pend)
+                   for sid, t in touched.items()):
                 break
             rem = deadline - loop.time()
             if rem <= 0:
@@ -781,6 +810,7 @@ class Kubelet:
         self.dispatch(uid)
 
     def _cleanup(self, uid):
+        self._runtime_uids.add(uid)   # the runtime may still hold leftovers: list before trusting the cache again
         self._rt_gen.pop(uid, None)
         self._rt_cache.pop(uid, None)
         self._rt_pending.pop(uid, None)
@@ -821,9 +851,7 @@ class Kubelet:
                 try:
                     obj = await self.client.get(kind, oname, ns)
                     for k, val in (obj.get("data") or {}).items():
-                        data = base64.b64decode(val) if kind == "secrets" else val.encode()
-                        with open(os.path.join(d, k), "wb") as f:
-                            f.write(data)
+                        _atomic_write(os.path.join(d, k), base64.b64decode(val) if kind == "secrets" else val.encode())
                 except m.StatusError as e:
                     if not ref.get("optional"):
                         raise RuntimeError(f"volume {name}: {kind[:-1]} {oname} not found") from e
@@ -848,8 +876,7 @@ class Kubelet:
                 for it in (v["downwardAPI"].get("items") or []):
                     fr = it.get("fieldRef") or {}
                     val = await self._env_from(pod, {"fieldRef": fr}) if fr else ""
-                    with open(os.path.join(d, it["path"]), "w") as f:
-                        f.write(val)
+                    _atomic_write(os.path.join(d, it["path"]), val.encode())
                 vols[name] = d
             else:  # emptyDir (and unknown types degrade to emptyDir)
                 d = os.path.join(base, "kubernetes.io~empty-dir", name)
@@ -951,7 +978,7 @@ class Kubelet:
         # orphaned sandboxes (pod deleted while the kubelet was down)
         for s in sbs:
             uid = s.labels.get(L_POD_UID, "")
-            if uid and uid not in self.pods and uid not in self.workers and self.informer and self.informer.has_synced():
+            if uid and uid not in self.pods and uid not in self.workers and self.sources_ready():
                 self.dispatch(uid)
 
     async def _evented_pleg(self):
@@ -991,9 +1018,17 @@ class Kubelet:
     async def container_gc(self) -> dict:
         """One pass of the container/sandbox garbage collector (active pods keep their newest
         dead container per container name for logs and restart accounting)."""
-        active = lambda uid: uid in self.pods and uid not in self.terminated_deleted   # noqa: E731
+        active = lambda uid: (uid in self.pods or uid in self.workers) and uid not in self.terminated_deleted   # noqa: E731
         return await self.runtime.garbage_collect(active, self.cfg.maximum_dead_containers_per_container,
-                                                  self.cfg.maximum_dead_containers, self.cfg.minimum_container_ttl_duration)
+                                                  self.cfg.maximum_dead_containers, self.cfg.minimum_container_ttl_duration,
+                                                  sources_ready=self.sources_ready())
+
+    def sources_ready(self) -> bool:
+        """config.SourcesReady.AllReady: every configured pod source has delivered its first
+        complete set (the API informer synced; --pod-manifest-path read once). Until then a pod
+        the kubelet does not know may simply not have been seen yet."""
+        api = self.informer is not None and self.informer.has_synced()
+        return api and (not self.cfg.pod_manifest_path or self._static_read)
 
     async def _gc_loop(self):
         while True:
@@ -1092,17 +1127,21 @@ class Kubelet:
                 uid = st.attributes.labels.get(L_POD_UID, "")
                 usage[uid] = usage.get(uid, 0) + int(st.memory.working_set_bytes.value)
             return usage
-        for uid in self.pods:
-            tot = 0
-            for sub in ("logs", "volumes"):
-                for dp, _dn, fns in os.walk(os.path.join(self.cfg.root_dir, "pods", uid, sub)):
-                    for fn in fns:
-                        try:
-                            tot += os.path.getsize(os.path.join(dp, fn))
-                        except OSError:
-                            pass
-            usage[uid] = tot
-        return usage
+        root = os.path.join(self.cfg.root_dir, "pods")
+
+        def walk(uids):   # directory walks block: off the event loop
+            for uid in uids:
+                tot = 0
+                for sub in ("logs", "volumes"):
+                    for dp, _dn, fns in os.walk(os.path.join(root, uid, sub)):
+                        for fn in fns:
+                            try:
+                                tot += os.path.getsize(os.path.join(dp, fn))
+                            except OSError:
+                                pass
+                usage[uid] = tot
+            return usage
+        return await asyncio.to_thread(walk, list(self.pods))
 
     async def eviction_pass(self):
         """One synchronize() of the eviction manager: conditions, then at most one eviction."""
@@ -1115,7 +1154,12 @@ class Kubelet:
         if not met:
             return None
         sig = sorted(met, key=lambda x: x.signal != "memory.available")[0].signal
-        victim, t = self.eviction.choose(self.active_pods(), obs, await self._pod_usage(sig))
+        cands = self.active_pods()
+        if self.gates("ExperimentalCriticalPodAnnotation"):
+            # static critical pods are never evicted: they are not re-admitted (eviction_manager.go:377-382)
+            cands = [p for p in cands if not (m.annotations_of(p).get(CRITICAL_ANNOTATION) == ""
+                                              and m.uid_of(p) in self.static)]
+        victim, t = self.eviction.choose(cands, obs, await self._pod_usage(sig))
         if victim is None:
             return None
         res = {"memory.available": "memory"}.get(t.signal, "ephemeral-storage")

@@ -16,6 +16,7 @@ import hashlib
 import json
 import logging
 import os
+import shutil
 import time
 
 import grpc
@@ -388,13 +389,18 @@ class RuntimeManager:
 
     # ------------------------------------------------------------ garbage collection
     async def garbage_collect(self, is_active, max_per_pod_container: int = 1, max_containers: int = -1,
-                              min_age: float = 0.0, now_ns: int | None = None) -> dict:
-        """kuberuntime_gc.go: dead containers older than min_age are evictable; per (pod,
-        container name) the newest max_per_pod_container stay (all go once the pod is gone);
-        then, with max_containers ≥ 0, the oldest are removed until the node is under it;
-        finally dead sandboxes without containers go, except each active pod's newest one.
-        Container log files are removed with their containers."""
+                              min_age: float = 0.0, now_ns: int | None = None, sources_ready: bool = True) -> dict:
+        """kuberuntime_gc.go GarbageCollect: dead containers older than min_age are evictable,
+        grouped in (pod, container name) units. Only when all pod sources are ready
+        (allSourcesReady, :212-219) does a pod unknown to the kubelet count as deleted, and then
+        all its units go; every other unit keeps its newest max_per_pod_container (<0: no limit).
+        With max_containers ≥ 0 the units are first cut to an equal share (min 1, :227-234) and
+        then the oldest go until the node is under it. Sandboxes (evictSandboxes, :256-311):
+        not ready and without containers; a deleted pod loses all of them, others keep their
+        newest. Container logs go with their containers; a deleted pod's directory (logs and
+        volumes) goes once nothing of it is left (evictPodLogsDirectories, sources ready only)."""
         now_ns = now_ns or time.time_ns()
+        deleted = (lambda uid: not is_active(uid)) if sources_ready else (lambda uid: False)   # noqa: E731
         sbs = await self.cri.list_pod_sandbox()
         conts = await self.cri.list_containers()
         sb_uid = {s.id: s.labels.get(L_POD_UID, "") for s in sbs}
@@ -407,15 +413,23 @@ class RuntimeManager:
             uid = sb_uid.get(c.pod_sandbox_id) or c.labels.get(L_POD_UID, "")
             groups.setdefault((uid, c.metadata.name), []).append(c)
         evict = []
-        for (uid, _name), lst in groups.items():
+        for key, lst in list(groups.items()):
             lst.sort(key=lambda c: c.created_at, reverse=True)
-            keep = max_per_pod_container if is_active(uid) else 0
-            evict += lst[keep:]
-            groups[(uid, _name)] = lst[:keep]
-        if max_containers >= 0:
+            if deleted(key[0]):
+                evict += lst
+                del groups[key]
+            elif max_per_pod_container >= 0:
+                evict += lst[max_per_pod_container:]
+                groups[key] = lst[:max_per_pod_container]
+        if max_containers >= 0 and groups and sum(map(len, groups.values())) > max_containers:
+            share = max(1, max_containers // len(groups))
+            for key, lst in groups.items():
+                evict += lst[share:]
+                groups[key] = lst[:share]
             rest = sorted((c for lst in groups.values() for c in lst), key=lambda c: c.created_at)
             evict += rest[:max(0, len(rest) - max_containers)]
         removed = 0
+        gone = set()
         for c in evict:
             try:
                 st, _ = await self.cri.container_status(c.id)
@@ -425,6 +439,7 @@ class RuntimeManager:
             try:
                 await self.cri.remove_container(c.id)
                 removed += 1
+                gone.add(c.id)
             except grpc.RpcError:
                 continue
             if log_path:
@@ -432,26 +447,40 @@ class RuntimeManager:
                     os.unlink(log_path)
                 except OSError:
                     pass
-        left = {c.pod_sandbox_id for c in conts if c not in evict}
-        newest: dict[str, object] = {}
+        left = {c.pod_sandbox_id for c in conts if c.id not in gone}
+        by_uid: dict[str, list] = {}
         for s in sbs:
-            uid = sb_uid[s.id]
-            if uid and (uid not in newest or s.created_at > newest[uid].created_at):
-                newest[uid] = s
+            by_uid.setdefault(sb_uid[s.id], []).append(s)
         sb_removed = 0
-        for s in sbs:
-            if s.state == C.SANDBOX_READY or s.id in left:
-                continue
-            uid = sb_uid[s.id]
-            if is_active(uid) and newest.get(uid) is s:
-                continue
+        remaining = {u for u in by_uid if u}
+        for uid, lst in by_uid.items():
+            lst.sort(key=lambda s: s.created_at, reverse=True)
+            candidates = lst if (uid and deleted(uid)) else lst[1:]
+            kept = len(lst) - len(candidates)
+            for s in candidates:
+                if s.state == C.SANDBOX_READY or s.id in left:
+                    kept += 1
+                    continue
+                try:
+                    await self.cri.remove_pod_sandbox(s.id)
+                    self.sandbox_ips.pop(s.id, None)
+                    sb_removed += 1
+                except grpc.RpcError:
+                    kept += 1
+            if not kept:
+                remaining.discard(uid)
+        dirs = 0
+        if sources_ready:
+            root = os.path.join(self.root, "pods")
             try:
-                await self.cri.remove_pod_sandbox(s.id)
-                self.sandbox_ips.pop(s.id, None)
-                sb_removed += 1
-            except grpc.RpcError:
-                pass
-        return {"containers": removed, "sandboxes": sb_removed}
+                names = os.listdir(root)
+            except OSError:
+                names = []
+            for uid in names:
+                if uid not in remaining and deleted(uid):
+                    shutil.rmtree(os.path.join(root, uid), ignore_errors=True)
+                    dirs += 1
+        return {"containers": removed, "sandboxes": sb_removed, "pod_dirs": dirs}
 
     async def remove_pod(self, uid: str, sandboxes=None):
         for s in sandboxes if sandboxes is not None else await self.cri.list_pod_sandbox(uid):

@@ -32,7 +32,7 @@ import uuid
 
 import grpc
 
-from ..grpcdesc.cri import API_VERSION, CRI as C
+from ..grpcdesc.cri import API_VERSION, CRI as C, EVENT_TRAILER
 from .hooks import DEFAULT_HOOKS_DIR, HookService
 from .images import NATIVE_BIN, ImageStore
 from .network import HostNetwork, NetworkError
@@ -157,6 +157,7 @@ class RocShim:
         self.started = 0
         self._adopt_tasks: set = set()
         self._event_streams: set[asyncio.Queue] = set()
+        self._last_ev: dict[str, int] = {}   # sandbox id -> created_at of the newest event emitted for it
         self.streaming = None
         self.streaming_port = 0     # loopback port of the exec/attach/port-forward server (0: any)
 
@@ -169,7 +170,8 @@ class RocShim:
             return
         sid = sid or c.sandbox_id
         sb = self.sandboxes.get(sid)
-        ts = now_ns()
+        ts = max(now_ns(), self._last_ev.get(sid, 0) + 1)   # strictly increasing per sandbox
+        self._last_ev[sid] = ts
         sst = sandbox_status_msg(sb, self.network.node_ip) if sb is not None else C.PodSandboxStatus(id=sid)
         ev = C.ContainerEventResponse(container_id=c.id if c is not None else sid, container_event_type=etype, created_at=ts,
                                       pod_sandbox_status=sst,
@@ -181,10 +183,25 @@ class RocShim:
     def _emit_removed(self, s: "Sandbox"):
         if not self._event_streams:
             return
-        ev = C.ContainerEventResponse(container_id=s.id, container_event_type=C.CONTAINER_DELETED_EVENT, created_at=now_ns(),
+        ts = max(now_ns(), self._last_ev.get(s.id, 0) + 1)
+        self._last_ev[s.id] = ts
+        ev = C.ContainerEventResponse(container_id=s.id, container_event_type=C.CONTAINER_DELETED_EVENT, created_at=ts,
                                       pod_sandbox_status=C.PodSandboxStatus(id=s.id, metadata=sandbox_meta(s)))
         for q in list(self._event_streams):
             q.put_nowait(ev)
+
+    def event_mark(self, sid: str | None) -> str:
+        """Trailer of a mutating CRI call: `<sandbox id>:<created_at>` of the newest event emitted
+        for the call's sandbox when the call returns (its state as of the return is the one that
+        event carries), or empty when no event exists to wait for (unknown target, no stream).
+        The kubelet matches its runtime cache to exactly that event (a container
+        event emitted before the sandbox's own STOPPED event must not count as the final state)."""
+        ts = self._last_ev.get(sid or "", 0)
+        if not sid or not ts:
+            return ""
+        if sid not in self.sandboxes:
+            self._last_ev.pop(sid, None)     # removed: nothing more will be emitted for it
+        return f"{sid}:{ts}"
 
     # ------------------------------------------------------------------ lifecycle
     async def start(self):
@@ -347,8 +364,7 @@ class RocShim:
             await self.remove_container(c.id)
         self.sandboxes.pop(sid, None)
         self._unckpt("sandboxes", sid)
-        if s.meta.get("uid"):
-            self._emit_removed(s)
+        self._emit_removed(s)
         shutil.rmtree(os.path.join(self.state_dir, "rootfs", sid), ignore_errors=True)
 
     # --------------------------------------------------------------- containers
@@ -669,18 +685,25 @@ class _Runtime:
         return C.StatusResponse(status=C.RuntimeStatus(conditions=conds),
                                 info={"isolation": self.r.isolation, "handlers": ",".join(sorted(HANDLERS))} if req.verbose else {})
 
+    def _mark(self, ctx, sid):
+        ctx.set_trailing_metadata(((EVENT_TRAILER, self.r.event_mark(sid)),))
+
     async def RunPodSandbox(self, req, ctx):
         try:
-            return C.RunPodSandboxResponse(pod_sandbox_id=await self.r.run_sandbox(req.config))
+            sid = await self.r.run_sandbox(req.config)
         except Exception as e:
             await _abort(ctx, e)
+        self._mark(ctx, sid)
+        return C.RunPodSandboxResponse(pod_sandbox_id=sid)
 
     async def StopPodSandbox(self, req, ctx):
         await self.r.stop_sandbox(req.pod_sandbox_id)
+        self._mark(ctx, req.pod_sandbox_id)
         return C.StopPodSandboxResponse()
 
     async def RemovePodSandbox(self, req, ctx):
         await self.r.remove_sandbox(req.pod_sandbox_id)
+        self._mark(ctx, req.pod_sandbox_id)
         return C.RemovePodSandboxResponse()
 
     def _sb_meta(self, s):
@@ -712,24 +735,35 @@ class _Runtime:
 
     async def CreateContainer(self, req, ctx):
         try:
-            return C.CreateContainerResponse(container_id=self.r.create_container(req.pod_sandbox_id, req.config,
-                                                                                  req.sandbox_config))
+            cid = self.r.create_container(req.pod_sandbox_id, req.config, req.sandbox_config)
         except Exception as e:
             await _abort(ctx, e)
+        self._mark(ctx, req.pod_sandbox_id)
+        return C.CreateContainerResponse(container_id=cid)
+
+    def _sid_of(self, cid):
+        c = self.r.containers.get(cid)
+        return c.sandbox_id if c is not None else None
 
     async def StartContainer(self, req, ctx):
+        sid = self._sid_of(req.container_id)
         try:
             await self.r.start_container(req.container_id)
         except Exception as e:
             await _abort(ctx, e)
+        self._mark(ctx, sid)
         return C.StartContainerResponse()
 
     async def StopContainer(self, req, ctx):
+        sid = self._sid_of(req.container_id)
         await self.r.stop_container(req.container_id, req.timeout)
+        self._mark(ctx, sid)
         return C.StopContainerResponse()
 
     async def RemoveContainer(self, req, ctx):
+        sid = self._sid_of(req.container_id)
         await self.r.remove_container(req.container_id)
+        self._mark(ctx, sid)
         return C.RemoveContainerResponse()
 
     def _c(self, c):

@@ -43,12 +43,38 @@ def _pod(uid, qos):
 
 def test_rank_and_admit():
     pods = [_pod("g", "Guaranteed"), _pod("b1", "Burstable"), _pod("b2", "Burstable"), _pod("e", "BestEffort")]
-    order = [p["metadata"]["uid"] for p in rank(pods, MEMORY, {"b1": GI, "b2": 3 * GI, "g": 5 * GI})]
-    assert order == ["e", "b2", "b1", "g"]          # QoS first, then usage above requests
+    usage = {"b1": GI, "b2": 3 * GI, "g": 5 * GI}
+    order = [p["metadata"]["uid"] for p in rank(pods, MEMORY, usage)]
+    # helpers.go rankMemoryPressure: no stats first, then pods above their request, then priority,
+    # then the larger usage above request (g: 4Gi over, b2: 2Gi over; b1 sits at its request)
+    assert order == ["e", "g", "b2", "b1"]
+    pods[2]["spec"]["priority"] = -10
+    assert [p["metadata"]["uid"] for p in rank(pods, MEMORY, usage)] == ["e", "b2", "g", "b1"]
+    assert [p["metadata"]["uid"] for p in rank(pods, MEMORY, usage, use_priority=False)] == ["e", "g", "b2", "b1"]
     em = EvictionManager(parse_thresholds("memory.available<1Gi"))
     assert em.admit(_pod("e", "BestEffort"), {"MemoryPressure"})[0] is False
     assert em.admit(_pod("b1", "Burstable"), {"MemoryPressure"})[0] is True
     assert em.admit(_pod("g", "Guaranteed"), {"DiskPressure"})[0] is False
+
+
+def test_min_reclaim_keeps_threshold_met_and_soft_grace_override():
+    """thresholdsMet(enforceMinReclaim): once met, memory.available<1Gi stays met until
+    available ≥ 1Gi + 500Mi; soft evictions use MaxPodGracePeriodSeconds, hard ones 0."""
+    ts = parse_thresholds("memory.available<1Gi", "nodefs.available<20%", "nodefs.available=0s", "memory.available=500Mi")
+    em = EvictionManager(ts, max_pod_grace=7)
+    assert em.met({MEMORY: (int(1.2 * GI), 64 * GI)}) == []
+    assert [t.signal for t in em.met({MEMORY: (int(0.9 * GI), 64 * GI)})] == [MEMORY]
+    assert [t.signal for t in em.met({MEMORY: (int(1.2 * GI), 64 * GI)})] == [MEMORY]   # not yet reclaimed
+    assert em.met({MEMORY: (int(1.6 * GI), 64 * GI)}) == []                            # ≥ 1Gi + 500Mi
+    assert em.met({MEMORY: (int(1.2 * GI), 64 * GI)}) == []                            # resolved: plain threshold again
+    pct = parse_thresholds("nodefs.available<10%", "", "", "nodefs.available=5%")[0]
+    assert pct.reclaim(100 * GI) == 5 * GI
+    hard = [t for t in ts if t.hard][0]
+    soft = [t for t in ts if not t.hard][0]
+    pod = _pod("b1", "Burstable")
+    pod["spec"]["terminationGracePeriodSeconds"] = 60
+    assert em.grace_for(pod, hard) == 0 and em.grace_for(pod, soft) == 7
+    assert EvictionManager(ts).grace_for(pod, soft) == 0
 
 
 async def test_memory_pressure_condition_admission_and_eviction():

@@ -318,3 +318,117 @@ def test_container_gc_keeps_newest_dead_container_per_pod_container():
 
     from tests.conftest import run
     run(go(), 60)
+
+
+def test_status_from_events_waits_for_the_calls_final_event():
+    """after StopPodSandbox the kubelet's runtime cache must come from the sandbox's
+    own STOPPED event (the call's trailer names it), not from the per-container events the
+    runtime emits first while the sandbox still shows READY; no-op calls need no event and an
+    event that never comes falls back to a re-list."""
+    import time
+    from amdkube.grpcdesc.cri import CRI as C
+    from amdkube.kubelet.cri_client import CURRENT_POD
+
+    async def go():
+        async with LocalCluster(gpus="none", relist_period=30, with_controllers=False) as lc:
+            k, c = lc.kubelet, lc.client
+            await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "ev"},
+                            "spec": {"restartPolicy": "Never", "containers": [
+                                {"name": n, "image": "busybox", "command": ["sleep", "60"]} for n in ("a", "b")]}}, "default")
+            pod = await wait_pod(c, "default", "ev", ("Running",), 20)
+            uid = m.uid_of(pod)
+            for _ in range(100):
+                if k._full_events and all(x.state == C.CONTAINER_RUNNING for x in lc.shim.containers.values()
+                                          if x.labels.get("io.kubernetes.pod.uid") == uid):
+                    break
+                await asyncio.sleep(0.02)
+            k.dispatch = lambda u: None          # keep the pod worker out of the way
+            await asyncio.sleep(0.2)
+            await k._cached_status(uid, fresh=True)
+            token = CURRENT_POD.set(uid)
+            try:
+                k.cri.take_touched(uid)
+                before = k.cri.pod_mutations(uid)
+                await k.runtime.kill_pod(uid, 0, pod, k._cached_sandboxes(uid))
+                assert k.cri.pod_mutations(uid) > before
+                touched = k.cri.take_touched(uid)
+            finally:
+                CURRENT_POD.reset(token)
+            assert len(touched) == 1 and all(ts > 0 for ts in touched.values()), touched
+            rt = await k._status_from_events(uid, touched)
+            assert rt is not None
+            assert [sb[1] for sb in rt.sandboxes] == [C.SANDBOX_NOTREADY], rt.sandboxes
+            assert all(x.state == C.CONTAINER_EXITED for lst in rt.containers.values() for x in lst)
+            # a no-op mutation (stop an exited container) is already covered by the cache
+            cid = next(x.id for x in lc.shim.containers.values() if x.labels.get("io.kubernetes.pod.uid") == uid)
+            token = CURRENT_POD.set(uid)
+            try:
+                await k.cri.stop_container(cid, 0)
+                noop = k.cri.take_touched(uid)
+            finally:
+                CURRENT_POD.reset(token)
+            t0 = time.perf_counter()
+            assert await k._status_from_events(uid, noop) is not None
+            assert time.perf_counter() - t0 < 0.1
+            # an event that never arrives: bounded wait, then None (the caller re-lists)
+            t0 = time.perf_counter()
+            assert await k._status_from_events(uid, {"f" * 32: time.time_ns() + 10**12}, timeout=0.05) is None
+            assert time.perf_counter() - t0 < 0.5
+
+    run(go(), 60)
+
+
+def test_gc_treats_unknown_pods_as_deleted_only_when_sources_ready(tmp_path):
+    """kuberuntime_gc.go:212-219, 299-309: with sources not ready an unknown pod keeps its
+    newest dead container and sandbox; once ready, everything of it goes (and its pod dir);
+    MaxContainers first cuts every unit to an equal share."""
+    from types import SimpleNamespace as NS
+    from amdkube.grpcdesc.cri import CRI as C
+    from amdkube.kubelet.kuberuntime import RuntimeManager
+
+    class FakeCRI:
+        def __init__(self):
+            self.sbs = [NS(id=f"s{i}", labels={"io.kubernetes.pod.uid": u}, state=C.SANDBOX_NOTREADY, created_at=i)
+                        for i, u in enumerate(("gone", "gone", "live"))]
+            self.conts = [NS(id=f"{u}-{n}-{i}", pod_sandbox_id=sid, labels={"io.kubernetes.pod.uid": u},
+                             metadata=NS(name=n), state=C.CONTAINER_EXITED, created_at=100 + i)
+                          for u, sid in (("gone", "s1"), ("live", "s2")) for n in ("x", "y") for i in range(3)]
+
+        async def list_pod_sandbox(self):
+            return list(self.sbs)
+
+        async def list_containers(self):
+            return list(self.conts)
+
+        async def container_status(self, cid):
+            return NS(log_path=""), {}
+
+        async def remove_container(self, cid):
+            self.conts = [c for c in self.conts if c.id != cid]
+
+        async def remove_pod_sandbox(self, sid):
+            self.sbs = [s for s in self.sbs if s.id != sid]
+
+    (tmp_path / "pods" / "gone" / "logs").mkdir(parents=True)
+    (tmp_path / "pods" / "live" / "logs").mkdir(parents=True)
+    active = {"live"}.__contains__
+
+    async def go():
+        cri = FakeCRI()
+        rm = RuntimeManager(cri, None, str(tmp_path))
+        out = await rm.garbage_collect(active, 1, -1, sources_ready=False)
+        assert sorted(c.id for c in cri.conts) == ["gone-x-2", "gone-y-2", "live-x-2", "live-y-2"]
+        assert [s.id for s in cri.sbs] == ["s1", "s2"] and out["pod_dirs"] == 0
+        assert (tmp_path / "pods" / "gone").exists()
+        out = await rm.garbage_collect(active, 1, -1, sources_ready=True)
+        assert sorted(c.id for c in cri.conts) == ["live-x-2", "live-y-2"]
+        assert [s.id for s in cri.sbs] == ["s2"] and out["pod_dirs"] == 1
+        assert not (tmp_path / "pods" / "gone").exists() and (tmp_path / "pods" / "live").exists()
+        cri2 = FakeCRI()
+        await rm.garbage_collect(lambda u: True, 3, 3, sources_ready=True)   # nothing on cri (rm bound to cri)
+        rm2 = RuntimeManager(cri2, None, str(tmp_path))
+        await rm2.garbage_collect(lambda u: True, -1, 3, sources_ready=True)
+        # 4 units × 3 → share max(1, 3 // 4) = 1 each, then the oldest go until 3 remain
+        assert sorted(c.id for c in cri2.conts) == ["gone-y-2", "live-x-2", "live-y-2"]
+
+    run(go(), 30)

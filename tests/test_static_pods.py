@@ -81,3 +81,38 @@ async def test_static_pod_mirror_lifecycle(tmp_path):
 
 async def _gone(c, name):
     return await c.get_or_none("pods", name, "kube-system") is None
+
+
+async def test_restarted_kubelet_adopts_running_static_pod(tmp_path):
+    """a static pod's creationTimestamp is re-stamped on every manifest read, so a
+    restarted kubelet must decide from runtime state (its startup ListPodSandbox), not from
+    timestamps, whether the runtime already holds the pod: the running sandbox is adopted,
+    never duplicated — even when the manifest is read long after the kubelet started."""
+    from amdkube.client import Client
+    from amdkube.kubelet.kubelet import Kubelet
+
+    mdir = tmp_path / "manifests"
+    mdir.mkdir()
+    write_manifest(str(mdir), "ctl", image="busybox", args=["-c", "sleep 60"])
+    async with LocalCluster(gpus="none", relist_period=0.2,
+                            kubelet_kw={"pod_manifest_path": str(mdir), "file_check_frequency": 0.2}) as lc:
+        async def one_running():
+            run = [x for x in lc.shim.containers.values() if x.state == 1]
+            return run if len(run) == 1 else None
+        first = await until(one_running)
+        sandboxes = set(lc.shim.sandboxes)
+        cfg = lc.kubelet.cfg
+        await lc.kubelet.stop()
+        await lc.kubelet.client.close()
+        k = Kubelet(Client(lc.api.url), cfg, smi_backend=lc.backend)
+        k.started_at -= 30.0          # the old timestamp heuristic would now call the static pod fresh
+        loop_fn = k._static_pods_loop
+
+        async def late_loop():   # the manifest is first read once the runtime's event stream is up
+            await asyncio.sleep(0.8)
+            await loop_fn()
+        k._static_pods_loop = late_loop
+        lc.kubelet = await k.start()
+        await asyncio.sleep(2.0)
+        assert set(lc.shim.sandboxes) == sandboxes
+        assert [x.id for x in lc.shim.containers.values() if x.state == 1] == [first[0].id]
