@@ -264,6 +264,8 @@ def validate_pod(pod: dict, old: dict | None = None) -> list[str]:
     from ..security.apparmor import validate_pod_annotations
     errs += validate_seccomp_annotations((pod.get("metadata") or {}).get("annotations"))
     errs += validate_pod_annotations(pod)
+    from ..kubelet.sysctl import validate_annotations as validate_sysctl_annotations
+    errs += validate_sysctl_annotations((pod.get("metadata") or {}).get("annotations"))
     if old is not None:
         if _strip_mutable(pod.get("spec") or {}) != _strip_mutable(old.get("spec") or {}):
             errs.append("spec: Forbidden: pod updates may not change fields other than `spec.containers[*].image`, "

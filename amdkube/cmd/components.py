@@ -217,6 +217,11 @@ def kubelet(argv):
     ap.add_argument("--file-check-frequency", type=float, default=20.0)
     ap.add_argument("--gpu-stats-backend", default="auto")
     ap.add_argument("--kube-api-qps", type=float, default=0)
+    ap.add_argument("--kube-reserved", default="", help="e.g. cpu=500m,memory=1Gi")
+    ap.add_argument("--system-reserved", default="", help="e.g. cpu=500m,memory=1Gi")
+    ap.add_argument("--enforce-node-allocatable", default="pods")
+    ap.add_argument("--cgroup-root", default="", help="cgroup v2 directory of the kubepods hierarchy")
+    ap.add_argument("--experimental-allowed-unsafe-sysctls", default="", help="comma-separated sysctls or patterns ending in *")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     klog.setup(a.v, "kubelet")
@@ -245,7 +250,10 @@ def kubelet(argv):
                         eviction_soft_grace_period=a.eviction_soft_grace_period,
                         eviction_minimum_reclaim=a.eviction_minimum_reclaim,
                         eviction_pressure_transition_period=a.eviction_pressure_transition_period,
-                        eviction_max_pod_grace_period=a.eviction_max_pod_grace_period)
+                        eviction_max_pod_grace_period=a.eviction_max_pod_grace_period,
+                        kube_reserved=a.kube_reserved, system_reserved=a.system_reserved,
+                        enforce_node_allocatable=a.enforce_node_allocatable, cgroup_root=a.cgroup_root,
+                        allowed_unsafe_sysctls=[x for x in a.experimental_allowed_unsafe_sysctls.split(",") if x])
 
     async def mk():
         smi = None

@@ -38,6 +38,7 @@ from ..deviceplugin.amd import TOPOLOGY_LABEL
 from ..grpcdesc.cri import CRI as C
 from ..utils.features import FeatureGate
 from ..utils.metrics import MICRO_BUCKETS, Counter, Gauge, Histogram, Summary, new_registry
+from .cm import enforce_pods_cgroup, node_allocatable as reserved_allocatable, parse_reserved
 from .cri_client import CURRENT_POD, CRIClient
 from .devicemanager import AdmissionError, ManagerImpl, ManagerStub
 from ..utils.trace import POD_TRACE
@@ -109,6 +110,11 @@ class KubeletConfig:
     maximum_dead_containers_per_container: int = 1    # --maximum-dead-containers-per-container
     maximum_dead_containers: int = -1                 # --maximum-dead-containers
     minimum_container_ttl_duration: float = 0.0       # --minimum-container-ttl-duration (s)
+    kube_reserved: str = ""                           # --kube-reserved cpu=…,memory=…,ephemeral-storage=…
+    system_reserved: str = ""                         # --system-reserved
+    enforce_node_allocatable: str = "pods"            # --enforce-node-allocatable (pods | none)
+    cgroup_root: str = ""                             # cgroup v2 dir holding kubepods (empty: no enforcement)
+    allowed_unsafe_sysctls: list = field(default_factory=list)   # --experimental-allowed-unsafe-sysctls
 
 
 class PodWorker:
@@ -167,6 +173,11 @@ class Kubelet:
                                         config.eviction_pressure_transition_period, config.eviction_max_pod_grace_period,
                                         use_priority=self.gates("PodPriority"))
         self.eviction_observer = lambda: observe(config.root_dir if os.path.isdir(config.root_dir) else "/")
+        from .sysctl import SAFE, SAFE_ANNOTATION, UNSAFE_ANNOTATION, Whitelist
+        self._sysctl_admit = (Whitelist(SAFE, SAFE_ANNOTATION), Whitelist(config.allowed_unsafe_sysctls, UNSAFE_ANNOTATION))
+        self._kube_reserved = parse_reserved(config.kube_reserved)
+        self._system_reserved = parse_reserved(config.system_reserved)
+        self._pods_cgroup_enforced = None
         self.pressure: set[str] = set()
         self.status = StatusManager(client, on_terminal=self._on_terminal)
         self.node: dict | None = None
@@ -192,6 +203,7 @@ class Kubelet:
         self.first_seen: dict[str, float] = {}
         self.started_at = time.time()
         self._runtime_uids: set[str] = set()
+        self._deadline_timers: set[str] = set()
         self._static_read = False
         self.last_sync_loop = time.time()
         self.sync_errors: dict[str, str] = {}
@@ -315,7 +327,7 @@ class Kubelet:
             removed = []
         for rname, dom in ext.items():
             cap[rname] = str(len(dom["resources"]))
-        alloc = dict(cap)
+        alloc = reserved_allocatable(cap, self._kube_reserved, self._system_reserved, self.eviction.thresholds)
         for rname, dom in ext.items():  # allocatable counts only healthy devices (fix #6 for node capacity)
             alloc[rname] = str(sum(1 for d in dom["resources"].values() if d.get("health") == "Healthy"))
         now = m.now_rfc3339()
@@ -341,6 +353,10 @@ class Kubelet:
                            "machineID": "", "systemUUID": "", "bootID": "", "kernelVersion": os.uname().release},
               "extendedResources": ext}
         st["_removed"] = removed
+        if self.cfg.cgroup_root and "pods" in self.cfg.enforce_node_allocatable.split(",") and \
+                self._pods_cgroup_enforced != (alloc.get("cpu"), alloc.get("memory")):
+            if enforce_pods_cgroup(self.cfg.cgroup_root, alloc):
+                self._pods_cgroup_enforced = (alloc.get("cpu"), alloc.get("memory"))
         return st
 
     async def update_node_status(self):
@@ -593,6 +609,10 @@ class Kubelet:
         ok, msg = self.eviction.admit(pod, self.pressure)   # eviction_manager.go Admit
         if not ok:
             return False, "Evicted", msg
+        for wl in self._sysctl_admit:       # kubelet.go:838-848 sysctl whitelists as admit handlers
+            ok, reason, msg = wl.admit(pod)
+            if not ok:
+                return False, reason, msg
         err = self.apparmor.validate(pod)   # lifecycle/handlers.go:142-165
         if err:
             return False, "AppArmor", f"Cannot enforce AppArmor: {err}"
@@ -658,8 +678,23 @@ class Kubelet:
             await self._finalize_delete(pod)
             return False
         sent_phase = (self.status.get(uid) or {}).get("phase") or (pod.get("status") or {}).get("phase")
-        if sent_phase in ("Succeeded", "Failed") and uid in self.status.terminal:
+        if sent_phase in ("Succeeded", "Failed"):
+            # terminal phases are final (status_manager.go: a terminal pod never goes back); a
+            # recomputation must not drop the reason of a kubelet-decided failure (deadline,
+            # eviction) that may not be written yet
             await self.runtime.kill_pod(uid, 0, pod, self._cached_sandboxes(uid))
+            return False
+        if sent_phase not in ("Succeeded", "Failed") and self._active_deadline_exceeded(pod):
+            # active_deadline.go: the pod sync handler fails the pod once it has been active on
+            # the node longer than spec.activeDeadlineSeconds (kubelet.go syncPod kills it)
+            msg = "Pod was active on the node longer than the specified deadline"
+            self.recorder.event(pod, "Normal", "DeadlineExceeded", msg)
+            grace = int((pod.get("spec") or {}).get("terminationGracePeriodSeconds", 30))
+            await self.runtime.kill_pod(uid, grace, pod, self._cached_sandboxes(uid))
+            rt = await self._cached_status(uid, fresh=True)
+            st = generate_status(pod, rt, self.cfg.node_ip, {}, [], m.now_rfc3339())
+            st.update({"phase": "Failed", "reason": "DeadlineExceeded", "message": msg})
+            self.status.set(pod, st)
             return False
         ctx = await self._pod_context(pod)
         POD_TRACE(uid, "sync_ctx")
@@ -687,6 +722,12 @@ class Kubelet:
         if st["phase"] in ("Succeeded", "Failed"):
             # release the sandbox (devices stay API-assigned)
             await self.runtime.kill_pod(uid, 0, pod, self._cached_sandboxes(uid))
+        ads = (pod.get("spec") or {}).get("activeDeadlineSeconds")
+        if ads is not None and st["phase"] not in ("Succeeded", "Failed") and uid not in self._deadline_timers:
+            start = m.parse_time(st.get("startTime"))
+            if start:
+                self._deadline_timers.add(uid)
+                asyncio.get_running_loop().call_later(max(0.0, start + float(ads) - time.time()) + 0.01, self.dispatch, uid)
         # container restarts waiting on back-off: re-sync when the back-off expires
         for c in (pod.get("spec") or {}).get("containers") or []:
             rem = self.runtime.backoff_remaining(uid, c["name"])
@@ -694,6 +735,13 @@ class Kubelet:
                 asyncio.get_running_loop().call_later(rem + 0.05, self.dispatch, uid)
                 break
         return False
+
+    def _active_deadline_exceeded(self, pod: dict) -> bool:
+        ads = (pod.get("spec") or {}).get("activeDeadlineSeconds")
+        if ads is None:
+            return False
+        start = m.parse_time((self.status.get(m.uid_of(pod)) or {}).get("startTime") or (pod.get("status") or {}).get("startTime"))
+        return bool(start) and time.time() - start >= float(ads)
 
     async def _already_running(self, uid: str) -> bool:
         try:
@@ -825,6 +873,7 @@ class Kubelet:
         self.first_seen.pop(uid, None)
         self.terminated_deleted.discard(uid)
         self.sync_errors.pop(uid, None)
+        self._deadline_timers.discard(uid)
         for k in [k for k in self._probe_state if k[0] == uid]:
             del self._probe_state[k]
 

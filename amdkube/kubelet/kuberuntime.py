@@ -23,6 +23,7 @@ import grpc
 
 from ..security.apparmor import profile_name as apparmor_profile_name
 from ..utils.trace import POD_TRACE
+from .sysctl import pod_sysctls
 from .qos import cgroup_parent
 from ..grpcdesc.cri import CRI as C
 from .cri_client import CRIClient
@@ -203,7 +204,8 @@ class RuntimeManager:
             hostname=spec.get("hostname") or md["name"], log_directory=log_dir, port_mappings=ports,
             labels={**(md.get("labels") or {}), L_POD_NAME: md["name"], L_POD_NS: md.get("namespace", ""), L_POD_UID: md["uid"]},
             annotations=ann, dns_config=self.dns.cri_config(pod) if self.dns is not None else None,
-            linux=C.LinuxPodSandboxConfig(cgroup_parent=cgroup_parent(pod), security_context=C.LinuxSandboxSecurityContext(
+            linux=C.LinuxPodSandboxConfig(cgroup_parent=cgroup_parent(pod), sysctls=pod_sysctls(pod),
+                                          security_context=C.LinuxSandboxSecurityContext(
                 namespace_options=C.NamespaceOption(host_network=bool(spec.get("hostNetwork")), host_pid=bool(spec.get("hostPID")),
                                                     host_ipc=bool(spec.get("hostIPC"))))))
 
