@@ -30,6 +30,10 @@ class ResourceInfo:
     verbs: tuple = ("create", "delete", "deletecollection", "get", "list", "patch", "update", "watch")
     defaulter: Callable | None = field(default=None, repr=False)
     validator: Callable | None = field(default=None, repr=False)
+    # served-only version: (group, plural) of the canonical resource whose storage it shares
+    # (extensions/v1beta1 deployments → apps deployments); None for a storage version
+    storage: tuple | None = None
+    to_storage: Callable | None = field(default=None, repr=False)     # request body → canonical (version defaults)
 
     @property
     def api_version(self) -> str:
@@ -48,13 +52,40 @@ class Scheme:
         self.by_kind: dict[tuple[str, str], ResourceInfo] = {}
         self.by_plural: dict[tuple[str, str], ResourceInfo] = {}
         self.by_name: dict[str, ResourceInfo] = {}
+        self.by_gvr: dict[tuple[str, str, str], ResourceInfo] = {}
 
     def add(self, ri: ResourceInfo):
         ri.list_kind = ri.list_kind or ri.kind + "List"
         self.by_kind[(ri.api_version, ri.kind)] = ri
-        self.by_plural[(ri.group, ri.plural)] = ri
+        self.by_gvr[(ri.group, ri.version, ri.plural)] = ri
+        if ri.storage is None or (ri.group, ri.plural) not in self.by_plural:
+            self.by_plural[(ri.group, ri.plural)] = ri
         for n in (ri.plural, ri.kind.lower(), *ri.short_names, ri.group_resource):
             self.by_name.setdefault(n, ri)
+
+    def add_alias(self, group: str, version: str, of: tuple, kind: str | None = None, to_storage=None) -> ResourceInfo:
+        """Serve an existing resource under another group/version (the apiserver's multi-version
+        serving: same storage, objects rewritten to the requested apiVersion on the way out)."""
+        canon = self.by_plural[of]
+        ri = ResourceInfo(group, version, kind or canon.kind, canon.plural, canon.namespaced, canon.short_names,
+                          canon.subresources, storage=of, to_storage=to_storage)
+        self.add(ri)
+        return ri
+
+    def storage_of(self, ri: ResourceInfo) -> ResourceInfo:
+        return self.by_plural[ri.storage] if ri.storage else ri
+
+    def served(self, group: str, version: str, plural: str) -> ResourceInfo | None:
+        return self.by_gvr.get((group, version, plural))
+
+    def storage_versions(self):
+        return [ri for ri in self.by_kind.values() if ri.storage is None]
+
+    def preferred_version(self, group: str) -> str | None:
+        vs = [ri.version for ri in self.by_kind.values() if ri.group == group and ri.storage is None]
+        if not vs:
+            vs = [ri.version for ri in self.by_kind.values() if ri.group == group]
+        return _version_sort(vs)[0] if vs else None
 
     def for_kind(self, api_version: str, kind: str) -> ResourceInfo | None:
         return self.by_kind.get((api_version, kind))
@@ -74,6 +105,18 @@ class Scheme:
         for ri in self.by_kind.values():
             out.setdefault(ri.api_version, []).append(ri)
         return out
+
+    def to_storage(self, obj: dict) -> dict:
+        """A body in a served-only version → its storage version (apiVersion and the version's
+        defaults); storage-version bodies are returned as they are."""
+        ri = self.for_object(obj)
+        if ri is None or ri.storage is None:
+            return obj
+        if ri.to_storage:
+            ri.to_storage(obj)
+        canon = self.by_plural[ri.storage]
+        obj["apiVersion"], obj["kind"] = canon.api_version, canon.kind
+        return obj
 
     def default(self, obj: dict) -> dict:
         ri = self.for_object(obj)
@@ -134,6 +177,13 @@ _ADMREG = [("MutatingWebhookConfiguration", "mutatingwebhookconfigurations", Fal
            ("ValidatingWebhookConfiguration", "validatingwebhookconfigurations", False, (), ())]
 _APIEXT = [("CustomResourceDefinition", "customresourcedefinitions", False, ("crd", "crds"), ("status",))]
 
+_EXTENSIONS = [("Ingress", "ingresses", True, ("ing",), ("status",)),
+               ("PodSecurityPolicy", "podsecuritypolicies", False, ("psp",), ())]
+_NETWORKING = [("NetworkPolicy", "networkpolicies", True, ("netpol",), ())]
+_SETTINGS = [("PodPreset", "podpresets", True, (), ())]
+_ADMREG_ALPHA = [("InitializerConfiguration", "initializerconfigurations", False, (), ())]
+_APIREG = [("APIService", "apiservices", False, (), ("status",))]
+
 for group, version, table in (("", "v1", _CORE), ("apps", "v1", _APPS), ("batch", "v1", _BATCH),
                               ("batch", "v1beta1", _BATCH_BETA), ("coordination.k8s.io", "v1", _COORD),
                               ("scheduling.k8s.io", "v1", _SCHED), ("autoscaling", "v1", _AUTOSCALING),
@@ -142,9 +192,68 @@ for group, version, table in (("", "v1", _CORE), ("apps", "v1", _APPS), ("batch"
                               ("storage.k8s.io", "v1beta1", _STORAGE_BETA),
                               ("authorization.k8s.io", "v1", _AUTHZ), ("authentication.k8s.io", "v1", _AUTHN),
                               ("apiextensions.k8s.io", "v1beta1", _APIEXT),
-                              ("admissionregistration.k8s.io", "v1beta1", _ADMREG)):
+                              ("admissionregistration.k8s.io", "v1beta1", _ADMREG),
+                              ("extensions", "v1beta1", _EXTENSIONS), ("networking.k8s.io", "v1", _NETWORKING),
+                              ("settings.k8s.io", "v1alpha1", _SETTINGS),
+                              ("admissionregistration.k8s.io", "v1alpha1", _ADMREG_ALPHA),
+                              ("apiregistration.k8s.io", "v1beta1", _APIREG)):
     for kind, plural, ns, short, subs in table:
         SCHEME.add(ResourceInfo(group, version, kind, plural, ns, short, subs))
+
+
+def _v1beta_selector_default(obj: dict):
+    """extensions/v1beta1, apps/v1beta1 defaulting: a missing spec.selector is the template's
+    labels (apps/v1 requires it, so it is filled before the object is converted)."""
+    spec = obj.setdefault("spec", {})
+    if not spec.get("selector"):
+        labels = ((spec.get("template") or {}).get("metadata") or {}).get("labels") or {}
+        if labels:
+            spec["selector"] = {"matchLabels": dict(labels)}
+
+
+# the reference release's other served versions (pkg/master/master.go DefaultAPIResourceConfigSource
+# + each group's install): same storage, rewritten apiVersion
+for _g, _v, _of, _conv in (
+        ("extensions", "v1beta1", ("apps", "deployments"), _v1beta_selector_default),
+        ("extensions", "v1beta1", ("apps", "daemonsets"), _v1beta_selector_default),
+        ("extensions", "v1beta1", ("apps", "replicasets"), _v1beta_selector_default),
+        ("extensions", "v1beta1", ("networking.k8s.io", "networkpolicies"), None),
+        ("apps", "v1beta1", ("apps", "deployments"), _v1beta_selector_default),
+        ("apps", "v1beta1", ("apps", "statefulsets"), _v1beta_selector_default),
+        ("apps", "v1beta1", ("apps", "controllerrevisions"), None),
+        ("apps", "v1beta2", ("apps", "deployments"), None), ("apps", "v1beta2", ("apps", "daemonsets"), None),
+        ("apps", "v1beta2", ("apps", "replicasets"), None), ("apps", "v1beta2", ("apps", "statefulsets"), None),
+        ("apps", "v1beta2", ("apps", "controllerrevisions"), None),
+        ("batch", "v2alpha1", ("batch", "cronjobs"), None),
+        ("autoscaling", "v2beta1", ("autoscaling", "horizontalpodautoscalers"), None),
+        ("rbac.authorization.k8s.io", "v1beta1", ("rbac.authorization.k8s.io", "roles"), None),
+        ("rbac.authorization.k8s.io", "v1beta1", ("rbac.authorization.k8s.io", "clusterroles"), None),
+        ("rbac.authorization.k8s.io", "v1beta1", ("rbac.authorization.k8s.io", "rolebindings"), None),
+        ("rbac.authorization.k8s.io", "v1beta1", ("rbac.authorization.k8s.io", "clusterrolebindings"), None),
+        ("rbac.authorization.k8s.io", "v1alpha1", ("rbac.authorization.k8s.io", "roles"), None),
+        ("rbac.authorization.k8s.io", "v1alpha1", ("rbac.authorization.k8s.io", "clusterroles"), None),
+        ("rbac.authorization.k8s.io", "v1alpha1", ("rbac.authorization.k8s.io", "rolebindings"), None),
+        ("rbac.authorization.k8s.io", "v1alpha1", ("rbac.authorization.k8s.io", "clusterrolebindings"), None),
+        ("storage.k8s.io", "v1beta1", ("storage.k8s.io", "storageclasses"), None),
+        ("scheduling.k8s.io", "v1alpha1", ("scheduling.k8s.io", "priorityclasses"), None),
+        ("authorization.k8s.io", "v1beta1", ("authorization.k8s.io", "subjectaccessreviews"), None),
+        ("authorization.k8s.io", "v1beta1", ("authorization.k8s.io", "selfsubjectaccessreviews"), None),
+        ("authorization.k8s.io", "v1beta1", ("authorization.k8s.io", "localsubjectaccessreviews"), None),
+        ("authentication.k8s.io", "v1beta1", ("authentication.k8s.io", "tokenreviews"), None)):
+    SCHEME.add_alias(_g, _v, _of, to_storage=_conv)
+
+
+def _version_sort(vs):
+    """Kubernetes version priority: GA > beta > alpha, then higher numbers first."""
+    import re as _re
+
+    def key(v):
+        mt = _re.match(r"^v(\d+)(?:(alpha|beta)(\d+))?$", v)
+        if not mt:
+            return (3, 0, 0, v)
+        major, stage, minor = int(mt.group(1)), mt.group(2), int(mt.group(3) or 0)
+        return ({None: 0, "beta": 1, "alpha": 2}[stage], -major, -minor, v)
+    return sorted(set(vs), key=key)
 
 
 def register_hooks(kind: str, api_version: str = "v1", defaulter=None, validator=None):

@@ -291,5 +291,6 @@ def _scheme_replace(ri: ResourceInfo, old: ResourceInfo | None):
 def _scheme_remove(ri: ResourceInfo):
     SCHEME.by_kind.pop((ri.api_version, ri.kind), None)
     SCHEME.by_plural.pop((ri.group, ri.plural), None)
+    SCHEME.by_gvr.pop((ri.group, ri.version, ri.plural), None)
     for k in [k for k, v in SCHEME.by_name.items() if v is ri]:
         del SCHEME.by_name[k]

@@ -232,6 +232,7 @@ class ResourceStore:
 
     def create(self, ns, obj, user=None, dry_run=False):
         ri = self.ri
+        SCHEME.to_storage(obj)   # a served-only version's body (extensions/v1beta1 …) → storage version
         md = obj.setdefault("metadata", {})
         obj["apiVersion"], obj["kind"] = ri.api_version, ri.kind
         if ri.namespaced:
@@ -333,7 +334,7 @@ class ResourceStore:
             if patch is not None:
                 new = apply_patch(cur, patch, content_type)
             else:
-                new = m.deepcopy(obj)
+                new = SCHEME.to_storage(m.deepcopy(obj))
             nmd = new.setdefault("metadata", {})
             if nmd.get("name", name) != name:
                 raise m.bad_request("the name of the object does not match the name on the URL")
@@ -436,7 +437,7 @@ class Registry:
         self.admission = admission
         self.services = services or ServiceAllocator()
         self.resources: dict[tuple[str, str], ResourceStore] = {}
-        for ri in SCHEME.by_kind.values():
+        for ri in SCHEME.storage_versions():
             if ri.plural == "bindings":
                 continue
             self.resources[(ri.group, ri.plural)] = ResourceStore(self, ri)

@@ -53,6 +53,24 @@ def _to_scale(obj: dict) -> dict:
             "status": {"replicas": int((obj.get("status") or {}).get("replicas", 0)), "selector": sel_str}}
 
 
+def _convert_out(obj, storage_ri, served):
+    """Storage-version object (or list) → the served version the client asked for."""
+    if isinstance(obj, dict):
+        if obj.get("apiVersion") == storage_ri.api_version and obj.get("kind") == storage_ri.kind:
+            obj["apiVersion"], obj["kind"] = served.api_version, served.kind
+        elif obj.get("kind") == storage_ri.list_kind:
+            obj["apiVersion"], obj["kind"] = served.api_version, served.list_kind
+            for it in obj.get("items") or []:
+                _convert_out(it, storage_ri, served)
+    return obj
+
+
+def _convert_frame(data: bytes, storage_ri, served) -> bytes:
+    ev = json.loads(data)
+    _convert_out(ev.get("object"), storage_ri, served)
+    return json.dumps(ev, separators=(",", ":")).encode() + b"\n"
+
+
 def _resp(obj, status=200) -> web.Response:
     body = obj if isinstance(obj, (bytes, bytearray)) else json.dumps(obj, separators=(",", ":")).encode()
     return web.Response(body=body, status=status, content_type=_JSON)
@@ -220,15 +238,17 @@ class APIServer:
         return _resp({"kind": "APIVersions", "versions": ["v1"],
                       "serverAddressByClientCIDRs": [{"clientCIDR": "0.0.0.0/0", "serverAddress": request.host}]})
 
+    @staticmethod
+    def _group_doc(g: str) -> dict:
+        from ..api.scheme import _version_sort
+        vs = _version_sort(ri.version for ri in SCHEME.by_kind.values() if ri.group == g)
+        pv = SCHEME.preferred_version(g)
+        return {"name": g, "versions": [{"groupVersion": f"{g}/{v}", "version": v} for v in vs],
+                "preferredVersion": {"groupVersion": f"{g}/{pv}", "version": pv}}
+
     async def api_groups(self, request):
-        groups = {}
-        for ri in SCHEME.by_kind.values():
-            if ri.group:
-                groups.setdefault(ri.group, set()).add(ri.version)
-        return _resp({"kind": "APIGroupList", "apiVersion": "v1", "groups": [
-            {"name": g, "versions": [{"groupVersion": f"{g}/{v}", "version": v} for v in sorted(vs)],
-             "preferredVersion": {"groupVersion": f"{g}/{sorted(vs)[0]}", "version": sorted(vs)[0]}}
-            for g, vs in sorted(groups.items())]})
+        groups = sorted({ri.group for ri in SCHEME.by_kind.values() if ri.group})
+        return _resp({"kind": "APIGroupList", "apiVersion": "v1", "groups": [self._group_doc(g) for g in groups]})
 
     def _resource_list(self, group, version):
         res = []
@@ -332,18 +352,17 @@ class APIServer:
             group, version, resource, ns, name, sub, watch = self._parse(request.path)
             if resource is None:
                 if version is None:  # /apis/<group>
-                    vs = sorted({ri.version for ri in SCHEME.by_kind.values() if ri.group == group})
-                    if not vs:
+                    if not any(ri.group == group for ri in SCHEME.by_kind.values()):
                         raise m.not_found("group", group)
                     code = 200
-                    return _resp({"kind": "APIGroup", "apiVersion": "v1", "name": group,
-                                  "versions": [{"groupVersion": f"{group}/{v}", "version": v} for v in vs],
-                                  "preferredVersion": {"groupVersion": f"{group}/{vs[0]}", "version": vs[0]}})
+                    return _resp({"kind": "APIGroup", "apiVersion": "v1", **self._group_doc(group)})
                 code = 200
                 return _resp(self._resource_list(group, version))
-            rs = self.registry.resources.get((group, resource))
-            if rs is None or rs.ri.version != version:
+            served = SCHEME.served(group, version, resource)
+            rs = self.registry.resources.get(served.storage or (served.group, served.plural)) if served is not None else None
+            if rs is None:
                 raise m.not_found("resource", f"{group}/{version}/{resource}")
+            conv = served if served.api_version != rs.ri.api_version else None
             q = request.query
             is_watch = watch or q.get("watch") in ("true", "1")
             kverb = {"GET": "watch" if is_watch else ("get" if name else "list"), "POST": "create", "PUT": "update",
@@ -359,7 +378,7 @@ class APIServer:
                 code = 200
                 if actx is not None:
                     self.auditor.stage(actx, "ResponseStarted", 200)
-                return await self._watch(request, rs, ns, name, q)
+                return await self._watch(request, rs, ns, name, q, conv)
             if name and top_sub in _STREAMING_SUBS:   # long-running: exempt from max-in-flight, like watches
                 if actx is not None:
                     self.auditor.stage(actx, "ResponseStarted", 101)
@@ -372,6 +391,8 @@ class APIServer:
                     raise m.too_many_requests()
                 await sem.acquire()
             resp = await self._handle(request, rs, ns, name, sub, user, q)
+            if conv is not None and resp.body:
+                resp = _resp(_convert_out(json.loads(resp.body), rs.ri, conv), resp.status)
             code = resp.status
             return resp
         except m.StatusError as e:
@@ -546,7 +567,7 @@ class APIServer:
             md["continue"] = nxt
         return _resp({"kind": ri.list_kind, "apiVersion": ri.api_version, "metadata": md, "items": items})
 
-    async def _watch(self, request, rs, ns, name, q):
+    async def _watch(self, request, rs, ns, name, q, conv=None):
         ri = rs.ri
         if not ri.namespaced:
             ns = ""
@@ -569,9 +590,12 @@ class APIServer:
         loop = asyncio.get_running_loop()
         deadline = loop.time() + timeout
         try:
+            frame = self._frame if conv is None else (lambda t: _convert_frame(self._frame(t), ri, conv))
             if initial:
                 buf = bytearray()
                 for o in initial:
+                    if conv is not None:
+                        o = _convert_out(o, ri, conv)
                     buf += b'{"type":"ADDED","object":' + json.dumps(o, separators=(",", ":")).encode() + b"}\n"
                 await resp.write(bytes(buf))
             while True:
@@ -586,13 +610,13 @@ class APIServer:
                             await resp.write(b'{"type":"ERROR","object":' + json.dumps(st).encode() + b"}\n")
                         break
                     continue
-                buf = bytearray(self._frame(ev))
+                buf = bytearray(frame(ev))
                 # drain whatever else is already queued into the same chunk (batching)
                 while not w.w.queue.empty():
                     nxt = w.w.queue.get_nowait()
                     if nxt is None:
                         break
-                    buf += self._frame(nxt)
+                    buf += frame(nxt)
                 await resp.write(bytes(buf))
         except (ConnectionResetError, asyncio.CancelledError):
             pass

@@ -398,7 +398,7 @@ async def cmd_version(c, a):
 
 async def cmd_api_resources(c, a):
     rows = [["NAME", "SHORTNAMES", "APIGROUP", "NAMESPACED", "KIND"]]
-    for ri in sorted(SCHEME.by_kind.values(), key=lambda r: (r.group, r.plural)):
+    for ri in sorted(SCHEME.storage_versions(), key=lambda r: (r.group, r.plural)):
         rows.append([ri.plural, ",".join(ri.short_names), ri.group, str(ri.namespaced).lower(), ri.kind])
     print(printers.table(rows))
 
