@@ -396,6 +396,17 @@ class Chain:
                 raise ValueError(f"unknown admission plugin {n!r}")
             self.plugins.append(REGISTRY[n](**config.get(n, {})))
 
+    def has(self, name: str) -> bool:
+        return any(p.name == name for p in self.plugins)
+
+    async def admit_async(self, a: Attributes, ctx):
+        """Plugins that call out (ImagePolicyWebhook): awaited by the apiserver before the
+        synchronous chain runs on the same object."""
+        for p in self.plugins:
+            fn = getattr(p, "admit_async", None)
+            if fn is not None and p.handles(a.operation):
+                await fn(a, ctx)
+
     def admit(self, a: Attributes, ctx):
         for p in self.plugins:
             if p.handles(a.operation):
@@ -405,3 +416,8 @@ class Chain:
         for p in self.plugins:
             if p.handles(a.operation):
                 p.validate(a, ctx)
+
+
+from . import admission_ext as _ext  # noqa: E402  (the reference's remaining plugins)
+
+REGISTRY.update({p.name: p for p in _ext.PLUGINS})

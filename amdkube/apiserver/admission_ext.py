@@ -1,0 +1,793 @@
+"""The reference release's remaining admission plugins (plugin/pkg/admission/* and
+staging/src/k8s.io/apiserver/pkg/admission/plugin/initialization), registered by their
+reference names (cmd/kube-apiserver/app/options/plugins.go):
+
+  AlwaysPullImages, LimitPodHardAntiAffinityTopology, EventRateLimit, DenyEscalatingExec,
+  DenyExecOnPrivileged, OwnerReferencesPermissionEnforcement, ImagePolicyWebhook,
+  InitialResources, PersistentVolumeLabel, PersistentVolumeClaimResize, PodPreset,
+  PodTolerationRestriction, PodSecurityPolicy, SecurityContextDeny, Initializers.
+
+Plugins that call out over the network (ImagePolicyWebhook) implement `admit_async`, which the
+apiserver awaits before the synchronous chain runs.
+"""
+from __future__ import annotations
+
+import copy
+import json
+import logging
+import time
+
+from ..api import meta as m
+from ..api.labels import selector_from_label_selector
+from ..api.quantity import Quantity
+from .admission import CONNECT, CREATE, DELETE, UPDATE, Plugin
+
+log = logging.getLogger("amdkube.admission")
+
+
+def _is_pod(a, sub=""):
+    return a.resource == "pods" and a.subresource == sub
+
+
+def _all_containers(pod):
+    spec = pod.get("spec") or {}
+    return list(spec.get("initContainers") or []) + list(spec.get("containers") or [])
+
+
+# ------------------------------------------------------------------ AlwaysPullImages
+class AlwaysPullImages(Plugin):
+    """alwayspullimages/admission.go: every (init) container pulls; validation rejects a pod
+    (create or update) that does not."""
+    name = "AlwaysPullImages"
+
+    def admit(self, a, ctx):
+        if _is_pod(a) and a.obj is not None:
+            for c in _all_containers(a.obj):
+                c["imagePullPolicy"] = "Always"
+
+    def validate(self, a, ctx):
+        if _is_pod(a) and a.obj is not None:
+            for c in _all_containers(a.obj):
+                if c.get("imagePullPolicy") != "Always":
+                    raise m.forbidden(f"spec.containers[{c.get('name')}].imagePullPolicy: Unsupported value: "
+                                      f"{c.get('imagePullPolicy')!r}: supported values: \"Always\"")
+
+
+# --------------------------------------------------- LimitPodHardAntiAffinityTopology
+class LimitPodHardAntiAffinityTopology(Plugin):
+    """antiaffinity/admission.go: required pod anti-affinity may only use the
+    kubernetes.io/hostname topology key."""
+    name = "LimitPodHardAntiAffinityTopology"
+
+    def validate(self, a, ctx):
+        if not _is_pod(a) or a.obj is None:
+            return
+        paa = (((a.obj.get("spec") or {}).get("affinity") or {}).get("podAntiAffinity") or {})
+        for t in paa.get("requiredDuringSchedulingIgnoredDuringExecution") or []:
+            if t.get("topologyKey") != "kubernetes.io/hostname":
+                raise m.forbidden(f"affinity.PodAntiAffinity.RequiredDuringScheduling has TopologyKey "
+                                  f"{t.get('topologyKey')} but only key kubernetes.io/hostname is allowed")
+
+
+# ------------------------------------------------------------------- EventRateLimit
+class _Bucket:
+    __slots__ = ("qps", "burst", "tokens", "t")
+
+    def __init__(self, qps, burst):
+        self.qps, self.burst, self.tokens, self.t = float(qps), int(burst), float(burst), time.monotonic()
+
+    def take(self) -> bool:
+        now = time.monotonic()
+        self.tokens = min(self.burst, self.tokens + (now - self.t) * self.qps)
+        self.t = now
+        if self.tokens >= 1.0:
+            self.tokens -= 1.0
+            return True
+        return False
+
+
+class EventRateLimit(Plugin):
+    """eventratelimit/admission.go + config.go: token buckets per limit type (Server,
+    Namespace, User, SourceAndObject), the last two in LRU caches of cacheSize; an event over
+    any limit is rejected with 429."""
+    name = "EventRateLimit"
+    operations = (CREATE,)
+
+    def __init__(self, limits=None):
+        self.limits = limits or [{"type": "Server", "qps": 5000, "burst": 20000}]
+        self.caches: list[tuple[dict, dict]] = [(lim, {}) for lim in self.limits]
+
+    @staticmethod
+    def _key(lim, a):
+        t = lim.get("type")
+        if t == "Server":
+            return ""
+        if t == "Namespace":
+            return a.namespace
+        if t == "User":
+            return (a.user or {}).get("name", "")
+        if t == "SourceAndObject":
+            ev = a.obj or {}
+            src, io = ev.get("source") or {}, ev.get("involvedObject") or {}
+            return "/".join(str(x) for x in (src.get("component"), src.get("host"), io.get("kind"), io.get("namespace"),
+                                             io.get("name"), io.get("uid"), io.get("apiVersion")))
+        raise ValueError(f"unknown EventRateLimit type {t!r}")
+
+    def validate(self, a, ctx):
+        if a.resource != "events":
+            return
+        for lim, cache in self.caches:
+            k = self._key(lim, a)
+            b = cache.pop(k, None) or _Bucket(lim.get("qps", 10), lim.get("burst", 100))
+            cache[k] = b                                   # most recently used last
+            size = int(lim.get("cacheSize", 4096))
+            while len(cache) > size:
+                cache.pop(next(iter(cache)))
+            if not b.take():
+                raise m.too_many_requests("limit reached on type %s for key %s" % (lim.get("type"), k))
+
+
+# ---------------------------------------------------------------- exec restrictions
+def _privileged(pod) -> bool:
+    return any(((c.get("securityContext") or {}).get("privileged")) for c in _all_containers(pod))
+
+
+class DenyEscalatingExec(Plugin):
+    """exec/admission.go: no exec/attach into a privileged pod or one that shares the host's
+    PID or IPC namespace."""
+    name = "DenyEscalatingExec"
+    operations = (CONNECT,)
+    host_checks = True
+
+    def validate(self, a, ctx):
+        if a.resource != "pods" or a.subresource not in ("exec", "attach"):
+            return
+        pod = a.old or ctx.get_object("pods", a.namespace, a.name) or {}
+        spec = pod.get("spec") or {}
+        if self.host_checks and spec.get("hostPID"):
+            raise m.forbidden("cannot exec into or attach to a container using host pid")
+        if self.host_checks and spec.get("hostIPC"):
+            raise m.forbidden("cannot exec into or attach to a container using host ipc")
+        if _privileged(pod):
+            raise m.forbidden("cannot exec into or attach to a privileged container")
+
+
+class DenyExecOnPrivileged(DenyEscalatingExec):
+    name = "DenyExecOnPrivileged"
+    host_checks = False
+
+
+# ------------------------------------------------- OwnerReferencesPermissionEnforcement
+class OwnerReferencesPermissionEnforcement(Plugin):
+    """gc/gc_admission.go: changing metadata.ownerReferences needs `delete` on the object;
+    setting blockOwnerDeletion on a reference needs `update` on the owner's finalizers."""
+    name = "OwnerReferencesPermissionEnforcement"
+
+    def validate(self, a, ctx):
+        if a.obj is None or a.subresource:
+            return
+        new = (a.obj.get("metadata") or {}).get("ownerReferences") or []
+        old = ((a.old or {}).get("metadata") or {}).get("ownerReferences") or []
+        if new == old:
+            return
+        if not ctx.authorize(a.user, "delete", _group_of(a.obj), a.resource, "", a.namespace, a.name):
+            raise m.forbidden(f"cannot set an ownerRef on a resource you can't delete: {a.resource}, {a.name}")
+        olds = {r.get("uid"): r for r in old}
+        for r in new:
+            if not r.get("blockOwnerDeletion"):
+                continue
+            prev = olds.get(r.get("uid"))
+            if prev is not None and prev.get("blockOwnerDeletion"):
+                continue
+            plural = ctx.plural_for_kind(r.get("apiVersion", ""), r.get("kind", ""))
+            if plural is None or not ctx.authorize(a.user, "update", r.get("apiVersion", "").rpartition("/")[0],
+                                                   plural, "finalizers", a.namespace, r.get("name", "")):
+                raise m.forbidden(f"cannot set blockOwnerDeletion if an ownerReference refers to a resource you can't "
+                                  f"set finalizers on: {r.get('kind')}, {r.get('name')}")
+
+
+def _group_of(obj):
+    av = obj.get("apiVersion", "")
+    return av.rpartition("/")[0] if "/" in av else ""
+
+
+# -------------------------------------------------------------------- ImagePolicyWebhook
+class ImagePolicyWebhook(Plugin):
+    """imagepolicy/admission.go: every pod create asks a backend (ImageReview,
+    imagepolicy.k8s.io/v1alpha1) whether its images may run; annotations matching
+    `*.image-policy.k8s.io/*` are forwarded; answers are cached (allowTTL / denyTTL); an
+    unreachable backend applies defaultAllow."""
+    name = "ImagePolicyWebhook"
+    operations = (CREATE, UPDATE)
+
+    def __init__(self, url="", allow_ttl=300, deny_ttl=30, default_allow=False, timeout=5.0, ca_file=None,
+                 insecure=False, client_cert=None, client_key=None):
+        self.url, self.allow_ttl, self.deny_ttl, self.default_allow = url, allow_ttl, deny_ttl, default_allow
+        self.timeout, self.ca_file, self.insecure = timeout, ca_file, insecure
+        self.client_cert, self.client_key = client_cert, client_key
+        self.cache: dict[str, tuple[float, bool, str]] = {}
+
+    def review_for(self, pod, ns):
+        ann = {k: v for k, v in m.annotations_of(pod).items() if ".image-policy.k8s.io/" in k}
+        return {"apiVersion": "imagepolicy.k8s.io/v1alpha1", "kind": "ImageReview",
+                "spec": {"containers": [{"image": c.get("image", "")} for c in _all_containers(pod)],
+                         "annotations": ann, "namespace": ns}}
+
+    async def admit_async(self, a, ctx):
+        if not _is_pod(a) or a.obj is None:
+            return
+        if a.operation == UPDATE and [c.get("image") for c in _all_containers(a.obj)] == \
+                [c.get("image") for c in _all_containers(a.old or {})]:
+            return
+        review = self.review_for(a.obj, a.namespace)
+        key = json.dumps(review["spec"], sort_keys=True)
+        hit = self.cache.get(key)
+        if hit is not None and hit[0] > time.monotonic():
+            allowed, reason = hit[1], hit[2]
+        else:
+            try:
+                allowed, reason = await self._ask(review)
+                self.cache[key] = (time.monotonic() + (self.allow_ttl if allowed else self.deny_ttl), allowed, reason)
+            except Exception as e:
+                log.warning("image policy webhook failed: %r (defaultAllow=%s)", e, self.default_allow)
+                if not self.default_allow:
+                    raise m.forbidden(f"image policy webhook backend denied one or more images: {e!r}")
+                a.obj.setdefault("metadata", {}).setdefault("annotations", {})[
+                    "alpha.image-policy.k8s.io/failed-open"] = "true"
+                return
+        if not allowed:
+            raise m.forbidden(f"image policy webhook backend denied one or more images: {reason}")
+
+    async def _ask(self, review):
+        import ssl
+        import aiohttp
+        sslctx = None
+        if self.url.startswith("https"):
+            sslctx = ssl.create_default_context(cafile=self.ca_file) if self.ca_file else ssl.create_default_context()
+            if self.insecure:
+                sslctx.check_hostname, sslctx.verify_mode = False, ssl.CERT_NONE
+            if self.client_cert:
+                sslctx.load_cert_chain(self.client_cert, self.client_key)
+        async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=self.timeout)) as s:
+            async with s.post(self.url, json=review, ssl=sslctx) as r:
+                if r.status >= 400:
+                    raise RuntimeError(f"HTTP {r.status}")
+                st = (await r.json()).get("status") or {}
+        return bool(st.get("allowed")), st.get("reason", "")
+
+
+# -------------------------------------------------------------------- InitialResources
+class InitialResources(Plugin):
+    """initialresources/admission.go (deprecated upstream): containers without cpu/memory
+    requests get the `percentile` of their image's historical usage (same image:tag, else
+    any tag of the image) when at least 60 samples exist, and the pod is annotated with what was
+    estimated. The data source is pluggable (`source.usage(resource, image, ns, exact) →
+    samples`); the reference's InfluxDB/GCM/Hawkular sources need services this build has no
+    access to, so a Prometheus source querying the kubelets' container metrics is provided."""
+    name = "InitialResources"
+    operations = (CREATE,)
+    SAMPLES_THRESHOLD = 60
+
+    def __init__(self, source=None, percentile=90, namespace_only=False):
+        self.source, self.percentile, self.ns_only = source, percentile, namespace_only
+
+    def admit(self, a, ctx):
+        if not _is_pod(a) or a.obj is None or self.source is None:
+            return
+        notes = []
+        for c in _all_containers(a.obj):
+            req = (c.setdefault("resources", {})).setdefault("requests", {})
+            lim = c["resources"].get("limits") or {}
+            for res in ("cpu", "memory"):
+                if res in req or res in lim:
+                    continue
+                v = self._estimate(res, c.get("image", ""), a.namespace if self.ns_only else "")
+                if v is not None:
+                    req[res] = f"{int(v)}m" if res == "cpu" else str(int(v))
+                    notes.append(f"{res} request for container {c.get('name')}")
+            if not req:
+                c["resources"].pop("requests")
+        if notes:
+            a.obj.setdefault("metadata", {}).setdefault("annotations", {})["kubernetes.io/initial-resources"] = \
+                "Initial Resources plugin set: " + "; ".join(notes)
+
+    def _estimate(self, res, image, ns):
+        for exact in (True, False):
+            samples = sorted(self.source.usage(res, image, ns, exact) or [])
+            if len(samples) >= self.SAMPLES_THRESHOLD:
+                i = min(len(samples) - 1, int(len(samples) * self.percentile / 100))
+                return samples[i]
+        return None
+
+
+class PrometheusUsageSource:
+    """Usage samples for InitialResources from a Prometheus server scraping the kubelets'
+    /metrics/cadvisor (container_cpu_usage_seconds_total rate in millicores, memory working set)."""
+
+    def __init__(self, url: str, window: str = "30d"):
+        self.url, self.window = url.rstrip("/"), window
+
+    def usage(self, res, image, ns, exact):
+        import urllib.parse
+        import urllib.request
+        sel = f'image="{image}"' if exact else f'image=~"{image.split(":")[0]}(:.*)?"'
+        if ns:
+            sel += f',namespace="{ns}"'
+        q = (f"rate(container_cpu_usage_seconds_total{{{sel}}}[5m]) * 1000" if res == "cpu"
+             else f"container_memory_working_set_bytes{{{sel}}}")
+        url = f"{self.url}/api/v1/query_range?" + urllib.parse.urlencode(
+            {"query": q, "start": time.time() - 86400 * 30, "end": time.time(), "step": "3600"})
+        with urllib.request.urlopen(url, timeout=5) as r:
+            data = json.loads(r.read())
+        return [float(v) for s in data.get("data", {}).get("result", []) for _t, v in s.get("values", [])]
+
+
+# -------------------------------------------------------------- PersistentVolumeLabel
+class PersistentVolumeLabel(Plugin):
+    """persistentvolume/label/admission.go: AWS EBS and GCE PD volumes get the zone/region
+    labels of their disk from the cloud provider (`cloud.volume_labels(pv)`)."""
+    name = "PersistentVolumeLabel"
+    operations = (CREATE,)
+
+    def __init__(self, cloud=None):
+        self.cloud = cloud
+
+    def admit(self, a, ctx):
+        if a.resource != "persistentvolumes" or a.subresource or a.obj is None:
+            return
+        spec = a.obj.get("spec") or {}
+        if "awsElasticBlockStore" not in spec and "gcePersistentDisk" not in spec:
+            return
+        cloud = self.cloud or getattr(ctx, "cloud", None)
+        if cloud is None or not hasattr(cloud, "volume_labels"):
+            raise m.forbidden("error querying volume labels: no cloud provider with volume support is configured")
+        labels = cloud.volume_labels(a.obj) or {}
+        if labels:
+            a.obj.setdefault("metadata", {}).setdefault("labels", {}).update(labels)
+
+
+# --------------------------------------------------------- PersistentVolumeClaimResize
+RESIZABLE = ("gcePersistentDisk", "awsElasticBlockStore", "cinder", "glusterfs", "rbd", "azureDisk", "azureFile",
+             "portworxVolume", "hostPath", "local")
+
+
+class PersistentVolumeClaimResize(Plugin):
+    """persistentvolume/resize/admission.go: growing a claim's storage request needs a bound
+    claim whose StorageClass sets allowVolumeExpansion and whose volume type can expand."""
+    name = "PersistentVolumeClaimResize"
+    operations = (UPDATE,)
+
+    def validate(self, a, ctx):
+        if a.resource != "persistentvolumeclaims" or a.subresource or a.obj is None or a.old is None:
+            return
+        def size(o):
+            s = (((o.get("spec") or {}).get("resources") or {}).get("requests") or {}).get("storage")
+            return Quantity(s).value() if s else 0
+        new, old = size(a.obj), size(a.old)
+        if new <= old:
+            return
+        if (a.old.get("status") or {}).get("phase") != "Bound":
+            raise m.forbidden("Only bound persistent volume claims can be expanded")
+        scn = (a.old.get("spec") or {}).get("storageClassName") or \
+            m.annotations_of(a.old).get("volume.beta.kubernetes.io/storage-class", "")
+        sc = ctx.get_object("storageclasses", "", scn) if scn else None
+        if not sc or not sc.get("allowVolumeExpansion"):
+            raise m.forbidden("only dynamically provisioned pvc can be resized and the storageclass that provisions the pvc must support resize")
+        pv = ctx.get_object("persistentvolumes", "", (a.old.get("spec") or {}).get("volumeName", "")) or {}
+        if not any(k in (pv.get("spec") or {}) for k in RESIZABLE):
+            raise m.forbidden("volume plugin does not support resize")
+
+
+# ------------------------------------------------------------------------- PodPreset
+PRESET_ANNOTATION_PREFIX = "podpreset.admission.kubernetes.io"
+
+
+class PodPreset(Plugin):
+    """podpreset/admission.go: presets whose selector matches a new pod inject env, envFrom,
+    volumeMounts into every container and volumes into the pod; any conflict (same env name or
+    volume name or mount path with a different definition) leaves the pod untouched; each
+    applied preset is recorded as podpreset.admission.kubernetes.io/podpreset-<name>=<rv>."""
+    name = "PodPreset"
+    operations = (CREATE,)
+
+    def admit(self, a, ctx):
+        if not _is_pod(a) or a.obj is None:
+            return
+        pod = a.obj
+        ann = m.annotations_of(pod)
+        if "kubernetes.io/config.mirror" in ann or ann.get(f"{PRESET_ANNOTATION_PREFIX}/exclude") == "true":
+            return
+        labels = (pod.get("metadata") or {}).get("labels") or {}
+        presets = [p for p in ctx.list_objects("podpresets", a.namespace, "settings.k8s.io")
+                   if selector_from_label_selector((p.get("spec") or {}).get("selector") or {}).matches(labels)]
+        if not presets:
+            return
+        try:
+            merged = self._merge(pod, presets)
+        except ValueError as e:
+            log.info("conflict applying pod presets to %s/%s: %s", a.namespace, m.name_of(pod), e)
+            return
+        pod["spec"] = merged
+        md = pod.setdefault("metadata", {})
+        md.setdefault("annotations", {}).update(
+            {f"{PRESET_ANNOTATION_PREFIX}/podpreset-{m.name_of(p)}": (p.get("metadata") or {}).get("resourceVersion", "")
+             for p in presets})
+
+    @staticmethod
+    def _merge(pod, presets):
+        spec = copy.deepcopy(pod.get("spec") or {})
+        vols = {v["name"]: v for v in spec.get("volumes") or []}
+        for p in presets:
+            for v in (p.get("spec") or {}).get("volumes") or []:
+                if v["name"] in vols and vols[v["name"]] != v:
+                    raise ValueError(f"merging volume {v['name']} for {m.name_of(p)} has a conflict")
+                vols.setdefault(v["name"], v)
+        spec["volumes"] = list(vols.values()) if vols else spec.get("volumes")
+        if spec.get("volumes") is None:
+            spec.pop("volumes", None)
+        for c in spec.get("containers") or []:
+            env = {e["name"]: e for e in c.get("env") or []}
+            mounts = {vm["mountPath"]: vm for vm in c.get("volumeMounts") or []}
+            env_from = list(c.get("envFrom") or [])
+            for p in presets:
+                ps = p.get("spec") or {}
+                for e in ps.get("env") or []:
+                    if e["name"] in env and env[e["name"]] != e:
+                        raise ValueError(f"merging env for {m.name_of(p)} has a conflict on {e['name']}")
+                    env.setdefault(e["name"], e)
+                for vm in ps.get("volumeMounts") or []:
+                    if vm["mountPath"] in mounts and mounts[vm["mountPath"]] != vm:
+                        raise ValueError(f"merging volume mounts for {m.name_of(p)} has a conflict on mount path {vm['mountPath']}")
+                    mounts.setdefault(vm["mountPath"], vm)
+                env_from += [x for x in ps.get("envFrom") or [] if x not in env_from]
+            if env:
+                c["env"] = list(env.values())
+            if mounts:
+                c["volumeMounts"] = list(mounts.values())
+            if env_from:
+                c["envFrom"] = env_from
+        return spec
+
+
+# ---------------------------------------------------------- PodTolerationRestriction
+NS_DEFAULT_TOLERATIONS = "scheduler.alpha.kubernetes.io/defaultTolerations"
+NS_WHITELIST_TOLERATIONS = "scheduler.alpha.kubernetes.io/tolerationsWhitelist"
+
+
+def _tol_map(ts):
+    return {t.get("key", ""): t for t in ts or []}
+
+
+def _tol_eq(x, y):
+    keys = ("key", "operator", "value", "effect", "tolerationSeconds")
+    norm = lambda t: tuple(t.get(k, "" if k != "tolerationSeconds" else None) or ("Equal" if k == "operator" and not t.get(k) else t.get(k, "")) for k in keys)  # noqa: E731
+    return norm(x) == norm(y)
+
+
+class PodTolerationRestriction(Plugin):
+    """podtolerationrestriction/admission.go: new pods get their namespace's default
+    tolerations (annotation, else the plugin's cluster default) merged in (conflicts rejected);
+    non-BestEffort pods tolerate memory pressure; every toleration must be on the namespace's
+    whitelist (annotation, else the cluster whitelist) when one is set."""
+    name = "PodTolerationRestriction"
+
+    def __init__(self, default=None, whitelist=None):
+        self.default, self.whitelist = default or [], whitelist or []
+
+    def _ns_list(self, ctx, ns, key):
+        obj = ctx.get_namespace(ns) or {}
+        v = m.annotations_of(obj).get(key)
+        if v is None:
+            return None
+        try:
+            return json.loads(v) if v.strip() else []
+        except ValueError as e:
+            raise m.forbidden(f"namespace {ns} annotation {key} is invalid: {e}")
+
+    def admit(self, a, ctx):
+        if not _is_pod(a) or a.obj is None:
+            return
+        spec = a.obj.setdefault("spec", {})
+        final = spec.get("tolerations") or []
+        if a.operation == CREATE:
+            ts = self._ns_list(ctx, a.namespace, NS_DEFAULT_TOLERATIONS)
+            ts = self.default if ts is None else ts
+            if ts:
+                mine = _tol_map(final)
+                if any(k in mine and not _tol_eq(v, mine[k]) for k, v in _tol_map(ts).items()):
+                    raise m.forbidden("namespace tolerations and pod tolerations conflict")
+                final = list(final) + [v for k, v in _tol_map(ts).items() if k not in mine]
+        from .registry import pod_qos
+        if pod_qos(a.obj) != "BestEffort" and "node.kubernetes.io/memory-pressure" not in _tol_map(final):
+            final = list(final) + [{"key": "node.kubernetes.io/memory-pressure", "operator": "Exists", "effect": "NoSchedule"}]
+        if final:
+            spec["tolerations"] = final
+
+    def validate(self, a, ctx):
+        if not _is_pod(a) or a.obj is None:
+            return
+        tols = (a.obj.get("spec") or {}).get("tolerations") or []
+        if not tols:
+            return
+        wl = self._ns_list(ctx, a.namespace, NS_WHITELIST_TOLERATIONS)
+        wl = self.whitelist if wl is None else wl
+        if wl:
+            w = _tol_map(wl)
+            if any(k not in w or not _tol_eq(v, w[k]) for k, v in _tol_map(tols).items()):
+                raise m.forbidden("pod tolerations (possibly merged with namespace default tolerations) conflict with its namespace whitelist")
+
+
+# ----------------------------------------------------------------- SecurityContextDeny
+class SecurityContextDeny(Plugin):
+    """securitycontext/scdeny/admission.go: pods may not set SELinux options, runAsUser,
+    supplementalGroups or fsGroup."""
+    name = "SecurityContextDeny"
+
+    def validate(self, a, ctx):
+        if not _is_pod(a) or a.obj is None:
+            return
+        psc = (a.obj.get("spec") or {}).get("securityContext") or {}
+        if psc.get("supplementalGroups") is not None:
+            raise m.forbidden("pod.Spec.SecurityContext.SupplementalGroups is forbidden")
+        if psc.get("seLinuxOptions") is not None:
+            raise m.forbidden("pod.Spec.SecurityContext.SELinuxOptions is forbidden")
+        if psc.get("runAsUser") is not None:
+            raise m.forbidden("pod.Spec.SecurityContext.RunAsUser is forbidden")
+        if psc.get("fsGroup") is not None:
+            raise m.forbidden("pod.Spec.SecurityContext.FSGroup is forbidden")
+        for c in _all_containers(a.obj):
+            sc = c.get("securityContext") or {}
+            if sc.get("seLinuxOptions") is not None:
+                raise m.forbidden("SecurityContext.SELinuxOptions is forbidden")
+            if sc.get("runAsUser") is not None:
+                raise m.forbidden("SecurityContext.RunAsUser is forbidden")
+
+
+# ------------------------------------------------------------------- PodSecurityPolicy
+PSP_ANNOTATION = "kubernetes.io/psp"
+
+
+class _PSPProvider:
+    """pkg/security/podsecuritypolicy/provider.go: default the pod's security context from the
+    policy (only where unset) and validate the result against it."""
+
+    def __init__(self, psp):
+        self.psp, self.spec, self.name = psp, psp.get("spec") or {}, m.name_of(psp)
+
+    def _first_id(self, strat):
+        rs = strat.get("ranges") or []
+        return rs[0].get("min") if strat.get("rule") == "MustRunAs" and rs else None
+
+    @staticmethod
+    def _in_ranges(v, ranges):
+        return any(r.get("min", 0) <= v <= r.get("max", 0) for r in ranges or [])
+
+    def default(self, pod):
+        spec = pod.setdefault("spec", {})
+        psc = spec.setdefault("securityContext", {})
+        fsg = self._first_id(self.spec.get("fsGroup") or {})
+        if fsg is not None and psc.get("fsGroup") is None:
+            psc["fsGroup"] = fsg
+        sg = self._first_id(self.spec.get("supplementalGroups") or {})
+        if sg is not None and not psc.get("supplementalGroups"):
+            psc["supplementalGroups"] = [sg]
+        se = self.spec.get("seLinux") or {}
+        if se.get("rule") == "MustRunAs" and se.get("seLinuxOptions") and psc.get("seLinuxOptions") is None:
+            psc["seLinuxOptions"] = dict(se["seLinuxOptions"])
+        if not psc:
+            spec.pop("securityContext")
+        uid = self._first_id(self.spec.get("runAsUser") or {})
+        for c in _all_containers(pod):
+            sc = c.setdefault("securityContext", {})
+            if uid is not None and sc.get("runAsUser") is None and (pod["spec"].get("securityContext") or {}).get("runAsUser") is None:
+                sc["runAsUser"] = uid
+            if (self.spec.get("runAsUser") or {}).get("rule") == "MustRunAsNonRoot" and sc.get("runAsNonRoot") is None \
+                    and sc.get("runAsUser") is None:
+                sc["runAsNonRoot"] = True
+            add = self.spec.get("defaultAddCapabilities") or []
+            drop = self.spec.get("requiredDropCapabilities") or []
+            if add or drop:
+                caps = sc.setdefault("capabilities", {})
+                cur_add, cur_drop = caps.get("add") or [], caps.get("drop") or []
+                caps["add"] = cur_add + [x for x in add if x not in cur_add and x not in cur_drop]
+                caps["drop"] = cur_drop + [x for x in drop if x not in cur_drop]
+                if not caps["add"]:
+                    caps.pop("add")
+                if not caps["drop"]:
+                    caps.pop("drop")
+            if self.spec.get("readOnlyRootFilesystem") and sc.get("readOnlyRootFilesystem") is None:
+                sc["readOnlyRootFilesystem"] = True
+            if sc.get("allowPrivilegeEscalation") is None and self.spec.get("defaultAllowPrivilegeEscalation") is not None:
+                sc["allowPrivilegeEscalation"] = bool(self.spec["defaultAllowPrivilegeEscalation"])
+            if not sc:
+                c.pop("securityContext")
+        return pod
+
+    def validate(self, pod) -> list[str]:
+        errs, s = [], self.spec
+        spec = pod.get("spec") or {}
+        psc = spec.get("securityContext") or {}
+        for k, name in (("hostNetwork", "hostNetwork"), ("hostPID", "hostPID"), ("hostIPC", "hostIPC")):
+            if spec.get(k) and not s.get(name):
+                errs.append(f"spec.securityContext.{k}: Invalid value: true: {k} is not allowed to be used")
+        for g in ("fsGroup", "supplementalGroups"):
+            strat = s.get(g) or {}
+            vals = psc.get(g)
+            vals = [vals] if isinstance(vals, int) else (vals or [])
+            if strat.get("rule") == "MustRunAs":
+                if not vals:
+                    errs.append(f"spec.securityContext.{g}: Invalid value: must be set")
+                for v in vals:
+                    if not self._in_ranges(v, strat.get("ranges")):
+                        errs.append(f"spec.securityContext.{g}: Invalid value: {v}: not in the policy's ranges")
+        se = s.get("seLinux") or {}
+        if se.get("rule") == "MustRunAs" and se.get("seLinuxOptions"):
+            for who in [psc] + [c.get("securityContext") or {} for c in _all_containers(pod)]:
+                if who.get("seLinuxOptions") not in (None, se["seLinuxOptions"]):
+                    errs.append("seLinuxOptions: Invalid value: does not match required seLinuxOptions")
+        allowed_vols = set(s.get("volumes") or [])
+        for v in spec.get("volumes") or []:
+            vt = next((k for k in v if k != "name"), "")
+            if "*" not in allowed_vols and vt not in allowed_vols:
+                errs.append(f"spec.volumes[{v.get('name')}]: Invalid value: {vt!r}: {vt} volumes are not allowed to be used")
+            if vt == "hostPath" and s.get("allowedHostPaths"):
+                p = (v.get("hostPath") or {}).get("path", "")
+                if not any(p.startswith(h.get("pathPrefix", "\0")) for h in s["allowedHostPaths"]):
+                    errs.append(f"spec.volumes[{v.get('name')}].hostPath.pathPrefix: Invalid value: {p!r}: is not allowed to be used")
+        ru = s.get("runAsUser") or {}
+        caps_allowed = set(s.get("allowedCapabilities") or []) | set(s.get("defaultAddCapabilities") or [])
+        for c in _all_containers(pod):
+            sc = c.get("securityContext") or {}
+            path = f"containers[{c.get('name')}].securityContext"
+            if sc.get("privileged") and not s.get("privileged"):
+                errs.append(f"{path}.privileged: Invalid value: true: Privileged containers are not allowed")
+            uid = sc.get("runAsUser", psc.get("runAsUser"))
+            if ru.get("rule") == "MustRunAs" and (uid is None or not self._in_ranges(uid, ru.get("ranges"))):
+                errs.append(f"{path}.runAsUser: Invalid value: {uid}: must be in the ranges: {ru.get('ranges')}")
+            if ru.get("rule") == "MustRunAsNonRoot":
+                nonroot = sc.get("runAsNonRoot", psc.get("runAsNonRoot"))
+                if uid == 0 or (uid is None and not nonroot):
+                    errs.append(f"{path}.runAsNonRoot: Invalid value: false: must be true")
+            caps = sc.get("capabilities") or {}
+            for cap in caps.get("add") or []:
+                if "*" not in caps_allowed and cap not in caps_allowed:
+                    errs.append(f"{path}.capabilities.add: Invalid value: {cap!r}: capability may not be added")
+            for cap in s.get("requiredDropCapabilities") or []:
+                if cap not in (caps.get("drop") or []):
+                    errs.append(f"{path}.capabilities.drop: Invalid value: {caps.get('drop')}: {cap} is required to be dropped but was not found")
+            if s.get("readOnlyRootFilesystem") and not sc.get("readOnlyRootFilesystem"):
+                errs.append(f"{path}.readOnlyRootFilesystem: Invalid value: false: ReadOnlyRootFilesystem must be set to true")
+            if s.get("allowPrivilegeEscalation") is False and sc.get("allowPrivilegeEscalation") is not False:
+                errs.append(f"{path}.allowPrivilegeEscalation: Invalid value: Allowing privilege escalation for containers is not allowed")
+            for p in c.get("ports") or []:
+                hp = p.get("hostPort") or 0
+                if hp and not any(r.get("min", 0) <= hp <= r.get("max", 0) for r in s.get("hostPorts") or []):
+                    errs.append(f"{path}.ports: Invalid value: {hp}: Host port {hp} is not allowed to be used")
+        return errs
+
+
+class PodSecurityPolicy(Plugin):
+    """security/podsecuritypolicy/admission.go: the policies the requesting user or the pod's
+    service account may `use` (extensions podsecuritypolicies, in the pod's namespace), sorted
+    by name; on create the first policy under which the (defaulted) pod validates is applied
+    and recorded as kubernetes.io/psp; on update the pod must validate unchanged; no usable
+    policy → 403 listing every policy's errors."""
+    name = "PodSecurityPolicy"
+
+    def __init__(self, fail_on_no_policies=True):
+        self.fail_on_no_policies = fail_on_no_policies
+
+    def _providers(self, a, ctx, pod):
+        policies = sorted(ctx.list_objects("podsecuritypolicies", "", "extensions"), key=m.name_of)
+        sa = (pod.get("spec") or {}).get("serviceAccountName")
+        sa_user = {"name": f"system:serviceaccount:{a.namespace}:{sa}",
+                   "groups": ["system:serviceaccounts", f"system:serviceaccounts:{a.namespace}"]} if sa else None
+        usable = [p for p in policies
+                  if (sa_user is not None and ctx.authorize(sa_user, "use", "extensions", "podsecuritypolicies", "", a.namespace, m.name_of(p)))
+                  or ctx.authorize(a.user or {}, "use", "extensions", "podsecuritypolicies", "", a.namespace, m.name_of(p))]
+        return policies, [_PSPProvider(p) for p in usable]
+
+    def admit(self, a, ctx):
+        if not _is_pod(a) or a.obj is None or a.operation != CREATE:
+            return
+        policies, providers = self._providers(a, ctx, a.obj)
+        if not policies and not self.fail_on_no_policies:
+            return
+        if not providers:
+            raise m.forbidden("unable to validate against any pod security policy: no providers available to validate pod request")
+        errors, first_mutated = {}, None
+        for pr in providers:    # computeSecurityContext: default, validate, prefer a non-mutating policy
+            cand = pr.default(copy.deepcopy(a.obj))
+            errs = pr.validate(cand)
+            if errs:
+                errors[pr.name] = errs
+                continue
+            if cand == a.obj:
+                first_mutated = (pr.name, cand)
+                break
+            if first_mutated is None:
+                first_mutated = (pr.name, cand)
+        if first_mutated is None:
+            raise m.forbidden(f"unable to validate against any pod security policy: {errors}")
+        name, cand = first_mutated
+        a.obj.clear()
+        a.obj.update(cand)
+        a.obj.setdefault("metadata", {}).setdefault("annotations", {})[PSP_ANNOTATION] = name
+
+    def validate(self, a, ctx):
+        if not _is_pod(a) or a.obj is None:
+            return
+        if a.operation == UPDATE and a.old is not None:
+            strip = lambda o: {k: v for k, v in o.items() if k != "metadata"}   # noqa: E731
+            if strip(a.obj) == strip(a.old):
+                return      # only metadata (GC fields, labels) changed
+        policies, providers = self._providers(a, ctx, a.obj)
+        if not policies and not self.fail_on_no_policies:
+            return
+        errors = {}
+        for pr in providers:
+            errs = pr.validate(a.obj)
+            if not errs:
+                return
+            errors[pr.name] = errs
+        raise m.forbidden(f"unable to validate against any pod security policy: {errors}")
+
+
+# ---------------------------------------------------------------------- Initializers
+class Initializers(Plugin):
+    """apiserver/pkg/admission/plugin/initialization: a new object whose resource matches an
+    InitializerConfiguration rule gets metadata.initializers.pending (every matching
+    initializer, in configuration order); it stays uninitialized — hidden from LIST/WATCH
+    without includeUninitialized — until initializers remove themselves. Clients that are not
+    allowed to `initialize` the resource may not set or change initializers."""
+    name = "Initializers"
+    operations = (CREATE, UPDATE)
+
+    def admit(self, a, ctx):
+        if a.obj is None or a.subresource or a.resource in ("initializerconfigurations",):
+            return
+        md = a.obj.setdefault("metadata", {})
+        if a.operation == CREATE:
+            if md.get("initializers") is not None:
+                if not ctx.authorize(a.user or {}, "initialize", _group_of(a.obj), a.resource, "", a.namespace, a.name):
+                    raise m.forbidden("must have the 'initialize' verb to set initializers on create")
+                return
+            names = []
+            for ic in ctx.list_objects("initializerconfigurations", "", "admissionregistration.k8s.io"):
+                for ini in ic.get("initializers") or []:
+                    if any(_rule_matches(r, a) for r in ini.get("rules") or []) and ini["name"] not in names:
+                        names.append(ini["name"])
+            if names:
+                md["initializers"] = {"pending": [{"name": n} for n in names]}
+        else:
+            old = ((a.old or {}).get("metadata") or {}).get("initializers")
+            if md.get("initializers") != old:
+                if old is None:
+                    raise m.forbidden("field is immutable once initialization has completed")
+                if not ctx.authorize(a.user or {}, "initialize", _group_of(a.obj), a.resource, "", a.namespace, a.name):
+                    raise m.forbidden("must have the 'initialize' verb to modify initializers")
+            if md.get("initializers") is not None and not (md["initializers"].get("pending")) \
+                    and md["initializers"].get("result") is None:
+                md.pop("initializers")
+
+
+def _rule_matches(rule, a) -> bool:
+    group = a.group if hasattr(a, "group") else ""
+    def has(lst, v):
+        return "*" in lst or v in lst
+    groups = rule.get("apiGroups") or []
+    gv = (a.obj or {}).get("apiVersion", "")
+    g, _, v = gv.rpartition("/") if "/" in gv else ("", "", gv)
+    return has(groups, g if not group else group) and has(rule.get("apiVersions") or [], v) and \
+        has(rule.get("resources") or [], a.resource)
+
+
+def is_uninitialized(obj) -> bool:
+    ini = ((obj or {}).get("metadata") or {}).get("initializers")
+    return bool(ini) and bool(ini.get("pending"))
+
+
+PLUGINS = (AlwaysPullImages, LimitPodHardAntiAffinityTopology, EventRateLimit, DenyEscalatingExec, DenyExecOnPrivileged,
+           OwnerReferencesPermissionEnforcement, ImagePolicyWebhook, InitialResources, PersistentVolumeLabel,
+           PersistentVolumeClaimResize, PodPreset, PodTolerationRestriction, PodSecurityPolicy, SecurityContextDeny,
+           Initializers)

@@ -467,6 +467,20 @@ class Registry:
                 return r.list(ns)[0]
         return []
 
+    authorizer = None   # set by the APIServer (admission plugins that check permissions)
+    cloud = None        # cloud provider (PersistentVolumeLabel)
+
+    def authorize(self, user, verb, group, resource, sub="", ns="", name="") -> bool:
+        if self.authorizer is None:
+            return True
+        from .auth import Attributes as AuthzAttributes
+        ok, _ = self.authorizer.authorize(AuthzAttributes(user or {}, verb, group, resource, sub, ns, name))
+        return ok
+
+    def plural_for_kind(self, api_version, kind):
+        ri = SCHEME.for_kind(api_version, kind)
+        return ri.plural if ri is not None else None
+
     def get_object(self, plural, ns, name):
         for (g, p), r in self.resources.items():
             if p == plural:

@@ -53,6 +53,14 @@ def _to_scale(obj: dict) -> dict:
             "status": {"replicas": int((obj.get("status") or {}).get("replicas", 0)), "selector": sel_str}}
 
 
+_USER_KEY = web.RequestKey("amdkube_user", dict) if hasattr(web, "RequestKey") else "amdkube_user"
+
+
+def _uninitialized(obj) -> bool:
+    ini = ((obj or {}).get("metadata") or {}).get("initializers")
+    return bool(ini) and bool(ini.get("pending"))
+
+
 def _convert_out(obj, storage_ri, served):
     """Storage-version object (or list) → the served version the client asked for."""
     if isinstance(obj, dict):
@@ -112,6 +120,7 @@ class APIServer:
         self.authn = Authenticator(self.registry, self.tokens, service_account_key, anonymous_auth)
         self.authn.user_tokens = len(token_auth or {})
         self.authz = UnionAuthorizer(authorization_mode, self.registry)
+        self.registry.authorizer = self.authz
         self._ro = asyncio.Semaphore(max_in_flight) if max_in_flight else None
         self._rw = asyncio.Semaphore(max_mutating_in_flight) if max_mutating_in_flight else None
         self.event_ttl = event_ttl
@@ -380,6 +389,7 @@ class APIServer:
                     self.auditor.stage(actx, "ResponseStarted", 200)
                 return await self._watch(request, rs, ns, name, q, conv)
             if name and top_sub in _STREAMING_SUBS:   # long-running: exempt from max-in-flight, like watches
+                request[_USER_KEY] = user
                 if actx is not None:
                     self.auditor.stage(actx, "ResponseStarted", 101)
                 resp = await self._stream(request, rs, ns, name, sub, q)
@@ -467,6 +477,8 @@ class APIServer:
             if name:
                 raise m.method_not_allowed("POST on a named resource")
             dry = q.get("dryRun") == "All"
+            await self.admission.admit_async(adm.Attributes(adm.CREATE, ri.plural, sub, ns, m.name_of(body), body, None, user,
+                                                            ri.kind), self.registry)
             mut, val = self.webhooks.active("CREATE", ri, sub, ns)
             if mut:
                 body = await self.webhooks.mutate(mut, "CREATE", ri, sub, ns, None, body, None, user)
@@ -474,6 +486,8 @@ class APIServer:
                 final = rs.create(ns, json.loads(json.dumps(body)), user, dry_run=True)
                 await self.webhooks.validate(val, "CREATE", ri, sub, ns, None, final, None, user)
             obj = rs.create(ns, body, user, dry_run=dry)
+            if not dry and q.get("includeUninitialized") not in ("true", "1") and _uninitialized(obj):
+                obj = await self._wait_initialized(rs, ns, m.name_of(obj))
             return _resp(obj, 201)
         if meth == "PUT":
             if not name:
@@ -484,6 +498,9 @@ class APIServer:
             subr = "status" if sub in ("status", "approval") else ""
             if sub == "finalize" and ri.plural == "namespaces":
                 subr = "finalize"
+            if not sub and self.admission.has("ImagePolicyWebhook"):
+                await self.admission.admit_async(adm.Attributes(adm.UPDATE, ri.plural, sub, ns, name, body, rs.get(ns, name),
+                                                                user, ri.kind), self.registry)
             mut, val = self.webhooks.active("UPDATE", ri, sub, ns)
             if mut or val:
                 old = rs.get(ns, name)
@@ -551,11 +568,37 @@ class APIServer:
             return _resp({"kind": ri.list_kind, "apiVersion": ri.api_version, "metadata": {}, "items": items})
         raise m.method_not_allowed(meth)
 
+    def _hide_uninitialized(self, q) -> bool:
+        return self.admission.has("Initializers") and q.get("includeUninitialized") not in ("true", "1")
+
+    async def _wait_initialized(self, rs, ns, name, timeout=30.0):
+        """initialization: a create returns once every initializer has run (pending empty);
+        a failed initialization (result set) deleted the object; past the timeout: 504."""
+        loop = asyncio.get_running_loop()
+        end = loop.time() + timeout
+        while loop.time() < end:
+            cur = rs.storage.get(rs.key(ns, name), ignore_not_found=True)
+            if cur is None:
+                raise m.StatusError(500, "InternalError", f"object {name} was deleted during initialization")
+            ini = (cur.get("metadata") or {}).get("initializers") or {}
+            if ini.get("result"):
+                st = ini["result"]
+                raise m.StatusError(int(st.get("code") or 500), st.get("reason") or "InternalError", st.get("message", ""))
+            if not _uninitialized(cur):
+                return cur
+            await asyncio.sleep(0.05)
+        raise m.StatusError(504, "Timeout", f"timed out waiting for the initialization of {name}")
+
     def _list(self, rs, ns, q):
         ri = rs.ri
         limit = int(q.get("limit", "0") or 0)
         cont = q.get("continue") or None
         ls, fs = q.get("labelSelector"), q.get("fieldSelector")
+        if self._hide_uninitialized(q):
+            items, rev, nxt = rs.list(ns, ls, fs, limit, cont)
+            md = {"resourceVersion": str(rev), **({"continue": nxt} if nxt else {})}
+            return _resp({"kind": ri.list_kind, "apiVersion": ri.api_version, "metadata": md,
+                          "items": [o for o in items if not _uninitialized(o)]})
         if not ls and not fs and not limit and not cont:
             raws, rev = rs.storage.list_raw(rs.prefix(ns))
             body = (b'{"kind":"' + ri.list_kind.encode() + b'","apiVersion":"' + ri.api_version.encode() +
@@ -591,6 +634,12 @@ class APIServer:
         deadline = loop.time() + timeout
         try:
             frame = self._frame if conv is None else (lambda t: _convert_frame(self._frame(t), ri, conv))
+            if self._hide_uninitialized(q):
+                initial = [o for o in initial if not _uninitialized(o)]
+                inner = frame
+
+                def frame(t):   # uninitialized objects are invisible; they appear once initialized
+                    return b"" if t[1] is not None and _uninitialized(t[1]) else inner(t)
             if initial:
                 buf = bytearray()
                 for o in initial:
@@ -660,6 +709,10 @@ class APIServer:
         if plural != "pods":
             raise m.not_found("subresource", sub)
         pod = rs.get(ns, name)
+        user = request.get(_USER_KEY)
+        attrs = adm.Attributes(adm.CONNECT, "pods", top, ns, name, None, pod, user, "Pod")
+        self.admission.admit(attrs, self.registry)      # DenyEscalatingExec / DenyExecOnPrivileged
+        self.admission.validate(attrs, self.registry)
         node_name = (pod.get("spec") or {}).get("nodeName")
         if not node_name:
             raise m.bad_request(f'pod "{name}" is not scheduled yet')
