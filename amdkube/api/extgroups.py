@@ -279,10 +279,13 @@ def validate_initializer_configuration(ic, old=None):
 
 # --------------------------------------------------------------------- APIService
 def validate_apiservice(a, old=None):
-    errs = _meta(a, False)
+    """Names are path segments (core group: `v1.`), not DNS subdomains."""
+    from .validation import validate_object_meta
+    errs = validate_object_meta(a, False, name_fn=lambda n: [] if n not in (".", "..") and "/" not in n and "%" not in n
+                                else ["may not contain '/' or '%' or be '.' or '..'"])
     spec = a.get("spec") or {}
     name, group, version = (a.get("metadata") or {}).get("name", ""), spec.get("group", ""), spec.get("version", "")
-    want = f"{version}.{group}" if group else version
+    want = f"{version}.{group}"
     if name != want:
         errs.append(f"metadata.name: Invalid value: {name!r}: must be `spec.version+\".\"+spec.group`: {want!r}")
     if not version:

@@ -121,6 +121,8 @@ class APIServer:
         self.authn.user_tokens = len(token_auth or {})
         self.authz = UnionAuthorizer(authorization_mode, self.registry)
         self.registry.authorizer = self.authz
+        from .aggregator import Aggregator
+        self.aggregator = Aggregator(self)
         self._ro = asyncio.Semaphore(max_in_flight) if max_in_flight else None
         self._rw = asyncio.Semaphore(max_mutating_in_flight) if max_mutating_in_flight else None
         self.event_ttl = event_ttl
@@ -153,6 +155,7 @@ class APIServer:
                 self.registry.create_namespace(ns)
         if "RBAC" in self.authz.modes:
             ensure_bootstrap_policy(self.registry)
+        self.aggregator.autoregister()
 
     # ---------------------------------------------------------------- lifecycle
     async def start(self, host="127.0.0.1", port=0):
@@ -172,6 +175,7 @@ class APIServer:
         self.port = self._site._server.sockets[0].getsockname()[1]
         self.host = host
         self._bg.append(asyncio.create_task(self._event_gc()))
+        self._bg.append(asyncio.create_task(self.aggregator.run_availability(), name="apiservice-availability"))
         self.crds.start()
         self._bg.append(self.crds._task)
         self._reconcile_master_service()
@@ -209,6 +213,7 @@ class APIServer:
         return f"{'https' if self.tls else 'http'}://{self.host}:{self.port}"
 
     async def stop(self):
+        await self.aggregator.close()
         for t in self._bg:
             t.cancel()
         await self.webhooks.close()
@@ -257,7 +262,8 @@ class APIServer:
 
     async def api_groups(self, request):
         groups = sorted({ri.group for ri in SCHEME.by_kind.values() if ri.group})
-        return _resp({"kind": "APIGroupList", "apiVersion": "v1", "groups": [self._group_doc(g) for g in groups]})
+        docs = [self._group_doc(g) for g in groups] + self.aggregator.group_docs(set(groups))
+        return _resp({"kind": "APIGroupList", "apiVersion": "v1", "groups": docs})
 
     def _resource_list(self, group, version):
         res = []
@@ -359,9 +365,19 @@ class APIServer:
         try:
             user = self._authenticate(request)
             group, version, resource, ns, name, sub, watch = self._parse(request.path)
+            target = self.aggregator.route(group, version) if request.path.startswith("/apis/") else None
+            if target is not None:      # an extension API server's group/version (kube-aggregator proxy)
+                resource = resource or ""
+                resp = await self.aggregator.proxy(request, target, user)
+                code = resp.status
+                return resp
             if resource is None:
                 if version is None:  # /apis/<group>
                     if not any(ri.group == group for ri in SCHEME.by_kind.values()):
+                        agg = [d for d in self.aggregator.group_docs(set()) if d["name"] == group]
+                        if agg:
+                            code = 200
+                            return _resp({"kind": "APIGroup", "apiVersion": "v1", **agg[0]})
                         raise m.not_found("group", group)
                     code = 200
                     return _resp({"kind": "APIGroup", "apiVersion": "v1", **self._group_doc(group)})
