@@ -222,6 +222,8 @@ def kubelet(argv):
     ap.add_argument("--enforce-node-allocatable", default="pods")
     ap.add_argument("--cgroup-root", default="", help="cgroup v2 directory of the kubepods hierarchy")
     ap.add_argument("--experimental-allowed-unsafe-sysctls", default="", help="comma-separated sysctls or patterns ending in *")
+    ap.add_argument("--cpu-manager-policy", default="none", choices=("none", "static"))
+    ap.add_argument("--cpu-manager-reconcile-period", type=float, default=10.0, help="seconds")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     klog.setup(a.v, "kubelet")
@@ -253,7 +255,8 @@ def kubelet(argv):
                         eviction_max_pod_grace_period=a.eviction_max_pod_grace_period,
                         kube_reserved=a.kube_reserved, system_reserved=a.system_reserved,
                         enforce_node_allocatable=a.enforce_node_allocatable, cgroup_root=a.cgroup_root,
-                        allowed_unsafe_sysctls=[x for x in a.experimental_allowed_unsafe_sysctls.split(",") if x])
+                        allowed_unsafe_sysctls=[x for x in a.experimental_allowed_unsafe_sysctls.split(",") if x],
+                        cpu_manager_policy=a.cpu_manager_policy, cpu_manager_reconcile_period=a.cpu_manager_reconcile_period)
 
     async def mk():
         smi = None

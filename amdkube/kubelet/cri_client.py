@@ -149,6 +149,11 @@ class CRIClient:
         self._cid_sid.pop(cid, None)
         await self._call("remove_container", self.rt.RemoveContainer, C.RemoveContainerRequest(container_id=cid))
 
+    async def update_container_resources(self, cid, cpuset_cpus: str = "", **res):
+        lr = C.LinuxContainerResources(cpuset_cpus=cpuset_cpus, **res)
+        await self._call("update_container_resources", self.rt.UpdateContainerResources,
+                         C.UpdateContainerResourcesRequest(container_id=cid, linux=lr))
+
     async def list_containers(self, sandbox_id: str | None = None):
         f = C.ContainerFilter(pod_sandbox_id=sandbox_id) if sandbox_id else None
         req = C.ListContainersRequest(filter=f) if f else C.ListContainersRequest()

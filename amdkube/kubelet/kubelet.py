@@ -115,6 +115,9 @@ class KubeletConfig:
     enforce_node_allocatable: str = "pods"            # --enforce-node-allocatable (pods | none)
     cgroup_root: str = ""                             # cgroup v2 dir holding kubepods (empty: no enforcement)
     allowed_unsafe_sysctls: list = field(default_factory=list)   # --experimental-allowed-unsafe-sysctls
+    cpu_manager_policy: str = "none"                  # --cpu-manager-policy (none | static)
+    cpu_manager_reconcile_period: float = 10.0        # --cpu-manager-reconcile-period (s)
+    cpu_topology: object = None                       # cpumanager.CPUTopology (None: discover from sysfs)
 
 
 class PodWorker:
@@ -177,6 +180,13 @@ class Kubelet:
         self._sysctl_admit = (Whitelist(SAFE, SAFE_ANNOTATION), Whitelist(config.allowed_unsafe_sysctls, UNSAFE_ANNOTATION))
         self._kube_reserved = parse_reserved(config.kube_reserved)
         self._system_reserved = parse_reserved(config.system_reserved)
+        from .cpumanager import CPUManager
+        self.cpu_manager = CPUManager(config.cpu_manager_policy, config.cpu_topology,
+                                      self._kube_reserved.get("cpu", 0) + self._system_reserved.get("cpu", 0),
+                                      os.path.join(config.root_dir, "cpu_manager_state"))
+        self.runtime.cpu_manager = self.cpu_manager
+        self.runtime.gpu_numa = self._gpu_numa
+        self._cpuset_applied: dict[str, str] = {}
         self._pods_cgroup_enforced = None
         self.pressure: set[str] = set()
         self.status = StatusManager(client, on_terminal=self._on_terminal)
@@ -248,6 +258,8 @@ class Kubelet:
                         asyncio.create_task(self._eviction_loop(), name="eviction")]
         if self.cfg.evented_pleg:
             self._tasks.append(asyncio.create_task(self._evented_pleg(), name="pleg-events"))
+        if self.cpu_manager.policy != "none":
+            self._tasks.append(asyncio.create_task(self._cpu_reconcile_loop(), name="cpu-manager"))
         if self.cfg.pod_manifest_path:
             # static pods run with or without an apiserver (kubeadm: the apiserver IS a static
             # pod), so registration is retried in the background (kubelet_node_status.go
@@ -857,8 +869,54 @@ class Kubelet:
         self._rt_gen[uid] = self._rt_gen.get(uid, 0) + 1
         self.dispatch(uid)
 
+    def _gpu_numa(self, pod: dict, container: dict) -> set[int]:
+        """NUMA nodes of the GPUs assigned to one container (the AMD plugin's amd.com/numa-node
+        device attribute): where the CPU manager places its exclusive CPUs."""
+        from ..api.helpers import pod_extended_resource_assigned
+        out: set[int] = set()
+        cap = self.dm.store.capacity if hasattr(self.dm, "store") else {}
+        for rname, dom in cap.items():
+            for did in pod_extended_resource_assigned(rname, container, pod):
+                v = ((dom["resources"].get(did) or {}).get("attributes") or {}).get("amd.com/numa-node")
+                if v is not None and str(v).lstrip("-").isdigit() and int(v) >= 0:
+                    out.add(int(v))
+        return out
+
+    async def cpu_reconcile(self):
+        """cpu_manager.go reconcileState: shared-pool containers follow the shared pool as
+        exclusive assignments come and go (CRI UpdateContainerResources)."""
+        cm = self.cpu_manager
+        if self.sources_ready():
+            cm.retain_only(set(self.pods) | set(self.workers))
+        shared = cm.default_set()
+        from .cpumanager import format_cpuset
+        want = format_cpuset(shared)
+        updated = 0
+        for c in await self.cri.list_containers():
+            if c.state != C.CONTAINER_RUNNING:
+                continue
+            uid, name = c.labels.get(L_POD_UID, ""), c.metadata.name
+            if not uid or cm.exclusive(uid, name) or self._cpuset_applied.get(c.id) == want:
+                continue
+            try:
+                await self.cri.update_container_resources(c.id, cpuset_cpus=want)
+                self._cpuset_applied[c.id] = want
+                updated += 1
+            except Exception as e:
+                log.debug("cpu manager: update of %s failed: %r", c.id, e)
+        return updated
+
+    async def _cpu_reconcile_loop(self):
+        while True:
+            await asyncio.sleep(self.cfg.cpu_manager_reconcile_period)
+            try:
+                await self.cpu_reconcile()
+            except Exception as e:
+                log.debug("cpu manager reconcile failed: %r", e)
+
     def _cleanup(self, uid):
         self._runtime_uids.add(uid)   # the runtime may still hold leftovers: list before trusting the cache again
+        self.cpu_manager.release_pod(uid)
         self._rt_gen.pop(uid, None)
         self._rt_cache.pop(uid, None)
         self._rt_pending.pop(uid, None)

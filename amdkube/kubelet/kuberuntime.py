@@ -154,6 +154,8 @@ class RuntimeManager:
         self.seccomp_root = os.path.join(root_dir, "seccomp")   # --seccomp-profile-root
         self._image_seen: dict[str, float] = {}
         self.legacy = None          # gpu_legacy.AMDGPUManager when the Accelerators gate is on
+        self.cpu_manager = None     # cpumanager.CPUManager
+        self.gpu_numa = None        # (pod, container) -> NUMA nodes of its GPUs
         self.dns = None             # dns.DNSConfigurer (pod resolv.conf)
         self.memory_capacity = 1 << 40   # node memory (burstable OOM score scaling), set by the kubelet
         self.active_pods = None
@@ -254,6 +256,9 @@ class RuntimeManager:
             lres.cpu_quota = max(1000, Quantity(res["cpu"]).milli_value() * 100)
         req_cpu = ((c.get("resources") or {}).get("requests") or {}).get("cpu") or res.get("cpu")
         lres.cpu_shares = max(2, Quantity(req_cpu).milli_value() * 1024 // 1000) if req_cpu else 2   # MilliCPUToShares
+        if self.cpu_manager is not None and self.cpu_manager.policy != "none":
+            # cpu_manager.go AddContainer: exclusive CPUs (near the container's GPUs) or the shared pool
+            lres.cpuset_cpus = self.cpu_manager.allocate(pod, c, self.gpu_numa(pod, c) if self.gpu_numa else None)
         md = pod["metadata"]
         cfg = C.ContainerConfig(
             metadata=C.ContainerMetadata(name=c["name"], attempt=restart_count), image=C.ImageSpec(image=c["image"]),

@@ -426,7 +426,7 @@ class RocShim:
         env["AMDKUBE_ROOTFS"] = root
         r = cfg.linux.resources if cfg.HasField("linux") else None
         resources = {"cpu_quota": r.cpu_quota, "cpu_period": r.cpu_period, "memory_limit": r.memory_limit_in_bytes,
-                     "cpu_shares": r.cpu_shares, "oom_score_adj": r.oom_score_adj} if r else {}
+                     "cpu_shares": r.cpu_shares, "oom_score_adj": r.oom_score_adj, "cpuset": r.cpuset_cpus} if r else {}
         if sandbox_cfg is not None and sandbox_cfg.HasField("linux") and sandbox_cfg.linux.cgroup_parent:
             resources["cgroup_parent"] = sandbox_cfg.linux.cgroup_parent.strip("/")
         sec = cfg.linux.security_context.seccomp_profile_path if cfg.HasField("linux") else ""
@@ -458,11 +458,12 @@ class RocShim:
 
     def _launch_argv(self, c: Container) -> list[str]:
         sec, aa = c.resources.get("seccomp_profile"), c.resources.get("apparmor_profile")
+        cpuset = c.resources.get("cpuset") or ""
         if self.isolation != "namespaces":
-            if not (sec or aa):
+            if not (sec or aa or cpuset):
                 return c.argv
             return ([self.nsexec_bin, "--no-namespaces"] + (["--seccomp", sec] if sec else []) +
-                    (["--apparmor", aa] if aa else []) + ["--"] + c.argv)
+                    (["--apparmor", aa] if aa else []) + (["--cpuset", cpuset] if cpuset else []) + ["--"] + c.argv)
         # (env isolation: the OOM score is applied to the spawned process directly, see start_container)
         keep = [d["host_path"] for d in c.devices if "/dri/" in d["host_path"]]
         # QoS hierarchy from the kubelet (kubepods/[burstable|besteffort]/pod<uid>), else per sandbox
@@ -485,6 +486,8 @@ class RocShim:
             a += ["--memory-max", str(c.resources["memory_limit"])]
         if c.resources.get("cpu_quota") and c.resources.get("cpu_period"):
             a += ["--cpu-max", f"{c.resources['cpu_quota']} {c.resources['cpu_period']}"]
+        if cpuset:
+            a += ["--cpuset", cpuset]
         if not any(d["host_path"].endswith("/kfd") for d in c.devices):
             a += ["--hide-kfd"]
         return a + ["--"] + c.argv
@@ -597,6 +600,46 @@ class RocShim:
         except FileNotFoundError:
             pass
 
+    def update_resources(self, cid: str, lr) -> None:
+        """CRI UpdateContainerResources (the CPU manager's shared-pool re-pinning): the new
+        cpuset applies to every task of the container (its process group; its cgroup leaf too
+        under namespaces isolation)."""
+        c = self.containers.get(cid)
+        if c is None:
+            raise LookupError(f"container {cid} not found")
+        if lr.cpuset_cpus:
+            from ..kubelet.cpumanager import parse_cpuset
+            cpus = parse_cpuset(lr.cpuset_cpus)
+            c.resources["cpuset"] = lr.cpuset_cpus
+            if c.state == C.CONTAINER_RUNNING and c.pid:
+                for pid in _group_pids(c.pid):
+                    try:
+                        os.sched_setaffinity(pid, cpus)
+                    except OSError:
+                        pass
+                if self.isolation == "namespaces":
+                    try:
+                        with open(os.path.join(self._cgroup_of(c), "cpuset.cpus"), "w") as f:
+                            f.write(lr.cpuset_cpus)
+                    except OSError:
+                        pass
+        for k, v in (("memory_limit", lr.memory_limit_in_bytes), ("cpu_quota", lr.cpu_quota), ("cpu_period", lr.cpu_period),
+                     ("cpu_shares", lr.cpu_shares)):
+            if v:
+                c.resources[k] = v
+        if self.isolation == "namespaces" and c.state == C.CONTAINER_RUNNING:
+            cg = self._cgroup_of(c)
+            for fname, val in (("memory.max", lr.memory_limit_in_bytes),
+                               ("cpu.max", f"{lr.cpu_quota} {lr.cpu_period}" if lr.cpu_quota and lr.cpu_period else 0),
+                               ("cpu.weight", _shares_to_weight(lr.cpu_shares) if lr.cpu_shares else 0)):
+                if val:
+                    try:
+                        with open(os.path.join(cg, fname), "w") as f:
+                            f.write(str(val))
+                    except OSError:
+                        pass
+        self._ckpt("containers", c)
+
     async def exec_sync(self, cid: str, cmd: list[str], timeout: int):
         c = self.containers.get(cid)
         if c is None or c.state != C.CONTAINER_RUNNING:
@@ -692,6 +735,23 @@ def _proc_stats(pid: int) -> tuple[int, int]:
         return cpu, rss
     except (OSError, IndexError, ValueError):
         return 0, 0
+
+
+def _group_pids(pgid: int) -> list[int]:
+    """Every task of a container: the members of its process group (rocshim starts each
+    container in its own session)."""
+    out = []
+    for d in os.listdir("/proc"):
+        if not d.isdigit():
+            continue
+        try:
+            with open(f"/proc/{d}/stat") as f:
+                parts = f.read().rsplit(")", 1)[1].split()
+            if int(parts[2]) == pgid:
+                out.append(int(d))
+        except (OSError, IndexError, ValueError):
+            continue
+    return out
 
 
 def _abort(ctx, e):
@@ -791,6 +851,13 @@ class _Runtime:
         self._mark(ctx, sid)
         return C.StopContainerResponse()
 
+    async def UpdateContainerResources(self, req, ctx):
+        try:
+            self.r.update_resources(req.container_id, req.linux)
+        except Exception as e:
+            await _abort(ctx, e)
+        return C.UpdateContainerResourcesResponse()
+
     async def RemoveContainer(self, req, ctx):
         sid = self._sid_of(req.container_id)
         await self.r.remove_container(req.container_id)
@@ -825,13 +892,6 @@ class _Runtime:
         st = container_status_msg(c)
         info = {"pid": str(c.pid), "handler": c.handler, "devices": json.dumps(c.devices)} if req.verbose else {}
         return C.ContainerStatusResponse(status=st, info=info)
-
-    async def UpdateContainerResources(self, req, ctx):
-        c = self.r.containers.get(req.container_id)
-        if c is not None:
-            c.resources = {"cpu_quota": req.linux.cpu_quota, "cpu_period": req.linux.cpu_period,
-                           "memory_limit": req.linux.memory_limit_in_bytes}
-        return C.UpdateContainerResourcesResponse()
 
     async def Exec(self, req, ctx):
         c = self.r.containers.get(req.container_id)

@@ -6,7 +6,7 @@
 // isolation = "the container's /dev/dri contains only its own render nodes":
 //
 //   amdkube-nsexec [--dev-root /dev] [--keep /dev/dri/renderD128 ...] [--hide-kfd]
-//                  [--cgroup /sys/fs/cgroup/amdkube/<pod>/<ctr>] [--memory-max BYTES]
+//                  [--cgroup /sys/fs/cgroup/amdkube/<pod>/<ctr>] [--memory-max BYTES] [--cpuset 0-3,8]
 //                  [--cpu-max "QUOTA PERIOD"] -- argv...
 //
 //  1. join (creating) a cgroup-v2 leaf and apply memory.max / cpu.max / cpu.weight
@@ -70,6 +70,24 @@ static bool apparmor_onexec(const std::string& profile) {
   return write_file("/proc/self/attr/apparmor/exec", cmd) || write_file("/proc/self/attr/exec", cmd);
 }
 
+// "0-3,8,10-11" → affinity mask (the CPU manager's exclusive or shared-pool cpuset)
+static bool parse_cpuset(const std::string& spec, cpu_set_t* set) {
+  CPU_ZERO(set);
+  std::stringstream ss(spec);
+  std::string part;
+  int n = 0;
+  while (std::getline(ss, part, ',')) {
+    if (part.empty()) continue;
+    size_t dash = part.find('-');
+    char* end = nullptr;
+    long lo = std::strtol(part.c_str(), &end, 10), hi = lo;
+    if (dash != std::string::npos) hi = std::strtol(part.c_str() + dash + 1, &end, 10);
+    if (lo < 0 || hi < lo || hi >= CPU_SETSIZE) return false;
+    for (long c = lo; c <= hi; ++c) { CPU_SET(c, set); ++n; }
+  }
+  return n > 0;
+}
+
 static int mkdir_p(const std::string& p) {
   std::string cur;
   for (size_t i = 0; i < p.size(); ++i) {
@@ -85,7 +103,7 @@ int main(int argc, char** argv) {
   std::string dev_root = "/dev", cgroup, mem_max, cpu_max, cpu_weight, oom_adj;
   std::vector<std::string> keep, binds;
   bool hide_kfd = false, no_ns = false;
-  std::string seccomp_profile, apparmor;
+  std::string seccomp_profile, apparmor, cpuset;
   int i = 1;
   for (; i < argc; ++i) {
     std::string a = argv[i];
@@ -104,6 +122,7 @@ int main(int argc, char** argv) {
     else if (a == "--seccomp" && i + 1 < argc) seccomp_profile = argv[++i];
     else if (a == "--apparmor" && i + 1 < argc) apparmor = argv[++i];
     else if (a == "--no-namespaces") no_ns = true;
+    else if (a == "--cpuset" && i + 1 < argc) cpuset = argv[++i];
     else {
       std::fprintf(stderr, "amdkube-nsexec: unknown argument %s\n", a.c_str());
       return 126;
@@ -125,6 +144,14 @@ int main(int argc, char** argv) {
       return 126;
     }
   }
+  if (!cpuset.empty()) {   // inherited by every process of the container
+    cpu_set_t set;
+    if (!parse_cpuset(cpuset, &set)) {
+      std::fprintf(stderr, "amdkube-nsexec: bad --cpuset %s\n", cpuset.c_str());
+      return 126;
+    }
+    if (sched_setaffinity(0, sizeof(set), &set) < 0) return die("sched_setaffinity");
+  }
   if (no_ns) {
     if (!apparmor.empty() && !apparmor_onexec(apparmor)) return die(("AppArmor profile " + apparmor).c_str());
     std::string err;
@@ -140,6 +167,7 @@ int main(int argc, char** argv) {
     if (!mem_max.empty()) write_file(cgroup + "/memory.max", mem_max);
     if (!cpu_max.empty()) write_file(cgroup + "/cpu.max", cpu_max);
     if (!cpu_weight.empty()) write_file(cgroup + "/cpu.weight", cpu_weight);
+    if (!cpuset.empty()) write_file(cgroup + "/cpuset.cpus", cpuset);   // when the cpuset controller is delegated
     if (!write_file(cgroup + "/cgroup.procs", std::to_string(getpid()))) return die("join cgroup");
   }
   // lowering the score needs CAP_SYS_RESOURCE, which the privileged launcher has
