@@ -224,6 +224,9 @@ def kubelet(argv):
     ap.add_argument("--experimental-allowed-unsafe-sysctls", default="", help="comma-separated sysctls or patterns ending in *")
     ap.add_argument("--cpu-manager-policy", default="none", choices=("none", "static"))
     ap.add_argument("--cpu-manager-reconcile-period", type=float, default=10.0, help="seconds")
+    ap.add_argument("--image-gc-high-threshold", type=int, default=85)
+    ap.add_argument("--image-gc-low-threshold", type=int, default=80)
+    ap.add_argument("--minimum-image-ttl-duration", type=float, default=120.0, help="seconds")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     klog.setup(a.v, "kubelet")
@@ -256,7 +259,9 @@ def kubelet(argv):
                         kube_reserved=a.kube_reserved, system_reserved=a.system_reserved,
                         enforce_node_allocatable=a.enforce_node_allocatable, cgroup_root=a.cgroup_root,
                         allowed_unsafe_sysctls=[x for x in a.experimental_allowed_unsafe_sysctls.split(",") if x],
-                        cpu_manager_policy=a.cpu_manager_policy, cpu_manager_reconcile_period=a.cpu_manager_reconcile_period)
+                        cpu_manager_policy=a.cpu_manager_policy, cpu_manager_reconcile_period=a.cpu_manager_reconcile_period,
+                        image_gc_high_threshold=a.image_gc_high_threshold, image_gc_low_threshold=a.image_gc_low_threshold,
+                        minimum_image_ttl_duration=a.minimum_image_ttl_duration)
 
     async def mk():
         smi = None

@@ -194,6 +194,9 @@ class CRIClient:
         return (await self._call("pull_image", self.img.PullImage, C.PullImageRequest(image=C.ImageSpec(image=image)),
                                  timeout=300)).image_ref
 
+    async def remove_image(self, image):
+        await self._call("remove_image", self.img.RemoveImage, C.RemoveImageRequest(image=C.ImageSpec(image=image)))
+
     async def list_images(self):
         return list((await self._call("list_images", self.img.ListImages, C.ListImagesRequest())).images)
 

@@ -118,6 +118,10 @@ class KubeletConfig:
     cpu_manager_policy: str = "none"                  # --cpu-manager-policy (none | static)
     cpu_manager_reconcile_period: float = 10.0        # --cpu-manager-reconcile-period (s)
     cpu_topology: object = None                       # cpumanager.CPUTopology (None: discover from sysfs)
+    image_gc_high_threshold: int = 85                 # --image-gc-high-threshold (%)
+    image_gc_low_threshold: int = 80                  # --image-gc-low-threshold (%)
+    minimum_image_ttl_duration: float = 120.0         # --minimum-image-ttl-duration (s)
+    image_gc_period: float = 300.0                    # ImageGCPeriod
 
 
 class PodWorker:
@@ -185,6 +189,10 @@ class Kubelet:
                                       self._kube_reserved.get("cpu", 0) + self._system_reserved.get("cpu", 0),
                                       os.path.join(config.root_dir, "cpu_manager_state"))
         self.runtime.cpu_manager = self.cpu_manager
+        from .images import ImageGCManager
+        self.image_gc = ImageGCManager(self.cri, config.image_gc_high_threshold, config.image_gc_low_threshold,
+                                       config.minimum_image_ttl_duration, recorder=self.recorder,
+                                       node_ref=lambda: {"kind": "Node", "metadata": {"name": self.node_name, "uid": self.node_name}})
         self.runtime.gpu_numa = self._gpu_numa
         self._cpuset_applied: dict[str, str] = {}
         self._pods_cgroup_enforced = None
@@ -1138,12 +1146,19 @@ class Kubelet:
         return api and (not self.cfg.pod_manifest_path or self._static_read)
 
     async def _gc_loop(self):
+        last_image_gc = time.monotonic()
         while True:
-            await asyncio.sleep(self.cfg.gc_period)
+            await asyncio.sleep(min(self.cfg.gc_period, self.cfg.image_gc_period))
             try:
                 await self.container_gc()
             except Exception as e:
                 log.debug("container GC failed: %r", e)
+            if time.monotonic() - last_image_gc >= self.cfg.image_gc_period:
+                last_image_gc = time.monotonic()
+                try:
+                    await self.image_gc.garbage_collect()
+                except Exception as e:
+                    log.debug("image GC failed: %r", e)
 
     async def _housekeeping(self):
         """Periodic resync (syncFrequency) of every pod; keeps the sync loop health probe fresh."""
@@ -1261,6 +1276,16 @@ class Kubelet:
         if not met:
             return None
         sig = sorted(met, key=lambda x: x.signal != "memory.available")[0].signal
+        if sig != "memory.available":
+            # reclaimNodeLevelResources: dead containers and unused images before evicting a pod
+            try:
+                await self.container_gc()
+                freed = await self.image_gc.delete_unused()
+            except Exception as e:
+                freed = 0
+                log.debug("node-level reclaim failed: %r", e)
+            if freed and not self.eviction.met(self.eviction_observer()):
+                return None
         cands = self.active_pods()
         if self.gates("ExperimentalCriticalPodAnnotation"):
             # static critical pods are never evicted: they are not re-admitted (eviction_manager.go:377-382)

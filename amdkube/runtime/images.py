@@ -51,9 +51,28 @@ def normalize(ref: str) -> str:
     return ref if ":" in last else ref + ":latest"
 
 
+def _tree_size(path: str) -> int:
+    if os.path.isfile(path):
+        return os.path.getsize(path)
+    tot = 0
+    for dp, _dn, fns in os.walk(path):
+        for fn in fns:
+            try:
+                tot += os.path.getsize(os.path.join(dp, fn))
+            except OSError:
+                pass
+    return tot
+
+
 class ImageStore:
+    """Images pulled from a local path are copied into `<state>/images/<digest>/` (the
+    runtime's image filesystem), so they occupy space there, report their size and free it
+    when removed (kubelet image GC); built-in images are preloaded and cannot be removed."""
+
     def __init__(self, state_dir: str):
         self.path = os.path.join(state_dir, "images.json")
+        self.blob_root = os.path.join(state_dir, "images")
+        os.makedirs(self.blob_root, exist_ok=True)
         self.images = builtin_images()
         if os.path.exists(self.path):
             with open(self.path) as f:
@@ -80,17 +99,44 @@ class ImageStore:
             return self.image_id(self.resolve(ref)[0])
         path = ref[len("file://"):] if ref.startswith("file://") else ref
         if os.path.isabs(path) and os.path.exists(path):
-            entry = os.path.join(path, "run") if os.path.isdir(path) else path
-            self.images[normalize(ref)] = {"entrypoint": [entry], "workdir": path if os.path.isdir(path) else ""}
+            digest = hashlib.sha256(normalize(ref).encode()).hexdigest()[:32]
+            blob = os.path.join(self.blob_root, digest)
+            shutil.rmtree(blob, ignore_errors=True)
+            if os.path.isdir(path):
+                shutil.copytree(path, blob, symlinks=True)
+                entry, workdir = os.path.join(blob, "run"), blob
+            else:
+                os.makedirs(blob)
+                entry = os.path.join(blob, os.path.basename(path))
+                shutil.copy2(path, entry)
+                workdir = ""
+            self.images[normalize(ref)] = {"entrypoint": [entry], "workdir": workdir, "blob": blob, "size": _tree_size(blob)}
             self._save()
             return self.image_id(normalize(ref))
         raise KeyError(f"image {ref!r} not found (no registry access; register it in images.json or pull a local path)")
 
     def remove(self, ref: str):
-        n = normalize(ref)
+        n = normalize(ref) if not ref.startswith("sha256:") else next(
+            (k for k in self.images if self.image_id(k) == ref), ref)
         if n in self.images and n not in builtin_images():
+            blob = self.images[n].get("blob")
             del self.images[n]
             self._save()
+            if blob and blob.startswith(self.blob_root + os.sep):
+                shutil.rmtree(blob, ignore_errors=True)
+
+    def removable(self, name: str) -> bool:
+        return name not in builtin_images()
+
+    def size(self, name: str) -> int:
+        spec = self.images.get(name) or {}
+        if "size" in spec:
+            return int(spec["size"])
+        ep = (spec.get("entrypoint") or [""])[0]
+        return _tree_size(ep) if ep.startswith(NATIVE_BIN) and os.path.exists(ep) else 0
+
+    def used_bytes(self) -> int:
+        return _tree_size(self.blob_root)
 
     def list(self):
         return [(n, self.image_id(n), spec) for n, spec in self.images.items()]

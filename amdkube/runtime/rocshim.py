@@ -961,7 +961,7 @@ class _Images:
         self.r = r
 
     def _img(self, name, iid):
-        return C.Image(id=iid, repo_tags=[name], size=0)
+        return C.Image(id=iid, repo_tags=[name], size=self.r.images.size(name))
 
     async def ListImages(self, req, ctx):
         return C.ListImagesResponse(images=[self._img(n, i) for n, i, _ in self.r.images.list()])
@@ -979,12 +979,22 @@ class _Images:
             await ctx.abort(grpc.StatusCode.NOT_FOUND, str(e))
 
     async def RemoveImage(self, req, ctx):
-        self.r.images.remove(req.image.image)
+        ref = req.image.image
+        name = next((n for n, i, _ in self.r.images.list() if i == ref), None) if ref.startswith("sha256:") else \
+            (self.r.images.resolve(ref) or (None,))[0]
+        if name is not None and not self.r.images.removable(name):
+            await ctx.abort(grpc.StatusCode.FAILED_PRECONDITION, f"image {name} is preloaded and cannot be removed")
+        if name is not None and any(c.image_ref == self.r.images.image_id(name) for c in self.r.containers.values()):
+            await ctx.abort(grpc.StatusCode.FAILED_PRECONDITION, f"image {name} is in use by a container")
+        self.r.images.remove(ref)
         return C.RemoveImageResponse()
 
     async def ImageFsInfo(self, req, ctx):
-        st = os.statvfs(self.r.state_dir)
-        used = (st.f_blocks - st.f_bfree) * st.f_frsize
+        """The image filesystem: bytes held by pulled images; storage_id names the directory
+        (the kubelet statvfs()es it for capacity, as cAdvisor does for the runtime's root)."""
+        root = self.r.images.blob_root
+        used = await asyncio.to_thread(self.r.images.used_bytes)
+        n = sum(1 for _ in os.scandir(root))
         return C.ImageFsInfoResponse(image_filesystems=[C.FilesystemUsage(
-            timestamp=now_ns(), storage_id=C.StorageIdentifier(uuid="rocshim"), used_bytes=C.UInt64Value(value=used),
-            inodes_used=C.UInt64Value(value=st.f_files - st.f_ffree))])
+            timestamp=now_ns(), storage_id=C.StorageIdentifier(uuid=os.path.abspath(root)), used_bytes=C.UInt64Value(value=used),
+            inodes_used=C.UInt64Value(value=n))])

@@ -102,3 +102,51 @@ def test_oom_killed_reason_from_cgroup_memory_events(tmp_path):
     assert shim._oom_killed(C_())
     shim.isolation = "env"
     assert not shim._oom_killed(C_())
+
+
+def test_image_gc_frees_unused_images_lru(tmp_path):
+    """image_gc_manager_test.go: above the high threshold, unused images go least recently used
+    first down to the low threshold; in-use, too-young and preloaded images stay."""
+    from amdkube.kubelet.images import ImageGCManager
+
+    async def go():
+        async with LocalCluster(gpus="none", relist_period=0.2, with_controllers=False) as lc:
+            c, k = lc.client, lc.kubelet
+            srcs = []
+            for i in range(3):
+                d = tmp_path / f"img{i}"
+                d.mkdir()
+                (d / "run").write_text("#!/bin/sh\nsleep 30\n")
+                os.chmod(d / "run", 0o755)
+                (d / "payload").write_bytes(os.urandom(64 * 1024))
+                srcs.append(str(d))
+            for i, s in enumerate(srcs):
+                await k.cri.pull_image(f"file://{s}")
+            imgs = {i.repo_tags[0]: i for i in await k.cri.list_images()}
+            names = [f"file://{s}:latest" for s in srcs]
+            assert all(imgs[n].size >= 64 * 1024 for n in names)
+            # image 2 is used by a running pod
+            await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "user"},
+                            "spec": {"containers": [{"name": "c", "image": f"file://{srcs[2]}"}]}}, "default")
+            await wait_pod(c, "default", "user", ("Running",), 20)
+            clock = [1000.0]
+            gc = ImageGCManager(k.cri, high=90, low=80, min_age=60, clock=lambda: clock[0])
+            await gc.detect()
+            clock[0] += 30
+            assert (await gc.free_space(10 ** 9)) == 0                 # every candidate is younger than min age
+            clock[0] += 100
+            await gc.detect()                                        # the running pod's image is "used" now
+            clock[0] += 10
+            gc.records[imgs[names[1]].id].last_used = clock[0] - 5    # image 1 used more recently than image 0
+            freed = await gc.free_space(1)
+            left = {i.repo_tags[0] for i in await k.cri.list_images()}
+            assert freed >= 64 * 1024 and names[0] not in left and names[1] in left and names[2] in left
+            freed = await gc.delete_unused()
+            left = {i.repo_tags[0] for i in await k.cri.list_images()}
+            assert names[1] not in left and names[2] in left and "busybox:latest" in left
+            assert len(os.listdir(os.path.join(lc.shim.state_dir, "images"))) == 1   # only the in-use blob remains
+            with pytest.raises(ValueError):
+                ImageGCManager(k.cri, high=50, low=80)
+            out = await ImageGCManager(k.cri, high=100, low=90).garbage_collect()
+            assert 0 <= out["usage_percent"] <= 100 and out["freed"] == 0
+    run(go(), 60)
