@@ -638,9 +638,44 @@ class Kubelet:
             return False, "AppArmor", f"Cannot enforce AppArmor: {err}"
         return True, "", ""
 
+    def _shortfall(self, pod: dict) -> dict[str, int]:
+        """What the node lacks to admit `pod` (preemption.go admissionRequirementList)."""
+        from .preemption import request
+        alloc = node_allocatable(self.node or {})
+        others = self.active_pods()
+        want = dict(pod_requests(pod))
+        want["pods"] = 1
+        out = {}
+        for k, v in want.items():
+            if k in alloc:
+                need = sum(request(p, k) for p in others) + v - alloc[k]
+                if need > 0:
+                    out[k] = need
+        return out
+
+    async def _preempt_for(self, pod: dict) -> bool:
+        """CriticalPodAdmissionHandler.HandleAdmissionFailure: evict what the critical pod needs."""
+        from .preemption import is_critical, pods_to_preempt
+        if not self.gates("ExperimentalCriticalPodAnnotation") or not is_critical(pod):
+            return False
+        try:
+            victims = pods_to_preempt(self.active_pods(), self._shortfall(pod))
+        except ValueError as e:
+            log.warning("cannot preempt for critical pod %s: %s", m.name_of(pod), e)
+            return False
+        msg = "Preempted in order to admit critical pod"
+        for v in victims:
+            self.recorder.event(v, "Warning", "Preempting", msg)
+            await self.runtime.kill_pod(m.uid_of(v), int((v.get("spec") or {}).get("terminationGracePeriodSeconds", 30)), v)
+            self.status.set(v, {"phase": "Failed", "reason": "Preempting", "message": msg,
+                                "conditions": (v.get("status") or {}).get("conditions") or []})
+        return bool(victims)
+
     async def _admit(self, pod: dict) -> bool:
         uid = m.uid_of(pod)
         ok, reason, msg = self.can_admit(pod)
+        if not ok and reason.startswith("OutOf") and await self._preempt_for(pod):
+            ok, reason, msg = self.can_admit(pod)
         if ok:
             try:
                 await self.dm.admit_pod(pod)

@@ -150,3 +150,46 @@ def test_image_gc_frees_unused_images_lru(tmp_path):
             out = await ImageGCManager(k.cri, high=100, low=90).garbage_collect()
             assert 0 <= out["usage_percent"] <= 100 and out["freed"] == 0
     run(go(), 60)
+
+
+def test_critical_pod_preemption_selection_and_admission():
+    """preemption_test.go: the minimal victim set, best-effort first, distance-ordered; on a
+    node without room a critical kube-system pod is admitted after evicting what it needs."""
+    from amdkube.kubelet.preemption import pods_to_preempt
+
+    def p(name, qos, cpu=None, mem=None, critical=False):
+        res = {}
+        if qos == "Guaranteed":
+            res = {"limits": {"cpu": cpu, "memory": mem}}
+        elif qos == "Burstable":
+            res = {"requests": {k: v for k, v in (("cpu", cpu), ("memory", mem)) if v}}
+        md = {"name": name, "namespace": "kube-system" if critical else "default", "uid": name}
+        if critical:
+            md["annotations"] = {"scheduler.alpha.kubernetes.io/critical-pod": ""}
+        return {"metadata": md, "spec": {"containers": [{"name": "c", "resources": res}]}}
+    pods = [p("be1", "BestEffort"), p("bu-small", "Burstable", "100m"), p("bu-big", "Burstable", "900m"),
+            p("gu", "Guaranteed", "2", "1Gi"), p("crit", "Guaranteed", "4", "1Gi", critical=True)]
+    names = lambda vs: sorted(m.name_of(v) for v in vs)   # noqa: E731
+    assert names(pods_to_preempt(pods, {"cpu": 800})) == ["bu-big"]          # closest single burstable pod
+    assert names(pods_to_preempt(pods, {"cpu": 2500})) == ["bu-big", "gu"]
+    assert names(pods_to_preempt(pods, {"pods": 1})) == ["be1"]
+    with pytest.raises(ValueError):
+        pods_to_preempt(pods, {"cpu": 10000})                               # critical pods are never victims
+
+    async def go():
+        async with LocalCluster(gpus="none", relist_period=0.2, with_controllers=False,
+                                kubelet_kw={"cpu_capacity": 2, "feature_gates": "ExperimentalCriticalPodAnnotation=true"}) as lc:
+            c = lc.client
+            await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "hog"},
+                            "spec": {"containers": [{"name": "c", "image": "busybox", "command": ["sleep", "60"],
+                                                     "resources": {"requests": {"cpu": "1500m"}}}]}}, "default")
+            await wait_pod(c, "default", "hog", ("Running",), 20)
+            crit = {"apiVersion": "v1", "kind": "Pod", "metadata": {
+                "name": "crit", "namespace": "kube-system", "annotations": {"scheduler.alpha.kubernetes.io/critical-pod": ""}},
+                "spec": {"nodeName": lc.node_name, "containers": [{"name": "c", "image": "busybox", "command": ["sleep", "60"],
+                                                                  "resources": {"requests": {"cpu": "1"}}}]}}
+            await c.create(crit, "kube-system")
+            await wait_pod(c, "kube-system", "crit", ("Running",), 20)
+            hog = await wait_pod(c, "default", "hog", ("Failed",), 20)
+            assert hog["status"]["reason"] == "Preempting"
+    run(go(), 60)
