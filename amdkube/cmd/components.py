@@ -32,14 +32,22 @@ def _client(a, **kw):
 
 def _run_forever(coro_factory):
     async def main():
-        comp = await coro_factory()
         stop = asyncio.Event()
         loop = asyncio.get_running_loop()
         for s in (signal.SIGINT, signal.SIGTERM):
             loop.add_signal_handler(s, stop.set)
-        await stop.wait()
-        if hasattr(comp, "stop"):
-            await comp.stop()
+        while True:
+            comp = await coro_factory()
+            # a component may ask to be rebuilt in place (dynamic kubelet config: the reference
+            # kubelet exits for its supervisor to restart it with the new checkpoint)
+            restart = getattr(comp, "restart_requested", None) or asyncio.Event()
+            done, _ = await asyncio.wait([asyncio.create_task(stop.wait()), asyncio.create_task(restart.wait())],
+                                         return_when=asyncio.FIRST_COMPLETED)
+            if hasattr(comp, "stop"):
+                await comp.stop()
+            if stop.is_set():
+                return
+            logging.getLogger("amdkube").info("restarting %s to apply new configuration", type(comp).__name__)
     prof_path = os.environ.get("AMDKUBE_CPROFILE")   # whole-process profile of a daemon, written on SIGTERM
     if prof_path:
         import cProfile
@@ -224,6 +232,8 @@ def kubelet(argv):
     ap.add_argument("--experimental-allowed-unsafe-sysctls", default="", help="comma-separated sysctls or patterns ending in *")
     ap.add_argument("--cpu-manager-policy", default="none", choices=("none", "static"))
     ap.add_argument("--cpu-manager-reconcile-period", type=float, default=10.0, help="seconds")
+    ap.add_argument("--config", default=None, help="KubeletConfiguration file (KubeletConfigFile gate)")
+    ap.add_argument("--dynamic-config-dir", default=None, help="checkpoints of Node.spec.configSource (DynamicKubeletConfig gate)")
     ap.add_argument("--image-gc-high-threshold", type=int, default=85)
     ap.add_argument("--image-gc-low-threshold", type=int, default=80)
     ap.add_argument("--minimum-image-ttl-duration", type=float, default=120.0, help="seconds")
@@ -261,7 +271,8 @@ def kubelet(argv):
                         allowed_unsafe_sysctls=[x for x in a.experimental_allowed_unsafe_sysctls.split(",") if x],
                         cpu_manager_policy=a.cpu_manager_policy, cpu_manager_reconcile_period=a.cpu_manager_reconcile_period,
                         image_gc_high_threshold=a.image_gc_high_threshold, image_gc_low_threshold=a.image_gc_low_threshold,
-                        minimum_image_ttl_duration=a.minimum_image_ttl_duration)
+                        minimum_image_ttl_duration=a.minimum_image_ttl_duration,
+                        config_file=a.config, dynamic_config_dir=a.dynamic_config_dir)
 
     async def mk():
         smi = None

@@ -122,6 +122,8 @@ class KubeletConfig:
     image_gc_low_threshold: int = 80                  # --image-gc-low-threshold (%)
     minimum_image_ttl_duration: float = 120.0         # --minimum-image-ttl-duration (s)
     image_gc_period: float = 300.0                    # ImageGCPeriod
+    config_file: str | None = None                    # --config (KubeletConfiguration file)
+    dynamic_config_dir: str | None = None             # --dynamic-config-dir
 
 
 class PodWorker:
@@ -142,6 +144,15 @@ def _semantic(pod: dict):
 
 class Kubelet:
     def __init__(self, client: Client, config: KubeletConfig, smi_backend=None):
+        from . import kubeletconfig as kcfg
+        self.dynamic = None
+        gates = FeatureGate(config.feature_gates)
+        if config.config_file:        # --config: a KubeletConfiguration file over the flags
+            config = kcfg.apply(config, kcfg.load_file(config.config_file))
+        if config.dynamic_config_dir and gates("DynamicKubeletConfig"):
+            self.dynamic = kcfg.DynamicConfig(config.dynamic_config_dir)
+            config = self.dynamic.bootstrap(config)
+        self.restart_requested = asyncio.Event()
         self.client = client
         self.cfg = config
         self.node_name = config.node_name
@@ -365,6 +376,9 @@ class Kubelet:
                  cond("DiskPressure", disk_pressure, "KubeletHasNoDiskPressure" if not disk_pressure else "KubeletHasDiskPressure",
                       "kubelet has no disk pressure" if not disk_pressure else "kubelet has disk pressure"),
                  cond("OutOfDisk", False, "KubeletHasSufficientDisk", "kubelet has sufficient disk space available")]
+        if self.dynamic is not None:
+            dc = self.dynamic.condition
+            conds.append(cond("ConfigOK", dc["status"] == "True", dc["reason"], dc["message"]))
         st = {"capacity": cap, "allocatable": alloc, "conditions": conds,
               "addresses": [{"type": "InternalIP", "address": self.cfg.node_ip}, {"type": "Hostname", "address": self.node_name}],
               "daemonEndpoints": {"kubeletEndpoint": {"Port": self.server.port if self.server else self.cfg.port}},
@@ -425,6 +439,12 @@ class Kubelet:
             except Exception as e:
                 log.warning("node status update failed: %r", e)
                 await asyncio.sleep(0.5)
+            if self.dynamic is not None and self.node is not None:
+                try:
+                    if await self.dynamic.sync(self.client, self.node):
+                        self.restart_requested.set()
+                except Exception as e:
+                    log.warning("dynamic config sync failed: %r", e)
 
     # ============================================================= pod sources
     def active_pods(self) -> list[dict]:
