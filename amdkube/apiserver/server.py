@@ -95,8 +95,23 @@ class APIServer:
                  anonymous_auth: bool = True, service_cidr: str = "10.0.0.0/24", node_port_range: str = "30000-32767",
                  service_account_key: bytes | None = None, tls_cert_file: str | None = None, tls_key_file: str | None = None,
                  client_ca_file: str | None = None, audit_log_path: str | None = None, audit_policy_file: str | None = None,
-                 audit_log_maxsize: int = 0, audit_log_maxbackup: int = 0):
+                 audit_log_maxsize: int = 0, audit_log_maxbackup: int = 0, kubelet_https: bool = False,
+                 kubelet_client_certificate: str | None = None, kubelet_client_key: str | None = None,
+                 kubelet_certificate_authority: str | None = None):
         self.store = store or MVCCStore()
+        # --kubelet-https / --kubelet-client-certificate / --kubelet-client-key /
+        # --kubelet-certificate-authority: how the apiserver reaches kubelets (logs, exec, proxy)
+        self.kubelet_scheme = "https" if kubelet_https else "http"
+        self.kubelet_ssl = None
+        if kubelet_https:
+            import ssl
+            ctx = ssl.create_default_context(ssl.Purpose.SERVER_AUTH, cafile=kubelet_certificate_authority)
+            ctx.check_hostname = False
+            if not kubelet_certificate_authority:
+                ctx.verify_mode = ssl.CERT_NONE
+            if kubelet_client_certificate:
+                ctx.load_cert_chain(kubelet_client_certificate, kubelet_client_key)
+            self.kubelet_ssl = ctx
         self.admission = adm.Chain(admission_plugins, admission_config)
         self.registry = Registry(self.store, self.admission, ServiceAllocator(service_cidr, parse_port_range(node_port_range)))
         from .crd import CRDManager
@@ -735,22 +750,22 @@ class APIServer:
         addr, port = self._kubelet_addr(node_name)
         qs = request.query_string
         if top == "portforward":
-            url, protos = f"http://{addr}:{port}/portForward/{ns}/{name}?{qs}", PORTFORWARD_PROTOCOLS
+            url, protos = f"{self.kubelet_scheme}://{addr}:{port}/portForward/{ns}/{name}?{qs}", PORTFORWARD_PROTOCOLS
         else:
             container = q.get("container") or ((pod.get("spec") or {}).get("containers") or [{}])[0].get("name", "")
-            url, protos = f"http://{addr}:{port}/{top}/{ns}/{name}/{container}?{qs}", CHANNEL_PROTOCOLS
+            url, protos = f"{self.kubelet_scheme}://{addr}:{port}/{top}/{ns}/{name}/{container}?{qs}", CHANNEL_PROTOCOLS
         ws = web.WebSocketResponse(protocols=protos, max_msg_size=0)
         if not ws.can_prepare(request).ok:
             raise m.bad_request(f"{top} needs a WebSocket upgrade (protocols {', '.join(protos)})")
         await ws.prepare(request)
-        return await bridge(ws, url, [ws.ws_protocol or protos[0]])
+        return await bridge(ws, url, [ws.ws_protocol or protos[0]], ssl=self.kubelet_ssl)
 
     async def _proxy(self, request, plural, ns, name, path, q):
         if self._http is None:
             self._http = ClientSession(timeout=ClientTimeout(total=None))
         if plural == "nodes":
             addr, port = self._kubelet_addr(name)
-            target = f"http://{addr}:{port}"
+            target = f"{self.kubelet_scheme}://{addr}:{port}"
         elif plural == "pods":
             pod_name, _, pport = name.partition(":")
             pod = self.registry.rs("pods").get(ns, pod_name)
@@ -779,7 +794,8 @@ class APIServer:
             raise m.not_found("subresource", "proxy")
         body = await request.read()
         hdrs = {k: v for k, v in request.headers.items() if k.lower() not in ("host", "authorization", "content-length")}
-        async with self._http.request(request.method, f"{target}/{path}", params=q, data=body or None, headers=hdrs) as r:
+        async with self._http.request(request.method, f"{target}/{path}", params=q, data=body or None, headers=hdrs,
+                                      ssl=self.kubelet_ssl if plural == "nodes" else None) as r:
             data = await r.read()
             return web.Response(status=r.status, body=data,
                                 headers={k: v for k, v in r.headers.items() if k.lower() in ("content-type", "cache-control")})
@@ -800,8 +816,8 @@ class APIServer:
         params = {k: v for k, v in q.items() if k in ("tailLines", "follow", "previous", "sinceSeconds", "timestamps")}
         if self._http is None:
             self._http = ClientSession(timeout=ClientTimeout(total=None))
-        url = f"http://{addr}:{port}/containerLogs/{ns}/{name}/{container}"
-        async with self._http.get(url, params=params) as r:
+        url = f"{self.kubelet_scheme}://{addr}:{port}/containerLogs/{ns}/{name}/{container}"
+        async with self._http.get(url, params=params, ssl=self.kubelet_ssl) as r:
             if r.status != 200:
                 raise m.StatusError(r.status, "BadRequest", (await r.text())[:500])
             out = web.StreamResponse(status=200, headers={"Content-Type": "text/plain"})

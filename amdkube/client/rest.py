@@ -107,6 +107,20 @@ class Client:
         self._session: aiohttp.ClientSession | None = None
         self._loop = None
 
+    def set_client_cert(self, cert_file: str, key_file: str):
+        """Certificate rotation (kubelet/certificate/transport.go): new connections present the
+        new client certificate; the pooled ones are closed so none keeps the old identity."""
+        if self.ssl is None:
+            return
+        self.ssl.load_cert_chain(cert_file, key_file)
+        sess, self._session = self._session, None
+        if sess is not None and not sess.closed:
+            import asyncio as _asyncio
+            try:
+                _asyncio.get_running_loop().create_task(sess.close())
+            except RuntimeError:
+                pass
+
     # ---------------------------------------------------------------- session
     @property
     def session(self) -> aiohttp.ClientSession:

@@ -83,6 +83,10 @@ def apiserver(argv):
     ap.add_argument("--client-ca-file", default=None)
     ap.add_argument("-v", type=int, default=0)
     ap.add_argument("--audit-log-path", default=None, help="write audit events (JSON lines) here; - for stdout")
+    ap.add_argument("--kubelet-https", default="false", choices=("true", "false"))
+    ap.add_argument("--kubelet-client-certificate", default=None)
+    ap.add_argument("--kubelet-client-key", default=None)
+    ap.add_argument("--kubelet-certificate-authority", default=None)
     ap.add_argument("--audit-policy-file", default=None, help="audit.k8s.io Policy (default: everything at Metadata)")
     ap.add_argument("--audit-log-maxsize", type=int, default=0, help="rotate the audit log at this many MB")
     ap.add_argument("--audit-log-maxbackup", type=int, default=0, help="rotated audit logs to keep")
@@ -109,7 +113,9 @@ def apiserver(argv):
                         service_account_key=open(a.service_account_key_file, "rb").read().strip() if a.service_account_key_file else None,
                         tls_cert_file=a.tls_cert_file, tls_key_file=a.tls_private_key_file, client_ca_file=a.client_ca_file,
                         audit_log_path=a.audit_log_path, audit_policy_file=a.audit_policy_file,
-                        audit_log_maxsize=a.audit_log_maxsize, audit_log_maxbackup=a.audit_log_maxbackup)
+                        audit_log_maxsize=a.audit_log_maxsize, audit_log_maxbackup=a.audit_log_maxbackup,
+                        kubelet_https=a.kubelet_https == "true", kubelet_client_certificate=a.kubelet_client_certificate,
+                        kubelet_client_key=a.kubelet_client_key, kubelet_certificate_authority=a.kubelet_certificate_authority)
         return await srv.start(a.bind_address, a.port)
     _run_forever(mk)
 
@@ -233,6 +239,15 @@ def kubelet(argv):
     ap.add_argument("--cpu-manager-policy", default="none", choices=("none", "static"))
     ap.add_argument("--cpu-manager-reconcile-period", type=float, default=10.0, help="seconds")
     ap.add_argument("--config", default=None, help="KubeletConfiguration file (KubeletConfigFile gate)")
+    ap.add_argument("--tls-cert-file", default=None)
+    ap.add_argument("--tls-private-key-file", default=None)
+    ap.add_argument("--client-ca-file", default=None)
+    ap.add_argument("--anonymous-auth", default="true", choices=("true", "false"))
+    ap.add_argument("--authentication-token-webhook", action="store_true")
+    ap.add_argument("--authorization-mode", default="AlwaysAllow", choices=("AlwaysAllow", "Webhook"))
+    ap.add_argument("--cert-dir", default=None)
+    ap.add_argument("--rotate-certificates", action="store_true")
+    ap.add_argument("--rotate-server-certificates", action="store_true")
     ap.add_argument("--dynamic-config-dir", default=None, help="checkpoints of Node.spec.configSource (DynamicKubeletConfig gate)")
     ap.add_argument("--image-gc-high-threshold", type=int, default=85)
     ap.add_argument("--image-gc-low-threshold", type=int, default=80)
@@ -272,7 +287,12 @@ def kubelet(argv):
                         cpu_manager_policy=a.cpu_manager_policy, cpu_manager_reconcile_period=a.cpu_manager_reconcile_period,
                         image_gc_high_threshold=a.image_gc_high_threshold, image_gc_low_threshold=a.image_gc_low_threshold,
                         minimum_image_ttl_duration=a.minimum_image_ttl_duration,
-                        config_file=a.config, dynamic_config_dir=a.dynamic_config_dir)
+                        config_file=a.config, dynamic_config_dir=a.dynamic_config_dir,
+                        tls_cert_file=a.tls_cert_file, tls_private_key_file=a.tls_private_key_file,
+                        client_ca_file=a.client_ca_file, anonymous_auth=a.anonymous_auth == "true",
+                        authentication_token_webhook=a.authentication_token_webhook,
+                        authorization_mode=a.authorization_mode, cert_dir=a.cert_dir,
+                        rotate_certificates=a.rotate_certificates, rotate_server_certificates=a.rotate_server_certificates)
 
     async def mk():
         smi = None

@@ -206,14 +206,30 @@ class CSRSigningController(Controller):
         self.csr_inf = self.mgr.factory.informer("certificatesigningrequests")
         self.csr_inf.add_handler(on_add=self.enqueue, on_update=lambda o, n: self.enqueue(n))
 
-    def sign(self, pem: bytes) -> bytes:
+    KEY_USAGES = {"digital signature": "digitalSignature", "key encipherment": "keyEncipherment",
+                  "content commitment": "nonRepudiation", "data encipherment": "dataEncipherment",
+                  "key agreement": "keyAgreement", "cert sign": "keyCertSign", "crl sign": "cRLSign"}
+    EXT_USAGES = {"client auth": "clientAuth", "server auth": "serverAuth", "code signing": "codeSigning",
+                  "email protection": "emailProtection", "timestamping": "timeStamping", "ocsp signing": "OCSPSigning"}
+
+    def sign(self, pem: bytes, usages=()) -> bytes:
+        """cfssl_signer.go: the CSR's subject and SANs, the requested key usages, the signing duration."""
         with tempfile.TemporaryDirectory() as d:
             req = os.path.join(d, "req.pem")
             with open(req, "wb") as f:
                 f.write(pem)
+            ku = [self.KEY_USAGES[u] for u in usages if u in self.KEY_USAGES]
+            eku = [self.EXT_USAGES[u] for u in usages if u in self.EXT_USAGES]
+            ext = os.path.join(d, "ext.cnf")
+            with open(ext, "w") as f:
+                f.write("basicConstraints=critical,CA:FALSE\n")
+                if ku:
+                    f.write(f"keyUsage=critical,{','.join(ku)}\n")
+                if eku:
+                    f.write(f"extendedKeyUsage={','.join(eku)}\n")
             r = subprocess.run(["openssl", "x509", "-req", "-in", req, "-CA", self.cert_file, "-CAkey", self.key_file,
                                 "-CAcreateserial", "-CAserial", os.path.join(d, "ca.srl"), "-days", str(self.days),
-                                "-sha256"], capture_output=True, timeout=20)
+                                "-sha256", "-extfile", ext, "-copy_extensions", "copy"], capture_output=True, timeout=20)
             if r.returncode != 0:
                 raise RuntimeError("signing failed: " + r.stderr.decode()[-300:])
             return r.stdout
@@ -226,7 +242,8 @@ class CSRSigningController(Controller):
         if csr is None or not _condition(csr, "Approved") or (csr.get("status") or {}).get("certificate"):
             return
         pem = base64.b64decode((csr.get("spec") or {}).get("request", ""))
-        cert = await asyncio.get_running_loop().run_in_executor(None, self.sign, pem)
+        usages = (csr.get("spec") or {}).get("usages") or []
+        cert = await asyncio.get_running_loop().run_in_executor(None, self.sign, pem, usages)
         csr = dict(csr, status=dict(csr.get("status") or {}, certificate=_b64(cert)))
         await self.client.update(csr, sub="status")
 

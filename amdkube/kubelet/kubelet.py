@@ -122,6 +122,15 @@ class KubeletConfig:
     image_gc_low_threshold: int = 80                  # --image-gc-low-threshold (%)
     minimum_image_ttl_duration: float = 120.0         # --minimum-image-ttl-duration (s)
     image_gc_period: float = 300.0                    # ImageGCPeriod
+    tls_cert_file: str | None = None                  # --tls-cert-file (serve HTTPS)
+    tls_private_key_file: str | None = None           # --tls-private-key-file
+    client_ca_file: str | None = None                 # --client-ca-file (x509 client authentication)
+    anonymous_auth: bool = True                       # --anonymous-auth
+    authentication_token_webhook: bool = False        # --authentication-token-webhook (TokenReview)
+    authorization_mode: str = "AlwaysAllow"           # --authorization-mode (AlwaysAllow | Webhook)
+    cert_dir: str | None = None                       # --cert-dir (rotated certificates)
+    rotate_certificates: bool = False                 # --rotate-certificates (client certificate rotation)
+    rotate_server_certificates: bool = False          # RotateKubeletServerCertificate: serving cert via CSR
     config_file: str | None = None                    # --config (KubeletConfiguration file)
     dynamic_config_dir: str | None = None             # --dynamic-config-dir
 
@@ -200,6 +209,25 @@ class Kubelet:
                                       self._kube_reserved.get("cpu", 0) + self._system_reserved.get("cpu", 0),
                                       os.path.join(config.root_dir, "cpu_manager_state"))
         self.runtime.cpu_manager = self.cpu_manager
+        from .auth import KubeletAuth
+        self.auth = KubeletAuth(self.node_name, client, config.anonymous_auth, config.authentication_token_webhook,
+                                config.authorization_mode)
+        self.cert_managers = []
+        cert_dir = config.cert_dir or os.path.join(config.root_dir, "pki")
+        if config.rotate_certificates and self.gates("RotateKubeletClientCertificate"):
+            from .certificate import CertManager
+            cmc = CertManager(client, cert_dir, self.node_name, "client")
+            cmc.listeners.append(lambda p: client.set_client_cert(p, p))
+            if cmc.current():
+                client.set_client_cert(cmc.current_path, cmc.current_path)
+            self.cert_managers.append(cmc)
+        self.server_cert_manager = None
+        if config.rotate_server_certificates and self.gates("RotateKubeletServerCertificate"):
+            from .certificate import CertManager
+            self.server_cert_manager = CertManager(client, cert_dir, self.node_name, "server",
+                                                   addresses=[config.node_ip, self.node_name])
+            self.server_cert_manager.listeners.append(lambda p: self.server and self.server.reload_cert(p))
+            self.cert_managers.append(self.server_cert_manager)
         from .images import ImageGCManager
         self.image_gc = ImageGCManager(self.cri, config.image_gc_high_threshold, config.image_gc_low_threshold,
                                        config.minimum_image_ttl_duration, recorder=self.recorder,
@@ -268,8 +296,16 @@ class Kubelet:
         self.status.start()
         if hasattr(self.dm, "store"):
             self.dm.store.listeners.append(lambda rname: self._node_dirty.set())
+        scm = self.server_cert_manager
+        if scm is not None and scm.current() is None:
+            try:   # the first serving certificate before the listener starts (needs an approved CSR)
+                await asyncio.wait_for(scm.rotate(), 30)
+            except Exception as e:
+                log.warning("no kubelet serving certificate yet (%r); serving without TLS until one is issued", e)
         from .server import KubeletServer
         self.server = await KubeletServer(self).start(self.cfg.address, self.cfg.port)
+        for cmgr in self.cert_managers:
+            self._tasks.append(asyncio.create_task(cmgr.run(), name=f"cert-rotation-{cmgr.kind}"))
         self._tasks += [asyncio.create_task(self._relist_loop(), name="pleg-relist"),
                         asyncio.create_task(self._prober_loop(), name="prober"),
                         asyncio.create_task(self._housekeeping(), name="housekeeping"),
@@ -931,6 +967,13 @@ class Kubelet:
     def _pleg_event(self, uid: str):
         self._rt_gen[uid] = self._rt_gen.get(uid, 0) + 1
         self.dispatch(uid)
+
+    def serving_cert(self) -> tuple[str | None, str | None]:
+        """The kubelet's HTTPS identity: a rotated server certificate, else --tls-cert-file."""
+        scm = self.server_cert_manager
+        if scm is not None and scm.current():
+            return scm.current_path, scm.current_path
+        return self.cfg.tls_cert_file, self.cfg.tls_private_key_file
 
     def _gpu_numa(self, pod: dict, container: dict) -> set[int]:
         """NUMA nodes of the GPUs assigned to one container (the AMD plugin's amd.com/numa-node

@@ -24,7 +24,8 @@ from .kuberuntime import L_POD_UID
 class KubeletServer:
     def __init__(self, kubelet):
         self.k = kubelet
-        app = self.app = web.Application()
+        mws = [kubelet.auth.middleware()] if getattr(kubelet, "auth", None) is not None else []
+        app = self.app = web.Application(middlewares=mws)
         app.router.add_get("/healthz", self.healthz)
         app.router.add_get("/healthz/syncloop", self.healthz)
         app.router.add_get("/pods", self.pods)
@@ -45,10 +46,32 @@ class KubeletServer:
         self.runner = None
         self.port = None
 
+    def _ssl(self):
+        """HTTPS when a serving certificate is configured (--tls-cert-file/--tls-private-key-file
+        or the rotated kubelet-server-current.pem); client certificates are requested and
+        verified against --client-ca-file. A rotation reloads the chain for new handshakes."""
+        cert, key = self.k.serving_cert()
+        if not cert:
+            return None
+        import ssl
+        ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+        ctx.load_cert_chain(cert, key)
+        if self.k.cfg.client_ca_file:
+            ctx.load_verify_locations(self.k.cfg.client_ca_file)
+            ctx.verify_mode = ssl.CERT_OPTIONAL
+        self.ssl = ctx
+        return ctx
+
+    def reload_cert(self, _path=None):
+        cert, key = self.k.serving_cert()
+        if self.ssl is not None and cert:
+            self.ssl.load_cert_chain(cert, key)
+
     async def start(self, host, port):
         self.runner = web.AppRunner(self.app, access_log=None)
         await self.runner.setup()
-        site = web.TCPSite(self.runner, host, port, reuse_address=True)
+        self.ssl = None
+        site = web.TCPSite(self.runner, host, port, reuse_address=True, ssl_context=self._ssl())
         await site.start()
         self.port = site._server.sockets[0].getsockname()[1]
         return self
