@@ -543,9 +543,12 @@ async def cmd_create_generator(c, a) -> bool:
         obj = {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": rest[0]}}
     elif kind in ("configmap", "cm"):
         obj = {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": rest[0]}, "data": lit()}
+    elif (kind == "secret" and rest and rest[0] in ("docker-registry", "tls")) or kind in ("service", "svc", "poddisruptionbudget", "pdb"):
+        from .more import create_more
+        obj = await create_more(c, a, kind, rest)
     elif kind == "secret":
         if rest[0] != "generic":
-            raise SystemExit("error: only `create secret generic` is supported")
+            raise SystemExit("error: create secret generic|docker-registry|tls NAME")
         obj = {"apiVersion": "v1", "kind": "Secret", "metadata": {"name": rest[1]}, "type": "Opaque",
                "data": {k: base64.b64encode(v.encode()).decode() for k, v in lit().items()}}
     elif kind in ("serviceaccount", "sa"):

@@ -404,6 +404,9 @@ async def cmd_api_resources(c, a):
 
 
 async def cmd_cluster_info(c, a):
+    if a.args and a.args[0] == "dump":
+        from .more import cmd_cluster_info_dump
+        return await cmd_cluster_info_dump(c, a)
     print(f"Kubernetes master is running at {c.server}")
 
 
@@ -432,7 +435,11 @@ COMMANDS = {"get": cmd_get, "describe": cmd_describe, "create": cmd_create, "app
             "top": cmd_top, "version": cmd_version, "api-resources": cmd_api_resources, "cluster-info": cmd_cluster_info,
             "wait": cmd_wait, "attach": cmd_attach}
 from .extra import COMMANDS as _EXTRA, add_arguments as _extra_args  # noqa: E402
+from . import more as _more  # noqa: E402
 COMMANDS.update(_EXTRA)
+COMMANDS.update(_more.COMMANDS)
+COMMANDS["apply"] = _more.cmd_apply       # three-way merge, --prune, *-last-applied
+COMMANDS["set"] = _more.cmd_set           # env/image/resources/selector/serviceaccount/subject
 
 
 _RESOURCE_CMDS = {"get", "describe", "delete", "label", "annotate", "scale", "patch", "wait", "edit", "explain", "expose",
@@ -450,6 +457,7 @@ def parser():
     for name in list(COMMANDS) + ["config"]:
         sp = sub.add_parser(name)
         _extra_args(sp)
+        _more.add_arguments(sp)
         sp.add_argument("args", nargs="*")
         sp.add_argument("-n", "--namespace", default=argparse.SUPPRESS)
         sp.add_argument("-o", "--output", default=None)

@@ -1,0 +1,146 @@
+"""kubectl: three-way apply (+ prune, *-last-applied), set env/resources/selector/
+serviceaccount/subject, create secret docker-registry|tls / service * / pdb, rolling-update,
+convert, api-versions, completion, plugin, cluster-info dump (pkg/kubectl/cmd/*_test.go)."""
+import asyncio
+import base64
+import io
+import json
+import os
+import contextlib
+
+import yaml
+
+from amdkube.api import meta as m
+from amdkube.kubectl.more import three_way, _SAME
+from amdkube.localcluster import LocalCluster
+from tests.conftest import run
+from tests.test_rollout import kubectl
+
+
+def test_three_way_patch():
+    orig = {"metadata": {"labels": {"a": "1", "b": "2"}}, "spec": {"containers": [{"name": "x", "image": "i1"},
+                                                                                 {"name": "y", "image": "i2"}]}}
+    cur = {"metadata": {"labels": {"a": "1", "b": "2", "c": "live"}}, "spec": {"containers": [
+        {"name": "x", "image": "i1", "imagePullPolicy": "Always"}, {"name": "y", "image": "i2"}]}}
+    mod = {"metadata": {"labels": {"a": "1"}}, "spec": {"containers": [{"name": "x", "image": "i9"}]}}
+    p = three_way(orig, mod, cur)
+    assert p == {"metadata": {"labels": {"b": None}},
+                 "spec": {"containers": [{"name": "x", "image": "i9"}, {"name": "y", "$patch": "delete"}]}}
+    assert three_way(orig, orig, orig) is _SAME
+
+
+def _write(tmp_path, name, docs):
+    p = tmp_path / name
+    p.write_text(yaml.safe_dump_all(docs))
+    return str(p)
+
+
+def test_kubectl_apply_set_create_convert_and_friends(tmp_path, capsys):
+    async def go():
+        async with LocalCluster(gpus="none", with_kubelet=False, with_controllers=False) as lc:
+            c = lc.client
+            cm = {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "app", "namespace": "default", "labels": {"tier": "x"}},
+                  "data": {"a": "1", "b": "2"}}
+            extra = {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "old", "namespace": "default", "labels": {"tier": "x"}},
+                     "data": {"z": "1"}}
+            f1 = _write(tmp_path, "v1.yaml", [cm, extra])
+            await kubectl(c, "apply", "-f", f1)
+            await c.patch("configmaps", "app", {"data": {"live": "kept"}}, "default")     # someone else's field
+            cm2 = json.loads(json.dumps(cm))
+            del cm2["data"]["b"]
+            cm2["data"]["a"] = "9"
+            f2 = _write(tmp_path, "v2.yaml", [cm2])
+            await kubectl(c, "apply", "-f", f2, "--prune", "-l", "tier=x")
+            got = await c.get("configmaps", "app", "default")
+            assert got["data"] == {"a": "9", "live": "kept"}                           # b deleted, live kept
+            assert await c.get_or_none("configmaps", "old", "default") is None           # pruned
+            capsys.readouterr()
+            await kubectl(c, "apply", "view-last-applied", "configmap/app")
+            assert yaml.safe_load(capsys.readouterr().out)["data"] == {"a": "9"}
+            # set *
+            dep = {"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": "web", "namespace": "default"},
+                   "spec": {"replicas": 1, "selector": {"matchLabels": {"app": "web"}}, "template": {
+                       "metadata": {"labels": {"app": "web"}}, "spec": {"containers": [{"name": "c", "image": "busybox"}]}}}}
+            await c.create(dep)
+            await kubectl(c, "set", "env", "deployment/web", "FOO=bar", "X=1")
+            await kubectl(c, "set", "env", "deployment/web", "X-")
+            await kubectl(c, "set", "resources", "deployment/web", "--limits", "cpu=200m,memory=64Mi")
+            await kubectl(c, "set", "serviceaccount", "deployment/web", "builder")
+            d = await c.get("deployments.apps", "web", "default")
+            ct = d["spec"]["template"]["spec"]["containers"][0]
+            assert ct["env"] == [{"name": "FOO", "value": "bar"}] and ct["resources"]["limits"]["cpu"] == "200m"
+            assert d["spec"]["template"]["spec"]["serviceAccountName"] == "builder"
+            await kubectl(c, "create", "rolebinding", "rb", "--clusterrole", "view", "--user", "alice")
+            await kubectl(c, "set", "subject", "rolebinding/rb", "--group", "devs", "--serviceaccount", "default:builder")
+            rb = await c.get("rolebindings.rbac.authorization.k8s.io", "rb", "default")
+            assert [s["name"] for s in rb["subjects"]] == ["alice", "devs", "builder"]
+            # create generators
+            await kubectl(c, "create", "secret", "docker-registry", "regcred", "--docker-username", "u",
+                          "--docker-password", "p", "--docker-server", "r.example.com")
+            sec = await c.get("secrets", "regcred", "default")
+            cfg = json.loads(base64.b64decode(sec["data"][".dockerconfigjson"]))
+            assert sec["type"] == "kubernetes.io/dockerconfigjson" and cfg["auths"]["r.example.com"]["username"] == "u"
+            (tmp_path / "t.crt").write_text("CERT")
+            (tmp_path / "t.key").write_text("KEY")
+            await kubectl(c, "create", "secret", "tls", "tls1", "--cert", str(tmp_path / "t.crt"), "--key", str(tmp_path / "t.key"))
+            assert (await c.get("secrets", "tls1", "default"))["type"] == "kubernetes.io/tls"
+            await kubectl(c, "create", "service", "nodeport", "np", "--tcp", "80:8080")
+            svc = await c.get("services", "np", "default")
+            assert svc["spec"]["type"] == "NodePort" and svc["spec"]["ports"][0]["targetPort"] == 8080
+            await kubectl(c, "create", "service", "externalname", "ext", "--external-name", "db.example.com")
+            assert (await c.get("services", "ext", "default"))["spec"]["externalName"] == "db.example.com"
+            await kubectl(c, "create", "pdb", "budget", "--selector", "app=web", "--min-available", "1")
+            assert (await c.get("poddisruptionbudgets.policy", "budget", "default"))["spec"]["minAvailable"] == 1
+            # convert, api-versions, completion
+            f3 = _write(tmp_path, "dep.yaml", [dict(dep, apiVersion="extensions/v1beta1")])
+            capsys.readouterr()
+            await kubectl(c, "convert", "-f", f3, "--output-version", "apps/v1beta2")
+            assert yaml.safe_load(capsys.readouterr().out)["apiVersion"] == "apps/v1beta2"
+            await kubectl(c, "api-versions")
+            out = capsys.readouterr().out.split()
+            assert "v1" in out and "extensions/v1beta1" in out and "apps/v1beta2" in out
+            await kubectl(c, "completion", "bash")
+            assert "complete -F" in capsys.readouterr().out
+            # cluster-info dump
+            await kubectl(c, "cluster-info", "dump", "--output-directory", str(tmp_path / "dump"))
+            assert os.path.exists(tmp_path / "dump" / "default" / "services.json")
+    run(go(), 60)
+
+
+def test_kubectl_plugin(tmp_path, capsys, monkeypatch):
+    pd = tmp_path / "plugins" / "hello"
+    pd.mkdir(parents=True)
+    (pd / "plugin.yaml").write_text(yaml.safe_dump({"name": "hello", "shortDesc": "says hello",
+                                                    "command": "echo hello-$KUBECTL_PLUGINS_CURRENT_NAMESPACE > out.txt"}))
+    monkeypatch.setenv("KUBECTL_PLUGINS_PATH", str(tmp_path / "plugins"))
+
+    async def go():
+        async with LocalCluster(gpus="none", with_kubelet=False, with_controllers=False) as lc:
+            await kubectl(lc.client, "plugin")
+            assert "says hello" in capsys.readouterr().out
+            await kubectl(lc.client, "plugin", "hello", "-n", "prod")
+            assert (pd / "out.txt").read_text().strip() == "hello-prod"
+    run(go(), 30)
+
+
+def test_kubectl_rolling_update():
+    async def go():
+        async with LocalCluster(gpus="none", relist_period=0.2) as lc:
+            c = lc.client
+            rc = {"apiVersion": "v1", "kind": "ReplicationController", "metadata": {"name": "frontend", "namespace": "default"},
+                  "spec": {"replicas": 2, "selector": {"app": "fe"}, "template": {"metadata": {"labels": {"app": "fe"}}, "spec": {
+                      "containers": [{"name": "c", "image": "busybox", "command": ["sleep", "60"]}]}}}}
+            await c.create(rc)
+            for _ in range(100):
+                if ((await c.get("replicationcontrollers", "frontend", "default")).get("status") or {}).get("readyReplicas") == 2:
+                    break
+                await asyncio.sleep(0.1)
+            await kubectl(c, "rolling-update", "frontend", "--image", "python:3", "--timeout", "30")
+            for _ in range(100):   # the renamed-away controller goes once the GC released its orphan finalizer
+                rcs, _ = await c.list("replicationcontrollers", "default")
+                if [m.name_of(x) for x in rcs] == ["frontend"]:
+                    break
+                await asyncio.sleep(0.1)
+            assert [m.name_of(x) for x in rcs] == ["frontend"]
+            assert rcs[0]["spec"]["template"]["spec"]["containers"][0]["image"] == "python:3"
+    run(go(), 90)
