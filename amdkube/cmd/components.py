@@ -424,7 +424,8 @@ def proxy(argv):
     ap.add_argument("--master", "--server", dest="server", default="http://127.0.0.1:8080")
     ap.add_argument("--kubeconfig", default=None, help="kubeconfig with the server, CA and credentials")
     ap.add_argument("--token", default=None, help="bearer token for the apiserver")
-    ap.add_argument("--proxy-mode", default="userspace", choices=("userspace", "iptables"))
+    ap.add_argument("--proxy-mode", default="userspace", choices=("userspace", "iptables", "ipvs"))
+    ap.add_argument("--ipvs-scheduler", default="rr")
     ap.add_argument("--bind-address", default="0.0.0.0", help="node address NodePorts listen on")
     ap.add_argument("--cluster-cidr", default="")
     ap.add_argument("--iptables-sync-period", type=float, default=30.0)
@@ -439,7 +440,8 @@ def proxy(argv):
 
     async def mk():
         return await ProxyServer(_client(a), a.proxy_mode, a.bind_address, a.cluster_cidr, a.iptables_sync_period,
-                                 a.iptables_min_sync_period, a.healthz_port, a.iptables_dump_file).start()
+                                 a.iptables_min_sync_period, a.healthz_port, a.iptables_dump_file,
+                                 ipvs_scheduler=a.ipvs_scheduler).start()
     _run_forever(mk)
 
 

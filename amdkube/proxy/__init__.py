@@ -28,14 +28,18 @@ log = logging.getLogger("amdkube.proxy")
 class ProxyServer:
     def __init__(self, client: Client, mode: str = "userspace", node_ip: str = "0.0.0.0", cluster_cidr: str = "",
                  sync_period: float = 30.0, min_sync_period: float = 0.0, healthz_port: int | None = None,
-                 iptables_dump: str | None = None, bind_cluster_ips: bool = True):
+                 iptables_dump: str | None = None, bind_cluster_ips: bool = True, ipvs_scheduler: str = "rr"):
         self.client = client
         if mode == "iptables":
             self.proxier = IptablesProxier(cluster_cidr, dump_path=iptables_dump)
+        elif mode == "ipvs":
+            from .ipvs import IPVSProxier
+            self.proxier = IPVSProxier(cluster_cidr, ipvs_scheduler, node_ips=[node_ip] if node_ip not in ("", "0.0.0.0") else [],
+                                       dump_path=iptables_dump)
         elif mode == "userspace":
             self.proxier = UserspaceProxier(node_ip, bind_cluster_ips=bind_cluster_ips)
         else:
-            raise ValueError(f"unknown proxy mode {mode!r} (userspace|iptables)")
+            raise ValueError(f"unknown proxy mode {mode!r} (userspace|iptables|ipvs)")
         self.tracker = ChangeTracker()
         self.sync_period, self.min_sync_period = sync_period, min_sync_period
         self.healthz_port = healthz_port

@@ -280,3 +280,39 @@ async def _ready_eps(c, name):
 
 async def _gone(c, res, name):
     return await c.get_or_none(res, name, "default") is None
+
+
+def test_ipvs_proxier_state_diff_and_restore():
+    """pkg/proxy/ipvs/proxier_test.go: virtual servers per cluster/external/LB/node-port
+    address, endpoints as real servers, ClientIP persistence, minimal diffs on change."""
+    import asyncio
+    from amdkube.proxy.config import ServiceInfo, ServicePortName
+    from amdkube.proxy.ipvs import IPVSProxier, parse_save, render_iptables, render_restore
+
+    web = ServicePortName("default", "web", "http")
+    dns = ServicePortName("kube-system", "dns", "dns")
+    services = {web: ServiceInfo("10.0.0.10", 80, "TCP", node_port=30080, external_ips=["192.168.1.50"]),
+                dns: ServiceInfo("10.0.0.53", 53, "UDP", session_affinity="ClientIP", affinity_timeout=600)}
+    eps = {web: [("10.244.0.5", 8080, "n1"), ("10.244.0.6", 8080, "n1")], dns: [("10.244.0.9", 53, "n1")]}
+    px = IPVSProxier("10.244.0.0/16", node_ips=["172.16.0.2"], dry_run=True)
+
+    async def go():
+        await px.sync(services, eps)
+        first = list(px.last_commands)
+        assert "-A -t 10.0.0.10:80 -s rr" in first and "-A -t 172.16.0.2:30080 -s rr" in first
+        assert "-A -t 192.168.1.50:80 -s rr" in first and "-A -u 10.0.0.53:53 -s rr -p 600" in first
+        assert "-a -t 10.0.0.10:80 -r 10.244.0.5:8080 -m -w 1" in first
+        assert px.addrs == {"10.0.0.10", "192.168.1.50", "10.0.0.53"}
+        eps[web] = [("10.244.0.6", 8080, "n1"), ("10.244.0.7", 8080, "n1")]
+        await px.sync(services, eps)
+        assert sorted(px.last_commands) == sorted([
+            "-a -t 10.0.0.10:80 -r 10.244.0.7:8080 -m -w 1", "-d -t 10.0.0.10:80 -r 10.244.0.5:8080",
+            "-a -t 192.168.1.50:80 -r 10.244.0.7:8080 -m -w 1", "-d -t 192.168.1.50:80 -r 10.244.0.5:8080",
+            "-a -t 172.16.0.2:30080 -r 10.244.0.7:8080 -m -w 1", "-d -t 172.16.0.2:30080 -r 10.244.0.5:8080"])
+        del services[dns]
+        await px.sync(services, eps)
+        assert px.last_commands == ["-D -u 10.0.0.53:53"] and "10.0.0.53" not in px.addrs
+        vs, rs = parse_save(render_restore(px.vs, px.rs))
+        assert vs == px.vs and rs == px.rs
+        assert "! -s 10.244.0.0/16" in render_iptables(services, "10.244.0.0/16")
+    asyncio.run(go())
