@@ -181,6 +181,7 @@ class Kubelet:
             self.dm = ManagerStub()
         self.recorder = EventRecorder(client, "kubelet", self.node_name)
         self.runtime = RuntimeManager(self.cri, self.dm, config.root_dir, self.recorder)
+        self.runtime.node_ip, self.runtime.cluster_domain = config.node_ip, config.cluster_domain
         import psutil as _ps
         self.runtime.memory_capacity = config.memory_capacity or _ps.virtual_memory().total
         from .dns import DNSConfigurer
@@ -239,6 +240,7 @@ class Kubelet:
         self.status = StatusManager(client, on_terminal=self._on_terminal)
         self.node: dict | None = None
         self.informer: Informer | None = None
+        self.svc_informer: Informer | None = None
         self.readiness: dict[str, dict[str, bool]] = {}
         self.liveness_failed: dict[str, set] = {}
         self._probe_state: dict[tuple, dict] = {}
@@ -337,6 +339,9 @@ class Kubelet:
                 await asyncio.sleep(delay)
                 delay = min(7.0, delay * 2)
         await self.dm.wait_initial_registration(5.0)
+        # service environment variables (kubelet.go serviceLister)
+        self.svc_informer = Informer(self.client, "services")
+        self.svc_informer.start()
         self.informer = Informer(self.client, "pods", field_selector=f"spec.nodeName={self.node_name}")
         self.informer.add_handler(on_add=self._on_pod_add, on_update=self._on_pod_update, on_delete=self._on_pod_delete)
         self.informer.start()
@@ -349,6 +354,8 @@ class Kubelet:
             t.cancel()
         if self.informer:
             await self.informer.stop()
+        if self.svc_informer is not None:
+            await self.svc_informer.stop()
         for w in self.workers.values():
             if w.task:
                 w.task.cancel()
@@ -1043,100 +1050,27 @@ class Kubelet:
 
     # ---------------------------------------------------- volumes / env context
     async def _pod_context(self, pod: dict) -> dict:
-        """Resolve volumes (emptyDir, hostPath, configMap, secret) and env per container."""
-        uid, ns = m.uid_of(pod), m.namespace_of(pod)
+        """Volumes and per-container env and mounts (podcontext.PodContext)."""
+        from .podcontext import PodContext
+        pc = PodContext(self)
+        vols = await pc.volumes(pod)
         spec = pod.get("spec") or {}
-        vols = {}
-        base = os.path.join(self.cfg.root_dir, "pods", uid, "volumes")
-        for v in spec.get("volumes") or []:
-            name = v["name"]
-            if "hostPath" in v:
-                p = v["hostPath"].get("path", "")
-                if v["hostPath"].get("type") in ("DirectoryOrCreate",):
-                    os.makedirs(p, exist_ok=True)
-                vols[name] = p
-            elif "configMap" in v or "secret" in v:
-                kind = "configmaps" if "configMap" in v else "secrets"
-                ref = v.get("configMap") or v.get("secret")
-                oname = ref.get("name") or ref.get("secretName")
-                d = os.path.join(base, f"kubernetes.io~{kind[:-1]}", name)
-                os.makedirs(d, exist_ok=True)
-                try:
-                    obj = await self.client.get(kind, oname, ns)
-                    for k, val in (obj.get("data") or {}).items():
-                        _atomic_write(os.path.join(d, k), base64.b64decode(val) if kind == "secrets" else val.encode())
-                except m.StatusError as e:
-                    if not ref.get("optional"):
-                        raise RuntimeError(f"volume {name}: {kind[:-1]} {oname} not found") from e
-                vols[name] = d
-            elif "persistentVolumeClaim" in v:
-                # volumemanager/populator: claim → bound volume → its host path (hostPath / local)
-                claim = v["persistentVolumeClaim"].get("claimName", "")
-                pvc = await self.client.get_or_none("persistentvolumeclaims", claim, ns)
-                pv_name = ((pvc or {}).get("spec") or {}).get("volumeName")
-                if not pv_name or ((pvc or {}).get("status") or {}).get("phase") != "Bound":
-                    raise RuntimeError(f"volume {name}: PersistentVolumeClaim {claim} is not bound")
-                pv = await self.client.get("persistentvolumes", pv_name)
-                ps = pv.get("spec") or {}
-                path = (ps.get("hostPath") or {}).get("path") or (ps.get("local") or {}).get("path")
-                if not path:
-                    raise RuntimeError(f"volume {name}: PersistentVolume {pv_name} has no host-local source")
-                os.makedirs(path, exist_ok=True)
-                vols[name] = path
-            elif "downwardAPI" in v:
-                d = os.path.join(base, "kubernetes.io~downward-api", name)
-                os.makedirs(d, exist_ok=True)
-                for it in (v["downwardAPI"].get("items") or []):
-                    fr = it.get("fieldRef") or {}
-                    val = await self._env_from(pod, {"fieldRef": fr}) if fr else ""
-                    _atomic_write(os.path.join(d, it["path"]), val.encode())
-                vols[name] = d
-            else:  # emptyDir (and unknown types degrade to emptyDir)
-                d = os.path.join(base, "kubernetes.io~empty-dir", name)
-                os.makedirs(d, exist_ok=True)
-                vols[name] = d
+        ns = m.namespace_of(pod)
+        services = []
+        if self.svc_informer is not None:
+            services = [s for s in self.svc_informer.list()
+                        if m.namespace_of(s) == ns or (m.namespace_of(s) == "default" and m.name_of(s) == "kubernetes")]
         env, mounts = {}, {}
         for c in (spec.get("initContainers") or []) + (spec.get("containers") or []):
-            e = {}
-            for ev in c.get("env") or []:
-                if "value" in ev:
-                    e[ev["name"]] = str(ev["value"])
-                elif "valueFrom" in ev:
-                    e[ev["name"]] = await self._env_from(pod, ev["valueFrom"])
-            for ef in c.get("envFrom") or []:
-                ref = ef.get("configMapRef") or ef.get("secretRef")
-                if ref:
-                    kind = "configmaps" if "configMapRef" in ef else "secrets"
-                    obj = await self.client.get_or_none(kind, ref["name"], ns) or {}
-                    for k, val in (obj.get("data") or {}).items():
-                        e[(ef.get("prefix") or "") + k] = base64.b64decode(val).decode() if kind == "secrets" else val
-            e.setdefault("HOSTNAME", m.name_of(pod))
-            e.setdefault("KUBERNETES_POD_NAME", m.name_of(pod))
-            e.setdefault("KUBERNETES_NAMESPACE", ns)
-            env[c["name"]] = e
+            env[c["name"]] = await pc.env(pod, c, services)
             mounts[c["name"]] = [{"container_path": vm["mountPath"], "host_path": os.path.join(vols[vm["name"]], vm.get("subPath", "")).rstrip("/"),
                                   "read_only": bool(vm.get("readOnly"))} for vm in c.get("volumeMounts") or [] if vm["name"] in vols]
         return {"env": env, "mounts": mounts}
 
     async def _env_from(self, pod, vf) -> str:
+        from .podcontext import PodContext
         if "fieldRef" in vf:
-            path = vf["fieldRef"].get("fieldPath", "")
-            md = pod.get("metadata") or {}
-            vals = {"metadata.name": md.get("name", ""), "metadata.namespace": md.get("namespace", ""),
-                    "metadata.uid": md.get("uid", ""), "spec.nodeName": self.node_name,
-                    "spec.serviceAccountName": (pod.get("spec") or {}).get("serviceAccountName", ""),
-                    "status.podIP": self.cfg.node_ip, "status.hostIP": self.cfg.node_ip}
-            if path.startswith("metadata.labels['"):
-                return (md.get("labels") or {}).get(path[len("metadata.labels['"):-2], "")
-            if path.startswith("metadata.annotations['"):
-                return (md.get("annotations") or {}).get(path[len("metadata.annotations['"):-2], "")
-            return vals.get(path, "")
-        for kind, key in (("configmaps", "configMapKeyRef"), ("secrets", "secretKeyRef")):
-            if key in vf:
-                ref = vf[key]
-                obj = await self.client.get_or_none(kind, ref["name"], m.namespace_of(pod)) or {}
-                val = (obj.get("data") or {}).get(ref["key"], "")
-                return base64.b64decode(val).decode() if kind == "secrets" and val else val
+            return PodContext(self).field(pod, vf["fieldRef"].get("fieldPath", ""))
         return ""
 
     # ================================================================ PLEG

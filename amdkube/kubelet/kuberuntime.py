@@ -33,6 +33,8 @@ log = logging.getLogger("amdkube.kuberuntime")
 L_POD_NAME, L_POD_NS, L_POD_UID = "io.kubernetes.pod.name", "io.kubernetes.pod.namespace", "io.kubernetes.pod.uid"
 L_CONTAINER = "io.kubernetes.container.name"
 A_HASH, A_RESTARTS, A_INIT = "io.kubernetes.container.hash", "io.kubernetes.container.restartCount", "io.amdkube.container.init"
+A_TERM_PATH = "io.kubernetes.container.terminationMessagePath"       # labels.go
+A_TERM_POLICY = "io.kubernetes.container.terminationMessagePolicy"
 
 BACKOFF_BASE, BACKOFF_MAX = 10.0, 300.0
 
@@ -155,6 +157,8 @@ class RuntimeManager:
         self._image_seen: dict[str, float] = {}
         self.legacy = None          # gpu_legacy.AMDGPUManager when the Accelerators gate is on
         self.cpu_manager = None     # cpumanager.CPUManager
+        self.node_ip = "127.0.0.1"
+        self.cluster_domain = ""
         self.gpu_numa = None        # (pod, container) -> NUMA nodes of its GPUs
         self.dns = None             # dns.DNSConfigurer (pod resolv.conf)
         self.memory_capacity = 1 << 40   # node memory (burstable OOM score scaling), set by the kubelet
@@ -237,14 +241,31 @@ class RuntimeManager:
             if la["devices"]:
                 opts = dict(opts, devices=list(opts["devices"]) + [d for d in la["devices"] if d not in opts["devices"]],
                             envs={**opts["envs"], **la["envs"]}, annotations={**opts["annotations"], **la["annotations"]})
-        envs = [C.KeyValue(key=k, value=v) for k, v in (ctx.get("env", {}).get(c["name"]) or {}).items()]
+        from .podcontext import POD_IP, expand, hosts_file, atomic_write
+        pod_ip = self.sandbox_ips.get(sid) or self.node_ip
+        cenv = {k: v.replace(POD_IP, pod_ip) for k, v in (ctx.get("env", {}).get(c["name"]) or {}).items()}
+        envs = [C.KeyValue(key=k, value=v) for k, v in cenv.items()]
         envs += [C.KeyValue(key=k, value=v) for k, v in opts["envs"].items()]
+        extra_mounts = []
+        spec = pod.get("spec") or {}
+        pdir = os.path.join(self.root, "pods", pod["metadata"]["uid"])
+        if not spec.get("hostNetwork"):
+            # kubelet_pods.go makeHostsMount: the kubelet-managed /etc/hosts (pod IP, hostname, hostAliases)
+            hp = os.path.join(pdir, "etc-hosts")
+            atomic_write(hp, hosts_file(pod, pod_ip, self.cluster_domain).encode(), 0o644)
+            extra_mounts.append({"container_path": "/etc/hosts", "host_path": hp, "read_only": False})
+        tm_path = c.get("terminationMessagePath") or "/dev/termination-log"
+        tm_host = os.path.join(pdir, "containers", c["name"], f"{restart_count}-termination-log")
+        os.makedirs(os.path.dirname(tm_host), exist_ok=True)
+        open(tm_host, "w").close()
+        extra_mounts.append({"container_path": tm_path, "host_path": tm_host, "read_only": False})
         mounts = [C.Mount(container_path=m["container_path"], host_path=m["host_path"], readonly=bool(m.get("read_only")))
-                  for m in (ctx.get("mounts", {}).get(c["name"]) or []) + opts["mounts"]]
+                  for m in (ctx.get("mounts", {}).get(c["name"]) or []) + opts["mounts"] + extra_mounts]
         devices = [C.Device(container_path=d["container_path"], host_path=d["host_path"], permissions=d.get("permissions", "rw"))
                    for d in opts["devices"]]
         ann = dict(opts["annotations"])
-        ann.update({A_HASH: container_hash(c), A_RESTARTS: str(restart_count), A_INIT: "true" if init else "false"})
+        ann.update({A_HASH: container_hash(c), A_RESTARTS: str(restart_count), A_INIT: "true" if init else "false",
+                    A_TERM_PATH: tm_path, A_TERM_POLICY: c.get("terminationMessagePolicy") or "File"})
         res = (c.get("resources") or {}).get("limits") or {}
         from ..api.quantity import Quantity
         from .qos import oom_score_adj
@@ -262,7 +283,8 @@ class RuntimeManager:
         md = pod["metadata"]
         cfg = C.ContainerConfig(
             metadata=C.ContainerMetadata(name=c["name"], attempt=restart_count), image=C.ImageSpec(image=c["image"]),
-            command=c.get("command") or [], args=c.get("args") or [], working_dir=c.get("workingDir") or "",
+            command=[expand(x, cenv) for x in c.get("command") or []], args=[expand(x, cenv) for x in c.get("args") or []],
+            working_dir=c.get("workingDir") or "",
             envs=envs, mounts=mounts, devices=devices,
             labels={L_POD_NAME: md["name"], L_POD_NS: md.get("namespace", ""), L_POD_UID: md["uid"], L_CONTAINER: c["name"]},
             annotations=ann, log_path=f"{c['name']}/{restart_count}.log",
@@ -273,7 +295,42 @@ class RuntimeManager:
         cid = await self.cri.create_container(sid, cfg, sandbox_cfg)
         await self.cri.start_container(cid)
         POD_TRACE(pod["metadata"]["uid"], "container_started")
+        post = ((c.get("lifecycle") or {}).get("postStart"))
+        if post:
+            # kuberuntime_container.go startContainer step 4: a failing postStart hook kills the container
+            err = await self.run_handler(pod, c, cid, post, pod_ip)
+            if err:
+                if self.recorder:
+                    self.recorder.event(pod, "Warning", "FailedPostStartHook", err)
+                await self.cri.stop_container(cid, 0)
+                raise RuntimeError(f"PostStartHookError: {err}")
         return cid
+
+    async def run_handler(self, pod, c, cid, handler: dict, pod_ip: str, timeout: int = 30) -> str:
+        """lifecycle/handlers.go HandlerRunner: exec in the container or HTTP GET; '' on success."""
+        if "exec" in handler:
+            try:
+                _out, err, code = await self.cri.exec_sync(cid, handler["exec"].get("command") or [], timeout)
+            except grpc.RpcError as e:
+                return f"Exec lifecycle hook ({handler['exec'].get('command')}) for Container {c['name']!r} failed - error: {e.details()}"
+            return "" if code == 0 else (f"Exec lifecycle hook ({handler['exec'].get('command')}) for Container {c['name']!r} "
+                                         f"failed - error: command exited with {code}, message: {err[-256:]!r}")
+        if "httpGet" in handler:
+            h = handler["httpGet"]
+            port = h.get("port")
+            if isinstance(port, str) and not port.isdigit():
+                port = next((p["containerPort"] for p in c.get("ports") or [] if p.get("name") == port), None)
+            url = f"{(h.get('scheme') or 'HTTP').lower()}://{h.get('host') or pod_ip}:{port}{h.get('path') or '/'}"
+            import aiohttp
+            try:
+                async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=timeout)) as s:
+                    async with s.get(url, headers={x["name"]: x["value"] for x in h.get("httpHeaders") or []}, ssl=False) as r:
+                        if r.status >= 400:
+                            return f"Http lifecycle hook ({url}) for Container {c['name']!r} failed - HTTP {r.status}"
+            except Exception as e:
+                return f"Http lifecycle hook ({url}) for Container {c['name']!r} failed - error: {e!r}"
+            return ""
+        return "a lifecycle handler needs exec or httpGet"
 
     # ------------------------------------------------------------------ sync
     async def sync_pod(self, pod: dict, st: PodRuntimeStatus, ctx: dict, liveness_failed: set | None = None) -> list[str]:
@@ -386,12 +443,12 @@ class RuntimeManager:
         if pod is not None:
             for sc in (pod.get("spec") or {}).get("containers") or []:
                 if sc["name"] == c.metadata.name:
-                    pre = ((sc.get("lifecycle") or {}).get("preStop") or {}).get("exec")
-                    if pre:
-                        try:
-                            await self.cri.exec_sync(c.id, pre.get("command") or [], min(grace, 30) or 1)
-                        except grpc.RpcError:
-                            pass
+                    pre = (sc.get("lifecycle") or {}).get("preStop")
+                    if pre:   # kuberuntime_container.go executePreStopHook, bounded by the grace period
+                        ip = self.sandbox_ips.get(c.pod_sandbox_id) or self.node_ip
+                        err = await self.run_handler(pod, sc, c.id, pre, ip, min(grace, 30) or 1)
+                        if err and self.recorder:
+                            self.recorder.event(pod, "Warning", "FailedPreStopHook", err)
         await self.cri.stop_container(c.id, grace)
 
     # ------------------------------------------------------------ garbage collection

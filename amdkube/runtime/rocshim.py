@@ -495,6 +495,31 @@ class RocShim:
     def _cgroup_of(self, c: Container) -> str:
         return os.path.join(self.cgroup_root, c.resources.get("cgroup_parent") or c.sandbox_id, c.id)
 
+    def _termination_message(self, c: Container) -> str:
+        """kuberuntime_container.go getTerminationMessage: the file the container wrote at its
+        terminationMessagePath (≤ 4 KiB), or — policy FallbackToLogsOnError, failed, nothing
+        written — the tail of its log (80 lines, 2 KiB)."""
+        path = c.annotations.get("io.kubernetes.container.terminationMessagePath", "")
+        host = next((mt["host_path"] for mt in c.mounts if mt["container_path"] == path), None) if path else None
+        msg = ""
+        if host:
+            try:
+                with open(host, "rb") as f:
+                    msg = f.read(4096).decode(errors="replace")
+            except OSError:
+                pass
+        if not msg and c.exit_code and c.annotations.get("io.kubernetes.container.terminationMessagePolicy") == \
+                "FallbackToLogsOnError":
+            try:
+                with open(c.log_path, "rb") as f:
+                    f.seek(0, os.SEEK_END)
+                    f.seek(max(0, f.tell() - 16384))
+                    lines = f.read().decode(errors="replace").splitlines()[-80:]
+                msg = "\n".join(lines)[-2048:]
+            except OSError:
+                pass
+        return msg
+
     def _oom_killed(self, c: Container) -> bool:
         """cgroup v2 memory.events `oom_kill` of the container's leaf (namespaces isolation):
         the container exit was the kernel OOM killer's doing (docker's State.OOMKilled)."""
@@ -559,6 +584,7 @@ class RocShim:
             c.exit_code, c.reason = rc, "OOMKilled"
         else:
             c.exit_code, c.reason = rc, ("Completed" if rc == 0 else "Error")
+        c.message = self._termination_message(c)
         self._ckpt("containers", c)
         self._emit(c, C.CONTAINER_STOPPED_EVENT)
 
