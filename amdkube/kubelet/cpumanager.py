@@ -101,6 +101,10 @@ class CPUTopology:
                 online = parse_cpuset(f.read().strip())
         except OSError:
             online = set(range(os.cpu_count() or 1))
+        try:   # only the CPUs this kubelet may hand out (its cgroup cpuset / affinity)
+            online &= os.sched_getaffinity(0)
+        except (AttributeError, OSError):
+            pass
         out = []
         for c in sorted(online):
             t = os.path.join(base, f"cpu{c}", "topology")
@@ -175,7 +179,7 @@ class CPUManager:
         if policy not in ("none", "static"):
             raise ValueError(f"unknown cpu manager policy {policy!r}")
         self.policy = policy
-        self.topo = topology or CPUTopology.discover()
+        self.topo = topology or (CPUTopology.discover() if policy == "static" else CPUTopology([]))
         self.state_file = state_file
         self.all = set(self.topo.cpus)
         self.assignments: dict[str, set[int]] = {}

@@ -106,6 +106,38 @@ def test_03_plugin_hbm_health_probe_marks_healthy():
     run(go(), 300)
 
 
+def test_05_cpu_manager_exclusive_cpus_near_the_gpu():
+    """Static CPU manager on the real node: a Guaranteed GPU pod gets exclusive CPUs, taken
+    from its GPU's NUMA node (amd.com/numa-node from amd-smi) when that node has room, and the
+    running workload is pinned to exactly them."""
+    from amdkube.kubelet.cpumanager import CPUTopology, parse_cpuset
+    topo = CPUTopology.discover()
+    if topo.num_cpus < 4:
+        pytest.skip("needs ≥ 4 allowed CPUs")
+
+    async def go():
+        async with LocalCluster(gpus="amdsmi", n_gpus=1, relist_period=0.5, with_controllers=False,
+                                kubelet_kw={"cpu_manager_policy": "static", "kube_reserved": "cpu=1"}) as lc:
+            node = await lc.wait_gpus(1, 60)
+            [dev] = node["status"]["extendedResources"]["amd.com/gpu"]["resources"].values()
+            numa = int(dev["attributes"].get("amd.com/numa-node", "-1"))
+            pod = vadd_pod("pinned", args=("--print-uuid",))
+            ct = pod["spec"]["containers"][0]
+            ct["image"], ct["command"] = "busybox", ["sh", "-c", f"grep Cpus_allowed_list /proc/self/status && exec {BIN}/rocm-vector-add"]
+            ct["args"] = []
+            ct["resources"] = {"limits": {"amd.com/gpu": "1", "cpu": "2", "memory": "512Mi"}}
+            await lc.client.create(pod)
+            p = await wait_pod(lc.client, "default", "pinned", ("Succeeded", "Failed"), 120)
+            logs = await lc.client.logs("default", "pinned")
+            assert p["status"]["phase"] == "Succeeded" and "Test PASSED" in logs, (p["status"], logs)
+            allowed = parse_cpuset(logs.split("Cpus_allowed_list:")[1].split()[0])
+            assert len(allowed) == 2 and not allowed & lc.kubelet.cpu_manager.reserved, allowed
+            local = {cpu for cpu, info in topo.cpus.items() if info.numa == numa} - lc.kubelet.cpu_manager.reserved
+            if numa >= 0 and len(local) >= 2:
+                assert allowed <= local, (allowed, numa)
+    run(go(), 300)
+
+
 def test_04_probe_binaries():
     r = subprocess.run([os.path.join(BIN, "hbm-probe"), "--mib", "1024", "--iters", "3"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
