@@ -124,6 +124,9 @@ class Aggregator:
 
     def _ssl(self, spec: dict):
         ctx = ssl.create_default_context()
+        pc = getattr(self.server, "proxy_client_cert", None)
+        if pc:     # the front-proxy client certificate the extension server's requestheader CA trusts
+            ctx.load_cert_chain(pc[0], pc[1])
         if spec.get("insecureSkipTLSVerify"):
             ctx.check_hostname, ctx.verify_mode = False, ssl.CERT_NONE
         elif spec.get("caBundle"):

@@ -145,13 +145,50 @@ class Authenticator:
                     groups.append(v)
         return {"name": cn, "uid": "", "groups": groups} if cn else None
 
+    requestheader: dict | None = None   # front-proxy (aggregator) authentication, see configure_requestheader
+
+    def configure_requestheader(self, ca_file: str, allowed_names=(), username_headers=("X-Remote-User",),
+                                group_headers=("X-Remote-Group",), extra_prefixes=("X-Remote-Extra-",)):
+        """authentication/request/headerrequest: a client certificate issued by
+        --requestheader-client-ca-file (and, with --requestheader-allowed-names, carrying one of
+        those CNs) may assert the user in X-Remote-User / X-Remote-Group / X-Remote-Extra-*."""
+        import ssl as _ssl
+        dec = _ssl._ssl._test_decode_cert(ca_file)
+        self.requestheader = {"issuer": dec.get("subject"), "allowed": set(allowed_names or ()),
+                              "users": list(username_headers), "groups": list(group_headers), "extra": list(extra_prefixes)}
+
+    def _from_request_headers(self, headers, peercert) -> dict | None:
+        rh = self.requestheader
+        if rh is None or not peercert or peercert.get("issuer") != rh["issuer"]:
+            return None
+        cn = (self.from_peer_cert(peercert) or {}).get("name")
+        if rh["allowed"] and cn not in rh["allowed"]:
+            return None
+        name = next((headers.get(h) for h in rh["users"] if headers.get(h)), None)
+        if not name:
+            return None
+        getall = getattr(headers, "getall", None)
+        groups = [g for h in rh["groups"] for g in ((getall(h, []) if getall else [headers.get(h)]) or []) if g]
+        extra = {}
+        for pre in rh["extra"]:
+            for k in headers.keys():
+                if k.lower().startswith(pre.lower()):
+                    extra.setdefault(k[len(pre):].lower(), []).extend(getall(k, []) if getall else [headers.get(k)])
+        return {"name": name, "uid": "", "groups": groups, "extra": extra}
+
     def authenticate(self, headers, peercert: dict | None = None) -> dict:
+        u = self._from_request_headers(headers, peercert)
+        if u is not None:
+            return self._with_authenticated(u)
         h = headers.get("Authorization", "")
         if h.startswith("Bearer "):
             u = self.authenticate_token(h[7:].strip())
             if u is None:
                 raise m.unauthorized()
             return u
+        rh = self.requestheader
+        if peercert and rh and peercert.get("issuer") == rh["issuer"] and not rh.get("client_ca_same"):
+            peercert = None   # a front-proxy certificate is no x509 identity of its own (client-ca ≠ requestheader CA)
         if peercert:
             u = self.from_peer_cert(peercert)
             if u is not None:

@@ -97,7 +97,9 @@ class APIServer:
                  client_ca_file: str | None = None, audit_log_path: str | None = None, audit_policy_file: str | None = None,
                  audit_log_maxsize: int = 0, audit_log_maxbackup: int = 0, kubelet_https: bool = False,
                  kubelet_client_certificate: str | None = None, kubelet_client_key: str | None = None,
-                 kubelet_certificate_authority: str | None = None):
+                 kubelet_certificate_authority: str | None = None, requestheader_client_ca_file: str | None = None,
+                 requestheader_allowed_names=(), proxy_client_cert_file: str | None = None,
+                 proxy_client_key_file: str | None = None):
         self.store = store or MVCCStore()
         # --kubelet-https / --kubelet-client-certificate / --kubelet-client-key /
         # --kubelet-certificate-authority: how the apiserver reaches kubelets (logs, exec, proxy)
@@ -134,6 +136,15 @@ class APIServer:
         self.tls = (tls_cert_file, tls_key_file, client_ca_file) if tls_cert_file else None
         self.authn = Authenticator(self.registry, self.tokens, service_account_key, anonymous_auth)
         self.authn.user_tokens = len(token_auth or {})
+        self.requestheader_ca = requestheader_client_ca_file
+        if requestheader_client_ca_file:
+            self.authn.configure_requestheader(requestheader_client_ca_file, requestheader_allowed_names)
+            if client_ca_file:
+                import ssl
+                self.authn.requestheader["client_ca_same"] = \
+                    ssl._ssl._test_decode_cert(client_ca_file).get("subject") == self.authn.requestheader["issuer"]
+        # the aggregator's identity towards extension API servers (--proxy-client-cert-file)
+        self.proxy_client_cert = (proxy_client_cert_file, proxy_client_key_file) if proxy_client_cert_file else None
         self.authz = UnionAuthorizer(authorization_mode, self.registry)
         self.registry.authorizer = self.authz
         from .aggregator import Aggregator
@@ -184,6 +195,9 @@ class APIServer:
             ctx.load_cert_chain(cert, key)
             if ca:   # --client-ca-file: request (not require) client certificates
                 ctx.load_verify_locations(ca)
+                ctx.verify_mode = ssl.CERT_OPTIONAL
+            if self.requestheader_ca:   # front-proxy certificates are checked against their own CA
+                ctx.load_verify_locations(self.requestheader_ca)
                 ctx.verify_mode = ssl.CERT_OPTIONAL
         self._site = web.TCPSite(self._runner, host, port, backlog=1024, reuse_address=True, ssl_context=ctx)
         await self._site.start()

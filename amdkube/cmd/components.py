@@ -90,6 +90,11 @@ def apiserver(argv):
     ap.add_argument("--audit-policy-file", default=None, help="audit.k8s.io Policy (default: everything at Metadata)")
     ap.add_argument("--audit-log-maxsize", type=int, default=0, help="rotate the audit log at this many MB")
     ap.add_argument("--audit-log-maxbackup", type=int, default=0, help="rotated audit logs to keep")
+    ap.add_argument("--requestheader-client-ca-file", default=None,
+                    help="CA of front-proxy client certs allowed to assert X-Remote-User/Group")
+    ap.add_argument("--requestheader-allowed-names", default="", help="front-proxy cert CNs accepted (empty: any)")
+    ap.add_argument("--proxy-client-cert-file", default=None, help="aggregator's client cert towards extension apiservers")
+    ap.add_argument("--proxy-client-key-file", default=None)
     a = ap.parse_args(argv)
     klog.setup(a.v, "apiserver")
     from ..apiserver import APIServer
@@ -115,7 +120,10 @@ def apiserver(argv):
                         audit_log_path=a.audit_log_path, audit_policy_file=a.audit_policy_file,
                         audit_log_maxsize=a.audit_log_maxsize, audit_log_maxbackup=a.audit_log_maxbackup,
                         kubelet_https=a.kubelet_https == "true", kubelet_client_certificate=a.kubelet_client_certificate,
-                        kubelet_client_key=a.kubelet_client_key, kubelet_certificate_authority=a.kubelet_certificate_authority)
+                        kubelet_client_key=a.kubelet_client_key, kubelet_certificate_authority=a.kubelet_certificate_authority,
+                        requestheader_client_ca_file=a.requestheader_client_ca_file,
+                        requestheader_allowed_names=[x for x in a.requestheader_allowed_names.split(",") if x],
+                        proxy_client_cert_file=a.proxy_client_cert_file, proxy_client_key_file=a.proxy_client_key_file)
         return await srv.start(a.bind_address, a.port)
     _run_forever(mk)
 
@@ -390,6 +398,41 @@ def exporter(argv):
     _run_forever(mk)
 
 
+def metrics_server(argv):
+    """Resource metrics API (metrics.k8s.io) behind the aggregator: register it with an
+    APIService pointing at a Service whose endpoints reach --secure-port."""
+    ap = argparse.ArgumentParser("amdkube metrics-server")
+    ap.add_argument("--master", "--server", dest="server", default="http://127.0.0.1:8080")
+    ap.add_argument("--kubeconfig", default=None)
+    ap.add_argument("--token", default=None)
+    ap.add_argument("--bind-address", default="0.0.0.0")
+    ap.add_argument("--secure-port", type=int, default=443)
+    ap.add_argument("--tls-cert-file", default=None)
+    ap.add_argument("--tls-private-key-file", default=None)
+    ap.add_argument("--requestheader-client-ca-file", default=None)
+    ap.add_argument("--requestheader-allowed-names", default="")
+    ap.add_argument("--metric-resolution", type=float, default=60.0, help="seconds between kubelet scrapes")
+    ap.add_argument("--kubelet-https", default="false", choices=("true", "false"))
+    ap.add_argument("--kubelet-insecure-tls", action="store_true")
+    ap.add_argument("--authorization-always-allow", action="store_true", help="skip authn/authz (testing only)")
+    ap.add_argument("-v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "metrics-server")
+    from ..metrics import MetricsServer
+
+    async def mk():
+        kssl = None
+        if a.kubelet_https == "true" and a.kubelet_insecure_tls:
+            import ssl
+            kssl = ssl.create_default_context()
+            kssl.check_hostname, kssl.verify_mode = False, ssl.CERT_NONE
+        return await MetricsServer(_client(a), a.metric_resolution, a.requestheader_client_ca_file,
+                                   [x for x in a.requestheader_allowed_names.split(",") if x], a.tls_cert_file,
+                                   a.tls_private_key_file, "https" if a.kubelet_https == "true" else "http", kssl,
+                                   authorize=not a.authorization_always_allow).start(a.bind_address, a.secure_port)
+    _run_forever(mk)
+
+
 def hollow_node(argv):
     ap = argparse.ArgumentParser("amdkube hollow-node")
     ap.add_argument("--server", default="http://127.0.0.1:8080")
@@ -562,4 +605,5 @@ def kubeadm(argv):
 COMPONENTS = {"dns": dns, "kube-dns": dns, "kubeadm": kubeadm, "proxy": proxy, "kube-proxy": proxy, "apiserver": apiserver, "kube-apiserver": apiserver, "scheduler": scheduler, "kube-scheduler": scheduler,
               "controller-manager": controller_manager, "kube-controller-manager": controller_manager, "kubelet": kubelet,
               "rocshim": rocshim, "amd-device-plugin": device_plugin, "device-plugin": device_plugin,
-              "amdgpu-exporter": exporter, "exporter": exporter, "hollow-node": hollow_node, "local-up": local_up}
+              "amdgpu-exporter": exporter, "exporter": exporter, "hollow-node": hollow_node, "local-up": local_up,
+              "metrics-server": metrics_server}

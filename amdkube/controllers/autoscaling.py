@@ -14,8 +14,9 @@ a second metric, the mean MI355X activity (amd-smi duty cycle, exported per cont
 the kubelet's accelerator stats) of the pods' assigned GPUs. The larger of the two
 proposals wins (the multi-metric rule of autoscaling/v2).
 
-Metrics come from the kubelets' /stats/summary (the reference reads them via Heapster);
-CPU usage is the rate between two successive cumulative samples.
+Metrics come from the resource metrics API (metrics.k8s.io, the metrics-server) when it is
+registered, else straight from the kubelets' /stats/summary, where CPU usage is the rate between
+two successive cumulative samples.
 """
 from __future__ import annotations
 
@@ -93,6 +94,45 @@ class KubeletSummaryMetrics:
             await self._http.close()
 
 
+class ResourceMetricsAPI:
+    """metrics/rest_metrics_client.go resourceMetricsClient: pod CPU from the resource metrics API
+    (metrics.k8s.io/v1beta1 PodMetrics, served by the metrics-server behind the aggregator) — the
+    reference 1.9 default (--horizontal-pod-autoscaler-use-rest-clients). GPU activity rides in
+    the metrics-server's amd.com/gpu-duty-cycle annotation. When the group is not served (no
+    metrics-server registered) the kubelet-summary source answers instead."""
+
+    def __init__(self, client, fallback=None):
+        self.client = client
+        self.fallback = fallback or KubeletSummaryMetrics(client)
+
+    async def _served(self) -> bool:
+        try:
+            groups = (await self.client.request("GET", "/apis")).get("groups") or []
+        except Exception:
+            return False
+        return any(g.get("name") == "metrics.k8s.io" for g in groups)
+
+    async def pod_metrics(self, ns: str) -> dict[str, dict]:
+        if not await self._served():
+            return await self.fallback.pod_metrics(ns)
+        try:
+            items = (await self.client.request("GET", f"/apis/metrics.k8s.io/v1beta1/namespaces/{ns}/pods")).get("items") or []
+        except Exception:
+            return await self.fallback.pod_metrics(ns)
+        out = {}
+        for pm in items:
+            ent = {"cpu_milli": float(sum(Quantity(ct["usage"]["cpu"]).as_fraction() * 1000
+                                          for ct in pm.get("containers") or []))}
+            duty = ((pm.get("metadata") or {}).get("annotations") or {}).get("amd.com/gpu-duty-cycle")
+            if duty is not None:
+                ent["gpu_util"] = float(duty)
+            out[m.name_of(pm)] = ent
+        return out
+
+    async def close(self):
+        await self.fallback.close()
+
+
 def _cpu_request_milli(pod) -> int:
     total = 0
     for c in (pod.get("spec") or {}).get("containers") or []:
@@ -142,7 +182,7 @@ class HorizontalPodAutoscalerController(Controller):
     def __init__(self, mgr, metrics=None, sync_period: float = 30.0, upscale_delay: float = 180.0,
                  downscale_delay: float = 300.0, clock=time.time):
         super().__init__(mgr)
-        self.metrics = metrics or KubeletSummaryMetrics(mgr.client)
+        self.metrics = metrics or ResourceMetricsAPI(mgr.client)
         self.sync_period, self.upscale_delay, self.downscale_delay = sync_period, upscale_delay, downscale_delay
         self.clock = clock
         self._poll = None

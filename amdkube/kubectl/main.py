@@ -354,36 +354,8 @@ async def cmd_run(c, a):
 
 
 async def cmd_top(c, a):
-    what = a.args[0] if a.args else "node"
-    nodes, _ = await c.list("nodes")
-    import aiohttp
-    rows = []
-    async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=10)) as s:
-        for n in nodes:
-            st = n.get("status") or {}
-            port = ((st.get("daemonEndpoints") or {}).get("kubeletEndpoint") or {}).get("Port")
-            addr = next((x["address"] for x in st.get("addresses") or [] if x.get("type") == "InternalIP"), "127.0.0.1")
-            if not port:
-                continue
-            try:
-                async with s.get(f"http://{addr}:{port}/stats/summary") as r:
-                    summ = await r.json()
-            except Exception:
-                continue
-            if what in ("node", "nodes", "no"):
-                mem = summ["node"]["memory"]
-                rows.append([m.name_of(n), f"{mem['usageBytes'] >> 20}Mi", str(len(summ["node"].get("accelerators") or []))])
-            else:  # gpu
-                owner = {}
-                for p in summ.get("pods") or []:
-                    for ct in p.get("containers") or []:
-                        for acc in ct.get("accelerators") or []:
-                            owner[acc["id"]] = f"{p['podRef']['namespace']}/{p['podRef']['name']}"
-                for acc in summ["node"].get("accelerators") or []:
-                    rows.append([m.name_of(n), acc["id"], acc["model"], f"{acc['dutyCycle']}%",
-                                 f"{acc['memoryUsed'] >> 20}Mi/{acc['memoryTotal'] >> 20}Mi", owner.get(acc["id"], "-")])
-    head = ["NAME", "MEMORY", "GPUS"] if what in ("node", "nodes", "no") else ["NODE", "GPU", "MODEL", "UTIL", "VRAM", "POD"]
-    print(printers.table([head] + rows))
+    from .top import cmd_top as top
+    await top(c, a)
 
 
 async def cmd_version(c, a):

@@ -518,6 +518,7 @@ def add_arguments(sp):
     sp.add_argument("--max-unavailable", default=None)
     sp.add_argument("--output-version", default=None)
     sp.add_argument("--output-directory", default=None)
+    sp.add_argument("--containers", action="store_true")
 
 
 COMMANDS = {"rolling-update": cmd_rolling_update, "convert": cmd_convert, "api-versions": cmd_api_versions,

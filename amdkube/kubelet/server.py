@@ -45,6 +45,7 @@ class KubeletServer:
         profiling.add_routes(app)
         self.runner = None
         self.port = None
+        self._cpu_prev: dict[str, tuple[float, int]] = {}
 
     def _ssl(self):
         """HTTPS when a serving certificate is configured (--tls-cert-file/--tls-private-key-file
@@ -151,20 +152,34 @@ class KubeletServer:
             ent = pods.setdefault(uid, {"podRef": {"name": m.name_of(p), "namespace": m.namespace_of(p), "uid": uid},
                                         "startTime": (p.get("status") or {}).get("startTime"), "containers": []})
             s = stats.get(c.id)
+            used = s.cpu.usage_core_nano_seconds.value if s else 0
             cont = {"name": c.metadata.name, "startTime": now,
-                    "cpu": {"time": now, "usageCoreNanoSeconds": s.cpu.usage_core_nano_seconds.value if s else 0},
+                    "cpu": {"time": now, "usageCoreNanoSeconds": used, "usageNanoCores": self._rate(c.id, used)},
                     "memory": {"time": now, "workingSetBytes": s.memory.working_set_bytes.value if s else 0}}
             ids = dev_map.get((m.namespace_of(p), m.name_of(p), c.metadata.name))
             if ids:
                 cont["accelerators"] = accel.accelerator_stats(ids)
             ent["containers"].append(cont)
+        node_used = int((cpu.user + cpu.system) * 1e9)
+        live = {c.id for c in conts} | {"__node__"}
+        for k in [k for k in self._cpu_prev if k not in live]:
+            del self._cpu_prev[k]
         return web.json_response({
             "node": {"nodeName": self.k.node_name, "startTime": m.now_rfc3339(),
-                     "cpu": {"time": now, "usageCoreNanoSeconds": int((cpu.user + cpu.system) * 1e9)},
+                     "cpu": {"time": now, "usageCoreNanoSeconds": node_used, "usageNanoCores": self._rate("__node__", node_used)},
                      "memory": {"time": now, "availableBytes": vm.available, "usageBytes": vm.total - vm.available,
                                 "workingSetBytes": vm.total - vm.available},
                      "accelerators": accel.accelerator_stats(None)},
             "pods": list(pods.values())})
+
+    def _rate(self, key: str, used_ns: int) -> int:
+        """usageNanoCores: CPU time per wall time since the previous summary (cAdvisor's rate)."""
+        t = time.monotonic()
+        prev = self._cpu_prev.get(key)
+        self._cpu_prev[key] = (t, used_ns)
+        if prev is None or t <= prev[0] or used_ns < prev[1]:
+            return 0
+        return int((used_ns - prev[1]) / (t - prev[0]))
 
     async def spec(self, req):
         import psutil
