@@ -22,13 +22,19 @@ import grpc
 
 from ..client import Client
 from ..deviceplugin.amd import make_plugins
-from ..grpcdesc.cri import API_VERSION, CRI as C
+from ..grpcdesc.cri import API_VERSION, CRI as C, EVENT_TRAILER
 from ..kubelet.kubelet import Kubelet, KubeletConfig
 from ..smi import FakeBackend
 
 
 class FakeRuntime:
-    """In-memory CRI server (reference pkg/kubelet/apis/cri/testing/fake_runtime_service.go)."""
+    """In-memory CRI server (reference pkg/kubelet/apis/cri/testing/fake_runtime_service.go).
+
+    It speaks the same evented contract as rocshim (the runtime a real MI355X node runs): every
+    lifecycle change emits a ContainerEventResponse with the sandbox's full status and all its
+    container statuses, and mutating calls return the `amdkube-event` trailer naming the newest
+    event of their sandbox, so a hollow kubelet does the same (list-free) work per pod as a
+    real one."""
 
     def __init__(self, socket_path: str, run_seconds: float | None = None):
         self.socket = socket_path
@@ -38,6 +44,9 @@ class FakeRuntime:
         self.server = None
         self.streams: set[asyncio.Queue] = set()
         self.calls: dict[str, int] = {}
+        self._last_ev: dict[str, int] = {}
+        self._removed_meta: dict[str, object] = {}
+        self.node_ip = "127.0.0.1"
 
     def _count(self, name):
         self.calls[name] = self.calls.get(name, 0) + 1
@@ -54,9 +63,28 @@ class FakeRuntime:
             await self.server.stop(0.2)
 
     def _emit(self, cid, sid, etype):
+        if not self.streams:
+            return
+        ts = max(time.time_ns(), self._last_ev.get(sid, 0) + 1)   # strictly increasing per sandbox
+        self._last_ev[sid] = ts
+        s = self.sandboxes.get(sid)
+        if s is None:     # removed: identity only
+            meta = self._removed_meta.pop(sid, None)
+            sst = C.PodSandboxStatus(id=sid, metadata=meta) if meta is not None else C.PodSandboxStatus(id=sid)
+            cst = []
+        else:
+            sst = C.PodSandboxStatus(network=C.PodSandboxNetworkStatus(ip=self.node_ip), **self._sb(sid, s))
+            cst = [self._cstatus(x, c) for x, c in self.containers.items() if c["sid"] == sid]
+        ev = C.ContainerEventResponse(container_id=cid, container_event_type=etype, created_at=ts,
+                                      pod_sandbox_status=sst, containers_statuses=cst)
         for q in list(self.streams):
-            q.put_nowait(C.ContainerEventResponse(container_id=cid, container_event_type=etype, created_at=time.time_ns(),
-                                                  pod_sandbox_status=C.PodSandboxStatus(id=sid)))
+            q.put_nowait(ev)
+
+    def _mark(self, ctx, sid):
+        ts = self._last_ev.get(sid or "", 0)
+        if sid and ts and sid not in self.sandboxes:
+            self._last_ev.pop(sid, None)
+        ctx.set_trailing_metadata(((EVENT_TRAILER, f"{sid}:{ts}" if sid and ts else ""),))
 
     async def Version(self, req, ctx):
         return C.VersionResponse(version=API_VERSION, runtime_name="fake", runtime_version="0.1", runtime_api_version="v1alpha1")
@@ -69,21 +97,33 @@ class FakeRuntime:
         self._count("RunPodSandbox")
         sid = uuid.uuid4().hex
         self.sandboxes[sid] = {"config": req.config, "state": C.SANDBOX_READY, "created": time.time_ns()}
+        self._emit(sid, sid, C.CONTAINER_STARTED_EVENT)
+        self._mark(ctx, sid)
         return C.RunPodSandboxResponse(pod_sandbox_id=sid)
 
     async def StopPodSandbox(self, req, ctx):
-        s = self.sandboxes.get(req.pod_sandbox_id)
+        sid = req.pod_sandbox_id
+        s = self.sandboxes.get(sid)
         if s:
-            s["state"] = C.SANDBOX_NOTREADY
             for cid, c in self.containers.items():
-                if c["sid"] == req.pod_sandbox_id and c["state"] == C.CONTAINER_RUNNING:
+                if c["sid"] == sid and c["state"] == C.CONTAINER_RUNNING:
                     self._exit(cid, 137)
+            if s["state"] != C.SANDBOX_NOTREADY:
+                s["state"] = C.SANDBOX_NOTREADY
+                self._emit(sid, sid, C.CONTAINER_STOPPED_EVENT)
+        self._mark(ctx, sid)
         return C.StopPodSandboxResponse()
 
     async def RemovePodSandbox(self, req, ctx):
-        self.sandboxes.pop(req.pod_sandbox_id, None)
-        for cid in [k for k, c in self.containers.items() if c["sid"] == req.pod_sandbox_id]:
+        sid = req.pod_sandbox_id
+        s = self.sandboxes.pop(sid, None)
+        for cid in [k for k, c in self.containers.items() if c["sid"] == sid]:
             del self.containers[cid]
+        if s is not None:
+            cfg = s["config"]
+            self._removed_meta[sid] = cfg.metadata
+            self._emit(sid, sid, C.CONTAINER_DELETED_EVENT)
+        self._mark(ctx, sid)
         return C.RemovePodSandboxResponse()
 
     def _sb(self, sid, s):
@@ -92,12 +132,14 @@ class FakeRuntime:
                     annotations=cfg.annotations)
 
     async def PodSandboxStatus(self, req, ctx):
+        self._count("PodSandboxStatus")
         s = self.sandboxes.get(req.pod_sandbox_id)
         if s is None:
             await ctx.abort(grpc.StatusCode.NOT_FOUND, "not found")
         return C.PodSandboxStatusResponse(status=C.PodSandboxStatus(**self._sb(req.pod_sandbox_id, s)))
 
     async def ListPodSandbox(self, req, ctx):
+        self._count("ListPodSandbox")
         out = []
         for sid, s in self.sandboxes.items():
             f = req.filter
@@ -111,6 +153,8 @@ class FakeRuntime:
         cid = uuid.uuid4().hex
         self.containers[cid] = {"sid": req.pod_sandbox_id, "config": req.config, "state": C.CONTAINER_CREATED,
                                 "created": time.time_ns(), "started": 0, "finished": 0, "exit": 0}
+        self._emit(cid, req.pod_sandbox_id, C.CONTAINER_CREATED_EVENT)
+        self._mark(ctx, req.pod_sandbox_id)
         return C.CreateContainerResponse(container_id=cid)
 
     def _exit(self, cid, code):
@@ -125,14 +169,24 @@ class FakeRuntime:
         self._emit(req.container_id, c["sid"], C.CONTAINER_STARTED_EVENT)
         if self.run_seconds is not None:
             asyncio.get_running_loop().call_later(self.run_seconds, self._exit, req.container_id, 0)
+        self._mark(ctx, c["sid"])
         return C.StartContainerResponse()
 
+    def _sid_of(self, cid):
+        c = self.containers.get(cid)
+        return c["sid"] if c is not None else None
+
     async def StopContainer(self, req, ctx):
+        sid = self._sid_of(req.container_id)
         self._exit(req.container_id, 137)
+        self._mark(ctx, sid)
         return C.StopContainerResponse()
 
     async def RemoveContainer(self, req, ctx):
-        self.containers.pop(req.container_id, None)
+        sid = self._sid_of(req.container_id)
+        if self.containers.pop(req.container_id, None) is not None:
+            self._emit(req.container_id, sid, C.CONTAINER_DELETED_EVENT)
+        self._mark(ctx, sid)
         return C.RemoveContainerResponse()
 
     def _c(self, cid, c):
@@ -146,16 +200,21 @@ class FakeRuntime:
                if (not f.pod_sandbox_id or f.pod_sandbox_id == c["sid"]) and (not f.id or f.id == cid)]
         return C.ListContainersResponse(containers=out)
 
+    @staticmethod
+    def _cstatus(cid, c):
+        cfg = c["config"]
+        return C.ContainerStatus(
+            id=cid, metadata=cfg.metadata, state=c["state"], created_at=c["created"], started_at=c["started"],
+            finished_at=c["finished"], exit_code=c["exit"], image=cfg.image, image_ref="fake",
+            reason="Completed" if c["state"] == C.CONTAINER_EXITED and c["exit"] == 0 else "",
+            labels=cfg.labels, annotations=cfg.annotations)
+
     async def ContainerStatus(self, req, ctx):
+        self._count("ContainerStatus")
         c = self.containers.get(req.container_id)
         if c is None:
             await ctx.abort(grpc.StatusCode.NOT_FOUND, "not found")
-        cfg = c["config"]
-        return C.ContainerStatusResponse(status=C.ContainerStatus(
-            id=req.container_id, metadata=cfg.metadata, state=c["state"], created_at=c["created"], started_at=c["started"],
-            finished_at=c["finished"], exit_code=c["exit"], image=cfg.image, image_ref="fake",
-            reason="Completed" if c["state"] == C.CONTAINER_EXITED and c["exit"] == 0 else "",
-            labels=cfg.labels, annotations=cfg.annotations))
+        return C.ContainerStatusResponse(status=self._cstatus(req.container_id, c))
 
     async def ListContainerStats(self, req, ctx):
         return C.ListContainerStatsResponse()

@@ -9,6 +9,8 @@ result is clipped to validation limits (3 nameservers, 6 search paths, 256 chars
 """
 from __future__ import annotations
 
+import os
+
 from ..grpcdesc.cri import CRI as C
 
 MAX_NAMESERVERS, MAX_SEARCH_PATHS, MAX_SEARCH_CHARS = 3, 6, 256
@@ -58,12 +60,20 @@ class DNSConfigurer:
         self.node_ip = node_ip
         self.recorder = recorder
 
+    _cache: tuple | None = None     # ((mtime_ns, size), parsed) of --resolv-conf
+
     def _host(self):
         if not self.resolv_conf:
             return [], [], []
         try:
+            st = os.stat(self.resolv_conf)
+            key = (st.st_mtime_ns, st.st_size, st.st_ino)
+            if self._cache is not None and self._cache[0] == key:
+                return tuple(list(x) for x in self._cache[1])
             with open(self.resolv_conf) as f:
-                return parse_resolv_conf(f.read())
+                parsed = parse_resolv_conf(f.read())
+            self._cache = (key, parsed)
+            return tuple(list(x) for x in parsed)
         except OSError:
             return [], [], []
 

@@ -133,6 +133,12 @@ def test_hollow_nodes_gpu_density():
             assert len(running) == 32, time.time() - t0
             ids = [(p["spec"]["nodeName"], d) for p in running for d in p["spec"]["extendedResources"][0]["assigned"]]
             assert len(set(ids)) == 32
+            # the kubelet learns each fresh pod's state from the runtime's full-state events:
+            # no per-pod status RPCs (only the startup snapshot and periodic relists list)
+            for n in nodes:
+                calls = n.runtime.calls
+                assert calls.get("RunPodSandbox", 0) == calls.get("CreateContainer", 0) >= 1, calls
+                assert calls.get("PodSandboxStatus", 0) == 0 and calls.get("ContainerStatus", 0) == 0, calls
         finally:
             for n in nodes:
                 await n.stop()
