@@ -10,9 +10,9 @@ Reference:
     provisioner creates `pvc-<claim uid>`. syncVolume: a volume whose claim is gone is
     Released, then reclaimed per persistentVolumeReclaimPolicy (Delete removes it and its
     provisioned data; Recycle scrubs it and makes it Available again; Retain keeps it).
-  * pkg/controller/volume/attachdetach — desired vs actual attachments per node from the
-    scheduled pods' volumes, reported in node.status.volumesAttached (VolumeAttachment
-    objects, storage.k8s.io/v1beta1, as CSI does).
+  * pkg/controller/volume/attachdetach — desired vs actual attachments of attachable volumes
+    per node, attached/detached through the volume plugins (amdkube/volume) and reported in
+    node.status.volumesAttached; safe detach waits for node.status.volumesInUse to drop it.
   * pkg/controller/volume/expand — a claim asking for more than its bound size on a class
     with allowVolumeExpansion grows the volume and then status.capacity.
   * pkg/controller/volume/pvcprotection, pvprotection — finalizers kubernetes.io/pvc-protection
@@ -25,14 +25,19 @@ scratch or dataset storage for GPU pods on one MI355X node.
 """
 from __future__ import annotations
 
+import asyncio
+import logging
 import os
 import shutil
+import time
 
 from ..api import meta as m
 from ..api.helpers import is_pod_terminal
 from ..api.labels import selector_from_label_selector
 from ..api.quantity import Quantity
 from .base import Controller, split_key
+
+log = logging.getLogger("amdkube.controllers.volumes")
 
 HOSTPATH_PROVISIONERS = ("amdkube.io/host-path", "kubernetes.io/host-path")
 DEFAULT_CLASS_ANN = "storageclass.kubernetes.io/is-default-class"
@@ -230,57 +235,142 @@ def pod_claims(pod) -> list[str]:
 
 
 class AttachDetachController(Controller):
+    """pkg/controller/volume/attachdetach: for every node, the attachable volumes of its
+    scheduled, non-terminal pods (desired) against what is attached (actual, seeded from
+    node.status.volumesAttached at start). Attach/detach run through the volume plugins (CSI:
+    a VolumeAttachment the driver's attacher fulfils; FlexVolume: the driver's attach/detach;
+    iSCSI/FC/RBD: no-op attach, the node logs in) as background operations, one per volume.
+    A volume still in node.status.volumesInUse is not detached until the kubelet unmounted it
+    or `max_wait_unmount` (6 min) passed. node.status.volumesAttached lists {name: unique
+    volume name, devicePath}; non-attachable volumes (hostPath, nfs, ...) never appear."""
     name = "attachdetach"
     workers = 1
-    attacher = "amdkube.io/host-path"
+
+    def __init__(self, mgr, plugins=None, max_wait_unmount: float = 360.0):
+        super().__init__(mgr)
+        self._plugins = plugins
+        self.max_wait_unmount = max_wait_unmount
+        self.attached: dict[str, dict[str, str]] = {}        # node -> unique -> devicePath
+        self._pending: set[tuple[str, str]] = set()
+        self._detach_wait: dict[tuple[str, str], float] = {}
+        self._ops: set[asyncio.Task] = set()
+        self._seeded = False
+
+    @property
+    def plugins(self):
+        if self._plugins is None:
+            from ..volume import NoopMounter, PluginMgr, VolumeHost, default_plugins
+            self._plugins = PluginMgr(default_plugins(), VolumeHost("/var/lib/kubelet", client=self.client, mounter=NoopMounter()))
+        return self._plugins
 
     def setup(self):
         f = self.mgr.factory
         self.pod_inf = self.mgr.pods
         self.pvc_inf = f.informer("persistentvolumeclaims")
-        self.va_inf = f.informer("volumeattachments")
+        self.pv_inf = f.informer("persistentvolumes")
         self.node_inf = self.mgr.nodes
         self.pod_inf.add_handler(on_add=self._pod, on_update=lambda o, n: self._pod(n), on_delete=self._pod)
+        self.node_inf.add_handler(on_add=self.enqueue, on_update=lambda o, n: self.enqueue(n))
 
     def _pod(self, pod):
         node = (pod.get("spec") or {}).get("nodeName")
         if node:
             self.enqueue(node)
 
-    async def sync(self, key):
-        _, node = split_key(key)
-        desired = {}
+    def _desired(self, node: str) -> dict:
+        from ..volume import Spec, VolumeError
+        out = {}
         for p in self.pod_inf.list():
             if (p.get("spec") or {}).get("nodeName") != node or is_pod_terminal(p):
                 continue
-            for c in pod_claims(p):
-                pvc = self.pvc_inf.get(f"{m.namespace_of(p)}/{c}")
-                pv = ((pvc or {}).get("spec") or {}).get("volumeName")
-                if pv:
-                    desired[f"{self.attacher.replace('/', '-').replace('.', '-')}-{pv}-{node}"] = pv
-        actual = {m.name_of(v): v for v in self.va_inf.list() if (v.get("spec") or {}).get("nodeName") == node}
-        for name, pv in desired.items():
-            if name not in actual:
+            for v in (p.get("spec") or {}).get("volumes") or []:
+                if "persistentVolumeClaim" in v:
+                    pvc = self.pvc_inf.get(f"{m.namespace_of(p)}/{v['persistentVolumeClaim'].get('claimName', '')}")
+                    pv = self.pv_inf.get(((pvc or {}).get("spec") or {}).get("volumeName") or "")
+                    if pv is None:
+                        continue
+                    spec = Spec(pv=pv, read_only=bool(v["persistentVolumeClaim"].get("readOnly")))
+                else:
+                    spec = Spec(volume=v)
                 try:
-                    await self.client.create({"apiVersion": "storage.k8s.io/v1beta1", "kind": "VolumeAttachment",
-                                              "metadata": {"name": name},
-                                              "spec": {"attacher": self.attacher, "nodeName": node,
-                                                       "source": {"persistentVolumeName": pv}}})
-                except m.StatusError as e:
-                    if not m.is_already_exists(e):   # the informer has not seen our own create yet
-                        raise
-                await self.client.patch("volumeattachments", name, {"status": {"attached": True}}, sub="status")
-        for name, va in actual.items():
-            if name not in desired:
-                try:
-                    await self.client.delete("volumeattachments", name)
-                except m.StatusError as e:
-                    if not m.is_not_found(e):
-                        raise
-        want = [{"name": f"kubernetes.io/{self.attacher}/{pv}", "devicePath": ""} for pv in sorted(set(desired.values()))]
+                    plugin = self.plugins.find_by_spec(spec)
+                except VolumeError:
+                    continue
+                if plugin.attachable:
+                    out[plugin.unique_name(spec, m.uid_of(p))] = (plugin, spec)
+        return out
+
+    def _seed(self):
+        """populateActualStateOfWorld: what the nodes say is attached."""
+        for n in self.node_inf.list():
+            att = {a.get("name", ""): a.get("devicePath", "") for a in (n.get("status") or {}).get("volumesAttached") or []}
+            if att:
+                self.attached.setdefault(m.name_of(n), {}).update(att)
+        self._seeded = True
+
+    def _op(self, node, unique, coro):
+        self._pending.add((node, unique))
+
+        async def run():
+            try:
+                await coro
+            except Exception as e:
+                log.warning("attachdetach: %s on %s: %r", unique, node, e)
+                self.queue.add_after(node, 2.0)
+            finally:
+                self._pending.discard((node, unique))
+                self.enqueue(node)
+        t = asyncio.create_task(run(), name=f"attachdetach-{unique}")
+        self._ops.add(t)
+        t.add_done_callback(self._ops.discard)
+
+    async def _attach(self, node, unique, plugin, spec):
+        device = await plugin.attach(spec, node)
+        self.attached.setdefault(node, {})[unique] = device or ""
+
+    async def _detach(self, node, unique):
+        from ..volume import VolumeError
+        plugin_name, _, vol = unique.rpartition("/")
+        try:
+            plugin = self.plugins.find_by_name(plugin_name)
+        except VolumeError:
+            plugin = None
+        if plugin is not None:
+            await plugin.detach(vol, node)
+        self.attached.get(node, {}).pop(unique, None)
+        self._detach_wait.pop((node, unique), None)
+
+    async def sync(self, key):
+        _, node = split_key(key)
+        if not self._seeded:
+            self._seed()
         n = self.node_inf.get(node)
-        if n is not None and ((n.get("status") or {}).get("volumesAttached") or []) != want:
-            await self.client.patch("nodes", node, {"status": {"volumesAttached": want}}, sub="status")
+        desired = self._desired(node) if n is not None else {}
+        actual = self.attached.setdefault(node, {})
+        for unique, (plugin, spec) in desired.items():
+            if unique not in actual and (node, unique) not in self._pending:
+                self._op(node, unique, self._attach(node, unique, plugin, spec))
+        in_use = set(((n or {}).get("status") or {}).get("volumesInUse") or [])
+        now = time.monotonic()
+        for unique in list(actual):
+            if unique in desired or (node, unique) in self._pending:
+                continue
+            if unique in in_use:
+                first = self._detach_wait.setdefault((node, unique), now)
+                if now - first < self.max_wait_unmount:
+                    self.queue.add_after(node, 1.0)    # the kubelet has not unmounted it yet
+                    continue
+            self._op(node, unique, self._detach(node, unique))
+        if n is None:
+            return
+        want = [{"name": u, "devicePath": d} for u, d in sorted(actual.items())]
+        if ((n.get("status") or {}).get("volumesAttached") or []) != want:
+            await self.client.patch("nodes", node, {"status": {"volumesAttached": want or None}}, sub="status")
+
+    async def stop(self):
+        for t in list(self._ops):
+            t.cancel()
+        await super().stop()
 
 
 class VolumeExpandController(Controller):

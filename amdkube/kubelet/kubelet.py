@@ -42,6 +42,7 @@ from .cm import enforce_pods_cgroup, node_allocatable as reserved_allocatable, p
 from .cri_client import CURRENT_POD, CRIClient
 from .devicemanager import AdmissionError, ManagerImpl, ManagerStub
 from ..utils.trace import POD_TRACE
+from ..volume import VolumeError
 from .kuberuntime import L_POD_UID, RuntimeManager, SandboxRef, apply_event
 from .qos import CRITICAL_ANNOTATION
 from .status import StatusManager, generate_status
@@ -133,6 +134,12 @@ class KubeletConfig:
     rotate_server_certificates: bool = False          # RotateKubeletServerCertificate: serving cert via CSR
     config_file: str | None = None                    # --config (KubeletConfiguration file)
     dynamic_config_dir: str | None = None             # --dynamic-config-dir
+    volume_plugin_dir: str | None = None              # --volume-plugin-dir (FlexVolume drivers; default <root>/volumeplugins)
+    enable_controller_attach_detach: bool = True      # --enable-controller-attach-detach
+    volume_mounter: str = "auto"                      # auto (system when root, else none) | system | none | fake
+    volume_mount_timeout: float = 120.0               # WaitForAttachAndMount timeout (s)
+    volume_reconcile_period: float = 2.0              # reconciler loop period (s)
+    volume_remount_period: float = 60.0               # re-render secret/configMap/downwardAPI/projected content (s)
 
 
 class PodWorker:
@@ -234,6 +241,7 @@ class Kubelet:
                                        config.minimum_image_ttl_duration, recorder=self.recorder,
                                        node_ref=lambda: {"kind": "Node", "metadata": {"name": self.node_name, "uid": self.node_name}})
         self.runtime.gpu_numa = self._gpu_numa
+        self.volume_manager = self._volume_manager(config)
         self._cpuset_applied: dict[str, str] = {}
         self._pods_cgroup_enforced = None
         self.pressure: set[str] = set()
@@ -269,6 +277,19 @@ class Kubelet:
         self.static: dict[str, dict] = {}      # uid -> static pod from --pod-manifest-path
         self.mirrors: dict[tuple, dict] = {}   # (ns, name) -> mirror pod in the API
         self._static_dirty = asyncio.Event()
+
+    def _volume_manager(self, config):
+        from ..volume import FakeMounter, NoopMounter, PluginMgr, SysMounter, VolumeHost, default_plugins
+        from .podcontext import PodContext
+        from .volumemanager import VolumeManager
+        kind = config.volume_mounter
+        if kind == "auto":
+            kind = "system" if os.geteuid() == 0 else "none"
+        mounter = {"system": SysMounter, "none": NoopMounter, "fake": FakeMounter}[kind]()
+        host = VolumeHost(config.root_dir, self.node_name, self.client, mounter, pod_context=PodContext(self),
+                          node_ip=config.node_ip, plugins_dir=config.volume_plugin_dir)
+        return VolumeManager(self, PluginMgr(default_plugins(), host), config.enable_controller_attach_detach,
+                             config.volume_reconcile_period, config.volume_mount_timeout, config.volume_remount_period)
 
     def _init_metrics(self):
         r = self.metrics
@@ -315,6 +336,7 @@ class Kubelet:
                         asyncio.create_task(self._eviction_loop(), name="eviction")]
         if self.cfg.evented_pleg:
             self._tasks.append(asyncio.create_task(self._evented_pleg(), name="pleg-events"))
+        self.volume_manager.start()
         if self.cpu_manager.policy != "none":
             self._tasks.append(asyncio.create_task(self._cpu_reconcile_loop(), name="cpu-manager"))
         if self.cfg.pod_manifest_path:
@@ -352,6 +374,7 @@ class Kubelet:
     async def stop(self):
         for t in self._tasks:
             t.cancel()
+        await self.volume_manager.stop()
         if self.informer:
             await self.informer.stop()
         if self.svc_informer is not None:
@@ -429,6 +452,9 @@ class Kubelet:
                            "architecture": "amd64", "containerRuntimeVersion": "rocshim://0.1.0", "osImage": "Linux",
                            "machineID": "", "systemUUID": "", "bootID": "", "kernelVersion": os.uname().release},
               "extendedResources": ext}
+        in_use = self.volume_manager.volumes_in_use()
+        if in_use or prev.get("volumesInUse"):
+            st["volumesInUse"] = in_use or None     # attachable volumes mounted or about to be (safe detach)
         st["_removed"] = removed
         if self.cfg.cgroup_root and "pods" in self.cfg.enforce_node_allocatable.split(",") and \
                 self._pods_cgroup_enforced != (alloc.get("cpu"), alloc.get("memory")):
@@ -788,6 +814,7 @@ class Kubelet:
             grace = md.get("deletionGracePeriodSeconds")
             grace = (pod.get("spec") or {}).get("terminationGracePeriodSeconds", 30) if grace is None else grace
             await self.runtime.kill_pod(uid, int(grace), pod)
+            self.volume_manager.remove_pod(uid)
             rt = await self.runtime.pod_status(uid)
             st = generate_status(pod, rt, self.cfg.node_ip, {}, [], m.now_rfc3339())
             if st["phase"] == "Running":
@@ -801,6 +828,7 @@ class Kubelet:
             # recomputation must not drop the reason of a kubelet-decided failure (deadline,
             # eviction) that may not be written yet
             await self.runtime.kill_pod(uid, 0, pod, self._cached_sandboxes(uid))
+            self.volume_manager.remove_pod(uid)     # terminated: its volumes go (populator findAndRemoveDeletedPods)
             return False
         if sent_phase not in ("Succeeded", "Failed") and self._active_deadline_exceeded(pod):
             # active_deadline.go: the pod sync handler fails the pod once it has been active on
@@ -814,7 +842,17 @@ class Kubelet:
             st.update({"phase": "Failed", "reason": "DeadlineExceeded", "message": msg})
             self.status.set(pod, st)
             return False
-        ctx = await self._pod_context(pod)
+        try:
+            ctx = await self._pod_context(pod)
+        except VolumeError as e:
+            # kubelet.go syncPod: "Unable to mount volumes for pod": the pod waits in
+            # ContainerCreating and the sync is retried
+            self.sync_errors[uid] = str(e)
+            rt = await self._cached_status(uid)
+            st = generate_status(pod, rt, self.cfg.node_ip, self.readiness.get(uid, {}), [], m.now_rfc3339())
+            self.status.set(pod, st)
+            asyncio.get_running_loop().call_later(2.0, self.dispatch, uid)
+            return False
         POD_TRACE(uid, "sync_ctx")
         rt = await self._cached_status(uid)
         mut0 = self.cri.pod_mutations(uid)
@@ -840,6 +878,7 @@ class Kubelet:
         if st["phase"] in ("Succeeded", "Failed"):
             # release the sandbox (devices stay API-assigned)
             await self.runtime.kill_pod(uid, 0, pod, self._cached_sandboxes(uid))
+            self.volume_manager.remove_pod(uid)
         ads = (pod.get("spec") or {}).get("activeDeadlineSeconds")
         if ads is not None and st["phase"] not in ("Succeeded", "Failed") and uid not in self._deadline_timers:
             start = m.parse_time(st.get("startTime"))
@@ -1030,6 +1069,7 @@ class Kubelet:
     def _cleanup(self, uid):
         self._runtime_uids.add(uid)   # the runtime may still hold leftovers: list before trusting the cache again
         self.cpu_manager.release_pod(uid)
+        self.volume_manager.remove_pod(uid)
         self._rt_gen.pop(uid, None)
         self._rt_cache.pop(uid, None)
         self._rt_pending.pop(uid, None)
@@ -1052,8 +1092,9 @@ class Kubelet:
     async def _pod_context(self, pod: dict) -> dict:
         """Volumes and per-container env and mounts (podcontext.PodContext)."""
         from .podcontext import PodContext
+        from .volumemanager import subpath
         pc = PodContext(self)
-        vols = await pc.volumes(pod)
+        vols = await self.volume_manager.wait_for_attach_and_mount(pod)
         spec = pod.get("spec") or {}
         ns = m.namespace_of(pod)
         services = []
@@ -1063,7 +1104,9 @@ class Kubelet:
         env, mounts = {}, {}
         for c in (spec.get("initContainers") or []) + (spec.get("containers") or []):
             env[c["name"]] = await pc.env(pod, c, services)
-            mounts[c["name"]] = [{"container_path": vm["mountPath"], "host_path": os.path.join(vols[vm["name"]], vm.get("subPath", "")).rstrip("/"),
+            mounts[c["name"]] = [{"container_path": vm["mountPath"],
+                                  "host_path": subpath(vols[vm["name"]], vm.get("subPath", ""),
+                                                       f"container {c['name']} mount {vm['name']}").rstrip("/"),
                                   "read_only": bool(vm.get("readOnly"))} for vm in c.get("volumeMounts") or [] if vm["name"] in vols]
         return {"env": env, "mounts": mounts}
 
@@ -1168,7 +1211,8 @@ class Kubelet:
         active = lambda uid: (uid in self.pods or uid in self.workers) and uid not in self.terminated_deleted   # noqa: E731
         return await self.runtime.garbage_collect(active, self.cfg.maximum_dead_containers_per_container,
                                                   self.cfg.maximum_dead_containers, self.cfg.minimum_container_ttl_duration,
-                                                  sources_ready=self.sources_ready())
+                                                  sources_ready=self.sources_ready(),
+                                                  has_volumes=self.volume_manager.has_mounts)
 
     def sources_ready(self) -> bool:
         """config.SourcesReady.AllReady: every configured pod source has delivered its first

@@ -453,7 +453,8 @@ class RuntimeManager:
 
     # ------------------------------------------------------------ garbage collection
     async def garbage_collect(self, is_active, max_per_pod_container: int = 1, max_containers: int = -1,
-                              min_age: float = 0.0, now_ns: int | None = None, sources_ready: bool = True) -> dict:
+                              min_age: float = 0.0, now_ns: int | None = None, sources_ready: bool = True,
+                              has_volumes=None) -> dict:
         """kuberuntime_gc.go GarbageCollect: dead containers older than min_age are evictable,
         grouped in (pod, container name) units. Only when all pod sources are ready
         (allSourcesReady, :212-219) does a pod unknown to the kubelet count as deleted, and then
@@ -462,7 +463,9 @@ class RuntimeManager:
         then the oldest go until the node is under it. Sandboxes (evictSandboxes, :256-311):
         not ready and without containers; a deleted pod loses all of them, others keep their
         newest. Container logs go with their containers; a deleted pod's directory (logs and
-        volumes) goes once nothing of it is left (evictPodLogsDirectories, sources ready only)."""
+        volumes) goes once nothing of it is left (evictPodLogsDirectories, sources ready only) and
+        no volume is still mounted in it (cleanupOrphanedPodDirs: `has_volumes(uid)`; deleting a
+        directory with a live network mount would delete the remote data)."""
         now_ns = now_ns or time.time_ns()
         deleted = (lambda uid: not is_active(uid)) if sources_ready else (lambda uid: False)   # noqa: E731
         sbs = await self.cri.list_pod_sandbox()
@@ -542,6 +545,8 @@ class RuntimeManager:
                 names = []
             for uid in names:
                 if uid not in remaining and deleted(uid):
+                    if has_volumes is not None and has_volumes(uid):
+                        continue
                     shutil.rmtree(os.path.join(root, uid), ignore_errors=True)
                     dirs += 1
         return {"containers": removed, "sandboxes": sb_removed, "pod_dirs": dirs}

@@ -1,12 +1,11 @@
-"""Per-pod volume and environment resolution (the kubelet's volume manager for node-local
-volume types and kubelet_pods.go makeEnvironmentVariables / makeMounts).
+"""Per-pod content and environment resolution (kubelet_pods.go makeEnvironmentVariables and
+the content half of the kubelet-rendered volume plugins).
 
-Volumes (pkg/volume/*): emptyDir, hostPath (with its `type` checks: DirectoryOrCreate,
-Directory, FileOrCreate, File, Socket, CharDevice, BlockDevice), configMap and secret (items
-key→path with mode, defaultMode, optional), downwardAPI (fieldRef and resourceFieldRef with
-divisor), projected (secret / configMap / downwardAPI sources into one directory), gitRepo
-(clone + checkout of a revision into `directory`), persistentVolumeClaim (bound hostPath /
-local volumes); files are written atomically (atomic_writer.go).
+Volume content (used by amdkube/volume/local.py; the volume manager owns the lifecycle):
+configMap and secret (items key→path with mode, defaultMode, optional), downwardAPI (fieldRef
+and resourceFieldRef with divisor), projected (secret / configMap / downwardAPI sources into
+one directory), gitRepo (clone + checkout of a revision into `directory`); files are written
+atomically (atomic_writer.go).
 
 Environment (kubelet_pods.go:504-640): service variables of every service of the pod's
 namespace plus the master `kubernetes` service (envvars.FromServices: <NAME>_SERVICE_HOST,
@@ -22,7 +21,6 @@ import base64
 import math
 import os
 import re
-import stat
 import subprocess
 
 from ..api import meta as m
@@ -177,77 +175,6 @@ class PodContext:
             else:
                 val = ""
             atomic_write(os.path.join(d, it["path"]), val.encode(), it.get("mode", default_mode))
-
-    async def volumes(self, pod: dict) -> dict[str, str]:
-        uid, ns = m.uid_of(pod), m.namespace_of(pod)
-        spec = pod.get("spec") or {}
-        base = os.path.join(self.k.cfg.root_dir, "pods", uid, "volumes")
-        vols = {}
-        for v in spec.get("volumes") or []:
-            name = v["name"]
-            what = f"volume {name}"
-            if "hostPath" in v:
-                hp = v["hostPath"]
-                p, typ = hp.get("path", ""), hp.get("type") or ""
-                if typ == "DirectoryOrCreate":
-                    os.makedirs(p, mode=0o755, exist_ok=True)
-                elif typ == "FileOrCreate":
-                    os.makedirs(os.path.dirname(p) or "/", exist_ok=True)
-                    if not os.path.exists(p):
-                        open(p, "a").close()
-                elif typ:
-                    check = {"Directory": stat.S_ISDIR, "File": stat.S_ISREG, "Socket": stat.S_ISSOCK,
-                             "CharDevice": stat.S_ISCHR, "BlockDevice": stat.S_ISBLK}.get(typ)
-                    try:
-                        ok = check is not None and check(os.stat(p).st_mode)
-                    except OSError:
-                        ok = False
-                    if not ok:
-                        raise RuntimeError(f"{what}: hostPath type check failed: {p} is not a {typ}")
-                vols[name] = p
-            elif "configMap" in v or "secret" in v:
-                kind = "configmaps" if "configMap" in v else "secrets"
-                d = os.path.join(base, f"kubernetes.io~{kind[:-1]}", name)
-                os.makedirs(d, exist_ok=True)
-                await self._projection(pod, d, kind, v.get("configMap") or v.get("secret"), 0o644, what)
-                vols[name] = d
-            elif "projected" in v:
-                d = os.path.join(base, "kubernetes.io~projected", name)
-                os.makedirs(d, exist_ok=True)
-                dm = v["projected"].get("defaultMode", 0o644)
-                for src in v["projected"].get("sources") or []:
-                    if "secret" in src:
-                        await self._projection(pod, d, "secrets", src["secret"], dm, what)
-                    elif "configMap" in src:
-                        await self._projection(pod, d, "configmaps", src["configMap"], dm, what)
-                    elif "downwardAPI" in src:
-                        await self._downward(pod, d, src["downwardAPI"].get("items"), dm)
-                vols[name] = d
-            elif "downwardAPI" in v:
-                d = os.path.join(base, "kubernetes.io~downward-api", name)
-                os.makedirs(d, exist_ok=True)
-                await self._downward(pod, d, v["downwardAPI"].get("items"), v["downwardAPI"].get("defaultMode", 0o644))
-                vols[name] = d
-            elif "gitRepo" in v:
-                vols[name] = await self._git_repo(os.path.join(base, "kubernetes.io~git-repo", name), v["gitRepo"], what)
-            elif "persistentVolumeClaim" in v:
-                claim = v["persistentVolumeClaim"].get("claimName", "")
-                pvc = await self.k.client.get_or_none("persistentvolumeclaims", claim, ns)
-                pv_name = ((pvc or {}).get("spec") or {}).get("volumeName")
-                if not pv_name or ((pvc or {}).get("status") or {}).get("phase") != "Bound":
-                    raise RuntimeError(f"{what}: PersistentVolumeClaim {claim} is not bound")
-                pv = await self.k.client.get("persistentvolumes", pv_name)
-                ps = pv.get("spec") or {}
-                path = (ps.get("hostPath") or {}).get("path") or (ps.get("local") or {}).get("path")
-                if not path:
-                    raise RuntimeError(f"{what}: PersistentVolume {pv_name} has no host-local source")
-                os.makedirs(path, exist_ok=True)
-                vols[name] = path
-            else:   # emptyDir (and volume types with no node-local form degrade to an empty directory)
-                d = os.path.join(base, "kubernetes.io~empty-dir", name)
-                os.makedirs(d, exist_ok=True)
-                vols[name] = d
-        return vols
 
     async def _git_repo(self, d: str, spec: dict, what: str) -> str:
         """git_repo.go SetUpAt: clone once into `directory` (or a subdirectory named after the

@@ -65,9 +65,13 @@ class LocalCluster:
             self.plugins = make_plugins(self.backend, self.resource_naming, plugins_dir=os.path.join(b, "plugins"),
                                         health_interval=5.0, health_probe=self.health_probe)
             self.plugin = self.plugins[0]
+        kw = dict(self.kubelet_kw)
+        # the in-process harness mounts nothing unless a test asks for real mounts (and then
+        # stop() unmounts whatever is left under its directory)
+        kw.setdefault("volume_mounter", "none")
         cfg = KubeletConfig(node_name=self.node_name, root_dir=os.path.join(b, "kubelet"), plugins_dir=os.path.join(b, "plugins"),
                             cri_socket=os.path.join(b, "rocshim.sock"), port=0, relist_period=self.relist_period,
-                            node_status_update_frequency=self.nsuf, **self.kubelet_kw)
+                            node_status_update_frequency=self.nsuf, **kw)
         self.kubelet = await Kubelet(Client(self.api.url, token=self.api.loopback_token, pool=128), cfg, smi_backend=self.backend).start()
         for p in self.plugins:
             await p.start()
@@ -111,6 +115,8 @@ class LocalCluster:
             except Exception:
                 pass
         if self._own_dir:
+            from .volume.mount import unmount_under
+            unmount_under(self.base)
             shutil.rmtree(self.base, ignore_errors=True)
 
     async def __aenter__(self):

@@ -1,0 +1,36 @@
+"""Volume types whose backends are cloud or vendor services this build cannot reach
+(pkg/volume/aws_ebs, gce_pd, azure_dd, cinder, vsphere_volume, photon_pd, portworx, scaleio,
+storageos, flocker). They are recognised — so a pod using one gets a precise FailedMount event
+instead of "no volume plugin matched" — but their set-up fails: attaching them needs the cloud
+provider's block-storage API (or the vendor's client library), and amdkube's cloud providers
+are bare metal and fake (no public-cloud SDKs exist offline on an MI355X host).
+"""
+from __future__ import annotations
+
+from . import VolumeError, VolumePlugin
+
+_TYPES = {
+    "awsElasticBlockStore": ("kubernetes.io/aws-ebs", "the AWS EC2 API"),
+    "gcePersistentDisk": ("kubernetes.io/gce-pd", "the GCE compute API"),
+    "azureDisk": ("kubernetes.io/azure-disk", "the Azure compute API"),
+    "cinder": ("kubernetes.io/cinder", "the OpenStack block-storage API"),
+    "vsphereVolume": ("kubernetes.io/vsphere-volume", "the vSphere API"),
+    "photonPersistentDisk": ("kubernetes.io/photon-pd", "the Photon controller API"),
+    "portworxVolume": ("kubernetes.io/portworx-volume", "the Portworx REST API"),
+    "scaleIO": ("kubernetes.io/scaleio", "the ScaleIO gateway and drv_cfg"),
+    "storageos": ("kubernetes.io/storageos", "the StorageOS API"),
+    "flocker": ("kubernetes.io/flocker", "the Flocker control service"),
+}
+
+
+class UnavailableBackendPlugin(VolumePlugin):
+    def __init__(self, key: str, name: str, needs: str):
+        self.source_key, self.name, self.needs = key, name, needs
+
+    async def set_up(self, spec, pod, dir, device_mount_path=None, fs_group=None):
+        raise VolumeError(f"{self.source_key} volume {spec.name()!r} needs {self.needs}, which this node cannot reach "
+                          f"(use csi, flexVolume, iscsi, rbd, nfs or local volumes on MI355X hosts)")
+
+
+def plugins() -> list[VolumePlugin]:
+    return [UnavailableBackendPlugin(k, n, why) for k, (n, why) in _TYPES.items()]
