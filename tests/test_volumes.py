@@ -443,3 +443,50 @@ def test_pod_dir_gc_keeps_directories_with_volumes(tmp_path):
         return await rm.garbage_collect(lambda uid: False, sources_ready=True, has_volumes=lambda uid: uid == "b")
     res = run(go(), 10)
     assert res["pod_dirs"] == 1 and not (tmp_path / "pods" / "a").exists() and (tmp_path / "pods" / "b").exists()
+
+
+def _can_mount_tmpfs(tmp_path) -> bool:
+    import subprocess
+    if os.geteuid() != 0:
+        return False
+    d = tmp_path / "probe"
+    d.mkdir()
+    if subprocess.run(["mount", "-t", "tmpfs", "tmpfs", str(d)], capture_output=True).returncode != 0:
+        return False
+    subprocess.run(["umount", str(d)], capture_output=True)
+    return True
+
+
+def test_real_tmpfs_mounts_for_secret_and_memory_volumes(tmp_path):
+    """With a privileged kubelet (system mounter) secret content lives on tmpfs, never on disk,
+    and memory-medium emptyDirs are tmpfs; both are unmounted when the pod goes."""
+    import pytest
+    if not _can_mount_tmpfs(tmp_path):
+        pytest.skip("needs root and mount(2)")
+    from amdkube.volume.mount import SysMounter
+
+    async def go():
+        async with LocalCluster(gpus="none", relist_period=0.2, with_controllers=False,
+                                kubelet_kw={"volume_mounter": "system", "volume_reconcile_period": 0.2}) as lc:
+            c = lc.client
+            await c.create({"apiVersion": "v1", "kind": "Secret", "metadata": {"name": "tok"}, "data": {"t": "czNjcjN0"}}, "default")
+            await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "sec"}, "spec": {
+                "volumes": [{"name": "s", "secret": {"secretName": "tok"}}, {"name": "shm", "emptyDir": {"medium": "Memory"}}],
+                "containers": [{"name": "c", "image": "busybox", "command": ["sleep", "30"],
+                                "volumeMounts": [{"name": "s", "mountPath": "/s"}, {"name": "shm", "mountPath": "/dev/shm"}]}]}},
+                           "default")
+            pod = await wait_pod(c, "default", "sec", timeout=30)
+            vols = os.path.join(lc.kubelet.cfg.root_dir, "pods", m.uid_of(pod), "volumes")
+            s_dir = os.path.join(vols, "kubernetes.io~secret", "s")
+            shm = os.path.join(vols, "kubernetes.io~empty-dir", "shm")
+            sm = SysMounter()
+            table = {mp.path: mp.type for mp in sm.list()}
+            assert table.get(os.path.realpath(s_dir)) == "tmpfs" and table.get(os.path.realpath(shm)) == "tmpfs"
+            assert open(os.path.join(s_dir, "t")).read() == "s3cr3t"
+            await c.delete("pods", "sec", "default", grace=0)
+
+            async def unmounted():
+                paths = {mp.path for mp in sm.list()}
+                return os.path.realpath(s_dir) not in paths and os.path.realpath(shm) not in paths
+            await _until(unmounted, 20)
+    run(go(), 60)
