@@ -320,7 +320,12 @@ def rocshim(argv):
     ap.add_argument("--state-dir", default="/var/lib/amdkube/rocshim")
     ap.add_argument("--hooks-dir", default="/usr/share/containers/docker/hooks.d")
     ap.add_argument("--isolation", default="env", choices=("env", "namespaces"))
-    ap.add_argument("--network-plugin", default="host", choices=("host", "cni"))
+    ap.add_argument("--network-plugin", default="host", choices=("host", "cni", "kubenet"),
+                    help="kubenet: pod network namespaces on the amdkube-bridge CNI plugin (cbr0 + host-local IPAM)")
+    ap.add_argument("--pod-namespaces", action="store_true",
+                    help="non-hostNetwork pods get their own net/ipc/uts namespaces (privileged; implied by kubenet)")
+    ap.add_argument("--bridge", default="cbr0")
+    ap.add_argument("--network-plugin-mtu", type=int, default=1460)
     ap.add_argument("--cni-conf-dir", default="/etc/cni/net.d")
     ap.add_argument("--cni-bin-dir", default=None, help="default: /opt/cni/bin plus amdkube's bundled plugins")
     ap.add_argument("--node-ip", default="127.0.0.1")
@@ -329,15 +334,19 @@ def rocshim(argv):
     klog.setup(a.v, "rocshim")
     from ..runtime import RocShim
     from ..runtime.images import NATIVE_BIN
-    from ..runtime.network import CNINetwork, HostNetwork
-    if a.network_plugin == "cni":
+    from ..runtime.network import CNINetwork, HostNetwork, KubenetNetwork
+    if a.network_plugin == "kubenet":
+        bins = a.cni_bin_dir.split(",") if a.cni_bin_dir else [os.path.join(NATIVE_BIN, "cni"), "/opt/cni/bin"]
+        net = KubenetNetwork(bins, a.state_dir, a.bridge, a.network_plugin_mtu, a.node_ip)
+    elif a.network_plugin == "cni":
         bins = a.cni_bin_dir.split(",") if a.cni_bin_dir else ["/opt/cni/bin", os.path.join(NATIVE_BIN, "cni")]
         net = CNINetwork(a.cni_conf_dir, bins, a.node_ip)
     else:
         net = HostNetwork(a.node_ip)
 
     async def mk():
-        return await RocShim(a.listen, a.state_dir, a.hooks_dir, a.isolation, network=net).start()
+        return await RocShim(a.listen, a.state_dir, a.hooks_dir, a.isolation, network=net,
+                             pod_namespaces=a.pod_namespaces or a.network_plugin == "kubenet").start()
     _run_forever(mk)
 
 

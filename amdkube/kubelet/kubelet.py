@@ -885,6 +885,10 @@ class Kubelet:
             if start:
                 self._deadline_timers.add(uid)
                 asyncio.get_running_loop().call_later(max(0.0, start + float(ads) - time.time()) + 0.01, self.dispatch, uid)
+        if errors:
+            # pod_workers.go: a failed sync is retried after the worker back-off (10 s, jittered)
+            import random
+            asyncio.get_running_loop().call_later(10.0 * (1 + 0.5 * random.random()), self.dispatch, uid)
         # container restarts waiting on back-off: re-sync when the back-off expires
         for c in (pod.get("spec") or {}).get("containers") or []:
             rem = self.runtime.backoff_remaining(uid, c["name"])

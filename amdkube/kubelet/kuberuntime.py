@@ -349,7 +349,16 @@ class RuntimeManager:
             attempt = (st.sandboxes[0][2] + 1) if st.sandboxes else 0
             sandbox_cfg = self.sandbox_config(pod, attempt, self.dm.pod_resources(pod))
             POD_TRACE(uid, "sandbox_start")
-            sid = await self.cri.run_pod_sandbox(sandbox_cfg)
+            try:
+                sid = await self.cri.run_pod_sandbox(sandbox_cfg)
+            except grpc.RpcError as e:
+                # kuberuntime_manager.go createPodSandbox: FailedCreatePodSandBox event, pod stays
+                # Pending, the next sync retries
+                msg = f"Failed create pod sandbox: {e.details() if hasattr(e, 'details') else e}"
+                if self.recorder is not None:
+                    self.recorder.event(pod, "Warning", "FailedCreatePodSandBox", msg)
+                errors.append(msg)
+                return errors
             POD_TRACE(uid, "sandbox_ready")
             st = PodRuntimeStatus(uid)
             st.sandboxes = [(sid, C.SANDBOX_READY, attempt, time.time_ns())]

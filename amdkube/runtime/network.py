@@ -167,3 +167,24 @@ class CNINetwork:
                 await self._exec(plugin, conf, "DEL", sid, meta, netns)
             except NetworkError as e:
                 log.warning("CNI DEL for %s: %s", sid, e)
+
+
+class KubenetNetwork(CNINetwork):
+    """pkg/kubelet/network/kubenet: the kubelet-managed pod network — one `cbr0` bridge owning
+    the node's pod CIDR gateway, a veth pair per pod, host-local addresses, hairpin mode and the
+    MTU — realised with amdkube's native `amdkube-bridge` + `amdkube-cni` plugins. The config is
+    generated from the pod CIDR the kubelet pushes (UpdateRuntimeConfig); until it is known the
+    network is not ready ("kubenet does not have netConfig")."""
+    name = "kubenet"
+
+    def __init__(self, bin_dirs: list[str], state_dir: str, bridge: str = "cbr0", mtu: int = 1460,
+                 node_ip: str = "127.0.0.1", timeout: float = 30.0):
+        super().__init__("", bin_dirs, node_ip, timeout)
+        self.bridge, self.mtu, self.state_dir = bridge, mtu, state_dir
+
+    def _netconf(self):
+        if not self.pod_cidr:
+            raise NetworkError("kubenet does not have netConfig: the node has no pod CIDR yet")
+        return {"cniVersion": "0.3.1", "name": "kubenet", "plugins": [{
+            "type": "amdkube-bridge", "bridge": self.bridge, "mtu": self.mtu, "isGateway": True, "hairpinMode": True,
+            "ipam": {"type": "amdkube-cni", "subnet": self.pod_cidr, "dataDir": os.path.join(self.state_dir, "ipam")}}]}

@@ -102,11 +102,13 @@ class Sandbox:
         self.proc = None
         self.ip = ""
         self.pod_network = False   # the network plugin set this sandbox up (CNI DEL on teardown)
+        self.own_ns = False        # the sandbox holds its own net/ipc/uts namespaces (pod networking)
+        self.port_mappings: list[dict] = []
 
     def to_json(self):
         return {"id": self.id, "meta": self.meta, "labels": self.labels, "annotations": self.annotations,
                 "log_dir": self.log_dir, "state": self.state, "created_at": self.created_at, "pid": self.pid,
-                "ip": self.ip, "pod_network": self.pod_network}
+                "ip": self.ip, "pod_network": self.pod_network, "own_ns": self.own_ns, "port_mappings": self.port_mappings}
 
 
 class Container:
@@ -137,7 +139,8 @@ class Container:
 
 class RocShim:
     def __init__(self, socket_path: str, state_dir: str, hooks_dir: str = DEFAULT_HOOKS_DIR, isolation: str = "env",
-                 cgroup_root: str = "/sys/fs/cgroup/amdkube", dev_root: str = "/dev", network=None):
+                 cgroup_root: str = "/sys/fs/cgroup/amdkube", dev_root: str = "/dev", network=None,
+                 pod_namespaces: bool = False):
         self.socket = socket_path
         self.state_dir = state_dir
         os.makedirs(os.path.join(state_dir, "sandboxes"), exist_ok=True)
@@ -147,6 +150,11 @@ class RocShim:
         self.hooks = HookService(hooks_dir, HANDLERS)
         self.isolation = isolation
         self.network = network or HostNetwork()
+        # pod networking: non-hostNetwork sandboxes get their own net/ipc/uts namespaces (needs
+        # a privileged rocshim) wired by the network plugin (amdkube-bridge); containers join them
+        self.pod_namespaces = pod_namespaces
+        from .hostport import HostPortManager
+        self.hostports = HostPortManager()
         self.cgroup_root = cgroup_root
         self.dev_root = dev_root
         self.sandboxes: dict[str, Sandbox] = {}
@@ -224,6 +232,7 @@ class RocShim:
             for s in list(self.sandboxes.values()):
                 await self.stop_sandbox(s.id)
         await self.hooks.stop()
+        await self.hostports.close()
         if self.streaming is not None:
             await self.streaming.stop()
         if self.server:
@@ -256,6 +265,7 @@ class RocShim:
             s = Sandbox(d["id"], b"", d["meta"], d["labels"], d["annotations"], d["log_dir"])
             s.state, s.created_at, s.pid = d["state"], d["created_at"], d["pid"]
             s.ip, s.pod_network = d.get("ip", ""), d.get("pod_network", False)
+            s.own_ns, s.port_mappings = d.get("own_ns", False), d.get("port_mappings") or []
             if s.state == C.SANDBOX_READY and not _alive(s.pid):
                 s.state = C.SANDBOX_NOTREADY
             self.sandboxes[s.id] = s
@@ -301,12 +311,26 @@ class RocShim:
         log_dir = cfg.log_directory or os.path.join(self.state_dir, "logs", sid)
         os.makedirs(log_dir, exist_ok=True)
         sysctls = dict(cfg.linux.sysctls) if cfg.HasField("linux") else {}
-        if sysctls:
-            # every rocshim sandbox shares the host's ipc and net namespaces (process containers):
-            # writing a namespaced sysctl would change the host, so the sandbox is refused
-            raise ValueError(f"sysctls {', '.join(sorted(sysctls))}: rocshim sandboxes share the host ipc/net namespaces "
-                             f"(isolation={self.isolation}); refusing to change host kernel parameters")
+        nso = None
+        try:
+            nso = cfg.linux.security_context.namespace_options
+        except AttributeError:
+            pass
+        host_net = bool(nso.host_network) if nso is not None else True
+        host_ipc = bool(nso.host_ipc) if nso is not None else True
+        own_ns = self.pod_namespaces and not host_net and not isinstance(self.network, HostNetwork)
+        for k in sysctls:
+            # a namespaced sysctl is only safe inside the pod's own namespace: net.* needs the
+            # pod network namespace, the IPC ones (kernel.shm*, kernel.msg*, kernel.sem,
+            # fs.mqueue.*) its IPC namespace — otherwise it would change the host
+            ipc_key = not k.startswith("net.")
+            if not own_ns or (ipc_key and host_ipc):
+                raise ValueError(f"sysctl {k}: the sandbox shares the host's {'ipc' if ipc_key else 'net'} namespace "
+                                 f"(pod namespaces={'on' if self.pod_namespaces else 'off'}); refusing to change host "
+                                 f"kernel parameters")
         s = Sandbox(sid, cfg.SerializeToString(), meta, dict(cfg.labels), dict(cfg.annotations), log_dir)
+        s.port_mappings = [{"host_ip": pm.host_ip, "host_port": pm.host_port, "container_port": pm.container_port,
+                            "protocol": {0: "TCP", 1: "UDP"}.get(int(pm.protocol), "TCP")} for pm in cfg.port_mappings]
         os.makedirs(os.path.join(self.state_dir, "rootfs", sid), exist_ok=True)
         dns = cfg.dns_config if cfg.HasField("dns_config") else None
         if dns is not None and (dns.servers or dns.searches or dns.options):
@@ -318,23 +342,32 @@ class RocShim:
                 lines.append("options " + " ".join(dns.options))
             with open(os.path.join(self.state_dir, "rootfs", sid, "resolv.conf"), "w") as f:
                 f.write("\n".join(lines) + "\n")
-        proc = await spawn([self.pause_bin])
+        if own_ns:
+            # the pause process owns the pod's namespaces; sysctls are written inside them
+            argv = [self.nsexec_bin, "--no-namespaces", "--unshare", "net,uts" if host_ipc else "net,ipc,uts"]
+            if cfg.hostname:
+                argv += ["--hostname", cfg.hostname]
+            for k, v in sorted(sysctls.items()):
+                argv += ["--sysctl", f"{k}={v}"]
+            proc = await spawn(argv + ["--", self.pause_bin])
+        else:
+            proc = await spawn([self.pause_bin])
         s.proc, s.pid = proc, proc.pid
-        host_net = True
-        try:
-            host_net = cfg.linux.security_context.namespace_options.host_network
-        except AttributeError:
-            pass
+        s.own_ns = own_ns
         if host_net or isinstance(self.network, HostNetwork):
             s.ip = self.network.node_ip
         else:
             try:
+                if own_ns:
+                    await _wait_ns(s.pid, proc)
                 s.ip = await self.network.setup(sid, meta, f"/proc/{s.pid}/ns/net")
                 s.pod_network = True
+                if own_ns:
+                    await self.hostports.add(sid, s.ip, s.port_mappings)
             except Exception:
+                await self.network.teardown(sid, meta, f"/proc/{s.pid}/ns/net")  # release a partial ADD
                 _kill(s.pid, signal.SIGKILL)
                 await proc.wait()
-                await self.network.teardown(sid, meta, f"/proc/{s.pid}/ns/net")  # release a partial ADD
                 raise
         self.sandboxes[sid] = s
         self._ckpt("sandboxes", s)
@@ -346,6 +379,12 @@ class RocShim:
         if s is None:
             return
         await asyncio.gather(*(self.stop_container(c.id, 2) for c in list(self.containers.values()) if c.sandbox_id == sid))
+        await self.hostports.remove(sid)
+        if s.pod_network and s.own_ns and s.pid and _alive(s.pid):
+            # the pod's network namespace dies with pause: tear the network down first
+            # (dockershim StopPodSandbox: TearDownPod before stopping the infra container)
+            await self.network.teardown(sid, s.meta, f"/proc/{s.pid}/ns/net")
+            s.pod_network = False
         if s.pid and _alive(s.pid):
             _kill(s.pid, signal.SIGTERM)
             if s.proc is not None:
@@ -456,19 +495,32 @@ class RocShim:
             return p
         raise ValueError(f"unsupported seccomp profile {spec!r}")
 
+    def _join_args(self, c: Container) -> list[str]:
+        s = self.sandboxes.get(c.sandbox_id)
+        if s is None or not s.own_ns or not s.pid:
+            return []
+        out = []
+        for t in ("net", "ipc", "uts"):
+            p = f"/proc/{s.pid}/ns/{t}"
+            if t == "ipc" and os.path.exists(p) and os.path.realpath(p) == os.path.realpath("/proc/self/ns/ipc"):
+                continue     # hostIPC pod: nothing to join
+            out += ["--join", f"{t}:{p}"]
+        return out
+
     def _launch_argv(self, c: Container) -> list[str]:
         sec, aa = c.resources.get("seccomp_profile"), c.resources.get("apparmor_profile")
         cpuset = c.resources.get("cpuset") or ""
+        join = self._join_args(c)
         if self.isolation != "namespaces":
-            if not (sec or aa or cpuset):
+            if not (sec or aa or cpuset or join):
                 return c.argv
-            return ([self.nsexec_bin, "--no-namespaces"] + (["--seccomp", sec] if sec else []) +
+            return ([self.nsexec_bin, "--no-namespaces"] + join + (["--seccomp", sec] if sec else []) +
                     (["--apparmor", aa] if aa else []) + (["--cpuset", cpuset] if cpuset else []) + ["--"] + c.argv)
         # (env isolation: the OOM score is applied to the spawned process directly, see start_container)
         keep = [d["host_path"] for d in c.devices if "/dri/" in d["host_path"]]
         # QoS hierarchy from the kubelet (kubepods/[burstable|besteffort]/pod<uid>), else per sandbox
         cg = self._cgroup_of(c)
-        a = [self.nsexec_bin, "--dev-root", self.dev_root, "--cgroup", cg]
+        a = [self.nsexec_bin, "--dev-root", self.dev_root, "--cgroup", cg] + join
         if c.resources.get("cpu_shares"):
             a += ["--cpu-weight", str(_shares_to_weight(c.resources["cpu_shares"]))]
         if c.resources.get("oom_score_adj"):
@@ -693,6 +745,25 @@ def _set_oom_score_adj(pid: int, adj: int):
             f.write(str(adj))
     except OSError:
         pass
+
+
+async def _wait_ns(pid: int, proc, timeout: float = 5.0):
+    """The pause launcher execs pause only after unsharing: wait until its net namespace is
+    not the launcher's parent's (or the process died)."""
+    mine = os.path.realpath("/proc/self/ns/net")
+    loop = asyncio.get_running_loop()
+    end = loop.time() + timeout
+    while loop.time() < end:
+        try:
+            if os.readlink(f"/proc/{pid}/ns/net") != os.readlink("/proc/self/ns/net") and \
+                    os.readlink(f"/proc/{pid}/exe").endswith("/pause"):
+                return
+        except OSError:
+            raise RuntimeError(f"pod sandbox process {pid} died while setting up its namespaces")
+        if proc.returncode is not None:
+            raise RuntimeError(f"pod sandbox process exited with {proc.returncode} while setting up its namespaces")
+        await asyncio.sleep(0.005)
+    raise RuntimeError(f"pod sandbox {pid} did not enter its own namespaces within {timeout}s (mine={mine})")
 
 
 def sandbox_meta(s) -> "C.PodSandboxMetadata":

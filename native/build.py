@@ -55,6 +55,8 @@ def targets(sanitize=False, cpu_only=False):
          ["g++", "-O2", "-std=c++17", n("native/seccomp_check.cpp"), "-o", "{out}"]),
         (n(BIN, "cni", "amdkube-cni"), [n("native/cni_ipam.cpp")],
          ["g++", "-O2", "-std=c++17", n("native/cni_ipam.cpp"), "-o", "{out}"]),
+        (n(BIN, "cni", "amdkube-bridge"), [n("native/cni_bridge.cpp")],
+         ["g++", "-O2", "-std=c++17", "-Wall", n("native/cni_bridge.cpp"), "-o", "{out}"]),
     ]
     if sanitize:
         san = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-g"]

@@ -22,6 +22,12 @@
 //  6. --apparmor NAME: request the AppArmor profile transition on exec (`exec NAME` into
 //     /proc/self/attr/apparmor/exec, or the pre-5.x /proc/self/attr/exec);
 //  7. exec the container's argv.
+// Pod namespaces (rocshim pod networking, applied first, in both modes):
+//   --unshare net,ipc,uts   the pod sandbox (pause) gets fresh network/IPC/UTS namespaces;
+//   --hostname NAME         the pod's hostname in its new UTS namespace;
+//   --join net:PATH ...     a container joins its sandbox's namespaces (/proc/<pause>/ns/<type>);
+//   --sysctl KEY=VALUE      namespaced sysctls (net.*, kernel.shm*, ...) written after the
+//                           namespaces are set up, so they apply to the pod, never the host.
 // `--no-namespaces` skips steps 1-4 (unprivileged `env` isolation still gets seccomp/AppArmor).
 // Any isolation step that fails is fatal (exit 126): a container never silently runs with
 // more devices, or fewer syscall restrictions, than it was given.
@@ -99,11 +105,61 @@ static int mkdir_p(const std::string& p) {
   return 0;
 }
 
+static int ns_flag(const std::string& t) {
+  if (t == "net") return CLONE_NEWNET;
+  if (t == "ipc") return CLONE_NEWIPC;
+  if (t == "uts") return CLONE_NEWUTS;
+  return 0;
+}
+
+static int pod_namespaces(const std::vector<std::string>& joins, const std::string& unshare_list,
+                          const std::string& hostname, const std::vector<std::string>& sysctls) {
+  for (auto& j : joins) {   // type:path
+    size_t c = j.find(':');
+    int flag = c == std::string::npos ? 0 : ns_flag(j.substr(0, c));
+    if (!flag) {
+      std::fprintf(stderr, "amdkube-nsexec: bad --join %s\n", j.c_str());
+      return 126;
+    }
+    int fd = open(j.substr(c + 1).c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return die(("open namespace " + j).c_str());
+    if (setns(fd, flag) < 0) return die(("setns " + j).c_str());
+    close(fd);
+  }
+  if (!unshare_list.empty()) {
+    int flags = 0;
+    std::stringstream ss(unshare_list);
+    std::string t;
+    while (std::getline(ss, t, ',')) {
+      int f = ns_flag(t);
+      if (!f) {
+        std::fprintf(stderr, "amdkube-nsexec: bad --unshare %s\n", t.c_str());
+        return 126;
+      }
+      flags |= f;
+    }
+    if (unshare(flags) < 0) return die(("unshare " + unshare_list).c_str());
+  }
+  if (!hostname.empty() && sethostname(hostname.data(), hostname.size()) < 0) return die("sethostname");
+  for (auto& kv : sysctls) {
+    size_t eq = kv.find('=');
+    if (eq == std::string::npos || eq == 0 || kv.find("..") != std::string::npos || kv[0] == '/') {
+      std::fprintf(stderr, "amdkube-nsexec: bad --sysctl %s\n", kv.c_str());
+      return 126;
+    }
+    std::string key = kv.substr(0, eq);
+    for (auto& ch : key) if (ch == '.') ch = '/';
+    if (!write_file("/proc/sys/" + key, kv.substr(eq + 1))) return die(("sysctl " + kv.substr(0, eq)).c_str());
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   std::string dev_root = "/dev", cgroup, mem_max, cpu_max, cpu_weight, oom_adj;
   std::vector<std::string> keep, binds;
   bool hide_kfd = false, no_ns = false;
-  std::string seccomp_profile, apparmor, cpuset;
+  std::string seccomp_profile, apparmor, cpuset, unshare_list, hostname;
+  std::vector<std::string> joins, sysctls;
   int i = 1;
   for (; i < argc; ++i) {
     std::string a = argv[i];
@@ -123,6 +179,10 @@ int main(int argc, char** argv) {
     else if (a == "--apparmor" && i + 1 < argc) apparmor = argv[++i];
     else if (a == "--no-namespaces") no_ns = true;
     else if (a == "--cpuset" && i + 1 < argc) cpuset = argv[++i];
+    else if (a == "--unshare" && i + 1 < argc) unshare_list = argv[++i];
+    else if (a == "--hostname" && i + 1 < argc) hostname = argv[++i];
+    else if (a == "--join" && i + 1 < argc) joins.push_back(argv[++i]);
+    else if (a == "--sysctl" && i + 1 < argc) sysctls.push_back(argv[++i]);
     else {
       std::fprintf(stderr, "amdkube-nsexec: unknown argument %s\n", a.c_str());
       return 126;
@@ -152,6 +212,7 @@ int main(int argc, char** argv) {
     }
     if (sched_setaffinity(0, sizeof(set), &set) < 0) return die("sched_setaffinity");
   }
+  if (int rc = pod_namespaces(joins, unshare_list, hostname, sysctls)) return rc;
   if (no_ns) {
     if (!apparmor.empty() && !apparmor_onexec(apparmor)) return die(("AppArmor profile " + apparmor).c_str());
     std::string err;

@@ -280,13 +280,16 @@ def test_container_gc_keeps_newest_dead_container_per_pod_container():
                            "default")
             await wait_pod(c, "default", "crash", ("Running", "Pending", "Failed"), 20)
             uid = (await c.get("pods", "crash", "default"))["metadata"]["uid"]
-            # two more attempts of the same container, created the way a restart does
-            for _ in range(60):
+            # two more attempts of the same container, created the way a restart does; wait for
+            # the kubelet's own first (immediate) restart to exit too, so the crash-loop back-off
+            # (10 s) keeps it from adding attempts while the GC runs
+            for _ in range(100):
                 dead = [x for x in lc.shim.containers.values() if x.labels.get("io.kubernetes.pod.uid") == uid and x.state == 2]
-                if dead:
+                if len(dead) >= 2:
                     break
                 await asyncio.sleep(0.05)
-            assert dead
+            assert len(dead) >= 2
+            dead.sort(key=lambda x: x.created_at)
             sid = dead[0].sandbox_id
             import copy
             for i in range(2):
