@@ -119,19 +119,54 @@ class BareMetalRoutes:
 
 
 class BareMetalInstances:
-    def __init__(self, client=None):
+    """cloud.go Instances for on-prem MI355X hosts. With an `instances` inventory in the cloud
+    config ({node: {addresses, providerID, instanceType, zone, region}} — what a bare-metal
+    provisioner such as an Ironic/Metal3 inventory knows) every answer comes from it and a node
+    missing from it does not exist; without one the Node objects are the inventory."""
+
+    def __init__(self, client=None, inventory: dict | None = None):
         self.client = client
+        self.inventory = dict(inventory or {})
+
+    async def _node(self, name):
+        return await self.client.get_or_none("nodes", name) if self.client else None
 
     async def node_addresses(self, node_name: str) -> list[dict]:
-        n = await self.client.get_or_none("nodes", node_name) if self.client else None
-        return list(((n or {}).get("status") or {}).get("addresses") or [])
+        if self.inventory:
+            inv = self.inventory.get(node_name)
+            if inv is None:
+                raise LookupError(f"instance {node_name} not found")
+            return [dict(a) for a in inv.get("addresses") or []]
+        return list((((await self._node(node_name)) or {}).get("status") or {}).get("addresses") or [])
 
     async def instance_exists(self, node_name: str) -> bool:
-        return (await self.client.get_or_none("nodes", node_name) if self.client else None) is not None
+        if self.inventory:
+            return node_name in self.inventory
+        return (await self._node(node_name)) is not None
+
+    async def instance_exists_by_provider_id(self, provider_id: str) -> bool:
+        if self.inventory:
+            return any(self.provider_id_of(n) == provider_id for n in self.inventory)
+        return True
+
+    def provider_id_of(self, node_name: str) -> str:
+        inv = self.inventory.get(node_name) or {}
+        return inv.get("providerID") or f"baremetal://{node_name}"
+
+    async def instance_id(self, node_name: str) -> str:
+        if self.inventory and node_name not in self.inventory:
+            raise LookupError(f"instance {node_name} not found")
+        return self.provider_id_of(node_name)
 
     async def instance_type(self, node_name: str) -> str:
-        n = await self.client.get_or_none("nodes", node_name) if self.client else None
+        if self.inventory:
+            return (self.inventory.get(node_name) or {}).get("instanceType", "amd-mi355x-8gpu")
+        n = await self._node(node_name)
         return m.labels_of(n or {}).get("beta.kubernetes.io/instance-type", "amd-mi355x-8gpu")
+
+    def zone_of(self, node_name: str, default: "Zone") -> "Zone":
+        inv = self.inventory.get(node_name) or {}
+        return Zone(inv.get("zone", default.failure_domain), inv.get("region", default.region))
 
 
 class BareMetal(Interface):
@@ -142,7 +177,7 @@ class BareMetal(Interface):
         self._lb = BareMetalLoadBalancer(config.get("loadBalancerIPRange", ""))
         self._routes = BareMetalRoutes(config.get("programRoutes"))
         self._zone = Zone(config.get("zone", ""), config.get("region", ""))
-        self._instances = BareMetalInstances()
+        self._instances = BareMetalInstances(inventory=config.get("instances"))
 
     def initialize(self, client=None):
         self._instances.client = client
@@ -158,6 +193,22 @@ class BareMetal(Interface):
 
     def instances(self):
         return self._instances
+
+    def zone_for_node(self, node_name: str) -> Zone:
+        return self._instances.zone_of(node_name, self._zone)
+
+    def labels_for_volume(self, pv: dict) -> dict:
+        """PVLabeler: node-local volumes (local, hostPath) carry the cluster's zone/region so the
+        scheduler's NoVolumeZoneConflict keeps their pods in the zone."""
+        spec = pv.get("spec") or {}
+        if not (spec.get("local") or spec.get("hostPath")):
+            return {}
+        out = {}
+        if self._zone.failure_domain:
+            out["failure-domain.beta.kubernetes.io/zone"] = self._zone.failure_domain
+        if self._zone.region:
+            out["failure-domain.beta.kubernetes.io/region"] = self._zone.region
+        return out
 
 
 class Fake(Interface):
@@ -205,6 +256,8 @@ class Fake(Interface):
                 outer.calls.append("delete-route")
                 outer.route_table.pop(route.name, None)
         self._lb, self._routes = LB(), Routes()
+        self._instances = BareMetalInstances(inventory=(config or {}).get("instances") or {})
+        self.volume_labels: dict[str, dict] = {}
 
     def load_balancer(self):
         return self._lb
@@ -214,6 +267,16 @@ class Fake(Interface):
 
     def zones(self):
         return Zone("fake-zone", "fake-region")
+
+    def instances(self):
+        return self._instances
+
+    def zone_for_node(self, node_name: str) -> Zone:
+        return self._instances.zone_of(node_name, Zone("fake-zone", "fake-region"))
+
+    def labels_for_volume(self, pv: dict) -> dict:
+        self.calls.append("labels-for-volume")
+        return dict(self.volume_labels.get(m.name_of(pv), {}))
 
 
 _PROVIDERS = {"baremetal": BareMetal, "fake": Fake}

@@ -203,6 +203,51 @@ def controller_manager(argv):
     _run_forever(mk)
 
 
+def cloud_controller_manager(argv):
+    """cmd/cloud-controller-manager: the cloud-specific control loops (cloud-node, service,
+    route, persistentvolume-labeler) split out of kube-controller-manager; kubelets run with
+    --cloud-provider=external and wait, tainted, to be initialised by it."""
+    ap = argparse.ArgumentParser("amdkube cloud-controller-manager")
+    ap.add_argument("--master", "--server", dest="server", default="http://127.0.0.1:8080")
+    ap.add_argument("--kubeconfig", default=None)
+    ap.add_argument("--token", default=None)
+    ap.add_argument("--cloud-provider", required=True, help="baremetal | fake")
+    ap.add_argument("--cloud-config", default=None, help="provider config (baremetal: loadBalancerIPRange, zone, region, "
+                                                         "instances inventory)")
+    ap.add_argument("--controllers", default="*", help="'*' = cloud-node,service,route,persistentvolume-labeler")
+    ap.add_argument("--allocate-node-cidrs", default="false")
+    ap.add_argument("--configure-cloud-routes", default="true")
+    ap.add_argument("--cluster-name", default="kubernetes")
+    ap.add_argument("--node-status-update-frequency", type=float, default=300.0)
+    ap.add_argument("--node-monitor-period", type=float, default=5.0)
+    ap.add_argument("--leader-elect", default="false")
+    ap.add_argument("-v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "cloud-controller-manager")
+    import yaml
+    from ..cloudprovider import get_cloud_provider
+    from ..controllers import CLOUD_CONTROLLERS, ControllerManager, Options
+    cfg = yaml.safe_load(open(a.cloud_config)) if a.cloud_config else None
+    opts = Options(cloud=get_cloud_provider(a.cloud_provider, cfg), cluster_name=a.cluster_name,
+                   allocate_node_cidrs=a.allocate_node_cidrs == "true", configure_cloud_routes=a.configure_cloud_routes == "true",
+                   extra={"node_status_update_frequency": a.node_status_update_frequency,
+                          "node_monitor_period": a.node_monitor_period})
+    names = []
+    for it in [x.strip() for x in a.controllers.split(",") if x.strip()]:
+        if it == "*":
+            names += [n for n in CLOUD_CONTROLLERS if n != "route" or (opts.allocate_node_cidrs and opts.configure_cloud_routes)]
+        elif it.startswith("-"):
+            names = [n for n in names if n != it[1:]]
+        elif it in CLOUD_CONTROLLERS:
+            names.append(it)
+        else:
+            raise SystemExit(f"unknown cloud controller {it!r} (have: {', '.join(CLOUD_CONTROLLERS)})")
+
+    async def mk():
+        return await ControllerManager(_client(a), names, a.leader_elect == "true", socket.gethostname(), options=opts).start()
+    _run_forever(mk)
+
+
 def kubelet(argv):
     ap = argparse.ArgumentParser("amdkube kubelet")
     ap.add_argument("--api-servers", "--server", dest="server", default="http://127.0.0.1:8080")
@@ -215,6 +260,9 @@ def kubelet(argv):
     ap.add_argument("--container-runtime-endpoint", default="/var/run/amdkube/rocshim.sock")
     ap.add_argument("--address", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=10250)
+    ap.add_argument("--cloud-provider", default="", help="'external': the cloud-controller-manager initialises the node")
+    ap.add_argument("--volume-plugin-dir", default=None, help="FlexVolume driver directory")
+    ap.add_argument("--enable-controller-attach-detach", default="true", choices=("true", "false"))
     ap.add_argument("--node-ip", default="127.0.0.1")
     ap.add_argument("--node-status-update-frequency", type=float, default=10.0)
     ap.add_argument("--pleg-relist-period", type=float, default=1.0)
@@ -296,6 +344,8 @@ def kubelet(argv):
                         image_gc_high_threshold=a.image_gc_high_threshold, image_gc_low_threshold=a.image_gc_low_threshold,
                         minimum_image_ttl_duration=a.minimum_image_ttl_duration,
                         config_file=a.config, dynamic_config_dir=a.dynamic_config_dir,
+                        cloud_provider=a.cloud_provider, volume_plugin_dir=a.volume_plugin_dir,
+                        enable_controller_attach_detach=a.enable_controller_attach_detach == "true",
                         tls_cert_file=a.tls_cert_file, tls_private_key_file=a.tls_private_key_file,
                         client_ca_file=a.client_ca_file, anonymous_auth=a.anonymous_auth == "true",
                         authentication_token_webhook=a.authentication_token_webhook,
@@ -615,4 +665,4 @@ COMPONENTS = {"dns": dns, "kube-dns": dns, "kubeadm": kubeadm, "proxy": proxy, "
               "controller-manager": controller_manager, "kube-controller-manager": controller_manager, "kubelet": kubelet,
               "rocshim": rocshim, "amd-device-plugin": device_plugin, "device-plugin": device_plugin,
               "amdgpu-exporter": exporter, "exporter": exporter, "hollow-node": hollow_node, "local-up": local_up,
-              "metrics-server": metrics_server}
+              "metrics-server": metrics_server, "cloud-controller-manager": cloud_controller_manager}

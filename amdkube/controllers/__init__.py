@@ -24,7 +24,7 @@ from .accounts import (BootstrapSignerController, CSRApprovingController, CSRCle
                        ServiceAccountsController, TokenCleanerController, TokensController)
 from .apps import CronJobController, ReplicationManager, StatefulSetController
 from .autoscaling import HorizontalPodAutoscalerController
-from .cloud import RouteController, ServiceLBController
+from .cloud import CloudNodeController, PersistentVolumeLabelController, RouteController, ServiceLBController
 from .lifecycle import GarbageCollector, NamespaceController, NodeLifecycleController, PodGCController
 from .networking import EndpointsController, NodeIPAMController
 from .policy import ClusterRoleAggregationController, DisruptionController, ResourceQuotaController, TTLController
@@ -90,9 +90,14 @@ ALL = {
     "pv-protection": lambda mgr, o: PVProtectionController(mgr),
     "service": lambda mgr, o: ServiceLBController(mgr, o.cloud, o.cluster_name),
     "route": lambda mgr, o: RouteController(mgr, o.cloud, o.cluster_name),
+    # cloud-controller-manager only (cmd/cloud-controller-manager/app/controllermanager.go)
+    "cloud-node": lambda mgr, o: CloudNodeController(mgr, o.cloud, o.extra.get("node_status_update_frequency", 300.0),
+                                                     o.extra.get("node_monitor_period", 5.0)),
+    "persistentvolume-labeler": lambda mgr, o: PersistentVolumeLabelController(mgr, o.cloud),
 }
 DISABLED_BY_DEFAULT = {"bootstrapsigner", "tokencleaner"}
-OPT_IN = DISABLED_BY_DEFAULT | {"nodeipam", "service", "route"}
+CLOUD_CONTROLLERS = ["cloud-node", "service", "route", "persistentvolume-labeler"]
+OPT_IN = DISABLED_BY_DEFAULT | {"nodeipam", "service", "route", "cloud-node", "persistentvolume-labeler"}
 
 
 def default_controllers(opts: Options) -> list[str]:

@@ -140,6 +140,7 @@ class KubeletConfig:
     volume_mount_timeout: float = 120.0               # WaitForAttachAndMount timeout (s)
     volume_reconcile_period: float = 2.0              # reconciler loop period (s)
     volume_remount_period: float = 60.0               # re-render secret/configMap/downwardAPI/projected content (s)
+    cloud_provider: str = ""                          # --cloud-provider ("external": cloud-controller-manager initialises the node)
 
 
 class PodWorker:
@@ -403,8 +404,18 @@ class Kubelet:
     async def register_node(self):
         labels = {"kubernetes.io/hostname": self.node_name, "beta.kubernetes.io/os": "linux",
                   "beta.kubernetes.io/arch": "amd64", **self.cfg.node_labels}
-        node = {"apiVersion": "v1", "kind": "Node", "metadata": {"name": self.node_name, "labels": labels},
-                "spec": {"taints": list(self.cfg.register_with_taints)} if self.cfg.register_with_taints else {},
+        taints = list(self.cfg.register_with_taints)
+        ann = {}
+        if self.cfg.cloud_provider == "external":
+            # kubelet_node_status.go: an external cloud provider initialises the node (providerID,
+            # addresses, zone) — register tainted until the cloud-controller-manager has done so,
+            # and tell it which address the operator chose
+            taints.append({"key": "node.cloudprovider.kubernetes.io/uninitialized", "value": "true", "effect": "NoSchedule"})
+            if self.cfg.node_ip:
+                ann["alpha.kubernetes.io/provided-node-ip"] = self.cfg.node_ip
+        node = {"apiVersion": "v1", "kind": "Node", "metadata": {"name": self.node_name, "labels": labels,
+                                                                "annotations": ann},
+                "spec": {"taints": taints} if taints else {},
                 "status": self._node_status_body({})}
         node["status"].pop("_removed", None)
         try:
@@ -455,6 +466,8 @@ class Kubelet:
         in_use = self.volume_manager.volumes_in_use()
         if in_use or prev.get("volumesInUse"):
             st["volumesInUse"] = in_use or None     # attachable volumes mounted or about to be (safe detach)
+        if self.cfg.cloud_provider == "external":
+            del st["addresses"]          # the cloud-controller-manager owns them
         st["_removed"] = removed
         if self.cfg.cgroup_root and "pods" in self.cfg.enforce_node_allocatable.split(",") and \
                 self._pods_cgroup_enforced != (alloc.get("cpu"), alloc.get("memory")):
