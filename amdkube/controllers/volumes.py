@@ -149,6 +149,15 @@ class PersistentVolumeBinderController(Controller):
             await self._finish_bind(pvc, pv)
             return
         pv = find_best_match(pvc, self.pv_inf.list())
+        sc0 = self._class(claim_class(pvc))
+        if sc0 is not None and sc0.get("volumeBindingMode") == "WaitForFirstConsumer":
+            # delayed binding (VolumeScheduling): the scheduler picks the volume together with
+            # the pod's node and pre-binds it (claimRef); only such a volume completes the claim
+            ref = ((pv or {}).get("spec") or {}).get("claimRef") or {}
+            if pv is None or ref.get("name") != name or ref.get("namespace") != ns:
+                if (pvc.get("status") or {}).get("phase") != "Pending":
+                    await self.client.patch("persistentvolumeclaims", name, {"status": {"phase": "Pending"}}, ns, sub="status")
+                return
         if pv is None:
             sc = self._class(claim_class(pvc))
             if sc is not None and sc.get("provisioner") in HOSTPATH_PROVISIONERS:

@@ -47,8 +47,11 @@ class Context:
 
 class GenericScheduler:
     def __init__(self, cache, predicates: list[str], priorities: dict[str, int], extenders=(), use_topology=True,
-                 trace_threshold: float = 0.1):
+                 trace_threshold: float = 0.1, volumes=None, volume_scheduling: bool = False):
         self.cache = cache
+        self.volumes = volumes                  # scheduler/volumes.VolumeLister (claims, volumes, classes)
+        self.volume_scheduling = volume_scheduling
+        self.volume_binds: dict[str, list] = {}  # pod key -> [(pvc, pv)] to pre-bind before the pod
         names = [p for p in ORDER if p in predicates] + [p for p in predicates if p not in ORDER]
         self.predicates = [(n, PREDICATES[n]) for n in names]
         self.priorities = [(n, PRIORITIES[n], w) for n, w in priorities.items() if w]
@@ -74,6 +77,8 @@ class GenericScheduler:
         if pi.ext_error:
             return None
         spec = pi.spec
+        if any("persistentVolumeClaim" in v for v in spec.get("volumes") or []):
+            return None     # the answer depends on claim/volume state, not just the node
         import json as _json
         rel = {"c": [(c.get("resources"), c.get("ports")) for c in spec.get("containers") or []],
                "i": [c.get("resources") for c in spec.get("initContainers") or []],
@@ -181,6 +186,10 @@ class GenericScheduler:
         """Returns (node name, extendedResourceBinding). Raises FitError."""
         trace = Trace(f"Scheduling {m.key_of(pod)}")
         pi = PodInfo(pod)
+        if (pod.get("spec") or {}).get("volumes"):
+            from .volumes import pod_volumes
+            pi.lister, pi.volume_scheduling = self.volumes, self.volume_scheduling
+            pi.vol = pod_volumes(pod, self.volumes)
         nodes = self.cache.ready_nodes()
         if not nodes:
             raise FitError(pod, 0, {})
@@ -198,6 +207,13 @@ class GenericScheduler:
         binding = extended.allocate(pi, host, self.use_topology) if pi.ext else {}
         if binding is None:
             raise FitError(pod, len(nodes), {host.name: ["device allocation failed"]})
+        vol = getattr(pi, "vol", None)
+        if vol is not None and vol.delayed and self.volume_scheduling:
+            from .volumes import match_delayed
+            pairs = match_delayed(vol.delayed, self.volumes, host.labels)
+            if pairs is None:
+                raise FitError(pod, len(nodes), {host.name: ["node(s) didn't find available persistent volumes to bind"]})
+            self.volume_binds[m.key_of(pod)] = pairs
         trace.log_if_long(self.trace_threshold)
         return host.name, binding
 

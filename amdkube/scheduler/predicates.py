@@ -4,9 +4,9 @@ Reference: plugin/pkg/scheduler/algorithm/predicates/predicates.go — PodFitsRe
 PodFitsHost, PodFitsHostPorts, PodMatchNodeSelector, GeneralPredicates (:965-1020),
 PodToleratesNodeTaints, CheckNodeCondition, CheckNodeMemoryPressure/DiskPressure,
 NoDiskConflict, MatchInterPodAffinity; registered names (policy-file compatibility) from
-algorithmprovider/defaults/defaults.go:119-215. Cloud-volume predicates (NoVolumeZoneConflict,
-Max{EBS,GCEPD,AzureDisk}VolumeCount, CheckVolumeBinding) are registered as always-fit:
-amdkube nodes carry no cloud volumes (SURVEY U26/U27 are P2).
+algorithmprovider/defaults/defaults.go:119-215. The volume predicates (NoVolumeZoneConflict,
+Max{EBS,GCEPD,AzureDisk}VolumeCount, CheckVolumeBinding) live in scheduler/volumes.py and read
+the claims/volumes the scheduler resolved for the pod (`pi.vol`).
 
 A PodInfo pre-computes everything derived from the pod once per scheduling attempt, so the
 per-node loop is dictionary lookups only.
@@ -164,13 +164,15 @@ def _vol_ids(pod):
 
 
 def no_disk_conflict(pi, ni, ctx=None):
+    """isVolumeConflict: the same GCE PD / RBD image / iSCSI IQN may be shared only when every
+    user mounts it read-only; an AWS EBS volume attaches to one instance, so never twice."""
     mine = _vol_ids(pi.pod)
     if not mine:
         return OK
     for p in ni.pods.values():
         for kind, vid, ro in _vol_ids(p):
             for k2, v2, ro2 in mine:
-                if kind == k2 and vid == v2 and not (ro and ro2):
+                if kind == k2 and vid == v2 and (kind == "awsElasticBlockStore" or not (ro and ro2)):
                     return _fail("node(s) had no available disk")
     return OK
 
@@ -231,6 +233,51 @@ def always_fit(pi, ni, ctx=None):
     return OK
 
 
+def no_volume_zone_conflict(pi, ni, ctx=None):
+    vol = getattr(pi, "vol", None)
+    if vol is None:
+        return OK
+    if vol.missing:
+        return _fail(f'persistentvolumeclaim "{vol.missing[0]}" not found')
+    from .volumes import no_volume_zone_conflict as zc
+    return OK if zc(vol.bound, ni.labels) else _fail("node(s) had no available volume zone")
+
+
+def _max_pd(kind):
+    def pred(pi, ni, ctx=None):
+        from .volumes import MAX_PD, max_pd_limit, pod_volumes
+        vol = getattr(pi, "vol", None)
+        idk = MAX_PD[kind][0]
+        mine = {src.get(idk) for k, src in (vol.sources if vol is not None else []) if k == kind}
+        if not mine:
+            return OK             # the reference's early exit: the pod adds no such disk
+        have = set()
+        for p in ni.pods.values():
+            for k, src in pod_volumes(p, getattr(pi, "lister", None)).sources:
+                if k == kind:
+                    have.add(src.get(idk))
+        if len(have | mine) > max_pd_limit(kind):
+            return _fail("node(s) exceed max volume count")
+        return OK
+    pred.__name__ = f"max_{kind}_count"
+    return pred
+
+
+def check_volume_binding(pi, ni, ctx=None):
+    vol = getattr(pi, "vol", None)
+    if vol is None or not getattr(pi, "volume_scheduling", False):
+        return OK
+    from .volumes import match_delayed, pv_node_affinity_ok
+    if vol.unbound:
+        return _fail("pod has unbound PersistentVolumeClaims")
+    for pvc, pv in vol.bound:
+        if not pv_node_affinity_ok(pv, ni.labels):
+            return _fail("node(s) had volume node affinity conflict")
+    if vol.delayed and match_delayed(vol.delayed, pi.lister, ni.labels) is None:
+        return _fail("node(s) didn't find available persistent volumes to bind")
+    return OK
+
+
 PREDICATES = {
     "PodFitsResources": pod_fits_resources,
     "PodFitsHost": pod_fits_host,
@@ -246,11 +293,11 @@ PREDICATES = {
     "CheckNodeDiskPressure": check_node_disk_pressure,
     "NoDiskConflict": no_disk_conflict,
     "MatchInterPodAffinity": match_inter_pod_affinity,
-    "NoVolumeZoneConflict": always_fit,
-    "MaxEBSVolumeCount": always_fit,
-    "MaxGCEPDVolumeCount": always_fit,
-    "MaxAzureDiskVolumeCount": always_fit,
-    "CheckVolumeBinding": always_fit,
+    "NoVolumeZoneConflict": no_volume_zone_conflict,
+    "MaxEBSVolumeCount": _max_pd("awsElasticBlockStore"),
+    "MaxGCEPDVolumeCount": _max_pd("gcePersistentDisk"),
+    "MaxAzureDiskVolumeCount": _max_pd("azureDisk"),
+    "CheckVolumeBinding": check_volume_binding,
 }
 
 # evaluation order (cheap → expensive), predicates.go predicatesOrdering

@@ -67,7 +67,10 @@ class Scheduler:
             prios = {k: v for k, v in prios.items() if k != "GPUTopologyPriority"}
         self.extenders = [HTTPExtender(e) for e in exts]
         self.cache = SchedulerCache()
-        self.algo = GenericScheduler(self.cache, preds, prios, self.extenders, use_topology=self.gates("GPUTopologyScheduling"))
+        from .volumes import VolumeLister
+        self.volumes = VolumeLister()
+        self.algo = GenericScheduler(self.cache, preds, prios, self.extenders, use_topology=self.gates("GPUTopologyScheduling"),
+                                     volumes=self.volumes, volume_scheduling=self.gates("VolumeScheduling"))
         self.queue = SchedulingQueue(self.gates("PodPriority"))
         self.recorder = EventRecorder(client, self.name)
         self.leader_elect = leader_elect
@@ -129,6 +132,11 @@ class Scheduler:
         else:
             self.queue.delete(pod)
 
+    def _on_volume_update(self, old, new):
+        if new.get("kind") == "PersistentVolume" and ((new.get("spec") or {}).get("claimRef")):
+            self.volumes.assumed.pop(m.name_of(new), None)     # our pre-binding is visible now
+        self.queue.move_all_to_active()
+
     def _on_node(self, node):
         self.cache.add_node(node)
         self.queue.move_all_to_active()
@@ -165,8 +173,18 @@ class Scheduler:
                                   on_delete=lambda n: self.cache.remove_node(n))
         self.pod_inf = Informer(self.client, "pods")
         self.pod_inf.add_handler(on_add=self._on_pod_add, on_update=self._on_pod_update, on_delete=self._on_pod_delete)
+        # claims, volumes and classes for the volume predicates; a claim or volume change may make
+        # an unschedulable pod schedulable
+        self.vol_infs = [Informer(self.client, r) for r in ("persistentvolumeclaims", "persistentvolumes", "storageclasses")]
+        self.volumes._pvcs, self.volumes._pvs, self.volumes._classes = self.vol_infs
+        for inf in self.vol_infs[:2]:
+            inf.add_handler(on_add=lambda o: self.queue.move_all_to_active(), on_update=self._on_volume_update)
+        for inf in self.vol_infs:
+            inf.start()
         self.node_inf.start()
         await self.node_inf.wait_synced(30)
+        for inf in self.vol_infs:
+            await inf.wait_synced(30)
         self.pod_inf.start()
         await self.pod_inf.wait_synced(30)
 
@@ -175,7 +193,7 @@ class Scheduler:
             t.cancel()
         for t in list(self._binds):
             t.cancel()
-        for inf in (self.pod_inf, self.node_inf):
+        for inf in (self.pod_inf, self.node_inf, *getattr(self, "vol_infs", [])):
             if inf:
                 await inf.stop()
         await self.recorder.stop()
@@ -249,15 +267,24 @@ class Scheduler:
             self.cache.assume_pod(assumed)
         except KeyError:
             return
-        t = asyncio.create_task(self._bind(pod, assumed, host, binding, t0))
+        vbinds = self.algo.volume_binds.pop(key, [])
+        for pvc, pv in vbinds:
+            self.volumes.assumed[m.name_of(pv)] = m.key_of(pvc)
+        t = asyncio.create_task(self._bind(pod, assumed, host, binding, t0, vbinds))
         self._binds.add(t)
         t.add_done_callback(self._binds.discard)
 
-    async def _bind(self, pod, assumed, host, binding, t0):
+    async def _bind(self, pod, assumed, host, binding, t0, vbinds=()):
         POD_TRACE(m.uid_of(pod), "sched_assumed")
         async with self.bind_sem:
             tb = time.perf_counter()
             try:
+                # scheduler_binder.go BindPodVolumes: pre-bind the chosen PVs to their claims;
+                # the PV controller completes the binding
+                for pvc, pv in vbinds:
+                    await self.client.patch("persistentvolumes", m.name_of(pv), {"spec": {"claimRef": {
+                        "kind": "PersistentVolumeClaim", "apiVersion": "v1", "namespace": m.namespace_of(pvc),
+                        "name": m.name_of(pvc), "uid": m.uid_of(pvc)}}})
                 bound_by_ext = False
                 for ext in self.extenders:
                     if ext.bind_verb:
@@ -270,6 +297,8 @@ class Scheduler:
                 self.bind_errors += 1
                 self.m_attempts.labels("error").inc()
                 self.cache.forget_pod(assumed)
+                for _pvc, pv in vbinds:
+                    self.volumes.assumed.pop(m.name_of(pv), None)
                 log.info("binding %s to %s rejected: %s", m.key_of(pod), host, e)
                 self.recorder.event(pod, "Warning", "FailedScheduling", f"Binding rejected: {e}")
                 if not (isinstance(e, m.StatusError) and (m.is_not_found(e) or "already assigned" in e.message)):
