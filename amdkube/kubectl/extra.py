@@ -296,19 +296,86 @@ def _kubeconfig_path(a):
     return getattr(a, "kubeconfig", None) or os.environ.get("KUBECONFIG") or os.path.expanduser("~/.kube/config")
 
 
+def _named(cfg, section, name, create=False, inner=None):
+    lst = cfg.setdefault(section, []) if create else (cfg.get(section) or [])
+    ent = next((x for x in lst if x.get("name") == name), None)
+    if ent is None and create:
+        ent = {"name": name, inner: {}}
+        lst.append(ent)
+    return ent
+
+
+def _file_data(path):
+    import base64
+    with open(path, "rb") as f:
+        return base64.b64encode(f.read()).decode()
+
+
+def _set_path(cfg, path: str, value):
+    """`kubectl config set PROPERTY_NAME VALUE`: dotted path where a list of named entries is
+    addressed by name (clusters.<name>.server, users.<name>.token, contexts.<name>.namespace)."""
+    parts = path.split(".")
+    cur = cfg
+    i = 0
+    while i < len(parts) - 1:
+        k = parts[i]
+        if k in ("clusters", "users", "contexts") and i + 1 < len(parts):
+            inner = {"clusters": "cluster", "users": "user", "contexts": "context"}[k]
+            ent = _named(cfg if cur is cfg else cur, k, parts[i + 1], create=value is not None, inner=inner)
+            if ent is None:
+                raise SystemExit(f"error: {path}: no {inner} named {parts[i + 1]!r}")
+            cur = ent.setdefault(inner, {})
+            i += 2
+            continue
+        cur = cur.setdefault(k, {}) if value is not None else cur.get(k, {})
+        i += 1
+    if value is None:
+        cur.pop(parts[-1], None)
+    else:
+        cur[parts[-1]] = value
+
+
 def cmd_config_sync(a):
+    """kubectl config (pkg/kubectl/cmd/config): view, current-context, get-contexts,
+    get-clusters, use-context, set-context, set-cluster, set-credentials, set, unset,
+    delete-context, delete-cluster, rename-context. Edits are written back to the kubeconfig."""
     import yaml
     path = _kubeconfig_path(a)
     sub = a.args[0] if a.args else "view"
     cfg = yaml.safe_load(open(path)) if os.path.exists(path) else {}
     cfg = cfg or {}
+    cfg.setdefault("apiVersion", "v1")
+    cfg.setdefault("kind", "Config")
+
+    def save(msg):
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            yaml.safe_dump(cfg, f, sort_keys=False)
+        os.replace(tmp, path)
+        print(msg)
+
+    def arg(i):
+        if len(a.args) <= i:
+            raise SystemExit(f"error: config {sub}: missing argument")
+        return a.args[i]
+
     if sub == "view":
         view = json.loads(json.dumps(cfg))
+        if getattr(a, "minify", False) and view.get("current-context"):
+            ctx = _named(view, "contexts", view["current-context"]) or {}
+            cc = ctx.get("context") or {}
+            view["contexts"] = [ctx] if ctx else []
+            view["clusters"] = [x for x in view.get("clusters") or [] if x.get("name") == cc.get("cluster")]
+            view["users"] = [x for x in view.get("users") or [] if x.get("name") == cc.get("user")]
         if not a.raw:
             for u in view.get("users") or []:
-                for k in ("client-key-data", "token", "client-certificate-data"):
+                for k in ("client-key-data", "token", "client-certificate-data", "password"):
                     if k in (u.get("user") or {}):
-                        u["user"][k] = "REDACTED" if k != "client-certificate-data" else "REDACTED"
+                        u["user"][k] = "REDACTED"
+            for cl in view.get("clusters") or []:
+                if "certificate-authority-data" in (cl.get("cluster") or {}):
+                    cl["cluster"]["certificate-authority-data"] = "DATA+OMITTED"
         print(yaml.safe_dump(view, sort_keys=False), end="")
     elif sub == "current-context":
         cur = cfg.get("current-context")
@@ -318,31 +385,96 @@ def cmd_config_sync(a):
     elif sub == "get-contexts":
         rows = [["CURRENT", "NAME", "CLUSTER", "AUTHINFO", "NAMESPACE"]]
         for ctx in cfg.get("contexts") or []:
+            if len(a.args) > 1 and ctx.get("name") not in a.args[1:]:
+                continue
             cc = ctx.get("context") or {}
             rows.append(["*" if ctx.get("name") == cfg.get("current-context") else "", ctx.get("name", ""),
                          cc.get("cluster", ""), cc.get("user", ""), cc.get("namespace", "")])
         print(printers.table(rows))
+    elif sub == "get-clusters":
+        print("\n".join(["NAME"] + [x.get("name", "") for x in cfg.get("clusters") or []]))
     elif sub == "use-context":
-        name = a.args[1]
-        if not any(x.get("name") == name for x in cfg.get("contexts") or []):
+        name = arg(1)
+        if _named(cfg, "contexts", name) is None:
             raise SystemExit(f"error: no context exists with the name: {name!r}")
         cfg["current-context"] = name
-        with open(path, "w") as f:
-            yaml.safe_dump(cfg, f, sort_keys=False)
-        print(f'Switched to context "{name}".')
+        save(f'Switched to context "{name}".')
     elif sub == "set-context":
-        name = a.args[1]
-        ctxs = cfg.setdefault("contexts", [])
-        ctx = next((x for x in ctxs if x.get("name") == name), None)
-        if ctx is None:
-            ctx = {"name": name, "context": {}}
-            ctxs.append(ctx)
+        name = cfg.get("current-context") if getattr(a, "current", False) else arg(1)
+        if not name:
+            raise SystemExit("error: no current context is set")
+        new = _named(cfg, "contexts", name) is None
+        ctx = _named(cfg, "contexts", name, create=True, inner="context")
         for kv in a.args[2:]:
             k, _, v = kv.lstrip("-").partition("=")
             ctx["context"][k] = v
-        with open(path, "w") as f:
-            yaml.safe_dump(cfg, f, sort_keys=False)
-        print(f'Context "{name}" modified.')
+        if getattr(a, "cfg_cluster", None):
+            ctx["context"]["cluster"] = a.cfg_cluster
+        if getattr(a, "user", None):      # --user is shared with the rolebinding generators (a list)
+            ctx["context"]["user"] = a.user[-1]
+        if a.namespace:
+            ctx["context"]["namespace"] = a.namespace
+        save(f'Context "{name}" {"created" if new else "modified"}.')
+    elif sub == "set-cluster":
+        name = arg(1)
+        new = _named(cfg, "clusters", name) is None
+        cl = _named(cfg, "clusters", name, create=True, inner="cluster")["cluster"]
+        if a.server:
+            cl["server"] = a.server
+        if a.certificate_authority:
+            if a.embed_certs:
+                cl["certificate-authority-data"] = _file_data(a.certificate_authority)
+                cl.pop("certificate-authority", None)
+            else:
+                cl["certificate-authority"] = os.path.abspath(a.certificate_authority)
+        if a.insecure_skip_tls_verify is not None:
+            cl["insecure-skip-tls-verify"] = a.insecure_skip_tls_verify == "true"
+        save(f'Cluster "{name}" {"set" if new else "modified"}.')
+    elif sub == "set-credentials":
+        name = arg(1)
+        new = _named(cfg, "users", name) is None
+        u = _named(cfg, "users", name, create=True, inner="user")["user"]
+        if getattr(a, "cfg_token", None):
+            u["token"] = a.cfg_token
+        if a.username:
+            u["username"] = a.username
+        if a.password:
+            u["password"] = a.password
+        for src, key in ((a.client_certificate, "client-certificate"), (a.client_key, "client-key")):
+            if src:
+                if a.embed_certs:
+                    u[key + "-data"] = _file_data(src)
+                    u.pop(key, None)
+                else:
+                    u[key] = os.path.abspath(src)
+        save(f'User "{name}" {"set" if new else "modified"}.')
+    elif sub == "set":
+        _set_path(cfg, arg(1), arg(2))
+        save(f'Property "{a.args[1]}" set.')
+    elif sub == "unset":
+        _set_path(cfg, arg(1), None)
+        save(f'Property "{a.args[1]}" unset.')
+    elif sub in ("delete-context", "delete-cluster"):
+        section = "contexts" if sub == "delete-context" else "clusters"
+        name = arg(1)
+        lst = cfg.get(section) or []
+        if not any(x.get("name") == name for x in lst):
+            raise SystemExit(f"error: cannot delete {section[:-1]} {name}, not in {path}")
+        cfg[section] = [x for x in lst if x.get("name") != name]
+        if section == "contexts" and cfg.get("current-context") == name:
+            print(f"warning: this removed your active context, use \"kubectl config use-context\" to select a different one")
+        save(f"deleted {section[:-1]} {name} from {path}")
+    elif sub == "rename-context":
+        old, new_name = arg(1), arg(2)
+        ctx = _named(cfg, "contexts", old)
+        if ctx is None:
+            raise SystemExit(f"error: cannot rename the context {old!r}, it's not in {path}")
+        if _named(cfg, "contexts", new_name) is not None:
+            raise SystemExit(f"error: cannot rename the context {old!r}, the context {new_name!r} already exists in {path}")
+        ctx["name"] = new_name
+        if cfg.get("current-context") == old:
+            cfg["current-context"] = new_name
+        save(f'Context "{old}" renamed to "{new_name}".')
     else:
         raise SystemExit(f"error: unknown config subcommand {sub!r}")
     return 0

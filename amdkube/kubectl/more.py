@@ -519,6 +519,20 @@ def add_arguments(sp):
     sp.add_argument("--output-version", default=None)
     sp.add_argument("--output-directory", default=None)
     sp.add_argument("--containers", action="store_true")
+    # kubectl config set-cluster / set-credentials / set-context / view --minify
+    sp.add_argument("--certificate-authority", default=None)
+    sp.add_argument("--insecure-skip-tls-verify", default=None, choices=("true", "false"))
+    sp.add_argument("--embed-certs", action="store_true")
+    sp.add_argument("--client-certificate", default=None)
+    sp.add_argument("--client-key", default=None)
+    sp.add_argument("--username", default=None)
+    sp.add_argument("--password", default=None)
+    sp.add_argument("--cluster", dest="cfg_cluster", default=None)
+    sp.add_argument("--current", action="store_true")
+    sp.add_argument("--minify", action="store_true")
+    sp.add_argument("--token", dest="cfg_token", default=None, help="set-credentials bearer token")
+    import argparse as _ap
+    sp.add_argument("--server", default=_ap.SUPPRESS, help="set-cluster: the API server URL (also the global flag)")
 
 
 COMMANDS = {"rolling-update": cmd_rolling_update, "convert": cmd_convert, "api-versions": cmd_api_versions,
