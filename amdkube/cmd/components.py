@@ -260,6 +260,7 @@ def kubelet(argv):
     ap.add_argument("--container-runtime-endpoint", default="/var/run/amdkube/rocshim.sock")
     ap.add_argument("--address", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=10250)
+    ap.add_argument("--runonce", action="store_true", help="run the static pods once, report, and exit (no API server)")
     ap.add_argument("--cloud-provider", default="", help="'external': the cloud-controller-manager initialises the node")
     ap.add_argument("--volume-plugin-dir", default=None, help="FlexVolume driver directory")
     ap.add_argument("--enable-controller-attach-detach", default="true", choices=("true", "false"))
@@ -361,6 +362,22 @@ def kubelet(argv):
             except Exception as e:
                 logging.getLogger("amdkube.kubelet").warning("no GPU stats backend: %s", e)
         return await Kubelet(_client(a, qps=a.kube_api_qps, chaos=a.chaos_chance), cfg, smi_backend=smi).start()
+    if a.runonce:
+        # runonce.go: static pods only, no API server; exit status says whether all came up
+        if not a.pod_manifest_path:
+            raise SystemExit("--runonce needs --pod-manifest-path")
+        from ..kubelet.runonce import NullClient, run_once, start_standalone
+
+        async def once():
+            k = await start_standalone(Kubelet(NullClient(), cfg))
+            try:
+                res = await run_once(k)
+            finally:
+                await k.volume_manager.stop()
+            for r in res:
+                print(json.dumps(r))
+            return 0 if all(not r["error"] for r in res) else 1
+        return asyncio.run(once())
     _run_forever(mk)
 
 
