@@ -176,7 +176,12 @@ message ListContainerStatsResponse { repeated ContainerStats stats = 1; }
 message ContainerAttributes { string id = 1; ContainerMetadata metadata = 2; map<string, string> labels = 3; map<string, string> annotations = 4; }
 message ContainerStats { ContainerAttributes attributes = 1; CpuUsage cpu = 2; MemoryUsage memory = 3; FilesystemUsage writable_layer = 4; }
 message CpuUsage { int64 timestamp = 1; UInt64Value usage_core_nano_seconds = 2; }
-message MemoryUsage { int64 timestamp = 1; UInt64Value working_set_bytes = 2; }
+message MemoryUsage {
+  int64 timestamp = 1; UInt64Value working_set_bytes = 2;
+  // later CRI revisions' additions, same field numbers (older peers ignore them)
+  UInt64Value available_bytes = 3; UInt64Value usage_bytes = 4; UInt64Value rss_bytes = 5;
+  UInt64Value page_faults = 6; UInt64Value major_page_faults = 7;
+}
 message GetEventsRequest {}
 enum ContainerEventType { CONTAINER_CREATED_EVENT = 0; CONTAINER_STARTED_EVENT = 1; CONTAINER_STOPPED_EVENT = 2; CONTAINER_DELETED_EVENT = 3; }
 message ContainerEventResponse {

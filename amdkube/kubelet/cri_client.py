@@ -132,6 +132,12 @@ class CRIClient:
     async def pod_sandbox_status(self, sid):
         return (await self._call("podsandbox_status", self.rt.PodSandboxStatus, C.PodSandboxStatusRequest(pod_sandbox_id=sid))).status
 
+    async def pod_sandbox_info(self, sid) -> dict:
+        """PodSandboxStatus(verbose=true).info: runtime-specific details (rocshim: the pause pid)."""
+        resp = await self._call("podsandbox_status", self.rt.PodSandboxStatus,
+                                C.PodSandboxStatusRequest(pod_sandbox_id=sid, verbose=True))
+        return dict(resp.info)
+
     async def create_container(self, sid, cfg, sandbox_cfg) -> str:
         req = C.CreateContainerRequest(pod_sandbox_id=sid, config=cfg, sandbox_config=sandbox_cfg)
         cid = (await self._call("create_container", self.rt.CreateContainer, req)).container_id

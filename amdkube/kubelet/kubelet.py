@@ -243,6 +243,8 @@ class Kubelet:
                                        node_ref=lambda: {"kind": "Node", "metadata": {"name": self.node_name, "uid": self.node_name}})
         self.runtime.gpu_numa = self._gpu_numa
         self.volume_manager = self._volume_manager(config)
+        from .stats import StatsProvider
+        self.stats = StatsProvider(self)
         self._cpuset_applied: dict[str, str] = {}
         self._pods_cgroup_enforced = None
         self.pressure: set[str] = set()
@@ -1358,8 +1360,59 @@ class Kubelet:
             return usage
         return await asyncio.to_thread(walk, list(self.pods))
 
+    async def local_storage_eviction(self) -> list[dict]:
+        """eviction_manager.go localStorageEviction (LocalStorageCapacityIsolation): evict, with no
+        grace, pods whose emptyDir use exceeds its sizeLimit, a container whose rootfs + logs
+        exceed its ephemeral-storage limit, or a pod over the sum of its containers' limits."""
+        from ..api.quantity import Quantity
+        summ = await self.stats.summary()
+        usage = {p["podRef"]["uid"]: p for p in summ["pods"]}
+        evicted = []
+        for pod in self.active_pods():
+            st = usage.get(m.uid_of(pod))
+            if st is None:
+                continue
+            spec = pod.get("spec") or {}
+            msg = None
+            vols = {v["name"]: v for v in st.get("volume") or []}
+            for v in spec.get("volumes") or []:
+                lim = (v.get("emptyDir") or {}).get("sizeLimit")
+                if lim and "emptyDir" in v and vols.get(v["name"], {}).get("usedBytes", 0) > Quantity(lim).value():
+                    msg = f'Usage of EmptyDir volume "{v["name"]}" exceeds the limit "{lim}". '
+                    break
+            limits, total_limit, all_limited = {}, 0, True
+            for c in spec.get("containers") or []:
+                lim = ((c.get("resources") or {}).get("limits") or {}).get("ephemeral-storage")
+                if lim:
+                    limits[c["name"]] = (lim, Quantity(lim).value())
+                    total_limit += limits[c["name"]][1]
+                else:
+                    all_limited = False
+            if msg is None:
+                for cs in st.get("containers") or []:
+                    lim = limits.get(cs["name"])
+                    used = (cs.get("rootfs") or {}).get("usedBytes", 0) + (cs.get("logs") or {}).get("usedBytes", 0)
+                    if lim and used > lim[1]:
+                        msg = f'Container {cs["name"]} exceeded its local ephemeral storage limit "{lim[0]}". '
+                        break
+            if msg is None and all_limited and limits and st.get("ephemeral-storage", {}).get("usedBytes", 0) > total_limit:
+                msg = f"Pod ephemeral local storage usage exceeds the total limit of containers {total_limit}. "
+            if msg is None:
+                continue
+            self.eviction.evictions += 1
+            self.m_evictions.labels("ephemeral-storage").inc()
+            self.recorder.event(pod, "Warning", "Evicted", msg)
+            await self.runtime.kill_pod(m.uid_of(pod), 0, pod)
+            self.status.set(pod, {"phase": "Failed", "reason": "Evicted", "message": msg,
+                                  "conditions": (pod.get("status") or {}).get("conditions") or []})
+            evicted.append(pod)
+        return evicted
+
     async def eviction_pass(self):
         """One synchronize() of the eviction manager: conditions, then at most one eviction."""
+        if self.gates("LocalStorageCapacityIsolation"):
+            if await self.local_storage_eviction():
+                return None
         obs = self.eviction_observer()
         pressure = self.eviction.conditions(obs)
         if pressure != self.pressure:

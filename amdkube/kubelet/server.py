@@ -18,7 +18,6 @@ from ..api import meta as m
 from ..grpcdesc.cri import CRI as C
 from ..utils import profiling
 from ..utils.metrics import CONTENT_TYPE, render
-from .kuberuntime import L_POD_UID
 
 
 class KubeletServer:
@@ -45,7 +44,6 @@ class KubeletServer:
         profiling.add_routes(app)
         self.runner = None
         self.port = None
-        self._cpu_prev: dict[str, tuple[float, int]] = {}
 
     def _ssl(self):
         """HTTPS when a serving certificate is configured (--tls-cert-file/--tls-private-key-file
@@ -112,10 +110,7 @@ class KubeletServer:
         return web.Response(body=render(self.k.metrics), headers={"Content-Type": CONTENT_TYPE})
 
     async def metrics_cadvisor(self, req):
-        from ..monitoring.collector import AcceleratorCollector
-        col = AcceleratorCollector(self.k.smi, self.k.node_name)
-        text = col.render_container_metrics(self._pod_devices())
-        return web.Response(text=text, headers={"Content-Type": CONTENT_TYPE})
+        return web.Response(text=await self.k.stats.render_cadvisor(), headers={"Content-Type": CONTENT_TYPE})
 
     def _pod_devices(self) -> list[dict]:
         """[{namespace, pod, container, devices: [ids]}] for running pods on this node."""
@@ -132,60 +127,11 @@ class KubeletServer:
         return out
 
     async def summary(self, req):
-        import psutil
-        now = m.now_rfc3339()
-        vm = psutil.virtual_memory()
-        cpu = psutil.cpu_times()
-        stats = {s.attributes.id: s for s in await self.k.cri.list_container_stats()}
-        conts = await self.k.cri.list_containers()
-        from ..monitoring.collector import AcceleratorCollector
-        accel = AcceleratorCollector(self.k.smi, self.k.node_name)
-        dev_map = {(d["namespace"], d["pod"], d["container"]): d["devices"] for d in self._pod_devices()}
-        pods = {}
-        for c in conts:
-            if c.state != C.CONTAINER_RUNNING:
-                continue
-            uid = c.labels.get(L_POD_UID, "")
-            p = self.k.pods.get(uid)
-            if p is None:
-                continue
-            ent = pods.setdefault(uid, {"podRef": {"name": m.name_of(p), "namespace": m.namespace_of(p), "uid": uid},
-                                        "startTime": (p.get("status") or {}).get("startTime"), "containers": []})
-            s = stats.get(c.id)
-            used = s.cpu.usage_core_nano_seconds.value if s else 0
-            cont = {"name": c.metadata.name, "startTime": now,
-                    "cpu": {"time": now, "usageCoreNanoSeconds": used, "usageNanoCores": self._rate(c.id, used)},
-                    "memory": {"time": now, "workingSetBytes": s.memory.working_set_bytes.value if s else 0}}
-            ids = dev_map.get((m.namespace_of(p), m.name_of(p), c.metadata.name))
-            if ids:
-                cont["accelerators"] = accel.accelerator_stats(ids)
-            ent["containers"].append(cont)
-        node_used = int((cpu.user + cpu.system) * 1e9)
-        live = {c.id for c in conts} | {"__node__"}
-        for k in [k for k in self._cpu_prev if k not in live]:
-            del self._cpu_prev[k]
-        return web.json_response({
-            "node": {"nodeName": self.k.node_name, "startTime": m.now_rfc3339(),
-                     "cpu": {"time": now, "usageCoreNanoSeconds": node_used, "usageNanoCores": self._rate("__node__", node_used)},
-                     "memory": {"time": now, "availableBytes": vm.available, "usageBytes": vm.total - vm.available,
-                                "workingSetBytes": vm.total - vm.available},
-                     "accelerators": accel.accelerator_stats(None)},
-            "pods": list(pods.values())})
-
-    def _rate(self, key: str, used_ns: int) -> int:
-        """usageNanoCores: CPU time per wall time since the previous summary (cAdvisor's rate)."""
-        t = time.monotonic()
-        prev = self._cpu_prev.get(key)
-        self._cpu_prev[key] = (t, used_ns)
-        if prev is None or t <= prev[0] or used_ns < prev[1]:
-            return 0
-        return int((used_ns - prev[1]) / (t - prev[0]))
+        return web.json_response(await self.k.stats.summary())
 
     async def spec(self, req):
-        import psutil
-        return web.json_response({"num_cores": psutil.cpu_count(), "memory_capacity": psutil.virtual_memory().total,
-                                  "machine_id": "", "system_uuid": "", "boot_id": "",
-                                  "accelerators": [dict(g) for g in (self.k.smi.gpus() if self.k.smi else [])]})
+        from ..monitoring.cadvisor import machine_info
+        return web.json_response({**machine_info(), "accelerators": [dict(g) for g in (self.k.smi.gpus() if self.k.smi else [])]})
 
     async def _find_container(self, ns, pod, cname):
         for uid, p in self.k.pods.items():

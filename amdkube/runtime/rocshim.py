@@ -154,7 +154,9 @@ class RocShim:
         # a privileged rocshim) wired by the network plugin (amdkube-bridge); containers join them
         self.pod_namespaces = pod_namespaces
         from .hostport import HostPortManager
+        from ..monitoring.cadvisor import DuCache
         self.hostports = HostPortManager()
+        self.du = DuCache(10.0)
         self.cgroup_root = cgroup_root
         self.dev_root = dev_root
         self.sandboxes: dict[str, Sandbox] = {}
@@ -821,17 +823,19 @@ def _alive(pid: int) -> bool:
         return False
 
 
-def _proc_stats(pid: int) -> tuple[int, int]:
-    """(cpu ns, rss bytes) of a process (best effort)."""
-    try:
-        with open(f"/proc/{pid}/stat") as f:
-            parts = f.read().split(")")[-1].split()
-        tck = os.sysconf("SC_CLK_TCK")
-        cpu = (int(parts[11]) + int(parts[12])) * 1_000_000_000 // tck
-        rss = int(parts[21]) * os.sysconf("SC_PAGE_SIZE")
-        return cpu, rss
-    except (OSError, IndexError, ValueError):
-        return 0, 0
+def _pgid_map() -> dict[int, list[int]]:
+    """Process group → its pids, from one /proc pass (a container is a process group)."""
+    out: dict[int, list[int]] = {}
+    for d in os.listdir("/proc"):
+        if not d.isdigit():
+            continue
+        try:
+            with open(f"/proc/{d}/stat") as f:
+                parts = f.read().rsplit(")", 1)[1].split()
+            out.setdefault(int(parts[2]), []).append(int(d))
+        except (OSError, IndexError, ValueError):
+            continue
+    return out
 
 
 def _group_pids(pgid: int) -> list[int]:
@@ -1016,26 +1020,48 @@ class _Runtime:
             await _abort(ctx, e)
         return C.ExecSyncResponse(stdout=out, stderr=err, exit_code=rc)
 
-    def _stats(self, c):
-        cpu, rss = _proc_stats(c.pid) if c.state == C.CONTAINER_RUNNING else (0, 0)
+    def _stats(self, c, pgmap=None):
+        """cAdvisor-equivalent container stats: the container's cgroup-v2 leaf when it has one
+        (namespaces isolation), else its process group; the writable layer is the container's
+        root directory (du, cached)."""
+        from ..monitoring.cadvisor import cgroup_stats, process_stats
+        st = None
+        if c.state == C.CONTAINER_RUNNING:
+            if self.r.isolation == "namespaces":
+                st = cgroup_stats(self.r._cgroup_of(c))
+            if st is None:
+                st = process_stats((pgmap or {}).get(c.pid) or [c.pid])
+        st = st or {}
         ts = now_ns()
-        return C.ContainerStats(attributes=C.ContainerAttributes(id=c.id, metadata=C.ContainerMetadata(name=c.name, attempt=c.attempt),
-                                                                 labels=c.labels, annotations=c.annotations),
-                                cpu=C.CpuUsage(timestamp=ts, usage_core_nano_seconds=C.UInt64Value(value=cpu)),
-                                memory=C.MemoryUsage(timestamp=ts, working_set_bytes=C.UInt64Value(value=rss)))
+        u = lambda k: C.UInt64Value(value=int(st.get(k, 0)))    # noqa: E731
+        root = os.path.join(self.r.state_dir, "rootfs", c.sandbox_id, c.name)
+        used, inodes = self.r.du.get(root) if os.path.isdir(root) else (0, 0)
+        return C.ContainerStats(
+            attributes=C.ContainerAttributes(id=c.id, metadata=C.ContainerMetadata(name=c.name, attempt=c.attempt),
+                                             labels=c.labels, annotations=c.annotations),
+            cpu=C.CpuUsage(timestamp=ts, usage_core_nano_seconds=u("cpu_ns")),
+            memory=C.MemoryUsage(timestamp=ts, working_set_bytes=u("working_set_bytes"), usage_bytes=u("usage_bytes"),
+                                 rss_bytes=u("rss_bytes"), page_faults=u("page_faults"), major_page_faults=u("major_page_faults")),
+            writable_layer=C.FilesystemUsage(timestamp=ts, storage_id=C.StorageIdentifier(uuid=root),
+                                             used_bytes=C.UInt64Value(value=used), inodes_used=C.UInt64Value(value=inodes)))
 
     async def ContainerStats(self, req, ctx):
         c = self.r.containers.get(req.container_id)
         if c is None:
             await ctx.abort(grpc.StatusCode.NOT_FOUND, "not found")
-        return C.ContainerStatsResponse(stats=self._stats(c))
+        pgmap = await asyncio.to_thread(_pgid_map) if self.r.isolation != "namespaces" else None
+        return C.ContainerStatsResponse(stats=await asyncio.to_thread(self._stats, c, pgmap))
 
     async def ListContainerStats(self, req, ctx):
         f = req.filter if req.HasField("filter") else None
-        out = [self._stats(c) for c in self.r.containers.values()
+        sel = [c for c in self.r.containers.values()
                if c.state == C.CONTAINER_RUNNING and (f is None or ((not f.id or f.id == c.id) and
                                                                     (not f.pod_sandbox_id or f.pod_sandbox_id == c.sandbox_id)))]
-        return C.ListContainerStatsResponse(stats=out)
+
+        def collect():    # /proc and cgroup reads block: one pass off the event loop
+            pgmap = _pgid_map() if self.r.isolation != "namespaces" else None
+            return [self._stats(c, pgmap) for c in sel]
+        return C.ListContainerStatsResponse(stats=await asyncio.to_thread(collect) if sel else [])
 
     async def UpdateRuntimeConfig(self, req, ctx):
         cidr = req.runtime_config.network_config.pod_cidr

@@ -193,3 +193,79 @@ def test_critical_pod_preemption_selection_and_admission():
             hog = await wait_pod(c, "default", "hog", ("Failed",), 20)
             assert hog["status"]["reason"] == "Preempting"
     run(go(), 60)
+
+
+def test_stats_summary_and_cadvisor_metrics(tmp_path):
+    """server/stats summary: container cpu/memory/rootfs/logs, pod volumes (du) and
+    ephemeral storage, node fs / imageFs / rlimit / kubelet system container; /metrics/cadvisor
+    container_* families (pkg/kubelet/server/stats/summary_test.go, cadvisor prometheus tests)."""
+    import aiohttp
+
+    async def go():
+        async with LocalCluster(gpus="none", relist_period=0.2, with_controllers=False,
+                                kubelet_kw={"volume_reconcile_period": 0.2}) as lc:
+            c = lc.client
+            await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "writer"}, "spec": {
+                "volumes": [{"name": "scratch", "emptyDir": {}}],
+                "containers": [{"name": "w", "image": "busybox", "command": [
+                    "sh", "-c", "head -c 2097152 /dev/zero > $AMDKUBE_ROOTFS/data/blob; echo logged; sleep 60"],
+                    "volumeMounts": [{"name": "scratch", "mountPath": "/data"}]}]}}, "default")
+            await wait_pod(c, "default", "writer", timeout=30)
+            url = f"http://127.0.0.1:{lc.kubelet.server.port}"
+            async with aiohttp.ClientSession() as s:
+                pod = None
+                for _ in range(100):
+                    summ = await (await s.get(url + "/stats/summary")).json()
+                    pod = next((p for p in summ["pods"] if p["podRef"]["name"] == "writer"), None)
+                    vols = {v["name"]: v for v in (pod or {}).get("volume") or []}
+                    if pod and vols.get("scratch", {}).get("usedBytes", 0) >= 2 << 20:
+                        break
+                    lc.kubelet.stats.du.forget("")      # re-measure (the du cache keeps results 10 s)
+                    await asyncio.sleep(0.1)
+                assert vols["scratch"]["usedBytes"] >= 2 << 20 and vols["scratch"]["capacityBytes"] > 0
+                ctr = pod["containers"][0]
+                assert ctr["name"] == "w" and ctr["memory"]["rssBytes"] > 0 and "usedBytes" in ctr["rootfs"]
+                assert ctr["logs"]["usedBytes"] > 0
+                assert pod["ephemeral-storage"]["usedBytes"] >= vols["scratch"]["usedBytes"]
+                node = summ["node"]
+                assert node["fs"]["capacityBytes"] > 0 and "usedBytes" in node["runtime"]["imageFs"]
+                assert node["rlimit"]["maxpid"] > 0 and node["systemContainers"][0]["name"] == "kubelet"
+                text = await (await s.get(url + "/metrics/cadvisor")).text()
+            assert 'container_cpu_usage_seconds_total{container_name="w",pod_name="writer",namespace="default",cpu="total"}' in text
+            assert "machine_cpu_cores " in text and "container_memory_working_set_bytes{" in text
+    run(go(), 60)
+
+
+def test_local_storage_capacity_isolation_eviction():
+    """eviction_manager_test.go TestLocalStorageEviction: emptyDir over its sizeLimit and a
+    container over its ephemeral-storage limit are evicted; a pod within its limits stays."""
+    async def go():
+        async with LocalCluster(gpus="none", relist_period=0.2, with_controllers=False,
+                                kubelet_kw={"feature_gates": "LocalStorageCapacityIsolation=true", "eviction_interval": 3600,
+                                            "volume_reconcile_period": 0.2}) as lc:
+            c = lc.client
+            fill = "head -c 3145728 /dev/zero > $AMDKUBE_ROOTFS/d/blob; sleep 60"
+            specs = {
+                "hog": {"volumes": [{"name": "d", "emptyDir": {"sizeLimit": "1Mi"}}],
+                        "containers": [{"name": "c", "image": "busybox", "command": ["sh", "-c", fill],
+                                        "volumeMounts": [{"name": "d", "mountPath": "/d"}]}]},
+                "chatty": {"containers": [{"name": "c", "image": "busybox",
+                                           "command": ["sh", "-c", "head -c 2097152 /dev/zero | tr '\\\\0' x; sleep 60"],
+                                           "resources": {"limits": {"ephemeral-storage": "1Mi"}}}]},
+                "fine": {"volumes": [{"name": "d", "emptyDir": {"sizeLimit": "100Mi"}}],
+                         "containers": [{"name": "c", "image": "busybox", "command": ["sh", "-c", fill],
+                                         "volumeMounts": [{"name": "d", "mountPath": "/d"}],
+                                         "resources": {"limits": {"ephemeral-storage": "50Mi"}}}]}}
+            for name, spec in specs.items():
+                await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name}, "spec": spec}, "default")
+            for name in specs:
+                await wait_pod(c, "default", name, timeout=30)
+            await asyncio.sleep(1.0)     # the writes land
+            lc.kubelet.stats.du.forget("")
+            evicted = {m.name_of(p) for p in await lc.kubelet.local_storage_eviction()}
+            assert evicted == {"hog", "chatty"}, evicted
+            for name, reason in (("hog", "EmptyDir volume"), ("chatty", "local ephemeral storage limit")):
+                p = await wait_pod(c, "default", name, ("Failed",), 20)
+                assert p["status"]["reason"] == "Evicted" and reason in p["status"]["message"], p["status"]
+            assert (await c.get("pods", "fine", "default"))["status"]["phase"] == "Running"
+    run(go(), 90)
