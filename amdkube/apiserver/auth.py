@@ -306,7 +306,7 @@ class NodeAuthorizer:
             return False, ""
         node = u["name"][len("system:node:"):]
         if not a.resource_request:
-            return a.verb == "get" and a.path in ("/healthz", "/version", "/api", "/apis"), ""
+            return a.verb == "get" and a.path in ("/healthz", "/version", "/api", "/apis", "/openapi/v2", "/swagger.json"), ""
         if a.verb in ("get", "list", "watch") and a.resource in self.READ:
             return True, "node read"
         if a.resource == "nodes":
@@ -405,7 +405,8 @@ def bootstrap_cluster_roles() -> list[dict]:
         cr("edit", [_rule(RW, WORKLOAD_GROUPS, WORKLOADS)]),
         cr("view", [_rule(READ, WORKLOAD_GROUPS, [w for w in WORKLOADS if w not in ("secrets", "pods/exec")])]),
         cr("system:discovery", [_rule(["get"], [], [], urls=["/healthz", "/version", "/version/", "/api", "/api/*", "/apis",
-                                                                  "/apis/*"])]),
+                                                                  "/apis/*", "/swagger.json", "/swaggerapi", "/swaggerapi/*",
+                                                                  "/openapi", "/openapi/*"])]),
         cr("system:basic-user", [_rule(["create"], ["authorization.k8s.io"], ["selfsubjectaccessreviews"])]),
         cr("system:node", [_rule(READ, [""], ["pods", "nodes", "services", "endpoints", "configmaps", "secrets",
                                                 "persistentvolumeclaims", "persistentvolumes"]),

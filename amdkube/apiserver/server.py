@@ -163,6 +163,8 @@ class APIServer:
         self.app.router.add_get("/healthz/{check}", self.healthz)
         self.app.router.add_get("/version", self.version)
         self.app.router.add_get("/metrics", self.metrics_handler)
+        self.app.router.add_get("/openapi/v2", self.openapi)
+        self.app.router.add_get("/swagger.json", self.openapi)
         self.app.router.add_get("/api", self.api_versions)
         self.app.router.add_get("/apis", self.api_groups)
         profiling.add_routes(self.app)
@@ -273,6 +275,16 @@ class APIServer:
     async def version(self, request):
         return _resp({"major": "1", "minor": "9", "gitVersion": GIT_VERSION, "platform": "linux/amd64",
                       "compiler": "cpython", "goVersion": "n/a"})
+
+    async def openapi(self, request):
+        """/openapi/v2 and /swagger.json (routes/openapi.go): the Swagger 2.0 document, ETag-cached."""
+        import hashlib
+        from ..api.openapi import document_bytes
+        body = await asyncio.to_thread(document_bytes, GIT_VERSION)
+        etag = '"' + hashlib.sha1(body).hexdigest() + '"'
+        if request.headers.get("If-None-Match") == etag:
+            return web.Response(status=304, headers={"ETag": etag})
+        return web.Response(body=body, headers={"Content-Type": "application/json", "ETag": etag})
 
     async def metrics_handler(self, request):
         return web.Response(body=render(self.metrics), headers={"Content-Type": CONTENT_TYPE})

@@ -638,17 +638,26 @@ async def cmd_cp(c, a):
 
 
 async def cmd_explain(c, a):
-    ri = SCHEME.resolve(a.args[0].split(".")[0]) if a.args else None
+    """kubectl explain RESOURCE[.FIELD...] [--recursive] [--api-version] from the server's OpenAPI
+    document (pkg/kubectl/explain: field lookup, model printer, recursive field printer)."""
+    from ..api.openapi import explain
+    from .main import openapi_definitions
+    if not a.args:
+        raise SystemExit("error: You must specify the type of resource to explain. Use \"kubectl api-resources\" for a complete list of supported resources.")
+    parts = a.args[0].split(".")
+    ri, fields = None, []
+    for n in range(len(parts), 0, -1):      # the longest resource[.group] prefix (deployments.apps.spec…)
+        ri = SCHEME.resolve(".".join(parts[:n]))
+        if ri is not None:
+            fields = parts[n:]
+            break
     if ri is None:
-        raise SystemExit("error: explain RESOURCE")
-    print(f"KIND:     {ri.kind}\nVERSION:  {ri.api_version}\n")
-    print(f"RESOURCE: {ri.plural} (namespaced: {str(ri.namespaced).lower()}; short names: {', '.join(ri.short_names) or '-'};"
-          f" subresources: {', '.join(ri.subresources) or '-'})")
-    print("\nFIELDS:\n   apiVersion\t<string>\n   kind\t<string>\n   metadata\t<Object>")
-    if ri.kind not in ("ConfigMap", "Secret", "Event", "Binding", "Endpoints", "ClusterRole", "Role"):
-        print("   spec\t<Object>")
-    if ri.plural in __import__("amdkube.apiserver.registry", fromlist=["_STATUS_KINDS"])._STATUS_KINDS:
-        print("   status\t<Object>")
+        raise SystemExit(f'error: the server doesn\'t have a resource type "{parts[0]}"')
+    api_version = a.explain_api_version or ri.api_version
+    try:
+        print(explain(await openapi_definitions(c), api_version, ri.kind, fields, recursive=a.recursive), end="")
+    except KeyError as e:
+        raise SystemExit(f"error: {e.args[0]}")
 
 
 # ------------------------------------------------------------------ create <generator>

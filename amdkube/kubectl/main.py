@@ -456,7 +456,44 @@ def parser():
         sp.add_argument("--for", dest="for_", default="condition=Ready")
         sp.add_argument("--timeout", type=float, default=30.0)
         sp.add_argument("--command", nargs=argparse.REMAINDER, default=None)
+        sp.add_argument("--validate", nargs="?", const=True, default=True,
+                        type=lambda s: s.lower() not in ("false", "0", "no"))
+        sp.add_argument("--recursive", action="store_true")
+        sp.add_argument("--api-version", dest="explain_api_version", default=None)
     return p
+
+
+async def openapi_definitions(c) -> dict:
+    """The server's /openapi/v2 definitions (kubectl's cached OpenAPI getter); this build's own
+    document when the server does not serve one."""
+    from ..api.openapi import definitions
+    try:
+        doc = await c.request("GET", "/openapi/v2")
+        if isinstance(doc, dict) and doc.get("definitions"):
+            return doc["definitions"]
+    except Exception:
+        pass
+    return definitions()
+
+
+async def validate_files(c, paths) -> list[str]:
+    """--validate (cmd/util/openapi/validation): one message per invalid file."""
+    from ..api.openapi import validate
+    defs = await openapi_definitions(c)
+    out = []
+    for p in paths:
+        files = [os.path.join(p, f) for f in sorted(os.listdir(p)) if f.endswith((".yaml", ".yml", ".json"))] \
+            if p != "-" and os.path.isdir(p) else [p]
+        for f in files:
+            if f == "-":
+                continue        # stdin is read once, by the command itself
+            errs = []
+            for doc in load_manifests(open(f).read()):
+                errs += validate(doc, defs)
+            if errs:
+                out.append(f'error validating "{f}": error validating data: [{", ".join(errs)}]; '
+                           "if you choose to ignore these errors, turn validation off with --validate=false")
+    return out
 
 
 def main(argv=None):
@@ -480,10 +517,18 @@ def main(argv=None):
         try:
             if a.cmd in _RESOURCE_CMDS and a.args:
                 first = a.args[0].split("/")[0].split(",")[0]
+                if a.cmd == "explain":
+                    first = first.split(".")[0]
                 if SCHEME.resolve(first) is None:
                     await c.discover()          # a custom resource: learn it from the server
             elif a.filename and any(SCHEME.for_object(d) is None for d in _read_files(a.filename)):
                 await c.discover()
+            if a.cmd in ("create", "apply", "replace") and a.filename and a.validate:
+                bad = await validate_files(c, a.filename)
+                if bad:
+                    for msg in bad:
+                        print(f"error: {msg}", file=sys.stderr)
+                    return 1
             return await COMMANDS[a.cmd](c, a)
         except m.StatusError as e:
             print(f"Error from server ({e.reason}): {e.message}", file=sys.stderr)

@@ -1,7 +1,8 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/r2e
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r2e/pytest_gpu.log 2>&1 &&
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('SMOKE OK')" > gpurun_out/r2e/smoke.log 2>&1 &&
-timeout -k 10 500 python -u bench.py --steps 20 --warmup 5 > gpurun_out/r2e/bench_n1.log 2>&1
+TAG=${TAG:-r2x}
+mkdir -p gpurun_out/${TAG:-r2x}
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${TAG:-r2x}/pytest_gpu.log 2>&1 &&
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('SMOKE OK')" > gpurun_out/${TAG:-r2x}/smoke.log 2>&1 &&
+timeout -k 10 500 python -u bench.py --steps 20 --warmup 5 > gpurun_out/${TAG:-r2x}/bench_n1.log 2>&1
 echo done
