@@ -14,7 +14,10 @@ Reference cmd/kubeadm/app (1.9): `kubeadm init` runs the phases
   signature made with the token; pin the CA by the sha256 of its public key,
   --discovery-token-ca-cert-hash), then TLS bootstrap (CSR as system:bootstrap:<id>,
   auto-approved, signed by the cluster CA) and writes kubelet.conf. `kubeadm reset` undoes a
-  node; `kubeadm token create|list|delete` manages bootstrap tokens.
+  node; `kubeadm token create|list|delete|generate` manages bootstrap tokens.
+  The phases themselves live in phases.py (`kubeadm alpha phase ...`), the stored
+  MasterConfiguration behind `kubeadm config view|upload|print-default`, and `kubeadm upgrade
+  plan|apply` in upgrade.py.
 
 MI355X specifics: a node that exposes /dev/kfd is labelled amd.com/gpu.present=true, and the
 AMD device-plugin DaemonSet (deploy/amd-gpu-device-plugin.yaml) is an addon selecting those
@@ -139,44 +142,7 @@ def _component_pod(name, args, env_root=ROOT, extra_mounts=()):
                                      "env": [{"name": "PYTHONPATH", "value": env_root}]}]}}
 
 
-def control_plane_manifests(cfg: dict) -> dict[str, dict]:
-    p, k = cfg["pki"], cfg["kubeconfig_dir"]
-    api = ["apiserver", "--bind-address", cfg["advertise"], "--port", str(cfg["port"]),
-           "--tls-cert-file", f"{p}/apiserver.crt", "--tls-private-key-file", f"{p}/apiserver.key",
-           "--client-ca-file", f"{p}/ca.crt", "--authorization-mode", "Node,RBAC", "--anonymous-auth", "true",
-           "--admission-control", ADMISSION, "--service-account-key-file", f"{p}/sa.key",
-           "--service-cluster-ip-range", cfg["service_cidr"], "--data-dir", cfg["data_dir"]]
-    cm = ["controller-manager", "--kubeconfig", f"{k}/controller-manager.conf", "--leader-elect", "true",
-          "--service-account-private-key-file", f"{p}/sa.key", "--root-ca-file", f"{p}/ca.crt",
-          "--cluster-signing-cert-file", f"{p}/ca.crt", "--cluster-signing-key-file", f"{p}/ca.key",
-          "--controllers", "*,bootstrapsigner,tokencleaner", "--hostpath-pv-root", os.path.join(cfg["data_dir"], "pv")]
-    if cfg.get("pod_cidr"):
-        cm += ["--allocate-node-cidrs", "true", "--cluster-cidr", cfg["pod_cidr"]]
-    sched = ["scheduler", "--kubeconfig", f"{k}/scheduler.conf", "--leader-elect", "true", "--port", "0"]
-    out = {}
-    for name, args in (("kube-apiserver", api), ("kube-controller-manager", cm), ("kube-scheduler", sched)):
-        out[name] = _component_pod(name, args)
-    return out
-
-
 # ------------------------------------------------------------------------- helpers
-def _preflight(cfg, errors_ok=()):
-    errs, warns = [], []
-    if shutil.which("openssl") is None:
-        errs.append("openssl is required for the PKI phase")
-    with socket.socket() as s:
-        try:
-            s.bind((cfg["advertise"], cfg["port"]))
-        except OSError:
-            errs.append(f"Port-{cfg['port']}: port {cfg['port']} is in use")
-    if os.path.isdir(cfg["manifests"]) and os.listdir(cfg["manifests"]):
-        errs.append(f"DirAvailable--{cfg['manifests']}: {cfg['manifests']} is not empty")
-    if not os.path.exists("/dev/kfd"):
-        warns.append("no /dev/kfd: this node has no MI355X (ROCm KFD) device; GPU pods will not schedule here")
-    errs = [e for e in errs if not any(e.startswith(x) for x in errors_ok)]
-    return errs, warns
-
-
 def _spawn(argv, log_path, env=None):
     logf = open(log_path, "ab")
     p = subprocess.Popen([sys.executable, "-m", "amdkube", *argv], stdout=logf, stderr=subprocess.STDOUT,
@@ -234,67 +200,44 @@ def _paths(base):
 
 
 def init(a) -> int:
-    cfg = _paths(a.base_dir)
-    cfg.update(advertise=a.apiserver_advertise_address, port=a.apiserver_bind_port, service_cidr=a.service_cidr,
-               pod_cidr=a.pod_network_cidr, kubelet_port=a.kubelet_port)
-    node = a.node_name or socket.gethostname()
-    errs, warns = _preflight(cfg, tuple(a.ignore_preflight_errors.split(",")) if a.ignore_preflight_errors else ())
+    """`kubeadm init`: every phase of phases.py in order (cmd/init.go Run)."""
+    from . import phases as ph
+    mc = ph.master_config(a)
+    cfg = ph.paths(a.base_dir, mc)
+    cfg.update(advertise=mc["api"]["advertiseAddress"], port=mc["api"]["bindPort"], kubelet_port=a.kubelet_port)
+    node = mc["nodeName"]
+    errs, warns = ph.phase_preflight(mc, cfg, tuple(x for x in a.ignore_preflight_errors.split(",") if x))
     for w in warns:
         print(f"[preflight] WARNING: {w}")
     if errs:
         print("[preflight] Some fatal errors occurred:\n" + "\n".join(f"\t[ERROR {e}]" for e in errs), file=sys.stderr)
         return 1
-    for d in (cfg["pki"], cfg["manifests"], cfg["data_dir"]):
-        os.makedirs(d, exist_ok=True)
-    p = cfg["pki"]
-    # certs
-    if not os.path.exists(f"{p}/ca.crt"):
-        new_ca(p)
-    first_svc = str(next(ipaddress.ip_network(a.service_cidr, strict=False).hosts()))
-    sans = [f"IP:{cfg['advertise']}", "IP:127.0.0.1", f"IP:{first_svc}", f"DNS:{node}", "DNS:kubernetes", "DNS:kubernetes.default",
-            "DNS:kubernetes.default.svc", f"DNS:kubernetes.default.svc.{a.service_dns_domain}", "DNS:localhost"]
-    new_cert(p, "apiserver", "kube-apiserver", sans=sans, server=True)
-    new_cert(p, "apiserver-kubelet-client", "kube-apiserver-kubelet-client", orgs=("system:masters",))
-    with open(f"{p}/sa.key", "wb") as f:
-        f.write(secrets.token_hex(32).encode())
-    os.chmod(f"{p}/sa.key", 0o600)
-    print(f"[certificates] Generated ca, apiserver (SANs {', '.join(sans)}), apiserver-kubelet-client and sa keys in {p}")
-    # kubeconfigs
-    ca = open(f"{p}/ca.crt", "rb").read()
-    server = f"https://{cfg['advertise']}:{cfg['port']}"
-    for fname, cn, orgs in (("admin.conf", "kubernetes-admin", ("system:masters",)),
-                            ("kubelet.conf", f"system:node:{node}", ("system:nodes",)),
-                            ("controller-manager.conf", "system:kube-controller-manager", ()),
-                            ("scheduler.conf", "system:kube-scheduler", ()),
-                            ("kube-proxy.conf", "system:kube-proxy", ())):
-        nm = fname[:-5]
-        new_cert(p, nm, cn, orgs=orgs)
-        write_yaml(os.path.join(cfg["kubeconfig_dir"], fname),
-                   kubeconfig(server, ca, cn, open(f"{p}/{nm}.crt", "rb").read(), open(f"{p}/{nm}.key", "rb").read()))
-    print(f"[kubeconfig] Wrote admin.conf, kubelet.conf, controller-manager.conf, scheduler.conf, kube-proxy.conf to {cfg['base']}")
-    # control plane
-    for name, pod in control_plane_manifests(cfg).items():
-        write_yaml(os.path.join(cfg["manifests"], f"{name}.yaml"), pod, 0o644)
-    print(f"[controlplane] Wrote static Pod manifests for kube-apiserver, kube-controller-manager, kube-scheduler to {cfg['manifests']}")
+    os.makedirs(cfg["base"], exist_ok=True)
+    done = ph.phase_certs(mc, cfg)
+    print(f"[certificates] Generated {', '.join(done)} in {cfg['pki']} (apiserver SANs {', '.join(ph.apiserver_sans(mc))})")
+    done = ph.phase_kubeconfig(mc, cfg)
+    print(f"[kubeconfig] Wrote {', '.join(done)} to {cfg['base']}")
+    print(f"[controlplane] Wrote static Pod manifests for {', '.join(ph.phase_controlplane(mc, cfg))} to {cfg['manifests']}")
+    print(f"[etcd] The store is embedded in kube-apiserver (data directory {ph.phase_etcd_local(mc, cfg)})")
     if a.start_kubelet:
         labels = f"{GPU_LABEL}=true" if os.path.exists("/dev/kfd") else ""
         start_node_agents(cfg, os.path.join(cfg["base"], "kubelet.conf"), node, labels)
         print(f"[init] Started rocshim and the kubelet (logs: {cfg['node_dir']}/logs)")
-    token = a.token or new_token()
-    rc = asyncio.run(_post_init(cfg, node, token, a.token_ttl, a.timeout, ca, server, a.skip_addons))
+    rc = asyncio.run(_post_init(mc, cfg, a.timeout, a.skip_addons))
     if rc != 0:
         return rc
+    ca = open(os.path.join(cfg["pki"], "ca.crt"), "rb").read()
     h = ca_cert_hash(ca)
     print("\nYour Kubernetes master has initialized successfully!\n\n"
           f"To use the cluster:  export KUBECONFIG={os.path.join(cfg['base'], 'admin.conf')}\n\n"
           "You can now join any number of machines by running the following on each node:\n\n"
-          f"  python -m amdkube kubeadm join {cfg['advertise']}:{cfg['port']} --token {token} "
+          f"  python -m amdkube kubeadm join {cfg['advertise']}:{cfg['port']} --token {mc['token']} "
           f"--discovery-token-ca-cert-hash {h}\n")
     return 0
 
 
-async def _post_init(cfg, node, token, ttl, timeout, ca, server, skip_addons):
-    from ..api import meta as m
+async def _post_init(mc, cfg, timeout, skip_addons):
+    from . import phases as ph
     c = _client(os.path.join(cfg["base"], "admin.conf"))
     try:
         print(f"[init] Waiting for the kubelet to boot up the control plane as Static Pods from {cfg['manifests']} "
@@ -304,39 +247,20 @@ async def _post_init(cfg, node, token, ttl, timeout, ca, server, skip_addons):
             print("[init] the control plane did not become healthy in time", file=sys.stderr)
             return 1
         print(f"[apiclient] All control plane components are healthy after {time.time() - t0:.1f} seconds")
-        # markmaster
-        end = time.time() + timeout
-        while time.time() < end and await c.get_or_none("nodes", node) is None:
-            await asyncio.sleep(0.2)
-        if await c.get_or_none("nodes", node) is not None:
-            await c.patch("nodes", node, {"metadata": {"labels": {MASTER_LABEL: ""}},
-                                          "spec": {"taints": [{"key": MASTER_LABEL, "effect": "NoSchedule"}]}})
-            print(f"[markmaster] Node {node} labelled {MASTER_LABEL}=\"\" and tainted {MASTER_LABEL}:NoSchedule")
-        # bootstrap token + RBAC + cluster-info
-        await _create_or_replace(c, token_secret(token, ttl, description="default kubeadm bootstrap token"))
-        for o in _bootstrap_rbac():
-            await _create_or_replace(c, o)
-        ci = {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "cluster-info", "namespace": "kube-public"},
-              "data": {"kubeconfig": yaml.safe_dump(kubeconfig(server, ca, "", None, None))}}
-        await _create_or_replace(c, ci)
-        print(f"[bootstraptoken] Using token: {token}; RBAC rules let bootstrap tokens post CSRs that are auto-approved; "
+        if await ph.phase_mark_master(c, mc["nodeName"], timeout):
+            print(f"[markmaster] Node {mc['nodeName']} labelled {MASTER_LABEL}=\"\" and tainted {MASTER_LABEL}:NoSchedule")
+        await ph.phase_bootstrap_token(c, mc, cfg)
+        print(f"[bootstraptoken] Using token: {mc['token']}; RBAC rules let bootstrap tokens post CSRs that are auto-approved; "
               "cluster-info published in kube-public")
+        await ph.phase_upload_config(c, mc)
+        print(f"[uploadconfig] Storing the configuration used in ConfigMap kube-system/{ph.CONFIG_MAP}")
         if not skip_addons:
-            for o in _addons(cfg):
-                await _create_or_replace(c, o)
-            print("[addons] Applied essential addon: kube-proxy; AMD GPU device plugin (nodes labelled amd.com/gpu.present)")
+            done = await ph.phase_addons(c, mc, cfg)
+            print(f"[addons] Applied essential addons: {', '.join(done)} (the AMD GPU device plugin runs on nodes "
+                  f"labelled {GPU_LABEL})")
         return 0
     finally:
         await c.close()
-
-
-async def _create_or_replace(c, obj):
-    from ..api import meta as m
-    try:
-        await c.create(obj, obj["metadata"].get("namespace"))
-    except m.StatusError as e:
-        if not m.is_already_exists(e):
-            raise
 
 
 def _bootstrap_rbac():
@@ -355,30 +279,6 @@ def _bootstrap_rbac():
          "roleRef": {"apiGroup": rb, "kind": "Role", "name": "kubeadm:bootstrap-signer-clusterinfo"},
          "subjects": [{"kind": "User", "apiGroup": rb, "name": "system:anonymous"}]},
     ]
-
-
-def _addons(cfg):
-    proxy = {"apiVersion": "apps/v1", "kind": "DaemonSet", "metadata": {"name": "kube-proxy", "namespace": "kube-system",
-                                                                         "labels": {"k8s-app": "kube-proxy"}},
-             "spec": {"selector": {"matchLabels": {"k8s-app": "kube-proxy"}},
-                      "template": {"metadata": {"labels": {"k8s-app": "kube-proxy"}},
-                                   "spec": {"hostNetwork": True, "tolerations": [{"key": MASTER_LABEL, "effect": "NoSchedule"}],
-                                            "containers": [{"name": "kube-proxy", "image": "python:3",
-                                                            "args": ["-m", "amdkube", "proxy", "--kubeconfig",
-                                                                     os.path.join(cfg["base"], "kube-proxy.conf"),
-                                                                     "--healthz-port", "0", "--bind-address", "127.0.0.1"],
-                                                            "env": [{"name": "PYTHONPATH", "value": ROOT}]}]}}}}
-    from ..api.scheme import load_manifests
-    out = [proxy]
-    for d in load_manifests(open(os.path.join(ROOT, "deploy", "amd-gpu-device-plugin.yaml")).read()):
-        if d and d.get("kind") == "DaemonSet":
-            tpl = d["spec"]["template"]["spec"]
-            tpl.setdefault("nodeSelector", {})[GPU_LABEL] = "true"
-            for ct in tpl.get("containers") or []:
-                ct.setdefault("env", []).append({"name": "PYTHONPATH", "value": ROOT})
-            d["metadata"].setdefault("namespace", "kube-system")
-            out.append(d)
-    return out
 
 
 # ---------------------------------------------------------------------------- join
@@ -507,7 +407,18 @@ def reset(a) -> int:
 
 
 # --------------------------------------------------------------------------- token
+def _kubeconfig_ca(path: str) -> bytes:
+    kc = yaml.safe_load(open(path))
+    cl = kc["clusters"][0]["cluster"]
+    if cl.get("certificate-authority-data"):
+        return base64.b64decode(cl["certificate-authority-data"])
+    return open(cl["certificate-authority"], "rb").read()
+
+
 def token_cmd(a) -> int:
+    if a.token_op == "generate":        # offline: just a well-formed random token
+        print(new_token())
+        return 0
     c = _client(a.kubeconfig)
 
     async def run():
@@ -515,8 +426,14 @@ def token_cmd(a) -> int:
         try:
             if a.token_op == "create":
                 t = a.token or new_token()
-                await c.create(token_secret(t, a.ttl or None, description=a.description or ""), "kube-system")
-                print(t)
+                await c.create(token_secret(t, a.ttl or None, usages=tuple(a.usages.split(",")),
+                                            groups=tuple(a.groups.split(",")), description=a.description or ""), "kube-system")
+                if a.print_join_command:
+                    ca = _kubeconfig_ca(a.kubeconfig)
+                    print(f"python -m amdkube kubeadm join {c.server.split('://', 1)[1]} --token {t} "
+                          f"--discovery-token-ca-cert-hash {ca_cert_hash(ca)}")
+                else:
+                    print(t)
             elif a.token_op == "list":
                 items, _ = await c.list("secrets", "kube-system")
                 print(f"{'TOKEN':<24}{'TTL':<10}{'EXPIRES':<22}{'USAGES':<28}DESCRIPTION")
@@ -539,19 +456,76 @@ def token_cmd(a) -> int:
     return 0
 
 
+def config_cmd(a) -> int:
+    """kubeadm config view | upload from-file | upload from-flags | print-default (cmd/config.go)."""
+    from . import phases as ph
+    if a.config_op == "print-default":
+        mc = ph.master_config(a)
+        mc["nodeName"] = "<node name>"
+        print(yaml.safe_dump(mc, sort_keys=False), end="")
+        return 0
+
+    async def run():
+        c = _client(a.kubeconfig)
+        try:
+            if a.config_op == "view":
+                cm = await c.get_or_none("configmaps", ph.CONFIG_MAP, "kube-system")
+                if cm is None:
+                    print(f"error: ConfigMap kube-system/{ph.CONFIG_MAP} not found (run `kubeadm config upload`)", file=sys.stderr)
+                    return 1
+                print(f"[config] Configuration of the cluster, from ConfigMap kube-system/{ph.CONFIG_MAP}:\n")
+                print((cm.get("data") or {}).get(ph.CONFIG_KEY, ""), end="")
+                return 0
+            if a.config_op == "upload":
+                if a.source == "from-file" and not a.config:
+                    print("error: from-file needs --config", file=sys.stderr)
+                    return 1
+                mc = ph.master_config(a)
+                await ph.phase_upload_config(c, mc)
+                print(f"[uploadconfig] Stored the configuration in ConfigMap kube-system/{ph.CONFIG_MAP}")
+                return 0
+            return 1
+        finally:
+            await c.close()
+    return asyncio.run(run())
+
+
+def version_cmd(a) -> int:
+    from .. import GIT_VERSION
+    info = {"major": "1", "minor": "9", "gitVersion": GIT_VERSION, "platform": "linux/amd64", "compiler": "cpython"}
+    if a.output == "short":
+        print(GIT_VERSION)
+    elif a.output == "json":
+        print(json.dumps({"clientVersion": info}, indent=2))
+    elif a.output == "yaml":
+        print(yaml.safe_dump({"clientVersion": info}, sort_keys=False), end="")
+    else:
+        print(f"kubeadm version: &version.Info{{Major:\"1\", Minor:\"9\", GitVersion:\"{GIT_VERSION}\", "
+              f"Platform:\"linux/amd64\", Compiler:\"cpython\"}}")
+    return 0
+
+
+def _cluster_flags(p, defaults=True):
+    p.add_argument("--base-dir", default="/etc/kubernetes")
+    p.add_argument("--config", default=None, help="a kubeadm.k8s.io/v1alpha1 MasterConfiguration file")
+    p.add_argument("--apiserver-advertise-address", default="127.0.0.1" if defaults else None)
+    p.add_argument("--apiserver-bind-port", type=int, default=6443 if defaults else None)
+    p.add_argument("--apiserver-cert-extra-sans", default="")
+    p.add_argument("--service-cidr", default="10.96.0.0/12" if defaults else None)
+    p.add_argument("--service-dns-domain", default="cluster.local" if defaults else None)
+    p.add_argument("--pod-network-cidr", default=None)
+    p.add_argument("--node-name", default=None)
+    p.add_argument("--kubernetes-version", default=None)
+    p.add_argument("--feature-gates", default="")
+    p.add_argument("--token", default=None)
+    p.add_argument("--token-ttl", type=float, default=24 * 3600.0)
+
+
 def main(argv) -> int:
     ap = argparse.ArgumentParser("amdkube kubeadm")
     sub = ap.add_subparsers(dest="cmd", required=True)
     i = sub.add_parser("init")
-    i.add_argument("--base-dir", default="/etc/kubernetes")
-    i.add_argument("--apiserver-advertise-address", default="127.0.0.1")
-    i.add_argument("--apiserver-bind-port", type=int, default=6443)
-    i.add_argument("--service-cidr", default="10.96.0.0/12")
-    i.add_argument("--service-dns-domain", default="cluster.local")
-    i.add_argument("--pod-network-cidr", default=None)
-    i.add_argument("--node-name", default=None)
-    i.add_argument("--token", default=None)
-    i.add_argument("--token-ttl", type=float, default=24 * 3600.0)
+    _cluster_flags(i)
     i.add_argument("--ignore-preflight-errors", default="")
     i.add_argument("--skip-addons", action="store_true")
     i.add_argument("--start-kubelet", action="store_true", help="start rocshim + kubelet (what systemd does for kubeadm)")
@@ -571,10 +545,27 @@ def main(argv) -> int:
     r.add_argument("--base-dir", default="/etc/kubernetes")
     r.add_argument("--drain-seconds", type=float, default=2.0)
     t = sub.add_parser("token")
-    t.add_argument("token_op", choices=("create", "list", "delete"))
+    t.add_argument("token_op", choices=("create", "list", "delete", "generate"))
     t.add_argument("token", nargs="?", default=None)
     t.add_argument("--kubeconfig", default="/etc/kubernetes/admin.conf")
     t.add_argument("--ttl", type=float, default=24 * 3600.0)
     t.add_argument("--description", default="")
+    t.add_argument("--usages", default="signing,authentication")
+    t.add_argument("--groups", default=BOOTSTRAP_GROUP)
+    t.add_argument("--print-join-command", action="store_true")
+    cf = sub.add_parser("config")
+    cf.add_argument("config_op", choices=("view", "upload", "print-default"))
+    cf.add_argument("source", nargs="?", choices=("from-file", "from-flags"), default="from-flags")
+    cf.add_argument("--kubeconfig", default="/etc/kubernetes/admin.conf")
+    _cluster_flags(cf)
+    al = sub.add_parser("alpha")
+    alsub = al.add_subparsers(dest="alpha_cmd", required=True)
+    from .phases import add_phase_parser, run_phase
+    add_phase_parser(alsub)
+    from . import upgrade
+    upgrade.add_parser(sub)
+    v = sub.add_parser("version")
+    v.add_argument("-o", "--output", default="", choices=("", "short", "json", "yaml"))
     a = ap.parse_args(argv)
-    return {"init": init, "join": join, "reset": reset, "token": token_cmd}[a.cmd](a)
+    return {"init": init, "join": join, "reset": reset, "token": token_cmd, "config": config_cmd,
+            "alpha": run_phase, "upgrade": upgrade.run, "version": version_cmd}[a.cmd](a)

@@ -62,11 +62,44 @@ def test_kubeadm_init_join_reset(tmp_path):
                      "--node-name", "worker-1", "--start-kubelet", "--kubelet-port", "0")
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
         asyncio.run(_check_cluster(os.path.join(master, "admin.conf")))
-        r = _kubeadm("token", "list", "--kubeconfig", os.path.join(master, "admin.conf"))
+        admin = os.path.join(master, "admin.conf")
+        r = _kubeadm("token", "list", "--kubeconfig", admin)
         assert token.split(".")[0] in r.stdout, r.stdout + r.stderr
+        r = _kubeadm("token", "create", "--kubeconfig", admin, "--print-join-command")
+        assert re.search(r"kubeadm join \S+ --token [a-z0-9]{6}\.[a-z0-9]{16} --discovery-token-ca-cert-hash " + re.escape(h),
+                         r.stdout), r.stdout + r.stderr
+        # the stored configuration, the upgrade plan and an upgrade that changes one component
+        r = _kubeadm("config", "view", "--kubeconfig", admin)
+        assert "kind: MasterConfiguration" in r.stdout and "nodeName: master-0" in r.stdout and "token:" not in r.stdout
+        r = _kubeadm("upgrade", "plan", "--kubeconfig", admin)
+        assert r.returncode == 0 and "kube-scheduler" in r.stdout and "up-to-date" in r.stdout, r.stdout + r.stderr
+        r = _kubeadm("upgrade", "apply", "v1.8.0", "--kubeconfig", admin, "--base-dir", master, "-y")
+        assert r.returncode == 1 and "lower than the minor release" in r.stderr
+        newcfg = tmp_path / "upgrade.yaml"
+        newcfg.write_text("apiVersion: kubeadm.k8s.io/v1alpha1\nkind: MasterConfiguration\n"
+                          "schedulerExtraArgs: {kube-api-qps: '400'}\n")
+        r = _kubeadm("upgrade", "apply", "--kubeconfig", admin, "--base-dir", master, "--config", str(newcfg), "-y",
+                     "--timeout", "90")
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+        assert "kube-apiserver is unchanged" in r.stdout and "Component kube-scheduler upgraded successfully" in r.stdout
+        asyncio.run(_check_upgraded(admin))
     finally:
         for d in (worker, master):
             _kubeadm("reset", "--base-dir", d, "--drain-seconds", "1.5")
+
+
+async def _check_upgraded(admin_conf):
+    c = Client.from_kubeconfig(admin_conf)
+    try:
+        p = await c.get("pods", "kube-scheduler-master-0", "kube-system")
+        args = p["spec"]["containers"][0]["args"]
+        assert args[args.index("--kube-api-qps") + 1] == "400", args
+        cm = await c.get("configmaps", "kubeadm-config", "kube-system")
+        assert "kube-api-qps" in cm["data"]["MasterConfiguration"]
+        ds = {m.name_of(d) for d in (await c.list("deployments.apps", "kube-system"))[0]}
+        assert "kube-dns" in ds
+    finally:
+        await c.close()
 
 
 async def _check_cluster(admin_conf):
