@@ -412,6 +412,8 @@ COMMANDS.update(_EXTRA)
 COMMANDS.update(_more.COMMANDS)
 COMMANDS["apply"] = _more.cmd_apply       # three-way merge, --prune, *-last-applied
 COMMANDS["set"] = _more.cmd_set           # env/image/resources/selector/serviceaccount/subject
+from .diff import cmd_alpha  # noqa: E402
+COMMANDS["alpha"] = cmd_alpha             # alpha diff LOCAL|LIVE|LAST|MERGED
 
 
 _RESOURCE_CMDS = {"get", "describe", "delete", "label", "annotate", "scale", "patch", "wait", "edit", "explain", "expose",
@@ -502,7 +504,11 @@ def main(argv=None):
     if "--" in argv:
         i = argv.index("--")
         argv, cmd_tail = argv[:i], argv[i + 1:]
-    a = parser().parse_args(argv)
+    p = parser()
+    a, extra = p.parse_known_args(argv)
+    if any(x.startswith("-") for x in extra):
+        p.error(f"unrecognized arguments: {' '.join(extra)}")
+    a.args = list(a.args) + extra      # positionals after flags (kubectl alpha diff -f x LAST LOCAL)
     if cmd_tail:
         a.command = cmd_tail
     elif a.command is None:

@@ -144,3 +144,41 @@ def test_served_document_explain_and_validate_through_kubectl(tmp_path, capsys):
             'unknown field "imagePulPolicy" in io.k8s.api.core.v1.Container]; if you choose to ignore these errors, '
             'turn validation off with --validate=false') in cap.err
     assert "pod/typo created" in cap.out
+
+
+def test_kubectl_alpha_diff(tmp_path, capsys):
+    """diff.go: LOCAL vs LIVE by default; MERGED is what apply would leave; LAST the annotation."""
+    f = tmp_path / "cm.yaml"
+
+    async def go():
+        async with LocalCluster(gpus="none", with_controllers=False, with_kubelet=False) as lc:
+            import asyncio
+
+            def k(*argv):
+                return asyncio.get_running_loop().run_in_executor(None, kubectl_main, ["-s", lc.api.url, *argv])
+            f.write_text("apiVersion: v1\nkind: ConfigMap\nmetadata: {name: gpu-cfg}\ndata: {arch: gfx950, cus: '256'}\n")
+            assert await k("alpha", "diff", "-f", str(f)) == 0     # not on the server: everything is added
+            assert await k("apply", "-f", str(f)) == 0
+            # a change made on the server outside apply, then an edit of the file
+            cm = await lc.client.get("configmaps", "gpu-cfg", "default")
+            cm["data"]["owner"] = "ops"
+            await lc.client.update(cm)
+            f.write_text("apiVersion: v1\nkind: ConfigMap\nmetadata: {name: gpu-cfg}\ndata: {arch: gfx950, cus: '304'}\n")
+            capsys.readouterr()
+            assert await k("alpha", "diff", "-f", str(f), "LAST", "LOCAL") == 0
+            last_local = capsys.readouterr().out
+            assert await k("alpha", "diff", "-f", str(f), "MERGED") == 0
+            merged_live = capsys.readouterr().out
+            try:
+                await k("alpha", "diff", "-f", str(f), "LOCAL", "NOPE")
+                raise AssertionError("accepted a bad version keyword")
+            except SystemExit as e:
+                assert 'Invalid parameter "NOPE"' in str(e)
+            return last_local, merged_live
+    last_local, merged_live = run(go(), 60)
+    # LAST → LOCAL: only the edited key
+    assert "-  cus: '256'" in last_local and "+  cus: '304'" in last_local and "owner" not in last_local
+    assert "--- LAST/v1.ConfigMap.default.gpu-cfg" in last_local
+    # MERGED vs LIVE: apply changes cus and keeps the server-side key
+    assert "-  cus: '304'" in merged_live and "+  cus: '256'" in merged_live
+    assert "owner" not in [ln for ln in merged_live.splitlines() if ln.startswith(("+ ", "- "))]
