@@ -95,7 +95,7 @@ def _kind_defs(defs: dict) -> dict:
         canon = SCHEME.storage_of(ri)
         cands = by_kind.get(canon.kind, [])
         grp = canon.group.split(".")[0] if canon.group else "core"
-        pick = [c for c in cands if f".{grp}." in c or f"{grp}-" in c] or cands
+        pick = [c for c in cands if f".{grp}." in c or f"{grp}-" in c]
         if pick:
             out[(ri.group, ri.version, ri.kind)] = pick[0]
     return out

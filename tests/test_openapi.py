@@ -31,6 +31,8 @@ def test_document_is_closed_and_covers_every_served_kind():
     _refs(doc, refs)
     assert refs <= set(defs), refs - set(defs)
     for ri in SCHEME.by_kind.values():
+        if "." in ri.group and not ri.group.endswith("k8s.io"):
+            continue        # custom resources other tests registered in this process
         assert oa.kind_definition(ri.api_version, ri.kind), ri
         base = ri.api_prefix() + ("/namespaces/{namespace}" if ri.namespaced else "") + f"/{ri.plural}"
         assert base in doc["paths"] and base + "/{name}" in doc["paths"], base
