@@ -19,9 +19,20 @@ log = logging.getLogger("amdkube.record")
 NORMAL, WARNING = "Normal", "Warning"
 
 
+SPAM_BURST, SPAM_QPS = 25, 1.0 / 300     # events_cache.go EventSourceObjectSpamFilter defaults
+
+
 class EventRecorder:
-    def __init__(self, client: Client, component: str, host: str = "", max_queue: int = 10000):
+    """`qps`/`burst` bound the rate of writes to the API (--event-qps/--event-burst; 0: no
+    bound); every (source, involved object) pair also gets the reference's spam filter: a
+    burst of 25 events, then one per five minutes."""
+
+    def __init__(self, client: Client, component: str, host: str = "", max_queue: int = 10000, qps: float = 0,
+                 burst: int = 10):
         self.client, self.component, self.host = client, component, host
+        from .rest import TokenBucket
+        self.limiter = TokenBucket(qps, burst) if qps else None
+        self._spam: dict[tuple, tuple[float, float]] = {}     # (kind, ns, name, uid) -> (tokens, last refill)
         self.queue: asyncio.Queue | None = None
         self.max_queue = max_queue
         self.cache: dict[tuple, tuple[str, str, int]] = {}  # key -> (ns, name, count)
@@ -50,10 +61,27 @@ class EventRecorder:
                "resourceVersion": md.get("resourceVersion", "")}
         self.queue.put_nowait((ref, etype, reason, message, time.time()))
 
+    def _spam_ok(self, ref) -> bool:
+        key = (ref["kind"], ref["namespace"], ref["name"], ref["uid"])
+        now = time.monotonic()
+        tokens, last = self._spam.get(key, (float(SPAM_BURST), now))
+        tokens = min(float(SPAM_BURST), tokens + (now - last) * SPAM_QPS)
+        if tokens < 1:
+            self._spam[key] = (tokens, now)
+            return False
+        self._spam[key] = (tokens - 1, now)
+        if len(self._spam) > 4096:
+            self._spam = {k: v for k, v in self._spam.items() if now - v[1] < 300}
+        return True
+
     async def _run(self):
         while True:
             ref, etype, reason, message, ts = await self.queue.get()
             try:
+                if not self._spam_ok(ref):
+                    continue
+                if self.limiter is not None:
+                    await self.limiter.wait()
                 await self._write(ref, etype, reason, message, ts)
             except asyncio.CancelledError:
                 raise

@@ -309,9 +309,75 @@ def kubelet(argv):
     ap.add_argument("--image-gc-high-threshold", type=int, default=85)
     ap.add_argument("--image-gc-low-threshold", type=int, default=80)
     ap.add_argument("--minimum-image-ttl-duration", type=float, default=120.0, help="seconds")
+    tf = lambda s: str(s).lower() in ("true", "1", "yes")   # noqa: E731
+    srcs = lambda s: [x.strip() for x in s.split(",") if x.strip()]   # noqa: E731
+    ap.add_argument("--bootstrap-kubeconfig", "--experimental-bootstrap-kubeconfig", dest="bootstrap_kubeconfig", default=None,
+                    help="token kubeconfig used to obtain a client certificate when --kubeconfig does not exist")
+    ap.add_argument("--enable-server", type=tf, default=True)
+    ap.add_argument("--enable-debugging-handlers", type=tf, default=True)
+    ap.add_argument("--read-only-port", type=int, default=10255, help="0 disables")
+    ap.add_argument("--healthz-port", type=int, default=10248, help="0 disables")
+    ap.add_argument("--healthz-bind-address", default="127.0.0.1")
+    ap.add_argument("--manifest-url", default=None)
+    ap.add_argument("--manifest-url-header", default="", help="comma-separated key:value headers")
+    ap.add_argument("--http-check-frequency", type=float, default=20.0, help="seconds")
+    ap.add_argument("--sync-frequency", type=float, default=60.0, help="seconds")
+    ap.add_argument("--register-node", type=tf, default=True)
+    ap.add_argument("--register-schedulable", type=tf, default=True)
+    ap.add_argument("--pod-cidr", default="")
+    ap.add_argument("--provider-id", default="")
+    ap.add_argument("--allow-privileged", type=tf, default=True)
+    ap.add_argument("--host-network-sources", type=srcs, default=["*"])
+    ap.add_argument("--host-pid-sources", type=srcs, default=["*"])
+    ap.add_argument("--host-ipc-sources", type=srcs, default=["*"])
+    ap.add_argument("--pods-per-core", type=int, default=0)
+    ap.add_argument("--serialize-image-pulls", type=tf, default=True)
+    ap.add_argument("--registry-qps", type=float, default=5.0)
+    ap.add_argument("--registry-burst", type=int, default=10)
+    ap.add_argument("--event-qps", type=float, default=5.0)
+    ap.add_argument("--event-burst", type=int, default=10)
+    ap.add_argument("--kube-api-burst", type=int, default=10)
+    ap.add_argument("--kube-api-content-type", default="application/json", help="only JSON is spoken")
+    ap.add_argument("--runtime-request-timeout", type=float, default=120.0, help="seconds")
+    ap.add_argument("--image-service-endpoint", default=None)
+    ap.add_argument("--keep-terminated-pod-volumes", type=tf, default=False)
+    ap.add_argument("--volume-stats-agg-period", type=float, default=60.0, help="seconds")
+    ap.add_argument("--cpu-cfs-quota", type=tf, default=True)
+    ap.add_argument("--protect-kernel-defaults", type=tf, default=False)
+    ap.add_argument("--fail-swap-on", "--experimental-fail-swap-on", dest="fail_swap_on", type=tf, default=True)
+    ap.add_argument("--oom-score-adj", type=int, default=-999)
+    ap.add_argument("--max-open-files", type=int, default=1000000)
+    ap.add_argument("--lock-file", default=None)
+    ap.add_argument("--exit-on-lock-contention", action="store_true")
+    ap.add_argument("--seccomp-profile-root", default=None, help="directory of localhost/<name> seccomp profiles")
+    ap.add_argument("--cgroup-driver", default="cgroupfs", choices=("cgroupfs", "systemd"))
+    ap.add_argument("--cgroups-per-qos", type=tf, default=True)
+    # accepted for command-line compatibility; the settings they tune do not exist on this runtime
+    for flag in ("--cadvisor-port", "--containerized", "--hairpin-mode", "--non-masquerade-cidr", "--iptables-masquerade-bit",
+                 "--iptables-drop-bit", "--make-iptables-util-chains", "--kubelet-cgroups", "--system-cgroups",
+                 "--kube-reserved-cgroup", "--system-reserved-cgroup", "--experimental-qos-reserved", "--cloud-config",
+                 "--streaming-connection-idle-timeout", "--master-service-namespace", "--require-kubeconfig",
+                 "--init-config-dir", "--bootstrap-checkpoint-path", "--experimental-mounter-path",
+                 "--experimental-check-node-capabilities-before-mount", "--experimental-kernel-memcg-notification",
+                 "--experimental-allocatable-ignore-eviction", "--enable-custom-metrics", "--contention-profiling",
+                 "--really-crash-for-testing", "--authentication-token-webhook-cache-ttl",
+                 "--authorization-webhook-cache-authorized-ttl", "--authorization-webhook-cache-unauthorized-ttl"):
+        ap.add_argument(flag, default=None, help=argparse.SUPPRESS)
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     klog.setup(a.v, "kubelet")
+    if a.cgroup_driver == "systemd":
+        raise SystemExit("kubelet: --cgroup-driver=systemd is not supported: amdkube manages cgroup v2 directly (cgroupfs)")
+    from ..kubelet import node_setup
+    lock = node_setup.acquire_lock(a.lock_file, a.exit_on_lock_contention,
+                                   on_contention=lambda: os._exit(0)) if a.lock_file else None   # noqa: F841
+    if a.fail_swap_on and not a.runonce:
+        node_setup.check_swap()
+    node_setup.apply_oom_score_adj(a.oom_score_adj)
+    node_setup.raise_nofile(a.max_open_files)
+    if a.bootstrap_kubeconfig and a.kubeconfig:
+        node_setup.bootstrap_client_cert(a.kubeconfig, a.bootstrap_kubeconfig,
+                                         a.cert_dir or os.path.join(a.root_dir, "pki"), a.node_name)
     from ..client import Client
     from ..kubelet.kubelet import Kubelet, KubeletConfig
     labels = dict(kv.split("=", 1) for kv in a.node_labels.split(",") if "=" in kv)
@@ -351,7 +417,22 @@ def kubelet(argv):
                         client_ca_file=a.client_ca_file, anonymous_auth=a.anonymous_auth == "true",
                         authentication_token_webhook=a.authentication_token_webhook,
                         authorization_mode=a.authorization_mode, cert_dir=a.cert_dir,
-                        rotate_certificates=a.rotate_certificates, rotate_server_certificates=a.rotate_server_certificates)
+                        rotate_certificates=a.rotate_certificates, rotate_server_certificates=a.rotate_server_certificates,
+                        enable_server=a.enable_server, enable_debugging_handlers=a.enable_debugging_handlers,
+                        read_only_port=a.read_only_port, healthz_port=a.healthz_port,
+                        healthz_bind_address=a.healthz_bind_address, manifest_url=a.manifest_url,
+                        manifest_url_header=dict(h.split(":", 1) for h in a.manifest_url_header.split(",") if ":" in h),
+                        http_check_frequency=a.http_check_frequency, sync_frequency=a.sync_frequency,
+                        register_node=a.register_node, register_schedulable=a.register_schedulable,
+                        pod_cidr=a.pod_cidr, provider_id=a.provider_id, allow_privileged=a.allow_privileged,
+                        host_network_sources=a.host_network_sources, host_pid_sources=a.host_pid_sources,
+                        host_ipc_sources=a.host_ipc_sources, pods_per_core=a.pods_per_core,
+                        serialize_image_pulls=a.serialize_image_pulls, registry_qps=a.registry_qps,
+                        registry_burst=a.registry_burst, event_qps=a.event_qps, event_burst=a.event_burst,
+                        runtime_request_timeout=a.runtime_request_timeout, image_service_endpoint=a.image_service_endpoint,
+                        keep_terminated_pod_volumes=a.keep_terminated_pod_volumes,
+                        volume_stats_agg_period=a.volume_stats_agg_period, cpu_cfs_quota=a.cpu_cfs_quota,
+                        protect_kernel_defaults=a.protect_kernel_defaults, seccomp_profile_root=a.seccomp_profile_root)
 
     async def mk():
         smi = None
@@ -361,7 +442,8 @@ def kubelet(argv):
                 smi = open_backend(a.gpu_stats_backend)
             except Exception as e:
                 logging.getLogger("amdkube.kubelet").warning("no GPU stats backend: %s", e)
-        return await Kubelet(_client(a, qps=a.kube_api_qps, chaos=a.chaos_chance), cfg, smi_backend=smi).start()
+        return await Kubelet(_client(a, qps=a.kube_api_qps, burst=a.kube_api_burst, chaos=a.chaos_chance), cfg,
+                             smi_backend=smi).start()
     if a.runonce:
         # runonce.go: static pods only, no API server; exit status says whether all came up
         if not a.pod_manifest_path:
@@ -645,7 +727,8 @@ def local_up(argv):
             break
         time.sleep(0.1)
     spawn("kubelet", ["kubelet", "--server", server, "--root-dir", os.path.join(b, "kubelet"), "--device-plugin-dir", plugins,
-                      "--container-runtime-endpoint", sock, "--gpu-stats-backend", "none" if a.no_gpus else a.backend]
+                      "--container-runtime-endpoint", sock, "--gpu-stats-backend", "none" if a.no_gpus else a.backend,
+                      "--read-only-port", "0", "--healthz-port", "0", "--fail-swap-on", "false"]
           + dns_flags)
     os.makedirs(os.path.expanduser("~/.amdkube"), exist_ok=True)
     json.dump({"server": server}, open(os.path.expanduser("~/.amdkube/config"), "w"))

@@ -164,6 +164,8 @@ def start_node_agents(cfg, kubeconfig_path, node_name, labels=""):
     args = ["kubelet", "--kubeconfig", kubeconfig_path, "--node-name", node_name, "--root-dir", os.path.join(d, "kubelet"),
             "--container-runtime-endpoint", sock, "--port", str(cfg.get("kubelet_port", 0)),
             "--node-status-update-frequency", "2", "--pleg-relist-period", "0.5", "--gpu-stats-backend", "none"]
+    if not cfg.get("kubelet_port"):     # an ephemeral API port: several kubelets share this host (tests)
+        args += ["--read-only-port", "0", "--healthz-port", "0"]
     if cfg.get("manifests"):
         args += ["--pod-manifest-path", cfg["manifests"], "--file-check-frequency", "1"]
     if labels:

@@ -17,15 +17,16 @@ CURRENT_POD: contextvars.ContextVar[str | None] = contextvars.ContextVar("amdkub
 
 
 class CRIClient:
-    def __init__(self, socket_path: str, timeout: float = 10.0, metrics=None):
+    def __init__(self, socket_path: str, timeout: float = 10.0, metrics=None, image_socket: str | None = None):
         self._pod_mut: dict[str, int] = {}
         self._cid_sid: dict[str, str] = {}
         # uid -> {sandbox id: created_at of the runtime event that carries the sandbox's state after
         # the pod worker's last mutating call on it}; None: a call's final event is unknown
         self._touched: dict[str, dict[str, int] | None] = {}
         self.socket = socket_path
+        self.image_socket = image_socket        # --image-service-endpoint (None: the runtime's socket)
         self.timeout = timeout
-        self.ch = None
+        self.ch = self.img_ch = None
         self.rt = self.img = None
         self.metrics = metrics  # (ops Counter, errs Counter, latency Summary) or None
 
@@ -34,12 +35,19 @@ class CRIClient:
         import asyncio
         await asyncio.wait_for(self.ch.channel_ready(), wait)
         self.rt = C.RuntimeService.stub(self.ch)
-        self.img = C.ImageService.stub(self.ch)
+        if self.image_socket and self.image_socket != self.socket:
+            self.img_ch = uds_channel(self.image_socket)
+            await asyncio.wait_for(self.img_ch.channel_ready(), wait)
+            self.img = C.ImageService.stub(self.img_ch)
+        else:
+            self.img = C.ImageService.stub(self.ch)
         return self
 
     async def close(self):
         if self.ch is not None:
             await self.ch.close()
+        if self.img_ch is not None:
+            await self.img_ch.close()
 
     _MUTATING = frozenset(("run_podsandbox", "stop_podsandbox", "remove_podsandbox", "create_container", "start_container",
                            "stop_container", "remove_container"))

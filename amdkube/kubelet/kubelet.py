@@ -141,6 +141,35 @@ class KubeletConfig:
     volume_reconcile_period: float = 2.0              # reconciler loop period (s)
     volume_remount_period: float = 60.0               # re-render secret/configMap/downwardAPI/projected content (s)
     cloud_provider: str = ""                          # --cloud-provider ("external": cloud-controller-manager initialises the node)
+    enable_server: bool = True                        # --enable-server (the authenticated API on --port)
+    enable_debugging_handlers: bool = True            # --enable-debugging-handlers (logs, exec, attach, portForward, run, pprof)
+    read_only_port: int = -1                          # --read-only-port (unauthenticated read-only API; -1/0: off; CLI default 10255)
+    healthz_port: int = -1                            # --healthz-port (-1/0: off; CLI default 10248)
+    healthz_bind_address: str = "127.0.0.1"           # --healthz-bind-address
+    manifest_url: str | None = None                   # --manifest-url (HTTP static pod source)
+    manifest_url_header: dict = field(default_factory=dict)   # --manifest-url-header
+    http_check_frequency: float = 20.0                # --http-check-frequency (s)
+    register_node: bool = True                        # --register-node
+    register_schedulable: bool = True                 # --register-schedulable (false: registers unschedulable)
+    pod_cidr: str = ""                                # --pod-cidr (standalone; the controller's CIDR wins)
+    provider_id: str = ""                             # --provider-id
+    allow_privileged: bool = True                     # --allow-privileged
+    host_network_sources: list = field(default_factory=lambda: ["*"])   # --host-network-sources (api, file, http, *)
+    host_pid_sources: list = field(default_factory=lambda: ["*"])       # --host-pid-sources
+    host_ipc_sources: list = field(default_factory=lambda: ["*"])       # --host-ipc-sources
+    pods_per_core: int = 0                            # --pods-per-core (0: only --max-pods)
+    serialize_image_pulls: bool = True                # --serialize-image-pulls
+    registry_qps: float = 5.0                         # --registry-qps (image pulls per second; 0: unlimited)
+    registry_burst: int = 10                          # --registry-burst
+    event_qps: float = 5.0                            # --event-qps (0: unlimited)
+    event_burst: int = 10                             # --event-burst
+    runtime_request_timeout: float = 10.0             # --runtime-request-timeout (s, per CRI call; CLI default 2m)
+    image_service_endpoint: str | None = None         # --image-service-endpoint (separate CRI image service)
+    keep_terminated_pod_volumes: bool = False         # --keep-terminated-pod-volumes
+    volume_stats_agg_period: float = 60.0             # --volume-stats-agg-period (du cache TTL, s)
+    cpu_cfs_quota: bool = True                        # --cpu-cfs-quota (CPU limits become CFS quota)
+    protect_kernel_defaults: bool = False             # --protect-kernel-defaults
+    seccomp_profile_root: str | None = None           # --seccomp-profile-root (default <root-dir>/seccomp)
 
 
 class PodWorker:
@@ -176,7 +205,9 @@ class Kubelet:
         self.gates = FeatureGate(config.feature_gates)
         self.metrics = new_registry()
         self._init_metrics()
-        self.cri = CRIClient(config.cri_socket, metrics=(self.m_rt_ops, self.m_rt_errs, self.m_rt_lat))
+        self.cri = CRIClient(config.cri_socket, metrics=(self.m_rt_ops, self.m_rt_errs, self.m_rt_lat),
+                             timeout=config.runtime_request_timeout or 10.0,
+                             image_socket=config.image_service_endpoint)
         self.pods: dict[str, dict] = {}
         self.admitted: set[str] = set()
         self.rejected: dict[str, tuple[str, str]] = {}
@@ -187,8 +218,12 @@ class Kubelet:
                                   v1beta1_socket=config.v1beta1_socket)
         else:
             self.dm = ManagerStub()
-        self.recorder = EventRecorder(client, "kubelet", self.node_name)
-        self.runtime = RuntimeManager(self.cri, self.dm, config.root_dir, self.recorder)
+        self.recorder = EventRecorder(client, "kubelet", self.node_name, qps=config.event_qps, burst=config.event_burst)
+        self.runtime = RuntimeManager(self.cri, self.dm, config.root_dir, self.recorder, image_pull_qps=config.registry_qps,
+                                      image_pull_burst=config.registry_burst, serialize_image_pulls=config.serialize_image_pulls)
+        self.runtime.cpu_cfs_quota = config.cpu_cfs_quota
+        if config.seccomp_profile_root:
+            self.runtime.seccomp_root = config.seccomp_profile_root
         self.runtime.node_ip, self.runtime.cluster_domain = config.node_ip, config.cluster_domain
         import psutil as _ps
         self.runtime.memory_capacity = config.memory_capacity or _ps.virtual_memory().total
@@ -244,7 +279,7 @@ class Kubelet:
         self.runtime.gpu_numa = self._gpu_numa
         self.volume_manager = self._volume_manager(config)
         from .stats import StatsProvider
-        self.stats = StatsProvider(self)
+        self.stats = StatsProvider(self, du_ttl=config.volume_stats_agg_period)
         self._cpuset_applied: dict[str, str] = {}
         self._pods_cgroup_enforced = None
         self.pressure: set[str] = set()
@@ -328,8 +363,18 @@ class Kubelet:
                 await asyncio.wait_for(scm.rotate(), 30)
             except Exception as e:
                 log.warning("no kubelet serving certificate yet (%r); serving without TLS until one is issued", e)
+        if self.cfg.protect_kernel_defaults:
+            from .node_setup import kernel_tunables
+            kernel_tunables(True)
         from .server import KubeletServer
-        self.server = await KubeletServer(self).start(self.cfg.address, self.cfg.port)
+        if self.cfg.enable_server:
+            self.server = await KubeletServer(self).start(self.cfg.address, self.cfg.port)
+        self.extra_servers = []
+        if self.cfg.read_only_port > 0:     # server.go ListenAndServeKubeletReadOnlyServer
+            self.extra_servers.append(await KubeletServer(self, mode="readonly").start(self.cfg.address, self.cfg.read_only_port))
+        if self.cfg.healthz_port > 0:       # cmd/kubelet/app/server.go healthz listener
+            self.extra_servers.append(await KubeletServer(self, mode="healthz").start(self.cfg.healthz_bind_address,
+                                                                                       self.cfg.healthz_port))
         for cmgr in self.cert_managers:
             self._tasks.append(asyncio.create_task(cmgr.run(), name=f"cert-rotation-{cmgr.kind}"))
         self._tasks += [asyncio.create_task(self._relist_loop(), name="pleg-relist"),
@@ -342,7 +387,7 @@ class Kubelet:
         self.volume_manager.start()
         if self.cpu_manager.policy != "none":
             self._tasks.append(asyncio.create_task(self._cpu_reconcile_loop(), name="cpu-manager"))
-        if self.cfg.pod_manifest_path:
+        if self.cfg.pod_manifest_path or self.cfg.manifest_url:
             # static pods run with or without an apiserver (kubeadm: the apiserver IS a static
             # pod), so registration is retried in the background (kubelet_node_status.go
             # registerWithAPIServer: exponential back-off up to 7 s)
@@ -390,6 +435,8 @@ class Kubelet:
         await self.dm.stop()
         if self.server:
             await self.server.stop()
+        for srv in getattr(self, "extra_servers", []):
+            await srv.stop()
         await self.cri.close()
 
     # ================================================================ node
@@ -397,13 +444,23 @@ class Kubelet:
         import psutil
         cpu = self.cfg.cpu_capacity or psutil.cpu_count() or 1
         mem = self.cfg.memory_capacity or psutil.virtual_memory().total
-        cap = {"cpu": str(cpu), "memory": f"{mem // 1024}Ki", "pods": str(self.cfg.max_pods)}
+        pods = self.cfg.max_pods
+        if self.cfg.pods_per_core > 0:      # kubelet_node_status.go: min(max-pods, cores × pods-per-core)
+            pods = min(pods, cpu * self.cfg.pods_per_core)
+        cap = {"cpu": str(cpu), "memory": f"{mem // 1024}Ki", "pods": str(pods)}
         if self.gpu_legacy is not None:   # kubelet_node_status.go:557-562
             from .gpu_legacy import RESOURCE
             cap[RESOURCE] = str(self.gpu_legacy.capacity())
         return cap
 
     async def register_node(self):
+        if not self.cfg.register_node:
+            # --register-node=false: the node object is someone else's; wait for it to exist
+            while (node := await self.client.get_or_none("nodes", self.node_name)) is None:
+                await asyncio.sleep(1.0)
+            self.node = node
+            await self.update_node_status()
+            return
         labels = {"kubernetes.io/hostname": self.node_name, "beta.kubernetes.io/os": "linux",
                   "beta.kubernetes.io/arch": "amd64", **self.cfg.node_labels}
         taints = list(self.cfg.register_with_taints)
@@ -415,10 +472,16 @@ class Kubelet:
             taints.append({"key": "node.cloudprovider.kubernetes.io/uninitialized", "value": "true", "effect": "NoSchedule"})
             if self.cfg.node_ip:
                 ann["alpha.kubernetes.io/provided-node-ip"] = self.cfg.node_ip
+        spec = {"taints": taints} if taints else {}
+        if not self.cfg.register_schedulable:
+            spec["unschedulable"] = True
+        if self.cfg.pod_cidr:
+            spec["podCIDR"] = self.cfg.pod_cidr
+        if self.cfg.provider_id:
+            spec["providerID"] = self.cfg.provider_id
         node = {"apiVersion": "v1", "kind": "Node", "metadata": {"name": self.node_name, "labels": labels,
                                                                 "annotations": ann},
-                "spec": {"taints": taints} if taints else {},
-                "status": self._node_status_body({})}
+                "spec": spec, "status": self._node_status_body({})}
         node["status"].pop("_removed", None)
         try:
             self.node = await self.client.create(node)
@@ -498,7 +561,7 @@ class Kubelet:
             ann[TOPOLOGY_LABEL] = labels[TOPOLOGY_LABEL]
         try:
             self.node = await self.client.patch("nodes", self.node_name, patch, sub="status")
-            cidr = (self.node.get("spec") or {}).get("podCIDR") or ""
+            cidr = (self.node.get("spec") or {}).get("podCIDR") or self.cfg.pod_cidr or ""
             if cidr and cidr != getattr(self, "_pod_cidr", ""):
                 # kubelet_network.go updatePodCIDR → CRI UpdateRuntimeConfig
                 await self.cri.update_runtime_config(cidr)
@@ -574,39 +637,76 @@ class Kubelet:
         the node name and the file content (config/common.go applyDefaults)."""
         import hashlib
         import uuid as _uuid
-        from ..api.scheme import load_manifests
         out = {}
+        for doc, fallback, source in self._file_docs() + self._http_docs():
+            md = doc.setdefault("metadata", {})
+            md["name"] = f"{md.get('name', fallback)}-{self.node_name}"
+            md["namespace"] = md.get("namespace") or "default"
+            h = hashlib.md5((self.node_name + json.dumps(doc, sort_keys=True)).encode()).hexdigest()
+            md["uid"] = str(_uuid.UUID(h))
+            md.setdefault("annotations", {}).update({HASH_ANNOTATION: h, SOURCE_ANNOTATION: source})
+            md.setdefault("creationTimestamp", m.now_rfc3339())
+            doc["apiVersion"], doc["kind"] = "v1", "Pod"
+            doc.setdefault("spec", {})["nodeName"] = self.node_name
+            doc["spec"].setdefault("restartPolicy", "Always")
+            doc.setdefault("status", {"phase": "Pending"})
+            out[md["uid"]] = doc
+        return out
+
+    def _file_docs(self) -> list[tuple[dict, str, str]]:
+        from ..api.scheme import load_manifests
         d = self.cfg.pod_manifest_path
+        if not d:
+            return []
         try:
             files = sorted(f for f in os.listdir(d) if f.endswith((".yaml", ".yml", ".json")) and not f.startswith("."))
         except OSError:
-            return out
+            return []
+        out = []
         for f in files:
             try:
                 with open(os.path.join(d, f)) as fh:
                     text = fh.read()
-                docs = [x for x in load_manifests(text) if x.get("kind", "Pod") == "Pod"]
+                out += [(x, os.path.splitext(f)[0], "file") for x in load_manifests(text) if x.get("kind", "Pod") == "Pod"]
             except Exception as e:
                 log.warning("static pod manifest %s is invalid: %r", f, e)
-                continue
-            for doc in docs:
-                md = doc.setdefault("metadata", {})
-                md["name"] = f"{md.get('name', os.path.splitext(f)[0])}-{self.node_name}"
-                md["namespace"] = md.get("namespace") or "default"
-                h = hashlib.md5((self.node_name + json.dumps(doc, sort_keys=True)).encode()).hexdigest()
-                md["uid"] = str(_uuid.UUID(h))
-                md.setdefault("annotations", {}).update({HASH_ANNOTATION: h, SOURCE_ANNOTATION: "file"})
-                md.setdefault("creationTimestamp", m.now_rfc3339())
-                doc["apiVersion"], doc["kind"] = "v1", "Pod"
-                doc.setdefault("spec", {})["nodeName"] = self.node_name
-                doc["spec"].setdefault("restartPolicy", "Always")
-                doc.setdefault("status", {"phase": "Pending"})
-                out[md["uid"]] = doc
+        return out
+
+    def _http_docs(self) -> list[tuple[dict, str, str]]:
+        """config/http.go: --manifest-url returns one Pod, a PodList or a v1 List of pods (with
+        --manifest-url-header sent); fetched at most every --http-check-frequency, and a failed
+        fetch keeps the last good answer."""
+        url = self.cfg.manifest_url
+        if not url:
+            return []
+        now = time.monotonic()
+        cached = getattr(self, "_http_cache", None)
+        if cached is not None and now - cached[0] < self.cfg.http_check_frequency:
+            return json.loads(cached[1])
+        import urllib.request
+        from ..api.scheme import load_manifests
+        try:
+            req = urllib.request.Request(url, headers=dict(self.cfg.manifest_url_header))
+            with urllib.request.urlopen(req, timeout=10) as r:
+                if r.status != 200:
+                    raise OSError(f"HTTP {r.status}")
+                text = r.read().decode()
+            docs = []
+            for d in load_manifests(text):
+                if d.get("kind") in ("PodList", "List"):
+                    docs += [x for x in d.get("items") or [] if x.get("kind", "Pod") == "Pod"]
+                elif d.get("kind", "Pod") == "Pod":
+                    docs.append(d)
+            out = [(x, "http-pod", "http") for x in docs]
+        except Exception as e:
+            log.warning("static pods from %s: %r", url, e)
+            return json.loads(cached[1]) if cached is not None else []
+        self._http_cache = (now, json.dumps(out))
         return out
 
     async def _static_pods_loop(self):
         while True:
-            want = self._read_manifests()
+            want = await asyncio.to_thread(self._read_manifests)
             for uid in [u for u in self.static if u not in want]:   # manifest removed or changed
                 old = self.static.pop(uid)
                 self.pods.pop(uid, None)
@@ -628,8 +728,11 @@ class Kubelet:
                     log.debug("mirror pod for %s: %r", m.name_of(pod), e)
             self._static_dirty.clear()
             self._static_read = True
+            period = self.cfg.file_check_frequency if self.cfg.pod_manifest_path else self.cfg.http_check_frequency
+            if self.cfg.pod_manifest_path and self.cfg.manifest_url:
+                period = min(period, self.cfg.http_check_frequency)
             try:
-                await asyncio.wait_for(self._static_dirty.wait(), self.cfg.file_check_frequency)
+                await asyncio.wait_for(self._static_dirty.wait(), period)
             except asyncio.TimeoutError:
                 pass
 
@@ -730,6 +833,9 @@ class Kubelet:
                                        ("NoExecute",))
         if taint:
             return False, "Taint", f"pod does not tolerate taint {taint.get('key')}={taint.get('value', '')}:NoExecute"
+        ok, reason, msg = self._can_run(pod)
+        if not ok:
+            return False, reason, msg
         ok, msg = self.eviction.admit(pod, self.pressure)   # eviction_manager.go Admit
         if not ok:
             return False, "Evicted", msg
@@ -740,6 +846,21 @@ class Kubelet:
         err = self.apparmor.validate(pod)   # lifecycle/handlers.go:142-165
         if err:
             return False, "AppArmor", f"Cannot enforce AppArmor: {err}"
+        return True, "", ""
+
+    def _can_run(self, pod: dict) -> tuple[bool, str, str]:
+        """kubelet_pods.go canRunPod: --allow-privileged and the --host-{network,pid,ipc}-sources
+        allow-lists (a pod's source is file, http or api)."""
+        spec = pod.get("spec") or {}
+        src = m.annotations_of(pod).get(SOURCE_ANNOTATION) or "api"
+        for field_, allowed in (("hostNetwork", self.cfg.host_network_sources), ("hostPID", self.cfg.host_pid_sources),
+                                ("hostIPC", self.cfg.host_ipc_sources)):
+            if spec.get(field_) and "*" not in allowed and src not in allowed:
+                return False, "Forbidden", f"pod with UID {m.uid_of(pod)} specified {field_}, but is disallowed for source {src}"
+        if not self.cfg.allow_privileged:
+            for c in (spec.get("initContainers") or []) + (spec.get("containers") or []):
+                if ((c.get("securityContext") or {}).get("privileged")):
+                    return False, "Forbidden", f"pod with UID {m.uid_of(pod)} specified privileged container, but is disallowed"
         return True, "", ""
 
     def _shortfall(self, pod: dict) -> dict[str, int]:
@@ -843,7 +964,8 @@ class Kubelet:
             # recomputation must not drop the reason of a kubelet-decided failure (deadline,
             # eviction) that may not be written yet
             await self.runtime.kill_pod(uid, 0, pod, self._cached_sandboxes(uid))
-            self.volume_manager.remove_pod(uid)     # terminated: its volumes go (populator findAndRemoveDeletedPods)
+            if not self.cfg.keep_terminated_pod_volumes:
+                self.volume_manager.remove_pod(uid)     # terminated: its volumes go (populator findAndRemoveDeletedPods)
             return False
         if sent_phase not in ("Succeeded", "Failed") and self._active_deadline_exceeded(pod):
             # active_deadline.go: the pod sync handler fails the pod once it has been active on
@@ -893,7 +1015,8 @@ class Kubelet:
         if st["phase"] in ("Succeeded", "Failed"):
             # release the sandbox (devices stay API-assigned)
             await self.runtime.kill_pod(uid, 0, pod, self._cached_sandboxes(uid))
-            self.volume_manager.remove_pod(uid)
+            if not self.cfg.keep_terminated_pod_volumes:
+                self.volume_manager.remove_pod(uid)
         ads = (pod.get("spec") or {}).get("activeDeadlineSeconds")
         if ads is not None and st["phase"] not in ("Succeeded", "Failed") and uid not in self._deadline_timers:
             start = m.parse_time(st.get("startTime"))
@@ -1238,7 +1361,7 @@ class Kubelet:
         complete set (the API informer synced; --pod-manifest-path read once). Until then a pod
         the kubelet does not know may simply not have been seen yet."""
         api = self.informer is not None and self.informer.has_synced()
-        return api and (not self.cfg.pod_manifest_path or self._static_read)
+        return api and (not (self.cfg.pod_manifest_path or self.cfg.manifest_url) or self._static_read)
 
     async def _gc_loop(self):
         last_image_gc = time.monotonic()

@@ -146,8 +146,15 @@ def apply_event(rt: PodRuntimeStatus, ev, sandbox_ips: dict) -> PodRuntimeStatus
 
 
 class RuntimeManager:
-    def __init__(self, cri: CRIClient, device_manager, root_dir: str, recorder=None, image_pull_qps: float = 0):
+    def __init__(self, cri: CRIClient, device_manager, root_dir: str, recorder=None, image_pull_qps: float = 0,
+                 image_pull_burst: int = 10, serialize_image_pulls: bool = True):
         self.cri = cri
+        # images/image_manager.go: --serialize-image-pulls (one pull at a time) and
+        # --registry-qps/--registry-burst (a token bucket in front of the puller)
+        from ..client.rest import TokenBucket
+        self._pull_sem = asyncio.Semaphore(1) if serialize_image_pulls else None
+        self._pull_limiter = TokenBucket(image_pull_qps, image_pull_burst or 1) if image_pull_qps else None
+        self.cpu_cfs_quota = True   # --cpu-cfs-quota
         self.dm = device_manager
         self.root = root_dir
         self.recorder = recorder
@@ -228,7 +235,13 @@ class RuntimeManager:
             raise RuntimeError(f"ErrImageNeverPull: image {image} not present with pull policy Never")
         if present is None or policy == "Always":
             try:
-                await self.cri.pull_image(image)
+                if self._pull_limiter is not None:
+                    await self._pull_limiter.wait()
+                if self._pull_sem is not None:
+                    async with self._pull_sem:
+                        await self.cri.pull_image(image)
+                else:
+                    await self.cri.pull_image(image)
             except grpc.RpcError as e:
                 if present is None:
                     raise RuntimeError(f"ErrImagePull: {e.details()}")
@@ -272,7 +285,7 @@ class RuntimeManager:
         lres = C.LinuxContainerResources(oom_score_adj=oom_score_adj(pod, c, self.memory_capacity))
         if "memory" in res:
             lres.memory_limit_in_bytes = Quantity(res["memory"]).value()
-        if "cpu" in res:
+        if "cpu" in res and self.cpu_cfs_quota:
             lres.cpu_period = 100000
             lres.cpu_quota = max(1000, Quantity(res["cpu"]).milli_value() * 100)
         req_cpu = ((c.get("resources") or {}).get("requests") or {}).get("cpu") or res.get("cpu")

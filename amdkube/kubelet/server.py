@@ -21,27 +21,34 @@ from ..utils.metrics import CONTENT_TYPE, render
 
 
 class KubeletServer:
-    def __init__(self, kubelet):
+    """mode "full": the authenticated API on --port (debugging handlers unless
+    --enable-debugging-handlers=false); "readonly": --read-only-port, unauthenticated, only the
+    default handlers (server.go ListenAndServeKubeletReadOnlyServer); "healthz": --healthz-port."""
+
+    def __init__(self, kubelet, mode: str = "full"):
         self.k = kubelet
-        mws = [kubelet.auth.middleware()] if getattr(kubelet, "auth", None) is not None else []
+        self.mode = mode
+        mws = [kubelet.auth.middleware()] if mode == "full" and getattr(kubelet, "auth", None) is not None else []
         app = self.app = web.Application(middlewares=mws)
         app.router.add_get("/healthz", self.healthz)
         app.router.add_get("/healthz/syncloop", self.healthz)
-        app.router.add_get("/pods", self.pods)
-        app.router.add_get("/runningpods/", self.running_pods)
-        app.router.add_get("/metrics", self.metrics)
-        app.router.add_get("/metrics/cadvisor", self.metrics_cadvisor)
-        app.router.add_get("/stats/summary", self.summary)
-        app.router.add_get("/stats/", self.summary)
-        app.router.add_get("/spec/", self.spec)
-        app.router.add_get("/spec", self.spec)
-        app.router.add_get("/containerLogs/{ns}/{pod}/{container}", self.logs)
-        app.router.add_post("/run/{ns}/{pod}/{container}", self.run)
-        for meth in ("GET", "POST"):
-            app.router.add_route(meth, "/exec/{ns}/{pod}/{container}", self.exec_stream)
-            app.router.add_route(meth, "/attach/{ns}/{pod}/{container}", self.attach_stream)
-            app.router.add_route(meth, "/portForward/{ns}/{pod}", self.port_forward)
-        profiling.add_routes(app)
+        if mode != "healthz":
+            app.router.add_get("/pods", self.pods)
+            app.router.add_get("/metrics", self.metrics)
+            app.router.add_get("/metrics/cadvisor", self.metrics_cadvisor)
+            app.router.add_get("/stats/summary", self.summary)
+            app.router.add_get("/stats/", self.summary)
+            app.router.add_get("/spec/", self.spec)
+            app.router.add_get("/spec", self.spec)
+        if mode == "full" and getattr(getattr(kubelet, "cfg", None), "enable_debugging_handlers", True):
+            app.router.add_get("/runningpods/", self.running_pods)
+            app.router.add_get("/containerLogs/{ns}/{pod}/{container}", self.logs)
+            app.router.add_post("/run/{ns}/{pod}/{container}", self.run)
+            for meth in ("GET", "POST"):
+                app.router.add_route(meth, "/exec/{ns}/{pod}/{container}", self.exec_stream)
+                app.router.add_route(meth, "/attach/{ns}/{pod}/{container}", self.attach_stream)
+                app.router.add_route(meth, "/portForward/{ns}/{pod}", self.port_forward)
+            profiling.add_routes(app)
         self.runner = None
         self.port = None
 
@@ -70,7 +77,7 @@ class KubeletServer:
         self.runner = web.AppRunner(self.app, access_log=None)
         await self.runner.setup()
         self.ssl = None
-        site = web.TCPSite(self.runner, host, port, reuse_address=True, ssl_context=self._ssl())
+        site = web.TCPSite(self.runner, host, port, reuse_address=True, ssl_context=self._ssl() if self.mode == "full" else None)
         await site.start()
         self.port = site._server.sockets[0].getsockname()[1]
         return self

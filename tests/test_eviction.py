@@ -91,7 +91,7 @@ async def test_memory_pressure_condition_admission_and_eviction():
         assert victim["metadata"]["name"] == "be"
         p = await wait_pod(c, "default", "be", ("Failed",), 10)
         assert p["status"]["reason"] == "Evicted" and "memory" in p["status"]["message"]
-        for _ in range(100):
+        for _ in range(400):
             node = await c.get("nodes", lc.node_name)
             conds = {x["type"]: x["status"] for x in node["status"]["conditions"]}
             if conds["MemoryPressure"] == "True":

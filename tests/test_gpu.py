@@ -138,6 +138,47 @@ def test_05_cpu_manager_exclusive_cpus_near_the_gpu():
     run(go(), 300)
 
 
+def test_06_accelerator_stats_of_a_running_gpu_pod():
+    """cAdvisor accelerator path on the real MI355X (F24, U18/U19): while a gpu-burn pod runs,
+    /stats/summary attributes the busy GPU to its container (memory in use, duty cycle) and
+    /metrics/cadvisor exports container_accelerator_* for it; the node lists the GPU too."""
+    async def go():
+        async with LocalCluster(gpus="amdsmi", n_gpus=1, relist_period=0.5, with_controllers=False) as lc:
+            node = await lc.wait_gpus(1, 60)
+            [did] = list(node["status"]["extendedResources"]["amd.com/gpu"]["resources"])
+            pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "burn", "namespace": "default"},
+                   "spec": {"restartPolicy": "Never", "containers": [{
+                       "name": "burn", "image": "amdkube/gpu-burn", "args": ["--ms", "6000"],
+                       "resources": {"limits": {"amd.com/gpu": "1"}}}]}}
+            await lc.client.create(pod)
+            await wait_pod(lc.client, "default", "burn", ("Running",), 60)
+            best, seen, text = {}, False, ""
+            loop = asyncio.get_running_loop()
+            end = loop.time() + 8
+            while loop.time() < end:
+                summ = await lc.kubelet.stats.summary()
+                for ps in summ["pods"]:
+                    if ps["podRef"]["name"] != "burn":
+                        continue
+                    for cs in ps["containers"]:
+                        for acc in cs.get("accelerators") or []:
+                            seen = True
+                            assert acc["id"] == did and acc["make"] == "amd", acc
+                            assert acc["memoryTotal"] >= 250 * 2 ** 30, acc
+                            for k in ("memoryUsed", "dutyCycle"):
+                                best[k] = max(best.get(k, 0), acc[k])
+                if best.get("dutyCycle", 0) > 0 and best.get("memoryUsed", 0) > 0:
+                    text = await lc.kubelet.stats.render_cadvisor()
+                    break
+                await asyncio.sleep(0.25)
+            assert seen and best.get("dutyCycle", 0) > 0 and best.get("memoryUsed", 0) > 0, best
+            assert f'container_accelerator_duty_cycle{{container_name="burn",pod_name="burn",namespace="default"' in text
+            assert any(a["id"] == did for a in summ["node"]["accelerators"])
+            p = await wait_pod(lc.client, "default", "burn", ("Succeeded", "Failed"), 60)
+            assert p["status"]["phase"] == "Succeeded", p["status"]
+    run(go(), 300)
+
+
 def test_04_probe_binaries():
     r = subprocess.run([os.path.join(BIN, "hbm-probe"), "--mib", "1024", "--iters", "3"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr

@@ -260,9 +260,13 @@ def test_local_storage_capacity_isolation_eviction():
                 await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name}, "spec": spec}, "default")
             for name in specs:
                 await wait_pod(c, "default", name, timeout=30)
-            await asyncio.sleep(1.0)     # the writes land
-            lc.kubelet.stats.du.forget("")
-            evicted = {m.name_of(p) for p in await lc.kubelet.local_storage_eviction()}
+            evicted = set()
+            for _ in range(60):          # until the writes have landed (slow under a loaded machine)
+                lc.kubelet.stats.du.forget("")
+                evicted |= {m.name_of(p) for p in await lc.kubelet.local_storage_eviction()}
+                if evicted >= {"hog", "chatty"}:
+                    break
+                await asyncio.sleep(0.25)
             assert evicted == {"hog", "chatty"}, evicted
             for name, reason in (("hog", "EmptyDir volume"), ("chatty", "local ephemeral storage limit")):
                 p = await wait_pod(c, "default", name, ("Failed",), 20)
