@@ -30,6 +30,40 @@ def _client(a, **kw):
     return Client(a.server, token=getattr(a, "token", None), **kw)
 
 
+async def _serve_health(component, host: str, port: int, name: str):
+    """/healthz and /metrics of a control-plane daemon (the reference's insecure --port)."""
+    from aiohttp import web
+    from ..utils import profiling
+    from ..utils.metrics import CONTENT_TYPE, new_registry, render
+    app = web.Application()
+
+    async def healthz(_):
+        return web.Response(text="ok")
+
+    async def metrics(_):
+        reg = getattr(component, "metrics", None) or new_registry()
+        return web.Response(body=render(reg), headers={"Content-Type": CONTENT_TYPE})
+    app.router.add_get("/healthz", healthz)
+    app.router.add_get("/metrics", metrics)
+    profiling.add_routes(app)
+    runner = web.AppRunner(app, access_log=None)
+    await runner.setup()
+    try:
+        await web.TCPSite(runner, host, port, reuse_address=True).start()
+    except OSError as e:
+        logging.getLogger(f"amdkube.{name}").warning("cannot serve /healthz on %s:%d: %s", host, port, e)
+        await runner.cleanup()
+        return None
+    logging.getLogger(f"amdkube.{name}").info("serving /healthz and /metrics on %s:%d", host, port)
+    stop = getattr(component, "stop", None)
+    if stop is not None:
+        async def stop_all():
+            await runner.cleanup()
+            await stop()
+        component.stop = stop_all
+    return runner
+
+
 def _run_forever(coro_factory):
     async def main():
         stop = asyncio.Event()
@@ -177,6 +211,37 @@ def controller_manager(argv):
     ap.add_argument("--horizontal-pod-autoscaler-upscale-delay", type=float, default=180.0)
     ap.add_argument("--horizontal-pod-autoscaler-downscale-delay", type=float, default=300.0)
     ap.add_argument("--hostpath-pv-root", default="/var/lib/amdkube/hostpath-pv")
+    ap.add_argument("--node-monitor-period", type=float, default=5.0)
+    ap.add_argument("--node-startup-grace-period", type=float, default=60.0)
+    ap.add_argument("--node-eviction-rate", type=float, default=0.1)
+    ap.add_argument("--secondary-node-eviction-rate", type=float, default=0.01)
+    ap.add_argument("--unhealthy-zone-threshold", type=float, default=0.55)
+    ap.add_argument("--large-cluster-size-threshold", type=int, default=50)
+    ap.add_argument("--enable-taint-manager", default="true", choices=("true", "false"))
+    ap.add_argument("--terminated-pod-gc-threshold", type=int, default=12500)
+    ap.add_argument("--feature-gates", default="", help="TaintBasedEvictions=false selects the legacy pod-deletion path")
+    ap.add_argument("--kube-api-qps", type=float, default=20.0)
+    ap.add_argument("--kube-api-burst", type=int, default=30)
+    ap.add_argument("--address", default="127.0.0.1", help="healthz/metrics listener")
+    ap.add_argument("--port", type=int, default=10252, help="healthz/metrics port (0: off)")
+    # accepted for command-line compatibility; this controller manager has no such knob
+    for flag in ("--concurrent-deployment-syncs", "--concurrent-endpoint-syncs", "--concurrent-gc-syncs",
+                 "--concurrent-namespace-syncs", "--concurrent-replicaset-syncs", "--concurrent-resource-quota-syncs",
+                 "--concurrent-service-syncs", "--concurrent-serviceaccount-token-syncs", "--concurrent-rc-syncs",
+                 "--deployment-controller-sync-period", "--namespace-sync-period", "--pvclaimbinder-sync-period",
+                 "--resource-quota-sync-period", "--route-reconciliation-period", "--node-sync-period", "--service-sync-period",
+                 "--min-resync-period", "--controller-start-interval", "--attach-detach-reconcile-sync-period",
+                 "--disable-attach-detach-reconcile-sync", "--horizontal-pod-autoscaler-tolerance",
+                 "--horizontal-pod-autoscaler-use-rest-clients", "--experimental-cluster-signing-duration",
+                 "--enable-dynamic-provisioning", "--enable-hostpath-provisioner", "--flex-volume-plugin-dir",
+                 "--use-service-account-credentials", "--service-cluster-ip-range", "--cidr-allocator-type",
+                 "--allow-untagged-cloud", "--deleting-pods-qps", "--deleting-pods-burst", "--register-retry-count",
+                 "--kube-api-content-type", "--profiling", "--contention-profiling", "--enable-garbage-collector",
+                 "--insecure-experimental-approve-all-kubelet-csrs-for-group", "--pv-recycler-increment-timeout-nfs",
+                 "--pv-recycler-minimum-timeout-hostpath", "--pv-recycler-minimum-timeout-nfs",
+                 "--pv-recycler-pod-template-filepath-hostpath", "--pv-recycler-pod-template-filepath-nfs",
+                 "--pv-recycler-timeout-increment-hostpath"):
+        ap.add_argument(flag, default=None, help=argparse.SUPPRESS)
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     klog.setup(a.v, "controller-manager")
@@ -194,12 +259,22 @@ def controller_manager(argv):
                    cluster_signing_cert_file=a.cluster_signing_cert_file, cluster_signing_key_file=a.cluster_signing_key_file,
                    hostpath_pv_root=a.hostpath_pv_root, hpa_sync_period=a.horizontal_pod_autoscaler_sync_period,
                    hpa_upscale_delay=a.horizontal_pod_autoscaler_upscale_delay,
-                   hpa_downscale_delay=a.horizontal_pod_autoscaler_downscale_delay)
+                   hpa_downscale_delay=a.horizontal_pod_autoscaler_downscale_delay,
+                   node_monitor_period=a.node_monitor_period, node_startup_grace=a.node_startup_grace_period,
+                   node_eviction_rate=a.node_eviction_rate, secondary_node_eviction_rate=a.secondary_node_eviction_rate,
+                   unhealthy_zone_threshold=a.unhealthy_zone_threshold,
+                   large_cluster_size_threshold=a.large_cluster_size_threshold,
+                   enable_taint_manager=a.enable_taint_manager == "true",
+                   terminated_pod_gc_threshold=a.terminated_pod_gc_threshold,
+                   taint_based_evictions="TaintBasedEvictions=false" not in a.feature_gates.replace(" ", ""))
     names = resolve_controllers(a.controllers, opts)
 
     async def mk():
-        return await ControllerManager(_client(a), names, a.leader_elect == "true", socket.gethostname(),
-                                       options=opts).start()
+        cm = await ControllerManager(_client(a, qps=a.kube_api_qps, burst=a.kube_api_burst), names,
+                                     a.leader_elect == "true", socket.gethostname(), options=opts).start()
+        if a.port:
+            await _serve_health(cm, a.address, a.port, "kube-controller-manager")
+        return cm
     _run_forever(mk)
 
 

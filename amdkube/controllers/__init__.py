@@ -53,18 +53,32 @@ class Options:
     hpa_upscale_delay: float = 180.0
     hpa_downscale_delay: float = 300.0
     hpa_metrics: object = None
+    node_monitor_period: float = 5.0              # --node-monitor-period
+    node_startup_grace: float = 60.0              # --node-startup-grace-period
+    node_eviction_rate: float = 0.1               # --node-eviction-rate (nodes/s per zone)
+    secondary_node_eviction_rate: float = 0.01    # --secondary-node-eviction-rate
+    unhealthy_zone_threshold: float = 0.55        # --unhealthy-zone-threshold
+    large_cluster_size_threshold: int = 50        # --large-cluster-size-threshold
+    enable_taint_manager: bool = True             # --enable-taint-manager
+    taint_based_evictions: bool = True            # --feature-gates TaintBasedEvictions
+    terminated_pod_gc_threshold: int = 12500      # --terminated-pod-gc-threshold
     extra: dict = field(default_factory=dict)
 
 
 ALL = {
-    "nodelifecycle": lambda mgr, o: NodeLifecycleController(mgr, grace=o.node_monitor_grace, eviction_timeout=o.pod_eviction_timeout),
+    "nodelifecycle": lambda mgr, o: NodeLifecycleController(
+        mgr, grace=o.node_monitor_grace, eviction_timeout=o.pod_eviction_timeout, period=o.node_monitor_period,
+        startup_grace=o.node_startup_grace, eviction_rate=o.node_eviction_rate,
+        secondary_eviction_rate=o.secondary_node_eviction_rate, unhealthy_zone_threshold=o.unhealthy_zone_threshold,
+        large_cluster_threshold=o.large_cluster_size_threshold, enable_taint_manager=o.enable_taint_manager,
+        taint_based_evictions=o.taint_based_evictions),
     "replicaset": lambda mgr, o: ReplicaSetController(mgr),
     "deployment": lambda mgr, o: DeploymentController(mgr),
     "daemonset": lambda mgr, o: DaemonSetController(mgr),
     "job": lambda mgr, o: JobController(mgr),
     "namespace": lambda mgr, o: NamespaceController(mgr),
     "garbagecollector": lambda mgr, o: GarbageCollector(mgr),
-    "podgc": lambda mgr, o: PodGCController(mgr),
+    "podgc": lambda mgr, o: PodGCController(mgr, threshold=o.terminated_pod_gc_threshold),
     "endpoint": lambda mgr, o: EndpointsController(mgr),
     "nodeipam": lambda mgr, o: NodeIPAMController(mgr, o.cluster_cidr, o.node_cidr_mask_size),
     "replicationcontroller": lambda mgr, o: ReplicationManager(mgr),

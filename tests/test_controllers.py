@@ -125,7 +125,9 @@ def test_namespace_deletion_and_node_lifecycle():
                             "spec": {"nodeName": "ghost", "containers": [{"name": "c", "image": "busybox"}],
                                      "tolerations": [{"key": "node.kubernetes.io/unreachable", "operator": "Exists",
                                                       "effect": "NoExecute", "tolerationSeconds": 0}]}})
-            nlc = NodeLifecycleController(lc.controllers, grace=1.0, eviction_timeout=0.0)
+            # (the kubelet's own node stays within the grace period: with every node down the
+            # controller would enter master disruption mode and evict nothing)
+            nlc = NodeLifecycleController(lc.controllers, grace=30.0, eviction_timeout=0.0)
             nlc.setup()
             await until(lambda: _has(lc, "ghost"), 10)
             await nlc.monitor_once()
@@ -141,3 +143,125 @@ def test_namespace_deletion_and_node_lifecycle():
 
 async def _has(lc, name):
     return any(m.name_of(n) == name for n in lc.controllers.nodes.list())
+
+
+def test_node_lifecycle_zones_rate_limits_and_taint_manager():
+    """node_controller_test.go (zone states, rate-limited tainting and eviction, master
+    disruption) and taint_controller_test.go (tolerationSeconds)."""
+    from amdkube.controllers.lifecycle import FULL, NORMAL, PARTIAL, zone_state
+    assert zone_state(3, 0, 0.55) == NORMAL and zone_state(0, 2, 0.55) == FULL
+    assert zone_state(2, 3, 0.55) == PARTIAL and zone_state(10, 3, 0.55) == NORMAL and zone_state(1, 2, 0.55) == NORMAL
+
+    async def go():
+        async with LocalCluster(gpus="none", with_kubelet=False) as lc:
+            c = lc.client
+            dead = "2000-01-01T00:00:00Z"
+
+            async def node(name, hb, zone="z1"):
+                await c.create({"apiVersion": "v1", "kind": "Node", "metadata": {"name": name, "labels": {
+                    "failure-domain.beta.kubernetes.io/region": "r", "failure-domain.beta.kubernetes.io/zone": zone}},
+                    "status": {"conditions": [{"type": "Ready", "status": "True", "lastHeartbeatTime": hb}]}})
+
+            async def pod(name, node_name, tols=None):
+                await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "default"},
+                                "spec": {"nodeName": node_name, "containers": [{"name": "c", "image": "busybox"}],
+                                         "tolerations": tols or []}})
+                p = await c.get("pods", name, "default")
+                p["status"] = {"phase": "Running", "conditions": [{"type": "Ready", "status": "True"}]}
+                await c.update_status(p)
+            for n in ("a1", "a2"):
+                await node(n, dead)
+            await node("b1", m.now_rfc3339(), "z2")
+            await pod("on-a1", "a1")      # DefaultTolerationSeconds admission: tolerates unreachable for 300 s
+            await pod("forever", "a1", [{"key": "node.kubernetes.io/unreachable", "operator": "Exists", "effect": "NoExecute"}])
+            await until(lambda: _count(lc, 3), 10)
+            await until(lambda: _pods(lc, 2), 10)
+            t0 = time.time()
+            # taint-based evictions: one node tainted per token (0.5/s)
+            nlc = NodeLifecycleController(lc.controllers, grace=1000.0, eviction_rate=0.5)
+            nlc.setup()
+            await nlc.monitor_once(now=t0)
+            assert nlc.zone_states == {"r:\x00:z1": FULL, "r:\x00:z2": NORMAL}
+            tainted = lambda ns: [n for n in ns if any(t["key"] == "node.kubernetes.io/unreachable"  # noqa: E731
+                                                       for t in (n.get("spec") or {}).get("taints") or [])]
+            nodes = [await c.get("nodes", n) for n in ("a1", "a2")]
+            assert len(tainted(nodes)) == 1
+            p = await c.get("pods", "on-a1", "default")
+            assert [x["status"] for x in p["status"]["conditions"] if x["type"] == "Ready"] == ["False"]
+            await until(lambda: _tainted(lc, "a1") if tainted(nodes)[0]["metadata"]["name"] == "a1" else _tainted(lc, "a2"), 10)
+            await nlc.monitor_once(now=t0 + 0.5)
+            assert len(tainted([await c.get("nodes", n) for n in ("a1", "a2")])) == 1
+            await nlc.monitor_once(now=t0 + 2.5)
+            assert len(tainted([await c.get("nodes", n) for n in ("a1", "a2")])) == 2
+            await until(lambda: _tainted(lc, "a1"), 10)
+            # the taint manager: the 300 s default toleration, the forever toleration
+            added = m.parse_time(next(t["timeAdded"] for t in (await c.get("nodes", "a1"))["spec"]["taints"]))
+            await nlc.taint_manager.process_once(now=added + 299)
+            assert not await _deleted(c, "on-a1")
+            await nlc.taint_manager.process_once(now=added + 301)
+            assert await _deleted(c, "on-a1") and not await _deleted(c, "forever")
+            # the legacy path (TaintBasedEvictions off): delete pods after --pod-eviction-timeout, rate limited
+            await pod("x1", "a1")
+            await pod("x2", "a2")
+            await until(lambda: _pods_named(lc, "x2"), 10)
+            legacy = NodeLifecycleController(lc.controllers, grace=1000.0, eviction_timeout=5.0, eviction_rate=0.5,
+                                             taint_based_evictions=False, enable_taint_manager=False)
+            legacy.setup()
+            await legacy.monitor_once(now=t0)
+            await legacy.monitor_once(now=t0 + 6)
+            assert sum([await _deleted(c, n) for n in ("x1", "x2")]) == 1
+            await legacy.monitor_once(now=t0 + 8.5)
+            assert all([await _deleted(c, n) for n in ("x1", "x2")])
+            # every zone down: master disruption mode lifts the taints and evicts nothing
+            b1 = await c.get("nodes", "b1")
+            b1["status"]["conditions"][0]["lastHeartbeatTime"] = dead
+            await c.update_status(b1)
+            for _ in range(100):
+                if get_cond(lc, "b1") == dead:
+                    break
+                await asyncio.sleep(0.05)
+            await nlc.monitor_once(now=t0 + 20)
+            assert nlc.master_disruption
+            for n in ("a1", "a2", "b1"):
+                assert not any(t["key"].startswith("node.kubernetes.io/") for t in (await c.get("nodes", n))["spec"].get("taints") or [])
+            # a user NoExecute taint on a healthy node: untolerating pods go at once
+            await node("g1", m.now_rfc3339(), "z3")
+            await pod("plain", "g1")
+            await pod("brief", "g1", [{"key": "maint", "operator": "Exists", "effect": "NoExecute", "tolerationSeconds": 30}])
+            await c.patch("nodes", "g1", {"spec": {"taints": [{"key": "maint", "value": "x", "effect": "NoExecute",
+                                                                "timeAdded": "2030-01-01T00:00:00Z"}]}})
+            await until(lambda: _tainted(lc, "g1"), 10)
+            await until(lambda: _pods_named(lc, "brief"), 10)
+            start = m.parse_time("2030-01-01T00:00:00Z")
+            await nlc.taint_manager.process_once(now=start + 1)
+            assert await _deleted(c, "plain") and not await _deleted(c, "brief")
+            await nlc.taint_manager.process_once(now=start + 31)
+            assert await _deleted(c, "brief")
+    run(go(), 120)
+
+
+def get_cond(lc, name):
+    for n in lc.controllers.nodes.list():
+        if m.name_of(n) == name:
+            return n["status"]["conditions"][0].get("lastHeartbeatTime")
+
+
+async def _count(lc, k):
+    return len(lc.controllers.nodes.list()) >= k
+
+
+async def _pods(lc, k):
+    return len([p for p in lc.controllers.pods.list() if (p.get("status") or {}).get("conditions")]) >= k
+
+
+async def _pods_named(lc, name):
+    return any(m.name_of(p) == name for p in lc.controllers.pods.list())
+
+
+async def _tainted(lc, name):
+    return any(m.name_of(n) == name and (n.get("spec") or {}).get("taints") for n in lc.controllers.nodes.list())
+
+
+async def _deleted(c, name):
+    p = await c.get_or_none("pods", name, "default")
+    return p is None or bool(p["metadata"].get("deletionTimestamp"))
