@@ -133,6 +133,10 @@ def validate_containers_extended_resources(containers, names: dict, path: str) -
     return errs
 
 
+# pkg/capabilities: cluster-wide switches the apiserver sets from its flags (--allow-privileged)
+CAPABILITIES = {"allow_privileged": True}
+
+
 def _validate_container(c: dict, path: str, init: bool) -> list[str]:
     errs = []
     name = c.get("name") or ""
@@ -164,6 +168,8 @@ def _validate_container(c: dict, path: str, init: bool) -> list[str]:
         for probe in ("livenessProbe", "readinessProbe"):
             if c.get(probe):
                 errs.append(f"{path}.{probe}: Invalid value: must not be set for init containers")
+    if (c.get("securityContext") or {}).get("privileged") and not CAPABILITIES["allow_privileged"]:
+        errs.append(f"{path}.securityContext.privileged: Forbidden: disallowed by cluster policy")
     return errs
 
 

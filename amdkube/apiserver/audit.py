@@ -82,14 +82,27 @@ def level_for(policy: dict, user: dict, verb: str, group: str, resource: str, su
     return "None", set()
 
 
+def legacy_line(ev: dict) -> str:
+    """--audit-log-format=legacy (plugin/pkg/audit/log/backend.go EventString)."""
+    u = ev.get("user") or {}
+    ref = ev.get("objectRef") or {}
+    resp = ev.get("responseStatus") or {}
+    return (f'{ev.get("stageTimestamp")} AUDIT: id="{ev.get("auditID")}" stage="{ev.get("stage")}" '
+            f'ip="{",".join(ev.get("sourceIPs") or [])}" method="{ev.get("verb")}" user="{u.get("username", "")}" '
+            f'groups="{",".join(u.get("groups") or [])}" as="<self>" asgroups="<lookup>" '
+            f'namespace="{ref.get("namespace", "<none>")}" uri="{ev.get("requestURI")}"'
+            + (f' response="{resp.get("code")}"' if resp else "") + "\n")
+
+
 class LogBackend:
-    def __init__(self, path: str, max_size_mb: int = 0, max_backup: int = 0):
+    def __init__(self, path: str, max_size_mb: int = 0, max_backup: int = 0, fmt: str = "json", max_age_days: int = 0):
         self.path, self.max_bytes, self.max_backup = path, max_size_mb * (1 << 20), max_backup
+        self.fmt, self.max_age = fmt, max_age_days * 86400
         self.f = None if path == "-" else open(path, "a", buffering=1)
         self.events = 0
 
     def write(self, ev: dict):
-        line = json.dumps(ev, separators=(",", ":")) + "\n"
+        line = legacy_line(ev) if self.fmt == "legacy" else json.dumps(ev, separators=(",", ":")) + "\n"
         self.events += 1
         if self.f is None:
             import sys
@@ -103,17 +116,97 @@ class LogBackend:
         self.f.close()
         stamp = time.strftime("%Y-%m-%dT%H-%M-%S", time.gmtime())
         os.replace(self.path, f"{self.path}-{stamp}.{time.time_ns() % 1000000:06d}")
+        base = os.path.basename(self.path) + "-"
+        d = os.path.dirname(os.path.abspath(self.path))
+        olds = sorted(f for f in os.listdir(d) if f.startswith(base))
         if self.max_backup:
-            base = os.path.basename(self.path) + "-"
-            d = os.path.dirname(os.path.abspath(self.path))
-            olds = sorted(f for f in os.listdir(d) if f.startswith(base))
             for f in olds[:-self.max_backup]:
                 os.unlink(os.path.join(d, f))
+        if self.max_age:            # --audit-log-maxage (days)
+            for f in olds:
+                fp = os.path.join(d, f)
+                try:
+                    if time.time() - os.path.getmtime(fp) > self.max_age:
+                        os.unlink(fp)
+                except OSError:
+                    pass
         self.f = open(self.path, "a", buffering=1)
 
     def close(self):
         if self.f is not None:
             self.f.close()
+
+
+class WebhookBackend:
+    """--audit-webhook-config-file (plugin/pkg/audit/webhook): events POSTed as an
+    audit.k8s.io EventList to the service a kubeconfig names. mode "batch" (default) buffers
+    up to --audit-webhook-batch-max-size events or --audit-webhook-batch-max-wait seconds per
+    request, dropping events beyond --audit-webhook-batch-buffer-size; "blocking" sends each
+    event before the request continues (here: as soon as the event loop allows)."""
+
+    def __init__(self, kubeconfig_path: str, mode: str = "batch", buffer_size: int = 10000, max_size: int = 400,
+                 max_wait: float = 30.0, throttle_qps: float = 10.0, throttle_burst: int = 15):
+        import asyncio
+        from ..client import Client
+        from ..client.rest import TokenBucket
+        self.client = Client.from_kubeconfig(kubeconfig_path, timeout=30.0)
+        self.mode, self.max_size, self.max_wait = mode, max_size, max_wait
+        self.queue: asyncio.Queue = asyncio.Queue(maxsize=buffer_size)
+        self.limiter = TokenBucket(throttle_qps, throttle_burst) if throttle_qps else None
+        self.sent = self.dropped = 0
+        self._task = None
+
+    def write(self, ev: dict):
+        import asyncio
+        if self._task is None:
+            self._task = asyncio.get_running_loop().create_task(self._run())
+        try:
+            self.queue.put_nowait(ev)
+        except asyncio.QueueFull:
+            self.dropped += 1
+
+    async def _send(self, items):
+        if self.limiter is not None:
+            await self.limiter.wait()
+        try:
+            await self.client.request("POST", "", body={"kind": "EventList", "apiVersion": "audit.k8s.io/v1beta1",
+                                                        "items": items})
+            self.sent += len(items)
+        except Exception:     # audit is best effort; a webhook outage must not stall the apiserver
+            self.dropped += len(items)
+
+    async def _run(self):
+        import asyncio
+        while True:
+            items = [await self.queue.get()]
+            if self.mode != "blocking":
+                end = asyncio.get_running_loop().time() + self.max_wait
+                while len(items) < self.max_size:
+                    left = end - asyncio.get_running_loop().time()
+                    if left <= 0:
+                        break
+                    try:
+                        items.append(await asyncio.wait_for(self.queue.get(), left))
+                    except asyncio.TimeoutError:
+                        break
+            await self._send(items)
+
+    def close(self):
+        if self._task is not None:
+            self._task.cancel()
+
+
+class MultiBackend:
+    def __init__(self, backends):
+        self.backends = backends
+
+    def write(self, ev: dict):
+        for b in self.backends:
+            b.write(ev)
+
+    def close(self):
+        for b in self.backends:
+            b.close()
 
 
 class Auditor:

@@ -87,11 +87,33 @@ class Authenticator:
         self.anonymous, self.bootstrap = anonymous, bootstrap_tokens
 
     user_tokens = None   # token-file entries besides the loopback token (None: count them all)
+    basic = None         # authx.BasicAuthenticator (--basic-auth-file)
+    oidc = None          # authx.OIDCAuthenticator (--oidc-*)
+    webhook = None       # authx.WebhookTokenAuthenticator (--authentication-token-webhook-config-file)
 
     @property
     def secured(self) -> bool:
         n = len(self.tokens) if self.user_tokens is None else self.user_tokens
-        return n > 0 or self.sa_key is not None
+        return n > 0 or self.sa_key is not None or any(x is not None for x in (self.basic, self.oidc, self.webhook))
+
+    async def authenticate_token_async(self, tok: str) -> dict | None:
+        """Local token authenticators first, then OIDC (tokens from its issuer), then the webhook."""
+        u = self.authenticate_token(tok)
+        if u is None and self.oidc is not None and self.oidc.claims_issuer(tok):
+            u = await self.oidc.authenticate(tok)
+        if u is None and self.webhook is not None:
+            u = await self.webhook.authenticate(tok)
+        return self._with_authenticated(u) if u is not None else None
+
+    async def authenticate_async(self, headers, peercert: dict | None = None) -> dict:
+        h = headers.get("Authorization", "")
+        if h.startswith("Bearer ") and (self.oidc is not None or self.webhook is not None) and \
+                self._from_request_headers(headers, peercert) is None:
+            u = await self.authenticate_token_async(h[7:].strip())
+            if u is None:
+                raise m.unauthorized()
+            return u
+        return self.authenticate(headers, peercert)
 
     def authenticate_token(self, tok: str) -> dict | None:
         u = self.tokens.get(tok)
@@ -181,6 +203,8 @@ class Authenticator:
         if u is not None:
             return self._with_authenticated(u)
         h = headers.get("Authorization", "")
+        if self.basic is not None and h.startswith("Basic "):
+            return self._with_authenticated(self.basic.authenticate(h))
         if h.startswith("Bearer "):
             u = self.authenticate_token(h[7:].strip())
             if u is None:
@@ -352,9 +376,21 @@ class RBACLite:
 
 
 class UnionAuthorizer:
-    def __init__(self, modes: str, registry):
+    def __init__(self, modes: str, registry, policy_file: str | None = None, webhook_config: str | None = None,
+                 webhook_authorized_ttl: float = 300.0, webhook_unauthorized_ttl: float = 30.0):
+        def abac():
+            from .authx import ABACAuthorizer
+            if not policy_file:
+                raise ValueError("authorization mode ABAC needs --authorization-policy-file")
+            return ABACAuthorizer(policy_file)
+
+        def webhook():
+            from .authx import WebhookAuthorizer
+            if not webhook_config:
+                raise ValueError("authorization mode Webhook needs --authorization-webhook-config-file")
+            return WebhookAuthorizer(webhook_config, webhook_authorized_ttl, webhook_unauthorized_ttl)
         table = {"AlwaysAllow": lambda: AlwaysAllow(), "AlwaysDeny": lambda: AlwaysDeny(), "RBAC": lambda: RBACAuthorizer(registry),
-                 "Node": lambda: NodeAuthorizer(registry), "RBACLite": lambda: RBACLite()}
+                 "Node": lambda: NodeAuthorizer(registry), "RBACLite": lambda: RBACLite(), "ABAC": abac, "Webhook": webhook}
         self.authorizers = []
         for mode in [x.strip() for x in modes.split(",") if x.strip()]:
             if mode not in table:
@@ -367,6 +403,17 @@ class UnionAuthorizer:
             return True, "system:masters"
         for z in self.authorizers:
             ok, why = z.authorize(a)
+            if ok:
+                return True, why
+        return False, ""
+
+    async def authorize_async(self, a: Attributes) -> tuple[bool, str]:
+        """The request path: authorizers that ask a remote service (Webhook) are awaited."""
+        if "system:masters" in (a.user.get("groups") or []):
+            return True, "system:masters"
+        for z in self.authorizers:
+            fn = getattr(z, "authorize_async", None)
+            ok, why = (await fn(a)) if fn is not None else z.authorize(a)
             if ok:
                 return True, why
         return False, ""

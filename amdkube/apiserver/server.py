@@ -99,8 +99,10 @@ class APIServer:
                  kubelet_client_certificate: str | None = None, kubelet_client_key: str | None = None,
                  kubelet_certificate_authority: str | None = None, requestheader_client_ca_file: str | None = None,
                  requestheader_allowed_names=(), proxy_client_cert_file: str | None = None,
-                 proxy_client_key_file: str | None = None):
+                 proxy_client_key_file: str | None = None, options: dict | None = None):
+        """`options`: the rest of kube-apiserver's flags (see _apply_options)."""
         self.store = store or MVCCStore()
+        self.opts = dict(options or {})
         # --kubelet-https / --kubelet-client-certificate / --kubelet-client-key /
         # --kubelet-certificate-authority: how the apiserver reaches kubelets (logs, exec, proxy)
         self.kubelet_scheme = "https" if kubelet_https else "http"
@@ -121,10 +123,21 @@ class APIServer:
         self.crds = CRDManager(self.registry)
         self.webhooks = WebhookDispatcher(self.registry)
         self.auditor = None
-        if audit_log_path:
-            from .audit import Auditor, LogBackend, load_policy
-            self.auditor = Auditor(load_policy(audit_policy_file), LogBackend(audit_log_path, audit_log_maxsize,
-                                                                               audit_log_maxbackup))
+        o = self.opts
+        if audit_log_path or o.get("audit_webhook_config_file"):
+            from .audit import Auditor, LogBackend, MultiBackend, WebhookBackend, load_policy
+            backends = []
+            if audit_log_path:
+                backends.append(LogBackend(audit_log_path, audit_log_maxsize, audit_log_maxbackup,
+                                           o.get("audit_log_format") or "json", int(o.get("audit_log_maxage") or 0)))
+            if o.get("audit_webhook_config_file"):
+                backends.append(WebhookBackend(o["audit_webhook_config_file"], o.get("audit_webhook_mode") or "batch",
+                                               int(o.get("audit_webhook_batch_buffer_size") or 10000),
+                                               int(o.get("audit_webhook_batch_max_size") or 400),
+                                               float(o.get("audit_webhook_batch_max_wait") or 30.0),
+                                               float(o.get("audit_webhook_batch_throttle_qps") or 10.0),
+                                               int(o.get("audit_webhook_batch_throttle_burst") or 15)))
+            self.auditor = Auditor(load_policy(audit_policy_file), backends[0] if len(backends) == 1 else MultiBackend(backends))
         self.tokens = dict(token_auth or {})
         # genericapiserver loopback client: the apiserver's own (and in-process components')
         # credential, a random bearer token for system:apiserver in system:masters
@@ -138,15 +151,24 @@ class APIServer:
         self.authn.user_tokens = len(token_auth or {})
         self.requestheader_ca = requestheader_client_ca_file
         if requestheader_client_ca_file:
-            self.authn.configure_requestheader(requestheader_client_ca_file, requestheader_allowed_names)
+            o = self.opts
+            self.authn.configure_requestheader(
+                requestheader_client_ca_file, requestheader_allowed_names,
+                tuple(o.get("requestheader_username_headers") or ("X-Remote-User",)),
+                tuple(o.get("requestheader_group_headers") or ("X-Remote-Group",)),
+                tuple(o.get("requestheader_extra_headers_prefix") or ("X-Remote-Extra-",)))
             if client_ca_file:
                 import ssl
                 self.authn.requestheader["client_ca_same"] = \
                     ssl._ssl._test_decode_cert(client_ca_file).get("subject") == self.authn.requestheader["issuer"]
         # the aggregator's identity towards extension API servers (--proxy-client-cert-file)
         self.proxy_client_cert = (proxy_client_cert_file, proxy_client_key_file) if proxy_client_cert_file else None
-        self.authz = UnionAuthorizer(authorization_mode, self.registry)
+        self.authz = UnionAuthorizer(authorization_mode, self.registry, self.opts.get("authorization_policy_file"),
+                                     self.opts.get("authorization_webhook_config_file"),
+                                     self.opts.get("authorization_webhook_cache_authorized_ttl", 300.0),
+                                     self.opts.get("authorization_webhook_cache_unauthorized_ttl", 30.0))
         self.registry.authorizer = self.authz
+        self._apply_options()
         from .aggregator import Aggregator
         self.aggregator = Aggregator(self)
         self._ro = asyncio.Semaphore(max_in_flight) if max_in_flight else None
@@ -158,7 +180,8 @@ class APIServer:
         self.m_lat = Histogram("apiserver_request_latencies", "Response latency distribution in microseconds for each verb, resource and subresource.",
                                ["verb", "resource", "subresource"], buckets=MICRO_BUCKETS, registry=self.metrics)
         self.watch_count = 0
-        self.app = web.Application(client_max_size=64 * 1024 * 1024)
+        self.app = web.Application(client_max_size=64 * 1024 * 1024,
+                                   middlewares=[self._cors_middleware] if self.opts.get("cors_allowed_origins") else [])
         self.app.router.add_get("/healthz", self.healthz)
         self.app.router.add_get("/healthz/{check}", self.healthz)
         self.app.router.add_get("/version", self.version)
@@ -167,7 +190,11 @@ class APIServer:
         self.app.router.add_get("/swagger.json", self.openapi)
         self.app.router.add_get("/api", self.api_versions)
         self.app.router.add_get("/apis", self.api_groups)
-        profiling.add_routes(self.app)
+        if self.opts.get("profiling", True):
+            profiling.add_routes(self.app)
+        if self.opts.get("enable_logs_handler", True):
+            self.app.router.add_get("/logs", self.logs_handler)
+            self.app.router.add_get("/logs/{path:.*}", self.logs_handler)
         self.app.router.add_route("*", "/api/{tail:.*}", self.dispatch)
         self.app.router.add_route("*", "/apis/{tail:.*}", self.dispatch)
         self._runner = None
@@ -185,6 +212,107 @@ class APIServer:
             ensure_bootstrap_policy(self.registry)
         self.aggregator.autoregister()
 
+    def _apply_options(self):
+        """Authenticators and policies from the remaining flags: --basic-auth-file, --oidc-*,
+        --authentication-token-webhook-config-file, --allow-privileged, --runtime-config,
+        --cors-allowed-origins, --min-request-timeout, --advertise-address,
+        --kubernetes-service-node-port, --insecure-port/--insecure-bind-address, --tls-sni-cert-key."""
+        import re as _re
+        o = self.opts
+        if o.get("basic_auth_file"):
+            from .authx import BasicAuthenticator
+            self.authn.basic = BasicAuthenticator(o["basic_auth_file"])
+        if o.get("oidc_issuer_url"):
+            from .authx import OIDCAuthenticator
+            if not o.get("oidc_client_id"):
+                raise ValueError("--oidc-issuer-url needs --oidc-client-id")
+            self.authn.oidc = OIDCAuthenticator(o["oidc_issuer_url"], o["oidc_client_id"], o.get("oidc_ca_file"),
+                                                o.get("oidc_username_claim") or "sub", o.get("oidc_username_prefix"),
+                                                o.get("oidc_groups_claim"), o.get("oidc_groups_prefix") or "")
+        if o.get("authentication_token_webhook_config_file"):
+            from .authx import WebhookTokenAuthenticator
+            self.authn.webhook = WebhookTokenAuthenticator(o["authentication_token_webhook_config_file"],
+                                                           o.get("authentication_token_webhook_cache_ttl", 120.0))
+        from ..api import validation as _val
+        _val.CAPABILITIES["allow_privileged"] = bool(o.get("allow_privileged", True))
+        # --runtime-config: group/version=true|false, api/all, api/legacy
+        self.disabled_gv: set[tuple[str, str]] = set()
+        gvs = {(ri.group, ri.version) for ri in SCHEME.by_kind.values()}
+        for item in [x.strip() for x in (o.get("runtime_config") or "").split(",") if x.strip()]:
+            key, _, val = item.partition("=")
+            on = val.lower() != "false"
+            if key == "api/all":
+                self.disabled_gv = set() if on else set(gvs)
+                continue
+            if key in ("api/legacy", "api/v1", "v1"):
+                target = {("", "v1")}
+            else:
+                g, _, v = key.partition("/")
+                target = {(g, v)} if v else {x for x in gvs if x[0] == g}
+            self.disabled_gv = (self.disabled_gv - target) if on else (self.disabled_gv | target)
+        self._cors = [_re.compile(x) for x in o.get("cors_allowed_origins") or []]
+        self.min_request_timeout = float(o.get("min_request_timeout", 1800))
+
+    @web.middleware
+    async def _cors_middleware(self, request, handler):
+        """--cors-allowed-origins (filters/cors.go): origins matching one of the regexps."""
+        origin = request.headers.get("Origin")
+        allowed = origin and any(r.search(origin) for r in self._cors)
+        if request.method == "OPTIONS" and allowed:
+            resp = web.Response(status=204)
+        else:
+            resp = await handler(request)
+        if allowed:
+            resp.headers.update({"Access-Control-Allow-Origin": origin, "Access-Control-Allow-Credentials": "true",
+                                 "Access-Control-Allow-Methods": "POST, GET, OPTIONS, PUT, DELETE, PATCH",
+                                 "Access-Control-Allow-Headers": "Content-Type, Content-Length, Accept-Encoding, "
+                                                                 "X-CSRF-Token, Authorization, X-Requested-With, If-Modified-Since",
+                                 "Access-Control-Expose-Headers": "Date"})
+        return resp
+
+    async def logs_handler(self, request):
+        """/logs/ (routes/logs.go): the node's /var/log for cluster admins (--enable-logs-handler)."""
+        import os as _os
+        user = await self._authenticate_async(request)
+        ok, _ = await self.authz.authorize_async(Attributes(user, "get", path=request.path, resource_request=False))
+        if not ok:
+            return _err(m.forbidden(f'User "{user.get("name")}" cannot get path "{request.path}"'))
+        root = _os.path.realpath(self.opts.get("logs_dir") or "/var/log")
+        rel = request.match_info.get("path", "")
+        target = _os.path.realpath(_os.path.join(root, rel))
+        if target != root and not target.startswith(root + _os.sep):
+            return web.Response(status=404)
+        if _os.path.isdir(target):
+            names = sorted(_os.listdir(target))
+            return web.Response(text="".join(f'<a href="{n}">{n}</a>\n' for n in names), content_type="text/html")
+        if not _os.path.isfile(target):
+            return web.Response(status=404)
+        return web.FileResponse(target)
+
+    def _sni_context(self, base_ctx):
+        """--tls-sni-cert-key cert,key[:name1,name2]: a serving certificate per requested server name."""
+        import ssl
+        entries = self.opts.get("tls_sni_cert_key") or []
+        if not entries:
+            return
+        by_name = {}
+        for cert, key, names in entries:
+            ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+            ctx.load_cert_chain(cert, key)
+            if not names:
+                info = ssl._ssl._test_decode_cert(cert)
+                names = [v for t, v in info.get("subjectAltName", ()) if t == "DNS"]
+            for n in names:
+                by_name[n.lower()] = ctx
+
+        def pick(sock, server_name, _ctx):
+            if server_name:
+                name = server_name.lower()
+                ctx = by_name.get(name) or by_name.get("*." + name.split(".", 1)[-1])
+                if ctx is not None:
+                    sock.context = ctx
+        base_ctx.sni_callback = pick
+
     # ---------------------------------------------------------------- lifecycle
     async def start(self, host="127.0.0.1", port=0):
         self._runner = web.AppRunner(self.app, access_log=None, handler_cancellation=True)
@@ -201,10 +329,20 @@ class APIServer:
             if self.requestheader_ca:   # front-proxy certificates are checked against their own CA
                 ctx.load_verify_locations(self.requestheader_ca)
                 ctx.verify_mode = ssl.CERT_OPTIONAL
+        if ctx is not None:
+            self._sni_context(ctx)
         self._site = web.TCPSite(self._runner, host, port, backlog=1024, reuse_address=True, ssl_context=ctx)
         await self._site.start()
         self.port = self._site._server.sockets[0].getsockname()[1]
         self.host = host
+        # --insecure-port next to the secure one: no authentication, no authorization (the
+        # reference's localhost port), for local tooling only
+        self.insecure_port = None
+        if ctx is not None and self.opts.get("insecure_port"):
+            ins = web.TCPSite(self._runner, self.opts.get("insecure_bind_address") or "127.0.0.1", self.opts["insecure_port"],
+                              reuse_address=True)
+            await ins.start()
+            self.insecure_port = ins._server.sockets[0].getsockname()[1]
         self._bg.append(asyncio.create_task(self._event_gc()))
         self._bg.append(asyncio.create_task(self.aggregator.run_availability(), name="apiservice-availability"))
         self.crds.start()
@@ -222,13 +360,16 @@ class APIServer:
                                                                     "labels": {"component": "apiserver", "provider": "kubernetes"}},
                "spec": {"clusterIP": first, "ports": [{"name": "https", "port": 443, "protocol": "TCP", "targetPort": self.port}],
                         "sessionAffinity": "ClientIP"}}
+        if self.opts.get("kubernetes_service_node_port"):    # --kubernetes-service-node-port
+            svc["spec"]["type"] = "NodePort"
+            svc["spec"]["ports"][0]["nodePort"] = int(self.opts["kubernetes_service_node_port"])
         rs = self.registry.rs("services")
         try:
             if rs.storage.get(rs.key("default", "kubernetes"), ignore_not_found=True) is None:
                 rs.create("default", svc)
         except m.StatusError as e:
             log.warning("cannot create the kubernetes service: %s", e)
-        ip = self.host if self.host not in ("0.0.0.0", "", "::") else "127.0.0.1"
+        ip = self.opts.get("advertise_address") or (self.host if self.host not in ("0.0.0.0", "", "::") else "127.0.0.1")
         ep = {"apiVersion": "v1", "kind": "Endpoints", "metadata": {"name": "kubernetes", "namespace": "default"},
               "subsets": [{"addresses": [{"ip": ip}], "ports": [{"name": "https", "port": self.port, "protocol": "TCP"}]}]}
         ers = self.registry.rs("endpoints")
@@ -294,16 +435,19 @@ class APIServer:
                       "serverAddressByClientCIDRs": [{"clientCIDR": "0.0.0.0/0", "serverAddress": request.host}]})
 
     @staticmethod
-    def _group_doc(g: str) -> dict:
+    def _group_doc(g: str, disabled=()) -> dict:
         from ..api.scheme import _version_sort
-        vs = _version_sort(ri.version for ri in SCHEME.by_kind.values() if ri.group == g)
+        vs = _version_sort(ri.version for ri in SCHEME.by_kind.values() if ri.group == g and (g, ri.version) not in disabled)
         pv = SCHEME.preferred_version(g)
+        if vs and pv not in vs:
+            pv = vs[0]
         return {"name": g, "versions": [{"groupVersion": f"{g}/{v}", "version": v} for v in vs],
                 "preferredVersion": {"groupVersion": f"{g}/{pv}", "version": pv}}
 
     async def api_groups(self, request):
         groups = sorted({ri.group for ri in SCHEME.by_kind.values() if ri.group})
-        docs = [self._group_doc(g) for g in groups] + self.aggregator.group_docs(set(groups))
+        docs = [d for d in (self._group_doc(g, self.disabled_gv) for g in groups) if d["versions"]] + \
+            self.aggregator.group_docs(set(groups))
         return _resp({"kind": "APIGroupList", "apiVersion": "v1", "groups": docs})
 
     def _resource_list(self, group, version):
@@ -323,8 +467,18 @@ class APIServer:
         pc = request.transport.get_extra_info("peercert") if self.tls and request.transport is not None else None
         return self.authn.authenticate(request.headers, pc)
 
-    def _authorize(self, user, verb, resource, group="", ns="", name="", sub=""):
-        ok, _ = self.authz.authorize(Attributes(user, verb, group, resource, sub, ns, name))
+    UNSECURED = {"name": "system:unsecured", "uid": "", "groups": ["system:masters", "system:authenticated"]}
+
+    async def _authenticate_async(self, request):
+        tr = request.transport
+        if getattr(self, "insecure_port", None) and tr is not None and \
+                (tr.get_extra_info("sockname") or (None, None))[1] == self.insecure_port:
+            return self.UNSECURED
+        pc = tr.get_extra_info("peercert") if self.tls and tr is not None else None
+        return await self.authn.authenticate_async(request.headers, pc)
+
+    async def _authorize(self, user, verb, resource, group="", ns="", name="", sub=""):
+        ok, _ = await self.authz.authorize_async(Attributes(user, verb, group, resource, sub, ns, name))
         if not ok:
             what = f"{resource}/{sub}" if sub else resource
             where = f' in the namespace "{ns}"' if ns else " at the cluster scope"
@@ -346,11 +500,11 @@ class APIServer:
                            content_type="application/merge-patch+json")
         return _to_scale(obj)
 
-    def _review(self, plural, body, requester=None, ns=""):
+    async def _review(self, plural, body, requester=None, ns=""):
         """SubjectAccessReview / TokenReview (authorization.k8s.io, authentication.k8s.io): computed, not stored."""
         spec = body.get("spec") or {}
         if plural == "tokenreviews":
-            u = self.authn.authenticate_token(spec.get("token", "")) if spec.get("token") else None
+            u = await self.authn.authenticate_token_async(spec.get("token", "")) if spec.get("token") else None
             st = {"authenticated": u is not None}
             if u is not None:
                 st["user"] = {"username": u.get("name"), "uid": u.get("uid", ""), "groups": u.get("groups") or []}
@@ -367,7 +521,7 @@ class APIServer:
                                ra.get("namespace", ""), ra.get("name", ""))
             else:
                 a = Attributes(user, (nra or {}).get("verb", ""), path=(nra or {}).get("path", ""), resource_request=False)
-            ok, why = self.authz.authorize(a)
+            ok, why = await self.authz.authorize_async(a)
             st = {"allowed": ok, "reason": why}
         return dict(body, status=st)
 
@@ -404,8 +558,10 @@ class APIServer:
         verb, resource, sub, code = request.method, "", "", 500
         sem = actx = resp = None
         try:
-            user = self._authenticate(request)
+            user = await self._authenticate_async(request)
             group, version, resource, ns, name, sub, watch = self._parse(request.path)
+            if (group, version) in self.disabled_gv:       # --runtime-config turned this group/version off
+                raise m.not_found("path", request.path)
             target = self.aggregator.route(group, version) if request.path.startswith("/apis/") else None
             if target is not None:      # an extension API server's group/version (kube-aggregator proxy)
                 resource = resource or ""
@@ -421,7 +577,7 @@ class APIServer:
                             return _resp({"kind": "APIGroup", "apiVersion": "v1", **agg[0]})
                         raise m.not_found("group", group)
                     code = 200
-                    return _resp({"kind": "APIGroup", "apiVersion": "v1", **self._group_doc(group)})
+                    return _resp({"kind": "APIGroup", "apiVersion": "v1", **self._group_doc(group, self.disabled_gv)})
                 code = 200
                 return _resp(self._resource_list(group, version))
             served = SCHEME.served(group, version, resource)
@@ -439,7 +595,7 @@ class APIServer:
             verb = kverb.upper()
             if self.auditor is not None:
                 actx = self.auditor.begin(request, user, kverb, group, version, resource, sub, ns, name or "")
-            self._authorize(user, kverb, resource, group, "" if not rs.ri.namespaced else ns, name or "", top_sub)
+            await self._authorize(user, kverb, resource, group, "" if not rs.ri.namespaced else ns, name or "", top_sub)
             if is_watch:
                 code = 200
                 if actx is not None:
@@ -528,7 +684,7 @@ class APIServer:
                           content_type="application/merge-patch+json")
                 return _resp(m.success_status({"name": name, "kind": "deployments"}), 201)
             if ri.plural in ("subjectaccessreviews", "selfsubjectaccessreviews", "localsubjectaccessreviews", "tokenreviews"):
-                return _resp(self._review(ri.plural, body, user, ns), 201)
+                return _resp(await self._review(ri.plural, body, user, ns), 201)
             if ri.plural == "pods" and sub == "" and name is None and body.get("kind") == "Binding":
                 return _resp(self.registry.bind(ns, body, user), 201)
             if name:
@@ -675,7 +831,8 @@ class APIServer:
         ls, fs = q.get("labelSelector"), q.get("fieldSelector")
         if name:
             fs = f"metadata.name={name}" + (f",{fs}" if fs else "")
-        timeout = float(q.get("timeoutSeconds") or (1800 + random.random() * 1800))
+        mrt = getattr(self, "min_request_timeout", 1800.0)     # --min-request-timeout: watches end in [min, 2·min)
+        timeout = float(q.get("timeoutSeconds") or (mrt + random.random() * mrt))
         initial = []
         if rv in ("", "0"):
             items, list_rev, _ = rs.list(ns, ls, fs)

@@ -99,7 +99,11 @@ def _run_forever(coro_factory):
 def apiserver(argv):
     ap = argparse.ArgumentParser("amdkube apiserver")
     ap.add_argument("--bind-address", default="127.0.0.1")
-    ap.add_argument("--port", "--insecure-port", type=int, default=8080)
+    ap.add_argument("--port", type=int, default=8080, help="the main listener (TLS when certificates are given)")
+    ap.add_argument("--secure-port", type=int, default=None, help="TLS listener (with --tls-cert-file)")
+    ap.add_argument("--insecure-port", type=int, default=None,
+                    help="unauthenticated listener next to --secure-port (alone: the main listener)")
+    ap.add_argument("--insecure-bind-address", default="127.0.0.1")
     ap.add_argument("--data-dir", default=None, help="MVCC store WAL/snapshot directory (etcd replacement)")
     ap.add_argument("--admission-control", default=None, help="ordered, comma-separated admission plugins")
     ap.add_argument("--resource-v2-resources", default="amd.com/gpu", help="container limits ResourceV2 converts")
@@ -129,8 +133,90 @@ def apiserver(argv):
     ap.add_argument("--requestheader-allowed-names", default="", help="front-proxy cert CNs accepted (empty: any)")
     ap.add_argument("--proxy-client-cert-file", default=None, help="aggregator's client cert towards extension apiservers")
     ap.add_argument("--proxy-client-key-file", default=None)
+    tf = lambda v: str(v).lower() in ("true", "1", "yes")   # noqa: E731
+    lst = lambda v: [x.strip() for x in v.split(",") if x.strip()]   # noqa: E731
+    ap.add_argument("--requestheader-username-headers", type=lst, default=["X-Remote-User"])
+    ap.add_argument("--requestheader-group-headers", type=lst, default=["X-Remote-Group"])
+    ap.add_argument("--requestheader-extra-headers-prefix", type=lst, default=["X-Remote-Extra-"])
+    ap.add_argument("--basic-auth-file", default=None)
+    ap.add_argument("--oidc-issuer-url", default=None)
+    ap.add_argument("--oidc-client-id", default=None)
+    ap.add_argument("--oidc-ca-file", default=None)
+    ap.add_argument("--oidc-username-claim", default="sub")
+    ap.add_argument("--oidc-username-prefix", default=None)
+    ap.add_argument("--oidc-groups-claim", default=None)
+    ap.add_argument("--oidc-groups-prefix", default="")
+    ap.add_argument("--authentication-token-webhook-config-file", default=None)
+    ap.add_argument("--authentication-token-webhook-cache-ttl", type=float, default=120.0, help="seconds")
+    ap.add_argument("--authorization-policy-file", default=None, help="ABAC policy (one JSON Policy per line)")
+    ap.add_argument("--authorization-webhook-config-file", default=None)
+    ap.add_argument("--authorization-webhook-cache-authorized-ttl", type=float, default=300.0, help="seconds")
+    ap.add_argument("--authorization-webhook-cache-unauthorized-ttl", type=float, default=30.0, help="seconds")
+    ap.add_argument("--experimental-encryption-provider-config", default=None, help="EncryptionConfig file")
+    ap.add_argument("--audit-log-format", default="json", choices=("json", "legacy"))
+    ap.add_argument("--audit-log-maxage", type=int, default=0, help="days to keep rotated audit logs")
+    ap.add_argument("--audit-webhook-config-file", default=None)
+    ap.add_argument("--audit-webhook-mode", default="batch", choices=("batch", "blocking"))
+    ap.add_argument("--audit-webhook-batch-buffer-size", type=int, default=10000)
+    ap.add_argument("--audit-webhook-batch-max-size", type=int, default=400)
+    ap.add_argument("--audit-webhook-batch-max-wait", type=float, default=30.0)
+    ap.add_argument("--audit-webhook-batch-throttle-qps", type=float, default=10.0)
+    ap.add_argument("--audit-webhook-batch-throttle-burst", type=int, default=15)
+    ap.add_argument("--advertise-address", default=None)
+    ap.add_argument("--kubernetes-service-node-port", type=int, default=0)
+    ap.add_argument("--allow-privileged", type=tf, default=True)
+    ap.add_argument("--runtime-config", default="", help="group/version=true|false, api/all=false, ...")
+    ap.add_argument("--cors-allowed-origins", type=lst, default=[])
+    ap.add_argument("--enable-logs-handler", type=tf, default=True)
+    ap.add_argument("--profiling", type=tf, default=True)
+    ap.add_argument("--min-request-timeout", type=float, default=1800.0, help="seconds (watch duration floor)")
+    ap.add_argument("--tls-sni-cert-key", action="append", default=[], help="cert,key[:name1,name2] (repeatable)")
+    ap.add_argument("--feature-gates", default="")
+    # accepted for command-line compatibility: etcd and watch-cache tuning of a store this
+    # apiserver embeds, SSH tunnels and other knobs with no counterpart here
+    for flag in ("--etcd-servers", "--etcd-servers-overrides", "--etcd-cafile", "--etcd-certfile", "--etcd-keyfile",
+                 "--etcd-prefix", "--etcd-quorum-read", "--etcd-compaction-interval", "--storage-backend",
+                 "--storage-media-type", "--storage-versions", "--watch-cache", "--watch-cache-sizes",
+                 "--default-watch-cache-size", "--deserialization-cache-size", "--target-ram-mb", "--apiserver-count",
+                 "--endpoint-reconciler-type", "--ssh-user", "--ssh-keyfile", "--cert-dir", "--external-hostname",
+                 "--public-address-override", "--kubelet-preferred-address-types", "--kubelet-timeout",
+                 "--kubelet-read-only-port", "--kubelet-port", "--max-connection-bytes-per-sec",
+                 "--http2-max-streams-per-connection", "--repair-malformed-updates", "--delete-collection-workers",
+                 "--enable-garbage-collector", "--enable-aggregator-routing", "--enable-swagger-ui", "--contention-profiling",
+                 "--master-service-namespace", "--request-timeout", "--tls-ca-file", "--kubeconfig",
+                 "--authentication-kubeconfig", "--authorization-kubeconfig", "--authentication-skip-lookup",
+                 "--admission-control-config-file", "--enable-bootstrap-token-auth", "--service-account-lookup",
+                 "--tls-cipher-suites", "--tls-min-version", "--log-flush-frequency", "--requestheader-extra-headers"):
+        ap.add_argument(flag, default=None, help=argparse.SUPPRESS)
     a = ap.parse_args(argv)
     klog.setup(a.v, "apiserver")
+    sni = []
+    for item in a.tls_sni_cert_key:
+        files, _, names = item.partition(":")
+        cert, _, key = files.partition(",")
+        sni.append((cert, key, [x for x in names.split(",") if x]))
+    transformer = None
+    if a.experimental_encryption_provider_config:
+        from ..apiserver.encryption import load as load_encryption
+        transformer = load_encryption(a.experimental_encryption_provider_config)
+    options = {k: getattr(a, k) for k in (
+        "requestheader_username_headers", "requestheader_group_headers", "requestheader_extra_headers_prefix",
+        "basic_auth_file", "oidc_issuer_url", "oidc_client_id", "oidc_ca_file", "oidc_username_claim",
+        "oidc_username_prefix", "oidc_groups_claim", "oidc_groups_prefix", "authentication_token_webhook_config_file",
+        "authentication_token_webhook_cache_ttl", "authorization_policy_file", "authorization_webhook_config_file",
+        "authorization_webhook_cache_authorized_ttl", "authorization_webhook_cache_unauthorized_ttl",
+        "audit_log_format", "audit_log_maxage", "audit_webhook_config_file", "audit_webhook_mode",
+        "audit_webhook_batch_buffer_size", "audit_webhook_batch_max_size", "audit_webhook_batch_max_wait",
+        "audit_webhook_batch_throttle_qps", "audit_webhook_batch_throttle_burst", "advertise_address",
+        "kubernetes_service_node_port", "allow_privileged", "runtime_config", "cors_allowed_origins",
+        "enable_logs_handler", "profiling", "min_request_timeout")}
+    options["tls_sni_cert_key"] = sni
+    main_port = a.port
+    if a.secure_port is not None and a.tls_cert_file:
+        main_port = a.secure_port
+        options.update(insecure_port=a.insecure_port, insecure_bind_address=a.insecure_bind_address)
+    elif a.insecure_port is not None:
+        main_port = a.insecure_port
     from ..apiserver import APIServer
     from ..apiserver.admission import DEFAULT_CHAIN
     from ..store import MVCCStore
@@ -143,7 +229,7 @@ def apiserver(argv):
                                     "groups": parts[3].split(",") if len(parts) > 3 else []}
 
     async def mk():
-        srv = APIServer(MVCCStore(a.data_dir), admission_plugins=(a.admission_control.split(",") if a.admission_control else DEFAULT_CHAIN),
+        srv = APIServer(MVCCStore(a.data_dir, transformer=transformer), admission_plugins=(a.admission_control.split(",") if a.admission_control else DEFAULT_CHAIN),
                         admission_config={"ResourceV2": {"resource_names": tuple(a.resource_v2_resources.split(","))}},
                         token_auth=tokens, authorization_mode=a.authorization_mode, anonymous_auth=a.anonymous_auth == "true",
                         max_in_flight=a.max_requests_inflight, max_mutating_in_flight=a.max_mutating_requests_inflight,
@@ -157,8 +243,9 @@ def apiserver(argv):
                         kubelet_client_key=a.kubelet_client_key, kubelet_certificate_authority=a.kubelet_certificate_authority,
                         requestheader_client_ca_file=a.requestheader_client_ca_file,
                         requestheader_allowed_names=[x for x in a.requestheader_allowed_names.split(",") if x],
-                        proxy_client_cert_file=a.proxy_client_cert_file, proxy_client_key_file=a.proxy_client_key_file)
-        return await srv.start(a.bind_address, a.port)
+                        proxy_client_cert_file=a.proxy_client_cert_file, proxy_client_key_file=a.proxy_client_key_file,
+                        options=options)
+        return await srv.start(a.bind_address, main_port)
     _run_forever(mk)
 
 

@@ -148,7 +148,7 @@ class Watcher:
 
 class MVCCStore:
     def __init__(self, data_dir: str | None = None, history: int = 200_000, max_queue: int = 500_000,
-                 snapshot_every: int = 50_000, fsync: bool = False):
+                 snapshot_every: int = 50_000, fsync: bool = False, transformer=None):
         self.kv: dict[str, KV] = {}
         # keys bucketed by their first two path components ("/registry/pods/"), so a range over one
         # resource never scans the others (admission lists quotas/limitranges on every create)
@@ -171,6 +171,9 @@ class MVCCStore:
         self._wal = None
         self._since_snapshot = 0
         self.commit_hooks = []  # fn(Event) called synchronously on commit (apiserver indexes)
+        # value transformer between memory and disk (encryption at rest): to_disk(key, bytes),
+        # from_disk(key, bytes); None keeps the bytes as they are
+        self.transformer = transformer
         if data_dir:
             os.makedirs(data_dir, exist_ok=True)
             self._recover()
@@ -250,7 +253,7 @@ class MVCCStore:
             self.rev = rev
             self.kv[key] = new
             self._index_put(key, new)
-            self._commit(Event(PUT, new, cur, rev), {"r": rev, "o": "p", "k": key, "v": _b(data)})
+            self._commit(Event(PUT, new, cur, rev), {"r": rev, "o": "p", "k": key, "v": data} if self._wal is not None else None)
             return new
 
     def delete(self, key: str, expect_mod_rev: int | None = None) -> KV:
@@ -268,8 +271,17 @@ class MVCCStore:
             self._commit(Event(DELETE, tomb, cur, rev), {"r": rev, "o": "d", "k": key})
             return cur
 
-    def _commit(self, ev: Event, rec: dict):
-        if self._wal is not None:
+    def _disk(self, key: str, data: bytes) -> str:
+        return _b(self.transformer.to_disk(key, data) if self.transformer is not None else data)
+
+    def _undisk(self, key: str, s: str) -> bytes:
+        data = _unb(s)
+        return self.transformer.from_disk(key, data) if self.transformer is not None else data
+
+    def _commit(self, ev: Event, rec: dict | None):
+        if self._wal is not None and rec is not None:
+            if "v" in rec:
+                rec["v"] = self._disk(rec["k"], rec["v"])
             self._wal.write((json.dumps(rec, separators=(",", ":")) + "\n").encode())
             if self.fsync:
                 os.fsync(self._wal.fileno())
@@ -359,7 +371,8 @@ class MVCCStore:
         tmp = path + ".tmp"
         with open(tmp, "w") as f:
             json.dump({"rev": self.rev, "compact_rev": self.compact_rev,
-                       "kv": [[k.key, _b(k.value), k.create_rev, k.mod_rev, k.version] for k in self.kv.values()]}, f)
+                       "kv": [[k.key, self._disk(k.key, k.value), k.create_rev, k.mod_rev, k.version]
+                              for k in self.kv.values()]}, f)
             f.flush()
             os.fsync(f.fileno())
         os.replace(tmp, path)
@@ -376,7 +389,7 @@ class MVCCStore:
             self.rev = s["rev"]
             self.compact_rev = s["rev"]
             for key, v, cr, mr, ver in s["kv"]:
-                self.kv[key] = KV(key, _unb(v), cr, mr, ver)
+                self.kv[key] = KV(key, self._undisk(key, v), cr, mr, ver)
         wal = os.path.join(self.data_dir, "wal.log")
         if os.path.exists(wal):
             with open(wal, "rb") as f:
@@ -391,7 +404,7 @@ class MVCCStore:
                     key = rec["k"]
                     cur = self.kv.get(key)
                     if rec["o"] == "p":
-                        self.kv[key] = KV(key, _unb(rec["v"]), cur.create_rev if cur else r, r,
+                        self.kv[key] = KV(key, self._undisk(key, rec["v"]), cur.create_rev if cur else r, r,
                                           (cur.version + 1) if cur else 1)
                     else:
                         self.kv.pop(key, None)
