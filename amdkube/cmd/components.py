@@ -15,6 +15,7 @@ import logging
 import os
 import signal
 import socket
+import shutil
 import subprocess
 import sys
 import time
@@ -262,15 +263,61 @@ def scheduler(argv):
     ap.add_argument("--feature-gates", default="")
     ap.add_argument("--kube-api-qps", type=float, default=0)
     ap.add_argument("--disable-preemption", action="store_true")
+    ap.add_argument("--config", default=None, help="KubeSchedulerConfiguration file (overrides the flags it sets)")
+    ap.add_argument("--address", default="127.0.0.1", help="healthz/metrics listener address")
+    ap.add_argument("--policy-configmap", default=None, help="ConfigMap whose policy.cfg holds the Policy")
+    ap.add_argument("--policy-configmap-namespace", default="kube-system")
+    ap.add_argument("--use-legacy-policy-config", default="false", choices=("true", "false"),
+                    help="true: --policy-config-file only, never --policy-configmap")
+    ap.add_argument("--hard-pod-affinity-symmetric-weight", type=int, default=1)
+    ap.add_argument("--lock-object-name", default="kube-scheduler")
+    ap.add_argument("--lock-object-namespace", default="kube-system")
+    ap.add_argument("--kube-api-burst", type=int, default=0)
+    for flag in ("--kube-api-content-type", "--failure-domains", "--profiling", "--contention-profiling"):
+        ap.add_argument(flag, default=None, help=argparse.SUPPRESS)
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     klog.setup(a.v, "scheduler")
+    if a.config:     # componentconfig KubeSchedulerConfiguration
+        import yaml
+        cfg = yaml.safe_load(open(a.config)) or {}
+        a.scheduler_name = cfg.get("schedulerName", a.scheduler_name)
+        src = cfg.get("algorithmSource") or {}
+        if src.get("provider"):
+            a.algorithm_provider = src["provider"]
+        pol = src.get("policy") or {}
+        if (pol.get("file") or {}).get("path"):
+            a.policy_config_file = pol["file"]["path"]
+        if pol.get("configMap"):
+            a.policy_configmap = pol["configMap"].get("name")
+            a.policy_configmap_namespace = pol["configMap"].get("namespace", a.policy_configmap_namespace)
+        a.hard_pod_affinity_symmetric_weight = int(cfg.get("hardPodAffinitySymmetricWeight", a.hard_pod_affinity_symmetric_weight))
+        le = cfg.get("leaderElection") or {}
+        if "leaderElect" in le:
+            a.leader_elect = "true" if le["leaderElect"] else "false"
+        a.lock_object_name = le.get("lockObjectName", a.lock_object_name)
+        a.lock_object_namespace = le.get("lockObjectNamespace", a.lock_object_namespace)
+        cc = cfg.get("clientConnection") or {}
+        a.kubeconfig = cc.get("kubeconfig") or a.kubeconfig
+        a.kube_api_qps = float(cc.get("qps", a.kube_api_qps))
+        a.kube_api_burst = int(cc.get("burst", a.kube_api_burst))
+        if cfg.get("healthzBindAddress"):
+            host, _, port = cfg["healthzBindAddress"].rpartition(":")
+            a.address, a.port = host or a.address, int(port)
+        a.disable_preemption = bool(cfg.get("disablePreemption", a.disable_preemption))
     from ..client import Client
     from ..scheduler import Scheduler
+    cm = None
+    if a.policy_configmap and a.use_legacy_policy_config != "true" and not a.policy_config_file:
+        cm = (a.policy_configmap_namespace, a.policy_configmap)
 
     async def mk():
-        return await Scheduler(_client(a, qps=a.kube_api_qps), a.scheduler_name, a.policy_config_file, a.algorithm_provider,
-                               a.feature_gates, a.leader_elect == "true", port=a.port, disable_preemption=a.disable_preemption).start()
+        return await Scheduler(_client(a, qps=a.kube_api_qps, burst=a.kube_api_burst), a.scheduler_name,
+                               a.policy_config_file, a.algorithm_provider, a.feature_gates, a.leader_elect == "true",
+                               port=a.port or None, disable_preemption=a.disable_preemption,
+                               hard_pod_affinity_weight=a.hard_pod_affinity_symmetric_weight,
+                               lock_object_name=a.lock_object_name, lock_object_namespace=a.lock_object_namespace,
+                               address=a.address, policy_configmap=cm).start()
     _run_forever(mk)
 
 
@@ -795,16 +842,63 @@ def proxy(argv):
     ap.add_argument("--iptables-min-sync-period", type=float, default=0.0)
     ap.add_argument("--healthz-port", type=int, default=10256)
     ap.add_argument("--iptables-dump-file", default=None, help="write every rendered ruleset here (dry-run inspection)")
+    tf = lambda v: str(v).lower() in ("true", "1", "yes")   # noqa: E731
+    ap.add_argument("--config", default=None, help="KubeProxyConfiguration file (its fields override the flags)")
+    ap.add_argument("--write-config-to", default=None, help="write the effective configuration here and exit")
+    ap.add_argument("--cleanup", "--cleanup-iptables", "--cleanup-ipvs", dest="cleanup", action="store_true",
+                    help="remove the rules this proxy installs and exit")
+    ap.add_argument("--masquerade-all", type=tf, default=False)
+    ap.add_argument("--iptables-masquerade-bit", type=int, default=14)
+    ap.add_argument("--ipvs-sync-period", type=float, default=30.0)
+    ap.add_argument("--ipvs-min-sync-period", type=float, default=0.0)
+    ap.add_argument("--healthz-bind-address", default="127.0.0.1")
+    ap.add_argument("--metrics-bind-address", default="127.0.0.1:10249")
+    ap.add_argument("--hostname-override", default="")
+    ap.add_argument("--oom-score-adj", type=int, default=-999)
+    ap.add_argument("--udp-timeout", type=float, default=0.25, help="userspace UDP idle timeout (s)")
+    ap.add_argument("--conntrack-max-per-core", type=int, default=32768)
+    ap.add_argument("--conntrack-min", type=int, default=131072)
+    ap.add_argument("--conntrack-max", type=int, default=0)
+    ap.add_argument("--conntrack-tcp-timeout-established", type=float, default=86400.0, help="seconds")
+    ap.add_argument("--conntrack-tcp-timeout-close-wait", type=float, default=3600.0, help="seconds")
+    ap.add_argument("--kube-api-qps", type=float, default=5.0)
+    ap.add_argument("--kube-api-burst", type=int, default=10)
+    for flag in ("--kube-api-content-type", "--config-sync-period", "--proxy-port-range", "--resource-container",
+                 "--profiling", "--feature-gates"):
+        ap.add_argument(flag, default=None, help=argparse.SUPPRESS)
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     klog.setup(a.v, "proxy")
-    from ..client import Client
+    from ..proxy import config_file
+    if a.config:
+        config_file.apply(a, config_file.load(a.config))
+    if a.write_config_to:
+        config_file.write(a, a.write_config_to)
+        print(f"Wrote configuration to: {a.write_config_to}")
+        return 0
+    if a.cleanup:       # server.go CleanupAndExit
+        from ..proxy import iptables as ipt
+        rules = ipt.cleanup(dry_run=os.geteuid() != 0)
+        if shutil.which("ipvsadm") and os.geteuid() == 0:
+            subprocess.run(["ipvsadm", "-C"], capture_output=True)
+            subprocess.run(["ip", "link", "del", "kube-ipvs0"], capture_output=True)
+        print(rules, end="")
+        return 0
+    from ..kubelet.node_setup import apply_oom_score_adj
+    apply_oom_score_adj(a.oom_score_adj)
+    config_file.apply_conntrack(a)
     from ..proxy import ProxyServer
+    mhost, _, mport = a.metrics_bind_address.rpartition(":")
+    sync, min_sync = (a.ipvs_sync_period, a.ipvs_min_sync_period) if a.proxy_mode == "ipvs" else \
+        (a.iptables_sync_period, a.iptables_min_sync_period)
 
     async def mk():
-        return await ProxyServer(_client(a), a.proxy_mode, a.bind_address, a.cluster_cidr, a.iptables_sync_period,
-                                 a.iptables_min_sync_period, a.healthz_port, a.iptables_dump_file,
-                                 ipvs_scheduler=a.ipvs_scheduler).start()
+        return await ProxyServer(_client(a, qps=a.kube_api_qps, burst=a.kube_api_burst), a.proxy_mode, a.bind_address,
+                                 a.cluster_cidr, sync, min_sync, a.healthz_port, a.iptables_dump_file,
+                                 ipvs_scheduler=a.ipvs_scheduler, masquerade_all=a.masquerade_all,
+                                 masquerade_bit=a.iptables_masquerade_bit, healthz_address=a.healthz_bind_address,
+                                 udp_idle_timeout=a.udp_timeout, metrics_address=(mhost or "127.0.0.1", int(mport or 0)),
+                                 hostname=a.hostname_override or socket.gethostname()).start()
     _run_forever(mk)
 
 

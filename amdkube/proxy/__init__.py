@@ -28,21 +28,27 @@ log = logging.getLogger("amdkube.proxy")
 class ProxyServer:
     def __init__(self, client: Client, mode: str = "userspace", node_ip: str = "0.0.0.0", cluster_cidr: str = "",
                  sync_period: float = 30.0, min_sync_period: float = 0.0, healthz_port: int | None = None,
-                 iptables_dump: str | None = None, bind_cluster_ips: bool = True, ipvs_scheduler: str = "rr"):
+                 iptables_dump: str | None = None, bind_cluster_ips: bool = True, ipvs_scheduler: str = "rr",
+                 masquerade_all: bool = False, masquerade_bit: int = 14, healthz_address: str = "127.0.0.1",
+                 udp_idle_timeout: float = 0.25, metrics_address: tuple | None = None, hostname: str = ""):
         self.client = client
+        self.hostname = hostname
         if mode == "iptables":
-            self.proxier = IptablesProxier(cluster_cidr, dump_path=iptables_dump)
+            self.proxier = IptablesProxier(cluster_cidr, dump_path=iptables_dump, masquerade_all=masquerade_all,
+                                           masquerade_bit=masquerade_bit)
         elif mode == "ipvs":
             from .ipvs import IPVSProxier
             self.proxier = IPVSProxier(cluster_cidr, ipvs_scheduler, node_ips=[node_ip] if node_ip not in ("", "0.0.0.0") else [],
-                                       dump_path=iptables_dump)
+                                       masquerade_all=masquerade_all, dump_path=iptables_dump)
         elif mode == "userspace":
-            self.proxier = UserspaceProxier(node_ip, bind_cluster_ips=bind_cluster_ips)
+            self.proxier = UserspaceProxier(node_ip, bind_cluster_ips=bind_cluster_ips, udp_idle_timeout=udp_idle_timeout)
         else:
             raise ValueError(f"unknown proxy mode {mode!r} (userspace|iptables|ipvs)")
         self.tracker = ChangeTracker()
         self.sync_period, self.min_sync_period = sync_period, min_sync_period
         self.healthz_port = healthz_port
+        self.healthz_address = healthz_address
+        self.metrics_address = metrics_address          # --metrics-bind-address (host, port) or None
         self.metrics = new_registry()
         self.m_sync = Histogram("kubeproxy_sync_proxy_rules_latency_microseconds", "SyncProxyRules latency",
                                 buckets=MICRO_BUCKETS, registry=self.metrics)
@@ -76,9 +82,14 @@ class ProxyServer:
             app.router.add_get("/metrics", self._metrics)
             self._runner = web.AppRunner(app, access_log=None)
             await self._runner.setup()
-            site = web.TCPSite(self._runner, "127.0.0.1", self.healthz_port)
+            site = web.TCPSite(self._runner, self.healthz_address, self.healthz_port)
             await site.start()
             self.healthz_port = site._server.sockets[0].getsockname()[1]
+            if self.metrics_address and self.metrics_address[1]:
+                try:
+                    await web.TCPSite(self._runner, *self.metrics_address).start()
+                except OSError as e:
+                    log.warning("metrics listener %s: %s", self.metrics_address, e)
         return self
 
     async def sync(self):

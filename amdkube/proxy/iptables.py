@@ -49,17 +49,28 @@ def sep_chain(spn: ServicePortName, proto: str, endpoint: str) -> str:
     return "KUBE-SEP-" + _hash(str(spn) + proto.lower() + endpoint)
 
 
+def masq_mark(bit: int = 14) -> str:
+    """--iptables-masquerade-bit: the fwmark bit that asks KUBE-POSTROUTING for SNAT."""
+    if not 0 <= bit <= 31:
+        raise ValueError("--iptables-masquerade-bit must be within [0, 31]")
+    v = f"{1 << bit:#x}"
+    return f"{v}/{v}"
+
+
 def render(services: dict[ServicePortName, ServiceInfo], endpoints: dict[ServicePortName, list],
-           cluster_cidr: str = "", node_ips: tuple = ()) -> str:
+           cluster_cidr: str = "", node_ips: tuple = (), masquerade_all: bool = False, masq: str = MASQ_MARK) -> str:
+    """masquerade_all (--masquerade-all): SNAT every packet sent to a service's cluster IP, not
+    only those from outside --cluster-cidr."""
+    mark = masq
     filt_chains = ["KUBE-SERVICES", "KUBE-FORWARD"]
     filt_rules: list[str] = []
     nat_chains = ["KUBE-SERVICES", "KUBE-NODEPORTS", "KUBE-POSTROUTING", KUBE_MARK_MASQ, "KUBE-MARK-DROP"]
     nat_rules = [
-        f'-A KUBE-POSTROUTING -m comment --comment "kubernetes service traffic requiring SNAT" -m mark --mark {MASQ_MARK} -j MASQUERADE',
-        f"-A {KUBE_MARK_MASQ} -j MARK --set-xmark {MASQ_MARK}",
+        f'-A KUBE-POSTROUTING -m comment --comment "kubernetes service traffic requiring SNAT" -m mark --mark {mark} -j MASQUERADE',
+        f"-A {KUBE_MARK_MASQ} -j MARK --set-xmark {mark}",
         "-A KUBE-MARK-DROP -j MARK --set-xmark 0x8000/0x8000",
     ]
-    filt_rules.append('-A KUBE-FORWARD -m comment --comment "kubernetes forwarding rules" -m mark --mark 0x4000/0x4000 -j ACCEPT')
+    filt_rules.append(f'-A KUBE-FORWARD -m comment --comment "kubernetes forwarding rules" -m mark --mark {mark} -j ACCEPT')
     for spn in sorted(services, key=str):
         info = services[spn]
         proto = info.protocol.lower()
@@ -74,7 +85,10 @@ def render(services: dict[ServicePortName, ServiceInfo], endpoints: dict[Service
             continue
         sc = svc_chain(spn, info.protocol)
         nat_chains.append(sc)
-        if cluster_cidr:
+        if masquerade_all:
+            nat_rules.append(f"-A KUBE-SERVICES {comment} -m {proto} -p {proto} "
+                             f"-d {info.cluster_ip}/32 --dport {info.port} -j {KUBE_MARK_MASQ}")
+        elif cluster_cidr:
             nat_rules.append(f"-A KUBE-SERVICES ! -s {cluster_cidr} {comment} -m {proto} -p {proto} "
                              f"-d {info.cluster_ip}/32 --dport {info.port} -j {KUBE_MARK_MASQ}")
         nat_rules.append(f"-A KUBE-SERVICES {comment} -m {proto} -p {proto} -d {info.cluster_ip}/32 --dport {info.port} -j {sc}")
@@ -118,8 +132,10 @@ def render(services: dict[ServicePortName, ServiceInfo], endpoints: dict[Service
 class IptablesProxier:
     mode = "iptables"
 
-    def __init__(self, cluster_cidr: str = "", dry_run: bool | None = None, dump_path: str | None = None):
+    def __init__(self, cluster_cidr: str = "", dry_run: bool | None = None, dump_path: str | None = None,
+                 masquerade_all: bool = False, masquerade_bit: int = 14):
         self.cluster_cidr = cluster_cidr
+        self.masquerade_all, self.masq = masquerade_all, masq_mark(masquerade_bit)
         self.binary = shutil.which("iptables-restore")
         self.dry_run = (self.binary is None or os.geteuid() != 0) if dry_run is None else dry_run
         self.dump_path = dump_path
@@ -127,7 +143,7 @@ class IptablesProxier:
         self.syncs = 0
 
     async def sync(self, services, endpoints):
-        rules = render(services, endpoints, self.cluster_cidr)
+        rules = render(services, endpoints, self.cluster_cidr, masquerade_all=self.masquerade_all, masq=self.masq)
         self.syncs += 1
         if rules == self.last_rules:
             return
@@ -145,3 +161,39 @@ class IptablesProxier:
 
     async def stop(self):
         pass
+
+
+def cleanup_rules(saved: str) -> str:
+    """iptables-restore input that flushes and deletes every KUBE-* chain found in
+    `iptables-save` output (proxier.go CleanupLeftovers), jump rules into them first."""
+    out, table, chains, jumps = [], None, [], []
+
+    def flush():
+        if table is None:
+            return
+        out.append(f"*{table}")
+        out.extend(f":{c} - [0:0]" for c in chains)
+        out.extend(jumps)
+        out.extend(f"-X {c}" for c in chains)
+        out.append("COMMIT")
+    for line in saved.splitlines():
+        if line.startswith("*"):
+            flush()
+            table, chains, jumps = line[1:], [], []
+        elif line.startswith(":KUBE-"):
+            chains.append(line[1:].split()[0])
+        elif line.startswith("-A ") and " -j KUBE-" in line and not line.split()[1].startswith("KUBE-"):
+            jumps.append("-D" + line[2:])
+    flush()
+    return "\n".join(out) + "\n"
+
+
+def cleanup(dry_run: bool = False) -> str:
+    save, restore = shutil.which("iptables-save"), shutil.which("iptables-restore")
+    if save is None or restore is None:
+        return ""
+    saved = subprocess.run([save], capture_output=True, text=True).stdout
+    rules = cleanup_rules(saved)
+    if not dry_run:
+        subprocess.run([restore, "--noflush"], input=rules, text=True, capture_output=True)
+    return rules

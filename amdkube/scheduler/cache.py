@@ -163,9 +163,15 @@ def _has_anti_affinity(pod) -> bool:
                 .get("requiredDuringSchedulingIgnoredDuringExecution"))
 
 
+def _has_affinity(pod) -> bool:
+    return bool((((pod.get("spec") or {}).get("affinity") or {}).get("podAffinity") or {})
+                .get("requiredDuringSchedulingIgnoredDuringExecution"))
+
+
 class SchedulerCache:
     def __init__(self, ttl: float = 30.0):
         self.anti_affinity_pods = 0  # pods carrying required anti-affinity (MatchInterPodAffinity fast path)
+        self.affinity_pods = 0       # pods carrying required affinity (hardPodAffinitySymmetricWeight)
         self.nodes: dict[str, NodeInfo] = {}
         self.pod_node: dict[str, str] = {}          # pod key -> node name
         self.pod_states: dict[str, dict] = {}       # pod key -> pod
@@ -175,6 +181,8 @@ class SchedulerCache:
     def _track(self, pod, delta):
         if _has_anti_affinity(pod):
             self.anti_affinity_pods += delta
+        if _has_affinity(pod):
+            self.affinity_pods += delta
 
     def _ni(self, name) -> NodeInfo:
         ni = self.nodes.get(name)

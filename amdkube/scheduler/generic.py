@@ -39,31 +39,44 @@ class FitError(Exception):
 
 
 class Context:
-    __slots__ = ("nodes", "any_anti_affinity")
+    __slots__ = ("nodes", "any_anti_affinity", "any_affinity", "hard_weight", "services")
 
-    def __init__(self, nodes, any_anti_affinity):
+    def __init__(self, nodes, any_anti_affinity, any_affinity=False, hard_weight=0, services=None):
         self.nodes, self.any_anti_affinity = nodes, any_anti_affinity
+        self.any_affinity, self.hard_weight = any_affinity, hard_weight
+        self.services = services or (lambda: [])
 
 
 class GenericScheduler:
     def __init__(self, cache, predicates: list[str], priorities: dict[str, int], extenders=(), use_topology=True,
-                 trace_threshold: float = 0.1, volumes=None, volume_scheduling: bool = False):
+                 trace_threshold: float = 0.1, volumes=None, volume_scheduling: bool = False, custom_predicates=None,
+                 custom_priorities=None, services=None, hard_affinity_weight: int = 1):
         self.cache = cache
         self.volumes = volumes                  # scheduler/volumes.VolumeLister (claims, volumes, classes)
         self.volume_scheduling = volume_scheduling
         self.volume_binds: dict[str, list] = {}  # pod key -> [(pvc, pv)] to pre-bind before the pod
-        names = [p for p in ORDER if p in predicates] + [p for p in predicates if p not in ORDER]
-        self.predicates = [(n, PREDICATES[n]) for n in names]
-        self.priorities = [(n, PRIORITIES[n], w) for n, w in priorities.items() if w]
-        self.extenders = list(extenders)
+        self.services = services
+        self.configure(predicates, priorities, custom_predicates or {}, custom_priorities or {}, extenders,
+                       hard_affinity_weight)
         self.use_topology = use_topology
         self.last_index = 0
         self.trace_threshold = trace_threshold
         self.ecache: dict[str, dict[str, tuple]] = {}
         self.ecache_hits = 0
 
+    def configure(self, predicates, priorities, custom_predicates, custom_priorities, extenders, hard_affinity_weight):
+        """(Re)build the algorithm from a policy: registered names plus policy-argument functions."""
+        names = [p for p in ORDER if p in predicates] + [p for p in predicates if p not in ORDER]
+        self.predicates = [(n, custom_predicates.get(n) or PREDICATES[n]) for n in names]
+        self.priorities = [(n, custom_priorities.get(n) or PRIORITIES[n], w) for n, w in priorities.items() if w]
+        self.extenders = list(extenders)
+        self.hard_affinity_weight = hard_affinity_weight
+        self.custom = bool(custom_predicates or custom_priorities)
+        self.ecache = {}
+
     def _ctx(self, nodes):
-        return Context(nodes, self.cache.anti_affinity_pods > 0)
+        return Context(nodes, self.cache.anti_affinity_pods > 0, getattr(self.cache, "affinity_pods", 0) > 0,
+                       self.hard_affinity_weight, self.services)
 
     # Equivalence cache (reference plugin/pkg/scheduler/core/equivalence_cache.go:38): pods with the
     # same scheduling-relevant spec get the same per-node answer as long as the node is unchanged.
@@ -72,7 +85,8 @@ class GenericScheduler:
     # the last identical pod are re-evaluated. Pods with inter-pod (anti-)affinity, or any cluster
     # with anti-affinity pods, bypass it (their answer depends on other nodes).
     def _equiv_key(self, pi):
-        if pi.pod_affinity or pi.pod_anti_affinity or pi.pref_affinity or pi.pref_anti or self.cache.anti_affinity_pods:
+        if pi.pod_affinity or pi.pod_anti_affinity or pi.pref_affinity or pi.pref_anti or self.cache.anti_affinity_pods or \
+                self.custom or (self.hard_affinity_weight and getattr(self.cache, "affinity_pods", 0)):
             return None
         if pi.ext_error:
             return None
@@ -102,7 +116,7 @@ class GenericScheduler:
         return (not reasons), reasons
 
     async def find_nodes_that_fit(self, pi, nodes):
-        ctx = self._ctx(nodes) if (pi.pod_affinity or pi.pod_anti_affinity) or any(
+        ctx = self._ctx(nodes) if (pi.pod_affinity or pi.pod_anti_affinity) or self.custom or any(
             n == "MatchInterPodAffinity" for n, _ in self.predicates) else None
         fit, failed = [], {}
         ek = self._equiv_key(pi)
@@ -139,6 +153,8 @@ class GenericScheduler:
     async def prioritize(self, pi, nodes, ctx) -> list[float]:
         if not self.priorities and not self.extenders:
             return [1.0] * len(nodes)
+        if ctx is None and (self.custom or (self.hard_affinity_weight and self.cache.affinity_pods)):
+            ctx = self._ctx(self.cache.ready_nodes())
         total = [0.0] * len(nodes)
         # per-node scores depend only on (pod class, node state) unless a priority normalises across
         # nodes; only the normalising ones (spread, affinity, taints) are recomputed every time

@@ -1,0 +1,125 @@
+"""Scheduler policy arguments (plugin/pkg/scheduler/api/types.go PredicateArgument /
+PriorityArgument; factory/plugins.go RegisterCustomFitPredicate / RegisterCustomPriorityFunction):
+policy entries that carry an `argument` build a predicate or priority of their own.
+
+  predicates: {"name": N, "argument": {"serviceAffinity": {"labels": [...]}}}
+                — pods of one service land on nodes that agree, for these labels, with the
+                  nodes the service's first pods landed on (predicates.go ServiceAffinity)
+              {"name": N, "argument": {"labelsPresence": {"labels": [...], "presence": bool}}}
+                — the node has all (presence) or none (absence) of the labels
+  priorities: {"name": N, "weight": W, "argument": {"serviceAntiAffinity": {"label": L}}}
+                — spread a service's pods over the values of label L (selector_spreading.go)
+              {"name": N, "weight": W, "argument": {"labelPreference": {"label": L, "presence": bool}}}
+                — prefer nodes that have (or lack) label L (node_label.go)
+"""
+from __future__ import annotations
+
+from ..api import meta as m
+from ..api.labels import selector_from_set
+from .predicates import OK, _fail
+
+MAX = 10.0
+
+
+def _service_pods(pi, ctx):
+    """Pods already placed that belong to a service selecting the incoming pod (same namespace)."""
+    ns = m.namespace_of(pi.pod)
+    sels = [selector_from_set((s.get("spec") or {}).get("selector") or {}) for s in (ctx.services() if ctx else [])
+            if m.namespace_of(s) == ns and (s.get("spec") or {}).get("selector")]
+    sels = [s for s in sels if s.matches(pi.labels)]
+    if not sels:
+        return []
+    out = []
+    for ni in ctx.nodes:
+        for p in ni.pods.values():
+            if m.namespace_of(p) == ns and m.key_of(p) != pi.key and any(s.matches(m.labels_of(p)) for s in sels):
+                out.append((p, ni))
+    return out
+
+
+def service_affinity(labels: list[str]):
+    def pred(pi, ni, ctx=None):
+        want = {k: pi.node_selector[k] for k in labels if k in pi.node_selector}
+        missing = [k for k in labels if k not in want]
+        if missing and ctx is not None:
+            placed = _service_pods(pi, ctx)
+            if placed:
+                first = placed[0][1]
+                for k in missing:
+                    if k in first.labels:
+                        want[k] = first.labels[k]
+        if all(ni.labels.get(k) == v for k, v in want.items()):
+            return OK
+        return _fail("CheckServiceAffinity")
+    return pred
+
+
+def labels_presence(labels: list[str], presence: bool):
+    def pred(pi, ni, ctx=None):
+        has = all(k in ni.labels for k in labels) if presence else not any(k in ni.labels for k in labels)
+        return OK if has else _fail("CheckNodeLabelPresence")
+    return pred
+
+
+def service_anti_affinity(label: str):
+    def prio(pi, nodes, ctx=None):
+        placed = _service_pods(pi, ctx) if ctx is not None else []
+        counts: dict[str, int] = {}
+        for _, ni in placed:
+            v = ni.labels.get(label)
+            if v is not None:
+                counts[v] = counts.get(v, 0) + 1
+        total = sum(counts.values())
+        out = []
+        for ni in nodes:
+            v = ni.labels.get(label)
+            if v is None:
+                out.append(0.0)
+            elif total == 0:
+                out.append(MAX)
+            else:
+                out.append(MAX * (total - counts.get(v, 0)) / total)
+        return out
+    return prio
+
+
+def label_preference(label: str, presence: bool):
+    def prio(pi, nodes, ctx=None):
+        return [MAX if (label in ni.labels) == presence else 0.0 for ni in nodes]
+    return prio
+
+
+def build(policy: dict) -> tuple[list, dict, dict, dict]:
+    """(predicate names, priority weights, custom predicates, custom priorities)."""
+    from .predicates import DEFAULT_PREDICATES, PREDICATES
+    from .priorities import DEFAULT_PRIORITIES, PRIORITIES
+    cpreds, cprios = {}, {}
+    preds = []
+    if "predicates" in policy:
+        for p in policy.get("predicates") or []:
+            arg = p.get("argument") or {}
+            if "serviceAffinity" in arg:
+                cpreds[p["name"]] = service_affinity(list(arg["serviceAffinity"].get("labels") or []))
+            elif "labelsPresence" in arg:
+                lp = arg["labelsPresence"]
+                cpreds[p["name"]] = labels_presence(list(lp.get("labels") or []), bool(lp.get("presence")))
+            elif p["name"] not in PREDICATES:
+                raise ValueError(f"unknown predicate {p['name']!r} and no argument to build it from")
+            preds.append(p["name"])
+    else:
+        preds = list(DEFAULT_PREDICATES)
+    prios = {}
+    if "priorities" in policy:
+        for p in policy.get("priorities") or []:
+            arg = p.get("argument") or {}
+            if "serviceAntiAffinity" in arg:
+                cprios[p["name"]] = service_anti_affinity(arg["serviceAntiAffinity"]["label"])
+            elif "labelPreference" in arg:
+                lp = arg["labelPreference"]
+                cprios[p["name"]] = label_preference(lp["label"], bool(lp.get("presence")))
+            elif p["name"] not in PRIORITIES:
+                raise ValueError(f"unknown priority {p['name']!r} and no argument to build it from")
+            prios[p["name"]] = int(p.get("weight", 1))
+    else:
+        prios = dict(DEFAULT_PRIORITIES)
+    return preds, prios, cpreds, cprios

@@ -104,13 +104,37 @@ def node_prefer_avoid_pods(pi, nodes, ctx=None):
     return out
 
 
+def _symmetric_hard(pi, nodes, ctx) -> list[int]:
+    """interpod_affinity.go: an existing pod's *required* affinity term that matches the incoming
+    pod pulls it into that pod's topology domain with hardPodAffinitySymmetricWeight."""
+    from .predicates import _term_selector, _term_namespaces
+    out = [0] * len(nodes)
+    for o in ctx.nodes:
+        for p in o.pods.values():
+            terms = ((((p.get("spec") or {}).get("affinity") or {}).get("podAffinity") or {})
+                     .get("requiredDuringSchedulingIgnoredDuringExecution") or [])
+            for term in terms:
+                if m.namespace_of(pi.pod) not in _term_namespaces(term, p) or not _term_selector(term).matches(pi.labels):
+                    continue
+                key = term.get("topologyKey")
+                val = o.labels.get(key)
+                if val is None:
+                    continue
+                for i, ni in enumerate(nodes):
+                    if ni.labels.get(key) == val:
+                        out[i] += ctx.hard_weight
+    return out
+
+
 def inter_pod_affinity(pi, nodes, ctx=None):
-    if not (pi.pref_affinity or pi.pref_anti):
+    sym = ctx is not None and ctx.hard_weight and ctx.any_affinity
+    if not (pi.pref_affinity or pi.pref_anti or sym):
         return [0.0] * len(nodes)
     from .predicates import _term_selector, _term_namespaces
     raw = []
-    for ni in nodes:
-        s = 0
+    hard = _symmetric_hard(pi, nodes, ctx) if sym else [0] * len(nodes)
+    for idx, ni in enumerate(nodes):
+        s = hard[idx]
         for weighted, sign in ((pi.pref_affinity, 1), (pi.pref_anti, -1)):
             for wt in weighted:
                 term = wt.get("podAffinityTerm") or {}

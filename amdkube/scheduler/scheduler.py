@@ -40,13 +40,17 @@ PROVIDERS = {
 }
 
 
-def load_policy(path_or_dict) -> tuple[list, dict, list]:
-    pol = path_or_dict
+def read_policy(path_or_dict) -> dict:
     if isinstance(path_or_dict, str):
         with open(path_or_dict) as f:
-            pol = json.load(f)
-    preds = [p["name"] for p in pol.get("predicates") or []] if "predicates" in pol else list(DEFAULT_PREDICATES)
-    prios = {p["name"]: int(p.get("weight", 1)) for p in pol.get("priorities") or []} if "priorities" in pol else dict(DEFAULT_PRIORITIES)
+            return json.load(f)
+    return path_or_dict
+
+
+def load_policy(path_or_dict) -> tuple[list, dict, list]:
+    from .policy_args import build
+    pol = read_policy(path_or_dict)
+    preds, prios, _, _ = build(pol)
     return preds, prios, list(pol.get("extenders") or [])
 
 
@@ -54,23 +58,41 @@ class Scheduler:
     def __init__(self, client: Client, scheduler_name: str = "default-scheduler", policy=None,
                  algorithm_provider: str = "DefaultProvider", feature_gates: str = "", leader_elect: bool = False,
                  identity: str | None = None, port: int | None = None, disable_preemption: bool = False,
-                 bind_concurrency: int = 256):
+                 bind_concurrency: int = 256, hard_pod_affinity_weight: int = 1, lock_object_name: str = "kube-scheduler",
+                 lock_object_namespace: str = "kube-system", address: str = "127.0.0.1",
+                 policy_configmap: tuple[str, str] | None = None):
+        """policy: a Policy file path or dict (--policy-config-file); policy_configmap: (namespace,
+        name) of a ConfigMap whose `policy.cfg` holds it (--policy-configmap), read at start."""
         self.client = client
         self.name = scheduler_name
         self.gates = FeatureGate(feature_gates)
+        self.policy_configmap = policy_configmap
+        self.hard_weight = hard_pod_affinity_weight
+        cpreds, cprios = {}, {}
         if policy is not None:
-            preds, prios, exts = load_policy(policy)
+            from .policy_args import build
+            pol = read_policy(policy)
+            preds, prios, cpreds, cprios = build(pol)
+            exts = list(pol.get("extenders") or [])
+            self.hard_weight = int(pol.get("hardPodAffinitySymmetricWeight", self.hard_weight))
         else:
             preds, prios = PROVIDERS[algorithm_provider]
             exts = []
+        self.lock_object = (lock_object_namespace, lock_object_name)
+        self.address = address
         if not self.gates("GPUTopologyScheduling"):
             prios = {k: v for k, v in prios.items() if k != "GPUTopologyPriority"}
         self.extenders = [HTTPExtender(e) for e in exts]
         self.cache = SchedulerCache()
         from .volumes import VolumeLister
         self.volumes = VolumeLister()
+        self.svc_inf = None
         self.algo = GenericScheduler(self.cache, preds, prios, self.extenders, use_topology=self.gates("GPUTopologyScheduling"),
-                                     volumes=self.volumes, volume_scheduling=self.gates("VolumeScheduling"))
+                                     volumes=self.volumes, volume_scheduling=self.gates("VolumeScheduling"),
+                                     custom_predicates=cpreds, custom_priorities=cprios,
+                                     services=lambda: self.svc_inf.list() if self.svc_inf is not None else [],
+                                     hard_affinity_weight=self.hard_weight)
+        self._needs_services = bool(cpreds or cprios)
         self.queue = SchedulingQueue(self.gates("PodPriority"))
         self.recorder = EventRecorder(client, self.name)
         self.leader_elect = leader_elect
@@ -149,12 +171,31 @@ class Scheduler:
             self.queue.move_all_to_active()
 
     # ------------------------------------------------------------ lifecycle
+    async def _policy_from_configmap(self):
+        """--policy-configmap: the Policy in a ConfigMap's `policy.cfg` (factory.go CreateFromConfig)."""
+        from .policy_args import build
+        ns, name = self.policy_configmap
+        cm = await self.client.get("configmaps", name, ns)
+        raw = (cm.get("data") or {}).get("policy.cfg")
+        if not raw:
+            raise ValueError(f"ConfigMap {ns}/{name} has no policy.cfg")
+        pol = json.loads(raw)
+        preds, prios, cpreds, cprios = build(pol)
+        if not self.gates("GPUTopologyScheduling"):
+            prios = {k: v for k, v in prios.items() if k != "GPUTopologyPriority"}
+        self.extenders = [HTTPExtender(e) for e in pol.get("extenders") or []]
+        self.hard_weight = int(pol.get("hardPodAffinitySymmetricWeight", self.hard_weight))
+        self.algo.configure(preds, prios, cpreds, cprios, self.extenders, self.hard_weight)
+        self._needs_services = bool(cpreds or cprios)
+
     async def start(self):
         self.recorder.start()
+        if self.policy_configmap is not None:
+            await self._policy_from_configmap()
         if self.port is not None:
             await self._serve()
         if self.leader_elect:
-            le = LeaderElector(self.client, "kube-scheduler", self.identity)
+            le = LeaderElector(self.client, self.lock_object[1], self.identity, ns=self.lock_object[0])
             self._tasks.append(asyncio.create_task(le.run(self._run_informers_and_loop)))
         else:
             await self._start_informers()
@@ -181,6 +222,9 @@ class Scheduler:
             inf.add_handler(on_add=lambda o: self.queue.move_all_to_active(), on_update=self._on_volume_update)
         for inf in self.vol_infs:
             inf.start()
+        if self._needs_services:        # serviceAffinity / serviceAntiAffinity policy arguments
+            self.svc_inf = Informer(self.client, "services")
+            self.svc_inf.start()
         self.node_inf.start()
         await self.node_inf.wait_synced(30)
         for inf in self.vol_infs:
@@ -193,7 +237,7 @@ class Scheduler:
             t.cancel()
         for t in list(self._binds):
             t.cancel()
-        for inf in (self.pod_inf, self.node_inf, *getattr(self, "vol_infs", [])):
+        for inf in (self.pod_inf, self.node_inf, self.svc_inf, *getattr(self, "vol_infs", [])):
             if inf:
                 await inf.stop()
         await self.recorder.stop()
@@ -220,7 +264,7 @@ class Scheduler:
         profiling.add_routes(app)
         self._runner = web.AppRunner(app, access_log=None)
         await self._runner.setup()
-        site = web.TCPSite(self._runner, "127.0.0.1", self.port)
+        site = web.TCPSite(self._runner, self.address, self.port)
         await site.start()
         self.port = site._server.sockets[0].getsockname()[1]
 
