@@ -13,12 +13,29 @@ import time
 
 from ..smi import device_id
 
+# cAdvisor's DutyCycle is the NVML average over the last 10 s (accelerators/nvidia.go:216-252)
+DUTY_CYCLE_WINDOW_S = 10.0
+
+
+def duty_cycle(backend, index: int, sample: dict) -> int:
+    """Percent busy over the last DUTY_CYCLE_WINDOW_S from the backend's activity sampler,
+    else the instantaneous gfx activity of `sample`."""
+    try:
+        avg = backend.average_activity(index, DUTY_CYCLE_WINDOW_S)
+    except Exception:
+        avg = None
+    if avg:
+        return int(round(avg["gfx_activity"]))
+    return int(sample.get("gfx_activity") or 0)
+
 
 class AcceleratorCollector:
     def __init__(self, backend, node: str = ""):
         self.b = backend
         self.node = node
         self._gpus = None
+        if backend:
+            backend.start_sampling()
 
     def gpus(self):
         if self._gpus is None:
@@ -44,7 +61,7 @@ class AcceleratorCollector:
                 s = {}
             out.append({"make": "amd", "model": g.get("market_name", ""), "id": did,
                         "memoryTotal": int(g.get("vram_total_bytes") or 0), "memoryUsed": int(s.get("vram_used_bytes") or 0),
-                        "dutyCycle": int(s.get("gfx_activity") or 0)})
+                        "dutyCycle": duty_cycle(self.b, g["index"], s)})
         return out
 
     def render_container_metrics(self, pod_devices: list[dict]) -> str:

@@ -3,7 +3,9 @@ promises, README.md:57, which is not in the repo — SURVEY §0.2 row 2).
 
 Serves `/metrics` with
   * node-level series `amd_gpu_*{gpu, uuid, node, model, pod, namespace, container}`:
-    utilization_percent, memory_utilization_percent, vram_used_bytes, vram_total_bytes,
+    utilization_percent, memory_utilization_percent (instantaneous) and their 10 s means
+    utilization_avg10s_percent / memory_utilization_avg10s_percent (native background
+    sampler, native/sampler_core.h), vram_used_bytes, vram_total_bytes,
     power_watts, power_limit_watts, temperature_celsius, temperature_memory_celsius,
     ecc_correctable_total, ecc_uncorrectable_total, ecc_deferred_total,
     xgmi_link_read_bytes_total / xgmi_link_write_bytes_total {peer}, health (1 = Healthy),
@@ -23,6 +25,7 @@ import aiohttp
 from aiohttp import web
 
 from ..smi import Backend, device_id
+from .collector import DUTY_CYCLE_WINDOW_S, duty_cycle
 from ..utils.metrics import CONTENT_TYPE
 
 log = logging.getLogger("amdkube.exporter")
@@ -39,6 +42,7 @@ class Exporter:
         self.kubelet_url = kubelet_url
         self.ecc_threshold = ecc_threshold
         self.gpus = backend.gpus()
+        self.sampling = backend.start_sampling()
         self.scrapes = 0
         self._runner = None
         self.port = None
@@ -97,6 +101,17 @@ class Exporter:
                                      ("ecc_deferred", "amd_gpu_ecc_deferred_total", "Deferred ECC errors")):
                 if key in s:
                     add(name, base, s[key], help_)
+            if self.sampling:
+                try:
+                    avg = self.b.average_activity(g["index"], DUTY_CYCLE_WINDOW_S)
+                except Exception:
+                    avg = None
+                if avg:
+                    add("amd_gpu_utilization_avg10s_percent", base, round(avg["gfx_activity"], 2),
+                        "GFX engine busy percent, mean of the background samples over the last 10 s")
+                    if "umc_activity" in avg:
+                        add("amd_gpu_memory_utilization_avg10s_percent", base, round(avg["umc_activity"], 2),
+                            "Memory controller busy percent, mean over the last 10 s")
             for key, name in (("power_watts", "amd_gpu_power_watts"), ("power_limit_watts", "amd_gpu_power_limit_watts")):
                 if key in s:
                     v = s[key]
@@ -118,7 +133,7 @@ class Exporter:
                       "acc_id": did}
                 add("container_accelerator_memory_total_bytes", cl, int(g.get("vram_total_bytes") or 0), "Total accelerator memory.")
                 add("container_accelerator_memory_used_bytes", cl, int(s.get("vram_used_bytes") or 0), "Total accelerator memory allocated.")
-                add("container_accelerator_duty_cycle", cl, int(s.get("gfx_activity") or 0),
+                add("container_accelerator_duty_cycle", cl, duty_cycle(self.b, g["index"], s),
                     "Percent of time over the past sample period during which the accelerator was actively processing.")
         for name, lines in fam.items():
             L.append(f"# HELP {name} {lines[0]}")

@@ -15,12 +15,15 @@ on a machine that exposes /dev/kfd (no silent fake fallback on real hardware).
 """
 from __future__ import annotations
 
+import atexit
+import collections
 import copy
 import glob
 import json
 import logging
 import os
 import threading
+import time
 
 log = logging.getLogger("amdkube.smi")
 FIXTURE_DIR = os.path.join(os.path.dirname(__file__), "fixtures")
@@ -141,6 +144,17 @@ class Backend:
     def link_metrics(self, index: int) -> list[dict]:
         return []
 
+    def start_sampling(self, period_ms: float = 100.0) -> bool:
+        """Begin background activity sampling for average_activity(); False = not supported
+        (callers then fall back to the instantaneous sample)."""
+        return False
+
+    def average_activity(self, index: int, window_s: float = 10.0) -> dict | None:
+        """Mean {gfx_activity, umc_activity, samples, span_s} over the last window_s seconds
+        (gonvml AverageGPUUtilization, vendor/github.com/mindprince/gonvml/bindings.go:218-260),
+        or None when nothing was sampled in the window."""
+        return None
+
     def close(self):
         pass
 
@@ -187,8 +201,19 @@ class AmdSmiBackend(Backend):
         with self._lock:
             return self.lib.link_metrics(index)
 
+    def start_sampling(self, period_ms: float = 100.0) -> bool:
+        """Native sampler thread (native/sampler_core.h); its ring holds >= 60 s of samples."""
+        with self._lock:
+            if not self.lib.sampler_state()["running"]:
+                self.lib.start_sampler(period_ms, max(64, int(60_000 / period_ms)))
+                atexit.register(self.lib.stop_sampler)  # joined before the library goes away
+        return True
+
+    def average_activity(self, index, window_s=10.0):
+        return self.lib.average_activity(index, window_s)
+
     def close(self):
-        self.lib.shutdown()
+        self.lib.shutdown()  # stops the sampler first
 
 
 def _props(path: str) -> dict:
@@ -277,6 +302,8 @@ class FakeBackend(Backend):
         self.data = partition_fixture(self.data, compute_partition, memory_partition)
         self.samples = {g["index"]: dict(self.data.get("sample_defaults", {})) for g in self.data["gpus"]}
         self.procs: dict[int, list] = {}
+        self.sampling = False
+        self.history: dict[int, collections.deque] = {i: collections.deque(maxlen=1024) for i in self.samples}
 
     def gpus(self):
         return copy.deepcopy(self.data["gpus"])
@@ -309,6 +336,34 @@ class FakeBackend(Backend):
 
     def set_sample(self, index, **kw):
         self.samples[index].update(kw)
+        if self.sampling and ("gfx_activity" in kw or "umc_activity" in kw):
+            self._record(index)
+
+    # activity sampling: every set_sample() while sampling is one sample
+    def _record(self, index, t: float | None = None):
+        s = self.samples[index]
+        self.history[index].append((time.monotonic() if t is None else t, float(s.get("gfx_activity") or 0),
+                                    s.get("umc_activity")))
+
+    def start_sampling(self, period_ms: float = 100.0) -> bool:
+        if not self.sampling:
+            self.sampling = True
+            for i in self.samples:
+                self._record(i)
+        return True
+
+    def average_activity(self, index, window_s=10.0):
+        if index not in self.history:
+            raise SMIError(f"gpu {index} not found")
+        since = time.monotonic() - window_s
+        pts = [p for p in self.history[index] if p[0] >= since]
+        if not pts:
+            return None
+        out = {"gfx_activity": sum(p[1] for p in pts) / len(pts), "samples": len(pts), "span_s": pts[-1][0] - pts[0][0]}
+        umc = [float(p[2]) for p in pts if p[2] is not None]
+        if umc:
+            out["umc_activity"] = sum(umc) / len(umc)
+        return out
 
 
 def has_kfd() -> bool:
@@ -376,6 +431,12 @@ class _Limited(Backend):
 
     def link_metrics(self, index):
         return self.inner.link_metrics(index)
+
+    def start_sampling(self, period_ms: float = 100.0) -> bool:
+        return self.inner.start_sampling(period_ms)
+
+    def average_activity(self, index, window_s=10.0):
+        return self.inner.average_activity(index, window_s)
 
     def close(self):
         self.inner.close()

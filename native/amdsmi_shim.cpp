@@ -11,6 +11,10 @@
 //   topology()     N x N link matrix {type, hops, weight, p2p}
 //   link_metrics(i) per-link xGMI bit rate / bandwidth / read+write KB counters
 //   processes(i)   per-process VRAM and engine time (container GPU accounting)
+//   start_sampler / average_activity / stop_sampler
+//                  background gfx/umc activity sampling (native/sampler_core.h) and its mean
+//                  over a window: gonvml AverageGPUUtilization (bindings.go:218-260), which
+//                  cAdvisor reports as the 10 s DutyCycle (accelerators/nvidia.go:216-252)
 // Every query is individually fault tolerant: an unsupported field is simply absent, so a
 // partitioned or virtualised GPU still enumerates. The GIL is released around library
 // calls (some sysfs-backed queries take milliseconds).
@@ -24,6 +28,8 @@
 #include <stdexcept>
 #include <string>
 #include <vector>
+
+#include "sampler_core.h"
 
 namespace py = pybind11;
 
@@ -98,7 +104,18 @@ void init(uint64_t flags) {
   }
 }
 
+amdkube::ActivitySampler& sampler() {
+  static amdkube::ActivitySampler s;
+  return s;
+}
+
+void stop_sampler() {
+  py::gil_scoped_release nogil;  // joins the sampler thread
+  sampler().stop();
+}
+
 void shutdown() {
+  stop_sampler();  // its thread calls into the library
   std::lock_guard<std::mutex> lk(g_mu);
   if (!g_inited) return;
   amdsmi_shut_down();
@@ -308,6 +325,48 @@ py::list processes(size_t i) {
   return out;
 }
 
+// Starts (or restarts) the background sampler over every enumerated GPU.
+void start_sampler(double period_ms, size_t capacity) {
+  if (!g_inited) throw std::runtime_error("amdsmi not initialised (call init())");
+  if (!(period_ms > 0)) throw std::invalid_argument("period_ms must be > 0");
+  std::vector<amdsmi_processor_handle> handles = g_gpus;  // the thread owns its copy
+  auto src = [handles](size_t d, amdkube::ActivitySample* out) {
+    amdsmi_engine_usage_t act;
+    std::memset(&act, 0, sizeof(act));
+    if (amdsmi_get_gpu_activity(handles[d], &act) != AMDSMI_STATUS_SUCCESS || act.gfx_activity == 0xFFFFFFFFu) return false;
+    out->gfx = act.gfx_activity;
+    if (act.umc_activity != 0xFFFFFFFFu) {
+      out->umc = act.umc_activity;
+      out->has_umc = true;
+    }
+    return true;
+  };
+  py::gil_scoped_release nogil;
+  sampler().start(handles.size(), src, static_cast<int64_t>(period_ms * 1e6), capacity);
+}
+
+// Mean activity of GPU i over the last window_s seconds; None when no sample falls inside.
+py::object average_activity(size_t i, double window_s) {
+  gpu(i);
+  const int64_t since = amdkube::steady_now_ns() - static_cast<int64_t>(window_s * 1e9);
+  auto a = sampler().average(i, since);
+  if (a.samples == 0) return py::none();
+  py::dict d;
+  d["gfx_activity"] = a.gfx;
+  if (a.umc_samples) d["umc_activity"] = a.umc;
+  d["samples"] = a.samples;
+  d["span_s"] = static_cast<double>(a.last_ns - a.first_ns) / 1e9;
+  return d;
+}
+
+py::dict sampler_state() {
+  py::dict d;
+  d["running"] = sampler().running();
+  d["ticks"] = sampler().ticks();
+  d["devices"] = sampler().devices();
+  return d;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_amdsmi, m) {
@@ -321,4 +380,8 @@ PYBIND11_MODULE(_amdsmi, m) {
   m.def("topology", &topology);
   m.def("link_metrics", &link_metrics);
   m.def("processes", &processes);
+  m.def("start_sampler", &start_sampler, py::arg("period_ms") = 100.0, py::arg("capacity") = 1024);
+  m.def("stop_sampler", &stop_sampler);
+  m.def("average_activity", &average_activity, py::arg("index"), py::arg("window_s") = 10.0);
+  m.def("sampler_state", &sampler_state);
 }

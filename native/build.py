@@ -2,10 +2,11 @@
 
   python native/build.py            # CPU-side pybind modules + pause (g++), HIP targets (hipcc, gfx950)
   python native/build.py --cpu-only # just the g++ targets (used by the CPU test tier)
-  python native/build.py --sanitize # also the ASan/UBSan host builds (pause, topo self-test)
+  python native/build.py --sanitize # also the ASan/UBSan host builds (pause, topo self-test, sampler)
+                                    # and the ThreadSanitizer build of the activity sampler
 
 Outputs: amdkube/_native/{_amdsmi,_topo,_hipops}.<ext> and amdkube/_native/bin/{pause,
-rocm-vector-add,hbm-probe,gpu-burn,xgmi-probe[,topo-selftest-asan,pause-asan]}.
+rocm-vector-add,hbm-probe,gpu-burn,xgmi-probe[,topo-selftest-asan,pause-asan,sampler-selftest-{asan,tsan}]}.
 Targets are rebuilt only when a source/header is newer than the output.
 """
 from __future__ import annotations
@@ -44,7 +45,7 @@ def targets(sanitize=False, cpu_only=False):
     t = [
         (n(OUT, "_topo" + EXT), [n("native/topo_alloc.cpp"), n("native/topo_core.h")],
          ["g++", "-O3", "-std=c++17", "-shared", "-fPIC", *py, n("native/topo_alloc.cpp"), "-o", "{out}"]),
-        (n(OUT, "_amdsmi" + EXT), [n("native/amdsmi_shim.cpp")],
+        (n(OUT, "_amdsmi" + EXT), [n("native/amdsmi_shim.cpp"), n("native/sampler_core.h")],
          ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", *py, *rocm_inc, n("native/amdsmi_shim.cpp"), *rpath,
           "-lamd_smi", "-o", "{out}"]),
         (n(BIN, "pause"), [n("native/pause.cpp")],
@@ -65,6 +66,11 @@ def targets(sanitize=False, cpu_only=False):
              ["g++", "-O1", "-std=c++17", *san, n("native/topo_selftest.cpp"), "-o", "{out}"]),
             (n(BIN, "pause-asan"), [n("native/pause.cpp")],
              ["g++", "-O1", "-std=c++17", *san, n("native/pause.cpp"), "-o", "{out}"]),
+            (n(BIN, "sampler-selftest-asan"), [n("native/sampler_selftest.cpp"), n("native/sampler_core.h")],
+             ["g++", "-O1", "-std=c++17", *san, n("native/sampler_selftest.cpp"), "-pthread", "-o", "{out}"]),
+            (n(BIN, "sampler-selftest-tsan"), [n("native/sampler_selftest.cpp"), n("native/sampler_core.h")],
+             ["g++", "-O1", "-std=c++17", "-fsanitize=thread", "-fno-omit-frame-pointer", "-g",
+              n("native/sampler_selftest.cpp"), "-pthread", "-o", "{out}"]),
         ]
     if not cpu_only:
         hip = _hipcc()

@@ -106,6 +106,32 @@ def test_exporter_metrics_and_attribution():
     run(go())
 
 
+def test_duty_cycle_is_the_10s_average(monkeypatch):
+    """cAdvisor DutyCycle = NVML average over 10 s (accelerators/nvidia.go:216-252): the
+    collector and the exporter read the backend's sampler window, not one instant."""
+    import time as _t
+    from amdkube.monitoring.collector import AcceleratorCollector
+    from amdkube.smi import device_id
+    fb = FakeBackend(n=2)
+    col = AcceleratorCollector(fb, "n1")          # starts sampling
+    assert fb.sampling
+    for v in (100, 100, 40, 0):                   # samples inside the window
+        fb.set_sample(1, gfx_activity=v, umc_activity=v // 2)
+    did = device_id(fb.gpus()[1])
+    st = col.accelerator_stats([did])[0]
+    assert st["dutyCycle"] == round((0 + 100 + 100 + 40 + 0) / 5)   # start_sampling recorded the initial 0
+    ex = Exporter(fb, node="n1")
+    text = ex.collect({did: ("ml", "trainer", "c")})
+    line = [l for l in text.splitlines() if l.startswith('amd_gpu_utilization_avg10s_percent{gpu="1"')][0]
+    assert float(line.split()[-1]) == 48.0
+    assert 'amd_gpu_utilization_percent{gpu="1"' in text and text.count("amd_gpu_memory_utilization_avg10s_percent{") == 2
+    # samples older than the window no longer count: only the instantaneous value remains
+    real = _t.monotonic
+    monkeypatch.setattr("amdkube.smi.backend.time.monotonic", lambda: real() + 11)
+    assert fb.average_activity(1, 10.0) is None
+    assert col.accelerator_stats([did])[0]["dutyCycle"] == 0
+
+
 def test_hollow_nodes_gpu_density():
     """kubemark-style: 4 hollow nodes × 8 simulated MI355X, 32 GPU pods, no double assignment."""
     async def go():

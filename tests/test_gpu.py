@@ -179,6 +179,32 @@ def test_06_accelerator_stats_of_a_running_gpu_pod():
     run(go(), 300)
 
 
+def test_07_native_activity_sampler_averages_a_burn():
+    """The shim's background sampler (native/sampler_core.h via _amdsmi.start_sampler) on the
+    real MI355X: while gpu-burn keeps the MFMA pipes busy for 2 s, the windowed mean over
+    its samples is busy, and an idle window after it reads lower (gonvml AverageGPUUtilization)."""
+    import time
+    from amdkube.smi import AmdSmiBackend
+    b = AmdSmiBackend()
+    try:
+        assert b.start_sampling(20.0)
+        b.lib.start_sampler(20.0, 1024)   # restart at 20 ms even if an earlier test left one at 100 ms
+        time.sleep(0.3)
+        p = subprocess.run([os.path.join(BIN, "gpu-burn"), "--ms", "2000"], capture_output=True, text=True, timeout=120)
+        assert p.returncode == 0, p.stderr
+        busy = b.average_activity(0, 2.5)
+        st = b.lib.sampler_state()
+        assert st["running"] and st["ticks"] >= 50, st
+        assert busy and busy["samples"] >= 50 and busy["span_s"] > 1.5, busy
+        assert busy["gfx_activity"] > 20, busy
+        time.sleep(1.5)
+        idle = b.average_activity(0, 1.0)
+        assert idle and idle["gfx_activity"] < busy["gfx_activity"], (idle, busy)
+    finally:
+        b.close()
+    assert not b.lib.sampler_state()["running"]
+
+
 def test_04_probe_binaries():
     r = subprocess.run([os.path.join(BIN, "hbm-probe"), "--mib", "1024", "--iters", "3"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr

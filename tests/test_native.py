@@ -42,6 +42,16 @@ def test_topology_asan_selftest():
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
 
 
+@pytest.mark.parametrize("binary", ["sampler-selftest-tsan", "sampler-selftest-asan"])
+def test_activity_sampler_sanitized_selftest(binary):
+    """native/sampler_core.h under ThreadSanitizer and ASan/UBSan: readers racing the sampler
+    thread and concurrent start/stop (TSan variant for the shim's sampler)."""
+    r = subprocess.run([os.path.join(BIN, binary)], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66"))
+    assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr[-3000:]
+    assert "WARNING: ThreadSanitizer" not in r.stderr
+
+
 @pytest.mark.parametrize("binary", ["pause", "pause-asan"])
 def test_pause_reaps_and_exits_on_term(binary, tmp_path):
     pid_file = tmp_path / "pid"
