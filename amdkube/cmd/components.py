@@ -1022,3 +1022,5 @@ COMPONENTS = {"dns": dns, "kube-dns": dns, "kubeadm": kubeadm, "proxy": proxy, "
               "rocshim": rocshim, "amd-device-plugin": device_plugin, "device-plugin": device_plugin,
               "amdgpu-exporter": exporter, "exporter": exporter, "hollow-node": hollow_node, "local-up": local_up,
               "metrics-server": metrics_server, "cloud-controller-manager": cloud_controller_manager}
+from .gendocs import GENERATORS as _GENERATORS  # noqa: E402  (gendocs/genkubedocs/genman/genyaml)
+COMPONENTS.update(_GENERATORS)

@@ -427,9 +427,12 @@ def parser():
     p.add_argument("--kubeconfig", default=None)
     p.add_argument("--context", default=None)
     p.add_argument("-n", "--namespace", default=None)
-    sub = p.add_subparsers(dest="cmd", required=True)
-    for name in list(COMMANDS) + ["config"]:
-        sp = sub.add_parser(name)
+    sub = p.add_subparsers(dest="cmd", required=True, metavar="command")
+    from . import help as _help
+    for name in list(COMMANDS) + ["config", "help"]:
+        sp = sub.add_parser(name, help=_help.short(name), description=_help.long_desc(name),
+                            epilog="Examples:\n" + _help.examples(name),
+                            formatter_class=argparse.RawDescriptionHelpFormatter)
         _extra_args(sp)
         _more.add_arguments(sp)
         sp.add_argument("args", nargs="*")
@@ -500,6 +503,10 @@ async def validate_files(c, paths) -> list[str]:
 
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
+    if not argv:
+        from .help import overview
+        print(overview())
+        return 0
     cmd_tail = []
     if "--" in argv:
         i = argv.index("--")
@@ -514,6 +521,10 @@ def main(argv=None):
     elif a.command is None:
         a.command = []
 
+    if a.cmd == "help":
+        from .help import command_help, overview
+        print(command_help(a.args[0]) if a.args else overview())
+        return 0
     if a.cmd == "config":   # kubeconfig edits need no server
         from .extra import cmd_config_sync
         return cmd_config_sync(a)
