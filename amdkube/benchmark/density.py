@@ -57,7 +57,11 @@ def _rs(name, replicas, gpu):
 
 
 async def run_density(n_nodes: int = 10, pods_per_node: int = 30, gpus_per_node: int = 8, node_procs: int = 2,
-                      timeout: float = 300.0, in_process: bool = False) -> dict:
+                      timeout: float = 300.0, in_process: bool = False, cm_qps: float = 1000.0, cm_burst: int = 1000) -> dict:
+    """cm_qps/cm_burst: the controller-manager's --kube-api-qps/--kube-api-burst. Its default
+    of 20 (the reference's) caps ReplicaSet pod creation at 20 pods/s, so density runs raise it
+    explicitly, as the reference's kubemark masters do (cluster/kubemark/gce/config-default.sh
+    KUBEMARK_MASTER_COMPONENTS_QPS_LIMITS)."""
     api = await APIServer(event_ttl=3600).start()
     client = Client(api.url, pool=128)
     sched = cm = None
@@ -65,10 +69,11 @@ async def run_density(n_nodes: int = 10, pods_per_node: int = 30, gpus_per_node:
     env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
     if in_process:
         sched = await Scheduler(Client(api.url, pool=256)).start()
-        cm = await ControllerManager(Client(api.url, pool=128), controllers=["replicaset"]).start()
+        cm = await ControllerManager(Client(api.url, pool=128, qps=cm_qps, burst=cm_burst), controllers=["replicaset"]).start()
     else:
         for argv in (["scheduler", "--master", api.url, "--port", "0"],
-                     ["controller-manager", "--master", api.url, "--controllers", "replicaset"]):
+                     ["controller-manager", "--master", api.url, "--controllers", "replicaset",
+                      "--kube-api-qps", str(cm_qps), "--kube-api-burst", str(cm_burst)]):
             procs.append(subprocess.Popen([sys.executable, "-m", "amdkube", *argv], cwd=ROOT, env=env,
                                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL))
     per = [n_nodes // node_procs + (1 if i < n_nodes % node_procs else 0) for i in range(node_procs)]
@@ -136,7 +141,7 @@ async def run_density(n_nodes: int = 10, pods_per_node: int = 30, gpus_per_node:
                     for d in er.get("assigned") or []]
         return {"nodes": n_nodes, "pods_per_node": pods_per_node, "gpu_pods": n_gpu, "cpu_pods": n_cpu, "pods": total,
                 "node_ready_s": round(node_ready_s, 2), "elapsed_s": round(elapsed, 3),
-                "saturation_pods_per_s": round(total / elapsed, 1),
+                "saturation_pods_per_s": round(total / elapsed, 1), "controller_manager_qps": cm_qps,
                 "startup_ms": {"p50": round(pct(e2e, 50), 1), "p90": round(pct(e2e, 90), 1), "p99": round(pct(e2e, 99), 1)},
                 "gpu_startup_ms": {"p50": round(pct(gpu_e2e, 50), 1), "p90": round(pct(gpu_e2e, 90), 1),
                                    "p99": round(pct(gpu_e2e, 99), 1)},
@@ -168,9 +173,13 @@ def main(argv=None):
     ap.add_argument("--gpus-per-node", type=int, default=8)
     ap.add_argument("--node-procs", type=int, default=2)
     ap.add_argument("--in-process", action="store_true", help="scheduler + controller-manager in the apiserver process")
+    ap.add_argument("--controller-manager-qps", type=float, default=1000.0,
+                    help="controller-manager --kube-api-qps (its default, 20, caps pod creation at 20/s)")
+    ap.add_argument("--controller-manager-burst", type=int, default=1000)
     a = ap.parse_args(argv)
     print(json.dumps(asyncio.run(run_density(a.nodes, a.pods_per_node, a.gpus_per_node, a.node_procs,
-                                             in_process=a.in_process))))
+                                             in_process=a.in_process, cm_qps=a.controller_manager_qps,
+                                             cm_burst=a.controller_manager_burst))))
 
 
 if __name__ == "__main__":

@@ -687,6 +687,8 @@ def rocshim(argv):
     ap.add_argument("--cni-conf-dir", default="/etc/cni/net.d")
     ap.add_argument("--cni-bin-dir", default=None, help="default: /opt/cni/bin plus amdkube's bundled plugins")
     ap.add_argument("--node-ip", default="127.0.0.1")
+    ap.add_argument("--registry-dir", default=None,
+                    help="directory standing in for image registries (<host>/<repo>/<tag>/, optional <host>/auth.json)")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     klog.setup(a.v, "rocshim")
@@ -704,7 +706,8 @@ def rocshim(argv):
 
     async def mk():
         return await RocShim(a.listen, a.state_dir, a.hooks_dir, a.isolation, network=net,
-                             pod_namespaces=a.pod_namespaces or a.network_plugin == "kubenet").start()
+                             pod_namespaces=a.pod_namespaces or a.network_plugin == "kubenet",
+                             registry_dir=a.registry_dir).start()
     _run_forever(mk)
 
 

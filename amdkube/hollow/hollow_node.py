@@ -267,7 +267,8 @@ class HollowNode:
         cfg = KubeletConfig(node_name=self.name, root_dir=os.path.join(b, "kubelet"), plugins_dir=os.path.join(b, "plugins"),
                             cri_socket=os.path.join(b, "cri.sock"), port=0, relist_period=2.0,
                             node_status_update_frequency=self.status_period, eviction_interval=3600.0,
-                            cpu_capacity=64, memory_capacity=1024 * 2 ** 30, volume_mounter="none")
+                            cpu_capacity=64, memory_capacity=1024 * 2 ** 30, volume_mounter="none",
+                            oom_watcher=False)   # kubemark: fake cAdvisor, no kernel OOM stream
         self.kubelet = await Kubelet(Client(self.server, pool=16), cfg, smi_backend=backend).start()
         if backend is not None:
             # per-node unique device IDs (a real cluster has distinct GPUs on every node)

@@ -204,9 +204,11 @@ class CRIClient:
         r = await self._call("image_status", self.img.ImageStatus, C.ImageStatusRequest(image=C.ImageSpec(image=image)))
         return r.image if r.HasField("image") else None
 
-    async def pull_image(self, image) -> str:
-        return (await self._call("pull_image", self.img.PullImage, C.PullImageRequest(image=C.ImageSpec(image=image)),
-                                 timeout=300)).image_ref
+    async def pull_image(self, image, auth=None) -> str:
+        req = C.PullImageRequest(image=C.ImageSpec(image=image))
+        if auth is not None:
+            req.auth.CopyFrom(auth)
+        return (await self._call("pull_image", self.img.PullImage, req, timeout=300)).image_ref
 
     async def remove_image(self, image):
         await self._call("remove_image", self.img.RemoveImage, C.RemoveImageRequest(image=C.ImageSpec(image=image)))

@@ -99,6 +99,9 @@ class KubeletConfig:
     eviction_max_pod_grace_period: int = 0
     chaos_chance: float = 0.0
     gpu_stats_backend: str = "none"                 # amdsmi|sysfs|fake|auto|none (per-container accelerator stats)
+    oom_watcher: bool = True                        # SystemOOM node events (oom_watcher.go)
+    oom_vmstat_path: str = "/proc/vmstat"
+    oom_kmsg_path: str | None = "/dev/kmsg"
     cpu_capacity: int | None = None
     memory_capacity: int | None = None
     pod_manifest_path: str | None = None            # static pods (--pod-manifest-path)
@@ -222,6 +225,7 @@ class Kubelet:
         self.runtime = RuntimeManager(self.cri, self.dm, config.root_dir, self.recorder, image_pull_qps=config.registry_qps,
                                       image_pull_burst=config.registry_burst, serialize_image_pulls=config.serialize_image_pulls)
         self.runtime.cpu_cfs_quota = config.cpu_cfs_quota
+        self._node_keyring = None     # credentialprovider.node_keyring, read on first use
         if config.seccomp_profile_root:
             self.runtime.seccomp_root = config.seccomp_profile_root
         self.runtime.node_ip, self.runtime.cluster_domain = config.node_ip, config.cluster_domain
@@ -384,6 +388,12 @@ class Kubelet:
                         asyncio.create_task(self._eviction_loop(), name="eviction")]
         if self.cfg.evented_pleg:
             self._tasks.append(asyncio.create_task(self._evented_pleg(), name="pleg-events"))
+        if self.cfg.oom_watcher:    # kubelet.go: oomWatcher.Start(nodeRef)
+            from .oom_watcher import OOMWatcher
+            self.oom_watcher = OOMWatcher(self.recorder, lambda: {"kind": "Node", "metadata": {"name": self.node_name,
+                                                                                               "uid": self.node_name}},
+                                          vmstat=self.cfg.oom_vmstat_path, kmsg=self.cfg.oom_kmsg_path)
+            self._tasks.append(asyncio.create_task(self.oom_watcher.run(), name="oom-watcher"))
         self.volume_manager.start()
         if self.cpu_manager.policy != "none":
             self._tasks.append(asyncio.create_task(self._cpu_reconcile_loop(), name="cpu-manager"))
@@ -1003,7 +1013,8 @@ class Kubelet:
             rt = new_rt if new_rt is not None else await self._cached_status(uid, fresh=True)
         for sb in rt.sandboxes:
             self._sandbox_uid[sb[0]] = uid
-        st = generate_status(pod, rt, self.cfg.node_ip, self.readiness.get(uid, {}), errors, m.now_rfc3339())
+        st = generate_status(pod, rt, self.cfg.node_ip, self.readiness.get(uid, {}), errors, m.now_rfc3339(),
+                             self.runtime.reasons.get(uid))
         prev_phase = (self.status.get(uid) or {}).get("phase")
         self.status.set(pod, st)
         if st["phase"] != prev_phase:
@@ -1223,6 +1234,7 @@ class Kubelet:
         self.rejected.pop(uid, None)
         self.status.forget(uid)
         self.readiness.pop(uid, None)
+        self.runtime.reasons.pop(uid, None)
         self.first_seen.pop(uid, None)
         self.terminated_deleted.discard(uid)
         self.sync_errors.pop(uid, None)
@@ -1250,7 +1262,23 @@ class Kubelet:
                                   "host_path": subpath(vols[vm["name"]], vm.get("subPath", ""),
                                                        f"container {c['name']} mount {vm['name']}").rstrip("/"),
                                   "read_only": bool(vm.get("readOnly"))} for vm in c.get("volumeMounts") or [] if vm["name"] in vols]
-        return {"env": env, "mounts": mounts}
+        return {"env": env, "mounts": mounts, "keyring": await self._pull_keyring(pod)}
+
+    async def _pull_keyring(self, pod: dict):
+        """Pod imagePullSecrets before the node's docker config (credentialprovider
+        MakeDockerKeyring); a missing secret only logs (kubelet_pods.go getPullSecretsForPod)."""
+        from .credentialprovider import UnionKeyring, node_keyring, secrets_keyring
+        if self._node_keyring is None:
+            self._node_keyring = node_keyring(self.cfg.root_dir)
+        secrets = []
+        for ref in (pod.get("spec") or {}).get("imagePullSecrets") or []:
+            s = await self.client.get_or_none("secrets", ref.get("name", ""), m.namespace_of(pod))
+            if s is None:
+                log.warning("unable to retrieve pull secret %s/%s for %s; the image pull may not succeed",
+                            m.namespace_of(pod), ref.get("name"), m.name_of(pod))
+            else:
+                secrets.append(s)
+        return UnionKeyring(secrets_keyring(secrets), self._node_keyring) if secrets else self._node_keyring
 
     async def _env_from(self, pod, vf) -> str:
         from .podcontext import PodContext

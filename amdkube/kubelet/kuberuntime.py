@@ -145,6 +145,27 @@ def apply_event(rt: PodRuntimeStatus, ev, sandbox_ips: dict) -> PodRuntimeStatus
     return new
 
 
+IMAGE_BACKOFF_BASE, IMAGE_BACKOFF_MAX = 10.0, 300.0
+
+
+class StartError(RuntimeError):
+    """A container start failure with its kubelet waiting reason (kubecontainer errors:
+    ErrImagePull, ImagePullBackOff, ErrImageNeverPull, CreateContainerConfigError,
+    CreateContainerError, RunContainerError, PostStartHookError)."""
+
+    def __init__(self, reason: str, message: str):
+        super().__init__(f"{reason}: {message}")
+        self.reason, self.message = reason, message
+
+
+def start_error_reason(e: BaseException) -> tuple[str, str]:
+    if isinstance(e, StartError):
+        return e.reason, e.message
+    if isinstance(e, grpc.RpcError):
+        return "RunContainerError", e.details() or str(e.code())
+    return "CreateContainerConfigError", str(e)
+
+
 class RuntimeManager:
     def __init__(self, cri: CRIClient, device_manager, root_dir: str, recorder=None, image_pull_qps: float = 0,
                  image_pull_burst: int = 10, serialize_image_pulls: bool = True):
@@ -162,6 +183,11 @@ class RuntimeManager:
         self.sandbox_ips: dict[str, str] = {}   # sandbox id -> IP (PodSandboxStatus is asked once per sandbox)
         self.seccomp_root = os.path.join(root_dir, "seccomp")   # --seccomp-profile-root
         self._image_seen: dict[str, float] = {}
+        # reason_cache.go: the last start failure per (pod uid, container) → (reason, message),
+        # shown as the waiting state of a container that has not been created
+        self.reasons: dict[str, dict[str, tuple[str, str]]] = {}
+        # images/puller.go: per-image pull back-off (10 s doubling to 300 s) → ImagePullBackOff
+        self.pull_backoff: dict[str, tuple[float, float]] = {}
         self.legacy = None          # gpu_legacy.AMDGPUManager when the Accelerators gate is on
         self.cpu_manager = None     # cpumanager.CPUManager
         self.node_ip = "127.0.0.1"
@@ -223,7 +249,23 @@ class RuntimeManager:
                                                     host_ipc=bool(spec.get("hostIPC"))))))
 
     # -------------------------------------------------------------- containers
-    async def ensure_image(self, c: dict):
+    async def _pull(self, image: str, keyring):
+        """kuberuntime_image.go PullImage: every matching credential in order, first success
+        wins; anonymous when none matches."""
+        creds = keyring.lookup(image) if keyring is not None else []
+        if not creds:
+            await self.cri.pull_image(image)
+            return
+        err = None
+        for a in creds:
+            try:
+                await self.cri.pull_image(image, a.to_cri(C))
+                return
+            except grpc.RpcError as e:
+                err = e
+        raise err
+
+    async def ensure_image(self, c: dict, keyring=None):
         image = c["image"]
         policy = c.get("imagePullPolicy", "IfNotPresent")
         if policy != "Always" and self._image_seen.get(image, 0.0) > time.monotonic():
@@ -232,22 +274,29 @@ class RuntimeManager:
         if present is not None:
             self._image_seen[image] = time.monotonic() + 30.0
         if policy == "Never" and present is None:
-            raise RuntimeError(f"ErrImageNeverPull: image {image} not present with pull policy Never")
+            raise StartError("ErrImageNeverPull", f'Container image "{image}" is not present with pull policy of Never')
         if present is None or policy == "Always":
+            until, _ = self.pull_backoff.get(image, (0.0, 0.0))
+            if present is None and time.monotonic() < until:
+                raise StartError("ImagePullBackOff", f'Back-off pulling image "{image}"')
             try:
                 if self._pull_limiter is not None:
                     await self._pull_limiter.wait()
                 if self._pull_sem is not None:
                     async with self._pull_sem:
-                        await self.cri.pull_image(image)
+                        await self._pull(image, keyring)
                 else:
-                    await self.cri.pull_image(image)
+                    await self._pull(image, keyring)
+                self.pull_backoff.pop(image, None)
             except grpc.RpcError as e:
                 if present is None:
-                    raise RuntimeError(f"ErrImagePull: {e.details()}")
+                    _, last = self.pull_backoff.get(image, (0.0, 0.0))
+                    delay = min(IMAGE_BACKOFF_MAX, last * 2 if last else IMAGE_BACKOFF_BASE)
+                    self.pull_backoff[image] = (time.monotonic() + delay, delay)
+                    raise StartError("ErrImagePull", e.details() or str(e.code()))
 
     async def start_container(self, pod: dict, c: dict, sid: str, sandbox_cfg, ctx: dict, restart_count: int, init: bool):
-        await self.ensure_image(c)
+        await self.ensure_image(c, ctx.get("keyring"))
         opts = await self.dm.init_container(pod, c)
         if self.legacy is not None:   # Accelerators gate: kubelet_pods.go:486-490 AllocateGPU
             la = self.legacy.allocate(pod, c, self.active_pods() if self.active_pods else [])
@@ -316,7 +365,7 @@ class RuntimeManager:
                 if self.recorder:
                     self.recorder.event(pod, "Warning", "FailedPostStartHook", err)
                 await self.cri.stop_container(cid, 0)
-                raise RuntimeError(f"PostStartHookError: {err}")
+                raise StartError("PostStartHookError", str(err))
         return cid
 
     async def run_handler(self, pod, c, cid, handler: dict, pod_ip: str, timeout: int = 30) -> str:
@@ -393,7 +442,9 @@ class RuntimeManager:
             rc = (cur.restart_count + 1) if cur is not None else 0
             try:
                 await self.start_container(pod, ic, sid, sandbox_cfg, ctx, rc, True)
+                self._clear_reason(uid, ic["name"])
             except Exception as e:
+                self.reasons.setdefault(uid, {})[ic["name"]] = start_error_reason(e)
                 errors.append(f"init container {ic['name']}: {e}")
             return errors
         for c in spec.get("containers") or []:
@@ -421,11 +472,19 @@ class RuntimeManager:
             rc = (cur.restart_count + 1) if cur is not None else 0
             try:
                 await self.start_container(pod, c, sid, sandbox_cfg, ctx, rc, False)
+                self._clear_reason(uid, c["name"])
             except grpc.RpcError as e:
+                self.reasons.setdefault(uid, {})[c["name"]] = start_error_reason(e)
                 errors.append(f"container {c['name']}: {e.details()}")
             except Exception as e:
+                self.reasons.setdefault(uid, {})[c["name"]] = start_error_reason(e)
                 errors.append(f"container {c['name']}: {e}")
         return errors
+
+    def _clear_reason(self, uid: str, name: str):
+        r = self.reasons.get(uid)
+        if r and r.pop(name, None) is not None and not r:
+            del self.reasons[uid]
 
     def _backoff_ok(self, uid, name) -> bool:
         now = time.monotonic()

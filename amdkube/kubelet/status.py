@@ -24,10 +24,13 @@ def _ts(ns: int) -> str | None:
     return time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(ns / 1e9))
 
 
-def container_status(spec_c: dict, rs, ready: bool, will_restart: bool, waiting_reason: str) -> dict:
+def container_status(spec_c: dict, rs, ready: bool, will_restart: bool, waiting_reason: str,
+                     last_error: tuple[str, str] | None = None) -> dict:
     out = {"name": spec_c["name"], "image": spec_c.get("image", ""), "imageID": "", "ready": False, "restartCount": 0}
     if rs is None:
-        out["state"] = {"waiting": {"reason": waiting_reason}}
+        # reason_cache.go: a container that failed to start waits with that failure's reason
+        out["state"] = {"waiting": {"reason": last_error[0], "message": last_error[1]} if last_error
+                        else {"reason": waiting_reason}}
         return out
     out["restartCount"] = rs.restart_count
     out["containerID"] = f"rocshim://{rs.id}"
@@ -41,8 +44,9 @@ def container_status(spec_c: dict, rs, ready: bool, will_restart: bool, waiting_
         if rs.message:
             term["message"] = rs.message
         if will_restart:
-            out["state"] = {"waiting": {"reason": "CrashLoopBackOff" if rs.exit_code else "Completed",
-                                        "message": f"back-off restarting failed container"}}
+            out["state"] = {"waiting": {"reason": last_error[0], "message": last_error[1]} if last_error else
+                            {"reason": "CrashLoopBackOff" if rs.exit_code else "Completed",
+                             "message": "back-off restarting failed container"}}
             out["lastState"] = {"terminated": term}
         else:
             out["state"] = {"terminated": term}
@@ -51,7 +55,10 @@ def container_status(spec_c: dict, rs, ready: bool, will_restart: bool, waiting_
     return out
 
 
-def generate_status(pod: dict, rt, node_ip: str, readiness: dict, errors: list[str], now: str) -> dict:
+def generate_status(pod: dict, rt, node_ip: str, readiness: dict, errors: list[str], now: str,
+                    reasons: dict | None = None) -> dict:
+    """`reasons`: container name → (reason, message) of its last start failure."""
+    reasons = reasons or {}
     spec = pod.get("spec") or {}
     old = pod.get("status") or {}
     policy = spec.get("restartPolicy", "Always")
@@ -68,7 +75,8 @@ def generate_status(pod: dict, rt, node_ip: str, readiness: dict, errors: list[s
             init_failed = True
         if not done:
             init_done = False
-        init_statuses.append(container_status(ic, rs, done, failed and policy != "Never", "PodInitializing"))
+        init_statuses.append(container_status(ic, rs, done, failed and policy != "Never", "PodInitializing",
+                                              reasons.get(ic["name"])))
     running = succeeded = failed_n = waiting = 0
     statuses = []
     all_ready = True
@@ -77,7 +85,8 @@ def generate_status(pod: dict, rt, node_ip: str, readiness: dict, errors: list[s
         if rs is None:
             waiting += 1
             all_ready = False
-            statuses.append(container_status(c, None, False, False, "ContainerCreating" if init_done else "PodInitializing"))
+            statuses.append(container_status(c, None, False, False, "ContainerCreating" if init_done else "PodInitializing",
+                                             reasons.get(c["name"]) if init_done else None))
             continue
         if rs.state == C.CONTAINER_RUNNING:
             running += 1
@@ -93,7 +102,7 @@ def generate_status(pod: dict, rt, node_ip: str, readiness: dict, errors: list[s
             else:
                 failed_n += 1
             restart = policy == "Always" or (policy == "OnFailure" and rs.exit_code != 0)
-            statuses.append(container_status(c, rs, False, restart, ""))
+            statuses.append(container_status(c, rs, False, restart, "", reasons.get(c["name"])))
         else:
             waiting += 1
             all_ready = False

@@ -5,10 +5,19 @@ entrypoint: a native binary, a script, or a directory with a `run` file. Built-i
 map the e2e workloads to amdkube's gfx950 binaries (the reference's cuda-vector-add image,
 test/images/cuda-vector-add, becomes `rocm/vector-add`). Extra images are registered from
 `images.json` in the runtime's state dir or via PullImage of a local path (`file:///...`).
+
+A registry directory (`rocshim --registry-dir`) stands in for remote registries:
+`<dir>/<host[:port]>/<repository>/<tag>/` holds an image tree (entrypoint `run`), and an
+optional `<dir>/<host[:port]>/auth.json` {"users": {"<name>": "<sha256 hex of password>"}}
+makes the registry private: PullImage then needs matching CRI AuthConfig credentials
+(username/password or `auth` = base64 "user:password"), which the kubelet takes from the
+pod's imagePullSecrets or the node's docker config (kubelet/credentialprovider.py).
 """
 from __future__ import annotations
 
+import base64
 import hashlib
+import hmac
 import json
 import os
 import shutil
@@ -69,7 +78,8 @@ class ImageStore:
     runtime's image filesystem), so they occupy space there, report their size and free it
     when removed (kubelet image GC); built-in images are preloaded and cannot be removed."""
 
-    def __init__(self, state_dir: str):
+    def __init__(self, state_dir: str, registry_dir: str | None = None):
+        self.registry_dir = registry_dir
         self.path = os.path.join(state_dir, "images.json")
         self.blob_root = os.path.join(state_dir, "images")
         os.makedirs(self.blob_root, exist_ok=True)
@@ -94,7 +104,43 @@ class ImageStore:
     def image_id(self, name: str) -> str:
         return "sha256:" + hashlib.sha256(json.dumps(self.images[name], sort_keys=True).encode()).hexdigest()
 
-    def pull(self, ref: str) -> str:
+    def _registry_image(self, ref: str) -> tuple[str, str] | None:
+        """(image tree, registry root) of `ref` in the registry directory, or None."""
+        if not self.registry_dir or ref.startswith(("file://", "/")):
+            return None
+        from ..kubelet.credentialprovider import split_image
+        host, port, repo = split_image(ref)
+        last = ref.split("@", 1)[0].rsplit("/", 1)[-1]
+        tag = last.split(":", 1)[1] if ":" in last else "latest"
+        reg = os.path.join(self.registry_dir, host + (f":{port}" if port else ""))
+        tree = os.path.join(reg, repo, tag)
+        return (tree, reg) if os.path.isdir(tree) else None
+
+    @staticmethod
+    def _authorized(reg: str, auth: dict | None) -> bool:
+        f = os.path.join(reg, "auth.json")
+        if not os.path.exists(f):
+            return True                                  # public registry
+        users = (json.load(open(f)).get("users") or {})
+        auth = auth or {}
+        user, pw = auth.get("username", ""), auth.get("password", "")
+        if not user and auth.get("auth"):
+            try:
+                user, _, pw = base64.b64decode(auth["auth"]).decode().partition(":")
+            except Exception:
+                return False
+        want = users.get(user)
+        return bool(user) and want is not None and hmac.compare_digest(hashlib.sha256(pw.encode()).hexdigest(), want)
+
+    def pull(self, ref: str, auth: dict | None = None) -> str:
+        reg = self._registry_image(ref)
+        if reg is not None:
+            tree, root = reg
+            if not self._authorized(root, auth):
+                raise PermissionError(f"pull access denied for {ref}: unauthorized: authentication required")
+            if self.resolve(ref) is None:
+                self._store(normalize(ref), tree)
+            return self.image_id(normalize(ref))
         if self.resolve(ref):
             return self.image_id(self.resolve(ref)[0])
         path = ref[len("file://"):] if ref.startswith("file://") else ref
@@ -114,6 +160,14 @@ class ImageStore:
             self._save()
             return self.image_id(normalize(ref))
         raise KeyError(f"image {ref!r} not found (no registry access; register it in images.json or pull a local path)")
+
+    def _store(self, name: str, tree: str):
+        digest = hashlib.sha256(name.encode()).hexdigest()[:32]
+        blob = os.path.join(self.blob_root, digest)
+        shutil.rmtree(blob, ignore_errors=True)
+        shutil.copytree(tree, blob, symlinks=True)
+        self.images[name] = {"entrypoint": [os.path.join(blob, "run")], "workdir": blob, "blob": blob, "size": _tree_size(blob)}
+        self._save()
 
     def remove(self, ref: str):
         n = normalize(ref) if not ref.startswith("sha256:") else next(

@@ -140,13 +140,13 @@ class Container:
 class RocShim:
     def __init__(self, socket_path: str, state_dir: str, hooks_dir: str = DEFAULT_HOOKS_DIR, isolation: str = "env",
                  cgroup_root: str = "/sys/fs/cgroup/amdkube", dev_root: str = "/dev", network=None,
-                 pod_namespaces: bool = False):
+                 pod_namespaces: bool = False, registry_dir: str | None = None):
         self.socket = socket_path
         self.state_dir = state_dir
         os.makedirs(os.path.join(state_dir, "sandboxes"), exist_ok=True)
         os.makedirs(os.path.join(state_dir, "containers"), exist_ok=True)
         os.makedirs(os.path.join(state_dir, "rootfs"), exist_ok=True)
-        self.images = ImageStore(state_dir)
+        self.images = ImageStore(state_dir, registry_dir)
         self.hooks = HookService(hooks_dir, HANDLERS)
         self.isolation = isolation
         self.network = network or HostNetwork()
@@ -1096,8 +1096,14 @@ class _Images:
         return C.ImageStatusResponse(image=self._img(res[0], self.r.images.image_id(res[0])))
 
     async def PullImage(self, req, ctx):
+        auth = None
+        if req.HasField("auth"):
+            auth = {"username": req.auth.username, "password": req.auth.password, "auth": req.auth.auth}
         try:
-            return C.PullImageResponse(image_ref=self.r.images.pull(req.image.image))
+            ref = await asyncio.to_thread(self.r.images.pull, req.image.image, auth)
+            return C.PullImageResponse(image_ref=ref)
+        except PermissionError as e:
+            await ctx.abort(grpc.StatusCode.UNAUTHENTICATED, str(e))
         except KeyError as e:
             await ctx.abort(grpc.StatusCode.NOT_FOUND, str(e))
 
