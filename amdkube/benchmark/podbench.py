@@ -71,7 +71,11 @@ class PodBench:
     def pod(self, name):
         return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "default", "labels": {"app": "podbench"}},
                 "spec": {"restartPolicy": "Never", "terminationGracePeriodSeconds": 0,
+                         # IfNotPresent, as for the reference's tagged e2e image (k8s.gcr.io/cuda-vector-add:v0.1):
+                         # an untagged image defaults to Always, and every start would then queue
+                         # behind the kubelet's serialized, --registry-qps=5 limited puller
                          "containers": [{"name": "vector-add", "image": self.image, "args": self.args,
+                                         "imagePullPolicy": "IfNotPresent",
                                          "resources": {"limits": {"amd.com/gpu": "1"}}}]}}
 
     async def start(self):
@@ -242,7 +246,10 @@ async def serve(args):
             if cmd.get("cmd") == "quit":
                 break
             if cmd.get("cmd") == "run":
+                cpu0 = lc.cpu_seconds() if hasattr(lc, "cpu_seconds") else {}
                 res = await pb.run(int(cmd.get("steps", 1)))
+                if cpu0:   # CPU seconds each node daemon spent on the steps
+                    res["node_cpu_s"] = {k: round(v - cpu0.get(k, 0.0), 3) for k, v in lc.cpu_seconds().items()}
                 res["scheduler"] = {"scheduled": lc.scheduler.scheduled, "bind_errors": lc.scheduler.bind_errors}
                 print(json.dumps(res), flush=True)
             if cmd.get("cmd") == "schedperf":

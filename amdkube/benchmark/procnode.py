@@ -61,7 +61,9 @@ class ProcessNode:
         env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
         for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
             env.pop(k, None)
-        p = subprocess.Popen([sys.executable, "-m", "amdkube", *args], stdout=log, stderr=subprocess.STDOUT, env=env,
+        prof = os.environ.get("AMDKUBE_PROFILE_DIR")     # cProfile every daemon (<dir>/<name>.prof)
+        pre = ["-m", "cProfile", "-o", os.path.join(prof, f"{name}.prof")] if prof else []
+        p = subprocess.Popen([sys.executable, *pre, "-m", "amdkube", *args], stdout=log, stderr=subprocess.STDOUT, env=env,
                              start_new_session=True, cwd=ROOT)
         self.procs.append(p)
         return p
@@ -106,6 +108,18 @@ class ProcessNode:
                 return node
             await asyncio.sleep(0.05)
         raise TimeoutError(f"node never advertised {n} GPUs (logs in {self.base})")
+
+    def cpu_seconds(self) -> dict:
+        """user+system CPU seconds of each node daemon so far (per-pod cost accounting)."""
+        import psutil
+        out = {}
+        for p in self.procs:
+            try:
+                t = psutil.Process(p.pid).cpu_times()
+                out[" ".join(p.args[2:4]) if "-m" in p.args[:2] else str(p.pid)] = round(t.user + t.system, 3)
+            except psutil.Error:
+                pass
+        return out
 
     async def stop(self):
         for p in reversed(self.procs):     # kubelet, plugin, then rocshim

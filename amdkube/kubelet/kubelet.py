@@ -1235,6 +1235,8 @@ class Kubelet:
         self.status.forget(uid)
         self.readiness.pop(uid, None)
         self.runtime.reasons.pop(uid, None)
+        for k in [k for k in self.runtime.pull_backoff if k[0] == uid]:
+            del self.runtime.pull_backoff[k]
         self.first_seen.pop(uid, None)
         self.terminated_deleted.discard(uid)
         self.sync_errors.pop(uid, None)
@@ -1553,9 +1555,10 @@ class Kubelet:
             self.eviction.evictions += 1
             self.m_evictions.labels("ephemeral-storage").inc()
             self.recorder.event(pod, "Warning", "Evicted", msg)
-            await self.runtime.kill_pod(m.uid_of(pod), 0, pod)
+            # terminal first: a sync racing the kill sees Failed and never restarts the containers
             self.status.set(pod, {"phase": "Failed", "reason": "Evicted", "message": msg,
                                   "conditions": (pod.get("status") or {}).get("conditions") or []})
+            await self.runtime.kill_pod(m.uid_of(pod), 0, pod)
             evicted.append(pod)
         return evicted
 
@@ -1596,7 +1599,8 @@ class Kubelet:
         self.eviction.evictions += 1
         self.m_evictions.labels(t.signal).inc()
         self.recorder.event(victim, "Warning", "Evicted", msg)
-        await self.runtime.kill_pod(m.uid_of(victim), self.eviction.grace_for(victim, t), victim)
+        # terminal first: a sync racing the kill sees Failed and never restarts the containers
         self.status.set(victim, {"phase": "Failed", "reason": "Evicted", "message": msg,
                                  "conditions": (victim.get("status") or {}).get("conditions") or []})
+        await self.runtime.kill_pod(m.uid_of(victim), self.eviction.grace_for(victim, t), victim)
         return victim

@@ -186,8 +186,8 @@ class RuntimeManager:
         # reason_cache.go: the last start failure per (pod uid, container) → (reason, message),
         # shown as the waiting state of a container that has not been created
         self.reasons: dict[str, dict[str, tuple[str, str]]] = {}
-        # images/puller.go: per-image pull back-off (10 s doubling to 300 s) → ImagePullBackOff
-        self.pull_backoff: dict[str, tuple[float, float]] = {}
+        # images/puller.go: pull back-off per (pod uid, image) (10 s doubling to 300 s) → ImagePullBackOff
+        self.pull_backoff: dict[tuple[str, str], tuple[float, float]] = {}
         self.legacy = None          # gpu_legacy.AMDGPUManager when the Accelerators gate is on
         self.cpu_manager = None     # cpumanager.CPUManager
         self.node_ip = "127.0.0.1"
@@ -265,8 +265,9 @@ class RuntimeManager:
                 err = e
         raise err
 
-    async def ensure_image(self, c: dict, keyring=None):
+    async def ensure_image(self, c: dict, keyring=None, uid: str = ""):
         image = c["image"]
+        bkey = (uid, image)        # puller.go: back-off per pod and image
         policy = c.get("imagePullPolicy", "IfNotPresent")
         if policy != "Always" and self._image_seen.get(image, 0.0) > time.monotonic():
             return   # present a moment ago (image GC runs on minutes, not per pod)
@@ -276,7 +277,7 @@ class RuntimeManager:
         if policy == "Never" and present is None:
             raise StartError("ErrImageNeverPull", f'Container image "{image}" is not present with pull policy of Never')
         if present is None or policy == "Always":
-            until, _ = self.pull_backoff.get(image, (0.0, 0.0))
+            until, _ = self.pull_backoff.get(bkey, (0.0, 0.0))
             if present is None and time.monotonic() < until:
                 raise StartError("ImagePullBackOff", f'Back-off pulling image "{image}"')
             try:
@@ -287,17 +288,19 @@ class RuntimeManager:
                         await self._pull(image, keyring)
                 else:
                     await self._pull(image, keyring)
-                self.pull_backoff.pop(image, None)
+                self.pull_backoff.pop(bkey, None)
             except grpc.RpcError as e:
                 if present is None:
-                    _, last = self.pull_backoff.get(image, (0.0, 0.0))
+                    _, last = self.pull_backoff.get(bkey, (0.0, 0.0))
                     delay = min(IMAGE_BACKOFF_MAX, last * 2 if last else IMAGE_BACKOFF_BASE)
-                    self.pull_backoff[image] = (time.monotonic() + delay, delay)
+                    self.pull_backoff[bkey] = (time.monotonic() + delay, delay)
                     raise StartError("ErrImagePull", e.details() or str(e.code()))
 
     async def start_container(self, pod: dict, c: dict, sid: str, sandbox_cfg, ctx: dict, restart_count: int, init: bool):
-        await self.ensure_image(c, ctx.get("keyring"))
+        await self.ensure_image(c, ctx.get("keyring"), pod["metadata"]["uid"])
+        POD_TRACE(pod["metadata"]["uid"], "image_ready")
         opts = await self.dm.init_container(pod, c)
+        POD_TRACE(pod["metadata"]["uid"], "devices_ready")
         if self.legacy is not None:   # Accelerators gate: kubelet_pods.go:486-490 AllocateGPU
             la = self.legacy.allocate(pod, c, self.active_pods() if self.active_pods else [])
             if la["devices"]:
@@ -355,6 +358,7 @@ class RuntimeManager:
                 apparmor_profile=apparmor_profile_name(pod, c["name"]),     # security_context.go:40
                 no_new_privs=not bool(((c.get("securityContext") or {}).get("allowPrivilegeEscalation", True))))))
         cid = await self.cri.create_container(sid, cfg, sandbox_cfg)
+        POD_TRACE(pod["metadata"]["uid"], "container_created")
         await self.cri.start_container(cid)
         POD_TRACE(pod["metadata"]["uid"], "container_started")
         post = ((c.get("lifecycle") or {}).get("postStart"))

@@ -27,6 +27,7 @@ import os
 import shutil
 import signal
 import subprocess
+import threading
 import time
 import uuid
 
@@ -137,6 +138,67 @@ class Container:
         return d
 
 
+class CheckpointWriter:
+    """Sandbox/container checkpoints written off the event loop (the image filesystem of a busy
+    node makes every open/replace/unlink cost ~0.3-1 ms, and a pod costs ~6 of them). One
+    writer thread drains the latest payload per file (None = delete), so a burst of updates to
+    one object costs one write. flush() (stop, tests) waits until everything queued is on disk;
+    a crash can lose at most the updates of the last few milliseconds, which recovery treats
+    like a missed event (the processes themselves are re-adopted from their pid/exit files)."""
+
+    def __init__(self):
+        self._pending: dict[str, bytes | None] = {}
+        self._cv = threading.Condition()
+        self._busy = False
+        self._stop = False
+        self._t = threading.Thread(target=self._run, name="rocshim-ckpt", daemon=True)
+        self._t.start()
+
+    def put(self, path: str, data: bytes | None):
+        with self._cv:
+            self._pending[path] = data
+            self._cv.notify_all()
+
+    def _run(self):
+        while True:
+            with self._cv:
+                while not self._pending and not self._stop:
+                    self._cv.wait()
+                if not self._pending and self._stop:
+                    return
+                batch, self._pending = self._pending, {}
+                self._busy = True
+            for path, data in batch.items():
+                try:
+                    if data is None:
+                        try:
+                            os.unlink(path)
+                        except FileNotFoundError:
+                            pass
+                    else:
+                        tmp = path + ".tmp"
+                        with open(tmp, "wb") as f:
+                            f.write(data)
+                        os.replace(tmp, path)
+                except OSError as e:
+                    log.warning("checkpoint %s: %s", path, e)
+            with self._cv:
+                self._busy = False
+                self._cv.notify_all()
+
+    def flush(self, timeout: float = 10.0):
+        end = time.monotonic() + timeout
+        with self._cv:
+            while (self._pending or self._busy) and time.monotonic() < end:
+                self._cv.wait(0.05)
+
+    def close(self):
+        self.flush()
+        with self._cv:
+            self._stop = True
+            self._cv.notify_all()
+
+
 class RocShim:
     def __init__(self, socket_path: str, state_dir: str, hooks_dir: str = DEFAULT_HOOKS_DIR, isolation: str = "env",
                  cgroup_root: str = "/sys/fs/cgroup/amdkube", dev_root: str = "/dev", network=None,
@@ -147,6 +209,7 @@ class RocShim:
         os.makedirs(os.path.join(state_dir, "containers"), exist_ok=True)
         os.makedirs(os.path.join(state_dir, "rootfs"), exist_ok=True)
         self.images = ImageStore(state_dir, registry_dir)
+        self.ckpt = CheckpointWriter()
         self.hooks = HookService(hooks_dir, HANDLERS)
         self.isolation = isolation
         self.network = network or HostNetwork()
@@ -241,20 +304,16 @@ class RocShim:
             await self.server.stop(0.5)
         for t in list(self._adopt_tasks):
             t.cancel()
+        await asyncio.to_thread(self.ckpt.flush)
 
     # --------------------------------------------------------------- checkpoints
     def _ckpt(self, kind: str, obj):
-        p = os.path.join(self.state_dir, kind, obj.id + ".json")
-        tmp = p + ".tmp"
-        with open(tmp, "w") as f:
-            f.write(json.dumps(obj.to_json(), separators=(",", ":")))   # one-shot C encoder (json.dump is pure Python)
-        os.replace(tmp, p)
+        # encoded now (the state as of this call), written by the checkpoint thread
+        self.ckpt.put(os.path.join(self.state_dir, kind, obj.id + ".json"),
+                      json.dumps(obj.to_json(), separators=(",", ":")).encode())
 
     def _unckpt(self, kind: str, oid: str):
-        try:
-            os.unlink(os.path.join(self.state_dir, kind, oid + ".json"))
-        except FileNotFoundError:
-            pass
+        self.ckpt.put(os.path.join(self.state_dir, kind, oid + ".json"), None)
 
     def _recover(self):
         for name in os.listdir(os.path.join(self.state_dir, "sandboxes")):
@@ -412,7 +471,7 @@ class RocShim:
         self.sandboxes.pop(sid, None)
         self._unckpt("sandboxes", sid)
         self._emit_removed(s)
-        shutil.rmtree(os.path.join(self.state_dir, "rootfs", sid), ignore_errors=True)
+        await asyncio.to_thread(shutil.rmtree, os.path.join(self.state_dir, "rootfs", sid), True)
 
     # --------------------------------------------------------------- containers
     def create_container(self, sid: str, cfg, sandbox_cfg) -> str:
@@ -675,10 +734,7 @@ class RocShim:
                 os.rmdir(self._cgroup_of(c))   # the container's cgroup leaf (empty once it exited)
             except OSError:
                 pass
-        try:
-            os.unlink(os.path.join(self.state_dir, "containers", cid + ".exit"))
-        except FileNotFoundError:
-            pass
+        self.ckpt.put(os.path.join(self.state_dir, "containers", cid + ".exit"), None)   # unlinked off-loop
 
     def update_resources(self, cid: str, lr) -> None:
         """CRI UpdateContainerResources (the CPU manager's shared-pool re-pinning): the new

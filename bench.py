@@ -49,6 +49,8 @@ def main():
     ap.add_argument("--backend", default="auto", help="amdsmi|sysfs|fake|auto")
     ap.add_argument("--no-sched-perf", action="store_true")
     ap.add_argument("--density-nodes", type=int, default=100, help="hollow-node density run (0 = skip)")
+    ap.add_argument("--image", default="rocm/vector-add", help="GPU pod image (CPU rehearsals: busybox)")
+    ap.add_argument("--pod-arg", action="append", default=[], help="GPU pod container argument (repeatable)")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -64,7 +66,8 @@ def main():
                   "TORCHELASTIC_RUN_ID"):
             env.pop(k, None)
         worker = subprocess.Popen([sys.executable, "-m", "amdkube.benchmark.podbench", "--gpus", str(n),
-                                   "--pods-per-gpu", str(a.pods_per_gpu), "--backend", a.backend, "--mode", a.mode],
+                                   "--pods-per-gpu", str(a.pods_per_gpu), "--backend", a.backend, "--mode", a.mode,
+                                   "--image", a.image, "--", *a.pod_arg],
                                   cwd=ROOT, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
         ready = json.loads(worker.stdout.readline() or "{}")
         if not ready.get("ready"):
@@ -155,6 +158,7 @@ def main():
                "p50_startup_all_pods_ms": res["p50_startup_all_pods_ms"], "p99_startup_all_pods_ms": res["p99_startup_all_pods_ms"],
                "p50_node_startup_ms": res["p50_node_startup_ms"], "p50_schedule_ms": res["p50_schedule_ms"],
                "p50_pod_runtime_ms": res["p50_pod_runtime_ms"], "failed_pods": res["failed"],
+               "node_cpu_s": res.get("node_cpu_s"),
                "sched_perf": sched, "density": density}
         if res["failed"]:
             out["failures"] = res["failures"]
