@@ -561,12 +561,14 @@ def kubelet(argv):
     ap.add_argument("--seccomp-profile-root", default=None, help="directory of localhost/<name> seccomp profiles")
     ap.add_argument("--cgroup-driver", default="cgroupfs", choices=("cgroupfs", "systemd"))
     ap.add_argument("--cgroups-per-qos", type=tf, default=True)
+    ap.add_argument("--bootstrap-checkpoint-path", default=None,
+                    help="directory for checkpoints of pods annotated node.kubernetes.io/bootstrap-checkpoint=true")
     # accepted for command-line compatibility; the settings they tune do not exist on this runtime
     for flag in ("--cadvisor-port", "--containerized", "--hairpin-mode", "--non-masquerade-cidr", "--iptables-masquerade-bit",
                  "--iptables-drop-bit", "--make-iptables-util-chains", "--kubelet-cgroups", "--system-cgroups",
                  "--kube-reserved-cgroup", "--system-reserved-cgroup", "--experimental-qos-reserved", "--cloud-config",
                  "--streaming-connection-idle-timeout", "--master-service-namespace", "--require-kubeconfig",
-                 "--init-config-dir", "--bootstrap-checkpoint-path", "--experimental-mounter-path",
+                 "--init-config-dir", "--experimental-mounter-path",
                  "--experimental-check-node-capabilities-before-mount", "--experimental-kernel-memcg-notification",
                  "--experimental-allocatable-ignore-eviction", "--enable-custom-metrics", "--contention-profiling",
                  "--really-crash-for-testing", "--authentication-token-webhook-cache-ttl",
@@ -602,6 +604,7 @@ def kubelet(argv):
                         relist_period=a.pleg_relist_period, max_pods=a.max_pods, node_labels=labels,
                         register_with_taints=taints, feature_gates=a.feature_gates, chaos_chance=a.chaos_chance,
                         pod_manifest_path=a.pod_manifest_path, file_check_frequency=a.file_check_frequency,
+                        bootstrap_checkpoint_path=a.bootstrap_checkpoint_path,
                         gpu_stats_backend=a.gpu_stats_backend,
                         cluster_dns=[x for x in a.cluster_dns.split(",") if x], cluster_domain=a.cluster_domain,
                         resolv_conf=a.resolv_conf,

@@ -105,6 +105,7 @@ class KubeletConfig:
     cpu_capacity: int | None = None
     memory_capacity: int | None = None
     pod_manifest_path: str | None = None            # static pods (--pod-manifest-path)
+    bootstrap_checkpoint_path: str | None = None    # --bootstrap-checkpoint-path (checkpoint.py)
     file_check_frequency: float = 20.0              # kubeletconfig FileCheckFrequency
     apparmor_fs: str | None = None                  # securityfs apparmor dir (None: discover from /proc/mounts)
     cluster_dns: list = field(default_factory=list)   # --cluster-dns
@@ -226,6 +227,10 @@ class Kubelet:
                                       image_pull_burst=config.registry_burst, serialize_image_pulls=config.serialize_image_pulls)
         self.runtime.cpu_cfs_quota = config.cpu_cfs_quota
         self._node_keyring = None     # credentialprovider.node_keyring, read on first use
+        from .checkpoint import PodCheckpointManager
+        self.pod_checkpoints = PodCheckpointManager(config.bootstrap_checkpoint_path) \
+            if config.bootstrap_checkpoint_path else None
+        self.restored: set[str] = set()   # UIDs started from checkpoints, not yet confirmed by the API
         if config.seccomp_profile_root:
             self.runtime.seccomp_root = config.seccomp_profile_root
         self.runtime.node_ip, self.runtime.cluster_domain = config.node_ip, config.cluster_domain
@@ -397,7 +402,8 @@ class Kubelet:
         self.volume_manager.start()
         if self.cpu_manager.policy != "none":
             self._tasks.append(asyncio.create_task(self._cpu_reconcile_loop(), name="cpu-manager"))
-        if self.cfg.pod_manifest_path or self.cfg.manifest_url:
+        restored = self._restore_checkpoints() if self.pod_checkpoints is not None else 0
+        if self.cfg.pod_manifest_path or self.cfg.manifest_url or restored:
             # static pods run with or without an apiserver (kubeadm: the apiserver IS a static
             # pod), so registration is retried in the background (kubelet_node_status.go
             # registerWithAPIServer: exponential back-off up to 7 s)
@@ -426,6 +432,8 @@ class Kubelet:
         self.informer.add_handler(on_add=self._on_pod_add, on_update=self._on_pod_update, on_delete=self._on_pod_delete)
         self.informer.start()
         await self.informer.wait_synced(30)
+        if self.restored:
+            self._reconcile_restored()
         self._tasks.append(asyncio.create_task(self._node_status_loop(), name="node-status"))
         self._static_dirty.set()   # create mirror pods now that the API is there
 
@@ -614,6 +622,9 @@ class Kubelet:
             return
         uid = m.uid_of(pod)
         self.pods[uid] = pod
+        self.restored.discard(uid)
+        if self.pod_checkpoints is not None:
+            self.pod_checkpoints.write_pod(pod)
         self.first_seen.setdefault(uid, time.time())
         POD_TRACE(uid, "kubelet_seen")
         self.dispatch(uid)
@@ -623,6 +634,8 @@ class Kubelet:
             self.mirrors[(m.namespace_of(pod), m.name_of(pod))] = pod
             return
         self.pods[m.uid_of(pod)] = pod
+        if self.pod_checkpoints is not None and (old is None or _semantic(old) != _semantic(pod)):
+            self.pod_checkpoints.write_pod(pod)
         # only semantic changes wake the pod worker (reference pkg/kubelet/config/config.go
         # checkAndUpdatePod / podsDifferSemantically): the kubelet's own status writes echo back
         # through the watch and must not trigger another runtime sync
@@ -638,7 +651,34 @@ class Kubelet:
             return
         uid = m.uid_of(pod)
         self.pods.pop(uid, None)
+        if self.pod_checkpoints is not None:
+            self.pod_checkpoints.delete_pod(pod)
         self.dispatch(uid)
+
+    def _restore_checkpoints(self) -> int:
+        """Checkpointed pods run before the API server is reachable (treated as new pods)."""
+        n = 0
+        for pod in self.pod_checkpoints.load_pods():
+            uid = m.uid_of(pod)
+            if uid in self.pods:
+                continue
+            self.restored.add(uid)
+            self.pods[uid] = pod
+            self.first_seen.setdefault(uid, time.time())
+            self.dispatch(uid)
+            n += 1
+        if n:
+            log.info("restored %d pod(s) from bootstrap checkpoints in %s", n, self.pod_checkpoints.path)
+        return n
+
+    def _reconcile_restored(self):
+        """The API server's pod list is the truth once synced: restored pods it does not know
+        were deleted while the kubelet was away."""
+        for uid in list(self.restored):
+            pod = self.pods.get(uid)
+            self.restored.discard(uid)
+            if pod is not None:
+                self._on_pod_delete(pod)
 
     # ============================================================= static pods
     def _read_manifests(self) -> dict[str, dict]:
