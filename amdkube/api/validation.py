@@ -10,6 +10,7 @@ here, against node state in the registry).
 from __future__ import annotations
 
 import json
+import re
 
 from .helpers import HEALTHY, UNHEALTHY, is_extended_resource_name, is_native_resource
 from .labels import (SelectorError, is_dns1123_label, is_dns1123_subdomain, is_qualified_name,
@@ -183,6 +184,51 @@ def _validate_node_selector_terms(terms, path) -> list[str]:
     return errs
 
 
+_CONFIG_KEY_RE = re.compile(r"^[-._a-zA-Z0-9]+$")
+
+
+def is_config_map_key(k: str) -> list[str]:
+    """validation.go IsConfigMapKey: a plain file name, never '.', '..' or '..'-prefixed."""
+    if not k or len(k) > 253:
+        return ["must be no more than 253 characters and non-empty"]
+    if not _CONFIG_KEY_RE.match(k):
+        return ["a valid config key must consist of alphanumeric characters, '-', '_' or '.'"]
+    if k in (".", "..") or k.startswith(".."):
+        return ["must not be '.' or '..' and must not start with '..'"]
+    return []
+
+
+def validate_local_descending_path(p: str, path: str) -> list[str]:
+    """validation.go validateLocalDescendingPath: relative, and no '..' element."""
+    if not p:
+        return [f"{path}: Required value"]
+    errs = []
+    if p.startswith("/"):
+        errs.append(f"{path}: Invalid value: {p!r}: must be a relative path")
+    if ".." in p.split("/"):
+        errs.append(f"{path}: Invalid value: {p!r}: must not contain '..'")
+    return errs
+
+
+def _validate_volume_items(v: dict, path: str) -> list[str]:
+    """validateKeyToPath / validateDownwardAPIVolumeFile / validateProjectionSources: every file
+    a secret, configMap, downwardAPI or projected volume writes stays inside the volume."""
+    errs = []
+    for src_key in ("secret", "configMap"):
+        for i, it in enumerate((v.get(src_key) or {}).get("items") or []):
+            if not it.get("key"):
+                errs.append(f"{path}.{src_key}.items[{i}].key: Required value")
+            errs += validate_local_descending_path(it.get("path") or "", f"{path}.{src_key}.items[{i}].path")
+    for i, it in enumerate((v.get("downwardAPI") or {}).get("items") or []):
+        errs += validate_local_descending_path(it.get("path") or "", f"{path}.downwardAPI.items[{i}].path")
+    for j, srcs in enumerate((v.get("projected") or {}).get("sources") or []):
+        for src_key in ("secret", "configMap", "downwardAPI"):
+            for i, it in enumerate((srcs.get(src_key) or {}).get("items") or []):
+                errs += validate_local_descending_path(it.get("path") or "",
+                                                       f"{path}.projected.sources[{j}].{src_key}.items[{i}].path")
+    return errs
+
+
 def validate_pod_spec(spec: dict, path="spec") -> list[str]:
     errs = []
     containers = spec.get("containers") or []
@@ -207,6 +253,7 @@ def validate_pod_spec(spec: dict, path="spec") -> list[str]:
         if n in vols:
             errs.append(f"{path}.volumes[{i}].name: Duplicate value: {n!r}")
         vols.add(n)
+        errs += _validate_volume_items(v, f"{path}.volumes[{i}]")
     for kind, lst in (("initContainers", inits), ("containers", containers)):
         for i, c in enumerate(lst):
             for j, m in enumerate(c.get("volumeMounts") or []):
@@ -364,6 +411,16 @@ def validate_generic_namespaced(obj, old=None):
     return validate_object_meta(obj, True)
 
 
+def validate_config_data(obj, old=None):
+    """ValidateConfigMap / ValidateSecret: every data key is a valid config key (it becomes a
+    file name in configMap and secret volumes)."""
+    errs = validate_object_meta(obj, True)
+    for field in ("data", "binaryData", "stringData"):
+        for k in (obj.get(field) or {}):
+            errs += [f"{field}[{k}]: Invalid value: {k!r}: {e}" for e in is_config_map_key(k)]
+    return errs
+
+
 def validate_event(ev, old=None):
     errs = validate_object_meta(ev, True)
     if not (ev.get("involvedObject") or {}).get("kind"):
@@ -389,6 +446,8 @@ def _validate_crd(obj, old=None):
 
 register_hooks("CustomResourceDefinition", "apiextensions.k8s.io/v1beta1", validator=_validate_crd)
 register_hooks("Service", defaulter=default_service, validator=validate_service)
-for _k in ("ConfigMap", "Secret", "ServiceAccount", "Endpoints", "LimitRange", "ResourceQuota",
+register_hooks("ConfigMap", validator=validate_config_data)
+register_hooks("Secret", validator=validate_config_data)
+for _k in ("ServiceAccount", "Endpoints", "LimitRange", "ResourceQuota",
            "PersistentVolumeClaim"):
     register_hooks(_k, validator=validate_generic_namespaced)

@@ -105,15 +105,15 @@ class Authenticator:
             u = await self.webhook.authenticate(tok)
         return self._with_authenticated(u) if u is not None else None
 
-    async def authenticate_async(self, headers, peercert: dict | None = None) -> dict:
+    async def authenticate_async(self, headers, peercert: dict | None = None, peer_der: bytes | None = None) -> dict:
         h = headers.get("Authorization", "")
         if h.startswith("Bearer ") and (self.oidc is not None or self.webhook is not None) and \
-                self._from_request_headers(headers, peercert) is None:
+                self._from_request_headers(headers, peercert, peer_der) is None:
             u = await self.authenticate_token_async(h[7:].strip())
             if u is None:
                 raise m.unauthorized()
             return u
-        return self.authenticate(headers, peercert)
+        return self.authenticate(headers, peercert, peer_der)
 
     def authenticate_token(self, tok: str) -> dict | None:
         u = self.tokens.get(tok)
@@ -175,13 +175,22 @@ class Authenticator:
         --requestheader-client-ca-file (and, with --requestheader-allowed-names, carrying one of
         those CNs) may assert the user in X-Remote-User / X-Remote-Group / X-Remote-Extra-*."""
         import ssl as _ssl
+        from ..utils.crypto import x509_pem_to_der
         dec = _ssl._ssl._test_decode_cert(ca_file)
-        self.requestheader = {"issuer": dec.get("subject"), "allowed": set(allowed_names or ()),
+        with open(ca_file, "rb") as f:
+            cas = x509_pem_to_der(f.read())
+        self.requestheader = {"issuer": dec.get("subject"), "allowed": set(allowed_names or ()), "ca_der": cas,
                               "users": list(username_headers), "groups": list(group_headers), "extra": list(extra_prefixes)}
 
-    def _from_request_headers(self, headers, peercert) -> dict | None:
+    def _from_request_headers(self, headers, peercert, peer_der: bytes | None = None) -> dict | None:
+        """The peer certificate must be SIGNED by the requestheader CA (headerrequest verifies
+        the chain against that pool alone): matching the issuer's name is not enough when the
+        client CA carries the same subject."""
+        from ..utils.crypto import x509_signed_by
         rh = self.requestheader
         if rh is None or not peercert or peercert.get("issuer") != rh["issuer"]:
+            return None
+        if peer_der is None or not any(x509_signed_by(peer_der, ca) for ca in rh.get("ca_der") or ()):
             return None
         cn = (self.from_peer_cert(peercert) or {}).get("name")
         if rh["allowed"] and cn not in rh["allowed"]:
@@ -198,8 +207,8 @@ class Authenticator:
                     extra.setdefault(k[len(pre):].lower(), []).extend(getall(k, []) if getall else [headers.get(k)])
         return {"name": name, "uid": "", "groups": groups, "extra": extra}
 
-    def authenticate(self, headers, peercert: dict | None = None) -> dict:
-        u = self._from_request_headers(headers, peercert)
+    def authenticate(self, headers, peercert: dict | None = None, peer_der: bytes | None = None) -> dict:
+        u = self._from_request_headers(headers, peercert, peer_der)
         if u is not None:
             return self._with_authenticated(u)
         h = headers.get("Authorization", "")

@@ -165,9 +165,12 @@ class OIDCAuthenticator:
         aud = claims.get("aud")
         if self.client_id not in (aud if isinstance(aud, list) else [aud]):
             return None
-        if claims.get("exp") is not None and claims["exp"] < time.time():
+        # oidc.go:255-270 (go-oidc VerifyJWT): a token without exp never expires, so it is refused;
+        # an email username needs an explicit boolean email_verified=true
+        exp = claims.get("exp")
+        if not isinstance(exp, (int, float)) or isinstance(exp, bool) or exp < time.time():
             return None
-        if self.username_claim == "email" and claims.get("email_verified") is False:
+        if self.username_claim == "email" and claims.get("email_verified") is not True:
             return None
         name = claims.get(self.username_claim)
         if not name:
@@ -240,11 +243,23 @@ class ABACAuthorizer:
                 self.policies.append(p.get("spec", p))
 
     @staticmethod
-    def _matches(p: dict, a) -> bool:
-        u = a.user
-        user_ok = p.get("user") and (p["user"] == "*" or p["user"] == u.get("name"))
-        group_ok = p.get("group") and (p["group"] == "*" or p["group"] in (u.get("groups") or []))
-        if not (user_ok or group_ok):
+    def _subject_matches(p: dict, u: dict) -> bool:
+        """abac.go subjectMatches: every subject field the policy sets must match (user AND
+        group when both are set), and at least one must be set."""
+        matched = False
+        if p.get("user"):
+            if p["user"] != "*" and p["user"] != u.get("name"):
+                return False
+            matched = True
+        if p.get("group"):
+            if p["group"] != "*" and p["group"] not in (u.get("groups") or []):
+                return False
+            matched = True
+        return matched
+
+    @classmethod
+    def _matches(cls, p: dict, a) -> bool:
+        if not cls._subject_matches(p, a.user):
             return False
         if p.get("readonly") and a.verb not in ("get", "list", "watch"):
             return False

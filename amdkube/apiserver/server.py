@@ -463,9 +463,18 @@ class APIServer:
                 "resources": res}
 
     # ------------------------------------------------------------------ auth
+    @staticmethod
+    def _peer_der(tr) -> bytes | None:
+        so = tr.get_extra_info("ssl_object") if tr is not None else None
+        try:
+            return so.getpeercert(binary_form=True) if so is not None else None
+        except (ValueError, AttributeError):
+            return None
+
     def _authenticate(self, request):
-        pc = request.transport.get_extra_info("peercert") if self.tls and request.transport is not None else None
-        return self.authn.authenticate(request.headers, pc)
+        tr = request.transport
+        pc = tr.get_extra_info("peercert") if self.tls and tr is not None else None
+        return self.authn.authenticate(request.headers, pc, self._peer_der(tr) if pc else None)
 
     UNSECURED = {"name": "system:unsecured", "uid": "", "groups": ["system:masters", "system:authenticated"]}
 
@@ -475,7 +484,7 @@ class APIServer:
                 (tr.get_extra_info("sockname") or (None, None))[1] == self.insecure_port:
             return self.UNSECURED
         pc = tr.get_extra_info("peercert") if self.tls and tr is not None else None
-        return await self.authn.authenticate_async(request.headers, pc)
+        return await self.authn.authenticate_async(request.headers, pc, self._peer_der(tr) if pc else None)
 
     async def _authorize(self, user, verb, resource, group="", ns="", name="", sub=""):
         ok, _ = await self.authz.authorize_async(Attributes(user, verb, group, resource, sub, ns, name))

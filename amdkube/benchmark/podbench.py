@@ -223,17 +223,23 @@ async def serve(args):
     logging.basicConfig(level=logging.WARNING, stream=sys.stderr)
     if args.procs:
         from amdkube.benchmark.procnode import ProcessNode
-        lc = ProcessNode(args.backend, args.gpus, relist_period=1.0, health_probe=args.health_probe)
+        lc = ProcessNode(args.backend, args.gpus, relist_period=1.0, health_probe=args.health_probe,
+                         isolation=args.isolation)
     else:
         lc = LocalCluster(gpus=args.backend, n_gpus=args.gpus, relist_period=1.0, with_controllers=False,
-                          health_probe=args.health_probe)
+                          health_probe=args.health_probe, isolation=args.isolation)
     await lc.start()
     await lc.wait_gpus(args.gpus, 60)
     node = await lc.client.get("nodes", lc.node_name)
     devs = list(((node["status"].get("extendedResources") or {}).get("amd.com/gpu") or {}).get("resources") or {})
     pb = PodBench(lc, args.gpus, args.pods_per_gpu, args.image, args.args, args.mode)
     await pb.start()
-    print(json.dumps({"ready": True, "gpus": devs, "backend": lc.backend.name if lc.backend else "none"}), flush=True)
+    iso = getattr(lc, "isolation", None)
+    if iso == "auto":
+        from amdkube.runtime.rocshim import probe_isolation, resolve_isolation
+        iso = resolve_isolation("auto", probe_isolation())
+    print(json.dumps({"ready": True, "gpus": devs, "backend": lc.backend.name if lc.backend else "none", "isolation": iso}),
+          flush=True)
     loop = asyncio.get_running_loop()
     reader = asyncio.StreamReader()
     await loop.connect_read_pipe(lambda: asyncio.StreamReaderProtocol(reader), sys.stdin)
@@ -270,6 +276,7 @@ def main():
     ap.add_argument("--backend", default="auto")
     ap.add_argument("--image", default="rocm/vector-add")
     ap.add_argument("--health-probe", default="none")
+    ap.add_argument("--isolation", default=None, help="rocshim device isolation (default: auto on real GPUs, env on fake)")
     ap.add_argument("args", nargs="*", default=[])
     asyncio.run(serve(ap.parse_args()))
 

@@ -47,8 +47,11 @@ class _SchedulerStats:
 
 class ProcessNode:
     def __init__(self, backend: str = "auto", n_gpus: int | None = None, node_name: str = "mi355x-node-0",
-                 relist_period: float = 1.0, health_probe: str = "none", scheduler_process: bool = True):
+                 relist_period: float = 1.0, health_probe: str = "none", scheduler_process: bool = True,
+                 isolation: str | None = None):
         self.scheduler_process = scheduler_process
+        # real GPUs: the strongest device isolation the node offers; the fake backend: advisory env
+        self.isolation = isolation or ("env" if backend in ("fake", "none") else "auto")
         self.backend_name, self.n_gpus, self.node_name = backend, n_gpus, node_name
         self.relist_period, self.health_probe = relist_period, health_probe
         self.base = tempfile.mkdtemp(prefix="ak-proc-", dir="/tmp")
@@ -80,7 +83,7 @@ class ProcessNode:
         sock = os.path.join(b, "rocshim.sock")
         plugins = os.path.join(b, "plugins")
         self._spawn("rocshim", ["rocshim", "--listen", sock, "--state-dir", os.path.join(b, "rocshim"),
-                                "--hooks-dir", os.path.join(b, "hooks.d")])
+                                "--hooks-dir", os.path.join(b, "hooks.d"), "--isolation", self.isolation])
         dp = ["amd-device-plugin", "--backend", self.backend_name, "--plugins-dir", plugins, "--health-interval", "5",
               "--health-probe", self.health_probe]
         if self.n_gpus:

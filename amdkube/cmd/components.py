@@ -680,7 +680,8 @@ def rocshim(argv):
     ap.add_argument("--listen", default="/var/run/amdkube/rocshim.sock")
     ap.add_argument("--state-dir", default="/var/lib/amdkube/rocshim")
     ap.add_argument("--hooks-dir", default="/usr/share/containers/docker/hooks.d")
-    ap.add_argument("--isolation", default="env", choices=("env", "namespaces"))
+    ap.add_argument("--isolation", default="auto", choices=("env", "landlock", "userns", "namespaces", "auto"),
+                    help="device isolation: auto probes the node (namespaces > userns > landlock > env)")
     ap.add_argument("--network-plugin", default="host", choices=("host", "cni", "kubenet"),
                     help="kubenet: pod network namespaces on the amdkube-bridge CNI plugin (cbr0 + host-local IPAM)")
     ap.add_argument("--pod-namespaces", action="store_true",
@@ -936,7 +937,7 @@ def local_up(argv):
     ap.add_argument("--port", type=int, default=8080)
     ap.add_argument("--backend", default="auto")
     ap.add_argument("--max-gpus", type=int, default=None)
-    ap.add_argument("--isolation", default="env")
+    ap.add_argument("--isolation", default="auto")
     ap.add_argument("--no-gpus", action="store_true")
     ap.add_argument("--exporter-port", type=int, default=9400)
     a = ap.parse_args(argv)

@@ -32,14 +32,22 @@ class PodCheckpointManager:
         return os.path.join(self.path, f"{POD_PREFIX}{pod['metadata']['uid']}.yaml")
 
     def write_pod(self, pod: dict) -> bool:
+        """Checkpoint an annotated pod; a pod that no longer carries the annotation loses its
+        checkpoint (it must not be restored from a stale copy). I/O errors are logged, never
+        raised into the informer handler."""
         if not self.wants(pod):
+            self.delete_pod(pod)
             return False
         p = self._file(pod)
         body = {k: v for k, v in pod.items() if k != "status"}   # the spec is what restarts it
         tmp = p + ".tmp"
-        with open(tmp, "w") as f:
-            json.dump(body, f)        # JSON is YAML; the reference writes the same encoding
-        os.replace(tmp, p)
+        try:
+            with open(tmp, "w") as f:
+                json.dump(body, f)        # JSON is YAML; the reference writes the same encoding
+            os.replace(tmp, p)
+        except OSError as e:
+            log.error("writing bootstrap checkpoint %s: %s", p, e)
+            return False
         return True
 
     def delete_pod(self, pod: dict):
@@ -47,6 +55,8 @@ class PodCheckpointManager:
             os.unlink(self._file(pod))
         except FileNotFoundError:
             pass
+        except OSError as e:
+            log.error("removing bootstrap checkpoint %s: %s", self._file(pod), e)
 
     def load_pods(self) -> list[dict]:
         out = []

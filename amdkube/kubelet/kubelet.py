@@ -231,6 +231,7 @@ class Kubelet:
         self.pod_checkpoints = PodCheckpointManager(config.bootstrap_checkpoint_path) \
             if config.bootstrap_checkpoint_path else None
         self.restored: set[str] = set()   # UIDs started from checkpoints, not yet confirmed by the API
+        self._ckpt_chain = None           # the newest queued bootstrap-checkpoint write
         if config.seccomp_profile_root:
             self.runtime.seccomp_root = config.seccomp_profile_root
         self.runtime.node_ip, self.runtime.cluster_domain = config.node_ip, config.cluster_domain
@@ -624,7 +625,7 @@ class Kubelet:
         self.pods[uid] = pod
         self.restored.discard(uid)
         if self.pod_checkpoints is not None:
-            self.pod_checkpoints.write_pod(pod)
+            self._checkpoint_io(self.pod_checkpoints.write_pod, pod)
         self.first_seen.setdefault(uid, time.time())
         POD_TRACE(uid, "kubelet_seen")
         self.dispatch(uid)
@@ -635,7 +636,7 @@ class Kubelet:
             return
         self.pods[m.uid_of(pod)] = pod
         if self.pod_checkpoints is not None and (old is None or _semantic(old) != _semantic(pod)):
-            self.pod_checkpoints.write_pod(pod)
+            self._checkpoint_io(self.pod_checkpoints.write_pod, pod)   # removes it when the annotation went away
         # only semantic changes wake the pod worker (reference pkg/kubelet/config/config.go
         # checkAndUpdatePod / podsDifferSemantically): the kubelet's own status writes echo back
         # through the watch and must not trigger another runtime sync
@@ -652,8 +653,20 @@ class Kubelet:
         uid = m.uid_of(pod)
         self.pods.pop(uid, None)
         if self.pod_checkpoints is not None:
-            self.pod_checkpoints.delete_pod(pod)
+            self._checkpoint_io(self.pod_checkpoints.delete_pod, pod)
         self.dispatch(uid)
+
+    def _checkpoint_io(self, fn, pod):
+        """Bootstrap-checkpoint writes run off the event loop, in order per kubelet (one chain of
+        executor jobs), so informer handlers never block on the disk."""
+        prev = self._ckpt_chain
+        loop = asyncio.get_running_loop()
+
+        async def step():
+            if prev is not None:
+                await prev
+            await loop.run_in_executor(None, fn, pod)
+        self._ckpt_chain = loop.create_task(step())
 
     def _restore_checkpoints(self) -> int:
         """Checkpointed pods run before the API server is reachable (treated as new pods)."""

@@ -51,6 +51,20 @@ def atomic_write(path: str, data: bytes, mode: int | None = None):
             pass
 
 
+def volume_file(d: str, rel: str) -> str:
+    """The host path of a file a secret/configMap/projected/downwardAPI volume writes: `rel` must
+    be relative with no '..' element (validateLocalDescendingPath), and the resolved target —
+    after any symlink already inside the volume — must stay under the volume directory. The API
+    server validates the same rule; this is the kubelet's own check on what it writes as root."""
+    if not rel or rel.startswith("/") or ".." in rel.split("/"):
+        raise ValueError(f"volume item path {rel!r} must be relative and must not contain '..'")
+    base = os.path.realpath(d)
+    target = os.path.realpath(os.path.join(base, rel))
+    if os.path.commonpath([base, target]) != base or target == base:
+        raise ValueError(f"volume item path {rel!r} escapes the volume directory")
+    return target
+
+
 def expand(s: str, env: dict[str, str]) -> str:
     """$(VAR) → env[VAR] when defined, else left as written; $$ → $."""
     def rep(mt):
@@ -160,7 +174,7 @@ class PodContext:
                     continue
                 raise RuntimeError(f"{what}: key {it['key']!r} not found in {kind[:-1]} {name!r}")
             val = data[it["key"]]
-            atomic_write(os.path.join(d, it["path"]), base64.b64decode(val) if kind == "secrets" else val.encode(),
+            atomic_write(volume_file(d, it.get("path") or ""), base64.b64decode(val) if kind == "secrets" else val.encode(),
                          it.get("mode", ref.get("defaultMode", default_mode)))
 
     async def _downward(self, pod, d, items, default_mode):
@@ -174,7 +188,7 @@ class PodContext:
                 val = resource_value(pod, it["resourceFieldRef"].get("containerName", ""), it["resourceFieldRef"], alloc)
             else:
                 val = ""
-            atomic_write(os.path.join(d, it["path"]), val.encode(), it.get("mode", default_mode))
+            atomic_write(volume_file(d, it.get("path") or ""), val.encode(), it.get("mode", default_mode))
 
     async def _git_repo(self, d: str, spec: dict, what: str) -> str:
         """git_repo.go SetUpAt: clone once into `directory` (or a subdirectory named after the

@@ -27,7 +27,7 @@ log = logging.getLogger("amdkube.localcluster")
 class LocalCluster:
     def __init__(self, gpus: str = "fake", n_gpus: int | None = None, node_name: str = "mi355x-node-0",
                  base_dir: str | None = None, with_controllers: bool = True, relist_period: float = 1.0,
-                 node_status_update_frequency: float = 10.0, scheduler_kw: dict | None = None, isolation: str = "env",
+                 node_status_update_frequency: float = 10.0, scheduler_kw: dict | None = None, isolation: str | None = None,
                  health_probe: str = "none", kubelet_kw: dict | None = None, with_kubelet: bool = True,
                  partition: str | None = None, resource_naming: str = "single", api_kw: dict | None = None,
                  controllers_kw: dict | None = None, shim_kw: dict | None = None):
@@ -41,7 +41,9 @@ class LocalCluster:
         self.nsuf = node_status_update_frequency
         self.scheduler_kw = scheduler_kw or {}
         self.kubelet_kw = kubelet_kw or {}
-        self.isolation = isolation
+        # a node on real GPUs isolates devices with the strongest mechanism it has (rocshim
+        # isolation=auto); the fake backend keeps the advisory env mode unless asked
+        self.isolation = isolation or ("env" if gpus in ("fake", "none") else "auto")
         self.health_probe = health_probe
         self.with_kubelet = with_kubelet
         self.api_kw, self.controllers_kw, self.shim_kw = api_kw or {}, controllers_kw or {}, shim_kw or {}

@@ -8,11 +8,27 @@ plugin's InitContainer response as carried in the CRI ContainerConfig:
   * env  — ROCR_VISIBLE_DEVICES from the plugin; inherited HIP/CUDA/ROCR visibility
            variables are scrubbed so a container sees exactly its assigned GPUs, and a
            container with no GPU devices gets HIP_VISIBLE_DEVICES=-1 (sees none);
-  * devices — /dev/kfd + /dev/dri/renderD<N>: in `isolation=namespaces` mode (root) the
-           native `amdkube-nsexec` helper gives the container a private /dev/dri holding
-           only its render nodes and joins a cgroup-v2 leaf with cpu/memory limits; in the
-           default `env` mode (unprivileged) the device list is validated and recorded.
-The runtime handler for a container is chosen by the hooks.d service (F21 semantics).
+  * devices — /dev/kfd + /dev/dri/renderD<N>, enforced by the kernel through the native
+           `amdkube-nsexec` launcher (native/devguard.h), strongest mechanism first
+           (`isolation=auto` probes the node once, `amdkube-nsexec --probe`):
+           `namespaces` (root): a private mount namespace whose /dev/dri holds only the
+                 container's render nodes, /dev/kfd masked for non-GPU containers, a cgroup-v2
+                 leaf with cpu/memory limits and a BPF device filter (226:* only the kept
+                 minors, kfd only with a GPU), Landlock layered under it, the capability
+                 bounding set cut to Docker's default, no_new_privs;
+           `userns` (unprivileged, user namespaces enabled): the same private /dev/dri in a
+                 mount namespace owned by a user namespace;
+           `landlock` (unprivileged, no user namespaces — the MI355X gpurun box): a Landlock
+                 ruleset under which every GPU node the container was not given is refused
+                 and mknod of device nodes fails; the `rocm` handler's devview preload makes
+                 those nodes read as absent, which ROCr skips (an EACCES it would not);
+           `env`: visibility variables only (advisory).
+The runtime handler for a container is chosen by the hooks.d service (F21 semantics). As the
+reference's `nvidia` OCI runtime is what makes a GPU usable inside a container
+(docker_container.go:132,157), the `rocm` handler is what gives one its GPUs here: the
+device view of the CRI device list plus the ROCm user space (an image rootfs gets /opt/rocm
+bound in read-only). Under `default` (runc semantics) the CRI devices are passed as they are,
+with no ROCm injection and no device-view preload.
 
 State (sandboxes + containers) is checkpointed as JSON so a restarted rocshim re-adopts
 running pods instead of orphaning them; exit codes of re-adopted processes
@@ -43,6 +59,59 @@ log = logging.getLogger("amdkube.rocshim")
 RUNTIME_NAME = "rocshim"
 RUNTIME_VERSION = "0.1.0"
 HANDLERS = {"rocm", "default"}
+ISOLATION_MODES = ("env", "landlock", "userns", "namespaces", "auto")
+DEVVIEW_LIB = os.path.join(os.path.dirname(NATIVE_BIN), "lib", "libamdkube-devview.so")
+# Docker's default capability set: what a non-privileged container keeps in guarded modes
+DEFAULT_CAPS = ("CHOWN", "DAC_OVERRIDE", "FSETID", "FOWNER", "MKNOD", "NET_RAW", "SETGID", "SETUID", "SETFCAP", "SETPCAP",
+                "NET_BIND_SERVICE", "SYS_CHROOT", "KILL", "AUDIT_WRITE")
+_PROBE: dict | None = None
+
+
+def probe_isolation(nsexec_bin: str | None = None) -> dict:
+    """What the node offers (`amdkube-nsexec --probe`, cached per process)."""
+    global _PROBE
+    if _PROBE is None:
+        try:
+            out = subprocess.run([nsexec_bin or os.path.join(NATIVE_BIN, "amdkube-nsexec"), "--probe"],
+                                 capture_output=True, text=True, timeout=10).stdout
+            _PROBE = json.loads(out.strip().splitlines()[-1])
+        except (OSError, ValueError, IndexError, subprocess.SubprocessError):
+            _PROBE = {"root": os.geteuid() == 0, "landlock_abi": 0, "userns": False, "cgroup2": False,
+                      "cgroup2_writable": False}
+    return _PROBE
+
+
+def resolve_isolation(mode: str, probe: dict) -> str:
+    """`auto` → the strongest mechanism the node has (root+cgroup2 → namespaces, user namespaces
+    → userns, Landlock → landlock, else env). An explicit mode is taken as asked."""
+    if mode not in ISOLATION_MODES:
+        raise ValueError(f"unknown isolation mode {mode!r} (one of {', '.join(ISOLATION_MODES)})")
+    if mode != "auto":
+        return mode
+    if probe.get("root") and probe.get("cgroup2_writable"):
+        return "namespaces"
+    if probe.get("userns") and not probe.get("root"):
+        return "userns"
+    if probe.get("landlock_abi", 0) >= 1:
+        return "landlock"
+    return "env"
+
+
+def container_caps(sc) -> str:
+    """Bounding set for a container from its CRI security context: privileged keeps all,
+    else Docker's default set plus adds minus drops ("ALL" honoured on either side)."""
+    if sc is None:
+        return ",".join(DEFAULT_CAPS)
+    if sc.privileged:
+        return "all"
+    caps = set(DEFAULT_CAPS)
+    add = [c.upper().removeprefix("CAP_") for c in sc.capabilities.add_capabilities] if sc.HasField("capabilities") else []
+    drop = [c.upper().removeprefix("CAP_") for c in sc.capabilities.drop_capabilities] if sc.HasField("capabilities") else []
+    if "ALL" in add:
+        return "all"
+    caps |= set(add)
+    caps = set() if "ALL" in drop else caps - set(drop)
+    return ",".join(sorted(caps)) or "none"
 SCRUB_ENV = ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL",
              "OMPI_COMM_WORLD_LOCAL_RANK", "LOCAL_RANK", "RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
              "TORCHELASTIC_RUN_ID", "GROUP_RANK", "LOCAL_WORLD_SIZE", "ROLE_RANK")
@@ -211,7 +280,8 @@ class RocShim:
         self.images = ImageStore(state_dir, registry_dir)
         self.ckpt = CheckpointWriter()
         self.hooks = HookService(hooks_dir, HANDLERS)
-        self.isolation = isolation
+        self.isolation_probe = probe_isolation() if isolation in ("auto", "landlock", "namespaces", "userns") else {}
+        self.isolation = resolve_isolation(isolation, self.isolation_probe)
         self.network = network or HostNetwork()
         # pod networking: non-hostNetwork sandboxes get their own net/ipc/uts namespaces (needs
         # a privileged rocshim) wired by the network plugin (amdkube-bridge); containers join them
@@ -498,7 +568,7 @@ class RocShim:
             env.pop("ROCR_VISIBLE_DEVICES", None)
             env["HIP_VISIBLE_DEVICES"] = "-1"  # non-GPU containers see no GPU
         for d in devices:
-            if not os.path.exists(d["host_path"]) and self.isolation == "namespaces":
+            if not os.path.exists(d["host_path"]) and self.isolation in ("namespaces", "userns", "landlock"):
                 raise FileNotFoundError(f"device {d['host_path']} does not exist on this host")
         tags = [iname]
         handler = self.hooks.get_runtime(tags, dict(cfg.annotations), dict(sandbox_cfg.annotations) if sandbox_cfg else {})
@@ -518,7 +588,7 @@ class RocShim:
             mounts.append({"container_path": "/etc/resolv.conf", "host_path": resolv, "readonly": True})
         # without a mount namespace, expose volumes as symlinks under the container's root
         for mnt in mounts:
-            if self.isolation != "namespaces" and mnt["container_path"].startswith("/"):
+            if not self.private_mounts and mnt["container_path"].startswith("/"):
                 link = os.path.join(root, mnt["container_path"].lstrip("/"))
                 os.makedirs(os.path.dirname(link), exist_ok=True)
                 if not os.path.lexists(link):
@@ -529,6 +599,11 @@ class RocShim:
                      "cpu_shares": r.cpu_shares, "oom_score_adj": r.oom_score_adj, "cpuset": r.cpuset_cpus} if r else {}
         if sandbox_cfg is not None and sandbox_cfg.HasField("linux") and sandbox_cfg.linux.cgroup_parent:
             resources["cgroup_parent"] = sandbox_cfg.linux.cgroup_parent.strip("/")
+        sc = cfg.linux.security_context if cfg.HasField("linux") and cfg.linux.HasField("security_context") else None
+        resources["caps"] = container_caps(sc)
+        resources["privileged"] = bool(sc is not None and sc.privileged)
+        if self.isolation in ("landlock", "userns", "namespaces") and handler == "rocm":
+            env = self._guarded_env(env, devices)
         sec = cfg.linux.security_context.seccomp_profile_path if cfg.HasField("linux") else ""
         if sec:
             resources["seccomp_profile"] = self._seccomp_file(sec)
@@ -568,20 +643,64 @@ class RocShim:
             out += ["--join", f"{t}:{p}"]
         return out
 
+    @property
+    def private_mounts(self) -> bool:
+        """The container gets its own mount namespace (volumes are bind mounts, not links)."""
+        return self.isolation in ("namespaces", "userns")
+
+    def _guarded_env(self, env: dict, devices: list[dict]) -> dict:
+        """`rocm` handler under a device guard: the container's view is exactly its devices.
+        ROCR_VISIBLE_DEVICES ordinals index the host's full GPU list, which the container no
+        longer sees, so an ordinal-only list is dropped (the view already selects); UUIDs stay.
+        Landlock mode adds the devview preload (absent, not refused, foreign nodes)."""
+        env = dict(env)
+        vis = env.get("ROCR_VISIBLE_DEVICES")
+        if vis and all(t.strip().isdigit() for t in vis.split(",")):
+            env.pop("ROCR_VISIBLE_DEVICES")
+        if self.isolation == "landlock" and os.path.exists(DEVVIEW_LIB):
+            pre = env.get("LD_PRELOAD", "")
+            env["LD_PRELOAD"] = DEVVIEW_LIB + (":" + pre if pre else "")
+            env["AMDKUBE_DEVVIEW_ROOT"] = self.dev_root
+            env["AMDKUBE_DEVVIEW_ALLOW"] = ",".join(d["host_path"] for d in devices)
+        return env
+
+    def _device_args(self, c: Container) -> list[str]:
+        """--keep (render/card nodes the container was given) and --hide-kfd (no GPU)."""
+        if c.resources.get("privileged"):
+            return []
+        a = []
+        for d in c.devices:
+            if "/dri/" in d["host_path"]:
+                a += ["--keep", d["host_path"]]
+        if not any(d["host_path"].endswith("/kfd") for d in c.devices):
+            a += ["--hide-kfd"]
+        return a
+
     def _launch_argv(self, c: Container) -> list[str]:
         sec, aa = c.resources.get("seccomp_profile"), c.resources.get("apparmor_profile")
         cpuset = c.resources.get("cpuset") or ""
         join = self._join_args(c)
-        if self.isolation != "namespaces":
+        if self.isolation == "landlock":
+            dev = ([] if c.resources.get("privileged") else ["--landlock"]) + ["--dev-root", self.dev_root] + self._device_args(c)
+            return ([self.nsexec_bin, "--no-namespaces"] + dev + join + (["--seccomp", sec] if sec else []) +
+                    (["--apparmor", aa] if aa else []) + (["--cpuset", cpuset] if cpuset else []) + ["--"] + c.argv)
+        if not self.private_mounts:
             if not (sec or aa or cpuset or join):
                 return c.argv
             return ([self.nsexec_bin, "--no-namespaces"] + join + (["--seccomp", sec] if sec else []) +
                     (["--apparmor", aa] if aa else []) + (["--cpuset", cpuset] if cpuset else []) + ["--"] + c.argv)
         # (env isolation: the OOM score is applied to the spawned process directly, see start_container)
-        keep = [d["host_path"] for d in c.devices if "/dri/" in d["host_path"]]
-        # QoS hierarchy from the kubelet (kubepods/[burstable|besteffort]/pod<uid>), else per sandbox
-        cg = self._cgroup_of(c)
-        a = [self.nsexec_bin, "--dev-root", self.dev_root, "--cgroup", cg] + join
+        a = [self.nsexec_bin, "--dev-root", self.dev_root] + join
+        if self.isolation == "userns":
+            a += ["--userns"]
+        else:
+            # QoS hierarchy from the kubelet (kubepods/[burstable|besteffort]/pod<uid>), else per sandbox
+            a += ["--cgroup", self._cgroup_of(c)]
+            if self.isolation_probe.get("cgroup2") and not c.resources.get("privileged"):
+                a += ["--device-cgroup"]
+        if self.isolation_probe.get("landlock_abi", 0) >= 1 and not c.resources.get("privileged"):
+            a += ["--landlock"]
+        a += ["--caps", c.resources.get("caps") or ",".join(DEFAULT_CAPS)]
         if c.resources.get("cpu_shares"):
             a += ["--cpu-weight", str(_shares_to_weight(c.resources["cpu_shares"]))]
         if c.resources.get("oom_score_adj"):
@@ -593,15 +712,14 @@ class RocShim:
         for mnt in c.mounts:   # volumes and the pod's resolv.conf in the private mount namespace
             if mnt["container_path"].startswith("/") and os.path.exists(mnt["host_path"]):
                 a += ["--bind", f"{mnt['host_path']}:{mnt['container_path']}" + (":ro" if mnt.get("readonly") else "")]
-        for k in keep:
-            a += ["--keep", k]
+        a += [x for x in self._device_args(c) if x != "--hide-kfd"]
         if c.resources.get("memory_limit"):
             a += ["--memory-max", str(c.resources["memory_limit"])]
         if c.resources.get("cpu_quota") and c.resources.get("cpu_period"):
             a += ["--cpu-max", f"{c.resources['cpu_quota']} {c.resources['cpu_period']}"]
         if cpuset:
             a += ["--cpuset", cpuset]
-        if not any(d["host_path"].endswith("/kfd") for d in c.devices):
+        if "--hide-kfd" in self._device_args(c):
             a += ["--hide-kfd"]
         return a + ["--"] + c.argv
 

@@ -30,7 +30,11 @@ def _crypto():
                 ("EVP_MD_CTX_new", vp, []), ("EVP_MD_CTX_free", None, [vp]), ("EVP_sha256", vp, []),
                 ("d2i_PUBKEY", vp, [vp, ctypes.POINTER(cp), ctypes.c_long]), ("EVP_PKEY_free", None, [vp]),
                 ("EVP_DigestVerifyInit", ip, [vp, vp, vp, vp, vp]),
-                ("EVP_DigestVerify", ip, [vp, cp, ctypes.c_size_t, cp, ctypes.c_size_t])):
+                ("EVP_DigestVerify", ip, [vp, cp, ctypes.c_size_t, cp, ctypes.c_size_t]),
+                ("d2i_X509", vp, [vp, ctypes.POINTER(cp), ctypes.c_long]), ("X509_free", None, [vp]),
+                ("X509_get_pubkey", vp, [vp]), ("X509_verify", ip, [vp, vp]),
+                ("BIO_new_mem_buf", vp, [cp, ip]), ("BIO_free", ip, [vp]),
+                ("PEM_read_bio_X509", vp, [vp, vp, vp, vp])):
             fn = getattr(lib, name)
             fn.restype, fn.argtypes = res, args
         _lib = lib
@@ -144,6 +148,45 @@ def rsa_sha256_verify(spki_der: bytes, data: bytes, signature: bytes) -> bool:
     finally:
         lib.EVP_MD_CTX_free(md)
         lib.EVP_PKEY_free(pkey)
+
+
+def x509_pem_to_der(pem: bytes) -> list[bytes]:
+    """Every CERTIFICATE block of a PEM bundle as DER."""
+    import base64
+    out, cur = [], None
+    for line in pem.decode(errors="replace").splitlines():
+        if line.startswith("-----BEGIN CERTIFICATE"):
+            cur = []
+        elif line.startswith("-----END CERTIFICATE") and cur is not None:
+            out.append(base64.b64decode("".join(cur)))
+            cur = None
+        elif cur is not None:
+            cur.append(line.strip())
+    return out
+
+
+def x509_signed_by(cert_der: bytes, issuer_der: bytes) -> bool:
+    """True when `cert_der`'s signature verifies under `issuer_der`'s public key (X509_verify):
+    the certificate was really issued by that CA, not just by one with the same subject name."""
+    lib = _crypto()
+    b1, b2 = ctypes.c_char_p(cert_der), ctypes.c_char_p(issuer_der)
+    cert = lib.d2i_X509(None, ctypes.byref(b1), len(cert_der))
+    ca = lib.d2i_X509(None, ctypes.byref(b2), len(issuer_der))
+    try:
+        if not cert or not ca:
+            return False
+        key = lib.X509_get_pubkey(ca)
+        if not key:
+            return False
+        try:
+            return lib.X509_verify(cert, key) == 1
+        finally:
+            lib.EVP_PKEY_free(key)
+    finally:
+        if cert:
+            lib.X509_free(cert)
+        if ca:
+            lib.X509_free(ca)
 
 
 def sha256(b: bytes) -> bytes:

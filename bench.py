@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--density-nodes", type=int, default=100, help="hollow-node density run (0 = skip)")
     ap.add_argument("--image", default="rocm/vector-add", help="GPU pod image (CPU rehearsals: busybox)")
     ap.add_argument("--pod-arg", action="append", default=[], help="GPU pod container argument (repeatable)")
+    ap.add_argument("--isolation", default=None, help="rocshim device isolation (default: auto on real GPUs)")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -67,13 +68,15 @@ def main():
             env.pop(k, None)
         worker = subprocess.Popen([sys.executable, "-m", "amdkube.benchmark.podbench", "--gpus", str(n),
                                    "--pods-per-gpu", str(a.pods_per_gpu), "--backend", a.backend, "--mode", a.mode,
-                                   "--image", a.image, "--", *a.pod_arg],
+                                   "--image", a.image, *(["--isolation", a.isolation] if a.isolation else []),
+                                   "--", *a.pod_arg],
                                   cwd=ROOT, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
         ready = json.loads(worker.stdout.readline() or "{}")
         if not ready.get("ready"):
             worker.kill()
             raise SystemExit("cluster worker failed to start")
-        print(f"[bench] node ready: {len(ready['gpus'])} GPU(s) via {ready['backend']}", file=sys.stderr, flush=True)
+        print(f"[bench] node ready: {len(ready['gpus'])} GPU(s) via {ready['backend']}, isolation={ready.get('isolation')}",
+              file=sys.stderr, flush=True)
 
     import torch
     import torch.distributed as dist
@@ -158,7 +161,7 @@ def main():
                "p50_startup_all_pods_ms": res["p50_startup_all_pods_ms"], "p99_startup_all_pods_ms": res["p99_startup_all_pods_ms"],
                "p50_node_startup_ms": res["p50_node_startup_ms"], "p50_schedule_ms": res["p50_schedule_ms"],
                "p50_pod_runtime_ms": res["p50_pod_runtime_ms"], "failed_pods": res["failed"],
-               "node_cpu_s": res.get("node_cpu_s"),
+               "node_cpu_s": res.get("node_cpu_s"), "isolation": ready.get("isolation"),
                "sched_perf": sched, "density": density}
         if res["failed"]:
             out["failures"] = res["failures"]

@@ -48,9 +48,11 @@ def targets(sanitize=False, cpu_only=False):
         (n(OUT, "_amdsmi" + EXT), [n("native/amdsmi_shim.cpp"), n("native/sampler_core.h")],
          ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", *py, *rocm_inc, n("native/amdsmi_shim.cpp"), *rpath,
           "-lamd_smi", "-o", "{out}"]),
+        (n(OUT, "lib", "libamdkube-devview.so"), [n("native/devview.c")],
+         ["gcc", "-O2", "-shared", "-fPIC", "-Wall", n("native/devview.c"), "-o", "{out}", "-ldl"]),
         (n(BIN, "pause"), [n("native/pause.cpp")],
          ["g++", "-O2", "-std=c++17", n("native/pause.cpp"), "-o", "{out}"]),
-        (n(BIN, "amdkube-nsexec"), [n("native/nsexec.cpp"), n("native/seccomp_bpf.h"), SYSCALL_TABLE],
+        (n(BIN, "amdkube-nsexec"), [n("native/nsexec.cpp"), n("native/seccomp_bpf.h"), n("native/devguard.h"), SYSCALL_TABLE],
          ["g++", "-O2", "-std=c++17", n("native/nsexec.cpp"), "-o", "{out}"]),
         (n(BIN, "seccomp-check"), [n("native/seccomp_check.cpp"), n("native/seccomp_bpf.h"), SYSCALL_TABLE],
          ["g++", "-O2", "-std=c++17", n("native/seccomp_check.cpp"), "-o", "{out}"]),
@@ -124,6 +126,7 @@ def stale(out, deps):
 
 def build(sanitize=False, cpu_only=False, force=False, jobs=4, verbose=False):
     os.makedirs(os.path.join(BIN, "cni"), exist_ok=True)
+    os.makedirs(os.path.join(OUT, "lib"), exist_ok=True)
     gen_syscall_table()
     init = os.path.join(OUT, "__init__.py")
     if not os.path.exists(init):

@@ -29,6 +29,18 @@
 //   --sysctl KEY=VALUE      namespaced sysctls (net.*, kernel.shm*, ...) written after the
 //                           namespaces are set up, so they apply to the pod, never the host.
 // `--no-namespaces` skips steps 1-4 (unprivileged `env` isolation still gets seccomp/AppArmor).
+// Device guards (devguard.h), enforced by the kernel whatever the container does with its env:
+//   --landlock        Landlock ruleset: only the --keep render nodes (and /dev/kfd unless
+//                     --hide-kfd) are openable among <dev-root>/dri/* and kfd; mknod of any
+//                     device node is refused. Works unprivileged (the GPU box has no userns);
+//                     in namespace modes it is layered under the private /dev/dri.
+//   --device-cgroup   root: attach a cgroup-v2 BPF device filter (char 226:* only the kept
+//                     minors; kfd only for GPU containers) to the container's --cgroup leaf.
+//   --userns          not root: a user namespace (uid/gid -> 0) owns the mount namespace, so
+//                     the private /dev/dri works without privileges where userns is enabled.
+//   --caps LIST|all   capability bounding set kept for the container (comma list of names,
+//                     default: the Docker default set); everything else is dropped, and
+//                     no_new_privs is set, before exec.
 // Any isolation step that fails is fatal (exit 126): a container never silently runs with
 // more devices, or fewer syscall restrictions, than it was given.
 #include <fcntl.h>
@@ -36,6 +48,7 @@
 #include <sys/mount.h>
 #include <sys/stat.h>
 #include <sys/types.h>
+#include <sys/wait.h>
 #include <unistd.h>
 
 #include <cerrno>
@@ -47,6 +60,11 @@
 #include <string>
 #include <vector>
 
+#include <linux/capability.h>
+#include <sys/prctl.h>
+#include <sys/syscall.h>
+
+#include "devguard.h"
 #include "seccomp_bpf.h"
 
 static int die(const char* what) {
@@ -154,10 +172,111 @@ static int pod_namespaces(const std::vector<std::string>& joins, const std::stri
   return 0;
 }
 
+// Docker's default capability set (the reference's containers run with it, docker/oci/defaults.go)
+static const char* kDefaultCaps[] = {"chown", "dac_override", "fsetid", "fowner", "mknod", "net_raw", "setgid", "setuid",
+                                     "setfcap", "setpcap", "net_bind_service", "sys_chroot", "kill", "audit_write"};
+static const char* kCapNames[] = {"chown", "dac_override", "dac_read_search", "fowner", "fsetid", "kill", "setgid",
+                                  "setuid", "setpcap", "linux_immutable", "net_bind_service", "net_broadcast", "net_admin",
+                                  "net_raw", "ipc_lock", "ipc_owner", "sys_module", "sys_rawio", "sys_chroot", "sys_ptrace",
+                                  "sys_pacct", "sys_admin", "sys_boot", "sys_nice", "sys_resource", "sys_time",
+                                  "sys_tty_config", "mknod", "lease", "audit_write", "audit_control", "setfcap",
+                                  "mac_override", "mac_admin", "syslog", "wake_alarm", "block_suspend", "audit_read",
+                                  "perfmon", "bpf", "checkpoint_restore"};
+
+static int cap_index(std::string n) {
+  for (auto& ch : n) ch = static_cast<char>(std::tolower(ch));
+  if (n.rfind("cap_", 0) == 0) n = n.substr(4);
+  for (int c = 0; c < static_cast<int>(sizeof(kCapNames) / sizeof(kCapNames[0])); ++c)
+    if (n == kCapNames[c]) return c;
+  return -1;
+}
+
+// Keep only `spec` (comma list, "all" keeps everything) in the bounding, inheritable and ambient
+// sets, then no_new_privs: an exec'd setuid binary cannot gain anything back.
+static bool limit_caps(const std::string& spec, std::string* err) {
+  if (spec == "all") return true;
+  uint64_t keep = 0;
+  std::stringstream ss(spec == "default" ? "" : spec);
+  std::string t;
+  if (spec == "default") {
+    for (auto* n : kDefaultCaps) keep |= 1ULL << cap_index(n);
+  }
+  while (std::getline(ss, t, ',')) {
+    if (t.empty() || t == "none") continue;
+    int c = cap_index(t);
+    if (c < 0) {
+      *err = "unknown capability " + t;
+      return false;
+    }
+    keep |= 1ULL << c;
+  }
+  prctl(PR_CAP_AMBIENT, PR_CAP_AMBIENT_CLEAR_ALL, 0, 0, 0);
+  for (int c = 0; c <= 63; ++c) {
+    if (keep & (1ULL << c)) continue;
+    if (prctl(PR_CAPBSET_READ, c, 0, 0, 0) <= 0) continue;   // absent or not supported
+    if (prctl(PR_CAPBSET_DROP, c, 0, 0, 0) < 0) {
+      *err = std::string("drop capability ") + (c < 41 ? kCapNames[c] : std::to_string(c)) + ": " + std::strerror(errno);
+      return false;
+    }
+  }
+  __user_cap_header_struct hdr{_LINUX_CAPABILITY_VERSION_3, 0};
+  __user_cap_data_struct data[2]{};
+  if (syscall(SYS_capget, &hdr, data) == 0) {
+    for (int w = 0; w < 2; ++w) {
+      uint32_t k = static_cast<uint32_t>(keep >> (32 * w));
+      data[w].effective &= k;
+      data[w].permitted &= k;
+      data[w].inheritable &= k;
+    }
+    if (syscall(SYS_capset, &hdr, data) < 0) {
+      *err = std::string("capset: ") + std::strerror(errno);
+      return false;
+    }
+  }
+  if (prctl(PR_SET_NO_NEW_PRIVS, 1, 0, 0, 0) < 0) {
+    *err = std::string("no_new_privs: ") + std::strerror(errno);
+    return false;
+  }
+  return true;
+}
+
+// not root: a user namespace owning the mount namespace (uid/gid map to 0 inside)
+static int enter_userns() {
+  uid_t uid = getuid();
+  gid_t gid = getgid();
+  if (unshare(CLONE_NEWUSER | CLONE_NEWNS) < 0) return die("unshare(CLONE_NEWUSER|CLONE_NEWNS)");
+  if (!write_file("/proc/self/setgroups", "deny")) return die("setgroups deny");
+  if (!write_file("/proc/self/uid_map", "0 " + std::to_string(uid) + " 1")) return die("uid_map");
+  if (!write_file("/proc/self/gid_map", "0 " + std::to_string(gid) + " 1")) return die("gid_map");
+  return 0;
+}
+
+// --probe: one JSON line naming the isolation mechanisms this node offers, for rocshim's
+// isolation=auto (root + cgroup v2 → namespaces; user namespaces → userns; Landlock → landlock).
+static int probe() {
+  int abi = amdkube_devguard::landlock_abi();
+  pid_t pid = fork();
+  bool userns = false;
+  if (pid == 0) _exit(unshare(CLONE_NEWUSER | CLONE_NEWNS) == 0 ? 0 : 1);
+  if (pid > 0) {
+    int st = 0;
+    waitpid(pid, &st, 0);
+    userns = WIFEXITED(st) && WEXITSTATUS(st) == 0;
+  }
+  struct stat cs;
+  bool cg2 = stat("/sys/fs/cgroup/cgroup.controllers", &cs) == 0;
+  std::printf("{\"root\": %s, \"landlock_abi\": %d, \"userns\": %s, \"cgroup2\": %s, \"cgroup2_writable\": %s}\n",
+              geteuid() == 0 ? "true" : "false", abi < 0 ? 0 : abi, userns ? "true" : "false", cg2 ? "true" : "false",
+              cg2 && access("/sys/fs/cgroup", W_OK) == 0 ? "true" : "false");
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc == 2 && std::string(argv[1]) == "--probe") return probe();
   std::string dev_root = "/dev", cgroup, mem_max, cpu_max, cpu_weight, oom_adj;
   std::vector<std::string> keep, binds;
-  bool hide_kfd = false, no_ns = false;
+  bool hide_kfd = false, no_ns = false, use_landlock = false, device_cgroup = false, userns = false;
+  std::string caps;
   std::string seccomp_profile, apparmor, cpuset, unshare_list, hostname;
   std::vector<std::string> joins, sysctls;
   int i = 1;
@@ -178,6 +297,10 @@ int main(int argc, char** argv) {
     else if (a == "--seccomp" && i + 1 < argc) seccomp_profile = argv[++i];
     else if (a == "--apparmor" && i + 1 < argc) apparmor = argv[++i];
     else if (a == "--no-namespaces") no_ns = true;
+    else if (a == "--landlock") use_landlock = true;
+    else if (a == "--device-cgroup") device_cgroup = true;
+    else if (a == "--userns") userns = true;
+    else if (a == "--caps" && i + 1 < argc) caps = argv[++i];
     else if (a == "--cpuset" && i + 1 < argc) cpuset = argv[++i];
     else if (a == "--unshare" && i + 1 < argc) unshare_list = argv[++i];
     else if (a == "--hostname" && i + 1 < argc) hostname = argv[++i];
@@ -214,8 +337,19 @@ int main(int argc, char** argv) {
   }
   if (int rc = pod_namespaces(joins, unshare_list, hostname, sysctls)) return rc;
   if (no_ns) {
-    if (!apparmor.empty() && !apparmor_onexec(apparmor)) return die(("AppArmor profile " + apparmor).c_str());
     std::string err;
+    if (use_landlock) {
+      // kernel-enforced device view for an unprivileged node (no mount namespace to hide nodes in)
+      if (!amdkube_devguard::landlock_apply(amdkube_devguard::plan(dev_root, keep, hide_kfd), &err)) {
+        std::fprintf(stderr, "amdkube-nsexec: %s\n", err.c_str());
+        return 126;
+      }
+    }
+    if (!caps.empty() && !limit_caps(caps, &err)) {
+      std::fprintf(stderr, "amdkube-nsexec: %s\n", err.c_str());
+      return 126;
+    }
+    if (!apparmor.empty() && !apparmor_onexec(apparmor)) return die(("AppArmor profile " + apparmor).c_str());
     if (!filter.empty() && !amdkube_seccomp::apply(filter, &err)) {
       std::fprintf(stderr, "amdkube-nsexec: %s\n", err.c_str());
       return 126;
@@ -230,10 +364,32 @@ int main(int argc, char** argv) {
     if (!cpu_weight.empty()) write_file(cgroup + "/cpu.weight", cpu_weight);
     if (!cpuset.empty()) write_file(cgroup + "/cpuset.cpus", cpuset);   // when the cpuset controller is delegated
     if (!write_file(cgroup + "/cgroup.procs", std::to_string(getpid()))) return die("join cgroup");
+    if (device_cgroup) {
+      std::string err;
+      if (!amdkube_devguard::cgroup_device_filter(cgroup, keep, dev_root, hide_kfd, &err)) {
+        std::fprintf(stderr, "amdkube-nsexec: %s\n", err.c_str());
+        return 126;
+      }
+    }
   }
   // lowering the score needs CAP_SYS_RESOURCE, which the privileged launcher has
   if (!oom_adj.empty() && !write_file("/proc/self/oom_score_adj", oom_adj)) return die("oom_score_adj");
-  if (unshare(CLONE_NEWNS) < 0) return die("unshare(CLONE_NEWNS)");
+  // the Landlock plan is taken on the host view (rules bind to the real inodes: the kept nodes
+  // stay reachable through their bind mounts, the real kfd stays denied behind the /dev/null bind)
+  int ll_rs = -1;
+  if (use_landlock) {
+    std::string err;
+    ll_rs = amdkube_devguard::landlock_ruleset(amdkube_devguard::plan(dev_root, keep, hide_kfd), &err);
+    if (ll_rs < 0) {
+      std::fprintf(stderr, "amdkube-nsexec: %s\n", err.c_str());
+      return 126;
+    }
+  }
+  if (userns && getuid() != 0) {
+    if (int rc = enter_userns()) return rc;
+  } else if (unshare(CLONE_NEWNS) < 0) {
+    return die("unshare(CLONE_NEWNS)");
+  }
   if (mount(nullptr, "/", nullptr, MS_REC | MS_PRIVATE, nullptr) < 0) return die("make / rprivate");
   // open the kept nodes inside the new namespace (a bind source must belong to it)
   std::vector<int> fds;
@@ -289,6 +445,21 @@ int main(int argc, char** argv) {
     if (mount(src.c_str(), dst.c_str(), nullptr, MS_BIND | MS_REC, nullptr) < 0) return die(("bind " + dst).c_str());
     if (ro && mount(nullptr, dst.c_str(), nullptr, MS_BIND | MS_REMOUNT | MS_RDONLY | MS_REC, nullptr) < 0)
       return die(("remount read-only " + dst).c_str());
+    // a new mount point is not beneath any granted inode: grant the volume itself
+    if (ll_rs >= 0 && !amdkube_devguard::landlock_grant(ll_rs, dst)) return die(("landlock grant " + dst).c_str());
+  }
+  {
+    std::string err;
+    // after the mounts: a Landlock-restricted process may not change its mount topology, so the
+    // container cannot unmount the private /dev/dri either
+    if (ll_rs >= 0 && !amdkube_devguard::landlock_restrict(ll_rs, &err)) {
+      std::fprintf(stderr, "amdkube-nsexec: %s\n", err.c_str());
+      return 126;
+    }
+    if (!limit_caps(caps.empty() ? "default" : caps, &err)) {
+      std::fprintf(stderr, "amdkube-nsexec: %s\n", err.c_str());
+      return 126;
+    }
   }
   if (!apparmor.empty() && !apparmor_onexec(apparmor)) return die(("AppArmor profile " + apparmor).c_str());
   if (!filter.empty()) {

@@ -70,6 +70,50 @@ def test_02_gpu_pod_runs_on_its_assigned_device():
     run(go(), 300)
 
 
+def test_02c_device_guard_on_mi355x():
+    """Enforced isolation on the real node (rocshim isolation=auto: Landlock on the unprivileged
+    gpurun box). A non-GPU pod that unsets every *_VISIBLE_DEVICES still cannot reach the GPU
+    (vector-add fails, /dev/kfd and the render node refuse to open); a GPU pod that unsets
+    ROCR_VISIBLE_DEVICES still passes on its own device; mknod of a DRM node is refused by the
+    kernel guard (EACCES from Landlock, before the capability check's EPERM)."""
+    unset = "unset ROCR_VISIBLE_DEVICES HIP_VISIBLE_DEVICES CUDA_VISIBLE_DEVICES GPU_DEVICE_ORDINAL; "
+    opener = ("import glob, os\n"
+              "for p in ['/dev/kfd'] + sorted(glob.glob('/dev/dri/*')):\n"
+              "    try:\n        os.close(os.open(p, os.O_RDWR)); print('OPENED', p)\n"
+              "    except OSError as e:\n        print('refused', p, e.strerror)\n"
+              "try:\n    os.mknod('/tmp/ak-mknod-226', 0o020600, os.makedev(226, 200)); print('MKNOD OK')\n"
+              "except OSError as e:\n    print('mknod', e.strerror)\n")
+
+    def pod(name, gpu, cmd):
+        p = vadd_pod(name, gpu=gpu)
+        c = p["spec"]["containers"][0]
+        c["image"], c["command"], c["args"] = "busybox", ["sh", "-c", cmd], []
+        return p
+
+    async def go():
+        async with LocalCluster(gpus="amdsmi", n_gpus=1, relist_period=0.5, with_controllers=False) as lc:
+            assert lc.shim.isolation in ("landlock", "userns", "namespaces"), lc.shim.isolation_probe
+            await lc.wait_gpus(1, 60)
+            await lc.client.create(pod("escape", False, unset + f"exec {BIN}/rocm-vector-add"))
+            await lc.client.create(pod("opener", False, unset + f"exec python3 -c \"{opener}\""))
+            for name in ("escape", "opener"):
+                await wait_pod(lc.client, "default", name, ("Succeeded", "Failed"), 120)
+            p = await lc.client.get("pods", "escape", "default")
+            logs = await lc.client.logs("default", "escape")
+            assert p["status"]["phase"] == "Failed" and "Test PASSED" not in logs, (p["status"], logs)
+            logs = await lc.client.logs("default", "opener")
+            assert "OPENED" not in logs and "refused /dev/kfd" in logs, logs
+            assert "mknod Permission denied" in logs, logs
+            await lc.client.create(pod("gpu-unset", True, unset + f"exec {BIN}/rocm-vector-add --print-uuid"))
+            p = await wait_pod(lc.client, "default", "gpu-unset", ("Succeeded", "Failed"), 120)
+            logs = await lc.client.logs("default", "gpu-unset")
+            assert p["status"]["phase"] == "Succeeded" and "Test PASSED" in logs, (p["status"], logs)
+            [did] = p["spec"]["extendedResources"][0]["assigned"]
+            assert f"uuid={lc.plugin.by_id[did]['hip_uuid']}" in logs, logs
+            print("device guard:", lc.shim.isolation, lc.shim.isolation_probe)
+    run(go(), 300)
+
+
 def test_02b_legacy_accelerators_pod_on_real_gpu():
     """Accelerators gate (F22): alpha.kubernetes.io/amd-gpu from the real render nodes; the pod
     gets /dev/kfd + its render node + ROCR_VISIBLE_DEVICES and vector-add passes."""

@@ -5,6 +5,7 @@ tests). The metrics-server authenticates the aggregator by its front-proxy clien
 authorizes the asserted user with a SubjectAccessReview against the main apiserver's RBAC."""
 import asyncio
 import io
+import os
 import ssl
 import subprocess
 from contextlib import redirect_stdout
@@ -36,10 +37,16 @@ def _leaf(d, ca, name, cn, server=False):
     return f"{d}/{name}.crt", f"{d}/{name}.key"
 
 
+def _der(path):
+    from amdkube.utils.crypto import x509_pem_to_der
+    return x509_pem_to_der(open(path, "rb").read())[0]
+
+
 def test_requestheader_authenticator(tmp_path):
     d = str(tmp_path)
     ca, _ = _ca(d, "front-proxy-ca")
     other, _ = _ca(d, "client-ca")
+    leaf, _ = _leaf(d, "front-proxy-ca", "fp", "front-proxy-client")
     issuer = ssl._ssl._test_decode_cert(ca)["subject"]
     a = Authenticator(None, {}, None, True)
     a.configure_requestheader(ca, ["front-proxy-client"])
@@ -47,13 +54,21 @@ def test_requestheader_authenticator(tmp_path):
     hdr = CIMultiDict([("X-Remote-User", "bob"), ("X-Remote-Group", "devs"), ("X-Remote-Group", "ops"),
                        ("X-Remote-Extra-Scopes", "view")])
     pc = {"issuer": issuer, "subject": ((("commonName", "front-proxy-client"),),)}
-    u = a.authenticate(hdr, pc)
+    u = a.authenticate(hdr, pc, _der(leaf))
     assert u["name"] == "bob" and u["groups"] == ["devs", "ops", "system:authenticated"] and u["extra"] == {"scopes": ["view"]}
     # a CN outside --requestheader-allowed-names, or another issuer, cannot assert identities
     bad_cn = {"issuer": issuer, "subject": ((("commonName", "mallory"),),)}
-    assert a.authenticate(hdr, bad_cn)["name"] == "system:anonymous"
+    assert a.authenticate(hdr, bad_cn, _der(leaf))["name"] == "system:anonymous"
     other_issuer = {"issuer": ssl._ssl._test_decode_cert(other)["subject"], "subject": pc["subject"]}
     assert a.authenticate(hdr, other_issuer)["name"] == "front-proxy-client"    # plain x509 identity, headers ignored
+    # a client CA with the SAME subject as the front-proxy CA issues a certificate
+    # whose issuer name matches; only the signature check tells them apart
+    os.makedirs(f"{d}/imp")
+    _ca(f"{d}/imp", "front-proxy-ca")
+    fake, _ = _leaf(f"{d}/imp", "front-proxy-ca", "fp", "front-proxy-client")
+    assert ssl._ssl._test_decode_cert(fake)["issuer"] == issuer
+    assert a.authenticate(hdr, pc, _der(fake))["name"] == "system:anonymous"    # X-Remote-User ignored
+    assert a.authenticate(hdr, pc)["name"] == "system:anonymous"                # no DER: never trusted
 
 
 def test_metrics_api_through_aggregator_and_kubectl_top(tmp_path):

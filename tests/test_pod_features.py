@@ -54,7 +54,7 @@ def test_env_volumes_hooks_and_termination_messages(tmp_path):
             await c.create({"apiVersion": "v1", "kind": "Service", "metadata": {"name": "db", "namespace": "default"},
                             "spec": {"ports": [{"port": 5432, "name": "pg"}]}})
             await c.create({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "cfg", "namespace": "default"},
-                            "data": {"greeting": "hi", "other": "x", "bad key": "skip"}})
+                            "data": {"greeting": "hi", "other": "x", "bad.key": "skip"}})
             await c.create({"apiVersion": "v1", "kind": "Secret", "metadata": {"name": "sec", "namespace": "default"},
                             "data": {"token": "czNjcjN0"}})
             for _ in range(50):    # the kubelet's service informer has the new service
@@ -91,7 +91,7 @@ def test_env_volumes_hooks_and_termination_messages(tmp_path):
             p = await wait_pod(c, "default", "feat", ("Failed",), 30)
             env = dict(line.split("=", 1) for line in (out / "env").read_text().splitlines() if "=" in line)
             assert env["MSG"] == "hi world" and env["CPU_M"] == "500" and env["CFG_greeting"] == "hi"
-            assert "CFG_bad key" not in env and env["DB_SERVICE_PORT_PG"] == "5432" and env["DB_SERVICE_HOST"]
+            assert "CFG_bad.key" not in env and env["DB_SERVICE_PORT_PG"] == "5432" and env["DB_SERVICE_HOST"]
             assert env["KUBERNETES_SERVICE_HOST"] and env["MY_IP"] == lc.kubelet.cfg.node_ip
             assert (out / "files").read_text().strip() == "hi64s3cr3tv1"     # values carry no trailing newline
             assert (out / "args").read_text().split() == ["hi", "$(MISSING)"]
