@@ -23,6 +23,7 @@ META = "io.k8s.apimachinery.pkg.apis.meta.v1"
 QUANTITY = "io.k8s.apimachinery.pkg.api.resource.Quantity"
 INT_OR_STRING = "io.k8s.apimachinery.pkg.util.intstr.IntOrString"
 TIME = f"{META}.Time"
+MICROTIME = f"{META}.MicroTime"
 PRIMS = {"string": {"type": "string"}, "integer": {"type": "integer", "format": "int32"},
          "long": {"type": "integer", "format": "int64"}, "boolean": {"type": "boolean"},
          "number": {"type": "number", "format": "double"}, "byte": {"type": "string", "format": "byte"},
@@ -48,7 +49,8 @@ def _parse(text: str) -> tuple[dict, dict]:
             raw[cur] = {"desc": desc.strip(), "kind": "+kind" in flags, "fields": []}
             prefix_of[cur] = prefix
             if raw[cur]["kind"]:
-                raw[cur]["fields"] += [(n, t, False, d) for n, t, d in KIND_FIELDS]
+                # +meta! : the reference marks metadata required on this kind (core/v1 Event)
+                raw[cur]["fields"] += [(n, t, n == "metadata" and "+meta!" in flags, d) for n, t, d in KIND_FIELDS]
             continue
         body, _, desc = line.strip().partition("  ")
         fname, ftype = body.split()[:2]
@@ -70,6 +72,8 @@ def _resolver(raw: dict, prefix_of: dict):
             return dict(PRIMS[t])
         if t == "time":
             return {"$ref": f"#/definitions/{TIME}"}
+        if t == "microtime":
+            return {"$ref": f"#/definitions/{MICROTIME}"}
         if t == "quantity":
             return {"$ref": f"#/definitions/{QUANTITY}"}
         if t == "ios":
@@ -92,6 +96,10 @@ def _kind_defs(defs: dict) -> dict:
         by_kind.setdefault(full.rsplit(".", 1)[1], []).append(full)
     out = {}
     for ri in SCHEME.by_kind.values():
+        own = f"io.k8s.api.{ri.group.split('.')[0] if ri.group else 'core'}.{ri.version}.{ri.kind}"
+        if own in defs:     # a version with its own shape (extensions/v1beta1 Deployment: rollbackTo)
+            out[(ri.group, ri.version, ri.kind)] = own
+            continue
         canon = SCHEME.storage_of(ri)
         cands = by_kind.get(canon.kind, [])
         grp = canon.group.split(".")[0] if canon.group else "core"
@@ -106,6 +114,8 @@ def definitions() -> dict:
     raw, prefix_of = _parse(TYPES)
     ref = _resolver(raw, prefix_of)
     defs = {TIME: {"description": "RFC 3339 timestamp with second precision.", "type": "string", "format": "date-time"},
+            MICROTIME: {"description": "RFC 3339 timestamp with microsecond precision.", "type": "string",
+                        "format": "date-time"},
             QUANTITY: {"description": "A fixed-point quantity such as 4, 500m, 288Gi or 1e3.", "type": "string"},
             INT_OR_STRING: {"description": "An integer or a string (a port number or name, a count or a percentage).",
                             "type": "string", "format": "int-or-string"}}

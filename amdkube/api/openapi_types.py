@@ -90,7 +90,7 @@ Preconditions  Conditions a DELETE checks.
   uid string
 WatchEvent  One event of a watch stream.
   type string!  ADDED, MODIFIED, DELETED or ERROR.
-  object object!  The object (or a Status for ERROR).
+  object io.k8s.apimachinery.pkg.runtime.RawExtension!  The object (or a Status for ERROR).
 APIResource  One resource of a group version.
   name string!
   singularName string!
@@ -112,7 +112,7 @@ APIGroup  One API group and its versions.
   name string!
   versions []GroupVersionForDiscovery!
   preferredVersion GroupVersionForDiscovery
-  serverAddressByClientCIDRs []ServerAddressByClientCIDR
+  serverAddressByClientCIDRs []ServerAddressByClientCIDR!
 APIGroupList  All API groups.
   apiVersion string
   kind string
@@ -127,7 +127,7 @@ APIVersions  Versions of the legacy core API.
   apiVersion string
   kind string
   versions []string!
-  serverAddressByClientCIDRs []ServerAddressByClientCIDR
+  serverAddressByClientCIDRs []ServerAddressByClientCIDR!
 
 @io.k8s.api.core.v1
 Pod +kind  A group of containers that share network, IPC and volumes and are scheduled onto one node together.
@@ -166,7 +166,6 @@ PodStatus  Observed state of a pod.
   conditions []PodCondition  PodScheduled, Initialized, Ready.
   message string  Why the pod is in its condition.
   reason string  Brief CamelCase reason (Evicted, ...).
-  nominatedNodeName string  Node on which preemption made room for this pod.
   hostIP string  IP of the node the pod runs on.
   podIP string  IP of the pod.
   startTime time  When the kubelet acknowledged the pod.
@@ -386,8 +385,12 @@ PodExtendedResource  A device-granular request of a pod (fork).
   affinity ExtendedResourceAffinity  Requirements over the devices' attributes.
   annotations {}string
   assigned []string  Device IDs the scheduler bound to this request.
+ResourceSelector  A requirement on a device attribute (the fork's alias of NodeSelectorRequirement).
+  key string!  Attribute name, e.g. amd.com/gpu-memory.
+  operator string!  In, NotIn, Exists, DoesNotExist, Gt or Lt.
+  values []string  Values for In/NotIn; a single integer for Gt/Lt.
 ExtendedResourceAffinity  Device attribute requirements (fork).
-  required []NodeSelectorRequirement
+  required []ResourceSelector
 ExtendedResourceDomain  Devices of one resource on a node (fork).
   resources {}ExtendedResource
 ExtendedResource  One device (fork).
@@ -781,7 +784,7 @@ AttachedVolume  A volume attached to a node.
   devicePath string!
 Binding +kind  Binds a pod to a node; the device IDs travel in target.extendedResourceBinding.
   target ObjectReference!
-Event +kind  A report of something that happened in the cluster.
+Event +kind +meta!  A report of something that happened in the cluster.
   involvedObject ObjectReference!
   reason string
   message string
@@ -790,6 +793,16 @@ Event +kind  A report of something that happened in the cluster.
   lastTimestamp time
   count integer
   type string  Normal or Warning.
+  eventTime microtime  When the event was first observed (events.k8s.io series).
+  series EventSeries  Data about the series this event belongs to; absent for a singleton.
+  action string  What was taken or failed regarding the involved object.
+  related ObjectReference  A secondary object the event is about.
+  reportingComponent string  Controller that emitted the event, e.g. kubernetes.io/kubelet.
+  reportingInstance string  ID of that controller instance, e.g. kubelet-xyzf.
+EventSeries  A series of events: something that kept happening.
+  count integer  Occurrences in the series up to the last heartbeat.
+  lastObservedTime microtime  Last occurrence observed.
+  state string  Ongoing or Finished.
 EventSource  Who reported an event.
   component string
   host string
@@ -835,7 +848,7 @@ LoadBalancerIngress  One ingress point.
   ip string
   hostname string
 Endpoints +kind  The addresses behind a service.
-  subsets []EndpointSubset
+  subsets []EndpointSubset!
 EndpointSubset  Addresses sharing a set of ports.
   addresses []EndpointAddress
   notReadyAddresses []EndpointAddress
@@ -919,13 +932,10 @@ DeploymentSpec  Desired state of a deployment.
   revisionHistoryLimit integer
   paused boolean
   progressDeadlineSeconds integer
-  rollbackTo RollbackConfig  extensions/v1beta1 and apps/v1beta1 only: the revision to roll back to.
-RollbackConfig  A rollback target.
-  revision long
 DeploymentRollback +kind  A rollback request (the deployments/rollback subresource).
   name string!
   updatedAnnotations {}string
-  rollbackTo RollbackConfig!
+  rollbackTo io.k8s.api.extensions.v1beta1.RollbackConfig!
 DeploymentStrategy  How pods are replaced.
   type string  Recreate or RollingUpdate.
   rollingUpdate RollingUpdateDeployment
@@ -956,7 +966,6 @@ DaemonSetSpec  Desired state of a daemon set.
   template PodTemplateSpec!
   updateStrategy DaemonSetUpdateStrategy
   minReadySeconds integer
-  templateGeneration long  extensions/v1beta1 only.
   revisionHistoryLimit integer
 DaemonSetUpdateStrategy  How daemon pods are replaced.
   type string  OnDelete or RollingUpdate.
@@ -973,6 +982,13 @@ DaemonSetStatus  Observed state of a daemon set.
   numberAvailable integer
   numberUnavailable integer
   collisionCount integer
+  conditions []DaemonSetCondition  Latest observations of the daemon set's state.
+DaemonSetCondition  One condition of a daemon set.
+  type string!
+  status string!  True, False or Unknown.
+  lastTransitionTime time
+  reason string
+  message string
 ReplicaSet +kind  Keeps a number of pod replicas running.
   spec ReplicaSetSpec
   status ReplicaSetStatus
@@ -1020,9 +1036,21 @@ StatefulSetStatus  Observed state of a stateful set.
   currentRevision string
   updateRevision string
   collisionCount integer
+  conditions []StatefulSetCondition  Latest observations of the stateful set's state.
+StatefulSetCondition  One condition of a stateful set.
+  type string!
+  status string!  True, False or Unknown.
+  lastTransitionTime time
+  reason string
+  message string
 ControllerRevision +kind  An immutable snapshot of a controller's template.
-  data object
+  data io.k8s.apimachinery.pkg.runtime.RawExtension
   revision long!
+
+@io.k8s.api.apps.v1beta1
+Deployment +kind  apps/v1beta1 form of a deployment (stored as apps/v1).
+  spec io.k8s.api.extensions.v1beta1.DeploymentSpec
+  status io.k8s.api.apps.v1.DeploymentStatus
 
 @io.k8s.api.batch.v1
 Job +kind  Runs pods to completion.
@@ -1095,18 +1123,70 @@ HorizontalPodAutoscalerSpec  Target and bounds.
   minReplicas integer
   maxReplicas integer!
   targetCPUUtilizationPercentage integer  autoscaling/v1 target.
-  metrics []MetricSpec  autoscaling/v2beta1 targets.
 CrossVersionObjectReference  The scaled object.
   kind string!
   name string!
   apiVersion string
+HorizontalPodAutoscalerStatus  Observed state of an autoscaler.
+  observedGeneration long
+  lastScaleTime time
+  currentReplicas integer!
+  desiredReplicas integer!
+  currentCPUUtilizationPercentage integer
+Scale +kind  The scale subresource.
+  spec ScaleSpec
+  status ScaleStatus
+ScaleSpec  Desired replicas.
+  replicas integer
+ScaleStatus  Observed replicas.
+  replicas integer!
+  selector string
+
+@io.k8s.api.autoscaling.v2beta1
+HorizontalPodAutoscaler +kind  Scales a workload on several metrics (CPU, memory, MI355X utilisation, custom).
+  spec HorizontalPodAutoscalerSpec
+  status HorizontalPodAutoscalerStatus
+HorizontalPodAutoscalerSpec  Target, bounds and metrics.
+  scaleTargetRef io.k8s.api.autoscaling.v1.CrossVersionObjectReference!
+  minReplicas integer
+  maxReplicas integer!
+  metrics []MetricSpec  Targets; the largest desired replica count wins.
+HorizontalPodAutoscalerStatus  Observed state of an autoscaler.
+  observedGeneration long
+  lastScaleTime time
+  currentReplicas integer!
+  desiredReplicas integer!
+  currentMetrics []MetricStatus!  Last read value of every metric.
+  conditions []HorizontalPodAutoscalerCondition!  Whether the autoscaler can scale, and why.
+HorizontalPodAutoscalerCondition  One condition of an autoscaler.
+  type string!  ScalingActive, AbleToScale or ScalingLimited.
+  status string!
+  lastTransitionTime time
+  reason string
+  message string
+MetricStatus  The last read value of one metric.
+  type string!  Object, Pods or Resource.
+  object ObjectMetricStatus
+  pods PodsMetricStatus
+  resource ResourceMetricStatus
+ObjectMetricStatus  A metric of another object.
+  target io.k8s.api.autoscaling.v1.CrossVersionObjectReference!
+  metricName string!
+  currentValue quantity!
+PodsMetricStatus  A per-pod metric averaged over the pods.
+  metricName string!
+  currentAverageValue quantity!
+ResourceMetricStatus  A resource metric averaged over the pods.
+  name string!
+  currentAverageUtilization integer
+  currentAverageValue quantity!
 MetricSpec  One autoscaling/v2beta1 metric target.
   type string!  Object, Pods or Resource.
   object ObjectMetricSource
   pods PodsMetricSource
   resource ResourceMetricSource
 ObjectMetricSource  A metric of another object.
-  target CrossVersionObjectReference!
+  target io.k8s.api.autoscaling.v1.CrossVersionObjectReference!
   metricName string!
   targetValue quantity!
 PodsMetricSource  A per-pod metric averaged over the pods.
@@ -1116,22 +1196,6 @@ ResourceMetricSource  A resource metric (cpu, memory, amd.com/gpu).
   name string!
   targetAverageUtilization integer
   targetAverageValue quantity
-HorizontalPodAutoscalerStatus  Observed state of an autoscaler.
-  observedGeneration long
-  lastScaleTime time
-  currentReplicas integer!
-  desiredReplicas integer!
-  currentCPUUtilizationPercentage integer
-  currentMetrics []object
-  conditions []object
-Scale +kind  The scale subresource.
-  spec ScaleSpec
-  status ScaleStatus
-ScaleSpec  Desired replicas.
-  replicas integer
-ScaleStatus  Observed replicas.
-  replicas integer!
-  selector string
 
 @io.k8s.api.policy.v1beta1
 PodDisruptionBudget +kind  Bounds voluntary disruptions of a set of pods.
@@ -1143,7 +1207,7 @@ PodDisruptionBudgetSpec  The bound.
   maxUnavailable ios
 PodDisruptionBudgetStatus  Observed state of a budget.
   observedGeneration long
-  disruptedPods {}time
+  disruptedPods {}time!
   disruptionsAllowed integer!
   currentHealthy integer!
   desiredHealthy integer!
@@ -1152,6 +1216,32 @@ Eviction +kind  A request to evict a pod, honouring disruption budgets.
   deleteOptions DeleteOptions
 
 @io.k8s.api.extensions.v1beta1
+Deployment +kind  extensions/v1beta1 form of a deployment (stored as apps/v1).
+  spec DeploymentSpec
+  status io.k8s.api.apps.v1.DeploymentStatus
+DeploymentSpec  Desired state of a deployment, with the v1beta1 rollback request.
+  replicas integer
+  selector io.k8s.apimachinery.pkg.apis.meta.v1.LabelSelector
+  template io.k8s.api.core.v1.PodTemplateSpec!
+  strategy io.k8s.api.apps.v1.DeploymentStrategy
+  minReadySeconds integer
+  revisionHistoryLimit integer
+  paused boolean
+  rollbackTo RollbackConfig  The revision to roll back to; cleared by the controller once done.
+  progressDeadlineSeconds integer
+RollbackConfig  A rollback target.
+  revision long  Revision to roll back to; 0 means the previous one.
+DaemonSet +kind  extensions/v1beta1 form of a daemon set (stored as apps/v1).
+  spec DaemonSetSpec
+  status io.k8s.api.apps.v1.DaemonSetStatus
+DaemonSetSpec  Desired state of a daemon set, with the v1beta1 template generation.
+  selector io.k8s.apimachinery.pkg.apis.meta.v1.LabelSelector
+  template io.k8s.api.core.v1.PodTemplateSpec!
+  updateStrategy io.k8s.api.apps.v1.DaemonSetUpdateStrategy
+  minReadySeconds integer
+  templateGeneration long  Generation of the template, kept for the OnDelete history.
+  revisionHistoryLimit integer
+
 Ingress +kind  HTTP routing into services.
   spec IngressSpec
   status IngressStatus
@@ -1195,6 +1285,9 @@ PodSecurityPolicySpec  The rules.
   defaultAllowPrivilegeEscalation boolean
   allowPrivilegeEscalation boolean
   allowedHostPaths []AllowedHostPath
+  allowedFlexVolumes []AllowedFlexVolume  Flexvolume drivers pods may use; empty allows all (when "flexVolume" is in volumes).
+AllowedFlexVolume  A Flexvolume driver pods may use.
+  driver string!  Name of the driver.
 HostPortRange  Allowed host ports.
   min integer!
   max integer!
@@ -1275,7 +1368,7 @@ CertificateSigningRequestCondition  Approved or Denied.
 Role +kind  Namespaced permissions.
   rules []PolicyRule!
 ClusterRole +kind  Cluster-wide permissions.
-  rules []PolicyRule  Empty for an aggregated role: the controller fills it from the selected roles.
+  rules []PolicyRule!  Empty for an aggregated role: the controller fills it from the selected roles.
   aggregationRule AggregationRule
 AggregationRule  Selects cluster roles whose rules are aggregated.
   clusterRoleSelectors []LabelSelector
@@ -1286,10 +1379,10 @@ PolicyRule  Allowed verbs on resources or URLs.
   resourceNames []string
   nonResourceURLs []string
 RoleBinding +kind  Grants a role within a namespace.
-  subjects []Subject
+  subjects []Subject!
   roleRef RoleRef!
 ClusterRoleBinding +kind  Grants a cluster role everywhere.
-  subjects []Subject
+  subjects []Subject!
   roleRef RoleRef!
 Subject  A user, group or service account.
   kind string!
@@ -1437,26 +1530,93 @@ CustomResourceDefinitionNames  Names of a custom resource.
   listKind string
   categories []string
 CustomResourceValidation  Validation schema.
-  openAPIV3Schema object
+  openAPIV3Schema JSONSchemaProps
+JSONSchemaProps  A JSON-Schema (draft 4, OpenAPI v3 subset) document; free-form below this point.
+  id string
+  $schema string
+  $ref string
+  description string
+  type string
+  format string
+  title string
+  default JSON
+  maximum number
+  exclusiveMaximum boolean
+  minimum number
+  exclusiveMinimum boolean
+  maxLength long
+  minLength long
+  pattern string
+  maxItems long
+  minItems long
+  uniqueItems boolean
+  multipleOf number
+  enum []JSON
+  maxProperties long
+  minProperties long
+  required []string
+  items JSONSchemaPropsOrArray
+  allOf []JSONSchemaProps
+  oneOf []JSONSchemaProps
+  anyOf []JSONSchemaProps
+  not JSONSchemaProps
+  properties {}JSONSchemaProps
+  additionalProperties JSONSchemaPropsOrBool
+  patternProperties {}JSONSchemaProps
+  dependencies {}JSONSchemaPropsOrStringArray
+  additionalItems JSONSchemaPropsOrBool
+  definitions {}JSONSchemaProps
+  externalDocs ExternalDocumentation
+  example JSON
+JSON  Any JSON value.
+  Raw byte!
+JSONSchemaPropsOrArray  A schema or an array of schemas.
+  Schema JSONSchemaProps!
+  JSONSchemas []JSONSchemaProps!
+JSONSchemaPropsOrBool  A schema or a boolean.
+  Allows boolean!
+  Schema JSONSchemaProps!
+JSONSchemaPropsOrStringArray  A schema or a list of property names.
+  Schema JSONSchemaProps!
+  Property []string!
+ExternalDocumentation  A link to more documentation.
+  description string
+  url string
+CustomResourceDefinitionCondition  One condition of a definition.
+  type string!  Established or NamesAccepted.
+  status string!
+  lastTransitionTime time
+  reason string
+  message string
 CustomResourceDefinitionStatus  Observed state of a definition.
-  conditions []object
-  acceptedNames CustomResourceDefinitionNames
+  conditions []CustomResourceDefinitionCondition!
+  acceptedNames CustomResourceDefinitionNames!
 
 @io.k8s.kube-aggregator.pkg.apis.apiregistration.v1beta1
 APIService +kind  A group version served by another server through the aggregator.
   spec APIServiceSpec
   status APIServiceStatus
 APIServiceSpec  Where the group version is served.
-  service ServiceReference
+  service ServiceReference!
   group string
   version string
   insecureSkipTLSVerify boolean
-  caBundle byte
+  caBundle byte!
   groupPriorityMinimum integer!
   versionPriority integer!
 ServiceReference  The serving service.
   namespace string
   name string
 APIServiceStatus  Availability.
-  conditions []object
+  conditions []APIServiceCondition
+APIServiceCondition  One condition of an API service.
+  type string!  Available.
+  status string!
+  lastTransitionTime time
+  reason string
+  message string
+
+@io.k8s.apimachinery.pkg.runtime
+RawExtension  An embedded object of any kind, carried as its own serialized bytes.
+  Raw byte!  The object's bytes (JSON or protobuf).
 """

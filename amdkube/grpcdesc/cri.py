@@ -55,7 +55,11 @@ enum MountPropagation { PROPAGATION_PRIVATE = 0; PROPAGATION_HOST_TO_CONTAINER =
 message Mount { string container_path = 1; string host_path = 2; bool readonly = 3; bool selinux_relabel = 4; MountPropagation propagation = 5; }
 message NamespaceOption { bool host_network = 1; bool host_pid = 2; bool host_ipc = 3; }
 message Int64Value { int64 value = 1; }
-message LinuxSandboxSecurityContext { NamespaceOption namespace_options = 1; bool readonly_rootfs = 4; bool privileged = 6; string seccomp_profile_path = 7; }
+message SELinuxOption { string user = 1; string role = 2; string type = 3; string level = 4; }
+message LinuxSandboxSecurityContext {
+  NamespaceOption namespace_options = 1; SELinuxOption selinux_options = 2; Int64Value run_as_user = 3; bool readonly_rootfs = 4;
+  repeated int64 supplemental_groups = 5; bool privileged = 6; string seccomp_profile_path = 7;
+}
 message LinuxPodSandboxConfig { string cgroup_parent = 1; LinuxSandboxSecurityContext security_context = 2; map<string, string> sysctls = 3; }
 message PodSandboxMetadata { string name = 1; string uid = 2; string namespace = 3; uint32 attempt = 4; }
 message PodSandboxConfig {
@@ -96,7 +100,7 @@ message LinuxContainerResources {
 }
 message Capability { repeated string add_capabilities = 1; repeated string drop_capabilities = 2; }
 message LinuxContainerSecurityContext {
-  Capability capabilities = 1; bool privileged = 2; NamespaceOption namespace_options = 3;
+  Capability capabilities = 1; bool privileged = 2; NamespaceOption namespace_options = 3; SELinuxOption selinux_options = 4;
   Int64Value run_as_user = 5; string run_as_username = 6; bool readonly_rootfs = 7;
   repeated int64 supplemental_groups = 8; string apparmor_profile = 9; string seccomp_profile_path = 10; bool no_new_privs = 11;
 }

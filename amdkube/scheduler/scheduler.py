@@ -31,6 +31,7 @@ from .predicates import DEFAULT_PREDICATES
 from .priorities import DEFAULT_PRIORITIES
 from .queue import SchedulingQueue
 
+NOMINATED_NODE_ANNOTATION = "NominatedNodeName"
 log = logging.getLogger("amdkube.scheduler")
 
 PROVIDERS = {
@@ -381,6 +382,9 @@ class Scheduler:
             except m.StatusError:
                 pass
         try:
-            await self.client.patch("pods", m.name_of(pod), {"status": {"nominatedNodeName": node}}, m.namespace_of(pod), sub="status")
+            # scheduler.go:227 — v1.9 records the nomination as a pod annotation
+            # (core.NominatedNodeAnnotationKey, generic_scheduler.go:66), not a status field
+            await self.client.patch("pods", m.name_of(pod), {"metadata": {"annotations": {NOMINATED_NODE_ANNOTATION: node}}},
+                                    m.namespace_of(pod))
         except m.StatusError:
             pass

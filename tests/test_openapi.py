@@ -14,7 +14,7 @@ from tests.conftest import ROOT, run
 
 def _refs(node, out):
     if isinstance(node, dict):
-        if "$ref" in node:
+        if isinstance(node.get("$ref"), str):       # (JSONSchemaProps has a *property* named $ref)
             out.add(node["$ref"].rsplit("/", 1)[1])
         for v in node.values():
             _refs(v, out)
@@ -36,10 +36,13 @@ def test_document_is_closed_and_covers_every_served_kind():
         assert oa.kind_definition(ri.api_version, ri.kind), ri
         base = ri.api_prefix() + ("/namespaces/{namespace}" if ri.namespaced else "") + f"/{ri.plural}"
         assert base in doc["paths"] and base + "/{name}" in doc["paths"], base
-    # served-only versions share their storage kind's definition
-    assert oa.kind_definition("extensions/v1beta1", "Deployment") == "io.k8s.api.apps.v1.Deployment"
+    # served-only versions share their storage kind's definition unless their shape differs
+    assert oa.kind_definition("apps/v1beta2", "Deployment") == "io.k8s.api.apps.v1.Deployment"
     gvks = defs["io.k8s.api.apps.v1.Deployment"]["x-kubernetes-group-version-kind"]
-    assert {"group": "extensions", "version": "v1beta1", "kind": "Deployment"} in gvks
+    assert {"group": "apps", "version": "v1beta2", "kind": "Deployment"} in gvks
+    assert oa.kind_definition("extensions/v1beta1", "Deployment") == "io.k8s.api.extensions.v1beta1.Deployment"
+    assert "rollbackTo" in defs["io.k8s.api.extensions.v1beta1.DeploymentSpec"]["properties"]
+    assert "rollbackTo" not in defs["io.k8s.api.apps.v1.DeploymentSpec"]["properties"]
     # the fork's device-granular fields
     assert defs["io.k8s.api.core.v1.Container"]["properties"]["extendedResourceRequests"]["items"] == {"type": "string"}
     assert defs["io.k8s.api.core.v1.PodSpec"]["properties"]["extendedResources"]["items"]["$ref"].endswith("PodExtendedResource")

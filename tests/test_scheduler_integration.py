@@ -183,10 +183,10 @@ def test_priority_preemption_frees_devices():
             end = loop.time() + 10
             while loop.time() < end:
                 h = await c.get("pods", "high", "default")
-                if (h.get("status") or {}).get("nominatedNodeName"):
+                if ((h.get("metadata") or {}).get("annotations") or {}).get("NominatedNodeName"):
                     break
                 await asyncio.sleep(0.02)
-            assert h["status"]["nominatedNodeName"] == "node-0000"
+            assert h["metadata"]["annotations"]["NominatedNodeName"] == "node-0000"
             # both 1-GPU victims are gone (or terminating); once removed, the 2-GPU pod binds
             for i in range(2):
                 v = await c.get_or_none("pods", f"low-{i}", "default")
