@@ -220,6 +220,10 @@ class AMDGPUPlugin(DevicePluginServer):
                 devs.append({"container_path": p, "host_path": p, "permissions": "rw"})
             if self.expose_card and g.get("card_minor") is not None:
                 p = f"{self.dev_root}/dri/card{g['card_minor']}"
+                # the primary node is optional for compute: hand it out only where the node has it
+                # (a container host may expose render nodes alone), never a path that is absent
+                if self.backend.name != "fake" and not os.path.exists(p):
+                    continue
                 devs.append({"container_path": p, "host_path": p, "permissions": "rw"})
         envs = {"ROCR_VISIBLE_DEVICES": ",".join(visibility_token(g) for g in gpus),
                 "AMD_GPU_DEVICE_IDS": ",".join(device_ids),
