@@ -1,7 +1,13 @@
 """Local image store for rocshim (CRI ImageService backend).
 
-There is no registry access on the target machines, so an "image" is a named, versioned
-entrypoint: a native binary, a script, or a directory with a `run` file. Built-in images
+Two kinds of image:
+  * rootfs — a real container image: a docker-archive (`docker save`) or OCI image layout,
+    pulled from a local path (`file:///…/image.tar` or an OCI directory). Its layers are
+    unpacked with whiteouts into a root filesystem and its config (Entrypoint, Cmd, Env,
+    WorkingDir, User) builds the container (runtime/oci.py; reference
+    pkg/kubelet/dockershim/docker_image.go:73, docker_container.go:88-172);
+  * scratch — a named, versioned entrypoint on the host: a native binary, a script, or a
+    directory with a `run` file (no registry access on the target machines). Built-in images
 map the e2e workloads to amdkube's gfx950 binaries (the reference's cuda-vector-add image,
 test/images/cuda-vector-add, becomes `rocm/vector-add`). Extra images are registered from
 `images.json` in the runtime's state dir or via PullImage of a local path (`file:///...`).
@@ -102,7 +108,31 @@ class ImageStore:
         return None
 
     def image_id(self, name: str) -> str:
-        return "sha256:" + hashlib.sha256(json.dumps(self.images[name], sort_keys=True).encode()).hexdigest()
+        spec = self.images[name]
+        if spec.get("kind") == "rootfs":
+            return spec["id"]          # the config digest, as docker reports it
+        return "sha256:" + hashlib.sha256(json.dumps(spec, sort_keys=True).encode()).hexdigest()
+
+    @staticmethod
+    def is_archive(path: str) -> bool:
+        if os.path.isdir(path):
+            return any(os.path.exists(os.path.join(path, f)) for f in ("index.json", "manifest.json")) and \
+                not os.path.exists(os.path.join(path, "run"))
+        import tarfile
+        try:
+            return os.path.isfile(path) and tarfile.is_tarfile(path)
+        except OSError:
+            return False
+
+    def _import(self, ref: str, path: str) -> str:
+        from .oci import import_image
+        rec = import_image(path, self.blob_root)
+        rec["size"] = _tree_size(rec["blob"])
+        names = [normalize(ref)] + [normalize(t) for t in rec.get("repo_tags") or []]
+        for n in names:
+            self.images[n] = rec
+        self._save()
+        return rec["id"]
 
     def _registry_image(self, ref: str) -> tuple[str, str] | None:
         """(image tree, registry root) of `ref` in the registry directory, or None."""
@@ -144,6 +174,8 @@ class ImageStore:
         if self.resolve(ref):
             return self.image_id(self.resolve(ref)[0])
         path = ref[len("file://"):] if ref.startswith("file://") else ref
+        if os.path.isabs(path) and os.path.exists(path) and self.is_archive(path):
+            return self._import(ref, path)
         if os.path.isabs(path) and os.path.exists(path):
             digest = hashlib.sha256(normalize(ref).encode()).hexdigest()[:32]
             blob = os.path.join(self.blob_root, digest)
@@ -173,11 +205,31 @@ class ImageStore:
         n = normalize(ref) if not ref.startswith("sha256:") else next(
             (k for k in self.images if self.image_id(k) == ref), ref)
         if n in self.images and n not in builtin_images():
-            blob = self.images[n].get("blob")
-            del self.images[n]
+            spec = self.images[n]
+            blob = spec.get("blob")
+            # a rootfs image is removed under every tag it was stored as (docker rmi by id)
+            for k in [k for k, v in self.images.items() if v is spec or (blob and v.get("blob") == blob)]:
+                del self.images[k]
             self._save()
             if blob and blob.startswith(self.blob_root + os.sep):
                 shutil.rmtree(blob, ignore_errors=True)
+            self._gc_layers()
+
+    def _gc_layers(self):
+        """Drop unpacked layer blobs no remaining image references (image GC frees layers)."""
+        d = os.path.join(self.blob_root, "layers")
+        if not os.path.isdir(d):
+            return
+        live = {lid.split(":", 1)[-1] for v in self.images.values() for lid in v.get("layers") or ()}
+        for f in os.listdir(d):
+            if f.endswith(".tar") and f[:-4] not in live:
+                try:
+                    os.unlink(os.path.join(d, f))
+                except OSError:
+                    pass
+
+    def layers(self, name: str) -> list[str]:
+        return list((self.images.get(name) or {}).get("layers") or [])
 
     def removable(self, name: str) -> bool:
         return name not in builtin_images()

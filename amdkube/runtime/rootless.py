@@ -1,0 +1,131 @@
+"""Run an image's program without a mount namespace (the unprivileged MI355X node has no user
+namespaces and no CAP_SYS_ADMIN, so it cannot pivot_root into the image).
+
+The program, its interpreter (`#!` line or the ELF PT_INTERP dynamic loader) and its shared
+libraries all come from the image's root filesystem: a dynamic executable is started as
+`<rootfs>/<PT_INTERP> --library-path <rootfs library dirs> <rootfs>/<program> args…`, so the
+image's own loader and libc run it, as they would under a chroot. What this cannot do is move
+absolute paths the program opens at run time (/etc/…, /data) under the image: those still
+resolve on the host, and volumes appear under $AMDKUBE_ROOTFS. Namespace-capable nodes
+(isolation=namespaces|userns) pivot_root into the image instead (native/nsexec.cpp --rootfs).
+"""
+from __future__ import annotations
+
+import os
+import struct
+
+LIB_DIRS = ("lib/x86_64-linux-gnu", "usr/lib/x86_64-linux-gnu", "lib64", "usr/lib64", "lib", "usr/lib",
+            "usr/local/lib")
+PT_INTERP = 3
+
+
+class RootfsExecError(OSError):
+    pass
+
+
+def _inside(root: str, p: str) -> str:
+    """Host path of container path `p` (absolute inside the image); symlinks are resolved
+    inside the image (an absolute link target is relative to the image root)."""
+    root = os.path.realpath(root)
+    parts = [x for x in p.split("/") if x and x != "."]
+    cur = root
+    hops = 0
+    while parts:
+        part = parts.pop(0)
+        if part == "..":
+            cur = os.path.dirname(cur) if cur != root else root
+            continue
+        nxt = os.path.join(cur, part)
+        if os.path.islink(nxt):
+            hops += 1
+            if hops > 40:
+                raise RootfsExecError(f"too many symlinks resolving {p}")
+            tgt = os.readlink(nxt)
+            parts = [x for x in tgt.split("/") if x and x != "."] + parts
+            cur = root if tgt.startswith("/") else cur
+            continue
+        cur = nxt
+    return cur
+
+
+def elf_interp(path: str) -> str | None:
+    """PT_INTERP of an ELF64 executable (None for a static binary); ValueError if not ELF."""
+    with open(path, "rb") as f:
+        head = f.read(64)
+        if head[:4] != b"\x7fELF":
+            raise ValueError("not an ELF file")
+        if head[4] != 2:
+            raise ValueError("only ELF64 images are supported")
+        end = "<" if head[5] == 1 else ">"
+        phoff, = struct.unpack(end + "Q", head[32:40])
+        phentsize, phnum = struct.unpack(end + "HH", head[54:58])
+        for i in range(phnum):
+            f.seek(phoff + i * phentsize)
+            ph = f.read(phentsize)
+            ptype, = struct.unpack(end + "I", ph[:4])
+            if ptype == PT_INTERP:
+                off, = struct.unpack(end + "Q", ph[8:16])
+                size, = struct.unpack(end + "Q", ph[32:40])
+                f.seek(off)
+                return f.read(size).rstrip(b"\x00").decode()
+    return None
+
+
+def library_dirs(root: str) -> list[str]:
+    out = []
+    for d in LIB_DIRS:
+        p = _inside(root, "/" + d)
+        if os.path.isdir(p) and p not in out:
+            out.append(p)
+    conf = _inside(root, "/etc/ld.so.conf.d")
+    if os.path.isdir(conf):
+        for fn in sorted(os.listdir(conf)):
+            try:
+                with open(os.path.join(conf, fn)) as f:
+                    for line in f:
+                        line = line.split("#", 1)[0].strip()
+                        if line.startswith("/") and os.path.isdir(_inside(root, line)):
+                            p = _inside(root, line)
+                            if p not in out:
+                                out.append(p)
+            except OSError:
+                pass
+    return out
+
+
+def resolve_program(root: str, prog: str, path_env: str, workdir: str = "/") -> str:
+    if "/" in prog:
+        host = _inside(root, prog if prog.startswith("/") else os.path.join(workdir, prog))
+        if os.path.isfile(host):
+            return host
+        raise RootfsExecError(f"{prog}: not found in the image")
+    for d in (path_env or "").split(":"):
+        if d.startswith("/"):
+            host = _inside(root, os.path.join(d, prog))
+            if os.path.isfile(host) and os.access(host, os.X_OK):
+                return host
+    raise RootfsExecError(f"{prog}: executable file not found in the image's $PATH")
+
+
+def rootfs_argv(root: str, argv: list[str], path_env: str, workdir: str = "/", depth: int = 0) -> list[str]:
+    """Host argv that runs container argv `argv` from image root `root`."""
+    if not argv:
+        raise RootfsExecError("no command")
+    if depth > 4:
+        raise RootfsExecError("interpreter chain too deep")
+    prog = resolve_program(root, argv[0], path_env, workdir)
+    with open(prog, "rb") as f:
+        head = f.read(256)
+    if head.startswith(b"#!"):
+        line = head[2:].split(b"\n", 1)[0].decode().strip().split(None, 1)
+        interp = [line[0]] + ([line[1]] if len(line) > 1 else [])
+        # the interpreter is the image's; the script it reads is passed by its host path
+        return rootfs_argv(root, interp + [prog] + list(argv[1:]), path_env, workdir, depth + 1)
+    interp = elf_interp(prog)
+    if interp is None:
+        return [prog] + list(argv[1:])
+    ld = _inside(root, interp)
+    if not os.path.isfile(ld):
+        raise RootfsExecError(f"{argv[0]}: the image has no dynamic loader {interp}")
+    return [ld, "--library-path", ":".join(library_dirs(root)), prog] + list(argv[1:])
+

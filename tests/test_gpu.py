@@ -114,6 +114,52 @@ def test_02c_device_guard_on_mi355x():
     run(go(), 300)
 
 
+def test_02d_rootfs_image_pod_on_mi355x(tmp_path):
+    """A real image: a docker archive built here from rocm-vector-add plus its shared-library
+    closure (everything but /opt/rocm, which comes from a hostPath volume and the rocm
+    handler), pulled from file://, runs as a GPU pod from the image's own loader and libc."""
+    import subprocess as sp
+    from amdkube.runtime.oci import write_docker_archive
+    vadd = os.path.join(BIN, "rocm-vector-add")
+    files = {vadd: "usr/local/bin/rocm-vector-add"}
+    for line in sp.run(["ldd", vadd], capture_output=True, text=True, check=True).stdout.splitlines():
+        for tok in line.split():
+            if tok.startswith("/") and os.path.exists(tok) and not tok.startswith("/opt/rocm"):
+                files[tok] = tok.lstrip("/")
+    entries, dirs = [], set()
+    for src, rel in sorted(files.items(), key=lambda kv: kv[1]):
+        d = os.path.dirname(rel)
+        while d and d not in dirs:
+            dirs.add(d)
+            d = os.path.dirname(d)
+        with open(os.path.realpath(src), "rb") as f:
+            entries.append((rel, f.read(), 0o755, None))
+    layer = [(d, None, 0o755, None) for d in sorted(dirs)] + entries
+    arch = str(tmp_path / "vadd-image.tar")
+    write_docker_archive(arch, [layer], {"Entrypoint": ["/usr/local/bin/rocm-vector-add"], "Cmd": ["--print-uuid"],
+                                         "Env": ["PATH=/usr/local/bin:/usr/bin:/bin"], "WorkingDir": "/"},
+                         ["amdkube/vadd-rootfs:r3"])
+
+    async def go():
+        async with LocalCluster(gpus="amdsmi", n_gpus=1, relist_period=0.5, with_controllers=False) as lc:
+            await lc.wait_gpus(1, 60)
+            pod = vadd_pod("image-pod")
+            c = pod["spec"]["containers"][0]
+            c["image"], c["imagePullPolicy"], c["args"] = f"file://{arch}", "IfNotPresent", []
+            c["volumeMounts"] = [{"name": "rocm", "mountPath": "/opt/rocm", "readOnly": True}]
+            pod["spec"]["volumes"] = [{"name": "rocm", "hostPath": {"path": "/opt/rocm"}}]
+            await lc.client.create(pod)
+            p = await wait_pod(lc.client, "default", "image-pod", ("Succeeded", "Failed"), 120)
+            logs = await lc.client.logs("default", "image-pod")
+            assert p["status"]["phase"] == "Succeeded" and "Test PASSED" in logs, (p["status"], logs)
+            [ct] = [x for x in lc.shim.containers.values() if x.name == "vadd"]
+            assert ct.resources.get("rootfs"), ct.resources      # ran from the unpacked image
+            [(name, spec)] = [(n, s) for n, s in lc.shim.images.images.items() if n.startswith("amdkube/vadd-rootfs")]
+            assert len(spec["layers"]) == 1 and spec["size"] > 0
+            print("rootfs image pod:", lc.shim.isolation, logs.strip().splitlines()[0])
+    run(go(), 300)
+
+
 def test_02b_legacy_accelerators_pod_on_real_gpu():
     """Accelerators gate (F22): alpha.kubernetes.io/amd-gpu from the real render nodes; the pod
     gets /dev/kfd + its render node + ROCR_VISIBLE_DEVICES and vector-add passes."""

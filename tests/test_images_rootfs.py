@@ -1,0 +1,221 @@
+"""Real container images: docker-archive / OCI-layout import, layer whiteouts, image config
+precedence, image GC of layers, and running an image (path-rooted on an unprivileged node,
+pivot_root into an overlay in namespace modes).
+
+Reference: dockershim PullImage (pkg/kubelet/dockershim/docker_image.go:73) and CreateContainer
+(docker_container.go:88-172) through dockerd; OCI image spec layer changesets (whiteouts)."""
+import asyncio
+import gzip
+import hashlib
+import io
+import json
+import os
+import shutil
+import subprocess
+import tarfile
+import tempfile
+
+import pytest
+
+from amdkube.grpcdesc.cri import CRI as C
+from amdkube.kubelet.cri_client import CRIClient
+from amdkube.runtime import RocShim
+from amdkube.runtime.images import NATIVE_BIN
+from amdkube.runtime.oci import ImageFormatError, apply_layer, import_image, write_docker_archive
+from amdkube.runtime.rootless import elf_interp, rootfs_argv
+from tests.conftest import run
+
+
+def host_closure(*progs) -> list[tuple]:
+    """Layer entries holding `progs` and their shared-library closure (ldd), at host paths."""
+    files = set()
+    for p in progs:
+        files.add(p)
+        out = subprocess.run(["ldd", p], capture_output=True, text=True).stdout
+        for line in out.splitlines():
+            parts = line.split()
+            for tok in parts:
+                if tok.startswith("/") and os.path.exists(tok):
+                    files.add(tok)
+    entries, dirs = [], set()
+    for f in sorted(files):
+        rel = f.lstrip("/")
+        d = os.path.dirname(rel)
+        while d and d not in dirs:
+            dirs.add(d)
+            d = os.path.dirname(d)
+        with open(os.path.realpath(f), "rb") as fh:
+            entries.append((rel, fh.read(), 0o755, None))
+    return [(d, None, 0o755, None) for d in sorted(dirs)] + entries
+
+
+def test_layer_whiteouts_opaque_and_replacement(tmp_path):
+    base = [("a", None, 0o755, None), ("a/x", b"x", 0o644, None), ("a/y", b"y", 0o644, None),
+            ("b", None, 0o755, None), ("b/old1", b"1", 0o644, None), ("b/sub", None, 0o755, None),
+            ("b/sub/old2", b"2", 0o644, None), ("c", b"file", 0o644, None), ("etc", None, 0o755, None),
+            ("etc/conf", b"v1", 0o644, None), ("lnk", b"", 0o777, "/etc/conf")]
+    top = [("a/.wh.x", b"", 0o644, None),            # delete a/x
+           ("b/.wh..wh..opq", b"", 0o644, None),     # hide everything lower layers put in b/
+           ("b/new", b"n", 0o644, None),
+           ("c", None, 0o755, None), ("c/inside", b"i", 0o644, None),   # file → directory
+           ("etc/conf", b"v2", 0o644, None)]
+    arch = tmp_path / "img.tar"
+    write_docker_archive(str(arch), [base, top], {"Entrypoint": ["/bin/true"]}, ["amdkube/test:1"])
+    rec = import_image(str(arch), str(tmp_path / "store"))
+    r = rec["rootfs"]
+    listing = sorted(os.path.relpath(os.path.join(dp, f), r) for dp, dn, fn in os.walk(r) for f in fn + dn)
+    assert listing == ["a", "a/y", "b", "b/new", "c", "c/inside", "etc", "etc/conf", "lnk"], listing
+    assert open(os.path.join(r, "etc/conf")).read() == "v2"
+    assert os.readlink(os.path.join(r, "lnk")) == "/etc/conf"      # absolute links stay (image-relative)
+    assert len(rec["layers"]) == 2 and all(x.startswith("sha256:") for x in rec["layers"])
+    assert rec["repo_tags"] == ["amdkube/test:1"] and rec["entrypoint"] == ["/bin/true"]
+
+
+@pytest.mark.parametrize("evil", [
+    [("../escape", b"x", 0o644, None)],
+    [("link", b"", 0o777, "/tmp"), ("link/pwned", b"x", 0o644, None)],     # write through a symlinked parent
+])
+def test_layer_cannot_write_outside_the_root(tmp_path, evil):
+    data = io.BytesIO()
+    with tarfile.open(fileobj=data, mode="w") as tf:
+        for name, body, mode, link in evil:
+            ti = tarfile.TarInfo(name)
+            ti.mode = mode
+            if link:
+                ti.type, ti.linkname = tarfile.SYMTYPE, link
+                tf.addfile(ti)
+            else:
+                ti.size = len(body)
+                tf.addfile(ti, io.BytesIO(body))
+    lp = tmp_path / "layer.tar"
+    lp.write_bytes(data.getvalue())
+    with pytest.raises(ImageFormatError):
+        apply_layer(str(lp), str(tmp_path / "root"))
+    assert not os.path.exists("/tmp/pwned") and not (tmp_path / "escape").exists()
+
+
+def _oci_layout(dirpath, layers, config):
+    """Write an OCI image layout (gzip layers) to `dirpath`."""
+    os.makedirs(os.path.join(dirpath, "blobs", "sha256"))
+
+    def put(b):
+        d = hashlib.sha256(b).hexdigest()
+        with open(os.path.join(dirpath, "blobs", "sha256", d), "wb") as f:
+            f.write(b)
+        return "sha256:" + d, len(b)
+    from amdkube.runtime.oci import _tar_bytes
+    descs, diffs = [], []
+    for entries in layers:
+        raw = _tar_bytes(entries)
+        diffs.append("sha256:" + hashlib.sha256(raw).hexdigest())
+        dg, n = put(gzip.compress(raw))
+        descs.append({"mediaType": "application/vnd.oci.image.layer.v1.tar+gzip", "digest": dg, "size": n})
+    cdg, cn = put(json.dumps({"architecture": "amd64", "os": "linux", "config": config,
+                              "rootfs": {"type": "layers", "diff_ids": diffs}}).encode())
+    mdg, mn = put(json.dumps({"schemaVersion": 2, "config": {"mediaType": "application/vnd.oci.image.config.v1+json",
+                                                             "digest": cdg, "size": cn}, "layers": descs}).encode())
+    with open(os.path.join(dirpath, "index.json"), "w") as f:
+        json.dump({"schemaVersion": 2, "manifests": [{"mediaType": "application/vnd.oci.image.manifest.v1+json",
+                                                      "digest": mdg, "size": mn,
+                                                      "annotations": {"org.opencontainers.image.ref.name": "oci/demo:2"}}]}, f)
+    with open(os.path.join(dirpath, "oci-layout"), "w") as f:
+        json.dump({"imageLayoutVersion": "1.0.0"}, f)
+
+
+def test_oci_layout_import_checks_digests(tmp_path):
+    lay = tmp_path / "oci"
+    _oci_layout(str(lay), [[("hello.txt", b"hi", 0o644, None)]], {"Cmd": ["cat", "/hello.txt"], "WorkingDir": "/w"})
+    rec = import_image(str(lay), str(tmp_path / "store"))
+    assert open(os.path.join(rec["rootfs"], "hello.txt")).read() == "hi"
+    assert rec["cmd"] == ["cat", "/hello.txt"] and rec["workdir"] == "/w" and rec["repo_tags"] == ["oci/demo:2"]
+    # a tampered blob fails the digest check
+    blobs = lay / "blobs" / "sha256"
+    layer = max(blobs.iterdir(), key=lambda p: p.stat().st_size if p.read_bytes()[:2] == b"\x1f\x8b" else -1)
+    layer.write_bytes(gzip.compress(b"tampered"))
+    with pytest.raises(ImageFormatError):
+        import_image(str(lay), str(tmp_path / "store2"))
+
+
+def test_rootfs_argv_runs_the_images_own_loader(tmp_path):
+    arch = tmp_path / "sh.tar"
+    write_docker_archive(str(arch), [host_closure("/bin/sh", "/bin/cat")], {"Entrypoint": ["/bin/sh", "-c"]}, [])
+    rec = import_image(str(arch), str(tmp_path / "store"))
+    assert elf_interp(os.path.join(rec["rootfs"], "bin/sh")).endswith("ld-linux-x86-64.so.2")
+    argv = rootfs_argv(rec["rootfs"], ["sh", "-c", "echo from-image"], "/usr/bin:/bin")
+    assert argv[0].startswith(rec["rootfs"]) and argv[1] == "--library-path"
+    assert subprocess.run(argv, capture_output=True, text=True).stdout.strip() == "from-image"
+
+
+def test_image_config_precedence_and_gc_through_cri(tmp_path):
+    arch = tmp_path / "app.tar"
+    layer = host_closure("/bin/sh") + [("srv", None, 0o755, None)]
+    write_docker_archive(str(arch), [layer], {"Entrypoint": ["/bin/sh", "-c"], "Cmd": ["echo CMD $GREETING; pwd"],
+                                              "Env": ["GREETING=from-image", "PATH=/usr/bin:/bin"], "WorkingDir": "/srv"},
+                         ["amdkube/app:1"])
+
+    async def go():
+        base = tempfile.mkdtemp(prefix="rsimg", dir="/tmp")
+        shim = await RocShim(os.path.join(base, "s.sock"), os.path.join(base, "state"), hooks_dir=os.path.join(base, "hooks")).start()
+        cri = await CRIClient(os.path.join(base, "s.sock")).connect()
+        try:
+            ref = await cri.pull_image(f"file://{arch}")
+            assert ref.startswith("sha256:")
+            before = (await cri.image_fs_info())[0].used_bytes.value
+            assert before > 0
+            assert os.listdir(os.path.join(base, "state", "images", "layers"))
+            sc = C.PodSandboxConfig(metadata=C.PodSandboxMetadata(name="p", uid="u1", namespace="default"))
+            sid = await cri.run_pod_sandbox(sc)
+            logs = {}
+            for name, cmd, args, envs in (("default", [], [], {}),                                   # Entrypoint + Cmd
+                                          ("args", [], ["echo ARGS $GREETING"], {"GREETING": "from-pod"}),  # Entrypoint + args
+                                          ("cmd", ["/bin/sh", "-c"], ["echo OWN"], {})):             # command replaces both
+                cfg = C.ContainerConfig(metadata=C.ContainerMetadata(name=name), image=C.ImageSpec(image="amdkube/app:1"),
+                                        command=cmd, args=args, envs=[C.KeyValue(key=k, value=v) for k, v in envs.items()])
+                cid = await cri.create_container(sid, cfg, sc)
+                await cri.start_container(cid)
+                for _ in range(300):
+                    st, _ = await cri.container_status(cid)
+                    if st.state == C.CONTAINER_EXITED:
+                        break
+                    await asyncio.sleep(0.01)
+                assert st.exit_code == 0, open(st.log_path).read()
+                logs[name] = open(st.log_path).read().split()
+            assert logs["default"][:2] == ["CMD", "from-image"] and logs["default"][2].endswith("/rootfs/srv")
+            assert logs["args"][:2] == ["ARGS", "from-pod"]
+            assert logs["cmd"] == ["OWN"]
+            await cri.stop_pod_sandbox(sid)
+            await cri.remove_pod_sandbox(sid)
+            await cri.remove_image(ref)
+            assert os.listdir(os.path.join(base, "state", "images", "layers")) == []   # layers freed
+            assert (await cri.image_fs_info())[0].used_bytes.value < before
+        finally:
+            await cri.close()
+            await shim.stop(kill_pods=True)
+            shutil.rmtree(base, ignore_errors=True)
+    run(go())
+
+
+@pytest.mark.skipif(os.geteuid() != 0, reason="pivot_root into an overlay needs root (or a user namespace)")
+def test_nsexec_pivots_into_the_image(tmp_path):
+    arch = tmp_path / "img.tar"
+    layer = host_closure("/bin/sh", "/bin/cat", "/bin/ls") + [("etc", None, 0o755, None), ("etc/marker", b"in-image", 0o644, None)]
+    write_docker_archive(str(arch), [layer], {}, [])
+    rec = import_image(str(arch), str(tmp_path / "store"))
+    vol = tmp_path / "vol"
+    vol.mkdir()
+    (vol / "data").write_text("volume-data")
+    upper = tmp_path / "ctr"
+    script = "cat /etc/marker; echo; cat /data/data; echo; for f in /dev/*; do printf '%s ' ${f#/dev/}; done; echo; echo w > /written; pwd"
+    p = subprocess.run([os.path.join(NATIVE_BIN, "amdkube-nsexec"), "--dev-root", "/dev", "--rootfs", rec["rootfs"],
+                        "--rootfs-upper", str(upper), "--workdir", "/etc", "--bind", f"{vol}:/data:ro", "--hide-kfd",
+                        "--", "/bin/sh", "-c", script], capture_output=True, text=True, timeout=30,
+                       env={"PATH": "/usr/bin:/bin"})
+    if p.returncode == 126 and "overlay" in p.stderr:
+        pytest.skip(f"no overlayfs here: {p.stderr.strip()}")
+    assert p.returncode == 0, p.stderr
+    out = p.stdout.splitlines()
+    assert out[0] == "in-image" and out[1] == "volume-data"
+    assert set(out[2].split()) >= {"null", "zero", "urandom", "shm"} and "kfd" not in out[2].split()
+    assert out[3] == "/etc"
+    # the write landed in the container's layer, not in the image
+    assert (upper / "upper" / "written").exists() and not os.path.exists(os.path.join(rec["rootfs"], "written"))
