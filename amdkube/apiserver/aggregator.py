@@ -28,6 +28,7 @@ from aiohttp import ClientSession, ClientTimeout, web
 
 from ..api import meta as m
 from ..api.scheme import SCHEME, _version_sort
+from ..utils import wait_event
 
 log = logging.getLogger("amdkube.aggregator")
 GROUP = "apiregistration.k8s.io"
@@ -224,10 +225,7 @@ class Aggregator:
                     rs.update("", m.name_of(cur), cur, subresource="status")
                 except Exception as e:    # noqa: BLE001 — one bad APIService must not stop the loop
                     log.debug("availability check of %s failed: %r", m.name_of(a), e)
-            try:
-                await asyncio.wait_for(self._dirty.wait(), period)
-            except asyncio.TimeoutError:
-                pass
+            await wait_event(self._dirty, period)
 
     async def close(self):
         if self._http is not None:

@@ -177,8 +177,8 @@ class CRDManager:
         return self
 
     async def stop(self):
-        if self._task is not None:
-            self._task.cancel()
+        from ..utils import cancel_and_wait
+        await cancel_and_wait([self._task])
 
     # ------------------------------------------------------------ serving
     def _install(self, crd: dict):

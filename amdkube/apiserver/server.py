@@ -385,9 +385,10 @@ class APIServer:
         return f"{'https' if self.tls else 'http'}://{self.host}:{self.port}"
 
     async def stop(self):
+        from ..utils import cancel_and_wait
+        await cancel_and_wait(self._bg)
         await self.aggregator.close()
-        for t in self._bg:
-            t.cancel()
+        await self.crds.stop()
         await self.webhooks.close()
         for w in self.store.all_watchers():
             w.close()

@@ -46,6 +46,7 @@ from ..volume import VolumeError
 from .kuberuntime import L_POD_UID, RuntimeManager, SandboxRef, apply_event
 from .qos import CRITICAL_ANNOTATION
 from .status import StatusManager, generate_status
+from ..utils import wait_event
 
 log = logging.getLogger("amdkube.kubelet")
 
@@ -439,16 +440,16 @@ class Kubelet:
         self._static_dirty.set()   # create mirror pods now that the API is there
 
     async def stop(self):
-        for t in self._tasks:
-            t.cancel()
+        from ..utils import cancel_and_wait
+        await cancel_and_wait(self._tasks)
         await self.volume_manager.stop()
         if self.informer:
             await self.informer.stop()
         if self.svc_informer is not None:
             await self.svc_informer.stop()
-        for w in self.workers.values():
-            if w.task:
-                w.task.cancel()
+        await cancel_and_wait([w.task for w in self.workers.values()])
+        if self._ckpt_chain is not None:
+            await asyncio.wait({self._ckpt_chain}, timeout=5)     # queued bootstrap-checkpoint writes land
         await self.status.stop()
         await self.recorder.stop()
         await self.dm.stop()
@@ -457,6 +458,7 @@ class Kubelet:
         for srv in getattr(self, "extra_servers", []):
             await srv.stop()
         await self.cri.close()
+        await self.client.close()
 
     # ================================================================ node
     def _capacity(self) -> dict:
@@ -595,10 +597,7 @@ class Kubelet:
 
     async def _node_status_loop(self):
         while True:
-            try:
-                await asyncio.wait_for(self._node_dirty.wait(), self.cfg.node_status_update_frequency)
-            except asyncio.TimeoutError:
-                pass
+            await wait_event(self._node_dirty, self.cfg.node_status_update_frequency)
             self._node_dirty.clear()
             try:
                 await self.update_node_status()
@@ -794,10 +793,7 @@ class Kubelet:
             period = self.cfg.file_check_frequency if self.cfg.pod_manifest_path else self.cfg.http_check_frequency
             if self.cfg.pod_manifest_path and self.cfg.manifest_url:
                 period = min(period, self.cfg.http_check_frequency)
-            try:
-                await asyncio.wait_for(self._static_dirty.wait(), period)
-            except asyncio.TimeoutError:
-                pass
+            await wait_event(self._static_dirty, period)
 
     async def _ensure_mirror(self, pod):
         """pkg/kubelet/pod/mirror_client.go: the API object that stands for a static pod."""

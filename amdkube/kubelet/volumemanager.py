@@ -35,6 +35,7 @@ from dataclasses import dataclass, field
 
 from ..api import meta as m
 from ..volume import PluginMgr, Spec, VolumeError, unescape_plugin_name
+from ..utils import wait_event
 
 log = logging.getLogger("amdkube.kubelet.volumemanager")
 
@@ -338,10 +339,7 @@ class VolumeManager:
 
     async def run(self):
         while True:
-            try:
-                await asyncio.wait_for(self._wake.wait(), self.period)
-            except asyncio.TimeoutError:
-                pass
+            await wait_event(self._wake, self.period)
             self._wake.clear()
             if not self.desired and not self.mounted and not self.attached:
                 continue

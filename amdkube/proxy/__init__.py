@@ -21,6 +21,7 @@ from ..utils.metrics import CONTENT_TYPE, MICRO_BUCKETS, Histogram, new_registry
 from .config import ChangeTracker, ServiceInfo, ServicePortName  # noqa: F401
 from .iptables import IptablesProxier
 from .userspace import LoadBalancerRR, UserspaceProxier  # noqa: F401
+from ..utils import wait_event
 
 log = logging.getLogger("amdkube.proxy")
 
@@ -101,10 +102,7 @@ class ProxyServer:
 
     async def _loop(self):
         while True:
-            try:
-                await asyncio.wait_for(self._wake.wait(), self.sync_period)
-            except asyncio.TimeoutError:
-                pass
+            await wait_event(self._wake, self.sync_period)
             self._wake.clear()
             if self.min_sync_period:
                 wait = self.last_sync + self.min_sync_period - time.time()

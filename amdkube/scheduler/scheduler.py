@@ -234,10 +234,8 @@ class Scheduler:
         await self.pod_inf.wait_synced(30)
 
     async def stop(self):
-        for t in self._tasks:
-            t.cancel()
-        for t in list(self._binds):
-            t.cancel()
+        from ..utils import cancel_and_wait
+        await cancel_and_wait(list(self._tasks) + list(self._binds))
         for inf in (self.pod_inf, self.node_inf, self.svc_inf, *getattr(self, "vol_infs", [])):
             if inf:
                 await inf.stop()
@@ -246,6 +244,7 @@ class Scheduler:
             await e.close()
         if self._runner:
             await self._runner.cleanup()
+        await self.client.close()
 
     async def _housekeeping(self):
         while True:

@@ -1,4 +1,6 @@
 import asyncio
+import gc
+import logging
 import os
 import sys
 
@@ -15,6 +17,37 @@ def pytest_configure(config):
     # native artefacts are not versioned: (re)build whatever is missing or stale (no-op when fresh)
     from native import build as nb
     nb.build(sanitize=True)
+
+
+# Shutdown hygiene: every component's stop() awaits its tasks and closes its sessions. asyncio
+# reports a leak through its logger (the loop's default exception handler); any such report
+# during a test fails it.
+_LEAK_MARKS = ("Task was destroyed but it is pending", "Unclosed client session", "Unclosed connector")
+
+
+class _LeakRecorder(logging.Handler):
+    def __init__(self):
+        super().__init__(logging.ERROR)
+        self.seen: list[str] = []
+
+    def emit(self, record):
+        msg = record.getMessage()
+        if msg.startswith(_LEAK_MARKS):
+            self.seen.append(msg.splitlines()[0] + " " + " ".join(msg.splitlines()[1:2])[:200])
+
+
+_LEAKS = _LeakRecorder()
+logging.getLogger("asyncio").addHandler(_LEAKS)
+
+
+@pytest.fixture(autouse=True)
+def no_leaked_tasks_or_sessions():
+    _LEAKS.seen.clear()
+    yield
+    gc.collect()
+    if _LEAKS.seen:
+        found, _LEAKS.seen[:] = list(_LEAKS.seen), []
+        pytest.fail("asyncio leak (a stop() that does not await its tasks or close its sessions):\n  " + "\n  ".join(found))
 
 
 def run(coro, timeout=60):

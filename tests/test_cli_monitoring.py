@@ -34,7 +34,10 @@ def server():
     t.start()
     ready.wait(10)
     yield box["srv"].url
+    asyncio.run_coroutine_threadsafe(box["srv"].stop(), loop).result(30)
     loop.call_soon_threadsafe(loop.stop)
+    t.join(10)
+    loop.close()
 
 
 def k(url, *args):
@@ -170,6 +173,7 @@ def test_hollow_nodes_gpu_density():
                 await n.stop()
             await sched.stop()
             await c.close()
+            await srv.stop()
             await srv.stop()
     run(go(), 120)
 
