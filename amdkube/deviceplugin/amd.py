@@ -35,6 +35,8 @@ from ..smi import Backend, device_id, visibility_token
 from ..smi.backend import parent_key, partition_count
 from .server import DevicePluginServer
 
+from ..smi.health import HEALTH_REASON_ATTR  # noqa: E402
+
 log = logging.getLogger("amdkube.deviceplugin.amd")
 
 RESOURCE = "amd.com/gpu"
@@ -114,6 +116,13 @@ def topology_label(gpus: list[dict], topo: list[list[dict]]) -> str:
     return json.dumps(out, separators=(",", ":"))
 
 
+def _attr_value(why: str) -> str:
+    """An attribute value must be a valid label value (≤ 63 chars of [-A-Za-z0-9_.])."""
+    import re
+    v = re.sub(r"[^-A-Za-z0-9_.]+", "_", why).strip("-_.")
+    return v[:63].rstrip("-_.") or "unhealthy"
+
+
 class AMDGPUPlugin(DevicePluginServer):
     def __init__(self, backend: Backend, resource_name: str = RESOURCE, plugins_dir: str = DEVICE_PLUGINS_PATH,
                  health_interval: float = 10.0, health_probe: str = "none", dev_root: str = "/dev",
@@ -133,6 +142,8 @@ class AMDGPUPlugin(DevicePluginServer):
         if len(self.by_id) != len(self.gpus):
             raise ValueError("device IDs are not unique on this node (partitions without distinct ids?)")
         self.reasons: dict[str, str] = {}
+        from ..smi.health import HealthMonitor
+        self.monitor = HealthMonitor(backend, ecc_threshold)
         self._task: asyncio.Task | None = None
         try:
             self.labels[TOPOLOGY_LABEL] = topology_label(node_gpus, backend.topology())
@@ -146,6 +157,8 @@ class AMDGPUPlugin(DevicePluginServer):
         self.devices = [{"ID": device_id(g), "health": HEALTHY, "Attributes": attributes(g)} for g in self.gpus]
 
     async def start(self):
+        for g in self.gpus:             # the RAS baseline new faults are judged against
+            self.monitor.snapshot(g["index"])
         if self.health_probe != "none":
             await self._probe_all()
         self._check_health(push=False)
@@ -154,8 +167,8 @@ class AMDGPUPlugin(DevicePluginServer):
         return self
 
     async def stop(self, grace: float = 0.5):
-        if self._task:
-            self._task.cancel()
+        from ..utils import cancel_and_wait
+        await cancel_and_wait([self._task])
         await super().stop(grace)
 
     # ------------------------------------------------------------------ health
@@ -163,14 +176,17 @@ class AMDGPUPlugin(DevicePluginServer):
         devs = []
         for d in self.devices:
             g = self.by_id[d["ID"]]
-            ok, why = self.backend.health(g["index"], self.ecc_threshold)
+            ok, why = self.monitor.check(g["index"])
             if d["ID"] in self.reasons and self.reasons[d["ID"]].startswith("probe:"):
                 ok, why = False, self.reasons[d["ID"]]
             self.reasons[d["ID"]] = "" if ok else why
             h = HEALTHY if ok else UNHEALTHY
             if h != d.get("health"):
                 log.warning("gpu %s is now %s %s", d["ID"], h, why)
-            devs.append(dict(d, health=h))
+            attrs = {k: v for k, v in d["Attributes"].items() if k != HEALTH_REASON_ATTR}
+            if not ok:     # why it was taken out of service, for kubectl describe node / the scheduler
+                attrs[HEALTH_REASON_ATTR] = _attr_value(why)
+            devs.append(dict(d, health=h, Attributes=attrs))
         if devs != self.devices:
             if push:
                 self.update(devs)

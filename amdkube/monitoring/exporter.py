@@ -41,6 +41,8 @@ class Exporter:
         self.node = node
         self.kubelet_url = kubelet_url
         self.ecc_threshold = ecc_threshold
+        from ..smi.health import HealthMonitor
+        self.monitor = HealthMonitor(backend, ecc_threshold)     # same judgement as the device plugin
         self.gpus = backend.gpus()
         self.sampling = backend.start_sampling()
         self.scrapes = 0
@@ -87,9 +89,20 @@ class Exporter:
                 up = 1
             except Exception:
                 s, up = {}, 0
-            healthy = 1 if up and s.get("ecc_uncorrectable", 0) <= self.ecc_threshold else 0
+            healthy = 1 if up and self.monitor.check(g["index"])[0] else 0
             add("amd_gpu_up", base, up, "1 if the GPU answered the last amd-smi query")
-            add("amd_gpu_health", base, healthy, "1 if the GPU is schedulable (no uncorrectable ECC errors)")
+            add("amd_gpu_health", base, healthy,
+                "1 if the GPU is schedulable (no new uncorrectable ECC/xGMI/bad-page faults since the exporter started)")
+            try:
+                ras = self.b.ras(g["index"]) if up else {}
+            except Exception:
+                ras = {}
+            if "xgmi_error" in ras:
+                add("amd_gpu_xgmi_error_status", base, ras["xgmi_error"], "xGMI error status (0 none, 1 error, 2 multiple)")
+            for state in ("retired", "pending", "unreservable"):
+                if f"bad_pages_{state}" in ras:
+                    add("amd_gpu_bad_pages", dict(base, state=state), ras[f"bad_pages_{state}"],
+                        "HBM pages the driver retired, has pending retirement, or could not reserve")
             add("amd_gpu_vram_total_bytes", base, int(g.get("vram_total_bytes") or 0), "Total HBM (VRAM) in bytes")
             for key, name, help_ in (("gfx_activity", "amd_gpu_utilization_percent", "GFX engine busy percent"),
                                      ("umc_activity", "amd_gpu_memory_utilization_percent", "Memory controller busy percent"),

@@ -144,6 +144,11 @@ class Backend:
     def link_metrics(self, index: int) -> list[dict]:
         return []
 
+    def ras(self, index: int) -> dict:
+        """RAS state beyond the ECC totals: xgmi_error (0 none, 1 error, 2 multiple),
+        bad_pages{,_retired,_pending,_unreservable}, bad_page_threshold; absent = unknown."""
+        return {}
+
     def start_sampling(self, period_ms: float = 100.0) -> bool:
         """Begin background activity sampling for average_activity(); False = not supported
         (callers then fall back to the instantaneous sample)."""
@@ -160,6 +165,8 @@ class Backend:
 
     # derived ------------------------------------------------------------
     def health(self, index: int, ecc_uncorrectable_threshold: int = 0) -> tuple[bool, str]:
+        """Stateless check against lifetime totals (kept for tools); the device plugin uses
+        smi.health.HealthMonitor, which judges NEW faults since it started."""
         try:
             s = self.sample(index)
         except Exception as e:  # a GPU we cannot even query is not schedulable
@@ -196,6 +203,10 @@ class AmdSmiBackend(Backend):
     def processes(self, index):
         with self._lock:
             return self.lib.processes(index)
+
+    def ras(self, index):
+        with self._lock:
+            return self.lib.ras(index)
 
     def link_metrics(self, index):
         with self._lock:
@@ -301,6 +312,7 @@ class FakeBackend(Backend):
             self.data["topology"] = [row[:n] for row in self.data["topology"][:n]]
         self.data = partition_fixture(self.data, compute_partition, memory_partition)
         self.samples = {g["index"]: dict(self.data.get("sample_defaults", {})) for g in self.data["gpus"]}
+        self.ras_state: dict[int, dict] = {}
         self.procs: dict[int, list] = {}
         self.sampling = False
         self.history: dict[int, collections.deque] = {i: collections.deque(maxlen=1024) for i in self.samples}
@@ -330,9 +342,28 @@ class FakeBackend(Backend):
         return [{"peer_bdf": k, "type": "xgmi", "bit_rate_gbps": 32, "max_bandwidth_gbps": 1224,
                  "read_kb": 0, "write_kb": 0} for k in peers]
 
+    def ras(self, index):
+        if index not in self.samples:
+            raise SMIError(f"gpu {index} not found")
+        r = self.ras_state.setdefault(index, {"xgmi_error": 0, "bad_pages": 0, "bad_pages_retired": 0,
+                                              "bad_pages_pending": 0, "bad_pages_unreservable": 0,
+                                              "bad_page_threshold": 512})
+        return dict(r)
+
     # fault injection
     def inject_ecc(self, index, uncorrectable=1):
         self.samples[index]["ecc_uncorrectable"] = self.samples[index].get("ecc_uncorrectable", 0) + uncorrectable
+
+    def inject_xgmi_error(self, index, status=1):
+        self.ras(index)
+        self.ras_state[index]["xgmi_error"] = status
+
+    def inject_bad_page(self, index, pending=1, retired=0):
+        r = self.ras(index)
+        r = self.ras_state[index]
+        r["bad_pages_pending"] += pending
+        r["bad_pages_retired"] += retired
+        r["bad_pages"] += pending + retired
 
     def set_sample(self, index, **kw):
         self.samples[index].update(kw)

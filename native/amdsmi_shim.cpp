@@ -239,6 +239,68 @@ py::dict sample(size_t i) {
   return d;
 }
 
+// RAS state beyond the ECC totals: xGMI error status, retired/pending bad pages, the bad-page
+// threshold and which blocks have ECC enabled. Each query's status is reported (`*_status`)
+// so callers can tell "no errors" from "not supported here" or "needs root".
+py::dict ras(size_t i) {
+  auto h = gpu(i);
+  py::dict d;
+  amdsmi_xgmi_status_t xs = AMDSMI_XGMI_STATUS_NO_ERRORS;
+  uint32_t nbad = 0, nres = 0, thr = 0;
+  uint64_t ecc_mask = 0;
+  std::vector<amdsmi_retired_page_record_t> recs;
+  amdsmi_status_t s_x, s_b, s_r, s_t, s_e, s_bb = AMDSMI_STATUS_SUCCESS;
+  amdsmi_error_count_t xe;
+  amdsmi_status_t s_xe;
+  {
+    py::gil_scoped_release nogil;
+    s_x = amdsmi_gpu_xgmi_error_status(h, &xs);
+    s_b = amdsmi_get_gpu_bad_page_info(h, &nbad, nullptr);
+    if (s_b == AMDSMI_STATUS_SUCCESS && nbad > 0) {
+      recs.resize(nbad);
+      s_bb = amdsmi_get_gpu_bad_page_info(h, &nbad, recs.data());
+      recs.resize(s_bb == AMDSMI_STATUS_SUCCESS ? nbad : 0);
+    }
+    s_r = amdsmi_get_gpu_memory_reserved_pages(h, &nres, nullptr);
+    s_t = amdsmi_get_gpu_bad_page_threshold(h, &thr);
+    s_e = amdsmi_get_gpu_ecc_enabled(h, &ecc_mask);
+    std::memset(&xe, 0, sizeof(xe));
+    s_xe = amdsmi_get_gpu_ecc_count(h, AMDSMI_GPU_BLOCK_XGMI_WAFL, &xe);
+  }
+  auto st = [](amdsmi_status_t s) {
+    const char* msg = nullptr;
+    amdsmi_status_code_to_string(s, &msg);
+    return std::string(msg ? msg : "?");
+  };
+  d["xgmi_error_status"] = st(s_x);
+  if (s_x == AMDSMI_STATUS_SUCCESS) d["xgmi_error"] = static_cast<int>(xs);
+  d["bad_pages_status"] = st(s_b == AMDSMI_STATUS_SUCCESS ? s_bb : s_b);
+  if (s_b == AMDSMI_STATUS_SUCCESS) {
+    int reserved = 0, pending = 0, unreservable = 0;
+    for (auto& r : recs) {
+      if (r.status == AMDSMI_MEM_PAGE_STATUS_RESERVED) ++reserved;
+      else if (r.status == AMDSMI_MEM_PAGE_STATUS_PENDING) ++pending;
+      else ++unreservable;
+    }
+    d["bad_pages"] = nbad;
+    d["bad_pages_retired"] = reserved;
+    d["bad_pages_pending"] = pending;
+    d["bad_pages_unreservable"] = unreservable;
+  }
+  d["reserved_pages_status"] = st(s_r);
+  if (s_r == AMDSMI_STATUS_SUCCESS) d["reserved_pages"] = nres;
+  d["bad_page_threshold_status"] = st(s_t);
+  if (s_t == AMDSMI_STATUS_SUCCESS) d["bad_page_threshold"] = thr;
+  d["ecc_enabled_status"] = st(s_e);
+  if (s_e == AMDSMI_STATUS_SUCCESS) d["ecc_enabled_blocks"] = ecc_mask;
+  d["xgmi_ecc_status"] = st(s_xe);
+  if (s_xe == AMDSMI_STATUS_SUCCESS) {
+    d["xgmi_ecc_correctable"] = xe.correctable_count;
+    d["xgmi_ecc_uncorrectable"] = xe.uncorrectable_count;
+  }
+  return d;
+}
+
 py::list list_gpus() {
   py::list out;
   for (size_t i = 0; i < count(); ++i) out.append(describe(i));
@@ -377,6 +439,7 @@ PYBIND11_MODULE(_amdsmi, m) {
   m.def("describe", &describe);
   m.def("list_gpus", &list_gpus);
   m.def("sample", &sample);
+  m.def("ras", &ras);
   m.def("topology", &topology);
   m.def("link_metrics", &link_metrics);
   m.def("processes", &processes);

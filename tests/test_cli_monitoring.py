@@ -91,12 +91,16 @@ def test_exporter_metrics_and_attribution():
     async def go():
         fb = FakeBackend(n=2)
         fb.set_sample(1, gfx_activity=87, vram_used_bytes=123)
-        fb.inject_ecc(0)
+        fb.inject_ecc(1)                        # historical error on GPU 1: not a new fault
         ex = Exporter(fb, node="n1")
+        ex.collect({})                          # baseline
+        fb.inject_ecc(0)                        # a NEW uncorrectable error on GPU 0
         from amdkube.smi import device_id
         text = ex.collect({device_id(fb.gpus()[1]): ("ml", "trainer", "c")})
         assert 'amd_gpu_health{gpu="0"' in text and text.count("amd_gpu_health{") == 2
         assert [l for l in text.splitlines() if l.startswith('amd_gpu_health{gpu="0"')][0].endswith(" 0")
+        assert [l for l in text.splitlines() if l.startswith('amd_gpu_health{gpu="1"')][0].endswith(" 1")
+        assert 'amd_gpu_xgmi_error_status{gpu="0"' in text and 'amd_gpu_bad_pages{gpu="0"' in text
         assert 'amd_gpu_utilization_percent{gpu="1",uuid="GPU-5b4a01c0d1e2f3a1",node="n1",model="AMD Instinct MI355X",namespace="ml",pod="trainer",container="c"} 87' in text
         assert 'container_accelerator_duty_cycle{container_name="c",pod_name="trainer",namespace="ml"' in text
         assert "amd_gpu_xgmi_link_write_bytes_total" in text

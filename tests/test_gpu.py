@@ -45,6 +45,29 @@ def test_01_amdsmi_backend_enumerates_mi355x():
     b.close()
 
 
+def test_01b_ras_queries_and_new_fault_health():
+    """The real RAS state reads without error (xGMI error status, bad pages, threshold, ECC
+    blocks; "not supported"/"no permission" are legitimate answers on a VM or without root),
+    and the delta monitor keeps the healthy part Healthy."""
+    from amdkube.smi import AmdSmiBackend
+    from amdkube.smi.health import HealthMonitor
+    b = AmdSmiBackend()
+    try:
+        r = b.ras(0)
+        print("ras:", r)
+        ok_states = ("SUCCESS", "NOT_SUPPORTED", "NO_PERM", "NOT_YET_IMPLEMENTED", "FILE_ERROR")
+        for k in ("xgmi_error_status", "bad_pages_status", "reserved_pages_status", "bad_page_threshold_status",
+                  "ecc_enabled_status", "xgmi_ecc_status"):
+            assert any(st in r[k] for st in ok_states), (k, r[k])
+        if "xgmi_error" in r:
+            assert r["xgmi_error"] in (0, 1, 2)
+        hm = HealthMonitor(b)
+        hm.snapshot(0)
+        assert hm.check(0) == (True, ""), hm.check(0)
+    finally:
+        b.close()
+
+
 def test_02_gpu_pod_runs_on_its_assigned_device():
     async def go():
         async with LocalCluster(gpus="amdsmi", n_gpus=1, relist_period=0.5, with_controllers=False) as lc:

@@ -1,0 +1,84 @@
+"""Device health judged on NEW faults (smi/health.py), published as a device attribute, with
+the reference's consequences: the kubelet refuses new pods on an Unhealthy device and leaves
+running ones alone (pkg/kubelet/cm/devicemanager/device_store.go:103-110,
+manager_store.go:116-118; test/e2e_node/gpu_device_plugin.go keeps running pods untouched)."""
+import asyncio
+
+from amdkube.localcluster import LocalCluster, wait_pod
+from amdkube.smi import FakeBackend
+from amdkube.smi.health import HEALTH_REASON_ATTR, HealthMonitor
+from tests.conftest import run
+
+
+def test_historical_errors_do_not_mark_a_part_unhealthy():
+    fb = FakeBackend(n=2)
+    fb.inject_ecc(0, uncorrectable=5)          # last year's errors
+    fb.inject_bad_page(0, pending=0, retired=3)
+    hm = HealthMonitor(fb, ecc_threshold=0)
+    hm.snapshot(0)
+    assert hm.check(0) == (True, "")
+    fb.inject_ecc(0)                           # a fresh one on a part already above the threshold
+    ok, why = hm.check(0)
+    assert not ok and "+1 since the plugin started" in why and "lifetime 6" in why
+    fb.samples[0]["ecc_uncorrectable"] = 5     # stays out of service until a new baseline
+    assert hm.check(0)[0] is False
+
+
+def test_xgmi_and_bad_page_faults():
+    fb = FakeBackend(n=3)
+    hm = HealthMonitor(fb)
+    for i in range(3):
+        hm.snapshot(i)
+    fb.inject_xgmi_error(0)
+    fb.inject_bad_page(1, pending=2)
+    fb.ras_state.setdefault(2, fb.ras(2))
+    fb.ras_state[2].update(bad_pages=512, bad_pages_retired=512)
+    assert hm.check(0) == (False, "xGMI link error")
+    assert hm.check(1) == (False, "2 new bad page(s) pending retirement")
+    ok, why = hm.check(2)
+    assert not ok and "threshold 512" in why
+
+
+def test_ecc_threshold_allows_a_budget():
+    fb = FakeBackend(n=1)
+    hm = HealthMonitor(fb, ecc_threshold=2)
+    hm.snapshot(0)
+    fb.inject_ecc(0, 2)
+    assert hm.check(0)[0]
+    fb.inject_ecc(0, 1)
+    assert not hm.check(0)[0]
+
+
+def test_fault_flips_device_publishes_reason_and_spares_the_running_pod():
+    async def go():
+        async with LocalCluster(gpus="fake", n_gpus=2, relist_period=0.2, node_status_update_frequency=0.2,
+                                with_controllers=False) as lc:
+            lc.plugin.health_interval = 0.1
+            fb = lc.backend
+            await lc.wait_gpus(2, 30)
+            pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "runner", "namespace": "default"},
+                   "spec": {"restartPolicy": "Never", "containers": [{"name": "c", "image": "busybox",
+                            "command": ["sleep", "30"], "resources": {"limits": {"amd.com/gpu": "1"}}}]}}
+            await lc.client.create(pod)
+            p = await wait_pod(lc.client, "default", "runner", ("Running",), 30)
+            [did] = p["spec"]["extendedResources"][0]["assigned"]
+            idx = lc.plugin.by_id[did]["index"]
+            fb.inject_xgmi_error(idx)
+            dev = None
+            for _ in range(200):
+                node = await lc.client.get("nodes", lc.node_name)
+                dev = node["status"]["extendedResources"]["amd.com/gpu"]["resources"][did]
+                if dev["health"] == "Unhealthy":
+                    break
+                await asyncio.sleep(0.05)
+            assert dev["health"] == "Unhealthy", dev
+            assert dev["attributes"][HEALTH_REASON_ATTR] == "xGMI_link_error"
+            # the running pod is left alone
+            p = await lc.client.get("pods", "runner", "default")
+            assert p["status"]["phase"] == "Running"
+            # a new 1-GPU pod lands on the healthy GPU, never the flagged one
+            pod["metadata"]["name"] = "next"
+            await lc.client.create(pod)
+            p2 = await wait_pod(lc.client, "default", "next", ("Running",), 30)
+            assert p2["spec"]["extendedResources"][0]["assigned"] != [did]
+    run(go(), 90)
