@@ -9,8 +9,9 @@ already above a threshold would hide every new error. So the monitor snapshots e
 state when it starts and flags:
 
   * uncorrectable ECC errors above `ecc_threshold` SINCE the snapshot (deferred errors too);
-  * an xGMI error status that was clear at the snapshot (link errors: the multi-GPU collectives
-    of a pod placed across this GPU would fail or crawl);
+  * an xGMI error status that was clear at the snapshot, or new uncorrectable errors in the
+    XGMI_WAFL RAS block (link errors: the multi-GPU collectives of a pod placed across this GPU
+    would fail or crawl);
   * new pages pending retirement or unreservable (memory the driver could not retire);
   * the bad-page count reaching the driver's bad-page threshold (the RAS EEPROM's limit:
     the part needs service);
@@ -75,6 +76,11 @@ class HealthMonitor:
             return f"deferred ECC errors: +{ddef} since the plugin started"
         if cur.get("xgmi_error", 0) and not base.get("xgmi_error", 0):
             return "xGMI link error" if cur["xgmi_error"] == 1 else "multiple xGMI link errors"
+        # the XGMI_WAFL RAS block's uncorrectable count: the same fault where the error-status
+        # file is not readable (the MI355X gpurun box answers that query with INVAL)
+        dx = cur.get("ras_xgmi_ecc_uncorrectable", 0) - base.get("ras_xgmi_ecc_uncorrectable", 0)
+        if dx > self.ecc_threshold:
+            return f"xGMI link uncorrectable errors: +{dx} since the plugin started"
         for k, what in (("bad_pages_pending", "pending retirement"), ("bad_pages_unreservable", "unreservable")):
             d = cur.get(k, 0) - base.get(k, 0)
             if d > 0:

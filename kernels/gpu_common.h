@@ -206,6 +206,29 @@ __global__ __launch_bounds__(256) void mfma_burn_kernel(float* __restrict__ out,
   out[static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x] = s;
 }
 
+// One wave computes C[32x32] = A[32xK] * B[Kx32] (bf16 in, fp32 out) with the burn's MFMA,
+// v_mfma_f32_32x32x16_bf16, K/16 chained steps. Operand lane maps (CDNA4): lane l, r = l&31,
+// h = l>>5 holds A[r][8h+j] and B[8h+j][r] (j = 0..7); accumulator register q of lane l is
+// C[(q&3) + 8(q>>2) + 4h][r]. The numerics check of the matrix-core path: the same layout the
+// burn relies on, against a torch fp32 matmul (tests/test_gpu.py).
+__global__ __launch_bounds__(64) void mfma_tile_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
+                                                       float* __restrict__ C, int k_steps) {
+  const int l = threadIdx.x, r = l & 31, h = l >> 5;
+  const int K = 16 * k_steps;
+  f32x16 acc = {};
+  for (int ks = 0; ks < k_steps; ++ks) {
+    bf16x8 a, b;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a[j] = A[r * K + ks * 16 + 8 * h + j];
+      b[j] = B[(ks * 16 + 8 * h + j) * 32 + r];
+    }
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) C[((q & 3) + 8 * (q >> 2) + 4 * h) * 32 + r] = acc[q];
+}
+
 // ---------------------------------------------------------------------------- runners
 inline int stream_grid(size_t items, int cu_count, int per_cu = 8) {
   size_t want = (items + 255) / 256;
@@ -271,6 +294,95 @@ inline VaddResult run_vector_add(size_t n, int dev) {
   }
   r.ok = r.mismatches == 0;
   return r;
+}
+
+// ---- host-supplied data: the kernels on caller-provided inputs (numerics vs torch fp32)
+struct DevBuf {
+  void* p = nullptr;
+  explicit DevBuf(size_t n) { AK_HIP(hipMalloc(&p, n ? n : 16)); }
+  ~DevBuf() { hipFree(p); }
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+};
+
+// c = a + b on the device with the pod workload's vadd_kernel
+inline std::vector<float> vector_add_host(const std::vector<float>& a, const std::vector<float>& b, int dev) {
+  if (a.size() != b.size()) throw std::invalid_argument("a and b differ in length");
+  AK_HIP(hipSetDevice(dev));
+  const size_t n = a.size(), bytes = n * sizeof(float);
+  DevBuf da(bytes), db(bytes), dc(bytes);
+  AK_HIP(hipMemcpy(da.p, a.data(), bytes, hipMemcpyHostToDevice));
+  AK_HIP(hipMemcpy(db.p, b.data(), bytes, hipMemcpyHostToDevice));
+  const int grid = stream_grid((n + 3) / 4, dev_info(dev).cu_count);
+  hipLaunchKernelGGL(vadd_kernel, dim3(grid), dim3(256), 0, 0, static_cast<const float*>(da.p),
+                     static_cast<const float*>(db.p), static_cast<float*>(dc.p), n);
+  AK_HIP(hipGetLastError());
+  std::vector<float> c(n);
+  AK_HIP(hipMemcpy(c.data(), dc.p, bytes, hipMemcpyDeviceToHost));
+  return c;
+}
+
+// the HBM probe's write pattern for n16 16-byte words (checked against a torch re-derivation)
+inline std::vector<uint32_t> hbm_pattern_host(size_t n16, uint32_t seed, int dev) {
+  AK_HIP(hipSetDevice(dev));
+  DevBuf d(n16 * 16);
+  const int grid = stream_grid(n16, dev_info(dev).cu_count, HBM_BLOCKS_PER_CU);
+  hipLaunchKernelGGL(hbm_write_kernel, dim3(grid), dim3(256), 0, 0, static_cast<v4u*>(d.p), n16, seed);
+  AK_HIP(hipGetLastError());
+  std::vector<uint32_t> out(n16 * 4);
+  AK_HIP(hipMemcpy(out.data(), d.p, n16 * 16, hipMemcpyDeviceToHost));
+  return out;
+}
+
+// the probe's verify kernel on caller data: mismatching 32-bit words against the pattern
+inline unsigned long long hbm_verify_host(const std::vector<uint32_t>& words, uint32_t seed, int dev) {
+  if (words.size() % 4) throw std::invalid_argument("need a whole number of 16-byte words");
+  AK_HIP(hipSetDevice(dev));
+  const size_t n16 = words.size() / 4;
+  DevBuf d(n16 * 16), e(sizeof(unsigned long long));
+  AK_HIP(hipMemcpy(d.p, words.data(), n16 * 16, hipMemcpyHostToDevice));
+  AK_HIP(hipMemset(e.p, 0, sizeof(unsigned long long)));
+  const int grid = stream_grid(n16, dev_info(dev).cu_count, HBM_BLOCKS_PER_CU);
+  hipLaunchKernelGGL(hbm_verify_kernel, dim3(grid), dim3(256), 0, 0, static_cast<const v4u*>(d.p), n16, seed,
+                     static_cast<unsigned long long*>(e.p));
+  AK_HIP(hipGetLastError());
+  unsigned long long bad = 0;
+  AK_HIP(hipMemcpy(&bad, e.p, sizeof(bad), hipMemcpyDeviceToHost));
+  return bad;
+}
+
+// the probe's copy kernel on caller data
+inline std::vector<uint32_t> hbm_copy_host(const std::vector<uint32_t>& words, int dev) {
+  if (words.size() % 4) throw std::invalid_argument("need a whole number of 16-byte words");
+  AK_HIP(hipSetDevice(dev));
+  const size_t n16 = words.size() / 4;
+  DevBuf s(n16 * 16), d(n16 * 16);
+  AK_HIP(hipMemcpy(s.p, words.data(), n16 * 16, hipMemcpyHostToDevice));
+  const int grid = stream_grid(n16, dev_info(dev).cu_count, HBM_BLOCKS_PER_CU);
+  hipLaunchKernelGGL(hbm_copy_kernel, dim3(grid), dim3(256), 0, 0, static_cast<const v4u*>(s.p), static_cast<v4u*>(d.p),
+                     n16);
+  AK_HIP(hipGetLastError());
+  std::vector<uint32_t> out(words.size());
+  AK_HIP(hipMemcpy(out.data(), d.p, n16 * 16, hipMemcpyDeviceToHost));
+  return out;
+}
+
+// C[32x32] fp32 = A[32xK] bf16 * B[Kx32] bf16 on one wave (K a multiple of 16, <= 1024)
+inline std::vector<float> mfma_tile_host(const std::vector<uint16_t>& a_bits, const std::vector<uint16_t>& b_bits,
+                                         int k, int dev) {
+  if (k <= 0 || k % 16 || k > 1024) throw std::invalid_argument("K must be a positive multiple of 16, at most 1024");
+  if (a_bits.size() != static_cast<size_t>(32 * k) || b_bits.size() != static_cast<size_t>(32 * k))
+    throw std::invalid_argument("A must be 32xK and B Kx32 bf16");
+  AK_HIP(hipSetDevice(dev));
+  DevBuf da(a_bits.size() * 2), db(b_bits.size() * 2), dc(32 * 32 * sizeof(float));
+  AK_HIP(hipMemcpy(da.p, a_bits.data(), a_bits.size() * 2, hipMemcpyHostToDevice));
+  AK_HIP(hipMemcpy(db.p, b_bits.data(), b_bits.size() * 2, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(mfma_tile_kernel, dim3(1), dim3(64), 0, 0, static_cast<const __bf16*>(da.p),
+                     static_cast<const __bf16*>(db.p), static_cast<float*>(dc.p), k / 16);
+  AK_HIP(hipGetLastError());
+  std::vector<float> c(32 * 32);
+  AK_HIP(hipMemcpy(c.data(), dc.p, c.size() * sizeof(float), hipMemcpyDeviceToHost));
+  return c;
 }
 
 struct HbmResult {

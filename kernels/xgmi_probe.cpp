@@ -3,7 +3,9 @@
 // The reference has no collective or interconnect awareness at all. For
 // topology-aware placement amdkube needs ground truth: this probe runs, over every GPU
 // visible to the pod (one process, one communicator via ncclCommInitAll), an all-reduce
-// bus-bandwidth sweep and a pairwise hipMemcpyPeer matrix. On an 8x MI355X node every GPU
+// bus-bandwidth sweep and a pairwise hipMemcpyPeer matrix. Before timing anything it checks
+// the collective's RESULT: rank i fills element e with (i+1) + 0.5*(e%7) (exact in fp32), and
+// after a sum all-reduce every rank must hold n(n+1)/2 + 0.5*n*(e%7) in every element. On an 8x MI355X node every GPU
 // pair has one direct xGMI link (7 links x ~153 GB/s per GPU), so a ring all-reduce over k
 // GPUs is per-link bound; the probe reports algbw and busbw = algbw * 2(k-1)/k.
 //   xgmi-probe [--max-mib M] [--iters K] [--no-p2p]
@@ -17,6 +19,7 @@
 #include <stdexcept>
 #include <string>
 #include <vector>
+#include <sstream>
 
 #define CHECK_HIP(x)                                                                          \
   do {                                                                                        \
@@ -28,6 +31,22 @@
     ncclResult_t r = (x);                                                                         \
     if (r != ncclSuccess) throw std::runtime_error(std::string(#x) + ": " + ncclGetErrorString(r)); \
   } while (0)
+
+__global__ void fill_rank(float* buf, size_t count, int rank) {
+  for (size_t e = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; e < count;
+       e += static_cast<size_t>(gridDim.x) * blockDim.x)
+    buf[e] = static_cast<float>(rank + 1) + 0.5f * static_cast<float>(e % 7);
+}
+
+__global__ void count_wrong(const float* buf, size_t count, int n, unsigned long long* bad) {
+  unsigned long long b = 0;
+  for (size_t e = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; e < count;
+       e += static_cast<size_t>(gridDim.x) * blockDim.x) {
+    float want = 0.5f * n * (n + 1) + 0.5f * n * static_cast<float>(e % 7);
+    b += buf[e] != want;
+  }
+  if (b) atomicAdd(bad, b);
+}
 
 int main(int argc, char** argv) {
   size_t max_mib = 256;
@@ -42,7 +61,10 @@ int main(int argc, char** argv) {
     int n = 0;
     CHECK_HIP(hipGetDeviceCount(&n));
     if (n < 1) throw std::runtime_error("no GPUs visible");
-    std::printf("{\"gpus\":%d,\"allreduce\":[", n);
+    std::ostringstream js;   // printed once at the end: RCCL writes its banner to stdout at init
+    char tmp[256];
+    std::snprintf(tmp, sizeof tmp, "{\"gpus\":%d,", n);
+    js << tmp;
     std::vector<ncclComm_t> comms(n);
     std::vector<int> devs(n);
     for (int i = 0; i < n; ++i) devs[i] = i;
@@ -56,6 +78,39 @@ int main(int argc, char** argv) {
       CHECK_HIP(hipMemset(buf[i], 0, max_bytes));
       CHECK_HIP(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
     }
+    // correctness: rank-dependent values, sum all-reduce, every element checked on every rank
+    const size_t vcount = (max_bytes < (64u << 20) ? max_bytes : (64u << 20)) / sizeof(float);
+    unsigned long long wrong_total = 0;
+    {
+      for (int i = 0; i < n; ++i) {
+        CHECK_HIP(hipSetDevice(i));
+        hipLaunchKernelGGL(fill_rank, dim3(1024), dim3(256), 0, st[i], buf[i], vcount, i);
+        CHECK_HIP(hipGetLastError());
+      }
+      CHECK_NCCL(ncclGroupStart());
+      for (int i = 0; i < n; ++i) CHECK_NCCL(ncclAllReduce(buf[i], buf[i], vcount, ncclFloat, ncclSum, comms[i], st[i]));
+      CHECK_NCCL(ncclGroupEnd());
+      for (int i = 0; i < n; ++i) {
+        CHECK_HIP(hipSetDevice(i));
+        unsigned long long* bad = nullptr;
+        CHECK_HIP(hipMalloc(&bad, sizeof(*bad)));
+        CHECK_HIP(hipMemsetAsync(bad, 0, sizeof(*bad), st[i]));
+        hipLaunchKernelGGL(count_wrong, dim3(1024), dim3(256), 0, st[i], buf[i], vcount, n, bad);
+        CHECK_HIP(hipGetLastError());
+        unsigned long long h = 0;
+        CHECK_HIP(hipMemcpyAsync(&h, bad, sizeof(h), hipMemcpyDeviceToHost, st[i]));
+        CHECK_HIP(hipStreamSynchronize(st[i]));
+        CHECK_HIP(hipFree(bad));
+        wrong_total += h;
+      }
+      std::snprintf(tmp, sizeof tmp, "\"verify\":{\"elements\":%zu,\"ranks\":%d,\"wrong\":%llu},", vcount, n, wrong_total);
+      js << tmp;
+      for (int i = 0; i < n; ++i) {
+        CHECK_HIP(hipSetDevice(i));
+        CHECK_HIP(hipMemset(buf[i], 0, max_bytes));
+      }
+    }
+    js << "\"allreduce\":[";
     bool first = true;
     for (size_t bytes = 1 << 20; bytes <= max_bytes; bytes <<= 2) {
       size_t count = bytes / sizeof(float);
@@ -78,13 +133,14 @@ int main(int argc, char** argv) {
       double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / iters;
       double alg = bytes / s / 1e9;
       double bus = n > 1 ? alg * 2.0 * (n - 1) / n : alg;
-      std::printf("%s{\"bytes\":%zu,\"us\":%.1f,\"algbw_gbps\":%.2f,\"busbw_gbps\":%.2f}", first ? "" : ",", bytes, s * 1e6,
-                  alg, bus);
+      std::snprintf(tmp, sizeof tmp, "%s{\"bytes\":%zu,\"us\":%.1f,\"algbw_gbps\":%.2f,\"busbw_gbps\":%.2f}", first ? "" : ",",
+                    bytes, s * 1e6, alg, bus);
+      js << tmp;
       first = false;
     }
-    std::printf("],\"p2p_gbps\":[");
+    js << "],\"p2p_gbps\":[";
     for (int i = 0; i < n; ++i) {
-      std::printf("%s[", i ? "," : "");
+      js << (i ? ",[" : "[");
       for (int j = 0; j < n; ++j) {
         double gbps = 0;
         if (p2p && i != j) {
@@ -104,16 +160,23 @@ int main(int argc, char** argv) {
             gbps = bytes / s / 1e9;
           }
         }
-        std::printf("%s%.1f", j ? "," : "", gbps);
+        std::snprintf(tmp, sizeof tmp, "%s%.1f", j ? "," : "", gbps);
+        js << tmp;
       }
-      std::printf("]");
+      js << "]";
     }
-    std::printf("]}\n");
+    js << "]}";
+    std::fflush(stdout);
+    std::printf("%s\n", js.str().c_str());
     for (int i = 0; i < n; ++i) {
       ncclCommDestroy(comms[i]);
       hipSetDevice(i);
       hipFree(buf[i]);
       hipStreamDestroy(st[i]);
+    }
+    if (wrong_total) {
+      std::fprintf(stderr, "xgmi-probe: all-reduce returned %llu wrong elements\n", wrong_total);
+      return 5;
     }
     return 0;
   } catch (const std::exception& e) {

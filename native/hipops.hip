@@ -3,6 +3,7 @@
 // The AMD device plugin uses these as its health probe (HBM pattern check before a GPU
 // is advertised Healthy) and the GPU test tier uses them to check the kernels against a
 // host fp32 reference. Kernels live in kernels/gpu_common.h (shared with the pod binaries).
+#include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -66,6 +67,62 @@ PYBIND11_MODULE(_hipops, m) {
         return o;
       },
       py::arg("mib") = 1024, py::arg("iters") = 5, py::arg("device") = 0);
+  // caller-supplied data (numpy arrays, e.g. torch.Tensor.numpy()) → the same kernels
+  m.def(
+      "vector_add_arrays",
+      [](py::array_t<float, py::array::c_style | py::array::forcecast> a,
+         py::array_t<float, py::array::c_style | py::array::forcecast> b, int dev) {
+        std::vector<float> va(a.data(), a.data() + a.size()), vb(b.data(), b.data() + b.size()), vc;
+        {
+          py::gil_scoped_release nogil;
+          vc = amdkube::vector_add_host(va, vb, dev);
+        }
+        return py::array_t<float>(vc.size(), vc.data());
+      },
+      py::arg("a"), py::arg("b"), py::arg("device") = 0);
+  m.def(
+      "hbm_pattern",
+      [](size_t n16, uint32_t seed, int dev) {
+        std::vector<uint32_t> w;
+        {
+          py::gil_scoped_release nogil;
+          w = amdkube::hbm_pattern_host(n16, seed, dev);
+        }
+        return py::array_t<uint32_t>(w.size(), w.data());
+      },
+      py::arg("n16"), py::arg("seed") = 0x5eedu, py::arg("device") = 0);
+  m.def(
+      "hbm_verify_words",
+      [](py::array_t<uint32_t, py::array::c_style | py::array::forcecast> words, uint32_t seed, int dev) {
+        std::vector<uint32_t> w(words.data(), words.data() + words.size());
+        py::gil_scoped_release nogil;
+        return amdkube::hbm_verify_host(w, seed, dev);
+      },
+      py::arg("words"), py::arg("seed") = 0x5eedu, py::arg("device") = 0);
+  m.def(
+      "hbm_copy_words",
+      [](py::array_t<uint32_t, py::array::c_style | py::array::forcecast> words, int dev) {
+        std::vector<uint32_t> w(words.data(), words.data() + words.size()), o;
+        {
+          py::gil_scoped_release nogil;
+          o = amdkube::hbm_copy_host(w, dev);
+        }
+        return py::array_t<uint32_t>(o.size(), o.data());
+      },
+      py::arg("words"), py::arg("device") = 0);
+  m.def(
+      "mfma_tile",
+      [](py::array_t<uint16_t, py::array::c_style | py::array::forcecast> a_bits,
+         py::array_t<uint16_t, py::array::c_style | py::array::forcecast> b_bits, int k, int dev) {
+        std::vector<uint16_t> a(a_bits.data(), a_bits.data() + a_bits.size()), b(b_bits.data(), b_bits.data() + b_bits.size());
+        std::vector<float> c;
+        {
+          py::gil_scoped_release nogil;
+          c = amdkube::mfma_tile_host(a, b, k, dev);
+        }
+        return py::array_t<float>({32, 32}, c.data());
+      },
+      py::arg("a_bits"), py::arg("b_bits"), py::arg("k"), py::arg("device") = 0);
   m.def(
       "mfma_burn",
       [](double ms, int dev) {

@@ -106,11 +106,23 @@ def test_many_gpu_pods_never_double_assigned():
             done = {}
             for n in names:
                 done[n] = await wait_pod(c, "default", n, ("Succeeded",), 40)
-            # at no time were two running pods on one GPU: check via kubelet start/finish intervals
+            # at no time were two running pods on one GPU: the runtime's own nanosecond start/exit
+            # times of every container, grouped by the render node it was given
             spans = {}
-            for n, p in done.items():
-                gid = p["spec"]["extendedResources"][0]["assigned"][0]
-                cs = p["status"]["containerStatuses"][0]["state"]["terminated"]
-                spans.setdefault(gid, []).append((cs["startedAt"], cs["finishedAt"]))
-            assert len(spans) <= 4
+            pod_of = {}
+            for ct in lc.shim.containers.values():
+                render = [d["host_path"] for d in ct.devices if "/dri/render" in d["host_path"]]
+                if not render:
+                    continue
+                assert len(render) == 1 and ct.started_at and ct.finished_at, vars(ct)
+                spans.setdefault(render[0], []).append((ct.started_at, ct.finished_at))
+                pod_of[ct.id] = ct.sandbox_id
+            assert sum(len(v) for v in spans.values()) == 12 and len(spans) <= 4, spans
+            for dev, iv in spans.items():
+                iv.sort()
+                for (s0, e0), (s1, e1) in zip(iv, iv[1:]):
+                    assert e0 <= s1, f"two pods ran on {dev} at once: [{s0}, {e0}] overlaps [{s1}, {e1}]"
+            # and the API agrees on who had which GPU
+            gids = [p["spec"]["extendedResources"][0]["assigned"][0] for p in done.values()]
+            assert len(set(gids)) <= 4
     run(go(), 120)

@@ -39,6 +39,18 @@ def test_xgmi_and_bad_page_faults():
     assert not ok and "threshold 512" in why
 
 
+def test_xgmi_block_errors_when_the_status_file_is_unreadable():
+    fb = FakeBackend(n=1)
+    hm = HealthMonitor(fb)
+    fb.ras(0)
+    fb.ras_state[0].pop("xgmi_error")
+    fb.ras_state[0]["xgmi_ecc_uncorrectable"] = 4      # historical
+    hm.snapshot(0)
+    assert hm.check(0)[0]
+    fb.ras_state[0]["xgmi_ecc_uncorrectable"] = 5
+    assert hm.check(0) == (False, "xGMI link uncorrectable errors: +1 since the plugin started")
+
+
 def test_ecc_threshold_allows_a_budget():
     fb = FakeBackend(n=1)
     hm = HealthMonitor(fb, ecc_threshold=2)
