@@ -19,6 +19,10 @@ from ..scheduler import Scheduler
 from ..smi import FakeBackend, device_id
 
 
+def m_name(p: dict) -> str:
+    return (p.get("metadata") or {}).get("name", "")
+
+
 def fake_node(i: int, gpus: int, backend: FakeBackend | None):
     st = {"capacity": {"cpu": "4", "memory": "32Gi", "pods": "110"}, "allocatable": {"cpu": "4", "memory": "32Gi", "pods": "110"},
           "conditions": [{"type": "Ready", "status": "True", "lastHeartbeatTime": "2030-01-01T00:00:00Z"}]}
@@ -46,13 +50,32 @@ def pod(i: int, gpu: bool):
             "spec": {"containers": [c]}}
 
 
-async def run_schedperf(n_nodes=100, n_pods=3000, gpus_per_node=8, gpu_pods=True, create_concurrency=64):
+def bound_pod(i: int, n_nodes: int):
+    """An existing pod already running on a node (scheduler_bench_test.go makeBasePod + NodeName):
+    it occupies the node's cpu/memory/pod slots the scheduler must account for."""
+    p = pod(i, False)
+    p["metadata"]["name"] = f"existing-{i:06d}"
+    p["spec"]["nodeName"] = f"node-{i % n_nodes:04d}"
+    return p
+
+
+async def run_schedperf(n_nodes=100, n_pods=3000, gpus_per_node=8, gpu_pods=True, create_concurrency=64,
+                        existing_pods=0):
+    """scheduler_test.go (100 nodes / 3000 pods) and scheduler_bench_test.go:32-55 (100/1000
+    nodes × 0/1000 existing pods): `existing_pods` are bound before the clock starts."""
     api = await APIServer(event_ttl=3600).start()
     client = Client(api.url, pool=128)
     fb = FakeBackend()
     try:
         for i in range(n_nodes):
             await client.create(fake_node(i, gpus_per_node, fb))
+        if existing_pods:
+            esem = asyncio.Semaphore(create_concurrency)
+
+            async def mk_existing(i):
+                async with esem:
+                    await client.create(bound_pod(i, n_nodes))
+            await asyncio.gather(*(mk_existing(i) for i in range(existing_pods)))
         sched = await Scheduler(Client(api.url, pool=256)).start()
         sched.recorder.enabled = False  # events are not on the measured path in scheduler_perf either
         # gpu_pods=True: every pod asks for a GPU (capped at the GPUs there are); "mixed": the
@@ -86,6 +109,7 @@ async def run_schedperf(n_nodes=100, n_pods=3000, gpus_per_node=8, gpu_pods=True
         await creator
         # verify: no device handed out twice
         items, _ = await client.list("pods", "default")
+        items = [p for p in items if not m_name(p).startswith("existing-")]
         seen, dup = set(), 0
         for p in items:
             for pres in (p.get("spec") or {}).get("extendedResources") or []:
@@ -94,7 +118,9 @@ async def run_schedperf(n_nodes=100, n_pods=3000, gpus_per_node=8, gpu_pods=True
                     seen.add(d)
         # no full interval (everything scheduled within 1 s of the 1 % mark): the run's own rate
         tail_rate = (sched.scheduled - prev) / max(1e-9, time.perf_counter() - t_start) if not samples else None
-        res = {"nodes": n_nodes, "pods": want, "gpu_pods": gpu_pods, "scheduled": sched.scheduled, "elapsed_s": round(el, 3),
+        res = {"nodes": n_nodes, "existing_pods": existing_pods, "pods": want, "gpu_pods": gpu_pods,
+               "gpu_pods_scheduled": sum(1 for p in items if (p.get("spec") or {}).get("extendedResources")),
+               "scheduled": sched.scheduled, "elapsed_s": round(el, 3),
                "avg_pods_per_s": round(sched.scheduled / el, 1),
                "min_interval_pods_per_s": round(min(samples), 1) if samples else round(tail_rate, 1),
                "intervals": samples,
@@ -105,3 +131,19 @@ async def run_schedperf(n_nodes=100, n_pods=3000, gpus_per_node=8, gpu_pods=True
     finally:
         await client.close()
         await api.stop()
+
+
+def main(argv=None):
+    import argparse
+    ap = argparse.ArgumentParser("amdkube scheduler_perf")
+    ap.add_argument("--nodes", type=int, default=100)
+    ap.add_argument("--pods", type=int, default=3000)
+    ap.add_argument("--existing", type=int, default=0, help="pods bound to nodes before the measured run")
+    ap.add_argument("--gpu-pods", default="mixed", choices=("mixed", "all", "none"))
+    a = ap.parse_args(argv)
+    gp = {"mixed": "mixed", "all": True, "none": False}[a.gpu_pods]
+    print(json.dumps(asyncio.run(run_schedperf(a.nodes, a.pods, gpu_pods=gp, existing_pods=a.existing))), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -26,6 +26,47 @@ def matching_free(pi, ni, rname, selector, exclude=()) -> list[str]:
     return [d for d, dev in avail.items() if d not in exclude and selector.matches(dev.get("attributes") or {})]
 
 
+def _shared_selectors(pi) -> bool:
+    """True when two requests draw on one resource name and one of them has a selector: the
+    per-request count check can then pass although no disjoint assignment exists."""
+    seen: dict[str, bool] = {}
+    for _, rname, _n, sel in pi.ext:
+        if rname in seen and (not sel.empty() or seen[rname]):
+            return True
+        seen[rname] = seen.get(rname, False) or not sel.empty()
+    return False
+
+
+def _match(pi, ni, exclude=()) -> dict | None:
+    """Exact feasibility: a disjoint assignment of devices to every request (each request of
+    n devices is n slots; bipartite matching by augmenting paths — tiny graphs: ≤ 8 devices
+    per resource on an MI355X node, 64 with CPX partitions). {pres name: [ids]} or None."""
+    slots, cands = [], []
+    for pname, rname, n, sel in pi.ext:
+        c = matching_free(pi, ni, rname, sel, exclude)
+        for _ in range(n):
+            slots.append(pname)
+            cands.append(c)
+    owner: dict[str, int] = {}
+
+    def augment(i, seen):
+        for d in cands[i]:
+            if d in seen:
+                continue
+            seen.add(d)
+            if d not in owner or augment(owner[d], seen):
+                owner[d] = i
+                return True
+        return False
+    for i in range(len(slots)):
+        if not augment(i, set()):
+            return None
+    out: dict[str, list[str]] = {}
+    for d, i in sorted(owner.items()):
+        out.setdefault(slots[i], []).append(d)
+    return out
+
+
 def fits(pi, ni) -> tuple[bool, list[str]]:
     if pi.ext_error:
         return False, [pi.ext_error]
@@ -37,6 +78,9 @@ def fits(pi, ni) -> tuple[bool, list[str]]:
         need[rname] = need.get(rname, 0) + n
         if len(cand) < n or len(ni.available_devices(rname)) < need[rname]:
             return False, [f"Insufficient {rname}"]
+    if _shared_selectors(pi) and _match(pi, ni) is None:
+        # overlapping selectors on one resource name: the counts fit, no disjoint choice does
+        return False, [f"Insufficient {pi.ext[0][1]}"]
     return True, []
 
 
@@ -47,10 +91,13 @@ def allocate(pi, ni, use_topology: bool = True) -> dict | None:
     binding = {}
     taken: set[str] = set()
     t = ni.topology() if use_topology else None
-    for pname, rname, n, sel in pi.ext:
+    # most constrained request first, so a narrow selector is not starved by a wide one
+    order = sorted(pi.ext, key=lambda e: len(matching_free(pi, ni, e[1], e[3]))) if _shared_selectors(pi) else pi.ext
+    for pname, rname, n, sel in order:
         cand = matching_free(pi, ni, rname, sel, taken)
         if len(cand) < n:
-            return None
+            m = _match(pi, ni)       # the greedy order failed: take any disjoint assignment
+            return {k: {"resources": v} for k, v in m.items()} if m is not None else None
         chosen = None
         if t is not None:
             ids, index, numa, link, parent = t

@@ -214,6 +214,7 @@ class GenericScheduler:
         if not fit:
             raise FitError(pod, len(nodes), failed)
         trace.step("Prioritizing")
+        scores = None
         if len(fit) == 1:
             host = fit[0]
         else:
@@ -222,7 +223,17 @@ class GenericScheduler:
             host = self.select_host(fit, scores)
         binding = extended.allocate(pi, host, self.use_topology) if pi.ext else {}
         if binding is None:
-            raise FitError(pod, len(nodes), {host.name: ["device allocation failed"]})
+            # the device choice failed on the best host: the next-ranked hosts get their turn
+            failed_alloc = {host.name: ["device allocation failed"]}
+            order = sorted(range(len(fit)), key=lambda i: -scores[i]) if scores is not None else range(len(fit))
+            for alt in (fit[i] for i in order if fit[i] is not host):
+                binding = extended.allocate(pi, alt, self.use_topology)
+                if binding is not None:
+                    host = alt
+                    break
+                failed_alloc[alt.name] = ["device allocation failed"]
+            if binding is None:
+                raise FitError(pod, len(nodes), failed_alloc)
         vol = getattr(pi, "vol", None)
         if vol is not None and vol.delayed and self.volume_scheduling:
             from .volumes import match_delayed

@@ -81,7 +81,7 @@ def node_affinity(pi, nodes, ctx=None):
 def taint_toleration(pi, nodes, ctx=None):
     tols = [t for t in pi.tolerations if t.get("effect") in (None, "", "PreferNoSchedule")]
     raw = [sum(1 for t in ni.taints if t.get("effect") == "PreferNoSchedule" and not tolerations_tolerate_taint(tols, t))
-           for ni in nodes]
+           if ni.taints else 0 for ni in nodes]
     mx = max(raw) if raw else 0
     return [MAX * (1 - r / mx) if mx else MAX for r in raw]
 

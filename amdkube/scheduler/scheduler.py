@@ -301,12 +301,12 @@ class Scheduler:
             return
         self.m_algo.observe((time.perf_counter() - t0) * 1e6)
         # assume: nodeName + chosen devices (fix #1: devices are reserved before the bind)
-        assumed = json.loads(json.dumps(pod))
-        assumed["spec"]["nodeName"] = host
-        if binding and self.gates("ReserveDevicesOnAssume"):
-            for pres in assumed["spec"].get("extendedResources") or []:
-                if pres.get("name") in binding:
-                    pres["assigned"] = list(binding[pres["name"]]["resources"])
+        # a structural copy of only what assume changes (the informer's object is never mutated)
+        spec = dict(pod.get("spec") or {}, nodeName=host)
+        if binding and self.gates("ReserveDevicesOnAssume") and spec.get("extendedResources"):
+            spec["extendedResources"] = [dict(pres, assigned=list(binding[pres["name"]]["resources"]))
+                                         if pres.get("name") in binding else pres for pres in spec["extendedResources"]]
+        assumed = dict(pod, spec=spec)
         try:
             self.cache.assume_pod(assumed)
         except KeyError:

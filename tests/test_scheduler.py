@@ -231,3 +231,42 @@ def test_policy_file(tmp_path):
                              "priorities": [{"name": "GPUTopologyPriority", "weight": 3}]}))
     preds, prios, exts = load_policy(str(p))
     assert preds == ["GeneralPredicates"] and prios == {"GPUTopologyPriority": 3} and exts == []
+
+
+def test_overlapping_selectors_on_one_resource_name():
+    """Two requests of amd.com/gpu whose selectors overlap: the per-request counts fit on node
+    'a' (1 big GPU each) but no disjoint assignment exists there; the pod goes to 'b'."""
+    big = [{"key": "amd.com/gpu-memory", "operator": "Gt", "values": ["100000"]}]
+    a = node("a", gpus=2, mem=[294912, 1024])
+    b = node("b", gpus=2, mem=[294912, 294912])
+    c, g = sched([a, b])
+    p = pod(multi=[("r1", 1, big), ("r2", 1, big)])
+    pi = PodInfo(p)
+    assert extended.fits(pi, c.nodes["a"]) == (False, ["Insufficient amd.com/gpu"])
+    assert extended.fits(pi, c.nodes["b"])[0]
+    host, binding = run(g.schedule(p))
+    assert host == "b"
+    assert {binding["r1"]["resources"][0], binding["r2"]["resources"][0]} == set(c.nodes["b"].available_devices("amd.com/gpu"))
+    # a narrow selector next to a wide one on the same node: allocate serves the narrow one first
+    wide = PodInfo(pod(multi=[("w", 1, None), ("n", 1, big)]))
+    bind = extended.allocate(wide, c.nodes["a"])
+    big_id = [d for d, dv in c.nodes["a"].available_devices("amd.com/gpu").items()
+              if dv["attributes"]["amd.com/gpu-memory"] == "294912"][0]
+    assert bind["n"]["resources"] == [big_id] and bind["w"]["resources"] != [big_id]
+
+
+def test_allocation_failure_tries_the_next_ranked_host(monkeypatch):
+    c, g = sched([node("a", gpus=8), node("b", gpus=8)])
+    real = extended.allocate
+    tried = []
+
+    def flaky(pi, ni, use_topology=True):
+        tried.append(ni.name)
+        return None if len(tried) == 1 else real(pi, ni, use_topology)
+    monkeypatch.setattr(extended, "allocate", flaky)
+    host, binding = run(g.schedule(pod(gpus=2)))
+    assert tried[0] != host and len(tried) == 2 and len(binding["gpus"]["resources"]) == 2
+    monkeypatch.setattr(extended, "allocate", lambda *a, **k: None)
+    with pytest.raises(FitError) as e:
+        run(g.schedule(pod("q", gpus=2)))
+    assert set(e.value.failed) == {"a", "b"}
