@@ -22,6 +22,7 @@ from ..api import meta as m
 from ..api.labels import is_dns1123_label, is_dns1123_subdomain
 from ..api.scheme import SCHEME, ResourceInfo
 from ..store import PUT
+from ..store.storage import decode_kv
 
 FINALIZER = "customresourcecleanup.apiextensions.k8s.io"
 PREFIX = "/registry/customresourcedefinitions/"
@@ -167,7 +168,7 @@ class CRDManager:
         registry.store.commit_hooks.append(self._on_commit)
         kvs, _, _ = registry.store.range(PREFIX)
         for kv in kvs:
-            self._install(json.loads(kv.value))
+            self._install(decode_kv(kv.value))
 
     def start(self):
         self._wake = asyncio.Event()
@@ -213,7 +214,7 @@ class CRDManager:
             return
         name = k[len(PREFIX):]
         if ev.type == PUT:
-            self._install(json.loads(ev.kv.value))
+            self._install(decode_kv(ev.kv.value))
         else:
             self._uninstall(name)
         self._pending.add(name)

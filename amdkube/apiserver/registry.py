@@ -26,6 +26,7 @@ from ..api.labels import parse_field_selector, parse_selector
 from ..api.scheme import SCHEME, ResourceInfo
 from ..api.validation import validate_binding
 from ..store import Filter, MVCCStore, Storage, event_object, PUT
+from ..store.storage import decode_kv
 from . import admission as adm
 from .service import ServiceAllocator
 
@@ -190,7 +191,7 @@ def pod_qos(pod) -> str:
 class ResourceStore:
     def __init__(self, api: "Registry", ri: ResourceInfo):
         self.api, self.ri = api, ri
-        self.storage = Storage(api.store, ri.plural)
+        self.storage = Storage(api.store, ri.plural, getattr(api, "media_type", "application/json"))
         self.fields_fn = FIELDS.get(ri.plural, default_fields)
         self.has_status = ri.plural in _STATUS_KINDS or ri.plural == "customresourcedefinitions"
         self.generation = ri.plural in _GENERATION_KINDS
@@ -432,8 +433,10 @@ def _validate_pod_status(pod):
 class Registry:
     """All resource stores + admission context + the node device-assignment index."""
 
-    def __init__(self, store: MVCCStore, admission: adm.Chain, services: ServiceAllocator | None = None):
+    def __init__(self, store: MVCCStore, admission: adm.Chain, services: ServiceAllocator | None = None,
+                 media_type: str = "application/json"):
         self.store = store
+        self.media_type = media_type     # --storage-media-type: how objects are encoded in the store
         self.admission = admission
         self.services = services or ServiceAllocator()
         self.resources: dict[tuple[str, str], ResourceStore] = {}
@@ -517,7 +520,7 @@ class Registry:
     def _rebuild_index(self):
         kvs, _, _ = self.store.range("/registry/pods/")
         for kv in kvs:
-            self._index_pod(kv.key, json.loads(kv.value))
+            self._index_pod(kv.key, decode_kv(kv.value))
         self.services.rebuild(self.store.range("/registry/services/")[0])  # ipallocator/portallocator repair
 
     # ------------------------------------------------------------ eviction

@@ -27,6 +27,7 @@ from ..api.scheme import SCHEME
 from ..store import MVCCStore, PUT
 from ..utils import profiling
 from ..utils.metrics import CONTENT_TYPE, MICRO_BUCKETS, Counter, Histogram, new_registry, render
+from ..store.storage import json_bytes
 from . import admission as adm
 from .registry import Registry
 from .service import ServiceAllocator, parse_port_range
@@ -79,6 +80,20 @@ def _convert_frame(data: bytes, storage_ri, served) -> bytes:
     return json.dumps(ev, separators=(",", ":")).encode() + b"\n"
 
 
+def _wants_protobuf(request) -> bool:
+    """Accept lists application/vnd.kubernetes.protobuf before any JSON type (or without one)."""
+    acc = request.headers.get("Accept", "")
+    if "protobuf" not in acc:
+        return False
+    for part in acc.split(","):
+        mt = part.split(";", 1)[0].strip().lower()
+        if mt.startswith("application/vnd.kubernetes.protobuf"):
+            return True
+        if mt in ("application/json", "*/*", "application/*"):
+            return False
+    return False
+
+
 def _resp(obj, status=200) -> web.Response:
     body = obj if isinstance(obj, (bytes, bytearray)) else json.dumps(obj, separators=(",", ":")).encode()
     return web.Response(body=body, status=status, content_type=_JSON)
@@ -117,7 +132,11 @@ class APIServer:
                 ctx.load_cert_chain(kubelet_client_certificate, kubelet_client_key)
             self.kubelet_ssl = ctx
         self.admission = adm.Chain(admission_plugins, admission_config)
-        self.registry = Registry(self.store, self.admission, ServiceAllocator(service_cidr, parse_port_range(node_port_range)))
+        smt = self.opts.get("storage_media_type") or "application/json"
+        if smt not in ("application/json", "application/vnd.kubernetes.protobuf"):
+            raise ValueError(f"--storage-media-type {smt!r}: application/json or application/vnd.kubernetes.protobuf")
+        self.registry = Registry(self.store, self.admission, ServiceAllocator(service_cidr, parse_port_range(node_port_range)),
+                                 media_type=smt)
         from .crd import CRDManager
         from .webhook import WebhookDispatcher
         self.crds = CRDManager(self.registry)
@@ -181,7 +200,8 @@ class APIServer:
                                ["verb", "resource", "subresource"], buckets=MICRO_BUCKETS, registry=self.metrics)
         self.watch_count = 0
         self.app = web.Application(client_max_size=64 * 1024 * 1024,
-                                   middlewares=[self._cors_middleware] if self.opts.get("cors_allowed_origins") else [])
+                                   middlewares=([self._cors_middleware] if self.opts.get("cors_allowed_origins") else []) +
+                                   [self._protobuf_middleware])
         self.app.router.add_get("/healthz", self.healthz)
         self.app.router.add_get("/healthz/{check}", self.healthz)
         self.app.router.add_get("/version", self.version)
@@ -623,7 +643,7 @@ class APIServer:
                 if sem.locked():
                     raise m.too_many_requests()
                 await sem.acquire()
-            resp = await self._handle(request, rs, ns, name, sub, user, q)
+            resp = await self._handle(request, rs, ns, name, sub, user, q, as_stored=conv is None)
             if conv is not None and resp.body:
                 resp = _resp(_convert_out(json.loads(resp.body), rs.ri, conv), resp.status)
             code = resp.status
@@ -653,12 +673,40 @@ class APIServer:
         if "yaml" in ct:
             import yaml
             return yaml.safe_load(data)
-        if data.startswith(b"k8s\x00"):
-            from ..api.scheme import decode_envelope
-            return decode_envelope(data)
+        if data.startswith(b"k8s\x00") or "protobuf" in ct:
+            from ..api import protobuf as pb
+            try:
+                return pb.decode(data)
+            except (pb.ProtoError, ValueError) as e:
+                raise m.bad_request(f"protobuf body: {e}")
         return json.loads(data)
 
-    async def _handle(self, request, rs, ns, name, sub, user, q):
+    @web.middleware
+    async def _protobuf_middleware(self, request, handler):
+        """Content negotiation (apiserver/pkg/endpoints/handlers/negotiation): a client whose
+        Accept prefers application/vnd.kubernetes.protobuf gets the `k8s\x00` envelope for every
+        kind with a protobuf schema (errors included: meta/v1 Status); other kinds stay JSON."""
+        resp = await handler(request)
+        if not _wants_protobuf(request) or not isinstance(resp, web.Response) or resp.content_type != _JSON:
+            return resp
+        body = resp.body
+        if not isinstance(body, (bytes, bytearray)) or not body[:1] == b"{":
+            return resp
+        from ..api import protobuf as pb
+        try:
+            obj = json.loads(body)
+            if not (isinstance(obj, dict) and pb.supports(obj)):
+                return resp
+            data = pb.encode(obj)
+        except (ValueError, pb.ProtoError):
+            return resp
+        out = web.Response(body=data, status=resp.status, content_type=pb.MEDIA_TYPE)
+        for k, v in resp.headers.items():
+            if k.lower() not in ("content-type", "content-length"):
+                out.headers[k] = v
+        return out
+
+    async def _handle(self, request, rs, ns, name, sub, user, q, as_stored=False):
         meth = request.method
         ri = rs.ri
         if ri.namespaced is False:
@@ -671,10 +719,23 @@ class APIServer:
                     raise m.not_found("subresource", sub)
                 if sub == "scale":
                     return _resp(_to_scale(rs.get(ns, name)))
+                if as_stored and _wants_protobuf(request):
+                    kv = rs.storage.store.get(rs.key(ns, name))
+                    if kv is not None and kv.value[:4] == b"k8s\x00":
+                        # protobuf storage, protobuf client, same version: the stored bytes ARE the answer
+                        return web.Response(body=kv.value, content_type="application/vnd.kubernetes.protobuf")
                 raw = rs.storage.get_raw(rs.key(ns, name))
                 if raw is None:
                     raise m.not_found(ri.group_resource, name)
                 return _resp(raw)
+            if as_stored and _wants_protobuf(request) and rs.storage.media_type != _JSON \
+                    and not any(q.get(k) for k in ("labelSelector", "fieldSelector", "limit", "continue")) \
+                    and not self._hide_uninitialized(q):
+                from ..api import protobuf as pb
+                kvs, rev, _ = rs.storage.store.range(rs.prefix(ns))
+                body = pb.list_from_stored(ri.api_version, ri.list_kind, str(rev), [kv.value for kv in kvs])
+                if body is not None:
+                    return web.Response(body=body, content_type=pb.MEDIA_TYPE)
             return self._list(rs, ns, q)
         if meth == "POST":
             body = await self._body(request)
@@ -850,7 +911,9 @@ class APIServer:
             w = rs.watch(ns, str(list_rev), ls, fs)
         else:
             w = rs.watch(ns, rv, ls, fs)
-        resp = web.StreamResponse(status=200, headers={"Content-Type": _JSON, "Transfer-Encoding": "chunked"})
+        proto = _wants_protobuf(request)
+        ctype = "application/vnd.kubernetes.protobuf;stream=watch" if proto else _JSON
+        resp = web.StreamResponse(status=200, headers={"Content-Type": ctype, "Transfer-Encoding": "chunked"})
         resp.enable_chunked_encoding()
         await resp.prepare(request)
         self.watch_count += 1
@@ -858,6 +921,14 @@ class APIServer:
         deadline = loop.time() + timeout
         try:
             frame = self._frame if conv is None else (lambda t: _convert_frame(self._frame(t), ri, conv))
+            if proto:
+                # length-delimited meta/v1 WatchEvent frames, objects enveloped (framer.go)
+                from ..api import protobuf as pb
+                json_frame = frame
+
+                def frame(t, _jf=json_frame):
+                    ev = json.loads(_jf(t))
+                    return pb.encode_watch_event(ev["type"], ev["object"])
             if self._hide_uninitialized(q):
                 initial = [o for o in initial if not _uninitialized(o)]
                 inner = frame
@@ -869,7 +940,10 @@ class APIServer:
                 for o in initial:
                     if conv is not None:
                         o = _convert_out(o, ri, conv)
-                    buf += b'{"type":"ADDED","object":' + json.dumps(o, separators=(",", ":")).encode() + b"}\n"
+                    if proto:
+                        buf += pb.encode_watch_event("ADDED", o)
+                    else:
+                        buf += b'{"type":"ADDED","object":' + json.dumps(o, separators=(",", ":")).encode() + b"}\n"
                 await resp.write(bytes(buf))
             while True:
                 rem = deadline - loop.time()
@@ -880,7 +954,8 @@ class APIServer:
                     if w.closed:
                         if getattr(w.w, "err", None):
                             st = m.gone(f"watch closed: {w.w.err}").status()
-                            await resp.write(b'{"type":"ERROR","object":' + json.dumps(st).encode() + b"}\n")
+                            await resp.write(pb.encode_watch_event("ERROR", st) if proto else
+                                             b'{"type":"ERROR","object":' + json.dumps(st).encode() + b"}\n")
                         break
                     continue
                 buf = bytearray(frame(ev))
@@ -906,7 +981,7 @@ class APIServer:
     def _frame(t) -> bytes:
         typ, obj, ev = t
         if ev.type == PUT:
-            data = ev.kv.value
+            data = json_bytes(ev.kv.value)
         else:
             data = json.dumps(obj, separators=(",", ":")).encode()
         return b'{"type":"' + typ.encode() + b'","object":' + data + b"}\n"

@@ -20,6 +20,7 @@ import json
 import random
 
 from ..api import meta as m
+from ..store.storage import decode_kv
 
 DEFAULT_SERVICE_CIDR = "10.0.0.0/24"          # kube-apiserver --service-cluster-ip-range default
 DEFAULT_NODE_PORT_RANGE = (30000, 32767)      # --service-node-port-range default 30000-32767
@@ -73,7 +74,7 @@ class ServiceAllocator:
 
     def rebuild(self, kvs):
         for kv in kvs:
-            self.index(kv.key, json.loads(kv.value))
+            self.index(kv.key, decode_kv(kv.value))
 
     # ------------------------------------------------------------- allocate
     def _usable(self, ip) -> bool:

@@ -94,10 +94,14 @@ class Client:
     def __init__(self, server: str, token: str | None = None, qps: float = 0, burst: int = 0,
                  chaos: float = 0.0, user_agent: str = "amdkube", timeout: float = 60.0, pool: int = 64,
                  ca_file: str | None = None, ca_data: str | None = None, cert_file: str | None = None,
-                 key_file: str | None = None, insecure: bool = False):
+                 key_file: str | None = None, insecure: bool = False, content_type: str = "application/json"):
         self.server = server.rstrip("/")
         self.ssl = _ssl_context(ca_file, ca_data, cert_file, key_file, insecure) if self.server.startswith("https") else None
-        self.headers = {"User-Agent": user_agent, "Accept": "application/json"}
+        # --kube-api-content-type: application/vnd.kubernetes.protobuf asks for the protobuf
+        # encoding (JSON stays acceptable for kinds without a protobuf schema)
+        self.proto = content_type == "application/vnd.kubernetes.protobuf"
+        accept = "application/vnd.kubernetes.protobuf, application/json" if self.proto else "application/json"
+        self.headers = {"User-Agent": user_agent, "Accept": accept}
         if token:
             self.headers["Authorization"] = f"Bearer {token}"
         self.limiter = TokenBucket(qps, burst or int(qps * 2) or 1) if qps else None
@@ -203,6 +207,12 @@ class Client:
         async with self.session.request(method, self.server + path, params=params, data=data, headers=headers,
                                         timeout=to) as r:
             payload = await r.read()
+            if payload[:4] == b"k8s\x00":
+                from ..api import protobuf as pb
+                obj = pb.decode(payload)
+                if r.status >= 400:
+                    raise m.StatusError.from_status(obj)
+                return payload if raw else obj
             if r.status >= 400:
                 try:
                     st = json.loads(payload)
@@ -333,6 +343,16 @@ class Client:
                 except ValueError:
                     raise m.StatusError(r.status, "Unknown", payload.decode(errors="replace"))
             buf = b""
+            if "protobuf" in r.headers.get("Content-Type", ""):
+                from ..api import protobuf as pb
+                async for chunk in r.content.iter_any():
+                    buf += chunk
+                    events, buf = pb.decode_watch_frames(buf)
+                    for typ, obj in events:
+                        if typ == "ERROR":
+                            raise m.StatusError.from_status(obj)
+                        yield typ, obj
+                return
             async for chunk in r.content.iter_any():
                 buf += chunk
                 while True:

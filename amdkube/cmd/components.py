@@ -173,11 +173,14 @@ def apiserver(argv):
     ap.add_argument("--min-request-timeout", type=float, default=1800.0, help="seconds (watch duration floor)")
     ap.add_argument("--tls-sni-cert-key", action="append", default=[], help="cert,key[:name1,name2] (repeatable)")
     ap.add_argument("--feature-gates", default="")
+    ap.add_argument("--storage-media-type", default="application/json",
+                    choices=("application/json", "application/vnd.kubernetes.protobuf"),
+                    help="encoding of objects in the store (the reference's etcd3 default is protobuf)")
     # accepted for command-line compatibility: etcd and watch-cache tuning of a store this
     # apiserver embeds, SSH tunnels and other knobs with no counterpart here
     for flag in ("--etcd-servers", "--etcd-servers-overrides", "--etcd-cafile", "--etcd-certfile", "--etcd-keyfile",
                  "--etcd-prefix", "--etcd-quorum-read", "--etcd-compaction-interval", "--storage-backend",
-                 "--storage-media-type", "--storage-versions", "--watch-cache", "--watch-cache-sizes",
+                 "--storage-versions", "--watch-cache", "--watch-cache-sizes",
                  "--default-watch-cache-size", "--deserialization-cache-size", "--target-ram-mb", "--apiserver-count",
                  "--endpoint-reconciler-type", "--ssh-user", "--ssh-keyfile", "--cert-dir", "--external-hostname",
                  "--public-address-override", "--kubelet-preferred-address-types", "--kubelet-timeout",
@@ -210,7 +213,7 @@ def apiserver(argv):
         "audit_webhook_batch_buffer_size", "audit_webhook_batch_max_size", "audit_webhook_batch_max_wait",
         "audit_webhook_batch_throttle_qps", "audit_webhook_batch_throttle_burst", "advertise_address",
         "kubernetes_service_node_port", "allow_privileged", "runtime_config", "cors_allowed_origins",
-        "enable_logs_handler", "profiling", "min_request_timeout")}
+        "enable_logs_handler", "profiling", "min_request_timeout", "storage_media_type")}
     options["tls_sni_cert_key"] = sni
     main_port = a.port
     if a.secure_port is not None and a.tls_cert_file:

@@ -8,7 +8,11 @@ where an object leaving the filter is delivered as DELETED and entering as ADDED
 
 Objects are stored as compact JSON whose metadata.resourceVersion already equals the
 commit revision (embedded at commit time), so GET/LIST/WATCH can stream stored bytes
-without re-encoding.
+without re-encoding. With `--storage-media-type application/vnd.kubernetes.protobuf` a
+Storage writes the reference's etcd format instead: the `k8s\x00` protobuf envelope
+(api/protobuf.py), falling back to JSON for kinds without a protobuf schema and for objects
+that would lose amdkube-only fields in the typed encoding. Reads sniff the magic, so a store
+may hold both (as one migrating between media types does).
 """
 from __future__ import annotations
 
@@ -20,24 +24,45 @@ from ..api import meta as m
 from .mvcc import CASFailed, Compacted, KeyExists, KeyNotFound, MVCCStore, PUT, DELETE, Event
 
 
-def _with_rv(obj: dict):
+PROTO_MAGIC = b"k8s\x00"
+JSON_MEDIA_TYPE = "application/json"
+PROTO_MEDIA_TYPE = "application/vnd.kubernetes.protobuf"
+
+
+def _with_rv(obj: dict, media_type: str = JSON_MEDIA_TYPE):
     def build(rev: int) -> bytes:
         obj.setdefault("metadata", {})["resourceVersion"] = str(rev)
+        if media_type == PROTO_MEDIA_TYPE:
+            from ..api import protobuf as pb
+            if pb.supports(obj):
+                data = pb.encode(obj)
+                if pb.lossless(obj, data):
+                    return data
         return json.dumps(obj, separators=(",", ":")).encode()
     return build
 
 
 def decode_kv(value: bytes) -> dict:
+    if value[:4] == PROTO_MAGIC:
+        from ..api import protobuf as pb
+        return pb.decode(value)
     return json.loads(value)
+
+
+def json_bytes(value: bytes) -> bytes:
+    """The stored value as JSON bytes (transcoding a protobuf-stored object)."""
+    if value[:4] == PROTO_MAGIC:
+        return json.dumps(decode_kv(value), separators=(",", ":")).encode()
+    return value
 
 
 def event_object(ev: Event) -> dict:
     """Decoded object for an event (cached on the event, shared read-only)."""
     if ev.cache is None:
         if ev.type == PUT:
-            ev.cache = json.loads(ev.kv.value)
+            ev.cache = decode_kv(ev.kv.value)
         else:
-            o = json.loads(ev.prev.value)
+            o = decode_kv(ev.prev.value)
             o.setdefault("metadata", {})["resourceVersion"] = str(ev.rev)
             ev.cache = o
     return ev.cache
@@ -47,7 +72,7 @@ def event_prev_object(ev: Event) -> dict | None:
     if ev.prev is None:
         return None
     if ev.prev_cache is None:
-        ev.prev_cache = json.loads(ev.prev.value)
+        ev.prev_cache = decode_kv(ev.prev.value)
     return ev.prev_cache
 
 
@@ -120,14 +145,15 @@ class Storage:
     # fields whose exact-match watches are indexed (cacher.go: pods by spec.nodeName)
     TRIGGER_FIELDS = ("spec.nodeName",)
 
-    def __init__(self, store: MVCCStore, resource: str = "object"):
+    def __init__(self, store: MVCCStore, resource: str = "object", media_type: str = JSON_MEDIA_TYPE):
         self.store = store
         self.resource = resource
+        self.media_type = media_type
 
     # -------------------------------------------------------------- basic ops
     def create(self, key: str, obj: dict) -> dict:
         try:
-            self.store.put(key, _with_rv(obj), expect_mod_rev=0)
+            self.store.put(key, _with_rv(obj, self.media_type), expect_mod_rev=0)
         except KeyExists:
             raise m.already_exists(self.resource, key.rsplit("/", 1)[-1])
         return obj
@@ -141,8 +167,9 @@ class Storage:
         return decode_kv(kv.value)
 
     def get_raw(self, key: str) -> bytes | None:
+        """The object as JSON bytes (stored bytes when stored as JSON)."""
         kv = self.store.get(key)
-        return kv.value if kv else None
+        return json_bytes(kv.value) if kv else None
 
     def guaranteed_update(self, key: str, try_update: Callable[[dict], dict | None],
                           precond_uid: str | None = None, precond_rv: str | None = None,
@@ -170,7 +197,7 @@ class Storage:
             if new is None:
                 return cur
             try:
-                self.store.put(key, _with_rv(new), expect_mod_rev=mod)
+                self.store.put(key, _with_rv(new, self.media_type), expect_mod_rev=mod)
                 return new
             except (CASFailed, KeyExists, KeyNotFound):
                 continue
@@ -213,7 +240,7 @@ class Storage:
 
     def list_raw(self, prefix: str):
         kvs, rev, _ = self.store.range(prefix)
-        return [kv.value for kv in kvs], rev
+        return [json_bytes(kv.value) for kv in kvs], rev
 
     # ------------------------------------------------------------------ watch
     def watch(self, prefix: str, rv: str | int | None, flt: Filter | None = None, exact=False) -> "FilteredWatch":

@@ -322,6 +322,94 @@ def test_07_native_activity_sampler_averages_a_burn():
     assert not b.lib.sampler_state()["running"]
 
 
+def test_08_restart_continuity_and_exporter_scrape():
+    """test/e2e_node/gpu_device_plugin.go:45-143 on MI355X: a running gpu-burn pod keeps its
+    device across a kubelet restart and while the device plugin is down (capacity 0), capacity
+    returns without flapping when the plugin comes back, a second 1-GPU pod waits until the
+    first one ends; the amd-smi exporter attributes the busy GPU's series to the pod."""
+    import aiohttp
+    from amdkube.client import Client
+    from amdkube.deviceplugin.amd import make_plugins
+    from amdkube.kubelet.kubelet import Kubelet
+    from amdkube.monitoring.exporter import Exporter
+
+    def burn(name, ms):
+        return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "default"},
+                "spec": {"restartPolicy": "Never", "containers": [{
+                    "name": "burn", "image": "amdkube/gpu-burn", "args": ["--ms", str(ms)],
+                    "resources": {"limits": {"amd.com/gpu": "1"}}}]}}
+
+    async def capacity(lc):
+        node = await lc.client.get("nodes", lc.node_name)
+        return (node["status"].get("capacity") or {}).get("amd.com/gpu", "0")
+
+    async def go():
+        async with LocalCluster(gpus="amdsmi", n_gpus=1, relist_period=0.5, node_status_update_frequency=0.5,
+                                with_controllers=False) as lc:
+            await lc.wait_gpus(1, 60)
+            await lc.client.create(burn("burn", 25000))
+            p = await wait_pod(lc.client, "default", "burn", ("Running",), 60)
+            assigned = p["spec"]["extendedResources"][0]["assigned"]
+            cid = p["status"]["containerStatuses"][0]["containerID"]
+            # exporter scrape while the burn runs: series attributed to the pod
+            ex = await Exporter(lc.backend, node=lc.node_name,
+                                kubelet_url=f"http://127.0.0.1:{lc.kubelet.server.port}").start("127.0.0.1", 0)
+            try:
+                await asyncio.sleep(1.0)
+                async with aiohttp.ClientSession() as s:
+                    async with s.get(f"http://127.0.0.1:{ex.port}/metrics") as r:
+                        text = await r.text()
+            finally:
+                await ex.stop()
+            for series in ("amd_gpu_utilization_percent", "amd_gpu_vram_used_bytes", "amd_gpu_power_watts",
+                           "amd_gpu_temperature_celsius", "amd_gpu_ecc_uncorrectable_total"):
+                lines = [ln for ln in text.splitlines() if ln.startswith(series + "{")]
+                assert lines and all('pod="burn"' in ln and 'namespace="default"' in ln for ln in lines), (series, lines)
+            # kubelet restart: same container, same GPU
+            cfg = lc.kubelet.cfg
+            await lc.kubelet.stop()
+            lc.kubelet = await Kubelet(Client(lc.api.url, token=lc.api.loopback_token), cfg, smi_backend=lc.backend).start()
+            await asyncio.sleep(1.5)
+            p = await lc.client.get("pods", "burn", "default")
+            assert p["status"]["phase"] == "Running" and p["status"]["containerStatuses"][0]["containerID"] == cid, p["status"]
+            assert p["spec"]["extendedResources"][0]["assigned"] == assigned
+            # a second 1-GPU pod waits: the node's only GPU is taken
+            await lc.client.create(burn("second", 500))
+            # plugin down: capacity → 0, the burn keeps running
+            for pl in lc.plugins:
+                await pl.stop()
+            for _ in range(100):
+                if await capacity(lc) == "0":
+                    break
+                await asyncio.sleep(0.1)
+            assert await capacity(lc) == "0"
+            p = await lc.client.get("pods", "burn", "default")
+            assert p["status"]["phase"] == "Running" and p["status"]["containerStatuses"][0]["containerID"] == cid
+            # plugin back: capacity returns and stays (no flap)
+            lc.plugins = make_plugins(lc.backend, lc.resource_naming, plugins_dir=os.path.join(lc.base, "plugins"),
+                                      health_interval=5.0, health_probe="none")
+            for pl in lc.plugins:
+                await pl.start()
+            lc.plugin = lc.plugins[0]
+            for _ in range(100):
+                if await capacity(lc) == "1":
+                    break
+                await asyncio.sleep(0.1)
+            seen = []
+            for _ in range(20):
+                seen.append(await capacity(lc))
+                await asyncio.sleep(0.1)
+            assert set(seen) == {"1"}, seen
+            p2 = await lc.client.get("pods", "second", "default")
+            assert p2["status"]["phase"] == "Pending" and not p2["spec"].get("nodeName"), p2["status"]
+            # the first ends → the second runs on the freed GPU
+            p = await wait_pod(lc.client, "default", "burn", ("Succeeded", "Failed"), 60)
+            assert p["status"]["phase"] == "Succeeded", p["status"]
+            p2 = await wait_pod(lc.client, "default", "second", ("Succeeded", "Failed"), 90)
+            assert p2["status"]["phase"] == "Succeeded" and p2["spec"]["extendedResources"][0]["assigned"] == assigned
+    run(go(), 240)
+
+
 def test_04_probe_binaries():
     r = subprocess.run([os.path.join(BIN, "hbm-probe"), "--mib", "1024", "--iters", "3"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr

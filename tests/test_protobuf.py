@@ -1,0 +1,241 @@
+"""Kubernetes protobuf object encoding (api/protobuf.py) and its use on the wire and in storage.
+
+Reference: staging/src/k8s.io/apimachinery/pkg/runtime/serializer/protobuf/protobuf.go:42,88,171
+(`k8s\\x00` + runtime.Unknown), staging/src/k8s.io/api/core/v1/generated.proto (the fork's tags:
+Container.extendedResourceRequests = 22 at :617-619, PodSpec.extendedResources = 27,
+NodeStatus.extendedResources = 11, ObjectReference.extendedResourceBinding = 8), the watch
+framer (4-byte length + WatchEvent) and etcd3 storage of protobuf-enveloped objects."""
+import asyncio
+import json
+import os
+import struct
+
+import pytest
+
+from amdkube.api import protobuf as pb
+from amdkube.client import Client
+from amdkube.localcluster import LocalCluster
+from tests.conftest import run
+
+
+def wire_fields(buf: bytes) -> list[tuple[int, int, bytes | int]]:
+    """Schema-free protobuf parse: [(field number, wire type, value)]."""
+    out, i = [], 0
+
+    def varint():
+        nonlocal i
+        v, shift = 0, 0
+        while True:
+            b = buf[i]
+            i += 1
+            v |= (b & 0x7F) << shift
+            shift += 7
+            if not b & 0x80:
+                return v
+    while i < len(buf):
+        key = varint()
+        num, wt = key >> 3, key & 7
+        if wt == 0:
+            out.append((num, wt, varint()))
+        elif wt == 2:
+            n = varint()
+            out.append((num, wt, buf[i:i + n]))
+            i += n
+        elif wt == 1:
+            out.append((num, wt, buf[i:i + 8]))
+            i += 8
+        elif wt == 5:
+            out.append((num, wt, buf[i:i + 4]))
+            i += 4
+        else:
+            raise ValueError(f"wire type {wt}")
+    return out
+
+
+def field(buf, num):
+    return [v for n, _, v in wire_fields(buf) if n == num]
+
+
+GPU_POD = {
+    "apiVersion": "v1", "kind": "Pod",
+    "metadata": {"name": "trainer", "namespace": "ml", "uid": "u-1", "resourceVersion": "42", "labels": {"app": "t"},
+                 "creationTimestamp": "2026-10-17T03:00:00Z", "ownerReferences": [{"apiVersion": "apps/v1", "kind": "ReplicaSet",
+                                                                                   "name": "rs", "uid": "u-0", "controller": True}]},
+    "spec": {"nodeName": "mi355x-node-0", "restartPolicy": "Never", "terminationGracePeriodSeconds": 30,
+             "containers": [{"name": "c", "image": "rocm/vector-add", "command": ["rocm-vector-add"], "args": ["--print-uuid"],
+                             "extendedResourceRequests": ["gpus"],
+                             "resources": {"limits": {"cpu": "2", "memory": "8Gi"}, "requests": {"cpu": "500m"}},
+                             "env": [{"name": "A", "value": ""}, {"name": "POD", "valueFrom": {"fieldRef": {"fieldPath": "metadata.name"}}}],
+                             "ports": [{"containerPort": 8080, "protocol": "TCP"}],
+                             "livenessProbe": {"httpGet": {"path": "/healthz", "port": "http"}, "initialDelaySeconds": 3},
+                             "readinessProbe": {"exec": {"command": ["true"]}},
+                             "volumeMounts": [{"name": "rocm", "mountPath": "/opt/rocm", "readOnly": True}]}],
+             "volumes": [{"name": "rocm", "hostPath": {"path": "/opt/rocm"}},
+                         {"name": "cfg", "configMap": {"name": "cfg", "items": [{"key": "k", "path": "p"}], "defaultMode": 420}}],
+             "tolerations": [{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"}],
+             "extendedResources": [{"name": "gpus", "resources": {"limits": {"amd.com/gpu": "4"}, "requests": {"amd.com/gpu": "4"}},
+                                    "affinity": {"required": [{"key": "amd.com/gpu-memory", "operator": "Gt", "values": ["262143"]}]},
+                                    "assigned": ["GPU-a", "GPU-b", "GPU-c", "GPU-d"]}]},
+    "status": {"phase": "Running", "podIP": "10.0.0.5", "startTime": "2026-10-17T03:00:01Z",
+               "conditions": [{"type": "Ready", "status": "True", "lastProbeTime": None,
+                               "lastTransitionTime": "2026-10-17T03:00:02Z"}],
+               "containerStatuses": [{"name": "c", "ready": True, "restartCount": 0, "image": "rocm/vector-add", "imageID": "",
+                                      "state": {"running": {"startedAt": "2026-10-17T03:00:01Z"}}}]}}
+
+NODE = {"apiVersion": "v1", "kind": "Node", "metadata": {"name": "mi355x-node-0", "annotations": {"amd.com/gpu-topology": "{}"}},
+        "spec": {"taints": [{"key": "k", "value": "v", "effect": "NoSchedule"}]},
+        "status": {"capacity": {"amd.com/gpu": "8", "cpu": "256"}, "allocatable": {"amd.com/gpu": "8"},
+                   "extendedResources": {"amd.com/gpu": {"resources": {
+                       f"GPU-{i}": {"id": f"GPU-{i}", "health": "Healthy" if i else "Unhealthy",
+                                    "attributes": {"amd.com/gpu-memory": "294912", "amd.com/gpu-type": "MI355X"}}
+                       for i in range(8)}}},
+                   "conditions": [{"type": "Ready", "status": "True", "lastHeartbeatTime": "2026-10-17T03:00:00Z"}],
+                   "addresses": [{"type": "InternalIP", "address": "127.0.0.1"}],
+                   "daemonEndpoints": {"kubeletEndpoint": {"Port": 10250}}}}
+
+BINDING = {"apiVersion": "v1", "kind": "Binding", "metadata": {"name": "trainer", "namespace": "ml"},
+           "target": {"kind": "Node", "name": "mi355x-node-0",
+                      "extendedResourceBinding": {"gpus": {"resources": ["GPU-a", "GPU-b"]}}}}
+
+EVENT = {"apiVersion": "v1", "kind": "Event", "metadata": {"name": "e1", "namespace": "ml"},
+         "involvedObject": {"kind": "Pod", "name": "trainer", "namespace": "ml"}, "reason": "Scheduled", "message": "ok",
+         "count": 2, "type": "Normal", "firstTimestamp": "2026-10-17T03:00:00Z",
+         "eventTime": "2026-10-17T03:00:00.123456Z", "series": {"count": 2, "lastObservedTime": "2026-10-17T03:00:05.000001Z",
+                                                                  "state": "Ongoing"},
+         "reportingComponent": "amdkube-scheduler", "reportingInstance": "s-1", "action": "Binding",
+         "related": {"kind": "Node", "name": "mi355x-node-0"}}
+
+OTHERS = [
+    {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "ml"}, "spec": {"finalizers": ["kubernetes"]},
+     "status": {"phase": "Active"}},
+    {"apiVersion": "v1", "kind": "Secret", "metadata": {"name": "s", "namespace": "ml"}, "type": "Opaque",
+     "data": {"token": "czNjcjN0", "empty": ""}},
+    {"apiVersion": "v1", "kind": "Service", "metadata": {"name": "svc", "namespace": "ml"},
+     "spec": {"ports": [{"name": "http", "port": 80, "targetPort": "http"}, {"port": 81, "targetPort": 8081}],
+              "selector": {"app": "t"}, "clusterIP": "10.0.0.10", "type": "ClusterIP"}},
+    {"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": "d", "namespace": "ml", "generation": 3},
+     "spec": {"replicas": 2, "selector": {"matchLabels": {"app": "t"}},
+              "strategy": {"type": "RollingUpdate", "rollingUpdate": {"maxSurge": "25%", "maxUnavailable": 0}},
+              "template": {"metadata": {"labels": {"app": "t"}}, "spec": {"containers": [{"name": "c", "image": "x"}]}}}},
+    {"apiVersion": "apiextensions.k8s.io/v1beta1", "kind": "CustomResourceDefinition", "metadata": {"name": "gpujobs.amd.com"},
+     "spec": {"group": "amd.com", "version": "v1", "scope": "Namespaced",
+              "names": {"plural": "gpujobs", "kind": "GPUJob", "shortNames": ["gj"]},
+              "validation": {"openAPIV3Schema": {"type": "object", "properties": {
+                  "spec": {"type": "object", "required": ["gpus"], "properties": {
+                      "gpus": {"type": "integer", "minimum": 1, "maximum": 8},
+                      "tags": {"type": "array", "items": {"type": "string"}},
+                      "extra": {"type": "object", "additionalProperties": True}}}}}}}},
+]
+
+
+@pytest.mark.parametrize("obj", [GPU_POD, NODE, BINDING, EVENT] + OTHERS, ids=lambda o: o["kind"])
+def test_json_proto_round_trip(obj):
+    data = pb.encode(obj)
+    assert data[:4] == b"k8s\x00"
+    unknown = data[4:]
+    type_meta = field(unknown, 1)[0]
+    assert field(type_meta, 1) == [obj["apiVersion"].encode()] and field(type_meta, 2) == [obj["kind"].encode()]
+    assert pb.lossless(obj, data), json.dumps(pb.decode(data))[:600]
+
+
+def test_fork_fields_carry_the_reference_tags():
+    raw = field(pb.encode(GPU_POD)[4:], 2)[0]              # Unknown.raw = the Pod message
+    spec = field(raw, 2)[0]                                  # Pod.spec = 2
+    container = field(spec, 2)[0]                            # PodSpec.containers = 2
+    assert field(container, 22) == [b"gpus"]                 # Container.extendedResourceRequests = 22
+    [pres] = field(spec, 27)                                 # PodSpec.extendedResources = 27
+    assert field(pres, 1) == [b"gpus"] and field(pres, 5) == [b"GPU-a", b"GPU-b", b"GPU-c", b"GPU-d"]   # name 1, assigned 5
+    nraw = field(pb.encode(NODE)[4:], 2)[0]
+    status = field(nraw, 3)[0]                               # Node.status = 3
+    assert len(field(status, 11)) == 1                       # NodeStatus.extendedResources = 11 (one map entry)
+    braw = field(pb.encode(BINDING)[4:], 2)[0]
+    target = field(braw, 2)[0]                               # Binding.target = 2
+    [entry] = field(target, 8)                               # ObjectReference.extendedResourceBinding = 8
+    assert field(entry, 1) == [b"gpus"]
+    # Time is {seconds = 1, nanos = 2}; a Quantity is {string = 1}
+    md = field(raw, 1)[0]
+    ts = field(md, 8)[0]                                     # ObjectMeta.creationTimestamp = 8
+    assert field(ts, 1) == [1792206000]
+
+
+def test_lists_watch_frames_and_lossy_objects():
+    pl = {"apiVersion": "v1", "kind": "PodList", "metadata": {"resourceVersion": "7"}, "items": [GPU_POD, GPU_POD]}
+    assert pb.lossless(pl)
+    frames = pb.encode_watch_event("ADDED", GPU_POD) + pb.encode_watch_event("DELETED", NODE)
+    n = struct.unpack(">I", frames[:4])[0]
+    events, rest = pb.decode_watch_frames(frames + frames[:3])
+    assert [t for t, _ in events] == ["ADDED", "DELETED"] and rest == frames[:3] and n > 0
+    assert events[0][1]["spec"]["extendedResources"][0]["assigned"] == ["GPU-a", "GPU-b", "GPU-c", "GPU-d"]
+    # a field the v1.9 schema does not have does not survive: storage keeps such objects as JSON
+    lossy = json.loads(json.dumps(GPU_POD))
+    lossy["spec"]["amdkubeOnly"] = {"x": 1}
+    assert not pb.lossless(lossy)
+    assert pb.message_for("amd.com/v1", "GPUJob") is None       # custom resources have no protobuf
+
+
+def test_durations_and_times():
+    for s, ns in (("0s", 0), ("1.5s", 1_500_000_000), ("2m30s", 150_000_000_000), ("1h0m0s", 3_600_000_000_000),
+                  ("300ms", 300_000_000)):
+        assert pb.parse_duration(s) == ns
+        assert pb.parse_duration(pb.format_duration(ns)) == ns
+    assert pb.format_duration(3_723_000_000_000) == "1h2m3s"
+
+
+def test_apiserver_negotiates_protobuf_and_stores_it():
+    async def go():
+        async with LocalCluster(gpus="none", with_kubelet=False, with_controllers=False,
+                                api_kw={"options": {"storage_media_type": pb.MEDIA_TYPE}}) as lc:
+            pc = Client(lc.api.url, token=lc.api.loopback_token, content_type=pb.MEDIA_TYPE)
+            try:
+                await pc.create({"apiVersion": "v1", "kind": "Node", "metadata": {"name": "mi355x-node-0"},
+                                 "status": NODE["status"]})
+                pod = json.loads(json.dumps(GPU_POD))
+                for k in ("uid", "resourceVersion", "creationTimestamp", "ownerReferences"):
+                    pod["metadata"].pop(k)
+                pod["spec"].pop("nodeName")
+                pod.pop("status")
+                events = []
+
+                async def watch():
+                    async for typ, obj in pc.watch("pods", "ml", timeout_seconds=5):
+                        events.append((typ, obj))
+                        if len(events) == 2:
+                            return
+                await lc.client.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "ml"}})
+                wt = asyncio.create_task(watch())
+                await asyncio.sleep(0.2)
+                created = await pc.create(pod, "ml")                # protobuf request and response
+                assert created["metadata"]["uid"] and created["spec"]["extendedResources"][0]["name"] == "gpus"
+                await pc.bind("ml", "trainer", "mi355x-node-0", {"gpus": {"resources": ["GPU-1", "GPU-2", "GPU-3", "GPU-4"]}})
+                await asyncio.wait_for(wt, 10)
+                assert [t for t, _ in events] == ["ADDED", "MODIFIED"]
+                assert events[1][1]["spec"]["extendedResources"][0]["assigned"] == ["GPU-1", "GPU-2", "GPU-3", "GPU-4"]
+                # the store holds the reference's etcd format; JSON clients read it transparently
+                kv = lc.api.store.get("/registry/pods/ml/trainer")
+                assert kv.value[:4] == b"k8s\x00"
+                got = await lc.client.get("pods", "trainer", "ml")
+                assert got["spec"]["nodeName"] == "mi355x-node-0"
+                items, _ = await pc.list("pods", "ml")
+                assert items[0]["metadata"]["name"] == "trainer"
+                # raw protobuf over HTTP, and a protobuf Status for errors
+                import aiohttp
+                async with aiohttp.ClientSession() as s:
+                    h = {"Accept": pb.MEDIA_TYPE, "Authorization": f"Bearer {lc.api.loopback_token}"}
+                    async with s.get(f"{lc.api.url}/api/v1/namespaces/ml/pods/trainer", headers=h) as r:
+                        body = await r.read()
+                        assert r.headers["Content-Type"].startswith(pb.MEDIA_TYPE) and body[:4] == b"k8s\x00"
+                        assert body == lc.api.store.get("/registry/pods/ml/trainer").value   # stored bytes served as-is
+                    # the LIST fast path splices stored items; it must decode to what the JSON path returns
+                    async with s.get(f"{lc.api.url}/api/v1/namespaces/ml/pods", headers=h) as r:
+                        spliced = pb.decode(await r.read())
+                    async with s.get(f"{lc.api.url}/api/v1/namespaces/ml/pods?labelSelector=", headers={
+                            "Authorization": h["Authorization"]}) as r:
+                        plain = await r.json()
+                    assert spliced["kind"] == "PodList" and spliced["metadata"]["resourceVersion"] == plain["metadata"]["resourceVersion"]
+                    assert spliced["items"] == plain["items"]
+                    async with s.get(f"{lc.api.url}/api/v1/namespaces/ml/pods/nope", headers=h) as r:
+                        st = pb.decode(await r.read())
+                        assert r.status == 404 and st["kind"] == "Status" and st["reason"] == "NotFound"
+            finally:
+                await pc.close()
+    run(go(), 60)
