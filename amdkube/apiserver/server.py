@@ -997,9 +997,11 @@ class APIServer:
         return addr, int(port)
 
     async def _stream(self, request, rs, ns, name, sub, q):
-        """pods/{name}/exec|attach|portforward (WebSocket relayed to the node's kubelet,
+        """pods/{name}/exec|attach|portforward (WebSocket relayed to the node's kubelet, SPDY/3.1
+        spliced through to it,
         registry/core/pod/rest/subresources.go) and pods|services|nodes/{name}/proxy/{path}
         (HTTP proxy to the pod IP, a service endpoint or the kubelet)."""
+        from ..runtime import spdy
         from ..runtime.streaming import CHANNEL_PROTOCOLS, PORTFORWARD_PROTOCOLS, bridge
         plural = rs.ri.plural
         top, _, rest = sub.partition("/")
@@ -1022,6 +1024,8 @@ class APIServer:
         else:
             container = q.get("container") or ((pod.get("spec") or {}).get("containers") or [{}])[0].get("name", "")
             url, protos = f"{self.kubelet_scheme}://{addr}:{port}/{top}/{ns}/{name}/{container}?{qs}", CHANNEL_PROTOCOLS
+        if spdy.is_upgrade(request):
+            return await spdy.upgrade_proxy(request, url, ssl=self.kubelet_ssl)
         ws = web.WebSocketResponse(protocols=protos, max_msg_size=0)
         if not ws.can_prepare(request).ok:
             raise m.bad_request(f"{top} needs a WebSocket upgrade (protocols {', '.join(protos)})")

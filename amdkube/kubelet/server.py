@@ -14,6 +14,8 @@ import time
 
 from aiohttp import web
 
+from ..runtime import spdy
+
 from ..api import meta as m
 from ..grpcdesc.cri import CRI as C
 from ..utils import profiling
@@ -163,6 +165,8 @@ class KubeletServer:
             return web.Response(status=400, text="command is required")
         url = await self.k.cri.exec_url(cs.id, cmd, self._flag(req, "tty"), self._flag(req, "stdin"),
                                         self._flag(req, "stdout", True), self._flag(req, "stderr", True))
+        if spdy.is_upgrade(req):
+            return await spdy.upgrade_proxy(req, url)
         ws = web.WebSocketResponse(protocols=CHANNEL_PROTOCOLS, max_msg_size=0)
         await ws.prepare(req)
         return await bridge(ws, url, [ws.ws_protocol or CHANNEL_PROTOCOLS[0]])
@@ -175,6 +179,8 @@ class KubeletServer:
             return web.Response(status=404, text=f"container {cname} of pod {ns}/{pod} not found")
         url = await self.k.cri.attach_url(cs.id, self._flag(req, "tty"), self._flag(req, "stdin"),
                                           self._flag(req, "stdout", True), self._flag(req, "stderr", True))
+        if spdy.is_upgrade(req):
+            return await spdy.upgrade_proxy(req, url)
         ws = web.WebSocketResponse(protocols=CHANNEL_PROTOCOLS, max_msg_size=0)
         await ws.prepare(req)
         return await bridge(ws, url, [ws.ws_protocol or CHANNEL_PROTOCOLS[0]])
@@ -189,8 +195,12 @@ class KubeletServer:
                 rt = await self.k.runtime.pod_status(uid)
                 ready = rt.ready_sandbox()
                 sid = ready[0] if ready else None
-        if sid is None or not ports:
-            return web.Response(status=404 if sid is None else 400, text="pod sandbox not ready" if sid is None else "port is required")
+        if sid is None:
+            return web.Response(status=404, text="pod sandbox not ready")
+        if spdy.is_upgrade(req):          # SPDY clients name the port per stream (the `port` header)
+            return await spdy.upgrade_proxy(req, await self.k.cri.port_forward_url(sid, ports))
+        if not ports:
+            return web.Response(status=400, text="port is required")
         url = await self.k.cri.port_forward_url(sid, ports)
         ws = web.WebSocketResponse(protocols=PORTFORWARD_PROTOCOLS, max_msg_size=0)
         await ws.prepare(req)
