@@ -363,6 +363,8 @@ class APIServer:
                               reuse_address=True)
             await ins.start()
             self.insecure_port = ins._server.sockets[0].getsockname()[1]
+        if hasattr(self.store, "start"):           # an etcd-backed replica applies its watch on this loop
+            self.store.start(asyncio.get_running_loop())
         self._bg.append(asyncio.create_task(self._event_gc()))
         self._bg.append(asyncio.create_task(self.aggregator.run_availability(), name="apiservice-availability"))
         self.crds.start()
@@ -394,8 +396,17 @@ class APIServer:
               "subsets": [{"addresses": [{"ip": ip}], "ports": [{"name": "https", "port": self.port, "protocol": "TCP"}]}]}
         ers = self.registry.rs("endpoints")
         cur = ers.storage.get(ers.key("default", "kubernetes"), ignore_not_found=True)
+        if cur is not None and int(self.opts.get("apiserver_count") or 1) > 1:
+            # --apiserver-count > 1 (the master-count reconciler): keep the other apiservers' addresses
+            mine = ep["subsets"][0]
+            merged = [s for s in cur.get("subsets") or [] if s != mine]
+            ep["subsets"] = sorted(merged + [mine], key=lambda s: json.dumps(s, sort_keys=True))
         if cur is None:
-            ers.create("default", ep)
+            try:
+                ers.create("default", ep)
+            except m.StatusError as e:          # another apiserver created it first
+                if e.code != 409:
+                    raise
         elif cur.get("subsets") != ep["subsets"]:
             ep["metadata"]["resourceVersion"] = cur["metadata"]["resourceVersion"]
             ers.update("default", "kubernetes", ep)

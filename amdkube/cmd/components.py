@@ -178,10 +178,17 @@ def apiserver(argv):
                     help="encoding of objects in the store (the reference's etcd3 default is protobuf)")
     # accepted for command-line compatibility: etcd and watch-cache tuning of a store this
     # apiserver embeds, SSH tunnels and other knobs with no counterpart here
-    for flag in ("--etcd-servers", "--etcd-servers-overrides", "--etcd-cafile", "--etcd-certfile", "--etcd-keyfile",
+    ap.add_argument("--etcd-servers", default=None,
+                    help="etcd v3 endpoints (amdkube etcd or etcd) shared by several apiservers; unset: the embedded store")
+    ap.add_argument("--etcd-cafile", default=None)
+    ap.add_argument("--etcd-certfile", default=None)
+    ap.add_argument("--etcd-keyfile", default=None)
+    ap.add_argument("--apiserver-count", type=int, default=1,
+                    help="apiservers sharing the store: the kubernetes endpoints keep every one's address")
+    for flag in ("--etcd-servers-overrides",
                  "--etcd-prefix", "--etcd-quorum-read", "--etcd-compaction-interval", "--storage-backend",
                  "--storage-versions", "--watch-cache", "--watch-cache-sizes",
-                 "--default-watch-cache-size", "--deserialization-cache-size", "--target-ram-mb", "--apiserver-count",
+                 "--default-watch-cache-size", "--deserialization-cache-size", "--target-ram-mb",
                  "--endpoint-reconciler-type", "--ssh-user", "--ssh-keyfile", "--cert-dir", "--external-hostname",
                  "--public-address-override", "--kubelet-preferred-address-types", "--kubelet-timeout",
                  "--kubelet-read-only-port", "--kubelet-port", "--max-connection-bytes-per-sec",
@@ -213,7 +220,7 @@ def apiserver(argv):
         "audit_webhook_batch_buffer_size", "audit_webhook_batch_max_size", "audit_webhook_batch_max_wait",
         "audit_webhook_batch_throttle_qps", "audit_webhook_batch_throttle_burst", "advertise_address",
         "kubernetes_service_node_port", "allow_privileged", "runtime_config", "cors_allowed_origins",
-        "enable_logs_handler", "profiling", "min_request_timeout", "storage_media_type")}
+        "enable_logs_handler", "profiling", "min_request_timeout", "storage_media_type", "apiserver_count")}
     options["tls_sni_cert_key"] = sni
     main_port = a.port
     if a.secure_port is not None and a.tls_cert_file:
@@ -233,7 +240,13 @@ def apiserver(argv):
                                     "groups": parts[3].split(",") if len(parts) > 3 else []}
 
     async def mk():
-        srv = APIServer(MVCCStore(a.data_dir, transformer=transformer), admission_plugins=(a.admission_control.split(",") if a.admission_control else DEFAULT_CHAIN),
+        if a.etcd_servers:
+            from ..store.etcd3 import Etcd3Store
+            store = await asyncio.to_thread(Etcd3Store, a.etcd_servers, ca=a.etcd_cafile, cert=a.etcd_certfile,
+                                            key=a.etcd_keyfile, transformer=transformer)
+        else:
+            store = MVCCStore(a.data_dir, transformer=transformer)
+        srv = APIServer(store, admission_plugins=(a.admission_control.split(",") if a.admission_control else DEFAULT_CHAIN),
                         admission_config={"ResourceV2": {"resource_names": tuple(a.resource_v2_resources.split(","))}},
                         token_auth=tokens, authorization_mode=a.authorization_mode, anonymous_auth=a.anonymous_auth == "true",
                         max_in_flight=a.max_requests_inflight, max_mutating_in_flight=a.max_mutating_requests_inflight,
@@ -251,6 +264,31 @@ def apiserver(argv):
                         options=options)
         return await srv.start(a.bind_address, main_port)
     _run_forever(mk)
+
+
+def etcd(argv):
+    """The etcd v3 API over amdkube's MVCC store (store/etcdserver.py), for apiservers that share
+    one store via --etcd-servers."""
+    ap = argparse.ArgumentParser("amdkube etcd")
+    ap.add_argument("--listen-client-urls", default="http://127.0.0.1:2379")
+    ap.add_argument("--data-dir", default=None, help="WAL + snapshot directory (default: memory only)")
+    ap.add_argument("--cert-file", default=None)
+    ap.add_argument("--key-file", default=None)
+    ap.add_argument("--trusted-ca-file", default=None, help="require client certificates signed by this CA")
+    ap.add_argument("--snapshot-count", type=int, default=50_000, help="WAL records between snapshots")
+    ap.add_argument("-v", type=int, default=0)
+    for flag in ("--name", "--advertise-client-urls", "--initial-cluster", "--initial-advertise-peer-urls",
+                 "--listen-peer-urls", "--initial-cluster-state", "--initial-cluster-token", "--client-cert-auth",
+                 "--peer-cert-file", "--peer-key-file", "--peer-trusted-ca-file", "--quota-backend-bytes"):
+        ap.add_argument(flag, default=None, help=argparse.SUPPRESS)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "etcd")
+    from ..store.etcdserver import serve
+    listen = a.listen_client_urls.split(",")[0].split("://", 1)[-1]
+    try:
+        asyncio.run(serve(a.data_dir, listen, a.cert_file, a.key_file, a.trusted_ca_file, a.snapshot_count))
+    except KeyboardInterrupt:
+        pass
 
 
 def scheduler(argv):
@@ -1027,7 +1065,7 @@ def kubeadm(argv):
     return main(argv)
 
 
-COMPONENTS = {"dns": dns, "kube-dns": dns, "kubeadm": kubeadm, "proxy": proxy, "kube-proxy": proxy, "apiserver": apiserver, "kube-apiserver": apiserver, "scheduler": scheduler, "kube-scheduler": scheduler,
+COMPONENTS = {"etcd": etcd, "dns": dns, "kube-dns": dns, "kubeadm": kubeadm, "proxy": proxy, "kube-proxy": proxy, "apiserver": apiserver, "kube-apiserver": apiserver, "scheduler": scheduler, "kube-scheduler": scheduler,
               "controller-manager": controller_manager, "kube-controller-manager": controller_manager, "kubelet": kubelet,
               "rocshim": rocshim, "amd-device-plugin": device_plugin, "device-plugin": device_plugin,
               "amdgpu-exporter": exporter, "exporter": exporter, "hollow-node": hollow_node, "local-up": local_up,

@@ -1,0 +1,304 @@
+"""An apiserver store backed by a remote etcd v3 (`amdkube etcd` or any etcd speaking the v3
+API), so several apiservers share one keyspace (`--etcd-servers`).
+
+Reference: staging/src/k8s.io/apiserver/pkg/storage/etcd3/store.go (writes are etcd Txns:
+Create `If(ModRevision==0).Then(Put)` :152-200, GuaranteedUpdate/Delete `If(ModRevision==X)
+.Then(Put|Delete).Else(Get)` :263, :208-256) and pkg/storage/cacher.go (reads and watches are
+served from a watch-fed in-memory cache).
+
+Etcd3Store IS an MVCCStore: a full local replica the apiserver reads, indexes and watches
+exactly as it does the embedded store (commit hooks, trigger-indexed watchers, history for
+watch-from-revision), fed by ONE etcd watch over the whole keyspace from a background thread.
+Mutations go to etcd as CAS Txns over a blocking gRPC channel, then wait until the replica
+has applied the Txn's revision, so a write is visible to its writer's next read (and to its
+watchers) before the call returns. Other apiservers' writes arrive through the watch.
+
+Stored objects embed metadata.resourceVersion (amdkube serves stored bytes as-is), so a value
+must be rendered for the revision its Txn will commit at. Every apiserver Txn therefore also
+puts a fence key and compares its mod_revision with the replica's: success proves no other
+apiserver committed in between, so the commit revision is the replica's + 1 (the reference
+never stores the version and sets it from mod_revision on decode instead — etcd3/store.go
+versioner). Writes from several apiservers are linearised through the fence; a fence-only
+conflict catches the replica up and retries.
+"""
+from __future__ import annotations
+
+import logging
+import queue
+import threading
+import time
+
+import grpc
+
+from ..grpcdesc.etcd import ETCD as E, EQUAL, EV_PUT, GREATER, T_MOD, T_VERSION
+from .etcdserver import prefix_end
+from .mvcc import DELETE, KV, PUT, CASFailed, Event, KeyExists, KeyNotFound, MVCCStore
+
+log = logging.getLogger("amdkube.etcd3")
+ALL = b"\x00"          # key "\0" with range_end "\0": the whole keyspace
+FENCE = "/amdkube.io/revision-fence"       # written by every apiserver Txn (see Etcd3Store._write)
+_FENCE_B = FENCE.encode()
+
+
+def _s(b: bytes) -> str:
+    return b.decode("utf-8", "surrogateescape")
+
+
+def _b(s: str) -> bytes:
+    return s.encode("utf-8", "surrogateescape")
+
+
+def _channel(endpoint: str, ca=None, cert=None, key=None):
+    target = endpoint.split("://", 1)[-1].rstrip("/")
+    opts = [("grpc.max_receive_message_length", 256 << 20), ("grpc.max_send_message_length", 64 << 20)]
+    if endpoint.startswith("https://") or ca:
+        creds = grpc.ssl_channel_credentials(root_certificates=open(ca, "rb").read() if ca else None,
+                                             private_key=open(key, "rb").read() if key else None,
+                                             certificate_chain=open(cert, "rb").read() if cert else None)
+        return grpc.secure_channel(target, creds, options=opts)
+    return grpc.insecure_channel(target, options=opts)
+
+
+class Etcd3Store(MVCCStore):
+    def __init__(self, endpoints, ca: str | None = None, cert: str | None = None, key: str | None = None,
+                 history: int = 200_000, max_queue: int = 500_000, timeout: float = 10.0, transformer=None):
+        # `transformer` (encryption at rest) applies to the bytes etcd holds; the replica keeps plaintext
+        super().__init__(None, history=history, max_queue=max_queue, transformer=transformer)
+        eps = [e for e in (endpoints.split(",") if isinstance(endpoints, str) else endpoints) if e]
+        self.endpoint = eps[0]
+        self.timeout = timeout
+        self._chan = _channel(self.endpoint, ca, cert, key)
+        self._kvs = E.KV.stub(self._chan)
+        self._watch = E.Watch.stub(self._chan)
+        self._maint = E.Maintenance.stub(self._chan)
+        self._events: queue.Queue = queue.Queue()
+        self._stop = threading.Event()
+        self._loop = None
+        self._thread: threading.Thread | None = None
+        self._call = None
+        self.synced_rev = 0
+        self.resyncs = 0
+        self._initial_sync()
+        self._thread = threading.Thread(target=self._follow, name="etcd3-watch", daemon=True)
+        self._thread.start()
+
+    # ------------------------------------------------------------------ sync
+    def status(self):
+        return self._maint.Status(E.StatusRequest(), timeout=self.timeout)
+
+    def _initial_sync(self):
+        r = self._kvs.Range(E.RangeRequest(key=ALL, range_end=ALL), timeout=self.timeout)
+        with self._lock:
+            for kv in r.kvs:
+                k = _s(kv.key)
+                new = KV(k, self._plain(k, kv.value), kv.create_revision, kv.mod_revision, kv.version)
+                self.kv[k] = new
+                self._index_put(k, new)
+            self.rev = self.compact_rev = self.synced_rev = r.header.revision
+
+    def start(self, loop):
+        """Apply followed events on `loop` (the apiserver's) as they arrive; until then they wait
+        in the queue for the next write or drain()."""
+        self._loop = loop
+        self._kick()
+
+    def _requests(self, first):
+        yield first
+        self._stop.wait()
+
+    def _follow(self):
+        backoff = 0.1
+        while not self._stop.is_set():
+            req = E.WatchRequest(create_request=E.WatchCreateRequest(key=ALL, range_end=ALL,
+                                                                     start_revision=self.synced_rev + 1, prev_kv=True))
+            try:
+                self._call = self._watch.Watch(self._requests(req))
+                for resp in self._call:
+                    if resp.compact_revision:
+                        self._events.put(("resync", None))
+                        self._kick()
+                        break
+                    if resp.canceled:
+                        break
+                    if resp.events:
+                        self.synced_rev = max(self.synced_rev, resp.events[-1].kv.mod_revision)
+                        self._events.put(("events", list(resp.events)))
+                        self._kick()
+                        backoff = 0.1
+            except grpc.RpcError as e:
+                if self._stop.is_set():
+                    return
+                log.warning("etcd watch broke (%s); re-watching from %d", e.code(), self.synced_rev + 1)
+            if self._stop.wait(backoff):
+                return
+            backoff = min(backoff * 2, 2.0)
+
+    def _kick(self):
+        loop = self._loop
+        if loop is not None and not loop.is_closed():
+            try:
+                loop.call_soon_threadsafe(self.drain)
+            except RuntimeError:
+                pass
+
+    def drain(self, until: int = 0, timeout: float | None = None):
+        """Apply queued watch events (on the loop thread). With `until`, block until the replica
+        has reached that revision."""
+        deadline = time.monotonic() + (timeout or self.timeout)
+        while True:
+            try:
+                if until and self.rev < until:
+                    item = self._events.get(timeout=max(0.0, deadline - time.monotonic()))
+                else:
+                    item = self._events.get_nowait()
+            except queue.Empty:
+                if until and self.rev < until:
+                    raise TimeoutError(f"etcd replica did not reach revision {until} (at {self.rev})")
+                return
+            kind, payload = item
+            if kind == "resync":
+                self._resync()
+            else:
+                for ev in payload:
+                    self._apply(ev)
+
+    def _apply(self, ev):
+        key, rev = _s(ev.kv.key), ev.kv.mod_revision
+        with self._lock:
+            if rev <= self.rev and key in self.kv and self.kv[key].mod_rev >= rev:
+                return                                   # already applied (re-watch overlap)
+            cur = self.kv.get(key)
+            if ev.type == EV_PUT:
+                new = KV(key, self._plain(key, ev.kv.value), ev.kv.create_revision, rev, ev.kv.version)
+                self.kv[key] = new
+                self._index_put(key, new)
+                self.rev = max(self.rev, rev)
+                if key != FENCE:                        # the fence is bookkeeping, not an object
+                    self._commit(Event(PUT, new, cur, rev), None)
+            else:
+                self.rev = max(self.rev, rev)
+                if cur is None:
+                    return
+                del self.kv[key]
+                self._index_del(key)
+                self._commit(Event(DELETE, KV(key, cur.value, cur.create_rev, rev, 0), cur, rev), None)
+
+    def _plain(self, key: str, value: bytes) -> bytes:
+        return self.transformer.from_disk(key, value) if self.transformer is not None and key != FENCE else value
+
+    def _sealed(self, key: str, value: bytes) -> bytes:
+        return self.transformer.to_disk(key, value) if self.transformer is not None else value
+
+    def _resync(self):
+        """The watch fell behind a compaction: re-list and turn the difference into events."""
+        self.resyncs += 1
+        r = self._kvs.Range(E.RangeRequest(key=ALL, range_end=ALL), timeout=self.timeout)
+        seen = set()
+        with self._lock:
+            for kv in r.kvs:
+                k = _s(kv.key)
+                seen.add(k)
+                cur = self.kv.get(k)
+                if cur is None or cur.mod_rev != kv.mod_revision:
+                    self._apply(E.Event(type=EV_PUT, kv=kv))
+            for k in [k for k in self.kv if k not in seen]:
+                self._apply(E.Event(type=1, kv=E.KeyValue(key=_b(k), mod_revision=r.header.revision)))
+            self.rev = max(self.rev, r.header.revision)
+            self.synced_rev = max(self.synced_rev, r.header.revision)
+
+    # ------------------------------------------------------------------ writes
+    def _txn(self, compare, success, failure):
+        try:
+            return self._kvs.Txn(E.TxnRequest(compare=compare, success=success, failure=failure), timeout=self.timeout)
+        except grpc.RpcError as e:
+            raise ConnectionError(f"etcd {self.endpoint}: {e.code().name}: {e.details()}") from None
+
+    def _write(self, key: str, value, expect_mod_rev: int | None, delete: bool):
+        """One fenced CAS Txn. The fence compare fails when any other apiserver committed since
+        this replica's view, so a success means the commit revision is exactly rev+1 and the
+        resourceVersion rendered into the value is right; a fence-only failure catches up and
+        retries, an object compare failure is the caller's conflict."""
+        bkey = _b(key)
+        for _ in range(1000):
+            self.drain()
+            fence = self.kv.get(FENCE)
+            guess = self.rev + 1
+            cmp = [E.Compare(key=_FENCE_B, target=T_MOD, result=EQUAL, mod_revision=fence.mod_rev if fence else 0)]
+            if expect_mod_rev is not None and (expect_mod_rev or not delete):
+                cmp.append(E.Compare(key=bkey, target=T_MOD, result=EQUAL, mod_revision=expect_mod_rev))
+            elif delete:
+                cmp.append(E.Compare(key=bkey, target=T_VERSION, result=GREATER, version=0))   # must exist
+            data = None
+            if delete:
+                op = E.RequestOp(request_delete_range=E.DeleteRangeRequest(key=bkey, prev_kv=True))
+            else:
+                data = value(guess) if callable(value) else value
+                op = E.RequestOp(request_put=E.PutRequest(key=bkey, value=self._sealed(key, data)))
+            resp = self._txn(cmp, [E.RequestOp(request_put=E.PutRequest(key=_FENCE_B)), op],
+                             [E.RequestOp(request_range=E.RangeRequest(key=_FENCE_B)),
+                              E.RequestOp(request_range=E.RangeRequest(key=bkey))])
+            if resp.succeeded:
+                rev = resp.header.revision
+                if data is not None and callable(value) and rev != guess:
+                    # a writer outside the fence committed in between: re-render at the real revision
+                    log.warning("etcd3: %s committed at %d, rendered for %d; rewriting", key, rev, guess)
+                    self.drain(until=rev)
+                    return self._write(key, value, rev, False)
+                self.drain(until=rev)
+                return resp, rev, data
+            frr, orr = resp.responses[0].response_range, resp.responses[1].response_range
+            cur_mod = orr.kvs[0].mod_revision if orr.kvs else 0
+            object_ok = (cur_mod == expect_mod_rev) if (expect_mod_rev is not None and (expect_mod_rev or not delete)) \
+                else (not delete or cur_mod != 0)
+            if not object_ok:
+                self.drain(until=orr.header.revision)
+                cur = self.kv.get(key)
+                if cur is None and orr.kvs:
+                    kv = orr.kvs[0]
+                    cur = KV(key, self._plain(key, kv.value), kv.create_revision, kv.mod_revision, kv.version)
+                if expect_mod_rev == 0 and not delete:
+                    raise KeyExists(key)
+                if cur is None:
+                    raise KeyNotFound(key)
+                raise CASFailed(cur)
+            self.drain(until=frr.kvs[0].mod_revision if frr.kvs else 0)     # only the fence moved
+        raise ConnectionError(f"etcd3: {key}: the revision fence kept moving")
+
+    def put(self, key: str, value, expect_mod_rev: int | None = None) -> KV:
+        _, rev, data = self._write(key, value, expect_mod_rev, False)
+        got = self.kv.get(key)
+        if got is not None and got.mod_rev == rev:
+            return got
+        return KV(key, data, got.create_rev if got else rev, rev, 0)     # already replaced in the replica
+
+    def delete(self, key: str, expect_mod_rev: int | None = None) -> KV:
+        resp, _, _ = self._write(key, None, expect_mod_rev, True)
+        pk = resp.responses[1].response_delete_range.prev_kvs[0]
+        return KV(key, self._plain(key, pk.value), pk.create_revision, pk.mod_revision, pk.version)
+
+    def batch(self, ops):
+        raise NotImplementedError("Etcd3Store writes go through put/delete (one etcd Txn each)")
+
+    def compact(self, rev: int):
+        try:
+            self._kvs.Compact(E.CompactionRequest(revision=rev), timeout=self.timeout)
+        except grpc.RpcError as e:
+            if e.code() != grpc.StatusCode.OUT_OF_RANGE:
+                raise
+        super().compact(rev)
+
+    def snapshot(self):
+        pass                       # etcd owns durability
+
+    def close(self):
+        self._stop.set()
+        if self._call is not None:
+            self._call.cancel()
+        if self._thread is not None:
+            self._thread.join(timeout=5)
+        super().close()
+        self._chan.close()
+
+
+def prefix_range(prefix: str) -> tuple[bytes, bytes]:
+    return _b(prefix), prefix_end(_b(prefix))

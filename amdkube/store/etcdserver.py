@@ -1,0 +1,435 @@
+"""`amdkube etcd`: the etcd v3 gRPC API (KV, Watch, Lease, Maintenance.Status) served from the
+MVCC store, so several apiservers can share one store the way the reference's apiservers share
+etcd (staging/src/k8s.io/apiserver/pkg/storage/etcd3/store.go:152-260 drives exactly these
+calls: Create = Txn(If mod_revision==0 Then Put), GuaranteedUpdate / Delete = Txn(If
+mod_revision==X Then Put|DeleteRange Else Range), List = Range(prefix, prefix+1[, revision]),
+Watch = Watch(create{key, range_end, start_revision, prev_kv}), compact.go = Compact).
+
+Semantics follow etcd's (etcdserver/apply.go, mvcc/kvstore_txn.go):
+* a Txn's chosen branch commits at ONE revision (MVCCStore.batch), a Txn of ranges only
+  does not advance it; Range at an old `revision` is rebuilt from the store's event history
+  (compacted: OUT_OF_RANGE "required revision has been compacted"; future: "required revision
+  is a future revision");
+* a watch from a compacted revision is created and immediately canceled with
+  `compact_revision` set (the client re-lists), events are batched per response with prev_kv
+  on request and NOPUT/NODELETE filters;
+* leases carry keys; an expired or revoked lease deletes them in one revision.
+Not provided: members/auth/cluster RPCs, defragment/snapshot/hash, multi-op txn nesting.
+"""
+from __future__ import annotations
+
+import asyncio
+import bisect
+import logging
+import random
+import time
+
+import grpc
+
+from ..grpcdesc.etcd import (EQUAL, ETCD as E, EV_DELETE, EV_PUT, GREATER, LESS, NOT_EQUAL, T_CREATE, T_MOD,
+                             T_VALUE, T_VERSION)
+from .mvcc import PUT, MVCCStore
+
+log = logging.getLogger("amdkube.etcd")
+VERSION = "3.1.11-amdkube"
+NOPUT, NODELETE = 0, 1
+
+
+def _s(b: bytes) -> str:
+    return b.decode("utf-8", "surrogateescape")
+
+
+def _b(s: str) -> bytes:
+    return s.encode("utf-8", "surrogateescape")
+
+
+def prefix_end(key: bytes) -> bytes:
+    """clientv3.GetPrefixRangeEnd: the key with its last non-0xff byte incremented."""
+    k = bytearray(key)
+    for i in range(len(k) - 1, -1, -1):
+        if k[i] < 0xFF:
+            k[i] += 1
+            return bytes(k[:i + 1])
+    return b"\x00"
+
+
+class _Abort(Exception):
+    def __init__(self, code, msg):
+        super().__init__(msg)
+        self.code, self.msg = code, msg
+
+
+class EtcdServer:
+    def __init__(self, store: MVCCStore, cluster_id: int | None = None, member_id: int | None = None):
+        self.store = store
+        rnd = random.Random()
+        self.cluster_id = cluster_id or rnd.getrandbits(63)
+        self.member_id = member_id or rnd.getrandbits(63)
+        self.leases: dict[int, list] = {}          # id -> [ttl, deadline, set(keys)]
+        self.key_lease: dict[str, int] = {}
+        self.server: grpc.aio.Server | None = None
+        self.port = 0
+        self._tasks: list[asyncio.Task] = []
+
+    # ------------------------------------------------------------------ lifecycle
+    async def start(self, address: str = "127.0.0.1:0", credentials=None):
+        self.server = grpc.aio.server(options=[("grpc.max_receive_message_length", 64 << 20),
+                                               ("grpc.max_send_message_length", 256 << 20)])
+        for svc in ("KV", "Watch", "Lease", "Maintenance"):
+            self.server.add_generic_rpc_handlers((E.services[svc].handler(self),))
+        self.port = (self.server.add_secure_port(address, credentials) if credentials is not None
+                     else self.server.add_insecure_port(address))
+        await self.server.start()
+        self._tasks.append(asyncio.create_task(self._lease_reaper()))
+        self.address = f"{address.rsplit(':', 1)[0]}:{self.port}"
+        return self
+
+    async def stop(self, grace: float = 0.5):
+        from ..utils import cancel_and_wait
+        await cancel_and_wait(self._tasks)
+        if self.server is not None:
+            await self.server.stop(grace)
+        for w in self.store.all_watchers():
+            w.close()
+
+    def header(self, rev: int | None = None):
+        return E.ResponseHeader(cluster_id=self.cluster_id, member_id=self.member_id,
+                                revision=self.store.rev if rev is None else rev, raft_term=1)
+
+    def _kv(self, kv, keys_only=False):
+        return E.KeyValue(key=_b(kv.key), create_revision=kv.create_rev, mod_revision=kv.mod_rev, version=kv.version,
+                          value=b"" if keys_only else kv.value, lease=self.key_lease.get(kv.key, 0))
+
+    # ------------------------------------------------------------------ ranges
+    def _keys(self, key: bytes, end: bytes) -> list[str]:
+        st = self.store
+        if not end:
+            return [_s(key)] if _s(key) in st.kv else []
+        if end == prefix_end(key) and key:
+            return st._candidates(_s(key))
+        lo = _s(key)
+        ks = sorted(st.kv) if end == b"\x00" else sorted(k for k in st.kv if lo <= k < _s(end))
+        return ks[bisect.bisect_left(ks, lo):]
+
+    def _at(self, req_key: bytes, end: bytes, rev: int) -> dict[str, object]:
+        """The range as it was at `rev`: the current state with every later event undone."""
+        st = self.store
+        if rev <= st.compact_rev:
+            raise _Abort(grpc.StatusCode.OUT_OF_RANGE, "etcdserver: mvcc: required revision has been compacted")
+        if rev > st.rev:
+            raise _Abort(grpc.StatusCode.OUT_OF_RANGE, "etcdserver: mvcc: required revision is a future revision")
+        lo, hi = _s(req_key), _s(end)
+
+        def inside(k):
+            if not end:
+                return k == lo
+            return k >= lo and (end == b"\x00" or k < hi)
+        state = {k: st.kv[k] for k in self._keys(req_key, end)}
+        for ev in reversed(st.history):
+            if ev.rev <= rev:
+                break
+            k = ev.kv.key
+            if not inside(k):
+                continue
+            if ev.prev is None:
+                state.pop(k, None)
+            else:
+                state[k] = ev.prev
+        return state
+
+    def _range(self, r):
+        st = self.store
+        if r.revision and r.revision != st.rev:
+            state = self._at(r.key, r.range_end, r.revision)
+            kvs = [state[k] for k in sorted(state)]
+        else:
+            kvs = [st.kv[k] for k in self._keys(r.key, r.range_end) if k in st.kv]
+        if r.min_mod_revision or r.max_mod_revision or r.min_create_revision or r.max_create_revision:
+            kvs = [kv for kv in kvs if (not r.min_mod_revision or kv.mod_rev >= r.min_mod_revision)
+                   and (not r.max_mod_revision or kv.mod_rev <= r.max_mod_revision)
+                   and (not r.min_create_revision or kv.create_rev >= r.min_create_revision)
+                   and (not r.max_create_revision or kv.create_rev <= r.max_create_revision)]
+        if r.sort_target or r.sort_order:
+            target = {0: lambda kv: kv.key, 1: lambda kv: kv.version, 2: lambda kv: kv.create_rev,
+                      3: lambda kv: kv.mod_rev, 4: lambda kv: kv.value}[r.sort_target]
+            kvs.sort(key=target, reverse=r.sort_order == 2)
+        count = len(kvs)
+        more = bool(r.limit and count > r.limit)
+        if r.limit:
+            kvs = kvs[:r.limit]
+        resp = E.RangeResponse(header=self.header(), more=more, count=count)
+        if not r.count_only:
+            resp.kvs.extend(self._kv(kv, r.keys_only) for kv in kvs)
+        return resp
+
+    # ------------------------------------------------------------------ KV service
+    async def Range(self, req, ctx):
+        try:
+            return self._range(req)
+        except _Abort as e:
+            await ctx.abort(e.code, e.msg)
+
+    def _check_lease(self, lease: int):
+        if lease and lease not in self.leases:
+            raise _Abort(grpc.StatusCode.NOT_FOUND, "etcdserver: requested lease not found")
+
+    def _attach(self, key: str, lease: int):
+        old = self.key_lease.pop(key, 0)
+        if old in self.leases:
+            self.leases[old][2].discard(key)
+        if lease:
+            self.key_lease[key] = lease
+            self.leases[lease][2].add(key)
+
+    def _detach(self, key: str):
+        self._attach(key, 0)
+
+    def _apply_ops(self, ops):
+        """Commit a list of RequestOp (one revision); returns ResponseOps."""
+        batch, plan = [], []
+        for op in ops:
+            kind = op.WhichOneof("request")
+            if kind == "request_put":
+                p = op.request_put
+                self._check_lease(p.lease)
+                batch.append(("put", _s(p.key), p.value))
+                plan.append(("put", p, len(batch) - 1))
+            elif kind == "request_delete_range":
+                d = op.request_delete_range
+                keys = self._keys(d.key, d.range_end)
+                first = len(batch)
+                batch.extend(("delete", k) for k in keys)
+                plan.append(("del", d, (first, len(batch))))
+            elif kind == "request_range":
+                plan.append(("range", op.request_range, None))
+        ranges_before = {i: self._range(p) for i, (k, p, _) in enumerate(plan) if k == "range"}
+        rev, prevs = self.store.batch(batch) if batch else (self.store.rev, [])
+        out = []
+        for i, (kind, p, where) in enumerate(plan):
+            if kind == "put":
+                self._attach(_s(p.key), p.lease)
+                r = E.PutResponse(header=self.header(rev))
+                if p.prev_kv and prevs[where] is not None:
+                    r.prev_kv.CopyFrom(self._kv(prevs[where]))
+                out.append(E.ResponseOp(response_put=r))
+            elif kind == "del":
+                lo, hi = where
+                gone = [pv for pv in prevs[lo:hi] if pv is not None]
+                for pv in gone:
+                    self._detach(pv.key)
+                r = E.DeleteRangeResponse(header=self.header(rev), deleted=len(gone))
+                if p.prev_kv:
+                    r.prev_kvs.extend(self._kv(pv) for pv in gone)
+                out.append(E.ResponseOp(response_delete_range=r))
+            else:
+                out.append(E.ResponseOp(response_range=ranges_before[i]))
+        return rev, out
+
+    async def Put(self, req, ctx):
+        try:
+            _, [r] = self._apply_ops([E.RequestOp(request_put=req)])
+        except _Abort as e:
+            await ctx.abort(e.code, e.msg)
+        return r.response_put
+
+    async def DeleteRange(self, req, ctx):
+        _, [r] = self._apply_ops([E.RequestOp(request_delete_range=req)])
+        return r.response_delete_range
+
+    def _compare(self, c) -> bool:
+        kv = self.store.kv.get(_s(c.key))
+        which = c.WhichOneof("target_union")
+        if c.target == T_VALUE:
+            if kv is None:
+                return False            # etcd: a value compare on a missing key is false
+            have, want = kv.value, c.value
+        else:
+            have = 0 if kv is None else {T_VERSION: kv.version, T_CREATE: kv.create_rev, T_MOD: kv.mod_rev}[c.target]
+            want = getattr(c, which) if which else 0
+        return {EQUAL: have == want, NOT_EQUAL: have != want, GREATER: have > want, LESS: have < want}[c.result]
+
+    async def Txn(self, req, ctx):
+        try:
+            ok = all(self._compare(c) for c in req.compare)
+            rev, out = self._apply_ops(req.success if ok else req.failure)
+        except _Abort as e:
+            await ctx.abort(e.code, e.msg)
+        resp = E.TxnResponse(header=self.header(rev), succeeded=ok)
+        resp.responses.extend(out)
+        return resp
+
+    async def Compact(self, req, ctx):
+        st = self.store
+        if req.revision > st.rev:
+            await ctx.abort(grpc.StatusCode.OUT_OF_RANGE, "etcdserver: mvcc: required revision is a future revision")
+        if req.revision <= st.compact_rev:
+            await ctx.abort(grpc.StatusCode.OUT_OF_RANGE, "etcdserver: mvcc: required revision has been compacted")
+        st.compact(req.revision)
+        return E.CompactionResponse(header=self.header())
+
+    # ------------------------------------------------------------------ Watch service
+    def _watch_scope(self, c):
+        """(prefix, exact, in_range) for an MVCCStore watcher covering [key, range_end)."""
+        lo, end = c.key, c.range_end
+        if not end:
+            return _s(lo), True, None
+        if lo and end == prefix_end(lo):
+            return _s(lo), False, None
+        slo, send = _s(lo), _s(end)
+        common = ""
+        if end != b"\x00":
+            for a, b in zip(slo, send):
+                if a != b:
+                    break
+                common += a
+        return common, False, (lambda k: k >= slo and (end == b"\x00" or k < send))
+
+    async def Watch(self, requests, ctx):
+        out: asyncio.Queue = asyncio.Queue()
+        watches: dict[int, tuple] = {}
+        next_id = iter(range(1, 1 << 62))
+
+        async def pump(wid, w, c):
+            filters = set(c.filters)
+            try:
+                while True:
+                    ev = await w.next()
+                    if ev is None:
+                        out.put_nowait(E.WatchResponse(header=self.header(), watch_id=wid, canceled=True))
+                        return
+                    batch = [ev]
+                    while not w.queue.empty():
+                        nxt = w.queue.get_nowait()
+                        if nxt is None:
+                            w.queue.put_nowait(None)
+                            break
+                        batch.append(nxt)
+                    resp = E.WatchResponse(header=self.header(), watch_id=wid)
+                    for e in batch:
+                        typ = EV_PUT if e.type == PUT else EV_DELETE
+                        if (typ == EV_PUT and NOPUT in filters) or (typ == EV_DELETE and NODELETE in filters):
+                            continue
+                        pe = resp.events.add(type=typ)
+                        pe.kv.CopyFrom(self._kv(e.kv) if e.type == PUT else
+                                       E.KeyValue(key=_b(e.kv.key), mod_revision=e.rev))
+                        if c.prev_kv and e.prev is not None:
+                            pe.prev_kv.CopyFrom(self._kv(e.prev))
+                    if resp.events:
+                        out.put_nowait(resp)
+            except asyncio.CancelledError:
+                pass
+
+        async def progress(wid):
+            while True:
+                await asyncio.sleep(10)
+                out.put_nowait(E.WatchResponse(header=self.header(), watch_id=wid))
+
+        async def reader():
+            async for req in requests:
+                kind = req.WhichOneof("request_union")
+                if kind == "create_request":
+                    c = req.create_request
+                    wid = next(next_id)
+                    prefix, exact, inside = self._watch_scope(c)
+                    st = self.store
+                    if c.start_revision and c.start_revision <= st.compact_rev:
+                        out.put_nowait(E.WatchResponse(header=self.header(), watch_id=wid, created=True))
+                        out.put_nowait(E.WatchResponse(header=self.header(), watch_id=wid, canceled=True,
+                                                       compact_revision=st.compact_rev))
+                        continue
+                    transform = (lambda ev, f=inside: ev if f(ev.kv.key) else None) if inside else None
+                    w = st.watch(prefix, c.start_revision, exact=exact, transform=transform)
+                    out.put_nowait(E.WatchResponse(header=self.header(), watch_id=wid, created=True))
+                    tasks = [asyncio.create_task(pump(wid, w, c))]
+                    if c.progress_notify:
+                        tasks.append(asyncio.create_task(progress(wid)))
+                    watches[wid] = (w, tasks)
+                elif kind == "cancel_request":
+                    wid = req.cancel_request.watch_id
+                    ent = watches.pop(wid, None)
+                    if ent is not None:
+                        ent[0].close()
+                        for t in ent[1]:
+                            t.cancel()
+                        out.put_nowait(E.WatchResponse(header=self.header(), watch_id=wid, canceled=True))
+        rd = asyncio.create_task(reader())
+        try:
+            while True:
+                get = asyncio.ensure_future(out.get())
+                done, _ = await asyncio.wait({get, rd} if not rd.done() else {get}, return_when=asyncio.FIRST_COMPLETED)
+                if get in done:
+                    yield get.result()
+                    continue
+                get.cancel()
+                if rd.exception() is not None:
+                    return
+        finally:
+            rd.cancel()
+            for w, tasks in watches.values():
+                w.close()
+                for t in tasks:
+                    t.cancel()
+
+    # ------------------------------------------------------------------ Lease service
+    async def LeaseGrant(self, req, ctx):
+        lid = req.ID or random.getrandbits(62) + 1
+        if lid in self.leases:
+            return E.LeaseGrantResponse(header=self.header(), ID=lid, TTL=req.TTL, error="lease already exists")
+        ttl = max(req.TTL, 1)
+        self.leases[lid] = [ttl, time.monotonic() + ttl, set()]
+        return E.LeaseGrantResponse(header=self.header(), ID=lid, TTL=ttl)
+
+    def _expire(self, lid: int):
+        ent = self.leases.pop(lid, None)
+        if ent is None:
+            return False
+        keys = sorted(k for k in ent[2] if k in self.store.kv)
+        for k in ent[2]:
+            self.key_lease.pop(k, None)
+        if keys:
+            self.store.batch([("delete", k) for k in keys])
+        return True
+
+    async def LeaseRevoke(self, req, ctx):
+        if not self._expire(req.ID):
+            await ctx.abort(grpc.StatusCode.NOT_FOUND, "etcdserver: requested lease not found")
+        return E.LeaseRevokeResponse(header=self.header())
+
+    async def LeaseKeepAlive(self, requests, ctx):
+        async for req in requests:
+            ent = self.leases.get(req.ID)
+            if ent is None:
+                yield E.LeaseKeepAliveResponse(header=self.header(), ID=req.ID, TTL=0)
+                continue
+            ent[1] = time.monotonic() + ent[0]
+            yield E.LeaseKeepAliveResponse(header=self.header(), ID=req.ID, TTL=ent[0])
+
+    async def _lease_reaper(self):
+        while True:
+            await asyncio.sleep(0.25)
+            now = time.monotonic()
+            for lid in [lid for lid, ent in self.leases.items() if ent[1] <= now]:
+                self._expire(lid)
+
+    # ------------------------------------------------------------------ Maintenance
+    async def Status(self, req, ctx):
+        size = sum(len(kv.value) + len(kv.key) for kv in self.store.kv.values())
+        return E.StatusResponse(header=self.header(), version=VERSION, dbSize=size, leader=self.member_id,
+                                raftIndex=self.store.rev, raftTerm=1)
+
+
+async def serve(data_dir: str | None, listen: str, cert=None, key=None, ca=None, snapshot_every: int = 50_000):
+    """`amdkube etcd`: run until cancelled."""
+    creds = None
+    if cert and key:
+        creds = grpc.ssl_server_credentials([(open(key, "rb").read(), open(cert, "rb").read())],
+                                            root_certificates=open(ca, "rb").read() if ca else None,
+                                            require_client_auth=bool(ca))
+    store = MVCCStore(data_dir, snapshot_every=snapshot_every)
+    srv = await EtcdServer(store).start(listen, creds)
+    print(f"amdkube etcd: serving the etcd v3 API on {srv.address} (revision {store.rev})", flush=True)
+    try:
+        await asyncio.Event().wait()
+    finally:
+        await srv.stop()
+        store.close()

@@ -271,6 +271,34 @@ class MVCCStore:
             self._commit(Event(DELETE, tomb, cur, rev), {"r": rev, "o": "d", "k": key})
             return cur
 
+    def batch(self, ops: list[tuple]) -> tuple[int, list]:
+        """Apply [("put", key, value) | ("delete", key)] at ONE new revision, as an etcd Txn
+        branch does. Returns (revision, [previous KV or None per op]); a batch that changes
+        nothing (only deletes of absent keys) does not advance the revision."""
+        with self._lock:
+            rev = self.rev + 1
+            prevs, staged = [], []
+            for op in ops:
+                key = op[1]
+                cur = self.kv.get(key)
+                prevs.append(cur)
+                if op[0] == "put":
+                    data = op[2](rev) if callable(op[2]) else op[2]
+                    new = KV(key, data, cur.create_rev if cur else rev, rev, (cur.version + 1) if cur else 1)
+                    self.kv[key] = new
+                    self._index_put(key, new)
+                    staged.append((Event(PUT, new, cur, rev), {"r": rev, "o": "p", "k": key, "v": data} if self._wal is not None else None))
+                elif cur is not None:
+                    del self.kv[key]
+                    self._index_del(key)
+                    staged.append((Event(DELETE, KV(key, cur.value, cur.create_rev, rev, 0), cur, rev), {"r": rev, "o": "d", "k": key}))
+            if not staged:
+                return self.rev, prevs
+            self.rev = rev
+            for ev, rec in staged:
+                self._commit(ev, rec)
+            return rev, prevs
+
     def _disk(self, key: str, data: bytes) -> str:
         return _b(self.transformer.to_disk(key, data) if self.transformer is not None else data)
 
@@ -383,11 +411,12 @@ class MVCCStore:
 
     def _recover(self):
         snap = os.path.join(self.data_dir, "snapshot.json")
+        snap_rev = 0
         if os.path.exists(snap):
             with open(snap) as f:
                 s = json.load(f)
             self.rev = s["rev"]
-            self.compact_rev = s["rev"]
+            self.compact_rev = snap_rev = s["rev"]
             for key, v, cr, mr, ver in s["kv"]:
                 self.kv[key] = KV(key, self._undisk(key, v), cr, mr, ver)
         wal = os.path.join(self.data_dir, "wal.log")
@@ -399,7 +428,7 @@ class MVCCStore:
                     except ValueError:
                         break  # torn tail write
                     r = rec["r"]
-                    if r <= self.rev:
+                    if r <= snap_rev:       # a batch writes several records at one revision
                         continue
                     key = rec["k"]
                     cur = self.kv.get(key)

@@ -13,14 +13,16 @@ from google.protobuf import descriptor_pb2
 
 SOURCES = {"deviceplugin_v1alpha": "pkg/kubelet/apis/deviceplugin/v1alpha/api.pb.go",
            "pluginregistration_v1beta": "pkg/kubelet/apis/pluginregistration/v1beta/api.pb.go",
-           "cri_v1alpha1_runtime": "pkg/kubelet/apis/cri/v1alpha1/runtime/api.pb.go"}
+           "cri_v1alpha1_runtime": "pkg/kubelet/apis/cri/v1alpha1/runtime/api.pb.go",
+           "etcdserverpb_rpc": "vendor/github.com/coreos/etcd/etcdserver/etcdserverpb/rpc.pb.go",
+           "mvccpb_kv": "vendor/github.com/coreos/etcd/mvcc/mvccpb/kv.pb.go"}
 OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "fixtures", "reference_descriptors")
 
 
 def main(ref):
     for name, rel in SOURCES.items():
         text = open(os.path.join(ref, rel)).read()
-        start = text.index("var fileDescriptorApi = []byte{")
+        start = re.search(r"var fileDescriptor\w+ = \[\]byte\{", text).start()
         blob = bytes(int(h, 16) for h in re.findall(r"0x([0-9a-fA-F]{2})", text[start:text.index("\n}", start)]))
         descriptor_pb2.FileDescriptorProto.FromString(gzip.decompress(blob))    # must parse
         with open(os.path.join(OUT, name + ".pb.gz"), "wb") as f:
