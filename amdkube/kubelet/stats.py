@@ -85,6 +85,16 @@ class StatsProvider:
             pass
         return tot
 
+    async def _container_pids(self, cid: str) -> set[int] | None:
+        """The container's process tree (CRI ContainerStatus verbose info carries its pid)."""
+        from ..monitoring.collector import container_pids
+        try:
+            _, info = await self.k.cri.container_status(cid, verbose=True)
+            pid = int((info or {}).get("pid") or 0)
+        except Exception:
+            return None
+        return container_pids(pid) if pid else None
+
     async def summary(self) -> dict:
         import psutil
         now = m.now_rfc3339()
@@ -121,7 +131,7 @@ class StatsProvider:
             cont["logs"] = {"time": now, "usedBytes": self._logs(uid, c.metadata.name)}
             ids = dev_map.get((m.namespace_of(p), m.name_of(p), c.metadata.name))
             if ids:
-                cont["accelerators"] = accel.accelerator_stats(ids)
+                cont["accelerators"] = accel.accelerator_stats(ids, await self._container_pids(c.id))
             ent["containers"].append(cont)
         for uid, ent in pods.items():
             vols, local = await asyncio.to_thread(self._volume_stats, uid, now)
@@ -203,6 +213,9 @@ class StatsProvider:
                 L.append(f"container_network_receive_bytes_total{{{lab}}} {net.get('rxBytes', 0)}")
                 L.append(f"container_network_transmit_bytes_total{{{lab}}} {net.get('txBytes', 0)}")
         text = "\n".join(L) + "\n"
-        if self.k.server is not None:
-            text += AcceleratorCollector(self.k.smi, self.k.node_name).render_container_metrics(self.k.server._pod_devices())
+        if self.k.server is not None:     # the summary's per-container stats (process-attributed VRAM)
+            pd = [{"namespace": p["podRef"]["namespace"], "pod": p["podRef"]["name"], "container": c["name"],
+                   "devices": [a["id"] for a in c["accelerators"]], "stats": c["accelerators"]}
+                  for p in summ["pods"] for c in p["containers"] if c.get("accelerators")]
+            text += AcceleratorCollector(self.k.smi, self.k.node_name).render_container_metrics(pd)
         return text

@@ -126,6 +126,7 @@ def partition_fixture(data: dict, compute: str = "SPX", memory: str = "NPS1") ->
 
 class Backend:
     name = "base"
+    per_process = False     # processes() reports per-PID VRAM (container attribution)
 
     def gpus(self) -> list[dict]:
         raise NotImplementedError
@@ -177,6 +178,8 @@ class Backend:
 
 
 class AmdSmiBackend(Backend):
+    per_process = True
+
     name = "amdsmi"
 
     def __init__(self):
@@ -296,6 +299,8 @@ class SysfsBackend(Backend):
 
 
 class FakeBackend(Backend):
+    per_process = True
+
     """Fixture-driven backend; mutable so tests can inject faults (ECC errors, lost GPUs)."""
     name = "fake"
 
@@ -430,6 +435,10 @@ def open_backend(kind: str = "auto", fixture: str | None = None, n: int | None =
 
 
 class _Limited(Backend):
+    @property
+    def per_process(self):
+        return self.inner.per_process
+
     """Expose only the first n physical GPUs (allocatable-GPU scaling runs: 1/2/4/8); on a
     partitioned node every partition of those GPUs stays visible."""
 

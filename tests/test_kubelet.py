@@ -144,8 +144,21 @@ def test_kubelet_http_api_and_metrics():
                 assert len(summ["node"]["accelerators"]) == 2
                 acc = summ["pods"][0]["containers"][0]["accelerators"]
                 assert len(acc) == 1 and acc[0]["make"] == "amd"
+                # VRAM is attributed by process: only what the container's own processes hold counts
+                # (a partitioned GPU's device-level number would include its neighbours)
+                from amdkube.smi import device_id
+                smi = lc.kubelet.smi
+                fake = getattr(smi, "inner", smi)
+                idx = next(g["index"] for g in smi.gpus() if device_id(g) == acc[0]["id"])
+                cid = next(x.id for x in await lc.kubelet.cri.list_containers() if x.metadata.name == "c")
+                _, info = await lc.kubelet.cri.container_status(cid, verbose=True)
+                fake.procs[idx] = [{"pid": int(info["pid"]), "vram_bytes": 123456789}, {"pid": 1, "vram_bytes": 5 << 30}]
+                summ = await (await s.get(base + "/stats/summary")).json()
+                assert summ["pods"][0]["containers"][0]["accelerators"][0]["memoryUsed"] == 123456789
                 cad = await (await s.get(base + "/metrics/cadvisor")).text()
                 assert 'container_accelerator_memory_total_bytes{container_name="c",pod_name="s"' in cad
+                assert [ln for ln in cad.splitlines() if ln.startswith("container_accelerator_memory_used_bytes")][0] \
+                    .endswith(" 123456789")
                 met = await (await s.get(base + "/metrics")).text()
                 assert "kubelet_device_plugin_registration_count_total" in met and "kubelet_pod_start_latency_microseconds" in met
                 logs = await (await s.get(base + "/containerLogs/default/s/c")).text()
