@@ -15,6 +15,7 @@ process list it falls back to the device's VRAM in use, as cAdvisor's NVML colle
 """
 from __future__ import annotations
 
+import os
 import time
 
 from ..smi import device_id
@@ -81,10 +82,13 @@ class AcceleratorCollector:
             used = int(s.get("vram_used_bytes") or 0)
             if pids is not None and getattr(self.b, "per_process", False):
                 try:
-                    used = sum(int(p.get("vram_bytes") or 0) for p in self.b.processes(g["index"])
-                               if int(p.get("pid", -1)) in pids)
+                    procs = self.b.processes(g["index"])
                 except Exception:
-                    pass
+                    procs = None
+                # only when the SMI's PIDs are ours to compare (same PID namespace): otherwise keep
+                # the device-level number rather than attribute nothing
+                if procs is not None and (not procs or any(os.path.exists(f"/proc/{int(p.get('pid', -1))}") for p in procs)):
+                    used = sum(int(p.get("vram_bytes") or 0) for p in procs if int(p.get("pid", -1)) in pids)
             out.append({"make": "amd", "model": g.get("market_name", ""), "id": did,
                         "memoryTotal": int(g.get("vram_total_bytes") or 0), "memoryUsed": used,
                         "dutyCycle": duty_cycle(self.b, g["index"], s)})
