@@ -276,17 +276,34 @@ def etcd(argv):
     ap.add_argument("--key-file", default=None)
     ap.add_argument("--trusted-ca-file", default=None, help="require client certificates signed by this CA")
     ap.add_argument("--snapshot-count", type=int, default=50_000, help="WAL records between snapshots")
+    ap.add_argument("--name", default="default", help="this member's name in --initial-cluster")
+    ap.add_argument("--initial-cluster", default="",
+                    help="name=peerURL,... of every member: a raft group (static membership)")
+    ap.add_argument("--listen-peer-urls", default=None, help="raft + forwarded client calls (default: this member's "
+                                                              "--initial-cluster URL)")
+    ap.add_argument("--heartbeat-interval", type=int, default=100, help="ms")
+    ap.add_argument("--election-timeout", type=int, default=1000, help="ms")
     ap.add_argument("-v", type=int, default=0)
-    for flag in ("--name", "--advertise-client-urls", "--initial-cluster", "--initial-advertise-peer-urls",
-                 "--listen-peer-urls", "--initial-cluster-state", "--initial-cluster-token", "--client-cert-auth",
-                 "--peer-cert-file", "--peer-key-file", "--peer-trusted-ca-file", "--quota-backend-bytes"):
+    for flag in ("--advertise-client-urls", "--initial-advertise-peer-urls", "--initial-cluster-state",
+                 "--initial-cluster-token", "--client-cert-auth", "--peer-cert-file", "--peer-key-file",
+                 "--peer-trusted-ca-file", "--quota-backend-bytes"):
         ap.add_argument(flag, default=None, help=argparse.SUPPRESS)
     a = ap.parse_args(argv)
     klog.setup(a.v, "etcd")
     from ..store.etcdserver import serve
-    listen = a.listen_client_urls.split(",")[0].split("://", 1)[-1]
+    strip = lambda u: u.split("://", 1)[-1].rstrip("/")   # noqa: E731
+    listen = strip(a.listen_client_urls.split(",")[0])
+    peers = {}
+    for item in filter(None, a.initial_cluster.split(",")):
+        n, _, url = item.partition("=")
+        peers[n.strip()] = strip(url)
+    if peers and a.name not in peers:
+        ap.error(f"--name {a.name} is not in --initial-cluster")
+    peer_listen = strip(a.listen_peer_urls.split(",")[0]) if a.listen_peer_urls else peers.get(a.name)
     try:
-        asyncio.run(serve(a.data_dir, listen, a.cert_file, a.key_file, a.trusted_ca_file, a.snapshot_count))
+        asyncio.run(serve(a.data_dir, listen, a.cert_file, a.key_file, a.trusted_ca_file, a.snapshot_count,
+                          name=a.name, peers=peers, peer_listen=peer_listen,
+                          heartbeat=a.heartbeat_interval / 1000.0, election=a.election_timeout / 1000.0))
     except KeyboardInterrupt:
         pass
 

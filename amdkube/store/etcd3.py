@@ -64,30 +64,55 @@ class Etcd3Store(MVCCStore):
                  history: int = 200_000, max_queue: int = 500_000, timeout: float = 10.0, transformer=None):
         # `transformer` (encryption at rest) applies to the bytes etcd holds; the replica keeps plaintext
         super().__init__(None, history=history, max_queue=max_queue, transformer=transformer)
-        eps = [e for e in (endpoints.split(",") if isinstance(endpoints, str) else endpoints) if e]
-        self.endpoint = eps[0]
+        self.endpoints = [e for e in (endpoints.split(",") if isinstance(endpoints, str) else endpoints) if e]
         self.timeout = timeout
-        self._chan = _channel(self.endpoint, ca, cert, key)
-        self._kvs = E.KV.stub(self._chan)
-        self._watch = E.Watch.stub(self._chan)
-        self._maint = E.Maintenance.stub(self._chan)
+        self._creds = (ca, cert, key)
+        self._ep = 0
+        self._chan = None
+        self._connect(0)
         self._events: queue.Queue = queue.Queue()
         self._stop = threading.Event()
         self._loop = None
         self._thread: threading.Thread | None = None
-        self._call = None
+        self._watch_call = None
         self.synced_rev = 0
         self.resyncs = 0
         self._initial_sync()
         self._thread = threading.Thread(target=self._follow, name="etcd3-watch", daemon=True)
         self._thread.start()
 
+    # ------------------------------------------------------------------ endpoints
+    def _connect(self, i: int):
+        """Talk to endpoint i (a member of an etcd cluster; any member forwards to the leader)."""
+        if self._chan is not None:
+            self._chan.close()
+        self._ep = i % len(self.endpoints)
+        self.endpoint = self.endpoints[self._ep]
+        self._chan = _channel(self.endpoint, *self._creds)
+        self._kvs = E.KV.stub(self._chan)
+        self._maint = E.Maintenance.stub(self._chan)
+
+    def _call(self, method: str, req, retry_timeouts: bool = False):
+        """A unary KV call with fail-over: an unreachable member (or one without a leader) sends
+        the call to the next endpoint. A timed-out write is not retried (it may have committed)."""
+        retry = {grpc.StatusCode.UNAVAILABLE} | ({grpc.StatusCode.DEADLINE_EXCEEDED} if retry_timeouts else set())
+        deadline = time.monotonic() + max(self.timeout, 3.0)
+        while True:
+            try:
+                return getattr(self._kvs, method)(req, timeout=self.timeout)
+            except grpc.RpcError as e:
+                if e.code() not in retry or time.monotonic() > deadline:
+                    raise
+                log.warning("etcd %s: %s (%s); trying the next endpoint", self.endpoint, method, e.code().name)
+                self._connect(self._ep + 1)
+                time.sleep(0.1)
+
     # ------------------------------------------------------------------ sync
     def status(self):
         return self._maint.Status(E.StatusRequest(), timeout=self.timeout)
 
     def _initial_sync(self):
-        r = self._kvs.Range(E.RangeRequest(key=ALL, range_end=ALL), timeout=self.timeout)
+        r = self._call("Range", E.RangeRequest(key=ALL, range_end=ALL), retry_timeouts=True)
         with self._lock:
             for kv in r.kvs:
                 k = _s(kv.key)
@@ -107,13 +132,16 @@ class Etcd3Store(MVCCStore):
         self._stop.wait()
 
     def _follow(self):
-        backoff = 0.1
+        backoff, ep, chan = 0.1, self._ep, None
         while not self._stop.is_set():
             req = E.WatchRequest(create_request=E.WatchCreateRequest(key=ALL, range_end=ALL,
                                                                      start_revision=self.synced_rev + 1, prev_kv=True))
+            if chan is None:
+                chan = _channel(self.endpoints[ep % len(self.endpoints)], *self._creds)
             try:
-                self._call = self._watch.Watch(self._requests(req))
-                for resp in self._call:
+                # every member applies the same log, so a watch resumes at the same revision on any of them
+                self._watch_call = E.Watch.stub(chan).Watch(self._requests(req))
+                for resp in self._watch_call:
                     if resp.compact_revision:
                         self._events.put(("resync", None))
                         self._kick()
@@ -127,11 +155,16 @@ class Etcd3Store(MVCCStore):
                         backoff = 0.1
             except grpc.RpcError as e:
                 if self._stop.is_set():
-                    return
-                log.warning("etcd watch broke (%s); re-watching from %d", e.code(), self.synced_rev + 1)
+                    break
+                log.warning("etcd watch on %s broke (%s); re-watching from %d", self.endpoints[ep % len(self.endpoints)],
+                            e.code(), self.synced_rev + 1)
+                chan.close()
+                chan, ep = None, ep + 1
             if self._stop.wait(backoff):
-                return
+                break
             backoff = min(backoff * 2, 2.0)
+        if chan is not None:
+            chan.close()
 
     def _kick(self):
         loop = self._loop
@@ -192,7 +225,7 @@ class Etcd3Store(MVCCStore):
     def _resync(self):
         """The watch fell behind a compaction: re-list and turn the difference into events."""
         self.resyncs += 1
-        r = self._kvs.Range(E.RangeRequest(key=ALL, range_end=ALL), timeout=self.timeout)
+        r = self._call("Range", E.RangeRequest(key=ALL, range_end=ALL), retry_timeouts=True)
         seen = set()
         with self._lock:
             for kv in r.kvs:
@@ -209,7 +242,7 @@ class Etcd3Store(MVCCStore):
     # ------------------------------------------------------------------ writes
     def _txn(self, compare, success, failure):
         try:
-            return self._kvs.Txn(E.TxnRequest(compare=compare, success=success, failure=failure), timeout=self.timeout)
+            return self._call("Txn", E.TxnRequest(compare=compare, success=success, failure=failure))
         except grpc.RpcError as e:
             raise ConnectionError(f"etcd {self.endpoint}: {e.code().name}: {e.details()}") from None
 
@@ -281,7 +314,7 @@ class Etcd3Store(MVCCStore):
 
     def compact(self, rev: int):
         try:
-            self._kvs.Compact(E.CompactionRequest(revision=rev), timeout=self.timeout)
+            self._call("Compact", E.CompactionRequest(revision=rev))
         except grpc.RpcError as e:
             if e.code() != grpc.StatusCode.OUT_OF_RANGE:
                 raise
@@ -292,8 +325,8 @@ class Etcd3Store(MVCCStore):
 
     def close(self):
         self._stop.set()
-        if self._call is not None:
-            self._call.cancel()
+        if self._watch_call is not None:
+            self._watch_call.cancel()
         if self._thread is not None:
             self._thread.join(timeout=5)
         super().close()

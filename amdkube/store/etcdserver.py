@@ -53,6 +53,19 @@ def prefix_end(key: bytes) -> bytes:
     return b"\x00"
 
 
+K_TXN, K_PUT, K_DELETE, K_COMPACT, K_LEASE_GRANT, K_LEASE_REVOKE = 1, 2, 3, 4, 5, 6
+_REQ = {K_TXN: E.TxnRequest, K_PUT: E.PutRequest, K_DELETE: E.DeleteRangeRequest, K_COMPACT: E.CompactionRequest,
+        K_LEASE_GRANT: E.LeaseGrantRequest, K_LEASE_REVOKE: E.LeaseRevokeRequest}
+_METHOD = {K_TXN: "Txn", K_PUT: "Put", K_DELETE: "DeleteRange", K_COMPACT: "Compact", K_LEASE_GRANT: "LeaseGrant",
+           K_LEASE_REVOKE: "LeaseRevoke"}
+_KV_KINDS = {K_TXN, K_PUT, K_DELETE, K_COMPACT}
+
+
+def _hash_id(name: str) -> int:
+    import hashlib
+    return int.from_bytes(hashlib.sha256(name.encode()).digest()[:8], "big") & ((1 << 63) - 1)
+
+
 class _Abort(Exception):
     def __init__(self, code, msg):
         super().__init__(msg)
@@ -60,26 +73,46 @@ class _Abort(Exception):
 
 
 class EtcdServer:
-    def __init__(self, store: MVCCStore, cluster_id: int | None = None, member_id: int | None = None):
+    def __init__(self, store: MVCCStore, cluster_id: int | None = None, member_id: int | None = None,
+                 name: str = "default", peers: dict[str, str] | None = None, data_dir: str | None = None,
+                 heartbeat: float = 0.1, election: float = 1.0, compact_every: int = 10_000):
         self.store = store
-        rnd = random.Random()
-        self.cluster_id = cluster_id or rnd.getrandbits(63)
-        self.member_id = member_id or rnd.getrandbits(63)
+        self.compact_every = compact_every
+        self.name = name
+        self.peers = peers or {}
+        self.cluster_id = cluster_id or (_hash_id(",".join(f"{k}={v}" for k, v in sorted(self.peers.items())))
+                                         if self.peers else random.getrandbits(63))
+        self.member_id = member_id or _hash_id(name)
         self.leases: dict[int, list] = {}          # id -> [ttl, deadline, set(keys)]
         self.key_lease: dict[str, int] = {}
         self.server: grpc.aio.Server | None = None
         self.port = 0
         self._tasks: list[asyncio.Task] = []
+        self.raft = None
+        self._raft_args = (data_dir, heartbeat, election)
+        self._fwd: dict[str, grpc.aio.Channel] = {}
 
     # ------------------------------------------------------------------ lifecycle
-    async def start(self, address: str = "127.0.0.1:0", credentials=None):
-        self.server = grpc.aio.server(options=[("grpc.max_receive_message_length", 64 << 20),
+    async def start(self, address: str = "127.0.0.1:0", credentials=None, peer_address: str | None = None):
+        """Serve the client API on `address`; with a cluster, also on `peer_address`, which
+        carries the raft service (members forward client calls to the leader over it)."""
+        self.server = grpc.aio.server(options=[("grpc.max_receive_message_length", 256 << 20),
                                                ("grpc.max_send_message_length", 256 << 20)])
         for svc in ("KV", "Watch", "Lease", "Maintenance"):
             self.server.add_generic_rpc_handlers((E.services[svc].handler(self),))
+        if len(self.peers) > 1:
+            from .raft import Raft
+            data_dir, hb, el = self._raft_args
+            self.raft = Raft(self.name, self.peers, data_dir, self, heartbeat=hb, election=el,
+                             compact_every=self.compact_every)
+            self.server.add_generic_rpc_handlers((self.raft.handler(),))
         self.port = (self.server.add_secure_port(address, credentials) if credentials is not None
                      else self.server.add_insecure_port(address))
+        if peer_address:
+            self.peer_port = self.server.add_insecure_port(peer_address)
         await self.server.start()
+        if self.raft is not None:
+            await self.raft.start()
         self._tasks.append(asyncio.create_task(self._lease_reaper()))
         self.address = f"{address.rsplit(':', 1)[0]}:{self.port}"
         return self
@@ -87,10 +120,103 @@ class EtcdServer:
     async def stop(self, grace: float = 0.5):
         from ..utils import cancel_and_wait
         await cancel_and_wait(self._tasks)
+        if self.raft is not None:
+            await self.raft.stop()
+        for ch in self._fwd.values():
+            await ch.close()
         if self.server is not None:
             await self.server.stop(grace)
         for w in self.store.all_watchers():
             w.close()
+
+    # ------------------------------------------------------------------ raft state machine
+    def apply(self, index: int, data: bytes):
+        """Raft apply: one committed client mutation, deterministic on every member."""
+        kind, body = data[0], data[1:]
+        return self._exec(kind, _REQ[kind].FromString(body))
+
+    def snapshot(self) -> bytes:
+        import json as _json
+        return _json.dumps({"store": self.store.dump_state(),
+                            "leases": {str(k): [v[0], sorted(v[2])] for k, v in self.leases.items()}}).encode()
+
+    def restore(self, data: bytes):
+        import json as _json
+        d = _json.loads(data)
+        self.store.load_state(d["store"])
+        self.leases, self.key_lease = {}, {}
+        for lid, (ttl, keys) in d["leases"].items():
+            self.leases[int(lid)] = [ttl, time.monotonic() + ttl, set(keys)]
+            for k in keys:
+                self.key_lease[k] = int(lid)
+
+    def on_leader(self):
+        """A new leader restarts every lease's clock (etcd lessor Promote)."""
+        now = time.monotonic()
+        for ent in self.leases.values():
+            ent[1] = now + ent[0]
+
+    def _leader_channel(self, leader: str):
+        ch = self._fwd.get(leader)
+        if ch is None:
+            ch = self._fwd[leader] = grpc.aio.insecure_channel(self.peers[leader])
+        return ch
+
+    async def _submit(self, kind: int, req, ctx):
+        """A mutation: applied here (single member), proposed (raft leader) or forwarded to the
+        leader (raft follower)."""
+        from .raft import NotLeader
+        try:
+            if self.raft is None:
+                return self._exec(kind, req)
+            try:
+                return await self.raft.propose(bytes([kind]) + req.SerializeToString())
+            except NotLeader as e:
+                leader = e.leader or self.raft.leader
+                if not leader or leader == self.name:
+                    raise _Abort(grpc.StatusCode.UNAVAILABLE, "etcdserver: no leader") from None
+                stub = E.KV.stub(self._leader_channel(leader)) if kind in _KV_KINDS else E.Lease.stub(self._leader_channel(leader))
+                try:
+                    return await getattr(stub, _METHOD[kind])(req, timeout=10)
+                except grpc.RpcError as ge:
+                    raise _Abort(ge.code(), ge.details()) from None
+            except asyncio.TimeoutError:
+                raise _Abort(grpc.StatusCode.UNAVAILABLE, "etcdserver: request timed out") from None
+        except _Abort as e:
+            await ctx.abort(e.code, e.msg)
+
+    def _exec(self, kind: int, req):
+        if kind == K_TXN:
+            ok = all(self._compare(c) for c in req.compare)
+            rev, out = self._apply_ops(req.success if ok else req.failure)
+            resp = E.TxnResponse(header=self.header(rev), succeeded=ok)
+            resp.responses.extend(out)
+            return resp
+        if kind == K_PUT:
+            _, [r] = self._apply_ops([E.RequestOp(request_put=req)])
+            return r.response_put
+        if kind == K_DELETE:
+            _, [r] = self._apply_ops([E.RequestOp(request_delete_range=req)])
+            return r.response_delete_range
+        if kind == K_COMPACT:
+            st = self.store
+            if req.revision > st.rev:
+                raise _Abort(grpc.StatusCode.OUT_OF_RANGE, "etcdserver: mvcc: required revision is a future revision")
+            if req.revision <= st.compact_rev:
+                raise _Abort(grpc.StatusCode.OUT_OF_RANGE, "etcdserver: mvcc: required revision has been compacted")
+            st.compact(req.revision)
+            return E.CompactionResponse(header=self.header())
+        if kind == K_LEASE_GRANT:
+            if req.ID in self.leases:
+                return E.LeaseGrantResponse(header=self.header(), ID=req.ID, TTL=req.TTL, error="lease already exists")
+            ttl = max(req.TTL, 1)
+            self.leases[req.ID] = [ttl, time.monotonic() + ttl, set()]
+            return E.LeaseGrantResponse(header=self.header(), ID=req.ID, TTL=ttl)
+        if kind == K_LEASE_REVOKE:
+            if not self._expire(req.ID):
+                raise _Abort(grpc.StatusCode.NOT_FOUND, "etcdserver: requested lease not found")
+            return E.LeaseRevokeResponse(header=self.header())
+        raise _Abort(grpc.StatusCode.INTERNAL, f"unknown entry kind {kind}")
 
     def header(self, rev: int | None = None):
         return E.ResponseHeader(cluster_id=self.cluster_id, member_id=self.member_id,
@@ -165,6 +291,18 @@ class EtcdServer:
     # ------------------------------------------------------------------ KV service
     async def Range(self, req, ctx):
         try:
+            if self.raft is not None and not req.serializable:
+                from .raft import NotLeader
+                try:
+                    await self.raft.read_barrier()
+                except (NotLeader, TimeoutError):
+                    leader = self.raft.leader
+                    if not leader or leader == self.name:
+                        raise _Abort(grpc.StatusCode.UNAVAILABLE, "etcdserver: no leader") from None
+                    try:
+                        return await E.KV.stub(self._leader_channel(leader)).Range(req, timeout=10)
+                    except grpc.RpcError as ge:
+                        raise _Abort(ge.code(), ge.details()) from None
             return self._range(req)
         except _Abort as e:
             await ctx.abort(e.code, e.msg)
@@ -226,15 +364,10 @@ class EtcdServer:
         return rev, out
 
     async def Put(self, req, ctx):
-        try:
-            _, [r] = self._apply_ops([E.RequestOp(request_put=req)])
-        except _Abort as e:
-            await ctx.abort(e.code, e.msg)
-        return r.response_put
+        return await self._submit(K_PUT, req, ctx)
 
     async def DeleteRange(self, req, ctx):
-        _, [r] = self._apply_ops([E.RequestOp(request_delete_range=req)])
-        return r.response_delete_range
+        return await self._submit(K_DELETE, req, ctx)
 
     def _compare(self, c) -> bool:
         kv = self.store.kv.get(_s(c.key))
@@ -249,23 +382,10 @@ class EtcdServer:
         return {EQUAL: have == want, NOT_EQUAL: have != want, GREATER: have > want, LESS: have < want}[c.result]
 
     async def Txn(self, req, ctx):
-        try:
-            ok = all(self._compare(c) for c in req.compare)
-            rev, out = self._apply_ops(req.success if ok else req.failure)
-        except _Abort as e:
-            await ctx.abort(e.code, e.msg)
-        resp = E.TxnResponse(header=self.header(rev), succeeded=ok)
-        resp.responses.extend(out)
-        return resp
+        return await self._submit(K_TXN, req, ctx)
 
     async def Compact(self, req, ctx):
-        st = self.store
-        if req.revision > st.rev:
-            await ctx.abort(grpc.StatusCode.OUT_OF_RANGE, "etcdserver: mvcc: required revision is a future revision")
-        if req.revision <= st.compact_rev:
-            await ctx.abort(grpc.StatusCode.OUT_OF_RANGE, "etcdserver: mvcc: required revision has been compacted")
-        st.compact(req.revision)
-        return E.CompactionResponse(header=self.header())
+        return await self._submit(K_COMPACT, req, ctx)
 
     # ------------------------------------------------------------------ Watch service
     def _watch_scope(self, c):
@@ -372,12 +492,9 @@ class EtcdServer:
 
     # ------------------------------------------------------------------ Lease service
     async def LeaseGrant(self, req, ctx):
-        lid = req.ID or random.getrandbits(62) + 1
-        if lid in self.leases:
-            return E.LeaseGrantResponse(header=self.header(), ID=lid, TTL=req.TTL, error="lease already exists")
-        ttl = max(req.TTL, 1)
-        self.leases[lid] = [ttl, time.monotonic() + ttl, set()]
-        return E.LeaseGrantResponse(header=self.header(), ID=lid, TTL=ttl)
+        if not req.ID:                                 # the ID is chosen before replication
+            req = E.LeaseGrantRequest(TTL=req.TTL, ID=random.getrandbits(62) + 1)
+        return await self._submit(K_LEASE_GRANT, req, ctx)
 
     def _expire(self, lid: int):
         ent = self.leases.pop(lid, None)
@@ -391,11 +508,14 @@ class EtcdServer:
         return True
 
     async def LeaseRevoke(self, req, ctx):
-        if not self._expire(req.ID):
-            await ctx.abort(grpc.StatusCode.NOT_FOUND, "etcdserver: requested lease not found")
-        return E.LeaseRevokeResponse(header=self.header())
+        return await self._submit(K_LEASE_REVOKE, req, ctx)
 
     async def LeaseKeepAlive(self, requests, ctx):
+        if self.raft is not None and self.raft.role != "leader" and self.raft.leader and self.raft.leader != self.name:
+            stub = E.Lease.stub(self._leader_channel(self.raft.leader))      # relay to the leader's lessor
+            async for resp in stub.LeaseKeepAlive(requests):
+                yield resp
+            return
         async for req in requests:
             ent = self.leases.get(req.ID)
             if ent is None:
@@ -407,26 +527,44 @@ class EtcdServer:
     async def _lease_reaper(self):
         while True:
             await asyncio.sleep(0.25)
+            if self.raft is not None and self.raft.role != "leader":
+                continue                               # only the leader's lessor expires leases
             now = time.monotonic()
             for lid in [lid for lid, ent in self.leases.items() if ent[1] <= now]:
-                self._expire(lid)
+                if self.raft is None:
+                    self._expire(lid)
+                else:
+                    try:
+                        await self.raft.propose(bytes([K_LEASE_REVOKE]) + E.LeaseRevokeRequest(ID=lid).SerializeToString())
+                    except Exception as e:     # lost leadership or the lease went meanwhile
+                        log.debug("lease %d expiry not committed: %s", lid, e)
 
     # ------------------------------------------------------------------ Maintenance
     async def Status(self, req, ctx):
         size = sum(len(kv.value) + len(kv.key) for kv in self.store.kv.values())
-        return E.StatusResponse(header=self.header(), version=VERSION, dbSize=size, leader=self.member_id,
-                                raftIndex=self.store.rev, raftTerm=1)
+        if self.raft is None:
+            return E.StatusResponse(header=self.header(), version=VERSION, dbSize=size, leader=self.member_id,
+                                    raftIndex=self.store.rev, raftTerm=1)
+        r = self.raft
+        return E.StatusResponse(header=self.header(), version=VERSION, dbSize=size,
+                                leader=_hash_id(r.leader) if r.leader else 0, raftIndex=r.commit, raftTerm=r.term)
 
 
-async def serve(data_dir: str | None, listen: str, cert=None, key=None, ca=None, snapshot_every: int = 50_000):
-    """`amdkube etcd`: run until cancelled."""
+async def serve(data_dir: str | None, listen: str, cert=None, key=None, ca=None, snapshot_every: int = 50_000,
+                name: str = "default", peers: dict[str, str] | None = None, peer_listen: str | None = None,
+                heartbeat: float = 0.1, election: float = 1.0):
+    """`amdkube etcd`: run until cancelled. With `peers` (--initial-cluster) the member joins a
+    raft group; its store then lives in memory and the raft log under data_dir is the WAL."""
     creds = None
     if cert and key:
         creds = grpc.ssl_server_credentials([(open(key, "rb").read(), open(cert, "rb").read())],
                                             root_certificates=open(ca, "rb").read() if ca else None,
                                             require_client_auth=bool(ca))
-    store = MVCCStore(data_dir, snapshot_every=snapshot_every)
-    srv = await EtcdServer(store).start(listen, creds)
+    clustered = bool(peers) and len(peers) > 1
+    store = MVCCStore(None if clustered else data_dir, snapshot_every=snapshot_every)
+    srv = await EtcdServer(store, name=name, peers=peers if clustered else None, data_dir=data_dir,
+                           heartbeat=heartbeat, election=election, compact_every=snapshot_every
+                           ).start(listen, creds, peer_listen if clustered else None)
     print(f"amdkube etcd: serving the etcd v3 API on {srv.address} (revision {store.rev})", flush=True)
     try:
         await asyncio.Event().wait()

@@ -204,7 +204,8 @@ class MVCCStore:
 
     def _candidates(self, prefix: str) -> list[str]:
         b = self._bucket_of(prefix)
-        if len(b) <= len(prefix) and prefix.startswith(b) and b.endswith("/"):
+        # the bucket holds every match only when the prefix reaches a full "/a/b/" bucket
+        if len(b) <= len(prefix) and prefix.startswith(b) and b.endswith("/") and b.count("/") >= 3:
             keys = self._sorted.get(b)
             if keys is None:
                 keys = self._sorted[b] = sorted(self.buckets.get(b, ()))
@@ -408,6 +409,29 @@ class MVCCStore:
             self._wal.close()
         self._wal = open(os.path.join(self.data_dir, "wal.log"), "wb", buffering=0)
         self._since_snapshot = 0
+
+    def dump_state(self) -> dict:
+        """The whole keyspace at this revision (a raft snapshot of the store)."""
+        with self._lock:
+            return {"rev": self.rev, "compact_rev": self.compact_rev,
+                    "kv": [[k.key, _b(k.value), k.create_rev, k.mod_rev, k.version] for k in self.kv.values()]}
+
+    def load_state(self, st: dict):
+        """Replace the keyspace with a dumped one (raft InstallSnapshot): history restarts at its
+        revision and every open watch ends (its clients re-list)."""
+        with self._lock:
+            self.kv.clear()
+            self.buckets.clear()
+            self._sorted.clear()
+            for key, v, cr, mr, ver in st["kv"]:
+                kv = self.kv[key] = KV(key, _unb(v), cr, mr, ver)
+                self._index_put(key, kv)
+            self.rev = st["rev"]
+            self.compact_rev = max(st.get("compact_rev", 0), st["rev"])
+            self.history.clear()
+        for w in self.all_watchers():
+            w.err = "store restored from a snapshot"
+            w.close()
 
     def _recover(self):
         snap = os.path.join(self.data_dir, "snapshot.json")

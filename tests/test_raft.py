@@ -1,0 +1,210 @@
+"""A 3-member `amdkube etcd` raft group (reference role: the etcd cluster under the apiservers;
+the raft behaviour itself follows the Raft paper — leader election, log replication, commit by
+majority, InstallSnapshot — and is checked here end to end with real processes):
+
+* one leader; writes through any member land on all of them at the same revisions;
+* a linearizable read on a follower is answered by the leader;
+* the leader is killed: a new one is elected and a client with every endpoint carries on,
+  including its watch;
+* the killed member restarts from its data dir, far enough behind that the compacted log
+  forces an InstallSnapshot, and converges on the same keyspace and revision.
+"""
+import asyncio
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+
+import grpc
+import pytest
+
+from amdkube.grpcdesc.etcd import ETCD as E
+from amdkube.store.etcd3 import Etcd3Store
+from amdkube.store.etcdserver import _hash_id, prefix_end
+
+
+def _ports(n):
+    socks, out = [], []
+    for _ in range(n):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        socks.append(s)
+        out.append(s.getsockname()[1])
+    for s in socks:
+        s.close()
+    return out
+
+
+class Cluster:
+    def __init__(self, tmp, n=3):
+        ports = _ports(2 * n)
+        self.names = [f"m{i}" for i in range(n)]
+        self.client = {nm: f"127.0.0.1:{ports[i]}" for i, nm in enumerate(self.names)}
+        self.peer = {nm: f"127.0.0.1:{ports[n + i]}" for i, nm in enumerate(self.names)}
+        self.tmp, self.procs = tmp, {}
+
+    def start(self, nm):
+        ic = ",".join(f"{k}=http://{v}" for k, v in self.peer.items())
+        self.procs[nm] = subprocess.Popen(
+            [sys.executable, "-m", "amdkube", "etcd", "--name", nm, "--initial-cluster", ic,
+             "--listen-client-urls", f"http://{self.client[nm]}", "--listen-peer-urls", f"http://{self.peer[nm]}",
+             "--data-dir", str(self.tmp / nm), "--heartbeat-interval", "50", "--election-timeout", "400",
+             "--snapshot-count", "40"], stdout=subprocess.DEVNULL, stderr=open(self.tmp / f"{nm}.log", "ab"))
+
+    def kill(self, nm):
+        p = self.procs.pop(nm)
+        p.send_signal(signal.SIGKILL)
+        p.wait(10)
+
+    def stop(self):
+        for p in self.procs.values():
+            p.terminate()
+        for p in self.procs.values():
+            try:
+                p.wait(10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+
+    def status(self, nm, timeout=1.0):
+        with grpc.insecure_channel(self.client[nm]) as ch:
+            return E.Maintenance.stub(ch).Status(E.StatusRequest(), timeout=timeout)
+
+    def leader(self, among=None, timeout=20.0):
+        """The member every live member agrees leads, once there is one."""
+        end = time.time() + timeout
+        ids = {_hash_id(nm): nm for nm in self.names}
+        while time.time() < end:
+            seen = set()
+            for nm in (among or list(self.procs)):
+                try:
+                    seen.add(self.status(nm).leader)
+                except grpc.RpcError:
+                    seen.add(None)
+            if len(seen) == 1 and None not in seen and 0 not in seen and ids.get(next(iter(seen))) in (among or self.procs):
+                return ids[seen.pop()]
+            time.sleep(0.1)
+        raise AssertionError(f"no agreed leader: {seen}")
+
+    def local(self, nm, prefix=b"/r/"):
+        """Serializable (member-local) view of a prefix."""
+        with grpc.insecure_channel(self.client[nm]) as ch:
+            r = E.KV.stub(ch).Range(E.RangeRequest(key=prefix, range_end=prefix_end(prefix), serializable=True), timeout=2)
+        return [(kv.key, kv.value, kv.mod_revision) for kv in r.kvs]
+
+
+@pytest.mark.timeout(180)
+async def test_three_member_raft_group(tmp_path):
+    c = Cluster(tmp_path)
+    try:
+        for nm in c.names:
+            c.start(nm)
+        leader = await asyncio.to_thread(c.leader)
+        followers = [nm for nm in c.names if nm != leader]
+        store = await asyncio.to_thread(Etcd3Store, [c.client[followers[0]], c.client[leader], c.client[followers[1]]])
+        try:
+            store.start(asyncio.get_running_loop())
+            for i in range(10):                     # writes through a follower are forwarded to the leader
+                kv = store.put(f"/r/k{i}", f"v{i}".encode(), expect_mod_rev=0)
+                assert kv.value == f"v{i}".encode()
+            want = sorted((f"/r/k{i}".encode(), f"v{i}".encode(), store.get(f"/r/k{i}").mod_rev) for i in range(10))
+
+            async def converged(members, expect, timeout=15):
+                end = time.time() + timeout
+                while time.time() < end:
+                    views = list((await views_of(members)).values())
+                    if all(v == expect for v in views):
+                        return
+                    await asyncio.sleep(0.1)
+                raise AssertionError(f"members diverge: {views}")
+
+            async def views_of(members):
+                out = {}
+                for nm in members:
+                    try:
+                        out[nm] = await asyncio.to_thread(c.local, nm)
+                    except grpc.RpcError as e:
+                        out[nm] = f"{e.code()} (proc rc={c.procs[nm].poll() if nm in c.procs else 'killed'})"
+                return out
+            await converged(c.names, want)
+            # a linearizable read on a follower is answered by the leader
+            with grpc.insecure_channel(c.client[followers[1]]) as ch:
+                r = E.KV.stub(ch).Range(E.RangeRequest(key=b"/r/k3"), timeout=5)
+                assert r.kvs[0].value == b"v3"
+
+            # the watch keeps flowing across a leader failure
+            w = store.watch("/r/", store.rev + 1)
+            c.kill(leader)
+            new_leader = await asyncio.to_thread(c.leader, followers)
+            assert new_leader in followers
+            for i in range(10, 70):                 # > --snapshot-count: the survivors compact their logs
+                store.put(f"/r/k{i}", f"v{i}".encode())
+            got = []
+            while len(got) < 60:
+                ev = await asyncio.wait_for(w.next(), 20)
+                got.append(ev.kv.key)
+            assert got == [f"/r/k{i}" for i in range(10, 70)]
+            w.close()
+            want = sorted((f"/r/k{i}".encode(), f"v{i}".encode(), store.get(f"/r/k{i}").mod_rev) for i in range(70))
+            await converged(followers, want)
+            # the old leader comes back from its data dir, behind the compacted log: snapshot + catch-up
+            c.start(leader)
+            await converged(c.names, want, timeout=30)
+            assert (await asyncio.to_thread(c.leader)) in c.names
+            assert len({(await asyncio.to_thread(c.status, nm)).header.revision for nm in c.names}) == 1
+            assert os.path.exists(tmp_path / leader / "raft" / "snap.bin")
+        finally:
+            store.close()
+    finally:
+        c.stop()
+
+
+class _SM:
+    def __init__(self):
+        self.applied = []
+
+    def apply(self, i, data):
+        self.applied.append((i, data))
+        return data
+
+    def snapshot(self):
+        return repr(self.applied).encode()
+
+    def restore(self, data):
+        import ast
+        self.applied = ast.literal_eval(data.decode())
+
+
+async def test_raft_log_matching_votes_and_persistence(tmp_path):
+    """Handler-level Raft rules (§5.1-5.4 of the paper) on one member, no network."""
+    from amdkube.store.raft import RAFT as R, Raft
+    sm = _SM()
+    r = Raft("b", {"a": "127.0.0.1:1", "b": "127.0.0.1:2", "c": "127.0.0.1:3"}, str(tmp_path), sm)
+
+    def ents(*spec):
+        return [R.Entry(term=t, index=i, data=f"{i}@{t}".encode()) for i, t in spec]
+    ok = await r.AppendEntries(R.AppendRequest(term=1, leader="a", prev_log_index=0, prev_log_term=0,
+                                               entries=ents((1, 1), (2, 1), (3, 1)), leader_commit=1), None)
+    assert ok.success and ok.match_index == 3 and r.commit == 1 and sm.applied == [(1, b"1@1")]
+    # a gap is refused with a hint at our end of log
+    gap = await r.AppendEntries(R.AppendRequest(term=1, leader="a", prev_log_index=7, prev_log_term=1), None)
+    assert not gap.success and gap.conflict_index == 4
+    # a new leader (term 2) overwrites the uncommitted tail from index 3 on
+    ok = await r.AppendEntries(R.AppendRequest(term=2, leader="c", prev_log_index=2, prev_log_term=1,
+                                               entries=ents((3, 2), (4, 2)), leader_commit=4), None)
+    assert ok.success and [(e.index, e.term) for e in r.log] == [(1, 1), (2, 1), (3, 2), (4, 2)]
+    assert sm.applied[-1] == (4, b"4@2") and r.leader == "c"
+    # mismatched prev term: hint back to the first index of that term
+    bad = await r.AppendEntries(R.AppendRequest(term=2, leader="c", prev_log_index=4, prev_log_term=9), None)
+    assert not bad.success and bad.conflict_index == 3
+    # stale terms are refused; votes need an up-to-date log and one vote per term
+    assert not (await r.AppendEntries(R.AppendRequest(term=1, leader="a"), None)).success
+    assert not (await r.RequestVote(R.VoteRequest(term=3, candidate="a", last_log_index=9, last_log_term=1), None)).granted
+    assert (await r.RequestVote(R.VoteRequest(term=3, candidate="c", last_log_index=4, last_log_term=2), None)).granted
+    assert not (await r.RequestVote(R.VoteRequest(term=3, candidate="a", last_log_index=4, last_log_term=2), None)).granted
+    await r.stop()
+    # term, vote and log survive a restart
+    r2 = Raft("b", {"a": "127.0.0.1:1", "b": "127.0.0.1:2", "c": "127.0.0.1:3"}, str(tmp_path), _SM())
+    assert (r2.term, r2.voted_for, r2.last_index(), r2.last_term()) == (3, "c", 4, 2)
+    await r2.stop()
