@@ -337,6 +337,7 @@ class Raft:
     async def _replicate(self, p: str, term: int):
         stub, kick = self._stubs[p], self._kick[p]
         while self.role == LEADER and self.term == term:
+            kick.clear()             # anything appended or committed from here on triggers another send
             ni = self.next_index[p]
             try:
                 if ni <= self.snap_index:
@@ -380,7 +381,6 @@ class Raft:
             else:
                 self.next_index[p] = max(1, min(r.conflict_index or ni - 1, ni - 1))
                 continue
-            kick.clear()
             try:
                 await asyncio.wait_for(kick.wait(), self.heartbeat)
             except asyncio.TimeoutError:
