@@ -5,8 +5,10 @@ ProviderName, HasClusterID), plugins.go (RegisterCloudProvider / GetCloudProvide
 --cloud-provider name) and providers/fake (the recording fake used by controller tests).
 
 The reference ships AWS / GCE / Azure / vSphere / OpenStack / … drivers. An
-MI355X node runs on-prem or on a GPU cloud with no Kubernetes cloud integration, so the
-providers here are:
+MI355X node runs on-prem — bare metal or an OpenStack cloud — or on a GPU cloud with no
+Kubernetes cloud integration, so the providers here are:
+  * `openstack` (cloudprovider/openstack.py): Keystone + Nova instances/zones, Neutron router
+    routes, Octavia/LBaaS v2 load balancers with floating IPs, Cinder volumes;
   * `baremetal`: load balancers get addresses from a configured pool (the MetalLB model),
     routes are kept in a table and programmed with `ip route` when privileged, and instance
     data comes from the Node objects;
@@ -279,7 +281,26 @@ class Fake(Interface):
         return dict(self.volume_labels.get(m.name_of(pv), {}))
 
 
-_PROVIDERS = {"baremetal": BareMetal, "fake": Fake}
+def _openstack(config):
+    from .openstack import OpenStack
+    return OpenStack(config)
+
+
+_PROVIDERS = {"baremetal": BareMetal, "fake": Fake, "openstack": _openstack}
+
+
+def load_config(path: str | None):
+    """--cloud-config: YAML/JSON, or the reference's INI cloud.conf (returned as text for the
+    provider to parse)."""
+    if not path:
+        return None
+    import yaml
+    text = open(path).read()
+    try:
+        data = yaml.safe_load(text)
+    except yaml.YAMLError:
+        return text
+    return data if isinstance(data, dict) else text
 
 
 def register_cloud_provider(name: str, factory):

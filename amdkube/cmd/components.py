@@ -441,7 +441,8 @@ def controller_manager(argv):
     from ..client import Client
     from ..cloudprovider import get_cloud_provider
     from ..controllers import ControllerManager, Options, resolve_controllers
-    cfg = yaml.safe_load(open(a.cloud_config)) if a.cloud_config else None
+    from ..cloudprovider import load_config as _load_cloud_config
+    cfg = _load_cloud_config(a.cloud_config)
     rd = lambda p: open(p, "rb").read().strip() if p else None  # noqa: E731
     opts = Options(node_monitor_grace=a.node_monitor_grace_period, pod_eviction_timeout=a.pod_eviction_timeout,
                    cluster_cidr=a.cluster_cidr, node_cidr_mask_size=a.node_cidr_mask_size,
@@ -494,7 +495,8 @@ def cloud_controller_manager(argv):
     import yaml
     from ..cloudprovider import get_cloud_provider
     from ..controllers import CLOUD_CONTROLLERS, ControllerManager, Options
-    cfg = yaml.safe_load(open(a.cloud_config)) if a.cloud_config else None
+    from ..cloudprovider import load_config as _load_cloud_config
+    cfg = _load_cloud_config(a.cloud_config)
     opts = Options(cloud=get_cloud_provider(a.cloud_provider, cfg), cluster_name=a.cluster_name,
                    allocate_node_cidrs=a.allocate_node_cidrs == "true", configure_cloud_routes=a.configure_cloud_routes == "true",
                    extra={"node_status_update_frequency": a.node_status_update_frequency,

@@ -50,7 +50,7 @@ class ServiceLBController(Controller):
         if key == "@nodes":
             nodes = self.lb_nodes()
             for k, svc in list(self.known.items()):
-                lb.update(self.cluster, svc, nodes)
+                await asyncio.to_thread(lb.update, self.cluster, svc, nodes)
             return
         svc = self.svc_inf.get(key)
         wants = svc is not None and (svc.get("spec") or {}).get("type") == "LoadBalancer" \
@@ -58,7 +58,7 @@ class ServiceLBController(Controller):
         if not wants:
             old = self.known.pop(key, None)
             if old is not None:
-                lb.ensure_deleted(self.cluster, old)
+                await asyncio.to_thread(lb.ensure_deleted, self.cluster, old)
                 if svc is not None and ((svc.get("status") or {}).get("loadBalancer") or {}).get("ingress"):
                     ns, name = split_key(key)
                     await self.client.patch("services", name, {"status": {"loadBalancer": {}}}, ns, sub="status")
@@ -101,26 +101,32 @@ class RouteController(Controller):
             self.enqueue("@all")
 
     async def sync(self, key):
+        """route_controller.go reconcile: one route per node with a podCIDR (compared by target
+        node and CIDR, the way cloud route tables are keyed), stale ones removed."""
         routes = self.cloud.routes() if self.cloud else None
         if routes is None:
             return
-        have = {r.name: r for r in routes.list(self.cluster)}
+        have = await asyncio.to_thread(routes.list, self.cluster)
         want = {}
         for n in self.node_inf.list():
             cidr = (n.get("spec") or {}).get("podCIDR")
             if cidr:
-                want[f"{self.cluster}-{m.uid_of(n)}"] = Route(f"{self.cluster}-{m.uid_of(n)}", m.name_of(n), cidr)
+                want[m.name_of(n)] = Route(f"{self.cluster}-{m.uid_of(n)}", m.name_of(n), cidr)
                 ip = next((a["address"] for a in (n.get("status") or {}).get("addresses") or [] if a.get("type") == "InternalIP"), None)
                 if ip and hasattr(routes, "node_ips"):
                     routes.node_ips[m.name_of(n)] = ip
-        for name, r in want.items():
-            if have.get(name) != r:
-                routes.create(self.cluster, name, r)
-        for name, r in have.items():
-            if name.startswith(self.cluster + "-") and name not in want:
-                routes.delete(self.cluster, r)
+        present = {(r.target_node, r.destination_cidr) for r in have}
+        for node, r in want.items():
+            if (node, r.destination_cidr) not in present:
+                await asyncio.to_thread(routes.create, self.cluster, r.name, r)
+        for r in have:
+            w = want.get(r.target_node)
+            if (w is None or w.destination_cidr != r.destination_cidr) and \
+                    (r.name.startswith(self.cluster + "-") or r.target_node in {m.name_of(n) for n in self.node_inf.list()}
+                     or not getattr(routes, "named", True)):
+                await asyncio.to_thread(routes.delete, self.cluster, r)
         for n in self.node_inf.list():
-            if f"{self.cluster}-{m.uid_of(n)}" not in want:
+            if m.name_of(n) not in want:
                 continue
             conds = (n.get("status") or {}).get("conditions") or []
             cur = next((c for c in conds if c.get("type") == "NetworkUnavailable"), None)
@@ -315,7 +321,7 @@ class PersistentVolumeLabelController(Controller):
         pending = (((pv or {}).get("metadata") or {}).get("initializers") or {}).get("pending") or []
         if not pending or pending[0].get("name") != PVL_INITIALIZER:
             return
-        labels = self.cloud.labels_for_volume(pv) if hasattr(self.cloud, "labels_for_volume") else {}
+        labels = await asyncio.to_thread(self.cloud.labels_for_volume, pv) if hasattr(self.cloud, "labels_for_volume") else {}
         rest = [p for p in pending if p.get("name") != PVL_INITIALIZER]
         patch = {"metadata": {"initializers": {"pending": rest} if rest else None}}
         if labels:

@@ -40,6 +40,7 @@ from .base import Controller, split_key
 log = logging.getLogger("amdkube.controllers.volumes")
 
 HOSTPATH_PROVISIONERS = ("amdkube.io/host-path", "kubernetes.io/host-path")
+CINDER_PROVISIONER = "kubernetes.io/cinder"
 DEFAULT_CLASS_ANN = "storageclass.kubernetes.io/is-default-class"
 PVC_FINALIZER = "kubernetes.io/pvc-protection"
 PV_FINALIZER = "kubernetes.io/pv-protection"
@@ -162,6 +163,8 @@ class PersistentVolumeBinderController(Controller):
             sc = self._class(claim_class(pvc))
             if sc is not None and sc.get("provisioner") in HOSTPATH_PROVISIONERS:
                 pv = await self._provision(pvc, sc)
+            elif sc is not None and sc.get("provisioner") == CINDER_PROVISIONER and self._cinder() is not None:
+                pv = await self._provision_cinder(pvc, sc)
             else:
                 if (pvc.get("status") or {}).get("phase") != "Pending":
                     await self.client.patch("persistentvolumeclaims", name, {"status": {"phase": "Pending"}}, ns, sub="status")
@@ -182,6 +185,47 @@ class PersistentVolumeBinderController(Controller):
         st = {"phase": "Bound", "accessModes": ps.get("accessModes") or [], "capacity": dict(ps.get("capacity") or {})}
         if {k: (pvc.get("status") or {}).get(k) for k in st} != st:
             await self.client.patch("persistentvolumeclaims", name, {"status": st}, ns, sub="status")
+
+    def _cinder(self):
+        cloud = getattr(getattr(self.mgr, "opts", None), "cloud", None)
+        return cloud.volumes() if cloud is not None and hasattr(cloud, "volumes") else None
+
+    async def _provision_cinder(self, pvc, sc):
+        """cinder_util.go CreateVolume: a Cinder volume of the claim's size (GiB, rounded up) in
+        the class's availability zone and type, tagged with the claim; the PV is labelled with the
+        volume's zone and the region."""
+        from ..api.quantity import parse_quantity
+        size = ((pvc.get("spec") or {}).get("resources") or {}).get("requests", {}).get("storage", "1Gi")
+        gib = max(1, -(-int(parse_quantity(size).value()) // (1 << 30)))
+        params = sc.get("parameters") or {}
+        name = f"pvc-{m.uid_of(pvc)}"
+        tags = {"kubernetes.io/created-for/pvc/namespace": m.namespace_of(pvc),
+                "kubernetes.io/created-for/pvc/name": m.name_of(pvc), "kubernetes.io/created-for/pv/name": name}
+        vols = self._cinder()
+        vol = await asyncio.to_thread(vols.create, f"kubernetes-dynamic-{name}", gib, params.get("type", ""),
+                                      params.get("availability", ""), tags)
+        labels = {}
+        if vol.get("availability_zone"):
+            labels["failure-domain.beta.kubernetes.io/zone"] = vol["availability_zone"]
+        region = getattr(getattr(self.mgr.opts.cloud, "client", None), "region", "")
+        if region:
+            labels["failure-domain.beta.kubernetes.io/region"] = region
+        pv = {"apiVersion": "v1", "kind": "PersistentVolume",
+              "metadata": {"name": name, "labels": labels,
+                           "annotations": {"pv.kubernetes.io/provisioned-by": CINDER_PROVISIONER}},
+              "spec": {"capacity": {"storage": f"{gib}Gi"},
+                       "accessModes": (pvc.get("spec") or {}).get("accessModes") or ["ReadWriteOnce"],
+                       "persistentVolumeReclaimPolicy": sc.get("reclaimPolicy", "Delete"),
+                       "storageClassName": m.name_of(sc),
+                       "cinder": {"volumeID": vol["id"], "fsType": params.get("fsType", "ext4")},
+                       "claimRef": {"kind": "PersistentVolumeClaim", "namespace": m.namespace_of(pvc), "name": m.name_of(pvc),
+                                    "uid": m.uid_of(pvc), "apiVersion": "v1"}}}
+        try:
+            return await self.client.create(pv)
+        except m.StatusError as e:
+            if m.is_already_exists(e):
+                return await self.client.get("persistentvolumes", name)
+            raise
 
     async def _provision(self, pvc, sc):
         size = ((pvc.get("spec") or {}).get("resources") or {}).get("requests", {}).get("storage", "1Gi")
@@ -223,6 +267,9 @@ class PersistentVolumeBinderController(Controller):
         if policy == "Delete":
             if m.annotations_of(pv).get("pv.kubernetes.io/provisioned-by") in HOSTPATH_PROVISIONERS:
                 shutil.rmtree((ps.get("hostPath") or {}).get("path", "") or "/nonexistent", ignore_errors=True)
+            elif ps.get("cinder") and m.annotations_of(pv).get("pv.kubernetes.io/provisioned-by") == CINDER_PROVISIONER \
+                    and self._cinder() is not None:
+                await asyncio.to_thread(self._cinder().delete, ps["cinder"]["volumeID"])   # fails while attached: retried
             try:
                 await self.client.delete("persistentvolumes", name)
             except m.StatusError as e:
@@ -270,6 +317,7 @@ class AttachDetachController(Controller):
         if self._plugins is None:
             from ..volume import NoopMounter, PluginMgr, VolumeHost, default_plugins
             self._plugins = PluginMgr(default_plugins(), VolumeHost("/var/lib/kubelet", client=self.client, mounter=NoopMounter()))
+            self._plugins.host.cloud = getattr(getattr(self.mgr, "opts", None), "cloud", None)
         return self._plugins
 
     def setup(self):

@@ -88,6 +88,7 @@ class VolumeHost:
         self.dev_root = "/"          # where /dev/disk/by-path etc. are looked up (tests: a fake tree)
         self.sys_root = "/sys"
         self.attach_poll = 1.0       # seconds between device-appearance checks
+        self.cloud = None            # the cloud provider (attachable cloud volumes: cinder)
 
     def pod_dir(self, uid: str) -> str:
         return os.path.join(self.root_dir, "pods", uid)
@@ -270,4 +271,5 @@ def sha256_name(*parts: str) -> str:
 def default_plugins() -> list[VolumePlugin]:
     """ProbeVolumePlugins of the reference kubelet (cmd/kubelet/app/plugins.go), MI355X build."""
     from . import csi, local, network, unsupported
-    return [*local.plugins(), *network.plugins(), csi.CSIPlugin(), *unsupported.plugins()]
+    from . import cinder
+    return [*local.plugins(), *network.plugins(), csi.CSIPlugin(), *cinder.plugins(), *unsupported.plugins()]

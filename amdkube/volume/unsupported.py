@@ -1,9 +1,9 @@
 """Volume types whose backends are cloud or vendor services this build cannot reach
-(pkg/volume/aws_ebs, gce_pd, azure_dd, cinder, vsphere_volume, photon_pd, portworx, scaleio,
-storageos, flocker). They are recognised — so a pod using one gets a precise FailedMount event
+(pkg/volume/aws_ebs, gce_pd, azure_dd, vsphere_volume, photon_pd, portworx, scaleio,
+storageos, flocker; Cinder is implemented in volume/cinder.py over the OpenStack provider). They are recognised — so a pod using one gets a precise FailedMount event
 instead of "no volume plugin matched" — but their set-up fails: attaching them needs the cloud
 provider's block-storage API (or the vendor's client library), and amdkube's cloud providers
-are bare metal and fake (no public-cloud SDKs exist offline on an MI355X host).
+are OpenStack, bare metal and fake (no public-cloud SDKs exist offline on an MI355X host).
 """
 from __future__ import annotations
 
@@ -13,7 +13,6 @@ _TYPES = {
     "awsElasticBlockStore": ("kubernetes.io/aws-ebs", "the AWS EC2 API"),
     "gcePersistentDisk": ("kubernetes.io/gce-pd", "the GCE compute API"),
     "azureDisk": ("kubernetes.io/azure-disk", "the Azure compute API"),
-    "cinder": ("kubernetes.io/cinder", "the OpenStack block-storage API"),
     "vsphereVolume": ("kubernetes.io/vsphere-volume", "the vSphere API"),
     "photonPersistentDisk": ("kubernetes.io/photon-pd", "the Photon controller API"),
     "portworxVolume": ("kubernetes.io/portworx-volume", "the Portworx REST API"),
