@@ -177,3 +177,38 @@ def test_rocshim_landlock_mode_end_to_end(fake_dev):
             await shim.stop(kill_pods=True)
             subprocess.run(["rm", "-rf", base])
     run(go())
+
+
+@needs_landlock
+def test_exec_runs_inside_the_container_guard(fake_dev):
+    """CRI ExecSync (and the streaming exec, same argv) starts the process under the container's
+    own guard, the way docker exec enters the container: a GPU container's exec opens only its
+    render node, a non-GPU container's exec reaches neither kfd nor any node."""
+    async def go():
+        base = tempfile.mkdtemp(prefix="rsex", dir="/tmp")
+        shim = await RocShim(os.path.join(base, "s.sock"), os.path.join(base, "state"), hooks_dir=os.path.join(base, "hooks"),
+                             isolation="landlock", dev_root=fake_dev).start()
+        cri = await CRIClient(os.path.join(base, "s.sock")).connect()
+        try:
+            sc = C.PodSandboxConfig(metadata=C.PodSandboxMetadata(name="p", uid="u2", namespace="default"))
+            sid = await cri.run_pod_sandbox(sc)
+            prog = os.path.join(base, "open_all.py")
+            with open(prog, "w") as f:
+                f.write(OPEN_ALL)
+            seen = {}
+            for name, devs in (("gpu", [f"{fake_dev}/kfd", f"{fake_dev}/dri/renderD131"]), ("cpu", [])):
+                cfg = C.ContainerConfig(metadata=C.ContainerMetadata(name=name), image=C.ImageSpec(image="busybox"),
+                                        command=["sleep", "30"],
+                                        devices=[C.Device(container_path=d, host_path=d, permissions="rw") for d in devs])
+                cid = await cri.create_container(sid, cfg, sc)
+                await cri.start_container(cid)
+                out, err, rc = await cri.exec_sync(cid, [sys.executable, prog, fake_dev], 20)
+                assert rc == 0, err
+                seen[name] = json.loads(out.decode().strip().splitlines()[-1])
+            assert [k for k, v in seen["gpu"].items() if v == "ok"] == ["renderD131", "kfd"], seen["gpu"]
+            assert "ok" not in seen["cpu"].values(), seen["cpu"]
+        finally:
+            await cri.close()
+            await shim.stop(kill_pods=True)
+            subprocess.run(["rm", "-rf", base])
+    run(go())
