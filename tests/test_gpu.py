@@ -410,6 +410,75 @@ def test_08_restart_continuity_and_exporter_scrape():
     run(go(), 240)
 
 
+def test_09_gpu_pods_over_a_raft_store_with_protobuf_and_spdy_exec(tmp_path):
+    """The control plane's HA store on the MI355X node: the apiserver keeps its objects in a
+    3-member `amdkube etcd` raft group in the reference's protobuf storage format; a kubectl-style
+    SPDY exec runs vector-add INSIDE a running GPU pod's container (its device guard) and
+    passes, the same exec in a GPU-less pod finds no GPU; the store's leader is killed and
+    the next GPU pod still schedules and runs."""
+    import grpc
+    from amdkube.api import protobuf as pb
+    from amdkube.client.stream import exec_stream
+    from amdkube.grpcdesc.etcd import ETCD as E
+    from amdkube.store.etcd3 import Etcd3Store
+    from tests.test_raft import Cluster
+
+    def burn(name, ms, gpu=True):
+        c = {"name": "burn", "image": "amdkube/gpu-burn", "args": ["--ms", str(ms)]}
+        if gpu:
+            c["resources"] = {"limits": {"amd.com/gpu": "1"}}
+        else:
+            c = {"name": "plain", "image": "busybox", "command": ["sleep", str(ms // 1000)]}
+        return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "default"},
+                "spec": {"restartPolicy": "Never", "containers": [c]}}
+
+    async def go():
+        cl = Cluster(tmp_path)
+        for nm in cl.names:
+            cl.start(nm)
+        store = None
+        try:
+            leader = await asyncio.to_thread(cl.leader)
+            store = await asyncio.to_thread(Etcd3Store, list(cl.client.values()))
+            async with LocalCluster(gpus="amdsmi", n_gpus=1, relist_period=0.5, with_controllers=False,
+                                    api_kw={"store": store, "options": {"storage_media_type": pb.MEDIA_TYPE}}) as lc:
+                await lc.wait_gpus(1, 60)
+                c = lc.client
+                await c.create(burn("burner", 20000))
+                await c.create(burn("plain", 20000, gpu=False))
+                await wait_pod(c, "default", "burner", ("Running",), 60)
+                await wait_pod(c, "default", "plain", ("Running",), 60)
+                # the object as the store holds it: protobuf, replicated to every member
+                for nm in cl.names:
+                    with grpc.insecure_channel(cl.client[nm]) as ch:
+                        r = E.KV.stub(ch).Range(E.RangeRequest(key=b"/registry/pods/default/burner", serializable=True),
+                                                timeout=5)
+                    assert r.kvs and r.kvs[0].value[:4] == b"k8s\x00", nm
+                vadd = os.path.join(BIN, "rocm-vector-add")
+                out, err = bytearray(), bytearray()
+                rc = await exec_stream(c, "default", "burner", [vadd], on_stdout=out.extend, on_stderr=err.extend,
+                                       transport="spdy")
+                assert rc == 0 and b"Test PASSED" in out, (rc, bytes(out[-400:]), bytes(err[-400:]))
+                out, err = bytearray(), bytearray()
+                rc = await exec_stream(c, "default", "plain", [vadd], on_stdout=out.extend, on_stderr=err.extend,
+                                       transport="spdy")
+                assert rc != 0 and b"Test PASSED" not in out, (rc, bytes(out[-400:]))
+                p = await wait_pod(c, "default", "burner", ("Succeeded", "Failed"), 90)
+                assert p["status"]["phase"] == "Succeeded", p["status"]
+                # lose the store's leader: a new one is elected and the node keeps working
+                cl.kill(leader)
+                await asyncio.to_thread(cl.leader, [n for n in cl.names if n != leader])
+                await c.create(vadd_pod("after-failover"))
+                p = await wait_pod(c, "default", "after-failover", ("Succeeded", "Failed"), 120)
+                assert p["status"]["phase"] == "Succeeded", p["status"]
+                assert "Test PASSED" in await c.logs("default", "after-failover")
+        finally:
+            if store is not None:
+                store.close()
+            cl.stop()
+    run(go(), 400)
+
+
 def test_04_probe_binaries():
     r = subprocess.run([os.path.join(BIN, "hbm-probe"), "--mib", "1024", "--iters", "3"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
