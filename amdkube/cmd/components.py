@@ -530,7 +530,9 @@ def kubelet(argv):
     ap.add_argument("--address", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=10250)
     ap.add_argument("--runonce", action="store_true", help="run the static pods once, report, and exit (no API server)")
-    ap.add_argument("--cloud-provider", default="", help="'external': the cloud-controller-manager initialises the node")
+    ap.add_argument("--cloud-provider", default="", help="'external': the cloud-controller-manager initialises the node; "
+                                                          "openstack | baremetal: in-tree (addresses, providerID, zone)")
+    ap.add_argument("--cloud-config", default="", help="the in-tree provider's config (cloud.conf INI or YAML)")
     ap.add_argument("--volume-plugin-dir", default=None, help="FlexVolume driver directory")
     ap.add_argument("--enable-controller-attach-detach", default="true", choices=("true", "false"))
     ap.add_argument("--node-ip", default="127.0.0.1")
@@ -626,7 +628,7 @@ def kubelet(argv):
     # accepted for command-line compatibility; the settings they tune do not exist on this runtime
     for flag in ("--cadvisor-port", "--containerized", "--hairpin-mode", "--non-masquerade-cidr", "--iptables-masquerade-bit",
                  "--iptables-drop-bit", "--make-iptables-util-chains", "--kubelet-cgroups", "--system-cgroups",
-                 "--kube-reserved-cgroup", "--system-reserved-cgroup", "--experimental-qos-reserved", "--cloud-config",
+                 "--kube-reserved-cgroup", "--system-reserved-cgroup", "--experimental-qos-reserved",
                  "--streaming-connection-idle-timeout", "--master-service-namespace", "--require-kubeconfig",
                  "--init-config-dir", "--experimental-mounter-path",
                  "--experimental-check-node-capabilities-before-mount", "--experimental-kernel-memcg-notification",
@@ -683,7 +685,7 @@ def kubelet(argv):
                         image_gc_high_threshold=a.image_gc_high_threshold, image_gc_low_threshold=a.image_gc_low_threshold,
                         minimum_image_ttl_duration=a.minimum_image_ttl_duration,
                         config_file=a.config, dynamic_config_dir=a.dynamic_config_dir,
-                        cloud_provider=a.cloud_provider, volume_plugin_dir=a.volume_plugin_dir,
+                        cloud_provider=a.cloud_provider, cloud_config=a.cloud_config, volume_plugin_dir=a.volume_plugin_dir,
                         enable_controller_attach_detach=a.enable_controller_attach_detach == "true",
                         tls_cert_file=a.tls_cert_file, tls_private_key_file=a.tls_private_key_file,
                         client_ca_file=a.client_ca_file, anonymous_auth=a.anonymous_auth == "true",

@@ -146,6 +146,7 @@ class KubeletConfig:
     volume_reconcile_period: float = 2.0              # reconciler loop period (s)
     volume_remount_period: float = 60.0               # re-render secret/configMap/downwardAPI/projected content (s)
     cloud_provider: str = ""                          # --cloud-provider ("external": cloud-controller-manager initialises the node)
+    cloud_config: str = ""                            # --cloud-config (in-tree providers: openstack, baremetal)
     enable_server: bool = True                        # --enable-server (the authenticated API on --port)
     enable_debugging_handlers: bool = True            # --enable-debugging-handlers (logs, exec, attach, portForward, run, pprof)
     read_only_port: int = -1                          # --read-only-port (unauthenticated read-only API; -1/0: off; CLI default 10255)
@@ -207,6 +208,12 @@ class Kubelet:
         self.client = client
         self.cfg = config
         self.node_name = config.node_name
+        # an in-tree cloud provider (kubelet_node_status.go setNodeAddress / initialNode): the node's
+        # addresses, providerID, zone and instance type come from the cloud
+        self.cloud, self._cloud_addrs = None, None
+        if config.cloud_provider and config.cloud_provider != "external":
+            from ..cloudprovider import get_cloud_provider, load_config
+            self.cloud = get_cloud_provider(config.cloud_provider, load_config(config.cloud_config or None))
         self.gates = FeatureGate(config.feature_gates)
         self.metrics = new_registry()
         self._init_metrics()
@@ -494,6 +501,20 @@ class Kubelet:
             if self.cfg.node_ip:
                 ann["alpha.kubernetes.io/provided-node-ip"] = self.cfg.node_ip
         spec = {"taints": taints} if taints else {}
+        if self.cloud is not None and self.cloud.instances() is not None:
+            inst = self.cloud.instances()
+            if not self.cfg.provider_id:
+                self.cfg.provider_id = await inst.instance_id(self.node_name)
+            itype = await inst.instance_type(self.node_name)
+            if itype:
+                labels["beta.kubernetes.io/instance-type"] = itype
+            zone = await asyncio.to_thread(self.cloud.zone_for_node, self.node_name) if hasattr(self.cloud, "zone_for_node") \
+                else self.cloud.zones()
+            if zone is not None and zone.failure_domain:
+                labels["failure-domain.beta.kubernetes.io/zone"] = zone.failure_domain
+            if zone is not None and zone.region:
+                labels["failure-domain.beta.kubernetes.io/region"] = zone.region
+            await self.refresh_cloud_addresses()
         if not self.cfg.register_schedulable:
             spec["unschedulable"] = True
         if self.cfg.pod_cidr:
@@ -511,6 +532,25 @@ class Kubelet:
                 raise
             self.node = await self.client.get("nodes", self.node_name)
         await self.update_node_status()
+
+    async def refresh_cloud_addresses(self):
+        """The cloud's view of this node's addresses; with --node-ip that address must be one of
+        them and is listed first (kubelet_node_status.go setNodeAddress)."""
+        if self.cloud is None or self.cloud.instances() is None:
+            return
+        try:
+            addrs = await self.cloud.instances().node_addresses(self.node_name)
+        except Exception as e:
+            log.warning("cloud node addresses for %s: %r", self.node_name, e)
+            return
+        ip = self.cfg.node_ip
+        if ip and ip not in ("127.0.0.1", "0.0.0.0"):
+            hit = [a for a in addrs if a.get("address") == ip]
+            if not hit:
+                log.warning("--node-ip %s is not one of the cloud's addresses for %s", ip, self.node_name)
+                return
+            addrs = hit + [a for a in addrs if a.get("address") != ip]
+        self._cloud_addrs = addrs + [{"type": "Hostname", "address": self.node_name}]
 
     def _node_status_body(self, prev: dict) -> dict:
         cap = self._capacity()
@@ -554,6 +594,8 @@ class Kubelet:
             st["volumesInUse"] = in_use or None     # attachable volumes mounted or about to be (safe detach)
         if self.cfg.cloud_provider == "external":
             del st["addresses"]          # the cloud-controller-manager owns them
+        elif self._cloud_addrs:
+            st["addresses"] = list(self._cloud_addrs)
         st["_removed"] = removed
         if self.cfg.cgroup_root and "pods" in self.cfg.enforce_node_allocatable.split(",") and \
                 self._pods_cgroup_enforced != (alloc.get("cpu"), alloc.get("memory")):
@@ -600,6 +642,8 @@ class Kubelet:
             await wait_event(self._node_dirty, self.cfg.node_status_update_frequency)
             self._node_dirty.clear()
             try:
+                if self.cloud is not None:
+                    await self.refresh_cloud_addresses()
                 await self.update_node_status()
             except Exception as e:
                 log.warning("node status update failed: %r", e)

@@ -218,3 +218,28 @@ def test_controllers_drive_openstack(cloud):
                 await cm.stop()
                 await cmc.close()
     run(go(), 90)
+
+
+def test_kubelet_with_the_in_tree_openstack_provider(cloud, tmp_path):
+    """kubelet --cloud-provider=openstack --cloud-config cloud.conf: the node registers with
+    the server's providerID, the cloud's addresses (--node-ip first), instance type and zone."""
+    from tests.conftest import run
+    sid = cloud.add_server("mi355x-node-0", "10.0.0.21", floating_ip="203.0.113.77", az="az-gpu")
+    conf = tmp_path / "cloud.conf"
+    conf.write_text(f"[Global]\nauth-url = {cloud.url}/identity/v3\nusername = admin\npassword = secret\n"
+                    f"tenant-id = {cloud.project}\nregion = RegionOne\n")
+
+    async def go():
+        async with LocalCluster(gpus="fake", n_gpus=1, with_controllers=False, relist_period=0.2,
+                                kubelet_kw={"cloud_provider": "openstack", "cloud_config": str(conf),
+                                            "node_ip": "10.0.0.21"}) as lc:
+            n = await lc.client.get("nodes", lc.node_name)
+            assert n["spec"]["providerID"] == f"openstack:///{sid}"
+            lab = m.labels_of(n)
+            assert lab["beta.kubernetes.io/instance-type"] == "gpu.mi355x.8x"
+            assert lab["failure-domain.beta.kubernetes.io/zone"] == "az-gpu"
+            assert lab["failure-domain.beta.kubernetes.io/region"] == "RegionOne"
+            assert n["status"]["addresses"] == [{"type": "InternalIP", "address": "10.0.0.21"},
+                                                {"type": "ExternalIP", "address": "203.0.113.77"},
+                                                {"type": "Hostname", "address": "mi355x-node-0"}]
+    run(go(), 60)
