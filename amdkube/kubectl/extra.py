@@ -584,7 +584,8 @@ async def cmd_port_forward(c, a):
         if not running:
             raise SystemExit("error: no running pod found")
         name = m.name_of(running[0])
-    await api_port_forward(c, a.namespace or "default", name, rest)
+    from .main import stream_transport
+    await api_port_forward(c, a.namespace or "default", name, rest, transport=stream_transport())
 
 
 async def cmd_proxy(c, a):
@@ -613,6 +614,7 @@ async def cmd_proxy(c, a):
 async def cmd_cp(c, a):
     """Files move through exec streams (cat / sh -c 'cat > f'), as kubectl cp uses tar over exec."""
     from ..client.stream import exec_stream
+    from .main import stream_transport
     if len(a.args) != 2:
         raise SystemExit("error: cp SRC DST (one side as [NAMESPACE/]POD:PATH)")
     src, dst = a.args
@@ -622,7 +624,7 @@ async def cmd_cp(c, a):
         ns, _, pod = pod.rpartition("/")
         outb = bytearray()
         rc = await exec_stream(c, ns or a.namespace or "default", pod, ["cat", path], a.container,
-                               on_stdout=outb.extend, on_stderr=errb.extend)
+                               on_stdout=outb.extend, on_stderr=errb.extend, transport=stream_transport())
         if rc != 0:
             raise SystemExit(f"error: {errb.decode(errors='replace').strip()}")
         with open(dst, "wb") as f:
@@ -632,7 +634,7 @@ async def cmd_cp(c, a):
         ns, _, pod = pod.rpartition("/")
         data = open(src, "rb").read()
         rc = await exec_stream(c, ns or a.namespace or "default", pod, ["sh", "-c", 'cat > "$0"', path], a.container,
-                               stdin=data, on_stderr=errb.extend)
+                               stdin=data, on_stderr=errb.extend, transport=stream_transport())
         if rc != 0:
             raise SystemExit(f"error: {errb.decode(errors='replace').strip()}")
 

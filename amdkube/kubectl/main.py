@@ -263,20 +263,35 @@ async def _stdin_chunks():
         yield data
 
 
+def stream_transport() -> str:
+    """exec / attach / port-forward / cp speak SPDY/3.1 like a v1.9 kubectl;
+    AMDKUBE_STREAM_TRANSPORT=websocket selects the WebSocket channel protocol."""
+    return os.environ.get("AMDKUBE_STREAM_TRANSPORT", "spdy")
+
+
+def _term_size():
+    try:
+        sz = os.get_terminal_size(sys.stdout.fileno())
+        return sz.columns, sz.lines
+    except OSError:
+        return None
+
+
 async def cmd_exec(c, a):
-    """exec through the apiserver (pods/exec WebSocket), -i forwards stdin, -t asks for a tty."""
+    """exec through the apiserver (pods/exec, SPDY or WebSocket), -i forwards stdin, -t asks for a tty."""
     from ..client.stream import exec_stream
     out = lambda b: (sys.stdout.buffer.write(b), sys.stdout.buffer.flush())   # noqa: E731
     err = lambda b: (sys.stderr.buffer.write(b), sys.stderr.buffer.flush())   # noqa: E731
     return await exec_stream(c, a.namespace or "default", a.args[0].split("/", 1)[-1], a.command, a.container,
-                             stdin=_stdin_chunks() if a.stdin else None, tty=a.tty, on_stdout=out, on_stderr=err)
+                             stdin=_stdin_chunks() if a.stdin else None, tty=a.tty, on_stdout=out, on_stderr=err,
+                             transport=stream_transport(), resize=_term_size() if a.tty else None)
 
 
 async def cmd_attach(c, a):
     from ..client.stream import exec_stream
     out = lambda b: (sys.stdout.buffer.write(b), sys.stdout.buffer.flush())   # noqa: E731
     return await exec_stream(c, a.namespace or "default", a.args[0].split("/", 1)[-1], [], a.container, attach=True,
-                             on_stdout=out, on_stderr=out)
+                             on_stdout=out, on_stderr=out, transport=stream_transport())
 
 
 async def _meta_edit(c, a, field):
