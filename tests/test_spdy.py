@@ -6,6 +6,7 @@ drives the same path a v1.9 kubectl does: apiserver → kubelet → runtime stre
 relays splicing raw bytes."""
 import asyncio
 import json
+import os
 import socket
 import struct
 import zlib
@@ -122,6 +123,18 @@ async def test_spdy_exec_attach_port_forward_through_apiserver():
         out = bytearray()
         rc = await exec_stream(c, "default", "ticker", [], attach=True, on_stdout=out.extend, transport="spdy")
         assert rc == 4 and b"tick1\ntick2\ntick3\n" in bytes(out)
+
+        # kubectl cp (upload through stdin, download through stdout) rides SPDY by default
+        import tempfile
+        from amdkube.kubectl.main import main as kubectl
+        d = tempfile.mkdtemp(prefix="spdycp", dir="/tmp")
+        src, back = os.path.join(d, "src.bin"), os.path.join(d, "back.bin")
+        with open(src, "wb") as f:
+            f.write(os.urandom(300_000))
+        args = ["--server", c.server, "--token", c.headers["Authorization"].split(" ", 1)[1]]
+        assert await asyncio.to_thread(kubectl, args + ["cp", src, f"default/sh:{d}/in-pod.bin"]) in (0, None)
+        assert await asyncio.to_thread(kubectl, args + ["cp", f"default/sh:{d}/in-pod.bin", back]) in (0, None)
+        assert open(back, "rb").read() == open(src, "rb").read()
 
         # older protocol versions: v2 reports the exit as error-stream text
         url = (f"{c.server}/api/v1/namespaces/default/pods/sh/exec?command=sh&command=-c&command=exit+5"
