@@ -6,7 +6,8 @@
                                     # and the ThreadSanitizer build of the activity sampler
 
 Outputs: amdkube/_native/{_amdsmi,_topo,_hipops}.<ext> and amdkube/_native/bin/{pause,
-rocm-vector-add,hbm-probe,gpu-burn,xgmi-probe[,topo-selftest-asan,pause-asan,sampler-selftest-{asan,tsan}]}.
+rocm-vector-add,hbm-probe,gpu-burn,xgmi-probe[,topo-selftest-asan,pause-asan,amdkube-nsexec-asan,
+seccomp-check-asan,sampler-selftest-{asan,tsan}]}.
 Targets are rebuilt only when a source/header is newer than the output.
 """
 from __future__ import annotations
@@ -70,6 +71,13 @@ def targets(sanitize=False, cpu_only=False):
              ["g++", "-O1", "-std=c++17", *san, n("native/pause.cpp"), "-o", "{out}"]),
             (n(BIN, "sampler-selftest-asan"), [n("native/sampler_selftest.cpp"), n("native/sampler_core.h")],
              ["g++", "-O1", "-std=c++17", *san, n("native/sampler_selftest.cpp"), "-pthread", "-o", "{out}"]),
+            # the container launcher and the seccomp compiler: host code that parses untrusted input
+            # (profiles, mountinfo, flags) and changes privileges
+            (n(BIN, "amdkube-nsexec-asan"), [n("native/nsexec.cpp"), n("native/seccomp_bpf.h"), n("native/devguard.h"),
+                                             SYSCALL_TABLE],
+             ["g++", "-O1", "-std=c++17", *san, n("native/nsexec.cpp"), "-o", "{out}"]),
+            (n(BIN, "seccomp-check-asan"), [n("native/seccomp_check.cpp"), n("native/seccomp_bpf.h"), SYSCALL_TABLE],
+             ["g++", "-O1", "-std=c++17", *san, n("native/seccomp_check.cpp"), "-o", "{out}"]),
             (n(BIN, "sampler-selftest-tsan"), [n("native/sampler_selftest.cpp"), n("native/sampler_core.h")],
              ["g++", "-O1", "-std=c++17", "-fsanitize=thread", "-fno-omit-frame-pointer", "-g",
               n("native/sampler_selftest.cpp"), "-pthread", "-o", "{out}"]),

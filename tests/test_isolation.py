@@ -212,3 +212,28 @@ def test_exec_runs_inside_the_container_guard(fake_dev):
             await shim.stop(kill_pods=True)
             subprocess.run(["rm", "-rf", base])
     run(go())
+
+
+@needs_landlock
+def test_nsexec_under_asan_ubsan(fake_dev):
+    """The launcher built with AddressSanitizer + UBSan (host code only) enforces the same view
+    and reports no memory or undefined-behaviour error on the guard, mknod and seccomp paths."""
+    asan = os.path.join(os.path.dirname(NSEXEC), "amdkube-nsexec-asan")
+    if not os.path.exists(asan):
+        pytest.skip("sanitizer build absent (python native/build.py --sanitize)")
+    keep = f"{fake_dev}/dri/renderD130"
+    prof = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "amdkube", "runtime", "seccomp_default.json")
+    p = subprocess.run([asan, "--no-namespaces", "--landlock", "--dev-root", fake_dev, "--keep", keep, "--seccomp", prof,
+                        "--caps", "default", "--", sys.executable, "-c", OPEN_ALL, fake_dev],
+                       capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS="halt_on_error=1"))
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "AddressSanitizer" not in p.stderr and "runtime error" not in p.stderr, p.stderr[-2000:]
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert [k for k, v in r.items() if v == "ok"] == ["renderD130", "kfd"]
+    # a malformed profile is refused cleanly (parser under ASan)
+    bad = os.path.join(fake_dev, "..", "bad.json")
+    with open(bad, "w") as f:
+        f.write('{"defaultAction": "SCMP_ACT_ERRNO", "syscalls": [{"names": ["read"], "action": 7}]')
+    p = subprocess.run([asan, "--no-namespaces", "--seccomp", bad, "--", "true"], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 126 and "AddressSanitizer" not in p.stderr, p.stderr[-2000:]

@@ -114,3 +114,22 @@ async def test_pod_with_seccomp_annotations(tmp_path):
             await wait_pod(c, "default", name, ("Succeeded", "Failed"), 20)
             out[name] = (await c.logs("default", name)).strip()
         assert out["confined"].endswith("denied") and out["free"].endswith("made") and out["default"].endswith("denied"), out
+
+
+def test_seccomp_compiler_under_asan_matches(tmp_path):
+    """The profile compiler + BPF evaluator built with ASan/UBSan gives the same verdicts as the
+    production build over the default profile (host code under sanitizers)."""
+    asan = CHECK + "-asan"
+    if not os.path.exists(asan):
+        pytest.skip("sanitizer build absent (python native/build.py --sanitize)")
+    prof = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "amdkube", "runtime",
+                        "seccomp_default.json")
+    for call, args in (("read", ()), ("ioctl", (3, 0xC0184B01)), ("mount", ()), ("personality", (0,)),
+                       ("personality", (0xFFFFFFFF,)), ("clone", (0x10000000,)), ("kexec_load", ())):
+        outs = []
+        for binary in (CHECK, asan):
+            r = subprocess.run([binary, prof, call] + [str(a) for a in args], capture_output=True, text=True,
+                               env=dict(os.environ, ASAN_OPTIONS="abort_on_error=1", UBSAN_OPTIONS="halt_on_error=1"))
+            assert r.returncode == 0 and "runtime error" not in r.stderr, r.stderr
+            outs.append(r.stdout.strip())
+        assert outs[0] == outs[1], (call, outs)
