@@ -170,18 +170,27 @@ __global__ __launch_bounds__(256) void hbm_read_kernel(const v4u* __restrict__ b
   if (acc == 0x9e3779b9u) sink[0] = acc;  // keeps the loads live
 }
 
+// Copy: each workgroup owns one contiguous chunk and walks it in 8 x 256-lane tiles (8 x 16 B
+// in flight per lane), so every XCD streams long runs of consecutive DRAM pages instead of the
+// grid-stride interleave; 64 workgroups/CU. Round-3 sweep on MI355X (hack/exp/copy_sweep.hip,
+// 2 x 4 GiB): grid-stride 32/CU 5.01 TB/s, grid-stride 64/CU 5.20, chunked 64/CU 5.53,
+// hipMemcpyDtoD 4.70.
+constexpr int HBM_COPY_BLOCKS_PER_CU = 64;
+
 __global__ __launch_bounds__(256) void hbm_copy_kernel(const v4u* __restrict__ src, v4u* __restrict__ dst,
                                                        size_t n16) {
-  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
-  size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  for (; i + (HBM_UNROLL - 1) * stride < n16; i += HBM_UNROLL * stride) {
+  const size_t per = (n16 + gridDim.x - 1) / gridDim.x;
+  const size_t lo = static_cast<size_t>(blockIdx.x) * per;
+  const size_t hi = lo + per < n16 ? lo + per : n16;
+  size_t i = lo + threadIdx.x;
+  for (; i + (HBM_UNROLL - 1) * blockDim.x < hi; i += static_cast<size_t>(HBM_UNROLL) * blockDim.x) {
     v4u v[HBM_UNROLL];
 #pragma unroll
-    for (int u = 0; u < HBM_UNROLL; ++u) v[u] = ld_nt(src + i + u * stride);
+    for (int u = 0; u < HBM_UNROLL; ++u) v[u] = ld_nt(src + i + u * blockDim.x);
 #pragma unroll
-    for (int u = 0; u < HBM_UNROLL; ++u) st_nt(dst + i + u * stride, v[u]);
+    for (int u = 0; u < HBM_UNROLL; ++u) st_nt(dst + i + u * blockDim.x, v[u]);
   }
-  for (; i < n16; i += stride) st_nt(dst + i, ld_nt(src + i));
+  for (; i < hi; i += blockDim.x) st_nt(dst + i, ld_nt(src + i));
 }
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -358,7 +367,7 @@ inline std::vector<uint32_t> hbm_copy_host(const std::vector<uint32_t>& words, i
   const size_t n16 = words.size() / 4;
   DevBuf s(n16 * 16), d(n16 * 16);
   AK_HIP(hipMemcpy(s.p, words.data(), n16 * 16, hipMemcpyHostToDevice));
-  const int grid = stream_grid(n16, dev_info(dev).cu_count, HBM_BLOCKS_PER_CU);
+  const int grid = stream_grid(n16, dev_info(dev).cu_count, HBM_COPY_BLOCKS_PER_CU);
   hipLaunchKernelGGL(hbm_copy_kernel, dim3(grid), dim3(256), 0, 0, static_cast<const v4u*>(s.p), static_cast<v4u*>(d.p),
                      n16);
   AK_HIP(hipGetLastError());
@@ -428,7 +437,8 @@ inline HbmResult run_hbm_probe(size_t bytes, int iters, int dev, uint32_t seed =
   };
   double w = timed([&] { hipLaunchKernelGGL(hbm_write_kernel, dim3(grid), dim3(256), 0, 0, a, n16, seed); });
   double rd = timed([&] { hipLaunchKernelGGL(hbm_read_kernel, dim3(grid), dim3(256), 0, 0, a, n16, sink); });
-  double cp = timed([&] { hipLaunchKernelGGL(hbm_copy_kernel, dim3(grid), dim3(256), 0, 0, a, b, n16); });
+  const int copy_grid = stream_grid(n16, info.cu_count, HBM_COPY_BLOCKS_PER_CU);
+  double cp = timed([&] { hipLaunchKernelGGL(hbm_copy_kernel, dim3(copy_grid), dim3(256), 0, 0, a, b, n16); });
   AK_HIP(hipMemset(errs, 0, sizeof(unsigned long long)));
   AK_HIP(hipEventRecord(e0));
   hipLaunchKernelGGL(hbm_verify_kernel, dim3(grid), dim3(256), 0, 0, b, n16, seed, errs);
