@@ -277,7 +277,13 @@ class Etcd3Store(MVCCStore):
                     log.warning("etcd3: %s committed at %d, rendered for %d; rewriting", key, rev, guess)
                     self.drain(until=rev)
                     return self._write(key, value, rev, False)
-                self.drain(until=rev)
+                if rev == guess and self.rev == guess - 1:
+                    # nothing else committed in between (the revision moved by exactly this Txn), so
+                    # the replica is exact at rev-1 and this write can be applied now; the watch's
+                    # copy of the same events is skipped when it arrives
+                    self._apply_own(key, data, rev, delete)
+                else:
+                    self.drain(until=rev)
                 return resp, rev, data
             frr, orr = resp.responses[0].response_range, resp.responses[1].response_range
             cur_mod = orr.kvs[0].mod_revision if orr.kvs else 0
@@ -296,6 +302,18 @@ class Etcd3Store(MVCCStore):
                 raise CASFailed(cur)
             self.drain(until=frr.kvs[0].mod_revision if frr.kvs else 0)     # only the fence moved
         raise ConnectionError(f"etcd3: {key}: the revision fence kept moving")
+
+    def _apply_own(self, key: str, data, rev: int, delete: bool):
+        fence = self.kv.get(FENCE)
+        self._apply(E.Event(type=EV_PUT, kv=E.KeyValue(key=_FENCE_B, create_revision=fence.create_rev if fence else rev,
+                                                        mod_revision=rev, version=(fence.version + 1) if fence else 1)))
+        cur = self.kv.get(key)
+        if delete:
+            self._apply(E.Event(type=1, kv=E.KeyValue(key=_b(key), mod_revision=rev)))
+        else:
+            self._apply(E.Event(type=EV_PUT, kv=E.KeyValue(key=_b(key), value=self._sealed(key, data),
+                                                           create_revision=cur.create_rev if cur else rev, mod_revision=rev,
+                                                           version=(cur.version + 1) if cur else 1)))
 
     def put(self, key: str, value, expect_mod_rev: int | None = None) -> KV:
         _, rev, data = self._write(key, value, expect_mod_rev, False)
