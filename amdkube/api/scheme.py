@@ -34,6 +34,7 @@ class ResourceInfo:
     # (extensions/v1beta1 deployments → apps deployments); None for a storage version
     storage: tuple | None = None
     to_storage: Callable | None = field(default=None, repr=False)     # request body → canonical (version defaults)
+    from_storage: Callable | None = field(default=None, repr=False)   # stored object → this version's shape
 
     @property
     def api_version(self) -> str:
@@ -63,12 +64,13 @@ class Scheme:
         for n in (ri.plural, ri.kind.lower(), *ri.short_names, ri.group_resource):
             self.by_name.setdefault(n, ri)
 
-    def add_alias(self, group: str, version: str, of: tuple, kind: str | None = None, to_storage=None) -> ResourceInfo:
+    def add_alias(self, group: str, version: str, of: tuple, kind: str | None = None, to_storage=None,
+                  from_storage=None) -> ResourceInfo:
         """Serve an existing resource under another group/version (the apiserver's multi-version
         serving: same storage, objects rewritten to the requested apiVersion on the way out)."""
         canon = self.by_plural[of]
         ri = ResourceInfo(group, version, kind or canon.kind, canon.plural, canon.namespaced, canon.short_names,
-                          canon.subresources, storage=of, to_storage=to_storage)
+                          canon.subresources, storage=of, to_storage=to_storage, from_storage=from_storage)
         self.add(ri)
         return ri
 
@@ -225,7 +227,6 @@ for _g, _v, _of, _conv in (
         ("apps", "v1beta2", ("apps", "replicasets"), None), ("apps", "v1beta2", ("apps", "statefulsets"), None),
         ("apps", "v1beta2", ("apps", "controllerrevisions"), None),
         ("batch", "v2alpha1", ("batch", "cronjobs"), None),
-        ("autoscaling", "v2beta1", ("autoscaling", "horizontalpodautoscalers"), None),
         ("rbac.authorization.k8s.io", "v1beta1", ("rbac.authorization.k8s.io", "roles"), None),
         ("rbac.authorization.k8s.io", "v1beta1", ("rbac.authorization.k8s.io", "clusterroles"), None),
         ("rbac.authorization.k8s.io", "v1beta1", ("rbac.authorization.k8s.io", "rolebindings"), None),
@@ -241,6 +242,11 @@ for _g, _v, _of, _conv in (
         ("authorization.k8s.io", "v1beta1", ("authorization.k8s.io", "localsubjectaccessreviews"), None),
         ("authentication.k8s.io", "v1beta1", ("authentication.k8s.io", "tokenreviews"), None)):
     SCHEME.add_alias(_g, _v, _of, to_storage=_conv)
+
+# autoscaling/v2beta1 HPAs: multiple metrics, kept in annotations on the v1 storage object
+from . import autoscaling as _as   # noqa: E402
+SCHEME.add_alias("autoscaling", "v2beta1", ("autoscaling", "horizontalpodautoscalers"),
+                 to_storage=_as.v2_to_v1, from_storage=_as.v1_to_v2)
 
 
 def _version_sort(vs):

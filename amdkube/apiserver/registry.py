@@ -296,12 +296,33 @@ class ResourceStore:
             new["spec"] = m.deepcopy(cur.get("spec"))
             keep = m.deepcopy(cmd)
             keep["resourceVersion"] = md.get("resourceVersion", cmd.get("resourceVersion"))
+            if self.ri.plural == "horizontalpodautoscalers":
+                # v2beta1 status (current metrics, conditions) lives in annotations of the v1 object
+                from ..api.autoscaling import METRICS_ANNOTATION, STATUS_ANNOTATIONS
+                na, ka = md.get("annotations") or {}, dict(keep.get("annotations") or {})
+                for k in STATUS_ANNOTATIONS:
+                    if k in na:
+                        ka[k] = na[k]
+                    else:
+                        ka.pop(k, None)
+                if METRICS_ANNOTATION in (cmd.get("annotations") or {}):
+                    ka[METRICS_ANNOTATION] = cmd["annotations"][METRICS_ANNOTATION]
+                keep["annotations"] = ka or None
             new["metadata"] = keep
         elif self.has_status:
             if "status" in cur:
                 new["status"] = m.deepcopy(cur["status"])
             else:
                 new.pop("status", None)
+            if self.ri.plural == "horizontalpodautoscalers":   # status annotations change only via status
+                from ..api.autoscaling import STATUS_ANNOTATIONS
+                ca, na = cmd.get("annotations") or {}, dict(md.get("annotations") or {})
+                for k in STATUS_ANNOTATIONS:
+                    if k in ca:
+                        na[k] = ca[k]
+                    else:
+                        na.pop(k, None)
+                md["annotations"] = na or None
         if self.generation:
             md["generation"] = cmd.get("generation", 1) + (1 if new.get("spec") != cur.get("spec") else 0)
         if self.ri.plural == "services" and subresource != "status":
@@ -319,7 +340,8 @@ class ResourceStore:
                 else:
                     r.pop("assigned", None)
 
-    def update(self, ns, name, obj, subresource="", user=None, patch=None, content_type="", create_on_update=False):
+    def update(self, ns, name, obj, subresource="", user=None, patch=None, content_type="", create_on_update=False,
+               served=None):
         """PUT (obj) or PATCH (patch bytes). Returns (obj, created)."""
         key = self.key(ns, name)
         precond_rv = None if patch is not None else ((obj.get("metadata") or {}).get("resourceVersion") or None)
@@ -332,7 +354,14 @@ class ResourceStore:
                     created[0] = True
                     return None
                 raise m.not_found(self.ri.plural, name)
-            if patch is not None:
+            if patch is not None and served is not None and served.from_storage is not None:
+                # a patch written against a served version with its own shape (autoscaling/v2beta1):
+                # apply it to that view of the object, then convert back
+                view = m.deepcopy(cur)
+                view["apiVersion"], view["kind"] = served.api_version, served.kind
+                served.from_storage(view)
+                new = SCHEME.to_storage(apply_patch(view, patch, content_type))
+            elif patch is not None:
                 new = apply_patch(cur, patch, content_type)
             else:
                 new = SCHEME.to_storage(m.deepcopy(obj))

@@ -67,6 +67,8 @@ def _convert_out(obj, storage_ri, served):
     if isinstance(obj, dict):
         if obj.get("apiVersion") == storage_ri.api_version and obj.get("kind") == storage_ri.kind:
             obj["apiVersion"], obj["kind"] = served.api_version, served.kind
+            if served.from_storage is not None:
+                served.from_storage(obj)
         elif obj.get("kind") == storage_ri.list_kind:
             obj["apiVersion"], obj["kind"] = served.api_version, served.list_kind
             for it in obj.get("items") or []:
@@ -654,7 +656,7 @@ class APIServer:
                 if sem.locked():
                     raise m.too_many_requests()
                 await sem.acquire()
-            resp = await self._handle(request, rs, ns, name, sub, user, q, as_stored=conv is None)
+            resp = await self._handle(request, rs, ns, name, sub, user, q, as_stored=conv is None, served=conv)
             if conv is not None and resp.body:
                 resp = _resp(_convert_out(json.loads(resp.body), rs.ri, conv), resp.status)
             code = resp.status
@@ -717,7 +719,7 @@ class APIServer:
                 out.headers[k] = v
         return out
 
-    async def _handle(self, request, rs, ns, name, sub, user, q, as_stored=False):
+    async def _handle(self, request, rs, ns, name, sub, user, q, as_stored=False, served=None):
         meth = request.method
         ri = rs.ri
         if ri.namespaced is False:
@@ -829,7 +831,7 @@ class APIServer:
                 obj, _ = rs.update(ns, name, new, subresource=sub if sub == "status" else "", user=user)
                 return _resp(obj)
             obj, _ = rs.update(ns, name, None, subresource=sub if sub == "status" else "", user=user, patch=data,
-                               content_type=ct)
+                               content_type=ct, served=served)
             return _resp(obj)
         if meth == "DELETE":
             opts = {}

@@ -835,8 +835,9 @@ def exporter(argv):
 
 
 def metrics_server(argv):
-    """Resource metrics API (metrics.k8s.io) behind the aggregator: register it with an
-    APIService pointing at a Service whose endpoints reach --secure-port."""
+    """Resource metrics API (metrics.k8s.io) and the custom metrics API (custom.metrics.k8s.io:
+    gpu_utilization / gpu_memory_used_bytes / gpu_count per pod and node) behind the aggregator:
+    register an APIService per group pointing at a Service whose endpoints reach --secure-port."""
     ap = argparse.ArgumentParser("amdkube metrics-server")
     ap.add_argument("--master", "--server", dest="server", default="http://127.0.0.1:8080")
     ap.add_argument("--kubeconfig", default=None)

@@ -9,23 +9,33 @@ and to the scale-up limit max(2 × current, 4); a scale-up needs 3 min and a sca
 since the last rescale (--horizontal-pod-autoscaler-{upscale,downscale}-delay); status
 carries currentReplicas / desiredReplicas / currentCPUUtilizationPercentage / lastScaleTime.
 
-MI355X extension: the annotation `autoscaling.amd.com/target-gpu-utilization: "<pct>"` adds
-a second metric, the mean MI355X activity (amd-smi duty cycle, exported per container by
-the kubelet's accelerator stats) of the pods' assigned GPUs. The larger of the two
-proposals wins (the multi-metric rule of autoscaling/v2).
+autoscaling/v2beta1 (horizontal.go computeReplicasForMetrics, 1.9): spec.metrics may list
+Resource (cpu/memory, targetAverageUtilization or targetAverageValue), Pods (a per-pod custom
+metric averaged over the target's pods, targetAverageValue) and Object (one custom metric of
+another object, targetValue) sources; each proposes a replica count and the largest wins. The
+v1 storage object carries the extra metrics, currentMetrics and the AbleToScale /
+ScalingActive / ScalingLimited conditions in annotations (api/autoscaling.py); the controller
+writes status through the v2beta1 status subresource.
 
-Metrics come from the resource metrics API (metrics.k8s.io, the metrics-server) when it is
-registered, else straight from the kubelets' /stats/summary, where CPU usage is the rate between
-two successive cumulative samples.
+MI355X extensions: the custom metrics API of `amdkube metrics-server` serves gpu_utilization /
+gpu_memory_used_bytes / gpu_count per pod, so a Pods metric on gpu_utilization scales on MI355X
+activity. The older annotation `autoscaling.amd.com/target-gpu-utilization: "<pct>"` adds the
+same signal read from the resource metrics source, without the custom metrics API.
+
+Resource metrics come from the resource metrics API (metrics.k8s.io, the metrics-server) when it
+is registered, else straight from the kubelets' /stats/summary, where CPU usage is the rate
+between two successive cumulative samples.
 """
 from __future__ import annotations
 
 import asyncio
+import json
 import math
 import time
 
 import aiohttp
 
+from ..api import autoscaling as api_autoscaling
 from ..api import meta as m
 from ..api.helpers import is_pod_terminal
 from ..api.labels import selector_from_label_selector, selector_from_set
@@ -67,7 +77,7 @@ class KubeletSummaryMetrics:
                 ref = p.get("podRef") or {}
                 if ref.get("namespace") != ns:
                     continue
-                cpu_milli, gpu, ngpu = 0.0, 0.0, 0
+                cpu_milli, gpu, ngpu, mem = 0.0, 0.0, 0, 0
                 have_cpu = True
                 for c in p.get("containers") or []:
                     key = (ref.get("uid"), c.get("name"))
@@ -78,6 +88,7 @@ class KubeletSummaryMetrics:
                         have_cpu = False
                     else:
                         cpu_milli += max(0, cur - prev[1]) / (now - prev[0]) / 1e6
+                    mem += int(((c.get("memory") or {}).get("workingSetBytes")) or 0)
                     for a in c.get("accelerators") or []:
                         gpu += float(a.get("dutyCycle", 0))
                         ngpu += 1
@@ -86,6 +97,8 @@ class KubeletSummaryMetrics:
                     ent["cpu_milli"] = cpu_milli
                 if ngpu:
                     ent["gpu_util"] = gpu / ngpu
+                if mem:
+                    ent["memory_bytes"] = mem
                 out[ref.get("name")] = ent
         return out
 
@@ -121,8 +134,10 @@ class ResourceMetricsAPI:
             return await self.fallback.pod_metrics(ns)
         out = {}
         for pm in items:
-            ent = {"cpu_milli": float(sum(Quantity(ct["usage"]["cpu"]).as_fraction() * 1000
-                                          for ct in pm.get("containers") or []))}
+            cts = pm.get("containers") or []
+            ent = {"cpu_milli": float(sum(Quantity(ct["usage"]["cpu"]).as_fraction() * 1000 for ct in cts))}
+            if any("memory" in ct.get("usage", {}) for ct in cts):
+                ent["memory_bytes"] = int(sum(Quantity(ct["usage"].get("memory", "0")).value() for ct in cts))
             duty = ((pm.get("metadata") or {}).get("annotations") or {}).get("amd.com/gpu-duty-cycle")
             if duty is not None:
                 ent["gpu_util"] = float(duty)
@@ -133,34 +148,96 @@ class ResourceMetricsAPI:
         await self.fallback.close()
 
 
-def _cpu_request_milli(pod) -> int:
+class CustomMetricsAPI:
+    """metrics/rest_metrics_client.go customMetricsClient: Pods and Object metrics from the custom
+    metrics API (custom.metrics.k8s.io/v1beta1, behind the aggregator; `amdkube metrics-server`
+    serves gpu_utilization / gpu_memory_used_bytes / gpu_count)."""
+
+    def __init__(self, client):
+        self.client = client
+
+    async def pod_metric(self, ns: str, metric: str, selector: str) -> dict[str, float]:
+        d = await self.client.request("GET", f"/apis/{CMG}/namespaces/{ns}/pods/*/{metric}",
+                                      params={"labelSelector": selector} if selector else None)
+        return {(it.get("describedObject") or {}).get("name"): _num(it.get("value"))
+                for it in (d or {}).get("items") or []}
+
+    async def object_metric(self, ns: str, target: dict, metric: str) -> float:
+        plural = OBJECT_PLURALS.get(target.get("kind"), (target.get("kind") or "").lower() + "s")
+        d = await self.client.request("GET", f"/apis/{CMG}/namespaces/{ns}/{plural}/{target.get('name')}/{metric}")
+        items = (d or {}).get("items") or []
+        if not items:
+            raise LookupError(f"no value for {metric} of {target.get('kind')}/{target.get('name')}")
+        return _num(items[0].get("value"))
+
+
+CMG = "custom.metrics.k8s.io/v1beta1"
+OBJECT_PLURALS = {"Pod": "pods", "Service": "services", "Deployment": "deployments", "Node": "nodes",
+                  "Ingress": "ingresses", "ReplicaSet": "replicasets", "StatefulSet": "statefulsets"}
+
+
+def _num(q) -> float:
+    return float(Quantity(str(q)).as_fraction()) if q is not None else 0.0
+
+
+def _fmt(v: float) -> str:
+    """A float as the canonical quantity string the reference writes (milli-units below 1000 × int)."""
+    mv = int(round(v * 1000))
+    return str(mv // 1000) if mv % 1000 == 0 else f"{mv}m"
+
+
+def _request(pod, resource) -> int:
+    """Σ container requests of one resource (millicores for cpu, bytes otherwise); 0 when any
+    container has none — the reference then treats utilization as undefined for the pod."""
     total = 0
     for c in (pod.get("spec") or {}).get("containers") or []:
-        v = ((c.get("resources") or {}).get("requests") or {}).get("cpu")
+        v = ((c.get("resources") or {}).get("requests") or {}).get(resource)
         if v is None:
-            return 0  # reference: a pod missing a CPU request makes CPU utilization undefined
-        total += Quantity(v).milli_value()
+            return 0
+        total += Quantity(v).milli_value() if resource == "cpu" else Quantity(v).value()
     return total
 
 
-def cpu_proposal(pods, metrics, target_pct, current) -> tuple[int | None, int | None]:
-    usage = req = 0
+_USAGE_KEY = {"cpu": "cpu_milli", "memory": "memory_bytes"}
+
+
+def _cpu_request_milli(pod) -> int:
+    return _request(pod, "cpu")
+
+
+def _ratio_replicas(ratio: float, n: int, current: int) -> int:
+    return current if abs(ratio - 1.0) <= TOLERANCE else int(math.ceil(ratio * n))
+
+
+def resource_proposal(pods, metrics, resource, current, target_util=None, target_avg=None):
+    """replica_calculator.go GetResourceReplicas / GetRawResourceReplicas. Returns
+    (replicas, utilization %, average usage in the resource's base unit) or (None, None, None)."""
+    key = _USAGE_KEY.get(resource)
+    usage = req = 0.0
     n = 0
     for p in pods:
         mt = metrics.get(m.name_of(p)) or {}
-        r = _cpu_request_milli(p)
-        if "cpu_milli" not in mt or r <= 0:
+        if key is None or key not in mt:
             continue
-        usage += mt["cpu_milli"]
+        r = _request(p, resource)
+        if target_util is not None and r <= 0:
+            continue
+        usage += mt[key]
         req += r
         n += 1
-    if n == 0 or req == 0:
-        return None, None
-    util = int(round(usage * 100.0 / req))
-    ratio = util / float(target_pct)
-    if abs(ratio - 1.0) <= TOLERANCE:
-        return current, util
-    return int(math.ceil(ratio * n)), util
+    if n == 0 or (target_util is not None and req == 0):
+        return None, None, None
+    scale = 1000.0 if resource == "cpu" else 1.0        # cpu usage is in millicores
+    avg = usage / n / scale
+    if target_util is not None:
+        util = int(round(usage * 100.0 / req))
+        return _ratio_replicas(util / float(target_util), n, current), util, avg
+    return _ratio_replicas(avg / float(target_avg), n, current), None, avg
+
+
+def cpu_proposal(pods, metrics, target_pct, current) -> tuple[int | None, int | None]:
+    r, util, _ = resource_proposal(pods, metrics, "cpu", current, target_util=target_pct)
+    return r, util
 
 
 def gpu_proposal(pods, metrics, target_pct, current) -> tuple[int | None, float | None]:
@@ -169,13 +246,26 @@ def gpu_proposal(pods, metrics, target_pct, current) -> tuple[int | None, float 
     if not vals:
         return None, None
     util = sum(vals) / len(vals)
-    ratio = util / float(target_pct)
-    if abs(ratio - 1.0) <= TOLERANCE:
-        return current, util
-    return int(math.ceil(ratio * len(vals))), util
+    return _ratio_replicas(util / float(target_pct), len(vals), current), util
+
+
+def _set_condition(conds: list, typ: str, status: str, reason: str, message: str, now: str):
+    """horizontal.go setCondition: lastTransitionTime moves only when the status flips."""
+    for c in conds:
+        if c.get("type") == typ:
+            if c.get("status") != status:
+                c["lastTransitionTime"] = now
+            c.update(status=status, reason=reason, message=message)
+            return
+    conds.append({"type": typ, "status": status, "lastTransitionTime": now, "reason": reason, "message": message})
 
 
 class HorizontalPodAutoscalerController(Controller):
+    """horizontal.go reconcileAutoscaler over the autoscaling/v2beta1 metric list (read from the
+    stored v1 object's annotations, api/autoscaling.py): every metric proposes a replica count,
+    the largest wins (computeReplicasForMetrics); status gets currentMetrics and the
+    AbleToScale / ScalingActive / ScalingLimited conditions, written through the v2beta1
+    status subresource so the apiserver folds them back into the v1 annotations."""
     name = "horizontalpodautoscaling"
     workers = 1
 
@@ -183,6 +273,7 @@ class HorizontalPodAutoscalerController(Controller):
                  downscale_delay: float = 300.0, clock=time.time):
         super().__init__(mgr)
         self.metrics = metrics or ResourceMetricsAPI(mgr.client)
+        self.custom = self.metrics if hasattr(self.metrics, "pod_metric") else CustomMetricsAPI(mgr.client)
         self.sync_period, self.upscale_delay, self.downscale_delay = sync_period, upscale_delay, downscale_delay
         self.clock = clock
         self._poll = None
@@ -209,63 +300,179 @@ class HorizontalPodAutoscalerController(Controller):
             for h in self.hpa_inf.list():
                 self.enqueue(h)
 
+    def _event(self, hpa, typ, reason, msg):
+        rec = getattr(self.mgr, "recorder", None)
+        if rec is not None:
+            rec.event(hpa, typ, reason, msg)
+
+    async def _metric_proposals(self, hpa, ns, pods, selector_str, current):
+        """computeReplicasForMetrics: [(replicas, metric name, status entry)] plus the first
+        failure (reason, message) if any metric could not be read."""
+        specs = api_autoscaling.metrics_of(hpa)
+        ann = m.annotations_of(hpa)
+        explicit_cpu = (hpa.get("spec") or {}).get("targetCPUUtilizationPercentage") is not None
+        if GPU_TARGET_ANNOTATION in ann and not explicit_cpu and api_autoscaling.METRICS_ANNOTATION not in ann:
+            specs = []      # the GPU annotation alone replaces the defaulted 80 % CPU target
+        out, failure, resource_metrics = [], None, None
+        for ms in specs:
+            typ = ms.get("type")
+            try:
+                if typ == "Resource":
+                    if resource_metrics is None:
+                        resource_metrics = await self.metrics.pod_metrics(ns)
+                    r = ms.get("resource") or {}
+                    tu, tv = r.get("targetAverageUtilization"), r.get("targetAverageValue")
+                    rep, util, avg = resource_proposal(pods, resource_metrics, r.get("name"), current,
+                                                       target_util=tu, target_avg=_num(tv) if tu is None and tv else None)
+                    if rep is None:
+                        raise LookupError(f"did not receive metrics for any ready pods ({r.get('name')})")
+                    cur = {"name": r.get("name"), "currentAverageValue": _fmt(avg)}
+                    if util is not None:
+                        cur["currentAverageUtilization"] = util
+                    out.append((rep, f"{r.get('name')} resource" + (" utilization (percentage of request)" if util is not None else ""),
+                                {"type": "Resource", "resource": cur}))
+                elif typ == "Pods":
+                    pm = ms.get("pods") or {}
+                    vals = await self.custom.pod_metric(ns, pm.get("metricName"), selector_str)
+                    have = [vals[m.name_of(p)] for p in pods if m.name_of(p) in vals]
+                    if not have:
+                        raise LookupError(f"no metrics returned for pods/{pm.get('metricName')}")
+                    avg = sum(have) / len(have)
+                    rep = _ratio_replicas(avg / _num(pm.get("targetAverageValue")), len(have), current)
+                    out.append((rep, f"pods metric {pm.get('metricName')}",
+                                {"type": "Pods", "pods": {"metricName": pm.get("metricName"), "currentAverageValue": _fmt(avg)}}))
+                elif typ == "Object":
+                    om = ms.get("object") or {}
+                    val = await self.custom.object_metric(ns, om.get("target") or {}, om.get("metricName"))
+                    rep = _ratio_replicas(val / _num(om.get("targetValue")), current, current)
+                    out.append((rep, f"{om.get('metricName')} metric on {(om.get('target') or {}).get('kind')}",
+                                {"type": "Object", "object": {"target": om.get("target"), "metricName": om.get("metricName"),
+                                                              "currentValue": _fmt(val)}}))
+                else:
+                    raise LookupError(f"unknown metric source type {typ!r}")
+            except (LookupError, m.StatusError, aiohttp.ClientError, asyncio.TimeoutError, ZeroDivisionError, ValueError) as e:
+                if failure is None:
+                    failure = (f"FailedGet{typ}Metric", f"the HPA was unable to compute the replica count: {e}")
+        gt = ann.get(GPU_TARGET_ANNOTATION)
+        gpu_util = None
+        if gt:
+            if resource_metrics is None:
+                resource_metrics = await self.metrics.pod_metrics(ns)
+            rep, gpu_util = gpu_proposal(pods, resource_metrics, float(gt), current)
+            if rep is not None:
+                out.append((rep, "MI355X gpu utilization", None))
+        return out, failure, gpu_util
+
     async def sync(self, key):
         hpa = self.hpa_inf.get(key)
         if hpa is None:
             return
         ns, name = split_key(key)
         spec, st = hpa.get("spec") or {}, hpa.get("status") or {}
+        ann = m.annotations_of(hpa)
+        conds = api_autoscaling._load(ann.get(api_autoscaling.CONDITIONS_ANNOTATION))
+        now = self.clock()
+        stamp = m.format_time(now)
         ref = spec.get("scaleTargetRef") or {}
         plural = SCALE_TARGETS.get(ref.get("kind"))
-        if plural is None:
-            return
-        target = await self.client.get_or_none(plural, ref.get("name", ""), ns)
+        target = await self.client.get_or_none(plural, ref.get("name", ""), ns) if plural else None
         if target is None:
+            _set_condition(conds, "AbleToScale", "False", "FailedGetScale",
+                           f"the HPA controller was unable to get the target's current scale: {ref.get('kind')}/{ref.get('name')}", stamp)
+            self._event(hpa, "Warning", "FailedGetScale", f"unable to get the scale of {ref.get('kind')}/{ref.get('name')}")
+            await self._write_status(hpa, ns, name, {"currentReplicas": st.get("currentReplicas", 0),
+                                                     "desiredReplicas": st.get("desiredReplicas", 0)}, None, conds)
             return
+        _set_condition(conds, "AbleToScale", "True", "SucceededGetScale",
+                       "the HPA controller was able to get the target's current scale", stamp)
         tspec = target.get("spec") or {}
         current = int(tspec.get("replicas", 1))
         sel = tspec.get("selector") or {}
         selector = selector_from_set(sel) if ref.get("kind") == "ReplicationController" else selector_from_label_selector(sel)
+        selector_str = ",".join(f"{k}={v}" for k, v in sorted(sel.items())) if ref.get("kind") == "ReplicationController" \
+            else _selector_string(sel)
         pods = [p for p in self.pod_inf.list() if m.namespace_of(p) == ns and selector.matches(m.labels_of(p))
                 and not is_pod_terminal(p) and not (p.get("metadata") or {}).get("deletionTimestamp")
                 and (p.get("status") or {}).get("phase") == "Running"]
-        metrics = await self.metrics.pod_metrics(ns)
-        proposals = []
-        cpu_target = spec.get("targetCPUUtilizationPercentage", 80 if GPU_TARGET_ANNOTATION not in m.annotations_of(hpa) else None)
-        cpu_util = gpu_util = None
-        if cpu_target:
-            r, cpu_util = cpu_proposal(pods, metrics, cpu_target, current)
-            if r is not None:
-                proposals.append(r)
-        gt = m.annotations_of(hpa).get(GPU_TARGET_ANNOTATION)
-        if gt:
-            r, gpu_util = gpu_proposal(pods, metrics, float(gt), current)
-            if r is not None:
-                proposals.append(r)
-        desired = max(proposals) if proposals else current
         lo, hi = int(spec.get("minReplicas", 1)), int(spec.get("maxReplicas", current))
-        desired = max(lo, min(hi, desired, max(2 * current, 4)))
-        now = self.clock()
+        current_metrics, gpu_util, reason = None, None, ""
+        if current == 0:
+            desired = 0     # autoscaling is disabled for a target scaled to zero
+            _set_condition(conds, "ScalingActive", "False", "ScalingDisabled",
+                           "scaling is disabled since the replica count of the target is zero", stamp)
+        else:
+            proposals, failure, gpu_util = await self._metric_proposals(hpa, ns, pods, selector_str, current)
+            current_metrics = [p[2] for p in proposals if p[2] is not None]
+            if proposals:
+                desired, reason = max((p[0], p[1]) for p in proposals)
+                _set_condition(conds, "ScalingActive", "True", "ValidMetricFound",
+                               f"the HPA was able to successfully calculate a replica count from {reason}", stamp)
+            else:
+                desired = current
+                if failure is not None:
+                    _set_condition(conds, "ScalingActive", "False", failure[0], failure[1], stamp)
+                    self._event(hpa, "Warning", failure[0], failure[1])
+            bounded = max(lo, min(hi, desired, max(2 * current, 4)))
+            if desired > hi or (bounded < desired and bounded == max(2 * current, 4)):
+                limit = ("TooManyReplicas", "the desired replica count is more than the maximum replica count") \
+                    if desired > hi else ("ScaleUpLimit", "the desired replica count is increasing faster than the maximum scale rate")
+                _set_condition(conds, "ScalingLimited", "True", *limit, stamp)
+            elif desired < lo:
+                _set_condition(conds, "ScalingLimited", "True", "TooFewReplicas",
+                               "the desired replica count is less than the minimum replica count", stamp)
+            else:
+                _set_condition(conds, "ScalingLimited", "False", "DesiredWithinRange",
+                               "the desired count is within the acceptable range", stamp)
+            desired = bounded
         last = m.parse_time(st.get("lastScaleTime"))
         rescale = desired != current
         if rescale and last is not None:
-            if desired > current and now - last < self.upscale_delay:
+            up_blocked = desired > current and now - last < self.upscale_delay
+            down_blocked = desired < current and now - last < self.downscale_delay
+            if up_blocked or down_blocked:
                 rescale = False
-            if desired < current and now - last < self.downscale_delay:
-                rescale = False
+                _set_condition(conds, "AbleToScale", "False", "BackoffUpscale" if up_blocked else "BackoffDownscale",
+                               "the time since the previous scale is still within the "
+                               f"{'upscale' if up_blocked else 'downscale'} forbidden window", stamp)
         new_st = {"currentReplicas": current, "desiredReplicas": desired if rescale else current,
                   "observedGeneration": (hpa.get("metadata") or {}).get("generation", 1)}
-        if cpu_util is not None:
-            new_st["currentCPUUtilizationPercentage"] = cpu_util
         if rescale:
             await self.client.patch(plural, ref["name"], {"spec": {"replicas": desired}}, ns)
-            new_st["lastScaleTime"] = m.format_time(now)
+            new_st["lastScaleTime"] = stamp
+            _set_condition(conds, "AbleToScale", "True", "SucceededRescale",
+                           f"the HPA controller was able to update the target scale to {desired}", stamp)
+            self._event(hpa, "Normal", "SuccessfulRescale", f"New size: {desired}; reason: {reason} above target"
+                        if desired > current else f"New size: {desired}; reason: All metrics below target")
         elif st.get("lastScaleTime"):
             new_st["lastScaleTime"] = st["lastScaleTime"]
-        ann = {}
+        await self._write_status(hpa, ns, name, new_st, current_metrics, conds)
         if gpu_util is not None:
-            ann["autoscaling.amd.com/current-gpu-utilization"] = f"{gpu_util:.1f}"
-        if {k: st.get(k) for k in new_st} != new_st:
-            await self.client.patch("horizontalpodautoscalers", name, {"status": new_st}, ns, sub="status")
-        if ann and any(m.annotations_of(hpa).get(k) != v for k, v in ann.items()):
-            await self.client.patch("horizontalpodautoscalers", name, {"metadata": {"annotations": ann}}, ns)
+            v = f"{gpu_util:.1f}"
+            if ann.get("autoscaling.amd.com/current-gpu-utilization") != v:
+                await self.client.patch("horizontalpodautoscalers", name,
+                                        {"metadata": {"annotations": {"autoscaling.amd.com/current-gpu-utilization": v}}}, ns)
+
+    async def _write_status(self, hpa, ns, name, new_st, current_metrics, conds):
+        """Through the v2beta1 status subresource; skipped when nothing but timestamps would change."""
+        old = api_autoscaling.v1_to_v2(json.loads(json.dumps(hpa))).get("status") or {}
+        body = dict(new_st)
+        if current_metrics is not None:
+            body["currentMetrics"] = current_metrics
+        body["conditions"] = conds
+        same = all(old.get(k) == v for k, v in new_st.items()) and \
+            (current_metrics is None or old.get("currentMetrics", []) == current_metrics) and \
+            [{k: c.get(k) for k in ("type", "status", "reason", "message")} for c in old.get("conditions") or []] == \
+            [{k: c.get(k) for k in ("type", "status", "reason", "message")} for c in conds]
+        if same:
+            return
+        await self.client.request("PATCH", f"/apis/autoscaling/v2beta1/namespaces/{ns}/horizontalpodautoscalers/{name}/status",
+                                  body={"status": body}, content_type="application/merge-patch+json")
+
+
+def _selector_string(sel: dict) -> str:
+    parts = [f"{k}={v}" for k, v in sorted((sel.get("matchLabels") or {}).items())]
+    for e in sel.get("matchExpressions") or []:
+        op, vals = e.get("operator"), ",".join(e.get("values") or [])
+        parts.append({"In": f"{e['key']} in ({vals})", "NotIn": f"{e['key']} notin ({vals})",
+                      "Exists": e["key"], "DoesNotExist": f"!{e['key']}"}.get(op, e["key"]))
+    return ",".join(parts)

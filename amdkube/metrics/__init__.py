@@ -10,7 +10,16 @@ and pod, and serves
   /apis/metrics.k8s.io/v1beta1/nodes[/NAME]
   /apis/metrics.k8s.io/v1beta1/pods, /namespaces/NS/pods[/NAME]   (labelSelector supported)
 
-behind front-proxy authentication (the aggregator's client certificate, verified against
+and the custom metrics API (custom.metrics.k8s.io/v1beta1, staging/src/k8s.io/metrics/pkg/apis/
+custom_metrics: MetricValueList of MetricValue{describedObject, metricName, timestamp, window,
+value}) with the MI355X series autoscalers want — per pod `gpu_utilization` (duty cycle, %, the
+busiest of the pod's GPUs), `gpu_memory_used_bytes` (its containers' VRAM), `gpu_count`; per
+node the same over all its GPUs —
+
+  /apis/custom.metrics.k8s.io/v1beta1/namespaces/NS/pods/{NAME|*}/METRIC   (labelSelector for *)
+  /apis/custom.metrics.k8s.io/v1beta1/nodes/{NAME|*}/METRIC
+
+all behind front-proxy authentication (the aggregator's client certificate, verified against
 --requestheader-client-ca-file, asserting X-Remote-User/Group) or a bearer token checked by
 TokenReview, and authorization delegated to the main apiserver (SubjectAccessReview, verbs
 get/list on nodes.metrics.k8s.io / pods.metrics.k8s.io).
@@ -28,6 +37,8 @@ from ..api.labels import parse_selector
 
 log = logging.getLogger("amdkube.metrics")
 GV = "metrics.k8s.io/v1beta1"
+CGV = "custom.metrics.k8s.io/v1beta1"
+POD_METRICS = ("gpu_utilization", "gpu_memory_used_bytes", "gpu_count")
 
 
 def _cpu(nano: int) -> str:
@@ -64,7 +75,14 @@ class MetricsServer:
         app.router.add_get("/apis/metrics.k8s.io/v1beta1/pods", self.list_pods)
         app.router.add_get("/apis/metrics.k8s.io/v1beta1/namespaces/{ns}/pods", self.list_pods)
         app.router.add_get("/apis/metrics.k8s.io/v1beta1/namespaces/{ns}/pods/{name}", self.get_pod)
+        app.router.add_get("/apis/custom.metrics.k8s.io", self.custom_group)
+        app.router.add_get("/apis/custom.metrics.k8s.io/v1beta1", self.custom_resources)
+        app.router.add_get("/apis/custom.metrics.k8s.io/v1beta1/namespaces/{ns}/pods/{name}/{metric}", self.custom_pods)
+        app.router.add_get("/apis/custom.metrics.k8s.io/v1beta1/nodes/{name}/{metric}", self.custom_nodes)
         app.router.add_get("/healthz", lambda r: web.Response(text="ok"))
+        self.custom: dict[tuple, dict] = {}        # ("pod", ns, name) | ("node", "", name) -> {metric: value}
+        self.node_labels: dict[str, dict] = {}
+        self.stamp = ""
 
     # ------------------------------------------------------------------ scraping
     async def scrape_once(self):
@@ -88,11 +106,16 @@ class MetricsServer:
                 return None
         now = m.now_rfc3339()
         window = f"{int(self.resolution)}s"
+        custom: dict[tuple, dict] = {}
         for res in await asyncio.gather(*(one(n) for n in nodes)):
             if res is None:
                 continue
             n, summ = res
             node = summ.get("node") or {}
+            nacc = node.get("accelerators") or []
+            custom[("node", "", m.name_of(n))] = {
+                "gpu_utilization": str(max((a.get("dutyCycle", 0) for a in nacc), default=0)),
+                "gpu_memory_used_bytes": str(sum(a.get("memoryUsed", 0) for a in nacc)), "gpu_count": str(len(nacc))}
             self.nodes[m.name_of(n)] = {"kind": "NodeMetrics", "apiVersion": GV,
                                         "metadata": {"name": m.name_of(n), "creationTimestamp": now,
                                                      "labels": m.labels_of(n)},
@@ -110,6 +133,10 @@ class MetricsServer:
                        "metadata": {"name": key[1], "namespace": key[0], "creationTimestamp": now,
                                     "labels": self.labels.get(key, {})},
                        "timestamp": now, "window": window, "containers": cs}
+                custom[("pod", key[0], key[1])] = {
+                    "gpu_utilization": str(max((a.get("dutyCycle", 0) for a in accel), default=0)),
+                    "gpu_memory_used_bytes": str(sum(a.get("memoryUsed", 0) for a in accel)),
+                    "gpu_count": str(len({a.get("id") for a in accel}))}
                 if accel:   # amdkube: the pod's MI355X duty cycle and VRAM next to CPU/memory
                     obj["metadata"]["annotations"] = {"amd.com/gpu-duty-cycle": str(max(a.get("dutyCycle", 0) for a in accel)),
                                                       "amd.com/gpu-memory-used": str(sum(a.get("memoryUsed", 0) for a in accel))}
@@ -117,6 +144,8 @@ class MetricsServer:
         live = {(m.namespace_of(p), m.name_of(p)) for p in pods}
         for k in [k for k in self.pods if k not in live]:
             del self.pods[k]
+        self.custom, self.stamp = custom, now
+        self.node_labels = {m.name_of(n): m.labels_of(n) for n in nodes}
         self.scrapes += 1
 
     async def _loop(self):
@@ -151,15 +180,20 @@ class MetricsServer:
             raise web.HTTPUnauthorized(text="Unauthorized")
         parts = request.path.split("/")
         if len(parts) > 4:
+            group = "custom.metrics.k8s.io" if parts[2] == "custom.metrics.k8s.io" else "metrics.k8s.io"
             res = "nodes" if "nodes" in parts else "pods"
+            if group == "custom.metrics.k8s.io" and request.match_info.get("metric"):
+                res = f"{res}/{request.match_info['metric']}"     # custom metrics authorize per metric
             ns = request.match_info.get("ns", "")
-            verb = "get" if request.match_info.get("name") else "list"
+            nm = request.match_info.get("name", "")
+            verb = "get" if nm and nm != "*" else "list"
             sar = await self.client.create({"apiVersion": "authorization.k8s.io/v1", "kind": "SubjectAccessReview", "spec": {
                 "user": user["name"], "groups": user.get("groups") or [],
-                "resourceAttributes": {"verb": verb, "group": "metrics.k8s.io", "resource": res, "namespace": ns,
-                                       "name": request.match_info.get("name", "")}}})
+                "resourceAttributes": {"verb": verb, "group": group, "resource": res.split("/")[0],
+                                       "subresource": res.split("/")[1] if "/" in res else "", "namespace": ns,
+                                       "name": "" if nm == "*" else nm}}})
             if not (sar.get("status") or {}).get("allowed"):
-                raise web.HTTPForbidden(text=f'User "{user["name"]}" cannot {verb} {res}.metrics.k8s.io')
+                raise web.HTTPForbidden(text=f'User "{user["name"]}" cannot {verb} {res}.{group}')
         return await handler(request)
 
     # ---------------------------------------------------------------- handlers
@@ -198,6 +232,47 @@ class MetricsServer:
         if o is None:
             raise web.HTTPNotFound(text=f'podmetrics "{r.match_info["name"]}" not found')
         return web.json_response(o)
+
+    # ------------------------------------------------------------ custom metrics
+    async def custom_group(self, r):
+        return web.json_response({"kind": "APIGroup", "apiVersion": "v1", "name": "custom.metrics.k8s.io",
+                                  "versions": [{"groupVersion": CGV, "version": "v1beta1"}],
+                                  "preferredVersion": {"groupVersion": CGV, "version": "v1beta1"}})
+
+    async def custom_resources(self, r):
+        res = [{"name": f"pods/{mt}", "singularName": "", "namespaced": True, "kind": "MetricValueList", "verbs": ["get"]}
+               for mt in POD_METRICS]
+        res += [{"name": f"nodes/{mt}", "singularName": "", "namespaced": False, "kind": "MetricValueList", "verbs": ["get"]}
+                for mt in POD_METRICS]
+        return web.json_response({"kind": "APIResourceList", "apiVersion": "v1", "groupVersion": CGV, "resources": res})
+
+    def _values(self, kind, ns, name, metric, labels_of, q):
+        if metric not in POD_METRICS:
+            raise web.HTTPNotFound(text=f'the server could not find the metric {metric} for {kind.lower()}s')
+        sel = parse_selector(q["labelSelector"]) if q.get("labelSelector") else None
+        items = []
+        scope = "pod" if kind == "Pod" else "node"
+        for (sc, ons, oname), vals in sorted(self.custom.items()):
+            if sc != scope or ons != ns or (name != "*" and oname != name):
+                continue
+            if sel is not None and not sel.matches(labels_of(ons, oname)):
+                continue
+            ref = {"kind": kind, "name": oname, "apiVersion": "/v1"}
+            if ns:
+                ref["namespace"] = ons
+            items.append({"describedObject": ref, "metricName": metric, "timestamp": self.stamp,
+                          "window": int(self.resolution), "value": vals[metric]})
+        if name != "*" and not items:
+            raise web.HTTPNotFound(text=f'the server could not find the metric {metric} for {kind.lower()}s {name}')
+        return web.json_response({"kind": "MetricValueList", "apiVersion": CGV, "metadata": {"selfLink": ""}, "items": items})
+
+    async def custom_pods(self, r):
+        return self._values("Pod", r.match_info["ns"], r.match_info["name"], r.match_info["metric"],
+                            lambda ns, n: self.labels.get((ns, n), {}), r.query)
+
+    async def custom_nodes(self, r):
+        return self._values("Node", "", r.match_info["name"], r.match_info["metric"],
+                            lambda ns, n: self.node_labels.get(n, {}), r.query)
 
     # --------------------------------------------------------------- lifecycle
     async def start(self, host="127.0.0.1", port=0):
