@@ -4,9 +4,11 @@ Reference: pkg/cloudprovider/cloud.go (Interface: Instances, LoadBalancer, Route
 ProviderName, HasClusterID), plugins.go (RegisterCloudProvider / GetCloudProvider by
 --cloud-provider name) and providers/fake (the recording fake used by controller tests).
 
-The reference ships AWS / GCE / Azure / vSphere / OpenStack / … drivers. An
-MI355X node runs on-prem — bare metal or an OpenStack cloud — or on a GPU cloud with no
-Kubernetes cloud integration, so the providers here are:
+The reference ships AWS / GCE / Azure / vSphere / OpenStack / … drivers; the
+fork's README names EC2 and GCP GPU VMs next to on-prem DGX hosts. An MI355X node runs on-prem
+(bare metal or an OpenStack cloud) or on a public GPU cloud, so the providers here are:
+  * `aws` (cloudprovider/aws.py): EC2 instances/zones/routes, classic ELB, EBS volumes — the
+    query APIs spoken directly with Signature V4;
   * `openstack` (cloudprovider/openstack.py): Keystone + Nova instances/zones, Neutron router
     routes, Octavia/LBaaS v2 load balancers with floating IPs, Cinder volumes;
   * `baremetal`: load balancers get addresses from a configured pool (the MetalLB model),
@@ -286,7 +288,12 @@ def _openstack(config):
     return OpenStack(config)
 
 
-_PROVIDERS = {"baremetal": BareMetal, "fake": Fake, "openstack": _openstack}
+def _aws(config):
+    from .aws import AWS
+    return AWS(config)
+
+
+_PROVIDERS = {"baremetal": BareMetal, "fake": Fake, "openstack": _openstack, "aws": _aws}
 
 
 def load_config(path: str | None):

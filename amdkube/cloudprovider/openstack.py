@@ -438,6 +438,8 @@ def _secs(v) -> int:
 
 class Volumes:
     """Cinder block storage attached to servers through Nova (openstack_volumes.go)."""
+    provisioner = "kubernetes.io/cinder"
+    source_key = "cinder"
 
     def __init__(self, os_, cfg: dict):
         self.os, self.cfg = os_, cfg
@@ -495,6 +497,27 @@ class Volumes:
 
     def zone(self, vid: str) -> str:
         return self.get(vid).get("availability_zone", "")
+
+    def device_candidates(self, vid: str, device_path: str = "") -> list[str]:
+        """By serial first; Nova's reported device only with [BlockStorage] trust-device-path."""
+        pats = device_candidates(vid)
+        if device_path and str(self.cfg.get("trust-device-path", "false")).lower() == "true":
+            pats = [device_path] + pats
+        return pats
+
+    # ---- the provisioner interface (controllers/volumes.py)
+    def provision(self, name: str, gib: int, params: dict, tags: dict, pvc_name: str) -> tuple[dict, dict]:
+        """cinder_util.go CreateVolume: the class's availability zone and type."""
+        vol = self.create(f"kubernetes-dynamic-{name}", gib, params.get("type", ""), params.get("availability", ""), tags)
+        labels = {}
+        if vol.get("availability_zone"):
+            labels["failure-domain.beta.kubernetes.io/zone"] = vol["availability_zone"]
+        if self.os.client.region:
+            labels["failure-domain.beta.kubernetes.io/region"] = self.os.client.region
+        return {"volumeID": vol["id"], "fsType": params.get("fsType", "ext4")}, labels
+
+    def delete_source(self, src: dict):
+        self.delete(src["volumeID"])
 
 
 def device_candidates(vid: str) -> list[str]:

@@ -163,8 +163,8 @@ class PersistentVolumeBinderController(Controller):
             sc = self._class(claim_class(pvc))
             if sc is not None and sc.get("provisioner") in HOSTPATH_PROVISIONERS:
                 pv = await self._provision(pvc, sc)
-            elif sc is not None and sc.get("provisioner") == CINDER_PROVISIONER and self._cinder() is not None:
-                pv = await self._provision_cinder(pvc, sc)
+            elif sc is not None and self._cloud_disks() is not None and sc.get("provisioner") == self._cloud_disks().provisioner:
+                pv = await self._provision_cloud(pvc, sc)
             else:
                 if (pvc.get("status") or {}).get("phase") != "Pending":
                     await self.client.patch("persistentvolumeclaims", name, {"status": {"phase": "Pending"}}, ns, sub="status")
@@ -186,14 +186,15 @@ class PersistentVolumeBinderController(Controller):
         if {k: (pvc.get("status") or {}).get(k) for k in st} != st:
             await self.client.patch("persistentvolumeclaims", name, {"status": st}, ns, sub="status")
 
-    def _cinder(self):
+    def _cloud_disks(self):
+        """The cloud provider's block-disk service (Cinder, EBS, GCE PD, Azure disks), if any."""
         cloud = getattr(getattr(self.mgr, "opts", None), "cloud", None)
         return cloud.volumes() if cloud is not None and hasattr(cloud, "volumes") else None
 
-    async def _provision_cinder(self, pvc, sc):
-        """cinder_util.go CreateVolume: a Cinder volume of the claim's size (GiB, rounded up) in
-        the class's availability zone and type, tagged with the claim; the PV is labelled with the
-        volume's zone and the region."""
+    async def _provision_cloud(self, pvc, sc):
+        """The in-tree cloud provisioners (cinder_util.go, aws_util.go, gce_util.go,
+        azure_provision.go CreateVolume): a disk of the claim's size in GiB, rounded up, with the
+        class's parameters, tagged with the claim; the PV carries the disk's zone/region labels."""
         from ..api.quantity import parse_quantity
         size = ((pvc.get("spec") or {}).get("resources") or {}).get("requests", {}).get("storage", "1Gi")
         gib = max(1, -(-int(parse_quantity(size).value()) // (1 << 30)))
@@ -201,23 +202,15 @@ class PersistentVolumeBinderController(Controller):
         name = f"pvc-{m.uid_of(pvc)}"
         tags = {"kubernetes.io/created-for/pvc/namespace": m.namespace_of(pvc),
                 "kubernetes.io/created-for/pvc/name": m.name_of(pvc), "kubernetes.io/created-for/pv/name": name}
-        vols = self._cinder()
-        vol = await asyncio.to_thread(vols.create, f"kubernetes-dynamic-{name}", gib, params.get("type", ""),
-                                      params.get("availability", ""), tags)
-        labels = {}
-        if vol.get("availability_zone"):
-            labels["failure-domain.beta.kubernetes.io/zone"] = vol["availability_zone"]
-        region = getattr(getattr(self.mgr.opts.cloud, "client", None), "region", "")
-        if region:
-            labels["failure-domain.beta.kubernetes.io/region"] = region
+        disks = self._cloud_disks()
+        source, labels = await asyncio.to_thread(disks.provision, name, gib, params, tags, m.name_of(pvc))
         pv = {"apiVersion": "v1", "kind": "PersistentVolume",
-              "metadata": {"name": name, "labels": labels,
-                           "annotations": {"pv.kubernetes.io/provisioned-by": CINDER_PROVISIONER}},
+              "metadata": {"name": name, "labels": {k: v for k, v in labels.items() if v},
+                           "annotations": {"pv.kubernetes.io/provisioned-by": disks.provisioner}},
               "spec": {"capacity": {"storage": f"{gib}Gi"},
                        "accessModes": (pvc.get("spec") or {}).get("accessModes") or ["ReadWriteOnce"],
                        "persistentVolumeReclaimPolicy": sc.get("reclaimPolicy", "Delete"),
-                       "storageClassName": m.name_of(sc),
-                       "cinder": {"volumeID": vol["id"], "fsType": params.get("fsType", "ext4")},
+                       "storageClassName": m.name_of(sc), disks.source_key: source,
                        "claimRef": {"kind": "PersistentVolumeClaim", "namespace": m.namespace_of(pvc), "name": m.name_of(pvc),
                                     "uid": m.uid_of(pvc), "apiVersion": "v1"}}}
         try:
@@ -267,9 +260,10 @@ class PersistentVolumeBinderController(Controller):
         if policy == "Delete":
             if m.annotations_of(pv).get("pv.kubernetes.io/provisioned-by") in HOSTPATH_PROVISIONERS:
                 shutil.rmtree((ps.get("hostPath") or {}).get("path", "") or "/nonexistent", ignore_errors=True)
-            elif ps.get("cinder") and m.annotations_of(pv).get("pv.kubernetes.io/provisioned-by") == CINDER_PROVISIONER \
-                    and self._cinder() is not None:
-                await asyncio.to_thread(self._cinder().delete, ps["cinder"]["volumeID"])   # fails while attached: retried
+            elif self._cloud_disks() is not None and ps.get(self._cloud_disks().source_key) \
+                    and m.annotations_of(pv).get("pv.kubernetes.io/provisioned-by") == self._cloud_disks().provisioner:
+                disks = self._cloud_disks()
+                await asyncio.to_thread(disks.delete_source, ps[disks.source_key])   # fails while attached: retried
             try:
                 await self.client.delete("persistentvolumes", name)
             except m.StatusError as e:

@@ -146,7 +146,7 @@ class KubeletConfig:
     volume_reconcile_period: float = 2.0              # reconciler loop period (s)
     volume_remount_period: float = 60.0               # re-render secret/configMap/downwardAPI/projected content (s)
     cloud_provider: str = ""                          # --cloud-provider ("external": cloud-controller-manager initialises the node)
-    cloud_config: str = ""                            # --cloud-config (in-tree providers: openstack, baremetal)
+    cloud_config: str = ""                            # --cloud-config (in-tree providers: aws, gce, azure, openstack, baremetal)
     enable_server: bool = True                        # --enable-server (the authenticated API on --port)
     enable_debugging_handlers: bool = True            # --enable-debugging-handlers (logs, exec, attach, portForward, run, pprof)
     read_only_port: int = -1                          # --read-only-port (unauthenticated read-only API; -1/0: off; CLI default 10255)
@@ -504,7 +504,9 @@ class Kubelet:
         if self.cloud is not None and self.cloud.instances() is not None:
             inst = self.cloud.instances()
             if not self.cfg.provider_id:
-                self.cfg.provider_id = await inst.instance_id(self.node_name)
+                # cloudprovider.GetInstanceProviderID: "<provider>://<instance id>"
+                iid = await inst.instance_id(self.node_name)
+                self.cfg.provider_id = iid if "://" in iid else f"{self.cloud.name}://{iid}"
             itype = await inst.instance_type(self.node_name)
             if itype:
                 labels["beta.kubernetes.io/instance-type"] = itype

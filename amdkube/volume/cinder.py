@@ -1,10 +1,13 @@
-"""OpenStack Cinder volumes (pkg/volume/cinder: attacher.go, cinder.go, cinder_util.go).
+"""Cloud block disks attached through the cloud provider: OpenStack Cinder (pkg/volume/cinder:
+attacher.go, cinder.go, cinder_util.go), AWS EBS (pkg/volume/aws_ebs: attacher.go, aws_ebs.go,
+aws_util.go), GCE persistent disks (pkg/volume/gce_pd) and Azure managed disks
+(pkg/volume/azure_dd).
 
-Attachable block volumes: the attach/detach controller attaches the volume to the node's Nova
-server through the cloud provider (`--cloud-provider=openstack`, cloudprovider/openstack.py),
-the kubelet waits for the disk to appear by its serial (/dev/disk/by-id/virtio-<id[:20]>,
-the device Nova reported only with [BlockStorage] trust-device-path), formats it if blank,
-mounts it once per node and bind-mounts it into pods (the shared _Block machinery).
+One flow for all of them: the attach/detach controller attaches the disk to the node's
+instance through `--cloud-provider`'s volumes() (cloudprovider/{openstack,aws,gce,azure}.py),
+the kubelet waits for the disk to appear under one of the provider's device paths (by serial /
+by-id first, the device the cloud reported last), formats it if blank, mounts it once per node
+and bind-mounts it into pods (the shared _Block machinery).
 """
 from __future__ import annotations
 
@@ -14,39 +17,50 @@ from . import VolumeError
 from .network import _Block
 
 
-class CinderPlugin(_Block):
-    name = "kubernetes.io/cinder"
-    source_key = "cinder"
+class CloudDiskPlugin(_Block):
+    """A block disk whose attach/detach go through the cloud provider's volumes()."""
+    provider = ""         # cloud provider name that serves this volume type
+    id_field = ""         # the source field naming the disk
 
     def volume_name(self, spec) -> str:
-        return spec.source("cinder").get("volumeID", "")
+        return spec.source(self.source_key).get(self.id_field, "")
 
     def _volumes(self):
         cloud = getattr(self.host, "cloud", None)
         vols = cloud.volumes() if cloud is not None and hasattr(cloud, "volumes") else None
-        if vols is None:
-            raise VolumeError("cinder volumes need the OpenStack cloud provider (--cloud-provider=openstack)")
+        if vols is None or getattr(vols, "source_key", self.source_key) != self.source_key:
+            raise VolumeError(f"{self.source_key} volumes need the {self.provider} cloud provider (--cloud-provider={self.provider})")
         return vols
 
     async def attach(self, spec, node: str) -> str:
         vid = self.volume_name(spec)
         if not vid:
-            raise VolumeError(f"cinder volume {spec.name()!r} has no volumeID")
+            raise VolumeError(f"{self.source_key} volume {spec.name()!r} has no {self.id_field}")
         return await asyncio.to_thread(self._volumes().attach, node, vid)
 
     async def wait_for_attach(self, spec, device_path, pod, timeout):
-        from ..cloudprovider.openstack import device_candidates
         vid = self.volume_name(spec)
-        pats = device_candidates(vid)
-        cloud = getattr(self.host, "cloud", None)
-        trust = str(((getattr(cloud, "cfg", None) or {}).get("blockstorage") or {}).get("trust-device-path", "false")).lower()
-        if device_path and trust == "true":
-            pats = [device_path] + pats
-        return await self._wait_device(pats, timeout, f"cinder volume {vid}")
+        pats = self._volumes().device_candidates(vid, device_path)
+        return await self._wait_device(pats, timeout, f"{self.source_key} volume {vid}")
 
     async def detach(self, volume_name: str, node: str):
         await asyncio.to_thread(self._volumes().detach, node, volume_name)
 
 
+class CinderPlugin(CloudDiskPlugin):
+    name = "kubernetes.io/cinder"
+    source_key = "cinder"
+    provider = "openstack"
+    id_field = "volumeID"
+
+
+class AWSEBSPlugin(CloudDiskPlugin):
+    """aws_ebs: volumeID `aws://<zone>/vol-…`; partition and readOnly from the source."""
+    name = "kubernetes.io/aws-ebs"
+    source_key = "awsElasticBlockStore"
+    provider = "aws"
+    id_field = "volumeID"
+
+
 def plugins():
-    return [CinderPlugin()]
+    return [CinderPlugin(), AWSEBSPlugin()]

@@ -124,13 +124,16 @@ def test_network_filesystems(tmp_path):
         for x in (d, d2, d3):
             await mgr.find_by_spec(nfs).tear_down(x)
         assert len(fm.actions("unmount")) == 3 and not fm.mounts
-        # cloud disks are recognised and fail with a precise reason
-        ebs = Spec(volume={"name": "e", "awsElasticBlockStore": {"volumeID": "vol-1"}})
+        # vendor volumes without a reachable backend are recognised and fail with a precise reason
+        pwx = Spec(volume={"name": "e", "portworxVolume": {"volumeID": "vol-1"}})
         try:
-            await mgr.find_by_spec(ebs).set_up(ebs, _pod(), str(tmp_path / "e"))
+            await mgr.find_by_spec(pwx).set_up(pwx, _pod(), str(tmp_path / "e"))
             raise AssertionError("expected failure")
         except VolumeError as e:
-            assert "AWS EC2 API" in str(e)
+            assert "Portworx REST API" in str(e)
+        # an EBS disk is a real attachable plugin, served through the AWS cloud provider
+        ebs = Spec(volume={"name": "e", "awsElasticBlockStore": {"volumeID": "vol-1"}})
+        assert mgr.find_by_spec(ebs).attachable and mgr.find_by_spec(ebs).name == "kubernetes.io/aws-ebs"
     run(go(), 10)
 
 
