@@ -9,6 +9,8 @@ fork's README names EC2 and GCP GPU VMs next to on-prem DGX hosts. An MI355X nod
 (bare metal or an OpenStack cloud) or on a public GPU cloud, so the providers here are:
   * `aws` (cloudprovider/aws.py): EC2 instances/zones/routes, classic ELB, EBS volumes — the
     query APIs spoken directly with Signature V4;
+  * `gce` (cloudprovider/gce.py): Compute Engine instances/zones/routes, external load
+    balancers (address, firewall, health check, target pool, forwarding rule), persistent disks;
   * `openstack` (cloudprovider/openstack.py): Keystone + Nova instances/zones, Neutron router
     routes, Octavia/LBaaS v2 load balancers with floating IPs, Cinder volumes;
   * `baremetal`: load balancers get addresses from a configured pool (the MetalLB model),
@@ -293,7 +295,12 @@ def _aws(config):
     return AWS(config)
 
 
-_PROVIDERS = {"baremetal": BareMetal, "fake": Fake, "openstack": _openstack, "aws": _aws}
+def _gce(config):
+    from .gce import GCE
+    return GCE(config)
+
+
+_PROVIDERS = {"baremetal": BareMetal, "fake": Fake, "openstack": _openstack, "aws": _aws, "gce": _gce}
 
 
 def load_config(path: str | None):

@@ -62,5 +62,20 @@ class AWSEBSPlugin(CloudDiskPlugin):
     id_field = "volumeID"
 
 
+class GCEPDPlugin(CloudDiskPlugin):
+    """gce_pd: pdName names a zonal persistent disk, attached with deviceName = pdName."""
+    name = "kubernetes.io/gce-pd"
+    source_key = "gcePersistentDisk"
+    provider = "gce"
+    id_field = "pdName"
+
+    async def attach(self, spec, node: str) -> str:
+        vid = self.volume_name(spec)
+        if not vid:
+            raise VolumeError(f"gcePersistentDisk volume {spec.name()!r} has no pdName")
+        ro = spec.source_read_only(self.source_key)
+        return await asyncio.to_thread(self._volumes().attach, node, vid, ro)
+
+
 def plugins():
-    return [CinderPlugin(), AWSEBSPlugin()]
+    return [CinderPlugin(), AWSEBSPlugin(), GCEPDPlugin()]

@@ -1,16 +1,15 @@
 """Volume types whose backends are cloud or vendor services this build cannot reach
-(pkg/volume/gce_pd, azure_dd, vsphere_volume, photon_pd, portworx, scaleio,
-storageos, flocker; Cinder and AWS EBS are implemented in volume/cinder.py over the OpenStack and AWS providers). They are recognised — so a pod using one gets a precise FailedMount event
+(pkg/volume/azure_dd, vsphere_volume, photon_pd, portworx, scaleio,
+storageos, flocker; Cinder, AWS EBS and GCE PD are implemented in volume/cinder.py over the OpenStack, AWS and GCE providers). They are recognised — so a pod using one gets a precise FailedMount event
 instead of "no volume plugin matched" — but their set-up fails: attaching them needs the cloud
 provider's block-storage API (or the vendor's client library), and amdkube's cloud providers
-are AWS, OpenStack, bare metal and fake (no public-cloud SDKs exist offline on an MI355X host).
+are AWS, GCE, OpenStack, bare metal and fake (no public-cloud SDKs exist offline on an MI355X host).
 """
 from __future__ import annotations
 
 from . import VolumeError, VolumePlugin
 
 _TYPES = {
-    "gcePersistentDisk": ("kubernetes.io/gce-pd", "the GCE compute API"),
     "azureDisk": ("kubernetes.io/azure-disk", "the Azure compute API"),
     "vsphereVolume": ("kubernetes.io/vsphere-volume", "the vSphere API"),
     "photonPersistentDisk": ("kubernetes.io/photon-pd", "the Photon controller API"),
