@@ -11,6 +11,8 @@ fork's README names EC2 and GCP GPU VMs next to on-prem DGX hosts. An MI355X nod
     query APIs spoken directly with Signature V4;
   * `gce` (cloudprovider/gce.py): Compute Engine instances/zones/routes, external load
     balancers (address, firewall, health check, target pool, forwarding rule), persistent disks;
+  * `azure` (cloudprovider/azure.py): ARM VMs/NICs, route table, the per-cluster load balancer
+    with its NSG rules, managed disks — the cloud that rents AMD Instinct VMs;
   * `openstack` (cloudprovider/openstack.py): Keystone + Nova instances/zones, Neutron router
     routes, Octavia/LBaaS v2 load balancers with floating IPs, Cinder volumes;
   * `baremetal`: load balancers get addresses from a configured pool (the MetalLB model),
@@ -300,7 +302,12 @@ def _gce(config):
     return GCE(config)
 
 
-_PROVIDERS = {"baremetal": BareMetal, "fake": Fake, "openstack": _openstack, "aws": _aws, "gce": _gce}
+def _azure(config):
+    from .azure import Azure
+    return Azure(config)
+
+
+_PROVIDERS = {"baremetal": BareMetal, "fake": Fake, "openstack": _openstack, "aws": _aws, "gce": _gce, "azure": _azure}
 
 
 def load_config(path: str | None):

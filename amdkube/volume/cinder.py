@@ -77,5 +77,25 @@ class GCEPDPlugin(CloudDiskPlugin):
         return await asyncio.to_thread(self._volumes().attach, node, vid, ro)
 
 
+class AzureDiskPlugin(CloudDiskPlugin):
+    """azure_dd (kind Managed): diskURI names the managed disk; attach answers the LUN and the
+    kubelet finds the disk by it (azure_common_linux.go findDiskByLun)."""
+    name = "kubernetes.io/azure-disk"
+    source_key = "azureDisk"
+    provider = "azure"
+    id_field = "diskURI"
+
+    async def attach(self, spec, node: str) -> str:
+        src = spec.source(self.source_key)
+        if (src.get("kind") or "Shared") != "Managed":
+            raise VolumeError(f"azureDisk volume {spec.name()!r}: kind {src.get('kind') or 'Shared'} (blob disks) is not "
+                              "supported; use kind: Managed")
+        uri = self.volume_name(spec)
+        if not uri:
+            raise VolumeError(f"azureDisk volume {spec.name()!r} has no diskURI")
+        caching = src.get("cachingMode") or "ReadOnly"
+        return await asyncio.to_thread(self._volumes().attach, node, uri, caching)
+
+
 def plugins():
-    return [CinderPlugin(), AWSEBSPlugin(), GCEPDPlugin()]
+    return [CinderPlugin(), AWSEBSPlugin(), GCEPDPlugin(), AzureDiskPlugin()]

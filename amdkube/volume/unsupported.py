@@ -1,16 +1,16 @@
-"""Volume types whose backends are cloud or vendor services this build cannot reach
-(pkg/volume/azure_dd, vsphere_volume, photon_pd, portworx, scaleio,
-storageos, flocker; Cinder, AWS EBS and GCE PD are implemented in volume/cinder.py over the OpenStack, AWS and GCE providers). They are recognised — so a pod using one gets a precise FailedMount event
-instead of "no volume plugin matched" — but their set-up fails: attaching them needs the cloud
-provider's block-storage API (or the vendor's client library), and amdkube's cloud providers
-are AWS, GCE, OpenStack, bare metal and fake (no public-cloud SDKs exist offline on an MI355X host).
+"""Volume types whose backends are vendor services this build cannot reach (pkg/volume/
+vsphere_volume, photon_pd, portworx, scaleio, storageos, flocker). Cinder, AWS EBS, GCE PD and
+Azure managed disks are real plugins (volume/cinder.py) over the OpenStack, AWS, GCE and Azure
+providers. These are recognised — so a pod using one gets a precise FailedMount event instead
+of "no volume plugin matched" — but their set-up fails: attaching them needs the vendor's API
+or client library (vCenter, Photon controller, Portworx, ScaleIO gateway + drv_cfg, StorageOS,
+Flocker control service), none of which an MI355X host has.
 """
 from __future__ import annotations
 
 from . import VolumeError, VolumePlugin
 
 _TYPES = {
-    "azureDisk": ("kubernetes.io/azure-disk", "the Azure compute API"),
     "vsphereVolume": ("kubernetes.io/vsphere-volume", "the vSphere API"),
     "photonPersistentDisk": ("kubernetes.io/photon-pd", "the Photon controller API"),
     "portworxVolume": ("kubernetes.io/portworx-volume", "the Portworx REST API"),
