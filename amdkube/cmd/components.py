@@ -479,7 +479,7 @@ def cloud_controller_manager(argv):
     ap.add_argument("--master", "--server", dest="server", default="http://127.0.0.1:8080")
     ap.add_argument("--kubeconfig", default=None)
     ap.add_argument("--token", default=None)
-    ap.add_argument("--cloud-provider", required=True, help="baremetal | fake")
+    ap.add_argument("--cloud-provider", required=True, help="aws | gce | azure | openstack | baremetal | fake")
     ap.add_argument("--cloud-config", default=None, help="provider config (baremetal: loadBalancerIPRange, zone, region, "
                                                          "instances inventory)")
     ap.add_argument("--controllers", default="*", help="'*' = cloud-node,service,route,persistentvolume-labeler")
@@ -514,6 +514,34 @@ def cloud_controller_manager(argv):
 
     async def mk():
         return await ControllerManager(_client(a), names, a.leader_elect == "true", socket.gethostname(), options=opts).start()
+    _run_forever(mk)
+
+
+def gke_certificates_controller(argv):
+    """cmd/gke-certificates-controller: signs approved CSRs through an external signing webhook
+    (the kubeconfig of --cluster-signing-gke-kubeconfig) instead of a local CA key, optionally
+    approving every kubelet client CSR of one group."""
+    ap = argparse.ArgumentParser("amdkube gke-certificates-controller")
+    ap.add_argument("--master", "--server", dest="server", default="http://127.0.0.1:8080")
+    ap.add_argument("--kubeconfig", default=None, help="kubeconfig with authorization and master location information")
+    ap.add_argument("--token", default=None)
+    ap.add_argument("--cluster-signing-gke-kubeconfig", required=True,
+                    help="kubeconfig of the signing service certificates are POSTed to")
+    ap.add_argument("--cluster-signing-gke-retry-backoff", type=float, default=0.5,
+                    help="initial backoff (s) between signing attempts; later attempts double it")
+    ap.add_argument("--insecure-experimental-approve-all-kubelet-csrs-for-group", default="",
+                    help="auto-approve every kubelet client CSR from members of this group")
+    ap.add_argument("-v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "gke-certificates-controller")
+    from ..controllers import ControllerManager, Options
+    opts = Options(extra={"signing_kubeconfig": a.cluster_signing_gke_kubeconfig,
+                          "signing_retry_backoff": a.cluster_signing_gke_retry_backoff,
+                          "approve_group": a.insecure_experimental_approve_all_kubelet_csrs_for_group})
+    names = ["csrsigning-webhook"] + (["csrapproving-group"] if a.insecure_experimental_approve_all_kubelet_csrs_for_group else [])
+
+    async def mk():
+        return await ControllerManager(_client(a), names, False, socket.gethostname(), options=opts).start()
     _run_forever(mk)
 
 
@@ -1091,6 +1119,7 @@ COMPONENTS = {"etcd": etcd, "dns": dns, "kube-dns": dns, "kubeadm": kubeadm, "pr
               "controller-manager": controller_manager, "kube-controller-manager": controller_manager, "kubelet": kubelet,
               "rocshim": rocshim, "amd-device-plugin": device_plugin, "device-plugin": device_plugin,
               "amdgpu-exporter": exporter, "exporter": exporter, "hollow-node": hollow_node, "local-up": local_up,
-              "metrics-server": metrics_server, "cloud-controller-manager": cloud_controller_manager}
+              "metrics-server": metrics_server, "cloud-controller-manager": cloud_controller_manager,
+              "gke-certificates-controller": gke_certificates_controller}
 from .gendocs import GENERATORS as _GENERATORS  # noqa: E402  (gendocs/genkubedocs/genman/genyaml)
 COMPONENTS.update(_GENERATORS)

@@ -111,6 +111,7 @@ COMPONENT_SYNOPSIS = {
     "hollow-node": "A kubemark hollow node: a real kubelet and AMD device plugin over a simulated 8xMI355X.",
     "local-up": "Starts a single-node cluster on this host (local-up-cluster).",
     "metrics-server": "Serves metrics.k8s.io node and pod metrics from kubelet summaries.",
+    "gke-certificates-controller": "Signs approved certificate signing requests through an external signing webhook.",
     "rocshim": "The CRI runtime: pause sandboxes and process containers with only their GPUs' device nodes.",
 }
 

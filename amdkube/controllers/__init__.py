@@ -21,6 +21,7 @@ from dataclasses import dataclass, field
 
 from ..client import Client, EventRecorder, LeaderElector, SharedInformerFactory
 from .accounts import (BootstrapSignerController, CSRApprovingController, CSRCleanerController, CSRSigningController,
+                       GroupCSRApprovingController, WebhookSigningController,
                        ServiceAccountsController, TokenCleanerController, TokensController)
 from .apps import CronJobController, ReplicationManager, StatefulSetController
 from .autoscaling import HorizontalPodAutoscalerController
@@ -108,10 +109,15 @@ ALL = {
     "cloud-node": lambda mgr, o: CloudNodeController(mgr, o.cloud, o.extra.get("node_status_update_frequency", 300.0),
                                                      o.extra.get("node_monitor_period", 5.0)),
     "persistentvolume-labeler": lambda mgr, o: PersistentVolumeLabelController(mgr, o.cloud),
+    # gke-certificates-controller only (cmd/gke-certificates-controller/app)
+    "csrsigning-webhook": lambda mgr, o: WebhookSigningController(mgr, o.extra["signing_kubeconfig"],
+                                                                  o.extra.get("signing_retry_backoff", 0.5)),
+    "csrapproving-group": lambda mgr, o: GroupCSRApprovingController(mgr, o.extra["approve_group"]),
 }
 DISABLED_BY_DEFAULT = {"bootstrapsigner", "tokencleaner"}
 CLOUD_CONTROLLERS = ["cloud-node", "service", "route", "persistentvolume-labeler"]
-OPT_IN = DISABLED_BY_DEFAULT | {"nodeipam", "service", "route", "cloud-node", "persistentvolume-labeler"}
+OPT_IN = DISABLED_BY_DEFAULT | {"nodeipam", "service", "route", "cloud-node", "persistentvolume-labeler",
+                                "csrsigning-webhook", "csrapproving-group"}
 
 
 def default_controllers(opts: Options) -> list[str]:

@@ -248,6 +248,81 @@ class CSRSigningController(Controller):
         await self.client.update(csr, sub="status")
 
 
+class WebhookSigningController(Controller):
+    """cmd/gke-certificates-controller gke_signer.go: approved CSRs are POSTed (certificates.k8s.io/
+    v1beta1 JSON) to the signing service a kubeconfig names; its answer's status.certificate is
+    written back through the status subresource. Retries back off exponentially from
+    --cluster-signing-gke-retry-backoff; a failure is a Warning SigningError event and a requeue."""
+    name = "csrsigning-webhook"
+    workers = 1
+
+    def __init__(self, mgr, kubeconfig: str, retry_backoff: float = 0.5, attempts: int = 5):
+        super().__init__(mgr)
+        self.kubeconfig, self.retry_backoff, self.attempts = kubeconfig, retry_backoff, attempts
+        self._hook = None
+
+    def setup(self):
+        self.csr_inf = self.mgr.factory.informer("certificatesigningrequests")
+        self.csr_inf.add_handler(on_add=self.enqueue, on_update=lambda o, n: self.enqueue(n))
+
+    async def stop(self):
+        if self._hook is not None:
+            await self._hook.close()
+        await super().stop()
+
+    async def _sign(self, csr: dict) -> str:
+        from ..apiserver.authx import _webhook_client
+        if self._hook is None:
+            self._hook = _webhook_client(self.kubeconfig)
+        body = {**csr, "apiVersion": "certificates.k8s.io/v1beta1", "kind": "CertificateSigningRequest"}
+        delay, last = self.retry_backoff, None
+        for attempt in range(self.attempts):
+            try:
+                out = await self._hook.request("POST", "", body=body)
+                cert = ((out or {}).get("status") or {}).get("certificate")
+                if not cert:
+                    raise RuntimeError("the signing service answered without status.certificate")
+                return cert
+            except m.StatusError as e:
+                last = RuntimeError(f"server responded with error: {e}")
+                if e.code < 500 and e.code != 429:
+                    break           # a rejection: retrying will not help
+            except Exception as e:  # noqa: BLE001 — connection errors are retried
+                last = e
+            if attempt + 1 < self.attempts:
+                await asyncio.sleep(delay)
+                delay *= 2
+        raise last
+
+    async def sync(self, key):
+        _, name = split_key(key)
+        csr = self.csr_inf.get(name)
+        if csr is None or not _condition(csr, "Approved") or (csr.get("status") or {}).get("certificate"):
+            return
+        try:
+            cert = await self._sign(csr)
+        except Exception as e:
+            rec = getattr(self.mgr, "recorder", None)
+            if rec is not None:
+                rec.event(csr, "Warning", "SigningError", f"error while calling GKE: {e}")
+            raise
+        csr = dict(csr, status=dict(csr.get("status") or {}, certificate=cert))
+        await self.client.update(csr, sub="status")
+
+
+class GroupCSRApprovingController(CSRApprovingController):
+    """--insecure-experimental-approve-all-kubelet-csrs-for-group: every kubelet client CSR from a
+    member of the group is approved without a SubjectAccessReview (gke-certificates-controller)."""
+    name = "csrapproving-group"
+
+    def __init__(self, mgr, group: str):
+        super().__init__(mgr)
+        self.group = group
+
+    async def _allowed(self, spec, subresource) -> bool:
+        return self.group in (spec.get("groups") or [])
+
+
 class CSRCleanerController(Controller):
     name = "csrcleaner"
     workers = 1
