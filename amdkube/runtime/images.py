@@ -9,7 +9,7 @@ Two kinds of image:
   * scratch — a named, versioned entrypoint on the host: a native binary, a script, or a
     directory with a `run` file (no registry access on the target machines). Built-in images
 map the e2e workloads to amdkube's gfx950 binaries (the reference's cuda-vector-add image,
-test/images/cuda-vector-add, becomes `rocm/vector-add`). Extra images are registered from
+test/images/cuda-vector-add, becomes `rocm/vector-add`, the HSA build; `rocm/vector-add-hip` is the HIP one). Extra images are registered from
 `images.json` in the runtime's state dir or via PullImage of a local path (`file:///...`).
 
 A registry directory (`rocshim --registry-dir`) stands in for remote registries:
@@ -41,7 +41,11 @@ def builtin_images() -> dict[str, dict]:
     sh = shutil.which("sh") or "/bin/sh"
     return {
         "amdkube/pause:3.1": {"entrypoint": [_b("pause")]},
-        "rocm/vector-add:latest": {"entrypoint": [_b("rocm-vector-add")]},
+        # the GPU-pod workload runs on the bare ROCr runtime (kernels/hsa_vector_add.cpp: 250 ms
+        # per pod on MI355X against 320 ms for the HIP build); the HIP build stays available
+        "rocm/vector-add:latest": {"entrypoint": [_b("hsa-vector-add")]},
+        "amdkube/hsa-vector-add:latest": {"entrypoint": [_b("hsa-vector-add")]},
+        "rocm/vector-add-hip:latest": {"entrypoint": [_b("rocm-vector-add")]},
         "amdkube/rocm-vector-add:latest": {"entrypoint": [_b("rocm-vector-add")]},
         "amdkube/hbm-probe:latest": {"entrypoint": [_b("hbm-probe")]},
         "amdkube/gpu-burn:latest": {"entrypoint": [_b("gpu-burn")]},

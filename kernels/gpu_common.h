@@ -123,6 +123,13 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ v4u ld_nt(const v4u* p) { return __builtin_nontemporal_load(p); }
 __device__ __forceinline__ void st_nt(v4u* p, v4u v) { __builtin_nontemporal_store(v, p); }
 
+// Pure writes go out with the default cache policy: on MI355X plain 16-B stores stream at
+// 6.0-6.1 TB/s against 5.5-5.8 non-temporal (hack/exp/copy_sweep2.hip, 1 and 4 GiB), best at
+// 16 WG/CU for a 1 GiB buffer. Copies keep nt on both sides and run 128 WG/CU (5.72 / 5.80 TB/s
+// on 1 / 4 GiB against 5.39 / 5.79 at 64).
+constexpr int HBM_WRITE_BLOCKS_PER_CU = 16;
+__device__ __forceinline__ void st_plain(v4u* p, v4u v) { *p = v; }
+
 __device__ __forceinline__ v4u pattern_v(size_t i, uint32_t seed) {
   uint4 p = pattern(i, seed);
   return v4u{p.x, p.y, p.z, p.w};
@@ -143,9 +150,9 @@ __global__ __launch_bounds__(256) void hbm_write_kernel(v4u* __restrict__ buf, s
   size_t i = lo + threadIdx.x;
   for (; i + (HBM_UNROLL - 1) * b < hi; i += HBM_UNROLL * b) {
 #pragma unroll
-    for (int u = 0; u < HBM_UNROLL; ++u) st_nt(buf + i + u * b, pattern_v(i + u * b, seed));
+    for (int u = 0; u < HBM_UNROLL; ++u) st_plain(buf + i + u * b, pattern_v(i + u * b, seed));
   }
-  for (; i < hi; i += b) st_nt(buf + i, pattern_v(i, seed));
+  for (; i < hi; i += b) st_plain(buf + i, pattern_v(i, seed));
 }
 
 __device__ __forceinline__ unsigned mismatches(v4u v, v4u e) {
@@ -195,7 +202,7 @@ __global__ __launch_bounds__(256) void hbm_read_kernel(const v4u* __restrict__ b
 // grid-stride interleave; 64 workgroups/CU. Round-3 sweep on MI355X (hack/exp/copy_sweep.hip,
 // 2 x 4 GiB): grid-stride 32/CU 5.01 TB/s, grid-stride 64/CU 5.20, chunked 64/CU 5.53,
 // hipMemcpyDtoD 4.70.
-constexpr int HBM_COPY_BLOCKS_PER_CU = 64;
+constexpr int HBM_COPY_BLOCKS_PER_CU = 128;
 
 __global__ __launch_bounds__(256) void hbm_copy_kernel(const v4u* __restrict__ src, v4u* __restrict__ dst,
                                                        size_t n16) {
@@ -355,7 +362,7 @@ inline std::vector<float> vector_add_host(const std::vector<float>& a, const std
 inline std::vector<uint32_t> hbm_pattern_host(size_t n16, uint32_t seed, int dev) {
   AK_HIP(hipSetDevice(dev));
   DevBuf d(n16 * 16);
-  const int grid = stream_grid(n16, dev_info(dev).cu_count, HBM_BLOCKS_PER_CU);
+  const int grid = stream_grid(n16, dev_info(dev).cu_count, HBM_WRITE_BLOCKS_PER_CU);
   hipLaunchKernelGGL(hbm_write_kernel, dim3(grid), dim3(256), 0, 0, static_cast<v4u*>(d.p), n16, seed);
   AK_HIP(hipGetLastError());
   std::vector<uint32_t> out(n16 * 4);
@@ -455,7 +462,8 @@ inline HbmResult run_hbm_probe(size_t bytes, int iters, int dev, uint32_t seed =
     AK_HIP(hipEventElapsedTime(&ms, e0, e1));
     return static_cast<double>(ms) / iters;
   };
-  double w = timed([&] { hipLaunchKernelGGL(hbm_write_kernel, dim3(grid), dim3(256), 0, 0, a, n16, seed); });
+  const int write_grid = stream_grid(n16, info.cu_count, HBM_WRITE_BLOCKS_PER_CU);
+  double w = timed([&] { hipLaunchKernelGGL(hbm_write_kernel, dim3(write_grid), dim3(256), 0, 0, a, n16, seed); });
   double rd = timed([&] { hipLaunchKernelGGL(hbm_read_kernel, dim3(grid), dim3(256), 0, 0, a, n16, sink); });
   const int copy_grid = stream_grid(n16, info.cu_count, HBM_COPY_BLOCKS_PER_CU);
   double cp = timed([&] { hipLaunchKernelGGL(hbm_copy_kernel, dim3(copy_grid), dim3(256), 0, 0, a, b, n16); });

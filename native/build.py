@@ -6,7 +6,7 @@
                                     # and the ThreadSanitizer build of the activity sampler
 
 Outputs: amdkube/_native/{_amdsmi,_topo,_hipops}.<ext> and amdkube/_native/bin/{pause,
-rocm-vector-add,hbm-probe,gpu-burn,xgmi-probe[,topo-selftest-asan,pause-asan,amdkube-nsexec-asan,
+rocm-vector-add,hsa-vector-add,hbm-probe,gpu-burn,xgmi-probe[,topo-selftest-asan,pause-asan,amdkube-nsexec-asan,
 seccomp-check-asan,sampler-selftest-{asan,tsan}]}.
 Targets are rebuilt only when a source/header is newer than the output.
 """
@@ -92,6 +92,13 @@ def targets(sanitize=False, cpu_only=False):
             (n(OUT, "_hipops" + EXT), [n("native/hipops.hip"), hdr],
              [*ho, "-shared", "-fPIC", *py, n("native/hipops.hip"), "-o", "{out}"]),
             (n(BIN, "rocm-vector-add"), [n("kernels/vector_add.hip"), hdr], [*ho, n("kernels/vector_add.hip"), "-o", "{out}"]),
+            # the HIP-free pod workload: a bare gfx950 code object, then the HSA host embedding it
+            (n(BIN, "hsa-vector-add"), [n("kernels/hsa_vector_add.cpp"), n("kernels/vadd_kernel.hip")],
+             ["sh", "-c", f'"$0" --offload-arch={ARCH} -O3 --offload-device-only --no-gpu-bundle-output -c '
+              f'{n("kernels/vadd_kernel.hip")} -o {n(OUT, "lib", "vadd_" + ARCH + ".co")} && '
+              f'g++ -O2 -std=c++17 -Wall -DVADD_CO_PATH=\\"{n(OUT, "lib", "vadd_" + ARCH + ".co")}\\" '
+              f'-I{ROCM}/include {n("kernels/hsa_vector_add.cpp")} -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lhsa-runtime64 -o "$1"',
+              hip, "{out}"]),
             (n(BIN, "hbm-probe"), [n("kernels/hbm_probe.hip"), hdr], [*ho, n("kernels/hbm_probe.hip"), "-o", "{out}"]),
             (n(BIN, "gpu-burn"), [n("kernels/gpu_burn.hip"), hdr], [*ho, n("kernels/gpu_burn.hip"), "-o", "{out}"]),
             (n(BIN, "xgmi-probe"), [n("kernels/xgmi_probe.cpp")],

@@ -496,6 +496,23 @@ def test_04_probe_binaries():
     assert r.returncode == 0 and json.loads(r.stdout)["bf16_tflops"] > 500, r.stdout
 
 
+def test_04b_hsa_vector_add_matches_the_hip_build():
+    """The pod workload on the bare ROCr runtime (AQL dispatch of the embedded gfx950 code
+    object): every element checked on the host for ragged sizes, and the same device identity
+    (UUID, PCI bus, ISA) as the HIP build reports."""
+    def run_one(binary, *args):
+        r = subprocess.run([os.path.join(BIN, binary), "--json", *args], capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0 and "Test PASSED" in r.stdout, (binary, args, r.stdout, r.stderr)
+        return json.loads(next(x for x in r.stdout.splitlines() if x.startswith("{")))
+    hip_id = run_one("rocm-vector-add")
+    for n in ("50000", "50001", "7", "1", "1048579"):
+        d = run_one("hsa-vector-add", "-n", n)
+        assert d["ok"] and d["runtime"] == "hsa" and d["n"] == int(n)
+        assert (d["uuid"], d["bus"], d["arch"]) == (hip_id["uuid"], hip_id["bus"], hip_id["arch"]), (d, hip_id)
+    r = subprocess.run([os.path.join(BIN, "hsa-vector-add"), "--expect-devices", "2"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 3 and "expected 2 visible GPU(s), found 1" in r.stderr
+
+
 # --- in-process HIP from here on (no process spawning after this point) -------------------
 def test_90_hip_vector_add_matches_fp32_reference():
     from amdkube.ops import hip
