@@ -22,6 +22,8 @@ fork's README names EC2 and GCP GPU VMs next to on-prem DGX hosts. An MI355X nod
 """
 from __future__ import annotations
 
+import asyncio
+import functools
 import ipaddress
 import logging
 import os
@@ -32,6 +34,16 @@ from dataclasses import dataclass
 from ..api import meta as m
 
 log = logging.getLogger("amdkube.cloudprovider")
+
+
+def off_loop(fn):
+    """The public-cloud providers speak blocking HTTP (`requests`): their Instances methods are
+    awaited by the kubelet and the cloud controllers, so each call runs in a worker thread
+    instead of stalling the event loop for a slow cloud API."""
+    @functools.wraps(fn)
+    async def wrapper(*a, **kw):
+        return await asyncio.to_thread(fn, *a, **kw)
+    return wrapper
 
 
 @dataclass(frozen=True)

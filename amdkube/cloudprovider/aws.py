@@ -40,7 +40,7 @@ import time
 import xml.etree.ElementTree as ET
 from urllib.parse import quote, urlsplit
 
-from . import Interface, Route, Zone
+from . import Interface, Route, Zone, off_loop
 from ..api import meta as m
 
 log = logging.getLogger("amdkube.cloudprovider.aws")
@@ -313,27 +313,32 @@ class Instances:
             raise
         return got[0] if got else None
 
-    async def node_addresses(self, name: str) -> list[dict]:
+    @off_loop
+    def node_addresses(self, name: str) -> list[dict]:
         return node_addresses(self.by_name(name))
 
-    async def node_addresses_by_provider_id(self, pid: str) -> list[dict]:
+    @off_loop
+    def node_addresses_by_provider_id(self, pid: str) -> list[dict]:
         inst = self.by_id(instance_id_from_provider_id(pid))
         if inst is None:
             raise LookupError(f"instance not found: {pid}")
         return node_addresses(inst)
 
-    async def instance_exists(self, name: str) -> bool:
+    @off_loop
+    def instance_exists(self, name: str) -> bool:
         try:
             self.by_name(name)
             return True
         except LookupError:
             return False
 
-    async def instance_exists_by_provider_id(self, pid: str) -> bool:
+    @off_loop
+    def instance_exists_by_provider_id(self, pid: str) -> bool:
         inst = self.by_id(instance_id_from_provider_id(pid))
         return inst is not None and (inst.get("instanceState") or {}).get("name") != "terminated"
 
-    async def instance_id(self, name: str) -> str:
+    @off_loop
+    def instance_id(self, name: str) -> str:
         inst = self.by_name(name)
         return f"/{_az(inst)}/{inst['instanceId']}"
 
@@ -341,7 +346,8 @@ class Instances:
         inst = self.by_name(name)
         return f"aws:///{_az(inst)}/{inst['instanceId']}"
 
-    async def instance_type(self, name: str) -> str:
+    @off_loop
+    def instance_type(self, name: str) -> str:
         return self.by_name(name).get("instanceType", "")
 
 

@@ -36,7 +36,7 @@ import re
 import threading
 import time
 
-from . import Interface, Route, Zone
+from . import Interface, Route, Zone, off_loop
 from ..api import meta as m
 
 log = logging.getLogger("amdkube.cloudprovider.azure")
@@ -192,30 +192,42 @@ class Instances:
             pub = (pip.get("properties") or {}).get("ipAddress", "")
         return props.get("privateIPAddress", ""), pub
 
-    async def node_addresses(self, name: str) -> list[dict]:
+    @off_loop
+    def node_addresses(self, name: str) -> list[dict]:
+        return self._addresses(name)
+
+    def _addresses(self, name: str) -> list[dict]:
         priv, pub = self.ips(name)
         out = [{"type": "InternalIP", "address": priv}, {"type": "Hostname", "address": name}]
         if pub:
             out.append({"type": "ExternalIP", "address": pub})
         return out
 
-    async def node_addresses_by_provider_id(self, pid: str) -> list[dict]:
-        return await self.node_addresses(node_name_from_provider_id(pid))
+    @off_loop
+    def node_addresses_by_provider_id(self, pid: str) -> list[dict]:
+        return self._addresses(node_name_from_provider_id(pid))
 
-    async def instance_exists(self, name: str) -> bool:
+    @off_loop
+    def instance_exists(self, name: str) -> bool:
+        return self._exists(name)
+
+    def _exists(self, name: str) -> bool:
         try:
             self.vm(name)
             return True
         except LookupError:
             return False
 
-    async def instance_exists_by_provider_id(self, pid: str) -> bool:
-        return await self.instance_exists(node_name_from_provider_id(pid))
+    @off_loop
+    def instance_exists_by_provider_id(self, pid: str) -> bool:
+        return self._exists(node_name_from_provider_id(pid))
 
-    async def instance_id(self, name: str) -> str:
+    @off_loop
+    def instance_id(self, name: str) -> str:
         return self.vm(name)["id"]
 
-    async def instance_type(self, name: str) -> str:
+    @off_loop
+    def instance_type(self, name: str) -> str:
         return ((self.vm(name).get("properties") or {}).get("hardwareProfile") or {}).get("vmSize", "")
 
 

@@ -33,7 +33,7 @@ import re
 import threading
 import time
 
-from . import Interface, Route, Zone
+from . import Interface, Route, Zone, off_loop
 from ..api import meta as m
 
 log = logging.getLogger("amdkube.cloudprovider.gce")
@@ -197,7 +197,8 @@ class Instances:
     def _is_self(self, name: str) -> bool:
         return self.gce.self_name and canonical_instance_name(name) == self.gce.self_name
 
-    async def node_addresses(self, name: str) -> list[dict]:
+    @off_loop
+    def node_addresses(self, name: str) -> list[dict]:
         if self._is_self(name):
             out = [{"type": "InternalIP", "address": self.gce.md.get("instance/network-interfaces/0/ip").strip()}]
             try:
@@ -209,18 +210,21 @@ class Instances:
             return out
         return addresses_of(self.get(name))
 
-    async def node_addresses_by_provider_id(self, pid: str) -> list[dict]:
+    @off_loop
+    def node_addresses_by_provider_id(self, pid: str) -> list[dict]:
         project, zone, name = split_provider_id(pid)
         return addresses_of(self.gce.client.call("GET", f"projects/{project}/zones/{zone}/instances/{name}"))
 
-    async def instance_exists(self, name: str) -> bool:
+    @off_loop
+    def instance_exists(self, name: str) -> bool:
         try:
             self.get(name)
             return True
         except LookupError:
             return False
 
-    async def instance_exists_by_provider_id(self, pid: str) -> bool:
+    @off_loop
+    def instance_exists_by_provider_id(self, pid: str) -> bool:
         project, zone, name = split_provider_id(pid)
         try:
             self.gce.client.call("GET", f"projects/{project}/zones/{zone}/instances/{name}")
@@ -230,11 +234,13 @@ class Instances:
                 return False
             raise
 
-    async def instance_id(self, name: str) -> str:
+    @off_loop
+    def instance_id(self, name: str) -> str:
         inst = self.get(name)
         return f"{self.gce.project}/{inst['zone']}/{inst['name']}"
 
-    async def instance_type(self, name: str) -> str:
+    @off_loop
+    def instance_type(self, name: str) -> str:
         return _last(self.get(name).get("machineType", ""))
 
 
