@@ -545,6 +545,25 @@ def gke_certificates_controller(argv):
     _run_forever(mk)
 
 
+def rktshim(argv):
+    """CRI over rkt (pkg/kubelet/rkt, pkg/kubelet/rktshim): point the kubelet's
+    --container-runtime-endpoint at --listen to run pods as rkt pods."""
+    ap = argparse.ArgumentParser("amdkube rktshim")
+    ap.add_argument("--listen", default="/var/run/amdkube/rktshim.sock")
+    ap.add_argument("--state-dir", default="/var/lib/amdkube/rktshim")
+    ap.add_argument("--rkt-path", default="rkt", help="the rkt binary (with any global flags, e.g. '--dir=…')")
+    ap.add_argument("--insecure-options", default="image", help="rkt fetch --insecure-options")
+    ap.add_argument("--node-ip", default="127.0.0.1")
+    ap.add_argument("-v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "rktshim")
+    from ..runtime.rktshim import RktShim
+
+    async def mk():
+        return await RktShim(a.listen, a.state_dir, rkt=a.rkt_path, insecure_options=a.insecure_options, node_ip=a.node_ip).start()
+    _run_forever(mk)
+
+
 def kubelet(argv):
     ap = argparse.ArgumentParser("amdkube kubelet")
     ap.add_argument("--api-servers", "--server", dest="server", default="http://127.0.0.1:8080")
@@ -1120,6 +1139,6 @@ COMPONENTS = {"etcd": etcd, "dns": dns, "kube-dns": dns, "kubeadm": kubeadm, "pr
               "rocshim": rocshim, "amd-device-plugin": device_plugin, "device-plugin": device_plugin,
               "amdgpu-exporter": exporter, "exporter": exporter, "hollow-node": hollow_node, "local-up": local_up,
               "metrics-server": metrics_server, "cloud-controller-manager": cloud_controller_manager,
-              "gke-certificates-controller": gke_certificates_controller}
+              "gke-certificates-controller": gke_certificates_controller, "rktshim": rktshim}
 from .gendocs import GENERATORS as _GENERATORS  # noqa: E402  (gendocs/genkubedocs/genman/genyaml)
 COMPONENTS.update(_GENERATORS)

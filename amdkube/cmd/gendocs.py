@@ -112,6 +112,7 @@ COMPONENT_SYNOPSIS = {
     "local-up": "Starts a single-node cluster on this host (local-up-cluster).",
     "metrics-server": "Serves metrics.k8s.io node and pod metrics from kubelet summaries.",
     "gke-certificates-controller": "Signs approved certificate signing requests through an external signing webhook.",
+    "rktshim": "CRI runtime that runs pods as rkt pods through the rkt command line.",
     "rocshim": "The CRI runtime: pause sandboxes and process containers with only their GPUs' device nodes.",
 }
 

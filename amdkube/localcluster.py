@@ -30,7 +30,7 @@ class LocalCluster:
                  node_status_update_frequency: float = 10.0, scheduler_kw: dict | None = None, isolation: str | None = None,
                  health_probe: str = "none", kubelet_kw: dict | None = None, with_kubelet: bool = True,
                  partition: str | None = None, resource_naming: str = "single", api_kw: dict | None = None,
-                 controllers_kw: dict | None = None, shim_kw: dict | None = None):
+                 controllers_kw: dict | None = None, shim_kw: dict | None = None, runtime: str = "rocshim"):
         self.gpus, self.n_gpus, self.node_name = gpus, n_gpus, node_name
         self.partition, self.resource_naming = partition, resource_naming
         self.plugins: list = []
@@ -47,6 +47,7 @@ class LocalCluster:
         self.health_probe = health_probe
         self.with_kubelet = with_kubelet
         self.api_kw, self.controllers_kw, self.shim_kw = api_kw or {}, controllers_kw or {}, shim_kw or {}
+        self.runtime = runtime        # "rocshim" (default) or "rkt" (runtime/rktshim.py; shim_kw: rkt=…)
         self.api = self.client = self.scheduler = self.controllers = self.shim = self.plugin = self.kubelet = None
         self.backend = None
 
@@ -60,8 +61,12 @@ class LocalCluster:
             self.controllers = await ControllerManager(Client(self.api.url, token=self.api.loopback_token), **self.controllers_kw).start()
         if not self.with_kubelet:
             return self
-        self.shim = await RocShim(os.path.join(b, "rocshim.sock"), os.path.join(b, "rocshim"),
-                                  hooks_dir=os.path.join(b, "hooks.d"), isolation=self.isolation, **self.shim_kw).start()
+        if self.runtime == "rkt":
+            from .runtime.rktshim import RktShim
+            self.shim = await RktShim(os.path.join(b, "rocshim.sock"), os.path.join(b, "rktshim"), **self.shim_kw).start()
+        else:
+            self.shim = await RocShim(os.path.join(b, "rocshim.sock"), os.path.join(b, "rocshim"),
+                                      hooks_dir=os.path.join(b, "hooks.d"), isolation=self.isolation, **self.shim_kw).start()
         if self.gpus != "none":
             self.backend = open_backend(self.gpus, n=self.n_gpus, partition=self.partition)
             self.plugins = make_plugins(self.backend, self.resource_naming, plugins_dir=os.path.join(b, "plugins"),
