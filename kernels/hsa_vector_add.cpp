@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstddef>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -183,10 +184,9 @@ Kernel kernel(hsa_executable_t exe, hsa_agent_t gpu, const char* name) {
   return k;
 }
 
-// One AQL kernel-dispatch packet over `items` work-items (rounded up to whole work-groups),
-// with the barrier bit so packets on the queue run in order; system-scope fences both sides.
-void dispatch(hsa_queue_t* q, const Kernel& k, void* kargs, uint64_t items, hsa_signal_t completion) {
-  const uint64_t groups = (items + kWG - 1) / kWG;
+// One AQL kernel-dispatch packet of `groups` work-groups, with the barrier bit so packets on
+// the queue run in order; system-scope fences both sides.
+void dispatch(hsa_queue_t* q, const Kernel& k, void* kargs, uint64_t groups, hsa_signal_t completion) {
   if (groups == 0 || groups * kWG > UINT32_MAX) throw Fail{"bad dispatch size", HSA_STATUS_ERROR};
   const uint64_t idx = hsa_queue_add_write_index_screlease(q, 1);
   while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {
@@ -211,18 +211,27 @@ void dispatch(hsa_queue_t* q, const Kernel& k, void* kargs, uint64_t items, hsa_
   hsa_signal_store_screlease(q->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
 }
 
-struct CopyArgs {  // amdkube_copy: src, dst, float count
+struct CopyArgs {  // amdkube_copy: src, dst, float count, work-groups launched
   const float* src;
   float* dst;
   unsigned long long n;
+  unsigned groups;
 };
 
-struct Args {  // the kernarg segment of amdkube_vadd: four explicit arguments, 32 bytes
+struct Args {  // amdkube_vadd: a, b, c, float count, work-groups launched
   const float* a;
   const float* b;
   float* c;
   unsigned long long n;
+  unsigned groups;
 };
+
+// the streaming grid: one work-group per 256 16-byte words, at most 64 per CU (gpu_common.h)
+uint32_t stream_groups(uint64_t floats, uint32_t cus) {
+  const uint64_t want = (floats / 4 + kWG - 1) / kWG;
+  const uint64_t cap = static_cast<uint64_t>(cus ? cus : 256) * 64;
+  return static_cast<uint32_t>(want < 1 ? 1 : (want < cap ? want : cap));
+}
 
 }  // namespace
 
@@ -286,7 +295,8 @@ int main(int argc, char** argv) {
     check(hsa_executable_load_agent_code_object(exe, gpu, reader, nullptr, nullptr), "load code object (gfx950 only)");
     check(hsa_executable_freeze(exe, nullptr), "freeze executable");
     const Kernel vadd = kernel(exe, gpu, "amdkube_vadd.kd"), copy = kernel(exe, gpu, "amdkube_copy.kd");
-    if (vadd.kasz < sizeof(Args) || copy.kasz < sizeof(CopyArgs)) throw Fail{"unexpected kernarg segment size", HSA_STATUS_ERROR};
+    if (vadd.kasz != offsetof(Args, groups) + sizeof(unsigned) || copy.kasz != offsetof(CopyArgs, groups) + sizeof(unsigned))
+      throw Fail{"unexpected kernarg segment size", HSA_STATUS_ERROR};
     tr.mark("code object");
 
     // data: host staging (GPU-accessible system memory) and device buffers
@@ -318,17 +328,18 @@ int main(int argc, char** argv) {
     check(hsa_amd_memory_pool_allocate(pools.kernarg, 3 * slot, 0, reinterpret_cast<void**>(&kargs)), "kernarg alloc");
     check(hsa_amd_agents_allow_access(1, &gpu, nullptr, kargs), "kernarg access");
     std::memset(kargs, 0, 3 * slot);
-    *reinterpret_cast<CopyArgs*>(kargs) = CopyArgs{ha, da, 2 * static_cast<unsigned long long>(stride)};
-    *reinterpret_cast<Args*>(kargs + slot) = Args{da, db, dc, static_cast<unsigned long long>(n)};
-    *reinterpret_cast<CopyArgs*>(kargs + 2 * slot) = CopyArgs{dc, hc, static_cast<unsigned long long>(n)};
+    const uint32_t g_in = stream_groups(2 * stride, id.cus), g_add = stream_groups(n, id.cus);
+    *reinterpret_cast<CopyArgs*>(kargs) = CopyArgs{ha, da, 2 * static_cast<unsigned long long>(stride), g_in};
+    *reinterpret_cast<Args*>(kargs + slot) = Args{da, db, dc, static_cast<unsigned long long>(n), g_add};
+    *reinterpret_cast<CopyArgs*>(kargs + 2 * slot) = CopyArgs{dc, hc, static_cast<unsigned long long>(n), g_add};
 
     hsa_queue_t* q = nullptr;
     check(hsa_queue_create(gpu, 64, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &q), "queue");
     tr.mark("queue");
     const auto t0 = std::chrono::steady_clock::now();
-    dispatch(q, copy, kargs, (2 * stride / 4 + 1), hsa_signal_t{0});     // host a,b → device
-    dispatch(q, vadd, kargs + slot, n, hsa_signal_t{0});                 // c = a + b on device memory
-    dispatch(q, copy, kargs + 2 * slot, (n / 4 + 1), done);             // device c → host
+    dispatch(q, copy, kargs, g_in, hsa_signal_t{0});                     // host a,b → device
+    dispatch(q, vadd, kargs + slot, g_add, hsa_signal_t{0});             // c = a + b on device memory
+    dispatch(q, copy, kargs + 2 * slot, g_add, done);                    // device c → host
     wait_zero(done, "vector add");
     const double kernel_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     tr.mark("gpu work");
