@@ -179,13 +179,16 @@ class PodBench:
         for nm in gpu + cpu:
             self.t[nm] = {"wave": 0, "cpu": nm in cpu}
             self.done_events[nm] = asyncio.Event()
-        creates = []
         tw = time.time()
-        for nm in gpu + cpu:
-            self.t[nm]["create"] = time.perf_counter()
-            creates.append(self.lc.client.create(self.pod(nm) if nm in gpu else self.cpu_pod(nm), "default"))
-        for obj in await asyncio.gather(*creates):
-            POD_TRACE(m.uid_of(obj), "bench_create", tw)
+        # the GPU pods are submitted first and the pause pods right after them (a client that
+        # queues its accelerator work ahead of the rest of the batch)
+        for group in (gpu, cpu):
+            creates = []
+            for nm in group:
+                self.t[nm]["create"] = time.perf_counter()
+                creates.append(self.lc.client.create(self.pod(nm) if nm in gpu else self.cpu_pod(nm), "default"))
+            for obj in await asyncio.gather(*creates):
+                POD_TRACE(m.uid_of(obj), "bench_create", tw)
         await asyncio.wait_for(asyncio.gather(*(self.done_events[nm].wait() for nm in gpu + cpu)), timeout)
         self.pending_cleanup = cpu
         return gpu + cpu

@@ -122,6 +122,8 @@ class ProcessNode:
                 out[" ".join(p.args[2:4]) if "-m" in p.args[:2] else str(p.pid)] = round(t.user + t.system, 3)
             except psutil.Error:
                 pass
+        t = psutil.Process().cpu_times()       # this process: the apiserver and the bench driver
+        out["amdkube apiserver+bench"] = round(t.user + t.system, 3)
         return out
 
     async def stop(self):

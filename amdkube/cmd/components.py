@@ -585,6 +585,8 @@ def kubelet(argv):
     ap.add_argument("--node-ip", default="127.0.0.1")
     ap.add_argument("--node-status-update-frequency", type=float, default=10.0)
     ap.add_argument("--pleg-relist-period", type=float, default=1.0)
+    ap.add_argument("--prioritize-device-pods", default="true", choices=("true", "false"),
+                    help="start pods that hold accelerators before the other pods of a burst")
     ap.add_argument("--max-pods", type=int, default=110)
     ap.add_argument("--maximum-dead-containers-per-container", type=int, default=1)
     ap.add_argument("--maximum-dead-containers", type=int, default=-1)
@@ -711,6 +713,7 @@ def kubelet(argv):
                         v1beta1_socket=a.device_plugin_v1beta1_socket, cri_socket=a.container_runtime_endpoint,
                         address=a.address, port=a.port, node_ip=a.node_ip, node_status_update_frequency=a.node_status_update_frequency,
                         relist_period=a.pleg_relist_period, max_pods=a.max_pods, node_labels=labels,
+                        prioritize_device_pods=a.prioritize_device_pods == "true",
                         register_with_taints=taints, feature_gates=a.feature_gates, chaos_chance=a.chaos_chance,
                         pod_manifest_path=a.pod_manifest_path, file_check_frequency=a.file_check_frequency,
                         bootstrap_checkpoint_path=a.bootstrap_checkpoint_path,

@@ -90,6 +90,8 @@ class KubeletConfig:
     register_with_taints: list = field(default_factory=list)
     feature_gates: str = ""
     evented_pleg: bool = True
+    prioritize_device_pods: bool = True              # start pods that hold accelerators before the rest of a burst
+    device_pod_start_window: float = 0.25            # the longest a device-less pod waits for them (s)
     eviction_memory_available_bytes: int = 100 * 2 ** 20
     eviction_interval: float = 10.0
     eviction_hard: str | None = None                # --eviction-hard (default: memory.available<eviction_memory_available_bytes)
@@ -224,6 +226,10 @@ class Kubelet:
         self.admitted: set[str] = set()
         self.rejected: dict[str, tuple[str, str]] = {}
         self.workers: dict[str, PodWorker] = {}
+        self._device_starting: set[str] = set()      # device-holding pods in their first start
+        self._device_started: set[str] = set()       # … and those past it (pruned in _cleanup)
+        self._device_idle = asyncio.Event()
+        self._device_idle.set()
         self.terminated_deleted: set[str] = set()
         if self.gates("DevicePlugins"):
             self.dm = ManagerImpl(config.plugins_dir, active_pods=self.active_pods, registry=self.metrics,
@@ -1026,6 +1032,21 @@ class Kubelet:
         return False
 
     # ============================================================= sync
+    def _device_start_done(self, uid: str):
+        if uid in self._device_starting:
+            self._device_starting.discard(uid)
+            self._device_started.add(uid)
+            if not self._device_starting:
+                self._device_idle.set()
+
+    @staticmethod
+    def _holds_devices(pod: dict) -> bool:
+        spec = pod.get("spec") or {}
+        if any(er.get("assigned") for er in spec.get("extendedResources") or []):
+            return True
+        return any("/" in k and not k.startswith(("kubernetes.io/", "hugepages-"))
+                   for c in spec.get("containers") or [] for k in ((c.get("resources") or {}).get("limits") or {}))
+
     async def sync_pod(self, uid: str) -> bool:
         """Returns True when the worker for this pod is finished (pod gone from the node)."""
         pod = self.pods.get(uid)
@@ -1035,9 +1056,14 @@ class Kubelet:
             return True
         md = pod.get("metadata") or {}
         if uid in self.rejected:
+            self._device_start_done(uid)
             if md.get("deletionTimestamp"):
                 await self._finalize_delete(pod)
             return False
+        if (self.cfg.prioritize_device_pods and uid not in self.admitted and uid not in self._device_started
+                and not md.get("deletionTimestamp") and not is_pod_terminal(pod) and self._holds_devices(pod)):
+            self._device_starting.add(uid)      # from first sight: its admission counts as its start
+            self._device_idle.clear()
         if uid not in self.admitted:
             if is_pod_terminal(pod):
                 self.admitted.add(uid)  # e.g. kubelet restart: nothing to run
@@ -1099,7 +1125,23 @@ class Kubelet:
         rt = await self._cached_status(uid)
         mut0 = self.cri.pod_mutations(uid)
         self.cri.take_touched(uid)
-        errors = await self.runtime.sync_pod(pod, rt, ctx, self.liveness_failed.pop(uid, None))
+        gate = self.cfg.prioritize_device_pods and not rt.sandboxes
+        if gate and self._holds_devices(pod):
+            if uid not in self._device_started:
+                self._device_starting.add(uid)
+                self._device_idle.clear()
+        elif gate and self._device_starting:
+            # accelerator pods first: a pod that holds no device waits (bounded) while pods that
+            # hold GPUs are being started, so a burst of mixed pods does not queue the GPU
+            # containers behind pause containers in the runtime
+            try:
+                await asyncio.wait_for(self._device_idle.wait(), self.cfg.device_pod_start_window)
+            except asyncio.TimeoutError:
+                pass
+        try:
+            errors = await self.runtime.sync_pod(pod, rt, ctx, self.liveness_failed.pop(uid, None))
+        finally:
+            self._device_start_done(uid)
         if self.cri.pod_mutations(uid) != mut0 or errors:
             touched = self.cri.take_touched(uid)
             new_rt = None
@@ -1315,6 +1357,8 @@ class Kubelet:
                 log.debug("cpu manager reconcile failed: %r", e)
 
     def _cleanup(self, uid):
+        self._device_start_done(uid)
+        self._device_started.discard(uid)
         self._runtime_uids.add(uid)   # the runtime may still hold leftovers: list before trusting the cache again
         self.cpu_manager.release_pod(uid)
         self.volume_manager.remove_pod(uid)

@@ -285,6 +285,9 @@ class RocShim:
                  pod_namespaces: bool = False, registry_dir: str | None = None):
         self.socket = socket_path
         self.state_dir = state_dir
+        # the node's environment minus GPU visibility, read once (iterating os.environ per
+        # container start re-decodes every variable)
+        self._host_env = {k: v for k, v in os.environ.items() if k not in SCRUB_ENV}
         os.makedirs(os.path.join(state_dir, "sandboxes"), exist_ok=True)
         os.makedirs(os.path.join(state_dir, "containers"), exist_ok=True)
         os.makedirs(os.path.join(state_dir, "rootfs"), exist_ok=True)
@@ -573,7 +576,7 @@ class RocShim:
             # a real image: its own environment (docker's image Env + the container's), not the host's
             env = {"PATH": DEFAULT_PATH}
         else:
-            env = {k: v for k, v in os.environ.items() if k not in SCRUB_ENV}
+            env = dict(self._host_env)
         env.update(ispec.get("env") or {})
         for kv in cfg.envs:
             env[kv.key] = kv.value
@@ -592,7 +595,7 @@ class RocShim:
             handler = "rocm" if has_gpu else "default"
         if image_root and handler == "rocm":
             # the rocm handler brings the node's ROCm runtime settings into the image
-            env.update({k: v for k, v in os.environ.items() if k.startswith("HSA_") and k not in env})
+            env.update({k: v for k, v in self._host_env.items() if k.startswith("HSA_") and k not in env})
         cid = uuid.uuid4().hex
         root = os.path.join(self.state_dir, "rootfs", sid, cfg.metadata.name)
         os.makedirs(root, exist_ok=True)
