@@ -20,7 +20,7 @@ import time
 from ..api import meta as m
 from ..api.labels import selector_from_label_selector
 from ..api.quantity import Quantity
-from .admission import CONNECT, CREATE, DELETE, UPDATE, Plugin
+from .admission import CONNECT, CREATE, UPDATE, Plugin
 
 log = logging.getLogger("amdkube.admission")
 

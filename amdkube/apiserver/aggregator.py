@@ -20,14 +20,13 @@ works without a service proxy on the control-plane host.
 from __future__ import annotations
 
 import asyncio
-import json
 import logging
 import ssl
 
 from aiohttp import ClientSession, ClientTimeout, web
 
 from ..api import meta as m
-from ..api.scheme import SCHEME, _version_sort
+from ..api.scheme import SCHEME
 from ..utils import wait_event
 
 log = logging.getLogger("amdkube.aggregator")

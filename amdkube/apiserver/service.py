@@ -16,7 +16,6 @@ Allocation and the store write happen in one event-loop step, so two creates can
 from __future__ import annotations
 
 import ipaddress
-import json
 import random
 
 from ..api import meta as m

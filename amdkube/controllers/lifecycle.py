@@ -15,7 +15,7 @@ import time
 from ..api import meta as m
 from ..api.helpers import get_condition, is_pod_terminal, tolerations_tolerate_taint
 from ..api.scheme import SCHEME
-from .base import Controller, split_key
+from .base import Controller
 
 UNREACHABLE_TAINT = {"key": "node.kubernetes.io/unreachable", "effect": "NoExecute"}
 NOT_READY_TAINT = {"key": "node.kubernetes.io/not-ready", "effect": "NoExecute"}

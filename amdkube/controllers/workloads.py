@@ -15,7 +15,7 @@ import time
 
 from ..api import meta as m
 from ..api.helpers import find_untolerated_taint, get_condition, is_pod_ready, is_pod_terminal
-from ..api.labels import node_requirements_as_selector, selector_from_label_selector
+from ..api.labels import node_requirements_as_selector
 from .base import Controller, split_key
 
 

@@ -19,7 +19,6 @@ amdkube differences (latency-driven, SURVEY §6 north star):
 from __future__ import annotations
 
 import asyncio
-import base64
 import json
 import logging
 import os

@@ -8,7 +8,6 @@ the runtime's streaming server, server.go:296-330 with redirect-container-stream
 from __future__ import annotations
 
 import asyncio
-import json
 import os
 import time
 

@@ -52,7 +52,7 @@ import grpc
 from ..grpcdesc.cri import API_VERSION, CRI as C, EVENT_TRAILER
 from .hooks import DEFAULT_HOOKS_DIR, HookService
 from .images import NATIVE_BIN, ImageStore
-from .network import HostNetwork, NetworkError
+from .network import HostNetwork
 
 log = logging.getLogger("amdkube.rocshim")
 

@@ -16,7 +16,6 @@ may hold both (as one migrating between media types does).
 """
 from __future__ import annotations
 
-import asyncio
 import json
 from typing import Callable
 
