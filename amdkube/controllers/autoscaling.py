@@ -157,14 +157,16 @@ class CustomMetricsAPI:
         self.client = client
 
     async def pod_metric(self, ns: str, metric: str, selector: str) -> dict[str, float]:
-        d = await self.client.request("GET", f"/apis/{CMG}/namespaces/{ns}/pods/*/{metric}",
+        d = await self.client.request("GET", f"/apis/{CMG}/namespaces/{_seg(ns)}/pods/*/{_seg(metric)}",
                                       params={"labelSelector": selector} if selector else None)
         return {(it.get("describedObject") or {}).get("name"): _num(it.get("value"))
                 for it in (d or {}).get("items") or []}
 
     async def object_metric(self, ns: str, target: dict, metric: str) -> float:
         plural = OBJECT_PLURALS.get(target.get("kind"), (target.get("kind") or "").lower() + "s")
-        d = await self.client.request("GET", f"/apis/{CMG}/namespaces/{ns}/{plural}/{target.get('name')}/{metric}")
+        # every segment comes from the HPA's spec: quoted so none can step out of the metrics API
+        d = await self.client.request("GET", f"/apis/{CMG}/namespaces/{_seg(ns)}/{_seg(plural)}/{_seg(target.get('name') or '')}/"
+                                             f"{_seg(metric)}")
         items = (d or {}).get("items") or []
         if not items:
             raise LookupError(f"no value for {metric} of {target.get('kind')}/{target.get('name')}")
@@ -172,6 +174,15 @@ class CustomMetricsAPI:
 
 
 CMG = "custom.metrics.k8s.io/v1beta1"
+
+
+def _seg(v: str) -> str:
+    """One URL path segment: '/', '..' and the like cannot change the request's path."""
+    from urllib.parse import quote
+    v = str(v)
+    if v in ("", ".", ".."):
+        raise LookupError(f"invalid metric path segment {v!r}")
+    return quote(v, safe="")
 OBJECT_PLURALS = {"Pod": "pods", "Service": "services", "Deployment": "deployments", "Node": "nodes",
                   "Ingress": "ingresses", "ReplicaSet": "replicasets", "StatefulSet": "statefulsets"}
 

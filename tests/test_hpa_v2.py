@@ -251,3 +251,29 @@ async def test_custom_metrics_api_drives_gpu_hpa(tmp_path):
 def test_metrics_server_help_mentions_custom_metrics():
     from amdkube.cmd import components
     assert "custom.metrics.k8s.io" in components.metrics_server.__doc__
+
+
+def test_custom_metrics_paths_stay_inside_the_metrics_api():
+    """Object-metric targets come from the HPA's spec: a name such as '../../api/v1/secrets'
+    must not turn the controller's request into a read of another API path."""
+    import asyncio as _asyncio
+
+    import pytest as _pytest
+
+    from amdkube.controllers.autoscaling import CustomMetricsAPI
+    seen = []
+
+    class C:
+        async def request(self, method, path, **kw):
+            seen.append(path)
+            return {"items": [{"value": "3"}]}
+
+    async def go():
+        api = CustomMetricsAPI(C())
+        assert await api.object_metric("ml", {"kind": "Service", "name": "../../../api/v1/secrets"}, "qps") == 3.0
+        with _pytest.raises(LookupError):
+            await api.object_metric("ml", {"kind": "Service", "name": ".."}, "qps")
+        await api.pod_metric("ml", "gpu/../x", "app=a")
+    _asyncio.run(go())
+    assert seen[0] == "/apis/custom.metrics.k8s.io/v1beta1/namespaces/ml/services/..%2F..%2F..%2Fapi%2Fv1%2Fsecrets/qps"
+    assert seen[1].endswith("/pods/*/gpu%2F..%2Fx")
