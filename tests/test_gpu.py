@@ -296,6 +296,62 @@ def test_06_accelerator_stats_of_a_running_gpu_pod():
     run(go(), 300)
 
 
+def test_06b_hpa_scales_on_mi355x_activity(tmp_path):
+    """The GPU autoscaling path on real hardware: amd-smi duty cycle of a gpu-burn pod →
+    kubelet summary → metrics-server custom.metrics.k8s.io (behind the aggregator) → an
+    autoscaling/v2beta1 HPA with a Pods metric on gpu_utilization scales its Deployment."""
+    from amdkube.metrics import MetricsServer
+    from tests.test_metrics_server import _ca, _leaf
+    d = str(tmp_path)
+    _ca(d, "serving-ca")
+    scert, skey = _leaf(d, "serving-ca", "metrics", "metrics-server", server=True)
+
+    async def go():
+        kw = {"hpa_sync_period": 0.5, "hpa_upscale_delay": 0.0, "hpa_downscale_delay": 600.0}
+        async with LocalCluster(gpus="amdsmi", n_gpus=1, relist_period=0.5, controllers_kw=kw) as lc:
+            c = lc.client
+            await lc.wait_gpus(1, 60)
+            ms = await MetricsServer(c, resolution=0.5, tls_cert=scert, tls_key=skey, authorize=False).start()
+            try:
+                await c.create({"apiVersion": "v1", "kind": "Service", "metadata": {"name": "metrics-server", "namespace": "kube-system"},
+                                "spec": {"ports": [{"port": 443, "targetPort": ms.port}]}})
+                await c.create({"apiVersion": "v1", "kind": "Endpoints", "metadata": {"name": "metrics-server", "namespace": "kube-system"},
+                                "subsets": [{"addresses": [{"ip": "127.0.0.1"}], "ports": [{"port": ms.port}]}]})
+                await c.create({"apiVersion": "apiregistration.k8s.io/v1beta1", "kind": "APIService",
+                                "metadata": {"name": "v1beta1.custom.metrics.k8s.io"},
+                                "spec": {"group": "custom.metrics.k8s.io", "version": "v1beta1", "groupPriorityMinimum": 100,
+                                         "versionPriority": 100, "insecureSkipTLSVerify": True,
+                                         "service": {"namespace": "kube-system", "name": "metrics-server"}}})
+                tpl = {"metadata": {"labels": {"app": "burn"}}, "spec": {"containers": [{
+                    "name": "burn", "image": "amdkube/gpu-burn", "args": ["--ms", "30000"],
+                    "resources": {"limits": {"amd.com/gpu": "1"}}}]}}
+                await c.create({"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": "burn"},
+                                "spec": {"replicas": 1, "selector": {"matchLabels": {"app": "burn"}}, "template": tpl}}, "default")
+                await c.request("POST", "/apis/autoscaling/v2beta1/namespaces/default/horizontalpodautoscalers", body={
+                    "apiVersion": "autoscaling/v2beta1", "kind": "HorizontalPodAutoscaler", "metadata": {"name": "burn"},
+                    "spec": {"scaleTargetRef": {"apiVersion": "apps/v1", "kind": "Deployment", "name": "burn"},
+                             "minReplicas": 1, "maxReplicas": 2,
+                             "metrics": [{"type": "Pods", "pods": {"metricName": "gpu_utilization", "targetAverageValue": "10"}}]}})
+                loop = asyncio.get_running_loop()
+                end, h, util = loop.time() + 90, None, None
+                while loop.time() < end:
+                    dep = await c.get("deployments", "burn", "default")
+                    h = await c.request("GET", "/apis/autoscaling/v2beta1/namespaces/default/horizontalpodautoscalers/burn")
+                    cur = (h.get("status") or {}).get("currentMetrics") or []
+                    util = cur[0]["pods"]["currentAverageValue"] if cur else util
+                    if dep["spec"]["replicas"] == 2:
+                        break
+                    await asyncio.sleep(0.5)
+                print("hpa status:", json.dumps(h.get("status")))
+                assert dep["spec"]["replicas"] == 2, (h.get("status"), util)
+                assert float(util.rstrip("m")) / (1000 if util.endswith("m") else 1) > 10, util
+                conds = {x["type"]: x for x in h["status"]["conditions"]}
+                assert conds["ScalingActive"]["reason"] == "ValidMetricFound"
+            finally:
+                await ms.stop()
+    run(go(), 200)
+
+
 def test_07_native_activity_sampler_averages_a_burn():
     """The shim's background sampler (native/sampler_core.h via _amdsmi.start_sampler) on the
     real MI355X: while gpu-burn keeps the MFMA pipes busy for 2 s, the windowed mean over
