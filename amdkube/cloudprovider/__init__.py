@@ -15,6 +15,10 @@ fork's README names EC2 and GCP GPU VMs next to on-prem DGX hosts. An MI355X nod
     with its NSG rules, managed disks — the cloud that rents AMD Instinct VMs;
   * `openstack` (cloudprovider/openstack.py): Keystone + Nova instances/zones, Neutron router
     routes, Octavia/LBaaS v2 load balancers with floating IPs, Cinder volumes;
+  * `cloudstack` (cloudprovider/cloudstack.py): signed query API — VMs, zones, public-IP load
+    balancer rules; the virtual router's metadata service without API keys;
+  * `ovirt` (cloudprovider/ovirt.py): the engine's VM list (XML) for node addresses and IDs;
+  * `photon` (cloudprovider/photon.py): Photon controller VMs, flavors and persistent disks;
   * `baremetal`: load balancers get addresses from a configured pool (the MetalLB model),
     routes are kept in a table and programmed with `ip route` when privileged, and instance
     data comes from the Node objects;
@@ -319,7 +323,23 @@ def _azure(config):
     return Azure(config)
 
 
-_PROVIDERS = {"baremetal": BareMetal, "fake": Fake, "openstack": _openstack, "aws": _aws, "gce": _gce, "azure": _azure}
+def _cloudstack(config):
+    from .cloudstack import CloudStack
+    return CloudStack(config)
+
+
+def _ovirt(config):
+    from .ovirt import OVirt
+    return OVirt(config)
+
+
+def _photon(config):
+    from .photon import Photon
+    return Photon(config)
+
+
+_PROVIDERS = {"baremetal": BareMetal, "fake": Fake, "openstack": _openstack, "aws": _aws, "gce": _gce, "azure": _azure,
+              "cloudstack": _cloudstack, "ovirt": _ovirt, "photon": _photon}
 
 
 def load_config(path: str | None):

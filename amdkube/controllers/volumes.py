@@ -163,8 +163,8 @@ class PersistentVolumeBinderController(Controller):
             sc = self._class(claim_class(pvc))
             if sc is not None and sc.get("provisioner") in HOSTPATH_PROVISIONERS:
                 pv = await self._provision(pvc, sc)
-            elif sc is not None and self._cloud_disks() is not None and sc.get("provisioner") == self._cloud_disks().provisioner:
-                pv = await self._provision_cloud(pvc, sc)
+            elif sc is not None and sc.get("provisioner") in self._provisioners():
+                pv = await self._provision_cloud(pvc, sc, self._provisioners()[sc["provisioner"]])
             else:
                 if (pvc.get("status") or {}).get("phase") != "Pending":
                     await self.client.patch("persistentvolumeclaims", name, {"status": {"phase": "Pending"}}, ns, sub="status")
@@ -191,7 +191,17 @@ class PersistentVolumeBinderController(Controller):
         cloud = getattr(getattr(self.mgr, "opts", None), "cloud", None)
         return cloud.volumes() if cloud is not None and hasattr(cloud, "volumes") else None
 
-    async def _provision_cloud(self, pvc, sc):
+    def _provisioners(self) -> dict:
+        """Dynamic provisioners by StorageClass provisioner name: the cloud's disks and the
+        vendor storage backends (volume/vendor.py)."""
+        from ..volume.vendor import provisioners
+        out = {p.provisioner: p for p in provisioners()}
+        d = self._cloud_disks()
+        if d is not None:
+            out[d.provisioner] = d
+        return out
+
+    async def _provision_cloud(self, pvc, sc, disks):
         """The in-tree cloud provisioners (cinder_util.go, aws_util.go, gce_util.go,
         azure_provision.go CreateVolume): a disk of the claim's size in GiB, rounded up, with the
         class's parameters, tagged with the claim; the PV carries the disk's zone/region labels."""
@@ -202,8 +212,10 @@ class PersistentVolumeBinderController(Controller):
         name = f"pvc-{m.uid_of(pvc)}"
         tags = {"kubernetes.io/created-for/pvc/namespace": m.namespace_of(pvc),
                 "kubernetes.io/created-for/pvc/name": m.name_of(pvc), "kubernetes.io/created-for/pv/name": name}
-        disks = self._cloud_disks()
-        source, labels = await asyncio.to_thread(disks.provision, name, gib, params, tags, m.name_of(pvc))
+        if hasattr(disks, "aprovision"):
+            source, labels = await disks.aprovision(self.client, name, gib, params, tags, m.name_of(pvc))
+        else:
+            source, labels = await asyncio.to_thread(disks.provision, name, gib, params, tags, m.name_of(pvc))
         pv = {"apiVersion": "v1", "kind": "PersistentVolume",
               "metadata": {"name": name, "labels": {k: v for k, v in labels.items() if v},
                            "annotations": {"pv.kubernetes.io/provisioned-by": disks.provisioner}},
@@ -260,10 +272,12 @@ class PersistentVolumeBinderController(Controller):
         if policy == "Delete":
             if m.annotations_of(pv).get("pv.kubernetes.io/provisioned-by") in HOSTPATH_PROVISIONERS:
                 shutil.rmtree((ps.get("hostPath") or {}).get("path", "") or "/nonexistent", ignore_errors=True)
-            elif self._cloud_disks() is not None and ps.get(self._cloud_disks().source_key) \
-                    and m.annotations_of(pv).get("pv.kubernetes.io/provisioned-by") == self._cloud_disks().provisioner:
-                disks = self._cloud_disks()
-                await asyncio.to_thread(disks.delete_source, ps[disks.source_key])   # fails while attached: retried
+            elif (disks := self._provisioners().get(m.annotations_of(pv).get("pv.kubernetes.io/provisioned-by"))) is not None \
+                    and ps.get(disks.source_key):
+                if hasattr(disks, "adelete"):
+                    await disks.adelete(self.client, ps[disks.source_key])
+                else:
+                    await asyncio.to_thread(disks.delete_source, ps[disks.source_key])   # fails while attached: retried
             try:
                 await self.client.delete("persistentvolumes", name)
             except m.StatusError as e:

@@ -1,7 +1,7 @@
 """Cloud block disks attached through the cloud provider: OpenStack Cinder (pkg/volume/cinder:
 attacher.go, cinder.go, cinder_util.go), AWS EBS (pkg/volume/aws_ebs: attacher.go, aws_ebs.go,
 aws_util.go), GCE persistent disks (pkg/volume/gce_pd) and Azure managed disks
-(pkg/volume/azure_dd).
+(pkg/volume/azure_dd) and Photon persistent disks (pkg/volume/photon_pd).
 
 One flow for all of them: the attach/detach controller attaches the disk to the node's
 instance through `--cloud-provider`'s volumes() (cloudprovider/{openstack,aws,gce,azure}.py),
@@ -97,5 +97,13 @@ class AzureDiskPlugin(CloudDiskPlugin):
         return await asyncio.to_thread(self._volumes().attach, node, uri, caching)
 
 
+class PhotonPDPlugin(CloudDiskPlugin):
+    """photon_pd: pdID names a Photon persistent disk; it shows up by its WWN."""
+    name = "kubernetes.io/photon-pd"
+    source_key = "photonPersistentDisk"
+    provider = "photon"
+    id_field = "pdID"
+
+
 def plugins():
-    return [CinderPlugin(), AWSEBSPlugin(), GCEPDPlugin(), AzureDiskPlugin()]
+    return [CinderPlugin(), AWSEBSPlugin(), GCEPDPlugin(), AzureDiskPlugin(), PhotonPDPlugin()]

@@ -1,10 +1,8 @@
-"""Volume types whose backends are vendor services this build cannot reach (pkg/volume/
-vsphere_volume, photon_pd, portworx, scaleio, storageos, flocker). Cinder, AWS EBS, GCE PD and
-Azure managed disks are real plugins (volume/cinder.py) over the OpenStack, AWS, GCE and Azure
-providers. These are recognised — so a pod using one gets a precise FailedMount event instead
-of "no volume plugin matched" — but their set-up fails: attaching them needs the vendor's API
-or client library (vCenter, Photon controller, Portworx, ScaleIO gateway + drv_cfg, StorageOS,
-Flocker control service), none of which an MI355X host has.
+"""Volume types recognised without a backend: a pod using one gets a precise FailedMount event
+instead of "no volume plugin matched". Every in-tree type of the reference now has a real
+plugin (volume/cinder.py for the cloud disks, volume/vendor.py for Flocker, StorageOS,
+Portworx and ScaleIO, volume/vsphere.py for vSphere) — this table is kept for types a build
+leaves out.
 """
 from __future__ import annotations
 
@@ -12,11 +10,6 @@ from . import VolumeError, VolumePlugin
 
 _TYPES = {
     "vsphereVolume": ("kubernetes.io/vsphere-volume", "the vSphere API"),
-    "photonPersistentDisk": ("kubernetes.io/photon-pd", "the Photon controller API"),
-    "portworxVolume": ("kubernetes.io/portworx-volume", "the Portworx REST API"),
-    "scaleIO": ("kubernetes.io/scaleio", "the ScaleIO gateway and drv_cfg"),
-    "storageos": ("kubernetes.io/storageos", "the StorageOS API"),
-    "flocker": ("kubernetes.io/flocker", "the Flocker control service"),
 }
 
 
