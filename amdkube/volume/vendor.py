@@ -45,8 +45,17 @@ GIB = 1 << 30
 
 
 def _http():
+    """A requests session whose transport failures surface as VolumeError (FailedMount events
+    name the unreachable backend instead of a raw connection traceback)."""
     import requests
-    return requests.Session()
+
+    class Session(requests.Session):
+        def request(self, method, url, *a, **kw):
+            try:
+                return super().request(method, url, *a, **kw)
+            except requests.RequestException as e:
+                raise VolumeError(f"storage backend at {url.split('?', 1)[0]} is unreachable: {e.__class__.__name__}") from e
+    return Session()
 
 
 def _raise(r, what: str):

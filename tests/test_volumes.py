@@ -124,13 +124,13 @@ def test_network_filesystems(tmp_path):
         for x in (d, d2, d3):
             await mgr.find_by_spec(nfs).tear_down(x)
         assert len(fm.actions("unmount")) == 3 and not fm.mounts
-        # vendor volumes without a reachable backend are recognised and fail with a precise reason
+        # a vendor volume whose backend is unreachable fails with a precise reason
         pwx = Spec(volume={"name": "e", "portworxVolume": {"volumeID": "vol-1"}})
         try:
             await mgr.find_by_spec(pwx).set_up(pwx, _pod(), str(tmp_path / "e"))
             raise AssertionError("expected failure")
         except VolumeError as e:
-            assert "Portworx REST API" in str(e)
+            assert "storage backend at http://127.0.0.1:9001/v1/osd-volumes/vol-1 is unreachable" in str(e)
         # an EBS disk is a real attachable plugin, served through the AWS cloud provider
         ebs = Spec(volume={"name": "e", "awsElasticBlockStore": {"volumeID": "vol-1"}})
         assert mgr.find_by_spec(ebs).attachable and mgr.find_by_spec(ebs).name == "kubernetes.io/aws-ebs"
