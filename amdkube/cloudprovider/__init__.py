@@ -19,6 +19,8 @@ fork's README names EC2 and GCP GPU VMs next to on-prem DGX hosts. An MI355X nod
     balancer rules; the virtual router's metadata service without API keys;
   * `ovirt` (cloudprovider/ovirt.py): the engine's VM list (XML) for node addresses and IDs;
   * `photon` (cloudprovider/photon.py): Photon controller VMs, flavors and persistent disks;
+  * `vsphere` (cloudprovider/vsphere.py): vCenter over the vim25 SOAP API — VMs by inventory
+    path, guest addresses, VMDK create/attach/detach/delete;
   * `baremetal`: load balancers get addresses from a configured pool (the MetalLB model),
     routes are kept in a table and programmed with `ip route` when privileged, and instance
     data comes from the Node objects;
@@ -338,8 +340,14 @@ def _photon(config):
     return Photon(config)
 
 
+def _vsphere(config):
+    from .vsphere import VSphere
+    return VSphere(config)
+
+
 _PROVIDERS = {"baremetal": BareMetal, "fake": Fake, "openstack": _openstack, "aws": _aws, "gce": _gce, "azure": _azure,
-              "cloudstack": _cloudstack, "ovirt": _ovirt, "photon": _photon}
+              "cloudstack": _cloudstack, "ovirt": _ovirt, "photon": _photon,
+              "vsphere": _vsphere}
 
 
 def load_config(path: str | None):

@@ -479,7 +479,7 @@ def cloud_controller_manager(argv):
     ap.add_argument("--master", "--server", dest="server", default="http://127.0.0.1:8080")
     ap.add_argument("--kubeconfig", default=None)
     ap.add_argument("--token", default=None)
-    ap.add_argument("--cloud-provider", required=True, help="aws | gce | azure | openstack | baremetal | fake")
+    ap.add_argument("--cloud-provider", required=True, help="aws | gce | azure | openstack | vsphere | cloudstack | ovirt | photon | baremetal | fake")
     ap.add_argument("--cloud-config", default=None, help="provider config (baremetal: loadBalancerIPRange, zone, region, "
                                                          "instances inventory)")
     ap.add_argument("--controllers", default="*", help="'*' = cloud-node,service,route,persistentvolume-labeler")
@@ -578,7 +578,7 @@ def kubelet(argv):
     ap.add_argument("--port", type=int, default=10250)
     ap.add_argument("--runonce", action="store_true", help="run the static pods once, report, and exit (no API server)")
     ap.add_argument("--cloud-provider", default="", help="'external': the cloud-controller-manager initialises the node; "
-                                                          "openstack | baremetal: in-tree (addresses, providerID, zone)")
+                                                          "aws | gce | azure | openstack | vsphere | cloudstack | ovirt | photon | baremetal: in-tree (addresses, providerID, zone)")
     ap.add_argument("--cloud-config", default="", help="the in-tree provider's config (cloud.conf INI or YAML)")
     ap.add_argument("--volume-plugin-dir", default=None, help="FlexVolume driver directory")
     ap.add_argument("--enable-controller-attach-detach", default="true", choices=("true", "false"))

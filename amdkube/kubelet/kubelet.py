@@ -147,7 +147,7 @@ class KubeletConfig:
     volume_reconcile_period: float = 2.0              # reconciler loop period (s)
     volume_remount_period: float = 60.0               # re-render secret/configMap/downwardAPI/projected content (s)
     cloud_provider: str = ""                          # --cloud-provider ("external": cloud-controller-manager initialises the node)
-    cloud_config: str = ""                            # --cloud-config (in-tree providers: aws, gce, azure, openstack, baremetal)
+    cloud_config: str = ""                            # --cloud-config (in-tree providers: aws, gce, azure, openstack, vsphere, cloudstack, ovirt, photon, baremetal)
     enable_server: bool = True                        # --enable-server (the authenticated API on --port)
     enable_debugging_handlers: bool = True            # --enable-debugging-handlers (logs, exec, attach, portForward, run, pprof)
     read_only_port: int = -1                          # --read-only-port (unauthenticated read-only API; -1/0: off; CLI default 10255)

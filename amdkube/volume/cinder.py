@@ -1,7 +1,8 @@
 """Cloud block disks attached through the cloud provider: OpenStack Cinder (pkg/volume/cinder:
 attacher.go, cinder.go, cinder_util.go), AWS EBS (pkg/volume/aws_ebs: attacher.go, aws_ebs.go,
 aws_util.go), GCE persistent disks (pkg/volume/gce_pd) and Azure managed disks
-(pkg/volume/azure_dd) and Photon persistent disks (pkg/volume/photon_pd).
+(pkg/volume/azure_dd) Photon persistent disks (pkg/volume/photon_pd) and vSphere
+VMDKs (pkg/volume/vsphere_volume).
 
 One flow for all of them: the attach/detach controller attaches the disk to the node's
 instance through `--cloud-provider`'s volumes() (cloudprovider/{openstack,aws,gce,azure}.py),
@@ -105,5 +106,14 @@ class PhotonPDPlugin(CloudDiskPlugin):
     id_field = "pdID"
 
 
+class VSphereVolumePlugin(CloudDiskPlugin):
+    """vsphere_volume: volumePath `[datastore] kubevols/<disk>.vmdk`, attached to the node VM's
+    SCSI controller and found by the disk's WWN."""
+    name = "kubernetes.io/vsphere-volume"
+    source_key = "vsphereVolume"
+    provider = "vsphere"
+    id_field = "volumePath"
+
+
 def plugins():
-    return [CinderPlugin(), AWSEBSPlugin(), GCEPDPlugin(), AzureDiskPlugin(), PhotonPDPlugin()]
+    return [CinderPlugin(), AWSEBSPlugin(), GCEPDPlugin(), AzureDiskPlugin(), PhotonPDPlugin(), VSphereVolumePlugin()]

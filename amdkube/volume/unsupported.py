@@ -1,16 +1,14 @@
 """Volume types recognised without a backend: a pod using one gets a precise FailedMount event
 instead of "no volume plugin matched". Every in-tree type of the reference now has a real
 plugin (volume/cinder.py for the cloud disks, volume/vendor.py for Flocker, StorageOS,
-Portworx and ScaleIO, volume/vsphere.py for vSphere) — this table is kept for types a build
+Portworx and ScaleIO) — this table is kept for types a build
 leaves out.
 """
 from __future__ import annotations
 
 from . import VolumeError, VolumePlugin
 
-_TYPES = {
-    "vsphereVolume": ("kubernetes.io/vsphere-volume", "the vSphere API"),
-}
+_TYPES: dict[str, tuple[str, str]] = {}
 
 
 class UnavailableBackendPlugin(VolumePlugin):
