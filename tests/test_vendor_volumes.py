@@ -200,3 +200,63 @@ def test_every_reference_volume_type_has_a_plugin():
                 "gcePersistentDisk", "azureDisk", "vsphereVolume"):
         assert mgr.find_by_spec(Spec({"name": "x", key: {}})).source_key == key
     assert asyncio.iscoroutinefunction(vendor.ScaleIOProvisioner().aprovision)
+
+
+def test_pv_controller_provisions_and_reclaims_vendor_and_vsphere_volumes(tmp_path, monkeypatch):
+    """The PV binder's dynamic provisioning (persistentvolume/pv_controller.go provisionClaim /
+    deleteVolumeOperation) through a vendor provisioner (Portworx) and a cloud one (vSphere)."""
+    from amdkube.api import meta as m
+    from amdkube.client import Client
+    from amdkube.cloudprovider import get_cloud_provider
+    from amdkube.controllers import ControllerManager, Options
+    from amdkube.localcluster import LocalCluster
+    from tests.fake_vsphere import FakeVCenter
+    px, vc = FakePortworx().start(), FakeVCenter().start()
+    monkeypatch.setenv("AMDKUBE_PORTWORX_ENDPOINT", px.url)
+
+    async def go():
+        async with LocalCluster(gpus="fake", n_gpus=1, with_controllers=False, relist_period=0.2) as lc:
+            c = lc.client
+            for name, prov, params in (("px", "kubernetes.io/portworx-volume", {"repl": "3"}),
+                                       ("vs", "kubernetes.io/vsphere-volume", {"diskformat": "thin"})):
+                await c.create({"apiVersion": "storage.k8s.io/v1", "kind": "StorageClass", "metadata": {"name": name},
+                                "provisioner": prov, "parameters": params})
+                await c.create({"apiVersion": "v1", "kind": "PersistentVolumeClaim", "metadata": {"name": name, "namespace": "default"},
+                                "spec": {"storageClassName": name, "accessModes": ["ReadWriteOnce"],
+                                         "resources": {"requests": {"storage": "3Gi"}}}}, "default")
+            cmc = Client(lc.api.url, token=lc.api.loopback_token)
+            cm = await ControllerManager(cmc, ["persistentvolume-binder", "pvc-protection", "pv-protection"],
+                                         options=Options(cloud=get_cloud_provider("vsphere", vc.config()))).start()
+            try:
+                async def until(fn, t=30):
+                    end = asyncio.get_running_loop().time() + t
+                    while asyncio.get_running_loop().time() < end:
+                        v = await fn()
+                        if v:
+                            return v
+                        await asyncio.sleep(0.05)
+                    raise AssertionError("condition not met")
+                pvs = {}
+                for name in ("px", "vs"):
+                    async def bound(name=name):
+                        p = await c.get("persistentvolumeclaims", name, "default")
+                        return p if (p.get("status") or {}).get("phase") == "Bound" else None
+                    pvs[name] = await c.get("persistentvolumes", (await until(bound))["spec"]["volumeName"])
+                vid = pvs["px"]["spec"]["portworxVolume"]["volumeID"]
+                assert px.vols[vid]["spec"]["size"] == 3 << 30 and px.vols[vid]["spec"]["ha_level"] == 3
+                path = pvs["vs"]["spec"]["vsphereVolume"]["volumePath"]
+                assert path in vc.disks and m.annotations_of(pvs["vs"])["pv.kubernetes.io/provisioned-by"] == "kubernetes.io/vsphere-volume"
+                for name in ("px", "vs"):
+                    await c.delete("persistentvolumeclaims", name, "default")
+
+                async def gone():
+                    return vid not in px.vols and path not in vc.disks
+                await until(gone)
+            finally:
+                await cm.stop()
+                await cmc.close()
+    try:
+        run(go(), 90)
+    finally:
+        px.stop()
+        vc.stop()
