@@ -12,12 +12,14 @@ Reference:
 from __future__ import annotations
 
 import asyncio
+import logging
 
 from ..api import meta as m
 from ..api.helpers import is_node_ready
 from ..cloudprovider import Route
 from .base import Controller, split_key
 
+log = logging.getLogger("amdkube.controllers.cloud")
 MASTER_LABEL = "node-role.kubernetes.io/master"
 
 
@@ -220,7 +222,8 @@ class CloudNodeController(Controller):
         itype = await inst.instance_type(name)
         if itype:
             labels[INSTANCE_TYPE_LABEL] = itype
-        zone = self.cloud.zone_for_node(name) if hasattr(self.cloud, "zone_for_node") else self.cloud.zones()
+        zone = await asyncio.to_thread(self.cloud.zone_for_node, name) if hasattr(self.cloud, "zone_for_node") \
+            else self.cloud.zones()
         if zone is not None and zone.failure_domain:
             labels[ZONE_LABEL] = zone.failure_domain
         if zone is not None and zone.region:
@@ -259,8 +262,12 @@ class CloudNodeController(Controller):
             if ready is None or ready.get("status") == "True":
                 continue
             pid = (node.get("spec") or {}).get("providerID")
-            exists = await inst.instance_exists_by_provider_id(pid) if pid and hasattr(inst, "instance_exists_by_provider_id") \
-                else await inst.instance_exists(m.name_of(node))
+            try:
+                exists = await inst.instance_exists_by_provider_id(pid) if pid and hasattr(inst, "instance_exists_by_provider_id") \
+                    else await inst.instance_exists(m.name_of(node))
+            except Exception as e:      # noqa: BLE001 — a cloud that cannot tell (or is unreachable) keeps the node
+                log.warning("cloud existence check for node %s: %r", m.name_of(node), e)
+                continue
             if exists:
                 continue
             self.mgr.recorder.event({"kind": "Node", "metadata": {"name": m.name_of(node), "uid": m.uid_of(node)}}, "Normal",
