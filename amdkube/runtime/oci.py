@@ -25,6 +25,7 @@ import hashlib
 import io
 import json
 import os
+import re
 import shutil
 import tarfile
 import tempfile
@@ -35,6 +36,17 @@ OPAQUE = ".wh..wh..opq"
 
 class ImageFormatError(ValueError):
     pass
+
+
+_DIGEST_LEN = {"sha256": 64, "sha512": 128}    # the OCI image-spec's registered digest algorithms
+
+
+def _hash_file(path: str, algo: str) -> str:
+    h = hashlib.new(algo)
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
 
 
 def _sha256_file(path: str) -> str:
@@ -149,13 +161,21 @@ def read_archive(path: str, work: str) -> tuple[dict, list[str], list[str]]:
         os.makedirs(src)
         with tarfile.open(path, "r:*") as tf:
             tf.extractall(src, filter="data")
+    src = os.path.realpath(src)
+
+    def member(rel) -> str:
+        """A file named by the archive's own metadata: it must resolve inside the archive."""
+        p = os.path.join(src, str(rel))
+        if os.path.isabs(str(rel)) or not _inside(src, p):
+            raise ImageFormatError(f"archive path {rel!r} leaves the archive")
+        return p
     if os.path.exists(os.path.join(src, "manifest.json")):          # docker save
         man = _read_json(os.path.join(src, "manifest.json"))
         if not isinstance(man, list) or not man:
             raise ImageFormatError("manifest.json: expected a non-empty list")
         m0 = man[0]
-        cfg = _read_json(os.path.join(src, m0["Config"]))
-        layers = [os.path.join(src, lp) for lp in m0.get("Layers") or []]
+        cfg = _read_json(member(m0["Config"]))
+        layers = [member(lp) for lp in m0.get("Layers") or []]
         tags = list(m0.get("RepoTags") or [])
     elif os.path.exists(os.path.join(src, "index.json")):           # OCI image layout
         idx = _read_json(os.path.join(src, "index.json"))
@@ -164,11 +184,13 @@ def read_archive(path: str, work: str) -> tuple[dict, list[str], list[str]]:
             raise ImageFormatError("index.json lists no manifest")
 
         def blob(digest):
-            algo, _, hexd = digest.partition(":")
-            p = os.path.join(src, "blobs", algo, hexd)
+            algo, _, hexd = str(digest).partition(":")
+            if algo not in _DIGEST_LEN or not re.fullmatch(f"[0-9a-f]{{{_DIGEST_LEN[algo]}}}", hexd):
+                raise ImageFormatError(f"unsupported or malformed digest {digest!r}")
+            p = member(os.path.join("blobs", algo, hexd))
             if not os.path.exists(p):
                 raise ImageFormatError(f"missing blob {digest}")
-            if algo == "sha256" and _sha256_file(p) != hexd:
+            if _hash_file(p, algo) != hexd:
                 raise ImageFormatError(f"blob {digest} does not match its digest")
             return p
         m = _read_json(blob(mans[0]["digest"]))

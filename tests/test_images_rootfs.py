@@ -136,6 +136,27 @@ def test_oci_layout_import_checks_digests(tmp_path):
         import_image(str(lay), str(tmp_path / "store2"))
 
 
+def test_archive_metadata_cannot_name_files_outside_the_archive(tmp_path):
+    """manifest.json Config/Layers and index.json digests are archive-relative: a '../' path or a
+    digest that is not hex of its algorithm's length is refused, not read from the host."""
+    secret = tmp_path / "host-secret.json"
+    secret.write_text("{}")
+    dock = tmp_path / "dock"
+    dock.mkdir()
+    (dock / "manifest.json").write_text(json.dumps([{"Config": "../host-secret.json", "Layers": []}]))
+    with pytest.raises(ImageFormatError, match="leaves the archive"):
+        import_image(str(dock), str(tmp_path / "s1"))
+    (dock / "manifest.json").write_text(json.dumps([{"Config": str(secret), "Layers": []}]))
+    with pytest.raises(ImageFormatError, match="leaves the archive"):
+        import_image(str(dock), str(tmp_path / "s2"))
+    lay = tmp_path / "oci"
+    _oci_layout(str(lay), [[("a", b"a", 0o644, None)]], {})
+    for bad in ("sha512:../../host-secret.json", "md5:" + "0" * 32, "sha256:" + "0" * 63):
+        (lay / "index.json").write_text(json.dumps({"schemaVersion": 2, "manifests": [{"digest": bad}]}))
+        with pytest.raises(ImageFormatError, match="digest"):
+            import_image(str(lay), str(tmp_path / "s3"))
+
+
 def test_rootfs_argv_runs_the_images_own_loader(tmp_path):
     arch = tmp_path / "sh.tar"
     write_docker_archive(str(arch), [host_closure("/bin/sh", "/bin/cat")], {"Entrypoint": ["/bin/sh", "-c"]}, [])
