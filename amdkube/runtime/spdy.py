@@ -40,6 +40,7 @@ EXEC_PROTOCOLS = ("v4.channel.k8s.io", "v3.channel.k8s.io", "v2.channel.k8s.io",
 PORTFORWARD_PROTOCOLS = ("portforward.k8s.io",)
 STREAM_CREATION_TIMEOUT = 30.0
 MAX_DATA = 64 * 1024
+MAX_HEADER_BLOCK = 1 << 20     # inflated name/value block bound (a small compressed block can expand ~1000x)
 
 SYN_STREAM, SYN_REPLY, RST_STREAM, SETTINGS, PING, GOAWAY, HEADERS, WINDOW_UPDATE = 1, 2, 3, 4, 6, 7, 8, 9
 FLAG_FIN, FLAG_UNIDIRECTIONAL = 0x01, 0x02
@@ -284,7 +285,10 @@ class Session:
                 if version != 3:
                     self._spawn(self.close())
                     return
-                self._control(ftype, flags, payload)
+                try:
+                    self._control(ftype, flags, payload)
+                except (struct.error, zlib.error, UnicodeDecodeError) as e:   # malformed header block
+                    raise SpdyError(f"malformed SPDY control frame: {e}") from e
             else:
                 st = self.streams.get(w0 & 0x7FFFFFFF)
                 if st is not None:
@@ -297,7 +301,12 @@ class Session:
         t.add_done_callback(self._tasks.discard)
 
     def _headers(self, block: bytes) -> dict:
-        return decode_headers(self._inflate.decompress(block)) if block else {}
+        if not block:
+            return {}
+        raw = self._inflate.decompress(block, MAX_HEADER_BLOCK)
+        if self._inflate.unconsumed_tail:       # a header block that inflates past the bound
+            raise SpdyError(f"SPDY header block inflates beyond {MAX_HEADER_BLOCK} bytes")
+        return decode_headers(raw)
 
     def _control(self, ftype: int, flags: int, p: bytes):
         if ftype == SYN_STREAM:
@@ -373,7 +382,10 @@ class _Feed:
         self.sink, self.on_eof = sink, on_eof
 
     def feed_data(self, data: bytes):
-        self.sink(data)
+        try:
+            self.sink(data)
+        except SpdyError:              # protocol violation by the peer: end the session, not the server
+            self.on_eof()
         return False, b""
 
     def feed_eof(self):
@@ -464,7 +476,7 @@ async def connect(url: str, protocols, headers: dict | None = None, ssl=None, me
                 if not data:
                     break
                 sess.feed(data)
-        except (ConnectionError, OSError):
+        except (ConnectionError, OSError, SpdyError):
             pass
         finally:
             sess.connection_lost()

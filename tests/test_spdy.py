@@ -197,3 +197,23 @@ async def test_spdy_refuses_bad_streams():
     await client.close()
     assert json.dumps(spdy.exec_streams_expected("v4.channel.k8s.io", True, True, True, True), default=sorted) == \
         json.dumps(["error", "resize", "stdin", "stdout"])
+
+
+def test_header_block_bombs_and_garbage_end_the_session():
+    """A SYN_STREAM whose header block inflates past MAX_HEADER_BLOCK, or a truncated block,
+    is a SpdyError (the session ends) rather than unbounded memory or an unhandled error."""
+
+    def syn(block):
+        return spdy.control_frame(spdy.SYN_STREAM, struct.pack(">IIH", 1, 0, 0) + block)
+
+    bomb = struct.pack(">I", 1) + struct.pack(">I", 1) + b"x" + struct.pack(">I", 4 << 20) + b"a" * (4 << 20)
+    z = zlib.compressobj(zlib.Z_DEFAULT_COMPRESSION, zlib.DEFLATED, 15, zdict=spdy.DICTIONARY)
+    packed = z.compress(bomb) + z.flush(zlib.Z_SYNC_FLUSH)
+    assert len(packed) < (1 << 24)
+
+    async def run():
+        for frame in (syn(packed), syn(b"\x00garbage")):
+            sess = spdy.Session(server=True)
+            with pytest.raises(spdy.SpdyError):
+                sess.feed(frame)
+    asyncio.run(run())
