@@ -279,14 +279,16 @@ def etcd(argv):
     ap.add_argument("--name", default="default", help="this member's name in --initial-cluster")
     ap.add_argument("--initial-cluster", default="",
                     help="name=peerURL,... of every member: a raft group (static membership)")
-    ap.add_argument("--listen-peer-urls", default=None, help="raft + forwarded client calls (default: this member's "
-                                                              "--initial-cluster URL)")
+    ap.add_argument("--listen-peer-urls", default=None, help="raft + member-to-member calls only (default: this "
+                                                              "member's --initial-cluster URL)")
+    ap.add_argument("--peer-cert-file", default=None, help="peer listener + peer channels: mutual TLS")
+    ap.add_argument("--peer-key-file", default=None)
+    ap.add_argument("--peer-trusted-ca-file", default=None, help="require peer certificates signed by this CA")
     ap.add_argument("--heartbeat-interval", type=int, default=100, help="ms")
     ap.add_argument("--election-timeout", type=int, default=1000, help="ms")
     ap.add_argument("-v", type=int, default=0)
     for flag in ("--advertise-client-urls", "--initial-advertise-peer-urls", "--initial-cluster-state",
-                 "--initial-cluster-token", "--client-cert-auth", "--peer-cert-file", "--peer-key-file",
-                 "--peer-trusted-ca-file", "--quota-backend-bytes"):
+                 "--initial-cluster-token", "--client-cert-auth", "--quota-backend-bytes"):
         ap.add_argument(flag, default=None, help=argparse.SUPPRESS)
     a = ap.parse_args(argv)
     klog.setup(a.v, "etcd")
@@ -303,7 +305,8 @@ def etcd(argv):
     try:
         asyncio.run(serve(a.data_dir, listen, a.cert_file, a.key_file, a.trusted_ca_file, a.snapshot_count,
                           name=a.name, peers=peers, peer_listen=peer_listen,
-                          heartbeat=a.heartbeat_interval / 1000.0, election=a.election_timeout / 1000.0))
+                          heartbeat=a.heartbeat_interval / 1000.0, election=a.election_timeout / 1000.0,
+                          peer_cert=a.peer_cert_file, peer_key=a.peer_key_file, peer_ca=a.peer_trusted_ca_file))
     except KeyboardInterrupt:
         pass
 

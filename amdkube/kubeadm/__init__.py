@@ -67,13 +67,15 @@ def new_ca(d, name="ca", cn="kubernetes"):
 
 
 def new_cert(d, name, cn, orgs=(), sans=(), server=False, ca="ca", days=365):
+    """`server`: False = client cert, True = server cert, "peer" = both (etcd peer certs)."""
     subj = "".join(f"/O={o}" for o in orgs) + f"/CN={cn}"
     _ssl("req", "-new", "-newkey", "rsa:2048", "-nodes", "-keyout", f"{d}/{name}.key", "-out", f"{d}/{name}.csr", "-subj", subj)
     os.chmod(f"{d}/{name}.key", 0o600)
     ext = f"{d}/{name}.ext"
+    eku = "serverAuth,clientAuth" if server == "peer" else "serverAuth" if server else "clientAuth"
     with open(ext, "w") as f:
         f.write("basicConstraints=CA:FALSE\nkeyUsage=digitalSignature,keyEncipherment\n")
-        f.write(f"extendedKeyUsage={'serverAuth' if server else 'clientAuth'}\n")
+        f.write(f"extendedKeyUsage={eku}\n")
         if sans:
             f.write("subjectAltName=" + ",".join(sans) + "\n")
     _ssl("x509", "-req", "-in", f"{d}/{name}.csr", "-CA", f"{d}/{ca}.crt", "-CAkey", f"{d}/{ca}.key", "-CAcreateserial",

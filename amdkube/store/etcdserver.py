@@ -15,6 +15,16 @@ Semantics follow etcd's (etcdserver/apply.go, mvcc/kvstore_txn.go):
   on request and NOPUT/NODELETE filters;
 * leases carry keys; an expired or revoked lease deletes them in one revision.
 Not provided: members/auth/cluster RPCs, defragment/snapshot/hash, multi-op txn nesting.
+
+Clustered (`--initial-cluster`), the client API and the peer API listen apart, as etcd's
+--listen-client-urls / --listen-peer-urls do. The peer listener carries only member-to-member
+traffic: the raft service and `amdkube.etcdpeer.Peer` — Propose (a follower hands a client
+mutation to the leader as a raft proposal, etcd's MsgProp), ReadIndex (a follower's
+linearizable read: the leader confirms its lease and returns its commit index, the follower
+serves once it has applied that far — etcd's ReadIndex) and KeepAlive (lease renewals relayed to
+the leader's lessor, etcd's /leases peer handler). With --peer-cert-file/--peer-key-file/
+--peer-trusted-ca-file the peer listener and every peer channel use mutual TLS; the client
+services are never reachable on it.
 """
 from __future__ import annotations
 
@@ -26,6 +36,7 @@ import time
 
 import grpc
 
+from ..grpcdesc.compiler import ProtoModule
 from ..grpcdesc.etcd import (EQUAL, ETCD as E, EV_DELETE, EV_PUT, GREATER, LESS, NOT_EQUAL, T_CREATE, T_MOD,
                              T_VALUE, T_VERSION)
 from .mvcc import PUT, MVCCStore
@@ -56,9 +67,28 @@ def prefix_end(key: bytes) -> bytes:
 K_TXN, K_PUT, K_DELETE, K_COMPACT, K_LEASE_GRANT, K_LEASE_REVOKE = 1, 2, 3, 4, 5, 6
 _REQ = {K_TXN: E.TxnRequest, K_PUT: E.PutRequest, K_DELETE: E.DeleteRangeRequest, K_COMPACT: E.CompactionRequest,
         K_LEASE_GRANT: E.LeaseGrantRequest, K_LEASE_REVOKE: E.LeaseRevokeRequest}
-_METHOD = {K_TXN: "Txn", K_PUT: "Put", K_DELETE: "DeleteRange", K_COMPACT: "Compact", K_LEASE_GRANT: "LeaseGrant",
-           K_LEASE_REVOKE: "LeaseRevoke"}
 _KV_KINDS = {K_TXN, K_PUT, K_DELETE, K_COMPACT}
+_RESP = {K_TXN: E.TxnResponse, K_PUT: E.PutResponse, K_DELETE: E.DeleteRangeResponse, K_COMPACT: E.CompactionResponse,
+         K_LEASE_GRANT: E.LeaseGrantResponse, K_LEASE_REVOKE: E.LeaseRevokeResponse}
+_CODES = {c.value[0]: c for c in grpc.StatusCode}
+_SRV_OPTS = [("grpc.max_receive_message_length", 256 << 20), ("grpc.max_send_message_length", 256 << 20)]
+
+PEER = ProtoModule("""
+syntax = "proto3";
+package amdkube.etcdpeer;
+
+service Peer {
+  rpc Propose(ProposeRequest) returns (ProposeResponse) {}
+  rpc ReadIndex(ReadIndexRequest) returns (ReadIndexResponse) {}
+  rpc KeepAlive(KeepAliveRequest) returns (KeepAliveResponse) {}
+}
+message ProposeRequest { bytes data = 1; }
+message ProposeResponse { bytes result = 1; int32 code = 2; string message = 3; string leader = 4; }
+message ReadIndexRequest {}
+message ReadIndexResponse { uint64 index = 1; int32 code = 2; string leader = 3; }
+message KeepAliveRequest { int64 id = 1; }
+message KeepAliveResponse { int64 ttl = 1; bool found = 2; }
+""", "amdkube/etcdpeer.proto")
 
 
 def _hash_id(name: str) -> int:
@@ -75,7 +105,8 @@ class _Abort(Exception):
 class EtcdServer:
     def __init__(self, store: MVCCStore, cluster_id: int | None = None, member_id: int | None = None,
                  name: str = "default", peers: dict[str, str] | None = None, data_dir: str | None = None,
-                 heartbeat: float = 0.1, election: float = 1.0, compact_every: int = 10_000):
+                 heartbeat: float = 0.1, election: float = 1.0, compact_every: int = 10_000,
+                 peer_tls: tuple[str, str, str | None] | None = None):
         self.store = store
         self.compact_every = compact_every
         self.name = name
@@ -91,25 +122,47 @@ class EtcdServer:
         self.raft = None
         self._raft_args = (data_dir, heartbeat, election)
         self._fwd: dict[str, grpc.aio.Channel] = {}
+        # (cert file, key file, trusted CA file or None): mutual TLS between members
+        self.peer_tls = peer_tls
+        self.peer_server: grpc.aio.Server | None = None
+        self.peer_port = 0
 
     # ------------------------------------------------------------------ lifecycle
+    def _peer_channel(self, target: str):
+        """A channel to another member's peer listener (raft + Peer), under peer TLS if set."""
+        if not self.peer_tls:
+            return grpc.aio.insecure_channel(target, options=_SRV_OPTS)
+        cert, key, ca = self.peer_tls
+        creds = grpc.ssl_channel_credentials(root_certificates=open(ca, "rb").read() if ca else None,
+                                             private_key=open(key, "rb").read(), certificate_chain=open(cert, "rb").read())
+        return grpc.aio.secure_channel(target, creds, options=_SRV_OPTS)
+
     async def start(self, address: str = "127.0.0.1:0", credentials=None, peer_address: str | None = None):
-        """Serve the client API on `address`; with a cluster, also on `peer_address`, which
-        carries the raft service (members forward client calls to the leader over it)."""
-        self.server = grpc.aio.server(options=[("grpc.max_receive_message_length", 256 << 20),
-                                               ("grpc.max_send_message_length", 256 << 20)])
+        """Serve the client API (KV, Watch, Lease, Maintenance) on `address`. With a cluster, a
+        second server on `peer_address` (default: this member's --initial-cluster URL) carries
+        the raft and Peer services and nothing else."""
+        self.server = grpc.aio.server(options=_SRV_OPTS)
         for svc in ("KV", "Watch", "Lease", "Maintenance"):
             self.server.add_generic_rpc_handlers((E.services[svc].handler(self),))
+        self.port = (self.server.add_secure_port(address, credentials) if credentials is not None
+                     else self.server.add_insecure_port(address))
         if len(self.peers) > 1:
             from .raft import Raft
             data_dir, hb, el = self._raft_args
             self.raft = Raft(self.name, self.peers, data_dir, self, heartbeat=hb, election=el,
-                             compact_every=self.compact_every)
-            self.server.add_generic_rpc_handlers((self.raft.handler(),))
-        self.port = (self.server.add_secure_port(address, credentials) if credentials is not None
-                     else self.server.add_insecure_port(address))
-        if peer_address:
-            self.peer_port = self.server.add_insecure_port(peer_address)
+                             compact_every=self.compact_every, channel=self._peer_channel)
+            self.peer_server = grpc.aio.server(options=_SRV_OPTS)
+            self.peer_server.add_generic_rpc_handlers((self.raft.handler(), PEER.Peer.handler(self)))
+            paddr = peer_address or self.peers[self.name]
+            if self.peer_tls:
+                cert, key, ca = self.peer_tls
+                pcreds = grpc.ssl_server_credentials([(open(key, "rb").read(), open(cert, "rb").read())],
+                                                     root_certificates=open(ca, "rb").read() if ca else None,
+                                                     require_client_auth=bool(ca))
+                self.peer_port = self.peer_server.add_secure_port(paddr, pcreds)
+            else:
+                self.peer_port = self.peer_server.add_insecure_port(paddr)
+            await self.peer_server.start()
         await self.server.start()
         if self.raft is not None:
             await self.raft.start()
@@ -126,6 +179,8 @@ class EtcdServer:
             await ch.close()
         if self.server is not None:
             await self.server.stop(grace)
+        if self.peer_server is not None:
+            await self.peer_server.stop(grace)
         for w in self.store.all_watchers():
             w.close()
 
@@ -159,31 +214,79 @@ class EtcdServer:
     def _leader_channel(self, leader: str):
         ch = self._fwd.get(leader)
         if ch is None:
-            ch = self._fwd[leader] = grpc.aio.insecure_channel(self.peers[leader])
+            ch = self._fwd[leader] = self._peer_channel(self.peers[leader])
         return ch
 
-    async def _submit(self, kind: int, req, ctx):
-        """A mutation: applied here (single member), proposed (raft leader) or forwarded to the
-        leader (raft follower)."""
+    def _leader_or_abort(self, hint: str | None = None) -> str:
+        leader = hint or self.raft.leader
+        if not leader or leader == self.name:
+            raise _Abort(grpc.StatusCode.UNAVAILABLE, "etcdserver: no leader")
+        return leader
+
+    async def _propose(self, data: bytes):
+        """Commit one entry through raft: proposed here when leading, else handed to the leader
+        over the peer channel (a hop to a stale leader is redirected by its hint)."""
         from .raft import NotLeader
+        kind = data[0]
+        hint = None
+        for _ in range(3):
+            try:
+                return await self.raft.propose(data)
+            except NotLeader as e:
+                hint = e.leader or hint
+            leader = self._leader_or_abort(hint)
+            try:
+                r = await PEER.Peer.stub(self._leader_channel(leader)).Propose(PEER.ProposeRequest(data=data), timeout=10)
+            except grpc.RpcError as ge:
+                raise _Abort(ge.code(), ge.details()) from None
+            if not r.code:
+                return _RESP[kind].FromString(r.result)
+            if r.code != grpc.StatusCode.UNAVAILABLE.value[0] or not r.leader:
+                raise _Abort(_CODES.get(r.code, grpc.StatusCode.UNKNOWN), r.message)
+            hint = r.leader
+            await asyncio.sleep(0.05)
+        raise _Abort(grpc.StatusCode.UNAVAILABLE, "etcdserver: leader changed")
+
+    async def _submit(self, kind: int, req, ctx):
+        """A mutation: applied here (single member) or committed through raft."""
         try:
             if self.raft is None:
                 return self._exec(kind, req)
             try:
-                return await self.raft.propose(bytes([kind]) + req.SerializeToString())
-            except NotLeader as e:
-                leader = e.leader or self.raft.leader
-                if not leader or leader == self.name:
-                    raise _Abort(grpc.StatusCode.UNAVAILABLE, "etcdserver: no leader") from None
-                stub = E.KV.stub(self._leader_channel(leader)) if kind in _KV_KINDS else E.Lease.stub(self._leader_channel(leader))
-                try:
-                    return await getattr(stub, _METHOD[kind])(req, timeout=10)
-                except grpc.RpcError as ge:
-                    raise _Abort(ge.code(), ge.details()) from None
+                return await self._propose(bytes([kind]) + req.SerializeToString())
             except asyncio.TimeoutError:
                 raise _Abort(grpc.StatusCode.UNAVAILABLE, "etcdserver: request timed out") from None
         except _Abort as e:
             await ctx.abort(e.code, e.msg)
+
+    # ------------------------------------------------------------------ Peer service (peer listener only)
+    async def Propose(self, req, ctx):
+        """A follower's client mutation, proposed by this member if it leads."""
+        from .raft import NotLeader
+        try:
+            result = await self.raft.propose(req.data)
+            return PEER.ProposeResponse(result=result.SerializeToString())
+        except NotLeader as e:
+            return PEER.ProposeResponse(code=grpc.StatusCode.UNAVAILABLE.value[0], message="etcdserver: not leader",
+                                        leader=e.leader or "")
+        except _Abort as e:
+            return PEER.ProposeResponse(code=e.code.value[0], message=e.msg)
+        except asyncio.TimeoutError:
+            return PEER.ProposeResponse(code=grpc.StatusCode.UNAVAILABLE.value[0], message="etcdserver: request timed out")
+
+    async def ReadIndex(self, req, ctx):
+        from .raft import NotLeader
+        try:
+            return PEER.ReadIndexResponse(index=await self.raft.read_barrier())
+        except (NotLeader, TimeoutError):
+            return PEER.ReadIndexResponse(code=grpc.StatusCode.UNAVAILABLE.value[0], leader=self.raft.leader or "")
+
+    async def KeepAlive(self, req, ctx):
+        ent = self.leases.get(req.id)
+        if ent is None or self.raft.role != "leader":
+            return PEER.KeepAliveResponse(found=False)
+        ent[1] = time.monotonic() + ent[0]
+        return PEER.KeepAliveResponse(ttl=ent[0], found=True)
 
     def _exec(self, kind: int, req):
         if kind == K_TXN:
@@ -296,13 +399,18 @@ class EtcdServer:
                 try:
                     await self.raft.read_barrier()
                 except (NotLeader, TimeoutError):
-                    leader = self.raft.leader
-                    if not leader or leader == self.name:
-                        raise _Abort(grpc.StatusCode.UNAVAILABLE, "etcdserver: no leader") from None
+                    # ReadIndex: the leader vouches for its commit index; serve it once applied here
+                    leader = self._leader_or_abort()
                     try:
-                        return await E.KV.stub(self._leader_channel(leader)).Range(req, timeout=10)
+                        r = await PEER.Peer.stub(self._leader_channel(leader)).ReadIndex(PEER.ReadIndexRequest(), timeout=10)
                     except grpc.RpcError as ge:
                         raise _Abort(ge.code(), ge.details()) from None
+                    if r.code:
+                        raise _Abort(grpc.StatusCode.UNAVAILABLE, "etcdserver: leader changed") from None
+                    try:
+                        await self.raft.wait_applied(r.index, timeout=10)
+                    except asyncio.TimeoutError:
+                        raise _Abort(grpc.StatusCode.UNAVAILABLE, "etcdserver: request timed out") from None
             return self._range(req)
         except _Abort as e:
             await ctx.abort(e.code, e.msg)
@@ -511,12 +619,19 @@ class EtcdServer:
         return await self._submit(K_LEASE_REVOKE, req, ctx)
 
     async def LeaseKeepAlive(self, requests, ctx):
-        if self.raft is not None and self.raft.role != "leader" and self.raft.leader and self.raft.leader != self.name:
-            stub = E.Lease.stub(self._leader_channel(self.raft.leader))      # relay to the leader's lessor
-            async for resp in stub.LeaseKeepAlive(requests):
-                yield resp
-            return
         async for req in requests:
+            if self.raft is not None and self.raft.role != "leader":
+                leader = self.raft.leader                  # relay to the leader's lessor
+                ttl = 0
+                if leader and leader != self.name:
+                    try:
+                        r = await PEER.Peer.stub(self._leader_channel(leader)).KeepAlive(
+                            PEER.KeepAliveRequest(id=req.ID), timeout=5)
+                        ttl = r.ttl if r.found else 0
+                    except grpc.RpcError as ge:
+                        log.debug("lease %d keepalive relay to %s failed: %s", req.ID, leader, ge.code())
+                yield E.LeaseKeepAliveResponse(header=self.header(), ID=req.ID, TTL=ttl)
+                continue
             ent = self.leases.get(req.ID)
             if ent is None:
                 yield E.LeaseKeepAliveResponse(header=self.header(), ID=req.ID, TTL=0)
@@ -552,7 +667,7 @@ class EtcdServer:
 
 async def serve(data_dir: str | None, listen: str, cert=None, key=None, ca=None, snapshot_every: int = 50_000,
                 name: str = "default", peers: dict[str, str] | None = None, peer_listen: str | None = None,
-                heartbeat: float = 0.1, election: float = 1.0):
+                heartbeat: float = 0.1, election: float = 1.0, peer_cert=None, peer_key=None, peer_ca=None):
     """`amdkube etcd`: run until cancelled. With `peers` (--initial-cluster) the member joins a
     raft group; its store then lives in memory and the raft log under data_dir is the WAL."""
     creds = None
@@ -563,7 +678,8 @@ async def serve(data_dir: str | None, listen: str, cert=None, key=None, ca=None,
     clustered = bool(peers) and len(peers) > 1
     store = MVCCStore(None if clustered else data_dir, snapshot_every=snapshot_every)
     srv = await EtcdServer(store, name=name, peers=peers if clustered else None, data_dir=data_dir,
-                           heartbeat=heartbeat, election=election, compact_every=snapshot_every
+                           heartbeat=heartbeat, election=election, compact_every=snapshot_every,
+                           peer_tls=(peer_cert, peer_key, peer_ca) if peer_cert and peer_key else None,
                            ).start(listen, creds, peer_listen if clustered else None)
     print(f"amdkube etcd: serving the etcd v3 API on {srv.address} (revision {store.rev})", flush=True)
     try:

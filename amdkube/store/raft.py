@@ -10,14 +10,24 @@ is static (`--initial-cluster`). Linearizable reads use the leader lease: a majo
 acknowledged an AppendEntries within the election timeout.
 
 Durability, per member under `<data-dir>/raft/`: `state.json` (term, vote; fsynced before a
-vote or a term change is answered), `log.bin` (length-prefixed Entry records, fsynced before
-AppendEntries is acknowledged), `snap.bin` (state-machine snapshot + last included index/term;
-the log is cut behind it every `compact_every` applied entries).
+vote or a term change is answered), `log.bin` (length-prefixed Entry records, fdatasynced
+before AppendEntries is acknowledged), `snap.bin` (state-machine snapshot + last included
+index/term; the log is cut behind it every `compact_every` applied entries).
+
+Group commit (etcd's Ready batching, vendor/github.com/coreos/etcd/raft/node.go:52 and
+etcdserver/raft.go:134): a proposal only appends to the leader's in-memory log and wakes the
+flusher and the replicators. The flusher writes every entry appended since its last write with
+ONE write + fdatasync in a worker thread, while proposals keep arriving on the loop; the
+replicators ship everything a follower lacks in one AppendEntries (≤ MAX_BATCH entries), and a
+follower persists the batch with one fdatasync before acknowledging. The leader counts itself
+toward the commit quorum only up to its own persisted index (`persisted`), so N concurrent
+proposals cost about one leader fsync + one round trip + one follower fsync, not N of each.
 
 The state machine is the caller's: `apply(index, data) -> result` (deterministic: every
 member applies the same entries in the same order, so every member's store has the same
 revisions), `snapshot() -> bytes`, `restore(bytes)`. Peers talk the `amdkube.raft.Raft` gRPC
-service on the same port as the etcd client API.
+service on the peer listener only (store/etcdserver.py serves it apart from the client API,
+under peer TLS when configured); `channel(target)` makes the peer channels.
 """
 from __future__ import annotations
 
@@ -62,6 +72,7 @@ message SnapshotResponse { uint64 term = 1; }
 
 FOLLOWER, CANDIDATE, LEADER = "follower", "candidate", "leader"
 MAX_BATCH = 512
+_CHAN_OPTS = [("grpc.max_send_message_length", 256 << 20), ("grpc.max_receive_message_length", 256 << 20)]
 
 
 class NotLeader(Exception):
@@ -72,8 +83,10 @@ class NotLeader(Exception):
 
 class Raft:
     def __init__(self, name: str, peers: dict[str, str], data_dir: str | None, sm,
-                 heartbeat: float = 0.1, election: float = 1.0, compact_every: int = 10_000, fsync: bool = True):
+                 heartbeat: float = 0.1, election: float = 1.0, compact_every: int = 10_000, fsync: bool = True,
+                 channel=None):
         self.name, self.peers, self.sm = name, dict(peers), sm
+        self._channel = channel or (lambda target: grpc.aio.insecure_channel(target, options=_CHAN_OPTS))
         self.others = [p for p in sorted(peers) if p != name]
         self.heartbeat, self.election, self.compact_every, self.fsync = heartbeat, election, compact_every, fsync
         self.dir = os.path.join(data_dir, "raft") if data_dir else None
@@ -94,8 +107,14 @@ class Raft:
         self._last_heard = time.monotonic()
         self._timeout = self._new_timeout()
         self._logf = None
+        self.persisted = 0                       # highest log index durably on this member's disk
+        self._disk = asyncio.Lock()              # log file writers: the flusher, AppendEntries, snapshots
+        self._flushing = False                   # a flusher write is in flight in its worker thread
+        self._flush_ev = asyncio.Event()
+        self._apply_waiters: list[tuple[int, asyncio.Future]] = []
         self.leader_changed = asyncio.Event()
         self._load()
+        self.persisted = self.last_index()
 
     # ------------------------------------------------------------------ persistence
     def _load(self):
@@ -143,13 +162,16 @@ class Raft:
                 os.fsync(f.fileno())
         os.replace(p + ".tmp", p)
 
-    def _append_disk(self, entries):
-        if self._logf is None:
-            return
-        self._logf.write(b"".join(struct.pack(">I", len(b)) + b for b in (e.SerializeToString() for e in entries)))
-        self._logf.flush()
+    def _write_entries(self, f, entries):
+        f.write(b"".join(struct.pack(">I", len(b)) + b for b in (e.SerializeToString() for e in entries)))
+        f.flush()
         if self.fsync:
-            os.fsync(self._logf.fileno())
+            os.fdatasync(f.fileno())
+
+    def _append_disk(self, entries):
+        if self._logf is not None:
+            self._write_entries(self._logf, entries)
+        self.persisted = self.last_index()
 
     def _rewrite_log(self):
         if not self.dir:
@@ -164,6 +186,7 @@ class Raft:
                 os.fsync(f.fileno())
         os.replace(p + ".tmp", p)
         self._logf = open(p, "ab")
+        self.persisted = self.last_index()
 
     def _save_snapshot(self, data: bytes):
         if not self.dir:
@@ -200,12 +223,12 @@ class Raft:
     # ------------------------------------------------------------------ lifecycle
     async def start(self):
         for p in self.others:
-            ch = grpc.aio.insecure_channel(self.peers[p], options=[("grpc.max_send_message_length", 256 << 20),
-                                                                   ("grpc.max_receive_message_length", 256 << 20)])
+            ch = self._channel(self.peers[p])
             self._chans.append(ch)
             self._stubs[p] = RAFT.Raft.stub(ch)
         self._last_heard = time.monotonic()
         self._tasks.append(asyncio.create_task(self._ticker(), name="raft-ticker"))
+        self._tasks.append(asyncio.create_task(self._flusher(), name="raft-flusher"))
         if len(self.peers) == 1:
             await self._become_leader()
         return self
@@ -216,9 +239,13 @@ class Raft:
         for ch in self._chans:
             await ch.close()
         self._fail_pending(NotLeader(None))
-        if self._logf is not None:
-            self._logf.close()
-            self._logf = None
+        for _, fut in self._apply_waiters:
+            if not fut.done():
+                fut.cancel()
+        async with self._disk:                 # a flusher write still in its thread finishes first
+            if self._logf is not None:
+                self._logf.close()
+                self._logf = None
 
     def handler(self):
         return RAFT.Raft.handler(self)
@@ -295,12 +322,38 @@ class Raft:
 
     # ------------------------------------------------------------------ proposals
     def _append_local(self, data: bytes) -> int:
+        """Leader append: memory only; the flusher persists it with whatever else arrives
+        meanwhile (group commit) and the replicators ship it in their next batch."""
         e = RAFT.Entry(term=self.term, index=self.last_index() + 1, data=data)
         self.log.append(e)
-        self._append_disk([e])
+        self._flush_ev.set()
         for ev in self._kick.values():
             ev.set()
         return e.index
+
+    async def _flusher(self):
+        """One write + fdatasync for every entry appended since the previous one."""
+        while True:
+            await self._flush_ev.wait()
+            self._flush_ev.clear()
+            async with self._disk:
+                lo, hi = self.persisted + 1, self.last_index()
+                if hi < lo:
+                    continue
+                entries = self.log[max(0, lo - self.snap_index - 1):hi - self.snap_index]
+                if self._logf is not None and entries:
+                    self._flushing = True
+                    try:
+                        await asyncio.to_thread(self._write_entries, self._logf, entries)
+                    except OSError as e:
+                        log.error("raft %s: log write failed: %s", self.name, e)
+                        await asyncio.sleep(self.heartbeat)
+                        self._flush_ev.set()
+                        continue
+                    finally:
+                        self._flushing = False
+                self.persisted = max(self.persisted, hi)
+            self._advance_commit()
 
     async def propose(self, data: bytes, timeout: float = 10.0):
         """Replicate `data`; the state machine's result once a majority has it and it is applied here."""
@@ -309,7 +362,6 @@ class Raft:
         idx = self._append_local(data)
         fut = asyncio.get_running_loop().create_future()
         self._pending[idx] = (self.term, fut)
-        self._advance_commit()
         return await asyncio.wait_for(fut, timeout)
 
     def has_lease(self) -> bool:
@@ -326,7 +378,7 @@ class Raft:
             if self.role != LEADER:
                 raise NotLeader(self.leader)
             if self.has_lease() and self.term_at(self.commit) == self.term and self.applied >= self.commit:
-                return
+                return self.commit
             if time.monotonic() > end:
                 raise TimeoutError("raft: leadership not confirmed")
             for ev in self._kick.values():
@@ -343,7 +395,8 @@ class Raft:
                 if ni <= self.snap_index:
                     data = self.sm.snapshot() if self.applied == self.snap_index else None
                     if data is None:
-                        self._compact(force=True)
+                        async with self._disk:
+                            self._compact(force=True)
                         continue
                     r = await stub.InstallSnapshot(RAFT.SnapshotRequest(term=term, leader=self.name, last_index=self.snap_index,
                                                                          last_term=self.snap_term, data=data),
@@ -389,7 +442,7 @@ class Raft:
     def _advance_commit(self):
         if self.role != LEADER:
             return
-        matches = sorted([self.last_index()] + [self.match_index[p] for p in self.others], reverse=True)
+        matches = sorted([self.persisted] + [self.match_index[p] for p in self.others], reverse=True)
         n = matches[self.quorum() - 1]
         if n > self.commit and self.term_at(n) == self.term:
             self.commit = n
@@ -415,9 +468,28 @@ class Raft:
                     ent[1].set_exception(err)
                 else:
                     ent[1].set_result(result)
+        if self._apply_waiters:
+            keep = []
+            for idx, fut in self._apply_waiters:
+                if idx <= self.applied:
+                    if not fut.done():
+                        fut.set_result(None)
+                else:
+                    keep.append((idx, fut))
+            self._apply_waiters = keep
         self._compact()
 
+    async def wait_applied(self, index: int, timeout: float = 5.0):
+        """Until this member has applied `index` (a follower serving a ReadIndex read)."""
+        if self.applied >= index:
+            return
+        fut = asyncio.get_running_loop().create_future()
+        self._apply_waiters.append((index, fut))
+        await asyncio.wait_for(fut, timeout)
+
     def _compact(self, force: bool = False):
+        if self._flushing:
+            return                  # the flusher's thread holds the log file; the next apply compacts
         if not force and self.applied - self.snap_index < self.compact_every:
             return
         if self.applied <= self.snap_index:
@@ -445,6 +517,10 @@ class Raft:
         return RAFT.VoteResponse(term=self.term, granted=granted)
 
     async def AppendEntries(self, req, ctx):
+        async with self._disk:
+            return self._append_entries(req)
+
+    def _append_entries(self, req):
         if req.term < self.term:
             return RAFT.AppendResponse(term=self.term, success=False)
         if req.term > self.term or self.role != FOLLOWER or self.leader != req.leader:
@@ -477,8 +553,10 @@ class Raft:
             self.log.extend(new)
         if truncated:
             self._rewrite_log()
-        elif new:
-            self._append_disk(new)
+        elif self.persisted < self.last_index():
+            # the new entries, plus any a deposed leader appended but had not flushed yet: one
+            # write + fdatasync before the acknowledgement
+            self._append_disk(self.log[max(0, self.persisted - self.snap_index):])
         last_new = prev + len(req.entries)
         if req.leader_commit > self.commit:
             self.commit = min(req.leader_commit, max(last_new, self.commit))
@@ -486,6 +564,10 @@ class Raft:
         return RAFT.AppendResponse(term=self.term, success=True, match_index=last_new)
 
     async def InstallSnapshot(self, req, ctx):
+        async with self._disk:
+            return self._install_snapshot(req)
+
+    def _install_snapshot(self, req):
         if req.term < self.term:
             return RAFT.SnapshotResponse(term=self.term)
         self._step_down(req.term, req.leader)
@@ -505,4 +587,5 @@ class Raft:
 
     def status(self) -> dict:
         return {"name": self.name, "role": self.role, "term": self.term, "leader": self.leader, "commit": self.commit,
-                "applied": self.applied, "last_index": self.last_index(), "snap_index": self.snap_index}
+                "applied": self.applied, "last_index": self.last_index(), "persisted": self.persisted,
+                "snap_index": self.snap_index}

@@ -82,6 +82,27 @@ def timed_puts(store, n=N):
             "p99_ms": round(lat[int(n * 0.99)] * 1e3, 3)}
 
 
+async def concurrent_puts(endpoint, writers=64, n=4000):
+    """Raw etcd Puts from `writers` concurrent clients (one aio channel each) through `endpoint`."""
+    chans = [grpc.aio.insecure_channel(endpoint) for _ in range(writers)]
+    lat = []
+
+    async def writer(w):
+        kv = E.KV.stub(chans[w])
+        for i in range(w, n, writers):
+            a = time.perf_counter()
+            await kv.Put(E.PutRequest(key=f"/registry/conc/k{i}".encode(), value=VALUE), timeout=30)
+            lat.append(time.perf_counter() - a)
+    t0 = time.perf_counter()
+    await asyncio.gather(*(writer(w) for w in range(writers)))
+    el = time.perf_counter() - t0
+    for c in chans:
+        await c.close()
+    lat.sort()
+    return {"writers": writers, "puts": n, "puts_per_s": round(n / el, 1), "p50_ms": round(lat[n // 2] * 1e3, 3),
+            "p99_ms": round(lat[int(n * 0.99)] * 1e3, 3)}
+
+
 async def pod_creates(store, n=500):
     srv = await APIServer(store).start()
     c = Client(srv.url, token=srv.loopback_token)
@@ -109,6 +130,7 @@ async def main():
                 s.start(asyncio.get_running_loop())
                 out[label] = timed_puts(s)
                 s.close()
+                out[label]["concurrent"] = await concurrent_puts(eps[-1])
                 s = await asyncio.to_thread(Etcd3Store, eps[-1:] + eps[:-1])
                 out[label]["apiserver_pod_creates_per_s"] = await pod_creates(s)
                 s.close()

@@ -1,0 +1,9 @@
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+TAG=${TAG:-r4a}
+export TMPDIR=/tmp
+mkdir -p gpurun_out/$TAG
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/$TAG/pytest_gpu.log 2>&1 &&
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('SMOKE OK')" > gpurun_out/$TAG/smoke.log 2>&1 &&
+timeout -k 10 500 python -u bench.py --steps 20 --warmup 5 > gpurun_out/$TAG/bench_n1.log 2>&1 &&
+echo done

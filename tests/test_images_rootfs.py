@@ -97,6 +97,33 @@ def test_layer_cannot_write_outside_the_root(tmp_path, evil):
     assert lp.exists()     # nothing beside the root was whited out
 
 
+@pytest.mark.parametrize("victim_is_dir", [False, True])
+def test_layer_symlinked_parent_cannot_delete_host_files(tmp_path, victim_is_dir):
+    """A layer holding `x -> <host dir>` and then `x/victim` must be refused BEFORE the existing
+    `<host dir>/victim` is removed to make room for the new entry."""
+    host = tmp_path / "host"
+    host.mkdir()
+    if victim_is_dir:
+        (host / "victim").mkdir()
+        (host / "victim" / "keep").write_text("precious")
+    else:
+        (host / "victim").write_text("precious")
+    data = io.BytesIO()
+    with tarfile.open(fileobj=data, mode="w") as tf:
+        ti = tarfile.TarInfo("x")
+        ti.type, ti.linkname = tarfile.SYMTYPE, str(host)
+        tf.addfile(ti)
+        ti = tarfile.TarInfo("x/victim")
+        ti.size = 4
+        tf.addfile(ti, io.BytesIO(b"evil"))
+    lp = tmp_path / "layer.tar"
+    lp.write_bytes(data.getvalue())
+    with pytest.raises(ImageFormatError):
+        apply_layer(str(lp), str(tmp_path / "root"))
+    keep = host / "victim" / "keep" if victim_is_dir else host / "victim"
+    assert keep.read_text() == "precious"
+
+
 def _oci_layout(dirpath, layers, config):
     """Write an OCI image layout (gzip layers) to `dirpath`."""
     os.makedirs(os.path.join(dirpath, "blobs", "sha256"))

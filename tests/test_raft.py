@@ -208,3 +208,105 @@ async def test_raft_log_matching_votes_and_persistence(tmp_path):
     r2 = Raft("b", {"a": "127.0.0.1:1", "b": "127.0.0.1:2", "c": "127.0.0.1:3"}, str(tmp_path), _SM())
     assert (r2.term, r2.voted_for, r2.last_index(), r2.last_term()) == (3, "c", 4, 2)
     await r2.stop()
+
+
+async def _inproc_cluster(tmp_path, peer_tls=None, n=3):
+    from amdkube.store import MVCCStore
+    from amdkube.store.etcdserver import EtcdServer
+    ps = _ports(n)
+    peers = {f"m{i}": f"127.0.0.1:{ps[i]}" for i in range(n)}
+    srvs = {}
+    for nm in peers:
+        srvs[nm] = await EtcdServer(MVCCStore(None), name=nm, peers=peers, data_dir=str(tmp_path / nm), heartbeat=0.05,
+                                    election=0.4, peer_tls=peer_tls).start("127.0.0.1:0", None, peers[nm])
+    end = time.time() + 20
+    while time.time() < end:
+        leaders = [nm for nm, s in srvs.items() if s.raft.role == "leader"]
+        if len(leaders) == 1 and all(s.raft.leader == leaders[0] for s in srvs.values()):
+            return srvs, leaders[0], peers
+        await asyncio.sleep(0.05)
+    raise AssertionError("no leader")
+
+
+@pytest.mark.timeout(120)
+async def test_group_commit_batches_concurrent_proposals(tmp_path, monkeypatch):
+    """256 concurrent Puts through a follower: every one commits at its own revision, and the
+    leader persisted them with far fewer log writes (one write + fdatasync per flush) than
+    proposals — the Ready batching of etcd (raft/node.go:52, etcdserver/raft.go:134)."""
+    from amdkube.store.raft import Raft
+    writes = {"n": 0}
+    orig = Raft._write_entries
+
+    def counting(self, f, entries):
+        if self.role == "leader":
+            writes["n"] += 1
+        return orig(self, f, entries)
+    monkeypatch.setattr(Raft, "_write_entries", counting)
+    srvs, leader, _ = await _inproc_cluster(tmp_path)
+    try:
+        follower = next(nm for nm in srvs if nm != leader)
+        ch = grpc.aio.insecure_channel(srvs[follower].address)
+        kv = E.KV.stub(ch)
+        base = writes["n"]
+        rs = await asyncio.gather(*(kv.Put(E.PutRequest(key=f"/g/{i}".encode(), value=b"v"), timeout=20) for i in range(256)))
+        revs = sorted(r.header.revision for r in rs)
+        assert revs == list(range(revs[0], revs[0] + 256))
+        flushes = writes["n"] - base
+        assert flushes < 128, flushes
+        # a follower's linearizable read (ReadIndex over the peer channel) sees every write
+        r = await kv.Range(E.RangeRequest(key=b"/g/", range_end=prefix_end(b"/g/")), timeout=10)
+        assert r.count == 256
+        await ch.close()
+    finally:
+        for s in srvs.values():
+            await s.stop()
+
+
+@pytest.mark.timeout(120)
+async def test_peer_listener_serves_only_member_traffic_under_mutual_tls(tmp_path):
+    """The client API is not reachable on the peer listener and raft is not reachable on the
+    client listener; with peer TLS a client without a member certificate cannot reach the peer
+    services at all (advisor r3: the peer port bypassed client TLS)."""
+    from amdkube.kubeadm import new_ca, new_cert
+    from amdkube.store.etcdserver import PEER
+    from amdkube.store.raft import RAFT
+    d = tmp_path / "pki"
+    d.mkdir()
+    new_ca(str(d), "peer-ca", "etcd-peer-ca")
+    new_cert(str(d), "peer", "etcd-peer", sans=("IP:127.0.0.1", "DNS:localhost"), server="peer", ca="peer-ca")
+    tls = (str(d / "peer.crt"), str(d / "peer.key"), str(d / "peer-ca.crt"))
+    srvs, leader, peers = await _inproc_cluster(tmp_path, peer_tls=tls)
+    try:
+        s = srvs[leader]
+        async with grpc.aio.insecure_channel(s.address) as ch:
+            await E.KV.stub(ch).Put(E.PutRequest(key=b"/t/a", value=b"1"), timeout=10)
+        # raft is not on the client port
+        async with grpc.aio.insecure_channel(s.address) as ch:
+            with pytest.raises(grpc.RpcError) as ei:
+                await RAFT.Raft.stub(ch).InstallSnapshot(RAFT.SnapshotRequest(term=99, leader="x"), timeout=5)
+            assert ei.value.code() == grpc.StatusCode.UNIMPLEMENTED
+        # plaintext to the peer port fails
+        async with grpc.aio.insecure_channel(peers[leader]) as ch:
+            with pytest.raises(grpc.RpcError):
+                await PEER.Peer.stub(ch).Propose(PEER.ProposeRequest(data=b"\x02"), timeout=3)
+        # TLS without a client certificate fails the handshake
+        ca = open(tls[2], "rb").read()
+        async with grpc.aio.secure_channel(peers[leader], grpc.ssl_channel_credentials(root_certificates=ca)) as ch:
+            with pytest.raises(grpc.RpcError):
+                await PEER.Peer.stub(ch).ReadIndex(PEER.ReadIndexRequest(), timeout=3)
+        # a member certificate reaches Peer, but never the client services
+        async with s._peer_channel(peers[leader]) as ch:
+            r = await PEER.Peer.stub(ch).ReadIndex(PEER.ReadIndexRequest(), timeout=5)
+            assert r.index >= 1 and not r.code
+            with pytest.raises(grpc.RpcError) as ei:
+                await E.KV.stub(ch).Range(E.RangeRequest(key=b"/t/a"), timeout=5)
+            assert ei.value.code() == grpc.StatusCode.UNIMPLEMENTED
+        # writes through a follower still commit over the TLS peer channel
+        follower = next(nm for nm in srvs if nm != leader)
+        async with grpc.aio.insecure_channel(srvs[follower].address) as ch:
+            await E.KV.stub(ch).Put(E.PutRequest(key=b"/t/b", value=b"2"), timeout=10)
+            r = await E.KV.stub(ch).Range(E.RangeRequest(key=b"/t/b"), timeout=10)
+            assert r.kvs[0].value == b"2"
+    finally:
+        for s in srvs.values():
+            await s.stop()
