@@ -104,7 +104,7 @@ ALL = {
     "pvc-protection": lambda mgr, o: PVCProtectionController(mgr),
     "pv-protection": lambda mgr, o: PVProtectionController(mgr),
     "service": lambda mgr, o: ServiceLBController(mgr, o.cloud, o.cluster_name),
-    "route": lambda mgr, o: RouteController(mgr, o.cloud, o.cluster_name),
+    "route": lambda mgr, o: RouteController(mgr, o.cloud, o.cluster_name, o.cluster_cidr),
     # cloud-controller-manager only (cmd/cloud-controller-manager/app/controllermanager.go)
     "cloud-node": lambda mgr, o: CloudNodeController(mgr, o.cloud, o.extra.get("node_status_update_frequency", 300.0),
                                                      o.extra.get("node_monitor_period", 5.0)),

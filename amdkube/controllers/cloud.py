@@ -12,6 +12,7 @@ Reference:
 from __future__ import annotations
 
 import asyncio
+import ipaddress
 import logging
 
 from ..api import meta as m
@@ -77,10 +78,22 @@ class RouteController(Controller):
     workers = 1
     period = 10.0
 
-    def __init__(self, mgr, cloud, cluster_name: str = "kubernetes"):
+    def __init__(self, mgr, cloud, cluster_name: str = "kubernetes", cluster_cidr: str = "10.244.0.0/16"):
         super().__init__(mgr)
         self.cloud, self.cluster = cloud, cluster_name
+        self.cluster_cidr = ipaddress.ip_network(cluster_cidr, strict=False)
         self._poll = None
+
+    def responsible_for(self, r) -> bool:
+        """route_controller.go:264-275 isResponsibleForRoute: only routes whose destination
+        (first and last address) lies inside --cluster-cidr are ours to delete — a NAT default
+        route or a tenant route in the same table is never touched."""
+        try:
+            net = ipaddress.ip_network(r.destination_cidr, strict=False)
+        except ValueError:
+            return False
+        c = self.cluster_cidr
+        return net.version == c.version and c[0] <= net[0] and net[-1] <= c[-1]
 
     def setup(self):
         self.node_inf = self.mgr.nodes
@@ -123,9 +136,7 @@ class RouteController(Controller):
                 await asyncio.to_thread(routes.create, self.cluster, r.name, r)
         for r in have:
             w = want.get(r.target_node)
-            if (w is None or w.destination_cidr != r.destination_cidr) and \
-                    (r.name.startswith(self.cluster + "-") or r.target_node in {m.name_of(n) for n in self.node_inf.list()}
-                     or not getattr(routes, "named", True)):
+            if (w is None or w.destination_cidr != r.destination_cidr) and self.responsible_for(r):
                 await asyncio.to_thread(routes.delete, self.cluster, r)
         for n in self.node_inf.list():
             if m.name_of(n) not in want:

@@ -1038,6 +1038,30 @@ class Kubelet:
             if not self._device_starting:
                 self._device_idle.set()
 
+    def _device_start_pause(self, uid: str):
+        """Out of the start window without counting as started (the gate re-adds it later)."""
+        if uid in self._device_starting:
+            self._device_starting.discard(uid)
+            if not self._device_starting:
+                self._device_idle.set()
+
+    async def _context_holding_device_window(self, uid: str, pod: dict) -> dict:
+        """The pod's volumes/env context. A device pod whose volumes take longer than the start
+        window (a missing ConfigMap waits up to the mount timeout) stops holding device-less
+        pods behind it; the start gate takes it back once its volumes are there."""
+        if uid not in self._device_starting:
+            return await self._pod_context(pod)
+        task = asyncio.ensure_future(self._pod_context(pod))
+        try:
+            try:
+                return await asyncio.wait_for(asyncio.shield(task), self.cfg.device_pod_start_window)
+            except asyncio.TimeoutError:
+                self._device_start_pause(uid)
+                return await task
+        finally:
+            if not task.done():
+                task.cancel()
+
     @staticmethod
     def _holds_devices(pod: dict) -> bool:
         spec = pod.get("spec") or {}
@@ -1047,7 +1071,17 @@ class Kubelet:
                    for c in spec.get("containers") or [] for k in ((c.get("resources") or {}).get("limits") or {}))
 
     async def sync_pod(self, uid: str) -> bool:
-        """Returns True when the worker for this pod is finished (pod gone from the node)."""
+        """Returns True when the worker for this pod is finished (pod gone from the node).
+
+        Whatever path a sync takes (rejected, deleted, terminal, waiting on a volume, started),
+        it ends the pod's device-start window, so a GPU pod that waits on a missing Secret does
+        not hold every device-less pod's first start behind `device_pod_start_window`."""
+        try:
+            return await self._sync_pod(uid)
+        finally:
+            self._device_start_done(uid)
+
+    async def _sync_pod(self, uid: str) -> bool:
         pod = self.pods.get(uid)
         if pod is None:
             await self.runtime.kill_and_remove(uid, self._cached_sandboxes(uid))
@@ -1110,7 +1144,7 @@ class Kubelet:
             self.status.set(pod, st)
             return False
         try:
-            ctx = await self._pod_context(pod)
+            ctx = await self._context_holding_device_window(uid, pod)
         except VolumeError as e:
             # kubelet.go syncPod: "Unable to mount volumes for pod": the pod waits in
             # ContainerCreating and the sync is retried

@@ -472,3 +472,55 @@ async def test_cloud_load_balancer_and_routes():
 
 async def _true(v):
     return v
+
+
+async def test_route_controller_deletes_only_routes_inside_the_cluster_cidr():
+    """route_controller.go:264-275 isResponsibleForRoute: a NAT-instance default route named like
+    an instance route (AWS lists every instance route as `{cluster}-{cidr}`) and a tenant route
+    outside --cluster-cidr survive; a stale in-cluster route is deleted."""
+    from amdkube.cloudprovider import Route
+    from amdkube.controllers.cloud import RouteController
+
+    class Routes:
+        named = False
+
+        def __init__(self):
+            self.rs = [Route("kubernetes-0.0.0.0/0", "nat-instance", "0.0.0.0/0"),
+                       Route("tenant", "db-server", "172.16.5.0/24"),
+                       Route("kubernetes-stale", "gone-node", "10.244.7.0/24"),
+                       Route("kubernetes-n1", "n1", "10.244.1.0/24")]
+            self.deleted = []
+
+        def list(self, cluster):
+            return list(self.rs)
+
+        def create(self, cluster, name, r):
+            self.rs.append(r)
+
+        def delete(self, cluster, r):
+            self.deleted.append(r.destination_cidr)
+            self.rs.remove(r)
+
+    class Cloud:
+        def __init__(self):
+            self.r = Routes()
+
+        def routes(self):
+            return self.r
+
+    class Nodes:
+        def list(self):
+            return [{"metadata": {"name": "n1", "uid": "u1"}, "spec": {"podCIDR": "10.244.1.0/24"}, "status": {
+                "conditions": [{"type": "NetworkUnavailable", "status": "False"}]}}]
+
+    class Mgr:
+        client = None
+        nodes = Nodes()
+    cloud = Cloud()
+    rc = RouteController(Mgr(), cloud, "kubernetes", "10.244.0.0/16")
+    rc.node_inf = Mgr.nodes
+    await rc.sync("@all")
+    assert cloud.r.deleted == ["10.244.7.0/24"]
+    assert {r.destination_cidr for r in cloud.r.rs} == {"0.0.0.0/0", "172.16.5.0/24", "10.244.1.0/24"}
+    assert not rc.responsible_for(Route("x", "n", "10.0.0.0/8"))          # wider than the cluster CIDR
+    assert rc.responsible_for(Route("x", "n", "10.244.255.0/24"))

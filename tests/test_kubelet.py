@@ -448,3 +448,31 @@ def test_gc_treats_unknown_pods_as_deleted_only_when_sources_ready(tmp_path):
         assert sorted(c.id for c in cri2.conts) == ["gone-y-2", "live-x-2", "live-y-2"]
 
     run(go(), 30)
+
+
+async def test_gpu_pod_waiting_on_a_volume_does_not_hold_the_device_start_window():
+    """A GPU pod stuck on a missing ConfigMap leaves the kubelet's device-start set, so a
+    device-less pod's first start is not delayed by device_pod_start_window (advisor r3)."""
+    import time as _t
+    from amdkube.localcluster import LocalCluster, wait_pod
+    async with LocalCluster(gpus="fake", n_gpus=1, with_controllers=False, relist_period=0.2,
+                            kubelet_kw={"device_pod_start_window": 1.0}) as lc:
+        c = lc.client
+        await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "gpu-stuck"},
+                        "spec": {"containers": [{"name": "c", "image": "busybox", "command": ["sleep", "30"],
+                                                 "resources": {"limits": {"amd.com/gpu": "1"}},
+                                                 "volumeMounts": [{"name": "cfg", "mountPath": "/cfg"}]}],
+                                 "volumes": [{"name": "cfg", "configMap": {"name": "does-not-exist"}}]}}, "default")
+        end = _t.time() + 10
+        seen = False
+        while _t.time() < end:
+            seen = seen or bool(lc.kubelet._device_starting)
+            if seen and not lc.kubelet._device_starting:
+                break
+            await asyncio.sleep(0.02)
+        assert seen and not lc.kubelet._device_starting
+        t0 = _t.time()
+        await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "plain"},
+                        "spec": {"containers": [{"name": "c", "image": "busybox", "command": ["sleep", "30"]}]}}, "default")
+        await wait_pod(c, "default", "plain", ("Running",), 20)
+        assert _t.time() - t0 < 0.9, "the device-less pod waited out the device-start window"
