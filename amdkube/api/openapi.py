@@ -133,6 +133,15 @@ def definitions() -> dict:
         defs[full] = {"description": d["desc"], "properties": props}
         if req:
             defs[full]["required"] = req
+    # the strategic-merge-patch struct tags, as the reference's swagger.json carries them
+    from .patchmeta import PATCH_META
+    for full, fields in PATCH_META.items():
+        for fname, (strategy, key) in fields.items():
+            p = (defs.get(full) or {}).get("properties", {}).get(fname)
+            if p is not None:
+                p["x-kubernetes-patch-strategy"] = strategy
+                if key:
+                    p["x-kubernetes-patch-merge-key"] = key
     kinds = _kind_defs(defs)
     for (g, v, k), full in sorted(kinds.items()):
         defs[full].setdefault("x-kubernetes-group-version-kind", []).append({"group": g, "version": v, "kind": k})

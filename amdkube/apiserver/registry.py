@@ -45,43 +45,6 @@ def _json_merge_patch(target, patch):
     return out
 
 
-_MERGE_KEYS = {"containers": "name", "initContainers": "name", "volumes": "name", "env": "name", "ports": "containerPort",
-               "volumeMounts": "mountPath", "conditions": "type", "extendedResources": "name", "tolerations": "key",
-               "taints": "key", "addresses": "type"}
-
-
-def _strategic_merge_patch(target, patch, key=None):
-    """Strategic merge: like merge-patch, but lists with a known merge key merge by key."""
-    if isinstance(patch, list) and isinstance(target, list) and key in _MERGE_KEYS:
-        mk = _MERGE_KEYS[key]
-        out = [copy.deepcopy(x) for x in target]
-        idx = {x.get(mk): i for i, x in enumerate(out) if isinstance(x, dict)}
-        for item in patch:
-            if isinstance(item, dict) and item.get("$patch") == "delete":
-                if item.get(mk) in idx:
-                    out = [x for x in out if not (isinstance(x, dict) and x.get(mk) == item.get(mk))]
-                    idx = {x.get(mk): i for i, x in enumerate(out) if isinstance(x, dict)}
-                continue
-            if isinstance(item, dict) and item.get(mk) in idx:
-                out[idx[item[mk]]] = _strategic_merge_patch(out[idx[item[mk]]], item)
-            else:
-                out.append(copy.deepcopy(item))
-        return out
-    if not isinstance(patch, dict):
-        return copy.deepcopy(patch)
-    if not isinstance(target, dict):
-        target = {}
-    out = dict(target)
-    for k, v in patch.items():
-        if k.startswith("$"):
-            continue
-        if v is None:
-            out.pop(k, None)
-        else:
-            out[k] = _strategic_merge_patch(target.get(k), v, k)
-    return out
-
-
 def _json_pointer(path):
     return [p.replace("~1", "/").replace("~0", "~") for p in path.lstrip("/").split("/")] if path else []
 
@@ -122,6 +85,10 @@ def _json_patch(doc, ops):
 
 
 def apply_patch(cur: dict, patch_body: bytes, content_type: str) -> dict:
+    """PATCH (staging/src/k8s.io/apiserver/pkg/endpoints/handlers/patch.go): JSON patch, JSON
+    merge patch, or strategic merge patch interpreted against the kind's schema (the patch
+    strategy and merge key of every nested field, api/strategicpatch.py). Custom resources have
+    no strategic schema: the reference answers 415 for them."""
     try:
         patch = json.loads(patch_body)
     except ValueError as e:
@@ -129,7 +96,18 @@ def apply_patch(cur: dict, patch_body: bytes, content_type: str) -> dict:
     if "json-patch" in content_type:
         return _json_patch(cur, patch)
     if "strategic-merge" in content_type:
-        return _strategic_merge_patch(cur, patch)
+        from ..api import strategicpatch as smp
+        node = smp.schema_for(cur.get("apiVersion"), cur.get("kind"))
+        if node is None and SCHEME.for_kind(cur.get("apiVersion") or "", cur.get("kind") or "") is None:
+            raise m.StatusError(415, "UnsupportedMediaType",
+                                f"the body of the request was in an unknown format - accepted media types include: "
+                                f"application/json-patch+json, application/merge-patch+json")
+        try:
+            return smp.apply(cur, patch, node)
+        except smp.PatchError as e:
+            raise m.bad_request(str(e))
+    if not isinstance(patch, dict):
+        raise m.bad_request("a merge patch must be a JSON object")
     return _json_merge_patch(cur, patch)
 
 

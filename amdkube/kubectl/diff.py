@@ -34,7 +34,7 @@ def _file_name(obj: dict) -> str:
 
 def merged(local: dict, live: dict | None) -> dict:
     """The object apply would leave on the server."""
-    from ..apiserver.registry import _strategic_merge_patch
+    from ..api import strategicpatch as smp
     if live is None:
         out = copy.deepcopy(local)
         out.setdefault("metadata", {}).setdefault("annotations", {})[LAST_APPLIED] = json.dumps(local, sort_keys=True)
@@ -43,7 +43,13 @@ def merged(local: dict, live: dict | None) -> dict:
     modified = copy.deepcopy(local)
     modified.setdefault("metadata", {}).setdefault("annotations", {})[LAST_APPLIED] = json.dumps(local, sort_keys=True)
     patch = three_way(original, modified, live)
-    return copy.deepcopy(live) if patch is _SAME else _strategic_merge_patch(copy.deepcopy(live), patch)
+    if patch is _SAME:
+        return copy.deepcopy(live)
+    node = smp.schema_for(live.get("apiVersion"), live.get("kind"))
+    if node is None and SCHEME.for_object(live) is None:
+        from ..apiserver.registry import _json_merge_patch
+        return _json_merge_patch(copy.deepcopy(live), patch)
+    return smp.apply(live, patch, node)
 
 
 async def version_of(c, which: str, local: dict, ns_default: str) -> dict | None:

@@ -1,7 +1,9 @@
 """kubectl: the rest of the reference release's command set (pkg/kubectl/cmd).
 
   * apply with a real three-way merge (apply.go: patch = last-applied → manifest → live,
-    deletions for fields the manifest dropped, `$patch: delete` for list items),
+    deletions for fields the manifest dropped, `$patch: delete` for list items, all driven by
+    the kind's patch strategies and merge keys — api/strategicpatch.py), a JSON-merge three-way
+    patch for custom resources, 409 retries and --force re-creation,
     `--prune -l` (apply.go pruner: objects with a last-applied annotation matching the selector
     that the manifests no longer contain), `apply view-last-applied|set-last-applied|
     edit-last-applied`;
@@ -27,47 +29,30 @@ import sys
 import yaml
 
 from ..api import meta as m
+from ..api import strategicpatch as smp
 from ..api.scheme import SCHEME
 from .extra import _ns, _res, _target
 
 LAST_APPLIED = "kubectl.kubernetes.io/last-applied-configuration"
-_MERGE_KEYS = {"containers": "name", "initContainers": "name", "volumes": "name", "env": "name", "ports": "containerPort",
-               "volumeMounts": "mountPath", "extendedResources": "name", "tolerations": "key", "imagePullSecrets": "name"}
-
-
 # ---------------------------------------------------------------- three-way merge
-def three_way(original, modified, current, key=None):
-    """strategicpatch.CreateThreeWayMergePatch for JSON objects: what turns `current` into
-    `modified`, deleting what `original` (the last applied manifest) had and `modified` drops."""
-    if isinstance(modified, dict) and isinstance(current, dict):
-        patch = {}
-        original = original if isinstance(original, dict) else {}
-        for k in original:
-            if k not in modified and k in current:
-                patch[k] = None
-        for k, v in modified.items():
-            sub = three_way(original.get(k), v, current.get(k), k)
-            if sub is not _SAME:
-                patch[k] = sub
-        return patch if patch else _SAME
-    if isinstance(modified, list) and isinstance(current, list) and key in _MERGE_KEYS and \
-            all(isinstance(x, dict) for x in modified + current):
-        mk = _MERGE_KEYS[key]
-        cur = {x.get(mk): x for x in current}
-        orig = {x.get(mk): x for x in (original or []) if isinstance(x, dict)}
-        out = []
-        for item in modified:
-            kv = item.get(mk)
-            if kv in cur:
-                sub = three_way(orig.get(kv), item, cur[kv], None)
-                if sub is not _SAME:
-                    out.append({mk: kv, **sub})
-            else:
-                out.append(item)
-        names = {x.get(mk) for x in modified}
-        out += [{mk: kv, "$patch": "delete"} for kv in orig if kv not in names and kv in cur]
-        return out if out else _SAME
-    return _SAME if modified == current else modified
+def apply_patch_for(original: dict | None, modified: dict, current: dict) -> tuple[dict | None, str]:
+    """(patch, content type) that turns `current` into `modified`, deleting what `original`
+    (the last applied manifest) had and `modified` drops (apply.go patcher.patchSimple):
+    a strategic three-way patch over the kind's schema (strategicpatch.CreateThreeWayMergePatch)
+    for built-in kinds, a JSON merge three-way patch for kinds without one (custom resources).
+    None when nothing changes."""
+    node = smp.schema_for(modified.get("apiVersion"), modified.get("kind"))
+    if node is None and SCHEME.for_object(modified) is None:
+        patch, ctype = smp.create_three_way_json_merge(original, modified, current), "application/merge-patch+json"
+    else:
+        patch, ctype = smp.create_three_way(original, modified, current, node), "application/strategic-merge-patch+json"
+    return (patch or None), ctype
+
+
+def three_way(original, modified, current):
+    """The apply patch alone (kubectl diff's MERGED view and tests); _SAME when empty."""
+    patch, _ = apply_patch_for(original, modified, current)
+    return _SAME if patch is None else patch
 
 
 class _Same:
@@ -100,14 +85,42 @@ async def apply_docs(c, a, docs):
         original = json.loads(m.annotations_of(cur).get(LAST_APPLIED) or "{}")
         modified = copy.deepcopy(doc)
         modified.setdefault("metadata", {}).setdefault("annotations", {})[LAST_APPLIED] = manifest
-        patch = three_way(original, modified, cur)
-        if patch is _SAME:
-            print(f"{ri.kind.lower()}/{name} unchanged")
-            continue
-        await c.patch(res, name, patch, ns, patch_type="application/strategic-merge-patch+json")
-        print(f"{ri.kind.lower()}/{name} configured")
+        for attempt in range(5):            # apply.go maxPatchRetry: a 409 re-reads the live object
+            try:
+                patch, ctype = apply_patch_for(original, modified, cur)
+            except smp.PatchError as e:
+                raise SystemExit(f"error: {ri.kind.lower()}/{name}: {e}")
+            if patch is None:
+                print(f"{ri.kind.lower()}/{name} unchanged")
+                break
+            try:
+                await c.patch(res, name, patch, ns, patch_type=ctype)
+            except m.StatusError as e:
+                if e.code == 409 and attempt < 4:
+                    cur = await c.get(res, name, ns)
+                    continue
+                if getattr(a, "force", False) and e.code in (409, 422):
+                    await c.delete(res, name, ns)             # --force: delete and re-create
+                    await _wait_gone(c, res, name, ns)
+                    doc.setdefault("metadata", {}).setdefault("annotations", {})[LAST_APPLIED] = manifest
+                    await c.create(doc, ns)
+                    print(f"{ri.kind.lower()}/{name} replaced")
+                    break
+                raise
+            print(f"{ri.kind.lower()}/{name} configured")
+            break
     if getattr(a, "prune", False):
         await _prune(c, a, applied)
+
+
+async def _wait_gone(c, res, name, ns, timeout: float = 30.0):
+    import asyncio
+    import time
+    end = time.monotonic() + timeout
+    while await c.get_or_none(res, name, ns) is not None:
+        if time.monotonic() > end:
+            raise SystemExit(f"error: timed out waiting for {res}/{name} to be deleted")
+        await asyncio.sleep(0.2)
 
 
 PRUNE_WHITELIST = ("configmaps", "endpoints", "namespaces", "persistentvolumeclaims", "persistentvolumes", "pods",

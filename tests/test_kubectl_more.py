@@ -18,14 +18,16 @@ from tests.test_rollout import kubectl
 
 
 def test_three_way_patch():
-    orig = {"metadata": {"labels": {"a": "1", "b": "2"}}, "spec": {"containers": [{"name": "x", "image": "i1"},
-                                                                                 {"name": "y", "image": "i2"}]}}
-    cur = {"metadata": {"labels": {"a": "1", "b": "2", "c": "live"}}, "spec": {"containers": [
+    pod = {"apiVersion": "v1", "kind": "Pod"}
+    orig = {**pod, "metadata": {"labels": {"a": "1", "b": "2"}}, "spec": {"containers": [{"name": "x", "image": "i1"},
+                                                                                        {"name": "y", "image": "i2"}]}}
+    cur = {**pod, "metadata": {"labels": {"a": "1", "b": "2", "c": "live"}}, "spec": {"containers": [
         {"name": "x", "image": "i1", "imagePullPolicy": "Always"}, {"name": "y", "image": "i2"}]}}
-    mod = {"metadata": {"labels": {"a": "1"}}, "spec": {"containers": [{"name": "x", "image": "i9"}]}}
+    mod = {**pod, "metadata": {"labels": {"a": "1"}}, "spec": {"containers": [{"name": "x", "image": "i9"}]}}
     p = three_way(orig, mod, cur)
     assert p == {"metadata": {"labels": {"b": None}},
-                 "spec": {"containers": [{"name": "x", "image": "i9"}, {"name": "y", "$patch": "delete"}]}}
+                 "spec": {"$setElementOrder/containers": [{"name": "x"}],
+                          "containers": [{"name": "x", "image": "i9"}, {"name": "y", "$patch": "delete"}]}}
     assert three_way(orig, orig, orig) is _SAME
 
 
@@ -144,3 +146,35 @@ def test_kubectl_rolling_update():
             assert [m.name_of(x) for x in rcs] == ["frontend"]
             assert rcs[0]["spec"]["template"]["spec"]["containers"][0]["image"] == "python:3"
     run(go(), 90)
+
+
+def test_apply_two_port_service_and_strategic_patch_of_ports(tmp_path, capsys):
+    """Round-3 review repro: `kubectl apply` of a 2-port Service with one changed targetPort
+    kept only a duplicated port, and a strategic PATCH of spec.ports failed in the server.
+    ServiceSpec.ports merges by `port` (core/v1/types.go:3372)."""
+    async def go():
+        async with LocalCluster(gpus="none", with_kubelet=False, with_controllers=False) as lc:
+            c = lc.client
+
+            def svc(tp):
+                return {"apiVersion": "v1", "kind": "Service", "metadata": {"name": "web", "namespace": "default"},
+                        "spec": {"selector": {"app": "web"}, "ports": [
+                            {"name": "http", "port": 80, "targetPort": tp},
+                            {"name": "https", "port": 443, "targetPort": 8443}]}}
+            await kubectl(c, "apply", "-f", _write(tmp_path, "s1.yaml", [svc(8080)]))
+            await kubectl(c, "apply", "-f", _write(tmp_path, "s2.yaml", [svc(8081)]))
+            live = await c.get("services", "web", "default")
+            ports = {p["name"]: (p["port"], p["targetPort"]) for p in live["spec"]["ports"]}
+            assert ports == {"http": (80, 8081), "https": (443, 8443)}
+            assert len(live["spec"]["ports"]) == 2
+            # a strategic PATCH of one port by its merge key
+            out = await c.patch("services", "web", {"spec": {"ports": [{"port": 443, "targetPort": 9443}]}}, "default",
+                                patch_type="application/strategic-merge-patch+json")
+            assert [(p["port"], p["targetPort"]) for p in out["spec"]["ports"]] == [(80, 8081), (443, 9443)]
+            # a port dropped from the manifest is removed, the other kept
+            one = svc(8081)
+            one["spec"]["ports"] = one["spec"]["ports"][:1]
+            await kubectl(c, "apply", "-f", _write(tmp_path, "s3.yaml", [one]))
+            live = await c.get("services", "web", "default")
+            assert [p["port"] for p in live["spec"]["ports"]] == [80]
+    run(go())
