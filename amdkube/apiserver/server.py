@@ -14,6 +14,7 @@ Fast paths (all single-threaded on the event loop, no locks):
 from __future__ import annotations
 
 import asyncio
+import collections
 import json
 import logging
 import random
@@ -200,6 +201,9 @@ class APIServer:
                                ["verb", "resource", "subresource", "code"], registry=self.metrics)
         self.m_lat = Histogram("apiserver_request_latencies", "Response latency distribution in microseconds for each verb, resource and subresource.",
                                ["verb", "resource", "subresource"], buckets=MICRO_BUCKETS, registry=self.metrics)
+        # exact per-request latencies for the SLO report (metrics_util.go HighLatencyRequests
+        # reads the apiserver's latency summary quantiles; this keeps the raw samples instead)
+        self.lat_samples: collections.deque = collections.deque(maxlen=200_000)
         self.watch_count = 0
         self.app = web.Application(client_max_size=64 * 1024 * 1024,
                                    middlewares=([self._cors_middleware] if self.opts.get("cors_allowed_origins") else []) +
@@ -676,7 +680,31 @@ class APIServer:
                 self.auditor.stage(actx, "ResponseComplete", code, getattr(request, "_read_bytes", None), resp)
             self.m_count.labels(verb, resource or "", sub or "", str(code)).inc()
             if verb != "WATCH":
-                self.m_lat.labels(verb, resource or "", sub or "").observe((time.perf_counter() - t0) * 1e6)
+                dt = time.perf_counter() - t0
+                self.m_lat.labels(verb, resource or "", sub or "").observe(dt * 1e6)
+                self.lat_samples.append((verb, resource or "", sub or "", dt))
+
+    def latency_summary(self, since: int = 0) -> dict:
+        """API call latency percentiles over the samples from index `since` on, as the
+        reference's density SLO reads them (test/e2e/framework/metrics_util.go:52-59): the worst
+        (verb, resource, subresource) p99 of non-LIST calls (limit 1 s) and of LISTs (5 s)."""
+        groups: dict[tuple, list] = {}
+        for verb, res, sub, dt in list(self.lat_samples)[since:]:
+            if verb in ("WATCH", "CONNECT"):
+                continue
+            groups.setdefault((verb, res, sub), []).append(dt)
+
+        def p(xs, q):
+            xs = sorted(xs)
+            return xs[min(len(xs) - 1, int(q / 100.0 * len(xs)))]
+        rows = [{"verb": v, "resource": r, "subresource": s, "count": len(xs), "p50_ms": round(p(xs, 50) * 1e3, 3),
+                 "p90_ms": round(p(xs, 90) * 1e3, 3), "p99_ms": round(p(xs, 99) * 1e3, 3)} for (v, r, s), xs in groups.items()]
+        rows.sort(key=lambda x: -x["p99_ms"])
+        nonlist = [x for x in rows if x["verb"] != "LIST"]
+        lists = [x for x in rows if x["verb"] == "LIST"]
+        return {"api_p99_ms": nonlist[0]["p99_ms"] if nonlist else None,
+                "api_list_p99_ms": lists[0]["p99_ms"] if lists else None,
+                "calls": sum(x["count"] for x in rows), "worst": rows[:5]}
 
     async def _body(self, request):
         data = await request.read()

@@ -13,8 +13,16 @@ Startup latency (the SLO metric, ≤ 5 s p50/p90/p99) is reported for the first 
 burst (pods that found a free GPU at creation, i.e. no queueing); node-side latency
 (bind → start) is reported for every pod.
 
+Node density (test/e2e_node/density_test.go, {"cmd":"node_density"}): the reference's two
+limit-checked tests on this node — a batch of 10 pods created at once (startup p50/p90/p99 ≤
+16/18/20 s, whole batch ≤ 25 s, :72-92) and 10 pods created in sequence beside 50 running
+background pods (p50/p90/p99 ≤ 5/9/10 s, :213-229) — run with pause pods as in the reference
+and again with GPU pods, while the kubelet's and the runtime's CPU (cores, per 1 s window,
+p50/p95 ≤ 0.30/0.50 and 0.40/0.60) and RSS (≤ 100 / 500 MiB, :76-83) are sampled, plus the
+apiserver's API call p99 (≤ 1 s, test/e2e/framework/metrics_util.go:52).
+
 Protocol (stdin/stdout JSON lines, used by bench.py): {"cmd":"run","steps":K} → result line;
-{"cmd":"quit"}.
+{"cmd":"node_density"} → result line; {"cmd":"quit"}.
 """
 from __future__ import annotations
 
@@ -43,6 +51,77 @@ def pct(xs, q):
     return xs[k]
 
 
+# test/e2e_node/density_test.go:72-92, 76-83, 213-229; test/e2e/framework/metrics_util.go:52
+DENSITY_LIMITS = {"batch10_startup_ms": {"p50": 16000, "p90": 18000, "p99": 20000}, "batch10_batch_ms": 25000,
+                  "seq10_bg50_startup_ms": {"p50": 5000, "p90": 9000, "p99": 10000},
+                  "kubelet_cpu_cores": {"p50": 0.30, "p95": 0.50}, "runtime_cpu_cores": {"p50": 0.40, "p95": 0.60},
+                  "kubelet_rss_mib": 100, "runtime_rss_mib": 500, "api_p99_ms": 1000}
+
+
+class ResourceSampler:
+    """density_test.go's ResourceCollector (1 s housekeeping): CPU cores per 1 s window and RSS
+    of named node daemons, sampled with psutil."""
+
+    def __init__(self, pids: dict[str, int], period: float = 1.0):
+        import psutil
+        self.period = period
+        self.procs = {}
+        for name, pid in pids.items():
+            try:
+                self.procs[name] = psutil.Process(pid)
+            except psutil.Error:
+                pass
+        self.cores: dict[str, list] = {n: [] for n in self.procs}
+        self.rss: dict[str, list] = {n: [] for n in self.procs}
+        self._task = None
+
+    def _times(self):
+        import psutil
+        out = {}
+        for n, p in self.procs.items():
+            try:
+                t = p.cpu_times()
+                out[n] = (t.user + t.system, p.memory_info().rss)
+            except psutil.Error:
+                pass
+        return out
+
+    def _window(self):
+        cur, t1 = self._times(), time.monotonic()
+        for n, (cpu, rss) in cur.items():
+            if n in self._prev:
+                self.cores[n].append((cpu - self._prev[n][0]) / max(1e-6, t1 - self._t0))
+            self.rss[n].append(rss)
+        self._prev, self._t0 = cur, t1
+
+    async def _run(self):
+        while True:
+            await asyncio.sleep(self.period)
+            self._window()
+
+    def start(self):
+        self._prev, self._t0 = self._times(), time.monotonic()
+        self._task = asyncio.create_task(self._run())
+
+    async def stop(self) -> dict:
+        if self._task:
+            self._task.cancel()
+            try:
+                await self._task
+            except asyncio.CancelledError:
+                pass
+        if time.monotonic() - self._t0 >= 0.2 or not any(self.cores.values()):
+            self._window()                      # the last (partial) window
+        out = {}
+        for n in self.procs:
+            cs, rs = self.cores[n], self.rss[n]
+            out[n] = {"cpu_cores_p50": round(pct(cs, 50), 3) if cs else None,
+                      "cpu_cores_p95": round(pct(cs, 95), 3) if cs else None,
+                      "rss_mib_max": round(max(rs) / 2**20, 1) if rs else None,
+                      "rss_mib_last": round(rs[-1] / 2**20, 1) if rs else None, "windows": len(cs)}
+        return out
+
+
 def cpu_pods_for(n_gpus: int) -> int:
     """Density composition: the reference's 30 pods per node (density.go) as 8 GPU pods (one
     per MI355X of a full node) + 22 pause pods, scaled to N allocatable GPUs (weak scaling)."""
@@ -61,6 +140,7 @@ class PodBench:
         self.failed: list[str] = []
         self._watch_task = None
         self.deleting: set = set()
+        self.step_devices: list[list[str]] = []      # per density step: the distinct GPUs its pods ran on
 
     def cpu_pod(self, name):
         return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "default", "labels": {"app": "podbench"}},
@@ -103,6 +183,10 @@ class PodBench:
         if "bound" not in rec and (obj.get("spec") or {}).get("nodeName"):
             rec["bound"] = now
             POD_TRACE(uid, "bench_bound")
+        if "devices" not in rec:
+            ids = [d for er in (obj.get("spec") or {}).get("extendedResources") or [] for d in er.get("assigned") or []]
+            if ids:
+                rec["devices"] = ids
         st = obj.get("status") or {}
         if "started" not in rec:
             for cs in st.get("containerStatuses") or []:
@@ -191,10 +275,12 @@ class PodBench:
                 POD_TRACE(m.uid_of(obj), "bench_create", tw)
         await asyncio.wait_for(asyncio.gather(*(self.done_events[nm].wait() for nm in gpu + cpu)), timeout)
         self.pending_cleanup = cpu
+        self.step_devices.append(sorted({d for nm in gpu for d in self.t[nm].get("devices", [])}))
         return gpu + cpu
 
     async def run(self, steps: int):
         t0 = time.perf_counter()
+        self.step_devices = []
         names = []
         for _ in range(steps):
             names += await (self.density_step() if self.mode == "density" else self.step())
@@ -219,7 +305,116 @@ class PodBench:
                 "p50_startup_ms": ms(pct(first, 50)), "p90_startup_ms": ms(pct(first, 90)), "p99_startup_ms": ms(pct(first, 99)),
                 "p50_startup_all_ms": ms(pct(allstart, 50)), "p50_node_startup_ms": ms(pct(node, 50)),
                 "p99_node_startup_ms": ms(pct(node, 99)), "p50_schedule_ms": ms(pct(sched, 50)),
-                "p50_pod_runtime_ms": ms(pct(life, 50))}
+                "p50_pod_runtime_ms": ms(pct(life, 50)),
+                "gpu_devices_per_step": [len(d) for d in self.step_devices],
+                "gpu_devices_seen": sorted({d for ds in self.step_devices for d in ds})}
+
+    # ------------------------------------------------------------ node density (density_test.go)
+    async def _create_and_wait(self, names: list[str], gpu: set, interval: float = 0.0, timeout: float = 300.0):
+        """Create pods (GPU pods for names in `gpu`, pause pods otherwise) `interval` apart; wait
+        until each is Running (pause) or Succeeded (GPU). Returns (create→started lags, batch s)."""
+        t0 = time.perf_counter()
+        for nm in names:
+            self.t[nm] = {"wave": 0, "cpu": nm not in gpu}
+            self.done_events[nm] = asyncio.Event()
+        creates = []
+        for nm in names:
+            self.t[nm]["create"] = time.perf_counter()
+            creates.append(asyncio.ensure_future(self.lc.client.create(self.pod(nm) if nm in gpu else self.cpu_pod(nm),
+                                                                       "default")))
+            if interval:
+                await asyncio.sleep(interval)
+        await asyncio.gather(*creates)
+        await asyncio.wait_for(asyncio.gather(*(self.done_events[nm].wait() for nm in names)), timeout)
+        lags = [self.t[nm]["started"] - self.t[nm]["create"] for nm in names]
+        return lags, time.perf_counter() - t0
+
+    def _names(self, prefix: str, n: int) -> list[str]:
+        out = []
+        for _ in range(n):
+            self.seq += 1
+            out.append(f"{prefix}-{self.seq:06d}")
+        return out
+
+    async def _cleanup(self, names):
+        for nm in names:
+            if nm not in self.deleting:
+                self.deleting.add(nm)
+                await self._delete(nm)
+        end = time.monotonic() + 60
+        while time.monotonic() < end:
+            left, _ = await self.lc.client.list("pods", "default", label_selector="app=podbench")
+            if not left:
+                return
+            await asyncio.sleep(0.1)
+
+    async def node_density(self, pids: dict[str, int], api=None) -> dict:
+        """density_test.go's limit-checked tests, with pause pods (the reference's) and GPU pods."""
+        api_mark = len(api.lat_samples) if api is not None else 0
+        sampler = ResourceSampler(pids)
+        sampler.start()
+        ms = lambda v: None if v is None else round(v * 1000, 2)  # noqa: E731
+        lat = lambda xs: {"p50": ms(pct(xs, 50)), "p90": ms(pct(xs, 90)), "p99": ms(pct(xs, 99))}  # noqa: E731
+        out = {}
+        old, self.pending_cleanup = self.pending_cleanup, []
+        await self._cleanup(old)
+        # create a batch of 10 pods, 0 interval (density_test.go:72-92)
+        names = self._names("batch", 10)
+        lags, el = await self._create_and_wait(names, set())
+        out["batch10_startup_ms"], out["batch10_batch_ms"] = lat(lags), ms(el)
+        await self._cleanup(names)
+        # the same batch as GPU pods (amd.com/gpu: 1 each; they queue for the node's GPUs)
+        names = self._names("gbatch", 10)
+        lags, el = await self._create_and_wait(names, set(names))
+        out["batch10_gpu_startup_ms"], out["batch10_gpu_batch_ms"] = lat(lags), ms(el)
+        await self._cleanup(names)
+        # 10 pods in sequence beside 50 background pods (density_test.go:213-229), GPU pods
+        bg = self._names("bg", 50)
+        await self._create_and_wait(bg, set())
+        lags = []
+        for nm in self._names("seq", 10):
+            lag, _ = await self._create_and_wait([nm], {nm})
+            lags += lag
+        out["seq10_bg50_startup_ms"] = lat(lags)
+        # and with pause pods, as the reference runs it
+        lags = []
+        seqp = self._names("seqp", 10)
+        for nm in seqp:
+            lag, _ = await self._create_and_wait([nm], set())
+            lags += lag
+        out["seq10_bg50_pause_startup_ms"] = lat(lags)
+        await self._cleanup(bg + seqp)
+        res = await sampler.stop()
+        for role in ("kubelet", "runtime"):
+            r = res.get(role) or {}
+            out[f"{role}_cpu_cores_p50"], out[f"{role}_cpu_cores_p95"] = r.get("cpu_cores_p50"), r.get("cpu_cores_p95")
+            out[f"{role}_rss_mib"] = r.get("rss_mib_max")
+        out["resource_windows"] = min((r.get("windows") or 0 for r in res.values()), default=0)
+        if api is not None:
+            summ = api.latency_summary(api_mark)
+            out["api_p99_ms"], out["api_list_p99_ms"], out["api_worst"] = summ["api_p99_ms"], summ["api_list_p99_ms"], summ["worst"][:3]
+        out["limits"] = DENSITY_LIMITS
+        out["within_limits"] = _within(out)
+        return out
+
+
+def _within(r: dict) -> bool:
+    """Every reported density value at or under its reference limit."""
+    L = DENSITY_LIMITS
+    checks = []
+    for k in ("batch10_startup_ms", "seq10_bg50_startup_ms"):
+        checks += [(r.get(k) or {}).get(q) is not None and r[k][q] <= L[k][q] for q in ("p50", "p90", "p99")]
+    checks.append(r.get("batch10_batch_ms") is not None and r["batch10_batch_ms"] <= L["batch10_batch_ms"])
+    for role in ("kubelet", "runtime"):
+        lim = L[f"{role}_cpu_cores"]
+        for q in ("p50", "p95"):
+            v = r.get(f"{role}_cpu_cores_{q}")
+            checks.append(v is not None and v <= lim[q])
+        v = r.get(f"{role}_rss_mib")
+        checks.append(v is not None and v <= L[f"{role}_rss_mib"])
+    if r.get("api_p99_ms") is not None:
+        checks.append(r["api_p99_ms"] <= L["api_p99_ms"])
+    return all(checks)
 
 
 async def serve(args):
@@ -260,6 +455,13 @@ async def serve(args):
                 if cpu0:   # CPU seconds each node daemon spent on the steps
                     res["node_cpu_s"] = {k: round(v - cpu0.get(k, 0.0), 3) for k, v in lc.cpu_seconds().items()}
                 res["scheduler"] = {"scheduled": lc.scheduler.scheduled, "bind_errors": lc.scheduler.bind_errors}
+                print(json.dumps(res), flush=True)
+            if cmd.get("cmd") == "node_density":
+                pids = lc.daemon_pids() if hasattr(lc, "daemon_pids") else {"kubelet": os.getpid(), "runtime": os.getpid()}
+                try:
+                    res = await pb.node_density(pids, getattr(lc, "api", None))
+                except Exception as e:          # reported, never fatal to the headline bench
+                    res = {"error": repr(e)}
                 print(json.dumps(res), flush=True)
             if cmd.get("cmd") == "schedperf":
                 from amdkube.benchmark.schedperf import run_schedperf

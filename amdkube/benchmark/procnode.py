@@ -112,6 +112,17 @@ class ProcessNode:
             await asyncio.sleep(0.05)
         raise TimeoutError(f"node never advertised {n} GPUs (logs in {self.base})")
 
+    def daemon_pids(self) -> dict[str, int]:
+        """{"kubelet": pid, "runtime": pid (rocshim), "device-plugin": pid, "scheduler": pid}."""
+        role = {"kubelet": "kubelet", "rocshim": "runtime", "amd-device-plugin": "device-plugin", "scheduler": "scheduler"}
+        out = {}
+        for p in self.procs:
+            args = p.args
+            i = args.index("amdkube") + 1 if "amdkube" in args else None
+            if i is not None and i < len(args) and args[i] in role:
+                out[role[args[i]]] = p.pid
+        return out
+
     def cpu_seconds(self) -> dict:
         """user+system CPU seconds of each node daemon so far (per-pod cost accounting)."""
         import psutil

@@ -19,9 +19,12 @@ percentiles are reported beside it. churn — GPU pods only, P per GPU per step 
 process-lifetime bound; docs/PERFORMANCE.md).
 
 Baselines: density saturation ≥ 8 pods/s (vs_baseline = value / 8),
-pod startup p50/p90/p99 ≤ 5 s, scheduler throughput ≥ 30 pods/s (goal 100). Extra fields:
-scheduler_perf (100 nodes / 3000 pods) and the density test on 100 hollow 8×MI355X nodes
-(amdkube/benchmark/density.py), both run after the timed region.
+pod startup p50/p90/p99 ≤ 5 s, scheduler throughput ≥ 30 pods/s (goal 100). Extra fields,
+all measured after the timed region: the node-density tests of test/e2e_node/density_test.go
+(batch of 10, 10 in sequence beside 50 background pods) with the kubelet's and runtime's CPU
+cores p50/p95 and RSS and the API call p99, each beside its reference limit
+(podbench.DENSITY_LIMITS); scheduler_perf (100 nodes / 3000 pods); the density test on 100
+hollow 8×MI355X nodes (amdkube/benchmark/density.py).
 """
 from __future__ import annotations
 
@@ -48,6 +51,8 @@ def main():
                     help="density: the reference density.go mix on the real node (default); churn: GPU pods only")
     ap.add_argument("--backend", default="auto", help="amdsmi|sysfs|fake|auto")
     ap.add_argument("--no-sched-perf", action="store_true")
+    ap.add_argument("--no-node-density", action="store_true",
+                    help="skip the density_test.go batch/sequence tests with resource sampling (after the timed region)")
     ap.add_argument("--density-nodes", type=int, default=100, help="hollow-node density run (0 = skip)")
     ap.add_argument("--image", default="rocm/vector-add", help="GPU pod image (CPU rehearsals: busybox)")
     ap.add_argument("--pod-arg", action="append", default=[], help="GPU pod container argument (repeatable)")
@@ -116,6 +121,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     if rank == 0:
+        node_density = None
+        if not a.no_node_density:
+            worker.stdin.write(json.dumps({"cmd": "node_density"}) + "\n")
+            worker.stdin.flush()
+            node_density = json.loads(worker.stdout.readline())
         sched = None
         if not a.no_sched_perf:
             worker.stdin.write(json.dumps({"cmd": "schedperf", "nodes": 100, "pods": 3000}) + "\n")
@@ -162,7 +172,16 @@ def main():
                "p50_node_startup_ms": res["p50_node_startup_ms"], "p50_schedule_ms": res["p50_schedule_ms"],
                "p50_pod_runtime_ms": res["p50_pod_runtime_ms"], "failed_pods": res["failed"],
                "node_cpu_s": res.get("node_cpu_s"), "isolation": ready.get("isolation"),
+               "gpu_devices_per_step": res.get("gpu_devices_per_step"), "gpu_devices_seen": res.get("gpu_devices_seen"),
                "sched_perf": sched, "density": density}
+        if node_density is not None:
+            # the reference node-density thresholds (test/e2e_node/density_test.go, metrics_util.go),
+            # each value beside its limit in node_density["limits"]
+            for k in ("kubelet_cpu_cores_p50", "kubelet_cpu_cores_p95", "runtime_cpu_cores_p50", "runtime_cpu_cores_p95",
+                      "kubelet_rss_mib", "runtime_rss_mib", "batch10_startup_ms", "batch10_batch_ms",
+                      "seq10_bg50_startup_ms", "api_p99_ms"):
+                out[k] = node_density.get(k)
+            out["node_density"] = node_density
         if res["failed"]:
             out["failures"] = res["failures"]
         print(json.dumps(out), flush=True)
