@@ -808,6 +808,9 @@ def rocshim(argv):
     ap.add_argument("--node-ip", default="127.0.0.1")
     ap.add_argument("--registry-dir", default=None,
                     help="directory standing in for image registries (<host>/<repo>/<tag>/, optional <host>/auth.json)")
+    ap.add_argument("--insecure-registry", action="append", default=[],
+                    help="registry host[:port] pulled over plain http (loopback registries always are), as dockerd's flag")
+    ap.add_argument("--registry-ca", default=None, help="CA bundle for https registries")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     klog.setup(a.v, "rocshim")
@@ -826,7 +829,8 @@ def rocshim(argv):
     async def mk():
         return await RocShim(a.listen, a.state_dir, a.hooks_dir, a.isolation, network=net,
                              pod_namespaces=a.pod_namespaces or a.network_plugin == "kubenet",
-                             registry_dir=a.registry_dir).start()
+                             registry_dir=a.registry_dir, insecure_registries=a.insecure_registry,
+                             registry_ca=a.registry_ca).start()
     _run_forever(mk)
 
 

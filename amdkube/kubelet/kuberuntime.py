@@ -277,8 +277,10 @@ class RuntimeManager:
         if policy == "Never" and present is None:
             raise StartError("ErrImageNeverPull", f'Container image "{image}" is not present with pull policy of Never')
         if present is None or policy == "Always":
+            # image_manager.go:121-141: a pull that fails is ErrImagePull (and backs off) even
+            # when an older copy is present — Always means the registry must agree
             until, _ = self.pull_backoff.get(bkey, (0.0, 0.0))
-            if present is None and time.monotonic() < until:
+            if time.monotonic() < until:
                 raise StartError("ImagePullBackOff", f'Back-off pulling image "{image}"')
             try:
                 if self._pull_limiter is not None:
@@ -290,11 +292,10 @@ class RuntimeManager:
                     await self._pull(image, keyring)
                 self.pull_backoff.pop(bkey, None)
             except grpc.RpcError as e:
-                if present is None:
-                    _, last = self.pull_backoff.get(bkey, (0.0, 0.0))
-                    delay = min(IMAGE_BACKOFF_MAX, last * 2 if last else IMAGE_BACKOFF_BASE)
-                    self.pull_backoff[bkey] = (time.monotonic() + delay, delay)
-                    raise StartError("ErrImagePull", e.details() or str(e.code()))
+                _, last = self.pull_backoff.get(bkey, (0.0, 0.0))
+                delay = min(IMAGE_BACKOFF_MAX, last * 2 if last else IMAGE_BACKOFF_BASE)
+                self.pull_backoff[bkey] = (time.monotonic() + delay, delay)
+                raise StartError("ErrImagePull", e.details() or str(e.code()))
 
     async def start_container(self, pod: dict, c: dict, sid: str, sandbox_cfg, ctx: dict, restart_count: int, init: bool):
         await self.ensure_image(c, ctx.get("keyring"), pod["metadata"]["uid"])

@@ -12,6 +12,11 @@ map the e2e workloads to amdkube's gfx950 binaries (the reference's cuda-vector-
 test/images/cuda-vector-add, becomes `rocm/vector-add`, the HSA build; `rocm/vector-add-hip` is the HIP one). Extra images are registered from
 `images.json` in the runtime's state dir or via PullImage of a local path (`file:///...`).
 
+Registry pulls: a reference naming a registry host (`registry.local:5000/rocm/app:1`,
+`host.domain/repo@sha256:…`) is pulled over the Docker Registry HTTP API v2 (runtime/registry.py:
+token/basic auth with the CRI AuthConfig, manifest lists, digest-verified blobs) and unpacked
+like an archive import.
+
 A registry directory (`rocshim --registry-dir`) stands in for remote registries:
 `<dir>/<host[:port]>/<repository>/<tag>/` holds an image tree (entrypoint `run`), and an
 optional `<dir>/<host[:port]>/auth.json` {"users": {"<name>": "<sha256 hex of password>"}}
@@ -88,8 +93,13 @@ class ImageStore:
     runtime's image filesystem), so they occupy space there, report their size and free it
     when removed (kubelet image GC); built-in images are preloaded and cannot be removed."""
 
-    def __init__(self, state_dir: str, registry_dir: str | None = None):
+    def __init__(self, state_dir: str, registry_dir: str | None = None, registry_client=None):
         self.registry_dir = registry_dir
+        # Docker Registry HTTP API v2 pulls of `host[:port]/repo[:tag|@digest]` (runtime/registry.py)
+        if registry_client is None:
+            from .registry import RegistryClient
+            registry_client = RegistryClient()
+        self.registry = registry_client
         self.path = os.path.join(state_dir, "images.json")
         self.blob_root = os.path.join(state_dir, "images")
         os.makedirs(self.blob_root, exist_ok=True)
@@ -168,6 +178,12 @@ class ImageStore:
 
     def pull(self, ref: str, auth: dict | None = None) -> str:
         reg = self._registry_image(ref)
+        if reg is None and self.registry_dir and not ref.startswith(("file://", "/")):
+            from ..kubelet.credentialprovider import split_image
+            host, port, _ = split_image(ref)
+            if os.path.isdir(os.path.join(self.registry_dir, host + (f":{port}" if port else ""))):
+                # a registry the directory stands in for: what it lacks does not exist
+                raise KeyError(f"image {ref!r} not found in registry {host}")
         if reg is not None:
             tree, root = reg
             if not self._authorized(root, auth):
@@ -175,6 +191,9 @@ class ImageStore:
             if self.resolve(ref) is None:
                 self._store(normalize(ref), tree)
             return self.image_id(normalize(ref))
+        from .registry import is_remote
+        if is_remote(ref) and self.registry is not None:
+            return self._pull_remote(ref, auth)
         if self.resolve(ref):
             return self.image_id(self.resolve(ref)[0])
         path = ref[len("file://"):] if ref.startswith("file://") else ref
@@ -196,6 +215,24 @@ class ImageStore:
             self._save()
             return self.image_id(normalize(ref))
         raise KeyError(f"image {ref!r} not found (no registry access; register it in images.json or pull a local path)")
+
+    def _pull_remote(self, ref: str, auth: dict | None) -> str:
+        """A registry pull. A tag already held is re-checked against the registry's manifest
+        digest (dockerd's pull of an existing tag): unchanged, nothing is downloaded."""
+        from .registry import parse_reference, pull_image
+        name = normalize(ref)
+        have = self.images.get(name)
+        if have is not None and have.get("repo_digests"):
+            host, repo, tag = parse_reference(ref)
+            _, digest = self.registry.manifest(host, repo, tag, auth)
+            if f"{host}/{repo}@{digest}" in have["repo_digests"]:
+                return have["id"]
+        rec = pull_image(ref, self.blob_root, auth, self.registry)
+        rec["size"] = _tree_size(rec["blob"])
+        for n in {name, normalize(rec["repo_digests"][0])}:
+            self.images[n] = rec
+        self._save()
+        return rec["id"]
 
     def _store(self, name: str, tree: str):
         digest = hashlib.sha256(name.encode()).hexdigest()[:32]

@@ -238,31 +238,41 @@ def image_spec(cfg: dict) -> dict:
 def import_image(path: str, store_root: str) -> dict:
     """Unpack an archive into `<store_root>/<id>/rootfs`; returns the image record."""
     os.makedirs(store_root, exist_ok=True)
-    layers_root = os.path.join(store_root, "layers")
-    os.makedirs(layers_root, exist_ok=True)
     with tempfile.TemporaryDirectory(dir=store_root, prefix=".import-") as work:
         cfg, layers, tags = read_archive(path, work)
-        spec = image_spec(cfg)
-        cfg_bytes = json.dumps(cfg, sort_keys=True).encode()
-        iid = hashlib.sha256(cfg_bytes).hexdigest()
-        dest = os.path.join(store_root, iid)
-        shutil.rmtree(dest, ignore_errors=True)
-        rootfs = os.path.join(dest, "rootfs")
-        os.makedirs(rootfs)
-        diff_ids, sizes = [], []
-        for i, lp in enumerate(layers):
-            did = "sha256:" + _diff_id(lp)    # digest of the uncompressed layer
-            if spec["diff_ids"] and i < len(spec["diff_ids"]) and spec["diff_ids"][i] != did:
-                raise ImageFormatError(f"layer {i}: diff id {did} does not match the config's {spec['diff_ids'][i]}")
-            apply_layer(lp, rootfs)
-            diff_ids.append(did)
-            sizes.append(os.path.getsize(lp))
-            # keep the layer blob by diff id (shared by images built on it)
-            keep = os.path.join(layers_root, did.split(":", 1)[1] + ".tar")
-            if not os.path.exists(keep):
-                shutil.copyfile(lp, keep)
-        with open(os.path.join(dest, "config.json"), "wb") as f:
-            f.write(cfg_bytes)
+        return import_layers(cfg, layers, tags, store_root)
+
+
+def import_layers(cfg: dict, layers: list[str], tags: list[str], store_root: str) -> dict:
+    """Apply layer files (plain or gzip tars, in order) into `<store_root>/<id>/rootfs`, checking
+    each against the config's rootfs.diff_ids; returns the image record. Shared by archive
+    imports and registry pulls (runtime/registry.py)."""
+    os.makedirs(store_root, exist_ok=True)
+    layers_root = os.path.join(store_root, "layers")
+    os.makedirs(layers_root, exist_ok=True)
+    spec = image_spec(cfg)
+    cfg_bytes = json.dumps(cfg, sort_keys=True).encode()
+    iid = hashlib.sha256(cfg_bytes).hexdigest()
+    dest = os.path.join(store_root, iid)
+    shutil.rmtree(dest, ignore_errors=True)
+    rootfs = os.path.join(dest, "rootfs")
+    os.makedirs(rootfs)
+    diff_ids, sizes = [], []
+    for i, lp in enumerate(layers):
+        did = "sha256:" + _diff_id(lp)    # digest of the uncompressed layer
+        if spec["diff_ids"] and i < len(spec["diff_ids"]) and spec["diff_ids"][i] != did:
+            raise ImageFormatError(f"layer {i}: diff id {did} does not match the config's {spec['diff_ids'][i]}")
+        apply_layer(lp, rootfs)
+        diff_ids.append(did)
+        sizes.append(os.path.getsize(lp))
+        # keep the layer blob by diff id (shared by images built on it)
+        keep = os.path.join(layers_root, did.split(":", 1)[1] + ".tar")
+        if not os.path.exists(keep):
+            shutil.copyfile(lp, keep)
+    if spec["diff_ids"] and len(spec["diff_ids"]) != len(layers):
+        raise ImageFormatError(f"the config lists {len(spec['diff_ids'])} layers, the manifest {len(layers)}")
+    with open(os.path.join(dest, "config.json"), "wb") as f:
+        f.write(cfg_bytes)
     return {"kind": "rootfs", "id": "sha256:" + iid, "rootfs": rootfs, "blob": dest, "layers": diff_ids,
             "layer_sizes": sizes, "repo_tags": tags, "entrypoint": spec["entrypoint"], "cmd": spec["cmd"],
             "env": spec["env"], "workdir": spec["workdir"], "user": spec["user"]}

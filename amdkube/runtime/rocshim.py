@@ -282,7 +282,8 @@ class CheckpointWriter:
 class RocShim:
     def __init__(self, socket_path: str, state_dir: str, hooks_dir: str = DEFAULT_HOOKS_DIR, isolation: str = "env",
                  cgroup_root: str = "/sys/fs/cgroup/amdkube", dev_root: str = "/dev", network=None,
-                 pod_namespaces: bool = False, registry_dir: str | None = None):
+                 pod_namespaces: bool = False, registry_dir: str | None = None, insecure_registries=(),
+                 registry_ca: str | None = None):
         self.socket = socket_path
         self.state_dir = state_dir
         # the node's environment minus GPU visibility, read once (iterating os.environ per
@@ -291,7 +292,8 @@ class RocShim:
         os.makedirs(os.path.join(state_dir, "sandboxes"), exist_ok=True)
         os.makedirs(os.path.join(state_dir, "containers"), exist_ok=True)
         os.makedirs(os.path.join(state_dir, "rootfs"), exist_ok=True)
-        self.images = ImageStore(state_dir, registry_dir)
+        from .registry import RegistryClient
+        self.images = ImageStore(state_dir, registry_dir, RegistryClient(insecure_registries, registry_ca))
         self.ckpt = CheckpointWriter()
         self.hooks = HookService(hooks_dir, HANDLERS)
         self.isolation_probe = probe_isolation() if isolation in ("auto", "landlock", "namespaces", "userns") else {}
@@ -1375,6 +1377,10 @@ class _Images:
             await ctx.abort(grpc.StatusCode.UNAUTHENTICATED, str(e))
         except KeyError as e:
             await ctx.abort(grpc.StatusCode.NOT_FOUND, str(e))
+        except ValueError as e:            # oci.ImageFormatError: a bad manifest, a blob failing its digest
+            await ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, f"pulling {req.image.image}: {e}")
+        except Exception as e:             # registry.RegistryError: transport / protocol
+            await ctx.abort(grpc.StatusCode.UNAVAILABLE, f"pulling {req.image.image}: {e}")
 
     async def RemoveImage(self, req, ctx):
         ref = req.image.image

@@ -8,6 +8,9 @@
 // after a sum all-reduce every rank must hold n(n+1)/2 + 0.5*n*(e%7) in every element. On an 8x MI355X node every GPU
 // pair has one direct xGMI link (7 links x ~153 GB/s per GPU), so a ring all-reduce over k
 // GPUs is per-link bound; the probe reports algbw and busbw = algbw * 2(k-1)/k.
+// It also prints, per rank, the PCI bus id and UUID of the GPU the communicator opened, so the
+// placement the scheduler bound (spec.extendedResources[].assigned → amd.com/pci-bus) can be
+// checked against what RCCL actually ran on inside the pod.
 //   xgmi-probe [--max-mib M] [--iters K] [--no-p2p]
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -63,8 +66,19 @@ int main(int argc, char** argv) {
     if (n < 1) throw std::runtime_error("no GPUs visible");
     std::ostringstream js;   // printed once at the end: RCCL writes its banner to stdout at init
     char tmp[256];
-    std::snprintf(tmp, sizeof tmp, "{\"gpus\":%d,", n);
+    std::snprintf(tmp, sizeof tmp, "{\"gpus\":%d,\"devices\":[", n);
     js << tmp;
+    for (int i = 0; i < n; ++i) {
+      char bus[64] = {0};
+      CHECK_HIP(hipDeviceGetPCIBusId(bus, sizeof bus, i));
+      hipUUID u;
+      CHECK_HIP(hipDeviceGetUuid(&u, i));
+      char hex[33];
+      for (int b = 0; b < 16; ++b) std::snprintf(hex + 2 * b, 3, "%02x", static_cast<unsigned char>(u.bytes[b]));
+      std::snprintf(tmp, sizeof tmp, "%s{\"rank\":%d,\"bus\":\"%s\",\"uuid\":\"%s\"}", i ? "," : "", i, bus, hex);
+      js << tmp;
+    }
+    js << "],";
     std::vector<ncclComm_t> comms(n);
     std::vector<int> devs(n);
     for (int i = 0; i < n; ++i) devs[i] = i;

@@ -162,6 +162,8 @@ def test_02d_rootfs_image_pod_on_mi355x(tmp_path):
         with open(os.path.realpath(src), "rb") as f:
             entries.append((rel, f.read(), 0o755, None))
     layer = [(d, None, 0o755, None) for d in sorted(dirs)] + entries
+    if os.environ.get("_AMDKUBE_RETURN_LAYER"):
+        return layer
     arch = str(tmp_path / "vadd-image.tar")
     write_docker_archive(arch, [layer], {"Entrypoint": ["/usr/local/bin/rocm-vector-add"], "Cmd": ["--print-uuid"],
                                          "Env": ["PATH=/usr/local/bin:/usr/bin:/bin"], "WorkingDir": "/"},
@@ -184,6 +186,42 @@ def test_02d_rootfs_image_pod_on_mi355x(tmp_path):
             [(name, spec)] = [(n, s) for n, s in lc.shim.images.images.items() if n.startswith("amdkube/vadd-rootfs")]
             assert len(spec["layers"]) == 1 and spec["size"] > 0
             print("rootfs image pod:", lc.shim.isolation, logs.strip().splitlines()[0])
+    run(go(), 300)
+
+
+def test_02e_registry_pulled_image_pod_on_mi355x(tmp_path, monkeypatch):
+    """The same vector-add image served by an in-test Docker Registry v2 on localhost behind
+    token auth: the pod's imagePullSecrets authenticate the pull, the layers are digest-checked
+    and unpacked, and the image runs as a GPU pod on MI355X (round-3 review, registry pull)."""
+    import base64
+    from tests.fake_registry import FakeRegistry
+    monkeypatch.setenv("_AMDKUBE_RETURN_LAYER", "1")
+    layer = test_02d_rootfs_image_pod_on_mi355x(tmp_path)
+    monkeypatch.delenv("_AMDKUBE_RETURN_LAYER")
+
+    async def go():
+        with FakeRegistry(users={"ci": "s3cret"}) as reg:
+            reg.push("rocm/vadd", "r4", [layer], {"Entrypoint": ["/usr/local/bin/rocm-vector-add"], "Cmd": ["--print-uuid"],
+                                                  "Env": ["PATH=/usr/local/bin:/usr/bin:/bin"], "WorkingDir": "/"})
+            async with LocalCluster(gpus="amdsmi", n_gpus=1, relist_period=0.5, with_controllers=False) as lc:
+                await lc.wait_gpus(1, 60)
+                cfg = {"auths": {reg.host: {"auth": base64.b64encode(b"ci:s3cret").decode()}}}
+                await lc.client.create({"apiVersion": "v1", "kind": "Secret", "metadata": {"name": "regcred"},
+                                        "type": "kubernetes.io/dockerconfigjson",
+                                        "data": {".dockerconfigjson": base64.b64encode(json.dumps(cfg).encode()).decode()}},
+                                       "default")
+                pod = vadd_pod("registry-pod")
+                c = pod["spec"]["containers"][0]
+                c["image"], c["args"] = f"{reg.host}/rocm/vadd:r4", []
+                c["volumeMounts"] = [{"name": "rocm", "mountPath": "/opt/rocm", "readOnly": True}]
+                pod["spec"]["volumes"] = [{"name": "rocm", "hostPath": {"path": "/opt/rocm"}}]
+                pod["spec"]["imagePullSecrets"] = [{"name": "regcred"}]
+                await lc.client.create(pod)
+                p = await wait_pod(lc.client, "default", "registry-pod", ("Succeeded", "Failed"), 180)
+                logs = await lc.client.logs("default", "registry-pod")
+                assert p["status"]["phase"] == "Succeeded" and "Test PASSED" in logs, (p["status"], logs)
+                assert any(path.startswith("/token?") for _, path, _ in reg.log)
+                print("registry image pod:", logs.strip().splitlines()[0])
     run(go(), 300)
 
 
@@ -532,6 +570,40 @@ def test_09_gpu_pods_over_a_raft_store_with_protobuf_and_spdy_exec(tmp_path):
             if store is not None:
                 store.close()
             cl.stop()
+    run(go(), 400)
+
+
+def test_04a_xgmi_probe_gang_pod_runs_rccl_on_exactly_its_gpus():
+    """BASELINE config 4 / SURVEY §7.7: the RCCL probe runs as a pod on the GPUs the scheduler
+    bound. A gang of min(4, node GPUs) is requested; inside the pod RCCL opens exactly that many
+    ranks, its all-reduce sums are right, and the PCI buses of the GPUs the communicator opened
+    are exactly the amd.com/pci-bus attributes of spec.extendedResources[].assigned (the device
+    list the container was given, docker_container.go:155-172)."""
+    from amdkube.smi import AmdSmiBackend
+    b = AmdSmiBackend()
+    n_node = len(b.gpus())
+    b.close()
+    k = min(4, n_node)
+
+    async def go():
+        async with LocalCluster(gpus="amdsmi", relist_period=0.5, with_controllers=False) as lc:
+            node = await lc.wait_gpus(k, 60)
+            await lc.client.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "xgmi", "namespace": "default"},
+                                    "spec": {"restartPolicy": "Never", "containers": [{
+                                        "name": "probe", "image": "amdkube/xgmi-probe:latest",
+                                        "args": ["--max-mib", "16", "--iters", "2"],
+                                        "resources": {"limits": {"amd.com/gpu": str(k)}}}]}})
+            pod = await wait_pod(lc.client, "default", "xgmi", ("Succeeded", "Failed"), 180)
+            logs = await lc.client.logs("default", "xgmi")
+            assert pod["status"]["phase"] == "Succeeded", (pod["status"], logs[-2000:])
+            x = json.loads(logs[logs.index("{\"gpus\""):logs.rindex("}") + 1])
+            assigned = [d for er in pod["spec"]["extendedResources"] for d in er["assigned"]]
+            assert len(assigned) == k and x["gpus"] == k and x["verify"]["ranks"] == k and x["verify"]["wrong"] == 0, x
+            attrs = node["status"]["extendedResources"]["amd.com/gpu"]["resources"]
+            want = sorted(attrs[d]["attributes"]["amd.com/pci-bus"].replace("-", ":").lower() for d in assigned)
+            got = sorted(d["bus"].lower() for d in x["devices"])
+            assert got == want, (got, want, assigned)
+            print("xgmi-probe pod:", k, "rank(s) on", got, "busbw", [r["busbw_gbps"] for r in x["allreduce"]])
     run(go(), 400)
 
 
