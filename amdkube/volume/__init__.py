@@ -270,6 +270,6 @@ def sha256_name(*parts: str) -> str:
 
 def default_plugins() -> list[VolumePlugin]:
     """ProbeVolumePlugins of the reference kubelet (cmd/kubelet/app/plugins.go), MI355X build."""
-    from . import csi, local, network, unsupported
+    from . import csi, local, network
     from . import cinder, vendor
-    return [*local.plugins(), *network.plugins(), csi.CSIPlugin(), *cinder.plugins(), *vendor.plugins(), *unsupported.plugins()]
+    return [*local.plugins(), *network.plugins(), csi.CSIPlugin(), *cinder.plugins(), *vendor.plugins()]
