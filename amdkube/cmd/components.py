@@ -847,9 +847,14 @@ def device_plugin(argv):
                     help="partitioned GPUs: single=amd.com/gpu for all, mixed=amd.com/<cpx>_<nps> per partition type")
     ap.add_argument("--partition", default=None, help="fake backend only: compute/memory mode, e.g. CPX/NPS2")
     ap.add_argument("--register-v1beta1", default=None, help="kubelet.sock of an upstream v1beta1 kubelet")
+    ap.add_argument("--health-state-file", default=None,
+                    help="checkpoint of RAS baselines and GPU faults (default: <plugins-dir>/../amdkube-gpu-health.json; "
+                         "'' keeps health state in memory only)")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     klog.setup(a.v, "amd-device-plugin")
+    state = a.health_state_file if a.health_state_file is not None else \
+        os.path.join(os.path.dirname(os.path.abspath(a.plugins_dir)), "amdkube-gpu-health.json")
     from ..deviceplugin.amd import make_plugins
     from ..smi import open_backend
 
@@ -864,13 +869,39 @@ def device_plugin(argv):
     async def mk():
         backend = open_backend(a.backend, a.fixture, a.max_gpus, a.partition)
         plugins = make_plugins(backend, a.resource_naming, a.resource_name, plugins_dir=a.plugins_dir,
-                               health_interval=a.health_interval, health_probe=a.health_probe)
+                               health_interval=a.health_interval, health_probe=a.health_probe,
+                               health_state=state or None)
         for p in plugins:
             await p.start()
             if a.register_v1beta1:
                 await p.register_v1beta1(a.register_v1beta1)
         return _Group(plugins)
     _run_forever(mk)
+
+
+def gpu_health(argv):
+    """`amdkube gpu-health show|reset [DEVICE_ID…|all]`: the device plugin's GPU fault
+    checkpoint, and the operator's way to put a repaired GPU back into service."""
+    ap = argparse.ArgumentParser("amdkube gpu-health")
+    ap.add_argument("action", choices=("show", "reset"))
+    ap.add_argument("devices", nargs="*", default=[])
+    ap.add_argument("--state-file", default="/var/lib/kubelet/device-plugin/amdkube-gpu-health.json")
+    a = ap.parse_args(argv)
+    if a.action == "show":
+        try:
+            with open(a.state_file) as f:
+                gpus = (json.load(f) or {}).get("gpus") or {}
+        except FileNotFoundError:
+            gpus = {}
+        for did, ent in sorted(gpus.items()):
+            print(f"{did}\t{'Unhealthy: ' + ent['sticky'] if ent.get('sticky') else 'Healthy'}")
+        return 0
+    if not a.devices:
+        ap.error("reset needs device IDs or 'all'")
+    from ..smi.health import request_reset
+    request_reset(a.state_file, a.devices)
+    print(f"reset requested for {', '.join(a.devices)} (applied on the plugin's next health check)")
+    return 0
 
 
 def exporter(argv):
@@ -1147,6 +1178,7 @@ def kubeadm(argv):
 COMPONENTS = {"etcd": etcd, "dns": dns, "kube-dns": dns, "kubeadm": kubeadm, "proxy": proxy, "kube-proxy": proxy, "apiserver": apiserver, "kube-apiserver": apiserver, "scheduler": scheduler, "kube-scheduler": scheduler,
               "controller-manager": controller_manager, "kube-controller-manager": controller_manager, "kubelet": kubelet,
               "rocshim": rocshim, "amd-device-plugin": device_plugin, "device-plugin": device_plugin,
+              "gpu-health": gpu_health,
               "amdgpu-exporter": exporter, "exporter": exporter, "hollow-node": hollow_node, "local-up": local_up,
               "metrics-server": metrics_server, "cloud-controller-manager": cloud_controller_manager,
               "gke-certificates-controller": gke_certificates_controller, "rktshim": rktshim}

@@ -127,7 +127,7 @@ class AMDGPUPlugin(DevicePluginServer):
     def __init__(self, backend: Backend, resource_name: str = RESOURCE, plugins_dir: str = DEVICE_PLUGINS_PATH,
                  health_interval: float = 10.0, health_probe: str = "none", dev_root: str = "/dev",
                  ecc_threshold: int = 0, expose_card: bool = True, init_timeout: int = 10,
-                 devices: list[dict] | None = None):
+                 devices: list[dict] | None = None, health_state: str | None = None):
         super().__init__(resource_name, plugins_dir, init_timeout)
         self.backend = backend
         self.health_interval = health_interval
@@ -143,7 +143,10 @@ class AMDGPUPlugin(DevicePluginServer):
             raise ValueError("device IDs are not unique on this node (partitions without distinct ids?)")
         self.reasons: dict[str, str] = {}
         from ..smi.health import HealthMonitor
-        self.monitor = HealthMonitor(backend, ecc_threshold)
+        # health_state: checkpoint of RAS baselines + sticky faults, so a restart does not
+        # re-advertise a faulted GPU Healthy (smi/health.py)
+        by_index = {g["index"]: device_id(g) for g in node_gpus}
+        self.monitor = HealthMonitor(backend, ecc_threshold, health_state, key_of=lambda i: by_index.get(i, str(i)))
         self._task: asyncio.Task | None = None
         try:
             self.labels[TOPOLOGY_LABEL] = topology_label(node_gpus, backend.topology())
@@ -193,10 +196,23 @@ class AMDGPUPlugin(DevicePluginServer):
             else:
                 self.devices = devs
 
+    def _apply_resets(self):
+        """`amdkube gpu-health reset`: clear the named devices' faults (fresh RAS baseline)."""
+        ids = self.monitor.pending_resets()
+        if not ids:
+            return
+        for did, g in self.by_id.items():
+            if "all" in ids or did in ids:
+                log.warning("gpu %s: health reset by the operator", did)
+                self.monitor.reset(g["index"])
+                if self.reasons.get(did, "").startswith("probe:"):
+                    self.reasons[did] = ""
+
     async def _health_loop(self):
         while True:
             await asyncio.sleep(self.health_interval)
             try:
+                self._apply_resets()
                 self._check_health()
             except Exception as e:  # keep serving; the next tick retries
                 log.error("health check failed: %s", e)

@@ -70,7 +70,8 @@ class LocalCluster:
         if self.gpus != "none":
             self.backend = open_backend(self.gpus, n=self.n_gpus, partition=self.partition)
             self.plugins = make_plugins(self.backend, self.resource_naming, plugins_dir=os.path.join(b, "plugins"),
-                                        health_interval=5.0, health_probe=self.health_probe)
+                                        health_interval=5.0, health_probe=self.health_probe,
+                                        health_state=os.path.join(b, "amdkube-gpu-health.json"))
             self.plugin = self.plugins[0]
         kw = dict(self.kubelet_kw)
         # the in-process harness mounts nothing unless a test asks for real mounts (and then

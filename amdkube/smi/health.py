@@ -17,21 +17,82 @@ state when it starts and flags:
     the part needs service);
   * any RAS/SMI query that fails outright.
 
-A flagged device stays Unhealthy until the plugin restarts (a fresh snapshot), the same
-lifetime the reference gives a ListAndWatch health flip. The reason is kept per device and
-published as the `amd.com/health-reason` attribute.
+A flagged device stays Unhealthy until an operator resets it. With a `state_file` the
+baselines and the sticky reasons are checkpointed (keyed by device ID, like the kubelet's
+device checkpoint, pkg/kubelet/cm/devicemanager/manager_store.go), so a plugin restart keeps
+judging against the ORIGINAL baseline and a faulted GPU is re-advertised Unhealthy with its
+reason instead of being re-baselined into service. `amdkube gpu-health reset <id|all>` drops a
+`<state_file>.reset` request that the running plugin applies on its next health tick (fresh
+baseline, fault cleared). Without a state file the state lives as long as the process. The
+reason is published as the `amd.com/health-reason` attribute.
 """
 from __future__ import annotations
 
+import json
+import logging
+import os
+import time
+
 HEALTH_REASON_ATTR = "amd.com/health-reason"
+log = logging.getLogger("amdkube.health")
+
+
+def request_reset(state_file: str, device_ids: list[str]):
+    """Ask the plugin that owns `state_file` to clear these devices' faults ("all": every one)."""
+    with open(state_file + ".reset", "a") as f:
+        for d in device_ids:
+            f.write(d + "\n")
 
 
 class HealthMonitor:
-    def __init__(self, backend, ecc_threshold: int = 0):
+    def __init__(self, backend, ecc_threshold: int = 0, state_file: str | None = None, key_of=None):
         self.backend = backend
         self.ecc_threshold = ecc_threshold
         self.baseline: dict[int, dict] = {}
         self.sticky: dict[int, str] = {}
+        self.state_file = state_file
+        self.key_of = key_of or str
+        self._saved: dict[str, dict] = self._load()
+
+    # ------------------------------------------------------------------ checkpoint
+    def _load(self) -> dict:
+        if not self.state_file or not os.path.exists(self.state_file):
+            return {}
+        try:
+            with open(self.state_file) as f:
+                return dict((json.load(f) or {}).get("gpus") or {})
+        except (OSError, ValueError) as e:
+            log.error("health state %s unreadable (%s); starting from fresh baselines", self.state_file, e)
+            return {}
+
+    def _save(self):
+        if not self.state_file:
+            return
+        os.makedirs(os.path.dirname(os.path.abspath(self.state_file)), exist_ok=True)
+        tmp = self.state_file + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump({"gpus": self._saved}, f, sort_keys=True, default=str)
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, self.state_file)
+
+    def pending_resets(self) -> set[str]:
+        """Device IDs (or "all") an operator asked to reset since the last call."""
+        if not self.state_file:
+            return set()
+        req = self.state_file + ".reset"
+        try:
+            with open(req) as f:
+                ids = {line.strip() for line in f if line.strip()}
+            os.unlink(req)
+            return ids
+        except FileNotFoundError:
+            return set()
+
+    def reset(self, index: int):
+        """Clear a device's fault and judge it from a fresh baseline from now on."""
+        self.sticky.pop(index, None)
+        self.snapshot(index, fresh=True)
 
     def _state(self, index: int) -> dict:
         st = dict(self.backend.sample(index))
@@ -42,11 +103,22 @@ class HealthMonitor:
             st["ras_error"] = str(e)
         return st
 
-    def snapshot(self, index: int) -> dict:
+    def snapshot(self, index: int, fresh: bool = False) -> dict:
+        """The baseline new faults are judged against: the checkpointed one when there is one
+        (a restart keeps it and any sticky fault), else the device's state now."""
+        key = self.key_of(index)
+        ent = self._saved.get(key)
+        if ent is not None and not fresh:
+            self.baseline[index] = ent.get("baseline") or {}
+            if ent.get("sticky"):
+                self.sticky[index] = ent["sticky"]
+            return self.baseline[index]
         try:
             self.baseline[index] = self._state(index)
         except Exception as e:   # noqa: BLE001
             self.baseline[index] = {"snapshot_error": str(e)}
+        self._saved[key] = {"baseline": self.baseline[index], "sticky": "", "since": time.time()}
+        self._save()
         return self.baseline[index]
 
     def check(self, index: int) -> tuple[bool, str]:
@@ -62,6 +134,9 @@ class HealthMonitor:
         why = self._judge(base, cur)
         if why:
             self.sticky[index] = why
+            ent = self._saved.setdefault(self.key_of(index), {"baseline": base})
+            ent["sticky"], ent["faulted_at"] = why, time.time()
+            self._save()
             return False, why
         return True, ""
 

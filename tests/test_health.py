@@ -94,3 +94,54 @@ def test_fault_flips_device_publishes_reason_and_spares_the_running_pod():
             p2 = await wait_pod(lc.client, "default", "next", ("Running",), 30)
             assert p2["spec"]["extendedResources"][0]["assigned"] != [did]
     run(go(), 90)
+
+
+def test_fault_survives_a_plugin_restart_until_an_operator_reset(tmp_path):
+    """Round-3 review: the baseline and sticky faults lived only in memory, so a restarted plugin
+    re-baselined and re-advertised a faulted GPU Healthy. With the checkpoint the restarted
+    plugin keeps the GPU Unhealthy with its reason, and judges against the ORIGINAL baseline
+    (errors that happened while it was down still count) until `amdkube gpu-health reset`."""
+    import subprocess
+    import sys
+    from amdkube.deviceplugin.amd import AMDGPUPlugin
+    from amdkube.smi import device_id
+    state = str(tmp_path / "health.json")
+    fb = FakeBackend(n=2)
+
+    async def plugin():
+        p = AMDGPUPlugin(fb, plugins_dir=str(tmp_path / "plugins"), health_interval=0.05, health_state=state)
+        await p.start()
+        return p
+
+    async def go():
+        p = await plugin()
+        ids = [device_id(g) for g in fb.gpus()]
+        fb.inject_xgmi_error(0)
+        for _ in range(100):
+            if p.devices[0]["health"] == "Unhealthy":
+                break
+            await asyncio.sleep(0.02)
+        assert p.devices[0]["health"] == "Unhealthy" and p.devices[1]["health"] == "Healthy"
+        await p.stop()
+        # the fault clears at the source (driver reload), and GPU 1 takes ECC errors while the
+        # plugin is down: the restart must not re-baseline either
+        fb.ras_state[0]["xgmi_error"] = 0
+        fb.inject_ecc(1, uncorrectable=3)
+        p = await plugin()
+        h = {d["ID"]: (d["health"], d["Attributes"].get(HEALTH_REASON_ATTR)) for d in p.devices}
+        assert h[ids[0]] == ("Unhealthy", "xGMI_link_error"), h
+        assert h[ids[1]][0] == "Unhealthy" and "ECC" in h[ids[1]][1], h
+        # the operator puts GPU 0 back; GPU 1 stays out
+        r = subprocess.run([sys.executable, "-m", "amdkube", "gpu-health", "reset", ids[0], "--state-file", state],
+                           capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, r.stderr
+        for _ in range(100):
+            if p.devices[0]["health"] == "Healthy":
+                break
+            await asyncio.sleep(0.02)
+        assert p.devices[0]["health"] == "Healthy" and p.devices[1]["health"] == "Unhealthy"
+        show = subprocess.run([sys.executable, "-m", "amdkube", "gpu-health", "show", "--state-file", state],
+                              capture_output=True, text=True, timeout=60).stdout
+        assert f"{ids[0]}\tHealthy" in show and f"{ids[1]}\tUnhealthy" in show
+        await p.stop()
+    run(go())
