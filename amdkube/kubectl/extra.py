@@ -480,9 +480,59 @@ def cmd_config_sync(a):
     return 0
 
 
+async def auth_reconcile(c, a):
+    """`kubectl auth reconcile -f FILE` (pkg/kubectl/cmd/auth/reconcile.go:153 RunReconcile):
+    Roles / ClusterRoles gain missing rules (coverage-checked, api/rbac.py), bindings gain
+    missing subjects and are re-created when their roleRef changed; objects annotated
+    rbac.authorization.kubernetes.io/autoupdate=false are left alone. Nothing is removed."""
+    from ..api import rbac
+    from .main import _read_files
+    if not a.filename:
+        raise SystemExit('error: required flag(s) "filename" not set')
+    kinds = {"Role": ("roles", rbac.reconcile_role), "ClusterRole": ("clusterroles", rbac.reconcile_role),
+             "RoleBinding": ("rolebindings", rbac.reconcile_binding),
+             "ClusterRoleBinding": ("clusterrolebindings", rbac.reconcile_binding)}
+    for doc in _read_files(a.filename):
+        kind = doc.get("kind")
+        if kind not in kinds or not str(doc.get("apiVersion", "")).startswith("rbac.authorization.k8s.io/"):
+            continue                                         # reconcile visits RBAC objects only
+        res, fn = kinds[kind]
+        res = res + ".rbac.authorization.k8s.io"
+        name = m.name_of(doc)
+        ns = (m.namespace_of(doc) or a.namespace or "default") if kind in ("Role", "RoleBinding") else ""
+        if ns:
+            doc.setdefault("metadata", {})["namespace"] = ns
+            if await c.get_or_none("namespaces", ns) is None:   # RoleModifier creates the namespace
+                await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+        for attempt in range(4):
+            cur = await c.get_or_none(res, name, ns)
+            r = fn(cur, doc)
+            if r["protected"]:
+                break
+            try:
+                if r["operation"] == rbac.RECREATE:
+                    await c.delete(res, name, ns, uid=m.uid_of(cur))
+                if r["operation"] in (rbac.CREATE, rbac.RECREATE):
+                    obj = dict(r["object"])
+                    obj.setdefault("metadata", {}).pop("resourceVersion", None)
+                    obj["metadata"].pop("uid", None)
+                    await c.create(obj, ns)
+                elif r["operation"] == rbac.UPDATE:
+                    await c.update(r["object"])
+                break
+            except m.StatusError as e:
+                if e.code in (404, 409) and attempt < 3:        # changed under us: re-run
+                    continue
+                raise
+        print(f"{kind.lower()}.rbac.authorization.k8s.io/{name} reconciled")
+    return 0
+
+
 async def cmd_auth(c, a):
+    if a.args and a.args[0] == "reconcile":
+        return await auth_reconcile(c, a)
     if len(a.args) < 3 or a.args[0] != "can-i":
-        raise SystemExit("error: auth can-i VERB RESOURCE[/NAME]")
+        raise SystemExit("error: auth can-i VERB RESOURCE[/NAME] | auth reconcile -f FILE")
     verb, target = a.args[1], a.args[2]
     r, _, name = target.partition("/")
     ri = SCHEME.resolve(r)

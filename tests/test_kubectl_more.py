@@ -178,3 +178,79 @@ def test_apply_two_port_service_and_strategic_patch_of_ports(tmp_path, capsys):
             live = await c.get("services", "web", "default")
             assert [p["port"] for p in live["spec"]["ports"]] == [80]
     run(go())
+
+
+def test_auth_reconcile_rbac(tmp_path, capsys):
+    """kubectl auth reconcile (pkg/kubectl/cmd/auth/reconcile.go, pkg/registry/rbac/reconciliation):
+    idempotent on the bootstrap roles, missing rules/subjects are added (never removed), a
+    changed roleRef re-creates the binding, autoupdate=false protects an object."""
+    from amdkube.api import rbac
+
+    async def go():
+        async with LocalCluster(gpus="none", with_kubelet=False, with_controllers=False,
+                                api_kw={"authorization_mode": "RBAC"}) as lc:
+            c = lc.client
+            boot = [r for r in (await c.list("clusterroles.rbac.authorization.k8s.io"))[0]
+                    if m.name_of(r).startswith("system:")][:10]
+            assert boot, "no bootstrap cluster roles"
+            rvs = {m.name_of(r): r["metadata"]["resourceVersion"] for r in boot}
+            docs = [{"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
+                     "metadata": {"name": m.name_of(r), "labels": r["metadata"].get("labels") or {},
+                                  "annotations": r["metadata"].get("annotations") or {}},
+                     "rules": r.get("rules") or []} for r in boot]
+            f = _write(tmp_path, "boot.yaml", docs)
+            await kubectl(c, "auth", "reconcile", "-f", f)
+            await kubectl(c, "auth", "reconcile", "-f", f)
+            for r in (await c.list("clusterroles.rbac.authorization.k8s.io"))[0]:
+                if m.name_of(r) in rvs:
+                    assert r["metadata"]["resourceVersion"] == rvs[m.name_of(r)], m.name_of(r)   # untouched
+            # a role missing a rule gains it; an extra live rule stays (union)
+            role = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role",
+                    "metadata": {"name": "gpu-reader", "namespace": "team", "labels": {"tier": "gpu"}},
+                    "rules": [{"apiGroups": [""], "resources": ["pods", "pods/log"], "verbs": ["get", "list"]}]}
+            rb = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "RoleBinding",
+                  "metadata": {"name": "readers", "namespace": "team"},
+                  "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "Role", "name": "gpu-reader"},
+                  "subjects": [{"kind": "User", "name": "alice", "apiGroup": "rbac.authorization.k8s.io"}]}
+            await kubectl(c, "auth", "reconcile", "-f", _write(tmp_path, "r1.yaml", [role, rb]))   # creates (and the namespace)
+            live = await c.get("roles.rbac.authorization.k8s.io", "gpu-reader", "team")
+            live["rules"].append({"apiGroups": ["apps"], "resources": ["deployments"], "verbs": ["get"]})
+            await c.update(live)
+            role["rules"].append({"apiGroups": [""], "resources": ["services"], "verbs": ["watch"]})
+            rb["subjects"].append({"kind": "User", "name": "bob", "apiGroup": "rbac.authorization.k8s.io"})
+            await kubectl(c, "auth", "reconcile", "-f", _write(tmp_path, "r2.yaml", [role, rb]))
+            live = await c.get("roles.rbac.authorization.k8s.io", "gpu-reader", "team")
+            ok, missing = rbac.covers(live["rules"], role["rules"])
+            assert ok, missing
+            assert any("deployments" in (r.get("resources") or []) for r in live["rules"])
+            assert live["metadata"]["labels"] == {"tier": "gpu"}
+            b = await c.get("rolebindings.rbac.authorization.k8s.io", "readers", "team")
+            assert {s["name"] for s in b["subjects"]} == {"alice", "bob"}
+            # a changed roleRef re-creates the binding (new uid)
+            old_uid = m.uid_of(b)
+            rb["roleRef"]["name"] = "other"
+            await kubectl(c, "auth", "reconcile", "-f", _write(tmp_path, "r3.yaml", [rb]))
+            b = await c.get("rolebindings.rbac.authorization.k8s.io", "readers", "team")
+            assert b["roleRef"]["name"] == "other" and m.uid_of(b) != old_uid
+            # protected: left alone
+            live = await c.get("roles.rbac.authorization.k8s.io", "gpu-reader", "team")
+            live["metadata"].setdefault("annotations", {})[rbac.AUTOUPDATE] = "false"
+            live = await c.update(live)
+            role["rules"].append({"apiGroups": [""], "resources": ["secrets"], "verbs": ["get"]})
+            await kubectl(c, "auth", "reconcile", "-f", _write(tmp_path, "r4.yaml", [role]))
+            again = await c.get("roles.rbac.authorization.k8s.io", "gpu-reader", "team")
+            assert again["metadata"]["resourceVersion"] == live["metadata"]["resourceVersion"]
+    run(go())
+    assert "reconciled" in capsys.readouterr().out
+
+
+def test_rbac_rule_coverage():
+    from amdkube.api.rbac import covers
+    owner = [{"apiGroups": [""], "resources": ["pods", "*/status"], "verbs": ["get", "list"]},
+             {"nonResourceURLs": ["/healthz", "/api/*"], "verbs": ["get"]},
+             {"apiGroups": ["apps"], "resources": ["deployments"], "verbs": ["*"], "resourceNames": ["web"]}]
+    assert covers(owner, [{"apiGroups": [""], "resources": ["pods", "nodes/status"], "verbs": ["get"]}])[0]
+    assert covers(owner, [{"nonResourceURLs": ["/api/v1"], "verbs": ["get"]}])[0]
+    ok, miss = covers(owner, [{"apiGroups": ["apps"], "resources": ["deployments"], "verbs": ["update"]}])
+    assert not ok and miss == [{"apiGroups": ["apps"], "resources": ["deployments"], "verbs": ["update"]}]
+    assert covers(owner, [{"apiGroups": ["apps"], "resources": ["deployments"], "verbs": ["update"], "resourceNames": ["web"]}])[0]
