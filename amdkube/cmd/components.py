@@ -904,6 +904,71 @@ def gpu_health(argv):
     return 0
 
 
+def addon_manager(argv):
+    """cluster/addons/addon-manager/kube-addons.sh as a daemon (amdkube/addons.py). The reference's
+    environment knobs are flags here, with the environment as the default."""
+    ap = argparse.ArgumentParser("amdkube addon-manager")
+    ap.add_argument("--server", default="http://127.0.0.1:8080")
+    ap.add_argument("--kubeconfig", default=None)
+    ap.add_argument("--addon-path", default=os.environ.get("ADDON_PATH", "/etc/kubernetes/addons"))
+    ap.add_argument("--admission-controls-path", default="/etc/kubernetes/admission-controls")
+    ap.add_argument("--namespace-manifest", default=None, help="the kube-system Namespace manifest (/opt/namespace.yaml)")
+    ap.add_argument("--check-interval", type=float,
+                    default=float(os.environ.get("TEST_ADDON_CHECK_INTERVAL_SEC", "60")))
+    ap.add_argument("--leader-election", default=os.environ.get("ADDON_MANAGER_LEADER_ELECTION", "true"),
+                    choices=("true", "false"))
+    ap.add_argument("--once", action="store_true", help="bootstrap, one ensure+reconcile pass, exit")
+    ap.add_argument("-v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "addon-manager")
+    from ..addons import AddonManager
+
+    def mk_mgr():
+        return AddonManager(_client(a), a.addon_path, a.admission_controls_path, a.check_interval,
+                            leader_election=a.leader_election == "true", namespace_manifest=a.namespace_manifest)
+    if a.once:
+        async def once():
+            mgr = mk_mgr()
+            await mgr.bootstrap(30.0)
+            await mgr.sync_once()
+            await mgr.client.close()
+        asyncio.run(once())
+        return 0
+
+    async def mk():
+        return await mk_mgr().start()
+    _run_forever(mk)
+
+
+def node_problem_detector(argv):
+    """node-problem-detector with the system-log monitors of deploy/node-problem-detector
+    (monitoring/problemdetector.py); flags as in npd.yaml:46-51 and the reference's NPD e2e."""
+    ap = argparse.ArgumentParser("amdkube node-problem-detector")
+    ap.add_argument("--server", default="http://127.0.0.1:8080")
+    ap.add_argument("--apiserver-override", default=None, help="URL of the apiserver (?inClusterConfig=false is ignored)")
+    ap.add_argument("--kubeconfig", default=None)
+    ap.add_argument("--hostname-override", default=os.environ.get("NODE_NAME") or socket.gethostname())
+    ap.add_argument("--system-log-monitors", default="", help="comma-separated monitor configs")
+    ap.add_argument("--gpu-health-state", default="/var/lib/kubelet/device-plugin/amdkube-gpu-health.json",
+                    help="the AMD device plugin's health checkpoint; gpuFault rules report into it ('' = off)")
+    ap.add_argument("--resync-period", type=float, default=10.0)
+    ap.add_argument("--logtostderr", action="store_true")
+    ap.add_argument("-v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "node-problem-detector")
+    if a.apiserver_override:
+        a.server = a.apiserver_override.split("?", 1)[0]
+    from ..monitoring.problemdetector import MonitorConfig, NodeProblemDetector
+    configs = [MonitorConfig.load(p) for p in a.system_log_monitors.split(",") if p]
+    if not configs:
+        ap.error("no --system-log-monitors")
+
+    async def mk():
+        return await NodeProblemDetector(_client(a), a.hostname_override, configs, a.gpu_health_state or None,
+                                         resync=a.resync_period).start()
+    _run_forever(mk)
+
+
 def exporter(argv):
     ap = argparse.ArgumentParser("amdkube amdgpu-exporter")
     ap.add_argument("--backend", default="auto")
@@ -1178,7 +1243,7 @@ def kubeadm(argv):
 COMPONENTS = {"etcd": etcd, "dns": dns, "kube-dns": dns, "kubeadm": kubeadm, "proxy": proxy, "kube-proxy": proxy, "apiserver": apiserver, "kube-apiserver": apiserver, "scheduler": scheduler, "kube-scheduler": scheduler,
               "controller-manager": controller_manager, "kube-controller-manager": controller_manager, "kubelet": kubelet,
               "rocshim": rocshim, "amd-device-plugin": device_plugin, "device-plugin": device_plugin,
-              "gpu-health": gpu_health,
+              "gpu-health": gpu_health, "addon-manager": addon_manager, "node-problem-detector": node_problem_detector,
               "amdgpu-exporter": exporter, "exporter": exporter, "hollow-node": hollow_node, "local-up": local_up,
               "metrics-server": metrics_server, "cloud-controller-manager": cloud_controller_manager,
               "gke-certificates-controller": gke_certificates_controller, "rktshim": rktshim}

@@ -208,11 +208,27 @@ class AMDGPUPlugin(DevicePluginServer):
                 if self.reasons.get(did, "").startswith("probe:"):
                     self.reasons[did] = ""
 
+    def _apply_external_faults(self):
+        """Kernel-log faults from the node-problem-detector's amdgpu rules: the named PCI address
+        (a partitioned GPU's parent address covers all of its partitions) or device ID."""
+        for ent in self.monitor.pending_faults():
+            dev = str(ent["device"]).lower()
+            why = f"{ent.get('source') or 'kernel log'}: {ent['reason']}"
+            hit = False
+            for did, g in self.by_id.items():
+                if dev in (did.lower(), str(g.get("bdf") or "").lower(), str(g.get("parent_bdf") or "").lower()):
+                    log.warning("gpu %s: %s", did, why)
+                    self.monitor.fault(g["index"], why)
+                    hit = True
+            if not hit:
+                log.info("kernel-log fault on %s names no GPU of this plugin", dev)
+
     async def _health_loop(self):
         while True:
             await asyncio.sleep(self.health_interval)
             try:
                 self._apply_resets()
+                self._apply_external_faults()
                 self._check_health()
             except Exception as e:  # keep serving; the next tick retries
                 log.error("health check failed: %s", e)

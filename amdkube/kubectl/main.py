@@ -94,17 +94,34 @@ def _emit(objs, a, kind=None, single=False, out=None):
             print(f"No resources found.", file=out)
 
 
-def _read_files(paths) -> list[dict]:
+MANIFEST_EXTS = (".yaml", ".yml", ".json")
+
+
+def manifest_paths(p: str, recursive: bool = False) -> list[str]:
+    """A directory's manifests (resource.FileVisitorForSTDIN / ExpandPathsToFileVisitors: only
+    .json/.yaml/.yml, sub-directories with --recursive), or the file itself."""
+    if not os.path.isdir(p):
+        return [p]
+    out = []
+    for f in sorted(os.listdir(p)):
+        fp = os.path.join(p, f)
+        if os.path.isdir(fp):
+            if recursive:
+                out += manifest_paths(fp, True)
+        elif f.endswith(MANIFEST_EXTS):
+            out.append(fp)
+    return out
+
+
+def _read_files(paths, recursive: bool = False) -> list[dict]:
     docs = []
     for p in paths:
         if p == "-":
             docs += load_manifests(sys.stdin.read())
-        elif os.path.isdir(p):
-            for f in sorted(os.listdir(p)):
-                if f.endswith((".yaml", ".yml", ".json")):
-                    docs += load_manifests(open(os.path.join(p, f)).read())
-        else:
-            docs += load_manifests(open(p).read())
+            continue
+        for fp in manifest_paths(p, recursive):
+            with open(fp) as f:
+                docs += load_manifests(f.read())
     return docs
 
 

@@ -63,9 +63,20 @@ class _Same:
 _SAME = _Same()
 
 
-async def apply_docs(c, a, docs):
+async def apply_docs(c, a, docs, out=print, allow_empty: bool = False):
+    """`out`: where the per-object result lines go. With -l only the manifests whose labels
+    match are applied (the builder's LabelSelectorParam filters local files too), and
+    `allow_empty` lets a prune run when none match (apply.go returns "no objects passed to
+    apply" first, so removing an addon's last manifest never prunes it; the addon manager
+    passes True)."""
+    from ..api.labels import parse_selector
+    sel = parse_selector(a.selector) if getattr(a, "selector", None) else None
     applied = set()
+    count = 0
     for doc in docs:
+        if sel is not None and not sel.matches(m.labels_of(doc)):
+            continue
+        count += 1
         ri = SCHEME.for_object(doc)
         if ri is None:
             raise SystemExit(f"error: unknown kind {doc.get('apiVersion')}/{doc.get('kind')}")
@@ -80,8 +91,10 @@ async def apply_docs(c, a, docs):
         if cur is None:
             doc.setdefault("metadata", {}).setdefault("annotations", {})[LAST_APPLIED] = manifest
             obj = await c.create(doc, ns)
-            print(f"{ri.kind.lower()}/{m.name_of(obj)} created")
+            applied.add(m.uid_of(obj))
+            out(f"{ri.kind.lower()}/{m.name_of(obj)} created")
             continue
+        applied.add(m.uid_of(cur))
         original = json.loads(m.annotations_of(cur).get(LAST_APPLIED) or "{}")
         modified = copy.deepcopy(doc)
         modified.setdefault("metadata", {}).setdefault("annotations", {})[LAST_APPLIED] = manifest
@@ -91,7 +104,7 @@ async def apply_docs(c, a, docs):
             except smp.PatchError as e:
                 raise SystemExit(f"error: {ri.kind.lower()}/{name}: {e}")
             if patch is None:
-                print(f"{ri.kind.lower()}/{name} unchanged")
+                out(f"{ri.kind.lower()}/{name} unchanged")
                 break
             try:
                 await c.patch(res, name, patch, ns, patch_type=ctype)
@@ -103,14 +116,17 @@ async def apply_docs(c, a, docs):
                     await c.delete(res, name, ns)             # --force: delete and re-create
                     await _wait_gone(c, res, name, ns)
                     doc.setdefault("metadata", {}).setdefault("annotations", {})[LAST_APPLIED] = manifest
-                    await c.create(doc, ns)
-                    print(f"{ri.kind.lower()}/{name} replaced")
+                    applied.add(m.uid_of(await c.create(doc, ns)))
+                    out(f"{ri.kind.lower()}/{name} replaced")
                     break
                 raise
-            print(f"{ri.kind.lower()}/{name} configured")
+            out(f"{ri.kind.lower()}/{name} configured")
             break
+    if count == 0 and not allow_empty:
+        raise SystemExit("error: no objects passed to apply")
     if getattr(a, "prune", False):
-        await _prune(c, a, applied)
+        await _prune(c, a, applied, out)
+    return applied
 
 
 async def _wait_gone(c, res, name, ns, timeout: float = 30.0):
@@ -128,21 +144,42 @@ PRUNE_WHITELIST = ("configmaps", "endpoints", "namespaces", "persistentvolumecla
                    "deployments.apps", "replicasets.apps", "statefulsets.apps", "ingresses.extensions")
 
 
-async def _prune(c, a, applied):
+def prune_resources(whitelist) -> list[str]:
+    """--prune-whitelist <group>/<version>/<Kind> entries (core/v1/ConfigMap) → resources."""
+    if not whitelist:
+        return list(PRUNE_WHITELIST)
+    out = []
+    for gvk in whitelist:
+        parts = gvk.split("/")
+        if len(parts) != 3:
+            raise SystemExit(f"error: invalid GroupVersionKind format: {gvk}, please follow <group/version/kind>")
+        group = "" if parts[0] == "core" else parts[0]
+        ri = SCHEME.for_object({"apiVersion": f"{group}/{parts[1]}" if group else parts[1], "kind": parts[2]})
+        if ri is None:
+            raise SystemExit(f"error: unknown prune resource {gvk}")
+        out.append(ri.plural if not ri.group else f"{ri.plural}.{ri.group}")
+    return out
+
+
+async def _prune(c, a, applied, out=print):
     if not a.selector and not a.all:
         raise SystemExit("error: all resources selected for prune without explicitly passing --all or -l")
-    namespaces = {ns for (_g, _p, ns, _n) in applied if ns} or {a.namespace or "default"}
-    for res in PRUNE_WHITELIST:
+    # `applied`: (group, plural, namespace, name) of every manifest plus the UIDs it created or
+    # patched; the pruner skips visited UIDs (apply.go visitedUids), so a kind served by two
+    # groups (extensions and apps DaemonSets) is never pruned through its other name
+    namespaces = {t[2] for t in applied if isinstance(t, tuple) and t[2]} or {a.namespace or "default"}
+    for res in prune_resources(getattr(a, "prune_whitelist", None)):
         ri = SCHEME.resolve(res)
         for ns in (namespaces if ri.namespaced else {""}):
             items, _ = await c.list(res, ns, a.selector)
             for o in items:
                 if LAST_APPLIED not in m.annotations_of(o):
                     continue
-                if (ri.group, ri.plural, m.namespace_of(o) if ri.namespaced else "", m.name_of(o)) in applied:
+                if m.uid_of(o) in applied or \
+                        (ri.group, ri.plural, m.namespace_of(o) if ri.namespaced else "", m.name_of(o)) in applied:
                     continue
                 await c.delete(res, m.name_of(o), m.namespace_of(o) if ri.namespaced else "")
-                print(f"{ri.kind.lower()}/{m.name_of(o)} pruned")
+                out(f"{ri.kind.lower()}/{m.name_of(o)} pruned")
 
 
 async def cmd_apply(c, a):
@@ -182,7 +219,7 @@ async def cmd_apply(c, a):
         await c.patch(_res(ri), name, {"metadata": {"annotations": {LAST_APPLIED: json.dumps(new, sort_keys=True)}}}, ns)
         print(f"{ri.kind.lower()}/{name} edited")
         return
-    docs = _read_files(a.filename)
+    docs = _read_files(a.filename, getattr(a, "recursive", False))
     if a.output and a.dry_run:
         _emit(docs, a, docs[0]["kind"] if docs else "List")
         return
@@ -512,6 +549,7 @@ async def cmd_cluster_info_dump(c, a):
 
 def add_arguments(sp):
     sp.add_argument("--prune", action="store_true")
+    sp.add_argument("--prune-whitelist", action="append", default=[])
     sp.add_argument("--dry-run", action="store_true")
     sp.add_argument("--create-annotation", action="store_true")
     sp.add_argument("--env", "-e", action="append", default=[])

@@ -630,7 +630,10 @@ class Kubelet:
         if labels.get(TOPOLOGY_LABEL):
             ann[TOPOLOGY_LABEL] = labels[TOPOLOGY_LABEL]
         try:
-            self.node = await self.client.patch("nodes", self.node_name, patch, sub="status")
+            # strategic merge (nodeutil.PatchNodeStatus): conditions and addresses merge by
+            # `type`, so conditions other components own (node-problem-detector) survive
+            self.node = await self.client.patch("nodes", self.node_name, patch, sub="status",
+                                                patch_type="application/strategic-merge-patch+json")
             cidr = (self.node.get("spec") or {}).get("podCIDR") or self.cfg.pod_cidr or ""
             if cidr and cidr != getattr(self, "_pod_cidr", ""):
                 # kubelet_network.go updatePodCIDR → CRI UpdateRuntimeConfig

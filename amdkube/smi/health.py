@@ -25,6 +25,11 @@ reason instead of being re-baselined into service. `amdkube gpu-health reset <id
 `<state_file>.reset` request that the running plugin applies on its next health tick (fresh
 baseline, fault cleared). Without a state file the state lives as long as the process. The
 reason is published as the `amd.com/health-reason` attribute.
+
+Faults the RAS counters cannot see come from the kernel log: the node-problem-detector's
+amdgpu rules (monitoring/problemdetector.py) append `{"device": <pci address|device id>,
+"reason": …}` lines to `<state_file>.faults`; `pending_faults()` hands them to the plugin,
+which makes them sticky like any other fault (`fault()`).
 """
 from __future__ import annotations
 
@@ -88,6 +93,39 @@ class HealthMonitor:
             return ids
         except FileNotFoundError:
             return set()
+
+    def pending_faults(self) -> list[dict]:
+        """Faults reported from outside (the node-problem-detector) since the last call."""
+        if not self.state_file:
+            return []
+        req = self.state_file + ".faults"
+        try:
+            tmp = req + f".{os.getpid()}"
+            os.replace(req, tmp)              # take the whole file; a writer appending now starts a new one
+        except FileNotFoundError:
+            return []
+        out = []
+        with open(tmp) as f:
+            for line in f:
+                try:
+                    ent = json.loads(line)
+                except ValueError:
+                    continue
+                if isinstance(ent, dict) and ent.get("device") and ent.get("reason"):
+                    out.append(ent)
+        os.unlink(tmp)
+        return out
+
+    def fault(self, index: int, why: str):
+        """Take a device out of service until an operator resets it (checkpointed)."""
+        if index in self.sticky:
+            return
+        if index not in self.baseline:
+            self.snapshot(index)
+        self.sticky[index] = why
+        ent = self._saved.setdefault(self.key_of(index), {"baseline": self.baseline.get(index) or {}})
+        ent["sticky"], ent["faulted_at"] = why, time.time()
+        self._save()
 
     def reset(self, index: int):
         """Clear a device's fault and judge it from a fresh baseline from now on."""
