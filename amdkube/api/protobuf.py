@@ -24,6 +24,13 @@ descriptor_pb2 at first use, then converts between the API's JSON dicts and mess
 
 Fields the schema does not know are dropped by an encode, as the reference's typed decode
 would; `lossless()` tells a caller (storage) whether an object survives the round trip.
+
+The hot path is native: amdkube/_native/_kproto (native/kproto.cpp) walks the dicts and writes
+/reads wire bytes directly from a flat table built here from the same descriptors, and reports
+losslessness during the encode (`encode_checked`), so storage no longer decodes every write to
+find out. The message-object path below stays for the rare types _kproto hands back by
+callback (Duration, RawExtension, JSON Schema props) and as the fallback when the extension is
+not built (AMDKUBE_REQUIRE_NATIVE=1 makes that an error).
 Watch streams frame each WatchEvent with a 4-byte big-endian length
 (apimachinery/pkg/util/framer LengthDelimitedFramer); the event's object is itself enveloped.
 """
@@ -325,6 +332,8 @@ def _fill_special(msg, d, fq) -> bool:
             msg.property.extend(d)
         else:
             _fill(msg.schema, d, f"{APIEXT}.JSONSchemaProps")
+    elif fq.endswith(".ExtraValue"):          # a JSON list of strings (authentication ExtraValue)
+        msg.items.extend(str(x) for x in d)
     else:
         return False
     return True
@@ -334,8 +343,12 @@ _SPECIAL = {TIME, MICROTIME, DURATION, QUANTITY, INTORSTR, RAWEXT, f"{APIEXT}.JS
             f"{APIEXT}.JSONSchemaPropsOrBool", f"{APIEXT}.JSONSchemaPropsOrStringArray"}
 
 
+def _is_special(fq: str) -> bool:
+    return fq in _SPECIAL or fq.endswith(".ExtraValue")
+
+
 def _fill(msg, d, fq: str):
-    if fq in _SPECIAL:
+    if _is_special(fq):
         _fill_special(msg, d, fq)
         return
     if not isinstance(d, dict):
@@ -396,11 +409,13 @@ def _dump_special(msg, fq):
         return _dump(msg.schema, f"{APIEXT}.JSONSchemaProps") if msg.HasField("schema") else msg.allows
     if fq == f"{APIEXT}.JSONSchemaPropsOrStringArray":
         return list(msg.property) if len(msg.property) else _dump(msg.schema, f"{APIEXT}.JSONSchemaProps")
+    if fq.endswith(".ExtraValue"):
+        return list(msg.items)
     raise KeyError(fq)
 
 
 def _dump(msg, fq: str):
-    if fq in _SPECIAL:
+    if _is_special(fq):
         return _dump_special(msg, fq)
     by_num = _plan(msg.DESCRIPTOR).by_num
     out = {}
@@ -423,6 +438,92 @@ def _dump(msg, fq: str):
     return out
 
 
+# ------------------------------------------------------------------------- native layer
+_SP_CODES = {TIME: 1, MICROTIME: 2, QUANTITY: 3, INTORSTR: 4}
+_KINDS = {SCALAR: 0, MSG: 1, REP_SCALAR: 2, REP_MSG: 3, MAP_SCALAR: 4, MAP_MSG: 5}
+
+
+class _Native:
+    """The _kproto table: one entry per message of the wire table, in a fixed order."""
+
+    def __init__(self, mod):
+        self.mod = mod
+        sc = schema()
+        self.names = [f"{pkg}.{mn}" for pkg in sorted(sc.packages) for mn in sorted(sc.packages[pkg])]
+        self.index = {n: i for i, n in enumerate(self.names)}
+        descs = [sc.pool.FindMessageTypeByName(n) for n in self.names]
+        entries = []
+        for fq, desc in zip(self.names, descs):
+            if fq in _SP_CODES:
+                special = _SP_CODES[fq]
+            elif fq.endswith(".ExtraValue"):
+                special = 5
+            elif fq in _SPECIAL:
+                special = 9
+            else:
+                special = 0
+            ov = sc.json.get(fq) or {}
+            rename, inline = ov.get("rename") or {}, set(ov.get("inline") or ())
+            fields = []
+            for fd in sorted(desc.fields, key=lambda f: f.number):
+                mt = fd.message_type
+                if fd.name in inline:
+                    fields.append((fd.number, None, 6, 0, 0, self.index[mt.full_name]))
+                    continue
+                key = rename.get(fd.name, fd.name)
+                if mt is not None and mt.GetOptions().map_entry:
+                    kfd, vfd = mt.fields_by_name["key"], mt.fields_by_name["value"]
+                    if vfd.message_type is not None:
+                        fields.append((fd.number, key, 5, 11, kfd.type, self.index[vfd.message_type.full_name]))
+                    else:
+                        fields.append((fd.number, key, 4, vfd.type, kfd.type, -1))
+                elif mt is not None:
+                    fields.append((fd.number, key, 3 if fd.is_repeated else 1, 11, 0, self.index[mt.full_name]))
+                else:
+                    fields.append((fd.number, key, 2 if fd.is_repeated else 0, fd.type, 0, -1))
+            entries.append([special, fields, None])
+
+        def keys(i, seen=()):
+            out = set()
+            for num, key, kind, _st, _kt, sub in entries[i][1]:
+                if kind == 6:
+                    if sub not in seen:
+                        out |= keys(sub, seen + (i,))
+                else:
+                    out.add(key)
+            return out
+        for i, e in enumerate(entries):
+            e[2] = frozenset(keys(i))
+        mod.init([tuple(e) for e in entries], ProtoError, self._enc_cb, self._dec_cb)
+
+    def _enc_cb(self, mi: int, value):
+        fq = self.names[mi]
+        msg = schema().cls(fq)()
+        _fill(msg, value, fq)
+        if fq == DURATION:
+            ok = isinstance(value, str) and format_duration(msg.duration) == value
+        elif fq in (RAWEXT, f"{APIEXT}.JSON"):
+            ok = True
+        else:
+            ok = _norm(_dump(msg, fq)) == _norm(value)
+        return msg.SerializeToString(), ok
+
+    def _dec_cb(self, mi: int, data: bytes):
+        fq = self.names[mi]
+        return _dump(schema().cls(fq).FromString(data), fq)
+
+
+@functools.lru_cache(maxsize=1)
+def native() -> _Native | None:
+    try:
+        from .._native import _kproto
+    except ImportError as e:
+        if os.environ.get("AMDKUBE_REQUIRE_NATIVE") == "1":
+            raise ImportError(f"amdkube._native._kproto is not built ({e}); run native/build.py") from e
+        return None
+    return _Native(_kproto)
+
+
 # ------------------------------------------------------------------------- public API
 def to_message(obj: dict, fq: str):
     msg = schema().cls(fq)()
@@ -434,30 +535,64 @@ def from_message(msg) -> dict:
     return _dump(msg, msg.DESCRIPTOR.full_name)
 
 
-def encode(obj: dict) -> bytes:
-    """`k8s\\x00` + runtime.Unknown for an object of a kind with a protobuf schema."""
+def encode_raw(obj: dict, fq: str, strict: bool = False) -> tuple[bytes, bool | None]:
+    """The object's own message bytes; with `strict` also whether a decode gives it back."""
+    nat = native()
+    if nat is not None:
+        return nat.mod.encode(obj, nat.index[fq], strict)
+    return to_message(obj, fq).SerializeToString(), None
+
+
+def decode_raw(raw: bytes, fq: str) -> dict:
+    nat = native()
+    if nat is not None:
+        return nat.mod.decode(raw, nat.index[fq])
+    return from_message(schema().cls(fq).FromString(raw))
+
+
+def _encode(obj: dict, strict: bool) -> tuple[bytes, bool | None]:
     av, kind = obj.get("apiVersion", ""), obj.get("kind", "")
     fq = message_for(av, kind)
     if fq is None:
         raise ProtoError(f"no protobuf schema for {av} {kind}")
-    raw = to_message(obj, fq).SerializeToString()
-    unk = schema().cls(f"{RUNTIME}.Unknown")(raw=raw)
-    unk.typeMeta.apiVersion, unk.typeMeta.kind = av, kind
-    return MAGIC + unk.SerializeToString()
+    raw, ok = encode_raw(obj, fq, strict)
+    return envelope(av, kind, raw), ok
+
+
+def encode(obj: dict) -> bytes:
+    """`k8s\\x00` + runtime.Unknown for an object of a kind with a protobuf schema."""
+    return _encode(obj, False)[0]
+
+
+def encode_checked(obj: dict) -> tuple[bytes, bool]:
+    """(encode(obj), lossless(obj, that)) — natively in one pass."""
+    data, ok = _encode(obj, True)
+    return data, (lossless(obj, data) if ok is None else ok)
+
+
+def envelope_parts(data: bytes) -> tuple[str, str, bytes, str]:
+    """(apiVersion, kind, raw, contentType) of a `k8s\\x00` runtime.Unknown."""
+    if not data.startswith(MAGIC):
+        raise ProtoError("missing the k8s protobuf magic")
+    nat = native()
+    if nat is not None:
+        parts = nat.mod.envelope_parts(data)
+        if parts is None:
+            raise ProtoError("malformed runtime.Unknown envelope")
+        return parts
+    unk = schema().cls(f"{RUNTIME}.Unknown").FromString(data[4:])
+    return unk.typeMeta.apiVersion, unk.typeMeta.kind, unk.raw, unk.contentType
 
 
 def decode(data: bytes) -> dict:
-    if not data.startswith(MAGIC):
-        raise ProtoError("missing the k8s protobuf magic")
-    unk = schema().cls(f"{RUNTIME}.Unknown").FromString(data[4:])
-    av, kind = unk.typeMeta.apiVersion, unk.typeMeta.kind
-    if unk.contentType and "json" in unk.contentType:      # a JSON payload in the envelope
-        obj = json.loads(unk.raw)
+    av, kind, raw, ctype = envelope_parts(data)
+    if ctype and "json" in ctype:      # a JSON payload in the envelope
+        obj = json.loads(raw)
     else:
         fq = message_for(av, kind)
         if fq is None:
             raise ProtoError(f"no protobuf schema for {av} {kind}")
-        obj = from_message(schema().cls(fq).FromString(unk.raw))
+        obj = decode_raw(raw, fq)
     out = {"apiVersion": av, "kind": kind} if av or kind else {}
     out.update(obj)
     if kind.endswith("List") and isinstance(out.get("items"), list):
@@ -491,11 +626,14 @@ def lossless(obj: dict, data: bytes | None = None) -> bool:
 
 
 def encode_watch_event(etype: str, obj: dict) -> bytes:
-    """One frame of a protobuf watch: 4-byte big-endian length + meta/v1 WatchEvent whose object
-    is the enveloped object (staging/.../endpoints/handlers/watch.go, framer)."""
-    ev = schema().cls(f"{META}.WatchEvent")(type=etype)
-    ev.object.raw = encode(obj) if supports(obj) else MAGIC + _json_unknown(obj)
-    b = ev.SerializeToString()
+    """One frame of a protobuf watch: 4-byte big-endian length + meta/v1 WatchEvent{type = 1,
+    object = 2 (RawExtension{raw = 1})} whose object is the enveloped object
+    (staging/.../endpoints/handlers/watch.go, framer)."""
+    return watch_frame(etype, encode(obj) if supports(obj) else MAGIC + _json_unknown(obj))
+
+
+def watch_frame(etype: str, enveloped: bytes) -> bytes:
+    b = _ld(1, etype.encode()) + _ld(2, _ld(1, enveloped))
     return struct.pack(">I", len(b)) + b
 
 
@@ -534,6 +672,10 @@ def unwrap_raw(data: bytes) -> bytes | None:
     envelope's top-level fields — no decode; None if the payload is not a protobuf object."""
     if data[:4] != MAGIC:
         return None
+    nat = native()
+    if nat is not None:
+        parts = nat.mod.envelope_parts(data)
+        return None if parts is None or "json" in parts[3] else parts[2]
     i, n, raw, json_payload = 4, len(data), None, False
     while i < n:
         key, shift = 0, 0
@@ -570,6 +712,9 @@ def envelope(api_version: str, kind: str, raw: bytes) -> bytes:
 def list_from_stored(api_version: str, list_kind: str, resource_version: str, stored: list[bytes]) -> bytes | None:
     """A <Kind>List envelope spliced from stored protobuf objects (ListMeta = 1, items = 2) without
     decoding any item; None when an item is stored as JSON."""
+    nat = native()
+    if nat is not None:
+        return nat.mod.splice_list(api_version, list_kind, resource_version, stored)
     parts = [_ld(1, _ld(2, resource_version.encode()))]       # ListMeta.resourceVersion = 2
     for v in stored:
         raw = unwrap_raw(v)

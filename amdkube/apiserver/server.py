@@ -28,7 +28,7 @@ from ..api.scheme import SCHEME
 from ..store import MVCCStore, PUT
 from ..utils import profiling
 from ..utils.metrics import CONTENT_TYPE, MICRO_BUCKETS, Counter, Histogram, new_registry, render
-from ..store.storage import json_bytes
+from ..store.storage import kv_json, kv_proto
 from . import admission as adm
 from .registry import Registry
 from .service import ServiceAllocator, parse_port_range
@@ -762,19 +762,21 @@ class APIServer:
                     return _resp(_to_scale(rs.get(ns, name)))
                 if as_stored and _wants_protobuf(request):
                     kv = rs.storage.store.get(rs.key(ns, name))
-                    if kv is not None and kv.value[:4] == b"k8s\x00":
-                        # protobuf storage, protobuf client, same version: the stored bytes ARE the answer
-                        return web.Response(body=kv.value, content_type="application/vnd.kubernetes.protobuf")
+                    body = kv_proto(kv) if kv is not None else None
+                    if body is not None:
+                        # protobuf client, same version: the stored bytes (or their cached transcode)
+                        return web.Response(body=body, content_type="application/vnd.kubernetes.protobuf")
                 raw = rs.storage.get_raw(rs.key(ns, name))
                 if raw is None:
                     raise m.not_found(ri.group_resource, name)
                 return _resp(raw)
-            if as_stored and _wants_protobuf(request) and rs.storage.media_type != _JSON \
+            if as_stored and _wants_protobuf(request) \
                     and not any(q.get(k) for k in ("labelSelector", "fieldSelector", "limit", "continue")) \
                     and not self._hide_uninitialized(q):
                 from ..api import protobuf as pb
                 kvs, rev, _ = rs.storage.store.range(rs.prefix(ns))
-                body = pb.list_from_stored(ri.api_version, ri.list_kind, str(rev), [kv.value for kv in kvs])
+                vals = [kv_proto(kv) for kv in kvs]
+                body = None if None in vals else pb.list_from_stored(ri.api_version, ri.list_kind, str(rev), vals)
                 if body is not None:
                     return web.Response(body=body, content_type=pb.MEDIA_TYPE)
             return self._list(rs, ns, q)
@@ -968,6 +970,10 @@ class APIServer:
                 json_frame = frame
 
                 def frame(t, _jf=json_frame):
+                    if conv is None and t[2].type == PUT:    # the object's (cached) protobuf form
+                        raw = kv_proto(t[2].kv)
+                        if raw is not None:
+                            return pb.watch_frame(t[0], raw)
                     ev = json.loads(_jf(t))
                     return pb.encode_watch_event(ev["type"], ev["object"])
             if self._hide_uninitialized(q):
@@ -1022,7 +1028,7 @@ class APIServer:
     def _frame(t) -> bytes:
         typ, obj, ev = t
         if ev.type == PUT:
-            data = json_bytes(ev.kv.value)
+            data = kv_json(ev.kv)
         else:
             data = json.dumps(obj, separators=(",", ":")).encode()
         return b'{"type":"' + typ.encode() + b'","object":' + data + b"}\n"

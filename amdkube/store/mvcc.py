@@ -48,10 +48,13 @@ class Compacted(Exception):
 
 
 class KV:
-    __slots__ = ("key", "value", "create_rev", "mod_rev", "version")
+    # alt: the value in the other wire format (JSON <-> protobuf), filled on first demand by
+    # store/storage.py; a KV never changes, so neither does its transcode
+    __slots__ = ("key", "value", "create_rev", "mod_rev", "version", "alt")
 
     def __init__(self, key, value, create_rev, mod_rev, version):
         self.key, self.value, self.create_rev, self.mod_rev, self.version = key, value, create_rev, mod_rev, version
+        self.alt = None
 
     def __repr__(self):
         return f"KV({self.key!r}, rev={self.mod_rev})"

@@ -34,8 +34,8 @@ def _with_rv(obj: dict, media_type: str = JSON_MEDIA_TYPE):
         if media_type == PROTO_MEDIA_TYPE:
             from ..api import protobuf as pb
             if pb.supports(obj):
-                data = pb.encode(obj)
-                if pb.lossless(obj, data):
+                data, ok = pb.encode_checked(obj)
+                if ok:
                     return data
         return json.dumps(obj, separators=(",", ":")).encode()
     return build
@@ -53,6 +53,37 @@ def json_bytes(value: bytes) -> bytes:
     if value[:4] == PROTO_MAGIC:
         return json.dumps(decode_kv(value), separators=(",", ":")).encode()
     return value
+
+
+# Serving the format a KV is NOT stored in costs a transcode. A KV is immutable, so the transcode
+# is done once and kept on it (the reference's later cachingObject, which memoizes each object's
+# serialization per encoding for all watchers and lists: apiserver/pkg/storage/cacher/
+# caching_object.go). A LIST in the other format is then a splice of cached bytes.
+def kv_json(kv) -> bytes:
+    v = kv.value
+    if v[:4] != PROTO_MAGIC:
+        return v
+    alt = kv.alt
+    if alt is None:
+        alt = kv.alt = json_bytes(v)
+    return alt
+
+
+def kv_proto(kv) -> bytes | None:
+    """The KV's object as a `k8s\x00` protobuf envelope; None for kinds without a protobuf schema."""
+    v = kv.value
+    if v[:4] == PROTO_MAGIC:
+        return v
+    alt = kv.alt
+    if alt is None:
+        from ..api import protobuf as pb
+        try:
+            obj = json.loads(v)
+            alt = pb.encode(obj) if isinstance(obj, dict) and pb.supports(obj) else b""
+        except (ValueError, pb.ProtoError):
+            alt = b""
+        kv.alt = alt
+    return alt or None
 
 
 def event_object(ev: Event) -> dict:
@@ -168,7 +199,7 @@ class Storage:
     def get_raw(self, key: str) -> bytes | None:
         """The object as JSON bytes (stored bytes when stored as JSON)."""
         kv = self.store.get(key)
-        return json_bytes(kv.value) if kv else None
+        return kv_json(kv) if kv else None
 
     def guaranteed_update(self, key: str, try_update: Callable[[dict], dict | None],
                           precond_uid: str | None = None, precond_rv: str | None = None,
@@ -239,7 +270,7 @@ class Storage:
 
     def list_raw(self, prefix: str):
         kvs, rev, _ = self.store.range(prefix)
-        return [json_bytes(kv.value) for kv in kvs], rev
+        return [kv_json(kv) for kv in kvs], rev
 
     # ------------------------------------------------------------------ watch
     def watch(self, prefix: str, rv: str | int | None, flt: Filter | None = None, exact=False) -> "FilteredWatch":

@@ -5,7 +5,7 @@
   python native/build.py --sanitize # also the ASan/UBSan host builds (pause, topo self-test, sampler)
                                     # and the ThreadSanitizer build of the activity sampler
 
-Outputs: amdkube/_native/{_amdsmi,_topo,_hipops}.<ext> and amdkube/_native/bin/{pause,
+Outputs: amdkube/_native/{_amdsmi,_topo,_kproto,_hipops}.<ext> and amdkube/_native/bin/{pause,
 rocm-vector-add,hsa-vector-add,hbm-probe,gpu-burn,xgmi-probe[,topo-selftest-asan,pause-asan,amdkube-nsexec-asan,
 seccomp-check-asan,sampler-selftest-{asan,tsan}]}.
 Targets are rebuilt only when a source/header is newer than the output.
@@ -46,6 +46,10 @@ def targets(sanitize=False, cpu_only=False):
     t = [
         (n(OUT, "_topo" + EXT), [n("native/topo_alloc.cpp"), n("native/topo_core.h")],
          ["g++", "-O3", "-std=c++17", "-shared", "-fPIC", *py, n("native/topo_alloc.cpp"), "-o", "{out}"]),
+        # the apiserver's JSON <-> protobuf transcoder (plain CPython API)
+        (n(OUT, "_kproto" + EXT), [n("native/kproto.cpp")],
+         ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wall", "-fno-strict-aliasing",
+          f"-I{sysconfig.get_paths()['include']}", n("native/kproto.cpp"), "-o", "{out}"]),
         (n(OUT, "_amdsmi" + EXT), [n("native/amdsmi_shim.cpp"), n("native/sampler_core.h")],
          ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", *py, *rocm_inc, n("native/amdsmi_shim.cpp"), *rpath,
           "-lamd_smi", "-o", "{out}"]),

@@ -239,3 +239,70 @@ def test_apiserver_negotiates_protobuf_and_stores_it():
             finally:
                 await pc.close()
     run(go(), 60)
+
+
+def _python_path(obj):
+    """The message-object (upb) path the native transcoder replaced."""
+    fq = pb.message_for(obj["apiVersion"], obj["kind"])
+    return fq, pb.to_message(obj, fq).SerializeToString()
+
+
+@pytest.mark.parametrize("obj", [GPU_POD, NODE, BINDING, EVENT] + OTHERS, ids=lambda o: o["kind"])
+def test_native_transcoder_matches_the_message_path(obj):
+    """native/kproto.cpp against the upb message path: each decodes the other's bytes to the same
+    object, and its own bytes parse under the generated descriptors to the same message."""
+    nat = pb.native()
+    assert nat is not None, "amdkube._native._kproto is not built"
+    fq, py_raw = _python_path(obj)
+    nat_raw, ok = nat.mod.encode(obj, nat.index[fq], True)
+    assert ok is True
+    cls = pb.schema().cls(fq)
+    assert cls.FromString(nat_raw) == cls.FromString(py_raw)        # same message, field for field
+    assert nat.mod.decode(py_raw, nat.index[fq]) == pb.from_message(cls.FromString(py_raw))
+    assert pb._norm(nat.mod.decode(nat_raw, nat.index[fq])) == pb._norm({k: v for k, v in obj.items()
+                                                                          if k not in ("apiVersion", "kind")})
+
+
+def test_native_lossless_flag_agrees_with_a_round_trip():
+    base = json.loads(json.dumps(GPU_POD))
+    variants = []
+    v = json.loads(json.dumps(base)); v["spec"]["amdkubeOnly"] = {"x": 1}; variants.append(v)              # unknown key
+    v = json.loads(json.dumps(base)); v["metadata"]["creationTimestamp"] = "2026-10-17T05:00:00+02:00"; variants.append(v)
+    v = json.loads(json.dumps(base)); v["metadata"]["creationTimestamp"] = "2026-10-17T03:00:00.5Z"; variants.append(v)
+    v = json.loads(json.dumps(base)); v["spec"]["terminationGracePeriodSeconds"] = "30"; variants.append(v)  # coerced
+    v = json.loads(json.dumps(base)); v["spec"]["hostNetwork"] = 1; variants.append(v)
+    v = json.loads(json.dumps(base)); v["spec"]["containers"][0]["image"] = 7; variants.append(v)
+    v = json.loads(json.dumps(base)); v["spec"]["nodeSelector"] = {}; variants.append(v)                    # empty: fine
+    v = json.loads(json.dumps(base)); v["metadata"]["labels"]["gone"] = None; variants.append(v)           # None: fine
+    for v in variants:       # the native flag is conservative: lossless only when a decode gives v back
+        data, ok = pb.encode_checked(v)
+        assert not ok or pb.lossless(v, data), json.dumps(v)[:300]
+    assert [pb.encode_checked(v)[1] for v in variants] == [False, False, False, False, False, False, True, True]
+    with pytest.raises(pb.ProtoError):
+        pb.encode({"apiVersion": "v1", "kind": "Pod", "metadata": {"creationTimestamp": "yesterday"}})
+    with pytest.raises(pb.ProtoError):
+        pb.encode({"apiVersion": "v1", "kind": "Pod", "spec": {"containers": "c"}})
+    with pytest.raises(pb.ProtoError):
+        pb.decode(pb.encode(GPU_POD)[:-5])                     # truncated
+
+
+def test_native_transcoder_is_faster_than_the_message_path():
+    import time
+    pods = {"apiVersion": "v1", "kind": "PodList", "metadata": {"resourceVersion": "1"},
+            "items": [dict(GPU_POD, metadata=dict(GPU_POD["metadata"], name=f"p{i}")) for i in range(200)]}
+    fq = "k8s.io.api.core.v1.PodList"
+    nat = pb.native()
+
+    def best(fn, n=5):
+        t = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            fn()
+            t.append(time.perf_counter() - t0)
+        return min(t)
+    t_py_enc = best(lambda: pb.to_message(pods, fq).SerializeToString())
+    t_nat_enc = best(lambda: nat.mod.encode(pods, nat.index[fq]))
+    raw = nat.mod.encode(pods, nat.index[fq])[0]
+    t_py_dec = best(lambda: pb.from_message(pb.schema().cls(fq).FromString(raw)))
+    t_nat_dec = best(lambda: nat.mod.decode(raw, nat.index[fq]))
+    assert t_nat_enc * 3 < t_py_enc and t_nat_dec * 3 < t_py_dec, (t_nat_enc, t_py_enc, t_nat_dec, t_py_dec)
