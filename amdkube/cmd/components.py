@@ -302,13 +302,25 @@ def etcd(argv):
     if peers and a.name not in peers:
         ap.error(f"--name {a.name} is not in --initial-cluster")
     peer_listen = strip(a.listen_peer_urls.split(",")[0]) if a.listen_peer_urls else peers.get(a.name)
+    coro = serve(a.data_dir, listen, a.cert_file, a.key_file, a.trusted_ca_file, a.snapshot_count,
+                 name=a.name, peers=peers, peer_listen=peer_listen,
+                 heartbeat=a.heartbeat_interval / 1000.0, election=a.election_timeout / 1000.0,
+                 peer_cert=a.peer_cert_file, peer_key=a.peer_key_file, peer_ca=a.peer_trusted_ca_file)
+    prof_path = os.environ.get("AMDKUBE_CPROFILE")
+    pr = None
+    if prof_path:
+        import cProfile
+        pr = cProfile.Profile()
+        pr.enable()
+        signal.signal(signal.SIGTERM, lambda *_: (_ for _ in ()).throw(KeyboardInterrupt()))
     try:
-        asyncio.run(serve(a.data_dir, listen, a.cert_file, a.key_file, a.trusted_ca_file, a.snapshot_count,
-                          name=a.name, peers=peers, peer_listen=peer_listen,
-                          heartbeat=a.heartbeat_interval / 1000.0, election=a.election_timeout / 1000.0,
-                          peer_cert=a.peer_cert_file, peer_key=a.peer_key_file, peer_ca=a.peer_trusted_ca_file))
+        asyncio.run(coro)
     except KeyboardInterrupt:
         pass
+    finally:
+        if pr is not None:
+            pr.disable()
+            pr.dump_stats(f"{prof_path}.{a.name}.{os.getpid()}")
 
 
 def scheduler(argv):

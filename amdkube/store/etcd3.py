@@ -69,7 +69,7 @@ class Etcd3Store(MVCCStore):
         self._creds = (ca, cert, key)
         self._ep = 0
         self._chan = None
-        self._connect(0)
+        self._connect(self._leader_endpoint())
         self._events: queue.Queue = queue.Queue()
         self._stop = threading.Event()
         self._loop = None
@@ -82,6 +82,25 @@ class Etcd3Store(MVCCStore):
         self._thread.start()
 
     # ------------------------------------------------------------------ endpoints
+    def _leader_endpoint(self) -> int:
+        """Index of the endpoint that currently leads its raft group (0 when none answers or
+        the cluster is one member). Any member accepts writes and forwards them, but the
+        forward is a peer round trip and a follower's watch only sees a commit one more
+        AppendEntries later, so writes go to the leader when it is known."""
+        if len(self.endpoints) < 2:
+            return 0
+        for i, ep in enumerate(self.endpoints):
+            ch = _channel(ep, *self._creds)
+            try:
+                st = E.Maintenance.stub(ch).Status(E.StatusRequest(), timeout=1.0)
+                if st.leader and st.leader == st.header.member_id:
+                    return i
+            except grpc.RpcError:
+                continue
+            finally:
+                ch.close()
+        return 0
+
     def _connect(self, i: int):
         """Talk to endpoint i (a member of an etcd cluster; any member forwards to the leader)."""
         if self._chan is not None:
@@ -104,7 +123,8 @@ class Etcd3Store(MVCCStore):
                 if e.code() not in retry or time.monotonic() > deadline:
                     raise
                 log.warning("etcd %s: %s (%s); trying the next endpoint", self.endpoint, method, e.code().name)
-                self._connect(self._ep + 1)
+                lead = self._leader_endpoint()
+                self._connect(lead if lead != self._ep else self._ep + 1)
                 time.sleep(0.1)
 
     # ------------------------------------------------------------------ sync

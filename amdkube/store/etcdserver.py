@@ -40,6 +40,7 @@ from ..grpcdesc.compiler import ProtoModule
 from ..grpcdesc.etcd import (EQUAL, ETCD as E, EV_DELETE, EV_PUT, GREATER, LESS, NOT_EQUAL, T_CREATE, T_MOD,
                              T_VALUE, T_VERSION)
 from .mvcc import PUT, MVCCStore
+from .peerwire import stub as peer_stub
 
 log = logging.getLogger("amdkube.etcd")
 VERSION = "3.1.11-amdkube"
@@ -121,21 +122,17 @@ class EtcdServer:
         self._tasks: list[asyncio.Task] = []
         self.raft = None
         self._raft_args = (data_dir, heartbeat, election)
-        self._fwd: dict[str, grpc.aio.Channel] = {}
+        self._fwd: dict = {}            # member name -> peerwire.PeerChannel
         # (cert file, key file, trusted CA file or None): mutual TLS between members
         self.peer_tls = peer_tls
-        self.peer_server: grpc.aio.Server | None = None
+        self.peer_server = None         # peerwire.PeerServer
         self.peer_port = 0
 
     # ------------------------------------------------------------------ lifecycle
     def _peer_channel(self, target: str):
-        """A channel to another member's peer listener (raft + Peer), under peer TLS if set."""
-        if not self.peer_tls:
-            return grpc.aio.insecure_channel(target, options=_SRV_OPTS)
-        cert, key, ca = self.peer_tls
-        creds = grpc.ssl_channel_credentials(root_certificates=open(ca, "rb").read() if ca else None,
-                                             private_key=open(key, "rb").read(), certificate_chain=open(cert, "rb").read())
-        return grpc.aio.secure_channel(target, creds, options=_SRV_OPTS)
+        """A connection to another member's peer listener (raft + Peer), under peer TLS if set."""
+        from .peerwire import PeerChannel, client_ssl
+        return PeerChannel(target, client_ssl(*self.peer_tls) if self.peer_tls else None)
 
     async def start(self, address: str = "127.0.0.1:0", credentials=None, peer_address: str | None = None):
         """Serve the client API (KV, Watch, Lease, Maintenance) on `address`. With a cluster, a
@@ -147,22 +144,14 @@ class EtcdServer:
         self.port = (self.server.add_secure_port(address, credentials) if credentials is not None
                      else self.server.add_insecure_port(address))
         if len(self.peers) > 1:
-            from .raft import Raft
+            from .raft import RAFT, Raft
             data_dir, hb, el = self._raft_args
             self.raft = Raft(self.name, self.peers, data_dir, self, heartbeat=hb, election=el,
                              compact_every=self.compact_every, channel=self._peer_channel)
-            self.peer_server = grpc.aio.server(options=_SRV_OPTS)
-            self.peer_server.add_generic_rpc_handlers((self.raft.handler(), PEER.Peer.handler(self)))
-            paddr = peer_address or self.peers[self.name]
-            if self.peer_tls:
-                cert, key, ca = self.peer_tls
-                pcreds = grpc.ssl_server_credentials([(open(key, "rb").read(), open(cert, "rb").read())],
-                                                     root_certificates=open(ca, "rb").read() if ca else None,
-                                                     require_client_auth=bool(ca))
-                self.peer_port = self.peer_server.add_secure_port(paddr, pcreds)
-            else:
-                self.peer_port = self.peer_server.add_insecure_port(paddr)
-            await self.peer_server.start()
+            from .peerwire import PeerServer, server_ssl
+            self.peer_server = PeerServer([(RAFT.Raft, self.raft), (PEER.Peer, self)],
+                                          server_ssl(*self.peer_tls) if self.peer_tls else None)
+            self.peer_port = await self.peer_server.start(peer_address or self.peers[self.name])
         await self.server.start()
         if self.raft is not None:
             await self.raft.start()
@@ -180,7 +169,7 @@ class EtcdServer:
         if self.server is not None:
             await self.server.stop(grace)
         if self.peer_server is not None:
-            await self.peer_server.stop(grace)
+            await self.peer_server.stop()
         for w in self.store.all_watchers():
             w.close()
 
@@ -236,7 +225,7 @@ class EtcdServer:
                 hint = e.leader or hint
             leader = self._leader_or_abort(hint)
             try:
-                r = await PEER.Peer.stub(self._leader_channel(leader)).Propose(PEER.ProposeRequest(data=data), timeout=10)
+                r = await peer_stub(PEER.Peer, self._leader_channel(leader)).Propose(PEER.ProposeRequest(data=data), timeout=10)
             except grpc.RpcError as ge:
                 raise _Abort(ge.code(), ge.details()) from None
             if not r.code:
@@ -402,7 +391,7 @@ class EtcdServer:
                     # ReadIndex: the leader vouches for its commit index; serve it once applied here
                     leader = self._leader_or_abort()
                     try:
-                        r = await PEER.Peer.stub(self._leader_channel(leader)).ReadIndex(PEER.ReadIndexRequest(), timeout=10)
+                        r = await peer_stub(PEER.Peer, self._leader_channel(leader)).ReadIndex(PEER.ReadIndexRequest(), timeout=10)
                     except grpc.RpcError as ge:
                         raise _Abort(ge.code(), ge.details()) from None
                     if r.code:
@@ -625,7 +614,7 @@ class EtcdServer:
                 ttl = 0
                 if leader and leader != self.name:
                     try:
-                        r = await PEER.Peer.stub(self._leader_channel(leader)).KeepAlive(
+                        r = await peer_stub(PEER.Peer, self._leader_channel(leader)).KeepAlive(
                             PEER.KeepAliveRequest(id=req.ID), timeout=5)
                         ttl = r.ttl if r.found else 0
                     except grpc.RpcError as ge:

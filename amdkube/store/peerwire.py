@@ -1,0 +1,263 @@
+"""Member-to-member transport of the raft group: length-prefixed protobuf frames over one TCP
+(optionally mutual-TLS) connection per peer, calls multiplexed by id.
+
+etcd does not run raft over gRPC either: its peers talk rafthttp, long-lived HTTP streams of
+raft messages (vendor/github.com/coreos/etcd/rafthttp/stream.go). The reason holds here too:
+Python gRPC aio costs about a millisecond per unary round trip on loopback, which put one
+full millisecond into every commit (leader → follower AppendEntries → ack). This transport
+costs a tenth of that, so a commit is bounded by the follower's fdatasync, not the RPC stack.
+
+Frames: u32 big-endian length, then
+  request   u8 0 | u32 id | u8 len(path) | path "/pkg.Service/Method" | request message
+  response  u8 1 | u32 id | response message
+  error     u8 2 | u32 id | u8 grpc status code | utf-8 message
+The server dispatches each request to its own task (handlers may wait on raft), so replies can
+come back out of order; the client matches them by id. Failures surface as `PeerRpcError`, a
+grpc.RpcError with code()/details(), so raft and the etcd server handle them as before.
+"""
+from __future__ import annotations
+
+import asyncio
+import itertools
+import logging
+import ssl
+import struct
+
+import grpc
+
+log = logging.getLogger("amdkube.peerwire")
+
+REQ, RESP, ERR = 0, 1, 2
+MAX_FRAME = 256 << 20
+
+
+class PeerRpcError(grpc.RpcError):
+    def __init__(self, code: grpc.StatusCode, details: str):
+        super().__init__(f"{code.name}: {details}")
+        self._code, self._details = code, details
+
+    def code(self):
+        return self._code
+
+    def details(self):
+        return self._details
+
+
+_CODES = {c.value[0]: c for c in grpc.StatusCode}
+
+
+def server_ssl(cert: str, key: str, ca: str | None) -> ssl.SSLContext:
+    ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+    ctx.load_cert_chain(cert, key)
+    if ca:
+        ctx.load_verify_locations(ca)
+        ctx.verify_mode = ssl.CERT_REQUIRED          # members only
+    return ctx
+
+
+def client_ssl(cert: str, key: str, ca: str | None) -> ssl.SSLContext:
+    ctx = ssl.create_default_context(ssl.Purpose.SERVER_AUTH, cafile=ca)
+    ctx.load_cert_chain(cert, key)
+    return ctx
+
+
+async def _read_frame(reader: asyncio.StreamReader) -> bytes:
+    (n,) = struct.unpack(">I", await reader.readexactly(4))
+    if n < 5 or n > MAX_FRAME:
+        raise ConnectionError(f"bad peer frame length {n}")
+    return await reader.readexactly(n)
+
+
+class PeerServer:
+    """Serves the methods of `bindings` [(compiler.Service, impl)] to member connections."""
+
+    def __init__(self, bindings, ssl_ctx: ssl.SSLContext | None = None):
+        self.methods = {}
+        for svc, impl in bindings:
+            for name, req, _resp, stream, cstream in svc.methods:
+                fn = getattr(impl, name, None)
+                if fn is not None and not stream and not cstream:
+                    self.methods[f"/{svc.full_name}/{name}"] = (req, fn)
+        self.ssl = ssl_ctx
+        self.server: asyncio.AbstractServer | None = None
+        self._conns: set[asyncio.Task] = set()
+        self.port = 0
+
+    async def start(self, address: str) -> int:
+        host, _, port = address.rpartition(":")
+        self.server = await asyncio.start_server(self._serve, host or "127.0.0.1", int(port), ssl=self.ssl,
+                                                 limit=1 << 20, reuse_address=True)
+        self.port = self.server.sockets[0].getsockname()[1]
+        return self.port
+
+    async def stop(self):
+        if self.server is not None:
+            self.server.close()
+        for t in list(self._conns):
+            t.cancel()
+        for t in list(self._conns):
+            try:
+                await t
+            except (asyncio.CancelledError, Exception):
+                pass
+        if self.server is not None:
+            await self.server.wait_closed()
+
+    async def _serve(self, reader, writer):
+        task = asyncio.current_task()
+        self._conns.add(task)
+        inflight: set[asyncio.Task] = set()
+        try:
+            while True:
+                frame = await _read_frame(reader)
+                kind, cid = frame[0], struct.unpack_from(">I", frame, 1)[0]
+                if kind != REQ:
+                    raise ConnectionError("peer sent a non-request frame")
+                plen = frame[5]
+                path = frame[6:6 + plen].decode()
+                t = asyncio.create_task(self._one(writer, cid, path, frame[6 + plen:]))
+                inflight.add(t)
+                t.add_done_callback(inflight.discard)
+        except (asyncio.IncompleteReadError, ConnectionError, ssl.SSLError, OSError):
+            pass
+        except asyncio.CancelledError:
+            pass
+        finally:
+            for t in list(inflight):
+                t.cancel()
+            writer.close()
+            self._conns.discard(task)
+
+    async def _one(self, writer, cid: int, path: str, payload: bytes):
+        ent = self.methods.get(path)
+        if ent is None:
+            body = bytes([ERR]) + struct.pack(">IB", cid, grpc.StatusCode.UNIMPLEMENTED.value[0]) + f"no method {path}".encode()
+        else:
+            req_cls, fn = ent
+            try:
+                resp = await fn(req_cls.FromString(payload), None)
+                body = bytes([RESP]) + struct.pack(">I", cid) + resp.SerializeToString()
+            except asyncio.CancelledError:
+                raise
+            except Exception as e:   # noqa: BLE001 — the caller gets the error, the connection lives on
+                log.debug("peer method %s failed: %r", path, e)
+                body = bytes([ERR]) + struct.pack(">IB", cid, grpc.StatusCode.UNKNOWN.value[0]) + str(e)[:4000].encode()
+        try:
+            writer.write(struct.pack(">I", len(body)) + body)
+            if len(body) > 1 << 16:
+                await writer.drain()
+        except (ConnectionError, RuntimeError):
+            pass
+
+
+class PeerChannel:
+    """One lazily (re)connected connection to a member's peer listener."""
+
+    def __init__(self, target: str, ssl_ctx: ssl.SSLContext | None = None):
+        self.target = target.split("://", 1)[-1].rstrip("/")
+        self.ssl = ssl_ctx
+        self._reader = self._writer = None
+        self._rtask: asyncio.Task | None = None
+        self._pending: dict[int, asyncio.Future] = {}
+        self._ids = itertools.count(1)
+        self._lock = asyncio.Lock()
+        self.closed = False
+
+    async def _connect(self):
+        async with self._lock:
+            if self._writer is not None:
+                return
+            if self.closed:
+                raise PeerRpcError(grpc.StatusCode.CANCELLED, "channel closed")
+            host, _, port = self.target.rpartition(":")
+            try:
+                self._reader, self._writer = await asyncio.open_connection(
+                    host, int(port), ssl=self.ssl, server_hostname=host if self.ssl else None, limit=1 << 20)
+            except (OSError, ssl.SSLError) as e:
+                raise PeerRpcError(grpc.StatusCode.UNAVAILABLE, f"connect {self.target}: {e}") from None
+            self._rtask = asyncio.create_task(self._read_loop(self._reader, self._writer), name=f"peer-{self.target}")
+
+    async def _read_loop(self, reader, writer):
+        err = PeerRpcError(grpc.StatusCode.UNAVAILABLE, f"connection to {self.target} lost")
+        try:
+            while True:
+                frame = await _read_frame(reader)
+                kind, cid = frame[0], struct.unpack_from(">I", frame, 1)[0]
+                fut = self._pending.pop(cid, None)
+                if fut is None or fut.done():
+                    continue
+                if kind == RESP:
+                    fut.set_result(frame[5:])
+                else:
+                    code = _CODES.get(frame[5], grpc.StatusCode.UNKNOWN)
+                    fut.set_exception(PeerRpcError(code, frame[6:].decode(errors="replace")))
+        except (asyncio.IncompleteReadError, ConnectionError, ssl.SSLError, OSError):
+            pass
+        except asyncio.CancelledError:
+            err = PeerRpcError(grpc.StatusCode.CANCELLED, "channel closed")
+        finally:
+            if self._writer is writer:
+                self._reader = self._writer = None
+            writer.close()
+            for fut in self._pending.values():
+                if not fut.done():
+                    fut.set_exception(err)
+            self._pending.clear()
+
+    async def call(self, path: str, payload: bytes, timeout: float | None = None) -> bytes:
+        if self._writer is None:
+            await self._connect()
+        cid = next(self._ids) & 0xFFFFFFFF
+        fut = asyncio.get_running_loop().create_future()
+        self._pending[cid] = fut
+        p = path.encode()
+        body = struct.pack(">BIB", REQ, cid, len(p)) + p + payload
+        try:
+            self._writer.write(struct.pack(">I", len(body)) + body)
+            if len(body) > 1 << 16:
+                await self._writer.drain()
+        except (ConnectionError, AttributeError, RuntimeError) as e:
+            self._pending.pop(cid, None)
+            raise PeerRpcError(grpc.StatusCode.UNAVAILABLE, f"send to {self.target}: {e}") from None
+        try:
+            return await asyncio.wait_for(fut, timeout)
+        except asyncio.TimeoutError:
+            self._pending.pop(cid, None)
+            raise PeerRpcError(grpc.StatusCode.DEADLINE_EXCEEDED, f"{path} to {self.target} timed out") from None
+
+    async def close(self):
+        self.closed = True
+        if self._rtask is not None:
+            self._rtask.cancel()
+            try:
+                await self._rtask
+            except (asyncio.CancelledError, Exception):
+                pass
+        if self._writer is not None:
+            self._writer.close()
+            self._writer = None
+
+    async def __aenter__(self):
+        return self
+
+    async def __aexit__(self, *exc):
+        await self.close()
+
+
+class _Stub:
+    def __init__(self, svc, channel: PeerChannel):
+        for name, req, resp, stream, cstream in svc.methods:
+            if stream or cstream:
+                continue
+            setattr(self, name, self._method(channel, f"/{svc.full_name}/{name}", resp))
+
+    @staticmethod
+    def _method(channel, path, resp_cls):
+        async def call(request, timeout: float | None = None):
+            return resp_cls.FromString(await channel.call(path, request.SerializeToString(), timeout))
+        return call
+
+
+def stub(svc, channel: PeerChannel) -> _Stub:
+    """`svc` (a grpcdesc.compiler.Service)'s unary methods as coroutines over `channel`."""
+    return _Stub(svc, channel)

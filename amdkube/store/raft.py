@@ -25,9 +25,14 @@ proposals cost about one leader fsync + one round trip + one follower fsync, not
 
 The state machine is the caller's: `apply(index, data) -> result` (deterministic: every
 member applies the same entries in the same order, so every member's store has the same
-revisions), `snapshot() -> bytes`, `restore(bytes)`. Peers talk the `amdkube.raft.Raft` gRPC
-service on the peer listener only (store/etcdserver.py serves it apart from the client API,
-under peer TLS when configured); `channel(target)` makes the peer channels.
+revisions), `snapshot() -> bytes`, `restore(bytes)`. Peers call the `amdkube.raft.Raft` methods
+over the peer transport (store/peerwire.py: framed protobuf over TCP, like etcd's rafthttp
+rather than gRPC) on the peer listener only (store/etcdserver.py serves it apart from the
+client API, under peer TLS when configured); `channel(target)` makes the peer channels.
+
+Commit notification has its own lane per follower (`_notify_commit`), so the empty
+AppendEntries that tells a follower about a new commit index never holds the next batch of
+entries back by a round trip.
 """
 from __future__ import annotations
 
@@ -42,6 +47,7 @@ import time
 import grpc
 
 from ..grpcdesc.compiler import ProtoModule
+from .peerwire import PeerChannel, stub as peer_stub
 
 log = logging.getLogger("amdkube.raft")
 
@@ -72,7 +78,6 @@ message SnapshotResponse { uint64 term = 1; }
 
 FOLLOWER, CANDIDATE, LEADER = "follower", "candidate", "leader"
 MAX_BATCH = 512
-_CHAN_OPTS = [("grpc.max_send_message_length", 256 << 20), ("grpc.max_receive_message_length", 256 << 20)]
 
 
 class NotLeader(Exception):
@@ -86,7 +91,7 @@ class Raft:
                  heartbeat: float = 0.1, election: float = 1.0, compact_every: int = 10_000, fsync: bool = True,
                  channel=None):
         self.name, self.peers, self.sm = name, dict(peers), sm
-        self._channel = channel or (lambda target: grpc.aio.insecure_channel(target, options=_CHAN_OPTS))
+        self._channel = channel or PeerChannel
         self.others = [p for p in sorted(peers) if p != name]
         self.heartbeat, self.election, self.compact_every, self.fsync = heartbeat, election, compact_every, fsync
         self.dir = os.path.join(data_dir, "raft") if data_dir else None
@@ -100,6 +105,7 @@ class Raft:
         self.acked: dict[str, float] = {}
         self._pending: dict[int, tuple[int, asyncio.Future]] = {}
         self._kick: dict[str, asyncio.Event] = {}
+        self._commit_kick: dict[str, asyncio.Event] = {}
         self._tasks: list[asyncio.Task] = []
         self._repl: list[asyncio.Task] = []
         self._stubs: dict[str, object] = {}
@@ -225,7 +231,7 @@ class Raft:
         for p in self.others:
             ch = self._channel(self.peers[p])
             self._chans.append(ch)
-            self._stubs[p] = RAFT.Raft.stub(ch)
+            self._stubs[p] = peer_stub(RAFT.Raft, ch)
         self._last_heard = time.monotonic()
         self._tasks.append(asyncio.create_task(self._ticker(), name="raft-ticker"))
         self._tasks.append(asyncio.create_task(self._flusher(), name="raft-flusher"))
@@ -314,7 +320,10 @@ class Raft:
         self.match_index = {p: 0 for p in self.others}
         self.acked = {}
         self._kick = {p: asyncio.Event() for p in self.others}
+        self._commit_kick = {p: asyncio.Event() for p in self.others}
         self._repl = [asyncio.create_task(self._replicate(p, self.term), name=f"raft-repl-{p}") for p in self.others]
+        self._repl += [asyncio.create_task(self._notify_commit(p, self.term), name=f"raft-commit-{p}")
+                       for p in self.others]
         self._append_local(b"")                       # a no-op of this term lets the commit index move
         if hasattr(self.sm, "on_leader"):
             self.sm.on_leader()
@@ -439,6 +448,35 @@ class Raft:
             except asyncio.TimeoutError:
                 pass
 
+    async def _notify_commit(self, p: str, term: int):
+        """The commit lane: an empty AppendEntries at the follower's known match point carrying
+        the new commit index (etcd's bcastAppend after maybeCommit), on its own call so it never
+        delays the next batch of entries behind a round trip, as one in-flight call per peer
+        would. Followers apply at once, so their watches and ReadIndex reads see the write."""
+        stub, kick = self._stubs[p], self._commit_kick[p]
+        told = 0
+        while self.role == LEADER and self.term == term:
+            await kick.wait()
+            kick.clear()
+            prev = self.match_index.get(p, 0)
+            commit = min(self.commit, prev)
+            if commit <= told or prev < self.snap_index:
+                continue
+            pt = self.term_at(prev)
+            if pt is None:
+                continue
+            try:
+                r = await stub.AppendEntries(RAFT.AppendRequest(term=term, leader=self.name, prev_log_index=prev,
+                                                                prev_log_term=pt, leader_commit=commit),
+                                             timeout=self.election)
+            except grpc.RpcError:
+                continue
+            if r.term > self.term:
+                self._step_down(r.term)
+                return
+            if r.success:
+                told = commit
+
     def _advance_commit(self):
         if self.role != LEADER:
             return
@@ -447,7 +485,7 @@ class Raft:
         if n > self.commit and self.term_at(n) == self.term:
             self.commit = n
             self._apply()
-            for ev in self._kick.values():            # tell followers about the new commit index now
+            for ev in self._commit_kick.values():     # tell followers about the new commit index now
                 ev.set()
 
     # ------------------------------------------------------------------ apply

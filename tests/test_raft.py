@@ -295,12 +295,17 @@ async def test_peer_listener_serves_only_member_traffic_under_mutual_tls(tmp_pat
             with pytest.raises(grpc.RpcError):
                 await PEER.Peer.stub(ch).ReadIndex(PEER.ReadIndexRequest(), timeout=3)
         # a member certificate reaches Peer, but never the client services
+        from amdkube.store.peerwire import PeerChannel, stub
         async with s._peer_channel(peers[leader]) as ch:
-            r = await PEER.Peer.stub(ch).ReadIndex(PEER.ReadIndexRequest(), timeout=5)
+            r = await stub(PEER.Peer, ch).ReadIndex(PEER.ReadIndexRequest(), timeout=5)
             assert r.index >= 1 and not r.code
             with pytest.raises(grpc.RpcError) as ei:
-                await E.KV.stub(ch).Range(E.RangeRequest(key=b"/t/a"), timeout=5)
+                await stub(E.KV, ch).Range(E.RangeRequest(key=b"/t/a"), timeout=5)
             assert ei.value.code() == grpc.StatusCode.UNIMPLEMENTED
+        # the peer transport without TLS cannot talk to the TLS listener either
+        async with PeerChannel(peers[leader]) as ch:
+            with pytest.raises(grpc.RpcError):
+                await stub(PEER.Peer, ch).ReadIndex(PEER.ReadIndexRequest(), timeout=3)
         # writes through a follower still commit over the TLS peer channel
         follower = next(nm for nm in srvs if nm != leader)
         async with grpc.aio.insecure_channel(srvs[follower].address) as ch:
