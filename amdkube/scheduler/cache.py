@@ -177,6 +177,26 @@ class SchedulerCache:
         self.pod_states: dict[str, dict] = {}       # pod key -> pod
         self.assumed: dict[str, float | None] = {}  # pod key -> deadline (None until binding finished)
         self.ttl = ttl
+        # names of nodes whose NodeInfo changed, in order (log[i] has sequence log_base + i): the
+        # scheduler's per-equivalence-class fit index replays it to re-check only those nodes
+        self.log: list[str] = []
+        self.log_base = 0
+        self.prefer_no_schedule = 0  # ready nodes carrying a PreferNoSchedule taint
+
+    def _touch(self, name: str):
+        self.log.append(name)
+        if len(self.log) > 200_000:         # indexes further behind than this rebuild
+            cut = len(self.log) // 2
+            del self.log[:cut]
+            self.log_base += cut
+
+    @property
+    def seq(self) -> int:
+        return self.log_base + len(self.log)
+
+    @staticmethod
+    def _pns(ni) -> bool:
+        return ni.node is not None and any(t.get("effect") == "PreferNoSchedule" for t in ni.taints)
 
     def _track(self, pod, delta):
         if _has_anti_affinity(pod):
@@ -192,7 +212,11 @@ class SchedulerCache:
 
     # ------------------------------------------------------------------ nodes
     def add_node(self, node: dict):
-        self._ni(m.name_of(node)).set_node(node)
+        ni = self._ni(m.name_of(node))
+        self.prefer_no_schedule -= self._pns(ni)
+        ni.set_node(node)
+        self.prefer_no_schedule += self._pns(ni)
+        self._touch(ni.name)
 
     update_node = add_node
 
@@ -201,6 +225,8 @@ class SchedulerCache:
         ni = self.nodes.get(name)
         if ni is None:
             return
+        self.prefer_no_schedule -= self._pns(ni)
+        self._touch(name)
         if ni.pods:
             ni.node = None  # keep pods until they go away (cache.go RemoveNode)
             ni.allocatable = {}
@@ -218,6 +244,7 @@ class SchedulerCache:
             raise KeyError(f"pod {key} is in the cache, so can't be assumed")
         node = (pod.get("spec") or {}).get("nodeName")
         self._ni(node).add_pod(key, pod)
+        self._touch(node)
         self.pod_node[key] = node
         self.pod_states[key] = pod
         self.assumed[key] = None
@@ -235,6 +262,7 @@ class SchedulerCache:
         node = self.pod_node.pop(key, None)
         if node and node in self.nodes:
             self.nodes[node].remove_pod(key)
+            self._touch(node)
         old = self.pod_states.pop(key, None)
         if old is not None:
             self._track(old, -1)
@@ -249,12 +277,14 @@ class SchedulerCache:
             old_node = self.pod_node.get(key)
             if old_node and old_node in self.nodes:
                 self.nodes[old_node].remove_pod(key)
+                self._touch(old_node)
             old = self.pod_states.get(key)
             if old is not None:
                 self._track(old, -1)
         elif key in self.pod_states:
             self.remove_pod(self.pod_states[key])
         self._ni(node).add_pod(key, pod)
+        self._touch(node)
         self.pod_node[key] = node
         self.pod_states[key] = pod
         self._track(pod, 1)
@@ -268,6 +298,7 @@ class SchedulerCache:
         if node and node in self.nodes:
             ni = self.nodes[node]
             ni.remove_pod(key)
+            self._touch(node)
             if ni.node is None and not ni.pods:
                 del self.nodes[node]
         old = self.pod_states.pop(key, None)

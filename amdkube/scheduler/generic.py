@@ -38,6 +38,20 @@ class FitError(Exception):
         super().__init__(f"0/{n_nodes} nodes are available: {msg}." if n_nodes else "no nodes available to schedule pods")
 
 
+class _FitIndex:
+    """One equivalence class's answer for every ready node, kept current by replaying the
+    cache's node-change log: `fit` maps node name -> the node-local priority total, `failed`
+    node name -> predicate failure reasons. A pod of the class costs O(nodes changed since the
+    last pod of the class) instead of O(nodes) (scheduler_perf at 1000 nodes: each bind changes
+    one node)."""
+    __slots__ = ("pos", "fit", "failed")
+
+    def __init__(self):
+        self.pos = -1
+        self.fit: dict[str, float] = {}
+        self.failed: dict[str, list] = {}
+
+
 class Context:
     __slots__ = ("nodes", "any_anti_affinity", "any_affinity", "hard_weight", "services")
 
@@ -63,6 +77,7 @@ class GenericScheduler:
         self.trace_threshold = trace_threshold
         self.ecache: dict[str, dict[str, tuple]] = {}
         self.ecache_hits = 0
+        self.findex: dict[str, _FitIndex] = {}
 
     def configure(self, predicates, priorities, custom_predicates, custom_priorities, extenders, hard_affinity_weight):
         """(Re)build the algorithm from a policy: registered names plus policy-argument functions."""
@@ -73,6 +88,7 @@ class GenericScheduler:
         self.hard_affinity_weight = hard_affinity_weight
         self.custom = bool(custom_predicates or custom_priorities)
         self.ecache = {}
+        self.findex = {}
 
     def _ctx(self, nodes):
         return Context(nodes, self.cache.anti_affinity_pods > 0, getattr(self.cache, "affinity_pods", 0) > 0,
@@ -114,6 +130,67 @@ class GenericScheduler:
             ok, r = extended.fits(pi, ni)
             reasons += r
         return (not reasons), reasons
+
+    # ------------------------------------------------------------ fast path
+    def _uniform_others(self, pi) -> bool:
+        """Whether every node-normalising priority gives all nodes the same score for this pod
+        (so they cannot change the choice and need not run): no controller to spread, no
+        preferred node or pod (anti-)affinity, no PreferNoSchedule taint anywhere."""
+        for name, _fn, _w in self.priorities:
+            if name in LOCAL_PRIORITIES:
+                continue
+            if name == "SelectorSpreadPriority" and pi.owner is None:
+                continue
+            if name == "NodeAffinityPriority" and not pi.preferred_terms:
+                continue
+            if name == "TaintTolerationPriority" and not self.cache.prefer_no_schedule:
+                continue
+            if name == "InterPodAffinityPriority" and not (pi.pref_affinity or pi.pref_anti) and \
+                    not (self.hard_affinity_weight and getattr(self.cache, "affinity_pods", 0)):
+                continue
+            return False
+        return True
+
+    def _eval_node(self, pi, ni, local) -> tuple[bool, list, float]:
+        ok, reasons = self.pod_fits_on_node(pi, ni, None)
+        score = 0.0
+        if ok:
+            for _name, fn, w in local:
+                score += fn(pi, [ni], None)[0] * w
+        return ok, reasons, score
+
+    def _fit_index(self, pi, ek) -> _FitIndex:
+        c = self.cache
+        idx = self.findex.get(ek)
+        local = [(n, fn, w) for n, fn, w in self.priorities if n in LOCAL_PRIORITIES]
+        if idx is None or idx.pos < c.log_base:
+            if len(self.findex) > 4096:
+                self.findex.clear()
+            idx = self.findex[ek] = _FitIndex()
+            for ni in c.ready_nodes():
+                ok, reasons, score = self._eval_node(pi, ni, local)
+                if ok:
+                    idx.fit[ni.name] = score
+                else:
+                    idx.failed[ni.name] = reasons
+        else:
+            changed = dict.fromkeys(c.log[idx.pos - c.log_base:])
+            self.ecache_hits += max(0, len(idx.fit) + len(idx.failed) - len(changed))
+            for name in changed:
+                ni = c.nodes.get(name)
+                if ni is None or ni.node is None:
+                    idx.fit.pop(name, None)
+                    idx.failed.pop(name, None)
+                    continue
+                ok, reasons, score = self._eval_node(pi, ni, local)
+                if ok:
+                    idx.failed.pop(name, None)
+                    idx.fit[name] = score
+                else:
+                    idx.fit.pop(name, None)
+                    idx.failed[name] = reasons
+        idx.pos = c.seq
+        return idx
 
     async def find_nodes_that_fit(self, pi, nodes):
         ctx = self._ctx(nodes) if (pi.pod_affinity or pi.pod_anti_affinity) or self.custom or any(
@@ -206,21 +283,39 @@ class GenericScheduler:
             from .volumes import pod_volumes
             pi.lister, pi.volume_scheduling = self.volumes, self.volume_scheduling
             pi.vol = pod_volumes(pod, self.volumes)
-        nodes = self.cache.ready_nodes()
-        if not nodes:
-            raise FitError(pod, 0, {})
-        trace.step("Computing predicates")
-        fit, failed, ctx = await self.find_nodes_that_fit(pi, nodes)
-        if not fit:
-            raise FitError(pod, len(nodes), failed)
-        trace.step("Prioritizing")
-        scores = None
-        if len(fit) == 1:
-            host = fit[0]
+        ek = None if self.extenders or self.custom else self._equiv_key(pi)
+        if ek is not None and self._uniform_others(pi):
+            # incremental path: the class's fit index, only changed nodes re-checked
+            pi.equiv = ek
+            trace.step("Computing predicates (fit index)")
+            idx = self._fit_index(pi, ek)
+            n_ready = len(idx.fit) + len(idx.failed)
+            if not n_ready:
+                raise FitError(pod, 0, {})
+            if not idx.fit:
+                raise FitError(pod, n_ready, dict(idx.failed))
+            names = list(idx.fit)
+            fit = [self.cache.nodes[n] for n in names]
+            scores = list(idx.fit.values()) if len(fit) > 1 else None
+            n_nodes = n_ready
+            host = fit[0] if scores is None else self.select_host(fit, scores)
         else:
-            scores = await self.prioritize(pi, fit, ctx)
-            trace.step("Selecting host")
-            host = self.select_host(fit, scores)
+            nodes = self.cache.ready_nodes()
+            n_nodes = len(nodes)
+            if not nodes:
+                raise FitError(pod, 0, {})
+            trace.step("Computing predicates")
+            fit, failed, ctx = await self.find_nodes_that_fit(pi, nodes)
+            if not fit:
+                raise FitError(pod, len(nodes), failed)
+            trace.step("Prioritizing")
+            scores = None
+            if len(fit) == 1:
+                host = fit[0]
+            else:
+                scores = await self.prioritize(pi, fit, ctx)
+                trace.step("Selecting host")
+                host = self.select_host(fit, scores)
         binding = extended.allocate(pi, host, self.use_topology) if pi.ext else {}
         if binding is None:
             # the device choice failed on the best host: the next-ranked hosts get their turn
@@ -233,13 +328,13 @@ class GenericScheduler:
                     break
                 failed_alloc[alt.name] = ["device allocation failed"]
             if binding is None:
-                raise FitError(pod, len(nodes), failed_alloc)
+                raise FitError(pod, n_nodes, failed_alloc)
         vol = getattr(pi, "vol", None)
         if vol is not None and vol.delayed and self.volume_scheduling:
             from .volumes import match_delayed
             pairs = match_delayed(vol.delayed, self.volumes, host.labels)
             if pairs is None:
-                raise FitError(pod, len(nodes), {host.name: ["node(s) didn't find available persistent volumes to bind"]})
+                raise FitError(pod, n_nodes, {host.name: ["node(s) didn't find available persistent volumes to bind"]})
             self.volume_binds[m.key_of(pod)] = pairs
         trace.log_if_long(self.trace_threshold)
         return host.name, binding

@@ -270,3 +270,53 @@ def test_allocation_failure_tries_the_next_ranked_host(monkeypatch):
     with pytest.raises(FitError) as e:
         run(g.schedule(pod("q", gpus=2)))
     assert set(e.value.failed) == {"a", "b"}
+
+
+def test_fit_index_decides_like_a_full_scan():
+    """The incremental per-equivalence-class fit index (only nodes changed since the last pod of
+    the class are re-checked) picks the same host, devices and failure as evaluating every node,
+    across binds, node updates (taint, removal) and pod removal."""
+    import asyncio
+    import random
+    rnd = random.Random(7)
+
+    def world():
+        nodes = [node(f"n{i}", gpus=rnd.choice((0, 2, 4, 8)), cpu=str(rnd.choice((2, 4, 8)))) for i in range(24)]
+        return sched(nodes)
+
+    rnd.seed(7)
+    c_fast, g_fast = world()
+    rnd.seed(7)
+    c_slow, g_slow = world()
+    g_slow._uniform_others = lambda pi: False          # always the full scan
+    script = random.Random(11)
+    bound = []
+    for step in range(160):
+        kind = script.random()
+        if kind < 0.07 and bound:                      # a pod goes away
+            p = bound.pop(script.randrange(len(bound)))
+            c_fast.remove_pod(p)
+            c_slow.remove_pod(p)
+            continue
+        if kind < 0.1:                                 # a node is tainted NoSchedule, or comes back
+            n = node(f"n{script.randrange(24)}", gpus=8, cpu="8",
+                     taints=[{"key": "k", "effect": "NoSchedule"}] if script.random() < 0.5 else None)
+            c_fast.update_node(n)
+            c_slow.update_node(n)
+            continue
+        p = pod(f"p{step}", gpus=script.choice((0, 0, 1, 2)), cpu=script.choice(("100m", "500m", "1")))
+        results = []
+        for c, g in ((c_fast, g_fast), (c_slow, g_slow)):
+            try:
+                h, b = asyncio.run(g.schedule(p))
+                results.append((h, b))
+                assigned = {k: v["resources"] for k, v in b.items()} if b else None
+                c.assume_pod(pod(p["metadata"]["name"], gpus=len((b or {}).get("gpus", {}).get("resources", [])),
+                                 cpu=p["spec"]["containers"][0]["resources"]["requests"]["cpu"],
+                                 node_name=h, assigned=assigned))
+            except FitError as e:
+                results.append(("fit-error", str(e)))
+        assert results[0] == results[1], (step, results)
+        if results[0][0] != "fit-error":
+            bound.append(pod(p["metadata"]["name"], node_name=results[0][0]))
+    assert g_fast.findex and g_fast.ecache_hits > 0
