@@ -4,16 +4,23 @@ namespaces and no CAP_SYS_ADMIN, so it cannot pivot_root into the image).
 The program, its interpreter (`#!` line or the ELF PT_INTERP dynamic loader) and its shared
 libraries all come from the image's root filesystem: a dynamic executable is started as
 `<rootfs>/<PT_INTERP> --library-path <rootfs library dirs> <rootfs>/<program> args…`, so the
-image's own loader and libc run it, as they would under a chroot. What this cannot do is move
-absolute paths the program opens at run time (/etc/…, /data) under the image: those still
-resolve on the host, and volumes appear under $AMDKUBE_ROOTFS. Namespace-capable nodes
-(isolation=namespaces|userns) pivot_root into the image instead (native/nsexec.cpp --rootfs).
+image's own loader and libc run it, as they would under a chroot. The paths the program opens
+at run time are moved under the image by the rootview preload (native/rootview.c, armed by
+`rootview_env`): /etc/… is the image's, volumes appear at their mount paths, /tmp is the
+container's own, /dev, /proc and /sys stay the host's, and programs the workload execs run
+through the image's loader too. Images without a glibc loader (musl, static) cannot take a
+glibc preload and keep the host view. Namespace-capable nodes (isolation=namespaces|userns)
+pivot_root into the image instead (native/nsexec.cpp --rootfs).
 """
 from __future__ import annotations
 
 import os
 import struct
 
+ROOTVIEW_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native", "lib",
+                            "libamdkube-rootview.so")
+GLIBC_LOADERS = ("/lib64/ld-linux-x86-64.so.2", "/lib/x86_64-linux-gnu/ld-linux-x86-64.so.2",
+                 "/usr/lib64/ld-linux-x86-64.so.2", "/usr/lib/x86_64-linux-gnu/ld-linux-x86-64.so.2")
 LIB_DIRS = ("lib/x86_64-linux-gnu", "usr/lib/x86_64-linux-gnu", "lib64", "usr/lib64", "lib", "usr/lib",
             "usr/local/lib")
 PT_INTERP = 3
@@ -129,3 +136,26 @@ def rootfs_argv(root: str, argv: list[str], path_env: str, workdir: str = "/", d
         raise RootfsExecError(f"{argv[0]}: the image has no dynamic loader {interp}")
     return [ld, "--library-path", ":".join(library_dirs(root)), prog] + list(argv[1:])
 
+
+
+def rootview_env(root: str, mounts: list[dict], scratch: str, passthrough: tuple[str, ...] = (),
+                 env: dict | None = None) -> dict:
+    """Environment that arms the rootview preload for a container of image root `root`:
+    `mounts` ({container_path, host_path}) keep their paths, `passthrough` host paths (the rocm
+    handler's /opt/rocm) stay visible at the same path, /tmp is `scratch`/tmp. {} when the image
+    has no glibc loader or the preload is not built."""
+    if not os.path.exists(ROOTVIEW_LIB) or not any(os.path.isfile(_inside(root, ld)) for ld in GLIBC_LOADERS):
+        return {}
+    tmp = os.path.join(scratch, "tmp")
+    os.makedirs(tmp, exist_ok=True)
+    os.chmod(tmp, 0o1777)
+    taken = {m["container_path"].rstrip("/") or "/" for m in mounts}
+    table = [f"{m['container_path']}={m['host_path']}" for m in mounts
+             if m["container_path"].startswith("/") and "\n" not in m["container_path"] + m["host_path"]]
+    table += [f"{h}={h}" for h in passthrough if os.path.exists(h) and h not in taken]
+    if "/tmp" not in taken:
+        table.append(f"/tmp={tmp}")
+    pre = (env or {}).get("LD_PRELOAD", "")
+    return {"AMDKUBE_ROOTVIEW": os.path.realpath(root), "AMDKUBE_ROOTVIEW_MOUNTS": "\n".join(table),
+            "AMDKUBE_ROOTVIEW_LIBPATH": ":".join(library_dirs(root)),
+            "LD_PRELOAD": ROOTVIEW_LIB + (":" + pre if pre else "")}

@@ -36,6 +36,11 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+/* bind dlsym/dlvsym to their original version, not glibc 2.34's: the preload must also load into
+ * images whose glibc predates 2.34 */
+__asm__(".symver dlsym,dlsym@GLIBC_2.2.5");
+__asm__(".symver dlvsym,dlvsym@GLIBC_2.2.5");
+
 static int listed(const char* list, const char* path) {
   size_t n = strlen(path);
   const char* p = list;

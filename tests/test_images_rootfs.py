@@ -231,7 +231,7 @@ def test_image_config_precedence_and_gc_through_cri(tmp_path):
                     await asyncio.sleep(0.01)
                 assert st.exit_code == 0, open(st.log_path).read()
                 logs[name] = open(st.log_path).read().split()
-            assert logs["default"][:2] == ["CMD", "from-image"] and logs["default"][2].endswith("/rootfs/srv")
+            assert logs["default"][:2] == ["CMD", "from-image"] and logs["default"][2] == "/srv"   # rootview: image paths
             assert logs["args"][:2] == ["ARGS", "from-pod"]
             assert logs["cmd"] == ["OWN"]
             await cri.stop_pod_sandbox(sid)
@@ -270,3 +270,58 @@ def test_nsexec_pivots_into_the_image(tmp_path):
     assert out[3] == "/etc"
     # the write landed in the container's layer, not in the image
     assert (upper / "upper" / "written").exists() and not os.path.exists(os.path.join(rec["rootfs"], "written"))
+
+
+def test_rootview_makes_the_image_root_the_containers_root(tmp_path):
+    """No mount namespace (isolation=env, as on the unprivileged MI355X node): the rootview
+    preload (native/rootview.c) moves a workload's own file-system calls under the image. /etc
+    is the image's (an absolute symlink in the image resolves inside it), the host's files are
+    gone, volumes sit at their mount paths, /tmp is the container's own, cwd reads as a
+    container path, and programs the workload execs — a `#!` script too — come from the image."""
+    arch = tmp_path / "view.tar"
+    layer = host_closure("/bin/sh", "/bin/cat", "/bin/ls") + [
+        ("etc", None, 0o755, None), ("etc/marker", b"in-image\n", 0o644, None),
+        ("etc/abs-link", None, 0o777, "/etc/marker"), ("srv", None, 0o755, None),
+        ("usr", None, 0o755, None), ("usr/local", None, 0o755, None), ("usr/local/bin", None, 0o755, None),
+        ("usr/local/bin/hello.sh", b"#!/bin/sh\necho hello-from-image-script\n", 0o755, None)]
+    write_docker_archive(str(arch), [layer], {"Entrypoint": ["/bin/sh", "-c"], "Env": ["PATH=/usr/local/bin:/usr/bin:/bin"],
+                                              "WorkingDir": "/srv"}, ["amdkube/view:1"])
+    vol = tmp_path / "vol"
+    vol.mkdir()
+    (vol / "f").write_text("from-volume\n")
+    script = ("cat /etc/marker; cat /etc/abs-link; cat /etc/hostname 2>/dev/null || echo no-host-etc; pwd; "
+              "echo scratch > /tmp/rv-probe; cat /tmp/rv-probe; cat /data/f; hello.sh; echo $(ls /)")
+
+    async def go():
+        base = tempfile.mkdtemp(prefix="rsview", dir="/tmp")
+        shim = await RocShim(os.path.join(base, "s.sock"), os.path.join(base, "state"), hooks_dir=os.path.join(base, "hooks")).start()
+        cri = await CRIClient(os.path.join(base, "s.sock")).connect()
+        try:
+            await cri.pull_image(f"file://{arch}")
+            sc = C.PodSandboxConfig(metadata=C.PodSandboxMetadata(name="p", uid="u2", namespace="default"))
+            sid = await cri.run_pod_sandbox(sc)
+            cfg = C.ContainerConfig(metadata=C.ContainerMetadata(name="v"), image=C.ImageSpec(image="amdkube/view:1"),
+                                    args=[script], mounts=[C.Mount(container_path="/data", host_path=str(vol))])
+            cid = await cri.create_container(sid, cfg, sc)
+            await cri.start_container(cid)
+            for _ in range(500):
+                st, _ = await cri.container_status(cid)
+                if st.state == C.CONTAINER_EXITED:
+                    break
+                await asyncio.sleep(0.01)
+            out = open(st.log_path).read()
+            assert st.exit_code == 0, out
+            lines = out.split("\n")
+            assert lines[:8] == ["in-image", "in-image", "no-host-etc", "/srv", "scratch", "from-volume",
+                                 "hello-from-image-script", lines[7]], lines
+            listing = set(lines[7].split())
+            # the image's directories, not the host's (mount points are not listed: no mount table)
+            assert {"bin", "etc", "srv", "usr"} <= listing and not listing & {"root", "home", "opt", "var"}, listing
+            assert not os.path.exists("/tmp/rv-probe")                 # the container's /tmp, not the host's
+            await cri.stop_pod_sandbox(sid)
+            await cri.remove_pod_sandbox(sid)
+        finally:
+            await cri.close()
+            await shim.stop(kill_pods=True)
+            shutil.rmtree(base, ignore_errors=True)
+    run(go())
