@@ -81,8 +81,7 @@ def _frag(all_free, numa, chosen, parent=None, psize=1):
         qp = sum(c * c for c in pp.values())
         fpar = 1.0 - qp / float(total * min(total, psize))
         return 0.5 * fg + 0.5 * max(0.0, fpar)
-    rs = set(rem)
-    pairs = sum(1 for d in rem if d % 2 == 0 and (d + 1) in rs and numa[d] == numa[d + 1])
+    pairs = sum(c // 2 for c in per.values())     # 2-GPU gangs still placeable inside one NUMA domain
     fp = 1.0 - (2.0 * pairs) / total
     return 0.75 * fg + 0.25 * max(0.0, fp)
 

@@ -103,9 +103,11 @@ inline double fragmentation(const Problem& p, const std::vector<int>& chosen) {
     double frag_parent = 1.0 - qp / (static_cast<double>(total) * std::min(total, p.parent_size));
     return 0.5 * frag_groups + 0.5 * std::max(0.0, frag_parent);
   }
+  // devices left that can still form a 2-GPU gang inside one NUMA domain: on MI355X every GPU
+  // pair is one xGMI hop, so the domain (the CPU socket's PCIe root), not the device index, is
+  // what a future gang should not straddle
   double pairs = 0.0;
-  for (size_t d = 0; d + 1 < n; d += 2)
-    if (rem[d] && rem[d + 1] && p.numa[d] == p.numa[d + 1]) pairs += 1.0;
+  for (int c : per_group) pairs += c / 2;
   double frag_pairs = 1.0 - (2.0 * pairs) / total;
   return 0.75 * frag_groups + 0.25 * std::max(0.0, frag_pairs);
 }
