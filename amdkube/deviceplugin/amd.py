@@ -95,7 +95,16 @@ def resource_groups(gpus: list[dict], strategy: str = "single", base: str = RESO
 
 
 def topology_label(gpus: list[dict], topo: list[list[dict]]) -> str:
+    """The `amd.com/gpu-topology` annotation the scheduler's allocator reads: device IDs, NUMA
+    node, and a link cost per pair. The cost is the driver's link weight; where the driver
+    reports the xGMI link bandwidth of every pair (amdsmi minmax bandwidth), the cost scales
+    inversely with it (15 for the fastest pair), so a slower link costs more than a faster
+    one rather than every xGMI hop costing the same."""
     ids = [device_id(g) for g in gpus]
+    off = [e for i, row in enumerate(topo) for j, e in enumerate(row) if i != j]
+    bws = [int(e.get("max_bw_mbps") or 0) for e in off]
+    by_bw = bool(off) and all(b > 0 for b in bws)
+    best = max(bws) if by_bw else 0
     link = []
     for i, row in enumerate(topo):
         r = []
@@ -103,9 +112,12 @@ def topology_label(gpus: list[dict], topo: list[list[dict]]) -> str:
             if i == j:
                 r.append(0)
                 continue
-            w = e.get("weight")
-            if not w:
-                w = {"xgmi": 15, "pcie": 40}.get(e.get("type"), 60) * max(1, int(e.get("hops") or 1))
+            if by_bw:
+                w = max(1, round(15 * best / int(e["max_bw_mbps"])))
+            else:
+                w = e.get("weight")
+                if not w:
+                    w = {"xgmi": 15, "pcie": 40}.get(e.get("type"), 60) * max(1, int(e.get("hops") or 1))
             r.append(int(w))
         link.append(r)
     out = {"ids": ids, "numa": [int(g.get("numa_node") or 0) for g in gpus], "link": link,

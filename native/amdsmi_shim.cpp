@@ -340,6 +340,12 @@ py::list topology() {
           e["type"] = "unknown";
         }
         if (amdsmi_topo_get_link_weight(g_gpus[i], g_gpus[j], &weight) == AMDSMI_STATUS_SUCCESS) e["weight"] = weight;
+        uint64_t bw_min = 0, bw_max = 0;   // the driver's xGMI link limits (1-hop xGMI pairs only)
+        if (amdsmi_get_minmax_bandwidth_between_processors(g_gpus[i], g_gpus[j], &bw_min, &bw_max) ==
+                AMDSMI_STATUS_SUCCESS && bw_max > 0) {
+          e["min_bw_mbps"] = bw_min;
+          e["max_bw_mbps"] = bw_max;
+        }
         if (amdsmi_is_P2P_accessible(g_gpus[i], g_gpus[j], &p2p) == AMDSMI_STATUS_SUCCESS) e["p2p"] = p2p;
       }
       row.append(e);

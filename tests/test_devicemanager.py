@@ -211,3 +211,22 @@ def test_merge_container_specs_first_wins():
         {"envs": {"A": "2", "B": "3"}, "devices": [{"container_path": "/dev/x", "host_path": "/dev/y"}], "annotations": {"k": "2"}},
     ])
     assert out["envs"] == {"A": "1", "B": "3"} and len(out["devices"]) == 1 and out["annotations"] == {"k": "1"}
+
+
+def test_topology_label_costs_scale_with_reported_xgmi_bandwidth():
+    """Where amd-smi reports every pair's xGMI bandwidth the link cost is inverse to it (the
+    fastest pair costs 15); otherwise the driver's link weight is used as is."""
+    import json
+    from amdkube.deviceplugin.amd import topology_label
+    from amdkube.smi import FakeBackend
+    fb = FakeBackend(n=4)
+    gpus, topo = fb.gpus(), fb.topology()
+    plain = json.loads(topology_label(gpus, topo))
+    for i, row in enumerate(topo):
+        for j, e in enumerate(row):
+            if i != j:
+                e["max_bw_mbps"] = 64000 if {i, j} != {0, 3} else 32000
+    bw = json.loads(topology_label(gpus, topo))
+    assert bw["link"][0][1] == 15 and bw["link"][0][3] == bw["link"][3][0] == 30
+    assert all(bw["link"][i][i] == 0 for i in range(4))
+    assert plain["link"] != bw["link"] and plain["ids"] == bw["ids"]
