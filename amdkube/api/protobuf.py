@@ -45,6 +45,7 @@ import struct
 from datetime import datetime, timezone
 
 from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+from google.protobuf.message import DecodeError
 
 MAGIC = b"k8s\x00"
 MEDIA_TYPE = "application/vnd.kubernetes.protobuf"
@@ -499,7 +500,10 @@ class _Native:
     def _enc_cb(self, mi: int, value):
         fq = self.names[mi]
         msg = schema().cls(fq)()
-        _fill(msg, value, fq)
+        try:
+            _fill(msg, value, fq)
+        except (TypeError, AttributeError) as e:
+            raise ProtoError(f"{fq}: {e}") from None
         if fq == DURATION:
             ok = isinstance(value, str) and format_duration(msg.duration) == value
         elif fq in (RAWEXT, f"{APIEXT}.JSON"):
@@ -510,7 +514,10 @@ class _Native:
 
     def _dec_cb(self, mi: int, data: bytes):
         fq = self.names[mi]
-        return _dump(schema().cls(fq).FromString(data), fq)
+        try:
+            return _dump(schema().cls(fq).FromString(data), fq)
+        except DecodeError as e:
+            raise ProtoError(f"{fq}: {e}") from None
 
 
 @functools.lru_cache(maxsize=1)
@@ -547,11 +554,16 @@ def decode_raw(raw: bytes, fq: str) -> dict:
     nat = native()
     if nat is not None:
         return nat.mod.decode(raw, nat.index[fq])
-    return from_message(schema().cls(fq).FromString(raw))
+    try:
+        return from_message(schema().cls(fq).FromString(raw))
+    except DecodeError as e:
+        raise ProtoError(f"{fq}: {e}") from None
 
 
 def _encode(obj: dict, strict: bool) -> tuple[bytes, bool | None]:
     av, kind = obj.get("apiVersion", ""), obj.get("kind", "")
+    if not isinstance(av, str) or not isinstance(kind, str):
+        raise ProtoError("apiVersion and kind must be strings")
     fq = message_for(av, kind)
     if fq is None:
         raise ProtoError(f"no protobuf schema for {av} {kind}")
@@ -580,7 +592,10 @@ def envelope_parts(data: bytes) -> tuple[str, str, bytes, str]:
         if parts is None:
             raise ProtoError("malformed runtime.Unknown envelope")
         return parts
-    unk = schema().cls(f"{RUNTIME}.Unknown").FromString(data[4:])
+    try:
+        unk = schema().cls(f"{RUNTIME}.Unknown").FromString(data[4:])
+    except DecodeError as e:
+        raise ProtoError(f"malformed runtime.Unknown envelope: {e}") from None
     return unk.typeMeta.apiVersion, unk.typeMeta.kind, unk.raw, unk.contentType
 
 
@@ -603,7 +618,8 @@ def decode(data: bytes) -> dict:
 
 
 def supports(obj: dict) -> bool:
-    return message_for(obj.get("apiVersion", ""), obj.get("kind", "")) is not None
+    av, kind = obj.get("apiVersion", ""), obj.get("kind", "")
+    return isinstance(av, str) and isinstance(kind, str) and message_for(av, kind) is not None
 
 
 def _norm(v):
@@ -731,7 +747,10 @@ def decode_watch_frames(buf: bytes) -> tuple[list[tuple[str, dict]], bytes]:
         n = struct.unpack(">I", buf[:4])[0]
         if len(buf) < 4 + n:
             break
-        ev = schema().cls(f"{META}.WatchEvent").FromString(buf[4:4 + n])
+        try:
+            ev = schema().cls(f"{META}.WatchEvent").FromString(buf[4:4 + n])
+        except DecodeError as e:
+            raise ProtoError(f"malformed watch frame: {e}") from None
         out.append((ev.type, decode(ev.object.raw)))
         buf = buf[4 + n:]
     return out, buf
