@@ -139,7 +139,7 @@ def rootfs_argv(root: str, argv: list[str], path_env: str, workdir: str = "/", d
 
 
 def rootview_env(root: str, mounts: list[dict], scratch: str, passthrough: tuple[str, ...] = (),
-                 env: dict | None = None) -> dict:
+                 env: dict | None = None, workdir: str = "/") -> dict:
     """Environment that arms the rootview preload for a container of image root `root`:
     `mounts` ({container_path, host_path}) keep their paths, `passthrough` host paths (the rocm
     handler's /opt/rocm) stay visible at the same path, /tmp is `scratch`/tmp. {} when the image
@@ -158,4 +158,5 @@ def rootview_env(root: str, mounts: list[dict], scratch: str, passthrough: tuple
     pre = (env or {}).get("LD_PRELOAD", "")
     return {"AMDKUBE_ROOTVIEW": os.path.realpath(root), "AMDKUBE_ROOTVIEW_MOUNTS": "\n".join(table),
             "AMDKUBE_ROOTVIEW_LIBPATH": ":".join(library_dirs(root)),
-            "LD_PRELOAD": ROOTVIEW_LIB + (":" + pre if pre else "")}
+            "LD_PRELOAD": ROOTVIEW_LIB + (":" + pre if pre else ""),
+            "PWD": workdir or "/"}          # shells trust $PWD for their logical cwd
