@@ -373,6 +373,59 @@ int utimensat(int fd, const char* p, const struct timespec* t, int fl) {
   REAL(utimensat, utimensat_fn); char vb[PATH_MAX]; return real_utimensat(fd, p ? VA(fd, p, fl) : p, t, fl);
 }
 
+/* file-system space and type (LLVM's cache pruning, df-style checks) */
+#include <sys/statfs.h>
+#include <sys/statvfs.h>
+typedef int (*statvfs_fn)(const char*, struct statvfs*);
+typedef int (*statvfs64_fn)(const char*, struct statvfs64*);
+typedef int (*statfs_fn)(const char*, struct statfs*);
+typedef int (*statfs64_fn)(const char*, struct statfs64*);
+int statvfs(const char* p, struct statvfs* b) { REAL(statvfs, statvfs_fn); char vb[PATH_MAX]; return real_statvfs(V(p), b); }
+int statvfs64(const char* p, struct statvfs64* b) { REAL(statvfs64, statvfs64_fn); char vb[PATH_MAX]; return real_statvfs64(V(p), b); }
+int statfs(const char* p, struct statfs* b) { REAL(statfs, statfs_fn); char vb[PATH_MAX]; return real_statfs(V(p), b); }
+int statfs64(const char* p, struct statfs64* b) { REAL(statfs64, statfs64_fn); char vb[PATH_MAX]; return real_statfs64(V(p), b); }
+typedef long (*pathconf_fn)(const char*, int);
+long pathconf(const char* p, int name) { REAL(pathconf, pathconf_fn); char vb[PATH_MAX]; return real_pathconf(V(p), name); }
+typedef int (*mknod_fn)(const char*, mode_t, dev_t);
+int mknod(const char* p, mode_t m, dev_t d) { REAL(mknod, mknod_fn); char vb[PATH_MAX]; return real_mknod(VN(p), m, d); }
+typedef int (*mkfifo_fn)(const char*, mode_t);
+int mkfifo(const char* p, mode_t m) { REAL(mkfifo, mkfifo_fn); char vb[PATH_MAX]; return real_mkfifo(VN(p), m); }
+typedef int (*fchmodat_fn)(int, const char*, mode_t, int);
+int fchmodat(int fd, const char* p, mode_t m, int fl) {
+  REAL(fchmodat, fchmodat_fn); char vb[PATH_MAX]; return real_fchmodat(fd, VA(fd, p, fl), m, fl);
+}
+typedef int (*fchownat_fn)(int, const char*, uid_t, gid_t, int);
+int fchownat(int fd, const char* p, uid_t u, gid_t g, int fl) {
+  REAL(fchownat, fchownat_fn); char vb[PATH_MAX];
+  return real_fchownat(fd, (fl & AT_EMPTY_PATH) && !*p ? p : VA(fd, p, fl), u, g, fl);
+}
+#include <utime.h>
+typedef int (*utime_fn)(const char*, const struct utimbuf*);
+int utime(const char* p, const struct utimbuf* t) { REAL(utime, utime_fn); char vb[PATH_MAX]; return real_utime(V(p), t); }
+typedef int (*lutimes_fn)(const char*, const struct timeval*);
+int lutimes(const char* p, const struct timeval* t) { REAL(lutimes, lutimes_fn); char vb[PATH_MAX]; return real_lutimes(VN(p), t); }
+typedef int (*symlinkat_fn)(const char*, int, const char*);
+int symlinkat(const char* target, int fd, const char* p) {
+  REAL(symlinkat, symlinkat_fn); char vb[PATH_MAX]; return real_symlinkat(target, fd, view_at(fd, p, 0, vb, sizeof vb));
+}
+typedef int (*linkat_fn)(int, const char*, int, const char*, int);
+int linkat(int fa, const char* a, int fb, const char* b, int fl) {
+  REAL(linkat, linkat_fn); char va[PATH_MAX], vb[PATH_MAX];
+  return real_linkat(fa, view_at(fa, a, (fl & AT_SYMLINK_FOLLOW) != 0, va, sizeof va), fb, view_at(fb, b, 0, vb, sizeof vb), fl);
+}
+typedef int (*renameat2_fn)(int, const char*, int, const char*, unsigned int);
+int renameat2(int fa, const char* a, int fb, const char* b, unsigned int fl) {
+  REAL(renameat2, renameat2_fn); char va[PATH_MAX], vb[PATH_MAX];
+  return real_renameat2(fa, view_at(fa, a, 0, va, sizeof va), fb, view_at(fb, b, 0, vb, sizeof vb), fl);
+}
+typedef DIR* (*opendir64_fn)(const char*);
+typedef int (*scandir64_fn)(const char*, struct dirent64***, int (*)(const struct dirent64*),
+                            int (*)(const struct dirent64**, const struct dirent64**));
+int scandir64(const char* p, struct dirent64*** l, int (*s)(const struct dirent64*),
+              int (*c)(const struct dirent64**, const struct dirent64**)) {
+  REAL(scandir64, scandir64_fn); char vb[PATH_MAX]; return real_scandir64(V(p), l, s, c);
+}
+
 ssize_t readlink(const char* p, char* out, size_t n) {
   reals();
   char vb[PATH_MAX];
