@@ -142,13 +142,15 @@ def rootview_env(root: str, mounts: list[dict], scratch: str, passthrough: tuple
                  env: dict | None = None, workdir: str = "/") -> dict:
     """Environment that arms the rootview preload for a container of image root `root`:
     `mounts` ({container_path, host_path}) keep their paths, `passthrough` host paths (the rocm
-    handler's /opt/rocm) stay visible at the same path, /tmp is `scratch`/tmp. {} when the image
-    has no glibc loader or the preload is not built."""
+    handler's /opt/rocm) stay visible at the same path, /tmp is `scratch`/tmp, and writes to the
+    image's files land in `scratch`/upper (copied up first), so the shared image stays as pulled.
+    {} when the image has no glibc loader or the preload is not built."""
     if not os.path.exists(ROOTVIEW_LIB) or not any(os.path.isfile(_inside(root, ld)) for ld in GLIBC_LOADERS):
         return {}
-    tmp = os.path.join(scratch, "tmp")
+    tmp, upper = os.path.join(scratch, "tmp"), os.path.join(scratch, "upper")
     os.makedirs(tmp, exist_ok=True)
     os.chmod(tmp, 0o1777)
+    os.makedirs(upper, exist_ok=True)
     taken = {m["container_path"].rstrip("/") or "/" for m in mounts}
     table = [f"{m['container_path']}={m['host_path']}" for m in mounts
              if m["container_path"].startswith("/") and "\n" not in m["container_path"] + m["host_path"]]
@@ -156,7 +158,8 @@ def rootview_env(root: str, mounts: list[dict], scratch: str, passthrough: tuple
     if "/tmp" not in taken:
         table.append(f"/tmp={tmp}")
     pre = (env or {}).get("LD_PRELOAD", "")
-    return {"AMDKUBE_ROOTVIEW": os.path.realpath(root), "AMDKUBE_ROOTVIEW_MOUNTS": "\n".join(table),
+    return {"AMDKUBE_ROOTVIEW": os.path.realpath(root), "AMDKUBE_ROOTVIEW_UPPER": os.path.realpath(upper),
+            "AMDKUBE_ROOTVIEW_MOUNTS": "\n".join(table),
             "AMDKUBE_ROOTVIEW_LIBPATH": ":".join(library_dirs(root)),
             "LD_PRELOAD": ROOTVIEW_LIB + (":" + pre if pre else ""),
             "PWD": workdir or "/"}          # shells trust $PWD for their logical cwd

@@ -54,9 +54,11 @@ def targets(sanitize=False, cpu_only=False):
          ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", *py, *rocm_inc, n("native/amdsmi_shim.cpp"), *rpath,
           "-lamd_smi", "-o", "{out}"]),
         (n(OUT, "lib", "libamdkube-devview.so"), [n("native/devview.c")],
-         ["gcc", "-O2", "-shared", "-fPIC", "-Wall", n("native/devview.c"), "-o", "{out}", "-ldl"]),
+         ["gcc", "-O2", "-shared", "-fPIC", "-Wall", "-fno-delete-null-pointer-checks", n("native/devview.c"), "-o",
+          "{out}", "-ldl"]),
         (n(OUT, "lib", "libamdkube-rootview.so"), [n("native/rootview.c")],
-         ["gcc", "-O2", "-shared", "-fPIC", "-Wall", n("native/rootview.c"), "-o", "{out}", "-ldl"]),
+         ["gcc", "-O2", "-shared", "-fPIC", "-Wall", "-Wno-nonnull-compare", "-Wno-format-truncation",
+          "-fno-delete-null-pointer-checks", n("native/rootview.c"), "-o", "{out}", "-ldl"]),
         (n(BIN, "pause"), [n("native/pause.cpp")],
          ["g++", "-O2", "-std=c++17", n("native/pause.cpp"), "-o", "{out}"]),
         (n(BIN, "amdkube-nsexec"), [n("native/nsexec.cpp"), n("native/seccomp_bpf.h"), n("native/devguard.h"), SYSCALL_TABLE],

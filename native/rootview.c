@@ -35,6 +35,7 @@
 #include <string.h>
 #include <sys/stat.h>
 #include <sys/time.h>
+#include <pthread.h>
 #include <unistd.h>
 
 /* bind dlsym/dlvsym to their original version, not glibc 2.34's: the preload must also load into
@@ -48,6 +49,8 @@ static struct mount_ent g_mounts[MAX_MOUNTS];
 static int g_nmounts;
 static char g_root[PATH_MAX];
 static size_t g_rlen;
+static char g_upper[PATH_MAX];          /* the container's own layer (AMDKUBE_ROOTVIEW_UPPER) */
+static size_t g_ulen;
 static int g_on;
 
 static void add_mount(const char* c, size_t cl, const char* h, size_t hl) {
@@ -67,6 +70,13 @@ __attribute__((constructor)) static void rootview_init(void) {
   while (g_rlen > 1 && r[g_rlen - 1] == '/') g_rlen--;
   memcpy(g_root, r, g_rlen);
   g_root[g_rlen] = 0;
+  const char* u = getenv("AMDKUBE_ROOTVIEW_UPPER");
+  if (u && u[0] == '/' && strlen(u) < PATH_MAX) {
+    g_ulen = strlen(u);
+    while (g_ulen > 1 && u[g_ulen - 1] == '/') g_ulen--;
+    memcpy(g_upper, u, g_ulen);
+    g_upper[g_ulen] = 0;
+  }
   /* volumes: "cpath=hpath" entries separated by newlines */
   const char* m = getenv("AMDKUBE_ROOTVIEW_MOUNTS");
   while (m && *m) {
@@ -93,14 +103,63 @@ static int under(const char* path, const char* prefix, size_t n) {
   return strncmp(path, prefix, n) == 0 && (path[n] == 0 || path[n] == '/');
 }
 
-/* host path of a normalized absolute container path (no symlink resolution) */
-static void map_plain(const char* cpath, char* out, size_t n) {
+typedef ssize_t (*readlink_fn)(const char*, char*, size_t);
+typedef int (*lstat_fn)(const char*, struct stat*);
+typedef char* (*getcwd_fn)(char*, size_t);
+typedef int (*mkdir_fn)(const char*, mode_t);
+typedef int (*symlink_fn)(const char*, const char*);
+typedef int (*open_fn)(const char*, int, ...);
+static readlink_fn real_readlink_p;
+static lstat_fn real_lstat_p;
+static getcwd_fn real_getcwd_p;
+static mkdir_fn real_mkdir_p;
+static symlink_fn real_symlink_p;
+static open_fn real_open_p;
+
+static void reals(void) {
+  if (!real_readlink_p) real_readlink_p = (readlink_fn)dlsym(RTLD_NEXT, "readlink");
+  if (!real_lstat_p) real_lstat_p = (lstat_fn)dlsym(RTLD_NEXT, "lstat");
+  if (!real_getcwd_p) real_getcwd_p = (getcwd_fn)dlsym(RTLD_NEXT, "getcwd");
+  if (!real_mkdir_p) real_mkdir_p = (mkdir_fn)dlsym(RTLD_NEXT, "mkdir");
+  if (!real_symlink_p) real_symlink_p = (symlink_fn)dlsym(RTLD_NEXT, "symlink");
+  if (!real_open_p) real_open_p = (open_fn)dlsym(RTLD_NEXT, "open");
+}
+
+static int exists(const char* host) {
+  struct stat st;
+  reals();
+  return real_lstat_p && real_lstat_p(host, &st) == 0;
+}
+
+/* the mount-table entry of a container path, -1 for the image's own layers */
+static int mount_of(const char* cpath) {
   int best = -1;
   size_t bl = 0;
   for (int i = 0; i < g_nmounts; i++)
     if (g_mounts[i].clen > bl && under(cpath, g_mounts[i].cpath, g_mounts[i].clen)) { best = i; bl = g_mounts[i].clen; }
-  if (best >= 0) snprintf(out, n, "%s%s", g_mounts[best].hpath, cpath + g_mounts[best].clen);
-  else snprintf(out, n, "%s%s", g_root, strcmp(cpath, "/") == 0 ? "" : cpath);
+  return best;
+}
+
+static void lower_of(const char* cpath, char* out, size_t n) {
+  snprintf(out, n, "%s%s", g_root, strcmp(cpath, "/") == 0 ? "" : cpath);
+}
+static void upper_of(const char* cpath, char* out, size_t n) {
+  snprintf(out, n, "%s%s", g_upper, strcmp(cpath, "/") == 0 ? "" : cpath);
+}
+
+/* host path a READ of a normalized absolute container path sees: a volume, else the
+ * container's copy (upper) when it has one, else the image (lower) */
+static void map_plain(const char* cpath, char* out, size_t n) {
+  int m = mount_of(cpath);
+  if (m >= 0) {
+    snprintf(out, n, "%s%s", g_mounts[m].hpath, cpath + g_mounts[m].clen);
+    return;
+  }
+  if (g_ulen) {
+    upper_of(cpath, out, n);
+    if (exists(out)) return;
+  }
+  lower_of(cpath, out, n);
 }
 
 /* container path of a host path (getcwd, /proc/self/fd); the host path itself when outside */
@@ -109,6 +168,10 @@ static void unmap(const char* host, char* out, size_t n) {
   size_t bl = 0;
   for (int i = 0; i < g_nmounts; i++)
     if (g_mounts[i].hlen > bl && under(host, g_mounts[i].hpath, g_mounts[i].hlen)) { best = i; bl = g_mounts[i].hlen; }
+  if (g_ulen && under(host, g_upper, g_ulen) && g_ulen >= bl) {
+    snprintf(out, n, "%s", host[g_ulen] ? host + g_ulen : "/");
+    return;
+  }
   if (best >= 0 && (g_rlen <= bl || !under(host, g_root, g_rlen))) {
     snprintf(out, n, "%s%s", g_mounts[best].cpath, host + g_mounts[best].hlen);
     return;
@@ -120,19 +183,6 @@ static void unmap(const char* host, char* out, size_t n) {
   snprintf(out, n, "%s", host);
 }
 
-typedef ssize_t (*readlink_fn)(const char*, char*, size_t);
-typedef int (*lstat_fn)(const char*, struct stat*);
-typedef char* (*getcwd_fn)(char*, size_t);
-static readlink_fn real_readlink_p;
-static lstat_fn real_lstat_p;
-static getcwd_fn real_getcwd_p;
-
-static void reals(void) {
-  if (!real_readlink_p) real_readlink_p = (readlink_fn)dlsym(RTLD_NEXT, "readlink");
-  if (!real_lstat_p) real_lstat_p = (lstat_fn)dlsym(RTLD_NEXT, "lstat");
-  if (!real_getcwd_p) real_getcwd_p = (getcwd_fn)dlsym(RTLD_NEXT, "getcwd");
-}
-
 /* the container's working directory (container path) */
 static int container_cwd(char* out, size_t n) {
   char host[PATH_MAX];
@@ -142,14 +192,13 @@ static int container_cwd(char* out, size_t n) {
   return 0;
 }
 
-/* Resolve container path `in` (relative to container dir `base`) to a host path, following
- * symlinks inside the view (the last component too when `follow`). Returns 0 or -1/errno. */
-static int resolve(const char* base, const char* in, int follow, char* out, size_t n) {
+/* Resolve container path `in` (relative to container dir `base`) to a normalized container path,
+ * following symlinks inside the view (the last component too when `follow`). 0 or -1/errno. */
+static int resolve_c(const char* base, const char* in, int follow, char* cur, size_t curn) {
   char todo[PATH_MAX * 2];
-  char cur[PATH_MAX];                     /* resolved container path so far */
   if (in[0] == '/') snprintf(todo, sizeof todo, "%s", in);
   else snprintf(todo, sizeof todo, "%s/%s", base, in);
-  strcpy(cur, "");
+  cur[0] = 0;
   reals();
   int hops = 0;
   char* p = todo;
@@ -170,7 +219,7 @@ static int resolve(const char* base, const char* in, int follow, char* out, size
       continue;
     }
     size_t cl = strlen(cur);
-    if (cl + 1 + len >= sizeof cur) { errno = ENAMETOOLONG; return -1; }
+    if (cl + 1 + len >= curn) { errno = ENAMETOOLONG; return -1; }
     cur[cl] = '/';
     memcpy(cur + cl + 1, comp, len + 1);
     int last = (*p == 0) || (strspn(p, "/") == strlen(p));
@@ -191,16 +240,102 @@ static int resolve(const char* base, const char* in, int follow, char* out, size
     snprintf(todo, sizeof todo, "%s", rest);
     p = todo;
   }
-  map_plain(cur[0] ? cur : "/", out, n);
+  if (!cur[0]) strcpy(cur, "/");
   return 0;
 }
 
-/* host path for a path argument; NULL/relative-to-dirfd handled; returns `path` when off */
-static const char* view_at(int dirfd, const char* path, int follow, char* buf, size_t n) {
+static int resolve(const char* base, const char* in, int follow, char* out, size_t n) {
+  char cur[PATH_MAX];
+  if (resolve_c(base, in, follow, cur, sizeof cur) != 0) return -1;
+  map_plain(cur, out, n);
+  return 0;
+}
+
+/* ---- the container's own layer (copy-up): image files are never written in place. A write
+ * goes to <upper>/<path>, the file copied up first; a new name is created there; reads and
+ * listings see the upper entry over the image's. Deleting an image file is refused (EROFS):
+ * there are no whiteouts. */
+static int upper_dirs(const char* cpath) {   /* mkdir -p dirname(cpath) under upper, image modes */
+  char part[PATH_MAX];
+  size_t n = strlen(cpath);
+  for (size_t i = 1; i < n; i++) {
+    if (cpath[i] != '/') continue;
+    memcpy(part, cpath, i);
+    part[i] = 0;
+    char up[PATH_MAX], lo[PATH_MAX];
+    upper_of(part, up, sizeof up);
+    if (exists(up)) continue;
+    lower_of(part, lo, sizeof lo);
+    struct stat st;
+    mode_t mode = (real_lstat_p && real_lstat_p(lo, &st) == 0 && S_ISDIR(st.st_mode)) ? (st.st_mode & 07777) : 0755;
+    if (real_mkdir_p(up, mode | 0700) != 0 && errno != EEXIST) return -1;
+  }
+  return 0;
+}
+
+static int copy_file(const char* from, const char* to, mode_t mode) {
+  int in = real_open_p(from, O_RDONLY | O_CLOEXEC, 0);
+  if (in < 0) return -1;
+  int out = real_open_p(to, O_WRONLY | O_CREAT | O_EXCL | O_CLOEXEC, mode | 0600);
+  if (out < 0) { int e = errno; close(in); errno = e; return errno == EEXIST ? 0 : -1; }
+  char buf[65536];
+  ssize_t k;
+  int rc = 0;
+  while ((k = read(in, buf, sizeof buf)) > 0) {
+    for (ssize_t off = 0; off < k;) {
+      ssize_t w = write(out, buf + off, (size_t)(k - off));
+      if (w <= 0) { rc = -1; break; }
+      off += w;
+    }
+    if (rc) break;
+  }
+  if (k < 0) rc = -1;
+  close(in);
+  if (fchmod(out, mode) != 0) rc = rc ? rc : 0;
+  close(out);
+  return rc;
+}
+
+enum { M_READ = 0, M_WRITE = 1, M_NEW = 2, M_DEL = 3 };
+
+/* host path for container path `cpath` under access `mode`; NULL + errno when refused */
+static const char* place(const char* cpath, int mode, char* out, size_t n) {
+  reals();
+  if (mode == M_READ || !g_ulen || mount_of(cpath) >= 0) {
+    map_plain(cpath, out, n);
+    return out;
+  }
+  char lo[PATH_MAX];
+  upper_of(cpath, out, n);
+  if (exists(out)) return out;
+  lower_of(cpath, lo, sizeof lo);
+  struct stat st;
+  int in_image = real_lstat_p(lo, &st) == 0;
+  if (mode == M_DEL) {
+    if (in_image) { errno = EROFS; return NULL; }
+    return out;                                      /* ENOENT from the call itself */
+  }
+  if (upper_dirs(cpath) != 0) return NULL;
+  if (!in_image || mode == M_NEW) return out;        /* a new name (or replacing one) lives in upper */
+  if (S_ISDIR(st.st_mode)) {
+    if (real_mkdir_p(out, st.st_mode & 07777) != 0 && errno != EEXIST) return NULL;
+  } else if (S_ISLNK(st.st_mode)) {
+    char tgt[PATH_MAX];
+    ssize_t k = real_readlink_p(lo, tgt, sizeof tgt - 1);
+    if (k > 0) { tgt[k] = 0; real_symlink_p(tgt, out); }
+  } else if (S_ISREG(st.st_mode)) {
+    if (copy_file(lo, out, st.st_mode & 07777) != 0) return NULL;
+  }
+  return out;
+}
+
+/* host path for a path argument; NULL/relative-to-dirfd handled; returns `path` when off, NULL
+ * (errno set) when the access is refused */
+static const char* view_mode(int dirfd, const char* path, int follow, int mode, char* buf, size_t n) {
   if (!g_on || !path || !*path) return path;
-  /* a host path inside the image root is already mapped: the loader hands the program its host
-   * path as argv[0], and a program re-opening its own file must find it */
-  if (path[0] == '/' && under(path, g_root, g_rlen)) return path;
+  /* a host path inside the image root (or the container's layer) is already mapped: the loader
+   * hands the program its host path as argv[0], and a program re-opening its own file must find it */
+  if (path[0] == '/' && (under(path, g_root, g_rlen) || (g_ulen && under(path, g_upper, g_ulen)))) return path;
   char base[PATH_MAX];
   if (path[0] != '/') {
     if (dirfd == AT_FDCWD) {
@@ -217,8 +352,13 @@ static const char* view_at(int dirfd, const char* path, int follow, char* buf, s
   } else {
     strcpy(base, "/");
   }
-  if (resolve(base, path, follow, buf, n) != 0) return path;
-  return buf;
+  char cpath[PATH_MAX];
+  if (resolve_c(base, path, follow, cpath, sizeof cpath) != 0) return path;
+  return place(cpath, mode, buf, n);
+}
+
+static const char* view_at(int dirfd, const char* path, int follow, char* buf, size_t n) {
+  return view_mode(dirfd, path, follow, M_READ, buf, n);
 }
 
 #define V(p) view_at(AT_FDCWD, (p), 1, vb, sizeof vb)
@@ -230,53 +370,68 @@ static const char* view_at(int dirfd, const char* path, int follow, char* buf, s
   if (!real_##name) real_##name = (type)dlsym(RTLD_NEXT, #name);                        \
   if (!real_##name) real_##name = (type)dlvsym(RTLD_NEXT, #name, "GLIBC_2.2.5");        \
   if (!real_##name) { errno = ENOSYS; return -1; }
+/* a mutating call: `h` is the host path or NULL (refused, errno set) */
+#define MUT(h, fd, p, follow, mode) const char* h = view_mode((fd), (p), (follow), (mode), vb, sizeof vb); if (!h) return -1
 
 static mode_t mode_arg(int flags, va_list ap) {
   return (flags & O_CREAT) || (flags & O_TMPFILE) == O_TMPFILE ? (mode_t)va_arg(ap, int) : 0;
 }
 static int nofollow(int flags) { return (flags & O_NOFOLLOW) || ((flags & O_CREAT) && (flags & O_EXCL)); }
+static int writes(int flags) { return (flags & (O_WRONLY | O_RDWR | O_CREAT | O_TRUNC | O_APPEND)) != 0; }
 
 /* ------------------------------------------------------------------ opens */
-typedef int (*open_fn)(const char*, int, ...);
 typedef int (*openat_fn)(int, const char*, int, ...);
 typedef int (*open2_fn)(const char*, int);
 typedef int (*openat2_fn)(int, const char*, int);
-#define OPEN_BODY(name, call)                                  \
-  va_list ap; va_start(ap, flags); mode_t m = mode_arg(flags, ap); va_end(ap); \
-  char vb[PATH_MAX]; return call;
+#define OPEN_BODY(fd, call)                                                              \
+  va_list ap; va_start(ap, flags); mode_t m = mode_arg(flags, ap); va_end(ap);           \
+  char vb[PATH_MAX];                                                                     \
+  MUT(h, fd, path, !nofollow(flags), writes(flags) ? M_WRITE : M_READ);                  \
+  return call;
 
-int open(const char* path, int flags, ...) {
-  REAL(open, open_fn);
-  OPEN_BODY(open, real_open(view_at(AT_FDCWD, path, !nofollow(flags), vb, sizeof vb), flags, m))
+int open(const char* path, int flags, ...) { REAL(open, open_fn); OPEN_BODY(AT_FDCWD, real_open(h, flags, m)) }
+int open64(const char* path, int flags, ...) { REAL(open64, open_fn); OPEN_BODY(AT_FDCWD, real_open64(h, flags, m)) }
+int openat(int fd, const char* path, int flags, ...) { REAL(openat, openat_fn); OPEN_BODY(fd, real_openat(fd, h, flags, m)) }
+int openat64(int fd, const char* path, int flags, ...) { REAL(openat64, openat_fn); OPEN_BODY(fd, real_openat64(fd, h, flags, m)) }
+int __open_2(const char* path, int flags) {
+  REAL(__open_2, open2_fn); char vb[PATH_MAX]; MUT(h, AT_FDCWD, path, 1, writes(flags) ? M_WRITE : M_READ);
+  return real___open_2(h, flags);
 }
-int open64(const char* path, int flags, ...) {
-  REAL(open64, open_fn);
-  OPEN_BODY(open64, real_open64(view_at(AT_FDCWD, path, !nofollow(flags), vb, sizeof vb), flags, m))
+int __open64_2(const char* path, int flags) {
+  REAL(__open64_2, open2_fn); char vb[PATH_MAX]; MUT(h, AT_FDCWD, path, 1, writes(flags) ? M_WRITE : M_READ);
+  return real___open64_2(h, flags);
 }
-int openat(int fd, const char* path, int flags, ...) {
-  REAL(openat, openat_fn);
-  OPEN_BODY(openat, real_openat(fd, view_at(fd, path, !nofollow(flags), vb, sizeof vb), flags, m))
-}
-int openat64(int fd, const char* path, int flags, ...) {
-  REAL(openat64, openat_fn);
-  OPEN_BODY(openat64, real_openat64(fd, view_at(fd, path, !nofollow(flags), vb, sizeof vb), flags, m))
-}
-int __open_2(const char* path, int flags) { REAL(__open_2, open2_fn); char vb[PATH_MAX]; return real___open_2(V(path), flags); }
-int __open64_2(const char* path, int flags) { REAL(__open64_2, open2_fn); char vb[PATH_MAX]; return real___open64_2(V(path), flags); }
 int __openat_2(int fd, const char* path, int flags) {
-  REAL(__openat_2, openat2_fn); char vb[PATH_MAX]; return real___openat_2(fd, view_at(fd, path, 1, vb, sizeof vb), flags);
+  REAL(__openat_2, openat2_fn); char vb[PATH_MAX]; MUT(h, fd, path, 1, writes(flags) ? M_WRITE : M_READ);
+  return real___openat_2(fd, h, flags);
 }
 int __openat64_2(int fd, const char* path, int flags) {
-  REAL(__openat64_2, openat2_fn); char vb[PATH_MAX]; return real___openat64_2(fd, view_at(fd, path, 1, vb, sizeof vb), flags);
+  REAL(__openat64_2, openat2_fn); char vb[PATH_MAX]; MUT(h, fd, path, 1, writes(flags) ? M_WRITE : M_READ);
+  return real___openat64_2(fd, h, flags);
 }
-int creat(const char* path, mode_t m) { typedef int (*fn)(const char*, mode_t); REAL(creat, fn); char vb[PATH_MAX]; return real_creat(V(path), m); }
+int creat(const char* path, mode_t m) {
+  typedef int (*fn)(const char*, mode_t); REAL(creat, fn); char vb[PATH_MAX]; MUT(h, AT_FDCWD, path, 1, M_WRITE);
+  return real_creat(h, m);
+}
 
+static int fmode_writes(const char* mode) { return mode && (strchr(mode, 'w') || strchr(mode, 'a') || strchr(mode, '+')); }
 typedef FILE* (*fopen_fn)(const char*, const char*);
-FILE* fopen(const char* path, const char* mode) { REAL(fopen, fopen_fn); char vb[PATH_MAX]; return real_fopen(V(path), mode); }
-FILE* fopen64(const char* path, const char* mode) { REAL(fopen64, fopen_fn); char vb[PATH_MAX]; return real_fopen64(V(path), mode); }
+FILE* fopen(const char* path, const char* mode) {
+  REAL(fopen, fopen_fn); char vb[PATH_MAX];
+  const char* h = view_mode(AT_FDCWD, path, 1, fmode_writes(mode) ? M_WRITE : M_READ, vb, sizeof vb);
+  return h ? real_fopen(h, mode) : NULL;
+}
+FILE* fopen64(const char* path, const char* mode) {
+  REAL(fopen64, fopen_fn); char vb[PATH_MAX];
+  const char* h = view_mode(AT_FDCWD, path, 1, fmode_writes(mode) ? M_WRITE : M_READ, vb, sizeof vb);
+  return h ? real_fopen64(h, mode) : NULL;
+}
 typedef FILE* (*freopen_fn)(const char*, const char*, FILE*);
 FILE* freopen(const char* path, const char* mode, FILE* f) {
-  REAL(freopen, freopen_fn); char vb[PATH_MAX]; return real_freopen(path ? V(path) : NULL, mode, f);
+  REAL(freopen, freopen_fn); char vb[PATH_MAX];
+  const char* h = path ? view_mode(AT_FDCWD, path, 1, fmode_writes(mode) ? M_WRITE : M_READ, vb, sizeof vb) : NULL;
+  if (path && !h) return NULL;
+  return real_freopen(h, mode, f);
 }
 
 /* ------------------------------------------------------------------ stat family */
@@ -323,55 +478,253 @@ int faccessat(int fd, const char* p, int m, int fl) {
   REAL(faccessat, faccessat_fn); char vb[PATH_MAX]; return real_faccessat(fd, VA(fd, p, fl), m, fl);
 }
 
-/* ------------------------------------------------------------------ directories, links, names */
+/* ------------------------------------------------------------------ directory listings
+ * A directory the container has written into exists twice: the image's and the container's
+ * copy. A DIR* opened on it walks the image's entries, then the container's entries the image
+ * does not have. */
+#define MAX_UDIRS 64
+static struct { DIR* d; DIR* up; int phase; char upper[PATH_MAX]; char lower[PATH_MAX]; } g_udirs[MAX_UDIRS];
+static pthread_mutex_t g_udirs_mu = PTHREAD_MUTEX_INITIALIZER;
+
 typedef DIR* (*opendir_fn)(const char*);
-DIR* opendir(const char* p) { REAL(opendir, opendir_fn); char vb[PATH_MAX]; return real_opendir(V(p)); }
-typedef int (*scandir_fn)(const char*, struct dirent***, int (*)(const struct dirent*),
-                          int (*)(const struct dirent**, const struct dirent**));
-int scandir(const char* p, struct dirent*** l, int (*s)(const struct dirent*), int (*c)(const struct dirent**, const struct dirent**)) {
-  REAL(scandir, scandir_fn); char vb[PATH_MAX]; return real_scandir(V(p), l, s, c);
+typedef int (*closedir_fn)(DIR*);
+typedef struct dirent* (*readdir_fn)(DIR*);
+typedef struct dirent64* (*readdir64_fn)(DIR*);
+
+DIR* opendir(const char* p) {
+  REAL(opendir, opendir_fn);
+  if (!g_on || !p || !*p || (p[0] == '/' && (under(p, g_root, g_rlen) || (g_ulen && under(p, g_upper, g_ulen)))))
+    return real_opendir(p);
+  char vb[PATH_MAX];
+  const char* h = V(p);
+  if (!g_ulen || h != vb || !under(h, g_upper, g_ulen)) return real_opendir(h);
+  char lo[PATH_MAX];
+  snprintf(lo, sizeof lo, "%s%s", g_root, h + g_ulen);
+  struct stat st;
+  if (!real_lstat_p || real_lstat_p(lo, &st) != 0 || !S_ISDIR(st.st_mode)) return real_opendir(h);
+  DIR* d = real_opendir(lo);                 /* both layers: the image's listing first */
+  if (!d) return real_opendir(h);
+  pthread_mutex_lock(&g_udirs_mu);
+  int slot = -1;
+  for (int i = 0; i < MAX_UDIRS; i++)
+    if (!g_udirs[i].d) { slot = i; break; }
+  if (slot >= 0) {
+    g_udirs[slot].d = d;
+    g_udirs[slot].up = NULL;
+    g_udirs[slot].phase = 0;
+    snprintf(g_udirs[slot].upper, PATH_MAX, "%s", h);
+    snprintf(g_udirs[slot].lower, PATH_MAX, "%s", lo);
+  }
+  pthread_mutex_unlock(&g_udirs_mu);
+  if (slot < 0) {                            /* table full: the container's listing alone */
+    REAL(closedir, closedir_fn);
+    real_closedir(d);
+    return real_opendir(h);
+  }
+  return d;
 }
+
+int closedir(DIR* d) {
+  REAL(closedir, closedir_fn);
+  pthread_mutex_lock(&g_udirs_mu);
+  for (int i = 0; i < MAX_UDIRS; i++)
+    if (g_udirs[i].d == d) {
+      if (g_udirs[i].up) real_closedir(g_udirs[i].up);
+      g_udirs[i].d = NULL;
+      g_udirs[i].up = NULL;
+    }
+  pthread_mutex_unlock(&g_udirs_mu);
+  return real_closedir(d);
+}
+
+static int udir_slot(DIR* d) {
+  int s = -1;
+  pthread_mutex_lock(&g_udirs_mu);
+  for (int i = 0; i < MAX_UDIRS; i++)
+    if (g_udirs[i].d == d) { s = i; break; }
+  pthread_mutex_unlock(&g_udirs_mu);
+  return s;
+}
+
+static int shadowed(int s, const char* name) {      /* the image already listed this name */
+  if (!strcmp(name, ".") || !strcmp(name, "..")) return 1;
+  char lo[PATH_MAX];
+  snprintf(lo, sizeof lo, "%s/%s", g_udirs[s].lower, name);
+  return exists(lo);
+}
+
+#define READDIR_BODY(real, type)                                                   \
+  int s = udir_slot(d);                                                            \
+  if (s < 0) return real(d);                                                       \
+  if (g_udirs[s].phase == 0) {                                                     \
+    type* e = real(d);                                                             \
+    if (e) return e;                                                               \
+    g_udirs[s].phase = 1;                                                          \
+    REAL(opendir, opendir_fn);                                                     \
+    g_udirs[s].up = real_opendir(g_udirs[s].upper);                                \
+  }                                                                                \
+  if (!g_udirs[s].up) return NULL;                                                 \
+  type* e;                                                                         \
+  while ((e = real(g_udirs[s].up)) && shadowed(s, e->d_name)) {                    \
+  }                                                                                \
+  return e;
+
+struct dirent* readdir(DIR* d) { REAL(readdir, readdir_fn); READDIR_BODY(real_readdir, struct dirent) }
+struct dirent64* readdir64(DIR* d) { REAL(readdir64, readdir64_fn); READDIR_BODY(real_readdir64, struct dirent64) }
+
+/* glibc's scandir opens the directory internally (the preload would not see it): a scandir
+ * over this preload's opendir/readdir, same contract */
+#define SCANDIR_BODY(type, rd)                                                          \
+  DIR* d = opendir(p);                                                                  \
+  if (!d) return -1;                                                                    \
+  size_t cap = 16, n = 0;                                                               \
+  type** v = malloc(cap * sizeof *v);                                                   \
+  if (!v) { closedir(d); return -1; }                                                   \
+  type* e;                                                                              \
+  while ((e = rd(d))) {                                                                 \
+    if (sel && !sel(e)) continue;                                                       \
+    if (n == cap) {                                                                     \
+      type** nv = realloc(v, (cap *= 2) * sizeof *v);                                   \
+      if (!nv) { for (size_t i = 0; i < n; i++) free(v[i]); free(v); closedir(d); errno = ENOMEM; return -1; } \
+      v = nv;                                                                           \
+    }                                                                                   \
+    size_t sz = e->d_reclen > sizeof(type) ? e->d_reclen : sizeof(type);                \
+    v[n] = malloc(sz);                                                                  \
+    if (!v[n]) break;                                                                   \
+    memcpy(v[n++], e, e->d_reclen < sz ? e->d_reclen : sz);                             \
+  }                                                                                     \
+  closedir(d);                                                                          \
+  if (cmp) qsort(v, n, sizeof *v, (int (*)(const void*, const void*))cmp);              \
+  *list = v;                                                                            \
+  return (int)n;
+
+int scandir(const char* p, struct dirent*** list, int (*sel)(const struct dirent*),
+            int (*cmp)(const struct dirent**, const struct dirent**)) {
+  SCANDIR_BODY(struct dirent, readdir)
+}
+int scandir64(const char* p, struct dirent64*** list, int (*sel)(const struct dirent64*),
+              int (*cmp)(const struct dirent64**, const struct dirent64**)) {
+  SCANDIR_BODY(struct dirent64, readdir64)
+}
+
+/* ------------------------------------------------------------------ names and metadata */
 typedef int (*chdir_fn)(const char*);
 int chdir(const char* p) { REAL(chdir, chdir_fn); char vb[PATH_MAX]; return real_chdir(V(p)); }
-typedef int (*mkdir_fn)(const char*, mode_t);
 typedef int (*mkdirat_fn)(int, const char*, mode_t);
-int mkdir(const char* p, mode_t m) { REAL(mkdir, mkdir_fn); char vb[PATH_MAX]; return real_mkdir(VN(p), m); }
-int mkdirat(int fd, const char* p, mode_t m) { REAL(mkdirat, mkdirat_fn); char vb[PATH_MAX]; return real_mkdirat(fd, view_at(fd, p, 0, vb, sizeof vb), m); }
+static int taken(int fd, const char* p) {           /* a new name that the view already shows */
+  char vb[PATH_MAX];
+  const char* h = view_at(fd, p, 0, vb, sizeof vb);
+  return h && exists(h);
+}
+int mkdir(const char* p, mode_t m) {
+  REAL(mkdir, mkdir_fn); char vb[PATH_MAX];
+  if (g_on && taken(AT_FDCWD, p)) { errno = EEXIST; return -1; }
+  MUT(h, AT_FDCWD, p, 0, M_NEW); return real_mkdir(h, m);
+}
+int mkdirat(int fd, const char* p, mode_t m) {
+  REAL(mkdirat, mkdirat_fn); char vb[PATH_MAX];
+  if (g_on && taken(fd, p)) { errno = EEXIST; return -1; }
+  MUT(h, fd, p, 0, M_NEW); return real_mkdirat(fd, h, m);
+}
 typedef int (*path1_fn)(const char*);
-int rmdir(const char* p) { REAL(rmdir, path1_fn); char vb[PATH_MAX]; return real_rmdir(VN(p)); }
-int unlink(const char* p) { REAL(unlink, path1_fn); char vb[PATH_MAX]; return real_unlink(VN(p)); }
+int rmdir(const char* p) { REAL(rmdir, path1_fn); char vb[PATH_MAX]; MUT(h, AT_FDCWD, p, 0, M_DEL); return real_rmdir(h); }
+int unlink(const char* p) { REAL(unlink, path1_fn); char vb[PATH_MAX]; MUT(h, AT_FDCWD, p, 0, M_DEL); return real_unlink(h); }
 typedef int (*unlinkat_fn)(int, const char*, int);
-int unlinkat(int fd, const char* p, int fl) { REAL(unlinkat, unlinkat_fn); char vb[PATH_MAX]; return real_unlinkat(fd, view_at(fd, p, 0, vb, sizeof vb), fl); }
+int unlinkat(int fd, const char* p, int fl) {
+  REAL(unlinkat, unlinkat_fn); char vb[PATH_MAX]; MUT(h, fd, p, 0, M_DEL); return real_unlinkat(fd, h, fl);
+}
 typedef int (*path2_fn)(const char*, const char*);
 int rename(const char* a, const char* b) {
   REAL(rename, path2_fn); char va[PATH_MAX], vb[PATH_MAX];
-  return real_rename(view_at(AT_FDCWD, a, 0, va, sizeof va), view_at(AT_FDCWD, b, 0, vb, sizeof vb));
+  const char* ha = view_mode(AT_FDCWD, a, 0, M_WRITE, va, sizeof va);
+  if (!ha) return -1;
+  MUT(hb, AT_FDCWD, b, 0, M_NEW);
+  return real_rename(ha, hb);
 }
 typedef int (*renameat_fn)(int, const char*, int, const char*);
 int renameat(int fa, const char* a, int fb, const char* b) {
   REAL(renameat, renameat_fn); char va[PATH_MAX], vb[PATH_MAX];
-  return real_renameat(fa, view_at(fa, a, 0, va, sizeof va), fb, view_at(fb, b, 0, vb, sizeof vb));
+  const char* ha = view_mode(fa, a, 0, M_WRITE, va, sizeof va);
+  if (!ha) return -1;
+  MUT(hb, fb, b, 0, M_NEW);
+  return real_renameat(fa, ha, fb, hb);
+}
+typedef int (*renameat2_fn)(int, const char*, int, const char*, unsigned int);
+int renameat2(int fa, const char* a, int fb, const char* b, unsigned int fl) {
+  REAL(renameat2, renameat2_fn); char va[PATH_MAX], vb[PATH_MAX];
+  const char* ha = view_mode(fa, a, 0, M_WRITE, va, sizeof va);
+  if (!ha) return -1;
+  MUT(hb, fb, b, 0, M_NEW);
+  return real_renameat2(fa, ha, fb, hb, fl);
 }
 int link(const char* a, const char* b) {
   REAL(link, path2_fn); char va[PATH_MAX], vb[PATH_MAX];
-  return real_link(view_at(AT_FDCWD, a, 0, va, sizeof va), view_at(AT_FDCWD, b, 0, vb, sizeof vb));
+  const char* ha = view_at(AT_FDCWD, a, 0, va, sizeof va);
+  MUT(hb, AT_FDCWD, b, 0, M_NEW);
+  return real_link(ha, hb);
+}
+typedef int (*linkat_fn)(int, const char*, int, const char*, int);
+int linkat(int fa, const char* a, int fb, const char* b, int fl) {
+  REAL(linkat, linkat_fn); char va[PATH_MAX], vb[PATH_MAX];
+  const char* ha = view_at(fa, a, (fl & AT_SYMLINK_FOLLOW) != 0, va, sizeof va);
+  MUT(hb, fb, b, 0, M_NEW);
+  return real_linkat(fa, ha, fb, hb, fl);
 }
 int symlink(const char* target, const char* b) {   /* the link text stays a container path */
-  REAL(symlink, path2_fn); char vb[PATH_MAX]; return real_symlink(target, VN(b));
+  REAL(symlink, path2_fn); char vb[PATH_MAX];
+  if (g_on && taken(AT_FDCWD, b)) { errno = EEXIST; return -1; }
+  MUT(h, AT_FDCWD, b, 0, M_NEW); return real_symlink(target, h);
+}
+typedef int (*symlinkat_fn)(const char*, int, const char*);
+int symlinkat(const char* target, int fd, const char* p) {
+  REAL(symlinkat, symlinkat_fn); char vb[PATH_MAX];
+  if (g_on && taken(fd, p)) { errno = EEXIST; return -1; }
+  MUT(h, fd, p, 0, M_NEW); return real_symlinkat(target, fd, h);
+}
+typedef int (*mknod_fn)(const char*, mode_t, dev_t);
+int mknod(const char* p, mode_t m, dev_t d) {
+  REAL(mknod, mknod_fn); char vb[PATH_MAX];
+  if (g_on && taken(AT_FDCWD, p)) { errno = EEXIST; return -1; }
+  MUT(h, AT_FDCWD, p, 0, M_NEW); return real_mknod(h, m, d);
+}
+typedef int (*mkfifo_fn)(const char*, mode_t);
+int mkfifo(const char* p, mode_t m) {
+  REAL(mkfifo, mkfifo_fn); char vb[PATH_MAX];
+  if (g_on && taken(AT_FDCWD, p)) { errno = EEXIST; return -1; }
+  MUT(h, AT_FDCWD, p, 0, M_NEW); return real_mkfifo(h, m);
 }
 typedef int (*chmod_fn)(const char*, mode_t);
-int chmod(const char* p, mode_t m) { REAL(chmod, chmod_fn); char vb[PATH_MAX]; return real_chmod(V(p), m); }
-typedef int (*chown_fn)(const char*, uid_t, gid_t);
-int chown(const char* p, uid_t u, gid_t g) { REAL(chown, chown_fn); char vb[PATH_MAX]; return real_chown(V(p), u, g); }
-int lchown(const char* p, uid_t u, gid_t g) { REAL(lchown, chown_fn); char vb[PATH_MAX]; return real_lchown(VN(p), u, g); }
-typedef int (*truncate_fn)(const char*, off_t);
-int truncate(const char* p, off_t l) { REAL(truncate, truncate_fn); char vb[PATH_MAX]; return real_truncate(V(p), l); }
-typedef int (*utimes_fn)(const char*, const struct timeval*);
-int utimes(const char* p, const struct timeval* t) { REAL(utimes, utimes_fn); char vb[PATH_MAX]; return real_utimes(V(p), t); }
-typedef int (*utimensat_fn)(int, const char*, const struct timespec*, int);
-int utimensat(int fd, const char* p, const struct timespec* t, int fl) {
-  REAL(utimensat, utimensat_fn); char vb[PATH_MAX]; return real_utimensat(fd, p ? VA(fd, p, fl) : p, t, fl);
+int chmod(const char* p, mode_t m) { REAL(chmod, chmod_fn); char vb[PATH_MAX]; MUT(h, AT_FDCWD, p, 1, M_WRITE); return real_chmod(h, m); }
+typedef int (*fchmodat_fn)(int, const char*, mode_t, int);
+int fchmodat(int fd, const char* p, mode_t m, int fl) {
+  REAL(fchmodat, fchmodat_fn); char vb[PATH_MAX]; MUT(h, fd, p, !(fl & AT_SYMLINK_NOFOLLOW), M_WRITE);
+  return real_fchmodat(fd, h, m, fl);
 }
+typedef int (*chown_fn)(const char*, uid_t, gid_t);
+int chown(const char* p, uid_t u, gid_t g) { REAL(chown, chown_fn); char vb[PATH_MAX]; MUT(h, AT_FDCWD, p, 1, M_WRITE); return real_chown(h, u, g); }
+int lchown(const char* p, uid_t u, gid_t g) { REAL(lchown, chown_fn); char vb[PATH_MAX]; MUT(h, AT_FDCWD, p, 0, M_WRITE); return real_lchown(h, u, g); }
+typedef int (*fchownat_fn)(int, const char*, uid_t, gid_t, int);
+int fchownat(int fd, const char* p, uid_t u, gid_t g, int fl) {
+  REAL(fchownat, fchownat_fn); char vb[PATH_MAX];
+  if ((fl & AT_EMPTY_PATH) && p && !*p) return real_fchownat(fd, p, u, g, fl);
+  MUT(h, fd, p, !(fl & AT_SYMLINK_NOFOLLOW), M_WRITE);
+  return real_fchownat(fd, h, u, g, fl);
+}
+typedef int (*truncate_fn)(const char*, off_t);
+int truncate(const char* p, off_t l) { REAL(truncate, truncate_fn); char vb[PATH_MAX]; MUT(h, AT_FDCWD, p, 1, M_WRITE); return real_truncate(h, l); }
+typedef int (*utimes_fn)(const char*, const struct timeval*);
+int utimes(const char* p, const struct timeval t[2]) { REAL(utimes, utimes_fn); char vb[PATH_MAX]; MUT(h, AT_FDCWD, p, 1, M_WRITE); return real_utimes(h, t); }
+int lutimes(const char* p, const struct timeval t[2]) { REAL(lutimes, utimes_fn); char vb[PATH_MAX]; MUT(h, AT_FDCWD, p, 0, M_WRITE); return real_lutimes(h, t); }
+typedef int (*utimensat_fn)(int, const char*, const struct timespec*, int);
+int utimensat(int fd, const char* p, const struct timespec t[2], int fl) {
+  REAL(utimensat, utimensat_fn); char vb[PATH_MAX];
+  if (!p) return real_utimensat(fd, p, t, fl);
+  MUT(h, fd, p, !(fl & AT_SYMLINK_NOFOLLOW), M_WRITE);
+  return real_utimensat(fd, h, t, fl);
+}
+#include <utime.h>
+typedef int (*utime_fn)(const char*, const struct utimbuf*);
+int utime(const char* p, const struct utimbuf* t) { REAL(utime, utime_fn); char vb[PATH_MAX]; MUT(h, AT_FDCWD, p, 1, M_WRITE); return real_utime(h, t); }
 
 /* file-system space and type (LLVM's cache pruning, df-style checks) */
 #include <sys/statfs.h>
@@ -386,45 +739,6 @@ int statfs(const char* p, struct statfs* b) { REAL(statfs, statfs_fn); char vb[P
 int statfs64(const char* p, struct statfs64* b) { REAL(statfs64, statfs64_fn); char vb[PATH_MAX]; return real_statfs64(V(p), b); }
 typedef long (*pathconf_fn)(const char*, int);
 long pathconf(const char* p, int name) { REAL(pathconf, pathconf_fn); char vb[PATH_MAX]; return real_pathconf(V(p), name); }
-typedef int (*mknod_fn)(const char*, mode_t, dev_t);
-int mknod(const char* p, mode_t m, dev_t d) { REAL(mknod, mknod_fn); char vb[PATH_MAX]; return real_mknod(VN(p), m, d); }
-typedef int (*mkfifo_fn)(const char*, mode_t);
-int mkfifo(const char* p, mode_t m) { REAL(mkfifo, mkfifo_fn); char vb[PATH_MAX]; return real_mkfifo(VN(p), m); }
-typedef int (*fchmodat_fn)(int, const char*, mode_t, int);
-int fchmodat(int fd, const char* p, mode_t m, int fl) {
-  REAL(fchmodat, fchmodat_fn); char vb[PATH_MAX]; return real_fchmodat(fd, VA(fd, p, fl), m, fl);
-}
-typedef int (*fchownat_fn)(int, const char*, uid_t, gid_t, int);
-int fchownat(int fd, const char* p, uid_t u, gid_t g, int fl) {
-  REAL(fchownat, fchownat_fn); char vb[PATH_MAX];
-  return real_fchownat(fd, (fl & AT_EMPTY_PATH) && !*p ? p : VA(fd, p, fl), u, g, fl);
-}
-#include <utime.h>
-typedef int (*utime_fn)(const char*, const struct utimbuf*);
-int utime(const char* p, const struct utimbuf* t) { REAL(utime, utime_fn); char vb[PATH_MAX]; return real_utime(V(p), t); }
-typedef int (*lutimes_fn)(const char*, const struct timeval*);
-int lutimes(const char* p, const struct timeval* t) { REAL(lutimes, lutimes_fn); char vb[PATH_MAX]; return real_lutimes(VN(p), t); }
-typedef int (*symlinkat_fn)(const char*, int, const char*);
-int symlinkat(const char* target, int fd, const char* p) {
-  REAL(symlinkat, symlinkat_fn); char vb[PATH_MAX]; return real_symlinkat(target, fd, view_at(fd, p, 0, vb, sizeof vb));
-}
-typedef int (*linkat_fn)(int, const char*, int, const char*, int);
-int linkat(int fa, const char* a, int fb, const char* b, int fl) {
-  REAL(linkat, linkat_fn); char va[PATH_MAX], vb[PATH_MAX];
-  return real_linkat(fa, view_at(fa, a, (fl & AT_SYMLINK_FOLLOW) != 0, va, sizeof va), fb, view_at(fb, b, 0, vb, sizeof vb), fl);
-}
-typedef int (*renameat2_fn)(int, const char*, int, const char*, unsigned int);
-int renameat2(int fa, const char* a, int fb, const char* b, unsigned int fl) {
-  REAL(renameat2, renameat2_fn); char va[PATH_MAX], vb[PATH_MAX];
-  return real_renameat2(fa, view_at(fa, a, 0, va, sizeof va), fb, view_at(fb, b, 0, vb, sizeof vb), fl);
-}
-typedef DIR* (*opendir64_fn)(const char*);
-typedef int (*scandir64_fn)(const char*, struct dirent64***, int (*)(const struct dirent64*),
-                            int (*)(const struct dirent64**, const struct dirent64**));
-int scandir64(const char* p, struct dirent64*** l, int (*s)(const struct dirent64*),
-              int (*c)(const struct dirent64**, const struct dirent64**)) {
-  REAL(scandir64, scandir64_fn); char vb[PATH_MAX]; return real_scandir64(V(p), l, s, c);
-}
 
 ssize_t readlink(const char* p, char* out, size_t n) {
   reals();

@@ -290,7 +290,8 @@ def test_rootview_makes_the_image_root_the_containers_root(tmp_path):
     vol.mkdir()
     (vol / "f").write_text("from-volume\n")
     script = ("cat /etc/marker; cat /etc/abs-link; cat /etc/hostname 2>/dev/null || echo no-host-etc; pwd; "
-              "echo scratch > /tmp/rv-probe; cat /tmp/rv-probe; cat /data/f; hello.sh; echo $(ls /)")
+              "echo scratch > /tmp/rv-probe; cat /tmp/rv-probe; cat /data/f; hello.sh; echo $(ls /); "
+              "echo changed > /etc/marker; cat /etc/marker; echo new > /etc/added; echo $(ls /etc)")
 
     async def go():
         base = tempfile.mkdtemp(prefix="rsview", dir="/tmp")
@@ -317,6 +318,12 @@ def test_rootview_makes_the_image_root_the_containers_root(tmp_path):
             listing = set(lines[7].split())
             # the image's directories, not the host's (mount points are not listed: no mount table)
             assert {"bin", "etc", "srv", "usr"} <= listing and not listing & {"root", "home", "opt", "var"}, listing
+            # writes land in the container's own layer: the view sees them, the image does not change
+            assert lines[8] == "changed" and sorted(lines[9].split()) == ["abs-link", "added", "marker"], lines[8:10]
+            rootfs = os.path.join(base, "state", "images")
+            marker = [os.path.join(dp, f) for dp, _, fs in os.walk(rootfs) for f in fs if f == "marker"]
+            assert marker and all(open(x).read() == "in-image\n" for x in marker), marker
+            assert not [f for _, _, fs in os.walk(rootfs) for f in fs if f == "added"]
             assert not os.path.exists("/tmp/rv-probe")                 # the container's /tmp, not the host's
             await cri.stop_pod_sandbox(sid)
             await cri.remove_pod_sandbox(sid)
