@@ -315,6 +315,18 @@ static const char* place(const char* cpath, int mode, char* out, size_t n) {
     if (in_image) { errno = EROFS; return NULL; }
     return out;                                      /* ENOENT from the call itself */
   }
+  {                                                  /* the parent must exist in the view */
+    char parent[PATH_MAX], ph[PATH_MAX];
+    snprintf(parent, sizeof parent, "%s", cpath);
+    char* sl = strrchr(parent, '/');
+    if (sl == parent) sl[1] = 0; else if (sl) *sl = 0;
+    map_plain(parent, ph, sizeof ph);
+    struct stat pst;
+    typedef int (*stat_fn_t)(const char*, struct stat*);
+    static stat_fn_t real_stat_p;
+    if (!real_stat_p) real_stat_p = (stat_fn_t)dlsym(RTLD_NEXT, "stat");
+    if (!real_stat_p || real_stat_p(ph, &pst) != 0 || !S_ISDIR(pst.st_mode)) { errno = ENOENT; return NULL; }
+  }
   if (upper_dirs(cpath) != 0) return NULL;
   if (!in_image || mode == M_NEW) return out;        /* a new name (or replacing one) lives in upper */
   if (S_ISDIR(st.st_mode)) {
