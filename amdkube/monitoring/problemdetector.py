@@ -196,6 +196,7 @@ class LogWatcher:
         self._f = None
         self._proc: subprocess.Popen | None = None
         self._partial = ""
+        self._head = b""           # the file's first bytes, to notice a copytruncate rotation
         self._parser = FileLogParser(cfg.plugin_config) if cfg.plugin == "filelog" else None
 
     def open(self) -> bool:
@@ -238,7 +239,10 @@ class LogWatcher:
                         if e is not None:
                             out.append(e)
         elif self._f is not None:
+            self._follow_rotation()
             chunk = self._f.read()
+            if len(self._head) < 64:
+                self._head = os.pread(self._f.fileno(), 64, 0)
             if chunk:
                 text = self._partial + chunk
                 lines = text.split("\n")
@@ -264,6 +268,30 @@ class LogWatcher:
                 msg = rest.split("kernel: ", 1)[1] if "kernel: " in rest else rest
                 out.append(LogEntry(t, msg))
         return out
+
+    def _follow_rotation(self):
+        """A log rotated away (new inode at the path) is reopened from its start; one truncated in
+        place is read again from offset 0 (what `tail -F` does for NPD's filelog plugin)."""
+        try:
+            st = os.stat(self.cfg.log_path)
+            cur = os.fstat(self._f.fileno())
+        except OSError:
+            return
+        if (st.st_ino, st.st_dev) != (cur.st_ino, cur.st_dev):
+            rest = self._f.read()                     # whatever the old file still had
+            if rest:
+                self._partial += rest
+            self._f.close()
+            self._f = open(self.cfg.log_path, "r", errors="replace")
+            self._head = b""
+            return
+        # truncated in place: shorter than what was read, or its first bytes are not the ones seen
+        head = os.pread(self._f.fileno(), 64, 0)
+        pos = self._f.tell()
+        if st.st_size < pos or (self._head and head[:len(self._head)] != self._head):
+            self._f.seek(0)
+            self._partial = ""
+            self._head = b""
 
     def close(self):
         if self._fd is not None:

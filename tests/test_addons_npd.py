@@ -290,3 +290,23 @@ def test_deploy_addons_parse_and_carry_the_mode_label():
     assert ("DaemonSet", "node-problem-detector") in kinds and ("DaemonSet", "amd-gpu-device-plugin") in kinds
     for doc in docs:
         assert m.labels_of(doc).get("addonmanager.kubernetes.io/mode") in ("Reconcile", "EnsureExists"), doc["metadata"]
+
+
+def test_filelog_follows_rotation_and_truncation(tmp_path):
+    from amdkube.monitoring.problemdetector import LogWatcher
+    log_file = tmp_path / "kern.log"
+    log_file.write_text("")
+    cfg = MonitorConfig.parse(_ref_config(str(log_file), "1h"))
+    w = LogWatcher(cfg, boot=0)
+    assert w.open()
+    now = time.time()
+    _inject(str(log_file), now, "first", 1)
+    assert [e.message for e in w.read()] == ["first"]
+    os.rename(log_file, tmp_path / "kern.log.1")            # logrotate: move away, new file
+    log_file.write_text("")
+    _inject(str(log_file), now, "after rotation", 1)
+    assert [e.message for e in w.read()] == ["after rotation"]
+    log_file.write_text("")                                   # copytruncate
+    _inject(str(log_file), now, "after truncation", 1)
+    assert [e.message for e in w.read()] == ["after truncation"]
+    w.close()
