@@ -156,13 +156,123 @@ class NamespaceExists(Plugin):
             raise m.not_found("namespaces", a.namespace)
 
 
+MIRROR_POD_ANNOTATION = "kubernetes.io/config.mirror"
+SA_TOKEN_MOUNT_PATH = "/var/run/secrets/kubernetes.io/serviceaccount"
+ENFORCE_MOUNTABLE_SECRETS = "kubernetes.io/enforce-mountable-secrets"
+
+
+def _forbid(pod: dict, msg: str) -> m.StatusError:
+    """admission.NewForbidden: `pods "<name>" is forbidden: <why>`."""
+    name = m.name_of(pod) or (pod.get("metadata") or {}).get("generateName", "")
+    return m.forbidden(f'pods "{name}" is forbidden: {msg}')
+
+
 class ServiceAccount(Plugin):
+    """plugin/pkg/admission/serviceaccount/admission.go: default `serviceAccountName`, refuse a
+    pod naming a ServiceAccount that does not exist, mount the account's API token secret at
+    /var/run/secrets/kubernetes.io/serviceaccount in every container (unless the pod or the
+    account sets automountServiceAccountToken: false, or a container already mounts that path),
+    copy the account's imagePullSecrets into a pod without any, enforce mountable secrets when
+    the account asks for it, and keep mirror pods free of accounts and secrets.
+
+    Deliberate difference: the reference also refuses a pod while the "default" account or its
+    token does not exist yet (RequireAPIToken, "retry after the token is automatically
+    created"); here a missing default account or token mounts nothing, so clusters run without
+    the ServiceAccount/token controllers (the benches, the node e2e setups) still start pods.
+    `require_api_token=True` restores the reference's refusal."""
     name = "ServiceAccount"
     operations = (CREATE,)
 
+    def __init__(self, require_api_token: bool = False):
+        self.require_api_token = require_api_token
+
+    @staticmethod
+    def _secret_names(pod: dict) -> set[str]:
+        spec = pod.get("spec") or {}
+        out = {v["secret"].get("secretName") for v in spec.get("volumes") or [] if (v.get("secret") or {}).get("secretName")}
+        for c in (spec.get("containers") or []) + (spec.get("initContainers") or []):
+            for e in c.get("env") or []:
+                ref = ((e.get("valueFrom") or {}).get("secretKeyRef") or {}).get("name")
+                if ref:
+                    out.add(ref)
+            for ef in c.get("envFrom") or []:
+                ref = (ef.get("secretRef") or {}).get("name")
+                if ref:
+                    out.add(ref)
+        return out
+
+    def _token_secret(self, sa: dict, ctx) -> str:
+        """The first API token secret the account references (getReferencedServiceAccountToken)."""
+        ns, name = m.namespace_of(sa), m.name_of(sa)
+        for ref in sa.get("secrets") or []:
+            sec = ctx.get_object("secrets", ns, ref.get("name", ""))
+            if sec and sec.get("type") == "kubernetes.io/service-account-token" and \
+                    m.annotations_of(sec).get("kubernetes.io/service-account.name") == name:
+                return m.name_of(sec)
+        return ""
+
     def admit(self, a, ctx):
-        if a.resource == "pods" and not a.subresource:
-            a.obj.setdefault("spec", {}).setdefault("serviceAccountName", "default")
+        if a.resource != "pods" or a.subresource:
+            return
+        pod = a.obj
+        spec = pod.setdefault("spec", {})
+        if MIRROR_POD_ANNOTATION in m.annotations_of(pod):
+            if spec.get("serviceAccountName") or spec.get("serviceAccount"):
+                raise _forbid(pod, "a mirror pod may not reference service accounts")
+            if self._secret_names(pod):
+                raise _forbid(pod, "a mirror pod may not reference secrets")
+            return
+        sa_name = spec.get("serviceAccountName") or spec.get("serviceAccount") or "default"
+        spec["serviceAccountName"] = sa_name
+        sa = ctx.get_object("serviceaccounts", a.namespace, sa_name)
+        if sa is None:
+            if sa_name != "default" or self.require_api_token:
+                raise _forbid(pod, f"error looking up service account {a.namespace}/{sa_name}: "
+                                                          f"serviceaccount \"{sa_name}\" not found")
+            return
+        automount = spec.get("automountServiceAccountToken")
+        if automount is None:
+            automount = sa.get("automountServiceAccountToken")
+        if automount is not False:
+            self._mount_token(sa, pod, ctx)
+        if not spec.get("imagePullSecrets") and sa.get("imagePullSecrets"):
+            spec["imagePullSecrets"] = [dict(x) for x in sa["imagePullSecrets"]]
+        if m.annotations_of(sa).get(ENFORCE_MOUNTABLE_SECRETS) == "true":
+            allowed = {r.get("name") for r in sa.get("secrets") or []}
+            for sname in sorted(self._secret_names(pod)):
+                if sname not in allowed:
+                    raise _forbid(pod, f'volume with secret.secretName="{sname}" is not allowed '
+                                                              f"because service account {sa_name} does not reference that secret")
+            pulls = {r.get("name") for r in sa.get("imagePullSecrets") or []}
+            for i, ref in enumerate(spec.get("imagePullSecrets") or []):
+                if ref.get("name") not in pulls:
+                    raise _forbid(pod, f'imagePullSecrets[{i}].name="{ref.get("name")}" is not '
+                                                              f"allowed because service account {sa_name} does not "
+                                                              f"reference that imagePullSecret")
+
+    def _mount_token(self, sa: dict, pod: dict, ctx):
+        token = self._token_secret(sa, ctx)
+        if not token:
+            if self.require_api_token:
+                raise m.StatusError(504, "ServerTimeout", f"No API token found for service account "
+                                                          f"\"{m.name_of(sa)}\", retry after the token is "
+                                                          f"automatically created and added to the service account")
+            return
+        spec = pod["spec"]
+        volumes = spec.setdefault("volumes", [])
+        vol_name = next((v["name"] for v in volumes if (v.get("secret") or {}).get("secretName") == token), "")
+        has_volume = bool(vol_name)
+        if not vol_name:
+            names = {v.get("name") for v in volumes}
+            vol_name = token if token not in names else f"{token}-{uuid.uuid4().hex[:5]}"
+        need = False
+        for c in (spec.get("initContainers") or []) + (spec.get("containers") or []):
+            if any(vm.get("mountPath") == SA_TOKEN_MOUNT_PATH for vm in c.get("volumeMounts") or []):
+                continue
+            c.setdefault("volumeMounts", []).append({"name": vol_name, "readOnly": True, "mountPath": SA_TOKEN_MOUNT_PATH})
+            need = True
+        if need and not has_volume:
+            volumes.append({"name": vol_name, "secret": {"secretName": token}})
 
 
 class DefaultTolerationSeconds(Plugin):

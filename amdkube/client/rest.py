@@ -25,6 +25,13 @@ class ChaosError(ConnectionResetError):
     pass
 
 
+IN_CLUSTER_TOKEN_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+
+class ConfigError(RuntimeError):
+    pass
+
+
 class TokenBucket:
     def __init__(self, qps: float, burst: int):
         self.qps, self.burst = qps, max(1, burst)
@@ -147,6 +154,28 @@ class Client:
         c = load_kubeconfig(path, context)
         return cls(c["server"], token=c.get("token"), ca_file=c.get("ca_file"), ca_data=c.get("ca_data"),
                    cert_file=c.get("cert_file"), key_file=c.get("key_file"), insecure=c.get("insecure", False), **kw)
+
+    @classmethod
+    def in_cluster(cls, **kw) -> "Client":
+        """rest.InClusterConfig (staging/src/k8s.io/client-go/rest/config.go): the apiserver from
+        KUBERNETES_SERVICE_HOST/PORT, the pod's ServiceAccount token and the cluster CA from the
+        token volume the ServiceAccount admission plugin mounts. A container without a mount
+        namespace finds the volume under $AMDKUBE_ROOTFS. ConfigError when not in a pod."""
+        host, port = os.environ.get("KUBERNETES_SERVICE_HOST"), os.environ.get("KUBERNETES_SERVICE_PORT")
+        if not host or not port:
+            raise ConfigError("unable to load in-cluster configuration, KUBERNETES_SERVICE_HOST and "
+                              "KUBERNETES_SERVICE_PORT must be defined")
+        base = IN_CLUSTER_TOKEN_DIR
+        if not os.path.exists(os.path.join(base, "token")) and os.environ.get("AMDKUBE_ROOTFS"):
+            base = os.path.join(os.environ["AMDKUBE_ROOTFS"], base.lstrip("/"))
+        try:
+            with open(os.path.join(base, "token")) as f:
+                token = f.read().strip()
+        except OSError as e:
+            raise ConfigError(f"no in-cluster ServiceAccount token: {e}") from None
+        ca = os.path.join(base, "ca.crt")
+        h = f"[{host}]" if ":" in host else host
+        return cls(f"https://{h}:{port}", token=token, ca_file=ca if os.path.exists(ca) else None, **kw)
 
     async def discover(self) -> int:
         """Learn resources the local scheme does not know (custom resources) from the server's

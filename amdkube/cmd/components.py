@@ -24,10 +24,19 @@ from ..utils import log as klog
 
 
 def _client(a, **kw):
-    """--kubeconfig wins over --server (plus the kubelet's --token from TLS bootstrap)."""
+    """--kubeconfig wins over --server (plus the kubelet's --token from TLS bootstrap); a component
+    left at the default --server inside a pod uses the in-cluster config (ServiceAccount token,
+    cluster CA, KUBERNETES_SERVICE_HOST), as client-go's BuildConfigFromFlags falls back to it."""
     from ..client import Client
     if getattr(a, "kubeconfig", None):
         return Client.from_kubeconfig(a.kubeconfig, **kw)
+    if a.server in ("http://127.0.0.1:8080", "", None) and os.environ.get("KUBERNETES_SERVICE_HOST") \
+            and not getattr(a, "token", None):
+        from ..client.rest import ConfigError
+        try:
+            return Client.in_cluster(**kw)
+        except ConfigError as e:
+            logging.getLogger("amdkube").warning("in-cluster config unavailable (%s); using --server %s", e, a.server)
     return Client(a.server, token=getattr(a, "token", None), **kw)
 
 
