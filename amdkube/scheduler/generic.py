@@ -38,6 +38,9 @@ class FitError(Exception):
         super().__init__(f"0/{n_nodes} nodes are available: {msg}." if n_nodes else "no nodes available to schedule pods")
 
 
+FIT_INDEX_CLASSES = 256    # equivalence classes kept (least recently used dropped first)
+
+
 class _FitIndex:
     """One equivalence class's answer for every ready node, kept current by replaying the
     cache's node-change log: `fit` maps node name -> the node-local priority total, `failed`
@@ -161,12 +164,12 @@ class GenericScheduler:
 
     def _fit_index(self, pi, ek) -> _FitIndex:
         c = self.cache
-        idx = self.findex.get(ek)
+        idx = self.findex.pop(ek, None)          # re-inserted below: the dict's order is recency (LRU)
         local = [(n, fn, w) for n, fn, w in self.priorities if n in LOCAL_PRIORITIES]
         if idx is None or idx.pos < c.log_base:
-            if len(self.findex) > 4096:
-                self.findex.clear()
-            idx = self.findex[ek] = _FitIndex()
+            while len(self.findex) >= FIT_INDEX_CLASSES:  # each class holds an entry per node
+                self.findex.pop(next(iter(self.findex)))
+            idx = _FitIndex()
             for ni in c.ready_nodes():
                 ok, reasons, score = self._eval_node(pi, ni, local)
                 if ok:
@@ -190,6 +193,7 @@ class GenericScheduler:
                     idx.fit.pop(name, None)
                     idx.failed[name] = reasons
         idx.pos = c.seq
+        self.findex[ek] = idx
         return idx
 
     async def find_nodes_that_fit(self, pi, nodes):
