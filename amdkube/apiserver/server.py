@@ -26,7 +26,7 @@ from .. import GIT_VERSION
 from ..api import meta as m
 from ..api.scheme import SCHEME
 from ..store import MVCCStore, PUT
-from ..utils import profiling
+from ..utils import greenbridge, profiling
 from ..utils.metrics import CONTENT_TYPE, MICRO_BUCKETS, Counter, Histogram, new_registry, render
 from ..store.storage import kv_json, kv_proto
 from . import admission as adm
@@ -120,6 +120,7 @@ class APIServer:
                  proxy_client_key_file: str | None = None, options: dict | None = None):
         """`options`: the rest of kube-apiserver's flags (see _apply_options)."""
         self.store = store or MVCCStore()
+        self._bridged = bool(getattr(self.store, "async_writes", False))
         self.opts = dict(options or {})
         # --kubelet-https / --kubelet-client-certificate / --kubelet-client-key /
         # --kubelet-certificate-authority: how the apiserver reaches kubelets (logs, exec, proxy)
@@ -747,6 +748,14 @@ class APIServer:
                 out.headers[k] = v
         return out
 
+    async def _w(self, fn, *args, **kwargs):
+        """A registry write. Over a remote store it runs bridged (utils/greenbridge.py): where
+        the store would wait on etcd, this request yields the loop to the others, and writes
+        issued meanwhile are committed together."""
+        if self._bridged:
+            return await greenbridge.run_sync(fn, *args, **kwargs)
+        return fn(*args, **kwargs)
+
     async def _handle(self, request, rs, ns, name, sub, user, q, as_stored=False, served=None):
         meth = request.method
         ri = rs.ri
@@ -784,9 +793,9 @@ class APIServer:
             body = await self._body(request)
             if name and sub == "binding" and ri.plural == "pods":
                 body.setdefault("metadata", {}).setdefault("name", name)
-                return _resp(self.registry.bind(ns, body, user), 201)
+                return _resp(await self._w(self.registry.bind, ns, body, user), 201)
             if name and sub == "eviction" and ri.plural == "pods":
-                self.registry.evict(ns, name, body, user)
+                await self._w(self.registry.evict, ns, name, body, user)
                 return _resp(m.success_status(), 201)
             if name and sub == "rollback" and ri.plural == "deployments":
                 # extensions/v1beta1 DeploymentRollback (registry/extensions/deployment/storage:
@@ -794,13 +803,13 @@ class APIServer:
                 patch = {"spec": {"rollbackTo": body.get("rollbackTo") or {"revision": 0}}}
                 if body.get("updatedAnnotations"):
                     patch["metadata"] = {"annotations": body["updatedAnnotations"]}
-                rs.update(ns, name, None, user=user, patch=json.dumps(patch).encode(),
-                          content_type="application/merge-patch+json")
+                await self._w(rs.update, ns, name, None, user=user, patch=json.dumps(patch).encode(),
+                              content_type="application/merge-patch+json")
                 return _resp(m.success_status({"name": name, "kind": "deployments"}), 201)
             if ri.plural in ("subjectaccessreviews", "selfsubjectaccessreviews", "localsubjectaccessreviews", "tokenreviews"):
                 return _resp(await self._review(ri.plural, body, user, ns), 201)
             if ri.plural == "pods" and sub == "" and name is None and body.get("kind") == "Binding":
-                return _resp(self.registry.bind(ns, body, user), 201)
+                return _resp(await self._w(self.registry.bind, ns, body, user), 201)
             if name:
                 raise m.method_not_allowed("POST on a named resource")
             dry = q.get("dryRun") == "All"
@@ -812,7 +821,7 @@ class APIServer:
             if val:
                 final = rs.create(ns, json.loads(json.dumps(body)), user, dry_run=True)
                 await self.webhooks.validate(val, "CREATE", ri, sub, ns, None, final, None, user)
-            obj = rs.create(ns, body, user, dry_run=dry)
+            obj = await self._w(rs.create, ns, body, user, dry_run=dry)
             if not dry and q.get("includeUninitialized") not in ("true", "1") and _uninitialized(obj):
                 obj = await self._wait_initialized(rs, ns, m.name_of(obj))
             return _resp(obj, 201)
@@ -821,7 +830,7 @@ class APIServer:
                 raise m.method_not_allowed("PUT on a collection")
             body = await self._body(request)
             if sub == "scale":
-                return _resp(self._set_scale(rs, ns, name, body, user))
+                return _resp(await self._w(self._set_scale, rs, ns, name, body, user))
             subr = "status" if sub in ("status", "approval") else ""
             if sub == "finalize" and ri.plural == "namespaces":
                 subr = "finalize"
@@ -835,7 +844,7 @@ class APIServer:
                     body = await self.webhooks.mutate(mut, "UPDATE", ri, sub, ns, name, body, old, user)
                 if val:
                     await self.webhooks.validate(val, "UPDATE", ri, sub, ns, name, body, old, user)
-            obj, created = rs.update(ns, name, body, subresource=subr, user=user)
+            obj, created = await self._w(rs.update, ns, name, body, subresource=subr, user=user)
             return _resp(obj, 201 if created else 200)
         if meth == "PATCH":
             if not name:
@@ -845,7 +854,7 @@ class APIServer:
             if sub == "scale":
                 from .registry import apply_patch
                 cur = _to_scale(rs.get(ns, name))
-                return _resp(self._set_scale(rs, ns, name, apply_patch(cur, data, ct), user))
+                return _resp(await self._w(self._set_scale, rs, ns, name, apply_patch(cur, data, ct), user))
             mut, val = self.webhooks.active("UPDATE", ri, sub, ns)
             if mut or val:
                 # webhooks see the patched object; it is then written as an update conditioned on the
@@ -858,10 +867,10 @@ class APIServer:
                 if val:
                     await self.webhooks.validate(val, "UPDATE", ri, sub, ns, name, new, old, user)
                 new.setdefault("metadata", {})["resourceVersion"] = (old.get("metadata") or {}).get("resourceVersion")
-                obj, _ = rs.update(ns, name, new, subresource=sub if sub == "status" else "", user=user)
+                obj, _ = await self._w(rs.update, ns, name, new, subresource=sub if sub == "status" else "", user=user)
                 return _resp(obj)
-            obj, _ = rs.update(ns, name, None, subresource=sub if sub == "status" else "", user=user, patch=data,
-                               content_type=ct, served=served)
+            obj, _ = await self._w(rs.update, ns, name, None, subresource=sub if sub == "status" else "", user=user,
+                                   patch=data, content_type=ct, served=served)
             return _resp(obj)
         if meth == "DELETE":
             opts = {}
@@ -882,13 +891,13 @@ class APIServer:
             if val and name:
                 await self.webhooks.validate(val, "DELETE", ri, sub, ns, name, None, rs.get(ns, name), user)
             if name:
-                obj, now = rs.delete(ns, name, grace=grace, precond_uid=uid, user=user, propagation=prop)
+                obj, now = await self._w(rs.delete, ns, name, grace=grace, precond_uid=uid, user=user, propagation=prop)
                 return _resp(obj if not now or ri.plural == "pods" else m.success_status(
                     {"name": name, "kind": ri.plural, "uid": m.uid_of(obj)}))
             items, _, _ = rs.list(ns, q.get("labelSelector"), q.get("fieldSelector"))
             for it in items:
                 try:
-                    rs.delete(m.namespace_of(it), m.name_of(it), grace=grace, user=user, propagation=prop)
+                    await self._w(rs.delete, m.namespace_of(it), m.name_of(it), grace=grace, user=user, propagation=prop)
                 except m.StatusError as e:
                     if not m.is_not_found(e):
                         raise

@@ -295,6 +295,9 @@ def etcd(argv):
     ap.add_argument("--peer-trusted-ca-file", default=None, help="require peer certificates signed by this CA")
     ap.add_argument("--heartbeat-interval", type=int, default=100, help="ms")
     ap.add_argument("--election-timeout", type=int, default=1000, help="ms")
+    ap.add_argument("--client-wire-port", type=int, default=0,
+                    help="port of the framed client lane next to the gRPC API (0: any free port, -1: off); "
+                         "advertised to clients in Status metadata")
     ap.add_argument("-v", type=int, default=0)
     for flag in ("--advertise-client-urls", "--initial-advertise-peer-urls", "--initial-cluster-state",
                  "--initial-cluster-token", "--client-cert-auth", "--quota-backend-bytes"):
@@ -314,7 +317,8 @@ def etcd(argv):
     coro = serve(a.data_dir, listen, a.cert_file, a.key_file, a.trusted_ca_file, a.snapshot_count,
                  name=a.name, peers=peers, peer_listen=peer_listen,
                  heartbeat=a.heartbeat_interval / 1000.0, election=a.election_timeout / 1000.0,
-                 peer_cert=a.peer_cert_file, peer_key=a.peer_key_file, peer_ca=a.peer_trusted_ca_file)
+                 peer_cert=a.peer_cert_file, peer_key=a.peer_key_file, peer_ca=a.peer_trusted_ca_file,
+                 wire_port=a.client_wire_port)
     prof_path = os.environ.get("AMDKUBE_CPROFILE")
     pr = None
     if prof_path:

@@ -20,6 +20,12 @@ apiserver committed in between, so the commit revision is the replica's + 1 (the
 never stores the version and sets it from mod_revision on decode instead — etcd3/store.go
 versioner). Writes from several apiservers are linearised through the fence; a fence-only
 conflict catches the replica up and retries.
+
+Transport: gRPC, the etcd v3 API, works against any etcd. An `amdkube etcd` member also
+advertises its client wire lane (store/peerwire.py framing, in the Status initial metadata);
+when it does, the KV calls and the watch go over that lane instead (a blocking socket per
+call site, no gRPC stack on either end), which takes most of a Txn's cost out of every
+apiserver write.
 """
 from __future__ import annotations
 
@@ -31,13 +37,29 @@ import time
 import grpc
 
 from ..grpcdesc.etcd import ETCD as E, EQUAL, EV_PUT, GREATER, T_MOD, T_VERSION
-from .etcdserver import prefix_end
+from .etcdserver import WIRE_METADATA, prefix_end
+from .peerwire import PeerChannel, SyncChannel, client_ssl
+from ..utils import greenbridge
 from .mvcc import DELETE, KV, PUT, CASFailed, Event, KeyExists, KeyNotFound, MVCCStore
 
 log = logging.getLogger("amdkube.etcd3")
 ALL = b"\x00"          # key "\0" with range_end "\0": the whole keyspace
 FENCE = "/amdkube.io/revision-fence"       # written by every apiserver Txn (see Etcd3Store._write)
 _FENCE_B = FENCE.encode()
+
+
+MAX_BATCH = 256        # writes per group-committed Txn
+
+
+class _Op:
+    __slots__ = ("key", "value", "expect", "delete", "fut", "data", "tries")
+
+    def __init__(self, key, value, expect, delete, fut):
+        self.key, self.value, self.expect, self.delete, self.fut = key, value, expect, delete, fut
+        self.data, self.tries = None, 0
+
+
+_KV_RESP = {name: resp for name, _req, resp, _s, _c in E.services["KV"].methods}
 
 
 def _s(b: bytes) -> str:
@@ -61,12 +83,20 @@ def _channel(endpoint: str, ca=None, cert=None, key=None):
 
 class Etcd3Store(MVCCStore):
     def __init__(self, endpoints, ca: str | None = None, cert: str | None = None, key: str | None = None,
-                 history: int = 200_000, max_queue: int = 500_000, timeout: float = 10.0, transformer=None):
+                 history: int = 200_000, max_queue: int = 500_000, timeout: float = 10.0, transformer=None,
+                 wire: bool = True):
         # `transformer` (encryption at rest) applies to the bytes etcd holds; the replica keeps plaintext
         super().__init__(None, history=history, max_queue=max_queue, transformer=transformer)
         self.endpoints = [e for e in (endpoints.split(",") if isinstance(endpoints, str) else endpoints) if e]
         self.timeout = timeout
         self._creds = (ca, cert, key)
+        self._use_wire = wire
+        self._wire_ports: dict[int, int] = {}       # endpoint index -> advertised wire port (0: none)
+        self._wire: SyncChannel | None = None
+        self._watch_wire: SyncChannel | None = None
+        self._achan: PeerChannel | None = None      # the loop's own connection for group commits
+        self._pending: list[_Op] = []
+        self._flusher = None
         self._ep = 0
         self._chan = None
         self._connect(self._leader_endpoint())
@@ -89,27 +119,60 @@ class Etcd3Store(MVCCStore):
         AppendEntries later, so writes go to the leader when it is known."""
         if len(self.endpoints) < 2:
             return 0
-        for i, ep in enumerate(self.endpoints):
-            ch = _channel(ep, *self._creds)
-            try:
-                st = E.Maintenance.stub(ch).Status(E.StatusRequest(), timeout=1.0)
-                if st.leader and st.leader == st.header.member_id:
-                    return i
-            except grpc.RpcError:
-                continue
-            finally:
-                ch.close()
+        for i in range(len(self.endpoints)):
+            st = self._probe(i)
+            if st is not None and st.leader and st.leader == st.header.member_id:
+                return i
         return 0
+
+    def _probe(self, i: int):
+        """Status of endpoint i (None when it does not answer); notes its wire lane port."""
+        ch = _channel(self.endpoints[i], *self._creds)
+        try:
+            st, call = E.Maintenance.stub(ch).Status.with_call(E.StatusRequest(), timeout=1.0)
+            port = dict(call.initial_metadata() or ()).get(WIRE_METADATA)
+            self._wire_ports[i] = int(port) if port and port.isdigit() else 0
+            return st
+        except grpc.RpcError:
+            return None
+        finally:
+            ch.close()
+
+    def _wire_channel(self, i: int) -> SyncChannel | None:
+        if not self._use_wire:
+            return None
+        if i not in self._wire_ports:
+            self._probe(i)
+        port = self._wire_ports.get(i, 0)
+        if not port:
+            return None
+        ep = self.endpoints[i]
+        host = ep.split("://", 1)[-1].rstrip("/").rpartition(":")[0]
+        ca, cert, key = self._creds
+        tls = client_ssl(cert, key, ca) if (ep.startswith("https://") or ca) else None
+        return SyncChannel(f"{host}:{port}", tls)
 
     def _connect(self, i: int):
         """Talk to endpoint i (a member of an etcd cluster; any member forwards to the leader)."""
         if self._chan is not None:
             self._chan.close()
+        if self._wire is not None:
+            self._wire.close()
         self._ep = i % len(self.endpoints)
         self.endpoint = self.endpoints[self._ep]
         self._chan = _channel(self.endpoint, *self._creds)
         self._kvs = E.KV.stub(self._chan)
         self._maint = E.Maintenance.stub(self._chan)
+        self._wire = self._wire_channel(self._ep)
+
+    @property
+    def async_writes(self) -> bool:
+        """Writes from greenbridge.run_sync handlers are group-committed without blocking."""
+        return greenbridge.available()
+
+    @property
+    def transport(self) -> str:
+        return "wire" if self._wire is not None else "grpc"
 
     def _call(self, method: str, req, retry_timeouts: bool = False):
         """A unary KV call with fail-over: an unreachable member (or one without a leader) sends
@@ -118,6 +181,9 @@ class Etcd3Store(MVCCStore):
         deadline = time.monotonic() + max(self.timeout, 3.0)
         while True:
             try:
+                if self._wire is not None:
+                    return _KV_RESP[method].FromString(
+                        self._wire.call(f"/etcdserverpb.KV/{method}", req.SerializeToString(), self.timeout))
                 return getattr(self._kvs, method)(req, timeout=self.timeout)
             except grpc.RpcError as e:
                 if e.code() not in retry or time.monotonic() > deadline:
@@ -158,10 +224,15 @@ class Etcd3Store(MVCCStore):
                                                                      start_revision=self.synced_rev + 1, prev_kv=True))
             if chan is None:
                 chan = _channel(self.endpoints[ep % len(self.endpoints)], *self._creds)
+                self._watch_wire = self._wire_channel(ep % len(self.endpoints))
             try:
                 # every member applies the same log, so a watch resumes at the same revision on any of them
-                self._watch_call = E.Watch.stub(chan).Watch(self._requests(req))
-                for resp in self._watch_call:
+                if self._watch_wire is not None:
+                    stream = (E.WatchResponse.FromString(b) for b in
+                              self._watch_wire.stream("/etcdserverpb.Watch/Watch", req.SerializeToString()))
+                else:
+                    self._watch_call = stream = E.Watch.stub(chan).Watch(self._requests(req))
+                for resp in stream:
                     if resp.compact_revision:
                         self._events.put(("resync", None))
                         self._kick()
@@ -179,12 +250,16 @@ class Etcd3Store(MVCCStore):
                 log.warning("etcd watch on %s broke (%s); re-watching from %d", self.endpoints[ep % len(self.endpoints)],
                             e.code(), self.synced_rev + 1)
                 chan.close()
+                if self._watch_wire is not None:
+                    self._watch_wire.close()
                 chan, ep = None, ep + 1
             if self._stop.wait(backoff):
                 break
             backoff = min(backoff * 2, 2.0)
         if chan is not None:
             chan.close()
+        if self._watch_wire is not None:
+            self._watch_wire.close()
 
     def _kick(self):
         loop = self._loop
@@ -266,21 +341,48 @@ class Etcd3Store(MVCCStore):
         except grpc.RpcError as e:
             raise ConnectionError(f"etcd {self.endpoint}: {e.code().name}: {e.details()}") from None
 
+    @staticmethod
+    def _object_compare(bkey: bytes, expect_mod_rev: int | None, delete: bool):
+        if expect_mod_rev is not None and (expect_mod_rev or not delete):
+            return E.Compare(key=bkey, target=T_MOD, result=EQUAL, mod_revision=expect_mod_rev)
+        if delete:
+            return E.Compare(key=bkey, target=T_VERSION, result=GREATER, version=0)      # must exist
+        return None
+
+    @staticmethod
+    def _object_ok(cur_mod: int, expect_mod_rev: int | None, delete: bool) -> bool:
+        if expect_mod_rev is not None and (expect_mod_rev or not delete):
+            return cur_mod == expect_mod_rev
+        return not delete or cur_mod != 0
+
+    def _conflict(self, key: str, orr, expect_mod_rev: int | None, delete: bool) -> Exception:
+        """The caller's error for an object compare that failed (replica caught up first)."""
+        self.drain(until=orr.header.revision)
+        cur = self.kv.get(key)
+        if cur is None and orr.kvs:
+            kv = orr.kvs[0]
+            cur = KV(key, self._plain(key, kv.value), kv.create_revision, kv.mod_revision, kv.version)
+        if expect_mod_rev == 0 and not delete:
+            return KeyExists(key)
+        if cur is None:
+            return KeyNotFound(key)
+        return CASFailed(cur)
+
     def _write(self, key: str, value, expect_mod_rev: int | None, delete: bool):
         """One fenced CAS Txn. The fence compare fails when any other apiserver committed since
         this replica's view, so a success means the commit revision is exactly rev+1 and the
         resourceVersion rendered into the value is right; a fence-only failure catches up and
-        retries, an object compare failure is the caller's conflict."""
+        retries, an object compare failure is the caller's conflict. Returns (the op's
+        ResponseOp, commit revision, the bytes written)."""
         bkey = _b(key)
         for _ in range(1000):
             self.drain()
             fence = self.kv.get(FENCE)
             guess = self.rev + 1
             cmp = [E.Compare(key=_FENCE_B, target=T_MOD, result=EQUAL, mod_revision=fence.mod_rev if fence else 0)]
-            if expect_mod_rev is not None and (expect_mod_rev or not delete):
-                cmp.append(E.Compare(key=bkey, target=T_MOD, result=EQUAL, mod_revision=expect_mod_rev))
-            elif delete:
-                cmp.append(E.Compare(key=bkey, target=T_VERSION, result=GREATER, version=0))   # must exist
+            oc = self._object_compare(bkey, expect_mod_rev, delete)
+            if oc is not None:
+                cmp.append(oc)
             data = None
             if delete:
                 op = E.RequestOp(request_delete_range=E.DeleteRangeRequest(key=bkey, prev_kv=True))
@@ -301,50 +403,158 @@ class Etcd3Store(MVCCStore):
                     # nothing else committed in between (the revision moved by exactly this Txn), so
                     # the replica is exact at rev-1 and this write can be applied now; the watch's
                     # copy of the same events is skipped when it arrives
-                    self._apply_own(key, data, rev, delete)
+                    self._apply_own([(key, data, delete)], rev)
                 else:
                     self.drain(until=rev)
-                return resp, rev, data
+                return resp.responses[1], rev, data
             frr, orr = resp.responses[0].response_range, resp.responses[1].response_range
             cur_mod = orr.kvs[0].mod_revision if orr.kvs else 0
-            object_ok = (cur_mod == expect_mod_rev) if (expect_mod_rev is not None and (expect_mod_rev or not delete)) \
-                else (not delete or cur_mod != 0)
-            if not object_ok:
-                self.drain(until=orr.header.revision)
-                cur = self.kv.get(key)
-                if cur is None and orr.kvs:
-                    kv = orr.kvs[0]
-                    cur = KV(key, self._plain(key, kv.value), kv.create_revision, kv.mod_revision, kv.version)
-                if expect_mod_rev == 0 and not delete:
-                    raise KeyExists(key)
-                if cur is None:
-                    raise KeyNotFound(key)
-                raise CASFailed(cur)
+            if not self._object_ok(cur_mod, expect_mod_rev, delete):
+                raise self._conflict(key, orr, expect_mod_rev, delete)
             self.drain(until=frr.kvs[0].mod_revision if frr.kvs else 0)     # only the fence moved
         raise ConnectionError(f"etcd3: {key}: the revision fence kept moving")
 
-    def _apply_own(self, key: str, data, rev: int, delete: bool):
+    def _apply_own(self, ops, rev: int):
+        """Apply this replica's own committed Txn (fence + ops, all at `rev`) without waiting
+        for the watch to bring it back."""
         fence = self.kv.get(FENCE)
         self._apply(E.Event(type=EV_PUT, kv=E.KeyValue(key=_FENCE_B, create_revision=fence.create_rev if fence else rev,
                                                         mod_revision=rev, version=(fence.version + 1) if fence else 1)))
-        cur = self.kv.get(key)
-        if delete:
-            self._apply(E.Event(type=1, kv=E.KeyValue(key=_b(key), mod_revision=rev)))
-        else:
-            self._apply(E.Event(type=EV_PUT, kv=E.KeyValue(key=_b(key), value=self._sealed(key, data),
-                                                           create_revision=cur.create_rev if cur else rev, mod_revision=rev,
-                                                           version=(cur.version + 1) if cur else 1)))
+        for key, data, delete in ops:
+            cur = self.kv.get(key)
+            if delete:
+                self._apply(E.Event(type=1, kv=E.KeyValue(key=_b(key), mod_revision=rev)))
+            else:
+                self._apply(E.Event(type=EV_PUT, kv=E.KeyValue(key=_b(key), value=self._sealed(key, data),
+                                                               create_revision=cur.create_rev if cur else rev,
+                                                               mod_revision=rev, version=(cur.version + 1) if cur else 1)))
+
+    # ------------------------------------------------------------------ group commit (bridged writes)
+    async def _submit_op(self, key: str, value, expect_mod_rev: int | None, delete: bool):
+        """A write from a request handler running under greenbridge.run_sync: queued, and
+        committed together with every other write queued meanwhile in ONE fenced Txn (one
+        revision, one raft entry), so concurrent requests share the round trip instead of
+        each stalling the loop for one."""
+        op = _Op(key, value, expect_mod_rev, delete, self._loop.create_future())
+        self._pending.append(op)
+        if self._flusher is None:
+            self._flusher = self._loop.create_task(self._flush())
+        return await op.fut
+
+    async def _flush(self):
+        try:
+            while self._pending:
+                batch, rest, keys = [], [], set()
+                for op in self._pending:          # one op per key per Txn (etcd refuses duplicates)
+                    if op.key in keys or len(batch) >= MAX_BATCH:
+                        rest.append(op)
+                    else:
+                        keys.add(op.key)
+                        batch.append(op)
+                self._pending = rest
+                try:
+                    redo = await self._commit_batch(batch)
+                except Exception as e:        # noqa: BLE001 — every waiter gets the failure
+                    redo = []
+                    for op in batch:
+                        if not op.fut.done():
+                            op.fut.set_exception(e)
+                self._pending[:0] = redo
+        finally:
+            self._flusher = None
+
+    async def _commit_batch(self, batch: list) -> list:
+        """One fenced Txn for `batch`; resolves the ops it settles, returns those to retry."""
+        self.drain()
+        fence = self.kv.get(FENCE)
+        guess = self.rev + 1
+        cmp = [E.Compare(key=_FENCE_B, target=T_MOD, result=EQUAL, mod_revision=fence.mod_rev if fence else 0)]
+        success = [E.RequestOp(request_put=E.PutRequest(key=_FENCE_B))]
+        failure = [E.RequestOp(request_range=E.RangeRequest(key=_FENCE_B))]
+        for op in batch:
+            bkey = _b(op.key)
+            oc = self._object_compare(bkey, op.expect, op.delete)
+            if oc is not None:
+                cmp.append(oc)
+            if op.delete:
+                op.data = None
+                success.append(E.RequestOp(request_delete_range=E.DeleteRangeRequest(key=bkey, prev_kv=True)))
+            else:
+                op.data = op.value(guess) if callable(op.value) else op.value
+                success.append(E.RequestOp(request_put=E.PutRequest(key=bkey, value=self._sealed(op.key, op.data))))
+            failure.append(E.RequestOp(request_range=E.RangeRequest(key=bkey)))
+        resp = await self._atxn(E.TxnRequest(compare=cmp, success=success, failure=failure))
+        if resp.succeeded:
+            rev = resp.header.revision
+            redo = []
+            if rev != guess:
+                self.drain(until=rev)
+                # a writer outside the fence committed in between: re-render at the real revision
+                redo = [op for op in batch if callable(op.value) and not op.delete]
+                for op in redo:
+                    log.warning("etcd3: %s committed at %d, rendered for %d; rewriting", op.key, rev, guess)
+                    op.expect = rev
+            elif self.rev == guess - 1:
+                self._apply_own([(op.key, op.data, op.delete) for op in batch], rev)
+            else:
+                self.drain(until=rev)
+            for i, op in enumerate(batch):
+                if op not in redo:
+                    op.fut.set_result((resp.responses[1 + i], rev, op.data))
+            return redo
+        redo = []
+        self.drain(until=resp.header.revision)
+        for i, op in enumerate(batch):
+            orr = resp.responses[1 + i].response_range
+            cur_mod = orr.kvs[0].mod_revision if orr.kvs else 0
+            if self._object_ok(cur_mod, op.expect, op.delete):
+                redo.append(op)                   # failed only with the rest: next Txn
+            else:
+                op.fut.set_exception(self._conflict(op.key, orr, op.expect, op.delete))
+        if redo and len(redo) == len(batch):
+            op = redo[0]                          # the fence alone moved: caught up above
+            op.tries += 1
+            if op.tries > 1000:
+                for o in redo:
+                    o.fut.set_exception(ConnectionError(f"etcd3: {o.key}: the revision fence kept moving"))
+                return []
+        return redo
+
+    async def _atxn(self, req):
+        """The Txn without blocking the loop: over the wire lane's async connection when the
+        member has one, else the blocking gRPC call in a worker thread. A lost connection
+        falls back to the blocking path, which fails over between endpoints."""
+        try:
+            if self._wire is not None:
+                target = self._wire.target
+                if self._achan is None or self._achan.target != target:
+                    if self._achan is not None:
+                        await self._achan.close()
+                    self._achan = PeerChannel(target, self._wire.ssl)
+                return E.TxnResponse.FromString(await self._achan.call("/etcdserverpb.KV/Txn", req.SerializeToString(),
+                                                                       self.timeout))
+            return await self._loop.run_in_executor(None, lambda: self._kvs.Txn(req, timeout=self.timeout))
+        except grpc.RpcError as e:
+            if e.code() != grpc.StatusCode.UNAVAILABLE:
+                raise ConnectionError(f"etcd {self.endpoint}: {e.code().name}: {e.details()}") from None
+        return self._txn(req.compare, req.success, req.failure)
 
     def put(self, key: str, value, expect_mod_rev: int | None = None) -> KV:
-        _, rev, data = self._write(key, value, expect_mod_rev, False)
+        if self._loop is not None and greenbridge.bridged():
+            _, rev, data = greenbridge.await_only(self._submit_op(key, value, expect_mod_rev, False))
+        else:
+            _, rev, data = self._write(key, value, expect_mod_rev, False)
         got = self.kv.get(key)
         if got is not None and got.mod_rev == rev:
             return got
         return KV(key, data, got.create_rev if got else rev, rev, 0)     # already replaced in the replica
 
     def delete(self, key: str, expect_mod_rev: int | None = None) -> KV:
-        resp, _, _ = self._write(key, None, expect_mod_rev, True)
-        pk = resp.responses[1].response_delete_range.prev_kvs[0]
+        if self._loop is not None and greenbridge.bridged():
+            r, _, _ = greenbridge.await_only(self._submit_op(key, None, expect_mod_rev, True))
+        else:
+            r, _, _ = self._write(key, None, expect_mod_rev, True)
+        pk = r.response_delete_range.prev_kvs[0]
         return KV(key, self._plain(key, pk.value), pk.create_revision, pk.mod_revision, pk.version)
 
     def batch(self, ops):
@@ -365,10 +575,18 @@ class Etcd3Store(MVCCStore):
         self._stop.set()
         if self._watch_call is not None:
             self._watch_call.cancel()
+        if self._watch_wire is not None:
+            self._watch_wire.close()            # unblocks the watch thread's read
         if self._thread is not None:
             self._thread.join(timeout=5)
         super().close()
         self._chan.close()
+        if self._wire is not None:
+            self._wire.close()
+        ach, self._achan = self._achan, None
+        if ach is not None and ach._writer is not None:
+            ach.closed = True
+            ach._writer.close()                 # its reader task ends with the connection
 
 
 def prefix_range(prefix: str) -> tuple[bytes, bytes]:

@@ -44,6 +44,7 @@ from .peerwire import stub as peer_stub
 
 log = logging.getLogger("amdkube.etcd")
 VERSION = "3.1.11-amdkube"
+WIRE_METADATA = "amdkube-wire"     # Status initial metadata: the client wire lane's port
 NOPUT, NODELETE = 0, 1
 
 
@@ -127,6 +128,8 @@ class EtcdServer:
         self.peer_tls = peer_tls
         self.peer_server = None         # peerwire.PeerServer
         self.peer_port = 0
+        self.wire_server = None         # peerwire.PeerServer carrying the client API (KV, Watch, Status)
+        self.wire_port = 0
 
     # ------------------------------------------------------------------ lifecycle
     def _peer_channel(self, target: str):
@@ -134,15 +137,22 @@ class EtcdServer:
         from .peerwire import PeerChannel, client_ssl
         return PeerChannel(target, client_ssl(*self.peer_tls) if self.peer_tls else None)
 
-    async def start(self, address: str = "127.0.0.1:0", credentials=None, peer_address: str | None = None):
+    async def start(self, address: str = "127.0.0.1:0", credentials=None, peer_address: str | None = None,
+                    wire_address: str | None = None, wire_ssl=None):
         """Serve the client API (KV, Watch, Lease, Maintenance) on `address`. With a cluster, a
         second server on `peer_address` (default: this member's --initial-cluster URL) carries
-        the raft and Peer services and nothing else."""
+        the raft and Peer services and nothing else. With `wire_address`, the KV, Watch and
+        Status methods are also served over peerwire framing (under `wire_ssl`, the client TLS
+        of the gRPC listener) and the port is advertised in Status's initial metadata."""
         self.server = grpc.aio.server(options=_SRV_OPTS)
         for svc in ("KV", "Watch", "Lease", "Maintenance"):
             self.server.add_generic_rpc_handlers((E.services[svc].handler(self),))
         self.port = (self.server.add_secure_port(address, credentials) if credentials is not None
                      else self.server.add_insecure_port(address))
+        if wire_address is not None:
+            from .peerwire import PeerServer
+            self.wire_server = PeerServer([(E.services[svc], self) for svc in ("KV", "Watch", "Maintenance")], wire_ssl)
+            self.wire_port = await self.wire_server.start(wire_address)
         if len(self.peers) > 1:
             from .raft import RAFT, Raft
             data_dir, hb, el = self._raft_args
@@ -170,6 +180,8 @@ class EtcdServer:
             await self.server.stop(grace)
         if self.peer_server is not None:
             await self.peer_server.stop()
+        if self.wire_server is not None:
+            await self.wire_server.stop()
         for w in self.store.all_watchers():
             w.close()
 
@@ -645,6 +657,8 @@ class EtcdServer:
 
     # ------------------------------------------------------------------ Maintenance
     async def Status(self, req, ctx):
+        if self.wire_port and hasattr(ctx, "send_initial_metadata"):
+            await ctx.send_initial_metadata(((WIRE_METADATA, str(self.wire_port)),))
         size = sum(len(kv.value) + len(kv.key) for kv in self.store.kv.values())
         if self.raft is None:
             return E.StatusResponse(header=self.header(), version=VERSION, dbSize=size, leader=self.member_id,
@@ -656,21 +670,27 @@ class EtcdServer:
 
 async def serve(data_dir: str | None, listen: str, cert=None, key=None, ca=None, snapshot_every: int = 50_000,
                 name: str = "default", peers: dict[str, str] | None = None, peer_listen: str | None = None,
-                heartbeat: float = 0.1, election: float = 1.0, peer_cert=None, peer_key=None, peer_ca=None):
+                heartbeat: float = 0.1, election: float = 1.0, peer_cert=None, peer_key=None, peer_ca=None,
+                wire_port: int = 0):
     """`amdkube etcd`: run until cancelled. With `peers` (--initial-cluster) the member joins a
-    raft group; its store then lives in memory and the raft log under data_dir is the WAL."""
-    creds = None
+    raft group; its store then lives in memory and the raft log under data_dir is the WAL.
+    `wire_port` (-1: off, 0: any free port) is the client wire lane on the client listener's host."""
+    creds = wire_ssl = None
     if cert and key:
         creds = grpc.ssl_server_credentials([(open(key, "rb").read(), open(cert, "rb").read())],
                                             root_certificates=open(ca, "rb").read() if ca else None,
                                             require_client_auth=bool(ca))
+        from .peerwire import server_ssl
+        wire_ssl = server_ssl(cert, key, ca)
+    wire_address = None if wire_port < 0 else f"{listen.rsplit(':', 1)[0]}:{wire_port}"
     clustered = bool(peers) and len(peers) > 1
     store = MVCCStore(None if clustered else data_dir, snapshot_every=snapshot_every)
     srv = await EtcdServer(store, name=name, peers=peers if clustered else None, data_dir=data_dir,
                            heartbeat=heartbeat, election=election, compact_every=snapshot_every,
                            peer_tls=(peer_cert, peer_key, peer_ca) if peer_cert and peer_key else None,
-                           ).start(listen, creds, peer_listen if clustered else None)
-    print(f"amdkube etcd: serving the etcd v3 API on {srv.address} (revision {store.rev})", flush=True)
+                           ).start(listen, creds, peer_listen if clustered else None, wire_address, wire_ssl)
+    print(f"amdkube etcd: serving the etcd v3 API on {srv.address} (revision {store.rev})"
+          + (f", client wire lane on port {srv.wire_port}" if srv.wire_port else ""), flush=True)
     try:
         await asyncio.Event().wait()
     finally:

@@ -7,10 +7,20 @@ Python gRPC aio costs about a millisecond per unary round trip on loopback, whic
 full millisecond into every commit (leader → follower AppendEntries → ack). This transport
 costs a tenth of that, so a commit is bounded by the follower's fdatasync, not the RPC stack.
 
+The same framing also carries the etcd client API between `amdkube etcd` and the apiserver's
+Etcd3Store (the "wire lane", EtcdServer.start(wire_address=...)): the apiserver makes one
+blocking KV call per write, and gRPC's per-call cost on both ends was most of an etcd-1 Txn.
+gRPC stays the public client API; the lane is advertised to clients in the `amdkube-wire`
+initial metadata of Maintenance.Status and used only by clients that see it.
+
 Frames: u32 big-endian length, then
   request   u8 0 | u32 id | u8 len(path) | path "/pkg.Service/Method" | request message
   response  u8 1 | u32 id | response message
   error     u8 2 | u32 id | u8 grpc status code | utf-8 message
+  message   u8 3 | u32 id | one server-stream message          (streaming methods)
+  end       u8 4 | u32 id                                      (stream finished)
+  cancel    u8 5 | u32 id                                      (client ends its stream)
+  cmessage  u8 6 | u32 id | one more client-stream message     (bidi methods)
 The server dispatches each request to its own task (handlers may wait on raft), so replies can
 come back out of order; the client matches them by id. Failures surface as `PeerRpcError`, a
 grpc.RpcError with code()/details(), so raft and the etcd server handle them as before.
@@ -20,14 +30,16 @@ from __future__ import annotations
 import asyncio
 import itertools
 import logging
+import socket
 import ssl
 import struct
+import threading
 
 import grpc
 
 log = logging.getLogger("amdkube.peerwire")
 
-REQ, RESP, ERR = 0, 1, 2
+REQ, RESP, ERR, MSG, END, CANCEL, CMSG = 0, 1, 2, 3, 4, 5, 6
 MAX_FRAME = 256 << 20
 
 
@@ -55,10 +67,32 @@ def server_ssl(cert: str, key: str, ca: str | None) -> ssl.SSLContext:
     return ctx
 
 
-def client_ssl(cert: str, key: str, ca: str | None) -> ssl.SSLContext:
+def client_ssl(cert: str | None, key: str | None, ca: str | None) -> ssl.SSLContext:
     ctx = ssl.create_default_context(ssl.Purpose.SERVER_AUTH, cafile=ca)
-    ctx.load_cert_chain(cert, key)
+    if cert and key:
+        ctx.load_cert_chain(cert, key)
     return ctx
+
+
+class _Ctx:
+    """The handler context a PeerServer passes where gRPC passes its ServicerContext."""
+
+    async def abort(self, code, details):
+        raise PeerRpcError(code, details)
+
+    def invocation_metadata(self):
+        return ()
+
+
+_CTX = _Ctx()
+
+
+def _frame(kind: int, cid: int, body: bytes = b"") -> bytes:
+    return struct.pack(">IBI", 5 + len(body), kind, cid) + body
+
+
+def _err_frame(cid: int, code: grpc.StatusCode, msg: str) -> bytes:
+    return _frame(ERR, cid, bytes([code.value[0]]) + msg[:4000].encode())
 
 
 async def _read_frame(reader: asyncio.StreamReader) -> bytes:
@@ -73,10 +107,15 @@ class PeerServer:
 
     def __init__(self, bindings, ssl_ctx: ssl.SSLContext | None = None):
         self.methods = {}
+        self.streams = {}               # streaming methods: path -> (req_cls, fn, client_streaming)
         for svc, impl in bindings:
             for name, req, _resp, stream, cstream in svc.methods:
                 fn = getattr(impl, name, None)
-                if fn is not None and not stream and not cstream:
+                if fn is None:
+                    continue
+                if stream or cstream:
+                    self.streams[f"/{svc.full_name}/{name}"] = (req, fn, cstream)
+                else:
                     self.methods[f"/{svc.full_name}/{name}"] = (req, fn)
         self.ssl = ssl_ctx
         self.server: asyncio.AbstractServer | None = None
@@ -107,15 +146,32 @@ class PeerServer:
         task = asyncio.current_task()
         self._conns.add(task)
         inflight: set[asyncio.Task] = set()
+        streams: dict[int, tuple] = {}           # id -> (task, request queue, request class)
         try:
             while True:
                 frame = await _read_frame(reader)
                 kind, cid = frame[0], struct.unpack_from(">I", frame, 1)[0]
+                if kind == CMSG or kind == CANCEL:
+                    ent = streams.get(cid)
+                    if ent is not None:
+                        if kind == CANCEL:
+                            ent[0].cancel()
+                        else:
+                            ent[1].put_nowait(ent[2].FromString(frame[5:]))
+                    continue
                 if kind != REQ:
                     raise ConnectionError("peer sent a non-request frame")
                 plen = frame[5]
                 path = frame[6:6 + plen].decode()
-                t = asyncio.create_task(self._one(writer, cid, path, frame[6 + plen:]))
+                sm = self.streams.get(path)
+                if sm is not None:
+                    q: asyncio.Queue = asyncio.Queue()
+                    q.put_nowait(sm[0].FromString(frame[6 + plen:]))
+                    t = asyncio.create_task(self._stream(writer, cid, sm, q))
+                    streams[cid] = (t, q, sm[0])
+                    t.add_done_callback(lambda _t, c=cid: streams.pop(c, None))
+                else:
+                    t = asyncio.create_task(self._one(writer, cid, path, frame[6 + plen:]))
                 inflight.add(t)
                 t.add_done_callback(inflight.discard)
         except (asyncio.IncompleteReadError, ConnectionError, ssl.SSLError, OSError):
@@ -135,10 +191,12 @@ class PeerServer:
         else:
             req_cls, fn = ent
             try:
-                resp = await fn(req_cls.FromString(payload), None)
+                resp = await fn(req_cls.FromString(payload), _CTX)
                 body = bytes([RESP]) + struct.pack(">I", cid) + resp.SerializeToString()
             except asyncio.CancelledError:
                 raise
+            except PeerRpcError as e:
+                body = bytes([ERR]) + struct.pack(">IB", cid, e.code().value[0]) + e.details()[:4000].encode()
             except Exception as e:   # noqa: BLE001 — the caller gets the error, the connection lives on
                 log.debug("peer method %s failed: %r", path, e)
                 body = bytes([ERR]) + struct.pack(">IB", cid, grpc.StatusCode.UNKNOWN.value[0]) + str(e)[:4000].encode()
@@ -148,6 +206,148 @@ class PeerServer:
                 await writer.drain()
         except (ConnectionError, RuntimeError):
             pass
+
+    async def _stream(self, writer, cid: int, ent, q: asyncio.Queue):
+        """A streaming method: its responses go out as MSG frames, then END (or ERR)."""
+        req_cls, fn, client_streaming = ent
+
+        async def requests():
+            while True:
+                yield await q.get()
+
+        try:
+            gen = fn(requests() if client_streaming else q.get_nowait(), _CTX)
+            async for resp in gen:
+                writer.write(_frame(MSG, cid, resp.SerializeToString()))
+                if writer.transport.get_write_buffer_size() > 1 << 20:
+                    await writer.drain()                 # a slow reader holds the stream, not memory
+            writer.write(_frame(END, cid))
+        except asyncio.CancelledError:
+            pass
+        except PeerRpcError as e:
+            writer.write(_err_frame(cid, e.code(), e.details()))
+        except (ConnectionError, RuntimeError):
+            pass
+        except Exception as e:   # noqa: BLE001
+            log.debug("peer stream %d failed: %r", cid, e)
+            try:
+                writer.write(_err_frame(cid, grpc.StatusCode.UNKNOWN, str(e)))
+            except (ConnectionError, RuntimeError):
+                pass
+
+
+class SyncChannel:
+    """A blocking client of a PeerServer for callers that block anyway (Etcd3Store's writes,
+    its watch thread): one call in flight per channel, no event loop involved. A stream gets
+    a channel of its own. Connection and protocol failures are PeerRpcError(UNAVAILABLE) and
+    drop the socket; the next call reconnects."""
+
+    def __init__(self, target: str, ssl_ctx: ssl.SSLContext | None = None, connect_timeout: float = 3.0):
+        self.target = target.split("://", 1)[-1].rstrip("/")
+        self.ssl = ssl_ctx
+        self.connect_timeout = connect_timeout
+        self._sock: socket.socket | None = None
+        self._ids = itertools.count(1)
+        self._lock = threading.Lock()
+
+    def _connect(self) -> socket.socket:
+        if self._sock is None:
+            host, _, port = self.target.rpartition(":")
+            try:
+                s = socket.create_connection((host, int(port)), timeout=self.connect_timeout)
+                s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                if self.ssl is not None:
+                    s = self.ssl.wrap_socket(s, server_hostname=host)
+            except (OSError, ssl.SSLError) as e:
+                raise PeerRpcError(grpc.StatusCode.UNAVAILABLE, f"connect {self.target}: {e}") from None
+            self._sock = s
+        return self._sock
+
+    def _drop(self):
+        if self._sock is not None:
+            try:
+                self._sock.close()
+            except OSError:
+                pass
+            self._sock = None
+
+    def _recv(self, s: socket.socket, n: int) -> bytes:
+        buf = bytearray()
+        while len(buf) < n:
+            chunk = s.recv(n - len(buf))
+            if not chunk:
+                raise ConnectionError("connection closed")
+            buf += chunk
+        return bytes(buf)
+
+    def _read(self, s: socket.socket) -> bytes:
+        (n,) = struct.unpack(">I", self._recv(s, 4))
+        if n < 5 or n > MAX_FRAME:
+            raise ConnectionError(f"bad peer frame length {n}")
+        return self._recv(s, n)
+
+    def _send_req(self, s: socket.socket, cid: int, path: str, payload: bytes):
+        p = path.encode()
+        s.sendall(_frame(REQ, cid, bytes([len(p)]) + p + payload))
+
+    def call(self, path: str, payload: bytes, timeout: float | None = None) -> bytes:
+        with self._lock:
+            s = self._connect()
+            cid = next(self._ids) & 0xFFFFFFFF
+            try:
+                s.settimeout(timeout)
+                self._send_req(s, cid, path, payload)
+                while True:
+                    frame = self._read(s)
+                    if struct.unpack_from(">I", frame, 1)[0] == cid:
+                        break
+            except socket.timeout:
+                self._drop()              # a late reply must not be read as the next call's
+                raise PeerRpcError(grpc.StatusCode.DEADLINE_EXCEEDED, f"{path} to {self.target} timed out") from None
+            except (OSError, ConnectionError, ssl.SSLError) as e:
+                self._drop()
+                raise PeerRpcError(grpc.StatusCode.UNAVAILABLE, f"{path} to {self.target}: {e}") from None
+        if frame[0] == RESP:
+            return frame[5:]
+        if frame[0] == ERR:
+            raise PeerRpcError(_CODES.get(frame[5], grpc.StatusCode.UNKNOWN), frame[6:].decode(errors="replace"))
+        self._drop()
+        raise PeerRpcError(grpc.StatusCode.UNAVAILABLE, f"{path}: unexpected frame kind {frame[0]}")
+
+    def stream(self, path: str, payload: bytes):
+        """Open a streaming call; yields each response message's bytes until the server ends
+        it. close() from another thread unblocks the reader (as a cancelled call)."""
+        s = self._connect()
+        cid = next(self._ids) & 0xFFFFFFFF
+        try:
+            s.settimeout(None)
+            self._send_req(s, cid, path, payload)
+            while True:
+                frame = self._read(s)
+                if struct.unpack_from(">I", frame, 1)[0] != cid:
+                    continue
+                if frame[0] == MSG:
+                    yield frame[5:]
+                elif frame[0] == END:
+                    return
+                elif frame[0] == ERR:
+                    raise PeerRpcError(_CODES.get(frame[5], grpc.StatusCode.UNKNOWN), frame[6:].decode(errors="replace"))
+                else:
+                    raise ConnectionError(f"unexpected frame kind {frame[0]}")
+        except (OSError, ConnectionError, ssl.SSLError) as e:
+            closed = self._sock is None
+            self._drop()
+            raise PeerRpcError(grpc.StatusCode.CANCELLED if closed else grpc.StatusCode.UNAVAILABLE,
+                               f"{path} stream to {self.target}: {e}") from None
+
+    def close(self):
+        s, self._sock = self._sock, None
+        if s is not None:
+            try:
+                s.shutdown(socket.SHUT_RDWR)
+            except OSError:
+                pass
+            s.close()
 
 
 class PeerChannel:

@@ -3,7 +3,8 @@
   embedded   MVCCStore.put in process (the default apiserver store)
   etcd-1     Etcd3Store fenced CAS Txn against one `amdkube etcd` process
   raft-3     the same against a 3-member raft group (client talks to a follower: forward + commit)
-  apiserver  pod creates/s through APIServer over each backend (serial client)
+  apiserver  pod creates/s through APIServer over each backend: one serial client, and 32
+             concurrent clients (writes from concurrent requests group-commit into shared Txns)
 
   python hack/etcd_bench.py            prints one JSON object
 """
@@ -103,17 +104,21 @@ async def concurrent_puts(endpoint, writers=64, n=4000):
             "p99_ms": round(lat[int(n * 0.99)] * 1e3, 3)}
 
 
-async def pod_creates(store, n=500):
+async def pod_creates(store, n=500, clients=1):
     srv = await APIServer(store).start()
-    c = Client(srv.url, token=srv.loopback_token)
+    cs = [Client(srv.url, token=srv.loopback_token) for _ in range(clients)]
+
+    async def one(k):
+        for i in range(k, n, clients):
+            await cs[k].create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": f"p{clients}-{i}", "namespace": "default"},
+                                "spec": {"containers": [{"name": "c", "image": "busybox"}]}}, "default")
     try:
         t0 = time.perf_counter()
-        for i in range(n):
-            await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": f"p{i}", "namespace": "default"},
-                            "spec": {"containers": [{"name": "c", "image": "busybox"}]}}, "default")
+        await asyncio.gather(*(one(k) for k in range(clients)))
         return round(n / (time.perf_counter() - t0), 1)
     finally:
-        await c.close()
+        for c in cs:
+            await c.close()
         await srv.stop()
 
 
@@ -121,6 +126,7 @@ async def main():
     out = {}
     out["embedded"] = timed_puts(MVCCStore())
     out["embedded"]["apiserver_pod_creates_per_s"] = await pod_creates(MVCCStore())
+    out["embedded"]["apiserver_pod_creates_per_s_32_clients"] = await pod_creates(MVCCStore(), 1000, 32)
     for label, n in (("etcd-1", 1), ("raft-3", 3)):
         with tempfile.TemporaryDirectory() as tmp:
             procs, client = spawn(tmp, n)
@@ -132,7 +138,9 @@ async def main():
                 s.close()
                 out[label]["concurrent"] = await concurrent_puts(eps[-1])
                 s = await asyncio.to_thread(Etcd3Store, eps[-1:] + eps[:-1])
+                out[label]["transport"] = s.transport
                 out[label]["apiserver_pod_creates_per_s"] = await pod_creates(s)
+                out[label]["apiserver_pod_creates_per_s_32_clients"] = await pod_creates(s, 1000, 32)
                 s.close()
             finally:
                 for p in procs:

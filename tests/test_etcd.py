@@ -8,6 +8,7 @@ image, so behaviour against a real etcd server is parity unpinned; the semantics
 ones the reference's etcd3 storage relies on."""
 import asyncio
 import gzip
+import json
 import os
 import socket
 import subprocess
@@ -85,16 +86,19 @@ class ServerThread:
     """The etcd server on its own thread and loop (a blocking client on the test's loop must not
     wait on a server running on that same loop)."""
 
-    def __init__(self, store=None):
+    def __init__(self, store=None, wire=False, tls=None):
         self.store = store or MVCCStore()
         self.ready = threading.Event()
         self.loop = None
+        self.wire, self.tls = wire, tls        # tls: (grpc server credentials, ssl.SSLContext)
 
     def __enter__(self):
         def run():
             async def main():
                 self.loop = asyncio.get_running_loop()
-                self.srv = await EtcdServer(self.store).start("127.0.0.1:0")
+                creds, wire_ssl = self.tls or (None, None)
+                self.srv = await EtcdServer(self.store).start("127.0.0.1:0", creds, None,
+                                                              "127.0.0.1:0" if self.wire else None, wire_ssl)
                 self.stop_ev = asyncio.Event()
                 self.ready.set()
                 await self.stop_ev.wait()
@@ -226,10 +230,12 @@ def test_watch_prev_kv_filters_cancel_compaction_and_leases():
         ch.close()
 
 
-async def test_replicas_share_one_store_with_fenced_cas():
-    with ServerThread() as st:
+@pytest.mark.parametrize("wire", [False, True], ids=["grpc", "wire"])
+async def test_replicas_share_one_store_with_fenced_cas(wire):
+    with ServerThread(wire=wire) as st:
         a, b = Etcd3Store(st.address), Etcd3Store(st.address)
         try:
+            assert a.transport == b.transport == ("wire" if wire else "grpc")
             loop = asyncio.get_running_loop()
             a.start(loop)
             b.start(loop)
@@ -280,7 +286,8 @@ async def test_two_apiservers_over_amdkube_etcd(tmp_path):
         line = await asyncio.wait_for(asyncio.to_thread(proc.stdout.readline), 60)
         assert b"serving the etcd v3 API" in line, line
         ep = f"http://127.0.0.1:{port}"
-        s1, s2 = await asyncio.to_thread(Etcd3Store, ep), await asyncio.to_thread(Etcd3Store, ep)
+        s1, s2 = await asyncio.to_thread(Etcd3Store, ep), await asyncio.to_thread(Etcd3Store, ep, wire=False)
+        assert (s1.transport, s2.transport) == ("wire", "grpc")      # both lanes serve one keyspace
         api1 = await APIServer(s1, options={"apiserver_count": 2}).start()
         api2 = await APIServer(s2, options={"apiserver_count": 2}).start()
         c1, c2 = Client(api1.url, token=api1.loopback_token), Client(api2.url, token=api2.loopback_token)
@@ -356,4 +363,127 @@ async def test_encryption_at_rest_through_etcd(tmp_path):
             raw = st.store.get("/registry/secrets/default/s").value
             assert raw.startswith(b"k8s:enc:aescbc:v1:k1:") and b"plaintext-value" not in raw
         finally:
+            s.close()
+
+
+def test_wire_lane_errors_watch_and_tls(tmp_path):
+    """The client wire lane: etcd errors keep their gRPC codes, the watch streams over it, the
+    lane is advertised only in Status metadata, and it carries the gRPC listener's client TLS."""
+    from amdkube.store.peerwire import PeerRpcError, SyncChannel, server_ssl
+    with ServerThread(wire=True) as st:
+        assert st.srv.wire_port
+        ch = grpc.insecure_channel(st.address)
+        _, call = E.Maintenance.stub(ch).Status.with_call(E.StatusRequest())
+        assert dict(call.initial_metadata())["amdkube-wire"] == str(st.srv.wire_port)
+        ch.close()
+        w = SyncChannel(f"127.0.0.1:{st.srv.wire_port}")
+        r = E.PutResponse.FromString(w.call("/etcdserverpb.KV/Put", E.PutRequest(key=b"/k", value=b"v").SerializeToString(), 5))
+        with pytest.raises(PeerRpcError) as ei:             # unknown lease: NOT_FOUND, as over gRPC
+            w.call("/etcdserverpb.KV/Put", E.PutRequest(key=b"/k", value=b"v", lease=7).SerializeToString(), 5)
+        assert ei.value.code() == grpc.StatusCode.NOT_FOUND
+        with pytest.raises(PeerRpcError) as ei:
+            w.call("/etcdserverpb.Lease/LeaseGrant", E.LeaseGrantRequest(TTL=5).SerializeToString(), 5)
+        assert ei.value.code() == grpc.StatusCode.UNIMPLEMENTED       # only KV, Watch and Status ride the lane
+        ws = SyncChannel(f"127.0.0.1:{st.srv.wire_port}")
+        req = E.WatchRequest(create_request=E.WatchCreateRequest(key=b"/", range_end=prefix_end(b"/"),
+                                                                 start_revision=r.header.revision))
+        got = []
+
+        def follow():
+            try:
+                for b in ws.stream("/etcdserverpb.Watch/Watch", req.SerializeToString()):
+                    got.extend(e.kv.key for e in E.WatchResponse.FromString(b).events)
+            except PeerRpcError as e:
+                got.append(e.code())
+        t = threading.Thread(target=follow)
+        t.start()
+        w.call("/etcdserverpb.KV/Put", E.PutRequest(key=b"/k2", value=b"v").SerializeToString(), 5)
+        deadline = time.time() + 5
+        while len(got) < 2 and time.time() < deadline:
+            time.sleep(0.02)
+        ws.close()                                           # cancels the stream from another thread
+        t.join(5)
+        assert got == [b"/k", b"/k2", grpc.StatusCode.CANCELLED]
+        w.close()
+    from amdkube.kubeadm import new_ca, new_cert
+    d = tmp_path / "pki"
+    d.mkdir()
+    new_ca(str(d), "ca", "etcd-ca")
+    new_cert(str(d), "s", "etcd", sans=("IP:127.0.0.1",), server=True)
+    new_cert(str(d), "c", "apiserver-etcd-client")
+    paths = {n: str(d / n) for n in ("ca.crt", "s.crt", "s.key", "c.crt", "c.key")}
+    creds = grpc.ssl_server_credentials([(open(paths["s.key"], "rb").read(), open(paths["s.crt"], "rb").read())],
+                                        root_certificates=open(paths["ca.crt"], "rb").read(), require_client_auth=True)
+    with ServerThread(wire=True, tls=(creds, server_ssl(paths["s.crt"], paths["s.key"], paths["ca.crt"]))) as st:
+        s = Etcd3Store(f"https://{st.address}", ca=paths["ca.crt"], cert=paths["c.crt"], key=paths["c.key"])
+        try:
+            assert s.transport == "wire"
+            s.put("/registry/x/tls", b"v")
+            assert st.store.get("/registry/x/tls").value == b"v"
+        finally:
+            s.close()
+        bare = SyncChannel(f"127.0.0.1:{st.srv.wire_port}")   # plaintext / no client cert: refused
+        with pytest.raises(PeerRpcError):
+            bare.call("/etcdserverpb.KV/Range", E.RangeRequest(key=b"/").SerializeToString(), 2)
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("wire", [False, True], ids=["grpc", "wire"])
+async def test_concurrent_requests_group_commit_over_etcd(wire):
+    """Writes of concurrent requests share fenced Txns (several objects per revision), and
+    each object still carries the resourceVersion it was committed at; conflicts stay per
+    object: of two creates of one name one is a 409, of two updates from one resourceVersion
+    one is a 409, and a delete racing a delete is a 404."""
+    with ServerThread(wire=wire) as st:
+        s = await asyncio.to_thread(Etcd3Store, st.address)
+        srv = await APIServer(s).start()
+        cs = [Client(srv.url, token=srv.loopback_token) for _ in range(8)]
+        try:
+            assert srv._bridged
+            names = [f"p{i}" for i in range(40)] + ["p3"]
+
+            async def create(i, n):
+                try:
+                    return await cs[i % 8].create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": n, "namespace": "default"},
+                                                   "spec": {"containers": [{"name": "c", "image": "busybox"}]}}, "default")
+                except m.StatusError as e:
+                    return e.code
+            res = await asyncio.gather(*(create(i, n) for i, n in enumerate(names)))
+            assert sorted(r for r in res if isinstance(r, int)) == [409]
+            made = [r for r in res if isinstance(r, dict)]
+            assert len(made) == 40
+            revs = {r["metadata"]["resourceVersion"] for r in made}
+            assert len(revs) < 40                       # committed in shared Txns
+            for r in made:
+                kv = st.store.get(f"/registry/pods/default/{r['metadata']['name']}")
+                assert str(kv.mod_rev) == r["metadata"]["resourceVersion"]
+                assert json.loads(kv.value)["metadata"]["resourceVersion"] == r["metadata"]["resourceVersion"]
+            got = await cs[0].get("pods", "p5", "default")
+
+            async def update(i):
+                o = json.loads(json.dumps(got))
+                o["metadata"]["labels"] = {"by": str(i)}
+                try:
+                    return await cs[i].update(o)
+                except m.StatusError as e:
+                    return e.code
+            ups = await asyncio.gather(*(update(i) for i in range(4)))
+            assert sorted(u for u in ups if isinstance(u, int)) == [409, 409, 409]
+            [won] = [u for u in ups if isinstance(u, dict)]
+            assert (await cs[1].get("pods", "p5", "default"))["metadata"]["labels"] == won["metadata"]["labels"]
+
+            async def delete(i, n):
+                try:
+                    await cs[i].delete("pods", n, "default", grace=0)
+                    return 200
+                except m.StatusError as e:
+                    return e.code
+            dels = await asyncio.gather(*(delete(i, f"p{10 + i // 2}") for i in range(8)))
+            assert sorted(dels) == [200] * 4 + [404] * 4
+            items, _ = await cs[0].list("pods", "default")
+            assert len(items) == 36 and all(st.store.get(f"/registry/pods/default/{i['metadata']['name']}") for i in items)
+        finally:
+            for c in cs:
+                await c.close()
+            await srv.stop()
             s.close()
