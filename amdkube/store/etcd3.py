@@ -499,7 +499,7 @@ class Etcd3Store(MVCCStore):
             else:
                 self.drain(until=rev)
             for i, op in enumerate(batch):
-                if op not in redo:
+                if op not in redo and not op.fut.done():     # a cancelled request's write still commits
                     op.fut.set_result((resp.responses[1 + i], rev, op.data))
             return redo
         redo = []
@@ -509,14 +509,15 @@ class Etcd3Store(MVCCStore):
             cur_mod = orr.kvs[0].mod_revision if orr.kvs else 0
             if self._object_ok(cur_mod, op.expect, op.delete):
                 redo.append(op)                   # failed only with the rest: next Txn
-            else:
+            elif not op.fut.done():
                 op.fut.set_exception(self._conflict(op.key, orr, op.expect, op.delete))
         if redo and len(redo) == len(batch):
             op = redo[0]                          # the fence alone moved: caught up above
             op.tries += 1
             if op.tries > 1000:
                 for o in redo:
-                    o.fut.set_exception(ConnectionError(f"etcd3: {o.key}: the revision fence kept moving"))
+                    if not o.fut.done():
+                        o.fut.set_exception(ConnectionError(f"etcd3: {o.key}: the revision fence kept moving"))
                 return []
         return redo
 
