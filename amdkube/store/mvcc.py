@@ -21,6 +21,7 @@ from __future__ import annotations
 import asyncio
 import base64
 import collections
+import fcntl
 import json
 import os
 import threading
@@ -149,9 +150,38 @@ class Watcher:
         return ev
 
 
+class DataDirLocked(RuntimeError):
+    pass
+
+
+def lock_data_dir(path: str, wait: float = 10.0):
+    """Hold `<path>/LOCK` (flock, exclusive) for as long as the returned file stays open: two
+    processes appending one WAL or raft log would interleave records, so the second one
+    waits up to `wait` seconds (a restarted static pod while the old process still exits)
+    and then refuses (etcd takes the same lock on its WAL files: pkg/fileutil LockFile)."""
+    os.makedirs(path, exist_ok=True)
+    f = open(os.path.join(path, "LOCK"), "a+")
+    deadline = time.monotonic() + wait
+    while True:
+        try:
+            fcntl.flock(f.fileno(), fcntl.LOCK_EX | fcntl.LOCK_NB)
+            f.seek(0)
+            f.truncate()
+            f.write(f"{os.getpid()}\n")
+            f.flush()
+            return f
+        except BlockingIOError:
+            if time.monotonic() >= deadline:
+                f.seek(0)
+                holder = f.read().strip() or "?"
+                f.close()
+                raise DataDirLocked(f"data directory {path} is in use by another process (pid {holder})") from None
+            time.sleep(0.05)
+
+
 class MVCCStore:
     def __init__(self, data_dir: str | None = None, history: int = 200_000, max_queue: int = 500_000,
-                 snapshot_every: int = 50_000, fsync: bool = False, transformer=None):
+                 snapshot_every: int = 50_000, fsync: bool = False, transformer=None, lock_wait: float = 10.0):
         self.kv: dict[str, KV] = {}
         # keys bucketed by their first two path components ("/registry/pods/"), so a range over one
         # resource never scans the others (admission lists quotas/limitranges on every create)
@@ -177,9 +207,14 @@ class MVCCStore:
         # value transformer between memory and disk (encryption at rest): to_disk(key, bytes),
         # from_disk(key, bytes); None keeps the bytes as they are
         self.transformer = transformer
+        self._dir_lock = None
         if data_dir:
-            os.makedirs(data_dir, exist_ok=True)
-            self._recover()
+            self._dir_lock = lock_data_dir(data_dir, lock_wait)
+            try:
+                self._recover()
+            except BaseException:
+                self._dir_lock.close()
+                raise
             self._wal = open(os.path.join(data_dir, "wal.log"), "ab", buffering=0)
 
     # ----------------------------------------------------------------- reads
@@ -475,6 +510,9 @@ class MVCCStore:
         if self._wal is not None:
             self._wal.close()
             self._wal = None
+        if self._dir_lock is not None:
+            self._dir_lock.close()             # releases the flock
+            self._dir_lock = None
 
 
 def _b(v: bytes) -> str:

@@ -126,7 +126,8 @@ class Raft:
     def _load(self):
         if not self.dir:
             return
-        os.makedirs(self.dir, exist_ok=True)
+        from .mvcc import lock_data_dir
+        self._dir_lock = lock_data_dir(self.dir)
         st = os.path.join(self.dir, "state.json")
         if os.path.exists(st):
             d = json.load(open(st))
@@ -252,6 +253,9 @@ class Raft:
             if self._logf is not None:
                 self._logf.close()
                 self._logf = None
+        if getattr(self, "_dir_lock", None) is not None:
+            self._dir_lock.close()
+            self._dir_lock = None
 
     def handler(self):
         return RAFT.Raft.handler(self)

@@ -67,6 +67,7 @@ def test_service_cluster_ip_and_node_port_allocation(tmp_path):
     rs.delete("default", "c")
     d = rs.create("default", _svc("d", [{"port": 80}], "NodePort"))
     # repair: a restarted apiserver on the same store sees every allocation
+    store.close()
     api2 = APIServer(MVCCStore(str(tmp_path / "s")), service_cidr="10.96.0.0/29", node_port_range="30000-30002")
     alloc = api2.registry.services
     assert ip_a in alloc.ips and d["spec"]["clusterIP"] in alloc.ips

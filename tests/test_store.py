@@ -2,6 +2,7 @@
 Hypothesis model check that the store is linearizable against a dict model."""
 import asyncio
 import json
+import time
 
 import pytest
 from hypothesis import given, settings, strategies as st
@@ -149,3 +150,20 @@ def test_triggered_watch_equals_filtered_watch(ops):
         plain.close()
         assert not s.triggered
     run(go())
+
+
+def test_data_dir_is_locked_while_a_store_holds_it(tmp_path):
+    """A second store (here: same process, its own open file) on a held data directory waits
+    for the lock and then refuses; closing the first releases it."""
+    from amdkube.store.mvcc import DataDirLocked
+    d = str(tmp_path / "data")
+    s = MVCCStore(data_dir=d)
+    s.put("/k", b"1")
+    t0 = time.monotonic()
+    with pytest.raises(DataDirLocked, match="in use by another process"):
+        MVCCStore(data_dir=d, lock_wait=0.3)
+    assert time.monotonic() - t0 >= 0.25
+    s.close()
+    s2 = MVCCStore(data_dir=d, lock_wait=0.3)
+    assert s2.get("/k").value == b"1"
+    s2.close()
