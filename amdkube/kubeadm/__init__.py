@@ -222,7 +222,7 @@ def init(a) -> int:
     done = ph.phase_kubeconfig(mc, cfg)
     print(f"[kubeconfig] Wrote {', '.join(done)} to {cfg['base']}")
     print(f"[controlplane] Wrote static Pod manifests for {', '.join(ph.phase_controlplane(mc, cfg))} to {cfg['manifests']}")
-    print(f"[etcd] The store is embedded in kube-apiserver (data directory {ph.phase_etcd_local(mc, cfg)})")
+    print(f"[etcd] {ph.phase_etcd_local(mc, cfg)}")
     if a.start_kubelet:
         labels = f"{GPU_LABEL}=true" if os.path.exists("/dev/kfd") else ""
         start_node_agents(cfg, os.path.join(cfg["base"], "kubelet.conf"), node, labels)
@@ -384,6 +384,7 @@ def reset(a) -> int:
     cfg = _paths(a.base_dir)
     pids = os.path.join(cfg["node_dir"], "pids.json")
     man = cfg["manifests"]
+    etcd_dir = _local_etcd_data_dir(man)
     if os.path.isdir(man):   # the kubelet tears static pods down once their manifests go
         for f in os.listdir(man):
             os.unlink(os.path.join(man, f))
@@ -405,9 +406,26 @@ def reset(a) -> int:
                     os.killpg(pid, signal.SIGKILL)
             except (OSError, ValueError, ProcessLookupError):
                 pass
+    # unmountKubeletDirectory: volumes (secret/configMap tmpfs, bind mounts) still mounted under
+    # the kubelet's root would survive the rmtree below
+    from ..volume.mount import unmount_under
+    unmount_under(cfg["base"])
     shutil.rmtree(cfg["base"], ignore_errors=True)
-    print(f"[reset] Stopped the node agents and removed {cfg['base']}")
+    if etcd_dir:                    # resetEtcd: the local etcd's data directory goes too
+        shutil.rmtree(etcd_dir, ignore_errors=True)
+    print(f"[reset] Stopped the node agents and removed {cfg['base']}" + (f" and {etcd_dir}" if etcd_dir else ""))
     return 0
+
+
+def _local_etcd_data_dir(manifests: str) -> str | None:
+    """--data-dir of the local etcd static Pod, read before its manifest goes (reset.go getEtcdDataDir)."""
+    path = os.path.join(manifests, "etcd.yaml")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        pod = yaml.safe_load(f) or {}
+    args = ((pod.get("spec") or {}).get("containers") or [{}])[0].get("args") or []
+    return args[args.index("--data-dir") + 1] if "--data-dir" in args[:-1] else None
 
 
 # --------------------------------------------------------------------------- token

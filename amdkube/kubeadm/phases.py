@@ -8,8 +8,12 @@ of them on its own, against the same --base-dir and --config:
   certs            ca, apiserver, apiserver-kubelet-client, sa, front-proxy-ca, front-proxy-client
   kubeconfig       admin, kubelet, controller-manager, scheduler, kube-proxy, user (--client-name)
   controlplane     static Pod manifests: apiserver, controller-manager, scheduler
-  etcd local       the store is the apiserver's embedded MVCC store (--data-dir); this phase
-                   prepares that directory (there is no separate etcd Pod)
+  etcd local       where the apiserver keeps its objects (etcd_mode): by default the
+                   apiserver's embedded MVCC store (--data-dir), this phase preparing that
+                   directory; with `etcd.dataDir` set, an `amdkube etcd` static Pod on that
+                   directory that the apiserver reaches through --etcd-servers (the
+                   reference's local etcd, app/phases/etcd/local.go); with `etcd.endpoints`,
+                   an external etcd (caFile/certFile/keyFile) and no local store at all
   mark-master      master label + NoSchedule taint
   bootstrap-token  create, cluster-info, node allow-post-csrs, node allow-auto-approve
   upload-config    the MasterConfiguration in kube-system/kubeadm-config (read back by
@@ -228,13 +232,48 @@ def _with_extra(args: list[str], extra: dict) -> list[str]:
     return out
 
 
+def etcd_mode(mc: dict) -> str:
+    """"external" (etcd.endpoints), "local" (etcd.dataDir: an `amdkube etcd` static Pod) or
+    "embedded" (neither: the apiserver's own store, amdkube's default and fastest path)."""
+    e = mc.get("etcd") or {}
+    return "external" if e.get("endpoints") else "local" if e.get("dataDir") else "embedded"
+
+
+def local_etcd_url(mc: dict) -> str:
+    extra = (mc.get("etcd") or {}).get("extraArgs") or {}
+    return str(extra.get("listen-client-urls") or "http://127.0.0.1:2379").split(",")[0]
+
+
+def etcd_manifest(mc: dict) -> dict:
+    """The local etcd static Pod (GetEtcdPodSpec): `amdkube etcd` on etcd.dataDir."""
+    e = mc.get("etcd") or {}
+    args = _with_extra(["--listen-client-urls", local_etcd_url(mc), "--advertise-client-urls", local_etcd_url(mc),
+                        "--data-dir", e["dataDir"]], e.get("extraArgs") or {})
+    pod = _component_pod("etcd", ["etcd", *args])
+    pod["metadata"]["annotations"][VERSION_ANNOTATION] = mc["kubernetesVersion"]
+    return pod
+
+
+def _store_args(mc: dict, p: dict) -> list[str]:
+    mode, e = etcd_mode(mc), mc.get("etcd") or {}
+    if mode == "embedded":
+        return ["--data-dir", p["data_dir"]]
+    if mode == "local":
+        return ["--etcd-servers", local_etcd_url(mc)]
+    out = ["--etcd-servers", ",".join(e["endpoints"])]
+    for key, flag in (("caFile", "--etcd-cafile"), ("certFile", "--etcd-certfile"), ("keyFile", "--etcd-keyfile")):
+        if e.get(key):
+            out += [flag, e[key]]
+    return out
+
+
 def control_plane_manifests(mc: dict, p: dict) -> dict[str, dict]:
     d, k = p["pki"], p["kubeconfig_dir"]
     api = ["--bind-address", mc["api"]["advertiseAddress"], "--port", str(mc["api"]["bindPort"]),
            "--tls-cert-file", f"{d}/apiserver.crt", "--tls-private-key-file", f"{d}/apiserver.key",
            "--client-ca-file", f"{d}/ca.crt", "--authorization-mode", "Node,RBAC", "--anonymous-auth", "true",
            "--admission-control", ADMISSION, "--service-account-key-file", f"{d}/sa.key",
-           "--service-cluster-ip-range", mc["networking"]["serviceSubnet"], "--data-dir", p["data_dir"],
+           "--service-cluster-ip-range", mc["networking"]["serviceSubnet"], *_store_args(mc, p),
            "--kubelet-client-certificate", f"{d}/apiserver-kubelet-client.crt",
            "--kubelet-client-key", f"{d}/apiserver-kubelet-client.key"]
     if os.path.exists(f"{d}/front-proxy-ca.crt"):
@@ -276,8 +315,17 @@ def phase_controlplane(mc: dict, p: dict, which: str = "all") -> list[str]:
 
 
 def phase_etcd_local(mc: dict, p: dict) -> str:
+    """What this node keeps the cluster's objects in; returns a line for the init log."""
+    mode = etcd_mode(mc)
+    if mode == "external":
+        return f"Using the external etcd at {', '.join(mc['etcd']['endpoints'])}"
+    if mode == "local":
+        os.makedirs(p["manifests"], exist_ok=True)
+        path = os.path.join(p["manifests"], "etcd.yaml")
+        write_yaml(path, etcd_manifest(mc), 0o644)
+        return f"Wrote Static Pod manifest for a local etcd instance to {path} (data directory {mc['etcd']['dataDir']})"
     os.makedirs(p["data_dir"], exist_ok=True)
-    return p["data_dir"]
+    return f"The store is embedded in kube-apiserver (data directory {p['data_dir']})"
 
 
 # -------------------------------------------------------------------- cluster-side phases
@@ -482,7 +530,7 @@ def run_phase(a) -> int:
     if a.phase == "etcd":
         if sub not in ("all", "local"):
             raise SystemExit("error: only `etcd local` is supported")
-        print(f"[etcd] The store is embedded in kube-apiserver; prepared its data directory {phase_etcd_local(mc, p)}")
+        print(f"[etcd] {phase_etcd_local(mc, p)}")
         return 0
     kc = a.kubeconfig or os.path.join(a.base_dir, "admin.conf")
 

@@ -142,3 +142,68 @@ async def _check_cluster(admin_conf):
         assert any(x["spec"]["username"].startswith("system:bootstrap:") and x["status"].get("certificate") for x in csrs)
     finally:
         await c.close()
+
+
+def test_kubeadm_local_etcd_static_pod(tmp_path):
+    """etcd.dataDir in the MasterConfiguration: kubeadm writes an `amdkube etcd` static Pod
+    (app/phases/etcd/local.go), the apiserver stores through --etcd-servers, the objects land
+    in etcd's data directory, and reset removes that directory (reset.go resetEtcd)."""
+    base, etcd_dir = str(tmp_path / "master"), str(tmp_path / "etcd-data")
+    port, eport = _free_port(), _free_port()
+    cfg = tmp_path / "cfg.yaml"
+    cfg.write_text("apiVersion: kubeadm.k8s.io/v1alpha1\nkind: MasterConfiguration\n"
+                   f"etcd:\n  dataDir: {etcd_dir}\n  extraArgs:\n    listen-client-urls: http://127.0.0.1:{eport}\n")
+    try:
+        r = _kubeadm("init", "--base-dir", base, "--config", str(cfg), "--apiserver-bind-port", str(port),
+                     "--node-name", "master-0", "--start-kubelet", "--kubelet-port", "0", "--skip-addons", "--timeout", "90")
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+        assert "Wrote Static Pod manifest for a local etcd instance" in r.stdout
+        import yaml
+        api = yaml.safe_load(open(os.path.join(base, "manifests", "kube-apiserver.yaml")))["spec"]["containers"][0]["args"]
+        assert api[api.index("--etcd-servers") + 1] == f"http://127.0.0.1:{eport}" and "--data-dir" not in api
+
+        async def check():
+            c = Client.from_kubeconfig(os.path.join(base, "admin.conf"))
+            try:
+                await c.create({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "in-etcd"}, "data": {"k": "v"}},
+                               "default")
+                end = asyncio.get_running_loop().time() + 60
+                while True:           # the mirror pods of the static pods appear
+                    pods = {m.name_of(p) for p in (await c.list("pods", "kube-system"))[0]}
+                    if "etcd-master-0" in pods or asyncio.get_running_loop().time() > end:
+                        return pods
+                    await asyncio.sleep(0.3)
+            finally:
+                await c.close()
+        pods = asyncio.run(check())
+        assert {"etcd-master-0", "kube-apiserver-master-0"} <= pods
+        assert b"in-etcd" in open(os.path.join(etcd_dir, "wal.log"), "rb").read()
+    finally:
+        r = _kubeadm("reset", "--base-dir", base, "--drain-seconds", "1.5")
+    assert r.returncode == 0 and etcd_dir in r.stdout and not os.path.exists(etcd_dir)
+
+
+def test_kubeadm_store_modes():
+    """embedded (default) / local etcd static Pod / external etcd with client TLS."""
+    from amdkube.kubeadm import phases as ph
+    base = {"api": {"advertiseAddress": "127.0.0.1", "bindPort": 6443}, "kubernetesVersion": "v1.9.0",
+            "networking": {"serviceSubnet": "10.96.0.0/12", "podSubnet": ""}}
+    p = ph.paths("/etc/kubernetes")
+
+    def api_args(mc):
+        return ph.control_plane_manifests(mc, p)["kube-apiserver"]["spec"]["containers"][0]["args"]
+    a = api_args(base)
+    assert ph.etcd_mode(base) == "embedded" and a[a.index("--data-dir") + 1] == p["data_dir"] and "--etcd-servers" not in a
+    ext = dict(base, etcd={"endpoints": ["https://10.0.0.1:2379", "https://10.0.0.2:2379"], "caFile": "/pki/etcd-ca.crt",
+                           "certFile": "/pki/c.crt", "keyFile": "/pki/c.key"})
+    a = api_args(ext)
+    assert ph.etcd_mode(ext) == "external" and "--data-dir" not in a
+    assert a[a.index("--etcd-servers") + 1] == "https://10.0.0.1:2379,https://10.0.0.2:2379"
+    assert [a[a.index(f) + 1] for f in ("--etcd-cafile", "--etcd-certfile", "--etcd-keyfile")] == \
+        ["/pki/etcd-ca.crt", "/pki/c.crt", "/pki/c.key"]
+    loc = dict(base, etcd={"dataDir": "/var/lib/etcd", "extraArgs": {"snapshot-count": "10000"}})
+    a = api_args(loc)
+    assert ph.etcd_mode(loc) == "local" and a[a.index("--etcd-servers") + 1] == "http://127.0.0.1:2379"
+    e = ph.etcd_manifest(loc)["spec"]["containers"][0]["args"]
+    assert e[:2] == ["-m", "amdkube"] and e[2] == "etcd" and e[e.index("--data-dir") + 1] == "/var/lib/etcd"
+    assert e[e.index("--snapshot-count") + 1] == "10000"
