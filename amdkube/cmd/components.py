@@ -115,6 +115,9 @@ def apiserver(argv):
                     help="unauthenticated listener next to --secure-port (alone: the main listener)")
     ap.add_argument("--insecure-bind-address", default="127.0.0.1")
     ap.add_argument("--data-dir", default=None, help="MVCC store WAL/snapshot directory (etcd replacement)")
+    ap.add_argument("--data-dir-lock-wait", type=float, default=10.0,
+                    help="seconds to wait for another process to release --data-dir (a self-hosted apiserver "
+                         "taking over from its static Pod waits for the hand-off)")
     ap.add_argument("--admission-control", default=None, help="ordered, comma-separated admission plugins")
     ap.add_argument("--resource-v2-resources", default="amd.com/gpu", help="container limits ResourceV2 converts")
     ap.add_argument("--token-auth-file", default=None)
@@ -254,7 +257,7 @@ def apiserver(argv):
             store = await asyncio.to_thread(Etcd3Store, a.etcd_servers, ca=a.etcd_cafile, cert=a.etcd_certfile,
                                             key=a.etcd_keyfile, transformer=transformer)
         else:
-            store = MVCCStore(a.data_dir, transformer=transformer)
+            store = await asyncio.to_thread(MVCCStore, a.data_dir, transformer=transformer, lock_wait=a.data_dir_lock_wait)
         srv = APIServer(store, admission_plugins=(a.admission_control.split(",") if a.admission_control else DEFAULT_CHAIN),
                         admission_config={"ResourceV2": {"resource_names": tuple(a.resource_v2_resources.split(","))}},
                         token_auth=tokens, authorization_mode=a.authorization_mode, anonymous_auth=a.anonymous_auth == "true",

@@ -262,6 +262,10 @@ async def _post_init(mc, cfg, timeout, skip_addons):
             done = await ph.phase_addons(c, mc, cfg)
             print(f"[addons] Applied essential addons: {', '.join(done)} (the AMD GPU device plugin runs on nodes "
                   f"labelled {GPU_LABEL})")
+        if (mc.get("featureGates") or {}).get("SelfHosting"):
+            from .selfhosting import create_self_hosted_control_plane
+            print("[self-hosted] Creating self-hosted control plane.")
+            await create_self_hosted_control_plane(c, cfg["manifests"], mc["nodeName"], timeout)
         return 0
     finally:
         await c.close()

@@ -19,6 +19,8 @@ of them on its own, against the same --base-dir and --config:
   upload-config    the MasterConfiguration in kube-system/kubeadm-config (read back by
                    `kubeadm config view` and `kubeadm upgrade`)
   addon            kube-proxy, kube-dns, amd-gpu-device-plugin
+  selfhosting      convert-from-staticpods: the control plane as DaemonSets (selfhosting.py);
+                   `init --feature-gates SelfHosting=true` runs it last
 
 The MasterConfiguration (kubeadm.k8s.io/v1alpha1) is built from flags or read from --config;
 its api/networking/nodeName/kubernetesVersion/certificatesDir/apiServerCertSANs/
@@ -286,7 +288,10 @@ def control_plane_manifests(mc: dict, p: dict) -> dict[str, dict]:
     if mc["networking"].get("podSubnet"):
         cm += ["--allocate-node-cidrs", "true", "--cluster-cidr", mc["networking"]["podSubnet"]]
     sched = ["--kubeconfig", f"{k}/scheduler.conf", "--leader-elect", "true", "--port", "0"]
-    gates = ",".join(f"{g}={str(v).lower()}" for g, v in sorted((mc.get("featureGates") or {}).items()))
+    from ..utils.features import KNOWN
+    # kubeadm's own gates (SelfHosting, StoreCertsInSecrets, HighAvailability, CoreDNS) stay
+    # with kubeadm (cmd/kubeadm/app/features); only component gates reach the scheduler
+    gates = ",".join(f"{g}={str(v).lower()}" for g, v in sorted((mc.get("featureGates") or {}).items()) if g in KNOWN)
     out = {}
     for name, comp, args, extra in (("kube-apiserver", "apiserver", api, mc.get("apiServerExtraArgs") or {}),
                                     ("kube-controller-manager", "controller-manager", cm, mc.get("controllerManagerExtraArgs") or {}),
@@ -478,7 +483,9 @@ async def phase_addons(c, mc: dict, p: dict, which: str = "all") -> list[str]:
 def add_phase_parser(sub):
     ph = sub.add_parser("phase", help="run one phase of kubeadm init")
     ph.add_argument("phase", choices=("preflight", "certs", "kubeconfig", "controlplane", "etcd", "mark-master",
-                                      "bootstrap-token", "upload-config", "addon"))
+                                      "bootstrap-token", "upload-config", "addon", "selfhosting"))
+    ph.add_argument("--dry-run", action="store_true", help="selfhosting: print the DaemonSets instead")
+    ph.add_argument("--timeout", type=float, default=120.0)
     ph.add_argument("sub", nargs="*", default=[])
     ph.add_argument("--base-dir", default="/etc/kubernetes")
     ph.add_argument("--config", default=None)
@@ -552,6 +559,14 @@ def run_phase(a) -> int:
                 return 0
             if a.phase == "addon":
                 print(f"[addons] Applied: {', '.join(await phase_addons(c, mc, p, sub))}")
+                return 0
+            if a.phase == "selfhosting":
+                if sub not in ("all", "convert-from-staticpods"):
+                    raise SystemExit("error: the selfhosting phase is `selfhosting convert-from-staticpods`")
+                from .selfhosting import create_self_hosted_control_plane
+                done = await create_self_hosted_control_plane(c, p["manifests"], mc["nodeName"], a.timeout, a.dry_run)
+                if not a.dry_run:
+                    print(f"[self-hosted] Converted {', '.join(done) or 'nothing (no static control-plane Pods left)'}")
                 return 0
         finally:
             await c.close()

@@ -15,6 +15,7 @@ app/phases/upgrade/{policy,staticpods,postupgrade,versiongetter}.go).
 from __future__ import annotations
 
 import asyncio
+import json
 import os
 import re
 import shutil
@@ -24,7 +25,7 @@ import time
 import yaml
 
 from .. import GIT_VERSION
-from . import _client, _wait_healthy, write_yaml
+from . import _client, _wait_healthy, selfhosting, write_yaml
 from .phases import (VERSION_ANNOTATION, control_plane_manifests, load_config_file, merge_config, paths, phase_addons,
                      phase_bootstrap_token, phase_upload_config, read_cluster_config)
 
@@ -166,6 +167,13 @@ async def apply(a) -> int:
         print(f"[upgrade/staticpods] Writing new Static Pod manifests to {p['manifests']} (backup in {backup})")
         for comp in COMPONENTS:
             path = os.path.join(p["manifests"], f"{comp}.yaml")
+            ds = await c.get_or_none("daemonsets.apps", selfhosting.PREFIX + comp, "kube-system")
+            if ds is not None and not os.path.exists(path):
+                # a self-hosted component: roll its DaemonSet (selfhosted upgrade path) instead of a manifest
+                rc = await _upgrade_self_hosted(c, comp, ds, manifests[comp], a.timeout)
+                if rc:
+                    return rc
+                continue
             mirror = await _mirror(c, comp, node)
             old_hash = ((mirror or {}).get("metadata", {}).get("annotations") or {}).get(_MIRROR)
             if os.path.exists(path):
@@ -194,6 +202,26 @@ async def apply(a) -> int:
         return 0
     finally:
         await c.close()
+
+
+async def _upgrade_self_hosted(c, comp: str, ds: dict, manifest: dict, timeout: float) -> int:
+    new = selfhosting.build_daemonset(comp, json.loads(json.dumps(manifest.get("spec") or {})))
+    if ds["spec"]["template"]["spec"] == new["spec"]["template"]["spec"]:
+        print(f"[upgrade/selfhosted] {comp} is unchanged")
+        return 0
+    ds["spec"]["template"] = new["spec"]["template"]
+    await selfhosting.create_or_update_daemonset(c, dict(ds, apiVersion="apps/v1", kind="DaemonSet"))
+    want = new["spec"]["template"]["spec"]["containers"][0].get("args")
+
+    async def rolled():
+        pods, _ = await c.list("pods", "kube-system", label_selector=f"k8s-app={selfhosting.PREFIX}{comp}")
+        return bool(pods) and all(p["spec"]["containers"][0].get("args") == want
+                                  and (p.get("status") or {}).get("phase") == "Running" for p in pods)
+    if not await selfhosting._poll(rolled, timeout) or not await selfhosting._poll(lambda: selfhosting.api_healthy(c), timeout):
+        print(f"[upgrade/selfhosted] {comp} did not roll out in {timeout:.0f}s", file=sys.stderr)
+        return 1
+    print(f"[upgrade/selfhosted] Component {comp} upgraded successfully (DaemonSet {selfhosting.PREFIX}{comp})")
+    return 0
 
 
 def add_parser(sub):

@@ -68,6 +68,100 @@ def _rev(o) -> int:
         return 0
 
 
+async def _owned_revisions(c, obj) -> list[dict]:
+    """The ControllerRevisions a DaemonSet or StatefulSet recorded, oldest first."""
+    items, _ = await c.list("controllerrevisions.apps", m.namespace_of(obj))
+    uid = m.uid_of(obj)
+    return sorted((r for r in items if (m.controller_ref(r) or {}).get("uid") == uid), key=lambda r: int(r.get("revision", 0)))
+
+
+def _revision_template(r) -> dict:
+    return json.loads(json.dumps(((r.get("data") or {}).get("spec") or {}).get("template") or {}))
+
+
+async def _rollout_history_based(c, a, sub, ri, name, ns, res):
+    """rollout history/undo/status of DaemonSets and StatefulSets (pkg/kubectl/history.go
+    DaemonSetHistoryViewer/StatefulSetHistoryViewer, rollback.go, rollout_status.go)."""
+    kind = ri.kind
+    if sub == "history":
+        obj = await c.get(res, name, ns)
+        revs = await _owned_revisions(c, obj)
+        if a.revision:
+            r = next((x for x in revs if int(x.get("revision", 0)) == a.revision), None)
+            if r is None:
+                raise SystemExit(f"error: unable to find the specified revision {a.revision}")
+            print(f'{kind.lower()}s "{name}" with revision #{a.revision}')
+            print(dump_yaml({"Pod Template": _revision_template(r)}), end="")
+            return 0
+        rows = [["REVISION", "CHANGE-CAUSE"]]
+        for r in revs:
+            rows.append([str(r.get("revision", 0)), ((r.get("metadata") or {}).get("annotations") or {}).get(CHANGE_CAUSE, "<none>")])
+        print(f'{kind.lower()}s "{name}"')
+        print(printers.table(rows))
+        return 0
+    if sub == "undo":
+        obj = await c.get(res, name, ns)
+        revs = await _owned_revisions(c, obj)
+        if a.to_revision:
+            target = next((r for r in revs if int(r.get("revision", 0)) == a.to_revision), None)
+            if target is None:
+                raise SystemExit(f"error: unable to find specified revision {a.to_revision} in history")
+        else:
+            if len(revs) < 2:
+                raise SystemExit("error: no last revision to roll back to")
+            target = revs[-2]
+        tpl = _revision_template(target)
+        if tpl == ((obj.get("spec") or {}).get("template") or {}):
+            print(f"{kind.lower()}.apps/{name} skipped rollback (current template already matches revision "
+                  f"{target.get('revision')})")
+            return 0
+        obj["spec"]["template"] = tpl
+        await c.update(dict(obj, apiVersion=obj.get("apiVersion") or "apps/v1", kind=kind))
+        print(f"{kind.lower()}.apps/{name} rolled back")
+        return 0
+    end = time.time() + a.timeout
+    while True:
+        obj = await c.get(res, name, ns)
+        spec, st = obj.get("spec") or {}, obj.get("status") or {}
+        gen = (obj.get("metadata") or {}).get("generation", 1)
+        strategy = (spec.get("updateStrategy") or {}).get("type", "RollingUpdate")
+        if strategy != "RollingUpdate":
+            raise SystemExit("error: Status is available only for RollingUpdate strategy type" if kind == "DaemonSet"
+                             else f"error: {strategy} updateStrategy does not have a Status")
+        done = False
+        if int(st.get("observedGeneration", 0)) < gen:
+            msg = f"Waiting for {'daemon set' if kind == 'DaemonSet' else 'statefulset'} spec update to be observed..."
+        elif kind == "DaemonSet":
+            want, upd, av = (int(st.get(k, 0)) for k in ("desiredNumberScheduled", "updatedNumberScheduled", "numberAvailable"))
+            if upd < want:
+                msg = f"Waiting for rollout to finish: {upd} out of {want} new pods have been updated..."
+            elif av < want:
+                msg = f"Waiting for rollout to finish: {av} of {want} updated pods are available..."
+            else:
+                msg, done = f'daemon set "{name}" successfully rolled out', True
+        else:
+            want, ready, upd = int(spec.get("replicas", 1)), int(st.get("readyReplicas", 0)), int(st.get("updatedReplicas", 0))
+            part = int(((spec.get("updateStrategy") or {}).get("rollingUpdate") or {}).get("partition", 0))
+            if ready < want:
+                msg = f"Waiting for {want - ready} pods to be ready..."
+            elif part > 0:
+                if upd < want - part:
+                    msg = f"Waiting for partitioned roll out to finish: {upd} out of {want - part} new pods have been updated..."
+                else:
+                    msg, done = f"partitioned roll out complete: {upd} new pods have been updated...", True
+            elif st.get("updateRevision") != st.get("currentRevision"):
+                msg = f"waiting for statefulset rolling update to complete {upd} pods at revision {st.get('updateRevision')}..."
+            else:
+                msg, done = f"statefulset rolling update complete {ready} pods at revision {st.get('currentRevision')}...", True
+        if done:
+            print(msg)
+            return 0
+        if not a.watch_status or time.time() > end:
+            print(msg)
+            return 1
+        await asyncio.sleep(0.2)
+
+
 async def cmd_rollout(c, a):
     if not a.args:
         raise SystemExit("error: rollout needs a subcommand: status|history|undo|pause|resume")
@@ -75,6 +169,11 @@ async def cmd_rollout(c, a):
     ri, name, _ = _target(a, 1)
     ns = _ns(a, ri)
     res = _res(ri)
+    if ri.kind in ("DaemonSet", "StatefulSet"):
+        if sub in ("pause", "resume"):
+            raise SystemExit(f"error: {ri.plural} \"{name}\" is not supported ({sub} works on deployments)")
+        if sub in ("history", "undo", "status"):
+            return await _rollout_history_based(c, a, sub, ri, name, ns, res)
     if sub == "pause" or sub == "resume":
         await c.patch(res, name, {"spec": {"paused": sub == "pause" or None}}, ns)
         print(f"{ri.kind.lower()}/{name} {'paused' if sub == 'pause' else 'resumed'}")
@@ -800,6 +899,7 @@ COMMANDS = {"rollout": cmd_rollout, "expose": cmd_expose, "autoscale": cmd_autos
 
 def add_arguments(sp):
     sp.add_argument("--to-revision", type=int, default=0)
+    sp.add_argument("--revision", type=int, default=0, help="rollout history: show this revision's template")
     sp.add_argument("--watch-status", type=lambda s: s != "false", default=True)
     sp.add_argument("--port", default=None)
     sp.add_argument("--target-port", default=None)

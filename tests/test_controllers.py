@@ -265,3 +265,65 @@ async def _tainted(lc, name):
 async def _deleted(c, name):
     p = await c.get_or_none("pods", name, "default")
     return p is None or bool(p["metadata"].get("deletionTimestamp"))
+
+
+def test_daemonset_rolling_update_history_and_undo(capsys):
+    """RollingUpdate (maxUnavailable 1): a new template replaces every node's pod, never more
+    than one node without an available pod; every template is a ControllerRevision, and
+    `kubectl rollout history/undo/status daemonset` work over them (update.go, history.go)."""
+    from amdkube.kubectl.main import main as kubectl
+
+    async def go():
+        async with LocalCluster(gpus="none", relist_period=0.2) as lc:
+            c = lc.client
+            hollow = [await HollowNode(lc.api.url, f"hollow-{i}", gpus=0).start() for i in range(3)]
+            try:
+                await c.create({"apiVersion": "apps/v1", "kind": "DaemonSet", "metadata": {"name": "agent", "namespace": "default"},
+                                "spec": {"selector": {"matchLabels": {"app": "agent"}}, "template": tpl({"app": "agent"}),
+                                         "updateStrategy": {"type": "RollingUpdate", "rollingUpdate": {"maxUnavailable": 1}}}})
+
+                async def rolled(want_label):
+                    ds = await c.get("daemonsets.apps", "agent", "default")
+                    st = ds.get("status") or {}
+                    pods, _ = await c.list("pods", "default", label_selector="app=agent")
+                    live = [p for p in pods if not p["metadata"].get("deletionTimestamp")]
+                    ok = (st.get("updatedNumberScheduled") == st.get("numberAvailable") == st.get("desiredNumberScheduled") == 4
+                          and len(live) == 4 and all(m.labels_of(p).get("v") == want_label for p in live)
+                          and st.get("observedGeneration") == ds["metadata"].get("generation"))
+                    return ok and live
+                first = await until(lambda: rolled(None), 40)
+                h1 = {m.labels_of(p)["controller-revision-hash"] for p in first}
+                assert len(h1) == 1
+                # watch availability while the template changes
+                worst = [0]
+
+                async def sample():
+                    while True:
+                        ds = await c.get("daemonsets.apps", "agent", "default")
+                        worst[0] = max(worst[0], int((ds.get("status") or {}).get("numberUnavailable", 0)))
+                        await asyncio.sleep(0.02)
+                sampler = asyncio.create_task(sample())
+                await c.patch("daemonsets.apps", "agent", {"spec": {"template": {"metadata": {"labels": {"app": "agent", "v": "2"}}}}},
+                              "default", patch_type="application/strategic-merge-patch+json")
+                second = await until(lambda: rolled("2"), 60)
+                sampler.cancel()
+                assert worst[0] <= 1, worst
+                assert {m.labels_of(p)["controller-revision-hash"] for p in second}.isdisjoint(h1)
+                revs, _ = await c.list("controllerrevisions.apps", "default")
+                assert sorted(r["revision"] for r in revs if (m.controller_ref(r) or {}).get("name") == "agent") == [1, 2]
+                kc = ["--server", lc.api.url, "--token", lc.api.loopback_token, "-n", "default"]
+                assert await asyncio.to_thread(kubectl, kc + ["rollout", "history", "daemonset/agent"]) == 0
+                assert await asyncio.to_thread(kubectl, kc + ["rollout", "status", "daemonset/agent"]) == 0
+                assert await asyncio.to_thread(kubectl, kc + ["rollout", "undo", "daemonset/agent"]) == 0
+                third = await until(lambda: rolled(None), 60)
+                assert {m.labels_of(p)["controller-revision-hash"] for p in third} == h1
+                revs, _ = await c.list("controllerrevisions.apps", "default")
+                assert sorted((r["revision"], r["metadata"]["labels"]["controller-revision-hash"] in h1) for r in revs
+                              if (m.controller_ref(r) or {}).get("name") == "agent") == [(2, False), (3, True)]
+            finally:
+                for h in hollow:
+                    await h.stop()
+    run(go(), 200)
+    out = capsys.readouterr().out
+    assert 'daemonsets "agent"' in out and "REVISION" in out and 'daemon set "agent" successfully rolled out' in out
+    assert "daemonset.apps/agent rolled back" in out

@@ -207,3 +207,53 @@ def test_kubeadm_store_modes():
     e = ph.etcd_manifest(loc)["spec"]["containers"][0]["args"]
     assert e[:2] == ["-m", "amdkube"] and e[2] == "etcd" and e[e.index("--data-dir") + 1] == "/var/lib/etcd"
     assert e[e.index("--snapshot-count") + 1] == "10000"
+
+
+def test_kubeadm_self_hosting(tmp_path):
+    """--feature-gates SelfHosting=true: the static control plane becomes DaemonSets
+    self-hosted-kube-{apiserver,controller-manager,scheduler} (selfhosting.go); the static
+    manifests and their mirror pods go, the self-hosted apiserver takes over the embedded
+    store's data directory, and the cluster keeps its objects and keeps working."""
+    base = str(tmp_path / "master")
+    port = _free_port()
+    try:
+        r = _kubeadm("init", "--base-dir", base, "--apiserver-bind-port", str(port), "--node-name", "master-0",
+                     "--start-kubelet", "--kubelet-port", "0", "--skip-addons", "--feature-gates", "SelfHosting=true",
+                     "--timeout", "120", timeout=300)
+        assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-3000:]
+        for comp in ("kube-apiserver", "kube-controller-manager", "kube-scheduler"):
+            assert f"self-hosted {comp} ready" in r.stdout, r.stdout[-3000:]
+            assert not os.path.exists(os.path.join(base, "manifests", f"{comp}.yaml"))
+
+        async def check():
+            c = Client.from_kubeconfig(os.path.join(base, "admin.conf"))
+            try:
+                pods = {m.name_of(p): p for p in (await c.list("pods", "kube-system"))[0]}
+                assert not {"kube-apiserver-master-0", "kube-controller-manager-master-0", "kube-scheduler-master-0"} & set(pods)
+                for comp in ("kube-apiserver", "kube-controller-manager", "kube-scheduler"):
+                    ds = await c.get("daemonsets.apps", f"self-hosted-{comp}", "kube-system")
+                    spec = ds["spec"]["template"]["spec"]
+                    assert spec["nodeSelector"] == {"node-role.kubernetes.io/master": ""} and spec["dnsPolicy"] == "ClusterFirstWithHostNet"
+                    mine = [p for p in pods.values() if m.labels_of(p).get("k8s-app") == f"self-hosted-{comp}"]
+                    assert len(mine) == 1 and mine[0]["status"]["phase"] == "Running"
+                # objects written before the hand-off are still there; the scheduler and the
+                # controller-manager of the self-hosted plane still act
+                assert await c.get_or_none("configmaps", "kubeadm-config", "kube-system") is not None
+                await c.create({"apiVersion": "apps/v1", "kind": "ReplicaSet", "metadata": {"name": "after", "namespace": "kube-system"},
+                                "spec": {"replicas": 1, "selector": {"matchLabels": {"app": "after"}},
+                                         "template": {"metadata": {"labels": {"app": "after"}},
+                                                      "spec": {"tolerations": [{"key": "node-role.kubernetes.io/master", "effect": "NoSchedule"}],
+                                                               "containers": [{"name": "c", "image": "amdkube/pause:3.1"}]}}}},
+                               "kube-system")
+                end = asyncio.get_running_loop().time() + 60
+                while asyncio.get_running_loop().time() < end:
+                    ps, _ = await c.list("pods", "kube-system", label_selector="app=after")
+                    if ps and ps[0]["spec"].get("nodeName") == "master-0" and ps[0]["status"].get("phase") == "Running":
+                        return
+                    await asyncio.sleep(0.3)
+                raise AssertionError("a pod created after self-hosting was not scheduled and started")
+            finally:
+                await c.close()
+        asyncio.run(check())
+    finally:
+        _kubeadm("reset", "--base-dir", base, "--drain-seconds", "1.5")
