@@ -151,6 +151,8 @@ class PeerServer:
             while True:
                 frame = await _read_frame(reader)
                 kind, cid = frame[0], struct.unpack_from(">I", frame, 1)[0]
+                if kind == REQ and (len(frame) < 6 or len(frame) < 6 + frame[5]):
+                    raise ConnectionError("truncated request frame")
                 if kind == CMSG or kind == CANCEL:
                     ent = streams.get(cid)
                     if ent is not None:
@@ -162,7 +164,7 @@ class PeerServer:
                 if kind != REQ:
                     raise ConnectionError("peer sent a non-request frame")
                 plen = frame[5]
-                path = frame[6:6 + plen].decode()
+                path = frame[6:6 + plen].decode(errors="replace")
                 sm = self.streams.get(path)
                 if sm is not None:
                     q: asyncio.Queue = asyncio.Queue()
@@ -178,6 +180,8 @@ class PeerServer:
             pass
         except asyncio.CancelledError:
             pass
+        except Exception as e:       # noqa: BLE001 — a malformed message ends this connection only
+            log.debug("peer connection dropped: %r", e)
         finally:
             for t in list(inflight):
                 t.cancel()

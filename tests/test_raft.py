@@ -315,3 +315,41 @@ async def test_peer_listener_serves_only_member_traffic_under_mutual_tls(tmp_pat
     finally:
         for s in srvs.values():
             await s.stop()
+
+
+async def test_peerwire_server_survives_malformed_frames():
+    """Garbage on a peerwire listener (truncated, oversized, undecodable, unknown kinds) ends
+    that connection only; the server keeps answering well-formed calls."""
+    import random
+    import struct
+    from amdkube.grpcdesc.etcd import ETCD as E
+    from amdkube.store.etcdserver import EtcdServer
+    from amdkube.store.mvcc import MVCCStore
+    from amdkube.store.peerwire import SyncChannel
+    srv = await EtcdServer(MVCCStore()).start("127.0.0.1:0", None, None, "127.0.0.1:0")
+    rnd = random.Random(7)
+    try:
+        good = E.PutRequest(key=b"/k", value=b"v").SerializeToString()
+        path = b"/etcdserverpb.KV/Put"
+        frames = [b"\x00\x00\x00\x05\x00\x00\x00\x00\x01",                          # REQ without a path length
+                  b"\x00\x00\x00\x06\x00\x00\x00\x00\x01\xff",                      # path longer than the frame
+                  b"\xff\xff\xff\xff",                                              # oversized
+                  struct.pack(">IBIB", 6 + len(path) + 3, 0, 1, len(path)) + path + b"\xff\xff\xff",   # undecodable body
+                  struct.pack(">IBIB", 6 + 9, 0, 2, 9) + b"/\xff\xfe\x00x/yz",     # non-UTF-8 path
+                  struct.pack(">IBI", 5, 9, 3),                                      # unknown kind
+                  struct.pack(">IBIB", 6 + 26, 0, 4, 26) + b"/etcdserverpb.Watch/Watch" + b"\x0a\xff"]   # bad stream opener
+        frames += [bytes(rnd.getrandbits(8) for _ in range(rnd.randint(1, 64))) for _ in range(40)]
+        for f in frames:
+            r, w = await asyncio.open_connection("127.0.0.1", srv.wire_port)
+            w.write(f)
+            try:
+                await asyncio.wait_for(r.read(1 << 16), 1.0)
+            except (asyncio.TimeoutError, ConnectionError):
+                pass
+            w.close()
+        ch = SyncChannel(f"127.0.0.1:{srv.wire_port}")
+        resp = E.PutResponse.FromString(await asyncio.to_thread(ch.call, "/etcdserverpb.KV/Put", good, 5))
+        assert resp.header.revision >= 1
+        ch.close()
+    finally:
+        await srv.stop()
