@@ -442,6 +442,12 @@ class Kubelet:
         # service environment variables (kubelet.go serviceLister)
         self.svc_informer = Informer(self.client, "services")
         self.svc_informer.start()
+        # this node's own object, as the reference's node lister (kubelet.go nodeInfo): labels a
+        # controller sets (the master label, a DaemonSet's nodeSelector target) reach admission
+        # at once instead of at the next status update
+        self.node_informer = Informer(self.client, "nodes", field_selector=f"metadata.name={self.node_name}")
+        self.node_informer.add_handler(on_add=self._on_node, on_update=lambda old, new: self._on_node(new))
+        self.node_informer.start()
         self.informer = Informer(self.client, "pods", field_selector=f"spec.nodeName={self.node_name}")
         self.informer.add_handler(on_add=self._on_pod_add, on_update=self._on_pod_update, on_delete=self._on_pod_delete)
         self.informer.start()
@@ -451,6 +457,15 @@ class Kubelet:
         self._tasks.append(asyncio.create_task(self._node_status_loop(), name="node-status"))
         self._static_dirty.set()   # create mirror pods now that the API is there
 
+    def _on_node(self, node: dict):
+        cur = self.node or {}
+        try:
+            newer = int(m.rv_of(node) or 0) >= int(m.rv_of(cur) or 0)
+        except ValueError:
+            newer = True
+        if newer:
+            self.node = node
+
     async def stop(self):
         from ..utils import cancel_and_wait
         await cancel_and_wait(self._tasks)
@@ -459,6 +474,8 @@ class Kubelet:
             await self.informer.stop()
         if self.svc_informer is not None:
             await self.svc_informer.stop()
+        if getattr(self, "node_informer", None) is not None:
+            await self.node_informer.stop()
         await cancel_and_wait([w.task for w in self.workers.values()])
         if self._ckpt_chain is not None:
             await asyncio.wait({self._ckpt_chain}, timeout=5)     # queued bootstrap-checkpoint writes land

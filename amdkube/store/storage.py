@@ -173,7 +173,7 @@ def field_trigger(fields_fn: Callable, field: str) -> Callable:
 
 class Storage:
     # fields whose exact-match watches are indexed (cacher.go: pods by spec.nodeName)
-    TRIGGER_FIELDS = ("spec.nodeName",)
+    TRIGGER_FIELDS = ("spec.nodeName", "metadata.name")      # + each kubelet's watch of its own Node
 
     def __init__(self, store: MVCCStore, resource: str = "object", media_type: str = JSON_MEDIA_TYPE):
         self.store = store
