@@ -118,22 +118,32 @@ class StatefulSetController(Controller):
                     raise
 
     async def _revision(self, sts) -> str:
-        """Record the template as a ControllerRevision (history.go) and return its hash."""
+        """Record the template as the newest ControllerRevision (history.go) and return its hash:
+        a new template gets one past the highest revision, a template that comes back (a
+        rollback) has its old revision renumbered to the newest."""
         tpl = (sts.get("spec") or {}).get("template") or {}
         h = template_hash(tpl)
+        uid = m.uid_of(sts)
+        cache = self.__dict__.setdefault("_recorded", {})
+        if cache.get(uid) == h:
+            return h
         ns, name = m.namespace_of(sts), m.name_of(sts)
-        rname = f"{name}-{h}"
-        if await self.client.get_or_none("controllerrevisions", rname, ns) is None:
+        revs = [r for r in (await self.client.list("controllerrevisions.apps", ns))[0] if (m.controller_ref(r) or {}).get("uid") == uid]
+        top = max((int(r.get("revision", 0)) for r in revs), default=0)
+        mine = next((r for r in revs if m.labels_of(r).get(REVISION_LABEL) == h), None)
+        if mine is None:
             try:
                 await self.client.create({"apiVersion": "apps/v1", "kind": "ControllerRevision",
-                                          "metadata": {"name": rname, "namespace": ns,
+                                          "metadata": {"name": f"{name}-{h}", "namespace": ns,
                                                        "labels": dict(m.labels_of(sts), **{REVISION_LABEL: h}),
                                                        "ownerReferences": [m.new_controller_ref(sts, "apps/v1", "StatefulSet")]},
-                                          "data": {"spec": {"template": tpl}}, "revision": int(sts["metadata"].get("generation", 1))},
-                                         ns)
+                                          "data": {"spec": {"template": tpl}}, "revision": top + 1}, ns)
             except m.StatusError as e:
                 if not m.is_already_exists(e):
                     raise
+        elif int(mine.get("revision", 0)) < top:
+            await self.client.update(dict(mine, apiVersion="apps/v1", kind="ControllerRevision", revision=top + 1))
+        cache[uid] = h
         return h
 
     async def sync(self, key):

@@ -327,3 +327,42 @@ def test_daemonset_rolling_update_history_and_undo(capsys):
     out = capsys.readouterr().out
     assert 'daemonsets "agent"' in out and "REVISION" in out and 'daemon set "agent" successfully rolled out' in out
     assert "daemonset.apps/agent rolled back" in out
+
+
+def test_statefulset_rollout_history_and_undo(capsys):
+    """StatefulSet templates are ControllerRevisions numbered 1, 2, ...; `kubectl rollout undo`
+    brings the previous template back as the newest revision and the pods follow it."""
+    from amdkube.kubectl.main import main as kubectl
+
+    async def go():
+        async with LocalCluster(gpus="none", relist_period=0.2) as lc:
+            c = lc.client
+            await c.create({"apiVersion": "apps/v1", "kind": "StatefulSet", "metadata": {"name": "db", "namespace": "default"},
+                            "spec": {"replicas": 2, "serviceName": "db", "selector": {"matchLabels": {"app": "db"}},
+                                     "template": tpl({"app": "db"})}})
+
+            async def at(label):
+                sts = await c.get("statefulsets.apps", "db", "default")
+                st = sts.get("status") or {}
+                pods, _ = await c.list("pods", "default", label_selector="app=db")
+                live = [p for p in pods if not p["metadata"].get("deletionTimestamp")]
+                return (st.get("readyReplicas") == 2 == st.get("updatedReplicas") and len(live) == 2
+                        and all(m.labels_of(p).get("v") == label for p in live) and st.get("updateRevision") == st.get("currentRevision")
+                        and {m.labels_of(p)["controller-revision-hash"] for p in live})
+            h1 = await until(lambda: at(None), 60)
+            await c.patch("statefulsets.apps", "db", {"spec": {"template": {"metadata": {"labels": {"app": "db", "v": "2"}}}}},
+                          "default", patch_type="application/strategic-merge-patch+json")
+            h2 = await until(lambda: at("2"), 60)
+            assert h1 != h2
+            kc = ["--server", lc.api.url, "--token", lc.api.loopback_token, "-n", "default"]
+            assert await asyncio.to_thread(kubectl, kc + ["rollout", "history", "statefulset/db"]) == 0
+            assert await asyncio.to_thread(kubectl, kc + ["rollout", "undo", "statefulset/db"]) == 0
+            assert await until(lambda: at(None), 60) == h1
+            revs, _ = await c.list("controllerrevisions.apps", "default")
+            mine = sorted((r["revision"], r["metadata"]["labels"]["controller-revision-hash"]) for r in revs
+                          if (m.controller_ref(r) or {}).get("name") == "db")
+            assert [r for r, _ in mine] == [2, 3] and mine[-1][1] in h1
+            assert await asyncio.to_thread(kubectl, kc + ["rollout", "status", "statefulset/db"]) == 0
+    run(go(), 200)
+    out = capsys.readouterr().out
+    assert 'statefulsets "db"' in out and "statefulset.apps/db rolled back" in out and "rolling update complete 2 pods" in out
