@@ -519,7 +519,7 @@ class DaemonSetController(Controller):
             by_node.setdefault((p.get("spec") or {}).get("nodeName", ""), []).append(p)
         mrs = int(spec.get("minReadySeconds", 0))
         now, wake = time.time(), None
-        desired = current = ready = updated = available = 0
+        desired = current = ready = updated = available = misscheduled = 0
         old_avail, old_unavail = [], []
         for node in self.node_inf.list():
             nn = m.name_of(node)
@@ -545,6 +545,7 @@ class DaemonSetController(Controller):
                     for extra in have[1:]:
                         await self.client.delete("pods", m.name_of(extra), ns)
             else:
+                misscheduled += int(bool(have))
                 for p in have:
                     await self.client.delete("pods", m.name_of(p), ns)
             for p in by_node.get(nn, []):
@@ -569,7 +570,7 @@ class DaemonSetController(Controller):
         if wake is not None:
             self.queue.add_after(key, wake + 0.05)
         st = {"desiredNumberScheduled": desired, "currentNumberScheduled": current, "numberReady": ready,
-              "numberMisscheduled": 0, "updatedNumberScheduled": updated, "numberAvailable": available,
+              "numberMisscheduled": misscheduled, "updatedNumberScheduled": updated, "numberAvailable": available,
               "numberUnavailable": desired - available,
               "observedGeneration": (ds.get("metadata") or {}).get("generation", 1)}
         if {k: (ds.get("status") or {}).get(k) for k in st} != st:
