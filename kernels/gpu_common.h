@@ -123,11 +123,17 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ v4u ld_nt(const v4u* p) { return __builtin_nontemporal_load(p); }
 __device__ __forceinline__ void st_nt(v4u* p, v4u v) { __builtin_nontemporal_store(v, p); }
 
-// Pure writes go out with the default cache policy: on MI355X plain 16-B stores stream at
-// 6.0-6.1 TB/s against 5.5-5.8 non-temporal (hack/exp/copy_sweep2.hip, 1 and 4 GiB), best at
-// 16 WG/CU for a 1 GiB buffer. Copies keep nt on both sides and run 128 WG/CU (5.72 / 5.80 TB/s
-// on 1 / 4 GiB against 5.39 / 5.79 at 64).
-constexpr int HBM_WRITE_BLOCKS_PER_CU = 16;
+// Pure writes go out with the default cache policy as a narrow grid-stride "front": half as many
+// workgroups as CUs (128 on MI355X), 256 lanes, two 16-B stores in flight per lane, so the whole
+// chip writes one ~1 MiB window that sweeps the buffer in address order and the HBM sees long
+// runs of consecutive pages. Round-4 sweeps on MI355X, hashed pattern, 1 / 4 GiB
+// (hack/exp/write_sweep4.hip, front_sweep5.hip): front 128 x 2-deep 6.82-6.96 / 6.83-7.09 TB/s,
+// front 96 5.3, front 160 6.1, front 256 5.8-6.0, per-workgroup chunks at 16 WG/CU 5.85 / 5.7,
+// hipMemsetD32 (the runtime's own 256 x 256 front) 6.45-6.75. Copies keep nt on both sides and
+// run chunked at 128 WG/CU (5.72 / 5.80 TB/s on 1 / 4 GiB); fronts did not help them
+// (copy_sweep4.hip: 5.1-5.9).
+constexpr int HBM_WRITE_UNROLL = 2;
+inline int write_front_grid(int cu_count) { return cu_count > 1 ? cu_count / 2 : 1; }
 __device__ __forceinline__ void st_plain(v4u* p, v4u v) { *p = v; }
 
 __device__ __forceinline__ v4u pattern_v(size_t i, uint32_t seed) {
@@ -144,15 +150,13 @@ __device__ __forceinline__ void chunk_of(size_t n16, size_t* lo, size_t* hi) {
 }
 
 __global__ __launch_bounds__(256) void hbm_write_kernel(v4u* __restrict__ buf, size_t n16, uint32_t seed) {
-  size_t lo, hi;
-  chunk_of(n16, &lo, &hi);
-  const size_t b = blockDim.x;
-  size_t i = lo + threadIdx.x;
-  for (; i + (HBM_UNROLL - 1) * b < hi; i += HBM_UNROLL * b) {
+  const size_t st = static_cast<size_t>(gridDim.x) * blockDim.x;
+  size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (; i + (HBM_WRITE_UNROLL - 1) * st < n16; i += HBM_WRITE_UNROLL * st) {
 #pragma unroll
-    for (int u = 0; u < HBM_UNROLL; ++u) st_plain(buf + i + u * b, pattern_v(i + u * b, seed));
+    for (int u = 0; u < HBM_WRITE_UNROLL; ++u) st_plain(buf + i + u * st, pattern_v(i + u * st, seed));
   }
-  for (; i < hi; i += b) st_plain(buf + i, pattern_v(i, seed));
+  for (; i < n16; i += st) st_plain(buf + i, pattern_v(i, seed));
 }
 
 __device__ __forceinline__ unsigned mismatches(v4u v, v4u e) {
@@ -362,7 +366,7 @@ inline std::vector<float> vector_add_host(const std::vector<float>& a, const std
 inline std::vector<uint32_t> hbm_pattern_host(size_t n16, uint32_t seed, int dev) {
   AK_HIP(hipSetDevice(dev));
   DevBuf d(n16 * 16);
-  const int grid = stream_grid(n16, dev_info(dev).cu_count, HBM_WRITE_BLOCKS_PER_CU);
+  const int grid = write_front_grid(dev_info(dev).cu_count);
   hipLaunchKernelGGL(hbm_write_kernel, dim3(grid), dim3(256), 0, 0, static_cast<v4u*>(d.p), n16, seed);
   AK_HIP(hipGetLastError());
   std::vector<uint32_t> out(n16 * 4);
@@ -462,7 +466,7 @@ inline HbmResult run_hbm_probe(size_t bytes, int iters, int dev, uint32_t seed =
     AK_HIP(hipEventElapsedTime(&ms, e0, e1));
     return static_cast<double>(ms) / iters;
   };
-  const int write_grid = stream_grid(n16, info.cu_count, HBM_WRITE_BLOCKS_PER_CU);
+  const int write_grid = write_front_grid(info.cu_count);
   double w = timed([&] { hipLaunchKernelGGL(hbm_write_kernel, dim3(write_grid), dim3(256), 0, 0, a, n16, seed); });
   double rd = timed([&] { hipLaunchKernelGGL(hbm_read_kernel, dim3(grid), dim3(256), 0, 0, a, n16, sink); });
   const int copy_grid = stream_grid(n16, info.cu_count, HBM_COPY_BLOCKS_PER_CU);
