@@ -115,6 +115,8 @@ def apiserver(argv):
                     help="unauthenticated listener next to --secure-port (alone: the main listener)")
     ap.add_argument("--insecure-bind-address", default="127.0.0.1")
     ap.add_argument("--data-dir", default=None, help="MVCC store WAL/snapshot directory (etcd replacement)")
+    ap.add_argument("--store-conflict-chance", type=float, default=0.0,
+                    help="fault injection: share of conditional store writes that fail as a lost race (retried above)")
     ap.add_argument("--data-dir-lock-wait", type=float, default=10.0,
                     help="seconds to wait for another process to release --data-dir (a self-hosted apiserver "
                          "taking over from its static Pod waits for the hand-off)")
@@ -258,6 +260,7 @@ def apiserver(argv):
                                             key=a.etcd_keyfile, transformer=transformer)
         else:
             store = await asyncio.to_thread(MVCCStore, a.data_dir, transformer=transformer, lock_wait=a.data_dir_lock_wait)
+        store.conflict_chance = a.store_conflict_chance
         srv = APIServer(store, admission_plugins=(a.admission_control.split(",") if a.admission_control else DEFAULT_CHAIN),
                         admission_config={"ResourceV2": {"resource_names": tuple(a.resource_v2_resources.split(","))}},
                         token_auth=tokens, authorization_mode=a.authorization_mode, anonymous_auth=a.anonymous_auth == "true",

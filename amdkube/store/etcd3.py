@@ -541,6 +541,8 @@ class Etcd3Store(MVCCStore):
         return self._txn(req.compare, req.success, req.failure)
 
     def put(self, key: str, value, expect_mod_rev: int | None = None) -> KV:
+        if expect_mod_rev:
+            self._inject_conflict(self.kv.get(key))
         if self._loop is not None and greenbridge.bridged():
             _, rev, data = greenbridge.await_only(self._submit_op(key, value, expect_mod_rev, False))
         else:
@@ -551,6 +553,8 @@ class Etcd3Store(MVCCStore):
         return KV(key, data, got.create_rev if got else rev, rev, 0)     # already replaced in the replica
 
     def delete(self, key: str, expect_mod_rev: int | None = None) -> KV:
+        if expect_mod_rev:
+            self._inject_conflict(self.kv.get(key))
         if self._loop is not None and greenbridge.bridged():
             r, _, _ = greenbridge.await_only(self._submit_op(key, None, expect_mod_rev, True))
         else:

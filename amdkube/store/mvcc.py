@@ -24,6 +24,7 @@ import collections
 import fcntl
 import json
 import os
+import random
 import threading
 import time
 
@@ -207,6 +208,11 @@ class MVCCStore:
         # value transformer between memory and disk (encryption at rest): to_disk(key, bytes),
         # from_disk(key, bytes); None keeps the bytes as they are
         self.transformer = transformer
+        # fault injection: this share of conditional writes whose precondition holds
+        # fails as if another writer had won the race, so every GuaranteedUpdate-style retry
+        # loop above the store gets exercised (apiserver --store-conflict-chance)
+        self.conflict_chance = 0.0
+        self.injected_conflicts = 0
         self._dir_lock = None
         if data_dir:
             self._dir_lock = lock_data_dir(data_dir, lock_wait)
@@ -286,6 +292,8 @@ class MVCCStore:
                     if cur is None:
                         raise KeyNotFound(key)
                     raise CASFailed(cur)
+                if expect_mod_rev:
+                    self._inject_conflict(cur)
             rev = self.rev + 1
             data = value(rev) if callable(value) else value
             new = KV(key, data, cur.create_rev if cur else rev, rev, (cur.version + 1) if cur else 1)
@@ -295,6 +303,11 @@ class MVCCStore:
             self._commit(Event(PUT, new, cur, rev), {"r": rev, "o": "p", "k": key, "v": data} if self._wal is not None else None)
             return new
 
+    def _inject_conflict(self, cur):
+        if self.conflict_chance and cur is not None and random.random() < self.conflict_chance:
+            self.injected_conflicts += 1
+            raise CASFailed(cur)
+
     def delete(self, key: str, expect_mod_rev: int | None = None) -> KV:
         with self._lock:
             cur = self.kv.get(key)
@@ -302,6 +315,8 @@ class MVCCStore:
                 raise KeyNotFound(key)
             if expect_mod_rev and cur.mod_rev != expect_mod_rev:
                 raise CASFailed(cur)
+            if expect_mod_rev:
+                self._inject_conflict(cur)
             rev = self.rev + 1
             self.rev = rev
             del self.kv[key]

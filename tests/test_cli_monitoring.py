@@ -242,3 +242,43 @@ def test_chaos_client_and_informer_recovery():
             await good.close()
             await srv.stop()
     run(go(), 60)
+
+
+def test_store_conflict_injection_exercises_retry_loops():
+    """--store-conflict-chance: half the conditional writes lose a simulated race; updates,
+    patches, status writes, bindings and deletes still succeed through the apiserver's
+    GuaranteedUpdate retries, and a precondition that really is stale is still a 409."""
+    from amdkube.api import meta as m
+    from amdkube.store import MVCCStore
+    store = MVCCStore()
+    store.conflict_chance = 0.5
+
+    async def go():
+        srv = await APIServer(store).start()
+        c = Client(srv.url, token=srv.loopback_token)
+        try:
+            cm = await c.create({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "x", "namespace": "default"},
+                                 "data": {"n": "0"}}, "default")
+            for i in range(1, 21):
+                cm["data"]["n"] = str(i)
+                cm = await c.update(cm)
+                await c.patch("configmaps", "x", {"metadata": {"labels": {"i": str(i)}}}, "default")
+                cm = await c.get("configmaps", "x", "default")
+            assert cm["data"]["n"] == "20" and cm["metadata"]["labels"]["i"] == "20"
+            stale = dict(cm, metadata=dict(cm["metadata"], resourceVersion="1"))
+            with pytest.raises(m.StatusError) as ei:
+                await c.update(stale)
+            assert ei.value.code == 409
+            await c.create({"apiVersion": "v1", "kind": "Node", "metadata": {"name": "n1"},
+                            "status": {"capacity": {"cpu": "4", "memory": "4Gi", "pods": "10"}}})
+            await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p", "namespace": "default"},
+                            "spec": {"containers": [{"name": "c", "image": "busybox"}]}}, "default")
+            await c.bind("default", "p", "n1")
+            assert (await c.get("pods", "p", "default"))["spec"]["nodeName"] == "n1"
+            await c.delete("configmaps", "x", "default")
+            assert await c.get_or_none("configmaps", "x", "default") is None
+            assert store.injected_conflicts >= 10
+        finally:
+            await c.close()
+            await srv.stop()
+    run(go(), 60)
