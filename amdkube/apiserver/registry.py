@@ -20,6 +20,7 @@ import json
 import time
 
 from ..api import meta as m
+from ..utils.trace import POD_TRACE
 from ..api.helpers import (HEALTHY, pod_assigned_devices, pod_extended_resource_count, pod_extended_resource_name,
                            ExtendedResourceError, set_condition, is_pod_terminal)
 from ..api.labels import parse_field_selector, parse_selector
@@ -245,7 +246,10 @@ class ResourceStore:
         self.api.admission.validate(attrs, self.api)
         if dry_run:
             return obj
-        return self.storage.create(self.key(md.get("namespace", ""), md["name"]), obj)
+        out = self.storage.create(self.key(md.get("namespace", ""), md["name"]), obj)
+        if self.ri.plural == "pods":
+            POD_TRACE(md.get("uid", ""), "api_created")
+        return out
 
     def prepare_for_create(self, obj):
         p = self.ri.plural

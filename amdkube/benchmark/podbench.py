@@ -250,9 +250,6 @@ class PodBench:
         step ends when every pause pod is Running and every GPU pod has Succeeded. The previous
         step's pause pods are deleted while this one runs."""
         old, self.pending_cleanup = self.pending_cleanup, []
-        for nm in old:
-            self.deleting.add(nm)
-            asyncio.create_task(self._delete(nm))
         gpu, cpu = [], []
         for _ in range(self.n):
             self.seq += 1
@@ -273,6 +270,13 @@ class PodBench:
                 creates.append(self.lc.client.create(self.pod(nm) if nm in gpu else self.cpu_pod(nm), "default"))
             for obj in await asyncio.gather(*creates):
                 POD_TRACE(m.uid_of(obj), "bench_create", tw)
+                if group is gpu:
+                    POD_TRACE(m.uid_of(obj), "bench_gpu_pod", tw)
+        # the previous step's pause pods go once this step's pods are in (their deletes would
+        # otherwise queue in the apiserver ahead of this step's creates)
+        for nm in old:
+            self.deleting.add(nm)
+            asyncio.create_task(self._delete(nm))
         await asyncio.wait_for(asyncio.gather(*(self.done_events[nm].wait() for nm in gpu + cpu)), timeout)
         self.pending_cleanup = cpu
         self.step_devices.append(sorted({d for nm in gpu for d in self.t[nm].get("devices", [])}))
@@ -483,6 +487,17 @@ def main():
     ap.add_argument("--health-probe", default="none")
     ap.add_argument("--isolation", default=None, help="rocshim device isolation (default: auto on real GPUs, env on fake)")
     ap.add_argument("args", nargs="*", default=[])
+    prof_path = os.environ.get("AMDKUBE_CPROFILE")      # the bench process itself (apiserver + client)
+    if prof_path:
+        import cProfile
+        pr = cProfile.Profile()
+        pr.enable()
+        try:
+            asyncio.run(serve(ap.parse_args()))
+        finally:
+            pr.disable()
+            pr.dump_stats(f"{prof_path}.podbench.{os.getpid()}")
+        return
     asyncio.run(serve(ap.parse_args()))
 
 

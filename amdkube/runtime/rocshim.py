@@ -156,15 +156,32 @@ class PidProc:
         return await asyncio.shield(self._fut)
 
 
-async def spawn(argv, stdout=None, stderr=None, env=None, cwd=None):
-    """Start argv in its own session with stdin from /dev/null; pidfd-watched when possible."""
-    p = subprocess.Popen(argv, stdin=subprocess.DEVNULL, stdout=stdout if stdout is not None else subprocess.DEVNULL,
-                         stderr=stderr if stderr is not None else subprocess.DEVNULL, env=env, cwd=cwd,
-                         start_new_session=True)
+def _popen(argv, stdout, stderr, env, cwd, log_path, oom_score_adj=None):
+    """fork/exec (and the log file's open, and the child's oom_score_adj) off the event loop: a
+    spawn is ~1 ms of syscalls that would otherwise stall every other CRI call the runtime is
+    serving."""
+    logf = open(log_path, "ab", buffering=0) if log_path else None
+    try:
+        out = logf if logf is not None else (stdout if stdout is not None else subprocess.DEVNULL)
+        err = logf if logf is not None else (stderr if stderr is not None else subprocess.DEVNULL)
+        p = subprocess.Popen(argv, stdin=subprocess.DEVNULL, stdout=out, stderr=err, env=env, cwd=cwd,
+                             start_new_session=True)
+    finally:
+        if logf is not None:
+            logf.close()
     try:
         fd = os.pidfd_open(p.pid)
     except (AttributeError, OSError):
         fd = None
+    if oom_score_adj:
+        _set_oom_score_adj(p.pid, oom_score_adj)
+    return p, fd
+
+
+async def spawn(argv, stdout=None, stderr=None, env=None, cwd=None, log_path=None, oom_score_adj=None):
+    """Start argv in its own session with stdin from /dev/null (stdout and stderr appended to
+    `log_path` when given); pidfd-watched when possible."""
+    p, fd = await asyncio.to_thread(_popen, argv, stdout, stderr, env, cwd, log_path, oom_score_adj)
     if fd is None:   # old kernel: a thread waits for the child
         loop = asyncio.get_running_loop()
         proc = PidProc.__new__(PidProc)
@@ -184,6 +201,7 @@ class Sandbox:
         self.ip = ""
         self.pod_network = False   # the network plugin set this sandbox up (CNI DEL on teardown)
         self.own_ns = False        # the sandbox holds its own net/ipc/uts namespaces (pod networking)
+        self.resolv = False        # rootfs/<id>/resolv.conf was written (the pod's DNS config)
         self.port_mappings: list[dict] = []
 
     def to_json(self):
@@ -216,6 +234,29 @@ class Container:
                                             "state", "created_at", "started_at", "finished_at", "exit_code", "reason",
                                             "message", "pid")}
         return d
+
+
+def _prepare_sandbox_fs(log_dir: str, rootfs: str, resolv: str | None):
+    os.makedirs(log_dir, exist_ok=True)
+    os.makedirs(rootfs, exist_ok=True)
+    if resolv is not None:
+        with open(os.path.join(rootfs, "resolv.conf"), "w") as f:
+            f.write(resolv)
+
+
+def _prepare_container_fs(root: str, log_dir: str, links: list[tuple[str, str]]):
+    """A container's directories and volume links (run in a worker thread: directory creation
+    costs ~0.2 ms a call on a journaled filesystem, several per container)."""
+    os.makedirs(root, exist_ok=True)
+    os.makedirs(log_dir, exist_ok=True)
+    made = set()
+    for link, target in links:
+        parent = os.path.dirname(link)
+        if parent not in made:
+            os.makedirs(parent, exist_ok=True)
+            made.add(parent)
+        if not os.path.lexists(link):
+            os.symlink(target, link)
 
 
 class CheckpointWriter:
@@ -316,6 +357,7 @@ class RocShim:
         self.started = 0
         self._adopt_tasks: set = set()
         self._event_streams: set[asyncio.Queue] = set()
+        self._starting: set[str] = set()     # container ids whose process is being launched
         self._last_ev: dict[str, int] = {}   # sandbox id -> created_at of the newest event emitted for it
         self.streaming = None
         self.streaming_port = 0     # loopback port of the exec/attach/port-forward server (0: any)
@@ -413,6 +455,7 @@ class RocShim:
             s.state, s.created_at, s.pid = d["state"], d["created_at"], d["pid"]
             s.ip, s.pod_network = d.get("ip", ""), d.get("pod_network", False)
             s.own_ns, s.port_mappings = d.get("own_ns", False), d.get("port_mappings") or []
+            s.resolv = os.path.exists(os.path.join(self.state_dir, "rootfs", s.id, "resolv.conf"))
             if s.state == C.SANDBOX_READY and not _alive(s.pid):
                 s.state = C.SANDBOX_NOTREADY
             self.sandboxes[s.id] = s
@@ -456,7 +499,6 @@ class RocShim:
         meta = {"name": cfg.metadata.name, "uid": cfg.metadata.uid, "namespace": cfg.metadata.namespace,
                 "attempt": cfg.metadata.attempt}
         log_dir = cfg.log_directory or os.path.join(self.state_dir, "logs", sid)
-        os.makedirs(log_dir, exist_ok=True)
         sysctls = dict(cfg.linux.sysctls) if cfg.HasField("linux") else {}
         nso = None
         try:
@@ -478,8 +520,8 @@ class RocShim:
         s = Sandbox(sid, cfg.SerializeToString(), meta, dict(cfg.labels), dict(cfg.annotations), log_dir)
         s.port_mappings = [{"host_ip": pm.host_ip, "host_port": pm.host_port, "container_port": pm.container_port,
                             "protocol": {0: "TCP", 1: "UDP"}.get(int(pm.protocol), "TCP")} for pm in cfg.port_mappings]
-        os.makedirs(os.path.join(self.state_dir, "rootfs", sid), exist_ok=True)
         dns = cfg.dns_config if cfg.HasField("dns_config") else None
+        resolv = None
         if dns is not None and (dns.servers or dns.searches or dns.options):
             # the pod's resolv.conf (dockershim rewriteResolvFile), mounted at /etc/resolv.conf
             lines = [f"nameserver {x}" for x in dns.servers]
@@ -487,8 +529,9 @@ class RocShim:
                 lines.append("search " + " ".join(dns.searches))
             if dns.options:
                 lines.append("options " + " ".join(dns.options))
-            with open(os.path.join(self.state_dir, "rootfs", sid, "resolv.conf"), "w") as f:
-                f.write("\n".join(lines) + "\n")
+            resolv = "\n".join(lines) + "\n"
+        await asyncio.to_thread(_prepare_sandbox_fs, log_dir, os.path.join(self.state_dir, "rootfs", sid), resolv)
+        s.resolv = resolv is not None
         if own_ns:
             # the pause process owns the pod's namespaces; sysctls are written inside them
             argv = [self.nsexec_bin, "--no-namespaces", "--unshare", "net,uts" if host_ipc else "net,ipc,uts"]
@@ -560,7 +603,7 @@ class RocShim:
         await asyncio.to_thread(shutil.rmtree, os.path.join(self.state_dir, "rootfs", sid), True)
 
     # --------------------------------------------------------------- containers
-    def create_container(self, sid: str, cfg, sandbox_cfg) -> str:
+    async def create_container(self, sid: str, cfg, sandbox_cfg) -> str:
         s = self.sandboxes.get(sid)
         if s is None or s.state != C.SANDBOX_READY:
             raise LookupError(f"sandbox {sid} not found or not ready")
@@ -600,7 +643,6 @@ class RocShim:
             env.update({k: v for k, v in self._host_env.items() if k.startswith("HSA_") and k not in env})
         cid = uuid.uuid4().hex
         root = os.path.join(self.state_dir, "rootfs", sid, cfg.metadata.name)
-        os.makedirs(root, exist_ok=True)
         if image_root:
             workdir = cfg.working_dir or ispec.get("workdir") or "/"
             cwd = os.path.join(image_root, workdir.lstrip("/"))    # path-rooted launch; nsexec chdirs itself
@@ -609,21 +651,19 @@ class RocShim:
         else:
             workdir = ""
             cwd = cfg.working_dir or ispec.get("workdir") or root
-            if not os.path.isdir(cwd):
+            if cwd != root and not os.path.isdir(cwd):      # root itself is created below
                 cwd = root
         log_path = os.path.join(s.log_dir, cfg.log_path) if cfg.log_path else os.path.join(s.log_dir, f"{cfg.metadata.name}_{cfg.metadata.attempt}.log")
-        os.makedirs(os.path.dirname(log_path), exist_ok=True)
         mounts = [{"container_path": m.container_path, "host_path": m.host_path, "readonly": m.readonly} for m in cfg.mounts]
         resolv = os.path.join(self.state_dir, "rootfs", sid, "resolv.conf")
-        if os.path.exists(resolv) and not any(x["container_path"] == "/etc/resolv.conf" for x in mounts):
+        if s.resolv and not any(x["container_path"] == "/etc/resolv.conf" for x in mounts):
             mounts.append({"container_path": "/etc/resolv.conf", "host_path": resolv, "readonly": True})
         # without a mount namespace, expose volumes as symlinks under the container's root
-        for mnt in mounts:
-            if not self.private_mounts and mnt["container_path"].startswith("/"):
-                link = os.path.join(root, mnt["container_path"].lstrip("/"))
-                os.makedirs(os.path.dirname(link), exist_ok=True)
-                if not os.path.lexists(link):
-                    os.symlink(mnt["host_path"], link)
+        links = [(os.path.join(root, mnt["container_path"].lstrip("/")), mnt["host_path"]) for mnt in mounts
+                 if not self.private_mounts and mnt["container_path"].startswith("/")]
+        await asyncio.to_thread(_prepare_container_fs, root, os.path.dirname(log_path), links)
+        if self.sandboxes.get(sid) is not s or s.state != C.SANDBOX_READY:
+            raise LookupError(f"sandbox {sid} went away while container {cfg.metadata.name} was created")
         env["AMDKUBE_ROOTFS"] = root
         if image_root and not self.private_mounts:
             # no mount namespace: the rootview preload makes the image's root the process's `/`
@@ -871,21 +911,24 @@ class RocShim:
         c = self.containers.get(cid)
         if c is None:
             raise LookupError(f"container {cid} not found")
-        if c.state != C.CONTAINER_CREATED:
+        if c.state != C.CONTAINER_CREATED or cid in self._starting:
             raise ValueError(f"container {cid} is not in created state")
-        logf = open(c.log_path, "ab", buffering=0)
+        self._starting.add(cid)          # the launch below yields the loop: no second start meanwhile
         try:
-            proc = await spawn(self._launch_argv(c), stdout=logf, stderr=logf, env=c.env, cwd=c.cwd)
+            proc = await spawn(self._launch_argv(c), env=c.env, cwd=c.cwd, log_path=c.log_path,
+                               oom_score_adj=c.resources.get("oom_score_adj") if self.isolation != "namespaces" else None)
         except (OSError, ValueError) as e:
-            logf.close()
             c.state, c.exit_code, c.reason, c.message = C.CONTAINER_EXITED, 128, "StartError", str(e)
             c.finished_at = now_ns()
             self._ckpt("containers", c)
             raise
-        logf.close()
+        finally:
+            self._starting.discard(cid)
+        if self.containers.get(cid) is not c:           # removed while it launched
+            _killpg(proc.pid, signal.SIGKILL)
+            await proc.wait()
+            raise LookupError(f"container {cid} was removed while starting")
         c.proc, c.pid = proc, proc.pid
-        if self.isolation != "namespaces" and c.resources.get("oom_score_adj"):
-            _set_oom_score_adj(proc.pid, c.resources["oom_score_adj"])
         c.state, c.started_at = C.CONTAINER_RUNNING, now_ns()
         self.started += 1
         self._ckpt("containers", c)
@@ -894,11 +937,9 @@ class RocShim:
 
     async def _wait(self, c: Container):
         rc = await c.proc.wait()
-        try:
-            with open(os.path.join(self.state_dir, "containers", c.id + ".exit"), "w") as f:
-                f.write(str(rc))
-        except OSError:
-            pass
+        # written by the checkpoint thread, ordered before the container's checkpoint and any
+        # later removal of the same file
+        self.ckpt.put(os.path.join(self.state_dir, "containers", c.id + ".exit"), str(rc).encode())
         self._finish(c, rc)
 
     def _finish(self, c: Container, rc):
@@ -1202,7 +1243,7 @@ class _Runtime:
 
     async def CreateContainer(self, req, ctx):
         try:
-            cid = self.r.create_container(req.pod_sandbox_id, req.config, req.sandbox_config)
+            cid = await self.r.create_container(req.pod_sandbox_id, req.config, req.sandbox_config)
         except Exception as e:
             await _abort(ctx, e)
         self._mark(ctx, req.pod_sandbox_id)
