@@ -63,6 +63,14 @@ def container_hash(c: dict) -> str:
     return hashlib.sha1(json.dumps(c, sort_keys=True).encode()).hexdigest()[:16]
 
 
+
+def _container_files(hosts, tm_host: str):
+    from .podcontext import atomic_write
+    if hosts is not None:
+        atomic_write(hosts[0], hosts[1], 0o644)
+    os.makedirs(os.path.dirname(tm_host), exist_ok=True)
+    open(tm_host, "w").close()
+
 class ContainerRuntimeStatus:
     __slots__ = ("id", "name", "state", "exit_code", "reason", "message", "created_at", "started_at", "finished_at",
                  "restart_count", "hash", "image", "image_ref", "init", "log_path", "sandbox_id")
@@ -232,7 +240,12 @@ class RuntimeManager:
     def sandbox_config(self, pod: dict, attempt: int, annotations: dict) -> "C.PodSandboxConfig":
         md, spec = pod["metadata"], pod.get("spec") or {}
         log_dir = os.path.join(self.root, "pods", md["uid"], "logs")
-        os.makedirs(log_dir, exist_ok=True)
+        made = self.__dict__.setdefault("_made_dirs", set())
+        if log_dir not in made:            # the config is rebuilt on every sync; the directory once
+            os.makedirs(log_dir, exist_ok=True)
+            made.add(log_dir)
+            if len(made) > 4096:
+                made.clear()
         ports = [C.PortMapping(container_port=p.get("containerPort", 0), host_port=p.get("hostPort", 0),
                                protocol=C.UDP if p.get("protocol") == "UDP" else C.TCP)
                  for c in spec.get("containers") or [] for p in c.get("ports") or []]
@@ -315,15 +328,15 @@ class RuntimeManager:
         extra_mounts = []
         spec = pod.get("spec") or {}
         pdir = os.path.join(self.root, "pods", pod["metadata"]["uid"])
+        hosts = None
         if not spec.get("hostNetwork"):
             # kubelet_pods.go makeHostsMount: the kubelet-managed /etc/hosts (pod IP, hostname, hostAliases)
             hp = os.path.join(pdir, "etc-hosts")
-            atomic_write(hp, hosts_file(pod, pod_ip, self.cluster_domain).encode(), 0o644)
+            hosts = (hp, hosts_file(pod, pod_ip, self.cluster_domain).encode())
             extra_mounts.append({"container_path": "/etc/hosts", "host_path": hp, "read_only": False})
         tm_path = c.get("terminationMessagePath") or "/dev/termination-log"
         tm_host = os.path.join(pdir, "containers", c["name"], f"{restart_count}-termination-log")
-        os.makedirs(os.path.dirname(tm_host), exist_ok=True)
-        open(tm_host, "w").close()
+        _container_files(hosts, tm_host)
         extra_mounts.append({"container_path": tm_path, "host_path": tm_host, "read_only": False})
         mounts = [C.Mount(container_path=m["container_path"], host_path=m["host_path"], readonly=bool(m.get("read_only")))
                   for m in (ctx.get("mounts", {}).get(c["name"]) or []) + opts["mounts"] + extra_mounts]
