@@ -61,3 +61,25 @@ def test_runonce_command_exit_status(tmp_path):
     finally:
         shim.terminate()
         shim.wait(10)
+        _kill_runtime_leftovers(tmp_path / "shim")
+
+
+def _kill_runtime_leftovers(state_dir):
+    """A --runonce kubelet leaves its pods running (that is the point of runonce), and a
+    runtime keeps its sandboxes across its own restart: kill what the runtime recorded."""
+    import glob
+    import signal
+    for f in glob.glob(os.path.join(str(state_dir), "*", "*.json")):
+        try:
+            pid = int(json.load(open(f)).get("pid") or 0)
+        except (OSError, ValueError, AttributeError):
+            continue
+        if pid > 1:
+            try:
+                os.killpg(pid, signal.SIGKILL)
+            except (ProcessLookupError, PermissionError):
+                try:
+                    os.kill(pid, signal.SIGKILL)
+                except (ProcessLookupError, PermissionError):
+                    pass
+
