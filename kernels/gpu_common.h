@@ -456,7 +456,7 @@ inline HbmResult run_hbm_probe(size_t bytes, int iters, int dev, uint32_t seed =
   AK_HIP(hipEventCreate(&e1));
   const int grid = stream_grid(n16, info.cu_count, HBM_BLOCKS_PER_CU);
   auto timed = [&](auto&& launch) {
-    launch();  // warm-up (page-in / first-touch)
+    for (int w = 0; w < 3; ++w) launch();  // warm-up: page-in / first touch, and the clock ramp
     AK_HIP(hipGetLastError());
     AK_HIP(hipEventRecord(e0));
     for (int it = 0; it < iters; ++it) launch();
