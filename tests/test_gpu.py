@@ -8,6 +8,7 @@ import asyncio
 import json
 import os
 import subprocess
+import time
 
 import pytest
 
@@ -539,9 +540,11 @@ def test_09_gpu_pods_over_a_raft_store_with_protobuf_and_spdy_exec(tmp_path):
                 await lc.wait_gpus(1, 60)
                 c = lc.client
                 await c.create(burn("burner", 20000))
-                await c.create(burn("plain", 20000, gpu=False))
+                await c.create(burn("plain", 120000, gpu=False))      # outlives both execs
+                t0 = time.monotonic()
                 await wait_pod(c, "default", "burner", ("Running",), 60)
                 await wait_pod(c, "default", "plain", ("Running",), 60)
+                print(f"test_09: both pods running after {time.monotonic() - t0:.2f}s", flush=True)
                 # the object as the store holds it: protobuf, replicated to every member
                 for nm in cl.names:
                     with grpc.insecure_channel(cl.client[nm]) as ch:
@@ -553,6 +556,7 @@ def test_09_gpu_pods_over_a_raft_store_with_protobuf_and_spdy_exec(tmp_path):
                 rc = await exec_stream(c, "default", "burner", [vadd], on_stdout=out.extend, on_stderr=err.extend,
                                        transport="spdy")
                 assert rc == 0 and b"Test PASSED" in out, (rc, bytes(out[-400:]), bytes(err[-400:]))
+                print(f"test_09: exec in the GPU pod done at {time.monotonic() - t0:.2f}s", flush=True)
                 out, err = bytearray(), bytearray()
                 rc = await exec_stream(c, "default", "plain", [vadd], on_stdout=out.extend, on_stderr=err.extend,
                                        transport="spdy")
