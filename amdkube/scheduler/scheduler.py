@@ -280,10 +280,6 @@ class Scheduler:
             except Exception as e:
                 log.exception("scheduling %s crashed: %r", m.key_of(pod), e)
                 self.queue.add_unschedulable(pod)
-            # let the bind just started go out now (the reference binds in a goroutine while
-            # the next pod is scheduled); without this a burst is scheduled to the end before
-            # its first binding request leaves
-            await asyncio.sleep(0)
 
     async def schedule_one(self, pod: dict):
         key = m.key_of(pod)
