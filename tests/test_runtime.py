@@ -154,3 +154,35 @@ def test_images_pull_and_unknown_image():
             await cri.close()
             await shim.stop()
     run(go())
+
+
+def test_launches_in_flight_at_stop_do_not_outlive_the_runtime():
+    """Sandbox and container processes are launched from worker threads; a launch that lands
+    after stop(kill_pods=True) began is killed instead of being left behind untracked."""
+    async def go():
+        base = tempfile.mkdtemp(prefix="rs", dir="/tmp")
+        shim = await RocShim(os.path.join(base, "s.sock"), os.path.join(base, "state"),
+                             hooks_dir=os.path.join(base, "hooks")).start()
+        import amdkube.runtime.rocshim as rs
+        pids = []
+        real_spawn = rs.spawn
+
+        async def slow_spawn(argv, **kw):
+            proc = await real_spawn(argv, **kw)       # the process exists ...
+            pids.append(proc.pid)
+            await asyncio.sleep(0.2)                  # ... and its launch is still in flight at stop()
+            return proc
+        rs.spawn = slow_spawn
+        try:
+            t = asyncio.create_task(shim.run_sandbox(sandbox_cfg("late", "u-late")))
+            await asyncio.sleep(0.1)
+            await shim.stop(kill_pods=True)
+            with pytest.raises(RuntimeError, match="shutting down"):
+                await t
+        finally:
+            rs.spawn = real_spawn
+        assert not shim.sandboxes and len(pids) == 1
+        assert not os.path.exists(f"/proc/{pids[0]}") or open(f"/proc/{pids[0]}/stat").read().split()[2] == "Z"
+        with pytest.raises(RuntimeError, match="shutting down"):
+            await shim._launch(["/bin/true"])
+    run(go())
