@@ -206,7 +206,10 @@ async def apply(a) -> int:
 
 async def _upgrade_self_hosted(c, comp: str, ds: dict, manifest: dict, timeout: float) -> int:
     new = selfhosting.build_daemonset(comp, json.loads(json.dumps(manifest.get("spec") or {})))
-    if ds["spec"]["template"]["spec"] == new["spec"]["template"]["spec"]:
+
+    def key(spec):       # what a manifest decides; the stored template also carries API defaults
+        return [(c.get("name"), c.get("image"), c.get("command"), c.get("args"), c.get("env")) for c in spec.get("containers") or []]
+    if key(ds["spec"]["template"]["spec"]) == key(new["spec"]["template"]["spec"]):
         print(f"[upgrade/selfhosted] {comp} is unchanged")
         return 0
     ds["spec"]["template"] = new["spec"]["template"]

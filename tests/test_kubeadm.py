@@ -255,5 +255,26 @@ def test_kubeadm_self_hosting(tmp_path):
             finally:
                 await c.close()
         asyncio.run(check())
+        # an upgrade of a self-hosted component rolls its DaemonSet (no static manifest comes back)
+        newcfg = tmp_path / "upgrade.yaml"
+        newcfg.write_text("apiVersion: kubeadm.k8s.io/v1alpha1\nkind: MasterConfiguration\n"
+                          "schedulerExtraArgs: {kube-api-qps: '300'}\n")
+        admin = os.path.join(base, "admin.conf")
+        r = _kubeadm("upgrade", "apply", "--kubeconfig", admin, "--base-dir", base, "--config", str(newcfg), "-y",
+                     "--timeout", "90", timeout=200)
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+        assert "Component kube-scheduler upgraded successfully (DaemonSet self-hosted-kube-scheduler)" in r.stdout, r.stdout
+        assert "[upgrade/selfhosted] kube-apiserver is unchanged" in r.stdout, r.stdout
+        assert not os.path.exists(os.path.join(base, "manifests", "kube-scheduler.yaml"))
+
+        async def rolled():
+            c = Client.from_kubeconfig(admin)
+            try:
+                pods, _ = await c.list("pods", "kube-system", label_selector="k8s-app=self-hosted-kube-scheduler")
+                args = pods[0]["spec"]["containers"][0]["args"]
+                assert len(pods) == 1 and args[args.index("--kube-api-qps") + 1] == "300", args
+            finally:
+                await c.close()
+        asyncio.run(rolled())
     finally:
         _kubeadm("reset", "--base-dir", base, "--drain-seconds", "1.5")
