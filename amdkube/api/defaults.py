@@ -107,6 +107,11 @@ def _default_template_owner(obj: dict, replicas=True):
 
 def default_daemonset(ds: dict):
     _default_template_owner(ds, replicas=False)
+    if ds.get("apiVersion") == "extensions/v1beta1":
+        # extensions/v1beta1 keeps the pre-1.6 behaviour (pkg/apis/extensions/v1beta1/defaults.go):
+        # OnDelete unless asked, and a templateGeneration
+        ds["spec"].setdefault("updateStrategy", {"type": "OnDelete"})
+        ds["spec"].setdefault("templateGeneration", 1)
     ds["spec"].setdefault("updateStrategy", {"type": "RollingUpdate", "rollingUpdate": {"maxUnavailable": 1}})
     ds["spec"].setdefault("revisionHistoryLimit", 10)
     return ds
@@ -152,6 +157,11 @@ register_hooks("Node", defaulter=default_node)
 register_hooks("Namespace", defaulter=default_namespace)
 register_hooks("Service", defaulter=default_service)
 register_hooks("DaemonSet", "apps/v1", defaulter=default_daemonset)
+for _gv in ("apps/v1beta2", "extensions/v1beta1"):
+    try:
+        register_hooks("DaemonSet", _gv, defaulter=default_daemonset)
+    except KeyError:
+        pass
 register_hooks("ReplicaSet", "apps/v1", defaulter=default_replicaset)
 register_hooks("Deployment", "apps/v1", defaulter=default_deployment)
 register_hooks("Job", "batch/v1", defaulter=default_job)
