@@ -30,7 +30,6 @@ import argparse
 import asyncio
 import base64
 import hashlib
-import ipaddress
 import json
 import os
 import secrets
@@ -39,7 +38,6 @@ import signal
 import socket
 import subprocess
 import sys
-import tempfile
 import time
 
 import yaml

@@ -40,7 +40,7 @@ import time
 import yaml
 
 from .. import GIT_VERSION
-from . import (ADMISSION, BOOTSTRAP_GROUP, GPU_LABEL, MASTER_LABEL, ROOT, _bootstrap_rbac, _client, _component_pod,
+from . import (ADMISSION, GPU_LABEL, MASTER_LABEL, ROOT, _bootstrap_rbac, _client, _component_pod,
                kubeconfig, new_ca, new_cert, new_token, token_secret, write_yaml)
 
 CONFIG_MAP = "kubeadm-config"

@@ -1,13 +1,12 @@
 """MVCC store: CAS, watch-from-revision, compaction, WAL+snapshot recovery, and a
 Hypothesis model check that the store is linearizable against a dict model."""
-import asyncio
 import json
 import time
 
 import pytest
 from hypothesis import given, settings, strategies as st
 
-from amdkube.store import CASFailed, Compacted, KeyExists, MVCCStore, Storage, Filter, PUT, DELETE
+from amdkube.store import CASFailed, Compacted, KeyExists, MVCCStore, Storage, Filter, DELETE
 from amdkube.store.storage import FilteredWatch
 from amdkube.api import labels as L
 from amdkube.api import meta as m
@@ -115,7 +114,6 @@ def test_triggered_watch_equals_filtered_watch(ops):
     """The spec.nodeName trigger index (store.triggered) is an optimisation only: a watch it
     indexes must deliver exactly the events an unindexed watch with the same filter delivers."""
     from amdkube.apiserver.registry import pod_fields
-    from amdkube.store.storage import field_trigger
 
     async def go():
         s = MVCCStore()
