@@ -27,7 +27,7 @@ from amdkube.grpcdesc.etcd import ETCD as E
 from amdkube.store import MVCCStore
 from amdkube.store.etcd3 import FENCE, Etcd3Store
 from amdkube.store.etcdserver import EtcdServer, prefix_end
-from amdkube.store.mvcc import CASFailed, KeyExists, KeyNotFound
+from amdkube.store.mvcc import KV, CASFailed, KeyExists, KeyNotFound
 
 FIX = os.path.join(os.path.dirname(__file__), "fixtures", "reference_descriptors")
 
@@ -486,4 +486,29 @@ async def test_concurrent_requests_group_commit_over_etcd(wire):
             for c in cs:
                 await c.close()
             await srv.stop()
+            s.close()
+
+
+async def test_cancelled_bridged_write_leaves_the_store_consistent():
+    """A request cancelled while its write waits in the group-commit queue (a client that went
+    away): the write still commits or not at all, the flusher carries on, later writes work
+    and the replica matches etcd."""
+    from amdkube.utils import greenbridge
+    with ServerThread(wire=True) as st:
+        s = await asyncio.to_thread(Etcd3Store, st.address)
+        s.start(asyncio.get_running_loop())
+        try:
+            tasks = [asyncio.create_task(greenbridge.run_sync(s.put, f"/registry/c/{i}", b"v", 0)) for i in range(20)]
+            await asyncio.sleep(0)
+            for t in tasks[::3]:
+                t.cancel()
+            done = await asyncio.gather(*tasks, return_exceptions=True)
+            assert all(isinstance(r, (KV, asyncio.CancelledError)) for r in done), done
+            kv = await greenbridge.run_sync(s.put, "/registry/c/after", b"x", 0)
+            assert kv.value == b"x"
+            s.drain(until=kv.mod_rev)
+            ours = {k: v.value for k, v in s.kv.items() if k.startswith("/registry/c/")}
+            theirs = {k: v.value for k, v in st.store.kv.items() if k.startswith("/registry/c/")}
+            assert ours == theirs and "/registry/c/after" in ours
+        finally:
             s.close()
