@@ -261,9 +261,10 @@ async def _post_init(mc, cfg, timeout, skip_addons):
             print(f"[addons] Applied essential addons: {', '.join(done)} (the AMD GPU device plugin runs on nodes "
                   f"labelled {GPU_LABEL})")
         if (mc.get("featureGates") or {}).get("SelfHosting"):
-            from .selfhosting import create_self_hosted_control_plane
+            from .selfhosting import create_self_hosted_control_plane, secrets_of
             print("[self-hosted] Creating self-hosted control plane.")
-            await create_self_hosted_control_plane(c, cfg["manifests"], mc["nodeName"], timeout)
+            await create_self_hosted_control_plane(c, cfg["manifests"], mc["nodeName"], timeout,
+                                                   secrets=secrets_of(mc, cfg))
         return 0
     finally:
         await c.close()

@@ -563,8 +563,9 @@ def run_phase(a) -> int:
             if a.phase == "selfhosting":
                 if sub not in ("all", "convert-from-staticpods"):
                     raise SystemExit("error: the selfhosting phase is `selfhosting convert-from-staticpods`")
-                from .selfhosting import create_self_hosted_control_plane
-                done = await create_self_hosted_control_plane(c, p["manifests"], mc["nodeName"], a.timeout, a.dry_run)
+                from .selfhosting import create_self_hosted_control_plane, secrets_of
+                done = await create_self_hosted_control_plane(c, p["manifests"], mc["nodeName"], a.timeout, a.dry_run,
+                                                              secrets=secrets_of(mc, p))
                 if not a.dry_run:
                     print(f"[self-hosted] Converted {', '.join(done) or 'nothing (no static control-plane Pods left)'}")
                 return 0

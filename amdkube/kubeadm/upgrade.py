@@ -170,7 +170,7 @@ async def apply(a) -> int:
             ds = await c.get_or_none("daemonsets.apps", selfhosting.PREFIX + comp, "kube-system")
             if ds is not None and not os.path.exists(path):
                 # a self-hosted component: roll its DaemonSet (selfhosted upgrade path) instead of a manifest
-                rc = await _upgrade_self_hosted(c, comp, ds, manifests[comp], a.timeout)
+                rc = await _upgrade_self_hosted(c, comp, ds, manifests[comp], a.timeout, p)
                 if rc:
                     return rc
                 continue
@@ -204,8 +204,11 @@ async def apply(a) -> int:
         await c.close()
 
 
-async def _upgrade_self_hosted(c, comp: str, ds: dict, manifest: dict, timeout: float) -> int:
-    new = selfhosting.build_daemonset(comp, json.loads(json.dumps(manifest.get("spec") or {})))
+async def _upgrade_self_hosted(c, comp: str, ds: dict, manifest: dict, timeout: float, p: dict) -> int:
+    # a plane converted with StoreCertsInSecrets keeps reading its Secrets
+    vols = {v.get("name") for v in ds["spec"]["template"]["spec"].get("volumes") or []}
+    secrets = (p["pki"], p["kubeconfig_dir"]) if vols & {selfhosting.CERTS_VOLUME, selfhosting.KUBECONFIG_VOLUME} else None
+    new = selfhosting.build_daemonset(comp, json.loads(json.dumps(manifest.get("spec") or {})), secrets)
 
     def key(spec):       # what a manifest decides; the stored template also carries API defaults
         return [(c.get("name"), c.get("image"), c.get("command"), c.get("args"), c.get("env")) for c in spec.get("containers") or []]

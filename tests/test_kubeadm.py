@@ -6,6 +6,7 @@ signed by the cluster CA)."""
 from __future__ import annotations
 
 import asyncio
+import base64
 import os
 import re
 import socket
@@ -210,15 +211,17 @@ def test_kubeadm_store_modes():
 
 
 def test_kubeadm_self_hosting(tmp_path):
-    """--feature-gates SelfHosting=true: the static control plane becomes DaemonSets
-    self-hosted-kube-{apiserver,controller-manager,scheduler} (selfhosting.go); the static
-    manifests and their mirror pods go, the self-hosted apiserver takes over the embedded
-    store's data directory, and the cluster keeps its objects and keeps working."""
+    """--feature-gates SelfHosting=true,StoreCertsInSecrets=true: the static control plane
+    becomes DaemonSets self-hosted-kube-{apiserver,controller-manager,scheduler}
+    (selfhosting.go) that read their certificates and kubeconfigs from kube-system Secrets
+    (selfhosting_volumes.go); the static manifests and their mirror pods go, the self-hosted
+    apiserver takes over the embedded store's data directory, and the cluster keeps its
+    objects and keeps working."""
     base = str(tmp_path / "master")
     port = _free_port()
     try:
         r = _kubeadm("init", "--base-dir", base, "--apiserver-bind-port", str(port), "--node-name", "master-0",
-                     "--start-kubelet", "--kubelet-port", "0", "--skip-addons", "--feature-gates", "SelfHosting=true",
+                     "--start-kubelet", "--kubelet-port", "0", "--skip-addons", "--feature-gates", "SelfHosting=true,StoreCertsInSecrets=true",
                      "--timeout", "120", timeout=300)
         assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-3000:]
         for comp in ("kube-apiserver", "kube-controller-manager", "kube-scheduler"):
@@ -234,11 +237,22 @@ def test_kubeadm_self_hosting(tmp_path):
                     ds = await c.get("daemonsets.apps", f"self-hosted-{comp}", "kube-system")
                     spec = ds["spec"]["template"]["spec"]
                     assert spec["nodeSelector"] == {"node-role.kubernetes.io/master": ""} and spec["dnsPolicy"] == "ClusterFirstWithHostNet"
+                    vols = {v["name"]: v for v in spec.get("volumes") or []}
+                    args = spec["containers"][0]["args"]
+                    if comp != "kube-scheduler":
+                        assert [x["secret"]["name"] for x in vols["k8s-certs"]["projected"]["sources"]][:1] == ["ca"]
+                    if comp != "kube-apiserver":
+                        conf = "scheduler.conf" if comp == "kube-scheduler" else "controller-manager.conf"
+                        assert vols["kubeconfig"]["secret"]["secretName"] == conf
+                        assert args[args.index("--kubeconfig") + 1] == os.path.join(base, "kubeconfig", conf)
                     mine = [p for p in pods.values() if m.labels_of(p).get("k8s-app") == f"self-hosted-{comp}"]
                     assert len(mine) == 1 and mine[0]["status"]["phase"] == "Running"
                 # objects written before the hand-off are still there; the scheduler and the
                 # controller-manager of the self-hosted plane still act
                 assert await c.get_or_none("configmaps", "kubeadm-config", "kube-system") is not None
+                tls = await c.get("secrets", "apiserver", "kube-system")
+                assert tls["type"] == "kubernetes.io/tls" and set(tls["data"]) == {"tls.crt", "tls.key"}
+                assert base64.b64decode(tls["data"]["tls.crt"]) == open(os.path.join(base, "pki", "apiserver.crt"), "rb").read()
                 await c.create({"apiVersion": "apps/v1", "kind": "ReplicaSet", "metadata": {"name": "after", "namespace": "kube-system"},
                                 "spec": {"replicas": 1, "selector": {"matchLabels": {"app": "after"}},
                                          "template": {"metadata": {"labels": {"app": "after"}},
@@ -273,8 +287,44 @@ def test_kubeadm_self_hosting(tmp_path):
                 pods, _ = await c.list("pods", "kube-system", label_selector="k8s-app=self-hosted-kube-scheduler")
                 args = pods[0]["spec"]["containers"][0]["args"]
                 assert len(pods) == 1 and args[args.index("--kube-api-qps") + 1] == "300", args
+                assert args[args.index("--kubeconfig") + 1] == os.path.join(base, "kubeconfig", "scheduler.conf")
             finally:
                 await c.close()
         asyncio.run(rolled())
     finally:
         _kubeadm("reset", "--base-dir", base, "--drain-seconds", "1.5")
+
+
+def test_self_hosting_secret_volumes_and_rootfs_paths(tmp_path, monkeypatch):
+    """The StoreCertsInSecrets mutators (podspec_mutation.go setSelfHostedVolumesFor*) and how
+    a process container resolves a command-line path inside its volumes."""
+    from amdkube.__main__ import rootfs_paths
+    from amdkube.kubeadm import selfhosting as sh
+    pki = tmp_path / "pki"
+    pki.mkdir()
+    for f in ("ca.crt", "ca.key", "apiserver.crt", "apiserver.key", "sa.key"):
+        (pki / f).write_text(f)
+    spec = lambda args: {"containers": [{"name": "c", "args": list(args)}]}    # noqa: E731
+    plain = sh.build_daemonset("kube-scheduler", spec(["--kubeconfig", "/k/scheduler.conf"]))
+    assert "volumes" not in plain["spec"]["template"]["spec"]
+    api = sh.build_daemonset("kube-apiserver", spec(["--data-dir", "/d"]), (str(pki), "/k"))["spec"]["template"]["spec"]
+    srcs = api["volumes"][0]["projected"]["sources"]
+    assert [x["secret"]["name"] for x in srcs] == ["ca", "apiserver", "sa"]      # front-proxy files absent
+    assert api["containers"][0]["volumeMounts"] == [{"name": "k8s-certs", "mountPath": str(pki), "readOnly": True}]
+    assert api["containers"][0]["args"][-2:] == ["--data-dir-lock-wait", sh.LOCK_WAIT]
+    cm = sh.build_daemonset("kube-controller-manager", spec(["--kubeconfig", "/k/controller-manager.conf"]),
+                            (str(pki), "/k"))["spec"]["template"]["spec"]
+    assert [x["secret"]["name"] for x in cm["volumes"][0]["projected"]["sources"]] == ["ca", "sa"]
+    assert cm["volumes"][1] == {"name": "kubeconfig", "secret": {"secretName": "controller-manager.conf"}}
+    assert cm["containers"][0]["args"] == ["--kubeconfig", "/k/kubeconfig/controller-manager.conf"]
+    again = sh.set_secret_volumes("kube-controller-manager", cm, str(pki), "/k")     # idempotent
+    assert len(again["volumes"]) == 2 and len(again["containers"][0]["volumeMounts"]) == 2
+    # $AMDKUBE_ROOTFS: a path that exists in the container's view wins over the host's
+    root = tmp_path / "root"
+    (root / "k" / "kubeconfig").mkdir(parents=True)
+    (root / "k" / "kubeconfig" / "x.conf").write_text("")
+    monkeypatch.setenv("AMDKUBE_ROOTFS", str(root))
+    assert rootfs_paths(["--kubeconfig", "/k/kubeconfig/x.conf", "--a=/k/kubeconfig/x.conf", "/nope", "rel"]) == \
+        ["--kubeconfig", f"{root}/k/kubeconfig/x.conf", f"--a={root}/k/kubeconfig/x.conf", "/nope", "rel"]
+    monkeypatch.delenv("AMDKUBE_ROOTFS")
+    assert rootfs_paths(["/k/kubeconfig/x.conf"]) == ["/k/kubeconfig/x.conf"]
