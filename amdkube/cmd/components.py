@@ -1166,13 +1166,27 @@ def dns(argv):
     ap.add_argument("--dns-bind-address", default="127.0.0.1")
     ap.add_argument("--dns-port", type=int, default=53)
     ap.add_argument("--upstream", default=None, help="comma-separated upstream servers (default: the host's resolv.conf)")
+    ap.add_argument("-conf", "--conf", dest="conf", default=None,
+                    help="a CoreDNS Corefile (dns/corefile.py): its kubernetes zone, proxy upstreams and port; "
+                         "--domain/--upstream/--dns-port given explicitly win")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     klog.setup(a.v, "dns")
     from ..dns import DNSServer
+    up = [x for x in a.upstream.split(",") if x] if a.upstream is not None else None
+    if a.conf:
+        from ..dns.corefile import parse
+        with open(a.conf) as f:
+            cf = parse(f.read())
+        given = set(argv)
+        if not given & {"--domain", "--cluster-domain"}:
+            a.domain = cf["domain"]
+        if "--dns-port" not in given:
+            a.dns_port = cf["port"]
+        if up is None:
+            up = cf["upstream"]
 
     async def mk():
-        up = [x for x in a.upstream.split(",") if x] if a.upstream is not None else None
         return await DNSServer(_client(a), a.domain, a.dns_bind_address, a.dns_port, up).start()
     _run_forever(mk)
 

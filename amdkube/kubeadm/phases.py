@@ -435,7 +435,9 @@ def addon_objects(mc: dict, p: dict, which: str = "all") -> list[dict]:
                                                                             os.path.join(p["base"], "kube-proxy.conf"),
                                                                             "--healthz-port", "0", "--bind-address", "127.0.0.1"],
                                                                    "env": env}]}}}})
-    if which in ("all", "kube-dns"):
+    if which in ("all", "kube-dns") and (mc.get("featureGates") or {}).get("CoreDNS"):
+        out += coredns_objects(mc, p, env, tol)
+    elif which in ("all", "kube-dns"):
         labels = {"k8s-app": "kube-dns"}
         out.append({"apiVersion": "apps/v1", "kind": "Deployment",
                     "metadata": {"name": "kube-dns", "namespace": "kube-system", "labels": labels,
@@ -470,6 +472,67 @@ def addon_objects(mc: dict, p: dict, which: str = "all") -> list[dict]:
     if which not in ("all", *ADDONS):
         raise SystemExit(f"error: unknown addon {which!r} (one of {', '.join(ADDONS)})")
     return out
+
+
+COREFILE = """.:53 {{
+    errors
+    log
+    health
+    kubernetes {domain} {cidr} {{
+       pods insecure
+    }}
+    prometheus
+    proxy . /etc/resolv.conf
+    cache 30
+}}
+"""
+
+
+def coredns_objects(mc: dict, p: dict, env: list, tol: list) -> list[dict]:
+    """The CoreDNS feature gate (addons/dns/dns.go coreDNSAddon, manifests.go): ConfigMap
+    coredns with the Corefile, ServiceAccount coredns, ClusterRole/Binding system:coredns, a
+    Deployment coredns whose pods carry k8s-app=kube-dns and read the Corefile from the
+    ConfigMap volume at /etc/coredns (`amdkube dns -conf`, dns/corefile.py), and the Service
+    kube-dns. The pods listen on 10053 (unprivileged); the Service maps 53 to it."""
+    labels, rb = {"k8s-app": "kube-dns"}, "rbac.authorization.k8s.io/v1"
+    corefile = COREFILE.format(domain=mc["networking"]["dnsDomain"], cidr=mc["networking"]["serviceSubnet"])
+    ann = {VERSION_ANNOTATION: mc["kubernetesVersion"]}
+    return [
+        {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "coredns", "namespace": "kube-system"},
+         "data": {"Corefile": corefile}},
+        {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": "coredns", "namespace": "kube-system"}},
+        {"apiVersion": rb, "kind": "ClusterRole",
+         "metadata": {"name": "system:coredns", "labels": {"kubernetes.io/bootstrapping": "rbac-defaults"}},
+         "rules": [{"apiGroups": [""], "resources": ["endpoints", "services", "pods", "namespaces"], "verbs": ["list", "watch"]}]},
+        {"apiVersion": rb, "kind": "ClusterRoleBinding",
+         "metadata": {"name": "system:coredns", "labels": {"kubernetes.io/bootstrapping": "rbac-defaults"},
+                      "annotations": {"rbac.authorization.kubernetes.io/autoupdate": "true"}},
+         "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole", "name": "system:coredns"},
+         "subjects": [{"kind": "ServiceAccount", "name": "coredns", "namespace": "kube-system"}]},
+        {"apiVersion": "apps/v1", "kind": "Deployment",
+         "metadata": {"name": "coredns", "namespace": "kube-system", "labels": labels, "annotations": ann},
+         "spec": {"replicas": 1, "selector": {"matchLabels": labels},
+                  "template": {"metadata": {"labels": labels},
+                               "spec": {"serviceAccountName": "coredns",
+                                        "tolerations": tol + [{"key": "CriticalAddonsOnly", "operator": "Exists"}],
+                                        "priorityClassName": "system-cluster-critical",
+                                        "volumes": [{"name": "config-volume", "configMap": {
+                                            "name": "coredns", "items": [{"key": "Corefile", "path": "Corefile"}]}}],
+                                        "containers": [{"name": "coredns", "image": "python:3",
+                                                        "args": ["-m", "amdkube", "dns", "-conf", "/etc/coredns/Corefile",
+                                                                 "--kubeconfig", os.path.join(p["base"], "kube-proxy.conf"),
+                                                                 "--dns-bind-address", "0.0.0.0", "--dns-port", "10053"],
+                                                        "volumeMounts": [{"name": "config-volume", "mountPath": "/etc/coredns"}],
+                                                        "ports": [{"name": "dns", "containerPort": 10053, "protocol": "UDP"},
+                                                                  {"name": "dns-tcp", "containerPort": 10053, "protocol": "TCP"}],
+                                                        "env": env}]}}}},
+        {"apiVersion": "v1", "kind": "Service",
+         "metadata": {"name": "kube-dns", "namespace": "kube-system",
+                      "labels": dict(labels, **{"kubernetes.io/name": "CoreDNS"})},
+         "spec": {"selector": labels, "clusterIP": dns_ip(mc),
+                  "ports": [{"name": "dns", "port": 53, "protocol": "UDP", "targetPort": 10053},
+                            {"name": "dns-tcp", "port": 53, "protocol": "TCP", "targetPort": 10053}]}},
+    ]
 
 
 async def phase_addons(c, mc: dict, p: dict, which: str = "all") -> list[str]:

@@ -105,3 +105,81 @@ def test_headless_hostnames_and_srv():
     assert r.lookup("9.3.244.10.in-addr.arpa", PTR)[0] == NXDOMAIN          # no hostname: no PTR
     assert r.lookup("5.1.244.10.in-addr.arpa", PTR)[1]
     assert r.lookup("svc.cluster.local", A) == (0, [])                       # empty non-terminal: NODATA
+
+
+def test_corefile_parse_and_kubeadm_coredns_addon(tmp_path):
+    """The CoreDNS feature gate (kubeadm addons/dns coreDNSAddon): the Corefile kubeadm writes
+    parses to the cluster domain, port and resolv.conf upstreams; the addon objects."""
+    from amdkube.dns.corefile import CorefileError, parse
+    from amdkube.kubeadm import phases as ph
+    rc = tmp_path / "resolv.conf"
+    rc.write_text("nameserver 10.0.0.2\nnameserver 10.0.0.3\n")
+    text = ph.COREFILE.format(domain="corp.local", cidr="10.96.0.0/12").replace("/etc/resolv.conf", str(rc))
+    cf = parse(text)
+    assert (cf["domain"], cf["port"], cf["upstream"], cf["cache"]) == ("corp.local", 53, ["10.0.0.2", "10.0.0.3"], 30)
+    assert cf["plugins"] == ["errors", "log", "health", "kubernetes", "prometheus", "proxy", "cache"]
+    assert parse(".:1053 {\n kubernetes a.b\n forward . dns://9.9.9.9\n}\n")["upstream"] == ["9.9.9.9"]
+    for bad in (".:53 {\n errors\n}\n", ".:53 {\n kubernetes x\n", "nothing"):
+        try:
+            parse(bad)
+            raise AssertionError(bad)
+        except CorefileError:
+            pass
+    mc = {"networking": {"dnsDomain": "corp.local", "serviceSubnet": "10.96.0.0/12"}, "kubernetesVersion": "v1.9.0",
+          "featureGates": {"CoreDNS": True}}
+    objs = {(o["kind"], o["metadata"]["name"]): o for o in ph.addon_objects(mc, {"base": "/k"}, "kube-dns")}
+    assert set(objs) == {("ConfigMap", "coredns"), ("ServiceAccount", "coredns"), ("ClusterRole", "system:coredns"),
+                         ("ClusterRoleBinding", "system:coredns"), ("Deployment", "coredns"), ("Service", "kube-dns")}
+    assert "kubernetes corp.local 10.96.0.0/12" in objs[("ConfigMap", "coredns")]["data"]["Corefile"]
+    tpl = objs[("Deployment", "coredns")]["spec"]["template"]
+    assert tpl["metadata"]["labels"] == objs[("Service", "kube-dns")]["spec"]["selector"] == {"k8s-app": "kube-dns"}
+    args = tpl["spec"]["containers"][0]["args"]
+    assert args[args.index("-conf") + 1] == "/etc/coredns/Corefile"
+    assert objs[("Service", "kube-dns")]["spec"]["clusterIP"] == "10.96.0.10"
+    mc["featureGates"] = {}
+    assert [o["metadata"]["name"] for o in ph.addon_objects(mc, {"base": "/k"}, "kube-dns")] == ["kube-dns", "kube-dns"]
+
+
+async def test_dns_component_serves_from_a_corefile_in_the_container_view(tmp_path):
+    """`amdkube dns -conf /etc/coredns/Corefile` as the CoreDNS addon pod runs it: the ConfigMap
+    volume sits under $AMDKUBE_ROOTFS, the zone comes from the Corefile."""
+    import socket
+    import subprocess
+    import sys
+    from amdkube.apiserver import APIServer
+    from amdkube.kubeadm import phases as ph
+    root = tmp_path / "root"
+    (root / "etc" / "coredns").mkdir(parents=True)
+    (root / "etc" / "coredns" / "Corefile").write_text(
+        ph.COREFILE.format(domain="corp.local", cidr="10.96.0.0/12").replace("proxy . /etc/resolv.conf", ""))
+    with socket.socket(socket.AF_INET, socket.SOCK_DGRAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    srv = await APIServer().start()
+    proc = None
+    try:
+        from amdkube.client import Client
+        c = Client(srv.url, token=srv.loopback_token)
+        await c.create({"apiVersion": "v1", "kind": "Service", "metadata": {"name": "api"},
+                        "spec": {"ports": [{"port": 80}]}}, "default")
+        cip = (await c.get("services", "api", "default"))["spec"]["clusterIP"]
+        env = dict(os.environ, AMDKUBE_ROOTFS=str(root))
+        proc = subprocess.Popen([sys.executable, "-m", "amdkube", "dns", "-conf", "/etc/coredns/Corefile", "--master", srv.url,
+                                 "--token", srv.loopback_token, "--dns-bind-address", "127.0.0.1", "--dns-port", str(port)],
+                                env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+        for _ in range(200):
+            try:
+                _, ans = await resolve("api.default.svc.corp.local", A, ("127.0.0.1", port))
+            except (OSError, asyncio.TimeoutError):
+                ans = []
+            if ans:
+                break
+            assert proc.poll() is None, proc.stderr.read().decode()[-2000:]
+            await asyncio.sleep(0.1)
+        assert cip in str(ans), ans
+        await c.close()
+    finally:
+        if proc is not None:
+            proc.terminate()
+            proc.wait(10)
+        await srv.stop()
