@@ -84,7 +84,19 @@ def master_config(a) -> dict:
             k, v = kv.split("=", 1)
             mc["featureGates"][k.strip()] = v.strip().lower() == "true"
     path = getattr(a, "config", None)
-    return merge_config(mc, load_config_file(path)) if path else mc
+    mc = merge_config(mc, load_config_file(path)) if path else mc
+    resolve_gate_dependencies(mc.setdefault("featureGates", {}))
+    return mc
+
+
+def resolve_gate_dependencies(gates: dict) -> dict:
+    """features.ResolveFeatureGateDependencies: StoreCertsInSecrets needs SelfHosting;
+    HighAvailability needs both."""
+    if gates.get("StoreCertsInSecrets"):
+        gates["SelfHosting"] = True
+    if gates.get("HighAvailability"):
+        gates["SelfHosting"] = gates["StoreCertsInSecrets"] = True
+    return gates
 
 
 def load_config_file(path: str) -> dict:
@@ -278,6 +290,8 @@ def control_plane_manifests(mc: dict, p: dict) -> dict[str, dict]:
            "--service-cluster-ip-range", mc["networking"]["serviceSubnet"], *_store_args(mc, p),
            "--kubelet-client-certificate", f"{d}/apiserver-kubelet-client.crt",
            "--kubelet-client-key", f"{d}/apiserver-kubelet-client.key"]
+    if (mc.get("featureGates") or {}).get("HighAvailability"):      # several apiservers share the endpoints
+        api += ["--endpoint-reconciler-type", "lease"]
     if os.path.exists(f"{d}/front-proxy-ca.crt"):
         api += ["--requestheader-client-ca-file", f"{d}/front-proxy-ca.crt", "--requestheader-allowed-names", "front-proxy-client",
                 "--proxy-client-cert-file", f"{d}/front-proxy-client.crt", "--proxy-client-key-file", f"{d}/front-proxy-client.key"]

@@ -328,3 +328,19 @@ def test_self_hosting_secret_volumes_and_rootfs_paths(tmp_path, monkeypatch):
         ["--kubeconfig", f"{root}/k/kubeconfig/x.conf", f"--a={root}/k/kubeconfig/x.conf", "/nope", "rel"]
     monkeypatch.delenv("AMDKUBE_ROOTFS")
     assert rootfs_paths(["/k/kubeconfig/x.conf"]) == ["/k/kubeconfig/x.conf"]
+
+
+def test_kubeadm_feature_gate_dependencies():
+    """features.ResolveFeatureGateDependencies and the HighAvailability apiserver flag."""
+    from amdkube.kubeadm import phases as ph
+    assert ph.resolve_gate_dependencies({"StoreCertsInSecrets": True}) == {"StoreCertsInSecrets": True, "SelfHosting": True}
+    assert ph.resolve_gate_dependencies({"HighAvailability": True}) == \
+        {"HighAvailability": True, "SelfHosting": True, "StoreCertsInSecrets": True}
+    assert ph.resolve_gate_dependencies({"CoreDNS": True}) == {"CoreDNS": True}
+    mc = {"api": {"advertiseAddress": "127.0.0.1", "bindPort": 6443}, "kubernetesVersion": "v1.9.0",
+          "networking": {"serviceSubnet": "10.96.0.0/12", "dnsDomain": "cluster.local"}, "featureGates": {"HighAvailability": True}}
+    p = {"pki": "/nonexistent/pki", "kubeconfig_dir": "/k", "data_dir": "/d"}
+    args = ph.control_plane_manifests(mc, p)["kube-apiserver"]["spec"]["containers"][0]["args"]
+    assert args[args.index("--endpoint-reconciler-type") + 1] == "lease"
+    mc["featureGates"] = {}
+    assert "--endpoint-reconciler-type" not in ph.control_plane_manifests(mc, p)["kube-apiserver"]["spec"]["containers"][0]["args"]
