@@ -71,6 +71,9 @@ def _atomic_write(path: str, data: bytes):
     os.replace(tmp, path)
 
 
+MAX_IMAGES_IN_NODE_STATUS, MAX_NAMES_PER_IMAGE = 50, 5     # kubelet_node_status.go:52-57
+
+
 @dataclass
 class KubeletConfig:
     node_name: str = field(default_factory=socket.gethostname)
@@ -627,9 +630,25 @@ class Kubelet:
                 self._pods_cgroup_enforced = (alloc.get("cpu"), alloc.get("memory"))
         return st
 
+    async def _node_images(self):
+        """setNodeStatusImages (kubelet_node_status.go:692-720): the runtime's images, largest
+        first, at most 50, each named by up to 5 of its digests and tags; what the scheduler's
+        ImageLocalityPriority scores. None when the runtime cannot list them."""
+        try:
+            imgs = await self.cri.list_images()
+        except Exception as e:
+            log.debug("image list for node status failed: %r", e)
+            return None
+        imgs = sorted(imgs, key=lambda i: -int(i.size))[:MAX_IMAGES_IN_NODE_STATUS]
+        return [{"names": (list(i.repo_digests) + list(i.repo_tags))[:MAX_NAMES_PER_IMAGE] or [i.id],
+                 "sizeBytes": int(i.size)} for i in imgs]
+
     async def update_node_status(self):
         prev = (self.node or {}).get("status") or {}
         body = self._node_status_body(prev)
+        images = await self._node_images()
+        if images is not None:
+            body["images"] = images
         removed = body.pop("_removed", [])
         patch = {"status": body}
         # resources that vanished must be deleted explicitly (merge patch: null removes the key)

@@ -28,7 +28,7 @@ TOPOLOGY_ANNOTATION = "amd.com/gpu-topology"
 
 class NodeInfo:
     __slots__ = ("node", "name", "pods", "requested", "nonzero", "ports", "allocatable", "devices", "device_owner",
-                 "generation", "_topo_src", "_topo", "labels", "taints", "owners")
+                 "generation", "_topo_src", "_topo", "labels", "taints", "groups")
 
     def __init__(self, name: str):
         self.name = name
@@ -45,7 +45,9 @@ class NodeInfo:
         self._topo = None
         self.labels: dict = {}
         self.taints: list = []
-        self.owners: dict[str, int] = {}  # controller uid -> pods on this node (SelectorSpreadPriority)
+        # (namespace, sorted labels) -> live pods on this node with exactly those labels: the
+        # selector-spreading count matches each distinct label set once, not each pod
+        self.groups: dict[tuple, int] = {}
 
     # ------------------------------------------------------------------ node
     def set_node(self, node: dict):
@@ -69,9 +71,9 @@ class NodeInfo:
         self.nonzero[1] += mem
         for p in pod_host_ports(pod):
             self.ports[p] = self.ports.get(p, 0) + 1
-        ou = (m.controller_ref(pod) or {}).get("uid")
-        if ou:
-            self.owners[ou] = self.owners.get(ou, 0) + 1
+        g = _group(pod)
+        if g is not None:
+            self.groups[g] = self.groups.get(g, 0) + 1
         for rname, ids in pod_assigned_devices(pod).items():
             own = self.device_owner.setdefault(rname, {})
             for did in ids:
@@ -91,13 +93,13 @@ class NodeInfo:
             self.ports[p] -= 1
             if self.ports[p] <= 0:
                 del self.ports[p]
-        ou = (m.controller_ref(pod) or {}).get("uid")
-        if ou:
-            c = self.owners.get(ou, 0) - 1
+        g = _group(pod)
+        if g is not None:
+            c = self.groups.get(g, 0) - 1
             if c > 0:
-                self.owners[ou] = c
+                self.groups[g] = c
             else:
-                self.owners.pop(ou, None)
+                self.groups.pop(g, None)
         for rname, ids in pod_assigned_devices(pod).items():
             own = self.device_owner.get(rname, {})
             for did in ids:
@@ -140,12 +142,21 @@ class NodeInfo:
         n.requested = dict(self.requested)
         n.nonzero = list(self.nonzero)
         n.ports = dict(self.ports)
-        n.owners = dict(self.owners)
+        n.groups = dict(self.groups)
         n.devices = self.devices
         n.device_owner = {r: dict(o) for r, o in self.device_owner.items()}
         n._topo_src, n._topo = self._topo_src, self._topo
         n.generation = self.generation
         return n
+
+
+def _group(pod: dict):
+    """The spreading group of a pod: None for a pod being deleted (selector_spreading.go skips
+    pods with a deletionTimestamp)."""
+    md = pod.get("metadata") or {}
+    if md.get("deletionTimestamp"):
+        return None
+    return md.get("namespace") or "", tuple(sorted((md.get("labels") or {}).items()))
 
 
 def nonzero_requests(pod: dict) -> tuple[int, int]:

@@ -17,14 +17,15 @@ from ..api import meta as m
 from ..utils.trace import Trace
 from . import extended
 from .predicates import ORDER, PREDICATES, PodInfo
-from .priorities import PRIORITIES
+from .priorities import PRIORITIES, pod_selectors
 
 log = logging.getLogger("amdkube.scheduler")
 
 
 # priorities whose per-node value depends only on that node and the pod (cacheable per node generation)
 LOCAL_PRIORITIES = {"LeastRequestedPriority", "MostRequestedPriority", "BalancedResourceAllocation",
-                    "NodePreferAvoidPodsPriority", "ImageLocalityPriority", "GPUTopologyPriority"}
+                    "NodePreferAvoidPodsPriority", "ImageLocalityPriority", "GPUTopologyPriority",
+                    "ResourceLimitsPriority", "EqualPriority"}
 
 
 class FitError(Exception):
@@ -56,19 +57,23 @@ class _FitIndex:
 
 
 class Context:
-    __slots__ = ("nodes", "any_anti_affinity", "any_affinity", "hard_weight", "services")
+    __slots__ = ("nodes", "any_anti_affinity", "any_affinity", "hard_weight", "services", "listers")
 
-    def __init__(self, nodes, any_anti_affinity, any_affinity=False, hard_weight=0, services=None):
+    def __init__(self, nodes, any_anti_affinity, any_affinity=False, hard_weight=0, services=None, listers=None):
         self.nodes, self.any_anti_affinity = nodes, any_anti_affinity
         self.any_affinity, self.hard_weight = any_affinity, hard_weight
         self.services = services or (lambda: [])
+        self.listers = listers
 
 
 class GenericScheduler:
     def __init__(self, cache, predicates: list[str], priorities: dict[str, int], extenders=(), use_topology=True,
                  trace_threshold: float = 0.1, volumes=None, volume_scheduling: bool = False, custom_predicates=None,
-                 custom_priorities=None, services=None, hard_affinity_weight: int = 1):
+                 custom_priorities=None, services=None, hard_affinity_weight: int = 1, listers=None):
+        from .listers import ControllerListers
         self.cache = cache
+        # Services/RCs/RSs/StatefulSets for the spreading priorities (metadata.go getSelectors)
+        self.listers = listers or ControllerListers(services=services)
         self.volumes = volumes                  # scheduler/volumes.VolumeLister (claims, volumes, classes)
         self.volume_scheduling = volume_scheduling
         self.volume_binds: dict[str, list] = {}  # pod key -> [(pvc, pv)] to pre-bind before the pod
@@ -93,9 +98,14 @@ class GenericScheduler:
         self.ecache = {}
         self.findex = {}
 
+    @property
+    def _lctx(self):
+        """A node-less context carrying only the listers (selector lookups)."""
+        return Context((), False, listers=self.listers)
+
     def _ctx(self, nodes):
         return Context(nodes, self.cache.anti_affinity_pods > 0, getattr(self.cache, "affinity_pods", 0) > 0,
-                       self.hard_affinity_weight, self.services)
+                       self.hard_affinity_weight, self.services, self.listers)
 
     # Equivalence cache (reference plugin/pkg/scheduler/core/equivalence_cache.go:38): pods with the
     # same scheduling-relevant spec get the same per-node answer as long as the node is unchanged.
@@ -113,7 +123,8 @@ class GenericScheduler:
         if any("persistentVolumeClaim" in v for v in spec.get("volumes") or []):
             return None     # the answer depends on claim/volume state, not just the node
         import json as _json
-        rel = {"c": [(c.get("resources"), c.get("ports")) for c in spec.get("containers") or []],
+        # images are part of the class: ImageLocalityPriority is a node-local score
+        rel = {"c": [(c.get("resources"), c.get("ports"), c.get("image")) for c in spec.get("containers") or []],
                "i": [c.get("resources") for c in spec.get("initContainers") or []],
                "ns": spec.get("nodeSelector"), "aff": spec.get("affinity"), "tol": spec.get("tolerations"),
                "nn": spec.get("nodeName"), "x": [(r.get("resources"), r.get("affinity")) for r in spec.get("extendedResources") or []],
@@ -142,7 +153,9 @@ class GenericScheduler:
         for name, _fn, _w in self.priorities:
             if name in LOCAL_PRIORITIES:
                 continue
-            if name == "SelectorSpreadPriority" and pi.owner is None:
+            if name == "SelectorSpreadPriority" and not pod_selectors(pi, self._lctx):
+                continue
+            if name == "ServiceSpreadingPriority" and not pod_selectors(pi, self._lctx, services_only=True):
                 continue
             if name == "NodeAffinityPriority" and not pi.preferred_terms:
                 continue
@@ -234,7 +247,8 @@ class GenericScheduler:
     async def prioritize(self, pi, nodes, ctx) -> list[float]:
         if not self.priorities and not self.extenders:
             return [1.0] * len(nodes)
-        if ctx is None and (self.custom or (self.hard_affinity_weight and self.cache.affinity_pods)):
+        if ctx is None and (self.custom or (self.hard_affinity_weight and self.cache.affinity_pods) or
+                            any(n not in LOCAL_PRIORITIES for n, _fn, _w in self.priorities)):
             ctx = self._ctx(self.cache.ready_nodes())
         total = [0.0] * len(nodes)
         # per-node scores depend only on (pod class, node state) unless a priority normalises across

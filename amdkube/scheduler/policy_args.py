@@ -62,23 +62,38 @@ def labels_presence(labels: list[str], presence: bool):
 
 
 def service_anti_affinity(label: str):
+    """ServiceAntiAffinity.CalculateAntiAffinityPriority (selector_spreading.go:185-254): the
+    first Service selecting the pod names the pods to spread; a labelled node scores
+    10 * (service pods - service pods in its label value) / service pods, an unlabelled one 0.
+    The denominator counts every service pod, wherever it runs; the per-value counts only those
+    on the nodes being scored."""
     def prio(pi, nodes, ctx=None):
-        placed = _service_pods(pi, ctx) if ctx is not None else []
+        ns = m.namespace_of(pi.pod)
+        svcs = [s for s in (ctx.services() if ctx is not None else [])
+                if m.namespace_of(s) == ns and (s.get("spec") or {}).get("selector")
+                and selector_from_set(s["spec"]["selector"]).matches(pi.labels)]
+        labeled = {ni.name: ni.labels[label] for ni in nodes if label in ni.labels}
         counts: dict[str, int] = {}
-        for _, ni in placed:
-            v = ni.labels.get(label)
-            if v is not None:
-                counts[v] = counts.get(v, 0) + 1
-        total = sum(counts.values())
+        total = 0
+        if svcs:
+            sel = selector_from_set(svcs[0]["spec"]["selector"])
+            for ni in ctx.nodes:
+                for p in ni.pods.values():
+                    if m.namespace_of(p) != ns or not sel.matches(m.labels_of(p)):
+                        continue
+                    total += 1
+                    v = labeled.get(ni.name)
+                    if v is not None:
+                        counts[v] = counts.get(v, 0) + 1
         out = []
         for ni in nodes:
-            v = ni.labels.get(label)
+            v = labeled.get(ni.name)
             if v is None:
                 out.append(0.0)
             elif total == 0:
                 out.append(MAX)
             else:
-                out.append(MAX * (total - counts.get(v, 0)) / total)
+                out.append(float(int(MAX * (total - counts.get(v, 0)) / total)))
         return out
     return prio
 

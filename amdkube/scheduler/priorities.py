@@ -3,8 +3,9 @@
 Reference: plugin/pkg/scheduler/algorithm/priorities/* — least_requested.go,
 balanced_resource_allocation.go, most_requested.go, selector_spreading.go,
 node_affinity.go, taint_toleration.go, node_prefer_avoid_pods.go (weight 10000),
-interpod_affinity.go, image_locality.go; defaults in algorithmprovider/defaults/
-defaults.go:217-260. New: GPUTopologyPriority (xGMI/NUMA subset quality + best fit, see
+interpod_affinity.go, image_locality.go, resource_limits.go; EqualPriority and
+ServiceSpreadingPriority (algorithmprovider/defaults/defaults.go:91-115); defaults at
+defaults.go:217-260. Scores are the reference's integers 0..10 where its map/reduce truncates. New: GPUTopologyPriority (xGMI/NUMA subset quality + best fit, see
 extended.topology_score) — the reference has no topology awareness.
 """
 from __future__ import annotations
@@ -61,13 +62,94 @@ def balanced_allocation(pi, nodes, ctx=None):
     return out
 
 
+ZONE_WEIGHTING = 2.0 / 3.0
+ZONE_LABEL = "failure-domain.beta.kubernetes.io/zone"
+REGION_LABEL = "failure-domain.beta.kubernetes.io/region"
+
+
+def zone_key(labels: dict) -> str:
+    """pkg/util/node/node.go GetZoneKey: region and zone joined; "" when the node has neither."""
+    region, zone = labels.get(REGION_LABEL, ""), labels.get(ZONE_LABEL, "")
+    if not region and not zone:
+        return ""
+    return region + ":\x00:" + zone
+
+
+def pod_selectors(pi, ctx, services_only=False) -> list:
+    """Selectors of the Services/RCs/RSs/StatefulSets that pick the pod, once per attempt."""
+    attr = "_svc_sel" if services_only else "_spread_sel"
+    sel = getattr(pi, attr, None)
+    if sel is None:
+        listers = getattr(ctx, "listers", None) if ctx is not None else None
+        sel = listers.selectors(pi.pod, services_only) if listers is not None else []
+        setattr(pi, attr, sel)
+    return sel
+
+
+def _spread_counts(pi, nodes, sels) -> list[int]:
+    """CalculateSpreadPriorityMap: per node, the live pods of the pod's namespace that any of the
+    selectors matches. Nodes keep pods grouped by (namespace, labels), so each distinct label set
+    is matched once per call."""
+    ns = (pi.pod.get("metadata") or {}).get("namespace") or ""
+    memo: dict = {}
+    out = []
+    for ni in nodes:
+        c = 0
+        for (gns, lk), n in ni.groups.items():
+            if gns != ns:
+                continue
+            hit = memo.get(lk)
+            if hit is None:
+                ls = dict(lk)
+                hit = memo[lk] = any(s.matches(ls) for s in sels)
+            if hit:
+                c += n
+        out.append(c)
+    return out
+
+
+def _spread_reduce(counts, nodes) -> list[float]:
+    """CalculateSpreadPriorityReduce (selector_spreading.go:119-161): fewer matching pods on the
+    node scores higher; with zone labels, 2/3 of the score comes from the node's zone total."""
+    by_zone: dict[str, int] = {}
+    zones = []
+    for c, ni in zip(counts, nodes):
+        z = zone_key(ni.labels)
+        zones.append(z)
+        if z:
+            by_zone[z] = by_zone.get(z, 0) + c
+    max_node = max(counts) if counts else 0
+    max_zone = max(by_zone.values()) if by_zone else 0
+    out = []
+    for c, z in zip(counts, zones):
+        f = MAX * (max_node - c) / max_node if max_node > 0 else MAX
+        if by_zone and z:
+            zs = MAX * (max_zone - by_zone[z]) / max_zone if max_zone > 0 else MAX
+            f = f * (1.0 - ZONE_WEIGHTING) + ZONE_WEIGHTING * zs
+        out.append(float(int(f)))
+    return out
+
+
 def selector_spread(pi, nodes, ctx=None):
-    if pi.owner is None:
+    """SelectorSpreadPriority: spread the pods selected by the same Service, RC, RS or StatefulSet
+    over nodes and zones (selector_spreading.go:34-161)."""
+    sels = pod_selectors(pi, ctx)
+    if not sels:
         return [MAX] * len(nodes)
-    uid = pi.owner.get("uid")
-    counts = [ni.owners.get(uid, 0) for ni in nodes]
-    mx = max(counts) if counts else 0
-    return [MAX * (mx - c) / mx if mx else MAX for c in counts]
+    return _spread_reduce(_spread_counts(pi, nodes, sels), nodes)
+
+
+def service_spreading(pi, nodes, ctx=None):
+    """ServiceSpreadingPriority: SelectorSpread over Services only (defaults.go:91-102)."""
+    sels = pod_selectors(pi, ctx, services_only=True)
+    if not sels:
+        return [MAX] * len(nodes)
+    return _spread_reduce(_spread_counts(pi, nodes, sels), nodes)
+
+
+def equal(pi, nodes, ctx=None):
+    """EqualPriority (core/generic_scheduler.go EqualPriorityMap): every node scores 1."""
+    return [1.0] * len(nodes)
 
 
 def node_affinity(pi, nodes, ctx=None):
@@ -151,8 +233,68 @@ def inter_pod_affinity(pi, nodes, ctx=None):
     return [MAX * (r - lo) / (hi - lo) if hi > lo else 0.0 for r in raw]
 
 
+MB = 1024 * 1024
+MIN_IMG_SIZE, MAX_IMG_SIZE = 23 * MB, 1000 * MB
+
+
+def image_score(total: int) -> float:
+    """image_locality.go calculateScoreFromSize: 0 below 23 MiB, 10 from 1000 MiB, linear
+    (integer) buckets between."""
+    if total == 0 or total < MIN_IMG_SIZE:
+        return 0.0
+    if total >= MAX_IMG_SIZE:
+        return MAX
+    return float(int(MAX) * (total - MIN_IMG_SIZE) // (MAX_IMG_SIZE - MIN_IMG_SIZE) + 1)
+
+
 def image_locality(pi, nodes, ctx=None):
-    return [0.0] * len(nodes)
+    """ImageLocalityPriority (image_locality.go:32-62): the summed size of the pod's container
+    images already present on the node (node.status.images, reported by the kubelet)."""
+    images = [c.get("image") for c in pi.spec.get("containers") or []]
+    out = []
+    for ni in nodes:
+        sizes = {}
+        for img in ((ni.node or {}).get("status") or {}).get("images") or []:
+            for name in img.get("names") or []:
+                sizes[name] = int(img.get("sizeBytes") or 0)
+        out.append(image_score(sum(sizes.get(i, 0) for i in images)))
+    return out
+
+
+def _pod_limits(pod) -> tuple[int, int]:
+    """resource_limits.go getResourceLimits: summed container limits, raised to the largest init
+    container limit (milli-CPU, memory bytes)."""
+    from ..api.quantity import Quantity
+    spec = pod.get("spec") or {}
+    cpu = mem = 0
+    for c in spec.get("containers") or []:
+        lim = (c.get("resources") or {}).get("limits") or {}
+        if "cpu" in lim:
+            cpu += Quantity(lim["cpu"]).milli_value()
+        if "memory" in lim:
+            mem += Quantity(lim["memory"]).value()
+    for c in spec.get("initContainers") or []:
+        lim = (c.get("resources") or {}).get("limits") or {}
+        if "cpu" in lim:
+            cpu = max(cpu, Quantity(lim["cpu"]).milli_value())
+        if "memory" in lim:
+            mem = max(mem, Quantity(lim["memory"]).value())
+    return cpu, mem
+
+
+def resource_limits(pi, nodes, ctx=None):
+    """ResourceLimitsPriority (resource_limits.go:37-72, gate ResourceLimitsPriorityFunction):
+    1 for a node whose allocatable CPU or memory covers the pod's limit, else 0."""
+    lim = getattr(pi, "_limits", None)
+    if lim is None:
+        lim = pi._limits = _pod_limits(pi.pod)
+    cpu, mem = lim
+    out = []
+    for ni in nodes:
+        ac, am = ni.allocatable.get("cpu", 0), ni.allocatable.get("memory", 0)
+        ok = (cpu and ac and cpu <= ac) or (mem and am and mem <= am)
+        out.append(1.0 if ok else 0.0)
+    return out
 
 
 def gpu_topology(pi, nodes, ctx=None):
@@ -169,8 +311,14 @@ PRIORITIES = {
     "NodePreferAvoidPodsPriority": node_prefer_avoid_pods,
     "InterPodAffinityPriority": inter_pod_affinity,
     "ImageLocalityPriority": image_locality,
+    "ServiceSpreadingPriority": service_spreading,
+    "EqualPriority": equal,
+    "ResourceLimitsPriority": resource_limits,      # registered only with its feature gate
     "GPUTopologyPriority": gpu_topology,
 }
+
+# registered in the reference only when the named gate is on (defaults.go:113-115)
+GATED_PRIORITIES = {"ResourceLimitsPriority": "ResourceLimitsPriorityFunction"}
 
 DEFAULT_PRIORITIES = {"SelectorSpreadPriority": 1, "InterPodAffinityPriority": 1, "LeastRequestedPriority": 1,
                       "BalancedResourceAllocation": 1, "NodePreferAvoidPodsPriority": 10000, "NodeAffinityPriority": 1,

@@ -81,19 +81,24 @@ class Scheduler:
             exts = []
         self.lock_object = (lock_object_namespace, lock_object_name)
         self.address = address
-        if not self.gates("GPUTopologyScheduling"):
-            prios = {k: v for k, v in prios.items() if k != "GPUTopologyPriority"}
         self.extenders = [HTTPExtender(e) for e in exts]
         self.cache = SchedulerCache()
         from .volumes import VolumeLister
         self.volumes = VolumeLister()
+        prios = self._gate_priorities(prios)
         self.svc_inf = None
+        self.ctl_infs: dict[str, Informer] = {}     # replicationcontrollers/replicasets/statefulsets
+        from .listers import ControllerListers
+        listers = ControllerListers(services=lambda: self.svc_inf.list() if self.svc_inf is not None else [],
+                                    rcs=lambda: self._ctl_list("replicationcontrollers"),
+                                    rss=lambda: self._ctl_list("replicasets"),
+                                    sss=lambda: self._ctl_list("statefulsets"))
         self.algo = GenericScheduler(self.cache, preds, prios, self.extenders, use_topology=self.gates("GPUTopologyScheduling"),
                                      volumes=self.volumes, volume_scheduling=self.gates("VolumeScheduling"),
                                      custom_predicates=cpreds, custom_priorities=cprios,
-                                     services=lambda: self.svc_inf.list() if self.svc_inf is not None else [],
+                                     services=listers.services, listers=listers,
                                      hard_affinity_weight=self.hard_weight)
-        self._needs_services = bool(cpreds or cprios)
+        self._set_needs(cpreds, cprios, prios)
         self.queue = SchedulingQueue(self.gates("PodPriority"))
         self.recorder = EventRecorder(client, self.name)
         self.leader_elect = leader_elect
@@ -115,6 +120,31 @@ class Scheduler:
         self.failed = 0
         self.bind_errors = 0
         self._runner = None
+
+    def _gate_priorities(self, prios: dict) -> dict:
+        """Drop priorities whose gate is off: GPUTopologyPriority (GPUTopologyScheduling) and the
+        reference's gated ResourceLimitsPriority (defaults.go:113-115); a policy that names a
+        gated-off priority is refused, as the reference's registry would not know the name."""
+        from .priorities import GATED_PRIORITIES
+        out = {}
+        for k, v in prios.items():
+            if k == "GPUTopologyPriority" and not self.gates("GPUTopologyScheduling"):
+                continue
+            gate = GATED_PRIORITIES.get(k)
+            if gate and not self.gates(gate):
+                raise ValueError(f"priority {k!r} is registered only with feature gate {gate}=true")
+            out[k] = v
+        return out
+
+    def _set_needs(self, cpreds, cprios, prios):
+        # serviceAffinity/serviceAntiAffinity arguments read Services; the spreading priorities
+        # read Services plus the controllers
+        self._needs_controllers = "SelectorSpreadPriority" in prios
+        self._needs_services = bool(cpreds or cprios) or self._needs_controllers or "ServiceSpreadingPriority" in prios
+
+    def _ctl_list(self, resource: str) -> list:
+        inf = self.ctl_infs.get(resource)
+        return inf.list() if inf is not None else []
 
     # ----------------------------------------------------------- informers
     def _responsible(self, pod) -> bool:
@@ -183,12 +213,11 @@ class Scheduler:
             raise ValueError(f"ConfigMap {ns}/{name} has no policy.cfg")
         pol = json.loads(raw)
         preds, prios, cpreds, cprios = build(pol)
-        if not self.gates("GPUTopologyScheduling"):
-            prios = {k: v for k, v in prios.items() if k != "GPUTopologyPriority"}
+        prios = self._gate_priorities(prios)
         self.extenders = [HTTPExtender(e) for e in pol.get("extenders") or []]
         self.hard_weight = int(pol.get("hardPodAffinitySymmetricWeight", self.hard_weight))
         self.algo.configure(preds, prios, cpreds, cprios, self.extenders, self.hard_weight)
-        self._needs_services = bool(cpreds or cprios)
+        self._set_needs(cpreds, cprios, prios)
 
     async def start(self):
         self.recorder.start()
@@ -224,12 +253,16 @@ class Scheduler:
             inf.add_handler(on_add=lambda o: self.queue.move_all_to_active(), on_update=self._on_volume_update)
         for inf in self.vol_infs:
             inf.start()
-        if self._needs_services:        # serviceAffinity / serviceAntiAffinity policy arguments
+        if self._needs_services:
             self.svc_inf = Informer(self.client, "services")
             self.svc_inf.start()
+        if self._needs_controllers:
+            for r in ("replicationcontrollers", "replicasets", "statefulsets"):
+                self.ctl_infs[r] = Informer(self.client, r)
+                self.ctl_infs[r].start()
         self.node_inf.start()
         await self.node_inf.wait_synced(30)
-        for inf in self.vol_infs:
+        for inf in (*self.vol_infs, *([self.svc_inf] if self.svc_inf else []), *self.ctl_infs.values()):
             await inf.wait_synced(30)
         self.pod_inf.start()
         await self.pod_inf.wait_synced(30)
@@ -237,7 +270,7 @@ class Scheduler:
     async def stop(self):
         from ..utils import cancel_and_wait
         await cancel_and_wait(list(self._tasks) + list(self._binds))
-        for inf in (self.pod_inf, self.node_inf, self.svc_inf, *getattr(self, "vol_infs", [])):
+        for inf in (self.pod_inf, self.node_inf, self.svc_inf, *self.ctl_infs.values(), *getattr(self, "vol_infs", [])):
             if inf:
                 await inf.stop()
         await self.recorder.stop()
