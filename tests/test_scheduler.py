@@ -275,20 +275,26 @@ def test_allocation_failure_tries_the_next_ranked_host(monkeypatch):
 def test_fit_index_decides_like_a_full_scan():
     """The incremental per-equivalence-class fit index (only nodes changed since the last pod of
     the class are re-checked) picks the same host, devices and failure as evaluating every node,
-    across binds, node updates (taint, removal) and pod removal."""
+    across binds, node updates (taint, removal) and pod removal — with ImageLocalityPriority on and
+    pods that differ only in their image (the image is part of the equivalence class)."""
     import asyncio
     import random
     rnd = random.Random(7)
+    images = ["img/a", "img/b", "img/c"]
 
     def world():
         nodes = [node(f"n{i}", gpus=rnd.choice((0, 2, 4, 8)), cpu=str(rnd.choice((2, 4, 8)))) for i in range(24)]
-        return sched(nodes)
+        for n in nodes:
+            n["status"]["images"] = [{"names": [im], "sizeBytes": rnd.choice((0, 100, 400, 900)) << 20}
+                                     for im in images if rnd.random() < 0.5]
+        return sched(nodes, priorities={**DEFAULT_PRIORITIES, "ImageLocalityPriority": 3})
 
     rnd.seed(7)
     c_fast, g_fast = world()
     rnd.seed(7)
     c_slow, g_slow = world()
-    g_slow._uniform_others = lambda pi: False          # always the full scan
+    g_slow._uniform_others = lambda pi: False          # always the full scan,
+    g_slow._equiv_key = lambda pi: None                 # with no equivalence cache at all
     script = random.Random(11)
     bound = []
     for step in range(160):
@@ -305,6 +311,7 @@ def test_fit_index_decides_like_a_full_scan():
             c_slow.update_node(n)
             continue
         p = pod(f"p{step}", gpus=script.choice((0, 0, 1, 2)), cpu=script.choice(("100m", "500m", "1")))
+        p["spec"]["containers"][0]["image"] = script.choice(images)
         results = []
         for c, g in ((c_fast, g_fast), (c_slow, g_slow)):
             try:
