@@ -27,7 +27,8 @@ from ..api import meta as m
 from ..api.scheme import SCHEME
 from ..store import MVCCStore, PUT
 from ..utils import greenbridge, profiling
-from ..utils.metrics import CONTENT_TYPE, MICRO_BUCKETS, Counter, Histogram, new_registry, render
+from ..utils.metrics import CONTENT_TYPE, Counter, Histogram, new_registry, render
+from ..utils.quantiles import QuantileSummary
 from ..store.storage import kv_json, kv_proto
 from . import admission as adm
 from .registry import Registry
@@ -198,10 +199,16 @@ class APIServer:
         self._rw = asyncio.Semaphore(max_mutating_in_flight) if max_mutating_in_flight else None
         self.event_ttl = event_ttl
         self.metrics = new_registry()
+        # endpoints/metrics/metrics.go:37-70: the request counter, the latency histogram
+        # (ExponentialBuckets(125000, 2, 7)) and the latency Summary (quantiles 0.5/0.9/0.99 over
+        # 5 h) that the e2e API-responsiveness check reads (metrics_util.go:264-350)
         self.m_count = Counter("apiserver_request_count", "Counter of apiserver requests broken out for each verb, API resource, client, and HTTP response contentType and code.",
-                               ["verb", "resource", "subresource", "code"], registry=self.metrics)
+                               ["verb", "resource", "subresource", "scope", "client", "contentType", "code"], registry=self.metrics)
         self.m_lat = Histogram("apiserver_request_latencies", "Response latency distribution in microseconds for each verb, resource and subresource.",
-                               ["verb", "resource", "subresource"], buckets=MICRO_BUCKETS, registry=self.metrics)
+                               ["verb", "resource", "subresource", "scope"], buckets=tuple(125000 * 2 ** i for i in range(7)),
+                               registry=self.metrics)
+        self.m_lat_summary = QuantileSummary("apiserver_request_latencies_summary", "Response latency summary in microseconds for each verb, resource and subresource.",
+                                             ["verb", "resource", "subresource", "scope"], registry=self.metrics, max_age=5 * 3600.0)
         # exact per-request latencies for the SLO report (metrics_util.go HighLatencyRequests
         # reads the apiserver's latency summary quantiles; this keeps the raw samples instead)
         self.lat_samples: collections.deque = collections.deque(maxlen=200_000)
@@ -213,6 +220,7 @@ class APIServer:
         self.app.router.add_get("/healthz/{check}", self.healthz)
         self.app.router.add_get("/version", self.version)
         self.app.router.add_get("/metrics", self.metrics_handler)
+        self.app.router.add_delete("/metrics", self.metrics_reset)
         self.app.router.add_get("/openapi/v2", self.openapi)
         self.app.router.add_get("/swagger.json", self.openapi)
         self.app.router.add_get("/api", self.api_versions)
@@ -469,6 +477,18 @@ class APIServer:
     async def metrics_handler(self, request):
         return web.Response(body=render(self.metrics), headers={"Content-Type": CONTENT_TYPE})
 
+    async def metrics_reset(self, request):
+        """DELETE /metrics (routes/metrics.go MetricsWithReset → metrics.Reset): the e2e framework
+        resets the request metrics before a measured phase (metrics_util.go ResetMetrics)."""
+        try:
+            user = await self._authenticate_async(request)
+            await self._authorize_nonresource(user, "delete", "/metrics")
+        except m.StatusError as e:
+            return _err(e)
+        for metric in (self.m_count, self.m_lat, self.m_lat_summary):
+            metric.clear()
+        return web.Response(text="metrics reset\n")
+
     async def api_versions(self, request):
         return _resp({"kind": "APIVersions", "versions": ["v1"],
                       "serverAddressByClientCIDRs": [{"clientCIDR": "0.0.0.0/0", "serverAddress": request.host}]})
@@ -532,6 +552,11 @@ class APIServer:
             where = f' in the namespace "{ns}"' if ns else " at the cluster scope"
             raise m.forbidden(f'User "{user.get("name")}" cannot {verb} {what}{" " + repr(name) if name else ""}'
                               f'{" in API group " + repr(group) if group else ""}{where}')
+
+    async def _authorize_nonresource(self, user, verb, path):
+        ok, _ = await self.authz.authorize_async(Attributes(user, verb, path=path, resource_request=False))
+        if not ok:
+            raise m.forbidden(f'User "{user.get("name")}" cannot {verb} path "{path}"')
 
     def _set_scale(self, rs, ns, name, scale: dict, user) -> dict:
         """PUT/PATCH .../scale: only spec.replicas changes; a resourceVersion in the Scale is a
@@ -604,6 +629,7 @@ class APIServer:
     async def dispatch(self, request: web.Request):
         t0 = time.perf_counter()
         verb, resource, sub, code = request.method, "", "", 500
+        scope = ""
         sem = actx = resp = None
         try:
             user = await self._authenticate_async(request)
@@ -633,6 +659,8 @@ class APIServer:
             if rs is None:
                 raise m.not_found("resource", f"{group}/{version}/{resource}")
             conv = served if served.api_version != rs.ri.api_version else None
+            # metrics.go cleanScope
+            scope = "namespace" if ns else ("resource" if name else "cluster")
             q = request.query
             is_watch = watch or q.get("watch") in ("true", "1")
             kverb = {"GET": "watch" if is_watch else ("get" if name else "list"), "POST": "create", "PUT": "update",
@@ -679,10 +707,15 @@ class APIServer:
                 sem.release()
             if actx is not None:
                 self.auditor.stage(actx, "ResponseComplete", code, getattr(request, "_read_bytes", None), resp)
-            self.m_count.labels(verb, resource or "", sub or "", str(code)).inc()
+            client = request.headers.get("User-Agent", "")
+            client = "Browser" if client.startswith("Mozilla/") else client
+            ctype = (resp.headers.get("Content-Type", "") if resp is not None else "").split(";")[0]
+            self.m_count.labels(verb, resource or "", sub or "", scope, client, ctype, str(code)).inc()
             if verb != "WATCH":
                 dt = time.perf_counter() - t0
-                self.m_lat.labels(verb, resource or "", sub or "").observe(dt * 1e6)
+                us = float(int(dt * 1e6))          # elapsed / time.Microsecond
+                self.m_lat.labels(verb, resource or "", sub or "", scope).observe(us)
+                self.m_lat_summary.labels(verb, resource or "", sub or "", scope).observe(us)
                 self.lat_samples.append((verb, resource or "", sub or "", dt))
 
     def latency_summary(self, since: int = 0) -> dict:

@@ -23,7 +23,8 @@ import grpc
 
 from ...api.helpers import (pod_extended_resource, pod_extended_resource_name, ExtendedResourceError)
 from ...grpcdesc.deviceplugin import DEVICE_PLUGINS_PATH, V1BETA1 as B
-from ...utils.metrics import Counter, Summary
+from ...utils.metrics import Counter
+from ...utils.quantiles import QuantileSummary as Summary
 from .endpoint import EndpointHandler, RegistrationError
 from .run_options import merge_container_specs
 from .stores import EndpointStore, ManagerStore, PodResourceCache

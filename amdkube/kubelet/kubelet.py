@@ -36,7 +36,8 @@ from ..client import Client, EventRecorder, Informer
 from ..deviceplugin.amd import TOPOLOGY_LABEL
 from ..grpcdesc.cri import CRI as C
 from ..utils.features import FeatureGate
-from ..utils.metrics import MICRO_BUCKETS, Counter, Gauge, Histogram, Summary, new_registry
+from ..utils.metrics import Counter, Gauge, new_registry
+from ..utils.quantiles import QuantileSummary as Summary
 from .cm import enforce_pods_cgroup, node_allocatable as reserved_allocatable, parse_reserved
 from .cri_client import CURRENT_POD, CRIClient
 from .devicemanager import AdmissionError, ManagerImpl, ManagerStub
@@ -358,8 +359,10 @@ class Kubelet:
     def _init_metrics(self):
         r = self.metrics
         self.m_pod_start = Summary("kubelet_pod_start_latency_microseconds", "Latency in microseconds for a single pod to go from pending to running.", registry=r)
-        self.m_worker = Histogram("kubelet_pod_worker_latency_microseconds", "Latency in microseconds to sync a single pod.", ["operation_type"], buckets=MICRO_BUCKETS, registry=r)
+        self.m_worker = Summary("kubelet_pod_worker_latency_microseconds", "Latency in microseconds to sync a single pod. Broken down by operation type: create, update, or sync", ["operation_type"], registry=r)
         self.m_pleg = Summary("kubelet_pleg_relist_latency_microseconds", "Latency in microseconds for relisting pods in PLEG.", registry=r)
+        self.m_pleg_interval = Summary("kubelet_pleg_relist_interval_microseconds", "Interval in microseconds between relisting in PLEG.", registry=r)
+        self.m_containers_per_pod = Summary("kubelet_containers_per_pod_count", "The number of containers per pod.", registry=r)
         self.m_rt_ops = Counter("kubelet_runtime_operations", "Cumulative number of runtime operations by operation type.", ["operation_type"], registry=r)
         self.m_rt_errs = Counter("kubelet_runtime_operations_errors", "Cumulative number of runtime operation errors by operation type.", ["operation_type"], registry=r)
         self.m_rt_lat = Summary("kubelet_runtime_operations_latency_microseconds", "Latency in microseconds of runtime operations.", ["operation_type"], registry=r)
@@ -924,6 +927,9 @@ class Kubelet:
         w = self.workers.get(uid)
         if w is None:
             w = self.workers[uid] = PodWorker(uid)
+            pod = self.pods.get(uid)
+            if pod is not None:        # kubelet.go dispatchWork on SyncPodCreate
+                self.m_containers_per_pod.observe(len((pod.get("spec") or {}).get("containers") or []))
             w.task = asyncio.create_task(self._worker_loop(w), name=f"podworker-{uid[:8]}")
         w.pending.set()
 
@@ -1501,9 +1507,13 @@ class Kubelet:
 
     # ================================================================ PLEG
     async def _relist_loop(self):
+        last = None
         while True:
             await asyncio.sleep(self.cfg.relist_period)
             t0 = time.perf_counter()
+            if last is not None:
+                self.m_pleg_interval.observe((t0 - last) * 1e6)
+            last = t0
             try:
                 await self.relist()
             except Exception as e:

@@ -5,7 +5,7 @@
   python native/build.py --sanitize # also the ASan/UBSan host builds (pause, topo self-test, sampler)
                                     # and the ThreadSanitizer build of the activity sampler
 
-Outputs: amdkube/_native/{_amdsmi,_topo,_kproto,_hipops}.<ext> and amdkube/_native/bin/{pause,
+Outputs: amdkube/_native/{_amdsmi,_topo,_kproto,_quantile,_hipops}.<ext> and amdkube/_native/bin/{pause,
 rocm-vector-add,hsa-vector-add,hbm-probe,gpu-burn,xgmi-probe[,topo-selftest-asan,pause-asan,amdkube-nsexec-asan,
 seccomp-check-asan,sampler-selftest-{asan,tsan}]}.
 Targets are rebuilt only when a source/header is newer than the output.
@@ -50,6 +50,9 @@ def targets(sanitize=False, cpu_only=False):
         (n(OUT, "_kproto" + EXT), [n("native/kproto.cpp")],
          ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wall", "-fno-strict-aliasing",
           f"-I{sysconfig.get_paths()['include']}", n("native/kproto.cpp"), "-o", "{out}"]),
+        # Prometheus Summary quantile streams (kubelet / device manager / apiserver latencies)
+        (n(OUT, "_quantile" + EXT), [n("native/quantile.cpp"), n("native/quantile_core.h")],
+         ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", *py, n("native/quantile.cpp"), "-o", "{out}"]),
         (n(OUT, "_amdsmi" + EXT), [n("native/amdsmi_shim.cpp"), n("native/sampler_core.h")],
          ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", *py, *rocm_inc, n("native/amdsmi_shim.cpp"), *rpath,
           "-lamd_smi", "-o", "{out}"]),
@@ -75,6 +78,8 @@ def targets(sanitize=False, cpu_only=False):
         t += [
             (n(BIN, "topo-selftest-asan"), [n("native/topo_selftest.cpp"), n("native/topo_core.h")],
              ["g++", "-O1", "-std=c++17", *san, n("native/topo_selftest.cpp"), "-o", "{out}"]),
+            (n(BIN, "quantile-selftest-asan"), [n("native/quantile_selftest.cpp"), n("native/quantile_core.h")],
+             ["g++", "-O1", "-std=c++17", *san, n("native/quantile_selftest.cpp"), "-o", "{out}"]),
             (n(BIN, "pause-asan"), [n("native/pause.cpp")],
              ["g++", "-O1", "-std=c++17", *san, n("native/pause.cpp"), "-o", "{out}"]),
             (n(BIN, "sampler-selftest-asan"), [n("native/sampler_selftest.cpp"), n("native/sampler_core.h")],

@@ -106,7 +106,7 @@ def test_manager_plugin_handling_and_reregistration():
         await wait_for(lambda: "example.com/fpga" not in m.store.peek())
         cap, removed = m.get_capacity()
         assert removed == ["example.com/fpga"] and m.get_capacity()[1] == []
-        assert b'kubelet_device_plugin_registration_count_total{resource_name="amd.com/gpu"} 2.0' in render(reg)
+        assert b'kubelet_device_plugin_registration_count{resource_name="amd.com/gpu"} 2.0' in render(reg)
         await p1b.stop()
         await m.stop()
     run(go())

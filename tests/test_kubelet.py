@@ -160,7 +160,7 @@ def test_kubelet_http_api_and_metrics():
                 assert [ln for ln in cad.splitlines() if ln.startswith("container_accelerator_memory_used_bytes")][0] \
                     .endswith(" 123456789")
                 met = await (await s.get(base + "/metrics")).text()
-                assert "kubelet_device_plugin_registration_count_total" in met and "kubelet_pod_start_latency_microseconds" in met
+                assert "kubelet_device_plugin_registration_count" in met and "kubelet_pod_start_latency_microseconds" in met
                 logs = await (await s.get(base + "/containerLogs/default/s/c")).text()
                 assert logs.strip().startswith("GPU-")
     run(go(), 60)
