@@ -107,6 +107,10 @@ def _err(e: m.StatusError) -> web.Response:
     return _resp(e.status(), e.code)
 
 
+_METRIC_VERBS = {"create": "POST", "update": "PUT", "patch": "PATCH", "delete": "DELETE",
+                 "deletecollection": "DELETECOLLECTION", "get": "GET", "list": "LIST", "watch": "WATCH"}
+
+
 class APIServer:
     def __init__(self, store: MVCCStore | None = None, admission_plugins=adm.DEFAULT_CHAIN, admission_config=None,
                  token_auth: dict | None = None, authorization_mode: str = "AlwaysAllow",
@@ -668,7 +672,8 @@ class APIServer:
             top_sub = sub.split("/")[0] if sub else ""
             if name and top_sub in _STREAMING_SUBS:
                 kverb = "create"   # exec/attach/portforward/proxy always need create on the subresource
-            verb = kverb.upper()
+            # the verb label the reference's metrics carry (installer.go actions + cleanVerb)
+            verb = "CONNECT" if name and top_sub in _STREAMING_SUBS else _METRIC_VERBS.get(kverb, kverb.upper())
             if self.auditor is not None:
                 actx = self.auditor.begin(request, user, kverb, group, version, resource, sub, ns, name or "")
             await self._authorize(user, kverb, resource, group, "" if not rs.ri.namespaced else ns, name or "", top_sub)
