@@ -152,7 +152,25 @@ def default_service(s: dict):
     return s
 
 
+def default_limit_range(lr: dict):
+    """SetDefaults_LimitRangeItem (pkg/apis/core/v1/defaults.go:339-369) on every Container item:
+    default <- max, defaultRequest <- default, then <- min."""
+    for i, item in enumerate((lr.get("spec") or {}).get("limits") or []):
+        for k in ("max", "min", "default", "defaultRequest", "maxLimitRequestRatio"):
+            normalize_resource_list(item.get(k))
+        if item.get("type") == "Container":
+            default, dreq = item.setdefault("default", {}), item.setdefault("defaultRequest", {})
+            for k, v in (item.get("max") or {}).items():
+                default.setdefault(k, v)
+            for k, v in default.items():
+                dreq.setdefault(k, v)
+            for k, v in (item.get("min") or {}).items():
+                dreq.setdefault(k, v)
+    return lr
+
+
 register_hooks("Pod", defaulter=default_pod)
+register_hooks("LimitRange", defaulter=default_limit_range)
 register_hooks("Node", defaulter=default_node)
 register_hooks("Namespace", defaulter=default_namespace)
 register_hooks("Service", defaulter=default_service)

@@ -69,10 +69,13 @@ class Quantity:
 
     # ------------------------------------------------------------- arithmetic
     def __add__(self, o):
-        return Quantity(self.value_ + Quantity(o).value_, self.format)
+        # Quantity.Add: a zero receiver takes the other operand's format
+        o = Quantity(o)
+        return Quantity(self.value_ + o.value_, o.format if self.value_ == 0 else self.format)
 
     def __sub__(self, o):
-        return Quantity(self.value_ - Quantity(o).value_, self.format)
+        o = Quantity(o)
+        return Quantity(self.value_ - o.value_, o.format if self.value_ == 0 else self.format)
 
     def __neg__(self):
         return Quantity(-self.value_, self.format)

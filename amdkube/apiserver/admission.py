@@ -11,9 +11,10 @@ Plugins implemented:
   * ExtendedResourceToleration — tolerate NoSchedule taints keyed by requested extended
     resources (plugin/pkg/admission/extendedresourcetoleration/admission.go:32-80); it
     also considers the fork's pod-level extendedResources.
-  * NamespaceLifecycle, NamespaceAutoProvision/Exists, LimitRanger (default requests/
-    limits), ResourceQuota (object-count + requests quota), ServiceAccount (default SA
-    name), DefaultTolerationSeconds, Priority, PodNodeSelector, AlwaysAdmit, AlwaysDeny.
+  * NamespaceLifecycle, NamespaceAutoProvision/Exists, LimitRanger (Container/Pod/PVC
+    defaults and min/max/maxLimitRequestRatio), ResourceQuota (evaluators of amdkube.quota,
+    scopes, CAS-reserved status.used), ServiceAccount (default SA name),
+    DefaultTolerationSeconds, Priority, PodNodeSelector, AlwaysAdmit, AlwaysDeny.
 """
 from __future__ import annotations
 
@@ -28,11 +29,12 @@ CREATE, UPDATE, DELETE, CONNECT = "CREATE", "UPDATE", "DELETE", "CONNECT"
 
 
 class Attributes:
-    __slots__ = ("operation", "resource", "subresource", "namespace", "name", "obj", "old", "user", "kind")
+    __slots__ = ("operation", "resource", "subresource", "namespace", "name", "obj", "old", "user", "kind", "group")
 
-    def __init__(self, operation, resource, subresource, namespace, name, obj, old=None, user=None, kind=""):
+    def __init__(self, operation, resource, subresource, namespace, name, obj, old=None, user=None, kind="", group=""):
         self.operation, self.resource, self.subresource = operation, resource, subresource
         self.namespace, self.name, self.obj, self.old, self.user, self.kind = namespace, name, obj, old, user, kind
+        self.group = group
 
 
 class Plugin:
@@ -291,78 +293,278 @@ class DefaultTolerationSeconds(Plugin):
                 tols.append({"key": key, "operator": "Exists", "effect": "NoExecute", "tolerationSeconds": self.seconds})
 
 
+LIMIT_RANGER_ANNOTATION = "kubernetes.io/limit-ranger"
+
+
+def _forbidden(a, msg: str) -> m.StatusError:
+    """admission.NewForbidden: `<resource> "<name>" is forbidden: <reason>`."""
+    return m.forbidden(f'{a.resource} "{a.name}" is forbidden: {msg}')
+
+
+def _lr_values(req, lim, enforced) -> tuple[int, int, int]:
+    """requestLimitEnforcedValues: milli-units unless a value would overflow them."""
+    vals = [Quantity(x) if x is not None else Quantity(0) for x in (req, lim, enforced)]
+    if all(v.value() <= _MAX_MILLI for v in vals):
+        return tuple(v.milli_value() for v in vals)
+    return tuple(v.value() for v in vals)
+
+
+_MAX_MILLI = (1 << 63) // 1000
+
+
+def _min_constraint(ltype, r, enforced, request, limit):
+    req, lim = request.get(r), limit.get(r)
+    rv, lv, ev = _lr_values(req, lim, enforced)
+    if req is None:
+        return f"minimum {r} usage per {ltype} is {Quantity(enforced)}.  No request is specified."
+    if rv < ev:
+        return f"minimum {r} usage per {ltype} is {Quantity(enforced)}, but request is {Quantity(req)}."
+    if lim is not None and lv < ev:
+        return f"minimum {r} usage per {ltype} is {Quantity(enforced)}, but limit is {Quantity(lim)}."
+    return None
+
+
+def _max_request_constraint(ltype, r, enforced, request):
+    req = request.get(r)
+    rv, _, ev = _lr_values(req, None, enforced)
+    if req is None:
+        return f"maximum {r} usage per {ltype} is {Quantity(enforced)}.  No request is specified."
+    if rv > ev:
+        return f"maximum {r} usage per {ltype} is {Quantity(enforced)}, but request is {Quantity(req)}."
+    return None
+
+
+def _max_constraint(ltype, r, enforced, request, limit):
+    req, lim = request.get(r), limit.get(r)
+    rv, lv, ev = _lr_values(req, lim, enforced)
+    if lim is None:
+        return f"maximum {r} usage per {ltype} is {Quantity(enforced)}.  No limit is specified."
+    if lv > ev:
+        return f"maximum {r} usage per {ltype} is {Quantity(enforced)}, but limit is {Quantity(lim)}."
+    if req is not None and rv > ev:
+        return f"maximum {r} usage per {ltype} is {Quantity(enforced)}, but request is {Quantity(req)}."
+    return None
+
+
+def _ratio_constraint(ltype, r, enforced, request, limit):
+    req, lim = request.get(r), limit.get(r)
+    rv, lv, _ = _lr_values(req, lim, enforced)
+    e = Quantity(enforced)
+    if req is None or rv == 0:
+        return f"{r} max limit to request ratio per {ltype} is {e}, but no request is specified or request is 0."
+    if lim is None or lv == 0:
+        return f"{r} max limit to request ratio per {ltype} is {e}, but no limit is specified or limit is 0."
+    observed = lv / rv
+    shown = observed
+    cap = float(e.value())
+    if e.value() <= _MAX_MILLI:
+        observed *= 1000
+        cap = float(e.milli_value())
+    if observed > cap:
+        return f"{r} max limit to request ratio per {ltype} is {e}, but provided ratio is {shown:f}."
+    return None
+
+
+def _check_item(ltype, item, request, limit, errs):
+    for r, v in (item.get("min") or {}).items():
+        e = _min_constraint(ltype, r, v, request, limit)
+        if e:
+            errs.append(e)
+    for r, v in (item.get("max") or {}).items():
+        e = _max_constraint(ltype, r, v, request, limit)
+        if e:
+            errs.append(e)
+    for r, v in (item.get("maxLimitRequestRatio") or {}).items():
+        e = _ratio_constraint(ltype, r, v, request, limit)
+        if e:
+            errs.append(e)
+
+
+def _sum_lists(lists: list[dict]) -> dict:
+    """limitranger sum(): a resource is summed only when every container sets it."""
+    keys = {k for rl in lists for k in rl}
+    out = {}
+    for k in keys:
+        if all(k in rl for rl in lists):
+            tot = sum(Quantity(rl[k]).milli_value() if k == "cpu" else Quantity(rl[k]).value() for rl in lists)
+            out[k] = f"{tot}m" if k == "cpu" else str(tot)
+    return out
+
+
+def default_container_requirements(lr: dict) -> tuple[dict, dict]:
+    """defaultContainerResourceRequirements: (default requests, default limits) of the Container
+    items. A stored LimitRange is already defaulted (SetDefaults_LimitRangeItem, in
+    amdkube.api.defaults: default <- max, defaultRequest <- default <- min)."""
+    reqs, lims = {}, {}
+    for item in (lr.get("spec") or {}).get("limits") or []:
+        if item.get("type") != "Container":
+            continue
+        reqs.update(item.get("defaultRequest") or {})
+        lims.update(item.get("default") or {})
+    return reqs, lims
+
+
 class LimitRanger(Plugin):
-    """Apply LimitRange container defaults (default / defaultRequest) and max checks."""
+    """plugin/pkg/admission/limitranger/admission.go: mutate pods with the Container defaults
+    (default / defaultRequest, recorded in the kubernetes.io/limit-ranger annotation), then
+    enforce min / max / maxLimitRequestRatio per Container (containers and init containers), per
+    Pod (the containers' sum, raised to the largest init container), and min / max storage
+    request per PersistentVolumeClaim. Runs on CREATE and UPDATE, never on subresources."""
     name = "LimitRanger"
-    operations = (CREATE,)
+    operations = (CREATE, UPDATE)
+
+    @staticmethod
+    def _supports(a) -> bool:
+        return not a.subresource and a.resource in ("pods", "persistentvolumeclaims") and a.obj is not None
 
     def admit(self, a, ctx):
-        if a.resource != "pods" or a.subresource:
+        if not self._supports(a) or a.resource != "pods":
             return
         for lr in ctx.list_objects("limitranges", a.namespace):
-            for item in (lr.get("spec") or {}).get("limits") or []:
-                if item.get("type") != "Container":
-                    continue
-                for c in a.obj.get("spec", {}).get("containers") or []:
+            reqs, lims = default_container_requirements(lr)
+            if not reqs and not lims:
+                continue
+            spec = a.obj.setdefault("spec", {})
+            notes = []
+            for kind, label in (("containers", "container"), ("initContainers", "init container")):
+                for c in spec.get(kind) or []:
                     res = c.setdefault("resources", {})
-                    for k, v in (item.get("default") or {}).items():
-                        res.setdefault("limits", {}).setdefault(k, v)
-                    for k, v in (item.get("defaultRequest") or {}).items():
-                        res.setdefault("requests", {}).setdefault(k, v)
+                    cl, cr = res.setdefault("limits", {}), res.setdefault("requests", {})
+                    set_l = sorted(k for k in lims if k not in cl)
+                    set_r = sorted(k for k in reqs if k not in cr)
+                    for k in set_l:
+                        cl[k] = lims[k]
+                    for k in set_r:
+                        cr[k] = reqs[k]
+                    if set_r:
+                        notes.append(", ".join(set_r) + f" request for {label} {c.get('name', '')}")
+                    if set_l:
+                        notes.append(", ".join(set_l) + f" limit for {label} {c.get('name', '')}")
+                    if not cl:
+                        res.pop("limits")
+                    if not cr:
+                        res.pop("requests")
+            if notes:
+                a.obj.setdefault("metadata", {}).setdefault("annotations", {})[LIMIT_RANGER_ANNOTATION] = \
+                    "LimitRanger plugin set: " + "; ".join(notes)
 
     def validate(self, a, ctx):
-        if a.resource != "pods" or a.subresource:
+        if not self._supports(a):
             return
         for lr in ctx.list_objects("limitranges", a.namespace):
-            for item in (lr.get("spec") or {}).get("limits") or []:
-                if item.get("type") != "Container":
-                    continue
-                for c in a.obj.get("spec", {}).get("containers") or []:
-                    lim = (c.get("resources") or {}).get("limits") or {}
-                    for k, mx in (item.get("max") or {}).items():
-                        if k in lim and Quantity(lim[k]) > Quantity(mx):
-                            raise m.forbidden(f"maximum {k} usage per Container is {mx}, but limit is {lim[k]}")
+            errs: list[str] = []
+            items = (lr.get("spec") or {}).get("limits") or []
+            if a.resource == "persistentvolumeclaims":
+                reqs = (((a.obj.get("spec") or {}).get("resources") or {}).get("requests") or {})
+                for item in items:
+                    if item.get("type") != "PersistentVolumeClaim":
+                        continue
+                    for r, v in (item.get("min") or {}).items():
+                        e = _min_constraint("PersistentVolumeClaim", r, v, reqs, {})
+                        if e:
+                            errs.append(e)
+                    for r, v in (item.get("max") or {}).items():
+                        e = _max_request_constraint("PersistentVolumeClaim", r, v, reqs)
+                        if e:
+                            errs.append(e)
+            else:
+                spec = a.obj.get("spec") or {}
+                for item in items:
+                    t = item.get("type")
+                    if t == "Container":
+                        for c in (spec.get("containers") or []) + (spec.get("initContainers") or []):
+                            res = c.get("resources") or {}
+                            _check_item("Container", item, res.get("requests") or {}, res.get("limits") or {}, errs)
+                    elif t == "Pod":
+                        cs = spec.get("containers") or []
+                        preq = _sum_lists([((c.get("resources") or {}).get("requests") or {}) for c in cs])
+                        plim = _sum_lists([((c.get("resources") or {}).get("limits") or {}) for c in cs])
+                        for c in spec.get("initContainers") or []:
+                            res = c.get("resources") or {}
+                            for dst, src in ((preq, res.get("requests") or {}), (plim, res.get("limits") or {})):
+                                for k, v in src.items():
+                                    if k not in dst or Quantity(dst[k]) < Quantity(v):
+                                        dst[k] = v
+                        _check_item("Pod", item, preq, plim, errs)
+            if errs:
+                raise _forbidden(a, errs[0] if len(errs) == 1 else "[" + ", ".join(errs) + "]")
 
 
 class ResourceQuota(Plugin):
-    """Enforce `pods`, `count/<res>`, `requests.<r>` and extended-resource hard limits."""
+    """plugin/pkg/admission/resourcequota (controller.go checkRequest :372-517): for every quota
+    in the namespace that the object's evaluator matches (a limited resource name, every scope),
+    require the quota's status to be populated, check the container constraints, and charge the
+    object's usage (its delta on UPDATE) against status.used; the charge is written back to the
+    quota's status with a compare-and-swap on the quota object, re-checked against the current
+    status on every CAS miss, so concurrent admissions (on one apiserver or several sharing an
+    etcd) serialize on the quota and can never both take its last unit."""
     name = "ResourceQuota"
-    operations = (CREATE,)
+    operations = (CREATE, UPDATE)
 
     def validate(self, a, ctx):
-        if a.subresource or not a.namespace:
+        if a.subresource or not a.namespace or a.obj is None:
             return
-        quotas = ctx.list_objects("resourcequotas", a.namespace)
+        from .. import quota as Q
+        ev = Q.evaluator_for(a.resource, a.group)
+        if a.operation not in ev.operations:
+            return
+        quotas = [qq for qq in ctx.list_objects("resourcequotas", a.namespace) if ev.matches(qq, a.obj)]
         if not quotas:
             return
-        pods = [p for p in ctx.list_objects("pods", a.namespace)
-                if (p.get("status") or {}).get("phase") not in ("Succeeded", "Failed")] if a.resource == "pods" else []
-        for q in quotas:
-            hard = (q.get("spec") or {}).get("hard") or {}
-            for k, v in hard.items():
-                lim = Quantity(v)
-                if a.resource == "pods" and k == "pods" and len(pods) + 1 > lim.value():
-                    raise m.forbidden(f'exceeded quota: {m.name_of(q)}, requested: pods=1, used: pods={len(pods)}, limited: pods={v}')
-                if k == f"count/{a.resource}" and len(ctx.list_objects(a.resource, a.namespace)) + 1 > lim.value():
-                    raise m.forbidden(f"exceeded quota: {m.name_of(q)}, requested: {k}=1, limited: {k}={v}")
-                if a.resource == "pods" and (k.startswith("requests.") or is_extended_resource_name(k)):
-                    r = k[len("requests."):] if k.startswith("requests.") else k
-                    used = sum(_pod_usage(p, r) for p in pods)
-                    want = _pod_usage(a.obj, r)
-                    if want and used + want > (lim.milli_value() if r == "cpu" else lim.value()):
-                        raise m.forbidden(f"exceeded quota: {m.name_of(q)}, requested: {k}={want}, used: {k}={used}, limited: {k}={v}")
+        for qq in quotas:
+            hard_names = list(((qq.get("status") or {}).get("hard") or {}))
+            err = ev.constraints(ev.matching_resources(hard_names), a.obj)
+            if err:
+                raise _forbidden(a, f"failed quota: {m.name_of(qq)}: {err}")
+            if not Q.has_usage_stats(qq):
+                raise _forbidden(a, f"status unknown for quota: {m.name_of(qq)}")
+        delta = Q.pod_usage(a.obj) if ev is Q.POD_EVALUATOR else ev.usage(a.obj)
+        neg = Q.negative(delta)
+        if neg:
+            raise _forbidden(a, f"quota usage is negative for resource(s): {', '.join(neg)}")
+        if a.operation == UPDATE and a.old is not None:
+            prev = Q.pod_usage(a.old) if ev is Q.POD_EVALUATOR else ev.usage(a.old)
+            delta = Q.subtract_non_negative(delta, prev)
+        if Q.is_zero(delta):
+            return
+        charged = []
+        try:
+            for qq in quotas:
+                self._charge(ctx, Q, qq, delta, a)
+                charged.append(qq)
+        except m.StatusError:
+            for qq in charged:             # give back what an earlier quota already took
+                try:
+                    self._charge(ctx, Q, qq, delta, a, refund=True)
+                except m.StatusError:
+                    pass                   # the quota controller recomputes usage anyway
+            raise
 
+    @staticmethod
+    def _charge(ctx, Q, quota, delta, a, refund=False):
+        name = m.name_of(quota)
 
-def _pod_usage(pod, r):
-    req = pod_requests(pod)
-    if r in req:
-        return req[r]
-    n = 0
-    for pres in (pod.get("spec") or {}).get("extendedResources") or []:
-        lim = (pres.get("resources") or {}).get("limits") or {}
-        if r in lim:
-            n += Quantity(lim[r]).value()
-    return n
+        def apply(cur):
+            if cur is None:
+                raise _forbidden(a, f"status unknown for quota: {name}")
+            st = cur.get("status") or {}
+            hard = Q.parse_list(st.get("hard"))
+            used = Q.parse_list(st.get("used"))
+            requested = Q.mask(delta, hard)
+            if not requested:
+                return None
+            if refund:
+                new_used = Q.subtract_non_negative(used, requested)
+            else:
+                new_used = Q.add(used, requested)
+                ok, exceeded = Q.less_than_or_equal(Q.mask(new_used, requested), hard)
+                if not ok:
+                    raise _forbidden(a, f"exceeded quota: {name}, requested: {Q.pretty(Q.mask(requested, exceeded))}, "
+                                        f"used: {Q.pretty(Q.mask(used, exceeded))}, limited: {Q.pretty(Q.mask(hard, exceeded))}")
+            out = m.deepcopy(cur)
+            out.setdefault("status", {})["used"] = {**(st.get("used") or {}), **Q.format_list(Q.mask(new_used, requested))}
+            return out
+        ctx.guaranteed_update_object("resourcequotas", m.namespace_of(quota), name, apply)
 
 
 class Priority(Plugin):

@@ -237,7 +237,8 @@ class ResourceStore:
             spec = obj.setdefault("spec", {})
             spec["username"], spec["uid"] = user.get("name", ""), user.get("uid", "")
             spec["groups"] = list(user.get("groups") or [])
-        attrs = adm.Attributes(adm.CREATE, ri.plural, "", md.get("namespace", ""), md.get("name", ""), obj, None, user, ri.kind)
+        attrs = adm.Attributes(adm.CREATE, ri.plural, "", md.get("namespace", ""), md.get("name", ""), obj, None, user, ri.kind,
+                               ri.group)
         self.api.admission.admit(attrs, self.api)
         SCHEME.default(obj)  # admission may add fields (e.g. ResourceV2) that need defaults
         errs = SCHEME.validate(obj)
@@ -352,7 +353,8 @@ class ResourceStore:
                 raise m.bad_request("the name of the object does not match the name on the URL")
             self._prepare_update(new, cur, subresource)
             SCHEME.default(new)
-            attrs = adm.Attributes(adm.UPDATE, self.ri.plural, subresource, ns, name, new, cur, user, self.ri.kind)
+            attrs = adm.Attributes(adm.UPDATE, self.ri.plural, subresource, ns, name, new, cur, user, self.ri.kind,
+                                   self.ri.group)
             self.api.admission.admit(attrs, self.api)
             errs = SCHEME.validate(new, cur) if not subresource else []
             if self.ri.plural == "pods" and subresource == "status":
@@ -387,7 +389,7 @@ class ResourceStore:
         """Returns (obj, deleted_now)."""
         key = self.key(ns, name)
         cur = self.storage.get(key)
-        attrs = adm.Attributes(adm.DELETE, self.ri.plural, "", ns, name, None, cur, user, self.ri.kind)
+        attrs = adm.Attributes(adm.DELETE, self.ri.plural, "", ns, name, None, cur, user, self.ri.kind, self.ri.group)
         self.api.admission.admit(attrs, self.api)
         self.api.admission.validate(attrs, self.api)
         md = cur.get("metadata") or {}
@@ -494,6 +496,14 @@ class Registry:
     def plural_for_kind(self, api_version, kind):
         ri = SCHEME.for_kind(api_version, kind)
         return ri.plural if ri is not None else None
+
+    def guaranteed_update_object(self, plural, ns, name, try_update, group=""):
+        """Read-modify-CAS an object straight in storage (no admission, no validation): the
+        ResourceQuota admission's status reservation (controller.go UpdateQuotaStatus)."""
+        for (g, p), r in self.resources.items():
+            if p == plural and (not group or g == group):
+                return r.storage.guaranteed_update(r.key(ns, name), try_update)
+        raise m.not_found(plural, name)
 
     def get_object(self, plural, ns, name):
         for (g, p), r in self.resources.items():

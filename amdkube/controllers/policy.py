@@ -7,11 +7,11 @@ Reference:
     matching pods not being deleted, disruptionsAllowed = max(currentHealthy -
     desiredHealthy, 0) minus pods evicted (status.disruptedPods) but not yet gone; entries
     older than 2 min expire.
-  * pkg/controller/resourcequota/resource_quota_controller.go + pkg/quota/evaluator/core —
-    status.used for pods, count/<resource>, services, configmaps, secrets,
-    persistentvolumeclaims, replicationcontrollers, resourcequotas and requests.* /
-    limits.* of non-terminal pods; status.hard mirrors spec.hard. Extended resources
-    (amd.com/gpu) count from the device-granular spec.extendedResources too.
+  * pkg/controller/resourcequota/resource_quota_controller.go over amdkube.quota (the
+    pkg/quota/evaluator/core evaluators): status.used for pods (compute, requests.*, limits.*,
+    scopes), services (nodeports, loadbalancers), PVCs (storage, per StorageClass) and object
+    counts; status.hard mirrors spec.hard. Extended resources (amd.com/gpu) count from the
+    device-granular spec.extendedResources too.
   * pkg/controller/ttl/ttl_controller.go — node annotation node.alpha.kubernetes.io/ttl from
     cluster size (0 s up to 100 nodes, 15 ≤ 500, 30 ≤ 1000, 60 ≤ 2000, 300 ≤ 5000, else 600).
   * pkg/controller/clusterroleaggregation — a ClusterRole with aggregationRule gets the union
@@ -23,9 +23,8 @@ import math
 import time
 
 from ..api import meta as m
-from ..api.helpers import is_pod_ready, is_pod_terminal, pod_requests
+from ..api.helpers import is_pod_ready, is_pod_terminal
 from ..api.labels import selector_from_label_selector
-from ..api.quantity import Quantity
 from .base import Controller, split_key
 
 DISRUPTED_TIMEOUT = 120.0
@@ -128,39 +127,18 @@ class DisruptionController(Controller):
 
 
 # ------------------------------------------------------------------------ quota usage
-def _pod_resource_usage(pod) -> dict[str, int]:
-    out: dict[str, int] = {}
-    spec = pod.get("spec") or {}
-    for c in spec.get("containers") or []:
-        res = c.get("resources") or {}
-        for kind in ("requests", "limits"):
-            for r, v in (res.get(kind) or {}).items():
-                q = Quantity(v)
-                n = q.milli_value() if r == "cpu" else q.value()
-                out[f"{kind}.{r}"] = out.get(f"{kind}.{r}", 0) + n
-    for pres in spec.get("extendedResources") or []:
-        for kind in ("requests", "limits"):
-            for r, v in ((pres.get("resources") or {}).get(kind) or {}).items():
-                out[f"{kind}.{r}"] = out.get(f"{kind}.{r}", 0) + Quantity(v).value()
-    for r, v in pod_requests(pod).items():
-        out.setdefault(f"requests.{r}", v)
-    for k in [k for k in out if k.startswith("requests.")]:
-        out[k[len("requests."):]] = out[k]   # bare "cpu" / "amd.com/gpu" mean requests
-    return out
-
-
-def _fmt(name: str, v: int) -> str:
-    if name.endswith("cpu"):
-        return f"{v}m" if v % 1000 else str(v // 1000)
-    return str(v)
-
-
-COUNTED = {"services": "services", "configmaps": "configmaps", "secrets": "secrets",
-           "persistentvolumeclaims": "persistentvolumeclaims", "replicationcontrollers": "replicationcontrollers",
-           "resourcequotas": "resourcequotas"}
+# object kinds whose count a quota can limit: (group, plural); the legacy names and count/<res>
+COUNTED = {("", "services"), ("", "configmaps"), ("", "secrets"), ("", "persistentvolumeclaims"),
+           ("", "replicationcontrollers"), ("", "resourcequotas"), ("apps", "deployments"), ("apps", "replicasets"),
+           ("apps", "statefulsets"), ("apps", "daemonsets"), ("batch", "jobs"), ("batch", "cronjobs")}
 
 
 class ResourceQuotaController(Controller):
+    """pkg/controller/resourcequota/resource_quota_controller.go: status.hard := spec.hard and
+    status.used := the namespace's usage under amdkube.quota's evaluators and the quota's scopes.
+    A quota is re-synced when its spec.hard changes (never on a status-only update: those are the
+    admission plugin's reservations, :118-130), when an object it counts changes, and every
+    30 s (the full resync that settles reservations of objects that never got created)."""
     name = "resourcequota"
     resync = 30.0
 
@@ -168,11 +146,21 @@ class ResourceQuotaController(Controller):
         f = self.mgr.factory
         self.q_inf = f.informer("resourcequotas")
         self.pod_inf = self.mgr.pods
-        self.count_infs = {p: f.informer(p) for p in COUNTED}
-        self.q_inf.add_handler(on_add=self.enqueue, on_update=lambda o, n: self.enqueue(n))
-        self.pod_inf.add_handler(on_add=self._ns, on_update=lambda o, n: self._ns(n), on_delete=self._ns)
+        self.count_infs = {gr: f.informer(gr[1]) for gr in COUNTED}
+        self.q_inf.add_handler(on_add=self.enqueue, on_update=self._quota_update)
+        self.pod_inf.add_handler(on_add=self._ns, on_update=self._pod_update, on_delete=self._ns)
         for inf in self.count_infs.values():
-            inf.add_handler(on_add=self._ns, on_delete=self._ns)
+            inf.add_handler(on_add=self._ns, on_update=lambda o, n: self._ns(n), on_delete=self._ns)
+
+    def _quota_update(self, old, new):
+        if (old.get("spec") or {}) != (new.get("spec") or {}) or not (new.get("status") or {}).get("hard"):
+            self.enqueue(new)
+
+    def _pod_update(self, old, new):
+        # replenishment: a pod that turns terminal (or starts deleting) frees its usage
+        if is_pod_terminal(new) != is_pod_terminal(old) or \
+                bool((new.get("metadata") or {}).get("deletionTimestamp")) != bool((old.get("metadata") or {}).get("deletionTimestamp")):
+            self._ns(new)
 
     def _ns(self, obj):
         ns = m.namespace_of(obj)
@@ -180,26 +168,20 @@ class ResourceQuotaController(Controller):
             if m.namespace_of(q) == ns:
                 self.enqueue(q)
 
+    def _objects(self, ns):
+        def lister(group, resource):
+            inf = self.pod_inf if (group, resource) == ("", "pods") else self.count_infs.get((group, resource))
+            return [o for o in inf.list() if m.namespace_of(o) == ns] if inf is not None else []
+        return lister
+
     async def sync(self, key):
+        from .. import quota as Q
         q = self.q_inf.get(key)
         if q is None:
             return
         ns, name = split_key(key)
         hard = (q.get("spec") or {}).get("hard") or {}
-        pods = [p for p in self.pod_inf.list() if m.namespace_of(p) == ns and not is_pod_terminal(p)]
-        usage: dict[str, int] = {}
-        for p in pods:
-            for k, v in _pod_resource_usage(p).items():
-                usage[k] = usage.get(k, 0) + v
-        used = {}
-        for r in hard:
-            if r in ("pods", "count/pods"):
-                used[r] = str(len(pods))
-            elif r in COUNTED or (r.startswith("count/") and r[6:] in COUNTED):
-                plural = r[6:] if r.startswith("count/") else r
-                used[r] = str(sum(1 for o in self.count_infs[plural].list() if m.namespace_of(o) == ns))
-            else:
-                used[r] = _fmt(r, usage.get(r, 0))
+        used = Q.format_list(Q.calculate_usage(q, self._objects(ns)))
         st = {"hard": dict(hard), "used": used}
         if (q.get("status") or {}) != st:
             await self.client.patch("resourcequotas", name, {"status": st}, ns, sub="status")

@@ -1,0 +1,182 @@
+"""A small evaluator for the Go expressions table-driven reference tests are written in.
+
+The reference's `_test.go` tables are composite literals built from a handful of local helper
+calls (`validPod("x", 2, getResourceRequirements(getComputeResourceList("100m", ""), ...))`).
+`hack/extract_*_cases.py` scripts feed a test file's table through this evaluator with Python
+versions of those helpers, and write the result as a JSON fixture that amdkube's tests replay;
+no case is retyped by hand.
+
+Supported: string/int/float/bool literals, identifiers (qualified: `api.LimitTypePod`), calls,
+`&T{...}` / `T{...}` / `[]T{...}` / `map[K]V{...}` composite literals (keyed -> dict, positional
+-> list), `nil`, comments. Anything else raises, so a table the evaluator cannot read fails
+the extraction loudly instead of being skipped.
+"""
+from __future__ import annotations
+
+import re
+
+_TOKEN = re.compile(r"""
+    (?P<ws>\s+|//[^\n]*|/\*.*?\*/)
+  | (?P<str>"(?:[^"\\]|\\.)*"|`[^`]*`)
+  | (?P<num>-?\d+(?:\.\d+)?(?:[eE][-+]?\d+)?)
+  | (?P<ident>[A-Za-z_][A-Za-z0-9_]*(?:\.[A-Za-z_][A-Za-z0-9_]*)*)
+  | (?P<punct>\[\]|[(){}\[\],:&*=])
+""", re.S | re.X)
+
+
+def tokenize(src: str) -> list[tuple[str, str]]:
+    out, pos = [], 0
+    while pos < len(src):
+        mt = _TOKEN.match(src, pos)
+        if mt is None:
+            raise SyntaxError(f"goexpr: cannot tokenize at {src[pos:pos + 40]!r}")
+        pos = mt.end()
+        kind = mt.lastgroup
+        if kind != "ws":
+            out.append((kind, mt.group(kind)))
+    return out
+
+
+class Evaluator:
+    def __init__(self, funcs: dict | None = None, names: dict | None = None):
+        self.funcs = dict(funcs or {})
+        self.names = {"nil": None, "true": True, "false": False, **(names or {})}
+
+    # ------------------------------------------------------------------ driver
+    def eval(self, src: str):
+        self.toks, self.i = tokenize(src), 0
+        v = self.expr()
+        if self.i != len(self.toks):
+            raise SyntaxError(f"goexpr: trailing tokens {self.toks[self.i:self.i + 5]}")
+        return v
+
+    def peek(self, k=0):
+        j = self.i + k
+        return self.toks[j] if j < len(self.toks) else ("eof", "")
+
+    def take(self, val=None):
+        t = self.peek()
+        if val is not None and t[1] != val:
+            raise SyntaxError(f"goexpr: expected {val!r}, got {t}")
+        self.i += 1
+        return t
+
+    # ------------------------------------------------------------------ grammar
+    def expr(self):
+        kind, val = self.peek()
+        if val == "&":
+            self.take()
+            return self.expr()
+        if kind == "str":
+            self.take()
+            return _unquote(val)
+        if kind == "num":
+            self.take()
+            return float(val) if any(c in val for c in ".eE") else int(val)
+        if val == "[]":
+            self.take()
+            self.type_name()
+            return self.literal_body()
+        if val == "{":
+            return self.literal_body()
+        if kind == "ident":
+            if val == "map" and self.peek(1)[1] == "[":
+                self.type_name()
+                return self.literal_body()
+            self.take()
+            nxt = self.peek()[1]
+            if nxt == "(":
+                args = self.args()
+                fn = self.funcs.get(val)
+                if fn is None:
+                    raise NameError(f"goexpr: no helper for {val}()")
+                return fn(*args)
+            if nxt == "{":
+                return self.literal_body()
+            if val in self.names:
+                return self.names[val]
+            raise NameError(f"goexpr: unknown name {val}")
+        raise SyntaxError(f"goexpr: unexpected {kind} {val!r}")
+
+    def type_name(self):
+        """Skip a type: *pkg.T, []T, map[K]V."""
+        while True:
+            kind, val = self.peek()
+            if val in ("*", "[]"):
+                self.take()
+                continue
+            if val == "map":
+                self.take()
+                self.take("[")
+                self.type_name()
+                self.take("]")
+                continue
+            if kind == "ident":
+                self.take()
+                return
+            raise SyntaxError(f"goexpr: bad type at {val!r}")
+
+    def args(self):
+        self.take("(")
+        out = []
+        while self.peek()[1] != ")":
+            out.append(self.expr())
+            if self.peek()[1] == ",":
+                self.take()
+        self.take(")")
+        return out
+
+    def literal_body(self):
+        self.take("{")
+        keyed, items = None, []
+        while self.peek()[1] != "}":
+            if self.peek(1)[1] == ":" and self.peek()[0] in ("ident", "str"):
+                k = self.take()[1]
+                k = _unquote(k) if k.startswith(('"', "`")) else k
+                self.take(":")
+                keyed = keyed if keyed is not None else {}
+                keyed[k] = self.expr()
+            else:
+                items.append(self.expr())
+            if self.peek()[1] == ",":
+                self.take()
+        self.take("}")
+        if keyed is not None:
+            return keyed
+        return items
+
+
+def _unquote(s: str) -> str:
+    if s.startswith("`"):
+        return s[1:-1]
+    return bytes(s[1:-1], "utf-8").decode("unicode_escape")
+
+
+def block_after(src: str, anchor: str, start: int = 0) -> tuple[str, int]:
+    """The balanced `{...}` literal that starts at the first `{` after `anchor` (inclusive), and
+    the offset just past it. String literals and comments are skipped while balancing."""
+    i = src.index(anchor, start)
+    j = src.index("{", i + len(anchor) - 1)
+    depth, k = 0, j
+    while k < len(src):
+        c = src[k]
+        if c == '"':
+            k += 1
+            while src[k] != '"':
+                k += 2 if src[k] == "\\" else 1
+        elif c == "`":
+            k = src.index("`", k + 1)
+        elif src.startswith("//", k):
+            k = src.index("\n", k)
+        elif c == "{":
+            depth += 1
+        elif c == "}":
+            depth -= 1
+            if depth == 0:
+                return src[j:k + 1], k + 1
+        k += 1
+    raise SyntaxError(f"unbalanced literal after {anchor!r}")
+
+
+def line_of(src: str, offset: int) -> int:
+    return src.count("\n", 0, offset) + 1

@@ -307,6 +307,11 @@ async def test_quota_serviceaccounts_tokens_rbac(tmp_path):
             # resource quota usage
             await admin.create({"apiVersion": "v1", "kind": "ResourceQuota", "metadata": {"name": "q"},
                                 "spec": {"hard": {"pods": "10", "configmaps": "5", "requests.cpu": "4", "amd.com/gpu": "8"}}}, "team")
+
+            async def populated():     # e2e waitForResourceQuota: admission needs status.used first
+                q = await admin.get("resourcequotas", "q", "team")
+                return q if (q.get("status") or {}).get("used") else None
+            await until(populated)
             await admin.create({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "cm"}, "data": {}}, "team")
             await admin.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p"},
                                 "spec": {"containers": [{"name": "c", "image": "x", "resources": {
