@@ -230,6 +230,20 @@ class ResourceStore:
         if self.generation:
             md["generation"] = 1
         SCHEME.default(obj)
+        key = self.key(md.get("namespace", ""), md["name"])
+        try:
+            out = self._create_checked(key, obj, md, user, dry_run)
+        finally:
+            if ri.plural == "services":      # allocations of a create that did not commit go back
+                self.api.services.release_pending(key)
+        if dry_run:
+            return out
+        if self.ri.plural == "pods":
+            POD_TRACE(md.get("uid", ""), "api_created")
+        return out
+
+    def _create_checked(self, key, obj, md, user, dry_run):
+        ri = self.ri
         self.prepare_for_create(obj)
         if ri.plural == "certificatesigningrequests" and user is not None:
             # certificates/strategy.go PrepareForCreate: the requester is who authenticated, not
@@ -247,10 +261,7 @@ class ResourceStore:
         self.api.admission.validate(attrs, self.api)
         if dry_run:
             return obj
-        out = self.storage.create(self.key(md.get("namespace", ""), md["name"]), obj)
-        if self.ri.plural == "pods":
-            POD_TRACE(md.get("uid", ""), "api_created")
-        return out
+        return self.storage.create(key, obj)
 
     def prepare_for_create(self, obj):
         p = self.ri.plural
@@ -373,7 +384,11 @@ class ResourceStore:
                     delete_after[0] = True
             return new
 
-        res = self.storage.guaranteed_update(key, try_update, precond_rv=precond_rv, ignore_not_found=create_on_update)
+        try:
+            res = self.storage.guaranteed_update(key, try_update, precond_rv=precond_rv, ignore_not_found=create_on_update)
+        finally:
+            if self.ri.plural == "services":
+                self.api.services.release_pending(key)
         if created[0]:
             return self.create(ns, obj, user), True
         if res is None:
@@ -459,6 +474,8 @@ class Registry:
             self.resources[(ri.group, ri.plural)] = ResourceStore(self, ri)
         # node -> rname -> device id -> pod key ; pod key -> list[(node, rname, id)]
         self.device_index: dict[str, dict[str, dict[str, str]]] = {}
+        self._device_claims: dict[tuple[str, str, str], str] = {}   # (node, resource, id) -> binding pod (in flight)
+        self._claims_by_pod: dict[str, list] = {}
         self._pod_devices: dict[str, list[tuple[str, str, str]]] = {}
         store.commit_hooks.append(self._on_commit)
         self._rebuild_index()
@@ -619,8 +636,16 @@ class Registry:
             set_condition(pod, {"type": "PodScheduled", "status": "True"}, m.now_rfc3339())
             return pod
 
-        pods.storage.guaranteed_update(key, assign, precond_uid=(binding.get("metadata") or {}).get("uid"))
+        try:
+            pods.storage.guaranteed_update(key, assign, precond_uid=(binding.get("metadata") or {}).get("uid"))
+        finally:
+            self._release_device_claims(key)
         return m.success_status()
+
+    def _release_device_claims(self, pod_key: str):
+        for slot in self._claims_by_pod.pop(pod_key, ()):
+            if self._device_claims.get(slot) == pod_key:
+                del self._device_claims[slot]
 
     def _check_device_binding(self, pod, pres_list, ext, node, node_name, pod_key):
         name = m.name_of(pod)
@@ -653,9 +678,16 @@ class Registry:
                     raise m.invalid("Binding", name, [f"target.extendedResourceBinding[{pname}]: Invalid value: device {did!r} of {rname} does not exist on node {node_name}"])
                 if (dev.get("health") or HEALTHY) != HEALTHY:
                     raise m.conflict("pods", name, f"device {did} of {rname} on node {node_name} is Unhealthy")
-                owner = used.get(did)
+                owner = used.get(did) or self._device_claims.get((node_name, rname, did))
                 if owner and owner != pod_key:
                     raise m.conflict("pods", name, f"device {did} of {rname} on node {node_name} is already assigned to pod {owner.split('/', 3)[-1]}")
                 if (rname, did) in claimed:
                     raise m.invalid("Binding", name, [f"device {did} bound twice in one binding"])
                 claimed.add((rname, did))
+        # claim the devices until this bind's write settles: over a bridged store other binds
+        # run while it is in flight, and the device index moves only on commit
+        slots = self._claims_by_pod.setdefault(pod_key, [])
+        for rname, did in claimed:
+            slot = (node_name, rname, did)
+            if self._device_claims.setdefault(slot, pod_key) == pod_key and slot not in slots:
+                slots.append(slot)

@@ -40,6 +40,10 @@ class ServiceAllocator:
         self.ips: dict[str, str] = {}          # ip -> service key
         self.ports: dict[tuple[str, int], str] = {}  # (proto, port) -> service key
         self._by_key: dict[str, tuple[list, list]] = {}
+        # allocations handed to a write that has not committed yet: over a bridged store
+        # (Etcd3Store group commit) other requests run while it is in flight, and must not be
+        # given the same address or port. Released once the write settled (release_pending).
+        self._pending: dict[str, set] = {}
         self._rng = random.Random()
         # the first usable address is reserved for the `kubernetes` service (master.go
         # ServiceIPRange: first IP of the range)
@@ -71,6 +75,22 @@ class ServiceAllocator:
                 ports.append(k)
         self._by_key[key] = (ips, ports)
 
+    def _reserve(self, key: str, kind: str, v):
+        table = self.ips if kind == "ip" else self.ports
+        if v not in table:
+            table[v] = key
+            self._pending.setdefault(key, set()).add((kind, v))
+
+    def release_pending(self, key: str):
+        """Drop `key`'s in-flight reservations that its committed object does not hold (the
+        write failed, or allocated something it then did not keep)."""
+        ips, ports = self._by_key.get(key, ([], []))
+        for kind, v in self._pending.pop(key, ()):
+            if kind == "ip" and v not in ips and self.ips.get(v) == key:
+                del self.ips[v]
+            elif kind == "port" and v not in ports and self.ports.get(v) == key:
+                del self.ports[v]
+
     def rebuild(self, kvs):
         for kv in kvs:
             self.index(kv.key, decode_kv(kv.value))
@@ -94,6 +114,7 @@ class ServiceAllocator:
                                                  f"The range of valid IPs is {self.net}"])
             if str(ip) in self.ips and self.ips[str(ip)] != key:
                 raise m.invalid("Service", key.rsplit("/", 1)[-1], [f"spec.clusterIP: Invalid value: {requested!r}: provided IP is already allocated"])
+            self._reserve(key, "ip", str(ip))
             return str(ip)
         first = int(self.net.network_address) + (1 if self.net.version == 4 and self.net.prefixlen < 31 else 0)
         last = int(self.net.broadcast_address) - (1 if self.net.version == 4 and self.net.prefixlen < 31 else 0)
@@ -102,6 +123,7 @@ class ServiceAllocator:
         for i in range(size):
             ip = str(ipaddress.ip_address(first + (start + i) % size))
             if ip not in self.ips:
+                self._reserve(key, "ip", ip)
                 return ip
         raise m.StatusError(500, "InternalError", "failed to allocate a serviceIP: range is full")
 
@@ -114,12 +136,14 @@ class ServiceAllocator:
             owner = self.ports.get((proto, requested))
             if (owner and owner != key) or (proto, requested) in taken:
                 raise m.invalid("Service", key.rsplit("/", 1)[-1], [f"spec.ports[].nodePort: Invalid value: {requested}: provided port is already allocated"])
+            self._reserve(key, "port", (proto, requested))
             return requested
         size = hi - lo + 1
         start = self._rng.randrange(size)
         for i in range(size):
             p = lo + (start + i) % size
             if (proto, p) not in self.ports and (proto, p) not in taken:
+                self._reserve(key, "port", (proto, p))
                 return p
         raise m.StatusError(500, "InternalError", "failed to allocate a nodePort: range is full")
 

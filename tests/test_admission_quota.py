@@ -436,3 +436,66 @@ async def test_concurrent_creates_over_etcd_admit_exactly_the_quota():
                 await c.close()
             await srv.stop()
             s.close()
+
+
+@pytest.mark.timeout(180)
+async def test_concurrent_bridged_binds_and_service_allocations_never_collide():
+    """with bridged writes over Etcd3Store other requests run while a write is
+    in flight. Eight concurrent binds of eight pods to the SAME device: exactly one wins, the
+    rest get 409. Eight concurrent Services asking for one clusterIP / one nodePort: one each.
+    24 Services auto-allocated concurrently get 24 distinct clusterIPs and nodePorts."""
+    from amdkube.apiserver import APIServer
+    from amdkube.benchmark.schedperf import fake_node
+    from amdkube.client import Client
+    from amdkube.smi import FakeBackend
+    from amdkube.store.etcd3 import Etcd3Store
+    from tests.test_etcd import ServerThread
+    with ServerThread(wire=True) as st:
+        s = await asyncio.to_thread(Etcd3Store, st.address)
+        srv = await APIServer(s).start()
+        cs = [Client(srv.url, token=srv.loopback_token) for _ in range(8)]
+        try:
+            assert srv._bridged
+            node = fake_node(0, 8, FakeBackend())
+            await cs[0].create(node)
+            dev = sorted(node["status"]["extendedResources"]["amd.com/gpu"]["resources"])[0]
+            for i in range(8):
+                await cs[0].create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": f"g{i}", "namespace": "default"},
+                                    "spec": {"containers": [{"name": "c", "image": "x", "resources": {"limits": {"amd.com/gpu": "1"}}}]}},
+                                   "default")
+            pods = [await cs[0].get("pods", f"g{i}", "default") for i in range(8)]
+
+            async def bind(i):
+                pres = pods[i]["spec"]["extendedResources"][0]["name"]
+                try:
+                    await cs[i].bind("default", f"g{i}", node["metadata"]["name"], {pres: {"resources": [dev]}})
+                    return 201
+                except m.StatusError as e:
+                    return e.code
+            codes = await asyncio.gather(*(bind(i) for i in range(8)))
+            assert sorted(codes) == [201] + [409] * 7, codes
+            owners = [p for p in (await cs[0].list("pods", "default"))[0]
+                      if dev in sum((r.get("assigned") or [] for r in p["spec"].get("extendedResources") or []), [])]
+            assert len(owners) == 1
+
+            async def svc(i, **spec):
+                try:
+                    return await cs[i % 8].create({"apiVersion": "v1", "kind": "Service",
+                                                   "metadata": {"name": f"s{i}-{len(spec)}", "namespace": "default"},
+                                                   "spec": {"ports": [{"port": 80}], **spec}}, "default")
+                except m.StatusError as e:
+                    return e
+            ips = await asyncio.gather(*(svc(i, clusterIP="10.0.0.77") for i in range(8)))
+            assert sum(isinstance(r, dict) for r in ips) == 1
+            nps = await asyncio.gather(*(svc(i, type="NodePort", ports=[{"port": 80, "nodePort": 30777}]) for i in range(8, 16)))
+            assert sum(isinstance(r, dict) for r in nps) == 1
+            autos = await asyncio.gather(*(svc(i, type="NodePort", selector={"a": str(i)}) for i in range(16, 40)))
+            assert all(isinstance(r, dict) for r in autos)
+            assert len({r["spec"]["clusterIP"] for r in autos}) == 24
+            assert len({r["spec"]["ports"][0]["nodePort"] for r in autos}) == 24
+            assert not srv.registry.services._pending and not srv.registry._device_claims
+        finally:
+            for c in cs:
+                await c.close()
+            await srv.stop()
+            s.close()
