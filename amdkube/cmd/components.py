@@ -304,6 +304,8 @@ def etcd(argv):
     ap.add_argument("--client-wire-port", type=int, default=0,
                     help="port of the framed client lane next to the gRPC API (0: any free port, -1: off); "
                          "advertised to clients in Status metadata")
+    ap.add_argument("--max-txn-ops", type=int, default=128, help="most compares / success / failure ops in one Txn")
+    ap.add_argument("--max-request-bytes", type=int, default=3 * 512 * 1024, help="largest client request accepted")
     ap.add_argument("-v", type=int, default=0)
     for flag in ("--advertise-client-urls", "--initial-advertise-peer-urls", "--initial-cluster-state",
                  "--initial-cluster-token", "--client-cert-auth", "--quota-backend-bytes"):
@@ -324,7 +326,7 @@ def etcd(argv):
                  name=a.name, peers=peers, peer_listen=peer_listen,
                  heartbeat=a.heartbeat_interval / 1000.0, election=a.election_timeout / 1000.0,
                  peer_cert=a.peer_cert_file, peer_key=a.peer_key_file, peer_ca=a.peer_trusted_ca_file,
-                 wire_port=a.client_wire_port)
+                 wire_port=a.client_wire_port, max_txn_ops=a.max_txn_ops, max_request_bytes=a.max_request_bytes)
     prof_path = os.environ.get("AMDKUBE_CPROFILE")
     pr = None
     if prof_path:

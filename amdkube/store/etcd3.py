@@ -48,15 +48,29 @@ FENCE = "/amdkube.io/revision-fence"       # written by every apiserver Txn (see
 _FENCE_B = FENCE.encode()
 
 
-MAX_BATCH = 256        # writes per group-committed Txn
+# etcd refuses a Txn with more than --max-txn-ops (default 128) compares or success/failure ops
+# (v3rpc/key.go checkTxnRequest) and a request over --max-request-bytes (1.5 MiB, v3_server.go):
+# a group-committed Txn carries the fence plus at most 127 writes, and about 1 MiB of values
+MAX_BATCH = 127
+MAX_BATCH_BYTES = 1 << 20
 
 
 class _Op:
-    __slots__ = ("key", "value", "expect", "delete", "fut", "data", "tries")
+    __slots__ = ("key", "value", "expect", "delete", "fut", "data", "tries", "solo")
 
     def __init__(self, key, value, expect, delete, fut):
         self.key, self.value, self.expect, self.delete, self.fut = key, value, expect, delete, fut
-        self.data, self.tries = None, 0
+        self.data, self.tries, self.solo = None, 0, False
+
+
+def _invalid_argument(e: BaseException) -> bool:
+    code = getattr(e, "code", None)
+    if callable(code):
+        try:
+            return code() == grpc.StatusCode.INVALID_ARGUMENT
+        except Exception:       # noqa: BLE001
+            return False
+    return "INVALID_ARGUMENT" in str(e)
 
 
 _KV_RESP = {name: resp for name, _req, resp, _s, _c in E.services["KV"].methods}
@@ -446,7 +460,10 @@ class Etcd3Store(MVCCStore):
             while self._pending:
                 batch, rest, keys = [], [], set()
                 for op in self._pending:          # one op per key per Txn (etcd refuses duplicates)
-                    if op.key in keys or len(batch) >= MAX_BATCH:
+                    if op.solo and not batch:
+                        batch.append(op)          # an op etcd refused in a batch is retried alone
+                        keys.add(op.key)
+                    elif op.key in keys or len(batch) >= MAX_BATCH or op.solo or (batch and batch[0].solo):
                         rest.append(op)
                     else:
                         keys.add(op.key)
@@ -454,11 +471,19 @@ class Etcd3Store(MVCCStore):
                 self._pending = rest
                 try:
                     redo = await self._commit_batch(batch)
-                except Exception as e:        # noqa: BLE001 — every waiter gets the failure
+                except Exception as e:        # noqa: BLE001
                     redo = []
-                    for op in batch:
-                        if not op.fut.done():
-                            op.fut.set_exception(e)
+                    if len(batch) > 1 and _invalid_argument(e):
+                        # etcd refused the Txn as a whole (too many ops / too large): each write
+                        # alone may well succeed, so none fails for the others
+                        log.warning("etcd3: batch of %d refused (%s); retrying one by one", len(batch), e)
+                        for op in batch:
+                            op.solo = True
+                        redo = batch
+                    else:
+                        for op in batch:          # every waiter gets the failure
+                            if not op.fut.done():
+                                op.fut.set_exception(e)
                 self._pending[:0] = redo
         finally:
             self._flusher = None
@@ -471,8 +496,13 @@ class Etcd3Store(MVCCStore):
         cmp = [E.Compare(key=_FENCE_B, target=T_MOD, result=EQUAL, mod_revision=fence.mod_rev if fence else 0)]
         success = [E.RequestOp(request_put=E.PutRequest(key=_FENCE_B))]
         failure = [E.RequestOp(request_range=E.RangeRequest(key=_FENCE_B))]
-        for op in batch:
+        size, over = 0, []
+        for n, op in enumerate(batch):
             bkey = _b(op.key)
+            if n and size > MAX_BATCH_BYTES:
+                over = batch[n:]                  # past the request-size budget: next Txn
+                batch = batch[:n]
+                break
             oc = self._object_compare(bkey, op.expect, op.delete)
             if oc is not None:
                 cmp.append(oc)
@@ -481,8 +511,15 @@ class Etcd3Store(MVCCStore):
                 success.append(E.RequestOp(request_delete_range=E.DeleteRangeRequest(key=bkey, prev_kv=True)))
             else:
                 op.data = op.value(guess) if callable(op.value) else op.value
-                success.append(E.RequestOp(request_put=E.PutRequest(key=bkey, value=self._sealed(op.key, op.data))))
+                sealed = self._sealed(op.key, op.data)
+                size += len(sealed)
+                success.append(E.RequestOp(request_put=E.PutRequest(key=bkey, value=sealed)))
+            size += 2 * len(bkey) + 32
             failure.append(E.RequestOp(request_range=E.RangeRequest(key=bkey)))
+        redo = await self._commit_ops(batch, cmp, success, failure, guess)
+        return over + redo
+
+    async def _commit_ops(self, batch, cmp, success, failure, guess) -> list:
         resp = await self._atxn(E.TxnRequest(compare=cmp, success=success, failure=failure))
         if resp.succeeded:
             rev = resp.header.revision

@@ -98,6 +98,13 @@ def _hash_id(name: str) -> int:
     return int.from_bytes(hashlib.sha256(name.encode()).digest()[:8], "big") & ((1 << 63) - 1)
 
 
+# etcd's request limits: --max-txn-ops (embed/config.go DefaultMaxTxnOps) and
+# --max-request-bytes (DefaultMaxRequestBytes = 1.5 MiB); refused as InvalidArgument
+# (v3rpc/key.go checkTxnRequest ErrGRPCTooManyOps; v3_server.go ErrRequestTooLarge)
+DEFAULT_MAX_TXN_OPS = 128
+DEFAULT_MAX_REQUEST_BYTES = 3 * 512 * 1024
+
+
 class _Abort(Exception):
     def __init__(self, code, msg):
         super().__init__(msg)
@@ -108,8 +115,10 @@ class EtcdServer:
     def __init__(self, store: MVCCStore, cluster_id: int | None = None, member_id: int | None = None,
                  name: str = "default", peers: dict[str, str] | None = None, data_dir: str | None = None,
                  heartbeat: float = 0.1, election: float = 1.0, compact_every: int = 10_000,
-                 peer_tls: tuple[str, str, str | None] | None = None):
+                 peer_tls: tuple[str, str, str | None] | None = None, max_txn_ops: int = DEFAULT_MAX_TXN_OPS,
+                 max_request_bytes: int = DEFAULT_MAX_REQUEST_BYTES):
         self.store = store
+        self.max_txn_ops, self.max_request_bytes = max_txn_ops, max_request_bytes
         self.compact_every = compact_every
         self.name = name
         self.peers = peers or {}
@@ -472,7 +481,15 @@ class EtcdServer:
                 out.append(E.ResponseOp(response_range=ranges_before[i]))
         return rev, out
 
+    async def _too_large(self, req, ctx) -> bool:
+        if req.ByteSize() > self.max_request_bytes:
+            await ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, "etcdserver: request is too large")
+            return True
+        return False
+
     async def Put(self, req, ctx):
+        if await self._too_large(req, ctx):
+            return None
         return await self._submit(K_PUT, req, ctx)
 
     async def DeleteRange(self, req, ctx):
@@ -491,6 +508,12 @@ class EtcdServer:
         return {EQUAL: have == want, NOT_EQUAL: have != want, GREATER: have > want, LESS: have < want}[c.result]
 
     async def Txn(self, req, ctx):
+        n = self.max_txn_ops
+        if len(req.compare) > n or len(req.success) > n or len(req.failure) > n:
+            await ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, "etcdserver: too many operations in txn request")
+            return None
+        if await self._too_large(req, ctx):
+            return None
         return await self._submit(K_TXN, req, ctx)
 
     async def Compact(self, req, ctx):
@@ -671,7 +694,8 @@ class EtcdServer:
 async def serve(data_dir: str | None, listen: str, cert=None, key=None, ca=None, snapshot_every: int = 50_000,
                 name: str = "default", peers: dict[str, str] | None = None, peer_listen: str | None = None,
                 heartbeat: float = 0.1, election: float = 1.0, peer_cert=None, peer_key=None, peer_ca=None,
-                wire_port: int = 0):
+                wire_port: int = 0, max_txn_ops: int = DEFAULT_MAX_TXN_OPS,
+                max_request_bytes: int = DEFAULT_MAX_REQUEST_BYTES):
     """`amdkube etcd`: run until cancelled. With `peers` (--initial-cluster) the member joins a
     raft group; its store then lives in memory and the raft log under data_dir is the WAL.
     `wire_port` (-1: off, 0: any free port) is the client wire lane on the client listener's host."""
@@ -688,6 +712,7 @@ async def serve(data_dir: str | None, listen: str, cert=None, key=None, ca=None,
     srv = await EtcdServer(store, name=name, peers=peers if clustered else None, data_dir=data_dir,
                            heartbeat=heartbeat, election=election, compact_every=snapshot_every,
                            peer_tls=(peer_cert, peer_key, peer_ca) if peer_cert and peer_key else None,
+                           max_txn_ops=max_txn_ops, max_request_bytes=max_request_bytes,
                            ).start(listen, creds, peer_listen if clustered else None, wire_address, wire_ssl)
     print(f"amdkube etcd: serving the etcd v3 API on {srv.address} (revision {store.rev})"
           + (f", client wire lane on port {srv.wire_port}" if srv.wire_port else ""), flush=True)

@@ -512,3 +512,43 @@ async def test_cancelled_bridged_write_leaves_the_store_consistent():
             assert ours == theirs and "/registry/c/after" in ours
         finally:
             s.close()
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("wire", [False, True], ids=["grpc", "wire"])
+async def test_group_commit_respects_etcd_txn_limits(wire):
+    """etcd refuses a Txn with more than --max-txn-ops ops or over
+    --max-request-bytes (InvalidArgument). 300 concurrent creates of 24 KiB ConfigMaps commit in
+    Txns of at most 127 writes and ~1 MiB; with the member's limit cut to 8 ops, a refused batch
+    is retried write by write, so no request fails for the others."""
+    with ServerThread(wire=wire) as st:
+        s = await asyncio.to_thread(Etcd3Store, st.address)
+        srv = await APIServer(s, max_in_flight=0, max_mutating_in_flight=0).start()
+        cs = [Client(srv.url, token=srv.loopback_token) for _ in range(8)]
+        seen = []
+        orig = s._atxn
+
+        async def spy(req):
+            seen.append((len(req.success), req.ByteSize()))
+            return await orig(req)
+        s._atxn = spy
+        try:
+            blob = "x" * (24 << 10)
+
+            async def create(i, prefix):
+                return await cs[i % 8].create({"apiVersion": "v1", "kind": "ConfigMap",
+                                               "metadata": {"name": f"{prefix}{i}", "namespace": "default"},
+                                               "data": {"blob": blob}}, "default")
+            made = await asyncio.gather(*(create(i, "a") for i in range(300)))
+            assert len(made) == 300
+            assert max(n for n, _ in seen) <= 128 and max(b for _, b in seen) <= 3 * 512 * 1024
+            st.srv.max_txn_ops = 8
+            made = await asyncio.gather(*(create(i, "b") for i in range(60)))
+            assert len(made) == 60
+            items, _ = await cs[0].list("configmaps", "default")
+            assert len(items) == 360
+        finally:
+            for c in cs:
+                await c.close()
+            await srv.stop()
+            s.close()
