@@ -389,8 +389,73 @@ class APIServer:
         self.crds.start()
         self._bg.append(self.crds._task)
         self._reconcile_master_service()
+        if self.opts.get("endpoint_reconciler_type") == "lease":
+            self._bg.append(asyncio.create_task(self._lease_endpoints_loop(), name="master-leases"))
         log.info("apiserver serving on http://%s:%d", host, self.port)
         return self
+
+    # pkg/master/reconcilers/lease.go: every apiserver keeps a lease on its address under
+    # /masterleases/ (TTL 15 s, renewed every 10 s: EndpointInterval, MasterEndpointReconcileTTL);
+    # the kubernetes endpoints list exactly the addresses with a live lease
+    LEASE_PREFIX = "/registry/masterleases/"
+    LEASE_TTL, LEASE_INTERVAL = 15.0, 10.0
+
+    def _advertise_ip(self) -> str:
+        return self.opts.get("advertise_address") or (self.host if self.host not in ("0.0.0.0", "", "::") else "127.0.0.1")
+
+    async def _lease_endpoints_loop(self):
+        while True:
+            try:
+                await self._w(self.reconcile_lease_endpoints)
+            except Exception as e:       # noqa: BLE001 — retried next interval
+                log.warning("master lease reconcile failed: %r", e)
+            await asyncio.sleep(self.LEASE_INTERVAL)
+
+    def reconcile_lease_endpoints(self, now: float | None = None, remove: bool = False):
+        """Renew (or, on shutdown, drop) this apiserver's lease, expire stale ones, and set the
+        kubernetes endpoints to every address that still holds one (lease.go ReconcileEndpoints)."""
+        now = time.time() if now is None else now
+        ip = self._advertise_ip()
+        key = self.LEASE_PREFIX + ip
+        if remove:
+            try:
+                self.store.delete(key)
+            except Exception:       # noqa: BLE001 — already gone
+                pass
+        else:
+            self.store.put(key, json.dumps({"ip": ip, "port": self.port, "expires": now + self.LEASE_TTL}).encode())
+        kvs, _, _ = self.store.range(self.LEASE_PREFIX)
+        live = []
+        for kv in kvs:
+            try:
+                d = json.loads(kv.value)
+            except ValueError:
+                continue
+            if float(d.get("expires", 0)) > now:
+                live.append(d["ip"])
+            else:
+                try:
+                    self.store.delete(kv.key, expect_mod_rev=kv.mod_rev)
+                except Exception:   # noqa: BLE001 — renewed or removed meanwhile
+                    pass
+        subsets = [{"addresses": [{"ip": a} for a in sorted(set(live))],
+                    "ports": [{"name": "https", "port": self.port, "protocol": "TCP"}]}] if live else []
+        ers = self.registry.rs("endpoints")
+
+        def upd(cur):      # read-modify-CAS: another apiserver may have written it meanwhile
+            if (cur.get("subsets") or []) == subsets:
+                return None
+            new = m.deepcopy(cur)
+            new["subsets"] = subsets
+            return new
+        try:
+            ers.storage.guaranteed_update(ers.key("default", "kubernetes"), upd)
+        except m.StatusError as e:
+            if e.code != 404:
+                raise
+            ers.create("default", {"apiVersion": "v1", "kind": "Endpoints",
+                                   "metadata": {"name": "kubernetes", "namespace": "default"}, "subsets": subsets})
+        return sorted(set(live))
 
     def _reconcile_master_service(self):
         """pkg/master/controller.go: the `kubernetes` service (first IP of the service range, port
@@ -410,7 +475,13 @@ class APIServer:
                 rs.create("default", svc)
         except m.StatusError as e:
             log.warning("cannot create the kubernetes service: %s", e)
-        ip = self.opts.get("advertise_address") or (self.host if self.host not in ("0.0.0.0", "", "::") else "127.0.0.1")
+        mode = self.opts.get("endpoint_reconciler_type") or "master-count"
+        if mode == "none":
+            return
+        if mode == "lease":
+            self.reconcile_lease_endpoints()
+            return
+        ip = self._advertise_ip()
         ep = {"apiVersion": "v1", "kind": "Endpoints", "metadata": {"name": "kubernetes", "namespace": "default"},
               "subsets": [{"addresses": [{"ip": ip}], "ports": [{"name": "https", "port": self.port, "protocol": "TCP"}]}]}
         ers = self.registry.rs("endpoints")
@@ -437,6 +508,11 @@ class APIServer:
     async def stop(self):
         from ..utils import cancel_and_wait
         await cancel_and_wait(self._bg)
+        if self.opts.get("endpoint_reconciler_type") == "lease":
+            try:        # hand the address back at once instead of waiting out the TTL
+                await self._w(self.reconcile_lease_endpoints, remove=True)
+            except Exception as e:      # noqa: BLE001
+                log.debug("dropping the master lease failed: %r", e)
         await self.aggregator.close()
         await self.crds.stop()
         await self.webhooks.close()

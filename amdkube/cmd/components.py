@@ -199,11 +199,14 @@ def apiserver(argv):
     ap.add_argument("--etcd-keyfile", default=None)
     ap.add_argument("--apiserver-count", type=int, default=1,
                     help="apiservers sharing the store: the kubernetes endpoints keep every one's address")
+    ap.add_argument("--endpoint-reconciler-type", default="master-count", choices=("master-count", "lease", "none"),
+                    help="how the kubernetes service endpoints are kept: master-count (--apiserver-count), "
+                         "lease (every apiserver renews a lease; endpoints list the live ones), none")
     for flag in ("--etcd-servers-overrides",
                  "--etcd-prefix", "--etcd-quorum-read", "--etcd-compaction-interval", "--storage-backend",
                  "--storage-versions", "--watch-cache", "--watch-cache-sizes",
                  "--default-watch-cache-size", "--deserialization-cache-size", "--target-ram-mb",
-                 "--endpoint-reconciler-type", "--ssh-user", "--ssh-keyfile", "--cert-dir", "--external-hostname",
+                 "--ssh-user", "--ssh-keyfile", "--cert-dir", "--external-hostname",
                  "--public-address-override", "--kubelet-preferred-address-types", "--kubelet-timeout",
                  "--kubelet-read-only-port", "--kubelet-port", "--max-connection-bytes-per-sec",
                  "--http2-max-streams-per-connection", "--repair-malformed-updates", "--delete-collection-workers",
@@ -234,7 +237,8 @@ def apiserver(argv):
         "audit_webhook_batch_buffer_size", "audit_webhook_batch_max_size", "audit_webhook_batch_max_wait",
         "audit_webhook_batch_throttle_qps", "audit_webhook_batch_throttle_burst", "advertise_address",
         "kubernetes_service_node_port", "allow_privileged", "runtime_config", "cors_allowed_origins",
-        "enable_logs_handler", "profiling", "min_request_timeout", "storage_media_type", "apiserver_count")}
+        "enable_logs_handler", "profiling", "min_request_timeout", "storage_media_type", "apiserver_count",
+        "endpoint_reconciler_type")}
     options["tls_sni_cert_key"] = sni
     main_port = a.port
     if a.secure_port is not None and a.tls_cert_file:

@@ -26,6 +26,13 @@ reason instead of being re-baselined into service. `amdkube gpu-health reset <id
 baseline, fault cleared). Without a state file the state lives as long as the process. The
 reason is published as the `amd.com/health-reason` attribute.
 
+The checkpointed counters are only comparable while the counters they came from live: ECC and
+xGMI counters restart at 0 after a reboot or a driver reload, while the state file (under
+/var/lib/kubelet) survives both. The checkpoint therefore records the instance it was taken
+in (the kernel boot_id and the amdgpu module's load time); when that changed, or when any
+counter went DOWN, the baseline is retaken from the device's state now, keeping the sticky
+reasons (a faulted GPU stays out of service until an operator resets it).
+
 Faults the RAS counters cannot see come from the kernel log: the node-problem-detector's
 amdgpu rules (monitoring/problemdetector.py) append `{"device": <pci address|device id>,
 "reason": …}` lines to `<state_file>.faults`; `pending_faults()` hands them to the plugin,
@@ -42,6 +49,26 @@ HEALTH_REASON_ATTR = "amd.com/health-reason"
 log = logging.getLogger("amdkube.health")
 
 
+BOOT_ID = "/proc/sys/kernel/random/boot_id"
+AMDGPU_MODULE = "/sys/module/amdgpu"
+COUNTERS = ("ecc_uncorrectable", "ecc_deferred", "ecc_correctable", "ras_xgmi_ecc_uncorrectable",
+            "bad_pages_pending", "bad_pages_unreservable", "bad_pages")
+
+
+def instance_id(boot_id_path: str = BOOT_ID, module_path: str = AMDGPU_MODULE) -> str:
+    """This boot and this load of the amdgpu driver: counters are comparable only within it."""
+    try:
+        with open(boot_id_path) as f:
+            boot = f.read().strip()
+    except OSError:
+        boot = ""
+    try:
+        loaded = str(int(os.stat(module_path).st_ctime))
+    except OSError:
+        loaded = ""
+    return f"{boot}/{loaded}"
+
+
 def request_reset(state_file: str, device_ids: list[str]):
     """Ask the plugin that owns `state_file` to clear these devices' faults ("all": every one)."""
     with open(state_file + ".reset", "a") as f:
@@ -50,14 +77,23 @@ def request_reset(state_file: str, device_ids: list[str]):
 
 
 class HealthMonitor:
-    def __init__(self, backend, ecc_threshold: int = 0, state_file: str | None = None, key_of=None):
+    def __init__(self, backend, ecc_threshold: int = 0, state_file: str | None = None, key_of=None,
+                 instance=instance_id):
         self.backend = backend
         self.ecc_threshold = ecc_threshold
         self.baseline: dict[int, dict] = {}
         self.sticky: dict[int, str] = {}
         self.state_file = state_file
         self.key_of = key_of or str
+        self.instance = instance() if callable(instance) else str(instance)
+        self._saved_instance = None
         self._saved: dict[str, dict] = self._load()
+        if self._saved and self._saved_instance != self.instance:
+            log.warning("health state %s was taken in another boot or driver load (%s, now %s): "
+                        "counters restarted, baselines are retaken (faults stay)", state_file,
+                        self._saved_instance, self.instance)
+            for ent in self._saved.values():
+                ent["stale"] = True
 
     # ------------------------------------------------------------------ checkpoint
     def _load(self) -> dict:
@@ -65,7 +101,9 @@ class HealthMonitor:
             return {}
         try:
             with open(self.state_file) as f:
-                return dict((json.load(f) or {}).get("gpus") or {})
+                doc = json.load(f) or {}
+            self._saved_instance = doc.get("instance")
+            return dict(doc.get("gpus") or {})
         except (OSError, ValueError) as e:
             log.error("health state %s unreadable (%s); starting from fresh baselines", self.state_file, e)
             return {}
@@ -76,7 +114,7 @@ class HealthMonitor:
         os.makedirs(os.path.dirname(os.path.abspath(self.state_file)), exist_ok=True)
         tmp = self.state_file + ".tmp"
         with open(tmp, "w") as f:
-            json.dump({"gpus": self._saved}, f, sort_keys=True, default=str)
+            json.dump({"gpus": self._saved, "instance": self.instance}, f, sort_keys=True, default=str)
             f.flush()
             os.fsync(f.fileno())
         os.replace(tmp, self.state_file)
@@ -86,13 +124,15 @@ class HealthMonitor:
         if not self.state_file:
             return set()
         req = self.state_file + ".reset"
+        tmp = req + f".{os.getpid()}"
         try:
-            with open(req) as f:
-                ids = {line.strip() for line in f if line.strip()}
-            os.unlink(req)
-            return ids
+            os.replace(req, tmp)              # take the whole file; a later request starts a new one
         except FileNotFoundError:
             return set()
+        with open(tmp) as f:
+            ids = {line.strip() for line in f if line.strip()}
+        os.unlink(tmp)
+        return ids
 
     def pending_faults(self) -> list[dict]:
         """Faults reported from outside (the node-problem-detector) since the last call."""
@@ -146,16 +186,19 @@ class HealthMonitor:
         (a restart keeps it and any sticky fault), else the device's state now."""
         key = self.key_of(index)
         ent = self._saved.get(key)
+        keep = ""
         if ent is not None and not fresh:
-            self.baseline[index] = ent.get("baseline") or {}
             if ent.get("sticky"):
                 self.sticky[index] = ent["sticky"]
-            return self.baseline[index]
+            if not ent.get("stale"):
+                self.baseline[index] = ent.get("baseline") or {}
+                return self.baseline[index]
+            keep = ent.get("sticky") or ""      # another boot/driver load: retake, keep the fault
         try:
             self.baseline[index] = self._state(index)
         except Exception as e:   # noqa: BLE001
             self.baseline[index] = {"snapshot_error": str(e)}
-        self._saved[key] = {"baseline": self.baseline[index], "sticky": "", "since": time.time()}
+        self._saved[key] = {"baseline": self.baseline[index], "sticky": keep, "since": time.time()}
         self._save()
         return self.baseline[index]
 
@@ -169,6 +212,15 @@ class HealthMonitor:
             cur = self._state(index)
         except Exception as e:   # noqa: BLE001
             return False, f"smi query failed: {e}"
+        if any(cur.get(k, 0) < base.get(k, 0) for k in COUNTERS if isinstance(cur.get(k, 0), (int, float))):
+            # a counter went down: the driver restarted them (reload, reset) under a live plugin;
+            # judge from here on
+            log.warning("GPU %s RAS counters went down (%s -> %s); taking a fresh baseline", self.key_of(index),
+                        {k: base.get(k) for k in COUNTERS if k in base}, {k: cur.get(k) for k in COUNTERS if k in cur})
+            self.baseline[index] = cur
+            self._saved[self.key_of(index)] = {"baseline": cur, "sticky": "", "since": time.time()}
+            self._save()
+            return True, ""
         why = self._judge(base, cur)
         if why:
             self.sticky[index] = why

@@ -552,3 +552,42 @@ async def test_group_commit_respects_etcd_txn_limits(wire):
                 await c.close()
             await srv.stop()
             s.close()
+
+
+@pytest.mark.timeout(120)
+async def test_lease_endpoint_reconciler_lists_live_apiservers():
+    """--endpoint-reconciler-type=lease (pkg/master/reconcilers/lease.go), what kubeadm's
+    HighAvailability gate selects: two apiservers over one etcd each hold a master lease and the
+    `kubernetes` endpoints list both; a stopped apiserver drops its address at once; a lease
+    not renewed within its TTL expires."""
+    with ServerThread(wire=True) as st:
+        s1, s2 = await asyncio.to_thread(Etcd3Store, st.address), await asyncio.to_thread(Etcd3Store, st.address)
+        a1 = await APIServer(s1, options={"endpoint_reconciler_type": "lease", "advertise_address": "10.9.0.1"}).start()
+        a2 = await APIServer(s2, options={"endpoint_reconciler_type": "lease", "advertise_address": "10.9.0.2"}).start()
+        c = Client(a1.url, token=a1.loopback_token)
+        try:
+            await asyncio.sleep(0.2)
+            await a1._w(a1.reconcile_lease_endpoints)
+
+            async def addrs():
+                ep = await c.get("endpoints", "kubernetes", "default")
+                return sorted(a["ip"] for sub in ep.get("subsets") or [] for a in sub["addresses"])
+            assert await addrs() == ["10.9.0.1", "10.9.0.2"]
+            await a2.stop()
+            await a1._w(a1.reconcile_lease_endpoints)
+            assert await addrs() == ["10.9.0.1"]
+            # a lease nobody renews for longer than the TTL is dropped
+            s2b = await asyncio.to_thread(Etcd3Store, st.address)
+            a3 = await APIServer(s2b, options={"endpoint_reconciler_type": "lease", "advertise_address": "10.9.0.3"}).start()
+            await a1._w(a1.reconcile_lease_endpoints)
+            assert await addrs() == ["10.9.0.1", "10.9.0.3"]
+            await a1._w(a1.reconcile_lease_endpoints, time.time() + 60)
+            assert await addrs() == ["10.9.0.1"]
+            a3.opts["endpoint_reconciler_type"] = "none"      # crashed, not stopped: no goodbye
+            await a3.stop()
+            s2b.close()
+        finally:
+            await c.close()
+            await a1.stop()
+            s1.close()
+            s2.close()

@@ -145,3 +145,63 @@ def test_fault_survives_a_plugin_restart_until_an_operator_reset(tmp_path):
         assert f"{ids[0]}\tHealthy" in show and f"{ids[1]}\tUnhealthy" in show
         await p.stop()
     run(go())
+
+
+def test_checkpoint_from_another_boot_is_rebaselined_but_faults_stay(tmp_path):
+    """ECC/xGMI counters restart at 0 after a reboot or driver reload while the state
+    file survives. A checkpoint from another boot/driver instance is re-baselined (else the
+    subtraction would hide new errors until the old count is exceeded), keeping sticky faults."""
+    state = str(tmp_path / "health.json")
+    fb = FakeBackend(n=2)
+    fb.inject_ecc(0, uncorrectable=7)
+    hm = HealthMonitor(fb, state_file=state, instance="boot-A/1")
+    hm.snapshot(0)
+    hm.snapshot(1)
+    hm.fault(1, "operator: bad HBM stack")
+    # reboot: the counters restart at 0, then one new uncorrectable error
+    fb2 = FakeBackend(n=2)
+    hm2 = HealthMonitor(fb2, state_file=state, instance="boot-B/1")
+    hm2.snapshot(0)
+    hm2.snapshot(1)
+    assert hm2.baseline[0].get("ecc_uncorrectable", 0) == 0
+    fb2.inject_ecc(0)
+    ok, why = hm2.check(0)
+    assert not ok and "+1 since the plugin started" in why
+    assert hm2.check(1) == (False, "operator: bad HBM stack")
+    # the same instance keeps the original baseline (a plain plugin restart)
+    hm3 = HealthMonitor(fb2, state_file=state, instance="boot-B/1")
+    hm3.snapshot(1)
+    assert hm3.check(1)[0] is False
+
+
+def test_counters_going_down_under_a_live_monitor_rebaseline():
+    fb = FakeBackend(n=1)
+    fb.inject_ecc(0, uncorrectable=4)
+    hm = HealthMonitor(fb, instance="x")
+    hm.snapshot(0)
+    fb.samples[0]["ecc_uncorrectable"] = 0        # driver reload under the plugin
+    assert hm.check(0) == (True, "")
+    fb.inject_ecc(0)
+    ok, why = hm.check(0)
+    assert not ok and "+1" in why
+
+
+def test_reset_requests_are_taken_atomically(tmp_path):
+    """A reset appended while the plugin collects requests lands in a new file and is read on
+    the next tick instead of being unlinked unread."""
+    from amdkube.smi.health import request_reset
+    state = str(tmp_path / "h.json")
+    hm = HealthMonitor(FakeBackend(n=1), state_file=state, instance="x")
+    request_reset(state, ["GPU-a"])
+    import os
+    real_replace = os.replace
+
+    def replace_then_append(src, dst):
+        real_replace(src, dst)
+        request_reset(state, ["GPU-b"])            # arrives between the take and the read
+    os.replace = replace_then_append
+    try:
+        assert hm.pending_resets() == {"GPU-a"}
+    finally:
+        os.replace = real_replace
+    assert hm.pending_resets() == {"GPU-b"}
