@@ -146,6 +146,8 @@ def default_service(s: dict):
     spec = s.setdefault("spec", {})
     spec.setdefault("type", "ClusterIP")
     spec.setdefault("sessionAffinity", "None")
+    if spec["type"] in ("NodePort", "LoadBalancer"):
+        spec.setdefault("externalTrafficPolicy", "Cluster")     # SetDefaults_Service
     for p in spec.get("ports") or []:
         p.setdefault("protocol", "TCP")
         p.setdefault("targetPort", p.get("port"))

@@ -50,6 +50,32 @@ def validate_service(svc: dict, old=None) -> list[str]:
     sel = spec.get("selector") or {}
     if not isinstance(sel, dict):
         errs.append("spec.selector: Invalid value: must be a map")
+    # validation.go validateServiceExternalTrafficFieldsValue / ValidateService (source ranges)
+    etp = spec.get("externalTrafficPolicy")
+    if etp:
+        if t not in ("NodePort", "LoadBalancer"):
+            errs.append(f"spec.externalTrafficPolicy: Invalid value: {etp!r}: ExternalTrafficPolicy can only be set on "
+                        "NodePort and LoadBalancer service")
+        elif etp not in ("Cluster", "Local"):
+            errs.append(f"spec.externalTrafficPolicy: Unsupported value: {etp!r}: supported values: Cluster, Local")
+    hc = spec.get("healthCheckNodePort")
+    if hc:
+        if not (t == "LoadBalancer" and etp == "Local"):
+            errs.append(f"spec.healthCheckNodePort: Invalid value: {hc!r}: HealthCheckNodePort can only be set on "
+                        "LoadBalancer service with ExternalTrafficPolicy=Local")
+        elif not isinstance(hc, int) or not 0 < hc < 65536:
+            errs.append(f"spec.healthCheckNodePort: Invalid value: {hc!r}: must be between 1 and 65535, inclusive")
+    ranges = spec.get("loadBalancerSourceRanges") or []
+    if ranges:
+        import ipaddress
+        if t != "LoadBalancer":
+            errs.append("spec.loadBalancerSourceRanges: Forbidden: may only be used when `type` is 'LoadBalancer'")
+        for i, r in enumerate(ranges):
+            try:
+                ipaddress.ip_network(str(r).strip(), strict=False)
+            except ValueError:
+                errs.append(f"spec.loadBalancerSourceRanges[{i}]: Invalid value: {r!r}: must be a list of IP ranges. "
+                            "For example, 10.240.0.0/24,10.250.0.0/24")
     return errs
 
 
@@ -57,6 +83,8 @@ def default_service(svc: dict):
     spec = svc.setdefault("spec", {})
     spec.setdefault("type", "ClusterIP")
     spec.setdefault("sessionAffinity", "None")
+    if spec["type"] in ("NodePort", "LoadBalancer"):
+        spec.setdefault("externalTrafficPolicy", "Cluster")     # SetDefaults_Service
     for p in spec.get("ports") or []:
         p.setdefault("protocol", "TCP")
         p.setdefault("targetPort", p.get("port"))

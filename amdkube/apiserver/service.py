@@ -73,6 +73,10 @@ class ServiceAllocator:
                 k = (p.get("protocol", "TCP"), int(p["nodePort"]))
                 self.ports[k] = key
                 ports.append(k)
+        if spec.get("healthCheckNodePort"):
+            k = ("TCP", int(spec["healthCheckNodePort"]))
+            self.ports[k] = key
+            ports.append(k)
         self._by_key[key] = (ips, ports)
 
     def _reserve(self, key: str, kind: str, v):
@@ -172,11 +176,13 @@ class ServiceAllocator:
         elif not old_ip and spec["clusterIP"] != "None":
             spec["clusterIP"] = self.allocate_ip(key, spec["clusterIP"])
         old = {(p.get("protocol", "TCP"), p.get("port")): p.get("nodePort") for p in cspec.get("ports") or []}
-        self._node_ports(key, spec, old)
+        self._node_ports(key, spec, old, cspec.get("healthCheckNodePort"))
 
-    def _node_ports(self, key, spec, old):
+    def _node_ports(self, key, spec, old, old_hc=None):
         need = spec.get("type") in ("NodePort", "LoadBalancer")
         taken: set = set()
+        if spec.get("healthCheckNodePort"):
+            taken.add(("TCP", int(spec["healthCheckNodePort"])))
         for p in spec.get("ports") or []:
             proto = p.setdefault("protocol", "TCP")
             if not need:
@@ -188,3 +194,12 @@ class ServiceAllocator:
             req = p.get("nodePort") or old.get((proto, p.get("port")))
             p["nodePort"] = self.allocate_port(key, proto, int(req) if req else None, taken)
             taken.add((proto, p["nodePort"]))
+        # rest.go: a LoadBalancer with externalTrafficPolicy=Local gets a health-check node port
+        # (spec.healthCheckNodePort, kept across updates) that kube-proxy answers on every node
+        if spec.get("type") == "LoadBalancer" and spec.get("externalTrafficPolicy") == "Local":
+            req = spec.get("healthCheckNodePort") or old_hc
+            if req:
+                taken.discard(("TCP", int(req)))
+            spec["healthCheckNodePort"] = self.allocate_port(key, "TCP", int(req) if req else None, taken)
+        elif spec.get("healthCheckNodePort") and spec.get("healthCheckNodePort") == old_hc:
+            spec.pop("healthCheckNodePort")     # released with the Local LoadBalancer it belonged to

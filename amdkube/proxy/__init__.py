@@ -3,7 +3,10 @@
 ProxyServer watches services and endpoints and drives one proxier:
   * `userspace`: real listeners per service port with round-robin / ClientIP affinity;
   * `iptables`: the reference's nat/filter ruleset, applied with iptables-restore when
-    privileged, otherwise rendered (dry run).
+    privileged, otherwise rendered (dry run);
+  * `ipvs`: IPVS virtual servers plus the iptables masquerade linkage.
+For externalTrafficPolicy=Local services it serves each healthCheckNodePort
+(proxy/healthcheck.py).
 It serves /healthz on --healthz-port (reference healthcheck.go: 503 once the last
 successful sync is older than 2 × the sync period) and /metrics with
 kubeproxy_sync_proxy_rules_latency_microseconds.
@@ -34,18 +37,23 @@ class ProxyServer:
                  udp_idle_timeout: float = 0.25, metrics_address: tuple | None = None, hostname: str = ""):
         self.client = client
         self.hostname = hostname
+        nip = node_ip if node_ip not in ("", "0.0.0.0") else ""
         if mode == "iptables":
             self.proxier = IptablesProxier(cluster_cidr, dump_path=iptables_dump, masquerade_all=masquerade_all,
-                                           masquerade_bit=masquerade_bit)
+                                           masquerade_bit=masquerade_bit, hostname=hostname, node_ip=nip)
         elif mode == "ipvs":
             from .ipvs import IPVSProxier
-            self.proxier = IPVSProxier(cluster_cidr, ipvs_scheduler, node_ips=[node_ip] if node_ip not in ("", "0.0.0.0") else [],
-                                       masquerade_all=masquerade_all, dump_path=iptables_dump)
+            self.proxier = IPVSProxier(cluster_cidr, ipvs_scheduler, node_ips=[nip] if nip else [],
+                                       masquerade_all=masquerade_all, dump_path=iptables_dump, hostname=hostname,
+                                       masquerade_bit=masquerade_bit)
         elif mode == "userspace":
             self.proxier = UserspaceProxier(node_ip, bind_cluster_ips=bind_cluster_ips, udp_idle_timeout=udp_idle_timeout)
         else:
             raise ValueError(f"unknown proxy mode {mode!r} (userspace|iptables|ipvs)")
         self.tracker = ChangeTracker()
+        # healthCheckNodePort listeners for externalTrafficPolicy=Local (iptables and ipvs modes)
+        from .healthcheck import HealthCheckServer
+        self.health = HealthCheckServer(hostname) if mode in ("iptables", "ipvs") else None
         self.sync_period, self.min_sync_period = sync_period, min_sync_period
         self.healthz_port = healthz_port
         self.healthz_address = healthz_address
@@ -96,7 +104,13 @@ class ProxyServer:
     async def sync(self):
         t0 = time.perf_counter()
         self.tracker.dirty = False
-        await self.proxier.sync(self.tracker.service_map(), self.tracker.endpoint_map())
+        svcs, eps = self.tracker.service_map(), self.tracker.endpoint_map()
+        await self.proxier.sync(svcs, eps)
+        if self.health is not None:
+            from .iptables import health_check_state
+            hc_svcs, hc_eps = health_check_state(svcs, eps, self.hostname)
+            await self.health.sync_services(hc_svcs)
+            self.health.sync_endpoints(hc_eps)
         self.last_sync = time.time()
         self.m_sync.observe((time.perf_counter() - t0) * 1e6)
 
@@ -131,5 +145,7 @@ class ProxyServer:
         await self.svc_inf.stop()
         await self.ep_inf.stop()
         await self.proxier.stop()
+        if self.health is not None:
+            await self.health.stop()
         if self._runner:
             await self._runner.cleanup()

@@ -35,7 +35,9 @@ class ServiceInfo:
     affinity_timeout: int = DEFAULT_AFFINITY_TIMEOUT
     external_ips: list = field(default_factory=list)
     lb_ingress: list = field(default_factory=list)
-    only_local: bool = False
+    only_local: bool = False        # externalTrafficPolicy: Local on a NodePort/LoadBalancer service
+    source_ranges: list = field(default_factory=list)     # spec.loadBalancerSourceRanges
+    health_check_node_port: int = 0
 
 
 def service_infos(svc: dict) -> dict[ServicePortName, ServiceInfo]:
@@ -47,11 +49,18 @@ def service_infos(svc: dict) -> dict[ServicePortName, ServiceInfo]:
     timeout = (((spec.get("sessionAffinityConfig") or {}).get("clientIP") or {}).get("timeoutSeconds")
                or DEFAULT_AFFINITY_TIMEOUT)
     ingress = [i.get("ip") for i in (((svc.get("status") or {}).get("loadBalancer") or {}).get("ingress") or []) if i.get("ip")]
+    # apiservice.RequestsOnlyLocalTraffic: Local only means something for NodePort/LoadBalancer
+    local = spec.get("externalTrafficPolicy") == "Local" and spec.get("type") in ("NodePort", "LoadBalancer")
+    ranges = [r.strip() for r in spec.get("loadBalancerSourceRanges") or [] if r.strip()]
+    if not ranges:          # the legacy annotation (pkg/api/service/util.go GetLoadBalancerSourceRanges)
+        ann = (m.annotations_of(svc) or {}).get("service.beta.kubernetes.io/load-balancer-source-ranges", "")
+        ranges = [r.strip() for r in ann.split(",") if r.strip()]
+    hc = int(spec.get("healthCheckNodePort") or 0) if local and spec.get("type") == "LoadBalancer" else 0
     for p in spec.get("ports") or []:
         spn = ServicePortName(m.namespace_of(svc), m.name_of(svc), p.get("name", ""))
         out[spn] = ServiceInfo(ip, int(p["port"]), p.get("protocol", "TCP"), int(p.get("nodePort") or 0),
                                spec.get("sessionAffinity", "None"), int(timeout), list(spec.get("externalIPs") or []),
-                               ingress, spec.get("externalTrafficPolicy") == "Local")
+                               ingress, local, ranges, hc)
     return out
 
 

@@ -6,7 +6,14 @@ the --ipvs-scheduler (rr by default) and, for ClientIP affinity, persistence for
 timeout; the ready endpoints are its real servers (masquerading forward, weight 1). Every
 cluster/external/LB address is bound to the dummy interface kube-ipvs0 so the node accepts the
 traffic. iptables only supplies the masquerade marks (KUBE-POSTROUTING, KUBE-MARK-MASQ for
-traffic from outside --cluster-cidr or with --masquerade-all).
+traffic from outside --cluster-cidr or with --masquerade-all), linked from nat PREROUTING/OUTPUT
+(-> KUBE-SERVICES) and POSTROUTING (-> KUBE-POSTROUTING) like the reference's
+linkKubeServiceChain (proxier.go:1676-1700).
+
+externalTrafficPolicy=Local: the virtual servers of the node ports, external IPs and load-balancer
+IPs get only this node's endpoints (syncEndpoint onlyNodeLocalEndpoints, :1565-1590); unlike
+the v1.9 reference, the cluster IP keeps every endpoint (traffic inside the cluster is not
+subject to the external traffic policy).
 
 The proxier computes the desired state, diffs it with what it applied last (or with
 `ipvsadm -Sn` when it owns the host) and emits the minimal ipvsadm-restore / ip-addr / iptables
@@ -20,7 +27,13 @@ import shutil
 import subprocess
 
 from .config import ServiceInfo, ServicePortName
-from .iptables import KUBE_MARK_MASQ, MASQ_MARK
+from .iptables import KUBE_MARK_MASQ, MASQ_MARK, ensure_jumps
+
+IPVS_JUMPS = (
+    ("nat", "OUTPUT", '-m comment --comment "kubernetes service portals" -j KUBE-SERVICES'),
+    ("nat", "PREROUTING", '-m comment --comment "kubernetes service portals" -j KUBE-SERVICES'),
+    ("nat", "POSTROUTING", '-m comment --comment "kubernetes postrouting rules" -j KUBE-POSTROUTING'),
+)
 
 log = logging.getLogger("amdkube.proxy.ipvs")
 DUMMY = "kube-ipvs0"
@@ -32,22 +45,23 @@ def _flag(proto: str) -> str:
 
 
 def desired(services: dict[ServicePortName, ServiceInfo], endpoints: dict[ServicePortName, list], node_ips=(),
-            scheduler: str = "rr"):
+            scheduler: str = "rr", hostname: str = ""):
     """(virtual servers {(proto, vip, port): {scheduler, persistent}}, real servers
     {(proto, vip, port): {(ip, port)}}, addresses bound to kube-ipvs0)."""
     vs, rs, addrs = {}, {}, set()
     for spn, info in sorted(services.items(), key=lambda kv: str(kv[0])):
         eps = {(ip, port) for ip, port, _node in endpoints.get(spn, [])}
+        local = {(ip, port) for ip, port, node in endpoints.get(spn, []) if hostname and node == hostname}
         persist = info.affinity_timeout if info.session_affinity == "ClientIP" else 0
         vips = [info.cluster_ip] + list(info.external_ips) + list(info.lb_ingress)
         addrs.update(v for v in vips if v)
-        targets = [(v, info.port) for v in vips if v]
+        targets = [(v, info.port, v != info.cluster_ip) for v in vips if v]
         if info.node_port:
-            targets += [(nip, info.node_port) for nip in node_ips]
-        for vip, port in targets:
+            targets += [(nip, info.node_port, True) for nip in node_ips]
+        for vip, port, external in targets:
             key = (info.protocol.upper(), vip, port)
             vs[key] = {"scheduler": scheduler, "persistent": persist}
-            rs[key] = set(eps)
+            rs[key] = set(local if (external and info.only_local) else eps)
     return vs, rs, addrs
 
 
@@ -86,10 +100,10 @@ def diff(old_vs, old_rs, vs, rs) -> list[str]:
     return cmds
 
 
-def render_iptables(services, cluster_cidr: str = "", masquerade_all: bool = False) -> str:
+def render_iptables(services, cluster_cidr: str = "", masquerade_all: bool = False, masq: str = MASQ_MARK) -> str:
     rules = ["*nat", ":KUBE-SERVICES - [0:0]", ":KUBE-POSTROUTING - [0:0]", f":{KUBE_MARK_MASQ} - [0:0]",
-             f'-A KUBE-POSTROUTING -m comment --comment "kubernetes service traffic requiring SNAT" -m mark --mark {MASQ_MARK} -j MASQUERADE',
-             f"-A {KUBE_MARK_MASQ} -j MARK --set-xmark {MASQ_MARK}"]
+             f'-A KUBE-POSTROUTING -m comment --comment "kubernetes service traffic requiring SNAT" -m mark --mark {masq} -j MASQUERADE',
+             f"-A {KUBE_MARK_MASQ} -j MARK --set-xmark {masq}"]
     for spn, info in sorted(services.items(), key=lambda kv: str(kv[0])):
         base = f'-A KUBE-SERVICES -m comment --comment "{spn} cluster IP" -p {info.protocol.lower()} -d {info.cluster_ip}/32 --dport {info.port}'
         if masquerade_all:
@@ -125,11 +139,14 @@ class IPVSProxier:
     mode = "ipvs"
 
     def __init__(self, cluster_cidr: str = "", scheduler: str = "rr", node_ips=(), masquerade_all: bool = False,
-                 dry_run: bool | None = None, dump_path: str | None = None):
+                 dry_run: bool | None = None, dump_path: str | None = None, hostname: str = "", masquerade_bit: int = 14):
+        from .iptables import masq_mark
         if scheduler not in SCHEDULERS:
             raise ValueError(f"unknown ipvs scheduler {scheduler!r}")
         self.cluster_cidr, self.scheduler, self.node_ips = cluster_cidr, scheduler, tuple(node_ips)
-        self.masquerade_all = masquerade_all
+        self.masquerade_all, self.hostname, self.masq = masquerade_all, hostname, masq_mark(masquerade_bit)
+        self.iptables = shutil.which("iptables")
+        self.ensured: list = []
         self.ipvsadm = shutil.which("ipvsadm")
         self.dry_run = (self.ipvsadm is None or os.geteuid() != 0) if dry_run is None else dry_run
         self.dump_path = dump_path
@@ -144,7 +161,8 @@ class IPVSProxier:
         return parse_save(r.stdout) if r.returncode == 0 else (self.vs, self.rs)
 
     async def sync(self, services, endpoints):
-        vs, rs, addrs = desired(services, endpoints, self.node_ips, self.scheduler)
+        vs, rs, addrs = desired(services, endpoints, self.node_ips, self.scheduler, self.hostname)
+        self.ensured = ensure_jumps(self.iptables, IPVS_JUMPS, self.dry_run)
         old_vs, old_rs = self._host_state()
         cmds = diff(old_vs, old_rs, vs, rs)
         self.syncs += 1
@@ -167,8 +185,8 @@ class IPVSProxier:
                 subprocess.run(["ip", "addr", "del", f"{ip}/32", "dev", DUMMY], capture_output=True)
             ipt = shutil.which("iptables-restore")
             if ipt:
-                subprocess.run([ipt, "--noflush"], input=render_iptables(services, self.cluster_cidr, self.masquerade_all),
-                               text=True, capture_output=True)
+                subprocess.run([ipt, "--noflush"], input=render_iptables(services, self.cluster_cidr, self.masquerade_all,
+                                                                         self.masq), text=True, capture_output=True)
         self.vs, self.rs, self.addrs = vs, rs, addrs
 
     async def stop(self):

@@ -123,9 +123,10 @@ def test_iptables_ruleset():
     assert len(last) == 1 and last[0].endswith(sep_chain(web, "TCP", "10.244.1.2:8080"))
     assert sum(1 for ln in lines if ln.startswith(f"-A {sc}") and "--rcheck --seconds 600" in ln) == 3
     assert any("DNAT --to-destination 10.244.0.3:8080" in ln and "--set" in ln for ln in lines)
-    # no endpoints → filter REJECT, no SVC chain
+    # no endpoints → filter REJECT; the SVC chain is declared but empty (TestClusterIPReject)
     assert any(ln.startswith("-A KUBE-SERVICES") and "lonely has no endpoints" in ln and "-j REJECT" in ln for ln in lines)
-    assert svc_chain(lonely, "UDP") not in rules
+    assert f":{svc_chain(lonely, 'UDP')} - [0:0]" in lines
+    assert not any(ln.startswith(f"-A {svc_chain(lonely, 'UDP')}") for ln in lines)
     nat_commit = len(lines) - 1 - lines[::-1].index("COMMIT")
     assert lines[nat_commit - 1].endswith("-j KUBE-NODEPORTS")
 
