@@ -464,7 +464,9 @@ async def test_cloud_load_balancer_and_routes():
         routes = bm.routes()
         await until(lambda: _true(any(r.target_node == lc.node_name for r in routes.list("kubernetes"))))
         # the service stops being a LoadBalancer → balancer released, status cleared
-        await c.patch("services", "lb", {"spec": {"type": "ClusterIP", "ports": [{"port": 80, "nodePort": None}]}}, "default")
+        # (as in the reference, the NodePort/LoadBalancer-only externalTrafficPolicy goes with the type)
+        await c.patch("services", "lb", {"spec": {"type": "ClusterIP", "externalTrafficPolicy": None,
+                                                  "ports": [{"port": 80, "nodePort": None}]}}, "default")
         await until(lambda: _true(not bm.load_balancer().assigned))
     # the fake provider records the same calls
     async with LocalCluster(gpus="none", with_kubelet=False, controllers_kw={"cloud": fake}) as lc:
