@@ -131,9 +131,14 @@ def default_deployment(d: dict):
 
 
 def default_job(j: dict):
+    """pkg/apis/batch/v1/defaults.go SetDefaults_Job: a Job with neither completions nor
+    parallelism runs one pod to one completion; parallelism alone leaves completions unset
+    (a work-queue Job)."""
     spec = j.setdefault("spec", {})
-    spec.setdefault("completions", 1)
-    spec.setdefault("parallelism", 1)
+    if spec.get("completions") is None and spec.get("parallelism") is None:
+        spec["completions"] = 1
+    if spec.get("parallelism") is None:
+        spec["parallelism"] = 1
     spec.setdefault("backoffLimit", 6)
     tpl = spec.setdefault("template", {})
     tspec = tpl.setdefault("spec", {})

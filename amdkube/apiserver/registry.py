@@ -167,6 +167,22 @@ def pod_qos(pod) -> str:
     return "Guaranteed" if guaranteed else "Burstable"
 
 
+def _generate_job_selector(job: dict):
+    """pkg/registry/batch/job/strategy.go generateSelector: unless spec.manualSelector, the Job
+    selects its pods by its own uid (controller-uid), set on the template with job-name."""
+    spec = job.setdefault("spec", {})
+    if spec.get("manualSelector"):
+        return
+    uid, name = job["metadata"]["uid"], job["metadata"].get("name", "")
+    tmd = spec.setdefault("template", {}).setdefault("metadata", {})
+    labels = tmd.setdefault("labels", {})
+    labels["controller-uid"] = uid
+    labels["job-name"] = name
+    sel = spec.get("selector") or {}
+    sel.setdefault("matchLabels", {})["controller-uid"] = uid
+    spec["selector"] = sel
+
+
 class ResourceStore:
     def __init__(self, api: "Registry", ri: ResourceInfo):
         self.api, self.ri = api, ri
@@ -273,6 +289,8 @@ class ResourceStore:
             obj["status"] = {"phase": "Active"}
         elif p in _STATUS_KINDS and p not in ("nodes",):
             obj["status"] = {}
+        if p == "jobs":
+            _generate_job_selector(obj)
         if p == "services":
             md = obj["metadata"]
             self.api.services.prepare_create(self.key(md.get("namespace", ""), md.get("name", "")), obj)

@@ -14,6 +14,7 @@ log = logging.getLogger("amdkube.controllers")
 class Controller:
     name = "controller"
     workers = 2
+    max_requeues: int | None = 15      # retries of a failing key before it is dropped (None: no cap)
 
     def __init__(self, mgr):
         self.mgr = mgr
@@ -45,14 +46,16 @@ class Controller:
             except ShutDown:
                 return
             try:
-                await self.sync(key)
-                self.queue.forget(key)
+                # a sync may return False: done, but keep the key's rate-limit history (the
+                # reference's syncHandler `forget` result, e.g. the Job controller's back-off)
+                if await self.sync(key) is not False:
+                    self.queue.forget(key)
                 self.syncs += 1
             except asyncio.CancelledError:
                 raise
             except Exception as e:
                 log.debug("%s: sync %s failed: %r", self.name, key, e)
-                if self.queue.num_requeues(key) < 15:
+                if self.max_requeues is None or self.queue.num_requeues(key) < self.max_requeues:
                     self.queue.add_rate_limited(key)
             finally:
                 self.queue.done(key)

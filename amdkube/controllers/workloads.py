@@ -3,8 +3,7 @@
 Reference: pkg/controller/replicaset (manage replicas via controllerRef + expectations),
 pkg/controller/deployment (ReplicaSets per pod-template-hash; Recreate / RollingUpdate),
 pkg/controller/daemon (one pod per eligible node — how the AMD device plugin is rolled
-out, deploy/amd-gpu-device-plugin.yaml), pkg/controller/job (parallelism / completions /
-backoffLimit). Slimmed to the behaviour the GPU-pod path needs (P1).
+out, deploy/amd-gpu-device-plugin.yaml). The Job controller is in controllers/job.py.
 """
 from __future__ import annotations
 
@@ -577,55 +576,4 @@ class DaemonSetController(Controller):
             await self.client.patch("daemonsets", name, {"status": st}, ns, sub="status")
 
 
-class JobController(Controller):
-    name = "job"
-
-    def setup(self):
-        f = self.mgr.factory
-        self.job_inf = f.informer("jobs")
-        self.pod_inf = self.mgr.pods
-        self.job_inf.add_handler(on_add=self.enqueue, on_update=lambda o, n: self.enqueue(n), on_delete=self.enqueue)
-        self.pod_inf.add_handler(on_add=self._pod, on_update=lambda o, n: self._pod(n), on_delete=self._pod)
-
-    def _pod(self, pod):
-        ref = m.controller_ref(pod)
-        if ref and ref.get("kind") == "Job":
-            self.enqueue(f"{m.namespace_of(pod)}/{ref['name']}")
-
-    async def sync(self, key):
-        job = self.job_inf.get(key)
-        if job is None or (job.get("metadata") or {}).get("deletionTimestamp"):
-            return
-        ns, name = split_key(key)
-        st = job.get("status") or {}
-        if any(c.get("type") in ("Complete", "Failed") and c.get("status") == "True" for c in st.get("conditions") or []):
-            return
-        spec = job.get("spec") or {}
-        pods = _owned(self.pod_inf.list(), job)
-        succeeded = sum(1 for p in pods if (p.get("status") or {}).get("phase") == "Succeeded")
-        failed = sum(1 for p in pods if (p.get("status") or {}).get("phase") == "Failed")
-        active = [p for p in pods if not is_pod_terminal(p) and not (p.get("metadata") or {}).get("deletionTimestamp")]
-        completions, parallelism = int(spec.get("completions", 1)), int(spec.get("parallelism", 1))
-        new = {"succeeded": succeeded, "failed": failed, "active": len(active), "startTime": st.get("startTime") or m.now_rfc3339()}
-        conds = []
-        if succeeded >= completions:
-            conds = [{"type": "Complete", "status": "True", "lastTransitionTime": m.now_rfc3339()}]
-            new["completionTime"] = m.now_rfc3339()
-            for p in active:
-                await self.client.delete("pods", m.name_of(p), ns)
-            new["active"] = 0
-        elif failed > int(spec.get("backoffLimit", 6)):
-            conds = [{"type": "Failed", "status": "True", "reason": "BackoffLimitExceeded",
-                      "message": "Job has reached the specified backoff limit", "lastTransitionTime": m.now_rfc3339()}]
-            for p in active:
-                await self.client.delete("pods", m.name_of(p), ns)
-            new["active"] = 0
-        else:
-            want = min(parallelism, completions - succeeded) - len(active)
-            for _ in range(max(0, want)):
-                await self.client.create(_pod_from_template(job, "batch/v1", "Job", {"job-name": name}), ns)
-            new["active"] = len(active) + max(0, want)
-        if conds:
-            new["conditions"] = conds
-        if {k: st.get(k) for k in new if k not in ("startTime",)} != {k: v for k, v in new.items() if k != "startTime"}:
-            await self.client.patch("jobs", name, {"status": new}, ns, sub="status")
+from .job import JobController  # noqa: E402,F401  (moved to controllers/job.py)
