@@ -611,6 +611,129 @@ def test_04a_xgmi_probe_gang_pod_runs_rccl_on_exactly_its_gpus():
     run(go(), 400)
 
 
+def _xgmi_pod(name, k, sizes_mib=256):
+    return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "default"},
+            "spec": {"restartPolicy": "Never", "containers": [{
+                "name": "probe", "image": "amdkube/xgmi-probe:latest",
+                "args": ["--max-mib", str(sizes_mib), "--iters", "5"],
+                "resources": {"limits": {"amd.com/gpu": str(k)}}}]}}
+
+
+def _per_link_gbps(b, idx: list[int]) -> float | None:
+    """The xGMI per-link bandwidth amd-smi reports between the given GPUs (the driver's max of
+    amdsmi_get_minmax_bandwidth_between_processors, MB/s; else link_metrics max_bandwidth)."""
+    topo = b.topology()
+    vals = [topo[i][j].get("max_bw_mbps") for i in idx for j in idx if i != j]
+    vals = [v / 1000.0 for v in vals if v]
+    if vals:
+        return min(vals)
+    for i in idx:
+        lm = [x.get("max_bandwidth_gbps") for x in b.link_metrics(i) if x.get("max_bandwidth_gbps")]
+        if lm:
+            return float(min(lm))
+    return None
+
+
+def test_04c_xgmi_allreduce_bandwidth_at_expectation():
+    """BASELINE config 4: an xgmi-probe pod on min(4, n) GPUs measures the RCCL all-reduce at
+    256 MiB; its bus bandwidth must reach at least half the per-link xGMI bandwidth amd-smi
+    reports (a PCIe fallback would not). With n >= 8, two 4-GPU probe pods run at once on
+    disjoint sets that each sit in one NUMA domain. On a 1-GPU node there is no link: the
+    bandwidth assertion is skipped with the reason, the pod must still run and verify."""
+    from amdkube.smi import AmdSmiBackend
+    b = AmdSmiBackend()
+    n_node = len(b.gpus())
+    k = min(4, n_node)
+
+    async def go():
+        async with LocalCluster(gpus="amdsmi", relist_period=0.5, with_controllers=False) as lc:
+            node = await lc.wait_gpus(k, 60)
+            attrs = node["status"]["extendedResources"]["amd.com/gpu"]["resources"]
+            names = ["bw-a", "bw-b"] if n_node >= 8 else ["bw-a"]
+            for nm in names:
+                await lc.client.create(_xgmi_pod(nm, k))
+            out = {}
+            for nm in names:
+                pod = await wait_pod(lc.client, "default", nm, ("Succeeded", "Failed"), 240)
+                logs = await lc.client.logs("default", nm)
+                assert pod["status"]["phase"] == "Succeeded", (pod["status"], logs[-2000:])
+                x = json.loads(logs[logs.index("{\"gpus\""):logs.rindex("}") + 1])
+                assert x["verify"]["wrong"] == 0 and x["gpus"] == k, x
+                out[nm] = (pod, x)
+            if len(names) == 2:
+                sets = [set(d for er in out[nm][0]["spec"]["extendedResources"] for d in er["assigned"]) for nm in names]
+                assert not (sets[0] & sets[1]), sets
+                for s_ in sets:
+                    numa = {attrs[d]["attributes"].get("amd.com/numa-node") for d in s_}
+                    assert len(numa) == 1, (s_, numa)
+            if k < 2:
+                print("xgmi bandwidth assertion skipped: 1 GPU on this node, no xGMI link to measure")
+                return
+            for nm in names:
+                pod, x = out[nm]
+                assigned = [d for er in pod["spec"]["extendedResources"] for d in er["assigned"]]
+                idx = [int(attrs[d]["attributes"]["amd.com/index"]) for d in assigned]
+                link = _per_link_gbps(b, idx)
+                big = max(x["allreduce"], key=lambda r: r["bytes"])
+                assert big["bytes"] >= 256 << 20, x["allreduce"]
+                if link is None:
+                    pytest.skip("amd-smi reports no xGMI link bandwidth on this node")
+                assert big["busbw_gbps"] >= 0.5 * link, (nm, big, link)
+                print(f"{nm}: all-reduce busbw {big['busbw_gbps']:.1f} GB/s >= 0.5 x {link:.1f} GB/s per link")
+    try:
+        run(go(), 600)
+    finally:
+        b.close()
+
+
+def test_03b_gpu_selector_pods_on_real_attributes():
+    """BASELINE config 3: a pod asking for min(4, n) GPUs with `amd.com/gpu-type In [MI355X]`
+    and `amd.com/gpu-memory Gt 262143` (MiB) runs to Succeeded on the assigned GPUs of the real
+    amd-smi backend; one asking for `gpu-memory Gt 1000000` stays Pending with a
+    FailedScheduling event."""
+    from amdkube.smi import AmdSmiBackend
+    b = AmdSmiBackend()
+    k = min(4, len(b.gpus()))
+    b.close()
+
+    def sel_pod(name, mem_gt):
+        return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "default"},
+                "spec": {"restartPolicy": "Never",
+                         "extendedResources": [{"name": "gpus", "resources": {"limits": {"amd.com/gpu": str(k)}},
+                                                "affinity": {"required": [
+                                                    {"key": "amd.com/gpu-type", "operator": "In", "values": ["MI355X"]},
+                                                    {"key": "amd.com/gpu-memory", "operator": "Gt", "values": [str(mem_gt)]}]}}],
+                         "containers": [{"name": "vadd", "image": "rocm/vector-add", "args": ["--print-uuid"],
+                                         "extendedResourceRequests": ["gpus"]}]}}
+
+    async def go():
+        async with LocalCluster(gpus="amdsmi", relist_period=0.5, with_controllers=False) as lc:
+            node = await lc.wait_gpus(k, 60)
+            attrs = node["status"]["extendedResources"]["amd.com/gpu"]["resources"]
+            await lc.client.create(sel_pod("fits", 262143))
+            p = await wait_pod(lc.client, "default", "fits", ("Succeeded", "Failed"), 180)
+            logs = await lc.client.logs("default", "fits")
+            assert p["status"]["phase"] == "Succeeded" and "Test PASSED" in logs, (p["status"], logs[-1500:])
+            assigned = p["spec"]["extendedResources"][0]["assigned"]
+            assert len(assigned) == k
+            for d in assigned:
+                assert attrs[d]["attributes"]["amd.com/gpu-type"] == "MI355X"
+                assert int(attrs[d]["attributes"]["amd.com/gpu-memory"]) > 262143
+            await lc.client.create(sel_pod("too-big", 1000000))
+            deadline = time.time() + 30
+            why = None
+            while time.time() < deadline and why is None:
+                evs, _ = await lc.client.list("events", "default")
+                why = next((e for e in evs if (e.get("involvedObject") or {}).get("name") == "too-big"
+                            and e.get("reason") == "FailedScheduling"), None)
+                await asyncio.sleep(0.3)
+            assert why is not None, "no FailedScheduling event"
+            p = await lc.client.get("pods", "too-big", "default")
+            assert p["status"]["phase"] == "Pending" and not p["spec"].get("nodeName")
+            print("selector pod ran on", assigned, "| unsatisfiable one:", why.get("message"))
+    run(go(), 300)
+
+
 def test_04_probe_binaries():
     r = subprocess.run([os.path.join(BIN, "hbm-probe"), "--mib", "1024", "--iters", "3"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
