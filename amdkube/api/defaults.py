@@ -39,6 +39,10 @@ def _default_container(c: dict):
             req.setdefault(k, v)
     for p in c.get("ports") or []:
         p.setdefault("protocol", "TCP")
+    for e in c.get("env") or []:               # SetDefaults_ObjectFieldSelector
+        fr = (e.get("valueFrom") or {}).get("fieldRef")
+        if fr is not None:
+            fr.setdefault("apiVersion", "v1")
     for probe in ("livenessProbe", "readinessProbe"):
         pr = c.get(probe)
         if pr:
@@ -70,6 +74,9 @@ def default_pod_spec(spec: dict):
     for v in spec.get("volumes") or []:
         if not any(k for k in v if k != "name"):
             v["emptyDir"] = {}
+        for it in (v.get("downwardAPI") or {}).get("items") or []:
+            if it.get("fieldRef") is not None:
+                it["fieldRef"].setdefault("apiVersion", "v1")
 
 
 def default_pod(pod: dict):

@@ -162,15 +162,156 @@ def _validate_container(c: dict, path: str, init: bool) -> list[str]:
         if hp and key in ports:
             errs.append(f"{path}.ports[{i}].hostPort: Duplicate value: {hp}")
         ports.add(key)
-    for i, e in enumerate(c.get("env") or []):
-        if not e.get("name"):
-            errs.append(f"{path}.env[{i}].name: Required value")
+    errs += validate_env(c.get("env") or [], path + ".env")
+    errs += validate_env_from(c.get("envFrom") or [], path + ".envFrom")
     if init:
         for probe in ("livenessProbe", "readinessProbe"):
             if c.get(probe):
                 errs.append(f"{path}.{probe}: Invalid value: must not be set for init containers")
     if (c.get("securityContext") or {}).get("privileged") and not CAPABILITIES["allow_privileged"]:
         errs.append(f"{path}.securityContext.privileged: Forbidden: disallowed by cluster policy")
+    return errs
+
+
+_ENV_NAME_RE = re.compile(r"^[-._a-zA-Z][-._a-zA-Z0-9]*$")
+ENV_FIELD_PATHS = ("metadata.name", "metadata.namespace", "metadata.uid", "spec.nodeName", "spec.serviceAccountName",
+                   "status.hostIP", "status.podIP")
+VOLUME_FIELD_PATHS = ("metadata.name", "metadata.namespace", "metadata.labels", "metadata.annotations", "metadata.uid")
+ENV_RESOURCE_FIELDS = ("limits.cpu", "limits.memory", "limits.ephemeral-storage", "requests.cpu", "requests.memory",
+                       "requests.ephemeral-storage")
+
+
+def is_env_var_name(v: str) -> list[str]:
+    """apimachinery validation.go IsEnvVarName (:305-319) with hasChDirPrefix (:380-391)."""
+    errs = []
+    if not _ENV_NAME_RE.match(v):
+        errs.append("a valid environment variable name must consist of alphabetic characters, digits, '_', '-', or '.', "
+                    "and must not start with a digit (e.g. 'my.env-name',  or 'MY_ENV.NAME',  or 'MyEnvName1', regex used "
+                    "for validation is '[-._a-zA-Z][-._a-zA-Z0-9]*')")
+    if v == ".":
+        errs.append("must not be '.'")
+    elif v == "..":
+        errs.append("must not be '..'")
+    elif v.startswith(".."):
+        errs.append("must not start with '..'")
+    return errs
+
+
+def _validate_ref_name(name: str, path: str) -> list[str]:
+    """ValidateConfigMapName / ValidateSecretName: a DNS-1123 subdomain."""
+    if not name:
+        return [f"{path}: Required value"]
+    return [f"{path}: Invalid value: {name!r}: {msg}" for msg in is_dns1123_subdomain(name)]
+
+
+def _split_subscript(fp: str):
+    """fieldpath.SplitMaybeSubscriptedPath: "metadata.labels['k']" -> ("metadata.labels", "k")."""
+    if not fp.endswith("']"):
+        return fp, None
+    base, sep, sub = fp[:-2].partition("['")
+    if not sep or not base:
+        return fp, None
+    return base, sub
+
+
+_DOWNWARD_LABELS = ("metadata.annotations", "metadata.labels", "metadata.name", "metadata.namespace", "metadata.uid",
+                    "spec.nodeName", "spec.restartPolicy", "spec.serviceAccountName", "spec.schedulerName",
+                    "status.phase", "status.hostIP", "status.podIP")
+
+
+def validate_object_field_selector(fs: dict, expressions, path: str) -> list[str]:
+    """validateObjectFieldSelector (validation.go:1948-1985) with ConvertDownwardAPIFieldLabel
+    (pods/helpers.go:29-62): apiVersion v1, a convertible label, a subscript only on labels /
+    annotations (the key a qualified name), otherwise one of `expressions`."""
+    version, fp = fs.get("apiVersion") or "", fs.get("fieldPath") or ""
+    if not version:
+        return [f"{path}.apiVersion: Required value"]
+    if not fp:
+        return [f"{path}.fieldPath: Required value"]
+    base, sub = _split_subscript(fp)
+    conv_err = None
+    if version != "v1":
+        conv_err = f"unsupported pod version: {version}"
+    elif sub is not None and base not in ("metadata.annotations", "metadata.labels"):
+        conv_err = f"field label does not support subscript: {fp}"
+    elif sub is None and fp not in _DOWNWARD_LABELS and fp != "spec.host":
+        conv_err = f"field label not supported: {fp}"
+    if conv_err:
+        return [f"{path}.fieldPath: Invalid value: {fp!r}: error converting fieldPath: {conv_err}"]
+    if fp == "spec.host":
+        fp = "spec.nodeName"
+    if sub is not None:
+        key = sub.lower() if base == "metadata.annotations" else sub
+        return [f"{path}: Invalid value: {sub!r}: {msg}" for msg in is_qualified_name(key)]
+    if fp not in expressions:
+        return [f"{path}.fieldPath: Unsupported value: {fp!r}: supported values: "
+                + ", ".join(f'"{x}"' for x in sorted(expressions))]
+    return []
+
+
+def validate_env(env: list, path: str) -> list[str]:
+    """core/validation ValidateEnv + validateEnvVarValueFrom (validation.go:1879-1940)."""
+    errs = []
+    for i, e in enumerate(env):
+        p = f"{path}[{i}]"
+        name = e.get("name") or ""
+        if not name:
+            errs.append(f"{p}.name: Required value")
+        else:
+            errs += [f"{p}.name: Invalid value: {name!r}: {msg}" for msg in is_env_var_name(name)]
+        vf = e.get("valueFrom")
+        if vf is None:
+            continue
+        vp = f"{p}.valueFrom"
+        n = 0
+        fr = vf.get("fieldRef")
+        if fr is not None:
+            n += 1
+            errs += validate_object_field_selector(fr, ENV_FIELD_PATHS, vp + ".fieldRef")
+        rf = vf.get("resourceFieldRef")
+        if rf is not None:
+            n += 1
+            res = rf.get("resource") or ""
+            if not res:
+                errs.append(f"{vp}.resourceFieldRef.resource: Required value")
+            elif res not in ENV_RESOURCE_FIELDS:
+                errs.append(f"{vp}.resourceFieldRef.resource: Unsupported value: {res!r}")
+        for kind in ("configMapKeyRef", "secretKeyRef"):
+            ref = vf.get(kind)
+            if ref is None:
+                continue
+            n += 1
+            errs += _validate_ref_name(ref.get("name") or "", f"{vp}.{kind}.name")
+            key = ref.get("key") or ""
+            if not key:
+                errs.append(f"{vp}.{kind}.key: Required value")
+            else:
+                errs += [f"{vp}.{kind}.key: Invalid value: {key!r}: {msg}" for msg in is_config_map_key(key)]
+        if n == 0:
+            errs.append(f"{vp}: Invalid value: \"\": must specify one of: `fieldRef`, `resourceFieldRef`, "
+                        "`configMapKeyRef` or `secretKeyRef`")
+        elif e.get("value"):
+            errs.append(f"{vp}: Invalid value: \"\": may not be specified when `value` is not empty")
+        elif n > 1:
+            errs.append(f"{vp}: Invalid value: \"\": may not have more than one field specified at a time")
+    return errs
+
+
+def validate_env_from(env_from: list, path: str) -> list[str]:
+    """ValidateEnvFrom (validation.go:2007-2035): prefix is an env var name; one source."""
+    errs = []
+    for i, e in enumerate(env_from):
+        p = f"{path}[{i}]"
+        prefix = e.get("prefix") or ""
+        if prefix:
+            errs += [f"{p}.prefix: Invalid value: {prefix!r}: {msg}" for msg in is_env_var_name(prefix)]
+        srcs = [k for k in ("configMapRef", "secretRef") if e.get(k) is not None]
+        for k in srcs:
+            errs += _validate_ref_name((e.get(k) or {}).get("name") or "", f"{p}.{k}.name")
+        if not srcs:
+            errs.append(f"{path}: Invalid value: \"\": must specify one of: `configMapRef` or `secretRef`")
+        elif len(srcs) > 1:
+            errs.append(f"{path}: Invalid value: \"\": may not have more than one field specified at a time")
     return errs
 
 
@@ -221,6 +362,9 @@ def _validate_volume_items(v: dict, path: str) -> list[str]:
             errs += validate_local_descending_path(it.get("path") or "", f"{path}.{src_key}.items[{i}].path")
     for i, it in enumerate((v.get("downwardAPI") or {}).get("items") or []):
         errs += validate_local_descending_path(it.get("path") or "", f"{path}.downwardAPI.items[{i}].path")
+        if it.get("fieldRef") is not None:       # validateDownwardAPIVolumeFile
+            errs += validate_object_field_selector(it["fieldRef"], VOLUME_FIELD_PATHS,
+                                                   f"{path}.downwardAPI.items[{i}].fieldRef")
     for j, srcs in enumerate((v.get("projected") or {}).get("sources") or []):
         for src_key in ("secret", "configMap", "downwardAPI"):
             for i, it in enumerate((srcs.get(src_key) or {}).get("items") or []):

@@ -147,3 +147,84 @@ def test_manifests_and_envelope():
     assert [d["kind"] for d in docs] == ["Pod", "Node"]
     env = encode_envelope(docs[0])
     assert env.startswith(b"k8s\x00") and decode_envelope(env) == docs[0]
+
+
+# TestValidateEnv / TestValidateEnvFrom (pkg/apis/core/validation/validation_test.go:3847-4360)
+def _env_pod(env=None, env_from=None):
+    c = {"name": "c", "image": "x"}
+    if env is not None:
+        c["env"] = env
+    if env_from is not None:
+        c["envFrom"] = env_from
+    pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p", "namespace": "d"}, "spec": {"containers": [c]}}
+    SCHEME.default(pod)
+    return validate_pod(pod)
+
+
+def _fr(path, version="v1"):
+    return {"valueFrom": {"fieldRef": {"apiVersion": version, "fieldPath": path}}}
+
+
+def test_validate_env_success_cases():
+    env = [{"name": n, "value": "value"} for n in ("abc", "ABC", "AbC_123", "a.b.c", "a-b-c")] + [{"name": "abc", "value": ""}]
+    env += [{"name": "abc", **_fr(p)} for p in ("metadata.annotations['key']", "metadata.labels['key']", "metadata.name",
+                                                  "metadata.namespace", "metadata.uid", "spec.nodeName",
+                                                  "spec.serviceAccountName", "status.hostIP", "status.podIP")]
+    env += [{"name": "secret_value", "valueFrom": {"secretKeyRef": {"name": "some-secret", "key": "secret-key"}}},
+            {"name": "ENV_VAR_1", "valueFrom": {"configMapKeyRef": {"name": "some-config-map", "key": "some-key"}}},
+            {"name": "defaulted", "valueFrom": {"fieldRef": {"fieldPath": "metadata.name"}}}]   # apiVersion defaults to v1
+    assert _env_pod(env) == []
+
+
+@pytest.mark.parametrize("env,needle", [
+    ([{"name": ""}], "env[0].name: Required value"),
+    ([{"name": "a!b"}], "env[0].name: Invalid value: 'a!b': a valid environment variable name"),
+    ([{"name": "1=bad", "value": "x"}], "must not start with a digit"),
+    ([{"name": "."}], "env[0].name: Invalid value: '.': must not be"),
+    ([{"name": ".."}], "env[0].name: Invalid value: '..': must not be"),
+    ([{"name": "..abc"}], "env[0].name: Invalid value: '..abc': must not start with"),
+    ([{"name": "abc", "value": "foo", **_fr("metadata.name")}], "valueFrom: Invalid value: \"\": may not be specified when `value`"),
+    ([{"name": "abc", "valueFrom": {}}], "must specify one of: `fieldRef`, `resourceFieldRef`, `configMapKeyRef` or `secretKeyRef`"),
+    ([{"name": "abc", "valueFrom": {"fieldRef": {"apiVersion": "v1", "fieldPath": "metadata.name"},
+                                    "secretKeyRef": {"name": "a-secret", "key": "a-key"}}}],
+     "may not have more than one field specified at a time"),
+    ([{"name": "abc", "valueFrom": {"secretKeyRef": {"name": "$%^&*#", "key": "a-key"}}}], "secretKeyRef.name: Invalid value"),
+    ([{"name": "abc", "valueFrom": {"configMapKeyRef": {"name": "$%^&*#", "key": "k"}}}], "configMapKeyRef.name: Invalid value"),
+    ([{"name": "abc", "valueFrom": {"fieldRef": {"apiVersion": "v1"}}}], "valueFrom.fieldRef.fieldPath: Required value"),
+    ([{"name": "abc", **_fr("metadata.whoops")}], "fieldRef.fieldPath: Invalid value: 'metadata.whoops': error converting fieldPath"),
+    ([{"name": "abc", **_fr("metadata.name['key']")}], "error converting fieldPath: field label does not support subscript"),
+    ([{"name": "abc", **_fr("metadata.labels")}], "fieldRef.fieldPath: Unsupported value: 'metadata.labels': supported values: "
+                                                  '"metadata.name", "metadata.namespace", "metadata.uid", "spec.nodeName", '
+                                                  '"spec.serviceAccountName", "status.hostIP", "status.podIP"'),
+    ([{"name": "abc", **_fr("metadata.annotations['invalid~key']")}], "valueFrom.fieldRef: Invalid value: 'invalid~key'"),
+    ([{"name": "abc", **_fr("metadata.labels['Www.k8s.io/test']")}], "valueFrom.fieldRef: Invalid value: 'Www.k8s.io/test'"),
+    ([{"name": "abc", **_fr("status.phase")}], "fieldRef.fieldPath: Unsupported value: 'status.phase'"),
+    ([{"name": "abc", "valueFrom": {"resourceFieldRef": {"resource": "limits.gpu"}}}], "resourceFieldRef.resource: Unsupported value"),
+])
+def test_validate_env_error_cases(env, needle):
+    errs = _env_pod(env)
+    assert errs and all(needle in e for e in errs), errs
+
+
+def test_validate_env_from():
+    ok = [{"configMapRef": {"name": "abc"}}, {"prefix": "pre_", "configMapRef": {"name": "abc"}},
+          {"prefix": "a.b", "secretRef": {"name": "abc"}}, {"secretRef": {"name": "abc"}}]
+    assert _env_pod(env_from=ok) == []
+    for ef, needle in [([{"configMapRef": {"name": ""}}], "envFrom[0].configMapRef.name: Required value"),
+                       ([{"configMapRef": {"name": "$"}}], "envFrom[0].configMapRef.name: Invalid value"),
+                       ([{"prefix": "a!b", "configMapRef": {"name": "abc"}}], "envFrom[0].prefix: Invalid value: 'a!b'"),
+                       ([{"secretRef": {"name": "&"}}], "envFrom[0].secretRef.name: Invalid value"),
+                       ([{"prefix": "a!b"}], "must specify one of: `configMapRef` or `secretRef`"),
+                       ([{"configMapRef": {"name": "a"}, "secretRef": {"name": "b"}}], "may not have more than one field")]:
+        errs = _env_pod(env_from=ef)
+        assert errs and any(needle in e for e in errs), (ef, errs)
+
+
+def test_downward_api_volume_field_paths():
+    pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p", "namespace": "d"},
+           "spec": {"containers": [{"name": "c", "image": "x"}], "volumes": [{"name": "v", "downwardAPI": {"items": [
+               {"path": "labels", "fieldRef": {"fieldPath": "metadata.labels"}},
+               {"path": "ip", "fieldRef": {"fieldPath": "status.podIP"}}]}}]}}
+    SCHEME.default(pod)
+    errs = validate_pod(pod)
+    assert len(errs) == 1 and "items[1].fieldRef.fieldPath: Unsupported value: 'status.podIP'" in errs[0], errs
