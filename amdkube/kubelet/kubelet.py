@@ -507,6 +507,14 @@ class Kubelet:
         if self.gpu_legacy is not None:   # kubelet_node_status.go:557-562
             from .gpu_legacy import RESOURCE
             cap[RESOURCE] = str(self.gpu_legacy.capacity())
+        if self.gates("LocalStorageCapacityIsolation"):
+            # kubelet_node_status.go:599-606: the root filesystem's size (container manager capacity)
+            import shutil
+            try:
+                cap["ephemeral-storage"] = str(shutil.disk_usage(
+                    self.cfg.root_dir if os.path.isdir(self.cfg.root_dir) else "/").total)
+            except OSError:
+                cap["ephemeral-storage"] = "0"
         return cap
 
     async def register_node(self):

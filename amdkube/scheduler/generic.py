@@ -16,7 +16,7 @@ import logging
 from ..api import meta as m
 from ..utils.trace import Trace
 from . import extended
-from .predicates import ORDER, PREDICATES, PodInfo
+from .predicates import ERR_VOLUME_BIND_CONFLICT, ORDER, PREDICATES, PodInfo
 from .priorities import PRIORITIES, pod_selectors
 
 log = logging.getLogger("amdkube.scheduler")
@@ -31,11 +31,13 @@ LOCAL_PRIORITIES = {"LeastRequestedPriority", "MostRequestedPriority", "Balanced
 class FitError(Exception):
     def __init__(self, pod, n_nodes, failed: dict):
         self.pod, self.n_nodes, self.failed = pod, n_nodes, failed
+        # FitError.Error (core/generic_scheduler.go:70-88): a histogram of reasons, "<n> <reason>"
+        # strings sorted as strings
         counts: dict[str, int] = {}
         for reasons in failed.values():
-            for r in set(reasons):
+            for r in reasons:
                 counts[r] = counts.get(r, 0) + 1
-        msg = ", ".join(f"{c} {r}" for r, c in sorted(counts.items(), key=lambda x: (-x[1], x[0])))
+        msg = ", ".join(sorted(f"{c} {r}" for r, c in counts.items()))
         super().__init__(f"0/{n_nodes} nodes are available: {msg}." if n_nodes else "no nodes available to schedule pods")
 
 
@@ -137,9 +139,7 @@ class GenericScheduler:
         for name, fn in self.predicates:
             ok, r = fn(pi, ni, ctx)
             if not ok:
-                reasons += r
-                if name in ("CheckNodeCondition",):
-                    break
+                reasons += r       # every predicate runs and reports (podFitsOnNode, no early exit)
         if not reasons:
             ok, r = extended.fits(pi, ni)
             reasons += r
@@ -352,7 +352,7 @@ class GenericScheduler:
             from .volumes import match_delayed
             pairs = match_delayed(vol.delayed, self.volumes, host.labels)
             if pairs is None:
-                raise FitError(pod, n_nodes, {host.name: ["node(s) didn't find available persistent volumes to bind"]})
+                raise FitError(pod, n_nodes, {host.name: [ERR_VOLUME_BIND_CONFLICT]})
             self.volume_binds[m.key_of(pod)] = pairs
         trace.log_if_long(self.trace_threshold)
         return host.name, binding

@@ -16,48 +16,52 @@ from __future__ import annotations
 
 from ..api import meta as m
 from ..api.labels import selector_from_set
-from .predicates import OK, _fail
+from .predicates import ERR_NODE_LABEL_PRESENCE_VIOLATED, ERR_SERVICE_AFFINITY_VIOLATED, OK, _fail
 
 MAX = 10.0
 
 
-def _service_pods(pi, ctx):
-    """Pods already placed that belong to a service selecting the incoming pod (same namespace)."""
+def _service_affinity_pods(pi, ni, ctx):
+    """serviceAffinityMetadataProducer + FilterOutPods (predicates.go:829-847, :898): when a
+    Service in the pod's namespace selects it, the placed pods of that namespace whose labels
+    carry all of the pod's labels, as (pod, node) — pods the candidate node's NodeInfo does not
+    hold are skipped."""
     ns = m.namespace_of(pi.pod)
-    sels = [selector_from_set((s.get("spec") or {}).get("selector") or {}) for s in (ctx.services() if ctx else [])
-            if m.namespace_of(s) == ns and (s.get("spec") or {}).get("selector")]
-    sels = [s for s in sels if s.matches(pi.labels)]
-    if not sels:
+    if not any(m.namespace_of(s) == ns and (s.get("spec") or {}).get("selector") is not None
+               and selector_from_set((s.get("spec") or {}).get("selector") or {}).matches(pi.labels)
+               for s in (ctx.services() if ctx else [])):
         return []
+    own = selector_from_set(pi.labels)
     out = []
-    for ni in ctx.nodes:
-        for p in ni.pods.values():
-            if m.namespace_of(p) == ns and m.key_of(p) != pi.key and any(s.matches(m.labels_of(p)) for s in sels):
-                out.append((p, ni))
+    for other in (ctx.nodes if ctx else [ni]):
+        for p in other.pods.values():
+            if m.namespace_of(p) == ns and own.matches(m.labels_of(p)):
+                out.append((p, other))
     return out
 
 
 def service_affinity(labels: list[str]):
+    """checkServiceAffinity (predicates.go:886-922): labels the pod's nodeSelector does not pin
+    are taken from the node of the first placed pod of its service."""
     def pred(pi, ni, ctx=None):
         want = {k: pi.node_selector[k] for k in labels if k in pi.node_selector}
-        missing = [k for k in labels if k not in want]
-        if missing and ctx is not None:
-            placed = _service_pods(pi, ctx)
+        if len(want) < len(labels):
+            placed = _service_affinity_pods(pi, ni, ctx)
             if placed:
                 first = placed[0][1]
-                for k in missing:
-                    if k in first.labels:
+                for k in labels:
+                    if k not in want and k in first.labels:
                         want[k] = first.labels[k]
         if all(ni.labels.get(k) == v for k, v in want.items()):
             return OK
-        return _fail("CheckServiceAffinity")
+        return _fail(ERR_SERVICE_AFFINITY_VIOLATED)
     return pred
 
 
 def labels_presence(labels: list[str], presence: bool):
     def pred(pi, ni, ctx=None):
         has = all(k in ni.labels for k in labels) if presence else not any(k in ni.labels for k in labels)
-        return OK if has else _fail("CheckNodeLabelPresence")
+        return OK if has else _fail(ERR_NODE_LABEL_PRESENCE_VIOLATED)
     return pred
 
 

@@ -122,10 +122,13 @@ def no_volume_zone_conflict(pv_list, node_labels: dict) -> bool:
 
 
 def max_pd_limit(kind: str) -> int:
-    env = os.environ.get("KUBE_MAX_PD_VOLS")
-    if env and env.isdigit():
-        return int(env)
-    return MAX_PD[kind][1]
+    """getMaxVols (predicates.go:272-284): KUBE_MAX_PD_VOLS when it is a positive integer."""
+    env = os.environ.get("KUBE_MAX_PD_VOLS", "")
+    try:
+        n = int(env)
+    except ValueError:
+        n = 0
+    return n if n > 0 else MAX_PD[kind][1]
 
 
 def pv_node_affinity_ok(pv: dict, node_labels: dict) -> bool:

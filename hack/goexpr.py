@@ -20,7 +20,7 @@ _TOKEN = re.compile(r"""
   | (?P<str>"(?:[^"\\]|\\.)*"|`[^`]*`)
   | (?P<num>-?\d+(?:\.\d+)?(?:[eE][-+]?\d+)?)
   | (?P<ident>[A-Za-z_][A-Za-z0-9_]*(?:\.[A-Za-z_][A-Za-z0-9_]*)*)
-  | (?P<punct>\[\]|[(){}\[\],:&*=])
+  | (?P<punct>\[\]|[(){}\[\],:&*=+])
 """, re.S | re.X)
 
 
@@ -37,10 +37,18 @@ def tokenize(src: str) -> list[tuple[str, str]]:
     return out
 
 
+class GoField(str):
+    """A composite-literal key written as a bare Go identifier (a struct field name), as opposed
+    to a string / named-constant map key; `hook`s rename only these."""
+
+
 class Evaluator:
-    def __init__(self, funcs: dict | None = None, names: dict | None = None):
+    def __init__(self, funcs: dict | None = None, names: dict | None = None, hook=None):
         self.funcs = dict(funcs or {})
         self.names = {"nil": None, "true": True, "false": False, **(names or {})}
+        # hook(type_name | None, value) post-processes every keyed struct literal (type_name None
+        # for an element whose type Go lets the source elide); map literals are left alone.
+        self.hook = hook
 
     # ------------------------------------------------------------------ driver
     def eval(self, src: str):
@@ -63,10 +71,17 @@ class Evaluator:
 
     # ------------------------------------------------------------------ grammar
     def expr(self):
-        kind, val = self.peek()
-        if val == "&":
+        v = self.unary()
+        while self.peek()[1] == "+":              # string concatenation / integer sum
             self.take()
-            return self.expr()
+            v = v + self.unary()
+        return v
+
+    def unary(self):
+        kind, val = self.peek()
+        if val in ("&", "*"):
+            self.take()
+            return self.unary()
         if kind == "str":
             self.take()
             return _unquote(val)
@@ -78,11 +93,11 @@ class Evaluator:
             self.type_name()
             return self.literal_body()
         if val == "{":
-            return self.literal_body()
+            return self._hooked(None, self.literal_body())
         if kind == "ident":
             if val == "map" and self.peek(1)[1] == "[":
                 self.type_name()
-                return self.literal_body()
+                return self.literal_body(is_map=True)
             self.take()
             nxt = self.peek()[1]
             if nxt == "(":
@@ -92,11 +107,20 @@ class Evaluator:
                     raise NameError(f"goexpr: no helper for {val}()")
                 return fn(*args)
             if nxt == "{":
-                return self.literal_body()
+                return self._hooked(val, self.literal_body(is_map=val in self.map_types))
             if val in self.names:
                 return self.names[val]
             raise NameError(f"goexpr: unknown name {val}")
         raise SyntaxError(f"goexpr: unexpected {kind} {val!r}")
+
+    map_types: frozenset = frozenset()
+
+    def _hooked(self, type_name, v):
+        if v == [] and self.hook is not None:
+            v = {}                      # `T{}`: an empty struct (empty slices are written []T{})
+        if self.hook is not None and isinstance(v, dict) and any(isinstance(k, GoField) for k in v):
+            return self.hook(type_name, v)
+        return v
 
     def type_name(self):
         """Skip a type: *pkg.T, []T, map[K]V."""
@@ -126,13 +150,20 @@ class Evaluator:
         self.take(")")
         return out
 
-    def literal_body(self):
+    def literal_body(self, is_map=False):
         self.take("{")
         keyed, items = None, []
         while self.peek()[1] != "}":
-            if self.peek(1)[1] == ":" and self.peek()[0] in ("ident", "str"):
-                k = self.take()[1]
-                k = _unquote(k) if k.startswith(('"', "`")) else k
+            if self.peek(1)[1] == ":" and self.peek()[0] in ("ident", "str", "num"):
+                kind, k = self.take()
+                if kind == "str":
+                    k = _unquote(k)
+                elif kind == "num":
+                    k = int(k)
+                elif k in self.names and (is_map or "." in k):
+                    k = self.names[k]
+                elif not is_map:
+                    k = GoField(k)
                 self.take(":")
                 keyed = keyed if keyed is not None else {}
                 keyed[k] = self.expr()
@@ -180,3 +211,62 @@ def block_after(src: str, anchor: str, start: int = 0) -> tuple[str, int]:
 
 def line_of(src: str, offset: int) -> int:
     return src.count("\n", 0, offset) + 1
+
+
+# ---------------------------------------------------------------------------- k8s API objects
+# Go struct field -> JSON name where the json tag is not the field name with its leading
+# acronym lower-cased; None = an embedded struct whose fields are inlined.
+JSON_FIELD = {"ObjectMeta": "metadata", "ListMeta": "metadata", "RBDImage": "image", "RBDPool": "pool",
+              "CephMonitors": "monitors", "TypeMeta": None, "VolumeSource": None, "PersistentVolumeSource": None,
+              "LocalObjectReference": None, "Handler": None, "PodSecurityPolicySpec": "spec"}
+
+
+def json_key(field: str) -> str:
+    if field in JSON_FIELD:
+        return JSON_FIELD[field]
+    i = 0
+    while i < len(field) and field[i].isupper():
+        i += 1
+    if i == len(field):
+        return field.lower()                      # UID, IQN, RBD
+    if i > 1:
+        i -= 1                                    # PDName -> pdName, HostIP -> hostIP
+    return field[:i].lower() + field[i:]
+
+
+def k8s_hook(type_name, v: dict) -> dict:
+    """A keyed Go struct literal -> the JSON object the apiserver would serve."""
+    out = {}
+    for k, val in v.items():
+        if not isinstance(k, GoField):
+            out[k] = val
+            continue
+        jk = json_key(k)
+        if jk is None:
+            if isinstance(val, dict):
+                out.update(val)
+            continue
+        if val is None:
+            continue
+        out[jk] = val
+    return out
+
+
+_CONST = re.compile(r'^\s+([A-Z]\w*)\s+(?:[\w.]+\s+)?=\s+"((?:[^"\\]|\\.)*)"', re.M)
+
+
+def go_string_constants(path: str, prefix: str) -> dict:
+    """`Name Type = "value"` constants of a Go file as {prefix + Name: value}."""
+    return {prefix + n: val for n, val in _CONST.findall(open(path).read())}
+
+
+def k8s_names(ref: str) -> dict:
+    """The core/v1 and meta/v1 string constants tables refer to (v1.ResourceCPU, metav1.LabelSelectorOpIn)."""
+    import os
+    names = {}
+    names.update(go_string_constants(os.path.join(ref, "staging/src/k8s.io/api/core/v1/types.go"), "v1."))
+    names.update(go_string_constants(os.path.join(ref, "staging/src/k8s.io/apimachinery/pkg/apis/meta/v1/types.go"),
+                                     "metav1."))
+    names.update(go_string_constants(os.path.join(ref, "staging/src/k8s.io/api/storage/v1/types.go"), "storagev1."))
+    names.update(go_string_constants(os.path.join(ref, "pkg/kubelet/apis/well_known_labels.go"), "kubeletapis."))
+    return names

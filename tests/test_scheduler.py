@@ -190,7 +190,7 @@ def test_predicates_taints_selector_resources_condition():
     with pytest.raises(FitError) as ei:
         asyncio.run(g.schedule(pod(cpu="2")))
     msg = str(ei.value)
-    assert "taints" in msg and "Insufficient cpu" in msg and "not ready" in msg
+    assert "PodToleratesNodeTaints" in msg and "Insufficient cpu" in msg and "NodeNotReady" in msg
     p = pod(cpu="500m")
     p["spec"]["tolerations"] = [{"key": "dedicated", "operator": "Equal", "value": "ml", "effect": "NoSchedule"}]
     p["spec"]["nodeSelector"] = {"kubernetes.io/hostname": "node-0000"}

@@ -65,7 +65,7 @@ def test_zone_conflict_and_missing_claims():
     c, g = _sched(_nodes("rack-a", "rack-c", None), [pv], [_pvc("data", volume="pv-a")])
     fit, failed, _ = asyncio.run(g.find_nodes_that_fit(_pi(g, _vpod("p", "data")), c.ready_nodes()))
     assert sorted(ni.name for ni in fit) == ["n0", "n2"]        # rack-a is one of the PV's zones; n2 has no zone
-    assert failed["n1"] == ["node(s) had no available volume zone"]
+    assert failed["n1"] == ["NoVolumeZoneConflict"]
     with pytest.raises(FitError) as e:
         asyncio.run(g.schedule(_vpod("q", "nope")))
     assert 'persistentvolumeclaim "nope" not found' in str(e.value)
@@ -91,10 +91,10 @@ def test_max_cloud_disk_count_and_disk_conflicts(monkeypatch):
     asyncio.run(g.schedule(_vpod("same", inline=[gce(1)])))             # shared read-only, already counted
     with pytest.raises(FitError) as e:
         asyncio.run(g.schedule(_vpod("same-rw", inline=[gce(1, False)])))
-    assert "no available disk" in str(e.value)                         # NoDiskConflict: a writer needs it alone
+    assert "NoDiskConflict" in str(e.value)                      # NoDiskConflict: a writer needs it alone
     with pytest.raises(FitError) as e:
         asyncio.run(g.schedule(_vpod("third", inline=[gce(9)])))
-    assert "exceed max volume count" in str(e.value)
+    assert "MaxVolumeCount" in str(e.value)
     with pytest.raises(FitError):
         asyncio.run(g.schedule(_vpod("via-pv", "g3")))                 # counted through its PV too
     asyncio.run(g.schedule(_vpod("ebs", inline=[{"name": "e", "awsElasticBlockStore": {"volumeID": "v"}}])))   # other kind
@@ -120,7 +120,7 @@ def test_local_pv_affinity_and_delayed_binding_choice():
     assert host == "n0"
     with pytest.raises(FitError) as e:
         asyncio.run(g.schedule(_vpod("r", "pinned", "scratch")))     # n0 has no 50Gi volume; n1 is not the pinned node
-    assert "volume node affinity conflict" in str(e.value) and "didn't find available persistent volumes" in str(e.value)
+    assert "VolumeNodeAffinityConflict" in str(e.value) and "VolumeBindingNoMatch" in str(e.value)
     with pytest.raises(FitError) as e:
         asyncio.run(g.schedule(_vpod("s", "imm")))
     assert "unbound PersistentVolumeClaims" in str(e.value)
