@@ -45,7 +45,7 @@ def hard_eviction_reservation(thresholds, capacity: dict[str, int]) -> dict[str,
         res = {"memory.available": "memory", "nodefs.available": "ephemeral-storage"}.get(t.signal)
         if res is None or res not in capacity:
             continue
-        out[res] = out.get(res, 0) + t.value(capacity[res])
+        out[res] = out.get(res, 0) + t.quantity(capacity[res])
     return out
 
 

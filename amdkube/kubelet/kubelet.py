@@ -199,6 +199,24 @@ def _semantic(pod: dict):
             md.get("deletionGracePeriodSeconds"))
 
 
+class _ImageGCAdapter:
+    """eviction.ImageGC over the kubelet's image garbage collector."""
+    def __init__(self, k):
+        self.k = k
+
+    async def delete_unused_images(self) -> int:
+        return int(await self.k.image_gc.delete_unused() or 0)
+
+
+class _ContainerGCAdapter:
+    """eviction.ContainerGC: remove every dead container."""
+    def __init__(self, k):
+        self.k = k
+
+    async def delete_all_unused_containers(self):
+        await self.k.container_gc()
+
+
 class Kubelet:
     def __init__(self, client: Client, config: KubeletConfig, smi_backend=None):
         from . import kubeletconfig as kcfg
@@ -264,13 +282,19 @@ class Kubelet:
             self.runtime.legacy, self.runtime.active_pods = self.gpu_legacy, self.active_pods
         from ..security.apparmor import Validator as AppArmorValidator
         self.apparmor = AppArmorValidator(self.gates("AppArmor"), apparmor_fs=config.apparmor_fs)
-        from .eviction import EvictionManager, observe, parse_thresholds
+        from .eviction import Config as EvictionConfig, EvictionManager, parse_thresholds
         hard = config.eviction_hard if config.eviction_hard is not None else f"memory.available<{config.eviction_memory_available_bytes}"
-        self.eviction = EvictionManager(parse_thresholds(hard, config.eviction_soft, config.eviction_soft_grace_period,
-                                                         config.eviction_minimum_reclaim),
-                                        config.eviction_pressure_transition_period, config.eviction_max_pod_grace_period,
-                                        use_priority=self.gates("PodPriority"))
-        self.eviction_observer = lambda: observe(config.root_dir if os.path.isdir(config.root_dir) else "/")
+        # cmd/kubelet/app/server.go: ParseThresholdConfig(enforceNodeAllocatable, evictionHard, ...)
+        thresholds = parse_thresholds(hard, config.eviction_soft, config.eviction_soft_grace_period,
+                                      config.eviction_minimum_reclaim,
+                                      [x.strip() for x in (config.enforce_node_allocatable or "").split(",")])
+        self.eviction = EvictionManager(
+            EvictionConfig(thresholds, config.eviction_pressure_transition_period, config.eviction_max_pod_grace_period),
+            kill_pod=self._evict_kill, summary=lambda: self.stats.summary(), image_gc=_ImageGCAdapter(self),
+            container_gc=_ContainerGCAdapter(self), recorder=self.recorder,
+            node_ref={"kind": "Node", "name": self.node_name, "uid": self.node_name, "namespace": ""},
+            clock=time.monotonic, gates=self.gates)
+        self.eviction.on_eviction = lambda what: self.m_evictions.labels(what).inc()
         from .sysctl import SAFE, SAFE_ANNOTATION, UNSAFE_ANNOTATION, Whitelist
         self._sysctl_admit = (Whitelist(SAFE, SAFE_ANNOTATION), Whitelist(config.allowed_unsafe_sysctls, UNSAFE_ANNOTATION))
         self._kube_reserved = parse_reserved(config.kube_reserved)
@@ -999,9 +1023,9 @@ class Kubelet:
         ok, reason, msg = self._can_run(pod)
         if not ok:
             return False, reason, msg
-        ok, msg = self.eviction.admit(pod, self.pressure)   # eviction_manager.go Admit
+        ok, reason, msg = self.eviction.admit(pod)   # eviction_manager.go Admit
         if not ok:
-            return False, "Evicted", msg
+            return False, reason, msg
         for wl in self._sysctl_admit:       # kubelet.go:838-848 sysctl whitelists as admit handlers
             ok, reason, msg = wl.admit(pod)
             if not ok:
@@ -1716,120 +1740,41 @@ class Kubelet:
             except Exception as e:
                 log.debug("eviction pass failed: %r", e)
 
-    async def _pod_usage(self, signal: str) -> dict[str, int]:
-        """Per-pod usage for ranking: memory working set from the runtime's container stats,
-        or bytes of logs + emptyDir volumes for disk signals."""
-        from .eviction import MEMORY
-        usage: dict[str, int] = {}
-        if signal == MEMORY:
-            for st in await self.cri.list_container_stats():
-                uid = st.attributes.labels.get(L_POD_UID, "")
-                usage[uid] = usage.get(uid, 0) + int(st.memory.working_set_bytes.value)
-            return usage
-        root = os.path.join(self.cfg.root_dir, "pods")
-
-        def walk(uids):   # directory walks block: off the event loop
-            for uid in uids:
-                tot = 0
-                for sub in ("logs", "volumes"):
-                    for dp, _dn, fns in os.walk(os.path.join(root, uid, sub)):
-                        for fn in fns:
-                            try:
-                                tot += os.path.getsize(os.path.join(dp, fn))
-                            except OSError:
-                                pass
-                usage[uid] = tot
-            return usage
-        return await asyncio.to_thread(walk, list(self.pods))
-
-    async def local_storage_eviction(self) -> list[dict]:
-        """eviction_manager.go localStorageEviction (LocalStorageCapacityIsolation): evict, with no
-        grace, pods whose emptyDir use exceeds its sizeLimit, a container whose rootfs + logs
-        exceed its ephemeral-storage limit, or a pod over the sum of its containers' limits."""
-        from ..api.quantity import Quantity
-        summ = await self.stats.summary()
-        usage = {p["podRef"]["uid"]: p for p in summ["pods"]}
-        evicted = []
-        for pod in self.active_pods():
-            st = usage.get(m.uid_of(pod))
-            if st is None:
-                continue
-            spec = pod.get("spec") or {}
-            msg = None
-            vols = {v["name"]: v for v in st.get("volume") or []}
-            for v in spec.get("volumes") or []:
-                lim = (v.get("emptyDir") or {}).get("sizeLimit")
-                if lim and "emptyDir" in v and vols.get(v["name"], {}).get("usedBytes", 0) > Quantity(lim).value():
-                    msg = f'Usage of EmptyDir volume "{v["name"]}" exceeds the limit "{lim}". '
-                    break
-            limits, total_limit, all_limited = {}, 0, True
-            for c in spec.get("containers") or []:
-                lim = ((c.get("resources") or {}).get("limits") or {}).get("ephemeral-storage")
-                if lim:
-                    limits[c["name"]] = (lim, Quantity(lim).value())
-                    total_limit += limits[c["name"]][1]
-                else:
-                    all_limited = False
-            if msg is None:
-                for cs in st.get("containers") or []:
-                    lim = limits.get(cs["name"])
-                    used = (cs.get("rootfs") or {}).get("usedBytes", 0) + (cs.get("logs") or {}).get("usedBytes", 0)
-                    if lim and used > lim[1]:
-                        msg = f'Container {cs["name"]} exceeded its local ephemeral storage limit "{lim[0]}". '
-                        break
-            if msg is None and all_limited and limits and st.get("ephemeral-storage", {}).get("usedBytes", 0) > total_limit:
-                msg = f"Pod ephemeral local storage usage exceeds the total limit of containers {total_limit}. "
-            if msg is None:
-                continue
-            self.eviction.evictions += 1
-            self.m_evictions.labels("ephemeral-storage").inc()
-            self.recorder.event(pod, "Warning", "Evicted", msg)
-            # terminal first: a sync racing the kill sees Failed and never restarts the containers
-            self.status.set(pod, {"phase": "Failed", "reason": "Evicted", "message": msg,
-                                  "conditions": (pod.get("status") or {}).get("conditions") or []})
-            await self.runtime.kill_pod(m.uid_of(pod), 0, pod)
-            evicted.append(pod)
-        return evicted
-
     async def eviction_pass(self):
-        """One synchronize() of the eviction manager: conditions, then at most one eviction."""
-        if self.gates("LocalStorageCapacityIsolation"):
-            if await self.local_storage_eviction():
-                return None
-        obs = self.eviction_observer()
-        pressure = self.eviction.conditions(obs)
+        """One synchronize() of the eviction manager (eviction_manager.go:199-371); the node
+        conditions it holds feed the next node status."""
+        evicted = await self.eviction.synchronize(self._has_dedicated_image_fs, self.active_pods,
+                                                  self._eviction_capacity())
+        pressure = self.eviction.conditions
         if pressure != self.pressure:
             self.pressure = pressure
             self._node_dirty.set()
-        met = self.eviction.met(obs)
-        if not met:
-            return None
-        sig = sorted(met, key=lambda x: x.signal != "memory.available")[0].signal
-        if sig != "memory.available":
-            # reclaimNodeLevelResources: dead containers and unused images before evicting a pod
-            try:
-                await self.container_gc()
-                freed = await self.image_gc.delete_unused()
-            except Exception as e:
-                freed = 0
-                log.debug("node-level reclaim failed: %r", e)
-            if freed and not self.eviction.met(self.eviction_observer()):
-                return None
-        cands = self.active_pods()
-        if self.gates("ExperimentalCriticalPodAnnotation"):
-            # static critical pods are never evicted: they are not re-admitted (eviction_manager.go:377-382)
-            cands = [p for p in cands if not (m.annotations_of(p).get(CRITICAL_ANNOTATION) == ""
-                                              and m.uid_of(p) in self.static)]
-        victim, t = self.eviction.choose(cands, obs, await self._pod_usage(sig))
-        if victim is None:
-            return None
-        res = {"memory.available": "memory"}.get(t.signal, "ephemeral-storage")
-        msg = f"The node was low on resource: {res}."
-        self.eviction.evictions += 1
-        self.m_evictions.labels(t.signal).inc()
-        self.recorder.event(victim, "Warning", "Evicted", msg)
-        # terminal first: a sync racing the kill sees Failed and never restarts the containers
-        self.status.set(victim, {"phase": "Failed", "reason": "Evicted", "message": msg,
-                                 "conditions": (victim.get("status") or {}).get("conditions") or []})
-        await self.runtime.kill_pod(m.uid_of(victim), self.eviction.grace_for(victim, t), victim)
-        return victim
+        return evicted[0] if evicted else None
+
+    async def _evict_kill(self, pod: dict, status: dict, grace: int):
+        """killPodNow: the pod turns Failed/Evicted first (a sync racing the kill sees a terminal
+        pod and never restarts its containers), then its containers stop with `grace`."""
+        self.status.set(pod, {**status, "conditions": (pod.get("status") or {}).get("conditions") or []})
+        await self.runtime.kill_pod(m.uid_of(pod), grace, pod)
+
+    async def _has_dedicated_image_fs(self) -> bool:
+        """DiskInfoProvider.HasDedicatedImageFs: the runtime's image filesystem is a different
+        device from the kubelet's root directory."""
+        try:
+            fsu = (await self.cri.image_fs_info())[0]
+            path = fsu.storage_id.uuid
+            root = self.cfg.root_dir if os.path.isdir(self.cfg.root_dir) else "/"
+            return bool(path) and os.path.exists(path) and os.stat(path).st_dev != os.stat(root).st_dev
+        except Exception:
+            return False
+
+    def _eviction_capacity(self):
+        """CapacityProvider: node memory capacity and the node-allocatable reservation
+        (kube + system reserved + hard eviction, cm GetNodeAllocatableReservation)."""
+        from .cm import hard_eviction_reservation
+        from .eviction import CapacityProvider
+        from ..api.quantity import Quantity
+        cap = {k: Quantity(v).value() for k, v in self._capacity().items() if k in ("memory", "ephemeral-storage")}
+        ev = hard_eviction_reservation([t for t in self.eviction.thresholds if t.hard], cap)
+        res = {k: self._kube_reserved.get(k, 0) + self._system_reserved.get(k, 0) + ev.get(k, 0) for k in cap}
+        return CapacityProvider(cap, res)

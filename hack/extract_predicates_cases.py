@@ -18,7 +18,7 @@ import re
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from goexpr import Evaluator, block_after, k8s_hook, k8s_names, line_of  # noqa: E402
+from goexpr import Evaluator, eval_locals, func_body, k8s_hook, k8s_names, table  # noqa: E402
 
 REF = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
 PKG = "plugin/pkg/scheduler/algorithm/predicates"
@@ -106,68 +106,6 @@ def error_reasons(ref: str) -> dict:
 def preprocess(src: str) -> str:
     src = re.sub(r"new\(([\w.]+)\)", r"&\1{}", src)
     return re.sub(r"makeResources\(([^()]*)\)\.Capacity", r"makeResourcesCapacity(\1)", src)
-
-
-def func_body(src: str, name: str) -> tuple[int, int]:
-    start = src.index(f"func {name}(")
-    _, end = block_after(src, "{", src.index(")", start))
-    return start, end
-
-
-def statement_extent(src: str, i: int) -> int:
-    """End offset of the Go expression starting at i (to the end of its line, brackets balanced)."""
-    depth = 0
-    while i < len(src):
-        c = src[i]
-        if c == '"':
-            i += 1
-            while src[i] != '"':
-                i += 2 if src[i] == "\\" else 1
-        elif c == "`":
-            i = src.index("`", i + 1)
-        elif src.startswith("//", i):
-            if depth == 0:
-                return i
-            i = src.index("\n", i)
-            continue
-        elif c in "({[":
-            depth += 1
-        elif c in ")}]":
-            depth -= 1
-        elif c == "\n" and depth == 0:
-            return i
-        i += 1
-    return i
-
-
-def eval_locals(src: str, ev: Evaluator, start: int, end: int):
-    """Evaluate every `\\tname := <expr>` (and `name = <expr>` of a `var (...)` block) at the top
-    level of a function body, in order; a statement the evaluator cannot read is skipped (it is
-    harness, not data)."""
-    for mt in re.finditer(r"^\t(\w+) := |^\t\t(\w+)\s+= ", src[start:end], re.M):
-        i = start + mt.end()
-        j = statement_extent(src, i)
-        try:
-            ev.names[mt.group(1) or mt.group(2)] = ev.eval(src[i:j])
-        except (SyntaxError, NameError, KeyError, ValueError, TypeError):
-            pass
-
-
-def struct_fields(type_body: str) -> list[str]:
-    return [m.group(1) for m in re.finditer(r"^\s*(\w+)\s+[\w.*\[\]]", type_body.strip("{}"), re.M)]
-
-
-def table(src: str, ev: Evaluator, var: str, start: int) -> tuple[list, int]:
-    at = src.index(f"{var} := []struct", start)
-    type_body, k = block_after(src, "struct {", at)
-    body, _ = block_after(src, "{", k)
-    fields = struct_fields(type_body)
-    out = []
-    for c in ev.eval(body):
-        if isinstance(c, list):
-            c = dict(zip(fields, c))
-        out.append(c)
-    return out, line_of(src, at)
 
 
 TABLES = [   # (test function, table variable, fixture key)

@@ -37,6 +37,14 @@ def tokenize(src: str) -> list[tuple[str, str]]:
     return out
 
 
+class _Unhashable:
+    """A map key that is an object; the literal becomes a list of [key, value] pairs."""
+    __slots__ = ("v",)
+
+    def __init__(self, v):
+        self.v = v
+
+
 class GoField(str):
     """A composite-literal key written as a bare Go identifier (a struct field name), as opposed
     to a string / named-constant map key; `hook`s rename only these."""
@@ -109,7 +117,12 @@ class Evaluator:
             if nxt == "{":
                 return self._hooked(val, self.literal_body(is_map=val in self.map_types))
             if val in self.names:
-                return self.names[val]
+                v = self.names[val]
+                while self.peek()[1] == "[" and self.peek(1)[0] == "num" and self.peek(2)[1] == "]":
+                    self.take()
+                    v = v[int(self.take()[1])]          # indexing a table variable: xs[1]
+                    self.take("]")
+                return v
             raise NameError(f"goexpr: unknown name {val}")
         raise SyntaxError(f"goexpr: unexpected {kind} {val!r}")
 
@@ -162,6 +175,8 @@ class Evaluator:
                     k = int(k)
                 elif k in self.names and (is_map or "." in k):
                     k = self.names[k]
+                    if isinstance(k, (dict, list)):     # a map keyed by objects (map[*v1.Pod]T): keep pairs
+                        k = _Unhashable(k)
                 elif not is_map:
                     k = GoField(k)
                 self.take(":")
@@ -173,6 +188,8 @@ class Evaluator:
                 self.take()
         self.take("}")
         if keyed is not None:
+            if any(isinstance(k, _Unhashable) for k in keyed):
+                return [[k.v if isinstance(k, _Unhashable) else k, v] for k, v in keyed.items()]
             return keyed
         return items
 
@@ -211,6 +228,79 @@ def block_after(src: str, anchor: str, start: int = 0) -> tuple[str, int]:
 
 def line_of(src: str, offset: int) -> int:
     return src.count("\n", 0, offset) + 1
+
+
+# ---------------------------------------------------------------------------- reading test files
+def func_body(src: str, name: str) -> tuple[int, int]:
+    start = src.index(f"func {name}(")
+    _, end = block_after(src, "{", src.index(")", start))
+    return start, end
+
+
+def statement_extent(src: str, i: int) -> int:
+    """End offset of the Go expression starting at i (to the end of its line, brackets balanced)."""
+    depth = 0
+    while i < len(src):
+        c = src[i]
+        if c == '"':
+            i += 1
+            while src[i] != '"':
+                i += 2 if src[i] == "\\" else 1
+        elif c == "`":
+            i = src.index("`", i + 1)
+        elif src.startswith("//", i):
+            if depth == 0:
+                return i
+            i = src.index("\n", i)
+            continue
+        elif c in "({[":
+            depth += 1
+        elif c in ")}]":
+            depth -= 1
+        elif c == "\n" and depth == 0:
+            return i
+        i += 1
+    return i
+
+
+def eval_locals(src: str, ev: Evaluator, start: int, end: int):
+    """Evaluate every `\\tname := <expr>` (and `name = <expr>` of a `var (...)` block) at the top
+    level of a function body, in order; a statement the evaluator cannot read is skipped (it is
+    harness, not data)."""
+    for mt in re.finditer(r"^\t(\w+) := |^\t\t(\w+)\s+= ", src[start:end], re.M):
+        i = start + mt.end()
+        j = statement_extent(src, i)
+        try:
+            ev.names[mt.group(1) or mt.group(2)] = ev.eval(src[i:j])
+        except (SyntaxError, NameError, KeyError, ValueError, TypeError):
+            pass
+
+
+def struct_fields(type_body: str) -> list[str]:
+    return [m.group(1) for m in re.finditer(r"^\s*(\w+)\s+[\w.*\[\]]", type_body.strip("{}"), re.M)]
+
+
+def table(src: str, ev: Evaluator, var: str, start: int) -> tuple[list, int]:
+    """The cases of `var := []struct{...}{...}` (or `map[string]struct{...}{...}`, each case
+    gaining its key as "name") after `start`, positional cases keyed by the struct's fields."""
+    mt = re.compile(rf"\b{re.escape(var)} := (\[\]struct|map\[string\]struct)").search(src, start)
+    if mt is None:
+        raise ValueError(f"no table {var!r}")
+    at = mt.start()
+    type_body, k = block_after(src, "struct {", at)
+    body, _ = block_after(src, "{", k)
+    fields = struct_fields(type_body)
+    raw = ev.eval(body)
+    if mt.group(1).startswith("map"):
+        raw = [{**v, "name": name} if isinstance(v, dict) else {**dict(zip(fields, v)), "name": name}
+               for name, v in ((ev_key, val) for ev_key, val in raw.items())]
+    out = []
+    for c in raw:
+        if isinstance(c, list):
+            c = dict(zip(fields, c))
+        out.append(c)
+    return out, line_of(src, at)
+
 
 
 # ---------------------------------------------------------------------------- k8s API objects

@@ -263,12 +263,14 @@ def test_local_storage_capacity_isolation_eviction():
             evicted = set()
             for _ in range(60):          # until the writes have landed (slow under a loaded machine)
                 lc.kubelet.stats.du.forget("")
-                evicted |= {m.name_of(p) for p in await lc.kubelet.local_storage_eviction()}
+                k = lc.kubelet
+                evicted |= {m.name_of(p) for p in await k.eviction.local_storage_eviction(k.active_pods(), await k.stats.summary())}
                 if evicted >= {"hog", "chatty"}:
                     break
                 await asyncio.sleep(0.25)
             assert evicted == {"hog", "chatty"}, evicted
-            for name, reason in (("hog", "EmptyDir volume"), ("chatty", "local ephemeral storage limit")):
+            # the status names the resource (eviction_manager.go evictPod): EmptyDir / ephemeral-storage
+            for name, reason in (("hog", "low on resource: EmptyDir"), ("chatty", "low on resource: ephemeral-storage")):
                 p = await wait_pod(c, "default", name, ("Failed",), 20)
                 assert p["status"]["reason"] == "Evicted" and reason in p["status"]["message"], p["status"]
             assert (await c.get("pods", "fine", "default"))["status"]["phase"] == "Running"
