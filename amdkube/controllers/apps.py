@@ -26,6 +26,7 @@ import time
 
 from ..api import meta as m
 from ..api.helpers import is_pod_ready, is_pod_terminal
+from ..api.labels import selector_from_set
 from .base import Controller, split_key
 from .workloads import ReplicaSetController, _owned, template_hash
 
@@ -34,20 +35,12 @@ POD_NAME_LABEL = "statefulset.kubernetes.io/pod-name"
 
 
 class ReplicationManager(ReplicaSetController):
+    """pkg/controller/replication: the ReplicaSet controller over a v1 map selector."""
     name = "replicationcontroller"
     owner_api, owner_kind, plural = "v1", "ReplicationController", "replicationcontrollers"
 
-    def setup(self):
-        f = self.mgr.factory
-        self.rs_inf = f.informer("replicationcontrollers")
-        self.pod_inf = self.mgr.pods
-        self.rs_inf.add_handler(on_add=self.enqueue, on_update=lambda o, n: self.enqueue(n), on_delete=self.enqueue)
-        self.pod_inf.add_handler(on_add=self._pod, on_update=lambda o, n: self._pod(n), on_delete=self._pod)
-
-    def _pod(self, pod):
-        ref = m.controller_ref(pod)
-        if ref and ref.get("kind") == "ReplicationController":
-            self.enqueue(f"{m.namespace_of(pod)}/{ref['name']}")
+    def selector_of(self, rc):
+        return selector_from_set((rc.get("spec") or {}).get("selector") or {})
 
 
 # ============================================================================ StatefulSet

@@ -32,6 +32,7 @@ from ..api import meta as m
 from ..api.helpers import is_pod_ready, is_pod_terminal
 from ..client.workqueue import ItemExponentialFailureRateLimiter, RateLimitingQueue
 from .base import Controller, split_key
+from .controller_utils import sort_active_pods
 
 DEFAULT_JOB_BACKOFF, MAX_JOB_BACKOFF = 10.0, 360.0
 SLOW_START_INITIAL_BATCH = 1
@@ -51,22 +52,6 @@ def _condition(kind: str, reason: str = "", message: str = "") -> dict:
     now = m.now_rfc3339()
     return {"type": kind, "status": "True", "lastProbeTime": now, "lastTransitionTime": now, "reason": reason,
             "message": message}
-
-
-def active_pod_order(p: dict):
-    """controller.ActivePods Less: pods to delete first sort first (unscheduled, pending,
-    not ready, ready for less time, more restarts, newer)."""
-    st = p.get("status") or {}
-    phase_rank = {"Pending": 0, "Unknown": 1, "Running": 2}.get(st.get("phase"), 1)
-    ready = is_pod_ready(p)
-    ready_since = 0.0
-    for c in st.get("conditions") or []:
-        if c.get("type") == "Ready" and c.get("status") == "True":
-            ready_since = m.parse_time(c.get("lastTransitionTime")) or 0.0
-    restarts = max((cs.get("restartCount", 0) for cs in st.get("containerStatuses") or []), default=0)
-    created = m.parse_time((p.get("metadata") or {}).get("creationTimestamp")) or 0.0
-    return (bool((p.get("spec") or {}).get("nodeName")), phase_rank, ready, -ready_since if ready else 0.0,
-            -restarts, -created)
 
 
 async def sync_job(job: dict, pods: list, pod_control, previous_retry: int = 0, now: float | None = None,
@@ -129,7 +114,7 @@ async def _manage(job: dict, active_pods: list, succeeded: int, pod_control) -> 
     err: Exception | None = None
     if active > parallelism:
         diff = active - parallelism
-        for p in sorted(active_pods, key=active_pod_order)[:diff]:
+        for p in sort_active_pods(list(active_pods))[:diff]:
             try:
                 await pod_control.delete(p)
                 active -= 1

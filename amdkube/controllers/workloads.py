@@ -38,61 +38,7 @@ def _pod_from_template(owner, api_version, kind, extra_labels=None, node=None):
     return pod
 
 
-class ReplicaSetController(Controller):
-    name = "replicaset"
-    burst = 500
-    owner_api, owner_kind, plural = "apps/v1", "ReplicaSet", "replicasets"
-
-    def setup(self):
-        f = self.mgr.factory
-        self.rs_inf = f.informer("replicasets")
-        self.pod_inf = self.mgr.pods
-        self.rs_inf.add_handler(on_add=self.enqueue, on_update=lambda o, n: self.enqueue(n), on_delete=self.enqueue)
-        self.pod_inf.add_handler(on_add=self._pod, on_update=lambda o, n: self._pod(n), on_delete=self._pod)
-
-    def _pod(self, pod):
-        ref = m.controller_ref(pod)
-        if ref and ref.get("kind") == "ReplicaSet":
-            self.enqueue(f"{m.namespace_of(pod)}/{ref['name']}")
-
-    async def sync(self, key):
-        rs = self.rs_inf.get(key)
-        if rs is None or (rs.get("metadata") or {}).get("deletionTimestamp"):
-            return
-        ns, name = split_key(key)
-        pods = [p for p in _owned(self.pod_inf.list(), rs) if not is_pod_terminal(p)
-                and not (p.get("metadata") or {}).get("deletionTimestamp")]
-        want = int((rs.get("spec") or {}).get("replicas", 1))
-        diff = want - len(pods)
-        if diff > 0:
-            for _ in range(min(diff, self.burst)):
-                await self.client.create(_pod_from_template(rs, self.owner_api, self.owner_kind), ns)
-        elif diff < 0:
-            # delete not-ready / unscheduled pods first (controller_utils ActivePods ordering)
-            pods.sort(key=lambda p: (bool((p.get("spec") or {}).get("nodeName")), is_pod_ready(p),
-                                     (p.get("metadata") or {}).get("creationTimestamp", "")))
-            for p in pods[:-diff]:
-                try:
-                    await self.client.delete("pods", m.name_of(p), ns)
-                except m.StatusError:
-                    pass
-        ready = [p for p in pods if is_pod_ready(p)]
-        # availability = Ready for minReadySeconds (podutil.IsPodAvailable)
-        mrs = int((rs.get("spec") or {}).get("minReadySeconds", 0))
-        avail, wake = 0, None
-        now = time.time()
-        for p in ready:
-            since = m.parse_time((get_condition(p, "Ready") or {}).get("lastTransitionTime")) or 0.0
-            if mrs == 0 or since + mrs <= now:
-                avail += 1
-            else:
-                wake = min(wake or 1e18, since + mrs - now)
-        if wake is not None:
-            self.queue.add_after(key, wake + 0.05)
-        st = {"replicas": len(pods), "readyReplicas": len(ready), "availableReplicas": avail,
-              "fullyLabeledReplicas": len(pods), "observedGeneration": (rs.get("metadata") or {}).get("generation", 1)}
-        if {k: (rs.get("status") or {}).get(k) for k in st} != st:
-            await self.client.patch(self.plural, name, {"status": st}, ns, sub="status")
+from .replicaset import ReplicaSetController  # noqa: E402,F401  (controllers/replicaset.py)
 
 
 def template_hash(tpl) -> str:
