@@ -320,6 +320,12 @@ class ResourceStore:
                 if METRICS_ANNOTATION in (cmd.get("annotations") or {}):
                     ka[METRICS_ANNOTATION] = cmd["annotations"][METRICS_ANNOTATION]
                 keep["annotations"] = ka or None
+            if self.ri.plural == "deployments":
+                # deploymentStatusStrategy keeps spec and labels only: the controller records
+                # the revision annotation through /status (registry/extensions/deployment)
+                keep["annotations"] = m.deepcopy(md.get("annotations"))
+                if keep["annotations"] is None:
+                    keep.pop("annotations")
             new["metadata"] = keep
         elif self.has_status:
             if "status" in cur:

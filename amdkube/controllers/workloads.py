@@ -45,10 +45,6 @@ def template_hash(tpl) -> str:
     return hashlib.sha1(json.dumps(tpl, sort_keys=True).encode()).hexdigest()[:10]
 
 
-REVISION = "deployment.kubernetes.io/revision"
-DESIRED = "deployment.kubernetes.io/desired-replicas"
-MAX_REPLICAS = "deployment.kubernetes.io/max-replicas"
-HASH_LABEL = "pod-template-hash"
 REVISION_HASH_LABEL = "controller-revision-hash"          # DaemonSet and StatefulSet pods / ControllerRevisions
 TEMPLATE_GEN_LABEL = "pod-template-generation"
 
@@ -60,295 +56,7 @@ def _int_or_percent(v, total: int, round_up: bool) -> int:
     return int(v)
 
 
-def resolve_fenceposts(d: dict) -> tuple[int, int]:
-    """(maxSurge, maxUnavailable) for a RollingUpdate deployment (deployment_util.go:959
-    ResolveFenceposts): surge rounds up, unavailable rounds down, and both 0 means 1 unavailable."""
-    spec = d.get("spec") or {}
-    want = int(spec.get("replicas", 1))
-    ru = (spec.get("strategy") or {}).get("rollingUpdate") or {}
-    surge = _int_or_percent(ru.get("maxSurge", "25%"), want, True)
-    unavail = _int_or_percent(ru.get("maxUnavailable", "25%"), want, False)
-    if surge == 0 and unavail == 0:
-        unavail = 1
-    return surge, unavail
-
-
-def _rev(rs) -> int:
-    try:
-        return int(((rs.get("metadata") or {}).get("annotations") or {}).get(REVISION, "0"))
-    except ValueError:
-        return 0
-
-
-def _reps(rs) -> int:
-    return int((rs.get("spec") or {}).get("replicas", 0))
-
-
-def _st(rs, k) -> int:
-    return int((rs.get("status") or {}).get(k, 0))
-
-
-def _copyable(d: dict) -> dict:
-    """Deployment annotations that follow it onto its ReplicaSets (deployment_util.go
-    skipCopyAnnotation): everything but last-applied and the controller's own keys."""
-    skip = {"kubectl.kubernetes.io/last-applied-configuration", REVISION, DESIRED, MAX_REPLICAS,
-            "deployment.kubernetes.io/revision-history"}
-    return {k: v for k, v in ((d.get("metadata") or {}).get("annotations") or {}).items() if k not in skip}
-
-
-def _strip_hash(tpl: dict) -> dict:
-    t = json.loads(json.dumps(tpl or {}))
-    (t.get("metadata") or {}).get("labels", {}).pop(HASH_LABEL, None)
-    return t
-
-
-class DeploymentController(Controller):
-    """pkg/controller/deployment: one ReplicaSet per template (pod-template-hash), revision
-    annotations (max + 1 on every new or re-adopted template, deployment_util.go:50-60),
-    RollingUpdate with maxSurge/maxUnavailable (rolling.go:31-235: scale the new RS up to
-    replicas + surge, scale old RSs down while availability stays ≥ replicas − maxUnavailable,
-    unhealthy old replicas first), Recreate (recreate.go: old to zero, wait for their pods,
-    then new), paused deployments only scale (sync.go:40), spec.rollbackTo (rollback.go:31-117),
-    revisionHistoryLimit cleanup, and the Available / Progressing conditions with
-    progressDeadlineSeconds (progress.go)."""
-    name = "deployment"
-
-    def __init__(self, mgr, clock=time.time):
-        super().__init__(mgr)
-        self.clock = clock
-
-    def setup(self):
-        f = self.mgr.factory
-        self.d_inf = f.informer("deployments")
-        self.rs_inf = f.informer("replicasets")
-        self.pod_inf = self.mgr.pods
-        self.d_inf.add_handler(on_add=self.enqueue, on_update=lambda o, n: self.enqueue(n), on_delete=self.enqueue)
-        self.rs_inf.add_handler(on_add=self._rs, on_update=lambda o, n: self._rs(n), on_delete=self._rs)
-        self.pod_inf.add_handler(on_delete=self._pod)
-
-    def _rs(self, rs):
-        ref = m.controller_ref(rs)
-        if ref and ref.get("kind") == "Deployment":
-            self.enqueue(f"{m.namespace_of(rs)}/{ref['name']}")
-
-    def _pod(self, pod):   # Recreate waits for old pods to be gone
-        ref = m.controller_ref(pod)
-        if ref and ref.get("kind") == "ReplicaSet":
-            rs = self.rs_inf.get(f"{m.namespace_of(pod)}/{ref['name']}")
-            if rs is not None:
-                self._rs(rs)
-
-    def _event(self, d, etype, reason, msg):
-        rec = getattr(self.mgr, "recorder", None)
-        if rec is not None:
-            rec.event(d, etype, reason, msg)
-
-    async def _scale(self, d, rs, n: int):
-        if _reps(rs) == n:
-            return rs
-        ann = {DESIRED: str(int((d.get("spec") or {}).get("replicas", 1))),
-               MAX_REPLICAS: str(int((d.get("spec") or {}).get("replicas", 1)) + self._surge(d))}
-        rs = await self.client.patch("replicasets", m.name_of(rs), {"metadata": {"annotations": ann}, "spec": {"replicas": n}},
-                                     m.namespace_of(rs))
-        self._event(d, "Normal", "ScalingReplicaSet",
-                    f"Scaled {'up' if n > _reps(rs) else 'down'} replica set {m.name_of(rs)} to {n}")
-        return rs
-
-    @staticmethod
-    def _surge(d) -> int:
-        if ((d.get("spec") or {}).get("strategy") or {}).get("type") == "Recreate":
-            return 0
-        return resolve_fenceposts(d)[0]
-
-    async def sync(self, key):
-        d = self.d_inf.get(key)
-        if d is None or (d.get("metadata") or {}).get("deletionTimestamp"):
-            return
-        ns, name = split_key(key)
-        spec = d.get("spec") or {}
-        rss = _owned(self.rs_inf.list(), d)
-        if spec.get("rollbackTo") is not None:
-            await self._rollback(d, rss)
-            return
-        want = int(spec.get("replicas", 1))
-        h = template_hash(spec.get("template") or {})
-        new = next((r for r in rss if m.labels_of(r).get(HASH_LABEL) == h), None)
-        olds = sorted([r for r in rss if r is not new], key=lambda r: (r.get("metadata") or {}).get("creationTimestamp", ""))
-        max_rev = max((_rev(r) for r in olds), default=0)
-        recreate = (spec.get("strategy") or {}).get("type") == "Recreate"
-        if spec.get("paused"):
-            # a paused deployment only scales (proportionally is not needed with one active RS)
-            if new is not None and _reps(new) != want and not any(_reps(r) for r in olds):
-                await self._scale(d, new, want)
-            await self._status(d, new, rss, paused=True)
-            return
-        if new is None:
-            tpl = json.loads(json.dumps(spec.get("template") or {}))
-            tpl.setdefault("metadata", {}).setdefault("labels", {})[HASH_LABEL] = h
-            sel = json.loads(json.dumps(spec.get("selector") or {}))
-            sel.setdefault("matchLabels", {})[HASH_LABEL] = h
-            surge = self._surge(d)
-            if recreate:
-                start = 0
-            else:
-                start = max(0, min(want, want + surge - sum(_reps(r) for r in olds)))
-            rs = {"apiVersion": "apps/v1", "kind": "ReplicaSet",
-                  "metadata": {"name": f"{name}-{h}", "namespace": ns, "labels": {**(tpl["metadata"]["labels"])},
-                               "annotations": {**_copyable(d), REVISION: str(max_rev + 1), DESIRED: str(want),
-                                               MAX_REPLICAS: str(want + surge)},
-                               "ownerReferences": [m.new_controller_ref(d, "apps/v1", "Deployment")]},
-                  "spec": {"replicas": start, "selector": sel, "template": tpl,
-                           "minReadySeconds": int(spec.get("minReadySeconds", 0))}}
-            new = await self.client.create(rs, ns)
-            self._event(d, "Normal", "ScalingReplicaSet", f"Scaled up replica set {m.name_of(new)} to {start}")
-        elif _rev(new) <= max_rev:
-            # an old template came back (rollback or a revert): it becomes the newest revision
-            new = await self.client.patch("replicasets", m.name_of(new),
-                                          {"metadata": {"annotations": {**_copyable(d), REVISION: str(max_rev + 1)}}}, ns)
-        if (d.get("metadata") or {}).get("annotations", {}).get(REVISION) != str(_rev(new)):
-            await self.client.patch("deployments", name, {"metadata": {"annotations": {REVISION: str(_rev(new))}}}, ns)
-        if recreate:
-            await self._recreate(d, new, olds, want)
-        else:
-            await self._rolling(d, new, olds, want)
-        rss = _owned(self.rs_inf.list(), d)
-        await self._status(d, new, rss)
-        await self._cleanup(d, new, olds)
-
-    async def _recreate(self, d, new, olds, want):
-        active = [r for r in olds if _reps(r)]
-        for r in active:
-            await self._scale(d, r, 0)
-        uids = {m.uid_of(r) for r in olds}
-        running = [p for p in self.pod_inf.list() if (m.controller_ref(p) or {}).get("uid") in uids and not is_pod_terminal(p)]
-        if active or running:
-            return
-        await self._scale(d, new, want)
-
-    async def _rolling(self, d, new, olds, want):
-        surge, unavail = resolve_fenceposts(d)
-        all_rs = [new] + olds
-        total = sum(_reps(r) for r in all_rs)
-        # reconcileNewReplicaSet
-        if _reps(new) > want:
-            new = await self._scale(d, new, want)
-        elif _reps(new) < want:
-            n = min(want, _reps(new) + max(0, want + surge - total))
-            if n != _reps(new):
-                new = await self._scale(d, new, n)
-        # reconcileOldReplicaSets
-        total = sum(_reps(r) for r in [new] + olds)
-        old_count = sum(_reps(r) for r in olds)
-        if not old_count:
-            return
-        min_avail = want - unavail
-        new_unavail = _reps(new) - _st(new, "availableReplicas")
-        budget = total - min_avail - new_unavail
-        if budget <= 0:
-            return
-        for r in olds:   # cleanupUnhealthyReplicas: oldest first
-            if budget <= 0:
-                break
-            unhealthy = _reps(r) - _st(r, "availableReplicas")
-            k = min(unhealthy, budget)
-            if k > 0:
-                await self._scale(d, r, _reps(r) - k)
-                r.setdefault("spec", {})["replicas"] = _reps(r) - k
-                budget -= k
-        # scaleDownOldReplicaSetsForRollingUpdate: keep total availability ≥ min_avail
-        avail = sum(_st(r, "availableReplicas") for r in [new] + olds)
-        can = avail - min_avail
-        for r in olds:
-            if can <= 0:
-                break
-            k = min(_reps(r), can)
-            if k > 0:
-                await self._scale(d, r, _reps(r) - k)
-                can -= k
-
-    async def _rollback(self, d, rss):
-        ns, name = m.namespace_of(d), m.name_of(d)
-        to = int(((d.get("spec") or {}).get("rollbackTo") or {}).get("revision", 0))
-        revs = sorted((_rev(r), r) for r in rss)
-        if to == 0:
-            to = revs[-2][0] if len(revs) >= 2 else 0   # LastRevision: the one before the current
-        target = next((r for v, r in revs if v == to and to), None)
-        patch = {"spec": {"rollbackTo": None}}
-        if target is None:
-            self._event(d, "Warning", "DeploymentRollbackRevisionNotFound", "Unable to find the revision to rollback to.")
-        elif _strip_hash((target.get("spec") or {}).get("template")) == _strip_hash((d.get("spec") or {}).get("template")):
-            self._event(d, "Warning", "DeploymentRollbackTemplateUnchanged",
-                        f"The rollback revision contains the same template as current deployment {name!r}")
-        else:
-            patch["spec"]["template"] = _strip_hash((target.get("spec") or {}).get("template"))
-            self._event(d, "Normal", "DeploymentRollback", f"Rolled back deployment {name!r} to revision {to}")
-        await self.client.patch("deployments", name, patch, ns)
-
-    async def _cleanup(self, d, new, olds):
-        limit = (d.get("spec") or {}).get("revisionHistoryLimit", 10)
-        dead = [r for r in olds if _reps(r) == 0 and _st(r, "replicas") == 0]
-        dead.sort(key=_rev)
-        for r in dead[:max(0, len(dead) - int(limit))]:
-            try:
-                await self.client.delete("replicasets", m.name_of(r), m.namespace_of(r))
-            except m.StatusError:
-                pass
-
-    async def _status(self, d, new, rss, paused=False):
-        ns, name = m.namespace_of(d), m.name_of(d)
-        spec = d.get("spec") or {}
-        want = int(spec.get("replicas", 1))
-        unavail = resolve_fenceposts(d)[1] if (spec.get("strategy") or {}).get("type") != "Recreate" else 0
-        avail = sum(_st(r, "availableReplicas") for r in rss)
-        updated = _st(new, "replicas") if new is not None else 0
-        total = sum(_st(r, "replicas") for r in rss)
-        st = {"replicas": total, "updatedReplicas": updated,
-              "readyReplicas": sum(_st(r, "readyReplicas") for r in rss), "availableReplicas": avail,
-              "unavailableReplicas": max(0, total - avail) if total >= want else max(0, want - avail),
-              "observedGeneration": (d.get("metadata") or {}).get("generation", 1)}
-        now = m.format_time(self.clock())
-        old = {c["type"]: c for c in (d.get("status") or {}).get("conditions") or []}
-
-        def cond(typ, status, reason, msg):
-            prev = old.get(typ)
-            if prev and prev.get("status") == status and prev.get("reason") == reason:
-                return prev
-            return {"type": typ, "status": status, "reason": reason, "message": msg, "lastUpdateTime": now,
-                    "lastTransitionTime": prev["lastTransitionTime"] if prev and prev.get("status") == status else now}
-
-        conds = [cond("Available", "True" if avail >= want - unavail else "False",
-                      "MinimumReplicasAvailable" if avail >= want - unavail else "MinimumReplicasUnavailable",
-                      "Deployment has minimum availability." if avail >= want - unavail
-                      else "Deployment does not have minimum availability.")]
-        complete = new is not None and updated == want and avail >= want and total == want
-        rs_name = m.name_of(new) if new is not None else ""
-        if paused:
-            conds.append(cond("Progressing", "Unknown", "DeploymentPaused", "Deployment is paused"))
-        elif complete:
-            conds.append(cond("Progressing", "True", "NewReplicaSetAvailable", f'ReplicaSet "{rs_name}" has successfully progressed.'))
-        else:
-            prev = old.get("Progressing")
-            deadline = spec.get("progressDeadlineSeconds", 600)
-            changed = {k: (d.get("status") or {}).get(k) for k in st} != st
-            if prev and prev.get("reason") == "ProgressDeadlineExceeded":
-                conds.append(prev)
-            elif (deadline is not None and prev is not None and not changed and prev.get("status") == "True" and
-                    self.clock() - (m.parse_time(prev.get("lastUpdateTime")) or self.clock()) > int(deadline)):
-                conds.append(cond("Progressing", "False", "ProgressDeadlineExceeded",
-                                  f'ReplicaSet "{rs_name}" has timed out progressing.'))
-                self._event(d, "Warning", "ProgressDeadlineExceeded", f"Deployment {name!r} has timed out progressing.")
-            else:
-                c = {"type": "Progressing", "status": "True", "reason": "ReplicaSetUpdated",
-                     "message": f'ReplicaSet "{rs_name}" is progressing.', "lastUpdateTime": now,
-                     "lastTransitionTime": prev["lastTransitionTime"] if prev and prev.get("status") == "True" else now}
-                if prev and prev.get("reason") == "ReplicaSetUpdated" and not changed:
-                    c = prev   # no progress since the last sync: keep lastUpdateTime for the deadline
-                conds.append(c)
-                if deadline is not None:
-                    self.queue.add_after(m.key_of(d), float(deadline) + 1.0)
-        st["conditions"] = conds
-        if {k: (d.get("status") or {}).get(k) for k in st} != st:
-            await self.client.patch("deployments", name, {"status": st}, ns, sub="status")
+from .deployment import DeploymentController  # noqa: E402,F401  (controllers/deployment.py)
 
 
 class DaemonSetController(Controller):

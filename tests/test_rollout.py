@@ -12,7 +12,7 @@ import time
 import yaml
 
 from amdkube.api import meta as m
-from amdkube.controllers.workloads import resolve_fenceposts
+from amdkube.controllers.deployment import resolve_fenceposts as _fenceposts
 from amdkube.kubectl.extra import cmd_config_sync, parse_taint
 from amdkube.kubectl.main import COMMANDS, parser
 from amdkube.localcluster import LocalCluster
@@ -34,6 +34,11 @@ async def kubectl(c, *argv):
     if a.command is None:
         a.command = []
     return await COMMANDS[a.cmd](c, a)
+
+
+def resolve_fenceposts(d):
+    ru = ((d.get("spec") or {}).get("strategy") or {}).get("rollingUpdate") or {}
+    return _fenceposts(ru.get("maxSurge", "25%"), ru.get("maxUnavailable", "25%"), d["spec"]["replicas"])
 
 
 def test_fenceposts():
