@@ -291,6 +291,16 @@ def _template_sans_hash(t):
     return t
 
 
+def _prune(v):
+    """Drop null / empty maps and lists: apiequality.Semantic holds nil and empty alike."""
+    if isinstance(v, dict):
+        out = {k: _prune(x) for k, x in v.items()}
+        return {k: x for k, x in out.items() if x is not None and x != {} and x != []}
+    if isinstance(v, list):
+        return [_prune(x) for x in v]
+    return v
+
+
 def equal_ignore_hash(t1, t2) -> bool:
     """EqualIgnoreHash: the labels agree except pod-template-hash, and the rest is equal."""
     l1 = ((t1 or {}).get("metadata") or {}).get("labels") or {}
@@ -307,7 +317,7 @@ def equal_ignore_hash(t1, t2) -> bool:
         md.pop("labels", None)
         if not md:
             t.pop("metadata", None)
-        return t
+        return _prune(t)
     return strip(t1) == strip(t2)
 
 
