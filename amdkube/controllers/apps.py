@@ -2,14 +2,7 @@
 
 Reference:
   * pkg/controller/replication — the ReplicaSet logic over a v1 map selector.
-  * pkg/controller/statefulset/stateful_set_control.go (1.9, apps/v1 defaults) — pods
-    `<set>-<ordinal>` with hostname/subdomain from spec.serviceName; volumeClaimTemplates
-    become PVCs `<claim>-<set>-<ordinal>` created before their pod; OrderedReady creates
-    ordinal i only when 0..i-1 are Running and Ready and scales down from the highest
-    ordinal, one pod at a time; Parallel does not wait; failed pods are replaced;
-    RollingUpdate (default) replaces pods whose controller-revision-hash differs from the
-    update revision from the highest ordinal down to spec.updateStrategy.rollingUpdate
-    .partition, one at a time, once the set is ready; ControllerRevisions record templates.
+  * pkg/controller/statefulset — controllers/statefulset.py (re-exported here).
   * pkg/controller/cronjob/{cronjob_controller.go, utils.go} — polled every 10 s;
     getRecentUnmetScheduleTimes since lastScheduleTime (or creation), >100 misses is an
     error; startingDeadlineSeconds drops too-late starts; concurrencyPolicy Allow / Forbid
@@ -25,10 +18,9 @@ import json
 import time
 
 from ..api import meta as m
-from ..api.helpers import is_pod_ready, is_pod_terminal
 from ..api.labels import selector_from_set
 from .base import Controller, split_key
-from .workloads import ReplicaSetController, _owned, template_hash
+from .workloads import ReplicaSetController
 
 REVISION_LABEL = "controller-revision-hash"
 POD_NAME_LABEL = "statefulset.kubernetes.io/pod-name"
@@ -43,162 +35,7 @@ class ReplicationManager(ReplicaSetController):
         return selector_from_set((rc.get("spec") or {}).get("selector") or {})
 
 
-# ============================================================================ StatefulSet
-def _running_ready(p) -> bool:
-    return (p.get("status") or {}).get("phase") == "Running" and is_pod_ready(p)
-
-
-class StatefulSetController(Controller):
-    name = "statefulset"
-
-    def setup(self):
-        f = self.mgr.factory
-        self.sts_inf = f.informer("statefulsets")
-        self.pvc_inf = f.informer("persistentvolumeclaims")
-        self.pod_inf = self.mgr.pods
-        self.sts_inf.add_handler(on_add=self.enqueue, on_update=lambda o, n: self.enqueue(n), on_delete=self.enqueue)
-        self.pod_inf.add_handler(on_add=self._pod, on_update=lambda o, n: self._pod(n), on_delete=self._pod)
-
-    def _pod(self, pod):
-        ref = m.controller_ref(pod)
-        if ref and ref.get("kind") == "StatefulSet":
-            self.enqueue(f"{m.namespace_of(pod)}/{ref['name']}")
-
-    @staticmethod
-    def ordinal(set_name: str, pod: dict) -> int:
-        n = m.name_of(pod)
-        pre, _, o = n.rpartition("-")
-        return int(o) if pre == set_name and o.isdigit() else -1
-
-    def new_pod(self, sts, ordinal, revision):
-        name = m.name_of(sts)
-        tpl = json.loads(json.dumps((sts.get("spec") or {}).get("template") or {}))
-        md = tpl.get("metadata") or {}
-        pname = f"{name}-{ordinal}"
-        labels = dict(md.get("labels") or {})
-        labels.update({POD_NAME_LABEL: pname, REVISION_LABEL: revision})
-        spec = tpl.get("spec") or {}
-        spec["hostname"] = pname
-        if (sts.get("spec") or {}).get("serviceName"):
-            spec["subdomain"] = sts["spec"]["serviceName"]
-        vols = [v for v in spec.get("volumes") or []]
-        for ct in (sts.get("spec") or {}).get("volumeClaimTemplates") or []:
-            cname = m.name_of(ct)
-            vols = [v for v in vols if v.get("name") != cname]
-            vols.append({"name": cname, "persistentVolumeClaim": {"claimName": f"{cname}-{pname}"}})
-        if vols:
-            spec["volumes"] = vols
-        return {"apiVersion": "v1", "kind": "Pod",
-                "metadata": {"name": pname, "namespace": m.namespace_of(sts), "labels": labels,
-                             "annotations": dict(md.get("annotations") or {}),
-                             "ownerReferences": [m.new_controller_ref(sts, "apps/v1", "StatefulSet")]},
-                "spec": spec}
-
-    async def _ensure_claims(self, sts, ordinal):
-        ns, name = m.namespace_of(sts), m.name_of(sts)
-        for ct in (sts.get("spec") or {}).get("volumeClaimTemplates") or []:
-            cname = f"{m.name_of(ct)}-{name}-{ordinal}"
-            if self.pvc_inf.get(f"{ns}/{cname}") is not None:
-                continue
-            labels = dict(((sts.get("spec") or {}).get("selector") or {}).get("matchLabels") or {})
-            pvc = {"apiVersion": "v1", "kind": "PersistentVolumeClaim",
-                   "metadata": {"name": cname, "namespace": ns, "labels": labels},
-                   "spec": json.loads(json.dumps(ct.get("spec") or {}))}
-            try:
-                await self.client.create(pvc, ns)
-            except m.StatusError as e:
-                if not m.is_already_exists(e):
-                    raise
-
-    async def _revision(self, sts) -> str:
-        """Record the template as the newest ControllerRevision (history.go) and return its hash:
-        a new template gets one past the highest revision, a template that comes back (a
-        rollback) has its old revision renumbered to the newest."""
-        tpl = (sts.get("spec") or {}).get("template") or {}
-        h = template_hash(tpl)
-        uid = m.uid_of(sts)
-        cache = self.__dict__.setdefault("_recorded", {})
-        if cache.get(uid) == h:
-            return h
-        ns, name = m.namespace_of(sts), m.name_of(sts)
-        revs = [r for r in (await self.client.list("controllerrevisions.apps", ns))[0] if (m.controller_ref(r) or {}).get("uid") == uid]
-        top = max((int(r.get("revision", 0)) for r in revs), default=0)
-        mine = next((r for r in revs if m.labels_of(r).get(REVISION_LABEL) == h), None)
-        if mine is None:
-            try:
-                await self.client.create({"apiVersion": "apps/v1", "kind": "ControllerRevision",
-                                          "metadata": {"name": f"{name}-{h}", "namespace": ns,
-                                                       "labels": dict(m.labels_of(sts), **{REVISION_LABEL: h}),
-                                                       "ownerReferences": [m.new_controller_ref(sts, "apps/v1", "StatefulSet")]},
-                                          "data": {"spec": {"template": tpl}}, "revision": top + 1}, ns)
-            except m.StatusError as e:
-                if not m.is_already_exists(e):
-                    raise
-        elif int(mine.get("revision", 0)) < top:
-            await self.client.update(dict(mine, apiVersion="apps/v1", kind="ControllerRevision", revision=top + 1))
-        cache[uid] = h
-        return h
-
-    async def sync(self, key):
-        sts = self.sts_inf.get(key)
-        if sts is None or (sts.get("metadata") or {}).get("deletionTimestamp"):
-            return
-        ns, name = split_key(key)
-        spec = sts.get("spec") or {}
-        replicas = int(spec.get("replicas", 1))
-        parallel = spec.get("podManagementPolicy") == "Parallel"
-        revision = await self._revision(sts)
-        pods = {}
-        for p in _owned(self.pod_inf.list(), sts):
-            o = self.ordinal(name, p)
-            if o >= 0:
-                pods[o] = p
-        # 1. replace failed pods, create missing ones (in order unless Parallel)
-        for o in range(replicas):
-            p = pods.get(o)
-            if p is not None and (p.get("status") or {}).get("phase") == "Failed" and \
-                    not (p.get("metadata") or {}).get("deletionTimestamp"):
-                await self.client.delete("pods", m.name_of(p), ns, grace=0)
-                return
-            if p is None:
-                await self._ensure_claims(sts, o)
-                await self.client.create(self.new_pod(sts, o, revision), ns)
-                if not parallel:
-                    return
-                continue
-            if not parallel and not _running_ready(p):
-                break  # OrderedReady: wait for this ordinal before touching the next one
-        # 2. scale down from the highest ordinal, one at a time
-        extra = sorted((o for o in pods if o >= replicas), reverse=True)
-        if extra:
-            if not parallel and not all(_running_ready(pods[o]) for o in pods if o < replicas):
-                await self._status(sts, pods, revision)
-                return
-            for o in (extra if parallel else extra[:1]):
-                if not (pods[o].get("metadata") or {}).get("deletionTimestamp"):
-                    await self.client.delete("pods", m.name_of(pods[o]), ns)
-        # 3. rolling update, highest ordinal first, down to the partition
-        us = spec.get("updateStrategy") or {}
-        if us.get("type", "RollingUpdate") == "RollingUpdate" and not extra:
-            partition = int(((us.get("rollingUpdate") or {}).get("partition")) or 0)
-            live = [pods[o] for o in range(replicas) if o in pods]
-            if len(live) == replicas and all(_running_ready(p) for p in live):
-                for o in range(replicas - 1, partition - 1, -1):
-                    if m.labels_of(pods[o]).get(REVISION_LABEL) != revision:
-                        await self.client.delete("pods", m.name_of(pods[o]), ns)
-                        break
-        await self._status(sts, pods, revision)
-
-    async def _status(self, sts, pods, revision):
-        ns, name = m.namespace_of(sts), m.name_of(sts)
-        live = [p for p in pods.values() if not is_pod_terminal(p)]
-        updated = sum(1 for p in live if m.labels_of(p).get(REVISION_LABEL) == revision)
-        st = {"replicas": len(live), "readyReplicas": sum(1 for p in live if _running_ready(p)),
-              "currentReplicas": len(live), "updatedReplicas": updated, "updateRevision": f"{name}-{revision}",
-              "currentRevision": f"{name}-{revision}" if updated == len(live) else (sts.get("status") or {}).get("currentRevision", ""),
-              "observedGeneration": (sts.get("metadata") or {}).get("generation", 1)}
-        if {k: (sts.get("status") or {}).get(k) for k in st} != st:
-            await self.client.patch("statefulsets", name, {"status": st}, ns, sub="status")
+from .statefulset import StatefulSetController  # noqa: E402,F401  (controllers/statefulset.py)
 
 
 # ============================================================================== cron

@@ -76,7 +76,10 @@ async def _owned_revisions(c, obj) -> list[dict]:
 
 
 def _revision_template(r) -> dict:
-    return json.loads(json.dumps(((r.get("data") or {}).get("spec") or {}).get("template") or {}))
+    """The template a revision restores (its data is a `$patch: replace` of spec.template)."""
+    tpl = json.loads(json.dumps(((r.get("data") or {}).get("spec") or {}).get("template") or {}))
+    tpl.pop("$patch", None)
+    return tpl
 
 
 async def _rollout_history_based(c, a, sub, ri, name, ns, res):

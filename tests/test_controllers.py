@@ -359,7 +359,7 @@ def test_statefulset_rollout_history_and_undo(capsys):
             assert await asyncio.to_thread(kubectl, kc + ["rollout", "undo", "statefulset/db"]) == 0
             assert await until(lambda: at(None), 60) == h1
             revs, _ = await c.list("controllerrevisions.apps", "default")
-            mine = sorted((r["revision"], r["metadata"]["labels"]["controller-revision-hash"]) for r in revs
+            mine = sorted((r["revision"], r["metadata"]["name"]) for r in revs          # pods carry the revision's name
                           if (m.controller_ref(r) or {}).get("name") == "db")
             assert [r for r, _ in mine] == [2, 3] and mine[-1][1] in h1
             assert await asyncio.to_thread(kubectl, kc + ["rollout", "status", "statefulset/db"]) == 0
