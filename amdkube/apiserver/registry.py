@@ -341,6 +341,15 @@ class ResourceStore:
                     else:
                         na.pop(k, None)
                 md["annotations"] = na or None
+        if self.ri.plural == "daemonsets" and subresource != "status":
+            # daemonSetStrategy.PrepareForUpdate: a changed template bumps spec.templateGeneration
+            # (the extensions/v1beta1 field; apps/v1 objects do not carry it)
+            cs, ns_ = cur.get("spec") or {}, new.get("spec") or {}
+            if "templateGeneration" in cs:
+                if cs.get("template") != ns_.get("template"):
+                    ns_["templateGeneration"] = int(cs["templateGeneration"] or 0) + 1
+                else:
+                    ns_["templateGeneration"] = cs["templateGeneration"]
         if self.generation:
             md["generation"] = cmd.get("generation", 1) + (1 if new.get("spec") != cur.get("spec") else 0)
         if self.ri.plural == "services" and subresource != "status":
