@@ -197,3 +197,19 @@ for _gv in ("apps/v1beta2", "extensions/v1beta1"):
 register_hooks("ReplicaSet", "apps/v1", defaulter=default_replicaset)
 register_hooks("Deployment", "apps/v1", defaulter=default_deployment)
 register_hooks("Job", "batch/v1", defaulter=default_job)
+
+
+def default_pod_security_policy(psp: dict):
+    """SetDefaults_PodSecurityPolicySpec (extensions/v1beta1/defaults.go): privilege escalation
+    is allowed unless the policy says otherwise."""
+    spec = psp.setdefault("spec", {})
+    if spec.get("allowPrivilegeEscalation") is None:
+        spec["allowPrivilegeEscalation"] = True
+    return psp
+
+
+for _gv in ("extensions/v1beta1", "policy/v1beta1"):
+    try:
+        register_hooks("PodSecurityPolicy", _gv, defaulter=default_pod_security_policy)
+    except KeyError:
+        pass

@@ -547,190 +547,71 @@ class SecurityContextDeny(Plugin):
 PSP_ANNOTATION = "kubernetes.io/psp"
 
 
-class _PSPProvider:
-    """pkg/security/podsecuritypolicy/provider.go: default the pod's security context from the
-    policy (only where unset) and validate the result against it."""
-
-    def __init__(self, psp):
-        self.psp, self.spec, self.name = psp, psp.get("spec") or {}, m.name_of(psp)
-
-    def _first_id(self, strat):
-        rs = strat.get("ranges") or []
-        return rs[0].get("min") if strat.get("rule") == "MustRunAs" and rs else None
-
-    @staticmethod
-    def _in_ranges(v, ranges):
-        return any(r.get("min", 0) <= v <= r.get("max", 0) for r in ranges or [])
-
-    def default(self, pod):
-        spec = pod.setdefault("spec", {})
-        psc = spec.setdefault("securityContext", {})
-        fsg = self._first_id(self.spec.get("fsGroup") or {})
-        if fsg is not None and psc.get("fsGroup") is None:
-            psc["fsGroup"] = fsg
-        sg = self._first_id(self.spec.get("supplementalGroups") or {})
-        if sg is not None and not psc.get("supplementalGroups"):
-            psc["supplementalGroups"] = [sg]
-        se = self.spec.get("seLinux") or {}
-        if se.get("rule") == "MustRunAs" and se.get("seLinuxOptions") and psc.get("seLinuxOptions") is None:
-            psc["seLinuxOptions"] = dict(se["seLinuxOptions"])
-        if not psc:
-            spec.pop("securityContext")
-        uid = self._first_id(self.spec.get("runAsUser") or {})
-        for c in _all_containers(pod):
-            sc = c.setdefault("securityContext", {})
-            if uid is not None and sc.get("runAsUser") is None and (pod["spec"].get("securityContext") or {}).get("runAsUser") is None:
-                sc["runAsUser"] = uid
-            if (self.spec.get("runAsUser") or {}).get("rule") == "MustRunAsNonRoot" and sc.get("runAsNonRoot") is None \
-                    and sc.get("runAsUser") is None:
-                sc["runAsNonRoot"] = True
-            add = self.spec.get("defaultAddCapabilities") or []
-            drop = self.spec.get("requiredDropCapabilities") or []
-            if add or drop:
-                caps = sc.setdefault("capabilities", {})
-                cur_add, cur_drop = caps.get("add") or [], caps.get("drop") or []
-                caps["add"] = cur_add + [x for x in add if x not in cur_add and x not in cur_drop]
-                caps["drop"] = cur_drop + [x for x in drop if x not in cur_drop]
-                if not caps["add"]:
-                    caps.pop("add")
-                if not caps["drop"]:
-                    caps.pop("drop")
-            if self.spec.get("readOnlyRootFilesystem") and sc.get("readOnlyRootFilesystem") is None:
-                sc["readOnlyRootFilesystem"] = True
-            if sc.get("allowPrivilegeEscalation") is None and self.spec.get("defaultAllowPrivilegeEscalation") is not None:
-                sc["allowPrivilegeEscalation"] = bool(self.spec["defaultAllowPrivilegeEscalation"])
-            if not sc:
-                c.pop("securityContext")
-        return pod
-
-    def validate(self, pod) -> list[str]:
-        errs, s = [], self.spec
-        spec = pod.get("spec") or {}
-        psc = spec.get("securityContext") or {}
-        for k, name in (("hostNetwork", "hostNetwork"), ("hostPID", "hostPID"), ("hostIPC", "hostIPC")):
-            if spec.get(k) and not s.get(name):
-                errs.append(f"spec.securityContext.{k}: Invalid value: true: {k} is not allowed to be used")
-        for g in ("fsGroup", "supplementalGroups"):
-            strat = s.get(g) or {}
-            vals = psc.get(g)
-            vals = [vals] if isinstance(vals, int) else (vals or [])
-            if strat.get("rule") == "MustRunAs":
-                if not vals:
-                    errs.append(f"spec.securityContext.{g}: Invalid value: must be set")
-                for v in vals:
-                    if not self._in_ranges(v, strat.get("ranges")):
-                        errs.append(f"spec.securityContext.{g}: Invalid value: {v}: not in the policy's ranges")
-        se = s.get("seLinux") or {}
-        if se.get("rule") == "MustRunAs" and se.get("seLinuxOptions"):
-            for who in [psc] + [c.get("securityContext") or {} for c in _all_containers(pod)]:
-                if who.get("seLinuxOptions") not in (None, se["seLinuxOptions"]):
-                    errs.append("seLinuxOptions: Invalid value: does not match required seLinuxOptions")
-        allowed_vols = set(s.get("volumes") or [])
-        for v in spec.get("volumes") or []:
-            vt = next((k for k in v if k != "name"), "")
-            if "*" not in allowed_vols and vt not in allowed_vols:
-                errs.append(f"spec.volumes[{v.get('name')}]: Invalid value: {vt!r}: {vt} volumes are not allowed to be used")
-            if vt == "hostPath" and s.get("allowedHostPaths"):
-                p = (v.get("hostPath") or {}).get("path", "")
-                if not any(p.startswith(h.get("pathPrefix", "\0")) for h in s["allowedHostPaths"]):
-                    errs.append(f"spec.volumes[{v.get('name')}].hostPath.pathPrefix: Invalid value: {p!r}: is not allowed to be used")
-        ru = s.get("runAsUser") or {}
-        caps_allowed = set(s.get("allowedCapabilities") or []) | set(s.get("defaultAddCapabilities") or [])
-        for c in _all_containers(pod):
-            sc = c.get("securityContext") or {}
-            path = f"containers[{c.get('name')}].securityContext"
-            if sc.get("privileged") and not s.get("privileged"):
-                errs.append(f"{path}.privileged: Invalid value: true: Privileged containers are not allowed")
-            uid = sc.get("runAsUser", psc.get("runAsUser"))
-            if ru.get("rule") == "MustRunAs" and (uid is None or not self._in_ranges(uid, ru.get("ranges"))):
-                errs.append(f"{path}.runAsUser: Invalid value: {uid}: must be in the ranges: {ru.get('ranges')}")
-            if ru.get("rule") == "MustRunAsNonRoot":
-                nonroot = sc.get("runAsNonRoot", psc.get("runAsNonRoot"))
-                if uid == 0 or (uid is None and not nonroot):
-                    errs.append(f"{path}.runAsNonRoot: Invalid value: false: must be true")
-            caps = sc.get("capabilities") or {}
-            for cap in caps.get("add") or []:
-                if "*" not in caps_allowed and cap not in caps_allowed:
-                    errs.append(f"{path}.capabilities.add: Invalid value: {cap!r}: capability may not be added")
-            for cap in s.get("requiredDropCapabilities") or []:
-                if cap not in (caps.get("drop") or []):
-                    errs.append(f"{path}.capabilities.drop: Invalid value: {caps.get('drop')}: {cap} is required to be dropped but was not found")
-            if s.get("readOnlyRootFilesystem") and not sc.get("readOnlyRootFilesystem"):
-                errs.append(f"{path}.readOnlyRootFilesystem: Invalid value: false: ReadOnlyRootFilesystem must be set to true")
-            if s.get("allowPrivilegeEscalation") is False and sc.get("allowPrivilegeEscalation") is not False:
-                errs.append(f"{path}.allowPrivilegeEscalation: Invalid value: Allowing privilege escalation for containers is not allowed")
-            for p in c.get("ports") or []:
-                hp = p.get("hostPort") or 0
-                if hp and not any(r.get("min", 0) <= hp <= r.get("max", 0) for r in s.get("hostPorts") or []):
-                    errs.append(f"{path}.ports: Invalid value: {hp}: Host port {hp} is not allowed to be used")
-        return errs
-
-
 class PodSecurityPolicy(Plugin):
-    """security/podsecuritypolicy/admission.go: the policies the requesting user or the pod's
-    service account may `use` (extensions podsecuritypolicies, in the pod's namespace), sorted
-    by name; on create the first policy under which the (defaulted) pod validates is applied
-    and recorded as kubernetes.io/psp; on update the pod must validate unchanged; no usable
-    policy → 403 listing every policy's errors."""
+    """plugin/pkg/admission/security/podsecuritypolicy/admission.go over security/psp.py: every
+    policy (name order) is tried on a copy of the pod; one that validates without changing the
+    pod wins, else (create only) the first that validates with changes; the requesting user or
+    the pod's service account must be authorized to `use` it; the winner is recorded as
+    kubernetes.io/psp. On update the pod must be admitted unchanged. Forbidden otherwise,
+    listing the errors of the policies the requester may use."""
     name = "PodSecurityPolicy"
 
     def __init__(self, fail_on_no_policies=True):
         self.fail_on_no_policies = fail_on_no_policies
 
-    def _providers(self, a, ctx, pod):
-        policies = sorted(ctx.list_objects("podsecuritypolicies", "", "extensions"), key=m.name_of)
+    def _authorized(self, a, ctx, pod):
         sa = (pod.get("spec") or {}).get("serviceAccountName")
         sa_user = {"name": f"system:serviceaccount:{a.namespace}:{sa}",
                    "groups": ["system:serviceaccounts", f"system:serviceaccounts:{a.namespace}"]} if sa else None
-        usable = [p for p in policies
-                  if (sa_user is not None and ctx.authorize(sa_user, "use", "extensions", "podsecuritypolicies", "", a.namespace, m.name_of(p)))
-                  or ctx.authorize(a.user or {}, "use", "extensions", "podsecuritypolicies", "", a.namespace, m.name_of(p))]
-        return policies, [_PSPProvider(p) for p in usable]
 
-    def admit(self, a, ctx):
-        if not _is_pod(a) or a.obj is None or a.operation != CREATE:
-            return
-        policies, providers = self._providers(a, ctx, a.obj)
-        if not policies and not self.fail_on_no_policies:
-            return
-        if not providers:
-            raise m.forbidden("unable to validate against any pod security policy: no providers available to validate pod request")
-        errors, first_mutated = {}, None
-        for pr in providers:    # computeSecurityContext: default, validate, prefer a non-mutating policy
-            cand = pr.default(copy.deepcopy(a.obj))
-            errs = pr.validate(cand)
-            if errs:
-                errors[pr.name] = errs
-                continue
-            if cand == a.obj:
-                first_mutated = (pr.name, cand)
-                break
-            if first_mutated is None:
-                first_mutated = (pr.name, cand)
-        if first_mutated is None:
-            raise m.forbidden(f"unable to validate against any pod security policy: {errors}")
-        name, cand = first_mutated
-        a.obj.clear()
-        a.obj.update(cand)
-        a.obj.setdefault("metadata", {}).setdefault("annotations", {})[PSP_ANNOTATION] = name
+        def ok(name):
+            return (sa_user is not None and ctx.authorize(sa_user, "use", "extensions", "podsecuritypolicies", "",
+                                                          a.namespace, name)) or \
+                ctx.authorize(a.user or {}, "use", "extensions", "podsecuritypolicies", "", a.namespace, name)
+        return ok
 
-    def validate(self, a, ctx):
+    def _compute(self, a, ctx, mutation_allowed):
+        from ..security import psp
+        policies = ctx.list_objects("podsecuritypolicies", "", "extensions")
+        try:
+            return psp.compute_security_context(policies, a.obj, self._authorized(a, ctx, a.obj), mutation_allowed,
+                                                self.fail_on_no_policies)
+        except PermissionError as e:
+            raise m.forbidden(f"unable to validate against any pod security policy: {e}") from None
+
+    @staticmethod
+    def _ignore(a) -> bool:
         if not _is_pod(a) or a.obj is None:
-            return
+            return True
         if a.operation == UPDATE and a.old is not None:
             strip = lambda o: {k: v for k, v in o.items() if k != "metadata"}   # noqa: E731
             if strip(a.obj) == strip(a.old):
-                return      # only metadata (GC fields, labels) changed
-        policies, providers = self._providers(a, ctx, a.obj)
-        if not policies and not self.fail_on_no_policies:
+                return True      # only metadata (GC fields, labels) changed: IsOnlyMutatingGCFields
+        return False
+
+    def admit(self, a, ctx):
+        if self._ignore(a) or a.operation != CREATE:
             return
-        errors = {}
-        for pr in providers:
-            errs = pr.validate(a.obj)
-            if not errs:
-                return
-            errors[pr.name] = errs
-        raise m.forbidden(f"unable to validate against any pod security policy: {errors}")
+        allowed, name, errs = self._compute(a, ctx, True)
+        if allowed is None:
+            raise m.forbidden(f"unable to validate against any pod security policy: {[str(e) for e in errs]}")
+        if allowed is not a.obj:
+            a.obj.clear()
+            a.obj.update(allowed)
+        if name:
+            md = a.obj.setdefault("metadata", {})
+            if md.get("annotations") is None:
+                md["annotations"] = {}
+            md["annotations"][PSP_ANNOTATION] = name
+
+    def validate(self, a, ctx):
+        if self._ignore(a):
+            return
+        from ..security.psp import _semantic_equal
+        allowed, _, errs = self._compute(a, ctx, False)
+        if allowed is not None and _semantic_equal(allowed, a.obj):
+            return
+        raise m.forbidden(f"unable to validate against any pod security policy: {[str(e) for e in errs]}")
 
 
 # ---------------------------------------------------------------------- Initializers
