@@ -291,3 +291,39 @@ def test_get_max_vols(c, monkeypatch):
     from amdkube.scheduler.volumes import max_pd_limit
     monkeypatch.setenv("KUBE_MAX_PD_VOLS", c["rawMaxVols"])
     assert max_pd_limit("awsElasticBlockStore") == c["expected"]
+
+
+# ------------------------------------------------------------------ utils_test.go (ports)
+def _decode(s):
+    """decode(): "PROTO/IP/PORT" -> amdkube's (ip, proto, port) host-port tuple."""
+    proto, ip, port = s.split("/")
+    return ip, proto, int(port)
+
+
+@pytest.mark.parametrize("s,want", [("UDP/127.0.0.1/80", ("127.0.0.1", "UDP", 80)),
+                                    ("TCP/127.0.0.1/80", ("127.0.0.1", "TCP", 80)),
+                                    ("TCP/0.0.0.0/80", ("0.0.0.0", "TCP", 80))])
+def test_decode_host_port(s, want):
+    from amdkube.api.helpers import pod_host_ports
+    proto, ip, port = s.split("/")
+    p = {"spec": {"containers": [{"ports": [{"protocol": proto, "hostIP": ip, "hostPort": int(port), "containerPort": 1}]}]}}
+    assert [tuple(x) for x in pod_host_ports(p)] == [want] == [_decode(s)]
+
+
+@pytest.mark.parametrize("special,others,want", [
+    ("TCP/0.0.0.0/80", ["TCP/127.0.0.2/8080", "TCP/127.0.0.1/80", "UDP/127.0.0.2/8080"], True),
+    ("TCP/0.0.0.0/80", ["TCP/127.0.0.2/8080", "UDP/127.0.0.1/80", "UDP/127.0.0.2/8080"], False),
+    ("TCP/0.0.0.0/80", ["TCP/127.0.0.2/8080", "TCP/127.0.0.1/8090", "UDP/127.0.0.2/8080"], False),
+    ("TCP/0.0.0.0/80", ["UDP/127.0.0.2/8080", "UDP/127.0.0.1/8090", "TCP/127.0.0.2/8080"], False),
+], ids=["test-1", "test-2", "test-3", "test-4"])
+def test_special_port_conflict_check(special, others, want):
+    assert P.ports_conflict({_decode(o) for o in others}, {_decode(special)}) == want
+
+
+@pytest.mark.parametrize("existing,wanted,want", [
+    ("UDP/127.0.0.1/8080", "UDP/127.0.0.1/8080", True), ("UDP/127.0.0.2/8080", "UDP/127.0.0.1/8080", False),
+    ("TCP/127.0.0.1/8080", "UDP/127.0.0.1/8080", False), ("TCP/0.0.0.0/8080", "TCP/127.0.0.1/8080", True),
+    ("TCP/127.0.0.1/8080", "TCP/0.0.0.0/8080", True),
+], ids=["test1", "test2", "test3", "test4", "test5"])
+def test_ports_conflict(existing, wanted, want):
+    assert P.ports_conflict({_decode(existing)}, {_decode(wanted)}) == want
