@@ -26,6 +26,7 @@ import re
 
 from .labels import SelectorError, is_dns1123_label, is_dns1123_subdomain, selector_from_label_selector
 from .scheme import register_hooks
+from .field import go_slice, go_value
 
 _IANA_SVC = re.compile(r"^[a-z0-9]([a-z0-9-]*[a-z0-9])?$")
 
@@ -50,16 +51,16 @@ def _port(p, path, allow_name=True):
         if p.isdigit():
             return _port(int(p), path)
         if len(p) > 15 or not _IANA_SVC.match(p) or "--" in p or not re.search("[a-z]", p):
-            return [f"{path}: Invalid value: {p!r}: must be a valid IANA service name"]
+            return [f"{path}: Invalid value: {go_value(p)}: must be a valid IANA service name"]
         return []
-    return [f"{path}: Invalid value: {p!r}"]
+    return [f"{path}: Invalid value: {go_value(p)}"]
 
 
 def _cidr(s, path):
     try:
         return ipaddress.ip_network(s, strict=False), []
     except ValueError:
-        return None, [f"{path}: Invalid value: {s!r}: must be a valid CIDR"]
+        return None, [f"{path}: Invalid value: {go_value(s)}: must be a valid CIDR"]
 
 
 # ----------------------------------------------------------------- NetworkPolicy
@@ -84,7 +85,7 @@ def _peers(peers, path):
                 errs += e
                 if net is not None and sub is not None and (sub.version != net.version or not sub.subnet_of(net)
                                                             or sub.prefixlen <= net.prefixlen):
-                    errs.append(f"{pp}.ipBlock.except[{j}]: Invalid value: {ex!r}: must be a strict subset of `cidr`")
+                    errs.append(f"{pp}.ipBlock.except[{j}]: Invalid value: {go_value(ex)}: must be a strict subset of `cidr`")
     return errs
 
 
@@ -92,7 +93,7 @@ def _np_ports(ports, path):
     errs = []
     for i, p in enumerate(ports or []):
         if p.get("protocol", "TCP") not in ("TCP", "UDP"):
-            errs.append(f"{path}[{i}].protocol: Unsupported value: {p.get('protocol')!r}: supported values: \"TCP\", \"UDP\"")
+            errs.append(f"{path}[{i}].protocol: Unsupported value: {go_value(p.get('protocol'))}: supported values: \"TCP\", \"UDP\"")
         if p.get("port") is not None:
             errs += _port(p["port"], f"{path}[{i}].port")
     return errs
@@ -109,9 +110,9 @@ def validate_network_policy(np, old=None):
     pts = spec.get("policyTypes") or []
     for i, t in enumerate(pts):
         if t not in ("Ingress", "Egress"):
-            errs.append(f"spec.policyTypes[{i}]: Unsupported value: {t!r}: supported values: \"Ingress\", \"Egress\"")
+            errs.append(f"spec.policyTypes[{i}]: Unsupported value: {go_value(t)}: supported values: \"Ingress\", \"Egress\"")
     if len(pts) > 2 or len(set(pts)) != len(pts):
-        errs.append(f"spec.policyTypes: Invalid value: {pts!r}: may not contain duplicates or more than 2 entries")
+        errs.append(f"spec.policyTypes: Invalid value: {go_slice('networking.PolicyType', pts)}: may not contain duplicates or more than 2 entries")
     return errs
 
 
@@ -133,7 +134,7 @@ def _backend(b, path):
     if not sn:
         errs.append(f"{path}.serviceName: Required value")
     elif not re.match(r"^[a-z]([-a-z0-9]*[a-z0-9])?$", sn) or len(sn) > 63:
-        errs.append(f"{path}.serviceName: Invalid value: {sn!r}: a DNS-1035 label")
+        errs.append(f"{path}.serviceName: Invalid value: {go_value(sn)}: a DNS-1035 label")
     if b.get("servicePort") in (None, "", 0):
         errs.append(f"{path}.servicePort: Required value")
     else:
@@ -153,27 +154,27 @@ def validate_ingress(ing, old=None):
         if host:
             try:
                 ipaddress.ip_address(host)
-                errs.append(f"spec.rules[{i}].host: Invalid value: {host!r}: must be a DNS name, not an IP address")
+                errs.append(f"spec.rules[{i}].host: Invalid value: {go_value(host)}: must be a DNS name, not an IP address")
             except ValueError:
                 h = host[2:] if host.startswith("*.") else host
                 for e in is_dns1123_subdomain(h):
-                    errs.append(f"spec.rules[{i}].host: Invalid value: {host!r}: {e}")
+                    errs.append(f"spec.rules[{i}].host: Invalid value: {go_value(host)}: {e}")
         for j, p in enumerate(((r.get("http") or {}).get("paths")) or []):
             path = p.get("path", "")
             if path:
                 if not path.startswith("/"):
-                    errs.append(f"spec.rules[{i}].http.paths[{j}].path: Invalid value: {path!r}: must be an absolute path")
+                    errs.append(f"spec.rules[{i}].http.paths[{j}].path: Invalid value: {go_value(path)}: must be an absolute path")
                 try:
                     re.compile(path)
                 except re.error:
-                    errs.append(f"spec.rules[{i}].http.paths[{j}].path: Invalid value: {path!r}: must be a valid regex")
+                    errs.append(f"spec.rules[{i}].http.paths[{j}].path: Invalid value: {go_value(path)}: must be a valid regex")
             errs += _backend(p.get("backend") or {}, f"spec.rules[{i}].http.paths[{j}].backend")
         if r.get("http") is not None and not (r["http"].get("paths")):
             errs.append(f"spec.rules[{i}].http.paths: Required value")
     for i, t in enumerate(spec.get("tls") or []):
         for j, h in enumerate(t.get("hosts") or []):
             for e in is_dns1123_subdomain(h[2:] if h.startswith("*.") else h):
-                errs.append(f"spec.tls[{i}].hosts[{j}]: Invalid value: {h!r}: {e}")
+                errs.append(f"spec.tls[{i}].hosts[{j}]: Invalid value: {go_value(h)}: {e}")
     return errs
 
 
@@ -200,28 +201,28 @@ def validate_psp(psp, old=None):
     spec = psp.get("spec") or {}
     ru = spec.get("runAsUser") or {}
     if ru.get("rule") not in ("MustRunAs", "MustRunAsNonRoot", "RunAsAny"):
-        errs.append(f"spec.runAsUser.rule: Unsupported value: {ru.get('rule')!r}")
+        errs.append(f"spec.runAsUser.rule: Unsupported value: {go_value(ru.get('rule'))}")
     if ru.get("rule") == "MustRunAs" and not ru.get("ranges"):
         errs.append("spec.runAsUser.ranges: Invalid value: must provide at least one range")
     errs += _id_ranges(ru.get("ranges"), "spec.runAsUser.ranges")
     se = spec.get("seLinux") or {}
     if se.get("rule") not in ("MustRunAs", "RunAsAny"):
-        errs.append(f"spec.seLinux.rule: Unsupported value: {se.get('rule')!r}")
+        errs.append(f"spec.seLinux.rule: Unsupported value: {go_value(se.get('rule'))}")
     for f in ("supplementalGroups", "fsGroup"):
         g = spec.get(f) or {}
         if g.get("rule") not in ("MustRunAs", "RunAsAny"):
-            errs.append(f"spec.{f}.rule: Unsupported value: {g.get('rule')!r}")
+            errs.append(f"spec.{f}.rule: Unsupported value: {go_value(g.get('rule'))}")
         errs += _id_ranges(g.get("ranges"), f"spec.{f}.ranges")
     for i, v in enumerate(spec.get("volumes") or []):
         if v not in FS_TYPES:
-            errs.append(f"spec.volumes[{i}]: Unsupported value: {v!r}")
+            errs.append(f"spec.volumes[{i}]: Unsupported value: {go_value(v)}")
     for i, hp in enumerate(spec.get("hostPorts") or []):
         if hp.get("min", 0) > hp.get("max", 0) or not (0 <= hp.get("min", 0) <= 65535) or not (0 <= hp.get("max", 0) <= 65535):
             errs.append(f"spec.hostPorts[{i}]: Invalid value: min/max must be 0-65535 with min ≤ max")
     both = set(spec.get("allowedCapabilities") or []) & set(spec.get("requiredDropCapabilities") or [])
     both |= set(spec.get("defaultAddCapabilities") or []) & set(spec.get("requiredDropCapabilities") or [])
     if both:
-        errs.append(f"spec.requiredDropCapabilities: Invalid value: {sorted(both)!r}: capability is both added and dropped")
+        errs.append(f"spec.requiredDropCapabilities: Invalid value: {go_slice('core.Capability', sorted(both))}: capability is both added and dropped")
     for i, hp in enumerate(spec.get("allowedHostPaths") or []):
         if not hp.get("pathPrefix"):
             errs.append(f"spec.allowedHostPaths[{i}].pathPrefix: Required value")
@@ -241,9 +242,9 @@ def validate_pod_preset(pp, old=None):
     names = set()
     for i, v in enumerate(spec.get("volumes") or []):
         n = v.get("name", "")
-        errs += [f"spec.volumes[{i}].name: Invalid value: {n!r}: {e}" for e in is_dns1123_label(n)]
+        errs += [f"spec.volumes[{i}].name: Invalid value: {go_value(n)}: {e}" for e in is_dns1123_label(n)]
         if n in names:
-            errs.append(f"spec.volumes[{i}].name: Duplicate value: {n!r}")
+            errs.append(f"spec.volumes[{i}].name: Duplicate value: {go_value(n)}")
         names.add(n)
     for i, vm in enumerate(spec.get("volumeMounts") or []):
         if not vm.get("name") or not vm.get("mountPath"):
@@ -260,10 +261,10 @@ def validate_initializer_configuration(ic, old=None):
     for i, ini in enumerate(ic.get("initializers") or []):
         n = ini.get("name", "")
         if len(n.split(".")) < 3:
-            errs.append(f"initializers[{i}].name: Invalid value: {n!r}: should be a domain with at least three segments separated by dots")
-        errs += [f"initializers[{i}].name: Invalid value: {n!r}: {e}" for e in is_dns1123_subdomain(n)]
+            errs.append(f"initializers[{i}].name: Invalid value: {go_value(n)}: should be a domain with at least three segments separated by dots")
+        errs += [f"initializers[{i}].name: Invalid value: {go_value(n)}: {e}" for e in is_dns1123_subdomain(n)]
         if n in seen:
-            errs.append(f"initializers[{i}].name: Duplicate value: {n!r}")
+            errs.append(f"initializers[{i}].name: Duplicate value: {go_value(n)}")
         seen.add(n)
         for j, r in enumerate(ini.get("rules") or []):
             for f in ("apiGroups", "apiVersions", "resources"):
@@ -287,13 +288,13 @@ def validate_apiservice(a, old=None):
     name, group, version = (a.get("metadata") or {}).get("name", ""), spec.get("group", ""), spec.get("version", "")
     want = f"{version}.{group}"
     if name != want:
-        errs.append(f"metadata.name: Invalid value: {name!r}: must be `spec.version+\".\"+spec.group`: {want!r}")
+        errs.append(f"metadata.name: Invalid value: {go_value(name)}: must be `spec.version+\".\"+spec.group`: {want!r}")
     if not version:
         errs.append("spec.version: Required value")
     elif is_dns1123_label(version):
-        errs.append(f"spec.version: Invalid value: {version!r}: a DNS-1123 label")
+        errs.append(f"spec.version: Invalid value: {go_value(version)}: a DNS-1123 label")
     if group and is_dns1123_subdomain(group):
-        errs.append(f"spec.group: Invalid value: {group!r}: a DNS-1123 subdomain")
+        errs.append(f"spec.group: Invalid value: {go_value(group)}: a DNS-1123 subdomain")
     gp, vp = spec.get("groupPriorityMinimum", 0), spec.get("versionPriority", 0)
     if not (0 < gp <= 20000):
         errs.append(f"spec.groupPriorityMinimum: Invalid value: {gp}: must be positive and less than 20000")

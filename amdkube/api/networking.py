@@ -3,6 +3,7 @@ ValidateService, pkg/apis/core/v1/defaults.go SetDefaults_Service)."""
 from __future__ import annotations
 
 from .labels import is_dns1123_label
+from .field import go_value
 
 SERVICE_TYPES = ("ClusterIP", "NodePort", "LoadBalancer", "ExternalName")
 
@@ -13,7 +14,7 @@ def validate_service(svc: dict, old=None) -> list[str]:
     spec = svc.get("spec") or {}
     t = spec.get("type", "ClusterIP")
     if t not in SERVICE_TYPES:
-        errs.append(f"spec.type: Unsupported value: {t!r}: supported values: {', '.join(SERVICE_TYPES)}")
+        errs.append(f"spec.type: Unsupported value: {go_value(t)}: supported values: {', '.join(SERVICE_TYPES)}")
     if t == "ExternalName":
         if not spec.get("externalName"):
             errs.append("spec.externalName: Required value")
@@ -28,25 +29,25 @@ def validate_service(svc: dict, old=None) -> list[str]:
             errs.append(f"{pref}.name: Required value")
         if p.get("name"):
             if p["name"] in seen_names:
-                errs.append(f"{pref}.name: Duplicate value: {p['name']!r}")
+                errs.append(f"{pref}.name: Duplicate value: {go_value(p['name'])}")
             seen_names.add(p["name"])
         port = p.get("port")
         if not isinstance(port, int) or not 0 < port < 65536:
-            errs.append(f"{pref}.port: Invalid value: {port!r}: must be between 1 and 65535, inclusive")
+            errs.append(f"{pref}.port: Invalid value: {go_value(port)}: must be between 1 and 65535, inclusive")
         proto = p.get("protocol", "TCP")
         if proto not in ("TCP", "UDP"):
-            errs.append(f"{pref}.protocol: Unsupported value: {proto!r}: supported values: TCP, UDP")
+            errs.append(f"{pref}.protocol: Unsupported value: {go_value(proto)}: supported values: TCP, UDP")
         if (proto, port) in seen_ports:
             errs.append(f"{pref}: Duplicate value: {proto}/{port}")
         seen_ports.add((proto, port))
         tp = p.get("targetPort")
         if tp is not None and not ((isinstance(tp, int) and 0 < tp < 65536) or (isinstance(tp, str) and tp)):
-            errs.append(f"{pref}.targetPort: Invalid value: {tp!r}")
+            errs.append(f"{pref}.targetPort: Invalid value: {go_value(tp)}")
         if p.get("nodePort") and t == "ClusterIP":
             errs.append(f"{pref}.nodePort: Forbidden: may not be used when `type` is 'ClusterIP'")
     aff = spec.get("sessionAffinity", "None")
     if aff not in ("None", "ClientIP"):
-        errs.append(f"spec.sessionAffinity: Unsupported value: {aff!r}")
+        errs.append(f"spec.sessionAffinity: Unsupported value: {go_value(aff)}")
     sel = spec.get("selector") or {}
     if not isinstance(sel, dict):
         errs.append("spec.selector: Invalid value: must be a map")
@@ -54,17 +55,17 @@ def validate_service(svc: dict, old=None) -> list[str]:
     etp = spec.get("externalTrafficPolicy")
     if etp:
         if t not in ("NodePort", "LoadBalancer"):
-            errs.append(f"spec.externalTrafficPolicy: Invalid value: {etp!r}: ExternalTrafficPolicy can only be set on "
+            errs.append(f"spec.externalTrafficPolicy: Invalid value: {go_value(etp)}: ExternalTrafficPolicy can only be set on "
                         "NodePort and LoadBalancer service")
         elif etp not in ("Cluster", "Local"):
-            errs.append(f"spec.externalTrafficPolicy: Unsupported value: {etp!r}: supported values: Cluster, Local")
+            errs.append(f"spec.externalTrafficPolicy: Unsupported value: {go_value(etp)}: supported values: Cluster, Local")
     hc = spec.get("healthCheckNodePort")
     if hc:
         if not (t == "LoadBalancer" and etp == "Local"):
-            errs.append(f"spec.healthCheckNodePort: Invalid value: {hc!r}: HealthCheckNodePort can only be set on "
+            errs.append(f"spec.healthCheckNodePort: Invalid value: {go_value(hc)}: HealthCheckNodePort can only be set on "
                         "LoadBalancer service with ExternalTrafficPolicy=Local")
         elif not isinstance(hc, int) or not 0 < hc < 65536:
-            errs.append(f"spec.healthCheckNodePort: Invalid value: {hc!r}: must be between 1 and 65535, inclusive")
+            errs.append(f"spec.healthCheckNodePort: Invalid value: {go_value(hc)}: must be between 1 and 65535, inclusive")
     ranges = spec.get("loadBalancerSourceRanges") or []
     if ranges:
         import ipaddress
@@ -74,7 +75,7 @@ def validate_service(svc: dict, old=None) -> list[str]:
             try:
                 ipaddress.ip_network(str(r).strip(), strict=False)
             except ValueError:
-                errs.append(f"spec.loadBalancerSourceRanges[{i}]: Invalid value: {r!r}: must be a list of IP ranges. "
+                errs.append(f"spec.loadBalancerSourceRanges[{i}]: Invalid value: {go_value(r)}: must be a list of IP ranges. "
                             "For example, 10.240.0.0/24,10.250.0.0/24")
     return errs
 

@@ -12,6 +12,7 @@ from __future__ import annotations
 import json
 import re
 
+from .field import go_value as gv
 from .helpers import HEALTHY, UNHEALTHY, is_extended_resource_name, is_native_resource
 from .labels import (SelectorError, is_dns1123_label, is_dns1123_subdomain, is_qualified_name,
                      is_valid_label_value, node_requirements_as_selector, selector_from_label_selector)
@@ -28,20 +29,20 @@ def validate_object_meta(obj: dict, namespaced: bool, name_fn=is_dns1123_subdoma
     if not name and not md.get("generateName"):
         errs.append("metadata.name: Required value: name or generateName is required")
     elif name:
-        errs += [f"metadata.name: Invalid value: {name!r}: {e}" for e in name_fn(name)]
+        errs += [f"metadata.name: Invalid value: {gv(name)}: {e}" for e in name_fn(name)]
     ns = md.get("namespace") or ""
     if namespaced and not ns:
         errs.append("metadata.namespace: Required value")
     if not namespaced and ns:
         errs.append("metadata.namespace: Forbidden: not allowed on this type")
     if ns:
-        errs += [f"metadata.namespace: Invalid value: {ns!r}: {e}" for e in is_dns1123_label(ns)]
+        errs += [f"metadata.namespace: Invalid value: {gv(ns)}: {e}" for e in is_dns1123_label(ns)]
     for k, v in (md.get("labels") or {}).items():
-        errs += [f"metadata.labels: Invalid value: {k!r}: {e}" for e in is_qualified_name(k)]
-        errs += [f"metadata.labels: Invalid value: {v!r}: {e}" for e in is_valid_label_value(str(v))]
+        errs += [f"metadata.labels: Invalid value: {gv(k)}: {e}" for e in is_qualified_name(k)]
+        errs += [f"metadata.labels: Invalid value: {gv(v)}: {e}" for e in is_valid_label_value(str(v))]
     ann = md.get("annotations") or {}
     for k in ann:
-        errs += [f"metadata.annotations: Invalid value: {k!r}: {e}" for e in is_qualified_name(k.lower())]
+        errs += [f"metadata.annotations: Invalid value: {gv(k)}: {e}" for e in is_qualified_name(k.lower())]
     if sum(len(k) + len(str(v)) for k, v in ann.items()) > 256 * 1024:
         errs.append("metadata.annotations: Too long: must have at most 262144 characters")
     return errs
@@ -51,15 +52,15 @@ def _validate_resource_list(rl: dict | None, path: str) -> list[str]:
     errs = []
     for k, v in (rl or {}).items():
         if is_qualified_name(k):
-            errs.append(f"{path}[{k}]: Invalid value: {k!r}: must be a standard resource name or fully qualified")
+            errs.append(f"{path}[{k}]: Invalid value: {gv(k)}: must be a standard resource name or fully qualified")
         try:
             q = Quantity(v)
             if q.as_fraction() < 0:
-                errs.append(f"{path}[{k}]: Invalid value: {v!r}: must be greater than or equal to 0")
+                errs.append(f"{path}[{k}]: Invalid value: {gv(v)}: must be greater than or equal to 0")
             if not is_native_resource(k) and q.as_fraction().denominator != 1:
-                errs.append(f"{path}[{k}]: Invalid value: {v!r}: must be an integer")
+                errs.append(f"{path}[{k}]: Invalid value: {gv(v)}: must be an integer")
         except QuantityError as e:
-            errs.append(f"{path}[{k}]: Invalid value: {v!r}: {e}")
+            errs.append(f"{path}[{k}]: Invalid value: {gv(v)}: {e}")
     return errs
 
 
@@ -72,10 +73,10 @@ def validate_resource_requirements(res: dict | None, path: str) -> list[str]:
     for k, v in req.items():
         if k in lim:
             if Quantity(v) > Quantity(lim[k]):
-                errs.append(f"{path}.requests[{k}]: Invalid value: {v!r}: must be less than or equal to {k} limit")
+                errs.append(f"{path}.requests[{k}]: Invalid value: {gv(v)}: must be less than or equal to {k} limit")
             if (is_extended_resource_name(k) or k == "alpha.kubernetes.io/amd-gpu") and Quantity(v) != Quantity(lim[k]):
                 # extended resources and the legacy GPU resource (validation.go:4448-4449) cannot overcommit
-                errs.append(f"{path}.requests[{k}]: Invalid value: {v!r}: must be equal to {k} limit")
+                errs.append(f"{path}.requests[{k}]: Invalid value: {gv(v)}: must be equal to {k} limit")
         elif is_extended_resource_name(k):
             errs.append(f"{path}.limits[{k}]: Required value: Limit must be set for non overcommitable resources")
     return errs
@@ -91,7 +92,7 @@ def validate_extended_resources(pres_list: list[dict] | None, path="spec.extende
         if not name:
             errs.append(f"{p}.name: Invalid value: Extended resource name can't be empty")
         if name in coll:
-            errs.append(f"{p}.name: Invalid value: {name!r}: Extended resource name should be unique")
+            errs.append(f"{p}.name: Invalid value: {gv(name)}: Extended resource name should be unique")
         coll[name] = 0
         res = r.get("resources") or {}
         lim, req = res.get("limits") or {}, res.get("requests") or {}
@@ -125,10 +126,10 @@ def validate_containers_extended_resources(containers, names: dict, path: str) -
     for ci, c in enumerate(containers or []):
         for ref in c.get("extendedResourceRequests") or []:
             if ref not in names:
-                errs.append(f"{path}[{ci}].extendedResourceRequests: Invalid value: {ref!r}: Reference to unknown extended resource")
+                errs.append(f"{path}[{ci}].extendedResourceRequests: Invalid value: {gv(ref)}: Reference to unknown extended resource")
                 continue
             if names[ref] != 0:
-                errs.append(f"{path}[{ci}].extendedResourceRequests: Invalid value: {ref!r}: Multiple reference to extended resource (sharing is not allowed)")
+                errs.append(f"{path}[{ci}].extendedResourceRequests: Invalid value: {gv(ref)}: Multiple reference to extended resource (sharing is not allowed)")
                 continue
             names[ref] += 1
     return errs
@@ -144,7 +145,7 @@ def _validate_container(c: dict, path: str, init: bool) -> list[str]:
     if not name:
         errs.append(f"{path}.name: Required value")
     else:
-        errs += [f"{path}.name: Invalid value: {name!r}: {e}" for e in is_dns1123_label(name)]
+        errs += [f"{path}.name: Invalid value: {gv(name)}: {e}" for e in is_dns1123_label(name)]
     if not c.get("image"):
         errs.append(f"{path}.image: Required value")
     errs += validate_resource_requirements(c.get("resources"), path + ".resources")
@@ -152,12 +153,12 @@ def _validate_container(c: dict, path: str, init: bool) -> list[str]:
     for i, p in enumerate(c.get("ports") or []):
         cp = p.get("containerPort")
         if not isinstance(cp, int) or not 0 < cp < 65536:
-            errs.append(f"{path}.ports[{i}].containerPort: Invalid value: {cp!r}: must be between 1 and 65535")
+            errs.append(f"{path}.ports[{i}].containerPort: Invalid value: {gv(cp)}: must be between 1 and 65535")
         hp = p.get("hostPort") or 0
         if hp and not 0 < hp < 65536:
-            errs.append(f"{path}.ports[{i}].hostPort: Invalid value: {hp!r}")
+            errs.append(f"{path}.ports[{i}].hostPort: Invalid value: {gv(hp)}")
         if p.get("protocol", "TCP") not in ("TCP", "UDP", "SCTP"):
-            errs.append(f"{path}.ports[{i}].protocol: Unsupported value: {p.get('protocol')!r}")
+            errs.append(f"{path}.ports[{i}].protocol: Unsupported value: {gv(p.get('protocol'))}")
         key = (hp, p.get("protocol", "TCP"))
         if hp and key in ports:
             errs.append(f"{path}.ports[{i}].hostPort: Duplicate value: {hp}")
@@ -201,7 +202,7 @@ def _validate_ref_name(name: str, path: str) -> list[str]:
     """ValidateConfigMapName / ValidateSecretName: a DNS-1123 subdomain."""
     if not name:
         return [f"{path}: Required value"]
-    return [f"{path}: Invalid value: {name!r}: {msg}" for msg in is_dns1123_subdomain(name)]
+    return [f"{path}: Invalid value: {gv(name)}: {msg}" for msg in is_dns1123_subdomain(name)]
 
 
 def _split_subscript(fp: str):
@@ -237,14 +238,14 @@ def validate_object_field_selector(fs: dict, expressions, path: str) -> list[str
     elif sub is None and fp not in _DOWNWARD_LABELS and fp != "spec.host":
         conv_err = f"field label not supported: {fp}"
     if conv_err:
-        return [f"{path}.fieldPath: Invalid value: {fp!r}: error converting fieldPath: {conv_err}"]
+        return [f"{path}.fieldPath: Invalid value: {gv(fp)}: error converting fieldPath: {conv_err}"]
     if fp == "spec.host":
         fp = "spec.nodeName"
     if sub is not None:
         key = sub.lower() if base == "metadata.annotations" else sub
-        return [f"{path}: Invalid value: {sub!r}: {msg}" for msg in is_qualified_name(key)]
+        return [f"{path}: Invalid value: {gv(sub)}: {msg}" for msg in is_qualified_name(key)]
     if fp not in expressions:
-        return [f"{path}.fieldPath: Unsupported value: {fp!r}: supported values: "
+        return [f"{path}.fieldPath: Unsupported value: {gv(fp)}: supported values: "
                 + ", ".join(f'"{x}"' for x in sorted(expressions))]
     return []
 
@@ -258,7 +259,7 @@ def validate_env(env: list, path: str) -> list[str]:
         if not name:
             errs.append(f"{p}.name: Required value")
         else:
-            errs += [f"{p}.name: Invalid value: {name!r}: {msg}" for msg in is_env_var_name(name)]
+            errs += [f"{p}.name: Invalid value: {gv(name)}: {msg}" for msg in is_env_var_name(name)]
         vf = e.get("valueFrom")
         if vf is None:
             continue
@@ -275,7 +276,7 @@ def validate_env(env: list, path: str) -> list[str]:
             if not res:
                 errs.append(f"{vp}.resourceFieldRef.resource: Required value")
             elif res not in ENV_RESOURCE_FIELDS:
-                errs.append(f"{vp}.resourceFieldRef.resource: Unsupported value: {res!r}")
+                errs.append(f"{vp}.resourceFieldRef.resource: Unsupported value: {gv(res)}")
         for kind in ("configMapKeyRef", "secretKeyRef"):
             ref = vf.get(kind)
             if ref is None:
@@ -286,7 +287,7 @@ def validate_env(env: list, path: str) -> list[str]:
             if not key:
                 errs.append(f"{vp}.{kind}.key: Required value")
             else:
-                errs += [f"{vp}.{kind}.key: Invalid value: {key!r}: {msg}" for msg in is_config_map_key(key)]
+                errs += [f"{vp}.{kind}.key: Invalid value: {gv(key)}: {msg}" for msg in is_config_map_key(key)]
         if n == 0:
             errs.append(f"{vp}: Invalid value: \"\": must specify one of: `fieldRef`, `resourceFieldRef`, "
                         "`configMapKeyRef` or `secretKeyRef`")
@@ -304,7 +305,7 @@ def validate_env_from(env_from: list, path: str) -> list[str]:
         p = f"{path}[{i}]"
         prefix = e.get("prefix") or ""
         if prefix:
-            errs += [f"{p}.prefix: Invalid value: {prefix!r}: {msg}" for msg in is_env_var_name(prefix)]
+            errs += [f"{p}.prefix: Invalid value: {gv(prefix)}: {msg}" for msg in is_env_var_name(prefix)]
         srcs = [k for k in ("configMapRef", "secretRef") if e.get(k) is not None]
         for k in srcs:
             errs += _validate_ref_name((e.get(k) or {}).get("name") or "", f"{p}.{k}.name")
@@ -345,9 +346,9 @@ def validate_local_descending_path(p: str, path: str) -> list[str]:
         return [f"{path}: Required value"]
     errs = []
     if p.startswith("/"):
-        errs.append(f"{path}: Invalid value: {p!r}: must be a relative path")
+        errs.append(f"{path}: Invalid value: {gv(p)}: must be a relative path")
     if ".." in p.split("/"):
-        errs.append(f"{path}: Invalid value: {p!r}: must not contain '..'")
+        errs.append(f"{path}: Invalid value: {gv(p)}: must not contain '..'")
     return errs
 
 
@@ -385,35 +386,35 @@ def validate_pod_spec(spec: dict, path="spec") -> list[str]:
             errs += _validate_container(c, f"{path}.{kind}[{i}]", kind == "initContainers")
             n = c.get("name")
             if n in names:
-                errs.append(f"{path}.{kind}[{i}].name: Duplicate value: {n!r}")
+                errs.append(f"{path}.{kind}[{i}].name: Duplicate value: {gv(n)}")
             names.add(n)
     rp = spec.get("restartPolicy", "Always")
     if rp not in RESTART_POLICIES:
-        errs.append(f"{path}.restartPolicy: Unsupported value: {rp!r}")
+        errs.append(f"{path}.restartPolicy: Unsupported value: {gv(rp)}")
     vols = set()
     for i, v in enumerate(spec.get("volumes") or []):
         n = v.get("name") or ""
-        errs += [f"{path}.volumes[{i}].name: Invalid value: {n!r}: {e}" for e in is_dns1123_label(n)]
+        errs += [f"{path}.volumes[{i}].name: Invalid value: {gv(n)}: {e}" for e in is_dns1123_label(n)]
         if n in vols:
-            errs.append(f"{path}.volumes[{i}].name: Duplicate value: {n!r}")
+            errs.append(f"{path}.volumes[{i}].name: Duplicate value: {gv(n)}")
         vols.add(n)
         errs += _validate_volume_items(v, f"{path}.volumes[{i}]")
     for kind, lst in (("initContainers", inits), ("containers", containers)):
         for i, c in enumerate(lst):
             for j, m in enumerate(c.get("volumeMounts") or []):
                 if m.get("name") not in vols:
-                    errs.append(f"{path}.{kind}[{i}].volumeMounts[{j}].name: Not found: {m.get('name')!r}")
+                    errs.append(f"{path}.{kind}[{i}].volumeMounts[{j}].name: Not found: {gv(m.get('name'))}")
     for k, v in (spec.get("nodeSelector") or {}).items():
-        errs += [f"{path}.nodeSelector: Invalid value: {k!r}: {e}" for e in is_qualified_name(k)]
-        errs += [f"{path}.nodeSelector: Invalid value: {v!r}: {e}" for e in is_valid_label_value(str(v))]
+        errs += [f"{path}.nodeSelector: Invalid value: {gv(k)}: {e}" for e in is_qualified_name(k)]
+        errs += [f"{path}.nodeSelector: Invalid value: {gv(v)}: {e}" for e in is_valid_label_value(str(v))]
     for i, t in enumerate(spec.get("tolerations") or []):
         op = t.get("operator") or "Equal"
         if op not in ("Equal", "Exists"):
-            errs.append(f"{path}.tolerations[{i}].operator: Unsupported value: {op!r}")
+            errs.append(f"{path}.tolerations[{i}].operator: Unsupported value: {gv(op)}")
         if op == "Exists" and t.get("value"):
             errs.append(f"{path}.tolerations[{i}].operator: Invalid value: value must be empty when `operator` is 'Exists'")
         if t.get("effect") not in (None, "", "NoSchedule", "PreferNoSchedule", "NoExecute"):
-            errs.append(f"{path}.tolerations[{i}].effect: Unsupported value: {t.get('effect')!r}")
+            errs.append(f"{path}.tolerations[{i}].effect: Unsupported value: {gv(t.get('effect'))}")
     na = ((spec.get("affinity") or {}).get("nodeAffinity") or {})
     req = na.get("requiredDuringSchedulingIgnoredDuringExecution") or {}
     errs += _validate_node_selector_terms(req.get("nodeSelectorTerms"),
@@ -486,13 +487,13 @@ def validate_node(node: dict, old: dict | None = None) -> list[str]:
             if dev.get("id", did) != did:
                 errs.append(f"{p}.id: Invalid value: must equal the map key")
             if dev.get("health", HEALTHY) not in (HEALTHY, UNHEALTHY):
-                errs.append(f"{p}.health: Unsupported value: {dev.get('health')!r}")
+                errs.append(f"{p}.health: Unsupported value: {gv(dev.get('health'))}")
             for k, v in (dev.get("attributes") or {}).items():
-                errs += [f"{p}.attributes: Invalid value: {k!r}: {e}" for e in is_qualified_name(k)]
-                errs += [f"{p}.attributes: Invalid value: {v!r}: {e}" for e in is_valid_label_value(str(v))]
+                errs += [f"{p}.attributes: Invalid value: {gv(k)}: {e}" for e in is_qualified_name(k)]
+                errs += [f"{p}.attributes: Invalid value: {gv(v)}: {e}" for e in is_valid_label_value(str(v))]
     for i, t in enumerate((node.get("spec") or {}).get("taints") or []):
         if t.get("effect") not in ("NoSchedule", "PreferNoSchedule", "NoExecute"):
-            errs.append(f"spec.taints[{i}].effect: Unsupported value: {t.get('effect')!r}")
+            errs.append(f"spec.taints[{i}].effect: Unsupported value: {gv(t.get('effect'))}")
         errs += [f"spec.taints[{i}].key: Invalid value: {e}" for e in is_qualified_name(t.get("key") or "")]
     return errs
 
@@ -561,7 +562,7 @@ def validate_config_data(obj, old=None):
     errs = validate_object_meta(obj, True)
     for field in ("data", "binaryData", "stringData"):
         for k in (obj.get(field) or {}):
-            errs += [f"{field}[{k}]: Invalid value: {k!r}: {e}" for e in is_config_map_key(k)]
+            errs += [f"{field}[{k}]: Invalid value: {gv(k)}: {e}" for e in is_config_map_key(k)]
     return errs
 
 

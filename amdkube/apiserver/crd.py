@@ -23,6 +23,7 @@ from ..api.labels import is_dns1123_label, is_dns1123_subdomain
 from ..api.scheme import SCHEME, ResourceInfo
 from ..store import PUT
 from ..store.storage import decode_kv
+from ..api.field import go_value
 
 FINALIZER = "customresourcecleanup.apiextensions.k8s.io"
 PREFIX = "/registry/customresourcedefinitions/"
@@ -48,7 +49,7 @@ def validate_crd(crd: dict, old: dict | None = None) -> list[str]:
         errs.append(f"metadata.name: Invalid value: must be spec.names.plural+\".\"+spec.group")
     for sn in names.get("shortNames") or []:
         if is_dns1123_label(sn):
-            errs.append(f"spec.names.shortNames: Invalid value: {sn!r}")
+            errs.append(f"spec.names.shortNames: Invalid value: {go_value(sn)}")
     if old is not None:
         for f in ("group", "scope"):
             if (old.get("spec") or {}).get(f) != spec.get(f):
@@ -80,7 +81,7 @@ def validate_schema(v, s: dict, path: str = "") -> list[str]:
     elif t in _TYPES and not isinstance(v, _TYPES[t]):
         return [f"{p}: Invalid value: must be of type {t}"]
     if "enum" in s and v not in s["enum"]:
-        errs.append(f"{p}: Unsupported value: {v!r}: supported values: {', '.join(map(repr, s['enum']))}")
+        errs.append(f"{p}: Unsupported value: {go_value(v)}: supported values: {', '.join(map(repr, s['enum']))}")
     if isinstance(v, (int, float)) and not isinstance(v, bool):
         if "minimum" in s and (v < s["minimum"] or (s.get("exclusiveMinimum") and v == s["minimum"])):
             errs.append(f"{p}: Invalid value: {v}: should be greater than {'' if s.get('exclusiveMinimum') else 'or equal to '}{s['minimum']}")
@@ -94,7 +95,7 @@ def validate_schema(v, s: dict, path: str = "") -> list[str]:
         if "maxLength" in s and len(v) > s["maxLength"]:
             errs.append(f"{p}: Invalid value: should be at most {s['maxLength']} chars long")
         if "pattern" in s and not re.search(s["pattern"], v):
-            errs.append(f"{p}: Invalid value: {v!r}: should match {s['pattern']!r}")
+            errs.append(f"{p}: Invalid value: {go_value(v)}: should match {s['pattern']!r}")
     if isinstance(v, list):
         if "minItems" in s and len(v) < s["minItems"]:
             errs.append(f"{p}: Invalid value: should have at least {s['minItems']} items")

@@ -30,6 +30,7 @@ from ..store import Filter, MVCCStore, Storage, event_object, PUT
 from ..store.storage import decode_kv
 from . import admission as adm
 from .service import ServiceAllocator
+from ..api.field import go_value
 
 
 def _json_merge_patch(target, patch):
@@ -487,7 +488,7 @@ def _validate_pod_status(pod):
     errs = []
     ph = (pod.get("status") or {}).get("phase")
     if ph and ph not in ("Pending", "Running", "Succeeded", "Failed", "Unknown"):
-        errs.append(f"status.phase: Unsupported value: {ph!r}")
+        errs.append(f"status.phase: Unsupported value: {go_value(ph)}")
     return errs
 
 

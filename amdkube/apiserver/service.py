@@ -20,6 +20,7 @@ import random
 
 from ..api import meta as m
 from ..store.storage import decode_kv
+from ..api.field import go_value
 
 DEFAULT_SERVICE_CIDR = "10.0.0.0/24"          # kube-apiserver --service-cluster-ip-range default
 DEFAULT_NODE_PORT_RANGE = (30000, 32767)      # --service-node-port-range default 30000-32767
@@ -112,12 +113,12 @@ class ServiceAllocator:
             try:
                 ip = ipaddress.ip_address(requested)
             except ValueError:
-                raise m.invalid("Service", key.rsplit("/", 1)[-1], [f"spec.clusterIP: Invalid value: {requested!r}: must be a valid IP address"])
+                raise m.invalid("Service", key.rsplit("/", 1)[-1], [f"spec.clusterIP: Invalid value: {go_value(requested)}: must be a valid IP address"])
             if not self._usable(ip):
-                raise m.invalid("Service", key.rsplit("/", 1)[-1], [f"spec.clusterIP: Invalid value: {requested!r}: provided IP is not in the valid range. "
+                raise m.invalid("Service", key.rsplit("/", 1)[-1], [f"spec.clusterIP: Invalid value: {go_value(requested)}: provided IP is not in the valid range. "
                                                  f"The range of valid IPs is {self.net}"])
             if str(ip) in self.ips and self.ips[str(ip)] != key:
-                raise m.invalid("Service", key.rsplit("/", 1)[-1], [f"spec.clusterIP: Invalid value: {requested!r}: provided IP is already allocated"])
+                raise m.invalid("Service", key.rsplit("/", 1)[-1], [f"spec.clusterIP: Invalid value: {go_value(requested)}: provided IP is already allocated"])
             self._reserve(key, "ip", str(ip))
             return str(ip)
         first = int(self.net.network_address) + (1 if self.net.version == 4 and self.net.prefixlen < 31 else 0)

@@ -14,6 +14,8 @@ from __future__ import annotations
 
 import re
 
+from ..api.field import go_value
+
 SAFE_ANNOTATION = "security.alpha.kubernetes.io/sysctls"
 UNSAFE_ANNOTATION = "security.alpha.kubernetes.io/unsafe-sysctls"
 MAX_LEN = 253
@@ -54,16 +56,16 @@ def validate_annotations(annotations: dict | None, path: str = "metadata.annotat
         try:
             pairs = parse_annotation(ann.get(key))
         except ValueError as e:
-            errs.append(f"{path}[{key}]: Invalid value: {ann.get(key)!r}: {e}")
+            errs.append(f"{path}[{key}]: Invalid value: {go_value(ann.get(key))}: {e}")
             continue
         for i, (k, _v) in enumerate(pairs):
             if len(k) > MAX_LEN or not SYSCTL_RE.match(k):
-                errs.append(f"{path}[{key}][{i}].name: Invalid value: {k!r}: must have at most {MAX_LEN} characters "
+                errs.append(f"{path}[{key}][{i}].name: Invalid value: {go_value(k)}: must have at most {MAX_LEN} characters "
                             f"and match regex {SYSCTL_RE.pattern}")
         names[key] = {k for k, _ in pairs}
     both = sorted(names.get(SAFE_ANNOTATION, set()) & names.get(UNSAFE_ANNOTATION, set()))
     if both:
-        errs.append(f"{path}[{UNSAFE_ANNOTATION}]: Invalid value: {', '.join(both)!r}: can not be safe and unsafe")
+        errs.append(f"{path}[{UNSAFE_ANNOTATION}]: Invalid value: {go_value(', '.join(both))}: can not be safe and unsafe")
     return errs
 
 

@@ -7,6 +7,8 @@ CRI seccomp_profile_path (kubelet/kuberuntime.py::seccomp_profile).
 """
 from __future__ import annotations
 
+from ..api.field import go_value
+
 SECCOMP_POD_ANNOTATION = "seccomp.security.alpha.kubernetes.io/pod"
 SECCOMP_CONTAINER_PREFIX = "container.seccomp.security.alpha.kubernetes.io/"
 
@@ -28,5 +30,5 @@ def validate_seccomp_annotations(annotations: dict) -> list[str]:
         if k == SECCOMP_POD_ANNOTATION or k.startswith(SECCOMP_CONTAINER_PREFIX):
             e = validate_seccomp_profile(v)
             if e:
-                errs.append(f"metadata.annotations[{k}]: Invalid value: {v!r}: {e}")
+                errs.append(f"metadata.annotations[{k}]: Invalid value: {go_value(v)}: {e}")
     return errs

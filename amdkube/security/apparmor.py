@@ -17,6 +17,8 @@ from __future__ import annotations
 
 import os
 
+from ..api.field import go_value
+
 CONTAINER_ANNOTATION_PREFIX = "container.apparmor.security.beta.kubernetes.io/"
 DEFAULT_PROFILE_ANNOTATION = "apparmor.security.beta.kubernetes.io/defaultProfileName"
 ALLOWED_PROFILES_ANNOTATION = "apparmor.security.beta.kubernetes.io/allowedProfileNames"
@@ -56,10 +58,10 @@ def validate_pod_annotations(pod: dict, gate_enabled: bool = True) -> list[str]:
             errs.append(f"{path}: Forbidden: AppArmor is disabled by feature-gate")
             continue
         if k[len(CONTAINER_ANNOTATION_PREFIX):] not in names:
-            errs.append(f"{path}: Invalid value: {k[len(CONTAINER_ANNOTATION_PREFIX):]!r}: container not found")
+            errs.append(f"{path}: Invalid value: {go_value(k[len(CONTAINER_ANNOTATION_PREFIX):])}: container not found")
         e = validate_profile_format(v)
         if e:
-            errs.append(f"{path}: Invalid value: {v!r}: {e}")
+            errs.append(f"{path}: Invalid value: {go_value(v)}: {e}")
     return errs
 
 

@@ -19,7 +19,8 @@ detail").
 from __future__ import annotations
 
 import copy
-import json
+
+from ..api.field import FieldError, forbidden, go_slice, invalid, required  # noqa: F401  (FieldError re-exported)
 
 SECCOMP_POD_ANNOTATION = "seccomp.security.alpha.kubernetes.io/pod"
 SECCOMP_CONTAINER_PREFIX = "container.seccomp.security.alpha.kubernetes.io/"
@@ -49,57 +50,6 @@ _VOLUME_KEYS = (("hostPath", "hostPath"), ("emptyDir", "emptyDir"), ("gcePersist
                 ("vsphereVolume", "vsphereVolume"), ("quobyte", "quobyte"), ("azureDisk", "azureDisk"),
                 ("photonPersistentDisk", "photonPersistentDisk"), ("storageos", "storageos"),
                 ("projected", "projected"), ("portworxVolume", "portworxVolume"), ("scaleIO", "scaleIO"))
-
-
-# ============================================================================ field errors
-class GoRepr(str):
-    """A value already rendered the way Go's %#v prints it."""
-
-
-def go_slice(type_name: str, items) -> GoRepr:
-    if items is None:
-        return GoRepr(f"[]{type_name}(nil)")
-    return GoRepr(f"[]{type_name}{{" + ", ".join(json.dumps(x) if isinstance(x, str) else str(x) for x in items) + "}")
-
-
-def _gov(v) -> str:
-    """%#v of a field.Error's bad value (nil and nil pointers print as "null")."""
-    if isinstance(v, GoRepr):
-        return str(v)
-    if isinstance(v, bool):
-        return "true" if v else "false"
-    if v is None:
-        return '"null"'
-    if isinstance(v, str):
-        return json.dumps(v)
-    return str(v)
-
-
-class FieldError:
-    REQUIRED, FORBIDDEN, INVALID = "Required value", "Forbidden", "Invalid value"
-
-    def __init__(self, kind: str, field: str, value=None, detail: str = ""):
-        self.type, self.field, self.value, self.detail = kind, field, value, detail
-
-    def __str__(self):
-        body = self.type if self.type in (self.REQUIRED, self.FORBIDDEN) else f"{self.type}: {_gov(self.value)}"
-        if self.detail:
-            body += f": {self.detail}"
-        return f"{self.field}: {body}"
-
-    __repr__ = __str__
-
-
-def invalid(path, value, detail):
-    return FieldError(FieldError.INVALID, path, value, detail)
-
-
-def required(path, detail=""):
-    return FieldError(FieldError.REQUIRED, path, None, detail)
-
-
-def forbidden(path, detail):
-    return FieldError(FieldError.FORBIDDEN, path, None, detail)
 
 
 def _key(path: str, key: str) -> str:

@@ -178,11 +178,11 @@ def test_validate_env_success_cases():
 
 @pytest.mark.parametrize("env,needle", [
     ([{"name": ""}], "env[0].name: Required value"),
-    ([{"name": "a!b"}], "env[0].name: Invalid value: 'a!b': a valid environment variable name"),
+    ([{"name": "a!b"}], 'env[0].name: Invalid value: \"a!b\": a valid environment variable name'),
     ([{"name": "1=bad", "value": "x"}], "must not start with a digit"),
-    ([{"name": "."}], "env[0].name: Invalid value: '.': must not be"),
-    ([{"name": ".."}], "env[0].name: Invalid value: '..': must not be"),
-    ([{"name": "..abc"}], "env[0].name: Invalid value: '..abc': must not start with"),
+    ([{"name": "."}], 'env[0].name: Invalid value: \".\": must not be'),
+    ([{"name": ".."}], 'env[0].name: Invalid value: \"..\": must not be'),
+    ([{"name": "..abc"}], 'env[0].name: Invalid value: \"..abc\": must not start with'),
     ([{"name": "abc", "value": "foo", **_fr("metadata.name")}], "valueFrom: Invalid value: \"\": may not be specified when `value`"),
     ([{"name": "abc", "valueFrom": {}}], "must specify one of: `fieldRef`, `resourceFieldRef`, `configMapKeyRef` or `secretKeyRef`"),
     ([{"name": "abc", "valueFrom": {"fieldRef": {"apiVersion": "v1", "fieldPath": "metadata.name"},
@@ -191,14 +191,14 @@ def test_validate_env_success_cases():
     ([{"name": "abc", "valueFrom": {"secretKeyRef": {"name": "$%^&*#", "key": "a-key"}}}], "secretKeyRef.name: Invalid value"),
     ([{"name": "abc", "valueFrom": {"configMapKeyRef": {"name": "$%^&*#", "key": "k"}}}], "configMapKeyRef.name: Invalid value"),
     ([{"name": "abc", "valueFrom": {"fieldRef": {"apiVersion": "v1"}}}], "valueFrom.fieldRef.fieldPath: Required value"),
-    ([{"name": "abc", **_fr("metadata.whoops")}], "fieldRef.fieldPath: Invalid value: 'metadata.whoops': error converting fieldPath"),
+    ([{"name": "abc", **_fr("metadata.whoops")}], 'fieldRef.fieldPath: Invalid value: \"metadata.whoops\": error converting fieldPath'),
     ([{"name": "abc", **_fr("metadata.name['key']")}], "error converting fieldPath: field label does not support subscript"),
-    ([{"name": "abc", **_fr("metadata.labels")}], "fieldRef.fieldPath: Unsupported value: 'metadata.labels': supported values: "
+    ([{"name": "abc", **_fr("metadata.labels")}], 'fieldRef.fieldPath: Unsupported value: \"metadata.labels\": supported values: '
                                                   '"metadata.name", "metadata.namespace", "metadata.uid", "spec.nodeName", '
                                                   '"spec.serviceAccountName", "status.hostIP", "status.podIP"'),
-    ([{"name": "abc", **_fr("metadata.annotations['invalid~key']")}], "valueFrom.fieldRef: Invalid value: 'invalid~key'"),
-    ([{"name": "abc", **_fr("metadata.labels['Www.k8s.io/test']")}], "valueFrom.fieldRef: Invalid value: 'Www.k8s.io/test'"),
-    ([{"name": "abc", **_fr("status.phase")}], "fieldRef.fieldPath: Unsupported value: 'status.phase'"),
+    ([{"name": "abc", **_fr("metadata.annotations['invalid~key']")}], 'valueFrom.fieldRef: Invalid value: \"invalid~key\"'),
+    ([{"name": "abc", **_fr("metadata.labels['Www.k8s.io/test']")}], 'valueFrom.fieldRef: Invalid value: \"Www.k8s.io/test\"'),
+    ([{"name": "abc", **_fr("status.phase")}], 'fieldRef.fieldPath: Unsupported value: \"status.phase\"'),
     ([{"name": "abc", "valueFrom": {"resourceFieldRef": {"resource": "limits.gpu"}}}], "resourceFieldRef.resource: Unsupported value"),
 ])
 def test_validate_env_error_cases(env, needle):
@@ -212,7 +212,7 @@ def test_validate_env_from():
     assert _env_pod(env_from=ok) == []
     for ef, needle in [([{"configMapRef": {"name": ""}}], "envFrom[0].configMapRef.name: Required value"),
                        ([{"configMapRef": {"name": "$"}}], "envFrom[0].configMapRef.name: Invalid value"),
-                       ([{"prefix": "a!b", "configMapRef": {"name": "abc"}}], "envFrom[0].prefix: Invalid value: 'a!b'"),
+                       ([{"prefix": "a!b", "configMapRef": {"name": "abc"}}], 'envFrom[0].prefix: Invalid value: \"a!b\"'),
                        ([{"secretRef": {"name": "&"}}], "envFrom[0].secretRef.name: Invalid value"),
                        ([{"prefix": "a!b"}], "must specify one of: `configMapRef` or `secretRef`"),
                        ([{"configMapRef": {"name": "a"}, "secretRef": {"name": "b"}}], "may not have more than one field")]:
@@ -227,4 +227,4 @@ def test_downward_api_volume_field_paths():
                {"path": "ip", "fieldRef": {"fieldPath": "status.podIP"}}]}}]}}
     SCHEME.default(pod)
     errs = validate_pod(pod)
-    assert len(errs) == 1 and "items[1].fieldRef.fieldPath: Unsupported value: 'status.podIP'" in errs[0], errs
+    assert len(errs) == 1 and 'items[1].fieldRef.fieldPath: Unsupported value: \"status.podIP\"' in errs[0], errs

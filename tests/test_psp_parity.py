@@ -1131,3 +1131,24 @@ def test_policy_authorization_errors(allowed, n_errs):
     allowed_pod, _, errs = P.compute_security_context(ctx.list_objects("podsecuritypolicies", ""), pod,
                                                       plugin._authorized(a, ctx, pod), True)
     assert allowed_pod is None and len(errs) == n_errs
+
+
+def test_validate_never_selects_a_mutating_policy():
+    """computeSecurityContext with mutation disallowed (the validate phase): a policy that would
+    change the pod is skipped before authorization is consulted, so only non-mutating policies can
+    admit; with none, the pod is rejected even though a mutating policy validates it."""
+    mutating = restrictive_psp("mutating", runAsUser={"rule": "MustRunAs", "ranges": [{"min": 1, "max": 1}]})
+    pod = _unpriv_runasany_pod()
+    asked = []
+
+    def authorized(name):
+        asked.append(name)
+        return True
+    admitted, name, errs = P.compute_security_context([mutating], _c(pod), authorized, False)
+    assert (admitted, name, errs) == (None, "", []) and asked == []
+    admitted, name, _ = P.compute_security_context([mutating], _c(pod), authorized, True)
+    assert name == "mutating" and admitted["spec"]["containers"][0]["securityContext"]["runAsUser"] == 1
+    privileged = permissive_psp("privileged")
+    asked.clear()
+    admitted, name, _ = P.compute_security_context([mutating, privileged], _c(pod), authorized, False)
+    assert name == "privileged" and asked == ["privileged"] and P._semantic_equal(admitted, pod)
