@@ -729,7 +729,11 @@ def kubelet(argv):
     a = ap.parse_args(argv)
     klog.setup(a.v, "kubelet")
     if a.cgroup_driver == "systemd":
-        raise SystemExit("kubelet: --cgroup-driver=systemd is not supported: amdkube manages cgroup v2 directly (cgroupfs)")
+        from ..kubelet.cgroups import use_systemd
+        if not (use_systemd() or os.environ.get("AMDKUBE_SYSTEMD_BUS")):
+            # cgroup_manager_linux.go newManager: "systemd cgroup manager not available"
+            raise SystemExit("kubelet: --cgroup-driver=systemd: systemd cgroup manager not available "
+                             "(systemd is not the init system of this node)")
     from ..kubelet import node_setup
     lock = node_setup.acquire_lock(a.lock_file, a.exit_on_lock_contention,
                                    on_contention=lambda: os._exit(0)) if a.lock_file else None   # noqa: F841
@@ -796,7 +800,8 @@ def kubelet(argv):
                         runtime_request_timeout=a.runtime_request_timeout, image_service_endpoint=a.image_service_endpoint,
                         keep_terminated_pod_volumes=a.keep_terminated_pod_volumes,
                         volume_stats_agg_period=a.volume_stats_agg_period, cpu_cfs_quota=a.cpu_cfs_quota,
-                        protect_kernel_defaults=a.protect_kernel_defaults, seccomp_profile_root=a.seccomp_profile_root)
+                        protect_kernel_defaults=a.protect_kernel_defaults, seccomp_profile_root=a.seccomp_profile_root,
+                        cgroup_driver=a.cgroup_driver)
 
     async def mk():
         smi = None
@@ -848,6 +853,9 @@ def rocshim(argv):
     ap.add_argument("--insecure-registry", action="append", default=[],
                     help="registry host[:port] pulled over plain http (loopback registries always are), as dockerd's flag")
     ap.add_argument("--registry-ca", default=None, help="CA bundle for https registries")
+    ap.add_argument("--cgroup-driver", default="cgroupfs", choices=("cgroupfs", "systemd"),
+                    help="systemd: pods are slices and containers transient scopes, created over systemd's D-Bus API "
+                         "(must match the kubelet's --cgroup-driver)")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     klog.setup(a.v, "rocshim")
@@ -867,7 +875,7 @@ def rocshim(argv):
         return await RocShim(a.listen, a.state_dir, a.hooks_dir, a.isolation, network=net,
                              pod_namespaces=a.pod_namespaces or a.network_plugin == "kubenet",
                              registry_dir=a.registry_dir, insecure_registries=a.insecure_registry,
-                             registry_ca=a.registry_ca).start()
+                             registry_ca=a.registry_ca, cgroup_driver=a.cgroup_driver).start()
     _run_forever(mk)
 
 

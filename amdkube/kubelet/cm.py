@@ -72,21 +72,24 @@ def node_allocatable(capacity: dict[str, str], kube_reserved: dict[str, int], sy
     return out
 
 
-def enforce_pods_cgroup(cgroup_root: str, allocatable: dict[str, str], cpu_period_us: int = 100000) -> bool:
-    """Write the pods cgroup's limits (cgroup v2) from allocatable. False when the cgroup tree is
-    not there or not writable (e.g. an unprivileged node): allocatable is still reported and
-    scheduled against, only the kernel cap is missing."""
-    cg = os.path.join(cgroup_root, "kubepods")
+def enforce_pods_cgroup(cgroup_root: str, allocatable: dict[str, str], cpu_period_us: int = 100000,
+                        manager=None) -> bool:
+    """Write the pods cgroup's limits (cgroup v2) from allocatable, through the configured
+    cgroup driver (`manager`, a cgroups.CgroupManager; cgroupfs under cgroup_root by default):
+    /kubepods is the directory `kubepods` or, with systemd, the unit kubepods.slice. False when
+    the cgroup tree is not there or not writable (e.g. an unprivileged node): allocatable is
+    still reported and scheduled against, only the kernel cap is missing."""
+    from .cgroups import CgroupManager
+    manager = manager or CgroupManager("cgroupfs", cgroup_root)
+    res = {}
+    if "memory" in allocatable:
+        res["memory"] = Quantity(allocatable["memory"]).value()
+    if "cpu" in allocatable:
+        res["cpu_quota"] = max(1000, Quantity(allocatable["cpu"]).milli_value() * cpu_period_us // 1000)
+        res["cpu_period"] = cpu_period_us
     try:
-        os.makedirs(cg, exist_ok=True)
-        if "memory" in allocatable:
-            with open(os.path.join(cg, "memory.max"), "w") as f:
-                f.write(str(Quantity(allocatable["memory"]).value()))
-        if "cpu" in allocatable:
-            quota = Quantity(allocatable["cpu"]).milli_value() * cpu_period_us // 1000
-            with open(os.path.join(cg, "cpu.max"), "w") as f:
-                f.write(f"{max(1000, quota)} {cpu_period_us}")
+        manager.create("/kubepods", res)
         return True
-    except OSError as e:
-        log.debug("pods cgroup limits not enforced under %s: %r", cg, e)
+    except Exception as e:
+        log.debug("pods cgroup limits not enforced under %s: %r", manager.path("/kubepods"), e)
         return False

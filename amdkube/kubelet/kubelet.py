@@ -179,6 +179,7 @@ class KubeletConfig:
     keep_terminated_pod_volumes: bool = False         # --keep-terminated-pod-volumes
     volume_stats_agg_period: float = 60.0             # --volume-stats-agg-period (du cache TTL, s)
     cpu_cfs_quota: bool = True                        # --cpu-cfs-quota (CPU limits become CFS quota)
+    cgroup_driver: str = "cgroupfs"                   # --cgroup-driver: cgroupfs | systemd (slices and scopes)
     protect_kernel_defaults: bool = False             # --protect-kernel-defaults
     seccomp_profile_root: str | None = None           # --seccomp-profile-root (default <root-dir>/seccomp)
 
@@ -261,6 +262,7 @@ class Kubelet:
         self.runtime = RuntimeManager(self.cri, self.dm, config.root_dir, self.recorder, image_pull_qps=config.registry_qps,
                                       image_pull_burst=config.registry_burst, serialize_image_pulls=config.serialize_image_pulls)
         self.runtime.cpu_cfs_quota = config.cpu_cfs_quota
+        self.runtime.cgroup_driver = config.cgroup_driver
         self._node_keyring = None     # credentialprovider.node_keyring, read on first use
         from .checkpoint import PodCheckpointManager
         self.pod_checkpoints = PodCheckpointManager(config.bootstrap_checkpoint_path) \
@@ -333,6 +335,7 @@ class Kubelet:
         self.stats = StatsProvider(self, du_ttl=config.volume_stats_agg_period)
         self._cpuset_applied: dict[str, str] = {}
         self._pods_cgroup_enforced = None
+        self._cgroup_manager = None         # cgroups.CgroupManager for --cgroup-driver
         self.pressure: set[str] = set()
         self.status = StatusManager(client, on_terminal=self._on_terminal)
         self.node: dict | None = None
@@ -395,9 +398,24 @@ class Kubelet:
         self.m_evictions = Counter("kubelet_evictions", "Cumulative number of pod evictions by eviction signal", ["eviction_signal"], registry=r)
 
     # ================================================================ lifecycle
+    async def _check_cgroup_driver(self):
+        """dockershim NewDockerService (docker_service.go:237-253): the kubelet and its runtime
+        must agree on the cgroup driver, or pods would land in cgroups nobody enforces. A runtime
+        that does not report one (CRI Status info `cgroupDriver`) is not checked."""
+        try:
+            st = await self.cri.status()
+            rt = dict(getattr(st, "info", {}) or {}).get("cgroupDriver", "")
+        except Exception as e:
+            log.debug("runtime status for the cgroup driver check: %r", e)
+            return
+        if rt and rt != self.cfg.cgroup_driver:
+            raise RuntimeError(f"misconfiguration: kubelet cgroup driver: {self.cfg.cgroup_driver!r} is different from "
+                               f"the container runtime's cgroup driver: {rt!r}")
+
     async def start(self):
         os.makedirs(os.path.join(self.cfg.root_dir, "pods"), exist_ok=True)
         await self.cri.connect()
+        await self._check_cgroup_driver()
         # pods the runtime already holds anything of (a previous kubelet incarnation): decided
         # from runtime state, never from creation timestamps (static pods get a fresh
         # creationTimestamp on every manifest read; API clocks may run ahead of the node's)
@@ -661,7 +679,10 @@ class Kubelet:
         st["_removed"] = removed
         if self.cfg.cgroup_root and "pods" in self.cfg.enforce_node_allocatable.split(",") and \
                 self._pods_cgroup_enforced != (alloc.get("cpu"), alloc.get("memory")):
-            if enforce_pods_cgroup(self.cfg.cgroup_root, alloc):
+            if self._cgroup_manager is None:
+                from .cgroups import CgroupManager
+                self._cgroup_manager = CgroupManager(self.cfg.cgroup_driver, self.cfg.cgroup_root)
+            if enforce_pods_cgroup(self.cfg.cgroup_root, alloc, manager=self._cgroup_manager):
                 self._pods_cgroup_enforced = (alloc.get("cpu"), alloc.get("memory"))
         return st
 

@@ -78,11 +78,12 @@ FIELDS = {
     "maximumDeadContainersPerContainer": ("maximum_dead_containers_per_container", int),
     "maximumDeadContainers": ("maximum_dead_containers", int),
     "minimumGCAge": ("minimum_container_ttl_duration", _dur),
+    "cgroupDriver": ("cgroup_driver", str),
 }
 # accepted for compatibility, no effect here (the reference's knobs for parts this kubelet
-# implements differently: docker, cgroup drivers, authn/z webhooks, cAdvisor port, ...)
+# implements differently: docker, the QoS cgroup root, authn/z webhooks, cAdvisor port, ...)
 IGNORED = {"kind", "apiVersion", "configTrialDuration", "crashLoopThreshold", "authentication", "authorization",
-           "cgroupDriver", "cgroupsPerQOS", "cgroupRoot", "hairpinMode", "readOnlyPort", "tlsCertFile", "tlsPrivateKeyFile",
+           "cgroupsPerQOS", "cgroupRoot", "hairpinMode", "readOnlyPort", "tlsCertFile", "tlsPrivateKeyFile",
            "registryPullQPS", "registryBurst", "eventRecordQPS", "eventBurst", "enableDebuggingHandlers", "healthzPort",
            "healthzBindAddress", "oomScoreAdj", "streamingConnectionIdleTimeout", "volumeStatsAggPeriod",
            "runtimeRequestTimeout", "serializeImagePulls", "kubeAPIQPS", "kubeAPIBurst", "podPidsLimit", "hostnameOverride",

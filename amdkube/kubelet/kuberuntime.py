@@ -184,6 +184,7 @@ class RuntimeManager:
         self._pull_sem = asyncio.Semaphore(1) if serialize_image_pulls else None
         self._pull_limiter = TokenBucket(image_pull_qps, image_pull_burst or 1) if image_pull_qps else None
         self.cpu_cfs_quota = True   # --cpu-cfs-quota
+        self.cgroup_driver = "cgroupfs"   # --cgroup-driver
         self.dm = device_manager
         self.root = root_dir
         self.recorder = recorder
@@ -256,7 +257,7 @@ class RuntimeManager:
             hostname=spec.get("hostname") or md["name"], log_directory=log_dir, port_mappings=ports,
             labels={**(md.get("labels") or {}), L_POD_NAME: md["name"], L_POD_NS: md.get("namespace", ""), L_POD_UID: md["uid"]},
             annotations=ann, dns_config=self.dns.cri_config(pod) if self.dns is not None else None,
-            linux=C.LinuxPodSandboxConfig(cgroup_parent=cgroup_parent(pod), sysctls=pod_sysctls(pod),
+            linux=C.LinuxPodSandboxConfig(cgroup_parent=cgroup_parent(pod, self.cgroup_driver), sysctls=pod_sysctls(pod),
                                           security_context=C.LinuxSandboxSecurityContext(
                 namespace_options=C.NamespaceOption(host_network=bool(spec.get("hostNetwork")), host_pid=bool(spec.get("hostPID")),
                                                     host_ipc=bool(spec.get("hostIPC"))))))

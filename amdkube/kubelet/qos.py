@@ -55,9 +55,21 @@ def oom_score_adj(pod: dict, container: dict, memory_capacity: int) -> int:
     return int(min(999, max(2, adj)))
 
 
-def cgroup_parent(pod: dict) -> str:
+def pod_cgroup_name(pod: dict) -> str:
+    """The internal name of the pod's cgroup (pod_container_manager_linux.go GetPodContainerName)."""
     uid = (pod.get("metadata") or {}).get("uid", "")
     q = pod_qos(pod)
     if q == GUARANTEED:
-        return f"kubepods/pod{uid}"
-    return f"kubepods/{q.lower()}/pod{uid}"
+        return f"/kubepods/pod{uid}"
+    return f"/kubepods/{q.lower()}/pod{uid}"
+
+
+def cgroup_parent(pod: dict, driver: str = "cgroupfs") -> str:
+    """The CRI sandbox's cgroup parent: the driver's literal name (cgroupManager.Name) — a
+    relative path for cgroupfs, the expanded slice path for systemd
+    (kubepods.slice/kubepods-burstable.slice/kubepods-burstable-pod<uid>.slice/)."""
+    name = pod_cgroup_name(pod)
+    if driver == "systemd":
+        from .cgroups import to_systemd
+        return to_systemd(name, True)
+    return name.lstrip("/")

@@ -156,7 +156,7 @@ class PidProc:
         return await asyncio.shield(self._fut)
 
 
-def _popen(argv, stdout, stderr, env, cwd, log_path, oom_score_adj=None):
+def _popen(argv, stdout, stderr, env, cwd, log_path, oom_score_adj=None, pass_fds=()):
     """fork/exec (and the log file's open, and the child's oom_score_adj) off the event loop: a
     spawn is ~1 ms of syscalls that would otherwise stall every other CRI call the runtime is
     serving."""
@@ -165,7 +165,7 @@ def _popen(argv, stdout, stderr, env, cwd, log_path, oom_score_adj=None):
         out = logf if logf is not None else (stdout if stdout is not None else subprocess.DEVNULL)
         err = logf if logf is not None else (stderr if stderr is not None else subprocess.DEVNULL)
         p = subprocess.Popen(argv, stdin=subprocess.DEVNULL, stdout=out, stderr=err, env=env, cwd=cwd,
-                             start_new_session=True)
+                             start_new_session=True, pass_fds=pass_fds)
     finally:
         if logf is not None:
             logf.close()
@@ -178,10 +178,10 @@ def _popen(argv, stdout, stderr, env, cwd, log_path, oom_score_adj=None):
     return p, fd
 
 
-async def spawn(argv, stdout=None, stderr=None, env=None, cwd=None, log_path=None, oom_score_adj=None):
+async def spawn(argv, stdout=None, stderr=None, env=None, cwd=None, log_path=None, oom_score_adj=None, pass_fds=()):
     """Start argv in its own session with stdin from /dev/null (stdout and stderr appended to
     `log_path` when given); pidfd-watched when possible."""
-    p, fd = await asyncio.to_thread(_popen, argv, stdout, stderr, env, cwd, log_path, oom_score_adj)
+    p, fd = await asyncio.to_thread(_popen, argv, stdout, stderr, env, cwd, log_path, oom_score_adj, pass_fds)
     if fd is None:   # old kernel: a thread waits for the child
         loop = asyncio.get_running_loop()
         proc = PidProc.__new__(PidProc)
@@ -321,10 +321,13 @@ class CheckpointWriter:
 
 
 class RocShim:
+    cgroup_driver = "cgroupfs"               # --cgroup-driver (systemd: slices and transient scopes)
+    systemd = None                           # kubelet.cgroups.SystemdUnits under the systemd driver
+
     def __init__(self, socket_path: str, state_dir: str, hooks_dir: str = DEFAULT_HOOKS_DIR, isolation: str = "env",
                  cgroup_root: str = "/sys/fs/cgroup/amdkube", dev_root: str = "/dev", network=None,
                  pod_namespaces: bool = False, registry_dir: str | None = None, insecure_registries=(),
-                 registry_ca: str | None = None):
+                 registry_ca: str | None = None, cgroup_driver: str = "cgroupfs", systemd_units=None):
         self.socket = socket_path
         self.state_dir = state_dir
         # the node's environment minus GPU visibility, read once (iterating os.environ per
@@ -347,7 +350,18 @@ class RocShim:
         from ..monitoring.cadvisor import DuCache
         self.hostports = HostPortManager()
         self.du = DuCache(10.0)
-        self.cgroup_root = cgroup_root
+        # cgroupfs: the runtime's own tree under cgroup_root (kubepods/... leaves it makes itself);
+        # systemd: systemd owns the hierarchy from the cgroup mount, pods are slices the kubelet
+        # names (kubepods-burstable-pod<uid>.slice) and each container a transient scope
+        from ..kubelet.cgroups import CGROUPFS, SYSTEMD, CgroupError, SystemdUnits, use_systemd
+        if cgroup_driver not in (CGROUPFS, SYSTEMD):
+            raise CgroupError(f"invalid cgroup driver {cgroup_driver!r} (cgroupfs or systemd)")
+        if cgroup_driver == SYSTEMD and systemd_units is None and not (use_systemd() or os.environ.get("AMDKUBE_SYSTEMD_BUS")):
+            raise CgroupError("--cgroup-driver=systemd: systemd is not the init system of this node (no /run/systemd/system)")
+        self.cgroup_driver = cgroup_driver
+        self.systemd = (systemd_units or SystemdUnits()) if cgroup_driver == SYSTEMD else None
+        self._slices: set[str] = set()       # pod slices this runtime started (systemd driver)
+        self.cgroup_root = "/sys/fs/cgroup" if cgroup_driver == SYSTEMD and cgroup_root == "/sys/fs/cgroup/amdkube" else cgroup_root
         self.dev_root = dev_root
         self.sandboxes: dict[str, Sandbox] = {}
         self.containers: dict[str, Container] = {}
@@ -621,6 +635,14 @@ class RocShim:
             await self.remove_container(c.id)
         self.sandboxes.pop(sid, None)
         self._unckpt("sandboxes", sid)
+        if self.systemd is not None:
+            slice_name = self._sandbox_slice(s)
+            if slice_name in self._slices:
+                self._slices.discard(slice_name)
+                try:
+                    await asyncio.to_thread(self.systemd.stop, slice_name)
+                except Exception as e:
+                    log.debug("systemd: stopping %s: %r", slice_name, e)
         self._emit_removed(s)
         await asyncio.to_thread(shutil.rmtree, os.path.join(self.state_dir, "rootfs", sid), True)
 
@@ -695,7 +717,7 @@ class RocShim:
         resources = {"cpu_quota": r.cpu_quota, "cpu_period": r.cpu_period, "memory_limit": r.memory_limit_in_bytes,
                      "cpu_shares": r.cpu_shares, "oom_score_adj": r.oom_score_adj, "cpuset": r.cpuset_cpus} if r else {}
         if sandbox_cfg is not None and sandbox_cfg.HasField("linux") and sandbox_cfg.linux.cgroup_parent:
-            resources["cgroup_parent"] = sandbox_cfg.linux.cgroup_parent.strip("/")
+            resources["cgroup_parent"] = self._cgroup_parent(sandbox_cfg.linux.cgroup_parent)
         sc = cfg.linux.security_context if cfg.HasField("linux") and cfg.linux.HasField("security_context") else None
         if image_root:
             resources["rootfs"], resources["workdir"] = image_root, workdir
@@ -886,8 +908,62 @@ class RocShim:
         """The container's writable layer (overlay upper/work and the merged mount point)."""
         return os.path.join(self.state_dir, "rootfs", c.sandbox_id, c.name, ".layer")
 
+    def _sandbox_slice(self, s) -> str:
+        try:
+            cfg = C.PodSandboxConfig.FromString(s.config_bytes)
+            return os.path.basename(self._cgroup_parent(cfg.linux.cgroup_parent)) if cfg.linux.cgroup_parent else ""
+        except Exception:
+            return ""
+
+    def _cgroup_parent(self, parent: str) -> str:
+        """The pod's cgroup as a path under cgroup_root. systemd: a slice name
+        (kubepods-burstable-pod<uid>.slice, as dockershim's ConvertCgroupFsNameToSystemd hands
+        docker) or its expanded form; anything else is refused, as runc's systemd driver does."""
+        if self.cgroup_driver != "systemd":
+            return parent.strip("/")
+        from ..kubelet.cgroups import CgroupError, expand_slice
+        base = os.path.basename(parent.rstrip("/"))
+        if not base.endswith(".slice"):
+            raise CgroupError(f"cgroup parent {parent!r}: the systemd cgroup driver needs a *.slice parent")
+        return expand_slice(base).strip("/")
+
     def _cgroup_of(self, c: Container) -> str:
+        if self.cgroup_driver == "systemd":
+            parent = c.resources.get("cgroup_parent") or "amdkube.slice"
+            return os.path.join(self.cgroup_root, parent, f"amdkube-{c.id}.scope")
         return os.path.join(self.cgroup_root, c.resources.get("cgroup_parent") or c.sandbox_id, c.id)
+
+    def _scope_properties(self, c: Container, pid: int) -> list:
+        """The transient scope of a container (runc's systemd driver: Slice, PIDs, Delegate and
+        the resource limits as unit properties)."""
+        from ..kubelet.cgroups import unit_properties
+        parent = c.resources.get("cgroup_parent") or "amdkube.slice"
+        props = [("Description", ("s", f"amdkube container {c.id}")), ("Slice", ("s", os.path.basename(parent))),
+                 ("PIDs", ("au", [pid])), ("Delegate", ("b", True)), ("MemoryAccounting", ("b", True)),
+                 ("CPUAccounting", ("b", True)), ("DefaultDependencies", ("b", False))]
+        return props + unit_properties({"memory": c.resources.get("memory_limit"),
+                                        "cpu_weight": _shares_to_weight(c.resources["cpu_shares"]) if c.resources.get("cpu_shares") else 0,
+                                        "cpu_quota": c.resources.get("cpu_quota"), "cpu_period": c.resources.get("cpu_period")})
+
+    def _place_in_scope(self, c: Container, pid: int):
+        """systemd driver: the pod slice (started once, with its parents implied by the name),
+        then the container's scope made with the launcher's pid; blocking D-Bus round trips, run
+        off the event loop."""
+        slice_name = os.path.basename(c.resources.get("cgroup_parent") or "amdkube.slice")
+        if slice_name not in self._slices:
+            try:
+                self.systemd.start_transient(slice_name, [("Description", ("s", f"amdkube pod {slice_name}"))])
+            except Exception as e:
+                if "exists" not in str(e):
+                    raise
+            self._slices.add(slice_name)
+        self.systemd.start_transient(f"amdkube-{c.id}.scope", self._scope_properties(c, pid))
+        deadline = time.monotonic() + 5
+        leaf = self._cgroup_of(c)
+        while not os.path.isdir(leaf):
+            if time.monotonic() > deadline:
+                raise RuntimeError(f"systemd did not create {leaf}")
+            time.sleep(0.005)
 
     def _termination_message(self, c: Container) -> str:
         """kuberuntime_container.go getTerminationMessage: the file the container wrote at its
@@ -937,8 +1013,12 @@ class RocShim:
             raise ValueError(f"container {cid} is not in created state")
         self._starting.add(cid)          # the launch below yields the loop: no second start meanwhile
         try:
-            proc = await self._launch(self._launch_argv(c), env=c.env, cwd=c.cwd, log_path=c.log_path,
-                               oom_score_adj=c.resources.get("oom_score_adj") if self.isolation != "namespaces" else None)
+            argv = self._launch_argv(c)
+            if self.cgroup_driver == "systemd" and "--cgroup" in argv:
+                proc = await self._launch_in_scope(c, argv)
+            else:
+                proc = await self._launch(argv, env=c.env, cwd=c.cwd, log_path=c.log_path,
+                                          oom_score_adj=c.resources.get("oom_score_adj") if self.isolation != "namespaces" else None)
         except (OSError, ValueError, RuntimeError) as e:
             c.state, c.exit_code, c.reason, c.message = C.CONTAINER_EXITED, 128, "StartError", str(e)
             c.finished_at = now_ns()
@@ -956,6 +1036,28 @@ class RocShim:
         self._ckpt("containers", c)
         self._emit(c, C.CONTAINER_STARTED_EVENT)
         c.waiter = asyncio.create_task(self._wait(c))
+
+    async def _launch_in_scope(self, c: Container, argv: list[str]):
+        """nsexec waits on a pipe until systemd has put its pid in the container's scope, then
+        joins the scope's cgroup (already its own), applies the limits and execs."""
+        r, w = os.pipe()
+        try:
+            argv = argv[:1] + ["--cgroup-wait-fd", str(r)] + argv[1:]
+            proc = await self._launch(argv, env=c.env, cwd=c.cwd, log_path=c.log_path, pass_fds=(r,))
+        except BaseException:
+            os.close(w)
+            raise
+        finally:
+            os.close(r)
+        try:
+            await asyncio.to_thread(self._place_in_scope, c, proc.pid)
+        except Exception as e:
+            os.close(w)                       # EOF: nsexec refuses to run the container
+            await proc.wait()
+            raise RuntimeError(f"systemd scope for container {c.id}: {e}") from e
+        os.write(w, b"1")
+        os.close(w)
+        return proc
 
     async def _wait(self, c: Container):
         rc = await c.proc.wait()
@@ -1012,6 +1114,11 @@ class RocShim:
         self._unckpt("containers", cid)
         self._emit(c, C.CONTAINER_DELETED_EVENT)
         if self.isolation == "namespaces":
+            if self.systemd is not None:
+                try:
+                    await asyncio.to_thread(self.systemd.stop, f"amdkube-{c.id}.scope")
+                except Exception as e:
+                    log.debug("systemd: stopping the scope of %s: %r", c.id, e)
             try:
                 os.rmdir(self._cgroup_of(c))   # the container's cgroup leaf (empty once it exited)
             except OSError:
@@ -1213,7 +1320,8 @@ class _Runtime:
                  C.RuntimeCondition(type="NetworkReady", status=net_ok, reason="" if net_ok else "NetworkPluginNotReady",
                                     message=net_msg)]
         return C.StatusResponse(status=C.RuntimeStatus(conditions=conds),
-                                info={"isolation": self.r.isolation, "handlers": ",".join(sorted(HANDLERS))} if req.verbose else {})
+                                info={"isolation": self.r.isolation, "handlers": ",".join(sorted(HANDLERS)),
+                                      "cgroupDriver": self.r.cgroup_driver} if req.verbose else {})
 
     def _mark(self, ctx, sid):
         ctx.set_trailing_metadata(((EVENT_TRAILER, self.r.event_mark(sid)),))

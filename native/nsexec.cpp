@@ -7,8 +7,10 @@
 //
 //   amdkube-nsexec [--dev-root /dev] [--keep /dev/dri/renderD128 ...] [--hide-kfd]
 //                  [--cgroup /sys/fs/cgroup/amdkube/<pod>/<ctr>] [--memory-max BYTES] [--cpuset 0-3,8]
-//                  [--cpu-max "QUOTA PERIOD"] -- argv...
+//                  [--cpu-max "QUOTA PERIOD"] [--cgroup-wait-fd N] -- argv...
 //
+//  0. --cgroup-wait-fd N: block until the runtime has placed this process in its cgroup
+//     (systemd driver: a transient scope made with this pid) and writes one byte to fd N;
 //  1. join (creating) a cgroup-v2 leaf and apply memory.max / cpu.max / cpu.weight
 //     (--cpu-weight, from the kubelet's cpu shares) and the OOM score (--oom-score-adj, QoS);
 //  2. unshare a private mount namespace;
@@ -403,6 +405,7 @@ int main(int argc, char** argv) {
   std::string caps, rootfs, rootfs_upper, workdir, user;
   std::string seccomp_profile, apparmor, cpuset, unshare_list, hostname;
   std::vector<std::string> joins, sysctls;
+  int wait_fd = -1;
   int i = 1;
   for (; i < argc; ++i) {
     std::string a = argv[i];
@@ -434,6 +437,7 @@ int main(int argc, char** argv) {
     else if (a == "--hostname" && i + 1 < argc) hostname = argv[++i];
     else if (a == "--join" && i + 1 < argc) joins.push_back(argv[++i]);
     else if (a == "--sysctl" && i + 1 < argc) sysctls.push_back(argv[++i]);
+    else if (a == "--cgroup-wait-fd" && i + 1 < argc) wait_fd = std::atoi(argv[++i]);
     else {
       std::fprintf(stderr, "amdkube-nsexec: unknown argument %s\n", a.c_str());
       return 126;
@@ -452,6 +456,18 @@ int main(int argc, char** argv) {
     std::string err;
     if (!amdkube_seccomp::compile(ss.str(), &filter, &err)) {
       std::fprintf(stderr, "amdkube-nsexec: seccomp profile %s: %s\n", seccomp_profile.c_str(), err.c_str());
+      return 126;
+    }
+  }
+  if (wait_fd >= 0) {
+    // the runtime first places this process in its cgroup (the systemd driver: a transient
+    // scope created with our pid) and then releases it: one byte = placed, EOF = failed
+    char b = 0;
+    ssize_t n;
+    do n = read(wait_fd, &b, 1); while (n < 0 && errno == EINTR);
+    close(wait_fd);
+    if (n != 1) {
+      std::fprintf(stderr, "amdkube-nsexec: the runtime did not place the container in its cgroup\n");
       return 126;
     }
   }
