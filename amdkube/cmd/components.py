@@ -1014,6 +1014,157 @@ def node_problem_detector(argv):
     _run_forever(mk)
 
 
+def cluster_proportional_autoscaler(argv):
+    """cluster/addons/dns-horizontal-autoscaler (clusteraddons/proportional.py)."""
+    ap = argparse.ArgumentParser("amdkube cluster-proportional-autoscaler")
+    ap.add_argument("--server", default="http://127.0.0.1:8080")
+    ap.add_argument("--kubeconfig", default=None)
+    ap.add_argument("--namespace", default=os.environ.get("MY_POD_NAMESPACE", "kube-system"))
+    ap.add_argument("--configmap", required=True, help="ConfigMap holding the linear / ladder params")
+    ap.add_argument("--target", required=True, help="Deployment/<name>, ReplicationController/<name> or ReplicaSet/<name>")
+    ap.add_argument("--default-params", default="", help='JSON, e.g. {"linear":{"coresPerReplica":256,"nodesPerReplica":16}}')
+    ap.add_argument("--poll-period-seconds", type=float, default=10.0)
+    ap.add_argument("--logtostderr", default="true")
+    ap.add_argument("-v", "--v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "cluster-proportional-autoscaler")
+    from ..clusteraddons.proportional import ProportionalAutoscaler
+
+    class _Runner:
+        def __init__(self, pa):
+            self.stop_ev = asyncio.Event()
+            self.task = asyncio.create_task(pa.run(self.stop_ev))
+
+        async def stop(self):
+            self.stop_ev.set()
+            await self.task
+
+    async def mk():
+        return _Runner(ProportionalAutoscaler(_client(a), a.namespace, a.configmap, a.target, a.default_params,
+                                              a.poll_period_seconds))
+    _run_forever(mk)
+
+
+def ip_masq_agent(argv):
+    """cluster/addons/ip-masq-agent (clusteraddons/ipmasq.py)."""
+    ap = argparse.ArgumentParser("amdkube ip-masq-agent")
+    ap.add_argument("--config", default="/etc/config/ip-masq-agent")
+    ap.add_argument("--dry-run", action="store_true", help="render the chain without changing the host's tables")
+    ap.add_argument("-v", "--v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "ip-masq-agent")
+    from ..clusteraddons.ipmasq import MasqAgent
+
+    class _Runner:
+        def __init__(self, agent):
+            self.stop_ev = asyncio.Event()
+            self.task = asyncio.create_task(agent.run(self.stop_ev))
+
+        async def stop(self):
+            self.stop_ev.set()
+            await self.task
+
+    async def mk():
+        return _Runner(MasqAgent(a.config, dry_run=True if a.dry_run else None))
+    _run_forever(mk)
+
+
+def dashboard(argv):
+    """cluster/addons/dashboard (clusteraddons/dashboard.py)."""
+    ap = argparse.ArgumentParser("amdkube dashboard")
+    ap.add_argument("--server", "--apiserver-host", dest="server", default="http://127.0.0.1:8080")
+    ap.add_argument("--kubeconfig", default=None)
+    ap.add_argument("--port", type=int, default=9090, help="HTTP port (kubernetes-dashboard's --insecure-port)")
+    ap.add_argument("--address", default="0.0.0.0")
+    ap.add_argument("--log-store-url", default="", help="the log store for the Logs view, e.g. http://elasticsearch-logging:9200")
+    ap.add_argument("-v", "--v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "dashboard")
+    from aiohttp import web
+    from ..clusteraddons.dashboard import Dashboard
+
+    class _Runner:
+        async def start(self):
+            self.runner = web.AppRunner(Dashboard(_client(a), a.log_store_url).app())
+            await self.runner.setup()
+            await web.TCPSite(self.runner, a.address, a.port).start()
+            return self
+
+        async def stop(self):
+            await self.runner.cleanup()
+
+    async def mk():
+        return await _Runner().start()
+    _run_forever(mk)
+
+
+def log_store(argv):
+    """The elasticsearch-logging service of cluster/addons/fluentd-elasticsearch (clusterlogging/store.py)."""
+    ap = argparse.ArgumentParser("amdkube log-store")
+    ap.add_argument("--data-dir", default="/data")
+    ap.add_argument("--port", type=int, default=9200)
+    ap.add_argument("--address", default="0.0.0.0")
+    ap.add_argument("--retention-days", type=int, default=7)
+    ap.add_argument("-v", "--v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "log-store")
+    from aiohttp import web
+    from ..clusterlogging.store import LogStore, app
+
+    class _Runner:
+        async def start(self):
+            self.store = LogStore(a.data_dir, a.retention_days)
+            self.runner = web.AppRunner(app(self.store))
+            await self.runner.setup()
+            await web.TCPSite(self.runner, a.address, a.port).start()
+            self.task = asyncio.create_task(self._curate())
+            return self
+
+        async def _curate(self):
+            while True:
+                self.store.enforce_retention()
+                await asyncio.sleep(3600)
+
+        async def stop(self):
+            self.task.cancel()
+            await self.runner.cleanup()
+
+    async def mk():
+        return await _Runner().start()
+    _run_forever(mk)
+
+
+def log_shipper(argv):
+    """The fluentd DaemonSet of cluster/addons/fluentd-elasticsearch (clusterlogging/shipper.py)."""
+    ap = argparse.ArgumentParser("amdkube log-shipper")
+    ap.add_argument("--server", default="http://127.0.0.1:8080")
+    ap.add_argument("--kubeconfig", default=None)
+    ap.add_argument("--elasticsearch-url", default="http://elasticsearch-logging:9200")
+    ap.add_argument("--containers-glob", default="/var/log/containers/*.log")
+    ap.add_argument("--component-log", action="append", default=[], help="PATH[:TAG] of a glog-format log, repeatable")
+    ap.add_argument("--pos-file", default="/var/log/amdkube-log-shipper.pos")
+    ap.add_argument("--node-name", default=os.environ.get("NODE_NAME") or socket.gethostname())
+    ap.add_argument("--flush-interval", type=float, default=5.0)
+    ap.add_argument("-v", "--v", type=int, default=0)
+    a = ap.parse_args(argv)
+    klog.setup(a.v, "log-shipper")
+    from ..clusterlogging.shipper import Shipper
+
+    class _Runner:
+        def __init__(self, sh):
+            self.stop_ev = asyncio.Event()
+            self.task = asyncio.create_task(sh.run(self.stop_ev))
+
+        async def stop(self):
+            self.stop_ev.set()
+            await self.task
+
+    async def mk():
+        return _Runner(Shipper(a.elasticsearch_url, a.containers_glob, a.component_log, a.pos_file, _client(a), a.node_name,
+                               flush_interval=a.flush_interval))
+    _run_forever(mk)
+
+
 def exporter(argv):
     ap = argparse.ArgumentParser("amdkube amdgpu-exporter")
     ap.add_argument("--backend", default="auto")
@@ -1303,6 +1454,8 @@ COMPONENTS = {"etcd": etcd, "dns": dns, "kube-dns": dns, "kubeadm": kubeadm, "pr
               "controller-manager": controller_manager, "kube-controller-manager": controller_manager, "kubelet": kubelet,
               "rocshim": rocshim, "amd-device-plugin": device_plugin, "device-plugin": device_plugin,
               "gpu-health": gpu_health, "addon-manager": addon_manager, "node-problem-detector": node_problem_detector,
+              "cluster-proportional-autoscaler": cluster_proportional_autoscaler, "ip-masq-agent": ip_masq_agent,
+              "dashboard": dashboard, "log-store": log_store, "log-shipper": log_shipper,
               "amdgpu-exporter": exporter, "exporter": exporter, "hollow-node": hollow_node, "local-up": local_up,
               "metrics-server": metrics_server, "cloud-controller-manager": cloud_controller_manager,
               "gke-certificates-controller": gke_certificates_controller, "rktshim": rktshim}

@@ -114,6 +114,13 @@ COMPONENT_SYNOPSIS = {
     "gke-certificates-controller": "Signs approved certificate signing requests through an external signing webhook.",
     "rktshim": "CRI runtime that runs pods as rkt pods through the rkt command line.",
     "rocshim": "The CRI runtime: pause sandboxes and process containers with only their GPUs' device nodes.",
+    "cluster-proportional-autoscaler": "Scales a workload (kube-dns) linearly or by ladder steps with the cluster's "
+                                       "nodes, cores and GPUs.",
+    "ip-masq-agent": "Keeps the nat IP-MASQ-AGENT chain: pod traffic to non-masquerade CIDRs keeps its source, the rest "
+                     "is masqueraded.",
+    "dashboard": "Web UI over the cluster: nodes with their MI355X GPUs, workloads, pods with logs, services, events.",
+    "log-store": "The elasticsearch-logging service: an Elasticsearch-compatible bulk/search API over per-day log indices.",
+    "log-shipper": "Tails container and component logs on the node, adds pod metadata and ships them to the log store.",
 }
 
 

@@ -79,6 +79,9 @@ MAX_IMAGES_IN_NODE_STATUS, MAX_NAMES_PER_IMAGE = 50, 5     # kubelet_node_status
 class KubeletConfig:
     node_name: str = field(default_factory=socket.gethostname)
     root_dir: str = "/var/lib/kubelet"
+    # legacy container log symlinks for cluster logging (kuberuntime legacyContainerLogsDir):
+    # "" = /var/log/containers for the default root dir, <root_dir>/containers-logs otherwise
+    container_logs_dir: str = ""
     plugins_dir: str = "/var/lib/kubelet/device-plugin/plugins"
     v1beta1_socket: str | None = None
     cri_socket: str = "/var/run/amdkube/rocshim.sock"
@@ -263,6 +266,9 @@ class Kubelet:
                                       image_pull_burst=config.registry_burst, serialize_image_pulls=config.serialize_image_pulls)
         self.runtime.cpu_cfs_quota = config.cpu_cfs_quota
         self.runtime.cgroup_driver = config.cgroup_driver
+        self.runtime.legacy_logs_dir = config.container_logs_dir or (
+            "/var/log/containers" if os.path.abspath(config.root_dir) == "/var/lib/kubelet"
+            else os.path.join(config.root_dir, "containers-logs"))
         self._node_keyring = None     # credentialprovider.node_keyring, read on first use
         from .checkpoint import PodCheckpointManager
         self.pod_checkpoints = PodCheckpointManager(config.bootstrap_checkpoint_path) \

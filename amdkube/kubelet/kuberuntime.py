@@ -175,6 +175,9 @@ def start_error_reason(e: BaseException) -> tuple[str, str]:
 
 
 class RuntimeManager:
+    cgroup_driver = "cgroupfs"      # --cgroup-driver
+    legacy_logs_dir = ""            # /var/log/containers symlinks (cluster logging); "" = none
+
     def __init__(self, cri: CRIClient, device_manager, root_dir: str, recorder=None, image_pull_qps: float = 0,
                  image_pull_burst: int = 10, serialize_image_pulls: bool = True):
         self.cri = cri
@@ -184,7 +187,6 @@ class RuntimeManager:
         self._pull_sem = asyncio.Semaphore(1) if serialize_image_pulls else None
         self._pull_limiter = TokenBucket(image_pull_qps, image_pull_burst or 1) if image_pull_qps else None
         self.cpu_cfs_quota = True   # --cpu-cfs-quota
-        self.cgroup_driver = "cgroupfs"   # --cgroup-driver
         self.dm = device_manager
         self.root = root_dir
         self.recorder = recorder
@@ -376,6 +378,8 @@ class RuntimeManager:
         POD_TRACE(pod["metadata"]["uid"], "container_created")
         await self.cri.start_container(cid)
         POD_TRACE(pod["metadata"]["uid"], "container_started")
+        if self.legacy_logs_dir:
+            self._legacy_log_link(md, c["name"], cid, os.path.join(sandbox_cfg.log_directory, cfg.log_path))
         post = ((c.get("lifecycle") or {}).get("postStart"))
         if post:
             # kuberuntime_container.go startContainer step 4: a failing postStart hook kills the container
@@ -386,6 +390,42 @@ class RuntimeManager:
                 await self.cri.stop_container(cid, 0)
                 raise StartError("PostStartHookError", str(err))
         return cid
+
+    def legacy_log_symlink(self, pod_name: str, namespace: str, container: str, cid: str) -> str:
+        """kuberuntime_container.go legacyLogSymlink / logSymlink: `<pod>_<ns>_<container>-<id>.log`,
+        cut to ext4's 255-byte file name limit."""
+        name = f"{pod_name}_{namespace}_{container}-{cid}"[:255 - len(".log")]
+        return os.path.join(self.legacy_logs_dir, name + ".log")
+
+    def _legacy_log_link(self, md: dict, container: str, cid: str, target: str):
+        """startContainer: symlink the container's log into the legacy directory the cluster
+        logging agent tails (a failure is logged, never fatal — as the reference)."""
+        link = self.legacy_log_symlink(md["name"], md.get("namespace", ""), container, cid)
+        try:
+            os.makedirs(self.legacy_logs_dir, exist_ok=True)
+            if os.path.lexists(link):
+                os.unlink(link)
+            os.symlink(target, link)
+        except OSError as e:
+            log.warning("failed to create legacy symbolic link %s to container %s log %s: %r", link, cid, target, e)
+
+    def remove_legacy_log_links(self, cid: str | None = None) -> int:
+        """The container's symlink (removeContainerLog), or — cid None — every dangling one
+        (container_gc.go: dead symlinks left by containers removed elsewhere)."""
+        if not self.legacy_logs_dir or not os.path.isdir(self.legacy_logs_dir):
+            return 0
+        n = 0
+        for f in os.listdir(self.legacy_logs_dir):
+            p = os.path.join(self.legacy_logs_dir, f)
+            if not f.endswith(".log") or not os.path.islink(p):
+                continue
+            if (cid is not None and f.endswith(f"-{cid}.log")) or (cid is None and not os.path.exists(p)):
+                try:
+                    os.unlink(p)
+                    n += 1
+                except OSError:
+                    pass
+        return n
 
     async def run_handler(self, pod, c, cid, handler: dict, pod_ip: str, timeout: int = 30) -> str:
         """lifecycle/handlers.go HandlerRunner: exec in the container or HTTP GET; '' on success."""
@@ -614,6 +654,8 @@ class RuntimeManager:
                     os.unlink(log_path)
                 except OSError:
                     pass
+            self.remove_legacy_log_links(c.id)
+        self.remove_legacy_log_links()
         left = {c.pod_sandbox_id for c in conts if c.id not in gone}
         by_uid: dict[str, list] = {}
         for s in sbs:
