@@ -203,106 +203,16 @@ int __openat64_2(int dirfd, const char* path, int flags) {
 
 /* stdio opens go through glibc-internal open calls the preload cannot see */
 typedef FILE* (*fopen_fn)(const char*, const char*);
-
-/* KFD topology of the GPUs the container was not given. ROCr's thunk snapshots every topology
- * node at hsa_init: the node's properties, then one properties file per cache it lists (an
- * MI355X GPU node lists ~540; the 8-GPU host ~4,400 files, most of hsa_init's 26 ms topology
- * snapshot). A GPU whose render node is absent from the container's view is skipped by ROCr
- * after that snapshot, so its node properties are served with `caches_count 0` and the cache
- * reads never happen. Only foreign GPU nodes change; AMDKUBE_DEVVIEW_TOPOLOGY=full turns it off,
- * AMDKUBE_DEVVIEW_KFD_TOPOLOGY moves the topology root (tests). */
-struct memfile { char* buf; size_t len, off; };
-static ssize_t mem_read(void* c, char* out, size_t n) {
-  struct memfile* m = c;
-  size_t k = m->len - m->off;
-  if (k > n) k = n;
-  memcpy(out, m->buf + m->off, k);
-  m->off += k;
-  return (ssize_t)k;
-}
-static int mem_seek(void* c, off64_t* pos, int whence) {
-  struct memfile* m = c;
-  off64_t base = whence == SEEK_SET ? 0 : whence == SEEK_CUR ? (off64_t)m->off : (off64_t)m->len;
-  if (base + *pos < 0 || base + *pos > (off64_t)m->len) { errno = EINVAL; return -1; }
-  m->off = (size_t)(base + *pos);
-  *pos = (off64_t)m->off;
-  return 0;
-}
-static int mem_close(void* c) {
-  struct memfile* m = c;
-  free(m->buf);
-  free(m);
-  return 0;
-}
-
-static long prop_value(const char* text, const char* key) {
-  size_t kl = strlen(key);
-  for (const char* p = text; p && *p; p = strchr(p, '\n') ? strchr(p, '\n') + 1 : NULL)
-    if (strncmp(p, key, kl) == 0 && p[kl] == ' ') return strtol(p + kl + 1, NULL, 10);
-  return -1;
-}
-
-static FILE* foreign_gpu_node(const char* path, const char* mode, fopen_fn real) {
-  const char* allow = getenv("AMDKUBE_DEVVIEW_ALLOW");
-  const char* opt = getenv("AMDKUBE_DEVVIEW_TOPOLOGY");
-  if (g_off || !allow || (opt && strcmp(opt, "full") == 0) || !path || mode[0] != 'r' || strchr(mode, '+')) return NULL;
-  const char* topo = getenv("AMDKUBE_DEVVIEW_KFD_TOPOLOGY");
-  if (!topo || !*topo) topo = "/sys/devices/virtual/kfd/kfd/topology";
-  size_t tl = strlen(topo);
-  if (strncmp(path, topo, tl) != 0 || strncmp(path + tl, "/nodes/", 7) != 0) return NULL;
-  const char* p = path + tl + 7;
-  if (*p < '0' || *p > '9') return NULL;
-  while (*p >= '0' && *p <= '9') p++;
-  if (strcmp(p, "/properties") != 0) return NULL;
-  FILE* f = real(path, mode);
-  if (!f) return NULL;
-  size_t cap = 16384, len = 0;
-  char* buf = malloc(cap + 1);
-  if (!buf) return f;
-  len = fread(buf, 1, cap, f);
-  fclose(f);
-  buf[len] = 0;
-  long minor = prop_value(buf, "drm_render_minor"), simd = prop_value(buf, "simd_count");
-  char* cc = NULL;
-  for (char* q = buf; q && *q; q = strchr(q, '\n') ? strchr(q, '\n') + 1 : NULL)
-    if (strncmp(q, "caches_count ", 13) == 0) { cc = q; break; }
-  if (simd > 0 && minor > 0 && cc) {
-    size_t rl;
-    const char* root = dev_root(&rl);
-    char node[PATH_MAX];
-    snprintf(node, sizeof node, "%.*s/dri/renderD%ld", (int)rl, root, minor);
-    if (!listed(allow, node)) {
-      char* v = cc + 13;
-      char* end = v;
-      while (*end >= '0' && *end <= '9') end++;
-      if (end > v) {                       /* "caches_count N" -> "caches_count 0" */
-        memmove(v + 1, end, len - (size_t)(end - buf) + 1);
-        *v = '0';
-        len -= (size_t)(end - v) - 1;
-      }
-    }
-  }
-  struct memfile* m = malloc(sizeof *m);
-  if (!m) { free(buf); return real(path, mode); }
-  m->buf = buf, m->len = len, m->off = 0;
-  cookie_io_functions_t io = {mem_read, NULL, mem_seek, mem_close};
-  FILE* out = fopencookie(m, "r", io);
-  if (!out) { free(buf); free(m); return real(path, mode); }
-  return out;
-}
-
 FILE* fopen(const char* path, const char* mode) {
   REAL(fopen, fopen_fn);
   if (hidden(path)) { errno = ENOENT; return NULL; }
-  FILE* f = foreign_gpu_node(path, mode, real_fopen);
-  return f ? f : real_fopen(path, mode);
+  return real_fopen(path, mode);
 }
 
 FILE* fopen64(const char* path, const char* mode) {
   REAL(fopen64, fopen_fn);
   if (hidden(path)) { errno = ENOENT; return NULL; }
-  FILE* f = foreign_gpu_node(path, mode, real_fopen64);
-  return f ? f : real_fopen64(path, mode);
+  return real_fopen64(path, mode);
 }
 
 /* stat-family probes of a hidden node agree with open: it does not exist */

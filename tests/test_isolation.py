@@ -271,53 +271,3 @@ def test_devview_libdrm_style_enumeration_sees_only_its_own_node(fake_dev, tmp_p
     r = json.loads(p.stdout)
     assert r["probe"]["renderD128"]["open"] == "Permission denied"
     assert len(r["readdir"]) == 17
-
-
-_FOPEN_READ = r"""
-import ctypes, json, sys
-libc = ctypes.CDLL(None)
-libc.fopen.restype = ctypes.c_void_p
-libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
-libc.fread.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]
-libc.fseek.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_int]
-libc.fclose.argtypes = [ctypes.c_void_p]
-out = {}
-for path in sys.argv[1:]:
-    f = libc.fopen(path.encode(), b"r")
-    buf = ctypes.create_string_buffer(8192)
-    n = libc.fread(buf, 1, 8191, f)
-    libc.fseek(f, 0, 0)                      # the thunk may re-read: seeking works on the copy
-    n2 = libc.fread(buf, 1, 8191, f)
-    libc.fclose(f)
-    assert n == n2
-    out[path] = buf.raw[:n].decode()
-print(json.dumps(out))
-"""
-
-
-def test_devview_trims_the_topology_of_foreign_gpus(fake_dev, tmp_path):
-    """A foreign GPU's KFD topology node reports no caches, so ROCr's thunk skips reading its
-    ~540 cache properties files at hsa_init; the container's own GPU and CPU nodes are untouched."""
-    if not os.path.exists(DEVVIEW_LIB):
-        pytest.skip("devview preload not built")
-    topo = tmp_path / "topology"
-    nodes = {0: "cpu_cores_count 96\nsimd_count 0\ncaches_count 12\ndrm_render_minor 0\n",
-             1: "cpu_cores_count 0\nsimd_count 1024\ncaches_count 542\nio_links_count 8\ndrm_render_minor 128\n",
-             2: "cpu_cores_count 0\nsimd_count 1024\ncaches_count 542\nio_links_count 8\ndrm_render_minor 129\n"}
-    for i, text in nodes.items():
-        (topo / "nodes" / str(i)).mkdir(parents=True)
-        (topo / "nodes" / str(i) / "properties").write_text(text)
-    (topo / "nodes" / "1" / "gpu_id").write_text("1234\n")
-    env = dict(os.environ, LD_PRELOAD=DEVVIEW_LIB, AMDKUBE_DEVVIEW_ROOT=fake_dev,
-               AMDKUBE_DEVVIEW_ALLOW=os.path.join(fake_dev, "dri", "renderD129"), AMDKUBE_DEVVIEW_KFD_TOPOLOGY=str(topo))
-    paths = [str(topo / "nodes" / str(i) / "properties") for i in nodes] + [str(topo / "nodes" / "1" / "gpu_id")]
-    r = subprocess.run([sys.executable, "-c", _FOPEN_READ, *paths], env=env, capture_output=True, text=True, timeout=60)
-    assert r.returncode == 0, r.stderr
-    got = json.loads(r.stdout)
-    assert got[paths[0]] == nodes[0]                                          # a CPU node is untouched
-    assert got[paths[1]] == nodes[1].replace("caches_count 542", "caches_count 0")   # renderD128: not given
-    assert got[paths[2]] == nodes[2]                                          # the container's own GPU
-    assert got[paths[3]] == "1234\n"                                          # other topology files pass through
-    r = subprocess.run([sys.executable, "-c", _FOPEN_READ, paths[1]], env=dict(env, AMDKUBE_DEVVIEW_TOPOLOGY="full"),
-                       capture_output=True, text=True, timeout=60)
-    assert json.loads(r.stdout)[paths[1]] == nodes[1]
