@@ -336,3 +336,10 @@ def test_update_pod_enqueues_by_membership_and_change():
     new["metadata"]["labels"] = {"app": "b"}
     c._pod_update(old, new)                                   # moved from s1 to s2: both
     assert {run(c.queue.get()) for _ in range(2)} == {"ns/s1", "ns/s2"}
+
+
+def test_pack_subsets_not_ready_trumps_ready_in_either_order():
+    """mapAddressByPort keeps not-ready once seen, whichever subset came first."""
+    nr_first = [{"notReadyAddresses": [{"ip": "1.2.3.4"}], "ports": [{"port": 111}]},
+                {"addresses": [{"ip": "1.2.3.4"}], "ports": [{"port": 111}]}]
+    assert N.repack_subsets(nr_first) == [{"notReadyAddresses": [{"ip": "1.2.3.4"}], "ports": [{"port": 111}]}]
