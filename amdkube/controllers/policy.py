@@ -1,12 +1,15 @@
 """Disruption budgets, resource-quota usage, node TTL and ClusterRole aggregation.
 
 Reference:
-  * pkg/controller/disruption/disruption.go — for every PodDisruptionBudget: expectedPods
-    from the pods' controllers' scale (or the matching pod count), desiredHealthy from
-    minAvailable / maxUnavailable (int or percent, rounded up), currentHealthy = ready
-    matching pods not being deleted, disruptionsAllowed = max(currentHealthy -
-    desiredHealthy, 0) minus pods evicted (status.disruptedPods) but not yet gone; entries
-    older than 2 min expire.
+  * pkg/controller/disruption/disruption.go — for every PodDisruptionBudget (an empty selector
+    selects no pods): expectedPods from the scale of the pods' controllers, each found by UID
+    (ReplicaSet, Deployment through its ReplicaSet, ReplicationController, StatefulSet) for a
+    percentage minAvailable or any maxUnavailable, else the matching pod count; desiredHealthy
+    from minAvailable / maxUnavailable (rounded up); currentHealthy = ready matching pods not
+    being deleted and not recently evicted (status.disruptedPods, kept 2 min, the budget
+    rechecked when the first expires); disruptionsAllowed = currentHealthy - desiredHealthy,
+    0 when negative or no pods are expected. A pod without a known controller makes the sync
+    fail safe: the old status with disruptionsAllowed 0.
   * pkg/controller/resourcequota/resource_quota_controller.go over amdkube.quota (the
     pkg/quota/evaluator/core evaluators): status.used for pods (compute, requests.*, limits.*,
     scopes), services (nodeports, loadbalancers), PVCs (storage, per StorageClass) and object
@@ -27,28 +30,38 @@ from ..api.helpers import is_pod_ready, is_pod_terminal
 from ..api.labels import selector_from_label_selector
 from .base import Controller, split_key
 
-DISRUPTED_TIMEOUT = 120.0
+DISRUPTED_TIMEOUT = 120.0          # DeletionTimeout: an evicted pod not gone by then counts again
 
 
 def _int_or_percent(v, total: int, round_up: bool = True) -> int:
+    """intstr.GetValueFromIntOrPercent."""
     if isinstance(v, str) and v.endswith("%"):
         f = float(v[:-1]) * total / 100.0
         return int(math.ceil(f) if round_up else math.floor(f))
     return int(v)
 
 
+class _NoController(Exception):
+    pass
+
+
 class DisruptionController(Controller):
+    """pkg/controller/disruption/disruption.go."""
     name = "disruption"
 
     def setup(self):
         f = self.mgr.factory
         self.pdb_inf = f.informer("poddisruptionbudgets")
         self.pod_inf = self.mgr.pods
-        self.scale_infs = {k: f.informer(p) for k, p in (("ReplicaSet", "replicasets"), ("Deployment", "deployments"),
-                                                          ("StatefulSet", "statefulsets"),
-                                                          ("ReplicationController", "replicationcontrollers"))}
+        self.rc_inf, self.rs_inf = f.informer("replicationcontrollers"), f.informer("replicasets")
+        self.d_inf, self.ss_inf = f.informer("deployments"), f.informer("statefulsets")
         self.pdb_inf.add_handler(on_add=self.enqueue, on_update=lambda o, n: self.enqueue(n), on_delete=lambda o: None)
         self.pod_inf.add_handler(on_add=self._pod, on_update=lambda o, n: self._pod(n), on_delete=self._pod)
+
+    def _event(self, obj, etype, reason, msg):
+        rec = getattr(self.mgr, "recorder", None)
+        if rec is not None:
+            rec.event(obj, etype, reason, msg)
 
     def _pod(self, pod):
         labels = m.labels_of(pod)
@@ -58,72 +71,145 @@ class DisruptionController(Controller):
 
     @staticmethod
     def _selects(pdb, labels) -> bool:
+        """getPodsForPdb: an empty selector selects nothing."""
         sel = (pdb.get("spec") or {}).get("selector")
-        return bool(sel) and selector_from_label_selector(sel).matches(labels)
+        return bool(sel) and bool(sel.get("matchLabels") or sel.get("matchExpressions")) and \
+            selector_from_label_selector(sel).matches(labels)
 
-    def _expected(self, pods) -> int:
-        """getExpectedScale: the sum of the controllers' replicas (a Deployment owns through its RS)."""
-        seen, total = set(), 0
+    # ---------------------------------------------------------------- finders
+    def _owner(self, inf, ns, ref):
+        o = inf.get(f"{ns}/{ref.get('name')}")
+        return o if o is not None and m.uid_of(o) == ref.get("uid") else None
+
+    def _finders(self, ref, ns):
+        """finders(): (uid, scale) of the pod's controller, if it is one of the supported kinds.
+        A ReplicaSet owned by a Deployment is answered by the Deployment finder."""
+        kind = ref.get("kind")
+        if kind == "ReplicaSet":
+            rs = self._owner(self.rs_inf, ns, ref)
+            if rs is None:
+                return None
+            dref = m.controller_ref(rs)
+            if dref is None:
+                return m.uid_of(rs), int((rs.get("spec") or {}).get("replicas", 1))
+            if dref.get("kind") == "Deployment":
+                d = self._owner(self.d_inf, ns, dref)
+                if d is not None:
+                    return m.uid_of(d), int((d.get("spec") or {}).get("replicas", 1))
+            return None
+        for k, inf in (("ReplicationController", self.rc_inf), ("StatefulSet", self.ss_inf)):
+            if kind == k:
+                o = self._owner(inf, ns, ref)
+                return (m.uid_of(o), int((o.get("spec") or {}).get("replicas", 1))) if o is not None else None
+        return None
+
+    def expected_scale(self, pdb, pods) -> int:
+        """getExpectedScale: the sum of the scales of the pods' controllers, each counted once."""
+        scale: dict[str, int] = {}
         for p in pods:
             ref = m.controller_ref(p)
-            if not ref:
-                return -1
-            key = (ref.get("kind"), m.namespace_of(p), ref.get("name"))
-            if key in seen:
+            if ref is None:
+                msg = f'found no controller ref for pod "{m.name_of(p)}"'
+                self._event(pdb, "Warning", "NoControllerRef", msg)
+                raise _NoController(msg)
+            if ref.get("uid") in scale:
                 continue
-            seen.add(key)
-            inf = self.scale_infs.get(ref.get("kind"))
-            owner = inf.get(f"{m.namespace_of(p)}/{ref.get('name')}") if inf else None
-            if owner is None:
-                return -1
-            dref = m.controller_ref(owner) if ref.get("kind") == "ReplicaSet" else None
-            if dref and dref.get("kind") == "Deployment":
-                d = self.scale_infs["Deployment"].get(f"{m.namespace_of(p)}/{dref.get('name')}")
-                if d is not None and ("Deployment", m.namespace_of(p), dref.get("name")) not in seen:
-                    seen.add(("Deployment", m.namespace_of(p), dref.get("name")))
-                    total += int((d.get("spec") or {}).get("replicas", 1))
+            found = self._finders(ref, m.namespace_of(p))
+            if found is None:
+                msg = f'found no controllers for pod "{m.name_of(p)}"'
+                self._event(pdb, "Warning", "NoControllers", msg)
+                raise _NoController(msg)
+            scale[found[0]] = found[1]
+        return sum(scale.values())
+
+    def expected_pod_count(self, pdb, pods) -> tuple[int, int]:
+        """getExpectedPodCount -> (expectedCount, desiredHealthy)."""
+        spec = pdb.get("spec") or {}
+        if spec.get("maxUnavailable") is not None:
+            expected = self.expected_scale(pdb, pods)
+            return expected, max(0, expected - _int_or_percent(spec["maxUnavailable"], expected))
+        mina = spec.get("minAvailable")
+        if mina is None:
+            return 0, 0
+        if isinstance(mina, str):
+            expected = self.expected_scale(pdb, pods)
+            return expected, _int_or_percent(mina, expected)
+        return len(pods), int(mina)
+
+    def disrupted_pod_map(self, pods, pdb, now: float) -> tuple[dict, float | None]:
+        """buildDisruptedPodMap: evictions of pods still present and not yet being deleted, within
+        the deletion timeout; and the earliest time one of them expires (to recheck then)."""
+        old = (pdb.get("status") or {}).get("disruptedPods") or {}
+        result, recheck = {}, None
+        if not old:
+            return result, recheck
+        for p in pods:
+            if (p.get("metadata") or {}).get("deletionTimestamp") or m.name_of(p) not in old:
                 continue
-            total += int((owner.get("spec") or {}).get("replicas", 1))
-        return total
+            t = m.parse_time(old[m.name_of(p)]) or 0
+            if t + DISRUPTED_TIMEOUT < now:
+                self._event(p, "Warning", "NotDeleted",
+                            f"Pod was expected by PDB {m.namespace_of(pdb)}/{m.name_of(pdb)} to be deleted but it wasn't")
+                continue
+            result[m.name_of(p)] = old[m.name_of(p)]
+            recheck = t + DISRUPTED_TIMEOUT if recheck is None else min(recheck, t + DISRUPTED_TIMEOUT)
+        return result, recheck
+
+    @staticmethod
+    def count_healthy(pods, disrupted: dict, now: float) -> int:
+        """countHealthyPods: ready pods not being deleted and not expected to be deleted soon."""
+        n = 0
+        for p in pods:
+            if (p.get("metadata") or {}).get("deletionTimestamp"):
+                continue
+            t = disrupted.get(m.name_of(p))
+            if t is not None and (m.parse_time(t) or 0) + DISRUPTED_TIMEOUT > now:
+                continue
+            if is_pod_ready(p):
+                n += 1
+        return n
+
+    async def _update(self, pdb, status: dict):
+        body = dict(pdb, status=status)
+        try:
+            await self.client.update(body, sub="status")   # CAS on resourceVersion vs concurrent evictions
+        except m.StatusError as e:
+            if not m.is_conflict(e):
+                raise
+            self.enqueue(m.key_of(pdb))
 
     async def sync(self, key):
         pdb = self.pdb_inf.get(key)
         if pdb is None:
             return
-        ns, name = split_key(key)
-        spec, old = pdb.get("spec") or {}, pdb.get("status") or {}
+        try:
+            await self._try_sync(pdb)
+        except _NoController:
+            # failSafe: the budget's last status stands, but nothing may be disrupted
+            await self._update(pdb, dict(pdb.get("status") or {}, disruptionsAllowed=0))
+
+    async def _try_sync(self, pdb):
+        ns = m.namespace_of(pdb)
         pods = [p for p in self.pod_inf.list() if m.namespace_of(p) == ns and self._selects(pdb, m.labels_of(p))]
-        healthy = sum(1 for p in pods if is_pod_ready(p) and not (p.get("metadata") or {}).get("deletionTimestamp")
-                      and not is_pod_terminal(p))
-        if "maxUnavailable" in spec:
-            expected = self._expected(pods)
-            if expected < 0:
-                expected = len(pods)
-            desired = max(0, expected - _int_or_percent(spec["maxUnavailable"], expected))
-        else:
-            mina = spec.get("minAvailable", 1)
-            if isinstance(mina, str) and mina.endswith("%"):
-                expected = self._expected(pods)
-                if expected < 0:
-                    expected = len(pods)
-                desired = _int_or_percent(mina, expected)
-            else:
-                expected, desired = len(pods), int(mina)
+        if not pods:
+            self._event(pdb, "Normal", "NoPods", "No matching pods found")
+        expected, desired = self.expected_pod_count(pdb, pods)
         now = time.time()
-        live = {m.name_of(p) for p in pods if not (p.get("metadata") or {}).get("deletionTimestamp")}
-        disrupted = {k: v for k, v in (old.get("disruptedPods") or {}).items()
-                     if k in live and now - (m.parse_time(v) or 0) < DISRUPTED_TIMEOUT}
-        allowed = max(0, healthy - desired - len(disrupted))
+        disrupted, recheck = self.disrupted_pod_map(pods, pdb, now)
+        healthy = self.count_healthy(pods, disrupted, now)
+        allowed = healthy - desired
+        if expected <= 0 or allowed <= 0:
+            allowed = 0
+        old = pdb.get("status") or {}
         st = {"currentHealthy": healthy, "desiredHealthy": desired, "expectedPods": expected, "disruptionsAllowed": allowed,
-              "disruptedPods": disrupted, "observedGeneration": (pdb.get("metadata") or {}).get("generation", 1)}
-        if {k: old.get(k) for k in st} != st:
-            body = dict(pdb, status=st)
-            try:
-                await self.client.update(body, sub="status")   # CAS on resourceVersion vs concurrent evictions
-            except m.StatusError as e:
-                if not m.is_conflict(e):
-                    raise
-                self.enqueue(key)
+              "disruptedPods": disrupted, "observedGeneration": (pdb.get("metadata") or {}).get("generation", 0)}
+        # a status never written (fields absent) is always written, as the reference's nil
+        # DisruptedPods never DeepEquals the computed map
+        if any(k not in old for k in st if k != "disruptedPods") or \
+                {k: (old.get(k) or {}) if k == "disruptedPods" else old.get(k) for k in st} != st:
+            await self._update(pdb, st)
+        if recheck is not None:
+            self.queue.add_after(m.key_of(pdb), max(0.0, recheck - now))
 
 
 # ------------------------------------------------------------------------ quota usage
