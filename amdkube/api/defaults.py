@@ -199,6 +199,25 @@ register_hooks("Deployment", "apps/v1", defaulter=default_deployment)
 register_hooks("Job", "batch/v1", defaulter=default_job)
 
 
+def default_cronjob(cj: dict, history_limits: bool = True):
+    """SetDefaults_CronJob (batch/v1beta1/defaults.go): concurrency Allow, not suspended, and
+    3 successful / 1 failed finished jobs kept (batch/v2alpha1 leaves the limits unset)."""
+    spec = cj.setdefault("spec", {})
+    spec.setdefault("concurrencyPolicy", "Allow")
+    spec.setdefault("suspend", False)
+    if history_limits:
+        spec.setdefault("successfulJobsHistoryLimit", 3)
+        spec.setdefault("failedJobsHistoryLimit", 1)
+    return cj
+
+
+for _gv, _limits in (("batch/v1beta1", True), ("batch/v2alpha1", False)):
+    try:
+        register_hooks("CronJob", _gv, defaulter=lambda cj, _l=_limits: default_cronjob(cj, _l))
+    except KeyError:
+        pass
+
+
 def default_pod_security_policy(psp: dict):
     """SetDefaults_PodSecurityPolicySpec (extensions/v1beta1/defaults.go): privilege escalation
     is allowed unless the policy says otherwise."""

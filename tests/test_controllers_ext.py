@@ -259,7 +259,8 @@ async def test_cronjob_creates_jobs_and_forbids_overlap():
         assert len(await jobs()) == 1     # Forbid: the first job is still active
         cj = await c.get("cronjobs", "tick", "default")
         assert cj["status"]["active"][0]["name"] == m.name_of(js[0]) and cj["status"]["lastScheduleTime"]
-        assert js[0]["metadata"]["annotations"]["cronjob.kubernetes.io/scheduled-time"]
+        # getJobFromTemplate: the name carries the scheduled time (getTimeHash: Unix seconds)
+        assert m.name_of(js[0]) == f"tick-{int(m.parse_time(cj['status']['lastScheduleTime']))}"
         await c.patch("cronjobs", "tick", {"spec": {"concurrencyPolicy": "Replace"}}, "default")
         first = m.uid_of(js[0])
 
