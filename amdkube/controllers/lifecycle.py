@@ -10,12 +10,15 @@ finalizers), pkg/controller/podgc (terminated-pod threshold, orphaned pods on de
 from __future__ import annotations
 
 import asyncio
+import logging
 import time
 
 from ..api import meta as m
 from ..api.helpers import get_condition, is_pod_terminal, tolerations_tolerate_taint
 from ..api.scheme import SCHEME
 from .base import Controller
+
+log = logging.getLogger("amdkube.controllers.lifecycle")
 
 UNREACHABLE_TAINT = {"key": "node.kubernetes.io/unreachable", "effect": "NoExecute"}
 NOT_READY_TAINT = {"key": "node.kubernetes.io/not-ready", "effect": "NoExecute"}
@@ -429,6 +432,10 @@ class GarbageCollector(Controller):
 
 
 class PodGCController(Controller):
+    """pkg/controller/podgc/gc_controller.go: every gcCheckPeriod (20 s) terminated pods beyond
+    --terminated-pod-gc-threshold (oldest first; 0 disables this step), pods bound to nodes that
+    no longer exist (checked against a fresh node list) and unscheduled pods that are being
+    deleted are force-deleted."""
     name = "podgc"
 
     def __init__(self, mgr, threshold: int = 12500, period: float = 20.0):     # --terminated-pod-gc-threshold
@@ -437,7 +444,6 @@ class PodGCController(Controller):
 
     def setup(self):
         self.pods = self.mgr.pods
-        self.nodes = self.mgr.nodes
 
     async def start(self):
         self.tasks.append(asyncio.create_task(self._loop()))
@@ -446,25 +452,55 @@ class PodGCController(Controller):
         while True:
             await asyncio.sleep(self.period)
             try:
-                await self.gc_once()
-            except Exception:
-                pass
+                await self.gc()
+            except Exception as e:
+                log.debug("podgc: %r", e)
 
-    async def gc_once(self):
+    async def delete_pod(self, ns: str, name: str):
+        await self.client.delete("pods", name, ns, grace=0)
+
+    async def _delete(self, p):
+        try:
+            await self.delete_pod(m.namespace_of(p), m.name_of(p))
+        except m.StatusError as e:
+            if not m.is_not_found(e):
+                log.debug("podgc: deleting %s: %r", m.key_of(p), e)
+
+    @staticmethod
+    def is_pod_terminated(pod) -> bool:
+        return (pod.get("status") or {}).get("phase", "") not in ("Pending", "Running", "Unknown")
+
+    async def gc(self):
         pods = self.pods.list()
-        term = sorted([p for p in pods if is_pod_terminal(p)], key=lambda p: (p.get("metadata") or {}).get("creationTimestamp", ""))
-        for p in term[:max(0, len(term) - self.threshold)]:
-            await self.client.delete("pods", m.name_of(p), m.namespace_of(p), grace=0)
-        nodes = {m.name_of(n) for n in self.nodes.list()}
-        if not self.nodes.has_synced():
+        if self.threshold > 0:
+            await self.gc_terminated(pods)
+        await self.gc_orphaned(pods)
+        await self.gc_unscheduled_terminating(pods)
+
+
+    async def gc_terminated(self, pods):
+        term = [p for p in pods if self.is_pod_terminated(p)]
+        term.sort(key=lambda p: (m.parse_time((p.get("metadata") or {}).get("creationTimestamp")) or 0.0, m.name_of(p)))
+        n = len(term) - self.threshold
+        if n > 0:
+            await asyncio.gather(*(self._delete(p) for p in term[:n]))
+
+    async def gc_orphaned(self, pods):
+        try:
+            nodes, _ = await self.client.list("nodes")
+        except Exception as e:
+            log.debug("podgc: listing nodes: %r", e)
             return
+        names = {m.name_of(n) for n in nodes}
         for p in pods:
             nn = (p.get("spec") or {}).get("nodeName")
-            if nn and nn not in nodes:
-                try:
-                    await self.client.delete("pods", m.name_of(p), m.namespace_of(p), grace=0)
-                except m.StatusError:
-                    pass
+            if nn and nn not in names:
+                await self._delete(p)
+
+    async def gc_unscheduled_terminating(self, pods):
+        for p in pods:
+            if (p.get("metadata") or {}).get("deletionTimestamp") and not (p.get("spec") or {}).get("nodeName"):
+                await self._delete(p)
 
     async def sync(self, key):
         pass

@@ -16,7 +16,8 @@ Reference:
     counts; status.hard mirrors spec.hard. Extended resources (amd.com/gpu) count from the
     device-granular spec.extendedResources too.
   * pkg/controller/ttl/ttl_controller.go — node annotation node.alpha.kubernetes.io/ttl from
-    cluster size (0 s up to 100 nodes, 15 ≤ 500, 30 ≤ 1000, 60 ≤ 2000, 300 ≤ 5000, else 600).
+    cluster size with hysteresis (0 s up to 100 nodes, 15 s from 90 to 500, 30 s 450-1000, 60 s
+    900-2000, 300 s 1800-10000, then 600 s).
   * pkg/controller/clusterroleaggregation — a ClusterRole with aggregationRule gets the union
     of the rules of every ClusterRole its clusterRoleSelectors match.
 """
@@ -275,37 +276,70 @@ class ResourceQuotaController(Controller):
 
 # --------------------------------------------------------------------------- node TTL
 TTL_ANNOTATION = "node.alpha.kubernetes.io/ttl"
-TTL_BOUNDARIES = ((100, 0), (500, 15), (1000, 30), (2000, 60), (5000, 300))
+# ttlBoundaries: overlapping (sizeMin, sizeMax, ttl) steps; the step moves up only when the node
+# count passes sizeMax and down only when it falls under sizeMin (hysteresis)
+TTL_BOUNDARIES = ((0, 100, 0), (90, 500, 15), (450, 1000, 30), (900, 2000, 60), (1800, 10000, 300),
+                  (9000, 2**31 - 1, 600))
 
 
 def ttl_for(nodes: int) -> int:
-    for limit, ttl in TTL_BOUNDARIES:
-        if nodes <= limit:
+    """The TTL a cluster grown from empty to `nodes` nodes settles on."""
+    for _lo, hi, ttl in TTL_BOUNDARIES:
+        if nodes <= hi:
             return ttl
-    return 600
+    return TTL_BOUNDARIES[-1][2]
 
 
 class TTLController(Controller):
+    """pkg/controller/ttl/ttl_controller.go: the node annotation node.alpha.kubernetes.io/ttl (how
+    long kubelets may cache secrets / config maps) follows cluster size with hysteresis."""
     name = "ttl"
     workers = 1
 
+    def __init__(self, mgr):
+        super().__init__(mgr)
+        self.node_count, self.boundary_step, self.desired_ttl = 0, 0, 0
+
     def setup(self):
         self.node_inf = self.mgr.nodes
-        self.node_inf.add_handler(on_add=lambda n: self._all(), on_update=lambda o, n: self.enqueue(n),
-                                  on_delete=lambda n: self._all())
+        self.node_inf.add_handler(on_add=self.add_node, on_update=lambda o, n: self.enqueue(n), on_delete=self.delete_node)
 
-    def _all(self):
-        for n in self.node_inf.list():
-            self.enqueue(n)
+    def add_node(self, node):
+        self.node_count += 1
+        if self.node_count > TTL_BOUNDARIES[self.boundary_step][1]:
+            self.boundary_step += 1
+            self.desired_ttl = TTL_BOUNDARIES[self.boundary_step][2]
+            for n in self.node_inf.list():      # every node's annotation changes with the step
+                self.enqueue(n)
+        if m.name_of(node):
+            self.enqueue(node)
 
-    async def sync(self, key):
-        _, name = split_key(key)
+    def delete_node(self, node):
+        self.node_count -= 1
+        if self.node_count < TTL_BOUNDARIES[self.boundary_step][0]:
+            self.boundary_step -= 1
+            self.desired_ttl = TTL_BOUNDARIES[self.boundary_step][2]
+            for n in self.node_inf.list():
+                self.enqueue(n)
+
+    @staticmethod
+    def ttl_patch(node, ttl: int) -> dict:
+        """patchNodeWithAnnotation's strategic merge patch: empty when the value is already set."""
+        if m.annotations_of(node).get(TTL_ANNOTATION) == str(ttl):
+            return {}
+        return {"metadata": {"annotations": {TTL_ANNOTATION: str(ttl)}}}
+
+    async def update_node_if_needed(self, name: str):
         node = self.node_inf.get(name)
         if node is None:
             return
-        want = str(ttl_for(len(self.node_inf.list())))
-        if m.annotations_of(node).get(TTL_ANNOTATION) != want:
-            await self.client.patch("nodes", name, {"metadata": {"annotations": {TTL_ANNOTATION: want}}})
+        if m.annotations_of(node).get(TTL_ANNOTATION) == str(self.desired_ttl):
+            return
+        await self.client.patch("nodes", name, self.ttl_patch(node, self.desired_ttl),
+                                patch_type="application/strategic-merge-patch+json")
+
+    async def sync(self, key):
+        await self.update_node_if_needed(split_key(key)[1])
 
 
 # ------------------------------------------------------------- ClusterRole aggregation

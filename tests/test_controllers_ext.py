@@ -72,7 +72,7 @@ def test_cron_schedule_semantics():
 
 
 def test_ttl_boundaries_and_jws():
-    assert [ttl_for(n) for n in (1, 100, 101, 500, 1000, 2000, 5000, 5001)] == [0, 0, 15, 15, 30, 60, 300, 600]
+    assert [ttl_for(n) for n in (1, 100, 101, 500, 1000, 2000, 5000, 10001)] == [0, 0, 15, 15, 30, 60, 300, 600]
     jws = detached_jws("kubeconfig-bytes", "abcdef", "0123456789abcdef")
     head, empty, sig = jws.split(".")
     assert empty == "" and verify_detached_jws(jws, "kubeconfig-bytes", "abcdef", "0123456789abcdef")
