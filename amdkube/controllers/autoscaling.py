@@ -2,9 +2,11 @@
 
 Reference: pkg/controller/podautoscaler/horizontal.go + replica_calculator.go (1.9,
 autoscaling/v1): every --horizontal-pod-autoscaler-sync-period (30 s) read the target's
-scale; utilization = Σ usage / Σ requests over the target's running pods that report
+scale; utilization = Σ usage / Σ requests over the target's ready pods that report
 metrics; usageRatio = utilization / target; inside the 10 % tolerance nothing changes,
-else desired = ceil(usageRatio × pods-with-metrics); clamp to [minReplicas, maxReplicas]
+else desired = ceil(usageRatio × pods-with-metrics). Pods without metrics count as at target
+on a scale-down and idle on a scale-up, unready pods as idle on a scale-up, and a rebalanced
+ratio that flips direction keeps the count (replica_calculator.go, integer milli-units); clamp to [minReplicas, maxReplicas]
 and to the scale-up limit max(2 × current, 4); a scale-up needs 3 min and a scale-down 5 min
 since the last rescale (--horizontal-pod-autoscaler-{upscale,downscale}-delay); status
 carries currentReplicas / desiredReplicas / currentCPUUtilizationPercentage / lastScaleTime.
@@ -37,7 +39,7 @@ import aiohttp
 
 from ..api import autoscaling as api_autoscaling
 from ..api import meta as m
-from ..api.helpers import is_pod_terminal
+from ..api.helpers import is_pod_ready
 from ..api.labels import selector_from_label_selector, selector_from_set
 from ..api.quantity import Quantity
 from .base import Controller, split_key
@@ -193,62 +195,144 @@ def _num(q) -> float:
 
 def _fmt(v: float) -> str:
     """A float as the canonical quantity string the reference writes (milli-units below 1000 × int)."""
-    mv = int(round(v * 1000))
+    return _fmt_milli(int(round(v * 1000)))
+
+
+def _fmt_milli(mv: int) -> str:
+    """resource.NewMilliQuantity(mv, DecimalSI).String() for the values the controller writes."""
     return str(mv // 1000) if mv % 1000 == 0 else f"{mv}m"
 
 
-def _request(pod, resource) -> int:
-    """Σ container requests of one resource (millicores for cpu, bytes otherwise); 0 when any
-    container has none — the reference then treats utilization as undefined for the pod."""
-    total = 0
-    for c in (pod.get("spec") or {}).get("containers") or []:
-        v = ((c.get("resources") or {}).get("requests") or {}).get(resource)
-        if v is None:
-            return 0
-        total += Quantity(v).milli_value() if resource == "cpu" else Quantity(v).value()
-    return total
-
-
 _USAGE_KEY = {"cpu": "cpu_milli", "memory": "memory_bytes"}
-
-
-def _cpu_request_milli(pod) -> int:
-    return _request(pod, "cpu")
 
 
 def _ratio_replicas(ratio: float, n: int, current: int) -> int:
     return current if abs(ratio - 1.0) <= TOLERANCE else int(math.ceil(ratio * n))
 
 
-def resource_proposal(pods, metrics, resource, current, target_util=None, target_avg=None):
-    """replica_calculator.go GetResourceReplicas / GetRawResourceReplicas. Returns
-    (replicas, utilization %, average usage in the resource's base unit) or (None, None, None)."""
-    key = _USAGE_KEY.get(resource)
-    usage = req = 0.0
-    n = 0
+# ---- replica calculator (replica_calculator.go, metrics/utilization.go), in integer milli-units
+def resource_utilization_ratio(metrics: dict, requests: dict, target: int) -> tuple[float, int, int]:
+    """GetResourceUtilizationRatio: metrics of pods with no known request are extraneous; the
+    utilization is an integer percentage and the raw average an integer milli-value."""
+    total = req = n = 0
+    for name, v in metrics.items():
+        if name not in requests:
+            continue
+        total, req, n = total + v, req + requests[name], n + 1
+    if req == 0:
+        raise LookupError("no metrics returned matched known pods")
+    util = total * 100 // req
+    return util / target, util, total // n
+
+
+def metric_utilization_ratio(metrics: dict, target: int) -> tuple[float, int]:
+    """GetMetricUtilizationRatio: every metric counts, superfluous ones included."""
+    util = sum(metrics.values()) // len(metrics)
+    return util / target, util
+
+
+def _classify(pods, metrics) -> tuple[int, set, set]:
+    """Pods not Running-and-Ready are unready (their metrics dropped); ready pods without a metric
+    are missing; the rest count."""
+    ready, unready, missing = 0, set(), set()
     for p in pods:
-        mt = metrics.get(m.name_of(p)) or {}
-        if key is None or key not in mt:
-            continue
-        r = _request(p, resource)
-        if target_util is not None and r <= 0:
-            continue
-        usage += mt[key]
-        req += r
-        n += 1
-    if n == 0 or (target_util is not None and req == 0):
-        return None, None, None
-    scale = 1000.0 if resource == "cpu" else 1.0        # cpu usage is in millicores
-    avg = usage / n / scale
-    if target_util is not None:
-        util = int(round(usage * 100.0 / req))
-        return _ratio_replicas(util / float(target_util), n, current), util, avg
-    return _ratio_replicas(avg / float(target_avg), n, current), None, avg
+        name = m.name_of(p)
+        if (p.get("status") or {}).get("phase") != "Running" or not is_pod_ready(p):
+            unready.add(name)
+            metrics.pop(name, None)
+        elif name not in metrics:
+            missing.add(name)
+        else:
+            ready += 1
+    return ready, unready, missing
 
 
-def cpu_proposal(pods, metrics, target_pct, current) -> tuple[int | None, int | None]:
-    r, util, _ = resource_proposal(pods, metrics, "cpu", current, target_util=target_pct)
-    return r, util
+def _replicas_from(current, ratio, ready, unready, missing, metrics, missing_down, zero_missing_at_one, recompute,
+                   tolerance=TOLERANCE) -> int:
+    """The shared tail of GetResourceReplicas and calcPlainMetricReplicas: with no unready pods on a
+    scale-up and nothing missing, ceil(ratio × ready pods) outside the tolerance. Otherwise missing
+    pods count as at target on a scale-down and idle on a scale-up, unready pods as idle on a
+    scale-up, and a recomputed ratio that falls inside the tolerance or flips direction keeps the
+    current count."""
+    rebalance = bool(unready) and ratio > 1.0
+    if not rebalance and not missing:
+        return current if abs(1.0 - ratio) <= tolerance else int(math.ceil(ratio * ready))
+    if missing:
+        if ratio < 1.0:
+            for name in missing:
+                metrics[name] = missing_down(name)
+        elif ratio > 1.0 or zero_missing_at_one:
+            for name in missing:
+                metrics[name] = 0
+    if rebalance:
+        for name in unready:
+            metrics[name] = 0
+    new = recompute(metrics)
+    if abs(1.0 - new) <= tolerance or (ratio < 1.0 < new) or (ratio > 1.0 > new):
+        return current
+    return int(math.ceil(new * len(metrics)))
+
+
+def get_resource_replicas(current: int, target_util: int, resource: str, pods, metrics: dict, ns: str = "",
+                          tolerance: float = TOLERANCE) -> tuple[int, int, int]:
+    """GetResourceReplicas: (replicas, utilization %, raw average milli-value). `metrics` maps pod
+    name → Σ container usage in milli-units; every container of every pod needs a request."""
+    if not metrics:
+        raise LookupError(f"unable to get metrics for resource {resource}: no metrics returned from heapster")
+    if not pods:
+        raise LookupError("no pods returned by selector while calculating replica count")
+    metrics, requests = dict(metrics), {}
+    for p in pods:
+        total = 0
+        for c in (p.get("spec") or {}).get("containers") or []:
+            q = ((c.get("resources") or {}).get("requests") or {}).get(resource)
+            if q is None:
+                raise LookupError(f"missing request for {resource} on container {c.get('name', '')} in pod {ns}/{m.name_of(p)}")
+            total += Quantity(str(q)).milli_value()
+        requests[m.name_of(p)] = total
+    ready, unready, missing = _classify(pods, metrics)
+    if not metrics:
+        raise LookupError("did not receive metrics for any ready pods")
+    ratio, util, raw = resource_utilization_ratio(metrics, requests, target_util)
+    rep = _replicas_from(current, ratio, ready, unready, missing, metrics, requests.__getitem__, False,
+                         lambda mt: resource_utilization_ratio(mt, requests, target_util)[0], tolerance)
+    return rep, util, raw
+
+
+def get_plain_metric_replicas(current: int, target: int, pods, metrics: dict, tolerance: float = TOLERANCE) -> tuple[int, int]:
+    """calcPlainMetricReplicas (GetRawResourceReplicas / GetMetricReplicas): (replicas, average
+    milli-value) against a per-pod target milli-value."""
+    if not pods:
+        raise LookupError("no pods returned by selector while calculating replica count")
+    metrics = dict(metrics)
+    ready, unready, missing = _classify(pods, metrics)
+    if not metrics:
+        raise LookupError("did not receive metrics for any ready pods")
+    ratio, util = metric_utilization_ratio(metrics, target)
+    rep = _replicas_from(current, ratio, ready, unready, missing, metrics, lambda _: target, True,
+                         lambda mt: metric_utilization_ratio(mt, target)[0], tolerance)
+    return rep, util
+
+
+def get_object_metric_replicas(current: int, target: int, value: int, tolerance: float = TOLERANCE) -> int:
+    """GetObjectMetricReplicas: one object's milli-value against the target, scaled over the
+    current replica count."""
+    ratio = value / target
+    return current if abs(1.0 - ratio) <= tolerance else int(math.ceil(ratio * current))
+
+
+def _milli(v) -> int:
+    """A metric source's base-unit float as the integer milli-value the calculator works in."""
+    return int(round(v * 1000))
+
+
+def resource_metrics_milli(raw: dict, resource: str) -> dict:
+    """Pod → Σ usage in milli-units from a resource metrics source (cpu_milli is already milli)."""
+    key = _USAGE_KEY.get(resource)
+    if key is None:
+        return {}
+    return {name: int(round(mt[key])) if resource == "cpu" else int(mt[key]) * 1000
+            for name, mt in raw.items() if key in mt}
 
 
 def gpu_proposal(pods, metrics, target_pct, current) -> tuple[int | None, float | None]:
@@ -332,33 +416,37 @@ class HorizontalPodAutoscalerController(Controller):
                     if resource_metrics is None:
                         resource_metrics = await self.metrics.pod_metrics(ns)
                     r = ms.get("resource") or {}
+                    rname = r.get("name")
                     tu, tv = r.get("targetAverageUtilization"), r.get("targetAverageValue")
-                    rep, util, avg = resource_proposal(pods, resource_metrics, r.get("name"), current,
-                                                       target_util=tu, target_avg=_num(tv) if tu is None and tv else None)
-                    if rep is None:
-                        raise LookupError(f"did not receive metrics for any ready pods ({r.get('name')})")
-                    cur = {"name": r.get("name"), "currentAverageValue": _fmt(avg)}
-                    if util is not None:
-                        cur["currentAverageUtilization"] = util
-                    out.append((rep, f"{r.get('name')} resource" + (" utilization (percentage of request)" if util is not None else ""),
+                    # the metrics API is asked with the target's selector: metrics of other pods never arrive
+                    names = {m.name_of(p) for p in pods}
+                    mt = {k: v for k, v in resource_metrics_milli(resource_metrics, rname).items() if k in names}
+                    if tu is not None:
+                        rep, util, raw = get_resource_replicas(current, int(tu), rname, pods, mt, ns)
+                        cur = {"name": rname, "currentAverageUtilization": util, "currentAverageValue": _fmt_milli(raw)}
+                    else:
+                        if not mt:
+                            raise LookupError(f"unable to get metrics for resource {rname}: no metrics returned from heapster")
+                        rep, raw = get_plain_metric_replicas(current, Quantity(str(tv)).milli_value(), pods, mt)
+                        cur = {"name": rname, "currentAverageValue": _fmt_milli(raw)}
+                    out.append((rep, f"{rname} resource" + (" utilization (percentage of request)" if tu is not None else ""),
                                 {"type": "Resource", "resource": cur}))
                 elif typ == "Pods":
                     pm = ms.get("pods") or {}
                     vals = await self.custom.pod_metric(ns, pm.get("metricName"), selector_str)
-                    have = [vals[m.name_of(p)] for p in pods if m.name_of(p) in vals]
-                    if not have:
-                        raise LookupError(f"no metrics returned for pods/{pm.get('metricName')}")
-                    avg = sum(have) / len(have)
-                    rep = _ratio_replicas(avg / _num(pm.get("targetAverageValue")), len(have), current)
+                    if not vals:
+                        raise LookupError(f"unable to get metric {pm.get('metricName')}: no metrics returned from custom metrics API")
+                    rep, avg = get_plain_metric_replicas(current, Quantity(str(pm.get("targetAverageValue"))).milli_value(), pods,
+                                                         {k: _milli(v) for k, v in vals.items()})
                     out.append((rep, f"pods metric {pm.get('metricName')}",
-                                {"type": "Pods", "pods": {"metricName": pm.get("metricName"), "currentAverageValue": _fmt(avg)}}))
+                                {"type": "Pods", "pods": {"metricName": pm.get("metricName"), "currentAverageValue": _fmt_milli(avg)}}))
                 elif typ == "Object":
                     om = ms.get("object") or {}
-                    val = await self.custom.object_metric(ns, om.get("target") or {}, om.get("metricName"))
-                    rep = _ratio_replicas(val / _num(om.get("targetValue")), current, current)
+                    val = _milli(await self.custom.object_metric(ns, om.get("target") or {}, om.get("metricName")))
+                    rep = get_object_metric_replicas(current, Quantity(str(om.get("targetValue"))).milli_value(), val)
                     out.append((rep, f"{om.get('metricName')} metric on {(om.get('target') or {}).get('kind')}",
                                 {"type": "Object", "object": {"target": om.get("target"), "metricName": om.get("metricName"),
-                                                              "currentValue": _fmt(val)}}))
+                                                              "currentValue": _fmt_milli(val)}}))
                 else:
                     raise LookupError(f"unknown metric source type {typ!r}")
             except (LookupError, m.StatusError, aiohttp.ClientError, asyncio.TimeoutError, ZeroDivisionError, ValueError) as e:
@@ -402,9 +490,9 @@ class HorizontalPodAutoscalerController(Controller):
         selector = selector_from_set(sel) if ref.get("kind") == "ReplicationController" else selector_from_label_selector(sel)
         selector_str = ",".join(f"{k}={v}" for k, v in sorted(sel.items())) if ref.get("kind") == "ReplicationController" \
             else _selector_string(sel)
-        pods = [p for p in self.pod_inf.list() if m.namespace_of(p) == ns and selector.matches(m.labels_of(p))
-                and not is_pod_terminal(p) and not (p.get("metadata") or {}).get("deletionTimestamp")
-                and (p.get("status") or {}).get("phase") == "Running"]
+        # every pod the selector matches, as the reference's pod list: the calculator itself sets
+        # unready (not Running and Ready) and metric-less pods aside
+        pods = [p for p in self.pod_inf.list() if m.namespace_of(p) == ns and selector.matches(m.labels_of(p))]
         lo, hi = int(spec.get("minReplicas", 1)), int(spec.get("maxReplicas", current))
         current_metrics, gpu_util, reason = None, None, ""
         if current == 0:

@@ -231,7 +231,10 @@ async def test_hpa_scales_on_gpu_and_cpu_utilization():
         fm.values = {m.name_of(p): {"cpu_milli": 900.0, "gpu_util": 50.0} for p in pods}
         await c.patch("horizontalpodautoscalers", "infer", {"spec": {"targetCPUUtilizationPercentage": 60}}, "default")
         await until(lambda: _replicas(c, "infer", 3))
-        # idle → down to minReplicas
+        await until(lambda: _status_ready(c, "deployments", "infer", 3), 30)
+        # idle → down to minReplicas; every pod reports (a pod without a metric counts as at target
+        # on a scale-down, replica_calculator.go)
+        pods = (await c.list("pods", "default", label_selector="app=infer"))[0]
         fm.values = {m.name_of(p): {"cpu_milli": 1.0, "gpu_util": 1.0} for p in pods}
         await until(lambda: _replicas(c, "infer", 1))
 

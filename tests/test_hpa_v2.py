@@ -12,9 +12,12 @@ from __future__ import annotations
 import copy
 import json
 
+import pytest
+
 from amdkube.api import autoscaling as A
 from amdkube.api import meta as m
-from amdkube.controllers.autoscaling import _fmt, _selector_string, resource_proposal
+from amdkube.controllers.autoscaling import (_fmt, _selector_string, get_plain_metric_replicas, get_resource_replicas,
+                                             resource_metrics_milli)
 from amdkube.localcluster import LocalCluster
 from amdkube.metrics import MetricsServer
 from tests.test_controllers_ext import _replicas, _status_ready, pod_tpl, until
@@ -58,17 +61,19 @@ def test_v2beta1_round_trips_through_v1_annotations():
 
 
 def test_replica_calculator_units():
-    pods = [{"metadata": {"name": f"p{i}"}, "spec": {"containers": [{"resources": {"requests": {"cpu": "500m", "memory": "1Gi"}}}]}}
-            for i in range(2)]
+    pods = [{"metadata": {"name": f"p{i}"}, "spec": {"containers": [{"resources": {"requests": {"cpu": "500m", "memory": "1Gi"}}}]},
+             "status": {"phase": "Running", "conditions": [{"type": "Ready", "status": "True"}]}} for i in range(2)]
     mt = {"p0": {"cpu_milli": 900.0, "memory_bytes": 3 << 30}, "p1": {"cpu_milli": 300.0, "memory_bytes": 1 << 30}}
-    # cpu utilization: 1200m of 1000m = 120 % vs 60 % → ceil(2 × 2) = 4
-    assert resource_proposal(pods, mt, "cpu", 2, target_util=60) == (4, 120, 0.6)
+    cpu, mem = resource_metrics_milli(mt, "cpu"), resource_metrics_milli(mt, "memory")
+    # cpu utilization: 1200m of 1000m = 120 % vs 60 % → ceil(2 × 2) = 4; raw average 600m
+    assert get_resource_replicas(2, 60, "cpu", pods, cpu) == (4, 120, 600)
     # raw memory average 2 Gi vs 1 Gi → 4; utilization 200 % vs 190 % is inside the 10 % tolerance
-    assert resource_proposal(pods, mt, "memory", 2, target_avg=float(1 << 30))[0] == 4
-    assert resource_proposal(pods, mt, "memory", 2, target_util=190)[:2] == (2, 200)
-    # a pod without a request leaves utilization undefined for that pod only
+    assert get_plain_metric_replicas(2, (1 << 30) * 1000, pods, mem) == (4, (2 << 30) * 1000)
+    assert get_resource_replicas(2, 190, "memory", pods, mem)[:2] == (2, 200)
+    # a container without a request makes the utilization undefined: the reference errors out
     del pods[1]["spec"]["containers"][0]["resources"]["requests"]["cpu"]
-    assert resource_proposal(pods, mt, "cpu", 2, target_util=60) == (3, 180, 0.9)   # 180 % / 60 % × 1 pod
+    with pytest.raises(LookupError, match="missing request for cpu"):
+        get_resource_replicas(2, 60, "cpu", pods, cpu)
     assert _fmt(0.6) == "600m" and _fmt(88.0) == "88" and _fmt(1.25) == "1250m"
     assert _selector_string({"matchLabels": {"b": "2", "a": "1"},
                              "matchExpressions": [{"key": "t", "operator": "In", "values": ["x", "y"]}]}) == "a=1,b=2,t in (x,y)"
