@@ -123,3 +123,11 @@ def test_computed_tolerance_alg_implementation():
     # just inside the tolerance margin nothing scales
     pct = int((abs(1 / (requested_to_used * (1 - TOLERANCE))) + .004) * 100)
     assert _resource(start, requests, levels, pct) == (start, expect_util, expect_raw)
+
+
+def test_missing_pods_at_exact_target():
+    """Not in the reference tests; read off replica_calculator.go: at a usage ratio of exactly 1.0
+    a plain metric still zero-fills missing pods (the `else` at :244) and so scales down, while a
+    resource metric leaves them out (`else if usageRatio > 1.0` at :131) and keeps the count."""
+    assert _metric(2, [15000], 15000) == (1, 15000)
+    assert _resource(2, [ONE] * 2, [500], 100) == (2, 100, CONTAINERS * 500)
