@@ -130,4 +130,4 @@ def test_missing_pods_at_exact_target():
     a plain metric still zero-fills missing pods (the `else` at :244) and so scales down, while a
     resource metric leaves them out (`else if usageRatio > 1.0` at :131) and keeps the count."""
     assert _metric(2, [15000], 15000) == (1, 15000)
-    assert _resource(2, [ONE] * 2, [500], 100) == (2, 100, CONTAINERS * 500)
+    assert _resource(2, [ONE] * 2, [1000], 100) == (2, 100, CONTAINERS * 1000)
