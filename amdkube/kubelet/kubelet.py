@@ -851,6 +851,8 @@ class Kubelet:
         the node name and the file content (config/common.go applyDefaults)."""
         import hashlib
         import uuid as _uuid
+
+        from ..api.defaults import default_pod
         out = {}
         for doc, fallback, source in self._file_docs() + self._http_docs():
             md = doc.setdefault("metadata", {})
@@ -864,6 +866,7 @@ class Kubelet:
             doc.setdefault("spec", {})["nodeName"] = self.node_name
             doc["spec"].setdefault("restartPolicy", "Always")
             doc.setdefault("status", {"phase": "Pending"})
+            default_pod(doc)            # decoded through the scheme: SetDefaults_Pod, as the apiserver would
             out[md["uid"]] = doc
         return out
 

@@ -4,7 +4,7 @@ Reference: pkg/apis/core/helper/qos/qos.go GetPodQOS (Guaranteed: every containe
 and memory limits with requests equal to them; BestEffort: no requests or limits at all;
 Burstable otherwise), pkg/kubelet/qos/policy.go GetContainerOOMScoreAdjust (Guaranteed
 −998, BestEffort 1000, Burstable 1000 − 1000·memoryRequest/memoryCapacity clamped to
-[2, 999]; critical pods −998), pkg/kubelet/cm/qos_container_manager_linux.go +
+[2, 999] from the memory request), pkg/kubelet/cm/qos_container_manager_linux.go +
 pod_container_manager_linux.go (cgroup parent kubepods/[burstable|besteffort]/pod<uid>).
 """
 from __future__ import annotations
@@ -13,46 +13,55 @@ from ..api.quantity import Quantity
 
 GUARANTEED, BURSTABLE, BEST_EFFORT = "Guaranteed", "Burstable", "BestEffort"
 CRITICAL_ANNOTATION = "scheduler.alpha.kubernetes.io/critical-pod"
-GUARANTEED_OOM, BEST_EFFORT_OOM, CRITICAL_OOM = -998, 1000, -998
+GUARANTEED_OOM, BEST_EFFORT_OOM = -998, 1000
+
+
+def _qos_resource(name: str) -> bool:
+    """isSupportedQoSComputeResource: cpu, memory and the hugepages-<size> resources."""
+    return name in ("cpu", "memory") or name.startswith("hugepages-")
 
 
 def pod_qos(pod: dict) -> str:
-    spec = pod.get("spec") or {}
-    requests, limits, any_set = {}, {}, False
+    """GetPodQOS over the app containers of an API-defaulted pod (requests already filled from
+    limits): positive quantities are summed per resource across containers; Guaranteed needs a cpu
+    and a memory limit in every container and equal summed requests and limits."""
+    requests, limits = {}, {}
     guaranteed = True
-    for c in (spec.get("initContainers") or []) + (spec.get("containers") or []):
+    for c in (pod.get("spec") or {}).get("containers") or []:
         r = c.get("resources") or {}
-        rq, li = dict(r.get("requests") or {}), dict(r.get("limits") or {})
-        for k, v in li.items():   # requests default to limits
-            rq.setdefault(k, v)
-        for k in ("cpu", "memory"):
-            if k in rq and Quantity(rq[k]).as_fraction() > 0:
-                any_set = True
-                requests[k] = True
-            if k in li and Quantity(li[k]).as_fraction() > 0:
-                any_set = True
-                limits[k] = True
-            if k not in li or k not in rq or Quantity(rq[k]) != Quantity(li[k]):
-                guaranteed = False
-    if not any_set:
+        for k, v in (r.get("requests") or {}).items():
+            q = Quantity(str(v)).as_fraction()
+            if _qos_resource(k) and q > 0:
+                requests[k] = requests.get(k, 0) + q
+        found = set()
+        for k, v in (r.get("limits") or {}).items():
+            q = Quantity(str(v)).as_fraction()
+            if _qos_resource(k) and q > 0:
+                found.add(k)
+                limits[k] = limits.get(k, 0) + q
+        if not {"cpu", "memory"} <= found:
+            guaranteed = False
+    if not requests and not limits:
         return BEST_EFFORT
-    return GUARANTEED if guaranteed and set(limits) == {"cpu", "memory"} else BURSTABLE
+    if guaranteed and all(k in limits and limits[k] == v for k, v in requests.items()) and len(requests) == len(limits):
+        return GUARANTEED
+    return BURSTABLE
 
 
 def oom_score_adj(pod: dict, container: dict, memory_capacity: int) -> int:
-    if ((pod.get("metadata") or {}).get("annotations") or {}).get(CRITICAL_ANNOTATION) is not None and \
-            ((pod.get("metadata") or {}).get("namespace") == "kube-system"):
-        return CRITICAL_OOM
+    """GetContainerOOMScoreAdjust: Burstable containers get 1000 − 1000·memoryRequest/capacity
+    from the container's memory request alone, floored at 2 and kept below BestEffort's 1000."""
     q = pod_qos(pod)
     if q == GUARANTEED:
         return GUARANTEED_OOM
     if q == BEST_EFFORT:
         return BEST_EFFORT_OOM
-    res = container.get("resources") or {}
-    mem = (res.get("requests") or {}).get("memory") or (res.get("limits") or {}).get("memory")
-    req = Quantity(mem).value() if mem else 0
-    adj = 1000 - (1000 * req) // max(1, memory_capacity)
-    return int(min(999, max(2, adj)))
+    mem = ((container.get("resources") or {}).get("requests") or {}).get("memory")
+    req = Quantity(str(mem)).value() if mem is not None else 0
+    adj = 1000 - (1000 * req) // memory_capacity
+    if adj < 1000 + GUARANTEED_OOM:
+        return 1000 + GUARANTEED_OOM
+    return adj - 1 if adj == BEST_EFFORT_OOM else adj
 
 
 def pod_cgroup_name(pod: dict) -> str:

@@ -67,7 +67,7 @@ def test_revert_and_cgroupfs_driver_identity():
 
 def test_pod_cgroup_parent_per_driver():
     from amdkube.kubelet.qos import cgroup_parent
-    g = {"metadata": {"uid": "ab-cd"}, "spec": {"containers": [{"resources": {"limits": {"cpu": "1", "memory": "1Gi"}}}]}}
+    g = {"metadata": {"uid": "ab-cd"}, "spec": {"containers": [{"resources": {"requests": {"cpu": "1", "memory": "1Gi"}, "limits": {"cpu": "1", "memory": "1Gi"}}}]}}
     b = {"metadata": {"uid": "ab-cd"}, "spec": {"containers": [{"resources": {"requests": {"cpu": "1"}}}]}}
     be = {"metadata": {"uid": "ab-cd"}, "spec": {"containers": [{}]}}
     assert [cgroup_parent(p) for p in (g, b, be)] == ["kubepods/podab-cd", "kubepods/burstable/podab-cd",

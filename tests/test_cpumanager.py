@@ -39,11 +39,11 @@ def test_static_policy_reserved_exclusive_shared_and_checkpoint(tmp_path):
     cm = CPUManager("static", TOPO, reserved_cpus_milli=1500, state_file=state)
     assert len(cm.reserved) == 2 and cm.reserved == {0, 8}          # ceil(1.5) CPUs = one whole core
     g = {"metadata": {"uid": "u1"}, "spec": {"containers": [
-        {"name": "c", "resources": {"limits": {"cpu": "4", "memory": "1Gi"}}}]}}
+        {"name": "c", "resources": {"requests": {"cpu": "4", "memory": "1Gi"}, "limits": {"cpu": "4", "memory": "1Gi"}}}]}}
     cs = parse_cpuset(cm.allocate(g, g["spec"]["containers"][0]))
     assert len(cs) == 4 and not cs & cm.reserved
     frac = {"metadata": {"uid": "u2"}, "spec": {"containers": [
-        {"name": "c", "resources": {"limits": {"cpu": "1500m", "memory": "1Gi"}}}]}}
+        {"name": "c", "resources": {"requests": {"cpu": "1500m", "memory": "1Gi"}, "limits": {"cpu": "1500m", "memory": "1Gi"}}}]}}
     assert parse_cpuset(cm.allocate(frac, frac["spec"]["containers"][0])) == cm.default_set()   # not integer: shared
     be = {"metadata": {"uid": "u3"}, "spec": {"containers": [{"name": "c"}]}}
     assert parse_cpuset(cm.allocate(be, be["spec"]["containers"][0])) == set(TOPO.cpus) - cs
@@ -67,11 +67,11 @@ def test_gpu_numa_preference():
     topo = CPUTopology.synthetic(2, 8, 2, numa_per_socket=2)       # 4 NUMA nodes of 4 cores
     cm = CPUManager("static", topo, reserved_cpus_milli=1000)
     pod = {"metadata": {"uid": "g"}, "spec": {"containers": [
-        {"name": "c", "resources": {"limits": {"cpu": "4", "memory": "1Gi"}}}]}}
+        {"name": "c", "resources": {"requests": {"cpu": "4", "memory": "1Gi"}, "limits": {"cpu": "4", "memory": "1Gi"}}}]}}
     cs = parse_cpuset(cm.allocate(pod, pod["spec"]["containers"][0], prefer_numa={3}))
     assert {topo.cpus[c].numa for c in cs} == {3}
     big = {"metadata": {"uid": "h"}, "spec": {"containers": [
-        {"name": "c", "resources": {"limits": {"cpu": "12", "memory": "1Gi"}}}]}}
+        {"name": "c", "resources": {"requests": {"cpu": "12", "memory": "1Gi"}, "limits": {"cpu": "12", "memory": "1Gi"}}}]}}
     cs2 = parse_cpuset(cm.allocate(big, big["spec"]["containers"][0], prefer_numa={3}))
     assert len(cs2) == 12 and not cs2 & cs                          # no room on node 3: anywhere
 

@@ -12,7 +12,8 @@ def _pod(*resources, uid="u1"):
 
 
 def test_qos_classes_and_oom_scores():
-    g = _pod({"limits": {"cpu": "2", "memory": "4Gi"}})
+    # API-defaulted shapes: requests filled from limits (GetPodQOS itself does not default)
+    g = _pod({"requests": {"cpu": "2", "memory": "4Gi"}, "limits": {"cpu": "2", "memory": "4Gi"}})
     b = _pod({"requests": {"memory": "1Gi"}})
     e = _pod({}, {"limits": {"amd.com/gpu": "1"}})
     assert (pod_qos(g), pod_qos(b), pod_qos(e)) == (GUARANTEED, BURSTABLE, BEST_EFFORT)
