@@ -20,10 +20,12 @@ def is_critical(pod: dict) -> bool:
 
 
 def request(pod: dict, res: str) -> int:
+    """resource.GetResourceRequest: 1 for pods, millicores for cpu, base units otherwise, from the
+    containers' requests (API-defaulted), plus the pod's device-granular extended resources."""
     if res == "pods":
         return 1
     from ..api.helpers import ExtendedResourceError, pod_extended_resource_count, pod_extended_resource_name
-    v = pod_requests(_defaulted(pod)).get(res, 0)
+    v = pod_requests(pod).get(res, 0)
     for pres in (pod.get("spec") or {}).get("extendedResources") or []:
         try:
             if pod_extended_resource_name(pres) == res:
@@ -31,18 +33,6 @@ def request(pod: dict, res: str) -> int:
         except (ExtendedResourceError, KeyError):
             pass
     return int(v)
-
-
-def _defaulted(pod: dict) -> dict:
-    """Requests default to limits (API defaulting) for objects that skipped it."""
-    spec = pod.get("spec") or {}
-    if not any((c.get("resources") or {}).get("limits") for c in spec.get("containers") or []):
-        return pod
-    cs = []
-    for c in spec.get("containers") or []:
-        res = c.get("resources") or {}
-        cs.append(dict(c, resources=dict(res, requests={**(res.get("limits") or {}), **(res.get("requests") or {})})))
-    return {"metadata": pod.get("metadata"), "spec": dict(spec, containers=cs)}
 
 
 def subtract(reqs: dict[str, int], pods) -> dict[str, int]:
@@ -67,18 +57,23 @@ def _smaller(a: dict, b: dict) -> bool:
 
 
 def by_distance(pods: list[dict], reqs: dict[str, int]) -> list[dict]:
+    """getPodsToPreemptByDistance: each round scans in order for the smallest distance (ties go to
+    the smaller request), then moves the last pod into the chosen slot, so later rounds see the
+    reference's order."""
     pods, out = list(pods), []
     while reqs:
         if not pods:
             raise ValueError(f"no set of running pods found to reclaim resources: {reqs}")
-        best = min(range(len(pods)), key=lambda i: distance(reqs, pods[i]))
-        bd = distance(reqs, pods[best])
+        best_d, best = float(len(reqs) + 1), 0
         for i, p in enumerate(pods):
-            if distance(reqs, p) == bd and _smaller(p, pods[best]):
-                best = i
-        victim = pods.pop(best)
-        out.append(victim)
+            d = distance(reqs, p)
+            if d < best_d or (d == best_d and _smaller(p, pods[best])):
+                best_d, best = d, i
+        victim = pods[best]
         reqs = subtract(reqs, [victim])
+        out.append(victim)
+        pods[best] = pods[-1]
+        pods.pop()
     return out
 
 

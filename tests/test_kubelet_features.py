@@ -160,7 +160,7 @@ def test_critical_pod_preemption_selection_and_admission():
     def p(name, qos, cpu=None, mem=None, critical=False):
         res = {}
         if qos == "Guaranteed":
-            res = {"limits": {"cpu": cpu, "memory": mem}}
+            res = {"requests": {"cpu": cpu, "memory": mem}, "limits": {"cpu": cpu, "memory": mem}}   # API-defaulted
         elif qos == "Burstable":
             res = {"requests": {k: v for k, v in (("cpu", cpu), ("memory", mem)) if v}}
         md = {"name": name, "namespace": "kube-system" if critical else "default", "uid": name}
