@@ -81,7 +81,8 @@ def add_or_update_toleration(spec: dict, tol: dict) -> bool:
 
 
 def is_critical(namespace: str, annotations: dict | None) -> bool:
-    return namespace == "kube-system" and CRITICAL_ANNOTATION in (annotations or {})
+    """kubelet/types IsCritical: kube-system and the critical-pod annotation with an empty value."""
+    return namespace == "kube-system" and (annotations or {}).get(CRITICAL_ANNOTATION) == ""
 
 
 def template_generation(ds):

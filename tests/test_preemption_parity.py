@@ -114,3 +114,16 @@ def test_tiny_burstable_benchmark_shape():
     """BenchmarkGetPodsToPreempt :139: 110 tiny pods (1m each) cover a 110m requirement."""
     out = pods_to_preempt([PODS["tinyBurstable"]] * 110, {"cpu": 110})
     assert len(out) == 110
+
+
+@pytest.mark.parametrize("ns,value,expected", [("ns", "", False), ("ns", "abc", False), ("kube-system", "abc", False),
+                                               ("kube-system", "", True)])
+def test_is_critical_pod(ns, value, expected):
+    """pkg/kubelet/types/pod_update_test.go TestIsCriticalPod :117, against every critical-pod
+    check in amdkube (kubelet preemption and eviction, DaemonSet controller)."""
+    from amdkube.controllers.daemonset import is_critical as ds_critical
+    from amdkube.kubelet.eviction import is_critical_pod
+    from amdkube.kubelet.preemption import is_critical
+    ann = {"scheduler.alpha.kubernetes.io/critical-pod": value}
+    p = {"metadata": {"name": "pod", "namespace": ns, "annotations": ann}}
+    assert is_critical(p) is expected and is_critical_pod(p) is expected and ds_critical(ns, ann) is expected
