@@ -42,7 +42,7 @@ def is_pod_available(p: dict, min_ready_seconds: int, now: float) -> bool:
     if not min_ready_seconds:
         return True
     since = m.parse_time((get_condition(p, "Ready") or {}).get("lastTransitionTime"))
-    return since is not None and since + min_ready_seconds <= now
+    return since is not None and since + min_ready_seconds < now          # Time.Before: strictly earlier
 
 
 def pod_from_template(template: dict, owner: dict, controller_ref: dict | None) -> dict:
