@@ -5,7 +5,7 @@ used â€” an image is in use while any container, running or not, references it â
 when the image filesystem is at or above --image-gc-high-threshold percent, frees
 capacity Ã— (100 âˆ’ --image-gc-low-threshold) / 100 âˆ’ available bytes by deleting unused images,
 least recently used first (then oldest detected), skipping images younger than
---minimum-image-ttl-duration. Failing to free enough records an ImageGCFailed event. The
+--minimum-image-ttl-duration. Failing to free enough records a FreeDiskSpaceFailed event. The
 eviction manager calls delete_unused() to reclaim disk under nodefs/imagefs pressure
 (eviction_manager.go reclaimNodeLevelResources).
 """
@@ -19,6 +19,10 @@ from dataclasses import dataclass
 log = logging.getLogger("amdkube.kubelet.images")
 
 
+class ImageGCError(RuntimeError):
+    pass
+
+
 @dataclass
 class ImageRecord:
     first_detected: float
@@ -29,8 +33,12 @@ class ImageRecord:
 class ImageGCManager:
     def __init__(self, cri, high: int = 85, low: int = 80, min_age: float = 120.0, clock=time.time, recorder=None,
                  node_ref=None):
-        if not 0 <= high <= 100 or not 0 <= low <= 100 or low > high:
-            raise ValueError(f"invalid image GC thresholds: high {high}, low {low}")
+        if not 0 <= high <= 100:
+            raise ValueError(f"invalid HighThresholdPercent {high}, must be in range [0-100]")
+        if not 0 <= low <= 100:
+            raise ValueError(f"invalid LowThresholdPercent {low}, must be in range [0-100]")
+        if low > high:
+            raise ValueError(f"LowThresholdPercent {low} can not be higher than HighThresholdPercent {high}")
         self.cri, self.high, self.low, self.min_age, self.clock = cri, high, low, min_age, clock
         self.recorder, self.node_ref = recorder, node_ref
         self.records: dict[str, ImageRecord] = {}
@@ -71,10 +79,8 @@ class ImageGCManager:
                        key=lambda x: (x[1].last_used, x[1].first_detected))
         freed = 0
         for rid, r in cands:
-            if freed >= amount:
-                break
             if now - r.first_detected < self.min_age:
-                continue
+                continue            # just pulled: a container may be about to use it
             try:
                 await self.cri.remove_image(rid)
             except Exception as e:
@@ -82,24 +88,36 @@ class ImageGCManager:
                 continue
             self.records.pop(rid, None)
             freed += r.size
+            if freed >= amount:
+                break
         return freed
 
+    def _event(self, reason: str, msg: str):
+        if self.recorder is not None and self.node_ref is not None:
+            self.recorder.event(self.node_ref(), "Warning", reason, msg)
+
     async def garbage_collect(self) -> dict:
+        """GarbageCollect: above the high threshold free down to the low one. A zero capacity
+        (InvalidDiskCapacity) or a shortfall (FreeDiskSpaceFailed) is an event and an error."""
         cap, avail = await self.fs_stats()
-        if cap <= 0:
-            return {"usage_percent": 0, "freed": 0}
+        if avail > cap:
+            log.warning("available %d is larger than capacity %d", avail, cap)
+            avail = cap
+        if cap == 0:
+            self._event("InvalidDiskCapacity", "invalid capacity 0 on image filesystem")
+            raise ImageGCError("invalid capacity 0 on image filesystem")
         usage = 100 - (avail * 100) // cap
         out = {"usage_percent": usage, "freed": 0}
         if usage >= self.high:
             amount = cap * (100 - self.low) // 100 - avail
-            if amount > 0:
-                freed = await self.free_space(amount)
-                out.update(freed=freed, wanted=amount)
-                if freed < amount:
-                    msg = (f"wanted to free {amount} bytes, but freed {freed} bytes space with errors in image deletion")
-                    log.warning("image GC: %s", msg)
-                    if self.recorder is not None and self.node_ref is not None:
-                        self.recorder.event(self.node_ref(), "Warning", "ImageGCFailed", msg)
+            freed = await self.free_space(amount)
+            out.update(freed=freed, wanted=amount)
+            if freed < amount:
+                msg = (f"failed to garbage collect required amount of images. Wanted to free {amount} bytes, "
+                       f"but freed {freed} bytes")
+                log.warning("image GC: %s", msg)
+                self._event("FreeDiskSpaceFailed", msg)
+                raise ImageGCError(msg)
         return out
 
     async def delete_unused(self) -> int:
