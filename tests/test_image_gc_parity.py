@@ -201,3 +201,9 @@ def test_validate_image_gc_policy(high, low, error):
         with pytest.raises(ValueError) as e:
             ImageGCManager(FakeRuntime(), high, low)
         assert str(e.value) == error
+
+
+def test_available_larger_than_capacity_is_clamped():
+    """Not in the reference tests; image_gc_manager.go:269 clamps available to capacity."""
+    gc, _, _ = manager(FakeRuntime(), fs=(1000, 1200))
+    assert run(gc.garbage_collect())["usage_percent"] == 0
