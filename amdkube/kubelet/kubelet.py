@@ -347,9 +347,10 @@ class Kubelet:
         self.node: dict | None = None
         self.informer: Informer | None = None
         self.svc_informer: Informer | None = None
-        self.readiness: dict[str, dict[str, bool]] = {}
-        self.liveness_failed: dict[str, set] = {}
-        self._probe_state: dict[tuple, dict] = {}
+        # prober_manager.go: one worker task per (pod, container, probe type)
+        from .prober import ProbeManager
+        self.probes = ProbeManager(self.status.get, runner=self._probe_exec, recorder=self.recorder,
+                                   on_change=self.dispatch)
         self._tasks: list[asyncio.Task] = []
         self._node_dirty = asyncio.Event()
         self._sandbox_uid: dict[str, str] = {}
@@ -455,7 +456,6 @@ class Kubelet:
         for cmgr in self.cert_managers:
             self._tasks.append(asyncio.create_task(cmgr.run(), name=f"cert-rotation-{cmgr.kind}"))
         self._tasks += [asyncio.create_task(self._relist_loop(), name="pleg-relist"),
-                        asyncio.create_task(self._prober_loop(), name="prober"),
                         asyncio.create_task(self._housekeeping(), name="housekeeping"),
                         asyncio.create_task(self._gc_loop(), name="container-gc"),
                         asyncio.create_task(self._eviction_loop(), name="eviction")]
@@ -531,6 +531,7 @@ class Kubelet:
         if getattr(self, "node_informer", None) is not None:
             await self.node_informer.stop()
         await cancel_and_wait([w.task for w in self.workers.values()])
+        await self.probes.stop()
         if self._ckpt_chain is not None:
             await asyncio.wait({self._ckpt_chain}, timeout=5)     # queued bootstrap-checkpoint writes land
         await self.status.stop()
@@ -1127,6 +1128,7 @@ class Kubelet:
                 ok, reason, msg = False, "UnexpectedAdmissionError", f"device admission failed: {e!r}"
         if ok:
             self.admitted.add(uid)
+            self.probes.add_pod(pod)       # HandlePodAdditions: probeManager.AddPod after admission
             POD_TRACE(uid, "admitted")
             return True
         self.rejected[uid] = (reason, msg)
@@ -1211,6 +1213,7 @@ class Kubelet:
                 # kubelet restart: the pod was admitted by the previous incarnation and is running;
                 # never kill it because a device plugin has not re-registered yet
                 self.admitted.add(uid)
+                self.probes.add_pod(pod)
                 try:
                     await self.dm.admit_pod(pod)  # refresh plugin annotations, best effort
                 except Exception:
@@ -1257,7 +1260,7 @@ class Kubelet:
             # ContainerCreating and the sync is retried
             self.sync_errors[uid] = str(e)
             rt = await self._cached_status(uid)
-            st = generate_status(pod, rt, self.cfg.node_ip, self.readiness.get(uid, {}), [], m.now_rfc3339())
+            st = generate_status(pod, rt, self.cfg.node_ip, self.probes.readiness_of(uid, pod, rt), [], m.now_rfc3339())
             self.status.set(pod, st)
             asyncio.get_running_loop().call_later(2.0, self.dispatch, uid)
             return False
@@ -1279,7 +1282,7 @@ class Kubelet:
             except asyncio.TimeoutError:
                 pass
         try:
-            errors = await self.runtime.sync_pod(pod, rt, ctx, self.liveness_failed.pop(uid, None))
+            errors = await self.runtime.sync_pod(pod, rt, ctx, self.probes.liveness_failed)
         finally:
             self._device_start_done(uid)
         if self.cri.pod_mutations(uid) != mut0 or errors:
@@ -1290,7 +1293,7 @@ class Kubelet:
             rt = new_rt if new_rt is not None else await self._cached_status(uid, fresh=True)
         for sb in rt.sandboxes:
             self._sandbox_uid[sb[0]] = uid
-        st = generate_status(pod, rt, self.cfg.node_ip, self.readiness.get(uid, {}), errors, m.now_rfc3339(),
+        st = generate_status(pod, rt, self.cfg.node_ip, self.probes.readiness_of(uid, pod, rt), errors, m.now_rfc3339(),
                              self.runtime.reasons.get(uid))
         prev_phase = (self.status.get(uid) or {}).get("phase")
         self.status.set(pod, st)
@@ -1512,7 +1515,7 @@ class Kubelet:
         self.admitted.discard(uid)
         self.rejected.pop(uid, None)
         self.status.forget(uid)
-        self.readiness.pop(uid, None)
+        self.probes.remove_pod(uid)
         self.runtime.reasons.pop(uid, None)
         for k in [k for k in self.runtime.pull_backoff if k[0] == uid]:
             del self.runtime.pull_backoff[k]
@@ -1520,8 +1523,6 @@ class Kubelet:
         self.terminated_deleted.discard(uid)
         self.sync_errors.pop(uid, None)
         self._deadline_timers.discard(uid)
-        for k in [k for k in self._probe_state if k[0] == uid]:
-            del self._probe_state[k]
 
     # ---------------------------------------------------- volumes / env context
     async def _pod_context(self, pod: dict) -> dict:
@@ -1700,66 +1701,11 @@ class Kubelet:
             self.last_sync_loop = time.time()
 
     # ================================================================ probes
-    async def _probe(self, uid, cname, probe) -> bool:
-        rt = None
-        try:
-            if "exec" in probe:
-                rt = rt or await self.runtime.pod_status(uid)
-                cs = rt.latest(cname)
-                if cs is None:
-                    return False
-                _, _, rc = await self.cri.exec_sync(cs.id, probe["exec"].get("command") or [], int(probe.get("timeoutSeconds", 1)))
-                return rc == 0
-            if "httpGet" in probe:
-                h = probe["httpGet"]
-                url = f"{h.get('scheme', 'HTTP').lower()}://{h.get('host') or self.cfg.node_ip}:{h.get('port')}{h.get('path', '/')}"
-                async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=probe.get("timeoutSeconds", 1))) as s:
-                    async with s.get(url) as r:
-                        return 200 <= r.status < 400
-            if "tcpSocket" in probe:
-                t = probe["tcpSocket"]
-                _, w = await asyncio.wait_for(asyncio.open_connection(t.get("host") or self.cfg.node_ip, int(t.get("port"))),
-                                              probe.get("timeoutSeconds", 1))
-                w.close()
-                return True
-        except Exception:
-            return False
-        return True
-
-    async def _prober_loop(self):
-        while True:
-            await asyncio.sleep(0.5)
-            now = time.time()
-            for uid, pod in list(self.pods.items()):
-                st = self.status.get(uid) or {}
-                if st.get("phase") != "Running":
-                    continue
-                running = {cs["name"]: cs for cs in st.get("containerStatuses") or [] if "running" in (cs.get("state") or {})}
-                for c in (pod.get("spec") or {}).get("containers") or []:
-                    if c["name"] not in running:
-                        continue
-                    for kind in ("readinessProbe", "livenessProbe"):
-                        pr = c.get(kind)
-                        if not pr:
-                            continue
-                        key = (uid, c["name"], kind)
-                        ps = self._probe_state.setdefault(key, {"next": now + pr.get("initialDelaySeconds", 0), "fail": 0, "ok": 0})
-                        if now < ps["next"]:
-                            continue
-                        ps["next"] = now + pr.get("periodSeconds", 10)
-                        ok = await self._probe(uid, c["name"], pr)
-                        ps["ok"], ps["fail"] = (ps["ok"] + 1, 0) if ok else (0, ps["fail"] + 1)
-                        if kind == "readinessProbe":
-                            prev = self.readiness.setdefault(uid, {}).get(c["name"])
-                            val = ps["ok"] >= pr.get("successThreshold", 1) if ok else not (ps["fail"] >= pr.get("failureThreshold", 3)) and bool(prev)
-                            if prev != val:
-                                self.readiness[uid][c["name"]] = val
-                                self.dispatch(uid)
-                        elif ps["fail"] >= pr.get("failureThreshold", 3):
-                            ps["fail"] = 0
-                            self.liveness_failed.setdefault(uid, set()).add(c["name"])
-                            self.recorder.event(pod, "Warning", "Unhealthy", f"Liveness probe failed for container {c['name']}")
-                            self.dispatch(uid)
+    async def _probe_exec(self, cid: str, cmd: list, timeout: float):
+        """The prober's exec runner (RunInContainer): combined output and exit status."""
+        out, err, code = await self.cri.exec_sync(cid.split("://", 1)[-1], cmd, max(1, int(timeout)))
+        text = b"".join(x if isinstance(x, bytes) else (x or "").encode() for x in (out, err))
+        return text.decode(errors="replace"), code
 
     # ================================================================ eviction
     async def _eviction_loop(self):

@@ -22,6 +22,7 @@ import time
 import grpc
 
 from ..security.apparmor import profile_name as apparmor_profile_name
+from ..utils.flowcontrol import Backoff
 from ..utils.trace import POD_TRACE
 from .sysctl import pod_sysctls
 from .qos import cgroup_parent
@@ -93,7 +94,7 @@ class PodRuntimeStatus:
     def __init__(self, uid):
         self.uid = uid
         self.sandboxes = []  # newest first: (id, state, attempt, created_at)
-        self.ip = ""        # the ready sandbox's pod IP (network plugin / CNI result)
+        self.ip = None      # the ready sandbox's pod IP (network plugin / CNI result); None = not known
         self.containers: dict[str, list[ContainerRuntimeStatus]] = {}  # name -> newest first
 
     def ready_sandbox(self):
@@ -149,8 +150,184 @@ def apply_event(rt: PodRuntimeStatus, ev, sandbox_ips: dict) -> PodRuntimeStatus
     if not gone and sst.state == C.SANDBOX_READY and sst.network.ip:
         sandbox_ips.setdefault(sid, sst.network.ip)
     ready = new.ready_sandbox()
-    new.ip = sandbox_ips.get(ready[0], "") if ready is not None else ""
+    new.ip = sandbox_ips.get(ready[0]) if ready is not None else ""
     return new
+
+
+def _go_duration(sec: float) -> str:
+    """time.Duration.String() for whole seconds: 10s, 1m20s, 5m0s."""
+    s = int(round(sec))
+    if s < 60:
+        return f"{s}s"
+    h, rem = divmod(s, 3600)
+    mnt, s = divmod(rem, 60)
+    return (f"{h}h" if h else "") + f"{mnt}m{s}s"
+
+
+def stable_key(pod: dict, c: dict) -> str:
+    """kuberuntime_manager.go getStableKey: the back-off key of one container spec of one pod
+    (a spec change starts a fresh back-off)."""
+    md = pod["metadata"]
+    return f"{md['name']}_{md.get('namespace', '')}_{md['uid']}_{c['name']}_{container_hash(c)}"
+
+
+class PodActions:
+    """kuberuntime_manager.go podActions (:356-379)."""
+    __slots__ = ("kill_pod", "create_sandbox", "sandbox_id", "attempt", "next_init", "to_start", "to_kill")
+
+    def __init__(self, kill_pod=False, create_sandbox=False, sandbox_id="", attempt=0, next_init=None,
+                 to_start=None, to_kill=None):
+        self.kill_pod, self.create_sandbox, self.sandbox_id, self.attempt = kill_pod, create_sandbox, sandbox_id, attempt
+        self.next_init = next_init                  # the init container (spec dict) to start next
+        self.to_start: list[int] = to_start if to_start is not None else []   # indexes into spec.containers
+        self.to_kill: dict[str, tuple] = to_kill if to_kill is not None else {}   # cid -> (name, spec, message)
+
+    def key(self, with_messages: bool = False):
+        kill = {cid: (v[0], v[1]["name"] if v[1] else None) + ((v[2],) if with_messages else ())
+                for cid, v in self.to_kill.items()}
+        return (self.kill_pod, self.create_sandbox, self.sandbox_id, self.attempt,
+                self.next_init["name"] if self.next_init else None, list(self.to_start), kill)
+
+    def __eq__(self, other):
+        return isinstance(other, PodActions) and self.key() == other.key()
+
+    def __repr__(self):
+        return "PodActions(kill_pod=%r, create_sandbox=%r, sandbox_id=%r, attempt=%r, next_init=%r, to_start=%r, to_kill=%r)" % self.key(True)
+
+
+def should_restart_on_failure(pod: dict) -> bool:
+    return ((pod.get("spec") or {}).get("restartPolicy") or "Always") != "Never"
+
+
+def _failed(cs) -> bool:
+    return cs.state == C.CONTAINER_EXITED and cs.exit_code != 0
+
+
+def should_container_be_restarted(c: dict, pod: dict, st: PodRuntimeStatus) -> bool:
+    """kubelet/container/helpers.go ShouldContainerBeRestarted (:65-94)."""
+    cs = st.latest(c["name"])
+    if cs is None:
+        return True
+    if cs.state == C.CONTAINER_RUNNING:
+        return False
+    if cs.state in (C.CONTAINER_UNKNOWN, C.CONTAINER_CREATED):
+        return True
+    policy = (pod.get("spec") or {}).get("restartPolicy") or "Always"
+    if policy == "Never":
+        return False
+    if policy == "OnFailure" and cs.exit_code == 0:
+        return False
+    return True
+
+
+def find_next_init_container(pod: dict, st: PodRuntimeStatus):
+    """kuberuntime_container.go findNextInitContainerToRun (:720-759): (status of the last
+    failed init container, next init container to run, done)."""
+    inits = (pod.get("spec") or {}).get("initContainers") or []
+    if not inits:
+        return None, None, True
+    for ic in reversed(inits):
+        cs = st.latest(ic["name"])
+        if cs is not None and _failed(cs):
+            return cs, ic, False
+    for i in range(len(inits) - 1, -1, -1):
+        cs = st.latest(inits[i]["name"])
+        if cs is None:
+            continue
+        if cs.state == C.CONTAINER_RUNNING:
+            return None, None, False
+        if cs.state == C.CONTAINER_EXITED:
+            if i == len(inits) - 1:
+                return None, None, True
+            return None, inits[i + 1], False
+    return None, inits[0], False
+
+
+def pod_sandbox_changed(pod: dict, st: PodRuntimeStatus):
+    """kuberuntime_manager.go podSandboxChanged (:383-421): (create, attempt, sandbox id).
+    A newest sandbox that is not ready, more than one ready sandbox, or a non-host-network
+    sandbox without an IP means a new sandbox."""
+    if not st.sandboxes:
+        return True, 0, ""
+    sid, state, attempt = st.sandboxes[0][0], st.sandboxes[0][1], st.sandboxes[0][2]
+    if sum(1 for s in st.sandboxes if s[1] == C.SANDBOX_READY) > 1:
+        return True, attempt + 1, sid
+    if state != C.SANDBOX_READY:
+        return True, attempt + 1, sid
+    if not (pod.get("spec") or {}).get("hostNetwork") and st.ip == "":
+        return True, attempt + 1, sid
+    return False, attempt, sid
+
+
+def compute_pod_actions(pod: dict, st: PodRuntimeStatus, liveness_failed=None) -> PodActions:
+    """kuberuntime_manager.go computePodActions (:441-558).
+
+    * a changed sandbox kills and recreates the pod (init containers from the first; under
+      OnFailure the succeeded containers stay done) — unless the policy is Never and the pod
+      already ran once, then it is only killed;
+    * init containers run one at a time; a failed one under Never kills the pod;
+    * a dead container is started when ShouldContainerBeRestarted says so;
+    * a running container whose spec hash changed is killed and always recreated; one that
+      failed its liveness probe is killed and recreated only when restartPolicy != Never;
+    * with nothing left running and nothing to start, the pod is killed.
+
+    `liveness_failed`: container ids (or a predicate over them) whose liveness is Failure."""
+    is_failed = (liveness_failed if callable(liveness_failed)
+                 else (lambda cid, s=liveness_failed or (): cid in s))
+    spec = pod.get("spec") or {}
+    create, attempt, sid = pod_sandbox_changed(pod, st)
+    acts = PodActions(kill_pod=create, create_sandbox=create, sandbox_id=sid, attempt=attempt)
+    conts = spec.get("containers") or []
+    if create:
+        if not should_restart_on_failure(pod) and attempt != 0:
+            # a Never pod that already ran is not restarted; the reference returns with
+            # CreateSandbox still set and relies on syncPod never reaching here for a finished
+            # pod — amdkube does not recreate a sandbox it will not use (later upstream fix)
+            acts.create_sandbox = False
+            return acts
+        inits = spec.get("initContainers") or []
+        if inits:
+            acts.next_init = inits[0]
+            return acts
+        onfail = spec.get("restartPolicy") == "OnFailure"
+        for i, c in enumerate(conts):
+            cs = st.latest(c["name"])
+            if onfail and cs is not None and cs.state != C.CONTAINER_RUNNING and cs.exit_code == 0:
+                continue
+            acts.to_start.append(i)
+        return acts
+    last, nxt, done = find_next_init_container(pod, st)
+    if not done:
+        if nxt is not None:
+            if last is not None and _failed(last) and not should_restart_on_failure(pod):
+                acts.kill_pod = True
+            else:
+                acts.next_init = nxt
+        return acts
+    keep = 0
+    for i, c in enumerate(conts):
+        cs = st.latest(c["name"])
+        if cs is None or cs.state != C.CONTAINER_RUNNING:
+            if should_container_be_restarted(c, pod, st):
+                acts.to_start.append(i)
+            continue
+        restart = should_restart_on_failure(pod)
+        if cs.hash and cs.hash != container_hash(c):
+            reason = f"Container spec hash changed ({cs.hash} vs {container_hash(c)})."
+            restart = True
+        elif is_failed(cs.id):
+            reason = "Container failed liveness probe."
+        else:
+            keep += 1
+            continue
+        message = reason
+        if restart:
+            message = f"{message}. Container will be killed and recreated."
+            acts.to_start.append(i)
+        acts.to_kill[cs.id] = (cs.name, c, message)
+    if keep == 0 and not acts.to_start:
+        acts.kill_pod = True
+    return acts
 
 
 IMAGE_BACKOFF_BASE, IMAGE_BACKOFF_MAX = 10.0, 300.0
@@ -190,7 +367,10 @@ class RuntimeManager:
         self.dm = device_manager
         self.root = root_dir
         self.recorder = recorder
-        self.backoff: dict[tuple[str, str], tuple[float, float]] = {}  # (uid, name) -> (until, last delay)
+        # kubelet.go:859 the container restart back-off (10 s doubling to 300 s), keyed by
+        # stable_key; (uid, name) -> (key, event time) of a start it is holding back
+        self.backoff = Backoff(BACKOFF_BASE, BACKOFF_MAX)
+        self._backoff_due: dict[tuple[str, str], tuple[str, float]] = {}
         self.sandbox_ips: dict[str, str] = {}   # sandbox id -> IP (PodSandboxStatus is asked once per sandbox)
         self.seccomp_root = os.path.join(root_dir, "seccomp")   # --seccomp-profile-root
         self._image_seen: dict[str, float] = {}
@@ -221,10 +401,10 @@ class RuntimeManager:
                 try:
                     ip = (await self.cri.pod_sandbox_status(ready[0])).network.ip
                 except grpc.RpcError:
-                    ip = ""
+                    ip = None       # unknown: not a reason to recreate the sandbox
                 if ip:
                     self.sandbox_ips[ready[0]] = ip
-            st.ip = ip or ""
+            st.ip = ip
         if len(self.cri._cid_sid) > 100000:
             self.cri._cid_sid.clear()
         for s in sbs:
@@ -454,111 +634,152 @@ class RuntimeManager:
         return "a lifecycle handler needs exec or httpGet"
 
     # ------------------------------------------------------------------ sync
-    async def sync_pod(self, pod: dict, st: PodRuntimeStatus, ctx: dict, liveness_failed: set | None = None) -> list[str]:
-        """One reconciliation step. Returns errors (pod-level messages)."""
-        errors = []
+    async def sync_pod(self, pod: dict, st: PodRuntimeStatus, ctx: dict, liveness_failed=None) -> list[str]:
+        """kuberuntime_manager.go SyncPod (:568-741): compute the actions, then (2) kill the
+        pod when the sandbox changed or nothing is left to run, (3) kill the containers that
+        must not keep running, (4) create the sandbox, (5) start the next init container,
+        (6) start the containers to start — each start behind doBackOff. Returns pod-level
+        error messages. `liveness_failed`: the container ids whose liveness result is Failure
+        (the probe manager's results cache)."""
+        errors: list[str] = []
         spec = pod.get("spec") or {}
         uid = pod["metadata"]["uid"]
-        policy = spec.get("restartPolicy", "Always")
-        sb = st.ready_sandbox()
-        ever_ran = any(c.state == C.CONTAINER_EXITED for lst in st.containers.values() for c in lst)
-        if sb is None:
-            if policy == "Never" and ever_ran:
-                return errors  # terminal; never recreate the sandbox
-            for c in st.running():
-                await self.cri.stop_container(c.id, 2)
-            attempt = (st.sandboxes[0][2] + 1) if st.sandboxes else 0
-            sandbox_cfg = self.sandbox_config(pod, attempt, self.dm.pod_resources(pod))
+        acts = compute_pod_actions(pod, st, liveness_failed)
+        if acts.create_sandbox and acts.sandbox_id and self.recorder is not None:
+            self.recorder.event(pod, "Normal", "SandboxChanged", "Pod sandbox changed, it will be killed and re-created.")
+        if acts.kill_pod and not acts.create_sandbox:
+            # nothing left to run: the pod is finished. Its containers are stopped here; the
+            # sandbox goes with the kubelet's terminal-phase release right after the status
+            # (which still reports the sandbox's IP) is generated
+            for cs in st.running():
+                c = next((x for x in spec.get("containers") or [] if x["name"] == cs.name), None)
+                msg = acts.to_kill.get(cs.id, (None, None, ""))[2]
+                try:
+                    await self.kill_container(pod, cs.id, c, msg)
+                except grpc.RpcError as e:
+                    errors.append(f"kill {cs.name}: {e.details()}")
+            return errors
+        if acts.kill_pod:
+            if st.sandboxes or st.running():
+                grace = int(spec.get("terminationGracePeriodSeconds", 30))
+                await self.kill_pod(uid, grace, pod, [SandboxRef(x[0], x[1]) for x in st.sandboxes], clear_backoff=False)
+                for c in st.running():     # containers whose sandbox is already gone
+                    if all(c.sandbox_id != x[0] or x[1] != C.SANDBOX_READY for x in st.sandboxes):
+                        await self.cri.stop_container(c.id, 0)
+            if acts.create_sandbox:
+                await self._purge_init_containers(pod, st)
+        else:
+            for cid, (name, c, message) in acts.to_kill.items():
+                try:
+                    await self.kill_container(pod, cid, c, message)
+                except grpc.RpcError as e:
+                    errors.append(f"kill {name}: {e.details()}")
+                    return errors
+        if not acts.create_sandbox and acts.next_init is None and not acts.to_start:
+            return errors
+        sid = acts.sandbox_id
+        if acts.create_sandbox:
+            sandbox_cfg = self.sandbox_config(pod, acts.attempt, self.dm.pod_resources(pod))
             POD_TRACE(uid, "sandbox_start")
             try:
                 sid = await self.cri.run_pod_sandbox(sandbox_cfg)
             except grpc.RpcError as e:
-                # kuberuntime_manager.go createPodSandbox: FailedCreatePodSandBox event, pod stays
-                # Pending, the next sync retries
+                # createPodSandbox failed: FailedCreatePodSandBox event; the pod stays Pending and
+                # the next sync retries
                 msg = f"Failed create pod sandbox: {e.details() if hasattr(e, 'details') else e}"
                 if self.recorder is not None:
                     self.recorder.event(pod, "Warning", "FailedCreatePodSandBox", msg)
                 errors.append(msg)
                 return errors
             POD_TRACE(uid, "sandbox_ready")
-            st = PodRuntimeStatus(uid)
-            st.sandboxes = [(sid, C.SANDBOX_READY, attempt, time.time_ns())]
         else:
-            sid = sb[0]
-            sandbox_cfg = self.sandbox_config(pod, sb[2], self.dm.pod_resources(pod))
-        # init containers, strictly in order
-        for ic in spec.get("initContainers") or []:
-            cur = st.latest(ic["name"])
-            if cur is not None and cur.state == C.CONTAINER_RUNNING:
-                return errors
-            if cur is not None and cur.state == C.CONTAINER_EXITED and cur.exit_code == 0:
+            sandbox_cfg = self.sandbox_config(pod, acts.attempt, self.dm.pod_resources(pod))
+        conts = spec.get("containers") or []
+        targets = ([(acts.next_init, True)] if acts.next_init is not None else []) + [(conts[i], False) for i in acts.to_start]
+        for c, init in targets:
+            if self.do_backoff(pod, c, st):
+                if init:
+                    return errors
                 continue
-            if cur is not None and cur.state == C.CONTAINER_EXITED:
-                if policy == "Never":
-                    return errors
-                if not self._backoff_ok(uid, ic["name"]):
-                    return errors
-            rc = (cur.restart_count + 1) if cur is not None else 0
-            try:
-                await self.start_container(pod, ic, sid, sandbox_cfg, ctx, rc, True)
-                self._clear_reason(uid, ic["name"])
-            except Exception as e:
-                self.reasons.setdefault(uid, {})[ic["name"]] = start_error_reason(e)
-                errors.append(f"init container {ic['name']}: {e}")
-            return errors
-        for c in spec.get("containers") or []:
+            # startContainer: the attempt carries over from the newest instance of this container
             cur = st.latest(c["name"])
-            h = container_hash(c)
-            if cur is not None and cur.state == C.CONTAINER_RUNNING:
-                if cur.hash and cur.hash != h or (liveness_failed and c["name"] in liveness_failed):
-                    await self.cri.stop_container(cur.id, int(spec.get("terminationGracePeriodSeconds", 30)))
-                    if self.recorder:
-                        self.recorder.event(pod, "Normal", "Killing", f"Killing container {c['name']} (spec changed or liveness failed)")
-                else:
-                    continue
-                cur = None if policy != "Never" else cur
-            if cur is not None and cur.state in (C.CONTAINER_EXITED, C.CONTAINER_UNKNOWN):
-                if policy == "Never" or (policy == "OnFailure" and cur.exit_code == 0):
-                    continue
-                if not self._backoff_ok(uid, c["name"]):
-                    continue
-            elif cur is not None and cur.state == C.CONTAINER_CREATED:
-                try:
-                    await self.cri.start_container(cur.id)
-                except grpc.RpcError as e:
-                    errors.append(f"start {c['name']}: {e.details()}")
-                continue
             rc = (cur.restart_count + 1) if cur is not None else 0
             try:
-                await self.start_container(pod, c, sid, sandbox_cfg, ctx, rc, False)
+                await self.start_container(pod, c, sid, sandbox_cfg, ctx, rc, init)
                 self._clear_reason(uid, c["name"])
             except grpc.RpcError as e:
                 self.reasons.setdefault(uid, {})[c["name"]] = start_error_reason(e)
-                errors.append(f"container {c['name']}: {e.details()}")
+                errors.append(f"{'init container' if init else 'container'} {c['name']}: {e.details()}")
             except Exception as e:
                 self.reasons.setdefault(uid, {})[c["name"]] = start_error_reason(e)
-                errors.append(f"container {c['name']}: {e}")
+                errors.append(f"{'init container' if init else 'container'} {c['name']}: {e}")
+            if init:
+                break
         return errors
+
+    async def _purge_init_containers(self, pod: dict, st: PodRuntimeStatus):
+        """kuberuntime_container.go purgeInitContainers: a new sandbox runs its init containers
+        again from the first, so the old instances must not count as done."""
+        names = {ic["name"] for ic in (pod.get("spec") or {}).get("initContainers") or []}
+        for n in names:
+            for cs in st.containers.get(n) or []:
+                if cs.state != C.CONTAINER_RUNNING:
+                    try:
+                        await self.cri.remove_container(cs.id)
+                    except grpc.RpcError as e:
+                        log.debug("purge init container %s: %s", cs.id, e.details())
+
+    async def kill_container(self, pod: dict, cid: str, c: dict | None, reason: str = "", grace: int | None = None):
+        """kuberuntime_container.go killContainer: preStop hook bounded by the grace period,
+        then StopContainer, with a Killing event naming the reason."""
+        spec = pod.get("spec") or {}
+        if grace is None:
+            grace = int(spec.get("terminationGracePeriodSeconds", 30))
+        if self.recorder is not None:
+            msg = f"Killing container with id rocshim://{cid}" + (f":{reason}" if reason else "")
+            self.recorder.event(pod, "Normal", "Killing", msg)
+        pre = ((c or {}).get("lifecycle") or {}).get("preStop")
+        if pre:
+            ip = self.sandbox_ips.get(self.cri._cid_sid.get(cid, "")) or self.node_ip
+            err = await self.run_handler(pod, c, cid, pre, ip, min(grace, 30) or 1)
+            if err and self.recorder:
+                self.recorder.event(pod, "Warning", "FailedPreStopHook", err)
+        await self.cri.stop_container(cid, grace)
 
     def _clear_reason(self, uid: str, name: str):
         r = self.reasons.get(uid)
         if r and r.pop(name, None) is not None and not r:
             del self.reasons[uid]
 
-    def _backoff_ok(self, uid, name) -> bool:
-        now = time.monotonic()
-        until, last = self.backoff.get((uid, name), (0.0, 0.0))
-        if now < until:
+    def do_backoff(self, pod: dict, c: dict, st: PodRuntimeStatus) -> bool:
+        """kuberuntime_manager.go doBackOff (:745-774): with the finish time of the newest
+        exited instance as the event time, a container still inside its back-off is not
+        started (BackOff event, CrashLoopBackOff waiting reason); otherwise the back-off
+        advances (Next) and the start goes ahead."""
+        last = next((x for x in st.containers.get(c["name"]) or [] if x.state == C.CONTAINER_EXITED), None)
+        if last is None:
             return False
-        delay = min(BACKOFF_MAX, last * 2 if last else BACKOFF_BASE)
-        self.backoff[(uid, name)] = (now + delay, delay)
-        return True
+        ts = last.finished_at / 1e9 if last.finished_at else time.time()
+        key = stable_key(pod, c)
+        md = pod["metadata"]
+        if self.backoff.is_in_backoff_since(key, ts):
+            if self.recorder is not None:
+                self.recorder.event(pod, "Warning", "BackOff", "Back-off restarting failed container")
+            msg = (f"Back-off {_go_duration(self.backoff.get(key))} restarting failed container={c['name']} "
+                   f"pod={md['name']}_{md.get('namespace', '')}({md['uid']})")
+            self.reasons.setdefault(md["uid"], {})[c["name"]] = ("CrashLoopBackOff", msg)
+            self._backoff_due[(md["uid"], c["name"])] = (key, ts)
+            return True
+        self.backoff.next(key, ts)
+        self._backoff_due.pop((md["uid"], c["name"]), None)
+        return False
 
     def backoff_remaining(self, uid, name) -> float:
-        until, _ = self.backoff.get((uid, name), (0.0, 0.0))
-        return max(0.0, until - time.monotonic())
+        """Seconds until a container held back by do_backoff may start (0 when none is held)."""
+        due = self._backoff_due.get((uid, name))
+        return self.backoff.remaining(*due) if due else 0.0
 
-    async def kill_pod(self, uid: str, grace: int = 30, pod: dict | None = None, sandboxes=None):
+    async def kill_pod(self, uid: str, grace: int = 30, pod: dict | None = None, sandboxes=None, clear_backoff: bool = True):
         sbs = sandboxes if sandboxes is not None else await self.cri.list_pod_sandbox(uid)
         hooks = pod is not None and any(((sc.get("lifecycle") or {}).get("preStop"))
                                         for sc in (pod.get("spec") or {}).get("containers") or [])
@@ -570,8 +791,10 @@ class RuntimeManager:
                 await asyncio.gather(*(self._kill_container(pod, c, grace) for c in conts if c.state == C.CONTAINER_RUNNING))
             # grace 0 and no preStop hook: StopPodSandbox kills the containers itself (one RPC, not 2 + N)
             await self.cri.stop_pod_sandbox(s.id)
-        for k in [k for k in self.backoff if k[0] == uid]:
-            del self.backoff[k]
+        if clear_backoff:
+            self.backoff.drop_prefix_containing(f"_{uid}_")
+            for k in [k for k in self._backoff_due if k[0] == uid]:
+                del self._backoff_due[k]
 
     async def kill_and_remove(self, uid: str, sandboxes=None):
         """The pod is gone from the API: one list, stop what still runs, remove everything."""

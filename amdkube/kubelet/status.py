@@ -24,9 +24,21 @@ def _ts(ns: int) -> str | None:
     return time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(ns / 1e9))
 
 
+def _terminated(rs) -> dict:
+    term = {"exitCode": rs.exit_code, "reason": rs.reason or ("Completed" if rs.exit_code == 0 else "Error"),
+            "startedAt": _ts(rs.started_at), "finishedAt": _ts(rs.finished_at), "containerID": f"rocshim://{rs.id}"}
+    if rs.message:
+        term["message"] = rs.message
+    return term
+
+
 def container_status(spec_c: dict, rs, ready: bool, will_restart: bool, waiting_reason: str,
-                     last_error: tuple[str, str] | None = None) -> dict:
+                     last_error: tuple[str, str] | None = None, prev=None) -> dict:
+    """convertToAPIContainerStatuses (kubelet_pods.go:1464-1605): the newest instance is the
+    state, the one before it the lastState; a container that will be restarted waits."""
     out = {"name": spec_c["name"], "image": spec_c.get("image", ""), "imageID": "", "ready": False, "restartCount": 0}
+    if prev is not None and prev.state in (C.CONTAINER_EXITED, C.CONTAINER_UNKNOWN, C.CONTAINER_CREATED):
+        out["lastState"] = {"terminated": _terminated(prev)}
     if rs is None:
         # reason_cache.go: a container that failed to start waits with that failure's reason
         out["state"] = {"waiting": {"reason": last_error[0], "message": last_error[1]} if last_error
@@ -39,10 +51,7 @@ def container_status(spec_c: dict, rs, ready: bool, will_restart: bool, waiting_
         out["state"] = {"running": {"startedAt": _ts(rs.started_at)}}
         out["ready"] = ready
     elif rs.state in (C.CONTAINER_EXITED, C.CONTAINER_UNKNOWN):
-        term = {"exitCode": rs.exit_code, "reason": rs.reason or ("Completed" if rs.exit_code == 0 else "Error"),
-                "startedAt": _ts(rs.started_at), "finishedAt": _ts(rs.finished_at), "containerID": f"rocshim://{rs.id}"}
-        if rs.message:
-            term["message"] = rs.message
+        term = _terminated(rs)
         if will_restart:
             out["state"] = {"waiting": {"reason": last_error[0], "message": last_error[1]} if last_error else
                             {"reason": "CrashLoopBackOff" if rs.exit_code else "Completed",
@@ -53,6 +62,11 @@ def container_status(spec_c: dict, rs, ready: bool, will_restart: bool, waiting_
     else:
         out["state"] = {"waiting": {"reason": "ContainerCreating"}}
     return out
+
+
+def _prev(rt, name):
+    lst = rt.containers.get(name) if rt is not None else None
+    return lst[1] if lst and len(lst) > 1 else None
 
 
 def generate_status(pod: dict, rt, node_ip: str, readiness: dict, errors: list[str], now: str,
@@ -94,7 +108,7 @@ def generate_status(pod: dict, rt, node_ip: str, readiness: dict, errors: list[s
             # (reference prober/worker.go: readiness initialValue = results.Failure)
             ready = readiness.get(c["name"], not c.get("readinessProbe"))
             all_ready &= ready
-            statuses.append(container_status(c, rs, ready, False, ""))
+            statuses.append(container_status(c, rs, ready, False, "", prev=_prev(rt, c["name"])))
         elif rs.state in (C.CONTAINER_EXITED, C.CONTAINER_UNKNOWN):
             all_ready = False
             if rs.exit_code == 0:
@@ -102,7 +116,8 @@ def generate_status(pod: dict, rt, node_ip: str, readiness: dict, errors: list[s
             else:
                 failed_n += 1
             restart = policy == "Always" or (policy == "OnFailure" and rs.exit_code != 0)
-            statuses.append(container_status(c, rs, False, restart, "", reasons.get(c["name"])))
+            statuses.append(container_status(c, rs, False, restart, "", reasons.get(c["name"]),
+                                             prev=None if restart else _prev(rt, c["name"])))
         else:
             waiting += 1
             all_ready = False

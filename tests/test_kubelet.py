@@ -93,19 +93,14 @@ def test_restart_policy_init_containers_probes_and_volumes():
             await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "crash", "namespace": "default"},
                             "spec": {"restartPolicy": "OnFailure", "containers": [{"name": "c", "image": "busybox", "command": ["sh", "-c", "exit 1"]}]}})
             lc.kubelet.runtime.backoff.clear()
-            import amdkube.kubelet.kuberuntime as kr
-            old = kr.BACKOFF_BASE
-            kr.BACKOFF_BASE = 0.2
-            try:
-                for _ in range(150):
-                    p = await c.get("pods", "crash", "default")
-                    cs = (p["status"].get("containerStatuses") or [{}])[0]
-                    if cs.get("restartCount", 0) >= 1:
-                        break
-                    await asyncio.sleep(0.1)
-                assert cs.get("restartCount", 0) >= 1, p["status"]
-            finally:
-                kr.BACKOFF_BASE = old
+            lc.kubelet.runtime.backoff.default = 0.2
+            for _ in range(150):
+                p = await c.get("pods", "crash", "default")
+                cs = (p["status"].get("containerStatuses") or [{}])[0]
+                if cs.get("restartCount", 0) >= 1:
+                    break
+                await asyncio.sleep(0.1)
+            assert cs.get("restartCount", 0) >= 1, p["status"]
     run(go(), 120)
 
 
