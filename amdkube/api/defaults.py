@@ -60,6 +60,11 @@ def default_pod_spec(spec: dict):
     spec.setdefault("securityContext", {})
     for c in spec.get("containers") or []:
         _default_container(c)
+        if spec.get("hostNetwork"):
+            # SetDefaults_PodSpec: a host-network pod's hostPort is its containerPort
+            for port in c.get("ports") or []:
+                if not port.get("hostPort"):
+                    port["hostPort"] = port.get("containerPort", 0)
     for c in spec.get("initContainers") or []:
         _default_container(c)
     # fork: ExtendedResources requests := limits (defaults.go:164-179)
@@ -119,7 +124,10 @@ def default_daemonset(ds: dict):
         # OnDelete unless asked, and a templateGeneration
         ds["spec"].setdefault("updateStrategy", {"type": "OnDelete"})
         ds["spec"].setdefault("templateGeneration", 1)
-    ds["spec"].setdefault("updateStrategy", {"type": "RollingUpdate", "rollingUpdate": {"maxUnavailable": 1}})
+    us = ds["spec"].setdefault("updateStrategy", {"type": "RollingUpdate", "rollingUpdate": {"maxUnavailable": 1}})
+    us.setdefault("type", "RollingUpdate")
+    if us["type"] == "RollingUpdate":
+        us.setdefault("rollingUpdate", {}).setdefault("maxUnavailable", 1)
     ds["spec"].setdefault("revisionHistoryLimit", 10)
     return ds
 
@@ -130,8 +138,13 @@ def default_replicaset(rs: dict):
 
 def default_deployment(d: dict):
     _default_template_owner(d)
-    d["spec"].setdefault("strategy", {"type": "RollingUpdate",
-                                      "rollingUpdate": {"maxUnavailable": "25%", "maxSurge": "25%"}})
+    st = d["spec"].setdefault("strategy", {"type": "RollingUpdate",
+                                           "rollingUpdate": {"maxUnavailable": "25%", "maxSurge": "25%"}})
+    st.setdefault("type", "RollingUpdate")
+    if st["type"] == "RollingUpdate":
+        ru = st.setdefault("rollingUpdate", {})
+        ru.setdefault("maxUnavailable", "25%")
+        ru.setdefault("maxSurge", "25%")
     d["spec"].setdefault("revisionHistoryLimit", 10)
     d["spec"].setdefault("progressDeadlineSeconds", 600)
     return d
@@ -230,5 +243,124 @@ def default_pod_security_policy(psp: dict):
 for _gv in ("extensions/v1beta1", "policy/v1beta1"):
     try:
         register_hooks("PodSecurityPolicy", _gv, defaulter=default_pod_security_policy)
+    except KeyError:
+        pass
+
+
+# ---------------------------------------------------------------- the remaining served kinds
+# (pkg/apis/*/v1*/defaults.go): every object is defaulted before it is validated, so each kind
+# the validators require defaulted fields of gets its defaulter here
+def _default_template(tpl: dict | None):
+    if tpl is not None:
+        default_pod_spec(tpl.setdefault("spec", {}))
+
+
+def default_statefulset(sts: dict):
+    """apps/v1 SetDefaults_StatefulSet: OrderedReady, RollingUpdate with partition 0, 1 replica,
+    10 revisions, selector from the template labels."""
+    spec = sts.setdefault("spec", {})
+    spec.setdefault("replicas", 1)
+    spec.setdefault("podManagementPolicy", "OrderedReady")
+    us = spec.setdefault("updateStrategy", {"type": "RollingUpdate"})
+    us.setdefault("type", "RollingUpdate")
+    if us["type"] == "RollingUpdate":
+        us.setdefault("rollingUpdate", {}).setdefault("partition", 0)
+    spec.setdefault("revisionHistoryLimit", 10)
+    tpl = spec.setdefault("template", {})
+    _default_template(tpl)
+    if "selector" not in spec and (tpl.get("metadata") or {}).get("labels"):
+        spec["selector"] = {"matchLabels": dict(tpl["metadata"]["labels"])}
+    return sts
+
+
+def default_replication_controller(rc: dict):
+    """core/v1 SetDefaults_ReplicationController: selector (and labels) from the template,
+    one replica."""
+    spec = rc.setdefault("spec", {})
+    tpl = spec.get("template")
+    labels = ((tpl or {}).get("metadata") or {}).get("labels") or {}
+    if labels:
+        spec.setdefault("selector", dict(labels))
+        md = rc.setdefault("metadata", {})
+        if not md.get("labels"):
+            md["labels"] = dict(labels)
+    spec.setdefault("replicas", 1)
+    _default_template(tpl)
+    return rc
+
+
+def default_pod_template(pt: dict):
+    _default_template(pt.get("template"))
+    return pt
+
+
+def default_cronjob_template(cj: dict, history_limits: bool = True):
+    default_cronjob(cj, history_limits)
+    jt = cj["spec"].setdefault("jobTemplate", {}).setdefault("spec", {})
+    tpl = jt.setdefault("template", {})
+    tpl.setdefault("spec", {}).setdefault("restartPolicy", "OnFailure")
+    _default_template(tpl)
+    return cj
+
+
+def default_secret(s: dict):
+    if not s.get("type"):
+        s["type"] = "Opaque"
+    return s
+
+
+def default_endpoints(ep: dict):
+    for ss in ep.get("subsets") or []:
+        for p in ss.get("ports") or []:
+            p.setdefault("protocol", "TCP")
+    return ep
+
+
+def default_persistent_volume(pv: dict):
+    pv.setdefault("spec", {}).setdefault("persistentVolumeReclaimPolicy", "Retain")
+    pv.setdefault("status", {}).setdefault("phase", "Pending")
+    return pv
+
+
+def default_persistent_volume_claim(pvc: dict):
+    pvc.setdefault("status", {}).setdefault("phase", "Pending")
+    return pvc
+
+
+def default_hpa(hpa: dict):
+    spec = hpa.setdefault("spec", {})
+    if spec.get("minReplicas") is None:
+        spec["minReplicas"] = 1
+    return hpa
+
+
+def default_storage_class(sc: dict):
+    if not sc.get("reclaimPolicy"):
+        sc["reclaimPolicy"] = "Delete"
+    return sc
+
+
+def default_rbac_subjects(obj: dict):
+    """rbac/v1 SetDefaults_Subject: users and groups are in the rbac API group."""
+    for s in obj.get("subjects") or []:
+        if not s.get("apiGroup") and s.get("kind") in ("User", "Group"):
+            s["apiGroup"] = "rbac.authorization.k8s.io"
+    return obj
+
+
+register_hooks("StatefulSet", "apps/v1", defaulter=default_statefulset)
+register_hooks("ReplicationController", defaulter=default_replication_controller)
+register_hooks("PodTemplate", defaulter=default_pod_template)
+register_hooks("Secret", defaulter=default_secret)
+register_hooks("Endpoints", defaulter=default_endpoints)
+register_hooks("PersistentVolume", defaulter=default_persistent_volume)
+register_hooks("PersistentVolumeClaim", defaulter=default_persistent_volume_claim)
+register_hooks("HorizontalPodAutoscaler", "autoscaling/v1", defaulter=default_hpa)
+register_hooks("StorageClass", "storage.k8s.io/v1", defaulter=default_storage_class)
+register_hooks("RoleBinding", "rbac.authorization.k8s.io/v1", defaulter=default_rbac_subjects)
+register_hooks("ClusterRoleBinding", "rbac.authorization.k8s.io/v1", defaulter=default_rbac_subjects)
+for _gv, _limits in (("batch/v1beta1", True), ("batch/v2alpha1", False)):
+    try:
+        register_hooks("CronJob", _gv, defaulter=lambda cj, _l=_limits: default_cronjob_template(cj, _l))
     except KeyError:
         pass

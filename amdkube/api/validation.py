@@ -139,41 +139,6 @@ def validate_containers_extended_resources(containers, names: dict, path: str) -
 CAPABILITIES = {"allow_privileged": True}
 
 
-def _validate_container(c: dict, path: str, init: bool) -> list[str]:
-    errs = []
-    name = c.get("name") or ""
-    if not name:
-        errs.append(f"{path}.name: Required value")
-    else:
-        errs += [f"{path}.name: Invalid value: {gv(name)}: {e}" for e in is_dns1123_label(name)]
-    if not c.get("image"):
-        errs.append(f"{path}.image: Required value")
-    errs += validate_resource_requirements(c.get("resources"), path + ".resources")
-    ports = set()
-    for i, p in enumerate(c.get("ports") or []):
-        cp = p.get("containerPort")
-        if not isinstance(cp, int) or not 0 < cp < 65536:
-            errs.append(f"{path}.ports[{i}].containerPort: Invalid value: {gv(cp)}: must be between 1 and 65535")
-        hp = p.get("hostPort") or 0
-        if hp and not 0 < hp < 65536:
-            errs.append(f"{path}.ports[{i}].hostPort: Invalid value: {gv(hp)}")
-        if p.get("protocol", "TCP") not in ("TCP", "UDP", "SCTP"):
-            errs.append(f"{path}.ports[{i}].protocol: Unsupported value: {gv(p.get('protocol'))}")
-        key = (hp, p.get("protocol", "TCP"))
-        if hp and key in ports:
-            errs.append(f"{path}.ports[{i}].hostPort: Duplicate value: {hp}")
-        ports.add(key)
-    errs += validate_env(c.get("env") or [], path + ".env")
-    errs += validate_env_from(c.get("envFrom") or [], path + ".envFrom")
-    if init:
-        for probe in ("livenessProbe", "readinessProbe"):
-            if c.get(probe):
-                errs.append(f"{path}.{probe}: Invalid value: must not be set for init containers")
-    if (c.get("securityContext") or {}).get("privileged") and not CAPABILITIES["allow_privileged"]:
-        errs.append(f"{path}.securityContext.privileged: Forbidden: disallowed by cluster policy")
-    return errs
-
-
 _ENV_NAME_RE = re.compile(r"^[-._a-zA-Z][-._a-zA-Z0-9]*$")
 ENV_FIELD_PATHS = ("metadata.name", "metadata.namespace", "metadata.uid", "spec.nodeName", "spec.serviceAccountName",
                    "status.hostIP", "status.podIP")
@@ -375,103 +340,15 @@ def _validate_volume_items(v: dict, path: str) -> list[str]:
 
 
 def validate_pod_spec(spec: dict, path="spec") -> list[str]:
-    errs = []
-    containers = spec.get("containers") or []
-    inits = spec.get("initContainers") or []
-    if not containers:
-        errs.append(f"{path}.containers: Required value")
-    names = set()
-    for kind, lst in (("initContainers", inits), ("containers", containers)):
-        for i, c in enumerate(lst):
-            errs += _validate_container(c, f"{path}.{kind}[{i}]", kind == "initContainers")
-            n = c.get("name")
-            if n in names:
-                errs.append(f"{path}.{kind}[{i}].name: Duplicate value: {gv(n)}")
-            names.add(n)
-    rp = spec.get("restartPolicy", "Always")
-    if rp not in RESTART_POLICIES:
-        errs.append(f"{path}.restartPolicy: Unsupported value: {gv(rp)}")
-    vols = set()
-    for i, v in enumerate(spec.get("volumes") or []):
-        n = v.get("name") or ""
-        errs += [f"{path}.volumes[{i}].name: Invalid value: {gv(n)}: {e}" for e in is_dns1123_label(n)]
-        if n in vols:
-            errs.append(f"{path}.volumes[{i}].name: Duplicate value: {gv(n)}")
-        vols.add(n)
-        errs += _validate_volume_items(v, f"{path}.volumes[{i}]")
-    for kind, lst in (("initContainers", inits), ("containers", containers)):
-        for i, c in enumerate(lst):
-            for j, m in enumerate(c.get("volumeMounts") or []):
-                if m.get("name") not in vols:
-                    errs.append(f"{path}.{kind}[{i}].volumeMounts[{j}].name: Not found: {gv(m.get('name'))}")
-    for k, v in (spec.get("nodeSelector") or {}).items():
-        errs += [f"{path}.nodeSelector: Invalid value: {gv(k)}: {e}" for e in is_qualified_name(k)]
-        errs += [f"{path}.nodeSelector: Invalid value: {gv(v)}: {e}" for e in is_valid_label_value(str(v))]
-    for i, t in enumerate(spec.get("tolerations") or []):
-        op = t.get("operator") or "Equal"
-        if op not in ("Equal", "Exists"):
-            errs.append(f"{path}.tolerations[{i}].operator: Unsupported value: {gv(op)}")
-        if op == "Exists" and t.get("value"):
-            errs.append(f"{path}.tolerations[{i}].operator: Invalid value: value must be empty when `operator` is 'Exists'")
-        if t.get("effect") not in (None, "", "NoSchedule", "PreferNoSchedule", "NoExecute"):
-            errs.append(f"{path}.tolerations[{i}].effect: Unsupported value: {gv(t.get('effect'))}")
-    na = ((spec.get("affinity") or {}).get("nodeAffinity") or {})
-    req = na.get("requiredDuringSchedulingIgnoredDuringExecution") or {}
-    errs += _validate_node_selector_terms(req.get("nodeSelectorTerms"),
-                                          f"{path}.affinity.nodeAffinity.requiredDuringSchedulingIgnoredDuringExecution.nodeSelectorTerms")
-    for i, pt in enumerate(na.get("preferredDuringSchedulingIgnoredDuringExecution") or []):
-        w = pt.get("weight", 0)
-        if not 1 <= int(w) <= 100:
-            errs.append(f"{path}.affinity.nodeAffinity.preferredDuringSchedulingIgnoredDuringExecution[{i}].weight: Invalid value: {w}: must be in the range 1-100")
-    gp = spec.get("terminationGracePeriodSeconds")
-    if gp is not None and gp < 0:
-        errs.append(f"{path}.terminationGracePeriodSeconds: Invalid value: must be >= 0")
-    ads = spec.get("activeDeadlineSeconds")
-    if ads is not None and ads <= 0:
-        errs.append(f"{path}.activeDeadlineSeconds: Invalid value: must be > 0")
-    coll, xerrs = validate_extended_resources(spec.get("extendedResources"), f"{path}.extendedResources")
-    errs += xerrs
-    errs += validate_containers_extended_resources(containers, dict(coll), f"{path}.containers")
-    errs += validate_containers_extended_resources(inits, dict(coll), f"{path}.initContainers")  # fix #9
-    return errs
-
-
-_MUTABLE_CONTAINER_FIELDS = ("image",)
-
-
-def _strip_mutable(spec: dict) -> dict:
-    import copy
-    s = json.loads(json.dumps(spec))
-    for kind in ("containers", "initContainers"):
-        for c in s.get(kind) or []:
-            for f in _MUTABLE_CONTAINER_FIELDS:
-                c.pop(f, None)
-    s.pop("activeDeadlineSeconds", None)
-    s.pop("tolerations", None)
-    for pres in s.get("extendedResources") or []:
-        pres.pop("assigned", None)  # only pods/binding writes assigned
-        if not pres.get("affinity"):
-            pres.pop("affinity", None)
-    return s
+    """ValidatePodSpec — corevalidation.validate_pod_spec (validation.go:2879)."""
+    from .corevalidation import validate_pod_spec as _v
+    return _v(spec, path)
 
 
 def validate_pod(pod: dict, old: dict | None = None) -> list[str]:
-    errs = validate_object_meta(pod, True)
-    errs += validate_pod_spec(pod.get("spec") or {})
-    from ..security import validate_seccomp_annotations
-    from ..security.apparmor import validate_pod_annotations
-    errs += validate_seccomp_annotations((pod.get("metadata") or {}).get("annotations"))
-    errs += validate_pod_annotations(pod)
-    from ..kubelet.sysctl import validate_annotations as validate_sysctl_annotations
-    errs += validate_sysctl_annotations((pod.get("metadata") or {}).get("annotations"))
-    if old is not None:
-        if _strip_mutable(pod.get("spec") or {}) != _strip_mutable(old.get("spec") or {}):
-            errs.append("spec: Forbidden: pod updates may not change fields other than `spec.containers[*].image`, "
-                        "`spec.initContainers[*].image`, `spec.activeDeadlineSeconds` or `spec.tolerations` (only additions to existing tolerations)")
-        old_nn = (old.get("spec") or {}).get("nodeName")
-        if old_nn and (pod.get("spec") or {}).get("nodeName") != old_nn:
-            errs.append("spec.nodeName: Forbidden: field is immutable once set")
-    return errs
+    """ValidatePod (+ ValidatePodUpdate when `old`) — corevalidation.validate_pod."""
+    from .corevalidation import validate_pod as _v
+    return _v(pod, old)
 
 
 def validate_node(node: dict, old: dict | None = None) -> list[str]:
@@ -515,43 +392,6 @@ def validate_binding(b: dict) -> list[str]:
     return errs
 
 
-def validate_namespace(ns: dict, old=None) -> list[str]:
-    return validate_object_meta(ns, False, is_dns1123_label)
-
-
-def _validate_template_owner(obj: dict, old=None, needs_selector=True) -> list[str]:
-    errs = validate_object_meta(obj, True)
-    spec = obj.get("spec") or {}
-    tpl = spec.get("template") or {}
-    errs += validate_pod_spec(tpl.get("spec") or {}, "spec.template.spec")
-    if needs_selector:
-        try:
-            sel = selector_from_label_selector(spec.get("selector"))
-            if not sel.matches((tpl.get("metadata") or {}).get("labels") or {}):
-                errs.append("spec.template.metadata.labels: Invalid value: `selector` does not match template `labels`")
-        except SelectorError as e:
-            errs.append(f"spec.selector: Invalid value: {e}")
-    if "replicas" in spec and (not isinstance(spec["replicas"], int) or spec["replicas"] < 0):
-        errs.append("spec.replicas: Invalid value: must be greater than or equal to 0")
-    return errs
-
-
-def validate_daemonset(ds, old=None):
-    errs = _validate_template_owner(ds, old)
-    rp = ((ds.get("spec") or {}).get("template") or {}).get("spec", {}).get("restartPolicy", "Always")
-    if rp != "Always":
-        errs.append("spec.template.spec.restartPolicy: Unsupported value: only 'Always' is supported")
-    return errs
-
-
-def validate_job(j, old=None):
-    errs = _validate_template_owner(j, old, needs_selector=False)
-    rp = ((j.get("spec") or {}).get("template") or {}).get("spec", {}).get("restartPolicy")
-    if rp not in ("OnFailure", "Never"):
-        errs.append("spec.template.spec.restartPolicy: Unsupported value: must be OnFailure or Never")
-    return errs
-
-
 def validate_generic_namespaced(obj, old=None):
     return validate_object_meta(obj, True)
 
@@ -573,14 +413,14 @@ def validate_event(ev, old=None):
     return errs
 
 
-register_hooks("Pod", validator=validate_pod)
+from . import corevalidation as _cv  # noqa: E402
+from . import groupvalidation as _gv  # noqa: E402
+
+validate_namespace = _cv.validate_namespace
+register_hooks("Pod", validator=_cv.validate_pod)
 register_hooks("Node", validator=validate_node)
-register_hooks("Namespace", validator=validate_namespace)
+register_hooks("Namespace", validator=_cv.validate_namespace)
 register_hooks("Event", validator=validate_event)
-register_hooks("DaemonSet", "apps/v1", validator=validate_daemonset)
-register_hooks("ReplicaSet", "apps/v1", validator=_validate_template_owner)
-register_hooks("Deployment", "apps/v1", validator=_validate_template_owner)
-register_hooks("Job", "batch/v1", validator=validate_job)
 from .networking import default_service, validate_service  # noqa: E402
 
 
@@ -591,8 +431,12 @@ def _validate_crd(obj, old=None):
 
 register_hooks("CustomResourceDefinition", "apiextensions.k8s.io/v1beta1", validator=_validate_crd)
 register_hooks("Service", defaulter=default_service, validator=validate_service)
-register_hooks("ConfigMap", validator=validate_config_data)
-register_hooks("Secret", validator=validate_config_data)
-for _k in ("ServiceAccount", "Endpoints", "LimitRange", "ResourceQuota",
-           "PersistentVolumeClaim"):
-    register_hooks(_k, validator=validate_generic_namespaced)
+for _k, _fn in (("ConfigMap", _cv.validate_config_map), ("Secret", _cv.validate_secret),
+                ("ServiceAccount", _cv.validate_service_account), ("Endpoints", _cv.validate_endpoints),
+                ("LimitRange", _cv.validate_limit_range), ("ResourceQuota", _cv.validate_resource_quota),
+                ("PersistentVolume", _cv.validate_persistent_volume),
+                ("PersistentVolumeClaim", _cv.validate_persistent_volume_claim),
+                ("ReplicationController", _cv.validate_replication_controller),
+                ("PodTemplate", _cv.validate_pod_template)):
+    register_hooks(_k, validator=_fn)
+_gv.register()

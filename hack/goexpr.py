@@ -95,7 +95,11 @@ class Evaluator:
             return _unquote(val)
         if kind == "num":
             self.take()
-            return float(val) if any(c in val for c in ".eE") else int(val)
+            if any(c in val for c in ".eE"):
+                return float(val)
+            if len(val.lstrip("-")) > 1 and val.lstrip("-").startswith("0"):
+                return int(val, 8)            # Go octal literal (file modes: 0644)
+            return int(val)
         if val == "[]":
             self.take()
             self.type_name()
@@ -148,6 +152,15 @@ class Evaluator:
                 self.type_name()
                 self.take("]")
                 continue
+            if val == "struct" and self.peek(1)[1] == "{":
+                # an anonymous struct type: skip its field list
+                self.take()
+                depth = 0
+                while True:
+                    v = self.take()[1]
+                    depth += (v == "{") - (v == "}")
+                    if depth == 0:
+                        return
             if kind == "ident":
                 self.take()
                 return
@@ -183,7 +196,13 @@ class Evaluator:
                 keyed = keyed if keyed is not None else {}
                 keyed[k] = self.expr()
             else:
-                items.append(self.expr())
+                e = self.expr()
+                if self.peek()[1] == ":":          # a computed map key: core.ResourceName(x): v
+                    self.take(":")
+                    keyed = keyed if keyed is not None else {}
+                    keyed[e if not isinstance(e, (dict, list)) else _Unhashable(e)] = self.expr()
+                else:
+                    items.append(e)
             if self.peek()[1] == ",":
                 self.take()
         self.take("}")

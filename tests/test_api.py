@@ -227,4 +227,5 @@ def test_downward_api_volume_field_paths():
                {"path": "ip", "fieldRef": {"fieldPath": "status.podIP"}}]}}]}}
     SCHEME.default(pod)
     errs = validate_pod(pod)
-    assert len(errs) == 1 and 'items[1].fieldRef.fieldPath: Unsupported value: \"status.podIP\"' in errs[0], errs
+    # validateDownwardAPIVolumeSource passes the volume's path, not the item's (validation.go:1003-1005)
+    assert len(errs) == 1 and 'downwardAPI.fieldRef.fieldPath: Unsupported value: \"status.podIP\"' in errs[0], errs

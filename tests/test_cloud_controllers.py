@@ -77,7 +77,10 @@ def test_cloud_node_initialisation_monitoring_and_pv_labels():
                 await _until(ghost_gone)
                 assert await c.get_or_none("nodes", "live") is not None
                 # PV labeler: local volumes get the zone, then become visible
-                pv = {"apiVersion": "v1", "kind": "PersistentVolume", "metadata": {"name": "scratch"},
+                aff = ('{"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": [{"matchExpressions": '
+                       '[{"key": "kubernetes.io/hostname", "operator": "In", "values": ["live"]}]}]}}')
+                pv = {"apiVersion": "v1", "kind": "PersistentVolume", "metadata": {
+                          "name": "scratch", "annotations": {"volume.alpha.kubernetes.io/node-affinity": aff}},
                       "spec": {"capacity": {"storage": "1Ti"}, "accessModes": ["ReadWriteOnce"], "local": {"path": "/mnt/nvme0"}}}
                 created = await c.request("POST", "/api/v1/persistentvolumes", params={"includeUninitialized": "true"}, body=pv)
                 assert created["metadata"]["initializers"]["pending"] == [{"name": "pvl.kubernetes.io"}]

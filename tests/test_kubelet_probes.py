@@ -96,7 +96,8 @@ def test_named_port_http_liveness_keeps_healthy_server():
                                                      "ports": [{"name": "http", "containerPort": port}],
                                                      "livenessProbe": {"httpGet": {"path": "/healthz", "port": "http",
                                                                                    "httpHeaders": [{"name": "X-Probe", "value": "yes"}]},
-                                                                       "periodSeconds": 1, "failureThreshold": 1},
+                                                                       "periodSeconds": 1, "failureThreshold": 3,
+                                                                       "timeoutSeconds": 5},
                                                      "readinessProbe": {"httpGet": {"path": "/healthz", "port": "http",
                                                                                     "httpHeaders": [{"name": "X-Probe", "value": "yes"}]},
                                                                         "periodSeconds": 1}}]}})

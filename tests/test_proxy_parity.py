@@ -235,7 +235,8 @@ def test_health_check_node_port_served_by_kube_proxy():
                         body = await r.json(content_type=None)
                         assert body == {"service": {"namespace": "default", "name": "lb"}, "localEndpoints": 1}
                     ep = await c.get("endpoints", "lb", "default")
-                    ep["subsets"][0]["addresses"][0]["nodeName"] = "elsewhere"
+                    # the endpoint moves off this node (a new address: validation refuses re-homing an IP)
+                    ep["subsets"][0]["addresses"][0] = {"ip": "10.244.1.9", "nodeName": "elsewhere"}
                     await c.update(ep)
                     for _ in range(100):
                         await px.sync()

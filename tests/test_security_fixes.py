@@ -26,8 +26,9 @@ from amdkube.kubelet.podcontext import volume_file
 
 
 def _pod(vol):
-    return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p", "namespace": "default"},
-            "spec": {"containers": [{"name": "c", "image": "busybox"}], "volumes": [vol]}}
+    from amdkube.api.scheme import SCHEME
+    return SCHEME.default({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p", "namespace": "default"},
+                           "spec": {"containers": [{"name": "c", "image": "busybox"}], "volumes": [vol]}})
 
 
 @pytest.mark.parametrize("path", ["../../../../etc/cron.d/x", "/etc/passwd", "a/../../b", ".."])
