@@ -16,7 +16,10 @@ import logging
 from ..api import meta as m
 from ..utils.trace import Trace
 from . import extended
-from .predicates import ERR_VOLUME_BIND_CONFLICT, ORDER, PREDICATES, PodInfo
+from .predicates import (ERR_NODE_LABEL_PRESENCE_VIOLATED, ERR_NODE_NETWORK_UNAVAILABLE, ERR_NODE_NOT_READY,
+                         ERR_NODE_SELECTOR_NOT_MATCH, ERR_NODE_UNKNOWN_CONDITION, ERR_NODE_UNSCHEDULABLE,
+                         ERR_POD_NOT_MATCH_HOST_NAME, ERR_TAINTS_TOLERATIONS_NOT_MATCH, ERR_VOLUME_BIND_CONFLICT,
+                         ERR_VOLUME_NODE_CONFLICT, ERR_VOLUME_ZONE_CONFLICT, ORDER, PREDICATES, PodInfo)
 from .priorities import PRIORITIES, pod_selectors
 
 log = logging.getLogger("amdkube.scheduler")
@@ -88,6 +91,7 @@ class GenericScheduler:
         self.ecache: dict[str, dict[str, tuple]] = {}
         self.ecache_hits = 0
         self.findex: dict[str, _FitIndex] = {}
+        self.queue = None               # the SchedulingQueue (nominated pods), set by the Scheduler
 
     def configure(self, predicates, priorities, custom_predicates, custom_priorities, extenders, hard_affinity_weight):
         """(Re)build the algorithm from a policy: registered names plus policy-argument functions."""
@@ -314,7 +318,16 @@ class GenericScheduler:
                 raise FitError(pod, n_ready, dict(idx.failed))
             names = list(idx.fit)
             fit = [self.cache.nodes[n] for n in names]
-            scores = list(idx.fit.values()) if len(fit) > 1 else None
+            scores = list(idx.fit.values())
+            if self.queue is not None and self.queue.nominated:
+                failed = dict(idx.failed)
+                keep = {ni.name for ni in self._filter_nominated(pi, fit, failed)}
+                if len(keep) != len(fit):
+                    scores = [s for ni, s in zip(fit, scores) if ni.name in keep]
+                    fit = [ni for ni in fit if ni.name in keep]
+                    if not fit:
+                        raise FitError(pod, n_ready, failed)
+            scores = scores if len(fit) > 1 else None
             n_nodes = n_ready
             host = fit[0] if scores is None else self.select_host(fit, scores)
         else:
@@ -324,6 +337,7 @@ class GenericScheduler:
                 raise FitError(pod, 0, {})
             trace.step("Computing predicates")
             fit, failed, ctx = await self.find_nodes_that_fit(pi, nodes)
+            fit = self._filter_nominated(pi, fit, failed, ctx)
             if not fit:
                 raise FitError(pod, len(nodes), failed)
             trace.step("Prioritizing")
@@ -334,7 +348,7 @@ class GenericScheduler:
                 scores = await self.prioritize(pi, fit, ctx)
                 trace.step("Selecting host")
                 host = self.select_host(fit, scores)
-        binding = extended.allocate(pi, host, self.use_topology) if pi.ext else {}
+        binding = extended.allocate(pi, self._with_nominated(pi, host) or host, self.use_topology) if pi.ext else {}
         if binding is None:
             # the device choice failed on the best host: the next-ranked hosts get their turn
             failed_alloc = {host.name: ["device allocation failed"]}
@@ -357,37 +371,255 @@ class GenericScheduler:
         trace.log_if_long(self.trace_threshold)
         return host.name, binding
 
+    # -------------------------------------------------------------- nominated pods
+    def _nominated_for(self, pi, node_name: str) -> list:
+        """Pods nominated to `node_name` (waiting for a preemption there) whose priority is at
+        least this pod's: it must not take the room freed for them (addNominatedPods :367-400)."""
+        q = self.queue
+        if q is None:
+            return []
+        return [p for p in q.waiting_pods_for_node(node_name)
+                if pod_priority(p) >= pi.priority and m.key_of(p) != pi.key]
+
+    def _with_nominated(self, pi, ni):
+        """A copy of the node with those nominated pods added — their devices simulated as
+        taken (the device allocator picks them on the copy) — or None when there are none."""
+        noms = self._nominated_for(pi, ni.name)
+        if not noms:
+            return None
+        sim = ni.clone()
+        for p in noms:
+            npi = PodInfo(p)
+            if npi.ext:
+                b = extended.allocate(npi, sim, False)
+                if b:
+                    got = {name: list(v["resources"]) for name, v in b.items()}
+                else:
+                    # its victims are still terminating: the devices free so far are its own
+                    got, taken = {}, set()
+                    for pname, rname, n, _sel in npi.ext:
+                        free = [d for d in sim.available_devices(rname) if d not in taken][:n]
+                        taken.update(free)
+                        got[pname] = free
+                spec = dict(p.get("spec") or {})
+                spec["extendedResources"] = [dict(r, assigned=got[r["name"]]) if r.get("name") in got else r
+                                             for r in spec.get("extendedResources") or []]
+                p = dict(p, spec=spec)
+            sim.add_pod(m.key_of(p), p)
+        return sim
+
+    def fits_with_nominated(self, pi, ni, ctx=None) -> tuple[bool, list[str]]:
+        """podFitsOnNode's first pass (:402-470): the node as it would be with the nominated
+        pods of equal or higher priority running. The second pass (without them) is the normal
+        evaluation; a node must pass both."""
+        sim = self._with_nominated(pi, ni)
+        if sim is None:
+            return True, []
+        return self.pod_fits_on_node(pi, sim, ctx)
+
+    def _filter_nominated(self, pi, fit, failed, ctx=None):
+        if self.queue is None or not self.queue.nominated:
+            return fit
+        out = []
+        for ni in fit:
+            ok, reasons = self.fits_with_nominated(pi, ni, ctx)
+            if ok:
+                out.append(ni)
+            else:
+                failed[ni.name] = reasons
+        return out
+
     # -------------------------------------------------------------- preemption
-    def preempt(self, pod: dict):
-        """Pick (node, victims) so `pod` fits after removing lower-priority pods (with devices)."""
+    def select_victims_on_node(self, pi, ni, pdbs=()):
+        """selectVictimsOnNode (generic_scheduler.go:872-955): remove every lower-priority pod;
+        if the pod then fits (nominated pods counted), reprieve victims from the highest
+        priority down — PDB-violating ones first — while it still fits. Returns
+        (victims, number of PDB-violating victims, fits). The device allocator is part of the
+        fit (fix #7)."""
+        sim = ni.clone()
+        potential = [p for p in ni.pods.values() if pod_priority(p) < pi.priority]
+        for p in potential:
+            sim.remove_pod(m.key_of(p))
+        potential.sort(key=pod_priority, reverse=True)       # util.HigherPriorityPod
+
+        ctx = None
+        if self.custom or any(n == "MatchInterPodAffinity" for n, _ in self.predicates):
+            # inter-pod (anti-)affinity sees the node as it would be after the preemption
+            ctx = self._ctx([sim if x.name == ni.name else x for x in self.cache.ready_nodes()])
+
+        def fits():
+            ok, _ = self.pod_fits_on_node(pi, sim, ctx)
+            return ok and self.fits_with_nominated(pi, sim, ctx)[0]
+        if not fits():
+            return None, 0, False
+        violating, non_violating = filter_pods_with_pdb_violation(potential, pdbs)
+        victims, n_violating = [], 0
+
+        def reprieve(p) -> bool:
+            sim.add_pod(m.key_of(p), p)
+            if fits():
+                return True
+            sim.remove_pod(m.key_of(p))
+            victims.append(p)
+            return False
+        for p in violating:
+            if not reprieve(p):
+                n_violating += 1
+        for p in non_violating:
+            reprieve(p)
+        return victims, n_violating, True
+
+    def select_nodes_for_preemption(self, pi, nodes, pdbs=()) -> dict:
+        """selectNodesForPreemption (:820-852): node name -> (victims, PDB violations) for every
+        node where the pod fits after preemption."""
+        out = {}
+        for ni in nodes:
+            victims, nviol, ok = self.select_victims_on_node(pi, ni, pdbs)
+            if ok:
+                out[ni.name] = (victims, nviol)
+        return out
+
+    def preempt(self, pod: dict, failed: dict | None = None, pdbs=()):
+        """(node, victims): the node pickOneNodeForPreemption chooses among the nodes where
+        preemption might help (all ready nodes when `failed` is None), without extenders."""
         pi = PodInfo(pod)
         if pi.spec.get("preemptionPolicy") == "Never":
             return None, []
-        best = None
-        for ni in self.cache.ready_nodes():
-            lower = sorted([p for p in ni.pods.values() if int((p.get("spec") or {}).get("priority") or 0) < pi.priority],
-                           key=lambda p: int((p.get("spec") or {}).get("priority") or 0))
-            if not lower:
-                continue
-            sim = ni.clone()
-            for p in lower:
-                sim.remove_pod(m.key_of(p))
-            ok, _ = self.pod_fits_on_node(pi, sim, None)
-            if not ok:
-                continue
-            victims = []
-            # reprieve as many victims as possible (highest priority first)
-            for p in reversed(lower):
-                sim.add_pod(m.key_of(p), p)
-                ok, _ = self.pod_fits_on_node(pi, sim, None)
-                if not ok:
-                    sim.remove_pod(m.key_of(p))
-                    victims.append(p)
-            if not victims:
-                continue
-            key = (max(int((v.get("spec") or {}).get("priority") or 0) for v in victims), len(victims))
-            if best is None or key < best[0]:
-                best = (key, ni.name, victims)
-        if best is None:
-            return None, []
-        return best[1], best[2]
+        nodes = self.cache.ready_nodes()
+        if failed is not None:
+            keep = set(nodes_where_preemption_might_help([ni.name for ni in nodes], failed))
+            nodes = [ni for ni in nodes if ni.name in keep]
+        cand = self.select_nodes_for_preemption(pi, nodes, pdbs)
+        name = pick_one_node_for_preemption(cand)
+        return (name, cand[name][0]) if name is not None else (None, [])
+
+    async def preempt_async(self, pod: dict, failed: dict, pdbs=()):
+        """genericScheduler.Preempt (generic_scheduler.go:199-262): (node, victims, pods whose
+        nomination is to be cleared). A pod whose earlier preemption still has victims
+        terminating on its nominated node is not eligible; when no node can help, the pod's own
+        nomination is cleared; a chosen node must pass the extenders with its victims removed;
+        lower-priority pods nominated to that node lose their nomination."""
+        pi = PodInfo(pod)
+        if pi.spec.get("preemptionPolicy") == "Never":
+            return None, [], []
+        if not pod_eligible_to_preempt_others(pod, self.cache):
+            return None, [], []
+        nodes = self.cache.ready_nodes()
+        if not nodes:
+            return None, [], []
+        keep = set(nodes_where_preemption_might_help([ni.name for ni in nodes], failed))
+        potential = [ni for ni in nodes if ni.name in keep]
+        if not potential:
+            return None, [], [pod]
+        cand = self.select_nodes_for_preemption(pi, potential, pdbs)
+        while cand:
+            name = pick_one_node_for_preemption(cand)
+            if name is None:
+                break
+            victims = cand[name][0]
+            if await self._node_passes_extenders(pod, name, victims):
+                lower = [p for p in (self.queue.waiting_pods_for_node(name) if self.queue is not None else [])
+                         if pod_priority(p) < pi.priority]
+                return name, victims, lower
+            del cand[name]
+        return None, [], []
+
+    async def _node_passes_extenders(self, pod, name, victims) -> bool:
+        """nodePassesExtendersForPreemption (:854-884): the node with its victims removed."""
+        filters = [e for e in self.extenders if e.filter_verb]
+        if not filters:
+            return True
+        ni = self.cache.nodes.get(name)
+        if ni is None or ni.node is None:
+            return False
+        for ext in filters:
+            try:
+                names, ext_failed = await ext.filter(pod, [ni.node])
+            except Exception as e:
+                log.warning("extender filter during preemption on %s: %r", name, e)
+                return False
+            if name in ext_failed or name not in set(names):
+                return False
+        return True
+
+
+def pod_priority(pod: dict) -> int:
+    """util.GetPodPriority: spec.priority, 0 when unset (no default PriorityClass)."""
+    return int((pod.get("spec") or {}).get("priority") or 0)
+
+
+# nodesWherePreemptionMightHelp (:957-997): failures that removing pods cannot fix
+UNRESOLVABLE = {ERR_NODE_SELECTOR_NOT_MATCH, ERR_POD_NOT_MATCH_HOST_NAME, ERR_TAINTS_TOLERATIONS_NOT_MATCH,
+                ERR_NODE_LABEL_PRESENCE_VIOLATED, ERR_NODE_NOT_READY, ERR_NODE_NETWORK_UNAVAILABLE,
+                ERR_NODE_UNSCHEDULABLE, ERR_NODE_UNKNOWN_CONDITION, ERR_VOLUME_ZONE_CONFLICT,
+                ERR_VOLUME_NODE_CONFLICT, ERR_VOLUME_BIND_CONFLICT}
+
+
+def nodes_where_preemption_might_help(names, failed: dict) -> list:
+    return [n for n in names if n not in failed or not any(r in UNRESOLVABLE for r in failed[n])]
+
+
+def pod_eligible_to_preempt_others(pod: dict, cache) -> bool:
+    """podEligibleToPreemptOthers (:999-1011): not while a lower-priority pod on the node the pod
+    is nominated to is still terminating (its earlier preemption is in progress)."""
+    from .queue import NOMINATED_NODE_ANNOTATION
+    node = ((pod.get("metadata") or {}).get("annotations") or {}).get(NOMINATED_NODE_ANNOTATION)
+    if not node:
+        return True
+    ni = cache.nodes.get(node)
+    if ni is None:
+        return True
+    prio = pod_priority(pod)
+    return not any((p.get("metadata") or {}).get("deletionTimestamp") and pod_priority(p) < prio
+                   for p in ni.pods.values())
+
+
+def filter_pods_with_pdb_violation(pods, pdbs):
+    """filterPodsWithPDBViolation (:889-917): a pod whose matching PDB allows no disruption is a
+    violating victim; order is kept."""
+    from ..api.labels import SelectorError, selector_from_label_selector
+    violating, non_violating = [], []
+    for p in pods:
+        labels = m.labels_of(p)
+        hit = False
+        if labels:
+            for pdb in pdbs or ():
+                if m.namespace_of(pdb) != m.namespace_of(p):
+                    continue
+                try:
+                    sel = selector_from_label_selector((pdb.get("spec") or {}).get("selector"))
+                except SelectorError:
+                    continue
+                if sel.empty() or not sel.matches(labels):
+                    continue
+                st = pdb.get("status") or {}
+                if int(st.get("disruptionsAllowed", st.get("podDisruptionsAllowed", 0)) or 0) <= 0:
+                    hit = True
+                    break
+        (violating if hit else non_violating).append(p)
+    return violating, non_violating
+
+
+def pick_one_node_for_preemption(node_to_victims: dict):
+    """pickOneNodeForPreemption (:657-760): a node needing no preemption; else fewest PDB
+    violations, then the lowest highest-priority victim (victims[0]), then the smallest sum
+    of priorities (each shifted by MaxInt32+1), then the fewest victims, then the first."""
+    if not node_to_victims:
+        return None
+    cands = []
+    for name, (victims, nviol) in node_to_victims.items():
+        if not victims:
+            return name
+        cands.append(name)
+
+    def narrow(names, key):
+        best = min(key(n) for n in names)
+        return [n for n in names if key(n) == best]
+    cands = narrow(cands, lambda n: node_to_victims[n][1])
+    if len(cands) > 1:
+        cands = narrow(cands, lambda n: pod_priority(node_to_victims[n][0][0]))
+    if len(cands) > 1:
+        cands = narrow(cands, lambda n: sum(pod_priority(p) + 2 ** 31 for p in node_to_victims[n][0]))
+    if len(cands) > 1:
+        cands = narrow(cands, lambda n: len(node_to_victims[n][0]))
+    return cands[0]

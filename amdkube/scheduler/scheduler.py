@@ -29,9 +29,7 @@ from .extender import HTTPExtender
 from .generic import FitError, GenericScheduler
 from .predicates import DEFAULT_PREDICATES
 from .priorities import DEFAULT_PRIORITIES
-from .queue import SchedulingQueue
-
-NOMINATED_NODE_ANNOTATION = "NominatedNodeName"
+from .queue import NOMINATED_NODE_ANNOTATION, SchedulingQueue
 log = logging.getLogger("amdkube.scheduler")
 
 PROVIDERS = {
@@ -100,6 +98,8 @@ class Scheduler:
                                      hard_affinity_weight=self.hard_weight)
         self._set_needs(cpreds, cprios, prios)
         self.queue = SchedulingQueue(self.gates("PodPriority"))
+        self.algo.queue = self.queue
+        self.pdb_inf = None             # PodDisruptionBudgets for preemption (cache.ListPDBs)
         self.recorder = EventRecorder(client, self.name)
         self.leader_elect = leader_elect
         self.identity = identity or f"{self.name}-{id(self):x}"
@@ -161,6 +161,7 @@ class Scheduler:
     def _on_pod_add(self, pod):
         if self._assigned_live(pod):
             self.cache.add_pod(pod)
+            self.queue.assigned_pod_added(pod)
         elif self._unassigned(pod):
             POD_TRACE(m.uid_of(pod), "sched_queued")
             self.queue.add(pod)
@@ -169,13 +170,15 @@ class Scheduler:
         if self._assigned_live(pod):
             self.cache.update_pod(old, pod)
             self.queue.delete(pod)
+            if m.labels_of(old) != m.labels_of(pod) or not self._assigned_live(old):
+                self.queue.assigned_pod_updated(pod)
         elif (pod.get("spec") or {}).get("nodeName"):
             # bound pod went terminal → its resources (incl. GPUs) are free again
             if self._assigned_live(old) or self.cache.is_assumed(pod) or m.key_of(pod) in self.cache.pod_states:
                 self.cache.remove_pod(pod)
                 self.queue.move_all_to_active()
         elif self._unassigned(pod):
-            self.queue.update(pod)
+            self.queue.update(pod, old)
         else:
             self.queue.delete(pod)
 
@@ -243,6 +246,9 @@ class Scheduler:
         self.node_inf = Informer(self.client, "nodes")
         self.node_inf.add_handler(on_add=self._on_node, on_update=self._on_node_update,
                                   on_delete=lambda n: self.cache.remove_node(n))
+        if self.gates("PodPriority") and not self.disable_preemption:
+            self.pdb_inf = Informer(self.client, "poddisruptionbudgets")
+            self.pdb_inf.start()
         self.pod_inf = Informer(self.client, "pods")
         self.pod_inf.add_handler(on_add=self._on_pod_add, on_update=self._on_pod_update, on_delete=self._on_pod_delete)
         # claims, volumes and classes for the volume predicates; a claim or volume change may make
@@ -270,7 +276,8 @@ class Scheduler:
     async def stop(self):
         from ..utils import cancel_and_wait
         await cancel_and_wait(list(self._tasks) + list(self._binds))
-        for inf in (self.pod_inf, self.node_inf, self.svc_inf, *self.ctl_infs.values(), *getattr(self, "vol_infs", [])):
+        for inf in (self.pod_inf, self.node_inf, self.svc_inf, self.pdb_inf, *self.ctl_infs.values(),
+                    *getattr(self, "vol_infs", [])):
             if inf:
                 await inf.stop()
         await self.recorder.stop()
@@ -312,7 +319,7 @@ class Scheduler:
                 raise
             except Exception as e:
                 log.exception("scheduling %s crashed: %r", m.key_of(pod), e)
-                self.queue.add_unschedulable(pod)
+                self.queue.add_unschedulable(pod, marked=True)
 
     async def schedule_one(self, pod: dict):
         key = m.key_of(pod)
@@ -329,9 +336,9 @@ class Scheduler:
             self.m_attempts.labels("unschedulable").inc()
             self.recorder.event(pod, "Warning", "FailedScheduling", str(e))
             asyncio.create_task(self._mark_unschedulable(pod, str(e)))
-            if not self.disable_preemption and self.gates("PodPriority") and int((pod.get("spec") or {}).get("priority") or 0) > 0:
-                await self._preempt(pod)
-            self.queue.add_unschedulable(pod)
+            if not self.disable_preemption and self.gates("PodPriority"):
+                pod = await self._preempt(pod, e)
+            self.queue.add_unschedulable(pod, marked=True)
             return
         self.m_algo.observe((time.perf_counter() - t0) * 1e6)
         # assume: nodeName + chosen devices (fix #1: devices are reserved before the bind)
@@ -380,7 +387,7 @@ class Scheduler:
                 log.info("binding %s to %s rejected: %s", m.key_of(pod), host, e)
                 self.recorder.event(pod, "Warning", "FailedScheduling", f"Binding rejected: {e}")
                 if not (isinstance(e, m.StatusError) and (m.is_not_found(e) or "already assigned" in e.message)):
-                    self.queue.add_unschedulable(pod)
+                    self.queue.add_unschedulable(pod, marked=True)
                     self.queue.move_all_to_active()
                 return
             self.cache.finish_binding(assumed)
@@ -403,21 +410,39 @@ class Scheduler:
         except Exception:
             pass
 
-    async def _preempt(self, pod):
+    async def _preempt(self, pod, fit_error) -> dict:
+        """scheduler.go preempt (:209-253): nominate the preemptor to the chosen node (the
+        NominatedNodeName annotation), delete the victims, clear the nominations the algorithm
+        hands back. Returns the preemptor as the queue must now hold it (with its nomination,
+        before the informer brings the patched object back)."""
         self.m_preempt.inc()
-        node, victims = self.algo.preempt(pod)
-        if not node:
-            return
-        for v in victims:
-            self.recorder.event(v, "Normal", "Preempted", f"by {m.key_of(pod)} on node {node}")
+        pdbs = self.pdb_inf.list() if self.pdb_inf is not None else []
+        node, victims, to_clear = await self.algo.preempt_async(pod, fit_error.failed, pdbs)
+        if node:
+            ann = dict(((pod.get("metadata") or {}).get("annotations")) or {}, **{NOMINATED_NODE_ANNOTATION: node})
             try:
-                await self.client.delete("pods", m.name_of(v), m.namespace_of(v))
+                await self.client.patch("pods", m.name_of(pod), {"metadata": {"annotations": {NOMINATED_NODE_ANNOTATION: node}}},
+                                        m.namespace_of(pod))
+            except m.StatusError as e:
+                log.info("nominating %s to %s: %s", m.key_of(pod), node, e)
+                return pod
+            pod = dict(pod, metadata=dict(pod.get("metadata") or {}, annotations=ann))
+            for v in victims:
+                try:
+                    await self.client.delete("pods", m.name_of(v), m.namespace_of(v))
+                except m.StatusError as e:
+                    log.info("preempting %s: %s", m.key_of(v), e)
+                    return pod
+                self.recorder.event(v, "Normal", "Preempted", f"by {m.key_of(pod)} on node {node}")
+        for p in to_clear:
+            # RemoveNominatedNodeAnnotation: a JSON merge patch that deletes the key
+            try:
+                await self.client.patch("pods", m.name_of(p), {"metadata": {"annotations": {NOMINATED_NODE_ANNOTATION: None}}},
+                                        m.namespace_of(p))
             except m.StatusError:
                 pass
-        try:
-            # scheduler.go:227 — v1.9 records the nomination as a pod annotation
-            # (core.NominatedNodeAnnotationKey, generic_scheduler.go:66), not a status field
-            await self.client.patch("pods", m.name_of(pod), {"metadata": {"annotations": {NOMINATED_NODE_ANNOTATION: node}}},
-                                    m.namespace_of(pod))
-        except m.StatusError:
-            pass
+            if m.key_of(p) == m.key_of(pod):
+                md = dict(pod.get("metadata") or {})
+                md["annotations"] = {k: v for k, v in (md.get("annotations") or {}).items() if k != NOMINATED_NODE_ANNOTATION}
+                pod = dict(pod, metadata=md)
+        return pod

@@ -218,7 +218,7 @@ def test_queue_priority_order_and_unschedulable_moves():
         q.add(pod("high", prio=10))
         q.add(pod("mid", prio=5))
         assert [(await q.pop())["metadata"]["name"] for _ in range(3)] == ["high", "mid", "low"]
-        q.add_unschedulable(pod("u"))
+        q.add_unschedulable(pod("u"), marked=True)
         assert len(q) == 0
         q.move_all_to_active()
         assert (await q.pop())["metadata"]["name"] == "u"

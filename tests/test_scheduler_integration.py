@@ -199,3 +199,41 @@ def test_priority_preemption_frees_devices():
         finally:
             await _stop(api, c, s)
     run(go())
+
+
+def test_nominated_preemptor_is_not_overtaken_by_a_lower_priority_pod():
+    """Priority inversion (scheduling_queue.go nominatedPods + addNominatedPods): a priority-1000
+    8-GPU pod preempts eight priority-0 1-GPU pods; a priority-0 1-GPU pod created while the
+    victims terminate must not take a freed GPU before the preemptor binds."""
+    async def go():
+        api, c, s = await _cluster(1, gpus=8)
+        try:
+            for i in range(8):
+                await c.create(_pod(f"low-{i}", gpus=1, prio=0))
+            for i in range(8):
+                await _node_of(c, f"low-{i}")
+            await c.create(_pod("big", gpus=8, prio=1000))
+            loop = asyncio.get_running_loop()
+            end = loop.time() + 10
+            while loop.time() < end:
+                h = await c.get("pods", "big", "default")
+                if ((h.get("metadata") or {}).get("annotations") or {}).get("NominatedNodeName"):
+                    break
+                await asyncio.sleep(0.02)
+            assert h["metadata"]["annotations"]["NominatedNodeName"] == "node-0000"
+            await c.create(_pod("sneak", gpus=1, prio=0))
+            await _condition(c, "sneak")
+            # the victims go one at a time; after each, the sneak pod is retried and must wait
+            for i in range(8):
+                if await c.get_or_none("pods", f"low-{i}", "default") is not None:
+                    await c.delete("pods", f"low-{i}", "default", grace=0)
+                await asyncio.sleep(0.05)
+                if i < 7:
+                    assert not (await c.get("pods", "sneak", "default"))["spec"].get("nodeName")
+            assert await _node_of(c, "big", timeout=15) == "node-0000"
+            sneak = await c.get("pods", "sneak", "default")
+            assert not sneak["spec"].get("nodeName")
+            assert len((await c.get("pods", "big", "default"))["spec"]["extendedResources"][0]["assigned"]) == 8
+        finally:
+            await _stop(api, c, s)
+    run(go(), 60)
