@@ -100,7 +100,7 @@ def apply_patch(cur: dict, patch_body: bytes, content_type: str) -> dict:
     if "strategic-merge" in content_type:
         from ..api import strategicpatch as smp
         node = smp.schema_for(cur.get("apiVersion"), cur.get("kind"))
-        if node is None and SCHEME.for_kind(cur.get("apiVersion") or "", cur.get("kind") or "") is None:
+        if node is None:        # every built-in kind has a schema: this is a custom resource
             raise m.StatusError(415, "UnsupportedMediaType",
                                 f"the body of the request was in an unknown format - accepted media types include: "
                                 f"application/json-patch+json, application/merge-patch+json")
@@ -414,7 +414,7 @@ class ResourceStore:
                 return None
             if nmd.get("deletionTimestamp") and not nmd.get("finalizers") and not (
                     self.ri.plural == "namespaces" and ((new.get("spec") or {}).get("finalizers"))):
-                if self.ri.plural != "pods":
+                if self.ri.plural != "pods" or nmd.get("deletionGracePeriodSeconds") == 0:
                     delete_after[0] = True
             return new
 
@@ -460,6 +460,9 @@ class ResourceStore:
                 if graceful:
                     prev = cm.get("deletionGracePeriodSeconds")
                     cm["deletionGracePeriodSeconds"] = graceful if prev is None else min(prev, graceful)
+                elif self.ri.plural == "pods":
+                    # a final (grace 0) delete held only by finalizers: removing the last one deletes it
+                    cm["deletionGracePeriodSeconds"] = 0
                 if finalizers:
                     cm["finalizers"] = sorted(set((cm.get("finalizers") or []) + finalizers))
                 if self.ri.plural == "namespaces":

@@ -122,6 +122,12 @@ class Informer:
             h.add(obj)
         return h
 
+    def remove_handler(self, h: ResourceEventHandler):
+        try:
+            self.handlers.remove(h)
+        except ValueError:
+            pass
+
     def has_synced(self) -> bool:
         return self.synced.is_set()
 

@@ -26,7 +26,8 @@ from .accounts import (BootstrapSignerController, CSRApprovingController, CSRCle
 from .apps import CronJobController, ReplicationManager, StatefulSetController
 from .autoscaling import HorizontalPodAutoscalerController
 from .cloud import CloudNodeController, PersistentVolumeLabelController, RouteController, ServiceLBController
-from .lifecycle import GarbageCollector, NamespaceController, NodeLifecycleController, PodGCController
+from .garbagecollector import GarbageCollector
+from .lifecycle import NamespaceController, NodeLifecycleController, PodGCController
 from .networking import EndpointsController, NodeIPAMController
 from .policy import ClusterRoleAggregationController, DisruptionController, ResourceQuotaController, TTLController
 from .volumes import (AttachDetachController, PersistentVolumeBinderController, PVCProtectionController,
@@ -78,7 +79,7 @@ ALL = {
     "daemonset": lambda mgr, o: DaemonSetController(mgr),
     "job": lambda mgr, o: JobController(mgr),
     "namespace": lambda mgr, o: NamespaceController(mgr),
-    "garbagecollector": lambda mgr, o: GarbageCollector(mgr),
+    "garbagecollector": lambda mgr, o: GarbageCollector(mgr, sync_period=o.extra.get("gc_discovery_period", 30.0)),
     "podgc": lambda mgr, o: PodGCController(mgr, threshold=o.terminated_pod_gc_threshold),
     "endpoint": lambda mgr, o: EndpointsController(mgr),
     "nodeipam": lambda mgr, o: NodeIPAMController(mgr, o.cluster_cidr, o.node_cidr_mask_size),

@@ -351,86 +351,6 @@ class NamespaceController(Controller):
             await self.client.request("PUT", f"/api/v1/namespaces/{key}/finalize", body=ns)
 
 
-class GarbageCollector(Controller):
-    name = "garbagecollector"
-    OWNED = ("pods", "replicasets", "jobs", "daemonsets", "deployments", "replicationcontrollers", "statefulsets",
-             "controllerrevisions", "cronjobs", "services", "endpoints", "configmaps", "secrets", "persistentvolumeclaims",
-             "horizontalpodautoscalers", "poddisruptionbudgets", "serviceaccounts")
-
-    def __init__(self, mgr, period: float = 2.0):
-        super().__init__(mgr)
-        self.period = period
-
-    def setup(self):
-        self.infs = {r: (self.mgr.pods if r == "pods" else self.mgr.factory.informer(r)) for r in self.OWNED}
-        for r, inf in self.infs.items():
-            inf.add_handler(on_delete=lambda o: self.queue.add("scan"),
-                            on_update=lambda o, n: self.queue.add("scan") if (n.get("metadata") or {}).get("deletionTimestamp") else None)
-
-    async def start(self):
-        await super().start()
-        self.tasks.append(asyncio.create_task(self._tick()))
-
-    async def _tick(self):
-        while True:
-            await asyncio.sleep(self.period)
-            self.queue.add("scan")
-
-    async def sync(self, key):
-        alive = {}
-        for r, inf in self.infs.items():
-            for o in inf.list():
-                alive[m.uid_of(o)] = (r, o)
-        for r, inf in self.infs.items():
-            for o in inf.list():
-                md = o.get("metadata") or {}
-                fins = md.get("finalizers") or []
-                if md.get("deletionTimestamp") and ("orphan" in fins or "foregroundDeletion" in fins):
-                    await self._finalize(r, o, alive)
-                    continue
-                refs = md.get("ownerReferences") or []
-                if refs and not any([await self._owner_alive(ref, o, alive) for ref in refs]):
-                    try:
-                        await self.client.delete(r, m.name_of(o), m.namespace_of(o), propagation="Background")
-                    except m.StatusError:
-                        pass
-
-    async def _owner_alive(self, ref, dependent, alive) -> bool:
-        """An owner of a watched kind is checked in the cache; any other kind with a GET
-        (garbagecollector.go attemptToDeleteItem → isDangling), unknown kinds count as alive."""
-        if ref.get("uid") in alive:
-            return True
-        from ..api.scheme import SCHEME
-        ri = SCHEME.for_kind(ref.get("apiVersion", ""), ref.get("kind", ""))
-        if ri is None:
-            return True
-        if ri.plural in self.infs:
-            return False
-        try:
-            o = await self.client.get(ri.plural, ref.get("name", ""), m.namespace_of(dependent) if ri.namespaced else "")
-        except m.StatusError as e:
-            return not m.is_not_found(e)
-        return m.uid_of(o) == ref.get("uid")
-
-    async def _finalize(self, r, owner, alive):
-        uid = m.uid_of(owner)
-        md = owner["metadata"]
-        deps = [(dr, d) for dr, d in alive.values() if any(ref.get("uid") == uid for ref in (d.get("metadata") or {}).get("ownerReferences") or [])]
-        if "orphan" in md["finalizers"]:
-            for dr, d in deps:
-                refs = [x for x in d["metadata"]["ownerReferences"] if x.get("uid") != uid]
-                await self.client.patch(dr, m.name_of(d), {"metadata": {"ownerReferences": refs or None}}, m.namespace_of(d))
-            fins = [f for f in md["finalizers"] if f != "orphan"]
-        else:
-            if deps:
-                for dr, d in deps:
-                    if not (d.get("metadata") or {}).get("deletionTimestamp"):
-                        await self.client.delete(dr, m.name_of(d), m.namespace_of(d))
-                return
-            fins = [f for f in md["finalizers"] if f != "foregroundDeletion"]
-        await self.client.patch(r, m.name_of(owner), {"metadata": {"finalizers": fins or None}}, m.namespace_of(owner))
-
-
 class PodGCController(Controller):
     """pkg/controller/podgc/gc_controller.go: every gcCheckPeriod (20 s) terminated pods beyond
     --terminated-pod-gc-threshold (oldest first; 0 disables this step), pods bound to nodes that

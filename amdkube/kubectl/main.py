@@ -203,7 +203,10 @@ async def _create_or_apply(c, a, apply=False):
                 patch = {k: v for k, v in doc.items() if k not in ("status",)}
                 patch.setdefault("metadata", {}).setdefault("annotations", {})[
                     "kubectl.kubernetes.io/last-applied-configuration"] = json.dumps(doc, sort_keys=True)
-                await c.patch(res, name, patch, ns, patch_type="application/strategic-merge-patch+json")
+                from ..api import strategicpatch as smp
+                ptype = "application/strategic-merge-patch+json" if smp.schema_for(doc.get("apiVersion"), doc.get("kind")) \
+                    else "application/merge-patch+json"        # custom resources have no strategic schema
+                await c.patch(res, name, patch, ns, patch_type=ptype)
                 print(f"{ri.kind.lower()}/{name} configured")
                 continue
             doc.setdefault("metadata", {}).setdefault("annotations", {})[

@@ -42,7 +42,7 @@ def apply_patch_for(original: dict | None, modified: dict, current: dict) -> tup
     for built-in kinds, a JSON merge three-way patch for kinds without one (custom resources).
     None when nothing changes."""
     node = smp.schema_for(modified.get("apiVersion"), modified.get("kind"))
-    if node is None and SCHEME.for_object(modified) is None:
+    if node is None:
         patch, ctype = smp.create_three_way_json_merge(original, modified, current), "application/merge-patch+json"
     else:
         patch, ctype = smp.create_three_way(original, modified, current, node), "application/strategic-merge-patch+json"
