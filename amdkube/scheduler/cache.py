@@ -179,10 +179,17 @@ def _has_affinity(pod) -> bool:
                 .get("requiredDuringSchedulingIgnoredDuringExecution"))
 
 
+def _has_pref_affinity(pod) -> bool:
+    aff = (pod.get("spec") or {}).get("affinity") or {}
+    return bool((aff.get("podAffinity") or {}).get("preferredDuringSchedulingIgnoredDuringExecution") or
+                (aff.get("podAntiAffinity") or {}).get("preferredDuringSchedulingIgnoredDuringExecution"))
+
+
 class SchedulerCache:
     def __init__(self, ttl: float = 30.0):
         self.anti_affinity_pods = 0  # pods carrying required anti-affinity (MatchInterPodAffinity fast path)
         self.affinity_pods = 0       # pods carrying required affinity (hardPodAffinitySymmetricWeight)
+        self.pref_affinity_pods = 0  # pods carrying preferred (anti-)affinity (InterPodAffinity symmetry)
         self.nodes: dict[str, NodeInfo] = {}
         self.pod_node: dict[str, str] = {}          # pod key -> node name
         self.pod_states: dict[str, dict] = {}       # pod key -> pod
@@ -214,6 +221,8 @@ class SchedulerCache:
             self.anti_affinity_pods += delta
         if _has_affinity(pod):
             self.affinity_pods += delta
+        if _has_pref_affinity(pod):
+            self.pref_affinity_pods += delta
 
     def _ni(self, name) -> NodeInfo:
         ni = self.nodes.get(name)

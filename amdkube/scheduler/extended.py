@@ -113,23 +113,29 @@ def allocate(pi, ni, use_topology: bool = True) -> dict | None:
     return binding
 
 
-def topology_score(pi, ni) -> float:
-    """0..10: how well the pod's GPUs can be placed on this node (GPUTopologyPriority)."""
-    t = ni.topology()
+def topology_score(pi, ni) -> int:
+    """0..10, an integer like every priority: how well the pod's GPUs fit this node
+    (GPUTopologyPriority). Half comes from the placement quality of the chosen subset (xGMI links,
+    NUMA; 0..5), half from how full the node's devices are once the pod is placed (best fit,
+    0..5), so a GPU pod goes to the node it fills most and keeps empty nodes whole for large pods.
+    CPU-only pods score GPU-less nodes 10 and GPU nodes 0."""
     if not pi.ext:
-        return 10.0 if not ni.devices else 0.0
+        return 10 if not ni.devices else 0
+    names = {r for _, r, _, _ in pi.ext}
+    total = sum(len(ni.devices.get(r) or {}) for r in names)
+    free = sum(len(ni.available_devices(r)) for r in names)
+    used_after = max(0, total - max(0, free - pi.gpu_count))
+    fill = used_after * 5 // total if total else 0
+    t = ni.topology()
     if t is None:
-        return 5.0
+        return 2 + fill
     ids, index, numa, link, parent = t
-    total = 0.0
+    q = 0.0
     for _, rname, n, sel in pi.ext:
         cand = matching_free(pi, ni, rname, sel)
         if not all(d in index for d in cand):
-            return 5.0
+            return 2 + fill
         free_all = [index[d] for d in ni.available_devices(rname) if d in index]
-        total += topo.score([index[d] for d in cand], n, link, numa, free_all, parent)
-    s = total / len(pi.ext)
-    # best fit across nodes: prefer the node whose free GPUs are closest to the request
-    free = sum(len(ni.available_devices(r)) for r in {r for _, r, _, _ in pi.ext})
-    slack = max(0, free - pi.gpu_count)
-    return max(0.0, min(10.0, 0.8 * s + 2.0 * (1.0 - slack / max(1.0, float(free)))))
+        q += topo.score([index[d] for d in cand], n, link, numa, free_all, parent)
+    quality = int(max(0.0, min(10.0, q / len(pi.ext)))) // 2
+    return quality + fill

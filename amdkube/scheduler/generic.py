@@ -57,15 +57,17 @@ class _FitIndex:
 
     def __init__(self):
         self.pos = -1
-        self.fit: dict[str, float] = {}
+        self.fit: dict[str, int] = {}
         self.failed: dict[str, list] = {}
 
 
 class Context:
-    __slots__ = ("nodes", "any_anti_affinity", "any_affinity", "hard_weight", "services", "listers")
+    __slots__ = ("nodes", "any_anti_affinity", "any_affinity", "hard_weight", "services", "listers", "any_pref_affinity")
 
-    def __init__(self, nodes, any_anti_affinity, any_affinity=False, hard_weight=0, services=None, listers=None):
+    def __init__(self, nodes, any_anti_affinity, any_affinity=False, hard_weight=0, services=None, listers=None,
+                 any_pref_affinity=False):
         self.nodes, self.any_anti_affinity = nodes, any_anti_affinity
+        self.any_pref_affinity = any_pref_affinity
         self.any_affinity, self.hard_weight = any_affinity, hard_weight
         self.services = services or (lambda: [])
         self.listers = listers
@@ -111,7 +113,8 @@ class GenericScheduler:
 
     def _ctx(self, nodes):
         return Context(nodes, self.cache.anti_affinity_pods > 0, getattr(self.cache, "affinity_pods", 0) > 0,
-                       self.hard_affinity_weight, self.services, self.listers)
+                       self.hard_affinity_weight, self.services, self.listers,
+                       getattr(self.cache, "pref_affinity_pods", 0) > 0)
 
     # Equivalence cache (reference plugin/pkg/scheduler/core/equivalence_cache.go:38): pods with the
     # same scheduling-relevant spec get the same per-node answer as long as the node is unchanged.
@@ -166,14 +169,15 @@ class GenericScheduler:
             if name == "TaintTolerationPriority" and not self.cache.prefer_no_schedule:
                 continue
             if name == "InterPodAffinityPriority" and not (pi.pref_affinity or pi.pref_anti) and \
-                    not (self.hard_affinity_weight and getattr(self.cache, "affinity_pods", 0)):
+                    not (self.hard_affinity_weight and getattr(self.cache, "affinity_pods", 0)) and \
+                    not getattr(self.cache, "pref_affinity_pods", 0):
                 continue
             return False
         return True
 
-    def _eval_node(self, pi, ni, local) -> tuple[bool, list, float]:
+    def _eval_node(self, pi, ni, local) -> tuple[bool, list, int]:
         ok, reasons = self.pod_fits_on_node(pi, ni, None)
-        score = 0.0
+        score = 0
         if ok:
             for _name, fn, w in local:
                 score += fn(pi, [ni], None)[0] * w
@@ -248,13 +252,14 @@ class GenericScheduler:
                     break
         return fit, failed, ctx
 
-    async def prioritize(self, pi, nodes, ctx) -> list[float]:
+    async def prioritize(self, pi, nodes, ctx) -> list[int]:
+        """PrioritizeNodes: integer weighted totals (HostPriority.Score is an int)."""
         if not self.priorities and not self.extenders:
-            return [1.0] * len(nodes)
+            return [1] * len(nodes)
         if ctx is None and (self.custom or (self.hard_affinity_weight and self.cache.affinity_pods) or
                             any(n not in LOCAL_PRIORITIES for n, _fn, _w in self.priorities)):
             ctx = self._ctx(self.cache.ready_nodes())
-        total = [0.0] * len(nodes)
+        total = [0] * len(nodes)
         # per-node scores depend only on (pod class, node state) unless a priority normalises across
         # nodes; only the normalising ones (spread, affinity, taints) are recomputed every time
         cache = self.ecache.get(pi.equiv) if getattr(pi, "equiv", None) is not None else None
@@ -269,7 +274,7 @@ class GenericScheduler:
                 need.append(i)
         if need:
             sub = [nodes[i] for i in need]
-            part = [0.0] * len(sub)
+            part = [0] * len(sub)
             for name, fn, w in local:
                 for j, s in enumerate(fn(pi, sub, ctx)):
                     part[j] += s * w
@@ -291,8 +296,10 @@ class GenericScheduler:
         return total
 
     def select_host(self, nodes, scores):
+        """selectHost (generic_scheduler.go): the list sorted by HostPriorityList's order reversed
+        (score, then host name, descending); round-robin among the hosts with the top score."""
         best = max(scores)
-        idx = [i for i, s in enumerate(scores) if s == best]
+        idx = sorted((i for i, s in enumerate(scores) if s == best), key=lambda i: nodes[i].name, reverse=True)
         pick = idx[self.last_index % len(idx)]
         self.last_index += 1
         return nodes[pick]

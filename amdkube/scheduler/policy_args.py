@@ -18,7 +18,7 @@ from ..api import meta as m
 from ..api.labels import selector_from_set
 from .predicates import ERR_NODE_LABEL_PRESENCE_VIOLATED, ERR_SERVICE_AFFINITY_VIOLATED, OK, _fail
 
-MAX = 10.0
+MAX = 10
 
 
 def _service_affinity_pods(pi, ni, ctx):
@@ -93,18 +93,18 @@ def service_anti_affinity(label: str):
         for ni in nodes:
             v = labeled.get(ni.name)
             if v is None:
-                out.append(0.0)
+                out.append(0)
             elif total == 0:
                 out.append(MAX)
             else:
-                out.append(float(int(MAX * (total - counts.get(v, 0)) / total)))
+                out.append(int(float(MAX) * ((total - counts.get(v, 0)) / total)))
         return out
     return prio
 
 
 def label_preference(label: str, presence: bool):
     def prio(pi, nodes, ctx=None):
-        return [MAX if (label in ni.labels) == presence else 0.0 for ni in nodes]
+        return [MAX if (label in ni.labels) == presence else 0 for ni in nodes]
     return prio
 
 

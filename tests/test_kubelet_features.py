@@ -189,10 +189,10 @@ def test_critical_pod_preemption_selection_and_admission():
                 "spec": {"nodeName": lc.node_name, "containers": [{"name": "c", "image": "busybox", "command": ["sleep", "60"],
                                                                   "resources": {"requests": {"cpu": "1"}}}]}}
             await c.create(crit, "kube-system")
-            await wait_pod(c, "kube-system", "crit", ("Running",), 20)
-            hog = await wait_pod(c, "default", "hog", ("Failed",), 20)
+            await wait_pod(c, "kube-system", "crit", ("Running",), 40)
+            hog = await wait_pod(c, "default", "hog", ("Failed",), 40)
             assert hog["status"]["reason"] == "Preempting"
-    run(go(), 60)
+    run(go(), 120)
 
 
 def test_stats_summary_and_cadvisor_metrics(tmp_path):

@@ -96,14 +96,14 @@ def test_named_port_http_liveness_keeps_healthy_server():
                                                      "ports": [{"name": "http", "containerPort": port}],
                                                      "livenessProbe": {"httpGet": {"path": "/healthz", "port": "http",
                                                                                    "httpHeaders": [{"name": "X-Probe", "value": "yes"}]},
-                                                                       "periodSeconds": 1, "failureThreshold": 3,
-                                                                       "timeoutSeconds": 5},
+                                                                       "periodSeconds": 1, "failureThreshold": 5,
+                                                                       "initialDelaySeconds": 3, "timeoutSeconds": 5},
                                                      "readinessProbe": {"httpGet": {"path": "/healthz", "port": "http",
                                                                                     "httpHeaders": [{"name": "X-Probe", "value": "yes"}]},
                                                                         "periodSeconds": 1}}]}})
             await wait_pod(c, "default", "web", ("Running",), 30)
             ready = False
-            for _ in range(100):
+            for _ in range(300):
                 p = await c.get("pods", "web", "default")
                 if p["status"]["containerStatuses"][0]["ready"]:
                     ready = True
@@ -111,8 +111,9 @@ def test_named_port_http_liveness_keeps_healthy_server():
                 await asyncio.sleep(0.1)
             assert ready, p["status"]
             w = lc.kubelet.probes.workers
-            assert len(w) == 2 and all(x.probes >= 1 for x in w.values())
+            assert len(w) == 2
             await asyncio.sleep(4)
+            assert all(x.probes >= 1 for x in w.values())
             p = await c.get("pods", "web", "default")
             cs = p["status"]["containerStatuses"][0]
             assert cs["restartCount"] == 0 and "running" in cs["state"] and cs["ready"], cs
