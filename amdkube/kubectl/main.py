@@ -39,59 +39,92 @@ def _client(a) -> Client:
     return Client(server or "http://127.0.0.1:8080", token=token, user_agent="kubectl/amdkube")
 
 
-def _jsonpath(obj, expr: str):
-    expr = expr.strip()
-    if expr.startswith("{") and expr.endswith("}"):
-        expr = expr[1:-1]
-    cur = [obj]
-    for part in re.findall(r"\.([^.\[]+)|\[(\*|\d+)\]", expr):
-        key, idx = part
-        nxt = []
-        for c in cur:
-            if key:
-                if isinstance(c, dict) and key in c:
-                    nxt.append(c[key])
-            elif idx == "*":
-                nxt.extend(c if isinstance(c, list) else [])
-            elif isinstance(c, list) and int(idx) < len(c):
-                nxt.append(c[int(idx)])
-        cur = nxt
-    return " ".join(json.dumps(x) if isinstance(x, (dict, list)) else str(x) for x in cur)
+def _jsonpath(obj, expr: str, allow_missing: bool = True):
+    from .jsonpath import JSONPath
+    return JSONPath("jsonpath", allow_missing).parse(expr).execute(obj)
 
 
-def _emit(objs, a, kind=None, single=False, out=None):
+def _read_template(a, value: str, kind: str) -> str:
+    """-o <kind>=<template> or <kind>-file=<path>, or --template."""
+    if value:
+        return value
+    tpl = getattr(a, "template", None)
+    if tpl:
+        return tpl
+    raise SystemExit(f"error: template format specified but no template given")
+
+
+def _emit(objs, a, kind=None, single=False, out=None, with_headers=True):
+    """The printer -o selects (pkg/kubectl/cmd/util/printing.go PrinterForOptions): json, yaml,
+    name, wide, jsonpath[-file], go-template[-file], custom-columns[-file], or the table;
+    --sort-by orders a list first (SortingPrinter)."""
+    from . import gotemplate
+    from .jsonpath import JSONPathError
     out = out or sys.stdout
     o = a.output or ""
+    allow_missing = getattr(a, "allow_missing_template_keys", True)
+    sort_by = getattr(a, "sort_by", None)
+    if sort_by and not single and len(objs) > 1:
+        try:
+            objs = printers.sort_objects(objs, sort_by)
+        except (ValueError, JSONPathError) as e:
+            raise SystemExit(f"error: {e}")
+    data = objs[0] if single and len(objs) == 1 else {"apiVersion": "v1", "kind": "List", "items": objs,
+                                                      "metadata": {"resourceVersion": "", "selfLink": ""}}
     if o == "json":
-        if single and len(objs) == 1:
-            print(json.dumps(objs[0], indent=2), file=out)
-        else:
-            print(json.dumps({"apiVersion": "v1", "kind": "List", "items": objs}, indent=2), file=out)
+        print(json.dumps(data, indent=4), file=out)
     elif o == "yaml":
-        print(dump_yaml(objs[0] if single and len(objs) == 1 else {"apiVersion": "v1", "kind": "List", "items": objs}), file=out, end="")
+        print(dump_yaml(data), file=out, end="")
     elif o == "name":
         for x in objs:
             print(f"{(x.get('kind') or kind or '').lower()}/{m.name_of(x)}", file=out)
-    elif o.startswith("jsonpath="):
-        expr = o[len("jsonpath="):]
-        if single and len(objs) == 1:
-            print(_jsonpath(objs[0], expr), file=out)
-        else:
-            print(_jsonpath({"items": objs}, expr), file=out)
-    else:
-        wide = o == "wide"
-        all_ns = getattr(a, "all_namespaces", False)
+    elif o.startswith(("jsonpath=", "jsonpath-file=")) or o == "jsonpath":
+        expr = o.split("=", 1)[1] if "=" in o else ""
+        if o.startswith("jsonpath-file="):
+            expr = open(expr).read()
+        expr = _read_template(a, expr, "jsonpath")
+        try:
+            print(_jsonpath(data, expr, allow_missing), file=out, end="")
+        except JSONPathError as e:
+            raise SystemExit(f"error: error executing jsonpath {expr!r}: {e}")
+    elif o.startswith(("go-template=", "go-template-file=", "template=", "templatefile=")) or o in ("go-template", "template"):
+        tpl = o.split("=", 1)[1] if "=" in o else ""
+        if o.startswith(("go-template-file=", "templatefile=")):
+            tpl = open(tpl).read()
+        tpl = _read_template(a, tpl, "go-template")
+        try:
+            print(gotemplate.render(tpl, data, allow_missing), file=out, end="")
+        except gotemplate.TemplateError as e:
+            raise SystemExit(f"error: error executing template {tpl!r}: {e}")
+    elif o.startswith(("custom-columns=", "custom-columns-file=")):
+        spec = o.split("=", 1)[1]
+        try:
+            if o.startswith("custom-columns-file="):
+                ccp = printers.CustomColumnsPrinter.from_template(open(spec).read())
+            else:
+                ccp = printers.CustomColumnsPrinter.from_spec(spec, getattr(a, "no_headers", False))
+        except (ValueError, JSONPathError) as e:
+            raise SystemExit(f"error: {e}")
+        print(ccp.print(objs), file=out, end="")
+    elif o in ("", "wide"):
         k = kind or (objs[0].get("kind") if objs else "")
-        if k == "Pod":
-            txt = printers.pods_table(objs, wide, all_ns)
-        elif k == "Node":
-            txt = printers.nodes_table(objs, wide)
-        else:
-            txt = printers.generic_table(objs, k, all_ns)
-        if objs:
-            print(txt, file=out)
-        else:
-            print(f"No resources found.", file=out)
+        if k == "Pod" and not single and not getattr(a, "show_all", True):
+            objs = [p for p in objs if (p.get("status") or {}).get("phase") not in ("Succeeded", "Failed")]
+        if not objs:
+            print("No resources found.", file=sys.stderr)
+            return
+        label_cols = []
+        for spec in getattr(a, "label_columns", None) or []:
+            label_cols += [x.strip() for x in spec.split(",") if x.strip()]
+        txt = printers.print_table(objs, k, wide=o == "wide", with_namespace=getattr(a, "all_namespaces", False),
+                                   show_labels=getattr(a, "show_labels", False), label_columns=label_cols,
+                                   no_headers=getattr(a, "no_headers", False) or not with_headers,
+                                   with_kind=getattr(a, "show_kind", False))
+        print(txt, file=out)
+    else:
+        raise SystemExit(f"error: unable to match a printer suitable for the output format \"{o}\", allowed formats "
+                         f"are: custom-columns,custom-columns-file,go-template,go-template-file,json,jsonpath,"
+                         f"jsonpath-file,name,template,templatefile,wide,yaml")
 
 
 MANIFEST_EXTS = (".yaml", ".yml", ".json")
@@ -158,32 +191,50 @@ async def cmd_get(c, a):
     for r, name in targets:
         ri = SCHEME.resolve(r)
         if ri is None:
+            try:
+                await c.discover()
+            except Exception:
+                pass
+            ri = SCHEME.resolve(r)
+        if ri is None:
             raise SystemExit(f'error: the server doesn\'t have a resource type "{r}"')
         ns = _ns(a, ri)
+        res = ri.plural if not ri.group else f"{ri.plural}.{ri.group}"
         if name:
-            objs = [await c.get(ri.plural if not ri.group else f"{ri.plural}.{ri.group}", name, ns)]
-            _emit(objs, a, ri.kind, single=True)
+            obj = await c.get(res, name, ns)
+            obj.setdefault("kind", ri.kind)
+            obj.setdefault("apiVersion", ri.api_version)
+            _emit([obj], a, ri.kind, single=True)
         else:
-            items, rv = await c.list(ri.plural if not ri.group else f"{ri.plural}.{ri.group}", ns, a.selector, a.field_selector)
+            items, rv = await c.list(res, ns, a.selector, a.field_selector)
             for it in items:
                 it.setdefault("kind", ri.kind)
                 it.setdefault("apiVersion", ri.api_version)
             _emit(items, a, ri.kind)
             if a.watch:
-                async for typ, obj in c.watch(ri.plural, ns, rv, a.selector, a.field_selector):
-                    _emit([obj], a, ri.kind)
+                async for typ, obj in c.watch(res, ns, rv, a.selector, a.field_selector):
+                    _emit([obj], a, ri.kind, with_headers=False)
 
 
 async def cmd_describe(c, a):
+    from .describe import describe, gather_extra
     for r, name in _split_targets(a.args):
         ri = SCHEME.resolve(r)
+        if ri is None:
+            raise SystemExit(f'error: the server doesn\'t have a resource type "{r}"')
         ns = _ns(a, ri)
-        objs = [await c.get(ri.plural, name, ns)] if name else (await c.list(ri.plural, ns, a.selector))[0]
+        res = ri.plural if not ri.group else f"{ri.plural}.{ri.group}"
+        objs = [await c.get(res, name, ns)] if name else (await c.list(res, ns, a.selector))[0]
         for o in objs:
             o.setdefault("kind", ri.kind)
-            evs, _ = await c.list("events", m.namespace_of(o) or "default",
-                                  field_selector=f"involvedObject.name={m.name_of(o)},involvedObject.kind={ri.kind}")
-            print(printers.describe(o, evs))
+            o.setdefault("apiVersion", ri.api_version)
+            fs = f"involvedObject.name={m.name_of(o)},involvedObject.kind={ri.kind}"
+            try:
+                evs, _ = await c.list("events", m.namespace_of(o) or ("default" if ri.namespaced else ""), field_selector=fs)
+            except m.StatusError:
+                evs = []
+            evs = [e for e in evs if (e.get("involvedObject") or {}).get("uid") in (None, "", m.uid_of(o))]
+            print(describe(o, evs, **(await gather_extra(c, o))))
             print()
 
 
@@ -500,6 +551,15 @@ def parser():
                         type=lambda s: s.lower() not in ("false", "0", "no"))
         sp.add_argument("--recursive", action="store_true")
         sp.add_argument("--api-version", dest="explain_api_version", default=None)
+        # printing flags (pkg/kubectl/cmd/util/printing.go AddPrinterFlags / AddOutputFlags)
+        sp.add_argument("--show-labels", action="store_true")
+        sp.add_argument("-L", "--label-columns", action="append", default=[])
+        sp.add_argument("--sort-by", default=None)
+        sp.add_argument("--no-headers", action="store_true")
+        sp.add_argument("--template", default=None)
+        sp.add_argument("--allow-missing-template-keys", type=lambda s: s != "false", default=True)
+        sp.add_argument("-a", "--show-all", action="store_true")
+        sp.add_argument("--show-kind", action="store_true")
     return p
 
 

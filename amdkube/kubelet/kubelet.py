@@ -1109,9 +1109,9 @@ class Kubelet:
         msg = "Preempted in order to admit critical pod"
         for v in victims:
             self.recorder.event(v, "Warning", "Preempting", msg)
-            await self.runtime.kill_pod(m.uid_of(v), int((v.get("spec") or {}).get("terminationGracePeriodSeconds", 30)), v)
-            self.status.set(v, {"phase": "Failed", "reason": "Preempting", "message": msg,
-                                "conditions": (v.get("status") or {}).get("conditions") or []})
+            # killPodNow through _evict_kill: terminal first, so a racing sync never restarts it
+            await self._evict_kill(v, {"phase": "Failed", "reason": "Preempting", "message": msg},
+                                   int((v.get("spec") or {}).get("terminationGracePeriodSeconds", 30)))
         return bool(victims)
 
     async def _admit(self, pod: dict) -> bool:

@@ -152,9 +152,17 @@ async def test_dns_component_serves_from_a_corefile_in_the_container_view(tmp_pa
     (root / "etc" / "coredns").mkdir(parents=True)
     (root / "etc" / "coredns" / "Corefile").write_text(
         ph.COREFILE.format(domain="corp.local", cidr="10.96.0.0/12").replace("proxy . /etc/resolv.conf", ""))
-    with socket.socket(socket.AF_INET, socket.SOCK_DGRAM) as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+    # the server binds UDP and TCP on the same port: pick one free for both
+    for _ in range(50):
+        with socket.socket(socket.AF_INET, socket.SOCK_DGRAM) as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+            try:
+                with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as t:
+                    t.bind(("127.0.0.1", port))
+                break
+            except OSError:
+                continue
     srv = await APIServer().start()
     proc = None
     try:

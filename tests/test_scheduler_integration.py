@@ -10,6 +10,7 @@ Node objects):
 """
 import asyncio
 
+import pytest
 from aiohttp import web
 
 from amdkube.apiserver import APIServer
@@ -93,7 +94,8 @@ def test_extender_filter_prioritize_bind():
         async def bind(r):
             body = await r.json()
             seen["bind"].append(body)
-            await api_holder["c"].bind(body["podNamespace"], body["podName"], body["node"], body.get("extendedResourceBinding"))
+            # ExtenderBindingArgs carries Go's field names (no json tags in the reference)
+            await api_holder["c"].bind(body["PodNamespace"], body["PodName"], body["Node"], body.get("extendedResourceBinding"))
             return web.json_response({})
 
         app = web.Application()
@@ -237,3 +239,100 @@ def test_nominated_preemptor_is_not_overtaken_by_a_lower_priority_pod():
         finally:
             await _stop(api, c, s)
     run(go(), 60)
+
+
+def test_extender_over_tls_with_client_certificate_and_node_cache(tmp_path):
+    """extender.go makeTransport + nodeCacheCapable: an HTTPS extender that demands a client
+    certificate gets `nodenames` (not full Node objects) for filter and prioritize, answers with
+    `nodenames`, and the pod lands where it says; httpTimeout is a Duration in nanoseconds."""
+    import ssl
+    from amdkube.kubeadm import new_ca, new_cert
+    d = str(tmp_path)
+    new_ca(d)
+    new_cert(d, "ext", "extender", sans=["IP:127.0.0.1", "DNS:localhost"], server=True)
+    new_cert(d, "sched", "system:kube-scheduler")
+
+    async def go():
+        seen = {"filter": [], "prioritize": [], "peer": []}
+
+        async def filt(r):
+            body = await r.json()
+            seen["filter"].append(body)
+            seen["peer"].append(r.transport.get_extra_info("peercert"))
+            keep = [n for n in body["nodenames"] if n != "node-0000"]
+            return web.json_response({"nodenames": keep, "failedNodes": {"node-0000": "cached: no"}})
+
+        async def prio(r):
+            body = await r.json()
+            seen["prioritize"].append(body)
+            return web.json_response([{"host": n, "score": 10 if n == "node-0002" else 1} for n in body["nodenames"]])
+
+        app = web.Application()
+        app.router.add_post("/ext/filter", filt)
+        app.router.add_post("/ext/prioritize", prio)
+        sctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+        sctx.load_cert_chain(f"{d}/ext.crt", f"{d}/ext.key")
+        sctx.load_verify_locations(f"{d}/ca.crt")
+        sctx.verify_mode = ssl.CERT_REQUIRED
+        runner = web.AppRunner(app)
+        await runner.setup()
+        site = web.TCPSite(runner, "127.0.0.1", 0, ssl_context=sctx)
+        await site.start()
+        port = site._server.sockets[0].getsockname()[1]
+        policy = {"kind": "Policy", "extenders": [{
+            "urlPrefix": f"https://127.0.0.1:{port}/ext", "filterVerb": "filter", "prioritizeVerb": "prioritize",
+            "weight": 5, "enableHttps": True, "nodeCacheCapable": True, "httpTimeout": 3_000_000_000,
+            "tlsConfig": {"CAFile": f"{d}/ca.crt", "CertFile": f"{d}/sched.crt", "KeyFile": f"{d}/sched.key"}}]}
+        api, c, s = await _cluster(3, policy=policy)
+        try:
+            ext = s.extenders[0]
+            assert ext.timeout == 3.0 and ext.node_cache_capable
+            await c.create(_pod("t1"))
+            assert await _node_of(c, "t1") == "node-0002"
+            assert seen["filter"] and all("nodes" not in b and set(b["nodenames"]) <= {"node-0000", "node-0001", "node-0002"}
+                                          for b in seen["filter"])
+            assert seen["prioritize"] and "node-0000" not in seen["prioritize"][0]["nodenames"]
+            assert seen["peer"][0] and dict(x[0] for x in seen["peer"][0]["subject"])["commonName"] == "system:kube-scheduler"
+            # without the client certificate the extender refuses the handshake: scheduling fails
+            from amdkube.scheduler.extender import HTTPExtender
+            bare = HTTPExtender({**policy["extenders"][0], "tlsConfig": {"CAFile": f"{d}/ca.crt"}})
+            try:
+                with pytest.raises(Exception):
+                    await bare.filter({"metadata": {"name": "x"}}, [{"metadata": {"name": "node-0001"}}])
+            finally:
+                await bare.close()
+        finally:
+            await _stop(api, c, s)
+            await runner.cleanup()
+    run(go(), 60)
+
+
+def test_extender_config_keys_and_errors():
+    """Go's case-insensitive decoding (BindVerb has no json tag), Duration nanoseconds, the 5 s
+    default, enableHttps without a CA → insecure, and the send() error text on a non-200 answer."""
+    import ssl
+    from amdkube.scheduler.extender import HTTPExtender, tls_context
+
+    e = HTTPExtender({"urlPrefix": "http://x/", "BindVerb": "bind", "FilterVerb": "f", "httpTimeout": 0})
+    assert e.bind_verb == "bind" and e.filter_verb == "f" and e.timeout == 5.0 and e.ssl is None
+    assert HTTPExtender({"urlPrefix": "http://x", "httpTimeout": 250_000_000}).timeout == 0.25
+    ctx = tls_context(True, None)
+    assert ctx is not None and ctx.verify_mode == ssl.CERT_NONE
+
+    async def go():
+        app = web.Application()
+        app.router.add_post("/e/filter", lambda r: web.Response(status=500))
+        runner = web.AppRunner(app)
+        await runner.setup()
+        site = web.TCPSite(runner, "127.0.0.1", 0)
+        await site.start()
+        port = site._server.sockets[0].getsockname()[1]
+        ext = HTTPExtender({"urlPrefix": f"http://127.0.0.1:{port}/e", "filterVerb": "filter", "prioritizeVerb": "filter"})
+        try:
+            with pytest.raises(RuntimeError, match=f"Failed filter with extender at URL http://127.0.0.1:{port}/e, code 500"):
+                await ext.filter({"metadata": {"name": "p"}}, [{"metadata": {"name": "n"}}])
+            assert await ext.prioritize({"metadata": {"name": "p"}}, [{"metadata": {"name": "n"}}]) == {}
+        finally:
+            await ext.close()
+            await runner.cleanup()
+    run(go())
