@@ -32,7 +32,10 @@ from .networking import EndpointsController, NodeIPAMController
 from .policy import ClusterRoleAggregationController, DisruptionController, ResourceQuotaController, TTLController
 from .volumes import (AttachDetachController, PersistentVolumeBinderController, PVCProtectionController,
                       PVProtectionController, VolumeExpandController)
-from .workloads import DaemonSetController, DeploymentController, JobController, ReplicaSetController
+from .daemonset import DaemonSetController
+from .deployment import DeploymentController
+from .job import JobController
+from .replicaset import ReplicaSetController
 
 
 @dataclass

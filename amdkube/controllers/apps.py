@@ -24,7 +24,7 @@ import time
 from ..api import meta as m
 from ..api.labels import selector_from_set
 from .base import Controller, split_key
-from .workloads import ReplicaSetController
+from .replicaset import ReplicaSetController
 
 log = logging.getLogger("amdkube.controllers.cronjob")
 

@@ -298,3 +298,22 @@ def recheck_deletion(get_fresh):
                                f"{fresh['metadata']['deletionTimestamp']}")
         return fresh
     return check
+
+
+def pod_from_template(owner, api_version, kind, extra_labels=None, node=None):
+    """GetPodFromTemplate (controller_utils.go): a pod from the owner's template, named after
+    the owner (generateName), labelled with the template's labels plus `extra_labels`,
+    controlled by the owner, optionally pinned to `node`."""
+    import json as _json
+    tpl = _json.loads(_json.dumps((owner.get("spec") or {}).get("template") or {}))
+    md = tpl.get("metadata") or {}
+    labels = dict(md.get("labels") or {})
+    labels.update(extra_labels or {})
+    pod = {"apiVersion": "v1", "kind": "Pod",
+           "metadata": {"generateName": m.name_of(owner) + "-", "namespace": m.namespace_of(owner), "labels": labels,
+                        "annotations": dict(md.get("annotations") or {}),
+                        "ownerReferences": [m.new_controller_ref(owner, api_version, kind)]},
+           "spec": tpl.get("spec") or {}}
+    if node:
+        pod["spec"]["nodeName"] = node
+    return pod

@@ -146,7 +146,7 @@ class _PodControl:
         self.ctl = ctl
 
     async def create(self, job):
-        from .workloads import _pod_from_template
+        from .controller_utils import pod_from_template as _pod_from_template
         key = m.key_of(job)
         self.ctl._expect(key, adds=1)
         try:

@@ -1,6 +1,6 @@
 #!/bin/bash
 B=amdkube/_native/bin
-H=hack/exp/hsa_status
+H=hack/gpu/experiments/hsa_status
 R=$(ls /dev/dri/renderD* | head -1)
 run() { echo "== $1"; shift; env -u ROCR_VISIBLE_DEVICES -u HIP_VISIBLE_DEVICES timeout -k 5 60 "$@" 2>&1 | tail -4; echo "rc=${PIPESTATUS[0]}"; }
 run "baseline" $H

@@ -4,7 +4,7 @@ Prints one JSON object: identity, capabilities, LSMs, user-namespace sysctls, wh
 unprivileged user+mount namespace can hide /dev/dri nodes and bind one back, whether a PID
 namespace can mount its own /proc, the Landlock ABI, cgroup-v2 delegation, and whether the
 GPU opens from inside such a namespace. Every experiment runs in a forked child so this
-process is never changed.   python hack/exp/probe_isolation.py > gpurun_out/iso_probe.json
+process is never changed.   python hack/gpu/experiments/probe_isolation.py > gpurun_out/iso_probe.json
 """
 from __future__ import annotations
 

@@ -9,5 +9,5 @@ timeout -k 10 120 python -u -m pytest tests/test_gpu.py -k "test_95 or test_92 o
 timeout -k 10 60 ./amdkube/_native/bin/hbm-probe --mib 1024 --iters 20 > $O/hbm_1g.json 2>&1 &&
 timeout -k 10 60 ./amdkube/_native/bin/hbm-probe --mib 4096 --iters 10 > $O/hbm_4g.json 2>&1 &&
 timeout -k 10 90 rocprofv3 --kernel-trace --stats -d $O/prof -o hbm -- ./amdkube/_native/bin/hbm-probe --mib 1024 --iters 10 > $O/prof.log 2>&1 &&
-timeout -k 10 60 hack/exp/vadd_front6 > $O/vadd_front6.jsonl 2>&1 &&
+timeout -k 10 60 hack/gpu/experiments/vadd_front6 > $O/vadd_front6.jsonl 2>&1 &&
 echo done
