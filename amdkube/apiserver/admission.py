@@ -29,12 +29,15 @@ CREATE, UPDATE, DELETE, CONNECT = "CREATE", "UPDATE", "DELETE", "CONNECT"
 
 
 class Attributes:
-    __slots__ = ("operation", "resource", "subresource", "namespace", "name", "obj", "old", "user", "kind", "group")
+    __slots__ = ("operation", "resource", "subresource", "namespace", "name", "obj", "old", "user", "kind", "group",
+                 "dry_run")
 
-    def __init__(self, operation, resource, subresource, namespace, name, obj, old=None, user=None, kind="", group=""):
+    def __init__(self, operation, resource, subresource, namespace, name, obj, old=None, user=None, kind="", group="",
+                 dry_run=False):
         self.operation, self.resource, self.subresource = operation, resource, subresource
         self.namespace, self.name, self.obj, self.old, self.user, self.kind = namespace, name, obj, old, user, kind
         self.group = group
+        self.dry_run = dry_run          # ?dryRun=All or a webhook preview: check, but change nothing
 
 
 class Plugin:
@@ -527,6 +530,12 @@ class ResourceQuota(Plugin):
             delta = Q.subtract_non_negative(delta, prev)
         if Q.is_zero(delta):
             return
+        if a.dry_run:
+            # a dry run (or the validating-webhook preview of a create) is checked against the
+            # quotas as they stand, but takes nothing: the real request charges once
+            for qq in quotas:
+                self._charge(ctx, Q, qq, delta, a, check_only=True)
+            return
         charged = []
         try:
             for qq in quotas:
@@ -541,7 +550,7 @@ class ResourceQuota(Plugin):
             raise
 
     @staticmethod
-    def _charge(ctx, Q, quota, delta, a, refund=False):
+    def _charge(ctx, Q, quota, delta, a, refund=False, check_only=False):
         name = m.name_of(quota)
 
         def apply(cur):
@@ -564,6 +573,9 @@ class ResourceQuota(Plugin):
             out = m.deepcopy(cur)
             out.setdefault("status", {})["used"] = {**(st.get("used") or {}), **Q.format_list(Q.mask(new_used, requested))}
             return out
+        if check_only:
+            apply(quota)
+            return
         ctx.guaranteed_update_object("resourcequotas", m.namespace_of(quota), name, apply)
 
 

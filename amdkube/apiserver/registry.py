@@ -269,7 +269,7 @@ class ResourceStore:
             spec["username"], spec["uid"] = user.get("name", ""), user.get("uid", "")
             spec["groups"] = list(user.get("groups") or [])
         attrs = adm.Attributes(adm.CREATE, ri.plural, "", md.get("namespace", ""), md.get("name", ""), obj, None, user, ri.kind,
-                               ri.group)
+                               ri.group, dry_run=dry_run)
         self.api.admission.admit(attrs, self.api)
         SCHEME.default(obj)  # admission may add fields (e.g. ResourceV2) that need defaults
         errs = SCHEME.validate(obj)

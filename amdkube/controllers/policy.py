@@ -271,7 +271,12 @@ class ResourceQuotaController(Controller):
         used = Q.format_list(Q.calculate_usage(q, self._objects(ns)))
         st = {"hard": dict(hard), "used": used}
         if (q.get("status") or {}) != st:
-            await self.client.patch("resourcequotas", name, {"status": st}, ns, sub="status")
+            # UpdateStatus with the resourceVersion that was read (resource_quota_controller.go
+            # :350-371): a reservation the admission plugin made since then is a conflict, and
+            # the key is retried once the informer has the newer quota
+            out = m.deepcopy(q)
+            out["status"] = st
+            await self.client.update_status(out)
 
 
 # --------------------------------------------------------------------------- node TTL

@@ -95,6 +95,44 @@ def revert_from_systemd(name: str) -> str:
     return n.replace("-", "/").replace("_", "-")
 
 
+RUNTIME_DEFAULT_ROOT = "/sys/fs/cgroup/amdkube"      # rocshim's cgroupfs-driver tree
+
+
+def cgroup2_mount_of(path: str, mountinfo: str = "/proc/self/mountinfo") -> str | None:
+    """The cgroup2 mount point `path` lies in (the deepest one), or None."""
+    path = os.path.abspath(path)
+    best = None
+    try:
+        with open(mountinfo) as f:
+            lines = f.read().splitlines()
+    except OSError:
+        return None
+    for line in lines:
+        left, _, right = line.partition(" - ")
+        fields = left.split()
+        if len(fields) < 5 or not right.startswith("cgroup2 "):
+            continue
+        mp = fields[4].replace("\\040", " ")
+        if (path == mp or path.startswith(mp.rstrip("/") + "/")) and (best is None or len(mp) > len(best)):
+            best = mp
+    return best
+
+
+def systemd_cgroup_root(root: str, mountinfo: str = "/proc/self/mountinfo") -> str:
+    """The cgroup root the systemd driver works under. systemd lays slices out from the cgroup2
+    mount, so a root inside that mount is only meaningful as the mount itself: the runtime's
+    cgroupfs default is remapped to it (as rocshim does), any other sub-directory is refused at
+    start instead of every pods-cgroup create waiting out a directory systemd never makes. A
+    root outside every cgroup2 mount (a test tree fed by a stand-in systemd) is kept."""
+    mount = cgroup2_mount_of(root, mountinfo)
+    if mount is None or os.path.abspath(root) == mount:
+        return root
+    if os.path.abspath(root) == RUNTIME_DEFAULT_ROOT:
+        return mount
+    raise CgroupError(f"--cgroup-driver=systemd: --cgroup-root {root} is not the cgroup2 mount {mount}; "
+                      f"systemd creates slices from the mount, so the root must be {mount}")
+
+
 def use_systemd(run_dir: str = "/run/systemd/system") -> bool:
     """libcontainer UseSystemd / sd_booted: systemd is the init system."""
     return os.path.isdir(run_dir)
@@ -129,27 +167,33 @@ class SystemdUnits:
     """The systemd manager calls the cgroup drivers need."""
 
     def __init__(self, connect=systemd_connection):
+        import threading
         self._connect = connect
         self._conn = None
+        # rocshim and the kubelet call from worker threads (asyncio.to_thread): one call at a
+        # time on the shared connection, and one reconnect
+        self._lock = threading.RLock()
 
     def _call(self, member: str, sig: str, *args):
         from ..utils.dbus import DBusError
-        for attempt in (0, 1):
-            if self._conn is None:
-                self._conn = self._connect()
-            try:
-                return self._conn.call(SYSTEMD_DEST, SYSTEMD_PATH, SYSTEMD_MANAGER, member, sig, *args)
-            except (OSError, DBusError) as e:
-                if isinstance(e, DBusError) and e.name != "org.freedesktop.DBus.Error.Disconnected":
-                    raise
-                self.close()                   # a restarted systemd: reconnect once
-                if attempt:
-                    raise
+        with self._lock:
+            for attempt in (0, 1):
+                if self._conn is None:
+                    self._conn = self._connect()
+                try:
+                    return self._conn.call(SYSTEMD_DEST, SYSTEMD_PATH, SYSTEMD_MANAGER, member, sig, *args)
+                except (OSError, DBusError) as e:
+                    if isinstance(e, DBusError) and e.name != "org.freedesktop.DBus.Error.Disconnected":
+                        raise
+                    self.close()                   # a restarted systemd: reconnect once
+                    if attempt:
+                        raise
 
     def close(self):
-        if self._conn is not None:
-            self._conn.close()
-            self._conn = None
+        with self._lock:
+            if self._conn is not None:
+                self._conn.close()
+                self._conn = None
 
     def start_transient(self, unit: str, properties: list) -> str:
         """StartTransientUnit(name, "replace", properties, aux=[]) -> the job's object path."""

@@ -266,6 +266,9 @@ class Kubelet:
                                       image_pull_burst=config.registry_burst, serialize_image_pulls=config.serialize_image_pulls)
         self.runtime.cpu_cfs_quota = config.cpu_cfs_quota
         self.runtime.cgroup_driver = config.cgroup_driver
+        if config.cgroup_driver == "systemd" and config.cgroup_root:
+            from .cgroups import systemd_cgroup_root
+            config.cgroup_root = systemd_cgroup_root(config.cgroup_root)
         self.runtime.legacy_logs_dir = config.container_logs_dir or (
             "/var/log/containers" if os.path.abspath(config.root_dir) == "/var/lib/kubelet"
             else os.path.join(config.root_dir, "containers-logs"))
@@ -341,6 +344,7 @@ class Kubelet:
         self.stats = StatsProvider(self, du_ttl=config.volume_stats_agg_period)
         self._cpuset_applied: dict[str, str] = {}
         self._pods_cgroup_enforced = None
+        self._cgroup_task: asyncio.Task | None = None
         self._cgroup_manager = None         # cgroups.CgroupManager for --cgroup-driver
         self.pressure: set[str] = set()
         self.status = StatusManager(client, on_terminal=self._on_terminal)
@@ -684,14 +688,28 @@ class Kubelet:
         elif self._cloud_addrs:
             st["addresses"] = list(self._cloud_addrs)
         st["_removed"] = removed
-        if self.cfg.cgroup_root and "pods" in self.cfg.enforce_node_allocatable.split(",") and \
-                self._pods_cgroup_enforced != (alloc.get("cpu"), alloc.get("memory")):
-            if self._cgroup_manager is None:
-                from .cgroups import CgroupManager
-                self._cgroup_manager = CgroupManager(self.cfg.cgroup_driver, self.cfg.cgroup_root)
-            if enforce_pods_cgroup(self.cfg.cgroup_root, alloc, manager=self._cgroup_manager):
-                self._pods_cgroup_enforced = (alloc.get("cpu"), alloc.get("memory"))
         return st
+
+    def _enforce_pods_cgroup(self, alloc: dict):
+        """enforceNodeAllocatableCgroups (node_container_manager_linux.go): the pods cgroup capped
+        at allocatable, once per allocatable value. Creating it under the systemd driver is a
+        D-Bus round trip plus a wait for systemd's directory, so it runs in a worker thread,
+        one at a time, and never holds up the node-status update (or the pod workers and PLEG
+        sharing its event loop); a failed attempt is retried on a later update."""
+        if not self.cfg.cgroup_root or "pods" not in self.cfg.enforce_node_allocatable.split(","):
+            return None
+        want = (alloc.get("cpu"), alloc.get("memory"))
+        if self._pods_cgroup_enforced == want or (self._cgroup_task is not None and not self._cgroup_task.done()):
+            return None
+        if self._cgroup_manager is None:
+            from .cgroups import CgroupManager
+            self._cgroup_manager = CgroupManager(self.cfg.cgroup_driver, self.cfg.cgroup_root)
+
+        async def enforce():
+            if await asyncio.to_thread(enforce_pods_cgroup, self.cfg.cgroup_root, dict(alloc), manager=self._cgroup_manager):
+                self._pods_cgroup_enforced = want
+        self._cgroup_task = asyncio.get_running_loop().create_task(enforce(), name="kubelet-pods-cgroup")
+        return self._cgroup_task
 
     async def _node_images(self):
         """setNodeStatusImages (kubelet_node_status.go:692-720): the runtime's images, largest
@@ -709,6 +727,7 @@ class Kubelet:
     async def update_node_status(self):
         prev = (self.node or {}).get("status") or {}
         body = self._node_status_body(prev)
+        self._enforce_pods_cgroup(body["allocatable"])
         images = await self._node_images()
         if images is not None:
             body["images"] = images

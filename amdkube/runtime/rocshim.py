@@ -361,7 +361,12 @@ class RocShim:
         self.cgroup_driver = cgroup_driver
         self.systemd = (systemd_units or SystemdUnits()) if cgroup_driver == SYSTEMD else None
         self._slices: set[str] = set()       # pod slices this runtime started (systemd driver)
-        self.cgroup_root = "/sys/fs/cgroup" if cgroup_driver == SYSTEMD and cgroup_root == "/sys/fs/cgroup/amdkube" else cgroup_root
+        self.cgroup_root = cgroup_root
+        if cgroup_driver == SYSTEMD:
+            from ..kubelet.cgroups import RUNTIME_DEFAULT_ROOT, systemd_cgroup_root
+            self.cgroup_root = systemd_cgroup_root(cgroup_root)
+            if self.cgroup_root == RUNTIME_DEFAULT_ROOT:       # no cgroup2 mount in view: the usual one
+                self.cgroup_root = "/sys/fs/cgroup"
         self.dev_root = dev_root
         self.sandboxes: dict[str, Sandbox] = {}
         self.containers: dict[str, Container] = {}
@@ -1055,8 +1060,18 @@ class RocShim:
             os.close(w)                       # EOF: nsexec refuses to run the container
             await proc.wait()
             raise RuntimeError(f"systemd scope for container {c.id}: {e}") from e
-        os.write(w, b"1")
-        os.close(w)
+        try:
+            os.write(w, b"1")
+        except OSError as e:
+            # nsexec is already gone (BrokenPipeError): reap it and drop the scope made for it
+            await proc.wait()
+            try:
+                await asyncio.to_thread(self.systemd.stop, f"amdkube-{c.id}.scope")
+            except Exception as se:
+                log.debug("stopping scope of %s: %r", c.id, se)
+            raise RuntimeError(f"container {c.id}: launcher exited before joining its scope: {e}") from e
+        finally:
+            os.close(w)
         return proc
 
     async def _wait(self, c: Container):

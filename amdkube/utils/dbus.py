@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import os
 import socket
+import threading
 import struct
 
 METHOD_CALL, METHOD_RETURN, ERROR, SIGNAL = 1, 2, 3, 4
@@ -194,6 +195,9 @@ class Connection:
         self.serial = 0
         self.unique_name = ""
         self._buf = b""
+        # one caller at a time: a call sends, then reads until its own reply; two threads
+        # interleaving would each discard the other's reply (and share _buf)
+        self._lock = threading.RLock()
 
     def connect(self) -> "Connection":
         s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
@@ -240,19 +244,20 @@ class Connection:
 
     def call(self, destination: str | None, path: str, interface: str, member: str, sig: str = "", *args):
         """A method call; returns the reply's body values or raises DBusError."""
-        if self.sock is None:
-            raise DBusError("org.freedesktop.DBus.Error.Disconnected", "not connected")
-        self.serial += 1
-        serial = self.serial
-        fields = {F_PATH: path, F_INTERFACE: interface, F_MEMBER: member}
-        if destination:
-            fields[F_DESTINATION] = destination
-        self.sock.sendall(encode_message(METHOD_CALL, serial, fields, sig, args))
-        while True:
-            mtype, _flags, _s, f, body = self._read_message()
-            if f.get(F_REPLY_SERIAL) != serial:
-                continue                      # a signal, or a reply to someone else
-            if mtype == ERROR:
-                raise DBusError(f.get(F_ERROR_NAME, "org.freedesktop.DBus.Error.Failed"),
-                                body[0] if body and isinstance(body[0], str) else "")
-            return body
+        with self._lock:
+            if self.sock is None:
+                raise DBusError("org.freedesktop.DBus.Error.Disconnected", "not connected")
+            self.serial += 1
+            serial = self.serial
+            fields = {F_PATH: path, F_INTERFACE: interface, F_MEMBER: member}
+            if destination:
+                fields[F_DESTINATION] = destination
+            self.sock.sendall(encode_message(METHOD_CALL, serial, fields, sig, args))
+            while True:
+                mtype, _flags, _s, f, body = self._read_message()
+                if f.get(F_REPLY_SERIAL) != serial:
+                    continue                      # a signal
+                if mtype == ERROR:
+                    raise DBusError(f.get(F_ERROR_NAME, "org.freedesktop.DBus.Error.Failed"),
+                                    body[0] if body and isinstance(body[0], str) else "")
+                return body

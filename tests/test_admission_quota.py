@@ -499,3 +499,42 @@ async def test_concurrent_bridged_binds_and_service_allocations_never_collide():
                 await c.close()
             await srv.stop()
             s.close()
+
+
+def test_quota_controller_status_write_conflicts_with_a_reservation_made_after_its_read():
+    """The controller writes status with the resourceVersion it read (resource_quota_controller.go
+    :350-371): when the admission plugin reserved usage between that read and the write, the
+    write is a 409 and the reservation stays, instead of being overwritten by stale usage."""
+    import types
+    from amdkube.controllers.policy import ResourceQuotaController
+    from amdkube.localcluster import LocalCluster
+
+    async def go():
+        async with LocalCluster(gpus="none", with_kubelet=False, with_controllers=False) as lc:
+            c = lc.client
+            q = await c.create({"apiVersion": "v1", "kind": "ResourceQuota", "metadata": {"name": "rq"},
+                                "spec": {"hard": {"pods": "3"}}}, "default")
+            q["status"] = {"hard": {"pods": "3"}, "used": {"pods": "0"}}
+            stale = await c.update_status(q)
+            ctrl = ResourceQuotaController(types.SimpleNamespace(client=c))
+            ctrl.q_inf = types.SimpleNamespace(get=lambda key: m.deepcopy(stale), list=lambda: [stale])
+            # the controller's pod informer still lags with two pods it counts
+            cached = [{"apiVersion": "v1", "kind": "Pod", "metadata": {"name": f"old{i}", "namespace": "default"},
+                       "spec": {"containers": [{"name": "c", "image": "busybox"}]}, "status": {"phase": "Running"}}
+                      for i in range(2)]
+            ctrl.pod_inf = types.SimpleNamespace(list=lambda: cached)
+            ctrl.count_infs = {}
+            # a reservation lands after the controller's read
+            await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "new"},
+                            "spec": {"containers": [{"name": "c", "image": "busybox"}]}}, "default")
+            assert (await c.get("resourcequotas", "rq", "default"))["status"]["used"] == {"pods": "1"}
+            with pytest.raises(m.StatusError) as e:
+                await ctrl.sync("default/rq")
+            assert e.value.code == 409
+            assert (await c.get("resourcequotas", "rq", "default"))["status"]["used"] == {"pods": "1"}
+            # once the informer has the newer quota the retried sync writes
+            fresh = await c.get("resourcequotas", "rq", "default")
+            ctrl.q_inf = types.SimpleNamespace(get=lambda key: m.deepcopy(fresh), list=lambda: [fresh])
+            await ctrl.sync("default/rq")
+            assert (await c.get("resourcequotas", "rq", "default"))["status"]["used"] == {"pods": "2"}
+    run(go(), 60)

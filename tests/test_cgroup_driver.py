@@ -385,3 +385,117 @@ def test_rocshim_reports_its_cgroup_driver(tmp_path):
     run(go())
     with pytest.raises(CG.CgroupError):
         RocShim(str(tmp_path / "x.sock"), str(tmp_path / "st"), cgroup_driver="openrc")
+
+
+def test_concurrent_scope_starts_share_one_connection(tmp_path):
+    """Many containers starting at once (rocshim's asyncio.to_thread calls) share one systemd
+    connection: every call gets its own reply and every scope is created exactly once."""
+    from concurrent.futures import ThreadPoolExecutor
+    sd = FakeSystemd(str(tmp_path / "cg"))
+    units = CG.SystemdUnits(connect=lambda: D.Connection(sd.path, timeout=3).connect())
+    try:
+        names = [f"cri-containerd-{i:02d}.scope" for i in range(24)]
+        with ThreadPoolExecutor(max_workers=12) as ex:
+            jobs = list(ex.map(lambda n: units.start_transient(n, [("Slice", ("s", "kubepods.slice")),
+                                                                     ("PIDs", ("au", [os.getpid()]))]), names))
+        assert len(jobs) == len(names) and all(j.startswith("/org/freedesktop/systemd1/job/") for j in jobs)
+        assert sorted(sd.units) == sorted(names)
+        assert [m for m, _ in sd.calls].count("StartTransientUnit") == len(names)    # no resend after a lost reply
+    finally:
+        units.close()
+        sd.close()
+
+
+def test_systemd_cgroup_root_is_the_cgroup2_mount(tmp_path):
+    mi = tmp_path / "mountinfo"
+    mi.write_text("22 1 0:21 / /sys rw,nosuid - sysfs sysfs rw\n"
+                  "30 22 0:26 / /sys/fs/cgroup rw,nosuid,nodev - cgroup2 cgroup2 rw,nsdelegate\n"
+                  "40 1 0:40 / /mnt/cg\\040two rw - cgroup2 none rw\n")
+    assert CG.cgroup2_mount_of("/sys/fs/cgroup/amdkube/x", str(mi)) == "/sys/fs/cgroup"
+    assert CG.cgroup2_mount_of("/mnt/cg two/a", str(mi)) == "/mnt/cg two"
+    assert CG.cgroup2_mount_of("/sys/fs/cgroupx", str(mi)) is None
+    assert CG.systemd_cgroup_root("/sys/fs/cgroup", str(mi)) == "/sys/fs/cgroup"
+    assert CG.systemd_cgroup_root(CG.RUNTIME_DEFAULT_ROOT, str(mi)) == "/sys/fs/cgroup"     # rocshim's default, remapped
+    assert CG.systemd_cgroup_root(str(tmp_path), str(mi)) == str(tmp_path)                  # no cgroup2 fs: a test tree
+    with pytest.raises(CG.CgroupError, match="is not the cgroup2 mount /sys/fs/cgroup"):
+        CG.systemd_cgroup_root("/sys/fs/cgroup/kubelet", str(mi))
+
+
+def test_kubelet_enforces_the_pods_cgroup_off_its_event_loop():
+    """A slow pods-cgroup create (systemd answering late, its directory appearing late) runs in a
+    worker thread: the kubelet's loop keeps turning, a second status update does not start a
+    second create, and a failed create is retried on a later update."""
+    import time
+    from types import SimpleNamespace
+    from amdkube.kubelet.kubelet import Kubelet
+
+    class SlowManager:
+        def __init__(self):
+            self.creates, self.fail = 0, True
+
+        def path(self, internal):
+            return "/x" + internal
+
+        def create(self, internal, res):
+            self.creates += 1
+            time.sleep(0.3)
+            if self.fail:
+                self.fail = False
+                raise CG.CgroupError("systemd did not create the slice")
+
+    async def go():
+        k = Kubelet.__new__(Kubelet)
+        k.cfg = SimpleNamespace(cgroup_root="/cg", enforce_node_allocatable="pods", cgroup_driver="systemd")
+        k._pods_cgroup_enforced, k._cgroup_task, k._cgroup_manager = None, None, SlowManager()
+        alloc = {"cpu": "3", "memory": "1Gi"}
+        ticks = 0
+
+        async def ticker():
+            nonlocal ticks
+            while True:
+                ticks += 1
+                await asyncio.sleep(0.01)
+        t = asyncio.get_running_loop().create_task(ticker())
+        task = k._enforce_pods_cgroup(alloc)
+        assert task is not None and k._enforce_pods_cgroup(alloc) is None      # one at a time
+        await task
+        assert ticks >= 10 and k._pods_cgroup_enforced is None                  # the loop ran; the create failed
+        await k._enforce_pods_cgroup(alloc)                                     # retried on the next update
+        assert k._pods_cgroup_enforced == ("3", "1Gi") and k._cgroup_manager.creates == 2
+        assert k._enforce_pods_cgroup(alloc) is None                            # nothing changed: nothing to do
+        t.cancel()
+    run(go())
+
+
+def test_launcher_gone_before_its_scope_is_joined(tmp_path):
+    """nsexec exits before the kubelet's go-ahead: the write end of the wait pipe is closed, the
+    launcher reaped, the scope made for it stopped, and the start fails."""
+    from types import SimpleNamespace
+    from amdkube.runtime import RocShim
+
+    async def go():
+        base = tempfile.mkdtemp(prefix="rsd", dir="/tmp")
+        shim = RocShim(os.path.join(base, "s.sock"), os.path.join(base, "state"), hooks_dir=os.path.join(base, "hooks"),
+                       cgroup_driver="systemd", systemd_units=CG.SystemdUnits(lambda: None))
+        stopped, waited, fds = [], [], []
+
+        class Proc:
+            pid = 4242
+
+            async def wait(self):
+                waited.append(True)
+                return 1
+
+        async def launch(argv, **kw):
+            fds.append(int(argv[argv.index("--cgroup-wait-fd") + 1]))
+            return Proc()
+        shim._launch = launch
+        shim._place_in_scope = lambda c, pid: None
+        shim.systemd.stop = lambda unit: stopped.append(unit)
+        before = set(os.listdir("/proc/self/fd"))
+        c = SimpleNamespace(id="c1", env={}, cwd="/", log_path=os.path.join(base, "log"))
+        with pytest.raises(RuntimeError, match="launcher exited before joining its scope"):
+            await shim._launch_in_scope(c, ["nsexec", "--", "true"])
+        assert waited and stopped == ["amdkube-c1.scope"]
+        assert set(os.listdir("/proc/self/fd")) <= before          # neither pipe end leaks
+    run(go())

@@ -119,3 +119,50 @@ async def test_mutating_and_validating_webhooks(tmp_path):
             assert (await c.create(pod("d"), "default"))["metadata"]["labels"] == {}
     finally:
         await runner.cleanup()
+
+
+async def test_quota_charges_once_with_a_validating_webhook_and_never_on_dry_run():
+    """The validating-webhook preview and ?dryRun=All run quota admission as checks only: with a
+    hard pods=3 quota exactly three creates are admitted, and a dry run takes nothing."""
+    seen = []
+
+    async def allow(req):
+        r = (await req.json())["request"]
+        seen.append(r["name"])
+        return web.json_response({"response": {"uid": r["uid"], "allowed": True}})
+
+    app = web.Application()
+    app.router.add_post("/allow", allow)
+    runner = web.AppRunner(app, access_log=None)
+    await runner.setup()
+    site = web.TCPSite(runner, "127.0.0.1", 0)
+    await site.start()
+    port = site._server.sockets[0].getsockname()[1]
+    try:
+        async with LocalCluster(gpus="none", with_kubelet=False, with_controllers=False) as lc:
+            c = lc.client
+            await c.create({"apiVersion": "admissionregistration.k8s.io/v1beta1", "kind": "ValidatingWebhookConfiguration",
+                            "metadata": {"name": "allow-all"},
+                            "webhooks": [{"name": "allow.amd.com", "failurePolicy": "Fail",
+                                          "rules": [{"operations": ["CREATE"], "apiGroups": [""], "apiVersions": ["v1"],
+                                                     "resources": ["pods"]}],
+                                          "clientConfig": {"url": f"http://127.0.0.1:{port}/allow"}}]})
+            q = await c.create({"apiVersion": "v1", "kind": "ResourceQuota", "metadata": {"name": "q"},
+                                "spec": {"hard": {"pods": "3"}}}, "default")
+            q["status"] = {"hard": {"pods": "3"}, "used": {"pods": "0"}}
+            await c.update_status(q)
+            pod = lambda n: {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": n},   # noqa: E731
+                             "spec": {"containers": [{"name": "c", "image": "busybox"}]}}
+            await c.request("POST", "/api/v1/namespaces/default/pods", params={"dryRun": "All"}, body=pod("dry"))
+            assert (await c.get("resourcequotas", "q", "default"))["status"]["used"]["pods"] == "0"
+            admitted = []
+            for i in range(5):
+                try:
+                    await c.create(pod(f"p{i}"), "default")
+                    admitted.append(i)
+                except m.StatusError as e:
+                    assert e.code == 403 and "exceeded quota: q" in e.message
+            assert admitted == [0, 1, 2] and "p0" in seen
+            assert (await c.get("resourcequotas", "q", "default"))["status"]["used"]["pods"] == "3"
+    finally:
+        await runner.cleanup()
