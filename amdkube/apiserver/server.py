@@ -1243,10 +1243,26 @@ class APIServer:
                                 headers={k: v for k, v in r.headers.items() if k.lower() in ("content-type", "cache-control")})
 
     async def _pod_log(self, request, ns, name, q):
+        """pods/log (registry/core/pod/rest/log.go + strategy.go LogLocation): the options are
+        validated (ValidatePodLogOptions → 422), the container defaults to the pod's only one
+        (else BadRequest naming the choices), an unscheduled pod has no log yet (empty body), and
+        the node's kubelet answers /containerLogs with the options passed through."""
+        from ..kubelet import logs as L
+        try:
+            opts = L.decode_log_query(q)
+        except ValueError as e:
+            raise m.bad_request(f"invalid log options: {e}") from None
+        errs = L.validate_pod_log_options(opts)
+        if errs:
+            raise m.invalid("PodLogOptions", name, [str(e) for e in errs])
         pod = self.registry.rs("pods").get(ns, name)
+        try:
+            container = L.log_location_container(pod, name, opts.get("container"))
+        except ValueError as e:
+            raise m.bad_request(str(e)) from None
         node_name = (pod.get("spec") or {}).get("nodeName")
         if not node_name:
-            raise m.bad_request(f'pod "{name}" is not scheduled yet')
+            return web.Response(body=b"", content_type="text/plain")
         node = self.registry.rs("nodes").get("", node_name)
         st = node.get("status") or {}
         port = (((st.get("daemonEndpoints") or {}).get("kubeletEndpoint")) or {}).get("Port")
@@ -1254,14 +1270,23 @@ class APIServer:
             next((a["address"] for a in st.get("addresses") or [] if a.get("type") == "Hostname"), "127.0.0.1")
         if not port:
             raise m.bad_request(f"node {node_name} has no kubelet endpoint")
-        container = q.get("container") or ((pod.get("spec") or {}).get("containers") or [{}])[0].get("name", "")
-        params = {k: v for k, v in q.items() if k in ("tailLines", "follow", "previous", "sinceSeconds", "timestamps")}
+        params = {}
+        for k in ("follow", "previous", "timestamps"):
+            if opts.get(k):
+                params[k] = "true"
+        for k in ("sinceSeconds", "tailLines", "limitBytes"):
+            if opts.get(k) is not None:
+                params[k] = str(opts[k])
+        if opts.get("sinceTime"):
+            params["sinceTime"] = L.format_rfc3339nano(L.parse_rfc3339(opts["sinceTime"]) // 10**9 * 10**9)
         if self._http is None:
             self._http = ClientSession(timeout=ClientTimeout(total=None))
         url = f"{self.kubelet_scheme}://{addr}:{port}/containerLogs/{ns}/{name}/{container}"
         async with self._http.get(url, params=params, ssl=self.kubelet_ssl) as r:
             if r.status != 200:
-                raise m.StatusError(r.status, "BadRequest", (await r.text())[:500])
+                # GenericHttpResponseChecker: the kubelet's answer becomes the status message
+                reason = {400: "BadRequest", 404: "NotFound", 422: "Invalid", 403: "Forbidden"}.get(r.status, "InternalError")
+                raise m.StatusError(r.status, reason, (await r.text()).strip()[:1024])
             out = web.StreamResponse(status=200, headers={"Content-Type": "text/plain"})
             await out.prepare(request)
             async for chunk in r.content.iter_any():

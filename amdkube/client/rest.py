@@ -339,14 +339,52 @@ class Client:
         body = {"apiVersion": "policy/v1beta1", "kind": "Eviction", "metadata": {"name": name, "namespace": ns}}
         return await self.request("POST", self.path(ri, ns, name, "eviction"), body=body)
 
-    async def logs(self, ns: str, name: str, container: str | None = None, tail: int | None = None) -> str:
-        ri = self.resource_info("pods")
+    @staticmethod
+    def _log_params(container=None, tail=None, previous=False, since_seconds=None, since_time=None, timestamps=False,
+                    limit_bytes=None, follow=False) -> dict:
+        """PodLogOptions as query parameters."""
         params = {}
         if container:
             params["container"] = container
         if tail is not None:
             params["tailLines"] = str(tail)
+        if previous:
+            params["previous"] = "true"
+        if since_seconds is not None:
+            params["sinceSeconds"] = str(since_seconds)
+        if since_time:
+            params["sinceTime"] = since_time
+        if timestamps:
+            params["timestamps"] = "true"
+        if limit_bytes is not None:
+            params["limitBytes"] = str(limit_bytes)
+        if follow:
+            params["follow"] = "true"
+        return params
+
+    async def logs(self, ns: str, name: str, container: str | None = None, tail: int | None = None, **opts) -> str:
+        """GET pods/{name}/log; `opts`: previous, since_seconds, since_time, timestamps, limit_bytes."""
+        ri = self.resource_info("pods")
+        params = self._log_params(container, tail, **opts)
         return (await self.request("GET", self.path(ri, ns, name, "log"), params=params, raw=True)).decode(errors="replace")
+
+    async def stream_logs(self, ns: str, name: str, container: str | None = None, tail: int | None = None, **opts):
+        """Async iterator over the chunks of a (followed) pod log."""
+        ri = self.resource_info("pods")
+        params = self._log_params(container, tail, follow=opts.pop("follow", True), **opts)
+        async with self.session.get(self.server + self.path(ri, ns, name, "log"), params=params,
+                                    timeout=aiohttp.ClientTimeout(total=None, sock_read=None)) as r:
+            if r.status >= 400:
+                payload = await r.read()
+                try:
+                    st = json.loads(payload)
+                except ValueError:
+                    st = None
+                if isinstance(st, dict) and st.get("kind") == "Status":
+                    raise m.StatusError.from_status(st)
+                raise m.StatusError(r.status, "Unknown", payload.decode(errors="replace")[:500])
+            async for chunk in r.content.iter_any():
+                yield chunk
 
     async def watch(self, resource: str, ns: str = "", resource_version: str = "", label_selector=None,
                     field_selector=None, timeout_seconds: int | None = None):

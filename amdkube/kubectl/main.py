@@ -307,8 +307,8 @@ async def cmd_delete(c, a):
 
 
 async def cmd_logs(c, a):
-    name = a.args[0].split("/", 1)[-1]
-    print(await c.logs(a.namespace or "default", name, a.container, a.tail if a.tail >= 0 else None), end="")
+    from .logs import cmd_logs as logs
+    return await logs(c, a)
 
 
 async def kubelet_exec(c, ns: str, name: str, container: str | None, cmd: list[str]) -> tuple[bytes, int]:
@@ -494,6 +494,7 @@ COMMANDS = {"get": cmd_get, "describe": cmd_describe, "create": cmd_create, "app
             "wait": cmd_wait, "attach": cmd_attach}
 from .extra import COMMANDS as _EXTRA, add_arguments as _extra_args  # noqa: E402
 from . import more as _more  # noqa: E402
+from . import logs as _logs  # noqa: E402
 COMMANDS.update(_EXTRA)
 COMMANDS.update(_more.COMMANDS)
 COMMANDS["apply"] = _more.cmd_apply       # three-way merge, --prune, *-last-applied
@@ -521,6 +522,7 @@ def parser():
                             formatter_class=argparse.RawDescriptionHelpFormatter)
         _extra_args(sp)
         _more.add_arguments(sp)
+        _logs.add_arguments(sp)
         sp.add_argument("args", nargs="*")
         sp.add_argument("-n", "--namespace", default=argparse.SUPPRESS)
         sp.add_argument("-o", "--output", default=None)
@@ -606,6 +608,7 @@ def main(argv=None):
     if "--" in argv:
         i = argv.index("--")
         argv, cmd_tail = argv[:i], argv[i + 1:]
+    argv = _logs.rewrite_short_flags(argv)
     p = parser()
     a, extra = p.parse_known_args(argv)
     if any(x.startswith("-") for x in extra):

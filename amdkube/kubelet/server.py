@@ -206,38 +206,46 @@ class KubeletServer:
         return await bridge(ws, url + "?" + "&".join(f"port={p}" for p in ports), [ws.ws_protocol or PORTFORWARD_PROTOCOLS[0]])
 
     async def logs(self, req):
+        """getContainerLogs (server.go:452-538) + GetKubeletContainerLogs (kubelet_pods.go:1216):
+        query → PodLogOptions (422 when invalid), the pod and container must exist (404), the
+        instance is chosen from the pod's status (validateContainerLogStatus; `previous` is the
+        last terminated one), then ReadLogs streams the CRI log file."""
+        from . import logs as L
         ns, pod, cname = req.match_info["ns"], req.match_info["pod"], req.match_info["container"]
-        cs = await self._find_container(ns, pod, cname)
-        if cs is None:
-            return web.Response(status=404, text=f"container {cname} of pod {ns}/{pod} not found")
-        _, info = await self.k.cri.container_status(cs.id, verbose=True)
-        path = cs.log_path
-        if not path or not os.path.exists(path):
-            return web.Response(text="")
-        tail = req.query.get("tailLines")
-        follow = req.query.get("follow") in ("true", "1")
-        with open(path, "rb") as f:
-            data = f.read()
-        if tail:
-            lines = data.splitlines(keepends=True)
-            data = b"".join(lines[-int(tail):])
-        if not follow:
-            return web.Response(body=data, content_type="text/plain")
-        resp = web.StreamResponse()
+        try:
+            opts = L.decode_log_query(req.query)
+        except ValueError:
+            return web.Response(status=400, text='{"message": "Unable to decode query."}')
+        if L.validate_pod_log_options(opts):
+            return web.Response(status=422, text='{"message": "Invalid request."}')
+        found = next(((uid, p) for uid, p in self.k.pods.items() if m.namespace_of(p) == ns and m.name_of(p) == pod), None)
+        if found is None:
+            return web.Response(status=404, text=f'pod "{pod}" does not exist\n')
+        uid, p = found
+        spec = p.get("spec") or {}
+        if not any(c.get("name") == cname for c in (spec.get("containers") or []) + (spec.get("initContainers") or [])):
+            return web.Response(status=404, text=f'container "{cname}" not found in pod "{pod}"\n')
+        status = self.k.status.get(uid) or p.get("status") or {}
+        try:
+            cid = L.validate_container_log_status(pod, status, cname, bool(opts.get("previous")))
+            st, _ = await self.k.cri.container_status(cid)
+        except ValueError as e:
+            return web.Response(status=400, text=str(e))
+        except Exception as e:
+            return web.Response(status=400, text=f'failed to get container status "{cid}": {e}')
+        path = st.log_path
+        resp = web.StreamResponse(headers={"Content-Type": "text/plain"})
+        resp.enable_chunked_encoding()
         await resp.prepare(req)
-        await resp.write(data)
-        off = os.path.getsize(path)
-        for _ in range(3600):
-            await asyncio.sleep(0.5)
-            st, _ = await self.k.cri.container_status(cs.id)
-            with open(path, "rb") as f:
-                f.seek(off)
-                chunk = f.read()
-            if chunk:
-                await resp.write(chunk)
-                off += len(chunk)
-            if st.state != C.CONTAINER_RUNNING:
-                break
+        if path and os.path.exists(path):
+            async def running():
+                try:
+                    s, _ = await self.k.cri.container_status(cid)
+                except Exception:
+                    return False
+                return s.state == C.CONTAINER_RUNNING
+            await L.read_logs(path, L.LogOptions.from_api(opts), resp.write, is_running=running,
+                              state_check_period=float(getattr(self.k.cfg, "log_state_check_period", L.STATE_CHECK_PERIOD)))
         await resp.write_eof()
         return resp
 

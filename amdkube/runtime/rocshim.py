@@ -137,11 +137,12 @@ class PidProc:
     """A child process watched through a pidfd on the event loop (Linux ≥ 5.3): no transport,
     pipes or per-child waiter thread, which asyncio.create_subprocess_exec costs per spawn
     (ThreadedChildWatcher). `wait()` returns the returncode as subprocess does (−signal)."""
-    __slots__ = ("pid", "returncode", "_popen", "_fd", "_fut")
+    __slots__ = ("pid", "returncode", "_popen", "_fd", "_fut", "pump")
 
     def __init__(self, popen: subprocess.Popen, fd: int):
         loop = asyncio.get_running_loop()
         self.pid, self.returncode, self._popen, self._fd = popen.pid, None, popen, fd
+        self.pump = None
         self._fut = loop.create_future()
         loop.add_reader(fd, self._exited)
 
@@ -155,40 +156,95 @@ class PidProc:
     async def wait(self):
         return await asyncio.shield(self._fut)
 
+    async def logs_flushed(self, timeout: float = 2.0):
+        """Wait (bounded) for the log pump to write the container's last output: it exits once
+        every writer of the pipes is gone, which a daemon the container left behind can delay."""
+        pump = self.pump
+        if pump is None:
+            return
+        try:
+            await asyncio.wait_for(asyncio.to_thread(pump.wait), timeout)
+        except asyncio.TimeoutError:
+            asyncio.get_running_loop().run_in_executor(None, pump.wait)     # reap it whenever it ends
+        self.pump = None
 
-def _popen(argv, stdout, stderr, env, cwd, log_path, oom_score_adj=None, pass_fds=()):
+
+LOGPUMP_BIN = os.path.join(NATIVE_BIN, "amdkube-logpump")
+
+
+def logpump_bin() -> str | None:
+    """native/logpump.cpp, the CRI-format log writer; None when it was not built (the
+    container's output then goes to its log file untagged — refused when AMDKUBE_REQUIRE_NATIVE
+    is set, as on the GPU box)."""
+    if os.access(LOGPUMP_BIN, os.X_OK):
+        return LOGPUMP_BIN
+    if os.environ.get("AMDKUBE_REQUIRE_NATIVE"):
+        raise RuntimeError(f"{LOGPUMP_BIN} is not built (python native/build.py)")
+    return None
+
+
+def _popen(argv, stdout, stderr, env, cwd, log_path, oom_score_adj=None, pass_fds=(), pump=None):
     """fork/exec (and the log file's open, and the child's oom_score_adj) off the event loop: a
     spawn is ~1 ms of syscalls that would otherwise stall every other CRI call the runtime is
-    serving."""
-    logf = open(log_path, "ab", buffering=0) if log_path else None
-    try:
+    serving. With a log path and `pump` (the logpump binary) the container's stdout and stderr
+    are pipes whose read ends the pump owns: it writes the CRI log format (timestamp, stream,
+    partial/full tag per line) and outlives this runtime process; without one they are the log
+    file itself."""
+    logf = pump_proc = None
+    out_w = err_w = None
+    if log_path and pump:
+        out_r, out_w = os.pipe()
+        err_r, err_w = os.pipe()
+        try:
+            pump_proc = subprocess.Popen([pump, "--log", log_path, "--stdout-fd", str(out_r), "--stderr-fd", str(err_r)],
+                                         stdin=subprocess.DEVNULL, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                                         pass_fds=(out_r, err_r), start_new_session=True)
+        except BaseException:
+            for fd in (out_w, err_w):
+                os.close(fd)
+            raise
+        finally:
+            os.close(out_r)
+            os.close(err_r)
+        out, err = out_w, err_w
+    else:
+        logf = open(log_path, "ab", buffering=0) if log_path else None
         out = logf if logf is not None else (stdout if stdout is not None else subprocess.DEVNULL)
         err = logf if logf is not None else (stderr if stderr is not None else subprocess.DEVNULL)
+    try:
         p = subprocess.Popen(argv, stdin=subprocess.DEVNULL, stdout=out, stderr=err, env=env, cwd=cwd,
                              start_new_session=True, pass_fds=pass_fds)
     finally:
         if logf is not None:
             logf.close()
+        for fd in (out_w, err_w):
+            if fd is not None:
+                os.close(fd)     # the pump sees EOF once the container's copies are gone too
     try:
         fd = os.pidfd_open(p.pid)
     except (AttributeError, OSError):
         fd = None
     if oom_score_adj:
         _set_oom_score_adj(p.pid, oom_score_adj)
-    return p, fd
+    return p, fd, pump_proc
 
 
-async def spawn(argv, stdout=None, stderr=None, env=None, cwd=None, log_path=None, oom_score_adj=None, pass_fds=()):
+async def spawn(argv, stdout=None, stderr=None, env=None, cwd=None, log_path=None, oom_score_adj=None, pass_fds=(),
+                log_pump=False):
     """Start argv in its own session with stdin from /dev/null (stdout and stderr appended to
-    `log_path` when given); pidfd-watched when possible."""
-    p, fd = await asyncio.to_thread(_popen, argv, stdout, stderr, env, cwd, log_path, oom_score_adj, pass_fds)
+    `log_path` when given — through the log pump with `log_pump`); pidfd-watched when
+    possible."""
+    pump = logpump_bin() if log_pump and log_path else None
+    p, fd, pump_proc = await asyncio.to_thread(_popen, argv, stdout, stderr, env, cwd, log_path, oom_score_adj, pass_fds, pump)
     if fd is None:   # old kernel: a thread waits for the child
         loop = asyncio.get_running_loop()
         proc = PidProc.__new__(PidProc)
         proc.pid, proc.returncode, proc._popen, proc._fd = p.pid, None, p, -1
         proc._fut = loop.run_in_executor(None, p.wait)
-        return proc
-    return PidProc(p, fd)
+    else:
+        proc = PidProc(p, fd)
+    proc.pump = pump_proc
+    return proc
 
 class Sandbox:
     def __init__(self, sid, config_bytes, meta, labels, annotations, log_dir):
@@ -985,14 +1041,9 @@ class RocShim:
                 pass
         if not msg and c.exit_code and c.annotations.get("io.kubernetes.container.terminationMessagePolicy") == \
                 "FallbackToLogsOnError":
-            try:
-                with open(c.log_path, "rb") as f:
-                    f.seek(0, os.SEEK_END)
-                    f.seek(max(0, f.tell() - 16384))
-                    lines = f.read().decode(errors="replace").splitlines()[-80:]
-                msg = "\n".join(lines)[-2048:]
-            except OSError:
-                pass
+            # readLastStringFromContainerLogs: the last 80 lines, at most 2 KiB, decoded
+            from ..kubelet.logs import read_text
+            msg = read_text(c.log_path, tail=80, keep_last=2048)
         return msg
 
     def _oom_killed(self, c: Container) -> bool:
@@ -1022,7 +1073,7 @@ class RocShim:
             if self.cgroup_driver == "systemd" and "--cgroup" in argv:
                 proc = await self._launch_in_scope(c, argv)
             else:
-                proc = await self._launch(argv, env=c.env, cwd=c.cwd, log_path=c.log_path,
+                proc = await self._launch(argv, env=c.env, cwd=c.cwd, log_path=c.log_path, log_pump=True,
                                           oom_score_adj=c.resources.get("oom_score_adj") if self.isolation != "namespaces" else None)
         except (OSError, ValueError, RuntimeError) as e:
             c.state, c.exit_code, c.reason, c.message = C.CONTAINER_EXITED, 128, "StartError", str(e)
@@ -1048,7 +1099,7 @@ class RocShim:
         r, w = os.pipe()
         try:
             argv = argv[:1] + ["--cgroup-wait-fd", str(r)] + argv[1:]
-            proc = await self._launch(argv, env=c.env, cwd=c.cwd, log_path=c.log_path, pass_fds=(r,))
+            proc = await self._launch(argv, env=c.env, cwd=c.cwd, log_path=c.log_path, log_pump=True, pass_fds=(r,))
         except BaseException:
             os.close(w)
             raise
@@ -1076,6 +1127,7 @@ class RocShim:
 
     async def _wait(self, c: Container):
         rc = await c.proc.wait()
+        await c.proc.logs_flushed(0.5)       # the termination-message fallback reads the log's tail
         # written by the checkpoint thread, ordered before the container's checkpoint and any
         # later removal of the same file
         self.ckpt.put(os.path.join(self.state_dir, "containers", c.id + ".exit"), str(rc).encode())

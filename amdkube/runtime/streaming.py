@@ -264,12 +264,15 @@ class StreamingServer:
         if req["stdin"]:
             await ch.finish(None, "containers run with stdin closed; attach is output-only")
             return resp
-        # stream what the container writes from now on (its stdout/stderr share the log file)
+        # stream what the container writes from now on: its log file's records (the CRI log
+        # format the log pump writes), each to its own stream
+        from ..kubelet import logs as L
         try:
             off = os.path.getsize(c.log_path)
         except OSError:
             off = 0
         from ..grpcdesc.cri import CRI as C
+        pending, parse = b"", None
         while not ch.closed():
             try:
                 with open(c.log_path, "rb") as f:
@@ -279,8 +282,19 @@ class StreamingServer:
                 data = b""
             if data:
                 off += len(data)
-                await ch.send(STDOUT, data)
+                pending += data
+                cut = pending.rfind(b"\n") + 1
+                lines, pending = pending[:cut].splitlines(keepends=True), pending[cut:]
+                for ln in lines:
+                    parse = parse or L.get_parse_func(ln, allow_raw=True)
+                    try:
+                        msg = parse(ln)
+                    except ValueError:
+                        continue
+                    await ch.send(STDERR if msg.stream == L.STDERR else STDOUT, msg.log)
             if c.state == C.CONTAINER_EXITED and not data:
+                if pending:
+                    await ch.send(STDOUT, pending)
                 await ch.finish(c.exit_code)
                 break
             await asyncio.sleep(0.05)

@@ -6,7 +6,8 @@
                                     # and the ThreadSanitizer build of the activity sampler
 
 Outputs: amdkube/_native/{_amdsmi,_topo,_kproto,_quantile,_hipops}.<ext> and amdkube/_native/bin/{pause,
-rocm-vector-add,hsa-vector-add,hbm-probe,gpu-burn,xgmi-probe[,topo-selftest-asan,pause-asan,amdkube-nsexec-asan,
+amdkube-nsexec,amdkube-logpump,rocm-vector-add,hsa-vector-add,hbm-probe,gpu-burn,xgmi-probe[,topo-selftest-asan,pause-asan,
+amdkube-nsexec-asan,amdkube-logpump-asan,
 seccomp-check-asan,sampler-selftest-{asan,tsan}]}.
 Targets are rebuilt only when a source/header is newer than the output.
 """
@@ -68,6 +69,8 @@ def targets(sanitize=False, cpu_only=False):
          ["g++", "-O2", "-std=c++17", n("native/nsexec.cpp"), "-o", "{out}"]),
         (n(BIN, "seccomp-check"), [n("native/seccomp_check.cpp"), n("native/seccomp_bpf.h"), SYSCALL_TABLE],
          ["g++", "-O2", "-std=c++17", n("native/seccomp_check.cpp"), "-o", "{out}"]),
+        (n(BIN, "amdkube-logpump"), [n("native/logpump.cpp")],
+         ["g++", "-O2", "-std=c++17", "-Wall", n("native/logpump.cpp"), "-o", "{out}"]),
         (n(BIN, "cni", "amdkube-cni"), [n("native/cni_ipam.cpp")],
          ["g++", "-O2", "-std=c++17", n("native/cni_ipam.cpp"), "-o", "{out}"]),
         (n(BIN, "cni", "amdkube-bridge"), [n("native/cni_bridge.cpp")],
@@ -89,6 +92,8 @@ def targets(sanitize=False, cpu_only=False):
             (n(BIN, "amdkube-nsexec-asan"), [n("native/nsexec.cpp"), n("native/seccomp_bpf.h"), n("native/devguard.h"),
                                              SYSCALL_TABLE],
              ["g++", "-O1", "-std=c++17", *san, n("native/nsexec.cpp"), "-o", "{out}"]),
+            (n(BIN, "amdkube-logpump-asan"), [n("native/logpump.cpp")],
+             ["g++", "-O1", "-std=c++17", *san, n("native/logpump.cpp"), "-o", "{out}"]),
             (n(BIN, "seccomp-check-asan"), [n("native/seccomp_check.cpp"), n("native/seccomp_bpf.h"), SYSCALL_TABLE],
              ["g++", "-O1", "-std=c++17", *san, n("native/seccomp_check.cpp"), "-o", "{out}"]),
             (n(BIN, "sampler-selftest-tsan"), [n("native/sampler_selftest.cpp"), n("native/sampler_core.h")],

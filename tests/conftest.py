@@ -55,6 +55,12 @@ def run(coro, timeout=60):
     return asyncio.run(asyncio.wait_for(coro, timeout))
 
 
+def log_text(path: str) -> str:
+    """A container's output from its log file (the CRI records the log pump writes, decoded)."""
+    from amdkube.kubelet.logs import read_text
+    return read_text(path)
+
+
 @pytest.fixture
 def arun():
     return run

@@ -22,7 +22,7 @@ import pytest
 
 from amdkube.kubelet import cgroups as CG
 from amdkube.utils import dbus as D
-from tests.conftest import run
+from tests.conftest import run, log_text
 
 
 # ------------------------------------------------------------------ names (reference tables)
@@ -311,10 +311,10 @@ def test_rocshim_places_containers_in_systemd_scopes(tmp_path):
             cid = await shim.create_container(sid, _ctr("c", ["sh", "-c", "echo in-scope"], mem=64 << 20), sc)
             await shim.start_container(cid)
             c = await _wait_exit(shim, cid)
-            if c.exit_code == 126 and "unshare" in open(c.log_path).read():
+            if c.exit_code == 126 and "unshare" in log_text(c.log_path):
                 pytest.skip("unshare not permitted in this container")
-            assert c.exit_code == 0, open(c.log_path).read()
-            assert open(c.log_path).read().strip() == "in-scope"
+            assert c.exit_code == 0, log_text(c.log_path)
+            assert log_text(c.log_path).strip() == "in-scope"
             starts = [b for m, b in sd.calls if m == "StartTransientUnit"]
             assert [s[0] for s in starts] == ["kubepods-burstable-podaa_bb.slice", f"amdkube-{cid}.scope"]
             props = dict(starts[1][2])
@@ -334,7 +334,7 @@ def test_rocshim_places_containers_in_systemd_scopes(tmp_path):
             cid = await shim.create_container(sid, _ctr("d", ["sh", "-c", "echo must-not-run"]), sc)
             with pytest.raises(RuntimeError, match="Permission denied"):
                 await shim.start_container(cid)
-            assert "must-not-run" not in open(shim.containers[cid].log_path).read()
+            assert "must-not-run" not in log_text(shim.containers[cid].log_path)
             # a non-slice parent is refused under the systemd driver
             with pytest.raises(CG.CgroupError):
                 shim._cgroup_parent("kubepods/burstable/podx")

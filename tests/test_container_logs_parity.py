@@ -1,0 +1,357 @@
+"""Container logs at reference parity: the CRI log format end to end.
+
+Transcribed tables:
+  * pkg/kubelet/kuberuntime/logs/logs_test.go — TestLogOptions, TestParseLog, TestWriteLogs,
+    TestWriteLogsWithBytesLimit;
+  * pkg/util/tail/tail_test.go — TestTail;
+  * pkg/kubelet/kubelet_test.go — TestValidateContainerLogStatus;
+  * pkg/registry/core/pod/strategy_test.go — TestCheckLogLocation;
+  * pkg/kubectl/cmd/util/factory_test.go — TestGetFirstPod's ByLogging cases.
+Plus the native log pump (native/logpump.cpp) round trip, and kubectl logs through a live
+cluster: --previous after a restart, --timestamps, --tail, --limit-bytes, --since,
+-f until the container exits, TYPE/NAME, and the multi-container BadRequest.
+"""
+from __future__ import annotations
+
+import asyncio
+import io
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+from amdkube.kubelet import logs as L
+from tests.conftest import run
+
+TS = "2016-10-20T18:39:20.57606443Z"
+
+
+# ------------------------------------------------------------------ logs_test.go
+def test_log_options():
+    now = L.parse_rfc3339("2017-11-01T10:00:00.123456789Z")
+    cases = [({}, L.LogOptions(tail=-1, bytes=-1)),
+             ({"tailLines": 8}, L.LogOptions(tail=8, bytes=-1)),
+             ({"limitBytes": 64}, L.LogOptions(tail=-1, bytes=64)),
+             ({"sinceTime": now}, L.LogOptions(tail=-1, bytes=-1, since=now)),
+             ({"sinceSeconds": 10}, L.LogOptions(tail=-1, bytes=-1, since=now - 10 * 10**9))]
+    for api, want in cases:
+        assert L.LogOptions.from_api(api, now) == want, api
+
+
+@pytest.mark.parametrize("line,msg,err", [
+    ('{"log":"docker stdout test log","stream":"stdout","time":"2016-10-20T18:39:20.57606443Z"}\n',
+     ("stdout", b"docker stdout test log"), False),
+    ('{"log":"docker stderr test log","stream":"stderr","time":"2016-10-20T18:39:20.57606443Z"}\n',
+     ("stderr", b"docker stderr test log"), False),
+    (f"{TS} stdout F cri stdout test log\n", ("stdout", b"cri stdout test log\n"), False),
+    (f"{TS} stderr F cri stderr test log\n", ("stderr", b"cri stderr test log\n"), False),
+    ("unsupported log format test log\n", None, True),
+    (f"{TS} stdout P cri stdout partial test log\n", ("stdout", b"cri stdout partial test log"), False),
+    (f"{TS} stdout P:TAG1:TAG2 cri stdout partial test log\n", ("stdout", b"cri stdout partial test log"), False),
+])
+def test_parse_log(line, msg, err):
+    line = line.encode()
+    if err:
+        with pytest.raises(ValueError, match="unsupported log format"):
+            L.get_parse_func(line)
+        return
+    parse = L.get_parse_func(line)
+    assert parse(line) == L.LogMessage(L.parse_rfc3339(TS), *msg)
+
+
+T1234 = 1234 * 10**9 + 4321      # time.Unix(1234, 4321)
+LOG = b"abcdefg\n"
+
+
+@pytest.mark.parametrize("stream,since,timestamp,out,err", [
+    ("stderr", None, False, b"", LOG),
+    ("stdout", None, False, LOG, b""),
+    ("stdout", T1234 + 10**9, False, b"", b""),                       # since is after the timestamp
+    ("stderr", None, True, b"", L.format_rfc3339nano(T1234).encode() + b" " + LOG),
+])
+def test_write_logs(stream, since, timestamp, out, err):
+    o, e = io.BytesIO(), io.BytesIO()
+    w = L.LogWriter(o.write, e.write, L.LogOptions(since=since, timestamp=timestamp, bytes=-1))
+    w.write(L.LogMessage(T1234, stream, LOG))
+    assert (o.getvalue(), e.getvalue()) == (out, err)
+
+
+def test_write_logs_with_bytes_limit():
+    ts = L.format_rfc3339nano(T1234).encode()
+    assert ts == b"1970-01-01T00:20:34.000004321Z"
+    cases = [(3, 0, 3, False, b"abc", b""),
+             (3, 0, len(LOG) + 3, False, b"abcdefg\nabc", b""),
+             (3, 0, 3 * len(LOG), False, LOG * 3, b""),
+             (0, 3, len(LOG) + 3, False, b"", b"abcdefg\nabc"),
+             (1, 2, len(LOG) + 3, False, LOG, b"abc"),
+             (3, 0, len(ts) + 1 + len(LOG) + 2, True, ts + b" " + LOG + ts[:2], b"")]
+    for n_out, n_err, limit, timestamp, want_out, want_err in cases:
+        o, e = io.BytesIO(), io.BytesIO()
+        w = L.LogWriter(o.write, e.write, L.LogOptions(timestamp=timestamp, bytes=limit))
+        for stream, n in (("stdout", n_out), ("stderr", n_err)):
+            for _ in range(n):
+                try:
+                    w.write(L.LogMessage(T1234, stream, LOG))
+                except L.MaximumWrite:
+                    pass
+        assert (o.getvalue(), e.getvalue()) == (want_out, want_err), (n_out, n_err, limit)
+
+
+def test_rfc3339nano_round_trip():
+    for s in ("2016-10-20T18:39:20.57606443Z", "2016-10-20T18:39:20Z", "2016-10-20T18:39:20.1Z"):
+        assert L.format_rfc3339nano(L.parse_rfc3339(s)) == s
+    assert L.parse_rfc3339("2016-10-20T20:39:20+02:00") == L.parse_rfc3339("2016-10-20T18:39:20Z")
+    assert L.format_rfc3339nano(L.ZERO_TIME_NS) == "0001-01-01T00:00:00Z"
+
+
+# ------------------------------------------------------------------ tail_test.go
+def test_tail():
+    line = b"a" * L.BLOCK_SIZE
+    data = (line + b"\n") * 4 + line[L.BLOCK_SIZE // 2:]          # an incomplete last line
+    for n, start in ((-1, 0), (0, (len(line) + 1) * 4), (1, (len(line) + 1) * 3), (9999, 0)):
+        assert L.find_tail_line_start_index(io.BytesIO(data), n) == start, n
+
+
+# -------------------------------------------------------- kubelet_test.go / validation
+@pytest.mark.parametrize("status,ok,prev_ok", [
+    ({"state": {"running": {}}, "lastState": {"terminated": {}}}, True, True),
+    ({"state": {"running": {}}}, True, False),
+    ({"state": {"terminated": {}}}, True, False),
+    ({"state": {"waiting": {}}}, False, False),
+    ({"state": {"waiting": {"reason": "ErrImagePull"}}}, False, False),
+    ({"state": {"waiting": {"reason": "ErrImagePullBackOff"}}}, False, False),
+])
+def test_validate_container_log_status(status, ok, prev_ok):
+    ps = {"containerStatuses": [dict(status, name="x")]}
+    for previous, expect in ((False, ok), (True, prev_ok)):
+        if expect:
+            L.validate_container_log_status("podName", ps, "x", previous)
+        else:
+            with pytest.raises(ValueError):
+                L.validate_container_log_status("podName", ps, "x", previous)
+    with pytest.raises(ValueError, match='container "blah" in pod "podName" is not available'):
+        L.validate_container_log_status("podName", ps, "blah", False)
+
+
+def test_validate_container_log_status_picks_the_instance():
+    ps = {"containerStatuses": [{"name": "x", "containerID": "rocshim://new", "state": {"running": {}},
+                                 "lastState": {"terminated": {"containerID": "rocshim://old"}}}]}
+    assert L.validate_container_log_status("p", ps, "x", False) == "new"
+    assert L.validate_container_log_status("p", ps, "x", True) == "old"
+    with pytest.raises(ValueError, match="is waiting to start: image can't be pulled"):
+        L.validate_container_log_status("p", {"containerStatuses": [{"name": "x", "state": {"waiting": {"reason": "ErrImagePull"}}}]},
+                                        "x", False)
+
+
+def _pod(conts, inits=()):
+    return {"spec": {"containers": [{"name": n} for n in conts], "initContainers": [{"name": n} for n in inits]}}
+
+
+@pytest.mark.parametrize("pod,container,err", [
+    (_pod([]), None, "a container name must be specified for pod test"),
+    (_pod(["mycontainer"]), None, None),
+    (_pod(["container1", "container2"]), None, "a container name must be specified for pod test, choose one of: [container1 container2]"),
+    (_pod(["container1", "container2"], ["initcontainer1"]), None,
+     "a container name must be specified for pod test, choose one of: [container1 container2] or one of the init containers: [initcontainer1]"),
+    (_pod(["container1", "container2"]), "unknown", "container unknown is not valid for pod test"),
+    (_pod(["container1", "container2"]), "container2", None),
+])
+def test_check_log_location(pod, container, err):
+    if err is None:
+        L.log_location_container(pod, "test", container)
+    else:
+        with pytest.raises(ValueError) as e:
+            L.log_location_container(pod, "test", container)
+        assert str(e.value) == err
+
+
+def test_validate_pod_log_options():
+    assert L.validate_pod_log_options({"tailLines": 0, "limitBytes": 1, "sinceSeconds": 1}) == []
+    msgs = [str(e) for e in L.validate_pod_log_options({"tailLines": -1, "limitBytes": 0, "sinceSeconds": 0})]
+    assert msgs == ["tailLines: Invalid value: -1: must be greater than or equal to 0",
+                    "limitBytes: Invalid value: 0: must be greater than 0",
+                    "sinceSeconds: Invalid value: 0: must be greater than 0"]
+    assert [str(e) for e in L.validate_pod_log_options({"sinceSeconds": 5, "sinceTime": TS})] == \
+        [": Forbidden: at most one of `sinceTime` or `sinceSeconds` may be specified"]
+
+
+# ------------------------------------------------------------ factory_test.go ByLogging
+def _pods(count, unready=-1, unhealthy=-1):
+    out = []
+    for i in range(count):
+        p = {"metadata": {"name": f"pod-{i + 1}", "creationTimestamp": f"2016-04-01T01:00:0{i}Z"},
+             "status": {"conditions": [{"type": "Ready", "status": "True"}]}}
+        out.append(p)
+    if 0 <= unready < count:
+        out[unready]["status"]["conditions"][0]["status"] = "False"
+    if 0 <= unhealthy < count:
+        out[unhealthy]["status"]["containerStatuses"] = [{"restartCount": 5}]
+    return out
+
+
+def test_get_first_pod_by_logging():
+    from amdkube.kubectl.logs import sort_by_logging
+    assert sort_by_logging(_pods(2))[0]["metadata"]["name"] == "pod-1"
+    assert sort_by_logging(_pods(2, unhealthy=1))[0]["metadata"]["name"] == "pod-2"
+    assert sort_by_logging(_pods(3, unready=0))[0]["metadata"]["name"] == "pod-2"
+    scheduled = _pods(2)
+    scheduled[1]["spec"] = {"nodeName": "n0"}
+    assert sort_by_logging(scheduled)[0]["metadata"]["name"] == "pod-2"
+
+
+def test_kubectl_logs_short_flags():
+    from amdkube.kubectl.logs import rewrite_short_flags
+    assert rewrite_short_flags(["-n", "ns", "logs", "-f", "p", "-p"]) == ["-n", "ns", "logs", "--follow", "p", "--previous"]
+    assert rewrite_short_flags(["log", "-fp", "x"]) == ["logs", "--follow", "--previous", "x"]
+    assert rewrite_short_flags(["get", "-f", "x.yaml"]) == ["get", "-f", "x.yaml"]
+
+
+# ------------------------------------------------------------------- the log pump
+def test_logpump_round_trip(tmp_path):
+    from amdkube.runtime.rocshim import logpump_bin
+    pump = logpump_bin()
+    assert pump, "native/logpump.cpp is not built"
+    log = tmp_path / "0.log"
+    script = ("import sys,time\n"
+              "sys.stdout.write('one\\n'); sys.stdout.flush()\n"
+              "sys.stderr.write('oops\\n'); sys.stderr.flush()\n"
+              "sys.stdout.write('x' * 40000 + '\\n'); sys.stdout.flush()\n"
+              "sys.stdout.write('no newline at the end')\n")
+    ro, wo = os.pipe()
+    re_, we = os.pipe()
+    p = subprocess.Popen([pump, "--log", str(log), "--stdout-fd", str(ro), "--stderr-fd", str(re_)], pass_fds=(ro, re_),
+                         start_new_session=True)
+    os.close(ro)
+    os.close(re_)
+    w = subprocess.Popen([sys.executable, "-c", script], stdout=wo, stderr=we)
+    os.close(wo)
+    os.close(we)
+    assert w.wait(30) == 0 and p.wait(30) == 0
+    recs = log.read_bytes().splitlines(keepends=True)
+    assert all(L.get_parse_func(r) is L.parse_cri_log for r in recs)
+    tags = [r.split(b" ", 3)[1:3] for r in recs]
+    assert tags[0] == [b"stdout", b"F"] and [b"stderr", b"F"] in tags
+    assert tags.count([b"stdout", b"P"]) == 3          # 40000 bytes: two 16 KiB partials, then the unterminated tail
+    out, err = [], []
+    L.read_logs_sync(str(log), L.LogOptions(), out.append, err.append)
+    assert b"".join(out) == b"one\n" + b"x" * 40000 + b"\nno newline at the end"
+    assert b"".join(err) == b"oops\n"
+    # --tail counts file records; --limit-bytes cuts the output
+    assert L.read_text(str(log), tail=1) == "no newline at the end"
+    assert L.read_text(str(log), limit=4) == "one\n"
+    assert L.read_text(str(log), keep_last=9) == "at the end"[-9:]
+
+
+def test_raw_log_files_still_read(tmp_path):
+    p = tmp_path / "raw.log"
+    p.write_bytes(b"plain line\nsecond\n")
+    assert L.read_text(str(p)) == "plain line\nsecond\n"
+    assert L.read_text(str(p), tail=1) == "second\n"
+
+
+# ---------------------------------------------------------------- end to end (kubectl)
+async def _kubectl(c, *args):
+    import contextlib
+    from amdkube.kubectl import main as km
+    buf, err = io.StringIO(), io.StringIO()
+
+    class Out(io.StringIO):
+        @property
+        def buffer(self):
+            return self
+
+        def write(self, b):
+            return buf.write(b.decode() if isinstance(b, bytes) else b)
+
+    a, extra = km.parser().parse_known_args(km._logs.rewrite_short_flags(list(args)))
+    a.args = list(a.args) + extra
+    if a.command is None:
+        a.command = []
+    with contextlib.redirect_stdout(Out()), contextlib.redirect_stderr(err):
+        rc = await km.COMMANDS[a.cmd](c, a)
+    return rc or 0, buf.getvalue(), err.getvalue()
+
+
+def test_kubectl_logs_through_the_cluster():
+    from amdkube.api import meta as m
+    from amdkube.localcluster import LocalCluster, wait_pod
+
+    async def go():
+        async with LocalCluster(gpus="none", relist_period=0.2) as lc:
+            c = lc.client
+            lc.kubelet.cfg.log_state_check_period = 0.3
+            # a container that prints its attempt, writes to stderr, and fails: restarted with back-off
+            await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "crash", "labels": {"app": "crash"}},
+                            "spec": {"restartPolicy": "Always", "containers": [{
+                                "name": "c", "image": "busybox",
+                                "command": ["sh", "-c", "echo start $(date +%s%N); echo to-stderr >&2; sleep 4; exit 3"]}]}},
+                           "default")
+            for _ in range(300):
+                p = await c.get("pods", "crash", "default")
+                cs = ((p.get("status") or {}).get("containerStatuses") or [{}])[0]
+                if cs.get("restartCount", 0) >= 1 and (cs.get("state") or {}).get("running"):
+                    break
+                await asyncio.sleep(0.1)
+            assert cs.get("restartCount", 0) >= 1, cs
+            rc, cur, _ = await _kubectl(c, "logs", "crash")
+            rc2, prev, _ = await _kubectl(c, "logs", "crash", "-p")
+            assert rc == 0 and rc2 == 0
+            assert cur.startswith("start ") and "to-stderr\n" in cur
+            assert prev.startswith("start ") and prev != cur            # the previous instance's own output
+            rc, ts_out, _ = await _kubectl(c, "logs", "crash", "--timestamps", "--tail", "1")
+            assert rc == 0 and ts_out.count("\n") == 1
+            stamp = ts_out.split(" ", 1)[0]
+            assert abs(L.parse_rfc3339(stamp) / 1e9 - time.time()) < 60
+            rc, head, _ = await _kubectl(c, "logs", "crash", "--limit-bytes", "5")
+            assert head == "start"
+            rc, none, _ = await _kubectl(c, "logs", "crash", "--since-time", "2099-01-01T00:00:00Z")
+            assert rc == 0 and none == ""
+            rc, _, err = await _kubectl(c, "logs", "crash", "--tail", "-5")
+            assert rc == 1 and "tailLines: Invalid value: -5: must be greater than or equal to 0" in err
+            rc, _, err = await _kubectl(c, "logs", "crash", "--limit-bytes", "-1")
+            assert rc == 1 and "limitBytes: Invalid value: -1: must be greater than 0" in err
+            # a two-container pod needs -c
+            await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "two"},
+                            "spec": {"containers": [{"name": "a", "image": "busybox", "command": ["sh", "-c", "echo from-a; sleep 30"]},
+                                                    {"name": "b", "image": "busybox", "command": ["sh", "-c", "echo from-b; sleep 30"]}]}},
+                           "default")
+            await wait_pod(c, "default", "two", ("Running",), 30)
+            with pytest.raises(m.StatusError) as e:
+                await c.logs("default", "two")
+            assert e.value.code == 400 and "choose one of: [a b]" in e.value.message
+            for _ in range(50):
+                rc, out_b, _ = await _kubectl(c, "logs", "two", "b")
+                if out_b:
+                    break
+                await asyncio.sleep(0.1)
+            assert out_b == "from-b\n"
+            rc, _, err = await _kubectl(c, "logs", "two", "-c", "a", "b")
+            assert rc == 1 and "only one of -c or an inline [CONTAINER] arg is allowed" in err
+            # -f streams until the container exits
+            await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "ticker"},
+                            "spec": {"restartPolicy": "Never", "containers": [{
+                                "name": "t", "image": "busybox",
+                                "command": ["sh", "-c", "for i in 1 2 3; do echo tick $i; sleep 0.3; done"]}]}}, "default")
+            await wait_pod(c, "default", "ticker", ("Running", "Succeeded"), 30)
+            t0 = time.monotonic()
+            rc, followed, _ = await _kubectl(c, "logs", "-f", "ticker")
+            assert rc == 0 and followed == "tick 1\ntick 2\ntick 3\n" and time.monotonic() - t0 < 15
+            # TYPE/NAME: a ReplicaSet's pod
+            await c.create({"apiVersion": "apps/v1", "kind": "ReplicaSet", "metadata": {"name": "rs"},
+                            "spec": {"replicas": 1, "selector": {"matchLabels": {"app": "rs"}},
+                                     "template": {"metadata": {"labels": {"app": "rs"}},
+                                                  "spec": {"containers": [{"name": "w", "image": "busybox",
+                                                                           "command": ["sh", "-c", "echo from-rs; sleep 30"]}]}}}},
+                           "default")
+            for _ in range(100):
+                rc, rs_out, _ = await _kubectl(c, "logs", "rs/rs")
+                if rs_out:
+                    break
+                await asyncio.sleep(0.1)
+            assert rs_out == "from-rs\n"
+            # -l: every matching pod's log
+            rc, sel_out, _ = await _kubectl(c, "logs", "-l", "app=crash")
+            assert rc == 0 and "start " in sel_out
+    run(go(), 120)

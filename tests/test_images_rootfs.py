@@ -23,7 +23,7 @@ from amdkube.runtime import RocShim
 from amdkube.runtime.images import NATIVE_BIN
 from amdkube.runtime.oci import ImageFormatError, apply_layer, import_image, write_docker_archive
 from amdkube.runtime.rootless import elf_interp, rootfs_argv
-from tests.conftest import run
+from tests.conftest import run, log_text
 
 
 def host_closure(*progs) -> list[tuple]:
@@ -229,8 +229,8 @@ def test_image_config_precedence_and_gc_through_cri(tmp_path):
                     if st.state == C.CONTAINER_EXITED:
                         break
                     await asyncio.sleep(0.01)
-                assert st.exit_code == 0, open(st.log_path).read()
-                logs[name] = open(st.log_path).read().split()
+                assert st.exit_code == 0, log_text(st.log_path)
+                logs[name] = log_text(st.log_path).split()
             assert logs["default"][:2] == ["CMD", "from-image"] and logs["default"][2] == "/srv"   # rootview: image paths
             assert logs["args"][:2] == ["ARGS", "from-pod"]
             assert logs["cmd"] == ["OWN"]
@@ -310,7 +310,7 @@ def test_rootview_makes_the_image_root_the_containers_root(tmp_path):
                 if st.state == C.CONTAINER_EXITED:
                     break
                 await asyncio.sleep(0.01)
-            out = open(st.log_path).read()
+            out = log_text(st.log_path)
             assert st.exit_code == 0, out
             lines = out.split("\n")
             assert lines[:8] == ["in-image", "in-image", "no-host-etc", "/srv", "scratch", "from-volume",

@@ -20,7 +20,7 @@ from amdkube.kubelet.cri_client import CRIClient
 from amdkube.runtime import RocShim
 from amdkube.runtime.images import NATIVE_BIN
 from amdkube.runtime.rocshim import DEVVIEW_LIB, container_caps, probe_isolation, resolve_isolation
-from tests.conftest import run
+from tests.conftest import run, log_text
 
 NSEXEC = os.path.join(NATIVE_BIN, "amdkube-nsexec")
 PROBE = probe_isolation(NSEXEC) if os.path.exists(NSEXEC) else {}
@@ -166,8 +166,8 @@ def test_rocshim_landlock_mode_end_to_end(fake_dev):
                     if st.state == C.CONTAINER_EXITED:
                         break
                     await asyncio.sleep(0.01)
-                assert st.exit_code == 0, open(st.log_path).read()
-                out[name] = (json.loads(open(st.log_path).read().strip().splitlines()[-1]), info["handler"])
+                assert st.exit_code == 0, log_text(st.log_path)
+                out[name] = (json.loads(log_text(st.log_path).strip().splitlines()[-1]), info["handler"])
             gpu, handler = out["gpu"]
             assert handler == "rocm"
             assert [k for k, v in gpu.items() if v == "ok"] == ["renderD134", "kfd"]

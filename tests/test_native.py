@@ -65,6 +65,41 @@ def test_pause_reaps_and_exits_on_term(binary, tmp_path):
     assert p.wait(5) == 0
 
 
+@pytest.mark.parametrize("binary", ["amdkube-logpump", "amdkube-logpump-asan"])
+def test_logpump_records_under_asan(binary, tmp_path):
+    """native/logpump.cpp (and its ASan/UBSan build) on bursts of mixed-size lines from both
+    streams: every byte comes back through the CRI decoder, per stream, in order."""
+    from amdkube.kubelet.logs import LogOptions, read_logs_sync
+    rng = random.Random(7)
+    chunks = {1: [], 2: []}
+    for _ in range(300):
+        fd = rng.choice((1, 2))
+        chunks[fd].append(b"y" * rng.choice((0, 1, 80, 4000, 20000, 40000)) + (b"\n" if rng.random() < 0.8 else b""))
+    spec = tmp_path / "spec.py"
+    spec.write_text("import itertools, os\n"
+                    f"c1={chunks[1]!r}\nc2={chunks[2]!r}\n"
+                    "for a, b in itertools.zip_longest(c1, c2):\n"
+                    "    a and os.write(1, a)\n"
+                    "    b and os.write(2, b)\n")
+    script = f"exec(open({str(spec)!r}).read())"
+    log = tmp_path / "0.log"
+    ro, wo = os.pipe()
+    re_, we = os.pipe()
+    pump = subprocess.Popen([os.path.join(BIN, binary), "--log", str(log), "--stdout-fd", str(ro), "--stderr-fd", str(re_)],
+                            pass_fds=(ro, re_), stderr=subprocess.PIPE)
+    os.close(ro)
+    os.close(re_)
+    w = subprocess.Popen([sys.executable, "-c", script], stdout=wo, stderr=we)
+    os.close(wo)
+    os.close(we)
+    assert w.wait(60) == 0
+    _, err = pump.communicate(timeout=60)
+    assert pump.returncode == 0, err.decode()[-2000:]
+    out, errs = [], []
+    read_logs_sync(str(log), LogOptions(), out.append, errs.append)
+    assert b"".join(out) == b"".join(chunks[1]) and b"".join(errs) == b"".join(chunks[2])
+
+
 @pytest.mark.skipif(os.geteuid() != 0, reason="mount namespaces need root")
 def test_nsexec_hides_other_render_nodes(tmp_path):
     dev = tmp_path / "dev"

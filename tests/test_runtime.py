@@ -13,7 +13,7 @@ import pytest
 from amdkube.grpcdesc.cri import CRI as C
 from amdkube.kubelet.cri_client import CRIClient
 from amdkube.runtime import HookService, RocShim
-from tests.conftest import run
+from tests.conftest import run, log_text
 
 
 def sandbox_cfg(name="p", uid="u1"):
@@ -80,7 +80,7 @@ def test_container_lifecycle_logs_exit_codes_and_env_scrub():
                     break
                 await asyncio.sleep(0.01)
             assert st.exit_code == 3 and st.reason == "Error"
-            assert open(st.log_path).read().strip() == "HIP=-1 ROCR=unset"  # non-GPU container sees no GPU
+            assert log_text(st.log_path).strip() == "HIP=-1 ROCR=unset"  # non-GPU container sees no GPU
             gid = await cri.create_container(sid, ctr_cfg("g", ["sh", "-c", "echo ROCR=$ROCR_VISIBLE_DEVICES HIP=${HIP_VISIBLE_DEVICES:-unset}"],
                                                           envs={"ROCR_VISIBLE_DEVICES": "GPU-abc"}, devices=["/dev/kfd"]), sc)
             await cri.start_container(gid)
@@ -90,7 +90,7 @@ def test_container_lifecycle_logs_exit_codes_and_env_scrub():
                     break
                 await asyncio.sleep(0.01)
             assert st.exit_code == 0
-            assert open(st.log_path).read().strip() == "ROCR=GPU-abc HIP=unset"
+            assert log_text(st.log_path).strip() == "ROCR=GPU-abc HIP=unset"
             assert info["handler"] == "rocm"
             lid = await cri.create_container(sid, ctr_cfg("long", ["sleep", "30"]), sc)
             await cri.start_container(lid)
