@@ -396,6 +396,12 @@ class ResourceStore:
             nmd = new.setdefault("metadata", {})
             if nmd.get("name", name) != name:
                 raise m.bad_request("the name of the object does not match the name on the URL")
+            if patch is not None and nmd.get("resourceVersion") and \
+                    nmd["resourceVersion"] != (cur.get("metadata") or {}).get("resourceVersion"):
+                # a patch that sets metadata.resourceVersion is a precondition (the patched object
+                # goes through Store.Update, which compares it: `kubectl label --resource-version`)
+                raise m.conflict(self.ri.plural, name, "the object has been modified; please apply your changes to "
+                                 "the latest version and try again")
             self._prepare_update(new, cur, subresource)
             SCHEME.default(new)
             attrs = adm.Attributes(adm.UPDATE, self.ri.plural, subresource, ns, name, new, cur, user, self.ri.kind,

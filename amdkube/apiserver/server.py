@@ -111,6 +111,28 @@ _METRIC_VERBS = {"create": "POST", "update": "PUT", "patch": "PATCH", "delete": 
                  "deletecollection": "DELETECOLLECTION", "get": "GET", "list": "LIST", "watch": "WATCH"}
 
 
+
+def _subresource_doc(ri, sub: str) -> dict:
+    """A subresource's APIResource entry as the reference's discovery serves it: its own kind
+    (Binding, Eviction in policy/v1beta1, Scale) and the verbs it accepts."""
+    doc = {"name": f"{ri.plural}/{sub}", "singularName": "", "namespaced": ri.namespaced, "kind": ri.kind,
+           "verbs": ["get", "patch", "update"]}
+    if sub == "binding":
+        doc.update(kind="Binding", verbs=["create"])
+    elif sub == "eviction":
+        doc.update(group="policy", version="v1beta1", kind="Eviction", verbs=["create"])
+    elif sub == "scale":
+        doc["kind"] = "Scale"
+        if not ri.group:
+            doc.update(group="autoscaling", version="v1")
+    elif sub == "log":
+        doc["verbs"] = ["get"]
+    elif sub in ("exec", "attach", "portforward"):
+        doc["verbs"] = ["create", "get"]
+    elif sub == "proxy":
+        doc["verbs"] = ["create", "delete", "get", "patch", "update"]
+    return doc
+
 class APIServer:
     def __init__(self, store: MVCCStore | None = None, admission_plugins=adm.DEFAULT_CHAIN, admission_config=None,
                  token_auth: dict | None = None, authorization_mode: str = "AlwaysAllow",
@@ -589,15 +611,14 @@ class APIServer:
             self.aggregator.group_docs(set(groups))
         return _resp({"kind": "APIGroupList", "apiVersion": "v1", "groups": docs})
 
-    def _resource_list(self, group, version):
+    def _resource_list(self, group, version):  # noqa: C901
         res = []
         for ri in SCHEME.by_kind.values():
             if ri.group == group and ri.version == version:
                 res.append({"name": ri.plural, "singularName": ri.kind.lower(), "namespaced": ri.namespaced,
                             "kind": ri.kind, "verbs": list(ri.verbs), "shortNames": list(ri.short_names)})
                 for sub in ri.subresources:
-                    res.append({"name": f"{ri.plural}/{sub}", "singularName": "", "namespaced": ri.namespaced,
-                                "kind": "Binding" if sub == "binding" else ri.kind, "verbs": ["get", "create", "update", "patch"]})
+                    res.append(_subresource_doc(ri, sub))
         return {"kind": "APIResourceList", "apiVersion": "v1", "groupVersion": f"{group}/{version}" if group else version,
                 "resources": res}
 

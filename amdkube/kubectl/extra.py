@@ -122,7 +122,7 @@ async def _rollout_history_based(c, a, sub, ri, name, ns, res):
         await c.update(dict(obj, apiVersion=obj.get("apiVersion") or "apps/v1", kind=kind))
         print(f"{kind.lower()}.apps/{name} rolled back")
         return 0
-    end = time.time() + a.timeout
+    end = time.time() + _timeout_of(a)
     while True:
         obj = await c.get(res, name, ns)
         spec, st = obj.get("spec") or {}, obj.get("status") or {}
@@ -207,7 +207,7 @@ async def cmd_rollout(c, a):
         print(f"{ri.kind.lower()}/{name} rolled back")
         return 0
     if sub == "status":
-        end = time.time() + a.timeout
+        end = time.time() + _timeout_of(a)
         while True:
             d = await c.get(res, name, ns)
             spec, st = d.get("spec") or {}, d.get("status") or {}
@@ -849,14 +849,14 @@ async def cmd_create_generator(c, a) -> bool:
     elif kind in ("serviceaccount", "sa"):
         obj = {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": rest[0]}}
     elif kind in ("deployment", "deploy"):
-        ct = {"name": rest[0], "image": a.image}
+        ct = {"name": rest[0], "image": a.image or "busybox"}
         if a.gpus:
             ct["resources"] = {"limits": {"amd.com/gpu": str(a.gpus)}}
         obj = {"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": rest[0], "labels": {"app": rest[0]}},
-               "spec": {"replicas": a.replicas, "selector": {"matchLabels": {"app": rest[0]}},
+               "spec": {"replicas": a.replicas if a.replicas is not None else 1, "selector": {"matchLabels": {"app": rest[0]}},
                         "template": {"metadata": {"labels": {"app": rest[0]}}, "spec": {"containers": [ct]}}}}
     elif kind == "job":
-        ct = {"name": rest[0], "image": a.image}
+        ct = {"name": rest[0], "image": a.image or "busybox"}
         if a.command:
             ct["command"] = a.command
         obj = {"apiVersion": "batch/v1", "kind": "Job", "metadata": {"name": rest[0]},
@@ -932,3 +932,8 @@ def add_arguments(sp):
 
 
 __all__ = ["COMMANDS", "add_arguments", "cmd_config_sync", "cmd_create_generator", "parse_taint", "port_forward", "sys"]
+
+
+def _timeout_of(a, default: float = 30.0) -> float:
+    t = getattr(a, "timeout", None)
+    return default if t is None else float(t)

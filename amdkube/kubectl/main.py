@@ -158,6 +158,21 @@ def _read_files(paths, recursive: bool = False) -> list[dict]:
     return docs
 
 
+def parse_duration_flag(s: str) -> float:
+    """A Go duration flag (`5m`, `30s`, `1h30m`) in seconds; a bare number is seconds."""
+    try:
+        return float(s)
+    except ValueError:
+        from ..api.protobuf import parse_duration
+        return parse_duration(s) / 1e9
+
+
+def timeout_of(a, default: float = 30.0) -> float:
+    """--timeout when given, else the command's own default."""
+    t = getattr(a, "timeout", None)
+    return default if t is None else float(t)
+
+
 def _ns(a, ri=None):
     if ri is not None and not ri.namespaced:
         return ""
@@ -365,57 +380,34 @@ async def cmd_attach(c, a):
                              on_stdout=out, on_stderr=out, transport=stream_transport())
 
 
-async def _meta_edit(c, a, field):
-    r, name = _split_targets(a.args[:1])[0] if "/" in a.args[0] else (a.args[0], a.args[1])
-    kvs = a.args[1:] if "/" in a.args[0] else a.args[2:]
-    ri = SCHEME.resolve(r)
-    patch = {}
-    for kv in kvs:
-        if kv.endswith("-"):
-            patch[kv[:-1]] = None
-        else:
-            k, v = kv.split("=", 1)
-            patch[k] = v
-    await c.patch(ri.plural, name, {"metadata": {field: patch}}, _ns(a, ri))
-    print(f"{ri.kind.lower()}/{name} {'labeled' if field == 'labels' else 'annotated'}")
-
-
 async def cmd_label(c, a):
-    await _meta_edit(c, a, "labels")
+    from .metacmds import cmd_label as label
+    return await label(c, a)
 
 
 async def cmd_annotate(c, a):
-    await _meta_edit(c, a, "annotations")
+    from .metacmds import cmd_annotate as annotate
+    return await annotate(c, a)
 
 
-async def cmd_cordon(c, a, value=True):
-    for n in a.args:
-        await c.patch("nodes", n.split("/", 1)[-1], {"spec": {"unschedulable": value or None}})
-        print(f"node/{n.split('/', 1)[-1]} {'cordoned' if value else 'uncordoned'}")
+async def cmd_cordon(c, a):
+    from .drain import cmd_cordon as cordon
+    return await cordon(c, a)
 
 
 async def cmd_uncordon(c, a):
-    await cmd_cordon(c, a, False)
+    from .drain import cmd_uncordon as uncordon
+    return await uncordon(c, a)
 
 
 async def cmd_drain(c, a):
-    node = a.args[0].split("/", 1)[-1]
-    await cmd_cordon(c, argparse.Namespace(args=[node]), True)
-    pods, _ = await c.list("pods", "", field_selector=f"spec.nodeName={node}")
-    for p in pods:
-        ref = m.controller_ref(p) or {}
-        if ref.get("kind") == "DaemonSet" and a.ignore_daemonsets:
-            continue
-        await c.evict(m.namespace_of(p), m.name_of(p))
-        print(f"pod/{m.name_of(p)} evicted")
-    print(f"node/{node} drained")
+    from .drain import cmd_drain as drain
+    return await drain(c, a)
 
 
 async def cmd_scale(c, a):
-    r, name = _split_targets(a.args)[0]
-    ri = SCHEME.resolve(r)
-    await c.patch(f"{ri.plural}.{ri.group}" if ri.group else ri.plural, name, {"spec": {"replicas": a.replicas}}, _ns(a, ri))
-    print(f"{ri.kind.lower()}/{name} scaled")
+    from .scale import cmd_scale as scale
+    return await scale(c, a)
 
 
 async def cmd_patch(c, a):
@@ -428,15 +420,8 @@ async def cmd_patch(c, a):
 
 
 async def cmd_run(c, a):
-    c0 = {"name": a.args[0], "image": a.image}
-    if a.command:
-        c0["command"] = a.command
-    if a.gpus:
-        c0["resources"] = {"limits": {"amd.com/gpu": str(a.gpus)}}
-    pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": a.args[0], "labels": {"run": a.args[0]}},
-           "spec": {"restartPolicy": a.restart, "containers": [c0]}}
-    obj = await c.create(pod, a.namespace or "default")
-    print(f"pod/{m.name_of(obj)} created")
+    from .run import cmd_run as run_
+    return await run_(c, a)
 
 
 async def cmd_top(c, a):
@@ -472,7 +457,7 @@ async def cmd_wait(c, a):
     r, name = _split_targets(a.args)[0]
     ri = SCHEME.resolve(r)
     cond = a.for_.split("=", 1)[1] if "=" in a.for_ else a.for_
-    end = time.time() + a.timeout
+    end = time.time() + timeout_of(a)
     while time.time() < end:
         o = await c.get_or_none(ri.plural, name, _ns(a, ri))
         if a.for_ == "delete" and o is None:
@@ -495,6 +480,10 @@ COMMANDS = {"get": cmd_get, "describe": cmd_describe, "create": cmd_create, "app
 from .extra import COMMANDS as _EXTRA, add_arguments as _extra_args  # noqa: E402
 from . import more as _more  # noqa: E402
 from . import logs as _logs  # noqa: E402
+from . import drain as _drain  # noqa: E402
+from . import metacmds as _metacmds  # noqa: E402
+from . import scale as _scale  # noqa: E402
+from . import run as _run  # noqa: E402
 COMMANDS.update(_EXTRA)
 COMMANDS.update(_more.COMMANDS)
 COMMANDS["apply"] = _more.cmd_apply       # three-way merge, --prune, *-last-applied
@@ -523,6 +512,10 @@ def parser():
         _extra_args(sp)
         _more.add_arguments(sp)
         _logs.add_arguments(sp)
+        _drain.add_arguments(sp)
+        _metacmds.add_arguments(sp)
+        _scale.add_arguments(sp)
+        _run.add_arguments(sp)
         sp.add_argument("args", nargs="*")
         sp.add_argument("-n", "--namespace", default=argparse.SUPPRESS)
         sp.add_argument("-o", "--output", default=None)
@@ -540,14 +533,14 @@ def parser():
         sp.add_argument("--cascade", type=lambda s: s != "false", default=True)
         sp.add_argument("--ignore-not-found", action="store_true")
         sp.add_argument("--ignore-daemonsets", action="store_true")
-        sp.add_argument("--replicas", type=int, default=1)
+        sp.add_argument("--replicas", "-r", type=int, default=None)
         sp.add_argument("-p", "--patch", default="{}")
         sp.add_argument("--type", default="strategic")
-        sp.add_argument("--image", default="busybox")
+        sp.add_argument("--image", default=None)
         sp.add_argument("--gpus", type=int, default=0)
         sp.add_argument("--restart", default="Always")
         sp.add_argument("--for", dest="for_", default="condition=Ready")
-        sp.add_argument("--timeout", type=float, default=30.0)
+        sp.add_argument("--timeout", type=parse_duration_flag, default=None)
         sp.add_argument("--command", nargs=argparse.REMAINDER, default=None)
         sp.add_argument("--validate", nargs="?", const=True, default=True,
                         type=lambda s: s.lower() not in ("false", "0", "no"))
@@ -609,8 +602,10 @@ def main(argv=None):
         i = argv.index("--")
         argv, cmd_tail = argv[:i], argv[i + 1:]
     argv = _logs.rewrite_short_flags(argv)
+    command_flag = "--command" in argv
     p = parser()
     a, extra = p.parse_known_args(argv)
+    a.command_flag = command_flag
     if any(x.startswith("-") for x in extra):
         p.error(f"unrecognized arguments: {' '.join(extra)}")
     a.args = list(a.args) + extra      # positionals after flags (kubectl alpha diff -f x LAST LOCAL)

@@ -380,7 +380,7 @@ async def cmd_rolling_update(c, a):
     print(f"Created {new_name}")
 
     async def ready(name, want):
-        for _ in range(int(a.timeout * 10)):
+        for _ in range(int(_timeout_of(a) * 10)):
             rc = await c.get("replicationcontrollers", name, ns)
             if (rc.get("status") or {}).get("readyReplicas", 0) >= want:
                 return
@@ -588,3 +588,8 @@ def add_arguments(sp):
 
 COMMANDS = {"rolling-update": cmd_rolling_update, "convert": cmd_convert, "api-versions": cmd_api_versions,
             "options": cmd_options, "completion": cmd_completion, "plugin": cmd_plugin}
+
+
+def _timeout_of(a, default: float = 30.0) -> float:
+    t = getattr(a, "timeout", None)
+    return default if t is None else float(t)

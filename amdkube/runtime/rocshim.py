@@ -136,7 +136,8 @@ def now_ns() -> int:
 class PidProc:
     """A child process watched through a pidfd on the event loop (Linux ≥ 5.3): no transport,
     pipes or per-child waiter thread, which asyncio.create_subprocess_exec costs per spawn
-    (ThreadedChildWatcher). `wait()` returns the returncode as subprocess does (−signal)."""
+    (ThreadedChildWatcher). `wait()` returns the returncode as subprocess does (−signal).
+    `pump` is the container's log pump (a future resolved when it has exited and been reaped)."""
     __slots__ = ("pid", "returncode", "_popen", "_fd", "_fut", "pump")
 
     def __init__(self, popen: subprocess.Popen, fd: int):
@@ -159,14 +160,36 @@ class PidProc:
     async def logs_flushed(self, timeout: float = 2.0):
         """Wait (bounded) for the log pump to write the container's last output: it exits once
         every writer of the pipes is gone, which a daemon the container left behind can delay."""
-        pump = self.pump
-        if pump is None:
-            return
+        if self.pump is not None and not self.pump.done():
+            try:
+                await asyncio.wait_for(asyncio.shield(self.pump), timeout)
+            except asyncio.TimeoutError:
+                pass
+
+
+def _reap_later(pid: int, pidfd: int | None):
+    """A future resolved once `pid` (our child) exits, reaped on the event loop through its
+    pidfd — or by a waiter thread on kernels without pidfds."""
+    loop = asyncio.get_running_loop()
+    fut = loop.create_future()
+
+    def reaped(_=None):
+        if not fut.done():
+            fut.set_result(None)
+    if pidfd is None:
+        loop.run_in_executor(None, os.waitpid, pid, 0).add_done_callback(reaped)
+        return fut
+
+    def exited():
+        loop.remove_reader(pidfd)
+        os.close(pidfd)
         try:
-            await asyncio.wait_for(asyncio.to_thread(pump.wait), timeout)
-        except asyncio.TimeoutError:
-            asyncio.get_running_loop().run_in_executor(None, pump.wait)     # reap it whenever it ends
-        self.pump = None
+            os.waitpid(pid, 0)
+        except ChildProcessError:
+            pass
+        reaped()
+    loop.add_reader(pidfd, exited)
+    return fut
 
 
 LOGPUMP_BIN = os.path.join(NATIVE_BIN, "amdkube-logpump")
@@ -183,50 +206,59 @@ def logpump_bin() -> str | None:
     return None
 
 
+def _spawn_pump(pump: str, log_path: str, out_r: int, err_r: int) -> int:
+    """posix_spawn (vfork-fast, unlike a fork of this whole process) of the log pump in a
+    session of its own, its read ends as fds 3 and 4 (dup2 clears close-on-exec on them only)."""
+    return os.posix_spawn(pump, [pump, "--log", log_path, "--stdout-fd", "3", "--stderr-fd", "4"], os.environ,
+                          file_actions=[(os.POSIX_SPAWN_DUP2, out_r, 3), (os.POSIX_SPAWN_DUP2, err_r, 4)], setsid=True)
+
+
 def _popen(argv, stdout, stderr, env, cwd, log_path, oom_score_adj=None, pass_fds=(), pump=None):
     """fork/exec (and the log file's open, and the child's oom_score_adj) off the event loop: a
     spawn is ~1 ms of syscalls that would otherwise stall every other CRI call the runtime is
     serving. With a log path and `pump` (the logpump binary) the container's stdout and stderr
     are pipes whose read ends the pump owns: it writes the CRI log format (timestamp, stream,
     partial/full tag per line) and outlives this runtime process; without one they are the log
-    file itself."""
-    logf = pump_proc = None
-    out_w = err_w = None
+    file itself. The container is started first; the pump follows (the pipes buffer meanwhile)."""
+    logf = None
+    pipes = None
     if log_path and pump:
         out_r, out_w = os.pipe()
         err_r, err_w = os.pipe()
-        try:
-            pump_proc = subprocess.Popen([pump, "--log", log_path, "--stdout-fd", str(out_r), "--stderr-fd", str(err_r)],
-                                         stdin=subprocess.DEVNULL, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
-                                         pass_fds=(out_r, err_r), start_new_session=True)
-        except BaseException:
-            for fd in (out_w, err_w):
-                os.close(fd)
-            raise
-        finally:
-            os.close(out_r)
-            os.close(err_r)
+        pipes = (out_r, out_w, err_r, err_w)
         out, err = out_w, err_w
     else:
         logf = open(log_path, "ab", buffering=0) if log_path else None
         out = logf if logf is not None else (stdout if stdout is not None else subprocess.DEVNULL)
         err = logf if logf is not None else (stderr if stderr is not None else subprocess.DEVNULL)
+    pump_pid = None
     try:
         p = subprocess.Popen(argv, stdin=subprocess.DEVNULL, stdout=out, stderr=err, env=env, cwd=cwd,
                              start_new_session=True, pass_fds=pass_fds)
+        if pipes:
+            os.close(pipes[1])
+            os.close(pipes[3])     # the pump sees EOF once the container's copies are gone
+            pipes = (pipes[0], None, pipes[2], None)
+            pump_pid = _spawn_pump(pump, log_path, pipes[0], pipes[2])
     finally:
         if logf is not None:
             logf.close()
-        for fd in (out_w, err_w):
+        for fd in pipes or ():
             if fd is not None:
-                os.close(fd)     # the pump sees EOF once the container's copies are gone too
+                os.close(fd)
     try:
         fd = os.pidfd_open(p.pid)
     except (AttributeError, OSError):
         fd = None
+    pump_fd = None
+    if pump_pid is not None:
+        try:
+            pump_fd = os.pidfd_open(pump_pid)
+        except (AttributeError, OSError):
+            pump_fd = None
     if oom_score_adj:
         _set_oom_score_adj(p.pid, oom_score_adj)
-    return p, fd, pump_proc
+    return p, fd, (pump_pid, pump_fd) if pump_pid is not None else None
 
 
 async def spawn(argv, stdout=None, stderr=None, env=None, cwd=None, log_path=None, oom_score_adj=None, pass_fds=(),
@@ -235,15 +267,16 @@ async def spawn(argv, stdout=None, stderr=None, env=None, cwd=None, log_path=Non
     `log_path` when given — through the log pump with `log_pump`); pidfd-watched when
     possible."""
     pump = logpump_bin() if log_pump and log_path else None
-    p, fd, pump_proc = await asyncio.to_thread(_popen, argv, stdout, stderr, env, cwd, log_path, oom_score_adj, pass_fds, pump)
+    p, fd, pump_info = await asyncio.to_thread(_popen, argv, stdout, stderr, env, cwd, log_path, oom_score_adj, pass_fds, pump)
     if fd is None:   # old kernel: a thread waits for the child
         loop = asyncio.get_running_loop()
         proc = PidProc.__new__(PidProc)
-        proc.pid, proc.returncode, proc._popen, proc._fd = p.pid, None, p, -1
+        proc.pid, proc.returncode, proc._popen, proc._fd, proc.pump = p.pid, None, p, -1, None
         proc._fut = loop.run_in_executor(None, p.wait)
     else:
         proc = PidProc(p, fd)
-    proc.pump = pump_proc
+    if pump_info is not None:
+        proc.pump = _reap_later(*pump_info)
     return proc
 
 class Sandbox:
@@ -1127,7 +1160,8 @@ class RocShim:
 
     async def _wait(self, c: Container):
         rc = await c.proc.wait()
-        await c.proc.logs_flushed(0.5)       # the termination-message fallback reads the log's tail
+        if rc and c.annotations.get("io.kubernetes.container.terminationMessagePolicy") == "FallbackToLogsOnError":
+            await c.proc.logs_flushed(0.5)   # the termination-message fallback reads the log's tail
         # written by the checkpoint thread, ordered before the container's checkpoint and any
         # later removal of the same file
         self.ckpt.put(os.path.join(self.state_dir, "containers", c.id + ".exit"), str(rc).encode())

@@ -1,0 +1,456 @@
+"""kubectl label / annotate / scale / run at reference parity.
+
+Transcribed: pkg/kubectl/cmd/label_test.go (TestValidateLabels, TestParseLabels, TestLabelFunc,
+TestLabelErrors), annotate_test.go (TestValidateAnnotationOverwrites, TestParseAnnotations,
+TestValidateAnnotations, TestUpdateAnnotations, TestAnnotateErrors), cmd/run_test.go
+(TestGetRestartPolicy, TestGenerateService, TestRunValidations), pkg/kubectl/run_test.go
+(TestGenerate, TestGeneratePod, TestGenerateDeployment, TestGenerateJob, TestGenerateCronJob*,
+TestParseEnv), pkg/kubectl/scale.go's precondition errors. Then the commands through a live
+cluster.
+"""
+from __future__ import annotations
+
+import asyncio
+import contextlib
+import io
+
+import pytest
+
+from amdkube.api import meta as m
+from amdkube.kubectl import metacmds as MC
+from amdkube.kubectl import run as R
+from amdkube.kubectl import scale as S
+from tests.conftest import run
+
+
+# ---------------------------------------------------------------------------- label
+@pytest.mark.parametrize("labels,new,err", [
+    ({"a": "b", "c": "d"}, {"a": "c", "d": "b"}, True),
+    ({"a": "b", "c": "d"}, {"b": "d", "c": "a"}, True),
+    ({"a": "b", "c": "d"}, {"b": "a", "d": "c"}, False),
+    ({}, {"b": "a", "d": "c"}, False),
+])
+def test_validate_labels(labels, new, err):
+    obj = {"metadata": {"labels": labels}}
+    if err:
+        with pytest.raises(MC.UsageError, match="already has a value"):
+            MC.validate_no_overwrites(obj, new)
+    else:
+        MC.validate_no_overwrites(obj, new)
+
+
+@pytest.mark.parametrize("spec,labels,remove,err", [
+    (["a=b", "c=d"], {"a": "b", "c": "d"}, None, False),
+    ([], {}, None, False),
+    (["a=b", "c=d", "e-"], {"a": "b", "c": "d"}, ["e"], False),
+    (["ab", "c=d"], None, None, True),
+    (["a=b", "c=d", "a-"], None, None, True),
+    (["a="], {"a": ""}, None, False),
+    (["a=%^$"], None, None, True),
+])
+def test_parse_labels(spec, labels, remove, err):
+    if err:
+        with pytest.raises(MC.UsageError):
+            MC.parse_labels(spec)
+        return
+    assert MC.parse_labels(spec) == (labels, remove)
+
+
+@pytest.mark.parametrize("labels,overwrite,version,new,remove,expected,err", [
+    ({"a": "b"}, False, "", {"a": "b"}, None, None, True),
+    ({"a": "b"}, True, "", {"a": "c"}, None, {"labels": {"a": "c"}}, False),
+    ({"a": "b"}, False, "", {"c": "d"}, None, {"labels": {"a": "b", "c": "d"}}, False),
+    ({"a": "b"}, False, "2", {"c": "d"}, None, {"labels": {"a": "b", "c": "d"}, "resourceVersion": "2"}, False),
+    ({"a": "b"}, False, "", {}, ["a"], {"labels": {}}, False),
+    ({"a": "b", "c": "d"}, False, "", {"e": "f"}, ["a"], {"labels": {"c": "d", "e": "f"}}, False),
+    (None, False, "", {"a": "b"}, None, {"labels": {"a": "b"}}, False),
+])
+def test_label_func(labels, overwrite, version, new, remove, expected, err):
+    obj = {"metadata": {"labels": labels} if labels is not None else {}}
+    if err:
+        with pytest.raises(MC.UsageError):
+            MC.label_func(obj, overwrite, version, new, remove)
+        return
+    MC.label_func(obj, overwrite, version, new, remove)
+    assert obj["metadata"] == expected
+
+
+def _args(*argv):
+    from amdkube.kubectl import main as km
+    argv = km._logs.rewrite_short_flags(list(argv))
+    a, extra = km.parser().parse_known_args(argv)
+    a.args = list(a.args) + extra
+    a.command_flag = "--command" in argv
+    if a.command is None:
+        a.command = []
+    return a
+
+
+async def _kubectl(c, *argv, tail=None):
+    from amdkube.kubectl import main as km
+    out, err = io.StringIO(), io.StringIO()
+    a = _args(*argv)
+    if tail is not None:
+        a.command = list(tail)
+    with contextlib.redirect_stdout(out), contextlib.redirect_stderr(err):
+        rc = await km.COMMANDS[a.cmd](c, a)
+    return rc or 0, out.getvalue(), err.getvalue()
+
+
+@pytest.mark.parametrize("cmd,args,msg", [
+    ("label", [], "one or more resources must be specified"),
+    ("label", ["pods"], "at least one label update is required"),
+    ("label", ["pods", "-"], "at least one label update is required"),
+    ("label", ["pods", "=bar"], "at least one label update is required"),
+    ("label", ["pods-"], "one or more resources must be specified"),
+    ("label", ["pods=bar"], "one or more resources must be specified"),
+    ("label", ["pods", "app=bar"], "resource(s) were provided, but no name, label selector, or --all flag specified"),
+    ("label", ["pods,deployments", "app=bar"], "resource(s) were provided, but no name, label selector, or --all flag specified"),
+    ("annotate", [], "one or more resources must be specified"),
+    ("annotate", ["pods"], "at least one annotation update is required"),
+    ("annotate", ["pods", "-"], "at least one annotation update is required"),
+    ("annotate", ["pods", "=bar"], "at least one annotation update is required"),
+    ("annotate", ["pods-"], "one or more resources must be specified"),
+    ("annotate", ["pods=bar"], "one or more resources must be specified"),
+])
+def test_label_and_annotate_errors(cmd, args, msg):
+    class NoServer:
+        async def list(self, *a, **k):
+            raise AssertionError("no request expected")
+        get = list
+
+    rc, out, err = run(_kubectl(NoServer(), cmd, *args))
+    assert rc == 1 and msg in err and out == ""
+
+
+# ------------------------------------------------------------------------- annotate
+@pytest.mark.parametrize("cur,new,err", [
+    ({"a": "A", "b": "B"}, {"a": "a", "c": "C"}, True),
+    ({"a": "A", "c": "C"}, {"b": "B", "c": "c"}, True),
+    ({"a": "A", "c": "C"}, {"b": "B", "d": "D"}, False),
+    ({}, {"a": "A", "b": "B"}, False),
+])
+def test_validate_annotation_overwrites(cur, new, err):
+    obj = {"metadata": {"annotations": cur}}
+    if err:
+        with pytest.raises(MC.UsageError, match="--overwrite is false but found the following declared annotation"):
+            MC.validate_no_annotation_overwrites(obj, new)
+    else:
+        MC.validate_no_annotation_overwrites(obj, new)
+
+
+URL = "https://test.com/index.htm?id=123#u=user-name"
+JSON = ("'{\"kind\":\"SerializedReference\",\"apiVersion\":\"v1\",\"reference\":{\"kind\":\"ReplicationController\","
+        "\"namespace\":\"default\",\"name\":\"my-nginx\",\"uid\":\"c544ee78-2665-11e5-8051-42010af0c213\","
+        "\"apiVersion\":\"v1\",\"resourceVersion\":\"61368\"}}'")
+
+
+@pytest.mark.parametrize("args,new,remove,err", [
+    (["a=b", "c=d"], {"a": "b", "c": "d"}, [], None),
+    (["url=" + URL, "fake.kubernetes.io/annotation=" + JSON], {"url": URL, "fake.kubernetes.io/annotation": JSON}, [], None),
+    ([], {}, [], None),
+    (["a=b", "c=d", "e-"], {"a": "b", "c": "d"}, ["e"], None),
+    (["ab", "c=d"], None, None, "invalid annotation format: ab"),
+    (["a="], {"a": ""}, [], None),
+    (["ab", "a="], None, None, "invalid annotation format: ab"),
+    (["-"], None, None, "invalid annotation format: -"),
+    (["=bar"], None, None, "invalid annotation format: =bar"),
+])
+def test_parse_annotations(args, new, remove, err):
+    if err:
+        with pytest.raises(MC.UsageError) as e:
+            MC.parse_pairs(args, "annotation", True)
+        assert str(e.value) == err
+        return
+    assert MC.parse_pairs(args, "annotation", True) == (new, remove)
+
+
+def test_validate_annotations():
+    with pytest.raises(MC.UsageError) as e:
+        MC.validate_annotations(["a"], {"a": "b", "c": "d"})
+    assert str(e.value) == "can not both modify and remove the following annotation(s) in the same command: a"
+    with pytest.raises(MC.UsageError) as e:
+        MC.validate_annotations(["a", "c"], {"a": "b", "c": "d"})
+    assert str(e.value) == "can not both modify and remove the following annotation(s) in the same command: a, c"
+
+
+@pytest.mark.parametrize("cur,overwrite,version,new,remove,expected,err", [
+    ({"a": "b"}, False, "", {"a": "b"}, None, None, True),
+    ({"a": "b"}, True, "", {"a": "c"}, None, {"annotations": {"a": "c"}}, False),
+    ({"a": "b"}, False, "", {"c": "d"}, None, {"annotations": {"a": "b", "c": "d"}}, False),
+    ({"a": "b"}, False, "2", {"c": "d"}, None, {"annotations": {"a": "b", "c": "d"}, "resourceVersion": "2"}, False),
+    ({"a": "b"}, False, "", {}, ["a"], {"annotations": {}}, False),
+    ({"a": "b", "c": "d"}, False, "", {"e": "f"}, ["a"], {"annotations": {"c": "d", "e": "f"}}, False),
+    ({"a": "b", "c": "d"}, False, "", {"e": "f"}, ["g"], {"annotations": {"a": "b", "c": "d", "e": "f"}}, False),
+    ({"a": "b", "c": "d"}, False, "", {}, ["e"], {"annotations": {"a": "b", "c": "d"}}, False),
+    (None, False, "", {"a": "b"}, None, {"annotations": {"a": "b"}}, False),
+])
+def test_update_annotations(cur, overwrite, version, new, remove, expected, err):
+    obj = {"metadata": {"annotations": cur} if cur is not None else {}}
+    if err:
+        with pytest.raises(MC.UsageError):
+            MC.update_annotations(obj, overwrite, version, new, remove)
+        return
+    MC.update_annotations(obj, overwrite, version, new, remove)
+    assert obj["metadata"] == expected
+
+
+# ------------------------------------------------------------------------------ run
+@pytest.mark.parametrize("inp,interactive,expected", [
+    ("", False, "Always"), ("", True, "OnFailure"), ("Always", True, "Always"), ("Never", True, "Never"),
+    ("Always", False, "Always"), ("Never", False, "Never"), ("foo", False, None),
+])
+def test_get_restart_policy(inp, interactive, expected):
+    if expected is None:
+        with pytest.raises(R.GenerateError):
+            R.get_restart_policy(inp, interactive)
+    else:
+        assert R.get_restart_policy(inp, interactive) == expected
+
+
+def _rc(labels, container, replicas=1):
+    return {"apiVersion": "v1", "kind": "ReplicationController", "metadata": {"name": "foo", "labels": labels},
+            "spec": {"replicas": replicas, "selector": labels,
+                     "template": {"metadata": {"labels": labels}, "spec": {"containers": [dict({"name": "foo", "image": "someimage"}, **container)]}}}}
+
+
+RUN = {"run": "foo"}
+FOOBAR = {"foo": "bar", "baz": "blah"}
+
+
+@pytest.mark.parametrize("params,expected", [
+    ({"name": "foo", "image": "someimage", "image-pull-policy": "Always", "replicas": "1", "port": ""},
+     _rc(RUN, {"imagePullPolicy": "Always"})),
+    ({"name": "foo", "image": "someimage", "replicas": "1", "port": "", "env": ["a=b", "c=d"]},
+     _rc(RUN, {"env": [{"name": "a", "value": "b"}, {"name": "c", "value": "d"}]})),
+    ({"name": "foo", "image": "someimage", "image-pull-policy": "Never", "replicas": "1", "port": "", "args": ["bar", "baz", "blah"]},
+     _rc(RUN, {"imagePullPolicy": "Never", "args": ["bar", "baz", "blah"]})),
+    ({"name": "foo", "image": "someimage", "replicas": "1", "port": "", "args": ["bar", "baz", "blah"], "command": "true"},
+     _rc(RUN, {"command": ["bar", "baz", "blah"]})),
+    ({"name": "foo", "image": "someimage", "replicas": "1", "port": "80"}, _rc(RUN, {"ports": [{"containerPort": 80}]})),
+    ({"name": "foo", "image": "someimage", "image-pull-policy": "IfNotPresent", "replicas": "1", "port": "80", "hostport": "80"},
+     _rc(RUN, {"imagePullPolicy": "IfNotPresent", "ports": [{"containerPort": 80, "hostPort": 80}]})),
+    ({"name": "foo", "image": "someimage", "replicas": "1", "hostport": "80"}, None),
+    ({"name": "foo", "image": "someimage", "replicas": "1", "labels": "foo=bar,baz=blah"}, _rc(FOOBAR, {})),
+    ({"name": "foo", "image": "someimage", "replicas": "1", "labels": "foo=bar,baz=blah", "requests": "cpu100m,memory=100Mi"}, None),
+    ({"name": "foo", "image": "someimage", "replicas": "1", "labels": "foo=bar,baz=blah", "requests": "cpu=100m&memory=100Mi"}, None),
+    ({"name": "foo", "image": "someimage", "replicas": "1", "labels": "foo=bar,baz=blah", "requests": "cpu="}, None),
+    ({"name": "foo", "image": "someimage", "replicas": "1", "labels": "foo=bar,baz=blah", "requests": "cpu=100m,memory=100Mi",
+      "limits": "cpu=400m,memory=200Mi"},
+     _rc(FOOBAR, {"resources": {"limits": {"cpu": "400m", "memory": "200Mi"}, "requests": {"cpu": "100m", "memory": "100Mi"}}})),
+])
+def test_generate_replication_controller(params, expected):
+    if expected is None:
+        with pytest.raises(R.GenerateError):
+            R.generate("run/v1", params)
+        return
+    assert R.generate("run/v1", params) == expected
+
+
+def _pod(labels, container, restart="Always"):
+    return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "foo", "labels": labels},
+            "spec": {"containers": [dict({"name": "foo", "image": "someimage", "imagePullPolicy": "IfNotPresent"}, **container)],
+                     "dnsPolicy": "ClusterFirst", "restartPolicy": restart}}
+
+
+@pytest.mark.parametrize("params,expected", [
+    ({"name": "foo", "image": "someimage", "port": ""}, _pod(RUN, {})),
+    ({"name": "foo", "image": "someimage", "env": ["a", "c"]}, None),
+    ({"name": "foo", "image": "someimage", "image-pull-policy": "Always", "env": ["a=b", "c=d"]},
+     _pod(RUN, {"imagePullPolicy": "Always", "env": [{"name": "a", "value": "b"}, {"name": "c", "value": "d"}]})),
+    ({"name": "foo", "image": "someimage", "port": "80"}, _pod(RUN, {"ports": [{"containerPort": 80}]})),
+    ({"name": "foo", "image": "someimage", "port": "80", "hostport": "80"}, _pod(RUN, {"ports": [{"containerPort": 80, "hostPort": 80}]})),
+    ({"name": "foo", "image": "someimage", "hostport": "80"}, None),
+    ({"name": "foo", "image": "someimage", "replicas": "1", "labels": "foo=bar,baz=blah"}, _pod(FOOBAR, {})),
+    ({"name": "foo", "image": "someimage", "replicas": "1", "labels": "foo=bar,baz=blah", "stdin": "true"},
+     _pod(FOOBAR, {"stdin": True, "stdinOnce": True})),
+    ({"name": "foo", "image": "someimage", "replicas": "1", "labels": "foo=bar,baz=blah", "stdin": "true", "leave-stdin-open": "true"},
+     _pod(FOOBAR, {"stdin": True})),
+])
+def test_generate_pod(params, expected):
+    if expected is None:
+        with pytest.raises(R.GenerateError):
+            R.generate("run-pod/v1", params)
+        return
+    assert R.generate("run-pod/v1", params) == expected
+
+
+FULL = {"name": "foo", "image": "someimage", "replicas": "3", "labels": "foo=bar,baz=blah", "port": "80", "hostport": "80",
+        "stdin": "true", "command": "true", "args": ["bar", "baz", "blah"], "env": ["a=b", "c=d"],
+        "requests": "cpu=100m,memory=100Mi", "limits": "cpu=400m,memory=200Mi"}
+FULL_CTR = {"name": "foo", "image": "someimage", "stdin": True, "command": ["bar", "baz", "blah"],
+            "ports": [{"containerPort": 80, "hostPort": 80}], "env": [{"name": "a", "value": "b"}, {"name": "c", "value": "d"}],
+            "resources": {"limits": {"cpu": "400m", "memory": "200Mi"}, "requests": {"cpu": "100m", "memory": "100Mi"}}}
+
+
+def test_generate_deployment_job_cronjob():
+    for gen, api in (("deployment/v1beta1", "extensions/v1beta1"), ("deployment/apps.v1beta1", "apps/v1beta1")):
+        assert R.generate(gen, FULL) == {
+            "apiVersion": api, "kind": "Deployment", "metadata": {"name": "foo", "labels": FOOBAR},
+            "spec": {"replicas": 3, "selector": {"matchLabels": FOOBAR},
+                     "template": {"metadata": {"labels": FOOBAR}, "spec": {"containers": [FULL_CTR]}}}}
+    job_params = dict(FULL, **{"leave-stdin-open": "true"})
+    job_params.pop("replicas")
+    assert R.generate("job/v1", job_params) == {
+        "apiVersion": "batch/v1", "kind": "Job", "metadata": {"name": "foo", "labels": FOOBAR},
+        "spec": {"template": {"metadata": {"labels": FOOBAR},
+                              "spec": {"containers": [FULL_CTR], "restartPolicy": "Never"}}}}
+    for gen, api in (("cronjob/v2alpha1", "batch/v2alpha1"), ("cronjob/v1beta1", "batch/v1beta1")):
+        cj = R.generate(gen, dict(job_params, schedule="0/5 * * * ?"))
+        assert cj == {"apiVersion": api, "kind": "CronJob", "metadata": {"name": "foo", "labels": FOOBAR},
+                      "spec": {"schedule": "0/5 * * * ?", "concurrencyPolicy": "Allow",
+                               "jobTemplate": {"spec": {"template": {"metadata": {"labels": FOOBAR},
+                                                                     "spec": {"containers": [FULL_CTR], "restartPolicy": "Never"}}}}}}
+    with pytest.raises(R.GenerateError, match="Parameter: schedule is required"):
+        R.generate("cronjob/v1beta1", job_params)
+
+
+@pytest.mark.parametrize("envs,ok", [
+    (["FOO=bar", "FOO_BAR=baz", "A.B=c", "-x=y", "a=b=c", "EMPTY="], True),
+    (["=novalue"], False), (["novalue"], False), (["1FOO=bar"], False),
+])
+def test_parse_env(envs, ok):
+    if ok:
+        assert [e["name"] for e in R.parse_envs(envs)] == [e.split("=", 1)[0] for e in envs]
+    else:
+        with pytest.raises(R.GenerateError, match="invalid env"):
+            R.parse_envs(envs)
+
+
+def test_generate_service():
+    assert R.generate_service({"name": "foo", "port": "80"}) == {
+        "apiVersion": "v1", "kind": "Service", "metadata": {"name": "foo"},
+        "spec": {"selector": {"run": "foo"}, "ports": [{"port": 80, "protocol": "TCP", "targetPort": 80}]}}
+    assert R.generate_service({"name": "foo", "port": "80", "labels": "app=bar"}) == {
+        "apiVersion": "v1", "kind": "Service", "metadata": {"name": "foo", "labels": {"app": "bar"}},
+        "spec": {"selector": {"app": "bar"}, "ports": [{"port": 80, "protocol": "TCP", "targetPort": 80}]}}
+    with pytest.raises(R.GenerateError):
+        R.generate_service({"name": "foo"})
+
+
+@pytest.mark.parametrize("args,msg", [
+    ([], "NAME is required"),
+    (["test"], "--image is required"),
+    (["test", "--image", "#"], "Invalid image name"),
+    (["test", "--image", "busybox", "--stdin", "--replicas", "2"], "stdin requires that replicas is 1"),
+    (["test", "--image", "busybox", "--rm"], "rm should only be used for attached containers"),
+    (["test", "--image", "busybox", "--attach", "--dry-run"], "can't be used with attached containers options"),
+    (["test", "--image", "busybox", "--stdin", "--dry-run"], "can't be used with attached containers options"),
+    (["test", "--image", "busybox", "--tty", "--stdin", "--dry-run"], "can't be used with attached containers options"),
+    (["test", "--image", "busybox", "--tty"], "stdin is required for containers with -t/--tty"),
+    (["test", "--image", "busybox", "--expose"], "--port must be set when exposing a service"),
+    (["test", "--image", "busybox", "--restart", "Never", "--replicas", "2"], "--restart=Never requires that --replicas=1, found 2"),
+    (["test", "--image", "busybox", "--image-pull-policy", "Sometimes"], "invalid image pull policy: Sometimes"),
+])
+def test_run_validations(args, msg):
+    class NoServer:
+        async def request(self, *a, **k):
+            raise AssertionError("no request expected")
+    rc, _, err = run(_kubectl(NoServer(), "run", *args))
+    assert rc == 1 and msg in err
+
+
+def test_image_reference_regexp():
+    for good in ("busybox", "rocm/vector-add:6.2", "registry.local:5000/ns/img@sha256:" + "a" * 64, "a_b__c-d.e"):
+        assert R.REFERENCE_RE.match(good), good
+    for bad in ("#", "UPPER", "img:", "-lead", "a//b"):
+        assert not R.REFERENCE_RE.match(bad), bad
+
+
+# ---------------------------------------------------------------------------- scale
+def test_scale_preconditions():
+    rc = {"kind": "ReplicationController", "metadata": {"resourceVersion": "7"}, "spec": {"replicas": 1}}
+    S.validate_preconditions(rc, -1, "")
+    with pytest.raises(S.PreconditionError, match="Expected replicas to be 3, was 1"):
+        S.validate_preconditions(rc, 3, "")
+    with pytest.raises(S.PreconditionError, match="Expected resource version to be 1, was 7"):
+        S.validate_preconditions(rc, -1, "1")
+    job = {"kind": "Job", "metadata": {}, "spec": {}}
+    with pytest.raises(S.PreconditionError, match="Expected parallelism to be 2, was nil"):
+        S.validate_preconditions(job, 2, "")
+
+
+# --------------------------------------------------------------------- live cluster
+def test_commands_through_the_cluster():
+    from amdkube.localcluster import LocalCluster, wait_pod
+
+    async def go():
+        async with LocalCluster(gpus="none", relist_period=0.2) as lc:
+            c = lc.client
+            for n in ("p1", "p2"):
+                await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": n, "labels": {"tier": "a"}},
+                                "spec": {"containers": [{"name": "c", "image": "busybox", "command": ["sleep", "60"]}]}}, "default")
+            # label: no overwrite without --overwrite; --overwrite; -l; removal of an absent key
+            rc, _, err = await _kubectl(c, "label", "pods", "p1", "tier=b")
+            assert rc == 1 and "'tier' already has a value (a), and --overwrite is false" in err
+            rc, out, _ = await _kubectl(c, "label", "pods", "p1", "tier=b", "--overwrite")
+            assert rc == 0 and out == 'pod "p1" labeled\n'
+            assert m.labels_of(await c.get("pods", "p1", "default"))["tier"] == "b"
+            rc, out, _ = await _kubectl(c, "label", "pods", "-l", "tier=a", "gpu=yes")
+            assert out == 'pod "p2" labeled\n'
+            rc, out, _ = await _kubectl(c, "label", "pod/p1", "missing-")
+            assert out == 'label "missing" not found.\npod "p1" not labeled\n'
+            rc, out, _ = await _kubectl(c, "label", "pods", "--all", "zone=z1")
+            assert sorted(out.splitlines()) == ['pod "p1" labeled', 'pod "p2" labeled']
+            rc, out, _ = await _kubectl(c, "label", "pods", "p2", "--list")
+            assert "gpu=yes" in out.splitlines() and "zone=z1" in out.splitlines()
+            # --resource-version is a precondition
+            rv = (await c.get("pods", "p1", "default"))["metadata"]["resourceVersion"]
+            with pytest.raises(m.StatusError) as e:
+                await _kubectl(c, "label", "pods", "p1", "x=1", "--resource-version", str(int(rv) - 1))
+            assert e.value.code == 409
+            rc, out, _ = await _kubectl(c, "label", "pods", "p1", "x=1", "--resource-version", rv)
+            assert out == 'pod "p1" labeled\n'
+            rc, _, err = await _kubectl(c, "label", "pods", "--all", "y=1", "--resource-version", rv)
+            assert rc == 1 and "--resource-version may only be used with a single resource" in err
+            # annotate
+            rc, out, _ = await _kubectl(c, "annotate", "pods", "p1", "note=hello")
+            assert out == 'pod "p1" annotated\n'
+            rc, _, err = await _kubectl(c, "annotate", "pods", "p1", "note=again")
+            assert rc == 1 and "--overwrite is false but found the following declared annotation(s): 'note' already has a value (hello)" in err
+            rc, out, _ = await _kubectl(c, "annotate", "pods", "p1", "note-")
+            assert "note" not in m.annotations_of(await c.get("pods", "p1", "default"))
+            # scale
+            await c.create({"apiVersion": "apps/v1", "kind": "ReplicaSet", "metadata": {"name": "rs"},
+                            "spec": {"replicas": 1, "selector": {"matchLabels": {"app": "rs"}},
+                                     "template": {"metadata": {"labels": {"app": "rs"}},
+                                                  "spec": {"containers": [{"name": "w", "image": "busybox", "command": ["sleep", "60"]}]}}}},
+                           "default")
+            rc, _, err = await _kubectl(c, "scale", "rs", "rs")
+            assert rc == 1 and "The --replicas=COUNT flag is required" in err
+            rc, _, err = await _kubectl(c, "scale", "rs", "rs", "--replicas", "3", "--current-replicas", "2")
+            assert rc == 1 and "Expected replicas to be 2, was 1" in err
+            rc, out, _ = await _kubectl(c, "scale", "rs", "rs", "--replicas", "3", "--current-replicas", "1", "--timeout", "30s")
+            assert rc == 0 and out == 'replicaset "rs" scaled\n'
+            st = (await c.get("replicasets", "rs", "default"))["status"]
+            assert st["replicas"] == 3
+            rc, out, _ = await _kubectl(c, "scale", "--replicas", "0", "rs/rs", "-o", "name")
+            assert out == "replicaset/rs\n"
+            rc, _, err = await _kubectl(c, "scale", "pods", "p1", "--replicas", "2")
+            assert rc == 1 and "no scaler has been implemented for" in err
+            # run: the default generators
+            rc, out, _ = await _kubectl(c, "run", "web", "--image", "busybox", "--port", "80", "--expose", "-l", "app=web",
+                                        tail=["sleep", "60"])
+            assert rc == 0 and out == 'service "web" created\ndeployment "web" created\n'
+            d = await c.get("deployments", "web", "default")
+            assert d["spec"]["template"]["spec"]["containers"][0]["args"] == ["sleep", "60"]
+            assert (await c.get("services", "web", "default"))["spec"]["selector"] == {"app": "web"}
+            rc, out, _ = await _kubectl(c, "run", "once", "--image", "busybox", "--restart", "Never", "--command", tail=["true"])
+            assert out == 'pod "once" created\n'
+            assert (await c.get("pods", "once", "default"))["spec"]["containers"][0]["command"] == ["true"]
+            rc, out, _ = await _kubectl(c, "run", "batch", "--image", "busybox", "--restart", "OnFailure", tail=["true"])
+            assert out == 'job "batch" created\n'
+            rc, out, _ = await _kubectl(c, "run", "tick", "--image", "busybox", "--schedule", "*/5 * * * *", "--restart", "OnFailure")
+            assert out == 'cronjob "tick" created\n'
+            rc, out, _ = await _kubectl(c, "run", "dry", "--image", "busybox", "--restart", "Never", "--dry-run", "-o", "json")
+            assert '"kind": "Pod"' in out and await c.get_or_none("pods", "dry", "default") is None
+            # attached, --rm, the exit code of a Never pod
+            rc, out, _ = await _kubectl(c, "run", "say", "--image", "busybox", "--restart", "Never", "--attach", "--rm",
+                                        "--command", tail=["sh", "-c", "echo said; exit 3"])
+            assert rc == 3 and "said" in out
+            for _ in range(50):
+                if await c.get_or_none("pods", "say", "default") is None:
+                    break
+                await asyncio.sleep(0.1)
+            assert await c.get_or_none("pods", "say", "default") is None
+    run(go(), 120)
