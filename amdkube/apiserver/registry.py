@@ -28,6 +28,7 @@ from ..api.scheme import SCHEME, ResourceInfo
 from ..api.validation import validate_binding
 from ..store import Filter, MVCCStore, Storage, event_object, PUT
 from ..store.storage import decode_kv
+from . import rbacescalation
 from . import admission as adm
 from .service import ServiceAllocator
 from ..api.field import go_value
@@ -272,6 +273,8 @@ class ResourceStore:
                                ri.group, dry_run=dry_run)
         self.api.admission.admit(attrs, self.api)
         SCHEME.default(obj)  # admission may add fields (e.g. ResourceV2) that need defaults
+        if ri.group == rbacescalation.GROUP:
+            rbacescalation.check(self.api, ri.plural, md.get("namespace", ""), obj, user)
         errs = SCHEME.validate(obj)
         if errs:
             raise m.invalid(ri.kind, md.get("name", ""), errs)
@@ -404,6 +407,8 @@ class ResourceStore:
                                  "the latest version and try again")
             self._prepare_update(new, cur, subresource)
             SCHEME.default(new)
+            if self.ri.group == rbacescalation.GROUP:
+                rbacescalation.check(self.api, self.ri.plural, ns, new, user, cur)
             attrs = adm.Attributes(adm.UPDATE, self.ri.plural, subresource, ns, name, new, cur, user, self.ri.kind,
                                    self.ri.group)
             self.api.admission.admit(attrs, self.api)
