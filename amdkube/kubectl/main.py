@@ -296,29 +296,8 @@ async def cmd_apply(c, a):
 
 
 async def cmd_delete(c, a):
-    targets = []
-    if a.filename:
-        for d in _read_files(a.filename):
-            ri = SCHEME.for_object(d)
-            targets.append((ri, m.name_of(d), m.namespace_of(d) or a.namespace or "default"))
-    else:
-        for r, name in _split_targets(a.args):
-            ri = SCHEME.resolve(r)
-            ns = _ns(a, ri) or ("default" if ri.namespaced else "")
-            if name:
-                targets.append((ri, name, ns))
-            elif a.all or a.selector:
-                items, _ = await c.list(ri.plural, ns, a.selector)
-                targets += [(ri, m.name_of(i), m.namespace_of(i)) for i in items]
-    for ri, name, ns in targets:
-        res = ri.plural if not ri.group else f"{ri.plural}.{ri.group}"
-        try:
-            await c.delete(res, name, ns if ri.namespaced else "", grace=a.grace_period if a.grace_period >= 0 else None,
-                           propagation="Background" if a.cascade else "Orphan")
-            print(f'{ri.kind.lower()} "{name}" deleted')
-        except m.StatusError as e:
-            if not (a.ignore_not_found and m.is_not_found(e)):
-                print(f"Error from server ({e.reason}): {e.message}", file=sys.stderr)
+    from .delete import cmd_delete as delete
+    return await delete(c, a)
 
 
 async def cmd_logs(c, a):
@@ -484,6 +463,7 @@ from . import drain as _drain  # noqa: E402
 from . import metacmds as _metacmds  # noqa: E402
 from . import scale as _scale  # noqa: E402
 from . import run as _run  # noqa: E402
+from . import delete as _delete  # noqa: E402
 COMMANDS.update(_EXTRA)
 COMMANDS.update(_more.COMMANDS)
 COMMANDS["apply"] = _more.cmd_apply       # three-way merge, --prune, *-last-applied
@@ -516,6 +496,7 @@ def parser():
         _metacmds.add_arguments(sp)
         _scale.add_arguments(sp)
         _run.add_arguments(sp)
+        _delete.add_arguments(sp)
         sp.add_argument("args", nargs="*")
         sp.add_argument("-n", "--namespace", default=argparse.SUPPRESS)
         sp.add_argument("-o", "--output", default=None)
@@ -531,7 +512,7 @@ def parser():
         sp.add_argument("--all", action="store_true")
         sp.add_argument("--grace-period", type=int, default=-1)
         sp.add_argument("--cascade", type=lambda s: s != "false", default=True)
-        sp.add_argument("--ignore-not-found", action="store_true")
+        sp.add_argument("--ignore-not-found", action="store_const", const=True, default=None)
         sp.add_argument("--ignore-daemonsets", action="store_true")
         sp.add_argument("--replicas", "-r", type=int, default=None)
         sp.add_argument("-p", "--patch", default="{}")

@@ -1160,8 +1160,9 @@ class RocShim:
 
     async def _wait(self, c: Container):
         rc = await c.proc.wait()
-        if rc and c.annotations.get("io.kubernetes.container.terminationMessagePolicy") == "FallbackToLogsOnError":
-            await c.proc.logs_flushed(0.5)   # the termination-message fallback reads the log's tail
+        # the exit is reported once the log holds everything the container wrote (as containerd
+        # waits for the IO copy): `logs` right after, and the termination-message fallback, see it all
+        await c.proc.logs_flushed(0.5)
         # written by the checkpoint thread, ordered before the container's checkpoint and any
         # later removal of the same file
         self.ckpt.put(os.path.join(self.state_dir, "containers", c.id + ".exit"), str(rc).encode())

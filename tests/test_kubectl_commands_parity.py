@@ -454,3 +454,48 @@ def test_commands_through_the_cluster():
                 await asyncio.sleep(0.1)
             assert await c.get_or_none("pods", "say", "default") is None
     run(go(), 120)
+
+
+def test_delete_through_the_cluster():
+    from amdkube.kubectl import delete as D
+    from amdkube.localcluster import LocalCluster, wait_pod
+
+    async def go():
+        async with LocalCluster(gpus="none", relist_period=0.2) as lc:
+            c = lc.client
+            for n in ("a1", "a2", "b1"):
+                await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": n, "labels": {"g": n[0]}},
+                                "spec": {"terminationGracePeriodSeconds": 2,
+                                         "containers": [{"name": "c", "image": "busybox", "command": ["sleep", "60"]}]}}, "default")
+            rc, _, err = await _kubectl(c, "delete")
+            assert rc == 1 and "You must provide one or more resources by argument or filename." in err
+            rc, _, err = await _kubectl(c, "delete", "pods")
+            assert rc == 1 and "resource(s) were provided, but no name, label selector, or --all flag specified" in err
+            rc, out, err = await _kubectl(c, "delete", "pod", "nope")
+            assert rc == 1 and 'Error from server (NotFound): pods "nope" not found' in err
+            rc, out, err = await _kubectl(c, "delete", "pod", "nope", "--ignore-not-found")
+            assert rc == 0 and out == "No resources found\n" and err == ""
+            rc, _, err = await _kubectl(c, "delete", "pod", "a1", "--now", "--grace-period", "5")
+            assert rc == 1 and "--now and --grace-period cannot be specified together" in err
+            rc, out, _ = await _kubectl(c, "delete", "pods", "-l", "g=a", "-o", "name")
+            assert sorted(out.split()) == ["pod/a1", "pod/a2"]
+            rc, out, err = await _kubectl(c, "delete", "pod", "b1", "--grace-period", "0", "--force")
+            assert rc == 0 and D.IMMEDIATE_WARNING in err and out == 'pod "b1" deleted\n'
+            # a workload: its pods are gone when the command returns
+            await c.create({"apiVersion": "apps/v1", "kind": "ReplicaSet", "metadata": {"name": "rs"},
+                            "spec": {"replicas": 2, "selector": {"matchLabels": {"app": "rs"}},
+                                     "template": {"metadata": {"labels": {"app": "rs"}},
+                                                  "spec": {"terminationGracePeriodSeconds": 1, "containers": [
+                                                      {"name": "w", "image": "busybox", "command": ["sleep", "60"]}]}}}},
+                           "default")
+            for _ in range(100):
+                if len((await c.list("pods", "default", "app=rs"))[0]) == 2:
+                    break
+                await asyncio.sleep(0.1)
+            rc, out, _ = await _kubectl(c, "delete", "rs", "rs")
+            assert rc == 0 and out == 'replicaset "rs" deleted\n'
+            assert (await c.list("pods", "default", "app=rs"))[0] == []
+            assert await c.get_or_none("replicasets", "rs", "default") is None
+            rc, out, _ = await _kubectl(c, "delete", "pods", "--all")
+            assert rc == 0
+    run(go(), 120)
