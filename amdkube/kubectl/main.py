@@ -200,35 +200,8 @@ def _split_targets(args):
 
 
 async def cmd_get(c, a):
-    targets = _split_targets(a.args)
-    if not targets:
-        raise SystemExit("error: you must specify the type of resource to get")
-    for r, name in targets:
-        ri = SCHEME.resolve(r)
-        if ri is None:
-            try:
-                await c.discover()
-            except Exception:
-                pass
-            ri = SCHEME.resolve(r)
-        if ri is None:
-            raise SystemExit(f'error: the server doesn\'t have a resource type "{r}"')
-        ns = _ns(a, ri)
-        res = ri.plural if not ri.group else f"{ri.plural}.{ri.group}"
-        if name:
-            obj = await c.get(res, name, ns)
-            obj.setdefault("kind", ri.kind)
-            obj.setdefault("apiVersion", ri.api_version)
-            _emit([obj], a, ri.kind, single=True)
-        else:
-            items, rv = await c.list(res, ns, a.selector, a.field_selector)
-            for it in items:
-                it.setdefault("kind", ri.kind)
-                it.setdefault("apiVersion", ri.api_version)
-            _emit(items, a, ri.kind)
-            if a.watch:
-                async for typ, obj in c.watch(res, ns, rv, a.selector, a.field_selector):
-                    _emit([obj], a, ri.kind, with_headers=False)
+    from .get import cmd_get as get
+    return await get(c, a)
 
 
 async def cmd_describe(c, a):

@@ -642,8 +642,9 @@ def label_headers(label_columns) -> list[str]:
 
 
 def print_table(objs, kind: str, wide: bool = False, with_namespace: bool = False, show_labels: bool = False,
-                label_columns=(), no_headers: bool = False, with_kind: bool = False) -> str:
-    """printRowsForHandlerEntry + printRows: the aligned table of one kind."""
+                label_columns=(), no_headers: bool = False, with_kind: bool | str = False) -> str:
+    """printRowsForHandlerEntry + printRows: the aligned table of one kind; `with_kind` prefixes
+    each name with that resource name (True: the kind, lower-cased)."""
     rows = []
     if not no_headers:
         head = columns_for(kind, wide) + label_headers(label_columns) + (["LABELS"] if show_labels else [])
@@ -651,7 +652,7 @@ def print_table(objs, kind: str, wide: bool = False, with_namespace: bool = Fals
     for o in objs:
         cells = rows_for(o, kind, wide)
         if with_kind:
-            cells[0] = f"{kind.lower()}/{cells[0]}"
+            cells[0] = f"{with_kind if isinstance(with_kind, str) else kind.lower()}/{cells[0]}"
         labels = m.labels_of(o)
         cells += [labels.get(c, "") for c in label_columns or []]
         if show_labels:

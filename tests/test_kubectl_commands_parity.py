@@ -499,3 +499,47 @@ def test_delete_through_the_cluster():
             rc, out, _ = await _kubectl(c, "delete", "pods", "--all")
             assert rc == 0
     run(go(), 120)
+
+
+def test_get_through_the_cluster(tmp_path):
+    from amdkube.localcluster import LocalCluster
+
+    async def go():
+        async with LocalCluster(gpus="none", relist_period=0.2, with_kubelet=False) as lc:
+            c = lc.client
+            await c.create({"apiVersion": "v1", "kind": "Service", "metadata": {"name": "s1"}, "spec": {"ports": [{"port": 80}]}},
+                           "default")
+            await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p1"},
+                            "spec": {"containers": [{"name": "c", "image": "busybox"}]}}, "default")
+            done = await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "done"},
+                                   "spec": {"containers": [{"name": "c", "image": "busybox"}]}}, "default")
+            done["status"] = {"phase": "Succeeded"}
+            await c.update_status(done)
+            # several types: a table each, names with the short form, a blank line between (stderr)
+            rc, out, err = await _kubectl(c, "get", "pods,svc")
+            lines = out.splitlines()
+            assert rc == 0 and any(x.startswith("po/p1 ") for x in lines) and any(x.startswith("svc/s1 ") for x in lines)
+            assert not any(x.startswith("po/done") for x in lines)               # finished pods hidden from lists
+            rc, out, _ = await _kubectl(c, "get", "pods", "-a")
+            assert "done" in out
+            rc, out, _ = await _kubectl(c, "get", "pods", "done")                  # named: never hidden
+            assert "done" in out
+            rc, out, err = await _kubectl(c, "get", "all")
+            assert "svc/kubernetes" in out and "po/p1" in out
+            # NotFound does not stop the others, and is reported after them
+            rc, out, err = await _kubectl(c, "get", "pods", "p1", "nope")
+            assert rc == 1 and "p1" in out and 'Error from server (NotFound): pods "nope" not found' in err
+            rc, out, err = await _kubectl(c, "get", "pods", "nope", "--ignore-not-found")
+            assert rc == 0 and out == "" and err == ""
+            rc, out, err = await _kubectl(c, "get", "pods", "-l", "none=here")
+            assert rc == 0 and err.strip() == "No resources found."
+            # generic printers: one object when one was named, a List otherwise
+            rc, out, _ = await _kubectl(c, "get", "svc", "s1", "-o", "json")
+            assert '"kind": "Service"' in out and '"kind": "List"' not in out
+            rc, out, _ = await _kubectl(c, "get", "svc/s1", "pod/p1", "-o", "name")
+            assert out.split() == ["service/s1", "pod/p1"]
+            f = tmp_path / "s.yaml"
+            f.write_text("apiVersion: v1\nkind: Service\nmetadata: {name: s1}\nspec: {ports: [{port: 80}]}\n")
+            rc, out, _ = await _kubectl(c, "get", "-f", str(f))
+            assert rc == 0 and out.splitlines()[1].startswith("s1 ")
+    run(go(), 60)
