@@ -18,6 +18,7 @@ import sys
 import time
 
 from ..api import meta as m
+from ..runtime import spdy
 from ..api.scheme import SCHEME, dump_yaml, load_manifests
 from ..client import Client
 from . import printers
@@ -156,6 +157,22 @@ def _read_files(paths, recursive: bool = False) -> list[dict]:
             with open(fp) as f:
                 docs += load_manifests(f.read())
     return docs
+
+
+def standard_error_message(e: m.StatusError) -> str:
+    """cmdutil checkErr (helpers.go:124-170) for API errors: an Invalid error lists its causes
+    ("The Pod "x" is invalid: ..." — one per line after "* " when there are several), any other
+    is `Error from server (<Reason>): <message>`."""
+    d = e.details or {}
+    if e.code == 422 and e.reason == "Invalid" and d.get("kind"):
+        head = f'The {d.get("kind")} "{d.get("name", "")}" is invalid'
+        causes = [(c.get("field") + ": " if c.get("field") else "") + c.get("message", "") for c in d.get("causes") or []]
+        if not causes:
+            return head
+        if len(causes) == 1:
+            return f"{head}: {causes[0]}"
+        return f"{head}: \n" + "\n".join(f"* {c}" for c in causes)
+    return f"Error from server ({e.reason}): {e.message}"
 
 
 def parse_duration_flag(s: str) -> float:
@@ -593,9 +610,17 @@ def main(argv=None):
                     for msg in bad:
                         print(f"error: {msg}", file=sys.stderr)
                     return 1
-            return await COMMANDS[a.cmd](c, a)
+            rc = await COMMANDS[a.cmd](c, a)
+            if a.cmd == "exec" and isinstance(rc, int) and rc > 0:
+                # remotecommand v4: a non-zero exit is an ExitError, printed by checkErr
+                print(f"command terminated with exit code {rc}", file=sys.stderr)
+            return rc
         except m.StatusError as e:
-            print(f"Error from server ({e.reason}): {e.message}", file=sys.stderr)
+            print(standard_error_message(e), file=sys.stderr)
+            return 1
+        except spdy.UpgradeRefused as e:
+            se = e.status_error()
+            print(standard_error_message(se) if se is not None else f"error: {e}", file=sys.stderr)
             return 1
         finally:
             await c.close()

@@ -108,6 +108,24 @@ class SpdyError(Exception):
     pass
 
 
+class UpgradeRefused(SpdyError):
+    """The server answered the upgrade with an error (its body: a metav1.Status, usually)."""
+
+    def __init__(self, status: int, body: str):
+        super().__init__(f"upgrade refused: {status}: {body}")
+        self.status_code, self.body = status, body
+
+    def status_error(self):
+        """The API error the body carries (meta.StatusError), or None."""
+        import json
+        from ..api import meta as m
+        try:
+            st = json.loads(self.body)
+        except ValueError:
+            return None
+        return m.StatusError.from_status(st) if isinstance(st, dict) and st.get("kind") == "Status" else None
+
+
 class Stream:
     """One SPDY stream: a byte pipe with half-close (FIN) in each direction."""
 
@@ -464,7 +482,7 @@ async def connect(url: str, protocols, headers: dict | None = None, ssl=None, me
     status, rh, body = await _response_head(reader)
     if status != 101:
         writer.close()
-        raise SpdyError(f"upgrade refused: {status}: {body.decode(errors='replace').strip()}")
+        raise UpgradeRefused(status, body.decode(errors="replace").strip())
     proto = next((v for k, v in rh if k.lower() == PROTOCOL_HEADER.lower()), "")
     sess = Session(server=False, on_stream=on_stream)
     sess.attach(writer.write, writer.drain, writer.close)

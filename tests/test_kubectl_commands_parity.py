@@ -543,3 +543,34 @@ def test_get_through_the_cluster(tmp_path):
             rc, out, _ = await _kubectl(c, "get", "-f", str(f))
             assert rc == 0 and out.splitlines()[1].startswith("s1 ")
     run(go(), 60)
+
+
+def test_standard_error_message():
+    from amdkube.kubectl.main import standard_error_message
+    one = m.StatusError(422, "Invalid", 'Pod "x" is invalid: spec.containers[0].image: Required value',
+                        {"kind": "Pod", "name": "x", "causes": [{"message": "spec.containers[0].image: Required value"}]})
+    assert standard_error_message(one) == 'The Pod "x" is invalid: spec.containers[0].image: Required value'
+    two = m.StatusError(422, "Invalid", "...", {"kind": "Pod", "name": "x", "causes": [{"message": "a: Required value"},
+                                                                                     {"field": "b", "message": "Invalid value: 1"}]})
+    assert standard_error_message(two) == 'The Pod "x" is invalid: \n* a: Required value\n* b: Invalid value: 1'
+    assert standard_error_message(m.not_found("pods", "nope")) == 'Error from server (NotFound): pods "nope" not found'
+
+
+def test_exec_exit_code_and_refusal(capfd):
+    from amdkube.kubectl import main as km
+    from amdkube.localcluster import LocalCluster, wait_pod
+
+    async def go():
+        async with LocalCluster(gpus="none", relist_period=0.2) as lc:
+            c = lc.client
+            await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p"},
+                            "spec": {"containers": [{"name": "c", "image": "busybox", "command": ["sleep", "60"]}]}}, "default")
+            await wait_pod(c, "default", "p", ("Running",), 30)
+            base = ["-s", lc.api.url, "--token", lc.api.loopback_token, "exec"]
+            rc = await asyncio.to_thread(km.main, base + ["p", "--", "sh", "-c", "echo out; exit 3"])
+            rc2 = await asyncio.to_thread(km.main, base + ["nope", "--", "true"])
+            return rc, rc2
+    rc, rc2 = run(go(), 90)
+    err = capfd.readouterr().err
+    assert rc == 3 and "command terminated with exit code 3" in err
+    assert rc2 == 1 and 'Error from server (NotFound): pods "nope" not found' in err
