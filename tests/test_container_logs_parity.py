@@ -355,3 +355,19 @@ def test_kubectl_logs_through_the_cluster():
             rc, sel_out, _ = await _kubectl(c, "logs", "-l", "app=crash")
             assert rc == 0 and "start " in sel_out
     run(go(), 120)
+
+
+def test_container_is_killed_when_its_log_pump_cannot_start(tmp_path, monkeypatch):
+    from amdkube.runtime import rocshim as R
+    marker = tmp_path / "ran"
+
+    def broken(*a, **k):
+        raise OSError("no pump")
+    monkeypatch.setattr(R, "_spawn_pump", broken)
+
+    async def go():
+        with pytest.raises(OSError, match="no pump"):
+            await R.spawn(["sh", "-c", f"sleep 0.5; touch {marker}"], log_path=str(tmp_path / "0.log"), log_pump=True)
+        await asyncio.sleep(1.0)
+        assert not marker.exists()
+    run(go())
