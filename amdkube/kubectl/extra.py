@@ -907,7 +907,7 @@ def add_arguments(sp):
     sp.add_argument("--port", default=None)
     sp.add_argument("--target-port", default=None)
     sp.add_argument("--name", default=None)
-    sp.add_argument("--protocol", default="TCP")
+    sp.add_argument("--protocol", default=None)
     sp.add_argument("--min", type=int, default=0)
     sp.add_argument("--max", type=int, default=1)
     sp.add_argument("--cpu-percent", type=int, default=-1)

@@ -454,12 +454,14 @@ from . import metacmds as _metacmds  # noqa: E402
 from . import scale as _scale  # noqa: E402
 from . import run as _run  # noqa: E402
 from . import delete as _delete  # noqa: E402
+from . import expose as _expose  # noqa: E402
 COMMANDS.update(_EXTRA)
 COMMANDS.update(_more.COMMANDS)
 COMMANDS["apply"] = _more.cmd_apply       # three-way merge, --prune, *-last-applied
 COMMANDS["set"] = _more.cmd_set           # env/image/resources/selector/serviceaccount/subject
 from .diff import cmd_alpha  # noqa: E402
 COMMANDS["alpha"] = cmd_alpha             # alpha diff LOCAL|LIVE|LAST|MERGED
+COMMANDS["expose"] = _expose.cmd_expose   # service/v2 generator
 
 
 _RESOURCE_CMDS = {"get", "describe", "delete", "label", "annotate", "scale", "patch", "wait", "edit", "explain", "expose",
@@ -487,6 +489,7 @@ def parser():
         _scale.add_arguments(sp)
         _run.add_arguments(sp)
         _delete.add_arguments(sp)
+        _expose.add_arguments(sp)
         sp.add_argument("args", nargs="*")
         sp.add_argument("-n", "--namespace", default=argparse.SUPPRESS)
         sp.add_argument("-o", "--output", default=None)
@@ -573,6 +576,7 @@ def main(argv=None):
         i = argv.index("--")
         argv, cmd_tail = argv[:i], argv[i + 1:]
     argv = _logs.rewrite_short_flags(argv)
+    argv = _expose.rewrite_flags(argv)
     command_flag = "--command" in argv
     p = parser()
     a, extra = p.parse_known_args(argv)

@@ -77,7 +77,7 @@ def test_label_func(labels, overwrite, version, new, remove, expected, err):
 
 def _args(*argv):
     from amdkube.kubectl import main as km
-    argv = km._logs.rewrite_short_flags(list(argv))
+    argv = km._expose.rewrite_flags(km._logs.rewrite_short_flags(list(argv)))
     a, extra = km.parser().parse_known_args(argv)
     a.args = list(a.args) + extra
     a.command_flag = "--command" in argv
@@ -574,3 +574,61 @@ def test_exec_exit_code_and_refusal(capfd):
     err = capfd.readouterr().err
     assert rc == 3 and "command terminated with exit code 3" in err
     assert rc2 == 1 and 'Error from server (NotFound): pods "nope" not found' in err
+
+
+def test_expose_through_the_cluster():
+    """expose_test.go TestRunExposeService's cases (services, selector/labels/name flags,
+    affinity, cluster IP, headless with and without a port, name truncation, multi-port and
+    multi-protocol objects), against a live apiserver."""
+    from amdkube.localcluster import LocalCluster
+
+    async def go():
+        async with LocalCluster(gpus="none", with_kubelet=False, with_controllers=False) as lc:
+            c = lc.client
+            await c.create({"apiVersion": "v1", "kind": "Service", "metadata": {"name": "baz"},
+                            "spec": {"selector": {"app": "go"}, "ports": [{"port": 1}]}}, "default")
+
+            async def expose(*args):
+                rc, out, err = await _kubectl(c, "expose", *args)
+                return rc, out, err
+            rc, out, _ = await expose("service", "baz", "--protocol", "UDP", "--port", "14", "--name", "foo", "--labels", "svc=test")
+            assert rc == 0 and out == 'service "foo" exposed\n'
+            svc = await c.get("services", "foo", "default")
+            assert svc["metadata"]["labels"] == {"svc": "test"} and svc["spec"]["selector"] == {"app": "go"}
+            assert svc["spec"]["ports"] == [{"protocol": "UDP", "port": 14, "targetPort": 14}]
+            rc, out, _ = await expose("service", "baz", "--selector", "func=stream", "--port", "14", "--name", "foo2",
+                                      "-l", "svc=test", "--type", "LoadBalancer", "--session-affinity", "ClientIP")
+            s2 = await c.get("services", "foo2", "default")
+            assert s2["spec"]["selector"] == {"func": "stream"} and s2["spec"]["type"] == "LoadBalancer"
+            assert s2["spec"]["sessionAffinity"] == "ClientIP" and s2["spec"]["ports"][0]["protocol"] == "TCP"
+            rc, out, _ = await expose("service", "baz", "--port", "14", "--name", "hl", "--cluster-ip", "None")
+            assert (await c.get("services", "hl", "default"))["spec"]["clusterIP"] == "None"
+            await c.create({"apiVersion": "v1", "kind": "Service", "metadata": {"name": "hsrc"},
+                            "spec": {"selector": {"app": "go"}, "clusterIP": "None"}}, "default")
+            rc, out, _ = await expose("service", "hsrc", "--name", "hl2", "--cluster-ip", "None", "--dry-run", "-o", "json")
+            assert '"ports": []' in out and '"clusterIP": "None"' in out
+            # a pod: its labels select it, its long name is cut to 63 characters
+            long = "a-name-that-is-toooo-big-for-a-service-because-it-can-only-handle-63-characters"
+            await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": long, "labels": {"svc": "frompod"}},
+                            "spec": {"containers": [{"name": "c", "image": "busybox",
+                                                     "ports": [{"containerPort": 90}, {"containerPort": 53, "protocol": "UDP"}]}]}},
+                           "default")
+            rc, out, _ = await expose("pod", long)
+            assert out == f'service "{long[:63]}" exposed\n'
+            sp = await c.get("services", long[:63], "default")
+            assert sp["spec"]["ports"] == [{"name": "port-1", "protocol": "TCP", "port": 90, "targetPort": 90},
+                                           {"name": "port-2", "protocol": "UDP", "port": 53, "targetPort": 53}]
+            assert sp["metadata"]["labels"] == {"svc": "frompod"}
+            # a deployment with matchExpressions cannot be exposed; unexposable kinds are refused
+            await c.create({"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": "d"},
+                            "spec": {"selector": {"matchLabels": {"a": "b"}, "matchExpressions": [{"key": "x", "operator": "Exists"}]},
+                                     "template": {"metadata": {"labels": {"a": "b", "x": "1"}},
+                                                  "spec": {"containers": [{"name": "c", "image": "busybox"}]}}}}, "default")
+            rc, _, err = await expose("deployment", "d", "--port", "80")
+            assert rc == 1 and "couldn't retrieve selectors via --selector flag or introspection" in err
+            await c.create({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "cm"}, "data": {}}, "default")
+            rc, _, err = await expose("configmap", "cm", "--port", "80")
+            assert rc == 1 and "cannot expose a { ConfigMap}" in err
+            rc, _, err = await expose("service", "baz", "--name", "noport", "--selector", "a=b", "--port", "", "--target-port", "x")
+            assert rc == 0
+    run(go(), 60)

@@ -209,7 +209,7 @@ def test_kubectl_generators_expose_autoscale_taint_auth_certs_explain(tmp_path, 
     from tests.conftest import run
     run(go(), 90)
     out = capsys.readouterr().out
-    assert "KIND:     Deployment" in out and "service/api exposed" in out
+    assert "KIND:     Deployment" in out and 'service "api" exposed' in out
     # kubeconfig editing works offline
     kc = tmp_path / "config"
     kc.write_text(yaml.safe_dump({"apiVersion": "v1", "kind": "Config", "current-context": "a",
