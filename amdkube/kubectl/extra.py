@@ -281,48 +281,6 @@ async def cmd_autoscale(c, a):
     print(f"horizontalpodautoscaler.autoscaling/{m.name_of(out)} autoscaled")
 
 
-def parse_taint(spec: str):
-    """`key=value:Effect` adds, `key:Effect-` / `key-` removes (taint.go parseTaints)."""
-    if spec.endswith("-"):
-        body = spec[:-1]
-        key, _, effect = body.partition(":")
-        return "remove", {"key": key, **({"effect": effect} if effect else {})}
-    kv, sep, effect = spec.partition(":")
-    if not sep or effect not in ("NoSchedule", "PreferNoSchedule", "NoExecute"):
-        raise SystemExit(f"error: invalid taint spec: {spec}")
-    key, _, value = kv.partition("=")
-    t = {"key": key, "effect": effect}
-    if value:
-        t["value"] = value
-    return "add", t
-
-
-async def cmd_taint(c, a):
-    if len(a.args) < 2:
-        raise SystemExit("error: taint NODE KEY[=VALUE]:EFFECT ...")
-    names = [x.split("/", 1)[-1] for x in a.args[:1]]
-    if a.args[0] in ("node", "nodes", "no"):
-        names, specs = [a.args[1]], a.args[2:]
-    else:
-        specs = a.args[1:]
-    for n in names:
-        node = await c.get("nodes", n)
-        taints = list((node.get("spec") or {}).get("taints") or [])
-        for sp in specs:
-            op, t = parse_taint(sp)
-            same = [x for x in taints if x["key"] == t["key"] and ("effect" not in t or x.get("effect") == t["effect"])]
-            if op == "remove":
-                if not same:
-                    raise SystemExit(f"error: taint {t['key']!r} not found")
-                taints = [x for x in taints if x not in same]
-            else:
-                if same and not a.overwrite:
-                    raise SystemExit(f"error: node {n} already has {t['key']} taint(s) with same effect(s) and --overwrite is false")
-                taints = [x for x in taints if x not in same] + [t]
-        await c.patch("nodes", n, {"spec": {"taints": taints or None}})
-        print(f"node/{n} tainted" if any(parse_taint(s)[0] == "add" for s in specs) else f"node/{n} untainted")
-
-
 async def cmd_set(c, a):
     if not a.args or a.args[0] != "image":
         raise SystemExit("error: supported: set image RESOURCE/NAME CONTAINER=IMAGE ...")
@@ -895,7 +853,7 @@ async def cmd_create_generator(c, a) -> bool:
     return True
 
 
-COMMANDS = {"rollout": cmd_rollout, "expose": cmd_expose, "autoscale": cmd_autoscale, "taint": cmd_taint, "set": cmd_set,
+COMMANDS = {"rollout": cmd_rollout, "expose": cmd_expose, "autoscale": cmd_autoscale, "set": cmd_set,
             "replace": cmd_replace, "edit": cmd_edit, "auth": cmd_auth, "certificate": cmd_certificate,
             "port-forward": cmd_port_forward, "proxy": cmd_proxy, "cp": cmd_cp, "explain": cmd_explain}
 
@@ -931,7 +889,7 @@ def add_arguments(sp):
     sp.add_argument("--role", default=None)
 
 
-__all__ = ["COMMANDS", "add_arguments", "cmd_config_sync", "cmd_create_generator", "parse_taint", "port_forward", "sys"]
+__all__ = ["COMMANDS", "add_arguments", "cmd_config_sync", "cmd_create_generator", "port_forward", "sys"]
 
 
 def _timeout_of(a, default: float = 30.0) -> float:

@@ -13,7 +13,8 @@ import yaml
 
 from amdkube.api import meta as m
 from amdkube.controllers.deployment import resolve_fenceposts as _fenceposts
-from amdkube.kubectl.extra import cmd_config_sync, parse_taint
+from amdkube.kubectl.extra import cmd_config_sync
+from amdkube.kubectl.taint import parse_taints
 from amdkube.kubectl.main import COMMANDS, parser
 from amdkube.localcluster import LocalCluster
 from tests.test_controllers import until
@@ -47,8 +48,8 @@ def test_fenceposts():
     assert resolve_fenceposts(d(1, "25%", "25%")) == (1, 0)
     assert resolve_fenceposts(d(5, 0, 0)) == (0, 1)
     assert resolve_fenceposts({"spec": {"replicas": 4}}) == (1, 1)
-    assert parse_taint("gpu=mi355x:NoSchedule") == ("add", {"key": "gpu", "value": "mi355x", "effect": "NoSchedule"})
-    assert parse_taint("gpu:NoSchedule-") == ("remove", {"key": "gpu", "effect": "NoSchedule"})
+    assert parse_taints(["gpu=mi355x:NoSchedule"]) == ([{"key": "gpu", "value": "mi355x", "effect": "NoSchedule"}], [])
+    assert parse_taints(["gpu:NoSchedule-"]) == ([], [{"key": "gpu", "effect": "NoSchedule"}])
 
 
 def test_rolling_update_bounds_history_undo_pause():
