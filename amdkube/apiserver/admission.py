@@ -54,6 +54,138 @@ class Plugin:
         pass
 
 
+def _resource_str(a) -> str:
+    """schema.GroupResource.String(): `pods`, `deployments.extensions`."""
+    return f"{a.resource}.{a.group}" if getattr(a, "group", "") else a.resource
+
+
+def new_forbidden(a, err) -> m.StatusError:
+    """admission.NewForbidden (apiserver/pkg/admission/errors.go): `<resource> "<name>" is
+    forbidden: <err>`, the name from the request, else the object's name or generateName, else
+    "Unknown"; a Forbidden error passes through unwrapped."""
+    if isinstance(err, m.StatusError):
+        if err.code == 403:
+            return err
+        err = err.message
+    name = a.name
+    if not name:
+        md = ((a.obj or {}).get("metadata") or {}) if isinstance(a.obj, dict) else {}
+        name = md.get("name") or md.get("generateName") or "Unknown"
+    return m.forbidden(f'{_resource_str(a)} "{name}" is forbidden: {err}')
+
+
+def forbidden_for(resource: str, name: str, err: str) -> m.StatusError:
+    """errors.NewForbidden(qualifiedResource, name, err)."""
+    return m.forbidden(f'{resource} "{name}" is forbidden: {err}')
+
+
+def unknown_error(msg: str) -> m.StatusError:
+    """A plain Go error returned by a plugin: the handler answers 500 with reason Unknown
+    (responsewriters.ErrorToAPIStatus)."""
+    return m.StatusError(500, "", msg)
+
+
+def internal_error_message(msg: str) -> str:
+    """errors.NewInternalError(err).Error()."""
+    return f"Internal error occurred: {msg}"
+
+
+def is_initialized(obj) -> bool:
+    ini = ((obj or {}).get("metadata") or {}).get("initializers")
+    return ini is None or not ini.get("pending")
+
+
+def is_updating_initialized(a) -> bool:
+    """kubeapiserver/admission/util IsUpdatingInitializedObject."""
+    return a.operation == UPDATE and is_initialized(a.old)
+
+
+def is_updating_uninitialized(a) -> bool:
+    return a.operation == UPDATE and not is_initialized(a.old)
+
+
+# ------------------------------------------------------- toleration helpers
+def _tol(t, k):
+    v = t.get(k)
+    return "" if v is None and k != "tolerationSeconds" else v
+
+
+def match_toleration(a: dict, b: dict) -> bool:
+    """core Toleration.MatchToleration: key, effect, operator and value equal."""
+    return all(_tol(a, k) == _tol(b, k) for k in ("key", "effect", "operator", "value"))
+
+
+def tolerations_equal(a: dict, b: dict) -> bool:
+    """pkg/util/tolerations AreEqual (tolerationSeconds included)."""
+    return match_toleration(a, b) and a.get("tolerationSeconds") == b.get("tolerationSeconds")
+
+
+def add_or_update_toleration(spec: dict, tol: dict) -> bool:
+    """helper.AddOrUpdateTolerationInPod: a matching toleration is replaced (nothing happens when
+    it is identical), otherwise the new one is appended."""
+    out, updated = [], False
+    for t in spec.get("tolerations") or []:
+        if match_toleration(tol, t):
+            if tolerations_equal(tol, t):
+                return False
+            out.append(dict(tol))
+            updated = True
+            continue
+        out.append(t)
+    if not updated:
+        out.append(dict(tol))
+    spec["tolerations"] = out
+    return True
+
+
+def _tol_map(ts) -> dict:
+    """ConvertTolerationToAMap: keyed by (key, effect), the last one wins."""
+    return {(_tol(t, "key"), _tol(t, "effect")): t for t in ts or []}
+
+
+def tolerations_conflict(first, second) -> bool:
+    """IsConflict: a (key, effect) present in both with another definition."""
+    b = _tol_map(second)
+    return any(k in b and not tolerations_equal(v, b[k]) for k, v in _tol_map(first).items())
+
+
+def merge_tolerations(first, second) -> list:
+    """MergeTolerations: `second`, then the tolerations of `first` whose (key, effect) it lacks."""
+    b = _tol_map(second)
+    return list(second or []) + [v for k, v in _tol_map(first).items() if k not in b]
+
+
+def verify_against_whitelist(tolerations, whitelist) -> bool:
+    if not whitelist:
+        return True
+    w = _tol_map(whitelist)
+    return all(k in w and tolerations_equal(v, w[k]) for k, v in _tol_map(tolerations).items())
+
+
+def convert_selector_to_labels_map(s: str) -> dict:
+    """labels.ConvertSelectorToLabelsMap: `k=v, k2=v2` (spaces trimmed), keys and values
+    validated as label keys and values."""
+    from ..api.labels import is_qualified_name, is_valid_label_value
+    out = {}
+    if not s:
+        return out
+    for term in s.split(","):
+        kv = term.strip().split("=")
+        if len(kv) != 2:
+            raise ValueError(f"invalid selector: {s}")
+        k, v = kv[0].strip(), kv[1].strip()
+        if is_qualified_name(k):
+            raise ValueError(f"invalid label key {k!r}: {'; '.join(is_qualified_name(k))}")
+        if is_valid_label_value(v):
+            raise ValueError(f"invalid label value: {v!r}: {'; '.join(is_valid_label_value(v))}")
+        out[k] = v
+    return out
+
+
+def labels_conflict(a: dict, b: dict) -> bool:
+    return any(k in b and b[k] != v for k, v in a.items())
+
+
 # MI355X partition resources advertised by the AMD plugin's "mixed" naming strategy
 PARTITION_RESOURCES = tuple(f"amd.com/{cp}_{mp}" for cp in ("spx", "dpx", "qpx", "cpx") for mp in ("nps1", "nps2"))
 
@@ -97,6 +229,10 @@ class ResourceV2(Plugin):
 
 
 class ExtendedResourceToleration(Plugin):
+    """extendedresourcetoleration/admission.go Admit: every extended resource a container or
+    init container asks for gets a `<name>:Exists:NoSchedule` toleration, in sorted order, through
+    AddOrUpdateTolerationInPod. amdkube also reads limits (the request defaults to the limit) and
+    the fork's pod-level extendedResources, which ResourceV2 writes before this plugin runs."""
     name = "ExtendedResourceToleration"
 
     def admit(self, a, ctx):
@@ -113,34 +249,36 @@ class ExtendedResourceToleration(Plugin):
                 names.add(pod_extended_resource_name(pres))
             except ExtendedResourceError:
                 pass
-        tols = spec.get("tolerations") or []
         for n in sorted(names):
-            if not any(t.get("key") == n and t.get("operator") == "Exists" and t.get("effect") in ("NoSchedule", None, "") for t in tols):
-                tols.append({"key": n, "operator": "Exists", "effect": "NoSchedule"})
-        if tols:
-            spec["tolerations"] = tols
+            add_or_update_toleration(spec, {"key": n, "operator": "Exists", "effect": "NoSchedule"})
 
 
 class NamespaceLifecycle(Plugin):
-    """Reject creation in missing/terminating namespaces; protect system namespaces."""
+    """apiserver/pkg/admission/plugin/namespace/lifecycle Admit: immortal namespaces cannot be
+    deleted ("this namespace may not be deleted"); namespaced writes other than deletes (access
+    reviews aside) need the namespace to exist (NotFound), and creations are refused while it is
+    Terminating ("unable to create new content in namespace X because it is being
+    terminated.")."""
     name = "NamespaceLifecycle"
     operations = (CREATE, UPDATE, DELETE)
     immortal = ("default", "kube-system", "kube-public")
+    ACCESS_REVIEWS = ("localsubjectaccessreviews", "subjectaccessreviews")
 
     def validate(self, a, ctx):
-        if a.resource == "namespaces":
+        if a.resource == "namespaces" and not a.subresource:
             if a.operation == DELETE and a.name in self.immortal:
-                raise m.forbidden(f'namespace "{a.name}" is protected and cannot be deleted')
+                raise forbidden_for("namespaces", a.name, "this namespace may not be deleted")
             return
-        if not a.namespace or a.operation != CREATE:
+        if not a.namespace or a.operation == DELETE:
             return
-        if a.resource in ("events",) or a.subresource:
+        if a.resource in self.ACCESS_REVIEWS and getattr(a, "group", "") in ("", "authorization.k8s.io"):
             return
         ns = ctx.get_namespace(a.namespace)
         if ns is None:
             raise m.not_found("namespaces", a.namespace)
-        if (ns.get("status") or {}).get("phase") == "Terminating":
-            raise m.forbidden(f'unable to create new content in namespace {a.namespace} because it is being terminated')
+        if a.operation == CREATE and (ns.get("status") or {}).get("phase") == "Terminating":
+            raise new_forbidden(a, f"unable to create new content in namespace {a.namespace} because it is being "
+                                   f"terminated.")
 
 
 class NamespaceAutoProvision(Plugin):
@@ -280,20 +418,36 @@ class ServiceAccount(Plugin):
             volumes.append({"name": vol_name, "secret": {"secretName": token}})
 
 
-class DefaultTolerationSeconds(Plugin):
-    name = "DefaultTolerationSeconds"
-    operations = (CREATE,)
+NOT_READY_TAINT_KEY = "node.kubernetes.io/not-ready"
+UNREACHABLE_TAINT_KEY = "node.kubernetes.io/unreachable"
 
-    def __init__(self, seconds=300):
-        self.seconds = seconds
+
+class DefaultTolerationSeconds(Plugin):
+    """defaulttolerationseconds/admission.go Admit (create and update): a pod that does not
+    already tolerate node.kubernetes.io/not-ready:NoExecute (or unreachable) — a toleration with
+    that key or no key, and NoExecute or no effect — gets `Exists:NoExecute` for
+    --default-not-ready-toleration-seconds / --default-unreachable-toleration-seconds (300)."""
+    name = "DefaultTolerationSeconds"
+
+    def __init__(self, seconds=300, not_ready_seconds=None, unreachable_seconds=None):
+        self.not_ready = seconds if not_ready_seconds is None else not_ready_seconds
+        self.unreachable = seconds if unreachable_seconds is None else unreachable_seconds
 
     def admit(self, a, ctx):
         if a.resource != "pods" or a.subresource:
             return
-        tols = a.obj.setdefault("spec", {}).setdefault("tolerations", [])
-        for key in ("node.kubernetes.io/not-ready", "node.kubernetes.io/unreachable"):
-            if not any(t.get("key") == key and t.get("effect") in ("NoExecute", None, "") for t in tols):
-                tols.append({"key": key, "operator": "Exists", "effect": "NoExecute", "tolerationSeconds": self.seconds})
+        spec = a.obj.setdefault("spec", {})
+        tols = spec.get("tolerations") or []
+
+        def tolerates(key):
+            return any(_tol(t, "key") in (key, "") and _tol(t, "effect") in ("NoExecute", "") for t in tols)
+        nr, ur = tolerates(NOT_READY_TAINT_KEY), tolerates(UNREACHABLE_TAINT_KEY)
+        if not nr:
+            add_or_update_toleration(spec, {"key": NOT_READY_TAINT_KEY, "operator": "Exists", "effect": "NoExecute",
+                                            "tolerationSeconds": self.not_ready})
+        if not ur:
+            add_or_update_toleration(spec, {"key": UNREACHABLE_TAINT_KEY, "operator": "Exists", "effect": "NoExecute",
+                                            "tolerationSeconds": self.unreachable})
 
 
 LIMIT_RANGER_ANNOTATION = "kubernetes.io/limit-ranger"
@@ -579,66 +733,141 @@ class ResourceQuota(Plugin):
         ctx.guaranteed_update_object("resourcequotas", m.namespace_of(quota), name, apply)
 
 
+SYSTEM_PRIORITY_CLASSES = {"system-cluster-critical": 2000000000, "system-node-critical": 2000001000}
+HIGHEST_USER_DEFINABLE_PRIORITY = 1000000000
+
+
 class Priority(Plugin):
+    """priority/admission.go: a new pod may not carry spec.priority itself; it gets the value of
+    its priorityClassName (the system classes are built in; an unknown name fails), else of the
+    globalDefault class, else 0. PriorityClass writes are checked: value at most 1e9, the system
+    names reserved, and only one globalDefault class."""
     name = "Priority"
-    operations = (CREATE,)
+    operations = (CREATE, UPDATE, DELETE)
 
     def admit(self, a, ctx):
-        if a.resource != "pods" or a.subresource:
+        if a.subresource or a.resource != "pods" or a.operation != CREATE:
             return
         spec = a.obj.setdefault("spec", {})
+        if spec.get("priority") is not None:
+            raise new_forbidden(a, "the integer value of priority must not be provided in pod spec. Priority "
+                                   "admission controller populates the value from the given PriorityClass name")
         pcn = spec.get("priorityClassName")
-        if pcn:
-            pc = ctx.get_object("priorityclasses", "", pcn)
-            if pc is None:
-                if pcn in ("system-cluster-critical", "system-node-critical"):
-                    spec["priority"] = 2000000000 if pcn == "system-cluster-critical" else 2000001000
-                    return
-                raise m.forbidden(f"no PriorityClass with name {pcn} was found")
-            spec["priority"] = int(pc.get("value", 0))
-        else:
-            default = [pc for pc in ctx.list_objects("priorityclasses", "") if pc.get("globalDefault")]
-            spec.setdefault("priority", int(default[0].get("value", 0)) if default else 0)
+        if not pcn:
+            dpc = self._default_class(ctx)
+            spec["priority"] = int(dpc.get("value", 0)) if dpc else 0
+            return
+        if pcn in SYSTEM_PRIORITY_CLASSES:
+            spec["priority"] = SYSTEM_PRIORITY_CLASSES[pcn]
+            return
+        pc = ctx.get_object("priorityclasses", "", pcn)
+        if pc is None:
+            raise unknown_error(f'failed to get default priority class {pcn}: priorityclass.scheduling.k8s.io "{pcn}" '
+                                f'not found')
+        spec["priority"] = int(pc.get("value", 0))
+
+    @staticmethod
+    def _default_class(ctx):
+        return next((pc for pc in ctx.list_objects("priorityclasses", "", "scheduling.k8s.io") if pc.get("globalDefault")),
+                    None)
+
+    def validate(self, a, ctx):
+        if a.subresource or a.resource != "priorityclasses" or a.operation == DELETE:
+            return
+        pc = a.obj or {}
+        if int(pc.get("value") or 0) > HIGHEST_USER_DEFINABLE_PRIORITY:
+            raise new_forbidden(a, f"maximum allowed value of a user defined priority is {HIGHEST_USER_DEFINABLE_PRIORITY}")
+        if m.name_of(pc) in SYSTEM_PRIORITY_CLASSES:
+            raise new_forbidden(a, f"the name of the priority class is a reserved name for system use only: {m.name_of(pc)}")
+        if pc.get("globalDefault"):
+            dpc = self._default_class(ctx)
+            if dpc is not None and (a.operation == CREATE or m.name_of(dpc) != m.name_of(pc)):
+                raise new_forbidden(a, f"PriorityClass {m.name_of(dpc)} is already marked as default. Only one default "
+                                       f"can exist")
 
 
 class PodNodeSelector(Plugin):
-    """Merge the namespace annotation scheduler.alpha.kubernetes.io/node-selector."""
+    """podnodeselector/admission.go: the namespace's scheduler.alpha.kubernetes.io/node-selector
+    annotation (else the plugin's clusterDefaultNodeSelector; an empty annotation means none) is
+    merged into the pod's nodeSelector — a label the pod sets differently is refused — and the
+    result must stay within the namespace's whitelist from the plugin configuration. Updates of
+    initialized pods are left alone (their node selector is immutable)."""
     name = "PodNodeSelector"
-    operations = (CREATE,)
     ANNOTATION = "scheduler.alpha.kubernetes.io/node-selector"
 
+    def __init__(self, cluster_node_selectors: dict | None = None, **config):
+        # podNodeSelectorPluginConfig: {clusterDefaultNodeSelector: ..., <namespace>: <whitelist>}
+        self.cluster = dict(cluster_node_selectors or config.get("podNodeSelectorPluginConfig") or {})
+
+    @staticmethod
+    def _ignore(a) -> bool:
+        return a.resource != "pods" or bool(a.subresource) or not isinstance(a.obj, dict)
+
+    def _namespace_selector(self, a, ctx) -> dict:
+        ns = ctx.get_namespace(a.namespace)
+        if ns is None:
+            raise m.not_found("namespaces", a.namespace)
+        ann = m.annotations_of(ns)
+        try:
+            if self.ANNOTATION in ann:
+                return convert_selector_to_labels_map(ann[self.ANNOTATION])
+            return convert_selector_to_labels_map(self.cluster.get("clusterDefaultNodeSelector", ""))
+        except ValueError as e:
+            raise unknown_error(str(e)) from None
+
     def admit(self, a, ctx):
-        if a.resource != "pods" or a.subresource:
+        if self._ignore(a) or is_updating_initialized(a):
             return
-        ns = ctx.get_namespace(a.namespace) or {}
-        sel = m.annotations_of(ns).get(self.ANNOTATION)
-        if not sel:
+        spec = a.obj.setdefault("spec", {})
+        ns_sel = self._namespace_selector(a, ctx)
+        pod_sel = spec.get("nodeSelector") or {}
+        if labels_conflict(ns_sel, pod_sel):
+            raise forbidden_for("pods", m.name_of(a.obj), "pod node label selector conflicts with its namespace node "
+                                                           "label selector")
+        merged = {**ns_sel, **pod_sel}
+        if merged or spec.get("nodeSelector") is not None:
+            spec["nodeSelector"] = merged
+        self.validate(a, ctx)
+
+    def validate(self, a, ctx):
+        if self._ignore(a):
             return
-        ns_sel = dict(kv.split("=", 1) for kv in sel.split(",") if "=" in kv)
-        pod_sel = a.obj.setdefault("spec", {}).setdefault("nodeSelector", {})
-        for k, v in ns_sel.items():
-            if k in pod_sel and pod_sel[k] != v:
-                raise m.forbidden("pod node label selector conflicts with its namespace node label selector")
-            pod_sel[k] = v
+        pod_sel = (a.obj.get("spec") or {}).get("nodeSelector") or {}
+        ns_sel = self._namespace_selector(a, ctx)
+        if labels_conflict(ns_sel, pod_sel):
+            raise forbidden_for("pods", m.name_of(a.obj), "pod node label selector conflicts with its namespace node "
+                                                           "label selector")
+        try:
+            whitelist = convert_selector_to_labels_map(self.cluster.get(a.namespace, ""))
+        except ValueError as e:
+            raise unknown_error(str(e)) from None
+        # labels.AreLabelsInWhiteList: an empty whitelist allows everything
+        if whitelist and any(k not in whitelist or whitelist[k] != v for k, v in pod_sel.items()):
+            raise forbidden_for("pods", m.name_of(a.obj), "pod node label selector labels conflict with its namespace "
+                                                           "whitelist")
+
+
+DEFAULT_CLASS_ANNOTATIONS = ("storageclass.kubernetes.io/is-default-class",
+                             "storageclass.beta.kubernetes.io/is-default-class")
 
 
 class DefaultStorageClass(Plugin):
-    """plugin/pkg/admission/storageclass/setdefault: a claim without a class gets the class
-    annotated storageclass.kubernetes.io/is-default-class=true (more than one default: 403)."""
+    """storageclass/setdefault/admission.go: a claim with neither spec.storageClassName nor the
+    volume.beta.kubernetes.io/storage-class annotation gets the class annotated (GA or beta)
+    is-default-class=true; more than one default is refused (a wrapped internal error)."""
     name = "DefaultStorageClass"
     operations = (CREATE,)
 
     def admit(self, a, ctx):
-        if a.resource != "persistentvolumeclaims" or a.subresource:
+        if a.resource != "persistentvolumeclaims" or a.subresource or not isinstance(a.obj, dict):
             return
         spec = a.obj.setdefault("spec", {})
-        if "storageClassName" in spec or "volume.beta.kubernetes.io/storage-class" in (a.obj.get("metadata") or {}).get(
-                "annotations", {}):
+        if spec.get("storageClassName") is not None or "volume.beta.kubernetes.io/storage-class" in m.annotations_of(a.obj):
             return
         defaults = [sc for sc in ctx.list_objects("storageclasses", "", "storage.k8s.io")
-                    if ((sc.get("metadata") or {}).get("annotations") or {}).get("storageclass.kubernetes.io/is-default-class") == "true"]
+                    if any(m.annotations_of(sc).get(k) == "true" for k in DEFAULT_CLASS_ANNOTATIONS)]
         if len(defaults) > 1:
-            raise m.forbidden(f"{len(defaults)} default StorageClasses were found")
+            raise new_forbidden(a, internal_error_message(f"{len(defaults)} default StorageClasses were found"))
         if defaults:
             spec["storageClassName"] = m.name_of(defaults[0])
 

@@ -20,7 +20,8 @@ import time
 from ..api import meta as m
 from ..api.labels import selector_from_label_selector
 from ..api.quantity import Quantity
-from .admission import CONNECT, CREATE, UPDATE, Plugin
+from .admission import (CONNECT, CREATE, UPDATE, Plugin, forbidden_for, is_updating_uninitialized, merge_tolerations,
+                        new_forbidden, tolerations_conflict, unknown_error, verify_against_whitelist)
 
 log = logging.getLogger("amdkube.admission")
 
@@ -37,7 +38,8 @@ def _all_containers(pod):
 # ------------------------------------------------------------------ AlwaysPullImages
 class AlwaysPullImages(Plugin):
     """alwayspullimages/admission.go: every (init) container pulls; validation rejects a pod
-    (create or update) that does not."""
+    (create or update) that does not, naming the first offending field
+    (`spec.initContainers[i].imagePullPolicy: Unsupported value: ...`)."""
     name = "AlwaysPullImages"
 
     def admit(self, a, ctx):
@@ -46,11 +48,15 @@ class AlwaysPullImages(Plugin):
                 c["imagePullPolicy"] = "Always"
 
     def validate(self, a, ctx):
-        if _is_pod(a) and a.obj is not None:
-            for c in _all_containers(a.obj):
+        if not _is_pod(a) or a.obj is None:
+            return
+        from ..api.field import go_quote
+        spec = a.obj.get("spec") or {}
+        for kind in ("initContainers", "containers"):
+            for i, c in enumerate(spec.get(kind) or []):
                 if c.get("imagePullPolicy") != "Always":
-                    raise m.forbidden(f"spec.containers[{c.get('name')}].imagePullPolicy: Unsupported value: "
-                                      f"{c.get('imagePullPolicy')!r}: supported values: \"Always\"")
+                    raise new_forbidden(a, f"spec.{kind}[{i}].imagePullPolicy: Unsupported value: "
+                                           f"{go_quote(c.get('imagePullPolicy') or '')}: supported values: \"Always\"")
 
 
 # --------------------------------------------------- LimitPodHardAntiAffinityTopology
@@ -65,8 +71,9 @@ class LimitPodHardAntiAffinityTopology(Plugin):
         paa = (((a.obj.get("spec") or {}).get("affinity") or {}).get("podAntiAffinity") or {})
         for t in paa.get("requiredDuringSchedulingIgnoredDuringExecution") or []:
             if t.get("topologyKey") != "kubernetes.io/hostname":
-                raise m.forbidden(f"affinity.PodAntiAffinity.RequiredDuringScheduling has TopologyKey "
-                                  f"{t.get('topologyKey')} but only key kubernetes.io/hostname is allowed")
+                raise forbidden_for("pods", m.name_of(a.obj),
+                                    f"affinity.PodAntiAffinity.RequiredDuringScheduling has TopologyKey "
+                                    f"{t.get('topologyKey') or ''} but only key kubernetes.io/hostname is allowed")
 
 
 # ------------------------------------------------------------------- EventRateLimit
@@ -134,7 +141,7 @@ def _privileged(pod) -> bool:
 
 class DenyEscalatingExec(Plugin):
     """exec/admission.go: no exec/attach into a privileged pod or one that shares the host's
-    PID or IPC namespace."""
+    PID or IPC namespace; a pod that cannot be read is refused too."""
     name = "DenyEscalatingExec"
     operations = (CONNECT,)
     host_checks = True
@@ -142,14 +149,16 @@ class DenyEscalatingExec(Plugin):
     def validate(self, a, ctx):
         if a.resource != "pods" or a.subresource not in ("exec", "attach"):
             return
-        pod = a.old or ctx.get_object("pods", a.namespace, a.name) or {}
+        pod = a.old or ctx.get_object("pods", a.namespace, a.name)
+        if pod is None:
+            raise new_forbidden(a, f'pods "{a.name}" not found')
         spec = pod.get("spec") or {}
         if self.host_checks and spec.get("hostPID"):
-            raise m.forbidden("cannot exec into or attach to a container using host pid")
+            raise new_forbidden(a, "cannot exec into or attach to a container using host pid")
         if self.host_checks and spec.get("hostIPC"):
-            raise m.forbidden("cannot exec into or attach to a container using host ipc")
+            raise new_forbidden(a, "cannot exec into or attach to a container using host ipc")
         if _privileged(pod):
-            raise m.forbidden("cannot exec into or attach to a privileged container")
+            raise new_forbidden(a, "cannot exec into or attach to a privileged container")
 
 
 class DenyExecOnPrivileged(DenyEscalatingExec):
@@ -454,67 +463,74 @@ NS_DEFAULT_TOLERATIONS = "scheduler.alpha.kubernetes.io/defaultTolerations"
 NS_WHITELIST_TOLERATIONS = "scheduler.alpha.kubernetes.io/tolerationsWhitelist"
 
 
-def _tol_map(ts):
-    return {t.get("key", ""): t for t in ts or []}
-
-
-def _tol_eq(x, y):
-    keys = ("key", "operator", "value", "effect", "tolerationSeconds")
-    norm = lambda t: tuple(t.get(k, "" if k != "tolerationSeconds" else None) or ("Equal" if k == "operator" and not t.get(k) else t.get(k, "")) for k in keys)  # noqa: E731
-    return norm(x) == norm(y)
+MEMORY_PRESSURE_TOLERATION = {"key": "node.kubernetes.io/memory-pressure", "operator": "Exists", "effect": "NoSchedule"}
 
 
 class PodTolerationRestriction(Plugin):
-    """podtolerationrestriction/admission.go: new pods get their namespace's default
-    tolerations (annotation, else the plugin's cluster default) merged in (conflicts rejected);
-    non-BestEffort pods tolerate memory pressure; every toleration must be on the namespace's
-    whitelist (annotation, else the cluster whitelist) when one is set."""
+    """podtolerationrestriction/admission.go: a new pod (or an update of an uninitialized one)
+    gets its namespace's default tolerations (the scheduler.alpha.kubernetes.io/defaultTolerations
+    annotation, an empty value meaning none; without the annotation the plugin's cluster default)
+    merged in (MergeTolerations; a (key, effect) defined differently is refused); non-BestEffort
+    pods also tolerate node.kubernetes.io/memory-pressure:NoSchedule; every toleration must then
+    be on the namespace's whitelist (annotation, else the cluster whitelist) when one is set."""
     name = "PodTolerationRestriction"
 
     def __init__(self, default=None, whitelist=None):
         self.default, self.whitelist = default or [], whitelist or []
 
     def _ns_list(self, ctx, ns, key):
-        obj = ctx.get_namespace(ns) or {}
-        v = m.annotations_of(obj).get(key)
-        if v is None:
+        """extractNSTolerations: None without the annotation, [] for an empty value."""
+        obj = ctx.get_namespace(ns)
+        if obj is None:
+            raise m.not_found("namespaces", ns)
+        ann = m.annotations_of(obj)
+        if key not in ann:
             return None
+        if not ann[key]:
+            return []
         try:
-            return json.loads(v) if v.strip() else []
+            v = json.loads(ann[key])
         except ValueError as e:
-            raise m.forbidden(f"namespace {ns} annotation {key} is invalid: {e}")
+            raise unknown_error(str(e)) from None
+        if v is not None and not isinstance(v, list):
+            raise unknown_error(f"json: cannot unmarshal {type(v).__name__} into Go value of type []v1.Toleration")
+        return v or []
 
     def admit(self, a, ctx):
-        if not _is_pod(a) or a.obj is None:
+        if not _is_pod(a) or not isinstance(a.obj, dict):
             return
         spec = a.obj.setdefault("spec", {})
         final = spec.get("tolerations") or []
-        if a.operation == CREATE:
+        if a.operation == CREATE or is_updating_uninitialized(a):
             ts = self._ns_list(ctx, a.namespace, NS_DEFAULT_TOLERATIONS)
-            ts = self.default if ts is None else ts
+            if ts is None:
+                ts = self.default
             if ts:
-                mine = _tol_map(final)
-                if any(k in mine and not _tol_eq(v, mine[k]) for k, v in _tol_map(ts).items()):
-                    raise m.forbidden("namespace tolerations and pod tolerations conflict")
-                final = list(final) + [v for k, v in _tol_map(ts).items() if k not in mine]
+                if final:
+                    if tolerations_conflict(ts, final):
+                        raise unknown_error("namespace tolerations and pod tolerations conflict")
+                    final = merge_tolerations(ts, final)
+                else:
+                    final = list(ts)
         from .registry import pod_qos
-        if pod_qos(a.obj) != "BestEffort" and "node.kubernetes.io/memory-pressure" not in _tol_map(final):
-            final = list(final) + [{"key": "node.kubernetes.io/memory-pressure", "operator": "Exists", "effect": "NoSchedule"}]
-        if final:
+        if pod_qos(a.obj) != "BestEffort":
+            final = merge_tolerations(final, [dict(MEMORY_PRESSURE_TOLERATION)])
+        if final or spec.get("tolerations") is not None:
             spec["tolerations"] = final
+        self.validate(a, ctx)
 
     def validate(self, a, ctx):
-        if not _is_pod(a) or a.obj is None:
+        if not _is_pod(a) or not isinstance(a.obj, dict):
             return
         tols = (a.obj.get("spec") or {}).get("tolerations") or []
         if not tols:
             return
         wl = self._ns_list(ctx, a.namespace, NS_WHITELIST_TOLERATIONS)
-        wl = self.whitelist if wl is None else wl
-        if wl:
-            w = _tol_map(wl)
-            if any(k not in w or not _tol_eq(v, w[k]) for k, v in _tol_map(tols).items()):
-                raise m.forbidden("pod tolerations (possibly merged with namespace default tolerations) conflict with its namespace whitelist")
+        if wl is None:
+            wl = self.whitelist
+        if wl and not verify_against_whitelist(tols, wl):
+            raise unknown_error("pod tolerations (possibly merged with namespace default tolerations) conflict with its "
+                                "namespace whitelist")
 
 
 # ----------------------------------------------------------------- SecurityContextDeny

@@ -1,0 +1,454 @@
+"""Admission plugins against the reference's tables.
+
+Transcribed from plugin/pkg/admission/*/admission_test.go:
+  defaulttolerationseconds (TestForgivenessAdmission, TestHandles), extendedresourcetoleration
+  (TestAdmit), podnodeselector (TestPodAdmission, TestHandles, TestIgnoreUpdatingInitializedPod),
+  podtolerationrestriction (TestPodAdmission, with its namespace annotations carried from case to
+  case as the Go test does), priority (TestPriorityClassAdmission, TestDefaultPriority,
+  TestPodAdmission), storageclass/setdefault (TestAdmission), alwayspullimages, antiaffinity and
+  exec (TestAdmission / TestInterPodAffinityAdmission / TestAdmission), and the namespace
+  lifecycle plugin (apiserver/pkg/admission/plugin/namespace/lifecycle/admission_test.go).
+"""
+from __future__ import annotations
+
+import copy
+import json
+
+import pytest
+
+from amdkube.api import meta as m
+from amdkube.apiserver import admission as A
+from amdkube.apiserver import admission_ext as X
+from amdkube.apiserver.admission import CONNECT, CREATE, DELETE, UPDATE, Attributes
+
+NR, UR = "node.kubernetes.io/not-ready", "node.kubernetes.io/unreachable"
+DNR, DUR = "node.alpha.kubernetes.io/notReady", "node.alpha.kubernetes.io/unreachable"
+
+
+class Ctx:
+    def __init__(self, namespaces=None, **objects):
+        self.namespaces = namespaces if namespaces is not None else {}
+        self.objects = objects
+
+    def get_namespace(self, n):
+        return self.namespaces.get(n)
+
+    def list_objects(self, plural, ns, group=""):
+        return list(self.objects.get(plural, []))
+
+    def get_object(self, plural, ns, name):
+        return next((o for o in self.objects.get(plural, []) if m.name_of(o) == name), None)
+
+
+def _ns(name="testNamespace", **ann):
+    return {name: {"metadata": {"name": name, "annotations": ann} if ann else {"name": name}}}
+
+
+def _pod(name="testPod", ns="testNamespace", **spec):
+    return {"metadata": {"name": name, "namespace": ns}, "spec": spec}
+
+
+def _attrs(obj, op=CREATE, ns="testNamespace", name=None, old=None, resource="pods", sub="", group=""):
+    return Attributes(op, resource, sub, ns, m.name_of(obj or {}) if name is None else name, obj, old, {}, group=group)
+
+
+def _t(key="", op="", effect="", value="", seconds=None):
+    t = {}
+    for k, v in (("key", key), ("operator", op), ("value", value), ("effect", effect)):
+        if v:
+            t[k] = v
+    if seconds is not None:
+        t["tolerationSeconds"] = seconds
+    return t
+
+
+# ------------------------------------------------------------ DefaultTolerationSeconds
+DEF_NR, DEF_UR = _t(NR, "Exists", "NoExecute", seconds=300), _t(UR, "Exists", "NoExecute", seconds=300)
+
+
+@pytest.mark.parametrize("desc,given,expected", [
+    ("pod has no tolerations", [], [DEF_NR, DEF_UR]),
+    ("pod has alpha tolerations, untouched", [_t(DNR, "Exists", "NoExecute", seconds=300), _t(DUR, "Exists", "NoExecute", seconds=300)],
+     [_t(DNR, "Exists", "NoExecute", seconds=300), _t(DUR, "Exists", "NoExecute", seconds=300), DEF_NR, DEF_UR]),
+    ("pod has alpha not-ready toleration", [_t(DNR, "Exists", "NoExecute", seconds=300)],
+     [_t(DNR, "Exists", "NoExecute", seconds=300), DEF_NR, DEF_UR]),
+    ("pod has alpha unreachable toleration", [_t(DUR, "Exists", "NoExecute", seconds=300)],
+     [_t(DUR, "Exists", "NoExecute", seconds=300), DEF_NR, DEF_UR]),
+    ("pod has tolerations, none for the node taints", [_t("foo", "Equal", "NoSchedule", "bar", 700)],
+     [_t("foo", "Equal", "NoSchedule", "bar", 700), DEF_NR, DEF_UR]),
+    ("pod tolerates not-ready", [_t(NR, "Exists", "NoExecute", seconds=700)], [_t(NR, "Exists", "NoExecute", seconds=700), DEF_UR]),
+    ("pod tolerates unreachable", [_t(UR, "Exists", "NoExecute", seconds=700)], [_t(UR, "Exists", "NoExecute", seconds=700), DEF_NR]),
+    ("pod tolerates both", [_t(NR, "Exists", "NoExecute", seconds=700), _t(UR, "Exists", "NoExecute", seconds=700)],
+     [_t(NR, "Exists", "NoExecute", seconds=700), _t(UR, "Exists", "NoExecute", seconds=700)]),
+    ("pod tolerates unreachable with any effect", [_t(UR, "Exists", seconds=700)],
+     [_t(UR, "Exists", seconds=700), DEF_NR]),
+    ("pod has a wildcard toleration", [_t(op="Exists", seconds=700)], [_t(op="Exists", seconds=700)]),
+])
+def test_default_toleration_seconds(desc, given, expected):
+    p = _pod(tolerations=copy.deepcopy(given))
+    A.DefaultTolerationSeconds().admit(_attrs(p, ns="foo", name="name"), Ctx())
+    assert p["spec"]["tolerations"] == expected, desc
+
+
+def test_default_toleration_seconds_handles():
+    h = A.DefaultTolerationSeconds()
+    assert [h.handles(op) for op in (UPDATE, CREATE, DELETE, CONNECT)] == [True, True, False, False]
+
+
+# --------------------------------------------------------- ExtendedResourceToleration
+ER1, ER2 = "example.com/device-ek", "example.com/device-do"
+
+
+def _c(*resources):
+    return {"name": "c", "resources": {"requests": {r: "1" for r in resources}}} if resources else {"name": "c"}
+
+
+@pytest.mark.parametrize("desc,spec,expected", [
+    ("empty pod", {}, None),
+    ("container without extended resources", {"containers": [{"name": "c", "resources": {"requests": {"cpu": "1"}}}]}, None),
+    ("init container without extended resources", {"initContainers": [{"name": "c", "resources": {"requests": {"cpu": "1"}}}]}, None),
+    ("container with an extended resource", {"containers": [_c(ER1)]}, [_t(ER1, "Exists", "NoSchedule")]),
+    ("init container with an extended resource", {"initContainers": [_c(ER2)]}, [_t(ER2, "Exists", "NoSchedule")]),
+    ("existing tolerations preserved", {"containers": [_c(ER1)], "tolerations": [_t("foo", "Equal", "NoSchedule", "bar")]},
+     [_t("foo", "Equal", "NoSchedule", "bar"), _t(ER1, "Exists", "NoSchedule")]),
+    ("multiple extended resources, sorted", {"containers": [_c(ER1)], "initContainers": [_c(ER2)]},
+     [_t(ER2, "Exists", "NoSchedule"), _t(ER1, "Exists", "NoSchedule")]),
+    ("existing correct toleration", {"containers": [_c(ER1)], "tolerations": [_t(ER1, "Exists", "NoSchedule")]},
+     [_t(ER1, "Exists", "NoSchedule")]),
+    ("same key, other effect and value", {"containers": [_c(ER1)], "tolerations": [_t(ER1, "Equal", "NoExecute", "foo")]},
+     [_t(ER1, "Equal", "NoExecute", "foo"), _t(ER1, "Exists", "NoSchedule")]),
+    ("wildcard toleration", {"containers": [_c(ER1)], "tolerations": [_t(op="Exists")]},
+     [_t(op="Exists"), _t(ER1, "Exists", "NoSchedule")]),
+])
+def test_extended_resource_toleration(desc, spec, expected):
+    p = _pod(**copy.deepcopy(spec))
+    A.ExtendedResourceToleration().admit(_attrs(p, ns="foo", name="name"), Ctx())
+    assert p["spec"].get("tolerations") == expected, desc
+
+
+# -------------------------------------------------------------------- PodNodeSelector
+@pytest.mark.parametrize("default,ns_sel,whitelist,pod_sel,merged,ignore_ns,admit,name", [
+    ("", None, "", {}, {}, True, True, "No node selectors"),
+    ("infra = false", None, "", {}, {"infra": "false"}, True, True, "Default node selector and no conflicts"),
+    ("", " infra = false ", "", {}, {"infra": "false"}, False, True, "TestNamespace node selector with whitespaces and no conflicts"),
+    ("infra = false", "infra=true", "", {}, {"infra": "true"}, False, True, "Default and namespace node selector, no conflicts"),
+    ("infra = false", "", "", {}, {}, False, True, "Empty namespace node selector and no conflicts"),
+    ("infra = false", "infra=true", "", {"env": "test"}, {"infra": "true", "env": "test"}, False, True,
+     "TestNamespace and pod node selector, no conflicts"),
+    ("env = test", "infra=true", "", {"infra": "false"}, None, False, False, "Conflicting pod and namespace node selector, one label"),
+    ("env=dev", "infra=false, env = test", "", {"env": "dev", "color": "blue"}, None, False, False,
+     "Conflicting pod and namespace node selector, multiple labels"),
+    ("env=dev", "infra=false, env = dev", "env=dev, infra=false, color=blue", {"env": "dev", "color": "blue"},
+     {"infra": "false", "env": "dev", "color": "blue"}, False, True, "Merged pod node selectors satisfy the whitelist"),
+    ("env=dev", "infra=false, env = dev", "env=dev, infra=true, color=blue", {"env": "dev", "color": "blue"}, None, False, False,
+     "Merged pod node selectors conflict with the whitelist"),
+    ("env=dev", None, "env=prd", {}, None, True, False, "Default node selector conflict with the whitelist"),
+])
+def test_pod_node_selector(default, ns_sel, whitelist, pod_sel, merged, ignore_ns, admit, name, _state={}):
+    # the Go test keeps one namespace object and only rewrites its annotation when a case sets one
+    if not ignore_ns:
+        _state["ns"] = _ns(**{A.PodNodeSelector.ANNOTATION: ns_sel})
+    ctx = Ctx(_state.get("ns") or _ns())
+    h = A.PodNodeSelector({"clusterDefaultNodeSelector": default, "testNamespace": whitelist})
+    p = _pod(nodeSelector=dict(pod_sel))
+    old = _pod(nodeSelector={"old": "true"})
+    old["metadata"]["initializers"] = {"pending": [{"name": "init"}]}
+    for op, o in ((CREATE, None), (UPDATE, old)):      # an update of an uninitialized pod acts as a create
+        for step in (h.admit, h.validate):
+            if admit:
+                step(_attrs(p, op, old=o), ctx)
+                assert p["spec"]["nodeSelector"] == merged, name
+            else:
+                with pytest.raises(m.StatusError) as e:
+                    step(_attrs(p, op, old=o), ctx)
+                assert e.value.code == 403 and e.value.message.startswith('pods "testPod" is forbidden: pod node label selector'), name
+
+
+def test_pod_node_selector_handles_and_initialized_updates():
+    h = A.PodNodeSelector(None)
+    assert [h.handles(op) for op in (CREATE, UPDATE, CONNECT, DELETE)] == [True, True, False, False]
+    ctx = Ctx(_ns(**{A.PodNodeSelector.ANNOTATION: "infra=true"}))
+    p = _pod(nodeSelector={"infra": "false"})
+    h.admit(_attrs(p, UPDATE, old=copy.deepcopy(p)), ctx)      # initialized: its node selector is immutable
+    assert p["spec"]["nodeSelector"] == {"infra": "false"}
+
+
+# --------------------------------------------------------- PodTolerationRestriction
+TK = _t("testKey", "Equal", "NoSchedule", "testValue")
+TK1 = _t("testKey", "Equal", "NoSchedule", "testValue1")
+TK2 = _t("testKey", "Equal", "NoSchedule", "testValue2")
+MP = _t("node.kubernetes.io/memory-pressure", "Exists", "NoSchedule")
+BEST_EFFORT = [{"name": "test"}]
+BURSTABLE = [{"name": "test", "resources": {"limits": {"cpu": "1000m"}, "requests": {"cpu": "500m"}}}]
+GUARANTEED = [{"name": "test", "resources": {"limits": {"cpu": "1000m"}, "requests": {"cpu": "1000m"}}}]
+
+PTR_CASES = [
+    (BEST_EFFORT, [TK], None, None, None, [], [TK], True, "default cluster tolerations with empty pod tolerations and nil namespace tolerations"),
+    (BEST_EFFORT, [TK], [], None, None, [TK], [TK], True, "default cluster tolerations with pod tolerations specified"),
+    (BEST_EFFORT, [], [TK], None, None, [TK], [TK], True, "namespace tolerations"),
+    (BEST_EFFORT, [], [TK], None, None, [], [TK], True, "no pod tolerations"),
+    (BEST_EFFORT, [], [TK], None, None, [TK1], None, False, "conflicting pod and namespace tolerations"),
+    (BEST_EFFORT, [TK2], [], None, None, [TK1], [TK1], True,
+     "conflicting pod and default cluster tolerations but overridden by empty namespace tolerations"),
+    (BEST_EFFORT, [], [TK], [TK], None, [], [TK], True, "merged pod tolerations satisfy whitelist"),
+    (BEST_EFFORT, [TK], [], None, None, [], [], True, "Override default cluster toleration by empty namespace level toleration"),
+    (BEST_EFFORT, None, None, [], [TK1], [TK], [TK], True,
+     "pod toleration conflicts with default cluster white list which is overridden by empty namespace whitelist"),
+    (BEST_EFFORT, [], [TK], [TK1], None, [], None, False, "merged pod tolerations conflict with the whitelist"),
+    (BURSTABLE, [], [TK], [], None, [], [MP, TK], True, "added memoryPressure/DiskPressure for Burstable pod"),
+    (GUARANTEED, [], [TK], [], None, [], [MP, TK], True, "added memoryPressure/DiskPressure for Guaranteed pod"),
+]
+
+
+def test_pod_toleration_restriction_table():
+    ns = {"metadata": {"name": "testNamespace"}}
+    for containers, default, ns_tols, whitelist, cluster_wl, pod_tols, merged, admit, name in PTR_CASES:
+        if ns_tols is not None:           # the Go test replaces the annotations only when a case sets them
+            ns["metadata"]["annotations"] = {X.NS_DEFAULT_TOLERATIONS: json.dumps(ns_tols)}
+        if whitelist is not None:
+            ns["metadata"]["annotations"][X.NS_WHITELIST_TOLERATIONS] = json.dumps(whitelist)
+        ctx = Ctx({"testNamespace": ns})
+        h = X.PodTolerationRestriction(default or [], cluster_wl or [])
+        p = _pod(containers=copy.deepcopy(containers), tolerations=copy.deepcopy(pod_tols))
+        old = copy.deepcopy(p)
+        old["metadata"]["initializers"] = {"pending": [{"name": "init"}]}
+        old["spec"]["tolerations"] = [TK1]
+        for op, o in ((CREATE, None), (UPDATE, old)):
+            q = copy.deepcopy(p)
+            if admit:
+                h.admit(_attrs(q, op, old=o), ctx)
+                assert q["spec"]["tolerations"] == merged, name
+            else:
+                with pytest.raises(m.StatusError) as e:
+                    h.admit(_attrs(q, op, old=o), ctx)
+                assert e.value.code == 500, name
+
+
+def test_pod_toleration_restriction_leaves_initialized_updates_to_the_whitelist():
+    ctx = Ctx(_ns(**{X.NS_DEFAULT_TOLERATIONS: json.dumps([TK])}))
+    p = _pod(containers=copy.deepcopy(BEST_EFFORT))
+    X.PodTolerationRestriction().admit(_attrs(p, UPDATE, old=copy.deepcopy(p)), ctx)
+    assert not p["spec"].get("tolerations")
+
+
+def test_pod_toleration_restriction_bad_annotation():
+    ctx = Ctx(_ns(**{X.NS_DEFAULT_TOLERATIONS: "{not json"}))
+    with pytest.raises(m.StatusError):
+        X.PodTolerationRestriction().admit(_attrs(_pod(containers=copy.deepcopy(BEST_EFFORT))), ctx)
+
+
+# ------------------------------------------------------------------------- Priority
+def _pc(name, value, default=False):
+    return {"apiVersion": "scheduling.k8s.io/v1alpha1", "kind": "PriorityClass", "metadata": {"name": name}, "value": value,
+            "globalDefault": default}
+
+
+DEFAULT1, DEFAULT2, NONDEFAULT1 = _pc("default1", 1000, True), _pc("default2", 2000, True), _pc("nondefault1", 2000)
+
+
+@pytest.mark.parametrize("name,existing,new,err", [
+    ("one default class", [], DEFAULT1, None),
+    ("more than one default classes", [DEFAULT1], DEFAULT2,
+     'priorityclasses.scheduling.k8s.io "default2" is forbidden: PriorityClass default1 is already marked as default. Only one default can exist'),
+    ("too high PriorityClass value", [], _pc("toohighclass", 1000000001),
+     'priorityclasses.scheduling.k8s.io "toohighclass" is forbidden: maximum allowed value of a user defined priority is 1000000000'),
+    ("system name conflict", [], _pc("system-cluster-critical", 1000000001),
+     'maximum allowed value of a user defined priority is 1000000000'),
+    ("system name with an allowed value", [], _pc("system-node-critical", 5),
+     'the name of the priority class is a reserved name for system use only: system-node-critical'),
+])
+def test_priority_class_admission(name, existing, new, err):
+    a = _attrs(new, ns="", resource="priorityclasses", group="scheduling.k8s.io")
+    if err is None:
+        A.Priority().validate(a, Ctx(priorityclasses=existing))
+    else:
+        with pytest.raises(m.StatusError) as e:
+            A.Priority().validate(a, Ctx(priorityclasses=existing))
+        assert err in e.value.message and e.value.code == 403, name
+
+
+def test_priority_default_class_update():
+    """TestDefaultPriority's "update default class and remove its global default" and the
+    update-to-the-same-default case: updating the default class itself is allowed."""
+    a = _attrs(_pc("default1", 5, True), UPDATE, ns="", resource="priorityclasses", group="scheduling.k8s.io",
+               old=DEFAULT1)
+    A.Priority().validate(a, Ctx(priorityclasses=[DEFAULT1]))
+    a = _attrs(_pc("other", 5, True), UPDATE, ns="", resource="priorityclasses", group="scheduling.k8s.io")
+    with pytest.raises(m.StatusError):
+        A.Priority().validate(a, Ctx(priorityclasses=[DEFAULT1]))
+
+
+MIRROR = {"kubernetes.io/config.mirror": "x"}
+
+
+@pytest.mark.parametrize("name,existing,spec,ann,expected,err", [
+    ("Pod with priority class", [DEFAULT1, NONDEFAULT1], {"priorityClassName": "default1"}, None, 1000, None),
+    ("Pod without priority class", [DEFAULT1], {}, None, 1000, None),
+    ("pod without priority class and no existing priority class", [], {}, None, 0, None),
+    ("pod without priority class and no default class", [NONDEFAULT1], {}, None, 0, None),
+    ("pod with a system priority class", [], {"priorityClassName": "system-cluster-critical"}, None, 2000000000, None),
+    ("Pod with non-existing priority class", [DEFAULT1, NONDEFAULT1], {"priorityClassName": "non-existing"}, None, None,
+     (500, 'failed to get default priority class non-existing: priorityclass.scheduling.k8s.io "non-existing" not found')),
+    ("pod with integer priority", [], {"priorityClassName": "default1", "priority": 1000}, None, None,
+     (403, 'pods "pod-w-integer-priority" is forbidden: the integer value of priority must not be provided in pod spec.')),
+    ("mirror pod with system priority class", [], {"priorityClassName": "system-cluster-critical"}, MIRROR, 2000000000, None),
+    ("mirror pod with integer priority", [], {"priorityClassName": "default1", "priority": 1000}, MIRROR, None,
+     (403, 'pods "pod-w-integer-priority" is forbidden: the integer value of priority must not be provided')),
+])
+def test_priority_pod_admission(name, existing, spec, ann, expected, err):
+    p = _pod("pod-w-integer-priority", **copy.deepcopy(spec))
+    if ann:
+        p["metadata"]["annotations"] = dict(ann)
+    if err is None:
+        A.Priority().admit(_attrs(p), Ctx(priorityclasses=existing))
+        assert p["spec"]["priority"] == expected, name
+    else:
+        with pytest.raises(m.StatusError) as e:
+            A.Priority().admit(_attrs(p), Ctx(priorityclasses=existing))
+        assert (e.value.code, e.value.message[:len(err[1])]) == err, name
+
+
+# -------------------------------------------------------------- DefaultStorageClass
+def _sc(name, ann=None):
+    return {"metadata": {"name": name, "annotations": ann or {}}, "provisioner": "x"}
+
+
+DEF_SC = _sc("default", {"storageclass.kubernetes.io/is-default-class": "true"})
+DEF_SC2 = _sc("default2", {"storageclass.kubernetes.io/is-default-class": "true"})
+BETA_SC = _sc("beta", {"storageclass.beta.kubernetes.io/is-default-class": "true"})
+NOT_DEF = _sc("nondefault", {"storageclass.kubernetes.io/is-default-class": "false"})
+NO_ANN = _sc("nondefault2")
+
+
+@pytest.mark.parametrize("name,classes,claim_class,claim_ann,expected,err", [
+    ("no default, no modification of PVCs", [NOT_DEF, NO_ANN], None, None, None, False),
+    ("one default, modify PVC with class=nil", [DEF_SC, NOT_DEF, NO_ANN], None, None, "default", False),
+    ("one default, no modification of PVC with class=''", [DEF_SC, NOT_DEF], "", None, "", False),
+    ("one default, no modification of PVC with class='foo'", [DEF_SC, NOT_DEF], "foo", None, "foo", False),
+    ("one default, no modification of PVC with the beta annotation", [DEF_SC],
+     None, {"volume.beta.kubernetes.io/storage-class": ""}, None, False),
+    ("two defaults, error with PVC with class=nil", [DEF_SC, DEF_SC2, NOT_DEF], None, None, None, True),
+    ("two defaults, no modification with PVC with class=''", [DEF_SC, DEF_SC2], "", None, "", False),
+    ("one beta default", [BETA_SC, NOT_DEF], None, None, "beta", False),
+])
+def test_default_storage_class(name, classes, claim_class, claim_ann, expected, err):
+    pvc = {"metadata": {"name": "claimWithNoClass", "namespace": "ns"}, "spec": {}}
+    if claim_class is not None:
+        pvc["spec"]["storageClassName"] = claim_class
+    if claim_ann:
+        pvc["metadata"]["annotations"] = dict(claim_ann)
+    a = _attrs(pvc, ns="ns", resource="persistentvolumeclaims")
+    if err:
+        with pytest.raises(m.StatusError) as e:
+            A.DefaultStorageClass().admit(a, Ctx(storageclasses=classes))
+        assert e.value.message == ('persistentvolumeclaims "claimWithNoClass" is forbidden: Internal error occurred: '
+                                   '2 default StorageClasses were found')
+    else:
+        A.DefaultStorageClass().admit(a, Ctx(storageclasses=classes))
+        assert pvc["spec"].get("storageClassName") == expected, name
+
+
+# ------------------------------------------------ AlwaysPullImages / anti-affinity / exec
+def test_always_pull_images_messages():
+    p = _pod("123", containers=[{"name": "ctr1", "image": "image"}, {"name": "ctr2", "image": "image", "imagePullPolicy": "Never"}],
+             initContainers=[{"name": "init1", "image": "image", "imagePullPolicy": "IfNotPresent"}])
+    a = _attrs(p, name="123")
+    with pytest.raises(m.StatusError) as e:
+        X.AlwaysPullImages().validate(a, Ctx())
+    assert e.value.message == ('pods "123" is forbidden: spec.initContainers[0].imagePullPolicy: Unsupported value: '
+                               '"IfNotPresent": supported values: "Always"')
+    X.AlwaysPullImages().admit(a, Ctx())
+    X.AlwaysPullImages().validate(a, Ctx())
+    assert {c["imagePullPolicy"] for c in p["spec"]["containers"] + p["spec"]["initContainers"]} == {"Always"}
+    # other resources and subresources are ignored
+    X.AlwaysPullImages().validate(_attrs(_pod(containers=[{"name": "c"}]), sub="exec"), Ctx())
+    X.AlwaysPullImages().validate(_attrs({"metadata": {"name": "x"}}, resource="services"), Ctx())
+
+
+def _anti(*keys):
+    return {"affinity": {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+        {"labelSelector": {"matchExpressions": [{"key": "security", "operator": "In", "values": ["S2"]}]}, "topologyKey": k}
+        for k in keys]}}}
+
+
+@pytest.mark.parametrize("spec,ok", [
+    (_anti("kubernetes.io/hostname"), True),
+    (_anti("failure-domain.beta.kubernetes.io/zone"), False),
+    (_anti("kubernetes.io/hostname", "failure-domain.beta.kubernetes.io/zone"), False),
+    ({"affinity": {"podAntiAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+        {"weight": 10, "podAffinityTerm": {"topologyKey": "failure-domain.beta.kubernetes.io/zone"}}]}}}, True),
+    ({"affinity": {"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+        {"topologyKey": "failure-domain.beta.kubernetes.io/zone"}]}}}, True),
+    ({}, True),
+])
+def test_inter_pod_affinity_admission(spec, ok):
+    p = _pod(**copy.deepcopy(spec))
+    if ok:
+        X.LimitPodHardAntiAffinityTopology().validate(_attrs(p), Ctx())
+    else:
+        with pytest.raises(m.StatusError) as e:
+            X.LimitPodHardAntiAffinityTopology().validate(_attrs(p), Ctx())
+        assert e.value.message == ('pods "testPod" is forbidden: affinity.PodAntiAffinity.RequiredDuringScheduling has '
+                                   'TopologyKey failure-domain.beta.kubernetes.io/zone but only key kubernetes.io/hostname is allowed')
+
+
+@pytest.mark.parametrize("spec,escalating,on_privileged", [
+    ({"hostPID": True}, "cannot exec into or attach to a container using host pid", None),
+    ({"hostIPC": True}, "cannot exec into or attach to a container using host ipc", None),
+    ({"containers": [{"name": "c", "securityContext": {"privileged": True}}]}, "cannot exec into or attach to a privileged container",
+     "cannot exec into or attach to a privileged container"),
+    ({"initContainers": [{"name": "i", "securityContext": {"privileged": True}}]},
+     "cannot exec into or attach to a privileged container", "cannot exec into or attach to a privileged container"),
+    ({"containers": [{"name": "c", "securityContext": {"privileged": False}}]}, None, None),
+    ({}, None, None),
+])
+def test_deny_exec(spec, escalating, on_privileged):
+    ctx = Ctx(pods=[_pod("pod", **spec)])
+    for plug, msg in ((X.DenyEscalatingExec(), escalating), (X.DenyExecOnPrivileged(), on_privileged)):
+        for sub in ("exec", "attach"):
+            a = Attributes(CONNECT, "pods", sub, "testNamespace", "pod", None, None, {})
+            if msg is None:
+                plug.validate(a, ctx)
+            else:
+                with pytest.raises(m.StatusError) as e:
+                    plug.validate(a, ctx)
+                assert e.value.message == f'pods "pod" is forbidden: {msg}'
+    # portforward is not exec or attach
+    X.DenyEscalatingExec().validate(Attributes(CONNECT, "pods", "portforward", "testNamespace", "pod", None, None, {}), ctx)
+
+
+# ------------------------------------------------------------------ NamespaceLifecycle
+def test_namespace_lifecycle():
+    h = A.NamespaceLifecycle()
+    active = {"metadata": {"name": "test"}, "status": {"phase": "Active"}}
+    terminating = {"metadata": {"name": "test"}, "status": {"phase": "Terminating"}}
+    pod = _pod("123", ns="test", containers=[{"name": "ctr", "image": "image"}])
+    h.validate(_attrs(pod, ns="test"), Ctx({"test": active}))
+    with pytest.raises(m.StatusError) as e:
+        h.validate(_attrs(pod, ns="test"), Ctx({"test": terminating}))
+    assert e.value.message == ('pods "123" is forbidden: unable to create new content in namespace test because it is '
+                               'being terminated.')
+    # updates and deletes in a terminating namespace are allowed (finalization needs them)
+    h.validate(_attrs(pod, UPDATE, ns="test", old=pod), Ctx({"test": terminating}))
+    h.validate(_attrs(pod, DELETE, ns="test"), Ctx({"test": terminating}))
+    # subresources are not exempt: a binding in a terminating namespace is refused
+    with pytest.raises(m.StatusError):
+        h.validate(_attrs({"metadata": {"name": "123"}}, ns="test", sub="binding"), Ctx({"test": terminating}))
+    # a missing namespace
+    with pytest.raises(m.StatusError) as e:
+        h.validate(_attrs(pod, ns="missing"), Ctx({}))
+    assert e.value.code == 404 and e.value.message == 'namespaces "missing" not found'
+    # access reviews skip the lookup; cluster-scoped objects too
+    h.validate(_attrs({"metadata": {}}, ns="missing", resource="localsubjectaccessreviews", group="authorization.k8s.io"), Ctx({}))
+    h.validate(_attrs({"metadata": {"name": "n"}}, ns="", resource="nodes"), Ctx({}))
+
+
+@pytest.mark.parametrize("ns,ok", [("default", False), ("kube-system", False), ("kube-public", False), ("other", True)])
+def test_namespace_lifecycle_immortal(ns, ok):
+    a = _attrs(None, DELETE, ns="", name=ns, resource="namespaces")
+    if ok:
+        A.NamespaceLifecycle().validate(a, Ctx())
+    else:
+        with pytest.raises(m.StatusError) as e:
+            A.NamespaceLifecycle().validate(a, Ctx())
+        assert e.value.message == f'namespaces "{ns}" is forbidden: this namespace may not be deleted'

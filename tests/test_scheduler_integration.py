@@ -21,12 +21,18 @@ from amdkube.smi import FakeBackend
 from tests.conftest import run
 
 
+PRIORITIES = (0, 1, 1000)
+
+
 async def _cluster(n_nodes=3, gpus=0, **kw):
     api = await APIServer().start()
     c = Client(api.url)
     fb = FakeBackend()
     for i in range(n_nodes):
         await c.create(fake_node(i, gpus, fb))
+    for prio in PRIORITIES:       # the Priority admission plugin resolves priorityClassName
+        await c.create({"apiVersion": "scheduling.k8s.io/v1alpha1", "kind": "PriorityClass",
+                        "metadata": {"name": f"prio-{prio}"}, "value": prio})
     s = await Scheduler(Client(api.url), **kw).start()
     return api, c, s
 
@@ -44,7 +50,7 @@ def _pod(name, labels=None, gpus=0, prio=None, affinity=None, cpu="100m"):
         c["resources"]["limits"]["amd.com/gpu"] = str(gpus)
     spec = {"containers": [c]}
     if prio is not None:
-        spec["priority"] = prio
+        spec["priorityClassName"] = f"prio-{prio}"
     if affinity:
         spec["affinity"] = affinity
     return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "default", "labels": labels or {}},
