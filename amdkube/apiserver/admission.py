@@ -18,6 +18,7 @@ Plugins implemented:
 """
 from __future__ import annotations
 
+import copy
 import uuid
 
 from ..api import meta as m
@@ -887,31 +888,174 @@ class StorageObjectInUseProtection(Plugin):
                 md["finalizers"] = list(md.get("finalizers") or []) + [fin]
 
 
+_SECRET_REF_SOURCES = ("cephfs", "flexVolume", "rbd", "scaleIO", "iscsi", "storageos")
+
+
+def pod_secret_names(pod: dict) -> list[str]:
+    """pkg/api/pod VisitPodSecretNames: imagePullSecrets, env/envFrom of every (init) container,
+    and the secret-bearing volume sources."""
+    spec = pod.get("spec") or {}
+    out = [r.get("name", "") for r in spec.get("imagePullSecrets") or []]
+    for c in (spec.get("initContainers") or []) + (spec.get("containers") or []):
+        out += [ef["secretRef"].get("name", "") for ef in c.get("envFrom") or [] if ef.get("secretRef")]
+        out += [e["valueFrom"]["secretKeyRef"].get("name", "") for e in c.get("env") or []
+                if (e.get("valueFrom") or {}).get("secretKeyRef")]
+    for v in spec.get("volumes") or []:
+        if v.get("azureFile"):
+            if v["azureFile"].get("secretName"):
+                out.append(v["azureFile"]["secretName"])
+        elif v.get("projected") is not None:
+            out += [src["secret"].get("name", "") for src in v["projected"].get("sources") or [] if src.get("secret")]
+        elif v.get("secret") is not None:
+            out.append(v["secret"].get("secretName", ""))
+        else:
+            for k in _SECRET_REF_SOURCES:
+                if v.get(k) is not None:
+                    if (v[k].get("secretRef") or None) is not None:
+                        out.append(v[k]["secretRef"].get("name", ""))
+                    break
+    return out
+
+
+def pod_configmap_names(pod: dict) -> list[str]:
+    """VisitPodConfigmapNames: env/envFrom of every (init) container, configMap and projected
+    configMap volume sources."""
+    spec = pod.get("spec") or {}
+    out = []
+    for c in (spec.get("initContainers") or []) + (spec.get("containers") or []):
+        out += [ef["configMapRef"].get("name", "") for ef in c.get("envFrom") or [] if ef.get("configMapRef")]
+        out += [e["valueFrom"]["configMapKeyRef"].get("name", "") for e in c.get("env") or []
+                if (e.get("valueFrom") or {}).get("configMapKeyRef")]
+    for v in spec.get("volumes") or []:
+        if v.get("projected") is not None:
+            out += [src["configMap"].get("name", "") for src in v["projected"].get("sources") or [] if src.get("configMap")]
+        elif v.get("configMap") is not None:
+            out.append(v["configMap"].get("name", ""))
+    return out
+
+
+def node_identity(user) -> tuple[str, bool]:
+    """auth/nodeidentifier NodeIdentity: a `system:node:<name>` user in the system:nodes group."""
+    name = (user or {}).get("name", "")
+    if not name.startswith("system:node:") or "system:nodes" not in ((user or {}).get("groups") or []):
+        return "", False
+    return name[len("system:node:"):], True
+
+
 class NodeRestriction(Plugin):
-    """plugin/pkg/admission/noderestriction: a kubelet (system:node:<name> in system:nodes) may
-    create only mirror pods bound to itself, update the status of its own pods, and modify only
-    its own Node object."""
+    """plugin/pkg/admission/noderestriction/admission.go: a kubelet (system:node:<name> in
+    system:nodes) may create only mirror pods bound to itself that reference no service account,
+    secret, configmap or claim; delete and evict only pods bound to itself; update the status of
+    its own pods; touch only its own Node (no configSource on create, no new configSource on
+    update); and change nothing of a claim but status.capacity and status.conditions (with
+    ExpandPersistentVolumes)."""
     name = "NodeRestriction"
     operations = (CREATE, UPDATE, DELETE)
 
+    def __init__(self, expand_persistent_volumes: bool | None = None):
+        self.expand = expand_persistent_volumes
+
     def admit(self, a, ctx):
-        u = a.user or {}
-        if "system:nodes" not in (u.get("groups") or []) or not u.get("name", "").startswith("system:node:"):
+        node, is_node = node_identity(a.user)
+        if not is_node:
             return
-        node = u["name"][len("system:node:"):]
-        if a.resource == "nodes":
-            if a.name != node and m.name_of(a.obj or {}) != node:
-                raise m.forbidden(f'node "{node}" cannot modify node "{a.name}"')
-        elif a.resource == "pods":
-            pod = a.obj if a.operation == CREATE else (a.old or {})
-            if a.operation == CREATE and not a.subresource:
-                ann = ((pod.get("metadata") or {}).get("annotations") or {})
-                if "kubernetes.io/config.mirror" not in ann:
-                    raise m.forbidden(f'pod does not have "kubernetes.io/config.mirror" annotation, node "{node}" can only create mirror pods')
-                if (pod.get("spec") or {}).get("nodeName") != node:
-                    raise m.forbidden(f'node "{node}" can only create pods with spec.nodeName set to itself')
-            elif a.subresource in ("status", "") and (pod.get("spec") or {}).get("nodeName") != node:
-                raise m.forbidden(f'node "{node}" can only update or delete pods bound to itself')
+        if not node:
+            raise new_forbidden(a, f'could not determine node from user "{(a.user or {}).get("name", "")}"')
+        if a.resource == "pods" and not getattr(a, "group", ""):
+            if a.subresource == "":
+                return self._pod(node, a, ctx)
+            if a.subresource == "status":
+                return self._pod_status(node, a)
+            if a.subresource == "eviction":
+                return self._pod_eviction(node, a, ctx)
+            raise new_forbidden(a, f'unexpected pod subresource "{a.subresource}"')
+        if a.resource == "nodes" and not getattr(a, "group", ""):
+            return self._node(node, a)
+        if a.resource == "persistentvolumeclaims" and not getattr(a, "group", ""):
+            if a.subresource == "status":
+                return self._pvc_status(node, a)
+            raise new_forbidden(a, "may only update PVC status")
+
+    def _existing_pod(self, a, ctx, name):
+        pod = ctx.get_object("pods", a.namespace, name)
+        if pod is None:
+            raise m.not_found("pods", name)
+        return pod
+
+    def _pod(self, node, a, ctx):
+        if a.operation == CREATE:
+            pod = a.obj or {}
+            if MIRROR_POD_ANNOTATION not in m.annotations_of(pod):
+                raise new_forbidden(a, f'pod does not have "{MIRROR_POD_ANNOTATION}" annotation, node "{node}" can only '
+                                       f'create mirror pods')
+            spec = pod.get("spec") or {}
+            if spec.get("nodeName") != node:
+                raise new_forbidden(a, f'node "{node}" can only create pods with spec.nodeName set to itself')
+            if spec.get("serviceAccountName"):
+                raise new_forbidden(a, f'node "{node}" can not create pods that reference a service account')
+            if pod_secret_names(pod):
+                raise new_forbidden(a, f'node "{node}" can not create pods that reference secrets')
+            if pod_configmap_names(pod):
+                raise new_forbidden(a, f'node "{node}" can not create pods that reference configmaps')
+            if any(v.get("persistentVolumeClaim") is not None for v in spec.get("volumes") or []):
+                raise new_forbidden(a, f'node "{node}" can not create pods that reference persistentvolumeclaims')
+            return
+        if a.operation == DELETE:
+            existing = self._existing_pod(a, ctx, a.name)
+            if (existing.get("spec") or {}).get("nodeName") != node:
+                raise new_forbidden(a, f'node "{node}" can only delete pods with spec.nodeName set to itself')
+            return
+        raise new_forbidden(a, f'unexpected operation "{a.operation}"')
+
+    def _pod_status(self, node, a):
+        if a.operation != UPDATE:
+            raise new_forbidden(a, f'unexpected operation "{a.operation}"')
+        if ((a.old or {}).get("spec") or {}).get("nodeName") != node:
+            raise new_forbidden(a, f'node "{node}" can only update pod status for pods with spec.nodeName set to itself')
+
+    def _pod_eviction(self, node, a, ctx):
+        if a.operation != CREATE:
+            raise new_forbidden(a, f"unexpected operation {a.operation}")
+        name = a.name or m.name_of(a.obj or {})
+        if not name:
+            raise new_forbidden(a, "could not determine pod from request data")
+        existing = self._existing_pod(a, ctx, name)
+        if (existing.get("spec") or {}).get("nodeName") != node:
+            raise new_forbidden(a, f"node {node} can only evict pods with spec.nodeName set to itself")
+
+    def _pvc_status(self, node, a):
+        if a.operation != UPDATE:
+            raise new_forbidden(a, f'unexpected operation "{a.operation}"')
+        expand = self.expand
+        if expand is None:
+            from ..utils.features import DEFAULT
+            expand = DEFAULT("ExpandPersistentVolumes")
+        if not expand:
+            raise new_forbidden(a, f'node "{node}" may not update persistentvolumeclaim metadata')
+
+        def strip(o):
+            o = copy.deepcopy(o or {})
+            (o.get("metadata") or {}).pop("resourceVersion", None)
+            st = o.get("status") or {}
+            st.pop("capacity", None)
+            st.pop("conditions", None)
+            return o
+        if strip(a.old) != strip(a.obj):
+            raise new_forbidden(a, f'node "{node}" may not update fields other than status.capacity and '
+                                   f'status.conditions')
+
+    def _node(self, node, a):
+        requested = a.name
+        if a.operation == CREATE:
+            if ((a.obj or {}).get("spec") or {}).get("configSource") is not None:
+                raise new_forbidden(a, "cannot create with non-nil configSource")
+            requested = requested or m.name_of(a.obj or {})
+        if requested != node:
+            raise new_forbidden(a, f'node "{node}" cannot modify node "{requested}"')
+        if a.operation == UPDATE:
+            new_cs = ((a.obj or {}).get("spec") or {}).get("configSource")
+            if new_cs is not None and new_cs != ((a.old or {}).get("spec") or {}).get("configSource"):
+                raise new_forbidden(a, "cannot update configSource to a new non-nil configSource")
 
 
 class AlwaysAdmit(Plugin):

@@ -7,7 +7,9 @@ Transcribed from plugin/pkg/admission/*/admission_test.go:
   case as the Go test does), priority (TestPriorityClassAdmission, TestDefaultPriority,
   TestPodAdmission), storageclass/setdefault (TestAdmission), alwayspullimages, antiaffinity and
   exec (TestAdmission / TestInterPodAffinityAdmission / TestAdmission), and the namespace
-  lifecycle plugin (apiserver/pkg/admission/plugin/namespace/lifecycle/admission_test.go).
+  lifecycle plugin (apiserver/pkg/admission/plugin/namespace/lifecycle/admission_test.go);
+  noderestriction (TestAdmit: the pod rows as a grid over pod kind, subresource and operation,
+  then the unknown/unnamed pod, reference, node, unrelated-object and unrelated-user rows).
 """
 from __future__ import annotations
 
@@ -144,11 +146,10 @@ def test_extended_resource_toleration(desc, spec, expected):
      "Merged pod node selectors conflict with the whitelist"),
     ("env=dev", None, "env=prd", {}, None, True, False, "Default node selector conflict with the whitelist"),
 ])
-def test_pod_node_selector(default, ns_sel, whitelist, pod_sel, merged, ignore_ns, admit, name, _state={}):
-    # the Go test keeps one namespace object and only rewrites its annotation when a case sets one
-    if not ignore_ns:
-        _state["ns"] = _ns(**{A.PodNodeSelector.ANNOTATION: ns_sel})
-    ctx = Ctx(_state.get("ns") or _ns())
+def test_pod_node_selector(default, ns_sel, whitelist, pod_sel, merged, ignore_ns, admit, name):
+    # the Go test leaves the previous case's annotation in place when a case ignores the namespace
+    # selector; each of those cases decides the same without it, so a bare namespace stands in
+    ctx = Ctx(_ns() if ignore_ns else _ns(**{A.PodNodeSelector.ANNOTATION: ns_sel}))
     h = A.PodNodeSelector({"clusterDefaultNodeSelector": default, "testNamespace": whitelist})
     p = _pod(nodeSelector=dict(pod_sel))
     old = _pod(nodeSelector={"old": "true"})
@@ -452,3 +453,163 @@ def test_namespace_lifecycle_immortal(ns, ok):
         with pytest.raises(m.StatusError) as e:
             A.NamespaceLifecycle().validate(a, Ctx())
         assert e.value.message == f'namespaces "{ns}" is forbidden: this namespace may not be deleted'
+
+
+# -------------------------------------------------------------------- NodeRestriction
+MYNODE = {"name": "system:node:mynode", "groups": ["system:nodes"]}
+BOB = {"name": "bob", "groups": []}
+
+
+def _nr_pod(name, node, mirror):
+    p = {"metadata": {"name": name, "namespace": "ns"}, "spec": {"nodeName": node} if node else {}}
+    if mirror:
+        p["metadata"]["annotations"] = {"kubernetes.io/config.mirror": ""}
+    return p
+
+
+NR_PODS = {"mirrorpod-self": _nr_pod("mymirrorpod", "mynode", True), "mirrorpod-other": _nr_pod("othermirrorpod", "othernode", True),
+           "mirrorpod-unbound": _nr_pod("unboundmirrorpod", "", True), "pod-self": _nr_pod("mypod", "mynode", False),
+           "pod-other": _nr_pod("otherpod", "othernode", False), "pod-unbound": _nr_pod("unboundpod", "", False)}
+
+
+def _nr_expect(kind, sub, op):
+    """The TestAdmit rows for one pod kind, subresource and operation (admission_test.go:113-477)."""
+    bound_self = kind.endswith("-self")
+    if sub == "":
+        if op == CREATE:
+            if not kind.startswith("mirror"):
+                return "can only create mirror pods"
+            return "" if bound_self else "spec.nodeName set to itself"
+        if op == UPDATE:
+            return "forbidden: unexpected operation"
+        return "" if bound_self else "spec.nodeName set to itself"
+    if sub == "status":
+        if op == UPDATE:
+            return "" if bound_self else "spec.nodeName set to itself"
+        return "forbidden: unexpected operation"
+    if op == CREATE:
+        return "" if bound_self else "spec.nodeName set to itself"
+    return "forbidden: unexpected operation"
+
+
+NR_GRID = [(k, sub, op, unnamed) for k in NR_PODS for sub in ("", "status", "eviction")
+           for op in ((CREATE, UPDATE, DELETE)) for unnamed in ((False, True) if sub == "eviction" and op == CREATE else (False,))]
+
+
+@pytest.mark.parametrize("kind,sub,op,unnamed", NR_GRID)
+def test_node_restriction_pods(kind, sub, op, unnamed):
+    pod = NR_PODS[kind]
+    ctx = Ctx(pods=list(NR_PODS.values()))
+    if sub == "eviction":
+        obj = {"metadata": {} if unnamed else {"name": m.name_of(pod), "namespace": "ns"}}
+    else:
+        obj = None if op == DELETE else copy.deepcopy(pod)
+    old = copy.deepcopy(pod) if op == UPDATE else None
+    a = Attributes(op, "pods", sub, "ns", m.name_of(pod), obj, old, MYNODE)
+    want = _nr_expect(kind, sub, op)
+    if not want:
+        A.NodeRestriction().admit(a, ctx)
+    else:
+        with pytest.raises(m.StatusError) as e:
+            A.NodeRestriction().admit(a, ctx)
+        assert want in f"{e.value.reason.lower()}: {e.value.message}" or want in e.value.message
+
+
+CONFIG_A = {"configMapRef": {"name": "foo", "namespace": "bar", "uid": "fooUID"}}
+CONFIG_B = {"configMapRef": {"name": "qux", "namespace": "bar", "uid": "quxUID"}}
+
+
+def _node(name, cs=None):
+    return {"metadata": {"name": name}, "spec": {"configSource": cs} if cs else {}}
+
+
+@pytest.mark.parametrize("name,resource,sub,op,obj,old,aname,user,err", [
+    ("forbid delete of unknown pod", "pods", "", DELETE, None, None, "unknown", MYNODE, "not found"),
+    ("forbid create of eviction for unknown pod", "pods", "eviction", CREATE, {"metadata": {"name": "unknown"}}, None, "unknown",
+     MYNODE, "not found"),
+    ("forbid create of unnamed eviction for unknown pod", "pods", "eviction", CREATE, {"metadata": {}}, None, "unknown", MYNODE,
+     "not found"),
+    ("allow create of eviction for unnamed pod", "pods", "eviction", CREATE, {"metadata": {"name": "mypod"}}, None, "", MYNODE, ""),
+    ("forbid create of unnamed eviction for unnamed pod", "pods", "eviction", CREATE, {"metadata": {}}, None, "", MYNODE,
+     "could not determine pod from request data"),
+    ("forbid create of pod referencing service account", "pods", "", CREATE,
+     {**_nr_pod("sapod", "mynode", True), "spec": {"nodeName": "mynode", "serviceAccountName": "foo"}}, None, "sapod", MYNODE,
+     "reference a service account"),
+    ("forbid create of pod referencing secret", "pods", "", CREATE,
+     {**_nr_pod("secretpod", "mynode", True), "spec": {"nodeName": "mynode", "volumes": [{"name": "v", "secret": {"secretName": "foo"}}]}},
+     None, "secretpod", MYNODE, "reference secrets"),
+    ("forbid create of pod referencing an env secret", "pods", "", CREATE,
+     {**_nr_pod("secretpod", "mynode", True), "spec": {"nodeName": "mynode", "containers": [
+         {"name": "c", "env": [{"name": "X", "valueFrom": {"secretKeyRef": {"name": "s", "key": "k"}}}]}]}},
+     None, "secretpod", MYNODE, "reference secrets"),
+    ("forbid create of pod referencing configmap", "pods", "", CREATE,
+     {**_nr_pod("cmpod", "mynode", True), "spec": {"nodeName": "mynode", "volumes": [{"name": "v", "configMap": {"name": "foo"}}]}},
+     None, "cmpod", MYNODE, "reference configmaps"),
+    ("forbid create of pod referencing persistentvolumeclaim", "pods", "", CREATE,
+     {**_nr_pod("pvcpod", "mynode", True), "spec": {"nodeName": "mynode", "volumes": [
+         {"name": "v", "persistentVolumeClaim": {"claimName": "foo"}}]}}, None, "pvcpod", MYNODE, "reference persistentvolumeclaims"),
+    ("allow create of my node", "nodes", "", CREATE, _node("mynode"), None, "mynode", MYNODE, ""),
+    ("allow create of my node pulling name from object", "nodes", "", CREATE, _node("mynode"), None, "", MYNODE, ""),
+    ("allow update of my node", "nodes", "", UPDATE, _node("mynode"), _node("mynode"), "mynode", MYNODE, ""),
+    ("allow delete of my node", "nodes", "", DELETE, None, None, "mynode", MYNODE, ""),
+    ("allow update of my node status", "nodes", "status", UPDATE, _node("mynode"), _node("mynode"), "mynode", MYNODE, ""),
+    ("forbid create of my node with non-nil configSource", "nodes", "", CREATE, _node("mynode", CONFIG_A), None, "mynode", MYNODE,
+     "create with non-nil configSource"),
+    ("forbid update of my node: nil configSource to new non-nil configSource", "nodes", "", UPDATE, _node("mynode", CONFIG_A),
+     _node("mynode"), "mynode", MYNODE, "update configSource to a new non-nil configSource"),
+    ("forbid update of my node: non-nil configSource to new non-nil configSource", "nodes", "", UPDATE, _node("mynode", CONFIG_B),
+     _node("mynode", CONFIG_A), "mynode", MYNODE, "update configSource to a new non-nil configSource"),
+    ("allow update of my node: non-nil configSource unchanged", "nodes", "", UPDATE, _node("mynode", CONFIG_A),
+     _node("mynode", CONFIG_A), "mynode", MYNODE, ""),
+    ("allow update of my node: non-nil configSource to nil configSource", "nodes", "", UPDATE, _node("mynode"),
+     _node("mynode", CONFIG_A), "mynode", MYNODE, ""),
+    ("forbid create of other node", "nodes", "", CREATE, _node("othernode"), None, "othernode", MYNODE, "cannot modify node"),
+    ("forbid create of other node pulling name from object", "nodes", "", CREATE, _node("othernode"), None, "", MYNODE,
+     "cannot modify node"),
+    ("forbid update of other node", "nodes", "", UPDATE, _node("othernode"), _node("othernode"), "othernode", MYNODE, "cannot modify node"),
+    ("forbid delete of other node", "nodes", "", DELETE, None, None, "othernode", MYNODE, "cannot modify node"),
+    ("forbid update of other node status", "nodes", "status", UPDATE, _node("othernode"), _node("othernode"), "othernode", MYNODE,
+     "cannot modify node"),
+    ("allow create of unrelated object", "configmaps", "", CREATE, {"metadata": {}}, None, "mycm", MYNODE, ""),
+    ("allow update of unrelated object", "configmaps", "", UPDATE, {"metadata": {}}, {"metadata": {}}, "mycm", MYNODE, ""),
+    ("allow delete of unrelated object", "configmaps", "", DELETE, None, None, "mycm", MYNODE, ""),
+    ("allow unrelated user creating a normal pod unbound", "pods", "", CREATE, _nr_pod("unboundpod", "", False), None, "unboundpod",
+     BOB, ""),
+    ("allow unrelated user update of normal pod unbound", "pods", "", UPDATE, _nr_pod("unboundpod", "", False),
+     _nr_pod("unboundpod", "", False), "unboundpod", BOB, ""),
+    ("allow unrelated user delete of normal pod status unbound", "pods", "status", DELETE, None, None, "unboundpod", BOB, ""),
+    ("forbid a node user without a node name", "pods", "", CREATE, _nr_pod("x", "", True), None, "x",
+     {"name": "system:node:", "groups": ["system:nodes"]}, 'could not determine node from user "system:node:"'),
+    ("a node name without the nodes group is not a node", "nodes", "", UPDATE, _node("othernode"), _node("othernode"), "othernode",
+     {"name": "system:node:mynode", "groups": []}, ""),
+    ("forbid a claim spec update by a node", "persistentvolumeclaims", "", UPDATE, {"metadata": {"name": "c"}},
+     {"metadata": {"name": "c"}}, "c", MYNODE, "may only update PVC status"),
+])
+def test_node_restriction_table(name, resource, sub, op, obj, old, aname, user, err):
+    ctx = Ctx(pods=list(NR_PODS.values()))
+    a = Attributes(op, resource, sub, "ns", aname, copy.deepcopy(obj), copy.deepcopy(old), user)
+    if not err:
+        A.NodeRestriction().admit(a, ctx)
+    else:
+        with pytest.raises(m.StatusError) as e:
+            A.NodeRestriction().admit(a, ctx)
+        assert err in e.value.message, name
+
+
+@pytest.mark.parametrize("expand,new_status,err", [
+    (False, {"capacity": {"storage": "2Gi"}}, 'node "mynode" may not update persistentvolumeclaim metadata'),
+    (True, {"capacity": {"storage": "2Gi"}, "conditions": [{"type": "Resizing", "status": "True"}]}, ""),
+    (True, {"phase": "Lost"}, 'node "mynode" may not update fields other than status.capacity and status.conditions'),
+])
+def test_node_restriction_claim_status(expand, new_status, err):
+    old = {"metadata": {"name": "c", "resourceVersion": "1"}, "spec": {"volumeName": "v"}, "status": {"phase": "Bound"}}
+    new = copy.deepcopy(old)
+    new["metadata"]["resourceVersion"] = "2"
+    new["status"].update(new_status)
+    a = Attributes(UPDATE, "persistentvolumeclaims", "status", "ns", "c", new, old, MYNODE)
+    if err:
+        with pytest.raises(m.StatusError) as e:
+            A.NodeRestriction(expand_persistent_volumes=expand).admit(a, Ctx())
+        assert err in e.value.message
+    else:
+        A.NodeRestriction(expand_persistent_volumes=expand).admit(a, Ctx())
