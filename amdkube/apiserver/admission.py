@@ -311,13 +311,21 @@ def _forbid(pod: dict, msg: str) -> m.StatusError:
     return m.forbidden(f'pods "{name}" is forbidden: {msg}')
 
 
+def _parse_bool(v: str) -> bool:
+    """strconv.ParseBool's true spellings (anything else, errors included, is false)."""
+    return v in ("1", "t", "T", "TRUE", "true", "True")
+
+
 class ServiceAccount(Plugin):
-    """plugin/pkg/admission/serviceaccount/admission.go: default `serviceAccountName`, refuse a
-    pod naming a ServiceAccount that does not exist, mount the account's API token secret at
-    /var/run/secrets/kubernetes.io/serviceaccount in every container (unless the pod or the
-    account sets automountServiceAccountToken: false, or a container already mounts that path),
-    copy the account's imagePullSecrets into a pod without any, enforce mountable secrets when
-    the account asks for it, and keep mirror pods free of accounts and secrets.
+    """plugin/pkg/admission/serviceaccount/admission.go (create, and updates of uninitialized
+    pods): default `serviceAccountName`; refuse a pod naming a ServiceAccount that does not
+    exist; mount the first API token secret the account references (a token secret annotated
+    with the account's name and, when set, uid) at /var/run/secrets/kubernetes.io/serviceaccount
+    in every container without a mount there (unless the pod, else the account, sets
+    automountServiceAccountToken: false); copy the account's imagePullSecrets into a pod without
+    any; with the kubernetes.io/enforce-mountable-secrets annotation (or LimitSecretReferences)
+    allow only secret volumes, env secretKeyRefs and imagePullSecrets the account references;
+    keep mirror pods free of accounts and secrets.
 
     Deliberate difference: the reference also refuses a pod while the "default" account or its
     token does not exist yet (RequireAPIToken, "retry after the token is automatically
@@ -325,74 +333,115 @@ class ServiceAccount(Plugin):
     the ServiceAccount/token controllers (the benches, the node e2e setups) still start pods.
     `require_api_token=True` restores the reference's refusal."""
     name = "ServiceAccount"
-    operations = (CREATE,)
+    operations = (CREATE, UPDATE)
 
-    def __init__(self, require_api_token: bool = False):
+    def __init__(self, require_api_token: bool = False, limit_secret_references: bool = False,
+                 mount_service_account_token: bool = True):
         self.require_api_token = require_api_token
+        self.limit_secret_references = limit_secret_references
+        self.mount_token = mount_service_account_token
 
     @staticmethod
-    def _secret_names(pod: dict) -> set[str]:
-        spec = pod.get("spec") or {}
-        out = {v["secret"].get("secretName") for v in spec.get("volumes") or [] if (v.get("secret") or {}).get("secretName")}
-        for c in (spec.get("containers") or []) + (spec.get("initContainers") or []):
-            for e in c.get("env") or []:
-                ref = ((e.get("valueFrom") or {}).get("secretKeyRef") or {}).get("name")
-                if ref:
-                    out.add(ref)
-            for ef in c.get("envFrom") or []:
-                ref = (ef.get("secretRef") or {}).get("name")
-                if ref:
-                    out.add(ref)
-        return out
-
-    def _token_secret(self, sa: dict, ctx) -> str:
-        """The first API token secret the account references (getReferencedServiceAccountToken)."""
-        ns, name = m.namespace_of(sa), m.name_of(sa)
-        for ref in sa.get("secrets") or []:
-            sec = ctx.get_object("secrets", ns, ref.get("name", ""))
-            if sec and sec.get("type") == "kubernetes.io/service-account-token" and \
-                    m.annotations_of(sec).get("kubernetes.io/service-account.name") == name:
-                return m.name_of(sec)
-        return ""
+    def _ignore(a) -> bool:
+        return a.resource != "pods" or getattr(a, "group", "") or not isinstance(a.obj, dict) or \
+            (a.obj.get("kind") not in (None, "Pod")) or is_updating_initialized(a)
 
     def admit(self, a, ctx):
-        if a.resource != "pods" or a.subresource:
+        if self._ignore(a):
             return
         pod = a.obj
-        spec = pod.setdefault("spec", {})
         if MIRROR_POD_ANNOTATION in m.annotations_of(pod):
-            if spec.get("serviceAccountName") or spec.get("serviceAccount"):
-                raise _forbid(pod, "a mirror pod may not reference service accounts")
-            if self._secret_names(pod):
-                raise _forbid(pod, "a mirror pod may not reference secrets")
-            return
-        sa_name = spec.get("serviceAccountName") or spec.get("serviceAccount") or "default"
-        spec["serviceAccountName"] = sa_name
+            return self.validate(a, ctx)
+        spec = pod.setdefault("spec", {})
+        if not spec.get("serviceAccountName"):
+            spec["serviceAccountName"] = "default"
+        sa_name = spec["serviceAccountName"]
         sa = ctx.get_object("serviceaccounts", a.namespace, sa_name)
         if sa is None:
             if sa_name != "default" or self.require_api_token:
-                raise _forbid(pod, f"error looking up service account {a.namespace}/{sa_name}: "
-                                                          f"serviceaccount \"{sa_name}\" not found")
+                raise new_forbidden(a, f'error looking up service account {a.namespace}/{sa_name}: serviceaccount '
+                                       f'"{sa_name}" not found')
             return
         automount = spec.get("automountServiceAccountToken")
         if automount is None:
             automount = sa.get("automountServiceAccountToken")
-        if automount is not False:
+        if self.mount_token and automount is not False:
             self._mount_token(sa, pod, ctx)
         if not spec.get("imagePullSecrets") and sa.get("imagePullSecrets"):
             spec["imagePullSecrets"] = [dict(x) for x in sa["imagePullSecrets"]]
-        if m.annotations_of(sa).get(ENFORCE_MOUNTABLE_SECRETS) == "true":
-            allowed = {r.get("name") for r in sa.get("secrets") or []}
-            for sname in sorted(self._secret_names(pod)):
-                if sname not in allowed:
-                    raise _forbid(pod, f'volume with secret.secretName="{sname}" is not allowed '
-                                                              f"because service account {sa_name} does not reference that secret")
-            pulls = {r.get("name") for r in sa.get("imagePullSecrets") or []}
-            for i, ref in enumerate(spec.get("imagePullSecrets") or []):
-                if ref.get("name") not in pulls:
-                    raise _forbid(pod, f'imagePullSecrets[{i}].name="{ref.get("name")}" is not '
-                                                              f"allowed because service account {sa_name} does not "
-                                                              f"reference that imagePullSecret")
+        self.validate(a, ctx)
+
+    def validate(self, a, ctx):
+        if self._ignore(a):
+            return
+        pod = a.obj
+        spec = pod.get("spec") or {}
+        if MIRROR_POD_ANNOTATION in m.annotations_of(pod):
+            if spec.get("serviceAccountName"):
+                raise new_forbidden(a, "a mirror pod may not reference service accounts")
+            if pod_secret_names(pod):
+                raise new_forbidden(a, "a mirror pod may not reference secrets")
+            return
+        sa_name = spec.get("serviceAccountName", "")
+        sa = ctx.get_object("serviceaccounts", a.namespace, sa_name)
+        if sa is None:
+            if sa_name != "default" or self.require_api_token:
+                raise new_forbidden(a, f'error looking up service account {a.namespace}/{sa_name}: serviceaccount '
+                                       f'"{sa_name}" not found')
+            return
+        if self.limit_secret_references or _parse_bool(m.annotations_of(sa).get(ENFORCE_MOUNTABLE_SECRETS, "")):
+            err = self._limit_secret_references(sa, pod)
+            if err:
+                raise new_forbidden(a, err)
+
+    @staticmethod
+    def _limit_secret_references(sa: dict, pod: dict) -> str:
+        mountable = {r.get("name") for r in sa.get("secrets") or []}
+        sa_name = m.name_of(sa)
+        spec = pod.get("spec") or {}
+        for v in spec.get("volumes") or []:
+            if v.get("secret") is not None and v["secret"].get("secretName", "") not in mountable:
+                return (f'volume with secret.secretName="{v["secret"].get("secretName", "")}" is not allowed because '
+                        f"service account {sa_name} does not reference that secret")
+        for kind, what in (("initContainers", "init container"), ("containers", "container")):
+            for c in spec.get(kind) or []:
+                for e in c.get("env") or []:
+                    ref = (e.get("valueFrom") or {}).get("secretKeyRef")
+                    if ref is not None and ref.get("name", "") not in mountable:
+                        return (f'{what} {c.get("name", "")} with envVar {e.get("name", "")} referencing '
+                                f'secret.secretName="{ref.get("name", "")}" is not allowed because service account '
+                                f"{sa_name} does not reference that secret")
+        pulls = {r.get("name") for r in sa.get("imagePullSecrets") or []}
+        for i, ref in enumerate(spec.get("imagePullSecrets") or []):
+            if ref.get("name") not in pulls:
+                return (f'imagePullSecrets[{i}].name="{ref.get("name", "")}" is not allowed because service account '
+                        f"{sa_name} does not reference that imagePullSecret")
+        return ""
+
+    @staticmethod
+    def service_account_tokens(sa: dict, ctx) -> list[dict]:
+        """getServiceAccountTokens: the namespace's token secrets that belong to the account
+        (IsServiceAccountToken: the name annotation matches, the uid annotation when set)."""
+        out = []
+        for sec in ctx.list_objects("secrets", m.namespace_of(sa)):
+            if sec.get("type") != "kubernetes.io/service-account-token":
+                continue
+            ann = m.annotations_of(sec)
+            if ann.get("kubernetes.io/service-account.name") != m.name_of(sa):
+                continue
+            uid = ann.get("kubernetes.io/service-account.uid", "")
+            if uid and uid != (sa.get("metadata") or {}).get("uid", ""):
+                continue
+            out.append(sec)
+        return out
+
+    def _token_secret(self, sa: dict, ctx) -> str:
+        """getReferencedServiceAccountToken: the first of the account's secrets that is one of
+        its tokens."""
+        if not sa.get("secrets"):
+            return ""
+        tokens = {m.name_of(t) for t in self.service_account_tokens(sa, ctx)}
+        return next((r.get("name") for r in sa["secrets"] if r.get("name") in tokens), "")
 
     def _mount_token(self, sa: dict, pod: dict, ctx):
         token = self._token_secret(sa, ctx)
@@ -403,7 +452,7 @@ class ServiceAccount(Plugin):
                                                           f"automatically created and added to the service account")
             return
         spec = pod["spec"]
-        volumes = spec.setdefault("volumes", [])
+        volumes = spec.get("volumes") or []
         vol_name = next((v["name"] for v in volumes if (v.get("secret") or {}).get("secretName") == token), "")
         has_volume = bool(vol_name)
         if not vol_name:
@@ -416,7 +465,7 @@ class ServiceAccount(Plugin):
             c.setdefault("volumeMounts", []).append({"name": vol_name, "readOnly": True, "mountPath": SA_TOKEN_MOUNT_PATH})
             need = True
         if need and not has_volume:
-            volumes.append({"name": vol_name, "secret": {"secretName": token}})
+            spec["volumes"] = list(volumes) + [{"name": vol_name, "secret": {"secretName": token}}]
 
 
 NOT_READY_TAINT_KEY = "node.kubernetes.io/not-ready"

@@ -613,3 +613,174 @@ def test_node_restriction_claim_status(expand, new_status, err):
         assert err in e.value.message
     else:
         A.NodeRestriction(expand_persistent_volumes=expand).admit(a, Ctx())
+
+
+# --------------------------------------------------------------------- ServiceAccount
+TOKEN_PATH = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+
+def _sa(name="default", uid="12345", secrets=(), pulls=(), ann=None, ns="myns"):
+    md = {"name": name, "namespace": ns, "uid": uid}
+    if ann:
+        md["annotations"] = ann
+    return {"metadata": md, "secrets": [{"name": s} for s in secrets], "imagePullSecrets": [{"name": s} for s in pulls]}
+
+
+def _token(name, sa="default", uid="12345", type_="kubernetes.io/service-account-token", ns="myns"):
+    return {"metadata": {"name": name, "namespace": ns, "annotations": {
+        "kubernetes.io/service-account.name": sa, "kubernetes.io/service-account.uid": uid}}, "type": type_}
+
+
+def _sa_attrs(pod, op=CREATE, old=None, resource="pods"):
+    return Attributes(op, resource, "", "myns", "myname", pod, old, {})
+
+
+def test_service_account_ignores():
+    h = A.ServiceAccount()
+    assert not h.handles(DELETE) and not h.handles(CONNECT) and h.handles(CREATE) and h.handles(UPDATE)
+    pod, old = {"spec": {}}, {"spec": {}}
+    h.admit(_sa_attrs(pod, UPDATE, old), Ctx())                      # update of an initialized pod
+    assert "serviceAccountName" not in pod["spec"]
+    h.admit(_sa_attrs({"spec": {}}, resource="configmaps"), Ctx())   # not a pod resource
+    h.admit(_sa_attrs(None), Ctx())                                  # nil object
+    h.admit(_sa_attrs({"kind": "Binding", "target": {}}), Ctx())     # not a pod object
+    mirror = {"metadata": {"annotations": {"kubernetes.io/config.mirror": "true"}}, "spec": {"containers": [{}]}}
+    h.admit(_sa_attrs(mirror), Ctx())
+    assert "serviceAccountName" not in mirror["spec"]
+
+
+@pytest.mark.parametrize("spec,msg", [
+    ({"serviceAccountName": "default"}, "a mirror pod may not reference service accounts"),
+    ({"volumes": [{"name": "v", "secret": {"secretName": "mysecret"}}]}, "a mirror pod may not reference secrets"),
+    ({"imagePullSecrets": [{"name": "pull"}]}, "a mirror pod may not reference secrets"),
+])
+def test_service_account_rejects_mirror_pods(spec, msg):
+    pod = {"metadata": {"annotations": {"kubernetes.io/config.mirror": "true"}}, "spec": spec}
+    with pytest.raises(m.StatusError) as e:
+        A.ServiceAccount().admit(_sa_attrs(pod), Ctx())
+    assert e.value.message == f'pods "myname" is forbidden: {msg}'
+
+
+def test_service_account_missing_token():
+    ctx = Ctx(serviceaccounts=[_sa()])
+    pod = {"spec": {"containers": [{}]}}
+    A.ServiceAccount().admit(_sa_attrs(pod), ctx)                    # tolerates a missing API token
+    assert pod["spec"]["serviceAccountName"] == "default" and not pod["spec"].get("volumes")
+    with pytest.raises(m.StatusError) as e:
+        A.ServiceAccount(require_api_token=True).admit(_sa_attrs({"spec": {"containers": [{}]}}), ctx)
+    assert e.value.code == 504 and e.value.reason == "ServerTimeout"
+    assert e.value.message == ('No API token found for service account "default", retry after the token is automatically '
+                               'created and added to the service account')
+
+
+def test_service_account_denies_invalid_service_account():
+    with pytest.raises(m.StatusError) as e:
+        A.ServiceAccount().admit(_sa_attrs({"spec": {"serviceAccountName": "other", "containers": [{}]}}), Ctx())
+    assert e.value.message == ('pods "myname" is forbidden: error looking up service account myns/other: serviceaccount '
+                               '"other" not found')
+
+
+def test_service_account_automounts_api_token():
+    ctx = Ctx(serviceaccounts=[_sa(secrets=["token-name"])], secrets=[_token("token-name")])
+    want_vol = {"name": "token-name", "secret": {"secretName": "token-name"}}
+    want_mount = {"name": "token-name", "readOnly": True, "mountPath": TOKEN_PATH}
+    h = A.ServiceAccount(require_api_token=True)
+    pod = {"spec": {"containers": [{}]}}
+    h.admit(_sa_attrs(pod), ctx)
+    assert pod["spec"]["volumes"] == [want_vol] and pod["spec"]["containers"][0]["volumeMounts"] == [want_mount]
+    # an update of an uninitialized pod is admitted like a create; the old pod's mounts do not count
+    old = {"metadata": {"initializers": {"pending": [{"name": "init"}]}},
+           "spec": {"containers": [{"volumeMounts": [{"name": "wrong-token-name", "readOnly": True, "mountPath": TOKEN_PATH}]}]}}
+    pod = {"spec": {"containers": [{}]}}
+    h.admit(_sa_attrs(pod, UPDATE, old), ctx)
+    assert pod["spec"]["volumes"] == [want_vol] and pod["spec"]["containers"][0]["volumeMounts"] == [want_mount]
+    # init containers get the mount too
+    pod = {"spec": {"initContainers": [{}], "containers": [{}]}}
+    h.admit(_sa_attrs(pod), ctx)
+    assert pod["spec"]["initContainers"][0]["volumeMounts"] == [want_mount] and len(pod["spec"]["volumes"]) == 1
+
+
+def test_service_account_respects_existing_mount():
+    ctx = Ctx(serviceaccounts=[_sa(secrets=["token-name"])], secrets=[_token("token-name")])
+    mine = {"name": "my-custom-mount", "readOnly": False, "mountPath": TOKEN_PATH}
+    pod = {"spec": {"containers": [{"volumeMounts": [dict(mine)]}]}}
+    A.ServiceAccount(require_api_token=True).admit(_sa_attrs(pod), ctx)
+    assert pod["spec"]["containers"][0]["volumeMounts"] == [mine] and not pod["spec"].get("volumes")
+
+
+def test_service_account_token_volume_name_collision():
+    ctx = Ctx(serviceaccounts=[_sa(secrets=["token-name"])], secrets=[_token("token-name")])
+    pod = {"spec": {"containers": [{}], "volumes": [{"name": "token-name", "emptyDir": {}}]}}
+    A.ServiceAccount().admit(_sa_attrs(pod), ctx)
+    vol = pod["spec"]["volumes"][1]
+    assert vol["name"].startswith("token-name-") and vol["secret"] == {"secretName": "token-name"}
+    assert pod["spec"]["containers"][0]["volumeMounts"][0]["name"] == vol["name"]
+
+
+ENFORCE = {"kubernetes.io/enforce-mountable-secrets": "true"}
+
+
+@pytest.mark.parametrize("spec", [
+    {"volumes": [{"name": "foo", "secret": {"secretName": "foo"}}], "containers": [{}]},
+    {"initContainers": [{"name": "container-1", "env": [{"name": "env-1", "valueFrom": {"secretKeyRef": {"name": "foo"}}}]}]},
+    {"containers": [{"name": "container-1", "env": [{"name": "env-1", "valueFrom": {"secretKeyRef": {"name": "foo"}}}]}]},
+])
+def test_service_account_allows_referenced_secret(spec):
+    ctx = Ctx(serviceaccounts=[_sa(secrets=["foo"], ann=ENFORCE)])
+    A.ServiceAccount().admit(_sa_attrs({"spec": copy.deepcopy(spec)}), ctx)
+
+
+@pytest.mark.parametrize("spec,msg", [
+    ({"volumes": [{"name": "foo", "secret": {"secretName": "foo"}}], "containers": [{}]},
+     'volume with secret.secretName="foo" is not allowed because service account default does not reference that secret'),
+    ({"initContainers": [{"name": "container-1", "env": [{"name": "env-1", "valueFrom": {"secretKeyRef": {"name": "foo"}}}]}]},
+     'init container container-1 with envVar env-1 referencing secret.secretName="foo" is not allowed because service account '
+     'default does not reference that secret'),
+    ({"containers": [{"name": "container-2", "env": [{"name": "env-1", "valueFrom": {"secretKeyRef": {"name": "foo"}}}]}]},
+     'container container-2 with envVar env-1 referencing secret.secretName="foo" is not allowed because service account '
+     'default does not reference that secret'),
+])
+def test_service_account_rejects_unreferenced_secrets(spec, msg):
+    ctx = Ctx(serviceaccounts=[_sa(ann=ENFORCE)])
+    with pytest.raises(m.StatusError) as e:
+        A.ServiceAccount().admit(_sa_attrs({"spec": copy.deepcopy(spec)}), ctx)
+    assert e.value.message == f'pods "myname" is forbidden: {msg}'
+    # a permissive account (annotation false or absent) allows them; LimitSecretReferences enforces for all
+    A.ServiceAccount().admit(_sa_attrs({"spec": copy.deepcopy(spec)}),
+                             Ctx(serviceaccounts=[_sa(ann={"kubernetes.io/enforce-mountable-secrets": "false"})]))
+    with pytest.raises(m.StatusError):
+        A.ServiceAccount(limit_secret_references=True).admit(_sa_attrs({"spec": copy.deepcopy(spec)}), Ctx(serviceaccounts=[_sa()]))
+
+
+def test_service_account_image_pull_secrets():
+    enforce = Ctx(serviceaccounts=[_sa(pulls=["foo"], ann=ENFORCE)])
+    A.ServiceAccount().admit(_sa_attrs({"spec": {"imagePullSecrets": [{"name": "foo"}]}}), enforce)
+    with pytest.raises(m.StatusError) as e:
+        A.ServiceAccount().admit(_sa_attrs({"spec": {"imagePullSecrets": [{"name": "bar"}]}}), enforce)
+    assert e.value.message == ('pods "myname" is forbidden: imagePullSecrets[0].name="bar" is not allowed because service '
+                               'account default does not reference that imagePullSecret')
+    ctx = Ctx(serviceaccounts=[_sa(pulls=["foo", "bar"])])
+    pod = {"spec": {"imagePullSecrets": [{"name": "lalala"}]}}          # TestDoNotAddImagePullSecrets
+    A.ServiceAccount().admit(_sa_attrs(pod), ctx)
+    assert pod["spec"]["imagePullSecrets"] == [{"name": "lalala"}]
+    pod = {"spec": {}}                                                  # TestAddImagePullSecrets
+    A.ServiceAccount().admit(_sa_attrs(pod), ctx)
+    assert pod["spec"]["imagePullSecrets"] == [{"name": "foo"}, {"name": "bar"}]
+
+
+def test_service_account_multiple_referenced_secrets():
+    ctx = Ctx(serviceaccounts=[_sa("mysa", "mysauid", secrets=["token1", "token2"])],
+              secrets=[_token("token2", "mysa", "mysauid"), _token("token1", "mysa", "mysauid")])
+    pod = {"spec": {"serviceAccountName": "mysa", "containers": [{"name": "container-1"}]}}
+    A.ServiceAccount(require_api_token=True).admit(_sa_attrs(pod), ctx)
+    assert [v["name"] for v in pod["spec"]["volumes"]] == ["token1"]
+
+
+def test_get_service_account_tokens():
+    sa = _sa(ns="namespace")
+    secrets = [_token("nonSATokenSecret", type_="kubernetes.io/dockercfg", ns="namespace"),
+               _token("differentSAToken", sa="someOtherSA", ns="namespace"),
+               _token("differentUID", uid="someOtherUID", ns="namespace"),
+               _token("matchingSAToken", ns="namespace")]
+    got = A.ServiceAccount.service_account_tokens(sa, Ctx(secrets=secrets))
+    assert [m.name_of(s) for s in got] == ["matchingSAToken"]
