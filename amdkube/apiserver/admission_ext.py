@@ -392,15 +392,17 @@ PRESET_ANNOTATION_PREFIX = "podpreset.admission.kubernetes.io"
 
 
 class PodPreset(Plugin):
-    """podpreset/admission.go: presets whose selector matches a new pod inject env, envFrom,
-    volumeMounts into every container and volumes into the pod; any conflict (same env name or
-    volume name or mount path with a different definition) leaves the pod untouched; each
+    """podpreset/admission.go: on pod creation (mirror pods and pods annotated
+    podpreset.admission.kubernetes.io/exclude=true aside) every preset of the namespace whose
+    selector matches the pod's labels is merged in — volumes by name, each container's env by
+    name, volumeMounts by name and by mount path, envFrom appended — unless any of them conflicts
+    (same name or path, another definition), in which case the pod is left untouched; each
     applied preset is recorded as podpreset.admission.kubernetes.io/podpreset-<name>=<rv>."""
     name = "PodPreset"
     operations = (CREATE,)
 
     def admit(self, a, ctx):
-        if not _is_pod(a) or a.obj is None:
+        if not _is_pod(a) or a.obj is None or a.operation != CREATE:
             return
         pod = a.obj
         ann = m.annotations_of(pod)
@@ -411,51 +413,70 @@ class PodPreset(Plugin):
                    if selector_from_label_selector((p.get("spec") or {}).get("selector") or {}).matches(labels)]
         if not presets:
             return
-        try:
-            merged = self._merge(pod, presets)
-        except ValueError as e:
-            log.info("conflict applying pod presets to %s/%s: %s", a.namespace, m.name_of(pod), e)
+        errs = self.conflicts(pod, presets)
+        if errs:
+            log.warning("conflict occurred while applying podpresets: %s on pod: %s err: %s",
+                        ",".join(m.name_of(p) for p in presets), (pod.get("metadata") or {}).get("generateName", ""), errs)
             return
-        pod["spec"] = merged
-        md = pod.setdefault("metadata", {})
-        md.setdefault("annotations", {}).update(
-            {f"{PRESET_ANNOTATION_PREFIX}/podpreset-{m.name_of(p)}": (p.get("metadata") or {}).get("resourceVersion", "")
-             for p in presets})
+        self.apply(pod, presets)
 
     @staticmethod
-    def _merge(pod, presets):
-        spec = copy.deepcopy(pod.get("spec") or {})
-        vols = {v["name"]: v for v in spec.get("volumes") or []}
+    def _merge_by(items, presets, field, keys, what):
+        """mergeEnv / mergeVolumes / mergeVolumeMounts: the originals, then each preset item
+        whose key is new; an existing key with another definition is an error."""
+        merged = list(items or [])
+        seen = [{it.get(k): it for it in merged} for k in keys]
+        errs = []
         for p in presets:
-            for v in (p.get("spec") or {}).get("volumes") or []:
-                if v["name"] in vols and vols[v["name"]] != v:
-                    raise ValueError(f"merging volume {v['name']} for {m.name_of(p)} has a conflict")
-                vols.setdefault(v["name"], v)
-        spec["volumes"] = list(vols.values()) if vols else spec.get("volumes")
-        if spec.get("volumes") is None:
+            for it in (p.get("spec") or {}).get(field) or []:
+                new = True
+                for idx, k in enumerate(keys):
+                    found = seen[idx].get(it.get(k))
+                    if found is None:
+                        seen[idx][it.get(k)] = it
+                    else:
+                        if idx == 0:
+                            new = False
+                        if found != it:
+                            on = it.get(k) if k == "name" else f"mount path {it.get(k)}"
+                            errs.append(f"merging {what} for {m.name_of(p)} has a conflict on {on}")
+                if new:
+                    merged.append(it)
+        return merged, errs
+
+    @classmethod
+    def conflicts(cls, pod, presets) -> list[str]:
+        """safeToApplyPodPresetsOnPod."""
+        spec = pod.get("spec") or {}
+        errs = cls._merge_by(spec.get("volumes"), presets, "volumes", ("name",), "volumes")[1]
+        for c in spec.get("containers") or []:
+            errs += cls._merge_by(c.get("env"), presets, "env", ("name",), "env")[1]
+            errs += cls._merge_by(c.get("volumeMounts"), presets, "volumeMounts", ("name", "mountPath"), "volume mounts")[1]
+        return errs
+
+    @classmethod
+    def apply(cls, pod, presets):
+        """applyPodPresetsOnPod."""
+        spec = pod.setdefault("spec", {})
+        vols = cls._merge_by(spec.get("volumes"), presets, "volumes", ("name",), "volumes")[0]
+        if vols:
+            spec["volumes"] = vols
+        else:
             spec.pop("volumes", None)
         for c in spec.get("containers") or []:
-            env = {e["name"]: e for e in c.get("env") or []}
-            mounts = {vm["mountPath"]: vm for vm in c.get("volumeMounts") or []}
-            env_from = list(c.get("envFrom") or [])
-            for p in presets:
-                ps = p.get("spec") or {}
-                for e in ps.get("env") or []:
-                    if e["name"] in env and env[e["name"]] != e:
-                        raise ValueError(f"merging env for {m.name_of(p)} has a conflict on {e['name']}")
-                    env.setdefault(e["name"], e)
-                for vm in ps.get("volumeMounts") or []:
-                    if vm["mountPath"] in mounts and mounts[vm["mountPath"]] != vm:
-                        raise ValueError(f"merging volume mounts for {m.name_of(p)} has a conflict on mount path {vm['mountPath']}")
-                    mounts.setdefault(vm["mountPath"], vm)
-                env_from += [x for x in ps.get("envFrom") or [] if x not in env_from]
-            if env:
-                c["env"] = list(env.values())
-            if mounts:
-                c["volumeMounts"] = list(mounts.values())
+            for field, keys, what in (("env", ("name",), "env"), ("volumeMounts", ("name", "mountPath"), "volume mounts")):
+                merged = cls._merge_by(c.get(field), presets, field, keys, what)[0]
+                if merged:
+                    c[field] = merged
+            env_from = list(c.get("envFrom") or []) + [x for p in presets for x in (p.get("spec") or {}).get("envFrom") or []]
             if env_from:
                 c["envFrom"] = env_from
-        return spec
+        md = pod.setdefault("metadata", {})
+        if md.get("annotations") is None:
+            md["annotations"] = {}
+        for p in presets:
+            md["annotations"][f"{PRESET_ANNOTATION_PREFIX}/podpreset-{m.name_of(p)}"] = \
+                (p.get("metadata") or {}).get("resourceVersion", "")
 
 
 # ---------------------------------------------------------- PodTolerationRestriction

@@ -784,3 +784,92 @@ def test_get_service_account_tokens():
                _token("matchingSAToken", ns="namespace")]
     got = A.ServiceAccount.service_account_tokens(sa, Ctx(secrets=secrets))
     assert [m.name_of(s) for s in got] == ["matchingSAToken"]
+
+
+# -------------------------------------------------------------------------- PodPreset
+def _pp(name="hello", **spec):
+    return {"metadata": {"name": name, "namespace": "namespace", "resourceVersion": "1"},
+            "spec": {"selector": {"matchExpressions": [{"key": "security", "operator": "In", "values": ["S2"]}]}, **spec}}
+
+
+def _env(*kv):
+    return [{"name": k, "value": v} for k, v in kv]
+
+
+def _vm(*np):
+    return [{"name": n, "mountPath": p} for n, p in np]
+
+
+@pytest.mark.parametrize("field,keys,what,orig,mod,result", [
+    ("env", ("name",), "env", None, _env(("abc", "value2"), ("ABC", "value3")), _env(("abc", "value2"), ("ABC", "value3"))),
+    ("env", ("name",), "env", _env(("abcd", "value2"), ("hello", "value3")), _env(("abc", "value2"), ("ABC", "value3")),
+     _env(("abcd", "value2"), ("hello", "value3"), ("abc", "value2"), ("ABC", "value3"))),
+    ("env", ("name",), "env", _env(("abc", "value3")), _env(("abc", "value2"), ("ABC", "value3")), None),
+    ("env", ("name",), "env", _env(("abc", "value2"), ("hello", "value3")), _env(("abc", "value2"), ("ABC", "value3")),
+     _env(("abc", "value2"), ("hello", "value3"), ("ABC", "value3"))),
+    ("volumeMounts", ("name", "mountPath"), "volume mounts", None, _vm(("simply-mounted-volume", "/opt/")),
+     _vm(("simply-mounted-volume", "/opt/"))),
+    ("volumeMounts", ("name", "mountPath"), "volume mounts", _vm(("etc-volume", "/etc/")), _vm(("simply-mounted-volume", "/opt/")),
+     _vm(("etc-volume", "/etc/"), ("simply-mounted-volume", "/opt/"))),
+    ("volumeMounts", ("name", "mountPath"), "volume mounts", _vm(("etc-volume", "/etc/")),
+     _vm(("simply-mounted-volume", "/opt/"), ("etc-volume", "/things/")), None),                     # conflict on name
+    ("volumeMounts", ("name", "mountPath"), "volume mounts", _vm(("etc-volume", "/etc/")),
+     _vm(("simply-mounted-volume", "/opt/"), ("things-volume", "/etc/")), None),                     # conflict on mount path
+    ("volumeMounts", ("name", "mountPath"), "volume mounts", _vm(("etc-volume", "/etc/")),
+     _vm(("simply-mounted-volume", "/opt/"), ("etc-volume", "/etc/")), _vm(("etc-volume", "/etc/"), ("simply-mounted-volume", "/opt/"))),
+    ("volumes", ("name",), "volumes", None, [{"name": "vol", "emptyDir": {}}], [{"name": "vol", "emptyDir": {}}]),
+    ("volumes", ("name",), "volumes", [{"name": "etc-volume", "hostPath": {"path": "/etc"}}], [{"name": "vol", "emptyDir": {}}],
+     [{"name": "etc-volume", "hostPath": {"path": "/etc"}}, {"name": "vol", "emptyDir": {}}]),
+    ("volumes", ("name",), "volumes", [{"name": "vol", "hostPath": {"path": "/etc"}}], [{"name": "vol", "emptyDir": {}}], None),
+    ("volumes", ("name",), "volumes", [{"name": "vol", "emptyDir": {}}], [{"name": "vol", "emptyDir": {}}],
+     [{"name": "vol", "emptyDir": {}}]),
+])
+def test_pod_preset_merges(field, keys, what, orig, mod, result):
+    merged, errs = X.PodPreset._merge_by(orig, [_pp(**{field: mod})], field, keys, what)
+    if result is None:
+        assert errs and errs[0].startswith(f"merging {what} for hello has a conflict on")
+    else:
+        assert not errs and merged == result
+
+
+def test_pod_preset_env_from_is_appended():
+    cm = {"configMapRef": {"name": "abc"}}
+    pod = {"metadata": {"name": "mypod", "labels": {"security": "S2"}}, "spec": {"containers": [
+        {"name": "c", "envFrom": [{"configMapRef": {"name": "thing"}}]}]}}
+    X.PodPreset.apply(pod, [_pp(envFrom=[cm, {"prefix": "pre_", **cm}])])
+    assert pod["spec"]["containers"][0]["envFrom"] == [{"configMapRef": {"name": "thing"}}, cm, {"prefix": "pre_", **cm}]
+
+
+def _preset_pod(labels=None, ann=None):
+    md = {"name": "mypod", "namespace": "namespace", "labels": labels if labels is not None else {"security": "S2"}}
+    if ann:
+        md["annotations"] = ann
+    return {"metadata": md, "spec": {"containers": [{"name": "mycontainer", "image": "image",
+                                                     "env": _env(("abc", "value2"), ("ABC", "value3"))}]}}
+
+
+def _preset_admit(pod, presets, ns="namespace"):
+    ctx = Ctx(podpresets=presets)
+    ctx.list_objects = lambda plural, n, group="": [p for p in presets if m.namespace_of(p) == n]
+    X.PodPreset().admit(Attributes(CREATE, "pods", "", ns, "mypod", pod, None, {}), ctx)
+
+
+def test_pod_preset_admit():
+    good = _pp(env=_env(("abcd", "value")), volumeMounts=_vm(("etc-volume", "/etc/")),
+               volumes=[{"name": "etc-volume", "hostPath": {"path": "/etc"}}], envFrom=[{"configMapRef": {"name": "abc"}}])
+    pod = _preset_pod()
+    _preset_admit(pod, [good])                                                        # TestAdmit
+    c = pod["spec"]["containers"][0]
+    assert c["env"] == _env(("abc", "value2"), ("ABC", "value3"), ("abcd", "value"))
+    assert c["volumeMounts"] == _vm(("etc-volume", "/etc/")) and c["envFrom"] == [{"configMapRef": {"name": "abc"}}]
+    assert pod["spec"]["volumes"] == [{"name": "etc-volume", "hostPath": {"path": "/etc"}}]
+    assert pod["metadata"]["annotations"] == {"podpreset.admission.kubernetes.io/podpreset-hello": "1"}
+    conflicting = _pp(env=_env(("abc", "value")))
+    for pod, presets, ns in ((_preset_pod(), [conflicting], "othernamespace"),              # DifferentNamespaceShouldDoNothing
+                             (_preset_pod(labels={"security": "S1"}), [conflicting], "namespace"),   # NonMatchingLabels
+                             (_preset_pod(), [conflicting], "namespace"),                   # ConflictShouldNotModifyPod
+                             (_preset_pod(ann={"kubernetes.io/config.mirror": "mirror"}), [good], "namespace"),   # MirrorPod
+                             (_preset_pod(ann={"podpreset.admission.kubernetes.io/exclude": "true"}), [good], "namespace")):
+        before = copy.deepcopy(pod)
+        _preset_admit(pod, presets, ns)
+        assert pod == before
