@@ -78,13 +78,15 @@ class LimitPodHardAntiAffinityTopology(Plugin):
 
 # ------------------------------------------------------------------- EventRateLimit
 class _Bucket:
-    __slots__ = ("qps", "burst", "tokens", "t")
+    """flowcontrol token bucket: starts full (burst tokens), refills at qps; TryAccept."""
+    __slots__ = ("qps", "burst", "tokens", "t", "clock")
 
-    def __init__(self, qps, burst):
-        self.qps, self.burst, self.tokens, self.t = float(qps), int(burst), float(burst), time.monotonic()
+    def __init__(self, qps, burst, clock=time.monotonic):
+        self.qps, self.burst, self.tokens, self.clock = float(qps), int(burst), float(burst), clock
+        self.t = clock()
 
     def take(self) -> bool:
-        now = time.monotonic()
+        now = self.clock()
         self.tokens = min(self.burst, self.tokens + (now - self.t) * self.qps)
         self.t = now
         if self.tokens >= 1.0:
@@ -94,14 +96,22 @@ class _Bucket:
 
 
 class EventRateLimit(Plugin):
-    """eventratelimit/admission.go + config.go: token buckets per limit type (Server,
-    Namespace, User, SourceAndObject), the last two in LRU caches of cacheSize; an event over
-    any limit is rejected with 429."""
+    """eventratelimit/admission.go + limitenforcer.go: one token bucket per limit (Server), or per
+    key in an LRU cache of cacheSize (default 4096) for Namespace, User and SourceAndObject (the
+    source component and host and the involved object's kind, namespace, name, uid and
+    apiVersion, concatenated); every limit takes its token for each Event create or update, and
+    any exhausted one rejects it with 429 "limit reached on type T for key K"."""
     name = "EventRateLimit"
-    operations = (CREATE,)
+    operations = (CREATE, UPDATE)
+    DEFAULT_CACHE_SIZE = 4096
+    TYPES = ("Server", "Namespace", "User", "SourceAndObject")
 
-    def __init__(self, limits=None):
+    def __init__(self, limits=None, clock=time.monotonic):
         self.limits = limits or [{"type": "Server", "qps": 5000, "burst": 20000}]
+        for lim in self.limits:
+            if lim.get("type") not in self.TYPES:
+                raise ValueError(f"unknown event rate limit type: {lim.get('type')}")
+        self.clock = clock
         self.caches: list[tuple[dict, dict]] = [(lim, {}) for lim in self.limits]
 
     @staticmethod
@@ -113,25 +123,35 @@ class EventRateLimit(Plugin):
             return a.namespace
         if t == "User":
             return (a.user or {}).get("name", "")
-        if t == "SourceAndObject":
-            ev = a.obj or {}
-            src, io = ev.get("source") or {}, ev.get("involvedObject") or {}
-            return "/".join(str(x) for x in (src.get("component"), src.get("host"), io.get("kind"), io.get("namespace"),
-                                             io.get("name"), io.get("uid"), io.get("apiVersion")))
-        raise ValueError(f"unknown EventRateLimit type {t!r}")
+        ev = a.obj if isinstance(a.obj, dict) else {}
+        src, io = ev.get("source") or {}, ev.get("involvedObject") or {}
+        return "".join(str(x or "") for x in (src.get("component"), src.get("host"), io.get("kind"), io.get("namespace"),
+                                               io.get("name"), io.get("uid"), io.get("apiVersion")))
+
+    def _bucket(self, lim, cache, key):
+        if lim.get("type") == "Server":
+            b = cache.get("")
+            if b is None:
+                b = cache[""] = _Bucket(lim.get("qps", 10), lim.get("burst", 100), self.clock)
+            return b
+        b = cache.pop(key, None) or _Bucket(lim.get("qps", 10), lim.get("burst", 100), self.clock)
+        cache[key] = b                                   # most recently used last
+        size = int(lim.get("cacheSize") or self.DEFAULT_CACHE_SIZE)
+        while len(cache) > size:
+            cache.pop(next(iter(cache)))
+        return b
 
     def validate(self, a, ctx):
-        if a.resource != "events":
+        kind = a.kind or ((a.obj or {}).get("kind") if isinstance(a.obj, dict) else "")
+        if kind != "Event" or getattr(a, "group", ""):
             return
+        rejection = None
         for lim, cache in self.caches:
             k = self._key(lim, a)
-            b = cache.pop(k, None) or _Bucket(lim.get("qps", 10), lim.get("burst", 100))
-            cache[k] = b                                   # most recently used last
-            size = int(lim.get("cacheSize", 4096))
-            while len(cache) > size:
-                cache.pop(next(iter(cache)))
-            if not b.take():
-                raise m.too_many_requests("limit reached on type %s for key %s" % (lim.get("type"), k))
+            if not self._bucket(lim, cache, k).take():
+                rejection = m.too_many_requests(f"limit reached on type {lim.get('type')} for key {k}")
+        if rejection is not None:
+            raise rejection
 
 
 # ---------------------------------------------------------------- exec restrictions

@@ -74,7 +74,7 @@ def test_always_pull_and_antiaffinity_and_scdeny():
 def test_event_rate_limit_buckets():
     plug = X.EventRateLimit([{"type": "Namespace", "qps": 0.001, "burst": 3, "cacheSize": 2},
                              {"type": "Server", "qps": 0.001, "burst": 100}])
-    ev = {"metadata": {"name": "e", "namespace": "ns"}, "involvedObject": {"kind": "Pod"}}
+    ev = {"kind": "Event", "metadata": {"name": "e", "namespace": "ns"}, "involvedObject": {"kind": "Pod"}}
     for _ in range(3):
         plug.validate(attrs(ev, resource="events"), Ctx())
     with pytest.raises(m.StatusError) as ei:

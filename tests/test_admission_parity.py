@@ -873,3 +873,107 @@ def test_pod_preset_admit():
         before = copy.deepcopy(pod)
         _preset_admit(pod, presets, ns)
         assert pod == before
+
+
+# --------------------------------------------------------------------- EventRateLimit
+def _rq(kind="Event", ns="", user="", event=None, delay=0, ok=True):
+    return (kind, ns, user, event, delay, ok)
+
+
+def _soi(factory):
+    """createSourceAndObjectKeyInclusionRequests."""
+    return [_rq(event=factory("A")), _rq(event=factory("A"), ok=False), _rq(event=factory("B"))]
+
+
+def _comp(c):
+    return {"source": {"component": c}}
+
+
+NS_A, NS_B = "A", "B"
+ERL_CASES = [
+    ("event not blocked when tokens available", dict(server=3), [_rq()]),
+    ("non-event not blocked", dict(server=3), [_rq("NonEvent")]),
+    ("event blocked after tokens exhausted", dict(server=3), [_rq(), _rq(), _rq(), _rq(ok=False)]),
+    ("non-event not blocked after tokens exhausted", dict(server=3), [_rq(), _rq(), _rq(), _rq("NonEvent")]),
+    ("non-events should not count against limit", dict(server=3), [_rq(), _rq(), _rq("NonEvent"), _rq()]),
+    ("event accepted after token refill", dict(server=3), [_rq(), _rq(), _rq(), _rq(ok=False), _rq(delay=1)]),
+    ("event blocked by namespace limits", dict(server=100, ns=(3, 10)), [_rq(ns="A")] * 3 + [_rq(ns="A", ok=False)]),
+    ("event from other namespace not blocked", dict(server=100, ns=(3, 10)), [_rq(ns="A")] * 3 + [_rq(ns="B")]),
+    ("events from other namespaces should not count against limit", dict(server=100, ns=(3, 10)),
+     [_rq(ns="A"), _rq(ns="A"), _rq(ns="B"), _rq(ns="A")]),
+    ("event accepted after namespace token refill", dict(server=100, ns=(3, 10)),
+     [_rq(ns="A")] * 3 + [_rq(ns="A", ok=False), _rq(ns="A", delay=1)]),
+    ("event from other namespaces should not clear namespace limits", dict(server=100, ns=(3, 10)),
+     [_rq(ns="A")] * 3 + [_rq(ns="B"), _rq(ns="A", ok=False)]),
+    ("namespace limits from lru namespace should clear when cache size exceeded", dict(server=100, ns=(3, 2)),
+     [_rq(ns="A"), _rq(ns="A"), _rq(ns="B"), _rq(ns="B"), _rq(ns="B"), _rq(ns="A"), _rq(ns="B", ok=False),
+      _rq(ns="A", ok=False), _rq(ns="C"), _rq(ns="A", ok=False), _rq(ns="B")]),
+    ("event blocked by source+object limits", dict(server=100, so=(3, 10)),
+     [_rq(event=_comp("A"))] * 3 + [_rq(event=_comp("A"), ok=False)]),
+    ("event from other source+object not blocked", dict(server=100, so=(3, 10)),
+     [_rq(event=_comp("A"))] * 3 + [_rq(event=_comp("B"))]),
+    ("events from other source+object should not count against limit", dict(server=100, so=(3, 10)),
+     [_rq(event=_comp("A")), _rq(event=_comp("A")), _rq(event=_comp("B")), _rq(event=_comp("A"))]),
+    ("event accepted after source+object token refill", dict(server=100, so=(3, 10)),
+     [_rq(event=_comp("A"))] * 3 + [_rq(event=_comp("A"), ok=False), _rq(event=_comp("A"), delay=1)]),
+    ("event from other source+object should not clear source+object limits", dict(server=100, so=(3, 10)),
+     [_rq(event=_comp("A"))] * 3 + [_rq(event=_comp("B")), _rq(event=_comp("A"), ok=False)]),
+    ("source+object limits from lru source+object should clear when cache size exceeded", dict(server=100, so=(3, 2)),
+     [_rq(event=_comp(c), ok=ok) for c, ok in (("A", True), ("A", True), ("B", True), ("B", True), ("B", True), ("A", True),
+                                              ("B", False), ("A", False), ("C", True), ("A", False), ("B", True))]),
+    ("source host should be included in source+object key", dict(server=100, so=(1, 10)),
+     _soi(lambda lbl: {"source": {"host": lbl}})),
+    ("involved object kind should be included in source+object key", dict(server=100, so=(1, 10)),
+     _soi(lambda lbl: {"involvedObject": {"kind": lbl}})),
+    ("involved object namespace should be included in source+object key", dict(server=100, so=(1, 10)),
+     _soi(lambda lbl: {"involvedObject": {"namespace": lbl}})),
+    ("involved object name should be included in source+object key", dict(server=100, so=(1, 10)),
+     _soi(lambda lbl: {"involvedObject": {"name": lbl}})),
+    ("involved object UID should be included in source+object key", dict(server=100, so=(1, 10)),
+     _soi(lambda lbl: {"involvedObject": {"uid": lbl}})),
+    ("involved object APIVersion should be included in source+object key", dict(server=100, so=(1, 10)),
+     _soi(lambda lbl: {"involvedObject": {"apiVersion": lbl}})),
+    ("event blocked by user limits", dict(user=(3, 10)), [_rq(user="A")] * 3 + [_rq(user="A", ok=False)]),
+    ("event from other user not blocked", dict(), [_rq(user="A")] * 3 + [_rq(user="B")]),
+    ("events from other user should not count against limit", dict(), [_rq(user="A"), _rq(user="A"), _rq(user="B"), _rq(user="A")]),
+]
+
+
+@pytest.mark.parametrize("name,cfg,requests", ERL_CASES, ids=[c[0] for c in ERL_CASES])
+def test_event_rate_limiting(name, cfg, requests):
+    now = [1000.0]
+    limits = []
+    if cfg.get("server"):
+        limits.append({"type": "Server", "qps": 1, "burst": cfg["server"]})
+    if cfg.get("ns"):
+        limits.append({"type": "Namespace", "qps": 1, "burst": cfg["ns"][0], "cacheSize": cfg["ns"][1]})
+    if cfg.get("user"):
+        limits.append({"type": "User", "qps": 1, "burst": cfg["user"][0], "cacheSize": cfg["user"][1]})
+    if cfg.get("so"):
+        limits.append({"type": "SourceAndObject", "qps": 1, "burst": cfg["so"][0], "cacheSize": cfg["so"][1]})
+    plug = X.EventRateLimit(limits or [{"type": "Server", "qps": 1, "burst": 10 ** 9}], clock=lambda: now[0])
+    for i, (kind, ns, user, event, delay, ok) in enumerate(requests):
+        now[0] += delay
+        a = Attributes(CREATE, "resource", "", ns, "name", copy.deepcopy(event) or {}, None, {"name": user}, kind)
+        if ok:
+            plug.validate(a, Ctx())
+        else:
+            with pytest.raises(m.StatusError) as e:
+                plug.validate(a, Ctx())
+            assert e.value.code == 429 and e.value.message.startswith("limit reached on type"), (name, i)
+
+
+def test_event_rate_limit_every_limit_takes_a_token():
+    """Validate consults every enforcer even after one rejected (the reference keeps the last
+    error): a Server rejection still spends the Namespace token."""
+    now = [0.0]
+    plug = X.EventRateLimit([{"type": "Server", "qps": 1, "burst": 1}, {"type": "Namespace", "qps": 1, "burst": 2}],
+                            clock=lambda: now[0])
+    a = Attributes(CREATE, "events", "", "ns", "e", {}, None, {}, "Event")
+    plug.validate(a, Ctx())
+    with pytest.raises(m.StatusError) as e:
+        plug.validate(a, Ctx())
+    assert e.value.message == "limit reached on type Server for key "
+    with pytest.raises(m.StatusError) as e:
+        plug.validate(a, Ctx())                       # both exhausted now; the last limit's error wins
+    assert e.value.message == "limit reached on type Namespace for key ns"
