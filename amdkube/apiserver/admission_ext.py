@@ -188,31 +188,39 @@ class DenyExecOnPrivileged(DenyEscalatingExec):
 
 # ------------------------------------------------- OwnerReferencesPermissionEnforcement
 class OwnerReferencesPermissionEnforcement(Plugin):
-    """gc/gc_admission.go: changing metadata.ownerReferences needs `delete` on the object;
-    setting blockOwnerDeletion on a reference needs `update` on the owner's finalizers."""
+    """gc/gc_admission.go: changing metadata.ownerReferences (any difference, order included)
+    needs `delete` on the object (subresource included; pods/status is whitelisted); each
+    reference newly set to blockOwnerDeletion needs `update` on the owner's finalizers."""
     name = "OwnerReferencesPermissionEnforcement"
+    WHITELIST = (("", "pods", "status"),)
 
     def validate(self, a, ctx):
-        if a.obj is None or a.subresource:
+        if (getattr(a, "group", ""), a.resource, a.subresource) in self.WHITELIST or not isinstance(a.obj, dict):
             return
         new = (a.obj.get("metadata") or {}).get("ownerReferences") or []
-        old = ((a.old or {}).get("metadata") or {}).get("ownerReferences") or []
-        if new == old:
+        if a.old is None:
+            if not new:
+                return
+        elif new == (((a.old or {}).get("metadata") or {}).get("ownerReferences") or []):
             return
-        if not ctx.authorize(a.user, "delete", _group_of(a.obj), a.resource, "", a.namespace, a.name):
-            raise m.forbidden(f"cannot set an ownerRef on a resource you can't delete: {a.resource}, {a.name}")
-        olds = {r.get("uid"): r for r in old}
+        if not ctx.authorize(a.user, "delete", getattr(a, "group", "") or _group_of(a.obj), a.resource, a.subresource,
+                             a.namespace, a.name):
+            raise new_forbidden(a, "cannot set an ownerRef on a resource you can't delete: , <nil>")
+        olds = {r.get("uid"): r for r in ((a.old or {}).get("metadata") or {}).get("ownerReferences") or []}
         for r in new:
             if not r.get("blockOwnerDeletion"):
                 continue
             prev = olds.get(r.get("uid"))
             if prev is not None and prev.get("blockOwnerDeletion"):
                 continue
-            plural = ctx.plural_for_kind(r.get("apiVersion", ""), r.get("kind", ""))
-            if plural is None or not ctx.authorize(a.user, "update", r.get("apiVersion", "").rpartition("/")[0],
-                                                   plural, "finalizers", a.namespace, r.get("name", "")):
-                raise m.forbidden(f"cannot set blockOwnerDeletion if an ownerReference refers to a resource you can't "
-                                  f"set finalizers on: {r.get('kind')}, {r.get('name')}")
+            av = r.get("apiVersion", "")
+            plural = ctx.plural_for_kind(av, r.get("kind", ""))
+            if plural is None:
+                raise new_forbidden(a, f"cannot set blockOwnerDeletion in this case because cannot find RESTMapping for "
+                                       f"APIVersion {av} Kind {r.get('kind', '')}: , no matches for kind")
+            if not ctx.authorize(a.user, "update", av.rpartition("/")[0], plural, "finalizers", a.namespace, r.get("name", "")):
+                raise new_forbidden(a, "cannot set blockOwnerDeletion if an ownerReference refers to a resource you can't "
+                                       "set finalizers on: , <nil>")
 
 
 def _group_of(obj):

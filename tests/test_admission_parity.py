@@ -977,3 +977,88 @@ def test_event_rate_limit_every_limit_takes_a_token():
     with pytest.raises(m.StatusError) as e:
         plug.validate(a, Ctx())                       # both exhausted now; the last limit's error wins
     assert e.value.message == "limit reached on type Namespace for key ns"
+
+
+# ------------------------------------------------- OwnerReferencesPermissionEnforcement
+def _gc_allow(user, verb, group, resource, sub="", ns="", name=""):
+    """gc_admission_test.go fakeAuthorizer."""
+    u = (user or {}).get("name")
+    if u == "non-deleter":
+        return not (verb == "delete" or (verb == "update" and sub == "finalizers"))
+    if u == "non-pod-deleter":
+        return not ((verb == "delete" and resource == "pods") or (verb == "update" and resource == "pods" and sub == "finalizers"))
+    if u == "non-rc-deleter":
+        return not ((verb == "delete" and resource == "replicationcontrollers")
+                    or (verb == "update" and resource == "replicationcontrollers" and sub == "finalizers"))
+    return True
+
+
+class GCCtx(Ctx):
+    def authorize(self, user, verb, group, resource, sub="", ns="", name=""):
+        return _gc_allow(user, verb, group, resource, sub, ns, name)
+
+    def plural_for_kind(self, av, kind):
+        return {"ReplicationController": "replicationcontrollers", "DaemonSet": "daemonsets", "Pod": "pods"}.get(kind)
+
+
+def _ref(kind, name, uid, block):
+    r = {"apiVersion": "v1" if kind != "DaemonSet" else "extensions/v1beta1", "kind": kind, "name": name, "uid": uid}
+    if block is not None:
+        r["blockOwnerDeletion"] = block
+    return r
+
+
+BLOCK_RC1, BLOCK_RC2 = _ref("ReplicationController", "rc1", "rc1", True), _ref("ReplicationController", "rc2", "rc2", True)
+NOTBLOCK_RC1, NOTBLOCK_RC2 = _ref("ReplicationController", "rc1", "rc1", False), _ref("ReplicationController", "rc2", "rc2", False)
+NILBLOCK_RC1, NILBLOCK_RC2 = _ref("ReplicationController", "rc1", "rc1", None), _ref("ReplicationController", "rc2", "rc2", None)
+BLOCK_DS1 = _ref("DaemonSet", "ds1", "ds1", True)
+
+
+def _owned(*refs):
+    return {"metadata": {"name": "p", "namespace": "ns", "ownerReferences": [dict(r) for r in refs]}}
+
+
+CANT_DELETE, CANT_BLOCK = "cannot set an ownerRef on a resource you can't delete", "cannot set blockOwnerDeletion"
+
+
+@pytest.mark.parametrize("name,user,resource,sub,old,new,err", [
+    ("super-user, create, no objectref change", "super", "pods", "", None, _owned(), None),
+    ("super-user, create, objectref change", "super", "pods", "", None, _owned(NILBLOCK_RC1), None),
+    ("non-deleter, create, no objectref change", "non-deleter", "pods", "", None, _owned(), None),
+    ("non-deleter, create, objectref change", "non-deleter", "pods", "", None, _owned(NILBLOCK_RC1), CANT_DELETE),
+    ("non-pod-deleter, create, objectref change", "non-pod-deleter", "pods", "", None, _owned(NILBLOCK_RC1), CANT_DELETE),
+    ("non-pod-deleter, create, objectref change, but not a pod", "non-pod-deleter", "not-pods", "", None, _owned(NILBLOCK_RC1), None),
+    ("non-deleter, update, no objectref change", "non-deleter", "pods", "", _owned(NILBLOCK_RC1), _owned(NILBLOCK_RC1), None),
+    ("non-deleter, update, objectref change", "non-deleter", "pods", "", _owned(), _owned(NILBLOCK_RC1), CANT_DELETE),
+    ("non-deleter, update, objectref change two", "non-deleter", "pods", "", _owned(NILBLOCK_RC1),
+     _owned(NILBLOCK_RC1, NILBLOCK_RC2), CANT_DELETE),
+    ("non-pod-deleter, update status, objectref change", "non-pod-deleter", "pods", "status", _owned(), _owned(NILBLOCK_RC1), None),
+    ("non-pod-deleter, update, objectref change", "non-pod-deleter", "pods", "", _owned(), _owned(NILBLOCK_RC1), CANT_DELETE),
+    ("super-user, create, some ownerReferences have blockOwnerDeletion=true", "super", "pods", "", None,
+     _owned(BLOCK_RC1, BLOCK_RC2), None),
+    ("non-rc-deleter, create, all ownerReferences have blockOwnerDeletion=false or nil", "non-rc-deleter", "pods", "", None,
+     _owned(NOTBLOCK_RC1, NILBLOCK_RC2), None),
+    ("non-rc-deleter, create, some ownerReferences have blockOwnerDeletion=true", "non-rc-deleter", "pods", "", None,
+     _owned(BLOCK_RC1, NOTBLOCK_RC2), CANT_BLOCK),
+    ("non-rc-deleter, create, blockOwnerDeletion=true pointing to a daemonset", "non-rc-deleter", "pods", "", None,
+     _owned(BLOCK_DS1), None),
+    ("non-rc-deleter, update, no ownerReferences change blockOwnerDeletion", "non-rc-deleter", "pods", "", _owned(NILBLOCK_RC1),
+     _owned(NOTBLOCK_RC1), None),
+    ("non-rc-deleter, update, blockOwnerDeletion false to true", "non-rc-deleter", "pods", "", _owned(NOTBLOCK_RC1),
+     _owned(BLOCK_RC1), CANT_BLOCK),
+    ("non-rc-deleter, update, blockOwnerDeletion nil to true", "non-rc-deleter", "pods", "", _owned(NILBLOCK_RC1),
+     _owned(BLOCK_RC1), CANT_BLOCK),
+    ("non-rc-deleter, update, already blocking", "non-rc-deleter", "pods", "", _owned(BLOCK_RC1),
+     _owned(BLOCK_RC1, NOTBLOCK_RC2), None),
+    ("non-rc-deleter, update, add a new blocking reference", "non-rc-deleter", "pods", "", _owned(BLOCK_RC1),
+     _owned(BLOCK_RC1, BLOCK_RC2), CANT_BLOCK),
+])
+def test_gc_admission(name, user, resource, sub, old, new, err):
+    a = Attributes(CREATE if old is None else UPDATE, resource, sub, "ns", "p", copy.deepcopy(new), copy.deepcopy(old),
+                   {"name": user})
+    if err is None:
+        X.OwnerReferencesPermissionEnforcement().validate(a, GCCtx())
+    else:
+        with pytest.raises(m.StatusError) as e:
+            X.OwnerReferencesPermissionEnforcement().validate(a, GCCtx())
+        assert e.value.code == 403 and err in e.value.message, name
