@@ -384,35 +384,47 @@ class PersistentVolumeLabel(Plugin):
 
 
 # --------------------------------------------------------- PersistentVolumeClaimResize
-RESIZABLE = ("gcePersistentDisk", "awsElasticBlockStore", "cinder", "glusterfs", "rbd", "azureDisk", "azureFile",
-             "portworxVolume", "hostPath", "local")
+RESIZABLE = ("glusterfs", "cinder", "rbd", "gcePersistentDisk", "awsElasticBlockStore")
+
+
+def _claim_class(pvc) -> str:
+    """helper.GetPersistentVolumeClaimClass: the beta annotation, else spec.storageClassName."""
+    ann = m.annotations_of(pvc)
+    if "volume.beta.kubernetes.io/storage-class" in ann:
+        return ann["volume.beta.kubernetes.io/storage-class"]
+    return (pvc.get("spec") or {}).get("storageClassName") or ""
 
 
 class PersistentVolumeClaimResize(Plugin):
     """persistentvolume/resize/admission.go: growing a claim's storage request needs a bound
-    claim whose StorageClass sets allowVolumeExpansion and whose volume type can expand."""
+    claim whose (unchanged) StorageClass sets allowVolumeExpansion and whose volume is one the
+    release can expand (GlusterFS, Cinder, RBD, GCE PD, AWS EBS)."""
     name = "PersistentVolumeClaimResize"
     operations = (UPDATE,)
 
     def validate(self, a, ctx):
-        if a.resource != "persistentvolumeclaims" or a.subresource or a.obj is None or a.old is None:
+        if a.resource != "persistentvolumeclaims" or a.subresource or not isinstance(a.obj, dict) or \
+                not isinstance(a.old, dict):
             return
+
         def size(o):
             s = (((o.get("spec") or {}).get("resources") or {}).get("requests") or {}).get("storage")
-            return Quantity(s).value() if s else 0
-        new, old = size(a.obj), size(a.old)
-        if new <= old:
+            return Quantity(s) if s else Quantity(0)
+        if not size(a.obj) > size(a.old):
             return
         if (a.old.get("status") or {}).get("phase") != "Bound":
-            raise m.forbidden("Only bound persistent volume claims can be expanded")
-        scn = (a.old.get("spec") or {}).get("storageClassName") or \
-            m.annotations_of(a.old).get("volume.beta.kubernetes.io/storage-class", "")
-        sc = ctx.get_object("storageclasses", "", scn) if scn else None
+            raise new_forbidden(a, "Only bound persistent volume claims can be expanded")
+        new_sc, old_sc = _claim_class(a.obj), _claim_class(a.old)
+        sc = ctx.get_object("storageclasses", "", new_sc) if new_sc and new_sc == old_sc else None
         if not sc or not sc.get("allowVolumeExpansion"):
-            raise m.forbidden("only dynamically provisioned pvc can be resized and the storageclass that provisions the pvc must support resize")
-        pv = ctx.get_object("persistentvolumes", "", (a.old.get("spec") or {}).get("volumeName", "")) or {}
-        if not any(k in (pv.get("spec") or {}) for k in RESIZABLE):
-            raise m.forbidden("volume plugin does not support resize")
+            raise new_forbidden(a, "only dynamically provisioned pvc can be resized and the storageclass that provisions "
+                                   "the pvc must support resize")
+        pv = ctx.get_object("persistentvolumes", "", (a.obj.get("spec") or {}).get("volumeName", ""))
+        if pv is None:
+            raise new_forbidden(a, "Error updating persistent volume claim because fetching associated persistent volume "
+                                   "failed")
+        if not any((pv.get("spec") or {}).get(k) is not None for k in RESIZABLE):
+            raise new_forbidden(a, "volume plugin does not support resize")
 
 
 # ------------------------------------------------------------------------- PodPreset
@@ -584,28 +596,30 @@ class PodTolerationRestriction(Plugin):
 
 # ----------------------------------------------------------------- SecurityContextDeny
 class SecurityContextDeny(Plugin):
-    """securitycontext/scdeny/admission.go: pods may not set SELinux options, runAsUser,
-    supplementalGroups or fsGroup."""
+    """securitycontext/scdeny/admission.go: pods may not set supplementalGroups, SELinux
+    options, runAsUser or fsGroup, nor containers SELinux options or runAsUser."""
     name = "SecurityContextDeny"
 
     def validate(self, a, ctx):
-        if not _is_pod(a) or a.obj is None:
+        if not _is_pod(a) or not isinstance(a.obj, dict):
             return
-        psc = (a.obj.get("spec") or {}).get("securityContext") or {}
-        if psc.get("supplementalGroups") is not None:
-            raise m.forbidden("pod.Spec.SecurityContext.SupplementalGroups is forbidden")
-        if psc.get("seLinuxOptions") is not None:
-            raise m.forbidden("pod.Spec.SecurityContext.SELinuxOptions is forbidden")
-        if psc.get("runAsUser") is not None:
-            raise m.forbidden("pod.Spec.SecurityContext.RunAsUser is forbidden")
-        if psc.get("fsGroup") is not None:
-            raise m.forbidden("pod.Spec.SecurityContext.FSGroup is forbidden")
+        name = m.name_of(a.obj)
+        psc = (a.obj.get("spec") or {}).get("securityContext")
+        if psc is not None:
+            for field, msg in (("supplementalGroups", "SecurityContext.SupplementalGroups is forbidden"),
+                               ("seLinuxOptions", "pod.Spec.SecurityContext.SELinuxOptions is forbidden"),
+                               ("runAsUser", "pod.Spec.SecurityContext.RunAsUser is forbidden"),
+                               ("fsGroup", "SecurityContext.FSGroup is forbidden")):
+                if psc.get(field) is not None:
+                    raise forbidden_for("pods", name, msg)
         for c in _all_containers(a.obj):
-            sc = c.get("securityContext") or {}
+            sc = c.get("securityContext")
+            if sc is None:
+                continue
             if sc.get("seLinuxOptions") is not None:
-                raise m.forbidden("SecurityContext.SELinuxOptions is forbidden")
+                raise forbidden_for("pods", name, "SecurityContext.SELinuxOptions is forbidden")
             if sc.get("runAsUser") is not None:
-                raise m.forbidden("SecurityContext.RunAsUser is forbidden")
+                raise forbidden_for("pods", name, "SecurityContext.RunAsUser is forbidden")
 
 
 # ------------------------------------------------------------------- PodSecurityPolicy

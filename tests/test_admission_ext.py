@@ -190,7 +190,7 @@ def test_pv_label_and_pvc_resize():
                                                                         "resources": {"requests": {"storage": size}}},
                 "status": {"phase": phase}}
     ctx = Ctx({"storageclasses": [{"metadata": {"name": "fast"}, "allowVolumeExpansion": True}],
-               "persistentvolumes": [{"metadata": {"name": "pv1"}, "spec": {"hostPath": {"path": "/x"}}}]})
+               "persistentvolumes": [{"metadata": {"name": "pv1"}, "spec": {"gcePersistentDisk": {"pdName": "d"}}}]})
     plug = X.PersistentVolumeClaimResize()
     plug.validate(attrs(pvc("2Gi"), UPDATE, "persistentvolumeclaims", old=pvc("1Gi")), ctx)
     with pytest.raises(m.StatusError):

@@ -1062,3 +1062,69 @@ def test_gc_admission(name, user, resource, sub, old, new, err):
         with pytest.raises(m.StatusError) as e:
             X.OwnerReferencesPermissionEnforcement().validate(a, GCCtx())
         assert e.value.code == 403 and err in e.value.message, name
+
+
+# ------------------------------------------------- PersistentVolumeClaimResize / scdeny
+def _claim(storage, phase, volume="", cls=None):
+    spec = {"resources": {"requests": {"storage": storage}}}
+    if volume:
+        spec["volumeName"] = volume
+    if cls is not None:
+        spec["storageClassName"] = cls
+    return {"metadata": {"name": "claim1", "namespace": "ns"}, "spec": spec, "status": {"phase": phase}}
+
+
+RESIZE_CTX = dict(storageclasses=[{"metadata": {"name": "gold"}, "allowVolumeExpansion": True}, {"metadata": {"name": "silver"}}],
+                  persistentvolumes=[{"metadata": {"name": "volume1"}, "spec": {"glusterfs": {"endpoints": "http://localhost:8080/"},
+                                                                               "storageClassName": "gold"}},
+                                     {"metadata": {"name": "volume2"}, "spec": {"hostPath": {}, "storageClassName": "gold"}}])
+
+
+@pytest.mark.parametrize("name,new,old,err", [
+    ("pvc-resize, update, no error", _claim("2Gi", "Bound", "volume1", "gold"), _claim("1Gi", "Bound", "volume1", "gold"), None),
+    ("pvc-resize, update, volume plugin error", _claim("2Gi", "Bound", "volume2", "gold"), _claim("1Gi", "Bound", "volume2", "gold"),
+     "volume plugin does not support resize"),
+    ("pvc-resize, update, dynamically provisioned error (no class)", _claim("2Gi", "Bound", "volume3"),
+     _claim("1Gi", "Bound", "volume3"),
+     "only dynamically provisioned pvc can be resized and the storageclass that provisions the pvc must support resize"),
+    ("pvc-resize, update, dynamically provisioned error (class without expansion)", _claim("2Gi", "Bound", "volume4", "silver"),
+     _claim("1Gi", "Bound", "volume4", "silver"),
+     "only dynamically provisioned pvc can be resized and the storageclass that provisions the pvc must support resize"),
+    ("PVC update with no change in size", _claim("1Gi", "Pending", "", "silver"), _claim("1Gi", "Bound", "volume4", "silver"), None),
+    ("expand pvc in pending state", _claim("2Gi", "Pending", "", "silver"), _claim("1Gi", "Pending", "", "silver"),
+     "Only bound persistent volume claims can be expanded"),
+    ("bound claim whose volume is missing", _claim("2Gi", "Bound", "gone", "gold"), _claim("1Gi", "Bound", "gone", "gold"),
+     "Error updating persistent volume claim because fetching associated persistent volume failed"),
+])
+def test_pvc_resize_admission(name, new, old, err):
+    a = Attributes(UPDATE, "persistentvolumeclaims", "", "ns", "claim1", copy.deepcopy(new), copy.deepcopy(old), {})
+    if err is None:
+        X.PersistentVolumeClaimResize().validate(a, Ctx(**RESIZE_CTX))
+    else:
+        with pytest.raises(m.StatusError) as e:
+            X.PersistentVolumeClaimResize().validate(a, Ctx(**RESIZE_CTX))
+        assert e.value.message == f'persistentvolumeclaims "claim1" is forbidden: {err}', name
+
+
+@pytest.mark.parametrize("psc,csc,err", [
+    ({"supplementalGroups": [1234]}, None, "SecurityContext.SupplementalGroups is forbidden"),
+    ({"seLinuxOptions": {"level": "s0"}}, None, "pod.Spec.SecurityContext.SELinuxOptions is forbidden"),
+    ({"runAsUser": 1}, None, "pod.Spec.SecurityContext.RunAsUser is forbidden"),
+    ({"fsGroup": 1234}, None, "SecurityContext.FSGroup is forbidden"),
+    (None, {"seLinuxOptions": {"level": "s0"}}, "SecurityContext.SELinuxOptions is forbidden"),
+    (None, {"runAsUser": 1}, "SecurityContext.RunAsUser is forbidden"),
+    ({}, {}, None),
+    (None, None, None),
+])
+def test_security_context_deny(psc, csc, err):
+    for kind in ("containers", "initContainers"):
+        spec = {kind: [{"name": "c", **({"securityContext": csc} if csc is not None else {})}]}
+        if psc is not None:
+            spec["securityContext"] = psc
+        a = _attrs({"metadata": {"name": "pod"}, "spec": spec})
+        if err is None:
+            X.SecurityContextDeny().validate(a, Ctx())
+        else:
+            with pytest.raises(m.StatusError) as e:
+                X.SecurityContextDeny().validate(a, Ctx())
+            assert e.value.message == f'pods "pod" is forbidden: {err}'
