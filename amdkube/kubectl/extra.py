@@ -122,45 +122,31 @@ async def _rollout_history_based(c, a, sub, ri, name, ns, res):
         await c.update(dict(obj, apiVersion=obj.get("apiVersion") or "apps/v1", kind=kind))
         print(f"{kind.lower()}.apps/{name} rolled back")
         return 0
+    return await _rollout_status(c, a, kind, res, name, ns)
+
+
+async def _rollout_status(c, a, kind, res, name, ns):
+    """rollout.go RunStatus over the StatusViewers of kubectl/rollout.py: print each new
+    message; without --watch stop after the first."""
+    from . import rollout as R
     end = time.time() + _timeout_of(a)
+    last = None
     while True:
         obj = await c.get(res, name, ns)
-        spec, st = obj.get("spec") or {}, obj.get("status") or {}
-        gen = (obj.get("metadata") or {}).get("generation", 1)
-        strategy = (spec.get("updateStrategy") or {}).get("type", "RollingUpdate")
-        if strategy != "RollingUpdate":
-            raise SystemExit("error: Status is available only for RollingUpdate strategy type" if kind == "DaemonSet"
-                             else f"error: {strategy} updateStrategy does not have a Status")
-        done = False
-        if int(st.get("observedGeneration", 0)) < gen:
-            msg = f"Waiting for {'daemon set' if kind == 'DaemonSet' else 'statefulset'} spec update to be observed..."
-        elif kind == "DaemonSet":
-            want, upd, av = (int(st.get(k, 0)) for k in ("desiredNumberScheduled", "updatedNumberScheduled", "numberAvailable"))
-            if upd < want:
-                msg = f"Waiting for rollout to finish: {upd} out of {want} new pods have been updated..."
-            elif av < want:
-                msg = f"Waiting for rollout to finish: {av} of {want} updated pods are available..."
+        try:
+            if kind == "Deployment":
+                msg, done = R.deployment_status(obj, name, int(getattr(a, "revision", 0) or 0))
             else:
-                msg, done = f'daemon set "{name}" successfully rolled out', True
-        else:
-            want, ready, upd = int(spec.get("replicas", 1)), int(st.get("readyReplicas", 0)), int(st.get("updatedReplicas", 0))
-            part = int(((spec.get("updateStrategy") or {}).get("rollingUpdate") or {}).get("partition", 0))
-            if ready < want:
-                msg = f"Waiting for {want - ready} pods to be ready..."
-            elif part > 0:
-                if upd < want - part:
-                    msg = f"Waiting for partitioned roll out to finish: {upd} out of {want - part} new pods have been updated..."
-                else:
-                    msg, done = f"partitioned roll out complete: {upd} new pods have been updated...", True
-            elif st.get("updateRevision") != st.get("currentRevision"):
-                msg = f"waiting for statefulset rolling update to complete {upd} pods at revision {st.get('updateRevision')}..."
-            else:
-                msg, done = f"statefulset rolling update complete {ready} pods at revision {st.get('currentRevision')}...", True
+                msg, done = R.VIEWERS[kind](obj, name)
+        except R.StatusError as e:
+            print(f"error: {e}", file=sys.stderr)
+            return 1
+        if msg != last:
+            print(msg, end="")
+            last = msg
         if done:
-            print(msg)
             return 0
         if not a.watch_status or time.time() > end:
-            print(msg)
             return 1
         await asyncio.sleep(0.2)
 
@@ -207,31 +193,7 @@ async def cmd_rollout(c, a):
         print(f"{ri.kind.lower()}/{name} rolled back")
         return 0
     if sub == "status":
-        end = time.time() + _timeout_of(a)
-        while True:
-            d = await c.get(res, name, ns)
-            spec, st = d.get("spec") or {}, d.get("status") or {}
-            want = int(spec.get("replicas", 1))
-            if st.get("observedGeneration", 0) >= (d.get("metadata") or {}).get("generation", 1):
-                prog = next((x for x in st.get("conditions") or [] if x.get("type") == "Progressing"), None)
-                if prog and prog.get("reason") == "ProgressDeadlineExceeded":
-                    raise SystemExit(f'error: deployment "{name}" exceeded its progress deadline')
-                upd = int(st.get("updatedReplicas", 0))
-                if upd < want:
-                    msg = f"Waiting for rollout to finish: {upd} out of {want} new replicas have been updated..."
-                elif int(st.get("replicas", 0)) > upd:
-                    msg = f"Waiting for rollout to finish: {int(st['replicas']) - upd} old replicas are pending termination..."
-                elif int(st.get("availableReplicas", 0)) < upd:
-                    msg = f"Waiting for rollout to finish: {st.get('availableReplicas', 0)} of {upd} updated replicas are available..."
-                else:
-                    print(f'deployment "{name}" successfully rolled out')
-                    return 0
-            else:
-                msg = "Waiting for deployment spec update to be observed..."
-            if not a.watch_status or time.time() > end:
-                print(msg)
-                return 1
-            await asyncio.sleep(0.2)
+        return await _rollout_status(c, a, "Deployment", res, name, ns)
     raise SystemExit(f"error: unknown rollout subcommand {sub!r}")
 
 
