@@ -365,4 +365,6 @@ def test_statefulset_rollout_history_and_undo(capsys):
             assert await asyncio.to_thread(kubectl, kc + ["rollout", "status", "statefulset/db"]) == 0
     run(go(), 200)
     out = capsys.readouterr().out
-    assert 'statefulsets "db"' in out and "statefulset.apps/db rolled back" in out and "rolling update complete 2 pods" in out
+    assert 'statefulsets "db"' in out and "statefulset.apps/db rolled back" in out
+    # the defaulted rollingUpdate block (partition 0) takes rollout_status.go's partition branch
+    assert "partitioned roll out complete: 2 new pods have been updated..." in out
