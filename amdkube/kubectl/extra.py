@@ -231,18 +231,6 @@ async def cmd_expose(c, a):
     print(f"service/{m.name_of(out)} exposed")
 
 
-async def cmd_autoscale(c, a):
-    ri, name, _ = _target(a)
-    ns = _ns(a, ri)
-    await c.get(_res(ri), name, ns)
-    hpa = {"apiVersion": "autoscaling/v1", "kind": "HorizontalPodAutoscaler", "metadata": {"name": a.name or name},
-           "spec": {"scaleTargetRef": {"apiVersion": ri.api_version, "kind": ri.kind, "name": name},
-                    "maxReplicas": a.max, **({"minReplicas": a.min} if a.min else {}),
-                    **({"targetCPUUtilizationPercentage": a.cpu_percent} if a.cpu_percent >= 0 else {})}}
-    out = await c.create(hpa, ns)
-    print(f"horizontalpodautoscaler.autoscaling/{m.name_of(out)} autoscaled")
-
-
 async def cmd_set(c, a):
     if not a.args or a.args[0] != "image":
         raise SystemExit("error: supported: set image RESOURCE/NAME CONTAINER=IMAGE ...")
@@ -815,7 +803,7 @@ async def cmd_create_generator(c, a) -> bool:
     return True
 
 
-COMMANDS = {"rollout": cmd_rollout, "expose": cmd_expose, "autoscale": cmd_autoscale, "set": cmd_set,
+COMMANDS = {"rollout": cmd_rollout, "expose": cmd_expose, "set": cmd_set,
             "replace": cmd_replace, "edit": cmd_edit, "auth": cmd_auth, "certificate": cmd_certificate,
             "port-forward": cmd_port_forward, "proxy": cmd_proxy, "cp": cmd_cp, "explain": cmd_explain}
 
@@ -828,9 +816,9 @@ def add_arguments(sp):
     sp.add_argument("--target-port", default=None)
     sp.add_argument("--name", default=None)
     sp.add_argument("--protocol", default=None)
-    sp.add_argument("--min", type=int, default=0)
-    sp.add_argument("--max", type=int, default=1)
-    sp.add_argument("--cpu-percent", type=int, default=-1)
+    sp.add_argument("--min", type=int, default=None)
+    sp.add_argument("--max", type=int, default=None)
+    sp.add_argument("--cpu-percent", type=int, default=None)
     sp.add_argument("--overwrite", action="store_true")
     sp.add_argument("--record", action="store_true")
     sp.add_argument("--force", action="store_true")

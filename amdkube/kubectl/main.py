@@ -456,6 +456,7 @@ from . import run as _run  # noqa: E402
 from . import delete as _delete  # noqa: E402
 from . import expose as _expose  # noqa: E402
 from . import taint as _taint  # noqa: E402
+from . import autoscale as _autoscale  # noqa: E402
 COMMANDS.update(_EXTRA)
 COMMANDS.update(_more.COMMANDS)
 COMMANDS["apply"] = _more.cmd_apply       # three-way merge, --prune, *-last-applied
@@ -464,6 +465,7 @@ from .diff import cmd_alpha  # noqa: E402
 COMMANDS["alpha"] = cmd_alpha             # alpha diff LOCAL|LIVE|LAST|MERGED
 COMMANDS["expose"] = _expose.cmd_expose   # service/v2 generator
 COMMANDS["taint"] = _taint.cmd_taint      # ParseTaints / ReorganizeTaints
+COMMANDS["autoscale"] = _autoscale.cmd_autoscale   # horizontalpodautoscaler/v1 generator
 
 
 _RESOURCE_CMDS = {"get", "describe", "delete", "label", "annotate", "scale", "patch", "wait", "edit", "explain", "expose",
