@@ -379,15 +379,6 @@ async def cmd_scale(c, a):
     return await scale(c, a)
 
 
-async def cmd_patch(c, a):
-    r, name = _split_targets(a.args)[0] if "/" in a.args[0] else (a.args[0], a.args[1])
-    ri = SCHEME.resolve(r)
-    pt = {"json": "application/json-patch+json", "merge": "application/merge-patch+json",
-          "strategic": "application/strategic-merge-patch+json"}[a.type]
-    await c.patch(ri.plural, name, json.loads(a.patch), _ns(a, ri), patch_type=pt)
-    print(f"{ri.kind.lower()}/{name} patched")
-
-
 async def cmd_run(c, a):
     from .run import cmd_run as run_
     return await run_(c, a)
@@ -443,7 +434,7 @@ async def cmd_wait(c, a):
 
 COMMANDS = {"get": cmd_get, "describe": cmd_describe, "create": cmd_create, "apply": cmd_apply, "delete": cmd_delete,
             "logs": cmd_logs, "exec": cmd_exec, "label": cmd_label, "annotate": cmd_annotate, "cordon": cmd_cordon,
-            "uncordon": cmd_uncordon, "drain": cmd_drain, "scale": cmd_scale, "patch": cmd_patch, "run": cmd_run,
+            "uncordon": cmd_uncordon, "drain": cmd_drain, "scale": cmd_scale, "run": cmd_run,
             "top": cmd_top, "version": cmd_version, "api-resources": cmd_api_resources, "cluster-info": cmd_cluster_info,
             "wait": cmd_wait, "attach": cmd_attach}
 from .extra import COMMANDS as _EXTRA, add_arguments as _extra_args  # noqa: E402
@@ -457,6 +448,7 @@ from . import delete as _delete  # noqa: E402
 from . import expose as _expose  # noqa: E402
 from . import taint as _taint  # noqa: E402
 from . import autoscale as _autoscale  # noqa: E402
+from . import patch as _patch  # noqa: E402
 COMMANDS.update(_EXTRA)
 COMMANDS.update(_more.COMMANDS)
 COMMANDS["apply"] = _more.cmd_apply       # three-way merge, --prune, *-last-applied
@@ -466,6 +458,7 @@ COMMANDS["alpha"] = cmd_alpha             # alpha diff LOCAL|LIVE|LAST|MERGED
 COMMANDS["expose"] = _expose.cmd_expose   # service/v2 generator
 COMMANDS["taint"] = _taint.cmd_taint      # ParseTaints / ReorganizeTaints
 COMMANDS["autoscale"] = _autoscale.cmd_autoscale   # horizontalpodautoscaler/v1 generator
+COMMANDS["patch"] = _patch.cmd_patch      # patched / not patched, --local, -f
 
 
 _RESOURCE_CMDS = {"get", "describe", "delete", "label", "annotate", "scale", "patch", "wait", "edit", "explain", "expose",
@@ -512,7 +505,7 @@ def parser():
         sp.add_argument("--ignore-not-found", action="store_const", const=True, default=None)
         sp.add_argument("--ignore-daemonsets", action="store_true")
         sp.add_argument("--replicas", "-r", type=int, default=None)
-        sp.add_argument("-p", "--patch", default="{}")
+        sp.add_argument("-p", "--patch", default=None)
         sp.add_argument("--type", default="strategic")
         sp.add_argument("--image", default=None)
         sp.add_argument("--gpus", type=int, default=0)
