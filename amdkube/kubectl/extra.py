@@ -255,30 +255,6 @@ async def cmd_set(c, a):
     print(f"{ri.kind.lower()}/{name} image updated")
 
 
-async def cmd_replace(c, a):
-    from .main import _read_files
-    for doc in _read_files(a.filename):
-        ri = SCHEME.for_object(doc)
-        ns = (m.namespace_of(doc) or a.namespace or "default") if ri.namespaced else ""
-        if a.force:
-            try:
-                await c.delete(_res(ri), m.name_of(doc), ns, grace=0)
-            except m.StatusError as e:
-                if not m.is_not_found(e):
-                    raise
-            for _ in range(100):
-                if await c.get_or_none(_res(ri), m.name_of(doc), ns) is None:
-                    break
-                await asyncio.sleep(0.05)
-            doc.get("metadata", {}).pop("resourceVersion", None)
-            await c.create(doc, ns)
-        else:
-            if ri.namespaced:
-                doc.setdefault("metadata", {})["namespace"] = ns
-            await c.update(doc)
-        print(f"{ri.kind.lower()}/{m.name_of(doc)} replaced")
-
-
 async def cmd_edit(c, a):
     ri, name, _ = _target(a)
     ns = _ns(a, ri)
@@ -804,7 +780,7 @@ async def cmd_create_generator(c, a) -> bool:
 
 
 COMMANDS = {"rollout": cmd_rollout, "expose": cmd_expose, "set": cmd_set,
-            "replace": cmd_replace, "edit": cmd_edit, "auth": cmd_auth, "certificate": cmd_certificate,
+            "edit": cmd_edit, "auth": cmd_auth, "certificate": cmd_certificate,
             "port-forward": cmd_port_forward, "proxy": cmd_proxy, "cp": cmd_cp, "explain": cmd_explain}
 
 

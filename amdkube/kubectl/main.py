@@ -449,6 +449,7 @@ from . import expose as _expose  # noqa: E402
 from . import taint as _taint  # noqa: E402
 from . import autoscale as _autoscale  # noqa: E402
 from . import patch as _patch  # noqa: E402
+from . import replace as _replace  # noqa: E402
 COMMANDS.update(_EXTRA)
 COMMANDS.update(_more.COMMANDS)
 COMMANDS["apply"] = _more.cmd_apply       # three-way merge, --prune, *-last-applied
@@ -459,6 +460,7 @@ COMMANDS["expose"] = _expose.cmd_expose   # service/v2 generator
 COMMANDS["taint"] = _taint.cmd_taint      # ParseTaints / ReorganizeTaints
 COMMANDS["autoscale"] = _autoscale.cmd_autoscale   # horizontalpodautoscaler/v1 generator
 COMMANDS["patch"] = _patch.cmd_patch      # patched / not patched, --local, -f
+COMMANDS["replace"] = _replace.cmd_replace   # unconditional PUT, --force delete-and-create
 
 
 _RESOURCE_CMDS = {"get", "describe", "delete", "label", "annotate", "scale", "patch", "wait", "edit", "explain", "expose",
@@ -501,6 +503,7 @@ def parser():
         sp.add_argument("--tail", type=int, default=-1)
         sp.add_argument("--all", action="store_true")
         sp.add_argument("--grace-period", type=int, default=-1)
+        sp.add_argument("--save-config", action="store_true")
         sp.add_argument("--cascade", type=lambda s: s != "false", default=True)
         sp.add_argument("--ignore-not-found", action="store_const", const=True, default=None)
         sp.add_argument("--ignore-daemonsets", action="store_true")
