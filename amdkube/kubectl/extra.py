@@ -221,7 +221,7 @@ async def cmd_expose(c, a):
         if not ports:
             raise SystemExit("error: couldn't find port via --port flag or introspection")
         port = ports[0]["containerPort"]
-    svc_type = a.type if a.type not in ("strategic", "merge", "json") else "ClusterIP"   # --type is shared with patch
+    svc_type = a.type if a.type not in (None, "strategic", "merge", "json") else "ClusterIP"   # --type is shared with patch
     svc = {"apiVersion": "v1", "kind": "Service",
            "metadata": {"name": a.name or name, "labels": dict(sel)},
            "spec": {"selector": dict(sel), "type": svc_type,
@@ -706,30 +706,26 @@ async def cmd_create_generator(c, a) -> bool:
     kind, rest = a.args[0], a.args[1:]
     ns = a.namespace or "default"
 
-    def lit():
-        out = {}
-        for kv in a.from_literal:
-            k, _, v = kv.partition("=")
-            out[k] = v
-        for fpath in a.from_file:
-            k, _, p = fpath.partition("=")
-            if not p:
-                k, p = os.path.basename(k), k
-            out[k] = open(p).read()
-        return out
-
     if kind in ("namespace", "ns"):
         obj = {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": rest[0]}}
     elif kind in ("configmap", "cm"):
-        obj = {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": rest[0]}, "data": lit()}
+        from .generators import GenerateError, generate_config_map
+        try:
+            obj = generate_config_map(rest[0] if rest else "", a.from_file, a.from_literal, a.from_env_file, a.append_hash)
+        except GenerateError as e:
+            raise SystemExit(f"error: {e}") from None
     elif (kind == "secret" and rest and rest[0] in ("docker-registry", "tls")) or kind in ("service", "svc", "poddisruptionbudget", "pdb"):
         from .more import create_more
         obj = await create_more(c, a, kind, rest)
     elif kind == "secret":
-        if rest[0] != "generic":
+        if not rest or rest[0] != "generic":
             raise SystemExit("error: create secret generic|docker-registry|tls NAME")
-        obj = {"apiVersion": "v1", "kind": "Secret", "metadata": {"name": rest[1]}, "type": "Opaque",
-               "data": {k: base64.b64encode(v.encode()).decode() for k, v in lit().items()}}
+        from .generators import GenerateError, generate_secret
+        try:
+            obj = generate_secret(rest[1] if len(rest) > 1 else "", a.type or "", a.from_file, a.from_literal,
+                                  a.from_env_file, a.append_hash)
+        except GenerateError as e:
+            raise SystemExit(f"error: {e}") from None
     elif kind in ("serviceaccount", "sa"):
         obj = {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": rest[0]}}
     elif kind in ("deployment", "deploy"):
@@ -803,6 +799,8 @@ def add_arguments(sp):
     sp.add_argument("--as-group", action="append", default=[])
     sp.add_argument("--from-literal", action="append", default=[])
     sp.add_argument("--from-file", action="append", default=[])
+    sp.add_argument("--from-env-file", default="")
+    sp.add_argument("--append-hash", action="store_true")
     sp.add_argument("--value", type=int, default=0)
     sp.add_argument("--global-default", action="store_true")
     sp.add_argument("--hard", default=None)

@@ -1,0 +1,162 @@
+"""The configmap/v1 and secret/v1 generators of `kubectl create configmap|secret generic`.
+
+Reference: pkg/kubectl/configmap.go and secret.go (StructuredGenerate, validate, the
+from-file/from-literal/from-env-file handlers), pkg/kubectl/util/util.go ParseFileSource /
+ParseLiteralSource, pkg/kubectl/env_file.go (addFromEnvFile: BOM on the first line, leading
+whitespace and #-comments skipped, IsEnvVarName keys, `KEY` alone takes the value from the
+environment) and pkg/kubectl/util/hash (--append-hash: the first 10 hex digits of the SHA-256 of
+{"data","kind","name"[,"type"]} with 0,1,3,a,e mapped to g,h,k,m,t).
+"""
+from __future__ import annotations
+
+import base64
+import hashlib
+import json
+import os
+
+from ..api.validation import is_config_map_key, is_env_var_name
+
+
+class GenerateError(Exception):
+    pass
+
+
+def parse_file_source(source: str) -> tuple[str, str]:
+    n = source.count("=")
+    if n == 0:
+        return os.path.basename(source.rstrip("/")) or source, source
+    if n == 1 and source.startswith("="):
+        raise GenerateError(f"key name for file path {source[1:]} missing.")
+    if n == 1 and source.endswith("="):
+        raise GenerateError(f"file path for key name {source[:-1]} missing.")
+    if n > 1:
+        raise GenerateError("Key names or file paths cannot contain '='.")
+    k, p = source.split("=")
+    return k, p
+
+
+def parse_literal_source(source: str) -> tuple[str, str]:
+    if source.startswith("=") or "=" not in source:
+        raise GenerateError(f"invalid literal source {source}, expected key=value")
+    k, v = source.split("=", 1)
+    return k, v
+
+
+def env_file_pairs(path: str) -> list[tuple[str, str]]:
+    out = []
+    with open(path, "rb") as f:
+        for i, raw in enumerate(f.read().split(b"\n")):
+            raw = raw.rstrip(b"\r")
+            try:
+                line = raw.decode("utf-8")
+            except UnicodeDecodeError:
+                raise GenerateError(f"env file {path} contains invalid utf8 bytes at line {i + 1}: {list(raw)}") from None
+            if i == 0 and line.startswith("﻿"):
+                line = line[1:]
+            line = line.lstrip()
+            if not line or line.startswith("#"):
+                continue
+            key, sep, value = line.partition("=")
+            errs = is_env_var_name(key)
+            if errs:
+                raise GenerateError(f'"{key}" is not a valid key name: {";".join(errs)}')
+            out.append((key, value if sep else os.environ.get(key, "")))
+    return out
+
+
+def _go_map(d: dict, secret: bool) -> str:
+    def val(v):
+        return "[" + " ".join(str(b) for b in v) + "]" if secret else v
+    return "map[" + " ".join(f"{k}:{val(d[k])}" for k in sorted(d)) + "]"
+
+
+def _add(data: dict, key: str, value, what: str):
+    errs = is_config_map_key(key)
+    if errs:
+        raise GenerateError(f'"{key}" is not a valid key name for a {what}: {";".join(errs)}')
+    if key in data:
+        raise GenerateError(f"cannot add key {key}, another key by that name already exists: {_go_map(data, what == 'Secret')}.")
+    data[key] = value
+
+
+def _collect(what: str, file_sources, literal_sources, env_file, to_value):
+    data: dict = {}
+    for src in file_sources or []:
+        key, path = parse_file_source(src)
+        if not os.path.exists(path):
+            raise GenerateError(f"error reading {path}: no such file or directory")
+        if os.path.isdir(path):
+            if "=" in src:
+                raise GenerateError("cannot give a key name for a directory path.")
+            for item in sorted(os.listdir(path)):
+                p = os.path.join(path, item)
+                if os.path.isfile(p) and not os.path.islink(p):
+                    with open(p, "rb") as f:
+                        _add(data, item, to_value(f.read()), what)
+        else:
+            with open(path, "rb") as f:
+                _add(data, key, to_value(f.read()), what)
+    for src in literal_sources or []:
+        k, v = parse_literal_source(src)
+        _add(data, k, to_value(v.encode()), what)
+    if env_file:
+        if not os.path.exists(env_file):
+            raise GenerateError(f"error reading {env_file}: no such file or directory")
+        if os.path.isdir(env_file):
+            raise GenerateError("env config file cannot be a directory")
+        for k, v in env_file_pairs(env_file):
+            _add(data, k, to_value(v.encode()), what)
+    return data
+
+
+def _encode_hash(hexdigest: str) -> str:
+    return hexdigest[:10].translate(str.maketrans({"0": "g", "1": "h", "3": "k", "a": "m", "e": "t"}))
+
+
+def _go_json(obj) -> str:
+    return json.dumps(obj, sort_keys=True, separators=(",", ":"), ensure_ascii=False)
+
+
+def encode_config_map(cm: dict) -> str:
+    return _go_json({"kind": "ConfigMap", "name": (cm.get("metadata") or {}).get("name", ""), "data": cm.get("data") or {}})
+
+
+def encode_secret(sec: dict) -> str:
+    return _go_json({"kind": "Secret", "type": sec.get("type", ""), "name": (sec.get("metadata") or {}).get("name", ""),
+                     "data": sec.get("data") or {}})
+
+
+def config_map_hash(cm: dict) -> str:
+    return _encode_hash(hashlib.sha256(encode_config_map(cm).encode()).hexdigest())
+
+
+def secret_hash(sec: dict) -> str:
+    return _encode_hash(hashlib.sha256(encode_secret(sec).encode()).hexdigest())
+
+
+def _validate(name, file_sources, literal_sources, env_file):
+    if not name:
+        raise GenerateError("name must be specified")
+    if env_file and (file_sources or literal_sources):
+        raise GenerateError("from-env-file cannot be combined with from-file or from-literal")
+
+
+def generate_config_map(name: str, file_sources=(), literal_sources=(), env_file: str = "", append_hash=False) -> dict:
+    _validate(name, file_sources, literal_sources, env_file)
+    data = _collect("ConfigMap", file_sources, literal_sources, env_file, lambda b: b.decode("utf-8", "replace"))
+    cm = {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": name}, "data": data}
+    if append_hash:
+        cm["metadata"]["name"] = f"{name}-{config_map_hash(cm)}"
+    return cm
+
+
+def generate_secret(name: str, type_: str = "", file_sources=(), literal_sources=(), env_file: str = "",
+                    append_hash=False) -> dict:
+    _validate(name, file_sources, literal_sources, env_file)
+    data = _collect("Secret", file_sources, literal_sources, env_file, lambda b: base64.b64encode(b).decode())
+    sec = {"apiVersion": "v1", "kind": "Secret", "metadata": {"name": name}, "data": data}
+    if type_:
+        sec["type"] = type_
+    if append_hash:
+        sec["metadata"]["name"] = f"{name}-{secret_hash(sec)}"
+    return sec

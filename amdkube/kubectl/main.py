@@ -509,7 +509,7 @@ def parser():
         sp.add_argument("--ignore-daemonsets", action="store_true")
         sp.add_argument("--replicas", "-r", type=int, default=None)
         sp.add_argument("-p", "--patch", default=None)
-        sp.add_argument("--type", default="strategic")
+        sp.add_argument("--type", default=None)
         sp.add_argument("--image", default=None)
         sp.add_argument("--gpus", type=int, default=0)
         sp.add_argument("--restart", default="Always")

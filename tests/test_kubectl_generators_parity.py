@@ -1,0 +1,136 @@
+"""configmap/v1 and secret/v1 generators against pkg/kubectl/configmap_test.go,
+secret_test.go, env_file_test.go and util/hash/hash_test.go (the --append-hash names are the
+reference's own vectors)."""
+from __future__ import annotations
+
+import pytest
+
+from amdkube.kubectl import generators as G
+
+
+@pytest.fixture
+def env_file(tmp_path):
+    def make(*lines):
+        p = tmp_path / "file.env"
+        p.write_text("\n".join(lines))
+        return str(p)
+    return make
+
+
+@pytest.mark.parametrize("kw,name,data,err", [
+    (dict(), "foo", {}, None),
+    (dict(append_hash=True), "foo-867km9574f", {}, None),
+    (dict(literal_sources=["key1=value1", "key2=value2"]), "foo", {"key1": "value1", "key2": "value2"}, None),
+    (dict(literal_sources=["key1=value1", "key2=value2"], append_hash=True), "foo-gcb75dd9gb",
+     {"key1": "value1", "key2": "value2"}, None),
+    (dict(literal_sources=["key1value1"]), None, None, "invalid literal source key1value1, expected key=value"),
+    (dict(file_sources=["key1=/file=2"]), None, None, "Key names or file paths cannot contain '='."),
+    (dict(file_sources=["key1==value"]), None, None, "Key names or file paths cannot contain '='."),
+    (dict(literal_sources=["key1==value1"]), "foo", {"key1": "=value1"}, None),
+    (dict(literal_sources=["key1==value1"], append_hash=True), "foo-bdgk9ttt7m", {"key1": "=value1"}, None),
+])
+def test_config_map_generate(kw, name, data, err):
+    if err:
+        with pytest.raises(G.GenerateError) as e:
+            G.generate_config_map("foo", **kw)
+        assert str(e.value) == err
+    else:
+        cm = G.generate_config_map("foo", **kw)
+        assert (cm["metadata"]["name"], cm["data"]) == (name, data)
+
+
+def test_config_map_from_env_file(env_file, monkeypatch):
+    path = env_file("key1=value1", "#", "", "key2=value2")
+    assert G.generate_config_map("valid_env", env_file=path)["data"] == {"key1": "value1", "key2": "value2"}
+    assert G.generate_config_map("valid_env", env_file=path, append_hash=True)["metadata"]["name"] == "valid_env-2cgh8552ch"
+    monkeypatch.setenv("g_key1", "1")
+    monkeypatch.setenv("g_key2", "2")
+    path = env_file("g_key1", "g_key2=")
+    cm = G.generate_config_map("getenv", env_file=path, append_hash=True)
+    assert cm["data"] == {"g_key1": "1", "g_key2": ""} and cm["metadata"]["name"] == "getenv-b4hh92hgdk"
+    with pytest.raises(G.GenerateError) as e:
+        G.generate_config_map("too_many_args", literal_sources=["key1=value1"], env_file=path)
+    assert str(e.value) == "from-env-file cannot be combined with from-file or from-literal"
+    with pytest.raises(G.GenerateError) as e:
+        G.generate_config_map("invalid_key", env_file=env_file("key#1=value1"))
+    assert str(e.value).startswith('"key#1" is not a valid key name: ')
+    # env_file_test.go: a BOM on the first line and leading whitespace are dropped
+    assert G.env_file_pairs(env_file("﻿A=1", "   B=2 ", "  # c")) == [("A", "1"), ("B", "2 ")]
+
+
+def test_config_map_keys_and_directories(tmp_path):
+    d = tmp_path / "dir"
+    d.mkdir()
+    (d / "a.conf").write_text("A")
+    (d / "b.conf").write_text("B")
+    (d / "sub").mkdir()
+    assert G.generate_config_map("x", file_sources=[str(d)])["data"] == {"a.conf": "A", "b.conf": "B"}
+    assert G.generate_config_map("x", file_sources=[f"k={d / 'a.conf'}"])["data"] == {"k": "A"}
+    with pytest.raises(G.GenerateError) as e:
+        G.generate_config_map("x", file_sources=[f"k={d}"])
+    assert str(e.value) == "cannot give a key name for a directory path."
+    with pytest.raises(G.GenerateError) as e:
+        G.generate_config_map("x", literal_sources=["a=1", "a=2"])
+    assert str(e.value) == "cannot add key a, another key by that name already exists: map[a:1]."
+    with pytest.raises(G.GenerateError) as e:
+        G.generate_config_map("x", literal_sources=["a b=1"])
+    assert str(e.value).startswith('"a b" is not a valid key name for a ConfigMap: ')
+    with pytest.raises(G.GenerateError) as e:
+        G.generate_config_map("")
+    assert str(e.value) == "name must be specified"
+
+
+@pytest.mark.parametrize("source,result,err", [
+    ("foo", ("foo", "foo"), None),
+    ("/some/dir/foo", ("foo", "/some/dir/foo"), None),
+    ("k=v", ("k", "v"), None),
+    ("=v", None, "key name for file path v missing."),
+    ("k=", None, "file path for key name k missing."),
+    ("a=b=c", None, "Key names or file paths cannot contain '='."),
+])
+def test_parse_file_source(source, result, err):
+    if err:
+        with pytest.raises(G.GenerateError) as e:
+            G.parse_file_source(source)
+        assert str(e.value) == err
+    else:
+        assert G.parse_file_source(source) == result
+
+
+@pytest.mark.parametrize("kw,name,err", [
+    (dict(), "foo", None),
+    (dict(append_hash=True), "foo-949tdgdkgg", None),
+    (dict(type_="my-type"), "foo", None),
+    (dict(type_="my-type", append_hash=True), "foo-dg474f9t76", None),
+    (dict(literal_sources=["key1=value1", "key2=value2"]), "foo", None),
+    (dict(literal_sources=["key1=value1", "key2=value2"], append_hash=True), "foo-tf72c228m4", None),
+    (dict(literal_sources=["key1value1"]), None, "invalid literal source key1value1, expected key=value"),
+    (dict(literal_sources=["key1==value1"], append_hash=True), "foo-fdcc8tkhh5", None),
+])
+def test_secret_generate(kw, name, err):
+    if err:
+        with pytest.raises(G.GenerateError) as e:
+            G.generate_secret("foo", **kw)
+        assert str(e.value) == err
+    else:
+        assert G.generate_secret("foo", **kw)["metadata"]["name"] == name
+
+
+@pytest.mark.parametrize("obj,encoded,h", [
+    ({"data": {}}, '{"data":{},"kind":"ConfigMap","name":""}', "42745tchd9"),
+    ({"data": {"one": ""}}, '{"data":{"one":""},"kind":"ConfigMap","name":""}', "9g67k2htb6"),
+    ({"data": {"two": "2", "one": "", "three": "3"}}, '{"data":{"one":"","three":"3","two":"2"},"kind":"ConfigMap","name":""}',
+     "f5h7t85m9b"),
+])
+def test_config_map_hash(obj, encoded, h):
+    assert G.encode_config_map(obj) == encoded and G.config_map_hash(obj) == h
+
+
+@pytest.mark.parametrize("obj,encoded,h", [
+    ({"type": "my-type", "data": {}}, '{"data":{},"kind":"Secret","name":"","type":"my-type"}', "t75bgf6ctb"),
+    ({"type": "my-type", "data": {"one": ""}}, '{"data":{"one":""},"kind":"Secret","name":"","type":"my-type"}', "74bd68bm66"),
+    ({"type": "my-type", "data": {"two": "Mg==", "one": "", "three": "Mw=="}},
+     '{"data":{"one":"","three":"Mw==","two":"Mg=="},"kind":"Secret","name":"","type":"my-type"}', "dgcb6h9tmk"),
+])
+def test_secret_hash(obj, encoded, h):
+    assert G.encode_secret(obj) == encoded and G.secret_hash(obj) == h
