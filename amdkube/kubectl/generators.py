@@ -160,3 +160,66 @@ def generate_secret(name: str, type_: str = "", file_sources=(), literal_sources
     if append_hash:
         sec["metadata"]["name"] = f"{name}-{secret_hash(sec)}"
     return sec
+
+
+# ---------------------------------------------------------------- service/v2 basic generators
+SERVICE_TYPES = {"clusterip": "ClusterIP", "nodeport": "NodePort", "loadbalancer": "LoadBalancer", "externalname": "ExternalName"}
+
+
+def _atoi(s: str) -> int:
+    try:
+        return int(s, 10)
+    except ValueError:
+        raise GenerateError(f'strconv.Atoi: parsing "{s}": invalid syntax') from None
+
+
+def parse_ports(spec: str) -> tuple[int, int | str]:
+    """service_basic.go parsePorts: `port[:targetPort]`, the target a number or a port name."""
+    from ..api.corevalidation import is_valid_port_name, is_valid_port_num
+    parts = spec.split(":")
+    port = _atoi(parts[0])
+    errs = is_valid_port_num(port)
+    if errs:
+        raise GenerateError(",".join(errs))
+    if len(parts) == 1:
+        return port, port
+    try:
+        target: int | str = int(parts[1], 10)
+    except ValueError:
+        errs = is_valid_port_name(parts[1])
+        if errs:
+            raise GenerateError(",".join(errs)) from None
+        return port, parts[1]
+    errs = is_valid_port_num(target)
+    if errs:
+        raise GenerateError(",".join(errs))
+    return port, target
+
+
+def generate_service(name: str, type_: str, tcp=(), cluster_ip: str = "", external_name: str = "", node_port: int = 0) -> dict:
+    """ServiceCommonGeneratorV1 (validate + StructuredGenerate): ports named after their
+    specifier with ':' turned into '-', label and selector app=<name>."""
+    from ..api.labels import is_dns1123_subdomain
+    if not name:
+        raise GenerateError("name must be specified")
+    if not type_:
+        raise GenerateError("type must be specified")
+    if cluster_ip == "None" and type_ != "ClusterIP":
+        raise GenerateError("ClusterIP=None can only be used with ClusterIP service type")
+    if cluster_ip != "None" and not tcp and type_ != "ExternalName":
+        raise GenerateError("at least one tcp port specifier must be provided")
+    if type_ == "ExternalName" and is_dns1123_subdomain(external_name):
+        raise GenerateError(f"invalid service external name {external_name}")
+    ports = []
+    for t in tcp or []:
+        port, target = parse_ports(t)
+        p = {"name": t.replace(":", "-"), "protocol": "TCP", "port": port, "targetPort": target}
+        if node_port:
+            p["nodePort"] = node_port
+        ports.append(p)
+    spec = {"type": type_, "selector": {"app": name}, "ports": ports}
+    if external_name:
+        spec["externalName"] = external_name
+    if cluster_ip:
+        spec["clusterIP"] = cluster_ip
+    return {"apiVersion": "v1", "kind": "Service", "metadata": {"name": name, "labels": {"app": name}}, "spec": spec}

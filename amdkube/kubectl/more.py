@@ -316,26 +316,15 @@ async def create_more(c, a, kind, rest) -> dict | None:
                 "data": {"tls.crt": base64.b64encode(open(a.cert, "rb").read()).decode(),
                          "tls.key": base64.b64encode(open(a.key, "rb").read()).decode()}}
     if kind in ("service", "svc") and rest:
-        stype = {"clusterip": "ClusterIP", "nodeport": "NodePort", "loadbalancer": "LoadBalancer",
-                 "externalname": "ExternalName"}.get(rest[0])
+        from .generators import SERVICE_TYPES, GenerateError, generate_service
+        stype = SERVICE_TYPES.get(rest[0])
         if stype is None:
             raise SystemExit("error: create service clusterip|nodeport|loadbalancer|externalname NAME")
-        name = rest[1]
-        spec = {"type": stype, "selector": {"app": name}}
-        if stype == "ExternalName":
-            spec = {"type": stype, "externalName": a.external_name}
-        else:
-            ports = []
-            for t in a.tcp:
-                p, _, tp = t.partition(":")
-                ports.append({"name": f"{p}-{tp or p}", "port": int(p), "protocol": "TCP",
-                              "targetPort": int(tp) if (tp or p).isdigit() else tp or p})
-                if stype == "NodePort" and a.node_port:
-                    ports[-1]["nodePort"] = a.node_port
-            spec["ports"] = ports
-            if stype == "ClusterIP" and a.clusterip == "None":
-                spec["clusterIP"] = "None"
-        return {"apiVersion": "v1", "kind": "Service", "metadata": {"name": name, "labels": {"app": name}}, "spec": spec}
+        try:
+            return generate_service(rest[1] if len(rest) > 1 else "", stype, a.tcp, a.clusterip or "",
+                                    a.external_name or "", int(a.node_port or 0) if stype == "NodePort" else 0)
+        except GenerateError as e:
+            raise SystemExit(f"error: {e}") from None
     if kind in ("poddisruptionbudget", "pdb") and rest:
         spec = {"selector": {"matchLabels": dict(kv.split("=", 1) for kv in (a.selector or "").split(",") if kv)}}
         if a.min_available:

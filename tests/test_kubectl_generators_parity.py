@@ -134,3 +134,40 @@ def test_config_map_hash(obj, encoded, h):
 ])
 def test_secret_hash(obj, encoded, h):
     assert G.encode_secret(obj) == encoded and G.secret_hash(obj) == h
+
+
+def _svc_port(name, port, target):
+    return {"name": name, "protocol": "TCP", "port": port, "targetPort": target}
+
+
+@pytest.mark.parametrize("name,tcp,cip,type_,ports,err", [
+    ("clusterip-ok", ["456", "321:908"], "", "ClusterIP", [_svc_port("456", 456, 456), _svc_port("321-908", 321, 908)], None),
+    ("clusterip-missing", None, "", "ClusterIP", None, "at least one tcp port specifier must be provided"),
+    ("clusterip-none-wrong-type", [], "None", "NodePort", None, "ClusterIP=None can only be used with ClusterIP service type"),
+    ("clusterip-none-ok", [], "None", "ClusterIP", [], None),
+    ("clusterip-none-and-port-mapping", ["456:9898"], "None", "ClusterIP", [_svc_port("456-9898", 456, 9898)], None),
+    ("loadbalancer-ok", ["456:9898"], "", "LoadBalancer", [_svc_port("456-9898", 456, 9898)], None),
+    ("invalid-port", ["65536"], "None", "ClusterIP", None, "must be between 1 and 65535, inclusive"),
+    ("invalid-port-mapping", ["8080:-abc"], "None", "ClusterIP", None, "must not begin or end with a hyphen"),
+    ("", None, "", "", None, "name must be specified"),
+    ("named-target", ["80:http"], "", "ClusterIP", [_svc_port("80-http", 80, "http")], None),
+])
+def test_service_common_generate(name, tcp, cip, type_, ports, err):
+    if err:
+        with pytest.raises(G.GenerateError) as e:
+            G.generate_service(name, type_, tcp, cip)
+        assert err in str(e.value)
+    else:
+        svc = G.generate_service(name, type_, tcp, cip)
+        assert svc["metadata"] == {"name": name, "labels": {"app": name}} and svc["spec"]["ports"] == ports
+        assert svc["spec"]["type"] == type_ and svc["spec"]["selector"] == {"app": name}
+        assert svc["spec"].get("clusterIP", "") == cip
+
+
+def test_service_external_name_and_node_port():
+    svc = G.generate_service("ext", "ExternalName", external_name="db.example.com")
+    assert svc["spec"]["externalName"] == "db.example.com" and svc["spec"]["ports"] == []
+    with pytest.raises(G.GenerateError) as e:
+        G.generate_service("ext", "ExternalName", external_name="Not_A_Name")
+    assert str(e.value) == "invalid service external name Not_A_Name"
+    assert G.generate_service("np", "NodePort", ["80:8080"], node_port=30080)["spec"]["ports"][0]["nodePort"] == 30080
