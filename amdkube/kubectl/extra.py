@@ -745,8 +745,11 @@ async def cmd_create_generator(c, a) -> bool:
         obj = {"apiVersion": "scheduling.k8s.io/v1alpha1", "kind": "PriorityClass", "metadata": {"name": rest[0]},
                "value": a.value, "globalDefault": a.global_default}
     elif kind in ("quota", "resourcequota"):
-        hard = dict(kv.split("=", 1) for kv in (a.hard or "").split(",") if kv)
-        obj = {"apiVersion": "v1", "kind": "ResourceQuota", "metadata": {"name": rest[0]}, "spec": {"hard": hard}}
+        from .generators import GenerateError, generate_quota
+        try:
+            obj = generate_quota(rest[0] if rest else "", a.hard or "", getattr(a, "scopes", "") or "")
+        except GenerateError as e:
+            raise SystemExit(f"error: {e}") from None
     elif kind in ("role", "clusterrole"):
         rules = [{"apiGroups": [""], "resources": a.resource, "verbs": a.verb}]
         obj = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role" if kind == "role" else "ClusterRole",
@@ -804,6 +807,7 @@ def add_arguments(sp):
     sp.add_argument("--value", type=int, default=0)
     sp.add_argument("--global-default", action="store_true")
     sp.add_argument("--hard", default=None)
+    sp.add_argument("--scopes", default=None)
     sp.add_argument("--verb", action="append", default=[])
     sp.add_argument("--resource", action="append", default=[])
     sp.add_argument("--user", action="append", default=[])

@@ -223,3 +223,97 @@ def generate_service(name: str, type_: str, tcp=(), cluster_ip: str = "", extern
     if cluster_ip:
         spec["clusterIP"] = cluster_ip
     return {"apiVersion": "v1", "kind": "Service", "metadata": {"name": name, "labels": {"app": name}}, "spec": spec}
+
+
+# ------------------------------------------------------ resourcequotas/v1 and poddisruptionbudget/v1beta1/v2
+def populate_resource_list(spec: str) -> dict | None:
+    """quota.go populateResourceListV1: `resource=quantity,...`."""
+    from ..api.quantity import Quantity
+    if not spec:
+        return None
+    out = {}
+    for stmt in spec.split(","):
+        parts = stmt.split("=")
+        if len(parts) != 2:
+            raise GenerateError(f"Invalid argument syntax {stmt}, expected <resource>=<value>")
+        try:
+            Quantity(parts[1])
+        except (ValueError, TypeError):
+            raise GenerateError("quantities must match the regular expression "
+                                "'^([+-]?[0-9.]+)([eEinumkKMGTP]*[-+]?[0-9]*)$'") from None
+        out[parts[0]] = parts[1]
+    return out
+
+
+def parse_scopes(spec: str) -> list | None:
+    if not spec:
+        return None
+    out = []
+    for s in spec.split(","):
+        if not s:
+            raise GenerateError('invalid resource quota scope ""')
+        out.append(s)
+    return out
+
+
+def generate_quota(name: str, hard: str = "", scopes: str = "") -> dict:
+    if not name:
+        raise GenerateError("name must be specified")
+    spec = {}
+    rl = populate_resource_list(hard)
+    if rl is not None:
+        spec["hard"] = rl
+    sc = parse_scopes(scopes)
+    if sc is not None:
+        spec["scopes"] = sc
+    return {"apiVersion": "v1", "kind": "ResourceQuota", "metadata": {"name": name}, "spec": spec}
+
+
+def parse_to_label_selector(selector: str) -> dict:
+    """metav1.ParseToLabelSelector: equality terms become matchLabels, set terms
+    matchExpressions; `!=`, `>` and `<` cannot be expressed."""
+    from ..api.labels import SelectorError, parse_selector
+    try:
+        sel = parse_selector(selector)
+    except SelectorError as e:
+        raise GenerateError(f'couldn\'t parse the selector string "{selector}": {e}') from None
+    ops = {"in": "In", "notin": "NotIn", "exists": "Exists", "!": "DoesNotExist"}
+    out = {"matchLabels": {}, "matchExpressions": []}
+    for r in getattr(sel, "reqs", []):
+        if r.op in ("=", "=="):
+            out["matchLabels"][r.key] = r.values[0]
+        elif r.op in ops:
+            e = {"key": r.key, "operator": ops[r.op]}
+            if r.values:
+                e["values"] = sorted(r.values)
+            out["matchExpressions"].append(e)
+        elif r.op in (">", "<", "gt", "lt"):
+            raise GenerateError(f'"{r.op}" isn\'t supported in label selectors')
+        else:
+            raise GenerateError(f'"{r.op}" is not a valid label selector operator')
+    return out
+
+
+def _int_or_string(s: str):
+    try:
+        return int(s, 10)
+    except ValueError:
+        return s
+
+
+def generate_pdb(name: str, selector: str = "", min_available: str = "", max_unavailable: str = "") -> dict:
+    """PodDisruptionBudgetV2Generator."""
+    if not name:
+        raise GenerateError("name must be specified")
+    if not selector:
+        raise GenerateError("a selector must be specified")
+    if not max_unavailable and not min_available:
+        raise GenerateError("one of min-available or max-unavailable must be specified")
+    if max_unavailable and min_available:
+        raise GenerateError("min-available and max-unavailable cannot be both specified")
+    spec = {"selector": parse_to_label_selector(selector)}
+    if max_unavailable:
+        spec["maxUnavailable"] = _int_or_string(max_unavailable)
+    else:
+        spec["minAvailable"] = _int_or_string(min_available)
+    return {"apiVersion": "policy/v1beta1", "kind": "PodDisruptionBudget", "metadata": {"name": name}, "spec": spec}

@@ -326,12 +326,11 @@ async def create_more(c, a, kind, rest) -> dict | None:
         except GenerateError as e:
             raise SystemExit(f"error: {e}") from None
     if kind in ("poddisruptionbudget", "pdb") and rest:
-        spec = {"selector": {"matchLabels": dict(kv.split("=", 1) for kv in (a.selector or "").split(",") if kv)}}
-        if a.min_available:
-            spec["minAvailable"] = int(a.min_available) if a.min_available.isdigit() else a.min_available
-        if a.max_unavailable:
-            spec["maxUnavailable"] = int(a.max_unavailable) if a.max_unavailable.isdigit() else a.max_unavailable
-        return {"apiVersion": "policy/v1beta1", "kind": "PodDisruptionBudget", "metadata": {"name": rest[0]}, "spec": spec}
+        from .generators import GenerateError, generate_pdb
+        try:
+            return generate_pdb(rest[0], a.selector or "", a.min_available or "", a.max_unavailable or "")
+        except GenerateError as e:
+            raise SystemExit(f"error: {e}") from None
     return None
 
 

@@ -171,3 +171,48 @@ def test_service_external_name_and_node_port():
         G.generate_service("ext", "ExternalName", external_name="Not_A_Name")
     assert str(e.value) == "invalid service external name Not_A_Name"
     assert G.generate_service("np", "NodePort", ["80:8080"], node_port=30080)["spec"]["ports"][0]["nodePort"] == 30080
+
+
+HARD = "cpu=10,memory=10Gi,pods=10"
+
+
+@pytest.mark.parametrize("name,hard,scopes,spec,err", [
+    ("foo", HARD, "", {"hard": {"cpu": "10", "memory": "10Gi", "pods": "10"}}, None),           # test_valid_case
+    ("", HARD, "", None, "name must be specified"),                                             # test_missing_required_param
+    ("foo", HARD, "BestEffort,NotTerminating", {"hard": {"cpu": "10", "memory": "10Gi", "pods": "10"},
+                                                 "scopes": ["BestEffort", "NotTerminating"]}, None),
+    ("foo", HARD, "", {"hard": {"cpu": "10", "memory": "10Gi", "pods": "10"}}, None),            # empty scopes
+    ("foo", HARD, "abc,", None, 'invalid resource quota scope ""'),
+    ("foo", "cpu", "", None, "Invalid argument syntax cpu, expected <resource>=<value>"),
+    ("foo", "cpu=ten", "", None, "quantities must match the regular expression"),
+])
+def test_quota_generate(name, hard, scopes, spec, err):
+    if err:
+        with pytest.raises(G.GenerateError) as e:
+            G.generate_quota(name, hard, scopes)
+        assert str(e.value).startswith(err)
+    else:
+        assert G.generate_quota(name, hard, scopes)["spec"] == spec
+
+
+@pytest.mark.parametrize("kw,spec,err", [
+    (dict(min_available="1", selector="app=rails"), {"selector": {"matchLabels": {"app": "rails"}, "matchExpressions": []},
+                                                     "minAvailable": 1}, None),
+    (dict(max_unavailable="50%", selector="app=rails"), {"selector": {"matchLabels": {"app": "rails"}, "matchExpressions": []},
+                                                         "maxUnavailable": "50%"}, None),
+    (dict(min_available="1", max_unavailable="1", selector="app=rails"), None,
+     "min-available and max-unavailable cannot be both specified"),
+    (dict(selector="app=rails"), None, "one of min-available or max-unavailable must be specified"),
+    (dict(min_available="1"), None, "a selector must be specified"),
+    (dict(min_available="1", selector="tier in (web,api),!legacy"),
+     {"selector": {"matchLabels": {}, "matchExpressions": [{"key": "tier", "operator": "In", "values": ["api", "web"]},
+                                                            {"key": "legacy", "operator": "DoesNotExist"}]}, "minAvailable": 1}, None),
+    (dict(min_available="1", selector="app!=rails"), None, '"!=" is not a valid label selector operator'),
+])
+def test_pdb_v2_generate(kw, spec, err):
+    if err:
+        with pytest.raises(G.GenerateError) as e:
+            G.generate_pdb("foo", **kw)
+        assert str(e.value) == err
+    else:
+        assert G.generate_pdb("foo", **kw)["spec"] == spec
