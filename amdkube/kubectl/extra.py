@@ -755,17 +755,13 @@ async def cmd_create_generator(c, a) -> bool:
         obj = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role" if kind == "role" else "ClusterRole",
                "metadata": {"name": rest[0]}, "rules": rules}
     elif kind in ("rolebinding", "clusterrolebinding"):
-        subjects = [{"kind": "User", "name": u, "apiGroup": "rbac.authorization.k8s.io"} for u in a.user]
-        subjects += [{"kind": "Group", "name": g, "apiGroup": "rbac.authorization.k8s.io"} for g in a.group]
-        for sa in a.serviceaccount:
-            sns, _, sname = sa.partition(":")
-            subjects.append({"kind": "ServiceAccount", "namespace": sns, "name": sname})
-        if a.clusterrole:
-            ref = {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole", "name": a.clusterrole}
-        else:
-            ref = {"apiGroup": "rbac.authorization.k8s.io", "kind": "Role", "name": a.role}
-        obj = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "RoleBinding" if kind == "rolebinding" else "ClusterRoleBinding",
-               "metadata": {"name": rest[0]}, "roleRef": ref, "subjects": subjects}
+        from .generators import GenerateError, generate_role_binding
+        try:
+            obj = generate_role_binding("RoleBinding" if kind == "rolebinding" else "ClusterRoleBinding",
+                                        rest[0] if rest else "", a.role or "", a.clusterrole or "", a.user, a.group,
+                                        a.serviceaccount)
+        except GenerateError as e:
+            raise SystemExit(f"error: {e}") from None
     else:
         return False
     ri = SCHEME.for_object(obj)

@@ -317,3 +317,36 @@ def generate_pdb(name: str, selector: str = "", min_available: str = "", max_una
     else:
         spec["minAvailable"] = _int_or_string(min_available)
     return {"apiVersion": "policy/v1beta1", "kind": "PodDisruptionBudget", "metadata": {"name": name}, "spec": spec}
+
+
+# ---------------------------------------------------- rolebinding.rbac.authorization.k8s.io/v1alpha1
+RBAC_GROUP = "rbac.authorization.k8s.io"
+
+
+def generate_role_binding(kind: str, name: str, role: str = "", cluster_role: str = "", users=(), groups=(),
+                          service_accounts=()) -> dict:
+    """RoleBindingGeneratorV1 / ClusterRoleBindingGeneratorV1: one role reference (a RoleBinding
+    takes exactly one of --role/--clusterrole), subjects de-duplicated and sorted per kind,
+    service accounts as <namespace>:<name>."""
+    if not name:
+        raise GenerateError("name must be specified")
+    if kind == "ClusterRoleBinding":
+        if not cluster_role:
+            raise GenerateError("clusterrole must be specified")
+        ref = {"apiGroup": RBAC_GROUP, "kind": "ClusterRole", "name": cluster_role}
+    else:
+        if bool(cluster_role) == bool(role):
+            raise GenerateError("exactly one of clusterrole or role must be specified")
+        ref = {"apiGroup": RBAC_GROUP, "kind": "Role", "name": role} if role else \
+            {"apiGroup": RBAC_GROUP, "kind": "ClusterRole", "name": cluster_role}
+    subjects = [{"kind": "User", "apiGroup": RBAC_GROUP, "name": u} for u in sorted(set(users or []))]
+    subjects += [{"kind": "Group", "apiGroup": RBAC_GROUP, "name": g} for g in sorted(set(groups or []))]
+    for sa in sorted(set(service_accounts or [])):
+        tokens = sa.split(":")
+        if len(tokens) != 2 or not tokens[1]:
+            raise GenerateError("serviceaccount must be <namespace>:<name>")
+        subjects.append({"kind": "ServiceAccount", "namespace": tokens[0], "name": tokens[1]})
+    obj = {"apiVersion": f"{RBAC_GROUP}/v1", "kind": kind, "metadata": {"name": name}, "roleRef": ref}
+    if subjects:
+        obj["subjects"] = subjects
+    return obj

@@ -216,3 +216,35 @@ def test_pdb_v2_generate(kw, spec, err):
         assert str(e.value) == err
     else:
         assert G.generate_pdb("foo", **kw)["spec"] == spec
+
+
+RB = "rbac.authorization.k8s.io"
+
+
+def test_role_binding_generate():
+    rb = G.generate_role_binding("RoleBinding", "foo", role="admin", users=["user2", "user1", "user1"], groups=["group1"],
+                                 service_accounts=["ns1:name1"])
+    assert rb["roleRef"] == {"apiGroup": RB, "kind": "Role", "name": "admin"}
+    assert rb["subjects"] == [{"kind": "User", "apiGroup": RB, "name": "user1"}, {"kind": "User", "apiGroup": RB, "name": "user2"},
+                              {"kind": "Group", "apiGroup": RB, "name": "group1"},
+                              {"kind": "ServiceAccount", "namespace": "ns1", "name": "name1"}]
+    assert G.generate_role_binding("RoleBinding", "foo", cluster_role="view")["roleRef"]["kind"] == "ClusterRole"
+    for kw, err in ((dict(role="a", cluster_role="b"), "exactly one of clusterrole or role must be specified"),
+                    (dict(), "exactly one of clusterrole or role must be specified"),
+                    (dict(role="a", service_accounts=["ns1"]), "serviceaccount must be <namespace>:<name>"),
+                    (dict(role="a", service_accounts=["ns1:"]), "serviceaccount must be <namespace>:<name>")):
+        with pytest.raises(G.GenerateError) as e:
+            G.generate_role_binding("RoleBinding", "foo", **kw)
+        assert str(e.value) == err
+    with pytest.raises(G.GenerateError) as e:
+        G.generate_role_binding("RoleBinding", "", role="a")
+    assert str(e.value) == "name must be specified"
+
+
+def test_cluster_role_binding_generate():
+    crb = G.generate_role_binding("ClusterRoleBinding", "foo", cluster_role="admin", groups=["group2", "group1"])
+    assert crb["roleRef"] == {"apiGroup": RB, "kind": "ClusterRole", "name": "admin"}
+    assert [s["name"] for s in crb["subjects"]] == ["group1", "group2"]
+    with pytest.raises(G.GenerateError) as e:
+        G.generate_role_binding("ClusterRoleBinding", "foo", role="admin")
+    assert str(e.value) == "clusterrole must be specified"
