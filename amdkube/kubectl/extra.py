@@ -743,7 +743,7 @@ async def cmd_create_generator(c, a) -> bool:
                "spec": {"template": {"spec": {"restartPolicy": "Never", "containers": [ct]}}}}
     elif kind in ("priorityclass", "pc"):
         obj = {"apiVersion": "scheduling.k8s.io/v1alpha1", "kind": "PriorityClass", "metadata": {"name": rest[0]},
-               "value": a.value, "globalDefault": a.global_default}
+               "value": a.value, "globalDefault": a.global_default, "description": a.description}
     elif kind in ("quota", "resourcequota"):
         from .generators import GenerateError, generate_quota
         try:
@@ -802,6 +802,7 @@ def add_arguments(sp):
     sp.add_argument("--append-hash", action="store_true")
     sp.add_argument("--value", type=int, default=0)
     sp.add_argument("--global-default", action="store_true")
+    sp.add_argument("--description", default="")
     sp.add_argument("--hard", default=None)
     sp.add_argument("--scopes", default=None)
     sp.add_argument("--verb", action="append", default=[])
