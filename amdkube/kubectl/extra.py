@@ -751,9 +751,14 @@ async def cmd_create_generator(c, a) -> bool:
         except GenerateError as e:
             raise SystemExit(f"error: {e}") from None
     elif kind in ("role", "clusterrole"):
-        rules = [{"apiGroups": [""], "resources": a.resource, "verbs": a.verb}]
-        obj = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role" if kind == "role" else "ClusterRole",
-               "metadata": {"name": rest[0]}, "rules": rules}
+        from .generators import GenerateError, generate_role
+        try:
+            obj = generate_role("Role" if kind == "role" else "ClusterRole", rest[0] if rest else "",
+                                [v for x in a.verb for v in x.split(",")], [r for x in a.resource for r in x.split(",")],
+                                [n for x in a.resource_name for n in x.split(",")],
+                                [u for x in a.non_resource_url for u in x.split(",")] if kind == "clusterrole" else [])
+        except GenerateError as e:
+            raise SystemExit(f"error: {e}") from None
     elif kind in ("rolebinding", "clusterrolebinding"):
         from .generators import GenerateError, generate_role_binding
         try:
@@ -807,6 +812,8 @@ def add_arguments(sp):
     sp.add_argument("--scopes", default=None)
     sp.add_argument("--verb", action="append", default=[])
     sp.add_argument("--resource", action="append", default=[])
+    sp.add_argument("--resource-name", action="append", default=[])
+    sp.add_argument("--non-resource-url", action="append", default=[])
     sp.add_argument("--user", action="append", default=[])
     sp.add_argument("--group", action="append", default=[])
     sp.add_argument("--serviceaccount", action="append", default=[])

@@ -350,3 +350,67 @@ def generate_role_binding(kind: str, name: str, role: str = "", cluster_role: st
     if subjects:
         obj["subjects"] = subjects
     return obj
+
+
+# ----------------------------------------------------------------- create role / clusterrole
+VALID_RESOURCE_VERBS = ("*", "get", "delete", "list", "create", "update", "patch", "watch", "proxy", "deletecollection", "use",
+                        "bind", "impersonate")
+SPECIAL_VERBS = {"use": {("extensions", "podsecuritypolicies")},
+                 "bind": {(RBAC_GROUP, "roles"), (RBAC_GROUP, "clusterroles")},
+                 "impersonate": {("", "users"), ("", "serviceaccounts"), ("", "groups"), ("authentication.k8s.io", "userextras")}}
+
+
+def _dedup(xs):
+    out = []
+    for x in xs or []:
+        if x not in out:
+            out.append(x)
+    return out
+
+
+def _resource_for(resource: str, group: str) -> tuple[str, str]:
+    """RESTMapper.ResourceFor: the plural and group the server serves (short and singular names
+    resolve); unknown resources keep what was given."""
+    from ..api.scheme import SCHEME
+    ri = SCHEME.resolve(f"{resource}.{group}" if group else resource)
+    return (ri.plural, ri.group) if ri is not None else (resource, group)
+
+
+def generate_role(kind: str, name: str, verbs=(), resources=(), resource_names=(), non_resource_urls=()) -> dict:
+    """create_role.go Complete/Validate/RunCreateRole (and create_clusterrole.go): verbs
+    de-duplicated ("*" alone wins) and checked, `resource[.group][/subresource]` specifiers mapped
+    to served groups, special verbs only on their resources, one rule per API group (sorted)
+    carrying every verb and resource name."""
+    if not name:
+        raise GenerateError("name must be specified")
+    vs = ["*"] if "*" in (verbs or []) else _dedup(verbs)
+    if not vs:
+        raise GenerateError("at least one verb must be specified")
+    for v in vs:
+        if v not in VALID_RESOURCE_VERBS:
+            raise GenerateError(f"invalid verb: '{v}'")
+    if not resources and not non_resource_urls:
+        raise GenerateError("at least one resource must be specified")
+    by_group: dict[str, list[str]] = {}
+    for spec in resources or []:
+        base, _, sub = spec.partition("/")
+        res, _, group = base.partition(".")
+        if not res:
+            raise GenerateError("resource must be specified if apiGroup/subresource specified")
+        res, group = _resource_for(res, group)
+        for v in vs:
+            if v in SPECIAL_VERBS and (group, res) not in SPECIAL_VERBS[v]:
+                raise GenerateError(f"can not perform '{v}' on '{res}' in group '{group}'")
+        full = f"{res}/{sub}" if sub else res
+        if full not in by_group.setdefault(group, []):
+            by_group[group].append(full)
+    rules = []
+    names = _dedup(resource_names)
+    for g in sorted(by_group):
+        rule = {"verbs": vs, "apiGroups": [g], "resources": by_group[g]}
+        if names:
+            rule["resourceNames"] = names
+        rules.append(rule)
+    if non_resource_urls:
+        rules.append({"verbs": vs, "nonResourceURLs": list(non_resource_urls)})
+    return {"apiVersion": f"{RBAC_GROUP}/v1", "kind": kind, "metadata": {"name": name}, "rules": rules}

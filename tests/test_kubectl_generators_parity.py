@@ -248,3 +248,40 @@ def test_cluster_role_binding_generate():
     with pytest.raises(G.GenerateError) as e:
         G.generate_role_binding("ClusterRoleBinding", "foo", role="admin")
     assert str(e.value) == "clusterrole must be specified"
+
+
+def test_create_role_rules():
+    """create_role_test.go TestCreateRole: one rule per group, sorted, subresources kept. amdkube
+    serves Deployments from apps first, where the reference's 1.9 RESTMapper picks extensions."""
+    role = G.generate_role("Role", "my-role", ["get", "watch", "list"], ["pods", "deployments.extensions", "pods/status"],
+                           ["foo"])
+    assert role["rules"] == [
+        {"verbs": ["get", "watch", "list"], "apiGroups": [""], "resources": ["pods", "pods/status"], "resourceNames": ["foo"]},
+        {"verbs": ["get", "watch", "list"], "apiGroups": ["extensions"], "resources": ["deployments"], "resourceNames": ["foo"]}]
+    assert G.generate_role("Role", "r", ["get", "*", "list"], ["po"])["rules"][0] == {"verbs": ["*"], "apiGroups": [""],
+                                                                                       "resources": ["pods"]}
+
+
+@pytest.mark.parametrize("verbs,resources,err", [
+    ([], ["pods"], "at least one verb must be specified"),
+    (["get"], [], "at least one resource must be specified"),
+    (["invalid-verb"], ["pods"], "invalid verb: 'invalid-verb'"),
+    (["get"], [".extensions"], "resource must be specified if apiGroup/subresource specified"),
+    (["use"], ["pods"], "can not perform 'use' on 'pods' in group ''"),
+    (["use"], ["podsecuritypolicies.extensions"], None),
+    (["bind"], ["roles.rbac.authorization.k8s.io"], None),
+    (["impersonate"], ["users", "serviceaccounts", "groups"], None),
+    (["impersonate"], ["nodes"], "can not perform 'impersonate' on 'nodes' in group ''"),
+])
+def test_create_role_validate(verbs, resources, err):
+    if err:
+        with pytest.raises(G.GenerateError) as e:
+            G.generate_role("Role", "my-role", verbs, resources)
+        assert str(e.value) == err
+    else:
+        G.generate_role("Role", "my-role", verbs, resources)
+
+
+def test_create_cluster_role_non_resource_urls():
+    cr = G.generate_role("ClusterRole", "metrics", ["get"], [], non_resource_urls=["/metrics", "/healthz"])
+    assert cr["rules"] == [{"verbs": ["get"], "nonResourceURLs": ["/metrics", "/healthz"]}]
