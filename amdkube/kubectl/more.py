@@ -304,11 +304,24 @@ async def cmd_set(c, a):
 # --------------------------------------------------------------------- generators
 async def create_more(c, a, kind, rest) -> dict | None:
     if kind == "secret" and rest and rest[0] == "docker-registry":
-        auth = base64.b64encode(f"{a.docker_username}:{a.docker_password}".encode()).decode()
-        cfg = {"auths": {a.docker_server: {"username": a.docker_username, "password": a.docker_password,
-                                           "email": a.docker_email, "auth": auth}}}
-        return {"apiVersion": "v1", "kind": "Secret", "metadata": {"name": rest[1]}, "type": "kubernetes.io/dockerconfigjson",
-                "data": {".dockerconfigjson": base64.b64encode(json.dumps(cfg).encode()).decode()}}
+        # secret_for_docker_registry.go: the four fields checked, .dockerconfigjson compact with
+        # the credentialprovider entry's omitempty fields (username, password, email, auth)
+        from .generators import secret_hash
+        name = rest[1] if len(rest) > 1 else ""
+        server = a.docker_server or "https://index.docker.io/v1/"
+        for val, what in ((name, "name"), (a.docker_username, "username"), (a.docker_password, "password"), (server, "server")):
+            if not val:
+                raise SystemExit(f"error: {what} must be specified")
+        entry = {"username": a.docker_username, "password": a.docker_password}
+        if a.docker_email:
+            entry["email"] = a.docker_email
+        entry["auth"] = base64.b64encode(f"{a.docker_username}:{a.docker_password}".encode()).decode()
+        cfg = json.dumps({"auths": {server: entry}}, separators=(",", ":"))
+        sec = {"apiVersion": "v1", "kind": "Secret", "metadata": {"name": name}, "type": "kubernetes.io/dockerconfigjson",
+               "data": {".dockerconfigjson": base64.b64encode(cfg.encode()).decode()}}
+        if getattr(a, "append_hash", False):
+            sec["metadata"]["name"] = f"{name}-{secret_hash(sec)}"
+        return sec
     if kind == "secret" and rest and rest[0] == "tls":
         if not (a.cert and a.key):
             raise SystemExit("error: --cert and --key are required")

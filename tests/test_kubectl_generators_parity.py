@@ -285,3 +285,35 @@ def test_create_role_validate(verbs, resources, err):
 def test_create_cluster_role_non_resource_urls():
     cr = G.generate_role("ClusterRole", "metrics", ["get"], [], non_resource_urls=["/metrics", "/healthz"])
     assert cr["rules"] == [{"verbs": ["get"], "nonResourceURLs": ["/metrics", "/healthz"]}]
+
+
+def test_docker_registry_secret():
+    """secret_for_docker_registry_test.go: compact .dockerconfigjson with username, password,
+    optional email and auth; the required fields and --append-hash."""
+    import argparse
+    import base64
+    import json as _json
+    from amdkube.kubectl.more import create_more
+    from tests.conftest import run
+
+    def args(**kw):
+        base = dict(docker_username="test-user", docker_password="test-password", docker_email="test-user@example.org",
+                    docker_server="https://index.docker.io/v1/", append_hash=False)
+        base.update(kw)
+        return argparse.Namespace(**base)
+    sec = run(create_more(None, args(), "secret", ["docker-registry", "foo"]))
+    raw = base64.b64decode(sec["data"][".dockerconfigjson"]).decode()
+    auth = base64.b64encode(b"test-user:test-password").decode()
+    assert raw == ('{"auths":{"https://index.docker.io/v1/":{"username":"test-user","password":"test-password",'
+                   '"email":"test-user@example.org","auth":"' + auth + '"}}}')
+    assert sec["type"] == "kubernetes.io/dockerconfigjson"
+    no_email = _json.loads(base64.b64decode(run(create_more(None, args(docker_email=""), "secret",
+                                                            ["docker-registry", "foo"]))["data"][".dockerconfigjson"]))
+    assert "email" not in no_email["auths"]["https://index.docker.io/v1/"]
+    hashed = run(create_more(None, args(append_hash=True), "secret", ["docker-registry", "foo"]))
+    assert hashed["metadata"]["name"] == "foo-" + G.secret_hash({**sec, "metadata": {"name": "foo"}})
+    for kw, msg in ((dict(docker_username=""), "username must be specified"),
+                    (dict(docker_password=""), "password must be specified")):
+        with pytest.raises(SystemExit) as e:
+            run(create_more(None, args(**kw), "secret", ["docker-registry", "foo"]))
+        assert str(e.value) == f"error: {msg}"
