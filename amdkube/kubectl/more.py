@@ -323,11 +323,24 @@ async def create_more(c, a, kind, rest) -> dict | None:
             sec["metadata"]["name"] = f"{name}-{secret_hash(sec)}"
         return sec
     if kind == "secret" and rest and rest[0] == "tls":
-        if not (a.cert and a.key):
-            raise SystemExit("error: --cert and --key are required")
-        return {"apiVersion": "v1", "kind": "Secret", "metadata": {"name": rest[1]}, "type": "kubernetes.io/tls",
-                "data": {"tls.crt": base64.b64encode(open(a.cert, "rb").read()).decode(),
-                         "tls.key": base64.b64encode(open(a.key, "rb").read()).decode()}}
+        # secret_for_tls.go: key and certificate required and loadable as a pair
+        import ssl
+        from .generators import secret_hash
+        name = rest[1] if len(rest) > 1 else ""
+        if not a.key:
+            raise SystemExit("error: key must be specified")
+        if not a.cert:
+            raise SystemExit("error: certificate must be specified")
+        try:
+            ssl.create_default_context(ssl.Purpose.CLIENT_AUTH).load_cert_chain(a.cert, a.key)
+        except (OSError, ssl.SSLError) as e:
+            raise SystemExit(f"error: failed to load key pair {e}") from None
+        with open(a.cert, "rb") as fc, open(a.key, "rb") as fk:
+            sec = {"apiVersion": "v1", "kind": "Secret", "metadata": {"name": name}, "type": "kubernetes.io/tls",
+                   "data": {"tls.crt": base64.b64encode(fc.read()).decode(), "tls.key": base64.b64encode(fk.read()).decode()}}
+        if getattr(a, "append_hash", False):
+            sec["metadata"]["name"] = f"{name}-{secret_hash(sec)}"
+        return sec
     if kind in ("service", "svc") and rest:
         from .generators import SERVICE_TYPES, GenerateError, generate_service
         stype = SERVICE_TYPES.get(rest[0])

@@ -317,3 +317,22 @@ def test_docker_registry_secret():
         with pytest.raises(SystemExit) as e:
             run(create_more(None, args(**kw), "secret", ["docker-registry", "foo"]))
         assert str(e.value) == f"error: {msg}"
+
+
+def test_tls_secret(tmp_path):
+    """secret_for_tls_test.go: the pair must load; key and certificate are required."""
+    import argparse
+    import subprocess
+    from amdkube.kubectl.more import create_more
+    from tests.conftest import run
+    crt, key = tmp_path / "tls.crt", tmp_path / "tls.key"
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-subj", "/CN=test", "-days", "1",
+                    "-keyout", str(key), "-out", str(crt)], check=True, capture_output=True)
+    sec = run(create_more(None, argparse.Namespace(cert=str(crt), key=str(key), append_hash=False), "secret", ["tls", "foo"]))
+    assert sec["type"] == "kubernetes.io/tls" and set(sec["data"]) == {"tls.crt", "tls.key"}
+    for kw, msg in ((dict(cert=str(crt), key=""), "error: key must be specified"),
+                    (dict(cert="", key=str(key)), "error: certificate must be specified"),
+                    (dict(cert=str(key), key=str(key)), "error: failed to load key pair")):
+        with pytest.raises(SystemExit) as e:
+            run(create_more(None, argparse.Namespace(append_hash=False, **kw), "secret", ["tls", "foo"]))
+        assert str(e.value).startswith(msg)
