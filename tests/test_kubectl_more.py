@@ -5,6 +5,7 @@ import asyncio
 import base64
 import io
 import json
+import subprocess
 import os
 import contextlib
 
@@ -82,8 +83,8 @@ def test_kubectl_apply_set_create_convert_and_friends(tmp_path, capsys):
             sec = await c.get("secrets", "regcred", "default")
             cfg = json.loads(base64.b64decode(sec["data"][".dockerconfigjson"]))
             assert sec["type"] == "kubernetes.io/dockerconfigjson" and cfg["auths"]["r.example.com"]["username"] == "u"
-            (tmp_path / "t.crt").write_text("CERT")
-            (tmp_path / "t.key").write_text("KEY")
+            subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-subj", "/CN=t", "-days", "1", "-keyout",
+                            str(tmp_path / "t.key"), "-out", str(tmp_path / "t.crt")], check=True, capture_output=True)   # the pair must load
             await kubectl(c, "create", "secret", "tls", "tls1", "--cert", str(tmp_path / "t.crt"), "--key", str(tmp_path / "t.key"))
             assert (await c.get("secrets", "tls1", "default"))["type"] == "kubernetes.io/tls"
             await kubectl(c, "create", "service", "nodeport", "np", "--tcp", "80:8080")
