@@ -706,6 +706,8 @@ async def cmd_create_generator(c, a) -> bool:
     kind, rest = a.args[0], a.args[1:]
     ns = a.namespace or "default"
 
+    if kind in ("namespace", "ns", "serviceaccount", "sa") and not rest:
+        raise SystemExit("error: name must be specified")      # namespace.go / serviceaccount.go validate()
     if kind in ("namespace", "ns"):
         obj = {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": rest[0]}}
     elif kind in ("configmap", "cm"):

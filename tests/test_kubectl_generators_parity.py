@@ -336,3 +336,17 @@ def test_tls_secret(tmp_path):
         with pytest.raises(SystemExit) as e:
             run(create_more(None, argparse.Namespace(append_hash=False, **kw), "secret", ["tls", "foo"]))
         assert str(e.value).startswith(msg)
+
+
+@pytest.mark.parametrize("kind", ["namespace", "serviceaccount"])
+def test_namespace_and_serviceaccount_need_a_name(kind):
+    """namespace_test.go / serviceaccount_test.go: a generator without a name fails."""
+    from tests.conftest import run
+    from tests.test_kubectl_commands_parity import _kubectl
+
+    class NoServer:
+        async def create(self, *a, **k):
+            raise AssertionError("no request expected")
+    with pytest.raises(SystemExit) as e:
+        run(_kubectl(NoServer(), "create", kind))
+    assert str(e.value) == "error: name must be specified"
