@@ -731,7 +731,15 @@ async def cmd_create_generator(c, a) -> bool:
     elif kind in ("serviceaccount", "sa"):
         obj = {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": rest[0]}}
     elif kind in ("deployment", "deploy"):
-        ct = {"name": rest[0], "image": a.image or "busybox"}
+        # deployment.go BaseDeploymentGenerator: a name and an image are required; the container is
+        # named after the image's last path element without tag or digest
+        if not rest:
+            raise SystemExit("error: name must be specified")
+        if not a.image:
+            raise SystemExit("error: at least one image must be specified")
+        cname = a.image.split("/")[-1]
+        cname = cname.split(":")[0] if ":" in cname else cname.split("@")[0]
+        ct = {"name": cname, "image": a.image}
         if a.gpus:
             ct["resources"] = {"limits": {"amd.com/gpu": str(a.gpus)}}
         obj = {"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": rest[0], "labels": {"app": rest[0]}},

@@ -350,3 +350,24 @@ def test_namespace_and_serviceaccount_need_a_name(kind):
     with pytest.raises(SystemExit) as e:
         run(_kubectl(NoServer(), "create", kind))
     assert str(e.value) == "error: name must be specified"
+
+
+def test_create_deployment_generator():
+    """deployment_test.go: name and image required; the container is named after the image."""
+    from tests.conftest import run
+    from tests.test_kubectl_commands_parity import _kubectl
+
+    class Capture:
+        created = None
+
+        async def create(self, obj, ns=""):
+            Capture.created = obj
+            return obj
+    run(_kubectl(Capture(), "create", "deployment", "foo", "--image", "registry.example.com/team/nginx:1.13@sha256:abc"))
+    ct = Capture.created["spec"]["template"]["spec"]["containers"][0]
+    assert ct["name"] == "nginx" and Capture.created["spec"]["selector"] == {"matchLabels": {"app": "foo"}}
+    for argv, msg in ((["create", "deployment", "foo"], "error: at least one image must be specified"),
+                      (["create", "deployment", "--image", "x"], "error: name must be specified")):
+        with pytest.raises(SystemExit) as e:
+            run(_kubectl(Capture(), *argv))
+        assert str(e.value) == msg
